@@ -1,0 +1,93 @@
+"""MI355X native probe tests (real GPU).  Run with ``pytest -m gpu``."""
+
+import json
+import os
+import subprocess
+
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module")
+def probe():
+    from triton_kubernetes_amd.ops import probe as p
+
+    assert p.device_count() >= 1
+    return p
+
+
+def test_device_is_mi355x(probe):
+    info = probe.device_info(0)
+    assert info.is_gfx950, info
+    assert info.wavefront_size == 64
+    assert info.compute_units == 256
+    assert info.total_mem_gib > 250
+
+
+def test_hbm_bandwidth(probe):
+    bw = probe.hbm_bandwidth(0, 2 << 30, iters=5)
+    print(json.dumps(bw))
+    # achievable is ~6.3 TB/s; a healthy GPU streams well above half of it
+    assert bw["read_gbps"] > 3500
+    assert bw["copy_gbps"] > 3500
+    assert bw["write_gbps"] > 3000
+
+
+@pytest.mark.parametrize("dtype,floor", [("bf16", 1300.0), ("fp8", 2600.0), ("f32", 80.0)])
+def test_mfma_peak(probe, dtype, floor):
+    r = probe.mfma_peak(0, dtype, iters=20000 if dtype != "f32" else 4000)
+    print(dtype, json.dumps(r))
+    assert r["tflops"] > floor
+
+
+def test_memtest_clean_and_detects_corruption(probe):
+    r = probe.memtest(0, 1 << 30, passes=1)
+    assert r["errors"] == 0
+    assert probe.memtest_selfcheck(0, 64 << 20, 5) == 5
+    assert probe.memtest_selfcheck(0, 64 << 20, 0) == 0
+
+
+def test_burnin_quick(probe):
+    res = probe.run_burnin(0, "quick")
+    print(json.dumps(res.to_json(), default=str))
+    assert res.ok, res.failures
+
+
+def test_rccl_single_rank_and_local():
+    from triton_kubernetes_amd.ops import rccl
+
+    assert rccl.version() > 0
+    uid = rccl.unique_id()
+    r = rccl.sweep_rank(0, 1, uid, 0, sizes=[1 << 20, 64 << 20], iters=5, warmup=2)
+    assert r.ok and len(r.busbw_gbps) == 2
+    r2 = rccl.sweep_local(1, sizes=[1 << 20], iters=5, warmup=1, dtype="bf16")
+    assert r2.ok
+
+
+def test_rccl_ready_executable():
+    from triton_kubernetes_amd.ops.native import executable
+
+    proc = subprocess.run([executable("rccl-ready"), "--ngpus", "1", "--iters", "3"], capture_output=True,
+                          text=True, timeout=300)
+    assert proc.returncode == 0, proc.stderr
+    doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["ok"] and doc["ngpus"] == 1
+
+
+def test_topology_amdsmi():
+    from triton_kubernetes_amd.ops import topo
+
+    doc = topo.discover()
+    print(json.dumps(doc)[:2000])
+    assert doc["gpus"], doc
+    g = doc["gpus"][0]
+    assert "MI355" in g.get("market_name", "") or g.get("target_graphics_version", "").startswith("gfx950")
+
+
+def test_labeller_executable():
+    from triton_kubernetes_amd.ops.native import executable
+
+    proc = subprocess.run([executable("amdgpu-topo-labeller")], capture_output=True, text=True, timeout=120)
+    assert proc.returncode == 0, proc.stdout + proc.stderr
+    assert json.loads(proc.stdout)["gpus"]

@@ -1,0 +1,123 @@
+"""Manta object-store backend (reference ``backend/manta/backend.go:1-205``).
+
+Layout: ``/stor/triton-kubernetes/<name>/{main.tf.json,terraform.tfstate}``.
+Terraform backend block: ``terraform.backend.manta = {account, key_material,
+key_id, path="/triton-kubernetes/<name>"}``.
+
+Deliberate fixes:
+
+* Q9 — the reference passes the key *path* as ``key_material``.  Terraform's
+  manta backend accepts either PEM text or a path in ``key_material``; we keep
+  the path (byte-compatible documents) but expose ``embed_key_material`` to
+  write the PEM instead;
+* ``states()`` paginates instead of stopping at 100 entries;
+* ``persist_state`` creates the manager directory first;
+* :meth:`lock` implements an advisory lock object ``<name>/.lock`` with an
+  owner token and TTL (the reference's TODO at ``backend.go:32``).
+"""
+
+import contextlib
+import json
+import os
+import time
+import uuid
+from typing import Any, Iterator, List, Optional, Tuple
+
+from ..cloud.triton import HTTPSignatureSigner, MantaClient
+from ..errors import BackendError
+from ..state import State
+from .base import CONFIG_FILE, TFSTATE_FILE, Backend
+
+ROOT = "/stor/triton-kubernetes"
+TF_ROOT = "/triton-kubernetes"
+
+
+class MantaBackend(Backend):
+    kind = "manta"
+
+    def __init__(
+        self,
+        account: str,
+        key_path: str,
+        key_id: str,
+        triton_url: str,
+        manta_url: str,
+        client: Optional[MantaClient] = None,
+        embed_key_material: bool = False,
+    ):
+        self.account = account
+        self.key_path = key_path
+        self.key_id = key_id
+        self.triton_url = triton_url
+        self.manta_url = manta_url
+        self.embed_key_material = embed_key_material
+        if client is None:
+            signer = HTTPSignatureSigner.from_path(account, key_path, key_id or None)
+            client = MantaClient(manta_url, signer)
+        self.client = client
+        self.client.put_directory(ROOT)
+
+    def _p(self, name: str, filename: Optional[str] = None) -> str:
+        base = f"{ROOT}/{name}"
+        return f"{base}/{filename}" if filename else base
+
+    def states(self) -> List[str]:
+        entries = self.client.list_directory(ROOT)
+        return [e["name"] for e in entries if e.get("type", "directory") == "directory"]
+
+    def state(self, name: str) -> State:
+        raw = self.client.get_object(self._p(name, CONFIG_FILE))
+        return State(name, raw if raw is not None else b"{}")
+
+    def persist_state(self, state: State) -> None:
+        self.client.put_directory(self._p(state.name))
+        self.client.put_object(self._p(state.name, CONFIG_FILE), state.bytes())
+
+    def delete_state(self, name: str) -> None:
+        self.client.delete(self._p(name, CONFIG_FILE))
+        self.client.delete(self._p(name, TFSTATE_FILE))
+        self.client.delete(self._p(name, ".lock"))
+        self.client.delete(self._p(name))
+
+    def state_terraform_config(self, name: str) -> Tuple[str, Any]:
+        material = self.key_path
+        if self.embed_key_material:
+            with open(os.path.expanduser(self.key_path), "r", encoding="utf-8") as fh:
+                material = fh.read()
+        return "terraform.backend.manta", {
+            "account": self.account,
+            "key_material": material,
+            "key_id": self.key_id,
+            "path": f"{TF_ROOT}/{name}",
+        }
+
+    def read_blob(self, name: str, filename: str) -> Optional[bytes]:
+        return self.client.get_object(self._p(name, filename))
+
+    def write_blob(self, name: str, filename: str, data: bytes) -> None:
+        self.client.put_directory(self._p(name))
+        self.client.put_object(self._p(name, filename), data)
+
+    @contextlib.contextmanager
+    def lock(self, name: str, timeout: float = 60.0, ttl: float = 900.0) -> Iterator[None]:
+        token = uuid.uuid4().hex
+        path = self._p(name, ".lock")
+        deadline = time.monotonic() + timeout
+        self.client.put_directory(self._p(name))
+        while True:
+            raw = self.client.get_object(path)
+            holder = json.loads(raw) if raw else None
+            if holder is None or holder.get("expires", 0) < time.time():
+                self.client.put_object(path, json.dumps({"token": token, "expires": time.time() + ttl}).encode())
+                check = json.loads(self.client.get_object(path) or b"{}")
+                if check.get("token") == token:
+                    break
+            if time.monotonic() > deadline:
+                raise BackendError(f"timed out waiting for the Manta state lock of '{name}'")
+            time.sleep(0.5)
+        try:
+            yield
+        finally:
+            raw = self.client.get_object(path)
+            if raw and json.loads(raw).get("token") == token:
+                self.client.delete(path)

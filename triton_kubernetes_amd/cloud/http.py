@@ -1,0 +1,162 @@
+"""Minimal HTTP(S) client on the standard library.
+
+All cloud/Rancher REST traffic goes through :class:`HTTPClient`: persistent
+per-host connections (``http.client`` keep-alive, one connection per thread),
+JSON helpers, optional TLS verification (Rancher uses self-signed certs: the
+reference calls it with ``curl --insecure``), and a request hook for signing
+(Triton/Manta HTTP signatures, AWS SigV4, bearer tokens).
+"""
+
+import http.client
+import json
+import ssl
+import threading
+import time
+import urllib.parse
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, Optional, Tuple
+
+from ..errors import TKError
+
+
+class HTTPError(TKError):
+    def __init__(self, status: int, body: bytes, method: str, url: str):
+        self.status = status
+        self.body = body
+        text = body.decode("utf-8", errors="replace")[:500]
+        super().__init__(f"{method} {url}: HTTP {status}: {text}")
+
+    def json(self) -> Any:
+        try:
+            return json.loads(self.body or b"null")
+        except ValueError:
+            return None
+
+
+@dataclass
+class Response:
+    status: int
+    headers: Dict[str, str]
+    body: bytes
+    elapsed: float = 0.0
+
+    def json(self) -> Any:
+        return json.loads(self.body or b"null")
+
+    def header(self, name: str, default: str = "") -> str:
+        return self.headers.get(name.lower(), default)
+
+
+Signer = Callable[[str, str, Dict[str, str], bytes], None]
+"""``signer(method, url, headers, body)`` mutates ``headers`` in place."""
+
+
+@dataclass
+class HTTPClient:
+    base_url: str = ""
+    verify_tls: bool = True
+    timeout: float = 30.0
+    signer: Optional[Signer] = None
+    default_headers: Dict[str, str] = field(default_factory=dict)
+    retries: int = 2
+    retry_backoff: float = 0.2
+
+    def __post_init__(self):
+        self._local = threading.local()
+
+    def _ssl_context(self) -> ssl.SSLContext:
+        ctx = ssl.create_default_context()
+        if not self.verify_tls:
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+        return ctx
+
+    def _conn(self, scheme: str, netloc: str) -> http.client.HTTPConnection:
+        pool = getattr(self._local, "pool", None)
+        if pool is None:
+            pool = self._local.pool = {}
+        key = (scheme, netloc)
+        conn = pool.get(key)
+        if conn is None:
+            if scheme == "https":
+                conn = http.client.HTTPSConnection(netloc, timeout=self.timeout, context=self._ssl_context())
+            else:
+                conn = http.client.HTTPConnection(netloc, timeout=self.timeout)
+            pool[key] = conn
+        return conn
+
+    def _drop(self, scheme: str, netloc: str) -> None:
+        pool = getattr(self._local, "pool", {})
+        conn = pool.pop((scheme, netloc), None)
+        if conn is not None:
+            conn.close()
+
+    def url(self, path: str) -> str:
+        if path.startswith("http://") or path.startswith("https://"):
+            return path
+        return self.base_url.rstrip("/") + "/" + path.lstrip("/")
+
+    def request(
+        self,
+        method: str,
+        path: str,
+        *,
+        params: Optional[Dict[str, Any]] = None,
+        json_body: Any = None,
+        data: Optional[bytes] = None,
+        headers: Optional[Dict[str, str]] = None,
+        ok: Tuple[int, ...] = (200, 201, 202, 204),
+    ) -> Response:
+        url = self.url(path)
+        if params:
+            url += ("&" if "?" in url else "?") + urllib.parse.urlencode(params, doseq=True)
+        hdrs = dict(self.default_headers)
+        hdrs.update(headers or {})
+        body = data or b""
+        if json_body is not None:
+            body = json.dumps(json_body).encode()
+            hdrs.setdefault("Content-Type", "application/json")
+        hdrs.setdefault("Accept", "application/json")
+        if self.signer is not None:
+            self.signer(method, url, hdrs, body)
+        parts = urllib.parse.urlsplit(url)
+        target = parts.path or "/"
+        if parts.query:
+            target += "?" + parts.query
+        attempt = 0
+        while True:
+            t0 = time.perf_counter()
+            try:
+                conn = self._conn(parts.scheme, parts.netloc)
+                conn.request(method, target, body=body if body or method in ("POST", "PUT") else None, headers=hdrs)
+                resp = conn.getresponse()
+                payload = resp.read()
+                out = Response(resp.status, {k.lower(): v for k, v in resp.getheaders()}, payload,
+                               time.perf_counter() - t0)
+                if resp.getheader("connection", "").lower() == "close":
+                    self._drop(parts.scheme, parts.netloc)
+                break
+            except (ConnectionError, http.client.HTTPException, OSError) as exc:
+                self._drop(parts.scheme, parts.netloc)
+                if attempt >= self.retries:
+                    raise TKError(f"{method} {url}: {exc}") from exc
+                attempt += 1
+                time.sleep(self.retry_backoff * attempt)
+        if out.status not in ok:
+            raise HTTPError(out.status, out.body, method, url)
+        return out
+
+    def get_json(self, path: str, **kw) -> Any:
+        return self.request("GET", path, **kw).json()
+
+    def post_json(self, path: str, body: Any, **kw) -> Any:
+        return self.request("POST", path, json_body=body, **kw).json()
+
+    def put_json(self, path: str, body: Any, **kw) -> Any:
+        return self.request("PUT", path, json_body=body, **kw).json()
+
+    def close(self) -> None:
+        pool = getattr(self._local, "pool", {})
+        for conn in pool.values():
+            conn.close()
+        pool.clear()

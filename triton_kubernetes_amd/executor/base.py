@@ -1,0 +1,62 @@
+"""Executor interface: turns a ``main.tf.json`` document into real resources.
+
+The reference has exactly one executor, ``shell/run_terraform.go`` (terraform
+init + apply / destroy in a temp dir).  We keep that (:class:`TerraformExecutor`)
+and add :class:`DirectExecutor`, a native implementation of the bare-metal
+module semantics that needs no Terraform binary and fans out to hosts in
+parallel.
+"""
+
+import json
+from typing import Dict, List, Optional
+
+from ..backend.base import Backend
+from ..state import State
+
+
+class Executor:
+    name = "abstract"
+
+    def apply(self, state: State, backend: Backend) -> None:
+        raise NotImplementedError
+
+    def destroy(self, state: State, backend: Backend, targets: List[str]) -> None:
+        """Destroy ``targets`` (``module.<key>`` addresses) or everything if empty."""
+        raise NotImplementedError
+
+    def outputs(self, state: State, backend: Backend, module_key: str) -> Dict[str, str]:
+        raise NotImplementedError
+
+    def print_outputs(self, state: State, backend: Backend, module_key: str, out) -> None:
+        outs = self.outputs(state, backend, module_key)
+        for k in sorted(outs):
+            out.write(f"{k} = {outs[k]}\n")
+        out.flush()
+
+
+def outputs_from_tfstate(raw: Optional[bytes], module_key: str) -> Dict[str, str]:
+    """Module outputs from a tfstate document.
+
+    Supports Terraform 0.11 (v3: ``modules[].path == ["root", key]``), the root
+    outputs written for Terraform >= 0.12 (``<key>__<output>``), and the
+    DirectExecutor's documents (v4-shaped with ``module_outputs``).
+    """
+    if not raw:
+        return {}
+    try:
+        doc = json.loads(raw)
+    except ValueError:
+        return {}
+    result: Dict[str, str] = {}
+    for mod in doc.get("modules", []) or []:  # v3
+        if mod.get("path") == ["root", module_key]:
+            for k, v in (mod.get("outputs") or {}).items():
+                result[k] = v.get("value") if isinstance(v, dict) else v
+    direct = (doc.get("module_outputs") or {}).get(module_key)
+    if isinstance(direct, dict):
+        result.update(direct)
+    prefix = f"{module_key}__"
+    for k, v in (doc.get("outputs") or {}).items():  # v4 root outputs
+        if k.startswith(prefix):
+            result[k[len(prefix):]] = v.get("value") if isinstance(v, dict) else v
+    return {k: ("" if v is None else str(v)) for k, v in result.items()}

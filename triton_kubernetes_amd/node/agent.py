@@ -1,0 +1,372 @@
+"""Node agent: executes bootstrap plans on a host, in-process.
+
+``tk-node-agent`` is the pull-side alternative to SSH delivery: it runs on a
+host (a systemd unit on real nodes, a thread per simulated node in tests and in
+``bench.py``) and executes :class:`~.plan.BootstrapPlan` steps natively.
+
+Security model: the agent never executes shell text it receives.  A plan's
+``shell`` fields are only for the SSH renderer; the agent dispatches on the
+step ``action`` and runs fixed, agent-side argv lists built from *validated*
+parameters (hostname, image reference, registry).  Every request must carry
+the agent's token (``X-TK-Agent-Token``); the agent refuses to start without
+one, generating a random token when none is given, and listens on 127.0.0.1
+unless told otherwise.
+
+Modes:
+
+* ``exec`` — runtime steps run the fixed commands (the container runtime must
+  already be installed; installing it is the SSH path's job);
+* ``sim`` — runtime steps are recorded as no-ops (simulated hosts have no
+  container runtime) and the ``agent`` step registers with Rancher through
+  ``POST /v3/connect/register`` instead of ``docker run rancher/agent``.
+
+In both modes the MI355X steps call the native probes directly on the agent's
+GPUs: topology labeller (N1), HBM/MFMA/memtest burn-in, RCCL env file and the
+node-level RCCL sweep (N2).
+
+HTTP API (JSON): ``GET /v1/info``, ``POST /v1/plan``, ``POST /v1/rccl-gate``
+(one rank of the cluster-wide RCCL gate), ``POST /v1/cleanup``.
+"""
+
+import base64
+import hmac
+import http.server
+import json
+import os
+import re
+import secrets
+import shutil
+import subprocess
+import threading
+import time
+import urllib.parse
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+from ..cloud.http import HTTPClient
+from ..parallel.rccl_env import render_env_file
+from ..rancher.fake import tunnel_params
+from ..utils.trace import span
+from .labels import labels_from_topology
+from .plan import BootstrapPlan, Step
+
+MODES = ("sim", "exec")
+_HOSTNAME_RE = re.compile(r"^[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?(\.[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?)*$")
+_IMAGE_RE = re.compile(r"^[A-Za-z0-9][A-Za-z0-9._/:@-]{0,254}$")
+_TOKEN_RE = re.compile(r"^[A-Za-z0-9._:-]{1,512}$")
+_URL_RE = re.compile(r"^https?://[A-Za-z0-9._:\[\]-]+(/[A-Za-z0-9._/-]*)?$")
+_ROLES = ("worker", "etcd", "controlplane")
+
+
+class StepFailed(RuntimeError):
+    def __init__(self, step: str, message: str):
+        super().__init__(f"step {step} failed: {message}")
+        self.step = step
+
+
+@dataclass
+class StepResult:
+    name: str
+    ok: bool
+    ms: float
+    detail: Any = None
+
+
+def _check(pattern: re.Pattern, value: str, what: str) -> str:
+    if not isinstance(value, str) or not pattern.match(value):
+        raise ValueError(f"invalid {what}: {value!r}")
+    return value
+
+
+@dataclass
+class NodeAgent:
+    name: str = "node"
+    mode: str = "sim"
+    devices: List[int] = field(default_factory=list)
+    root: str = "/"
+    token: str = ""
+    topology_override: Optional[Dict[str, Any]] = None
+    burnin_override: Optional[Callable[[int, str], Dict[str, Any]]] = None
+
+    def __post_init__(self):
+        if self.mode not in MODES:
+            raise ValueError(f"mode must be one of {MODES}")
+        if not self.token:
+            self.token = secrets.token_urlsafe(24)
+        self.lock = threading.Lock()
+        self.last_labels: Dict[str, str] = {}
+        self.history: List[Dict[str, Any]] = []
+        self._server: Optional[http.server.ThreadingHTTPServer] = None
+
+    # --- files ---------------------------------------------------------------------------
+    def path(self, p: str) -> str:
+        return os.path.join(self.root, p.lstrip("/")) if self.root not in ("", "/") else p
+
+    def write_file(self, p: str, data: str) -> str:
+        full = self.path(p)
+        os.makedirs(os.path.dirname(full), exist_ok=True)
+        with open(full, "w", encoding="utf-8") as fh:
+            fh.write(data)
+        return full
+
+    # --- plan execution ---------------------------------------------------------------------
+    def run_plan(self, plan: BootstrapPlan) -> Dict[str, Any]:
+        results: List[StepResult] = []
+        ctx: Dict[str, Any] = {"labels": {}, "capacity": {}}
+        t_plan = time.perf_counter()
+        error = None
+        with self.lock:
+            for step in plan.steps:
+                t0 = time.perf_counter()
+                try:
+                    with span(f"node.{step.action}", node=plan.hostname):
+                        detail = self._run_step(plan, step, ctx)
+                    results.append(StepResult(step.name, True, (time.perf_counter() - t0) * 1e3, detail))
+                except Exception as exc:  # noqa: BLE001 - reported to the executor
+                    results.append(StepResult(step.name, False, (time.perf_counter() - t0) * 1e3, str(exc)))
+                    error = f"{step.name}: {exc}"
+                    break
+        doc = {"hostname": plan.hostname, "ok": error is None, "error": error,
+               "ms": (time.perf_counter() - t_plan) * 1e3,
+               "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"]}
+        self.history.append(doc)
+        return doc
+
+    @staticmethod
+    def _run_argv(argv: List[str], stdin: Optional[str] = None, timeout: float = 1800) -> str:
+        proc = subprocess.run(argv, input=stdin, capture_output=True, text=True, timeout=timeout, check=False)
+        if proc.returncode != 0:
+            raise RuntimeError(f"{argv[0]} exited {proc.returncode}: {(proc.stderr or proc.stdout)[-1000:]}")
+        return proc.stdout
+
+    def _exec_runtime(self, plan: BootstrapPlan, step: Step) -> Any:
+        """Fixed command lists for the runtime actions (exec mode)."""
+        a = step.action
+        if a == "firewall":
+            if shutil.which("firewalld"):
+                self._run_argv(["systemctl", "disable", "--now", "firewalld.service"])
+            return {"firewalld": bool(shutil.which("firewalld"))}
+        if a == "runtime":
+            if not shutil.which("docker"):
+                raise RuntimeError("container runtime not installed (exec mode requires a pre-installed docker)")
+            return {"docker": self._run_argv(["docker", "version", "--format", "{{.Server.Version}}"]).strip()}
+        if a == "hostname":
+            hostname = _check(_HOSTNAME_RE, plan.hostname, "hostname")
+            return self._run_argv(["hostnamectl", "set-hostname", hostname])
+        if a == "registry_login":
+            reg = _check(_IMAGE_RE, step.params.get("registry", ""), "registry")
+            user = step.params.get("username", "")
+            password = step.params.get("password", "")
+            return self._run_argv(["docker", "login", "-u", user, "--password-stdin", reg], stdin=password)
+        raise StepFailed(step.name, f"unknown runtime action {a!r}")
+
+    def _exec_agent(self, plan: BootstrapPlan, step: Step, labels: Dict[str, str]) -> Any:
+        image = _check(_IMAGE_RE, step.params.get("image", ""), "agent image")
+        role = plan.role if plan.role in _ROLES else ""
+        if not role:
+            raise ValueError(f"invalid role {plan.role!r}")
+        argv = ["docker", "run", "-d", "--privileged", "--restart=unless-stopped", "--net=host",
+                "-v", "/etc/kubernetes:/etc/kubernetes", "-v", "/var/run:/var/run", image,
+                "--server", _check(_URL_RE, plan.rancher_url, "rancher url"),
+                "--token", _check(_TOKEN_RE, plan.token, "registration token"),
+                "--ca-checksum", _check(_TOKEN_RE, plan.ca_checksum, "ca checksum"), f"--{role}"]
+        for k in sorted(labels):
+            argv += ["--label", f"{k}={labels[k]}"]
+        return self._run_argv(argv)
+
+    def _run_step(self, plan: BootstrapPlan, step: Step, ctx: Dict[str, Any]) -> Any:
+        a = step.action
+        if a in ("firewall", "runtime", "hostname", "registry_login"):
+            if self.mode == "exec":
+                return self._exec_runtime(plan, step)
+            return {"simulated": True}
+        if a == "gpu_preflight":
+            return self._gpu_preflight(int(step.params.get("count", len(self.devices))))
+        if a == "gpu_labels":
+            topo = self._topology()
+            labels = labels_from_topology(topo)
+            ctx["labels"].update(labels)
+            self.last_labels = labels
+            self.write_file("/etc/triton-kubernetes/gpu-topology.json", json.dumps(topo))
+            self.write_file("/etc/triton-kubernetes/gpu-labels",
+                            "".join(f"{k}={v}\n" for k, v in sorted(labels.items())))
+            return labels
+        if a == "gpu_burnin":
+            level = step.params.get("level", "quick")
+            out = {}
+            for dev in self.devices:
+                res = self._burnin(dev, level)
+                out[str(dev)] = res
+                if not res.get("ok", False):
+                    raise StepFailed(step.name, f"GPU {dev}: {res.get('failures')}")
+            ctx["capacity"]["amd.com/gpu"] = len(self.devices)
+            return out
+        if a == "rccl_env":
+            return self.write_file("/etc/rccl/rccl.env", render_env_file(step.params.get("env", {})))
+        if a == "rccl_local":
+            if len(self.devices) < 2:
+                return {"skipped": "single GPU"}
+            from ..ops import rccl
+
+            res = rccl.sweep_local(len(self.devices))
+            if not res.ok:
+                raise StepFailed(step.name, "RCCL verification failed")
+            return res.to_json()
+        if a == "agent":
+            if plan.gpu is not None:
+                ctx["capacity"].setdefault("amd.com/gpu", len(self.devices))
+            if self.mode == "exec":
+                return self._exec_agent(plan, step, ctx["labels"])
+            return self._register(plan, ctx)
+        raise StepFailed(step.name, f"unknown action {a!r}")
+
+    def _gpu_preflight(self, expected: int) -> Dict[str, Any]:
+        if self.topology_override is not None:
+            n = len(self.topology_override.get("gpus", []))
+        else:
+            if not os.path.exists("/dev/kfd"):
+                raise RuntimeError("/dev/kfd missing (amdgpu driver not loaded)")
+            from ..ops import probe
+
+            total = probe.device_count()
+            n = min(total, len(self.devices)) if self.devices else total
+        if n < expected:
+            raise RuntimeError(f"expected {expected} GPUs, found {n}")
+        return {"gpus": n}
+
+    def _topology(self) -> Dict[str, Any]:
+        if self.topology_override is not None:
+            return self.topology_override
+        from ..ops import topo
+
+        doc = topo.discover()
+        gpus = doc.get("gpus", [])
+        if self.devices and gpus:
+            keep = [g for g in gpus if g.get("hip_id", g.get("index")) in self.devices]
+            if keep:
+                # re-index; drop links to GPUs that belong to other (simulated) nodes
+                idx = {g["index"]: i for i, g in enumerate(keep)}
+                trimmed = []
+                for g in keep:
+                    g = dict(g, index=idx[g["index"]])
+                    g["links"] = [dict(lk, peer=idx[lk["peer"]]) for lk in g.get("links", []) if lk["peer"] in idx]
+                    trimmed.append(g)
+                doc = dict(doc, gpus=trimmed)
+        return doc
+
+    def _burnin(self, dev: int, level: str) -> Dict[str, Any]:
+        if self.burnin_override is not None:
+            return self.burnin_override(dev, level)
+        from ..ops import probe
+
+        return probe.run_burnin(dev, level).to_json()
+
+    def _register(self, plan: BootstrapPlan, ctx: Dict[str, Any]) -> Dict[str, Any]:
+        roles = {"etcd": plan.role == "etcd", "controlplane": plan.role == "controlplane",
+                 "worker": plan.role == "worker"}
+        http = HTTPClient(base_url=plan.rancher_url, verify_tls=False)
+        hdrs = {"X-API-Tunnel-Token": plan.token,
+                "X-API-Tunnel-Params": tunnel_params(plan.hostname, roles, ctx["labels"], ctx["capacity"])}
+        return http.request("POST", "/v3/connect/register", headers=hdrs, data=b"{}").json()
+
+    # --- RCCL gate (one rank) -----------------------------------------------------------------
+    def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10) -> Dict[str, Any]:
+        from ..ops import rccl
+
+        dev = self.devices[0] if self.devices else 0
+        with span("node.rccl_gate", node=self.name, rank=rank, world=world):
+            res = rccl.sweep_rank(rank, world, uid, dev, sizes, iters=iters, warmup=2)
+        return res.to_json()
+
+    # --- HTTP server ----------------------------------------------------------------------------
+    def serve(self, host: str = "127.0.0.1", port: int = 0) -> str:
+        agent = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *args):
+                pass
+
+            def _reply(self, code: int, obj: Any):
+                body = json.dumps(obj).encode()
+                self.send_response(code)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def _body(self):
+                n = int(self.headers.get("Content-Length") or 0)
+                return json.loads(self.rfile.read(n) or b"{}") if n else {}
+
+            def _auth(self) -> bool:
+                return hmac.compare_digest(self.headers.get("X-TK-Agent-Token", ""), agent.token)
+
+            def do_GET(self):
+                if not self._auth():
+                    return self._reply(401, {"error": "unauthorized"})
+                if urllib.parse.urlsplit(self.path).path == "/v1/info":
+                    return self._reply(200, {"name": agent.name, "mode": agent.mode, "devices": agent.devices,
+                                             "labels": agent.last_labels})
+                return self._reply(404, {"error": "not found"})
+
+            def do_POST(self):
+                if not self._auth():
+                    return self._reply(401, {"error": "unauthorized"})
+                path = urllib.parse.urlsplit(self.path).path
+                try:
+                    body = self._body()
+                    if path == "/v1/plan":
+                        return self._reply(200, agent.run_plan(BootstrapPlan.from_json(body["plan"])))
+                    if path == "/v1/rccl-gate":
+                        uid = base64.b64decode(body["uid"])
+                        return self._reply(200, agent.rccl_gate(int(body["rank"]), int(body["world"]), uid,
+                                                                [int(s) for s in body.get("sizes", [1 << 20])],
+                                                                int(body.get("iters", 10))))
+                    if path == "/v1/cleanup":
+                        agent.last_labels = {}
+                        return self._reply(200, {"ok": True})
+                except Exception as exc:  # noqa: BLE001
+                    return self._reply(500, {"error": f"{type(exc).__name__}: {exc}"})
+                return self._reply(404, {"error": "not found"})
+
+        self._server = http.server.ThreadingHTTPServer((host, port), H)
+        self._server.daemon_threads = True
+        threading.Thread(target=self._server.serve_forever, name=f"agent-{self.name}", daemon=True).start()
+        h, p = self._server.server_address[:2]
+        return f"http://{h}:{p}"
+
+    def stop(self) -> None:
+        if self._server is not None:
+            self._server.shutdown()
+            self._server.server_close()
+            self._server = None
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    """``tk-node-agent``: serve the agent API on a host (127.0.0.1 by default)."""
+    import argparse
+
+    ap = argparse.ArgumentParser(prog="tk-node-agent")
+    ap.add_argument("--listen", default="127.0.0.1:7946")
+    ap.add_argument("--mode", default="exec", choices=MODES)
+    ap.add_argument("--devices", default="", help="comma-separated local GPU indices")
+    ap.add_argument("--token-file", default="", help="file holding the shared agent token")
+    ap.add_argument("--root", default="/")
+    args = ap.parse_args(argv)
+    token = ""
+    if args.token_file:
+        with open(args.token_file, "r", encoding="utf-8") as fh:
+            token = fh.read().strip()
+    host, _, port = args.listen.rpartition(":")
+    devices = [int(d) for d in args.devices.split(",") if d.strip()]
+    agent = NodeAgent(name=host, mode=args.mode, devices=devices, root=args.root, token=token)
+    url = agent.serve(host or "127.0.0.1", int(port))
+    print(json.dumps({"listening": url, "token_from_file": bool(token)}), flush=True)
+    try:
+        while True:
+            time.sleep(3600)
+    except KeyboardInterrupt:
+        agent.stop()
+    return 0

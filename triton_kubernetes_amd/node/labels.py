@@ -1,0 +1,109 @@
+"""Kubernetes node labels for AMD GPU nodes, derived from the N1 topology document.
+
+Label keys follow the ROCm k8s node-labeller's ``amd.com/gpu.*`` namespace,
+plus xGMI keys used for topology-aware scheduling:
+
+=====================================  =============================================
+``amd.com/gpu.present``                ``true``
+``amd.com/gpu.count``                  GPUs on the node
+``amd.com/gpu.product-name``           e.g. ``MI355X`` (from the market name)
+``amd.com/gpu.family``                 ``AI`` for Instinct parts
+``amd.com/gpu.device-id``              PCI device id
+``amd.com/gpu.cu-count``               CUs per GPU (min over GPUs)
+``amd.com/gpu.vram``                   VRAM per GPU, e.g. ``288G``
+``amd.com/gpu.target``                 ``gfx950``
+``amd.com/gpu.compute-partition``      ``spx`` / ``cpx`` ... (lower-cased)
+``amd.com/gpu.memory-partition``       ``nps1`` / ``nps4`` ...
+``amd.com/xgmi.hive-id``               hive id shared by the node's GPUs (hex)
+``amd.com/xgmi.links-per-gpu``         min xGMI peers over GPUs
+``amd.com/xgmi.fully-connected``       every GPU has an xGMI link to every other
+=====================================  =============================================
+
+Pods that need all 8 GPUs on one xGMI hive use node affinity on
+``amd.com/xgmi.fully-connected=true`` + ``amd.com/gpu.count=8``; multi-node jobs
+use pod affinity on ``amd.com/xgmi.hive-id`` to stay inside a hive where the
+fabric spans nodes (see ``k8s/manifests.py``).
+"""
+
+import re
+from typing import Any, Dict, List
+
+LABEL_PREFIX = "amd.com/"
+_VALUE_RE = re.compile(r"[^A-Za-z0-9._-]")
+
+
+def _label_value(v: Any) -> str:
+    s = _VALUE_RE.sub("-", str(v)).strip("-._")
+    return s[:63]
+
+
+def product_name(market_name: str) -> str:
+    m = re.search(r"(MI\d{3}[A-Z]*)", market_name or "")
+    return m.group(1) if m else _label_value(market_name)
+
+
+def labels_from_topology(doc: Dict[str, Any]) -> Dict[str, str]:
+    gpus: List[Dict[str, Any]] = doc.get("gpus") or []
+    if not gpus:
+        return {"amd.com/gpu.present": "false"}
+    labels: Dict[str, str] = {
+        "amd.com/gpu.present": "true",
+        "amd.com/gpu.count": str(len(gpus)),
+    }
+    names = {product_name(g.get("market_name", "")) for g in gpus if g.get("market_name")}
+    if len(names) == 1:
+        name = names.pop()
+        labels["amd.com/gpu.product-name"] = _label_value(name)
+        if name.startswith("MI"):
+            labels["amd.com/gpu.family"] = "AI"
+    dev_ids = {g.get("device_id") for g in gpus if g.get("device_id")}
+    if len(dev_ids) == 1:
+        labels["amd.com/gpu.device-id"] = _label_value(dev_ids.pop())
+    cus = [int(g["compute_units"]) for g in gpus if g.get("compute_units")]
+    if cus:
+        labels["amd.com/gpu.cu-count"] = str(min(cus))
+    vram = [int(g["vram_mb"]) for g in gpus if g.get("vram_mb")]
+    if vram:
+        labels["amd.com/gpu.vram"] = f"{min(vram) // 1024}G"
+    targets = {g.get("target_graphics_version") for g in gpus if g.get("target_graphics_version")}
+    if len(targets) == 1:
+        labels["amd.com/gpu.target"] = _label_value(targets.pop())
+    for key, label in (("compute_partition", "compute-partition"), ("memory_partition", "memory-partition")):
+        vals = {str(g.get(key, "")).lower() for g in gpus if g.get(key)}
+        if len(vals) == 1:
+            labels[f"amd.com/gpu.{label}"] = _label_value(vals.pop())
+    hives = {g.get("xgmi_hive_id") for g in gpus if g.get("xgmi_hive_id") not in (None, "", "0x0")}
+    if len(hives) == 1:
+        labels["amd.com/xgmi.hive-id"] = _label_value(hives.pop())
+    xgmi_peers = []
+    for g in gpus:
+        peers = {lk["peer"] for lk in g.get("links", []) if lk.get("type") == "XGMI"}
+        xgmi_peers.append(len(peers))
+    labels["amd.com/xgmi.links-per-gpu"] = str(min(xgmi_peers))
+    labels["amd.com/xgmi.fully-connected"] = "true" if len(gpus) > 1 and min(xgmi_peers) == len(gpus) - 1 \
+        else "false"
+    ecc = [int(g.get("ecc_uncorrectable", 0)) for g in gpus]
+    labels["amd.com/gpu.ecc-uncorrectable"] = str(sum(ecc))
+    return labels
+
+
+def agent_label_flags(labels: Dict[str, str]) -> List[str]:
+    """``--label k=v`` arguments for ``rancher/agent``."""
+    out: List[str] = []
+    for k in sorted(labels):
+        out += ["--label", f"{k}={labels[k]}"]
+    return out
+
+
+def synthetic_topology(ngpus: int = 8, hive: str = "0xabc123", product: str = "AMD Instinct MI355X",
+                       cus: int = 256, vram_mb: int = 294912) -> Dict[str, Any]:
+    """A fully connected 8xMI355X topology document (tests / dry runs)."""
+    gpus = []
+    for i in range(ngpus):
+        gpus.append({
+            "index": i, "market_name": product, "device_id": "0x75a3", "compute_units": cus, "vram_mb": vram_mb,
+            "target_graphics_version": "gfx950", "compute_partition": "SPX", "memory_partition": "NPS1",
+            "xgmi_hive_id": hive, "ecc_uncorrectable": 0,
+            "links": [{"peer": j, "type": "XGMI", "hops": 1, "p2p": True} for j in range(ngpus) if j != i],
+        })
+    return {"source": "synthetic", "gpus": gpus}

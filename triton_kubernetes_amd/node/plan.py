@@ -1,0 +1,193 @@
+"""Node bootstrap plans: one definition, two renderers.
+
+A :class:`BootstrapPlan` is the ordered list of steps a host runs to join a
+cluster (the reference's ``install_rancher_agent.sh.tpl``, S5, plus the MI355X
+steps).  It renders to
+
+* a POSIX shell script (:meth:`BootstrapPlan.render_shell`) delivered over SSH
+  or as cloud-init user-data — each step a function with timing markers
+  ``::tk-step <name> <status> <ms>`` that the executor parses; and
+* a structured document (:meth:`BootstrapPlan.to_json`) that a
+  :class:`~.agent.NodeAgent` executes step by step in-process, running the GPU
+  steps through the native MI355X probes.
+
+Step catalogue (``action`` ids):
+
+==================  ==============================================================
+``firewall``        stop/disable firewalld (S5)
+``runtime``         install the container runtime if absent, overlay2 (S1/S5/S6)
+``hostname``        ``hostnamectl set-hostname`` (S5)
+``registry_login``  ``docker login`` when registry credentials are given (S5)
+``gpu_preflight``   MI355X: amdgpu loaded, ``/dev/kfd`` + ``/dev/dri`` present, N GPUs
+``gpu_labels``      MI355X: N1 topology labeller -> node labels file
+``gpu_burnin``      MI355X: HBM / MFMA / memtest probes per GPU
+``rccl_env``        MI355X: write ``/etc/rccl/rccl.env``
+``rccl_local``      MI355X: node-level RCCL all-reduce sweep over the local GPUs (N2)
+``agent``           run ``rancher/agent`` with ``--server/--token/--ca-checksum/--<role>``
+                    and ``--label`` flags (GPU labels on MI355X nodes)
+==================  ==============================================================
+"""
+
+import json
+import shlex
+from dataclasses import asdict, dataclass, field
+from typing import Any, Dict, List, Optional
+
+from ..parallel.rccl_env import render_env_file
+
+DEFAULT_DOCKER_INSTALL_URL = "https://releases.rancher.com/install-docker/20.10.sh"
+DEFAULT_AGENT_IMAGE = "rancher/rancher-agent:v2.8.5"
+LABEL_FILE = "/etc/triton-kubernetes/gpu-labels"
+TOPOLOGY_FILE = "/etc/triton-kubernetes/gpu-topology.json"
+RCCL_ENV_FILE = "/etc/rccl/rccl.env"
+TOOLS_DIR = "/opt/triton-kubernetes/bin"
+
+ROLE_FLAG = {"worker": "worker", "etcd": "etcd", "control": "controlplane", "controlplane": "controlplane"}
+
+
+@dataclass
+class Step:
+    name: str
+    action: str
+    shell: str
+    params: Dict[str, Any] = field(default_factory=dict)
+    gpu: bool = False
+
+
+@dataclass
+class BootstrapPlan:
+    hostname: str
+    role: str  # worker | etcd | controlplane
+    rancher_url: str
+    token: str
+    ca_checksum: str
+    steps: List[Step] = field(default_factory=list)
+    gpu: Optional[Dict[str, Any]] = None
+
+    def step_names(self) -> List[str]:
+        return [s.name for s in self.steps]
+
+    def to_json(self) -> Dict[str, Any]:
+        return asdict(self)
+
+    @classmethod
+    def from_json(cls, doc: Dict[str, Any]) -> "BootstrapPlan":
+        steps = [Step(**s) for s in doc.get("steps", [])]
+        d = {k: v for k, v in doc.items() if k != "steps"}
+        return cls(steps=steps, **d)
+
+    def render_shell(self) -> str:
+        out = [
+            "#!/bin/bash",
+            f"# triton-kubernetes node bootstrap: {self.hostname} ({self.role})",
+            "set -euo pipefail",
+            "_tk_now() { date +%s%3N; }",
+            "_tk_step() { local n=$1; shift; local t0; t0=$(_tk_now); echo \"::tk-step $n start 0\";",
+            "  if \"$@\"; then echo \"::tk-step $n ok $(( $(_tk_now) - t0 ))\";",
+            "  else local rc=$?; echo \"::tk-step $n failed $(( $(_tk_now) - t0 ))\" >&2; exit $rc; fi; }",
+        ]
+        for s in self.steps:
+            body = s.shell.strip("\n")
+            out.append(f"step_{s.name}() {{")
+            out.extend("  " + ln if ln else "" for ln in body.splitlines())
+            out.append("}")
+        for s in self.steps:
+            out.append(f"_tk_step {s.name} step_{s.name}")
+        out.append("echo '::tk-done'")
+        return "\n".join(out) + "\n"
+
+
+def _q(v: Any) -> str:
+    return shlex.quote(str(v))
+
+
+def host_role(cfg: Dict[str, Any]) -> str:
+    labels = cfg.get("rancher_host_labels") or {}
+    for k in ("control", "etcd", "worker"):
+        if str(labels.get(k, "")).lower() == "true":
+            return ROLE_FLAG[k]
+    raise ValueError(f"node {cfg.get('hostname')!r} has no rancher_host_labels role")
+
+
+def build_host_plan(cfg: Dict[str, Any], rancher_url: str, token: str, ca_checksum: str,
+                    mi355x: bool = False) -> BootstrapPlan:
+    """Plan for a ``*-rancher-k8s-host`` module config with resolved interpolations."""
+    role = host_role(cfg)
+    hostname = cfg.get("hostname", "")
+    plan = BootstrapPlan(hostname, role, rancher_url, token, ca_checksum)
+    install_url = cfg.get("docker_engine_install_url") or DEFAULT_DOCKER_INSTALL_URL
+    image = cfg.get("rancher_agent_image") or DEFAULT_AGENT_IMAGE
+    reg, reg_user, reg_pass = (cfg.get("rancher_registry", ""), cfg.get("rancher_registry_username", ""),
+                               cfg.get("rancher_registry_password", ""))
+    plan.steps.append(Step("firewall", "firewall", """
+if command -v firewalld >/dev/null 2>&1; then
+  sudo systemctl stop firewalld.service || true
+  sudo systemctl disable firewalld.service || true
+fi"""))
+    plan.steps.append(Step("runtime", "runtime", f"""
+if ! command -v docker >/dev/null 2>&1; then
+  curl -fsSL {_q(install_url)} | sudo sh
+fi
+if [ ! -f /etc/docker/daemon.json ] || ! grep -q overlay2 /etc/docker/daemon.json; then
+  echo '{{"storage-driver": "overlay2"}}' | sudo tee /etc/docker/daemon.json >/dev/null
+  sudo systemctl restart docker || sudo service docker restart
+fi""", {"install_url": install_url}))
+    plan.steps.append(Step("hostname", "hostname", f"sudo hostnamectl set-hostname {_q(hostname)}",
+                           {"hostname": hostname}))
+    if reg_user:
+        plan.steps.append(Step("registry_login", "registry_login",
+                               f"echo {_q(reg_pass)} | sudo docker login -u {_q(reg_user)} --password-stdin {_q(reg)}",
+                               {"registry": reg, "username": reg_user, "password": reg_pass}))
+    label_args = ""
+    if mi355x:
+        ngpu = int(cfg.get("gpu_count", 8) or 8)
+        burnin = cfg.get("gpu_burnin", "quick")
+        env = dict(cfg.get("rccl_env") or {})
+        plan.gpu = {"product": cfg.get("gpu_product", "MI355X"), "count": ngpu, "burnin": burnin}
+        plan.steps.append(Step("gpu_preflight", "gpu_preflight", f"""
+lsmod | grep -q '^amdgpu' || {{ echo 'amdgpu kernel module not loaded' >&2; exit 1; }}
+test -c /dev/kfd || {{ echo '/dev/kfd missing' >&2; exit 1; }}
+test -d /dev/dri || {{ echo '/dev/dri missing' >&2; exit 1; }}
+n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
+[ "$n" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs, found $n render nodes" >&2; exit 1; }}
+sudo usermod -aG video,render "$(id -un)" || true""", {"count": ngpu}, gpu=True))
+        plan.steps.append(Step("gpu_labels", "gpu_labels", f"""
+sudo mkdir -p "$(dirname {LABEL_FILE})"
+{TOOLS_DIR}/amdgpu-topo-labeller | sudo tee {TOPOLOGY_FILE} >/dev/null
+{TOOLS_DIR}/amdgpu-topo-labeller --labels | sudo tee {LABEL_FILE} >/dev/null""", gpu=True))
+        if burnin != "off":
+            plan.steps.append(Step("gpu_burnin", "gpu_burnin", f"""
+{TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} | sudo tee /etc/triton-kubernetes/gpu-burnin.json""",
+                                   {"level": burnin}, gpu=True))
+        plan.steps.append(Step("rccl_env", "rccl_env", f"""
+sudo mkdir -p "$(dirname {RCCL_ENV_FILE})"
+sudo tee {RCCL_ENV_FILE} >/dev/null <<'TK_RCCL_EOF'
+{render_env_file(env).rstrip()}
+TK_RCCL_EOF""", {"env": env}, gpu=True))
+        if ngpu > 1:
+            plan.steps.append(Step("rccl_local", "rccl_local",
+                                   f"{TOOLS_DIR}/rccl-ready --ngpus {ngpu} --min-busbw "
+                                   f"{float(cfg.get('rccl_min_busbw', 0) or 0)}",
+                                   {"count": ngpu}, gpu=True))
+        label_args = f' $(sed "s/^/--label /" {LABEL_FILE} | tr "\\n" " ")'
+    plan.steps.append(Step("agent", "agent", (
+        f"sudo docker run -d --privileged --restart=unless-stopped --net=host "
+        f"-v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run {_q(image)} "
+        f"--server {_q(rancher_url)} --token {_q(token)} --ca-checksum {_q(ca_checksum)} --{role}{label_args}"),
+        {"image": image, "role": role}))
+    return plan
+
+
+def parse_step_markers(output: str) -> Dict[str, Dict[str, Any]]:
+    """``::tk-step`` markers of a shell run -> ``{step: {status, ms}}``."""
+    steps: Dict[str, Dict[str, Any]] = {}
+    for line in output.splitlines():
+        if line.startswith("::tk-step "):
+            parts = line.split()
+            if len(parts) >= 4:
+                steps[parts[1]] = {"status": parts[2], "ms": int(parts[3]) if parts[3].isdigit() else 0}
+    return steps
+
+
+def plan_json(plan: BootstrapPlan) -> str:
+    return json.dumps(plan.to_json())

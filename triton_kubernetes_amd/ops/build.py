@@ -1,0 +1,117 @@
+"""Build the native MI355X components in-tree (``triton_kubernetes_amd/ops/lib``).
+
+Targets (gfx950 only; ``hipcc`` cross-compiles without a GPU):
+
+=============================  ==========================================  =========
+artifact                       source                                      toolchain
+=============================  ==========================================  =========
+``libtk_gpu_probe.so``         ``csrc/tk_gpu_probe.hip`` (HBM/MFMA/memtest)  hipcc
+``libtk_rccl.so``              ``csrc/tk_rccl_probe.hip`` (N2, RCCL)          hipcc
+``rccl-ready``                 same, ``-DTK_RCCL_MAIN``                     hipcc
+``libtk_topo.so``              ``csrc/tk_topo.cpp`` (N1, amd_smi)            g++
+``amdgpu-topo-labeller``       same, ``-DTK_TOPO_MAIN``                     g++
+=============================  ==========================================  =========
+
+Usage: ``python -m triton_kubernetes_amd.ops.build [--force] [-j N]``.
+Rebuilds only targets whose sources are newer than the artifact.
+"""
+
+import argparse
+import concurrent.futures as cf
+import os
+import shutil
+import subprocess
+import sys
+from dataclasses import dataclass
+from typing import List, Sequence
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "lib")
+ROCM = os.environ.get("ROCM_PATH", "/opt/rocm")
+ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
+
+HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result", "-Wno-unused-value",
+             "-Wno-unused-command-line-argument"]
+RPATH = [f"-Wl,-rpath,{ROCM}/lib"]
+# VGPR-form MFMA accumulators: see the note at the top of csrc/tk_gpu_probe.hip
+MFMA_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+
+
+@dataclass
+class Target:
+    name: str
+    sources: List[str]
+    cmd: List[str]
+
+    @property
+    def output(self) -> str:
+        return os.path.join(LIB, self.name)
+
+    def stale(self) -> bool:
+        if not os.path.exists(self.output):
+            return True
+        mtime = os.path.getmtime(self.output)
+        return any(os.path.getmtime(s) > mtime for s in self.sources)
+
+
+def _hipcc() -> str:
+    return shutil.which("hipcc") or os.path.join(ROCM, "bin", "hipcc")
+
+
+def targets() -> List[Target]:
+    hipcc = _hipcc()
+    probe = os.path.join(CSRC, "tk_gpu_probe.hip")
+    rccl = os.path.join(CSRC, "tk_rccl_probe.hip")
+    topo = os.path.join(CSRC, "tk_topo.cpp")
+    out = lambda n: os.path.join(LIB, n)  # noqa: E731
+    return [
+        Target("libtk_gpu_probe.so", [probe],
+               [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-fPIC", "-shared", probe, "-o", out("libtk_gpu_probe.so"), *RPATH]),
+        Target("libtk_rccl.so", [rccl],
+               [hipcc, *HIP_FLAGS, "-fPIC", "-shared", rccl, "-o", out("libtk_rccl.so"), f"-L{ROCM}/lib",
+                "-lrccl", *RPATH]),
+        Target("rccl-ready", [rccl],
+               [hipcc, *HIP_FLAGS, "-DTK_RCCL_MAIN", rccl, "-o", out("rccl-ready"), f"-L{ROCM}/lib", "-lrccl",
+                *RPATH]),
+        Target("libtk_topo.so", [topo],
+               ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", f"-I{ROCM}/include", topo, "-o",
+                out("libtk_topo.so"), f"-L{ROCM}/lib", "-lamd_smi", *RPATH]),
+        Target("amdgpu-topo-labeller", [topo],
+               ["g++", "-O2", "-std=c++17", "-DTK_TOPO_MAIN", f"-I{ROCM}/include", topo, "-o",
+                out("amdgpu-topo-labeller"), f"-L{ROCM}/lib", "-lamd_smi", *RPATH]),
+    ]
+
+
+def _run(t: Target) -> str:
+    proc = subprocess.run(t.cmd, capture_output=True, text=True, check=False)
+    if proc.returncode != 0:
+        raise RuntimeError(f"building {t.name} failed:\n$ {' '.join(t.cmd)}\n{proc.stdout}\n{proc.stderr}")
+    return t.name
+
+
+def build(force: bool = False, jobs: int = 4, only: Sequence[str] = ()) -> List[str]:
+    os.makedirs(LIB, exist_ok=True)
+    todo = [t for t in targets() if (force or t.stale()) and (not only or t.name in only)]
+    built: List[str] = []
+    if not todo:
+        return built
+    with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as pool:
+        for name in pool.map(_run, todo):
+            built.append(name)
+    return built
+
+
+def main(argv: Sequence[str] = ()) -> int:
+    ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
+    ap.add_argument("--force", action="store_true")
+    ap.add_argument("-j", "--jobs", type=int, default=min(8, os.cpu_count() or 4))
+    ap.add_argument("targets", nargs="*")
+    args = ap.parse_args(list(argv) or sys.argv[1:])
+    built = build(args.force, args.jobs, args.targets)
+    print(f"built: {', '.join(built) if built else '(up to date)'} -> {LIB}")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,81 @@
+"""Command line for the native probes (what a node bootstrap or an operator runs).
+
+    python -m triton_kubernetes_amd.ops.cli burnin [--device N|--all] [--level quick|full]
+    python -m triton_kubernetes_amd.ops.cli topology
+    python -m triton_kubernetes_amd.ops.cli labels
+    python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
+    python -m triton_kubernetes_amd.ops.cli hbm|mfma [...]
+
+Every command prints one JSON document; the exit status is non-zero when the
+GPU(s) fail the gate.
+"""
+
+import argparse
+import json
+import sys
+from typing import Sequence
+
+
+def main(argv: Sequence[str] = ()) -> int:
+    ap = argparse.ArgumentParser(prog="tk-gpu")
+    sub = ap.add_subparsers(dest="cmd", required=True)
+    b = sub.add_parser("burnin")
+    b.add_argument("--device", type=int, default=0)
+    b.add_argument("--all", action="store_true")
+    b.add_argument("--level", default="quick", choices=["quick", "full", "off"])
+    sub.add_parser("topology")
+    sub.add_parser("labels")
+    r = sub.add_parser("rccl-local")
+    r.add_argument("--ngpus", type=int, default=0)
+    r.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    h = sub.add_parser("hbm")
+    h.add_argument("--device", type=int, default=0)
+    h.add_argument("--gib", type=float, default=4.0)
+    h.add_argument("--blocks-per-cu", type=int, default=16)
+    m = sub.add_parser("mfma")
+    m.add_argument("--device", type=int, default=0)
+    m.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "f32"])
+    m.add_argument("--iters", type=int, default=20000)
+    m.add_argument("--blocks-per-cu", type=int, default=2)
+    args = ap.parse_args(list(argv) or sys.argv[1:])
+
+    if args.cmd == "burnin":
+        from . import probe
+
+        devs = range(probe.device_count()) if args.all else [args.device]
+        results = [probe.run_burnin(d, args.level) for d in devs]
+        print(json.dumps([r.to_json() for r in results], indent=2, default=str))
+        return 0 if all(r.ok for r in results) else 1
+    if args.cmd == "topology":
+        from . import topo
+
+        print(json.dumps(topo.discover(), indent=2))
+        return 0
+    if args.cmd == "labels":
+        from ..node.labels import labels_from_topology
+        from . import topo
+
+        print(json.dumps(labels_from_topology(topo.discover()), indent=2, sort_keys=True))
+        return 0
+    if args.cmd == "rccl-local":
+        from . import probe, rccl
+
+        n = args.ngpus or probe.device_count()
+        res = rccl.sweep_local(n, dtype=args.dtype)
+        print(json.dumps(res.to_json(), indent=2))
+        return 0 if res.ok else 1
+    if args.cmd == "hbm":
+        from . import probe
+
+        print(json.dumps(probe.hbm_bandwidth(args.device, int(args.gib * (1 << 30)), 5, args.blocks_per_cu)))
+        return 0
+    if args.cmd == "mfma":
+        from . import probe
+
+        print(json.dumps(probe.mfma_peak(args.device, args.dtype, args.iters, 3, args.blocks_per_cu)))
+        return 0
+    return 2
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,284 @@
+// rccl-ready (N2): RCCL all-reduce readiness / bandwidth probe.
+//
+// The "GPU-ready" gate of the readiness waiter.  Two entry points:
+//
+//  * tkr_sweep_rank  — one rank of a multi-process (multi-node) communicator,
+//    bootstrapped from a ncclUniqueId the caller distributes (the cluster-wide
+//    gate across MI355X workers, one process per GPU);
+//  * tkr_sweep_local — one process driving every local GPU with
+//    ncclCommInitAll + grouped calls (the node-level gate on an 8xMI355X node,
+//    where all traffic is point-to-point xGMI).
+//
+// For each message size: ncclAllReduce(sum) of a buffer holding (rank + 1) on
+// every rank, verified on device against world*(world+1)/2 (exact in f32 and
+// in bf16 for world <= 15), timed with HIP events over `iters` launches after
+// `warmup`.  Reported as algbw = bytes / t and busbw = algbw * 2(n-1)/n (the
+// ring all-reduce bus bandwidth, comparable with the per-link xGMI rate).
+//
+// C ABI for ctypes; the stand-alone `rccl-ready` executable (-DTK_RCCL_MAIN)
+// runs the local sweep and exits non-zero when verification fails or the
+// largest message's busbw is below the --min-busbw threshold.
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <vector>
+
+static thread_local char g_err[512];
+extern "C" const char* tkr_last_error() { return g_err; }
+
+#define HIPCHECK(call)                                                                            \
+  do {                                                                                            \
+    hipError_t _e = (call);                                                                       \
+    if (_e != hipSuccess) {                                                                       \
+      snprintf(g_err, sizeof(g_err), "%s: %s", #call, hipGetErrorString(_e));                     \
+      return -1;                                                                                  \
+    }                                                                                             \
+  } while (0)
+
+#define NCCLCHECK(call)                                                                           \
+  do {                                                                                            \
+    ncclResult_t _r = (call);                                                                     \
+    if (_r != ncclSuccess) {                                                                      \
+      snprintf(g_err, sizeof(g_err), "%s: %s", #call, ncclGetErrorString(_r));                    \
+      return -2;                                                                                  \
+    }                                                                                             \
+  } while (0)
+
+__global__ void k_fill_f32(float* p, size_t n, float v) {
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = v;
+}
+__global__ void k_fill_bf16(__bf16* p, size_t n, float v) {
+  const __bf16 b = (__bf16)v;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x) p[i] = b;
+}
+__global__ void k_check_f32(const float* p, size_t n, float want, unsigned long long* bad) {
+  unsigned int c = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    c += (p[i] != want);
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, (unsigned long long)c);
+}
+__global__ void k_check_bf16(const __bf16* p, size_t n, float want, unsigned long long* bad) {
+  unsigned int c = 0;
+  for (size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    c += ((float)p[i] != want);
+  for (int off = 32; off > 0; off >>= 1) c += __shfl_down(c, off, 64);
+  if ((threadIdx.x & 63) == 0 && c) atomicAdd(bad, (unsigned long long)c);
+}
+
+extern "C" int tkr_version() {
+  int v = 0;
+  ncclGetVersion(&v);
+  return v;
+}
+
+extern "C" int tkr_unique_id(unsigned char* out128) {
+  ncclUniqueId id;
+  NCCLCHECK(ncclGetUniqueId(&id));
+  memcpy(out128, id.internal, NCCL_UNIQUE_ID_BYTES);
+  return 0;
+}
+
+struct RankBufs {
+  void* send = nullptr;
+  void* recv = nullptr;
+  unsigned long long* bad = nullptr;
+  hipStream_t stream = nullptr;
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+};
+
+static int alloc_bufs(RankBufs& b, size_t max_bytes) {
+  HIPCHECK(hipMalloc(&b.send, max_bytes));
+  HIPCHECK(hipMalloc(&b.recv, max_bytes));
+  HIPCHECK(hipMalloc(&b.bad, sizeof(unsigned long long)));
+  HIPCHECK(hipStreamCreateWithFlags(&b.stream, hipStreamNonBlocking));
+  HIPCHECK(hipEventCreate(&b.t0));
+  HIPCHECK(hipEventCreate(&b.t1));
+  return 0;
+}
+
+static void free_bufs(RankBufs& b) {
+  if (b.t0) (void)hipEventDestroy(b.t0);
+  if (b.t1) (void)hipEventDestroy(b.t1);
+  if (b.stream) (void)hipStreamDestroy(b.stream);
+  if (b.send) (void)hipFree(b.send);
+  if (b.recv) (void)hipFree(b.recv);
+  if (b.bad) (void)hipFree(b.bad);
+  b = RankBufs{};
+}
+
+static int fill(RankBufs& b, size_t count, int dtype, float v) {
+  if (dtype == 1) k_fill_bf16<<<512, 256, 0, b.stream>>>((__bf16*)b.send, count, v);
+  else k_fill_f32<<<512, 256, 0, b.stream>>>((float*)b.send, count, v);
+  HIPCHECK(hipGetLastError());
+  HIPCHECK(hipMemsetAsync(b.bad, 0, sizeof(unsigned long long), b.stream));
+  return 0;
+}
+
+static int check(RankBufs& b, size_t count, int dtype, float want) {
+  if (dtype == 1) k_check_bf16<<<512, 256, 0, b.stream>>>((const __bf16*)b.recv, count, want, b.bad);
+  else k_check_f32<<<512, 256, 0, b.stream>>>((const float*)b.recv, count, want, b.bad);
+  HIPCHECK(hipGetLastError());
+  return 0;
+}
+
+static inline size_t elem_size(int dtype) { return dtype == 1 ? 2 : 4; }
+static inline ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclBfloat16 : ncclFloat32; }
+
+// Multi-process: one rank.  Results per size in out arrays (length nsizes):
+// time_us (mean per all-reduce), algbw GB/s, busbw GB/s, errors (mismatches).
+extern "C" int tkr_sweep_rank(int rank, int world, const unsigned char* uid128, int device, const size_t* sizes,
+                              int nsizes, int iters, int warmup, int dtype, double* time_us, double* algbw,
+                              double* busbw, double* errors) {
+  HIPCHECK(hipSetDevice(device));
+  ncclUniqueId id;
+  memcpy(id.internal, uid128, NCCL_UNIQUE_ID_BYTES);
+  ncclComm_t comm;
+  NCCLCHECK(ncclCommInitRank(&comm, world, id, rank));
+  size_t max_bytes = 0;
+  for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
+  RankBufs b;
+  int rc = alloc_bufs(b, max_bytes);
+  const float want = (float)world * (float)(world + 1) / 2.0f;
+  for (int s = 0; rc == 0 && s < nsizes; ++s) {
+    const size_t count = sizes[s] / elem_size(dtype);
+    if ((rc = fill(b, count, dtype, (float)(rank + 1))) != 0) break;
+    for (int w = 0; w < warmup; ++w) {
+      ncclResult_t r = ncclAllReduce(b.send, b.recv, count, nccl_type(dtype), ncclSum, comm, b.stream);
+      if (r != ncclSuccess) { snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", ncclGetErrorString(r)); rc = -2; }
+    }
+    if (rc) break;
+    (void)hipEventRecord(b.t0, b.stream);
+    for (int it = 0; it < iters; ++it) {
+      ncclResult_t r = ncclAllReduce(b.send, b.recv, count, nccl_type(dtype), ncclSum, comm, b.stream);
+      if (r != ncclSuccess) { snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", ncclGetErrorString(r)); rc = -2; break; }
+    }
+    if (rc) break;
+    (void)hipEventRecord(b.t1, b.stream);
+    if ((rc = check(b, count, dtype, want)) != 0) break;
+    if (hipStreamSynchronize(b.stream) != hipSuccess) { snprintf(g_err, sizeof(g_err), "stream sync failed"); rc = -1; break; }
+    float ms = 0.f;
+    (void)hipEventElapsedTime(&ms, b.t0, b.t1);
+    unsigned long long bad = 0;
+    (void)hipMemcpy(&bad, b.bad, sizeof(bad), hipMemcpyDeviceToHost);
+    const double t = (double)ms * 1e-3 / (iters > 0 ? iters : 1);
+    time_us[s] = t * 1e6;
+    algbw[s] = (double)sizes[s] / t / 1e9;
+    busbw[s] = algbw[s] * (world > 1 ? 2.0 * (world - 1) / world : 1.0);
+    errors[s] = (double)bad;
+  }
+  free_bufs(b);
+  ncclCommDestroy(comm);
+  return rc;
+}
+
+// Single process, all `ndev` local GPUs (ncclCommInitAll).  Same outputs; the
+// error count is summed over devices, the time is the slowest device's.
+extern "C" int tkr_sweep_local(int ndev, const size_t* sizes, int nsizes, int iters, int warmup, int dtype,
+                               double* time_us, double* algbw, double* busbw, double* errors) {
+  if (ndev < 1) { snprintf(g_err, sizeof(g_err), "ndev must be >= 1"); return -1; }
+  std::vector<int> devs(ndev);
+  for (int d = 0; d < ndev; ++d) devs[d] = d;
+  std::vector<ncclComm_t> comms(ndev);
+  NCCLCHECK(ncclCommInitAll(comms.data(), ndev, devs.data()));
+  size_t max_bytes = 0;
+  for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
+  std::vector<RankBufs> bufs(ndev);
+  int rc = 0;
+  for (int d = 0; d < ndev && rc == 0; ++d) {
+    if (hipSetDevice(d) != hipSuccess) { rc = -1; break; }
+    rc = alloc_bufs(bufs[d], max_bytes);
+  }
+  const float want = (float)ndev * (float)(ndev + 1) / 2.0f;
+  for (int s = 0; rc == 0 && s < nsizes; ++s) {
+    const size_t count = sizes[s] / elem_size(dtype);
+    for (int d = 0; d < ndev && rc == 0; ++d) {
+      (void)hipSetDevice(d);
+      rc = fill(bufs[d], count, dtype, (float)(d + 1));
+    }
+    if (rc) break;
+    auto run = [&](int n) -> int {
+      for (int it = 0; it < n; ++it) {
+        NCCLCHECK(ncclGroupStart());
+        for (int d = 0; d < ndev; ++d)
+          NCCLCHECK(ncclAllReduce(bufs[d].send, bufs[d].recv, count, nccl_type(dtype), ncclSum, comms[d],
+                                  bufs[d].stream));
+        NCCLCHECK(ncclGroupEnd());
+      }
+      return 0;
+    };
+    if ((rc = run(warmup)) != 0) break;
+    for (int d = 0; d < ndev; ++d) { (void)hipSetDevice(d); (void)hipEventRecord(bufs[d].t0, bufs[d].stream); }
+    if ((rc = run(iters)) != 0) break;
+    double worst = 0.0;
+    unsigned long long bad_total = 0;
+    for (int d = 0; d < ndev && rc == 0; ++d) {
+      (void)hipSetDevice(d);
+      (void)hipEventRecord(bufs[d].t1, bufs[d].stream);
+      rc = check(bufs[d], count, dtype, want);
+    }
+    for (int d = 0; d < ndev && rc == 0; ++d) {
+      (void)hipSetDevice(d);
+      if (hipStreamSynchronize(bufs[d].stream) != hipSuccess) { rc = -1; break; }
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, bufs[d].t0, bufs[d].t1);
+      if (ms > worst) worst = ms;
+      unsigned long long bad = 0;
+      (void)hipMemcpy(&bad, bufs[d].bad, sizeof(bad), hipMemcpyDeviceToHost);
+      bad_total += bad;
+    }
+    if (rc) break;
+    const double t = worst * 1e-3 / (iters > 0 ? iters : 1);
+    time_us[s] = t * 1e6;
+    algbw[s] = (double)sizes[s] / t / 1e9;
+    busbw[s] = algbw[s] * (ndev > 1 ? 2.0 * (ndev - 1) / ndev : 1.0);
+    errors[s] = (double)bad_total;
+  }
+  for (int d = 0; d < ndev; ++d) {
+    (void)hipSetDevice(d);
+    free_bufs(bufs[d]);
+    ncclCommDestroy(comms[d]);
+  }
+  return rc;
+}
+
+#ifdef TK_RCCL_MAIN
+int main(int argc, char** argv) {
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
+    fprintf(stderr, "{\"error\":\"no HIP devices\"}\n");
+    return 3;
+  }
+  double min_busbw = 0.0;
+  int iters = 20, warmup = 5, dtype = 0;
+  for (int i = 1; i < argc; ++i) {
+    if (!strcmp(argv[i], "--min-busbw") && i + 1 < argc) min_busbw = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--iters") && i + 1 < argc) iters = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--ngpus") && i + 1 < argc) ndev = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--bf16")) dtype = 1;
+  }
+  std::vector<size_t> sizes;
+  for (size_t b = 1u << 20; b <= (1ull << 30); b <<= 2) sizes.push_back(b);
+  const int n = (int)sizes.size();
+  std::vector<double> t(n), alg(n), bus(n), err(n);
+  int rc = tkr_sweep_local(ndev, sizes.data(), n, iters, warmup, dtype, t.data(), alg.data(), bus.data(), err.data());
+  if (rc) {
+    fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
+    return 2;
+  }
+  double errs = 0;
+  printf("{\"ngpus\":%d,\"dtype\":\"%s\",\"results\":[", ndev, dtype ? "bf16" : "f32");
+  for (int i = 0; i < n; ++i) {
+    errs += err[i];
+    printf("%s{\"bytes\":%zu,\"time_us\":%.2f,\"algbw_gbps\":%.2f,\"busbw_gbps\":%.2f,\"errors\":%.0f}", i ? "," : "",
+           sizes[i], t[i], alg[i], bus[i], err[i]);
+  }
+  const bool ok = errs == 0 && bus[n - 1] >= min_busbw;
+  printf("],\"ok\":%s}\n", ok ? "true" : "false");
+  return ok ? 0 : 1;
+}
+#endif

@@ -1,0 +1,196 @@
+"""Python front-end of the MI355X burn-in probes (``csrc/tk_gpu_probe.hip``).
+
+``run_burnin(device, level)`` is what the MI355X host bootstrap executes per
+GPU before the node may advertise ``amd.com/gpu``.  Thresholds are fractions of
+MI355X figures (MI355X_MICROARCH.md): HBM3E ~6.3 TB/s achievable of 8 TB/s
+spec, dense bf16 MFMA ~2.5 PFLOP/s, block-scaled fp8 ~5 PFLOP/s.  A GPU that
+fails a threshold or the memtest marks the node not-ready.
+"""
+
+import ctypes
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Optional
+
+from .native import load
+
+# MI355X reference figures (dense; never the 2:1-sparsity marketing numbers)
+MI355X_HBM_ACHIEVABLE_GBPS = 6300.0
+MI355X_BF16_DENSE_TFLOPS = 2500.0
+MI355X_FP8_DENSE_TFLOPS = 5000.0
+MI355X_F32_MFMA_TFLOPS = 157.3
+MI355X_CUS = 256
+
+DTYPES = {"bf16": 0, "fp8": 1, "f32": 2}
+
+
+class _DeviceInfo(ctypes.Structure):
+    _fields_ = [
+        ("name", ctypes.c_char * 128),
+        ("arch", ctypes.c_char * 64),
+        ("compute_units", ctypes.c_int),
+        ("wavefront_size", ctypes.c_int),
+        ("clock_khz", ctypes.c_int),
+        ("mem_clock_khz", ctypes.c_int),
+        ("mem_bus_width", ctypes.c_int),
+        ("l2_bytes", ctypes.c_int),
+        ("lds_per_block", ctypes.c_int),
+        ("pci_domain", ctypes.c_int),
+        ("pci_bus", ctypes.c_int),
+        ("pci_device", ctypes.c_int),
+        ("total_mem", ctypes.c_longlong),
+        ("free_mem", ctypes.c_longlong),
+    ]
+
+
+class ProbeError(RuntimeError):
+    pass
+
+
+def _lib():
+    lib = load("libtk_gpu_probe.so")
+    lib.tkp_last_error.restype = ctypes.c_char_p
+    lib.tkp_hbm_bandwidth.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_mfma_peak.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                  ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_memtest_selfcheck.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_p2p_bandwidth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double)]
+    return lib
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise ProbeError(f"{what}: {_lib().tkp_last_error().decode(errors='replace')}")
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(_lib().tkp_device_count(ctypes.byref(n)), "device_count")
+    return n.value
+
+
+@dataclass
+class DeviceInfo:
+    index: int
+    name: str
+    arch: str
+    compute_units: int
+    wavefront_size: int
+    clock_mhz: float
+    total_mem_gib: float
+    free_mem_gib: float
+    l2_bytes: int
+    pci_bus_id: str
+
+    @property
+    def is_gfx950(self) -> bool:
+        return self.arch.split(":")[0] == "gfx950"
+
+
+def device_info(dev: int) -> DeviceInfo:
+    info = _DeviceInfo()
+    _check(_lib().tkp_device_info(dev, ctypes.byref(info)), "device_info")
+    return DeviceInfo(
+        index=dev, name=info.name.decode(errors="replace"), arch=info.arch.decode(errors="replace"),
+        compute_units=info.compute_units, wavefront_size=info.wavefront_size, clock_mhz=info.clock_khz / 1000.0,
+        total_mem_gib=info.total_mem / 2 ** 30, free_mem_gib=info.free_mem / 2 ** 30, l2_bytes=info.l2_bytes,
+        pci_bus_id=f"{info.pci_domain:04x}:{info.pci_bus:02x}:{info.pci_device:02x}.0")
+
+
+def hbm_bandwidth(dev: int, nbytes: int = 1 << 30, iters: int = 5, blocks_per_cu: int = 16) -> Dict[str, float]:
+    out = (ctypes.c_double * 3)()
+    _check(_lib().tkp_hbm_bandwidth(dev, nbytes, iters, blocks_per_cu, out), "hbm_bandwidth")
+    return {"read_gbps": out[0], "write_gbps": out[1], "copy_gbps": out[2]}
+
+
+def mfma_peak(dev: int, dtype: str = "bf16", iters: int = 20000, reps: int = 3,
+              blocks_per_cu: int = 2) -> Dict[str, float]:
+    out = (ctypes.c_double * 2)()
+    _check(_lib().tkp_mfma_peak(dev, DTYPES[dtype], iters, reps, blocks_per_cu, out), f"mfma_peak[{dtype}]")
+    return {"tflops": out[0], "ms": out[1]}
+
+
+def memtest(dev: int, nbytes: int = 1 << 30, passes: int = 2) -> Dict[str, float]:
+    out = (ctypes.c_double * 2)()
+    _check(_lib().tkp_memtest(dev, nbytes, passes, out), "memtest")
+    return {"errors": int(out[0]), "verify_gbps": out[1]}
+
+
+def memtest_selfcheck(dev: int, nbytes: int, corrupt: int) -> int:
+    out = (ctypes.c_double * 1)()
+    _check(_lib().tkp_memtest_selfcheck(dev, nbytes, corrupt, out), "memtest_selfcheck")
+    return int(out[0])
+
+
+def p2p_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 5) -> Dict[str, float]:
+    out = (ctypes.c_double * 2)()
+    _check(_lib().tkp_p2p_bandwidth(src, dst, nbytes, iters, out), "p2p_bandwidth")
+    return {"gbps": out[0], "peer_access": bool(out[1])}
+
+
+# --- burn-in policy ------------------------------------------------------------------
+LEVELS = {
+    # level: (hbm bytes, hbm iters, mfma iters, memtest bytes, memtest passes)
+    "quick": (1 << 30, 3, 4000, 1 << 30, 1),
+    "full": (16 << 30, 10, 40000, 64 << 30, 3),
+}
+
+
+@dataclass
+class Thresholds:
+    min_read_frac: float = 0.60
+    min_bf16_frac: float = 0.55
+    min_fp8_frac: float = 0.55
+    require_gfx950: bool = True
+    min_cus: int = MI355X_CUS
+
+
+@dataclass
+class BurninResult:
+    device: DeviceInfo
+    level: str
+    hbm: Dict[str, float] = field(default_factory=dict)
+    mfma: Dict[str, Dict[str, float]] = field(default_factory=dict)
+    memtest: Dict[str, float] = field(default_factory=dict)
+    failures: List[str] = field(default_factory=list)
+
+    @property
+    def ok(self) -> bool:
+        return not self.failures
+
+    def to_json(self) -> Dict:
+        d = asdict(self)
+        d["ok"] = self.ok
+        return d
+
+
+def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] = None) -> BurninResult:
+    th = thresholds or Thresholds()
+    info = device_info(dev)
+    res = BurninResult(info, level)
+    if level == "off":
+        return res
+    hbm_bytes, hbm_iters, mfma_iters, mt_bytes, mt_passes = LEVELS[level]
+    if th.require_gfx950 and not info.is_gfx950:
+        res.failures.append(f"arch {info.arch} is not gfx950")
+    if info.compute_units < th.min_cus:
+        res.failures.append(f"{info.compute_units} CUs < {th.min_cus}")
+    res.hbm = hbm_bandwidth(dev, hbm_bytes, hbm_iters)
+    if res.hbm["read_gbps"] < th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS:
+        res.failures.append(f"HBM read {res.hbm['read_gbps']:.0f} GB/s below "
+                            f"{th.min_read_frac:.0%} of {MI355X_HBM_ACHIEVABLE_GBPS:.0f}")
+    res.mfma["bf16"] = mfma_peak(dev, "bf16", mfma_iters)
+    res.mfma["fp8"] = mfma_peak(dev, "fp8", mfma_iters // 2)
+    if res.mfma["bf16"]["tflops"] < th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS:
+        res.failures.append(f"bf16 MFMA {res.mfma['bf16']['tflops']:.0f} TF below "
+                            f"{th.min_bf16_frac:.0%} of dense peak")
+    if res.mfma["fp8"]["tflops"] < th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS:
+        res.failures.append(f"fp8 MFMA {res.mfma['fp8']['tflops']:.0f} TF below "
+                            f"{th.min_fp8_frac:.0%} of dense peak")
+    res.memtest = memtest(dev, mt_bytes, mt_passes)
+    if res.memtest["errors"]:
+        res.failures.append(f"memtest: {res.memtest['errors']} mismatching words")
+    return res

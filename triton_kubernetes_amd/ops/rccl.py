@@ -1,0 +1,103 @@
+"""Python front-end of the RCCL readiness probe (N2, ``csrc/tk_rccl_probe.hip``)."""
+
+import ctypes
+from dataclasses import asdict, dataclass, field
+from typing import Dict, List, Sequence
+
+from .native import load
+
+UID_BYTES = 128
+DEFAULT_SIZES = [1 << 20, 16 << 20, 256 << 20]
+# MI355X: 7 xGMI links x ~153 GB/s per GPU; ring all-reduce is per-link bound.
+XGMI_LINK_GBPS = 153.0
+XGMI_LINKS_PER_GPU = 7
+
+
+class RCCLError(RuntimeError):
+    pass
+
+
+def _lib():
+    lib = load("libtk_rccl.so")
+    lib.tkr_last_error.restype = ctypes.c_char_p
+    lib.tkr_unique_id.argtypes = [ctypes.c_char_p]
+    dp = ctypes.POINTER(ctypes.c_double)
+    lib.tkr_sweep_rank.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, dp, dp, dp, dp]
+    lib.tkr_sweep_local.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_int, ctypes.c_int, dp, dp, dp, dp]
+    return lib
+
+
+def version() -> int:
+    return int(_lib().tkr_version())
+
+
+def unique_id() -> bytes:
+    buf = ctypes.create_string_buffer(UID_BYTES)
+    rc = _lib().tkr_unique_id(buf)
+    if rc != 0:
+        raise RCCLError(_lib().tkr_last_error().decode())
+    return buf.raw[:UID_BYTES]
+
+
+@dataclass
+class SweepResult:
+    world: int
+    dtype: str
+    sizes: List[int]
+    time_us: List[float] = field(default_factory=list)
+    algbw_gbps: List[float] = field(default_factory=list)
+    busbw_gbps: List[float] = field(default_factory=list)
+    errors: List[int] = field(default_factory=list)
+
+    @property
+    def ok(self) -> bool:
+        return all(e == 0 for e in self.errors)
+
+    @property
+    def peak_busbw(self) -> float:
+        return max(self.busbw_gbps) if self.busbw_gbps else 0.0
+
+    def to_json(self) -> Dict:
+        d = asdict(self)
+        d["ok"] = self.ok
+        d["peak_busbw_gbps"] = self.peak_busbw
+        return d
+
+
+def _arrays(n: int):
+    return [(ctypes.c_double * n)() for _ in range(4)]
+
+
+def sweep_rank(rank: int, world: int, uid: bytes, device: int, sizes: Sequence[int] = DEFAULT_SIZES,
+               iters: int = 10, warmup: int = 3, dtype: str = "f32") -> SweepResult:
+    n = len(sizes)
+    sz = (ctypes.c_size_t * n)(*sizes)
+    t, alg, bus, err = _arrays(n)
+    rc = _lib().tkr_sweep_rank(rank, world, uid, device, sz, n, iters, warmup, 1 if dtype == "bf16" else 0,
+                               t, alg, bus, err)
+    if rc != 0:
+        raise RCCLError(f"rank {rank}/{world}: {_lib().tkr_last_error().decode()}")
+    return SweepResult(world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err])
+
+
+def sweep_local(ndev: int, sizes: Sequence[int] = DEFAULT_SIZES, iters: int = 10, warmup: int = 3,
+                dtype: str = "f32") -> SweepResult:
+    n = len(sizes)
+    sz = (ctypes.c_size_t * n)(*sizes)
+    t, alg, bus, err = _arrays(n)
+    rc = _lib().tkr_sweep_local(ndev, sz, n, iters, warmup, 1 if dtype == "bf16" else 0, t, alg, bus, err)
+    if rc != 0:
+        raise RCCLError(_lib().tkr_last_error().decode())
+    return SweepResult(ndev, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err])
+
+
+def min_busbw_threshold(world: int, fraction: float = 0.5) -> float:
+    """Gate for an intra-node sweep: a fraction of the per-GPU xGMI capacity
+    a ring can use (ring all-reduce drives 2 links per GPU at a time; RCCL's
+    multi-ring schedules can use more)."""
+    if world <= 1:
+        return 0.0
+    return fraction * 2 * XGMI_LINK_GBPS

@@ -1,0 +1,132 @@
+"""Node GPU topology (N1): amd_smi via ``libtk_topo.so``, with a KFD-sysfs fallback.
+
+``discover()`` returns the JSON document of ``csrc/tk_topo.cpp``.  When the
+amd_smi path cannot run (no driver, old ROCm), the same document shape is
+derived from the KFD topology in ``/sys/class/kfd/kfd/topology/nodes`` — also
+the path the unit tests exercise with a fixture tree.
+"""
+
+import ctypes
+import glob
+import json
+import os
+import subprocess
+from typing import Any, Dict, List, Optional
+
+from .native import NativeUnavailable, executable, load
+
+KFD_TOPOLOGY = "/sys/class/kfd/kfd/topology/nodes"
+# io_link type values in KFD (kfd_topology.h): 11 = XGMI, 2 = PCIe
+_KFD_LINK_TYPES = {11: "XGMI", 2: "PCIE"}
+GFX_TARGETS = {90500: "gfx950", 90400: "gfx942", 90402: "gfx942", 90010: "gfx90a"}
+
+
+def amdsmi_topology(timeout: float = 60.0) -> Dict[str, Any]:
+    """Run the ``amdgpu-topo-labeller`` executable (amd_smi in its own process).
+
+    Kept out of process on purpose: amd_smi's library state and teardown then
+    never share an address space with the HIP runtime / RCCL of the caller.
+    """
+    exe = executable("amdgpu-topo-labeller")
+    proc = subprocess.run([exe], capture_output=True, text=True, timeout=timeout, check=False)
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
+    if not lines:
+        raise NativeUnavailable(f"amdgpu-topo-labeller produced no JSON (rc={proc.returncode}): {proc.stderr[-500:]}")
+    doc = json.loads(lines[-1])
+    doc["status"] = proc.returncode
+    return doc
+
+
+def amdsmi_topology_inprocess() -> Dict[str, Any]:
+    lib = load("libtk_topo.so")
+    lib.tkt_topology_json.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    size = 1 << 16
+    while True:
+        buf = ctypes.create_string_buffer(size)
+        rc = lib.tkt_topology_json(buf, size)
+        if rc < 0:
+            size = -rc + 1
+            continue
+        doc = json.loads(buf.value.decode())
+        doc["status"] = rc
+        return doc
+
+
+def _read_props(path: str) -> Dict[str, int]:
+    props: Dict[str, int] = {}
+    try:
+        with open(path, "r", encoding="utf-8") as fh:
+            for line in fh:
+                parts = line.split()
+                if len(parts) == 2:
+                    try:
+                        props[parts[0]] = int(parts[1])
+                    except ValueError:
+                        pass
+    except OSError:
+        pass
+    return props
+
+
+def kfd_topology(root: str = KFD_TOPOLOGY) -> Dict[str, Any]:
+    """GPU nodes (``simd_count > 0``) and their io_links from KFD sysfs."""
+    nodes = []
+    for node_dir in sorted(glob.glob(os.path.join(root, "*")), key=lambda p: int(os.path.basename(p))
+                           if os.path.basename(p).isdigit() else 1 << 30):
+        props = _read_props(os.path.join(node_dir, "properties"))
+        if props.get("simd_count", 0) <= 0:
+            continue
+        name = ""
+        try:
+            with open(os.path.join(node_dir, "name"), "r", encoding="utf-8") as fh:
+                name = fh.read().strip()
+        except OSError:
+            pass
+        links = []
+        for link in sorted(glob.glob(os.path.join(node_dir, "io_links", "*"))):
+            lp = _read_props(os.path.join(link, "properties"))
+            links.append({"kfd_to": lp.get("node_to", -1), "type": _KFD_LINK_TYPES.get(lp.get("type", -1), "OTHER"),
+                          "weight": lp.get("weight", 0)})
+        nodes.append({"kfd_node": int(os.path.basename(node_dir)), "name": name, "props": props, "links": links})
+    kfd_to_index = {n["kfd_node"]: i for i, n in enumerate(nodes)}
+    gpus: List[Dict[str, Any]] = []
+    for i, n in enumerate(nodes):
+        p = n["props"]
+        simd_per_cu = p.get("simd_per_cu", 4) or 4
+        gfx = GFX_TARGETS.get(p.get("gfx_target_version", 0), "")
+        gpu: Dict[str, Any] = {
+            "index": i,
+            "kfd_node": n["kfd_node"],
+            "market_name": n["name"],
+            "device_id": hex(p.get("device_id", 0)),
+            "compute_units": p.get("simd_count", 0) // simd_per_cu,
+            "numa_node": max(0, p.get("numa_node", 0) if "numa_node" in p else 0),
+            "xgmi_hive_id": hex(p.get("hive_id", 0)) if p.get("hive_id") else "0x0",
+            "links": [],
+        }
+        if gfx:
+            gpu["target_graphics_version"] = gfx
+        if "domain" in p or "location_id" in p:
+            loc = p.get("location_id", 0)
+            gpu["bdf"] = f"{p.get('domain', 0):04x}:{(loc >> 8) & 0xff:02x}:{(loc >> 3) & 0x1f:02x}.{loc & 7:x}"
+        for lk in n["links"]:
+            if lk["kfd_to"] in kfd_to_index:
+                gpu["links"].append({"peer": kfd_to_index[lk["kfd_to"]], "type": lk["type"],
+                                     "hops": 1, "p2p": lk["type"] == "XGMI"})
+        gpus.append(gpu)
+    return {"source": "kfd", "gpus": gpus}
+
+
+def discover(kfd_root: Optional[str] = None, prefer_amdsmi: bool = True) -> Dict[str, Any]:
+    """Best-effort topology: amd_smi first, KFD sysfs second, empty last."""
+    if prefer_amdsmi and kfd_root is None:
+        try:
+            doc = amdsmi_topology()
+            if doc.get("status") == 0 and doc.get("gpus"):
+                return doc
+        except (NativeUnavailable, OSError, ValueError, subprocess.SubprocessError):
+            pass
+    root = kfd_root or KFD_TOPOLOGY
+    if os.path.isdir(root):
+        return kfd_topology(root)
+    return {"source": "none", "gpus": []}

@@ -1,0 +1,213 @@
+"""Rancher v3 REST client.
+
+In-process replacements for the reference's shell + curl + jq scripts:
+
+* :meth:`RancherClient.bootstrap` — ``setup_rancher.sh.tpl`` (S3): wait for the
+  server, log in as admin/admin, create the non-expiring ``triton-kubernetes``
+  API token, change the admin password, set ``server-url``;
+* :meth:`RancherClient.ensure_cluster` — ``rancher_cluster.sh`` (S4): find or
+  create the RKE cluster by name, get or create its registration token, and the
+  CA checksum (sha256 of ``cacerts`` + newline, exactly what the script hashes);
+* new: cluster / node status, Kubernetes API through Rancher's ``/k8s/clusters``
+  proxy (used by the readiness waiter and the MI355X add-on step), cleanup.
+
+Waits poll adaptively (20 ms doubling to ``max_interval``) instead of the
+reference's fixed ``sleep 5``.
+"""
+
+import base64
+import hashlib
+import time
+from dataclasses import dataclass
+from typing import Any, Callable, Dict, List, Optional
+
+from ..cloud.http import HTTPClient, HTTPError
+from ..errors import TKError
+
+TOKEN_NAME = "triton-kubernetes"
+
+
+@dataclass
+class ClusterInfo:
+    cluster_id: str
+    registration_token: str
+    ca_checksum: str
+    existed: bool = False
+
+    def outputs(self) -> Dict[str, str]:
+        return {"rancher_cluster_id": self.cluster_id,
+                "rancher_cluster_registration_token": self.registration_token,
+                "rancher_cluster_ca_checksum": self.ca_checksum}
+
+
+def ca_checksum(cacerts: str) -> str:
+    return hashlib.sha256((cacerts + "\n").encode()).hexdigest()
+
+
+def wait_until(fn: Callable[[], Any], timeout: float, what: str, first: float = 0.02,
+               max_interval: float = 1.0) -> Any:
+    """Call ``fn`` until it returns a truthy value (adaptive backoff)."""
+    deadline = time.monotonic() + timeout
+    delay = first
+    last_exc: Optional[BaseException] = None
+    while True:
+        try:
+            value = fn()
+            if value:
+                return value
+        except (TKError, OSError) as exc:
+            last_exc = exc
+        if time.monotonic() >= deadline:
+            detail = f": {last_exc}" if last_exc else ""
+            raise TKError(f"timed out after {timeout:.0f}s waiting for {what}{detail}")
+        time.sleep(delay)
+        delay = min(max_interval, delay * 2)
+
+
+class RancherClient:
+    def __init__(self, url: str, access_key: str = "", secret_key: str = "", verify_tls: bool = False,
+                 timeout: float = 30.0):
+        self.url = url.rstrip("/")
+        self.access_key = access_key
+        self.secret_key = secret_key
+        self.http = HTTPClient(base_url=self.url, verify_tls=verify_tls, timeout=timeout)
+        self._apply_auth()
+
+    def _apply_auth(self) -> None:
+        if self.access_key or self.secret_key:
+            cred = base64.b64encode(f"{self.access_key}:{self.secret_key}".encode()).decode()
+            self.http.default_headers["Authorization"] = f"Basic {cred}"
+        else:
+            self.http.default_headers.pop("Authorization", None)
+
+    # --- server bootstrap (S3) -------------------------------------------------------
+    def ping(self) -> bool:
+        try:
+            self.http.request("GET", "/ping", ok=(200,))
+            return True
+        except TKError:
+            return False
+
+    def wait_for_server(self, timeout: float = 600.0) -> None:
+        wait_until(self.ping, timeout, f"Rancher at {self.url}")
+
+    def login(self, username: str, password: str) -> str:
+        data = self.http.post_json("/v3-public/localProviders/local?action=login",
+                                   {"username": username, "password": password, "ttl": 60000,
+                                    "description": "Initial Token"})
+        token = data.get("token", "")
+        if not token:
+            raise TKError("Rancher login returned no token")
+        return token
+
+    def bootstrap(self, admin_password: str, server_url: str, initial_password: str = "admin",
+                  timeout: float = 600.0) -> Dict[str, str]:
+        """Run S3 from the operator side; returns the manager module outputs."""
+        self.wait_for_server(timeout)
+        initial = self.login("admin", initial_password)
+        user, _, secret = initial.partition(":")
+        self.access_key, self.secret_key = user, secret
+        self._apply_auth()
+        tok = self.http.post_json("/v3/token", {"type": "token", "description": "Managed by triton-kubernetes",
+                                                "name": TOKEN_NAME, "ttl": 0, "expired": False,
+                                                "isDerived": False})
+        name = tok.get("name", "")
+        secret_key = tok.get("token", "").split(":", 1)[-1]
+        self.access_key, self.secret_key = name, secret_key
+        self._apply_auth()
+        if admin_password and admin_password != initial_password:
+            self.http.post_json("/v3/users?action=changepassword",
+                                {"currentPassword": initial_password, "newPassword": admin_password})
+        self.http.put_json("/v3/settings/server-url", {"baseType": "setting", "id": "server-url",
+                                                       "name": "server-url", "type": "setting",
+                                                       "value": server_url})
+        return {"rancher_url": server_url, "rancher_access_key": name, "rancher_secret_key": secret_key}
+
+    # --- clusters (S4) -------------------------------------------------------------------
+    def find_cluster(self, name: str) -> Optional[Dict[str, Any]]:
+        data = self.http.get_json("/v3/clusters", params={"name": name}).get("data", [])
+        return data[0] if data else None
+
+    def create_cluster(self, name: str, k8s_version: str, network_provider: str, k8s_registry: str = "",
+                       k8s_registry_username: str = "", k8s_registry_password: str = "") -> Dict[str, Any]:
+        rke: Dict[str, Any] = {
+            "ignoreDockerVersion": False,
+            "sshAgentAuth": False,
+            "type": "rancherKubernetesEngineConfig",
+            "kubernetesVersion": k8s_version,
+            "authentication": {"type": "authnConfig", "strategy": "x509"},
+            "network": {"type": "networkConfig", "plugin": network_provider},
+            "services": {"type": "rkeConfigServices", "kubeApi": {"podSecurityPolicy": False,
+                                                                 "type": "kubeAPIService"}},
+        }
+        if k8s_registry:
+            rke["privateRegistries"] = [{"url": k8s_registry, "user": k8s_registry_username,
+                                         "password": k8s_registry_password}]
+        body = {"type": "cluster", "googleKubernetesEngineConfig": None, "name": name,
+                "rancherKubernetesEngineConfig": rke, "id": ""}
+        return self.http.post_json("/v3/cluster", body)
+
+    def registration_token(self, cluster_id: str, create: bool) -> str:
+        if not create:
+            data = self.http.get_json(f"/v3/clusters/{cluster_id}/clusterregistrationtokens").get("data", [])
+            if data and data[0].get("token"):
+                return data[0]["token"]
+        resp = self.http.post_json("/v3/clusterregistrationtoken",
+                                   {"clusterId": cluster_id, "type": "clusterRegistrationToken"})
+        return resp.get("token", "")
+
+    def cacerts(self) -> str:
+        return self.http.get_json("/v3/settings/cacerts").get("value", "") or ""
+
+    def ensure_cluster(self, name: str, k8s_version: str = "v1.9.5-rancher1-1", network_provider: str = "flannel",
+                       k8s_registry: str = "", k8s_registry_username: str = "",
+                       k8s_registry_password: str = "") -> ClusterInfo:
+        existing = self.find_cluster(name)
+        if existing is not None:
+            cluster_id, existed = existing.get("id", ""), True
+        else:
+            cluster_id = self.create_cluster(name, k8s_version, network_provider, k8s_registry,
+                                             k8s_registry_username, k8s_registry_password).get("id", "")
+            existed = False
+        if not cluster_id:
+            raise TKError("Unable to create cluster!")
+        token = self.registration_token(cluster_id, create=not existed)
+        if not token:
+            raise TKError("Unable to create cluster registration token!")
+        return ClusterInfo(cluster_id, token, ca_checksum(self.cacerts()), existed)
+
+    # --- status -------------------------------------------------------------------------------
+    def cluster(self, cluster_id: str) -> Dict[str, Any]:
+        return self.http.get_json(f"/v3/clusters/{cluster_id}")
+
+    def cluster_state(self, cluster_id: str) -> str:
+        return str(self.cluster(cluster_id).get("state", ""))
+
+    def nodes(self, cluster_id: str) -> List[Dict[str, Any]]:
+        return self.http.get_json("/v3/nodes", params={"clusterId": cluster_id}).get("data", [])
+
+    def delete_cluster(self, cluster_id: str) -> None:
+        try:
+            self.http.request("DELETE", f"/v3/clusters/{cluster_id}")
+        except HTTPError as exc:
+            if exc.status != 404:
+                raise
+
+    def delete_node(self, node_id: str) -> None:
+        try:
+            self.http.request("DELETE", f"/v3/nodes/{node_id}")
+        except HTTPError as exc:
+            if exc.status != 404:
+                raise
+
+    # --- Kubernetes API via the Rancher proxy ------------------------------------------------
+    def k8s(self, cluster_id: str, method: str, path: str, body: Any = None, ok=(200, 201, 202, 204)) -> Any:
+        resp = self.http.request(method, f"/k8s/clusters/{cluster_id}/{path.lstrip('/')}", json_body=body, ok=ok)
+        return resp.json() if resp.body else None
+
+    def k8s_nodes(self, cluster_id: str) -> List[Dict[str, Any]]:
+        return (self.k8s(cluster_id, "GET", "/api/v1/nodes") or {}).get("items", [])
+
+    def kubeconfig(self, cluster_id: str) -> str:
+        data = self.http.post_json(f"/v3/clusters/{cluster_id}?action=generateKubeconfig", {})
+        return data.get("config", "")

@@ -1,0 +1,362 @@
+"""In-process fake Rancher 2.x server (the Rancher API fake SURVEY.md §4 calls for).
+
+Implements the v3 endpoints the framework uses plus a simulation of what the
+real server does after agents register:
+
+* S3 bootstrap endpoints (login, token, change password, settings);
+* S4 cluster endpoints (find/create cluster, registration tokens, cacerts);
+* ``POST /v3/connect/register`` — agent registration (``X-API-Tunnel-Token`` +
+  base64 JSON ``X-API-Tunnel-Params`` with hostname, roles, labels, capacity),
+  standing in for the rancher-agent websocket tunnel;
+* RKE simulation: a cluster turns ``active`` ``rke_seconds`` after it has at
+  least one etcd, one controlplane and one worker node; nodes then report the
+  Kubernetes ``Ready`` condition;
+* ``/k8s/clusters/<id>/...`` proxy: ``api/v1/nodes`` (labels, conditions,
+  allocatable) and a generic object store for applied manifests.  GPU nodes
+  advertise ``amd.com/gpu`` allocatable only once a DaemonSet whose name
+  contains ``device-plugin`` has been applied — as with the real ROCm plugin.
+
+Everything is in memory and thread-safe; it serves plain HTTP on 127.0.0.1.
+"""
+
+import base64
+import http.server
+import json
+import threading
+import time
+import urllib.parse
+import uuid
+from typing import Any, Dict, List, Optional, Tuple
+
+FAKE_CACERTS = "-----BEGIN CERTIFICATE-----\nMIIFAKECERTIFICATEFORTESTS\n-----END CERTIFICATE-----"
+
+
+class _State:
+    def __init__(self, rke_seconds: float, node_ready_seconds: float, admin_password: str):
+        self.mu = threading.RLock()
+        self.cond = threading.Condition(self.mu)
+        self.admin_password = admin_password
+        self.tokens: Dict[str, str] = {}  # name -> secret
+        self.settings: Dict[str, str] = {"cacerts": FAKE_CACERTS, "server-url": ""}
+        self.clusters: Dict[str, Dict[str, Any]] = {}
+        self.reg_tokens: Dict[str, Dict[str, Any]] = {}  # token -> {clusterId, id}
+        self.nodes: Dict[str, Dict[str, Any]] = {}
+        self.objects: Dict[str, Dict[str, Any]] = {}  # "<cluster>|<path>|<name>" -> object
+        self.rke_seconds = rke_seconds
+        self.node_ready_seconds = node_ready_seconds
+        self.requests = 0
+        self.log: List[Tuple[str, str]] = []
+
+
+class FakeRancher:
+    def __init__(self, rke_seconds: float = 0.0, node_ready_seconds: float = 0.0, admin_password: str = "admin",
+                 host: str = "127.0.0.1", port: int = 0):
+        self.state = _State(rke_seconds, node_ready_seconds, admin_password)
+        self._server = http.server.ThreadingHTTPServer((host, port), self._handler())
+        self._server.daemon_threads = True
+        self._thread: Optional[threading.Thread] = None
+
+    @property
+    def url(self) -> str:
+        host, port = self._server.server_address[:2]
+        return f"http://{host}:{port}"
+
+    def start(self) -> "FakeRancher":
+        self._thread = threading.Thread(target=self._server.serve_forever, name="fake-rancher", daemon=True)
+        self._thread.start()
+        return self
+
+    def stop(self) -> None:
+        self._server.shutdown()
+        self._server.server_close()
+
+    def __enter__(self):
+        return self.start()
+
+    def __exit__(self, *exc):
+        self.stop()
+
+    # --- simulation -----------------------------------------------------------------------
+    def _refresh(self) -> None:
+        st = self.state
+        now = time.time()
+        with st.mu:
+            for c in st.clusters.values():
+                roles = {"etcd": False, "controlplane": False, "worker": False}
+                for n in st.nodes.values():
+                    if n["clusterId"] == c["id"]:
+                        for r in roles:
+                            roles[r] = roles[r] or n["roles"].get(r, False)
+                if c["state"] != "active" and all(roles.values()):
+                    if c.get("ready_at") is None:
+                        c["ready_at"] = now + st.rke_seconds
+                    if now >= c["ready_at"]:
+                        c["state"] = "active"
+                        c["transitioning"] = "no"
+                        st.cond.notify_all()
+                if c["state"] == "active":
+                    for n in st.nodes.values():
+                        if n["clusterId"] == c["id"] and n["state"] != "active":
+                            if n.get("ready_at") is None:
+                                n["ready_at"] = max(now, c["ready_at"]) + st.node_ready_seconds
+                            if now >= n["ready_at"]:
+                                n["state"] = "active"
+
+    def device_plugin_applied(self, cluster_id: str) -> bool:
+        with self.state.mu:
+            return any(k.startswith(cluster_id + "|") and "daemonsets" in k and "device-plugin" in k
+                       for k in self.state.objects)
+
+    def k8s_nodes(self, cluster_id: str) -> List[Dict[str, Any]]:
+        self._refresh()
+        st = self.state
+        plugin = self.device_plugin_applied(cluster_id)
+        items = []
+        with st.mu:
+            for n in st.nodes.values():
+                if n["clusterId"] != cluster_id:
+                    continue
+                ready = n["state"] == "active"
+                labels = dict(n["labels"])
+                for r, on in n["roles"].items():
+                    if on:
+                        labels[f"node-role.kubernetes.io/{r}"] = "true"
+                alloc = {"cpu": "64", "memory": "1Ti", "pods": "110"}
+                if plugin and "amd.com/gpu" in n["capacity"]:
+                    alloc["amd.com/gpu"] = str(n["capacity"]["amd.com/gpu"])
+                items.append({
+                    "metadata": {"name": n["hostname"], "labels": labels},
+                    "status": {"conditions": [{"type": "Ready", "status": "True" if ready else "False"}],
+                               "allocatable": alloc, "capacity": dict(alloc)},
+                })
+        return items
+
+    # --- HTTP ------------------------------------------------------------------------------
+    def _handler(self):
+        fake = self
+
+        class H(http.server.BaseHTTPRequestHandler):
+            protocol_version = "HTTP/1.1"
+
+            def log_message(self, *args):  # quiet
+                pass
+
+            def _send(self, code: int, obj: Any = None, raw: Optional[bytes] = None):
+                body = raw if raw is not None else (json.dumps(obj).encode() if obj is not None else b"")
+                self.send_response(code)
+                self.send_header("Content-Type", "application/json")
+                self.send_header("Content-Length", str(len(body)))
+                self.end_headers()
+                self.wfile.write(body)
+
+            def _body(self) -> Any:
+                n = int(self.headers.get("Content-Length") or 0)
+                raw = self.rfile.read(n) if n else b""
+                try:
+                    return json.loads(raw) if raw else {}
+                except ValueError:
+                    return {}
+
+            def _authed(self) -> bool:
+                auth = self.headers.get("Authorization", "")
+                st = fake.state
+                if auth.startswith("Basic "):
+                    try:
+                        user, _, secret = base64.b64decode(auth[6:]).decode().partition(":")
+                    except ValueError:
+                        return False
+                    with st.mu:
+                        return st.tokens.get(user) == secret
+                if auth.startswith("Bearer "):
+                    user, _, secret = auth[7:].partition(":")
+                    with st.mu:
+                        return st.tokens.get(user) == secret
+                return False
+
+            def do_GET(self):
+                self._dispatch("GET")
+
+            def do_POST(self):
+                self._dispatch("POST")
+
+            def do_PUT(self):
+                self._dispatch("PUT")
+
+            def do_DELETE(self):
+                self._dispatch("DELETE")
+
+            def do_HEAD(self):
+                self._dispatch("HEAD")
+
+            def _dispatch(self, method: str):
+                st = fake.state
+                parts = urllib.parse.urlsplit(self.path)
+                path, query = parts.path.rstrip("/") or "/", urllib.parse.parse_qs(parts.query)
+                with st.mu:
+                    st.requests += 1
+                    st.log.append((method, self.path))
+                body = self._body() if method in ("POST", "PUT") else {}
+                try:
+                    code, obj = fake._route(method, path, query, body, self)
+                except Exception as exc:  # pragma: no cover - surfaced to the client
+                    code, obj = 500, {"type": "error", "message": str(exc)}
+                if isinstance(obj, bytes):
+                    self._send(code, raw=obj)
+                else:
+                    self._send(code, obj)
+
+        return H
+
+    def _route(self, method: str, path: str, query: Dict[str, List[str]], body: Any, h) -> Tuple[int, Any]:
+        st = self.state
+        if path == "/ping":
+            return 200, b"pong"
+        if path == "/v3-public/localProviders/local" and query.get("action") == ["login"]:
+            if body.get("username") == "admin" and body.get("password") == st.admin_password:
+                name, secret = f"token-{uuid.uuid4().hex[:5]}", uuid.uuid4().hex
+                with st.mu:
+                    st.tokens[name] = secret
+                return 201, {"token": f"{name}:{secret}", "type": "token"}
+            return 401, {"type": "error", "code": "Unauthorized"}
+        if path == "/v3/connect/register" and method == "POST":
+            return self._register(h)
+        if not h._authed():
+            return 401, {"type": "error", "code": "Unauthorized"}
+        if path == "/v3/token" and method == "POST":
+            name, secret = f"token-{uuid.uuid4().hex[:5]}", uuid.uuid4().hex
+            with st.mu:
+                st.tokens[name] = secret
+            return 201, {"name": name, "token": f"{name}:{secret}", "type": "token"}
+        if path == "/v3/users" and query.get("action") == ["changepassword"]:
+            if body.get("currentPassword") != st.admin_password:
+                return 400, {"type": "error", "message": "invalid current password"}
+            st.admin_password = body.get("newPassword", "")
+            return 200, {}
+        if path.startswith("/v3/settings/"):
+            key = path.rsplit("/", 1)[1]
+            if method == "PUT":
+                st.settings[key] = body.get("value", "")
+            return 200, {"id": key, "name": key, "value": st.settings.get(key, "")}
+        if path == "/v3/clusters" and method == "GET":
+            self._refresh()
+            names = query.get("name")
+            with st.mu:
+                data = [c for c in st.clusters.values() if not names or c["name"] in names]
+            return 200, {"data": data}
+        if path == "/v3/cluster" and method == "POST":
+            cid = f"c-{uuid.uuid4().hex[:5]}"
+            with st.mu:
+                st.clusters[cid] = {"id": cid, "name": body.get("name", ""), "state": "provisioning",
+                                    "transitioning": "yes", "rancherKubernetesEngineConfig":
+                                        body.get("rancherKubernetesEngineConfig", {}), "created": time.time()}
+                return 201, dict(st.clusters[cid])
+        if path.startswith("/v3/clusters/"):
+            rest = path[len("/v3/clusters/"):].split("/")
+            cid = rest[0]
+            with st.mu:
+                if cid not in st.clusters:
+                    return 404, {"type": "error", "code": "NotFound"}
+            if len(rest) == 2 and rest[1] == "clusterregistrationtokens":
+                with st.mu:
+                    data = [dict(t, token=tok) for tok, t in st.reg_tokens.items() if t["clusterId"] == cid]
+                return 200, {"data": data}
+            if method == "DELETE":
+                with st.mu:
+                    st.clusters.pop(cid, None)
+                    for nid in [n for n, v in st.nodes.items() if v["clusterId"] == cid]:
+                        st.nodes.pop(nid)
+                return 200, {}
+            if method == "POST" and query.get("action") == ["generateKubeconfig"]:
+                return 200, {"config": f"apiVersion: v1\nkind: Config\nclusters:\n- name: {cid}\n"}
+            self._refresh()
+            with st.mu:
+                return 200, dict(st.clusters[cid])
+        if path == "/v3/clusterregistrationtoken" and method == "POST":
+            tok = uuid.uuid4().hex + uuid.uuid4().hex[:8]
+            with st.mu:
+                st.reg_tokens[tok] = {"id": f"{body.get('clusterId')}:default-token", "clusterId": body.get("clusterId")}
+            return 201, {"token": tok, "clusterId": body.get("clusterId"), "type": "clusterRegistrationToken"}
+        if path == "/v3/nodes" and method == "GET":
+            self._refresh()
+            cids = query.get("clusterId")
+            with st.mu:
+                data = [dict(n) for n in st.nodes.values() if not cids or n["clusterId"] in cids]
+            return 200, {"data": data}
+        if path.startswith("/v3/nodes/") and method == "DELETE":
+            with st.mu:
+                st.nodes.pop(path.rsplit("/", 1)[1], None)
+            return 200, {}
+        if path.startswith("/k8s/clusters/"):
+            return self._k8s(method, path, body)
+        return 404, {"type": "error", "code": "NotFound", "path": path}
+
+    def _register(self, h) -> Tuple[int, Any]:
+        st = self.state
+        token = h.headers.get("X-API-Tunnel-Token", "")
+        with st.mu:
+            reg = st.reg_tokens.get(token)
+        if reg is None:
+            return 401, {"type": "error", "code": "InvalidRegistrationToken"}
+        try:
+            params = json.loads(base64.b64decode(h.headers.get("X-API-Tunnel-Params", "")) or b"{}")
+        except ValueError:
+            return 400, {"type": "error", "message": "bad tunnel params"}
+        node = params.get("node", {})
+        hostname = node.get("requestedHostname", "")
+        roles = {"etcd": bool(node.get("etcd")), "controlplane": bool(node.get("controlPlane")),
+                 "worker": bool(node.get("worker"))}
+        with st.mu:
+            existing = [nid for nid, n in st.nodes.items()
+                        if n["clusterId"] == reg["clusterId"] and n["hostname"] == hostname]
+            nid = existing[0] if existing else f"m-{uuid.uuid4().hex[:6]}"
+            st.nodes[nid] = {"id": nid, "clusterId": reg["clusterId"], "hostname": hostname,
+                             "nodeName": hostname, "roles": roles, "labels": dict(node.get("labels", {})),
+                             "capacity": dict(node.get("capacity", {})), "state": "registering",
+                             "registered": time.time(), "ready_at": None}
+            st.cond.notify_all()
+        self._refresh()
+        return 201, {"id": nid, "clusterId": reg["clusterId"]}
+
+    def _k8s(self, method: str, path: str, body: Any) -> Tuple[int, Any]:
+        st = self.state
+        rest = path[len("/k8s/clusters/"):]
+        cid, _, kpath = rest.partition("/")
+        with st.mu:
+            if cid not in st.clusters:
+                return 404, {"kind": "Status", "code": 404}
+        kpath = "/" + kpath
+        if kpath == "/api/v1/nodes" and method == "GET":
+            return 200, {"kind": "NodeList", "items": self.k8s_nodes(cid)}
+        if kpath == "/version":
+            return 200, {"major": "1", "minor": "9", "gitVersion": "v1.9.5"}
+        if method == "POST":
+            name = (body.get("metadata") or {}).get("name", uuid.uuid4().hex[:6])
+            key = f"{cid}|{kpath}|{name}"
+            with st.mu:
+                if key in st.objects:
+                    return 409, {"kind": "Status", "reason": "AlreadyExists", "code": 409}
+                st.objects[key] = body
+            return 201, body
+        if method in ("PUT", "GET", "DELETE"):
+            base, _, name = kpath.rpartition("/")
+            key = f"{cid}|{base}|{name}"
+            with st.mu:
+                if method == "PUT":
+                    st.objects[key] = body
+                    return 200, body
+                if method == "DELETE":
+                    return (200, st.objects.pop(key)) if key in st.objects else (404, {"code": 404})
+                if key in st.objects:
+                    return 200, st.objects[key]
+                items = [o for k, o in st.objects.items() if k.startswith(f"{cid}|{kpath}|")]
+                return 200, {"items": items}
+        return 404, {"kind": "Status", "code": 404}
+
+
+def tunnel_params(hostname: str, roles: Dict[str, bool], labels: Dict[str, str],
+                  capacity: Dict[str, Any]) -> str:
+    """The ``X-API-Tunnel-Params`` header a node agent sends (base64 JSON)."""
+    node = {"requestedHostname": hostname, "etcd": roles.get("etcd", False),
+            "controlPlane": roles.get("controlplane", False), "worker": roles.get("worker", False),
+            "labels": labels, "capacity": capacity}
+    return base64.b64encode(json.dumps({"node": node}).encode()).decode()

@@ -1,0 +1,181 @@
+"""``create manager|cluster|node`` (reference ``create/manager.go``, ``create/cluster.go``,
+``create/node.go``).
+
+Flow per command: select/validate -> provider plugin adds module(s) to the
+document -> confirmation -> executor apply -> persist.
+
+Failure semantics differ deliberately from the
+reference, which persists ``main.tf.json`` only after a successful apply and so
+orphans whatever a failed apply created:
+
+* a failed apply still persists the document (so ``destroy`` can reach every
+  resource that may exist) and records ``status.json`` = ``{"phase":
+  "apply_failed", "modules": [...], "error": ...}`` in the backend;
+* ``create manager`` with the name of a manager whose first apply failed
+  resumes it instead of failing with "already exists".
+"""
+
+import json
+import time
+from typing import Dict, List, Optional
+
+from ..backend.base import Backend
+from ..config.context import Context, not_blank
+from ..errors import Canceled, ConfigError, TKError
+from ..models import CLUSTER_CHOICES, CLUSTER_PROVIDERS, MANAGER_CHOICES, MANAGER_PROVIDERS, NODE_ENTRY_KEYS
+from ..models import NODE_PROVIDERS
+from ..models.common import nodes_added_message
+from ..state import State
+from ..utils.trace import span
+from .select import executor_for, select_cluster, select_manager
+
+STATUS_BLOB = "status.json"
+NO_MANAGERS = "No cluster managers, please create a cluster manager before creating a kubernetes cluster."
+
+
+def read_status(backend: Backend, name: str) -> Dict:
+    try:
+        raw = backend.read_blob(name, STATUS_BLOB)
+    except (NotImplementedError, TKError):
+        return {}
+    return json.loads(raw) if raw else {}
+
+
+def _write_status(backend: Backend, name: str, status: Dict) -> None:
+    try:
+        backend.write_blob(name, STATUS_BLOB, json.dumps(status, indent=2).encode())
+    except NotImplementedError:
+        pass
+
+
+def apply_and_persist(ctx: Context, backend: Backend, state: State, new_modules: List[str]) -> None:
+    """Run the executor, then persist; on failure persist + record status (see module doc)."""
+    executor = executor_for(ctx, state)
+    with backend.lock(state.name):
+        try:
+            with span("apply", executor=executor.name, modules=len(new_modules)):
+                executor.apply(state, backend)
+        except BaseException as exc:
+            backend.persist_state(state)
+            _write_status(backend, state.name, {"phase": "apply_failed", "modules": new_modules,
+                                                "error": str(exc), "time": time.time()})
+            if isinstance(exc, TKError):
+                raise TKError(f"{exc}\n(desired state persisted; re-run to resume or destroy to clean up)") \
+                    from exc
+            raise
+        backend.persist_state(state)
+        _write_status(backend, state.name, {"phase": "applied", "modules": new_modules, "time": time.time()})
+
+
+# --- manager ---------------------------------------------------------------------------
+def new_manager(ctx: Context, backend: Backend) -> None:
+    provider = ctx.resolve_choice("manager_cloud_provider", "Create Manager in which Cloud Provider",
+                                  MANAGER_CHOICES, transform=str.lower)
+    name = ctx.resolve("name", "Cluster Manager Name", validate=not_blank("manager name cannot be blank"))
+    if not name:
+        raise ConfigError("Invalid Cluster Manager Name")
+    if name in backend.states():
+        if read_status(backend, name).get("phase") != "apply_failed":
+            raise ConfigError(f"A Cluster Manager with the name '{name}' already exists.")
+        ctx.echo(f"Resuming creation of '{name}' after a failed apply.")
+    state = backend.state(name)
+    fn = MANAGER_PROVIDERS.get(provider)
+    if fn is None:
+        raise ConfigError(f"Unsupported cloud provider '{provider}', cannot create manager")
+    fn(ctx, state, name)
+    if not ctx.confirm("Proceed with the manager creation", "Proceed"):
+        ctx.echo("Manager creation canceled.")
+        return
+    path, obj = backend.state_terraform_config(name)
+    state.set_terraform_backend_config(path, obj)
+    apply_and_persist(ctx, backend, state, ["cluster-manager"])
+
+
+# --- cluster ----------------------------------------------------------------------------
+def _node_entry_overrides(entry: Dict, provider: str) -> Dict:
+    """Settings overrides for one ``nodes:`` entry (Q4 fix: every present key)."""
+    if not isinstance(entry, dict):
+        raise ConfigError("Could not read node configuration")
+    overrides = {str(k): v for k, v in entry.items()}
+    for key in NODE_ENTRY_KEYS["common"]:
+        overrides.setdefault(key, None)  # per-node keys never leak between entries
+    return overrides
+
+
+def new_cluster(ctx: Context, backend: Backend) -> Optional[str]:
+    managers = backend.states()
+    if not managers:
+        raise ConfigError(NO_MANAGERS)
+    manager = select_manager(ctx, managers)
+    state = backend.state(manager)
+    provider = ctx.resolve_choice("cluster_cloud_provider", "Create Cluster in which Cloud Provider",
+                                  CLUSTER_CHOICES, transform=str.lower)
+    fn = CLUSTER_PROVIDERS.get(provider)
+    if fn is None:
+        raise ConfigError(f"Unsupported cloud provider '{provider}', cannot create cluster")
+    before = set(state.modules())
+    name = fn(ctx, backend, state)
+    clusters = state.clusters()
+    if name not in clusters:
+        raise ConfigError(f"Couldn't find cluster key for cluster '{name}'.\n")
+    key = clusters[name]
+
+    if ctx.is_set("nodes"):
+        entries = ctx.settings.get("nodes")
+        if not isinstance(entries, list):
+            raise ConfigError("Could not read 'nodes' configuration")
+        for entry in entries:
+            saved = ctx.settings.push_overrides(_node_entry_overrides(entry, provider))
+            try:
+                hostnames = NODE_PROVIDERS[provider](ctx, manager, key, backend, state)
+            finally:
+                ctx.settings.pop_overrides(saved)
+            ctx.echo(nodes_added_message(hostnames))
+
+    if not ctx.non_interactive:
+        more = ctx.prompter.yes_no("Would you like to create nodes for this cluster")
+        while more:
+            hostnames = NODE_PROVIDERS[provider](ctx, manager, key, backend, state)
+            ctx.echo(nodes_added_message(hostnames))
+            more = ctx.prompter.yes_no("Would you like to create more nodes for this cluster")
+        if not ctx.confirm("Proceed with cluster creation", "Proceed"):
+            ctx.echo("Cluster creation canceled.")
+            return None
+
+    new_modules = sorted(set(state.modules()) - before)
+    apply_and_persist(ctx, backend, state, new_modules)
+    if ctx.settings.get_bool("wait"):
+        from ..readiness.waiter import wait_after_create
+
+        wait_after_create(ctx, backend, state, key)
+    return name
+
+
+# --- node -----------------------------------------------------------------------------------
+def new_node(ctx: Context, backend: Backend) -> Optional[List[str]]:
+    managers = backend.states()
+    if not managers:
+        raise ConfigError(NO_MANAGERS)
+    manager = select_manager(ctx, managers)
+    state = backend.state(manager)
+    _, key = select_cluster(ctx, state.clusters(), "Cluster to deploy node to")
+    parts = key.split("_")
+    if len(parts) < 3:
+        raise ConfigError(f"Could not determine cloud provider for cluster '{key}'")
+    fn = NODE_PROVIDERS.get(parts[1])
+    if fn is None:
+        raise ConfigError(f"Unsupported cloud provider '{parts[1]}', cannot create node")
+    before = set(state.modules())
+    hostnames = fn(ctx, manager, key, backend, state)
+    if not ctx.confirm("Proceed with the node creation", "Proceed"):
+        ctx.echo("Node creation canceled")
+        return None
+    apply_and_persist(ctx, backend, state, sorted(set(state.modules()) - before))
+    if ctx.settings.get_bool("wait"):
+        from ..readiness.waiter import wait_after_create
+
+        wait_after_create(ctx, backend, state, key)
+    return hostnames
+
+
+__all__ = ["new_manager", "new_cluster", "new_node", "apply_and_persist", "read_status", "Canceled"]

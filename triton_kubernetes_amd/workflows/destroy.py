@@ -1,0 +1,102 @@
+"""``destroy manager|cluster|node`` (reference ``destroy/*.go``).
+
+* manager — destroy the whole document, then delete the backend state;
+* cluster — ``-target=module.<cluster>`` plus one target per node (and the
+  MI355X add-on module if present), then drop those modules and persist;
+* node    — ``-target=module.<node>``, drop it, persist.
+
+Extension (opt-in via ``rancher_cleanup: true``): also
+remove the cluster / node objects from Rancher after the destroy.
+"""
+
+from ..backend.base import Backend
+from ..config.context import Context
+from ..errors import ConfigError
+from ..models.baremetal import addons_key
+from ..state import cluster_key_parts
+from ..utils.trace import span
+from .create import NO_MANAGERS
+from .select import executor_for, select_cluster, select_manager, select_node
+
+
+def delete_manager(ctx: Context, backend: Backend) -> None:
+    managers = backend.states()
+    if not managers:
+        raise ConfigError(NO_MANAGERS)
+    manager = select_manager(ctx, managers, sort=True)
+    state = backend.state(manager)
+    if not ctx.confirm(f'Are you sure you want to destroy "{manager}"', f'Destroy "{manager}"'):
+        ctx.echo("Destroy manager canceled.")
+        return
+    with backend.lock(manager):
+        with span("destroy", scope="manager"):
+            executor_for(ctx, state).destroy(state, backend, [])
+        backend.delete_state(manager)
+
+
+def delete_cluster(ctx: Context, backend: Backend) -> None:
+    managers = backend.states()
+    if not managers:
+        raise ConfigError("No cluster managers.")
+    manager = select_manager(ctx, managers)
+    state = backend.state(manager)
+    name, key = select_cluster(ctx, state.clusters(), "Cluster to delete")
+    if not ctx.confirm(f'Are you sure you want to destroy "{name}"', f'Destroy "{name}"'):
+        ctx.echo("Destroy cluster canceled.")
+        return
+    nodes = state.nodes(key)
+    targets = [key] + [nodes[h] for h in sorted(nodes)]
+    _, cluster_name = cluster_key_parts(key)
+    addon = addons_key(cluster_name)
+    if state.module(addon) is not None:
+        targets.insert(0, addon)
+    with backend.lock(manager):
+        cleanup = _rancher_cleanup_info(ctx, backend, state, key)
+        with span("destroy", scope="cluster", targets=len(targets)):
+            executor_for(ctx, state).destroy(state, backend, [f"module.{t}" for t in targets])
+        for t in targets:
+            state.delete_module(t)
+        backend.persist_state(state)
+    if cleanup:
+        cleanup()
+
+
+def delete_node(ctx: Context, backend: Backend) -> None:
+    managers = backend.states()
+    if not managers:
+        raise ConfigError("No cluster managers, please create a cluster manager before creating a kubernetes node.")
+    manager = select_manager(ctx, managers)
+    state = backend.state(manager)
+    _, key = select_cluster(ctx, state.clusters(), "Cluster to delete", sort=False)
+    hostname, node_key = select_node(ctx, state.nodes(key))
+    if not ctx.confirm(f'Are you sure you want to destroy "{hostname}"', f'Destroy "{hostname}"'):
+        ctx.echo("Destroy node canceled.")
+        return
+    with backend.lock(manager):
+        with span("destroy", scope="node"):
+            executor_for(ctx, state).destroy(state, backend, [f"module.{node_key}"])
+        state.delete_module(node_key)
+        backend.persist_state(state)
+
+
+def _rancher_cleanup_info(ctx: Context, backend: Backend, state, cluster_key: str):
+    """Return a callable deleting the Rancher cluster object (opt-in), or ``None``."""
+    if not ctx.settings.get_bool("rancher_cleanup"):
+        return None
+    from ..executor.base import outputs_from_tfstate
+    from ..rancher.client import RancherClient
+    from ..state import MANAGER_KEY
+
+    raw = backend.read_tfstate(state.name)
+    mgr = outputs_from_tfstate(raw, MANAGER_KEY)
+    cl = outputs_from_tfstate(raw, cluster_key)
+    if not mgr.get("rancher_url") or not cl.get("rancher_cluster_id"):
+        return None
+
+    def _cleanup():
+        client = RancherClient(mgr["rancher_url"], mgr.get("rancher_access_key", ""),
+                               mgr.get("rancher_secret_key", ""))
+        client.delete_cluster(cl["rancher_cluster_id"])
+        ctx.echo(f"Removed Rancher cluster {cl['rancher_cluster_id']}")
+
+    return _cleanup
