@@ -1,0 +1,178 @@
+"""``triton-kubernetes`` command line (reference ``cmd/*.go``).
+
+    triton-kubernetes [--config FILE] [--non-interactive] create  manager|cluster|node
+    triton-kubernetes [--config FILE] [--non-interactive] destroy manager|cluster|node
+    triton-kubernetes [--config FILE] [--non-interactive] get     manager|cluster
+    triton-kubernetes version
+
+Additions: ``wait cluster`` (the readiness waiter on an existing cluster),
+``gpu …`` (the native MI355X probes) and ``agent`` (the node agent).
+
+Exit codes follow the reference: argument errors exit 255 (``os.Exit(-1)``),
+workflow errors print the message and exit 1.  The dead ``-t/--toggle`` scaffold
+flag (``cmd/root.go:44``) is not reproduced.
+"""
+
+import argparse
+import os
+import sys
+from typing import List, Optional, Sequence, TextIO
+
+from .. import __version__
+from ..errors import Canceled, TKError
+
+# Injected at build time (the reference's -ldflags -X cmd.cliVersion).
+CLI_VERSION = ""
+try:  # pragma: no cover - generated file
+    from .._build_info import CLI_VERSION as _BUILD_VERSION  # type: ignore
+
+    CLI_VERSION = _BUILD_VERSION
+except ImportError:
+    pass
+
+VALID = {
+    "create": ["manager", "cluster", "node"],
+    "destroy": ["manager", "cluster", "node"],
+    "get": ["manager", "cluster"],
+    "wait": ["cluster"],
+}
+# the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
+_ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait"}
+
+
+class ArgError(Exception):
+    pass
+
+
+def version_text(cli_version: Optional[str] = None) -> str:
+    v = CLI_VERSION if cli_version is None else cli_version
+    prefix = ""
+    if not v:
+        prefix = "no version set for this build... "
+        v = "local"
+    return f"{prefix}triton-kubernetes v{__version__} ({v})\n"
+
+
+def _check_args(cmd: str, args: List[str]) -> str:
+    if len(args) != 1:
+        raise ArgError(f'"triton-kubernetes {_ARG_NAME[cmd]}" requires one argument')
+    if args[0] not in VALID[cmd]:
+        raise ArgError(f'invalid argument "{args[0]}" for "triton-kubernetes {_ARG_NAME[cmd]}"')
+    return args[0]
+
+
+def build_parser() -> argparse.ArgumentParser:
+    common = argparse.ArgumentParser(add_help=False)
+    common.add_argument("--config", default=argparse.SUPPRESS,
+                        help="config file (default is $HOME/.triton-kubernetes.yaml)")
+    common.add_argument("--non-interactive", action="store_true", default=argparse.SUPPRESS,
+                        help="Prevent interactive prompts")
+    root = argparse.ArgumentParser(
+        prog="triton-kubernetes", parents=[common],
+        description="A tool to deploy Kubernetes to multiple cloud providers and to bare-metal 8xMI355X nodes.")
+    sub = root.add_subparsers(dest="command")
+    for cmd, help_ in (("create", "Create cluster managers, kubernetes clusters or individual kubernetes cluster "
+                                  "nodes."),
+                       ("destroy", "Destroy cluster managers, kubernetes clusters or individual kubernetes "
+                                   "cluster nodes."),
+                       ("get", "Display resource information"),
+                       ("wait", "Wait until a cluster is kubectl-ready (and GPU-ready) and report timings")):
+        p = sub.add_parser(cmd, parents=[common], help=help_)
+        p.add_argument("args", nargs="*")
+    sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
+    g = sub.add_parser("gpu", help="MI355X node probes (burnin, topology, labels, rccl-local, hbm, mfma)")
+    g.add_argument("gpu_args", nargs=argparse.REMAINDER)
+    a = sub.add_parser("agent", help="Run the node agent (tk-node-agent)")
+    a.add_argument("agent_args", nargs=argparse.REMAINDER)
+    return root
+
+
+def make_context(ns: argparse.Namespace, out: TextIO, env=None):
+    from ..config import Context, Settings
+
+    settings = Settings.discover(getattr(ns, "config", None), env=env)
+    if getattr(ns, "non_interactive", False):
+        settings.set_flag("non-interactive", True)
+    ctx = Context(settings=settings, out=out)
+    if settings.non_interactive:
+        ctx.echo("Running in non interactive mode")
+    if settings.config_file_used:
+        ctx.echo(f"Using config file: {settings.config_file_used}")
+    return ctx
+
+
+def run(argv: Sequence[str], out: Optional[TextIO] = None, ctx=None) -> int:
+    out = out or sys.stdout
+    parser = build_parser()
+    ns = parser.parse_args(list(argv))
+    if ns.command is None:
+        parser.print_help(out)
+        return 0
+    if ns.command == "version":
+        out.write(version_text())
+        return 0
+    if ns.command == "gpu":
+        from ..ops.cli import main as gpu_main
+
+        return gpu_main(ns.gpu_args)
+    if ns.command == "agent":
+        from ..node.agent import main as agent_main
+
+        return agent_main(ns.agent_args)
+    try:
+        what = _check_args(ns.command, ns.args)
+    except ArgError as exc:
+        out.write(f"{exc}\n")
+        return 255
+    try:
+        if ctx is None:
+            ctx = make_context(ns, out)
+        from ..backend import prompt_for_backend
+
+        backend = prompt_for_backend(ctx)
+        return dispatch(ctx, backend, ns.command, what)
+    except Canceled:
+        return 0
+    except TKError as exc:
+        out.write(f"{exc}\n")
+        return 1
+    except KeyboardInterrupt:
+        out.write("^C\n")
+        return 1
+
+
+def dispatch(ctx, backend, command: str, what: str) -> int:
+    from .. import workflows as wf
+
+    ctx.echo(f"{command} {what} called")
+    if command == "create":
+        {"manager": wf.new_manager, "cluster": wf.new_cluster, "node": wf.new_node}[what](ctx, backend)
+    elif command == "destroy":
+        {"manager": wf.delete_manager, "cluster": wf.delete_cluster, "node": wf.delete_node}[what](ctx, backend)
+    elif command == "get":
+        {"manager": wf.get_manager, "cluster": wf.get_cluster}[what](ctx, backend)
+    elif command == "wait":
+        from ..readiness.waiter import wait_after_create
+        from ..workflows.select import select_cluster, select_manager
+
+        managers = backend.states()
+        if not managers:
+            raise TKError("No cluster managers.")
+        state = backend.state(select_manager(ctx, managers))
+        _, key = select_cluster(ctx, state.clusters(), "Cluster to wait for")
+        wait_after_create(ctx, backend, state, key)
+    return 0
+
+
+def main(argv: Optional[Sequence[str]] = None) -> int:
+    code = run(sys.argv[1:] if argv is None else argv)
+    trace = os.environ.get("TK_TRACE")
+    if trace:
+        from ..utils.trace import TRACER
+
+        TRACER.dump_chrome(trace)
+    return code
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -9,6 +9,7 @@ reference calls it with ``curl --insecure``), and a request hook for signing
 
 import http.client
 import json
+import socket
 import ssl
 import threading
 import time
@@ -83,6 +84,9 @@ class HTTPClient:
             else:
                 conn = http.client.HTTPConnection(netloc, timeout=self.timeout)
             pool[key] = conn
+        if conn.sock is None:
+            conn.connect()
+            conn.sock.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
         return conn
 
     def _drop(self, scheme: str, netloc: str) -> None:

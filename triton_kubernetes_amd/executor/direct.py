@@ -1,0 +1,367 @@
+"""DirectExecutor: native execution of the bare-metal module family.
+
+Implements, without a Terraform binary, the semantics of
+
+* ``bare-metal-rancher`` (T5): install docker + run ``rancher/server`` over SSH
+  (S1, S2), then bootstrap the API (S3) — from the operator side by default, or
+  on the host like the reference (``rancher_bootstrap: remote``).  A manager
+  ``host`` of the form ``rancher+https://…`` adopts an already running server;
+* ``bare-metal-rancher-k8s`` (T10): find-or-create the RKE cluster, its
+  registration token and CA checksum (S4) through the Rancher client;
+* ``bare-metal-rancher-k8s-host`` (T16) and ``bare-metal-mi355x-rancher-k8s-host``:
+  a :class:`~..node.plan.BootstrapPlan` per node, delivered by a transport
+  (SSH / node agent / local);
+* ``rancher-k8s-mi355x-addons``: wait for the cluster, then apply the ROCm
+  device plugin / labeller / RCCL manifests through Rancher's k8s proxy.
+
+Scheduling is a dependency-driven DAG walk over the ``${module.X.Y}``
+interpolations: every module whose inputs are available starts immediately,
+up to ``parallelism`` (default 64, vs Terraform's 10) in flight — so all N nodes
+of a cluster bootstrap concurrently and the add-on step overlaps them.
+
+State: a tfstate-compatible document (root outputs ``<module>__<output>`` plus
+per-module config hashes) written to the backend after *every* module, so a
+failed apply keeps completed modules and a re-run resumes (unchanged, already
+applied modules are skipped — the whole document is re-applied exactly like the
+reference's ``terraform apply`` of ``main.tf.json``).
+"""
+
+import concurrent.futures as cf
+import copy
+import hashlib
+import json
+import re
+import threading
+import time
+import uuid
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional, Set, Tuple
+
+from .. import __version__
+from ..backend.base import Backend
+from ..errors import ExecutorError, TKError
+from ..node.plan import TOOLS_DIR, build_host_plan
+from ..parallel.transport import HostRef, Transport, TransportRouter
+from ..rancher.client import RancherClient, wait_until
+from ..state import State
+from ..terraform.catalog import ModuleInfo, module_from_source
+from ..utils.trace import span
+from .base import Executor, outputs_from_tfstate
+
+INTERP_RE = re.compile(r"\$\{module\.([A-Za-z0-9_.-]+?)\.([A-Za-z0-9_]+)\}")
+SUPPORTED = {"bare-metal-rancher", "bare-metal-rancher-k8s", "bare-metal-rancher-k8s-host",
+             "bare-metal-mi355x-rancher-k8s-host", "rancher-k8s-mi355x-addons"}
+
+
+def config_hash(cfg: Any) -> str:
+    return hashlib.sha256(json.dumps(cfg, sort_keys=True).encode()).hexdigest()[:16]
+
+
+def module_deps(cfg: Any) -> Set[str]:
+    deps: Set[str] = set()
+
+    def walk(v: Any) -> None:
+        if isinstance(v, str):
+            deps.update(m.group(1) for m in INTERP_RE.finditer(v))
+        elif isinstance(v, dict):
+            for x in v.values():
+                walk(x)
+        elif isinstance(v, list):
+            for x in v:
+                walk(x)
+
+    walk(cfg)
+    return deps
+
+
+def resolve(cfg: Any, outputs: Dict[str, Dict[str, str]]) -> Any:
+    def sub(m: "re.Match") -> str:
+        mod, out = m.group(1), m.group(2)
+        try:
+            return str(outputs[mod][out])
+        except KeyError:
+            raise ExecutorError(f"module.{mod}.{out} is not available (module not applied?)") from None
+
+    if isinstance(cfg, str):
+        return INTERP_RE.sub(sub, cfg)
+    if isinstance(cfg, dict):
+        return {k: resolve(v, outputs) for k, v in cfg.items()}
+    if isinstance(cfg, list):
+        return [resolve(v, outputs) for v in cfg]
+    return cfg
+
+
+@dataclass
+class ModuleRun:
+    key: str
+    info: ModuleInfo
+    cfg: Dict[str, Any]
+    deps: Set[str]
+    status: str = "pending"  # pending | skipped | ok | failed | blocked
+    error: Optional[str] = None
+    start: float = 0.0
+    end: float = 0.0
+    detail: Any = None
+
+
+@dataclass
+class ApplyReport:
+    runs: Dict[str, ModuleRun] = field(default_factory=dict)
+    wall: float = 0.0
+
+    @property
+    def ok(self) -> bool:
+        return all(r.status in ("ok", "skipped") for r in self.runs.values())
+
+    def summary(self) -> Dict[str, Any]:
+        return {k: {"status": r.status, "seconds": round(r.end - r.start, 4) if r.end else None,
+                    "error": r.error} for k, r in self.runs.items()}
+
+
+class DirectExecutor(Executor):
+    name = "direct"
+
+    def __init__(self, transport: Optional[Transport] = None, parallelism: int = 64,
+                 rancher_factory: Optional[Callable[..., RancherClient]] = None, rancher_bootstrap: str = "operator",
+                 node_timeout: float = 3600.0, cluster_wait: float = 1800.0, upload_tools: bool = True,
+                 node_cleanup: bool = False, on_event: Optional[Callable[[str, Dict[str, Any]], None]] = None):
+        self.transport = transport or TransportRouter()
+        self.parallelism = max(1, parallelism)
+        self.rancher_factory = rancher_factory or (lambda url, ak="", sk="": RancherClient(url, ak, sk))
+        self.rancher_bootstrap = rancher_bootstrap
+        self.node_timeout = node_timeout
+        self.cluster_wait = cluster_wait
+        self.upload_tools = upload_tools
+        self.node_cleanup = node_cleanup
+        self.on_event = on_event
+        self.last_report: Optional[ApplyReport] = None
+        self._mu = threading.Lock()
+
+    # --- tfstate ---------------------------------------------------------------------------------
+    @staticmethod
+    def _load_tfstate(backend: Backend, name: str) -> Dict[str, Any]:
+        raw = backend.read_tfstate(name)
+        if raw:
+            try:
+                doc = json.loads(raw)
+                if isinstance(doc, dict) and "module_state" in doc:
+                    return doc
+            except ValueError:
+                pass
+        return {"version": 4, "terraform_version": f"tk-direct-{__version__}", "serial": 0,
+                "lineage": str(uuid.uuid4()), "outputs": {}, "resources": [], "module_outputs": {},
+                "module_state": {}}
+
+    def _save_tfstate(self, backend: Backend, name: str, doc: Dict[str, Any]) -> None:
+        with self._mu:
+            doc["serial"] = int(doc.get("serial", 0)) + 1
+            outputs = {}
+            for key, outs in doc["module_outputs"].items():
+                for k, v in outs.items():
+                    outputs[f"{key}__{k}"] = {"value": v, "type": "string"}
+            doc["outputs"] = outputs
+            backend.write_tfstate(name, json.dumps(doc, indent=2, sort_keys=True).encode())
+
+    # --- planning -------------------------------------------------------------------------------------
+    def plan(self, state: State) -> Dict[str, ModuleRun]:
+        runs: Dict[str, ModuleRun] = {}
+        for key, cfg in state.modules().items():
+            info = module_from_source(str(cfg.get("source", "")))
+            if info is None or info.name not in SUPPORTED:
+                raise ExecutorError(f"the direct executor does not implement module '{cfg.get('source')}' "
+                                    f"(module.{key}); use `executor: terraform`")
+            runs[key] = ModuleRun(key, info, cfg, module_deps(cfg))
+        # An add-on module is applied after every host of its cluster (Terraform
+        # would need an explicit depends_on): a failed node then blocks it
+        # instead of leaving it waiting for a cluster that cannot turn active.
+        for r in runs.values():
+            if r.info.kind == "addon":
+                clusters = {d for d in r.deps if runs.get(d) and runs[d].info.kind == "cluster"}
+                r.deps |= {k for k, h in runs.items() if h.info.kind == "host" and h.deps & clusters}
+        for r in runs.values():
+            missing = r.deps - set(runs)
+            if missing:
+                raise ExecutorError(f"module.{r.key} references unknown module(s): {', '.join(sorted(missing))}")
+        return runs
+
+    @staticmethod
+    def supports(state: State) -> bool:
+        for cfg in state.modules().values():
+            info = module_from_source(str(cfg.get("source", "")))
+            if info is None or info.name not in SUPPORTED:
+                return False
+        return bool(state.modules())
+
+    def _event(self, kind: str, **data: Any) -> None:
+        if self.on_event is not None:
+            self.on_event(kind, data)
+
+    # --- apply -------------------------------------------------------------------------------------------
+    def apply(self, state: State, backend: Backend) -> None:
+        report = self.apply_report(state, backend)
+        if not report.ok:
+            failed = [f"module.{k}: {r.error}" for k, r in report.runs.items() if r.status == "failed"]
+            raise ExecutorError("apply failed: " + "; ".join(failed))
+
+    def apply_report(self, state: State, backend: Backend) -> ApplyReport:
+        t0 = time.time()
+        runs = self.plan(state)
+        tf = self._load_tfstate(backend, state.name)
+        outputs: Dict[str, Dict[str, str]] = {k: dict(v) for k, v in tf["module_outputs"].items() if k in runs}
+        report = ApplyReport(runs)
+        pending = set(runs)
+        futures: Dict[cf.Future, str] = {}
+        with span("direct.apply", modules=len(runs)), \
+                cf.ThreadPoolExecutor(max_workers=self.parallelism, thread_name_prefix="tk-direct") as pool:
+            while pending or futures:
+                for key in sorted(pending):
+                    run = runs[key]
+                    if any(runs[d].status in ("failed", "blocked") for d in run.deps):
+                        run.status, run.error = "blocked", "dependency failed"
+                        pending.discard(key)
+                        continue
+                    if all(runs[d].status in ("ok", "skipped") for d in run.deps):
+                        pending.discard(key)
+                        prev = tf["module_state"].get(key)
+                        h = config_hash(run.cfg)
+                        if prev and prev.get("hash") == h and prev.get("status") == "ok" and key in outputs:
+                            run.status = "skipped"
+                            continue
+                        run.start = time.time()
+                        futures[pool.submit(self._apply_module, run, dict(outputs), state.name)] = key
+                if not futures:
+                    for key in pending:  # nothing running and nothing startable: a cycle
+                        runs[key].status, runs[key].error = "failed", "dependency cycle"
+                    pending.clear()
+                    break
+                done, _ = cf.wait(list(futures), return_when=cf.FIRST_COMPLETED)
+                for fut in done:
+                    key = futures.pop(fut)
+                    run = runs[key]
+                    run.end = time.time()
+                    try:
+                        outs, detail = fut.result()
+                        run.status, run.detail = "ok", detail
+                        outputs[key] = outs
+                        tf["module_outputs"][key] = outs
+                        tf["module_state"][key] = {"hash": config_hash(run.cfg), "status": "ok",
+                                                   "applied_at": run.end, "seconds": run.end - run.start,
+                                                   "source": run.cfg.get("source")}
+                    except Exception as exc:  # noqa: BLE001 - recorded per module
+                        run.status, run.error = "failed", str(exc)
+                        tf["module_state"][key] = {"hash": config_hash(run.cfg), "status": "failed",
+                                                   "error": str(exc), "applied_at": run.end}
+                    self._save_tfstate(backend, state.name, tf)
+                    self._event("module_done", key=key, status=run.status, seconds=run.end - run.start)
+        report.wall = time.time() - t0
+        self.last_report = report
+        return report
+
+    def _apply_module(self, run: ModuleRun, outputs: Dict[str, Dict[str, str]],
+                      manager_name: str) -> Tuple[Dict[str, str], Any]:
+        cfg = resolve(copy.deepcopy(run.cfg), outputs)
+        kind = run.info.kind
+        with span(f"module.{kind}", key=run.key, module=run.info.name):
+            if kind == "manager":
+                return self._apply_manager(cfg), None
+            if kind == "cluster":
+                return self._apply_cluster(cfg), None
+            if kind == "host":
+                return self._apply_host(run.key, cfg, run.info.mi355x)
+            if kind == "addon":
+                return self._apply_addons(cfg), None
+        raise ExecutorError(f"unsupported module kind {kind}")
+
+    # --- manager ---------------------------------------------------------------------------------------
+    def _apply_manager(self, cfg: Dict[str, Any]) -> Dict[str, str]:
+        host = str(cfg.get("host", ""))
+        password = cfg.get("rancher_admin_password", "")
+        if host.startswith("rancher+"):
+            url = host[len("rancher+"):]
+            client = self.rancher_factory(url)
+            return client.bootstrap(password, url, timeout=self.cluster_wait)
+        ref = HostRef(host, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "~/.ssh/id_rsa",
+                      cfg.get("bastion_host") or "")
+        from ..node.manager import manager_install_script, manager_setup_script
+
+        with span("manager.install", host=host):
+            self.transport.run_script(ref, manager_install_script(cfg), timeout=self.node_timeout)
+        url = f"https://{host}"
+        if self.rancher_bootstrap == "remote":
+            with span("manager.setup_remote", host=host):
+                out = self.transport.run_script(ref, manager_setup_script(cfg, url), timeout=self.node_timeout)
+            data = json.loads(out.strip().splitlines()[-1])
+            return {"rancher_url": url, "rancher_access_key": data["name"],
+                    "rancher_secret_key": data["token"].split(":", 1)[-1]}
+        client = self.rancher_factory(url)
+        return client.bootstrap(password, url, timeout=self.cluster_wait)
+
+    # --- cluster ---------------------------------------------------------------------------------------
+    def _apply_cluster(self, cfg: Dict[str, Any]) -> Dict[str, str]:
+        client = self.rancher_factory(cfg["rancher_api_url"], cfg.get("rancher_access_key", ""),
+                                      cfg.get("rancher_secret_key", ""))
+        info = client.ensure_cluster(cfg["name"], cfg.get("k8s_version") or "v1.9.5-rancher1-1",
+                                     cfg.get("k8s_network_provider") or "flannel", cfg.get("k8s_registry", ""),
+                                     cfg.get("k8s_registry_username", ""), cfg.get("k8s_registry_password", ""))
+        return info.outputs()
+
+    # --- host ------------------------------------------------------------------------------------------------
+    def _apply_host(self, key: str, cfg: Dict[str, Any], mi355x: bool) -> Tuple[Dict[str, str], Any]:
+        ref = HostRef(str(cfg.get("host", "")), cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
+                      cfg.get("bastion_host") or "")
+        plan = build_host_plan(cfg, cfg["rancher_api_url"], cfg["rancher_cluster_registration_token"],
+                               cfg["rancher_cluster_ca_checksum"], mi355x=mi355x)
+        if mi355x and self.upload_tools and ref.scheme == "ssh":
+            self._upload_tools(ref)
+        result = self.transport.run_plan(ref, plan, timeout=self.node_timeout)
+        if not result.get("ok"):
+            raise ExecutorError(f"{plan.hostname}: {result.get('error')}")
+        outs: Dict[str, str] = {}
+        if mi355x:
+            outs["gpu_node_labels"] = json.dumps(result.get("labels", {}), sort_keys=True)
+        return outs, result
+
+    def _upload_tools(self, ref: HostRef) -> None:
+        from ..ops.native import executable
+
+        for tool in ("amdgpu-topo-labeller", "gpu-burnin", "rccl-ready"):
+            self.transport.put_file(ref, executable(tool), f"{TOOLS_DIR}/{tool}")
+
+    # --- addons -------------------------------------------------------------------------------------------
+    def _apply_addons(self, cfg: Dict[str, Any]) -> Dict[str, str]:
+        from ..k8s.manifests import addon_manifests, apply_manifests
+
+        client = self.rancher_factory(cfg["rancher_api_url"], cfg.get("rancher_access_key", ""),
+                                      cfg.get("rancher_secret_key", ""))
+        cid = cfg["rancher_cluster_id"]
+        with span("addons.wait_active", cluster=cid):
+            wait_until(lambda: client.cluster_state(cid) == "active", self.cluster_wait, f"cluster {cid} active")
+        with span("addons.apply", cluster=cid):
+            applied = apply_manifests(client, cid, addon_manifests(cfg))
+        return {"addons_applied": str(len(applied))}
+
+    # --- destroy / outputs ------------------------------------------------------------------------------
+    def destroy(self, state: State, backend: Backend, targets: List[str]) -> None:
+        tf = self._load_tfstate(backend, state.name)
+        keys = [t[len("module."):] if t.startswith("module.") else t for t in targets] or list(state.modules())
+        if self.node_cleanup:
+            from ..node.manager import node_cleanup_script
+
+            for key in keys:
+                cfg = state.module(key) or {}
+                info = module_from_source(str(cfg.get("source", "")))
+                if info is not None and info.kind == "host":
+                    ref = HostRef(str(cfg.get("host", "")), cfg.get("ssh_user") or "ubuntu",
+                                  cfg.get("key_path") or "", cfg.get("bastion_host") or "")
+                    if ref.scheme != "agent":
+                        try:
+                            self.transport.run_script(ref, node_cleanup_script(), timeout=600)
+                        except TKError as exc:
+                            raise ExecutorError(f"cleanup of {cfg.get('hostname')}: {exc}") from exc
+        for key in keys:
+            tf["module_outputs"].pop(key, None)
+            tf["module_state"].pop(key, None)
+        self._save_tfstate(backend, state.name, tf)
+
+    def outputs(self, state: State, backend: Backend, module_key: str) -> Dict[str, str]:
+        return outputs_from_tfstate(backend.read_tfstate(state.name), module_key)

@@ -1,0 +1,52 @@
+"""Executor selection from settings.
+
+==========================  ================================================================
+``executor``                ``terraform`` | ``direct`` | ``auto`` (default)
+``terraform_binary``        path/name of the Terraform CLI (default ``terraform``)
+``terraform_parallelism``   ``-parallelism=N`` for apply/destroy (default: Terraform's 10)
+``direct_parallelism``      max modules in flight in the DirectExecutor (default 64)
+``agent_token``             shared token for ``agent+http://`` hosts
+``rancher_bootstrap``       ``operator`` (default) | ``remote``
+``node_cleanup``            run the agent cleanup script on destroy (default false)
+==========================  ================================================================
+
+``auto`` picks Terraform when the binary is on ``PATH``; otherwise the
+DirectExecutor when it implements every module of the document.
+"""
+
+from typing import Optional
+
+from ..config.context import Context
+from ..state import State
+from .base import Executor
+from .shell import which
+
+
+def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
+    s = ctx.settings
+    kind = (s.get_string("executor") or "auto").lower()
+    tf_bin = s.get_string("terraform_binary") or "terraform"
+    if kind == "auto":
+        if which(tf_bin):
+            kind = "terraform"
+        else:
+            from .direct import DirectExecutor
+
+            kind = "direct" if state is not None and DirectExecutor.supports(state) else "terraform"
+    if kind == "terraform":
+        from .terraform import TerraformExecutor
+
+        par = s.get_int("terraform_parallelism") if s.is_set("terraform_parallelism") else None
+        return TerraformExecutor(binary=tf_bin, parallelism=par)
+    if kind == "direct":
+        from ..parallel.transport import AgentTransport, SSHTransport, TransportRouter
+        from .direct import DirectExecutor
+
+        transport = ctx.extras.get("transport") or TransportRouter(
+            ssh=SSHTransport(), agent=AgentTransport(token=s.get_string("agent_token")))
+        par = s.get_int("direct_parallelism") if s.is_set("direct_parallelism") else 64
+        return DirectExecutor(transport=transport, parallelism=par,
+                              rancher_bootstrap=s.get_string("rancher_bootstrap") or "operator",
+                              node_cleanup=s.get_bool("node_cleanup"),
+                              rancher_factory=ctx.extras.get("rancher_factory"))
+    raise ValueError(f"unknown executor '{kind}' (terraform | direct | auto)")

@@ -1,0 +1,155 @@
+"""Kubernetes manifests for MI355X clusters + applying them through Rancher.
+
+* ROCm device plugin DaemonSet (advertises ``amd.com/gpu``), scheduled on nodes
+  labelled ``amd.com/gpu.present=true`` by the bootstrap labeller;
+* ROCm node-labeller DaemonSet (optional, keeps ``amd.com/gpu.*`` labels fresh);
+* ``rccl-env`` ConfigMap carrying the RCCL/HSA environment for GPU pods;
+* :func:`gpu_job_manifest` — an example/utility Job that requests all 8 GPUs
+  of one xGMI hive (node affinity on ``amd.com/xgmi.fully-connected`` and the
+  GPU count) and, for multi-node jobs, pod affinity on ``amd.com/xgmi.hive-id``
+  so ranks land inside one hive; the RCCL readiness Job (N2) is built with it.
+"""
+
+from typing import Any, Dict, List, Optional, Tuple
+
+from ..errors import TKError
+from ..parallel.rccl_env import default_rccl_env
+
+NAMESPACE = "kube-system"
+DEVICE_PLUGIN_NAME = "amdgpu-device-plugin"
+LABELLER_NAME = "amdgpu-node-labeller"
+GPU_SELECTOR = {"amd.com/gpu.present": "true"}
+
+
+def device_plugin_daemonset(image: str) -> Dict[str, Any]:
+    return {
+        "apiVersion": "apps/v1", "kind": "DaemonSet",
+        "metadata": {"name": DEVICE_PLUGIN_NAME, "namespace": NAMESPACE},
+        "spec": {
+            "selector": {"matchLabels": {"name": DEVICE_PLUGIN_NAME}},
+            "template": {
+                "metadata": {"labels": {"name": DEVICE_PLUGIN_NAME}},
+                "spec": {
+                    "nodeSelector": dict(GPU_SELECTOR),
+                    "priorityClassName": "system-node-critical",
+                    "tolerations": [{"key": "CriticalAddonsOnly", "operator": "Exists"},
+                                    {"key": "amd.com/gpu", "operator": "Exists", "effect": "NoSchedule"}],
+                    "containers": [{
+                        "name": "device-plugin", "image": image,
+                        "securityContext": {"allowPrivilegeEscalation": False,
+                                            "capabilities": {"drop": ["ALL"]}},
+                        "volumeMounts": [{"name": "dp", "mountPath": "/var/lib/kubelet/device-plugins"},
+                                         {"name": "sys", "mountPath": "/sys"}],
+                    }],
+                    "volumes": [{"name": "dp", "hostPath": {"path": "/var/lib/kubelet/device-plugins"}},
+                                {"name": "sys", "hostPath": {"path": "/sys"}}],
+                },
+            },
+        },
+    }
+
+
+def labeller_daemonset(image: str) -> Dict[str, Any]:
+    return {
+        "apiVersion": "apps/v1", "kind": "DaemonSet",
+        "metadata": {"name": LABELLER_NAME, "namespace": NAMESPACE},
+        "spec": {
+            "selector": {"matchLabels": {"name": LABELLER_NAME}},
+            "template": {
+                "metadata": {"labels": {"name": LABELLER_NAME}},
+                "spec": {
+                    "nodeSelector": dict(GPU_SELECTOR),
+                    "serviceAccountName": LABELLER_NAME,
+                    "containers": [{
+                        "name": "labeller", "image": image,
+                        "args": ["-vram", "-cu-count", "-simd-count", "-device-id", "-family", "-product-name",
+                                 "-driver-version", "-compute-partitioning-supported",
+                                 "-memory-partitioning-supported"],
+                        "env": [{"name": "DS_NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}],
+                        "securityContext": {"privileged": True},
+                        "volumeMounts": [{"name": "sys", "mountPath": "/sys"}, {"name": "dev", "mountPath": "/dev"}],
+                    }],
+                    "volumes": [{"name": "sys", "hostPath": {"path": "/sys"}},
+                                {"name": "dev", "hostPath": {"path": "/dev"}}],
+                },
+            },
+        },
+    }
+
+
+def rccl_configmap(env: Optional[Dict[str, str]] = None) -> Dict[str, Any]:
+    return {"apiVersion": "v1", "kind": "ConfigMap",
+            "metadata": {"name": "rccl-env", "namespace": NAMESPACE},
+            "data": dict(env or default_rccl_env())}
+
+
+def gpu_job_manifest(name: str, image: str, command: List[str], gpus_per_pod: int = 8, pods: int = 1,
+                     namespace: str = "default", hive_affinity: bool = True) -> Dict[str, Any]:
+    """A Job whose pods each take ``gpus_per_pod`` GPUs of one fully connected xGMI hive."""
+    node_terms = [{"matchExpressions": [
+        {"key": "amd.com/gpu.present", "operator": "In", "values": ["true"]},
+        {"key": "amd.com/gpu.count", "operator": "In", "values": [str(gpus_per_pod)]},
+    ]}]
+    if gpus_per_pod > 1:
+        node_terms[0]["matchExpressions"].append(
+            {"key": "amd.com/xgmi.fully-connected", "operator": "In", "values": ["true"]})
+    affinity: Dict[str, Any] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+        "nodeSelectorTerms": node_terms}}}
+    if hive_affinity and pods > 1:
+        affinity["podAffinity"] = {"preferredDuringSchedulingIgnoredDuringExecution": [{
+            "weight": 100,
+            "podAffinityTerm": {"labelSelector": {"matchLabels": {"job-name": name}},
+                                "topologyKey": "amd.com/xgmi.hive-id"}}]}
+    return {
+        "apiVersion": "batch/v1", "kind": "Job",
+        "metadata": {"name": name, "namespace": namespace},
+        "spec": {
+            "parallelism": pods, "completions": pods, "backoffLimit": 0,
+            "template": {
+                "metadata": {"labels": {"job-name": name}},
+                "spec": {
+                    "restartPolicy": "Never",
+                    "affinity": affinity,
+                    "containers": [{
+                        "name": "main", "image": image, "command": command,
+                        "envFrom": [{"configMapRef": {"name": "rccl-env"}}],
+                        "resources": {"limits": {"amd.com/gpu": str(gpus_per_pod)}},
+                        "securityContext": {"capabilities": {"add": ["SYS_PTRACE"]}},
+                    }],
+                    "hostIPC": True,
+                },
+            },
+        },
+    }
+
+
+def addon_manifests(cfg: Dict[str, Any]) -> List[Tuple[str, Dict[str, Any]]]:
+    """``(api collection path, object)`` pairs for the MI355X add-on module."""
+    out = [
+        (f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
+         device_plugin_daemonset(cfg.get("device_plugin_image") or "rocm/k8s-device-plugin:latest")),
+        (f"/api/v1/namespaces/{NAMESPACE}/configmaps", rccl_configmap()),
+    ]
+    if cfg.get("node_labeller_image"):
+        out.append((f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
+                    labeller_daemonset(cfg["node_labeller_image"])))
+    if str(cfg.get("rccl_gate", "false")).lower() == "true" and cfg.get("rccl_probe_image"):
+        out.append(("/apis/batch/v1/namespaces/default/jobs",
+                    gpu_job_manifest("rccl-ready", cfg["rccl_probe_image"], ["/opt/triton-kubernetes/bin/rccl-ready"])))
+    return out
+
+
+def apply_manifests(client, cluster_id: str, manifests: List[Tuple[str, Dict[str, Any]]]) -> List[str]:
+    """Create each object (PUT on 409 AlreadyExists) through Rancher's k8s proxy."""
+    applied = []
+    for path, obj in manifests:
+        name = obj["metadata"]["name"]
+        try:
+            client.k8s(cluster_id, "POST", path, obj, ok=(200, 201, 202))
+        except TKError as exc:
+            if getattr(exc, "status", None) == 409:
+                client.k8s(cluster_id, "PUT", f"{path}/{name}", obj, ok=(200, 201))
+            else:
+                raise
+        applied.append(f"{obj['kind']}/{name}")
+    return applied

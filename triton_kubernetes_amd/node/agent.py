@@ -32,6 +32,7 @@ import base64
 import hmac
 import http.server
 import json
+import socket
 import os
 import re
 import secrets
@@ -285,6 +286,11 @@ class NodeAgent:
         class H(http.server.BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
 
+            def setup(self):
+                super().setup()
+                # one request/response per segment: no Nagle/delayed-ACK stalls on keep-alive
+                self.request.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
+
             def log_message(self, *args):
                 pass
 
@@ -319,6 +325,10 @@ class NodeAgent:
                     body = self._body()
                     if path == "/v1/plan":
                         return self._reply(200, agent.run_plan(BootstrapPlan.from_json(body["plan"])))
+                    if path == "/v1/rccl-uid":
+                        from ..ops import rccl
+
+                        return self._reply(200, {"uid": base64.b64encode(rccl.unique_id()).decode()})
                     if path == "/v1/rccl-gate":
                         uid = base64.b64decode(body["uid"])
                         return self._reply(200, agent.rccl_gate(int(body["rank"]), int(body["world"]), uid,

@@ -1,0 +1,83 @@
+"""Manager-host scripts for the DirectExecutor's SSH path.
+
+Re-designs of the reference's manager bootstrap (S1-S3,
+``terraform/modules/files/*.sh.tpl``) for a current Rancher 2.x:
+
+* install the container runtime only if absent (the reference always pipes a
+  pinned 17.03 installer into ``sh``), data-root on ``/mnt/docker`` only when
+  that mount exists (the reference hard-codes ``/home/ubuntu``, Q10);
+* ``docker run rancher/rancher`` — polling with a 1 s interval instead of 5 s;
+* :func:`manager_setup_script` is the on-host variant of S3 used with
+  ``rancher_bootstrap: remote`` (operator cannot reach port 443).
+"""
+
+import json
+import shlex
+from typing import Any, Dict
+
+DEFAULT_DOCKER_INSTALL_URL = "https://releases.rancher.com/install-docker/20.10.sh"
+DEFAULT_SERVER_IMAGE = "rancher/rancher:v2.8.5"
+
+
+def _q(v: Any) -> str:
+    return shlex.quote(str(v))
+
+
+def manager_install_script(cfg: Dict[str, Any]) -> str:
+    url = cfg.get("docker_engine_install_url") or DEFAULT_DOCKER_INSTALL_URL
+    image = cfg.get("rancher_server_image") or DEFAULT_SERVER_IMAGE
+    reg, user, pw = (cfg.get("rancher_registry", ""), cfg.get("rancher_registry_username", ""),
+                     cfg.get("rancher_registry_password", ""))
+    login = f"echo {_q(pw)} | sudo docker login -u {_q(user)} --password-stdin {_q(reg)}\n" if user else ""
+    return f"""#!/bin/bash
+set -euo pipefail
+if command -v firewalld >/dev/null 2>&1; then sudo systemctl disable --now firewalld.service || true; fi
+if ! command -v docker >/dev/null 2>&1; then curl -fsSL {_q(url)} | sudo sh; fi
+if mountpoint -q /mnt && [ ! -f /etc/docker/daemon.json ]; then
+  echo '{{"storage-driver": "overlay2", "data-root": "/mnt/docker"}}' | sudo tee /etc/docker/daemon.json >/dev/null
+  sudo systemctl restart docker
+fi
+{login}sudo docker pull {_q(image)}
+if ! sudo docker ps --format '{{{{.Image}}}}' | grep -qx {_q(image)}; then
+  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 {_q(image)}
+fi
+for i in $(seq 1 600); do
+  curl -ksf https://127.0.0.1/ping >/dev/null 2>&1 && exit 0
+  sleep 1
+done
+echo 'rancher server did not come up' >&2; exit 1
+"""
+
+
+def manager_setup_script(cfg: Dict[str, Any], server_url: str) -> str:
+    """On-host API bootstrap (S3); prints the token JSON as the last line."""
+    pw = cfg.get("rancher_admin_password", "")
+    token_req = json.dumps({"type": "token", "description": "Managed by triton-kubernetes",
+                            "name": "triton-kubernetes", "ttl": 0})
+    url_req = json.dumps({"name": "server-url", "value": server_url})
+    pw_req = json.dumps({"currentPassword": "admin", "newPassword": pw})
+    login_req = json.dumps({"username": "admin", "password": "admin", "ttl": 60000})
+    return f"""#!/bin/bash
+set -euo pipefail
+R=https://127.0.0.1
+login=$(curl -ksf -X POST -H 'Content-Type: application/json' -d {_q(login_req)} "$R/v3-public/localProviders/local?action=login")
+initial=$(printf '%s' "$login" | python3 -c 'import json,sys; print(json.load(sys.stdin)["token"])')
+tok=$(curl -ksf -u "$initial" -X POST -H 'Content-Type: application/json' -d {_q(token_req)} "$R/v3/token")
+printf '%s' "$tok" > ~/rancher_api_key && chmod 600 ~/rancher_api_key
+ak=$(printf '%s' "$tok" | python3 -c 'import json,sys; print(json.load(sys.stdin)["name"])')
+sk=$(printf '%s' "$tok" | python3 -c 'import json,sys; print(json.load(sys.stdin)["token"].split(":",1)[1])')
+curl -ksf -u "$ak:$sk" -X POST -H 'Content-Type: application/json' -d {_q(pw_req)} "$R/v3/users?action=changepassword" >/dev/null
+curl -ksf -u "$ak:$sk" -X PUT -H 'Content-Type: application/json' -d {_q(url_req)} "$R/v3/settings/server-url" >/dev/null
+printf '%s\\n' "$tok"
+"""
+
+
+def node_cleanup_script() -> str:
+    """Remove the Rancher agent and RKE state from a host."""
+    return """#!/bin/bash
+set -uo pipefail
+ids=$(sudo docker ps -aq --filter 'ancestor=rancher/rancher-agent' 2>/dev/null; sudo docker ps -aq --filter 'label=io.rancher.rke.container.name' 2>/dev/null)
+[ -n "$ids" ] && sudo docker rm -f $ids >/dev/null
+sudo rm -rf /etc/kubernetes /var/lib/rancher /var/lib/etcd /etc/cni /opt/cni /var/lib/cni /etc/triton-kubernetes
+exit 0
+"""

@@ -68,6 +68,8 @@ def targets() -> List[Target]:
     return [
         Target("libtk_gpu_probe.so", [probe],
                [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-fPIC", "-shared", probe, "-o", out("libtk_gpu_probe.so"), *RPATH]),
+        Target("gpu-burnin", [probe],
+               [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-DTK_PROBE_MAIN", probe, "-o", out("gpu-burnin"), *RPATH]),
         Target("libtk_rccl.so", [rccl],
                [hipcc, *HIP_FLAGS, "-fPIC", "-shared", rccl, "-o", out("libtk_rccl.so"), f"-L{ROCM}/lib",
                 "-lrccl", *RPATH]),

@@ -1,0 +1,254 @@
+"""Host transports used by the DirectExecutor's fan-out.
+
+===================  =============================================================
+``ssh`` (default)    ``ssh``/``scp`` subprocesses with connection multiplexing
+                     (ControlMaster) and optional ``ProxyJump`` through the
+                     bastion — Terraform's ``remote-exec`` equivalent (T16), which
+                     in the reference ignores the bastion for managers (Q11)
+``agent``            HTTP to a ``tk-node-agent`` (``agent+http://host:port``
+                     host strings); the agent runs plan steps natively
+``local``            runs the rendered script with ``bash`` on this machine
+                     (single-box development)
+``recording``        test double: records plans/scripts, scripted failures
+===================  =============================================================
+
+Every transport returns the same result document for a plan:
+``{"hostname", "ok", "error", "ms", "steps": [{name, ok, ms}], "labels", ...}``.
+"""
+
+import os
+import shlex
+import subprocess
+import tempfile
+import threading
+import time
+from dataclasses import dataclass, field
+from typing import Any, Callable, Dict, List, Optional
+
+from ..cloud.http import HTTPClient
+from ..errors import ExecutorError
+from ..node.plan import BootstrapPlan, parse_step_markers
+
+
+@dataclass
+class HostRef:
+    address: str
+    ssh_user: str = "ubuntu"
+    key_path: str = "~/.ssh/id_rsa"
+    bastion_host: str = ""
+    bastion_user: str = ""
+
+    @property
+    def scheme(self) -> str:
+        if self.address.startswith("agent+"):
+            return "agent"
+        if self.address in ("local", "localhost-exec"):
+            return "local"
+        return "ssh"
+
+    @property
+    def agent_url(self) -> str:
+        return self.address[len("agent+"):]
+
+
+class Transport:
+    name = "abstract"
+
+    def run_plan(self, host: HostRef, plan: BootstrapPlan, timeout: float = 3600) -> Dict[str, Any]:
+        raise NotImplementedError
+
+    def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
+        raise NotImplementedError
+
+    def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
+        raise NotImplementedError
+
+
+def _shell_result(plan: BootstrapPlan, output: str, rc: int, ms: float, err: str = "") -> Dict[str, Any]:
+    markers = parse_step_markers(output + "\n" + err)
+    steps = [{"name": n, "ok": m["status"] == "ok", "ms": m["ms"]} for n, m in markers.items()
+             if m["status"] != "start"]
+    failed = [n for n, m in markers.items() if m["status"] == "failed"]
+    ok = rc == 0 and "::tk-done" in output
+    return {"hostname": plan.hostname, "ok": ok, "ms": ms, "steps": steps,
+            "error": None if ok else f"step {failed[0] if failed else '?'} failed (rc={rc}): {err[-800:]}",
+            "labels": {}, "capacity": {}}
+
+
+class SSHTransport(Transport):
+    name = "ssh"
+
+    def __init__(self, strict_host_keys: bool = False, connect_timeout: int = 15, control_dir: Optional[str] = None,
+                 extra_opts: Optional[List[str]] = None):
+        self.strict = strict_host_keys
+        self.connect_timeout = connect_timeout
+        self.control_dir = control_dir or tempfile.mkdtemp(prefix="tk-ssh-")
+        self.extra = list(extra_opts or [])
+
+    def base_opts(self, host: HostRef) -> List[str]:
+        opts = ["-o", "BatchMode=yes", "-o", f"ConnectTimeout={self.connect_timeout}",
+                "-o", "ControlMaster=auto", "-o", f"ControlPath={self.control_dir}/%C",
+                "-o", "ControlPersist=120s", "-o", "ServerAliveInterval=15"]
+        if not self.strict:
+            opts += ["-o", "StrictHostKeyChecking=no", "-o", "UserKnownHostsFile=/dev/null", "-o", "LogLevel=ERROR"]
+        if host.key_path:
+            opts += ["-i", os.path.expanduser(host.key_path)]
+        if host.bastion_host:
+            user = host.bastion_user or host.ssh_user
+            opts += ["-J", f"{user}@{host.bastion_host}"]
+        return opts + self.extra
+
+    def ssh_argv(self, host: HostRef, remote_cmd: str) -> List[str]:
+        return ["ssh", *self.base_opts(host), f"{host.ssh_user}@{host.address}", remote_cmd]
+
+    def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
+        proc = subprocess.run(self.ssh_argv(host, "bash -s"), input=script, capture_output=True, text=True,
+                              timeout=timeout, check=False)
+        if proc.returncode != 0:
+            raise ExecutorError(f"ssh {host.ssh_user}@{host.address}: exit {proc.returncode}: "
+                                f"{proc.stderr[-800:]}")
+        return proc.stdout
+
+    def run_plan(self, host: HostRef, plan: BootstrapPlan, timeout: float = 3600) -> Dict[str, Any]:
+        t0 = time.perf_counter()
+        proc = subprocess.run(self.ssh_argv(host, "bash -s"), input=plan.render_shell(), capture_output=True,
+                              text=True, timeout=timeout, check=False)
+        return _shell_result(plan, proc.stdout, proc.returncode, (time.perf_counter() - t0) * 1e3, proc.stderr)
+
+    def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
+        dirname = os.path.dirname(remote_path)
+        self.run_script(host, f"sudo mkdir -p {shlex.quote(dirname)} && sudo chown \"$(id -un)\" "
+                              f"{shlex.quote(dirname)}\n")
+        proc = subprocess.run(["scp", "-q", *self.base_opts(host), local_path,
+                               f"{host.ssh_user}@{host.address}:{remote_path}"], capture_output=True, text=True,
+                              check=False)
+        if proc.returncode != 0:
+            raise ExecutorError(f"scp {local_path} -> {host.address}:{remote_path}: {proc.stderr[-500:]}")
+        self.run_script(host, f"chmod {mode:o} {shlex.quote(remote_path)}\n")
+
+
+class LocalTransport(Transport):
+    """Runs scripts with the local ``bash`` (development / single-box)."""
+
+    name = "local"
+
+    def __init__(self, env: Optional[Dict[str, str]] = None):
+        self.env = env
+
+    def _env(self) -> Dict[str, str]:
+        e = dict(os.environ)
+        e.update(self.env or {})
+        return e
+
+    def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
+        proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, timeout=timeout,
+                              env=self._env(), check=False)
+        if proc.returncode != 0:
+            raise ExecutorError(f"local script exit {proc.returncode}: {proc.stderr[-800:]}")
+        return proc.stdout
+
+    def run_plan(self, host: HostRef, plan: BootstrapPlan, timeout: float = 3600) -> Dict[str, Any]:
+        t0 = time.perf_counter()
+        proc = subprocess.run(["bash", "-s"], input=plan.render_shell(), capture_output=True, text=True,
+                              timeout=timeout, env=self._env(), check=False)
+        return _shell_result(plan, proc.stdout, proc.returncode, (time.perf_counter() - t0) * 1e3, proc.stderr)
+
+    def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
+        os.makedirs(os.path.dirname(remote_path), exist_ok=True)
+        with open(local_path, "rb") as src, open(remote_path, "wb") as dst:
+            dst.write(src.read())
+        os.chmod(remote_path, mode)
+
+
+class AgentTransport(Transport):
+    name = "agent"
+
+    def __init__(self, token: str = "", tokens: Optional[Dict[str, str]] = None, timeout: float = 3600):
+        self.token = token
+        self.tokens = dict(tokens or {})
+        self.timeout = timeout
+        self._clients: Dict[str, HTTPClient] = {}
+        self._mu = threading.Lock()
+
+    def _client(self, host: HostRef) -> HTTPClient:
+        url = host.agent_url
+        with self._mu:
+            c = self._clients.get(url)
+            if c is None:
+                tok = self.tokens.get(url, self.token)
+                c = HTTPClient(base_url=url, timeout=self.timeout, retries=1,
+                               default_headers={"X-TK-Agent-Token": tok})
+                self._clients[url] = c
+            return c
+
+    def run_plan(self, host: HostRef, plan: BootstrapPlan, timeout: float = 3600) -> Dict[str, Any]:
+        return self._client(host).post_json("/v1/plan", {"plan": plan.to_json()})
+
+    def post(self, host: HostRef, path: str, body: Dict[str, Any]) -> Dict[str, Any]:
+        return self._client(host).post_json(path, body)
+
+    def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
+        raise ExecutorError("the node agent does not execute shell scripts; use an agent plan or the ssh transport")
+
+    def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
+        return None  # agents run the native probes in-process; nothing to upload
+
+
+@dataclass
+class RecordingTransport(Transport):
+    """Test double: records every call; ``fail`` maps hostname -> error text."""
+
+    fail: Dict[str, str] = field(default_factory=dict)
+    delay: float = 0.0
+    on_plan: Optional[Callable[[HostRef, BootstrapPlan], Dict[str, Any]]] = None
+    name: str = "recording"
+
+    def __post_init__(self):
+        self.plans: List[BootstrapPlan] = []
+        self.scripts: List[str] = []
+        self.files: List[str] = []
+        self._mu = threading.Lock()
+
+    def run_plan(self, host: HostRef, plan: BootstrapPlan, timeout: float = 3600) -> Dict[str, Any]:
+        with self._mu:
+            self.plans.append(plan)
+        if self.delay:
+            time.sleep(self.delay)
+        if self.on_plan is not None:
+            return self.on_plan(host, plan)
+        if plan.hostname in self.fail:
+            return {"hostname": plan.hostname, "ok": False, "error": self.fail[plan.hostname], "steps": []}
+        return {"hostname": plan.hostname, "ok": True, "error": None, "ms": self.delay * 1e3,
+                "steps": [{"name": s.name, "ok": True, "ms": 0} for s in plan.steps], "labels": {}, "capacity": {}}
+
+    def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
+        with self._mu:
+            self.scripts.append(script)
+        return ""
+
+    def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
+        with self._mu:
+            self.files.append(remote_path)
+
+
+class TransportRouter(Transport):
+    """Dispatch by :attr:`HostRef.scheme`."""
+
+    name = "router"
+
+    def __init__(self, ssh: Optional[Transport] = None, agent: Optional[Transport] = None,
+                 local: Optional[Transport] = None):
+        self.routes = {"ssh": ssh or SSHTransport(), "agent": agent or AgentTransport(),
+                       "local": local or LocalTransport()}
+
+    def for_host(self, host: HostRef) -> Transport:
+        return self.routes[host.scheme]
+
+    def run_plan(self, host, plan, timeout=3600):
+        return self.for_host(host).run_plan(host, plan, timeout)
+
+    def run_script(self, host, script, timeout=3600):
+        return self.for_host(host).run_script(host, script, timeout)
+
+    def put_file(self, host, local_path, remote_path, mode=0o755):
+        return self.for_host(host).put_file(host, local_path, remote_path, mode)

@@ -22,6 +22,7 @@ Everything is in memory and thread-safe; it serves plain HTTP on 127.0.0.1.
 import base64
 import http.server
 import json
+import socket
 import threading
 import time
 import urllib.parse
@@ -137,6 +138,11 @@ class FakeRancher:
 
         class H(http.server.BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
+
+            def setup(self):
+                super().setup()
+                # one request/response per segment: no Nagle/delayed-ACK stalls on keep-alive
+                self.request.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
 
             def log_message(self, *args):  # quiet
                 pass

@@ -1,0 +1,187 @@
+"""create -> kubectl-ready waiter (new; the reference stops at agent launch,
+``create/cluster.go:277-289``, so it never measures or guarantees readiness).
+
+Phases, each time-stamped (the BASELINE.json metric is ``ready - start``):
+
+1. ``cluster_active``   Rancher reports the cluster ``active`` (RKE done);
+2. ``nodes_ready``      every expected node is in the Kubernetes node list with
+                        condition ``Ready=True`` (read through Rancher's k8s proxy);
+3. ``gpus_allocatable`` every MI355X node advertises ``amd.com/gpu`` equal to its
+                        expected count (device plugin up);
+4. ``rccl_gate``        optional: one RCCL all-reduce sweep across all GPU nodes
+                        (N2), run by the node agents as one communicator.
+
+Polling is adaptive (20 ms doubling to 1 s), not the reference's fixed 5 s.
+"""
+
+import base64
+import concurrent.futures as cf
+import json
+import time
+from dataclasses import asdict, dataclass, field
+from typing import Any, Dict, List, Optional
+
+from ..errors import TKError
+from ..rancher.client import RancherClient, wait_until
+from ..utils.trace import span
+
+
+@dataclass
+class ReadinessSpec:
+    cluster_id: str
+    nodes: List[str]
+    gpu_nodes: Dict[str, int] = field(default_factory=dict)  # hostname -> expected amd.com/gpu
+    timeout: float = 3600.0
+    rccl_gate: bool = False
+    rccl_hosts: List[str] = field(default_factory=list)  # agent URLs of GPU nodes, rank order
+    rccl_sizes: List[int] = field(default_factory=lambda: [1 << 20, 64 << 20])
+    rccl_iters: int = 5
+
+
+@dataclass
+class ReadinessReport:
+    start: float
+    phases: Dict[str, float] = field(default_factory=dict)
+    nodes: Dict[str, Dict[str, Any]] = field(default_factory=dict)
+    rccl: Optional[Dict[str, Any]] = None
+
+    @property
+    def ready_seconds(self) -> float:
+        return max(self.phases.values()) - self.start if self.phases else 0.0
+
+    def to_json(self) -> Dict[str, Any]:
+        d = asdict(self)
+        d["phase_seconds"] = {k: round(v - self.start, 4) for k, v in self.phases.items()}
+        d["ready_seconds"] = round(self.ready_seconds, 4)
+        return d
+
+
+def _node_ready(item: Dict[str, Any]) -> bool:
+    for c in (item.get("status") or {}).get("conditions", []) or []:
+        if c.get("type") == "Ready":
+            return c.get("status") == "True"
+    return False
+
+
+def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float] = None,
+               agent_transport: Any = None) -> ReadinessReport:
+    rep = ReadinessReport(start=start if start is not None else time.time())
+    deadline = rep.start + spec.timeout
+
+    def left() -> float:
+        return max(1.0, deadline - time.time())
+
+    with span("ready.cluster_active", cluster=spec.cluster_id):
+        wait_until(lambda: client.cluster_state(spec.cluster_id) == "active", left(),
+                   f"cluster {spec.cluster_id} to become active")
+    rep.phases["cluster_active"] = time.time()
+
+    want = set(spec.nodes)
+
+    def nodes_ready() -> Optional[Dict[str, Dict[str, Any]]]:
+        items = {i["metadata"]["name"]: i for i in client.k8s_nodes(spec.cluster_id)}
+        if not want.issubset(items) or not all(_node_ready(items[n]) for n in want):
+            return None
+        return items
+
+    with span("ready.nodes", count=len(want)):
+        items = wait_until(nodes_ready, left(), f"{len(want)} nodes Ready")
+    rep.phases["nodes_ready"] = time.time()
+
+    if spec.gpu_nodes:
+        def gpus() -> Optional[Dict[str, Dict[str, Any]]]:
+            got = {i["metadata"]["name"]: i for i in client.k8s_nodes(spec.cluster_id)}
+            for host, n in spec.gpu_nodes.items():
+                alloc = ((got.get(host) or {}).get("status") or {}).get("allocatable", {})
+                if str(alloc.get("amd.com/gpu", "0")) != str(n):
+                    return None
+            return got
+
+        with span("ready.gpus", nodes=len(spec.gpu_nodes)):
+            items = wait_until(gpus, left(), "amd.com/gpu allocatable on every GPU node")
+        rep.phases["gpus_allocatable"] = time.time()
+
+    for name in want:
+        it = items.get(name, {})
+        rep.nodes[name] = {"labels": (it.get("metadata") or {}).get("labels", {}),
+                           "allocatable": (it.get("status") or {}).get("allocatable", {})}
+
+    if spec.rccl_gate and spec.rccl_hosts:
+        with span("ready.rccl_gate", world=len(spec.rccl_hosts)):
+            rep.rccl = rccl_gate(agent_transport, spec.rccl_hosts, spec.rccl_sizes, spec.rccl_iters)
+        if not rep.rccl.get("ok"):
+            raise TKError(f"RCCL readiness gate failed: {rep.rccl}")
+        rep.phases["rccl_gate"] = time.time()
+    return rep
+
+
+def rccl_gate(transport: Any, agent_urls: List[str], sizes: List[int], iters: int = 5) -> Dict[str, Any]:
+    """One RCCL communicator across the GPU node agents (rank i = agent_urls[i])."""
+    from ..parallel.transport import HostRef
+
+    hosts = [HostRef("agent+" + u if not u.startswith("agent+") else u) for u in agent_urls]
+    uid = transport.post(hosts[0], "/v1/rccl-uid", {})["uid"]
+    world = len(hosts)
+
+    def one(i: int) -> Dict[str, Any]:
+        return transport.post(hosts[i], "/v1/rccl-gate",
+                              {"uid": uid, "rank": i, "world": world, "sizes": sizes, "iters": iters})
+
+    with cf.ThreadPoolExecutor(max_workers=world) as pool:
+        results = list(pool.map(one, range(world)))
+    ok = all(r.get("ok") for r in results)
+    busbw = [max(r.get("busbw_gbps") or [0.0]) for r in results]
+    return {"ok": ok, "world": world, "min_peak_busbw_gbps": min(busbw) if busbw else 0.0, "ranks": results}
+
+
+def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, rccl_gate: bool = False):
+    """Build the client + spec for a cluster from the document and the executor's tfstate."""
+    from ..executor.base import outputs_from_tfstate
+    from ..state import MANAGER_KEY
+    from ..terraform.catalog import module_from_source
+
+    raw = backend.read_tfstate(state.name)
+    mgr = outputs_from_tfstate(raw, MANAGER_KEY)
+    cl = outputs_from_tfstate(raw, cluster_key)
+    if not mgr.get("rancher_url") or not cl.get("rancher_cluster_id"):
+        raise TKError("cluster outputs unavailable; cannot wait for readiness")
+    client = RancherClient(mgr["rancher_url"], mgr.get("rancher_access_key", ""), mgr.get("rancher_secret_key", ""))
+    nodes = state.nodes(cluster_key)
+    from ..models.baremetal import addons_key
+    from ..state import cluster_key_parts
+
+    # amd.com/gpu only appears once the device plugin runs, i.e. with the add-on module
+    has_plugin = state.module(addons_key(cluster_key_parts(cluster_key)[1])) is not None
+    gpu_nodes: Dict[str, int] = {}
+    rccl_hosts: List[str] = []
+    for host in sorted(nodes):
+        cfg = state.module(nodes[host]) or {}
+        info = module_from_source(str(cfg.get("source", "")))
+        if info is not None and info.mi355x:
+            if has_plugin:
+                gpu_nodes[host] = int(cfg.get("gpu_count", 8))
+            addr = str(cfg.get("host", ""))
+            if addr.startswith("agent+"):
+                rccl_hosts.append(addr[len("agent+"):])
+    spec = ReadinessSpec(cl["rancher_cluster_id"], sorted(nodes), gpu_nodes, timeout,
+                         rccl_gate and bool(rccl_hosts), rccl_hosts)
+    return client, spec
+
+
+def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[float] = None) -> ReadinessReport:
+    s = ctx.settings
+    timeout = float(s.get_string("wait_timeout") or 3600)
+    client, spec = spec_from_state(state, backend, cluster_key, timeout, s.get_bool("rccl_gate"))
+    transport = ctx.extras.get("agent_transport")
+    if transport is None and spec.rccl_gate:
+        from ..parallel.transport import AgentTransport
+
+        transport = AgentTransport(token=s.get_string("agent_token"))
+    rep = wait_ready(client, spec, start=start, agent_transport=transport)
+    ctx.echo(f"cluster ready in {rep.ready_seconds:.2f}s: " +
+             json.dumps(rep.to_json()["phase_seconds"], sort_keys=True))
+    return rep
+
+
+__all__ = ["ReadinessSpec", "ReadinessReport", "wait_ready", "rccl_gate", "spec_from_state", "wait_after_create",
+           "base64"]
