@@ -1,0 +1,168 @@
+"""DirectExecutor end to end against the fake Rancher and sim-mode node agents.
+
+The executor path is the one ``bench.py`` times; here the GPU steps use a
+synthetic 8xMI355X topology and a stubbed burn-in so the test runs on CPU.
+"""
+
+import json
+import tempfile
+
+import pytest
+
+from triton_kubernetes_amd.backend import LocalBackend
+from triton_kubernetes_amd.errors import TKError
+from triton_kubernetes_amd.executor.direct import DirectExecutor, module_deps, resolve
+from triton_kubernetes_amd.node.agent import NodeAgent
+from triton_kubernetes_amd.node.labels import synthetic_topology
+from triton_kubernetes_amd.parallel.transport import AgentTransport, RecordingTransport, TransportRouter
+from triton_kubernetes_amd.rancher.client import RancherClient
+from triton_kubernetes_amd.rancher.fake import FakeRancher
+from triton_kubernetes_amd.workflows import delete_cluster, delete_node, get_cluster, get_manager, new_cluster
+from triton_kubernetes_amd.workflows import new_manager, new_node
+
+from helpers import make_ctx, output
+
+TOKEN = "test-token-123456"
+
+
+@pytest.fixture
+def env(tmp_path):
+    fake = FakeRancher().start()
+    agents = []
+
+    def agent(name, gpus=0, fail_burnin=False):
+        a = NodeAgent(name=name, mode="sim", devices=list(range(gpus)), token=TOKEN, root=tempfile.mkdtemp(),
+                      topology_override=synthetic_topology(gpus) if gpus else None,
+                      burnin_override=lambda d, l: {"ok": not fail_burnin, "failures": ["hbm"] if fail_burnin else []})
+        agents.append(a)
+        return "agent+" + a.serve()
+
+    backend = LocalBackend(str(tmp_path / "state"))
+    base = {"executor": "direct", "agent_token": TOKEN}
+    yield fake, agent, backend, base
+    for a in agents:
+        a.stop()
+    fake.stop()
+
+
+def _manager(fake, backend, base):
+    new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="s3cret",
+                              host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
+                backend)
+
+
+def _nodes(cp, workers, gpu=True, count=8):
+    return [
+        {"rancher_host_label": "control", "node_count": 1, "hostname": "cp", "ssh_user": "u", "bastion_host": "",
+         "key_path": "k", "hosts": [cp]},
+        {"rancher_host_label": "etcd", "node_count": 1, "hostname": "etcd", "ssh_user": "u", "bastion_host": "",
+         "key_path": "k", "hosts": [cp]},
+        {"rancher_host_label": "worker", "node_count": len(workers), "hostname": "gpu", "ssh_user": "u",
+         "bastion_host": "", "key_path": "k", "hosts": workers, **({"gpu": "mi355x", "gpu_count": count}
+                                                                    if gpu else {})},
+    ]
+
+
+def test_full_bringup_with_gpu_addons_and_wait(env):
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    assert fake.state.admin_password == "s3cret"  # S3: password changed
+    cp = agent("cp")
+    workers = [agent(f"w{i}", gpus=8) for i in range(3)]
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
+                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
+                        nodes=_nodes(cp, workers)))
+    new_cluster(ctx, backend)
+    out = output(ctx)
+    assert "3 nodes added: gpu-1, gpu-2, gpu-3" in out
+    assert "cluster ready in" in out and "gpus_allocatable" in out
+    cid = list(fake.state.clusters)[0]
+    nodes = {n["metadata"]["name"]: n for n in fake.k8s_nodes(cid)}
+    assert nodes["gpu-1"]["status"]["allocatable"]["amd.com/gpu"] == "8"
+    labels = nodes["gpu-2"]["metadata"]["labels"]
+    assert labels["amd.com/gpu.product-name"] == "MI355X"
+    assert labels["amd.com/xgmi.fully-connected"] == "true" and labels["amd.com/xgmi.links-per-gpu"] == "7"
+    assert fake.state.clusters[cid]["rancherKubernetesEngineConfig"]["network"]["plugin"] == "calico"
+    tf = json.loads(backend.read_tfstate("mgr"))
+    assert tf["module_state"]["addons_baremetal_dev"]["status"] == "ok"
+    assert json.loads(tf["module_outputs"]["node_baremetal_dev_gpu-1"]["gpu_node_labels"])["amd.com/gpu.count"] == "8"
+
+    # get manager / cluster work without terraform (tfstate written by the executor)
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev"))
+    get_cluster(ctx, backend)
+    assert f"rancher_cluster_id = {cid}" in output(ctx)
+    ctx = make_ctx(dict(base, cluster_manager="mgr"))
+    get_manager(ctx, backend)
+    assert f"rancher_url = {fake.url}" in output(ctx)
+
+    # re-apply on `create node`: only the new node runs, the rest is skipped
+    w4 = agent("w4", gpus=8)
+    new_node(make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", rancher_host_label="worker",
+                           node_count=1, hostname="gpu", ssh_user="u", bastion_host="", key_path="k", hosts=[w4],
+                           gpu="mi355x")), backend)
+    tf2 = json.loads(backend.read_tfstate("mgr"))
+    assert tf2["module_state"]["node_baremetal_dev_gpu-4"]["status"] == "ok"
+    assert tf2["module_state"]["node_baremetal_dev_gpu-1"]["applied_at"] == \
+        tf["module_state"]["node_baremetal_dev_gpu-1"]["applied_at"]
+
+    delete_node(make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", hostname="gpu-4")), backend)
+    assert "node_baremetal_dev_gpu-4" not in json.loads(backend.read_tfstate("mgr"))["module_outputs"]
+    delete_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", rancher_cleanup=True)), backend)
+    assert backend.state("mgr").clusters() == {}
+    assert fake.state.clusters == {}  # Q7 extension: Rancher object removed
+
+
+def test_failed_node_blocks_addons_and_resume(env):
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    cp = agent("cp")
+    good, bad = agent("good", gpus=8), agent("bad", gpus=8, fail_burnin=True)
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
+                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", gpu_addons=True,
+                        nodes=_nodes(cp, [good, bad])))
+    with pytest.raises(TKError) as exc:
+        new_cluster(ctx, backend)
+    assert "gpu_burnin" in str(exc.value) and "hbm" in str(exc.value)
+    tf = json.loads(backend.read_tfstate("mgr"))
+    assert tf["module_state"]["node_baremetal_dev_gpu-2"]["status"] == "failed"
+    assert tf["module_state"]["node_baremetal_dev_gpu-1"]["status"] == "ok"
+    assert "addons_baremetal_dev" not in tf["module_state"]  # blocked, never started
+    assert "cluster_baremetal_dev" in backend.state("mgr").clusters().values()  # persisted for resume
+
+
+def test_dag_and_interpolation_helpers():
+    cfg = {"a": "${module.cluster-manager.rancher_url}/x", "b": ["${module.cluster_b_c.rancher_cluster_id}"],
+           "c": {"d": 1}}
+    assert module_deps(cfg) == {"cluster-manager", "cluster_b_c"}
+    out = resolve(cfg, {"cluster-manager": {"rancher_url": "https://r"}, "cluster_b_c": {"rancher_cluster_id": "c-1"}})
+    assert out == {"a": "https://r/x", "b": ["c-1"], "c": {"d": 1}}
+    with pytest.raises(TKError):
+        resolve(cfg, {})
+
+
+def test_unsupported_module_and_parallel_fanout(env):
+    fake, agent, backend, base = env
+    from triton_kubernetes_amd.state import State
+
+    st = State("x")
+    st.add_cluster("aws", "c", {"source": "g//terraform/modules/aws-rancher-k8s?ref=m", "name": "c"})
+    with pytest.raises(TKError) as exc:
+        DirectExecutor(transport=RecordingTransport()).apply(st, backend)
+    assert "does not implement module" in str(exc.value)
+
+    # 40 hosts with a 0.2 s bootstrap each: concurrent fan-out, not Terraform's waves of 10
+    _manager(fake, backend, base)
+    client = RancherClient(fake.url)
+    rec = RecordingTransport(delay=0.2)
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="wide",
+                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel",
+                        nodes=[{"rancher_host_label": "worker", "node_count": 40, "hostname": "w", "ssh_user": "u",
+                                "bastion_host": "", "key_path": "k", "hosts": [f"10.1.0.{i}" for i in range(40)]}]))
+    ctx.extras["transport"] = TransportRouter(ssh=rec, agent=AgentTransport(token=TOKEN))
+    import time
+
+    t0 = time.time()
+    new_cluster(ctx, backend)
+    assert len(rec.plans) == 40
+    assert time.time() - t0 < 2.5, "node bootstrap must fan out concurrently"
+    assert client.ping()

@@ -207,6 +207,8 @@ class NodeAgent:
         if a == "rccl_local":
             if len(self.devices) < 2:
                 return {"skipped": "single GPU"}
+            if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
+                return {"simulated": True}
             from ..ops import rccl
 
             res = rccl.sweep_local(len(self.devices))
@@ -275,6 +277,10 @@ class NodeAgent:
         from ..ops import rccl
 
         dev = self.devices[0] if self.devices else 0
+        # the communicator teardown is not part of the readiness answer: it is
+        # joined in stop() (or by the next process-exit drain), not here
+        rccl.set_async_teardown(True)
+        self._used_rccl = True
         with span("node.rccl_gate", node=self.name, rank=rank, world=world):
             res = rccl.sweep_rank(rank, world, uid, dev, sizes, iters=iters, warmup=2)
         return res.to_json()
@@ -352,6 +358,10 @@ class NodeAgent:
             self._server.shutdown()
             self._server.server_close()
             self._server = None
+        if getattr(self, "_used_rccl", False):
+            from ..ops import rccl
+
+            rccl.drain()
 
 
 def main(argv: Optional[List[str]] = None) -> int:

@@ -22,13 +22,20 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
+#include <thread>
 #include <vector>
 
 static thread_local char g_err[512];
+static thread_local double g_last_init_ms = 0.0;
 extern "C" const char* tkr_last_error() { return g_err; }
+// Wall time of the calling thread's last communicator init (ms).
+extern "C" double tkr_last_init_ms() { return g_last_init_ms; }
 
 #define HIPCHECK(call)                                                                            \
   do {                                                                                            \
@@ -126,6 +133,51 @@ static int check(RankBufs& b, size_t count, int dtype, float want) {
   return 0;
 }
 
+static inline double ms_since(std::chrono::steady_clock::time_point t) {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t).count();
+}
+
+// Per-thread phase timings of the last tkr_sweep_rank: init, alloc, sweep, teardown (ms).
+static thread_local double g_phase_ms[4] = {0, 0, 0, 0};
+extern "C" double tkr_last_phase_ms(int phase) { return (phase >= 0 && phase < 4) ? g_phase_ms[phase] : -1.0; }
+
+// Communicator teardown (ncclCommDestroy joins RCCL's proxy threads and frees
+// its device resources; ~0.5 s measured on MI355X, longer than init) is not
+// part of the readiness answer.  With async teardown on, it runs on a
+// background thread after the verified result is returned; tkr_drain() joins
+// every pending teardown and must run before process exit.
+static std::mutex g_td_mu;
+static std::vector<std::thread> g_td;
+static std::atomic<int> g_async_teardown{0};
+extern "C" void tkr_set_async_teardown(int on) { g_async_teardown.store(on); }
+
+static void teardown(ncclComm_t comm, RankBufs b, int device) {
+  auto work = [comm, b, device]() mutable {
+    (void)hipSetDevice(device);
+    free_bufs(b);
+    ncclCommDestroy(comm);
+  };
+  if (g_async_teardown.load()) {
+    std::lock_guard<std::mutex> lk(g_td_mu);
+    g_td.emplace_back(work);
+    g_phase_ms[3] = 0.0;
+  } else {
+    const auto t = std::chrono::steady_clock::now();
+    work();
+    g_phase_ms[3] = ms_since(t);
+  }
+}
+
+extern "C" int tkr_drain() {
+  std::vector<std::thread> pending;
+  {
+    std::lock_guard<std::mutex> lk(g_td_mu);
+    pending.swap(g_td);
+  }
+  for (auto& t : pending) t.join();
+  return (int)pending.size();
+}
+
 static inline size_t elem_size(int dtype) { return dtype == 1 ? 2 : 4; }
 static inline ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclBfloat16 : ncclFloat32; }
 
@@ -138,11 +190,16 @@ extern "C" int tkr_sweep_rank(int rank, int world, const unsigned char* uid128, 
   ncclUniqueId id;
   memcpy(id.internal, uid128, NCCL_UNIQUE_ID_BYTES);
   ncclComm_t comm;
+  const auto t_init = std::chrono::steady_clock::now();
   NCCLCHECK(ncclCommInitRank(&comm, world, id, rank));
+  g_last_init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_init).count();
   size_t max_bytes = 0;
   for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
   RankBufs b;
+  auto t_phase = std::chrono::steady_clock::now();
   int rc = alloc_bufs(b, max_bytes);
+  g_phase_ms[1] = ms_since(t_phase);
+  t_phase = std::chrono::steady_clock::now();
   const float want = (float)world * (float)(world + 1) / 2.0f;
   for (int s = 0; rc == 0 && s < nsizes; ++s) {
     const size_t count = sizes[s] / elem_size(dtype);
@@ -171,8 +228,9 @@ extern "C" int tkr_sweep_rank(int rank, int world, const unsigned char* uid128, 
     busbw[s] = algbw[s] * (world > 1 ? 2.0 * (world - 1) / world : 1.0);
     errors[s] = (double)bad;
   }
-  free_bufs(b);
-  ncclCommDestroy(comm);
+  g_phase_ms[2] = ms_since(t_phase);
+  g_phase_ms[0] = g_last_init_ms;
+  teardown(comm, b, device);
   return rc;
 }
 
@@ -184,7 +242,9 @@ extern "C" int tkr_sweep_local(int ndev, const size_t* sizes, int nsizes, int it
   std::vector<int> devs(ndev);
   for (int d = 0; d < ndev; ++d) devs[d] = d;
   std::vector<ncclComm_t> comms(ndev);
+  const auto t_init = std::chrono::steady_clock::now();
   NCCLCHECK(ncclCommInitAll(comms.data(), ndev, devs.data()));
+  g_last_init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_init).count();
   size_t max_bytes = 0;
   for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
   std::vector<RankBufs> bufs(ndev);

@@ -21,6 +21,10 @@ def _lib():
     lib = load("libtk_rccl.so")
     lib.tkr_last_error.restype = ctypes.c_char_p
     lib.tkr_unique_id.argtypes = [ctypes.c_char_p]
+    lib.tkr_last_init_ms.restype = ctypes.c_double
+    lib.tkr_last_phase_ms.restype = ctypes.c_double
+    lib.tkr_last_phase_ms.argtypes = [ctypes.c_int]
+    lib.tkr_set_async_teardown.argtypes = [ctypes.c_int]
     dp = ctypes.POINTER(ctypes.c_double)
     lib.tkr_sweep_rank.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -51,6 +55,8 @@ class SweepResult:
     algbw_gbps: List[float] = field(default_factory=list)
     busbw_gbps: List[float] = field(default_factory=list)
     errors: List[int] = field(default_factory=list)
+    init_ms: float = 0.0  # communicator init wall time
+    phase_ms: Dict[str, float] = field(default_factory=dict)  # init / alloc / sweep / teardown
 
     @property
     def ok(self) -> bool:
@@ -80,7 +86,21 @@ def sweep_rank(rank: int, world: int, uid: bytes, device: int, sizes: Sequence[i
                                t, alg, bus, err)
     if rc != 0:
         raise RCCLError(f"rank {rank}/{world}: {_lib().tkr_last_error().decode()}")
-    return SweepResult(world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err])
+    lib = _lib()
+    phases = {name: round(float(lib.tkr_last_phase_ms(i)), 3)
+              for i, name in enumerate(("init", "alloc", "sweep", "teardown"))}
+    return SweepResult(world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
+                       float(lib.tkr_last_init_ms()), phases)
+
+
+def set_async_teardown(on: bool) -> None:
+    """Run communicator teardown off the caller's critical path (see ``teardown`` in the HIP source)."""
+    _lib().tkr_set_async_teardown(1 if on else 0)
+
+
+def drain() -> int:
+    """Join pending asynchronous teardowns; call before the process exits."""
+    return int(_lib().tkr_drain())
 
 
 def sweep_local(ndev: int, sizes: Sequence[int] = DEFAULT_SIZES, iters: int = 10, warmup: int = 3,
@@ -91,7 +111,8 @@ def sweep_local(ndev: int, sizes: Sequence[int] = DEFAULT_SIZES, iters: int = 10
     rc = _lib().tkr_sweep_local(ndev, sz, n, iters, warmup, 1 if dtype == "bf16" else 0, t, alg, bus, err)
     if rc != 0:
         raise RCCLError(_lib().tkr_last_error().decode())
-    return SweepResult(ndev, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err])
+    return SweepResult(ndev, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
+                       float(_lib().tkr_last_init_ms()))
 
 
 def min_busbw_threshold(world: int, fraction: float = 0.5) -> float:
