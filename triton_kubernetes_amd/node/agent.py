@@ -279,10 +279,9 @@ class NodeAgent:
         dev = self.devices[0] if self.devices else 0
         # the communicator teardown is not part of the readiness answer: it is
         # joined in stop() (or by the next process-exit drain), not here
-        rccl.set_async_teardown(True)
         self._used_rccl = True
         with span("node.rccl_gate", node=self.name, rank=rank, world=world):
-            res = rccl.sweep_rank(rank, world, uid, dev, sizes, iters=iters, warmup=2)
+            res = rccl.sweep_rank(rank, world, uid, dev, sizes, iters=iters, warmup=2, async_teardown=True)
         return res.to_json()
 
     # --- HTTP server ----------------------------------------------------------------------------

@@ -1,5 +1,6 @@
 """Python front-end of the RCCL readiness probe (N2, ``csrc/tk_rccl_probe.hip``)."""
 
+import atexit
 import ctypes
 from dataclasses import asdict, dataclass, field
 from typing import Dict, List, Sequence
@@ -11,6 +12,9 @@ DEFAULT_SIZES = [1 << 20, 16 << 20, 256 << 20]
 # MI355X: 7 xGMI links x ~153 GB/s per GPU; ring all-reduce is per-link bound.
 XGMI_LINK_GBPS = 153.0
 XGMI_LINKS_PER_GPU = 7
+
+
+_ATEXIT = False
 
 
 class RCCLError(RuntimeError):
@@ -31,6 +35,10 @@ def _lib():
                                    ctypes.c_int, dp, dp, dp, dp]
     lib.tkr_sweep_local.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, dp, dp, dp, dp]
+    global _ATEXIT
+    if not _ATEXIT:
+        atexit.register(lib.tkr_drain)  # join async teardowns before interpreter exit
+        _ATEXIT = True
     return lib
 
 
@@ -78,12 +86,19 @@ def _arrays(n: int):
 
 
 def sweep_rank(rank: int, world: int, uid: bytes, device: int, sizes: Sequence[int] = DEFAULT_SIZES,
-               iters: int = 10, warmup: int = 3, dtype: str = "f32") -> SweepResult:
+               iters: int = 10, warmup: int = 3, dtype: str = "f32", async_teardown: bool = False) -> SweepResult:
+    """One rank of a multi-process sweep.  ``async_teardown`` moves the
+    communicator destroy (~0.5 s) off this call; :func:`drain` joins it."""
     n = len(sizes)
     sz = (ctypes.c_size_t * n)(*sizes)
     t, alg, bus, err = _arrays(n)
-    rc = _lib().tkr_sweep_rank(rank, world, uid, device, sz, n, iters, warmup, 1 if dtype == "bf16" else 0,
-                               t, alg, bus, err)
+    lib = _lib()
+    lib.tkr_set_async_teardown(1 if async_teardown else 0)  # thread-local in the library
+    try:
+        rc = lib.tkr_sweep_rank(rank, world, uid, device, sz, n, iters, warmup, 1 if dtype == "bf16" else 0,
+                                t, alg, bus, err)
+    finally:
+        lib.tkr_set_async_teardown(0)
     if rc != 0:
         raise RCCLError(f"rank {rank}/{world}: {_lib().tkr_last_error().decode()}")
     lib = _lib()

@@ -1,0 +1,1242 @@
+"""Generator of the Terraform module library (``terraform/modules/*``).
+
+The 19 modules are data here and written out as plain HCL files (committed;
+``tests/test_terraform_modules.py`` checks that they are in sync with this
+generator and internally consistent).  Run ``python -m
+triton_kubernetes_amd.terraform.generate`` after editing.
+
+Design (rewritten for Terraform >= 1.x and a current Rancher):
+
+* managers (T1-T5): VM (or the bare-metal host) -> docker via user-data or
+  remote-exec -> Rancher server -> API bootstrap on the host -> API key read
+  back with a ``data "external"`` SSH program (replaces ``matti/outputs/shell``);
+* clusters (T6-T11): ``data "external"`` find-or-create of the RKE cluster
+  (S4) + the provider network the hosts join;
+* hosts (T12-T17): the agent bootstrap (S5) as user-data / remote-exec, the
+  reference's ``control`` -> ``controlplane`` role mapping, optional data disks
+  (the GCP disk is now attached, Q15; vSphere CPU/memory are variables, Q15);
+* ``bare-metal-mi355x-rancher-k8s-host`` and ``rancher-k8s-mi355x-addons``.
+
+Every module pins ``required_version >= 1.3`` and its providers'
+sources (``joyent/triton``, ``hashicorp/aws|google|azurerm|vsphere|external``).
+"""
+
+import json
+import os
+import shutil
+import sys
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Sequence, Tuple
+
+from ..k8s.manifests import device_plugin_daemonset, labeller_daemonset, rccl_configmap, NAMESPACE
+from . import scripts
+from .catalog import MODULES_DIR
+
+CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ops", "csrc")
+
+DOCKER_URL = "https://releases.rancher.com/install-docker/24.0.sh"
+SERVER_IMAGE = "rancher/rancher:v2.8.5"
+AGENT_IMAGE = "rancher/rancher-agent:v2.8.5"
+
+PROVIDERS = {
+    "triton": ('triton = {\n      source  = "joyent/triton"\n      version = ">= 0.8"\n    }',
+               'provider "triton" {\n  account      = var.triton_account\n  key_material = file(pathexpand(var.triton_key_path))\n  key_id       = var.triton_key_id\n  url          = var.triton_url\n}'),
+    "aws": ('aws = {\n      source  = "hashicorp/aws"\n      version = ">= 4.0"\n    }',
+            'provider "aws" {\n  access_key = var.aws_access_key\n  secret_key = var.aws_secret_key\n  region     = var.aws_region\n}'),
+    "gcp": ('google = {\n      source  = "hashicorp/google"\n      version = ">= 4.0"\n    }',
+            'provider "google" {\n  credentials = file(pathexpand(var.gcp_path_to_credentials))\n  project     = var.gcp_project_id\n  region      = var.gcp_compute_region\n}'),
+    "azure": ('azurerm = {\n      source  = "hashicorp/azurerm"\n      version = ">= 3.0"\n    }',
+              'provider "azurerm" {\n  features {}\n  subscription_id = var.azure_subscription_id\n  client_id       = var.azure_client_id\n  client_secret   = var.azure_client_secret\n  tenant_id       = var.azure_tenant_id\n  environment     = var.azure_environment\n}'),
+    "vsphere": ('vsphere = {\n      source  = "hashicorp/vsphere"\n      version = ">= 2.0"\n    }',
+                'provider "vsphere" {\n  user                 = var.vsphere_user\n  password             = var.vsphere_password\n  vsphere_server       = var.vsphere_server\n  allow_unverified_ssl = true\n}'),
+    "external": ('external = {\n      source  = "hashicorp/external"\n      version = ">= 2.0"\n    }', ""),
+}
+
+
+@dataclass
+class Var:
+    name: str
+    default: Any = None  # None -> required
+    description: str = ""
+    type: Optional[str] = None
+    sensitive: bool = False
+
+    def hcl(self) -> str:
+        lines = [f'variable "{self.name}" {{']
+        if self.type:
+            lines.append(f"  type        = {self.type}")
+        if self.description:
+            lines.append(f"  description = {json.dumps(self.description)}")
+        if self.default is not None:
+            lines.append(f"  default     = {hcl_value(self.default)}")
+        if self.sensitive:
+            lines.append("  sensitive   = true")
+        lines.append("}")
+        return "\n".join(lines)
+
+
+@dataclass
+class Module:
+    name: str
+    providers: Sequence[str]
+    variables: List[Var]
+    main: str
+    outputs: List[Tuple[str, str, bool]]  # name, expression, sensitive
+    files: Dict[str, str] = field(default_factory=dict)  # filename -> content
+    copies: Dict[str, str] = field(default_factory=dict)  # filename -> source path to copy
+
+
+def hcl_value(v: Any, indent: int = 0) -> str:
+    pad = "  " * indent
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, (int, float)):
+        return json.dumps(v)
+    if isinstance(v, str):
+        return json.dumps(v).replace("${", "$${").replace("%{", "%%{")
+    if isinstance(v, list):
+        if not v:
+            return "[]"
+        inner = ",\n".join(f"{pad}  {hcl_value(x, indent + 1)}" for x in v)
+        return "[\n" + inner + f"\n{pad}]"
+    if isinstance(v, dict):
+        if not v:
+            return "{}"
+        inner = "\n".join(f"{pad}  {json.dumps(k)} = {hcl_value(x, indent + 1)}" for k, x in v.items())
+        return "{\n" + inner + f"\n{pad}}}"
+    raise TypeError(type(v))
+
+
+# --- variable sets ---------------------------------------------------------------------------
+def _rancher_image_vars(server: bool = True) -> List[Var]:
+    out = [Var("docker_engine_install_url", DOCKER_URL, "The URL to the shell script to install the docker engine.")]
+    if server:
+        out.append(Var("rancher_server_image", SERVER_IMAGE, "The Rancher Server image to use."))
+    out.append(Var("rancher_agent_image", AGENT_IMAGE, "The Rancher Agent image to use."))
+    out += [Var("rancher_registry", "", "The docker registry to use for rancher server and agent images"),
+            Var("rancher_registry_username", "", "The username to login as."),
+            Var("rancher_registry_password", "", "The password to use.", sensitive=True)]
+    return out
+
+
+MANAGER_BASE = [Var("name", None, "Human readable name used as prefix to generated names."),
+                Var("rancher_admin_password", None, "The Rancher admin password", sensitive=True)]
+CLUSTER_BASE = [
+    Var("name", None, "Human readable name used as prefix to generated names."),
+    Var("rancher_api_url", None), Var("rancher_access_key", None), Var("rancher_secret_key", None, sensitive=True),
+    Var("k8s_version", "v1.9.5-rancher1-1"), Var("k8s_network_provider", "flannel"),
+    Var("rancher_registry", ""), Var("rancher_registry_username", ""), Var("rancher_registry_password", "", sensitive=True),
+    Var("k8s_registry", ""), Var("k8s_registry_username", ""), Var("k8s_registry_password", "", sensitive=True),
+]
+HOST_BASE = [
+    Var("hostname", None), Var("rancher_api_url", None),
+    Var("rancher_cluster_registration_token", None, sensitive=True), Var("rancher_cluster_ca_checksum", None),
+    Var("rancher_host_labels", None, "A single-key map: {worker|etcd|control = \"true\"}", "map(string)"),
+] + _rancher_image_vars(server=False)
+
+TRITON_CREDS = [Var("triton_account", None), Var("triton_key_path", None), Var("triton_key_id", None),
+                Var("triton_url", "https://us-east-1.api.joyent.com")]
+AWS_CREDS = [Var("aws_access_key", None), Var("aws_secret_key", None, sensitive=True), Var("aws_region", None)]
+GCP_CREDS = [Var("gcp_path_to_credentials", None), Var("gcp_compute_region", None), Var("gcp_project_id", None)]
+AZURE_CREDS = [Var("azure_subscription_id", ""), Var("azure_client_id", ""), Var("azure_client_secret", "", sensitive=True),
+               Var("azure_tenant_id", ""), Var("azure_environment", "public"), Var("azure_location", "westus2")]
+AZURE_IMAGE = [Var("azure_image_publisher", "Canonical"), Var("azure_image_offer", "0001-com-ubuntu-server-jammy"),
+               Var("azure_image_sku", "22_04-lts-gen2"), Var("azure_image_version", "latest")]
+VSPHERE_CREDS = [Var("vsphere_user", None), Var("vsphere_password", None, sensitive=True), Var("vsphere_server", None)]
+VSPHERE_NAMES = [Var("vsphere_datacenter_name", None), Var("vsphere_datastore_name", None),
+                 Var("vsphere_resource_pool_name", None), Var("vsphere_network_name", None)]
+
+RKE_PORTS = [(22, 22), (80, 80), (443, 443), (2376, 2376), (2379, 2380), (6443, 6443), (8472, 8472),
+             (9099, 9099), (10250, 10252), (10254, 10256), (30000, 32767)]
+
+ROLE_LOCAL = """locals {
+  rancher_node_role_raw = keys(var.rancher_host_labels)[0]
+  rancher_node_role     = local.rancher_node_role_raw == "control" ? "controlplane" : local.rancher_node_role_raw
+}"""
+
+MANAGER_OUTPUTS = [
+    ("rancher_url", '"https://${local.rancher_master_ip}"', False),
+    ("rancher_access_key", "data.external.rancher_api_key.result.access_key", False),
+    ("rancher_secret_key", "data.external.rancher_api_key.result.secret_key", True),
+]
+CLUSTER_OUTPUTS = [
+    ("rancher_cluster_id", "data.external.rancher_cluster.result.cluster_id", False),
+    ("rancher_cluster_registration_token", "data.external.rancher_cluster.result.registration_token", True),
+    ("rancher_cluster_ca_checksum", "data.external.rancher_cluster.result.ca_checksum", False),
+]
+
+
+def _manager_tail(connection: str, install_docker_remote: bool) -> str:
+    """Rancher server install + bootstrap + API key read-back (shared by T1-T5)."""
+    docker = ""
+    after = ""
+    if install_docker_remote:
+        docker = f'''
+resource "terraform_data" "install_docker" {{
+  triggers_replace = [local.rancher_master_id]
+{connection}
+  provisioner "remote-exec" {{
+    inline = [templatefile("${{path.module}}/files/install_docker.sh.tftpl", {{
+      docker_engine_install_url = var.docker_engine_install_url
+      rancher_server_image      = var.rancher_server_image
+      rancher_registry          = var.rancher_registry
+      rancher_registry_username = var.rancher_registry_username
+      rancher_registry_password = var.rancher_registry_password
+    }})]
+  }}
+}}
+'''
+        after = "\n  depends_on       = [terraform_data.install_docker]"
+    return docker + f'''
+resource "terraform_data" "install_rancher_master" {{
+  triggers_replace = [local.rancher_master_id]{after}
+{connection}
+  provisioner "remote-exec" {{
+    inline = [templatefile("${{path.module}}/files/install_rancher_server.sh.tftpl", {{
+      rancher_server_image = var.rancher_server_image
+    }})]
+  }}
+}}
+
+resource "terraform_data" "setup_rancher_k8s" {{
+  triggers_replace = [local.rancher_master_id]
+  depends_on       = [terraform_data.install_rancher_master]
+{connection}
+  provisioner "remote-exec" {{
+    inline = [templatefile("${{path.module}}/files/setup_rancher.sh.tftpl", {{
+      rancher_host           = "https://127.0.0.1"
+      host_registration_url  = "https://${{local.rancher_master_ip}}"
+      rancher_admin_password = var.rancher_admin_password
+    }})]
+  }}
+}}
+
+# The API key written by setup_rancher is read back over SSH.
+data "external" "rancher_api_key" {{
+  depends_on = [terraform_data.setup_rancher_k8s]
+  program    = ["bash", "${{path.module}}/files/read_api_key.sh"]
+  query = {{
+    host         = local.rancher_master_ip
+    ssh_user     = local.ssh_user
+    key_path     = local.key_path
+    bastion_host = local.bastion_host
+  }}
+}}
+'''
+
+
+def _connection(host: str = "local.rancher_master_ip", user: str = "local.ssh_user", key: str = "local.key_path",
+                bastion: Optional[str] = "local.bastion_host") -> str:
+    lines = ["  connection {", '    type        = "ssh"', f"    user        = {user}", f"    host        = {host}",
+             f"    private_key = file(pathexpand({key}))"]
+    if bastion:
+        lines.append(f"    bastion_host = {bastion} == \"\" ? null : {bastion}")
+    lines.append("  }")
+    return "\n".join(lines)
+
+
+def _docker_userdata(server: bool) -> str:
+    image = "var.rancher_server_image" if server else '""'
+    return f'''templatefile("${{path.module}}/files/install_docker.sh.tftpl", {{
+    docker_engine_install_url = var.docker_engine_install_url
+    rancher_server_image      = {image}
+    rancher_registry          = var.rancher_registry
+    rancher_registry_username = var.rancher_registry_username
+    rancher_registry_password = var.rancher_registry_password
+  }})'''
+
+
+def _agent_userdata(disk_device: str = '""', disk_mount: str = '""', extra: str = '""') -> str:
+    return f'''templatefile("${{path.module}}/files/install_rancher_agent.sh.tftpl", {{
+    hostname                           = var.hostname
+    docker_engine_install_url          = var.docker_engine_install_url
+    rancher_api_url                    = var.rancher_api_url
+    rancher_cluster_registration_token = var.rancher_cluster_registration_token
+    rancher_cluster_ca_checksum        = var.rancher_cluster_ca_checksum
+    rancher_node_role                  = local.rancher_node_role
+    rancher_agent_image                = var.rancher_agent_image
+    rancher_registry                   = var.rancher_registry
+    rancher_registry_username          = var.rancher_registry_username
+    rancher_registry_password          = var.rancher_registry_password
+    disk_device                        = {disk_device}
+    disk_mount_path                    = {disk_mount}
+    extra_agent_args                   = {extra}
+  }})'''
+
+
+def _cluster_data(extra_query: str = "") -> str:
+    return f'''data "external" "rancher_cluster" {{
+  program = ["bash", "${{path.module}}/files/rancher_cluster.sh"]
+  query = {{
+    rancher_api_url       = var.rancher_api_url
+    rancher_access_key    = var.rancher_access_key
+    rancher_secret_key    = var.rancher_secret_key
+    name                  = var.name
+    k8s_version           = var.k8s_version
+    k8s_network_provider  = var.k8s_network_provider
+    k8s_registry          = var.k8s_registry
+    k8s_registry_username = var.k8s_registry_username
+    k8s_registry_password = var.k8s_registry_password{extra_query}
+  }}
+}}
+'''
+
+
+MANAGER_FILES = {"install_docker.sh.tftpl": scripts.INSTALL_DOCKER,
+                 "install_rancher_server.sh.tftpl": scripts.INSTALL_RANCHER_SERVER,
+                 "setup_rancher.sh.tftpl": scripts.SETUP_RANCHER, "read_api_key.sh": scripts.READ_API_KEY}
+CLUSTER_FILES = {"rancher_cluster.sh": scripts.RANCHER_CLUSTER}
+HOST_FILES = {"install_rancher_agent.sh.tftpl": scripts.INSTALL_RANCHER_AGENT}
+
+
+def _sg_rules(self_only: bool) -> str:
+    out = []
+    for lo, hi in RKE_PORTS:
+        src = "self = true" if self_only else 'cidr_blocks = ["0.0.0.0/0"]'
+        out.append(f"""  ingress {{
+    from_port = {lo}
+    to_port   = {hi}
+    protocol  = "tcp"
+    {src}
+  }}""")
+    out.append("""  ingress {
+    from_port = 8472
+    to_port   = 8472
+    protocol  = "udp"
+    self      = true
+  }
+  egress {
+    from_port   = 0
+    to_port     = 0
+    protocol    = "-1"
+    cidr_blocks = ["0.0.0.0/0"]
+  }""")
+    return "\n".join(out)
+
+
+# --- module definitions ---------------------------------------------------------------------------------
+def modules() -> List[Module]:
+    mods: List[Module] = []
+
+    # T1 triton-rancher
+    mods.append(Module("triton-rancher", ["triton", "external"],
+                       MANAGER_BASE + _rancher_image_vars() + TRITON_CREDS + [
+                           Var("triton_network_names", ["Joyent-SDC-Public"], type="list(string)"),
+                           Var("triton_image_name", "ubuntu-certified-22.04"), Var("triton_image_version", None),
+                           Var("triton_ssh_user", "ubuntu"),
+                           Var("master_triton_machine_package", "k4-highcpu-kvm-3.75G")],
+                       f'''data "triton_network" "networks" {{
+  count = length(var.triton_network_names)
+  name  = var.triton_network_names[count.index]
+}}
+
+data "triton_image" "image" {{
+  name        = var.triton_image_name
+  version     = var.triton_image_version
+  most_recent = true
+}}
+
+resource "triton_machine" "rancher_master" {{
+  package     = var.master_triton_machine_package
+  image       = data.triton_image.image.id
+  name        = var.name
+  user_script = {_docker_userdata(True)}
+  networks    = data.triton_network.networks[*].id
+  cns {{
+    services = [var.name]
+  }}
+  affinity = ["role!=~gcm"]
+  tags = {{
+    role = "gcm"
+  }}
+}}
+
+locals {{
+  rancher_master_id = triton_machine.rancher_master.id
+  rancher_master_ip = triton_machine.rancher_master.primaryip
+  ssh_user          = var.triton_ssh_user
+  key_path          = var.triton_key_path
+  bastion_host      = ""
+}}
+''' + _manager_tail(_connection(), False), MANAGER_OUTPUTS, dict(MANAGER_FILES)))
+
+    # T2 aws-rancher
+    mods.append(Module("aws-rancher", ["aws", "external"],
+                       MANAGER_BASE + _rancher_image_vars() + AWS_CREDS + [
+                           Var("aws_vpc_cidr", "10.0.0.0/16"), Var("aws_subnet_cidr", "10.0.2.0/24"),
+                           Var("aws_ami_id", None), Var("aws_instance_type", "t3.medium"), Var("aws_key_name", None),
+                           Var("aws_public_key_path", "~/.ssh/id_rsa.pub"), Var("aws_private_key_path", "~/.ssh/id_rsa"),
+                           Var("aws_ssh_user", "ubuntu")],
+                       f'''resource "aws_vpc" "default" {{
+  cidr_block           = var.aws_vpc_cidr
+  enable_dns_hostnames = true
+  tags = {{ Name = var.name }}
+}}
+
+resource "aws_internet_gateway" "default" {{
+  vpc_id = aws_vpc.default.id
+}}
+
+resource "aws_subnet" "public" {{
+  vpc_id                  = aws_vpc.default.id
+  cidr_block              = var.aws_subnet_cidr
+  map_public_ip_on_launch = true
+  depends_on              = [aws_internet_gateway.default]
+  tags = {{ Name = "${{var.name}}-public" }}
+}}
+
+resource "aws_route_table" "public" {{
+  vpc_id = aws_vpc.default.id
+  route {{
+    cidr_block = "0.0.0.0/0"
+    gateway_id = aws_internet_gateway.default.id
+  }}
+}}
+
+resource "aws_route_table_association" "public" {{
+  subnet_id      = aws_subnet.public.id
+  route_table_id = aws_route_table.public.id
+}}
+
+resource "aws_key_pair" "deployer" {{
+  count      = var.aws_public_key_path != "" ? 1 : 0
+  key_name   = var.aws_key_name
+  public_key = file(pathexpand(var.aws_public_key_path))
+}}
+
+resource "aws_security_group" "rancher" {{
+  name        = var.name
+  description = "Rancher server ${{var.name}}"
+  vpc_id      = aws_vpc.default.id
+  dynamic "ingress" {{
+    for_each = [22, 80, 443]
+    content {{
+      from_port   = ingress.value
+      to_port     = ingress.value
+      protocol    = "tcp"
+      cidr_blocks = ["0.0.0.0/0"]
+    }}
+  }}
+  egress {{
+    from_port   = 0
+    to_port     = 0
+    protocol    = "-1"
+    cidr_blocks = ["0.0.0.0/0"]
+  }}
+}}
+
+resource "aws_instance" "host" {{
+  ami                    = var.aws_ami_id
+  instance_type          = var.aws_instance_type
+  subnet_id              = aws_subnet.public.id
+  vpc_security_group_ids = [aws_security_group.rancher.id]
+  key_name               = var.aws_key_name
+  depends_on             = [aws_key_pair.deployer]
+  user_data              = {_docker_userdata(True)}
+  tags = {{ Name = var.name }}
+}}
+
+locals {{
+  rancher_master_id = aws_instance.host.id
+  rancher_master_ip = aws_instance.host.public_ip
+  ssh_user          = var.aws_ssh_user
+  key_path          = var.aws_private_key_path
+  bastion_host      = ""
+}}
+''' + _manager_tail(_connection(), False), MANAGER_OUTPUTS, dict(MANAGER_FILES)))
+
+    # T3 gcp-rancher
+    mods.append(Module("gcp-rancher", ["gcp", "external"],
+                       MANAGER_BASE + _rancher_image_vars() + GCP_CREDS + [
+                           Var("gcp_machine_type", "n1-standard-2"), Var("gcp_instance_zone", None),
+                           Var("gcp_image", "ubuntu-os-cloud/ubuntu-2204-lts"), Var("gcp_ssh_user", "ubuntu"),
+                           Var("gcp_public_key_path", "~/.ssh/id_rsa.pub"), Var("gcp_private_key_path", "~/.ssh/id_rsa")],
+                       f'''resource "google_compute_network" "default" {{
+  name                    = var.name
+  auto_create_subnetworks = true
+}}
+
+resource "google_compute_firewall" "default" {{
+  name    = var.name
+  network = google_compute_network.default.name
+  allow {{
+    protocol = "tcp"
+    ports    = ["22", "80", "443"]
+  }}
+  source_ranges = ["0.0.0.0/0"]
+  target_tags   = ["${{var.name}}-rancher"]
+}}
+
+resource "google_compute_instance" "host" {{
+  name         = var.name
+  machine_type = var.gcp_machine_type
+  zone         = var.gcp_instance_zone
+  tags         = ["${{var.name}}-rancher"]
+  boot_disk {{
+    initialize_params {{
+      image = var.gcp_image
+      size  = 100
+    }}
+  }}
+  network_interface {{
+    network = google_compute_network.default.name
+    access_config {{}}
+  }}
+  metadata = {{
+    ssh-keys = "${{var.gcp_ssh_user}}:${{file(pathexpand(var.gcp_public_key_path))}}"
+  }}
+  metadata_startup_script = {_docker_userdata(True)}
+}}
+
+locals {{
+  rancher_master_id = google_compute_instance.host.id
+  rancher_master_ip = google_compute_instance.host.network_interface[0].access_config[0].nat_ip
+  ssh_user          = var.gcp_ssh_user
+  key_path          = var.gcp_private_key_path
+  bastion_host      = ""
+}}
+''' + _manager_tail(_connection(), False), MANAGER_OUTPUTS, dict(MANAGER_FILES)))
+
+    # T4 azure-rancher (NSG uses destination ports — the reference's source_port_ranges bug Q6 is fixed)
+    mods.append(Module("azure-rancher", ["azure", "external"],
+                       MANAGER_BASE + _rancher_image_vars() + AZURE_CREDS + AZURE_IMAGE + [
+                           Var("azure_virtual_network_name", "rancher-network"),
+                           Var("azure_virtual_network_address_space", "10.0.0.0/16"),
+                           Var("azure_subnet_name", "rancher-subnet"), Var("azure_subnet_address_prefix", "10.0.2.0/24"),
+                           Var("azurerm_network_security_group_name", "rancher-firewall"),
+                           Var("azure_resource_group_name", ""), Var("azure_size", "Standard_D4s_v5"),
+                           Var("azure_ssh_user", "ubuntu"), Var("azure_public_key_path", "~/.ssh/id_rsa.pub"),
+                           Var("azure_private_key_path", "~/.ssh/id_rsa")],
+                       f'''locals {{
+  resource_group = var.azure_resource_group_name != "" ? var.azure_resource_group_name : "${{var.name}}-rancher"
+}}
+
+resource "azurerm_resource_group" "resource_group" {{
+  name     = local.resource_group
+  location = var.azure_location
+}}
+
+resource "azurerm_virtual_network" "vnet" {{
+  name                = var.azure_virtual_network_name
+  address_space       = [var.azure_virtual_network_address_space]
+  location            = var.azure_location
+  resource_group_name = azurerm_resource_group.resource_group.name
+}}
+
+resource "azurerm_subnet" "subnet" {{
+  name                 = var.azure_subnet_name
+  resource_group_name  = azurerm_resource_group.resource_group.name
+  virtual_network_name = azurerm_virtual_network.vnet.name
+  address_prefixes     = [var.azure_subnet_address_prefix]
+}}
+
+resource "azurerm_network_security_group" "rancher" {{
+  name                = var.azurerm_network_security_group_name
+  location            = var.azure_location
+  resource_group_name = azurerm_resource_group.resource_group.name
+  security_rule {{
+    name                       = "rancher"
+    priority                   = 1000
+    direction                  = "Inbound"
+    access                     = "Allow"
+    protocol                   = "Tcp"
+    source_port_range          = "*"
+    destination_port_ranges    = ["22", "80", "443"]
+    source_address_prefix      = "*"
+    destination_address_prefix = "*"
+  }}
+}}
+
+resource "azurerm_public_ip" "ip" {{
+  name                = "${{var.name}}-ip"
+  location            = var.azure_location
+  resource_group_name = azurerm_resource_group.resource_group.name
+  allocation_method   = "Static"
+  sku                 = "Standard"
+}}
+
+resource "azurerm_network_interface" "nic" {{
+  name                = "${{var.name}}-nic"
+  location            = var.azure_location
+  resource_group_name = azurerm_resource_group.resource_group.name
+  ip_configuration {{
+    name                          = "primary"
+    subnet_id                     = azurerm_subnet.subnet.id
+    private_ip_address_allocation = "Dynamic"
+    public_ip_address_id          = azurerm_public_ip.ip.id
+  }}
+}}
+
+resource "azurerm_network_interface_security_group_association" "nic" {{
+  network_interface_id      = azurerm_network_interface.nic.id
+  network_security_group_id = azurerm_network_security_group.rancher.id
+}}
+
+resource "azurerm_linux_virtual_machine" "host" {{
+  name                  = var.name
+  location              = var.azure_location
+  resource_group_name   = azurerm_resource_group.resource_group.name
+  size                  = var.azure_size
+  admin_username        = var.azure_ssh_user
+  network_interface_ids = [azurerm_network_interface.nic.id]
+  custom_data           = base64encode({_docker_userdata(True)})
+  admin_ssh_key {{
+    username   = var.azure_ssh_user
+    public_key = file(pathexpand(var.azure_public_key_path))
+  }}
+  os_disk {{
+    caching              = "ReadWrite"
+    storage_account_type = "Premium_LRS"
+  }}
+  source_image_reference {{
+    publisher = var.azure_image_publisher
+    offer     = var.azure_image_offer
+    sku       = var.azure_image_sku
+    version   = var.azure_image_version
+  }}
+}}
+
+locals {{
+  rancher_master_id = azurerm_linux_virtual_machine.host.id
+  rancher_master_ip = azurerm_public_ip.ip.ip_address
+  ssh_user          = var.azure_ssh_user
+  key_path          = var.azure_private_key_path
+  bastion_host      = ""
+}}
+''' + _manager_tail(_connection(), False), MANAGER_OUTPUTS, dict(MANAGER_FILES)))
+
+    # T5 bare-metal-rancher (the bastion is honoured, fixing Q11)
+    mods.append(Module("bare-metal-rancher", ["external"],
+                       MANAGER_BASE + _rancher_image_vars() + [
+                           Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""),
+                           Var("key_path", "~/.ssh/id_rsa")],
+                       '''locals {
+  rancher_master_id = var.host
+  rancher_master_ip = var.host
+  ssh_user          = var.ssh_user
+  key_path          = var.key_path
+  bastion_host      = var.bastion_host
+}
+''' + _manager_tail(_connection(), True), MANAGER_OUTPUTS, dict(MANAGER_FILES)))
+
+    # T6 triton-rancher-k8s
+    mods.append(Module("triton-rancher-k8s", ["external"], CLUSTER_BASE + TRITON_CREDS, _cluster_data(),
+                       CLUSTER_OUTPUTS, dict(CLUSTER_FILES)))
+
+    # T7 aws-rancher-k8s
+    mods.append(Module("aws-rancher-k8s", ["aws", "external"], CLUSTER_BASE + AWS_CREDS + [
+        Var("aws_vpc_cidr", "10.0.0.0/16"), Var("aws_subnet_cidr", "10.0.2.0/24"),
+        Var("aws_public_key_path", "~/.ssh/id_rsa.pub"), Var("aws_key_name", None)],
+        _cluster_data() + f'''
+resource "aws_vpc" "default" {{
+  cidr_block           = var.aws_vpc_cidr
+  enable_dns_hostnames = true
+  tags = {{ Name = var.name }}
+}}
+
+resource "aws_internet_gateway" "default" {{
+  vpc_id = aws_vpc.default.id
+}}
+
+resource "aws_subnet" "public" {{
+  vpc_id                  = aws_vpc.default.id
+  cidr_block              = var.aws_subnet_cidr
+  map_public_ip_on_launch = true
+  depends_on              = [aws_internet_gateway.default]
+  tags = {{ Name = "${{var.name}}-public" }}
+}}
+
+resource "aws_route_table" "public" {{
+  vpc_id = aws_vpc.default.id
+  route {{
+    cidr_block = "0.0.0.0/0"
+    gateway_id = aws_internet_gateway.default.id
+  }}
+}}
+
+resource "aws_route_table_association" "public" {{
+  subnet_id      = aws_subnet.public.id
+  route_table_id = aws_route_table.public.id
+}}
+
+resource "aws_key_pair" "deployer" {{
+  count      = var.aws_public_key_path != "" ? 1 : 0
+  key_name   = var.aws_key_name
+  public_key = file(pathexpand(var.aws_public_key_path))
+}}
+
+# RKE node ports (rancher.com/docs: port requirements)
+resource "aws_security_group" "rke_ports" {{
+  name        = var.name
+  description = "Security group for rancher hosts in ${{var.name}} cluster"
+  vpc_id      = aws_vpc.default.id
+{_sg_rules(True)}
+}}
+''', CLUSTER_OUTPUTS + [("aws_subnet_id", "aws_subnet.public.id", False),
+                          ("aws_security_group_id", "aws_security_group.rke_ports.id", False),
+                          ("aws_key_name", "var.aws_key_name", False)], dict(CLUSTER_FILES)))
+
+    # T8 gcp-rancher-k8s
+    ports = ", ".join(f'"{lo}-{hi}"' if lo != hi else f'"{lo}"' for lo, hi in RKE_PORTS)
+    mods.append(Module("gcp-rancher-k8s", ["gcp", "external"], CLUSTER_BASE + GCP_CREDS, _cluster_data() + f'''
+resource "google_compute_network" "default" {{
+  name                    = var.name
+  auto_create_subnetworks = true
+}}
+
+resource "google_compute_firewall" "rke_ports" {{
+  name    = var.name
+  network = google_compute_network.default.name
+  allow {{
+    protocol = "tcp"
+    ports    = [{ports}]
+  }}
+  allow {{
+    protocol = "udp"
+    ports    = ["8472"]
+  }}
+  source_tags = ["${{var.name}}-nodes"]
+  target_tags = ["${{var.name}}-nodes"]
+}}
+
+resource "google_compute_firewall" "ssh" {{
+  name          = "${{var.name}}-ssh"
+  network       = google_compute_network.default.name
+  source_ranges = ["0.0.0.0/0"]
+  target_tags   = ["${{var.name}}-nodes"]
+  allow {{
+    protocol = "tcp"
+    ports    = ["22", "80", "443", "6443"]
+  }}
+}}
+''', CLUSTER_OUTPUTS + [("gcp_compute_network_name", "google_compute_network.default.name", False),
+                          ("gcp_compute_firewall_host_tag", '"${var.name}-nodes"', False)], dict(CLUSTER_FILES)))
+
+    # T9 azure-rancher-k8s
+    mods.append(Module("azure-rancher-k8s", ["azure", "external"], CLUSTER_BASE + AZURE_CREDS + AZURE_IMAGE + [
+        Var("azure_virtual_network_name", "k8s-network"), Var("azure_virtual_network_address_space", "10.0.0.0/16"),
+        Var("azure_subnet_name", "k8s-subnet"), Var("azure_subnet_address_prefix", "10.0.2.0/24"),
+        Var("azurerm_network_security_group_name", "k8s-firewall")], _cluster_data() + '''
+resource "azurerm_resource_group" "resource_group" {
+  name     = "${var.name}-k8s"
+  location = var.azure_location
+}
+
+resource "azurerm_virtual_network" "vnet" {
+  name                = var.azure_virtual_network_name
+  address_space       = [var.azure_virtual_network_address_space]
+  location            = var.azure_location
+  resource_group_name = azurerm_resource_group.resource_group.name
+}
+
+resource "azurerm_subnet" "subnet" {
+  name                 = var.azure_subnet_name
+  resource_group_name  = azurerm_resource_group.resource_group.name
+  virtual_network_name = azurerm_virtual_network.vnet.name
+  address_prefixes     = [var.azure_subnet_address_prefix]
+}
+
+resource "azurerm_network_security_group" "rke_ports" {
+  name                = var.azurerm_network_security_group_name
+  location            = var.azure_location
+  resource_group_name = azurerm_resource_group.resource_group.name
+  security_rule {
+    name                       = "rke-internal"
+    priority                   = 1000
+    direction                  = "Inbound"
+    access                     = "Allow"
+    protocol                   = "*"
+    source_port_range          = "*"
+    destination_port_ranges    = ["2376", "2379-2380", "6443", "8472", "9099", "10250-10252", "10254-10256", "30000-32767"]
+    source_address_prefix      = "VirtualNetwork"
+    destination_address_prefix = "*"
+  }
+  security_rule {
+    name                       = "ssh-http"
+    priority                   = 1010
+    direction                  = "Inbound"
+    access                     = "Allow"
+    protocol                   = "Tcp"
+    source_port_range          = "*"
+    destination_port_ranges    = ["22", "80", "443"]
+    source_address_prefix      = "*"
+    destination_address_prefix = "*"
+  }
+}
+''', CLUSTER_OUTPUTS + [("azure_resource_group_name", "azurerm_resource_group.resource_group.name", False),
+                          ("azure_network_security_group_id", "azurerm_network_security_group.rke_ports.id", False),
+                          ("azure_subnet_id", "azurerm_subnet.subnet.id", False)], dict(CLUSTER_FILES)))
+
+    # T10 bare-metal-rancher-k8s
+    mods.append(Module("bare-metal-rancher-k8s", ["external"], CLUSTER_BASE, _cluster_data(), CLUSTER_OUTPUTS,
+                       dict(CLUSTER_FILES)))
+
+    # T11 vsphere-rancher-k8s (data sources validate the names)
+    mods.append(Module("vsphere-rancher-k8s", ["vsphere", "external"], CLUSTER_BASE + VSPHERE_CREDS + VSPHERE_NAMES,
+                       _cluster_data() + '''
+data "vsphere_datacenter" "dc" {
+  name = var.vsphere_datacenter_name
+}
+
+data "vsphere_datastore" "datastore" {
+  name          = var.vsphere_datastore_name
+  datacenter_id = data.vsphere_datacenter.dc.id
+}
+
+data "vsphere_resource_pool" "pool" {
+  name          = var.vsphere_resource_pool_name
+  datacenter_id = data.vsphere_datacenter.dc.id
+}
+
+data "vsphere_network" "network" {
+  name          = var.vsphere_network_name
+  datacenter_id = data.vsphere_datacenter.dc.id
+}
+''', CLUSTER_OUTPUTS + [("vsphere_datacenter_name", "data.vsphere_datacenter.dc.name", False),
+                          ("vsphere_datastore_name", "data.vsphere_datastore.datastore.name", False),
+                          ("vsphere_resource_pool_name", "data.vsphere_resource_pool.pool.name", False),
+                          ("vsphere_network_name", "data.vsphere_network.network.name", False)], dict(CLUSTER_FILES)))
+
+    # T12 triton-rancher-k8s-host
+    mods.append(Module("triton-rancher-k8s-host", ["triton"], HOST_BASE + TRITON_CREDS + [
+        Var("triton_network_names", ["Joyent-SDC-Public"], type="list(string)"),
+        Var("triton_image_name", "ubuntu-certified-22.04"), Var("triton_image_version", None),
+        Var("triton_ssh_user", "ubuntu"), Var("triton_machine_package", "k4-highcpu-kvm-3.75G")],
+        ROLE_LOCAL + f'''
+
+data "triton_network" "networks" {{
+  count = length(var.triton_network_names)
+  name  = var.triton_network_names[count.index]
+}}
+
+data "triton_image" "image" {{
+  name        = var.triton_image_name
+  version     = var.triton_image_version
+  most_recent = true
+}}
+
+resource "triton_machine" "host" {{
+  package     = var.triton_machine_package
+  image       = data.triton_image.image.id
+  name        = var.hostname
+  user_script = {_agent_userdata()}
+  networks    = data.triton_network.networks[*].id
+  cns {{
+    services = ["${{local.rancher_node_role}}.${{var.hostname}}"]
+  }}
+  affinity = ["role!=~${{local.rancher_node_role}}"]
+  tags = {{
+    role = local.rancher_node_role
+  }}
+}}
+''', [], dict(HOST_FILES)))
+
+    # T13 aws-rancher-k8s-host
+    mods.append(Module("aws-rancher-k8s-host", ["aws"], HOST_BASE + AWS_CREDS + [
+        Var("aws_ami_id", None), Var("aws_instance_type", "t3.large"), Var("aws_subnet_id", None),
+        Var("aws_security_group_id", None), Var("aws_key_name", None), Var("ebs_volume_device_name", ""),
+        Var("ebs_volume_mount_path", ""), Var("ebs_volume_type", "gp3"), Var("ebs_volume_iops", ""),
+        Var("ebs_volume_size", "")],
+        ROLE_LOCAL + f'''
+
+locals {{
+  # /dev/sdX is exposed as /dev/xvdX (Xen) or as an NVMe namespace (Nitro)
+  ebs_candidates = var.ebs_volume_device_name == "" ? "" : join(" ", [
+    var.ebs_volume_device_name,
+    replace(var.ebs_volume_device_name, "/dev/sd", "/dev/xvd"),
+    "/dev/nvme1n1",
+  ])
+}}
+
+resource "aws_instance" "host" {{
+  ami                    = var.aws_ami_id
+  instance_type          = var.aws_instance_type
+  subnet_id              = var.aws_subnet_id
+  vpc_security_group_ids = [var.aws_security_group_id]
+  key_name               = var.aws_key_name
+  user_data              = {_agent_userdata("local.ebs_candidates", "var.ebs_volume_mount_path")}
+  tags = {{ Name = var.hostname }}
+}}
+
+resource "aws_ebs_volume" "volume" {{
+  count             = var.ebs_volume_device_name != "" ? 1 : 0
+  availability_zone = aws_instance.host.availability_zone
+  type              = var.ebs_volume_type
+  size              = var.ebs_volume_size == "" ? 100 : tonumber(var.ebs_volume_size)
+  iops              = var.ebs_volume_iops == "" ? null : tonumber(var.ebs_volume_iops)
+}}
+
+resource "aws_volume_attachment" "volume" {{
+  count        = var.ebs_volume_device_name != "" ? 1 : 0
+  device_name  = var.ebs_volume_device_name
+  volume_id    = aws_ebs_volume.volume[0].id
+  instance_id  = aws_instance.host.id
+  force_detach = true
+}}
+''', [], dict(HOST_FILES)))
+
+    # T14 gcp-rancher-k8s-host (the data disk is attached: Q15 fixed)
+    mods.append(Module("gcp-rancher-k8s-host", ["gcp"], HOST_BASE + GCP_CREDS + [
+        Var("gcp_machine_type", "n1-standard-4"), Var("gcp_instance_zone", None),
+        Var("gcp_image", "ubuntu-os-cloud/ubuntu-2204-lts"), Var("gcp_compute_network_name", None),
+        Var("gcp_compute_firewall_host_tag", None), Var("gcp_disk_type", ""), Var("gcp_disk_size", ""),
+        Var("gcp_disk_mount_path", "")],
+        ROLE_LOCAL + f'''
+
+resource "google_compute_disk" "data" {{
+  count = var.gcp_disk_type != "" ? 1 : 0
+  name  = "${{var.hostname}}-data"
+  type  = var.gcp_disk_type
+  zone  = var.gcp_instance_zone
+  size  = tonumber(var.gcp_disk_size)
+}}
+
+resource "google_compute_instance" "host" {{
+  name         = var.hostname
+  machine_type = var.gcp_machine_type
+  zone         = var.gcp_instance_zone
+  tags         = [var.gcp_compute_firewall_host_tag]
+  boot_disk {{
+    initialize_params {{
+      image = var.gcp_image
+      size  = 100
+    }}
+  }}
+  dynamic "attached_disk" {{
+    for_each = google_compute_disk.data
+    content {{
+      source      = attached_disk.value.self_link
+      device_name = "data"
+    }}
+  }}
+  network_interface {{
+    network = var.gcp_compute_network_name
+    access_config {{}}
+  }}
+  metadata_startup_script = {_agent_userdata('var.gcp_disk_type != "" ? "/dev/disk/by-id/google-data" : ""', "var.gcp_disk_mount_path")}
+}}
+''', [], dict(HOST_FILES)))
+
+    # T15 azure-rancher-k8s-host
+    mods.append(Module("azure-rancher-k8s-host", ["azure"], HOST_BASE + AZURE_CREDS + AZURE_IMAGE + [
+        Var("azure_resource_group_name", None), Var("azure_network_security_group_id", None),
+        Var("azure_subnet_id", None), Var("azure_size", "Standard_D4s_v5"), Var("azure_ssh_user", "ubuntu"),
+        Var("azure_public_key_path", "~/.ssh/id_rsa.pub"), Var("azure_disk_mount_path", ""),
+        Var("azure_disk_size", "")],
+        ROLE_LOCAL + f'''
+
+resource "azurerm_public_ip" "ip" {{
+  name                = "${{var.hostname}}-ip"
+  location            = var.azure_location
+  resource_group_name = var.azure_resource_group_name
+  allocation_method   = "Static"
+  sku                 = "Standard"
+}}
+
+resource "azurerm_network_interface" "nic" {{
+  name                = "${{var.hostname}}-nic"
+  location            = var.azure_location
+  resource_group_name = var.azure_resource_group_name
+  ip_configuration {{
+    name                          = "primary"
+    subnet_id                     = var.azure_subnet_id
+    private_ip_address_allocation = "Dynamic"
+    public_ip_address_id          = azurerm_public_ip.ip.id
+  }}
+}}
+
+resource "azurerm_network_interface_security_group_association" "nic" {{
+  network_interface_id      = azurerm_network_interface.nic.id
+  network_security_group_id = var.azure_network_security_group_id
+}}
+
+resource "azurerm_linux_virtual_machine" "host" {{
+  name                  = var.hostname
+  location              = var.azure_location
+  resource_group_name   = var.azure_resource_group_name
+  size                  = var.azure_size
+  admin_username        = var.azure_ssh_user
+  network_interface_ids = [azurerm_network_interface.nic.id]
+  custom_data           = base64encode({_agent_userdata('var.azure_disk_mount_path != "" ? "/dev/disk/azure/scsi1/lun0" : ""', "var.azure_disk_mount_path")})
+  admin_ssh_key {{
+    username   = var.azure_ssh_user
+    public_key = file(pathexpand(var.azure_public_key_path))
+  }}
+  os_disk {{
+    caching              = "ReadWrite"
+    storage_account_type = "Premium_LRS"
+  }}
+  source_image_reference {{
+    publisher = var.azure_image_publisher
+    offer     = var.azure_image_offer
+    sku       = var.azure_image_sku
+    version   = var.azure_image_version
+  }}
+}}
+
+resource "azurerm_managed_disk" "data" {{
+  count                = var.azure_disk_mount_path != "" ? 1 : 0
+  name                 = "${{var.hostname}}-data"
+  location             = var.azure_location
+  resource_group_name  = var.azure_resource_group_name
+  storage_account_type = "Premium_LRS"
+  create_option        = "Empty"
+  disk_size_gb         = tonumber(var.azure_disk_size)
+}}
+
+resource "azurerm_virtual_machine_data_disk_attachment" "data" {{
+  count              = var.azure_disk_mount_path != "" ? 1 : 0
+  managed_disk_id    = azurerm_managed_disk.data[0].id
+  virtual_machine_id = azurerm_linux_virtual_machine.host.id
+  lun                = 0
+  caching            = "ReadWrite"
+}}
+''', [], dict(HOST_FILES)))
+
+    # T16 bare-metal-rancher-k8s-host
+    mods.append(Module("bare-metal-rancher-k8s-host", [], HOST_BASE + [
+        Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa")],
+        ROLE_LOCAL + f'''
+
+resource "terraform_data" "install_rancher_agent" {{
+  triggers_replace = [var.host]
+{_connection("var.host", "var.ssh_user", "var.key_path", "var.bastion_host")}
+  provisioner "remote-exec" {{
+    inline = [{_agent_userdata()}]
+  }}
+}}
+''', [], dict(HOST_FILES)))
+
+    # T17 vsphere-rancher-k8s-host (CPU / memory are variables: Q15 fixed)
+    mods.append(Module("vsphere-rancher-k8s-host", ["vsphere"], HOST_BASE + VSPHERE_CREDS + VSPHERE_NAMES + [
+        Var("vsphere_template_name", None), Var("ssh_user", "ubuntu"), Var("key_path", "~/.ssh/id_rsa"),
+        Var("vsphere_num_cpus", "2"), Var("vsphere_memory_mb", "2048")],
+        ROLE_LOCAL + f'''
+
+data "vsphere_datacenter" "dc" {{
+  name = var.vsphere_datacenter_name
+}}
+
+data "vsphere_datastore" "datastore" {{
+  name          = var.vsphere_datastore_name
+  datacenter_id = data.vsphere_datacenter.dc.id
+}}
+
+data "vsphere_resource_pool" "pool" {{
+  name          = var.vsphere_resource_pool_name
+  datacenter_id = data.vsphere_datacenter.dc.id
+}}
+
+data "vsphere_network" "network" {{
+  name          = var.vsphere_network_name
+  datacenter_id = data.vsphere_datacenter.dc.id
+}}
+
+data "vsphere_virtual_machine" "template" {{
+  name          = var.vsphere_template_name
+  datacenter_id = data.vsphere_datacenter.dc.id
+}}
+
+resource "vsphere_virtual_machine" "vm" {{
+  name             = var.hostname
+  resource_pool_id = data.vsphere_resource_pool.pool.id
+  datastore_id     = data.vsphere_datastore.datastore.id
+  num_cpus         = tonumber(var.vsphere_num_cpus)
+  memory           = tonumber(var.vsphere_memory_mb)
+  guest_id         = data.vsphere_virtual_machine.template.guest_id
+  network_interface {{
+    network_id = data.vsphere_network.network.id
+  }}
+  disk {{
+    label = "disk0"
+    size  = data.vsphere_virtual_machine.template.disks[0].size
+  }}
+  clone {{
+    template_uuid = data.vsphere_virtual_machine.template.id
+  }}
+}}
+
+resource "terraform_data" "install_rancher_agent" {{
+  triggers_replace = [vsphere_virtual_machine.vm.id]
+{_connection("vsphere_virtual_machine.vm.default_ip_address", "var.ssh_user", "var.key_path", None)}
+  provisioner "remote-exec" {{
+    inline = [{_agent_userdata()}]
+  }}
+}}
+''', [], dict(HOST_FILES)))
+
+    # MI355X bare-metal host
+    mods.append(Module("bare-metal-mi355x-rancher-k8s-host", ["external"], HOST_BASE + [
+        Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa"),
+        Var("gpu_product", "MI355X"), Var("gpu_count", "8", "GPUs the node must expose"),
+        Var("gpu_burnin", "quick", "quick | full | off"),
+        Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
+        Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)")],
+        ROLE_LOCAL + f'''
+
+locals {{
+  rccl_env_file = join("\\n", [for k in sort(keys(var.rccl_env)) : "${{k}}=\\"${{var.rccl_env[k]}}\\""])
+}}
+
+resource "terraform_data" "install_mi355x_node" {{
+  triggers_replace = [var.host]
+{_connection("var.host", "var.ssh_user", "var.key_path", "var.bastion_host")}
+  provisioner "remote-exec" {{
+    inline = ["sudo mkdir -p /opt/triton-kubernetes/src && sudo chown $(id -un) /opt/triton-kubernetes/src"]
+  }}
+  provisioner "file" {{
+    source      = "${{path.module}}/files/src/"
+    destination = "/opt/triton-kubernetes/src"
+  }}
+  provisioner "remote-exec" {{
+    inline = [templatefile("${{path.module}}/files/install_mi355x_node.sh.tftpl", {{
+      hostname                           = var.hostname
+      docker_engine_install_url          = var.docker_engine_install_url
+      rancher_api_url                    = var.rancher_api_url
+      rancher_cluster_registration_token = var.rancher_cluster_registration_token
+      rancher_cluster_ca_checksum        = var.rancher_cluster_ca_checksum
+      rancher_node_role                  = local.rancher_node_role
+      rancher_agent_image                = var.rancher_agent_image
+      rancher_registry                   = var.rancher_registry
+      rancher_registry_username          = var.rancher_registry_username
+      rancher_registry_password          = var.rancher_registry_password
+      gpu_count                          = tonumber(var.gpu_count)
+      gpu_burnin                         = var.gpu_burnin
+      rccl_env_file                      = local.rccl_env_file
+      rccl_min_busbw                     = var.rccl_min_busbw
+    }})]
+  }}
+}}
+
+data "external" "gpu_labels" {{
+  depends_on = [terraform_data.install_mi355x_node]
+  program    = ["bash", "${{path.module}}/files/read_gpu_labels.sh"]
+  query = {{
+    host         = var.host
+    ssh_user     = var.ssh_user
+    key_path     = var.key_path
+    bastion_host = var.bastion_host
+  }}
+}}
+''', [("gpu_node_labels", "data.external.gpu_labels.result.labels", False)],
+        {"install_mi355x_node.sh.tftpl": scripts.INSTALL_MI355X_NODE, "read_gpu_labels.sh": scripts.READ_REMOTE_LABELS},
+        {"src/tk_topo.cpp": os.path.join(CSRC, "tk_topo.cpp"),
+         "src/tk_gpu_probe.hip": os.path.join(CSRC, "tk_gpu_probe.hip"),
+         "src/tk_rccl_probe.hip": os.path.join(CSRC, "tk_rccl_probe.hip")}))
+
+    # MI355X cluster add-ons
+    manifests = {
+        "10-device-plugin.json": {"path": f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
+                                  "object": device_plugin_daemonset("${DEVICE_PLUGIN_IMAGE}")},
+        "20-rccl-env.json": {"path": f"/api/v1/namespaces/{NAMESPACE}/configmaps", "object": rccl_configmap()},
+        "30-node-labeller.json": {"path": f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
+                                  "object": labeller_daemonset("${NODE_LABELLER_IMAGE}")},
+    }
+    files = {"apply_addons.sh": scripts.APPLY_ADDONS}
+    for fname, doc in manifests.items():
+        files[f"manifests/{fname}.tftpl"] = json.dumps(doc, indent=2).replace("${DEVICE_PLUGIN_IMAGE}",
+                                                                              "${device_plugin_image}") \
+            .replace("${NODE_LABELLER_IMAGE}", "${node_labeller_image}")
+    mods.append(Module("rancher-k8s-mi355x-addons", ["external"], [
+        Var("name", None), Var("rancher_api_url", None), Var("rancher_access_key", None),
+        Var("rancher_secret_key", None, sensitive=True), Var("rancher_cluster_id", None),
+        Var("device_plugin_image", "rocm/k8s-device-plugin:latest"),
+        Var("node_labeller_image", "rocm/k8s-device-plugin:labeller-latest"),
+        Var("rccl_probe_image", ""), Var("rccl_gate", "true")],
+        '''locals {
+  manifest_dir = "${path.root}/.tk-addons-${var.name}"
+  manifests = {
+    for f in fileset("${path.module}/files/manifests", "*.tftpl") :
+    trimsuffix(f, ".tftpl") => templatefile("${path.module}/files/manifests/${f}", {
+      device_plugin_image = var.device_plugin_image
+      node_labeller_image = var.node_labeller_image
+    })
+  }
+}
+
+resource "terraform_data" "apply_addons" {
+  triggers_replace = [var.rancher_cluster_id, sha256(jsonencode(local.manifests))]
+  input            = length(local.manifests)
+  provisioner "local-exec" {
+    command = <<-EOT
+      mkdir -p "${local.manifest_dir}"
+      %{for name, body in local.manifests~}
+      printf '%s' '${replace(body, "'", "'\\\\''")}' > "${local.manifest_dir}/${name}"
+      %{endfor~}
+      MANIFEST_DIR="${local.manifest_dir}" bash "${path.module}/files/apply_addons.sh"
+    EOT
+    environment = {
+      RANCHER_URL        = var.rancher_api_url
+      RANCHER_ACCESS_KEY = var.rancher_access_key
+      RANCHER_SECRET_KEY = var.rancher_secret_key
+      CLUSTER_ID         = var.rancher_cluster_id
+    }
+  }
+}
+''', [("addons_applied", "tostring(terraform_data.apply_addons.output)", False)], files))
+    return mods
+
+
+def render_versions(mod: Module) -> str:
+    req = [PROVIDERS[p][0] for p in mod.providers]
+    body = "\n    ".join(req)
+    block = f"  required_providers {{\n    {body}\n  }}\n" if req else ""
+    return f"terraform {{\n  required_version = \">= 1.3\"\n{block}}}\n"
+
+
+def render_main(mod: Module) -> str:
+    provider_blocks = [PROVIDERS[p][1] for p in mod.providers if PROVIDERS[p][1]]
+    head = "# Generated by triton_kubernetes_amd.terraform.generate — edit the generator, not this file.\n\n"
+    return head + "\n\n".join(provider_blocks + [mod.main.strip()]) + "\n"
+
+
+def render_variables(mod: Module) -> str:
+    return "\n\n".join(v.hcl() for v in mod.variables) + "\n"
+
+
+def render_outputs(mod: Module) -> str:
+    out = []
+    for name, expr, sensitive in mod.outputs:
+        lines = [f'output "{name}" {{', f"  value = {expr}"]
+        if sensitive:
+            lines.append("  sensitive = true")
+        lines.append("}")
+        out.append("\n".join(lines))
+    return ("\n\n".join(out) + "\n") if out else "# This module has no outputs.\n"
+
+
+def rendered_files(mod: Module) -> Dict[str, str]:
+    files = {
+        "versions.tf": render_versions(mod),
+        "main.tf": render_main(mod),
+        "variables.tf": render_variables(mod),
+        "outputs.tf": render_outputs(mod),
+    }
+    for name, content in mod.files.items():
+        files[f"files/{name}"] = content
+    for name, src in mod.copies.items():
+        with open(src, "r", encoding="utf-8") as fh:
+            files[f"files/{name}"] = fh.read()
+    return files
+
+
+def write_all(root: str = MODULES_DIR) -> List[str]:
+    written = []
+    if os.path.isdir(root):
+        shutil.rmtree(root)
+    for mod in modules():
+        for rel, content in rendered_files(mod).items():
+            path = os.path.join(root, mod.name, rel)
+            os.makedirs(os.path.dirname(path), exist_ok=True)
+            with open(path, "w", encoding="utf-8") as fh:
+                fh.write(content)
+            if path.endswith(".sh"):
+                os.chmod(path, 0o755)
+            written.append(path)
+    return written
+
+
+if __name__ == "__main__":
+    paths = write_all()
+    print(f"wrote {len(paths)} files under {MODULES_DIR}")
+    sys.exit(0)

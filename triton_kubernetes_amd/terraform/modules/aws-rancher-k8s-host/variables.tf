@@ -1,0 +1,89 @@
+variable "hostname" {
+}
+
+variable "rancher_api_url" {
+}
+
+variable "rancher_cluster_registration_token" {
+  sensitive   = true
+}
+
+variable "rancher_cluster_ca_checksum" {
+}
+
+variable "rancher_host_labels" {
+  type        = map(string)
+  description = "A single-key map: {worker|etcd|control = \"true\"}"
+}
+
+variable "docker_engine_install_url" {
+  description = "The URL to the shell script to install the docker engine."
+  default     = "https://releases.rancher.com/install-docker/24.0.sh"
+}
+
+variable "rancher_agent_image" {
+  description = "The Rancher Agent image to use."
+  default     = "rancher/rancher-agent:v2.8.5"
+}
+
+variable "rancher_registry" {
+  description = "The docker registry to use for rancher server and agent images"
+  default     = ""
+}
+
+variable "rancher_registry_username" {
+  description = "The username to login as."
+  default     = ""
+}
+
+variable "rancher_registry_password" {
+  description = "The password to use."
+  default     = ""
+  sensitive   = true
+}
+
+variable "aws_access_key" {
+}
+
+variable "aws_secret_key" {
+  sensitive   = true
+}
+
+variable "aws_region" {
+}
+
+variable "aws_ami_id" {
+}
+
+variable "aws_instance_type" {
+  default     = "t3.large"
+}
+
+variable "aws_subnet_id" {
+}
+
+variable "aws_security_group_id" {
+}
+
+variable "aws_key_name" {
+}
+
+variable "ebs_volume_device_name" {
+  default     = ""
+}
+
+variable "ebs_volume_mount_path" {
+  default     = ""
+}
+
+variable "ebs_volume_type" {
+  default     = "gp3"
+}
+
+variable "ebs_volume_iops" {
+  default     = ""
+}
+
+variable "ebs_volume_size" {
+  default     = ""
+}

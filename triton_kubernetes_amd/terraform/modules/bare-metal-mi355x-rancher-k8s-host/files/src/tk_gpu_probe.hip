@@ -1,0 +1,537 @@
+// MI355X (gfx950 / CDNA4) node burn-in probes.
+//
+// The GPU half of the MI355X worker "readiness gate" (SURVEY.md §7.1 N1/N2
+// companions): before a worker is reported Ready with amd.com/gpu allocatable,
+// every GPU must (1) enumerate as gfx950 with its full CU count and HBM size,
+// (2) stream HBM3E near its achievable rate, (3) issue MFMA at near the dense
+// matrix peak, and (4) pass a pattern memtest.  These kernels are written for
+// the CDNA4 execution model directly:
+//
+//  * streaming kernels move 16 B per lane per access (global_load_dwordx4), keep
+//    several independent loads in flight per lane and launch >> 256 workgroups
+//    so all 8 XCDs / 256 CUs have enough waves to cover HBM latency;
+//  * the MFMA kernels keep operands register-resident (no memory traffic) and
+//    use independent accumulators so one wave per SIMD saturates the matrix
+//    pipe: v_mfma_f32_16x16x32_bf16 (16 cyc/SIMD), the block-scaled
+//    v_mfma_scale_f32_16x16x128_f8f6f4 (fp8, 2x bf16 per clock) and the exact
+//    f32 v_mfma_f32_16x16x4_f32 (1/16 of bf16);
+//  * stores are plain (not nontemporal): measured on MI355X, nt stores cost
+//    ~1/3 of the write bandwidth (4.0 vs ~6 TB/s);
+//  * built with -mllvm -amdgpu-mfma-vgpr-form: with AGPR-form accumulators
+//    hipcc (ROCm 7.2) rotates loop-carried accumulators through
+//    v_accvgpr_mov/read/write every iteration, halving the MFMA issue rate
+//    (measured 1.13 PF bf16); the VGPR form gives a clean back-to-back chain;
+//  * operand data is non-zero pseudo-random: zero operands let the chip hold a
+//    higher clock and overstate throughput (MI355X_MICROARCH.md "DVFS give-back").
+//
+// C ABI, loaded from Python with ctypes (triton_kubernetes_amd/ops/probe.py).
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <string>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+static thread_local char g_err[512];
+
+static int set_err(const char* what, hipError_t e) {
+  snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+  return (int)e == 0 ? -1 : (int)e;
+}
+
+#define CHECK(call)                                   \
+  do {                                                \
+    hipError_t _e = (call);                           \
+    if (_e != hipSuccess) return set_err(#call, _e);  \
+  } while (0)
+
+extern "C" const char* tkp_last_error() { return g_err; }
+
+// ---------------------------------------------------------------------------
+// Device enumeration
+// ---------------------------------------------------------------------------
+struct tkp_device_info {
+  char name[128];
+  char arch[64];
+  int compute_units;
+  int wavefront_size;
+  int clock_khz;
+  int mem_clock_khz;
+  int mem_bus_width;
+  int l2_bytes;
+  int lds_per_block;
+  int pci_domain;
+  int pci_bus;
+  int pci_device;
+  long long total_mem;
+  long long free_mem;
+};
+
+extern "C" int tkp_device_count(int* n) {
+  CHECK(hipGetDeviceCount(n));
+  return 0;
+}
+
+extern "C" int tkp_device_info(int dev, tkp_device_info* out) {
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, dev));
+  memset(out, 0, sizeof(*out));
+  strncpy(out->name, p.name, sizeof(out->name) - 1);
+  strncpy(out->arch, p.gcnArchName, sizeof(out->arch) - 1);
+  out->compute_units = p.multiProcessorCount;
+  out->wavefront_size = p.warpSize;
+  out->clock_khz = p.clockRate;
+  out->mem_clock_khz = p.memoryClockRate;
+  out->mem_bus_width = p.memoryBusWidth;
+  out->l2_bytes = p.l2CacheSize;
+  out->lds_per_block = (int)p.sharedMemPerBlock;
+  out->pci_domain = p.pciDomainID;
+  out->pci_bus = p.pciBusID;
+  out->pci_device = p.pciDeviceID;
+  out->total_mem = (long long)p.totalGlobalMem;
+  CHECK(hipSetDevice(dev));
+  size_t fr = 0, tot = 0;
+  CHECK(hipMemGetInfo(&fr, &tot));
+  out->free_mem = (long long)fr;
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// HBM streaming kernels
+// ---------------------------------------------------------------------------
+constexpr int STREAM_THREADS = 256;
+constexpr int STREAM_UNROLL = 8;  // independent 16-B loads in flight per lane
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_stream_read(const f32x4* __restrict__ src, size_t n4,
+                                                                 float* __restrict__ sink) {
+  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
+  size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x;
+  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  for (; i + (STREAM_UNROLL - 1) * stride < n4; i += STREAM_UNROLL * stride) {
+    f32x4 v[STREAM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) acc += v[u];
+  }
+  for (; i < n4; i += stride) acc += src[i];
+  const float s = acc[0] + acc[1] + acc[2] + acc[3];
+  if (s == 1.2345678e-30f) sink[threadIdx.x] = s;  // never true for the fill data; defeats DCE
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_stream_write(f32x4* __restrict__ dst, size_t n4, float v) {
+  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
+  const f32x4 x = {v, v + 1.f, v + 2.f, v + 3.f};
+  size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x;
+  for (; i + (STREAM_UNROLL - 1) * stride < n4; i += STREAM_UNROLL * stride) {
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) dst[i + u * stride] = x;
+  }
+  for (; i < n4; i += stride) dst[i] = x;
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_stream_copy(const f32x4* __restrict__ src,
+                                                                 f32x4* __restrict__ dst, size_t n4) {
+  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
+  size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x;
+  for (; i + (STREAM_UNROLL - 1) * stride < n4; i += STREAM_UNROLL * stride) {
+    f32x4 v[STREAM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) dst[i + u * stride] = v[u];
+  }
+  for (; i < n4; i += stride) dst[i] = src[i];
+}
+
+static int stream_grid(int dev, int blocks_per_cu) {
+  hipDeviceProp_t p;
+  if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 4096;
+  return p.multiProcessorCount * blocks_per_cu;
+}
+
+// out[0] = read GB/s, out[1] = write GB/s, out[2] = copy GB/s (bytes read + written).
+// Best of `iters` timed launches after one warm-up of each kernel.
+extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_per_cu, double* out) {
+  CHECK(hipSetDevice(dev));
+  if (iters < 1) iters = 1;
+  if (blocks_per_cu < 1) blocks_per_cu = 16;
+  const size_t n4 = bytes / sizeof(f32x4);
+  if (n4 == 0) { snprintf(g_err, sizeof(g_err), "bytes too small"); return -1; }
+  f32x4 *a = nullptr, *b = nullptr;
+  float* sink = nullptr;
+  CHECK(hipMalloc(&a, n4 * sizeof(f32x4)));
+  hipError_t e = hipMalloc(&b, n4 * sizeof(f32x4));
+  if (e != hipSuccess) { (void)hipFree(a); return set_err("hipMalloc(b)", e); }
+  CHECK(hipMalloc(&sink, STREAM_THREADS * sizeof(float)));
+  hipStream_t s;
+  CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t t0, t1;
+  CHECK(hipEventCreate(&t0));
+  CHECK(hipEventCreate(&t1));
+  const int grid = stream_grid(dev, blocks_per_cu);
+  double best[3] = {0, 0, 0};
+  // warm-up + fill
+  k_stream_write<<<grid, STREAM_THREADS, 0, s>>>(a, n4, 1.0f);
+  k_stream_write<<<grid, STREAM_THREADS, 0, s>>>(b, n4, 2.0f);
+  k_stream_read<<<grid, STREAM_THREADS, 0, s>>>(a, n4, sink);
+  k_stream_copy<<<grid, STREAM_THREADS, 0, s>>>(a, b, n4);
+  CHECK(hipGetLastError());
+  CHECK(hipStreamSynchronize(s));
+  for (int kind = 0; kind < 3; ++kind) {
+    for (int it = 0; it < iters; ++it) {
+      CHECK(hipEventRecord(t0, s));
+      if (kind == 0) k_stream_read<<<grid, STREAM_THREADS, 0, s>>>(a, n4, sink);
+      else if (kind == 1) k_stream_write<<<grid, STREAM_THREADS, 0, s>>>(b, n4, 3.0f);
+      else k_stream_copy<<<grid, STREAM_THREADS, 0, s>>>(a, b, n4);
+      CHECK(hipEventRecord(t1, s));
+      CHECK(hipEventSynchronize(t1));
+      float ms = 0.f;
+      CHECK(hipEventElapsedTime(&ms, t0, t1));
+      const double moved = (double)n4 * sizeof(f32x4) * (kind == 2 ? 2.0 : 1.0);
+      const double gbps = moved / (ms * 1e-3) / 1e9;
+      if (gbps > best[kind]) best[kind] = gbps;
+    }
+  }
+  CHECK(hipGetLastError());
+  for (int k = 0; k < 3; ++k) out[k] = best[k];
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  hipStreamDestroy(s);
+  hipFree(a);
+  hipFree(b);
+  hipFree(sink);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// MFMA peak kernels (register-resident operands, independent accumulators)
+// ---------------------------------------------------------------------------
+constexpr int MFMA_THREADS = 256;  // 4 waves = one per SIMD
+constexpr int MFMA_ACC = 4;        // independent accumulator chains per wave
+
+__device__ __forceinline__ uint32_t hash32(uint32_t x) {
+  x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+  return x;
+}
+
+__device__ __forceinline__ float rnd_unit(uint32_t seed) {
+  // uniform in [-1, 1), never exactly zero for the seeds used here
+  return ((hash32(seed) >> 8) * (1.0f / 8388608.0f)) - 1.0f + (1.0f / 16777216.0f);
+}
+
+__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_bf16(float* __restrict__ out, int iters) {
+  const uint32_t lane = blockIdx.x * MFMA_THREADS + threadIdx.x;
+  bf16x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    a[j] = (__bf16)rnd_unit(lane * 16 + j);
+    b[j] = (__bf16)rnd_unit(lane * 16 + 8 + j);
+  }
+  f32x4 acc[MFMA_ACC];
+#pragma unroll
+  for (int c = 0; c < MFMA_ACC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < MFMA_ACC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[c], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MFMA_ACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  if (s == 1.2345678e-30f) out[lane] = s;
+}
+
+__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_fp8(float* __restrict__ out, int iters) {
+  const uint32_t lane = blockIdx.x * MFMA_THREADS + threadIdx.x;
+  i32x8 a, b;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    // random e4m3 bytes with the NaN encodings (0x7f / 0xff) masked out
+    a[j] = (int)(hash32(lane * 16 + j) & 0x3e3e3e3eU);
+    b[j] = (int)(hash32(lane * 16 + 8 + j) & 0x3e3e3e3eU);
+  }
+  f32x4 acc[MFMA_ACC];
+#pragma unroll
+  for (int c = 0; c < MFMA_ACC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < MFMA_ACC; ++c)
+      // cbsz = blgp = 0: e4m3 A and B; E8M0 scale 127 == 1.0
+      acc[c] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(a, b, acc[c], 0, 0, 0, 127, 0, 127);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MFMA_ACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  if (s == 1.2345678e-30f) out[lane] = s;
+}
+
+__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_f32(float* __restrict__ out, int iters) {
+  const uint32_t lane = blockIdx.x * MFMA_THREADS + threadIdx.x;
+  const float a = rnd_unit(lane * 2), b = rnd_unit(lane * 2 + 1);
+  f32x4 acc[MFMA_ACC];
+#pragma unroll
+  for (int c = 0; c < MFMA_ACC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int i = 0; i < iters; ++i) {
+#pragma unroll
+    for (int c = 0; c < MFMA_ACC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[c], 0, 0, 0);
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int c = 0; c < MFMA_ACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  if (s == 1.2345678e-30f) out[lane] = s;
+}
+
+// dtype: 0 = bf16 (16x16x32), 1 = fp8 e4m3 block-scaled (16x16x128), 2 = f32 (16x16x4).
+// Returns dense TFLOP/s (best of `reps`) in out[0] and the kernel ms in out[1].
+extern "C" int tkp_mfma_peak(int dev, int dtype, int iters, int reps, int blocks_per_cu, double* out) {
+  CHECK(hipSetDevice(dev));
+  if (blocks_per_cu < 1) blocks_per_cu = 2;
+  if (reps < 1) reps = 1;
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, dev));
+  const int grid = p.multiProcessorCount * blocks_per_cu;
+  float* sink = nullptr;
+  CHECK(hipMalloc(&sink, (size_t)grid * MFMA_THREADS * sizeof(float)));
+  hipStream_t s;
+  CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t t0, t1;
+  CHECK(hipEventCreate(&t0));
+  CHECK(hipEventCreate(&t1));
+  double flop_per_inst;
+  switch (dtype) {
+    case 0: flop_per_inst = 2.0 * 16 * 16 * 32; break;
+    case 1: flop_per_inst = 2.0 * 16 * 16 * 128; break;
+    case 2: flop_per_inst = 2.0 * 16 * 16 * 4; break;
+    default: snprintf(g_err, sizeof(g_err), "unknown dtype %d", dtype); return -1;
+  }
+  auto launch = [&](int n) {
+    if (dtype == 0) k_mfma_bf16<<<grid, MFMA_THREADS, 0, s>>>(sink, n);
+    else if (dtype == 1) k_mfma_fp8<<<grid, MFMA_THREADS, 0, s>>>(sink, n);
+    else k_mfma_f32<<<grid, MFMA_THREADS, 0, s>>>(sink, n);
+  };
+  launch(iters / 4 + 1);  // warm-up (clock ramp)
+  CHECK(hipGetLastError());
+  CHECK(hipStreamSynchronize(s));
+  double best = 0.0, best_ms = 0.0;
+  for (int r = 0; r < reps; ++r) {
+    CHECK(hipEventRecord(t0, s));
+    launch(iters);
+    CHECK(hipEventRecord(t1, s));
+    CHECK(hipEventSynchronize(t1));
+    float ms = 0.f;
+    CHECK(hipEventElapsedTime(&ms, t0, t1));
+    const double waves = (double)grid * (MFMA_THREADS / 64);
+    const double flops = waves * (double)iters * MFMA_ACC * flop_per_inst;
+    const double tf = flops / (ms * 1e-3) / 1e12;
+    if (tf > best) { best = tf; best_ms = ms; }
+  }
+  CHECK(hipGetLastError());
+  out[0] = best;
+  out[1] = best_ms;
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  hipStreamDestroy(s);
+  hipFree(sink);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// HBM pattern memtest: address-hash pattern, written and verified in
+// streaming passes; mismatches are counted per wave (ballot + popcount) and
+// added with one atomic per wave.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint4 pattern(size_t i, uint32_t seed) {
+  const uint32_t h = hash32((uint32_t)i ^ seed ^ (uint32_t)(i >> 32) * 0x9e3779b9U);
+  return make_uint4(h, ~h, h ^ 0xa5a5a5a5U, h * 0x01000193U);
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_mem_fill(uint4* __restrict__ p, size_t n, uint32_t seed) {
+  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
+  for (size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x; i < n; i += stride) p[i] = pattern(i, seed);
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_mem_check(const uint4* __restrict__ p, size_t n, uint32_t seed,
+                                                               unsigned long long* __restrict__ errors) {
+  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
+  uint32_t bad = 0;
+  for (size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x; i < n; i += stride) {
+    const uint4 v = p[i];
+    const uint4 w = pattern(i, seed);
+    bad += (v.x != w.x) + (v.y != w.y) + (v.z != w.z) + (v.w != w.w);
+  }
+  // wave-level reduction: 64 lanes
+  for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
+  if ((threadIdx.x & 63) == 0 && bad) atomicAdd(errors, (unsigned long long)bad);
+}
+
+// out[0] = mismatching 32-bit words, out[1] = verify GB/s of the last pass.
+extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
+  CHECK(hipSetDevice(dev));
+  const size_t n = bytes / sizeof(uint4);
+  uint4* p = nullptr;
+  unsigned long long* err = nullptr;
+  CHECK(hipMalloc(&p, n * sizeof(uint4)));
+  CHECK(hipMalloc(&err, sizeof(unsigned long long)));
+  CHECK(hipMemset(err, 0, sizeof(unsigned long long)));
+  hipEvent_t t0, t1;
+  CHECK(hipEventCreate(&t0));
+  CHECK(hipEventCreate(&t1));
+  const int grid = stream_grid(dev, 16);
+  float ms = 0.f;
+  for (int ps = 0; ps < (passes < 1 ? 1 : passes); ++ps) {
+    const uint32_t seed = 0x1234567u + 0x9e3779b9u * (uint32_t)ps;
+    k_mem_fill<<<grid, STREAM_THREADS>>>(p, n, seed);
+    CHECK(hipEventRecord(t0, 0));
+    k_mem_check<<<grid, STREAM_THREADS>>>(p, n, seed, err);
+    CHECK(hipEventRecord(t1, 0));
+    CHECK(hipEventSynchronize(t1));
+    CHECK(hipEventElapsedTime(&ms, t0, t1));
+  }
+  CHECK(hipGetLastError());
+  unsigned long long h = 0;
+  CHECK(hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost));
+  out[0] = (double)h;
+  out[1] = (double)n * sizeof(uint4) / (ms * 1e-3) / 1e9;
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  hipFree(p);
+  hipFree(err);
+  return 0;
+}
+
+// Test hook: corrupt `count` words of a filled buffer to prove the checker
+// detects errors (used by the numerics test, never by the probe itself).
+extern "C" int tkp_memtest_selfcheck(int dev, size_t bytes, int corrupt, double* out) {
+  CHECK(hipSetDevice(dev));
+  const size_t n = bytes / sizeof(uint4);
+  uint4* p = nullptr;
+  unsigned long long* err = nullptr;
+  CHECK(hipMalloc(&p, n * sizeof(uint4)));
+  CHECK(hipMalloc(&err, sizeof(unsigned long long)));
+  CHECK(hipMemset(err, 0, sizeof(unsigned long long)));
+  const int grid = stream_grid(dev, 4);
+  k_mem_fill<<<grid, STREAM_THREADS>>>(p, n, 77u);
+  CHECK(hipDeviceSynchronize());
+  for (int c = 0; c < corrupt && (size_t)c < n; ++c) {
+    uint32_t junk = 0xdeadbeefu ^ (uint32_t)c;
+    CHECK(hipMemcpy(reinterpret_cast<char*>(p + (size_t)c * (n / (corrupt + 1))), &junk, 4,
+                    hipMemcpyHostToDevice));
+  }
+  k_mem_check<<<grid, STREAM_THREADS>>>(p, n, 77u, err);
+  CHECK(hipGetLastError());
+  unsigned long long h = 0;
+  CHECK(hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost));
+  out[0] = (double)h;
+  hipFree(p);
+  hipFree(err);
+  return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Peer (xGMI) copy bandwidth between two local GPUs.
+// ---------------------------------------------------------------------------
+extern "C" int tkp_p2p_bandwidth(int src, int dst, size_t bytes, int iters, double* out) {
+  int can = 0;
+  CHECK(hipDeviceCanAccessPeer(&can, dst, src));
+  out[1] = can;
+  CHECK(hipSetDevice(src));
+  void* a = nullptr;
+  CHECK(hipMalloc(&a, bytes));
+  CHECK(hipSetDevice(dst));
+  void* b = nullptr;
+  CHECK(hipMalloc(&b, bytes));
+  if (can) {
+    hipError_t e = hipDeviceEnablePeerAccess(src, 0);
+    if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) return set_err("hipDeviceEnablePeerAccess", e);
+    (void)hipGetLastError();
+  }
+  hipStream_t s;
+  CHECK(hipStreamCreate(&s));
+  hipEvent_t t0, t1;
+  CHECK(hipEventCreate(&t0));
+  CHECK(hipEventCreate(&t1));
+  CHECK(hipMemcpyPeerAsync(b, dst, a, src, bytes, s));
+  CHECK(hipStreamSynchronize(s));
+  double best = 0.0;
+  for (int i = 0; i < (iters < 1 ? 1 : iters); ++i) {
+    CHECK(hipEventRecord(t0, s));
+    CHECK(hipMemcpyPeerAsync(b, dst, a, src, bytes, s));
+    CHECK(hipEventRecord(t1, s));
+    CHECK(hipEventSynchronize(t1));
+    float ms = 0.f;
+    CHECK(hipEventElapsedTime(&ms, t0, t1));
+    const double gbps = (double)bytes / (ms * 1e-3) / 1e9;
+    if (gbps > best) best = gbps;
+  }
+  out[0] = best;
+  hipEventDestroy(t0);
+  hipEventDestroy(t1);
+  hipStreamDestroy(s);
+  hipFree(b);
+  CHECK(hipSetDevice(src));
+  hipFree(a);
+  return 0;
+}
+
+#ifdef TK_PROBE_MAIN
+// gpu-burnin: the on-node executable the SSH bootstrap runs (no Python needed).
+//   gpu-burnin [--all | --device N] [--level quick|full]
+//              [--min-read-gbps X] [--min-bf16-tflops Y] [--min-fp8-tflops Z]
+// Prints one JSON document; exit 1 when any GPU misses a threshold or the
+// memtest finds a mismatch (thresholds: 60 % of 6.3 TB/s achievable HBM read,
+// 55 % of the 2.5 / 5 PF dense bf16 / fp8 MFMA peaks).
+#include <cstdlib>
+#include <vector>
+
+int main(int argc, char** argv) {
+  int dev = 0, all = 0;
+  const char* level = "quick";
+  double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0;
+  for (int i = 1; i < argc; ++i) {
+    if (!strcmp(argv[i], "--all")) all = 1;
+    else if (!strcmp(argv[i], "--device") && i + 1 < argc) dev = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--level") && i + 1 < argc) level = argv[++i];
+    else if (!strcmp(argv[i], "--min-read-gbps") && i + 1 < argc) min_read = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--min-bf16-tflops") && i + 1 < argc) min_bf16 = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--min-fp8-tflops") && i + 1 < argc) min_fp8 = atof(argv[++i]);
+  }
+  const bool full = !strcmp(level, "full");
+  const size_t hbm_bytes = full ? (16ull << 30) : (1ull << 30);
+  const size_t mt_bytes = full ? (64ull << 30) : (1ull << 30);
+  const int mfma_iters = full ? 40000 : 4000;
+  int n = 0;
+  if (tkp_device_count(&n) != 0 || n < 1) {
+    printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    return 2;
+  }
+  std::vector<int> devs;
+  if (all) for (int d = 0; d < n; ++d) devs.push_back(d);
+  else devs.push_back(dev);
+  bool ok_all = true;
+  printf("{\"level\":\"%s\",\"gpus\":[", level);
+  for (size_t k = 0; k < devs.size(); ++k) {
+    const int d = devs[k];
+    struct tkp_device_info info;
+    memset(&info, 0, sizeof(info));
+    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[2] = {0, 0};
+    bool ok = tkp_device_info(d, &info) == 0 && tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, hbm) == 0 &&
+              tkp_mfma_peak(d, 0, mfma_iters, 3, 2, bf16) == 0 && tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, fp8) == 0 &&
+              tkp_memtest(d, mt_bytes, full ? 3 : 1, mt) == 0;
+    const bool pass = ok && strncmp(info.arch, "gfx950", 6) == 0 && hbm[0] >= min_read && bf16[0] >= min_bf16 &&
+                      fp8[0] >= min_fp8 && mt[0] == 0.0;
+    ok_all = ok_all && pass;
+    printf("%s{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"read_gbps\":%.1f,\"write_gbps\":%.1f,\"copy_gbps\":%.1f,"
+           "\"bf16_tflops\":%.1f,\"fp8_tflops\":%.1f,\"memtest_errors\":%.0f,\"ok\":%s%s%s%s}",
+           k ? "," : "", d, info.arch, info.compute_units, hbm[0], hbm[1], hbm[2], bf16[0], fp8[0], mt[0],
+           pass ? "true" : "false", ok ? "" : ",\"error\":\"", ok ? "" : g_err, ok ? "" : "\"");
+  }
+  printf("],\"ok\":%s}\n", ok_all ? "true" : "false");
+  return ok_all ? 0 : 1;
+}
+#endif

@@ -1,0 +1,1 @@
+# This module has no outputs.

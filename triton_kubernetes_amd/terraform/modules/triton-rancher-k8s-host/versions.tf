@@ -1,0 +1,9 @@
+terraform {
+  required_version = ">= 1.3"
+  required_providers {
+    triton = {
+      source  = "joyent/triton"
+      version = ">= 0.8"
+    }
+  }
+}

@@ -1,0 +1,230 @@
+"""Bootstrap scripts and templates shipped inside the Terraform modules (S1-S6 + MI355X).
+
+Terraform ``templatefile`` syntax: ``${var}`` is substituted, ``$${x}`` is a
+literal ``${x}`` and ``%{ if }`` directives are available.  These are fresh
+scripts for a current Rancher 2.x / Docker, not the reference's 0.11-era
+templates, and they fix the reference quirks Q10
+(hard-coded ``/home/ubuntu``, ``/etc/fstab`` overwritten with ``tee``).
+"""
+
+INSTALL_DOCKER = r"""#!/bin/bash
+# S1/S6: container runtime for a Rancher manager or node (cloud-init / remote-exec).
+set -euo pipefail
+if command -v firewalld >/dev/null 2>&1; then
+  sudo systemctl disable --now firewalld.service || true
+fi
+if ! command -v docker >/dev/null 2>&1; then
+  curl -fsSL "${docker_engine_install_url}" | sudo sh
+fi
+if [ ! -f /etc/docker/daemon.json ]; then
+  if mountpoint -q /mnt; then
+    echo '{"storage-driver": "overlay2", "data-root": "/mnt/docker"}' | sudo tee /etc/docker/daemon.json >/dev/null
+  else
+    echo '{"storage-driver": "overlay2"}' | sudo tee /etc/docker/daemon.json >/dev/null
+  fi
+  sudo systemctl restart docker || sudo service docker restart
+fi
+%{ if rancher_registry_username != "" ~}
+echo '${rancher_registry_password}' | sudo docker login -u '${rancher_registry_username}' --password-stdin '${rancher_registry}'
+%{ endif ~}
+%{ if rancher_server_image != "" ~}
+sudo docker pull '${rancher_server_image}'
+%{ endif ~}
+"""
+
+INSTALL_RANCHER_SERVER = r"""#!/bin/bash
+# S2: run the Rancher server container once docker and the image are present.
+set -euo pipefail
+for i in $(seq 1 600); do command -v docker >/dev/null 2>&1 && break; sleep 1; done
+for i in $(seq 1 600); do sudo docker image inspect '${rancher_server_image}' >/dev/null 2>&1 && break; sudo docker pull '${rancher_server_image}' || sleep 1; done
+if ! sudo docker ps --format '{{.Image}}' | grep -qx '${rancher_server_image}'; then
+  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 '${rancher_server_image}'
+fi
+"""
+
+SETUP_RANCHER = r"""#!/bin/bash
+# S3: bootstrap the Rancher API on the manager (token -> ~/rancher_api_key).
+set -euo pipefail
+R='${rancher_host}'
+for i in $(seq 1 900); do curl -ksf "$R/ping" >/dev/null 2>&1 && break; sleep 1; done
+json() { python3 -c "import json,sys; print(json.load(sys.stdin)$1)"; }
+login=$(curl -ksf -X POST -H 'Content-Type: application/json' \
+  -d '{"username":"admin","password":"admin","ttl":60000,"description":"Initial Token"}' \
+  "$R/v3-public/localProviders/local?action=login")
+initial=$(printf '%s' "$login" | json '["token"]')
+tok=$(curl -ksf -u "$initial" -X POST -H 'Content-Type: application/json' \
+  -d '{"type":"token","name":"triton-kubernetes","description":"Managed by triton-kubernetes","ttl":0}' "$R/v3/token")
+umask 077
+printf '%s' "$tok" > ~/rancher_api_key
+ak=$(printf '%s' "$tok" | json '["name"]')
+sk=$(printf '%s' "$tok" | json '["token"].split(":",1)[1]')
+curl -ksf -u "$ak:$sk" -X POST -H 'Content-Type: application/json' \
+  -d '{"currentPassword":"admin","newPassword":"${rancher_admin_password}"}' "$R/v3/users?action=changepassword" >/dev/null
+curl -ksf -u "$ak:$sk" -X PUT -H 'Content-Type: application/json' \
+  -d '{"name":"server-url","value":"${host_registration_url}"}' "$R/v3/settings/server-url" >/dev/null
+"""
+
+READ_API_KEY = r"""#!/bin/bash
+# data "external" program: read the manager's ~/rancher_api_key over SSH.
+# Replaces the reference's matti/outputs/shell registry module.
+set -euo pipefail
+eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
+opts=(-o BatchMode=yes -o StrictHostKeyChecking=no -o UserKnownHostsFile=/dev/null -o LogLevel=ERROR -i "${key_path/#\~/$HOME}")
+if [ -n "${bastion_host:-}" ]; then opts+=(-J "$ssh_user@$bastion_host"); fi
+tok=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_api_key')
+printf '%s' "$tok" | python3 -c '
+import json, sys
+t = json.load(sys.stdin)
+print(json.dumps({"access_key": t["name"], "secret_key": t["token"].split(":", 1)[1]}))'
+"""
+
+RANCHER_CLUSTER = r"""#!/bin/bash
+# S4: data "external" program run on the operator machine.  Idempotent
+# find-or-create of the RKE cluster, its registration token and CA checksum.
+set -euo pipefail
+eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
+api() { curl -ksf -u "$rancher_access_key:$rancher_secret_key" -H 'Accept: application/json' -H 'Content-Type: application/json' "$@"; }
+py() { python3 -c "$1"; }
+search=$(api "$rancher_api_url/v3/clusters?name=$name")
+cluster_id=$(printf '%s' "$search" | py 'import json,sys; d=json.load(sys.stdin)["data"]; print(d[0]["id"] if d else "")')
+existed=true
+if [ -z "$cluster_id" ]; then
+  existed=false
+  body=$(NAME="$name" VER="$k8s_version" NET="$k8s_network_provider" REG="${k8s_registry:-}" \
+         REGU="${k8s_registry_username:-}" REGP="${k8s_registry_password:-}" py '
+import json, os
+rke = {"ignoreDockerVersion": False, "sshAgentAuth": False, "type": "rancherKubernetesEngineConfig",
+       "kubernetesVersion": os.environ["VER"], "authentication": {"type": "authnConfig", "strategy": "x509"},
+       "network": {"type": "networkConfig", "plugin": os.environ["NET"]},
+       "services": {"type": "rkeConfigServices", "kubeApi": {"podSecurityPolicy": False, "type": "kubeAPIService"}}}
+if os.environ["REG"]:
+    rke["privateRegistries"] = [{"url": os.environ["REG"], "user": os.environ["REGU"], "password": os.environ["REGP"]}]
+print(json.dumps({"type": "cluster", "name": os.environ["NAME"], "rancherKubernetesEngineConfig": rke}))')
+  cluster_id=$(api -X POST -d "$body" "$rancher_api_url/v3/cluster" | py 'import json,sys; print(json.load(sys.stdin).get("id",""))')
+fi
+[ -n "$cluster_id" ] || { echo "Unable to create cluster!" >&2; exit 1; }
+token=""
+if [ "$existed" = true ]; then
+  token=$(api "$rancher_api_url/v3/clusters/$cluster_id/clusterregistrationtokens" | py 'import json,sys; d=json.load(sys.stdin)["data"]; print(d[0]["token"] if d else "")')
+fi
+if [ -z "$token" ]; then
+  token=$(api -X POST -d "{\"type\":\"clusterRegistrationToken\",\"clusterId\":\"$cluster_id\"}" \
+          "$rancher_api_url/v3/clusterregistrationtoken" | py 'import json,sys; print(json.load(sys.stdin).get("token",""))')
+fi
+[ -n "$token" ] || { echo "Unable to create cluster registration token!" >&2; exit 1; }
+checksum=$(api "$rancher_api_url/v3/settings/cacerts" | py 'import json,sys,hashlib; v=json.load(sys.stdin)["value"]; print(hashlib.sha256((v+"\n").encode()).hexdigest())')
+CID="$cluster_id" TOK="$token" SUM="$checksum" py 'import json,os; print(json.dumps({"cluster_id": os.environ["CID"], "registration_token": os.environ["TOK"], "ca_checksum": os.environ["SUM"]}))'
+"""
+
+INSTALL_RANCHER_AGENT = r"""#!/bin/bash
+# S5: join a node to the cluster (user-data or remote-exec).
+set -euo pipefail
+if command -v firewalld >/dev/null 2>&1; then sudo systemctl disable --now firewalld.service || true; fi
+if ! command -v docker >/dev/null 2>&1; then curl -fsSL "${docker_engine_install_url}" | sudo sh; fi
+if [ ! -f /etc/docker/daemon.json ]; then
+  echo '{"storage-driver": "overlay2"}' | sudo tee /etc/docker/daemon.json >/dev/null
+  sudo systemctl restart docker || sudo service docker restart
+fi
+sudo hostnamectl set-hostname '${hostname}'
+grep -q ' ${hostname}$' /etc/hosts || echo '127.0.0.1 ${hostname}' | sudo tee -a /etc/hosts >/dev/null
+%{ if rancher_registry_username != "" ~}
+echo '${rancher_registry_password}' | sudo docker login -u '${rancher_registry_username}' --password-stdin '${rancher_registry}'
+%{ endif ~}
+%{ if disk_device != "" && disk_mount_path != "" ~}
+# data disk: first of the candidate device names that exists; appended to fstab (never overwritten)
+for dev in ${disk_device}; do
+  if [ -b "$dev" ]; then
+    if ! sudo blkid "$dev" >/dev/null 2>&1; then sudo mkfs.ext4 -q -E nodiscard "$dev"; fi
+    sudo mkdir -p '${disk_mount_path}'
+    uuid=$(sudo blkid -s UUID -o value "$dev")
+    grep -q "$uuid" /etc/fstab || echo "UUID=$uuid ${disk_mount_path} ext4 defaults,noatime,nofail 0 2" | sudo tee -a /etc/fstab >/dev/null
+    sudo mount -a
+    break
+  fi
+done
+%{ endif ~}
+sudo docker run -d --privileged --restart=unless-stopped --net=host \
+  -v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run '${rancher_agent_image}' \
+  --server '${rancher_api_url}' --token '${rancher_cluster_registration_token}' \
+  --ca-checksum '${rancher_cluster_ca_checksum}' --${rancher_node_role}${extra_agent_args}
+"""
+
+INSTALL_MI355X_NODE = r"""#!/bin/bash
+# MI355X worker bootstrap: ROCm preflight, topology labels (N1), burn-in,
+# RCCL environment + node-level RCCL gate (N2), then the Rancher agent with
+# the GPU labels.  Tools are built on the node from the shipped sources when
+# no prebuilt binary was uploaded.
+set -euo pipefail
+T=/opt/triton-kubernetes/bin
+S=/opt/triton-kubernetes/src
+sudo mkdir -p $T /etc/triton-kubernetes /etc/rccl
+lsmod | grep -q '^amdgpu' || { echo 'amdgpu kernel module not loaded' >&2; exit 1; }
+test -c /dev/kfd || { echo '/dev/kfd missing' >&2; exit 1; }
+n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
+[ "$n" -ge ${gpu_count} ] || { echo "expected ${gpu_count} GPUs, found $n" >&2; exit 1; }
+sudo usermod -aG video,render "$(id -un)" || true
+ROCM=$${ROCM_PATH:-/opt/rocm}
+build() { # name, compiler, flags...
+  local name=$1; shift
+  [ -x "$T/$name" ] || sudo "$@" -o "$T/$name"
+}
+build amdgpu-topo-labeller g++ -O2 -std=c++17 -DTK_TOPO_MAIN -I$ROCM/include $S/tk_topo.cpp -L$ROCM/lib -lamd_smi -Wl,-rpath,$ROCM/lib
+build gpu-burnin $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip
+build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl
+$T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/dev/null
+$T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
+%{ if gpu_burnin != "off" ~}
+$T/gpu-burnin --all --level '${gpu_burnin}' | sudo tee /etc/triton-kubernetes/gpu-burnin.json
+%{ endif ~}
+sudo tee /etc/rccl/rccl.env >/dev/null <<'TK_RCCL_EOF'
+${rccl_env_file}
+TK_RCCL_EOF
+%{ if gpu_count > 1 ~}
+set -a; . /etc/rccl/rccl.env; set +a
+$T/rccl-ready --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
+%{ endif ~}
+labels=$(sed 's/^/--label /' /etc/triton-kubernetes/gpu-labels | tr '\n' ' ')
+if ! command -v docker >/dev/null 2>&1; then curl -fsSL "${docker_engine_install_url}" | sudo sh; fi
+sudo hostnamectl set-hostname '${hostname}'
+%{ if rancher_registry_username != "" ~}
+echo '${rancher_registry_password}' | sudo docker login -u '${rancher_registry_username}' --password-stdin '${rancher_registry}'
+%{ endif ~}
+sudo docker run -d --privileged --restart=unless-stopped --net=host \
+  -v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run '${rancher_agent_image}' \
+  --server '${rancher_api_url}' --token '${rancher_cluster_registration_token}' \
+  --ca-checksum '${rancher_cluster_ca_checksum}' --${rancher_node_role} $labels
+"""
+
+READ_REMOTE_LABELS = r"""#!/bin/bash
+# data "external" program: the GPU labels a MI355X node computed, as one JSON string.
+set -euo pipefail
+eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
+opts=(-o BatchMode=yes -o StrictHostKeyChecking=no -o UserKnownHostsFile=/dev/null -o LogLevel=ERROR -i "${key_path/#\~/$HOME}")
+if [ -n "${bastion_host:-}" ]; then opts+=(-J "$ssh_user@$bastion_host"); fi
+ssh "${opts[@]}" "$ssh_user@$host" 'cat /etc/triton-kubernetes/gpu-labels' | python3 -c '
+import json, sys
+labels = dict(l.strip().split("=", 1) for l in sys.stdin if "=" in l)
+print(json.dumps({"labels": json.dumps(labels, sort_keys=True)}))'
+"""
+
+APPLY_ADDONS = r"""#!/bin/bash
+# MI355X cluster add-ons: wait for the cluster, then create the manifests in
+# $MANIFEST_DIR through Rancher's Kubernetes proxy (PUT on 409).
+set -euo pipefail
+api() { curl -ksf -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" -H 'Content-Type: application/json' "$@"; }
+for i in $(seq 1 3600); do
+  state=$(api "$RANCHER_URL/v3/clusters/$CLUSTER_ID" | python3 -c 'import json,sys; print(json.load(sys.stdin).get("state",""))' || true)
+  [ "$state" = active ] && break
+  sleep 1
+done
+[ "$state" = active ] || { echo "cluster $CLUSTER_ID not active" >&2; exit 1; }
+for f in "$MANIFEST_DIR"/*.json; do
+  path=$(python3 -c 'import json,sys; print(json.load(open(sys.argv[1]))["path"])' "$f")
+  obj=$(python3 -c 'import json,sys; print(json.dumps(json.load(open(sys.argv[1]))["object"]))' "$f")
+  name=$(python3 -c 'import json,sys; print(json.load(open(sys.argv[1]))["object"]["metadata"]["name"])' "$f")
+  code=$(curl -ks -o /dev/null -w '%{http_code}' -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" \
+         -H 'Content-Type: application/json' -X POST -d "$obj" "$RANCHER_URL/k8s/clusters/$CLUSTER_ID$path")
+  if [ "$code" = 409 ]; then api -X PUT -d "$obj" "$RANCHER_URL/k8s/clusters/$CLUSTER_ID$path/$name" >/dev/null
+  elif [ "$code" -ge 300 ]; then echo "applying $f: HTTP $code" >&2; exit 1; fi
+done
+"""
