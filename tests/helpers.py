@@ -63,3 +63,19 @@ def make_ssh_key(path, kind: str = "rsa") -> str:
 
 def have(binary: str) -> bool:
     return shutil.which(binary) is not None
+
+
+def assert_blocks_match_modules(st) -> None:
+    """Every key a provider wrote into a module block is a variable of the generated module."""
+    from triton_kubernetes_amd.terraform import catalog, generate
+
+    declared = {m.name: {v.name for v in m.variables} for m in generate.modules()}
+    for key, block in (st.doc.get("module") or {}).items():
+        info = catalog.module_from_source(block["source"])
+        assert info is not None, f"{key}: unknown module source {block['source']}"
+        extra = set(block) - {"source"} - declared[info.name]
+        assert not extra, f"{key} -> {info.name}: keys not declared as module variables: {sorted(extra)}"
+        required = {v.name for m in generate.modules() if m.name == info.name for v in m.variables
+                    if v.default is None}
+        missing = required - set(block)
+        assert not missing, f"{key} -> {info.name}: required variables not set: {sorted(missing)}"

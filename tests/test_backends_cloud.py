@@ -1,0 +1,183 @@
+"""Backends (local / Manta / memory) and the stdlib cloud clients."""
+
+import base64
+import datetime
+import json
+import os
+import threading
+
+import pytest
+
+from triton_kubernetes_amd.backend import LocalBackend, MemoryBackend
+from triton_kubernetes_amd.backend.manta import MantaBackend
+from triton_kubernetes_amd.cloud.aws import sigv4_headers
+from triton_kubernetes_amd.cloud.fake_manta import FakeManta
+from triton_kubernetes_amd.cloud.gcp import make_jwt
+from triton_kubernetes_amd.cloud.triton import HTTPSignatureSigner, MantaClient
+from triton_kubernetes_amd.errors import BackendError, TKError
+from triton_kubernetes_amd.state import State
+from triton_kubernetes_amd.utils.sshkeys import load_private_key, rsa_pkcs1v15_verify
+
+from helpers import make_ssh_key
+
+
+def test_local_backend_layout(tmp_path):
+    be = LocalBackend(str(tmp_path / "root"))
+    assert be.states() == []
+    st = be.state("mgr")
+    assert st.doc == {}
+    st.set_manager({"name": "mgr"})
+    be.persist_state(st)
+    assert be.states() == ["mgr"]
+    assert os.path.isfile(tmp_path / "root" / "mgr" / "main.tf.json")
+    assert be.state_terraform_config("mgr") == ("terraform.backend.local",
+                                                {"path": str(tmp_path / "root" / "mgr" / "terraform.tfstate")})
+    be.write_tfstate("mgr", b"{}")
+    assert be.read_tfstate("mgr") == b"{}"
+    be.delete_state("mgr")
+    assert be.states() == []
+    with pytest.raises(BackendError):
+        be.state("../etc")
+
+
+def test_local_backend_default_root_is_home(tk_home):
+    be = LocalBackend()
+    assert be.root == str(tk_home / ".triton-kubernetes")
+
+
+def test_local_backend_lock_serialises_writers(tmp_path):
+    be = LocalBackend(str(tmp_path))
+    order = []
+
+    def writer(i):
+        with be.lock("mgr"):
+            st = be.state("mgr")
+            n = len(st.modules())
+            st.set_module(f"m{i}", {"i": i})
+            order.append(n)
+            be.persist_state(st)
+
+    ts = [threading.Thread(target=writer, args=(i,)) for i in range(8)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join()
+    assert len(be.state("mgr").modules()) == 8  # no lost update
+    assert "mgr" in be.states() and not any(s.startswith(".") for s in be.states())
+
+
+def test_memory_backend_records_calls():
+    be = MemoryBackend(states={"a": b'{"module":{}}'}, state_names=["a", "b"])
+    assert be.states() == ["a", "b"]
+    be.persist_state(State("c"))
+    assert "c" in be.states() and ("PersistState", ("c",)) in be.calls
+
+
+@pytest.fixture
+def manta(tmp_path):
+    key_path = make_ssh_key(tmp_path / "id_rsa")
+    key = load_private_key(key_path)
+    fake = FakeManta("acct").start()
+    fake.add_key(key)
+    yield fake, key_path, key
+    fake.stop()
+
+
+def test_manta_backend_roundtrip_with_signatures(manta):
+    fake, key_path, key = manta
+    be = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://triton", fake.url)
+    assert be.states() == []
+    st = be.state("mgr")
+    st.set_manager({"name": "mgr"})
+    be.persist_state(st)
+    assert be.states() == ["mgr"]
+    assert json.loads(be.state("mgr").bytes())["module"]["cluster-manager"]["name"] == "mgr"
+    path, cfg = be.state_terraform_config("mgr")
+    assert path == "terraform.backend.manta"
+    assert cfg == {"account": "acct", "key_material": key_path, "key_id": key.fingerprint_md5(),
+                   "path": "/triton-kubernetes/mgr"}
+    with be.lock("mgr"):
+        assert "/acct/stor/triton-kubernetes/mgr/.lock" in fake.objects
+    assert "/acct/stor/triton-kubernetes/mgr/.lock" not in fake.objects
+    be.write_tfstate("mgr", b'{"version":4}')
+    be.delete_state("mgr")
+    assert be.states() == [] and fake.rejected == 0
+
+
+def test_manta_pagination_beyond_100(manta):
+    fake, key_path, key = manta
+    client = MantaClient(fake.url, HTTPSignatureSigner("acct", key))
+    client.put_directory("/stor/triton-kubernetes")
+    for i in range(130):
+        client.put_directory(f"/stor/triton-kubernetes/m{i:03d}")
+    entries = client.list_directory("/stor/triton-kubernetes", limit=50)
+    assert len(entries) == 130  # the reference stops at 100
+
+
+def test_manta_rejects_bad_signature(manta, tmp_path):
+    fake, _, _ = manta
+    other = load_private_key(make_ssh_key(tmp_path / "other"))
+    client = MantaClient(fake.url, HTTPSignatureSigner("acct", other))
+    with pytest.raises(TKError) as exc:
+        client.put_directory("/stor/x")
+    assert "403" in str(exc.value) and fake.rejected == 1
+
+
+def test_http_signature_header(tmp_path):
+    key = load_private_key(make_ssh_key(tmp_path / "k"))
+    signer = HTTPSignatureSigner("acct", key)
+    hdrs = {}
+    signer("GET", "https://x/acct/machines", hdrs, b"")
+    auth = hdrs["Authorization"]
+    assert auth.startswith(f'Signature keyId="/acct/keys/{key.fingerprint_md5()}",algorithm="rsa-sha256"')
+    sig = base64.b64decode(auth.split('signature="')[1].rstrip('"'))
+    assert rsa_pkcs1v15_verify(key.n, key.e, f"date: {hdrs['Date']}".encode(), sig)
+
+
+def test_sigv4_get_vanilla_vector():
+    """AWS SigV4 test suite 'get-vanilla'."""
+    now = datetime.datetime(2015, 8, 30, 12, 36, 0)
+    hdrs = sigv4_headers("GET", "https://example.amazonaws.com/", b"", "AKIDEXAMPLE",
+                         "wJalrXUtnFEMI/K7MDENG+bPxRfiCYEXAMPLEKEY", "us-east-1", "service", now=now)
+    assert hdrs["Authorization"] == (
+        "AWS4-HMAC-SHA256 Credential=AKIDEXAMPLE/20150830/us-east-1/service/aws4_request, "
+        "SignedHeaders=host;x-amz-date, "
+        "Signature=5fa00fa31553b73ebf1942676e86291e8372ff2a2260956d9b8aae1d763fbf31")
+
+
+def test_gcp_jwt_rs256(tmp_path):
+    key_path = make_ssh_key(tmp_path / "sa")
+    key = load_private_key(key_path)
+    creds = {"client_email": "sa@p.iam.gserviceaccount.com", "private_key": open(key_path).read(),
+             "private_key_id": "abc"}
+    jwt = make_jwt(creds, "scope", now=1000)
+    head, claims, sig = jwt.split(".")
+    pad = lambda s: s + "=" * (-len(s) % 4)  # noqa: E731
+    assert json.loads(base64.urlsafe_b64decode(pad(head))) == {"alg": "RS256", "typ": "JWT", "kid": "abc"}
+    c = json.loads(base64.urlsafe_b64decode(pad(claims)))
+    assert c["iss"] == creds["client_email"] and c["exp"] == 4600
+    assert rsa_pkcs1v15_verify(key.n, key.e, f"{head}.{claims}".encode(), base64.urlsafe_b64decode(pad(sig)))
+
+
+def test_fingerprint_matches_ssh_keygen(tmp_path):
+    import subprocess
+
+    for kind in ("rsa", "ed25519", "ecdsa"):
+        path = make_ssh_key(tmp_path / f"k_{kind}", kind)
+        want = subprocess.run(["ssh-keygen", "-l", "-E", "md5", "-f", path], capture_output=True,
+                              text=True).stdout.split()[1]
+        assert want == "MD5:" + load_private_key(path).fingerprint_md5()
+
+
+def test_encrypted_key_needs_passphrase(tmp_path):
+    import subprocess
+
+    from triton_kubernetes_amd.utils.sshkeys import public_key_fingerprint
+
+    path = str(tmp_path / "enc")
+    subprocess.run(["ssh-keygen", "-q", "-t", "rsa", "-b", "2048", "-m", "PEM", "-N", "hunter22", "-f", path],
+                   check=True)
+    with pytest.raises(TKError) as exc:
+        public_key_fingerprint(path)  # non-interactive: no hanging prompt (Q14)
+    assert str(exc.value).startswith("Unable to parse private key:")
+    assert public_key_fingerprint(path, lambda: "hunter22") == load_private_key(path, "hunter22").fingerprint_md5()

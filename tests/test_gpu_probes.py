@@ -91,3 +91,16 @@ def test_labeller_executable():
     proc = subprocess.run([executable("amdgpu-topo-labeller")], capture_output=True, text=True, timeout=120)
     assert proc.returncode == 0, proc.stdout + proc.stderr
     assert json.loads(proc.stdout)["gpus"]
+
+
+def test_native_labels_match_python_spec():
+    """``amdgpu-topo-labeller --labels`` (C++) == labels_from_topology(JSON) (Python)."""
+    from triton_kubernetes_amd.node.labels import labels_from_topology
+    from triton_kubernetes_amd.ops import topo
+
+    native = topo.amdsmi_labels()
+    spec = labels_from_topology(topo.amdsmi_topology())
+    print(json.dumps(native, sort_keys=True))
+    assert native == spec
+    assert native["amd.com/gpu.product-name"] == "MI355X"
+    assert native["amd.com/gpu.target"] == "gfx950"

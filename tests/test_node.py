@@ -1,0 +1,217 @@
+"""Node layer: bootstrap plans (shell + agent renderers), GPU labels, KFD topology, node agent."""
+
+import json
+import os
+import subprocess
+
+import pytest
+
+from triton_kubernetes_amd.node.agent import NodeAgent
+from triton_kubernetes_amd.node.labels import agent_label_flags, labels_from_topology, product_name, synthetic_topology
+from triton_kubernetes_amd.node.plan import BootstrapPlan, build_host_plan, parse_step_markers
+from triton_kubernetes_amd.ops.topo import kfd_topology
+from triton_kubernetes_amd.parallel.transport import HostRef, LocalTransport
+
+WORKER = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}}
+GPU_WORKER = dict(WORKER, gpu_count=8, gpu_burnin="quick", rccl_env={"NCCL_MIN_NCHANNELS": "32"})
+
+
+def _bash_syntax_ok(script: str) -> None:
+    proc = subprocess.run(["bash", "-n"], input=script, capture_output=True, text=True, check=False)
+    assert proc.returncode == 0, proc.stderr
+
+
+def test_plan_steps_and_order():
+    plain = build_host_plan(WORKER, "https://r", "tok", "sum")
+    assert plain.step_names() == ["firewall", "runtime", "hostname", "agent"]
+    assert plain.gpu is None
+    gpu = build_host_plan(dict(GPU_WORKER, rancher_registry="reg.io", rancher_registry_username="u",
+                               rancher_registry_password="p"), "https://r", "tok", "sum", mi355x=True)
+    # burn-in precedes labels so the agent's topology prefetch overlaps it
+    assert gpu.step_names() == ["firewall", "runtime", "hostname", "registry_login", "gpu_preflight",
+                                "gpu_burnin", "gpu_labels", "rccl_env", "rccl_local", "agent"]
+    assert gpu.gpu == {"product": "MI355X", "count": 8, "burnin": "quick"}
+    off = build_host_plan(dict(GPU_WORKER, gpu_burnin="off", gpu_count=1), "https://r", "t", "s", mi355x=True)
+    assert "gpu_burnin" not in off.step_names() and "rccl_local" not in off.step_names()
+
+
+@pytest.mark.parametrize("mi355x", [False, True])
+def test_rendered_shell_is_valid_bash(mi355x):
+    plan = build_host_plan(dict(GPU_WORKER, hostname="x; rm -rf /"), "https://r", "t'ok", "sum", mi355x=mi355x)
+    script = plan.render_shell()
+    _bash_syntax_ok(script)
+    assert "'x; rm -rf /'" in script  # quoted, never spliced raw
+    if mi355x:
+        assert "--label" in script and 'NCCL_MIN_NCHANNELS="32"' in script
+
+
+def test_plan_json_roundtrip():
+    plan = build_host_plan(GPU_WORKER, "https://r", "tok", "sum", mi355x=True)
+    back = BootstrapPlan.from_json(json.loads(json.dumps(plan.to_json())))
+    assert back == plan
+
+
+def test_step_markers():
+    out = "noise\n::tk-step firewall start 0\n::tk-step firewall ok 12\n::tk-step agent failed 7\n"
+    assert parse_step_markers(out) == {"firewall": {"status": "ok", "ms": 12}, "agent": {"status": "failed", "ms": 7}}
+
+
+def _fake_bin(d, name, body):
+    p = d / name
+    p.write_text("#!/bin/bash\n" + body + "\n")
+    p.chmod(0o755)
+
+
+def test_local_transport_runs_plan_with_stub_tools(tmp_path):
+    """The rendered script runs end to end with stub sudo/docker; markers + the agent argv come back."""
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "sudo.log"
+    _fake_bin(bindir, "sudo", f'echo "$*" >> {log}; cat >/dev/null 2>&1 || true')
+    _fake_bin(bindir, "docker", "exit 0")
+    env = {"PATH": f"{bindir}:/usr/bin:/bin"}
+    plan = build_host_plan(WORKER, "https://rancher.example", "regtok", "cafe", mi355x=False)
+    res = LocalTransport(env=env).run_plan(HostRef("local"), plan)
+    assert res["ok"], res
+    assert [s["name"] for s in res["steps"]] == plan.step_names()
+    calls = log.read_text()
+    assert "hostnamectl set-hostname gpu-1" in calls
+    assert "--server https://rancher.example --token regtok --ca-checksum cafe --worker" in calls
+
+
+def test_local_transport_reports_failed_step(tmp_path):
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    _fake_bin(bindir, "sudo", 'case "$*" in hostnamectl*) exit 3;; esac; cat >/dev/null')
+    _fake_bin(bindir, "docker", "exit 0")
+    plan = build_host_plan(WORKER, "https://r", "t", "s")
+    res = LocalTransport(env={"PATH": f"{bindir}:/usr/bin:/bin"}).run_plan(HostRef("local"), plan)
+    assert not res["ok"]
+    assert "hostname" in (res.get("error") or "")
+
+
+def test_labels_from_synthetic_topology():
+    labels = labels_from_topology(synthetic_topology(8))
+    assert labels["amd.com/gpu.count"] == "8"
+    assert labels["amd.com/gpu.product-name"] == "MI355X"
+    assert labels["amd.com/gpu.family"] == "AI"
+    assert labels["amd.com/gpu.vram"] == "288G"
+    assert labels["amd.com/gpu.compute-partition"] == "spx"
+    assert labels["amd.com/xgmi.fully-connected"] == "true"
+    assert labels["amd.com/xgmi.links-per-gpu"] == "7"
+    assert labels["amd.com/xgmi.hive-id"] == "0xabc123"
+    assert labels_from_topology({"gpus": []}) == {"amd.com/gpu.present": "false"}
+    flags = agent_label_flags({"b": "2", "a": "1"})
+    assert flags == ["--label", "a=1", "--label", "b=2"]
+
+
+def test_product_name_device_id_wins():
+    # amd_smi's market name for an MI355X OAM part does not carry the X
+    assert product_name("AMD Instinct MI355 OAM", "0x75a3") == "MI355X"
+    assert product_name("AMD Instinct MI300X", "0xdead") == "MI300X"
+    assert product_name("weird name!", "") == "weird-name"
+
+
+def test_partial_xgmi_mesh_not_fully_connected():
+    topo = synthetic_topology(4)
+    topo["gpus"][0]["links"] = [lk for lk in topo["gpus"][0]["links"] if lk["peer"] != 3]
+    labels = labels_from_topology(topo)
+    assert labels["amd.com/xgmi.fully-connected"] == "false"
+    assert labels["amd.com/xgmi.links-per-gpu"] == "2"
+
+
+def _kfd_node(root, idx, props, name="", links=()):
+    d = root / str(idx)
+    (d / "io_links").mkdir(parents=True)
+    (d / "properties").write_text("".join(f"{k} {v}\n" for k, v in props.items()))
+    (d / "name").write_text(name + "\n")
+    for i, (to, typ) in enumerate(links):
+        ld = d / "io_links" / str(i)
+        ld.mkdir()
+        (ld / "properties").write_text(f"node_from {idx}\nnode_to {to}\ntype {typ}\nweight 15\n")
+
+
+def test_kfd_topology_fixture(tmp_path):
+    """A CPU node + two gfx950 GPU nodes linked by xGMI (type 11), as KFD sysfs lays it out."""
+    _kfd_node(tmp_path, 0, {"simd_count": 0, "cpu_cores_count": 96})
+    gpu = {"simd_count": 1024, "simd_per_cu": 4, "gfx_target_version": 90500, "device_id": 0x75a3,
+           "hive_id": 0x1234, "domain": 0, "location_id": 0x0500}
+    _kfd_node(tmp_path, 1, gpu, "", [(0, 2), (2, 11)])
+    _kfd_node(tmp_path, 2, dict(gpu, location_id=0x0600), "", [(0, 2), (1, 11)])
+    doc = kfd_topology(str(tmp_path))
+    assert doc["source"] == "kfd" and len(doc["gpus"]) == 2
+    g0 = doc["gpus"][0]
+    assert g0["compute_units"] == 256 and g0["target_graphics_version"] == "gfx950"
+    assert g0["bdf"] == "0000:05:00.0"
+    assert g0["links"] == [{"peer": 1, "type": "XGMI", "hops": 1, "p2p": True}]
+    labels = labels_from_topology(doc)
+    assert labels["amd.com/gpu.product-name"] == "MI355X"
+    assert labels["amd.com/xgmi.fully-connected"] == "true"
+    assert labels["amd.com/xgmi.hive-id"] == "0x1234"
+
+
+def test_agent_sim_plan_without_rancher_reaches_agent_step(tmp_path):
+    """GPU steps run against synthetic GPUs; files land under the agent root."""
+    calls = []
+
+    def burn(dev, level):
+        calls.append((dev, level))
+        return {"ok": True, "device": dev}
+
+    agent = NodeAgent("n1", "sim", devices=list(range(8)), root=str(tmp_path), token="t",
+                      topology_override=synthetic_topology(8), burnin_override=burn)
+    plan = build_host_plan(GPU_WORKER, "http://127.0.0.1:9", "tok", "sum", mi355x=True)
+    plan.steps = [s for s in plan.steps if s.action != "agent"]
+    res = agent.run_plan(plan)
+    assert res["ok"], res
+    assert sorted(calls) == [(d, "quick") for d in range(8)]
+    assert res["capacity"] == {"amd.com/gpu": 8}
+    assert res["labels"]["amd.com/gpu.count"] == "8"
+    assert (tmp_path / "etc/triton-kubernetes/gpu-labels").read_text().startswith("amd.com/")
+    assert 'NCCL_MIN_NCHANNELS="32"' in (tmp_path / "etc/rccl/rccl.env").read_text()
+
+
+def test_agent_burnin_failure_stops_plan(tmp_path):
+    agent = NodeAgent("n1", "sim", devices=[0, 1], root=str(tmp_path), token="t",
+                      topology_override=synthetic_topology(2),
+                      burnin_override=lambda d, lvl: {"ok": d != 1, "failures": ["hbm"]})
+    res = agent.run_plan(build_host_plan(dict(GPU_WORKER, gpu_count=2), "http://x", "t", "s", mi355x=True))
+    assert not res["ok"] and res["error"].startswith("gpu_burnin")
+    assert "gpu_labels" not in [s["name"] for s in res["steps"]]
+
+
+def test_agent_preflight_counts_gpus(tmp_path):
+    agent = NodeAgent("n1", "sim", devices=[0], root=str(tmp_path), token="t",
+                      topology_override=synthetic_topology(1))
+    res = agent.run_plan(build_host_plan(GPU_WORKER, "http://x", "t", "s", mi355x=True))
+    assert not res["ok"] and "expected 8 GPUs, found 1" in res["error"]
+
+
+def test_agent_http_requires_token(tmp_path):
+    from triton_kubernetes_amd.cloud.http import HTTPClient, HTTPError
+
+    agent = NodeAgent("n1", "sim", root=str(tmp_path), token="sekrit")
+    url = agent.serve()
+    try:
+        with pytest.raises(Exception) as exc:
+            HTTPClient(base_url=url).request("GET", "/v1/info")
+        assert "401" in str(exc.value) or isinstance(exc.value, HTTPError)
+        info = HTTPClient(base_url=url).request("GET", "/v1/info", headers={"X-TK-Agent-Token": "sekrit"}).json()
+        assert info["name"] == "n1"
+    finally:
+        agent.stop()
+
+
+def test_agent_rejects_bad_mode():
+    with pytest.raises(ValueError):
+        NodeAgent("n", "shell")
+    assert NodeAgent("n").token  # a token is always generated
+
+
+def test_exec_mode_validates_hostname(tmp_path):
+    agent = NodeAgent("n1", "exec", root=str(tmp_path), token="t")
+    plan = build_host_plan(dict(WORKER, hostname="bad host;reboot"), "http://x", "t", "s")
+    plan.steps = [s for s in plan.steps if s.action == "hostname"]
+    res = agent.run_plan(plan)
+    assert not res["ok"] and "invalid hostname" in res["error"]
+    assert os.path.exists(tmp_path) and not agent.history[-1]["ok"]

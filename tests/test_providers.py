@@ -13,7 +13,7 @@ from triton_kubernetes_amd.errors import TKError
 from triton_kubernetes_amd.models import aws, azure, baremetal, gcp, triton, vsphere
 from triton_kubernetes_amd.state import State
 
-from helpers import make_ctx, make_ssh_key
+from helpers import assert_blocks_match_modules, make_ctx, make_ssh_key
 
 BASE_MGR = {"rancher_admin_password": "pw"}
 BASE_CLUSTER = {"name": "dev", "k8s_version": "v1.9.5-rancher1-1", "k8s_network_provider": "flannel"}
@@ -48,6 +48,7 @@ def test_baremetal_manager_document():
     assert m["source"] == "github.com/joyent/triton-kubernetes//terraform/modules/bare-metal-rancher?ref=master"
     assert list(m) == ["source", "name", "rancher_admin_password", "host", "ssh_user", "key_path"]
     assert m["key_path"] == "~/.ssh/id_rsa"  # not expanded (reference quirk Q11 kept)
+    assert_blocks_match_modules(st)
 
 
 def test_baremetal_manager_required_keys():
@@ -84,6 +85,7 @@ def test_baremetal_cluster_and_nodes():
     more = baremetal.new_node(make_ctx(dict(NODE_BASE, node_count=1, ssh_user="u", bastion_host="", key_path="k",
                                             hosts=["10.0.0.3"])), "mgr", key, None, st)
     assert more == ["dev-w-3"]
+    assert_blocks_match_modules(st)
 
 
 def test_baremetal_node_errors():
@@ -117,6 +119,7 @@ def test_mi355x_node_and_addons():
     assert n["source"].endswith("terraform/modules/bare-metal-mi355x-rancher-k8s-host?ref=master")
     assert n["gpu_count"] == "8" and n["gpu_burnin"] == "quick" and n["gpu_product"] == "MI355X"
     assert n["rccl_env"]["NCCL_SOCKET_IFNAME"] == "eth0" and n["rccl_env"]["HSA_FORCE_FINE_GRAIN_PCIE"] == "1"
+    assert_blocks_match_modules(st)
     bad = make_ctx(dict(NODE_BASE, ssh_user="u", bastion_host="", key_path="k", gpu="h100", hosts=["a", "b"]))
     assert "Invalid gpu 'h100'" in _err(baremetal.new_node, bad, "m", key, None, st)
 
@@ -182,6 +185,7 @@ def test_triton_manager_cluster_node(key):
     n = st.module(f"node_triton_dev_{hosts[0]}")
     assert n["triton_account"] == "acct"  # copied by value from the cluster
     assert n["triton_machine_package"] == "k4-highcpu-kvm-7.75G"
+    assert_blocks_match_modules(st)
 
 
 def test_triton_validation_errors(key):
@@ -236,6 +240,7 @@ def test_aws_manager_cluster_node(tmp_path):
     hosts = aws.new_node(make_ctx(dict(NODE_BASE, aws_ami_id="a", aws_instance_type="t"), cloud=cloud), "mgr",
                          ckey, None, st)
     assert "ebs_volume_device_name" not in st.module(f"node_aws_dev_{hosts[0]}")
+    assert_blocks_match_modules(st)
 
 
 def test_aws_validation_errors():
@@ -289,6 +294,7 @@ def test_gcp_manager_cluster_node(gcp_creds, key, tmp_path):
     n = st.module(f"node_gcp_dev_{hosts[0]}")
     assert n["gcp_compute_network_name"] == "${module.cluster_gcp_dev.gcp_compute_network_name}"
     assert n["gcp_disk_type"] == ""
+    assert_blocks_match_modules(st)
     bad = make_ctx(dict(NODE_BASE, gcp_instance_zone="us-east1-b", gcp_machine_type="x", gcp_image="y"), cloud=cloud)
     assert _err(gcp.new_node, bad, "m", ckey, None, st) == "Selected GCP Instance Zone 'us-east1-b' does not exist."
 
@@ -314,6 +320,7 @@ def test_azure_manager_cluster_node(tmp_path, key):
                                          azure_disk_size="100"), cloud=cloud), "m", ckey, None, st)
     n = st.module(f"node_azure_dev_{hosts[0]}")
     assert n["azure_subnet_id"] == "${module.cluster_azure_dev.azure_subnet_id}" and n["azure_disk_size"] == "100"
+    assert_blocks_match_modules(st)
     bad = make_ctx(dict(NODE_BASE, azure_size="Standard_A0", azure_ssh_user="u", azure_public_key_path=str(pub),
                         azure_disk_mount_path="/data"), cloud=cloud)
     assert _err(azure.new_node, bad, "m", ckey, None, st) == \
@@ -341,5 +348,6 @@ def test_vsphere_cluster_and_node(key):
     n = st.module(f"node_vsphere_dev_{hosts[0]}")
     assert n["vsphere_datastore_name"] == "${module.cluster_vsphere_dev.vsphere_datastore_name}"
     assert n["vsphere_num_cpus"] == "16" and n["vsphere_user"] == "u"
+    assert_blocks_match_modules(st)
     vals.pop("vsphere_user")
     assert _err(vsphere.new_cluster, make_ctx(vals), None, st) == "vsphere_user must be specified."

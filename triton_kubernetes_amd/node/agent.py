@@ -29,6 +29,7 @@ HTTP API (JSON): ``GET /v1/info``, ``POST /v1/plan``, ``POST /v1/rccl-gate``
 """
 
 import base64
+import concurrent.futures as cf
 import hmac
 import http.server
 import json
@@ -116,6 +117,12 @@ class NodeAgent:
         ctx: Dict[str, Any] = {"labels": {}, "capacity": {}}
         t_plan = time.perf_counter()
         error = None
+        prefetch = None
+        if any(s.action == "gpu_labels" for s in plan.steps):
+            # topology discovery (amd_smi, host-side only) overlaps the preflight
+            # and burn-in kernels instead of running after them
+            prefetch = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="topo")
+            ctx["topology_future"] = prefetch.submit(self._topology)
         with self.lock:
             for step in plan.steps:
                 t0 = time.perf_counter()
@@ -127,6 +134,8 @@ class NodeAgent:
                     results.append(StepResult(step.name, False, (time.perf_counter() - t0) * 1e3, str(exc)))
                     error = f"{step.name}: {exc}"
                     break
+        if prefetch is not None:
+            prefetch.shutdown(wait=False)
         doc = {"hostname": plan.hostname, "ok": error is None, "error": error,
                "ms": (time.perf_counter() - t_plan) * 1e3,
                "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"]}
@@ -184,7 +193,8 @@ class NodeAgent:
         if a == "gpu_preflight":
             return self._gpu_preflight(int(step.params.get("count", len(self.devices))))
         if a == "gpu_labels":
-            topo = self._topology()
+            fut = ctx.get("topology_future")
+            topo = fut.result() if fut is not None else self._topology()
             labels = labels_from_topology(topo)
             ctx["labels"].update(labels)
             self.last_labels = labels
@@ -194,9 +204,16 @@ class NodeAgent:
             return labels
         if a == "gpu_burnin":
             level = step.params.get("level", "quick")
+            # every GPU of the node burns in concurrently (one host thread each;
+            # the probes pin their device per thread)
+            if len(self.devices) > 1:
+                with cf.ThreadPoolExecutor(max_workers=len(self.devices)) as pool:
+                    results = dict(zip(self.devices, pool.map(lambda d: self._burnin(d, level), self.devices)))
+            else:
+                results = {d: self._burnin(d, level) for d in self.devices}
             out = {}
             for dev in self.devices:
-                res = self._burnin(dev, level)
+                res = results[dev]
                 out[str(dev)] = res
                 if not res.get("ok", False):
                     raise StepFailed(step.name, f"GPU {dev}: {res.get('failures')}")

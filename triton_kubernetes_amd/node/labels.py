@@ -37,7 +37,15 @@ def _label_value(v: Any) -> str:
     return s[:63]
 
 
-def product_name(market_name: str) -> str:
+# PCI device id -> product, for parts whose market name is not the SKU name
+# (amd_smi reports an MI355X as "AMD Instinct MI355 OAM").  Mirrored in
+# ops/csrc/tk_topo.cpp:product_from_device_id.
+DEVICE_PRODUCTS = {"0x75a3": "MI355X", "0x74a5": "MI325X", "0x74a1": "MI300X"}
+
+
+def product_name(market_name: str, device_id: str = "") -> str:
+    if str(device_id).lower() in DEVICE_PRODUCTS:
+        return DEVICE_PRODUCTS[str(device_id).lower()]
     m = re.search(r"(MI\d{3}[A-Z]*)", market_name or "")
     return m.group(1) if m else _label_value(market_name)
 
@@ -50,7 +58,8 @@ def labels_from_topology(doc: Dict[str, Any]) -> Dict[str, str]:
         "amd.com/gpu.present": "true",
         "amd.com/gpu.count": str(len(gpus)),
     }
-    names = {product_name(g.get("market_name", "")) for g in gpus if g.get("market_name")}
+    names = {product_name(g.get("market_name", ""), g.get("device_id", "")) for g in gpus
+             if g.get("market_name") or str(g.get("device_id", "")).lower() in DEVICE_PRODUCTS}
     if len(names) == 1:
         name = names.pop()
         labels["amd.com/gpu.product-name"] = _label_value(name)

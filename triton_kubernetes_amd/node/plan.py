@@ -89,11 +89,17 @@ class BootstrapPlan:
         for s in self.steps:
             body = s.shell.strip("\n")
             out.append(f"step_{s.name}() {{")
-            out.extend("  " + ln if ln else "" for ln in body.splitlines())
+            # bodies are emitted verbatim: indenting them would break heredoc terminators
+            out.extend(body.splitlines())
             out.append("}")
+        # one compound command: bash parses all of it before running a step, and
+        # the steps' stdin is /dev/null, so a step that reads stdin cannot eat the
+        # rest of a script delivered through `bash -s`
+        out.append("{")
         for s in self.steps:
             out.append(f"_tk_step {s.name} step_{s.name}")
         out.append("echo '::tk-done'")
+        out.append("} </dev/null")
         return "\n".join(out) + "\n"
 
 
@@ -151,14 +157,17 @@ test -d /dev/dri || {{ echo '/dev/dri missing' >&2; exit 1; }}
 n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
 [ "$n" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs, found $n render nodes" >&2; exit 1; }}
 sudo usermod -aG video,render "$(id -un)" || true""", {"count": ngpu}, gpu=True))
+        # burn-in before labels: the agent discovers the topology concurrently
+        # with the burn-in kernels and only joins it at the labels step
+        if burnin != "off":
+            plan.steps.append(Step("gpu_burnin", "gpu_burnin", f"""
+sudo mkdir -p /etc/triton-kubernetes
+{TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} | sudo tee /etc/triton-kubernetes/gpu-burnin.json""",
+                                   {"level": burnin}, gpu=True))
         plan.steps.append(Step("gpu_labels", "gpu_labels", f"""
 sudo mkdir -p "$(dirname {LABEL_FILE})"
 {TOOLS_DIR}/amdgpu-topo-labeller | sudo tee {TOPOLOGY_FILE} >/dev/null
 {TOOLS_DIR}/amdgpu-topo-labeller --labels | sudo tee {LABEL_FILE} >/dev/null""", gpu=True))
-        if burnin != "off":
-            plan.steps.append(Step("gpu_burnin", "gpu_burnin", f"""
-{TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} | sudo tee /etc/triton-kubernetes/gpu-burnin.json""",
-                                   {"level": burnin}, gpu=True))
         plan.steps.append(Step("rccl_env", "rccl_env", f"""
 sudo mkdir -p "$(dirname {RCCL_ENV_FILE})"
 sudo tee {RCCL_ENV_FILE} >/dev/null <<'TK_RCCL_EOF'

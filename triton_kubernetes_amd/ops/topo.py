@@ -37,6 +37,20 @@ def amdsmi_topology(timeout: float = 60.0) -> Dict[str, Any]:
     return doc
 
 
+def amdsmi_labels(timeout: float = 60.0) -> Dict[str, str]:
+    """``amdgpu-topo-labeller --labels``: the node labels computed natively."""
+    exe = executable("amdgpu-topo-labeller")
+    proc = subprocess.run([exe, "--labels"], capture_output=True, text=True, timeout=timeout, check=False)
+    if proc.returncode != 0:
+        raise NativeUnavailable(f"amdgpu-topo-labeller --labels failed (rc={proc.returncode}): {proc.stderr[-500:]}")
+    out: Dict[str, str] = {}
+    for ln in proc.stdout.splitlines():
+        if ln.startswith("amd.com/") and "=" in ln:
+            k, v = ln.split("=", 1)
+            out[k] = v
+    return out
+
+
 def amdsmi_topology_inprocess() -> Dict[str, Any]:
     lib = load("libtk_topo.so")
     lib.tkt_topology_json.argtypes = [ctypes.c_char_p, ctypes.c_size_t]

@@ -274,7 +274,12 @@ def parse_private_key(text: str, passphrase: Optional[str] = None) -> PrivateKey
     elif label == "EC PRIVATE KEY":
         key = _ec_from_sec1(der)
     elif label == "OPENSSH PRIVATE KEY":
-        key = _from_openssh(der)
+        try:
+            key = _from_openssh(der)
+        except KeyParseError as exc:
+            if "passphrase" not in str(exc) or passphrase is None:
+                raise
+            return parse_private_key(_openssh_decrypt(text, passphrase))
     else:
         raise KeyParseError(f"ssh: unsupported key type \"{label}\"")
     key.pem = text
@@ -282,13 +287,27 @@ def parse_private_key(text: str, passphrase: Optional[str] = None) -> PrivateKey
 
 
 def _openssl_decrypt(text: str, passphrase: str) -> str:
-    proc = subprocess.run(
-        ["openssl", "pkey", "-passin", "stdin", "-traditional"],
-        input=(passphrase + "\n" + text).encode(), capture_output=True, check=False,
-    )
+    """Decrypt an encrypted PEM key (passphrase passed through the environment)."""
+    env = dict(os.environ, TK_KEY_PASS=passphrase)
+    proc = subprocess.run(["openssl", "pkey", "-passin", "env:TK_KEY_PASS", "-traditional"],
+                          input=text.encode(), capture_output=True, check=False, env=env)
     if proc.returncode != 0:
         raise KeyParseError("x509: decryption password incorrect")
     return proc.stdout.decode()
+
+
+def _openssh_decrypt(text: str, passphrase: str) -> str:
+    """Decrypt an encrypted OpenSSH-format key on a private temp copy via ssh-keygen."""
+    with tempfile.TemporaryDirectory(prefix="tk-key-") as d:
+        path = os.path.join(d, "key")
+        with open(os.open(path, os.O_WRONLY | os.O_CREAT, 0o600), "w") as fh:
+            fh.write(text)
+        proc = subprocess.run(["ssh-keygen", "-q", "-p", "-P", passphrase, "-N", "", "-f", path],
+                              capture_output=True, check=False)
+        if proc.returncode != 0:
+            raise KeyParseError("ssh: incorrect passphrase")
+        with open(path, "r", encoding="utf-8") as fh:
+            return fh.read()
 
 
 def load_private_key(path: str, passphrase: Optional[str] = None) -> PrivateKey:
