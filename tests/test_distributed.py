@@ -1,0 +1,50 @@
+"""Multi-process paths on CPU: the bench harness under torchrun with the gloo control group.
+
+``--sim-gpu`` swaps the GPU steps for synthetic topology / no-op burn-in, so this
+checks the distributed plumbing (agent URL all-gather, barriers, max-over-ranks
+timing, rank-0 JSON line) — never a measurement.
+"""
+
+import json
+import os
+import socket
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _free_port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("nproc", [2, 4])
+def test_bench_torchrun_gloo(nproc):
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--sim-gpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, proc.stdout  # rank 0 only
+    doc = json.loads(lines[0])
+    assert doc["n_gpus"] == nproc and doc["steps"] == 2 and doc["warmup"] == 1
+    assert doc["higher_is_better"] is False and doc["scaling"] == "weak" and doc["vs_baseline"] is None
+    assert doc["config"]["workers"] == nproc
+    assert doc["data"].startswith("SIM-GPU DRY RUN")
+    assert doc["value"] > 0 and abs(doc["ms_per_step"] - doc["value"] * 1000) < 1.0
+    # every worker was bootstrapped through its own rank's agent
+    assert doc["phase_ms_per_step"]["module.host"] > 0
+
+
+def test_bench_single_process_default():
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
+                           "--sim-gpu"], capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert proc.returncode == 0, proc.stderr[-2000:]
+    doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["n_gpus"] == 1 and doc["unit"] == "s"
