@@ -94,13 +94,22 @@ def test_labeller_executable():
 
 
 def test_native_labels_match_python_spec():
-    """``amdgpu-topo-labeller --labels`` (C++) == labels_from_topology(JSON) (Python)."""
+    """amd_smi and sysfs collectors (C++) agree, and both equal labels_from_topology (Python)."""
+    import time
+
     from triton_kubernetes_amd.node.labels import labels_from_topology
     from triton_kubernetes_amd.ops import topo
 
-    native = topo.amdsmi_labels()
-    spec = labels_from_topology(topo.amdsmi_topology())
-    print(json.dumps(native, sort_keys=True))
-    assert native == spec
-    assert native["amd.com/gpu.product-name"] == "MI355X"
-    assert native["amd.com/gpu.target"] == "gfx950"
+    t0 = time.perf_counter()
+    via_amdsmi = topo.amdsmi_labels(source="amdsmi")
+    t1 = time.perf_counter()
+    via_sysfs = topo.native_labels("sysfs")
+    t2 = time.perf_counter()
+    print(json.dumps({"amdsmi_ms": (t1 - t0) * 1e3, "sysfs_inprocess_ms": (t2 - t1) * 1e3}))
+    print(json.dumps(via_sysfs, sort_keys=True))
+    assert via_sysfs == via_amdsmi
+    assert via_amdsmi == labels_from_topology(topo.amdsmi_topology())
+    assert via_sysfs == labels_from_topology(topo.native_topology("sysfs"))
+    assert via_sysfs["amd.com/gpu.product-name"] == "MI355X"
+    assert via_sysfs["amd.com/gpu.target"] == "gfx950"
+    assert via_sysfs["amd.com/gpu.vram"] == "288G"

@@ -6,7 +6,9 @@
     triton-kubernetes version
 
 Additions: ``wait cluster`` (the readiness waiter on an existing cluster),
-``gpu …`` (the native MI355X probes) and ``agent`` (the node agent).
+``gpu …`` (the native MI355X probes), ``agent`` (the node agent) and
+``image`` (machine-image templates -> Packer JSON, the reference's
+``packer/packer-config``).
 
 Exit codes follow the reference: argument errors exit 255 (``os.Exit(-1)``),
 workflow errors print the message and exit 1.  The dead ``-t/--toggle`` scaffold
@@ -84,6 +86,8 @@ def build_parser() -> argparse.ArgumentParser:
     g.add_argument("gpu_args", nargs=argparse.REMAINDER)
     a = sub.add_parser("agent", help="Run the node agent (tk-node-agent)")
     a.add_argument("agent_args", nargs=argparse.REMAINDER)
+    i = sub.add_parser("image", help="Render a machine-image template to Packer JSON (packer-config)")
+    i.add_argument("image_args", nargs=argparse.REMAINDER)
     return root
 
 
@@ -119,6 +123,10 @@ def run(argv: Sequence[str], out: Optional[TextIO] = None, ctx=None) -> int:
         from ..node.agent import main as agent_main
 
         return agent_main(ns.agent_args)
+    if ns.command == "image":
+        from ..images.packer import main as image_main
+
+        return image_main(ns.image_args)
     try:
         what = _check_args(ns.command, ns.args)
     except ArgError as exc:

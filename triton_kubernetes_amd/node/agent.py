@@ -119,7 +119,7 @@ class NodeAgent:
         error = None
         prefetch = None
         if any(s.action == "gpu_labels" for s in plan.steps):
-            # topology discovery (amd_smi, host-side only) overlaps the preflight
+            # topology discovery (host-side sysfs reads) overlaps the preflight
             # and burn-in kernels instead of running after them
             prefetch = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="topo")
             ctx["topology_future"] = prefetch.submit(self._topology)

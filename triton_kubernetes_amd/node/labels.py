@@ -40,7 +40,7 @@ def _label_value(v: Any) -> str:
 # PCI device id -> product, for parts whose market name is not the SKU name
 # (amd_smi reports an MI355X as "AMD Instinct MI355 OAM").  Mirrored in
 # ops/csrc/tk_topo.cpp:product_from_device_id.
-DEVICE_PRODUCTS = {"0x75a3": "MI355X", "0x74a5": "MI325X", "0x74a1": "MI300X"}
+DEVICE_PRODUCTS = {"0x75a3": "MI355X", "0x75a0": "MI350X", "0x74a5": "MI325X", "0x74a1": "MI300X"}
 
 
 def product_name(market_name: str, device_id: str = "") -> str:
@@ -73,7 +73,8 @@ def labels_from_topology(doc: Dict[str, Any]) -> Dict[str, str]:
         labels["amd.com/gpu.cu-count"] = str(min(cus))
     vram = [int(g["vram_mb"]) for g in gpus if g.get("vram_mb")]
     if vram:
-        labels["amd.com/gpu.vram"] = f"{min(vram) // 1024}G"
+        # nearest GiB: the 294896 MiB an MI355X reports reads as 288G
+        labels["amd.com/gpu.vram"] = f"{(min(vram) + 512) // 1024}G"
     targets = {g.get("target_graphics_version") for g in gpus if g.get("target_graphics_version")}
     if len(targets) == 1:
         labels["amd.com/gpu.target"] = _label_value(targets.pop())

@@ -1,23 +1,32 @@
-// amdgpu-topo-labeller (N1): enumerate the node's AMD GPUs
-// through libamd_smi and emit one JSON document describing each GPU and every
-// GPU<->GPU link.  triton_kubernetes_amd.node.labels turns it into Kubernetes
-// node labels (product, count, CU count, VRAM, partition modes, xGMI hive id,
-// links per GPU, fully-connected flag) used by the device plugin, the
+// amdgpu-topo-labeller (N1): describe the node's AMD GPUs and
+// every GPU<->GPU link as one JSON document, or as the Kubernetes node labels
+// derived from it (product, count, CU count, VRAM, partition modes, xGMI hive
+// id, links per GPU, fully-connected flag) used by the device plugin, the
 // readiness waiter and xGMI-aware pod affinity.
+//
+// Two collectors fill the same GpuInfo records:
+//   amdsmi  libamd_smi (amdsmi_init + per-processor queries);
+//   sysfs   the KFD topology (/sys/class/kfd/kfd/topology/nodes) joined with
+//           the DRM device attributes (/sys/class/drm/renderD<minor>/device):
+//           plain file reads, no library state — ~1 ms instead of the tens of
+//           ms amdsmi_init costs, and safe inside a process that also runs HIP.
+// tests/test_gpu_probes.py checks on an MI355X that both give identical labels.
 //
 // Built twice from this file: libtk_topo.so (C ABI, loaded with ctypes) and the
 // stand-alone `amdgpu-topo-labeller` executable (-DTK_TOPO_MAIN) that the
 // bare-metal host bootstrap runs on nodes without Python tooling.
 
 #include <amd_smi/amdsmi.h>
+#include <dirent.h>
 
 #include <algorithm>
 #include <cctype>
 #include <cinttypes>
 #include <climits>
-#include <cstdint>
 #include <cstdarg>
+#include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <set>
@@ -26,58 +35,15 @@
 
 namespace {
 
-std::string esc(const char* s) {
+std::string esc(const std::string& s) {
   std::string o;
-  for (const char* p = s; *p; ++p) {
-    const unsigned char c = static_cast<unsigned char>(*p);
+  for (unsigned char c : s) {
     if (c == '"' || c == '\\') { o += '\\'; o += static_cast<char>(c); }
     else if (c < 0x20) { char b[8]; snprintf(b, sizeof(b), "\\u%04x", c); o += b; }
     else o += static_cast<char>(c);
   }
   return o;
 }
-
-const char* link_name(amdsmi_link_type_t t) {
-  switch (t) {
-    case AMDSMI_LINK_TYPE_INTERNAL: return "INTERNAL";
-    case AMDSMI_LINK_TYPE_PCIE: return "PCIE";
-    case AMDSMI_LINK_TYPE_XGMI: return "XGMI";
-    case AMDSMI_LINK_TYPE_NOT_APPLICABLE: return "NA";
-    default: return "UNKNOWN";
-  }
-}
-
-struct Link {
-  size_t peer;
-  const char* type;
-  uint64_t hops;
-  bool p2p;
-};
-
-// Everything the labeller knows about one GPU; the JSON document and the
-// label set are both rendered from this.
-struct GpuInfo {
-  amdsmi_processor_handle h{};
-  bool has_enum = false, has_bdf = false, has_asic = false, has_vram = false, has_numa = false;
-  bool has_xgmi = false, has_ecc = false;
-  amdsmi_enumeration_info_t en{};
-  amdsmi_bdf_t bdf{};
-  amdsmi_asic_info_t asic{};
-  amdsmi_vram_info_t vram{};
-  uint32_t numa = 0;
-  std::string compute_partition, memory_partition;
-  amdsmi_xgmi_info_t xg{};
-  amdsmi_error_count_t ec{};
-  std::vector<Link> links;
-};
-
-struct Topology {
-  int status = 0;
-  std::string error;
-  bool has_driver = false;
-  amdsmi_driver_info_t drv{};
-  std::vector<GpuInfo> gpus;
-};
 
 void appendf(std::string& o, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 void appendf(std::string& o, const char* fmt, ...) {
@@ -89,8 +55,55 @@ void appendf(std::string& o, const char* fmt, ...) {
   o += buf;
 }
 
-Topology collect() {
+struct Link {
+  size_t peer;
+  std::string type;  // XGMI | PCIE | ...
+  uint64_t hops;
+  bool p2p;
+};
+
+// Everything the labeller knows about one GPU, collector-independent.
+struct GpuInfo {
+  int64_t hip_id = -1, drm_render = -1, drm_card = -1;
+  std::string bdf, market_name, vendor_id, device_id, serial, gfx, compute_partition, memory_partition;
+  int64_t rev_id = -1, compute_units = -1, oam_id = -1, numa_node = -1;
+  uint64_t vram_mb = 0;
+  uint32_t vram_bit_width = 0;
+  bool has_xgmi = false, has_ecc = false;
+  uint64_t hive_id = 0, xgmi_node_id = 0;
+  uint32_t xgmi_lanes = 0;
+  uint64_t ecc_correctable = 0, ecc_uncorrectable = 0;
+  std::vector<Link> links;
+};
+
+struct Topology {
+  std::string source;
+  int status = 0;
+  std::string error;
+  std::string driver_name, driver_version;
+  std::vector<GpuInfo> gpus;
+};
+
+std::string hex64(uint64_t v) {
+  char b[32];
+  snprintf(b, sizeof(b), "0x%" PRIx64, v);
+  return b;
+}
+
+// ---------------------------------------------------------------- amd_smi --
+const char* link_name(amdsmi_link_type_t t) {
+  switch (t) {
+    case AMDSMI_LINK_TYPE_INTERNAL: return "INTERNAL";
+    case AMDSMI_LINK_TYPE_PCIE: return "PCIE";
+    case AMDSMI_LINK_TYPE_XGMI: return "XGMI";
+    case AMDSMI_LINK_TYPE_NOT_APPLICABLE: return "NA";
+    default: return "UNKNOWN";
+  }
+}
+
+Topology collect_amdsmi() {
   Topology t;
+  t.source = "amd_smi";
   amdsmi_status_t st = amdsmi_init(AMDSMI_INIT_AMD_GPUS);
   if (st != AMDSMI_STATUS_SUCCESS) {
     const char* msg = nullptr;
@@ -99,6 +112,7 @@ Topology collect() {
     t.status = static_cast<int>(st);
     return t;
   }
+  std::vector<amdsmi_processor_handle> hs;
   uint32_t nsock = 0;
   amdsmi_get_socket_handles(&nsock, nullptr);
   std::vector<amdsmi_socket_handle> socks(nsock);
@@ -110,91 +124,313 @@ Topology collect() {
     if (np) amdsmi_get_processor_handles(socks[s], &np, ph.data());
     for (auto h : ph) {
       processor_type_t pt;
-      if (amdsmi_get_processor_type(h, &pt) == AMDSMI_STATUS_SUCCESS && pt == AMDSMI_PROCESSOR_TYPE_AMD_GPU) {
-        t.gpus.emplace_back();
-        t.gpus.back().h = h;
-      }
+      if (amdsmi_get_processor_type(h, &pt) == AMDSMI_STATUS_SUCCESS && pt == AMDSMI_PROCESSOR_TYPE_AMD_GPU)
+        hs.push_back(h);
     }
   }
-  if (!t.gpus.empty())
-    t.has_driver = amdsmi_get_gpu_driver_info(t.gpus[0].h, &t.drv) == AMDSMI_STATUS_SUCCESS;
-  for (size_t i = 0; i < t.gpus.size(); ++i) {
-    GpuInfo& g = t.gpus[i];
-    auto h = g.h;
-    g.has_enum = amdsmi_get_gpu_enumeration_info(h, &g.en) == AMDSMI_STATUS_SUCCESS;
-    g.has_bdf = amdsmi_get_gpu_device_bdf(h, &g.bdf) == AMDSMI_STATUS_SUCCESS;
-    g.has_asic = amdsmi_get_gpu_asic_info(h, &g.asic) == AMDSMI_STATUS_SUCCESS;
-    g.has_vram = amdsmi_get_gpu_vram_info(h, &g.vram) == AMDSMI_STATUS_SUCCESS;
-    g.has_numa = amdsmi_topo_get_numa_node_number(h, &g.numa) == AMDSMI_STATUS_SUCCESS;
+  amdsmi_driver_info_t drv{};
+  if (!hs.empty() && amdsmi_get_gpu_driver_info(hs[0], &drv) == AMDSMI_STATUS_SUCCESS) {
+    t.driver_name = drv.driver_name;
+    t.driver_version = drv.driver_version;
+  }
+  for (size_t i = 0; i < hs.size(); ++i) {
+    auto h = hs[i];
+    GpuInfo g;
+    amdsmi_enumeration_info_t en{};
+    if (amdsmi_get_gpu_enumeration_info(h, &en) == AMDSMI_STATUS_SUCCESS) {
+      g.hip_id = en.hip_id;
+      g.drm_render = en.drm_render;
+      g.drm_card = en.drm_card;
+    }
+    amdsmi_bdf_t bdf{};
+    if (amdsmi_get_gpu_device_bdf(h, &bdf) == AMDSMI_STATUS_SUCCESS) {
+      char b[32];
+      snprintf(b, sizeof(b), "%04" PRIx64 ":%02" PRIx64 ":%02" PRIx64 ".%" PRIx64, (uint64_t)bdf.domain_number,
+               (uint64_t)bdf.bus_number, (uint64_t)bdf.device_number, (uint64_t)bdf.function_number);
+      g.bdf = b;
+    }
+    amdsmi_asic_info_t a{};
+    if (amdsmi_get_gpu_asic_info(h, &a) == AMDSMI_STATUS_SUCCESS) {
+      g.market_name = a.market_name;
+      char b[16];
+      snprintf(b, sizeof(b), "0x%x", a.vendor_id);
+      g.vendor_id = b;
+      g.device_id = hex64(a.device_id);
+      g.rev_id = a.rev_id;
+      g.serial = a.asic_serial;
+      if (a.num_of_compute_units != 0xFFFFFFFFu) g.compute_units = a.num_of_compute_units;
+      if (a.oam_id != 0xFFFFFFFFu) g.oam_id = a.oam_id;
+      if (a.target_graphics_version != 0xFFFFFFFFFFFFFFFFull) {
+        char gb[32];
+        snprintf(gb, sizeof(gb), "gfx%" PRIx64, a.target_graphics_version);
+        g.gfx = gb;
+      }
+    }
+    amdsmi_vram_info_t vram{};
+    if (amdsmi_get_gpu_vram_info(h, &vram) == AMDSMI_STATUS_SUCCESS) {
+      g.vram_mb = vram.vram_size;
+      g.vram_bit_width = vram.vram_bit_width;
+    }
+    uint32_t numa = 0;
+    if (amdsmi_topo_get_numa_node_number(h, &numa) == AMDSMI_STATUS_SUCCESS) g.numa_node = numa;
     char part[64] = {0};
     if (amdsmi_get_gpu_compute_partition(h, part, sizeof(part)) == AMDSMI_STATUS_SUCCESS) g.compute_partition = part;
     memset(part, 0, sizeof(part));
     if (amdsmi_get_gpu_memory_partition(h, part, sizeof(part)) == AMDSMI_STATUS_SUCCESS) g.memory_partition = part;
-    g.has_xgmi = amdsmi_get_xgmi_info(h, &g.xg) == AMDSMI_STATUS_SUCCESS;
-    g.has_ecc = amdsmi_get_gpu_total_ecc_count(h, &g.ec) == AMDSMI_STATUS_SUCCESS;
-    for (size_t j = 0; j < t.gpus.size(); ++j) {
+    amdsmi_xgmi_info_t xg{};
+    if (amdsmi_get_xgmi_info(h, &xg) == AMDSMI_STATUS_SUCCESS) {
+      g.has_xgmi = true;
+      g.hive_id = xg.xgmi_hive_id;
+      g.xgmi_node_id = xg.xgmi_node_id;
+      g.xgmi_lanes = xg.xgmi_lanes;
+    }
+    amdsmi_error_count_t ec{};
+    if (amdsmi_get_gpu_total_ecc_count(h, &ec) == AMDSMI_STATUS_SUCCESS) {
+      g.has_ecc = true;
+      g.ecc_correctable = ec.correctable_count;
+      g.ecc_uncorrectable = ec.uncorrectable_count;
+    }
+    for (size_t j = 0; j < hs.size(); ++j) {
       if (j == i) continue;
       uint64_t hops = 0;
       amdsmi_link_type_t lt = AMDSMI_LINK_TYPE_UNKNOWN;
-      if (amdsmi_topo_get_link_type(h, t.gpus[j].h, &hops, &lt) != AMDSMI_STATUS_SUCCESS) continue;
+      if (amdsmi_topo_get_link_type(h, hs[j], &hops, &lt) != AMDSMI_STATUS_SUCCESS) continue;
       bool p2p = false;
-      amdsmi_is_P2P_accessible(h, t.gpus[j].h, &p2p);
+      amdsmi_is_P2P_accessible(h, hs[j], &p2p);
       g.links.push_back({j, link_name(lt), hops, p2p});
     }
+    t.gpus.push_back(std::move(g));
   }
   amdsmi_shut_down();
   return t;
 }
 
+// ------------------------------------------------------------------ sysfs --
+bool read_file(const std::string& path, std::string* out) {
+  FILE* f = fopen(path.c_str(), "r");
+  if (!f) return false;
+  char buf[4096];
+  size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  fclose(f);
+  buf[n] = 0;
+  *out = buf;
+  while (!out->empty() && (out->back() == '\n' || out->back() == ' ')) out->pop_back();
+  return true;
+}
+
+// "key value" lines (KFD properties files).
+std::map<std::string, uint64_t> read_props(const std::string& path) {
+  std::map<std::string, uint64_t> m;
+  std::string s;
+  if (!read_file(path, &s)) return m;
+  size_t pos = 0;
+  while (pos < s.size()) {
+    size_t e = s.find('\n', pos);
+    if (e == std::string::npos) e = s.size();
+    const std::string line = s.substr(pos, e - pos);
+    pos = e + 1;
+    const size_t sp = line.find(' ');
+    if (sp == std::string::npos) continue;
+    char* end = nullptr;
+    const std::string v = line.substr(sp + 1);
+    const unsigned long long x = strtoull(v.c_str(), &end, 10);
+    if (end && *end == 0) m[line.substr(0, sp)] = x;
+  }
+  return m;
+}
+
+std::vector<int> numeric_entries(const std::string& dir) {
+  std::vector<int> ids;
+  DIR* d = opendir(dir.c_str());
+  if (!d) return ids;
+  while (dirent* e = readdir(d)) {
+    const char* n = e->d_name;
+    if (!*n) continue;
+    bool num = true;
+    for (const char* p = n; *p; ++p) num = num && isdigit(static_cast<unsigned char>(*p));
+    if (num) ids.push_back(atoi(n));
+  }
+  closedir(d);
+  std::sort(ids.begin(), ids.end());
+  return ids;
+}
+
+uint64_t prop(const std::map<std::string, uint64_t>& m, const char* k, uint64_t dflt = 0) {
+  auto it = m.find(k);
+  return it == m.end() ? dflt : it->second;
+}
+
+// gfx_target_version 90500 -> "gfx950" (major*10000 + minor*100 + stepping; minor/stepping print as hex digits)
+std::string gfx_name(uint64_t v) {
+  if (!v) return "";
+  char b[32];
+  snprintf(b, sizeof(b), "gfx%" PRIu64 "%" PRIx64 "%" PRIx64, v / 10000, (v / 100) % 100, v % 100);
+  return b;
+}
+
+// PCI device id -> market name, for the sysfs path (amd_smi reads it from the
+// ASIC).  Mirrored in node/labels.py:DEVICE_PRODUCTS.
+const char* market_from_device_id(uint64_t id) {
+  switch (id) {
+    case 0x75a3: return "AMD Instinct MI355X";
+    case 0x75a0: return "AMD Instinct MI350X";
+    case 0x74a5: return "AMD Instinct MI325X";
+    case 0x74a1: return "AMD Instinct MI300X";
+    default: return nullptr;
+  }
+}
+
+Topology collect_sysfs(const std::string& root) {
+  Topology t;
+  t.source = "sysfs";
+  const std::string kfd = root + "/sys/class/kfd/kfd/topology/nodes";
+  struct Node {
+    int kfd_node;
+    std::map<std::string, uint64_t> p;
+  };
+  const std::vector<int> all = numeric_entries(kfd);
+  if (all.empty()) {
+    t.status = 2;
+    t.error = "no KFD topology at " + kfd;
+    return t;
+  }
+  std::vector<Node> nodes;
+  for (int id : all) {
+    auto p = read_props(kfd + "/" + std::to_string(id) + "/properties");
+    if (prop(p, "simd_count") > 0) nodes.push_back({id, std::move(p)});
+  }
+  std::map<int, size_t> kfd_to_index;
+  for (size_t i = 0; i < nodes.size(); ++i) kfd_to_index[nodes[i].kfd_node] = i;
+  std::string ver;
+  if (read_file(root + "/sys/module/amdgpu/version", &ver)) t.driver_version = ver;
+  t.driver_name = "amdgpu";
+  for (size_t i = 0; i < nodes.size(); ++i) {
+    const auto& p = nodes[i].p;
+    GpuInfo g;
+    g.hip_id = static_cast<int64_t>(i);
+    const uint64_t minor = prop(p, "drm_render_minor", UINT64_MAX);
+    if (minor != UINT64_MAX) g.drm_render = static_cast<int64_t>(minor);
+    const uint64_t loc = prop(p, "location_id");
+    char b[64];
+    snprintf(b, sizeof(b), "%04" PRIx64 ":%02" PRIx64 ":%02" PRIx64 ".%" PRIx64, prop(p, "domain"),
+             (loc >> 8) & 0xff, (loc >> 3) & 0x1f, loc & 7);
+    g.bdf = b;
+    const uint64_t did = prop(p, "device_id");
+    snprintf(b, sizeof(b), "0x%" PRIx64, prop(p, "vendor_id"));
+    g.vendor_id = b;
+    g.device_id = hex64(did);
+    const uint64_t spc = prop(p, "simd_per_cu", 4) ? prop(p, "simd_per_cu", 4) : 4;
+    g.compute_units = static_cast<int64_t>(prop(p, "simd_count") / spc);
+    g.gfx = gfx_name(prop(p, "gfx_target_version"));
+    if (p.count("hive_id")) {
+      g.has_xgmi = true;
+      g.hive_id = prop(p, "hive_id");
+    }
+    if (const uint64_t uid = prop(p, "unique_id")) {
+      snprintf(b, sizeof(b), "%" PRIx64, uid);
+      g.serial = b;
+    }
+    // local memory: the KFD mem bank(s) of this node
+    const std::string nd = kfd + "/" + std::to_string(nodes[i].kfd_node);
+    uint64_t vram = 0;
+    for (int mb : numeric_entries(nd + "/mem_banks")) {
+      auto mp = read_props(nd + "/mem_banks/" + std::to_string(mb) + "/properties");
+      vram += prop(mp, "size_in_bytes");
+      if (!g.vram_bit_width) g.vram_bit_width = static_cast<uint32_t>(prop(mp, "width"));
+    }
+    // DRM device attributes (partition modes, VRAM total, NUMA node, RAS counters)
+    const std::string dev = root + "/sys/class/drm/renderD" + std::to_string(minor) + "/device";
+    std::string s;
+    if (read_file(dev + "/mem_info_vram_total", &s)) vram = strtoull(s.c_str(), nullptr, 10);
+    g.vram_mb = vram >> 20;
+    if (read_file(dev + "/current_compute_partition", &s)) g.compute_partition = s;
+    if (read_file(dev + "/current_memory_partition", &s)) g.memory_partition = s;
+    if (read_file(dev + "/numa_node", &s)) g.numa_node = std::max<int64_t>(0, atoll(s.c_str()));
+    if (read_file(dev + "/product_name", &s) && !s.empty()) g.market_name = s;
+    if (g.market_name.empty()) {
+      const char* m = market_from_device_id(did);
+      g.market_name = m ? m : "";
+    }
+    DIR* ras = opendir((dev + "/ras").c_str());
+    if (ras) {
+      while (dirent* e = readdir(ras)) {
+        const std::string n = e->d_name;
+        if (n.size() < 10 || n.compare(n.size() - 10, 10, "_err_count") != 0) continue;
+        std::string c;
+        if (!read_file(dev + "/ras/" + n, &c)) continue;
+        unsigned long long ue = 0, ce = 0;
+        const char* q = strstr(c.c_str(), "ue:");
+        if (q) ue = strtoull(q + 3, nullptr, 10);
+        q = strstr(c.c_str(), "ce:");
+        if (q) ce = strtoull(q + 3, nullptr, 10);
+        g.has_ecc = true;
+        g.ecc_uncorrectable += ue;
+        g.ecc_correctable += ce;
+      }
+      closedir(ras);
+    }
+    // links to other GPU nodes (io_links: direct; p2p_links: indirect peers)
+    std::set<size_t> seen;
+    for (const char* sub : {"io_links", "p2p_links"}) {
+      for (int l : numeric_entries(nd + "/" + sub)) {
+        auto lp = read_props(nd + "/" + sub + "/" + std::to_string(l) + "/properties");
+        auto it = kfd_to_index.find(static_cast<int>(prop(lp, "node_to", UINT64_MAX)));
+        if (it == kfd_to_index.end() || it->second == i || seen.count(it->second)) continue;
+        seen.insert(it->second);
+        const uint64_t type = prop(lp, "type");
+        const bool xgmi = type == 11;
+        g.links.push_back({it->second, xgmi ? "XGMI" : (type == 2 ? "PCIE" : "OTHER"), 1, xgmi});
+      }
+    }
+    t.gpus.push_back(std::move(g));
+  }
+  return t;
+}
+
+// ------------------------------------------------------------ renderers ----
 std::string render_json(const Topology& t) {
   std::string o;
   if (t.status != 0) {
-    appendf(o, "{\"source\":\"amd_smi\",\"error\":\"%s\",\"gpus\":[]}", esc(t.error.c_str()).c_str());
+    appendf(o, "{\"source\":\"%s\",\"error\":\"%s\",\"gpus\":[]}", t.source.c_str(), esc(t.error).c_str());
     return o;
   }
-  o += "{\"source\":\"amd_smi\",";
-  if (t.has_driver)
-    appendf(o, "\"driver\":{\"name\":\"%s\",\"version\":\"%s\"},", esc(t.drv.driver_name).c_str(),
-            esc(t.drv.driver_version).c_str());
+  appendf(o, "{\"source\":\"%s\",", t.source.c_str());
+  if (!t.driver_name.empty())
+    appendf(o, "\"driver\":{\"name\":\"%s\",\"version\":\"%s\"},", esc(t.driver_name).c_str(),
+            esc(t.driver_version).c_str());
   o += "\"gpus\":[";
   for (size_t i = 0; i < t.gpus.size(); ++i) {
     const GpuInfo& g = t.gpus[i];
     if (i) o += ",";
     appendf(o, "{\"index\":%zu", i);
-    if (g.has_enum)
-      appendf(o, ",\"hip_id\":%u,\"drm_render\":%u,\"drm_card\":%u", g.en.hip_id, g.en.drm_render, g.en.drm_card);
-    if (g.has_bdf)
-      appendf(o, ",\"bdf\":\"%04" PRIx64 ":%02" PRIx64 ":%02" PRIx64 ".%" PRIx64 "\"",
-              (uint64_t)g.bdf.domain_number, (uint64_t)g.bdf.bus_number, (uint64_t)g.bdf.device_number,
-              (uint64_t)g.bdf.function_number);
-    if (g.has_asic) {
-      const amdsmi_asic_info_t& a = g.asic;
-      appendf(o, ",\"market_name\":\"%s\",\"vendor_id\":\"0x%x\",\"device_id\":\"0x%" PRIx64 "\",\"rev_id\":%u",
-              esc(a.market_name).c_str(), a.vendor_id, a.device_id, a.rev_id);
-      appendf(o, ",\"asic_serial\":\"%s\"", esc(a.asic_serial).c_str());
-      if (a.num_of_compute_units != 0xFFFFFFFFu) appendf(o, ",\"compute_units\":%u", a.num_of_compute_units);
-      if (a.oam_id != 0xFFFFFFFFu) appendf(o, ",\"oam_id\":%u", a.oam_id);
-      if (a.target_graphics_version != 0xFFFFFFFFFFFFFFFFull)
-        appendf(o, ",\"target_graphics_version\":\"gfx%" PRIx64 "\"", a.target_graphics_version);
-    }
-    if (g.has_vram)
-      appendf(o, ",\"vram_mb\":%" PRIu64 ",\"vram_bit_width\":%u", g.vram.vram_size, g.vram.vram_bit_width);
-    if (g.has_numa) appendf(o, ",\"numa_node\":%u", g.numa);
+    if (g.hip_id >= 0) appendf(o, ",\"hip_id\":%" PRId64, g.hip_id);
+    if (g.drm_render >= 0) appendf(o, ",\"drm_render\":%" PRId64, g.drm_render);
+    if (g.drm_card >= 0) appendf(o, ",\"drm_card\":%" PRId64, g.drm_card);
+    if (!g.bdf.empty()) appendf(o, ",\"bdf\":\"%s\"", g.bdf.c_str());
+    if (!g.market_name.empty()) appendf(o, ",\"market_name\":\"%s\"", esc(g.market_name).c_str());
+    if (!g.vendor_id.empty()) appendf(o, ",\"vendor_id\":\"%s\"", g.vendor_id.c_str());
+    if (!g.device_id.empty()) appendf(o, ",\"device_id\":\"%s\"", g.device_id.c_str());
+    if (g.rev_id >= 0) appendf(o, ",\"rev_id\":%" PRId64, g.rev_id);
+    if (!g.serial.empty()) appendf(o, ",\"asic_serial\":\"%s\"", esc(g.serial).c_str());
+    if (g.compute_units >= 0) appendf(o, ",\"compute_units\":%" PRId64, g.compute_units);
+    if (g.oam_id >= 0) appendf(o, ",\"oam_id\":%" PRId64, g.oam_id);
+    if (!g.gfx.empty()) appendf(o, ",\"target_graphics_version\":\"%s\"", g.gfx.c_str());
+    if (g.vram_mb) appendf(o, ",\"vram_mb\":%" PRIu64 ",\"vram_bit_width\":%u", g.vram_mb, g.vram_bit_width);
+    if (g.numa_node >= 0) appendf(o, ",\"numa_node\":%" PRId64, g.numa_node);
     if (!g.compute_partition.empty())
-      appendf(o, ",\"compute_partition\":\"%s\"", esc(g.compute_partition.c_str()).c_str());
-    if (!g.memory_partition.empty())
-      appendf(o, ",\"memory_partition\":\"%s\"", esc(g.memory_partition.c_str()).c_str());
+      appendf(o, ",\"compute_partition\":\"%s\"", esc(g.compute_partition).c_str());
+    if (!g.memory_partition.empty()) appendf(o, ",\"memory_partition\":\"%s\"", esc(g.memory_partition).c_str());
     if (g.has_xgmi)
-      appendf(o, ",\"xgmi_hive_id\":\"0x%" PRIx64 "\",\"xgmi_node_id\":\"0x%" PRIx64 "\",\"xgmi_lanes\":%u",
-              g.xg.xgmi_hive_id, g.xg.xgmi_node_id, (unsigned)g.xg.xgmi_lanes);
+      appendf(o, ",\"xgmi_hive_id\":\"%s\",\"xgmi_node_id\":\"%s\",\"xgmi_lanes\":%u", hex64(g.hive_id).c_str(),
+              hex64(g.xgmi_node_id).c_str(), g.xgmi_lanes);
     if (g.has_ecc)
-      appendf(o, ",\"ecc_correctable\":%" PRIu64 ",\"ecc_uncorrectable\":%" PRIu64, g.ec.correctable_count,
-              g.ec.uncorrectable_count);
+      appendf(o, ",\"ecc_correctable\":%" PRIu64 ",\"ecc_uncorrectable\":%" PRIu64, g.ecc_correctable,
+              g.ecc_uncorrectable);
     o += ",\"links\":[";
     for (size_t k = 0; k < g.links.size(); ++k) {
       const Link& l = g.links[k];
-      appendf(o, "%s{\"peer\":%zu,\"type\":\"%s\",\"hops\":%" PRIu64 ",\"p2p\":%s}", k ? "," : "", l.peer, l.type,
-              l.hops, l.p2p ? "true" : "false");
+      appendf(o, "%s{\"peer\":%zu,\"type\":\"%s\",\"hops\":%" PRIu64 ",\"p2p\":%s}", k ? "," : "", l.peer,
+              l.type.c_str(), l.hops, l.p2p ? "true" : "false");
     }
     o += "]}";
   }
@@ -204,8 +440,7 @@ std::string render_json(const Topology& t) {
 
 // --- node labels -----------------------------------------------------------
 // Same rules as triton_kubernetes_amd/node/labels.py:labels_from_topology (the
-// Python side is the spec and is unit-tested; tests/test_labels.py checks this
-// renderer against it on the box).
+// Python side is the spec; tests compare the two on fixtures and on the box).
 
 // Kubernetes label value: [A-Za-z0-9._-], trimmed of leading/trailing '-._', <= 63.
 std::string label_value(const std::string& v) {
@@ -219,24 +454,22 @@ std::string label_value(const std::string& v) {
 
 // PCI device id -> product, for parts whose market name is not the SKU name
 // (amd_smi reports an MI355X as "AMD Instinct MI355 OAM").
-const char* product_from_device_id(uint64_t id) {
-  switch (id) {
-    case 0x75a3: return "MI355X";
-    case 0x74a5: return "MI325X";
-    case 0x74a1: return "MI300X";
-    default: return nullptr;
-  }
+const char* product_from_device_id(const std::string& id) {
+  static const std::map<std::string, const char*> m = {
+      {"0x75a3", "MI355X"}, {"0x75a0", "MI350X"}, {"0x74a5", "MI325X"}, {"0x74a1", "MI300X"}};
+  auto it = m.find(id);
+  return it == m.end() ? nullptr : it->second;
 }
 
 std::string product_name(const GpuInfo& g) {
-  if (const char* p = product_from_device_id(g.asic.device_id)) return p;
-  const char* m = g.asic.market_name;
-  for (const char* p = m; *p; ++p) {
-    if (p[0] == 'M' && p[1] == 'I' && isdigit((unsigned char)p[2]) && isdigit((unsigned char)p[3]) &&
-        isdigit((unsigned char)p[4])) {
-      const char* e = p + 5;
-      while (*e >= 'A' && *e <= 'Z') ++e;
-      return std::string(p, e);
+  if (const char* p = product_from_device_id(g.device_id)) return p;
+  const std::string& m = g.market_name;
+  for (size_t i = 0; i + 4 < m.size(); ++i) {
+    if (m[i] == 'M' && m[i + 1] == 'I' && isdigit((unsigned char)m[i + 2]) && isdigit((unsigned char)m[i + 3]) &&
+        isdigit((unsigned char)m[i + 4])) {
+      size_t e = i + 5;
+      while (e < m.size() && m[e] >= 'A' && m[e] <= 'Z') ++e;
+      return m.substr(i, e - i);
     }
   }
   return label_value(m);
@@ -256,36 +489,24 @@ std::string render_labels(const Topology& t) {
     L["amd.com/gpu.present"] = "true";
     L["amd.com/gpu.count"] = std::to_string(gs.size());
     std::set<std::string> names, dev_ids, targets, cparts, mparts, hives;
-    uint32_t min_cu = UINT32_MAX;
+    int64_t min_cu = INT64_MAX;
     uint64_t min_vram = UINT64_MAX;
     size_t min_xgmi = SIZE_MAX;
     uint64_t ecc = 0;
     for (const auto& g : gs) {
-      if (g.has_asic) {
-        if (g.asic.market_name[0] || product_from_device_id(g.asic.device_id)) names.insert(product_name(g));
-        char b[32];
-        snprintf(b, sizeof(b), "0x%" PRIx64, g.asic.device_id);
-        if (g.asic.device_id) dev_ids.insert(b);
-        if (g.asic.num_of_compute_units != 0xFFFFFFFFu && g.asic.num_of_compute_units)
-          min_cu = std::min(min_cu, g.asic.num_of_compute_units);
-        if (g.asic.target_graphics_version != 0xFFFFFFFFFFFFFFFFull) {
-          snprintf(b, sizeof(b), "gfx%" PRIx64, g.asic.target_graphics_version);
-          targets.insert(b);
-        }
-      }
-      if (g.has_vram && g.vram.vram_size) min_vram = std::min<uint64_t>(min_vram, g.vram.vram_size);
+      if (!g.market_name.empty() || product_from_device_id(g.device_id)) names.insert(product_name(g));
+      if (!g.device_id.empty() && g.device_id != "0x0") dev_ids.insert(g.device_id);
+      if (g.compute_units > 0) min_cu = std::min(min_cu, g.compute_units);
+      if (g.vram_mb) min_vram = std::min(min_vram, g.vram_mb);
+      if (!g.gfx.empty()) targets.insert(g.gfx);
       if (!g.compute_partition.empty()) cparts.insert(lower(g.compute_partition));
       if (!g.memory_partition.empty()) mparts.insert(lower(g.memory_partition));
-      if (g.has_xgmi && g.xg.xgmi_hive_id) {
-        char b[32];
-        snprintf(b, sizeof(b), "0x%" PRIx64, g.xg.xgmi_hive_id);
-        hives.insert(b);
-      }
+      if (g.has_xgmi && g.hive_id) hives.insert(hex64(g.hive_id));
       std::set<size_t> peers;
       for (const auto& l : g.links)
-        if (strcmp(l.type, "XGMI") == 0) peers.insert(l.peer);
+        if (l.type == "XGMI") peers.insert(l.peer);
       min_xgmi = std::min(min_xgmi, peers.size());
-      if (g.has_ecc) ecc += g.ec.uncorrectable_count;
+      ecc += g.ecc_uncorrectable;
     }
     if (names.size() == 1) {
       const std::string n = *names.begin();
@@ -293,8 +514,9 @@ std::string render_labels(const Topology& t) {
       if (n.rfind("MI", 0) == 0) L["amd.com/gpu.family"] = "AI";
     }
     if (dev_ids.size() == 1) L["amd.com/gpu.device-id"] = label_value(*dev_ids.begin());
-    if (min_cu != UINT32_MAX) L["amd.com/gpu.cu-count"] = std::to_string(min_cu);
-    if (min_vram != UINT64_MAX) L["amd.com/gpu.vram"] = std::to_string(min_vram / 1024) + "G";
+    if (min_cu != INT64_MAX) L["amd.com/gpu.cu-count"] = std::to_string(min_cu);
+    // nearest GiB: the 294896 MiB an MI355X reports reads as 288G
+    if (min_vram != UINT64_MAX) L["amd.com/gpu.vram"] = std::to_string((min_vram + 512) / 1024) + "G";
     if (targets.size() == 1) L["amd.com/gpu.target"] = label_value(*targets.begin());
     if (cparts.size() == 1) L["amd.com/gpu.compute-partition"] = label_value(*cparts.begin());
     if (mparts.size() == 1) L["amd.com/gpu.memory-partition"] = label_value(*mparts.begin());
@@ -308,43 +530,73 @@ std::string render_labels(const Topology& t) {
   return o;
 }
 
+Topology collect(const char* source, const char* root) {
+  const std::string src = source ? source : "auto";
+  const std::string r = (root && *root) ? root : "";
+  if (src == "sysfs") return collect_sysfs(r);
+  if (src == "amdsmi") return collect_amdsmi();
+  Topology t = collect_amdsmi();
+  if (t.status != 0 || t.gpus.empty()) {
+    Topology s = collect_sysfs(r);
+    if (s.status == 0) return s;
+  }
+  return t;
+}
+
+int copy_out(const std::string& j, char* buf, size_t len) {
+  if (j.size() + 1 > len) return -static_cast<int>(j.size() + 1);
+  memcpy(buf, j.c_str(), j.size() + 1);
+  return 0;
+}
+
 }  // namespace
 
-// Writes the JSON document into buf (NUL-terminated).  Returns 0 on success,
-// the amdsmi status on init failure (buf still holds a JSON error document),
-// or -(required size) if buf is too small.
-extern "C" int tkt_topology_json(char* buf, size_t len) {
-  const Topology t = collect();
-  const std::string j = render_json(t);
-  if (j.size() + 1 > len) return -static_cast<int>(j.size() + 1);
-  memcpy(buf, j.c_str(), j.size() + 1);
-  return t.status;
+// Writes the JSON document into buf (NUL-terminated).  source: "amdsmi",
+// "sysfs" or "auto" (amd_smi, sysfs when it fails); root prefixes the sysfs
+// paths (fixture trees in tests; NULL/"" for the live system).  Returns 0 on
+// success, the collector status on failure (buf still holds a JSON error
+// document), or -(required size) if buf is too small.
+extern "C" int tkt_topology_json_src(const char* source, const char* root, char* buf, size_t len) {
+  const Topology t = collect(source, root);
+  const int rc = copy_out(render_json(t), buf, len);
+  return rc < 0 ? rc : t.status;
 }
 
-// Same contract as tkt_topology_json, but the payload is the `key=value\n`
-// node label set.
-extern "C" int tkt_topology_labels(char* buf, size_t len) {
-  const Topology t = collect();
-  const std::string j = t.status == 0 ? render_labels(t) : std::string();
-  if (j.size() + 1 > len) return -static_cast<int>(j.size() + 1);
-  memcpy(buf, j.c_str(), j.size() + 1);
-  return t.status;
+// Same contract; the payload is the `key=value\n` node label set.
+extern "C" int tkt_topology_labels_src(const char* source, const char* root, char* buf, size_t len) {
+  const Topology t = collect(source, root);
+  const int rc = copy_out(t.status == 0 ? render_labels(t) : std::string(), buf, len);
+  return rc < 0 ? rc : t.status;
 }
+
+extern "C" int tkt_topology_json(char* buf, size_t len) { return tkt_topology_json_src("amdsmi", "", buf, len); }
+
+extern "C" int tkt_topology_labels(char* buf, size_t len) { return tkt_topology_labels_src("amdsmi", "", buf, len); }
 
 #ifdef TK_TOPO_MAIN
-// amdgpu-topo-labeller            topology JSON on stdout
-// amdgpu-topo-labeller --labels   one `amd.com/...=value` node label per line
+// amdgpu-topo-labeller [--labels] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
+//   default: topology JSON on stdout; --labels: one `amd.com/...=value` per line
 int main(int argc, char** argv) {
   bool labels = false;
+  const char* source = "auto";
+  const char* root = "";
   for (int i = 1; i < argc; ++i) {
     if (strcmp(argv[i], "--labels") == 0) {
       labels = true;
+    } else if (strcmp(argv[i], "--source") == 0 && i + 1 < argc) {
+      source = argv[++i];
+    } else if (strcmp(argv[i], "--sysfs-root") == 0 && i + 1 < argc) {
+      root = argv[++i];
     } else {
-      fprintf(stderr, "usage: %s [--labels]\n", argv[0]);
+      fprintf(stderr, "usage: %s [--labels] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]\n", argv[0]);
       return 64;
     }
   }
-  const Topology t = collect();
+  if (strcmp(source, "auto") != 0 && strcmp(source, "amdsmi") != 0 && strcmp(source, "sysfs") != 0) {
+    fprintf(stderr, "unknown --source '%s'\n", source);
+    return 64;
+  }
+  const Topology t = collect(source, root);
   if (labels) {
     if (t.status != 0) {
       fprintf(stderr, "amdgpu-topo-labeller: %s\n", t.error.c_str());

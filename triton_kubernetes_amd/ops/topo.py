@@ -1,9 +1,15 @@
-"""Node GPU topology (N1): amd_smi via ``libtk_topo.so``, with a KFD-sysfs fallback.
+"""Node GPU topology (N1): the native labeller ``csrc/tk_topo.cpp``.
 
-``discover()`` returns the JSON document of ``csrc/tk_topo.cpp``.  When the
-amd_smi path cannot run (no driver, old ROCm), the same document shape is
-derived from the KFD topology in ``/sys/class/kfd/kfd/topology/nodes`` — also
-the path the unit tests exercise with a fixture tree.
+``discover()`` returns its JSON document.  Sources, in the order tried:
+
+1. ``sysfs`` in-process (``libtk_topo.so``): KFD topology + DRM attributes,
+   plain file reads (~1 ms) — the default on the bootstrap critical path;
+2. ``amdsmi`` out of process (``amdgpu-topo-labeller``): amd_smi's own view,
+   kept in a child process so its library state never shares an address
+   space with HIP/RCCL (tens of ms, mostly ``amdsmi_init``);
+3. the pure-Python KFD reader below when no native build is present.
+
+The GPU tests assert that sources 1 and 2 yield identical node labels.
 """
 
 import ctypes
@@ -21,14 +27,15 @@ _KFD_LINK_TYPES = {11: "XGMI", 2: "PCIE"}
 GFX_TARGETS = {90500: "gfx950", 90400: "gfx942", 90402: "gfx942", 90010: "gfx90a"}
 
 
-def amdsmi_topology(timeout: float = 60.0) -> Dict[str, Any]:
+def amdsmi_topology(timeout: float = 60.0, source: str = "amdsmi") -> Dict[str, Any]:
     """Run the ``amdgpu-topo-labeller`` executable (amd_smi in its own process).
 
     Kept out of process on purpose: amd_smi's library state and teardown then
     never share an address space with the HIP runtime / RCCL of the caller.
     """
     exe = executable("amdgpu-topo-labeller")
-    proc = subprocess.run([exe], capture_output=True, text=True, timeout=timeout, check=False)
+    proc = subprocess.run([exe, "--source", source], capture_output=True, text=True, timeout=timeout,
+                          check=False)
     lines = [ln for ln in proc.stdout.splitlines() if ln.startswith("{")]
     if not lines:
         raise NativeUnavailable(f"amdgpu-topo-labeller produced no JSON (rc={proc.returncode}): {proc.stderr[-500:]}")
@@ -37,10 +44,11 @@ def amdsmi_topology(timeout: float = 60.0) -> Dict[str, Any]:
     return doc
 
 
-def amdsmi_labels(timeout: float = 60.0) -> Dict[str, str]:
+def amdsmi_labels(timeout: float = 60.0, source: str = "amdsmi", sysfs_root: str = "") -> Dict[str, str]:
     """``amdgpu-topo-labeller --labels``: the node labels computed natively."""
     exe = executable("amdgpu-topo-labeller")
-    proc = subprocess.run([exe, "--labels"], capture_output=True, text=True, timeout=timeout, check=False)
+    argv = [exe, "--labels", "--source", source] + (["--sysfs-root", sysfs_root] if sysfs_root else [])
+    proc = subprocess.run(argv, capture_output=True, text=True, timeout=timeout, check=False)
     if proc.returncode != 0:
         raise NativeUnavailable(f"amdgpu-topo-labeller --labels failed (rc={proc.returncode}): {proc.stderr[-500:]}")
     out: Dict[str, str] = {}
@@ -51,19 +59,39 @@ def amdsmi_labels(timeout: float = 60.0) -> Dict[str, str]:
     return out
 
 
-def amdsmi_topology_inprocess() -> Dict[str, Any]:
+def _native_call(fn_name: str, source: str, root: str) -> "tuple[int, str]":
     lib = load("libtk_topo.so")
-    lib.tkt_topology_json.argtypes = [ctypes.c_char_p, ctypes.c_size_t]
+    fn = getattr(lib, fn_name)
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    fn.restype = ctypes.c_int
     size = 1 << 16
     while True:
         buf = ctypes.create_string_buffer(size)
-        rc = lib.tkt_topology_json(buf, size)
+        rc = fn(source.encode(), root.encode(), buf, size)
         if rc < 0:
             size = -rc + 1
             continue
-        doc = json.loads(buf.value.decode())
-        doc["status"] = rc
-        return doc
+        return rc, buf.value.decode()
+
+
+def native_topology(source: str = "sysfs", sysfs_root: str = "") -> Dict[str, Any]:
+    """The labeller's JSON document, in-process.  Use ``source="sysfs"`` here:
+    amd_smi belongs in a child process (see :func:`amdsmi_topology`)."""
+    rc, text = _native_call("tkt_topology_json_src", source, sysfs_root)
+    doc = json.loads(text)
+    doc["status"] = rc
+    return doc
+
+
+def native_labels(source: str = "sysfs", sysfs_root: str = "") -> Dict[str, str]:
+    rc, text = _native_call("tkt_topology_labels_src", source, sysfs_root)
+    if rc != 0:
+        raise NativeUnavailable(f"native labeller ({source}) failed with status {rc}")
+    return dict(ln.split("=", 1) for ln in text.splitlines() if "=" in ln)
+
+
+def amdsmi_topology_inprocess() -> Dict[str, Any]:
+    return native_topology("amdsmi")
 
 
 def _read_props(path: str) -> Dict[str, int]:
@@ -131,15 +159,17 @@ def kfd_topology(root: str = KFD_TOPOLOGY) -> Dict[str, Any]:
     return {"source": "kfd", "gpus": gpus}
 
 
-def discover(kfd_root: Optional[str] = None, prefer_amdsmi: bool = True) -> Dict[str, Any]:
-    """Best-effort topology: amd_smi first, KFD sysfs second, empty last."""
-    if prefer_amdsmi and kfd_root is None:
-        try:
-            doc = amdsmi_topology()
-            if doc.get("status") == 0 and doc.get("gpus"):
-                return doc
-        except (NativeUnavailable, OSError, ValueError, subprocess.SubprocessError):
-            pass
+def discover(kfd_root: Optional[str] = None, prefer: str = "sysfs") -> Dict[str, Any]:
+    """Best-effort topology: native sysfs (or amd_smi), the other native source, Python KFD, empty."""
+    if kfd_root is None:
+        order = ["sysfs", "amdsmi"] if prefer == "sysfs" else ["amdsmi", "sysfs"]
+        for source in order:
+            try:
+                doc = native_topology("sysfs") if source == "sysfs" else amdsmi_topology()
+                if doc.get("status") == 0 and doc.get("gpus"):
+                    return doc
+            except (NativeUnavailable, OSError, ValueError, subprocess.SubprocessError):
+                continue
     root = kfd_root or KFD_TOPOLOGY
     if os.path.isdir(root):
         return kfd_topology(root)
