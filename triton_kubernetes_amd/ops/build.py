@@ -8,8 +8,8 @@ artifact                       source                                      toolc
 ``libtk_gpu_probe.so``         ``csrc/tk_gpu_probe.hip`` (HBM/MFMA/memtest)  hipcc
 ``libtk_rccl.so``              ``csrc/tk_rccl_probe.hip`` (N2, RCCL)          hipcc
 ``rccl-ready``                 same, ``-DTK_RCCL_MAIN``                     hipcc
-``libtk_topo.so``              ``csrc/tk_topo.cpp`` (N1, amd_smi)            g++
-``amdgpu-topo-labeller``       same, ``-DTK_TOPO_MAIN``                     g++
+``libtk_topo.so``              ``csrc/tk_topo.cpp`` (N1, sysfs collector)    g++
+``amdgpu-topo-labeller``       same + amd_smi, ``-DTK_TOPO_MAIN``           g++
 =============================  ==========================================  =========
 
 Usage: ``python -m triton_kubernetes_amd.ops.build [--force] [-j N]``.
@@ -76,11 +76,11 @@ def targets() -> List[Target]:
         Target("rccl-ready", [rccl],
                [hipcc, *HIP_FLAGS, "-DTK_RCCL_MAIN", rccl, "-o", out("rccl-ready"), f"-L{ROCM}/lib", "-lrccl",
                 *RPATH]),
+        # in-process library: sysfs collector only, no libamd_smi (see csrc/tk_topo.cpp)
         Target("libtk_topo.so", [topo],
-               ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", f"-I{ROCM}/include", topo, "-o",
-                out("libtk_topo.so"), f"-L{ROCM}/lib", "-lamd_smi", *RPATH]),
+               ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", topo, "-o", out("libtk_topo.so")]),
         Target("amdgpu-topo-labeller", [topo],
-               ["g++", "-O2", "-std=c++17", "-DTK_TOPO_MAIN", f"-I{ROCM}/include", topo, "-o",
+               ["g++", "-O2", "-std=c++17", "-DTK_TOPO_MAIN", "-DTK_TOPO_AMDSMI", f"-I{ROCM}/include", topo, "-o",
                 out("amdgpu-topo-labeller"), f"-L{ROCM}/lib", "-lamd_smi", *RPATH]),
     ]
 

@@ -12,11 +12,18 @@
 //           ms amdsmi_init costs, and safe inside a process that also runs HIP.
 // tests/test_gpu_probes.py checks on an MI355X that both give identical labels.
 //
-// Built twice from this file: libtk_topo.so (C ABI, loaded with ctypes) and the
-// stand-alone `amdgpu-topo-labeller` executable (-DTK_TOPO_MAIN) that the
-// bare-metal host bootstrap runs on nodes without Python tooling.
+// Built twice from this file:
+//   libtk_topo.so          C ABI for ctypes, sysfs collector only.  It is loaded
+//                          into processes that also run HIP and RCCL, so it
+//                          does not link libamd_smi at all (amd_smi's library
+//                          state next to librccl crashed dlopen on the box).
+//   amdgpu-topo-labeller   stand-alone executable (-DTK_TOPO_MAIN
+//                          -DTK_TOPO_AMDSMI): both collectors; the agent and
+//                          the bare-metal host bootstrap run it as a child.
 
+#ifdef TK_TOPO_AMDSMI
 #include <amd_smi/amdsmi.h>
+#endif
 #include <dirent.h>
 
 #include <algorithm>
@@ -91,6 +98,7 @@ std::string hex64(uint64_t v) {
 }
 
 // ---------------------------------------------------------------- amd_smi --
+#ifdef TK_TOPO_AMDSMI
 const char* link_name(amdsmi_link_type_t t) {
   switch (t) {
     case AMDSMI_LINK_TYPE_INTERNAL: return "INTERNAL";
@@ -204,6 +212,15 @@ Topology collect_amdsmi() {
   amdsmi_shut_down();
   return t;
 }
+#else
+Topology collect_amdsmi() {
+  Topology t;
+  t.source = "amd_smi";
+  t.status = 3;
+  t.error = "amd_smi collector not built into this library (run amdgpu-topo-labeller --source amdsmi)";
+  return t;
+}
+#endif
 
 // ------------------------------------------------------------------ sysfs --
 bool read_file(const std::string& path, std::string* out) {

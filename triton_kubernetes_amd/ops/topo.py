@@ -75,8 +75,8 @@ def _native_call(fn_name: str, source: str, root: str) -> "tuple[int, str]":
 
 
 def native_topology(source: str = "sysfs", sysfs_root: str = "") -> Dict[str, Any]:
-    """The labeller's JSON document, in-process.  Use ``source="sysfs"`` here:
-    amd_smi belongs in a child process (see :func:`amdsmi_topology`)."""
+    """The labeller's JSON document, in-process (sysfs collector; the library
+    is built without amd_smi, which runs in a child: :func:`amdsmi_topology`)."""
     rc, text = _native_call("tkt_topology_json_src", source, sysfs_root)
     doc = json.loads(text)
     doc["status"] = rc
@@ -88,10 +88,6 @@ def native_labels(source: str = "sysfs", sysfs_root: str = "") -> Dict[str, str]
     if rc != 0:
         raise NativeUnavailable(f"native labeller ({source}) failed with status {rc}")
     return dict(ln.split("=", 1) for ln in text.splitlines() if "=" in ln)
-
-
-def amdsmi_topology_inprocess() -> Dict[str, Any]:
-    return native_topology("amdsmi")
 
 
 def _read_props(path: str) -> Dict[str, int]:
