@@ -3,10 +3,12 @@
 import json
 import os
 import subprocess
+import sys
 
 import pytest
 
 pytestmark = pytest.mark.gpu
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 @pytest.fixture(scope="module")
@@ -113,3 +115,52 @@ def test_native_labels_match_python_spec():
     assert via_sysfs["amd.com/gpu.product-name"] == "MI355X"
     assert via_sysfs["amd.com/gpu.target"] == "gfx950"
     assert via_sysfs["amd.com/gpu.vram"] == "288G"
+
+
+def test_gate_comm_nonblocking_then_sweep():
+    from triton_kubernetes_amd.ops import rccl
+
+    g = rccl.GateComm(rccl.unique_id(), 1, 0, [0], blocking=False)
+    r = g.sweep([1 << 20, 16 << 20], iters=3, warmup=1)
+    print(json.dumps(r.phase_ms))
+    assert r.ok and r.phase_ms["init_total"] > 0 and len(r.busbw_gbps) == 2
+    g2 = rccl.GateComm(rccl.unique_id(), 1, 0, [0], blocking=False)
+    g2.abort()
+    assert rccl.pending_gates() == 0
+    rccl.drain()
+
+
+def test_gate_abort_mid_init_with_missing_peer():
+    """world=2 with only rank 0 present: init cannot finish; abort must return (own process, bounded)."""
+    code = ("import time; from triton_kubernetes_amd.ops import rccl; "
+            "g = rccl.GateComm(rccl.unique_id(), 2, 0, [0], blocking=False); time.sleep(0.3); "
+            "assert not g.ready(); g.abort(); assert rccl.pending_gates() == 0; rccl.drain(); print('aborted-ok')")
+    proc = subprocess.run(["timeout", "-k", "5", "90", sys.executable, "-c", code], capture_output=True, text=True,
+                          cwd=ROOT)
+    assert proc.returncode == 0 and "aborted-ok" in proc.stdout, proc.stdout[-2000:] + proc.stderr[-2000:]
+
+
+def test_agent_pipelined_gate_over_http():
+    import base64
+
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.parallel.transport import AgentTransport, HostRef
+
+    agent = NodeAgent("gate-test", "sim", devices=[0], token="t0k")
+    url = agent.serve()
+    try:
+        tr = AgentTransport(token="t0k")
+        host = HostRef("agent+" + url)
+        uid = tr.post(host, "/v1/rccl-uid", {})["uid"]
+        assert len(base64.b64decode(uid)) == 128
+        prep = tr.post(host, "/v1/rccl-prepare", {"uid": uid, "world": 1, "rank_base": 0, "ndev": 1})
+        assert prep["ok"] and prep["ranks"] == [0]
+        res = tr.post(host, "/v1/rccl-gate", {"uid": uid, "rank": 0, "world": 1, "ndev": 1, "sizes": [1 << 20],
+                                             "iters": 3})
+        assert res["ok"] and res["pipelined"] and res["ranks"] == [0]
+        # prepare then abort leaves nothing pending
+        uid2 = tr.post(host, "/v1/rccl-uid", {})["uid"]
+        tr.post(host, "/v1/rccl-prepare", {"uid": uid2, "world": 1, "rank_base": 0, "ndev": 1})
+        assert tr.post(host, "/v1/rccl-abort", {"uid": uid2})["aborted"] is True
+    finally:
+        agent.stop()

@@ -120,6 +120,13 @@ def test_mi355x_node_and_addons():
     assert n["gpu_count"] == "8" and n["gpu_burnin"] == "quick" and n["gpu_product"] == "MI355X"
     assert n["rccl_env"]["NCCL_SOCKET_IFNAME"] == "eth0" and n["rccl_env"]["HSA_FORCE_FINE_GRAIN_PCIE"] == "1"
     assert_blocks_match_modules(st)
+    baremetal.new_node(make_ctx(dict(NODE_BASE, node_count=1, ssh_user="u", bastion_host="", key_path="k",
+                                     gpu="mi355x", hosts=["c"], rccl_min_busbw="150")), "m", key, None, st)
+    assert st.module("node_baremetal_dev_dev-w-3")["rccl_min_busbw"] == "150"
+    assert_blocks_match_modules(st)
+    neg = make_ctx(dict(NODE_BASE, node_count=1, ssh_user="u", bastion_host="", key_path="k", gpu="mi355x",
+                        hosts=["d"], rccl_min_busbw="-1"))
+    assert _err(baremetal.new_node, neg, "m", key, None, st) == "rccl_min_busbw must be a non-negative number. Found '-1'."
     bad = make_ctx(dict(NODE_BASE, ssh_user="u", bastion_host="", key_path="k", gpu="h100", hosts=["a", "b"]))
     assert "Invalid gpu 'h100'" in _err(baremetal.new_node, bad, "m", key, None, st)
 

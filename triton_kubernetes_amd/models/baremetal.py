@@ -145,12 +145,21 @@ def _mi355x_fields(ctx: Context) -> Dict:
     overrides = s.get("rccl_env")
     if isinstance(overrides, dict):
         env.update({str(k): str(v) for k, v in overrides.items()})
-    return {
+    out = {
         "gpu_product": "MI355X",
         "gpu_count": str(int(count)),
         "gpu_burnin": burnin,
         "rccl_env": env,
     }
+    if s.is_set("rccl_min_busbw"):
+        busbw = s.get_string("rccl_min_busbw")
+        try:
+            if float(busbw) < 0:
+                raise ValueError
+        except ValueError as exc:
+            raise ConfigError(f"rccl_min_busbw must be a non-negative number. Found '{busbw}'.") from exc
+        out["rccl_min_busbw"] = busbw
+    return out
 
 
 def key_path_expanded(path: str) -> str:

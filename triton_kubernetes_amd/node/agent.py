@@ -24,8 +24,10 @@ In both modes the MI355X steps call the native probes directly on the agent's
 GPUs: topology labeller (N1), HBM/MFMA/memtest burn-in, RCCL env file and the
 node-level RCCL sweep (N2).
 
-HTTP API (JSON): ``GET /v1/info``, ``POST /v1/plan``, ``POST /v1/rccl-gate``
-(one rank of the cluster-wide RCCL gate), ``POST /v1/cleanup``.
+HTTP API (JSON): ``GET /v1/info``, ``POST /v1/plan``, ``POST /v1/rccl-uid``,
+``POST /v1/rccl-prepare`` (start this node's ranks of the cluster-wide RCCL
+communicator, non-blocking), ``POST /v1/rccl-gate`` (run them: verified
+all-reduce sweep), ``POST /v1/rccl-abort``, ``POST /v1/cleanup``.
 """
 
 import base64
@@ -96,6 +98,8 @@ class NodeAgent:
         if not self.token:
             self.token = secrets.token_urlsafe(24)
         self.lock = threading.Lock()
+        self._gate_mu = threading.Lock()
+        self._gates: Dict[bytes, Any] = {}
         self.last_labels: Dict[str, str] = {}
         self.history: List[Dict[str, Any]] = []
         self._server: Optional[http.server.ThreadingHTTPServer] = None
@@ -289,17 +293,68 @@ class NodeAgent:
                 "X-API-Tunnel-Params": tunnel_params(plan.hostname, roles, ctx["labels"], ctx["capacity"])}
         return http.request("POST", "/v3/connect/register", headers=hdrs, data=b"{}").json()
 
-    # --- RCCL gate (one rank) -----------------------------------------------------------------
-    def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10) -> Dict[str, Any]:
+    # --- RCCL gate (this node's ranks) ---------------------------------------------------------
+    # Gate communicators pending by uid: started by /v1/rccl-prepare, consumed by
+    # /v1/rccl-gate, released by /v1/rccl-abort, stop(), or expiry.
+    GATE_TTL_S = 900.0
+
+    def _gate_devices(self, ndev: int) -> List[int]:
+        devs = self.devices or [0]
+        if ndev < 1 or ndev > len(devs):
+            raise ValueError(f"gate wants {ndev} GPUs, agent has {len(devs)}")
+        return devs[:ndev]
+
+    def _expire_gates(self) -> None:
+        now = time.time()
+        with self._gate_mu:
+            stale = [k for k, (_, t) in self._gates.items() if now - t > self.GATE_TTL_S]
+            gates = [self._gates.pop(k)[0] for k in stale]
+        for g in gates:
+            g.abort()
+
+    def rccl_prepare(self, uid: bytes, world: int, rank_base: int, ndev: int = 1) -> Dict[str, Any]:
+        """Start this node's share of a cluster communicator (non-blocking init)."""
         from ..ops import rccl
 
-        dev = self.devices[0] if self.devices else 0
-        # the communicator teardown is not part of the readiness answer: it is
-        # joined in stop() (or by the next process-exit drain), not here
+        devs = self._gate_devices(ndev)
+        self._expire_gates()
         self._used_rccl = True
-        with span("node.rccl_gate", node=self.name, rank=rank, world=world):
-            res = rccl.sweep_rank(rank, world, uid, dev, sizes, iters=iters, warmup=2, async_teardown=True)
-        return res.to_json()
+        with span("node.rccl_prepare", node=self.name, rank_base=rank_base, world=world):
+            gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False)
+        with self._gate_mu:
+            old = self._gates.pop(uid, None)
+            self._gates[uid] = (gate, time.time())
+        if old is not None:
+            old[0].abort()
+        return {"ok": True, "ranks": list(range(rank_base, rank_base + len(devs))), "devices": devs}
+
+    def rccl_abort(self, uid: bytes) -> Dict[str, Any]:
+        with self._gate_mu:
+            entry = self._gates.pop(uid, None)
+        if entry is not None:
+            entry[0].abort()
+        return {"ok": True, "aborted": entry is not None}
+
+    def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10,
+                  ndev: int = 1) -> Dict[str, Any]:
+        """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
+        communicator from rccl_prepare when there is one, else a fresh init."""
+        from ..ops import rccl
+
+        with self._gate_mu:
+            entry = self._gates.pop(uid, None)
+        pipelined = entry is not None
+        self._used_rccl = True
+        with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=pipelined):
+            gate = entry[0] if entry is not None else \
+                rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
+            # the communicator teardown is not part of the readiness answer: it is
+            # joined in stop() (or by the next process-exit drain), not here
+            res = gate.sweep(sizes, iters=iters, warmup=2, async_teardown=True)
+        out = res.to_json()
+        out["pipelined"] = pipelined
+        out["ranks"] = list(range(rank, rank + len(gate.devices)))
+        return out
 
     # --- HTTP server ----------------------------------------------------------------------------
     def serve(self, host: str = "127.0.0.1", port: int = 0) -> str:
@@ -351,11 +406,18 @@ class NodeAgent:
                         from ..ops import rccl
 
                         return self._reply(200, {"uid": base64.b64encode(rccl.unique_id()).decode()})
+                    if path == "/v1/rccl-prepare":
+                        return self._reply(200, agent.rccl_prepare(base64.b64decode(body["uid"]),
+                                                                   int(body["world"]), int(body["rank_base"]),
+                                                                   int(body.get("ndev", 1))))
                     if path == "/v1/rccl-gate":
                         uid = base64.b64decode(body["uid"])
                         return self._reply(200, agent.rccl_gate(int(body["rank"]), int(body["world"]), uid,
                                                                 [int(s) for s in body.get("sizes", [1 << 20])],
-                                                                int(body.get("iters", 10))))
+                                                                int(body.get("iters", 10)),
+                                                                int(body.get("ndev", 1))))
+                    if path == "/v1/rccl-abort":
+                        return self._reply(200, agent.rccl_abort(base64.b64decode(body["uid"])))
                     if path == "/v1/cleanup":
                         agent.last_labels = {}
                         return self._reply(200, {"ok": True})
@@ -374,6 +436,11 @@ class NodeAgent:
             self._server.shutdown()
             self._server.server_close()
             self._server = None
+        with self._gate_mu:
+            pending = [g for g, _ in self._gates.values()]
+            self._gates.clear()
+        for g in pending:
+            g.abort()
         if getattr(self, "_used_rccl", False):
             from ..ops import rccl
 

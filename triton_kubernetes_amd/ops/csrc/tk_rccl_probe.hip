@@ -32,6 +32,7 @@
 #include <vector>
 
 static thread_local char g_err[512];
+static inline double ms_since(std::chrono::steady_clock::time_point t);
 static thread_local double g_last_init_ms = 0.0;
 extern "C" const char* tkr_last_error() { return g_err; }
 // Wall time of the calling thread's last communicator init (ms).
@@ -157,6 +158,14 @@ static void teardown(ncclComm_t comm, RankBufs b, int device) {
   auto work = [comm, b, device]() mutable {
     (void)hipSetDevice(device);
     free_bufs(b);
+    // finalize + wait also covers non-blocking communicators, whose finalize returns early
+    if (ncclCommFinalize(comm) == ncclInProgress) {
+      for (int i = 0; i < 1200000; ++i) {  // <= ~60 s
+        ncclResult_t st = ncclSuccess;
+        if (ncclCommGetAsyncError(comm, &st) != ncclSuccess || st != ncclInProgress) break;
+        std::this_thread::sleep_for(std::chrono::microseconds(50));
+      }
+    }
     ncclCommDestroy(comm);
   };
   if (g_async_teardown) {
@@ -189,56 +198,245 @@ static struct TeardownDrainer {
 static inline size_t elem_size(int dtype) { return dtype == 1 ? 2 : 4; }
 static inline ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclBfloat16 : ncclFloat32; }
 
-// Multi-process: one rank.  Results per size in out arrays (length nsizes):
-// time_us (mean per all-reduce), algbw GB/s, busbw GB/s, errors (mismatches).
+// ---------------------------------------------------------------------------------------------
+// Cluster gate communicators.  One process (a node agent) owns `ndev` local GPUs and joins the
+// cluster-wide communicator as ranks rank_base .. rank_base+ndev-1 (ncclCommInitRankConfig per
+// device inside one group).  With blocking=0 the init is RCCL's non-blocking mode: begin returns
+// at once and the bootstrap/topology/connection setup runs on RCCL's threads, so an agent can
+// start it when cluster membership is known and overlap it with the rest of the node bring-up;
+// the gate request later only waits for the remainder and runs the verified sweep.  A gate that
+// is never run (a node failed) is aborted with ncclCommAbort, which is legal mid-init.
+struct Gate {
+  std::vector<int> devices;
+  std::vector<ncclComm_t> comms;
+  int rank_base = 0, world = 0;
+  std::chrono::steady_clock::time_point t_begin;
+  double init_ms = -1.0;  // begin -> every comm ready
+};
+static std::mutex g_gate_mu;
+static std::vector<std::pair<int, Gate*>> g_gates;
+static int g_next_gate = 1;
+
+static Gate* take_gate(int h) {
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  for (size_t i = 0; i < g_gates.size(); ++i)
+    if (g_gates[i].first == h) {
+      Gate* g = g_gates[i].second;
+      g_gates.erase(g_gates.begin() + (long)i);
+      return g;
+    }
+  return nullptr;
+}
+
+static Gate* peek_gate(int h) {
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  for (auto& e : g_gates)
+    if (e.first == h) return e.second;
+  return nullptr;
+}
+
+// 0 when every communicator is ready, -2 on an RCCL error, -3 on timeout.
+static int wait_comms(const std::vector<ncclComm_t>& comms, double timeout_ms) {
+  const auto t0 = std::chrono::steady_clock::now();
+  for (;;) {
+    bool pending = false;
+    for (auto c : comms) {
+      ncclResult_t st = ncclSuccess;
+      ncclResult_t r = ncclCommGetAsyncError(c, &st);
+      if (r != ncclSuccess) st = r;
+      if (st == ncclInProgress) pending = true;
+      else if (st != ncclSuccess) {
+        snprintf(g_err, sizeof(g_err), "communicator error: %s", ncclGetErrorString(st));
+        return -2;
+      }
+    }
+    if (!pending) return 0;
+    if (ms_since(t0) > timeout_ms) {
+      snprintf(g_err, sizeof(g_err), "communicator not ready after %.0f ms", timeout_ms);
+      return -3;
+    }
+    std::this_thread::sleep_for(std::chrono::microseconds(50));
+  }
+}
+
+static int gate_ready(Gate* g, double timeout_ms) {
+  if (g->init_ms >= 0) return 0;
+  const int rc = wait_comms(g->comms, timeout_ms);
+  if (rc == 0) g->init_ms = ms_since(g->t_begin);
+  return rc;
+}
+
+// Returns a handle > 0, or < 0 on error (tkr_last_error()).
+extern "C" int tkr_gate_begin(const unsigned char* uid128, int world, int rank_base, int ndev, const int* devices,
+                              int blocking) {
+  if (ndev < 1 || world < ndev || rank_base < 0 || rank_base + ndev > world) {
+    snprintf(g_err, sizeof(g_err), "bad gate geometry: world=%d rank_base=%d ndev=%d", world, rank_base, ndev);
+    return -1;
+  }
+  ncclUniqueId id;
+  memcpy(id.internal, uid128, NCCL_UNIQUE_ID_BYTES);
+  Gate* g = new Gate();
+  g->devices.assign(devices, devices + ndev);
+  g->comms.assign(ndev, nullptr);
+  g->rank_base = rank_base;
+  g->world = world;
+  g->t_begin = std::chrono::steady_clock::now();
+  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+  cfg.blocking = blocking ? 1 : 0;
+  ncclResult_t r = ncclGroupStart();
+  for (int d = 0; d < ndev && (r == ncclSuccess || r == ncclInProgress); ++d) {
+    if (hipSetDevice(devices[d]) != hipSuccess) {
+      snprintf(g_err, sizeof(g_err), "hipSetDevice(%d) failed", devices[d]);
+      r = ncclInvalidArgument;
+      break;
+    }
+    r = ncclCommInitRankConfig(&g->comms[d], world, id, rank_base + d, &cfg);
+  }
+  ncclResult_t re = ncclGroupEnd();
+  if (r == ncclSuccess || r == ncclInProgress) r = re;
+  if (r != ncclSuccess && r != ncclInProgress) {
+    if (!g_err[0]) snprintf(g_err, sizeof(g_err), "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
+    for (auto c : g->comms)
+      if (c) ncclCommAbort(c);
+    delete g;
+    return -2;
+  }
+  if (blocking) g->init_ms = ms_since(g->t_begin);
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  const int h = g_next_gate++;
+  g_gates.emplace_back(h, g);
+  return h;
+}
+
+// 0 ready, 1 still initialising, < 0 error.
+extern "C" int tkr_gate_poll(int h) {
+  Gate* g = peek_gate(h);
+  if (!g) { snprintf(g_err, sizeof(g_err), "unknown gate %d", h); return -1; }
+  if (g->init_ms >= 0) return 0;
+  const int rc = wait_comms(g->comms, 0.0);
+  if (rc == 0) { g->init_ms = ms_since(g->t_begin); return 0; }
+  return rc == -3 ? 1 : rc;
+}
+
+extern "C" int tkr_gate_abort(int h) {
+  Gate* g = take_gate(h);
+  if (!g) return -1;
+  for (size_t d = 0; d < g->comms.size(); ++d) {
+    (void)hipSetDevice(g->devices[d]);
+    if (g->comms[d]) ncclCommAbort(g->comms[d]);
+  }
+  delete g;
+  return 0;
+}
+
+extern "C" int tkr_gate_pending() {
+  std::lock_guard<std::mutex> lk(g_gate_mu);
+  return (int)g_gates.size();
+}
+
+// Completes the handle's init (waiting at most timeout_ms), runs the verified all-reduce sweep
+// over its devices and tears the communicators down (async per tkr_set_async_teardown).  The
+// handle is consumed.  phase_ms[0..4]: init wait in this call, alloc, sweep, teardown, and the
+// total init time since begin.  Per-size outputs as for tkr_sweep_local (slowest device).
+extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters, int warmup, int dtype,
+                              double timeout_ms, double* time_us, double* algbw, double* busbw, double* errors,
+                              double* phase_ms) {
+  Gate* g = take_gate(h);
+  if (!g) { snprintf(g_err, sizeof(g_err), "unknown gate %d", h); return -1; }
+  const int ndev = (int)g->devices.size();
+  auto t_phase = std::chrono::steady_clock::now();
+  int rc = gate_ready(g, timeout_ms);
+  phase_ms[0] = ms_since(t_phase);
+  phase_ms[4] = g->init_ms;
+  if (rc) {
+    for (int d = 0; d < ndev; ++d) { (void)hipSetDevice(g->devices[d]); ncclCommAbort(g->comms[d]); }
+    delete g;
+    return rc;
+  }
+  size_t max_bytes = 0;
+  for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
+  std::vector<RankBufs> bufs(ndev);
+  t_phase = std::chrono::steady_clock::now();
+  for (int d = 0; d < ndev && rc == 0; ++d) {
+    if (hipSetDevice(g->devices[d]) != hipSuccess) { rc = -1; break; }
+    rc = alloc_bufs(bufs[d], max_bytes);
+  }
+  phase_ms[1] = ms_since(t_phase);
+  t_phase = std::chrono::steady_clock::now();
+  const float want = (float)g->world * (float)(g->world + 1) / 2.0f;
+  auto run = [&](size_t count, int n) -> int {
+    for (int it = 0; it < n; ++it) {
+      ncclResult_t r = ncclGroupStart();
+      for (int d = 0; d < ndev && r == ncclSuccess; ++d)
+        r = ncclAllReduce(bufs[d].send, bufs[d].recv, count, nccl_type(dtype), ncclSum, g->comms[d],
+                          bufs[d].stream);
+      ncclResult_t re = ncclGroupEnd();
+      if (r == ncclSuccess) r = re;
+      if (r == ncclInProgress) {
+        const int w = wait_comms(g->comms, timeout_ms);
+        if (w) return w;
+      } else if (r != ncclSuccess) {
+        snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", ncclGetErrorString(r));
+        return -2;
+      }
+    }
+    return 0;
+  };
+  for (int s = 0; rc == 0 && s < nsizes; ++s) {
+    const size_t count = sizes[s] / elem_size(dtype);
+    for (int d = 0; d < ndev && rc == 0; ++d) {
+      (void)hipSetDevice(g->devices[d]);
+      rc = fill(bufs[d], count, dtype, (float)(g->rank_base + d + 1));
+    }
+    if (rc || (rc = run(count, warmup)) != 0) break;
+    for (int d = 0; d < ndev; ++d) { (void)hipSetDevice(g->devices[d]); (void)hipEventRecord(bufs[d].t0, bufs[d].stream); }
+    if ((rc = run(count, iters)) != 0) break;
+    double worst = 0.0;
+    unsigned long long bad_total = 0;
+    for (int d = 0; d < ndev && rc == 0; ++d) {
+      (void)hipSetDevice(g->devices[d]);
+      (void)hipEventRecord(bufs[d].t1, bufs[d].stream);
+      rc = check(bufs[d], count, dtype, want);
+    }
+    for (int d = 0; d < ndev && rc == 0; ++d) {
+      (void)hipSetDevice(g->devices[d]);
+      if (hipStreamSynchronize(bufs[d].stream) != hipSuccess) { snprintf(g_err, sizeof(g_err), "stream sync failed"); rc = -1; break; }
+      float ms = 0.f;
+      (void)hipEventElapsedTime(&ms, bufs[d].t0, bufs[d].t1);
+      if (ms > worst) worst = ms;
+      unsigned long long bad = 0;
+      (void)hipMemcpy(&bad, bufs[d].bad, sizeof(bad), hipMemcpyDeviceToHost);
+      bad_total += bad;
+    }
+    if (rc) break;
+    const double t = worst * 1e-3 / (iters > 0 ? iters : 1);
+    time_us[s] = t * 1e6;
+    algbw[s] = (double)sizes[s] / t / 1e9;
+    busbw[s] = algbw[s] * (g->world > 1 ? 2.0 * (g->world - 1) / g->world : 1.0);
+    errors[s] = (double)bad_total;
+  }
+  phase_ms[2] = ms_since(t_phase);
+  t_phase = std::chrono::steady_clock::now();
+  for (int d = 0; d < ndev; ++d) teardown(g->comms[d], bufs[d], g->devices[d]);
+  phase_ms[3] = ms_since(t_phase);
+  delete g;
+  return rc;
+}
+
+// Multi-process: one rank on one device (blocking init + sweep + teardown).  Kept as the
+// single-call form of the gate; per-size outputs as above.
 extern "C" int tkr_sweep_rank(int rank, int world, const unsigned char* uid128, int device, const size_t* sizes,
                               int nsizes, int iters, int warmup, int dtype, double* time_us, double* algbw,
                               double* busbw, double* errors) {
-  HIPCHECK(hipSetDevice(device));
-  ncclUniqueId id;
-  memcpy(id.internal, uid128, NCCL_UNIQUE_ID_BYTES);
-  ncclComm_t comm;
-  const auto t_init = std::chrono::steady_clock::now();
-  NCCLCHECK(ncclCommInitRank(&comm, world, id, rank));
-  g_last_init_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_init).count();
-  size_t max_bytes = 0;
-  for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
-  RankBufs b;
-  auto t_phase = std::chrono::steady_clock::now();
-  int rc = alloc_bufs(b, max_bytes);
-  g_phase_ms[1] = ms_since(t_phase);
-  t_phase = std::chrono::steady_clock::now();
-  const float want = (float)world * (float)(world + 1) / 2.0f;
-  for (int s = 0; rc == 0 && s < nsizes; ++s) {
-    const size_t count = sizes[s] / elem_size(dtype);
-    if ((rc = fill(b, count, dtype, (float)(rank + 1))) != 0) break;
-    for (int w = 0; w < warmup; ++w) {
-      ncclResult_t r = ncclAllReduce(b.send, b.recv, count, nccl_type(dtype), ncclSum, comm, b.stream);
-      if (r != ncclSuccess) { snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", ncclGetErrorString(r)); rc = -2; }
-    }
-    if (rc) break;
-    (void)hipEventRecord(b.t0, b.stream);
-    for (int it = 0; it < iters; ++it) {
-      ncclResult_t r = ncclAllReduce(b.send, b.recv, count, nccl_type(dtype), ncclSum, comm, b.stream);
-      if (r != ncclSuccess) { snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", ncclGetErrorString(r)); rc = -2; break; }
-    }
-    if (rc) break;
-    (void)hipEventRecord(b.t1, b.stream);
-    if ((rc = check(b, count, dtype, want)) != 0) break;
-    if (hipStreamSynchronize(b.stream) != hipSuccess) { snprintf(g_err, sizeof(g_err), "stream sync failed"); rc = -1; break; }
-    float ms = 0.f;
-    (void)hipEventElapsedTime(&ms, b.t0, b.t1);
-    unsigned long long bad = 0;
-    (void)hipMemcpy(&bad, b.bad, sizeof(bad), hipMemcpyDeviceToHost);
-    const double t = (double)ms * 1e-3 / (iters > 0 ? iters : 1);
-    time_us[s] = t * 1e6;
-    algbw[s] = (double)sizes[s] / t / 1e9;
-    busbw[s] = algbw[s] * (world > 1 ? 2.0 * (world - 1) / world : 1.0);
-    errors[s] = (double)bad;
-  }
-  g_phase_ms[2] = ms_since(t_phase);
-  g_phase_ms[0] = g_last_init_ms;
-  teardown(comm, b, device);
+  const int h = tkr_gate_begin(uid128, world, rank, 1, &device, 1);
+  if (h < 0) return h;
+  double ph[5] = {0, 0, 0, 0, 0};
+  const int rc = tkr_gate_sweep(h, sizes, nsizes, iters, warmup, dtype, 600000.0, time_us, algbw, busbw, errors, ph);
+  g_last_init_ms = ph[4];
+  g_phase_ms[0] = ph[4];
+  g_phase_ms[1] = ph[1];
+  g_phase_ms[2] = ph[2];
+  g_phase_ms[3] = ph[3];
   return rc;
 }
 

@@ -35,6 +35,12 @@ def _lib():
                                    ctypes.c_int, dp, dp, dp, dp]
     lib.tkr_sweep_local.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
                                     ctypes.c_int, ctypes.c_int, dp, dp, dp, dp]
+    lib.tkr_gate_begin.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                   ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    lib.tkr_gate_poll.argtypes = [ctypes.c_int]
+    lib.tkr_gate_abort.argtypes = [ctypes.c_int]
+    lib.tkr_gate_sweep.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_int, ctypes.c_double, dp, dp, dp, dp, dp]
     global _ATEXIT
     if not _ATEXIT:
         atexit.register(lib.tkr_drain)  # join async teardowns before interpreter exit
@@ -106,6 +112,61 @@ def sweep_rank(rank: int, world: int, uid: bytes, device: int, sizes: Sequence[i
               for i, name in enumerate(("init", "alloc", "sweep", "teardown"))}
     return SweepResult(world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
                        float(lib.tkr_last_init_ms()), phases)
+
+
+class GateComm:
+    """This process's ranks ``rank_base .. rank_base+len(devices)-1`` of a cluster-wide
+    communicator (``tkr_gate_*``).  ``blocking=False`` starts RCCL's non-blocking
+    init and returns at once, so the init overlaps whatever the caller does next;
+    :meth:`sweep` waits for the rest, runs the verified all-reduce sweep and
+    consumes the handle.  :meth:`abort` releases a gate that will never run."""
+
+    def __init__(self, uid: bytes, world: int, rank_base: int, devices: Sequence[int], blocking: bool = False):
+        self.world, self.rank_base, self.devices = world, rank_base, list(devices)
+        devs = (ctypes.c_int * len(self.devices))(*self.devices)
+        h = _lib().tkr_gate_begin(uid, world, rank_base, len(self.devices), devs, 1 if blocking else 0)
+        if h < 0:
+            raise RCCLError(f"ranks {rank_base}+{len(self.devices)}/{world}: {_lib().tkr_last_error().decode()}")
+        self.handle = h
+
+    def ready(self) -> bool:
+        rc = _lib().tkr_gate_poll(self.handle)
+        if rc < 0:
+            raise RCCLError(_lib().tkr_last_error().decode())
+        return rc == 0
+
+    def sweep(self, sizes: Sequence[int], iters: int = 10, warmup: int = 3, dtype: str = "f32",
+              timeout_s: float = 600.0, async_teardown: bool = True) -> SweepResult:
+        if self.handle is None:
+            raise RCCLError("gate already consumed")
+        n = len(sizes)
+        sz = (ctypes.c_size_t * n)(*sizes)
+        t, alg, bus, err = _arrays(n)
+        ph = (ctypes.c_double * 5)()
+        lib = _lib()
+        lib.tkr_set_async_teardown(1 if async_teardown else 0)
+        try:
+            rc = lib.tkr_gate_sweep(self.handle, sz, n, iters, warmup, 1 if dtype == "bf16" else 0,
+                                    timeout_s * 1e3, t, alg, bus, err, ph)
+        finally:
+            lib.tkr_set_async_teardown(0)
+            self.handle = None
+        if rc != 0:
+            raise RCCLError(f"ranks {self.rank_base}+{len(self.devices)}/{self.world}: "
+                            f"{lib.tkr_last_error().decode()}")
+        phases = {"init_wait": round(ph[0], 3), "alloc": round(ph[1], 3), "sweep": round(ph[2], 3),
+                  "teardown": round(ph[3], 3), "init_total": round(ph[4], 3)}
+        return SweepResult(self.world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
+                           float(ph[4]), phases)
+
+    def abort(self) -> None:
+        if self.handle is not None:
+            _lib().tkr_gate_abort(self.handle)
+            self.handle = None
+
+
+def pending_gates() -> int:
+    return int(_lib().tkr_gate_pending())
 
 
 def set_async_teardown(on: bool) -> None:

@@ -1,0 +1,157 @@
+"""Cluster-wide RCCL gate: one communicator across every GPU of the cluster's MI355X workers.
+
+Each node agent owns its node's GPUs and joins as ranks ``rank_base .. rank_base+ndev-1``
+(``ops/rccl.py:GateComm``).  The gate has two halves:
+
+* :meth:`ClusterGate.prepare_async`: fetch a ``ncclUniqueId`` from the rank-0 agent and
+  ask every agent to *start* its communicator init (RCCL non-blocking mode).  This needs
+  only the cluster membership, which is known as soon as the node modules are in the
+  document, so ``create cluster`` starts it together with the apply.  Communicator
+  bring-up then overlaps node bootstrap instead of following it.
+* :meth:`ClusterGate.run`: after the readiness waiter has seen the cluster active, all
+  nodes Ready and ``amd.com/gpu`` allocatable, every agent finishes its init if needed,
+  runs the verified all-reduce sweep and tears the communicator down.
+
+If preparation failed, ``run`` falls back to a fresh uid and a plain (non-pipelined)
+gate.  :meth:`ClusterGate.abort` releases prepared communicators when the gate will not
+run, for example when a node failed and the apply raised.
+"""
+
+import concurrent.futures as cf
+import threading
+from dataclasses import dataclass
+from typing import Any, Dict, List, Optional, Sequence
+
+from ..parallel.transport import HostRef
+from ..utils.trace import span
+
+
+@dataclass
+class GateMember:
+    url: str  # agent base URL (without the "agent+" scheme prefix)
+    rank_base: int
+    ndev: int
+
+    @property
+    def host(self) -> HostRef:
+        return HostRef("agent+" + self.url)
+
+
+def members_from(urls: Sequence[str], ndevs: Optional[Sequence[int]] = None) -> List[GateMember]:
+    out: List[GateMember] = []
+    base = 0
+    for i, u in enumerate(urls):
+        n = int(ndevs[i]) if ndevs else 1
+        out.append(GateMember(u[len("agent+"):] if u.startswith("agent+") else u, base, n))
+        base += n
+    return out
+
+
+class ClusterGate:
+    def __init__(self, transport: Any, members: List[GateMember], sizes: Sequence[int], iters: int = 5):
+        if not members:
+            raise ValueError("a cluster gate needs at least one member")
+        self.transport = transport
+        self.members = members
+        self.world = sum(m.ndev for m in members)
+        self.sizes = list(sizes)
+        self.iters = iters
+        self.uid: Optional[str] = None
+        self.prepared = False
+        self.prepare_error: Optional[str] = None
+        self.done = False
+        self._thread: Optional[threading.Thread] = None
+        self._mu = threading.Lock()
+
+    # --- construction from the state document ---------------------------------------------------------
+    @classmethod
+    def from_state(cls, state, cluster_key: str, transport: Any, sizes: Sequence[int],
+                   iters: int = 5) -> Optional["ClusterGate"]:
+        """Gate over the cluster's MI355X host modules; None unless every one is an agent host."""
+        from ..terraform.catalog import module_from_source
+
+        urls: List[str] = []
+        ndevs: List[int] = []
+        for host in sorted(state.nodes(cluster_key)):
+            cfg = state.module(state.nodes(cluster_key)[host]) or {}
+            info = module_from_source(str(cfg.get("source", "")))
+            if info is None or not info.mi355x:
+                continue
+            addr = str(cfg.get("host", ""))
+            if not addr.startswith("agent+"):
+                return None  # SSH-managed GPU node: no agent to hold a communicator
+            urls.append(addr)
+            ndevs.append(int(cfg.get("gpu_count", 8) or 8))
+        if not urls:
+            return None
+        return cls(transport, members_from(urls, ndevs), sizes, iters)
+
+    # --- pipelined init ---------------------------------------------------------------------------------
+    def _post_all(self, path: str, body_for) -> List[Dict[str, Any]]:
+        def one(m: GateMember) -> Dict[str, Any]:
+            return self.transport.post(m.host, path, body_for(m))
+
+        if len(self.members) == 1:
+            return [one(self.members[0])]
+        with cf.ThreadPoolExecutor(max_workers=len(self.members)) as pool:
+            return list(pool.map(one, self.members))
+
+    def _prepare(self) -> None:
+        try:
+            with span("gate.prepare", world=self.world):
+                uid = self.transport.post(self.members[0].host, "/v1/rccl-uid", {})["uid"]
+                self._post_all("/v1/rccl-prepare", lambda m: {"uid": uid, "world": self.world,
+                                                               "rank_base": m.rank_base, "ndev": m.ndev})
+            with self._mu:
+                self.uid, self.prepared = uid, True
+        except Exception as exc:  # noqa: BLE001 - run() falls back to an unprepared gate
+            with self._mu:
+                self.prepare_error = f"{type(exc).__name__}: {exc}"
+                if "uid" in locals():
+                    self.uid = uid  # some agents may hold a pending init under it: abort() releases them
+
+    def prepare_async(self) -> "ClusterGate":
+        self._thread = threading.Thread(target=self._prepare, name="tk-gate-prepare", daemon=True)
+        self._thread.start()
+        return self
+
+    def _join(self) -> None:
+        if self._thread is not None:
+            self._thread.join()
+            self._thread = None
+
+    # --- the gate ---------------------------------------------------------------------------------------
+    def run(self) -> Dict[str, Any]:
+        self._join()
+        pipelined = self.prepared
+        if not pipelined:
+            if self.uid is not None:
+                self.abort()
+            self.uid = self.transport.post(self.members[0].host, "/v1/rccl-uid", {})["uid"]
+        uid = self.uid
+        results = self._post_all("/v1/rccl-gate", lambda m: {
+            "uid": uid, "rank": m.rank_base, "world": self.world, "ndev": m.ndev,
+            "sizes": self.sizes, "iters": self.iters})
+        self.done = True
+        ok = all(r.get("ok") for r in results)
+        busbw = [max(r.get("busbw_gbps") or [0.0]) for r in results]
+        return {"ok": ok, "world": self.world, "nodes": len(self.members), "pipelined": pipelined,
+                "prepare_error": self.prepare_error,
+                "min_peak_busbw_gbps": min(busbw) if busbw else 0.0, "ranks": results}
+
+    def abort(self) -> None:
+        """Release pending communicators on every agent (no-op once the gate ran)."""
+        self._join()
+        if self.done or self.uid is None:
+            return
+        uid = self.uid
+        for m in self.members:
+            try:
+                self.transport.post(m.host, "/v1/rccl-abort", {"uid": uid})
+            except Exception:  # noqa: BLE001 - best effort; agents also expire stale gates
+                pass
+        self.prepared = False
+        self.uid = None
+
+
+__all__ = ["ClusterGate", "GateMember", "members_from"]

@@ -8,14 +8,14 @@ Phases, each time-stamped (the BASELINE.json metric is ``ready - start``):
                         condition ``Ready=True`` (read through Rancher's k8s proxy);
 3. ``gpus_allocatable`` every MI355X node advertises ``amd.com/gpu`` equal to its
                         expected count (device plugin up);
-4. ``rccl_gate``        optional: one RCCL all-reduce sweep across all GPU nodes
-                        (N2), run by the node agents as one communicator.
+4. ``rccl_gate``        optional: one RCCL all-reduce sweep across every GPU of
+                        the GPU nodes (N2), run by the node agents as one
+                        communicator (``gate.py``; its init may already have been
+                        started, pipelined with the node bootstrap).
 
 Polling is adaptive (20 ms doubling to 1 s), not the reference's fixed 5 s.
 """
 
-import base64
-import concurrent.futures as cf
 import json
 import time
 from dataclasses import asdict, dataclass, field
@@ -34,6 +34,7 @@ class ReadinessSpec:
     timeout: float = 3600.0
     rccl_gate: bool = False
     rccl_hosts: List[str] = field(default_factory=list)  # agent URLs of GPU nodes, rank order
+    rccl_ndev: List[int] = field(default_factory=list)  # GPUs per rccl_hosts entry (default 1 each)
     rccl_sizes: List[int] = field(default_factory=lambda: [1 << 20, 64 << 20])
     rccl_iters: int = 5
 
@@ -64,7 +65,7 @@ def _node_ready(item: Dict[str, Any]) -> bool:
 
 
 def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float] = None,
-               agent_transport: Any = None) -> ReadinessReport:
+               agent_transport: Any = None, gate: Any = None) -> ReadinessReport:
     rep = ReadinessReport(start=start if start is not None else time.time())
     deadline = rep.start + spec.timeout
 
@@ -107,31 +108,25 @@ def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float
                            "allocatable": (it.get("status") or {}).get("allocatable", {})}
 
     if spec.rccl_gate and spec.rccl_hosts:
-        with span("ready.rccl_gate", world=len(spec.rccl_hosts)):
-            rep.rccl = rccl_gate(agent_transport, spec.rccl_hosts, spec.rccl_sizes, spec.rccl_iters)
+        if gate is None:
+            from .gate import ClusterGate, members_from
+
+            gate = ClusterGate(agent_transport, members_from(spec.rccl_hosts, spec.rccl_ndev or None),
+                               spec.rccl_sizes, spec.rccl_iters)
+        with span("ready.rccl_gate", world=gate.world, nodes=len(gate.members)):
+            rep.rccl = gate.run()
         if not rep.rccl.get("ok"):
             raise TKError(f"RCCL readiness gate failed: {rep.rccl}")
         rep.phases["rccl_gate"] = time.time()
     return rep
 
 
-def rccl_gate(transport: Any, agent_urls: List[str], sizes: List[int], iters: int = 5) -> Dict[str, Any]:
-    """One RCCL communicator across the GPU node agents (rank i = agent_urls[i])."""
-    from ..parallel.transport import HostRef
+def rccl_gate(transport: Any, agent_urls: List[str], sizes: List[int], iters: int = 5,
+              ndevs: Optional[List[int]] = None) -> Dict[str, Any]:
+    """One RCCL communicator across the GPU node agents (not pipelined; see gate.py)."""
+    from .gate import ClusterGate, members_from
 
-    hosts = [HostRef("agent+" + u if not u.startswith("agent+") else u) for u in agent_urls]
-    uid = transport.post(hosts[0], "/v1/rccl-uid", {})["uid"]
-    world = len(hosts)
-
-    def one(i: int) -> Dict[str, Any]:
-        return transport.post(hosts[i], "/v1/rccl-gate",
-                              {"uid": uid, "rank": i, "world": world, "sizes": sizes, "iters": iters})
-
-    with cf.ThreadPoolExecutor(max_workers=world) as pool:
-        results = list(pool.map(one, range(world)))
-    ok = all(r.get("ok") for r in results)
-    busbw = [max(r.get("busbw_gbps") or [0.0]) for r in results]
-    return {"ok": ok, "world": world, "min_peak_busbw_gbps": min(busbw) if busbw else 0.0, "ranks": results}
+    return ClusterGate(transport, members_from(agent_urls, ndevs), sizes, iters).run()
 
 
 def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, rccl_gate: bool = False):
@@ -154,6 +149,7 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
     has_plugin = state.module(addons_key(cluster_key_parts(cluster_key)[1])) is not None
     gpu_nodes: Dict[str, int] = {}
     rccl_hosts: List[str] = []
+    rccl_ndev: List[int] = []
     for host in sorted(nodes):
         cfg = state.module(nodes[host]) or {}
         info = module_from_source(str(cfg.get("source", "")))
@@ -163,25 +159,50 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
             addr = str(cfg.get("host", ""))
             if addr.startswith("agent+"):
                 rccl_hosts.append(addr[len("agent+"):])
+                rccl_ndev.append(int(cfg.get("gpu_count", 8) or 8))
     spec = ReadinessSpec(cl["rancher_cluster_id"], sorted(nodes), gpu_nodes, timeout,
-                         rccl_gate and bool(rccl_hosts), rccl_hosts)
+                         rccl_gate and bool(rccl_hosts), rccl_hosts, rccl_ndev)
     return client, spec
 
 
-def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[float] = None) -> ReadinessReport:
+def agent_transport_for(ctx) -> Any:
+    transport = ctx.extras.get("agent_transport")
+    if transport is None:
+        from ..parallel.transport import AgentTransport
+
+        transport = AgentTransport(token=ctx.settings.get_string("agent_token"))
+    return transport
+
+
+def early_gate(ctx, state, cluster_key: str) -> Any:
+    """Start the cluster RCCL gate's communicator init now (``wait`` + ``rccl_gate`` with
+    agent-managed GPU nodes; ``rccl_pipeline: false`` disables).  Returns the gate or None."""
+    s = ctx.settings
+    if not (s.get_bool("wait") and s.get_bool("rccl_gate")):
+        return None
+    if s.is_set("rccl_pipeline") and not s.get_bool("rccl_pipeline"):
+        return None
+    from .gate import ClusterGate
+
+    spec_sizes = ReadinessSpec("", []).rccl_sizes
+    gate = ClusterGate.from_state(state, cluster_key, agent_transport_for(ctx), spec_sizes)
+    return gate.prepare_async() if gate is not None else None
+
+
+def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[float] = None,
+                      gate: Any = None) -> ReadinessReport:
     s = ctx.settings
     timeout = float(s.get_string("wait_timeout") or 3600)
     client, spec = spec_from_state(state, backend, cluster_key, timeout, s.get_bool("rccl_gate"))
-    transport = ctx.extras.get("agent_transport")
-    if transport is None and spec.rccl_gate:
-        from ..parallel.transport import AgentTransport
-
-        transport = AgentTransport(token=s.get_string("agent_token"))
-    rep = wait_ready(client, spec, start=start, agent_transport=transport)
+    transport = agent_transport_for(ctx) if spec.rccl_gate else None
+    if gate is not None and (not spec.rccl_gate or gate.world != sum(spec.rccl_ndev or [1] * len(spec.rccl_hosts))):
+        gate.abort()  # membership changed since it was prepared
+        gate = None
+    rep = wait_ready(client, spec, start=start, agent_transport=transport, gate=gate)
     ctx.echo(f"cluster ready in {rep.ready_seconds:.2f}s: " +
              json.dumps(rep.to_json()["phase_seconds"], sort_keys=True))
     return rep
 
 
 __all__ = ["ReadinessSpec", "ReadinessReport", "wait_ready", "rccl_gate", "spec_from_state", "wait_after_create",
-           "base64"]
+           "early_gate", "agent_transport_for"]

@@ -67,6 +67,27 @@ def apply_and_persist(ctx: Context, backend: Backend, state: State, new_modules:
         _write_status(backend, state.name, {"phase": "applied", "modules": new_modules, "time": time.time()})
 
 
+def _apply_then_wait(ctx: Context, backend: Backend, state: State, cluster_key: str,
+                     new_modules: List[str]) -> None:
+    """Apply + persist, then (``wait``) the readiness waiter.  With ``rccl_gate`` on
+    agent-managed GPU nodes the gate's communicator init is started before the
+    apply, so it overlaps node bootstrap (readiness/gate.py)."""
+    gate = None
+    if ctx.settings.get_bool("wait"):
+        from ..readiness.waiter import early_gate
+
+        gate = early_gate(ctx, state, cluster_key)
+    try:
+        apply_and_persist(ctx, backend, state, new_modules)
+        if ctx.settings.get_bool("wait"):
+            from ..readiness.waiter import wait_after_create
+
+            wait_after_create(ctx, backend, state, cluster_key, gate=gate)
+    finally:
+        if gate is not None:
+            gate.abort()  # no-op once the gate ran
+
+
 # --- manager ---------------------------------------------------------------------------
 def new_manager(ctx: Context, backend: Backend) -> None:
     provider = ctx.resolve_choice("manager_cloud_provider", "Create Manager in which Cloud Provider",
@@ -143,11 +164,7 @@ def new_cluster(ctx: Context, backend: Backend) -> Optional[str]:
             return None
 
     new_modules = sorted(set(state.modules()) - before)
-    apply_and_persist(ctx, backend, state, new_modules)
-    if ctx.settings.get_bool("wait"):
-        from ..readiness.waiter import wait_after_create
-
-        wait_after_create(ctx, backend, state, key)
+    _apply_then_wait(ctx, backend, state, key, new_modules)
     return name
 
 
@@ -170,11 +187,7 @@ def new_node(ctx: Context, backend: Backend) -> Optional[List[str]]:
     if not ctx.confirm("Proceed with the node creation", "Proceed"):
         ctx.echo("Node creation canceled")
         return None
-    apply_and_persist(ctx, backend, state, sorted(set(state.modules()) - before))
-    if ctx.settings.get_bool("wait"):
-        from ..readiness.waiter import wait_after_create
-
-        wait_after_create(ctx, backend, state, key)
+    _apply_then_wait(ctx, backend, state, key, sorted(set(state.modules()) - before))
     return hostnames
 
 
