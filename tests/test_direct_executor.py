@@ -166,3 +166,46 @@ def test_unsupported_module_and_parallel_fanout(env):
     assert len(rec.plans) == 40
     assert time.time() - t0 < 2.5, "node bootstrap must fan out concurrently"
     assert client.ping()
+
+
+def test_pipelined_rccl_gate_through_agents(env):
+    """wait + rccl_gate: the gate's communicators are prepared with the apply and run after readiness."""
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    cp = agent("cp")
+    workers = [agent(f"w{i}", gpus=8) for i in range(3)]
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="gate",
+                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
+                        rccl_gate=True, nodes=_nodes(cp, workers)))
+    from triton_kubernetes_amd.utils.trace import TRACER
+
+    TRACER.reset()
+    new_cluster(ctx, backend)
+    spans = TRACER.report()["spans"]
+    gates = [s for s in spans if s["name"] == "node.rccl_gate"]
+    assert len(gates) == 3 and all(s["attrs"]["pipelined"] for s in gates)
+    assert sorted(s["attrs"]["rank"] for s in gates) == [0, 8, 16]
+    assert {s["attrs"]["world"] for s in gates} == {24}
+    prep = [s for s in spans if s["name"] == "gate.prepare"]
+    assert len(prep) == 1
+    assert "rccl_gate" in output(ctx)
+
+
+def test_gate_released_when_apply_fails(env):
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    cp = agent("cp")
+    good = agent("good", gpus=8)
+    bad = agent("bad", gpus=8, fail_burnin=True)
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="fail",
+                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
+                        rccl_gate=True, nodes=_nodes(cp, [good, bad])))
+    with pytest.raises(TKError):
+        new_cluster(ctx, backend)
+    # the prepared communicators were released on every agent
+    from triton_kubernetes_amd.cloud.http import HTTPClient
+
+    for h in (good, bad):
+        info = HTTPClient(base_url=h[len("agent+"):]).request("GET", "/v1/info",
+                                                             headers={"X-TK-Agent-Token": TOKEN}).json()
+        assert info["pending_gates"] == 0

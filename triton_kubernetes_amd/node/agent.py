@@ -82,6 +82,23 @@ def _check(pattern: re.Pattern, value: str, what: str) -> str:
     return value
 
 
+class _SimGate:
+    """Stand-in for ops.rccl.GateComm on agents with synthetic GPUs (no RCCL)."""
+
+    def __init__(self, devices: List[int]):
+        self.devices = list(devices)
+
+    def sweep(self, sizes, iters=10, warmup=3, dtype="f32", timeout_s=600.0, async_teardown=True):
+        from ..ops.rccl import SweepResult
+
+        n = len(sizes)
+        return SweepResult(len(self.devices), dtype, list(sizes), [0.0] * n, [0.0] * n, [0.0] * n, [0] * n, 0.0,
+                           {"simulated": 1.0})
+
+    def abort(self) -> None:
+        pass
+
+
 @dataclass
 class NodeAgent:
     name: str = "node"
@@ -314,13 +331,16 @@ class NodeAgent:
 
     def rccl_prepare(self, uid: bytes, world: int, rank_base: int, ndev: int = 1) -> Dict[str, Any]:
         """Start this node's share of a cluster communicator (non-blocking init)."""
-        from ..ops import rccl
-
         devs = self._gate_devices(ndev)
         self._expire_gates()
-        self._used_rccl = True
         with span("node.rccl_prepare", node=self.name, rank_base=rank_base, world=world):
-            gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False)
+            if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
+                gate: Any = _SimGate(devs)
+            else:
+                from ..ops import rccl
+
+                self._used_rccl = True
+                gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False)
         with self._gate_mu:
             old = self._gates.pop(uid, None)
             self._gates[uid] = (gate, time.time())
@@ -339,15 +359,19 @@ class NodeAgent:
                   ndev: int = 1) -> Dict[str, Any]:
         """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
         communicator from rccl_prepare when there is one, else a fresh init."""
-        from ..ops import rccl
-
         with self._gate_mu:
             entry = self._gates.pop(uid, None)
         pipelined = entry is not None
-        self._used_rccl = True
         with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=pipelined):
-            gate = entry[0] if entry is not None else \
-                rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
+            if entry is not None:
+                gate = entry[0]
+            elif self.topology_override is not None:
+                gate = _SimGate(self._gate_devices(ndev))
+            else:
+                from ..ops import rccl
+
+                self._used_rccl = True
+                gate = rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
             # the communicator teardown is not part of the readiness answer: it is
             # joined in stop() (or by the next process-exit drain), not here
             res = gate.sweep(sizes, iters=iters, warmup=2, async_teardown=True)
@@ -390,8 +414,10 @@ class NodeAgent:
                 if not self._auth():
                     return self._reply(401, {"error": "unauthorized"})
                 if urllib.parse.urlsplit(self.path).path == "/v1/info":
+                    with agent._gate_mu:
+                        pending = len(agent._gates)
                     return self._reply(200, {"name": agent.name, "mode": agent.mode, "devices": agent.devices,
-                                             "labels": agent.last_labels})
+                                             "labels": agent.last_labels, "pending_gates": pending})
                 return self._reply(404, {"error": "not found"})
 
             def do_POST(self):
@@ -403,9 +429,13 @@ class NodeAgent:
                     if path == "/v1/plan":
                         return self._reply(200, agent.run_plan(BootstrapPlan.from_json(body["plan"])))
                     if path == "/v1/rccl-uid":
-                        from ..ops import rccl
+                        if agent.topology_override is not None:
+                            raw = secrets.token_bytes(128)
+                        else:
+                            from ..ops import rccl
 
-                        return self._reply(200, {"uid": base64.b64encode(rccl.unique_id()).decode()})
+                            raw = rccl.unique_id()
+                        return self._reply(200, {"uid": base64.b64encode(raw).decode()})
                     if path == "/v1/rccl-prepare":
                         return self._reply(200, agent.rccl_prepare(base64.b64decode(body["uid"]),
                                                                    int(body["world"]), int(body["rank_base"]),
