@@ -1,0 +1,148 @@
+"""Rancher v3 client (S3/S4 semantics) against the fake server; k8s add-on manifests; waiter timeouts."""
+
+import base64
+import hashlib
+import json
+import time
+
+import pytest
+
+from triton_kubernetes_amd.errors import TKError
+from triton_kubernetes_amd.k8s.manifests import addon_manifests, apply_manifests, gpu_job_manifest
+from triton_kubernetes_amd.rancher.client import RancherClient, ca_checksum, wait_until
+from triton_kubernetes_amd.rancher.fake import FAKE_CACERTS, FakeRancher, tunnel_params
+from triton_kubernetes_amd.readiness.waiter import ReadinessSpec, wait_ready
+
+
+@pytest.fixture
+def rancher():
+    fake = FakeRancher().start()
+    client = RancherClient(fake.url)
+    outs = client.bootstrap("n3w-pass", fake.url, timeout=10)
+    yield fake, RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"]), outs
+    fake.stop()
+
+
+def test_ca_checksum_matches_reference_shasum():
+    # rancher_cluster.sh: echo "$cacerts" | shasum -a 256  -> trailing newline included
+    assert ca_checksum("abc") == hashlib.sha256(b"abc\n").hexdigest()
+
+
+def test_bootstrap_s3(rancher):
+    fake, client, outs = rancher
+    assert fake.state.admin_password == "n3w-pass"
+    assert fake.state.settings["server-url"] == fake.url
+    assert outs["rancher_url"] == fake.url and outs["rancher_access_key"] and outs["rancher_secret_key"]
+    assert client.ping()
+    # the initial admin/admin login no longer works
+    with pytest.raises(TKError):
+        RancherClient(fake.url).login("admin", "admin")
+
+
+def test_ensure_cluster_is_idempotent_s4(rancher):
+    fake, client, _ = rancher
+    a = client.ensure_cluster("dev", "v1.9.5-rancher1-1", "calico")
+    b = client.ensure_cluster("dev")
+    assert a.cluster_id == b.cluster_id and not a.existed and b.existed
+    assert a.registration_token == b.registration_token  # reused, not re-created
+    assert a.ca_checksum == ca_checksum(FAKE_CACERTS)
+    rke = fake.state.clusters[a.cluster_id]["rancherKubernetesEngineConfig"]
+    assert rke["kubernetesVersion"] == "v1.9.5-rancher1-1" and rke["network"]["plugin"] == "calico"
+    assert client.ensure_cluster("other").cluster_id != a.cluster_id
+
+
+def test_registry_passed_to_rke(rancher):
+    fake, client, _ = rancher
+    info = client.ensure_cluster("reg", k8s_registry="r.example", k8s_registry_username="u",
+                                 k8s_registry_password="p")
+    rke = fake.state.clusters[info.cluster_id]["rancherKubernetesEngineConfig"]
+    assert rke["privateRegistries"] == [{"url": "r.example", "user": "u", "password": "p"}]
+
+
+def _register(fake, token, host, roles, labels=None, capacity=None):
+    from triton_kubernetes_amd.cloud.http import HTTPClient
+
+    hdrs = {"X-API-Tunnel-Token": token,
+            "X-API-Tunnel-Params": tunnel_params(host, roles, labels or {}, capacity or {})}
+    return HTTPClient(base_url=fake.url).request("POST", "/v3/connect/register", headers=hdrs, data=b"{}").json()
+
+
+def test_cluster_lifecycle_and_gpu_allocatable(rancher):
+    fake, client, _ = rancher
+    info = client.ensure_cluster("gpu")
+    assert client.cluster_state(info.cluster_id) != "active"
+    _register(fake, info.registration_token, "cp", {"etcd": True, "controlplane": True, "worker": False})
+    _register(fake, info.registration_token, "g1", {"etcd": False, "controlplane": False, "worker": True},
+              {"amd.com/gpu.present": "true"}, {"amd.com/gpu": 8})
+    wait_until(lambda: client.cluster_state(info.cluster_id) == "active", 5, "active")
+    nodes = {n["metadata"]["name"]: n for n in client.k8s_nodes(info.cluster_id)}
+    assert nodes["g1"]["metadata"]["labels"]["amd.com/gpu.present"] == "true"
+    assert "amd.com/gpu" not in nodes["g1"]["status"].get("allocatable", {})  # no device plugin yet
+    applied = apply_manifests(client, info.cluster_id, addon_manifests({}))
+    assert applied == ["DaemonSet/amdgpu-device-plugin", "ConfigMap/rccl-env"]
+    nodes = {n["metadata"]["name"]: n for n in client.k8s_nodes(info.cluster_id)}
+    assert str(nodes["g1"]["status"]["allocatable"]["amd.com/gpu"]) == "8"
+    # re-apply: 409 -> PUT
+    assert apply_manifests(client, info.cluster_id, addon_manifests({})) == applied
+    client.delete_cluster(info.cluster_id)
+    client.delete_cluster(info.cluster_id)  # 404 tolerated
+    assert client.find_cluster("gpu") is None
+
+
+def test_bad_registration_token_rejected(rancher):
+    fake, _, _ = rancher
+    with pytest.raises(TKError):
+        _register(fake, "nope", "x", {"worker": True})
+
+
+def test_wait_until_adaptive_and_timeout():
+    calls = []
+
+    def fn():
+        calls.append(time.monotonic())
+        return "done" if len(calls) >= 4 else None
+
+    assert wait_until(fn, 5, "x", first=0.005) == "done"
+    gaps = [b - a for a, b in zip(calls, calls[1:])]
+    assert gaps[-1] > gaps[0]  # doubling
+    with pytest.raises(TKError, match="timed out after 0s waiting for never"):
+        wait_until(lambda: None, 0.05, "never", first=0.01)
+
+
+def test_waiter_times_out_on_missing_node(rancher):
+    fake, client, _ = rancher
+    info = client.ensure_cluster("partial")
+    for h, roles in (("a", {"etcd": True}), ("b", {"controlplane": True}), ("c", {"worker": True})):
+        _register(fake, info.registration_token, h, roles)
+    spec = ReadinessSpec(info.cluster_id, ["a", "b", "c", "d"], timeout=0.3)
+    with pytest.raises(TKError, match="4 nodes Ready"):
+        wait_ready(client, spec)
+    rep = wait_ready(client, ReadinessSpec(info.cluster_id, ["a", "b", "c"], timeout=5))
+    assert set(rep.phases) == {"cluster_active", "nodes_ready"} and rep.ready_seconds >= 0
+
+
+def test_gpu_job_manifest_affinity():
+    job = gpu_job_manifest("train", "img", ["run"], gpus_per_pod=8, pods=4)
+    pod = job["spec"]["template"]["spec"]
+    exprs = pod["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][
+        "nodeSelectorTerms"][0]["matchExpressions"]
+    keys = {e["key"]: e["values"] for e in exprs}
+    assert keys == {"amd.com/gpu.present": ["true"], "amd.com/gpu.count": ["8"],
+                    "amd.com/xgmi.fully-connected": ["true"]}
+    term = pod["affinity"]["podAffinity"]["preferredDuringSchedulingIgnoredDuringExecution"][0]["podAffinityTerm"]
+    assert term["topologyKey"] == "amd.com/xgmi.hive-id"
+    assert pod["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "8"
+    assert pod["containers"][0]["envFrom"] == [{"configMapRef": {"name": "rccl-env"}}]
+    single = gpu_job_manifest("one", "img", ["x"], gpus_per_pod=1)["spec"]["template"]["spec"]["affinity"]
+    assert "podAffinity" not in single
+    assert len(single["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"]["nodeSelectorTerms"][0][
+        "matchExpressions"]) == 2
+
+
+def test_addon_manifest_options():
+    names = [o["metadata"]["name"] for _, o in addon_manifests(
+        {"node_labeller_image": "rocm/k8s-device-plugin:labeller", "rccl_gate": "true",
+         "rccl_probe_image": "tk/rccl:1"})]
+    assert names == ["amdgpu-device-plugin", "rccl-env", "amdgpu-node-labeller", "rccl-ready"]
+    cm = addon_manifests({})[1][1]
+    assert cm["data"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
