@@ -6,6 +6,8 @@
     triton-kubernetes version
 
 Additions: ``wait cluster`` (the readiness waiter on an existing cluster),
+``backup cluster`` / ``restore cluster`` (namespace backup to the state backend
+or S3 — advertised by the reference README, never implemented there),
 ``gpu …`` (the native MI355X probes), ``agent`` (the node agent) and
 ``image`` (machine-image templates -> Packer JSON, the reference's
 ``packer/packer-config``).
@@ -37,9 +39,12 @@ VALID = {
     "destroy": ["manager", "cluster", "node"],
     "get": ["manager", "cluster"],
     "wait": ["cluster"],
+    "backup": ["cluster"],
+    "restore": ["cluster"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
-_ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait"}
+_ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
+             "restore": "restore"}
 
 
 class ArgError(Exception):
@@ -78,7 +83,9 @@ def build_parser() -> argparse.ArgumentParser:
                        ("destroy", "Destroy cluster managers, kubernetes clusters or individual kubernetes "
                                    "cluster nodes."),
                        ("get", "Display resource information"),
-                       ("wait", "Wait until a cluster is kubectl-ready (and GPU-ready) and report timings")):
+                       ("wait", "Wait until a cluster is kubectl-ready (and GPU-ready) and report timings"),
+                       ("backup", "Back up a cluster's namespaces to the state backend (local/manta) or S3"),
+                       ("restore", "Restore a cluster's namespaces from a backup")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
@@ -159,6 +166,14 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         {"manager": wf.delete_manager, "cluster": wf.delete_cluster, "node": wf.delete_node}[what](ctx, backend)
     elif command == "get":
         {"manager": wf.get_manager, "cluster": wf.get_cluster}[what](ctx, backend)
+    elif command == "backup":
+        from ..workflows.backup import backup_cluster
+
+        backup_cluster(ctx, backend)
+    elif command == "restore":
+        from ..workflows.backup import restore_cluster
+
+        restore_cluster(ctx, backend)
     elif command == "wait":
         from ..readiness.waiter import wait_after_create
         from ..workflows.select import select_cluster, select_manager

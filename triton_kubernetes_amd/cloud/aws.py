@@ -26,7 +26,7 @@ def _sign(key: bytes, msg: str) -> bytes:
 
 def sigv4_headers(method: str, url: str, body: bytes, access_key: str, secret_key: str, region: str,
                   service: str, now: Optional[datetime.datetime] = None,
-                  session_token: Optional[str] = None) -> Dict[str, str]:
+                  session_token: Optional[str] = None, content_sha256: bool = False) -> Dict[str, str]:
     """Signature Version 4 headers for one request (AWS general reference algorithm)."""
     now = now or datetime.datetime.utcnow()
     amz_date = now.strftime("%Y%m%dT%H%M%SZ")
@@ -39,6 +39,8 @@ def sigv4_headers(method: str, url: str, body: bytes, access_key: str, secret_ke
         f"{urllib.parse.quote(k, safe='-_.~')}={urllib.parse.quote(v, safe='-_.~')}" for k, v in sorted(query))
     payload_hash = hashlib.sha256(body).hexdigest()
     headers = {"host": host, "x-amz-date": amz_date}
+    if content_sha256:  # required by S3
+        headers["x-amz-content-sha256"] = payload_hash
     if session_token:
         headers["x-amz-security-token"] = session_token
     signed_headers = ";".join(sorted(headers))
@@ -60,6 +62,8 @@ def sigv4_headers(method: str, url: str, body: bytes, access_key: str, secret_ke
     }
     if session_token:
         out["X-Amz-Security-Token"] = session_token
+    if content_sha256:
+        out["X-Amz-Content-Sha256"] = payload_hash
     return out
 
 
@@ -109,3 +113,42 @@ class EC2Client:
 
     def for_region(self, region: str) -> "EC2Client":
         return EC2Client(self.access_key, self.secret_key, region, http=self.http)
+
+
+class S3Client:
+    """Minimal S3 object client (path-style URLs, SigV4): put / get / list — used for cluster backups."""
+
+    def __init__(self, access_key: str, secret_key: str, region: str = "us-east-1",
+                 endpoint: Optional[str] = None, http: Optional[HTTPClient] = None):
+        self.access_key, self.secret_key, self.region = access_key, secret_key, region
+        self.endpoint = (endpoint or f"https://s3.{region}.amazonaws.com").rstrip("/")
+        self.http = http or HTTPClient()
+
+    def _url(self, bucket: str, key: str = "", query: str = "") -> str:
+        path = f"/{bucket}" + (f"/{urllib.parse.quote(key, safe='/-_.~')}" if key else "")
+        return self.endpoint + path + (f"?{query}" if query else "")
+
+    def _req(self, method: str, url: str, body: bytes = b"", ok=(200,)):
+        hdrs = sigv4_headers(method, url, body, self.access_key, self.secret_key, self.region, "s3",
+                             content_sha256=True)
+        return self.http.request(method, url, headers=hdrs, data=body if body else None, ok=ok)
+
+    def put_object(self, bucket: str, key: str, data: bytes) -> None:
+        self._req("PUT", self._url(bucket, key), data, ok=(200, 201, 204))
+
+    def get_object(self, bucket: str, key: str) -> bytes:
+        return self._req("GET", self._url(bucket, key)).body
+
+    def list_keys(self, bucket: str, prefix: str = "") -> List[str]:
+        keys: List[str] = []
+        token = ""
+        while True:
+            q = {"list-type": "2", "prefix": prefix}
+            if token:
+                q["continuation-token"] = token
+            root = _strip_ns(ET.fromstring(self._req("GET", self._url(bucket, query=urllib.parse.urlencode(
+                sorted(q.items())))).body))
+            keys += [el.findtext("Key", "") for el in root.iter("Contents")]
+            token = root.findtext("NextContinuationToken", "") or ""
+            if root.findtext("IsTruncated", "false") != "true" or not token:
+                return keys

@@ -23,6 +23,7 @@
 #include <rccl/rccl.h>
 
 #include <atomic>
+#include <condition_variable>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -158,14 +159,6 @@ static void teardown(ncclComm_t comm, RankBufs b, int device) {
   auto work = [comm, b, device]() mutable {
     (void)hipSetDevice(device);
     free_bufs(b);
-    // finalize + wait also covers non-blocking communicators, whose finalize returns early
-    if (ncclCommFinalize(comm) == ncclInProgress) {
-      for (int i = 0; i < 1200000; ++i) {  // <= ~60 s
-        ncclResult_t st = ncclSuccess;
-        if (ncclCommGetAsyncError(comm, &st) != ncclSuccess || st != ncclInProgress) break;
-        std::this_thread::sleep_for(std::chrono::microseconds(50));
-      }
-    }
     ncclCommDestroy(comm);
   };
   if (g_async_teardown) {
@@ -200,18 +193,32 @@ static inline ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclBflo
 
 // ---------------------------------------------------------------------------------------------
 // Cluster gate communicators.  One process (a node agent) owns `ndev` local GPUs and joins the
-// cluster-wide communicator as ranks rank_base .. rank_base+ndev-1 (ncclCommInitRankConfig per
-// device inside one group).  With blocking=0 the init is RCCL's non-blocking mode: begin returns
-// at once and the bootstrap/topology/connection setup runs on RCCL's threads, so an agent can
-// start it when cluster membership is known and overlap it with the rest of the node bring-up;
-// the gate request later only waits for the remainder and runs the verified sweep.  A gate that
-// is never run (a node failed) is aborted with ncclCommAbort, which is legal mid-init.
+// cluster-wide communicator as ranks rank_base .. rank_base+ndev-1 (one ncclCommInitRank per
+// device inside one group).  With blocking=0 the init runs on a thread of its own: begin
+// returns at once, so an agent can start it as soon as cluster membership is known and overlap
+// the bootstrap / topology / connection setup with the rest of the node bring-up; the gate
+// request later only waits for the remainder and runs the verified sweep.
+//
+// Only the long-stable RCCL API is used (ncclCommInitRank, groups, ncclAllReduce,
+// ncclCommDestroy/Abort): inside a PyTorch process this library binds to the RCCL that torch
+// already loaded (same SONAME), which can be older than the headers it was compiled with, so
+// the versioned ncclConfig_t of ncclCommInitRankConfig is avoided.
+//
+// A gate that will never run (a node failed) is released with tkr_gate_abort.  If its init is
+// still waiting for peers that will not come, RCCL cannot be interrupted there; the init
+// thread is detached and cleans up after itself should the init ever complete.
 struct Gate {
   std::vector<int> devices;
   std::vector<ncclComm_t> comms;
   int rank_base = 0, world = 0;
   std::chrono::steady_clock::time_point t_begin;
   double init_ms = -1.0;  // begin -> every comm ready
+  std::mutex mu;
+  std::condition_variable cv;
+  int init_state = 0;  // 0 running, 1 ready, -2 failed
+  bool abandoned = false;
+  char err[512] = {0};
+  std::thread init_thread;
 };
 static std::mutex g_gate_mu;
 static std::vector<std::pair<int, Gate*>> g_gates;
@@ -235,35 +242,73 @@ static Gate* peek_gate(int h) {
   return nullptr;
 }
 
-// 0 when every communicator is ready, -2 on an RCCL error, -3 on timeout.
-static int wait_comms(const std::vector<ncclComm_t>& comms, double timeout_ms) {
-  const auto t0 = std::chrono::steady_clock::now();
-  for (;;) {
-    bool pending = false;
-    for (auto c : comms) {
-      ncclResult_t st = ncclSuccess;
-      ncclResult_t r = ncclCommGetAsyncError(c, &st);
-      if (r != ncclSuccess) st = r;
-      if (st == ncclInProgress) pending = true;
-      else if (st != ncclSuccess) {
-        snprintf(g_err, sizeof(g_err), "communicator error: %s", ncclGetErrorString(st));
-        return -2;
-      }
-    }
-    if (!pending) return 0;
-    if (ms_since(t0) > timeout_ms) {
-      snprintf(g_err, sizeof(g_err), "communicator not ready after %.0f ms", timeout_ms);
-      return -3;
-    }
-    std::this_thread::sleep_for(std::chrono::microseconds(50));
+static void destroy_comms(Gate* g, bool abort) {
+  for (size_t d = 0; d < g->comms.size(); ++d) {
+    if (!g->comms[d]) continue;
+    (void)hipSetDevice(g->devices[d]);
+    if (abort) ncclCommAbort(g->comms[d]);
+    else ncclCommDestroy(g->comms[d]);
+    g->comms[d] = nullptr;
   }
 }
 
-static int gate_ready(Gate* g, double timeout_ms) {
-  if (g->init_ms >= 0) return 0;
-  const int rc = wait_comms(g->comms, timeout_ms);
-  if (rc == 0) g->init_ms = ms_since(g->t_begin);
-  return rc;
+static void init_body(Gate* g, ncclUniqueId id) {
+  ncclResult_t r = ncclGroupStart();
+  for (size_t d = 0; d < g->devices.size() && r == ncclSuccess; ++d) {
+    if (hipSetDevice(g->devices[d]) != hipSuccess) {
+      snprintf(g->err, sizeof(g->err), "hipSetDevice(%d) failed", g->devices[d]);
+      r = ncclInvalidArgument;
+      break;
+    }
+    r = ncclCommInitRank(&g->comms[d], g->world, id, g->rank_base + (int)d);
+  }
+  ncclResult_t re = ncclGroupEnd();
+  if (r == ncclSuccess) r = re;
+  if (r != ncclSuccess && !g->err[0]) snprintf(g->err, sizeof(g->err), "ncclCommInitRank: %s", ncclGetErrorString(r));
+  bool orphan;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    g->init_ms = ms_since(g->t_begin);
+    g->init_state = r == ncclSuccess ? 1 : -2;
+    orphan = g->abandoned;
+  }
+  g->cv.notify_all();
+  if (orphan) {  // released while initialising: nobody else will touch it
+    destroy_comms(g, /*abort=*/true);
+    delete g;
+  }
+}
+
+// 0 ready, -2 init failed, -3 timeout.
+static int gate_wait(Gate* g, double timeout_ms) {
+  std::unique_lock<std::mutex> lk(g->mu);
+  const bool done = g->cv.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms),
+                                   [g] { return g->init_state != 0; });
+  if (!done) {
+    snprintf(g_err, sizeof(g_err), "communicator not ready after %.0f ms", timeout_ms);
+    return -3;
+  }
+  if (g->init_state < 0) {
+    snprintf(g_err, sizeof(g_err), "%s", g->err);
+    return -2;
+  }
+  return 0;
+}
+
+// Frees a gate taken out of the table: joins and destroys when its init is over, otherwise
+// hands it to the (detached) init thread.
+static void release_gate(Gate* g, bool abort) {
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    if (g->init_state == 0) {
+      g->abandoned = true;
+      g->init_thread.detach();
+      return;
+    }
+  }
+  if (g->init_thread.joinable()) g->init_thread.join();
+  destroy_comms(g, abort);
+  delete g;
 }
 
 // Returns a handle > 0, or < 0 on error (tkr_last_error()).
@@ -281,27 +326,17 @@ extern "C" int tkr_gate_begin(const unsigned char* uid128, int world, int rank_b
   g->rank_base = rank_base;
   g->world = world;
   g->t_begin = std::chrono::steady_clock::now();
-  ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-  cfg.blocking = blocking ? 1 : 0;
-  ncclResult_t r = ncclGroupStart();
-  for (int d = 0; d < ndev && (r == ncclSuccess || r == ncclInProgress); ++d) {
-    if (hipSetDevice(devices[d]) != hipSuccess) {
-      snprintf(g_err, sizeof(g_err), "hipSetDevice(%d) failed", devices[d]);
-      r = ncclInvalidArgument;
-      break;
+  if (blocking) {
+    init_body(g, id);
+    if (g->init_state < 0) {
+      snprintf(g_err, sizeof(g_err), "%s", g->err);
+      destroy_comms(g, true);
+      delete g;
+      return -2;
     }
-    r = ncclCommInitRankConfig(&g->comms[d], world, id, rank_base + d, &cfg);
+  } else {
+    g->init_thread = std::thread(init_body, g, id);
   }
-  ncclResult_t re = ncclGroupEnd();
-  if (r == ncclSuccess || r == ncclInProgress) r = re;
-  if (r != ncclSuccess && r != ncclInProgress) {
-    if (!g_err[0]) snprintf(g_err, sizeof(g_err), "ncclCommInitRankConfig: %s", ncclGetErrorString(r));
-    for (auto c : g->comms)
-      if (c) ncclCommAbort(c);
-    delete g;
-    return -2;
-  }
-  if (blocking) g->init_ms = ms_since(g->t_begin);
   std::lock_guard<std::mutex> lk(g_gate_mu);
   const int h = g_next_gate++;
   g_gates.emplace_back(h, g);
@@ -312,21 +347,22 @@ extern "C" int tkr_gate_begin(const unsigned char* uid128, int world, int rank_b
 extern "C" int tkr_gate_poll(int h) {
   Gate* g = peek_gate(h);
   if (!g) { snprintf(g_err, sizeof(g_err), "unknown gate %d", h); return -1; }
-  if (g->init_ms >= 0) return 0;
-  const int rc = wait_comms(g->comms, 0.0);
-  if (rc == 0) { g->init_ms = ms_since(g->t_begin); return 0; }
-  return rc == -3 ? 1 : rc;
+  std::lock_guard<std::mutex> lk(g->mu);
+  if (g->init_state < 0) { snprintf(g_err, sizeof(g_err), "%s", g->err); return -2; }
+  return g->init_state == 1 ? 0 : 1;
 }
 
+// 0 released, 1 released while still initialising (init thread detached), -1 unknown handle.
 extern "C" int tkr_gate_abort(int h) {
   Gate* g = take_gate(h);
   if (!g) return -1;
-  for (size_t d = 0; d < g->comms.size(); ++d) {
-    (void)hipSetDevice(g->devices[d]);
-    if (g->comms[d]) ncclCommAbort(g->comms[d]);
+  int pending;
+  {
+    std::lock_guard<std::mutex> lk(g->mu);
+    pending = g->init_state == 0;
   }
-  delete g;
-  return 0;
+  release_gate(g, /*abort=*/true);
+  return pending;
 }
 
 extern "C" int tkr_gate_pending() {
@@ -345,14 +381,14 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
   if (!g) { snprintf(g_err, sizeof(g_err), "unknown gate %d", h); return -1; }
   const int ndev = (int)g->devices.size();
   auto t_phase = std::chrono::steady_clock::now();
-  int rc = gate_ready(g, timeout_ms);
+  int rc = gate_wait(g, timeout_ms);
   phase_ms[0] = ms_since(t_phase);
   phase_ms[4] = g->init_ms;
   if (rc) {
-    for (int d = 0; d < ndev; ++d) { (void)hipSetDevice(g->devices[d]); ncclCommAbort(g->comms[d]); }
-    delete g;
+    release_gate(g, /*abort=*/true);
     return rc;
   }
+  if (g->init_thread.joinable()) g->init_thread.join();
   size_t max_bytes = 0;
   for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
   std::vector<RankBufs> bufs(ndev);
@@ -372,10 +408,7 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
                           bufs[d].stream);
       ncclResult_t re = ncclGroupEnd();
       if (r == ncclSuccess) r = re;
-      if (r == ncclInProgress) {
-        const int w = wait_comms(g->comms, timeout_ms);
-        if (w) return w;
-      } else if (r != ncclSuccess) {
+      if (r != ncclSuccess) {
         snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", ncclGetErrorString(r));
         return -2;
       }
@@ -417,7 +450,10 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
   }
   phase_ms[2] = ms_since(t_phase);
   t_phase = std::chrono::steady_clock::now();
-  for (int d = 0; d < ndev; ++d) teardown(g->comms[d], bufs[d], g->devices[d]);
+  for (int d = 0; d < ndev; ++d) {
+    teardown(g->comms[d], bufs[d], g->devices[d]);
+    g->comms[d] = nullptr;
+  }
   phase_ms[3] = ms_since(t_phase);
   delete g;
   return rc;

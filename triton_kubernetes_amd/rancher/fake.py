@@ -341,8 +341,14 @@ class FakeRancher:
             with st.mu:
                 if key in st.objects:
                     return 409, {"kind": "Status", "reason": "AlreadyExists", "code": 409}
-                st.objects[key] = body
-            return 201, body
+                # server-populated fields, as a real API server adds them
+                obj = json.loads(json.dumps(body))
+                meta = obj.setdefault("metadata", {})
+                meta.update({"uid": str(uuid.uuid4()), "resourceVersion": str(len(st.objects) + 1),
+                             "creationTimestamp": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())})
+                obj.setdefault("status", {})
+                st.objects[key] = obj
+            return 201, obj
         if method in ("PUT", "GET", "DELETE"):
             base, _, name = kpath.rpartition("/")
             key = f"{cid}|{base}|{name}"
