@@ -1225,9 +1225,16 @@ def write_all(root: str = MODULES_DIR) -> List[str]:
     if os.path.isdir(root):
         shutil.rmtree(root)
     for mod in modules():
+        copies = {f"files/{name}": src for name, src in mod.copies.items()}
         for rel, content in rendered_files(mod).items():
             path = os.path.join(root, mod.name, rel)
             os.makedirs(os.path.dirname(path), exist_ok=True)
+            if rel in copies:
+                # shipped sources stay single-copy: a relative symlink into the package
+                # (git keeps it; module sources fetched from git resolve it)
+                os.symlink(os.path.relpath(copies[rel], os.path.dirname(path)), path)
+                written.append(path)
+                continue
             with open(path, "w", encoding="utf-8") as fh:
                 fh.write(content)
             if path.endswith(".sh"):
