@@ -52,12 +52,19 @@ def parse_args():
     ap.add_argument("--rccl-mib", type=int, default=64, help="largest RCCL gate message (MiB)")
     ap.add_argument("--sim-gpu", action="store_true",
                     help="CPU dry run: synthetic topology, no burn-in kernels, no RCCL (never a valid measurement)")
+    ap.add_argument("--no-gate-pipeline", action="store_true",
+                    help="start the RCCL gate's communicator init after readiness instead of with the apply")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
     return ap.parse_args()
 
 
 def main() -> int:
     args = parse_args()
+    watchdog = float(os.environ.get("TK_BENCH_WATCHDOG", "0") or 0)
+    if watchdog > 0:  # debugging aid: dump every thread's Python stack periodically
+        import faulthandler
+
+        faulthandler.dump_traceback_later(watchdog, repeat=True, file=sys.stderr)
     import torch
     import torch.distributed as dist
 
@@ -118,7 +125,7 @@ def main() -> int:
         name = f"bench-{i}"
         cfg = dict(ctx_base, cluster_cloud_provider="baremetal", name=name, k8s_version="v1.9.5-rancher1-1",
                    k8s_network_provider="flannel", gpu_addons=True, wait=True,
-                   rccl_gate=not args.no_rccl_gate, wait_timeout=600,
+                   rccl_gate=not args.no_rccl_gate, rccl_pipeline=not args.no_gate_pipeline, wait_timeout=600,
                    nodes=[
                        {"rancher_host_label": "control", "node_count": 1, "hostname": f"{name}-cp",
                         "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": ["agent+" + cp_url]},
@@ -195,6 +202,7 @@ def main() -> int:
                 "workers": world, "gpus_per_worker": 1, "control_plane_nodes": 2,
                 "global_batch": world, "seq_len": 0, "parallelism": f"{world} workers (1 GPU each)",
                 "executor": "direct", "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate,
+                "rccl_gate_pipelined": not (args.no_rccl_gate or args.no_gate_pipeline),
             },
             "phase_ms_per_step": phase_ms,
         }

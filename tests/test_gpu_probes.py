@@ -131,11 +131,13 @@ def test_gate_comm_nonblocking_then_sweep():
 
 
 def test_gate_abort_mid_init_with_missing_peer():
-    """world=2 with only rank 0 present: init cannot finish; abort must return (own process, bounded)."""
+    """world=2 with only rank 0 present: init cannot finish; abort must return at once (own process, bounded)."""
     code = ("import time; from triton_kubernetes_amd.ops import rccl; "
             "g = rccl.GateComm(rccl.unique_id(), 2, 0, [0], blocking=False); time.sleep(0.3); "
-            "assert not g.ready(); g.abort(); assert rccl.pending_gates() == 0; rccl.drain(); print('aborted-ok')")
-    proc = subprocess.run(["timeout", "-k", "5", "90", sys.executable, "-c", code], capture_output=True, text=True,
+            "assert not g.ready(); t = time.time(); g.abort(); dt = time.time() - t; "
+            "assert dt < 1.0, dt; assert rccl.pending_gates() == 0 and rccl.abandoned_inits() == 1; "
+            "print('aborted-ok', round(dt * 1e3, 3)); rccl.exit_now(0)")
+    proc = subprocess.run(["timeout", "-k", "5", "60", sys.executable, "-c", code], capture_output=True, text=True,
                           cwd=ROOT)
     assert proc.returncode == 0 and "aborted-ok" in proc.stdout, proc.stdout[-2000:] + proc.stderr[-2000:]
 

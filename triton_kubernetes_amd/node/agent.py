@@ -502,4 +502,15 @@ def main(argv: Optional[List[str]] = None) -> int:
             time.sleep(3600)
     except KeyboardInterrupt:
         agent.stop()
+    if getattr(agent, "_used_rccl", False):
+        from ..ops import rccl
+
+        if rccl.abandoned_inits():
+            rccl.exit_now(0)  # an init blocked on absent peers would hang the normal exit
     return 0
+
+
+if __name__ == "__main__":
+    import sys
+
+    sys.exit(main())

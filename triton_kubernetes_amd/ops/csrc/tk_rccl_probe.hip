@@ -205,8 +205,10 @@ static inline ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclBflo
 // the versioned ncclConfig_t of ncclCommInitRankConfig is avoided.
 //
 // A gate that will never run (a node failed) is released with tkr_gate_abort.  If its init is
-// still waiting for peers that will not come, RCCL cannot be interrupted there; the init
-// thread is detached and cleans up after itself should the init ever complete.
+// still waiting for peers that will not come, RCCL cannot be interrupted there (there is no
+// bootstrap timeout); the init thread is detached and cleans up after itself should the init
+// ever complete.  tkr_gate_abandoned() counts such threads: a process holding one cannot run
+// the HIP/RCCL exit teardown safely and should leave with _exit (ops/rccl.py:exit_now).
 struct Gate {
   std::vector<int> devices;
   std::vector<ncclComm_t> comms;
@@ -223,6 +225,9 @@ struct Gate {
 static std::mutex g_gate_mu;
 static std::vector<std::pair<int, Gate*>> g_gates;
 static int g_next_gate = 1;
+// inits released while still waiting for peers (their threads are detached)
+static std::atomic<int> g_abandoned{0};
+extern "C" int tkr_gate_abandoned() { return g_abandoned.load(); }
 
 static Gate* take_gate(int h) {
   std::lock_guard<std::mutex> lk(g_gate_mu);
@@ -276,6 +281,7 @@ static void init_body(Gate* g, ncclUniqueId id) {
   if (orphan) {  // released while initialising: nobody else will touch it
     destroy_comms(g, /*abort=*/true);
     delete g;
+    g_abandoned.fetch_sub(1);
   }
 }
 
@@ -303,6 +309,7 @@ static void release_gate(Gate* g, bool abort) {
     if (g->init_state == 0) {
       g->abandoned = true;
       g->init_thread.detach();
+      g_abandoned.fetch_add(1);
       return;
     }
   }

@@ -169,6 +169,22 @@ def pending_gates() -> int:
     return int(_lib().tkr_gate_pending())
 
 
+def abandoned_inits() -> int:
+    """Gate inits released while still waiting for absent peers (detached threads)."""
+    return int(_lib().tkr_gate_abandoned())
+
+
+def exit_now(code: int = 0) -> None:
+    """Leave the process without the HIP/RCCL exit teardown, which cannot complete while an
+    abandoned init thread is blocked in RCCL's bootstrap.  Flushes stdio first."""
+    import os
+    import sys
+
+    sys.stdout.flush()
+    sys.stderr.flush()
+    os._exit(code)
+
+
 def set_async_teardown(on: bool) -> None:
     """Run communicator teardown off the caller's critical path (see ``teardown`` in the HIP source)."""
     _lib().tkr_set_async_teardown(1 if on else 0)
