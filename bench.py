@@ -120,6 +120,12 @@ def main() -> int:
         wf.new_manager(Context(settings=Settings(mgr, env={}), out=open(os.devnull, "w")), backend)
 
     sizes = [1 << 20, args.rccl_mib << 20]
+    # long-lived startup objects (torch, the package, servers) leave the GC's working set,
+    # so a full collection during a step does not walk them (a ~100 ms stall was measured)
+    import gc
+
+    gc.collect()
+    gc.freeze()
 
     def one_step(i: int) -> dict:
         name = f"bench-{i}"

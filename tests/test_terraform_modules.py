@@ -99,3 +99,81 @@ def test_mi355x_template_uses_labeller_flag_the_binary_implements():
     src = open(os.path.join(generate.CSRC, "tk_topo.cpp"), encoding="utf-8").read()
     assert '"--labels"' in src
     assert "amdgpu-topo-labeller --labels" in scripts.INSTALL_MI355X_NODE
+
+
+def _hcl_structure_errors(text: str) -> list:
+    """Lexical sanity of generated HCL: balanced {}/[]/() outside strings and comments,
+    terminated strings and ${...}/%{...} templates, closed heredocs."""
+    errs, stack = [], []
+    i, n, line = 0, len(text), 1
+    pairs = {"}": "{", "]": "[", ")": "("}
+    while i < n:
+        c = text[i]
+        if c == "\n":
+            line += 1
+        if c == "#" or text.startswith("//", i):
+            j = text.find("\n", i)
+            i = n if j < 0 else j
+            continue
+        if text.startswith("/*", i):
+            j = text.find("*/", i + 2)
+            if j < 0:
+                errs.append(f"line {line}: unterminated /* comment")
+                break
+            line += text.count("\n", i, j)
+            i = j + 2
+            continue
+        if text.startswith("<<", i):
+            m = re.match(r"<<-?([A-Za-z_]+)\n", text[i:])
+            if m:
+                end = re.search(r"^\s*" + m.group(1) + r"\s*$", text[i + m.end():], re.M)
+                if not end:
+                    errs.append(f"line {line}: heredoc {m.group(1)} not closed")
+                    break
+                seg = text[i:i + m.end() + end.end()]
+                line += seg.count("\n")
+                i += len(seg)
+                continue
+        if c == '"':
+            j, depth = i + 1, 0
+            while j < n:
+                if text[j] == "\\":
+                    j += 2
+                    continue
+                if text.startswith("${", j) or text.startswith("%{", j):
+                    depth += 1
+                    j += 2
+                    continue
+                if text[j] == "}" and depth:
+                    depth -= 1
+                elif text[j] == '"' and not depth:
+                    break
+                elif text[j] == "\n" and not depth:
+                    errs.append(f"line {line}: newline in string")
+                    break
+                j += 1
+            if j >= n:
+                errs.append(f"line {line}: unterminated string")
+                break
+            line += text.count("\n", i, j)
+            i = j + 1
+            continue
+        if c in "{[(":
+            stack.append((c, line))
+        elif c in "}])":
+            if not stack or stack[-1][0] != pairs[c]:
+                errs.append(f"line {line}: unbalanced {c!r}")
+                break
+            stack.pop()
+        i += 1
+    errs += [f"line {ln}: {ch!r} never closed" for ch, ln in stack]
+    return errs
+
+
+@pytest.mark.parametrize("mod", MODULES, ids=lambda m: m.name)
+def test_hcl_is_lexically_well_formed(mod):
+    for rel in ("main.tf", "variables.tf", "outputs.tf", "versions.tf"):
+        text = generate.rendered_files(mod)[rel]
+        assert not _hcl_structure_errors(text), (mod.name, rel, _hcl_structure_errors(text))
+    assert _hcl_structure_errors('a = { b = "x"') == ["line 1: '{' never closed"]
+    assert _hcl_structure_errors('a = "${var.x}" }')[0].startswith("line 1: unbalanced")

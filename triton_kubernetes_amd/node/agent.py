@@ -496,6 +496,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     devices = [int(d) for d in args.devices.split(",") if d.strip()]
     agent = NodeAgent(name=host, mode=args.mode, devices=devices, root=args.root, token=token)
     url = agent.serve(host or "127.0.0.1", int(port))
+    import gc
+
+    gc.collect()
+    gc.freeze()  # long-lived daemon: keep startup objects out of every later collection
     print(json.dumps({"listening": url, "token_from_file": bool(token)}), flush=True)
     try:
         while True:
