@@ -146,3 +146,30 @@ def test_addon_manifest_options():
     assert names == ["amdgpu-device-plugin", "rccl-env", "amdgpu-node-labeller", "rccl-ready"]
     cm = addon_manifests({})[1][1]
     assert cm["data"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
+
+
+def test_terraform_cluster_script_against_fake(rancher, tmp_path):
+    """The cluster modules' data "external" program (S4) speaks to Rancher like RancherClient does."""
+    import subprocess
+
+    from triton_kubernetes_amd.terraform import scripts
+
+    fake, client, outs = rancher
+    script = tmp_path / "ensure_cluster.sh"
+    script.write_text(scripts.RANCHER_CLUSTER)
+    query = {"name": "tf", "version": "v1.28.10-rancher1-1", "network": "calico", "api_url": fake.url,
+             "access_key": outs["rancher_access_key"], "secret_key": outs["rancher_secret_key"],
+             "registry": "", "registry_username": "", "registry_password": ""}
+
+    def run():
+        proc = subprocess.run(["bash", str(script)], input=json.dumps(query), capture_output=True, text=True,
+                              timeout=60)
+        assert proc.returncode == 0, proc.stderr
+        return json.loads(proc.stdout)
+
+    first, second = run(), run()
+    assert first == second  # found by name, registration token reused
+    info = client.ensure_cluster("tf")
+    assert first == {"cluster_id": info.cluster_id, "registration_token": info.registration_token,
+                     "ca_checksum": ca_checksum(FAKE_CACERTS)}
+    assert fake.state.clusters[info.cluster_id]["rancherKubernetesEngineConfig"]["network"]["plugin"] == "calico"

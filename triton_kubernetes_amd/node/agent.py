@@ -329,8 +329,10 @@ class NodeAgent:
         for g in gates:
             g.abort()
 
-    def rccl_prepare(self, uid: bytes, world: int, rank_base: int, ndev: int = 1) -> Dict[str, Any]:
-        """Start this node's share of a cluster communicator (non-blocking init)."""
+    def rccl_prepare(self, uid: bytes, world: int, rank_base: int, ndev: int = 1,
+                     max_bytes: int = 0) -> Dict[str, Any]:
+        """Start this node's share of a cluster communicator (non-blocking init; with
+        ``max_bytes`` the init thread also allocates the sweep buffers)."""
         devs = self._gate_devices(ndev)
         self._expire_gates()
         with span("node.rccl_prepare", node=self.name, rank_base=rank_base, world=world):
@@ -340,7 +342,7 @@ class NodeAgent:
                 from ..ops import rccl
 
                 self._used_rccl = True
-                gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False)
+                gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False, prealloc_bytes=max_bytes)
         with self._gate_mu:
             old = self._gates.pop(uid, None)
             self._gates[uid] = (gate, time.time())
@@ -380,9 +382,29 @@ class NodeAgent:
         out["ranks"] = list(range(rank, rank + len(gate.devices)))
         return out
 
+    # --- native warm start ------------------------------------------------------------------------
+    def warm_native(self) -> None:
+        """Load the native libraries (and everything they pull in) once, up front.
+
+        A dlopen issued while a gate's communicator init is running on another thread can
+        deadlock against the HIP runtime (dlopen holds the loader lock; the init thread holds
+        runtime locks and needs the loader lock) — observed under rocprofv3.  Loading them here,
+        before any request is served, keeps dlopen off the bring-up path."""
+        if self.topology_override is not None or not self.devices:
+            return
+        from ..ops import probe, rccl, topo
+
+        probe._lib()
+        rccl._lib()
+        try:
+            topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
+        except Exception:  # noqa: BLE001 - topology falls back to other sources later
+            pass
+
     # --- HTTP server ----------------------------------------------------------------------------
     def serve(self, host: str = "127.0.0.1", port: int = 0) -> str:
         agent = self
+        self.warm_native()
 
         class H(http.server.BaseHTTPRequestHandler):
             protocol_version = "HTTP/1.1"
@@ -439,7 +461,8 @@ class NodeAgent:
                     if path == "/v1/rccl-prepare":
                         return self._reply(200, agent.rccl_prepare(base64.b64decode(body["uid"]),
                                                                    int(body["world"]), int(body["rank_base"]),
-                                                                   int(body.get("ndev", 1))))
+                                                                   int(body.get("ndev", 1)),
+                                                                   int(body.get("max_bytes", 0))))
                     if path == "/v1/rccl-gate":
                         uid = base64.b64decode(body["uid"])
                         return self._reply(200, agent.rccl_gate(int(body["rank"]), int(body["world"]), uid,

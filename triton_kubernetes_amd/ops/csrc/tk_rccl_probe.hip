@@ -221,6 +221,8 @@ struct Gate {
   bool abandoned = false;
   char err[512] = {0};
   std::thread init_thread;
+  size_t prealloc_bytes = 0;     // sweep buffers allocated by the init thread after the comms
+  std::vector<RankBufs> bufs;    // (filled when prealloc_bytes > 0 and the init succeeded)
 };
 static std::mutex g_gate_mu;
 static std::vector<std::pair<int, Gate*>> g_gates;
@@ -270,6 +272,18 @@ static void init_body(Gate* g, ncclUniqueId id) {
   ncclResult_t re = ncclGroupEnd();
   if (r == ncclSuccess) r = re;
   if (r != ncclSuccess && !g->err[0]) snprintf(g->err, sizeof(g->err), "ncclCommInitRank: %s", ncclGetErrorString(r));
+  if (r == ncclSuccess && g->prealloc_bytes) {
+    // the sweep's buffers too, so the gate request only runs collectives
+    g->bufs.resize(g->devices.size());
+    for (size_t d = 0; d < g->devices.size(); ++d) {
+      (void)hipSetDevice(g->devices[d]);
+      if (alloc_bufs(g->bufs[d], g->prealloc_bytes) != 0) {
+        for (auto& b : g->bufs) free_bufs(b);
+        g->bufs.clear();
+        break;
+      }
+    }
+  }
   bool orphan;
   {
     std::lock_guard<std::mutex> lk(g->mu);
@@ -279,6 +293,7 @@ static void init_body(Gate* g, ncclUniqueId id) {
   }
   g->cv.notify_all();
   if (orphan) {  // released while initialising: nobody else will touch it
+    for (size_t d = 0; d < g->bufs.size(); ++d) { (void)hipSetDevice(g->devices[d]); free_bufs(g->bufs[d]); }
     destroy_comms(g, /*abort=*/true);
     delete g;
     g_abandoned.fetch_sub(1);
@@ -314,13 +329,15 @@ static void release_gate(Gate* g, bool abort) {
     }
   }
   if (g->init_thread.joinable()) g->init_thread.join();
+  for (size_t d = 0; d < g->bufs.size(); ++d) { (void)hipSetDevice(g->devices[d]); free_bufs(g->bufs[d]); }
   destroy_comms(g, abort);
   delete g;
 }
 
-// Returns a handle > 0, or < 0 on error (tkr_last_error()).
-extern "C" int tkr_gate_begin(const unsigned char* uid128, int world, int rank_base, int ndev, const int* devices,
-                              int blocking) {
+// Returns a handle > 0, or < 0 on error (tkr_last_error()).  prealloc_bytes > 0: the init
+// thread also allocates the sweep buffers (largest message size) once the comms are up.
+extern "C" int tkr_gate_begin_ex(const unsigned char* uid128, int world, int rank_base, int ndev,
+                                 const int* devices, int blocking, size_t prealloc_bytes) {
   if (ndev < 1 || world < ndev || rank_base < 0 || rank_base + ndev > world) {
     snprintf(g_err, sizeof(g_err), "bad gate geometry: world=%d rank_base=%d ndev=%d", world, rank_base, ndev);
     return -1;
@@ -332,6 +349,7 @@ extern "C" int tkr_gate_begin(const unsigned char* uid128, int world, int rank_b
   g->comms.assign(ndev, nullptr);
   g->rank_base = rank_base;
   g->world = world;
+  g->prealloc_bytes = prealloc_bytes;
   g->t_begin = std::chrono::steady_clock::now();
   if (blocking) {
     init_body(g, id);
@@ -348,6 +366,11 @@ extern "C" int tkr_gate_begin(const unsigned char* uid128, int world, int rank_b
   const int h = g_next_gate++;
   g_gates.emplace_back(h, g);
   return h;
+}
+
+extern "C" int tkr_gate_begin(const unsigned char* uid128, int world, int rank_base, int ndev, const int* devices,
+                              int blocking) {
+  return tkr_gate_begin_ex(uid128, world, rank_base, ndev, devices, blocking, 0);
 }
 
 // 0 ready, 1 still initialising, < 0 error.
@@ -398,11 +421,18 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
   if (g->init_thread.joinable()) g->init_thread.join();
   size_t max_bytes = 0;
   for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;
-  std::vector<RankBufs> bufs(ndev);
+  std::vector<RankBufs> bufs;
   t_phase = std::chrono::steady_clock::now();
-  for (int d = 0; d < ndev && rc == 0; ++d) {
-    if (hipSetDevice(g->devices[d]) != hipSuccess) { rc = -1; break; }
-    rc = alloc_bufs(bufs[d], max_bytes);
+  if (!g->bufs.empty() && g->prealloc_bytes >= max_bytes) {
+    bufs.swap(g->bufs);  // allocated by the init thread
+  } else {
+    for (size_t d = 0; d < g->bufs.size(); ++d) { (void)hipSetDevice(g->devices[d]); free_bufs(g->bufs[d]); }
+    g->bufs.clear();
+    bufs.resize(ndev);
+    for (int d = 0; d < ndev && rc == 0; ++d) {
+      if (hipSetDevice(g->devices[d]) != hipSuccess) { rc = -1; break; }
+      rc = alloc_bufs(bufs[d], max_bytes);
+    }
   }
   phase_ms[1] = ms_since(t_phase);
   t_phase = std::chrono::steady_clock::now();

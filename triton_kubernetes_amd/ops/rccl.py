@@ -37,6 +37,8 @@ def _lib():
                                     ctypes.c_int, ctypes.c_int, dp, dp, dp, dp]
     lib.tkr_gate_begin.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_int), ctypes.c_int]
+    lib.tkr_gate_begin_ex.argtypes = [ctypes.c_char_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t]
     lib.tkr_gate_poll.argtypes = [ctypes.c_int]
     lib.tkr_gate_abort.argtypes = [ctypes.c_int]
     lib.tkr_gate_sweep.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
@@ -121,10 +123,12 @@ class GateComm:
     :meth:`sweep` waits for the rest, runs the verified all-reduce sweep and
     consumes the handle.  :meth:`abort` releases a gate that will never run."""
 
-    def __init__(self, uid: bytes, world: int, rank_base: int, devices: Sequence[int], blocking: bool = False):
+    def __init__(self, uid: bytes, world: int, rank_base: int, devices: Sequence[int], blocking: bool = False,
+                 prealloc_bytes: int = 0):
         self.world, self.rank_base, self.devices = world, rank_base, list(devices)
         devs = (ctypes.c_int * len(self.devices))(*self.devices)
-        h = _lib().tkr_gate_begin(uid, world, rank_base, len(self.devices), devs, 1 if blocking else 0)
+        h = _lib().tkr_gate_begin_ex(uid, world, rank_base, len(self.devices), devs, 1 if blocking else 0,
+                                     int(prealloc_bytes))
         if h < 0:
             raise RCCLError(f"ranks {rank_base}+{len(self.devices)}/{world}: {_lib().tkr_last_error().decode()}")
         self.handle = h

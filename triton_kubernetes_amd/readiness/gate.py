@@ -101,7 +101,8 @@ class ClusterGate:
             with span("gate.prepare", world=self.world):
                 uid = self.transport.post(self.members[0].host, "/v1/rccl-uid", {})["uid"]
                 self._post_all("/v1/rccl-prepare", lambda m: {"uid": uid, "world": self.world,
-                                                               "rank_base": m.rank_base, "ndev": m.ndev})
+                                                               "rank_base": m.rank_base, "ndev": m.ndev,
+                                                               "max_bytes": max(self.sizes)})
             with self._mu:
                 self.uid, self.prepared = uid, True
         except Exception as exc:  # noqa: BLE001 - run() falls back to an unprepared gate

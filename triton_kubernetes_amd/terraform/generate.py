@@ -62,17 +62,79 @@ class Var:
     sensitive: bool = False
 
     def hcl(self) -> str:
-        lines = [f'variable "{self.name}" {{']
-        if self.type:
-            lines.append(f"  type        = {self.type}")
-        if self.description:
-            lines.append(f"  description = {json.dumps(self.description)}")
+        """Terraform >= 1.3 declaration: explicit type, description, default, validation."""
+        vtype = self.type or _infer_type(self.default)
+        desc = self.description or VAR_DOCS.get(self.name) or _doc_from_name(self.name)
+        lines = [f'variable "{self.name}" {{', f"  description = {json.dumps(desc)}", f"  type        = {vtype}"]
         if self.default is not None:
             lines.append(f"  default     = {hcl_value(self.default)}")
         if self.sensitive:
             lines.append("  sensitive   = true")
+        rule = VAR_VALIDATIONS.get(self.name)
+        if rule is not None:
+            cond, msg = rule
+            lines += ["", "  validation {", f"    condition     = {cond}",
+                      f"    error_message = {json.dumps(msg)}", "  }"]
         lines.append("}")
         return "\n".join(lines)
+
+
+def _infer_type(default: Any) -> str:
+    if isinstance(default, bool):
+        return "bool"
+    if isinstance(default, (list, tuple)):
+        return "list(string)"
+    if isinstance(default, dict):
+        return "map(string)"
+    if isinstance(default, (int, float)) and not isinstance(default, bool):
+        return "number"
+    return "string"
+
+
+def _doc_from_name(name: str) -> str:
+    words = name.replace("_", " ")
+    for prefix, cloud in (("aws ", "AWS"), ("gcp ", "GCP"), ("azure ", "Azure"), ("triton ", "Triton"),
+                          ("vsphere ", "vSphere"), ("ebs ", "EBS"), ("k8s ", "Kubernetes")):
+        if words.startswith(prefix):
+            words = cloud + " " + words[len(prefix):]
+    return words[0].upper() + words[1:] + "."
+
+
+# Descriptions for variables shared by many modules (the rest are derived from the name).
+VAR_DOCS = {
+    "rancher_api_url": "Base URL of the Rancher server (the cluster manager's rancher_url output).",
+    "rancher_access_key": "Rancher API access key (cluster manager output).",
+    "rancher_secret_key": "Rancher API secret key (cluster manager output).",
+    "rancher_cluster_registration_token": "Registration token of the cluster the node joins.",
+    "rancher_cluster_ca_checksum": "SHA-256 of the Rancher CA bundle, pinned by the agent.",
+    "rancher_server_image": "Rancher server container image.",
+    "rancher_agent_image": "Rancher agent container image.",
+    "rancher_registry": "Private registry serving the Rancher images (empty: Docker Hub).",
+    "rancher_registry_username": "User for rancher_registry.",
+    "rancher_registry_password": "Password for rancher_registry.",
+    "k8s_version": "RKE Kubernetes version.",
+    "k8s_network_provider": "CNI plugin of the cluster.",
+    "k8s_registry": "Private registry for the Kubernetes system images (empty: default).",
+    "k8s_registry_username": "User for k8s_registry.",
+    "k8s_registry_password": "Password for k8s_registry.",
+    "hostname": "Host name given to the node.",
+    "docker_engine_install_url": "Script that installs the container runtime when it is missing.",
+    "host": "Address of the machine reached over SSH.",
+    "ssh_user": "SSH login user.",
+    "key_path": "Private key used for SSH.",
+    "bastion_host": "Optional SSH jump host (empty: direct).",
+    "gpu_count": "GPUs the MI355X node must expose.",
+    "gpu_burnin": "Burn-in level run on every GPU before the node joins.",
+    "rccl_env": "Extra RCCL/HSA environment written to /etc/rccl/rccl.env.",
+}
+VAR_VALIDATIONS = {
+    "k8s_network_provider": ('contains(["calico", "flannel", "canal", "weave"], var.k8s_network_provider)',
+                             "k8s_network_provider must be one of calico, flannel, canal, weave."),
+    "gpu_burnin": ('contains(["quick", "full", "off"], var.gpu_burnin)', "gpu_burnin must be quick, full or off."),
+    "rancher_host_labels": ('length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], '
+                            'keys(var.rancher_host_labels)[0])',
+                            "rancher_host_labels must hold exactly one of worker, etcd or control."),
+}
 
 
 @dataclass
@@ -160,10 +222,18 @@ MANAGER_OUTPUTS = [
     ("rancher_secret_key", "data.external.rancher_api_key.result.secret_key", True),
 ]
 CLUSTER_OUTPUTS = [
-    ("rancher_cluster_id", "data.external.rancher_cluster.result.cluster_id", False),
-    ("rancher_cluster_registration_token", "data.external.rancher_cluster.result.registration_token", True),
-    ("rancher_cluster_ca_checksum", "data.external.rancher_cluster.result.ca_checksum", False),
+    ("rancher_cluster_id", 'data.external.cluster.result["cluster_id"]', False),
+    ("rancher_cluster_registration_token", 'data.external.cluster.result["registration_token"]', True),
+    ("rancher_cluster_ca_checksum", 'data.external.cluster.result["ca_checksum"]', False),
 ]
+OUTPUT_DOCS = {
+    "rancher_url": "URL of the Rancher server.",
+    "rancher_access_key": "API access key created for triton-kubernetes.",
+    "rancher_secret_key": "API secret key created for triton-kubernetes.",
+    "rancher_cluster_id": "Rancher id of the cluster (found by name or created).",
+    "rancher_cluster_registration_token": "Token nodes present when they register.",
+    "rancher_cluster_ca_checksum": "Checksum of the Rancher CA bundle that agents pin.",
+}
 
 
 def _manager_tail(connection: str, install_docker_remote: bool) -> str:
@@ -264,20 +334,33 @@ def _agent_userdata(disk_device: str = '""', disk_mount: str = '""', extra: str 
   }})'''
 
 
-def _cluster_data(extra_query: str = "") -> str:
-    return f'''data "external" "rancher_cluster" {{
-  program = ["bash", "${{path.module}}/files/rancher_cluster.sh"]
-  query = {{
-    rancher_api_url       = var.rancher_api_url
-    rancher_access_key    = var.rancher_access_key
-    rancher_secret_key    = var.rancher_secret_key
-    name                  = var.name
-    k8s_version           = var.k8s_version
-    k8s_network_provider  = var.k8s_network_provider
-    k8s_registry          = var.k8s_registry
-    k8s_registry_username = var.k8s_registry_username
-    k8s_registry_password = var.k8s_registry_password{extra_query}
-  }}
+def _cluster_data() -> str:
+    """S4 as a data source: find-or-create the RKE cluster by name, then its registration
+    token and CA checksum (files/ensure_cluster.sh, run on the operator machine)."""
+    return f'''locals {{
+  # everything ensure_cluster.sh needs, passed as its JSON query
+  cluster_request = merge(
+    {{
+      name    = var.name
+      version = var.k8s_version
+      network = var.k8s_network_provider
+    }},
+    {{
+      api_url    = var.rancher_api_url
+      access_key = var.rancher_access_key
+      secret_key = var.rancher_secret_key
+    }},
+    {{
+      registry          = var.k8s_registry
+      registry_username = var.k8s_registry_username
+      registry_password = var.k8s_registry_password
+    }},
+  )
+}}
+
+data "external" "cluster" {{
+  program = ["bash", "${{path.module}}/files/ensure_cluster.sh"]
+  query   = local.cluster_request
 }}
 '''
 
@@ -285,7 +368,7 @@ def _cluster_data(extra_query: str = "") -> str:
 MANAGER_FILES = {"install_docker.sh.tftpl": scripts.INSTALL_DOCKER,
                  "install_rancher_server.sh.tftpl": scripts.INSTALL_RANCHER_SERVER,
                  "setup_rancher.sh.tftpl": scripts.SETUP_RANCHER, "read_api_key.sh": scripts.READ_API_KEY}
-CLUSTER_FILES = {"rancher_cluster.sh": scripts.RANCHER_CLUSTER}
+CLUSTER_FILES = {"ensure_cluster.sh": scripts.RANCHER_CLUSTER}
 HOST_FILES = {"install_rancher_agent.sh.tftpl": scripts.INSTALL_RANCHER_AGENT}
 
 
@@ -1197,9 +1280,10 @@ def render_variables(mod: Module) -> str:
 def render_outputs(mod: Module) -> str:
     out = []
     for name, expr, sensitive in mod.outputs:
-        lines = [f'output "{name}" {{', f"  value = {expr}"]
+        lines = [f'output "{name}" {{', f"  description = {json.dumps(OUTPUT_DOCS.get(name, _doc_from_name(name)))}",
+                 f"  value       = {expr}"]
         if sensitive:
-            lines.append("  sensitive = true")
+            lines.append("  sensitive   = true")
         lines.append("}")
         out.append("\n".join(lines))
     return ("\n\n".join(out) + "\n") if out else "# This module has no outputs.\n"

@@ -1,89 +1,133 @@
 variable "hostname" {
+  description = "Host name given to the node."
+  type        = string
 }
 
 variable "rancher_api_url" {
+  description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
+  type        = string
 }
 
 variable "rancher_cluster_registration_token" {
+  description = "Registration token of the cluster the node joins."
+  type        = string
   sensitive   = true
 }
 
 variable "rancher_cluster_ca_checksum" {
+  description = "SHA-256 of the Rancher CA bundle, pinned by the agent."
+  type        = string
 }
 
 variable "rancher_host_labels" {
-  type        = map(string)
   description = "A single-key map: {worker|etcd|control = \"true\"}"
+  type        = map(string)
+
+  validation {
+    condition     = length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], keys(var.rancher_host_labels)[0])
+    error_message = "rancher_host_labels must hold exactly one of worker, etcd or control."
+  }
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "aws_access_key" {
+  description = "AWS access key."
+  type        = string
 }
 
 variable "aws_secret_key" {
+  description = "AWS secret key."
+  type        = string
   sensitive   = true
 }
 
 variable "aws_region" {
+  description = "AWS region."
+  type        = string
 }
 
 variable "aws_ami_id" {
+  description = "AWS ami id."
+  type        = string
 }
 
 variable "aws_instance_type" {
+  description = "AWS instance type."
+  type        = string
   default     = "t3.large"
 }
 
 variable "aws_subnet_id" {
+  description = "AWS subnet id."
+  type        = string
 }
 
 variable "aws_security_group_id" {
+  description = "AWS security group id."
+  type        = string
 }
 
 variable "aws_key_name" {
+  description = "AWS key name."
+  type        = string
 }
 
 variable "ebs_volume_device_name" {
+  description = "EBS volume device name."
+  type        = string
   default     = ""
 }
 
 variable "ebs_volume_mount_path" {
+  description = "EBS volume mount path."
+  type        = string
   default     = ""
 }
 
 variable "ebs_volume_type" {
+  description = "EBS volume type."
+  type        = string
   default     = "gp3"
 }
 
 variable "ebs_volume_iops" {
+  description = "EBS volume iops."
+  type        = string
   default     = ""
 }
 
 variable "ebs_volume_size" {
+  description = "EBS volume size."
+  type        = string
   default     = ""
 }

@@ -1,0 +1,49 @@
+#!/bin/bash
+# S4 as a Terraform data "external" program (operator machine): find the RKE cluster
+# by name or create it, then its registration token (reused when the cluster existed)
+# and the checksum of the Rancher CA bundle.  Query keys: name, version, network,
+# api_url, access_key, secret_key, registry, registry_username, registry_password.
+exec python3 -c '
+import base64, hashlib, json, ssl, sys, urllib.request
+
+q = json.load(sys.stdin)
+ctx = ssl.create_default_context()
+ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE  # self-signed Rancher certificates
+auth = "Basic " + base64.b64encode((q["access_key"] + ":" + q["secret_key"]).encode()).decode()
+
+
+def call(method, path, body=None):
+    req = urllib.request.Request(q["api_url"].rstrip("/") + path, method=method,
+                                 data=None if body is None else json.dumps(body).encode(),
+                                 headers={"Authorization": auth, "Accept": "application/json",
+                                          "Content-Type": "application/json"})
+    with urllib.request.urlopen(req, context=ctx, timeout=60) as resp:
+        return json.load(resp)
+
+
+found = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
+if found:
+    cluster_id = found[0]["id"]
+else:
+    rke = {"type": "rancherKubernetesEngineConfig", "kubernetesVersion": q["version"],
+           "ignoreDockerVersion": False, "sshAgentAuth": False,
+           "authentication": {"type": "authnConfig", "strategy": "x509"},
+           "network": {"type": "networkConfig", "plugin": q["network"]},
+           "services": {"type": "rkeConfigServices",
+                        "kubeApi": {"type": "kubeAPIService", "podSecurityPolicy": False}}}
+    if q.get("registry"):
+        rke["privateRegistries"] = [{"url": q["registry"], "user": q.get("registry_username", ""),
+                                     "password": q.get("registry_password", "")}]
+    cluster_id = call("POST", "/v3/cluster", {"type": "cluster", "name": q["name"],
+                                              "rancherKubernetesEngineConfig": rke}).get("id", "")
+if not cluster_id:
+    sys.exit("Unable to create cluster!")
+tokens = call("GET", "/v3/clusters/%s/clusterregistrationtokens" % cluster_id).get("data") if found else []
+token = (tokens[0].get("token") if tokens else "") or call(
+    "POST", "/v3/clusterregistrationtoken", {"type": "clusterRegistrationToken", "clusterId": cluster_id}).get("token")
+if not token:
+    sys.exit("Unable to create cluster registration token!")
+cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
+print(json.dumps({"cluster_id": cluster_id, "registration_token": token,
+                  "ca_checksum": hashlib.sha256((cacerts + "\n").encode()).hexdigest()}))
+'

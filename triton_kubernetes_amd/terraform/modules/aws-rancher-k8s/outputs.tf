@@ -1,24 +1,30 @@
 output "rancher_cluster_id" {
-  value = data.external.rancher_cluster.result.cluster_id
+  description = "Rancher id of the cluster (found by name or created)."
+  value       = data.external.cluster.result["cluster_id"]
 }
 
 output "rancher_cluster_registration_token" {
-  value = data.external.rancher_cluster.result.registration_token
-  sensitive = true
+  description = "Token nodes present when they register."
+  value       = data.external.cluster.result["registration_token"]
+  sensitive   = true
 }
 
 output "rancher_cluster_ca_checksum" {
-  value = data.external.rancher_cluster.result.ca_checksum
+  description = "Checksum of the Rancher CA bundle that agents pin."
+  value       = data.external.cluster.result["ca_checksum"]
 }
 
 output "aws_subnet_id" {
-  value = aws_subnet.public.id
+  description = "AWS subnet id."
+  value       = aws_subnet.public.id
 }
 
 output "aws_security_group_id" {
-  value = aws_security_group.rke_ports.id
+  description = "AWS security group id."
+  value       = aws_security_group.rke_ports.id
 }
 
 output "aws_key_name" {
-  value = var.aws_key_name
+  description = "AWS key name."
+  value       = var.aws_key_name
 }

@@ -1,12 +1,15 @@
 output "rancher_url" {
-  value = "https://${local.rancher_master_ip}"
+  description = "URL of the Rancher server."
+  value       = "https://${local.rancher_master_ip}"
 }
 
 output "rancher_access_key" {
-  value = data.external.rancher_api_key.result.access_key
+  description = "API access key created for triton-kubernetes."
+  value       = data.external.rancher_api_key.result.access_key
 }
 
 output "rancher_secret_key" {
-  value = data.external.rancher_api_key.result.secret_key
-  sensitive = true
+  description = "API secret key created for triton-kubernetes."
+  value       = data.external.rancher_api_key.result.secret_key
+  sensitive   = true
 }

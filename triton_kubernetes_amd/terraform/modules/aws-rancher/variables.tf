@@ -1,79 +1,109 @@
 variable "name" {
   description = "Human readable name used as prefix to generated names."
+  type        = string
 }
 
 variable "rancher_admin_password" {
   description = "The Rancher admin password"
+  type        = string
   sensitive   = true
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_server_image" {
   description = "The Rancher Server image to use."
+  type        = string
   default     = "rancher/rancher:v2.8.5"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "aws_access_key" {
+  description = "AWS access key."
+  type        = string
 }
 
 variable "aws_secret_key" {
+  description = "AWS secret key."
+  type        = string
   sensitive   = true
 }
 
 variable "aws_region" {
+  description = "AWS region."
+  type        = string
 }
 
 variable "aws_vpc_cidr" {
+  description = "AWS vpc cidr."
+  type        = string
   default     = "10.0.0.0/16"
 }
 
 variable "aws_subnet_cidr" {
+  description = "AWS subnet cidr."
+  type        = string
   default     = "10.0.2.0/24"
 }
 
 variable "aws_ami_id" {
+  description = "AWS ami id."
+  type        = string
 }
 
 variable "aws_instance_type" {
+  description = "AWS instance type."
+  type        = string
   default     = "t3.medium"
 }
 
 variable "aws_key_name" {
+  description = "AWS key name."
+  type        = string
 }
 
 variable "aws_public_key_path" {
+  description = "AWS public key path."
+  type        = string
   default     = "~/.ssh/id_rsa.pub"
 }
 
 variable "aws_private_key_path" {
+  description = "AWS private key path."
+  type        = string
   default     = "~/.ssh/id_rsa"
 }
 
 variable "aws_ssh_user" {
+  description = "AWS ssh user."
+  type        = string
   default     = "ubuntu"
 }

@@ -1,113 +1,167 @@
 variable "hostname" {
+  description = "Host name given to the node."
+  type        = string
 }
 
 variable "rancher_api_url" {
+  description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
+  type        = string
 }
 
 variable "rancher_cluster_registration_token" {
+  description = "Registration token of the cluster the node joins."
+  type        = string
   sensitive   = true
 }
 
 variable "rancher_cluster_ca_checksum" {
+  description = "SHA-256 of the Rancher CA bundle, pinned by the agent."
+  type        = string
 }
 
 variable "rancher_host_labels" {
-  type        = map(string)
   description = "A single-key map: {worker|etcd|control = \"true\"}"
+  type        = map(string)
+
+  validation {
+    condition     = length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], keys(var.rancher_host_labels)[0])
+    error_message = "rancher_host_labels must hold exactly one of worker, etcd or control."
+  }
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "azure_subscription_id" {
+  description = "Azure subscription id."
+  type        = string
   default     = ""
 }
 
 variable "azure_client_id" {
+  description = "Azure client id."
+  type        = string
   default     = ""
 }
 
 variable "azure_client_secret" {
+  description = "Azure client secret."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "azure_tenant_id" {
+  description = "Azure tenant id."
+  type        = string
   default     = ""
 }
 
 variable "azure_environment" {
+  description = "Azure environment."
+  type        = string
   default     = "public"
 }
 
 variable "azure_location" {
+  description = "Azure location."
+  type        = string
   default     = "westus2"
 }
 
 variable "azure_image_publisher" {
+  description = "Azure image publisher."
+  type        = string
   default     = "Canonical"
 }
 
 variable "azure_image_offer" {
+  description = "Azure image offer."
+  type        = string
   default     = "0001-com-ubuntu-server-jammy"
 }
 
 variable "azure_image_sku" {
+  description = "Azure image sku."
+  type        = string
   default     = "22_04-lts-gen2"
 }
 
 variable "azure_image_version" {
+  description = "Azure image version."
+  type        = string
   default     = "latest"
 }
 
 variable "azure_resource_group_name" {
+  description = "Azure resource group name."
+  type        = string
 }
 
 variable "azure_network_security_group_id" {
+  description = "Azure network security group id."
+  type        = string
 }
 
 variable "azure_subnet_id" {
+  description = "Azure subnet id."
+  type        = string
 }
 
 variable "azure_size" {
+  description = "Azure size."
+  type        = string
   default     = "Standard_D4s_v5"
 }
 
 variable "azure_ssh_user" {
+  description = "Azure ssh user."
+  type        = string
   default     = "ubuntu"
 }
 
 variable "azure_public_key_path" {
+  description = "Azure public key path."
+  type        = string
   default     = "~/.ssh/id_rsa.pub"
 }
 
 variable "azure_disk_mount_path" {
+  description = "Azure disk mount path."
+  type        = string
   default     = ""
 }
 
 variable "azure_disk_size" {
+  description = "Azure disk size."
+  type        = string
   default     = ""
 }

@@ -1,108 +1,166 @@
 variable "name" {
   description = "Human readable name used as prefix to generated names."
+  type        = string
 }
 
 variable "rancher_api_url" {
+  description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
+  type        = string
 }
 
 variable "rancher_access_key" {
+  description = "Rancher API access key (cluster manager output)."
+  type        = string
 }
 
 variable "rancher_secret_key" {
+  description = "Rancher API secret key (cluster manager output)."
+  type        = string
   sensitive   = true
 }
 
 variable "k8s_version" {
+  description = "RKE Kubernetes version."
+  type        = string
   default     = "v1.9.5-rancher1-1"
 }
 
 variable "k8s_network_provider" {
+  description = "CNI plugin of the cluster."
+  type        = string
   default     = "flannel"
+
+  validation {
+    condition     = contains(["calico", "flannel", "canal", "weave"], var.k8s_network_provider)
+    error_message = "k8s_network_provider must be one of calico, flannel, canal, weave."
+  }
 }
 
 variable "rancher_registry" {
+  description = "Private registry serving the Rancher images (empty: Docker Hub)."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
+  description = "User for rancher_registry."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
+  description = "Password for rancher_registry."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "k8s_registry" {
+  description = "Private registry for the Kubernetes system images (empty: default)."
+  type        = string
   default     = ""
 }
 
 variable "k8s_registry_username" {
+  description = "User for k8s_registry."
+  type        = string
   default     = ""
 }
 
 variable "k8s_registry_password" {
+  description = "Password for k8s_registry."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "azure_subscription_id" {
+  description = "Azure subscription id."
+  type        = string
   default     = ""
 }
 
 variable "azure_client_id" {
+  description = "Azure client id."
+  type        = string
   default     = ""
 }
 
 variable "azure_client_secret" {
+  description = "Azure client secret."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "azure_tenant_id" {
+  description = "Azure tenant id."
+  type        = string
   default     = ""
 }
 
 variable "azure_environment" {
+  description = "Azure environment."
+  type        = string
   default     = "public"
 }
 
 variable "azure_location" {
+  description = "Azure location."
+  type        = string
   default     = "westus2"
 }
 
 variable "azure_image_publisher" {
+  description = "Azure image publisher."
+  type        = string
   default     = "Canonical"
 }
 
 variable "azure_image_offer" {
+  description = "Azure image offer."
+  type        = string
   default     = "0001-com-ubuntu-server-jammy"
 }
 
 variable "azure_image_sku" {
+  description = "Azure image sku."
+  type        = string
   default     = "22_04-lts-gen2"
 }
 
 variable "azure_image_version" {
+  description = "Azure image version."
+  type        = string
   default     = "latest"
 }
 
 variable "azure_virtual_network_name" {
+  description = "Azure virtual network name."
+  type        = string
   default     = "k8s-network"
 }
 
 variable "azure_virtual_network_address_space" {
+  description = "Azure virtual network address space."
+  type        = string
   default     = "10.0.0.0/16"
 }
 
 variable "azure_subnet_name" {
+  description = "Azure subnet name."
+  type        = string
   default     = "k8s-subnet"
 }
 
 variable "azure_subnet_address_prefix" {
+  description = "Azure subnet address prefix."
+  type        = string
   default     = "10.0.2.0/24"
 }
 
 variable "azurerm_network_security_group_name" {
+  description = "Azurerm network security group name."
+  type        = string
   default     = "k8s-firewall"
 }

@@ -1,120 +1,168 @@
 variable "name" {
   description = "Human readable name used as prefix to generated names."
+  type        = string
 }
 
 variable "rancher_admin_password" {
   description = "The Rancher admin password"
+  type        = string
   sensitive   = true
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_server_image" {
   description = "The Rancher Server image to use."
+  type        = string
   default     = "rancher/rancher:v2.8.5"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "azure_subscription_id" {
+  description = "Azure subscription id."
+  type        = string
   default     = ""
 }
 
 variable "azure_client_id" {
+  description = "Azure client id."
+  type        = string
   default     = ""
 }
 
 variable "azure_client_secret" {
+  description = "Azure client secret."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "azure_tenant_id" {
+  description = "Azure tenant id."
+  type        = string
   default     = ""
 }
 
 variable "azure_environment" {
+  description = "Azure environment."
+  type        = string
   default     = "public"
 }
 
 variable "azure_location" {
+  description = "Azure location."
+  type        = string
   default     = "westus2"
 }
 
 variable "azure_image_publisher" {
+  description = "Azure image publisher."
+  type        = string
   default     = "Canonical"
 }
 
 variable "azure_image_offer" {
+  description = "Azure image offer."
+  type        = string
   default     = "0001-com-ubuntu-server-jammy"
 }
 
 variable "azure_image_sku" {
+  description = "Azure image sku."
+  type        = string
   default     = "22_04-lts-gen2"
 }
 
 variable "azure_image_version" {
+  description = "Azure image version."
+  type        = string
   default     = "latest"
 }
 
 variable "azure_virtual_network_name" {
+  description = "Azure virtual network name."
+  type        = string
   default     = "rancher-network"
 }
 
 variable "azure_virtual_network_address_space" {
+  description = "Azure virtual network address space."
+  type        = string
   default     = "10.0.0.0/16"
 }
 
 variable "azure_subnet_name" {
+  description = "Azure subnet name."
+  type        = string
   default     = "rancher-subnet"
 }
 
 variable "azure_subnet_address_prefix" {
+  description = "Azure subnet address prefix."
+  type        = string
   default     = "10.0.2.0/24"
 }
 
 variable "azurerm_network_security_group_name" {
+  description = "Azurerm network security group name."
+  type        = string
   default     = "rancher-firewall"
 }
 
 variable "azure_resource_group_name" {
+  description = "Azure resource group name."
+  type        = string
   default     = ""
 }
 
 variable "azure_size" {
+  description = "Azure size."
+  type        = string
   default     = "Standard_D4s_v5"
 }
 
 variable "azure_ssh_user" {
+  description = "Azure ssh user."
+  type        = string
   default     = "ubuntu"
 }
 
 variable "azure_public_key_path" {
+  description = "Azure public key path."
+  type        = string
   default     = "~/.ssh/id_rsa.pub"
 }
 
 variable "azure_private_key_path" {
+  description = "Azure private key path."
+  type        = string
   default     = "~/.ssh/id_rsa"
 }

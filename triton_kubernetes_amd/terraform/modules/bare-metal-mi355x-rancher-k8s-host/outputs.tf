@@ -1,3 +1,4 @@
 output "gpu_node_labels" {
-  value = data.external.gpu_labels.result.labels
+  description = "Gpu node labels."
+  value       = data.external.gpu_labels.result.labels
 }

@@ -1,83 +1,119 @@
 variable "hostname" {
+  description = "Host name given to the node."
+  type        = string
 }
 
 variable "rancher_api_url" {
+  description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
+  type        = string
 }
 
 variable "rancher_cluster_registration_token" {
+  description = "Registration token of the cluster the node joins."
+  type        = string
   sensitive   = true
 }
 
 variable "rancher_cluster_ca_checksum" {
+  description = "SHA-256 of the Rancher CA bundle, pinned by the agent."
+  type        = string
 }
 
 variable "rancher_host_labels" {
-  type        = map(string)
   description = "A single-key map: {worker|etcd|control = \"true\"}"
+  type        = map(string)
+
+  validation {
+    condition     = length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], keys(var.rancher_host_labels)[0])
+    error_message = "rancher_host_labels must hold exactly one of worker, etcd or control."
+  }
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "ssh_user" {
+  description = "SSH login user."
+  type        = string
   default     = "ubuntu"
 }
 
 variable "host" {
+  description = "Address of the machine reached over SSH."
+  type        = string
 }
 
 variable "bastion_host" {
+  description = "Optional SSH jump host (empty: direct)."
+  type        = string
   default     = ""
 }
 
 variable "key_path" {
+  description = "Private key used for SSH."
+  type        = string
   default     = "~/.ssh/id_rsa"
 }
 
 variable "gpu_product" {
+  description = "Gpu product."
+  type        = string
   default     = "MI355X"
 }
 
 variable "gpu_count" {
   description = "GPUs the node must expose"
+  type        = string
   default     = "8"
 }
 
 variable "gpu_burnin" {
   description = "quick | full | off"
+  type        = string
   default     = "quick"
+
+  validation {
+    condition     = contains(["quick", "full", "off"], var.gpu_burnin)
+    error_message = "gpu_burnin must be quick, full or off."
+  }
 }
 
 variable "rccl_env" {
-  type        = map(string)
   description = "RCCL / HSA environment for GPU pods"
+  type        = map(string)
   default     = {}
 }
 
 variable "rccl_min_busbw" {
   description = "node-level all-reduce bus bandwidth gate (GB/s)"
+  type        = string
   default     = "0"
 }

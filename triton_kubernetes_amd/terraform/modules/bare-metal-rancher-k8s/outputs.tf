@@ -1,12 +1,15 @@
 output "rancher_cluster_id" {
-  value = data.external.rancher_cluster.result.cluster_id
+  description = "Rancher id of the cluster (found by name or created)."
+  value       = data.external.cluster.result["cluster_id"]
 }
 
 output "rancher_cluster_registration_token" {
-  value = data.external.rancher_cluster.result.registration_token
-  sensitive = true
+  description = "Token nodes present when they register."
+  value       = data.external.cluster.result["registration_token"]
+  sensitive   = true
 }
 
 output "rancher_cluster_ca_checksum" {
-  value = data.external.rancher_cluster.result.ca_checksum
+  description = "Checksum of the Rancher CA bundle that agents pin."
+  value       = data.external.cluster.result["ca_checksum"]
 }

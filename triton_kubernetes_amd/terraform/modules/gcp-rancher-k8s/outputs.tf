@@ -1,20 +1,25 @@
 output "rancher_cluster_id" {
-  value = data.external.rancher_cluster.result.cluster_id
+  description = "Rancher id of the cluster (found by name or created)."
+  value       = data.external.cluster.result["cluster_id"]
 }
 
 output "rancher_cluster_registration_token" {
-  value = data.external.rancher_cluster.result.registration_token
-  sensitive = true
+  description = "Token nodes present when they register."
+  value       = data.external.cluster.result["registration_token"]
+  sensitive   = true
 }
 
 output "rancher_cluster_ca_checksum" {
-  value = data.external.rancher_cluster.result.ca_checksum
+  description = "Checksum of the Rancher CA bundle that agents pin."
+  value       = data.external.cluster.result["ca_checksum"]
 }
 
 output "gcp_compute_network_name" {
-  value = google_compute_network.default.name
+  description = "GCP compute network name."
+  value       = google_compute_network.default.name
 }
 
 output "gcp_compute_firewall_host_tag" {
-  value = "${var.name}-nodes"
+  description = "GCP compute firewall host tag."
+  value       = "${var.name}-nodes"
 }

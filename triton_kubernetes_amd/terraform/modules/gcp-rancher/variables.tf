@@ -1,71 +1,97 @@
 variable "name" {
   description = "Human readable name used as prefix to generated names."
+  type        = string
 }
 
 variable "rancher_admin_password" {
   description = "The Rancher admin password"
+  type        = string
   sensitive   = true
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_server_image" {
   description = "The Rancher Server image to use."
+  type        = string
   default     = "rancher/rancher:v2.8.5"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "gcp_path_to_credentials" {
+  description = "GCP path to credentials."
+  type        = string
 }
 
 variable "gcp_compute_region" {
+  description = "GCP compute region."
+  type        = string
 }
 
 variable "gcp_project_id" {
+  description = "GCP project id."
+  type        = string
 }
 
 variable "gcp_machine_type" {
+  description = "GCP machine type."
+  type        = string
   default     = "n1-standard-2"
 }
 
 variable "gcp_instance_zone" {
+  description = "GCP instance zone."
+  type        = string
 }
 
 variable "gcp_image" {
+  description = "GCP image."
+  type        = string
   default     = "ubuntu-os-cloud/ubuntu-2204-lts"
 }
 
 variable "gcp_ssh_user" {
+  description = "GCP ssh user."
+  type        = string
   default     = "ubuntu"
 }
 
 variable "gcp_public_key_path" {
+  description = "GCP public key path."
+  type        = string
   default     = "~/.ssh/id_rsa.pub"
 }
 
 variable "gcp_private_key_path" {
+  description = "GCP private key path."
+  type        = string
   default     = "~/.ssh/id_rsa"
 }

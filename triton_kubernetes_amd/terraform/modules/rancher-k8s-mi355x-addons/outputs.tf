@@ -1,3 +1,4 @@
 output "addons_applied" {
-  value = tostring(terraform_data.apply_addons.output)
+  description = "Addons applied."
+  value       = tostring(terraform_data.apply_addons.output)
 }

@@ -1,57 +1,74 @@
 variable "name" {
   description = "Human readable name used as prefix to generated names."
+  type        = string
 }
 
 variable "rancher_admin_password" {
   description = "The Rancher admin password"
+  type        = string
   sensitive   = true
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_server_image" {
   description = "The Rancher Server image to use."
+  type        = string
   default     = "rancher/rancher:v2.8.5"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "triton_account" {
+  description = "Triton account."
+  type        = string
 }
 
 variable "triton_key_path" {
+  description = "Triton key path."
+  type        = string
 }
 
 variable "triton_key_id" {
+  description = "Triton key id."
+  type        = string
 }
 
 variable "triton_url" {
+  description = "Triton url."
+  type        = string
   default     = "https://us-east-1.api.joyent.com"
 }
 
 variable "triton_network_names" {
+  description = "Triton network names."
   type        = list(string)
   default     = [
   "Joyent-SDC-Public"
@@ -59,16 +76,24 @@ variable "triton_network_names" {
 }
 
 variable "triton_image_name" {
+  description = "Triton image name."
+  type        = string
   default     = "ubuntu-certified-22.04"
 }
 
 variable "triton_image_version" {
+  description = "Triton image version."
+  type        = string
 }
 
 variable "triton_ssh_user" {
+  description = "Triton ssh user."
+  type        = string
   default     = "ubuntu"
 }
 
 variable "master_triton_machine_package" {
+  description = "Master triton machine package."
+  type        = string
   default     = "k4-highcpu-kvm-3.75G"
 }

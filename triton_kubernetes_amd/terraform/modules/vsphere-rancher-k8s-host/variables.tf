@@ -1,84 +1,126 @@
 variable "hostname" {
+  description = "Host name given to the node."
+  type        = string
 }
 
 variable "rancher_api_url" {
+  description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
+  type        = string
 }
 
 variable "rancher_cluster_registration_token" {
+  description = "Registration token of the cluster the node joins."
+  type        = string
   sensitive   = true
 }
 
 variable "rancher_cluster_ca_checksum" {
+  description = "SHA-256 of the Rancher CA bundle, pinned by the agent."
+  type        = string
 }
 
 variable "rancher_host_labels" {
-  type        = map(string)
   description = "A single-key map: {worker|etcd|control = \"true\"}"
+  type        = map(string)
+
+  validation {
+    condition     = length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], keys(var.rancher_host_labels)[0])
+    error_message = "rancher_host_labels must hold exactly one of worker, etcd or control."
+  }
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
+  type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
+  type        = string
   default     = "rancher/rancher-agent:v2.8.5"
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
   description = "The password to use."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "vsphere_user" {
+  description = "VSphere user."
+  type        = string
 }
 
 variable "vsphere_password" {
+  description = "VSphere password."
+  type        = string
   sensitive   = true
 }
 
 variable "vsphere_server" {
+  description = "VSphere server."
+  type        = string
 }
 
 variable "vsphere_datacenter_name" {
+  description = "VSphere datacenter name."
+  type        = string
 }
 
 variable "vsphere_datastore_name" {
+  description = "VSphere datastore name."
+  type        = string
 }
 
 variable "vsphere_resource_pool_name" {
+  description = "VSphere resource pool name."
+  type        = string
 }
 
 variable "vsphere_network_name" {
+  description = "VSphere network name."
+  type        = string
 }
 
 variable "vsphere_template_name" {
+  description = "VSphere template name."
+  type        = string
 }
 
 variable "ssh_user" {
+  description = "SSH login user."
+  type        = string
   default     = "ubuntu"
 }
 
 variable "key_path" {
+  description = "Private key used for SSH."
+  type        = string
   default     = "~/.ssh/id_rsa"
 }
 
 variable "vsphere_num_cpus" {
+  description = "VSphere num cpus."
+  type        = string
   default     = "2"
 }
 
 variable "vsphere_memory_mb" {
+  description = "VSphere memory mb."
+  type        = string
   default     = "2048"
 }

@@ -1,69 +1,111 @@
 variable "name" {
   description = "Human readable name used as prefix to generated names."
+  type        = string
 }
 
 variable "rancher_api_url" {
+  description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
+  type        = string
 }
 
 variable "rancher_access_key" {
+  description = "Rancher API access key (cluster manager output)."
+  type        = string
 }
 
 variable "rancher_secret_key" {
+  description = "Rancher API secret key (cluster manager output)."
+  type        = string
   sensitive   = true
 }
 
 variable "k8s_version" {
+  description = "RKE Kubernetes version."
+  type        = string
   default     = "v1.9.5-rancher1-1"
 }
 
 variable "k8s_network_provider" {
+  description = "CNI plugin of the cluster."
+  type        = string
   default     = "flannel"
+
+  validation {
+    condition     = contains(["calico", "flannel", "canal", "weave"], var.k8s_network_provider)
+    error_message = "k8s_network_provider must be one of calico, flannel, canal, weave."
+  }
 }
 
 variable "rancher_registry" {
+  description = "Private registry serving the Rancher images (empty: Docker Hub)."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_username" {
+  description = "User for rancher_registry."
+  type        = string
   default     = ""
 }
 
 variable "rancher_registry_password" {
+  description = "Password for rancher_registry."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "k8s_registry" {
+  description = "Private registry for the Kubernetes system images (empty: default)."
+  type        = string
   default     = ""
 }
 
 variable "k8s_registry_username" {
+  description = "User for k8s_registry."
+  type        = string
   default     = ""
 }
 
 variable "k8s_registry_password" {
+  description = "Password for k8s_registry."
+  type        = string
   default     = ""
   sensitive   = true
 }
 
 variable "vsphere_user" {
+  description = "VSphere user."
+  type        = string
 }
 
 variable "vsphere_password" {
+  description = "VSphere password."
+  type        = string
   sensitive   = true
 }
 
 variable "vsphere_server" {
+  description = "VSphere server."
+  type        = string
 }
 
 variable "vsphere_datacenter_name" {
+  description = "VSphere datacenter name."
+  type        = string
 }
 
 variable "vsphere_datastore_name" {
+  description = "VSphere datastore name."
+  type        = string
 }
 
 variable "vsphere_resource_pool_name" {
+  description = "VSphere resource pool name."
+  type        = string
 }
 
 variable "vsphere_network_name" {
+  description = "VSphere network name."
+  type        = string
 }

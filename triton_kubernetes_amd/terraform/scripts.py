@@ -79,41 +79,54 @@ print(json.dumps({"access_key": t["name"], "secret_key": t["token"].split(":", 1
 """
 
 RANCHER_CLUSTER = r"""#!/bin/bash
-# S4: data "external" program run on the operator machine.  Idempotent
-# find-or-create of the RKE cluster, its registration token and CA checksum.
-set -euo pipefail
-eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
-api() { curl -ksf -u "$rancher_access_key:$rancher_secret_key" -H 'Accept: application/json' -H 'Content-Type: application/json' "$@"; }
-py() { python3 -c "$1"; }
-search=$(api "$rancher_api_url/v3/clusters?name=$name")
-cluster_id=$(printf '%s' "$search" | py 'import json,sys; d=json.load(sys.stdin)["data"]; print(d[0]["id"] if d else "")')
-existed=true
-if [ -z "$cluster_id" ]; then
-  existed=false
-  body=$(NAME="$name" VER="$k8s_version" NET="$k8s_network_provider" REG="${k8s_registry:-}" \
-         REGU="${k8s_registry_username:-}" REGP="${k8s_registry_password:-}" py '
-import json, os
-rke = {"ignoreDockerVersion": False, "sshAgentAuth": False, "type": "rancherKubernetesEngineConfig",
-       "kubernetesVersion": os.environ["VER"], "authentication": {"type": "authnConfig", "strategy": "x509"},
-       "network": {"type": "networkConfig", "plugin": os.environ["NET"]},
-       "services": {"type": "rkeConfigServices", "kubeApi": {"podSecurityPolicy": False, "type": "kubeAPIService"}}}
-if os.environ["REG"]:
-    rke["privateRegistries"] = [{"url": os.environ["REG"], "user": os.environ["REGU"], "password": os.environ["REGP"]}]
-print(json.dumps({"type": "cluster", "name": os.environ["NAME"], "rancherKubernetesEngineConfig": rke}))')
-  cluster_id=$(api -X POST -d "$body" "$rancher_api_url/v3/cluster" | py 'import json,sys; print(json.load(sys.stdin).get("id",""))')
-fi
-[ -n "$cluster_id" ] || { echo "Unable to create cluster!" >&2; exit 1; }
-token=""
-if [ "$existed" = true ]; then
-  token=$(api "$rancher_api_url/v3/clusters/$cluster_id/clusterregistrationtokens" | py 'import json,sys; d=json.load(sys.stdin)["data"]; print(d[0]["token"] if d else "")')
-fi
-if [ -z "$token" ]; then
-  token=$(api -X POST -d "{\"type\":\"clusterRegistrationToken\",\"clusterId\":\"$cluster_id\"}" \
-          "$rancher_api_url/v3/clusterregistrationtoken" | py 'import json,sys; print(json.load(sys.stdin).get("token",""))')
-fi
-[ -n "$token" ] || { echo "Unable to create cluster registration token!" >&2; exit 1; }
-checksum=$(api "$rancher_api_url/v3/settings/cacerts" | py 'import json,sys,hashlib; v=json.load(sys.stdin)["value"]; print(hashlib.sha256((v+"\n").encode()).hexdigest())')
-CID="$cluster_id" TOK="$token" SUM="$checksum" py 'import json,os; print(json.dumps({"cluster_id": os.environ["CID"], "registration_token": os.environ["TOK"], "ca_checksum": os.environ["SUM"]}))'
+# S4 as a Terraform data "external" program (operator machine): find the RKE cluster
+# by name or create it, then its registration token (reused when the cluster existed)
+# and the checksum of the Rancher CA bundle.  Query keys: name, version, network,
+# api_url, access_key, secret_key, registry, registry_username, registry_password.
+exec python3 -c '
+import base64, hashlib, json, ssl, sys, urllib.request
+
+q = json.load(sys.stdin)
+ctx = ssl.create_default_context()
+ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE  # self-signed Rancher certificates
+auth = "Basic " + base64.b64encode((q["access_key"] + ":" + q["secret_key"]).encode()).decode()
+
+
+def call(method, path, body=None):
+    req = urllib.request.Request(q["api_url"].rstrip("/") + path, method=method,
+                                 data=None if body is None else json.dumps(body).encode(),
+                                 headers={"Authorization": auth, "Accept": "application/json",
+                                          "Content-Type": "application/json"})
+    with urllib.request.urlopen(req, context=ctx, timeout=60) as resp:
+        return json.load(resp)
+
+
+found = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
+if found:
+    cluster_id = found[0]["id"]
+else:
+    rke = {"type": "rancherKubernetesEngineConfig", "kubernetesVersion": q["version"],
+           "ignoreDockerVersion": False, "sshAgentAuth": False,
+           "authentication": {"type": "authnConfig", "strategy": "x509"},
+           "network": {"type": "networkConfig", "plugin": q["network"]},
+           "services": {"type": "rkeConfigServices",
+                        "kubeApi": {"type": "kubeAPIService", "podSecurityPolicy": False}}}
+    if q.get("registry"):
+        rke["privateRegistries"] = [{"url": q["registry"], "user": q.get("registry_username", ""),
+                                     "password": q.get("registry_password", "")}]
+    cluster_id = call("POST", "/v3/cluster", {"type": "cluster", "name": q["name"],
+                                              "rancherKubernetesEngineConfig": rke}).get("id", "")
+if not cluster_id:
+    sys.exit("Unable to create cluster!")
+tokens = call("GET", "/v3/clusters/%s/clusterregistrationtokens" % cluster_id).get("data") if found else []
+token = (tokens[0].get("token") if tokens else "") or call(
+    "POST", "/v3/clusterregistrationtoken", {"type": "clusterRegistrationToken", "clusterId": cluster_id}).get("token")
+if not token:
+    sys.exit("Unable to create cluster registration token!")
+cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
+print(json.dumps({"cluster_id": cluster_id, "registration_token": token,
+                  "ca_checksum": hashlib.sha256((cacerts + "\n").encode()).hexdigest()}))
+'
 """
 
 INSTALL_RANCHER_AGENT = r"""#!/bin/bash
