@@ -209,3 +209,38 @@ def test_gate_released_when_apply_fails(env):
         info = HTTPClient(base_url=h[len("agent+"):]).request("GET", "/v1/info",
                                                              headers={"X-TK-Agent-Token": TOKEN}).json()
         assert info["pending_gates"] == 0
+
+
+def test_host_retry_recovers_flaky_node(env):
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    calls = {"n": 0}
+    a = NodeAgent(name="flaky", mode="sim", devices=list(range(8)), token=TOKEN, root=tempfile.mkdtemp(),
+                  topology_override=synthetic_topology(8))
+
+    def burn(dev, level):
+        calls["n"] += 1
+        return {"ok": calls["n"] > 8, "failures": ["hbm"] if calls["n"] <= 8 else []}  # first pass fails
+
+    a.burnin_override = burn
+    url = "agent+" + a.serve()
+    try:
+        cp = agent("cp")
+        events = []
+        ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="retry",
+                            k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", host_retries=2,
+                            host_retry_backoff="0.01", nodes=_nodes(cp, [url])))
+        new_cluster(ctx, backend)
+        tf = json.loads(backend.read_tfstate("mgr"))
+        assert tf["module_state"]["node_baremetal_retry_gpu-1"]["status"] == "ok"
+        assert calls["n"] == 16  # 8 GPUs failed once, then 8 passed
+        # without retries the same flake fails the apply
+        calls["n"] = 0
+        ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="noretry",
+                            k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico",
+                            nodes=_nodes(cp, [url])))
+        with pytest.raises(TKError):
+            new_cluster(ctx, backend)
+        del events
+    finally:
+        a.stop()

@@ -124,7 +124,8 @@ class DirectExecutor(Executor):
     def __init__(self, transport: Optional[Transport] = None, parallelism: int = 64,
                  rancher_factory: Optional[Callable[..., RancherClient]] = None, rancher_bootstrap: str = "operator",
                  node_timeout: float = 3600.0, cluster_wait: float = 1800.0, upload_tools: bool = True,
-                 node_cleanup: bool = False, on_event: Optional[Callable[[str, Dict[str, Any]], None]] = None):
+                 node_cleanup: bool = False, on_event: Optional[Callable[[str, Dict[str, Any]], None]] = None,
+                 host_retries: int = 0, retry_backoff: float = 2.0):
         self.transport = transport or TransportRouter()
         self.parallelism = max(1, parallelism)
         self.rancher_factory = rancher_factory or (lambda url, ak="", sk="": RancherClient(url, ak, sk))
@@ -134,6 +135,10 @@ class DirectExecutor(Executor):
         self.upload_tools = upload_tools
         self.node_cleanup = node_cleanup
         self.on_event = on_event
+        # a host module whose bootstrap fails is re-run this many times (plans are idempotent:
+        # find-or-create cluster, runtime installed only when absent, agent re-registration)
+        self.host_retries = max(0, host_retries)
+        self.retry_backoff = retry_backoff
         self.last_report: Optional[ApplyReport] = None
         self._mu = threading.Lock()
 
@@ -267,7 +272,14 @@ class DirectExecutor(Executor):
             if kind == "cluster":
                 return self._apply_cluster(cfg), None
             if kind == "host":
-                return self._apply_host(run.key, cfg, run.info.mi355x)
+                for attempt in range(self.host_retries + 1):
+                    try:
+                        return self._apply_host(run.key, cfg, run.info.mi355x)
+                    except ExecutorError as exc:
+                        if attempt == self.host_retries:
+                            raise
+                        self._event("module_retry", key=run.key, attempt=attempt + 1, error=str(exc))
+                        time.sleep(self.retry_backoff * (2 ** attempt))
             if kind == "addon":
                 return self._apply_addons(cfg), None
         raise ExecutorError(f"unsupported module kind {kind}")

@@ -8,6 +8,8 @@
 ``agent_token``             shared token for ``agent+http://`` hosts
 ``rancher_bootstrap``       ``operator`` (default) | ``remote``
 ``node_cleanup``            run the agent cleanup script on destroy (default false)
+``host_retries``            re-run a failed host bootstrap this many times (default 0)
+``host_retry_backoff``      first retry delay in seconds, doubling per attempt (default 2)
 ==========================  ================================================================
 
 ``auto`` picks Terraform when the binary is on ``PATH``; otherwise the
@@ -48,5 +50,7 @@ def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
         return DirectExecutor(transport=transport, parallelism=par,
                               rancher_bootstrap=s.get_string("rancher_bootstrap") or "operator",
                               node_cleanup=s.get_bool("node_cleanup"),
+                              host_retries=s.get_int("host_retries") if s.is_set("host_retries") else 0,
+                              retry_backoff=float(s.get_string("host_retry_backoff") or 2.0),
                               rancher_factory=ctx.extras.get("rancher_factory"))
     raise ValueError(f"unknown executor '{kind}' (terraform | direct | auto)")
