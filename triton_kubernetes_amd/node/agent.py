@@ -116,6 +116,10 @@ class NodeAgent:
             self.token = secrets.token_urlsafe(24)
         self.lock = threading.Lock()
         self._gate_mu = threading.Lock()
+        # long-lived workers for topology prefetch and per-GPU burn-in: no thread is created
+        # on the bring-up path (thread creation contends with RCCL/HIP work in the process)
+        self._pool = cf.ThreadPoolExecutor(max_workers=len(self.devices) + 2,
+                                           thread_name_prefix=f"tk-agent-{self.name}")
         self._gates: Dict[bytes, Any] = {}
         self.last_labels: Dict[str, str] = {}
         self.history: List[Dict[str, Any]] = []
@@ -138,12 +142,10 @@ class NodeAgent:
         ctx: Dict[str, Any] = {"labels": {}, "capacity": {}}
         t_plan = time.perf_counter()
         error = None
-        prefetch = None
         if any(s.action == "gpu_labels" for s in plan.steps):
             # topology discovery (host-side sysfs reads) overlaps the preflight
             # and burn-in kernels instead of running after them
-            prefetch = cf.ThreadPoolExecutor(max_workers=1, thread_name_prefix="topo")
-            ctx["topology_future"] = prefetch.submit(self._topology)
+            ctx["topology_future"] = self._pool.submit(self._topology)
         with self.lock:
             for step in plan.steps:
                 t0 = time.perf_counter()
@@ -155,8 +157,6 @@ class NodeAgent:
                     results.append(StepResult(step.name, False, (time.perf_counter() - t0) * 1e3, str(exc)))
                     error = f"{step.name}: {exc}"
                     break
-        if prefetch is not None:
-            prefetch.shutdown(wait=False)
         doc = {"hostname": plan.hostname, "ok": error is None, "error": error,
                "ms": (time.perf_counter() - t_plan) * 1e3,
                "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"]}
@@ -228,8 +228,7 @@ class NodeAgent:
             # every GPU of the node burns in concurrently (one host thread each;
             # the probes pin their device per thread)
             if len(self.devices) > 1:
-                with cf.ThreadPoolExecutor(max_workers=len(self.devices)) as pool:
-                    results = dict(zip(self.devices, pool.map(lambda d: self._burnin(d, level), self.devices)))
+                results = dict(zip(self.devices, self._pool.map(lambda d: self._burnin(d, level), self.devices)))
             else:
                 results = {d: self._burnin(d, level) for d in self.devices}
             out = {}
@@ -485,6 +484,7 @@ class NodeAgent:
         return f"http://{h}:{p}"
 
     def stop(self) -> None:
+        self._pool.shutdown(wait=True)
         if self._server is not None:
             self._server.shutdown()
             self._server.server_close()

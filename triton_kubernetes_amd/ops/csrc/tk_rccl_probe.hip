@@ -24,6 +24,7 @@
 
 #include <atomic>
 #include <condition_variable>
+#include <functional>
 #include <chrono>
 #include <cstdio>
 #include <cstdlib>
@@ -146,10 +147,58 @@ extern "C" double tkr_last_phase_ms(int phase) { return (phase >= 0 && phase < 4
 // Communicator teardown (ncclCommDestroy joins RCCL's proxy threads and frees
 // its device resources; ~0.5 s measured on MI355X, longer than init) is not
 // part of the readiness answer.  With async teardown on, it runs on a
-// background thread after the verified result is returned; tkr_drain() joins
-// every pending teardown and must run before process exit.
-static std::mutex g_td_mu;
-static std::vector<std::thread> g_td;
+// background thread after the verified result is returned; tkr_drain() waits for
+// every pending teardown and should run before process exit.
+// One background worker owns every asynchronous teardown, in submission order: destroys
+// never run concurrently with each other (a thread per communicator piled up ~10 concurrent
+// ncclCommDestroy calls behind back-to-back gates and stalled the next bring-up), and the
+// worker is started once, not per gate.
+struct TeardownQueue {
+  std::mutex mu;
+  std::condition_variable cv, idle_cv;
+  std::vector<std::function<void()>> q;
+  bool busy = false, stop = false;
+  std::thread worker;
+
+  void submit(std::function<void()> fn) {
+    std::unique_lock<std::mutex> lk(mu);
+    q.push_back(std::move(fn));
+    if (!worker.joinable()) worker = std::thread([this] { run(); });
+    cv.notify_one();
+  }
+  void run() {
+    std::unique_lock<std::mutex> lk(mu);
+    for (;;) {
+      cv.wait(lk, [this] { return stop || !q.empty(); });
+      if (q.empty()) return;  // stop requested and nothing left
+      auto fn = std::move(q.front());
+      q.erase(q.begin());
+      busy = true;
+      lk.unlock();
+      fn();
+      lk.lock();
+      busy = false;
+      if (q.empty()) idle_cv.notify_all();
+    }
+  }
+  // Waits until every submitted teardown has run; returns how many were waited for.
+  int drain() {
+    std::unique_lock<std::mutex> lk(mu);
+    const int n = (int)q.size() + (busy ? 1 : 0);
+    idle_cv.wait(lk, [this] { return q.empty() && !busy; });
+    return n;
+  }
+  ~TeardownQueue() {  // process exit: finish queued work, then join the worker
+    {
+      std::lock_guard<std::mutex> lk(mu);
+      stop = true;
+    }
+    cv.notify_all();
+    if (worker.joinable()) worker.join();
+  }
+};
+static TeardownQueue g_teardowns;
+
 // Per calling thread: a gate served on one agent thread never changes the
 // teardown mode of probes running on other threads.
 static thread_local int g_async_teardown = 0;
@@ -162,8 +211,7 @@ static void teardown(ncclComm_t comm, RankBufs b, int device) {
     ncclCommDestroy(comm);
   };
   if (g_async_teardown) {
-    std::lock_guard<std::mutex> lk(g_td_mu);
-    g_td.emplace_back(work);
+    g_teardowns.submit(work);
     g_phase_ms[3] = 0.0;
   } else {
     const auto t = std::chrono::steady_clock::now();
@@ -172,21 +220,7 @@ static void teardown(ncclComm_t comm, RankBufs b, int device) {
   }
 }
 
-extern "C" int tkr_drain() {
-  std::vector<std::thread> pending;
-  {
-    std::lock_guard<std::mutex> lk(g_td_mu);
-    pending.swap(g_td);
-  }
-  for (auto& t : pending) t.join();
-  return (int)pending.size();
-}
-
-// Safety net: a joinable std::thread destroyed at exit calls std::terminate.
-// Declared after g_td, so it is destroyed (and joins) first.
-static struct TeardownDrainer {
-  ~TeardownDrainer() { tkr_drain(); }
-} g_drainer;
+extern "C" int tkr_drain() { return g_teardowns.drain(); }
 
 static inline size_t elem_size(int dtype) { return dtype == 1 ? 2 : 4; }
 static inline ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclBfloat16 : ncclFloat32; }
