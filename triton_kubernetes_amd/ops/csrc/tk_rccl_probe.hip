@@ -204,11 +204,18 @@ static TeardownQueue g_teardowns;
 static thread_local int g_async_teardown = 0;
 extern "C" void tkr_set_async_teardown(int on) { g_async_teardown = on; }
 
+// ncclCommAbort instead of ncclCommDestroy for the teardown (no in-flight work remains
+// after a verified sweep, so nothing is lost; it skips the graceful finalize).
+static std::atomic<int> g_teardown_abort{0};
+extern "C" void tkr_set_teardown_abort(int on) { g_teardown_abort = on; }
+
 static void teardown(ncclComm_t comm, RankBufs b, int device) {
-  auto work = [comm, b, device]() mutable {
+  const bool abort = g_teardown_abort.load() != 0;
+  auto work = [comm, b, device, abort]() mutable {
     (void)hipSetDevice(device);
     free_bufs(b);
-    ncclCommDestroy(comm);
+    if (abort) ncclCommAbort(comm);
+    else ncclCommDestroy(comm);
   };
   if (g_async_teardown) {
     g_teardowns.submit(work);

@@ -29,6 +29,7 @@ def _lib():
     lib.tkr_last_phase_ms.restype = ctypes.c_double
     lib.tkr_last_phase_ms.argtypes = [ctypes.c_int]
     lib.tkr_set_async_teardown.argtypes = [ctypes.c_int]
+    lib.tkr_set_teardown_abort.argtypes = [ctypes.c_int]
     dp = ctypes.POINTER(ctypes.c_double)
     lib.tkr_sweep_rank.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int, ctypes.c_int,
