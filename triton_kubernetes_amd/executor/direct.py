@@ -216,8 +216,10 @@ class DirectExecutor(Executor):
         report = ApplyReport(runs)
         pending = set(runs)
         futures: Dict[cf.Future, str] = {}
-        with span("direct.apply", modules=len(runs)), \
-                cf.ThreadPoolExecutor(max_workers=self.parallelism, thread_name_prefix="tk-direct") as pool:
+        from ..parallel.fanout import shared_pool
+
+        pool = shared_pool(f"tk-direct-{self.parallelism}", self.parallelism)
+        with span("direct.apply", modules=len(runs)):
             while pending or futures:
                 for key in sorted(pending):
                     run = runs[key]

@@ -99,8 +99,25 @@ def fan_out(items: Sequence[T], fn: Callable[[T], R], key: Callable[[T], str] = 
     return report
 
 
+_POOLS: Dict[str, cf.ThreadPoolExecutor] = {}
+_POOLS_MU = threading.Lock()
+
+
+def shared_pool(name: str, width: int) -> cf.ThreadPoolExecutor:
+    """A process-wide, never shut down worker pool (one per ``name``; ``width`` of the
+    first request wins).  Bring-up paths reuse its threads — and the keep-alive HTTP
+    connections those threads hold — instead of creating threads per operation, which
+    contends with HIP/RCCL work in GPU processes.  A task must never wait on work it
+    submitted to the same pool."""
+    with _POOLS_MU:
+        pool = _POOLS.get(name)
+        if pool is None:
+            pool = _POOLS[name] = cf.ThreadPoolExecutor(max_workers=max(1, width), thread_name_prefix=name)
+        return pool
+
+
 def describe_failures(report: FanOutReport) -> str:
     return "; ".join(f"{r.key}: {r.error}" for r in report.failures)
 
 
-__all__: List[Any] = ["fan_out", "FanOutReport", "TaskResult", "describe_failures", "DEFAULT_WIDTH"]
+__all__: List[Any] = ["fan_out", "FanOutReport", "TaskResult", "describe_failures", "DEFAULT_WIDTH", "shared_pool"]

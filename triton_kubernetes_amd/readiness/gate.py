@@ -22,6 +22,7 @@ import threading
 from dataclasses import dataclass
 from typing import Any, Dict, List, Optional, Sequence
 
+from ..parallel.fanout import shared_pool
 from ..parallel.transport import HostRef
 from ..utils.trace import span
 
@@ -60,7 +61,7 @@ class ClusterGate:
         self.prepared = False
         self.prepare_error: Optional[str] = None
         self.done = False
-        self._thread: Optional[threading.Thread] = None
+        self._thread: Optional[cf.Future] = None
         self._mu = threading.Lock()
 
     # --- construction from the state document ---------------------------------------------------------
@@ -93,8 +94,7 @@ class ClusterGate:
 
         if len(self.members) == 1:
             return [one(self.members[0])]
-        with cf.ThreadPoolExecutor(max_workers=len(self.members)) as pool:
-            return list(pool.map(one, self.members))
+        return list(shared_pool("tk-gate", 64).map(one, self.members))
 
     def _prepare(self) -> None:
         try:
@@ -112,13 +112,13 @@ class ClusterGate:
                     self.uid = uid  # some agents may hold a pending init under it: abort() releases them
 
     def prepare_async(self) -> "ClusterGate":
-        self._thread = threading.Thread(target=self._prepare, name="tk-gate-prepare", daemon=True)
-        self._thread.start()
+        # its own pool: _prepare itself fans out on "tk-gate"
+        self._thread = shared_pool("tk-gate-prepare", 4).submit(self._prepare)
         return self
 
     def _join(self) -> None:
         if self._thread is not None:
-            self._thread.join()
+            self._thread.result()
             self._thread = None
 
     # --- the gate ---------------------------------------------------------------------------------------
