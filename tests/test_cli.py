@@ -81,5 +81,6 @@ def test_entry_points_subprocess(tk_home):
 def test_help_lists_commands():
     code, out = _run([])
     assert code == 0
-    for word in ("create", "destroy", "get", "version", "wait", "gpu", "agent", "image"):
+    for word in ("create", "destroy", "get", "version", "wait", "gpu", "agent", "image", "backup", "restore",
+                 "userdata"):
         assert word in out

@@ -41,10 +41,11 @@ VALID = {
     "wait": ["cluster"],
     "backup": ["cluster"],
     "restore": ["cluster"],
+    "userdata": ["node"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
 _ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
-             "restore": "restore"}
+             "restore": "restore", "userdata": "userdata"}
 
 
 class ArgError(Exception):
@@ -85,7 +86,8 @@ def build_parser() -> argparse.ArgumentParser:
                        ("get", "Display resource information"),
                        ("wait", "Wait until a cluster is kubectl-ready (and GPU-ready) and report timings"),
                        ("backup", "Back up a cluster's namespaces to the state backend (local/manta) or S3"),
-                       ("restore", "Restore a cluster's namespaces from a backup")):
+                       ("restore", "Restore a cluster's namespaces from a backup"),
+                       ("userdata", "Print cloud-init user-data that bootstraps a node (PXE/MAAS delivery)")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
@@ -174,6 +176,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         from ..workflows.backup import restore_cluster
 
         restore_cluster(ctx, backend)
+    elif command == "userdata":
+        from ..workflows.userdata import node_userdata
+
+        node_userdata(ctx, backend)
     elif command == "wait":
         from ..readiness.waiter import wait_after_create
         from ..workflows.select import select_cluster, select_manager

@@ -103,6 +103,32 @@ class BootstrapPlan:
         return "\n".join(out) + "\n"
 
 
+def render_cloud_init(plan: "BootstrapPlan", rccl_env: Optional[Dict[str, str]] = None) -> str:
+    """``#cloud-config`` user-data that runs the plan at first boot.
+
+    For hosts provisioned by PXE/MAAS/cloud images instead of SSH: the RCCL
+    environment and the bootstrap script are written by cloud-init's
+    ``write_files`` (so the RCCL env exists before anything GPU-related starts),
+    then ``runcmd`` executes the script with its step markers logged to
+    ``/var/log/triton-kubernetes-bootstrap.log``."""
+    import yaml
+
+    files = []
+    if rccl_env is not None:
+        files.append({"path": RCCL_ENV_FILE, "permissions": "0644", "owner": "root:root",
+                      "content": render_env_file(rccl_env)})
+    files.append({"path": "/opt/triton-kubernetes/bootstrap.sh", "permissions": "0755", "owner": "root:root",
+                  "content": plan.render_shell()})
+    doc = {
+        "hostname": plan.hostname,
+        "preserve_hostname": False,
+        "write_files": files,
+        "runcmd": [["bash", "-c", "/opt/triton-kubernetes/bootstrap.sh "
+                                  ">> /var/log/triton-kubernetes-bootstrap.log 2>&1"]],
+    }
+    return "#cloud-config\n" + yaml.safe_dump(doc, sort_keys=False, default_flow_style=False, width=1 << 30)
+
+
 def _q(v: Any) -> str:
     return shlex.quote(str(v))
 
