@@ -395,6 +395,9 @@ class NodeAgent:
 
         probe._lib()
         rccl._lib()
+        quiet = float(os.environ.get("TK_TEARDOWN_QUIET_MS", "0") or 0)
+        if quiet > 0:
+            rccl.set_teardown_quiet_ms(quiet)
         try:
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later

@@ -153,12 +153,24 @@ extern "C" double tkr_last_phase_ms(int phase) { return (phase >= 0 && phase < 4
 // never run concurrently with each other (a thread per communicator piled up ~10 concurrent
 // ncclCommDestroy calls behind back-to-back gates and stalled the next bring-up), and the
 // worker is started once, not per gate.
+//
+// Teardowns can also wait for a quiet period (tkr_set_teardown_quiet_ms): a destroy
+// frees pinned host and device memory, and doing that while another bring-up allocates
+// stalled that bring-up (≈120 ms once per run, measured); with a quiet period the queue
+// runs only after `quiet_ms` without gate activity (begin / sweep) in the process.
 struct TeardownQueue {
   std::mutex mu;
   std::condition_variable cv, idle_cv;
   std::vector<std::function<void()>> q;
-  bool busy = false, stop = false;
+  bool busy = false, stop = false, flush = false;
   std::thread worker;
+  double quiet_ms = 0.0;
+  std::chrono::steady_clock::time_point last_activity = std::chrono::steady_clock::now();
+
+  void touch() {
+    std::lock_guard<std::mutex> lk(mu);
+    last_activity = std::chrono::steady_clock::now();
+  }
 
   void submit(std::function<void()> fn) {
     std::unique_lock<std::mutex> lk(mu);
@@ -171,6 +183,13 @@ struct TeardownQueue {
     for (;;) {
       cv.wait(lk, [this] { return stop || !q.empty(); });
       if (q.empty()) return;  // stop requested and nothing left
+      // hold off while bring-ups are active (unless draining / exiting)
+      while (!stop && !flush && quiet_ms > 0) {
+        const double since = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() -
+                                                                        last_activity).count();
+        if (since >= quiet_ms) break;
+        cv.wait_for(lk, std::chrono::duration<double, std::milli>(quiet_ms - since));
+      }
       auto fn = std::move(q.front());
       q.erase(q.begin());
       busy = true;
@@ -185,7 +204,10 @@ struct TeardownQueue {
   int drain() {
     std::unique_lock<std::mutex> lk(mu);
     const int n = (int)q.size() + (busy ? 1 : 0);
+    flush = true;
+    cv.notify_all();
     idle_cv.wait(lk, [this] { return q.empty() && !busy; });
+    flush = false;
     return n;
   }
   ~TeardownQueue() {  // process exit: finish queued work, then join the worker
@@ -228,6 +250,14 @@ static void teardown(ncclComm_t comm, RankBufs b, int device) {
 }
 
 extern "C" int tkr_drain() { return g_teardowns.drain(); }
+extern "C" void tkr_set_teardown_quiet_ms(double ms) {
+  std::lock_guard<std::mutex> lk(g_teardowns.mu);
+  g_teardowns.quiet_ms = ms > 0 ? ms : 0.0;
+}
+extern "C" int tkr_teardowns_pending() {
+  std::lock_guard<std::mutex> lk(g_teardowns.mu);
+  return (int)g_teardowns.q.size() + (g_teardowns.busy ? 1 : 0);
+}
 
 static inline size_t elem_size(int dtype) { return dtype == 1 ? 2 : 4; }
 static inline ncclDataType_t nccl_type(int dtype) { return dtype == 1 ? ncclBfloat16 : ncclFloat32; }
@@ -392,6 +422,7 @@ extern "C" int tkr_gate_begin_ex(const unsigned char* uid128, int world, int ran
   g->world = world;
   g->prealloc_bytes = prealloc_bytes;
   g->t_begin = std::chrono::steady_clock::now();
+  g_teardowns.touch();
   if (blocking) {
     init_body(g, id);
     if (g->init_state < 0) {
@@ -528,6 +559,7 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
   }
   phase_ms[2] = ms_since(t_phase);
   t_phase = std::chrono::steady_clock::now();
+  g_teardowns.touch();
   for (int d = 0; d < ndev; ++d) {
     teardown(g->comms[d], bufs[d], g->devices[d]);
     g->comms[d] = nullptr;

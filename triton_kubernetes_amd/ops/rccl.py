@@ -30,6 +30,7 @@ def _lib():
     lib.tkr_last_phase_ms.argtypes = [ctypes.c_int]
     lib.tkr_set_async_teardown.argtypes = [ctypes.c_int]
     lib.tkr_set_teardown_abort.argtypes = [ctypes.c_int]
+    lib.tkr_set_teardown_quiet_ms.argtypes = [ctypes.c_double]
     dp = ctypes.POINTER(ctypes.c_double)
     lib.tkr_sweep_rank.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_char_p, ctypes.c_int,
                                    ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int, ctypes.c_int,
@@ -193,6 +194,15 @@ def exit_now(code: int = 0) -> None:
 def set_async_teardown(on: bool) -> None:
     """Run communicator teardown off the caller's critical path (see ``teardown`` in the HIP source)."""
     _lib().tkr_set_async_teardown(1 if on else 0)
+
+
+def set_teardown_quiet_ms(ms: float) -> None:
+    """Run queued communicator teardowns only after ``ms`` without gate activity."""
+    _lib().tkr_set_teardown_quiet_ms(float(ms))
+
+
+def teardowns_pending() -> int:
+    return int(_lib().tkr_teardowns_pending())
 
 
 def drain() -> int:
