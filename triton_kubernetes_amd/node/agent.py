@@ -395,6 +395,8 @@ class NodeAgent:
 
         probe._lib()
         rccl._lib()
+        if os.environ.get("TK_PROBE_SCRATCH_CACHE") == "1":
+            probe.set_scratch_cache(True)
         quiet = float(os.environ.get("TK_TEARDOWN_QUIET_MS", "0") or 0)
         if quiet > 0:
             rccl.set_teardown_quiet_ms(quiet)

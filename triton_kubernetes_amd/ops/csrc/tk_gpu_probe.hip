@@ -28,7 +28,10 @@
 
 #include <hip/hip_runtime.h>
 
+#include <array>
 #include <cstdint>
+#include <map>
+#include <mutex>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -156,6 +159,86 @@ static int stream_grid(int dev, int blocks_per_cu) {
   return p.multiProcessorCount * blocks_per_cu;
 }
 
+// ---------------------------------------------------------------------------
+// Device scratch cache (opt-in: tkp_set_scratch_cache).  A long-lived node agent
+// runs the burn-in once per bring-up; with the cache on, the multi-GiB stream and
+// memtest buffers stay allocated between runs instead of a hipMalloc/hipFree of
+// GiBs each time.  tkp_release_scratch() returns them (the agent calls it when
+// it has been idle, and at stop).
+// ---------------------------------------------------------------------------
+namespace {
+constexpr int kScratchSlots = 3;  // 0/1: stream a/b, 2: memtest
+struct ScratchSlot {
+  void* p = nullptr;
+  size_t bytes = 0;
+  bool in_use = false;
+};
+std::mutex g_scr_mu;
+std::map<int, std::array<ScratchSlot, kScratchSlots>> g_scr;
+int g_scr_on = 0;
+}  // namespace
+
+static hipError_t scratch_get(int dev, int slot, size_t bytes, void** out) {
+  {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    if (g_scr_on) {
+      ScratchSlot& s = g_scr[dev][slot];
+      if (!s.in_use) {
+        s.in_use = true;
+        if (s.p && s.bytes >= bytes) {
+          *out = s.p;
+          return hipSuccess;
+        }
+        if (s.p) (void)hipFree(s.p);
+        s.p = nullptr;
+        s.bytes = 0;
+        hipError_t e = hipMalloc(&s.p, bytes);
+        if (e != hipSuccess) { s.in_use = false; s.p = nullptr; return e; }
+        s.bytes = bytes;
+        *out = s.p;
+        return hipSuccess;
+      }
+    }
+  }
+  return hipMalloc(out, bytes);
+}
+
+static void scratch_put(int dev, int slot, void* p) {
+  if (!p) return;
+  {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    auto it = g_scr.find(dev);
+    if (it != g_scr.end() && it->second[slot].p == p) {
+      it->second[slot].in_use = false;
+      return;
+    }
+  }
+  (void)hipFree(p);
+}
+
+extern "C" void tkp_set_scratch_cache(int on) {
+  std::lock_guard<std::mutex> lk(g_scr_mu);
+  g_scr_on = on;
+}
+
+// Frees every cached buffer not in use; returns the bytes released.
+extern "C" long long tkp_release_scratch() {
+  std::lock_guard<std::mutex> lk(g_scr_mu);
+  long long freed = 0;
+  for (auto& kv : g_scr) {
+    for (auto& s : kv.second) {
+      if (s.p && !s.in_use) {
+        (void)hipSetDevice(kv.first);
+        (void)hipFree(s.p);
+        freed += (long long)s.bytes;
+        s.p = nullptr;
+        s.bytes = 0;
+      }
+    }
+  }
+  return freed;
+}
+
 // out[0] = read GB/s, out[1] = write GB/s, out[2] = copy GB/s (bytes read + written).
 // Best of `iters` timed launches after one warm-up of each kernel.
 extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_per_cu, double* out) {
@@ -166,9 +249,9 @@ extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_pe
   if (n4 == 0) { snprintf(g_err, sizeof(g_err), "bytes too small"); return -1; }
   f32x4 *a = nullptr, *b = nullptr;
   float* sink = nullptr;
-  CHECK(hipMalloc(&a, n4 * sizeof(f32x4)));
-  hipError_t e = hipMalloc(&b, n4 * sizeof(f32x4));
-  if (e != hipSuccess) { (void)hipFree(a); return set_err("hipMalloc(b)", e); }
+  CHECK(scratch_get(dev, 0, n4 * sizeof(f32x4), reinterpret_cast<void**>(&a)));
+  hipError_t e = scratch_get(dev, 1, n4 * sizeof(f32x4), reinterpret_cast<void**>(&b));
+  if (e != hipSuccess) { scratch_put(dev, 0, a); return set_err("hipMalloc(b)", e); }
   CHECK(hipMalloc(&sink, STREAM_THREADS * sizeof(float)));
   hipStream_t s;
   CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -204,8 +287,8 @@ extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_pe
   hipEventDestroy(t0);
   hipEventDestroy(t1);
   hipStreamDestroy(s);
-  hipFree(a);
-  hipFree(b);
+  scratch_put(dev, 0, a);
+  scratch_put(dev, 1, b);
   hipFree(sink);
   return 0;
 }
@@ -376,7 +459,7 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   const size_t n = bytes / sizeof(uint4);
   uint4* p = nullptr;
   unsigned long long* err = nullptr;
-  CHECK(hipMalloc(&p, n * sizeof(uint4)));
+  CHECK(scratch_get(dev, 2, n * sizeof(uint4), reinterpret_cast<void**>(&p)));
   CHECK(hipMalloc(&err, sizeof(unsigned long long)));
   CHECK(hipMemset(err, 0, sizeof(unsigned long long)));
   hipEvent_t t0, t1;
@@ -400,7 +483,7 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   out[1] = (double)n * sizeof(uint4) / (ms * 1e-3) / 1e9;
   hipEventDestroy(t0);
   hipEventDestroy(t1);
-  hipFree(p);
+  scratch_put(dev, 2, p);
   hipFree(err);
   return 0;
 }

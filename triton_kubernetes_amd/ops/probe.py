@@ -58,6 +58,8 @@ def _lib():
                                           ctypes.POINTER(ctypes.c_double)]
     lib.tkp_p2p_bandwidth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_set_scratch_cache.argtypes = [ctypes.c_int]
+    lib.tkp_release_scratch.restype = ctypes.c_longlong
     return lib
 
 
@@ -194,3 +196,13 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
     if res.memtest["errors"]:
         res.failures.append(f"memtest: {res.memtest['errors']} mismatching words")
     return res
+
+
+def set_scratch_cache(on: bool) -> None:
+    """Keep the burn-in's multi-GiB buffers allocated between runs (long-lived agents)."""
+    _lib().tkp_set_scratch_cache(1 if on else 0)
+
+
+def release_scratch() -> int:
+    """Free cached burn-in buffers; returns the bytes released."""
+    return int(_lib().tkp_release_scratch())
