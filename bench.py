@@ -126,6 +126,21 @@ def main() -> int:
 
     gc.collect()
     gc.freeze()
+    gc_events = []  # (generation, ms) of every collection during the run, for the report
+    gc_t0 = {}
+
+    def _gc_cb(phase, info):
+        if phase == "start":
+            gc_t0["t"] = time.perf_counter()
+        elif "t" in gc_t0:
+            gc_events.append((info.get("generation"), round((time.perf_counter() - gc_t0.pop("t")) * 1e3, 3)))
+
+    gc.callbacks.append(_gc_cb)
+    gc_mode = os.environ.get("TK_BENCH_GC", "")
+    if gc_mode == "off":
+        gc.disable()
+    elif gc_mode.startswith("threshold:"):
+        gc.set_threshold(*[int(x) for x in gc_mode.split(":", 1)[1].split(",")])
 
     def one_step(i: int) -> dict:
         name = f"bench-{i}"
@@ -215,7 +230,8 @@ def main() -> int:
         print(json.dumps(line), flush=True)
         if args.report:
             with open(args.report, "w", encoding="utf-8") as fh:
-                json.dump({"line": line, "steps": results, "trace": TRACER.report()}, fh, indent=1, default=str)
+                json.dump({"line": line, "steps": results, "trace": TRACER.report(), "gc": gc_events},
+                          fh, indent=1, default=str)
     agent.stop()
     if cp_agent is not None:
         cp_agent.stop()
