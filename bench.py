@@ -60,11 +60,12 @@ def parse_args():
 
 def main() -> int:
     args = parse_args()
+    import faulthandler
+
     watchdog = float(os.environ.get("TK_BENCH_WATCHDOG", "0") or 0)
     if watchdog > 0:  # debugging aid: dump every thread's Python stack periodically
-        import faulthandler
-
         faulthandler.dump_traceback_later(watchdog, repeat=True, file=sys.stderr)
+    step_watchdog = float(os.environ.get("TK_BENCH_STEP_WATCHDOG", "0") or 0)
     import torch
     import torch.distributed as dist
 
@@ -87,6 +88,7 @@ def main() -> int:
     from triton_kubernetes_amd.config import Context, Settings
     from triton_kubernetes_amd.node.agent import NodeAgent
     from triton_kubernetes_amd.parallel.transport import AgentTransport
+    from triton_kubernetes_amd.utils import procstat
     from triton_kubernetes_amd.utils.trace import TRACER
 
     token = os.environ.get("TK_BENCH_TOKEN", "bench-token-0123456789")
@@ -159,9 +161,15 @@ def main() -> int:
                    ])
         ctx = Context(settings=Settings(cfg, env={}), out=open(os.devnull, "w"))
         ctx.extras["agent_transport"] = AgentTransport(token=token)
+        ps0 = procstat.snapshot()
         t0 = time.time()
+        if step_watchdog > 0:  # diagnosis: every thread's Python stack if a step overruns
+            faulthandler.dump_traceback_later(step_watchdog, file=sys.stderr)
         wf.new_cluster(ctx, backend)
-        return {"step": i, "seconds": time.time() - t0}
+        if step_watchdog > 0:
+            faulthandler.cancel_dump_traceback_later()
+        dt = time.time() - t0
+        return {"step": i, "seconds": dt, "proc": procstat.delta(ps0, procstat.snapshot())}
 
     def sync():
         if not args.sim_gpu:
@@ -230,7 +238,9 @@ def main() -> int:
         print(json.dumps(line), flush=True)
         if args.report:
             with open(args.report, "w", encoding="utf-8") as fh:
-                json.dump({"line": line, "steps": results, "trace": TRACER.report(), "gc": gc_events},
+                json.dump({"line": line, "steps": results, "trace": TRACER.report(), "gc": gc_events,
+                           "cpu_quota": procstat.cpu_quota(), "cpu_affinity": len(os.sched_getaffinity(0)),
+                           "cgroup_cpu_dir": procstat.cgroup_cpu_dir()},
                           fh, indent=1, default=str)
     agent.stop()
     if cp_agent is not None:

@@ -56,6 +56,21 @@ def test_burnin_quick(probe):
     assert res.ok, res.failures
 
 
+def test_burnin_arena_resident_across_runs(probe):
+    probe.release_scratch()  # the arena is process-wide: start from an empty one
+    held = probe.prealloc_scratch(0, "quick")
+    assert held == 3 << 30
+    try:
+        for _ in range(2):  # both runs stream/memtest through the resident buffers
+            res = probe.run_burnin(0, "quick")
+            assert res.ok, res.failures
+    finally:
+        freed = probe.release_scratch()
+        probe.set_scratch_cache(False)
+    assert freed == held
+    assert probe.release_scratch() == 0
+
+
 def test_rccl_single_rank_and_local():
     from triton_kubernetes_amd.ops import rccl
 

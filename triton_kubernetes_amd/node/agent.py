@@ -50,6 +50,7 @@ from typing import Any, Callable, Dict, List, Optional
 from ..cloud.http import HTTPClient
 from ..parallel.rccl_env import render_env_file
 from ..rancher.fake import tunnel_params
+from ..utils import procstat
 from ..utils.trace import span
 from .labels import labels_from_topology
 from .plan import BootstrapPlan, Step
@@ -141,6 +142,7 @@ class NodeAgent:
         results: List[StepResult] = []
         ctx: Dict[str, Any] = {"labels": {}, "capacity": {}}
         t_plan = time.perf_counter()
+        self._touch()
         error = None
         if any(s.action == "gpu_labels" for s in plan.steps):
             # topology discovery (host-side sysfs reads) overlaps the preflight
@@ -161,6 +163,7 @@ class NodeAgent:
                "ms": (time.perf_counter() - t_plan) * 1e3,
                "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"]}
         self.history.append(doc)
+        self._touch()
         return doc
 
     @staticmethod
@@ -389,14 +392,23 @@ class NodeAgent:
         deadlock against the HIP runtime (dlopen holds the loader lock; the init thread holds
         runtime locks and needs the loader lock) — observed under rocprofv3.  Loading them here,
         before any request is served, keeps dlopen off the bring-up path."""
+        # one fd-table resize now instead of RCU-synchronized resizes on the bring-up path
+        slots = int(os.environ.get("TK_FD_TABLE", "16384") or 0)
+        if slots > 0:
+            procstat.presize_fd_table(slots)
         if self.topology_override is not None or not self.devices:
             return
         from ..ops import probe, rccl, topo
 
         probe._lib()
         rccl._lib()
-        if os.environ.get("TK_PROBE_SCRATCH_CACHE") == "1":
-            probe.set_scratch_cache(True)
+        # burn-in arena: resident for the agent's lifetime, released after an idle period
+        if os.environ.get("TK_PROBE_SCRATCH_CACHE", "1") != "0":
+            level = os.environ.get("TK_PROBE_SCRATCH_LEVEL", "quick")
+            list(self._pool.map(lambda d: probe.prealloc_scratch(d, level), self.devices))
+            idle_s = float(os.environ.get("TK_PROBE_SCRATCH_IDLE_S", "300") or 0)
+            if idle_s > 0:
+                self._start_janitor(idle_s)
         quiet = float(os.environ.get("TK_TEARDOWN_QUIET_MS", "0") or 0)
         if quiet > 0:
             rccl.set_teardown_quiet_ms(quiet)
@@ -404,6 +416,44 @@ class NodeAgent:
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later
             pass
+
+    def _start_janitor(self, idle_s: float) -> None:
+        """One long-lived thread frees the burn-in arena once no plan has run for ``idle_s``
+        (the next burn-in re-allocates it)."""
+        if getattr(self, "_janitor", None) is not None:
+            return
+        self._idle_cv = threading.Condition()
+        self._last_active = time.monotonic()
+        self._stopping = False
+
+        def loop():
+            from ..ops import probe
+
+            held = True
+            with self._idle_cv:
+                while not self._stopping:
+                    if not held:
+                        self._idle_cv.wait()  # until a plan runs (its burn-in re-allocates) or stop
+                        held = True
+                        continue
+                    left = self._last_active + idle_s - time.monotonic()
+                    if left <= 0:
+                        probe.release_scratch()
+                        held = False
+                    else:
+                        self._idle_cv.wait(timeout=left)
+            probe.release_scratch()
+            probe.set_scratch_cache(False)
+
+        self._janitor = threading.Thread(target=loop, name=f"tk-agent-{self.name}-janitor", daemon=True)
+        self._janitor.start()
+
+    def _touch(self) -> None:
+        cv = getattr(self, "_idle_cv", None)
+        if cv is not None:
+            with cv:
+                self._last_active = time.monotonic()
+                cv.notify()
 
     # --- HTTP server ----------------------------------------------------------------------------
     def serve(self, host: str = "127.0.0.1", port: int = 0) -> str:
@@ -489,6 +539,13 @@ class NodeAgent:
         return f"http://{h}:{p}"
 
     def stop(self) -> None:
+        cv = getattr(self, "_idle_cv", None)
+        if cv is not None:
+            with cv:
+                self._stopping = True
+                cv.notify()
+            self._janitor.join(timeout=30)
+            self._janitor = None
         self._pool.shutdown(wait=True)
         if self._server is not None:
             self._server.shutdown()

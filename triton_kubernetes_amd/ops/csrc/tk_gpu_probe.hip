@@ -29,6 +29,8 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <chrono>
+#include <cstdlib>
 #include <cstdint>
 #include <map>
 #include <mutex>
@@ -48,10 +50,42 @@ static int set_err(const char* what, hipError_t e) {
   return (int)e == 0 ? -1 : (int)e;
 }
 
-#define CHECK(call)                                   \
-  do {                                                \
-    hipError_t _e = (call);                           \
-    if (_e != hipSuccess) return set_err(#call, _e);  \
+// Slow-call trace (diagnosis of bring-up stalls): with TKP_TRACE_MS=<ms> set, every
+// runtime call made through CHECK that takes longer than that is reported on stderr.
+static double trace_threshold_ms() {
+  static const double t = [] {
+    const char* v = getenv("TKP_TRACE_MS");
+    return v && *v ? atof(v) : -1.0;
+  }();
+  return t;
+}
+
+static double now_ms() {
+  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+#define CHECK(call)                                                                        \
+  do {                                                                                     \
+    const double _thr = trace_threshold_ms();                                              \
+    const double _t0 = _thr >= 0 ? now_ms() : 0.0;                                         \
+    hipError_t _e = (call);                                                                \
+    if (_thr >= 0) {                                                                       \
+      const double _dt = now_ms() - _t0;                                                   \
+      if (_dt > _thr) fprintf(stderr, "[tkp] %.3f ms at %.3f: %s\n", _dt, _t0, #call);     \
+    }                                                                                      \
+    if (_e != hipSuccess) return set_err(#call, _e);                                       \
+  } while (0)
+
+// Same timing as CHECK for cleanup calls whose status is ignored.
+#define TRACED(call)                                                                       \
+  do {                                                                                     \
+    const double _thr = trace_threshold_ms();                                              \
+    const double _t0 = _thr >= 0 ? now_ms() : 0.0;                                         \
+    (void)(call);                                                                          \
+    if (_thr >= 0) {                                                                       \
+      const double _dt = now_ms() - _t0;                                                   \
+      if (_dt > _thr) fprintf(stderr, "[tkp] %.3f ms at %.3f: %s\n", _dt, _t0, #call);     \
+    }                                                                                      \
   } while (0)
 
 extern "C" const char* tkp_last_error() { return g_err; }
@@ -160,11 +194,12 @@ static int stream_grid(int dev, int blocks_per_cu) {
 }
 
 // ---------------------------------------------------------------------------
-// Device scratch cache (opt-in: tkp_set_scratch_cache).  A long-lived node agent
-// runs the burn-in once per bring-up; with the cache on, the multi-GiB stream and
-// memtest buffers stay allocated between runs instead of a hipMalloc/hipFree of
-// GiBs each time.  tkp_release_scratch() returns them (the agent calls it when
-// it has been idle, and at stop).
+// Device scratch arena (tkp_set_scratch_cache / tkp_prealloc_scratch).  A long-lived
+// node agent allocates it at startup; the burn-in of every bring-up then streams and
+// memtests through resident buffers instead of a hipMalloc/hipFree of GiBs each time
+// (measured on MI355X: such allocations intermittently stall 0.1-0.8 s when they
+// follow recent frees).  tkp_release_scratch() returns them (the agent calls it when
+// it has been idle, and at stop).  Without the cache every call allocates and frees.
 // ---------------------------------------------------------------------------
 namespace {
 constexpr int kScratchSlots = 3;  // 0/1: stream a/b, 2: memtest
@@ -179,28 +214,39 @@ int g_scr_on = 0;
 }  // namespace
 
 static hipError_t scratch_get(int dev, int slot, size_t bytes, void** out) {
+  void* stale = nullptr;
+  bool cached = false;
   {
     std::lock_guard<std::mutex> lk(g_scr_mu);
     if (g_scr_on) {
       ScratchSlot& s = g_scr[dev][slot];
       if (!s.in_use) {
-        s.in_use = true;
+        s.in_use = true;  // claimed: allocation below runs without the lock (other devices proceed)
+        cached = true;
         if (s.p && s.bytes >= bytes) {
           *out = s.p;
           return hipSuccess;
         }
-        if (s.p) (void)hipFree(s.p);
+        stale = s.p;
         s.p = nullptr;
         s.bytes = 0;
-        hipError_t e = hipMalloc(&s.p, bytes);
-        if (e != hipSuccess) { s.in_use = false; s.p = nullptr; return e; }
-        s.bytes = bytes;
-        *out = s.p;
-        return hipSuccess;
       }
     }
   }
-  return hipMalloc(out, bytes);
+  if (stale) TRACED(hipFree(stale));
+  hipError_t e;
+  TRACED(e = hipMalloc(out, bytes));
+  if (cached) {
+    std::lock_guard<std::mutex> lk(g_scr_mu);
+    ScratchSlot& s = g_scr[dev][slot];
+    if (e == hipSuccess) {
+      s.p = *out;
+      s.bytes = bytes;
+    } else {
+      s.in_use = false;
+    }
+  }
+  return e;
 }
 
 static void scratch_put(int dev, int slot, void* p) {
@@ -213,12 +259,24 @@ static void scratch_put(int dev, int slot, void* p) {
       return;
     }
   }
-  (void)hipFree(p);
+  TRACED(hipFree(p));
 }
 
 extern "C" void tkp_set_scratch_cache(int on) {
   std::lock_guard<std::mutex> lk(g_scr_mu);
   g_scr_on = on;
+}
+
+// Allocates (or keeps) the stream pair and memtest slots for these sizes on `dev`.
+extern "C" int tkp_prealloc_scratch(int dev, size_t stream_bytes, size_t memtest_bytes) {
+  CHECK(hipSetDevice(dev));
+  const size_t sizes[kScratchSlots] = {stream_bytes, stream_bytes, memtest_bytes};
+  for (int slot = 0; slot < kScratchSlots; ++slot) {
+    void* p = nullptr;
+    CHECK(scratch_get(dev, slot, sizes[slot], &p));
+    scratch_put(dev, slot, p);
+  }
+  return 0;
 }
 
 // Frees every cached buffer not in use; returns the bytes released.
@@ -229,7 +287,7 @@ extern "C" long long tkp_release_scratch() {
     for (auto& s : kv.second) {
       if (s.p && !s.in_use) {
         (void)hipSetDevice(kv.first);
-        (void)hipFree(s.p);
+        TRACED(hipFree(s.p));
         freed += (long long)s.bytes;
         s.p = nullptr;
         s.bytes = 0;
@@ -284,12 +342,12 @@ extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_pe
   }
   CHECK(hipGetLastError());
   for (int k = 0; k < 3; ++k) out[k] = best[k];
-  hipEventDestroy(t0);
-  hipEventDestroy(t1);
-  hipStreamDestroy(s);
+  TRACED(hipEventDestroy(t0));
+  TRACED(hipEventDestroy(t1));
+  TRACED(hipStreamDestroy(s));
   scratch_put(dev, 0, a);
   scratch_put(dev, 1, b);
-  hipFree(sink);
+  TRACED(hipFree(sink));
   return 0;
 }
 
@@ -417,10 +475,10 @@ extern "C" int tkp_mfma_peak(int dev, int dtype, int iters, int reps, int blocks
   CHECK(hipGetLastError());
   out[0] = best;
   out[1] = best_ms;
-  hipEventDestroy(t0);
-  hipEventDestroy(t1);
-  hipStreamDestroy(s);
-  hipFree(sink);
+  TRACED(hipEventDestroy(t0));
+  TRACED(hipEventDestroy(t1));
+  TRACED(hipStreamDestroy(s));
+  TRACED(hipFree(sink));
   return 0;
 }
 
@@ -481,10 +539,10 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   CHECK(hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost));
   out[0] = (double)h;
   out[1] = (double)n * sizeof(uint4) / (ms * 1e-3) / 1e9;
-  hipEventDestroy(t0);
-  hipEventDestroy(t1);
+  TRACED(hipEventDestroy(t0));
+  TRACED(hipEventDestroy(t1));
   scratch_put(dev, 2, p);
-  hipFree(err);
+  TRACED(hipFree(err));
   return 0;
 }
 
@@ -511,8 +569,8 @@ extern "C" int tkp_memtest_selfcheck(int dev, size_t bytes, int corrupt, double*
   unsigned long long h = 0;
   CHECK(hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost));
   out[0] = (double)h;
-  hipFree(p);
-  hipFree(err);
+  TRACED(hipFree(p));
+  TRACED(hipFree(err));
   return 0;
 }
 
@@ -553,12 +611,12 @@ extern "C" int tkp_p2p_bandwidth(int src, int dst, size_t bytes, int iters, doub
     if (gbps > best) best = gbps;
   }
   out[0] = best;
-  hipEventDestroy(t0);
-  hipEventDestroy(t1);
-  hipStreamDestroy(s);
-  hipFree(b);
+  TRACED(hipEventDestroy(t0));
+  TRACED(hipEventDestroy(t1));
+  TRACED(hipStreamDestroy(s));
+  TRACED(hipFree(b));
   CHECK(hipSetDevice(src));
-  hipFree(a);
+  TRACED(hipFree(a));
   return 0;
 }
 

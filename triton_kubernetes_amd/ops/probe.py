@@ -11,6 +11,7 @@ import ctypes
 from dataclasses import asdict, dataclass, field
 from typing import Dict, List, Optional
 
+from ..utils.trace import span
 from .native import load
 
 # MI355X reference figures (dense; never the 2:1-sparsity marketing numbers)
@@ -59,6 +60,7 @@ def _lib():
     lib.tkp_p2p_bandwidth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
     lib.tkp_set_scratch_cache.argtypes = [ctypes.c_int]
+    lib.tkp_prealloc_scratch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t]
     lib.tkp_release_scratch.restype = ctypes.c_longlong
     return lib
 
@@ -180,22 +182,43 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
         res.failures.append(f"arch {info.arch} is not gfx950")
     if info.compute_units < th.min_cus:
         res.failures.append(f"{info.compute_units} CUs < {th.min_cus}")
-    res.hbm = hbm_bandwidth(dev, hbm_bytes, hbm_iters)
+    with span("burnin.hbm", dev=dev):
+        res.hbm = hbm_bandwidth(dev, hbm_bytes, hbm_iters)
     if res.hbm["read_gbps"] < th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS:
         res.failures.append(f"HBM read {res.hbm['read_gbps']:.0f} GB/s below "
                             f"{th.min_read_frac:.0%} of {MI355X_HBM_ACHIEVABLE_GBPS:.0f}")
-    res.mfma["bf16"] = mfma_peak(dev, "bf16", mfma_iters)
-    res.mfma["fp8"] = mfma_peak(dev, "fp8", mfma_iters // 2)
+    with span("burnin.mfma_bf16", dev=dev):
+        res.mfma["bf16"] = mfma_peak(dev, "bf16", mfma_iters)
+    with span("burnin.mfma_fp8", dev=dev):
+        res.mfma["fp8"] = mfma_peak(dev, "fp8", mfma_iters // 2)
     if res.mfma["bf16"]["tflops"] < th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS:
         res.failures.append(f"bf16 MFMA {res.mfma['bf16']['tflops']:.0f} TF below "
                             f"{th.min_bf16_frac:.0%} of dense peak")
     if res.mfma["fp8"]["tflops"] < th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS:
         res.failures.append(f"fp8 MFMA {res.mfma['fp8']['tflops']:.0f} TF below "
                             f"{th.min_fp8_frac:.0%} of dense peak")
-    res.memtest = memtest(dev, mt_bytes, mt_passes)
+    with span("burnin.memtest", dev=dev):
+        res.memtest = memtest(dev, mt_bytes, mt_passes)
     if res.memtest["errors"]:
         res.failures.append(f"memtest: {res.memtest['errors']} mismatching words")
     return res
+
+
+def prealloc_scratch(dev: int, level: str = "quick") -> int:
+    """Allocate the burn-in arena of ``level`` on ``dev`` now (turns the cache on).
+
+    A long-lived node agent calls this at startup, so a bring-up's burn-in streams
+    and memtests through resident buffers instead of a hipMalloc/hipFree of GiBs
+    per run; measured on MI355X, those big allocations intermittently stall for
+    0.1-0.8 s when they follow recent frees.  Returns the bytes held."""
+    if level not in LEVELS:
+        return 0
+    hbm_bytes, _, _, mt_bytes, _ = LEVELS[level]
+    lib = _lib()
+    lib.tkp_set_scratch_cache(1)
+    rc = lib.tkp_prealloc_scratch(dev, ctypes.c_size_t(hbm_bytes), ctypes.c_size_t(mt_bytes))
+    _check(rc, f"prealloc_scratch(dev {dev})")
+    return 2 * hbm_bytes + mt_bytes
 
 
 def set_scratch_cache(on: bool) -> None:
