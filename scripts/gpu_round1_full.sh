@@ -7,9 +7,9 @@ export PYTHONPATH="$GRAFT_REPO_ROOT"
 LOG=gpurun_out/run.log
 fatal() { case "$1" in 0|1|2) return 1;; esac; return 0; }
 
-timeout -k 10 600 python -m pytest tests -m gpu -q -s -p no:cacheprovider > gpurun_out/gpu_tests.log 2>&1
+timeout -k 10 600 python -m pytest tests -m gpu -q -s -p no:cacheprovider --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1
 rc=$?; echo "pytest_gpu rc=$rc" >> $LOG; if fatal $rc; then exit $rc; fi
-timeout -k 10 600 python bench.py --steps 10 --warmup 2 --report gpurun_out/bench_report.json > gpurun_out/bench.log 2>&1
+timeout -k 10 600 python bench.py --steps 20 --warmup 2 --report gpurun_out/bench_report.json > gpurun_out/bench.log 2>&1
 rc=$?; echo "bench rc=$rc" >> $LOG; if fatal $rc; then exit $rc; fi
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
 rc=$?; echo "smoke rc=$rc" >> $LOG; if fatal $rc; then exit $rc; fi
