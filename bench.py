@@ -78,10 +78,13 @@ def main() -> int:
     if distributed:
         # control-plane sync only (CPU); the GPU collectives are the native RCCL gate
         dist.init_process_group("gloo", init_method="env://")
+    device = local_rank
     if args.sim_gpu:
         args.no_rccl_gate = True
     else:
-        torch.cuda.set_device(local_rank)
+        # one GPU per rank; a launcher that masks devices per rank leaves each rank only its own
+        device = local_rank if torch.cuda.device_count() > local_rank else 0
+        torch.cuda.set_device(device)
 
     from triton_kubernetes_amd import workflows as wf
     from triton_kubernetes_amd.backend import LocalBackend
@@ -93,7 +96,7 @@ def main() -> int:
 
     token = os.environ.get("TK_BENCH_TOKEN", "bench-token-0123456789")
     work = tempfile.mkdtemp(prefix=f"tk-bench-r{rank}-")
-    agent = NodeAgent(name=f"mi355x-{rank}", mode="sim", devices=[local_rank], token=token,
+    agent = NodeAgent(name=f"mi355x-{rank}", mode="sim", devices=[device], token=token,
                       root=os.path.join(work, "node"))
     if args.sim_gpu:
         from triton_kubernetes_amd.node.labels import synthetic_topology

@@ -215,3 +215,55 @@ def test_exec_mode_validates_hostname(tmp_path):
     res = agent.run_plan(plan)
     assert not res["ok"] and "invalid hostname" in res["error"]
     assert os.path.exists(tmp_path) and not agent.history[-1]["ok"]
+
+
+def test_agent_janitor_frees_burnin_arena_when_idle(tmp_path, monkeypatch):
+    """The resident burn-in arena is released after an idle period, re-armed by the next
+    plan, and released (cache off) at stop."""
+    import time
+
+    from triton_kubernetes_amd.ops import probe
+
+    events = []
+    monkeypatch.setattr(probe, "release_scratch", lambda: events.append("release") or 0)
+    monkeypatch.setattr(probe, "set_scratch_cache", lambda on: events.append(f"cache={on}"))
+    agent = NodeAgent("n1", "sim", devices=[0], root=str(tmp_path), token="t",
+                      topology_override=synthetic_topology(1), burnin_override=lambda d, lvl: {"ok": True})
+    agent._start_janitor(0.1)
+    plan = build_host_plan(dict(GPU_WORKER, gpu_count=1), "http://x", "t", "s", mi355x=True)
+    plan.steps = [s for s in plan.steps if s.action != "agent"]
+    assert agent.run_plan(plan)["ok"]
+    assert events == []  # still within the idle window
+    deadline = time.time() + 5
+    while events.count("release") < 1 and time.time() < deadline:
+        time.sleep(0.02)
+    assert events == ["release"]
+    assert agent.run_plan(plan)["ok"]  # re-arms: released again after the next idle period
+    while events.count("release") < 2 and time.time() < deadline:
+        time.sleep(0.02)
+    assert events == ["release", "release"]
+    agent.stop()
+    assert events[-2:] == ["release", "cache=False"]
+
+
+def test_presize_fd_table_and_procstat():
+    """Grows the fd table once (in a child, so the test process is untouched) and reports
+    per-process counters."""
+    import sys
+
+    code = (
+        "import os, resource\n"
+        "from triton_kubernetes_amd.utils import procstat\n"
+        "before = procstat.snapshot()\n"
+        "n = procstat.presize_fd_table(4096)\n"
+        "fd = os.open('/dev/null', os.O_RDONLY)\n"
+        "after = procstat.snapshot()\n"
+        "d = procstat.delta(before, after)\n"
+        "print(n, fd, resource.getrlimit(resource.RLIMIT_NOFILE)[0] >= min(4096, resource.getrlimit(resource.RLIMIT_NOFILE)[1]),"
+        " d['threads'] >= 1, d['cpu_s'] >= 0, 'fds' in after)\n")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=root, check=True).stdout.split()
+    n, fd = int(out[0]), int(out[1])
+    assert 0 < n <= 4096
+    assert fd < 64  # the lowest free descriptor is still handed out first
+    assert out[2:] == ["True", "True", "True", "True"]
