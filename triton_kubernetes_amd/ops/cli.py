@@ -4,7 +4,7 @@
     python -m triton_kubernetes_amd.ops.cli topology
     python -m triton_kubernetes_amd.ops.cli labels
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
-    python -m triton_kubernetes_amd.ops.cli hbm|mfma [...]
+    python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
 
 Every command prints one JSON document; the exit status is non-zero when the
 GPU(s) fail the gate.
@@ -37,6 +37,8 @@ def main(argv: Sequence[str] = ()) -> int:
     m.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "f32"])
     m.add_argument("--iters", type=int, default=20000)
     m.add_argument("--blocks-per-cu", type=int, default=2)
+    m.add_argument("--clock", action="store_true",
+                   help="also report the in-kernel clock and FLOP/clk/SIMD (stamped diagnostic launch)")
     args = ap.parse_args(list(argv) or sys.argv[1:])
 
     if args.cmd == "burnin":
@@ -72,7 +74,10 @@ def main(argv: Sequence[str] = ()) -> int:
     if args.cmd == "mfma":
         from . import probe
 
-        print(json.dumps(probe.mfma_peak(args.device, args.dtype, args.iters, 3, args.blocks_per_cu)))
+        res = probe.mfma_peak(args.device, args.dtype, args.iters, 3, args.blocks_per_cu)
+        if args.clock:
+            res["clock"] = probe.mfma_clock(args.device, args.dtype, args.iters, blocks_per_cu=args.blocks_per_cu)
+        print(json.dumps(res))
         return 0
     return 2
 

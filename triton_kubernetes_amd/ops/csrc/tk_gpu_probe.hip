@@ -37,6 +37,8 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <algorithm>
+#include <vector>
 
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
@@ -143,48 +145,64 @@ extern "C" int tkp_device_info(int dev, tkp_device_info* out) {
 // HBM streaming kernels
 // ---------------------------------------------------------------------------
 constexpr int STREAM_THREADS = 256;
-constexpr int STREAM_UNROLL = 8;  // independent 16-B loads in flight per lane
+constexpr int STREAM_UNROLL = 8;  // independent 16-B accesses in flight per lane
+
+// Every workgroup streams ONE contiguous slice of the buffer (1/gridDim of it), each wave
+// touching 1 KiB runs of it with STREAM_UNROLL accesses in flight per lane.  Measured on
+// MI355X (scripts/native/hbm_stream.hip, 16 workgroups per CU, 1 GiB): read 6.75 TB/s,
+// write 6.2, copy 5.8 (bytes read + written), against 5.8 / 4.0 / 4.3 for the same loops
+// striding the whole grid across the buffer — per-workgroup contiguity keeps each CU's
+// accesses within few DRAM pages at a time.
+struct Slice {
+  size_t begin, end;
+};
+
+__device__ __forceinline__ Slice block_slice(size_t n) {
+  const size_t per = (n + gridDim.x - 1) / gridDim.x;
+  const size_t b = (size_t)blockIdx.x * per;
+  return {b < n ? b : n, b + per < n ? b + per : n};
+}
 
 __global__ __launch_bounds__(STREAM_THREADS) void k_stream_read(const f32x4* __restrict__ src, size_t n4,
                                                                  float* __restrict__ sink) {
-  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
-  size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x;
+  const Slice sl = block_slice(n4);
+  size_t i = sl.begin + threadIdx.x;
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-  for (; i + (STREAM_UNROLL - 1) * stride < n4; i += STREAM_UNROLL * stride) {
+  for (; i + (STREAM_UNROLL - 1) * STREAM_THREADS < sl.end; i += STREAM_UNROLL * STREAM_THREADS) {
     f32x4 v[STREAM_UNROLL];
 #pragma unroll
-    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * STREAM_THREADS);
 #pragma unroll
     for (int u = 0; u < STREAM_UNROLL; ++u) acc += v[u];
   }
-  for (; i < n4; i += stride) acc += src[i];
+  for (; i < sl.end; i += STREAM_THREADS) acc += src[i];
   const float s = acc[0] + acc[1] + acc[2] + acc[3];
   if (s == 1.2345678e-30f) sink[threadIdx.x] = s;  // never true for the fill data; defeats DCE
 }
 
 __global__ __launch_bounds__(STREAM_THREADS) void k_stream_write(f32x4* __restrict__ dst, size_t n4, float v) {
-  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
+  const Slice sl = block_slice(n4);
   const f32x4 x = {v, v + 1.f, v + 2.f, v + 3.f};
-  size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x;
-  for (; i + (STREAM_UNROLL - 1) * stride < n4; i += STREAM_UNROLL * stride) {
+  size_t i = sl.begin + threadIdx.x;
+  for (; i + (STREAM_UNROLL - 1) * STREAM_THREADS < sl.end; i += STREAM_UNROLL * STREAM_THREADS) {
 #pragma unroll
-    for (int u = 0; u < STREAM_UNROLL; ++u) dst[i + u * stride] = x;
+    for (int u = 0; u < STREAM_UNROLL; ++u) dst[i + u * STREAM_THREADS] = x;
   }
-  for (; i < n4; i += stride) dst[i] = x;
+  for (; i < sl.end; i += STREAM_THREADS) dst[i] = x;
 }
 
 __global__ __launch_bounds__(STREAM_THREADS) void k_stream_copy(const f32x4* __restrict__ src,
                                                                  f32x4* __restrict__ dst, size_t n4) {
-  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
-  size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x;
-  for (; i + (STREAM_UNROLL - 1) * stride < n4; i += STREAM_UNROLL * stride) {
+  const Slice sl = block_slice(n4);
+  size_t i = sl.begin + threadIdx.x;
+  for (; i + (STREAM_UNROLL - 1) * STREAM_THREADS < sl.end; i += STREAM_UNROLL * STREAM_THREADS) {
     f32x4 v[STREAM_UNROLL];
 #pragma unroll
-    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * stride);
+    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(src + i + u * STREAM_THREADS);
 #pragma unroll
-    for (int u = 0; u < STREAM_UNROLL; ++u) dst[i + u * stride] = v[u];
+    for (int u = 0; u < STREAM_UNROLL; ++u) dst[i + u * STREAM_THREADS] = v[u];
   }
-  for (; i < n4; i += stride) dst[i] = src[i];
+  for (; i < sl.end; i += STREAM_THREADS) dst[i] = src[i];
 }
 
 static int stream_grid(int dev, int blocks_per_cu) {
@@ -355,7 +373,11 @@ extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_pe
 // MFMA peak kernels (register-resident operands, independent accumulators)
 // ---------------------------------------------------------------------------
 constexpr int MFMA_THREADS = 256;  // 4 waves = one per SIMD
-constexpr int MFMA_ACC = 4;        // independent accumulator chains per wave
+constexpr int MFMA_ACC = 8;        // independent accumulator chains per wave
+constexpr int MFMA_UNROLL = 2;     // loop body = MFMA_ACC * MFMA_UNROLL MFMAs; `iters` is a multiple of it
+// Measured on MI355X (scripts/native/mfma_issue.hip, in-kernel clock): 4 chains with the
+// loop branch after every 4 MFMAs issue v_mfma_f32_16x16x32_bf16 at 18.0 cycles per SIMD;
+// 16 MFMAs per branch reach 16.8 (the 16-cycle floor plus ramp), fp8 35.0 -> 32.4 (of 32).
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
   x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
@@ -367,7 +389,9 @@ __device__ __forceinline__ float rnd_unit(uint32_t seed) {
   return ((hash32(seed) >> 8) * (1.0f / 8388608.0f)) - 1.0f + (1.0f / 16777216.0f);
 }
 
-__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_bf16(float* __restrict__ out, int iters) {
+template <bool kStamp>
+__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_bf16(float* __restrict__ out, int iters,
+                                                          unsigned long long* __restrict__ stamps) {
   const uint32_t lane = blockIdx.x * MFMA_THREADS + threadIdx.x;
   bf16x8 a, b;
 #pragma unroll
@@ -378,17 +402,33 @@ __global__ __launch_bounds__(MFMA_THREADS) void k_mfma_bf16(float* __restrict__ 
   f32x4 acc[MFMA_ACC];
 #pragma unroll
   for (int c = 0; c < MFMA_ACC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int i = 0; i < iters; ++i) {
+  unsigned long long c0 = 0, r0 = 0;
+  if constexpr (kStamp) {  // diagnostic build only: in-kernel clock = dMemtime / dMemrealtime * 100 MHz
+    c0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  for (int i = 0; i < iters; i += MFMA_UNROLL) {
 #pragma unroll
-    for (int c = 0; c < MFMA_ACC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[c], 0, 0, 0);
+    for (int u = 0; u < MFMA_UNROLL; ++u)
+#pragma unroll
+      for (int c = 0; c < MFMA_ACC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, acc[c], 0, 0, 0);
   }
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < MFMA_ACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  if constexpr (kStamp) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      stamps[2 * blockIdx.x] = c1 - c0;
+      stamps[2 * blockIdx.x + 1] = r1 - r0;
+    }
+  }
   if (s == 1.2345678e-30f) out[lane] = s;
 }
 
-__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_fp8(float* __restrict__ out, int iters) {
+template <bool kStamp>
+__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_fp8(float* __restrict__ out, int iters,
+                                                          unsigned long long* __restrict__ stamps) {
   const uint32_t lane = blockIdx.x * MFMA_THREADS + threadIdx.x;
   i32x8 a, b;
 #pragma unroll
@@ -400,7 +440,14 @@ __global__ __launch_bounds__(MFMA_THREADS) void k_mfma_fp8(float* __restrict__ o
   f32x4 acc[MFMA_ACC];
 #pragma unroll
   for (int c = 0; c < MFMA_ACC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int i = 0; i < iters; ++i) {
+  unsigned long long c0 = 0, r0 = 0;
+  if constexpr (kStamp) {  // diagnostic build only: in-kernel clock = dMemtime / dMemrealtime * 100 MHz
+    c0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  for (int i = 0; i < iters; i += MFMA_UNROLL) {
+#pragma unroll
+    for (int u = 0; u < MFMA_UNROLL; ++u)
 #pragma unroll
     for (int c = 0; c < MFMA_ACC; ++c)
       // cbsz = blgp = 0: e4m3 A and B; E8M0 scale 127 == 1.0
@@ -409,22 +456,45 @@ __global__ __launch_bounds__(MFMA_THREADS) void k_mfma_fp8(float* __restrict__ o
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < MFMA_ACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  if constexpr (kStamp) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      stamps[2 * blockIdx.x] = c1 - c0;
+      stamps[2 * blockIdx.x + 1] = r1 - r0;
+    }
+  }
   if (s == 1.2345678e-30f) out[lane] = s;
 }
 
-__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_f32(float* __restrict__ out, int iters) {
+template <bool kStamp>
+__global__ __launch_bounds__(MFMA_THREADS) void k_mfma_f32(float* __restrict__ out, int iters,
+                                                          unsigned long long* __restrict__ stamps) {
   const uint32_t lane = blockIdx.x * MFMA_THREADS + threadIdx.x;
   const float a = rnd_unit(lane * 2), b = rnd_unit(lane * 2 + 1);
   f32x4 acc[MFMA_ACC];
 #pragma unroll
   for (int c = 0; c < MFMA_ACC; ++c) acc[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int i = 0; i < iters; ++i) {
+  unsigned long long c0 = 0, r0 = 0;
+  if constexpr (kStamp) {  // diagnostic build only: in-kernel clock = dMemtime / dMemrealtime * 100 MHz
+    c0 = __builtin_amdgcn_s_memtime();
+    r0 = __builtin_amdgcn_s_memrealtime();
+  }
+  for (int i = 0; i < iters; i += MFMA_UNROLL) {
 #pragma unroll
-    for (int c = 0; c < MFMA_ACC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[c], 0, 0, 0);
+    for (int u = 0; u < MFMA_UNROLL; ++u)
+#pragma unroll
+      for (int c = 0; c < MFMA_ACC; ++c) acc[c] = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc[c], 0, 0, 0);
   }
   float s = 0.f;
 #pragma unroll
   for (int c = 0; c < MFMA_ACC; ++c) s += acc[c][0] + acc[c][1] + acc[c][2] + acc[c][3];
+  if constexpr (kStamp) {
+    const unsigned long long c1 = __builtin_amdgcn_s_memtime(), r1 = __builtin_amdgcn_s_memrealtime();
+    if (threadIdx.x == 0) {
+      stamps[2 * blockIdx.x] = c1 - c0;
+      stamps[2 * blockIdx.x + 1] = r1 - r0;
+    }
+  }
   if (s == 1.2345678e-30f) out[lane] = s;
 }
 
@@ -432,6 +502,7 @@ __global__ __launch_bounds__(MFMA_THREADS) void k_mfma_f32(float* __restrict__ o
 // Returns dense TFLOP/s (best of `reps`) in out[0] and the kernel ms in out[1].
 extern "C" int tkp_mfma_peak(int dev, int dtype, int iters, int reps, int blocks_per_cu, double* out) {
   CHECK(hipSetDevice(dev));
+  iters = (iters + MFMA_UNROLL - 1) / MFMA_UNROLL * MFMA_UNROLL;
   if (blocks_per_cu < 1) blocks_per_cu = 2;
   if (reps < 1) reps = 1;
   hipDeviceProp_t p;
@@ -452,11 +523,11 @@ extern "C" int tkp_mfma_peak(int dev, int dtype, int iters, int reps, int blocks
     default: snprintf(g_err, sizeof(g_err), "unknown dtype %d", dtype); return -1;
   }
   auto launch = [&](int n) {
-    if (dtype == 0) k_mfma_bf16<<<grid, MFMA_THREADS, 0, s>>>(sink, n);
-    else if (dtype == 1) k_mfma_fp8<<<grid, MFMA_THREADS, 0, s>>>(sink, n);
-    else k_mfma_f32<<<grid, MFMA_THREADS, 0, s>>>(sink, n);
+    if (dtype == 0) k_mfma_bf16<false><<<grid, MFMA_THREADS, 0, s>>>(sink, n, nullptr);
+    else if (dtype == 1) k_mfma_fp8<false><<<grid, MFMA_THREADS, 0, s>>>(sink, n, nullptr);
+    else k_mfma_f32<false><<<grid, MFMA_THREADS, 0, s>>>(sink, n, nullptr);
   };
-  launch(iters / 4 + 1);  // warm-up (clock ramp)
+  launch((iters / 4 + MFMA_UNROLL) / MFMA_UNROLL * MFMA_UNROLL);  // warm-up (clock ramp)
   CHECK(hipGetLastError());
   CHECK(hipStreamSynchronize(s));
   double best = 0.0, best_ms = 0.0;
@@ -482,6 +553,81 @@ extern "C" int tkp_mfma_peak(int dev, int dtype, int iters, int reps, int blocks
   return 0;
 }
 
+// Diagnostic: the clock the chip holds under this MFMA loop.  `warm_ms` of back-to-back
+// production launches first (the DVFS steady state), then one stamped launch; out[0] =
+// median in-kernel clock over workgroups (MHz), out[1] = MFMA FLOP per clock per SIMD at
+// that clock from the stamped launch (1024 bf16 / 2048 fp8 / 64 f32 is the per-clock
+// peak: a lower value is an issue problem, a lower clock is DVFS), out[2] = TFLOP/s of the
+// stamped launch.  Never part of the burn-in's timed launches.
+extern "C" int tkp_mfma_clock(int dev, int dtype, int iters, int blocks_per_cu, double warm_ms, double* out) {
+  CHECK(hipSetDevice(dev));
+  iters = (iters + MFMA_UNROLL - 1) / MFMA_UNROLL * MFMA_UNROLL;
+  if (blocks_per_cu < 1) blocks_per_cu = 2;
+  hipDeviceProp_t p;
+  CHECK(hipGetDeviceProperties(&p, dev));
+  const int grid = p.multiProcessorCount * blocks_per_cu;
+  double flop_per_inst;
+  switch (dtype) {
+    case 0: flop_per_inst = 2.0 * 16 * 16 * 32; break;
+    case 1: flop_per_inst = 2.0 * 16 * 16 * 128; break;
+    case 2: flop_per_inst = 2.0 * 16 * 16 * 4; break;
+    default: snprintf(g_err, sizeof(g_err), "unknown dtype %d", dtype); return -1;
+  }
+  float* sink = nullptr;
+  unsigned long long* stamps = nullptr;
+  CHECK(hipMalloc(&sink, (size_t)grid * MFMA_THREADS * sizeof(float)));
+  CHECK(hipMalloc(&stamps, (size_t)grid * 2 * sizeof(unsigned long long)));
+  hipStream_t s;
+  CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t t0, t1;
+  CHECK(hipEventCreate(&t0));
+  CHECK(hipEventCreate(&t1));
+  auto launch = [&](bool stamp) {
+    if (dtype == 0) {
+      if (stamp) k_mfma_bf16<true><<<grid, MFMA_THREADS, 0, s>>>(sink, iters, stamps);
+      else k_mfma_bf16<false><<<grid, MFMA_THREADS, 0, s>>>(sink, iters, nullptr);
+    } else if (dtype == 1) {
+      if (stamp) k_mfma_fp8<true><<<grid, MFMA_THREADS, 0, s>>>(sink, iters, stamps);
+      else k_mfma_fp8<false><<<grid, MFMA_THREADS, 0, s>>>(sink, iters, nullptr);
+    } else {
+      if (stamp) k_mfma_f32<true><<<grid, MFMA_THREADS, 0, s>>>(sink, iters, stamps);
+      else k_mfma_f32<false><<<grid, MFMA_THREADS, 0, s>>>(sink, iters, nullptr);
+    }
+  };
+  const auto w0 = std::chrono::steady_clock::now();
+  do {  // bounded: at most warm_ms (plus one batch) of launches
+    for (int k = 0; k < 8; ++k) launch(false);
+    CHECK(hipStreamSynchronize(s));
+  } while (std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - w0).count() < warm_ms);
+  CHECK(hipEventRecord(t0, s));
+  launch(true);
+  CHECK(hipEventRecord(t1, s));
+  CHECK(hipEventSynchronize(t1));
+  CHECK(hipGetLastError());
+  float ms = 0.f;
+  CHECK(hipEventElapsedTime(&ms, t0, t1));
+  std::vector<unsigned long long> h((size_t)grid * 2);
+  CHECK(hipMemcpy(h.data(), stamps, h.size() * sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  std::vector<double> mhz;
+  mhz.reserve(grid);
+  for (int b = 0; b < grid; ++b)
+    if (h[2 * b + 1] > 0) mhz.push_back((double)h[2 * b] / (double)h[2 * b + 1] * 100.0);
+  std::sort(mhz.begin(), mhz.end());
+  const double clk = mhz.empty() ? 0.0 : mhz[mhz.size() / 2];
+  const double waves = (double)grid * (MFMA_THREADS / 64);
+  const double flops = waves * (double)iters * MFMA_ACC * flop_per_inst;
+  const double simds = (double)p.multiProcessorCount * 4;
+  out[0] = clk;
+  out[2] = flops / (ms * 1e-3) / 1e12;
+  out[1] = clk > 0 ? flops / (ms * 1e-3) / (clk * 1e6) / simds : 0.0;
+  TRACED(hipEventDestroy(t0));
+  TRACED(hipEventDestroy(t1));
+  TRACED(hipStreamDestroy(s));
+  TRACED(hipFree(stamps));
+  TRACED(hipFree(sink));
+  return 0;
+}
+
 // ---------------------------------------------------------------------------
 // HBM pattern memtest: address-hash pattern, written and verified in
 // streaming passes; mismatches are counted per wave (ballot + popcount) and
@@ -493,19 +639,32 @@ __device__ __forceinline__ uint4 pattern(size_t i, uint32_t seed) {
 }
 
 __global__ __launch_bounds__(STREAM_THREADS) void k_mem_fill(uint4* __restrict__ p, size_t n, uint32_t seed) {
-  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
-  for (size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x; i < n; i += stride) p[i] = pattern(i, seed);
+  const Slice sl = block_slice(n);  // same contiguous-slice traversal as the stream kernels
+  size_t i = sl.begin + threadIdx.x;
+  for (; i + (STREAM_UNROLL - 1) * STREAM_THREADS < sl.end; i += STREAM_UNROLL * STREAM_THREADS) {
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) p[i + u * STREAM_THREADS] = pattern(i + u * STREAM_THREADS, seed);
+  }
+  for (; i < sl.end; i += STREAM_THREADS) p[i] = pattern(i, seed);
 }
 
 __global__ __launch_bounds__(STREAM_THREADS) void k_mem_check(const uint4* __restrict__ p, size_t n, uint32_t seed,
                                                                unsigned long long* __restrict__ errors) {
-  const size_t stride = (size_t)gridDim.x * STREAM_THREADS;
+  const Slice sl = block_slice(n);
   uint32_t bad = 0;
-  for (size_t i = (size_t)blockIdx.x * STREAM_THREADS + threadIdx.x; i < n; i += stride) {
-    const uint4 v = p[i];
-    const uint4 w = pattern(i, seed);
+  auto cmp = [&](const uint4 v, size_t j) {
+    const uint4 w = pattern(j, seed);
     bad += (v.x != w.x) + (v.y != w.y) + (v.z != w.z) + (v.w != w.w);
+  };
+  size_t i = sl.begin + threadIdx.x;
+  for (; i + (STREAM_UNROLL - 1) * STREAM_THREADS < sl.end; i += STREAM_UNROLL * STREAM_THREADS) {
+    uint4 v[STREAM_UNROLL];
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = p[i + u * STREAM_THREADS];
+#pragma unroll
+    for (int u = 0; u < STREAM_UNROLL; ++u) cmp(v[u], i + u * STREAM_THREADS);
   }
+  for (; i < sl.end; i += STREAM_THREADS) cmp(p[i], i);
   // wave-level reduction: 64 lanes
   for (int off = 32; off > 0; off >>= 1) bad += __shfl_down(bad, off, 64);
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(errors, (unsigned long long)bad);
@@ -645,7 +804,7 @@ int main(int argc, char** argv) {
   const bool full = !strcmp(level, "full");
   const size_t hbm_bytes = full ? (16ull << 30) : (1ull << 30);
   const size_t mt_bytes = full ? (64ull << 30) : (1ull << 30);
-  const int mfma_iters = full ? 40000 : 4000;
+  const int mfma_iters = full ? 20000 : 2000;  // x MFMA_ACC (8) chains per wave
   int n = 0;
   if (tkp_device_count(&n) != 0 || n < 1) {
     printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);

@@ -54,6 +54,8 @@ def _lib():
                                       ctypes.POINTER(ctypes.c_double)]
     lib.tkp_mfma_peak.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                   ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_mfma_clock.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
+                                   ctypes.POINTER(ctypes.c_double)]
     lib.tkp_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     lib.tkp_memtest_selfcheck.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_double)]
@@ -117,6 +119,26 @@ def mfma_peak(dev: int, dtype: str = "bf16", iters: int = 20000, reps: int = 3,
     return {"tflops": out[0], "ms": out[1]}
 
 
+# MFMA FLOP per clock per SIMD at full issue (MI355X_MICROARCH.md § Matrix cores)
+MFMA_PEAK_FLOP_PER_CLK = {"bf16": 1024.0, "fp8": 2048.0, "f32": 64.0}
+
+
+def mfma_clock(dev: int, dtype: str = "bf16", iters: int = 20000, warm_ms: float = 1500.0,
+               blocks_per_cu: int = 2) -> Dict[str, float]:
+    """Diagnostic: the in-kernel clock the chip holds under the MFMA loop (after ``warm_ms``
+    of back-to-back launches) and the loop's FLOP per clock per SIMD at that clock.
+
+    ``issue_efficiency`` near 1 means the kernel issues MFMAs at the per-clock peak, so the
+    gap between measured TFLOP/s and the 2.5 / 5 PF dense figures is the clock the chip
+    holds under load on random operands (DVFS), not the kernel."""
+    out = (ctypes.c_double * 3)()
+    _check(_lib().tkp_mfma_clock(dev, DTYPES[dtype], iters, blocks_per_cu, float(warm_ms), out),
+           f"mfma_clock[{dtype}]")
+    peak = MFMA_PEAK_FLOP_PER_CLK[dtype]
+    return {"mhz": round(out[0], 1), "flop_per_clk_per_simd": round(out[1], 1), "tflops": round(out[2], 1),
+            "issue_efficiency": round(out[1] / peak, 4) if peak else 0.0}
+
+
 def memtest(dev: int, nbytes: int = 1 << 30, passes: int = 2) -> Dict[str, float]:
     out = (ctypes.c_double * 2)()
     _check(_lib().tkp_memtest(dev, nbytes, passes, out), "memtest")
@@ -137,9 +159,9 @@ def p2p_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 5) -
 
 # --- burn-in policy ------------------------------------------------------------------
 LEVELS = {
-    # level: (hbm bytes, hbm iters, mfma iters, memtest bytes, memtest passes)
-    "quick": (1 << 30, 3, 4000, 1 << 30, 1),
-    "full": (16 << 30, 10, 40000, 64 << 30, 3),
+    # level: (hbm bytes, hbm iters, mfma iters (x 8 accumulator chains per wave), memtest bytes, memtest passes)
+    "quick": (1 << 30, 3, 2000, 1 << 30, 1),
+    "full": (16 << 30, 10, 20000, 64 << 30, 3),
 }
 
 
