@@ -205,6 +205,22 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_stream_copy(const f32x4* __r
   for (; i < sl.end; i += STREAM_THREADS) dst[i] = src[i];
 }
 
+// Burn-in streams run at the device's LOWEST stream priority by default
+// (TKP_STREAM_PRIORITY=normal for the default priority): a burn-in shares the GPU with
+// the cluster gate's RCCL communicator init, whose many small memset/copy kernels are
+// the bring-up's critical path — those dispatch ahead of queued burn-in workgroups.
+static hipError_t burnin_stream(hipStream_t* s) {
+  static const bool low = [] {
+    const char* v = getenv("TKP_STREAM_PRIORITY");
+    return !(v && !strcmp(v, "normal"));
+  }();
+  if (!low) return hipStreamCreateWithFlags(s, hipStreamNonBlocking);
+  int least = 0, greatest = 0;
+  hipError_t e = hipDeviceGetStreamPriorityRange(&least, &greatest);
+  if (e != hipSuccess) return e;
+  return hipStreamCreateWithPriority(s, hipStreamNonBlocking, least);
+}
+
 static int stream_grid(int dev, int blocks_per_cu) {
   hipDeviceProp_t p;
   if (hipGetDeviceProperties(&p, dev) != hipSuccess) return 4096;
@@ -330,7 +346,7 @@ extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_pe
   if (e != hipSuccess) { scratch_put(dev, 0, a); return set_err("hipMalloc(b)", e); }
   CHECK(hipMalloc(&sink, STREAM_THREADS * sizeof(float)));
   hipStream_t s;
-  CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  CHECK(burnin_stream(&s));
   hipEvent_t t0, t1;
   CHECK(hipEventCreate(&t0));
   CHECK(hipEventCreate(&t1));
@@ -511,7 +527,7 @@ extern "C" int tkp_mfma_peak(int dev, int dtype, int iters, int reps, int blocks
   float* sink = nullptr;
   CHECK(hipMalloc(&sink, (size_t)grid * MFMA_THREADS * sizeof(float)));
   hipStream_t s;
-  CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  CHECK(burnin_stream(&s));
   hipEvent_t t0, t1;
   CHECK(hipEventCreate(&t0));
   CHECK(hipEventCreate(&t1));
@@ -678,7 +694,9 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   unsigned long long* err = nullptr;
   CHECK(scratch_get(dev, 2, n * sizeof(uint4), reinterpret_cast<void**>(&p)));
   CHECK(hipMalloc(&err, sizeof(unsigned long long)));
-  CHECK(hipMemset(err, 0, sizeof(unsigned long long)));
+  hipStream_t s;
+  CHECK(burnin_stream(&s));
+  CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), s));
   hipEvent_t t0, t1;
   CHECK(hipEventCreate(&t0));
   CHECK(hipEventCreate(&t1));
@@ -686,20 +704,22 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   float ms = 0.f;
   for (int ps = 0; ps < (passes < 1 ? 1 : passes); ++ps) {
     const uint32_t seed = 0x1234567u + 0x9e3779b9u * (uint32_t)ps;
-    k_mem_fill<<<grid, STREAM_THREADS>>>(p, n, seed);
-    CHECK(hipEventRecord(t0, 0));
-    k_mem_check<<<grid, STREAM_THREADS>>>(p, n, seed, err);
-    CHECK(hipEventRecord(t1, 0));
+    k_mem_fill<<<grid, STREAM_THREADS, 0, s>>>(p, n, seed);
+    CHECK(hipEventRecord(t0, s));
+    k_mem_check<<<grid, STREAM_THREADS, 0, s>>>(p, n, seed, err);
+    CHECK(hipEventRecord(t1, s));
     CHECK(hipEventSynchronize(t1));
     CHECK(hipEventElapsedTime(&ms, t0, t1));
   }
   CHECK(hipGetLastError());
   unsigned long long h = 0;
-  CHECK(hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost));
+  CHECK(hipMemcpyAsync(&h, err, sizeof(h), hipMemcpyDeviceToHost, s));
+  CHECK(hipStreamSynchronize(s));
   out[0] = (double)h;
   out[1] = (double)n * sizeof(uint4) / (ms * 1e-3) / 1e9;
   TRACED(hipEventDestroy(t0));
   TRACED(hipEventDestroy(t1));
+  TRACED(hipStreamDestroy(s));
   scratch_put(dev, 2, p);
   TRACED(hipFree(err));
   return 0;
