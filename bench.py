@@ -111,6 +111,7 @@ def main() -> int:
 
     fake = cp_agent = None
     backend = ctx_base = None
+    devnull = open(os.devnull, "w", encoding="utf-8")  # workflow output (one handle for every step)
     if rank == 0:
         from triton_kubernetes_amd.rancher.fake import FakeRancher
 
@@ -122,7 +123,7 @@ def main() -> int:
                     "non-interactive": True, "cluster_manager": "bench"}
         mgr = dict(ctx_base, manager_cloud_provider="baremetal", name="bench", rancher_admin_password="bench-pw",
                    host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="~/.ssh/id_rsa")
-        wf.new_manager(Context(settings=Settings(mgr, env={}), out=open(os.devnull, "w")), backend)
+        wf.new_manager(Context(settings=Settings(mgr, env={}), out=devnull), backend)
 
     sizes = [1 << 20, args.rccl_mib << 20]
     # long-lived startup objects (torch, the package, servers) leave the GC's working set,
@@ -162,7 +163,7 @@ def main() -> int:
                         "hosts": ["agent+" + u for u in urls], "gpu": "mi355x", "gpu_count": 1,
                         "gpu_burnin": args.burnin},
                    ])
-        ctx = Context(settings=Settings(cfg, env={}), out=open(os.devnull, "w"))
+        ctx = Context(settings=Settings(cfg, env={}), out=devnull)
         ctx.extras["agent_transport"] = AgentTransport(token=token)
         ps0 = procstat.snapshot()
         t0 = time.time()
@@ -245,6 +246,7 @@ def main() -> int:
                            "cpu_quota": procstat.cpu_quota(), "cpu_affinity": len(os.sched_getaffinity(0)),
                            "cgroup_cpu_dir": procstat.cgroup_cpu_dir()},
                           fh, indent=1, default=str)
+    devnull.close()
     agent.stop()
     if cp_agent is not None:
         cp_agent.stop()
