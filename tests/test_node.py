@@ -100,7 +100,7 @@ def test_labels_from_synthetic_topology():
     assert labels["amd.com/xgmi.fully-connected"] == "true"
     assert labels["amd.com/xgmi.links-per-gpu"] == "7"
     assert labels["amd.com/xgmi.hive-id"] == "0xabc123"
-    assert labels_from_topology({"gpus": []}) == {"amd.com/gpu.present": "false"}
+    assert labels_from_topology({"gpus": []}) == {"amd.com/gpu.present": "false", "amd.com/rdma.count": "0"}
     flags = agent_label_flags({"b": "2", "a": "1"})
     assert flags == ["--label", "a=1", "--label", "b=2"]
 

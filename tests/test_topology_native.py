@@ -125,3 +125,83 @@ def test_executable_sysfs_root(tmp_path, native_ok):
     empty = subprocess.run([exe, "--labels", "--source", "sysfs", "--sysfs-root", str(tmp_path / "none")],
                            capture_output=True, text=True, timeout=60)
     assert empty.returncode == 2 and "no KFD topology" in empty.stderr
+
+
+def add_rdma(root, nics):
+    """RDMA devices under sys/class/infiniband: (name, state, link_layer, rate, netdev, numa)."""
+    for name, state, layer, rate, netdev, numa in nics:
+        dev = os.path.join(root, "sys/class/infiniband", name)
+        _write(f"{dev}/ports/1/state", f"{state}\n")
+        _write(f"{dev}/ports/1/link_layer", f"{layer}\n")
+        _write(f"{dev}/ports/1/rate", f"{rate}\n")
+        pci = os.path.join(root, "sys/devices/pci0000:00", f"0000:{0x1a + len(name):02x}:00.0")
+        _write(f"{pci}/numa_node", f"{numa}\n")
+        os.makedirs(f"{pci}/net/{netdev}", exist_ok=True)
+        os.symlink(pci, f"{dev}/device")
+    return root
+
+
+RDMA = [("mlx5_0", "4: ACTIVE", "Ethernet", "400 Gb/sec (4X NDR)", "ens1f0np0", 0),
+        ("mlx5_1", "1: DOWN", "Ethernet", "400 Gb/sec (4X NDR)", "ens1f1np1", 0),
+        ("mlx5_2", "4: ACTIVE", "Ethernet", "200 Gb/sec (4X HDR)", "ens2f0np0", 1)]
+
+
+def test_rdma_nics_python_reader_labels_and_rccl_env(tmp_path):
+    from triton_kubernetes_amd.parallel.rccl_env import site_env_from_topology
+
+    root = add_rdma(make_tree(str(tmp_path), ngpu=2), RDMA)
+    nics = topo.rdma_nics(root)
+    assert [n["name"] for n in nics] == ["mlx5_0", "mlx5_1", "mlx5_2"]
+    assert [n["port"] for n in nics] == [1, 0, 1] and [n["active"] for n in nics] == [True, False, True]
+    assert nics[0]["rate_gbps"] == 400 and nics[0]["netdev"] == "ens1f0np0" and nics[2]["numa_node"] == 1
+    assert nics[0]["bdf"].startswith("0000:")
+    labels = labels_from_topology({"gpus": [], "nics": nics})
+    assert labels["amd.com/rdma.count"] == "2"
+    assert labels["amd.com/rdma.link-layer"] == "ethernet" and labels["amd.com/rdma.rate-gbps"] == "200"
+    env = site_env_from_topology({"nics": nics})
+    assert env == {"NCCL_IB_HCA": "=mlx5_0:1,mlx5_2:1", "NCCL_IB_GID_INDEX": "3"}
+    assert site_env_from_topology({"nics": []}) == {}
+    ib = [dict(n, link_layer="InfiniBand") for n in nics]
+    assert site_env_from_topology({"nics": ib}) == {"NCCL_IB_HCA": "=mlx5_0:1,mlx5_2:1"}
+
+
+def test_rdma_native_matches_python(tmp_path, native_ok):
+    """C++ NIC collector, its labels and its RCCL env equal the Python mirror."""
+    from triton_kubernetes_amd.parallel.rccl_env import site_env_from_topology
+
+    root = add_rdma(make_tree(str(tmp_path), ngpu=8), RDMA)
+    doc = topo.native_topology("sysfs", root)
+    assert doc["status"] == 0
+    assert doc["nics"] == topo.rdma_nics(root)
+    labels = topo.native_labels("sysfs", root)
+    assert labels == labels_from_topology(doc)
+    assert labels["amd.com/rdma.count"] == "2"
+    assert topo.native_rccl_env(root) == site_env_from_topology(doc)
+    exe = executable("amdgpu-topo-labeller")
+    out = subprocess.run([exe, "--rccl-env", "--sysfs-root", root], capture_output=True, text=True, check=True).stdout
+    assert out.splitlines() == ['NCCL_IB_HCA="=mlx5_0:1,mlx5_2:1"', 'NCCL_IB_GID_INDEX="3"']
+
+
+def test_agent_rccl_env_merges_discovered_nics(tmp_path):
+    """The agent writes the discovered RDMA settings; an explicit rccl_env key wins."""
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.labels import synthetic_topology
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.parallel.rccl_env import parse_env_file
+
+    nics = topo.rdma_nics(add_rdma(str(tmp_path / "sys"), RDMA))
+    topology = dict(synthetic_topology(1), nics=nics)
+    agent = NodeAgent("n1", "sim", devices=[0], root=str(tmp_path / "node"), token="t",
+                      topology_override=topology, burnin_override=lambda d, lvl: {"ok": True})
+    cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
+           "rccl_env": {"NCCL_IB_GID_INDEX": "5", "NCCL_DEBUG": "INFO"}}
+    plan = build_host_plan(cfg, "http://x", "t", "s", mi355x=True)
+    plan.steps = [s for s in plan.steps if s.action != "agent"]
+    res = agent.run_plan(plan)
+    assert res["ok"], res
+    env = parse_env_file((tmp_path / "node/etc/rccl/rccl.env").read_text())
+    assert env["NCCL_IB_HCA"] == "=mlx5_0:1,mlx5_2:1"
+    assert env["NCCL_IB_GID_INDEX"] == "5" and env["NCCL_DEBUG"] == "INFO"
+    assert res["labels"]["amd.com/rdma.count"] == "2"
+    step = next(s for s in res["steps"] if s["name"] == "rccl_env")
+    assert step["detail"]["discovered"] == ["NCCL_IB_GID_INDEX", "NCCL_IB_HCA"]

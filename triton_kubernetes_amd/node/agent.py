@@ -48,7 +48,7 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, List, Optional
 
 from ..cloud.http import HTTPClient
-from ..parallel.rccl_env import render_env_file
+from ..parallel.rccl_env import render_env_file, site_env_from_topology
 from ..rancher.fake import tunnel_params
 from ..utils import procstat
 from ..utils.trace import span
@@ -220,6 +220,7 @@ class NodeAgent:
             fut = ctx.get("topology_future")
             topo = fut.result() if fut is not None else self._topology()
             labels = labels_from_topology(topo)
+            ctx["topology"] = topo
             ctx["labels"].update(labels)
             self.last_labels = labels
             self.write_file("/etc/triton-kubernetes/gpu-topology.json", json.dumps(topo))
@@ -243,7 +244,11 @@ class NodeAgent:
             ctx["capacity"]["amd.com/gpu"] = len(self.devices)
             return out
         if a == "rccl_env":
-            return self.write_file("/etc/rccl/rccl.env", render_env_file(step.params.get("env", {})))
+            # discovered inter-node settings, then the configured values (which win)
+            env = site_env_from_topology(ctx.get("topology") or {})
+            discovered = sorted(env)
+            env.update(step.params.get("env", {}))
+            return {"file": self.write_file("/etc/rccl/rccl.env", render_env_file(env)), "discovered": discovered}
         if a == "rccl_local":
             if len(self.devices) < 2:
                 return {"skipped": "single GPU"}

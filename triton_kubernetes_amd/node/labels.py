@@ -50,7 +50,26 @@ def product_name(market_name: str, device_id: str = "") -> str:
     return m.group(1) if m else _label_value(market_name)
 
 
+def rdma_labels(doc: Dict[str, Any]) -> Dict[str, str]:
+    """``amd.com/rdma.*``: the node's active RDMA ports (inter-node RCCL fabric)."""
+    active = [n for n in doc.get("nics", []) or [] if n.get("port", 0) > 0]
+    labels = {"amd.com/rdma.count": str(len(active))}
+    layers = {str(n.get("link_layer", "")).lower() for n in active if n.get("link_layer")}
+    if len(layers) == 1:
+        labels["amd.com/rdma.link-layer"] = _label_value(layers.pop())
+    rates = [int(n["rate_gbps"]) for n in active if n.get("rate_gbps")]
+    if rates:
+        labels["amd.com/rdma.rate-gbps"] = str(min(rates))
+    return labels
+
+
 def labels_from_topology(doc: Dict[str, Any]) -> Dict[str, str]:
+    labels = _gpu_labels(doc)
+    labels.update(rdma_labels(doc))
+    return labels
+
+
+def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     gpus: List[Dict[str, Any]] = doc.get("gpus") or []
     if not gpus:
         return {"amd.com/gpu.present": "false"}

@@ -194,11 +194,14 @@ sudo mkdir -p /etc/triton-kubernetes
 sudo mkdir -p "$(dirname {LABEL_FILE})"
 {TOOLS_DIR}/amdgpu-topo-labeller | sudo tee {TOPOLOGY_FILE} >/dev/null
 {TOOLS_DIR}/amdgpu-topo-labeller --labels | sudo tee {LABEL_FILE} >/dev/null""", gpu=True))
+        # discovered inter-node settings (active RDMA ports) first; the configured
+        # values follow, so an explicit rccl_env key wins when the file is sourced
         plan.steps.append(Step("rccl_env", "rccl_env", f"""
 sudo mkdir -p "$(dirname {RCCL_ENV_FILE})"
-sudo tee {RCCL_ENV_FILE} >/dev/null <<'TK_RCCL_EOF'
+{{ {TOOLS_DIR}/amdgpu-topo-labeller --rccl-env || true; cat <<'TK_RCCL_EOF'
 {render_env_file(env).rstrip()}
-TK_RCCL_EOF""", {"env": env}, gpu=True))
+TK_RCCL_EOF
+}} | sudo tee {RCCL_ENV_FILE} >/dev/null""", {"env": env}, gpu=True))
         if ngpu > 1:
             plan.steps.append(Step("rccl_local", "rccl_local",
                                    f"{TOOLS_DIR}/rccl-ready --ngpus {ngpu} --min-busbw "

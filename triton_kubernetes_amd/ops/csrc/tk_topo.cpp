@@ -1,8 +1,8 @@
 // amdgpu-topo-labeller (N1): describe the node's AMD GPUs and
 // every GPU<->GPU link as one JSON document, or as the Kubernetes node labels
 // derived from it (product, count, CU count, VRAM, partition modes, xGMI hive
-// id, links per GPU, fully-connected flag) used by the device plugin, the
-// readiness waiter and xGMI-aware pod affinity.
+// id, links per GPU, fully-connected flag, RDMA NICs) used by the device plugin,
+// the readiness waiter, xGMI-aware pod affinity and the inter-node RCCL settings.
 //
 // Two collectors fill the same GpuInfo records:
 //   amdsmi  libamd_smi (amdsmi_init + per-processor queries);
@@ -25,6 +25,7 @@
 #include <amd_smi/amdsmi.h>
 #endif
 #include <dirent.h>
+#include <unistd.h>
 
 #include <algorithm>
 #include <cctype>
@@ -83,12 +84,22 @@ struct GpuInfo {
   std::vector<Link> links;
 };
 
+// One RDMA device (/sys/class/infiniband/<name>): the inter-node fabric RCCL uses
+// between MI355X nodes (RoCE or InfiniBand NICs).
+struct NicInfo {
+  std::string name, link_layer, netdev, bdf;
+  int port = 0;             // first ACTIVE port (0: none active)
+  uint64_t rate_gbps = 0;   // of that port
+  int64_t numa_node = -1;
+};
+
 struct Topology {
   std::string source;
   int status = 0;
   std::string error;
   std::string driver_name, driver_version;
   std::vector<GpuInfo> gpus;
+  std::vector<NicInfo> nics;
 };
 
 std::string hex64(uint64_t v) {
@@ -404,6 +415,57 @@ Topology collect_sysfs(const std::string& root) {
   return t;
 }
 
+// RDMA NICs: /sys/class/infiniband/<dev>/ports/<n>/{state,link_layer,rate}, the netdev
+// under <dev>/device/net and the PCI function <dev>/device points at.  Same for both
+// collectors (amd_smi does not describe NICs).  Mirrored in ops/topo.py:rdma_nics.
+std::vector<NicInfo> collect_nics(const std::string& root) {
+  std::vector<NicInfo> out;
+  const std::string ib = root + "/sys/class/infiniband";
+  DIR* d = opendir(ib.c_str());
+  if (!d) return out;
+  std::vector<std::string> names;
+  while (dirent* e = readdir(d))
+    if (e->d_name[0] != '.') names.push_back(e->d_name);
+  closedir(d);
+  std::sort(names.begin(), names.end());
+  for (const auto& n : names) {
+    NicInfo nic;
+    nic.name = n;
+    const std::string dev = ib + "/" + n;
+    std::string s;
+    for (int port : numeric_entries(dev + "/ports")) {
+      const std::string pd = dev + "/ports/" + std::to_string(port);
+      if (!read_file(pd + "/state", &s) || s.find("ACTIVE") == std::string::npos) {
+        if (nic.link_layer.empty() && read_file(pd + "/link_layer", &s)) nic.link_layer = s;
+        continue;
+      }
+      nic.port = port;
+      if (read_file(pd + "/link_layer", &s)) nic.link_layer = s;
+      if (read_file(pd + "/rate", &s)) nic.rate_gbps = strtoull(s.c_str(), nullptr, 10);
+      break;
+    }
+    if (read_file(dev + "/device/numa_node", &s)) nic.numa_node = atoll(s.c_str());
+    DIR* nd = opendir((dev + "/device/net").c_str());
+    if (nd) {
+      std::vector<std::string> nets;
+      while (dirent* e = readdir(nd))
+        if (e->d_name[0] != '.') nets.push_back(e->d_name);
+      closedir(nd);
+      std::sort(nets.begin(), nets.end());
+      if (!nets.empty()) nic.netdev = nets.front();
+    }
+    char link[4096];
+    const ssize_t k = readlink((dev + "/device").c_str(), link, sizeof(link) - 1);
+    if (k > 0) {
+      link[k] = 0;
+      const char* base = strrchr(link, '/');
+      nic.bdf = base ? base + 1 : link;
+    }
+    out.push_back(std::move(nic));
+  }
+  return out;
+}
+
 // ------------------------------------------------------------ renderers ----
 std::string render_json(const Topology& t) {
   std::string o;
@@ -450,6 +512,17 @@ std::string render_json(const Topology& t) {
               l.type.c_str(), l.hops, l.p2p ? "true" : "false");
     }
     o += "]}";
+  }
+  o += "],\"nics\":[";
+  for (size_t i = 0; i < t.nics.size(); ++i) {
+    const NicInfo& n = t.nics[i];
+    appendf(o, "%s{\"name\":\"%s\",\"port\":%d,\"active\":%s,\"link_layer\":\"%s\",\"rate_gbps\":%" PRIu64,
+            i ? "," : "", esc(n.name).c_str(), n.port, n.port > 0 ? "true" : "false", esc(n.link_layer).c_str(),
+            n.rate_gbps);
+    if (!n.netdev.empty()) appendf(o, ",\"netdev\":\"%s\"", esc(n.netdev).c_str());
+    if (!n.bdf.empty()) appendf(o, ",\"bdf\":\"%s\"", esc(n.bdf).c_str());
+    if (n.numa_node >= 0) appendf(o, ",\"numa_node\":%" PRId64, n.numa_node);
+    o += "}";
   }
   o += "]}";
   return o;
@@ -542,14 +615,43 @@ std::string render_labels(const Topology& t) {
     L["amd.com/xgmi.fully-connected"] = (gs.size() > 1 && min_xgmi == gs.size() - 1) ? "true" : "false";
     L["amd.com/gpu.ecc-uncorrectable"] = std::to_string(ecc);
   }
+  // inter-node fabric: active RDMA ports
+  size_t active = 0;
+  std::set<std::string> layers;
+  uint64_t min_rate = UINT64_MAX;
+  for (const auto& n : t.nics) {
+    if (n.port <= 0) continue;
+    ++active;
+    if (!n.link_layer.empty()) layers.insert(lower(n.link_layer));
+    if (n.rate_gbps) min_rate = std::min(min_rate, n.rate_gbps);
+  }
+  L["amd.com/rdma.count"] = std::to_string(active);
+  if (layers.size() == 1) L["amd.com/rdma.link-layer"] = label_value(*layers.begin());
+  if (min_rate != UINT64_MAX) L["amd.com/rdma.rate-gbps"] = std::to_string(min_rate);
   std::string o;
   for (const auto& kv : L) o += kv.first + "=" + kv.second + "\n";
   return o;
 }
 
-Topology collect(const char* source, const char* root) {
-  const std::string src = source ? source : "auto";
-  const std::string r = (root && *root) ? root : "";
+// RCCL/NCCL settings for the inter-node fabric, one KEY="value" line each (sourced after
+// the static /etc/rccl/rccl.env defaults; explicit per-node overrides come later and win).
+// Mirrored in parallel/rccl_env.py:site_env_from_topology.
+std::string render_rccl_env(const Topology& t) {
+  std::string hca;
+  bool roce = false;
+  for (const auto& n : t.nics) {
+    if (n.port <= 0) continue;
+    hca += (hca.empty() ? "" : ",") + n.name + ":" + std::to_string(n.port);
+    roce = roce || lower(n.link_layer) == "ethernet";
+  }
+  std::string o;
+  if (hca.empty()) return o;
+  o += "NCCL_IB_HCA=\"=" + hca + "\"\n";  // leading '=': exact device names, not prefixes
+  if (roce) o += "NCCL_IB_GID_INDEX=\"3\"\n";  // RoCE v2 GID
+  return o;
+}
+
+Topology collect_gpus(const std::string& src, const std::string& r) {
   if (src == "sysfs") return collect_sysfs(r);
   if (src == "amdsmi") return collect_amdsmi();
   Topology t = collect_amdsmi();
@@ -557,6 +659,13 @@ Topology collect(const char* source, const char* root) {
     Topology s = collect_sysfs(r);
     if (s.status == 0) return s;
   }
+  return t;
+}
+
+Topology collect(const char* source, const char* root) {
+  const std::string r = (root && *root) ? root : "";
+  Topology t = collect_gpus(source ? source : "auto", r);
+  t.nics = collect_nics(r);
   return t;
 }
 
@@ -586,32 +695,48 @@ extern "C" int tkt_topology_labels_src(const char* source, const char* root, cha
   return rc < 0 ? rc : t.status;
 }
 
+// Same contract; the payload is the inter-node RCCL environment (KEY="value" lines).
+extern "C" int tkt_rccl_env_src(const char* root, char* buf, size_t len) {
+  Topology t;
+  t.nics = collect_nics((root && *root) ? root : "");
+  return copy_out(render_rccl_env(t), buf, len);
+}
+
 extern "C" int tkt_topology_json(char* buf, size_t len) { return tkt_topology_json_src("amdsmi", "", buf, len); }
 
 extern "C" int tkt_topology_labels(char* buf, size_t len) { return tkt_topology_labels_src("amdsmi", "", buf, len); }
 
 #ifdef TK_TOPO_MAIN
-// amdgpu-topo-labeller [--labels] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
-//   default: topology JSON on stdout; --labels: one `amd.com/...=value` per line
+// amdgpu-topo-labeller [--labels|--rccl-env] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
+//   default: topology JSON on stdout; --labels: one `amd.com/...=value` per line;
+//   --rccl-env: the inter-node RCCL settings for the node's active RDMA ports
 int main(int argc, char** argv) {
-  bool labels = false;
+  bool labels = false, rccl_env = false;
   const char* source = "auto";
   const char* root = "";
   for (int i = 1; i < argc; ++i) {
     if (strcmp(argv[i], "--labels") == 0) {
       labels = true;
+    } else if (strcmp(argv[i], "--rccl-env") == 0) {
+      rccl_env = true;
     } else if (strcmp(argv[i], "--source") == 0 && i + 1 < argc) {
       source = argv[++i];
     } else if (strcmp(argv[i], "--sysfs-root") == 0 && i + 1 < argc) {
       root = argv[++i];
     } else {
-      fprintf(stderr, "usage: %s [--labels] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]\n", argv[0]);
+      fprintf(stderr, "usage: %s [--labels|--rccl-env] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]\n", argv[0]);
       return 64;
     }
   }
   if (strcmp(source, "auto") != 0 && strcmp(source, "amdsmi") != 0 && strcmp(source, "sysfs") != 0) {
     fprintf(stderr, "unknown --source '%s'\n", source);
     return 64;
+  }
+  if (rccl_env) {  // NIC-only: no GPU collector runs
+    Topology t;
+    t.nics = collect_nics(root);
+    fputs(render_rccl_env(t).c_str(), stdout);
+    return 0;
   }
   const Topology t = collect(source, root);
   if (labels) {

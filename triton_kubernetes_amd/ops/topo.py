@@ -83,6 +83,21 @@ def native_topology(source: str = "sysfs", sysfs_root: str = "") -> Dict[str, An
     return doc
 
 
+def native_rccl_env(sysfs_root: str = "") -> Dict[str, str]:
+    """The labeller's inter-node RCCL settings (``amdgpu-topo-labeller --rccl-env``), in-process."""
+    from ..parallel.rccl_env import parse_env_file
+
+    lib = load("libtk_topo.so")
+    fn = lib.tkt_rccl_env_src
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_size_t]
+    fn.restype = ctypes.c_int
+    buf = ctypes.create_string_buffer(1 << 14)
+    rc = fn(sysfs_root.encode(), buf, len(buf))
+    if rc != 0:
+        raise NativeUnavailable(f"tkt_rccl_env_src failed ({rc})")
+    return parse_env_file(buf.value.decode())
+
+
 def native_labels(source: str = "sysfs", sysfs_root: str = "") -> Dict[str, str]:
     rc, text = _native_call("tkt_topology_labels_src", source, sysfs_root)
     if rc != 0:
@@ -155,6 +170,62 @@ def kfd_topology(root: str = KFD_TOPOLOGY) -> Dict[str, Any]:
     return {"source": "kfd", "gpus": gpus}
 
 
+def _read_text(path: str) -> Optional[str]:
+    try:
+        with open(path, "r", encoding="utf-8") as fh:
+            return fh.read().strip()
+    except OSError:
+        return None
+
+
+def rdma_nics(root: str = "") -> List[Dict[str, Any]]:
+    """RDMA devices under ``<root>/sys/class/infiniband`` (the inter-node RCCL fabric).
+
+    Mirror of ``csrc/tk_topo.cpp:collect_nics``: the first ACTIVE port of each device,
+    its link layer (``InfiniBand`` / ``Ethernet`` = RoCE) and rate, the netdev and PCI
+    function behind it, and its NUMA node."""
+    base = os.path.join(root or "/", "sys/class/infiniband")
+    try:
+        names = sorted(n for n in os.listdir(base) if not n.startswith("."))
+    except OSError:
+        return []
+    out: List[Dict[str, Any]] = []
+    for name in names:
+        dev = os.path.join(base, name)
+        nic: Dict[str, Any] = {"name": name, "port": 0, "active": False, "link_layer": "", "rate_gbps": 0}
+        ports_dir = os.path.join(dev, "ports")
+        try:
+            ports = sorted(int(p) for p in os.listdir(ports_dir) if p.isdigit())
+        except OSError:
+            ports = []
+        for port in ports:
+            pd = os.path.join(ports_dir, str(port))
+            state = _read_text(os.path.join(pd, "state")) or ""
+            if "ACTIVE" not in state:
+                if not nic["link_layer"]:
+                    nic["link_layer"] = _read_text(os.path.join(pd, "link_layer")) or ""
+                continue
+            nic.update(port=port, active=True, link_layer=_read_text(os.path.join(pd, "link_layer")) or "")
+            rate = (_read_text(os.path.join(pd, "rate")) or "").split()
+            nic["rate_gbps"] = int(rate[0]) if rate and rate[0].isdigit() else 0
+            break
+        try:
+            nets = sorted(n for n in os.listdir(os.path.join(dev, "device", "net")) if not n.startswith("."))
+        except OSError:
+            nets = []
+        if nets:
+            nic["netdev"] = nets[0]
+        try:
+            nic["bdf"] = os.path.basename(os.readlink(os.path.join(dev, "device")))
+        except OSError:
+            pass
+        numa = _read_text(os.path.join(dev, "device", "numa_node"))
+        if numa is not None and numa.lstrip("-").isdigit():
+            nic["numa_node"] = int(numa)
+        out.append(nic)
+    return out
+
+
 def discover(kfd_root: Optional[str] = None, prefer: str = "sysfs") -> Dict[str, Any]:
     """Best-effort topology: native sysfs (or amd_smi), the other native source, Python KFD, empty."""
     if kfd_root is None:
@@ -168,5 +239,7 @@ def discover(kfd_root: Optional[str] = None, prefer: str = "sysfs") -> Dict[str,
                 continue
     root = kfd_root or KFD_TOPOLOGY
     if os.path.isdir(root):
-        return kfd_topology(root)
-    return {"source": "none", "gpus": []}
+        doc = kfd_topology(root)
+        doc["nics"] = rdma_nics("" if kfd_root is None else os.path.join(kfd_root, *[".."] * 6))
+        return doc
+    return {"source": "none", "gpus": [], "nics": rdma_nics() if kfd_root is None else []}

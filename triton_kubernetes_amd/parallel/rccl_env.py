@@ -6,11 +6,13 @@ GPU pods by the device-plugin / addon manifests.
 Intra-node traffic on an 8xMI355X node is xGMI, point-to-point: each GPU has 7
 links of roughly 153 GB/s, so ring collectives are per-link bound and RCCL
 needs no socket/IB settings for it.  Inter-node traffic goes over RoCE/IB NICs
-whose names are site specific: ``NCCL_SOCKET_IFNAME`` / ``NCCL_IB_HCA`` are only
-written when configured (``rccl_env`` overrides in the node config).
+whose names are site specific: the node's active RDMA ports are discovered on the
+host (:func:`site_env_from_topology`, ``amdgpu-topo-labeller --rccl-env``) and written
+as ``NCCL_IB_HCA`` (+ the RoCE v2 GID index); ``rccl_env`` overrides in the node
+config win over both the defaults and the discovered values.
 """
 
-from typing import Dict, Mapping
+from typing import Any, Dict, Mapping
 
 # Values chosen for MI355X nodes; every one can be overridden per node.
 _DEFAULTS: Dict[str, str] = {
@@ -27,6 +29,20 @@ _DEFAULTS: Dict[str, str] = {
 }
 
 SITE_KEYS = ("NCCL_SOCKET_IFNAME", "NCCL_IB_HCA", "NCCL_IB_GID_INDEX", "NCCL_NET_GDR_LEVEL")
+
+
+def site_env_from_topology(topology: Mapping[str, Any]) -> Dict[str, str]:
+    """Inter-node settings derived from the node's RDMA NICs (``topology["nics"]``, as
+    discovered by the labeller): every active port in ``NCCL_IB_HCA`` (exact names), and
+    the RoCE v2 GID index when any of them is Ethernet.  Mirror of
+    ``csrc/tk_topo.cpp:render_rccl_env``; explicit per-node ``rccl_env`` keys override it."""
+    active = [n for n in topology.get("nics", []) or [] if n.get("port", 0) > 0]
+    if not active:
+        return {}
+    env = {"NCCL_IB_HCA": "=" + ",".join(f"{n['name']}:{n['port']}" for n in active)}
+    if any(str(n.get("link_layer", "")).lower() == "ethernet" for n in active):
+        env["NCCL_IB_GID_INDEX"] = "3"
+    return env
 
 
 def default_rccl_env() -> Dict[str, str]:

@@ -189,9 +189,10 @@ $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/
 %{ if gpu_burnin != "off" ~}
 $T/gpu-burnin --all --level '${gpu_burnin}' | sudo tee /etc/triton-kubernetes/gpu-burnin.json
 %{ endif ~}
-sudo tee /etc/rccl/rccl.env >/dev/null <<'TK_RCCL_EOF'
+{ $T/amdgpu-topo-labeller --rccl-env || true; cat <<'TK_RCCL_EOF'
 ${rccl_env_file}
 TK_RCCL_EOF
+} | sudo tee /etc/rccl/rccl.env >/dev/null
 %{ if gpu_count > 1 ~}
 set -a; . /etc/rccl/rccl.env; set +a
 $T/rccl-ready --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
