@@ -3,6 +3,7 @@
 import base64
 import hashlib
 import json
+import subprocess
 import time
 
 import pytest
@@ -121,7 +122,7 @@ def test_waiter_times_out_on_missing_node(rancher):
     assert set(rep.phases) == {"cluster_active", "nodes_ready"} and rep.ready_seconds >= 0
 
 
-def test_gpu_job_manifest_affinity():
+def test_gpu_job_manifest_affinity(tmp_path):
     job = gpu_job_manifest("train", "img", ["run"], gpus_per_pod=8, pods=4)
     pod = job["spec"]["template"]["spec"]
     exprs = pod["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][
@@ -133,6 +134,16 @@ def test_gpu_job_manifest_affinity():
     assert term["topologyKey"] == "amd.com/xgmi.hive-id"
     assert pod["containers"][0]["resources"]["limits"]["amd.com/gpu"] == "8"
     assert pod["containers"][0]["envFrom"] == [{"configMapRef": {"name": "rccl-env"}}]
+    # the node's own RCCL file (discovered RDMA ports) is sourced over the ConfigMap
+    cmd = pod["containers"][0]["command"]
+    assert cmd[:2] == ["/bin/sh", "-c"] and cmd[3:] == ["run"] and ". /etc/rccl/rccl.env" in cmd[2]
+    assert pod["volumes"][0]["hostPath"]["path"] == "/etc/rccl"
+    env_file = tmp_path / "rccl.env"
+    env_file.write_text('NCCL_IB_HCA="=mlx5_0:1"\n')
+    out = subprocess.run(["/bin/sh", "-c", cmd[2].replace("/etc/rccl/rccl.env", str(env_file)), "sh", "-c",
+                          'echo "$NCCL_IB_HCA $NCCL_DEBUG"'], capture_output=True, text=True,
+                         env={"NCCL_DEBUG": "WARN", "PATH": "/usr/bin:/bin"}, check=True).stdout
+    assert out.strip() == "=mlx5_0:1 WARN"
     single = gpu_job_manifest("one", "img", ["x"], gpus_per_pod=1)["spec"]["template"]["spec"]["affinity"]
     assert "podAffinity" not in single
     assert len(single["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"]["nodeSelectorTerms"][0][

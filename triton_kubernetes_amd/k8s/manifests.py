@@ -83,6 +83,10 @@ def rccl_configmap(env: Optional[Dict[str, str]] = None) -> Dict[str, Any]:
             "data": dict(env or default_rccl_env())}
 
 
+# sources the node's /etc/rccl/rccl.env (if any) over the ConfigMap env, then execs the command
+NODE_ENV_WRAPPER = 'set -a; [ -r /etc/rccl/rccl.env ] && . /etc/rccl/rccl.env; set +a; exec "$0" "$@"'
+
+
 def gpu_job_manifest(name: str, image: str, command: List[str], gpus_per_pod: int = 8, pods: int = 1,
                      namespace: str = "default", hive_affinity: bool = True) -> Dict[str, Any]:
     """A Job whose pods each take ``gpus_per_pod`` GPUs of one fully connected xGMI hive."""
@@ -111,11 +115,16 @@ def gpu_job_manifest(name: str, image: str, command: List[str], gpus_per_pod: in
                     "restartPolicy": "Never",
                     "affinity": affinity,
                     "containers": [{
-                        "name": "main", "image": image, "command": command,
+                        "name": "main", "image": image,
+                        # cluster defaults come from the ConfigMap; the node's own file (its
+                        # discovered RDMA ports, per-node overrides) is sourced on top
+                        "command": ["/bin/sh", "-c", NODE_ENV_WRAPPER, command[0]] + list(command[1:]),
                         "envFrom": [{"configMapRef": {"name": "rccl-env"}}],
                         "resources": {"limits": {"amd.com/gpu": str(gpus_per_pod)}},
                         "securityContext": {"capabilities": {"add": ["SYS_PTRACE"]}},
+                        "volumeMounts": [{"name": "rccl-env", "mountPath": "/etc/rccl", "readOnly": True}],
                     }],
+                    "volumes": [{"name": "rccl-env", "hostPath": {"path": "/etc/rccl", "type": "DirectoryOrCreate"}}],
                     "hostIPC": True,
                 },
             },
