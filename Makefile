@@ -5,7 +5,7 @@ PYTHON     ?= python3
 BUILD      := build
 PKG        := triton_kubernetes_amd
 
-.PHONY: all native modules test test-gpu bench smoke dist pyz wheel checksums clean
+.PHONY: all native modules test test-gpu sanitize bench smoke dist pyz wheel checksums clean
 
 all: native test
 
@@ -19,6 +19,10 @@ modules:
 
 test:
 	$(PYTHON) -m pytest tests -x -q -m "not gpu"
+
+# host-code memory/UB checks of the native labeller (ASan + UBSan build over a fixture tree)
+sanitize:
+	$(PYTHON) -m pytest tests/test_topology_native.py -q -k asan
 
 # on an MI355X box
 test-gpu: native

@@ -205,3 +205,34 @@ def test_agent_rccl_env_merges_discovered_nics(tmp_path):
     assert res["labels"]["amd.com/rdma.count"] == "2"
     step = next(s for s in res["steps"] if s["name"] == "rccl_env")
     assert step["detail"]["discovered"] == ["NCCL_IB_GID_INDEX", "NCCL_IB_HCA"]
+
+
+def test_labeller_clean_under_asan_ubsan(tmp_path):
+    """Race/memory-safety check of the native labeller's host code (the
+    reference has none): the sysfs collector built with AddressSanitizer + UBSan runs the
+    JSON, --labels and --rccl-env paths over the fixture tree (GPUs + RDMA NICs) with no
+    sanitizer report and the same output as the regular build."""
+    import shutil
+
+    gxx = shutil.which("g++")
+    if gxx is None:
+        pytest.skip("g++ not available")
+    src = os.path.join(os.path.dirname(topo.__file__), "csrc", "tk_topo.cpp")
+    exe = str(tmp_path / "labeller-asan")
+    build = subprocess.run([gxx, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
+                            "-fno-sanitize-recover=all", "-DTK_TOPO_MAIN", src, "-o", exe],
+                           capture_output=True, text=True)
+    assert build.returncode == 0, build.stderr[-2000:]
+    root = add_rdma(make_tree(str(tmp_path / "root"), ngpu=8, ue={3: 2}), RDMA)
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
+    env.pop("LD_PRELOAD", None)
+    ref = executable("amdgpu-topo-labeller") if os.path.exists(os.path.join(
+        os.path.dirname(topo.__file__), "lib", "amdgpu-topo-labeller")) else None
+    for args in ([], ["--labels"], ["--rccl-env"]):
+        argv = args + (["--source", "sysfs"] if args != ["--rccl-env"] else []) + ["--sysfs-root", root]
+        run = subprocess.run([exe] + argv, capture_output=True, text=True, env=env)
+        assert run.returncode == 0, run.stderr[-3000:]
+        assert "Sanitizer" not in run.stderr and "runtime error" not in run.stderr, run.stderr[-3000:]
+        if ref:
+            want = subprocess.run([ref] + argv, capture_output=True, text=True).stdout
+            assert run.stdout == want
