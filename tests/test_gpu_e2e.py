@@ -58,3 +58,54 @@ def test_real_gpu_bringup(tmp_path):
         w.stop()
         cp.stop()
         fake.stop()
+
+
+def _stub(bindir, name, body):
+    p = bindir / name
+    p.write_text("#!/bin/bash\n" + body + "\n")
+    p.chmod(0o755)
+
+
+def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
+    """The SSH path's rendered bash bootstrap, run for real on the box: the native tools
+    (gpu-burnin, amdgpu-topo-labeller incl. --rccl-env) from ops/lib, /etc relocated under
+    tmp_path, and only sudo/docker/systemctl/hostnamectl/usermod/lsmod stubbed (no root
+    and no container runtime on the box)."""
+    import os
+    import subprocess
+
+    from triton_kubernetes_amd.node.plan import TOOLS_DIR, build_host_plan, parse_step_markers
+    from triton_kubernetes_amd.ops.native import LIB_DIR
+    from triton_kubernetes_amd.parallel.rccl_env import parse_env_file
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "calls.log"
+    _stub(bindir, "sudo", 'exec "$@"')
+    for name in ("docker", "systemctl", "hostnamectl", "usermod"):
+        _stub(bindir, name, f'echo "{name} $*" >> {log}')
+    _stub(bindir, "lsmod", "echo 'Module Size Used by'; test -c /dev/kfd && echo 'amdgpu 1 0'")
+    etc = tmp_path / "etc"
+    (etc / "docker").mkdir(parents=True)
+    cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1, "gpu_burnin": "quick",
+           "rccl_env": {"NCCL_DEBUG": "WARN"}}
+    plan = build_host_plan(cfg, "https://rancher.example", "regtok", "cafe", mi355x=True)
+    script = plan.render_shell().replace("/etc/", f"{etc}/").replace(TOOLS_DIR, LIB_DIR)
+    env = dict(os.environ, PATH=f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
+    proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=300)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    steps = parse_step_markers(proc.stdout)
+    print("\n".join(ln for ln in proc.stdout.splitlines() if "tk-step" in ln))
+    assert all(steps.get(n, {}).get("status") == "ok" for n in plan.step_names()), steps
+    burn = json.loads((etc / "triton-kubernetes/gpu-burnin.json").read_text())
+    assert burn["ok"] and burn["gpus"] and all(g["ok"] for g in burn["gpus"]), burn
+    labels = dict(ln.split("=", 1) for ln in (etc / "triton-kubernetes/gpu-labels").read_text().splitlines())
+    assert labels["amd.com/gpu.count"] == "1" and labels["amd.com/gpu.target"] == "gfx950"
+    rccl = parse_env_file((etc / "rccl/rccl.env").read_text())
+    assert rccl["NCCL_DEBUG"] == "WARN"
+    if int(labels.get("amd.com/rdma.count", "0")) > 0:  # the box's RDMA ports land in the env
+        assert rccl["NCCL_IB_HCA"].startswith("=")
+    calls = log.read_text()
+    assert "hostnamectl set-hostname gpu-1" in calls
+    assert "--ca-checksum cafe --worker" in calls and "--label amd.com/gpu.product-name=MI355X" in calls
+    print(json.dumps({"steps": steps, "rccl_env": rccl}))

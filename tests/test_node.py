@@ -267,3 +267,17 @@ def test_presize_fd_table_and_procstat():
     assert 0 < n <= 4096
     assert fd < 64  # the lowest free descriptor is still handed out first
     assert out[2:] == ["True", "True", "True", "True"]
+
+
+def test_step_markers_name_steps_whose_bodies_assign_variables(tmp_path):
+    """Regression (found running the rendered bootstrap on an MI355X box): a step body that
+    assigns a variable named like a _tk_step local (bash scoping is dynamic) must not rename
+    the step in its ::tk-step markers."""
+    from triton_kubernetes_amd.node.plan import Step
+
+    plan = build_host_plan(WORKER, "https://r", "t", "s", mi355x=False)
+    plan.steps = [Step("clobber", "firewall", "n=1; t0=2; rc=3; name=4; true"), Step("after", "hostname", "true")]
+    proc = subprocess.run(["bash", "-s"], input=plan.render_shell(), capture_output=True, text=True, check=False)
+    assert proc.returncode == 0, proc.stderr
+    steps = parse_step_markers(proc.stdout)
+    assert list(steps) == ["clobber", "after"] and all(v["status"] == "ok" for v in steps.values())

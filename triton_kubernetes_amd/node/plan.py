@@ -82,9 +82,13 @@ class BootstrapPlan:
             f"# triton-kubernetes node bootstrap: {self.hostname} ({self.role})",
             "set -euo pipefail",
             "_tk_now() { date +%s%3N; }",
-            "_tk_step() { local n=$1; shift; local t0; t0=$(_tk_now); echo \"::tk-step $n start 0\";",
-            "  if \"$@\"; then echo \"::tk-step $n ok $(( $(_tk_now) - t0 ))\";",
-            "  else local rc=$?; echo \"::tk-step $n failed $(( $(_tk_now) - t0 ))\" >&2; exit $rc; fi; }",
+            # step bodies run inside _tk_step (bash scoping is dynamic): its locals carry a
+            # prefix no step body uses, so a body assigning e.g. `n=` cannot rename the step
+            "_tk_step() { local _tk_name=$1; shift; local _tk_t0; _tk_t0=$(_tk_now);",
+            "  echo \"::tk-step $_tk_name start 0\";",
+            "  if \"$@\"; then echo \"::tk-step $_tk_name ok $(( $(_tk_now) - _tk_t0 ))\";",
+            "  else local _tk_rc=$?; echo \"::tk-step $_tk_name failed $(( $(_tk_now) - _tk_t0 ))\" >&2;",
+            "    exit $_tk_rc; fi; }",
         ]
         for s in self.steps:
             body = s.shell.strip("\n")
@@ -180,8 +184,9 @@ fi""", {"install_url": install_url}))
 lsmod | grep -q '^amdgpu' || {{ echo 'amdgpu kernel module not loaded' >&2; exit 1; }}
 test -c /dev/kfd || {{ echo '/dev/kfd missing' >&2; exit 1; }}
 test -d /dev/dri || {{ echo '/dev/dri missing' >&2; exit 1; }}
-n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
-[ "$n" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs, found $n render nodes" >&2; exit 1; }}
+local found
+found=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
+[ "$found" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs, found $found render nodes" >&2; exit 1; }}
 sudo usermod -aG video,render "$(id -un)" || true""", {"count": ngpu}, gpu=True))
         # burn-in before labels: the agent discovers the topology concurrently
         # with the burn-in kernels and only joins it at the labels step
