@@ -109,3 +109,73 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
     assert "hostnamectl set-hostname gpu-1" in calls
     assert "--ca-checksum cafe --worker" in calls and "--label amd.com/gpu.product-name=MI355X" in calls
     print(json.dumps({"steps": steps, "rccl_env": rccl}))
+
+
+def _templatefile(text: str, values: dict) -> str:
+    """Enough of Terraform's templatefile() for the host scripts: ${var}, $${ escapes and
+    single-level %{ if <cond> ~} ... %{ endif ~} blocks (conditions use == != > with
+    variables and literals)."""
+    import re
+
+    out, keep = [], [True]
+    for line in text.splitlines():
+        m = re.match(r"^\s*%\{\s*if\s+(.*?)\s*~?\}\s*$", line)
+        if m:
+            cond = re.sub(r"\b([A-Za-z_][A-Za-z0-9_]*)\b", lambda v: repr(values[v.group(1)])
+                          if v.group(1) in values else v.group(1), m.group(1))
+            keep.append(keep[-1] and bool(eval(cond, {"__builtins__": {}})))  # noqa: S307 - test-owned input
+            continue
+        if re.match(r"^\s*%\{\s*endif\s*~?\}\s*$", line):
+            keep.pop()
+            continue
+        if keep[-1]:
+            out.append(line)
+    body = ("\n".join(out) + "\n").replace("$${", "\x00")
+    body = re.sub(r"\$\{([A-Za-z_][A-Za-z0-9_]*)\}", lambda m: str(values[m.group(1)]), body)
+    return body.replace("\x00", "${")
+
+
+def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
+    """The bare-metal-mi355x-rancher-k8s-host module's host script (what Terraform's
+    remote-exec runs), rendered like templatefile() and run on the box: it builds the
+    native tools from the shipped sources with hipcc/g++ on the node, then labels, burn-in,
+    RCCL env and the agent command.  Paths relocated under tmp_path; sudo/docker/
+    hostnamectl/usermod/lsmod stubbed."""
+    import os
+    import subprocess
+
+    from triton_kubernetes_amd.ops.build import CSRC
+    from triton_kubernetes_amd.parallel.rccl_env import parse_env_file
+    from triton_kubernetes_amd.terraform.generate import MODULES_DIR
+
+    tpl = open(os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files",
+                            "install_mi355x_node.sh.tftpl"), encoding="utf-8").read()
+    values = {"gpu_count": 1, "gpu_burnin": "quick", "rccl_env_file": 'NCCL_DEBUG="INFO"', "rccl_min_busbw": 0,
+              "docker_engine_install_url": "https://example.invalid/docker.sh", "hostname": "gpu-tf-1",
+              "rancher_registry_username": "", "rancher_registry_password": "", "rancher_registry": "",
+              "rancher_agent_image": "rancher/rancher-agent:v2.8.5", "rancher_api_url": "https://rancher.example",
+              "rancher_cluster_registration_token": "regtok", "rancher_cluster_ca_checksum": "cafe",
+              "rancher_node_role": "worker"}
+    tools, etc = tmp_path / "tools", tmp_path / "etc"
+    script = (_templatefile(tpl, values).replace("/opt/triton-kubernetes/bin", str(tools))
+              .replace("/opt/triton-kubernetes/src", CSRC).replace("/etc/", f"{etc}/"))
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "calls.log"
+    _stub(bindir, "sudo", 'exec "$@"')
+    for name in ("docker", "hostnamectl", "usermod"):
+        _stub(bindir, name, f'echo "{name} $*" >> {log}')
+    _stub(bindir, "lsmod", "echo 'Module Size Used by'; test -c /dev/kfd && echo 'amdgpu 1 0'")
+    env = dict(os.environ, PATH=f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
+    proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=280)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    for exe in ("amdgpu-topo-labeller", "gpu-burnin", "rccl-ready"):
+        assert os.access(tools / exe, os.X_OK), exe  # built on the node from the shipped sources
+    burn = json.loads((etc / "triton-kubernetes/gpu-burnin.json").read_text())
+    assert burn["ok"], burn
+    labels = (etc / "triton-kubernetes/gpu-labels").read_text()
+    assert "amd.com/gpu.product-name=MI355X" in labels
+    assert parse_env_file((etc / "rccl/rccl.env").read_text())["NCCL_DEBUG"] == "INFO"
+    calls = log.read_text()
+    assert "hostnamectl set-hostname gpu-tf-1" in calls
+    assert "--token regtok --ca-checksum cafe --worker --label amd.com/" in calls
