@@ -179,3 +179,38 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     calls = log.read_text()
     assert "hostnamectl set-hostname gpu-tf-1" in calls
     assert "--token regtok --ca-checksum cafe --worker --label amd.com/" in calls
+
+
+def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch):
+    """The production node agent mode (``exec``) over HTTP on the box: GPU steps run in
+    process (arena burn-in, sysfs labels, discovered RCCL env), runtime/agent steps run
+    their fixed argv against stubbed docker/hostnamectl (no container runtime on the box)."""
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.parallel.transport import AgentTransport, HostRef
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "calls.log"
+    _stub(bindir, "docker", f'echo "docker $*" >> {log}; [ "$1" = version ] && echo 24.0.7; exit 0')
+    _stub(bindir, "hostnamectl", f'echo "hostnamectl $*" >> {log}')
+    import os
+
+    monkeypatch.setenv("PATH", f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
+    agent = NodeAgent(name="w-exec", mode="exec", devices=[0], token="exec-token-123456", root=str(tmp_path / "root"))
+    url = agent.serve()
+    try:
+        cfg = {"hostname": "gpu-exec-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
+               "gpu_burnin": "quick", "rccl_env": {"NCCL_DEBUG": "WARN"}}
+        plan = build_host_plan(cfg, "https://rancher.example", "regtok123", "cafe0123", mi355x=True)
+        res = AgentTransport(token="exec-token-123456").run_plan(HostRef("agent+" + url), plan)
+    finally:
+        agent.stop()
+    assert res["ok"], res
+    names = [s["name"] for s in res["steps"]]
+    assert names == plan.step_names() and all(s["ok"] for s in res["steps"])
+    calls = log.read_text()
+    assert "hostnamectl set-hostname gpu-exec-1" in calls and "docker version" in calls
+    assert "--ca-checksum cafe0123 --worker --label amd.com/" in calls and "--label amd.com/gpu.count=1" in calls
+    assert (tmp_path / "root/etc/rccl/rccl.env").read_text().count("NCCL_DEBUG") == 1
+    print(json.dumps({s["name"]: round(s["ms"], 2) for s in res["steps"]}))
