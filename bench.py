@@ -17,7 +17,7 @@ waiter reports every phase done:
 * every worker advertises ``amd.com/gpu`` (device-plugin add-on applied);
 * per-GPU burn-in passed on each worker (HBM3E stream, bf16 + fp8 MFMA, memtest —
   hand-written gfx950 HIP kernels, run for real) and its topology labels
-  (amd_smi via the native labeller) attached at registration;
+  (KFD sysfs via the in-process native labeller, plus RDMA NICs) attached at registration;
 * a cluster-wide RCCL all-reduce gate across all N GPUs (native RCCL over xGMI).
 
 What is simulated (and therefore excluded): the Rancher server is the
@@ -228,8 +228,9 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "bf16",
             "data": ("SIM-GPU DRY RUN (not a measurement); " if args.sim_gpu else "") + ("synthetic: in-process Rancher v3 fake (RKE provisioning not simulated) and sim-mode host "
-                     "runtime steps; GPU steps real on MI355X (amd_smi topology labels, HBM/MFMA/memtest burn-in "
-                     f"level={args.burnin}, cluster-wide RCCL all-reduce gate {'off' if args.no_rccl_gate else 'on'})"),
+                     "runtime steps; GPU steps real on MI355X (native KFD-sysfs topology + RDMA labels, HBM/MFMA/memtest "
+                     f"burn-in level={args.burnin} through the agent's resident buffers, cluster-wide RCCL all-reduce "
+                     f"gate {'off' if args.no_rccl_gate else 'on'}: a fresh communicator per create)"),
             "config": {
                 "model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology labels",
                 "workers": world, "gpus_per_worker": 1, "control_plane_nodes": 2,
