@@ -6,6 +6,7 @@ Targets (gfx950 only; ``hipcc`` cross-compiles without a GPU):
 artifact                       source                                      toolchain
 =============================  ==========================================  =========
 ``libtk_gpu_probe.so``         ``csrc/tk_gpu_probe.hip`` (HBM/MFMA/memtest)  hipcc
+``libtk_gemm.so``              ``csrc/tk_gemm_screen.hip`` (ABFT GEMM screen)  hipcc
 ``libtk_rccl.so``              ``csrc/tk_rccl_probe.hip`` (N2, RCCL)          hipcc
 ``rccl-ready``                 same, ``-DTK_RCCL_MAIN``                     hipcc
 ``libtk_topo.so``              ``csrc/tk_topo.cpp`` (N1, sysfs collector)    g++
@@ -63,6 +64,7 @@ def targets() -> List[Target]:
     hipcc = _hipcc()
     probe = os.path.join(CSRC, "tk_gpu_probe.hip")
     rccl = os.path.join(CSRC, "tk_rccl_probe.hip")
+    gemm = os.path.join(CSRC, "tk_gemm_screen.hip")
     topo = os.path.join(CSRC, "tk_topo.cpp")
     out = lambda n: os.path.join(LIB, n)  # noqa: E731
     return [
@@ -70,6 +72,8 @@ def targets() -> List[Target]:
                [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-fPIC", "-shared", probe, "-o", out("libtk_gpu_probe.so"), *RPATH]),
         Target("gpu-burnin", [probe],
                [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-DTK_PROBE_MAIN", probe, "-o", out("gpu-burnin"), *RPATH]),
+        Target("libtk_gemm.so", [gemm],
+               [hipcc, *HIP_FLAGS, "-fPIC", "-shared", gemm, "-o", out("libtk_gemm.so"), *RPATH]),
         Target("libtk_rccl.so", [rccl],
                [hipcc, *HIP_FLAGS, "-fPIC", "-shared", rccl, "-o", out("libtk_rccl.so"), f"-L{ROCM}/lib",
                 "-lrccl", *RPATH]),

@@ -1,0 +1,409 @@
+// MI355X GEMM silent-data-corruption screen (burn-in step `gemm`).
+//
+// The MFMA peak loops in tk_gpu_probe.hip prove the matrix cores ISSUE at rate, but they
+// never check a result.  This screen runs a real LDS-tiled bf16 GEMM — HBM -> LDS (async
+// global_load_lds) -> VGPR fragments -> v_mfma_f32_16x16x32_bf16 — and verifies it with
+// algorithm-based fault tolerance (Huang & Abraham): for C = A * B^T,
+//
+//     sum_m C[m][n] = sum_k (sum_m A[m][k]) * B[n][k]      (column checksums)
+//     sum_n C[m][n] = sum_k A[m][k] * (sum_n B[n][k])      (row checksums)
+//
+// The GEMM epilogue reduces its accumulator tile to per-wave column/row partial sums in
+// registers (no C store in screen mode), and independent fp32 SIMT kernels compute the
+// right-hand sides from A and B.  A corrupted product — a bad MFMA, LDS or VGPR bit, a
+// wrong staged tile — shows up as a column AND a row mismatch, which also locates it.
+//
+// Kernel structure (gfx950, one 256x256 output tile per 512-thread workgroup):
+//  * 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 of C as 8 x 4 fragments of
+//    16x16 (32 f32x4 accumulators);
+//  * K in steps of 64: A and B tiles [256][64] bf16 (32 KiB each) are staged into LDS
+//    with 16-byte global_load_lds (8 per thread per step), two LDS buffers so the copy
+//    of step t+1 overlaps the MFMAs of step t;
+//  * the LDS image is XOR-swizzled by 16-byte chunk (chunk ^ ((row >> 1) & 7)): the
+//    swizzle is applied to the per-lane GLOBAL source address (the LDS-DMA destination
+//    is lane-linear), so the 16 lanes of a ds_read_b128 group read 16 distinct bank
+//    slots (row stride 128 B would otherwise give an 8-way conflict);
+//  * blocks are remapped so the tiles one XCD works on share A rows / B columns in its
+//    own L2 (blocks are dispatched round-robin over the 8 XCDs);
+//  * shapes: M, N multiples of 256, K a multiple of 64 — checked on the host before any
+//    launch (no bounds checks inside the tile loops).
+//
+// C ABI for ctypes: triton_kubernetes_amd/ops/gemm.py.
+
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cmath>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+
+static thread_local char g_err[512];
+
+static int set_err(const char* what, hipError_t e) {
+  snprintf(g_err, sizeof(g_err), "%s: %s (%d)", what, hipGetErrorString(e), (int)e);
+  return (int)e == 0 ? -1 : (int)e;
+}
+
+#define CHECK(call)                                  \
+  do {                                               \
+    hipError_t _e = (call);                          \
+    if (_e != hipSuccess) return set_err(#call, _e); \
+  } while (0)
+
+extern "C" const char* tkg_last_error() { return g_err; }
+
+namespace {
+constexpr int BM = 256, BN = 256, BK = 64;
+constexpr int WAVES_M = 2, WAVES_N = 4, THREADS = 64 * WAVES_M * WAVES_N;  // 512
+constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;                       // 128 x 64 per wave
+constexpr int FM = WM / 16, FN = WN / 16;                                 // 8 x 4 fragments
+constexpr int TILE_BYTES = BM * BK * 2;                                   // 32 KiB per operand tile
+constexpr int STAGE_BYTES = 2 * TILE_BYTES;                               // A + B
+constexpr int LDS_BYTES = 2 * STAGE_BYTES;                                // double buffered: 128 KiB
+constexpr int GLDS_PER_TILE = TILE_BYTES / (THREADS * 16);                // 4 per thread per operand
+
+// physical 16-byte chunk of logical chunk `c` in row `r` of a [rows][64] bf16 image
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+
+// Stage one [256][64] bf16 tile (rows row0.., k0..k0+63 of a K-contiguous matrix) into
+// LDS at `lds` (wave-uniform base + lane*16 per instruction; the swizzle goes on the source).
+__device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld, int row0, int k0, char* lds,
+                                           int tid) {
+#pragma unroll
+  for (int i = 0; i < GLDS_PER_TILE; ++i) {
+    const int slot = i * THREADS + tid;  // 16-byte slot of the image, lane-linear per wave
+    const int r = slot >> 3, cp = slot & 7;
+    const int c = cp ^ ((r >> 1) & 7);   // logical chunk this physical slot holds (XOR is an involution)
+    const __bf16* src = g + (size_t)(row0 + r) * ld + k0 + c * 8;
+    // LDS destination of lane 0 of this wave-instruction; lanes follow at +16 B
+    char* dst = lds + (size_t)(i * THREADS + (tid & ~63)) * 16;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), reinterpret_cast<__shared__ void*>(dst), 16,
+                                     0, 0);
+  }
+}
+
+__device__ __forceinline__ bf16x8 lds_frag(const char* img, int r, int c) {
+  return *reinterpret_cast<const bf16x8*>(img + r * 128 + swz(r, c) * 16);
+}
+
+// XCD-aware, bijective block -> tile map: blocks b, b+8, b+16.. run on one XCD; give each
+// XCD a contiguous range of tiles, walked in groups of GROUP_M tile-rows so neighbouring
+// blocks on an XCD share A rows and B columns in that XCD's L2.
+__device__ __forceinline__ void tile_of(int b, int nwg, int tiles_m, int tiles_n, int* tm, int* tn) {
+  const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
+  const int w = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
+  constexpr int GROUP_M = 8;
+  const int per_group = GROUP_M * tiles_n;
+  const int g = w / per_group, first_m = g * GROUP_M;
+  const int rows = min(tiles_m - first_m, GROUP_M);
+  const int in = w - g * per_group;
+  *tm = first_m + in % rows;
+  *tn = in / rows;
+}
+}  // namespace
+
+// mode 0: write C (fp32, row-major [M][N]); mode 1: screen — per-wave checksums only:
+// colpart[(tm*WAVES_M + wr)][n] = sum over the wave's 128 rows, rowpart[(tn*WAVES_N + wc)][m]
+// = sum over the wave's 64 columns.  inject >= 0 adds 1024.0 to the element C[inject/N][inject%N]
+// before the reduction (fault-injection self-test of the screen).
+template <int MODE>
+__global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                     float* __restrict__ C, float* __restrict__ colpart,
+                                                     float* __restrict__ rowpart, int M, int N, int K,
+                                                     long long inject) {
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid / WAVES_N, wc = wid % WAVES_N;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  int tm, tn;
+  tile_of(blockIdx.x, gridDim.x, tiles_m, tiles_n, &tm, &tn);
+  const int row0 = tm * BM, col0 = tn * BN;
+
+  f32x4 acc[FM][FN];
+#pragma unroll
+  for (int i = 0; i < FM; ++i)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BK;
+  stage_tile(A, K, row0, 0, smem, tid);
+  stage_tile(B, K, col0, 0, smem + TILE_BYTES, tid);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  const int fr = lane & 15, fq = lane >> 4;  // fragment row/col within 16, k-chunk group
+  for (int t = 0; t < nk; ++t) {
+    const char* cur = smem + (t & 1) * STAGE_BYTES;
+    if (t + 1 < nk) {  // next K-step into the other buffer (last read before the previous barrier)
+      char* nxt = smem + ((t + 1) & 1) * STAGE_BYTES;
+      stage_tile(A, K, row0, (t + 1) * BK, nxt, tid);
+      stage_tile(B, K, col0, (t + 1) * BK, nxt + TILE_BYTES, tid);
+    }
+    const char* a_img = cur;
+    const char* b_img = cur + TILE_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 bf[FN];
+#pragma unroll
+      for (int j = 0; j < FN; ++j) bf[j] = lds_frag(b_img, wc * WN + j * 16 + fr, kk * 4 + fq);
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int i = 0; i < FM; ++i) {
+        const bf16x8 af = lds_frag(a_img, wr * WM + i * 16 + fr, kk * 4 + fq);
+#pragma unroll
+        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
+      }
+      __builtin_amdgcn_s_setprio(0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next tile landed (this wave's share)
+    __syncthreads();                                   // ... everyone's; and `cur` is free again
+  }
+
+  // accumulator element (i, j, e): row = wr*WM + i*16 + fq*4 + e, col = wc*WN + j*16 + fr
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int i = 0; i < FM; ++i)
+#pragma unroll
+      for (int j = 0; j < FN; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int r = row0 + wr * WM + i * 16 + fq * 4 + e, c = col0 + wc * WN + j * 16 + fr;
+          C[(size_t)r * N + c] = acc[i][j][e];
+        }
+  } else {
+    if (inject >= 0) {
+      const long long ir = inject / N, ic = inject % N;
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (row0 + wr * WM + i * 16 + fq * 4 + e == ir && col0 + wc * WN + j * 16 + fr == ic) acc[i][j][e] += 1024.f;
+    }
+    // column sums over the wave's 128 rows: per lane over (i, e), then across the 4 lanes
+    // sharing a column (fq = 0..3 -> lanes fr, fr+16, fr+32, fr+48)
+#pragma unroll
+    for (int j = 0; j < FN; ++j) {
+      float s = 0.f;
+#pragma unroll
+      for (int i = 0; i < FM; ++i) s += acc[i][j][0] + acc[i][j][1] + acc[i][j][2] + acc[i][j][3];
+      s += __shfl_xor(s, 16, 64);
+      s += __shfl_xor(s, 32, 64);
+      if (fq == 0) colpart[(size_t)(tm * WAVES_M + wr) * N + col0 + wc * WN + j * 16 + fr] = s;
+    }
+    // row sums over the wave's 64 columns: per lane over j, then across the 16 lanes of a row group
+#pragma unroll
+    for (int i = 0; i < FM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float s = 0.f;
+#pragma unroll
+        for (int j = 0; j < FN; ++j) s += acc[i][j][e];
+        s += __shfl_xor(s, 1, 64);
+        s += __shfl_xor(s, 2, 64);
+        s += __shfl_xor(s, 4, 64);
+        s += __shfl_xor(s, 8, 64);
+        if (fr == 0) rowpart[(size_t)(tn * WAVES_N + wc) * M + row0 + wr * WM + i * 16 + fq * 4 + e] = s;
+      }
+    }
+  }
+}
+
+// --- checksum right-hand sides and comparison (fp32 SIMT, independent of the MFMA path) ----
+// out[k] += sum over this block's chunk of rows of X[r][k] (X is [rows][K] bf16); grid.y
+// splits the rows, partial sums meet in fp32 atomics (out / out_abs zeroed beforehand)
+constexpr int COLSUM_CHUNKS = 64;
+__global__ __launch_bounds__(256) void k_colsum_bf16(const __bf16* __restrict__ X, int rows, int K,
+                                                     float* __restrict__ out, float* __restrict__ out_abs) {
+  const int k = blockIdx.x * 256 + threadIdx.x;
+  if (k >= K) return;
+  const int per = (rows + gridDim.y - 1) / gridDim.y;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float s = 0.f, a = 0.f;
+  for (int r = r0; r < r1; ++r) {
+    const float v = (float)X[(size_t)r * K + k];
+    s += v;
+    a += fabsf(v);
+  }
+  atomicAdd(out + k, s);
+  atomicAdd(out_abs + k, a);
+}
+
+// expected[r] = sum_k X[r][k] * v[k]; bound[r] = sum_k |X[r][k]| * vabs[k]  (one wave per row)
+__global__ __launch_bounds__(256) void k_rowdot(const __bf16* __restrict__ X, int rows, int K, const float* __restrict__ v,
+                                                const float* __restrict__ vabs, float* __restrict__ expected,
+                                                float* __restrict__ bound) {
+  const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+  if (r >= rows) return;
+  float s = 0.f, b = 0.f;
+  for (int k = lane; k < K; k += 64) {
+    const float x = (float)X[(size_t)r * K + k];
+    s += x * v[k];
+    b += fabsf(x) * vabs[k];
+  }
+  for (int off = 32; off > 0; off >>= 1) {
+    s += __shfl_down(s, off, 64);
+    b += __shfl_down(b, off, 64);
+  }
+  if (lane == 0) {
+    expected[r] = s;
+    bound[r] = b;
+  }
+}
+
+// actual[x] = sum over `parts` partial rows; count |actual - expected| > rtol * bound + atol,
+// record the worst index and the largest normalised error
+__global__ __launch_bounds__(256) void k_compare(const float* __restrict__ part, int parts, int n,
+                                                 const float* __restrict__ expected, const float* __restrict__ bound,
+                                                 float rtol, float atol, unsigned int* __restrict__ bad,
+                                                 unsigned int* __restrict__ first_bad, float* __restrict__ max_err) {
+  const int x = blockIdx.x * 256 + threadIdx.x;
+  if (x >= n) return;
+  float s = 0.f;
+  for (int p = 0; p < parts; ++p) s += part[(size_t)p * n + x];
+  const float tol = rtol * bound[x] + atol;
+  const float err = fabsf(s - expected[x]);
+  if (!(err <= tol)) {  // NaN counts as bad
+    atomicAdd(bad, 1u);
+    atomicMin(first_bad, (unsigned int)x);
+  }
+  const float norm = err / tol;
+  // float max via int ordering (non-negative values)
+  atomicMax(reinterpret_cast<unsigned int*>(max_err), __float_as_uint(isnan(norm) ? 3.0e38f : norm));
+}
+
+// deterministic pseudo-random bf16 in [-1, 1)
+__global__ __launch_bounds__(256) void k_fill_bf16(__bf16* __restrict__ p, size_t n, uint32_t seed) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    uint32_t x = (uint32_t)i * 0x9e3779b9u ^ seed ^ (uint32_t)(i >> 32);
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    p[i] = (__bf16)(((x >> 8) * (1.0f / 8388608.0f)) - 1.0f);
+  }
+}
+
+static int check_shape(int M, int N, int K) {
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) {
+    snprintf(g_err, sizeof(g_err), "shape %dx%dx%d: M and N must be multiples of %d, K of %d", M, N, K, BM, BK);
+    return -1;
+  }
+  return 0;
+}
+
+static hipError_t launch_gemm(int mode, const __bf16* A, const __bf16* B, float* C, float* colpart, float* rowpart,
+                              int M, int N, int K, long long inject, hipStream_t s) {
+  const int grid = (M / BM) * (N / BN);
+  if (mode == 0) k_gemm_bt<0><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+  else k_gemm_bt<1><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+  return hipGetLastError();
+}
+
+static hipError_t set_lds_limit() {
+  static hipError_t once = [] {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_bt<0>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_bt<1>),
+                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+    return e;
+  }();
+  return once;
+}
+
+// C[M][N] (fp32) = A[M][K] * B[N][K]^T for device pointers on `dev` (tests: torch tensors).
+extern "C" int tkg_gemm_bt(int dev, const void* A, const void* B, void* C, int M, int N, int K) {
+  if (check_shape(M, N, K)) return -1;
+  CHECK(hipSetDevice(dev));
+  CHECK(set_lds_limit());
+  CHECK(launch_gemm(0, (const __bf16*)A, (const __bf16*)B, (float*)C, nullptr, nullptr, M, N, K, -1, 0));
+  CHECK(hipDeviceSynchronize());
+  return 0;
+}
+
+// The screen: random A[M][K], B[N][K]; `reps` timed checksum-mode GEMMs (best time), then the
+// ABFT comparison of the last one.  inject >= 0 corrupts C[inject/N][inject%N] (self-test).
+// out[0] TFLOP/s (best rep), out[1] ms of that rep, out[2] bad columns, out[3] bad rows,
+// out[4] first bad column (-1: none), out[5] first bad row, out[6] max normalised error
+// (err / tolerance over every checksum; < 1 passes).
+extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inject, double* out) {
+  if (check_shape(M, N, K)) return -1;
+  CHECK(hipSetDevice(dev));
+  CHECK(set_lds_limit());
+  __bf16 *A = nullptr, *B = nullptr;
+  float *colpart = nullptr, *rowpart = nullptr, *work = nullptr;
+  unsigned int* flags = nullptr;
+  const size_t parts_c = (size_t)(M / BM) * WAVES_M, parts_r = (size_t)(N / BN) * WAVES_N;
+  CHECK(hipMalloc(&A, (size_t)M * K * 2));
+  CHECK(hipMalloc(&B, (size_t)N * K * 2));
+  CHECK(hipMalloc(&colpart, parts_c * N * 4));
+  CHECK(hipMalloc(&rowpart, parts_r * M * 4));
+  // sA, |sA|, sB, |sB| (K each), colexp/colbound (N), rowexp/rowbound (M)
+  CHECK(hipMalloc(&work, ((size_t)4 * K + 2 * N + 2 * M) * 4));
+  CHECK(hipMalloc(&flags, 6 * 4));
+  float *sA = work, *sAabs = sA + K, *sB = sAabs + K, *sBabs = sB + K, *colexp = sBabs + K, *colbd = colexp + N,
+        *rowexp = colbd + N, *rowbd = rowexp + M;
+  hipStream_t s;
+  CHECK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  hipEvent_t e0, e1;
+  CHECK(hipEventCreate(&e0));
+  CHECK(hipEventCreate(&e1));
+  k_fill_bf16<<<2048, 256, 0, s>>>(A, (size_t)M * K, 0x51f15eedu);
+  k_fill_bf16<<<2048, 256, 0, s>>>(B, (size_t)N * K, 0x0b5e55edu);
+  CHECK(hipGetLastError());
+  CHECK(launch_gemm(1, A, B, nullptr, colpart, rowpart, M, N, K, -1, s));  // warm-up
+  double best = 1e30;
+  for (int r = 0; r < (reps < 1 ? 1 : reps); ++r) {
+    CHECK(hipEventRecord(e0, s));
+    CHECK(launch_gemm(1, A, B, nullptr, colpart, rowpart, M, N, K, inject, s));
+    CHECK(hipEventRecord(e1, s));
+    CHECK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CHECK(hipEventElapsedTime(&ms, e0, e1));
+    best = std::min(best, (double)ms);
+  }
+  // right-hand sides: column sums of A and B over M / N, then the two mat-vecs
+  CHECK(hipMemsetAsync(sA, 0, (size_t)4 * K * sizeof(float), s));  // sA, |sA|, sB, |sB|
+  k_colsum_bf16<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(A, M, K, sA, sAabs);
+  k_colsum_bf16<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(B, N, K, sB, sBabs);
+  k_rowdot<<<(N + 3) / 4, 256, 0, s>>>(B, N, K, sA, sAabs, colexp, colbd);
+  k_rowdot<<<(M + 3) / 4, 256, 0, s>>>(A, M, K, sB, sBabs, rowexp, rowbd);
+  const unsigned int init[6] = {0u, 0xffffffffu, 0u, 0u, 0xffffffffu, 0u};
+  CHECK(hipMemcpyAsync(flags, init, sizeof(init), hipMemcpyHostToDevice, s));
+  // fp32 reassociation error of two different summation orders over K*M (or K*N) products
+  const float rtol = 1e-6f, atol = 1e-3f;  // healthy runs measure ~1e-3 of this tolerance
+  k_compare<<<(N + 255) / 256, 256, 0, s>>>(colpart, (int)parts_c, N, colexp, colbd, rtol, atol, flags, flags + 1,
+                                            reinterpret_cast<float*>(flags + 2));
+  k_compare<<<(M + 255) / 256, 256, 0, s>>>(rowpart, (int)parts_r, M, rowexp, rowbd, rtol, atol, flags + 3, flags + 4,
+                                            reinterpret_cast<float*>(flags + 5));
+  CHECK(hipGetLastError());
+  unsigned int h[6];
+  CHECK(hipMemcpyAsync(h, flags, sizeof(h), hipMemcpyDeviceToHost, s));
+  CHECK(hipStreamSynchronize(s));
+  float maxc, maxr;
+  memcpy(&maxc, &h[2], 4);
+  memcpy(&maxr, &h[5], 4);
+  out[0] = 2.0 * M * N * (double)K / (best * 1e-3) / 1e12;
+  out[1] = best;
+  out[2] = h[0];
+  out[3] = h[3];
+  out[4] = h[0] ? (double)h[1] : -1.0;
+  out[5] = h[3] ? (double)h[4] : -1.0;
+  out[6] = std::max(maxc, maxr);
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  (void)hipStreamDestroy(s);
+  (void)hipFree(flags);
+  (void)hipFree(work);
+  (void)hipFree(rowpart);
+  (void)hipFree(colpart);
+  (void)hipFree(B);
+  (void)hipFree(A);
+  return 0;
+}
