@@ -70,8 +70,8 @@ def targets() -> List[Target]:
     return [
         Target("libtk_gpu_probe.so", [probe],
                [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-fPIC", "-shared", probe, "-o", out("libtk_gpu_probe.so"), *RPATH]),
-        Target("gpu-burnin", [probe],
-               [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-DTK_PROBE_MAIN", probe, "-o", out("gpu-burnin"), *RPATH]),
+        Target("gpu-burnin", [probe, gemm],
+               [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-DTK_PROBE_MAIN", probe, gemm, "-o", out("gpu-burnin"), *RPATH]),
         Target("libtk_gemm.so", [gemm],
                [hipcc, *HIP_FLAGS, "-fPIC", "-shared", gemm, "-o", out("libtk_gemm.so"), *RPATH]),
         Target("libtk_rccl.so", [rccl],

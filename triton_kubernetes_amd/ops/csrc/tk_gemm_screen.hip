@@ -17,8 +17,9 @@
 //  * 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 of C as 8 x 4 fragments of
 //    16x16 (32 f32x4 accumulators);
 //  * K in steps of 64: A and B tiles [256][64] bf16 (32 KiB each) are staged into LDS
-//    with 16-byte global_load_lds (8 per thread per step), two LDS buffers so the copy
-//    of step t+1 overlaps the MFMAs of step t;
+//    with 16-byte global_load_lds (8 per thread per step) into two LDS buffers; each
+//    step's fragments are read into VGPRs before its MFMAs, so the copy two steps ahead
+//    can start as soon as a barrier says every wave has read the buffer (see the loop);
 //  * the LDS image is XOR-swizzled by 16-byte chunk (chunk ^ ((row >> 1) & 7)): the
 //    swizzle is applied to the per-lane GLOBAL source address (the LDS-DMA destination
 //    is lane-linear), so the 16 lanes of a ds_read_b128 group read 16 distinct bank
@@ -72,21 +73,31 @@ constexpr int GLDS_PER_TILE = TILE_BYTES / (THREADS * 16);                // 4 p
 // physical 16-byte chunk of logical chunk `c` in row `r` of a [rows][64] bf16 image
 __device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
 
-// Stage one [256][64] bf16 tile (rows row0.., k0..k0+63 of a K-contiguous matrix) into
-// LDS at `lds` (wave-uniform base + lane*16 per instruction; the swizzle goes on the source).
-__device__ __forceinline__ void stage_tile(const __bf16* __restrict__ g, int ld, int row0, int k0, char* lds,
+// Stage one [256][64] bf16 tile (k0..k0+63 of a 256-row panel of a K-contiguous matrix)
+// into LDS at `lds`.  Buffer loads straight to LDS: the panel is one SRSRC descriptor
+// (wave-uniform), every lane keeps ONE 32-bit byte offset `voff` for all its copies (the
+// per-copy row step and k0 go in the scalar offset), and the LDS destination is the
+// wave-uniform base + lane*16.  The swizzle lives in `voff` (see panel_voffset).
+__device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t panel, int ld, int voff, int k0, char* lds,
                                            int tid) {
 #pragma unroll
   for (int i = 0; i < GLDS_PER_TILE; ++i) {
-    const int slot = i * THREADS + tid;  // 16-byte slot of the image, lane-linear per wave
-    const int r = slot >> 3, cp = slot & 7;
-    const int c = cp ^ ((r >> 1) & 7);   // logical chunk this physical slot holds (XOR is an involution)
-    const __bf16* src = g + (size_t)(row0 + r) * ld + k0 + c * 8;
-    // LDS destination of lane 0 of this wave-instruction; lanes follow at +16 B
     char* dst = lds + (size_t)(i * THREADS + (tid & ~63)) * 16;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const void*>(src), reinterpret_cast<__shared__ void*>(dst), 16,
-                                     0, 0);
+    const int soff = (i * (THREADS / 8) * ld + k0) * 2;  // copy i covers rows i*64 .. i*64+63
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(panel, reinterpret_cast<__shared__ void*>(dst), 16, voff, soff, 0, 0);
   }
+}
+
+// Byte offset of this thread's 16-byte chunk within a panel row group: slot tid of the
+// lane-linear LDS image is row r = tid/8 (+ 64 per copy), physical chunk tid%8, which
+// holds logical chunk (tid%8) ^ ((r >> 1) & 7) — the same for every copy (64 rows apart).
+__device__ __forceinline__ int panel_voffset(int ld, int tid) {
+  const int r = tid >> 3, c = (tid & 7) ^ ((r >> 1) & 7);
+  return (r * ld + c * 8) * 2;
+}
+
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_panel(const __bf16* base, int row0, int ld) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<__bf16*>(base + (size_t)row0 * ld), 0, BM * ld * 2, 0x00020000);
 }
 
 __device__ __forceinline__ bf16x8 lds_frag(const char* img, int r, int c) {
@@ -132,38 +143,54 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  // Pipeline: every fragment of a K-step is read into VGPRs before its MFMAs, so a
+  // buffer is free again once the reads retire.  Per step t: read frags(t) from buffer
+  // t&1 -> wait my reads and my copy of step t+1 -> barrier (everyone's reads of t done,
+  // everyone's copy of t+1 landed) -> start the copy of step t+2 into buffer t&1 -> MFMAs
+  // of step t.  The MFMAs run after the barrier, overlapping the copy in flight; no wave
+  // waits at a barrier for another wave's MFMAs.
   const int nk = K / BK;
-  stage_tile(A, K, row0, 0, smem, tid);
-  stage_tile(B, K, col0, 0, smem + TILE_BYTES, tid);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  const __amdgpu_buffer_rsrc_t pa = make_panel(A, row0, K), pb = make_panel(B, col0, K);
+  const int voff = panel_voffset(K, tid);
+  stage_tile(pa, K, voff, 0, smem, tid);
+  stage_tile(pb, K, voff, 0, smem + TILE_BYTES, tid);
+  if (nk > 1) {
+    stage_tile(pa, K, voff, BK, smem + STAGE_BYTES, tid);
+    stage_tile(pb, K, voff, BK, smem + STAGE_BYTES + TILE_BYTES, tid);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // step 0 landed (step 1's 8 copies may fly)
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
 
   const int fr = lane & 15, fq = lane >> 4;  // fragment row/col within 16, k-chunk group
   for (int t = 0; t < nk; ++t) {
-    const char* cur = smem + (t & 1) * STAGE_BYTES;
-    if (t + 1 < nk) {  // next K-step into the other buffer (last read before the previous barrier)
-      char* nxt = smem + ((t + 1) & 1) * STAGE_BYTES;
-      stage_tile(A, K, row0, (t + 1) * BK, nxt, tid);
-      stage_tile(B, K, col0, (t + 1) * BK, nxt + TILE_BYTES, tid);
-    }
-    const char* a_img = cur;
-    const char* b_img = cur + TILE_BYTES;
+    const char* a_img = smem + (t & 1) * STAGE_BYTES;
+    const char* b_img = a_img + TILE_BYTES;
+    bf16x8 bf[BK / 32][FN], af[BK / 32][FM];
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 bf[FN];
 #pragma unroll
-      for (int j = 0; j < FN; ++j) bf[j] = lds_frag(b_img, wc * WN + j * 16 + fr, kk * 4 + fq);
-      __builtin_amdgcn_s_setprio(1);
+      for (int j = 0; j < FN; ++j) bf[kk][j] = lds_frag(b_img, wc * WN + j * 16 + fr, kk * 4 + fq);
 #pragma unroll
-      for (int i = 0; i < FM; ++i) {
-        const bf16x8 af = lds_frag(a_img, wr * WM + i * 16 + fr, kk * 4 + fq);
-#pragma unroll
-        for (int j = 0; j < FN; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af, bf[j], acc[i][j], 0, 0, 0);
-      }
-      __builtin_amdgcn_s_setprio(0);
+      for (int i = 0; i < FM; ++i) af[kk][i] = lds_frag(a_img, wr * WM + i * 16 + fr, kk * 4 + fq);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // next tile landed (this wave's share)
-    __syncthreads();                                   // ... everyone's; and `cur` is free again
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) {
+      char* dst = smem + (t & 1) * STAGE_BYTES;
+      stage_tile(pa, K, voff, (t + 2) * BK, dst, tid);
+      stage_tile(pb, K, voff, (t + 2) * BK, dst + TILE_BYTES, tid);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+      for (int i = 0; i < FM; ++i)
+#pragma unroll
+        for (int j = 0; j < FN; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
   }
 
   // accumulator element (i, j, e): row = wr*WM + i*16 + fq*4 + e, col = wc*WN + j*16 + fr

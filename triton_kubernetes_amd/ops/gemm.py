@@ -42,6 +42,9 @@ def gemm_bt(a, b, out=None):
     """``out = a @ b.T`` in fp32 for bf16 CUDA tensors ``a [M,K]``, ``b [N,K]`` (contiguous)."""
     import torch
 
+    from .native import require_torch_first
+
+    require_torch_first()
     if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not (a.is_cuda and b.is_cuda):
         raise GemmError("gemm_bt wants bf16 CUDA tensors")
     if not (a.is_contiguous() and b.is_contiguous()) or a.shape[1] != b.shape[1]:

@@ -16,6 +16,11 @@ LIB_DIR = os.path.join(HERE, "lib")
 
 _lock = threading.Lock()
 _cache: Dict[str, ctypes.CDLL] = {}
+# Whether the first HIP library was loaded before torch: torch bundles its own
+# libamdhip64 / librccl under the same sonames as /opt/rocm's, and the one loaded first
+# serves the whole process; torch imported afterwards would run on the other build.
+_HIP_LIBS = {"libtk_gpu_probe.so", "libtk_gemm.so", "libtk_rccl.so"}
+_hip_before_torch = None
 
 
 class NativeUnavailable(RuntimeError):
@@ -41,6 +46,11 @@ def load(name: str, autobuild: bool = True) -> ctypes.CDLL:
         if not os.path.exists(path):
             raise NativeUnavailable(f"native library {path} is missing; run `python -m "
                                     "triton_kubernetes_amd.ops.build`")
+        global _hip_before_torch
+        if name in _HIP_LIBS and _hip_before_torch is None:
+            import sys
+
+            _hip_before_torch = "torch" not in sys.modules
         try:
             lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         except OSError as exc:
@@ -63,3 +73,13 @@ def executable(name: str) -> str:
 
         build(only=[name])
     return path
+
+
+def require_torch_first() -> None:
+    """Raise unless torch was imported before this process loaded a native HIP library
+    (callers that hand torch tensors to native code: both must share one HIP runtime)."""
+    import sys
+
+    if _hip_before_torch and "torch" in sys.modules:
+        raise NativeUnavailable("torch was imported after the native HIP libraries were loaded; import torch "
+                                "first so both use torch's HIP runtime")

@@ -1205,6 +1205,7 @@ data "external" "gpu_labels" {{
         {"install_mi355x_node.sh.tftpl": scripts.INSTALL_MI355X_NODE, "read_gpu_labels.sh": scripts.READ_REMOTE_LABELS},
         {"src/tk_topo.cpp": os.path.join(CSRC, "tk_topo.cpp"),
          "src/tk_gpu_probe.hip": os.path.join(CSRC, "tk_gpu_probe.hip"),
+         "src/tk_gemm_screen.hip": os.path.join(CSRC, "tk_gemm_screen.hip"),
          "src/tk_rccl_probe.hip": os.path.join(CSRC, "tk_rccl_probe.hip")}))
 
     # MI355X cluster add-ons

@@ -182,7 +182,7 @@ build() { # name, compiler, flags...
   [ -x "$T/$name" ] || sudo "$@" -o "$T/$name"
 }
 build amdgpu-topo-labeller g++ -O2 -std=c++17 -DTK_TOPO_MAIN -DTK_TOPO_AMDSMI -I$ROCM/include $S/tk_topo.cpp -L$ROCM/lib -lamd_smi -Wl,-rpath,$ROCM/lib
-build gpu-burnin $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip
+build gpu-burnin $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip
 build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl
 $T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/dev/null
 $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
