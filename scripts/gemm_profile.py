@@ -1,0 +1,10 @@
+#!/usr/bin/env python3
+"""One 8192^3 GEMM screen (for rocprofv3 counter passes over k_gemm_bt)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from triton_kubernetes_amd.ops import gemm  # noqa: E402
+
+r = gemm.screen(0, 8192, 8192, 8192, reps=2)
+print(r.to_json())
