@@ -38,6 +38,7 @@
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -164,10 +165,10 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
   __builtin_amdgcn_s_barrier();
 
   const int fr = lane & 15, fq = lane >> 4;  // fragment row/col within 16, k-chunk group
-  for (int t = 0; t < nk; ++t) {
+  bf16x8 bf[BK / 32][FN], af[BK / 32][FM];
+  auto read_frags = [&](int t) {
     const char* a_img = smem + (t & 1) * STAGE_BYTES;
     const char* b_img = a_img + TILE_BYTES;
-    bf16x8 bf[BK / 32][FN], af[BK / 32][FM];
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
 #pragma unroll
@@ -175,13 +176,8 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
 #pragma unroll
       for (int i = 0; i < FM; ++i) af[kk][i] = lds_frag(a_img, wr * WM + i * 16 + fr, kk * 4 + fq);
     }
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t + 2 < nk) {
-      char* dst = smem + (t & 1) * STAGE_BYTES;
-      stage_tile(pa, K, voff, (t + 2) * BK, dst, tid);
-      stage_tile(pb, K, voff, (t + 2) * BK, dst + TILE_BYTES, tid);
-    }
+  };
+  auto mfmas = [&]() {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk)
@@ -191,6 +187,22 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
         for (int j = 0; j < FN; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
+  };
+  auto stage = [&](int t) {  // K-step t into buffer t&1
+    char* dst = smem + (t & 1) * STAGE_BYTES;
+    stage_tile(pa, K, voff, t * BK, dst, tid);
+    stage_tile(pb, K, voff, t * BK, dst + TILE_BYTES, tid);
+  };
+
+  // (A variant with two wave groups staggered by one barrier slot, so one group's MFMAs
+  // cover the other's fragment reads, measured the same: 1162 / 1224 vs 1155 / 1238 TF at
+  // 4096^3 / 8192^3 — profiles/round1_gemm_pmc.md.)
+  for (int t = 0; t < nk; ++t) {
+    read_frags(t);
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < nk) stage(t + 2);
+    mfmas();
   }
 
   // accumulator element (i, j, e): row = wr*WM + i*16 + fq*4 + e, col = wc*WN + j*16 + fr
@@ -334,12 +346,12 @@ static hipError_t launch_gemm(int mode, const __bf16* A, const __bf16* B, float*
 
 static hipError_t set_lds_limit() {
   static hipError_t once = [] {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_bt<0>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute(reinterpret_cast<const void*>(&k_gemm_bt<1>),
-                              hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
-    return e;
+    const void* fns[] = {reinterpret_cast<const void*>(&k_gemm_bt<0>), reinterpret_cast<const void*>(&k_gemm_bt<1>)};
+    for (const void* f : fns) {
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
   }();
   return once;
 }
