@@ -62,19 +62,28 @@ static int set_err(const char* what, hipError_t e) {
 extern "C" const char* tkg_last_error() { return g_err; }
 
 namespace {
-constexpr int BM = 256, BN = 256, BK = 64;
+#ifndef TKG_BK
+#define TKG_BK 64
+#endif
+constexpr int BM = 256, BN = 256, BK = TKG_BK;                            // K-step 64 (default) or 32
 constexpr int WAVES_M = 2, WAVES_N = 4, THREADS = 64 * WAVES_M * WAVES_N;  // 512
 constexpr int WM = BM / WAVES_M, WN = BN / WAVES_N;                       // 128 x 64 per wave
 constexpr int FM = WM / 16, FN = WN / 16;                                 // 8 x 4 fragments
-constexpr int TILE_BYTES = BM * BK * 2;                                   // 32 KiB per operand tile
+constexpr int KSUB = BK / 32;                                             // MFMA K-steps per stage
+constexpr int TILE_BYTES = BM * BK * 2;                                   // per operand tile
 constexpr int STAGE_BYTES = 2 * TILE_BYTES;                               // A + B
-constexpr int LDS_BYTES = 2 * STAGE_BYTES;                                // double buffered: 128 KiB
-constexpr int GLDS_PER_TILE = TILE_BYTES / (THREADS * 16);                // 4 per thread per operand
+constexpr int NSTAGE = (128 * 1024) / STAGE_BYTES;                        // 128 KiB: 4 stages (BK 32) / 2 (BK 64)
+constexpr int LDS_BYTES = NSTAGE * STAGE_BYTES;
+constexpr int GLDS_PER_TILE = TILE_BYTES / (THREADS * 16);                // copies per thread per operand
+constexpr int CHUNKS = BK / 8;                                            // 16-byte chunks per row
+constexpr int ROWS_PER_BANKROW = 256 / (BK * 2);                          // rows sharing one 256-B bank row
+constexpr int ROWS_PER_COPY = THREADS / CHUNKS;                           // rows one copy instruction covers
 
-// physical 16-byte chunk of logical chunk `c` in row `r` of a [rows][64] bf16 image
-__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r >> 1) & 7); }
+// physical 16-byte chunk of logical chunk `c` in row `r`: the 16 lanes of a ds_read_b128
+// group (16 consecutive rows, one chunk) land in 16 distinct 16-byte bank slots
+__device__ __forceinline__ int swz(int r, int c) { return c ^ ((r / ROWS_PER_BANKROW) & (CHUNKS - 1)); }
 
-// Stage one [256][64] bf16 tile (k0..k0+63 of a 256-row panel of a K-contiguous matrix)
+// Stage one [256][BK] bf16 tile (k0..k0+BK-1 of a 256-row panel of a K-contiguous matrix)
 // into LDS at `lds`.  Buffer loads straight to LDS: the panel is one SRSRC descriptor
 // (wave-uniform), every lane keeps ONE 32-bit byte offset `voff` for all its copies (the
 // per-copy row step and k0 go in the scalar offset), and the LDS destination is the
@@ -84,16 +93,17 @@ __device__ __forceinline__ void stage_tile(__amdgpu_buffer_rsrc_t panel, int ld,
 #pragma unroll
   for (int i = 0; i < GLDS_PER_TILE; ++i) {
     char* dst = lds + (size_t)(i * THREADS + (tid & ~63)) * 16;
-    const int soff = (i * (THREADS / 8) * ld + k0) * 2;  // copy i covers rows i*64 .. i*64+63
+    const int soff = (i * ROWS_PER_COPY * ld + k0) * 2;  // copy i covers the next ROWS_PER_COPY rows
     __builtin_amdgcn_raw_ptr_buffer_load_lds(panel, reinterpret_cast<__shared__ void*>(dst), 16, voff, soff, 0, 0);
   }
 }
 
-// Byte offset of this thread's 16-byte chunk within a panel row group: slot tid of the
-// lane-linear LDS image is row r = tid/8 (+ 64 per copy), physical chunk tid%8, which
-// holds logical chunk (tid%8) ^ ((r >> 1) & 7) — the same for every copy (64 rows apart).
+// Byte offset of this thread's 16-byte chunk: slot tid of the lane-linear LDS image is row
+// r = tid / CHUNKS (+ ROWS_PER_COPY per copy), physical chunk tid % CHUNKS, which holds
+// logical chunk swz(r, tid % CHUNKS) — the same for every copy (the row step is a multiple
+// of the swizzle period).
 __device__ __forceinline__ int panel_voffset(int ld, int tid) {
-  const int r = tid >> 3, c = (tid & 7) ^ ((r >> 1) & 7);
+  const int r = tid / CHUNKS, c = swz(r, tid % CHUNKS);
   return (r * ld + c * 8) * 2;
 }
 
@@ -102,7 +112,21 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_panel(const __bf16* base,
 }
 
 __device__ __forceinline__ bf16x8 lds_frag(const char* img, int r, int c) {
-  return *reinterpret_cast<const bf16x8*>(img + r * 128 + swz(r, c) * 16);
+  return *reinterpret_cast<const bf16x8*>(img + r * (BK * 2) + swz(r, c) * 16);
+}
+
+// s_waitcnt vmcnt(n * copies per stage) for a runtime n in [0, NSTAGE): the count must be
+// an immediate
+__device__ __forceinline__ void wait_copies_but(int n) {
+  static_assert(2 * GLDS_PER_TILE == 4 || 2 * GLDS_PER_TILE == 8, "copies per stage");
+  if (n <= 0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if TKG_BK == 32
+  else if (n == 1) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  else if (n == 2) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+#else
+  else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+#endif
 }
 
 // XCD-aware, bijective block -> tile map: blocks b, b+8, b+16.. run on one XCD; give each
@@ -144,33 +168,26 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
 #pragma unroll
     for (int j = 0; j < FN; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // Pipeline: every fragment of a K-step is read into VGPRs before its MFMAs, so a
-  // buffer is free again once the reads retire.  Per step t: read frags(t) from buffer
-  // t&1 -> wait my reads and my copy of step t+1 -> barrier (everyone's reads of t done,
-  // everyone's copy of t+1 landed) -> start the copy of step t+2 into buffer t&1 -> MFMAs
-  // of step t.  The MFMAs run after the barrier, overlapping the copy in flight; no wave
-  // waits at a barrier for another wave's MFMAs.
   const int nk = K / BK;
   const __amdgpu_buffer_rsrc_t pa = make_panel(A, row0, K), pb = make_panel(B, col0, K);
   const int voff = panel_voffset(K, tid);
-  stage_tile(pa, K, voff, 0, smem, tid);
-  stage_tile(pb, K, voff, 0, smem + TILE_BYTES, tid);
-  if (nk > 1) {
-    stage_tile(pa, K, voff, BK, smem + STAGE_BYTES, tid);
-    stage_tile(pb, K, voff, BK, smem + STAGE_BYTES + TILE_BYTES, tid);
-    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // step 0 landed (step 1's 8 copies may fly)
-  } else {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
+  auto stage = [&](int t) {  // K-step t into buffer t % NSTAGE
+    char* dst = smem + (t % NSTAGE) * STAGE_BYTES;
+    stage_tile(pa, K, voff, t * BK, dst, tid);
+    stage_tile(pb, K, voff, t * BK, dst + TILE_BYTES, tid);
+  };
+  // prologue: the first NSTAGE steps in flight; wait for step 0 only
+  for (int t = 0; t < NSTAGE && t < nk; ++t) stage(t);
+  wait_copies_but(min(nk, NSTAGE) - 1);
   __builtin_amdgcn_s_barrier();
 
   const int fr = lane & 15, fq = lane >> 4;  // fragment row/col within 16, k-chunk group
-  bf16x8 bf[BK / 32][FN], af[BK / 32][FM];
+  bf16x8 bf[KSUB][FN], af[KSUB][FM];
   auto read_frags = [&](int t) {
-    const char* a_img = smem + (t & 1) * STAGE_BYTES;
+    const char* a_img = smem + (t % NSTAGE) * STAGE_BYTES;
     const char* b_img = a_img + TILE_BYTES;
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
+    for (int kk = 0; kk < KSUB; ++kk) {
 #pragma unroll
       for (int j = 0; j < FN; ++j) bf[kk][j] = lds_frag(b_img, wc * WN + j * 16 + fr, kk * 4 + fq);
 #pragma unroll
@@ -180,7 +197,7 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
   auto mfmas = [&]() {
     __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk)
+    for (int kk = 0; kk < KSUB; ++kk)
 #pragma unroll
       for (int i = 0; i < FM; ++i)
 #pragma unroll
@@ -188,20 +205,20 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bf[kk][j], acc[i][j], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
   };
-  auto stage = [&](int t) {  // K-step t into buffer t&1
-    char* dst = smem + (t & 1) * STAGE_BYTES;
-    stage_tile(pa, K, voff, t * BK, dst, tid);
-    stage_tile(pb, K, voff, t * BK, dst + TILE_BYTES, tid);
-  };
 
-  // (A variant with two wave groups staggered by one barrier slot, so one group's MFMAs
-  // cover the other's fragment reads, measured the same: 1162 / 1224 vs 1155 / 1238 TF at
-  // 4096^3 / 8192^3 — profiles/round1_gemm_pmc.md.)
+  // Every fragment of step t is read into VGPRs before its MFMAs, so buffer t % NSTAGE is
+  // free once the barrier after those reads has passed: step t + NSTAGE is copied into it
+  // right there, and the MFMAs run while the NSTAGE - 1 later steps are in flight.  Before
+  // the barrier each thread waits for its copy of step t+1 only (later ones keep flying),
+  // so the barrier also publishes step t+1 to every wave.
+  // (A variant with two wave groups staggered by one barrier slot measured the same at
+  // BK 64: 1162 / 1224 vs 1155 / 1238 TF at 4096^3 / 8192^3 — profiles/round1_gemm_pmc.md.)
   for (int t = 0; t < nk; ++t) {
     read_frags(t);
-    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    wait_copies_but(min(nk - 1, t + NSTAGE - 1) - (t + 1));
     __builtin_amdgcn_s_barrier();
-    if (t + 2 < nk) stage(t + 2);
+    if (t + NSTAGE < nk) stage(t + NSTAGE);
     mfmas();
   }
 
