@@ -5,6 +5,7 @@
     python -m triton_kubernetes_amd.ops.cli labels
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
     python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
+    python -m triton_kubernetes_amd.ops.cli gemm [--size N] [--reps R]
 
 Every command prints one JSON document; the exit status is non-zero when the
 GPU(s) fail the gate.
@@ -37,6 +38,10 @@ def main(argv: Sequence[str] = ()) -> int:
     m.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "f32"])
     m.add_argument("--iters", type=int, default=20000)
     m.add_argument("--blocks-per-cu", type=int, default=2)
+    g = sub.add_parser("gemm", help="checksum-verified GEMM screen (silent data corruption)")
+    g.add_argument("--device", type=int, default=0)
+    g.add_argument("--size", type=int, default=8192, help="M = N = K (a multiple of 256)")
+    g.add_argument("--reps", type=int, default=5)
     m.add_argument("--clock", action="store_true",
                    help="also report the in-kernel clock and FLOP/clk/SIMD (stamped diagnostic launch)")
     args = ap.parse_args(list(argv) or sys.argv[1:])
@@ -79,6 +84,12 @@ def main(argv: Sequence[str] = ()) -> int:
             res["clock"] = probe.mfma_clock(args.device, args.dtype, args.iters, blocks_per_cu=args.blocks_per_cu)
         print(json.dumps(res))
         return 0
+    if args.cmd == "gemm":
+        from . import gemm
+
+        res = gemm.screen(args.device, args.size, args.size, args.size, args.reps)
+        print(json.dumps(res.to_json()))
+        return 0 if res.ok else 1
     return 2
 
 
