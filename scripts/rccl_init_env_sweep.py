@@ -48,6 +48,10 @@ VARIANTS = {
     "proxy_shm_small": {"NCCL_PROXY_APPEND_BATCH_SIZE": "4", "NCCL_CREATE_THREAD_CONTEXT": "0"},
     "msccl_off": {"RCCL_MSCCL_ENABLE": "0", "RCCL_MSCCLPP_ENABLE": "0"},
     "rccl_kernel_trace_off": {"RCCL_KERNEL_COLL_TRACE_ENABLE": "0", "NCCL_COLLNET_ENABLE": "0", "NCCL_NVLS_ENABLE": "0"},
+    # glibc keeps the init's ~100 MiB topology-XML buffers in the heap instead of fresh mmaps
+    # (a fresh mapping page-faults on first touch; a reused heap chunk does not)
+    "malloc_heap": {"MALLOC_MMAP_THRESHOLD_": str(1 << 30), "MALLOC_TRIM_THRESHOLD_": str(4 << 30)},
+    "malloc_heap_tunables": {"GLIBC_TUNABLES": f"glibc.malloc.mmap_threshold={1 << 30}:glibc.malloc.trim_threshold={4 << 30}"},
 }
 
 
