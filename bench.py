@@ -253,6 +253,9 @@ def main() -> int:
         cp_agent.stop()
     if fake is not None:
         fake.stop()
+    import shutil
+
+    shutil.rmtree(work, ignore_errors=True)  # the run's manager state, agent roots and node files
     if distributed:
         dist.barrier()
         dist.destroy_process_group()

@@ -244,3 +244,71 @@ def test_host_retry_recovers_flaky_node(env):
         del events
     finally:
         a.stop()
+
+
+# --- create cost independent of the clusters already on the manager -------------------------------------
+
+
+def _plain_tfstate(doc):
+    from triton_kubernetes_amd.executor.tfstate import derived_outputs
+
+    full = dict(doc)
+    full["outputs"] = derived_outputs(doc["module_outputs"])
+    return json.dumps(full, indent=2, sort_keys=True).encode()
+
+
+def test_tfstate_codec_bytes_and_reuse():
+    from triton_kubernetes_amd.executor.tfstate import TfstateCodec
+
+    codec = TfstateCodec()
+    doc = {"version": 4, "serial": 1, "lineage": "l", "resources": [], "terraform_version": "t",
+           "module_outputs": {}, "module_state": {}}
+    assert codec.dumps("m", doc) == _plain_tfstate(doc)
+    for i in range(30):
+        key = f"node_baremetal_c{i // 5}_h-{i}"
+        doc["module_outputs"][key] = {"gpu_node_labels": json.dumps({"amd.com/gpu<&>": i}), "z": "é "}
+        doc["module_state"][key] = {"hash": f"{i:016x}", "status": "ok", "applied_at": 1.5 + i, "source": None}
+        if i % 7 == 0:
+            assert codec.dumps("m", doc) == _plain_tfstate(doc)
+    # replaced (not edited) entries and removed ones are picked up
+    doc["module_state"]["node_baremetal_c0_h-0"] = {"hash": "x", "status": "failed", "error": "boom"}
+    doc["module_outputs"]["node_baremetal_c0_h-1"] = {"gpu_node_labels": "{}"}
+    doc["module_outputs"].pop("node_baremetal_c0_h-2")
+    doc["module_state"].pop("node_baremetal_c0_h-3")
+    raw = codec.dumps("m", doc)
+    assert raw == _plain_tfstate(doc)
+    # a load of the bytes just saved reuses the document (no "outputs": derived on save) ...
+    again = codec.load("m", raw)
+    assert again["module_state"] == doc["module_state"] and "outputs" not in again
+    again["module_state"]["new"] = {"hash": "n", "status": "ok"}
+    assert "new" not in doc["module_state"]  # the copy's sections are its own
+    # ... and other bytes are parsed
+    other = codec.load("m", _plain_tfstate(dict(doc, serial=99)))
+    assert other["serial"] == 99 and other["module_outputs"] == doc["module_outputs"]
+    assert codec.load("m", b"not json") is None and codec.load("m", b'{"version": 4}') is None
+
+
+def test_fingerprint_matches_hash_and_deps():
+    from triton_kubernetes_amd.executor.direct import config_hash, fingerprint
+
+    cfgs = [{}, {"a": "${module.cluster-manager.rancher_url}", "q": "say \"${module.x_y.z}\" \\ é"},
+            {"n": [1, {"m": "${module.node_b_c_h.out}x${module.cluster_b_c.id}"}], "u": None, "f": 1.5}]
+    for cfg in cfgs:
+        assert fingerprint(cfg) == (config_hash(cfg), module_deps(cfg))
+
+
+def test_fake_rancher_settles_clusters(env):
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    cp = agent("cp")
+    for name in ("one", "two"):
+        new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name=name,
+                                  k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", wait=True,
+                                  nodes=_nodes(cp, [agent(f"{name}-w", gpus=8)]))), backend)
+    # a settled cluster is no longer walked by the simulation; each cluster lists its own nodes
+    assert fake.state.unsettled == set()
+    cids = {c["name"]: c["id"] for c in fake.state.clusters.values()}
+    assert {n["metadata"]["name"] for n in fake.k8s_nodes(cids["two"])} == {"cp-1", "etcd-1", "gpu-1"}
+    user, _, secret = RancherClient(fake.url).login("admin", "s3cret").partition(":")
+    client = RancherClient(fake.url, user, secret)
+    assert {n["clusterId"] for n in client.nodes(cids["one"])} == {cids["one"]}

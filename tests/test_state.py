@@ -107,3 +107,25 @@ def test_key_helpers_and_roundtrip():
         st.delete("module.nope")
     with pytest.raises(StateError):
         State("bad", b"[1,2]")
+
+
+def test_dumps_go_memo_matches_plain_encoding():
+    from hypothesis import given, settings
+    from hypothesis import strategies as st
+
+    from triton_kubernetes_amd.utils.jsonenc import dumps_go, dumps_go_plain
+
+    leaf = st.one_of(st.none(), st.booleans(), st.integers(), st.floats(allow_nan=False),
+                     st.text(alphabet="ab<>& é\"\\\n", max_size=6))
+    tree = st.recursive(leaf, lambda ch: st.one_of(st.lists(ch, max_size=3),
+                                                   st.dictionaries(st.text("xyz<", max_size=3), ch, max_size=3)),
+                        max_leaves=12)
+
+    @settings(max_examples=200, deadline=None)
+    @given(tree)
+    def check(obj):
+        for indent in ("\t", "  ", ""):
+            assert dumps_go(obj, indent) == dumps_go_plain(obj, indent)
+            assert dumps_go(obj, indent) == dumps_go_plain(obj, indent)  # memo hit
+
+    check()

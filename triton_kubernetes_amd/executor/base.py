@@ -8,7 +8,8 @@ parallel.
 """
 
 import json
-from typing import Dict, List, Optional
+import threading
+from typing import Any, Dict, List, Optional
 
 from ..backend.base import Backend
 from ..state import State
@@ -34,6 +35,26 @@ class Executor:
         out.flush()
 
 
+_PARSED: List[Any] = [None, None]  # [raw, document] of the last tfstate parsed here
+_PARSED_MU = threading.Lock()
+
+
+def _parsed(raw: bytes) -> Any:
+    """``json.loads(raw)``, reusing the last result for the same bytes (the readiness
+    waiter reads the manager's and the cluster's outputs from one tfstate).  The document
+    is shared: callers only read it."""
+    with _PARSED_MU:
+        if _PARSED[0] == raw:
+            return _PARSED[1]
+    try:
+        doc = json.loads(raw)
+    except ValueError:
+        return None
+    with _PARSED_MU:
+        _PARSED[0], _PARSED[1] = bytes(raw), doc
+    return doc
+
+
 def outputs_from_tfstate(raw: Optional[bytes], module_key: str) -> Dict[str, str]:
     """Module outputs from a tfstate document.
 
@@ -43,9 +64,8 @@ def outputs_from_tfstate(raw: Optional[bytes], module_key: str) -> Dict[str, str
     """
     if not raw:
         return {}
-    try:
-        doc = json.loads(raw)
-    except ValueError:
+    doc = _parsed(raw)
+    if not isinstance(doc, dict):
         return {}
     result: Dict[str, str] = {}
     for mod in doc.get("modules", []) or []:  # v3

@@ -47,6 +47,7 @@ from ..state import State
 from ..terraform.catalog import ModuleInfo, module_from_source
 from ..utils.trace import span
 from .base import Executor, outputs_from_tfstate
+from .tfstate import CODEC
 
 INTERP_RE = re.compile(r"\$\{module\.([A-Za-z0-9_.-]+?)\.([A-Za-z0-9_]+)\}")
 SUPPORTED = {"bare-metal-rancher", "bare-metal-rancher-k8s", "bare-metal-rancher-k8s-host",
@@ -55,6 +56,17 @@ SUPPORTED = {"bare-metal-rancher", "bare-metal-rancher-k8s", "bare-metal-rancher
 
 def config_hash(cfg: Any) -> str:
     return hashlib.sha256(json.dumps(cfg, sort_keys=True).encode()).hexdigest()[:16]
+
+
+def fingerprint(cfg: Any) -> Tuple[str, Set[str]]:
+    """``(config_hash(cfg), module_deps(cfg))`` from ONE C-encoder pass over ``cfg``.
+
+    Every apply re-plans every module of the manager, so this runs once per module per
+    create.  The interpolation pattern holds no ``"`` or ``\\``, so its matches in the
+    encoded text are exactly its matches in the document's strings.
+    """
+    text = json.dumps(cfg, sort_keys=True)
+    return hashlib.sha256(text.encode()).hexdigest()[:16], {m.group(1) for m in INTERP_RE.finditer(text)}
 
 
 def module_deps(cfg: Any) -> Set[str]:
@@ -97,6 +109,7 @@ class ModuleRun:
     info: ModuleInfo
     cfg: Dict[str, Any]
     deps: Set[str]
+    hash: str = ""
     status: str = "pending"  # pending | skipped | ok | failed | blocked
     error: Optional[str] = None
     start: float = 0.0
@@ -145,27 +158,18 @@ class DirectExecutor(Executor):
     # --- tfstate ---------------------------------------------------------------------------------
     @staticmethod
     def _load_tfstate(backend: Backend, name: str) -> Dict[str, Any]:
-        raw = backend.read_tfstate(name)
-        if raw:
-            try:
-                doc = json.loads(raw)
-                if isinstance(doc, dict) and "module_state" in doc:
-                    return doc
-            except ValueError:
-                pass
+        doc = CODEC.load(name, backend.read_tfstate(name))
+        if doc is not None:
+            return doc
         return {"version": 4, "terraform_version": f"tk-direct-{__version__}", "serial": 0,
-                "lineage": str(uuid.uuid4()), "outputs": {}, "resources": [], "module_outputs": {},
-                "module_state": {}}
+                "lineage": str(uuid.uuid4()), "resources": [], "module_outputs": {}, "module_state": {}}
 
     def _save_tfstate(self, backend: Backend, name: str, doc: Dict[str, Any]) -> None:
+        # executor/tfstate.py: only new or replaced entries are encoded; the root
+        # "outputs" (<key>__<output>) are derived from module_outputs there
         with self._mu:
             doc["serial"] = int(doc.get("serial", 0)) + 1
-            outputs = {}
-            for key, outs in doc["module_outputs"].items():
-                for k, v in outs.items():
-                    outputs[f"{key}__{k}"] = {"value": v, "type": "string"}
-            doc["outputs"] = outputs
-            backend.write_tfstate(name, json.dumps(doc, indent=2, sort_keys=True).encode())
+            backend.write_tfstate(name, CODEC.dumps(name, doc))
 
     # --- planning -------------------------------------------------------------------------------------
     def plan(self, state: State) -> Dict[str, ModuleRun]:
@@ -175,14 +179,20 @@ class DirectExecutor(Executor):
             if info is None or info.name not in SUPPORTED:
                 raise ExecutorError(f"the direct executor does not implement module '{cfg.get('source')}' "
                                     f"(module.{key}); use `executor: terraform`")
-            runs[key] = ModuleRun(key, info, cfg, module_deps(cfg))
+            h, deps = fingerprint(cfg)
+            runs[key] = ModuleRun(key, info, cfg, deps, h)
         # An add-on module is applied after every host of its cluster (Terraform
         # would need an explicit depends_on): a failed node then blocks it
         # instead of leaving it waiting for a cluster that cannot turn active.
+        hosts_of: Dict[str, Set[str]] = {}  # module key -> the host modules that reference it
+        for k, h in runs.items():
+            if h.info.kind == "host":
+                for d in h.deps:
+                    hosts_of.setdefault(d, set()).add(k)
         for r in runs.values():
             if r.info.kind == "addon":
-                clusters = {d for d in r.deps if runs.get(d) and runs[d].info.kind == "cluster"}
-                r.deps |= {k for k, h in runs.items() if h.info.kind == "host" and h.deps & clusters}
+                for d in [d for d in r.deps if runs.get(d) and runs[d].info.kind == "cluster"]:
+                    r.deps |= hosts_of.get(d, set())
         for r in runs.values():
             missing = r.deps - set(runs)
             if missing:
@@ -230,8 +240,7 @@ class DirectExecutor(Executor):
                     if all(runs[d].status in ("ok", "skipped") for d in run.deps):
                         pending.discard(key)
                         prev = tf["module_state"].get(key)
-                        h = config_hash(run.cfg)
-                        if prev and prev.get("hash") == h and prev.get("status") == "ok" and key in outputs:
+                        if prev and prev.get("hash") == run.hash and prev.get("status") == "ok" and key in outputs:
                             run.status = "skipped"
                             continue
                         run.start = time.time()
@@ -242,8 +251,11 @@ class DirectExecutor(Executor):
                     pending.clear()
                     break
                 done, _ = cf.wait(list(futures), return_when=cf.FIRST_COMPLETED)
+                # one save per batch of finished modules (entries are replaced, never edited:
+                # executor/tfstate.py caches their encoding by identity)
+                keys_done: Dict[cf.Future, str] = {}
                 for fut in done:
-                    key = futures.pop(fut)
+                    key = keys_done[fut] = futures.pop(fut)
                     run = runs[key]
                     run.end = time.time()
                     try:
@@ -251,15 +263,17 @@ class DirectExecutor(Executor):
                         run.status, run.detail = "ok", detail
                         outputs[key] = outs
                         tf["module_outputs"][key] = outs
-                        tf["module_state"][key] = {"hash": config_hash(run.cfg), "status": "ok",
+                        tf["module_state"][key] = {"hash": run.hash, "status": "ok",
                                                    "applied_at": run.end, "seconds": run.end - run.start,
                                                    "source": run.cfg.get("source")}
                     except Exception as exc:  # noqa: BLE001 - recorded per module
                         run.status, run.error = "failed", str(exc)
-                        tf["module_state"][key] = {"hash": config_hash(run.cfg), "status": "failed",
+                        tf["module_state"][key] = {"hash": run.hash, "status": "failed",
                                                    "error": str(exc), "applied_at": run.end}
-                    self._save_tfstate(backend, state.name, tf)
-                    self._event("module_done", key=key, status=run.status, seconds=run.end - run.start)
+                self._save_tfstate(backend, state.name, tf)
+                for fut in done:
+                    run = runs[keys_done[fut]]
+                    self._event("module_done", key=run.key, status=run.status, seconds=run.end - run.start)
         report.wall = time.time() - t0
         self.last_report = report
         return report

@@ -27,7 +27,7 @@ import threading
 import time
 import urllib.parse
 import uuid
-from typing import Any, Dict, List, Optional, Tuple
+from typing import Any, Dict, List, Optional, Set, Tuple
 
 FAKE_CACERTS = "-----BEGIN CERTIFICATE-----\nMIIFAKECERTIFICATEFORTESTS\n-----END CERTIFICATE-----"
 
@@ -42,7 +42,11 @@ class _State:
         self.clusters: Dict[str, Dict[str, Any]] = {}
         self.reg_tokens: Dict[str, Dict[str, Any]] = {}  # token -> {clusterId, id}
         self.nodes: Dict[str, Dict[str, Any]] = {}
+        # indexes, so a request costs the same however many clusters the server holds
+        self.cluster_nodes: Dict[str, Dict[str, Dict[str, Any]]] = {}  # cluster id -> node id -> node
+        self.unsettled: Set[str] = set()  # clusters not yet active, or with a node not yet active
         self.objects: Dict[str, Dict[str, Any]] = {}  # "<cluster>|<path>|<name>" -> object
+        self.cluster_objects: Dict[str, Dict[str, None]] = {}  # cluster id -> its object keys, in creation order
         self.rke_seconds = rke_seconds
         self.node_ready_seconds = node_ready_seconds
         self.requests = 0
@@ -79,34 +83,45 @@ class FakeRancher:
 
     # --- simulation -----------------------------------------------------------------------
     def _refresh(self) -> None:
+        """Advance the simulated RKE provisioning of the clusters still settling."""
         st = self.state
         now = time.time()
         with st.mu:
-            for c in st.clusters.values():
-                roles = {"etcd": False, "controlplane": False, "worker": False}
-                for n in st.nodes.values():
-                    if n["clusterId"] == c["id"]:
+            for cid in list(st.unsettled):
+                c = st.clusters.get(cid)
+                if c is None:
+                    st.unsettled.discard(cid)
+                    continue
+                nodes = st.cluster_nodes.get(cid, {}).values()
+                if c["state"] != "active":
+                    roles = {"etcd": False, "controlplane": False, "worker": False}
+                    for n in nodes:
                         for r in roles:
                             roles[r] = roles[r] or n["roles"].get(r, False)
-                if c["state"] != "active" and all(roles.values()):
-                    if c.get("ready_at") is None:
-                        c["ready_at"] = now + st.rke_seconds
-                    if now >= c["ready_at"]:
-                        c["state"] = "active"
-                        c["transitioning"] = "no"
-                        st.cond.notify_all()
+                    if all(roles.values()):
+                        if c.get("ready_at") is None:
+                            c["ready_at"] = now + st.rke_seconds
+                        if now >= c["ready_at"]:
+                            c["state"] = "active"
+                            c["transitioning"] = "no"
+                            st.cond.notify_all()
                 if c["state"] == "active":
-                    for n in st.nodes.values():
-                        if n["clusterId"] == c["id"] and n["state"] != "active":
+                    settled = True
+                    for n in nodes:
+                        if n["state"] != "active":
                             if n.get("ready_at") is None:
                                 n["ready_at"] = max(now, c["ready_at"]) + st.node_ready_seconds
                             if now >= n["ready_at"]:
                                 n["state"] = "active"
+                            else:
+                                settled = False
+                    if settled:
+                        st.unsettled.discard(cid)
 
     def device_plugin_applied(self, cluster_id: str) -> bool:
         with self.state.mu:
-            return any(k.startswith(cluster_id + "|") and "daemonsets" in k and "device-plugin" in k
-                       for k in self.state.objects)
+            return any("daemonsets" in k and "device-plugin" in k
+                       for k in self.state.cluster_objects.get(cluster_id, ()))
 
     def k8s_nodes(self, cluster_id: str) -> List[Dict[str, Any]]:
         self._refresh()
@@ -114,9 +129,7 @@ class FakeRancher:
         plugin = self.device_plugin_applied(cluster_id)
         items = []
         with st.mu:
-            for n in st.nodes.values():
-                if n["clusterId"] != cluster_id:
-                    continue
+            for n in st.cluster_nodes.get(cluster_id, {}).values():
                 ready = n["state"] == "active"
                 labels = dict(n["labels"])
                 for r, on in n["roles"].items():
@@ -255,6 +268,8 @@ class FakeRancher:
                 st.clusters[cid] = {"id": cid, "name": body.get("name", ""), "state": "provisioning",
                                     "transitioning": "yes", "rancherKubernetesEngineConfig":
                                         body.get("rancherKubernetesEngineConfig", {}), "created": time.time()}
+                st.cluster_nodes[cid] = {}
+                st.unsettled.add(cid)
                 return 201, dict(st.clusters[cid])
         if path.startswith("/v3/clusters/"):
             rest = path[len("/v3/clusters/"):].split("/")
@@ -269,8 +284,9 @@ class FakeRancher:
             if method == "DELETE":
                 with st.mu:
                     st.clusters.pop(cid, None)
-                    for nid in [n for n, v in st.nodes.items() if v["clusterId"] == cid]:
-                        st.nodes.pop(nid)
+                    st.unsettled.discard(cid)
+                    for nid in st.cluster_nodes.pop(cid, {}):
+                        st.nodes.pop(nid, None)
                 return 200, {}
             if method == "POST" and query.get("action") == ["generateKubeconfig"]:
                 return 200, {"config": f"apiVersion: v1\nkind: Config\nclusters:\n- name: {cid}\n"}
@@ -286,11 +302,16 @@ class FakeRancher:
             self._refresh()
             cids = query.get("clusterId")
             with st.mu:
-                data = [dict(n) for n in st.nodes.values() if not cids or n["clusterId"] in cids]
+                if cids:
+                    data = [dict(n) for c in cids for n in st.cluster_nodes.get(c, {}).values()]
+                else:
+                    data = [dict(n) for n in st.nodes.values()]
             return 200, {"data": data}
         if path.startswith("/v3/nodes/") and method == "DELETE":
             with st.mu:
-                st.nodes.pop(path.rsplit("/", 1)[1], None)
+                n = st.nodes.pop(path.rsplit("/", 1)[1], None)
+                if n is not None:
+                    st.cluster_nodes.get(n["clusterId"], {}).pop(n["id"], None)
             return 200, {}
         if path.startswith("/k8s/clusters/"):
             return self._k8s(method, path, body)
@@ -312,13 +333,14 @@ class FakeRancher:
         roles = {"etcd": bool(node.get("etcd")), "controlplane": bool(node.get("controlPlane")),
                  "worker": bool(node.get("worker"))}
         with st.mu:
-            existing = [nid for nid, n in st.nodes.items()
-                        if n["clusterId"] == reg["clusterId"] and n["hostname"] == hostname]
+            members = st.cluster_nodes.setdefault(reg["clusterId"], {})
+            existing = [nid for nid, n in members.items() if n["hostname"] == hostname]
             nid = existing[0] if existing else f"m-{uuid.uuid4().hex[:6]}"
-            st.nodes[nid] = {"id": nid, "clusterId": reg["clusterId"], "hostname": hostname,
-                             "nodeName": hostname, "roles": roles, "labels": dict(node.get("labels", {})),
-                             "capacity": dict(node.get("capacity", {})), "state": "registering",
-                             "registered": time.time(), "ready_at": None}
+            st.nodes[nid] = members[nid] = {
+                "id": nid, "clusterId": reg["clusterId"], "hostname": hostname, "nodeName": hostname,
+                "roles": roles, "labels": dict(node.get("labels", {})), "capacity": dict(node.get("capacity", {})),
+                "state": "registering", "registered": time.time(), "ready_at": None}
+            st.unsettled.add(reg["clusterId"])
             st.cond.notify_all()
         self._refresh()
         return 201, {"id": nid, "clusterId": reg["clusterId"]}
@@ -348,6 +370,7 @@ class FakeRancher:
                              "creationTimestamp": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())})
                 obj.setdefault("status", {})
                 st.objects[key] = obj
+                st.cluster_objects.setdefault(cid, {})[key] = None
             return 201, obj
         if method in ("PUT", "GET", "DELETE"):
             base, _, name = kpath.rpartition("/")
@@ -355,12 +378,17 @@ class FakeRancher:
             with st.mu:
                 if method == "PUT":
                     st.objects[key] = body
+                    st.cluster_objects.setdefault(cid, {})[key] = None
                     return 200, body
                 if method == "DELETE":
-                    return (200, st.objects.pop(key)) if key in st.objects else (404, {"code": 404})
+                    if key not in st.objects:
+                        return 404, {"code": 404}
+                    st.cluster_objects.get(cid, {}).pop(key, None)
+                    return 200, st.objects.pop(key)
                 if key in st.objects:
                     return 200, st.objects[key]
-                items = [o for k, o in st.objects.items() if k.startswith(f"{cid}|{kpath}|")]
+                prefix = f"{cid}|{kpath}|"
+                items = [st.objects[k] for k in st.cluster_objects.get(cid, ()) if k.startswith(prefix)]
                 return 200, {"items": items}
         return 404, {"kind": "Status", "code": 404}
 
