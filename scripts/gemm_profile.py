@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""One 8192^3 GEMM screen (for rocprofv3 counter passes over k_gemm_bt)."""
+"""One 8192^3 GEMM screen (for rocprofv3 counter passes over k_gemm_bt or, with TKG_SCHED=1, k_gemm8)."""
 import os
 import sys
 

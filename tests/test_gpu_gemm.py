@@ -73,4 +73,26 @@ def test_screen_full_size_throughput():
     r = gemm.screen(0, 8192, 8192, 8192, reps=5)
     print(json.dumps(r.to_json()))
     assert r.ok, r
-    assert r.tflops > 700, r
+    assert r.tflops > 1000, r  # 1.44-1.54 PF measured with the staggered schedule
+
+
+def test_schedules_agree_bitwise():
+    """The staggered 2-phase loop and the single-barrier loop feed every accumulator the same
+    MFMAs in the same K order, so their fp32 outputs are identical, bit for bit; the tail
+    shapes (one and two K-tiles) exercise the vmcnt(0) paths."""
+    import torch
+
+    from triton_kubernetes_amd.ops import gemm
+
+    g = torch.Generator(device="cuda").manual_seed(7)
+    try:
+        for m, n, k in ((256, 256, 64), (256, 512, 128), (768, 512, 192), (1024, 1024, 2048)):
+            a = torch.randn((m, k), device="cuda", generator=g).to(torch.bfloat16)
+            b = torch.randn((n, k), device="cuda", generator=g).to(torch.bfloat16)
+            assert gemm.set_schedule("single-barrier") == "single-barrier"
+            ref = gemm.gemm_bt(a, b)
+            assert gemm.set_schedule("staggered") == "staggered"
+            got = gemm.gemm_bt(a, b)
+            assert torch.equal(got, ref), (m, n, k, (got - ref).abs().max().item())
+    finally:
+        gemm.set_schedule("staggered")

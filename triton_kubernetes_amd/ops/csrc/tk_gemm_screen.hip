@@ -13,17 +13,20 @@
 // right-hand sides from A and B.  A corrupted product — a bad MFMA, LDS or VGPR bit, a
 // wrong staged tile — shows up as a column AND a row mismatch, which also locates it.
 //
-// Kernel structure (gfx950, one 256x256 output tile per 512-thread workgroup):
-//  * 8 waves as 2 (M) x 4 (N); each wave owns 128 x 64 of C as 8 x 4 fragments of
-//    16x16 (32 f32x4 accumulators);
-//  * K in steps of 64: A and B tiles [256][64] bf16 (32 KiB each) are staged into LDS
-//    with 16-byte global_load_lds (8 per thread per step) into two LDS buffers; each
-//    step's fragments are read into VGPRs before its MFMAs, so the copy two steps ahead
-//    can start as soon as a barrier says every wave has read the buffer (see the loop);
+// Kernel structure (gfx950, one 256x256 output tile per 512-thread workgroup, 8 waves,
+// 128 KiB of LDS, K in steps of 64, 16-byte buffer_load ... lds copies HBM -> LDS):
+//  * default, k_gemm8 (schedule 1, "staggered"): the LDS holds half-tiles ([128][64] bf16
+//    of A or B, two K-tiles deep); each wave owns four 64x32 quadrants and a K-tile is two
+//    phases of 32 MFMAs; the two wave groups run one barrier apart, so on every SIMD one
+//    wave issues MFMAs while the other reads LDS and issues copies (details at the kernel).
+//    1.41 / 1.54 PF at 4096^3 / 8192^3 on random data, MFMA pipe 77 % busy;
+//  * k_gemm_bt (schedule 0, "single-barrier", kept for A/B): whole [256][64] tiles in two
+//    buffers, one barrier per K-step, every wave reads then issues 64 MFMAs in lockstep —
+//    1.20 / 1.27 PF, MFMA pipe 61.5 % busy (profiles/round1_gemm_pmc.md);
 //  * the LDS image is XOR-swizzled by 16-byte chunk (chunk ^ ((row >> 1) & 7)): the
 //    swizzle is applied to the per-lane GLOBAL source address (the LDS-DMA destination
 //    is lane-linear), so the 16 lanes of a ds_read_b128 group read 16 distinct bank
-//    slots (row stride 128 B would otherwise give an 8-way conflict);
+//    slots (row stride 128 B would otherwise give an 8-way conflict; 0 conflicts measured);
 //  * blocks are remapped so the tiles one XCD works on share A rows / B columns in its
 //    own L2 (blocks are dispatched round-robin over the 8 XCDs);
 //  * shapes: M, N multiples of 256, K a multiple of 64 — checked on the host before any
@@ -64,6 +67,30 @@ extern "C" const char* tkg_last_error() { return g_err; }
 namespace {
 #ifndef TKG_BK
 #define TKG_BK 64
+#endif
+#ifndef TKG_DEFAULT_SCHED
+#define TKG_DEFAULT_SCHED 1
+#endif
+#ifndef TKG8_LGKM_EARLY  // 8-phase: retire every phase's LDS reads before its first barrier
+#define TKG8_LGKM_EARLY 0
+#endif
+#ifndef TKG8_VM_ONCE  // 8-phase: one vmcnt wait per K-tile (in P3) instead of three
+#define TKG8_VM_ONCE 1
+#endif
+#ifndef TKG8_STAGGER  // 8-phase: wave group 1 one barrier behind group 0
+#define TKG8_STAGGER 1
+#endif
+#ifndef TKG8_PRIO  // 8-phase: s_setprio 1 around the MFMA clusters
+#define TKG8_PRIO 1
+#endif
+#ifndef TKG8_PHASES  // 8-phase kernel: phases per K-tile (4: 16 MFMAs each; 2: 32 each)
+#define TKG8_PHASES 2
+#endif
+#ifndef TKG8_B1EARLY  // 2-phase: refill B1 with A0/B0 in Pb (A1 alone in Pa)
+#define TKG8_B1EARLY 0
+#endif
+#ifndef TKG_GROUP_M  // tile-rows per L2 group in the XCD-aware block map
+#define TKG_GROUP_M 8
 #endif
 constexpr int BM = 256, BN = 256, BK = TKG_BK;                            // K-step 64 (default) or 32
 constexpr int WAVES_M = 2, WAVES_N = 4, THREADS = 64 * WAVES_M * WAVES_N;  // 512
@@ -135,7 +162,7 @@ __device__ __forceinline__ void wait_copies_but(int n) {
 __device__ __forceinline__ void tile_of(int b, int nwg, int tiles_m, int tiles_n, int* tm, int* tn) {
   const int xcd = b & 7, q = nwg >> 3, rem = nwg & 7;
   const int w = (xcd < rem ? xcd * (q + 1) : rem * (q + 1) + (xcd - rem) * q) + (b >> 3);
-  constexpr int GROUP_M = 8;
+  constexpr int GROUP_M = TKG_GROUP_M;
   const int per_group = GROUP_M * tiles_n;
   const int g = w / per_group, first_m = g * GROUP_M;
   const int rows = min(tiles_m - first_m, GROUP_M);
@@ -273,6 +300,378 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
   }
 }
 
+// --- 8-phase schedule (two staggered wave groups) -------------------------------------------
+// Same 256x256 output tile, 8 waves, BK = 64, 128 KiB of LDS, but the LDS holds half-tiles:
+// slot (t & 1, h) for h = A0 | A1 | B0 | B1 = rows 0-127 / 128-255 of the A or B panel of
+// K-tile t, [128][64] bf16 each (16 KiB, same XOR swizzle).  Wave (wr, wc) owns the four
+// 64x32 quadrants (mh, nh): rows mh*128 + wr*64 .. +63, columns nh*128 + wc*32 .. +31, so
+// quadrant (mh, nh) reads only half-tiles A{mh} and B{nh}.  A K-tile is four phases
+//   P0: read A0 + B0 -> quadrant (0,0)    P1: read B1 -> (0,1)
+//   P2: read A1      -> (1,1)             P3: (no reads) -> (1,0)
+// (B0 and B1 stay in registers for the K-tile), each phase
+//   [ds_reads][stage one half-tile][s_waitcnt lgkmcnt(0) vmcnt(..)] s_barrier [16 MFMAs] s_barrier
+// Group wr = 1 runs one barrier behind group wr = 0 (one extra s_barrier at the start, the
+// other group's at the end), so on every SIMD — which holds one wave of each group — one wave
+// issues MFMAs while the other reads LDS and issues copies.
+// Staging: a slot is refilled one phase after its last read (P0(t): A1(t+1); P1..P3(t):
+// A0, B0, B1 of t+2); the reads are retired (lgkmcnt(0)) before the reading phase's first
+// barrier, which with the one-slot stagger orders them before the refill (WAR).  A half-tile
+// is waited for (vmcnt: 5 younger stages = 10 copies may stay in flight) before the first
+// barrier of the phase BEFORE the one that reads it (RAW, one barrier of margin for the
+// stagger).  The last two K-tiles wait with vmcnt(0): fewer younger copies exist there.
+namespace p8 {
+constexpr int BKP = 64, HROWS = 128;
+constexpr int HBYTES = HROWS * BKP * 2;       // 16 KiB
+constexpr int HCOPIES = HBYTES / (THREADS * 16);  // 2 copies per thread per half-tile
+constexpr int LDS = 8 * HBYTES;               // 128 KiB
+constexpr int ROWS_PER_COPY8 = THREADS / 8;    // 64
+static_assert(HCOPIES == 2, "copies per half-tile");
+
+__device__ __forceinline__ int swz8(int r, int c) { return c ^ ((r >> 1) & 7); }
+__device__ __forceinline__ bf16x8 frag(const char* img, int r, int c) {
+  return *reinterpret_cast<const bf16x8*>(img + r * (BKP * 2) + swz8(r, c) * 16);
+}
+__device__ __forceinline__ char* slot(char* smem, int t, int h) { return smem + ((t & 1) * 4 + h) * HBYTES; }
+__device__ __forceinline__ int voffset(int ld, int tid) {
+  const int r = tid >> 3, c = swz8(r, tid & 7);
+  return (r * ld + c * 8) * 2;
+}
+__device__ __forceinline__ void stage_half(__amdgpu_buffer_rsrc_t panel, int ld, int voff, int row_off, int k0,
+                                           char* dst, int tid) {
+#pragma unroll
+  for (int i = 0; i < HCOPIES; ++i) {
+    char* d = dst + (size_t)(i * THREADS + (tid & ~63)) * 16;
+    const int soff = ((row_off + i * ROWS_PER_COPY8) * ld + k0) * 2;
+    __builtin_amdgcn_raw_ptr_buffer_load_lds(panel, reinterpret_cast<__shared__ void*>(d), 16, voff, soff, 0, 0);
+  }
+}
+__device__ __forceinline__ void sync_phase(bool full) {
+  if (full) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+}
+__device__ __forceinline__ void sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
+__device__ __forceinline__ void barrier() {
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+}  // namespace p8
+
+template <int MODE>
+__global__ __launch_bounds__(THREADS) void k_gemm8(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+                                                   float* __restrict__ C, float* __restrict__ colpart,
+                                                   float* __restrict__ rowpart, int M, int N, int K,
+                                                   long long inject) {
+  using namespace p8;
+  extern __shared__ __attribute__((aligned(16))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63, wid = tid >> 6;
+  const int wr = wid >> 2, wc = wid & 3;
+  const int tiles_m = M / BM, tiles_n = N / BN;
+  int tm, tn;
+  tile_of(blockIdx.x, gridDim.x, tiles_m, tiles_n, &tm, &tn);
+  const int row0 = tm * BM, col0 = tn * BN;
+  const int fr = lane & 15, fq = lane >> 4;
+
+  f32x4 acc[2][2][4][2];
+#pragma unroll
+  for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) acc[mh][nh][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int nk = K / BKP;
+  const __amdgpu_buffer_rsrc_t pa = make_panel(A, row0, K), pb = make_panel(B, col0, K);
+  const int voff = voffset(K, tid);
+  auto stage = [&](int t, int h) {  // h: 0 A0, 1 A1, 2 B0, 3 B1
+    stage_half(h < 2 ? pa : pb, K, voff, (h & 1) * HROWS, t * BKP, slot(smem, t, h), tid);
+  };
+  bf16x8 a[2][4], b[2][2][2];
+  auto read_a = [&](int t, int mh) {
+    const char* img = slot(smem, t, mh);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) a[kk][i] = frag(img, wr * 64 + i * 16 + fr, kk * 4 + fq);
+  };
+  auto read_b = [&](int t, int nh) {
+    const char* img = slot(smem, t, 2 + nh);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) b[nh][kk][j] = frag(img, wc * 32 + j * 16 + fr, kk * 4 + fq);
+  };
+  auto quad = [&](int mh, int nh) {
+    if (TKG8_PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j)
+          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[nh][kk][j], acc[mh][nh][i][j], 0, 0, 0);
+    if (TKG8_PRIO) __builtin_amdgcn_s_setprio(0);
+  };
+
+#if TKG8_PHASES == 2 && TKG8_B1EARLY
+  // Two phases per K-tile, 32 MFMAs each:
+  //   Pa(t): read A0, B0, B1 -> quadrants (0,0), (0,1); refill A1 of t+1
+  //   Pb(t): read A1         -> quadrants (1,1), (1,0); refill A0, B0, B1 of t+2
+  // Every slot is refilled one phase after its last read, so each phase retires its reads
+  // (lgkmcnt(0)) before its first barrier.  Waits: Pa(t) retires A1(t) for Pb(t), Pb(t)
+  // retires A0/B0/B1 of t+1 for Pa(t+1); 4 younger stages (vmcnt(8)) may stay in flight,
+  // vmcnt(0) in the last K-tiles.
+  stage(0, 0);
+  stage(0, 2);
+  stage(0, 3);
+  stage(0, 1);
+  if (nk > 1) {
+    stage(1, 0);
+    stage(1, 2);
+    stage(1, 3);
+  }
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0, B1 of K-tile 0
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  barrier();
+  if (TKG8_STAGGER && wr == 1) barrier();  // the stagger
+
+  for (int t = 0; t < nk; ++t) {
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+    read_a(t, 0);
+    read_b(t, 0);
+    read_b(t, 1);
+    if (more1) {
+      stage(t + 1, 1);
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    barrier();
+    quad(0, 0);
+    quad(0, 1);
+    barrier();
+    read_a(t, 1);
+    if (more2) {
+      stage(t + 2, 0);
+      stage(t + 2, 2);
+      stage(t + 2, 3);
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    barrier();
+    quad(1, 1);
+    quad(1, 0);
+    barrier();
+  }
+#elif TKG8_PHASES == 2
+  // Two phases per K-tile, 32 MFMAs each:
+  //   Pa(t): read A0, B0, B1 -> quadrants (0,0), (0,1); refill B1, A1 of t+1
+  //   Pb(t): read A1         -> quadrants (1,1), (1,0); refill A0, B0 of t+2
+  // A0/B0(t) are refilled one phase after their reads (retired before Pa's barrier:
+  // lgkmcnt(4) leaves only the B1 reads in flight), B1(t) two phases after, A1(t) one.
+  // Waits: Pa(t) retires A1(t) (4 younger stages: vmcnt(8)), Pb(t) retires A0/B0/B1 of t+1
+  // (3 younger: vmcnt(6)); vmcnt(0) where fewer younger copies exist.
+  stage(0, 0);
+  stage(0, 2);
+  stage(0, 3);
+  stage(0, 1);
+  if (nk > 1) {
+    stage(1, 0);
+    stage(1, 2);
+  }
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0, B0, B1 of K-tile 0
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  barrier();
+  if (TKG8_STAGGER && wr == 1) barrier();  // the stagger
+
+  for (int t = 0; t < nk; ++t) {
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+    read_a(t, 0);
+    read_b(t, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(t, 1);
+    if (more1) {
+      stage(t + 1, 3);
+      stage(t + 1, 1);
+      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(4)" ::: "memory");
+    }
+    barrier();
+    quad(0, 0);
+    quad(0, 1);
+    barrier();
+    read_a(t, 1);
+    if (more2) {
+      stage(t + 2, 0);
+      stage(t + 2, 2);
+      asm volatile("s_waitcnt vmcnt(6) lgkmcnt(0)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+    }
+    barrier();
+    quad(1, 1);
+    quad(1, 0);
+    barrier();
+  }
+#else
+  // prologue: K-tile 0 whole, K-tile 1 but A1 (staged in P0(0)); wait for A0(0), B0(0)
+  stage(0, 0);
+  stage(0, 2);
+  stage(0, 3);
+  stage(0, 1);
+  if (nk > 1) {
+    stage(1, 0);
+    stage(1, 2);
+    stage(1, 3);
+  }
+#if TKG8_VM_ONCE
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // all of K-tile 0
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+  sync_phase(nk > 1);
+#endif
+  barrier();
+  if (TKG8_STAGGER && wr == 1) barrier();  // the stagger
+
+  for (int t = 0; t < nk; ++t) {
+    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
+    // P0: A0, B0 -> (0,0); refill A1 of t+1
+    read_a(t, 0);
+#if TKG8_LGKM_EARLY
+    read_b(t, 0);
+    if (more1) stage(t + 1, 1);
+#if !TKG8_VM_ONCE
+    sync_phase(more1);  // + B1(t) for P1
+#else
+    sync_lds();
+#endif
+#else
+    // A0(t)'s slot is refilled in P1: retire those 8 reads before the barrier; B0(t)'s slot
+    // is refilled two phases on, so its reads may land after it
+    __builtin_amdgcn_sched_barrier(0);
+    read_b(t, 0);
+    if (more1) stage(t + 1, 1);
+#if !TKG8_VM_ONCE
+    if (more1) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(4)" ::: "memory");
+#else
+    asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
+#endif
+#endif
+    barrier();
+    quad(0, 0);
+    barrier();
+    // P1: B1 -> (0,1); refill A0 of t+2
+    read_b(t, 1);
+    if (more2) stage(t + 2, 0);
+#if !TKG8_VM_ONCE
+    if (TKG8_LGKM_EARLY) sync_phase(more2);  // + A1(t) for P2
+    else if (more2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+    if (TKG8_LGKM_EARLY) sync_lds();
+#endif
+    barrier();
+    quad(0, 1);
+    barrier();
+    // P2: A1 -> (1,1); refill B0 of t+2
+    read_a(t, 1);
+    if (more2) stage(t + 2, 2);
+    if (TKG8_LGKM_EARLY) sync_lds();
+    barrier();
+    quad(1, 1);
+    barrier();
+    // P3: -> (1,0); refill B1 of t+2; retire what P0(t+1) reads (TKG8_VM_ONCE: all of t+1,
+    // 3 younger stages = 6 copies may stay in flight)
+    if (more2) stage(t + 2, 3);
+#if !TKG8_VM_ONCE
+    sync_phase(more2);
+#else
+    if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#endif
+    barrier();
+    quad(1, 0);
+    barrier();
+  }
+#endif
+  if (TKG8_STAGGER && wr == 0) barrier();  // match the stagger's extra barrier
+
+  // accumulator element (mh, nh, i, j, e): row = mh*128 + wr*64 + i*16 + fq*4 + e,
+  //                                         col = nh*128 + wc*32 + j*16 + fr
+  if constexpr (MODE == 0) {
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j)
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const int r = row0 + mh * 128 + wr * 64 + i * 16 + fq * 4 + e;
+              const int c = col0 + nh * 128 + wc * 32 + j * 16 + fr;
+              C[(size_t)r * N + c] = acc[mh][nh][i][j][e];
+            }
+  } else {
+    if (inject >= 0) {
+      const long long ir = inject / N, ic = inject % N;
+#pragma unroll
+      for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+        for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 2; ++j)
+#pragma unroll
+              for (int e = 0; e < 4; ++e)
+                if (row0 + mh * 128 + wr * 64 + i * 16 + fq * 4 + e == ir &&
+                    col0 + nh * 128 + wc * 32 + j * 16 + fr == ic)
+                  acc[mh][nh][i][j][e] += 1024.f;
+    }
+    // column sums over the wave's 128 rows (both row halves)
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int j = 0; j < 2; ++j) {
+        float s = 0.f;
+#pragma unroll
+        for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+            s += acc[mh][nh][i][j][0] + acc[mh][nh][i][j][1] + acc[mh][nh][i][j][2] + acc[mh][nh][i][j][3];
+        s += __shfl_xor(s, 16, 64);
+        s += __shfl_xor(s, 32, 64);
+        if (fq == 0) colpart[(size_t)(tm * WAVES_M + wr) * N + col0 + nh * 128 + wc * 32 + j * 16 + fr] = s;
+      }
+    // row sums over the wave's 64 columns (both column halves)
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float s = 0.f;
+#pragma unroll
+          for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+            for (int j = 0; j < 2; ++j) s += acc[mh][nh][i][j][e];
+          s += __shfl_xor(s, 1, 64);
+          s += __shfl_xor(s, 2, 64);
+          s += __shfl_xor(s, 4, 64);
+          s += __shfl_xor(s, 8, 64);
+          if (fr == 0)
+            rowpart[(size_t)(tn * WAVES_N + wc) * M + row0 + mh * 128 + wr * 64 + i * 16 + fq * 4 + e] = s;
+        }
+  }
+}
+
 // --- checksum right-hand sides and comparison (fp32 SIMT, independent of the MFMA path) ----
 // out[k] += sum over this block's chunk of rows of X[r][k] (X is [rows][K] bf16); grid.y
 // splits the rows, partial sums meet in fp32 atomics (out / out_abs zeroed beforehand)
@@ -353,19 +752,42 @@ static int check_shape(int M, int N, int K) {
   return 0;
 }
 
+// schedule: 0 = one barrier per K-step (k_gemm_bt), 1 = 8-phase staggered (k_gemm8, BK 64);
+// env TKG_SCHED or tkg_set_schedule() selects it (A/B in one process: scripts/gemm_ab.py)
+static int g_sched = -1;
+
+static int schedule() {
+  if (g_sched < 0) {
+    const char* e = getenv("TKG_SCHED");
+    g_sched = e ? atoi(e) : TKG_DEFAULT_SCHED;
+  }
+  return (g_sched == 1 && BK == p8::BKP) ? 1 : 0;
+}
+
+extern "C" int tkg_set_schedule(int s) {
+  g_sched = s;
+  return schedule();
+}
+
 static hipError_t launch_gemm(int mode, const __bf16* A, const __bf16* B, float* C, float* colpart, float* rowpart,
                               int M, int N, int K, long long inject, hipStream_t s) {
   const int grid = (M / BM) * (N / BN);
-  if (mode == 0) k_gemm_bt<0><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
-  else k_gemm_bt<1><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+  if (schedule() == 1) {
+    if (mode == 0) k_gemm8<0><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+    else k_gemm8<1><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+  } else {
+    if (mode == 0) k_gemm_bt<0><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+    else k_gemm_bt<1><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+  }
   return hipGetLastError();
 }
 
 static hipError_t set_lds_limit() {
   static hipError_t once = [] {
-    const void* fns[] = {reinterpret_cast<const void*>(&k_gemm_bt<0>), reinterpret_cast<const void*>(&k_gemm_bt<1>)};
+    const void* fns[] = {reinterpret_cast<const void*>(&k_gemm_bt<0>), reinterpret_cast<const void*>(&k_gemm_bt<1>),
+                         reinterpret_cast<const void*>(&k_gemm8<0>), reinterpret_cast<const void*>(&k_gemm8<1>)};
     for (const void* f : fns) {
-      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, LDS_BYTES);
+      hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
       if (e != hipSuccess) return e;
     }
     return hipSuccess;

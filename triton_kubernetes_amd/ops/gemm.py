@@ -30,7 +30,21 @@ def _lib():
                                 ctypes.c_int, ctypes.c_int, ctypes.c_int]
     lib.tkg_screen.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
+    lib.tkg_set_schedule.argtypes = [ctypes.c_int]
     return lib
+
+
+SCHEDULES = {"staggered": 1, "single-barrier": 0}
+
+
+def set_schedule(name: str) -> str:
+    """Select the GEMM main loop: ``staggered`` (default: two wave groups one barrier apart,
+    two phases per K-tile) or ``single-barrier`` (one barrier per K-step, kept for A/B).
+    Returns the schedule in effect."""
+    if name not in SCHEDULES:
+        raise GemmError(f"unknown schedule '{name}' ({' | '.join(SCHEDULES)})")
+    got = _lib().tkg_set_schedule(SCHEDULES[name])
+    return next(k for k, v in SCHEDULES.items() if v == got)
 
 
 def check_shape(m: int, n: int, k: int) -> None:
