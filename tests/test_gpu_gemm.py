@@ -96,3 +96,53 @@ def test_schedules_agree_bitwise():
             assert torch.equal(got, ref), (m, n, k, (got - ref).abs().max().item())
     finally:
         gemm.set_schedule("staggered")
+
+
+# --- fp8 e4m3 (block-scaled 16x16x128 MFMA, unit scales) ------------------------------------------
+
+
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (512, 768, 1024), (1024, 256, 4096)])
+def test_fp8_gemm_matches_fp32_reference(m, n, k):
+    import torch
+
+    from triton_kubernetes_amd.ops import gemm
+
+    g = torch.Generator(device="cuda").manual_seed(m * 3 + n + k)
+    a = (torch.rand((m, k), device="cuda", generator=g) * 4 - 2).to(torch.float8_e4m3fn)
+    b = (torch.rand((n, k), device="cuda", generator=g) * 4 - 2).to(torch.float8_e4m3fn)
+    got = gemm.gemm_bt(a, b)
+    ref = a.float() @ b.float().T
+    torch.cuda.synchronize()
+    err = (got - ref).abs().max().item()
+    assert err <= 1e-4 * max(1.0, (a.float().abs() @ b.float().abs().T).max().item()), err
+
+
+def test_fp8_gemm_exact_on_integer_data_asymmetric():
+    """Small integers are exact in e4m3 and their sums exact in fp32: any fragment, k-order
+    or epilogue mix-up of the fp8 path shows as a nonzero difference."""
+    import torch
+
+    from triton_kubernetes_amd.ops import gemm
+
+    m, n, k = 512, 256, 256
+    a = (torch.arange(m * k, device="cuda").reshape(m, k) % 7 - 3).to(torch.float8_e4m3fn)
+    b = ((torch.arange(n * k, device="cuda").reshape(n, k) * 3 + torch.arange(n, device="cuda")[:, None]) % 5 - 2
+         ).to(torch.float8_e4m3fn)
+    got = gemm.gemm_bt(a, b)
+    ref = a.float() @ b.float().T
+    torch.cuda.synchronize()
+    assert torch.equal(got, ref), (got - ref).abs().max().item()
+
+
+def test_fp8_screen_passes_catches_fault_and_runs_at_rate():
+    from triton_kubernetes_amd.ops import gemm
+
+    with pytest.raises(gemm.GemmError):
+        gemm.screen(0, 256, 256, 64, dtype="fp8")  # K must be a multiple of 128 for fp8
+    ok = gemm.screen(0, 8192, 8192, 8192, reps=5, dtype="fp8")
+    print(json.dumps(ok.to_json()))
+    assert ok.ok and ok.max_norm_error < 0.5 and ok.dtype == "fp8", ok
+    assert ok.tflops > 2000, ok
+    row, col = 777, 4095
+    bad = gemm.screen(0, 4096, 4096, 4096, reps=1, inject=row * 4096 + col, dtype="fp8")
+    assert not bad.ok and (bad.first_bad_row, bad.first_bad_column) == (row, col), bad

@@ -48,6 +48,8 @@
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4;
+typedef __attribute__((ext_vector_type(4))) int i32x4;
+typedef __attribute__((ext_vector_type(8))) int i32x8;
 
 static thread_local char g_err[512];
 
@@ -71,23 +73,11 @@ namespace {
 #ifndef TKG_DEFAULT_SCHED
 #define TKG_DEFAULT_SCHED 1
 #endif
-#ifndef TKG8_LGKM_EARLY  // 8-phase: retire every phase's LDS reads before its first barrier
-#define TKG8_LGKM_EARLY 0
-#endif
-#ifndef TKG8_VM_ONCE  // 8-phase: one vmcnt wait per K-tile (in P3) instead of three
-#define TKG8_VM_ONCE 1
-#endif
-#ifndef TKG8_STAGGER  // 8-phase: wave group 1 one barrier behind group 0
+#ifndef TKG8_STAGGER  // staggered schedule: wave group 1 one barrier behind group 0 (0: lockstep, for A/B)
 #define TKG8_STAGGER 1
 #endif
-#ifndef TKG8_PRIO  // 8-phase: s_setprio 1 around the MFMA clusters
+#ifndef TKG8_PRIO  // staggered schedule: s_setprio 1 around the MFMA clusters
 #define TKG8_PRIO 1
-#endif
-#ifndef TKG8_PHASES  // 8-phase kernel: phases per K-tile (4: 16 MFMAs each; 2: 32 each)
-#define TKG8_PHASES 2
-#endif
-#ifndef TKG8_B1EARLY  // 2-phase: refill B1 with A0/B0 in Pb (A1 alone in Pa)
-#define TKG8_B1EARLY 0
 #endif
 #ifndef TKG_GROUP_M  // tile-rows per L2 group in the XCD-aware block map
 #define TKG_GROUP_M 8
@@ -300,56 +290,62 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
   }
 }
 
-// --- 8-phase schedule (two staggered wave groups) -------------------------------------------
-// Same 256x256 output tile, 8 waves, BK = 64, 128 KiB of LDS, but the LDS holds half-tiles:
-// slot (t & 1, h) for h = A0 | A1 | B0 | B1 = rows 0-127 / 128-255 of the A or B panel of
-// K-tile t, [128][64] bf16 each (16 KiB, same XOR swizzle).  Wave (wr, wc) owns the four
-// 64x32 quadrants (mh, nh): rows mh*128 + wr*64 .. +63, columns nh*128 + wc*32 .. +31, so
-// quadrant (mh, nh) reads only half-tiles A{mh} and B{nh}.  A K-tile is four phases
-//   P0: read A0 + B0 -> quadrant (0,0)    P1: read B1 -> (0,1)
-//   P2: read A1      -> (1,1)             P3: (no reads) -> (1,0)
-// (B0 and B1 stay in registers for the K-tile), each phase
-//   [ds_reads][stage one half-tile][s_waitcnt lgkmcnt(0) vmcnt(..)] s_barrier [16 MFMAs] s_barrier
-// Group wr = 1 runs one barrier behind group wr = 0 (one extra s_barrier at the start, the
-// other group's at the end), so on every SIMD — which holds one wave of each group — one wave
-// issues MFMAs while the other reads LDS and issues copies.
-// Staging: a slot is refilled one phase after its last read (P0(t): A1(t+1); P1..P3(t):
-// A0, B0, B1 of t+2); the reads are retired (lgkmcnt(0)) before the reading phase's first
-// barrier, which with the one-slot stagger orders them before the refill (WAR).  A half-tile
-// is waited for (vmcnt: 5 younger stages = 10 copies may stay in flight) before the first
-// barrier of the phase BEFORE the one that reads it (RAW, one barrier of margin for the
-// stagger).  The last two K-tiles wait with vmcnt(0): fewer younger copies exist there.
+// --- staggered schedule (k_gemm8: bf16 and fp8) ------------------------------------------
+// Same 256x256 output tile, 8 waves and 128 KiB of LDS as k_gemm_bt; a K-tile is 128 bytes
+// of every row (64 bf16 or 128 fp8 e4m3), so one code path serves both element types.
+// The LDS holds half-tiles: slot (t & 1, h) for h = A0 | A1 | B0 | B1 = rows 0-127 /
+// 128-255 of the A or B panel of K-tile t, [128][128 B] each (16 KiB, same XOR swizzle).
+// Wave (wr, wc) owns four 64x32 quadrants (mh, nh): rows mh*128 + wr*64 .. +63, columns
+// nh*128 + wc*32 .. +31, so quadrant (mh, nh) reads only half-tiles A{mh} and B{nh}.  A
+// K-tile is two phases of 32 MFMAs (bf16: 16x16x32 x2 per fragment pair; fp8: one
+// block-scaled 16x16x128 at twice the cycles and four times the K):
+//   Pa(t): read A0, B0, B1 -> quadrants (0,0), (0,1); refill B1, A1 of t+1
+//   Pb(t): read A1         -> quadrants (1,1), (1,0); refill A0, B0 of t+2
+// each  [ds_reads][copies][s_waitcnt vmcnt(..) lgkmcnt(..)] s_barrier [32 MFMAs] s_barrier.
+// Group wr = 1 runs one barrier behind group wr = 0 (an extra s_barrier at the start, the
+// other group's at the end), so on every SIMD — which holds one wave of each group — one
+// wave issues MFMAs while the other reads LDS and issues copies.
+// WAR: A0/B0(t) are refilled one phase after their reads, so Pa retires those 12 reads
+// (lgkmcnt(4): the 4 B1 reads, issued last, may stay in flight) before its first barrier;
+// with the stagger that orders them before the other group's refill.  B1(t) is refilled two
+// phases on; A1(t) one phase on (Pb retires all its reads).
+// RAW: a half-tile is waited for before the first barrier of the phase BEFORE the one that
+// reads it (one barrier of margin for the stagger): Pa(t) retires A1(t) (4 younger stages
+// = 8 copies may stay in flight), Pb(t) retires A0/B0/B1 of t+1 (3 younger: vmcnt(6)); the
+// last K-tiles wait with vmcnt(0), where fewer younger copies exist.
+// (Variants measured on the way — four phases of 16 MFMAs, other wait placements, B1 refilled
+// early, no stagger — and their counters: profiles/round1_gemm_pmc.md.)
 namespace p8 {
-constexpr int BKP = 64, HROWS = 128;
-constexpr int HBYTES = HROWS * BKP * 2;       // 16 KiB
+constexpr int KT_BYTES = 128, HROWS = 128;       // bytes of a row per K-tile; rows per half-tile
+constexpr int HBYTES = HROWS * KT_BYTES;         // 16 KiB
 constexpr int HCOPIES = HBYTES / (THREADS * 16);  // 2 copies per thread per half-tile
-constexpr int LDS = 8 * HBYTES;               // 128 KiB
-constexpr int ROWS_PER_COPY8 = THREADS / 8;    // 64
+constexpr int LDS = 8 * HBYTES;                  // 128 KiB
+constexpr int ROWS_PER_COPY8 = THREADS / 8;       // 64
 static_assert(HCOPIES == 2, "copies per half-tile");
 
 __device__ __forceinline__ int swz8(int r, int c) { return c ^ ((r >> 1) & 7); }
-__device__ __forceinline__ bf16x8 frag(const char* img, int r, int c) {
-  return *reinterpret_cast<const bf16x8*>(img + r * (BKP * 2) + swz8(r, c) * 16);
+__device__ __forceinline__ u32x4 chunk(const char* img, int r, int c) {
+  return *reinterpret_cast<const u32x4*>(img + r * KT_BYTES + swz8(r, c) * 16);
 }
 __device__ __forceinline__ char* slot(char* smem, int t, int h) { return smem + ((t & 1) * 4 + h) * HBYTES; }
-__device__ __forceinline__ int voffset(int ld, int tid) {
+// this thread's byte offset in a panel of rows `ldb` bytes long (see panel_voffset)
+__device__ __forceinline__ int voffset(int ldb, int tid) {
   const int r = tid >> 3, c = swz8(r, tid & 7);
-  return (r * ld + c * 8) * 2;
+  return r * ldb + c * 16;
 }
-__device__ __forceinline__ void stage_half(__amdgpu_buffer_rsrc_t panel, int ld, int voff, int row_off, int k0,
+__device__ __forceinline__ void stage_half(__amdgpu_buffer_rsrc_t panel, int ldb, int voff, int row_off, int kb0,
                                            char* dst, int tid) {
 #pragma unroll
   for (int i = 0; i < HCOPIES; ++i) {
     char* d = dst + (size_t)(i * THREADS + (tid & ~63)) * 16;
-    const int soff = ((row_off + i * ROWS_PER_COPY8) * ld + k0) * 2;
+    const int soff = (row_off + i * ROWS_PER_COPY8) * ldb + kb0;
     __builtin_amdgcn_raw_ptr_buffer_load_lds(panel, reinterpret_cast<__shared__ void*>(d), 16, voff, soff, 0, 0);
   }
 }
-__device__ __forceinline__ void sync_phase(bool full) {
-  if (full) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(0)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t panel(const void* base, int row0, int ldb) {
+  return __builtin_amdgcn_make_buffer_rsrc(const_cast<char*>(static_cast<const char*>(base) + (size_t)row0 * ldb), 0,
+                                           BM * ldb, 0x00020000);
 }
-__device__ __forceinline__ void sync_lds() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 __device__ __forceinline__ void barrier() {
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
@@ -357,8 +353,9 @@ __device__ __forceinline__ void barrier() {
 }
 }  // namespace p8
 
-template <int MODE>
-__global__ __launch_bounds__(THREADS) void k_gemm8(const __bf16* __restrict__ A, const __bf16* __restrict__ B,
+// ESIZE 2: bf16, ESIZE 1: fp8 e4m3 (OCP).  K counts elements.
+template <int MODE, int ESIZE>
+__global__ __launch_bounds__(THREADS) void k_gemm8(const void* __restrict__ A, const void* __restrict__ B,
                                                    float* __restrict__ C, float* __restrict__ colpart,
                                                    float* __restrict__ rowpart, int M, int N, int K,
                                                    long long inject) {
@@ -382,98 +379,62 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const __bf16* __restrict__ A,
 #pragma unroll
         for (int j = 0; j < 2; ++j) acc[mh][nh][i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = K / BKP;
-  const __amdgpu_buffer_rsrc_t pa = make_panel(A, row0, K), pb = make_panel(B, col0, K);
-  const int voff = voffset(K, tid);
+  const int ldb = K * ESIZE, nk = ldb / KT_BYTES;
+  const __amdgpu_buffer_rsrc_t pa = panel(A, row0, ldb), pb = panel(B, col0, ldb);
+  const int voff = voffset(ldb, tid);
   auto stage = [&](int t, int h) {  // h: 0 A0, 1 A1, 2 B0, 3 B1
-    stage_half(h < 2 ? pa : pb, K, voff, (h & 1) * HROWS, t * BKP, slot(smem, t, h), tid);
+    stage_half(h < 2 ? pa : pb, ldb, voff, (h & 1) * HROWS, t * KT_BYTES, slot(smem, t, h), tid);
   };
-  bf16x8 a[2][4], b[2][2][2];
+  // A fragment of one 16-row group for the whole K-tile: two 16-byte chunks per lane.  bf16:
+  // chunks fq and 4 + fq (two 16x16x32 k-steps, lane holds k = 8 fq .. +7 of each); fp8:
+  // chunks 2 fq, 2 fq + 1 (one 16x16x128 step, lane holds k = 32 fq .. +31).  A and B use the
+  // same map, so every product pairs equal k.
+  u32x4 a[4][2], b[2][2][2];
+  auto ld_frag = [&](const char* img, int r, u32x4* f) {
+    if constexpr (ESIZE == 2) {
+      f[0] = chunk(img, r, fq);
+      f[1] = chunk(img, r, 4 + fq);
+    } else {
+      f[0] = chunk(img, r, 2 * fq);
+      f[1] = chunk(img, r, 2 * fq + 1);
+    }
+  };
   auto read_a = [&](int t, int mh) {
     const char* img = slot(smem, t, mh);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int i = 0; i < 4; ++i) a[kk][i] = frag(img, wr * 64 + i * 16 + fr, kk * 4 + fq);
+    for (int i = 0; i < 4; ++i) ld_frag(img, wr * 64 + i * 16 + fr, a[i]);
   };
   auto read_b = [&](int t, int nh) {
     const char* img = slot(smem, t, 2 + nh);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) b[nh][kk][j] = frag(img, wc * 32 + j * 16 + fr, kk * 4 + fq);
+    for (int j = 0; j < 2; ++j) ld_frag(img, wc * 32 + j * 16 + fr, b[nh][j]);
   };
   auto quad = [&](int mh, int nh) {
     if (TKG8_PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < 2; ++j) {
+        if constexpr (ESIZE == 2) {
 #pragma unroll
-        for (int j = 0; j < 2; ++j)
-          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[kk][i], b[nh][kk][j], acc[mh][nh][i][j], 0, 0, 0);
+          for (int kk = 0; kk < 2; ++kk)
+            acc[mh][nh][i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                __builtin_bit_cast(bf16x8, a[i][kk]), __builtin_bit_cast(bf16x8, b[nh][j][kk]), acc[mh][nh][i][j], 0,
+                0, 0);
+        } else {
+          const i32x8 av = __builtin_shufflevector(__builtin_bit_cast(i32x4, a[i][0]), __builtin_bit_cast(i32x4, a[i][1]),
+                                                   0, 1, 2, 3, 4, 5, 6, 7);
+          const i32x8 bv = __builtin_shufflevector(__builtin_bit_cast(i32x4, b[nh][j][0]),
+                                                   __builtin_bit_cast(i32x4, b[nh][j][1]), 0, 1, 2, 3, 4, 5, 6, 7);
+          // FMT 0 = fp8 e4m3 for A and B; E8M0 scales 127 = 2^0
+          acc[mh][nh][i][j] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(av, bv, acc[mh][nh][i][j], 0, 0, 0,
+                                                                               127, 0, 127);
+        }
+      }
     if (TKG8_PRIO) __builtin_amdgcn_s_setprio(0);
   };
 
-#if TKG8_PHASES == 2 && TKG8_B1EARLY
-  // Two phases per K-tile, 32 MFMAs each:
-  //   Pa(t): read A0, B0, B1 -> quadrants (0,0), (0,1); refill A1 of t+1
-  //   Pb(t): read A1         -> quadrants (1,1), (1,0); refill A0, B0, B1 of t+2
-  // Every slot is refilled one phase after its last read, so each phase retires its reads
-  // (lgkmcnt(0)) before its first barrier.  Waits: Pa(t) retires A1(t) for Pb(t), Pb(t)
-  // retires A0/B0/B1 of t+1 for Pa(t+1); 4 younger stages (vmcnt(8)) may stay in flight,
-  // vmcnt(0) in the last K-tiles.
-  stage(0, 0);
-  stage(0, 2);
-  stage(0, 3);
-  stage(0, 1);
-  if (nk > 1) {
-    stage(1, 0);
-    stage(1, 2);
-    stage(1, 3);
-  }
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");  // A0, B0, B1 of K-tile 0
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  barrier();
-  if (TKG8_STAGGER && wr == 1) barrier();  // the stagger
-
-  for (int t = 0; t < nk; ++t) {
-    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
-    read_a(t, 0);
-    read_b(t, 0);
-    read_b(t, 1);
-    if (more1) {
-      stage(t + 1, 1);
-      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    barrier();
-    quad(0, 0);
-    quad(0, 1);
-    barrier();
-    read_a(t, 1);
-    if (more2) {
-      stage(t + 2, 0);
-      stage(t + 2, 2);
-      stage(t + 2, 3);
-      asm volatile("s_waitcnt vmcnt(8) lgkmcnt(0)" ::: "memory");
-    } else {
-      asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
-    }
-    barrier();
-    quad(1, 1);
-    quad(1, 0);
-    barrier();
-  }
-#elif TKG8_PHASES == 2
-  // Two phases per K-tile, 32 MFMAs each:
-  //   Pa(t): read A0, B0, B1 -> quadrants (0,0), (0,1); refill B1, A1 of t+1
-  //   Pb(t): read A1         -> quadrants (1,1), (1,0); refill A0, B0 of t+2
-  // A0/B0(t) are refilled one phase after their reads (retired before Pa's barrier:
-  // lgkmcnt(4) leaves only the B1 reads in flight), B1(t) two phases after, A1(t) one.
-  // Waits: Pa(t) retires A1(t) (4 younger stages: vmcnt(8)), Pb(t) retires A0/B0/B1 of t+1
-  // (3 younger: vmcnt(6)); vmcnt(0) where fewer younger copies exist.
+  // prologue: K-tile 0 whole plus A0/B0 of K-tile 1; wait for A0, B0, B1 of K-tile 0
   stage(0, 0);
   stage(0, 2);
   stage(0, 3);
@@ -482,16 +443,38 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const __bf16* __restrict__ A,
     stage(1, 0);
     stage(1, 2);
   }
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // A0, B0, B1 of K-tile 0
+  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
   else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   barrier();
   if (TKG8_STAGGER && wr == 1) barrier();  // the stagger
 
+  // The MFMAs are pure register ops: without pins the compiler may move them across the
+  // s_barriers (it sank Pb's MFMAs into the next iteration of the fp8 loop).  An empty
+  // volatile asm that "rewrites" the fragments right after a phase's first barrier, and one
+  // that "reads" the accumulators before its second, keeps every MFMA in its slot.
+  auto pin_frags = [&](bool with_b) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(a[i][0]), "+v"(a[i][1]));
+    if (with_b) {
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(b[nh][j][0]), "+v"(b[nh][j][1]));
+    }
+  };
+  auto pin_acc = [&](int mh) {
+#pragma unroll
+    for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 2; ++j) asm volatile("" : "+v"(acc[mh][nh][i][j]));
+  };
   for (int t = 0; t < nk; ++t) {
     const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
     read_a(t, 0);
     read_b(t, 0);
-    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_sched_barrier(0);  // the B1 reads last: lgkmcnt(4) below leaves only them
     read_b(t, 1);
     if (more1) {
       stage(t + 1, 3);
@@ -501,8 +484,10 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const __bf16* __restrict__ A,
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(4)" ::: "memory");
     }
     barrier();
+    pin_frags(true);
     quad(0, 0);
     quad(0, 1);
+    pin_acc(0);
     barrier();
     read_a(t, 1);
     if (more2) {
@@ -513,92 +498,12 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const __bf16* __restrict__ A,
       asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)" ::: "memory");
     }
     barrier();
+    pin_frags(false);
     quad(1, 1);
     quad(1, 0);
+    pin_acc(1);
     barrier();
   }
-#else
-  // prologue: K-tile 0 whole, K-tile 1 but A1 (staged in P0(0)); wait for A0(0), B0(0)
-  stage(0, 0);
-  stage(0, 2);
-  stage(0, 3);
-  stage(0, 1);
-  if (nk > 1) {
-    stage(1, 0);
-    stage(1, 2);
-    stage(1, 3);
-  }
-#if TKG8_VM_ONCE
-  if (nk > 1) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");  // all of K-tile 0
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-  sync_phase(nk > 1);
-#endif
-  barrier();
-  if (TKG8_STAGGER && wr == 1) barrier();  // the stagger
-
-  for (int t = 0; t < nk; ++t) {
-    const bool more1 = t + 1 < nk, more2 = t + 2 < nk;
-    // P0: A0, B0 -> (0,0); refill A1 of t+1
-    read_a(t, 0);
-#if TKG8_LGKM_EARLY
-    read_b(t, 0);
-    if (more1) stage(t + 1, 1);
-#if !TKG8_VM_ONCE
-    sync_phase(more1);  // + B1(t) for P1
-#else
-    sync_lds();
-#endif
-#else
-    // A0(t)'s slot is refilled in P1: retire those 8 reads before the barrier; B0(t)'s slot
-    // is refilled two phases on, so its reads may land after it
-    __builtin_amdgcn_sched_barrier(0);
-    read_b(t, 0);
-    if (more1) stage(t + 1, 1);
-#if !TKG8_VM_ONCE
-    if (more1) asm volatile("s_waitcnt vmcnt(10) lgkmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0) lgkmcnt(4)" ::: "memory");
-#else
-    asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");
-#endif
-#endif
-    barrier();
-    quad(0, 0);
-    barrier();
-    // P1: B1 -> (0,1); refill A0 of t+2
-    read_b(t, 1);
-    if (more2) stage(t + 2, 0);
-#if !TKG8_VM_ONCE
-    if (TKG8_LGKM_EARLY) sync_phase(more2);  // + A1(t) for P2
-    else if (more2) asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#else
-    if (TKG8_LGKM_EARLY) sync_lds();
-#endif
-    barrier();
-    quad(0, 1);
-    barrier();
-    // P2: A1 -> (1,1); refill B0 of t+2
-    read_a(t, 1);
-    if (more2) stage(t + 2, 2);
-    if (TKG8_LGKM_EARLY) sync_lds();
-    barrier();
-    quad(1, 1);
-    barrier();
-    // P3: -> (1,0); refill B1 of t+2; retire what P0(t+1) reads (TKG8_VM_ONCE: all of t+1,
-    // 3 younger stages = 6 copies may stay in flight)
-    if (more2) stage(t + 2, 3);
-#if !TKG8_VM_ONCE
-    sync_phase(more2);
-#else
-    if (more2) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#endif
-    barrier();
-    quad(1, 0);
-    barrier();
-  }
-#endif
   if (TKG8_STAGGER && wr == 0) barrier();  // match the stagger's extra barrier
 
   // accumulator element (mh, nh, i, j, e): row = mh*128 + wr*64 + i*16 + fq*4 + e,
@@ -676,15 +581,27 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const __bf16* __restrict__ A,
 // out[k] += sum over this block's chunk of rows of X[r][k] (X is [rows][K] bf16); grid.y
 // splits the rows, partial sums meet in fp32 atomics (out / out_abs zeroed beforehand)
 constexpr int COLSUM_CHUNKS = 64;
-__global__ __launch_bounds__(256) void k_colsum_bf16(const __bf16* __restrict__ X, int rows, int K,
-                                                     float* __restrict__ out, float* __restrict__ out_abs) {
+
+// OCP fp8 e4m3 (e4m3fn: bias 7, no infinities, S.1111.111 = NaN) -> float
+__device__ __forceinline__ float e4m3_to_f(uint8_t v) {
+  const int e = (v >> 3) & 15, m = v & 7;
+  float x = e ? ldexpf(1.0f + m * 0.125f, e - 7) : ldexpf(m * 0.125f, -6);
+  if (e == 15 && m == 7) x = __builtin_nanf("");
+  return (v & 0x80) ? -x : x;
+}
+__device__ __forceinline__ float elem(const __bf16* p, size_t i) { return (float)p[i]; }
+__device__ __forceinline__ float elem(const uint8_t* p, size_t i) { return e4m3_to_f(p[i]); }
+
+template <typename T>
+__global__ __launch_bounds__(256) void k_colsum(const T* __restrict__ X, int rows, int K, float* __restrict__ out,
+                                                float* __restrict__ out_abs) {
   const int k = blockIdx.x * 256 + threadIdx.x;
   if (k >= K) return;
   const int per = (rows + gridDim.y - 1) / gridDim.y;
   const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
   float s = 0.f, a = 0.f;
   for (int r = r0; r < r1; ++r) {
-    const float v = (float)X[(size_t)r * K + k];
+    const float v = elem(X, (size_t)r * K + k);
     s += v;
     a += fabsf(v);
   }
@@ -693,14 +610,15 @@ __global__ __launch_bounds__(256) void k_colsum_bf16(const __bf16* __restrict__ 
 }
 
 // expected[r] = sum_k X[r][k] * v[k]; bound[r] = sum_k |X[r][k]| * vabs[k]  (one wave per row)
-__global__ __launch_bounds__(256) void k_rowdot(const __bf16* __restrict__ X, int rows, int K, const float* __restrict__ v,
+template <typename T>
+__global__ __launch_bounds__(256) void k_rowdot(const T* __restrict__ X, int rows, int K, const float* __restrict__ v,
                                                 const float* __restrict__ vabs, float* __restrict__ expected,
                                                 float* __restrict__ bound) {
   const int r = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
   if (r >= rows) return;
   float s = 0.f, b = 0.f;
   for (int k = lane; k < K; k += 64) {
-    const float x = (float)X[(size_t)r * K + k];
+    const float x = elem(X, (size_t)r * K + k);
     s += x * v[k];
     b += fabsf(x) * vabs[k];
   }
@@ -744,9 +662,23 @@ __global__ __launch_bounds__(256) void k_fill_bf16(__bf16* __restrict__ p, size_
   }
 }
 
-static int check_shape(int M, int N, int K) {
-  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % BK) {
-    snprintf(g_err, sizeof(g_err), "shape %dx%dx%d: M and N must be multiples of %d, K of %d", M, N, K, BM, BK);
+// deterministic pseudo-random finite fp8 e4m3 with |v| in [2^-4, 2): random sign, exponent
+// field 3..7, random mantissa (so products and sums stay well inside fp32)
+__global__ __launch_bounds__(256) void k_fill_fp8(uint8_t* __restrict__ p, size_t n, uint32_t seed) {
+  for (size_t i = (size_t)blockIdx.x * 256 + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+    uint32_t x = (uint32_t)i * 0x9e3779b9u ^ seed ^ (uint32_t)(i >> 32);
+    x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
+    p[i] = (uint8_t)(((x >> 31) << 7) | ((3 + (x >> 8) % 5) << 3) | (x & 7));
+  }
+}
+
+// elements per K-tile: 64 bf16 / 128 fp8 (schedule 1); BK for the single-barrier loop
+static int k_granule(int esize) { return esize == 1 ? 128 : BK; }
+
+static int check_shape(int M, int N, int K, int esize = 2) {
+  const int kg = k_granule(esize);
+  if (M <= 0 || N <= 0 || K <= 0 || M % BM || N % BN || K % kg) {
+    snprintf(g_err, sizeof(g_err), "shape %dx%dx%d: M and N must be multiples of %d, K of %d", M, N, K, BM, kg);
     return -1;
   }
   return 0;
@@ -761,7 +693,7 @@ static int schedule() {
     const char* e = getenv("TKG_SCHED");
     g_sched = e ? atoi(e) : TKG_DEFAULT_SCHED;
   }
-  return (g_sched == 1 && BK == p8::BKP) ? 1 : 0;
+  return (g_sched == 1 && BK * 2 == p8::KT_BYTES) ? 1 : 0;
 }
 
 extern "C" int tkg_set_schedule(int s) {
@@ -769,15 +701,19 @@ extern "C" int tkg_set_schedule(int s) {
   return schedule();
 }
 
-static hipError_t launch_gemm(int mode, const __bf16* A, const __bf16* B, float* C, float* colpart, float* rowpart,
-                              int M, int N, int K, long long inject, hipStream_t s) {
+static hipError_t launch_gemm(int mode, int esize, const void* A, const void* B, float* C, float* colpart,
+                              float* rowpart, int M, int N, int K, long long inject, hipStream_t s) {
   const int grid = (M / BM) * (N / BN);
-  if (schedule() == 1) {
-    if (mode == 0) k_gemm8<0><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
-    else k_gemm8<1><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+  if (esize == 1) {  // fp8: staggered schedule only
+    if (mode == 0) k_gemm8<0, 1><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+    else k_gemm8<1, 1><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+  } else if (schedule() == 1) {
+    if (mode == 0) k_gemm8<0, 2><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+    else k_gemm8<1, 2><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
   } else {
-    if (mode == 0) k_gemm_bt<0><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
-    else k_gemm_bt<1><<<grid, THREADS, LDS_BYTES, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+    const __bf16 *a = static_cast<const __bf16*>(A), *b = static_cast<const __bf16*>(B);
+    if (mode == 0) k_gemm_bt<0><<<grid, THREADS, LDS_BYTES, s>>>(a, b, C, colpart, rowpart, M, N, K, inject);
+    else k_gemm_bt<1><<<grid, THREADS, LDS_BYTES, s>>>(a, b, C, colpart, rowpart, M, N, K, inject);
   }
   return hipGetLastError();
 }
@@ -785,7 +721,8 @@ static hipError_t launch_gemm(int mode, const __bf16* A, const __bf16* B, float*
 static hipError_t set_lds_limit() {
   static hipError_t once = [] {
     const void* fns[] = {reinterpret_cast<const void*>(&k_gemm_bt<0>), reinterpret_cast<const void*>(&k_gemm_bt<1>),
-                         reinterpret_cast<const void*>(&k_gemm8<0>), reinterpret_cast<const void*>(&k_gemm8<1>)};
+                         reinterpret_cast<const void*>(&k_gemm8<0, 2>), reinterpret_cast<const void*>(&k_gemm8<1, 2>),
+                         reinterpret_cast<const void*>(&k_gemm8<0, 1>), reinterpret_cast<const void*>(&k_gemm8<1, 1>)};
     for (const void* f : fns) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
       if (e != hipSuccess) return e;
@@ -796,13 +733,22 @@ static hipError_t set_lds_limit() {
 }
 
 // C[M][N] (fp32) = A[M][K] * B[N][K]^T for device pointers on `dev` (tests: torch tensors).
-extern "C" int tkg_gemm_bt(int dev, const void* A, const void* B, void* C, int M, int N, int K) {
-  if (check_shape(M, N, K)) return -1;
+static int gemm_bt(int dev, int esize, const void* A, const void* B, void* C, int M, int N, int K) {
+  if (check_shape(M, N, K, esize)) return -1;
   CHECK(hipSetDevice(dev));
   CHECK(set_lds_limit());
-  CHECK(launch_gemm(0, (const __bf16*)A, (const __bf16*)B, (float*)C, nullptr, nullptr, M, N, K, -1, 0));
+  CHECK(launch_gemm(0, esize, A, B, (float*)C, nullptr, nullptr, M, N, K, -1, 0));
   CHECK(hipDeviceSynchronize());
   return 0;
+}
+
+extern "C" int tkg_gemm_bt(int dev, const void* A, const void* B, void* C, int M, int N, int K) {
+  return gemm_bt(dev, 2, A, B, C, M, N, K);
+}
+
+// fp8 e4m3 A[M][K], B[N][K] (bytes) -> C fp32
+extern "C" int tkg_gemm_fp8_bt(int dev, const void* A, const void* B, void* C, int M, int N, int K) {
+  return gemm_bt(dev, 1, A, B, C, M, N, K);
 }
 
 // The screen: random A[M][K], B[N][K]; `reps` timed checksum-mode GEMMs (best time), then the
@@ -810,16 +756,16 @@ extern "C" int tkg_gemm_bt(int dev, const void* A, const void* B, void* C, int M
 // out[0] TFLOP/s (best rep), out[1] ms of that rep, out[2] bad columns, out[3] bad rows,
 // out[4] first bad column (-1: none), out[5] first bad row, out[6] max normalised error
 // (err / tolerance over every checksum; < 1 passes).
-extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inject, double* out) {
-  if (check_shape(M, N, K)) return -1;
+static int screen(int dev, int esize, int M, int N, int K, int reps, long long inject, double* out) {
+  if (check_shape(M, N, K, esize)) return -1;
   CHECK(hipSetDevice(dev));
   CHECK(set_lds_limit());
-  __bf16 *A = nullptr, *B = nullptr;
+  void *A = nullptr, *B = nullptr;
   float *colpart = nullptr, *rowpart = nullptr, *work = nullptr;
   unsigned int* flags = nullptr;
   const size_t parts_c = (size_t)(M / BM) * WAVES_M, parts_r = (size_t)(N / BN) * WAVES_N;
-  CHECK(hipMalloc(&A, (size_t)M * K * 2));
-  CHECK(hipMalloc(&B, (size_t)N * K * 2));
+  CHECK(hipMalloc(&A, (size_t)M * K * esize));
+  CHECK(hipMalloc(&B, (size_t)N * K * esize));
   CHECK(hipMalloc(&colpart, parts_c * N * 4));
   CHECK(hipMalloc(&rowpart, parts_r * M * 4));
   // sA, |sA|, sB, |sB| (K each), colexp/colbound (N), rowexp/rowbound (M)
@@ -832,14 +778,19 @@ extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inje
   hipEvent_t e0, e1;
   CHECK(hipEventCreate(&e0));
   CHECK(hipEventCreate(&e1));
-  k_fill_bf16<<<2048, 256, 0, s>>>(A, (size_t)M * K, 0x51f15eedu);
-  k_fill_bf16<<<2048, 256, 0, s>>>(B, (size_t)N * K, 0x0b5e55edu);
+  if (esize == 1) {
+    k_fill_fp8<<<2048, 256, 0, s>>>(static_cast<uint8_t*>(A), (size_t)M * K, 0x51f15eedu);
+    k_fill_fp8<<<2048, 256, 0, s>>>(static_cast<uint8_t*>(B), (size_t)N * K, 0x0b5e55edu);
+  } else {
+    k_fill_bf16<<<2048, 256, 0, s>>>(static_cast<__bf16*>(A), (size_t)M * K, 0x51f15eedu);
+    k_fill_bf16<<<2048, 256, 0, s>>>(static_cast<__bf16*>(B), (size_t)N * K, 0x0b5e55edu);
+  }
   CHECK(hipGetLastError());
-  CHECK(launch_gemm(1, A, B, nullptr, colpart, rowpart, M, N, K, -1, s));  // warm-up
+  CHECK(launch_gemm(1, esize, A, B, nullptr, colpart, rowpart, M, N, K, -1, s));  // warm-up
   double best = 1e30;
   for (int r = 0; r < (reps < 1 ? 1 : reps); ++r) {
     CHECK(hipEventRecord(e0, s));
-    CHECK(launch_gemm(1, A, B, nullptr, colpart, rowpart, M, N, K, inject, s));
+    CHECK(launch_gemm(1, esize, A, B, nullptr, colpart, rowpart, M, N, K, inject, s));
     CHECK(hipEventRecord(e1, s));
     CHECK(hipEventSynchronize(e1));
     float ms = 0.f;
@@ -848,10 +799,19 @@ extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inje
   }
   // right-hand sides: column sums of A and B over M / N, then the two mat-vecs
   CHECK(hipMemsetAsync(sA, 0, (size_t)4 * K * sizeof(float), s));  // sA, |sA|, sB, |sB|
-  k_colsum_bf16<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(A, M, K, sA, sAabs);
-  k_colsum_bf16<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(B, N, K, sB, sBabs);
-  k_rowdot<<<(N + 3) / 4, 256, 0, s>>>(B, N, K, sA, sAabs, colexp, colbd);
-  k_rowdot<<<(M + 3) / 4, 256, 0, s>>>(A, M, K, sB, sBabs, rowexp, rowbd);
+  if (esize == 1) {
+    const uint8_t *a = static_cast<const uint8_t*>(A), *b = static_cast<const uint8_t*>(B);
+    k_colsum<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(a, M, K, sA, sAabs);
+    k_colsum<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(b, N, K, sB, sBabs);
+    k_rowdot<<<(N + 3) / 4, 256, 0, s>>>(b, N, K, sA, sAabs, colexp, colbd);
+    k_rowdot<<<(M + 3) / 4, 256, 0, s>>>(a, M, K, sB, sBabs, rowexp, rowbd);
+  } else {
+    const __bf16 *a = static_cast<const __bf16*>(A), *b = static_cast<const __bf16*>(B);
+    k_colsum<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(a, M, K, sA, sAabs);
+    k_colsum<<<dim3((K + 255) / 256, COLSUM_CHUNKS), 256, 0, s>>>(b, N, K, sB, sBabs);
+    k_rowdot<<<(N + 3) / 4, 256, 0, s>>>(b, N, K, sA, sAabs, colexp, colbd);
+    k_rowdot<<<(M + 3) / 4, 256, 0, s>>>(a, M, K, sB, sBabs, rowexp, rowbd);
+  }
   const unsigned int init[6] = {0u, 0xffffffffu, 0u, 0u, 0xffffffffu, 0u};
   CHECK(hipMemcpyAsync(flags, init, sizeof(init), hipMemcpyHostToDevice, s));
   // fp32 reassociation error of two different summation orders over K*M (or K*N) products
@@ -884,4 +844,13 @@ extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inje
   (void)hipFree(B);
   (void)hipFree(A);
   return 0;
+}
+
+extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inject, double* out) {
+  return screen(dev, 2, M, N, K, reps, inject, out);
+}
+
+// the same screen on fp8 e4m3 operands (block-scaled 16x16x128 MFMA, unit scales)
+extern "C" int tkg_screen_fp8(int dev, int M, int N, int K, int reps, long long inject, double* out) {
+  return screen(dev, 1, M, N, K, reps, inject, out);
 }

@@ -803,21 +803,24 @@ extern "C" int tkp_p2p_bandwidth(int src, int dst, size_t bytes, int iters, doub
 // gpu-burnin: the on-node executable the SSH bootstrap runs (no Python needed).
 //   gpu-burnin [--all | --device N] [--level quick|full]
 //              [--min-read-gbps X] [--min-bf16-tflops Y] [--min-fp8-tflops Z] [--min-gemm-tflops G]
+//              [--min-gemm-fp8-tflops F]
 // Prints one JSON document; exit 1 when any GPU misses a threshold, the memtest finds a
-// mismatch or the GEMM fails its row/column checksums (thresholds: 60 % of 6.3 TB/s
-// achievable HBM read, 55 % of the 2.5 / 5 PF dense bf16 / fp8 MFMA peaks, GEMM 30 % of
-// the bf16 peak — the same policy as ops/probe.py).
+// mismatch or a GEMM fails its row/column checksums (thresholds: 60 % of 6.3 TB/s
+// achievable HBM read, 55 % of the 2.5 / 5 PF dense bf16 / fp8 MFMA peaks, bf16 / fp8 GEMMs
+// 30 % of those peaks — the same policy as ops/probe.py).
 #include <cstdlib>
 #include <vector>
 
 // the checksum-verified GEMM screen (tk_gemm_screen.hip, linked into this executable)
 extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inject, double* out);
+extern "C" int tkg_screen_fp8(int dev, int M, int N, int K, int reps, long long inject, double* out);
 extern "C" const char* tkg_last_error();
 
 int main(int argc, char** argv) {
   int dev = 0, all = 0;
   const char* level = "quick";
-  double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0;
+  double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
+         min_gemm8 = 0.30 * 5000.0;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--all")) all = 1;
     else if (!strcmp(argv[i], "--device") && i + 1 < argc) dev = atoi(argv[++i]);
@@ -826,6 +829,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--min-bf16-tflops") && i + 1 < argc) min_bf16 = atof(argv[++i]);
     else if (!strcmp(argv[i], "--min-fp8-tflops") && i + 1 < argc) min_fp8 = atof(argv[++i]);
     else if (!strcmp(argv[i], "--min-gemm-tflops") && i + 1 < argc) min_gemm = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--min-gemm-fp8-tflops") && i + 1 < argc) min_gemm8 = atof(argv[++i]);
   }
   const bool full = !strcmp(level, "full");
   const size_t hbm_bytes = full ? (16ull << 30) : (1ull << 30);
@@ -846,21 +850,25 @@ int main(int argc, char** argv) {
     const int d = devs[k];
     struct tkp_device_info info;
     memset(&info, 0, sizeof(info));
-    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[2] = {0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0};
+    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[2] = {0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0},
+           gm8[7] = {0, 0, 0, 0, -1, -1, 0};
     bool ok = tkp_device_info(d, &info) == 0 && tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, hbm) == 0 &&
               tkp_mfma_peak(d, 0, mfma_iters, 3, 2, bf16) == 0 && tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, fp8) == 0 &&
               tkg_screen(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, gm) == 0 &&
+              tkg_screen_fp8(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, gm8) == 0 &&
               tkp_memtest(d, mt_bytes, full ? 3 : 1, mt) == 0;
     if (!ok && tkg_last_error()[0] && !g_err[0]) snprintf(g_err, sizeof(g_err), "%s", tkg_last_error());
-    const bool gemm_ok = gm[2] == 0.0 && gm[3] == 0.0;
+    const bool gemm_ok = gm[2] == 0.0 && gm[3] == 0.0, gemm8_ok = gm8[2] == 0.0 && gm8[3] == 0.0;
     const bool pass = ok && strncmp(info.arch, "gfx950", 6) == 0 && hbm[0] >= min_read && bf16[0] >= min_bf16 &&
-                      fp8[0] >= min_fp8 && gemm_ok && gm[0] >= min_gemm && mt[0] == 0.0;
+                      fp8[0] >= min_fp8 && gemm_ok && gm[0] >= min_gemm && gemm8_ok && gm8[0] >= min_gemm8 &&
+                      mt[0] == 0.0;
     ok_all = ok_all && pass;
     printf("%s{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"read_gbps\":%.1f,\"write_gbps\":%.1f,\"copy_gbps\":%.1f,"
            "\"bf16_tflops\":%.1f,\"fp8_tflops\":%.1f,\"gemm_tflops\":%.1f,\"gemm_checksum_ok\":%s,"
+           "\"gemm_fp8_tflops\":%.1f,\"gemm_fp8_checksum_ok\":%s,"
            "\"memtest_errors\":%.0f,\"ok\":%s%s%s%s}",
            k ? "," : "", d, info.arch, info.compute_units, hbm[0], hbm[1], hbm[2], bf16[0], fp8[0], gm[0],
-           gemm_ok ? "true" : "false", mt[0],
+           gemm_ok ? "true" : "false", gm8[0], gemm8_ok ? "true" : "false", mt[0],
            pass ? "true" : "false", ok ? "" : ",\"error\":\"", ok ? "" : g_err, ok ? "" : "\"");
   }
   printf("],\"ok\":%s}\n", ok_all ? "true" : "false");

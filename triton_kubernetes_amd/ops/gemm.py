@@ -13,7 +13,8 @@ from typing import Any, Dict
 from .native import load
 
 TILE_M = TILE_N = 256
-TILE_K = 64
+TILE_K = 64  # bf16 elements per K-tile (128 bytes of a row)
+TILE_K_FP8 = 128  # fp8 e4m3 elements per K-tile
 
 # level -> (M, N, K, timed reps)
 SCREEN_SIZES = {"quick": (4096, 4096, 4096, 2), "full": (8192, 8192, 8192, 5)}
@@ -28,8 +29,10 @@ def _lib():
     lib.tkg_last_error.restype = ctypes.c_char_p
     lib.tkg_gemm_bt.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                 ctypes.c_int, ctypes.c_int, ctypes.c_int]
+    lib.tkg_gemm_fp8_bt.argtypes = lib.tkg_gemm_bt.argtypes
     lib.tkg_screen.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
+    lib.tkg_screen_fp8.argtypes = lib.tkg_screen.argtypes
     lib.tkg_set_schedule.argtypes = [ctypes.c_int]
     return lib
 
@@ -47,30 +50,35 @@ def set_schedule(name: str) -> str:
     return next(k for k, v in SCHEDULES.items() if v == got)
 
 
-def check_shape(m: int, n: int, k: int) -> None:
-    if m <= 0 or n <= 0 or k <= 0 or m % TILE_M or n % TILE_N or k % TILE_K:
-        raise GemmError(f"shape {m}x{n}x{k}: M and N must be multiples of {TILE_M}, K of {TILE_K}")
+def check_shape(m: int, n: int, k: int, dtype: str = "bf16") -> None:
+    tk = TILE_K_FP8 if dtype == "fp8" else TILE_K
+    if m <= 0 or n <= 0 or k <= 0 or m % TILE_M or n % TILE_N or k % tk:
+        raise GemmError(f"shape {m}x{n}x{k}: M and N must be multiples of {TILE_M}, K of {tk}")
 
 
 def gemm_bt(a, b, out=None):
-    """``out = a @ b.T`` in fp32 for bf16 CUDA tensors ``a [M,K]``, ``b [N,K]`` (contiguous)."""
+    """``out = a @ b.T`` in fp32 for CUDA tensors ``a [M,K]``, ``b [N,K]`` (contiguous), both
+    bf16 or both fp8 e4m3 (``torch.float8_e4m3fn``: the block-scaled MFMA with unit scales)."""
     import torch
 
     from .native import require_torch_first
 
     require_torch_first()
-    if a.dtype != torch.bfloat16 or b.dtype != torch.bfloat16 or not (a.is_cuda and b.is_cuda):
-        raise GemmError("gemm_bt wants bf16 CUDA tensors")
+    fp8 = getattr(torch, "float8_e4m3fn", None)
+    if a.dtype != b.dtype or a.dtype not in (torch.bfloat16, fp8) or not (a.is_cuda and b.is_cuda):
+        raise GemmError("gemm_bt wants two bf16 or two float8_e4m3fn CUDA tensors")
     if not (a.is_contiguous() and b.is_contiguous()) or a.shape[1] != b.shape[1]:
         raise GemmError("gemm_bt wants contiguous a [M,K] and b [N,K]")
     m, k = a.shape
     n = b.shape[0]
-    check_shape(m, n, k)
+    dtype = "fp8" if a.dtype == fp8 else "bf16"
+    check_shape(m, n, k, dtype)
     if out is None:
         out = torch.empty((m, n), dtype=torch.float32, device=a.device)
     elif out.shape != (m, n) or out.dtype != torch.float32 or not out.is_contiguous():
         raise GemmError("out must be a contiguous fp32 [M,N] tensor")
-    rc = _lib().tkg_gemm_bt(a.device.index or 0, a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k)
+    fn = _lib().tkg_gemm_fp8_bt if dtype == "fp8" else _lib().tkg_gemm_bt
+    rc = fn(a.device.index or 0, a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k)
     if rc != 0:
         raise GemmError(_lib().tkg_last_error().decode())
     return out
@@ -88,6 +96,7 @@ class ScreenResult:
     first_bad_column: int
     first_bad_row: int
     max_norm_error: float  # |checksum error| / tolerance, worst over all rows and columns
+    dtype: str = "bf16"
 
     @property
     def ok(self) -> bool:
@@ -99,12 +108,16 @@ class ScreenResult:
         return d
 
 
-def screen(dev: int, m: int = 4096, n: int = 4096, k: int = 4096, reps: int = 2, inject: int = -1) -> ScreenResult:
-    """Run the checksum-verified GEMM; ``inject`` (row*N + col) corrupts one C element to
-    prove the screen catches it."""
-    check_shape(m, n, k)
+def screen(dev: int, m: int = 4096, n: int = 4096, k: int = 4096, reps: int = 2, inject: int = -1,
+           dtype: str = "bf16") -> ScreenResult:
+    """Run the checksum-verified GEMM on random ``dtype`` (bf16 | fp8) operands; ``inject``
+    (row*N + col) corrupts one C element to prove the screen catches it."""
+    if dtype not in ("bf16", "fp8"):
+        raise GemmError(f"unknown dtype '{dtype}' (bf16 | fp8)")
+    check_shape(m, n, k, dtype)
     out = (ctypes.c_double * 7)()
-    rc = _lib().tkg_screen(dev, m, n, k, reps, inject, out)
+    fn = _lib().tkg_screen_fp8 if dtype == "fp8" else _lib().tkg_screen
+    rc = fn(dev, m, n, k, reps, inject, out)
     if rc != 0:
         raise GemmError(_lib().tkg_last_error().decode())
-    return ScreenResult(m, n, k, out[0], out[1], int(out[2]), int(out[3]), int(out[4]), int(out[5]), out[6])
+    return ScreenResult(m, n, k, out[0], out[1], int(out[2]), int(out[3]), int(out[4]), int(out[5]), out[6], dtype)

@@ -170,8 +170,9 @@ class Thresholds:
     min_read_frac: float = 0.60
     min_bf16_frac: float = 0.55
     min_fp8_frac: float = 0.55
-    # the checksum-verified GEMM (ops/gemm.py): a fraction of the dense bf16 peak
+    # the checksum-verified GEMMs (ops/gemm.py): a fraction of the dense bf16 / fp8 peak
     min_gemm_frac: float = 0.30
+    min_gemm_fp8_frac: float = 0.30
     require_gfx950: bool = True
     min_cus: int = MI355X_CUS
 
@@ -183,6 +184,7 @@ class BurninResult:
     hbm: Dict[str, float] = field(default_factory=dict)
     mfma: Dict[str, Dict[str, float]] = field(default_factory=dict)
     gemm: Dict[str, Any] = field(default_factory=dict)
+    gemm_fp8: Dict[str, Any] = field(default_factory=dict)
     memtest: Dict[str, float] = field(default_factory=dict)
     failures: List[str] = field(default_factory=list)
 
@@ -222,17 +224,23 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
     if res.mfma["fp8"]["tflops"] < th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS:
         res.failures.append(f"fp8 MFMA {res.mfma['fp8']['tflops']:.0f} TF below "
                             f"{th.min_fp8_frac:.0%} of dense peak")
-    with span("burnin.gemm", dev=dev):
-        from . import gemm
+    from . import gemm
 
-        m, n, k, reps = gemm.SCREEN_SIZES[level]
-        g = gemm.screen(dev, m, n, k, reps)
-        res.gemm = g.to_json()
-    if not g.ok:
-        res.failures.append(f"GEMM checksum mismatch: {g.bad_rows} rows / {g.bad_columns} columns "
-                            f"(first at row {g.first_bad_row}, column {g.first_bad_column})")
-    if g.tflops < th.min_gemm_frac * MI355X_BF16_DENSE_TFLOPS:
-        res.failures.append(f"GEMM {g.tflops:.0f} TF below {th.min_gemm_frac:.0%} of dense bf16 peak")
+    m, n, k, reps = gemm.SCREEN_SIZES[level]
+    for dtype, peak, frac in (("bf16", MI355X_BF16_DENSE_TFLOPS, th.min_gemm_frac),
+                              ("fp8", MI355X_FP8_DENSE_TFLOPS, th.min_gemm_fp8_frac)):
+        with span(f"burnin.gemm_{dtype}", dev=dev):
+            g = gemm.screen(dev, m, n, k, reps, dtype=dtype)
+        if dtype == "bf16":
+            res.gemm = g.to_json()
+        else:
+            res.gemm_fp8 = g.to_json()
+        name = "GEMM" if dtype == "bf16" else "fp8 GEMM"
+        if not g.ok:
+            res.failures.append(f"{name} checksum mismatch: {g.bad_rows} rows / {g.bad_columns} columns "
+                                f"(first at row {g.first_bad_row}, column {g.first_bad_column})")
+        if g.tflops < frac * peak:
+            res.failures.append(f"{name} {g.tflops:.0f} TF below {frac:.0%} of dense {dtype} peak")
     with span("burnin.memtest", dev=dev):
         res.memtest = memtest(dev, mt_bytes, mt_passes)
     if res.memtest["errors"]:
