@@ -5,7 +5,7 @@
     python -m triton_kubernetes_amd.ops.cli labels
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
     python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
-    python -m triton_kubernetes_amd.ops.cli gemm [--size N] [--reps R] [--schedule staggered|single-barrier]
+    python -m triton_kubernetes_amd.ops.cli gemm [--size N] [--reps R] [--schedule staggered|single-barrier] [--dtype bf16|fp8]
 
 Every command prints one JSON document; the exit status is non-zero when the
 GPU(s) fail the gate.
@@ -43,7 +43,9 @@ def main(argv: Sequence[str] = ()) -> int:
     g.add_argument("--size", type=int, default=8192, help="M = N = K (a multiple of 256)")
     g.add_argument("--reps", type=int, default=5)
     g.add_argument("--schedule", default="staggered", choices=["staggered", "single-barrier"],
-                   help="GEMM main loop (single-barrier: the earlier loop, for A/B)")
+                   help="GEMM main loop (single-barrier: the earlier loop, for A/B; bf16 only)")
+    g.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
+                   help="operands: bf16, or fp8 e4m3 through the block-scaled MFMA")
     m.add_argument("--clock", action="store_true",
                    help="also report the in-kernel clock and FLOP/clk/SIMD (stamped diagnostic launch)")
     args = ap.parse_args(list(argv) or sys.argv[1:])
@@ -90,8 +92,8 @@ def main(argv: Sequence[str] = ()) -> int:
         from . import gemm
 
         gemm.set_schedule(args.schedule)
-        res = gemm.screen(args.device, args.size, args.size, args.size, args.reps)
-        print(json.dumps(dict(res.to_json(), schedule=args.schedule)))
+        res = gemm.screen(args.device, args.size, args.size, args.size, args.reps, dtype=args.dtype)
+        print(json.dumps(dict(res.to_json(), schedule=args.schedule if args.dtype == "bf16" else "staggered")))
         return 0 if res.ok else 1
     return 2
 
