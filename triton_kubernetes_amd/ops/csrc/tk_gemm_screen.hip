@@ -385,19 +385,17 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const void* __restrict__ A, c
   auto stage = [&](int t, int h) {  // h: 0 A0, 1 A1, 2 B0, 3 B1
     stage_half(h < 2 ? pa : pb, ldb, voff, (h & 1) * HROWS, t * KT_BYTES, slot(smem, t, h), tid);
   };
-  // A fragment of one 16-row group for the whole K-tile: two 16-byte chunks per lane.  bf16:
-  // chunks fq and 4 + fq (two 16x16x32 k-steps, lane holds k = 8 fq .. +7 of each); fp8:
-  // chunks 2 fq, 2 fq + 1 (one 16x16x128 step, lane holds k = 32 fq .. +31).  A and B use the
-  // same map, so every product pairs equal k.
+  // A fragment of one 16-row group for the whole K-tile: 16-byte chunks fq and 4 + fq of
+  // the row (bf16: one per 16x16x32 k-step, lane holds k = 8 fq .. +7 of each; fp8: both
+  // feed one 16x16x128 step).  A and B use the same map, so every product pairs equal k —
+  // for fp8 the MFMA's k positions are a permutation of the row's bytes, which leaves the
+  // dot product unchanged.  The natural fp8 map (chunks 2 fq, 2 fq + 1) would put the two
+  // lane quarters of a ds_read_b128 group on the same banks: 50 M conflict cycles per
+  // 8192^3 (profiles/round1_gemm_pmc.md); this one is conflict-free, as for bf16.
   u32x4 a[4][2], b[2][2][2];
   auto ld_frag = [&](const char* img, int r, u32x4* f) {
-    if constexpr (ESIZE == 2) {
-      f[0] = chunk(img, r, fq);
-      f[1] = chunk(img, r, 4 + fq);
-    } else {
-      f[0] = chunk(img, r, 2 * fq);
-      f[1] = chunk(img, r, 2 * fq + 1);
-    }
+    f[0] = chunk(img, r, fq);
+    f[1] = chunk(img, r, 4 + fq);
   };
   auto read_a = [&](int t, int mh) {
     const char* img = slot(smem, t, mh);
