@@ -173,7 +173,14 @@ def main() -> int:
         if step_watchdog > 0:
             faulthandler.cancel_dump_traceback_later()
         dt = time.time() - t0
-        return {"step": i, "seconds": dt, "proc": procstat.delta(ps0, procstat.snapshot())}
+        out = {"step": i, "seconds": dt, "proc": procstat.delta(ps0, procstat.snapshot())}
+        rep = ctx.extras.get("last_readiness")
+        ranks = ((rep.rccl or {}).get("ranks") or []) if rep is not None else []
+        phases = [r.get("phase_ms") or {} for r in ranks]
+        if phases:  # the gate's communicator init on every rank: where an N-GPU step goes
+            out["rccl"] = {k: round(max(float(p.get(k, 0.0)) for p in phases), 3)
+                           for k in ("init_total", "init_wait", "alloc", "sweep")}
+        return out
 
     def sync():
         if not args.sim_gpu:
@@ -215,6 +222,12 @@ def main() -> int:
             if sp["name"].startswith(("ready.", "module.", "node.", "direct.apply", "apply")):
                 phases.setdefault(sp["name"], []).append(sp["duration"])
         phase_ms = {k: round(sum(v) / max(1, args.steps) * 1000.0, 2) for k, v in sorted(phases.items())}
+        # RCCL gate, max over ranks per step, mean over steps: communicator init wall time,
+        # the part of it the readiness waiter still waited for, and the verified sweep
+        gate = [r["rccl"] for r in results if "rccl" in r]
+        for k in ("init_total", "init_wait", "sweep"):
+            if gate:
+                phase_ms[f"rccl.{k}_max_rank"] = round(sum(g[k] for g in gate) / len(gate), 2)
         line = {
             "metric": METRIC,
             "value": round(ms / 1000.0, 4),

@@ -199,6 +199,7 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
         gate.abort()  # membership changed since it was prepared
         gate = None
     rep = wait_ready(client, spec, start=start, agent_transport=transport, gate=gate)
+    ctx.extras["last_readiness"] = rep  # callers that time phases (bench.py) read it here
     ctx.echo(f"cluster ready in {rep.ready_seconds:.2f}s: " +
              json.dumps(rep.to_json()["phase_seconds"], sort_keys=True))
     return rep
