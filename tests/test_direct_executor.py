@@ -312,3 +312,33 @@ def test_fake_rancher_settles_clusters(env):
     user, _, secret = RancherClient(fake.url).login("admin", "s3cret").partition(":")
     client = RancherClient(fake.url, user, secret)
     assert {n["clusterId"] for n in client.nodes(cids["one"])} == {cids["one"]}
+
+
+def test_tfstate_codec_foreign_shapes_fall_back_to_plain_encoding():
+    from triton_kubernetes_amd.executor.tfstate import TfstateCodec
+
+    codec = TfstateCodec()
+    # module_outputs entries that are not objects, or non-string keys: plain json.dumps
+    odd = {"version": 4, "serial": 1, "module_outputs": {"m": "not-a-dict"}, "module_state": {"m": {"status": "ok"}}}
+    assert json.loads(codec.dumps("x", odd)) == odd
+    assert codec.load("x", codec.dumps("x", odd)) is not None  # parsed, not served from the cache
+    keyed = {"version": 4, "module_outputs": {}, "module_state": {1: {"status": "ok"}}}
+    assert json.loads(codec.dumps("y", keyed))["module_state"] == {"1": {"status": "ok"}}
+    codec.forget("x")
+    codec.forget("never-saved")
+
+
+def test_fake_rancher_node_delete_keeps_cluster_index(env):
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    cp = agent("cp")
+    new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
+                              k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", wait=True,
+                              nodes=_nodes(cp, [agent("w", gpus=8)]))), backend)
+    cid = next(iter(fake.state.clusters))
+    user, _, secret = RancherClient(fake.url).login("admin", "s3cret").partition(":")
+    client = RancherClient(fake.url, user, secret)
+    gpu = next(n for n in client.nodes(cid) if n["hostname"] == "gpu-1")
+    client.http.request("DELETE", f"/v3/nodes/{gpu['id']}", ok=(200,))
+    assert {n["metadata"]["name"] for n in fake.k8s_nodes(cid)} == {"cp-1", "etcd-1"}
+    assert gpu["id"] not in fake.state.nodes and gpu["id"] not in fake.state.cluster_nodes[cid]
