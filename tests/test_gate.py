@@ -27,9 +27,10 @@ class FakeAgents:
         if path == "/v1/rccl-prepare":
             if url == self.fail_prepare_on:
                 raise RuntimeError("agent unreachable")
+            uid = body.get("uid") or "UID-" + str(len(self.calls))  # no uid: host the rendezvous
             with self.mu:
-                self.pending[(url, body["uid"])] = body
-            return {"ok": True}
+                self.pending[(url, uid)] = dict(body, uid=uid)
+            return {"ok": True, "uid": uid}
         if path == "/v1/rccl-gate":
             with self.mu:
                 pipelined = self.pending.pop((url, body["uid"]), None) is not None
@@ -59,8 +60,10 @@ def test_pipelined_gate_runs_prepared_communicators():
     prep = [c for c in fake.calls if c[1] == "/v1/rccl-prepare"]
     assert sorted((c[0], c[2]["rank_base"], c[2]["ndev"], c[2]["world"]) for c in prep) == [
         ("http://a", 0, 8, 16), ("http://b", 8, 8, 16)]
+    # one request to the first member takes its unique id; the others join with it
+    assert "uid" not in prep[0][2] and "/v1/rccl-uid" not in fake.paths()
     runs = [c for c in fake.calls if c[1] == "/v1/rccl-gate"]
-    assert {c[2]["uid"] for c in runs} == {prep[0][2]["uid"]}
+    assert {c[2]["uid"] for c in runs} == {prep[1][2]["uid"]} == {gate.uid}
     assert all(r["pipelined"] for r in res["ranks"])
     assert res["min_peak_busbw_gbps"] == 10.0
     gate.abort()  # after run: no-op

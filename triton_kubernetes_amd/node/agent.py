@@ -25,7 +25,7 @@ GPUs: topology labeller (N1), HBM/MFMA/memtest burn-in, RCCL env file and the
 node-level RCCL sweep (N2).
 
 HTTP API (JSON): ``GET /v1/info``, ``POST /v1/plan``, ``POST /v1/rccl-uid``,
-``POST /v1/rccl-prepare`` (start this node's ranks of the cluster-wide RCCL
+``POST /v1/rccl-prepare`` (without a ``uid``: host the rendezvous and return it; start this node's ranks of the cluster-wide RCCL
 communicator, non-blocking), ``POST /v1/rccl-gate`` (run them: verified
 all-reduce sweep), ``POST /v1/rccl-abort``, ``POST /v1/cleanup``.
 """
@@ -122,6 +122,10 @@ class NodeAgent:
         self._pool = cf.ThreadPoolExecutor(max_workers=len(self.devices) + 2,
                                            thread_name_prefix=f"tk-agent-{self.name}")
         self._gates: Dict[bytes, Any] = {}
+        # one RCCL unique id kept ready (new_uid): the gate's first request gets it without
+        # an ncclGetUniqueId on the bring-up path; the pool makes the next one afterwards
+        self._spare_uid: Optional[bytes] = None
+        self._uid_mu = threading.Lock()
         self.last_labels: Dict[str, str] = {}
         self.history: List[Dict[str, Any]] = []
         self._server: Optional[http.server.ThreadingHTTPServer] = None
@@ -336,12 +340,43 @@ class NodeAgent:
         for g in gates:
             g.abort()
 
-    def rccl_prepare(self, uid: bytes, world: int, rank_base: int, ndev: int = 1,
+    def _make_uid(self) -> bytes:
+        if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
+            return secrets.token_bytes(128)
+        from ..ops import rccl
+
+        self._used_rccl = True
+        return rccl.unique_id()
+
+    def _refill_uid(self) -> None:
+        uid = self._make_uid()
+        with self._uid_mu:
+            if self._spare_uid is None:
+                self._spare_uid = uid
+
+    def new_uid(self) -> bytes:
+        """A fresh RCCL unique id (a bootstrap rendezvous address, specific to no cluster):
+        the spare if one is ready, otherwise made now; either way the next spare is made on
+        the agent's pool, off this request."""
+        with self._uid_mu:
+            uid, self._spare_uid = self._spare_uid, None
+        if uid is None:
+            uid = self._make_uid()
+        try:
+            self._pool.submit(self._refill_uid)
+        except RuntimeError:  # pool shut down: the agent is stopping
+            pass
+        return uid
+
+    def rccl_prepare(self, uid: Optional[bytes], world: int, rank_base: int, ndev: int = 1,
                      max_bytes: int = 0) -> Dict[str, Any]:
         """Start this node's share of a cluster communicator (non-blocking init; with
-        ``max_bytes`` the init thread also allocates the sweep buffers)."""
+        ``max_bytes`` the init thread also allocates the sweep buffers).  ``uid`` None: this
+        node hosts the rendezvous — it takes a new unique id and returns it for the others."""
         devs = self._gate_devices(ndev)
         self._expire_gates()
+        if uid is None:
+            uid = self.new_uid()
         with span("node.rccl_prepare", node=self.name, rank_base=rank_base, world=world):
             if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
                 gate: Any = _SimGate(devs)
@@ -355,7 +390,8 @@ class NodeAgent:
             self._gates[uid] = (gate, time.time())
         if old is not None:
             old[0].abort()
-        return {"ok": True, "ranks": list(range(rank_base, rank_base + len(devs))), "devices": devs}
+        return {"ok": True, "ranks": list(range(rank_base, rank_base + len(devs))), "devices": devs,
+                "uid": base64.b64encode(uid).decode()}
 
     def rccl_abort(self, uid: bytes) -> Dict[str, Any]:
         with self._gate_mu:
@@ -417,6 +453,7 @@ class NodeAgent:
         quiet = float(os.environ.get("TK_TEARDOWN_QUIET_MS", "0") or 0)
         if quiet > 0:
             rccl.set_teardown_quiet_ms(quiet)
+        self._refill_uid()  # the first gate's unique id, ready before any request
         try:
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later
@@ -510,15 +547,10 @@ class NodeAgent:
                     if path == "/v1/plan":
                         return self._reply(200, agent.run_plan(BootstrapPlan.from_json(body["plan"])))
                     if path == "/v1/rccl-uid":
-                        if agent.topology_override is not None:
-                            raw = secrets.token_bytes(128)
-                        else:
-                            from ..ops import rccl
-
-                            raw = rccl.unique_id()
-                        return self._reply(200, {"uid": base64.b64encode(raw).decode()})
+                        return self._reply(200, {"uid": base64.b64encode(agent.new_uid()).decode()})
                     if path == "/v1/rccl-prepare":
-                        return self._reply(200, agent.rccl_prepare(base64.b64decode(body["uid"]),
+                        uid = base64.b64decode(body["uid"]) if body.get("uid") else None
+                        return self._reply(200, agent.rccl_prepare(uid,
                                                                    int(body["world"]), int(body["rank_base"]),
                                                                    int(body.get("ndev", 1)),
                                                                    int(body.get("max_bytes", 0))))

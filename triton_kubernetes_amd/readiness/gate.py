@@ -3,8 +3,9 @@
 Each node agent owns its node's GPUs and joins as ranks ``rank_base .. rank_base+ndev-1``
 (``ops/rccl.py:GateComm``).  The gate has two halves:
 
-* :meth:`ClusterGate.prepare_async`: fetch a ``ncclUniqueId`` from the rank-0 agent and
-  ask every agent to *start* its communicator init (RCCL non-blocking mode).  This needs
+* :meth:`ClusterGate.prepare_async`: ask the rank-0 agent to start its ranks under a new
+  ``ncclUniqueId`` (it keeps one ready) and return the id, then ask every other agent to
+  *start* its communicator init with it (RCCL non-blocking mode).  This needs
   only the cluster membership, which is known as soon as the node modules are in the
   document, so ``create cluster`` starts it together with the apply.  Communicator
   bring-up then overlaps node bootstrap instead of following it.
@@ -99,17 +100,26 @@ class ClusterGate:
     def _prepare(self) -> None:
         try:
             with span("gate.prepare", world=self.world):
-                uid = self.transport.post(self.members[0].host, "/v1/rccl-uid", {})["uid"]
-                self._post_all("/v1/rccl-prepare", lambda m: {"uid": uid, "world": self.world,
-                                                               "rank_base": m.rank_base, "ndev": m.ndev,
-                                                               "max_bytes": max(self.sizes)})
+                # the first member hosts the rendezvous: one request takes its unique id and
+                # starts its ranks; the others join with that id
+                m0 = self.members[0]
+                first = self.transport.post(m0.host, "/v1/rccl-prepare", {
+                    "world": self.world, "rank_base": m0.rank_base, "ndev": m0.ndev, "max_bytes": max(self.sizes)})
+                uid = first["uid"]
+                with self._mu:
+                    self.uid = uid  # abort() can release member 0 even if a later post fails
+                if len(self.members) > 1:
+                    def one(m: GateMember) -> Dict[str, Any]:
+                        return self.transport.post(m.host, "/v1/rccl-prepare", {
+                            "uid": uid, "world": self.world, "rank_base": m.rank_base, "ndev": m.ndev,
+                            "max_bytes": max(self.sizes)})
+
+                    list(shared_pool("tk-gate", 64).map(one, self.members[1:]))
             with self._mu:
-                self.uid, self.prepared = uid, True
+                self.prepared = True
         except Exception as exc:  # noqa: BLE001 - run() falls back to an unprepared gate
             with self._mu:
                 self.prepare_error = f"{type(exc).__name__}: {exc}"
-                if "uid" in locals():
-                    self.uid = uid  # some agents may hold a pending init under it: abort() releases them
 
     def prepare_async(self) -> "ClusterGate":
         # its own pool: _prepare itself fans out on "tk-gate"
