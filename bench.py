@@ -115,13 +115,13 @@ def main() -> int:
     if rank == 0:
         from triton_kubernetes_amd.rancher.fake import FakeRancher
 
-        fake = FakeRancher().start()
+        fake = FakeRancher.for_manager("bench", "bench-admin-pw-0123").start()
         cp_agent = NodeAgent(name="control-plane", mode="sim", token=token, root=os.path.join(work, "cp"))
         cp_url = cp_agent.serve()
         backend = LocalBackend(os.path.join(work, "state"))
         ctx_base = {"backend_provider": "local", "executor": "direct", "agent_token": token,
                     "non-interactive": True, "cluster_manager": "bench"}
-        mgr = dict(ctx_base, manager_cloud_provider="baremetal", name="bench", rancher_admin_password="bench-pw",
+        mgr = dict(ctx_base, manager_cloud_provider="baremetal", name="bench", rancher_admin_password="bench-admin-pw-0123",
                    host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="~/.ssh/id_rsa")
         wf.new_manager(Context(settings=Settings(mgr, env={}), out=devnull), backend)
 
@@ -150,7 +150,7 @@ def main() -> int:
 
     def one_step(i: int) -> dict:
         name = f"bench-{i}"
-        cfg = dict(ctx_base, cluster_cloud_provider="baremetal", name=name, k8s_version="v1.9.5-rancher1-1",
+        cfg = dict(ctx_base, cluster_cloud_provider="baremetal", name=name, k8s_version="v1.28.10-rancher1-1",
                    k8s_network_provider="flannel", gpu_addons=True, wait=True,
                    rccl_gate=not args.no_rccl_gate, rccl_pipeline=not args.no_gate_pipeline, wait_timeout=600,
                    nodes=[

@@ -74,26 +74,26 @@ def config1(runs):
 
 
 def config2_3(runs):
-    fake = FakeRancher().start()
+    fake = FakeRancher.for_manager("mgr", "tk-admin-pw-0123").start()
     agents = [NodeAgent(name=f"n{i}", mode="sim", token=TOKEN, root=tempfile.mkdtemp()) for i in range(3)]
     urls = ["agent+" + a.serve() for a in agents]
     root = tempfile.mkdtemp()
     base = {"backend_provider": "local", "executor": "direct", "agent_token": TOKEN}
 
     # a fresh Rancher per run: the bootstrap changes the initial admin password
-    fresh = [FakeRancher().start() for _ in range(runs + 1)]
+    fresh = [FakeRancher.for_manager("mgr", "tk-admin-pw-0123").start() for _ in range(runs + 1)]
 
     def mgr(i):
         backend = LocalBackend(os.path.join(root, f"m{i}"))
         wf.new_manager(ctx_of(dict(base, manager_cloud_provider="baremetal", name="mgr",
-                                   rancher_admin_password="pw", host="rancher+" + fresh[i + 1].url, ssh_user="u",
+                                   rancher_admin_password="tk-admin-pw-0123", host="rancher+" + fresh[i + 1].url, ssh_user="u",
                                    bastion_host="", key_path="k")), backend)
 
     r2 = timed(mgr, runs)
     for f in fresh:
         f.stop()
     backend = LocalBackend(os.path.join(root, "c"))
-    wf.new_manager(ctx_of(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="pw",
+    wf.new_manager(ctx_of(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
                                host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
 
     def cluster(i):
@@ -102,7 +102,7 @@ def config2_3(runs):
                  {"rancher_host_label": "worker", "node_count": 2, "hostname": f"c{i}-w", "ssh_user": "u",
                   "bastion_host": "", "key_path": "k", "hosts": urls[1:]}]
         wf.new_cluster(ctx_of(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal",
-                                   name=f"three-{i + 1}", k8s_version="v1.9.5-rancher1-1",
+                                   name=f"three-{i + 1}", k8s_version="v1.28.10-rancher1-1",
                                    k8s_network_provider="flannel", nodes=nodes)), backend)
 
     r3 = timed(cluster, runs)
@@ -139,7 +139,7 @@ def config4(runs):
               "triton_image_version": "20180222", "triton_ssh_user": "ubuntu"}
     backend = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://tr.example", manta.url)
     wf.new_manager(ctx_of(dict(triton, backend_provider="manta", executor="terraform", manager_cloud_provider="triton",
-                               name="tmgr", rancher_admin_password="pw",
+                               name="tmgr", rancher_admin_password="tk-admin-pw-0123",
                                master_triton_machine_package="k4-highcpu-kvm-1.75G"), cloud=cloud), backend)
 
     def cluster(i):
@@ -149,7 +149,7 @@ def config4(runs):
                  for lbl, n in (("etcd", 1), ("control", 1), ("worker", 6))]
         wf.new_cluster(ctx_of(dict(triton, backend_provider="manta", executor="terraform", cluster_manager="tmgr",
                                    cluster_cloud_provider="triton", name=f"eight-{i + 1}",
-                                   k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", nodes=nodes),
+                                   k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", nodes=nodes),
                               cloud=cloud), backend)
 
     r4 = timed(cluster, runs)

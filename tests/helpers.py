@@ -66,16 +66,23 @@ def have(binary: str) -> bool:
 
 
 def assert_blocks_match_modules(st) -> None:
-    """Every key a provider wrote into a module block is a variable of the generated module."""
-    from triton_kubernetes_amd.terraform import catalog, generate
+    """Every module block of a rendered document points at a module directory that exists
+    (the packaged tree by default), every key it sets is a variable declared there, and
+    every required variable is set — read from the module's own .tf files with the HCL
+    parser, not from the generator's data."""
+    import os
 
-    declared = {m.name: {v.name for v in m.variables} for m in generate.modules()}
+    from triton_kubernetes_amd.terraform import catalog, hcl
+
     for key, block in (st.doc.get("module") or {}).items():
         info = catalog.module_from_source(block["source"])
         assert info is not None, f"{key}: unknown module source {block['source']}"
-        extra = set(block) - {"source"} - declared[info.name]
+        local = catalog.local_module_dir(block["source"])
+        mod_dir = local if local is not None else info.local_dir
+        assert os.path.isfile(os.path.join(mod_dir, "main.tf")), f"{key}: {block['source']} has no main.tf"
+        rep = hcl.check_module(mod_dir)
+        assert not rep.errors, rep.errors
+        extra = set(block) - {"source"} - rep.variables
         assert not extra, f"{key} -> {info.name}: keys not declared as module variables: {sorted(extra)}"
-        required = {v.name for m in generate.modules() if m.name == info.name for v in m.variables
-                    if v.default is None}
-        missing = required - set(block)
+        missing = rep.required - set(block)
         assert not missing, f"{key} -> {info.name}: required variables not set: {sorted(missing)}"

@@ -18,13 +18,13 @@ from helpers import make_ctx, output
 
 @pytest.fixture
 def cluster(tmp_path):
-    fake = FakeRancher().start()
+    fake = FakeRancher.for_manager("mgr", "tk-admin-pw-0123").start()
     backend = LocalBackend(str(tmp_path / "state"))
     base = {"executor": "direct"}
-    new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="pw",
+    new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
                               host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
     new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="prod",
-                              k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico")), backend)
+                              k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico")), backend)
     tf = json.loads(backend.read_tfstate("mgr"))
     mgr = tf["module_outputs"]["cluster-manager"]
     cid = tf["module_outputs"]["cluster_baremetal_prod"]["rancher_cluster_id"]

@@ -27,7 +27,7 @@ TOKEN = "test-token-123456"
 
 @pytest.fixture
 def env(tmp_path):
-    fake = FakeRancher().start()
+    fake = FakeRancher.for_manager("mgr", "s3cret-passw0rd").start()
     agents = []
 
     def agent(name, gpus=0, fail_burnin=False):
@@ -46,7 +46,7 @@ def env(tmp_path):
 
 
 def _manager(fake, backend, base):
-    new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="s3cret",
+    new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="s3cret-passw0rd",
                               host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
                 backend)
 
@@ -66,11 +66,11 @@ def _nodes(cp, workers, gpu=True, count=8):
 def test_full_bringup_with_gpu_addons_and_wait(env):
     fake, agent, backend, base = env
     _manager(fake, backend, base)
-    assert fake.state.admin_password == "s3cret"  # S3: password changed
+    assert fake.state.admin_password == "s3cret-passw0rd"  # S3: password changed
     cp = agent("cp")
     workers = [agent(f"w{i}", gpus=8) for i in range(3)]
     ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
-                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
+                        k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
                         nodes=_nodes(cp, workers)))
     new_cluster(ctx, backend)
     out = output(ctx)
@@ -118,7 +118,7 @@ def test_failed_node_blocks_addons_and_resume(env):
     cp = agent("cp")
     good, bad = agent("good", gpus=8), agent("bad", gpus=8, fail_burnin=True)
     ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
-                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", gpu_addons=True,
+                        k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", gpu_addons=True,
                         nodes=_nodes(cp, [good, bad])))
     with pytest.raises(TKError) as exc:
         new_cluster(ctx, backend)
@@ -155,7 +155,7 @@ def test_unsupported_module_and_parallel_fanout(env):
     client = RancherClient(fake.url)
     rec = RecordingTransport(delay=0.2)
     ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="wide",
-                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel",
+                        k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel",
                         nodes=[{"rancher_host_label": "worker", "node_count": 40, "hostname": "w", "ssh_user": "u",
                                 "bastion_host": "", "key_path": "k", "hosts": [f"10.1.0.{i}" for i in range(40)]}]))
     ctx.extras["transport"] = TransportRouter(ssh=rec, agent=AgentTransport(token=TOKEN))
@@ -175,7 +175,7 @@ def test_pipelined_rccl_gate_through_agents(env):
     cp = agent("cp")
     workers = [agent(f"w{i}", gpus=8) for i in range(3)]
     ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="gate",
-                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
+                        k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
                         rccl_gate=True, nodes=_nodes(cp, workers)))
     from triton_kubernetes_amd.utils.trace import TRACER
 
@@ -198,7 +198,7 @@ def test_gate_released_when_apply_fails(env):
     good = agent("good", gpus=8)
     bad = agent("bad", gpus=8, fail_burnin=True)
     ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="fail",
-                        k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
+                        k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico", gpu_addons=True, wait=True,
                         rccl_gate=True, nodes=_nodes(cp, [good, bad])))
     with pytest.raises(TKError):
         new_cluster(ctx, backend)
@@ -228,7 +228,7 @@ def test_host_retry_recovers_flaky_node(env):
         cp = agent("cp")
         events = []
         ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="retry",
-                            k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico", host_retries=2,
+                            k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico", host_retries=2,
                             host_retry_backoff="0.01", nodes=_nodes(cp, [url])))
         new_cluster(ctx, backend)
         tf = json.loads(backend.read_tfstate("mgr"))
@@ -237,7 +237,7 @@ def test_host_retry_recovers_flaky_node(env):
         # without retries the same flake fails the apply
         calls["n"] = 0
         ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="noretry",
-                            k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico",
+                            k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico",
                             nodes=_nodes(cp, [url])))
         with pytest.raises(TKError):
             new_cluster(ctx, backend)
@@ -303,13 +303,13 @@ def test_fake_rancher_settles_clusters(env):
     cp = agent("cp")
     for name in ("one", "two"):
         new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name=name,
-                                  k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", wait=True,
+                                  k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", wait=True,
                                   nodes=_nodes(cp, [agent(f"{name}-w", gpus=8)]))), backend)
     # a settled cluster is no longer walked by the simulation; each cluster lists its own nodes
     assert fake.state.unsettled == set()
     cids = {c["name"]: c["id"] for c in fake.state.clusters.values()}
     assert {n["metadata"]["name"] for n in fake.k8s_nodes(cids["two"])} == {"cp-1", "etcd-1", "gpu-1"}
-    user, _, secret = RancherClient(fake.url).login("admin", "s3cret").partition(":")
+    user, _, secret = RancherClient(fake.url).login("admin", "s3cret-passw0rd").partition(":")
     client = RancherClient(fake.url, user, secret)
     assert {n["clusterId"] for n in client.nodes(cids["one"])} == {cids["one"]}
 
@@ -333,10 +333,10 @@ def test_fake_rancher_node_delete_keeps_cluster_index(env):
     _manager(fake, backend, base)
     cp = agent("cp")
     new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
-                              k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", wait=True,
+                              k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", wait=True,
                               nodes=_nodes(cp, [agent("w", gpus=8)]))), backend)
     cid = next(iter(fake.state.clusters))
-    user, _, secret = RancherClient(fake.url).login("admin", "s3cret").partition(":")
+    user, _, secret = RancherClient(fake.url).login("admin", "s3cret-passw0rd").partition(":")
     client = RancherClient(fake.url, user, secret)
     gpu = next(n for n in client.nodes(cid) if n["hostname"] == "gpu-1")
     client.http.request("DELETE", f"/v3/nodes/{gpu['id']}", ok=(200,))

@@ -53,7 +53,7 @@ def test_baremetal_mi355x_examples_via_cli(tk_home, tmp_path, monkeypatch):
     mods = doc["module"]
     assert "addons_baremetal_mi355x" in mods
     gpu = mods["node_baremetal_mi355x_mi355x-gpu-1"]
-    assert gpu["source"].endswith("bare-metal-mi355x-rancher-k8s-host?ref=master")
+    assert gpu["source"].endswith("terraform/modules/bare-metal-mi355x-rancher-k8s-host")
     assert gpu["rccl_env"]["NCCL_SOCKET_IFNAME"] == "ens50f0" and gpu["gpu_count"] == "8"
     assert sum(1 for k in mods if k.startswith("node_")) == 8
     state = json.load(open(tk_home / ".triton-kubernetes" / "mi355x-manager" / "main.tf.json"))

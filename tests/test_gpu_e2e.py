@@ -23,17 +23,17 @@ def test_real_gpu_bringup(tmp_path):
     from helpers import make_ctx, output
 
     token = "gpu-e2e-token-1234"
-    fake = FakeRancher().start()
+    fake = FakeRancher.for_manager("mgr", "tk-admin-pw-0123").start()
     cp = NodeAgent(name="cp", mode="sim", token=token, root=tempfile.mkdtemp())
     w = NodeAgent(name="w0", mode="sim", devices=[0], token=token, root=tempfile.mkdtemp())
     cp_url, w_url = cp.serve(), w.serve()
     backend = LocalBackend(str(tmp_path / "state"))
     base = {"executor": "direct", "agent_token": token}
     try:
-        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="p",
+        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
                                   host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
         ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="gpu",
-                            k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", gpu_addons=True,
+                            k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", gpu_addons=True,
                             wait=True, rccl_gate=True, nodes=[
                                 {"rancher_host_label": "control", "node_count": 1, "hostname": "cp", "ssh_user": "u",
                                  "bastion_host": "", "key_path": "k", "hosts": ["agent+" + cp_url]},

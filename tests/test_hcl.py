@@ -1,0 +1,128 @@
+"""HCL2 parser + static module checker (terraform/hcl.py) over all 19 shipped modules.
+
+No terraform binary exists in CI, so the modules are parsed here: syntax (blocks,
+strings, heredocs, ``%{}`` directives), references (var/local/data/resource), and
+``templatefile`` vars against the placeholders of the template they render.  Each
+check must also fail on a deliberately broken fixture.
+"""
+
+import os
+import shutil
+
+import pytest
+
+from triton_kubernetes_amd.terraform import catalog, hcl
+
+MODULE_NAMES = sorted(os.listdir(catalog.MODULES_DIR))
+
+
+def test_all_nineteen_modules_present():
+    assert len(MODULE_NAMES) == 19 and set(MODULE_NAMES) == set(catalog.CATALOG)
+
+
+@pytest.mark.parametrize("name", MODULE_NAMES)
+def test_module_parses_and_cross_checks(name):
+    rep = hcl.check_module(os.path.join(catalog.MODULES_DIR, name))
+    assert not rep.errors, "\n".join(rep.errors)
+    assert set(rep.files) == {"main.tf", "variables.tf", "outputs.tf", "versions.tf"}
+    info = catalog.CATALOG[name]
+    assert set(info.outputs) <= rep.outputs
+
+
+@pytest.mark.parametrize("name", MODULE_NAMES)
+def test_templates_parse(name):
+    files = os.path.join(catalog.MODULES_DIR, name, "files")
+    for dirpath, _, fnames in os.walk(files):
+        for fn in fnames:
+            if fn.endswith(".tftpl"):
+                with open(os.path.join(dirpath, fn), encoding="utf-8") as fh:
+                    hcl.parse_template(fh.read(), fn)
+
+
+def test_templatefile_calls_found_and_matched():
+    rep = hcl.check_module(os.path.join(catalog.MODULES_DIR, "bare-metal-rancher"))
+    calls = [n for n in hcl.walk(rep.files["main.tf"]) if n.kind == "call" and n.value == "templatefile"]
+    assert [hcl._module_relative_path(c.children[0]) for c in calls] == [
+        "files/install_docker.sh.tftpl", "files/install_rancher_server.sh.tftpl", "files/setup_rancher.sh.tftpl"]
+
+
+GOOD = [
+    'a = { k = 1, k2 = 2 }',
+    'a = [for k, v in m : v if k != "x"]',
+    'a = {for k, v in m : k => v...}',
+    'x = a.b[0].c[*].d',
+    'x = !a && b || c ? 1 : -2',
+    'x = f(a...)',
+    'x = <<-EOT\n  %{for x in y~}\n  ${x}\n  %{endfor~}\n  EOT\n',
+    'x = "$${lit} %%{lit}"',
+    'resource "a" "b" {\n  dynamic "d" {\n    for_each = var.x\n    content { v = d.value }\n  }\n}\n',
+    'x = (\n  1 +\n  2\n)',
+]
+BAD = [
+    'a = {',
+    'x = 1 +',
+    'resource "a" "b" {\n c = "x\n}',
+    'a = <<EOT\nhello\n',
+    'a = "${var.x"',
+    'a = "%{ if x }y"',
+    'a = "%{ endif }"',
+    'a = [for x in y : ]',
+    'b {\n c = d e\n}',
+    'a = f(1,,2)',
+    'a = { k = 1 k2 = 2 }',
+    'a = "\\q"',
+    'block "x" {\n a = 1\n',
+]
+
+
+@pytest.mark.parametrize("src", GOOD)
+def test_parser_accepts(src):
+    hcl.parse(src)
+
+
+@pytest.mark.parametrize("src", BAD)
+def test_parser_rejects(src):
+    with pytest.raises(hcl.HCLSyntaxError):
+        hcl.parse(src)
+
+
+def _broken_copy(tmp_path, edit):
+    src = os.path.join(catalog.MODULES_DIR, "bare-metal-rancher")
+    dst = tmp_path / "bare-metal-rancher"
+    shutil.copytree(src, dst, symlinks=True)
+    edit(dst)
+    return hcl.check_module(str(dst))
+
+
+def _replace(path, old, new):
+    text = path.read_text()
+    assert old in text, old
+    path.write_text(text.replace(old, new, 1))
+
+
+@pytest.mark.parametrize("case,edit,expect", [
+    ("syntax", lambda d: _replace(d / "main.tf", "triggers_replace = [local.rancher_master_id]",
+                                  "triggers_replace = [local.rancher_master_id"), "expected"),
+    ("templatefile missing var", lambda d: _replace(d / "main.tf", "      bootstrap_password   = local.bootstrap_password\n",
+                                                    ""), "does not pass ['bootstrap_password']"),
+    ("templatefile unused var", lambda d: _replace(d / "main.tf", "      bootstrap_password   = local.bootstrap_password\n",
+                                                   "      bootstrap_password   = local.bootstrap_password\n"
+                                                   "      extra_thing          = 1\n"), "passes unused ['extra_thing']"),
+    ("undeclared var", lambda d: _replace(d / "main.tf", "var.ssh_user", "var.ssh_usr"), "undeclared variable var.ssh_usr"),
+    ("undefined local", lambda d: _replace(d / "main.tf", "local.rancher_master_ip\n", "local.rancher_master_ipp\n"),
+     "undefined local.rancher_master_ipp"),
+    ("undefined resource", lambda d: _replace(d / "main.tf", "[terraform_data.install_docker]",
+                                              "[terraform_data.install_dockr]"),
+     "undefined resource terraform_data.install_dockr"),
+    ("template directive", lambda d: _replace(d / "files" / "install_docker.sh.tftpl", "%{ endif ~}\n", "", ),
+     "is never closed"),
+    ("template missing file", lambda d: os.remove(d / "files" / "setup_rancher.sh.tftpl"), "missing file"),
+])
+def test_checker_catches_broken_fixture(tmp_path, case, edit, expect):
+    rep = _broken_copy(tmp_path, edit)
+    assert any(expect in e for e in rep.errors), (case, rep.errors)
+
+
+def test_template_names_respect_for_bindings():
+    parts = hcl.parse_template("%{ for x in items ~}${x}-${suffix}%{ endfor ~}${other.attr}")
+    assert hcl.template_names(parts) == {"items", "suffix", "other"}

@@ -67,7 +67,7 @@ def test_interactive_create_manager_over_terminal(tk_home):
         "",             # Private Registry [None]
         "",             # Rancher Server Image [Default]
         "",             # Rancher Agent Image [Default]
-        "s3cret",       # UI admin password
+        "s3cret-passw0rd",  # UI admin password
         "10.0.0.9",     # host
         "",             # ssh user [ubuntu]
         "",             # Bastion Host [None]
@@ -92,4 +92,4 @@ def test_interactive_create_manager_over_terminal(tk_home):
     except TKError as exc:  # surface the dialogue on failure
         raise AssertionError(out.getvalue()) from exc
     m = be.state("lab").manager()
-    assert m["host"] == "10.0.0.9" and m["ssh_user"] == "ubuntu" and m["rancher_admin_password"] == "s3cret"
+    assert m["host"] == "10.0.0.9" and m["ssh_user"] == "ubuntu" and m["rancher_admin_password"] == "s3cret-passw0rd"

@@ -5,6 +5,7 @@ Every provider's manager / cluster / node builder is driven through the real
 """
 
 import json
+import os
 
 import pytest
 
@@ -12,11 +13,12 @@ from triton_kubernetes_amd.cloud.fake import FakeCloud
 from triton_kubernetes_amd.errors import TKError
 from triton_kubernetes_amd.models import aws, azure, baremetal, gcp, triton, vsphere
 from triton_kubernetes_amd.state import State
+from triton_kubernetes_amd.terraform import catalog
 
 from helpers import assert_blocks_match_modules, make_ctx, make_ssh_key
 
-BASE_MGR = {"rancher_admin_password": "pw"}
-BASE_CLUSTER = {"name": "dev", "k8s_version": "v1.9.5-rancher1-1", "k8s_network_provider": "flannel"}
+BASE_MGR = {"rancher_admin_password": "tk-admin-pw-0123"}
+BASE_CLUSTER = {"name": "dev", "k8s_version": "v1.28.10-rancher1-1", "k8s_network_provider": "flannel"}
 NODE_BASE = {"rancher_host_label": "worker", "node_count": 2, "hostname": "dev-w"}
 
 
@@ -45,7 +47,9 @@ def test_baremetal_manager_document():
     baremetal.new_manager(make_ctx(dict(BASE_MGR, host="10.0.0.10", ssh_user="ubuntu", bastion_host="",
                                         key_path="~/.ssh/id_rsa")), st, "mgr")
     m = st.manager()
-    assert m["source"] == "github.com/joyent/triton-kubernetes//terraform/modules/bare-metal-rancher?ref=master"
+    # default: this package's own module tree (a local path Terraform reads directly)
+    assert m["source"] == os.path.join(catalog.PACKAGE_ROOT, "terraform", "modules", "bare-metal-rancher")
+    assert os.path.isfile(os.path.join(m["source"], "main.tf"))
     assert list(m) == ["source", "name", "rancher_admin_password", "host", "ssh_user", "key_path"]
     assert m["key_path"] == "~/.ssh/id_rsa"  # not expanded (reference quirk Q11 kept)
     assert_blocks_match_modules(st)
@@ -116,7 +120,7 @@ def test_mi355x_node_and_addons():
     baremetal.new_node(make_ctx(dict(NODE_BASE, ssh_user="u", bastion_host="", key_path="k", gpu="mi355x",
                                      hosts=["a", "b"], rccl_env={"NCCL_SOCKET_IFNAME": "eth0"})), "m", key, None, st)
     n = st.module("node_baremetal_dev_dev-w-1")
-    assert n["source"].endswith("terraform/modules/bare-metal-mi355x-rancher-k8s-host?ref=master")
+    assert n["source"].endswith("terraform/modules/bare-metal-mi355x-rancher-k8s-host")
     assert n["gpu_count"] == "8" and n["gpu_burnin"] == "quick" and n["gpu_product"] == "MI355X"
     assert n["rccl_env"]["NCCL_SOCKET_IFNAME"] == "eth0" and n["rccl_env"]["HSA_FORCE_FINE_GRAIN_PCIE"] == "1"
     assert_blocks_match_modules(st)
@@ -133,10 +137,8 @@ def test_mi355x_node_and_addons():
 
 def test_interactive_baremetal_manager_prompts():
     st = State("mgr")
-    answers = ["None", "Default", "Default", "pw", "10.0.0.9", "", "None", "~/.ssh/id_rsa"]
+    answers = ["None", "Default", "Default", "tk-admin-pw-0123", "10.0.0.9", "", "None", "~/.ssh/id_rsa"]
     ctx = make_ctx({}, answers=answers, non_interactive=False)
-    import os
-
     os.makedirs(os.path.expanduser("~/.ssh"), exist_ok=True)
     keyfile = os.path.expanduser("~/.ssh/id_rsa")
     created = not os.path.exists(keyfile)

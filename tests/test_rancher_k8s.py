@@ -17,9 +17,9 @@ from triton_kubernetes_amd.readiness.waiter import ReadinessSpec, wait_ready
 
 @pytest.fixture
 def rancher():
-    fake = FakeRancher().start()
+    fake = FakeRancher(bootstrap_password="b00tstrap-only").start()
     client = RancherClient(fake.url)
-    outs = client.bootstrap("n3w-pass", fake.url, timeout=10)
+    outs = client.bootstrap("n3w-passw0rd-123", fake.url, "b00tstrap-only", timeout=10)
     yield fake, RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"]), outs
     fake.stop()
 
@@ -31,24 +31,25 @@ def test_ca_checksum_matches_reference_shasum():
 
 def test_bootstrap_s3(rancher):
     fake, client, outs = rancher
-    assert fake.state.admin_password == "n3w-pass"
+    assert fake.state.admin_password == "n3w-passw0rd-123"
     assert fake.state.settings["server-url"] == fake.url
     assert outs["rancher_url"] == fake.url and outs["rancher_access_key"] and outs["rancher_secret_key"]
     assert client.ping()
-    # the initial admin/admin login no longer works
-    with pytest.raises(TKError):
-        RancherClient(fake.url).login("admin", "admin")
+    # neither admin/admin (Rancher >= 2.6 has none) nor the bootstrap password works now
+    for pw in ("admin", "b00tstrap-only"):
+        with pytest.raises(TKError):
+            RancherClient(fake.url).login("admin", pw)
 
 
 def test_ensure_cluster_is_idempotent_s4(rancher):
     fake, client, _ = rancher
-    a = client.ensure_cluster("dev", "v1.9.5-rancher1-1", "calico")
+    a = client.ensure_cluster("dev", "v1.28.10-rancher1-1", "calico")
     b = client.ensure_cluster("dev")
     assert a.cluster_id == b.cluster_id and not a.existed and b.existed
     assert a.registration_token == b.registration_token  # reused, not re-created
     assert a.ca_checksum == ca_checksum(FAKE_CACERTS)
     rke = fake.state.clusters[a.cluster_id]["rancherKubernetesEngineConfig"]
-    assert rke["kubernetesVersion"] == "v1.9.5-rancher1-1" and rke["network"]["plugin"] == "calico"
+    assert rke["kubernetesVersion"] == "v1.28.10-rancher1-1" and rke["network"]["plugin"] == "calico"
     assert client.ensure_cluster("other").cluster_id != a.cluster_id
 
 

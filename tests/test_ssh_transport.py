@@ -64,11 +64,11 @@ def test_ssh_argv_options(tmp_path):
 
 def test_cluster_over_ssh_runs_rendered_plans(tmp_path, fake_ssh):
     log, sudo_log = fake_ssh
-    fake = FakeRancher().start()
+    fake = FakeRancher.for_manager("mgr", "tk-admin-pw-0123").start()
     try:
         backend = LocalBackend(str(tmp_path / "state"))
         base = {"executor": "direct"}
-        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="pw",
+        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
                                   host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
                     backend)
         nodes = [{"rancher_host_label": "etcd", "node_count": 1, "hostname": "e", "ssh_user": "core",
@@ -76,7 +76,7 @@ def test_cluster_over_ssh_runs_rendered_plans(tmp_path, fake_ssh):
                  {"rancher_host_label": "worker", "node_count": 2, "hostname": "w", "ssh_user": "core",
                   "bastion_host": "jump.example", "key_path": "~/.ssh/id", "hosts": ["10.1.0.2", "10.1.0.3"]}]
         new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="ssh",
-                                  k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel", nodes=nodes)),
+                                  k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", nodes=nodes)),
                     backend)
         calls = _calls(log)
         targets = sorted(c[-2] for c in calls)
@@ -98,18 +98,18 @@ def test_cluster_over_ssh_runs_rendered_plans(tmp_path, fake_ssh):
 
 
 def test_unreachable_host_fails_only_its_module(tmp_path, fake_ssh):
-    fake = FakeRancher().start()
+    fake = FakeRancher.for_manager("mgr", "tk-admin-pw-0123").start()
     try:
         backend = LocalBackend(str(tmp_path / "state"))
         base = {"executor": "direct"}
-        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="pw",
+        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
                                   host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
                     backend)
         nodes = [{"rancher_host_label": "worker", "node_count": 2, "hostname": "w", "ssh_user": "core",
                   "bastion_host": "", "key_path": "k", "hosts": ["10.2.0.1", "fail-10.2.0.2"]}]
         with pytest.raises(TKError) as exc:
             new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="x",
-                                      k8s_version="v1.9.5-rancher1-1", k8s_network_provider="flannel",
+                                      k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel",
                                       nodes=nodes)), backend)
         assert "w-2" in str(exc.value) and "re-run to resume" in str(exc.value)
         tf = json.loads(backend.read_tfstate("mgr"))

@@ -31,14 +31,14 @@ def test_render_cloud_init_document():
 
 
 def test_userdata_node_from_applied_cluster(tmp_path):
-    fake = FakeRancher().start()
+    fake = FakeRancher.for_manager("mgr", "tk-admin-pw-0123").start()
     try:
         backend = LocalBackend(str(tmp_path / "state"))
         base = {"executor": "direct"}
-        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="pw",
+        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
                                   host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
         new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="pxe",
-                                  k8s_version="v1.9.5-rancher1-1", k8s_network_provider="calico")), backend)
+                                  k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico")), backend)
         # the node is only recorded (its delivery will be cloud-init): persist without applying the host
         from triton_kubernetes_amd.models import baremetal
 

@@ -1,0 +1,137 @@
+"""Pinned versions are coherent across every delivery path, and the fake Rancher enforces
+what a real Rancher v2.8.5 enforces (bootstrap password, KDM Kubernetes list, password length).
+
+Reference: ``/root/reference/create/cluster.go:349-356`` (k8s choices of its pinned
+server) and ``/root/reference/terraform/modules/triton-rancher/variables.tf:14-22``.
+"""
+
+import hashlib
+import os
+import re
+
+import pytest
+
+from triton_kubernetes_amd import versions
+from triton_kubernetes_amd.errors import ConfigError, TKError
+from triton_kubernetes_amd.models import baremetal
+from triton_kubernetes_amd.node import manager as node_manager
+from triton_kubernetes_amd.node import plan as node_plan
+from triton_kubernetes_amd.rancher.client import RancherClient
+from triton_kubernetes_amd.rancher.fake import FakeRancher
+from triton_kubernetes_amd.state import State
+from triton_kubernetes_amd.terraform import generate
+from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+
+from helpers import make_ctx
+
+OLD = "v1.9.5-rancher1-1"  # the reference's default: no RKE1 release of Rancher 2.8
+
+
+def _var_default(module: str, var: str) -> str:
+    text = open(os.path.join(MODULES_DIR, module, "variables.tf"), encoding="utf-8").read()
+    m = re.search(r'variable "%s" \{.*?default\s+=\s+"([^"]*)"' % var, text, re.S)
+    assert m, (module, var)
+    return m.group(1)
+
+
+def test_defaults_agree_everywhere():
+    assert versions.DEFAULT_K8S_VERSION in [v for _, v in versions.K8S_VERSIONS]
+    for mod in ("bare-metal-rancher-k8s", "triton-rancher-k8s", "aws-rancher-k8s", "gcp-rancher-k8s",
+                "azure-rancher-k8s", "vsphere-rancher-k8s"):
+        assert _var_default(mod, "k8s_version") == versions.DEFAULT_K8S_VERSION
+    for mod in ("bare-metal-rancher", "triton-rancher", "aws-rancher", "gcp-rancher", "azure-rancher"):
+        assert _var_default(mod, "rancher_server_image") == versions.SERVER_IMAGE
+        assert _var_default(mod, "docker_engine_install_url") == versions.DOCKER_INSTALL_URL
+    for mod in ("bare-metal-rancher-k8s-host", "bare-metal-mi355x-rancher-k8s-host", "aws-rancher-k8s-host"):
+        assert _var_default(mod, "rancher_agent_image") == versions.AGENT_IMAGE
+        assert _var_default(mod, "docker_engine_install_url") == versions.DOCKER_INSTALL_URL
+    assert node_manager.DEFAULT_SERVER_IMAGE == versions.SERVER_IMAGE
+    assert node_manager.DEFAULT_DOCKER_INSTALL_URL == node_plan.DEFAULT_DOCKER_INSTALL_URL == versions.DOCKER_INSTALL_URL
+    assert node_plan.DEFAULT_AGENT_IMAGE == versions.AGENT_IMAGE
+    assert versions.SERVER_IMAGE.endswith(versions.RANCHER_VERSION) and versions.AGENT_IMAGE.endswith(
+        versions.RANCHER_VERSION)
+    for img in (versions.DEVICE_PLUGIN_IMAGE, versions.NODE_LABELLER_IMAGE, versions.RCCL_PROBE_IMAGE):
+        assert ":" in img and not img.endswith(":latest") and "latest" not in img.split(":")[1]
+    assert _var_default("rancher-k8s-mi355x-addons", "device_plugin_image") == versions.DEVICE_PLUGIN_IMAGE
+
+
+def test_cli_rejects_kubernetes_releases_outside_the_pinned_rancher():
+    st = State("mgr")
+    st.set_manager({"source": "x", "name": "mgr"})
+    ctx = make_ctx({"name": "dev", "k8s_version": OLD, "k8s_network_provider": "flannel"})
+    with pytest.raises(ConfigError, match="not offered by Rancher v2.8.5"):
+        baremetal.new_cluster(ctx, None, st)
+    # the display name maps to the pinned release; a patch release of a pinned minor passes through
+    for given, want in (("v1.27", "v1.27.14-rancher1-1"), ("v1.28.12-rancher1-1", "v1.28.12-rancher1-1")):
+        st = State("mgr")
+        st.set_manager({"source": "x", "name": "mgr"})
+        baremetal.new_cluster(make_ctx({"name": "dev", "k8s_version": given, "k8s_network_provider": "flannel"}),
+                              None, st)
+        assert st.get("module.cluster_baremetal_dev.k8s_version") == want
+
+
+def test_short_admin_password_rejected():
+    st = State("mgr")
+    ctx = make_ctx({"name": "mgr", "rancher_admin_password": "admin", "host": "10.0.0.1", "ssh_user": "u",
+                    "bastion_host": "", "key_path": "k"})
+    with pytest.raises(ConfigError, match="at least 12 characters"):
+        baremetal.new_manager(ctx, st, "mgr")
+
+
+def test_fake_rancher_has_no_admin_admin_and_enforces_kdm():
+    with FakeRancher() as fake:  # started without CATTLE_BOOTSTRAP_PASSWORD: random first password
+        with pytest.raises(TKError):
+            RancherClient(fake.url).login("admin", "admin")
+    with FakeRancher(bootstrap_password="b00t-b00t-b00t") as fake:
+        with pytest.raises(TKError):
+            RancherClient(fake.url).bootstrap("long-enough-pw", fake.url, "admin", timeout=5)
+        with pytest.raises(TKError, match="at least 12"):  # password-min-length
+            RancherClient(fake.url).bootstrap("short", fake.url, "b00t-b00t-b00t", timeout=5)
+        outs = RancherClient(fake.url).bootstrap("long-enough-pw", fake.url, "b00t-b00t-b00t", timeout=5)
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        assert client.k8s_versions() == [v for _, v in versions.K8S_VERSIONS]
+        with pytest.raises(TKError, match="not offered"):  # client-side check against the server list
+            client.ensure_cluster("old", OLD)
+        with pytest.raises(TKError, match="HTTP 422"):  # and the server itself refuses it
+            client.create_cluster("old", OLD, "flannel")
+        assert client.ensure_cluster("new").cluster_id
+        # re-running the bootstrap after the password change (resume) logs in with the admin password
+        again = RancherClient(fake.url).bootstrap("long-enough-pw", fake.url, "b00t-b00t-b00t", timeout=5)
+        assert again["rancher_access_key"] and fake.state.admin_password == "long-enough-pw"
+
+
+def test_same_minor_release_substituted_from_the_server_list():
+    with FakeRancher(bootstrap_password="b00t-b00t-b00t", k8s_versions=["v1.28.15-rancher1-1", "v1.27.16-rancher1-1"]) \
+            as fake:
+        outs = RancherClient(fake.url).bootstrap("long-enough-pw", fake.url, "b00t-b00t-b00t", timeout=5)
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        info = client.ensure_cluster("dev", versions.DEFAULT_K8S_VERSION)
+        rke = fake.state.clusters[info.cluster_id]["rancherKubernetesEngineConfig"]
+        assert rke["kubernetesVersion"] == "v1.28.15-rancher1-1"
+        assert "using v1.28.15-rancher1-1" in client.last_version_note
+        with pytest.raises(TKError):
+            client.ensure_cluster("gone", "v1.26.15-rancher1-1")
+
+
+def test_bootstrap_password_same_in_python_and_terraform():
+    want = hashlib.sha256(b"tk-bootstrap:mgr:tk-admin-pw-0123").hexdigest()[:32]
+    assert versions.bootstrap_password("mgr", "tk-admin-pw-0123") == want
+    for mod in ("bare-metal-rancher", "triton-rancher", "aws-rancher", "gcp-rancher", "azure-rancher"):
+        main = open(os.path.join(MODULES_DIR, mod, "main.tf"), encoding="utf-8").read()
+        assert 'substr(sha256("tk-bootstrap:${var.name}:${var.rancher_admin_password}"), 0, 32)' in main
+        assert "bootstrap_password   = local.bootstrap_password" in main
+        server = open(os.path.join(MODULES_DIR, mod, "files", "install_rancher_server.sh.tftpl")).read()
+        assert "-e CATTLE_BOOTSTRAP_PASSWORD='${bootstrap_password}'" in server
+        setup = open(os.path.join(MODULES_DIR, mod, "files", "setup_rancher.sh.tftpl")).read()
+        assert '"password":"admin"' not in setup and "login_as '${bootstrap_password}'" in setup
+    script = node_manager.manager_install_script({"rancher_admin_password": "x" * 12}, want)
+    assert f"-e CATTLE_BOOTSTRAP_PASSWORD={want}" in script
+    assert "| sudo sh" not in script  # downloaded, then run
+
+
+def test_docker_install_checksum_is_enforced_when_given():
+    lines = node_manager.docker_install_lines("https://x/24.0.sh", "ab" * 32)
+    assert "sha256sum -c" in lines and "curl -fsSL -o /tmp/tk-install-docker.sh" in lines
+    assert "sha256sum" not in node_manager.docker_install_lines("https://x/24.0.sh")
+    tpl = generate.scripts.DOCKER_INSTALL
+    assert '%{ if docker_install_sha256 != "" ~}' in tpl and "| sudo sh" not in tpl

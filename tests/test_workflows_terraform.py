@@ -20,10 +20,10 @@ from triton_kubernetes_amd.workflows.create import read_status
 
 from helpers import install_fake_terraform, make_ctx, output, tf_calls
 
-MGR = {"manager_cloud_provider": "baremetal", "name": "mgr", "rancher_admin_password": "pw", "host": "10.0.0.10",
+MGR = {"manager_cloud_provider": "baremetal", "name": "mgr", "rancher_admin_password": "tk-admin-pw-0123", "host": "10.0.0.10",
        "ssh_user": "ubuntu", "bastion_host": "", "key_path": "~/.ssh/id_rsa", "executor": "terraform"}
 CLUSTER = {"cluster_manager": "mgr", "cluster_cloud_provider": "baremetal", "name": "dev",
-           "k8s_version": "v1.9.5-rancher1-1", "k8s_network_provider": "flannel", "executor": "terraform",
+           "k8s_version": "v1.28.10-rancher1-1", "k8s_network_provider": "flannel", "executor": "terraform",
            "nodes": [
                {"rancher_host_label": "etcd", "node_count": 1, "hostname": "dev-etcd", "ssh_user": "ubuntu",
                 "key_path": "~/.ssh/id_rsa", "bastion_host": "", "hosts": ["10.0.0.11"]},

@@ -46,6 +46,7 @@ from ..rancher.client import RancherClient, wait_until
 from ..state import State
 from ..terraform.catalog import ModuleInfo, module_from_source
 from ..utils.trace import span
+from ..versions import DEFAULT_K8S_VERSION, bootstrap_password
 from .base import Executor, outputs_from_tfstate
 from .tfstate import CODEC
 
@@ -304,31 +305,35 @@ class DirectExecutor(Executor):
     def _apply_manager(self, cfg: Dict[str, Any]) -> Dict[str, str]:
         host = str(cfg.get("host", ""))
         password = cfg.get("rancher_admin_password", "")
+        # the server's first-login password (CATTLE_BOOTSTRAP_PASSWORD): given for an adopted
+        # server, else the value every install path of this framework starts the server with
+        initial = cfg.get("rancher_bootstrap_password") or bootstrap_password(str(cfg.get("name", "")), password)
         if host.startswith("rancher+"):
             url = host[len("rancher+"):]
             client = self.rancher_factory(url)
-            return client.bootstrap(password, url, timeout=self.cluster_wait)
+            return client.bootstrap(password, url, initial, timeout=self.cluster_wait)
         ref = HostRef(host, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "~/.ssh/id_rsa",
                       cfg.get("bastion_host") or "")
         from ..node.manager import manager_install_script, manager_setup_script
 
         with span("manager.install", host=host):
-            self.transport.run_script(ref, manager_install_script(cfg), timeout=self.node_timeout)
+            self.transport.run_script(ref, manager_install_script(cfg, initial), timeout=self.node_timeout)
         url = f"https://{host}"
         if self.rancher_bootstrap == "remote":
             with span("manager.setup_remote", host=host):
-                out = self.transport.run_script(ref, manager_setup_script(cfg, url), timeout=self.node_timeout)
+                out = self.transport.run_script(ref, manager_setup_script(cfg, url, initial),
+                                                timeout=self.node_timeout)
             data = json.loads(out.strip().splitlines()[-1])
             return {"rancher_url": url, "rancher_access_key": data["name"],
                     "rancher_secret_key": data["token"].split(":", 1)[-1]}
         client = self.rancher_factory(url)
-        return client.bootstrap(password, url, timeout=self.cluster_wait)
+        return client.bootstrap(password, url, initial, timeout=self.cluster_wait)
 
     # --- cluster ---------------------------------------------------------------------------------------
     def _apply_cluster(self, cfg: Dict[str, Any]) -> Dict[str, str]:
         client = self.rancher_factory(cfg["rancher_api_url"], cfg.get("rancher_access_key", ""),
                                       cfg.get("rancher_secret_key", ""))
-        info = client.ensure_cluster(cfg["name"], cfg.get("k8s_version") or "v1.9.5-rancher1-1",
+        info = client.ensure_cluster(cfg["name"], cfg.get("k8s_version") or DEFAULT_K8S_VERSION,
                                      cfg.get("k8s_network_provider") or "flannel", cfg.get("k8s_registry", ""),
                                      cfg.get("k8s_registry_username", ""), cfg.get("k8s_registry_password", ""))
         return info.outputs()

@@ -19,21 +19,22 @@ from typing import Dict, List, Optional, Sequence, Tuple
 from ..config.context import Context, not_blank
 from ..errors import ConfigError
 from ..state import MANAGER_KEY, State
-from ..terraform.catalog import module_source
+from ..terraform.catalog import module_source, packaged_root
+from ..versions import K8S_VERSIONS, PASSWORD_MIN_LENGTH, normalize_k8s_version
 
-DEFAULT_SOURCE_URL = "github.com/joyent/triton-kubernetes"
+# The reference defaults to its own GitHub repo (create/cluster.go:20-21), which is
+# where its modules live.  This CLI's modules ship inside the package, so the default
+# is that directory (resolved at use: a zipapp extracts it to a cache first);
+# SOURCE_URL / SOURCE_REF still select a git or registry copy.
+DEFAULT_SOURCE_URL = ""  # "" = the packaged module tree (catalog.packaged_root())
 DEFAULT_SOURCE_REF = "master"
 
 DNS1123_RE = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*$")
 DNS1123_MESSAGE = ("A DNS-1123 subdomain must consist of lower case alphanumeric characters, '-' or '.', "
                    "and must start and end with an alphanumeric character")
 
-# interactive choices (create/cluster.go:349-356); display name -> value
-K8S_VERSIONS: List[Tuple[str, str]] = [
-    ("v1.8.10", "v1.8.10-rancher1-1"),
-    ("v1.9.5", "v1.9.5-rancher1-1"),
-    ("v1.10.0", "v1.10.0-rancher1-1"),
-]
+# interactive choices: display name -> value (create/cluster.go:349-356 offers the
+# releases of its pinned Rancher; these are the pinned Rancher v2.8.5's, versions.py)
 K8S_NETWORK_PROVIDERS = ["calico", "flannel"]
 HOST_LABELS = ["worker", "etcd", "control"]
 _ATOI_RE = re.compile(r"^[+-]?[0-9]+$")
@@ -48,6 +49,8 @@ def omit_empty(cfg: Dict, keys: Sequence[str]) -> Dict:
 
 def source_for(ctx: Context, module_path: str) -> str:
     url = ctx.get_string("source_url") if ctx.is_set("source_url") else DEFAULT_SOURCE_URL
+    if not url:
+        url = packaged_root()
     ref = ctx.get_string("source_ref") if ctx.is_set("source_ref") else DEFAULT_SOURCE_REF
     return module_source(url, module_path, ref)
 
@@ -129,6 +132,9 @@ def base_manager_config(ctx: Context, module_path: str, name: str) -> Dict:
         missing_message="UI Admin Password must be specified")
     if not cfg["rancher_admin_password"]:
         raise ConfigError("Invalid UI Admin password")
+    if len(cfg["rancher_admin_password"]) < PASSWORD_MIN_LENGTH:
+        # Rancher >= 2.6 rejects the password change with a shorter one (password-min-length)
+        raise ConfigError(f"UI Admin password must be at least {PASSWORD_MIN_LENGTH} characters")
     return omit_empty(cfg, ["rancher_admin_password", "rancher_server_image", "rancher_agent_image",
                             "rancher_registry", "rancher_registry_username", "rancher_registry_password"])
 
@@ -157,6 +163,10 @@ def base_cluster_config(ctx: Context, module_path: str) -> Dict:
     cfg["name"] = name
     cfg["k8s_version"] = ctx.resolve_choice("k8s_version", "Kubernetes Version",
                                             [d for d, _ in K8S_VERSIONS], values=[v for _, v in K8S_VERSIONS])
+    try:
+        cfg["k8s_version"] = normalize_k8s_version(cfg["k8s_version"])
+    except ValueError as exc:
+        raise ConfigError(str(exc)) from None
     cfg["k8s_network_provider"] = ctx.resolve_choice("k8s_network_provider", "Kubernetes Network Provider",
                                                      K8S_NETWORK_PROVIDERS)
     cfg["rancher_registry"] = ctx.resolve("private_registry", "Private Registry", required=False,

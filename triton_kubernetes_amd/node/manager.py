@@ -6,7 +6,9 @@ Re-designs of the reference's manager bootstrap (S1-S3,
 * install the container runtime only if absent (the reference always pipes a
   pinned 17.03 installer into ``sh``), data-root on ``/mnt/docker`` only when
   that mount exists (the reference hard-codes ``/home/ubuntu``, Q10);
-* ``docker run rancher/rancher`` — polling with a 1 s interval instead of 5 s;
+* ``docker run rancher/rancher`` with ``CATTLE_BOOTSTRAP_PASSWORD`` (Rancher ≥2.6
+  has no admin/admin; versions.bootstrap_password) — polling with a 1 s interval
+  instead of 5 s;
 * :func:`manager_setup_script` is the on-host variant of S3 used with
   ``rancher_bootstrap: remote`` (operator cannot reach port 443).
 """
@@ -15,15 +17,26 @@ import json
 import shlex
 from typing import Any, Dict
 
-DEFAULT_DOCKER_INSTALL_URL = "https://releases.rancher.com/install-docker/20.10.sh"
-DEFAULT_SERVER_IMAGE = "rancher/rancher:v2.8.5"
+from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
+from ..versions import SERVER_IMAGE as DEFAULT_SERVER_IMAGE
 
 
 def _q(v: Any) -> str:
     return shlex.quote(str(v))
 
 
-def manager_install_script(cfg: Dict[str, Any]) -> str:
+def docker_install_lines(url: str, sha256: str = "") -> str:
+    """Install the container runtime when absent: download, verify (when a checksum is
+    configured), then run — never ``curl | sh`` of an unchecked stream."""
+    check = (f"  echo {_q(sha256 + '  /tmp/tk-install-docker.sh')} | sha256sum -c - >/dev/null || "
+             f"{{ echo 'docker install script checksum mismatch' >&2; exit 1; }}\n") if sha256 else ""
+    return (f"if ! command -v docker >/dev/null 2>&1; then\n"
+            f"  curl -fsSL -o /tmp/tk-install-docker.sh {_q(url)}\n{check}"
+            f"  sudo sh /tmp/tk-install-docker.sh && rm -f /tmp/tk-install-docker.sh\n"
+            f"fi\n")
+
+
+def manager_install_script(cfg: Dict[str, Any], bootstrap_pw: str) -> str:
     url = cfg.get("docker_engine_install_url") or DEFAULT_DOCKER_INSTALL_URL
     image = cfg.get("rancher_server_image") or DEFAULT_SERVER_IMAGE
     reg, user, pw = (cfg.get("rancher_registry", ""), cfg.get("rancher_registry_username", ""),
@@ -32,14 +45,14 @@ def manager_install_script(cfg: Dict[str, Any]) -> str:
     return f"""#!/bin/bash
 set -euo pipefail
 if command -v firewalld >/dev/null 2>&1; then sudo systemctl disable --now firewalld.service || true; fi
-if ! command -v docker >/dev/null 2>&1; then curl -fsSL {_q(url)} | sudo sh; fi
-if mountpoint -q /mnt && [ ! -f /etc/docker/daemon.json ]; then
+{docker_install_lines(url, cfg.get("docker_install_sha256", ""))}if mountpoint -q /mnt && [ ! -f /etc/docker/daemon.json ]; then
   echo '{{"storage-driver": "overlay2", "data-root": "/mnt/docker"}}' | sudo tee /etc/docker/daemon.json >/dev/null
   sudo systemctl restart docker
 fi
 {login}sudo docker pull {_q(image)}
 if ! sudo docker ps --format '{{{{.Image}}}}' | grep -qx {_q(image)}; then
-  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 {_q(image)}
+  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 \\
+    -e CATTLE_BOOTSTRAP_PASSWORD={_q(bootstrap_pw)} {_q(image)}
 fi
 for i in $(seq 1 600); do
   curl -ksf https://127.0.0.1/ping >/dev/null 2>&1 && exit 0
@@ -49,24 +62,30 @@ echo 'rancher server did not come up' >&2; exit 1
 """
 
 
-def manager_setup_script(cfg: Dict[str, Any], server_url: str) -> str:
-    """On-host API bootstrap (S3); prints the token JSON as the last line."""
+def manager_setup_script(cfg: Dict[str, Any], server_url: str, bootstrap_pw: str) -> str:
+    """On-host API bootstrap (S3); prints the token JSON as the last line.  Logs in with
+    the bootstrap password, or — re-run after the change — with the admin password."""
     pw = cfg.get("rancher_admin_password", "")
     token_req = json.dumps({"type": "token", "description": "Managed by triton-kubernetes",
                             "name": "triton-kubernetes", "ttl": 0})
     url_req = json.dumps({"name": "server-url", "value": server_url})
-    pw_req = json.dumps({"currentPassword": "admin", "newPassword": pw})
-    login_req = json.dumps({"username": "admin", "password": "admin", "ttl": 60000})
+    pw_req = json.dumps({"currentPassword": bootstrap_pw, "newPassword": pw})
+    login_req = json.dumps({"username": "admin", "password": bootstrap_pw, "ttl": 60000})
+    relogin_req = json.dumps({"username": "admin", "password": pw, "ttl": 60000})
     return f"""#!/bin/bash
 set -euo pipefail
 R=https://127.0.0.1
-login=$(curl -ksf -X POST -H 'Content-Type: application/json' -d {_q(login_req)} "$R/v3-public/localProviders/local?action=login")
+changed=0
+login=$(curl -ksf -X POST -H 'Content-Type: application/json' -d {_q(login_req)} "$R/v3-public/localProviders/local?action=login") || {{
+  login=$(curl -ksf -X POST -H 'Content-Type: application/json' -d {_q(relogin_req)} "$R/v3-public/localProviders/local?action=login")
+  changed=1
+}}
 initial=$(printf '%s' "$login" | python3 -c 'import json,sys; print(json.load(sys.stdin)["token"])')
 tok=$(curl -ksf -u "$initial" -X POST -H 'Content-Type: application/json' -d {_q(token_req)} "$R/v3/token")
 printf '%s' "$tok" > ~/rancher_api_key && chmod 600 ~/rancher_api_key
 ak=$(printf '%s' "$tok" | python3 -c 'import json,sys; print(json.load(sys.stdin)["name"])')
 sk=$(printf '%s' "$tok" | python3 -c 'import json,sys; print(json.load(sys.stdin)["token"].split(":",1)[1])')
-curl -ksf -u "$ak:$sk" -X POST -H 'Content-Type: application/json' -d {_q(pw_req)} "$R/v3/users?action=changepassword" >/dev/null
+[ "$changed" = 1 ] || curl -ksf -u "$ak:$sk" -X POST -H 'Content-Type: application/json' -d {_q(pw_req)} "$R/v3/users?action=changepassword" >/dev/null
 curl -ksf -u "$ak:$sk" -X PUT -H 'Content-Type: application/json' -d {_q(url_req)} "$R/v3/settings/server-url" >/dev/null
 printf '%s\\n' "$tok"
 """

@@ -35,8 +35,10 @@ from typing import Any, Dict, List, Optional
 
 from ..parallel.rccl_env import render_env_file
 
-DEFAULT_DOCKER_INSTALL_URL = "https://releases.rancher.com/install-docker/20.10.sh"
-DEFAULT_AGENT_IMAGE = "rancher/rancher-agent:v2.8.5"
+from ..versions import AGENT_IMAGE as DEFAULT_AGENT_IMAGE
+from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
+from .manager import docker_install_lines
+
 LABEL_FILE = "/etc/triton-kubernetes/gpu-labels"
 TOPOLOGY_FILE = "/etc/triton-kubernetes/gpu-topology.json"
 RCCL_ENV_FILE = "/etc/rccl/rccl.env"
@@ -161,9 +163,7 @@ if command -v firewalld >/dev/null 2>&1; then
   sudo systemctl disable firewalld.service || true
 fi"""))
     plan.steps.append(Step("runtime", "runtime", f"""
-if ! command -v docker >/dev/null 2>&1; then
-  curl -fsSL {_q(install_url)} | sudo sh
-fi
+{docker_install_lines(install_url, cfg.get("docker_install_sha256", "")).rstrip()}
 if [ ! -f /etc/docker/daemon.json ] || ! grep -q overlay2 /etc/docker/daemon.json; then
   echo '{{"storage-driver": "overlay2"}}' | sudo tee /etc/docker/daemon.json >/dev/null
   sudo systemctl restart docker || sudo service docker restart

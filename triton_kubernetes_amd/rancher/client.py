@@ -3,8 +3,10 @@
 In-process replacements for the reference's shell + curl + jq scripts:
 
 * :meth:`RancherClient.bootstrap` — ``setup_rancher.sh.tpl`` (S3): wait for the
-  server, log in as admin/admin, create the non-expiring ``triton-kubernetes``
-  API token, change the admin password, set ``server-url``;
+  server, log in as admin with the bootstrap password the server was started with
+  (``CATTLE_BOOTSTRAP_PASSWORD``; Rancher ≥2.6 has no admin/admin), create the
+  non-expiring ``triton-kubernetes`` API token, change the admin password, set
+  ``server-url``;
 * :meth:`RancherClient.ensure_cluster` — ``rancher_cluster.sh`` (S4): find or
   create the RKE cluster by name, get or create its registration token, and the
   CA checksum (sha256 of ``cacerts`` + newline, exactly what the script hashes);
@@ -23,6 +25,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 from ..cloud.http import HTTPClient, HTTPError
 from ..errors import TKError
+from ..versions import DEFAULT_K8S_VERSION, resolve_against
 
 TOKEN_NAME = "triton-kubernetes"
 
@@ -70,6 +73,7 @@ class RancherClient:
         self.url = url.rstrip("/")
         self.access_key = access_key
         self.secret_key = secret_key
+        self.last_version_note = ""  # set when resolve_k8s_version substituted a release
         self.http = HTTPClient(base_url=self.url, verify_tls=verify_tls, timeout=timeout)
         self._apply_auth()
 
@@ -100,11 +104,21 @@ class RancherClient:
             raise TKError("Rancher login returned no token")
         return token
 
-    def bootstrap(self, admin_password: str, server_url: str, initial_password: str = "admin",
+    def bootstrap(self, admin_password: str, server_url: str, initial_password: str,
                   timeout: float = 600.0) -> Dict[str, str]:
-        """Run S3 from the operator side; returns the manager module outputs."""
+        """Run S3 from the operator side; returns the manager module outputs.
+
+        ``initial_password`` is the server's bootstrap password.  A server whose
+        bootstrap already changed it (a re-run after a later step failed) accepts the
+        admin password instead; the password change is then skipped."""
         self.wait_for_server(timeout)
-        initial = self.login("admin", initial_password)
+        try:
+            initial = self.login("admin", initial_password)
+        except HTTPError as exc:
+            if exc.status != 401 or not admin_password or admin_password == initial_password:
+                raise
+            initial = self.login("admin", admin_password)
+            initial_password = admin_password
         user, _, secret = initial.partition(":")
         self.access_key, self.secret_key = user, secret
         self._apply_auth()
@@ -159,13 +173,36 @@ class RancherClient:
     def cacerts(self) -> str:
         return self.http.get_json("/v3/settings/cacerts").get("value", "") or ""
 
-    def ensure_cluster(self, name: str, k8s_version: str = "v1.9.5-rancher1-1", network_provider: str = "flannel",
+    def setting(self, name: str) -> str:
+        try:
+            return str(self.http.get_json(f"/v3/settings/{name}").get("value", "") or "")
+        except HTTPError as exc:
+            if exc.status in (403, 404):
+                return ""
+            raise
+
+    def k8s_versions(self) -> List[str]:
+        """RKE1 releases this server offers (its KDM list, setting ``k8s-versions-current``)."""
+        return [v.strip() for v in self.setting("k8s-versions-current").split(",") if v.strip()]
+
+    def resolve_k8s_version(self, requested: str) -> str:
+        """``requested`` if offered, else the server's release of the same minor; a minor
+        the server does not offer is an error here rather than a failed RKE provision."""
+        try:
+            version, note = resolve_against(requested, self.k8s_versions())
+        except ValueError as exc:
+            raise TKError(str(exc)) from None
+        self.last_version_note = note
+        return version
+
+    def ensure_cluster(self, name: str, k8s_version: str = DEFAULT_K8S_VERSION, network_provider: str = "flannel",
                        k8s_registry: str = "", k8s_registry_username: str = "",
                        k8s_registry_password: str = "") -> ClusterInfo:
         existing = self.find_cluster(name)
         if existing is not None:
             cluster_id, existed = existing.get("id", ""), True
         else:
+            k8s_version = self.resolve_k8s_version(k8s_version)
             cluster_id = self.create_cluster(name, k8s_version, network_provider, k8s_registry,
                                              k8s_registry_username, k8s_registry_password).get("id", "")
             existed = False

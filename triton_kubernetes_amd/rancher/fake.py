@@ -3,8 +3,14 @@
 Implements the v3 endpoints the framework uses plus a simulation of what the
 real server does after agents register:
 
-* S3 bootstrap endpoints (login, token, change password, settings);
-* S4 cluster endpoints (find/create cluster, registration tokens, cacerts);
+* S3 bootstrap endpoints (login, token, change password, settings).  Like
+  Rancher ≥2.6 the server starts with a *bootstrap* admin password
+  (``CATTLE_BOOTSTRAP_PASSWORD``; random when not given — there is no admin/admin)
+  and refuses new passwords shorter than ``password-min-length`` (12);
+* S4 cluster endpoints (find/create cluster, registration tokens, cacerts).  A
+  cluster whose ``kubernetesVersion`` is not in the server's KDM list (setting
+  ``k8s-versions-current``: the pinned Rancher's RKE1 releases, versions.py) is
+  rejected with 422, as the real server does;
 * ``POST /v3/connect/register`` — agent registration (``X-API-Tunnel-Token`` +
   base64 JSON ``X-API-Tunnel-Params`` with hostname, roles, labels, capacity),
   standing in for the rancher-agent websocket tunnel;
@@ -22,23 +28,31 @@ Everything is in memory and thread-safe; it serves plain HTTP on 127.0.0.1.
 import base64
 import http.server
 import json
+import secrets
 import socket
 import threading
 import time
 import urllib.parse
 import uuid
-from typing import Any, Dict, List, Optional, Set, Tuple
+from typing import Any, Dict, List, Optional, Sequence, Set, Tuple
+
+from ..versions import DEFAULT_K8S_VERSION, K8S_VERSIONS, PASSWORD_MIN_LENGTH, RANCHER_VERSION, bootstrap_password
 
 FAKE_CACERTS = "-----BEGIN CERTIFICATE-----\nMIIFAKECERTIFICATEFORTESTS\n-----END CERTIFICATE-----"
 
 
 class _State:
-    def __init__(self, rke_seconds: float, node_ready_seconds: float, admin_password: str):
+    def __init__(self, rke_seconds: float, node_ready_seconds: float, admin_password: str,
+                 k8s_versions: Sequence[str]):
         self.mu = threading.RLock()
         self.cond = threading.Condition(self.mu)
         self.admin_password = admin_password
         self.tokens: Dict[str, str] = {}  # name -> secret
-        self.settings: Dict[str, str] = {"cacerts": FAKE_CACERTS, "server-url": ""}
+        self.settings: Dict[str, str] = {"cacerts": FAKE_CACERTS, "server-url": "",
+                                         "server-version": RANCHER_VERSION,
+                                         "k8s-versions-current": ",".join(k8s_versions),
+                                         "k8s-version": DEFAULT_K8S_VERSION,
+                                         "password-min-length": str(PASSWORD_MIN_LENGTH)}
         self.clusters: Dict[str, Dict[str, Any]] = {}
         self.reg_tokens: Dict[str, Dict[str, Any]] = {}  # token -> {clusterId, id}
         self.nodes: Dict[str, Dict[str, Any]] = {}
@@ -54,12 +68,21 @@ class _State:
 
 
 class FakeRancher:
-    def __init__(self, rke_seconds: float = 0.0, node_ready_seconds: float = 0.0, admin_password: str = "admin",
-                 host: str = "127.0.0.1", port: int = 0):
-        self.state = _State(rke_seconds, node_ready_seconds, admin_password)
+    def __init__(self, rke_seconds: float = 0.0, node_ready_seconds: float = 0.0,
+                 bootstrap_password: Optional[str] = None, host: str = "127.0.0.1", port: int = 0,
+                 k8s_versions: Optional[Sequence[str]] = None):
+        # a server started without CATTLE_BOOTSTRAP_PASSWORD has a random one nobody knows
+        pw = bootstrap_password if bootstrap_password is not None else secrets.token_hex(16)
+        self.state = _State(rke_seconds, node_ready_seconds, pw,
+                            list(k8s_versions) if k8s_versions is not None else [v for _, v in K8S_VERSIONS])
         self._server = http.server.ThreadingHTTPServer((host, port), self._handler())
         self._server.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
+
+    @classmethod
+    def for_manager(cls, name: str, admin_password: str, **kw: Any) -> "FakeRancher":
+        """A server started the way this framework starts one for manager ``name``."""
+        return cls(bootstrap_password=bootstrap_password(name, admin_password), **kw)
 
     @property
     def url(self) -> str:
@@ -249,6 +272,9 @@ class FakeRancher:
         if path == "/v3/users" and query.get("action") == ["changepassword"]:
             if body.get("currentPassword") != st.admin_password:
                 return 400, {"type": "error", "message": "invalid current password"}
+            if len(body.get("newPassword", "")) < int(st.settings["password-min-length"]):
+                return 422, {"type": "error", "code": "InvalidFormat",
+                             "message": f"Password must be at least {st.settings['password-min-length']} characters"}
             st.admin_password = body.get("newPassword", "")
             return 200, {}
         if path.startswith("/v3/settings/"):
@@ -263,6 +289,11 @@ class FakeRancher:
                 data = [c for c in st.clusters.values() if not names or c["name"] in names]
             return 200, {"data": data}
         if path == "/v3/cluster" and method == "POST":
+            version = (body.get("rancherKubernetesEngineConfig") or {}).get("kubernetesVersion", "")
+            offered = [v for v in st.settings["k8s-versions-current"].split(",") if v]
+            if version not in offered:
+                return 422, {"type": "error", "code": "InvalidBodyContent", "fieldName": "kubernetesVersion",
+                             "message": f"{version} is not a supported Kubernetes version"}
             cid = f"c-{uuid.uuid4().hex[:5]}"
             with st.mu:
                 st.clusters[cid] = {"id": cid, "name": body.get("name", ""), "state": "provisioning",
@@ -356,7 +387,10 @@ class FakeRancher:
         if kpath == "/api/v1/nodes" and method == "GET":
             return 200, {"kind": "NodeList", "items": self.k8s_nodes(cid)}
         if kpath == "/version":
-            return 200, {"major": "1", "minor": "9", "gitVersion": "v1.9.5"}
+            with st.mu:
+                v = st.clusters[cid]["rancherKubernetesEngineConfig"].get("kubernetesVersion", DEFAULT_K8S_VERSION)
+            major, minor = v.lstrip("v").split(".")[:2]
+            return 200, {"major": major, "minor": minor, "gitVersion": v.split("-")[0]}
         if method == "POST":
             name = (body.get("metadata") or {}).get("name", uuid.uuid4().hex[:6])
             key = f"{cid}|{kpath}|{name}"

@@ -84,9 +84,68 @@ CATALOG: Dict[str, ModuleInfo] = {m.name: m for m in _MODULES}
 REFERENCE_MODULES = [m.name for m in _MODULES if not m.mi355x]
 
 
+# The package directory: ``<PACKAGE_ROOT>/terraform/modules/<name>`` is this project's
+# module tree.  It is the default ``source_url`` (models/common.py), so documents point
+# at the modules that ship with this CLI instead of the reference's Terraform 0.11 ones.
+PACKAGE_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def is_local_source(source_url: str) -> bool:
+    """A filesystem location (Terraform copies absolute paths into its module cache)."""
+    return source_url.startswith(("/", "./", "../", "~"))
+
+
+def packaged_root() -> str:
+    """A real directory holding ``terraform/modules``: the package itself, or — when
+    running from a zipapp, whose files are not on disk — a per-version extraction under
+    ``~/.cache/triton-kubernetes``."""
+    if os.path.isdir(MODULES_DIR):
+        return PACKAGE_ROOT
+    import zipfile
+
+    from .. import __version__
+
+    archive = PACKAGE_ROOT
+    while archive and not os.path.isfile(archive):
+        archive = os.path.dirname(archive)
+    if not archive or not zipfile.is_zipfile(archive):
+        raise FileNotFoundError(f"terraform modules not found at {MODULES_DIR}")
+    inner = os.path.relpath(MODULES_DIR, archive).replace(os.sep, "/") + "/"
+    cache = os.path.join(os.path.expanduser("~"), ".cache", "triton-kubernetes", f"modules-{__version__}")
+    root = os.path.join(cache, "pkg")
+    if not os.path.isdir(os.path.join(root, "terraform", "modules")):
+        tmp = f"{cache}.tmp-{os.getpid()}"
+        with zipfile.ZipFile(archive) as zf:
+            for member in zf.namelist():
+                if member.startswith(inner) and not member.endswith("/"):
+                    rel = member[len(inner):]
+                    dest = os.path.join(tmp, "pkg", "terraform", "modules", *rel.split("/"))
+                    os.makedirs(os.path.dirname(dest), exist_ok=True)
+                    with zf.open(member) as src, open(dest, "wb") as out:
+                        out.write(src.read())
+        os.makedirs(os.path.dirname(cache), exist_ok=True)
+        try:
+            os.rename(tmp, cache)
+        except OSError:  # another process extracted it first
+            import shutil
+
+            shutil.rmtree(tmp, ignore_errors=True)
+    return root
+
+
 def module_source(source_url: str, module_path: str, source_ref: str) -> str:
-    """``<url>//<path>?ref=<ref>`` (``create/manager.go:160-171``)."""
+    """``<url>//<path>?ref=<ref>`` for a remote (git/registry) prefix
+    (``create/manager.go:160-171``); ``<dir>/<path>`` for a local directory, which
+    Terraform reads directly (no ``//`` subdir or ``?ref=`` on filesystem sources)."""
+    if is_local_source(source_url):
+        return os.path.join(os.path.abspath(os.path.expanduser(source_url)), module_path)
     return f"{source_url}//{module_path}?ref={source_ref}"
+
+
+def local_module_dir(source: str) -> Optional[str]:
+    """The directory a local ``source`` points at (None for remote sources)."""
+    path = source.split("?", 1)[0]
+    return path if is_local_source(path) else None
 
 
 def module_from_source(source: str) -> Optional[ModuleInfo]:

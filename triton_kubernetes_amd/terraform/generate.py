@@ -29,14 +29,15 @@ from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from ..k8s.manifests import device_plugin_daemonset, labeller_daemonset, rccl_configmap, NAMESPACE
+from .. import versions
 from . import scripts
 from .catalog import MODULES_DIR
 
 CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "ops", "csrc")
 
-DOCKER_URL = "https://releases.rancher.com/install-docker/24.0.sh"
-SERVER_IMAGE = "rancher/rancher:v2.8.5"
-AGENT_IMAGE = "rancher/rancher-agent:v2.8.5"
+DOCKER_URL = versions.DOCKER_INSTALL_URL
+SERVER_IMAGE = versions.SERVER_IMAGE
+AGENT_IMAGE = versions.AGENT_IMAGE
 
 PROVIDERS = {
     "triton": ('triton = {\n      source  = "joyent/triton"\n      version = ">= 0.8"\n    }',
@@ -126,8 +127,24 @@ VAR_DOCS = {
     "gpu_count": "GPUs the MI355X node must expose.",
     "gpu_burnin": "Burn-in level run on every GPU before the node joins.",
     "rccl_env": "Extra RCCL/HSA environment written to /etc/rccl/rccl.env.",
+    "docker_install_sha256": "SHA-256 the downloaded runtime install script must match (empty: not checked).",
+    "rancher_bootstrap_password": ("First-login password of the Rancher server (CATTLE_BOOTSTRAP_PASSWORD); "
+                                   "empty: derived from name and rancher_admin_password."),
 }
+# values spliced into single-quoted shell words and JSON bodies by the bootstrap scripts
+# (HCL string "['\"\\\\]" is the RE2 class ['"\\]: single quote, double quote, backslash)
+_SHELL_SAFE = (r'length(regexall("[' + "'" + r'\"\\\\]", var.{0})) == 0', "{0} must not contain quotes or backslashes.")
 VAR_VALIDATIONS = {
+    "rancher_admin_password": (f'length(var.rancher_admin_password) >= {versions.PASSWORD_MIN_LENGTH} && '
+                               + _SHELL_SAFE[0].format("rancher_admin_password"),
+                               f"rancher_admin_password must be at least {versions.PASSWORD_MIN_LENGTH} characters "
+                               "(Rancher >= 2.6) without quotes or backslashes."),
+    "rancher_bootstrap_password": (_SHELL_SAFE[0].format("rancher_bootstrap_password"),
+                                   _SHELL_SAFE[1].format("rancher_bootstrap_password")),
+    "k8s_version": ("contains([" + ", ".join(f'"{m}"' for m in versions.K8S_MINORS) + "], "
+                    'join(".", slice(split(".", var.k8s_version), 0, 2)))',
+                    f"k8s_version must be an RKE1 release of Rancher {versions.RANCHER_VERSION} "
+                    f"({', '.join(v for _, v in versions.K8S_VERSIONS)})."),
     "k8s_network_provider": ('contains(["calico", "flannel", "canal", "weave"], var.k8s_network_provider)',
                              "k8s_network_provider must be one of calico, flannel, canal, weave."),
     "gpu_burnin": ('contains(["quick", "full", "off"], var.gpu_burnin)', "gpu_burnin must be quick, full or off."),
@@ -171,7 +188,8 @@ def hcl_value(v: Any, indent: int = 0) -> str:
 
 # --- variable sets ---------------------------------------------------------------------------
 def _rancher_image_vars(server: bool = True) -> List[Var]:
-    out = [Var("docker_engine_install_url", DOCKER_URL, "The URL to the shell script to install the docker engine.")]
+    out = [Var("docker_engine_install_url", DOCKER_URL, "The URL to the shell script to install the docker engine."),
+           Var("docker_install_sha256", "")]
     if server:
         out.append(Var("rancher_server_image", SERVER_IMAGE, "The Rancher Server image to use."))
     out.append(Var("rancher_agent_image", AGENT_IMAGE, "The Rancher Agent image to use."))
@@ -182,11 +200,12 @@ def _rancher_image_vars(server: bool = True) -> List[Var]:
 
 
 MANAGER_BASE = [Var("name", None, "Human readable name used as prefix to generated names."),
-                Var("rancher_admin_password", None, "The Rancher admin password", sensitive=True)]
+                Var("rancher_admin_password", None, "The Rancher admin password", sensitive=True),
+                Var("rancher_bootstrap_password", "", sensitive=True)]
 CLUSTER_BASE = [
     Var("name", None, "Human readable name used as prefix to generated names."),
     Var("rancher_api_url", None), Var("rancher_access_key", None), Var("rancher_secret_key", None, sensitive=True),
-    Var("k8s_version", "v1.9.5-rancher1-1"), Var("k8s_network_provider", "flannel"),
+    Var("k8s_version", versions.DEFAULT_K8S_VERSION), Var("k8s_network_provider", "flannel"),
     Var("rancher_registry", ""), Var("rancher_registry_username", ""), Var("rancher_registry_password", "", sensitive=True),
     Var("k8s_registry", ""), Var("k8s_registry_username", ""), Var("k8s_registry_password", "", sensitive=True),
 ]
@@ -248,6 +267,7 @@ resource "terraform_data" "install_docker" {{
   provisioner "remote-exec" {{
     inline = [templatefile("${{path.module}}/files/install_docker.sh.tftpl", {{
       docker_engine_install_url = var.docker_engine_install_url
+      docker_install_sha256     = var.docker_install_sha256
       rancher_server_image      = var.rancher_server_image
       rancher_registry          = var.rancher_registry
       rancher_registry_username = var.rancher_registry_username
@@ -258,12 +278,20 @@ resource "terraform_data" "install_docker" {{
 '''
         after = "\n  depends_on       = [terraform_data.install_docker]"
     return docker + f'''
+locals {{
+  # Rancher >= 2.6 first login (CATTLE_BOOTSTRAP_PASSWORD); the same derivation as
+  # triton_kubernetes_amd.versions.bootstrap_password, so every delivery path agrees
+  bootstrap_password = (var.rancher_bootstrap_password != "" ? var.rancher_bootstrap_password :
+    substr(sha256("tk-bootstrap:${{var.name}}:${{var.rancher_admin_password}}"), 0, 32))
+}}
+
 resource "terraform_data" "install_rancher_master" {{
   triggers_replace = [local.rancher_master_id]{after}
 {connection}
   provisioner "remote-exec" {{
     inline = [templatefile("${{path.module}}/files/install_rancher_server.sh.tftpl", {{
       rancher_server_image = var.rancher_server_image
+      bootstrap_password   = local.bootstrap_password
     }})]
   }}
 }}
@@ -277,6 +305,7 @@ resource "terraform_data" "setup_rancher_k8s" {{
       rancher_host           = "https://127.0.0.1"
       host_registration_url  = "https://${{local.rancher_master_ip}}"
       rancher_admin_password = var.rancher_admin_password
+      bootstrap_password     = local.bootstrap_password
     }})]
   }}
 }}
@@ -309,6 +338,7 @@ def _docker_userdata(server: bool) -> str:
     image = "var.rancher_server_image" if server else '""'
     return f'''templatefile("${{path.module}}/files/install_docker.sh.tftpl", {{
     docker_engine_install_url = var.docker_engine_install_url
+    docker_install_sha256     = var.docker_install_sha256
     rancher_server_image      = {image}
     rancher_registry          = var.rancher_registry
     rancher_registry_username = var.rancher_registry_username
@@ -320,6 +350,7 @@ def _agent_userdata(disk_device: str = '""', disk_mount: str = '""', extra: str 
     return f'''templatefile("${{path.module}}/files/install_rancher_agent.sh.tftpl", {{
     hostname                           = var.hostname
     docker_engine_install_url          = var.docker_engine_install_url
+    docker_install_sha256              = var.docker_install_sha256
     rancher_api_url                    = var.rancher_api_url
     rancher_cluster_registration_token = var.rancher_cluster_registration_token
     rancher_cluster_ca_checksum        = var.rancher_cluster_ca_checksum
@@ -1175,6 +1206,7 @@ resource "terraform_data" "install_mi355x_node" {{
     inline = [templatefile("${{path.module}}/files/install_mi355x_node.sh.tftpl", {{
       hostname                           = var.hostname
       docker_engine_install_url          = var.docker_engine_install_url
+      docker_install_sha256              = var.docker_install_sha256
       rancher_api_url                    = var.rancher_api_url
       rancher_cluster_registration_token = var.rancher_cluster_registration_token
       rancher_cluster_ca_checksum        = var.rancher_cluster_ca_checksum
@@ -1224,8 +1256,8 @@ data "external" "gpu_labels" {{
     mods.append(Module("rancher-k8s-mi355x-addons", ["external"], [
         Var("name", None), Var("rancher_api_url", None), Var("rancher_access_key", None),
         Var("rancher_secret_key", None, sensitive=True), Var("rancher_cluster_id", None),
-        Var("device_plugin_image", "rocm/k8s-device-plugin:latest"),
-        Var("node_labeller_image", "rocm/k8s-device-plugin:labeller-latest"),
+        Var("device_plugin_image", versions.DEVICE_PLUGIN_IMAGE),
+        Var("node_labeller_image", versions.NODE_LABELLER_IMAGE),
         Var("rccl_probe_image", ""), Var("rccl_gate", "true")],
         '''locals {
   manifest_dir = "${path.root}/.tk-addons-${var.name}"

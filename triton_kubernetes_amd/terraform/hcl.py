@@ -1,0 +1,760 @@
+"""HCL2 native-syntax parser and a static checker for this project's Terraform modules.
+
+There is no ``terraform`` binary in CI, so the generated modules need a parser of
+their own to be checked at all.  This is a scannerless recursive-descent parser of
+the HCL2 native syntax Terraform ≥0.12 reads:
+
+* bodies of attributes (``name = expr``) and blocks (``type "label" ident { … }``);
+* expressions: literals, template strings with ``${…}`` interpolations and
+  ``%{if}/%{else}/%{endif}`` / ``%{for}/%{endfor}`` directives (strip markers ``~``),
+  heredocs (``<<EOT`` / ``<<-EOT``), tuples, objects, function calls (``f(a, b...)``),
+  traversals (``a.b[0].c``, ``.*``, ``[*]``), unary/binary operators with HCL's
+  precedence, conditionals and ``for`` expressions in both brackets;
+* newlines terminate attributes in bodies and separate object items, and are
+  insignificant inside ``()`` and ``[]``, as in the HCL spec.
+
+:func:`check_module` then does what ``terraform validate`` would catch first for
+these modules: every ``var.X`` declared, every ``local.X`` defined, every
+``data.T.N`` / ``T.N`` resource reference defined, and every
+``templatefile(path, {…})`` call passing exactly the names its template uses
+(Terraform fails on a missing one at apply time).  :func:`parse_template` checks
+``.tftpl`` files on their own (balanced directives, valid interpolation syntax).
+
+The reference ships Terraform 0.11 modules and has no checker; this is new
+("no terraform in the dev sandbox").
+"""
+
+import os
+import re
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional, Set, Tuple
+
+
+class HCLSyntaxError(ValueError):
+    def __init__(self, msg: str, src: str, pos: int, name: str = "<hcl>"):
+        line = src.count("\n", 0, pos) + 1
+        col = pos - (src.rfind("\n", 0, pos) + 1) + 1
+        super().__init__(f"{name}:{line}:{col}: {msg}")
+        self.line, self.col = line, col
+
+
+# --- AST ---------------------------------------------------------------------------------------
+@dataclass
+class Node:
+    kind: str  # lit | tmpl | trav | call | tuple | object | op | unary | cond | for | paren
+    value: Any = None
+    children: List["Node"] = field(default_factory=list)
+    pos: int = 0
+
+
+@dataclass
+class Attribute:
+    name: str
+    expr: Node
+    pos: int
+
+
+@dataclass
+class Block:
+    type: str
+    labels: List[str]
+    body: "Body"
+    pos: int
+
+
+@dataclass
+class Body:
+    attributes: List[Attribute] = field(default_factory=list)
+    blocks: List[Block] = field(default_factory=list)
+
+    def attr(self, name: str) -> Optional[Attribute]:
+        return next((a for a in self.attributes if a.name == name), None)
+
+    def blocks_of(self, kind: str) -> List[Block]:
+        return [b for b in self.blocks if b.type == kind]
+
+
+_IDENT_RE = re.compile(r"[A-Za-z_][A-Za-z0-9_-]*")
+_NUM_RE = re.compile(r"[0-9]+(\.[0-9]+)?([eE][+-]?[0-9]+)?")
+_BINARY = [("||",), ("&&",), ("==", "!="), ("<=", ">=", "<", ">"), ("+", "-"), ("*", "/", "%")]
+_KEYWORD_LITS = {"true": True, "false": False, "null": None}
+
+
+class _Parser:
+    def __init__(self, src: str, name: str):
+        self.s = src
+        self.n = len(src)
+        self.i = 0
+        self.name = name
+
+    # --- low level -------------------------------------------------------------------------------
+    def err(self, msg: str, pos: Optional[int] = None) -> HCLSyntaxError:
+        return HCLSyntaxError(msg, self.s, self.i if pos is None else pos, self.name)
+
+    def skip(self, newlines: bool) -> None:
+        """Skip blanks and comments (and newlines when ``newlines``)."""
+        s, n = self.s, self.n
+        while self.i < n:
+            c = s[self.i]
+            if c in " \t\r":
+                self.i += 1
+            elif c == "\n" and newlines:
+                self.i += 1
+            elif c == "#" or s.startswith("//", self.i):
+                j = s.find("\n", self.i)
+                self.i = n if j < 0 else j
+            elif s.startswith("/*", self.i):
+                j = s.find("*/", self.i + 2)
+                if j < 0:
+                    raise self.err("unterminated /* comment")
+                self.i = j + 2
+            else:
+                break
+
+    def peek(self, tok: str) -> bool:
+        return self.s.startswith(tok, self.i)
+
+    def eat(self, tok: str, newlines: bool) -> bool:
+        self.skip(newlines)
+        if self.s.startswith(tok, self.i):
+            self.i += len(tok)
+            return True
+        return False
+
+    def expect(self, tok: str, newlines: bool, what: str = "") -> None:
+        if not self.eat(tok, newlines):
+            found = self.s[self.i:self.i + 12].split("\n")[0] or "end of input"
+            raise self.err(f"expected {tok!r}{' ' + what if what else ''}, found {found!r}")
+
+    def ident(self, newlines: bool) -> Optional[str]:
+        self.skip(newlines)
+        m = _IDENT_RE.match(self.s, self.i)
+        if not m:
+            return None
+        self.i = m.end()
+        return m.group(0)
+
+    # --- bodies ------------------------------------------------------------------------------------
+    def body(self, closing: Optional[str]) -> Body:
+        out = Body()
+        while True:
+            self.skip(True)
+            if self.i >= self.n:
+                if closing:
+                    raise self.err(f"expected {closing!r} before end of input")
+                return out
+            if closing and self.peek(closing):
+                self.i += 1
+                return out
+            start = self.i
+            name = self.ident(False)
+            if name is None:
+                raise self.err("expected an attribute name or block type")
+            self.skip(False)
+            if self.peek("=") and not self.peek("=="):
+                self.i += 1
+                expr = self.expr(False)
+                out.attributes.append(Attribute(name, expr, start))
+                self.end_of_line()
+                continue
+            labels: List[str] = []
+            while True:
+                self.skip(False)
+                if self.peek('"'):
+                    lab = self.string()
+                    if lab.kind != "lit":
+                        raise self.err("block labels must be literal strings", lab.pos)
+                    labels.append(lab.value)
+                    continue
+                lab_ident = self.ident(False)
+                if lab_ident is not None:
+                    labels.append(lab_ident)
+                    continue
+                break
+            self.expect("{", False, f"to open block {name!r}")
+            blk = self.body("}")
+            out.blocks.append(Block(name, labels, blk, start))
+            self.end_of_line()
+
+    def end_of_line(self) -> None:
+        self.skip(False)
+        if self.i >= self.n or self.s[self.i] in "\n}":
+            if self.i < self.n and self.s[self.i] == "\n":
+                self.i += 1
+            return
+        raise self.err(f"unexpected {self.s[self.i:self.i + 12].split(chr(10))[0]!r} after a definition")
+
+    # --- expressions ------------------------------------------------------------------------------
+    def expr(self, nl: bool) -> Node:
+        cond = self.binary(0, nl)
+        self.skip(nl)
+        if self.peek("?"):
+            self.i += 1
+            a = self.expr(nl)
+            self.expect(":", nl, "in conditional")
+            b = self.expr(nl)
+            return Node("cond", None, [cond, a, b], cond.pos)
+        return cond
+
+    def binary(self, level: int, nl: bool) -> Node:
+        if level == len(_BINARY):
+            return self.unary(nl)
+        left = self.binary(level + 1, nl)
+        while True:
+            self.skip(nl)
+            op = next((o for o in _BINARY[level] if self.peek(o)), None)
+            # "=>" / "==" are not "=", "<" is not "<<" (heredoc) or "<=" handled above
+            if op is None or (op in ("<", ">") and self.peek(op + "=")) or (op == "/" and self.peek("//")) \
+                    or (op == "*" and self.peek("*/")):
+                return left
+            self.i += len(op)
+            right = self.binary(level + 1, nl)
+            left = Node("op", op, [left, right], left.pos)
+
+    def unary(self, nl: bool) -> Node:
+        self.skip(nl)
+        if self.peek("!") and not self.peek("!="):
+            pos = self.i
+            self.i += 1
+            return Node("unary", "!", [self.unary(nl)], pos)
+        if self.peek("-"):
+            pos = self.i
+            self.i += 1
+            return Node("unary", "-", [self.unary(nl)], pos)
+        return self.postfix(self.primary(nl), nl)
+
+    def postfix(self, node: Node, nl: bool) -> Node:
+        while True:
+            # traversal operators bind tightly: no newline may precede them
+            if self.peek(".*"):
+                self.i += 2
+                node = Node("trav", node.value if node.kind == "trav" else None, node.children + [Node("splat")]
+                            if node.kind == "trav" else [node, Node("splat")], node.pos)
+                continue
+            if self.peek(".") and not self.peek("..."):
+                self.i += 1
+                m = _NUM_RE.match(self.s, self.i)
+                name = None
+                if m:
+                    self.i = m.end()
+                    name = m.group(0)
+                else:
+                    name = self.ident(False)
+                if name is None:
+                    raise self.err("expected an attribute name after '.'")
+                node = self._extend(node, Node("attr", name, pos=self.i))
+                continue
+            if self.peek("["):
+                self.i += 1
+                self.skip(True)
+                if self.peek("*"):
+                    self.i += 1
+                    self.expect("]", True, "after '[*'")
+                    node = self._extend(node, Node("splat"))
+                    continue
+                key = self.expr(True)
+                self.expect("]", True, "to close an index")
+                node = self._extend(node, Node("index", None, [key]))
+                continue
+            return node
+
+    @staticmethod
+    def _extend(node: Node, step: Node) -> Node:
+        if node.kind == "trav":
+            return Node("trav", node.value, node.children + [step], node.pos)
+        return Node("trav", None, [node, step], node.pos)  # traversal of an expression result
+
+    def primary(self, nl: bool) -> Node:
+        self.skip(nl)
+        pos = self.i
+        if self.i >= self.n:
+            raise self.err("expected an expression before end of input")
+        c = self.s[self.i]
+        if c == '"':
+            return self.string()
+        if self.peek("<<"):
+            return self.heredoc()
+        if c.isdigit():
+            m = _NUM_RE.match(self.s, self.i)
+            self.i = m.end()
+            return Node("lit", float(m.group(0)) if ("." in m.group(0) or "e" in m.group(0).lower())
+                        else int(m.group(0)), pos=pos)
+        if c == "(":
+            self.i += 1
+            inner = self.expr(True)
+            self.expect(")", True, "to close '('")
+            return Node("paren", None, [inner], pos)
+        if c == "[":
+            self.i += 1
+            return self.tuple_or_for(pos)
+        if c == "{":
+            self.i += 1
+            return self.object_or_for(pos)
+        name = self.ident(False)
+        if name is None:
+            raise self.err(f"unexpected {self.s[self.i:self.i + 12].split(chr(10))[0]!r} in expression")
+        if name in _KEYWORD_LITS:
+            return Node("lit", _KEYWORD_LITS[name], pos=pos)
+        if self.peek("("):  # function call (no space allowed before '(' in practice; tolerate it)
+            self.i += 1
+            args: List[Node] = []
+            expand = False
+            while True:
+                self.skip(True)
+                if self.peek(")"):
+                    self.i += 1
+                    break
+                args.append(self.expr(True))
+                self.skip(True)
+                if self.peek("..."):
+                    self.i += 3
+                    expand = True
+                    self.expect(")", True, "after '...' argument expansion")
+                    break
+                if self.eat(",", True):
+                    continue
+                self.expect(")", True, f"to close the call to {name}()")
+                break
+            return Node("call", name, args, pos)
+        return Node("trav", name, [], pos)
+
+    def tuple_or_for(self, pos: int) -> Node:
+        self.skip(True)
+        if self._for_keyword():
+            names, coll = self.for_intro()
+            value = self.expr(True)
+            cond = self._for_if()
+            self.expect("]", True, "to close the for expression")
+            return Node("for", {"names": names, "object": False},
+                        [coll, value] + ([cond] if cond else []), pos)
+        items: List[Node] = []
+        while True:
+            self.skip(True)
+            if self.peek("]"):
+                self.i += 1
+                return Node("tuple", None, items, pos)
+            items.append(self.expr(True))
+            self.skip(True)
+            if self.eat(",", True):
+                continue
+            self.expect("]", True, "to close the tuple")
+            return Node("tuple", None, items, pos)
+
+    def object_or_for(self, pos: int) -> Node:
+        self.skip(True)
+        if self._for_keyword():
+            names, coll = self.for_intro()
+            key = self.expr(True)
+            self.expect("=>", True, "in object for expression")
+            value = self.expr(True)
+            self.skip(True)
+            group = self.eat("...", True)
+            cond = self._for_if()
+            self.expect("}", True, "to close the for expression")
+            return Node("for", {"names": names, "object": True, "group": group},
+                        [coll, key, value] + ([cond] if cond else []), pos)
+        items: List[Node] = []
+        while True:
+            self.skip(True)
+            if self.peek("}"):
+                self.i += 1
+                return Node("object", None, items, pos)
+            kpos = self.i
+            key = self.expr(False)
+            self.skip(False)
+            if self.peek("=") and not self.peek("==") and not self.peek("=>"):
+                self.i += 1
+            elif self.peek(":"):
+                self.i += 1
+            else:
+                raise self.err("expected '=' or ':' after an object key")
+            value = self.expr(False)
+            items.append(Node("item", None, [key, value], kpos))
+            self.skip(False)
+            if self.peek(","):
+                self.i += 1
+            elif self.peek("\n"):
+                self.i += 1
+            elif not self.peek("}"):
+                raise self.err("expected ',', a newline or '}' after an object item")
+
+    def _for_keyword(self) -> bool:
+        m = _IDENT_RE.match(self.s, self.i)
+        return bool(m and m.group(0) == "for" and self.s[m.end():m.end() + 1] in (" ", "\t", "\n"))
+
+    def for_intro(self) -> Tuple[List[str], Node]:
+        self.i += 3
+        names = [self.ident(True)]
+        if names[0] is None:
+            raise self.err("expected a variable name after 'for'")
+        if self.eat(",", True):
+            second = self.ident(True)
+            if second is None:
+                raise self.err("expected a second variable name after ','")
+            names.append(second)
+        if self.ident(True) != "in":
+            raise self.err("expected 'in' in for expression")
+        coll = self.expr(True)
+        self.expect(":", True, "after the for collection")
+        return names, coll
+
+    def _for_if(self) -> Optional[Node]:
+        self.skip(True)
+        m = _IDENT_RE.match(self.s, self.i)
+        if m and m.group(0) == "if":
+            self.i = m.end()
+            return self.expr(True)
+        return None
+
+    # --- templates ----------------------------------------------------------------------------------
+    def string(self) -> Node:
+        pos = self.i
+        self.i += 1  # opening quote
+        parts = self.template_parts(end='"', quoted=True)
+        return self._template_node(parts, pos)
+
+    def heredoc(self) -> Node:
+        pos = self.i
+        m = re.compile(r"<<(-?)([A-Za-z_][A-Za-z0-9_-]*)[ \t]*\n").match(self.s, self.i)
+        if not m:
+            raise self.err("malformed heredoc introducer")
+        marker = m.group(2)
+        end = re.compile(r"^[ \t]*" + re.escape(marker) + r"[ \t]*$", re.M).search(self.s, m.end())
+        if not end:
+            raise self.err(f"heredoc {marker!r} is never closed", pos)
+        sub = _Parser(self.s[:end.start()], self.name)
+        sub.i = m.end()
+        parts = sub.template_parts(end=None, quoted=False)
+        self.i = end.end()
+        return self._template_node(parts, pos)
+
+    @staticmethod
+    def _template_node(parts: List[Node], pos: int) -> Node:
+        if all(p.kind == "lit" for p in parts):
+            return Node("lit", "".join(p.value for p in parts), pos=pos)
+        return Node("tmpl", None, parts, pos)
+
+    def template_parts(self, end: Optional[str], quoted: bool) -> List[Node]:
+        """Literal text, ``${expr}`` and ``%{directive}`` up to ``end`` (None: end of input).
+        Directives are checked for nesting here (if/else/endif, for/endfor)."""
+        parts: List[Node] = []
+        buf: List[str] = []
+        stack: List[Tuple[str, int]] = []
+        s = self.s
+        while True:
+            if self.i >= self.n:
+                if end is not None:
+                    raise self.err("unterminated string")
+                break
+            c = s[self.i]
+            if end is not None and c == end:
+                self.i += 1
+                break
+            if quoted and c == "\n":
+                raise self.err("newline in a quoted string (use a heredoc)")
+            if quoted and c == "\\":
+                esc = s[self.i + 1:self.i + 2]
+                if esc in ('"', "\\", "n", "r", "t"):
+                    buf.append({"n": "\n", "r": "\r", "t": "\t"}.get(esc, esc))
+                    self.i += 2
+                    continue
+                if esc == "u":
+                    buf.append(chr(int(s[self.i + 2:self.i + 6], 16)))
+                    self.i += 6
+                    continue
+                raise self.err(f"invalid escape \\{esc}")
+            if s.startswith("$${", self.i) or s.startswith("%%{", self.i):
+                buf.append(s[self.i + 1:self.i + 3])
+                self.i += 3
+                continue
+            if s.startswith("${", self.i) or s.startswith("%{", self.i):
+                if buf:
+                    parts.append(Node("lit", "".join(buf)))
+                    buf = []
+                directive = s[self.i] == "%"
+                start = self.i
+                self.i += 2
+                if self.peek("~"):
+                    self.i += 1
+                if directive:
+                    parts.append(self._directive(stack, start))
+                else:
+                    e = self.expr(True)
+                    self.skip(True)
+                    if self.peek("~"):
+                        self.i += 1
+                    self.expect("}", True, "to close '${'")
+                    parts.append(Node("interp", None, [e], start))
+                continue
+            buf.append(c)
+            self.i += 1
+        if stack:
+            raise self.err(f"%{{{stack[-1][0]}}} is never closed", stack[-1][1])
+        if buf:
+            parts.append(Node("lit", "".join(buf)))
+        return parts
+
+    def _directive(self, stack: List[Tuple[str, int]], start: int) -> Node:
+        word = self.ident(True)
+        node: Node
+        if word == "if":
+            node = Node("if", None, [self.expr(True)], start)
+            stack.append(("if", start))
+        elif word == "else":
+            if not stack or stack[-1][0] != "if":
+                raise self.err("%{else} without %{if}", start)
+            node = Node("else", pos=start)
+        elif word == "endif":
+            if not stack or stack[-1][0] != "if":
+                raise self.err("%{endif} without %{if}", start)
+            stack.pop()
+            node = Node("endif", pos=start)
+        elif word == "for":
+            names = [self.ident(True)]
+            if self.eat(",", True):
+                names.append(self.ident(True))
+            if None in names or self.ident(True) != "in":
+                raise self.err("malformed %{for}", start)
+            node = Node("tfor", names, [self.expr(True)], start)
+            stack.append(("for", start))
+        elif word == "endfor":
+            if not stack or stack[-1][0] != "for":
+                raise self.err("%{endfor} without %{for}", start)
+            stack.pop()
+            node = Node("endfor", pos=start)
+        else:
+            raise self.err(f"unknown template directive %{{{word}}}", start)
+        self.skip(True)
+        if self.peek("~"):
+            self.i += 1
+        self.expect("}", True, "to close the directive")
+        return node
+
+
+def parse(src: str, name: str = "<hcl>") -> Body:
+    """Parse a ``.tf`` file (HCL2 native syntax); raises :class:`HCLSyntaxError`."""
+    p = _Parser(src, name)
+    return p.body(None)
+
+
+def parse_template(src: str, name: str = "<template>") -> List[Node]:
+    """Parse a ``templatefile`` template; raises :class:`HCLSyntaxError`."""
+    p = _Parser(src, name)
+    return p.template_parts(end=None, quoted=False)
+
+
+# --- analysis -----------------------------------------------------------------------------------------
+def walk(node: Any):
+    """Every Node under ``node`` (itself included), depth first."""
+    if isinstance(node, Node):
+        yield node
+        for ch in node.children:
+            yield from walk(ch)
+    elif isinstance(node, Body):
+        for a in node.attributes:
+            yield from walk(a.expr)
+        for b in node.blocks:
+            yield from walk(b.body)
+    elif isinstance(node, list):
+        for x in node:
+            yield from walk(x)
+
+
+def references(node: Any, bound: Optional[Set[str]] = None) -> List[Tuple[str, List[str], int]]:
+    """Traversals ``(root, [attr names...], pos)`` under ``node`` whose root is not bound
+    by an enclosing ``for`` (expression or template directive)."""
+    bound = set(bound or ())
+    out: List[Tuple[str, List[str], int]] = []
+
+    def visit(n: Any, b: Set[str]) -> None:
+        if isinstance(n, Body):
+            for a in n.attributes:
+                visit(a.expr, b)
+            for blk in n.blocks:
+                if blk.type == "variable":  # `type = list(string)` is a type constraint, not references
+                    for a in blk.body.attributes:
+                        if a.name != "type":
+                            visit(a.expr, b)
+                    visit(Body(blocks=blk.body.blocks), b)
+                elif blk.type == "dynamic" and blk.labels:  # binds its label (or iterator) in content
+                    it = blk.body.attr("iterator")
+                    name = it.expr.value if it is not None and it.expr.kind == "trav" else blk.labels[0]
+                    visit(blk.body, b | {name})
+                else:
+                    visit(blk.body, b)
+            return
+        if isinstance(n, list):
+            inner = set(b)
+            for x in n:  # template part lists: %{for} binds until %{endfor}
+                if isinstance(x, Node) and x.kind == "tfor":
+                    visit(x.children[0], inner)
+                    inner = inner | set(x.value)
+                else:
+                    visit(x, inner)
+            return
+        if not isinstance(n, Node):
+            return
+        if n.kind == "trav" and n.value is not None:
+            if n.value not in b:
+                out.append((n.value, [c.value for c in n.children if c.kind == "attr"], n.pos))
+            for c in n.children:
+                if c.kind == "index":
+                    visit(c.children[0], b)
+            return
+        if n.kind == "for":
+            visit(n.children[0], b)
+            inner = b | set(n.value["names"])
+            for c in n.children[1:]:
+                visit(c, inner)
+            return
+        if n.kind == "tmpl":
+            visit(n.children, b)
+            return
+        if n.kind == "item":  # object item: a bare-identifier key is a name, not a reference
+            key = n.children[0]
+            if not (key.kind == "trav" and key.value is not None and not key.children):
+                visit(key, b)
+            visit(n.children[1], b)
+            return
+        for c in n.children:
+            visit(c, b)
+
+    visit(node, bound)
+    return out
+
+
+def template_names(parts: List[Node]) -> Set[str]:
+    """Root names a template reads (its ``templatefile`` vars)."""
+    return {root for root, _, _ in references(parts)}
+
+
+def object_keys(node: Node) -> Optional[Set[str]]:
+    """Literal keys of an object constructor (None if it is not one)."""
+    if node.kind != "object":
+        return None
+    keys = set()
+    for item in node.children:
+        k = item.children[0]
+        if k.kind == "trav" and not k.children:
+            keys.add(k.value)
+        elif k.kind == "lit" and isinstance(k.value, str):
+            keys.add(k.value)
+        else:
+            return None
+    return keys
+
+
+_BUILTIN_ROOTS = {"path", "count", "each", "self", "terraform"}
+
+
+@dataclass
+class ModuleReport:
+    name: str
+    files: Dict[str, Body]
+    errors: List[str]
+    variables: Set[str]
+    required: Set[str]
+    outputs: Set[str]
+
+
+def check_module(module_dir: str) -> ModuleReport:
+    """Parse every ``.tf`` of a module and cross-check references and templatefile calls."""
+    name = os.path.basename(module_dir.rstrip("/"))
+    files: Dict[str, Body] = {}
+    errors: List[str] = []
+    for fn in sorted(os.listdir(module_dir)):
+        if fn.endswith(".tf"):
+            path = os.path.join(module_dir, fn)
+            with open(path, encoding="utf-8") as fh:
+                src = fh.read()
+            try:
+                files[fn] = parse(src, f"{name}/{fn}")
+            except HCLSyntaxError as exc:
+                errors.append(str(exc))
+    variables: Set[str] = set()
+    required: Set[str] = set()
+    locals_: Set[str] = set()
+    resources: Set[Tuple[str, str]] = set()
+    datas: Set[Tuple[str, str]] = set()
+    modules: Set[str] = set()
+    outputs: Set[str] = set()
+    for fn, body in files.items():
+        for b in body.blocks:
+            if b.type == "variable" and b.labels:
+                variables.add(b.labels[0])
+                if b.body.attr("default") is None:
+                    required.add(b.labels[0])
+            elif b.type == "locals":
+                locals_ |= {a.name for a in b.body.attributes}
+            elif b.type == "resource" and len(b.labels) == 2:
+                resources.add((b.labels[0], b.labels[1]))
+            elif b.type == "data" and len(b.labels) == 2:
+                datas.add((b.labels[0], b.labels[1]))
+            elif b.type == "module" and b.labels:
+                modules.add(b.labels[0])
+            elif b.type == "output" and b.labels:
+                outputs.add(b.labels[0])
+    resource_types = {t for t, _ in resources}
+    for fn, body in files.items():
+        for root, attrs, pos in references(body):
+            where = f"{name}/{fn}"
+            if root == "var":
+                if attrs and attrs[0] not in variables:
+                    errors.append(f"{where}: reference to undeclared variable var.{attrs[0]}")
+            elif root == "local":
+                if attrs and attrs[0] not in locals_:
+                    errors.append(f"{where}: reference to undefined local.{attrs[0]}")
+            elif root == "data":
+                if len(attrs) >= 2 and (attrs[0], attrs[1]) not in datas:
+                    errors.append(f"{where}: reference to undefined data.{attrs[0]}.{attrs[1]}")
+            elif root == "module":
+                if attrs and attrs[0] not in modules:
+                    errors.append(f"{where}: reference to undefined module.{attrs[0]}")
+            elif root in resource_types:
+                if attrs and (root, attrs[0]) not in resources:
+                    errors.append(f"{where}: reference to undefined resource {root}.{attrs[0]}")
+            elif root not in _BUILTIN_ROOTS:
+                errors.append(f"{where}: unknown reference {'.'.join([root] + attrs[:1])}")
+        for node in walk(body):
+            if node.kind == "call" and node.value == "templatefile":
+                errors += _check_templatefile(module_dir, f"{name}/{fn}", node)
+    return ModuleReport(name, files, errors, variables, required, outputs)
+
+
+def _check_templatefile(module_dir: str, where: str, call: Node) -> List[str]:
+    if len(call.children) != 2:
+        return [f"{where}: templatefile() takes 2 arguments"]
+    path_node, vars_node = call.children
+    rel = _module_relative_path(path_node)
+    if rel is None:
+        return []  # computed path (e.g. for-expression over fileset): checked by the caller's test
+    tpl_path = os.path.join(module_dir, rel)
+    if not os.path.isfile(tpl_path):
+        return [f"{where}: templatefile() of missing file {rel}"]
+    with open(tpl_path, encoding="utf-8") as fh:
+        try:
+            names = template_names(parse_template(fh.read(), rel))
+        except HCLSyntaxError as exc:
+            return [str(exc)]
+    keys = object_keys(vars_node)
+    if keys is None:
+        return [f"{where}: templatefile({rel}) vars must be an object constructor"]
+    errs = []
+    if names - keys:
+        errs.append(f"{where}: templatefile({rel}) does not pass {sorted(names - keys)}")
+    if keys - names:
+        errs.append(f"{where}: templatefile({rel}) passes unused {sorted(keys - names)}")
+    return errs
+
+
+def _module_relative_path(node: Node) -> Optional[str]:
+    """``"${path.module}/files/x.tftpl"`` -> ``files/x.tftpl``."""
+    if node.kind != "tmpl" or len(node.children) != 2:
+        return None
+    head, tail = node.children
+    if head.kind != "interp" or tail.kind != "lit":
+        return None
+    ref = head.children[0]
+    if ref.kind == "trav" and ref.value == "path" and [c.value for c in ref.children] == ["module"]:
+        return tail.value.lstrip("/")
+    return None

@@ -35,6 +35,12 @@ variable "docker_engine_install_url" {
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
 }
 
+variable "docker_install_sha256" {
+  description = "SHA-256 the downloaded runtime install script must match (empty: not checked)."
+  type        = string
+  default     = ""
+}
+
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
   type        = string

@@ -4,7 +4,7 @@
 # and the checksum of the Rancher CA bundle.  Query keys: name, version, network,
 # api_url, access_key, secret_key, registry, registry_username, registry_password.
 exec python3 -c '
-import base64, hashlib, json, ssl, sys, urllib.request
+import base64, hashlib, json, re, ssl, sys, urllib.parse, urllib.request
 
 q = json.load(sys.stdin)
 ctx = ssl.create_default_context()
@@ -21,11 +21,24 @@ def call(method, path, body=None):
         return json.load(resp)
 
 
+def k8s_version(requested):
+    # requested if the server offers it, else its newest release of the same minor
+    offered = [v for v in call("GET", "/v3/settings/k8s-versions-current").get("value", "").split(",") if v]
+    if not offered or requested in offered:
+        return requested
+    minor = requested.split(".")[:2]
+    same = [v for v in offered if v.split(".")[:2] == minor]
+    if not same:
+        sys.exit("Kubernetes version %s is not offered by the Rancher server (offered: %s)"
+                 % (requested, ", ".join(offered)))
+    return max(same, key=lambda v: [int(x) for x in re.findall(r"[0-9]+", v)])
+
+
 found = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
 if found:
     cluster_id = found[0]["id"]
 else:
-    rke = {"type": "rancherKubernetesEngineConfig", "kubernetesVersion": q["version"],
+    rke = {"type": "rancherKubernetesEngineConfig", "kubernetesVersion": k8s_version(q["version"]),
            "ignoreDockerVersion": False, "sshAgentAuth": False,
            "authentication": {"type": "authnConfig", "strategy": "x509"},
            "network": {"type": "networkConfig", "plugin": q["network"]},

@@ -22,7 +22,12 @@ variable "rancher_secret_key" {
 variable "k8s_version" {
   description = "RKE Kubernetes version."
   type        = string
-  default     = "v1.9.5-rancher1-1"
+  default     = "v1.28.10-rancher1-1"
+
+  validation {
+    condition     = contains(["v1.28", "v1.27", "v1.26"], join(".", slice(split(".", var.k8s_version), 0, 2)))
+    error_message = "k8s_version must be an RKE1 release of Rancher v2.8.5 (v1.28.10-rancher1-1, v1.27.14-rancher1-1, v1.26.15-rancher1-1)."
+  }
 }
 
 variable "k8s_network_provider" {

@@ -7,12 +7,35 @@ variable "rancher_admin_password" {
   description = "The Rancher admin password"
   type        = string
   sensitive   = true
+
+  validation {
+    condition     = length(var.rancher_admin_password) >= 12 && length(regexall("['\"\\\\]", var.rancher_admin_password)) == 0
+    error_message = "rancher_admin_password must be at least 12 characters (Rancher >= 2.6) without quotes or backslashes."
+  }
+}
+
+variable "rancher_bootstrap_password" {
+  description = "First-login password of the Rancher server (CATTLE_BOOTSTRAP_PASSWORD); empty: derived from name and rancher_admin_password."
+  type        = string
+  default     = ""
+  sensitive   = true
+
+  validation {
+    condition     = length(regexall("['\"\\\\]", var.rancher_bootstrap_password)) == 0
+    error_message = "rancher_bootstrap_password must not contain quotes or backslashes."
+  }
 }
 
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
   type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
+}
+
+variable "docker_install_sha256" {
+  description = "SHA-256 the downloaded runtime install script must match (empty: not checked)."
+  type        = string
+  default     = ""
 }
 
 variable "rancher_server_image" {

@@ -27,13 +27,13 @@ variable "rancher_cluster_id" {
 variable "device_plugin_image" {
   description = "Device plugin image."
   type        = string
-  default     = "rocm/k8s-device-plugin:latest"
+  default     = "rocm/k8s-device-plugin:1.31.0.6"
 }
 
 variable "node_labeller_image" {
   description = "Node labeller image."
   type        = string
-  default     = "rocm/k8s-device-plugin:labeller-latest"
+  default     = "rocm/k8s-device-plugin:labeller-1.31.0.6"
 }
 
 variable "rccl_probe_image" {

@@ -7,15 +7,22 @@ templates, and they fix the reference quirks Q10
 (hard-coded ``/home/ubuntu``, ``/etc/fstab`` overwritten with ``tee``).
 """
 
+# download, verify (when docker_install_sha256 is set), run — no `curl | sh` of an unchecked stream
+DOCKER_INSTALL = r"""if ! command -v docker >/dev/null 2>&1; then
+  curl -fsSL -o /tmp/tk-install-docker.sh '${docker_engine_install_url}'
+%{ if docker_install_sha256 != "" ~}
+  echo '${docker_install_sha256}  /tmp/tk-install-docker.sh' | sha256sum -c - >/dev/null || { echo 'docker install script checksum mismatch' >&2; exit 1; }
+%{ endif ~}
+  sudo sh /tmp/tk-install-docker.sh && rm -f /tmp/tk-install-docker.sh
+fi"""
+
 INSTALL_DOCKER = r"""#!/bin/bash
 # S1/S6: container runtime for a Rancher manager or node (cloud-init / remote-exec).
 set -euo pipefail
 if command -v firewalld >/dev/null 2>&1; then
   sudo systemctl disable --now firewalld.service || true
 fi
-if ! command -v docker >/dev/null 2>&1; then
-  curl -fsSL "${docker_engine_install_url}" | sudo sh
-fi
+""" + DOCKER_INSTALL + r"""
 if [ ! -f /etc/docker/daemon.json ]; then
   if mountpoint -q /mnt; then
     echo '{"storage-driver": "overlay2", "data-root": "/mnt/docker"}' | sudo tee /etc/docker/daemon.json >/dev/null
@@ -38,7 +45,9 @@ set -euo pipefail
 for i in $(seq 1 600); do command -v docker >/dev/null 2>&1 && break; sleep 1; done
 for i in $(seq 1 600); do sudo docker image inspect '${rancher_server_image}' >/dev/null 2>&1 && break; sudo docker pull '${rancher_server_image}' || sleep 1; done
 if ! sudo docker ps --format '{{.Image}}' | grep -qx '${rancher_server_image}'; then
-  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 '${rancher_server_image}'
+  # Rancher >= 2.6 has no admin/admin: the first login uses this bootstrap password
+  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 \
+    -e CATTLE_BOOTSTRAP_PASSWORD='${bootstrap_password}' '${rancher_server_image}'
 fi
 """
 
@@ -48,9 +57,15 @@ set -euo pipefail
 R='${rancher_host}'
 for i in $(seq 1 900); do curl -ksf "$R/ping" >/dev/null 2>&1 && break; sleep 1; done
 json() { python3 -c "import json,sys; print(json.load(sys.stdin)$1)"; }
-login=$(curl -ksf -X POST -H 'Content-Type: application/json' \
-  -d '{"username":"admin","password":"admin","ttl":60000,"description":"Initial Token"}' \
-  "$R/v3-public/localProviders/local?action=login")
+login_as() {
+  curl -ksf -X POST -H 'Content-Type: application/json' \
+    -d "{\"username\":\"admin\",\"password\":\"$1\",\"ttl\":60000,\"description\":\"Initial Token\"}" \
+    "$R/v3-public/localProviders/local?action=login"
+}
+# the bootstrap password the server was started with; a re-run after the password
+# change logs in with the admin password and skips the change
+changed=0
+login=$(login_as '${bootstrap_password}') || { login=$(login_as '${rancher_admin_password}'); changed=1; }
 initial=$(printf '%s' "$login" | json '["token"]')
 tok=$(curl -ksf -u "$initial" -X POST -H 'Content-Type: application/json' \
   -d '{"type":"token","name":"triton-kubernetes","description":"Managed by triton-kubernetes","ttl":0}' "$R/v3/token")
@@ -58,8 +73,8 @@ umask 077
 printf '%s' "$tok" > ~/rancher_api_key
 ak=$(printf '%s' "$tok" | json '["name"]')
 sk=$(printf '%s' "$tok" | json '["token"].split(":",1)[1]')
-curl -ksf -u "$ak:$sk" -X POST -H 'Content-Type: application/json' \
-  -d '{"currentPassword":"admin","newPassword":"${rancher_admin_password}"}' "$R/v3/users?action=changepassword" >/dev/null
+[ "$changed" = 1 ] || curl -ksf -u "$ak:$sk" -X POST -H 'Content-Type: application/json' \
+  -d '{"currentPassword":"${bootstrap_password}","newPassword":"${rancher_admin_password}"}' "$R/v3/users?action=changepassword" >/dev/null
 curl -ksf -u "$ak:$sk" -X PUT -H 'Content-Type: application/json' \
   -d '{"name":"server-url","value":"${host_registration_url}"}' "$R/v3/settings/server-url" >/dev/null
 """
@@ -84,7 +99,7 @@ RANCHER_CLUSTER = r"""#!/bin/bash
 # and the checksum of the Rancher CA bundle.  Query keys: name, version, network,
 # api_url, access_key, secret_key, registry, registry_username, registry_password.
 exec python3 -c '
-import base64, hashlib, json, ssl, sys, urllib.request
+import base64, hashlib, json, re, ssl, sys, urllib.parse, urllib.request
 
 q = json.load(sys.stdin)
 ctx = ssl.create_default_context()
@@ -101,11 +116,24 @@ def call(method, path, body=None):
         return json.load(resp)
 
 
+def k8s_version(requested):
+    # requested if the server offers it, else its newest release of the same minor
+    offered = [v for v in call("GET", "/v3/settings/k8s-versions-current").get("value", "").split(",") if v]
+    if not offered or requested in offered:
+        return requested
+    minor = requested.split(".")[:2]
+    same = [v for v in offered if v.split(".")[:2] == minor]
+    if not same:
+        sys.exit("Kubernetes version %s is not offered by the Rancher server (offered: %s)"
+                 % (requested, ", ".join(offered)))
+    return max(same, key=lambda v: [int(x) for x in re.findall(r"[0-9]+", v)])
+
+
 found = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
 if found:
     cluster_id = found[0]["id"]
 else:
-    rke = {"type": "rancherKubernetesEngineConfig", "kubernetesVersion": q["version"],
+    rke = {"type": "rancherKubernetesEngineConfig", "kubernetesVersion": k8s_version(q["version"]),
            "ignoreDockerVersion": False, "sshAgentAuth": False,
            "authentication": {"type": "authnConfig", "strategy": "x509"},
            "network": {"type": "networkConfig", "plugin": q["network"]},
@@ -133,7 +161,7 @@ INSTALL_RANCHER_AGENT = r"""#!/bin/bash
 # S5: join a node to the cluster (user-data or remote-exec).
 set -euo pipefail
 if command -v firewalld >/dev/null 2>&1; then sudo systemctl disable --now firewalld.service || true; fi
-if ! command -v docker >/dev/null 2>&1; then curl -fsSL "${docker_engine_install_url}" | sudo sh; fi
+""" + DOCKER_INSTALL + r"""
 if [ ! -f /etc/docker/daemon.json ]; then
   echo '{"storage-driver": "overlay2"}' | sudo tee /etc/docker/daemon.json >/dev/null
   sudo systemctl restart docker || sudo service docker restart
@@ -198,7 +226,7 @@ set -a; . /etc/rccl/rccl.env; set +a
 $T/rccl-ready --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
 %{ endif ~}
 labels=$(sed 's/^/--label /' /etc/triton-kubernetes/gpu-labels | tr '\n' ' ')
-if ! command -v docker >/dev/null 2>&1; then curl -fsSL "${docker_engine_install_url}" | sudo sh; fi
+""" + DOCKER_INSTALL + r"""
 sudo hostnamectl set-hostname '${hostname}'
 %{ if rancher_registry_username != "" ~}
 echo '${rancher_registry_password}' | sudo docker login -u '${rancher_registry_username}' --password-stdin '${rancher_registry}'

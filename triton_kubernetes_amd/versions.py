@@ -1,0 +1,100 @@
+"""Pinned component versions: one place, used by every delivery path.
+
+The reference pairs ``rancher/server:v2.0.0-beta2`` with the RKE releases that
+server shipped (``create/cluster.go:349-356``,
+``terraform/modules/triton-rancher/variables.tf:14-22``).  This framework pins
+Rancher v2.8.5 and offers only the RKE1 Kubernetes releases of that Rancher
+line; the CLI choices, the module defaults, the Rancher client, the DirectExecutor
+and the bench all read them from here, and the fake Rancher server rejects
+anything else (``rancher/fake.py``).
+
+Rancher ≥2.6 no longer starts with admin/admin: it takes the first admin
+password from ``CATTLE_BOOTSTRAP_PASSWORD`` (or generates a random one).  Every
+manager path starts the server with :func:`bootstrap_password` — derived from the
+manager name and the admin password, so a re-run of a half-finished bootstrap
+(the container already running) logs in with the same value — and then changes it
+to ``rancher_admin_password``.  The Terraform modules compute the same value
+(``sha256("tk-bootstrap:<name>:<password>")``, first 32 hex digits).
+"""
+
+import hashlib
+import re
+from typing import List, Optional, Sequence, Tuple
+
+RANCHER_VERSION = "v2.8.5"
+SERVER_IMAGE = f"rancher/rancher:{RANCHER_VERSION}"
+AGENT_IMAGE = f"rancher/rancher-agent:{RANCHER_VERSION}"
+
+# RKE1 Kubernetes releases of the Rancher v2.8.5 line (display name, kubernetesVersion).
+# The server's own list (setting ``k8s-versions-current``) is authoritative at create
+# time: a pinned patch release the server no longer offers is replaced by the server's
+# release of the same minor (RancherClient.resolve_k8s_version).
+K8S_VERSIONS: List[Tuple[str, str]] = [
+    ("v1.28", "v1.28.10-rancher1-1"),
+    ("v1.27", "v1.27.14-rancher1-1"),
+    ("v1.26", "v1.26.15-rancher1-1"),
+]
+DEFAULT_K8S_VERSION = K8S_VERSIONS[0][1]
+K8S_MINORS = tuple(d for d, _ in K8S_VERSIONS)
+
+# container runtime: Rancher's install script for a Docker release RKE1 v1.5 supports
+DOCKER_VERSION = "24.0"
+DOCKER_INSTALL_URL = f"https://releases.rancher.com/install-docker/{DOCKER_VERSION}.sh"
+
+# MI355X add-ons (pinned tags, never :latest)
+DEVICE_PLUGIN_IMAGE = "rocm/k8s-device-plugin:1.31.0.6"
+NODE_LABELLER_IMAGE = "rocm/k8s-device-plugin:labeller-1.31.0.6"
+# the RCCL readiness Job runs the node's installed rccl-ready (hostPath /opt/triton-kubernetes
+# and /opt/rocm), so any small glibc image serves; pinned by tag
+RCCL_PROBE_IMAGE = "ubuntu:22.04"
+# the RCCL-env injector (mutating admission webhook, k8s/webhook.py) runs the stdlib server
+WEBHOOK_IMAGE = "python:3.11-slim"
+
+# Rancher ≥2.6 refuses shorter admin passwords (setting password-min-length)
+PASSWORD_MIN_LENGTH = 12
+
+_K8S_RE = re.compile(r"^v(\d+)\.(\d+)(?:\.(\d+))?(-rancher\d+-\d+)?$")
+
+
+def bootstrap_password(manager_name: str, admin_password: str) -> str:
+    """First-login password handed to the server as ``CATTLE_BOOTSTRAP_PASSWORD``."""
+    return hashlib.sha256(f"tk-bootstrap:{manager_name}:{admin_password}".encode()).hexdigest()[:32]
+
+
+def k8s_minor(version: str) -> Optional[str]:
+    """``v1.28.10-rancher1-1`` / ``v1.28`` -> ``v1.28``; None if not a version string."""
+    m = _K8S_RE.match(version or "")
+    return f"v{m.group(1)}.{m.group(2)}" if m else None
+
+
+def normalize_k8s_version(value: str) -> str:
+    """Map a display name to its pinned release and reject releases outside the pinned
+    Rancher line (a v1.9 cluster cannot be created on Rancher 2.8)."""
+    for display, full in K8S_VERSIONS:
+        if value == display:
+            return full
+    minor = k8s_minor(value)
+    if minor is None or minor not in K8S_MINORS:
+        offered = ", ".join(full for _, full in K8S_VERSIONS)
+        raise ValueError(f"Kubernetes version '{value}' is not offered by Rancher {RANCHER_VERSION}; "
+                         f"choose one of: {offered}")
+    return value
+
+
+def resolve_against(requested: str, offered: Sequence[str]) -> Tuple[str, str]:
+    """``(version, note)``: ``requested`` if the server offers it, else the server's newest
+    release of the same minor (note says so).  Raises ValueError when the minor is absent."""
+    offered = [v for v in offered if v]
+    if not offered or requested in offered:
+        return requested, ""
+    minor = k8s_minor(requested)
+    same = [v for v in offered if k8s_minor(v) == minor]
+    if not same:
+        raise ValueError(f"Kubernetes version '{requested}' is not offered by the Rancher server "
+                         f"(offered: {', '.join(offered)})")
+
+    def key(v: str) -> Tuple[int, ...]:
+        return tuple(int(x) for x in re.findall(r"\d+", v))
+
+    best = max(same, key=key)
+    return best, f"{requested} is not offered by the server; using {best}"
