@@ -5,6 +5,7 @@ import datetime
 import json
 import os
 import threading
+import time
 
 import pytest
 
@@ -181,3 +182,103 @@ def test_encrypted_key_needs_passphrase(tmp_path):
         public_key_fingerprint(path)  # non-interactive: no hanging prompt (Q14)
     assert str(exc.value).startswith("Unable to parse private key:")
     assert public_key_fingerprint(path, lambda: "hunter22") == load_private_key(path, "hunter22").fingerprint_md5()
+
+
+def test_manta_create_then_destroy_manager_removes_every_object(manta, tmp_path):
+    """BASELINE config #4 teardown: status.json, backups and the lock are deleted before the
+    directory (reference backend/manta/backend.go:160-194); Manta refuses a non-empty one."""
+    from triton_kubernetes_amd import workflows as wf
+    from triton_kubernetes_amd.rancher.fake import FakeRancher
+    from helpers import make_ctx
+
+    fake, key_path, key = manta
+    be = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://triton", fake.url)
+    pw = "tk-admin-pw-0123"
+    with FakeRancher.for_manager("mgr", pw) as rancher:
+        wf.new_manager(make_ctx({"backend_provider": "manta", "executor": "direct",
+                                 "manager_cloud_provider": "baremetal", "name": "mgr",
+                                 "rancher_admin_password": pw, "host": "rancher+" + rancher.url,
+                                 "ssh_user": "u", "bastion_host": "", "key_path": "k"}), be)
+    be.write_blob("mgr", "backups.json", b'["b1"]')
+    be.write_blob("mgr", "backup-b1.json", b"{}")
+    names = {p.rsplit("/", 1)[1] for p in fake.objects if "/triton-kubernetes/mgr/" in p}
+    assert {"main.tf.json", "terraform.tfstate", "status.json", "backups.json", "backup-b1.json"} <= names
+    wf.delete_manager(make_ctx({"cluster_manager": "mgr", "executor": "direct"}), be)
+    assert be.states() == []
+    assert not any("/triton-kubernetes/mgr" in p for p in list(fake.objects) + list(fake.dirs))
+    be.delete_state("mgr")  # idempotent on a missing manager
+
+
+def test_manta_conditional_put_semantics(manta):
+    fake, key_path, key = manta
+    client = MantaClient(fake.url, HTTPSignatureSigner("acct", key))
+    client.put_directory("/stor/x")
+    e1 = client.put_object("/stor/x/o", b"1", if_none_match="*")
+    assert e1 and client.put_object("/stor/x/o", b"2", if_none_match="*") is None  # exists
+    assert client.put_object("/stor/x/o", b"3", if_match="stale") is None
+    e2 = client.put_object("/stor/x/o", b"4", if_match=e1)
+    assert e2 and e2 != e1 and client.get_object_etag("/stor/x/o") == (b"4", e2)
+    assert client.delete("/stor/x/o", if_match=e1) is False  # stale etag: not deleted
+    assert client.delete("/stor/x/o", if_match=e2) is True and client.get_object("/stor/x/o") is None
+    with pytest.raises(TKError, match="DirectoryNotEmpty"):
+        client.put_object("/stor/x/p", b"")
+        client.delete("/stor/x")
+
+
+def test_manta_lock_is_mutually_exclusive_under_contention(manta):
+    import threading
+
+    fake, key_path, key = manta
+    be = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://triton", fake.url)
+    holders, max_holders, order = [0], [0], []
+    mu = threading.Lock()
+    start = threading.Barrier(6)
+
+    def worker(i):
+        start.wait()
+        with be.lock("mgr", timeout=60, poll=0.01):
+            with mu:
+                holders[0] += 1
+                max_holders[0] = max(max_holders[0], holders[0])
+                order.append(i)
+            time.sleep(0.02)
+            with mu:
+                holders[0] -= 1
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(6)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert max_holders[0] == 1 and sorted(order) == list(range(6))
+    assert "/acct/stor/triton-kubernetes/mgr/.lock" not in fake.objects
+
+
+def test_manta_expired_lock_taken_over_by_exactly_one(manta):
+    import threading
+
+    fake, key_path, key = manta
+    be = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://triton", fake.url)
+    be.client.put_directory("/stor/triton-kubernetes/mgr")
+    be.client.put_object("/stor/triton-kubernetes/mgr/.lock", json.dumps({"token": "dead", "expires": 0}).encode())
+    winners = []
+    start = threading.Barrier(4)
+    release = threading.Event()
+
+    def worker(i):
+        start.wait()
+        try:
+            with be.lock("mgr", timeout=0.3, poll=0.01):
+                winners.append(i)
+                release.wait(2)
+        except Exception:  # noqa: BLE001 - the losers time out while the winner holds it
+            pass
+
+    threads = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
+    for t in threads:
+        t.start()
+    time.sleep(0.6)
+    release.set()
+    for t in threads:
+        t.join()
+    assert len(winners) == 1

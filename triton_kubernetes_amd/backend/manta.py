@@ -12,8 +12,14 @@ Deliberate fixes:
   write the PEM instead;
 * ``states()`` paginates instead of stopping at 100 entries;
 * ``persist_state`` creates the manager directory first;
-* :meth:`lock` implements an advisory lock object ``<name>/.lock`` with an
-  owner token and TTL (the reference's TODO at ``backend.go:32``).
+* :meth:`lock` implements a lock object ``<name>/.lock`` with an owner token and
+  TTL (the reference's TODO at ``backend.go:32``), taken with Manta's conditional
+  PUT — ``If-None-Match: *`` to create it, ``If-Match: <etag>`` to take over an
+  expired one and to release it — so two writers can never both hold it;
+* :meth:`delete_state` removes *every* object of the manager directory (state,
+  tfstate, ``status.json``, backups, the lock) before the directory, as the
+  reference removes each object it wrote before the directory
+  (``backend.go:160-194``); Manta refuses to delete a non-empty directory.
 """
 
 import contextlib
@@ -23,6 +29,7 @@ import time
 import uuid
 from typing import Any, Iterator, List, Optional, Tuple
 
+from ..cloud.http import HTTPError
 from ..cloud.triton import HTTPSignatureSigner, MantaClient
 from ..errors import BackendError
 from ..state import State
@@ -74,10 +81,31 @@ class MantaBackend(Backend):
         self.client.put_object(self._p(state.name, CONFIG_FILE), state.bytes())
 
     def delete_state(self, name: str) -> None:
-        self.client.delete(self._p(name, CONFIG_FILE))
-        self.client.delete(self._p(name, TFSTATE_FILE))
-        self.client.delete(self._p(name, ".lock"))
-        self.client.delete(self._p(name))
+        base = self._p(name)
+        try:
+            entries = self.client.list_directory(base)
+        except HTTPError as exc:
+            if exc.status == 404:  # nothing persisted under this name
+                return
+            raise
+        # the main document last: a half-finished delete still lists the manager
+        order = sorted(entries, key=lambda e: (e.get("name") == CONFIG_FILE, e.get("name", "")))
+        for e in order:
+            path = f"{base}/{e['name']}"
+            if e.get("type") == "directory":
+                self._delete_tree(path)
+            else:
+                self.client.delete(path)
+        self.client.delete(base)
+
+    def _delete_tree(self, path: str) -> None:
+        for e in self.client.list_directory(path):
+            child = f"{path}/{e['name']}"
+            if e.get("type") == "directory":
+                self._delete_tree(child)
+            else:
+                self.client.delete(child)
+        self.client.delete(path)
 
     def state_terraform_config(self, name: str) -> Tuple[str, Any]:
         material = self.key_path
@@ -99,25 +127,37 @@ class MantaBackend(Backend):
         self.client.put_object(self._p(name, filename), data)
 
     @contextlib.contextmanager
-    def lock(self, name: str, timeout: float = 60.0, ttl: float = 900.0) -> Iterator[None]:
+    def lock(self, name: str, timeout: float = 60.0, ttl: float = 900.0, poll: float = 0.25) -> Iterator[None]:
+        """Exclusive lock on the manager's documents.
+
+        Acquire: create ``.lock`` with ``If-None-Match: *`` (fails if any holder exists);
+        a holder past its expiry is replaced with ``If-Match: <its etag>``, so of several
+        writers racing for an expired lock exactly one wins.  Release: delete with
+        ``If-Match: <our etag>`` (a lock taken over after expiring is left alone)."""
         token = uuid.uuid4().hex
         path = self._p(name, ".lock")
         deadline = time.monotonic() + timeout
         self.client.put_directory(self._p(name))
+        etag: Optional[str] = None
         while True:
-            raw = self.client.get_object(path)
-            holder = json.loads(raw) if raw else None
-            if holder is None or holder.get("expires", 0) < time.time():
-                self.client.put_object(path, json.dumps({"token": token, "expires": time.time() + ttl}).encode())
-                check = json.loads(self.client.get_object(path) or b"{}")
-                if check.get("token") == token:
-                    break
+            body = json.dumps({"token": token, "expires": time.time() + ttl}).encode()
+            etag = self.client.put_object(path, body, if_none_match="*")
+            if etag is not None:
+                break
+            raw, held_etag = self.client.get_object_etag(path)
+            if raw is not None and held_etag:
+                try:
+                    holder = json.loads(raw)
+                except ValueError:
+                    holder = {}
+                if float(holder.get("expires", 0)) < time.time():
+                    etag = self.client.put_object(path, body, if_match=held_etag)
+                    if etag is not None:
+                        break
             if time.monotonic() > deadline:
                 raise BackendError(f"timed out waiting for the Manta state lock of '{name}'")
-            time.sleep(0.5)
+            time.sleep(poll)
         try:
             yield
         finally:
-            raw = self.client.get_object(path)
-            if raw and json.loads(raw).get("token") == token:
-                self.client.delete(path)
+            self.client.delete(path, if_match=etag or None)

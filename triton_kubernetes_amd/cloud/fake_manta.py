@@ -2,11 +2,16 @@
 
 Used by the Manta backend tests and by the Triton/Manta dry-run configuration
 (BASELINE.json config #4).  Every request must carry a valid joyent HTTP
-signature for a registered RSA public key (``add_key``).
+signature for a registered RSA public key (``add_key``).  Like Manta it refuses
+to delete a non-empty directory (``DirectoryNotEmpty``), returns an ``ETag`` for
+every object, and honours the conditional headers ``If-Match`` /
+``If-None-Match`` (``*`` or an etag list) on PUT, GET and DELETE with HTTP 412
+``PreconditionFailed``.
 """
 
 import base64
 import email.utils
+import hashlib
 import http.server
 import json
 import socket
@@ -24,7 +29,8 @@ class FakeManta:
         self.account = account
         self.keys: Dict[str, PrivateKey] = {}  # keyId path -> key (public half used)
         self.dirs = {f"/{account}/stor"}
-        self.objects: Dict[str, Tuple[bytes, str]] = {}
+        self.objects: Dict[str, Tuple[bytes, str, str]] = {}  # path -> (data, content type, etag)
+        self._etag_seq = 0
         self.mu = threading.Lock()
         self.requests = 0
         self.rejected = 0
@@ -90,6 +96,18 @@ class FakeManta:
                 parts = urllib.parse.urlsplit(self.path)
                 return urllib.parse.unquote(parts.path).rstrip("/"), urllib.parse.parse_qs(parts.query)
 
+            def _precondition_ok(self, path: str) -> bool:
+                """If-Match / If-None-Match against the object's current etag (fake.mu held)."""
+                cur = fake.objects.get(path)
+                etag = cur[2] if cur is not None else None
+                im, inm = self.headers.get("If-Match"), self.headers.get("If-None-Match")
+                tags = lambda v: {t.strip().strip('"') for t in v.split(",")}  # noqa: E731
+                if im is not None and (etag is None or (im.strip() != "*" and etag not in tags(im))):
+                    return False
+                if inm is not None and etag is not None and (inm.strip() == "*" or etag in tags(inm)):
+                    return False
+                return True
+
             def _guard(self) -> bool:
                 with fake.mu:
                     fake.requests += 1
@@ -112,9 +130,13 @@ class FakeManta:
                         return self._err(404, "DirectoryDoesNotExist")
                     if "type=directory" in self.headers.get("Content-Type", ""):
                         fake.dirs.add(path)
-                    else:
-                        fake.objects[path] = (data, self.headers.get("Content-Type", ""))
-                self._reply(204)
+                        return self._reply(204)
+                    if not self._precondition_ok(path):
+                        return self._err(412, "PreconditionFailed")
+                    fake._etag_seq += 1
+                    etag = hashlib.md5(data + str(fake._etag_seq).encode()).hexdigest()
+                    fake.objects[path] = (data, self.headers.get("Content-Type", ""), etag)
+                self._reply(204, extra={"ETag": etag})
 
             def do_GET(self):
                 if not self._guard():
@@ -122,8 +144,8 @@ class FakeManta:
                 path, q = self._path()
                 with fake.mu:
                     if path in fake.objects:
-                        data, ctype = fake.objects[path]
-                        return self._reply(200, data, ctype)
+                        data, ctype, etag = fake.objects[path]
+                        return self._reply(200, data, ctype, {"ETag": etag})
                     if path in fake.dirs:
                         names = sorted({p[len(path) + 1:].split("/", 1)[0] for p in list(fake.dirs) +
                                         list(fake.objects) if p.startswith(path + "/")})
@@ -144,6 +166,8 @@ class FakeManta:
                 path, _ = self._path()
                 with fake.mu:
                     if path in fake.objects:
+                        if not self._precondition_ok(path):
+                            return self._err(412, "PreconditionFailed")
                         del fake.objects[path]
                     elif path in fake.dirs:
                         if any(p.startswith(path + "/") for p in list(fake.dirs) + list(fake.objects)):

@@ -17,7 +17,7 @@ import email.utils
 import json
 import urllib.parse
 from dataclasses import dataclass
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Tuple
 
 from ..utils.sshkeys import PrivateKey, load_private_key
 from .http import HTTPClient, HTTPError
@@ -162,13 +162,43 @@ class MantaClient:
                 return None
             raise
 
-    def put_object(self, path: str, data: bytes, content_type: str = "application/json") -> None:
-        self.http.request("PUT", urllib.parse.quote(self._path(path)), data=data,
-                          headers={"Content-Type": content_type})
-
-    def delete(self, path: str, missing_ok: bool = True) -> None:
+    def get_object_etag(self, path: str) -> Tuple[Optional[bytes], Optional[str]]:
+        """``(body, etag)``; ``(None, None)`` when the object does not exist."""
         try:
-            self.http.request("DELETE", urllib.parse.quote(self._path(path)))
+            resp = self.http.request("GET", urllib.parse.quote(self._path(path)))
         except HTTPError as exc:
+            if exc.status == 404 or b"ResourceNotFound" in exc.body:
+                return None, None
+            raise
+        return resp.body, resp.header("etag") or None
+
+    def put_object(self, path: str, data: bytes, content_type: str = "application/json",
+                   if_match: Optional[str] = None, if_none_match: Optional[str] = None) -> Optional[str]:
+        """PUT an object; returns its new ETag.  With ``if_match`` / ``if_none_match``
+        (``"*"``: only if absent) the write is conditional: a failed precondition
+        (HTTP 412) returns None and changes nothing."""
+        headers = {"Content-Type": content_type}
+        if if_match is not None:
+            headers["If-Match"] = if_match
+        if if_none_match is not None:
+            headers["If-None-Match"] = if_none_match
+        try:
+            resp = self.http.request("PUT", urllib.parse.quote(self._path(path)), data=data, headers=headers)
+        except HTTPError as exc:
+            if exc.status == 412 and (if_match is not None or if_none_match is not None):
+                return None
+            raise
+        return resp.header("etag") or ""
+
+    def delete(self, path: str, missing_ok: bool = True, if_match: Optional[str] = None) -> bool:
+        """DELETE; False when ``if_match`` no longer matches (HTTP 412) or the object was absent."""
+        headers = {"If-Match": if_match} if if_match is not None else None
+        try:
+            self.http.request("DELETE", urllib.parse.quote(self._path(path)), headers=headers)
+            return True
+        except HTTPError as exc:
+            if if_match is not None and exc.status == 412:
+                return False
             if not (missing_ok and exc.status == 404):
                 raise
+            return False
