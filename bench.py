@@ -2,29 +2,40 @@
 """Headline benchmark: cluster create -> kubectl-ready wall-clock, bare-metal MI355X.
 
 Metric (BASELINE.json): "cluster create->kubectl-ready wall-clock (s),
-bare-metal at 1/2/4/8 workers" on config #5, "create cluster MI355X bare-metal
-N-worker + ROCm device-plugin + xGMI topology labels".
+bare-metal at 1/2/4/8 workers", measured on config #5: "create cluster MI355X
+bare-metal N-worker + ROCm device-plugin + xGMI topology labels".
 
-One rank per GPU (``torchrun --nproc-per-node N``); every rank is one simulated
-MI355X worker host running a :class:`NodeAgent` that owns its GPU.  A timed step
-is one complete ``create cluster`` through the framework's real code path —
-settings -> bare-metal provider -> ``main.tf.json`` -> DirectExecutor DAG ->
-Rancher client -> parallel node bootstrap -> readiness waiter — with a fresh
-cluster name per step, measured from the start of ``create cluster`` until the
-waiter reports every phase done:
+Shape.  ``--gpus N`` (the driver's N, one torchrun rank per GPU) is the number of
+MI355X GPUs the cluster's worker tier owns.  By default ONE worker node owns all of
+them -- one node agent with ``devices=0..N-1``, as on a real 8xMI355X node, so the
+per-node steps (burn-in of every GPU concurrently, topology labels) and the RCCL
+gate (``ndev=N`` grouped communicator init in one agent) run at node scale.
+``--workers W`` splits the N GPUs over W agents instead.  When the launcher masks
+devices per rank (each rank sees only its own GPU), every rank runs one 1-GPU agent.
 
-* cluster active, all nodes ``Ready``;
-* every worker advertises ``amd.com/gpu`` (device-plugin add-on applied);
-* per-GPU burn-in passed on each worker (HBM3E stream, bf16 + fp8 MFMA, memtest —
-  hand-written gfx950 HIP kernels, run for real) and its topology labels
-  (KFD sysfs via the in-process native labeller, plus RDMA NICs) attached at registration;
-* a cluster-wide RCCL all-reduce gate across all N GPUs (native RCCL over xGMI).
+Each timed step is a COLD create:
 
-What is simulated (and therefore excluded): the Rancher server is the
-in-process v3 fake, whose RKE provisioning is instantaneous, and the host
-runtime steps (docker install, hostname, agent container) are no-ops in the
-agents' ``sim`` mode.  The reference publishes no number for this metric, so
-``vs_baseline`` is null.
+1. fresh node-agent processes start (``python -m triton_kubernetes_amd.node.agent``:
+   HIP/RCCL load, burn-in arena allocation, RCCL unique id -- nothing carried over
+   from earlier steps), plus a fresh control-plane agent;
+2. ``create cluster`` runs through the framework's real code path -- settings ->
+   bare-metal provider -> ``main.tf.json`` -> DirectExecutor DAG -> Rancher client ->
+   parallel node bootstrap (per-GPU HBM/MFMA/memtest burn-in and topology labels,
+   for real on the MI355X) -> add-ons -> readiness waiter (cluster active, nodes Ready,
+   ``amd.com/gpu`` allocatable, cluster-wide RCCL all-reduce gate across all N GPUs);
+3. the agents shut down (communicator teardown, HIP release), inside the step.
+
+``value`` is the mean create -> kubectl-ready time (agent start to readiness);
+``ms_per_step`` is the whole step including the agent shutdown.  A WARM number (the
+same create against agents kept resident across steps, round 1's headline) is
+reported only as the secondary ``warm_create_to_ready_s``, measured after the timed
+region.
+
+Simulated (``config.simulated_phases``): the Rancher server is the in-process v3
+fake, so RKE provisioning is instantaneous (``rke_provisioning``); the host runtime
+install (``runtime_install``: firewall, docker, hostname, registry login) and the
+``docker run rancher/agent`` container (``agent_container``) are sim-mode no-ops of the
+agents.  The reference publishes no number for this metric, so ``vs_baseline`` is null.
 
 Rank 0 prints one JSON line (the driver's contract).
 """
@@ -32,6 +43,8 @@ Rank 0 prints one JSON line (the driver's contract).
 import argparse
 import json
 import os
+import signal
+import subprocess
 import sys
 import tempfile
 import time
@@ -40,6 +53,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 METRIC = "cluster create→kubectl-ready wall-clock (s), bare-metal at 1/2/4/8 workers"
+SIMULATED_PHASES = ["rke_provisioning", "runtime_install", "agent_container"]
 
 
 def parse_args():
@@ -47,25 +61,100 @@ def parse_args():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--workers", type=int, default=1, help="worker nodes the N GPUs are split over")
     ap.add_argument("--burnin", default="quick", choices=["quick", "full", "off"])
     ap.add_argument("--no-rccl-gate", action="store_true")
     ap.add_argument("--rccl-mib", type=int, default=64, help="largest RCCL gate message (MiB)")
+    ap.add_argument("--warm-steps", type=int, default=2,
+                    help="secondary: creates against resident agents after the timed region (0: skip)")
+    ap.add_argument("--agents", default="proc", choices=["proc", "inproc"],
+                    help="proc: every agent in its own fresh process (the headline); inproc: agents as "
+                         "objects in this process (the graft smoke: native libraries load here)")
     ap.add_argument("--sim-gpu", action="store_true",
                     help="CPU dry run: synthetic topology, no burn-in kernels, no RCCL (never a valid measurement)")
-    ap.add_argument("--no-gate-pipeline", action="store_true",
-                    help="start the RCCL gate's communicator init after readiness instead of with the apply")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
     return ap.parse_args()
 
 
+class AgentProc:
+    """One node agent in its own process (what systemd runs on a real node)."""
+
+    def __init__(self, name: str, devices, token_file: str, root: str, synthetic: int = 0):
+        argv = [sys.executable, "-u", "-m", "triton_kubernetes_amd.node.agent", "--mode", "sim",
+                "--listen", "127.0.0.1:0", "--name", name, "--token-file", token_file, "--root", root,
+                "--devices", ",".join(str(d) for d in devices)]
+        if synthetic:
+            argv += ["--synthetic-gpus", str(synthetic)]
+        env = dict(os.environ, PYTHONPATH=HERE + os.pathsep + os.environ.get("PYTHONPATH", ""))
+        self.name = name
+        self.proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=None, text=True, env=env,
+                                     start_new_session=True)
+        self.url = ""
+        self.signalled = False
+
+    def wait_url(self, timeout: float = 300.0) -> str:
+        # the agent prints one JSON line once it serves (native libraries loaded, arena ready)
+        import selectors
+
+        sel = selectors.DefaultSelector()
+        sel.register(self.proc.stdout, selectors.EVENT_READ)
+        deadline = time.monotonic() + timeout
+        while not self.url:
+            if self.proc.poll() is not None:
+                raise RuntimeError(f"agent {self.name} exited {self.proc.returncode} before serving")
+            if not sel.select(timeout=max(0.0, deadline - time.monotonic())):
+                raise RuntimeError(f"agent {self.name} did not start within {timeout:.0f}s")
+            line = self.proc.stdout.readline()
+            if line.startswith("{"):
+                self.url = json.loads(line)["listening"]
+        sel.close()
+        return self.url
+
+    def signal_stop(self) -> None:
+        if self.proc.poll() is None and not self.signalled:
+            self.proc.send_signal(signal.SIGTERM)
+            self.signalled = True
+
+    def stop(self, timeout: float = 120.0) -> int:
+        if self.proc.poll() is None:
+            self.signal_stop()
+            try:
+                self.proc.wait(timeout=timeout)
+            except subprocess.TimeoutExpired:
+                os.killpg(self.proc.pid, signal.SIGKILL)
+                self.proc.wait()
+        self.proc.stdout.close()
+        return self.proc.returncode
+
+
+class InprocAgent:
+    """Same interface as :class:`AgentProc`, the agent living in this process."""
+
+    def __init__(self, name: str, devices, token: str, root: str, synthetic: int = 0):
+        from triton_kubernetes_amd.node.agent import NodeAgent
+
+        self.name = name
+        self.agent = NodeAgent(name=name, mode="sim", devices=list(devices), token=token, root=root)
+        if synthetic:
+            from triton_kubernetes_amd.node.labels import synthetic_topology
+
+            self.agent.topology_override = synthetic_topology(synthetic)
+            self.agent.burnin_override = lambda dev, level: {"ok": True, "simulated": True, "level": level}
+        self.url = self.agent.serve()
+
+    def wait_url(self, timeout: float = 0.0) -> str:
+        return self.url
+
+    def signal_stop(self) -> None:
+        pass
+
+    def stop(self, timeout: float = 0.0) -> int:
+        self.agent.stop()
+        return 0
+
+
 def main() -> int:
     args = parse_args()
-    import faulthandler
-
-    watchdog = float(os.environ.get("TK_BENCH_WATCHDOG", "0") or 0)
-    if watchdog > 0:  # debugging aid: dump every thread's Python stack periodically
-        faulthandler.dump_traceback_later(watchdog, repeat=True, file=sys.stderr)
-    step_watchdog = float(os.environ.get("TK_BENCH_STEP_WATCHDOG", "0") or 0)
     import torch
     import torch.distributed as dist
 
@@ -74,50 +163,71 @@ def main() -> int:
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus and rank == 0:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
+    n_gpus = world
     distributed = world > 1
     if distributed:
-        # control-plane sync only (CPU); the GPU collectives are the native RCCL gate
+        # control-plane sync only (CPU); the GPU collectives are the agents' native RCCL gate
         dist.init_process_group("gloo", init_method="env://")
-    device = local_rank
     if args.sim_gpu:
         args.no_rccl_gate = True
+        visible = n_gpus
     else:
-        # one GPU per rank; a launcher that masks devices per rank leaves each rank only its own
-        device = local_rank if torch.cuda.device_count() > local_rank else 0
-        torch.cuda.set_device(device)
+        visible = torch.cuda.device_count()
+        torch.cuda.set_device(local_rank if visible > local_rank else 0)
 
+    # which agents this rank owns: (name, devices).  Unmasked: rank 0 owns every worker
+    # agent; masked (each rank sees one GPU): every rank owns a 1-GPU agent.
+    masked = not args.sim_gpu and visible < n_gpus
+    if masked:
+        workers = n_gpus
+        mine = [(f"mi355x-{rank}", [0])]
+    else:
+        workers = max(1, min(args.workers, n_gpus))
+        if n_gpus % workers:
+            raise SystemExit(f"--workers {workers} does not divide {n_gpus} GPUs")
+        per = n_gpus // workers
+        mine = [(f"mi355x-{w}", list(range(w * per, (w + 1) * per))) for w in range(workers)] if rank == 0 else []
+    gpus_per_worker = n_gpus // workers
+
+    from triton_kubernetes_amd import versions
     from triton_kubernetes_amd import workflows as wf
     from triton_kubernetes_amd.backend import LocalBackend
     from triton_kubernetes_amd.config import Context, Settings
-    from triton_kubernetes_amd.node.agent import NodeAgent
     from triton_kubernetes_amd.parallel.transport import AgentTransport
-    from triton_kubernetes_amd.utils import procstat
-    from triton_kubernetes_amd.utils.trace import TRACER
+    from triton_kubernetes_amd.utils.trace import TRACER, span
 
     token = os.environ.get("TK_BENCH_TOKEN", "bench-token-0123456789")
     work = tempfile.mkdtemp(prefix=f"tk-bench-r{rank}-")
-    agent = NodeAgent(name=f"mi355x-{rank}", mode="sim", devices=[device], token=token,
-                      root=os.path.join(work, "node"))
-    if args.sim_gpu:
-        from triton_kubernetes_amd.node.labels import synthetic_topology
+    token_file = os.path.join(work, "agent-token")
+    with open(token_file, "w", encoding="utf-8") as fh:
+        fh.write(token)
+    synthetic = gpus_per_worker if args.sim_gpu else 0
 
-        agent.topology_override = synthetic_topology(1)
-        agent.burnin_override = lambda dev, level: {"ok": True, "simulated": True}
-    my_url = agent.serve()
-    urls = [my_url]
-    if distributed:
-        urls = [None] * world
-        dist.all_gather_object(urls, my_url)
+    def start_agents(tag: str):
+        if args.agents == "inproc":
+            procs = [InprocAgent(name, devs, token, os.path.join(work, tag, name), synthetic) for name, devs in mine]
+            if rank == 0:
+                procs.append(InprocAgent("control-plane", [], token, os.path.join(work, tag, "cp")))
+            return procs
+        procs = [AgentProc(name, devs, token_file, os.path.join(work, tag, name), synthetic) for name, devs in mine]
+        if rank == 0:
+            procs.append(AgentProc("control-plane", [], token_file, os.path.join(work, tag, "cp")))
+        return procs
 
-    fake = cp_agent = None
-    backend = ctx_base = None
+    def gather_urls(procs):
+        local = [(p.name, p.wait_url()) for p in procs]
+        if distributed:
+            every = [None] * world
+            dist.all_gather_object(every, local)
+            local = [x for part in every for x in part]
+        return dict(local)
+
+    fake = backend = ctx_base = None
     devnull = open(os.devnull, "w", encoding="utf-8")  # workflow output (one handle for every step)
     if rank == 0:
         from triton_kubernetes_amd.rancher.fake import FakeRancher
 
         fake = FakeRancher.for_manager("bench", "bench-admin-pw-0123").start()
-        cp_agent = NodeAgent(name="control-plane", mode="sim", token=token, root=os.path.join(work, "cp"))
-        cp_url = cp_agent.serve()
         backend = LocalBackend(os.path.join(work, "state"))
         ctx_base = {"backend_provider": "local", "executor": "direct", "agent_token": token,
                     "non-interactive": True, "cluster_manager": "bench"}
@@ -125,61 +235,59 @@ def main() -> int:
                    host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="~/.ssh/id_rsa")
         wf.new_manager(Context(settings=Settings(mgr, env={}), out=devnull), backend)
 
-    sizes = [1 << 20, args.rccl_mib << 20]
-    # long-lived startup objects (torch, the package, servers) leave the GC's working set,
-    # so a full collection during a step does not walk them (a ~100 ms stall was measured)
-    import gc
-
-    gc.collect()
-    gc.freeze()
-    gc_events = []  # (generation, ms) of every collection during the run, for the report
-    gc_t0 = {}
-
-    def _gc_cb(phase, info):
-        if phase == "start":
-            gc_t0["t"] = time.perf_counter()
-        elif "t" in gc_t0:
-            gc_events.append((info.get("generation"), round((time.perf_counter() - gc_t0.pop("t")) * 1e3, 3)))
-
-    gc.callbacks.append(_gc_cb)
-    gc_mode = os.environ.get("TK_BENCH_GC", "")
-    if gc_mode == "off":
-        gc.disable()
-    elif gc_mode.startswith("threshold:"):
-        gc.set_threshold(*[int(x) for x in gc_mode.split(":", 1)[1].split(",")])
-
-    def one_step(i: int) -> dict:
-        name = f"bench-{i}"
-        cfg = dict(ctx_base, cluster_cloud_provider="baremetal", name=name, k8s_version="v1.28.10-rancher1-1",
+    def create(i: int, urls) -> dict:
+        """rank 0: one ``create cluster --wait`` against the agents at ``urls``."""
+        name = f"bench-{i}".replace("--", "-w")
+        cp = "agent+" + urls["control-plane"]
+        gpu_hosts = ["agent+" + urls[f"mi355x-{w}"] for w in range(workers)]
+        cfg = dict(ctx_base, cluster_cloud_provider="baremetal", name=name, k8s_version=versions.DEFAULT_K8S_VERSION,
                    k8s_network_provider="flannel", gpu_addons=True, wait=True,
-                   rccl_gate=not args.no_rccl_gate, rccl_pipeline=not args.no_gate_pipeline, wait_timeout=600,
+                   rccl_gate=not args.no_rccl_gate, rccl_gate_max_mib=args.rccl_mib, wait_timeout=600,
                    nodes=[
                        {"rancher_host_label": "control", "node_count": 1, "hostname": f"{name}-cp",
-                        "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": ["agent+" + cp_url]},
+                        "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": [cp]},
                        {"rancher_host_label": "etcd", "node_count": 1, "hostname": f"{name}-etcd",
-                        "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": ["agent+" + cp_url]},
-                       {"rancher_host_label": "worker", "node_count": world, "hostname": f"{name}-gpu",
-                        "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k",
-                        "hosts": ["agent+" + u for u in urls], "gpu": "mi355x", "gpu_count": 1,
-                        "gpu_burnin": args.burnin},
+                        "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": [cp]},
+                       {"rancher_host_label": "worker", "node_count": workers, "hostname": f"{name}-gpu",
+                        "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": gpu_hosts,
+                        "gpu": "mi355x", "gpu_count": gpus_per_worker, "gpu_burnin": args.burnin},
                    ])
         ctx = Context(settings=Settings(cfg, env={}), out=devnull)
         ctx.extras["agent_transport"] = AgentTransport(token=token)
-        ps0 = procstat.snapshot()
-        t0 = time.time()
-        if step_watchdog > 0:  # diagnosis: every thread's Python stack if a step overruns
-            faulthandler.dump_traceback_later(step_watchdog, file=sys.stderr)
         wf.new_cluster(ctx, backend)
-        if step_watchdog > 0:
-            faulthandler.cancel_dump_traceback_later()
-        dt = time.time() - t0
-        out = {"step": i, "seconds": dt, "proc": procstat.delta(ps0, procstat.snapshot())}
+        out = {}
         rep = ctx.extras.get("last_readiness")
-        ranks = ((rep.rccl or {}).get("ranks") or []) if rep is not None else []
-        phases = [r.get("phase_ms") or {} for r in ranks]
-        if phases:  # the gate's communicator init on every rank: where an N-GPU step goes
-            out["rccl"] = {k: round(max(float(p.get(k, 0.0)) for p in phases), 3)
-                           for k in ("init_total", "init_wait", "alloc", "sweep")}
+        if rep is not None:
+            out["phase_s"] = rep.to_json()["phase_seconds"]
+            ranks = (rep.rccl or {}).get("ranks") or []
+            phases = [r.get("phase_ms") or {} for r in ranks]
+            if phases:  # the gate's communicator phases, max over agents
+                out["rccl"] = {k: round(max(float(p.get(k, 0.0)) for p in phases), 3)
+                               for k in ("init_total", "init_wait", "alloc", "sweep")}
+                out["rccl_peak_busbw_gbps"] = rep.rccl.get("min_peak_busbw_gbps")
+        return out
+
+    def cold_step(i: int) -> dict:
+        """Fresh agents -> create -> readiness -> agents stop (every rank takes part)."""
+        t0 = time.perf_counter()
+        with span("bench.agents_start"):
+            procs = start_agents(f"s{i}")
+            urls = gather_urls(procs)
+        t_agents = time.perf_counter()
+        out = {"step": i}
+        if rank == 0:
+            out.update(create(i, urls))
+        t_ready = time.perf_counter()
+        if distributed:
+            dist.barrier()  # the create is done before any rank stops its agents
+        with span("bench.agents_stop"):
+            for p in procs:  # every agent shuts down concurrently
+                p.signal_stop()
+            rcs = [p.stop() for p in procs]
+        if any(rcs):
+            raise RuntimeError(f"agent exit codes {rcs}")
+        out.update(agents_start_s=round(t_agents - t0, 4), create_to_ready_s=round(t_ready - t0, 4),
+                   step_s=round(time.perf_counter() - t0, 4))
         return out
 
     def sync():
@@ -191,21 +299,15 @@ def main() -> int:
             dist.barrier()
         sync()
 
-    results = []
     for w in range(args.warmup):
         barrier()
-        if rank == 0:
-            one_step(-1 - w)
-        barrier()
-
+        cold_step(-1 - w)
     barrier()
     TRACER.reset()
+    results = []
     t_start = time.perf_counter()
     for i in range(args.steps):
-        if rank == 0:
-            results.append(one_step(i))
-        if distributed:
-            dist.barrier()
+        results.append(cold_step(i))
     sync()
     if distributed:
         dist.barrier()
@@ -214,25 +316,44 @@ def main() -> int:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         elapsed = float(t.item())
+    trace = TRACER.report()
+
+    # secondary: warm creates against agents kept resident (outside the timed region)
+    warm = []
+    if args.warm_steps > 0:
+        procs = start_agents("warm")
+        urls = gather_urls(procs)
+        for i in range(args.warm_steps + 1):  # the first one warms the agents, untimed
+            t0 = time.perf_counter()
+            if rank == 0:
+                create(1000 + i, urls)
+            if distributed:
+                dist.barrier()
+            if i:
+                warm.append(time.perf_counter() - t0)
+        for p in procs:
+            p.signal_stop()
+        for p in procs:
+            p.stop()
 
     if rank == 0:
         ms = elapsed / max(1, args.steps) * 1000.0
+        ready = [r["create_to_ready_s"] for r in results]
         phases = {}
-        for sp in TRACER.report()["spans"]:
-            if sp["name"].startswith(("ready.", "module.", "node.", "direct.apply", "apply")):
+        for sp in trace["spans"]:
+            if sp["name"].startswith(("ready.", "module.", "direct.apply", "apply", "bench.")):
                 phases.setdefault(sp["name"], []).append(sp["duration"])
         phase_ms = {k: round(sum(v) / max(1, args.steps) * 1000.0, 2) for k, v in sorted(phases.items())}
-        # RCCL gate, max over ranks per step, mean over steps: communicator init wall time,
-        # the part of it the readiness waiter still waited for, and the verified sweep
         gate = [r["rccl"] for r in results if "rccl" in r]
         for k in ("init_total", "init_wait", "sweep"):
             if gate:
                 phase_ms[f"rccl.{k}_max_rank"] = round(sum(g[k] for g in gate) / len(gate), 2)
+        sim = "SIM-GPU DRY RUN (not a measurement); " if args.sim_gpu else ""
         line = {
             "metric": METRIC,
-            "value": round(ms / 1000.0, 4),
+            "value": round(sum(ready) / max(1, len(ready)), 4),
             "unit": "s",
-            "n_gpus": world,
+            "n_gpus": n_gpus,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 2),
@@ -240,30 +361,36 @@ def main() -> int:
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "bf16",
-            "data": ("SIM-GPU DRY RUN (not a measurement); " if args.sim_gpu else "") + ("synthetic: in-process Rancher v3 fake (RKE provisioning not simulated) and sim-mode host "
-                     "runtime steps; GPU steps real on MI355X (native KFD-sysfs topology + RDMA labels, HBM/MFMA/memtest "
-                     f"burn-in level={args.burnin} through the agent's resident buffers, cluster-wide RCCL all-reduce "
-                     f"gate {'off' if args.no_rccl_gate else 'on'}: a fresh communicator per create)"),
+            "data": sim + ("synthetic cold create: fresh node-agent processes per step; simulated phases "
+                           "rke_provisioning (in-process Rancher v3 fake, instantaneous RKE), runtime_install "
+                           "(firewall/docker/hostname/registry-login no-ops) and agent_container (agent registers "
+                           "via the fake's connect API instead of docker run rancher/agent); real on MI355X: "
+                           f"native topology + RDMA labels, per-GPU HBM/MFMA/memtest burn-in level={args.burnin}, "
+                           f"cluster RCCL all-reduce gate {'off' if args.no_rccl_gate else 'on'} "
+                           f"(one communicator over all {n_gpus} GPUs)"),
             "config": {
                 "model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology labels",
-                "workers": world, "gpus_per_worker": 1, "control_plane_nodes": 2,
-                "global_batch": world, "seq_len": 0, "parallelism": f"{world} workers (1 GPU each)",
+                "workers": workers, "gpus_per_worker": gpus_per_worker, "visible_gpus": visible,
+                "control_plane_nodes": 2, "global_batch": n_gpus, "seq_len": 0,
+                "parallelism": f"{workers} worker node(s) x {gpus_per_worker} GPU(s)",
                 "executor": "direct", "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate,
-                "rccl_gate_pipelined": not (args.no_rccl_gate or args.no_gate_pipeline),
+                "start": ("cold (fresh agent processes per step)" if args.agents == "proc"
+                          else "cold agents in the bench process (fresh NodeAgent objects per step)"),
+                "rccl_gate_max_mib": args.rccl_mib,
+                "simulated_phases": list(SIMULATED_PHASES),
+                "rancher": versions.RANCHER_VERSION, "k8s_version": versions.DEFAULT_K8S_VERSION,
             },
+            "create_to_ready_s": ready,
+            "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),
+            "warm_create_to_ready_s": round(sum(warm) / len(warm), 4) if warm else None,
             "phase_ms_per_step": phase_ms,
         }
         print(json.dumps(line), flush=True)
         if args.report:
             with open(args.report, "w", encoding="utf-8") as fh:
-                json.dump({"line": line, "steps": results, "trace": TRACER.report(), "gc": gc_events,
-                           "cpu_quota": procstat.cpu_quota(), "cpu_affinity": len(os.sched_getaffinity(0)),
-                           "cgroup_cpu_dir": procstat.cgroup_cpu_dir()},
-                          fh, indent=1, default=str)
+                json.dump({"line": line, "steps": results, "warm_s": warm, "trace": trace}, fh, indent=1,
+                          default=str)
     devnull.close()
-    agent.stop()
-    if cp_agent is not None:
-        cp_agent.stop()
     if fake is not None:
         fake.stop()
     import shutil

@@ -5,12 +5,12 @@ set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export PYTHONPATH="$GRAFT_REPO_ROOT"
-LOG=gpurun_out/check.log
+LOG="$GRAFT_REPO_ROOT/gpurun_out/check.log"
 : > $LOG
 step() {  # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2
   local t0=$(date +%s%N)
-  timeout -k 10 "$secs" "$@" > "gpurun_out/$name.log" 2>&1
+  timeout -k 10 "$secs" "$@" > "$GRAFT_REPO_ROOT/gpurun_out/$name.log" 2>&1
   local rc=$?
   echo "$name rc=$rc wall_ms=$(( ($(date +%s%N) - t0) / 1000000 ))" >> $LOG
   echo "$name rc=$rc"
@@ -27,4 +27,8 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = burnin ]; then
   step burnin_quick 120 triton_kubernetes_amd/ops/lib/gpu-burnin --all --level quick
   step burnin_full 600 triton_kubernetes_amd/ops/lib/gpu-burnin --all --level full
+fi
+if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
+  cd /tmp && export TMPDIR=/tmp
+  step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --warm-steps 0
 fi

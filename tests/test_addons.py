@@ -1,0 +1,244 @@
+"""MI355X add-ons: one definition for both delivery paths, pinned images, and the
+RCCL-env injector webhook (unit + end to end through the fake Rancher's admission chain)."""
+
+import base64
+import json
+import os
+import tempfile
+import threading
+
+import pytest
+
+from triton_kubernetes_amd import versions
+from triton_kubernetes_amd.backend import LocalBackend
+from triton_kubernetes_amd.k8s import addons, webhook
+from triton_kubernetes_amd.k8s.manifests import apply_manifests
+from triton_kubernetes_amd.k8s.tls import serving_cert
+from triton_kubernetes_amd.node.agent import NodeAgent
+from triton_kubernetes_amd.node.labels import synthetic_topology
+from triton_kubernetes_amd.rancher.client import RancherClient
+from triton_kubernetes_amd.rancher.fake import FakeRancher
+from triton_kubernetes_amd.terraform import hcl
+from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+from triton_kubernetes_amd.workflows import new_cluster, new_manager
+
+from helpers import have, make_ctx
+
+TOKEN = "addon-token-123456"
+MOD = os.path.join(MODULES_DIR, addons.MODULE)
+
+
+def _terraform_render(cfg, values):
+    """What the Terraform module applies, evaluated from its own main.tf: the ``group_of``
+    map and the ``enabled`` conditions of ``locals``, then templatefile() on each file of
+    ``fileset(files/manifests, *.tftpl)`` in the order apply_addons.sh globs them."""
+    body = hcl.parse(open(os.path.join(MOD, "main.tf"), encoding="utf-8").read(), "main.tf")
+    local = next(b for b in body.blocks if b.type == "locals").body
+    group_of = {}
+    for item in next(a for a in local.attributes if a.name == "group_of").expr.children:
+        group_of[item.children[0].value] = item.children[1].value
+    enabled = {}
+    for item in next(a for a in local.attributes if a.name == "enabled").expr.children:
+        key, expr = item.children[0].value, item.children[1]
+        if expr.kind == "lit":
+            enabled[key] = bool(expr.value)
+        else:  # var.<name> ==/!= "<lit>"
+            var = expr.children[0].children[0].value
+            lit = expr.children[1].value
+            v = cfg.get(var, _var_default(var))
+            enabled[key] = (v == lit) if expr.value == "==" else (v != lit)
+    out = []
+    d = os.path.join(MOD, "files", "manifests")
+    for f in sorted(os.listdir(d)):
+        name = f[: -len(".tftpl")]
+        if enabled[group_of.get(name, "base")]:
+            doc = json.loads(addons.render_template(open(os.path.join(d, f), encoding="utf-8").read(), values))
+            out.append((doc["path"], doc["object"]))
+    return out
+
+
+def _var_default(name):
+    body = hcl.parse(open(os.path.join(MOD, "variables.tf"), encoding="utf-8").read(), "variables.tf")
+    blk = next(b for b in body.blocks if b.labels == [name])
+    return next(a.expr.value for a in blk.body.attributes if a.name == "default")
+
+
+@pytest.mark.parametrize("cfg", [
+    {},
+    {"rccl_env_injector": "false"},
+    {"rccl_gate": "false", "node_labeller_image": ""},
+    {"device_plugin_image": "registry.local/dp:1.2", "webhook_image": "registry.local/py:3.11"},
+])
+def test_terraform_and_direct_paths_render_the_same_objects(cfg):
+    cert = serving_cert(addons.INJECTOR, "kube-system") if have("openssl") else None
+    direct = addons.rendered_addons(cfg, cert)
+    tf = _terraform_render(cfg, addons.addon_values(addons.module_cfg_defaults(cfg), cert))
+    assert direct == tf
+    kinds = [o["kind"] for _, o in direct]
+    assert kinds[:2] == ["DaemonSet", "ConfigMap"]
+    assert ("MutatingWebhookConfiguration" in kinds) == (cfg.get("rccl_env_injector", "true") == "true")
+    assert ("Job" in kinds) == (cfg.get("rccl_gate", "true") == "true")
+
+
+def test_generated_templates_match_the_definition():
+    """Every object of k8s/addons.py is one module file (generator in sync), and the
+    module passes exactly the template variables the files use."""
+    d = os.path.join(MOD, "files", "manifests")
+    files = sorted(f for f in os.listdir(d) if f.endswith(".tftpl"))
+    assert files == sorted(o.file + ".tftpl" for o in addons.addon_templates())
+    for obj in addons.addon_templates():
+        assert open(os.path.join(d, obj.file + ".tftpl"), encoding="utf-8").read() == addons.template_text(obj)
+    used = set()
+    for f in files:
+        used |= hcl.template_names(hcl.parse_template(open(os.path.join(d, f), encoding="utf-8").read(), f))
+    assert used <= set(addons.TEMPLATE_VARS)
+    assert not hcl.check_module(MOD).errors
+
+
+def test_addon_images_are_pinned():
+    cfg = {"device_plugin_image": "", "node_labeller_image": None}
+    values = addons.addon_values(cfg)
+    for k in ("device_plugin_image", "node_labeller_image", "rccl_probe_image", "webhook_image"):
+        assert values[k] and not values[k].endswith(":latest") and ":" in values[k], (k, values[k])
+        assert _var_default(k) == values[k]
+    ctx = make_ctx({"gpu_addons": True})
+    from triton_kubernetes_amd.models.baremetal import add_mi355x_addons
+    from triton_kubernetes_amd.state import State
+
+    st = State("m", {})
+    key = add_mi355x_addons(ctx, st, "cluster_baremetal_x", "x")
+    mod = st.module(key)
+    assert mod["device_plugin_image"] == versions.DEVICE_PLUGIN_IMAGE
+    assert mod["node_labeller_image"] == versions.NODE_LABELLER_IMAGE
+    assert mod["rccl_probe_image"] == versions.RCCL_PROBE_IMAGE and mod["rccl_env_injector"] == "true"
+    declared = hcl.check_module(MOD).variables
+    assert set(mod) - {"source"} <= declared
+
+
+def _gpu_pod(name="train", env=None, annotations=None, gpus="8"):
+    c = {"name": "main", "image": "rocm/pytorch:6.4", "resources": {"limits": {"amd.com/gpu": gpus}}}
+    if env is not None:
+        c["env"] = env
+    meta = {"name": name}
+    if annotations is not None:
+        meta["annotations"] = annotations
+    return {"apiVersion": "v1", "kind": "Pod", "metadata": meta,
+            "spec": {"containers": [c, {"name": "sidecar", "image": "busybox"}]}}
+
+
+def test_webhook_patch_for_gpu_pods():
+    env = {"NCCL_DEBUG": "WARN", "HSA_NO_SCRATCH_RECLAIM": "1"}
+    pod = webhook.apply_patch(_gpu_pod(), webhook.patch_for_pod(_gpu_pod(), env))
+    main, side = pod["spec"]["containers"]
+    got = {e["name"]: e["value"] for e in main["env"]}
+    assert got == {"HSA_NO_SCRATCH_RECLAIM": "1", "NCCL_DEBUG": "WARN", "TK_RCCL_ENV_FILE": "/etc/rccl/rccl.env"}
+    assert main["volumeMounts"] == [{"name": webhook.VOLUME, "mountPath": "/etc/rccl", "readOnly": True}]
+    assert "env" not in side and "volumeMounts" not in side  # no GPUs requested
+    assert pod["spec"]["volumes"][0]["hostPath"]["path"] == "/etc/rccl"
+    assert pod["metadata"]["annotations"] == {"amd.com/rccl-env": "injected"}
+    # the workload's own value wins; existing env/annotations are appended to
+    pod2 = _gpu_pod(env=[{"name": "NCCL_DEBUG", "value": "INFO"}], annotations={"team": "a"})
+    out = webhook.apply_patch(pod2, webhook.patch_for_pod(pod2, env))
+    got = {e["name"]: e["value"] for e in out["spec"]["containers"][0]["env"]}
+    assert got["NCCL_DEBUG"] == "INFO" and got["HSA_NO_SCRATCH_RECLAIM"] == "1"
+    assert out["metadata"]["annotations"] == {"team": "a", "amd.com/rccl-env": "injected"}
+    # idempotent (re-invocation), opt-out, zero GPUs, non-GPU pods
+    assert webhook.patch_for_pod(out, env) == []
+    assert webhook.patch_for_pod(_gpu_pod(annotations={"amd.com/rccl-env-inject": "false"}), env) == []
+    assert webhook.patch_for_pod(_gpu_pod(gpus="0"), env) == []
+    plain = {"metadata": {"name": "web"}, "spec": {"containers": [{"name": "c", "image": "nginx"}]}}
+    assert webhook.patch_for_pod(plain, env) == []
+    # AdmissionReview framing
+    resp = webhook.review({"apiVersion": "admission.k8s.io/v1", "request": {"uid": "u1", "object": _gpu_pod()}},
+                          env)["response"]
+    assert resp["uid"] == "u1" and resp["allowed"] and resp["patchType"] == "JSONPatch"
+    assert json.loads(base64.b64decode(resp["patch"]))[0]["op"] == "add"
+
+
+@pytest.mark.skipif(not have("openssl"), reason="openssl needed for the serving certificate")
+def test_injector_end_to_end_through_admission(tmp_path):
+    """Create a cluster with the add-ons through the DirectExecutor, then run the injector
+    exactly as its Deployment does (TLS from the applied Secret, env from the applied
+    ConfigMap, source from the applied ConfigMap) and create pods through the proxy."""
+    fake = FakeRancher.for_manager("mgr", "s3cret-passw0rd").start()
+    agents = []
+
+    def agent(name, gpus=0):
+        a = NodeAgent(name=name, mode="sim", devices=list(range(gpus)), token=TOKEN, root=tempfile.mkdtemp(),
+                      topology_override=synthetic_topology(gpus) if gpus else None,
+                      burnin_override=lambda d, lvl: {"ok": True})
+        agents.append(a)
+        return "agent+" + a.serve()
+
+    srv = None
+    try:
+        backend = LocalBackend(str(tmp_path / "state"))
+        base = {"executor": "direct", "agent_token": TOKEN}
+        new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr",
+                                  rancher_admin_password="s3cret-passw0rd", host="rancher+" + fake.url,
+                                  ssh_user="ubuntu", bastion_host="", key_path="k")), backend)
+        cp, w = agent("cp"), agent("w", 8)
+        nodes = [{"rancher_host_label": "control", "node_count": 1, "hostname": "cp", "ssh_user": "u",
+                  "bastion_host": "", "key_path": "k", "hosts": [cp]},
+                 {"rancher_host_label": "etcd", "node_count": 1, "hostname": "etcd", "ssh_user": "u",
+                  "bastion_host": "", "key_path": "k", "hosts": [cp]},
+                 {"rancher_host_label": "worker", "node_count": 1, "hostname": "gpu", "ssh_user": "u",
+                  "bastion_host": "", "key_path": "k", "hosts": [w], "gpu": "mi355x", "gpu_count": 8}]
+        new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
+                                  k8s_version=versions.DEFAULT_K8S_VERSION, k8s_network_provider="calico", gpu_addons=True, wait=True, nodes=nodes)), backend)
+        cid = list(fake.state.clusters)[0]
+        objs = {(o["kind"], o["metadata"]["name"]): o for o in fake.state.objects.values()}
+        assert ("MutatingWebhookConfiguration", "rccl-env-injector") in objs
+        # the Deployment's volumes, materialised from the applied objects
+        secret = objs[("Secret", "rccl-env-injector-tls")]["data"]
+        (tmp_path / "tls.crt").write_bytes(base64.b64decode(secret["tls.crt"]))
+        (tmp_path / "tls.key").write_bytes(base64.b64decode(secret["tls.key"]))
+        envdir = tmp_path / "env"
+        envdir.mkdir()
+        for k, v in objs[("ConfigMap", "rccl-env")]["data"].items():
+            (envdir / k).write_text(v)
+        src = objs[("ConfigMap", "rccl-env-injector-src")]["data"]["webhook.py"]
+        assert src == addons.webhook_source()
+        ns = {}
+        exec(compile(src, "webhook.py", "exec"), ns)  # noqa: S102 - the shipped module, as the pod runs it
+        srv = ns["make_server"](0, str(envdir), str(tmp_path / "tls.crt"), str(tmp_path / "tls.key"), "127.0.0.1")
+        threading.Thread(target=srv.serve_forever, daemon=True).start()
+        fake.service_endpoints["rccl-env-injector.kube-system"] = f"https://127.0.0.1:{srv.server_address[1]}"
+
+        outs = json.loads(backend.read_tfstate("mgr"))["module_outputs"]["cluster-manager"]
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        created = client.k8s(cid, "POST", "/api/v1/namespaces/default/pods", _gpu_pod(), ok=(201,))
+        env = {e["name"]: e["value"] for e in created["spec"]["containers"][0]["env"]}
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["TK_RCCL_ENV_FILE"] == "/etc/rccl/rccl.env"
+        assert created["metadata"]["annotations"]["amd.com/rccl-env"] == "injected"
+        # kube-system is excluded by the namespace selector; CPU pods are untouched
+        sys_pod = client.k8s(cid, "POST", "/api/v1/namespaces/kube-system/pods", _gpu_pod("sys"), ok=(201,))
+        assert "env" not in sys_pod["spec"]["containers"][0]
+        web = {"metadata": {"name": "web"}, "spec": {"containers": [{"name": "c", "image": "nginx"}]}}
+        assert "env" not in client.k8s(cid, "POST", "/api/v1/namespaces/default/pods", web,
+                                       ok=(201,))["spec"]["containers"][0]
+        # a webhook the API server cannot verify is skipped (failurePolicy Ignore), not fatal
+        fake.service_endpoints["rccl-env-injector.kube-system"] = fake.url.replace("http://", "https://")
+        skipped = client.k8s(cid, "POST", "/api/v1/namespaces/default/pods", _gpu_pod("p2"), ok=(201,))
+        assert "env" not in skipped["spec"]["containers"][0]
+    finally:
+        if srv is not None:
+            srv.shutdown()
+        for a in agents:
+            a.stop()
+        fake.stop()
+
+
+def test_apply_is_idempotent_with_rbac_and_injector():
+    fake = FakeRancher(bootstrap_password="b00tstrap-only").start()
+    try:
+        client = RancherClient(fake.url)
+        outs = client.bootstrap("n3w-passw0rd-123", fake.url, "b00tstrap-only", timeout=10)
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        cid = client.ensure_cluster("x").cluster_id
+        objs = addons.rendered_addons({})
+        first = apply_manifests(client, cid, objs)
+        assert first == apply_manifests(client, cid, objs)  # 409 -> PUT
+        assert "ClusterRoleBinding/amdgpu-node-labeller" in first and first[-1] == "Job/rccl-ready"
+    finally:
+        fake.stop()

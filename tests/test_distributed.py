@@ -22,11 +22,12 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
-@pytest.mark.parametrize("nproc", [2, 4])
-def test_bench_torchrun_gloo(nproc):
+@pytest.mark.parametrize("nproc,workers", [(2, 1), (4, 1), (4, 2)])
+def test_bench_torchrun_gloo(nproc, workers):
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
-           "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--sim-gpu"]
+           "--gpus", str(nproc), "--steps", "2", "--warmup", "1", "--warm-steps", "1", "--workers", str(workers),
+           "--sim-gpu"]
     env = dict(os.environ, OMP_NUM_THREADS="1")
     proc = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
     assert proc.returncode == 0, proc.stderr[-3000:]
@@ -35,11 +36,19 @@ def test_bench_torchrun_gloo(nproc):
     doc = json.loads(lines[0])
     assert doc["n_gpus"] == nproc and doc["steps"] == 2 and doc["warmup"] == 1
     assert doc["higher_is_better"] is False and doc["scaling"] == "weak" and doc["vs_baseline"] is None
-    assert doc["config"]["workers"] == nproc
+    # one worker node owns all N GPUs unless --workers splits them
+    cfg = doc["config"]
+    assert cfg["workers"] == workers and cfg["gpus_per_worker"] * workers == nproc
+    assert cfg["simulated_phases"] == ["rke_provisioning", "runtime_install", "agent_container"]
+    assert cfg["start"].startswith("cold")
     assert doc["data"].startswith("SIM-GPU DRY RUN")
-    assert doc["value"] > 0 and abs(doc["ms_per_step"] - doc["value"] * 1000) < 1.0
-    # every worker was bootstrapped through its own rank's agent
+    for phase in cfg["simulated_phases"]:
+        assert phase in doc["data"]
+    # value: mean create->ready of the cold steps; ms_per_step adds the agents' shutdown
+    assert doc["value"] > 0 and doc["ms_per_step"] >= doc["value"] * 1000 - 1.0
+    assert len(doc["create_to_ready_s"]) == 2 and doc["warm_create_to_ready_s"] > 0
     assert doc["phase_ms_per_step"]["module.host"] > 0
+    assert doc["phase_ms_per_step"]["bench.agents_start"] > 0
 
 
 def test_bench_single_process_default():
@@ -48,3 +57,14 @@ def test_bench_single_process_default():
     assert proc.returncode == 0, proc.stderr[-2000:]
     doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
     assert doc["n_gpus"] == 1 and doc["unit"] == "s"
+    assert doc["config"]["gpus_per_worker"] == doc["config"]["visible_gpus"] == 1
+
+
+def test_bench_inproc_agents():
+    """The graft smoke's shape: agents as objects in the bench process."""
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "1", "--warmup", "0",
+                           "--agents", "inproc", "--warm-steps", "0", "--sim-gpu"],
+                          capture_output=True, text=True, timeout=120, cwd=ROOT)
+    assert proc.returncode == 0, proc.stderr[-2000:]
+    doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["warm_create_to_ready_s"] is None and "bench process" in doc["config"]["start"]

@@ -80,12 +80,13 @@ def test_cluster_lifecycle_and_gpu_allocatable(rancher):
     nodes = {n["metadata"]["name"]: n for n in client.k8s_nodes(info.cluster_id)}
     assert nodes["g1"]["metadata"]["labels"]["amd.com/gpu.present"] == "true"
     assert "amd.com/gpu" not in nodes["g1"]["status"].get("allocatable", {})  # no device plugin yet
-    applied = apply_manifests(client, info.cluster_id, addon_manifests({}))
+    base = {"node_labeller_image": "", "rccl_env_injector": "false", "rccl_gate": "false"}
+    applied = apply_manifests(client, info.cluster_id, addon_manifests(base))
     assert applied == ["DaemonSet/amdgpu-device-plugin", "ConfigMap/rccl-env"]
     nodes = {n["metadata"]["name"]: n for n in client.k8s_nodes(info.cluster_id)}
     assert str(nodes["g1"]["status"]["allocatable"]["amd.com/gpu"]) == "8"
     # re-apply: 409 -> PUT
-    assert apply_manifests(client, info.cluster_id, addon_manifests({})) == applied
+    assert apply_manifests(client, info.cluster_id, addon_manifests(base)) == applied
     client.delete_cluster(info.cluster_id)
     client.delete_cluster(info.cluster_id)  # 404 tolerated
     assert client.find_cluster("gpu") is None
@@ -152,10 +153,12 @@ def test_gpu_job_manifest_affinity(tmp_path):
 
 
 def test_addon_manifest_options():
-    names = [o["metadata"]["name"] for _, o in addon_manifests(
+    names = [f'{o["kind"]}/{o["metadata"]["name"]}' for _, o in addon_manifests(
         {"node_labeller_image": "rocm/k8s-device-plugin:labeller", "rccl_gate": "true",
-         "rccl_probe_image": "tk/rccl:1"})]
-    assert names == ["amdgpu-device-plugin", "rccl-env", "amdgpu-node-labeller", "rccl-ready"]
+         "rccl_probe_image": "tk/rccl:1", "rccl_env_injector": "false"})]
+    assert names == ["DaemonSet/amdgpu-device-plugin", "ConfigMap/rccl-env",
+                     "ServiceAccount/amdgpu-node-labeller", "ClusterRole/amdgpu-node-labeller",
+                     "ClusterRoleBinding/amdgpu-node-labeller", "DaemonSet/amdgpu-node-labeller", "Job/rccl-ready"]
     cm = addon_manifests({})[1][1]
     assert cm["data"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
 

@@ -362,15 +362,26 @@ class DirectExecutor(Executor):
 
     # --- addons -------------------------------------------------------------------------------------------
     def _apply_addons(self, cfg: Dict[str, Any]) -> Dict[str, str]:
-        from ..k8s.manifests import addon_manifests, apply_manifests
+        """The Terraform add-on module's objects, rendered from its own template files
+        (``k8s/addons.py``), with the injector's serving certificate made by ``openssl``
+        (the module uses the ``tls`` provider) -- while the nodes still bootstrap."""
+        from ..k8s import addons
+        from ..k8s.manifests import apply_manifests
 
         client = self.rancher_factory(cfg["rancher_api_url"], cfg.get("rancher_access_key", ""),
                                       cfg.get("rancher_secret_key", ""))
         cid = cfg["rancher_cluster_id"]
+        cert = None
+        if addons.enabled("env", addons.module_cfg_defaults(cfg)):
+            from ..k8s.tls import serving_cert
+
+            with span("addons.tls", cluster=cid):
+                cert = serving_cert(addons.INJECTOR, "kube-system")
+        manifests = addons.rendered_addons(cfg, cert)
         with span("addons.wait_active", cluster=cid):
             wait_until(lambda: client.cluster_state(cid) == "active", self.cluster_wait, f"cluster {cid} active")
         with span("addons.apply", cluster=cid):
-            applied = apply_manifests(client, cid, addon_manifests(cfg))
+            applied = apply_manifests(client, cid, manifests)
         return {"addons_applied": str(len(applied))}
 
     # --- destroy / outputs ------------------------------------------------------------------------------

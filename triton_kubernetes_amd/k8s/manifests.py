@@ -3,7 +3,8 @@
 * ROCm device plugin DaemonSet (advertises ``amd.com/gpu``), scheduled on nodes
   labelled ``amd.com/gpu.present=true`` by the bootstrap labeller;
 * ROCm node-labeller DaemonSet (optional, keeps ``amd.com/gpu.*`` labels fresh);
-* ``rccl-env`` ConfigMap carrying the RCCL/HSA environment for GPU pods;
+* ``rccl-env`` ConfigMap carrying the RCCL/HSA environment for GPU pods (the
+  injector webhook, ``webhook.py``, puts it into every pod requesting ``amd.com/gpu``);
 * :func:`gpu_job_manifest` — an example/utility Job that requests all 8 GPUs
   of one xGMI hive (node affinity on ``amd.com/xgmi.fully-connected`` and the
   GPU count) and, for multi-node jobs, pod affinity on ``amd.com/xgmi.hive-id``
@@ -88,8 +89,10 @@ NODE_ENV_WRAPPER = 'set -a; [ -r /etc/rccl/rccl.env ] && . /etc/rccl/rccl.env; s
 
 
 def gpu_job_manifest(name: str, image: str, command: List[str], gpus_per_pod: int = 8, pods: int = 1,
-                     namespace: str = "default", hive_affinity: bool = True) -> Dict[str, Any]:
-    """A Job whose pods each take ``gpus_per_pod`` GPUs of one fully connected xGMI hive."""
+                     namespace: str = "default", hive_affinity: bool = True,
+                     host_paths: Optional[Dict[str, str]] = None) -> Dict[str, Any]:
+    """A Job whose pods each take ``gpus_per_pod`` GPUs of one fully connected xGMI hive.
+    ``host_paths`` maps node directories to container mount points (read-only)."""
     node_terms = [{"matchExpressions": [
         {"key": "amd.com/gpu.present", "operator": "In", "values": ["true"]},
         {"key": "amd.com/gpu.count", "operator": "In", "values": [str(gpus_per_pod)]},
@@ -104,6 +107,11 @@ def gpu_job_manifest(name: str, image: str, command: List[str], gpus_per_pod: in
             "weight": 100,
             "podAffinityTerm": {"labelSelector": {"matchLabels": {"job-name": name}},
                                 "topologyKey": "amd.com/xgmi.hive-id"}}]}
+    mounts = [{"name": "rccl-env", "mountPath": "/etc/rccl", "readOnly": True}]
+    volumes = [{"name": "rccl-env", "hostPath": {"path": "/etc/rccl", "type": "DirectoryOrCreate"}}]
+    for i, (host, target) in enumerate(sorted((host_paths or {}).items())):
+        mounts.append({"name": f"host-{i}", "mountPath": target, "readOnly": True})
+        volumes.append({"name": f"host-{i}", "hostPath": {"path": host, "type": "Directory"}})
     return {
         "apiVersion": "batch/v1", "kind": "Job",
         "metadata": {"name": name, "namespace": namespace},
@@ -122,9 +130,9 @@ def gpu_job_manifest(name: str, image: str, command: List[str], gpus_per_pod: in
                         "envFrom": [{"configMapRef": {"name": "rccl-env"}}],
                         "resources": {"limits": {"amd.com/gpu": str(gpus_per_pod)}},
                         "securityContext": {"capabilities": {"add": ["SYS_PTRACE"]}},
-                        "volumeMounts": [{"name": "rccl-env", "mountPath": "/etc/rccl", "readOnly": True}],
+                        "volumeMounts": mounts,
                     }],
-                    "volumes": [{"name": "rccl-env", "hostPath": {"path": "/etc/rccl", "type": "DirectoryOrCreate"}}],
+                    "volumes": volumes,
                     "hostIPC": True,
                 },
             },
@@ -132,20 +140,13 @@ def gpu_job_manifest(name: str, image: str, command: List[str], gpus_per_pod: in
     }
 
 
-def addon_manifests(cfg: Dict[str, Any]) -> List[Tuple[str, Dict[str, Any]]]:
-    """``(api collection path, object)`` pairs for the MI355X add-on module."""
-    out = [
-        (f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
-         device_plugin_daemonset(cfg.get("device_plugin_image") or "rocm/k8s-device-plugin:latest")),
-        (f"/api/v1/namespaces/{NAMESPACE}/configmaps", rccl_configmap()),
-    ]
-    if cfg.get("node_labeller_image"):
-        out.append((f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
-                    labeller_daemonset(cfg["node_labeller_image"])))
-    if str(cfg.get("rccl_gate", "false")).lower() == "true" and cfg.get("rccl_probe_image"):
-        out.append(("/apis/batch/v1/namespaces/default/jobs",
-                    gpu_job_manifest("rccl-ready", cfg["rccl_probe_image"], ["/opt/triton-kubernetes/bin/rccl-ready"])))
-    return out
+def addon_manifests(cfg: Dict[str, Any], cert: Any = None) -> List[Tuple[str, Dict[str, Any]]]:
+    """``(api collection path, object)`` pairs of the MI355X add-on module, rendered from the
+    module's own template files (``k8s/addons.py``; the single source both paths share).
+    Without ``cert`` the injector's certificate fields are empty (dry runs, tests)."""
+    from .addons import rendered_addons
+
+    return rendered_addons(cfg, cert)
 
 
 def apply_manifests(client, cluster_id: str, manifests: List[Tuple[str, Dict[str, Any]]]) -> List[str]:

@@ -1,0 +1,216 @@
+"""RCCL-env injector: a mutating admission webhook for GPU pods.
+
+Every pod that requests ``amd.com/gpu`` (limits or requests, any container or init
+container) gets, at admission time:
+
+* the cluster's RCCL/HSA environment (the ``rccl-env`` ConfigMap, mounted into the
+  webhook's pod as files and re-read on every request) as literal ``env`` entries on each
+  GPU container -- a variable the container already sets wins, so a workload can
+  override any value;
+* the node's own ``/etc/rccl`` (written by the node bootstrap: discovered RDMA ports,
+  per-node overrides) mounted read-only at ``/etc/rccl`` plus ``TK_RCCL_ENV_FILE``
+  pointing at ``/etc/rccl/rccl.env``, so launchers can source the node values on top;
+* the annotation ``amd.com/rccl-env: injected``.
+
+A pod opts out with the annotation ``amd.com/rccl-env-inject: "false"``.  The
+ConfigMap lives in ``kube-system``; ``envFrom`` cannot reach across namespaces, which
+is why the values are injected literally.
+
+This replaces round 1's opt-in ``envFrom`` + wrapper in the example Job
+(``manifests.gpu_job_manifest``): the BASELINE north star asks for the RCCL env on
+every GPU workload, not only on Jobs that know about it.
+
+The module is deliberately stdlib-only and self-contained: the add-on manifests ship
+its source text in a ConfigMap and run it with a pinned Python image
+(``versions.WEBHOOK_IMAGE``); ``python webhook.py --cert ... --key ... --env-dir ...``.
+"""
+
+import base64
+import json
+import os
+import ssl
+import sys
+from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
+from typing import Any, Dict, List, Optional
+
+GPU_RESOURCE = "amd.com/gpu"
+OPT_OUT = "amd.com/rccl-env-inject"
+MARK = "amd.com/rccl-env"
+VOLUME = "tk-node-rccl-env"
+NODE_DIR = "/etc/rccl"
+ENV_FILE_VAR = "TK_RCCL_ENV_FILE"
+
+
+def _esc(key: str) -> str:
+    """JSON-pointer escaping of one path segment (RFC 6901)."""
+    return key.replace("~", "~0").replace("/", "~1")
+
+
+def _wants_gpu(container: Dict[str, Any]) -> bool:
+    res = container.get("resources") or {}
+    for part in ("limits", "requests"):
+        v = (res.get(part) or {}).get(GPU_RESOURCE)
+        if v is not None:
+            try:
+                if int(str(v)) > 0:
+                    return True
+            except ValueError:
+                return True  # a quantity we cannot parse still asks for GPUs
+    return False
+
+
+def load_env(env_dir: str) -> Dict[str, str]:
+    """A ConfigMap mounted as a directory: one file per key (``..data`` links skipped)."""
+    out: Dict[str, str] = {}
+    if not env_dir or not os.path.isdir(env_dir):
+        return out
+    for name in sorted(os.listdir(env_dir)):
+        path = os.path.join(env_dir, name)
+        if name.startswith(".") or not os.path.isfile(path):
+            continue
+        with open(path, "r", encoding="utf-8") as fh:
+            out[name] = fh.read()
+    return out
+
+
+def patch_for_pod(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
+    """RFC 6902 operations that inject ``env`` into ``pod``'s GPU containers ([] = none)."""
+    meta = pod.get("metadata") or {}
+    annotations = meta.get("annotations") or {}
+    if str(annotations.get(OPT_OUT, "")).lower() == "false" or annotations.get(MARK) == "injected":
+        return []
+    spec = pod.get("spec") or {}
+    ops: List[Dict[str, Any]] = []
+    touched = False
+    for kind in ("initContainers", "containers"):
+        for i, c in enumerate(spec.get(kind) or []):
+            if not _wants_gpu(c):
+                continue
+            touched = True
+            have = {e.get("name") for e in (c.get("env") or [])}
+            add = [{"name": k, "value": v} for k, v in sorted(env.items()) if k not in have]
+            if ENV_FILE_VAR not in have:
+                add.append({"name": ENV_FILE_VAR, "value": f"{NODE_DIR}/rccl.env"})
+            base = f"/spec/{kind}/{i}"
+            if add:
+                if c.get("env"):
+                    ops += [{"op": "add", "path": f"{base}/env/-", "value": e} for e in add]
+                else:
+                    ops.append({"op": "add", "path": f"{base}/env", "value": add})
+            mounts = c.get("volumeMounts") or []
+            if not any(m.get("mountPath") == NODE_DIR for m in mounts):
+                m = {"name": VOLUME, "mountPath": NODE_DIR, "readOnly": True}
+                if mounts:
+                    ops.append({"op": "add", "path": f"{base}/volumeMounts/-", "value": m})
+                else:
+                    ops.append({"op": "add", "path": f"{base}/volumeMounts", "value": [m]})
+    if not touched:
+        return []
+    vol = {"name": VOLUME, "hostPath": {"path": NODE_DIR, "type": "DirectoryOrCreate"}}
+    if not any(v.get("name") == VOLUME for v in spec.get("volumes") or []):
+        if spec.get("volumes"):
+            ops.append({"op": "add", "path": "/spec/volumes/-", "value": vol})
+        else:
+            ops.append({"op": "add", "path": "/spec/volumes", "value": [vol]})
+    if meta.get("annotations"):
+        ops.append({"op": "add", "path": f"/metadata/annotations/{_esc(MARK)}", "value": "injected"})
+    else:
+        ops.append({"op": "add", "path": "/metadata/annotations", "value": {MARK: "injected"}})
+    return ops
+
+
+def review(doc: Dict[str, Any], env: Dict[str, str]) -> Dict[str, Any]:
+    """admission.k8s.io/v1 AdmissionReview in -> AdmissionReview response out.  Never
+    denies: a pod the injector cannot parse is admitted unchanged."""
+    req = doc.get("request") or {}
+    resp: Dict[str, Any] = {"uid": req.get("uid", ""), "allowed": True}
+    obj = req.get("object")
+    if isinstance(obj, dict) and (req.get("kind") or {}).get("kind", "Pod") == "Pod":
+        ops = patch_for_pod(obj, env)
+        if ops:
+            resp["patchType"] = "JSONPatch"
+            resp["patch"] = base64.b64encode(json.dumps(ops).encode()).decode()
+    return {"apiVersion": doc.get("apiVersion", "admission.k8s.io/v1"), "kind": "AdmissionReview",
+            "response": resp}
+
+
+def apply_patch(obj: Dict[str, Any], ops: List[Dict[str, Any]]) -> Dict[str, Any]:
+    """Apply ``add`` operations (the only kind :func:`patch_for_pod` emits) -- the API
+    server's side, for tests and the fake Rancher's admission chain."""
+    out = json.loads(json.dumps(obj))
+    for op in ops:
+        if op["op"] != "add":
+            raise ValueError(f"unsupported op {op['op']}")
+        parts = [p.replace("~1", "/").replace("~0", "~") for p in op["path"].lstrip("/").split("/")]
+        cur: Any = out
+        for p in parts[:-1]:
+            cur = cur[int(p)] if isinstance(cur, list) else cur.setdefault(p, {})
+        last = parts[-1]
+        if isinstance(cur, list):
+            if last == "-":
+                cur.append(op["value"])
+            else:
+                cur.insert(int(last), op["value"])
+        else:
+            cur[last] = op["value"]
+    return out
+
+
+def make_server(port: int, env_dir: str, certfile: str = "", keyfile: str = "",
+                host: str = "0.0.0.0") -> ThreadingHTTPServer:
+    class H(BaseHTTPRequestHandler):
+        protocol_version = "HTTP/1.1"
+
+        def log_message(self, *args):
+            pass
+
+        def _reply(self, code: int, body: bytes, ctype: str = "application/json"):
+            self.send_response(code)
+            self.send_header("Content-Type", ctype)
+            self.send_header("Content-Length", str(len(body)))
+            self.end_headers()
+            self.wfile.write(body)
+
+        def do_GET(self):
+            if self.path in ("/healthz", "/readyz"):
+                return self._reply(200, b"ok", "text/plain")
+            return self._reply(404, b"{}")
+
+        def do_POST(self):
+            if not self.path.startswith("/mutate"):
+                return self._reply(404, b"{}")
+            n = int(self.headers.get("Content-Length") or 0)
+            try:
+                doc = json.loads(self.rfile.read(n) or b"{}")
+                out = review(doc, load_env(env_dir))
+            except ValueError as exc:
+                return self._reply(400, json.dumps({"error": str(exc)}).encode())
+            return self._reply(200, json.dumps(out).encode())
+
+    srv = ThreadingHTTPServer((host, port), H)
+    srv.daemon_threads = True
+    if certfile:
+        ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+        ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+        ctx.load_cert_chain(certfile, keyfile)
+        srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
+    return srv
+
+
+def main(argv: Optional[List[str]] = None) -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(prog="rccl-env-injector")
+    ap.add_argument("--port", type=int, default=8443)
+    ap.add_argument("--cert", default="/tls/tls.crt")
+    ap.add_argument("--key", default="/tls/tls.key")
+    ap.add_argument("--env-dir", default="/etc/rccl-env")
+    args = ap.parse_args(argv)
+    srv = make_server(args.port, args.env_dir, args.cert, args.key)
+    print(json.dumps({"listening": args.port, "env_keys": sorted(load_env(args.env_dir))}), flush=True)
+    srv.serve_forever()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

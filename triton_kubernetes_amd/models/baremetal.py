@@ -20,6 +20,7 @@ from typing import Dict, List
 from ..config.context import Context, expand_home, file_exists, not_blank
 from ..errors import ConfigError
 from ..state import MANAGER_KEY, State, cluster_key_parts
+from .. import versions
 from ..parallel.rccl_env import default_rccl_env
 from .common import add_nodes, base_cluster_config, base_manager_config, base_node_config, omit_empty, source_for
 
@@ -74,13 +75,18 @@ def add_mi355x_addons(ctx: Context, state: State, cluster: str, name: str) -> st
         "rancher_access_key": f"${{module.{MANAGER_KEY}.rancher_access_key}}",
         "rancher_secret_key": f"${{module.{MANAGER_KEY}.rancher_secret_key}}",
         "rancher_cluster_id": f"${{module.{cluster}.rancher_cluster_id}}",
-        "device_plugin_image": s.get_string("device_plugin_image") or "rocm/k8s-device-plugin:latest",
-        "node_labeller_image": s.get_string("node_labeller_image") or "rocm/k8s-device-plugin:labeller-latest",
-        "rccl_probe_image": s.get_string("rccl_probe_image") or "",
+        # pinned tags (versions.py), never :latest
+        "device_plugin_image": s.get_string("device_plugin_image") or versions.DEVICE_PLUGIN_IMAGE,
+        "node_labeller_image": (s.get_string("node_labeller_image") if s.is_set("node_labeller_image")
+                                else versions.NODE_LABELLER_IMAGE),
+        "rccl_probe_image": s.get_string("rccl_probe_image") or versions.RCCL_PROBE_IMAGE,
+        "webhook_image": s.get_string("webhook_image") or versions.WEBHOOK_IMAGE,
         "rccl_gate": "true" if s.get_bool("rccl_gate") or not s.is_set("rccl_gate") else "false",
+        "rccl_env_injector": ("true" if not s.is_set("rccl_env_injector") or s.get_bool("rccl_env_injector")
+                              else "false"),
     }
     key = addons_key(name)
-    state.set_module(key, omit_empty(addon, ["rccl_probe_image"]))
+    state.set_module(key, addon)
     return key
 
 

@@ -571,7 +571,9 @@ class NodeAgent:
 
         self._server = http.server.ThreadingHTTPServer((host, port), H)
         self._server.daemon_threads = True
-        threading.Thread(target=self._server.serve_forever, name=f"agent-{self.name}", daemon=True).start()
+        # short poll: stop() (server.shutdown) returns within ~20 ms instead of the default 0.5 s
+        threading.Thread(target=self._server.serve_forever, kwargs={"poll_interval": 0.02},
+                         name=f"agent-{self.name}", daemon=True).start()
         h, p = self._server.server_address[:2]
         return f"http://{h}:{p}"
 
@@ -609,6 +611,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--devices", default="", help="comma-separated local GPU indices")
     ap.add_argument("--token-file", default="", help="file holding the shared agent token")
     ap.add_argument("--root", default="/")
+    ap.add_argument("--name", default="", help="agent name (defaults to the listen host)")
+    ap.add_argument("--synthetic-gpus", type=int, default=0,
+                    help="tests / CPU dry runs only: a synthetic MI355X topology with this many GPUs, "
+                         "no burn-in kernels, no RCCL")
     args = ap.parse_args(argv)
     token = ""
     if args.token_file:
@@ -616,7 +622,20 @@ def main(argv: Optional[List[str]] = None) -> int:
             token = fh.read().strip()
     host, _, port = args.listen.rpartition(":")
     devices = [int(d) for d in args.devices.split(",") if d.strip()]
-    agent = NodeAgent(name=host, mode=args.mode, devices=devices, root=args.root, token=token)
+    agent = NodeAgent(name=args.name or host, mode=args.mode, devices=devices, root=args.root, token=token)
+    if args.synthetic_gpus > 0:
+        from .labels import synthetic_topology
+
+        agent.topology_override = synthetic_topology(args.synthetic_gpus)
+        agent.burnin_override = lambda dev, level: {"ok": True, "simulated": True, "level": level}
+
+    import signal
+
+    def _term(signum, frame):  # a supervisor's SIGTERM takes the same clean path as ^C (once)
+        signal.signal(signal.SIGTERM, signal.SIG_IGN)
+        raise KeyboardInterrupt
+
+    signal.signal(signal.SIGTERM, _term)
     url = agent.serve(host or "127.0.0.1", int(port))
     import gc
 

@@ -20,16 +20,24 @@ real server does after agents register:
 * ``/k8s/clusters/<id>/...`` proxy: ``api/v1/nodes`` (labels, conditions,
   allocatable) and a generic object store for applied manifests.  GPU nodes
   advertise ``amd.com/gpu`` allocatable only once a DaemonSet whose name
-  contains ``device-plugin`` has been applied — as with the real ROCm plugin.
+  contains ``device-plugin`` has been applied — as with the real ROCm plugin;
+* mutating admission: a Pod created through the proxy goes through every applied
+  ``MutatingWebhookConfiguration`` whose rules and namespace selector match — the
+  webhook is called over HTTPS, its certificate verified against the ``caBundle``
+  for ``<service>.<namespace>.svc`` (``service_endpoints`` maps a service to the
+  address it really listens on), and the returned JSONPatch is applied;
+  ``failurePolicy: Fail`` turns a webhook error into a rejected create.
 
 Everything is in memory and thread-safe; it serves plain HTTP on 127.0.0.1.
 """
 
 import base64
+import http.client
 import http.server
 import json
 import secrets
 import socket
+import ssl
 import threading
 import time
 import urllib.parse
@@ -75,6 +83,9 @@ class FakeRancher:
         pw = bootstrap_password if bootstrap_password is not None else secrets.token_hex(16)
         self.state = _State(rke_seconds, node_ready_seconds, pw,
                             list(k8s_versions) if k8s_versions is not None else [v for _, v in K8S_VERSIONS])
+        # "<service>.<namespace>" -> "https://127.0.0.1:<port>" (where an in-cluster
+        # webhook service of a test really listens)
+        self.service_endpoints: Dict[str, str] = {}
         self._server = http.server.ThreadingHTTPServer((host, port), self._handler())
         self._server.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
@@ -348,6 +359,9 @@ class FakeRancher:
             return self._k8s(method, path, body)
         return 404, {"type": "error", "code": "NotFound", "path": path}
 
+    def _admit(self, cid: str, namespace: str, pod: Dict[str, Any]) -> Dict[str, Any]:
+        return _admit_pod(self, cid, namespace, pod)
+
     def _register(self, h) -> Tuple[int, Any]:
         st = self.state
         token = h.headers.get("X-API-Tunnel-Token", "")
@@ -392,6 +406,12 @@ class FakeRancher:
             major, minor = v.lstrip("v").split(".")[:2]
             return 200, {"major": major, "minor": minor, "gitVersion": v.split("-")[0]}
         if method == "POST":
+            parts = kpath.strip("/").split("/")
+            if len(parts) == 5 and parts[:3] == ["api", "v1", "namespaces"] and parts[4] == "pods":
+                try:
+                    body = self._admit(cid, parts[3], body)
+                except _Rejected as exc:
+                    return 400, {"kind": "Status", "reason": "BadRequest", "code": 400, "message": str(exc)}
             name = (body.get("metadata") or {}).get("name", uuid.uuid4().hex[:6])
             key = f"{cid}|{kpath}|{name}"
             with st.mu:
@@ -425,6 +445,86 @@ class FakeRancher:
                 items = [st.objects[k] for k in st.cluster_objects.get(cid, ()) if k.startswith(prefix)]
                 return 200, {"items": items}
         return 404, {"kind": "Status", "code": 404}
+
+
+class _Rejected(Exception):
+    pass
+
+
+def _ns_selected(selector: Dict[str, Any], namespace: str) -> bool:
+    """namespaceSelector on the ``kubernetes.io/metadata.name`` label (all the fake knows)."""
+    labels = {"kubernetes.io/metadata.name": namespace}
+    for k, v in (selector.get("matchLabels") or {}).items():
+        if labels.get(k) != v:
+            return False
+    for e in selector.get("matchExpressions") or []:
+        have = labels.get(e.get("key"))
+        op, vals = e.get("operator"), e.get("values") or []
+        if (op == "In" and have not in vals) or (op == "NotIn" and have in vals) \
+                or (op == "Exists" and have is None) or (op == "DoesNotExist" and have is not None):
+            return False
+    return True
+
+
+def _rule_matches(rule: Dict[str, Any]) -> bool:
+    def has(key: str, want: str) -> bool:
+        vals = rule.get(key) or []
+        return "*" in vals or want in vals
+
+    return has("operations", "CREATE") and has("apiGroups", "") and has("apiVersions", "v1") \
+        and has("resources", "pods")
+
+
+def _call_webhook(fake: "FakeRancher", hook: Dict[str, Any], review: Dict[str, Any]) -> Dict[str, Any]:
+    cc = hook.get("clientConfig") or {}
+    svc = cc.get("service") or {}
+    base = fake.service_endpoints.get(f"{svc.get('name')}.{svc.get('namespace')}")
+    if base is None:
+        raise ConnectionError(f"service {svc.get('name')}.{svc.get('namespace')} has no endpoints")
+    u = urllib.parse.urlsplit(base)
+    ctx = ssl.create_default_context(cadata=base64.b64decode(cc.get("caBundle", "")).decode())
+    raw = socket.create_connection((u.hostname, u.port), timeout=float(hook.get("timeoutSeconds", 10)))
+    conn = http.client.HTTPConnection(u.hostname, u.port)
+    conn.sock = ctx.wrap_socket(raw, server_hostname=f"{svc['name']}.{svc['namespace']}.svc")
+    try:
+        data = json.dumps(review).encode()
+        conn.request("POST", svc.get("path", "/"), body=data, headers={"Content-Type": "application/json"})
+        resp = conn.getresponse()
+        out = resp.read()
+        if resp.status != 200:
+            raise ConnectionError(f"webhook HTTP {resp.status}")
+        return json.loads(out)
+    finally:
+        conn.close()
+
+
+def _admit_pod(fake: "FakeRancher", cid: str, namespace: str, pod: Dict[str, Any]) -> Dict[str, Any]:
+    from ..k8s.webhook import apply_patch
+
+    st = fake.state
+    prefix = f"{cid}|/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations|"
+    with st.mu:
+        configs = [st.objects[k] for k in st.cluster_objects.get(cid, ()) if k.startswith(prefix)]
+    for cfg in configs:
+        for hook in cfg.get("webhooks") or []:
+            if not any(_rule_matches(r) for r in hook.get("rules") or []):
+                continue
+            if not _ns_selected(hook.get("namespaceSelector") or {}, namespace):
+                continue
+            review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
+                      "request": {"uid": str(uuid.uuid4()), "kind": {"group": "", "version": "v1", "kind": "Pod"},
+                                  "operation": "CREATE", "namespace": namespace, "object": pod}}
+            try:
+                resp = _call_webhook(fake, hook, review).get("response") or {}
+            except (OSError, ValueError, ssl.SSLError) as exc:
+                if hook.get("failurePolicy", "Fail") == "Fail":
+                    raise _Rejected(f"failed calling webhook {hook.get('name')}: {exc}") from exc
+                continue
+            if not resp.get("allowed", False):
+                raise _Rejected(f"admission webhook {hook.get('name')} denied the request")
+            if resp.get("patch"):
+                pod = apply_patch(pod, json.loads(base64.b64decode(resp["patch"])))
+    return pod
 
 
 def tunnel_params(hostname: str, roles: Dict[str, bool], labels: Dict[str, str],

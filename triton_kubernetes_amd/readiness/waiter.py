@@ -165,6 +165,14 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
     return client, spec
 
 
+def gate_sizes(settings) -> List[int]:
+    """RCCL gate message sizes: 1 MiB and ``rccl_gate_max_mib`` (default 64 MiB)."""
+    mib = int(float(settings.get_string("rccl_gate_max_mib") or 64)) if settings.is_set("rccl_gate_max_mib") else 64
+    if mib < 1:
+        raise TKError(f"rccl_gate_max_mib must be >= 1. Found '{mib}'.")
+    return sorted({1 << 20, mib << 20})
+
+
 def agent_transport_for(ctx) -> Any:
     transport = ctx.extras.get("agent_transport")
     if transport is None:
@@ -184,8 +192,7 @@ def early_gate(ctx, state, cluster_key: str) -> Any:
         return None
     from .gate import ClusterGate
 
-    spec_sizes = ReadinessSpec("", []).rccl_sizes
-    gate = ClusterGate.from_state(state, cluster_key, agent_transport_for(ctx), spec_sizes)
+    gate = ClusterGate.from_state(state, cluster_key, agent_transport_for(ctx), gate_sizes(s))
     return gate.prepare_async() if gate is not None else None
 
 
@@ -194,6 +201,7 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
     s = ctx.settings
     timeout = float(s.get_string("wait_timeout") or 3600)
     client, spec = spec_from_state(state, backend, cluster_key, timeout, s.get_bool("rccl_gate"))
+    spec.rccl_sizes = gate_sizes(s)
     transport = agent_transport_for(ctx) if spec.rccl_gate else None
     if gate is not None and (not spec.rccl_gate or gate.world != sum(spec.rccl_ndev or [1] * len(spec.rccl_hosts))):
         gate.abort()  # membership changed since it was prepared
@@ -206,4 +214,4 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
 
 
 __all__ = ["ReadinessSpec", "ReadinessReport", "wait_ready", "rccl_gate", "spec_from_state", "wait_after_create",
-           "early_gate", "agent_transport_for"]
+           "early_gate", "agent_transport_for", "gate_sizes"]

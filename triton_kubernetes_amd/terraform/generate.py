@@ -28,7 +28,6 @@ import sys
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
-from ..k8s.manifests import device_plugin_daemonset, labeller_daemonset, rccl_configmap, NAMESPACE
 from .. import versions
 from . import scripts
 from .catalog import MODULES_DIR
@@ -51,6 +50,7 @@ PROVIDERS = {
     "vsphere": ('vsphere = {\n      source  = "hashicorp/vsphere"\n      version = ">= 2.0"\n    }',
                 'provider "vsphere" {\n  user                 = var.vsphere_user\n  password             = var.vsphere_password\n  vsphere_server       = var.vsphere_server\n  allow_unverified_ssl = true\n}'),
     "external": ('external = {\n      source  = "hashicorp/external"\n      version = ">= 2.0"\n    }', ""),
+    "tls": ('tls = {\n      source  = "hashicorp/tls"\n      version = ">= 4.0"\n    }', ""),
 }
 
 
@@ -1240,34 +1240,93 @@ data "external" "gpu_labels" {{
          "src/tk_gemm_screen.hip": os.path.join(CSRC, "tk_gemm_screen.hip"),
          "src/tk_rccl_probe.hip": os.path.join(CSRC, "tk_rccl_probe.hip")}))
 
-    # MI355X cluster add-ons
-    manifests = {
-        "10-device-plugin.json": {"path": f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
-                                  "object": device_plugin_daemonset("${DEVICE_PLUGIN_IMAGE}")},
-        "20-rccl-env.json": {"path": f"/api/v1/namespaces/{NAMESPACE}/configmaps", "object": rccl_configmap()},
-        "30-node-labeller.json": {"path": f"/apis/apps/v1/namespaces/{NAMESPACE}/daemonsets",
-                                  "object": labeller_daemonset("${NODE_LABELLER_IMAGE}")},
-    }
+    # MI355X cluster add-ons: one template per object from k8s/addons.py (the DirectExecutor
+    # renders these same files), filtered by group, then applied through Rancher's k8s proxy
+    from ..k8s import addons as addon_defs
+
+    templates = addon_defs.addon_templates()
     files = {"apply_addons.sh": scripts.APPLY_ADDONS}
-    for fname, doc in manifests.items():
-        files[f"manifests/{fname}.tftpl"] = json.dumps(doc, indent=2).replace("${DEVICE_PLUGIN_IMAGE}",
-                                                                              "${device_plugin_image}") \
-            .replace("${NODE_LABELLER_IMAGE}", "${node_labeller_image}")
-    mods.append(Module("rancher-k8s-mi355x-addons", ["external"], [
+    for obj in templates:
+        files[f"manifests/{obj.file}.tftpl"] = addon_defs.template_text(obj)
+    group_of = "\n".join(f'    {json.dumps(o.file)} = {json.dumps(o.group)}' for o in templates)
+    tvars = "\n".join(f"      {v} = local.values.{v}" for v in addon_defs.TEMPLATE_VARS)
+    mods.append(Module("rancher-k8s-mi355x-addons", ["external", "tls"], [
         Var("name", None), Var("rancher_api_url", None), Var("rancher_access_key", None),
         Var("rancher_secret_key", None, sensitive=True), Var("rancher_cluster_id", None),
         Var("device_plugin_image", versions.DEVICE_PLUGIN_IMAGE),
-        Var("node_labeller_image", versions.NODE_LABELLER_IMAGE),
-        Var("rccl_probe_image", ""), Var("rccl_gate", "true")],
+        Var("node_labeller_image", versions.NODE_LABELLER_IMAGE,
+            "Node labeller image (empty: no labeller DaemonSet or its RBAC)."),
+        Var("rccl_probe_image", versions.RCCL_PROBE_IMAGE,
+            "Image of the node-level rccl-ready Job (runs the node's installed tools)."),
+        Var("webhook_image", versions.WEBHOOK_IMAGE, "Python image running the RCCL-env injector webhook."),
+        Var("rccl_gate", "true", "Apply the rccl-ready Job (true/false)."),
+        Var("rccl_env_injector", "true",
+            "Inject the rccl-env values into every pod requesting amd.com/gpu (mutating webhook; true/false).")],
         '''locals {
   manifest_dir = "${path.root}/.tk-addons-${var.name}"
+  # group of every manifest file (k8s/addons.py) and whether the group is on
+  group_of = {
+''' + group_of + '''
+  }
+  enabled = {
+    base  = true
+    label = var.node_labeller_image != ""
+    env   = var.rccl_env_injector == "true"
+    gate  = var.rccl_gate == "true"
+  }
+  values = {
+    device_plugin_image = var.device_plugin_image
+    node_labeller_image = var.node_labeller_image
+    rccl_probe_image    = var.rccl_probe_image
+    webhook_image       = var.webhook_image
+    injector_ca_b64     = base64encode(tls_self_signed_cert.injector_ca.cert_pem)
+    injector_cert_b64   = base64encode(tls_locally_signed_cert.injector.cert_pem)
+    injector_key_b64    = base64encode(tls_private_key.injector.private_key_pem)
+  }
   manifests = {
     for f in fileset("${path.module}/files/manifests", "*.tftpl") :
     trimsuffix(f, ".tftpl") => templatefile("${path.module}/files/manifests/${f}", {
-      device_plugin_image = var.device_plugin_image
-      node_labeller_image = var.node_labeller_image
-    })
+''' + tvars + '''
+    }) if local.enabled[lookup(local.group_of, trimsuffix(f, ".tftpl"), "base")]
   }
+}
+
+# serving certificate of the RCCL-env injector (the API server verifies it against caBundle)
+resource "tls_private_key" "injector_ca" {
+  algorithm   = "ECDSA"
+  ecdsa_curve = "P256"
+}
+
+resource "tls_self_signed_cert" "injector_ca" {
+  private_key_pem       = tls_private_key.injector_ca.private_key_pem
+  is_ca_certificate     = true
+  validity_period_hours = 87600
+  allowed_uses          = ["cert_signing", "crl_signing"]
+  subject {
+    common_name = "rccl-env-injector-ca"
+  }
+}
+
+resource "tls_private_key" "injector" {
+  algorithm   = "ECDSA"
+  ecdsa_curve = "P256"
+}
+
+resource "tls_cert_request" "injector" {
+  private_key_pem = tls_private_key.injector.private_key_pem
+  dns_names = ["rccl-env-injector", "rccl-env-injector.kube-system", "rccl-env-injector.kube-system.svc",
+  "rccl-env-injector.kube-system.svc.cluster.local"]
+  subject {
+    common_name = "rccl-env-injector.kube-system.svc"
+  }
+}
+
+resource "tls_locally_signed_cert" "injector" {
+  cert_request_pem      = tls_cert_request.injector.cert_request_pem
+  ca_private_key_pem    = tls_private_key.injector_ca.private_key_pem
+  ca_cert_pem           = tls_self_signed_cert.injector_ca.cert_pem
+  validity_period_hours = 87600
+  allowed_uses          = ["digital_signature", "key_encipherment", "server_auth"]
 }
 
 resource "terraform_data" "apply_addons" {
@@ -1275,7 +1334,7 @@ resource "terraform_data" "apply_addons" {
   input            = length(local.manifests)
   provisioner "local-exec" {
     command = <<-EOT
-      mkdir -p "${local.manifest_dir}"
+      rm -rf "${local.manifest_dir}" && mkdir -p "${local.manifest_dir}"
       %{for name, body in local.manifests~}
       printf '%s' '${replace(body, "'", "'\\\\''")}' > "${local.manifest_dir}/${name}"
       %{endfor~}

@@ -31,19 +31,31 @@ variable "device_plugin_image" {
 }
 
 variable "node_labeller_image" {
-  description = "Node labeller image."
+  description = "Node labeller image (empty: no labeller DaemonSet or its RBAC)."
   type        = string
   default     = "rocm/k8s-device-plugin:labeller-1.31.0.6"
 }
 
 variable "rccl_probe_image" {
-  description = "Rccl probe image."
+  description = "Image of the node-level rccl-ready Job (runs the node's installed tools)."
   type        = string
-  default     = ""
+  default     = "ubuntu:22.04"
+}
+
+variable "webhook_image" {
+  description = "Python image running the RCCL-env injector webhook."
+  type        = string
+  default     = "python:3.11-slim"
 }
 
 variable "rccl_gate" {
-  description = "Rccl gate."
+  description = "Apply the rccl-ready Job (true/false)."
+  type        = string
+  default     = "true"
+}
+
+variable "rccl_env_injector" {
+  description = "Inject the rccl-env values into every pod requesting amd.com/gpu (mutating webhook; true/false)."
   type        = string
   default     = "true"
 }

@@ -5,5 +5,9 @@ terraform {
       source  = "hashicorp/external"
       version = ">= 2.0"
     }
+    tls = {
+      source  = "hashicorp/tls"
+      version = ">= 4.0"
+    }
   }
 }
