@@ -80,6 +80,8 @@ class AgentProc:
     """One node agent in its own process (what systemd runs on a real node)."""
 
     def __init__(self, name: str, devices, token_file: str, root: str, synthetic: int = 0):
+        with open(token_file, "r", encoding="utf-8") as fh:
+            self.token = fh.read().strip()
         argv = [sys.executable, "-u", "-m", "triton_kubernetes_amd.node.agent", "--mode", "sim",
                 "--listen", "127.0.0.1:0", "--name", name, "--token-file", token_file, "--root", root,
                 "--devices", ",".join(str(d) for d in devices)]
@@ -111,9 +113,19 @@ class AgentProc:
         return self.url
 
     def signal_stop(self) -> None:
-        if self.proc.poll() is None and not self.signalled:
+        """Ask the agent to stop (its API; a signal if that fails)."""
+        if self.proc.poll() is not None or self.signalled:
+            return
+        self.signalled = True
+        import urllib.request
+
+        try:
+            req = urllib.request.Request(self.url + "/v1/shutdown", data=b"{}", method="POST",
+                                         headers={"X-TK-Agent-Token": self.token,
+                                                  "Content-Type": "application/json"})
+            urllib.request.urlopen(req, timeout=10).read()
+        except OSError:
             self.proc.send_signal(signal.SIGTERM)
-            self.signalled = True
 
     def stop(self, timeout: float = 120.0) -> int:
         if self.proc.poll() is None:

@@ -8,7 +8,7 @@ export PYTHONPATH="$GRAFT_REPO_ROOT"
 LOG="$GRAFT_REPO_ROOT/gpurun_out/check.log"
 : > $LOG
 step() {  # step <name> <seconds> <cmd...>
-  local name=$1 secs=$2; shift 2
+  local name=$1 secs=$2; shift 2  # env assignments before "step" apply to the command
   local t0=$(date +%s%N)
   timeout -k 10 "$secs" "$@" > "$GRAFT_REPO_ROOT/gpurun_out/$name.log" 2>&1
   local rc=$?
@@ -31,4 +31,12 @@ fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
   step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --warm-steps 0
+fi
+if [ "$MODE" = coldinit ]; then
+  step rccl_cold_init 600 python scripts/rccl_cold_init.py
+fi
+if [ "$MODE" = ab ]; then
+  step bench_preload 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --report gpurun_out/bench_preload.json
+  TK_RCCL_PRELOAD=0 step bench_nopreload 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
+  step bench_preload2 300 python bench.py --steps 5 --warmup 1 --warm-steps 2
 fi

@@ -1,0 +1,95 @@
+"""Cluster RCCL gate for nodes without agents: ``rccl-ready --cluster`` per node over the
+host transport (``readiness/process_gate.py``), with the CPU stand-in of the tool."""
+
+import os
+import shutil
+import stat
+import sys
+import time
+
+import pytest
+
+from triton_kubernetes_amd.errors import TKError
+from triton_kubernetes_amd.parallel.transport import HostRef, LocalTransport
+from triton_kubernetes_amd.rancher.client import RancherClient
+from triton_kubernetes_amd.rancher.fake import FakeRancher, tunnel_params
+from triton_kubernetes_amd.readiness.process_gate import ProcessGate, gate_script
+from triton_kubernetes_amd.readiness.waiter import ReadinessSpec, wait_ready
+
+FIXTURE = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "fake_rccl_ready.py")
+
+
+@pytest.fixture
+def tools(tmp_path):
+    d = tmp_path / "bin"
+    d.mkdir()
+    exe = d / "rccl-ready"
+    exe.write_text(f"#!/bin/sh\nexec {sys.executable} {FIXTURE} \"$@\"\n")
+    exe.chmod(exe.stat().st_mode | stat.S_IEXEC)
+    env = tmp_path / "rccl.env"
+    env.write_text('NCCL_IB_HCA="=mlx5_0:1"\n')
+    return str(d), str(env)
+
+
+def _gate(tools, n=3, gpus=8, env=None, timeout=60.0):
+    d, env_file = tools
+    hosts = [HostRef("local") for _ in range(n)]
+    return ProcessGate(LocalTransport(env=env), hosts, [gpus] * n, [1 << 20, 64 << 20], iters=5, timeout=timeout,
+                       tools_dir=d, env_file=env_file)
+
+
+def test_process_gate_one_communicator_over_every_node(tools):
+    res = _gate(tools).run()
+    assert res["ok"] and res["world"] == 24 and res["nodes"] == 3 and res["mode"] == "process"
+    assert [r["rank_base"] for r in res["ranks"]] == [0, 8, 16]
+    assert all(r["world"] == 24 and r["rc"] == 0 for r in res["ranks"])
+    assert res["min_peak_busbw_gbps"] == 100.0
+    # each node's /etc/rccl/rccl.env was sourced before the tool ran
+    assert {r["env"] for r in res["ranks"]} == {"=mlx5_0:1"}
+
+
+def test_process_gate_fails_fast_when_a_node_fails(tools):
+    t0 = time.monotonic()
+    with pytest.raises(TKError, match="exited 2"):
+        _gate(tools, env={"FAKE_RCCL_FAIL_BASE": "8"}, timeout=60).run()
+    assert time.monotonic() - t0 < 20  # not the deadline: the others were killed
+
+
+def test_process_gate_deadline_without_unique_id(tools):
+    with pytest.raises(TKError, match="no unique id"):
+        _gate(tools, n=2, env={"FAKE_RCCL_NO_UID": "1"}, timeout=1.5).run()
+
+
+def test_gate_script_shape():
+    s = gate_script("/opt/triton-kubernetes/bin", 16, 8, 8, [1 << 20, 256 << 20], 5, "ab" * 128)
+    assert s.startswith("set -a; [ -r /etc/rccl/rccl.env ] && . /etc/rccl/rccl.env; set +a; exec ")
+    assert "--cluster --world 16 --rank-base 8 --ngpus 8 --max-mib 256 --iters 5" in s and "--uid abab" in s
+    assert "--uid-out" in gate_script("/x", 8, 0, 8, [1 << 20], 5, None)
+
+
+def test_waiter_runs_process_gate_for_ssh_nodes(tools):
+    fake = FakeRancher(bootstrap_password="b00tstrap-only").start()
+    try:
+        client = RancherClient(fake.url)
+        outs = client.bootstrap("n3w-passw0rd-123", fake.url, "b00tstrap-only", timeout=10)
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        info = client.ensure_cluster("ssh-gpu")
+        from triton_kubernetes_amd.cloud.http import HTTPClient
+
+        for host, roles in (("cp", {"etcd": True, "controlplane": True}), ("g1", {"worker": True}),
+                            ("g2", {"worker": True})):
+            HTTPClient(base_url=fake.url).request("POST", "/v3/connect/register", data=b"{}", headers={
+                "X-API-Tunnel-Token": info.registration_token,
+                "X-API-Tunnel-Params": tunnel_params(host, roles, {}, {})})
+        spec = ReadinessSpec(info.cluster_id, ["cp", "g1", "g2"], timeout=30, rccl_gate=True,
+                             rccl_process_hosts=[HostRef("local"), HostRef("local")], rccl_process_ndev=[8, 8])
+        rep = wait_ready(client, spec, host_transport=LocalTransport(), tools_dir=tools[0])
+        assert rep.rccl["ok"] and rep.rccl["world"] == 16 and "rccl_gate" in rep.phases
+        # no GPU nodes: the report says the gate was skipped, and why
+        spec2 = ReadinessSpec(info.cluster_id, ["cp"], timeout=10, rccl_gate=False,
+                              rccl_skip_reason="no MI355X nodes in the cluster")
+        rep2 = wait_ready(client, spec2)
+        assert rep2.rccl == {"ok": None, "skipped": "no MI355X nodes in the cluster"}
+        assert "rccl_gate" not in rep2.phases
+    finally:
+        fake.stop()

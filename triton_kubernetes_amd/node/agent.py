@@ -27,7 +27,8 @@ node-level RCCL sweep (N2).
 HTTP API (JSON): ``GET /v1/info``, ``POST /v1/plan``, ``POST /v1/rccl-uid``,
 ``POST /v1/rccl-prepare`` (without a ``uid``: host the rendezvous and return it; start this node's ranks of the cluster-wide RCCL
 communicator, non-blocking), ``POST /v1/rccl-gate`` (run them: verified
-all-reduce sweep), ``POST /v1/rccl-abort``, ``POST /v1/cleanup``.
+all-reduce sweep), ``POST /v1/rccl-abort``, ``POST /v1/cleanup``, ``POST /v1/shutdown``
+(the daemon stops and exits).
 """
 
 import base64
@@ -129,6 +130,7 @@ class NodeAgent:
         self.last_labels: Dict[str, str] = {}
         self.history: List[Dict[str, Any]] = []
         self._server: Optional[http.server.ThreadingHTTPServer] = None
+        self.shutdown_requested = threading.Event()
 
     # --- files ---------------------------------------------------------------------------
     def path(self, p: str) -> str:
@@ -565,6 +567,11 @@ class NodeAgent:
                     if path == "/v1/cleanup":
                         agent.last_labels = {}
                         return self._reply(200, {"ok": True})
+                    if path == "/v1/shutdown":
+                        # the daemon's main loop (main()) stops the agent and exits; an
+                        # embedded agent (no main loop) ignores it
+                        agent.shutdown_requested.set()
+                        return self._reply(200, {"ok": True})
                 except Exception as exc:  # noqa: BLE001
                     return self._reply(500, {"error": f"{type(exc).__name__}: {exc}"})
                 return self._reply(404, {"error": "not found"})
@@ -630,28 +637,32 @@ def main(argv: Optional[List[str]] = None) -> int:
         agent.burnin_override = lambda dev, level: {"ok": True, "simulated": True, "level": level}
 
     import signal
+    import sys
 
-    def _term(signum, frame):  # a supervisor's SIGTERM takes the same clean path as ^C (once)
-        signal.signal(signal.SIGTERM, signal.SIG_IGN)
-        raise KeyboardInterrupt
-
-    signal.signal(signal.SIGTERM, _term)
+    # SIGTERM / SIGINT / POST /v1/shutdown all take the same path: stop() (gates aborted,
+    # communicator teardowns drained, arena released), then a prompt exit
+    signal.signal(signal.SIGTERM, lambda *_: agent.shutdown_requested.set())
+    signal.signal(signal.SIGINT, lambda *_: agent.shutdown_requested.set())
     url = agent.serve(host or "127.0.0.1", int(port))
     import gc
 
     gc.collect()
     gc.freeze()  # long-lived daemon: keep startup objects out of every later collection
     print(json.dumps({"listening": url, "token_from_file": bool(token)}), flush=True)
-    try:
-        while True:
-            time.sleep(3600)
-    except KeyboardInterrupt:
-        agent.stop()
+    while not agent.shutdown_requested.wait(3600):
+        pass
+    t0 = time.perf_counter()
+    agent.stop()
+    print(json.dumps({"stopped": True, "stop_ms": round((time.perf_counter() - t0) * 1e3, 1)}), flush=True)
+    sys.stdout.flush()
+    sys.stderr.flush()
     if getattr(agent, "_used_rccl", False):
         from ..ops import rccl
 
-        if rccl.abandoned_inits():
-            rccl.exit_now(0)  # an init blocked on absent peers would hang the normal exit
+        # every communicator was torn down by stop(); an init blocked on absent peers
+        # would hang a normal exit, and the HIP runtime's own teardown adds nothing the
+        # kernel driver does not do at process exit
+        rccl.exit_now(0)
     return 0
 
 

@@ -659,19 +659,113 @@ extern "C" int tkr_sweep_local(int ndev, const size_t* sizes, int nsizes, int it
 }
 
 #ifdef TK_RCCL_MAIN
+// Cluster mode (one process per node, all its GPUs): the cluster-wide gate for nodes that
+// have no node agent (SSH / Terraform delivery; readiness/ssh_gate.py fans it out).
+//   rank-0 node:  rccl-ready --cluster --world W --rank-base 0 --ngpus n --uid-out
+//                 prints {"uid":"<256 hex>"} at once, then joins as ranks 0..n-1;
+//   other nodes:  rccl-ready --cluster --world W --rank-base B --ngpus n --uid <hex>.
+// Every process then runs the same verified all-reduce sweep (the agents' gate schedule:
+// 1 MiB and --max-mib, warmup 2) and prints one JSON result line.
+static int hexval(char c) {
+  if (c >= '0' && c <= '9') return c - '0';
+  if (c >= 'a' && c <= 'f') return c - 'a' + 10;
+  if (c >= 'A' && c <= 'F') return c - 'A' + 10;
+  return -1;
+}
+
+static int cluster_main(int world, int rank_base, int ndev, const char* uid_hex, bool uid_out, int max_mib,
+                        int iters, int dtype, double min_busbw, double timeout_s) {
+  unsigned char uid[NCCL_UNIQUE_ID_BYTES];
+  if (uid_out) {
+    if (tkr_unique_id(uid) != 0) {
+      fprintf(stderr, "{\"error\":\"ncclGetUniqueId: %s\"}\n", g_err);
+      return 2;
+    }
+    printf("{\"uid\":\"");
+    for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; ++i) printf("%02x", uid[i]);
+    printf("\"}\n");
+    fflush(stdout);
+  } else {
+    if (!uid_hex || strlen(uid_hex) != 2 * NCCL_UNIQUE_ID_BYTES) {
+      fprintf(stderr, "{\"error\":\"--uid needs %d hex digits\"}\n", 2 * NCCL_UNIQUE_ID_BYTES);
+      return 2;
+    }
+    for (int i = 0; i < NCCL_UNIQUE_ID_BYTES; ++i) {
+      const int hi = hexval(uid_hex[2 * i]), lo = hexval(uid_hex[2 * i + 1]);
+      if (hi < 0 || lo < 0) { fprintf(stderr, "{\"error\":\"bad --uid\"}\n"); return 2; }
+      uid[i] = (unsigned char)(hi * 16 + lo);
+    }
+  }
+  std::vector<int> devs(ndev);
+  for (int d = 0; d < ndev; ++d) devs[d] = d;
+  std::vector<size_t> sizes{1u << 20};
+  if ((size_t)max_mib << 20 > sizes[0]) sizes.push_back((size_t)max_mib << 20);
+  const int n = (int)sizes.size();
+  const size_t max_bytes = sizes[n - 1];
+  const int h = tkr_gate_begin_ex(uid, world, rank_base, ndev, devs.data(), /*blocking=*/0, max_bytes);
+  if (h < 0) {
+    fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
+    return 2;
+  }
+  std::vector<double> t(n), alg(n), bus(n), err(n);
+  double ph[5] = {0, 0, 0, 0, 0};
+  const int rc = tkr_gate_sweep(h, sizes.data(), n, iters, 2, dtype, timeout_s * 1e3, t.data(), alg.data(),
+                                bus.data(), err.data(), ph);
+  if (rc) {
+    fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
+    printf("{\"ok\":false,\"world\":%d,\"rank_base\":%d,\"ngpus\":%d,\"error\":\"sweep failed\"}\n", world,
+           rank_base, ndev);
+    return 2;
+  }
+  double errs = 0;
+  printf("{\"world\":%d,\"rank_base\":%d,\"ngpus\":%d,\"dtype\":\"%s\",\"init_ms\":%.1f,\"results\":[", world,
+         rank_base, ndev, dtype ? "bf16" : "f32", ph[4]);
+  for (int i = 0; i < n; ++i) {
+    errs += err[i];
+    printf("%s{\"bytes\":%zu,\"time_us\":%.2f,\"algbw_gbps\":%.2f,\"busbw_gbps\":%.2f,\"errors\":%.0f}", i ? "," : "",
+           sizes[i], t[i], alg[i], bus[i], err[i]);
+  }
+  const bool ok = errs == 0 && bus[n - 1] >= min_busbw;
+  printf("],\"ok\":%s}\n", ok ? "true" : "false");
+  fflush(stdout);
+  tkr_drain();
+  return ok ? 0 : 1;
+}
+
 int main(int argc, char** argv) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
     fprintf(stderr, "{\"error\":\"no HIP devices\"}\n");
     return 3;
   }
-  double min_busbw = 0.0;
-  int iters = 20, warmup = 5, dtype = 0;
+  double min_busbw = 0.0, timeout_s = 600.0;
+  int iters = 20, warmup = 5, dtype = 0, world = 0, rank_base = 0, max_mib = 64;
+  bool cluster = false, uid_out = false;
+  const char* uid_hex = nullptr;
+  const int visible = ndev;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--min-busbw") && i + 1 < argc) min_busbw = atof(argv[++i]);
     else if (!strcmp(argv[i], "--iters") && i + 1 < argc) iters = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--ngpus") && i + 1 < argc) ndev = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--bf16")) dtype = 1;
+    else if (!strcmp(argv[i], "--cluster")) cluster = true;
+    else if (!strcmp(argv[i], "--world") && i + 1 < argc) world = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--rank-base") && i + 1 < argc) rank_base = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--uid") && i + 1 < argc) uid_hex = argv[++i];
+    else if (!strcmp(argv[i], "--uid-out")) uid_out = true;
+    else if (!strcmp(argv[i], "--max-mib") && i + 1 < argc) max_mib = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--timeout-s") && i + 1 < argc) timeout_s = atof(argv[++i]);
+  }
+  if (ndev < 1 || ndev > visible) {
+    fprintf(stderr, "{\"error\":\"--ngpus %d but %d visible\"}\n", ndev, visible);
+    return 3;
+  }
+  if (cluster) {
+    if (world < ndev || rank_base < 0 || rank_base + ndev > world || (!uid_out && !uid_hex) || max_mib < 1) {
+      fprintf(stderr, "{\"error\":\"cluster mode needs --world >= --rank-base + --ngpus and --uid or --uid-out\"}\n");
+      return 2;
+    }
+    return cluster_main(world, rank_base, ndev, uid_hex, uid_out, max_mib, iters, dtype, min_busbw, timeout_s);
   }
   std::vector<size_t> sizes;
   for (size_t b = 1u << 20; b <= (1ull << 30); b <<= 2) sizes.push_back(b);

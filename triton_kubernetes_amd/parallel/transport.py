@@ -63,6 +63,12 @@ class Transport:
     def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
         raise NotImplementedError
 
+    def spawn(self, host: HostRef, script: str) -> subprocess.Popen:
+        """Start ``bash -c script`` on the host and return at once; stdout is a text pipe the
+        caller reads while it runs (the process-mode RCCL gate needs rank 0's first line
+        before the other nodes can start)."""
+        raise NotImplementedError
+
 
 def _shell_result(plan: BootstrapPlan, output: str, rc: int, ms: float, err: str = "") -> Dict[str, Any]:
     markers = parse_step_markers(output + "\n" + err)
@@ -126,6 +132,10 @@ class SSHTransport(Transport):
             raise ExecutorError(f"scp {local_path} -> {host.address}:{remote_path}: {proc.stderr[-500:]}")
         self.run_script(host, f"chmod {mode:o} {shlex.quote(remote_path)}\n")
 
+    def spawn(self, host: HostRef, script: str) -> subprocess.Popen:
+        return subprocess.Popen(self.ssh_argv(host, "bash -c " + shlex.quote(script)), stdin=subprocess.DEVNULL,
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
+
 
 class LocalTransport(Transport):
     """Runs scripts with the local ``bash`` (development / single-box)."""
@@ -158,6 +168,10 @@ class LocalTransport(Transport):
         with open(local_path, "rb") as src, open(remote_path, "wb") as dst:
             dst.write(src.read())
         os.chmod(remote_path, mode)
+
+    def spawn(self, host: HostRef, script: str) -> subprocess.Popen:
+        return subprocess.Popen(["bash", "-c", script], stdin=subprocess.DEVNULL, stdout=subprocess.PIPE,
+                                stderr=subprocess.PIPE, text=True, env=self._env())
 
 
 class AgentTransport(Transport):
@@ -252,3 +266,6 @@ class TransportRouter(Transport):
 
     def put_file(self, host, local_path, remote_path, mode=0o755):
         return self.for_host(host).put_file(host, local_path, remote_path, mode)
+
+    def spawn(self, host, script):
+        return self.for_host(host).spawn(host, script)

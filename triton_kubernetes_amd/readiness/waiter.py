@@ -9,9 +9,12 @@ Phases, each time-stamped (the BASELINE.json metric is ``ready - start``):
 3. ``gpus_allocatable`` every MI355X node advertises ``amd.com/gpu`` equal to its
                         expected count (device plugin up);
 4. ``rccl_gate``        optional: one RCCL all-reduce sweep across every GPU of
-                        the GPU nodes (N2), run by the node agents as one
-                        communicator (``gate.py``; its init may already have been
-                        started, pipelined with the node bootstrap).
+                        the GPU nodes (N2) as one communicator -- run by the node
+                        agents (``gate.py``; its init may already have been started,
+                        pipelined with the node bootstrap) or, for nodes delivered
+                        over SSH / Terraform, by one ``rccl-ready --cluster``
+                        process per node (``process_gate.py``).  When the gate
+                        cannot run the report says why (``rccl.skipped``).
 
 Polling is adaptive (20 ms doubling to 1 s), not the reference's fixed 5 s.
 """
@@ -37,6 +40,10 @@ class ReadinessSpec:
     rccl_ndev: List[int] = field(default_factory=list)  # GPUs per rccl_hosts entry (default 1 each)
     rccl_sizes: List[int] = field(default_factory=lambda: [1 << 20, 64 << 20])
     rccl_iters: int = 5
+    # GPU nodes without an agent: (HostRef, GPU count), gated by rccl-ready processes
+    rccl_process_hosts: List[Any] = field(default_factory=list)
+    rccl_process_ndev: List[int] = field(default_factory=list)
+    rccl_skip_reason: str = ""
 
 
 @dataclass
@@ -65,7 +72,8 @@ def _node_ready(item: Dict[str, Any]) -> bool:
 
 
 def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float] = None,
-               agent_transport: Any = None, gate: Any = None) -> ReadinessReport:
+               agent_transport: Any = None, gate: Any = None, host_transport: Any = None,
+               tools_dir: Optional[str] = None) -> ReadinessReport:
     rep = ReadinessReport(start=start if start is not None else time.time())
     deadline = rep.start + spec.timeout
 
@@ -115,6 +123,18 @@ def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float
                                spec.rccl_sizes, spec.rccl_iters)
         with span("ready.rccl_gate", world=gate.world, nodes=len(gate.members)):
             rep.rccl = gate.run()
+    elif spec.rccl_gate and spec.rccl_process_hosts:
+        from ..node.plan import TOOLS_DIR
+        from ..parallel.transport import TransportRouter
+        from .process_gate import ProcessGate
+
+        pgate = ProcessGate(host_transport or TransportRouter(), spec.rccl_process_hosts, spec.rccl_process_ndev,
+                            spec.rccl_sizes, spec.rccl_iters, timeout=left(), tools_dir=tools_dir or TOOLS_DIR)
+        with span("ready.rccl_gate", world=pgate.world, nodes=len(spec.rccl_process_hosts), mode="process"):
+            rep.rccl = pgate.run()
+    elif spec.rccl_skip_reason:
+        rep.rccl = {"ok": None, "skipped": spec.rccl_skip_reason}
+    if rep.rccl is not None and "skipped" not in rep.rccl:
         if not rep.rccl.get("ok"):
             raise TKError(f"RCCL readiness gate failed: {rep.rccl}")
         rep.phases["rccl_gate"] = time.time()
@@ -147,9 +167,13 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
 
     # amd.com/gpu only appears once the device plugin runs, i.e. with the add-on module
     has_plugin = state.module(addons_key(cluster_key_parts(cluster_key)[1])) is not None
+    from ..parallel.transport import HostRef
+
     gpu_nodes: Dict[str, int] = {}
     rccl_hosts: List[str] = []
     rccl_ndev: List[int] = []
+    proc_hosts: List[HostRef] = []
+    proc_ndev: List[int] = []
     for host in sorted(nodes):
         cfg = state.module(nodes[host]) or {}
         info = module_from_source(str(cfg.get("source", "")))
@@ -157,11 +181,26 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
             if has_plugin:
                 gpu_nodes[host] = int(cfg.get("gpu_count", 8))
             addr = str(cfg.get("host", ""))
+            n = int(cfg.get("gpu_count", 8) or 8)
             if addr.startswith("agent+"):
                 rccl_hosts.append(addr[len("agent+"):])
-                rccl_ndev.append(int(cfg.get("gpu_count", 8) or 8))
+                rccl_ndev.append(n)
+            elif addr:
+                proc_hosts.append(HostRef(addr, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
+                                          cfg.get("bastion_host") or ""))
+                proc_ndev.append(n)
+    skip = ""
+    if rccl_gate:
+        if rccl_hosts and proc_hosts:
+            # one communicator cannot yet span agent-held and process-held ranks
+            skip = (f"mixed delivery: {len(rccl_hosts)} agent and {len(proc_hosts)} SSH/Terraform MI355X "
+                    "nodes; gate each kind with a cluster of its own")
+            rccl_hosts, rccl_ndev, proc_hosts, proc_ndev = [], [], [], []
+        elif not (rccl_hosts or proc_hosts):
+            skip = "no MI355X nodes in the cluster"
     spec = ReadinessSpec(cl["rancher_cluster_id"], sorted(nodes), gpu_nodes, timeout,
-                         rccl_gate and bool(rccl_hosts), rccl_hosts, rccl_ndev)
+                         rccl_gate and bool(rccl_hosts or proc_hosts), rccl_hosts, rccl_ndev,
+                         rccl_process_hosts=proc_hosts, rccl_process_ndev=proc_ndev, rccl_skip_reason=skip)
     return client, spec
 
 
@@ -202,11 +241,13 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
     timeout = float(s.get_string("wait_timeout") or 3600)
     client, spec = spec_from_state(state, backend, cluster_key, timeout, s.get_bool("rccl_gate"))
     spec.rccl_sizes = gate_sizes(s)
-    transport = agent_transport_for(ctx) if spec.rccl_gate else None
-    if gate is not None and (not spec.rccl_gate or gate.world != sum(spec.rccl_ndev or [1] * len(spec.rccl_hosts))):
+    transport = agent_transport_for(ctx) if spec.rccl_gate and spec.rccl_hosts else None
+    if gate is not None and (not spec.rccl_hosts or gate.world != sum(spec.rccl_ndev or [1] * len(spec.rccl_hosts))):
         gate.abort()  # membership changed since it was prepared
         gate = None
-    rep = wait_ready(client, spec, start=start, agent_transport=transport, gate=gate)
+    rep = wait_ready(client, spec, start=start, agent_transport=transport, gate=gate,
+                     host_transport=ctx.extras.get("transport"),
+                     tools_dir=s.get_string("node_tools_dir") or None)
     ctx.extras["last_readiness"] = rep  # callers that time phases (bench.py) read it here
     ctx.echo(f"cluster ready in {rep.ready_seconds:.2f}s: " +
              json.dumps(rep.to_json()["phase_seconds"], sort_keys=True))
