@@ -180,6 +180,9 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     calls = log.read_text()
     assert "hostnamectl set-hostname gpu-tf-1" in calls
     assert "--token regtok --ca-checksum cafe --worker --label amd.com/" in calls
+    # the burn-in's coverage travels with the node
+    assert "--label amd.com/gpu.burnin-level=quick" in calls and "--label amd.com/gpu.burnin=passed" in calls
+    assert "--label amd.com/gpu.burnin-hbm-tested-gib=1" in calls
 
 
 def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch):

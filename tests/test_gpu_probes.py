@@ -66,6 +66,24 @@ def test_burnin_quick(probe):
     assert res.ok, res.failures
 
 
+def test_memtest_span_covers_most_of_hbm(probe):
+    """The full burn-in's memtest: every free byte but the headroom, distinct chunks held
+    at once (~270 GiB of the 288 GiB card), clean."""
+    res = probe.memtest_span(0, 0, chunk=32 << 30, headroom=8 << 30, passes=1)
+    print(json.dumps(res))
+    assert res["errors"] == 0
+    assert res["hbm_bytes"] > 250 << 30 and res["bytes"] > 0.85 * res["hbm_bytes"]
+
+
+def test_burnin_labels_record_coverage(probe):
+    from triton_kubernetes_amd.node.labels import burnin_labels
+
+    res = probe.run_burnin(0, "quick").to_json()
+    labels = burnin_labels("quick", {0: res})
+    assert labels["amd.com/gpu.burnin"] == "passed" and labels["amd.com/gpu.burnin-level"] == "quick"
+    assert labels["amd.com/gpu.burnin-hbm-tested-gib"] == "1" and float(labels["amd.com/gpu.burnin-hbm-tested-pct"]) < 1
+
+
 def test_burnin_arena_resident_across_runs(probe):
     probe.release_scratch()  # the arena is process-wide: start from an empty one
     held = probe.prealloc_scratch(0, "quick")
@@ -100,6 +118,28 @@ def test_rccl_ready_executable():
     assert proc.returncode == 0, proc.stderr
     doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
     assert doc["ok"] and doc["ngpus"] == 1
+
+
+def test_rccl_ready_cluster_mode_through_process_gate(tmp_path):
+    """The SSH/Terraform nodes' cluster gate with the real tool: rank-0 node prints the
+    unique id, joins, runs the verified sweep (1 node x 1 GPU here; the protocol is the
+    same for N nodes)."""
+    import os
+
+    from triton_kubernetes_amd.ops.native import LIB_DIR
+    from triton_kubernetes_amd.parallel.transport import HostRef, LocalTransport
+    from triton_kubernetes_amd.readiness.process_gate import ProcessGate
+
+    env_file = tmp_path / "rccl.env"
+    env_file.write_text('NCCL_DEBUG="WARN"\n')
+    gate = ProcessGate(LocalTransport(), [HostRef("local")], [1], [1 << 20, 16 << 20], iters=3, timeout=240,
+                       tools_dir=LIB_DIR, env_file=str(env_file))
+    res = gate.run()
+    assert res["ok"] and res["world"] == 1 and res["mode"] == "process", res
+    rank = res["ranks"][0]
+    assert rank["rc"] == 0 and [r["bytes"] for r in rank["results"]] == [1 << 20, 16 << 20]
+    assert all(r["errors"] == 0 for r in rank["results"]) and rank["init_ms"] > 0
+    assert os.path.exists(os.path.join(LIB_DIR, "rccl-ready"))
 
 
 def test_topology_amdsmi():

@@ -281,3 +281,27 @@ def test_step_markers_name_steps_whose_bodies_assign_variables(tmp_path):
     assert proc.returncode == 0, proc.stderr
     steps = parse_step_markers(proc.stdout)
     assert list(steps) == ["clobber", "after"] and all(v["status"] == "ok" for v in steps.values())
+
+
+def test_burnin_labels_formatting():
+    from triton_kubernetes_amd.node.labels import burnin_labels
+
+    gib = 1 << 30
+    res = {0: {"ok": True, "memtest": {"bytes": 280 * gib, "hbm_bytes": 288 * gib}},
+           1: {"ok": True, "memtest": {"bytes": 276 * gib, "hbm_bytes": 288 * gib}}}
+    assert burnin_labels("full", res) == {"amd.com/gpu.burnin": "passed", "amd.com/gpu.burnin-level": "full",
+                                          "amd.com/gpu.burnin-hbm-tested-gib": "276",
+                                          "amd.com/gpu.burnin-hbm-tested-pct": "95.8"}
+    res[1]["ok"] = False
+    assert burnin_labels("full", res)["amd.com/gpu.burnin"] == "failed"
+    assert burnin_labels("quick", {})["amd.com/gpu.burnin"] == "failed"
+
+
+def test_shell_plan_carries_burnin_labels():
+    from triton_kubernetes_amd.node.plan import BURNIN_LABEL_FILE, build_host_plan
+
+    cfg = {"hostname": "g", "rancher_host_labels": {"worker": "true"}, "gpu_count": 8, "gpu_burnin": "full"}
+    script = build_host_plan(cfg, "https://r", "tok", "ca", mi355x=True).render_shell()
+    assert "gpu-burnin --all --level full --labels /tmp/tk-burnin-labels" in script
+    assert f"sudo rm -f {BURNIN_LABEL_FILE}" in script
+    assert f"[ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}" in script

@@ -53,7 +53,7 @@ from ..parallel.rccl_env import render_env_file, site_env_from_topology
 from ..rancher.fake import tunnel_params
 from ..utils import procstat
 from ..utils.trace import span
-from .labels import labels_from_topology
+from .labels import burnin_labels, labels_from_topology
 from .plan import BootstrapPlan, Step
 
 MODES = ("sim", "exec")
@@ -248,6 +248,8 @@ class NodeAgent:
                 if not res.get("ok", False):
                     raise StepFailed(step.name, f"GPU {dev}: {res.get('failures')}")
             ctx["capacity"]["amd.com/gpu"] = len(self.devices)
+            # what the burn-in covered travels with the node (level, HBM held by the memtest)
+            ctx["labels"].update(burnin_labels(level, results))
             return out
         if a == "rccl_env":
             # discovered inter-node settings, then the configured values (which win)

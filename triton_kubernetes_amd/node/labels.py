@@ -116,6 +116,22 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     return labels
 
 
+def burnin_labels(level: str, results: Dict[Any, Dict[str, Any]]) -> Dict[str, str]:
+    """Node labels that say what the burn-in covered (same keys and formatting as
+    ``gpu-burnin --labels``, the SSH / Terraform path): pass/fail, the level, and the HBM
+    the memtest held -- the minimum over the node's GPUs, in GiB and percent of the card.
+    ``quick`` memtests 1 GiB (0.3 % of 288 GiB); ``full`` every free byte but 4 GiB."""
+    ok = all(r.get("ok", False) for r in results.values()) if results else False
+    tested = [int((r.get("memtest") or {}).get("bytes", 0)) for r in results.values()]
+    total = [int((r.get("memtest") or {}).get("hbm_bytes", 0)) for r in results.values()]
+    lo = min(tested) if tested else 0
+    frac = min((t / h for t, h in zip(tested, total) if h), default=0.0)
+    return {"amd.com/gpu.burnin": "passed" if ok else "failed",
+            "amd.com/gpu.burnin-level": level,
+            "amd.com/gpu.burnin-hbm-tested-gib": f"{lo / (1 << 30):.0f}",
+            "amd.com/gpu.burnin-hbm-tested-pct": f"{100.0 * frac:.1f}"}
+
+
 def agent_label_flags(labels: Dict[str, str]) -> List[str]:
     """``--label k=v`` arguments for ``rancher/agent``."""
     out: List[str] = []

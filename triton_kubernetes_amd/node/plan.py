@@ -40,6 +40,7 @@ from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
 from .manager import docker_install_lines
 
 LABEL_FILE = "/etc/triton-kubernetes/gpu-labels"
+BURNIN_LABEL_FILE = "/etc/triton-kubernetes/gpu-burnin-labels"
 TOPOLOGY_FILE = "/etc/triton-kubernetes/gpu-topology.json"
 RCCL_ENV_FILE = "/etc/rccl/rccl.env"
 TOOLS_DIR = "/opt/triton-kubernetes/bin"
@@ -187,13 +188,15 @@ test -d /dev/dri || {{ echo '/dev/dri missing' >&2; exit 1; }}
 local found
 found=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
 [ "$found" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs, found $found render nodes" >&2; exit 1; }}
-sudo usermod -aG video,render "$(id -un)" || true""", {"count": ngpu}, gpu=True))
+sudo usermod -aG video,render "$(id -un)" || true
+sudo rm -f {BURNIN_LABEL_FILE}""", {"count": ngpu}, gpu=True))
         # burn-in before labels: the agent discovers the topology concurrently
         # with the burn-in kernels and only joins it at the labels step
         if burnin != "off":
             plan.steps.append(Step("gpu_burnin", "gpu_burnin", f"""
 sudo mkdir -p /etc/triton-kubernetes
-{TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} | sudo tee /etc/triton-kubernetes/gpu-burnin.json""",
+{TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
+sudo install -m 0644 /tmp/tk-burnin-labels {BURNIN_LABEL_FILE}""",
                                    {"level": burnin}, gpu=True))
         plan.steps.append(Step("gpu_labels", "gpu_labels", f"""
 sudo mkdir -p "$(dirname {LABEL_FILE})"
@@ -212,7 +215,8 @@ TK_RCCL_EOF
                                    f"{TOOLS_DIR}/rccl-ready --ngpus {ngpu} --min-busbw "
                                    f"{float(cfg.get('rccl_min_busbw', 0) or 0)}",
                                    {"count": ngpu}, gpu=True))
-        label_args = f' $(sed "s/^/--label /" {LABEL_FILE} | tr "\\n" " ")'
+        label_args = (f' $(cat {LABEL_FILE} $([ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}) '
+                      f'| sed "s/^/--label /" | tr "\\n" " ")')
     plan.steps.append(Step("agent", "agent", (
         f"sudo docker run -d --privileged --restart=unless-stopped --net=host "
         f"-v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run {_q(image)} "

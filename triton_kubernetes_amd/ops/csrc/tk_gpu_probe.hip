@@ -37,6 +37,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <vector>
 #include <algorithm>
 #include <vector>
 
@@ -727,6 +728,72 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
 
 // Test hook: corrupt `count` words of a filled buffer to prove the checker
 // detects errors (used by the numerics test, never by the probe itself).
+// Memtest over a SPAN of HBM: `bytes` (0: all free HBM minus `headroom` bytes) held as
+// chunks of `chunk` bytes, all allocated at once so they cover distinct physical memory,
+// each filled with a per-pass pattern and verified.  out: [0] mismatching words,
+// [1] verify GB/s (last chunk, last pass), [2] bytes tested, [3] device HBM bytes.
+// This is the `full` burn-in's memtest (round 1 tested a fixed 64 GiB of 288).
+extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t headroom, int passes, double* out) {
+  CHECK(hipSetDevice(dev));
+  size_t free_b = 0, total_b = 0;
+  CHECK(hipMemGetInfo(&free_b, &total_b));
+  if (bytes == 0) bytes = free_b > headroom ? free_b - headroom : 0;
+  if (chunk == 0) chunk = 16ull << 30;
+  chunk = chunk / sizeof(uint4) * sizeof(uint4);
+  std::vector<uint4*> chunks;
+  std::vector<size_t> sizes;
+  for (size_t done = 0; done < bytes && chunk > 0;) {
+    const size_t want = (bytes - done < chunk ? bytes - done : chunk) / sizeof(uint4) * sizeof(uint4);
+    if (want == 0) break;
+    uint4* p = nullptr;
+    if (hipMalloc(&p, want) != hipSuccess) {
+      (void)hipGetLastError();
+      break;  // fragmentation: test what could be held
+    }
+    chunks.push_back(p);
+    sizes.push_back(want);
+    done += want;
+  }
+  unsigned long long* err = nullptr;
+  CHECK(hipMalloc(&err, sizeof(unsigned long long)));
+  hipStream_t s;
+  CHECK(burnin_stream(&s));
+  CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), s));
+  hipEvent_t t0, t1;
+  CHECK(hipEventCreate(&t0));
+  CHECK(hipEventCreate(&t1));
+  const int grid = stream_grid(dev, 16);
+  float ms = 0.f;
+  size_t tested = 0;
+  for (size_t c = 0; c < chunks.size(); ++c) {
+    const size_t n = sizes[c] / sizeof(uint4);
+    for (int ps = 0; ps < (passes < 1 ? 1 : passes); ++ps) {
+      const uint32_t seed = 0x1234567u + 0x9e3779b9u * (uint32_t)ps + 0x85ebca6bu * (uint32_t)c;
+      k_mem_fill<<<grid, STREAM_THREADS, 0, s>>>(chunks[c], n, seed);
+      CHECK(hipEventRecord(t0, s));
+      k_mem_check<<<grid, STREAM_THREADS, 0, s>>>(chunks[c], n, seed, err);
+      CHECK(hipEventRecord(t1, s));
+    }
+    tested += sizes[c];
+  }
+  CHECK(hipEventSynchronize(t1));
+  CHECK(hipEventElapsedTime(&ms, t0, t1));
+  CHECK(hipGetLastError());
+  unsigned long long h = 0;
+  CHECK(hipMemcpyAsync(&h, err, sizeof(h), hipMemcpyDeviceToHost, s));
+  CHECK(hipStreamSynchronize(s));
+  out[0] = (double)h;
+  out[1] = sizes.empty() ? 0.0 : (double)sizes.back() / (ms * 1e-3) / 1e9;
+  out[2] = (double)tested;
+  out[3] = (double)total_b;
+  TRACED(hipEventDestroy(t0));
+  TRACED(hipEventDestroy(t1));
+  TRACED(hipStreamDestroy(s));
+  for (uint4* p : chunks) TRACED(hipFree(p));
+  TRACED(hipFree(err));
+  return 0;
+}
+
 extern "C" int tkp_memtest_selfcheck(int dev, size_t bytes, int corrupt, double* out) {
   CHECK(hipSetDevice(dev));
   const size_t n = bytes / sizeof(uint4);
@@ -819,6 +886,7 @@ extern "C" const char* tkg_last_error();
 int main(int argc, char** argv) {
   int dev = 0, all = 0;
   const char* level = "quick";
+  const char* labels_path = nullptr;  // --labels FILE: node labels recording what was tested
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
   for (int i = 1; i < argc; ++i) {
@@ -830,10 +898,12 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--min-fp8-tflops") && i + 1 < argc) min_fp8 = atof(argv[++i]);
     else if (!strcmp(argv[i], "--min-gemm-tflops") && i + 1 < argc) min_gemm = atof(argv[++i]);
     else if (!strcmp(argv[i], "--min-gemm-fp8-tflops") && i + 1 < argc) min_gemm8 = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--labels") && i + 1 < argc) labels_path = argv[++i];
   }
   const bool full = !strcmp(level, "full");
   const size_t hbm_bytes = full ? (16ull << 30) : (1ull << 30);
-  const size_t mt_bytes = full ? (64ull << 30) : (1ull << 30);
+  // quick: 1 GiB; full: every free byte of HBM but 4 GiB, in 16 GiB chunks held at once
+  const size_t mt_bytes = full ? 0 : (1ull << 30);
   const int mfma_iters = full ? 20000 : 2000;  // x MFMA_ACC (8) chains per wave
   const int gemm_n = full ? 8192 : 4096, gemm_reps = full ? 5 : 2;  // ops/gemm.py:SCREEN_SIZES
   int n = 0;
@@ -845,33 +915,46 @@ int main(int argc, char** argv) {
   if (all) for (int d = 0; d < n; ++d) devs.push_back(d);
   else devs.push_back(dev);
   bool ok_all = true;
+  double min_tested = -1.0, min_frac = -1.0;
   printf("{\"level\":\"%s\",\"gpus\":[", level);
   for (size_t k = 0; k < devs.size(); ++k) {
     const int d = devs[k];
     struct tkp_device_info info;
     memset(&info, 0, sizeof(info));
-    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[2] = {0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0},
+    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[4] = {0, 0, 0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0},
            gm8[7] = {0, 0, 0, 0, -1, -1, 0};
     bool ok = tkp_device_info(d, &info) == 0 && tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, hbm) == 0 &&
               tkp_mfma_peak(d, 0, mfma_iters, 3, 2, bf16) == 0 && tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, fp8) == 0 &&
               tkg_screen(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, gm) == 0 &&
               tkg_screen_fp8(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, gm8) == 0 &&
-              tkp_memtest(d, mt_bytes, full ? 3 : 1, mt) == 0;
+              tkp_memtest_span(d, mt_bytes, 16ull << 30, 4ull << 30, full ? 3 : 1, mt) == 0;
     if (!ok && tkg_last_error()[0] && !g_err[0]) snprintf(g_err, sizeof(g_err), "%s", tkg_last_error());
     const bool gemm_ok = gm[2] == 0.0 && gm[3] == 0.0, gemm8_ok = gm8[2] == 0.0 && gm8[3] == 0.0;
     const bool pass = ok && strncmp(info.arch, "gfx950", 6) == 0 && hbm[0] >= min_read && bf16[0] >= min_bf16 &&
                       fp8[0] >= min_fp8 && gemm_ok && gm[0] >= min_gemm && gemm8_ok && gm8[0] >= min_gemm8 &&
                       mt[0] == 0.0;
     ok_all = ok_all && pass;
+    if (min_tested < 0 || mt[2] < min_tested) min_tested = mt[2];
+    if (mt[3] > 0 && (min_frac < 0 || mt[2] / mt[3] < min_frac)) min_frac = mt[2] / mt[3];
     printf("%s{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"read_gbps\":%.1f,\"write_gbps\":%.1f,\"copy_gbps\":%.1f,"
            "\"bf16_tflops\":%.1f,\"fp8_tflops\":%.1f,\"gemm_tflops\":%.1f,\"gemm_checksum_ok\":%s,"
            "\"gemm_fp8_tflops\":%.1f,\"gemm_fp8_checksum_ok\":%s,"
-           "\"memtest_errors\":%.0f,\"ok\":%s%s%s%s}",
+           "\"memtest_errors\":%.0f,\"memtest_bytes\":%.0f,\"hbm_bytes\":%.0f,\"ok\":%s%s%s%s}",
            k ? "," : "", d, info.arch, info.compute_units, hbm[0], hbm[1], hbm[2], bf16[0], fp8[0], gm[0],
-           gemm_ok ? "true" : "false", gm8[0], gemm8_ok ? "true" : "false", mt[0],
+           gemm_ok ? "true" : "false", gm8[0], gemm8_ok ? "true" : "false", mt[0], mt[2], mt[3],
            pass ? "true" : "false", ok ? "" : ",\"error\":\"", ok ? "" : g_err, ok ? "" : "\"");
   }
   printf("],\"ok\":%s}\n", ok_all ? "true" : "false");
+  if (labels_path) {
+    // same keys and formatting as node/labels.py:burnin_labels (the agent path)
+    FILE* f = fopen(labels_path, "w");
+    if (!f) { fprintf(stderr, "cannot write %s\n", labels_path); return 2; }
+    fprintf(f, "amd.com/gpu.burnin=%s\n", ok_all ? "passed" : "failed");
+    fprintf(f, "amd.com/gpu.burnin-level=%s\n", level);
+    fprintf(f, "amd.com/gpu.burnin-hbm-tested-gib=%.0f\n", min_tested > 0 ? min_tested / (double)(1ull << 30) : 0.0);
+    fprintf(f, "amd.com/gpu.burnin-hbm-tested-pct=%.1f\n", min_frac > 0 ? 100.0 * min_frac : 0.0);
+    fclose(f);
+  }
   return ok_all ? 0 : 1;
 }
 #endif

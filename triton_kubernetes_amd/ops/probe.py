@@ -57,6 +57,8 @@ def _lib():
     lib.tkp_mfma_clock.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_double,
                                    ctypes.POINTER(ctypes.c_double)]
     lib.tkp_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_memtest_span.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
+                                      ctypes.POINTER(ctypes.c_double)]
     lib.tkp_memtest_selfcheck.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_double)]
     lib.tkp_p2p_bandwidth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
@@ -145,6 +147,15 @@ def memtest(dev: int, nbytes: int = 1 << 30, passes: int = 2) -> Dict[str, float
     return {"errors": int(out[0]), "verify_gbps": out[1]}
 
 
+def memtest_span(dev: int, nbytes: int = 0, chunk: int = 16 << 30, headroom: int = 4 << 30,
+                 passes: int = 1) -> Dict[str, float]:
+    """Memtest of ``nbytes`` of HBM (0: all free HBM but ``headroom``) held as ``chunk``-byte
+    allocations at once, so the whole span is distinct physical memory."""
+    out = (ctypes.c_double * 4)()
+    _check(_lib().tkp_memtest_span(dev, nbytes, chunk, headroom, passes, out), "memtest_span")
+    return {"errors": int(out[0]), "verify_gbps": out[1], "bytes": int(out[2]), "hbm_bytes": int(out[3])}
+
+
 def memtest_selfcheck(dev: int, nbytes: int, corrupt: int) -> int:
     out = (ctypes.c_double * 1)()
     _check(_lib().tkp_memtest_selfcheck(dev, nbytes, corrupt, out), "memtest_selfcheck")
@@ -160,8 +171,10 @@ def p2p_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 5) -
 # --- burn-in policy ------------------------------------------------------------------
 LEVELS = {
     # level: (hbm bytes, hbm iters, mfma iters (x 8 accumulator chains per wave), memtest bytes, memtest passes)
+    # memtest bytes 0 = every free byte of HBM but 4 GiB (memtest_span); quick tests 1 GiB
+    # (0.35 % of 288 GiB) -- the node labels say which (node/labels.py:burnin_labels)
     "quick": (1 << 30, 3, 2000, 1 << 30, 1),
-    "full": (16 << 30, 10, 20000, 64 << 30, 3),
+    "full": (16 << 30, 10, 20000, 0, 3),
 }
 
 
@@ -242,7 +255,11 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
         if g.tflops < frac * peak:
             res.failures.append(f"{name} {g.tflops:.0f} TF below {frac:.0%} of dense {dtype} peak")
     with span("burnin.memtest", dev=dev):
-        res.memtest = memtest(dev, mt_bytes, mt_passes)
+        if mt_bytes:
+            res.memtest = memtest(dev, mt_bytes, mt_passes)
+            res.memtest.update(bytes=mt_bytes, hbm_bytes=int(info.total_mem_gib * (1 << 30)))
+        else:
+            res.memtest = memtest_span(dev, 0, passes=mt_passes)
     if res.memtest["errors"]:
         res.failures.append(f"memtest: {res.memtest['errors']} mismatching words")
     return res
@@ -258,6 +275,7 @@ def prealloc_scratch(dev: int, level: str = "quick") -> int:
     if level not in LEVELS:
         return 0
     hbm_bytes, _, _, mt_bytes, _ = LEVELS[level]
+    mt_bytes = mt_bytes or (1 << 30)  # the span memtest allocates its own chunks
     lib = _lib()
     lib.tkp_set_scratch_cache(1)
     rc = lib.tkp_prealloc_scratch(dev, ctypes.c_size_t(hbm_bytes), ctypes.c_size_t(mt_bytes))

@@ -207,15 +207,18 @@ sudo usermod -aG video,render "$(id -un)" || true
 ROCM=$${ROCM_PATH:-/opt/rocm}
 build() { # name, compiler, flags...
   local name=$1; shift
-  [ -x "$T/$name" ] || sudo "$@" -o "$T/$name"
+  # (re)built when missing or older than any shipped source
+  { [ -x "$T/$name" ] && [ -z "$(find "$S/" -newer "$T/$name" -print -quit)" ]; } || sudo "$@" -o "$T/$name"
 }
 build amdgpu-topo-labeller g++ -O2 -std=c++17 -DTK_TOPO_MAIN -DTK_TOPO_AMDSMI -I$ROCM/include $S/tk_topo.cpp -L$ROCM/lib -lamd_smi -Wl,-rpath,$ROCM/lib
 build gpu-burnin $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip
 build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl
 $T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/dev/null
 $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
+sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels
 %{ if gpu_burnin != "off" ~}
-$T/gpu-burnin --all --level '${gpu_burnin}' | sudo tee /etc/triton-kubernetes/gpu-burnin.json
+$T/gpu-burnin --all --level '${gpu_burnin}' --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
+sudo install -m 0644 /tmp/tk-burnin-labels /etc/triton-kubernetes/gpu-burnin-labels
 %{ endif ~}
 { $T/amdgpu-topo-labeller --rccl-env || true; cat <<'TK_RCCL_EOF'
 ${rccl_env_file}
@@ -225,7 +228,7 @@ TK_RCCL_EOF
 set -a; . /etc/rccl/rccl.env; set +a
 $T/rccl-ready --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
 %{ endif ~}
-labels=$(sed 's/^/--label /' /etc/triton-kubernetes/gpu-labels | tr '\n' ' ')
+labels=$(cat /etc/triton-kubernetes/gpu-labels $([ -r /etc/triton-kubernetes/gpu-burnin-labels ] && echo /etc/triton-kubernetes/gpu-burnin-labels) | sed 's/^/--label /' | tr '\n' ' ')
 """ + DOCKER_INSTALL + r"""
 sudo hostnamectl set-hostname '${hostname}'
 %{ if rancher_registry_username != "" ~}
@@ -243,7 +246,7 @@ set -euo pipefail
 eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
 opts=(-o BatchMode=yes -o StrictHostKeyChecking=no -o UserKnownHostsFile=/dev/null -o LogLevel=ERROR -i "${key_path/#\~/$HOME}")
 if [ -n "${bastion_host:-}" ]; then opts+=(-J "$ssh_user@$bastion_host"); fi
-ssh "${opts[@]}" "$ssh_user@$host" 'cat /etc/triton-kubernetes/gpu-labels' | python3 -c '
+ssh "${opts[@]}" "$ssh_user@$host" 'cat /etc/triton-kubernetes/gpu-labels; cat /etc/triton-kubernetes/gpu-burnin-labels 2>/dev/null || true' | python3 -c '
 import json, sys
 labels = dict(l.strip().split("=", 1) for l in sys.stdin if "=" in l)
 print(json.dumps({"labels": json.dumps(labels, sort_keys=True)}))'
