@@ -5,7 +5,7 @@ PYTHON     ?= python3
 BUILD      := build
 PKG        := triton_kubernetes_amd
 
-.PHONY: all native modules test test-gpu sanitize bench smoke dist pyz wheel checksums clean
+.PHONY: all native modules test test-gpu sanitize bench smoke dist pyz wheel build-deb build-rpm packages checksums clean
 
 all: native test
 
@@ -48,10 +48,21 @@ pyz:
 wheel:
 	$(PYTHON) -m pip wheel --no-deps --no-build-isolation -w $(BUILD) .
 
-dist: pyz checksums
+# .deb / .rpm of the CLI and of the MI355X node tools, written with the stdlib
+# (reference: fpm build-rpm / build-deb, Makefile:43-79); also writes sha256-checksums.txt
+build-deb: native
+	$(PYTHON) -m $(PKG).release.build --out $(BUILD) --formats pyz,deb
+
+build-rpm: native
+	$(PYTHON) -m $(PKG).release.build --out $(BUILD) --formats pyz,rpm
+
+packages: native
+	$(PYTHON) -m $(PKG).release.build --out $(BUILD) --formats pyz,deb,rpm
+
+dist: packages
 
 checksums:
-	cd $(BUILD) && sha256sum triton-kubernetes-*.pyz $$(ls *.whl 2>/dev/null) > sha256-checksums.txt
+	cd $(BUILD) && sha256sum triton-kubernetes-*.pyz *.deb *.rpm $$(ls *.whl 2>/dev/null) > sha256-checksums.txt
 
 clean:
 	rm -rf $(BUILD) $(PKG)/ops/lib
