@@ -36,7 +36,9 @@ if [ "$MODE" = coldinit ]; then
   step rccl_cold_init 600 python scripts/rccl_cold_init.py
 fi
 if [ "$MODE" = ab ]; then
-  step bench_preload 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --report gpurun_out/bench_preload.json
-  TK_RCCL_PRELOAD=0 step bench_nopreload 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
-  step bench_preload2 300 python bench.py --steps 5 --warmup 1 --warm-steps 2
+  # A/B of the agent-start RCCL code load, alternating arms
+  step bench_early1 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --report gpurun_out/bench_early1.json
+  TK_RCCL_LOAD_EARLY=0 step bench_late1 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
+  step bench_early2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
+  TK_RCCL_LOAD_EARLY=0 step bench_late2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
 fi

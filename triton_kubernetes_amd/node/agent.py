@@ -264,9 +264,18 @@ class NodeAgent:
                 return {"simulated": True}
             from ..ops import rccl
 
-            res = rccl.sweep_local(len(self.devices))
+            # every local GPU as one communicator (grouped init), the verified sweep, and the
+            # ~0.5 s-per-communicator teardown off the plan (drained at stop)
+            self._used_rccl = True
+            sizes = list(rccl.DEFAULT_SIZES)
+            gate = rccl.GateComm(self._make_uid(), len(self.devices), 0, self.devices, blocking=True,
+                                 prealloc_bytes=max(sizes))
+            res = gate.sweep(sizes, iters=10, warmup=2, async_teardown=True)
+            floor = float(step.params.get("min_busbw", 0) or 0)
             if not res.ok:
                 raise StepFailed(step.name, "RCCL verification failed")
+            if floor and res.peak_busbw < floor:
+                raise StepFailed(step.name, f"RCCL busbw {res.peak_busbw:.0f} GB/s below {floor:.0f}")
             return res.to_json()
         if a == "agent":
             if plan.gpu is not None:

@@ -214,7 +214,8 @@ TK_RCCL_EOF
             plan.steps.append(Step("rccl_local", "rccl_local",
                                    f"{TOOLS_DIR}/rccl-ready --ngpus {ngpu} --min-busbw "
                                    f"{float(cfg.get('rccl_min_busbw', 0) or 0)}",
-                                   {"count": ngpu}, gpu=True))
+                                   {"count": ngpu, "min_busbw": float(cfg.get("rccl_min_busbw", 0) or 0)},
+                                   gpu=True))
         label_args = (f' $(cat {LABEL_FILE} $([ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}) '
                       f'| sed "s/^/--label /" | tr "\\n" " ")')
     plan.steps.append(Step("agent", "agent", (
