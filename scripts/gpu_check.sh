@@ -42,3 +42,6 @@ if [ "$MODE" = ab ]; then
   step bench_early2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
   TK_RCCL_LOAD_EARLY=0 step bench_late2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
 fi
+if [ "$MODE" = kload ]; then
+  step rccl_kernel_load 300 python scripts/rccl_kernel_load.py
+fi
