@@ -92,6 +92,7 @@ class AgentProc:
         self.proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=None, text=True, env=env,
                                      start_new_session=True)
         self.url = ""
+        self.runtime = ""
         self.signalled = False
 
     def wait_url(self, timeout: float = 300.0) -> str:
@@ -108,7 +109,9 @@ class AgentProc:
                 raise RuntimeError(f"agent {self.name} did not start within {timeout:.0f}s")
             line = self.proc.stdout.readline()
             if line.startswith("{"):
-                self.url = json.loads(line)["listening"]
+                doc = json.loads(line)
+                self.url = doc["listening"]
+                self.runtime = doc.get("hip_runtime", "")
         sel.close()
         return self.url
 
@@ -226,8 +229,11 @@ def main() -> int:
             procs.append(AgentProc("control-plane", [], token_file, os.path.join(work, tag, "cp")))
         return procs
 
+    runtimes = set()
+
     def gather_urls(procs):
         local = [(p.name, p.wait_url()) for p in procs]
+        runtimes.update(getattr(p, "runtime", "") or "in-process" for p in procs if p.name != "control-plane")
         if distributed:
             every = [None] * world
             dist.all_gather_object(every, local)
@@ -391,6 +397,8 @@ def main() -> int:
                 "rccl_gate_max_mib": args.rccl_mib,
                 "simulated_phases": list(SIMULATED_PHASES),
                 "rancher": versions.RANCHER_VERSION, "k8s_version": versions.DEFAULT_K8S_VERSION,
+                # HIP runtime + RCCL the GPU agents ran on (ops/native.py:select_runtime)
+                "agent_hip_runtime": sorted(runtimes),
             },
             "create_to_ready_s": ready,
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),

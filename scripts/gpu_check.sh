@@ -33,7 +33,14 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --warm-steps 0
 fi
 if [ "$MODE" = coldinit ]; then
-  step rccl_cold_init 600 python scripts/rccl_cold_init.py
+  step rccl_cold_init 600 python scripts/rccl_cold_init.py ${COLD_VARIANTS:-}
+fi
+if [ "$MODE" = runtime ]; then
+  # cold bench on the system ROCm runtime vs the PyTorch-ROCm bundled runtime, alternating
+  step bench_sys1 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
+  TK_HIP_RUNTIME=torch step bench_torch1 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
+  step bench_sys2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
+  TK_HIP_RUNTIME=torch step bench_torch2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
 fi
 if [ "$MODE" = ab ]; then
   # A/B of the agent-start RCCL code load, alternating arms

@@ -40,6 +40,9 @@ VARIANTS = {
     "no_smi": {"RCCL_USE_ROCM_SMI_LIB": "0"},
     "debug_init": {"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT"},
     "sampled": {"TK_SAMPLE": "1"},
+    "torch_runtime": {"TK_HIP_RUNTIME": "torch"},
+    "torch_runtime_all_off": {"TK_HIP_RUNTIME": "torch", "RCCL_MSCCL_ENABLE": "0", "RCCL_MSCCLPP_ENABLE": "0",
+                              "NCCL_NET_PLUGIN": "none"},
 }
 
 
@@ -84,7 +87,9 @@ def child() -> None:
     g2 = rccl.GateComm(rccl.unique_id(), 1, 0, [0], blocking=True)
     g2.sweep([1 << 20], iters=2, warmup=1, async_teardown=False)
     mark("init2")
-    doc = {"ms": t, "ok": res.ok}
+    from triton_kubernetes_amd.ops.native import runtime_dir
+
+    doc = {"ms": t, "ok": res.ok, "runtime": runtime_dir(), "rccl_version": rccl.version()}
     if out_path:
         doc["top"] = summarize(out_path)
     print(json.dumps(doc), flush=True)

@@ -1,8 +1,9 @@
 """Node agent: executes bootstrap plans on a host, in-process.
 
 ``tk-node-agent`` is the pull-side alternative to SSH delivery: it runs on a
-host (a systemd unit on real nodes, a thread per simulated node in tests and in
-``bench.py``) and executes :class:`~.plan.BootstrapPlan` steps natively.
+host (a systemd unit on real nodes; a fresh process per simulated node and step in
+``bench.py``; an in-process object in tests) and executes :class:`~.plan.BootstrapPlan`
+steps natively.
 
 Security model: the agent never executes shell text it receives.  A plan's
 ``shell`` fields are only for the SSH renderer; the agent dispatches on the
@@ -659,7 +660,10 @@ def main(argv: Optional[List[str]] = None) -> int:
 
     gc.collect()
     gc.freeze()  # long-lived daemon: keep startup objects out of every later collection
-    print(json.dumps({"listening": url, "token_from_file": bool(token)}), flush=True)
+    from ..ops import native
+
+    print(json.dumps({"listening": url, "token_from_file": bool(token),
+                      "hip_runtime": native._runtime_dir or "not loaded"}), flush=True)
     while not agent.shutdown_requested.wait(3600):
         pass
     t0 = time.perf_counter()

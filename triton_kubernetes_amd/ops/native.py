@@ -27,6 +27,74 @@ class NativeUnavailable(RuntimeError):
     pass
 
 
+_runtime_dir = None
+_RUNTIME_LIBS = ("libhsa-runtime64.so", "libamd_comgr.so", "libamdhip64.so", "librccl.so")
+
+
+def _torch_lib_dir() -> str:
+    import importlib.util
+
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.submodule_search_locations:
+        return ""
+    d = os.path.join(list(spec.submodule_search_locations)[0], "lib")
+    return d if os.path.exists(os.path.join(d, "librccl.so")) and os.path.exists(os.path.join(d, "libamdhip64.so")) \
+        else ""
+
+
+def select_runtime() -> str:
+    """The HIP runtime + RCCL directory this process will use (``TK_HIP_RUNTIME``), without
+    loading anything: ``"system"`` or a directory.
+
+    * ``auto`` (default): the builds bundled with an installed PyTorch-ROCm wheel (its
+      ``lib/``, found without importing torch) when present -- the runtime and RCCL that
+      ``torch.distributed`` jobs on the node use, and the one the GPU test-suite runs on
+      (tests import torch first) -- else ``/opt/rocm``;
+    * ``system``: ``/opt/rocm`` (the libraries' RUNPATH);
+    * ``torch``: the PyTorch-ROCm builds, required;
+    * a path: a directory holding ``libamdhip64.so`` / ``librccl.so``.
+
+    Measured on MI355X (``profiles/round2/runtime_ab.md``): a cold process's first RCCL
+    communicator init takes ~0.9 s on the PyTorch-ROCm 7.0 build (RCCL 2.26.6) against
+    ~1.7 s on ``/opt/rocm`` 7.2 (RCCL 2.27.7), whose device code is one 544 MiB bundle."""
+    sel = os.environ.get("TK_HIP_RUNTIME", "auto") or "auto"
+    if sel == "system":
+        return "system"
+    if sel in ("auto", "torch"):
+        d = _torch_lib_dir()
+        if d:
+            return d
+        if sel == "torch":
+            raise NativeUnavailable("TK_HIP_RUNTIME=torch but no PyTorch-ROCm runtime is installed")
+        return "system"
+    return sel
+
+
+def runtime_dir() -> str:
+    """Load the selected runtime (:func:`select_runtime`) before the first native HIP
+    library: non-system runtimes are ``dlopen``ed with ``RTLD_GLOBAL``, so the
+    ``libamdhip64.so.7`` / ``librccl.so.1`` dependencies of ``ops/lib`` bind to them (same
+    sonames).  A process that already imported torch runs on torch's runtime regardless."""
+    global _runtime_dir
+    if _runtime_dir is not None:
+        return _runtime_dir
+    import sys
+
+    if "torch" in sys.modules:
+        _runtime_dir = "torch (imported)"
+        return _runtime_dir
+    d = select_runtime()
+    if d != "system":
+        for so in _RUNTIME_LIBS:
+            path = os.path.join(d, so)
+            if os.path.exists(path):
+                ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+            elif so in ("libamdhip64.so", "librccl.so"):
+                raise NativeUnavailable(f"HIP runtime {d}: {path} missing")
+    _runtime_dir = d
+    return d
+
+
 def lib_path(name: str) -> str:
     return os.path.join(LIB_DIR, name)
 
@@ -51,6 +119,7 @@ def load(name: str, autobuild: bool = True) -> ctypes.CDLL:
             import sys
 
             _hip_before_torch = "torch" not in sys.modules
+            runtime_dir()
         try:
             lib = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         except OSError as exc:
