@@ -56,6 +56,7 @@ class ProcessGate:
         self.sizes, self.iters, self.timeout = list(sizes), iters, timeout
         self.tools_dir, self.min_busbw, self.env_file = tools_dir, min_busbw, env_file
         self.bases = [sum(self.ndevs[:i]) for i in range(len(self.ndevs))]
+        self._pending = ""
 
     def _script(self, i: int, uid: Optional[str]) -> str:
         return gate_script(self.tools_dir, self.world, self.bases[i], self.ndevs[i], self.sizes, self.iters, uid,
@@ -74,10 +75,12 @@ class ProcessGate:
                 uid = self._read_uid(p0, deadline)
                 for i in range(1, len(self.hosts)):
                     procs.append(self.transport.spawn(self.hosts[i], self._script(i, uid)))
-                # drain every process's pipes until all exit (or the deadline / a failure)
+                # drain every process's pipes until all exit (or the deadline / a failure);
+                # raw reads, so a partial line can never block the loop past the deadline
+                outs[0] += self._pending
                 for i, p in enumerate(procs):
-                    sel.register(p.stdout, selectors.EVENT_READ, (i, "out"))
-                    sel.register(p.stderr, selectors.EVENT_READ, (i, "err"))
+                    sel.register(p.stdout.fileno(), selectors.EVENT_READ, (i, "out"))
+                    sel.register(p.stderr.fileno(), selectors.EVENT_READ, (i, "err"))
                 open_pipes = 2 * len(procs)
                 while open_pipes:
                     left = deadline - time.monotonic()
@@ -85,9 +88,9 @@ class ProcessGate:
                         raise TKError(f"RCCL process gate timed out after {self.timeout:.0f}s")
                     for key, _ in sel.select(timeout=min(left, 1.0)):
                         i, which = key.data
-                        chunk = key.fileobj.readline()
+                        chunk = os.read(key.fd, 65536).decode(errors="replace")
                         if not chunk:
-                            sel.unregister(key.fileobj)
+                            sel.unregister(key.fd)
                             open_pipes -= 1
                             continue
                         if which == "out":
@@ -121,8 +124,11 @@ class ProcessGate:
                 "min_peak_busbw_gbps": min(busbw) if busbw else 0.0, "ranks": ranks}
 
     def _read_uid(self, proc: Any, deadline: float) -> str:
+        """Rank 0's first stdout line; what follows it stays in ``self._pending``."""
         sel = selectors.DefaultSelector()
-        sel.register(proc.stdout, selectors.EVENT_READ)
+        fd = proc.stdout.fileno()
+        sel.register(fd, selectors.EVENT_READ)
+        buf = ""
         try:
             while True:
                 left = deadline - time.monotonic()
@@ -133,12 +139,16 @@ class ProcessGate:
                         raise TKError(f"RCCL process gate: first node exited {proc.returncode}: "
                                       f"{proc.stderr.read()[-400:]}")
                     continue
-                line = proc.stdout.readline()
-                if not line:
+                chunk = os.read(fd, 65536).decode(errors="replace")
+                if not chunk:
                     raise TKError(f"RCCL process gate: first node closed its output "
                                   f"(exit {proc.wait()}): {proc.stderr.read()[-400:]}")
-                if line.startswith("{") and '"uid"' in line:
-                    return json.loads(line)["uid"]
+                buf += chunk
+                while "\n" in buf:
+                    line, buf = buf.split("\n", 1)
+                    if line.startswith("{") and '"uid"' in line:
+                        self._pending = buf
+                        return json.loads(line)["uid"]
         finally:
             sel.close()
 
