@@ -30,7 +30,7 @@ if [ "$MODE" = all ] || [ "$MODE" = burnin ]; then
 fi
 if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   cd /tmp && export TMPDIR=/tmp
-  step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o bench -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --warm-steps 0
+  step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o "bench_%pid%" -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --warm-steps 0
 fi
 if [ "$MODE" = coldinit ]; then
   step rccl_cold_init 600 python scripts/rccl_cold_init.py ${COLD_VARIANTS:-}

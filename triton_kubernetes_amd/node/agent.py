@@ -674,10 +674,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     if getattr(agent, "_used_rccl", False):
         from ..ops import rccl
 
-        # every communicator was torn down by stop(); an init blocked on absent peers
-        # would hang a normal exit, and the HIP runtime's own teardown adds nothing the
-        # kernel driver does not do at process exit
-        rccl.exit_now(0)
+        # every communicator was torn down by stop(); only an init still blocked on absent
+        # peers would hang a normal exit (which also lets tools such as rocprofv3 finalize)
+        if rccl.abandoned_inits():
+            rccl.exit_now(0)
     return 0
 
 
