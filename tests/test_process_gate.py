@@ -2,7 +2,6 @@
 host transport (``readiness/process_gate.py``), with the CPU stand-in of the tool."""
 
 import os
-import shutil
 import stat
 import sys
 import time

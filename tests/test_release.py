@@ -3,7 +3,6 @@ stdlib .deb and .rpm writers, read back with dpkg-deb and the module's own rpm r
 
 import hashlib
 import os
-import shutil
 import subprocess
 
 import pytest
