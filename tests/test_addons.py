@@ -242,3 +242,34 @@ def test_apply_is_idempotent_with_rbac_and_injector():
         assert "ClusterRoleBinding/amdgpu-node-labeller" in first and first[-1] == "Job/rccl-ready"
     finally:
         fake.stop()
+
+
+@pytest.mark.skipif(not have("openssl"), reason="openssl needed for the serving certificate")
+def test_injector_certificate_is_kept_across_applies():
+    """Like Terraform's tls_* resources in state: a re-apply reuses the certificate, so
+    running webhook pods and the new caBundle always agree."""
+    from triton_kubernetes_amd.executor.direct import DirectExecutor
+
+    fake = FakeRancher(bootstrap_password="b00tstrap-only").start()
+    try:
+        client = RancherClient(fake.url)
+        outs = client.bootstrap("n3w-passw0rd-123", fake.url, "b00tstrap-only", timeout=10)
+        cid = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"]).ensure_cluster("x")
+        fake.state.clusters[cid.cluster_id]["state"] = "active"
+        ex = DirectExecutor(transport=None)
+        cfg = {"rancher_api_url": fake.url, "rancher_access_key": outs["rancher_access_key"],
+               "rancher_secret_key": outs["rancher_secret_key"], "rancher_cluster_id": cid.cluster_id}
+        _, private = ex._apply_addons(dict(cfg))
+        tls = private["injector_tls"]
+        assert "BEGIN CERTIFICATE" in tls["ca_pem"] and "PRIVATE KEY" in tls["key_pem"]
+
+        def secret():
+            return next(o for o in fake.state.objects.values() if o.get("kind") == "Secret")["data"]["tls.crt"]
+
+        first = secret()
+        _, again = ex._apply_addons(dict(cfg), private)
+        assert again == private and secret() == first
+        _, fresh = ex._apply_addons(dict(cfg, rccl_env_injector="false"))
+        assert fresh == {}
+    finally:
+        fake.stop()

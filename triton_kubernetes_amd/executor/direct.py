@@ -116,6 +116,9 @@ class ModuleRun:
     start: float = 0.0
     end: float = 0.0
     detail: Any = None
+    # module-private state kept in the tfstate between applies (what a Terraform module keeps
+    # in its resources' state, e.g. the add-ons' tls_* certificate)
+    prev_private: Optional[Dict[str, Any]] = None
 
 
 @dataclass
@@ -245,6 +248,7 @@ class DirectExecutor(Executor):
                             run.status = "skipped"
                             continue
                         run.start = time.time()
+                        run.prev_private = (prev or {}).get("private")
                         futures[pool.submit(self._apply_module, run, dict(outputs), state.name)] = key
                 if not futures:
                     for key in pending:  # nothing running and nothing startable: a cycle
@@ -267,6 +271,8 @@ class DirectExecutor(Executor):
                         tf["module_state"][key] = {"hash": run.hash, "status": "ok",
                                                    "applied_at": run.end, "seconds": run.end - run.start,
                                                    "source": run.cfg.get("source")}
+                        if isinstance(detail, dict) and detail.get("private"):
+                            tf["module_state"][key]["private"] = detail["private"]
                     except Exception as exc:  # noqa: BLE001 - recorded per module
                         run.status, run.error = "failed", str(exc)
                         tf["module_state"][key] = {"hash": run.hash, "status": "failed",
@@ -298,7 +304,8 @@ class DirectExecutor(Executor):
                         self._event("module_retry", key=run.key, attempt=attempt + 1, error=str(exc))
                         time.sleep(self.retry_backoff * (2 ** attempt))
             if kind == "addon":
-                return self._apply_addons(cfg), None
+                outs, private = self._apply_addons(cfg, run.prev_private)
+                return outs, {"private": private}
         raise ExecutorError(f"unsupported module kind {kind}")
 
     # --- manager ---------------------------------------------------------------------------------------
@@ -361,10 +368,14 @@ class DirectExecutor(Executor):
             self.transport.put_file(ref, executable(tool), f"{TOOLS_DIR}/{tool}")
 
     # --- addons -------------------------------------------------------------------------------------------
-    def _apply_addons(self, cfg: Dict[str, Any]) -> Dict[str, str]:
+    def _apply_addons(self, cfg: Dict[str, Any],
+                      private: Optional[Dict[str, Any]] = None) -> Tuple[Dict[str, str], Dict[str, Any]]:
         """The Terraform add-on module's objects, rendered from its own template files
         (``k8s/addons.py``), with the injector's serving certificate made by ``openssl``
-        (the module uses the ``tls`` provider) -- while the nodes still bootstrap."""
+        (the module uses the ``tls`` provider) -- while the nodes still bootstrap.  The
+        certificate is kept in the module's private tfstate entry and reused by later
+        applies, as Terraform keeps its ``tls_*`` resources, so re-applying never leaves
+        running webhook pods with a certificate the new ``caBundle`` rejects."""
         from ..k8s import addons
         from ..k8s.manifests import apply_manifests
 
@@ -373,16 +384,22 @@ class DirectExecutor(Executor):
         cid = cfg["rancher_cluster_id"]
         cert = None
         if addons.enabled("env", addons.module_cfg_defaults(cfg)):
-            from ..k8s.tls import serving_cert
+            from ..k8s.tls import ServingCert, serving_cert
 
-            with span("addons.tls", cluster=cid):
-                cert = serving_cert(addons.INJECTOR, "kube-system")
+            kept = (private or {}).get("injector_tls")
+            if kept:
+                cert = ServingCert(**kept)
+            else:
+                with span("addons.tls", cluster=cid):
+                    cert = serving_cert(addons.INJECTOR, "kube-system")
         manifests = addons.rendered_addons(cfg, cert)
         with span("addons.wait_active", cluster=cid):
             wait_until(lambda: client.cluster_state(cid) == "active", self.cluster_wait, f"cluster {cid} active")
         with span("addons.apply", cluster=cid):
             applied = apply_manifests(client, cid, manifests)
-        return {"addons_applied": str(len(applied))}
+        kept = {"injector_tls": {"ca_pem": cert.ca_pem, "cert_pem": cert.cert_pem, "key_pem": cert.key_pem}} \
+            if cert else {}
+        return {"addons_applied": str(len(applied))}, kept
 
     # --- destroy / outputs ------------------------------------------------------------------------------
     def destroy(self, state: State, backend: Backend, targets: List[str]) -> None:
