@@ -5,7 +5,8 @@ Speaks the same protocol as the native tool: with ``--uid-out`` it prints
 ``{"uid": <256 hex>}`` first (the hex encodes a TCP port this process listens on, like
 RCCL's bootstrap root), then waits until processes holding the remaining
 ``world - ngpus`` ranks have connected; with ``--uid`` it connects to that port and
-waits.  Every process then prints one result line.  ``FAKE_RCCL_FAIL_BASE=<rank base>``
+waits (an id that does not start with ``fa4e`` came from a simulated agent: no rendezvous).
+Every process then prints one result line.  ``FAKE_RCCL_FAIL_BASE=<rank base>``
 makes that process fail at once; ``FAKE_RCCL_NO_UID=1`` makes the root never print its id.
 The environment the gate script sourced is echoed back (``env``) so tests can check it.
 """
@@ -41,8 +42,9 @@ def main() -> int:
         srv.bind(("127.0.0.1", 0))
         srv.listen(64)
         port = srv.getsockname()[1]
-        print(json.dumps({"uid": f"{port:08x}".ljust(256, "0")}), flush=True)
-        have, conns = a.ngpus, []
+        print(json.dumps({"uid": ("fa4e" + f"{port:08x}").ljust(256, "0")}), flush=True)
+        # ranks held by agents (FAKE_RCCL_AGENT_RANKS) do not connect to this stand-in
+        have, conns = a.ngpus + int(os.environ.get("FAKE_RCCL_AGENT_RANKS", "0")), []
         while have < a.world:
             c, _ = srv.accept()
             have += int(c.recv(16).decode())
@@ -50,12 +52,13 @@ def main() -> int:
         for c in conns:
             c.sendall(b"go")
             c.close()
-    else:
-        port = int(a.uid[:8], 16)
+    elif a.uid.startswith("fa4e"):
+        port = int(a.uid[4:12], 16)
         c = socket.create_connection(("127.0.0.1", port), timeout=a.timeout_s)
         c.sendall(str(a.ngpus).encode())
         assert c.recv(2) == b"go"
         c.close()
+    # else: the id came from an agent (a sim gate in tests): nothing to rendezvous with
     sizes = [1 << 20, a.max_mib << 20]
     print(json.dumps({"world": a.world, "rank_base": a.rank_base, "ngpus": a.ngpus, "init_ms": 1.0,
                       "results": [{"bytes": b, "busbw_gbps": 100.0 + a.rank_base, "errors": 0} for b in sizes],

@@ -92,3 +92,29 @@ def test_waiter_runs_process_gate_for_ssh_nodes(tools):
         assert "rccl_gate" not in rep2.phases
     finally:
         fake.stop()
+
+
+def test_mixed_agent_and_process_nodes_share_one_gate(tools):
+    """Agent nodes join the process gate through their API, with the same unique id."""
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.labels import synthetic_topology
+    from triton_kubernetes_amd.parallel.transport import AgentTransport
+
+    token = "mixed-gate-token-12345"
+    agent = NodeAgent(name="a", mode="sim", devices=list(range(8)), token=token, root=str(tools[1]) + ".d",
+                      topology_override=synthetic_topology(8))
+    url = agent.serve()
+    try:
+        d, env_file = tools
+        for hosts in ([HostRef("local"), HostRef("agent+" + url)], [HostRef("agent+" + url), HostRef("local")]):
+            gate = ProcessGate(LocalTransport(env={"FAKE_RCCL_AGENT_RANKS": "8"}), hosts, [8, 8], [1 << 20, 64 << 20],
+                               iters=5, timeout=60, tools_dir=d, env_file=env_file,
+                               agent_transport=AgentTransport(token=token))
+            res = gate.run()
+            assert res["ok"] and res["mode"] == "mixed" and res["world"] == 16, res
+            assert sorted((r["kind"], r["rank_base"]) for r in res["ranks"]) == \
+                sorted([(("process" if h.scheme == "ssh" or h.address == "local" else "agent"), b)
+                        for h, b in zip(hosts, (0, 8))])
+        assert agent._gates == {}  # the agent's communicator was consumed, nothing pending
+    finally:
+        agent.stop()

@@ -18,8 +18,16 @@ the gate runs one ``rccl-ready --cluster`` process per node over the host transp
 Each node's ``/etc/rccl/rccl.env`` (discovered RDMA ports, per-node overrides, written by
 the bootstrap) is sourced first, so the gate runs with the environment GPU pods get.
 A deadline bounds the whole gate; on expiry or the first failure every process is killed.
+
+A cluster that mixes both kinds of MI355X nodes gets ONE communicator too: agent hosts
+(``agent+URL`` addresses) join through their API (``/v1/rccl-prepare`` with the unique id,
+then ``/v1/rccl-gate``), process hosts through ``rccl-ready --cluster``; both run the same
+sweep schedule, so their collectives match.  The id travels as base64 to agents and as hex
+to processes; whichever kind the first node is, it hosts the rendezvous.
 """
 
+import base64
+import concurrent.futures as cf
 import json
 import os
 import selectors
@@ -48,9 +56,12 @@ def gate_script(tools_dir: str, world: int, rank_base: int, ngpus: int, sizes: S
 class ProcessGate:
     def __init__(self, transport: Any, hosts: List[HostRef], ndevs: List[int], sizes: Sequence[int],
                  iters: int = 5, timeout: float = 600.0, tools_dir: str = TOOLS_DIR, min_busbw: float = 0.0,
-                 env_file: str = ENV_FILE):
+                 env_file: str = ENV_FILE, agent_transport: Any = None):
         if not hosts or len(hosts) != len(ndevs):
             raise ValueError("a process gate needs one GPU count per host")
+        if any(h.scheme == "agent" for h in hosts) and agent_transport is None:
+            raise ValueError("agent hosts in a process gate need an agent transport")
+        self.agent_transport = agent_transport
         self.transport, self.hosts, self.ndevs = transport, list(hosts), [int(n) for n in ndevs]
         self.world = sum(self.ndevs)
         self.sizes, self.iters, self.timeout = list(sizes), iters, timeout
@@ -62,31 +73,72 @@ class ProcessGate:
         return gate_script(self.tools_dir, self.world, self.bases[i], self.ndevs[i], self.sizes, self.iters, uid,
                            self.min_busbw, self.timeout, self.env_file)
 
+    def _is_agent(self, i: int) -> bool:
+        return self.hosts[i].scheme == "agent"
+
+    def _agent_prepare(self, i: int, uid_b64: Optional[str]) -> str:
+        body = {"world": self.world, "rank_base": self.bases[i], "ndev": self.ndevs[i], "max_bytes": max(self.sizes)}
+        if uid_b64:
+            body["uid"] = uid_b64
+        return self.agent_transport.post(self.hosts[i], "/v1/rccl-prepare", body)["uid"]
+
+    def _agent_gate(self, i: int, uid_b64: str) -> Dict[str, Any]:
+        res = self.agent_transport.post(self.hosts[i], "/v1/rccl-gate", {
+            "uid": uid_b64, "rank": self.bases[i], "world": self.world, "ndev": self.ndevs[i],
+            "sizes": self.sizes, "iters": self.iters})
+        res["results"] = [{"bytes": b, "busbw_gbps": bw, "errors": e} for b, bw, e in
+                          zip(res.get("sizes", []), res.get("busbw_gbps", []), res.get("errors", []))]
+        return res
+
     def run(self) -> Dict[str, Any]:
         deadline = time.monotonic() + self.timeout
-        procs: List[Any] = []
+        procs: Dict[int, Any] = {}
+        futs: Dict[int, cf.Future] = {}
         outs: List[str] = [""] * len(self.hosts)
         errs: List[str] = [""] * len(self.hosts)
         sel = selectors.DefaultSelector()
+        pool = cf.ThreadPoolExecutor(max_workers=max(1, 2 * sum(self._is_agent(i) for i in range(len(self.hosts)))),
+                                     thread_name_prefix="tk-pgate")
+        uid_b64 = None
+        ok_run = False
         try:
             with span("gate.process", world=self.world, nodes=len(self.hosts)):
-                p0 = self.transport.spawn(self.hosts[0], self._script(0, None))
-                procs.append(p0)
-                uid = self._read_uid(p0, deadline)
+                # 1. the first node hosts the rendezvous
+                if self._is_agent(0):
+                    uid_b64 = self._agent_prepare(0, None)
+                    uid = base64.b64decode(uid_b64).hex()
+                else:
+                    procs[0] = self.transport.spawn(self.hosts[0], self._script(0, None))
+                    uid = self._read_uid(procs[0], deadline)
+                    uid_b64 = base64.b64encode(bytes.fromhex(uid)).decode()
+                    outs[0] += self._pending
+                # 2. everyone else joins with it
+                prep = {i: pool.submit(self._agent_prepare, i, uid_b64)
+                        for i in range(1, len(self.hosts)) if self._is_agent(i)}
                 for i in range(1, len(self.hosts)):
-                    procs.append(self.transport.spawn(self.hosts[i], self._script(i, uid)))
+                    if not self._is_agent(i):
+                        procs[i] = self.transport.spawn(self.hosts[i], self._script(i, uid))
+                for f in prep.values():
+                    f.result(timeout=max(1.0, deadline - time.monotonic()))
+                # 3. agents run their ranks of the sweep while the processes run theirs
+                futs = {i: pool.submit(self._agent_gate, i, uid_b64)
+                        for i in range(len(self.hosts)) if self._is_agent(i)}
                 # drain every process's pipes until all exit (or the deadline / a failure);
                 # raw reads, so a partial line can never block the loop past the deadline
-                outs[0] += self._pending
-                for i, p in enumerate(procs):
+                for i, p in procs.items():
                     sel.register(p.stdout.fileno(), selectors.EVENT_READ, (i, "out"))
                     sel.register(p.stderr.fileno(), selectors.EVENT_READ, (i, "err"))
                 open_pipes = 2 * len(procs)
-                while open_pipes:
+                while open_pipes or any(not f.done() for f in futs.values()):
                     left = deadline - time.monotonic()
                     if left <= 0:
                         raise TKError(f"RCCL process gate timed out after {self.timeout:.0f}s")
-                    for key, _ in sel.select(timeout=min(left, 1.0)):
+                    if open_pipes:
+                        ready = sel.select(timeout=min(left, 0.2))
+                    else:
+                        ready = []
+                        cf.wait(list(futs.values()), timeout=min(left, 0.2), return_when=cf.FIRST_COMPLETED)
+                    for key, _ in ready:
                         i, which = key.data
                         chunk = os.read(key.fd, 65536).decode(errors="replace")
                         if not chunk:
@@ -97,30 +149,52 @@ class ProcessGate:
                             outs[i] += chunk
                         else:
                             errs[i] += chunk
-                    failed = [i for i, p in enumerate(procs) if p.poll() not in (None, 0)]
-                    if failed and any(p.poll() is None for p in procs):
+                    failed = [i for i, p in procs.items() if p.poll() not in (None, 0)]
+                    if failed and (any(p.poll() is None for p in procs.values())
+                                   or any(not f.done() for f in futs.values())):
                         # one node failed: the others would wait for it forever
                         raise TKError(f"RCCL process gate: node {self.hosts[failed[0]].address} exited "
                                       f"{procs[failed[0]].returncode}: {errs[failed[0]][-400:]}")
-                for p in procs:
+                    bad = [i for i, f in futs.items() if f.done() and f.exception() is not None]
+                    if bad:
+                        raise TKError(f"RCCL process gate: agent {self.hosts[bad[0]].address} failed: "
+                                      f"{futs[bad[0]].exception()}")
+                for p in procs.values():
                     p.wait(timeout=max(1.0, deadline - time.monotonic()))
+                ok_run = True
         finally:
             sel.close()
-            for p in procs:
+            for p in procs.values():
                 if p.poll() is None:
                     p.kill()
                     p.wait()
+            if not ok_run and uid_b64 is not None:
+                for i in range(len(self.hosts)):  # release agents' pending communicators
+                    if self._is_agent(i):
+                        try:
+                            self.agent_transport.post(self.hosts[i], "/v1/rccl-abort", {"uid": uid_b64})
+                        except Exception:  # noqa: BLE001 - best effort; agents expire stale gates
+                            pass
+            pool.shutdown(wait=False, cancel_futures=True)
         ranks = []
-        for i, p in enumerate(procs):
-            line = next((ln for ln in reversed(outs[i].splitlines()) if ln.startswith("{") and '"uid"' not in ln), "")
-            doc = json.loads(line) if line else {"ok": False}
-            doc.update(host=self.hosts[i].address, rc=p.returncode, rank_base=self.bases[i])
-            if p.returncode:
-                doc["stderr"] = errs[i][-400:]
+        for i in range(len(self.hosts)):
+            if self._is_agent(i):
+                doc = dict(futs[i].result())
+                doc.update(host=self.hosts[i].address, rc=0, rank_base=self.bases[i], kind="agent")
+            else:
+                p = procs[i]
+                line = next((ln for ln in reversed(outs[i].splitlines()) if ln.startswith("{") and '"uid"' not in ln),
+                            "")
+                doc = json.loads(line) if line else {"ok": False}
+                doc.update(host=self.hosts[i].address, rc=p.returncode, rank_base=self.bases[i], kind="process")
+                if p.returncode:
+                    doc["stderr"] = errs[i][-400:]
             ranks.append(doc)
         busbw = [max((r.get("busbw_gbps", 0.0) for r in d.get("results", [])), default=0.0) for d in ranks]
         ok = all(d.get("ok") and d["rc"] == 0 for d in ranks)
-        return {"ok": ok, "world": self.world, "nodes": len(self.hosts), "mode": "process", "pipelined": False,
+        kinds = {d["kind"] for d in ranks}
+        return {"ok": ok, "world": self.world, "nodes": len(self.hosts),
+                "mode": "process" if kinds == {"process"} else "mixed", "pipelined": False,
                 "min_peak_busbw_gbps": min(busbw) if busbw else 0.0, "ranks": ranks}
 
     def _read_uid(self, proc: Any, deadline: float) -> str:

@@ -129,7 +129,8 @@ def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float
         from .process_gate import ProcessGate
 
         pgate = ProcessGate(host_transport or TransportRouter(), spec.rccl_process_hosts, spec.rccl_process_ndev,
-                            spec.rccl_sizes, spec.rccl_iters, timeout=left(), tools_dir=tools_dir or TOOLS_DIR)
+                            spec.rccl_sizes, spec.rccl_iters, timeout=left(), tools_dir=tools_dir or TOOLS_DIR,
+                            agent_transport=agent_transport)
         with span("ready.rccl_gate", world=pgate.world, nodes=len(spec.rccl_process_hosts), mode="process"):
             rep.rccl = pgate.run()
     elif spec.rccl_skip_reason:
@@ -192,10 +193,20 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
     skip = ""
     if rccl_gate:
         if rccl_hosts and proc_hosts:
-            # one communicator cannot yet span agent-held and process-held ranks
-            skip = (f"mixed delivery: {len(rccl_hosts)} agent and {len(proc_hosts)} SSH/Terraform MI355X "
-                    "nodes; gate each kind with a cluster of its own")
-            rccl_hosts, rccl_ndev, proc_hosts, proc_ndev = [], [], [], []
+            # mixed delivery: one communicator through the process gate, whose agent members
+            # join via their API (process_gate.py); host order is the rank order
+            mixed = []
+            for host in sorted(nodes):
+                cfg = state.module(nodes[host]) or {}
+                info = module_from_source(str(cfg.get("source", "")))
+                if info is None or not info.mi355x or not cfg.get("host"):
+                    continue
+                addr = str(cfg["host"])
+                ref = HostRef(addr, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
+                              cfg.get("bastion_host") or "")
+                mixed.append((ref, int(cfg.get("gpu_count", 8) or 8)))
+            proc_hosts, proc_ndev = [m[0] for m in mixed], [m[1] for m in mixed]
+            rccl_hosts, rccl_ndev = [], []
         elif not (rccl_hosts or proc_hosts):
             skip = "no MI355X nodes in the cluster"
     spec = ReadinessSpec(cl["rancher_cluster_id"], sorted(nodes), gpu_nodes, timeout,
@@ -241,7 +252,8 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
     timeout = float(s.get_string("wait_timeout") or 3600)
     client, spec = spec_from_state(state, backend, cluster_key, timeout, s.get_bool("rccl_gate"))
     spec.rccl_sizes = gate_sizes(s)
-    transport = agent_transport_for(ctx) if spec.rccl_gate and spec.rccl_hosts else None
+    mixed = any(h.scheme == "agent" for h in spec.rccl_process_hosts)
+    transport = agent_transport_for(ctx) if spec.rccl_gate and (spec.rccl_hosts or mixed) else None
     if gate is not None and (not spec.rccl_hosts or gate.world != sum(spec.rccl_ndev or [1] * len(spec.rccl_hosts))):
         gate.abort()  # membership changed since it was prepared
         gate = None
