@@ -620,33 +620,6 @@ class NodeAgent:
             rccl.drain()
 
 
-def _early_rccl_load(devices: List[int]) -> None:
-    """Daemon start: load every native library now (so no dlopen runs while HIP is busy
-    elsewhere), then load RCCL's device code onto each GPU on a thread of its own while the
-    agent finishes starting.  A process's first communicator init otherwise does that load
-    on the gate's critical path (``profiles/round2/cold_rccl_init.md``).  No communicator
-    is created.  ``TK_RCCL_LOAD_EARLY=0`` disables."""
-    if os.environ.get("TK_RCCL_LOAD_EARLY", "1") == "0":
-        return
-    from ..ops import probe, rccl, topo
-
-    rccl._lib()
-    probe._lib()
-    try:
-        topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
-    except Exception:  # noqa: BLE001 - topology falls back to other sources later
-        pass
-
-    def load(dev: int) -> None:
-        try:
-            rccl.load_kernels(dev)
-        except rccl.RCCLError:
-            pass  # this RCCL build does not export the handle: the first init loads it
-
-    for d in devices:
-        threading.Thread(target=load, args=(d,), name=f"tk-rccl-load-{d}", daemon=True).start()
-
-
 def main(argv: Optional[List[str]] = None) -> int:
     """``tk-node-agent``: serve the agent API on a host (127.0.0.1 by default)."""
     import argparse
@@ -669,8 +642,6 @@ def main(argv: Optional[List[str]] = None) -> int:
     host, _, port = args.listen.rpartition(":")
     devices = [int(d) for d in args.devices.split(",") if d.strip()]
     agent = NodeAgent(name=args.name or host, mode=args.mode, devices=devices, root=args.root, token=token)
-    if args.synthetic_gpus <= 0 and devices:
-        _early_rccl_load(devices)
     if args.synthetic_gpus > 0:
         from .labels import synthetic_topology
 

@@ -22,8 +22,6 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
-#include <dlfcn.h>
-
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -86,26 +84,6 @@ extern "C" int tkr_version() {
   int v = 0;
   ncclGetVersion(&v);
   return v;
-}
-
-// Load RCCL's device code onto `device` now: hipFuncGetAttributes on RCCL's first kernel
-// handle makes the HIP runtime load librccl's code object for the device, the one call that
-// carries a process's whole first-init "kernels" phase (profiles/round2/rccl_kernel_load.json:
-// that call takes the full cost, the other 113 kernel handles are then free).  Public HIP
-// API on an exported symbol, no communicator.  Returns the wall ms; < 0 when the handle is
-// not exported by the RCCL build in use.
-extern "C" double tkr_load_kernels(int device) {
-  static const char* kSym = "_Z23ncclDevKernel_Generic_124ncclDevKernelArgsStorageILm4096EE";
-  const void* fn = dlsym(RTLD_DEFAULT, kSym);
-  if (!fn) { snprintf(g_err, sizeof(g_err), "RCCL kernel handle %s not exported", kSym); return -1.0; }
-  const auto t0 = std::chrono::steady_clock::now();
-  if (hipSetDevice(device) != hipSuccess) { snprintf(g_err, sizeof(g_err), "hipSetDevice(%d)", device); return -2.0; }
-  hipFuncAttributes attr;
-  if (hipFuncGetAttributes(&attr, fn) != hipSuccess) {
-    snprintf(g_err, sizeof(g_err), "hipFuncGetAttributes: %s", hipGetErrorString(hipGetLastError()));
-    return -3.0;
-  }
-  return std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }
 
 extern "C" int tkr_unique_id(unsigned char* out128) {

@@ -28,8 +28,6 @@ def _lib():
     lib.tkr_last_init_ms.restype = ctypes.c_double
     lib.tkr_last_phase_ms.restype = ctypes.c_double
     lib.tkr_last_phase_ms.argtypes = [ctypes.c_int]
-    lib.tkr_load_kernels.argtypes = [ctypes.c_int]
-    lib.tkr_load_kernels.restype = ctypes.c_double
     lib.tkr_set_async_teardown.argtypes = [ctypes.c_int]
     lib.tkr_set_teardown_abort.argtypes = [ctypes.c_int]
     lib.tkr_set_teardown_quiet_ms.argtypes = [ctypes.c_double]
@@ -52,15 +50,6 @@ def _lib():
         atexit.register(lib.tkr_drain)  # join async teardowns before interpreter exit
         _ATEXIT = True
     return lib
-
-
-def load_kernels(device: int) -> float:
-    """Load RCCL's device code onto ``device`` now (what a process's first communicator init
-    would otherwise do on its critical path); returns the wall ms.  Idempotent."""
-    ms = float(_lib().tkr_load_kernels(device))
-    if ms < 0:
-        raise RCCLError(_lib().tkr_last_error().decode())
-    return ms
 
 
 def version() -> int:
