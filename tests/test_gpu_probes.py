@@ -142,6 +142,30 @@ def test_rccl_ready_cluster_mode_through_process_gate(tmp_path):
     assert os.path.exists(os.path.join(LIB_DIR, "rccl-ready"))
 
 
+def test_process_gate_two_nodes_rendezvous_and_fail_fast(tmp_path):
+    """Two rccl-ready --cluster processes (world 2) on the box's one GPU: the unique id
+    travels from the first process to the second and the bootstrap rendezvous completes --
+    then RCCL refuses two ranks on one device ("invalid usage", its duplicate-GPU check runs
+    on the exchanged peer info), and the gate fails fast instead of hanging."""
+    import time
+
+    from triton_kubernetes_amd.errors import TKError
+    from triton_kubernetes_amd.ops.native import LIB_DIR
+    from triton_kubernetes_amd.parallel.transport import HostRef, LocalTransport
+    from triton_kubernetes_amd.readiness.process_gate import ProcessGate
+
+    gate = ProcessGate(LocalTransport(), [HostRef("local"), HostRef("local")], [1, 1], [1 << 20], iters=2,
+                       timeout=90, tools_dir=LIB_DIR, env_file=str(tmp_path / "none"))
+    t0 = time.monotonic()
+    try:
+        res = gate.run()
+        assert not res["ok"]
+        assert all("invalid usage" in r.get("stderr", "") for r in res["ranks"]), res
+    except TKError as exc:
+        assert "invalid usage" in str(exc), exc
+    assert time.monotonic() - t0 < 60
+
+
 def test_topology_amdsmi():
     from triton_kubernetes_amd.ops import topo
 
