@@ -112,27 +112,10 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
 
 
 def _templatefile(text: str, values: dict) -> str:
-    """Enough of Terraform's templatefile() for the host scripts: ${var}, $${ escapes and
-    single-level %{ if <cond> ~} ... %{ endif ~} blocks (conditions use == != > with
-    variables and literals)."""
-    import re
+    """Terraform's templatefile(), as terraform/hcl.py evaluates it (strip markers included)."""
+    from triton_kubernetes_amd.terraform.hcl import templatefile
 
-    out, keep = [], [True]
-    for line in text.splitlines():
-        m = re.match(r"^\s*%\{\s*if\s+(.*?)\s*~?\}\s*$", line)
-        if m:
-            cond = re.sub(r"\b([A-Za-z_][A-Za-z0-9_]*)\b", lambda v: repr(values[v.group(1)])
-                          if v.group(1) in values else v.group(1), m.group(1))
-            keep.append(keep[-1] and bool(eval(cond, {"__builtins__": {}})))  # noqa: S307 - test-owned input
-            continue
-        if re.match(r"^\s*%\{\s*endif\s*~?\}\s*$", line):
-            keep.pop()
-            continue
-        if keep[-1]:
-            out.append(line)
-    body = ("\n".join(out) + "\n").replace("$${", "\x00")
-    body = re.sub(r"\$\{([A-Za-z_][A-Za-z0-9_]*)\}", lambda m: str(values[m.group(1)]), body)
-    return body.replace("\x00", "${")
+    return templatefile(text, values)
 
 
 def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):

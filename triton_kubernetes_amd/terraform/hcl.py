@@ -45,6 +45,8 @@ class Node:
     value: Any = None
     children: List["Node"] = field(default_factory=list)
     pos: int = 0
+    # template parts only: whitespace strip markers ``~`` on the (left, right) of ``${``/``%{``
+    strip: Tuple[bool, bool] = (False, False)
 
 
 @dataclass
@@ -82,6 +84,7 @@ _KEYWORD_LITS = {"true": True, "false": False, "null": None}
 
 class _Parser:
     def __init__(self, src: str, name: str):
+        self._rstrip = False
         self.s = src
         self.n = len(src)
         self.i = 0
@@ -474,17 +477,21 @@ class _Parser:
                 directive = s[self.i] == "%"
                 start = self.i
                 self.i += 2
-                if self.peek("~"):
+                lstrip = self.peek("~")
+                if lstrip:
                     self.i += 1
                 if directive:
-                    parts.append(self._directive(stack, start))
+                    node = self._directive(stack, start)
                 else:
                     e = self.expr(True)
                     self.skip(True)
-                    if self.peek("~"):
+                    self._rstrip = self.peek("~")
+                    if self._rstrip:
                         self.i += 1
                     self.expect("}", True, "to close '${'")
-                    parts.append(Node("interp", None, [e], start))
+                    node = Node("interp", None, [e], start)
+                node.strip = (lstrip, self._rstrip)
+                parts.append(node)
                 continue
             buf.append(c)
             self.i += 1
@@ -525,7 +532,8 @@ class _Parser:
         else:
             raise self.err(f"unknown template directive %{{{word}}}", start)
         self.skip(True)
-        if self.peek("~"):
+        self._rstrip = self.peek("~")
+        if self._rstrip:
             self.i += 1
         self.expect("}", True, "to close the directive")
         return node
@@ -758,3 +766,193 @@ def _module_relative_path(node: Node) -> Optional[str]:
     if ref.kind == "trav" and ref.value == "path" and [c.value for c in ref.children] == ["module"]:
         return tail.value.lstrip("/")
     return None
+
+
+# --- template evaluation (templatefile) ---------------------------------------------------------------
+class TemplateError(ValueError):
+    pass
+
+
+def _apply_strip(parts: List[Node]) -> List[Node]:
+    """Terraform's ``~`` markers: remove the whitespace (newlines included) of the literal
+    next to the marked side."""
+    out = [Node(p.kind, p.value, p.children, p.pos, p.strip) for p in parts]
+    for i, p in enumerate(out):
+        if p.kind == "lit":
+            continue
+        left, right = p.strip
+        if left and i > 0 and out[i - 1].kind == "lit":
+            out[i - 1].value = out[i - 1].value.rstrip(" \t\r\n")
+        if right and i + 1 < len(out) and out[i + 1].kind == "lit":
+            out[i + 1].value = out[i + 1].value.lstrip(" \t\r\n")
+    return out
+
+
+_FUNCS = {
+    "length": lambda v: len(v),
+    "upper": lambda v: str(v).upper(),
+    "lower": lambda v: str(v).lower(),
+    "trimspace": lambda v: str(v).strip(),
+    "join": lambda sep, items: str(sep).join(str(x) for x in items),
+    "replace": lambda v, a, b: str(v).replace(str(a), str(b)),
+    "tostring": lambda v: _to_str(v),
+    "jsonencode": lambda v: __import__("json").dumps(v, separators=(",", ":")),
+    "base64encode": lambda v: __import__("base64").b64encode(str(v).encode()).decode(),
+    "keys": lambda m: sorted(m),
+    "values": lambda m: [m[k] for k in sorted(m)],
+    "element": lambda lst, i: lst[int(i) % len(lst)],
+    "contains": lambda lst, v: v in lst,
+}
+
+
+def _to_str(v: Any) -> str:
+    if isinstance(v, bool):
+        return "true" if v else "false"
+    if isinstance(v, float) and v.is_integer():
+        return str(int(v))
+    if isinstance(v, (dict, list)):
+        raise TemplateError(f"cannot interpolate a {type(v).__name__} into a string")
+    return str(v)
+
+
+def _num(v: Any) -> float:
+    if isinstance(v, bool):
+        raise TemplateError("a bool is not a number")
+    try:
+        return float(v)
+    except (TypeError, ValueError) as exc:
+        raise TemplateError(f"{v!r} is not a number") from exc
+
+
+def eval_expr(node: Node, env: Dict[str, Any]) -> Any:
+    """Evaluate the HCL expression subset templates use: literals, variables (with attribute
+    and index traversal), operators, conditionals, tuples/objects, string templates and a few
+    functions.  Unknown variables or functions raise :class:`TemplateError`, as Terraform does."""
+    k = node.kind
+    if k == "lit":
+        return node.value
+    if k == "paren":
+        return eval_expr(node.children[0], env)
+    if k == "trav":
+        if node.value is None:
+            base = eval_expr(node.children[0], env)
+            steps = node.children[1:]
+        else:
+            if node.value not in env:
+                raise TemplateError(f"undefined variable {node.value!r}")
+            base = env[node.value]
+            steps = node.children
+        for st in steps:
+            if st.kind == "attr":
+                base = base[st.value]
+            elif st.kind == "index":
+                key = eval_expr(st.children[0], env)
+                base = base[int(key)] if isinstance(base, list) else base[key]
+            else:
+                raise TemplateError(f"unsupported traversal {st.kind}")
+        return base
+    if k == "tmpl":
+        return render_parts(node.children, env)
+    if k == "unary":
+        v = eval_expr(node.children[0], env)
+        return (not v) if node.value == "!" else -_num(v)
+    if k == "op":
+        op = node.value
+        if op == "&&":
+            return bool(eval_expr(node.children[0], env)) and bool(eval_expr(node.children[1], env))
+        if op == "||":
+            return bool(eval_expr(node.children[0], env)) or bool(eval_expr(node.children[1], env))
+        a, b = eval_expr(node.children[0], env), eval_expr(node.children[1], env)
+        if op == "==":
+            return a == b
+        if op == "!=":
+            return a != b
+        ops = {"<": lambda x, y: x < y, ">": lambda x, y: x > y, "<=": lambda x, y: x <= y, ">=": lambda x, y: x >= y,
+               "+": lambda x, y: x + y, "-": lambda x, y: x - y, "*": lambda x, y: x * y, "/": lambda x, y: x / y,
+               "%": lambda x, y: x % y}
+        if op not in ops:
+            raise TemplateError(f"unsupported operator {op}")
+        r = ops[op](_num(a), _num(b))
+        return r
+    if k == "cond":
+        return eval_expr(node.children[1] if eval_expr(node.children[0], env) else node.children[2], env)
+    if k == "tuple":
+        return [eval_expr(c, env) for c in node.children]
+    if k == "object":
+        out = {}
+        for item in node.children:
+            key = item.children[0]
+            kv = key.value if key.kind == "trav" and not key.children else eval_expr(key, env)
+            out[kv] = eval_expr(item.children[1], env)
+        return out
+    if k == "call":
+        fn = _FUNCS.get(node.value)
+        if fn is None:
+            raise TemplateError(f"function {node.value}() is not supported by this evaluator")
+        return fn(*[eval_expr(c, env) for c in node.children])
+    raise TemplateError(f"unsupported expression {k}")
+
+
+def render_parts(parts: List[Node], env: Dict[str, Any]) -> str:
+    parts = _apply_strip(parts)
+    out: List[str] = []
+
+    def run(i: int, end_kinds: Tuple[str, ...], emit: bool) -> int:
+        while i < len(parts):
+            p = parts[i]
+            if p.kind in end_kinds:
+                return i
+            if p.kind == "lit":
+                if emit:
+                    out.append(p.value)
+                i += 1
+            elif p.kind == "interp":
+                if emit:
+                    out.append(_to_str(eval_expr(p.children[0], env)))
+                i += 1
+            elif p.kind == "if":
+                cond = bool(eval_expr(p.children[0], env)) if emit else False
+                j = run(i + 1, ("else", "endif"), emit and cond)
+                if parts[j].kind == "else":
+                    j = run(j + 1, ("endif",), emit and not cond)
+                i = j + 1
+            elif p.kind == "tfor":
+                coll = eval_expr(p.children[0], env) if emit else []
+                names = p.value
+                body_end = _matching_endfor(parts, i)
+                items = list(coll.items()) if isinstance(coll, dict) else list(enumerate(coll))
+                if isinstance(coll, dict):
+                    items = sorted(items)
+                for key, val in items if emit else []:
+                    saved = dict(env)
+                    if len(names) == 2:
+                        env[names[0]], env[names[1]] = key, val
+                    else:
+                        env[names[0]] = val
+                    run(i + 1, ("endfor",), True)
+                    env.clear()
+                    env.update(saved)
+                i = body_end + 1
+            else:
+                raise TemplateError(f"unexpected {p.kind}")
+        return i
+
+    run(0, (), True)
+    return "".join(out)
+
+
+def _matching_endfor(parts: List[Node], i: int) -> int:
+    depth = 0
+    for j in range(i, len(parts)):
+        if parts[j].kind == "tfor":
+            depth += 1
+        elif parts[j].kind == "endfor":
+            depth -= 1
+            if depth == 0:
+                return j
+    raise TemplateError("%{for} without %{endfor}")
+
+
+def templatefile(src: str, variables: Dict[str, Any], name: str = "<template>") -> str:
+    """Terraform's ``templatefile(path, vars)`` over template source ``src``."""
+    return render_parts(parse_template(src, name), dict(variables))
