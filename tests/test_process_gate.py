@@ -118,3 +118,44 @@ def test_mixed_agent_and_process_nodes_share_one_gate(tools):
         assert agent._gates == {}  # the agent's communicator was consumed, nothing pending
     finally:
         agent.stop()
+
+
+def test_spec_from_state_routes_each_delivery_kind():
+    """All-agent clusters keep the pipelined agent gate; SSH-only clusters get the process
+    gate; mixed clusters get one process gate whose agent members join via their API."""
+    import json as _json
+
+    from triton_kubernetes_amd.backend import MemoryBackend
+    from triton_kubernetes_amd.readiness.waiter import spec_from_state
+    from triton_kubernetes_amd.state import State
+    from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+    from triton_kubernetes_amd.terraform.catalog import module_source as _src
+
+    def module_source(name):
+        return _src(MODULES_DIR, name, "")
+
+    def state_with(hosts):
+        st = State("m", {})
+        st.set_manager({"source": module_source("bare-metal-rancher")})
+        key = st.add_cluster("baremetal", "c", {"source": module_source("bare-metal-rancher-k8s"), "name": "c"})
+        for i, h in enumerate(hosts):
+            st.add_node(key, f"g-{i}", {"source": module_source("bare-metal-mi355x-rancher-k8s-host"),
+                                        "hostname": f"g-{i}", "host": h, "gpu_count": 8, "ssh_user": "u"})
+        return st, key
+
+    be = MemoryBackend()
+    be.write_tfstate("m", _json.dumps({"module_outputs": {
+        "cluster-manager": {"rancher_url": "http://r", "rancher_access_key": "a", "rancher_secret_key": "s"},
+        "cluster_baremetal_c": {"rancher_cluster_id": "c-1"}}}).encode())
+    st, key = state_with(["agent+http://a:1", "agent+http://b:1"])
+    _, spec = spec_from_state(st, be, key, rccl_gate=True)
+    assert spec.rccl_gate and spec.rccl_hosts == ["http://a:1", "http://b:1"] and not spec.rccl_process_hosts
+    st, key = state_with(["10.0.0.1", "10.0.0.2"])
+    _, spec = spec_from_state(st, be, key, rccl_gate=True)
+    assert spec.rccl_gate and not spec.rccl_hosts and [h.address for h in spec.rccl_process_hosts] == ["10.0.0.1",
+                                                                                                      "10.0.0.2"]
+    st, key = state_with(["agent+http://a:1", "10.0.0.2"])
+    _, spec = spec_from_state(st, be, key, rccl_gate=True)
+    assert spec.rccl_gate and not spec.rccl_hosts and not spec.rccl_skip_reason
+    assert [h.address for h in spec.rccl_process_hosts] == ["agent+http://a:1", "10.0.0.2"]
+    assert spec.rccl_process_ndev == [8, 8]
