@@ -67,9 +67,10 @@ def have(binary: str) -> bool:
 
 def assert_blocks_match_modules(st) -> None:
     """Every module block of a rendered document points at a module directory that exists
-    (the packaged tree by default), every key it sets is a variable declared there, and
-    every required variable is set — read from the module's own .tf files with the HCL
-    parser, not from the generator's data."""
+    (the packaged tree by default), every key it sets is a variable declared there, every
+    required variable is set, and every value passes the variable's type and ``validation``
+    conditions — read from the module's own .tf files with the HCL parser and evaluator,
+    not from the generator's data."""
     import os
 
     from triton_kubernetes_amd.terraform import catalog, hcl
@@ -86,3 +87,6 @@ def assert_blocks_match_modules(st) -> None:
         assert not extra, f"{key} -> {info.name}: keys not declared as module variables: {sorted(extra)}"
         missing = rep.required - set(block)
         assert not missing, f"{key} -> {info.name}: required variables not set: {sorted(missing)}"
+        # what `terraform plan` would reject: types and the modules' own validation blocks
+        problems = hcl.check_inputs(mod_dir, block)
+        assert not problems, f"{key} -> {info.name}: {problems}"

@@ -126,3 +126,30 @@ def test_checker_catches_broken_fixture(tmp_path, case, edit, expect):
 def test_template_names_respect_for_bindings():
     parts = hcl.parse_template("%{ for x in items ~}${x}-${suffix}%{ endfor ~}${other.attr}")
     assert hcl.template_names(parts) == {"items", "suffix", "other"}
+
+
+def test_check_inputs_evaluates_the_modules_validations():
+    import os
+
+    from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+
+    mod = os.path.join(MODULES_DIR, "bare-metal-rancher-k8s")
+    base = {"name": "c", "rancher_api_url": "${module.cluster-manager.rancher_url}",
+            "rancher_access_key": "${module.cluster-manager.rancher_access_key}",
+            "rancher_secret_key": "${module.cluster-manager.rancher_secret_key}",
+            "k8s_version": "v1.28.10-rancher1-1", "k8s_network_provider": "calico"}
+    assert hcl.check_inputs(mod, base) == []
+    bad = hcl.check_inputs(mod, dict(base, k8s_version="v1.9.5-rancher1-1", k8s_network_provider="weird", extra=1))
+    assert any(e.startswith("k8s_version: k8s_version must be an RKE1 release") for e in bad), bad
+    assert any(e.startswith("k8s_network_provider:") for e in bad) and "unsupported argument 'extra'" in bad
+    assert "missing required argument 'name'" in hcl.check_inputs(mod, {k: v for k, v in base.items() if k != "name"})
+    mgr = os.path.join(MODULES_DIR, "bare-metal-rancher")
+    pw = {"name": "m", "host": "10.0.0.1", "rancher_admin_password": "short"}
+    assert any("at least 12 characters" in e for e in hcl.check_inputs(mgr, pw))
+    assert any("at least 12 characters" in e for e in hcl.check_inputs(mgr, dict(pw, rancher_admin_password="quote'pw123456")))
+    assert not [e for e in hcl.check_inputs(mgr, dict(pw, rancher_admin_password="long-enough-pw-1")) if "password" in e]
+    host = os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host")
+    errs = hcl.check_inputs(host, {"rancher_host_labels": {"worker": "true", "etcd": "true"}, "gpu_burnin": "max",
+                                   "gpu_count": "eight"})
+    assert any(e.startswith("rancher_host_labels:") for e in errs) and any(e.startswith("gpu_burnin:") for e in errs)
+    assert any("gpu_count: 'eight' is not a number" == e for e in errs), errs

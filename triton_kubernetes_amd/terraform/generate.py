@@ -1182,7 +1182,7 @@ resource "terraform_data" "install_rancher_agent" {{
     # MI355X bare-metal host
     mods.append(Module("bare-metal-mi355x-rancher-k8s-host", ["external"], HOST_BASE + [
         Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa"),
-        Var("gpu_product", "MI355X"), Var("gpu_count", "8", "GPUs the node must expose"),
+        Var("gpu_product", "MI355X"), Var("gpu_count", 8, "GPUs the node must expose"),
         Var("gpu_burnin", "quick", "quick | full | off"),
         Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
         Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)")],

@@ -802,6 +802,9 @@ _FUNCS = {
     "values": lambda m: [m[k] for k in sorted(m)],
     "element": lambda lst, i: lst[int(i) % len(lst)],
     "contains": lambda lst, v: v in lst,
+    "split": lambda sep, v: str(v).split(str(sep)),
+    "slice": lambda lst, a, b: list(lst)[int(a):int(b)],
+    "regexall": lambda pat, v: __import__("re").findall(str(pat), str(v)),
 }
 
 
@@ -956,3 +959,75 @@ def _matching_endfor(parts: List[Node], i: int) -> int:
 def templatefile(src: str, variables: Dict[str, Any], name: str = "<template>") -> str:
     """Terraform's ``templatefile(path, vars)`` over template source ``src``."""
     return render_parts(parse_template(src, name), dict(variables))
+
+
+def _var_type_ok(vtype: str, value: Any) -> bool:
+    """Terraform's conversion rules for the primitive / collection types the modules use."""
+    if isinstance(value, str) and "${" in value:
+        return True  # an interpolation: known only at apply time
+    if vtype == "string":
+        return isinstance(value, (str, int, float, bool))
+    if vtype == "number":
+        try:
+            float(value)
+            return not isinstance(value, bool)
+        except (TypeError, ValueError):
+            return False
+    if vtype == "bool":
+        return isinstance(value, bool) or str(value).lower() in ("true", "false")
+    if vtype.startswith("list("):
+        return isinstance(value, list)
+    if vtype.startswith("map("):
+        return isinstance(value, dict)
+    return True
+
+
+def check_inputs(module_dir: str, inputs: Dict[str, Any]) -> List[str]:
+    """What ``terraform plan`` would reject about one module call: unknown inputs, missing
+    required variables, values of the wrong type, and failing ``validation`` conditions
+    (evaluated with this module's evaluator).  Inputs that are interpolations
+    (``${module...}``) are only known at apply time and skip the value checks."""
+    rep = check_module(module_dir)
+    errors = list(rep.errors)
+    given = {k: v for k, v in inputs.items() if k != "source"}
+    errors += [f"unsupported argument {k!r}" for k in sorted(set(given) - rep.variables)]
+    errors += [f"missing required argument {k!r}" for k in sorted(rep.required - set(given))]
+    decls: Dict[str, Block] = {}
+    for body in rep.files.values():
+        for b in body.blocks:
+            if b.type == "variable" and b.labels:
+                decls[b.labels[0]] = b
+    values: Dict[str, Any] = {}
+    for name, blk in decls.items():
+        if name in given:
+            values[name] = given[name]
+        elif blk.body.attr("default") is not None:
+            try:
+                values[name] = eval_expr(blk.body.attr("default").expr, {})
+            except TemplateError:
+                values[name] = None
+    for name, blk in sorted(decls.items()):
+        if name not in given:
+            continue
+        v = given[name]
+        tattr = blk.body.attr("type")
+        if tattr is not None:
+            tname = tattr.expr.value if tattr.expr.kind == "trav" and not tattr.expr.children else \
+                (f"{tattr.expr.value}(string)" if tattr.expr.kind == "call" else "")
+            if tname and not _var_type_ok(tname, v):
+                errors.append(f"{name}: {v!r} is not a {tname}")
+        if isinstance(v, str) and "${" in v:
+            continue
+        for vb in blk.body.blocks:
+            if vb.type != "validation":
+                continue
+            cond = vb.body.attr("condition")
+            msg = vb.body.attr("error_message")
+            try:
+                ok = bool(eval_expr(cond.expr, {"var": values}))
+            except (TemplateError, KeyError, IndexError, TypeError) as exc:
+                errors.append(f"{name}: validation not evaluable: {exc}")
+                continue
+            if not ok:
+                errors.append(f"{name}: {eval_expr(msg.expr, {}) if msg is not None else 'invalid value'}")
+    return errors

@@ -97,8 +97,8 @@ variable "gpu_product" {
 
 variable "gpu_count" {
   description = "GPUs the node must expose"
-  type        = string
-  default     = "8"
+  type        = number
+  default     = 8
 }
 
 variable "gpu_burnin" {
