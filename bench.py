@@ -93,6 +93,7 @@ class AgentProc:
                                      start_new_session=True)
         self.url = ""
         self.runtime = ""
+        self.startup_ms = {}
         self.signalled = False
 
     def wait_url(self, timeout: float = 300.0) -> str:
@@ -112,6 +113,7 @@ class AgentProc:
                 doc = json.loads(line)
                 self.url = doc["listening"]
                 self.runtime = doc.get("hip_runtime", "")
+                self.startup_ms = doc.get("startup_ms", {})
         sel.close()
         return self.url
 
@@ -292,7 +294,7 @@ def main() -> int:
             procs = start_agents(f"s{i}")
             urls = gather_urls(procs)
         t_agents = time.perf_counter()
-        out = {"step": i}
+        out = {"step": i, "agent_startup_ms": {p.name: getattr(p, "startup_ms", {}) for p in procs}}
         if rank == 0:
             out.update(create(i, urls))
         t_ready = time.perf_counter()

@@ -451,23 +451,30 @@ class NodeAgent:
         slots = int(os.environ.get("TK_FD_TABLE", "16384") or 0)
         if slots > 0:
             procstat.presize_fd_table(slots)
+        t0 = time.perf_counter()
+        self.startup_ms: Dict[str, float] = {}
         if self.topology_override is not None or not self.devices:
             return
         from ..ops import probe, rccl, topo
 
         probe._lib()
         rccl._lib()
+        self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
         # burn-in arena: resident for the agent's lifetime, released after an idle period
         if os.environ.get("TK_PROBE_SCRATCH_CACHE", "1") != "0":
             level = os.environ.get("TK_PROBE_SCRATCH_LEVEL", "quick")
+            t1 = time.perf_counter()
             list(self._pool.map(lambda d: probe.prealloc_scratch(d, level), self.devices))
+            self.startup_ms["hip_init_arena"] = round((time.perf_counter() - t1) * 1e3, 1)
             idle_s = float(os.environ.get("TK_PROBE_SCRATCH_IDLE_S", "300") or 0)
             if idle_s > 0:
                 self._start_janitor(idle_s)
         quiet = float(os.environ.get("TK_TEARDOWN_QUIET_MS", "0") or 0)
         if quiet > 0:
             rccl.set_teardown_quiet_ms(quiet)
+        t2 = time.perf_counter()
         self._refill_uid()  # the first gate's unique id, ready before any request
+        self.startup_ms["uid"] = round((time.perf_counter() - t2) * 1e3, 1)
         try:
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later
@@ -624,6 +631,7 @@ def main(argv: Optional[List[str]] = None) -> int:
     """``tk-node-agent``: serve the agent API on a host (127.0.0.1 by default)."""
     import argparse
 
+    t_main = time.perf_counter()
     ap = argparse.ArgumentParser(prog="tk-node-agent")
     ap.add_argument("--listen", default="127.0.0.1:7946")
     ap.add_argument("--mode", default="exec", choices=MODES)
@@ -663,7 +671,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     from ..ops import native
 
     print(json.dumps({"listening": url, "token_from_file": bool(token),
-                      "hip_runtime": native._runtime_dir or "not loaded"}), flush=True)
+                      "hip_runtime": native._runtime_dir or "not loaded",
+                      "startup_ms": dict(getattr(agent, "startup_ms", {}),
+                                         main_to_serve=round((time.perf_counter() - t_main) * 1e3, 1))}),
+          flush=True)
     while not agent.shutdown_requested.wait(3600):
         pass
     t0 = time.perf_counter()
