@@ -194,7 +194,7 @@ def main() -> int:
 
     # which agents this rank owns: (name, devices).  Unmasked: rank 0 owns every worker
     # agent; masked (each rank sees one GPU): every rank owns a 1-GPU agent.
-    masked = not args.sim_gpu and visible < n_gpus
+    masked = (not args.sim_gpu and visible < n_gpus) or os.environ.get("TK_BENCH_ASSUME_MASKED") == "1"
     if masked:
         workers = n_gpus
         mine = [(f"mi355x-{rank}", [0])]

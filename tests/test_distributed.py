@@ -68,3 +68,16 @@ def test_bench_inproc_agents():
     assert proc.returncode == 0, proc.stderr[-2000:]
     doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
     assert doc["warm_create_to_ready_s"] is None and "bench process" in doc["config"]["start"]
+
+
+def test_bench_masked_launcher_one_agent_per_rank():
+    """A launcher that masks devices per rank: every rank starts a 1-GPU agent, and the
+    cluster has one worker per rank (the gate then spans the ranks' agents)."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "1", "--warmup", "0", "--warm-steps", "0", "--sim-gpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", TK_BENCH_ASSUME_MASKED="1")
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][0])
+    assert doc["config"]["workers"] == 2 and doc["config"]["gpus_per_worker"] == 1
