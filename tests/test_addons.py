@@ -144,7 +144,9 @@ def test_webhook_patch_for_gpu_pods():
     assert out["metadata"]["annotations"] == {"team": "a", "amd.com/rccl-env": "injected"}
     # idempotent (re-invocation), opt-out, zero GPUs, non-GPU pods
     assert webhook.patch_for_pod(out, env) == []
-    assert webhook.patch_for_pod(_gpu_pod(annotations={"amd.com/rccl-env-inject": "false"}), env) == []
+    # env opt-out: only the xGMI placement of an 8-GPU pod remains
+    assert [o["path"] for o in webhook.patch_for_pod(_gpu_pod(annotations={"amd.com/rccl-env-inject": "false"}),
+                                                     env)] == ["/spec/affinity"]
     assert webhook.patch_for_pod(_gpu_pod(gpus="0"), env) == []
     plain = {"metadata": {"name": "web"}, "spec": {"containers": [{"name": "c", "image": "nginx"}]}}
     assert webhook.patch_for_pod(plain, env) == []
@@ -211,6 +213,11 @@ def test_injector_end_to_end_through_admission(tmp_path):
         env = {e["name"]: e["value"] for e in created["spec"]["containers"][0]["env"]}
         assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["TK_RCCL_ENV_FILE"] == "/etc/rccl/rccl.env"
         assert created["metadata"]["annotations"]["amd.com/rccl-env"] == "injected"
+        # and the 8-GPU pod must land on one fully connected xGMI hive
+        terms = created["spec"]["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][
+            "nodeSelectorTerms"]
+        assert terms == [{"matchExpressions": [{"key": "amd.com/xgmi.fully-connected", "operator": "In",
+                                                "values": ["true"]}]}]
         # kube-system is excluded by the namespace selector; CPU pods are untouched
         sys_pod = client.k8s(cid, "POST", "/api/v1/namespaces/kube-system/pods", _gpu_pod("sys"), ok=(201,))
         assert "env" not in sys_pod["spec"]["containers"][0]
@@ -273,3 +280,30 @@ def test_injector_certificate_is_kept_across_applies():
         assert fresh == {}
     finally:
         fake.stop()
+
+
+def test_webhook_xgmi_placement():
+    env = {"NCCL_DEBUG": "WARN"}
+    # 8 GPUs: the pod's own required terms each gain the fully-connected hive constraint
+    pod = _gpu_pod(gpus="8")
+    pod["metadata"]["labels"] = {"amd.com/xgmi-group": "llama-70b"}
+    pod["spec"]["affinity"] = {"nodeAffinity": {"requiredDuringSchedulingIgnoredDuringExecution": {
+        "nodeSelectorTerms": [{"matchExpressions": [{"key": "zone", "operator": "In", "values": ["a"]}]},
+                              {"matchExpressions": [{"key": "zone", "operator": "In", "values": ["b"]}]}]}}}
+    out = webhook.apply_patch(pod, webhook.patch_for_pod(pod, env))
+    terms = out["spec"]["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][
+        "nodeSelectorTerms"]
+    assert all({"key": "amd.com/xgmi.fully-connected", "operator": "In", "values": ["true"]} in t["matchExpressions"]
+               for t in terms) and [t["matchExpressions"][0]["values"] for t in terms] == [["a"], ["b"]]
+    pref = out["spec"]["affinity"]["podAffinity"]["preferredDuringSchedulingIgnoredDuringExecution"]
+    assert pref == [{"weight": 100, "podAffinityTerm": {"labelSelector": {"matchLabels": {
+        "amd.com/xgmi-group": "llama-70b"}}, "topologyKey": "amd.com/xgmi.hive-id"}}]
+    assert webhook.placement_affinity(out) is None  # idempotent on re-invocation
+    # 1 GPU, no group: no placement; opt-outs are independent
+    one = webhook.apply_patch(_gpu_pod(gpus="1"), webhook.patch_for_pod(_gpu_pod(gpus="1"), env))
+    assert "affinity" not in one["spec"]
+    no_env = _gpu_pod(gpus="8", annotations={"amd.com/rccl-env-inject": "false"})
+    ops = webhook.patch_for_pod(no_env, env)
+    assert [o["path"] for o in ops] == ["/spec/affinity"]
+    no_place = _gpu_pod(gpus="8", annotations={"amd.com/xgmi-placement": "false"})
+    assert "/spec/affinity" not in [o["path"] for o in webhook.patch_for_pod(no_place, env)]

@@ -10,9 +10,15 @@ container) gets, at admission time:
 * the node's own ``/etc/rccl`` (written by the node bootstrap: discovered RDMA ports,
   per-node overrides) mounted read-only at ``/etc/rccl`` plus ``TK_RCCL_ENV_FILE``
   pointing at ``/etc/rccl/rccl.env``, so launchers can source the node values on top;
-* the annotation ``amd.com/rccl-env: injected``.
+* the annotation ``amd.com/rccl-env: injected``;
+* xGMI-aware placement (the BASELINE north star's "xGMI-topology-aware pod affinity"):
+  a pod asking for 2+ GPUs must land on a node whose GPUs form one fully connected xGMI
+  hive (``amd.com/xgmi.fully-connected=true``, added to every required node-selector term,
+  so a pod's own terms still apply), and pods sharing an ``amd.com/xgmi-group`` label
+  prefer the same hive (pod affinity on ``amd.com/xgmi.hive-id``).
 
-A pod opts out with the annotation ``amd.com/rccl-env-inject: "false"``.  The
+A pod opts out of the env with the annotation ``amd.com/rccl-env-inject: "false"`` and of
+the placement with ``amd.com/xgmi-placement: "false"``.  The
 ConfigMap lives in ``kube-system``; ``envFrom`` cannot reach across namespaces, which
 is why the values are injected literally.
 
@@ -39,6 +45,10 @@ MARK = "amd.com/rccl-env"
 VOLUME = "tk-node-rccl-env"
 NODE_DIR = "/etc/rccl"
 ENV_FILE_VAR = "TK_RCCL_ENV_FILE"
+PLACEMENT_OPT_OUT = "amd.com/xgmi-placement"
+GROUP_LABEL = "amd.com/xgmi-group"
+HIVE_KEY = "amd.com/xgmi.hive-id"
+FULLY_CONNECTED = {"key": "amd.com/xgmi.fully-connected", "operator": "In", "values": ["true"]}
 
 
 def _esc(key: str) -> str:
@@ -59,6 +69,53 @@ def _wants_gpu(container: Dict[str, Any]) -> bool:
     return False
 
 
+def _gpu_count(container: Dict[str, Any]) -> int:
+    res = container.get("resources") or {}
+    for part in ("limits", "requests"):
+        v = (res.get(part) or {}).get(GPU_RESOURCE)
+        if v is not None:
+            try:
+                return int(str(v))
+            except ValueError:
+                return 0
+    return 0
+
+
+def placement_affinity(pod: Dict[str, Any]) -> Optional[Dict[str, Any]]:
+    """The pod's ``spec.affinity`` with the xGMI placement added; None when nothing changes."""
+    meta = pod.get("metadata") or {}
+    if str((meta.get("annotations") or {}).get(PLACEMENT_OPT_OUT, "")).lower() == "false":
+        return None
+    spec = pod.get("spec") or {}
+    # GPUs the pod holds at once: its app containers together, or its largest init container
+    gpus = max(sum(_gpu_count(c) for c in spec.get("containers") or []),
+               max([_gpu_count(c) for c in spec.get("initContainers") or []], default=0))
+    group = (meta.get("labels") or {}).get(GROUP_LABEL)
+    if gpus < 2 and not group:
+        return None
+    aff = json.loads(json.dumps(spec.get("affinity") or {}))
+    changed = False
+    if gpus >= 2:
+        na = aff.setdefault("nodeAffinity", {})
+        req = na.setdefault("requiredDuringSchedulingIgnoredDuringExecution", {})
+        terms = req.setdefault("nodeSelectorTerms", [])
+        if not terms:
+            terms.append({})
+        for term in terms:  # terms are ORed: the hive constraint goes into each
+            exprs = term.setdefault("matchExpressions", [])
+            if not any(e.get("key") == FULLY_CONNECTED["key"] for e in exprs):
+                exprs.append(dict(FULLY_CONNECTED, values=list(FULLY_CONNECTED["values"])))
+                changed = True
+    if group:
+        pa = aff.setdefault("podAffinity", {})
+        pref = pa.setdefault("preferredDuringSchedulingIgnoredDuringExecution", [])
+        if not any((t.get("podAffinityTerm") or {}).get("topologyKey") == HIVE_KEY for t in pref):
+            pref.append({"weight": 100, "podAffinityTerm": {
+                "labelSelector": {"matchLabels": {GROUP_LABEL: group}}, "topologyKey": HIVE_KEY}})
+            changed = True
+    return aff if changed else None
+
+
 def load_env(env_dir: str) -> Dict[str, str]:
     """A ConfigMap mounted as a directory: one file per key (``..data`` links skipped)."""
     out: Dict[str, str] = {}
@@ -74,7 +131,18 @@ def load_env(env_dir: str) -> Dict[str, str]:
 
 
 def patch_for_pod(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
-    """RFC 6902 operations that inject ``env`` into ``pod``'s GPU containers ([] = none)."""
+    """RFC 6902 operations for a pod: the RCCL env on its GPU containers and the xGMI
+    placement ([] = nothing to change)."""
+    ops = _env_ops(pod, env)
+    spec = pod.get("spec") or {}
+    if any(_wants_gpu(c) for kind in ("initContainers", "containers") for c in spec.get(kind) or []):
+        aff = placement_affinity(pod)
+        if aff is not None:
+            ops.append({"op": "add", "path": "/spec/affinity", "value": aff})
+    return ops
+
+
+def _env_ops(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
     meta = pod.get("metadata") or {}
     annotations = meta.get("annotations") or {}
     if str(annotations.get(OPT_OUT, "")).lower() == "false" or annotations.get(MARK) == "injected":
