@@ -166,6 +166,25 @@ def test_process_gate_two_nodes_rendezvous_and_fail_fast(tmp_path):
     assert time.monotonic() - t0 < 60
 
 
+def test_link_check_on_this_box(tmp_path):
+    """The per-link xGMI check: on a one-GPU box it reports "single GPU" (exit 0, empty
+    labels); the copy primitive it times still runs (device to itself)."""
+    from triton_kubernetes_amd.ops import probe
+    from triton_kubernetes_amd.ops.native import executable
+
+    labels = tmp_path / "links"
+    proc = subprocess.run([executable("gpu-burnin"), "--p2p", "--labels", str(labels)], capture_output=True,
+                          text=True, timeout=120)
+    assert proc.returncode == 0, proc.stderr
+    doc = json.loads(proc.stdout.strip().splitlines()[-1])
+    if probe.device_count() < 2:
+        assert doc == {"skipped": "single GPU"} and labels.read_text() == ""
+    else:
+        assert doc["status"] == "passed" and "amd.com/xgmi.link-check=passed" in labels.read_text()
+    r = probe.p2p_bandwidth(0, 0, 64 << 20, 3)
+    assert r["gbps"] > 100  # a device-local copy through the same path
+
+
 def test_topology_amdsmi():
     from triton_kubernetes_amd.ops import topo
 

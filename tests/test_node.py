@@ -29,7 +29,7 @@ def test_plan_steps_and_order():
                                rancher_registry_password="p"), "https://r", "tok", "sum", mi355x=True)
     # burn-in precedes labels so the agent's topology prefetch overlaps it
     assert gpu.step_names() == ["firewall", "runtime", "hostname", "registry_login", "gpu_preflight",
-                                "gpu_burnin", "gpu_labels", "rccl_env", "rccl_local", "agent"]
+                                "gpu_burnin", "gpu_links", "gpu_labels", "rccl_env", "rccl_local", "agent"]
     assert gpu.gpu == {"product": "MI355X", "count": 8, "burnin": "quick"}
     off = build_host_plan(dict(GPU_WORKER, gpu_burnin="off", gpu_count=1), "https://r", "t", "s", mi355x=True)
     assert "gpu_burnin" not in off.step_names() and "rccl_local" not in off.step_names()
@@ -305,3 +305,30 @@ def test_shell_plan_carries_burnin_labels():
     assert "gpu-burnin --all --level full --labels /tmp/tk-burnin-labels" in script
     assert f"sudo rm -f {BURNIN_LABEL_FILE}" in script
     assert f"[ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}" in script
+
+
+def test_link_labels_verdicts():
+    from triton_kubernetes_amd.node.labels import link_labels
+
+    pairs = {f"{i}-{j}": 60.0 for i in range(4) for j in range(4) if i != j}
+    ok = link_labels({"pairs": pairs, "peer_access": {p: True for p in pairs}})
+    assert ok["status"] == "passed" and ok["labels"]["amd.com/xgmi.p2p-min-gbps"] == "60"
+    bad = dict(pairs, **{"2-3": 20.0})
+    v = link_labels({"pairs": bad, "peer_access": {p: True for p in bad}})
+    assert v["status"] == "degraded" and v["degraded"] == ["2-3"] and v["labels"]["amd.com/xgmi.link-check"] == "degraded"
+    err = link_labels({"pairs": pairs, "peer_access": dict({p: True for p in pairs}, **{"0-1": False})})
+    assert err["status"] == "error"
+    assert link_labels({"pairs": {}, "errors": []})["status"] == "skipped"
+
+
+def test_multi_gpu_plan_checks_links():
+    from triton_kubernetes_amd.node.plan import build_host_plan
+
+    cfg = {"hostname": "g", "rancher_host_labels": {"worker": "true"}, "gpu_count": 8, "gpu_burnin": "quick",
+           "gpu_link_min_frac": 0.6}
+    plan = build_host_plan(cfg, "https://r", "tok", "ca", mi355x=True)
+    names = plan.step_names()
+    assert names.index("gpu_burnin") < names.index("gpu_links") < names.index("gpu_labels")
+    assert "gpu-burnin --p2p --min-link-frac 0.6" in plan.render_shell()
+    one = build_host_plan(dict(cfg, gpu_count=1), "https://r", "tok", "ca", mi355x=True)
+    assert "gpu_links" not in one.step_names()

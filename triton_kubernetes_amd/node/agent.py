@@ -54,7 +54,7 @@ from ..parallel.rccl_env import render_env_file, site_env_from_topology
 from ..rancher.fake import tunnel_params
 from ..utils import procstat
 from ..utils.trace import span
-from .labels import burnin_labels, labels_from_topology
+from .labels import burnin_labels, labels_from_topology, link_labels
 from .plan import BootstrapPlan, Step
 
 MODES = ("sim", "exec")
@@ -252,6 +252,20 @@ class NodeAgent:
             # what the burn-in covered travels with the node (level, HBM held by the memtest)
             ctx["labels"].update(burnin_labels(level, results))
             return out
+        if a == "gpu_links":
+            # every ordered GPU pair's peer copy, one at a time: a degraded xGMI link fails the
+            # node; a pair the runtime cannot measure is recorded, not fatal
+            if len(self.devices) < 2:
+                return {"skipped": "single GPU"}
+            if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
+                return {"simulated": True}
+            from ..ops import probe
+
+            verdict = link_labels(probe.link_matrix(self.devices), float(step.params.get("min_frac", 0.5)))
+            ctx["labels"].update(verdict["labels"])
+            if verdict["status"] == "degraded":
+                raise StepFailed(step.name, f"degraded xGMI links: {verdict['degraded']}")
+            return verdict
         if a == "rccl_env":
             # discovered inter-node settings, then the configured values (which win)
             env = site_env_from_topology(ctx.get("topology") or {})

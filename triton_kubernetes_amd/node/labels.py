@@ -132,6 +132,25 @@ def burnin_labels(level: str, results: Dict[Any, Dict[str, Any]]) -> Dict[str, s
             "amd.com/gpu.burnin-hbm-tested-pct": f"{100.0 * frac:.1f}"}
 
 
+def link_labels(matrix: Dict[str, Any], min_frac: float = 0.5) -> Dict[str, Any]:
+    """Verdict and labels of a node's peer-to-peer link matrix (``ops/probe.py:link_matrix``
+    or ``gpu-burnin --p2p``): a pair below ``min_frac`` of the node's median is a degraded
+    xGMI link; a pair without peer access or whose copy failed is an error.  Returns
+    ``{"labels": {...}, "degraded": [...], "status": passed|degraded|error}``."""
+    vals = sorted(matrix.get("pairs", {}).values())
+    errors = list(matrix.get("errors", []))
+    errors += [f"{p}: no peer access" for p, ok in sorted(matrix.get("peer_access", {}).items()) if not ok]
+    if not vals:
+        return {"labels": {}, "degraded": [], "status": "error" if errors else "skipped"}
+    median = vals[len(vals) // 2] if len(vals) % 2 else 0.5 * (vals[len(vals) // 2 - 1] + vals[len(vals) // 2])
+    degraded = sorted(p for p, v in matrix["pairs"].items() if v < min_frac * median)
+    status = "error" if errors else ("degraded" if degraded else "passed")
+    labels = {"amd.com/xgmi.link-check": status,
+              "amd.com/xgmi.p2p-min-gbps": f"{vals[0]:.0f}",
+              "amd.com/xgmi.p2p-median-gbps": f"{median:.0f}"}
+    return {"labels": labels, "degraded": degraded, "errors": errors, "status": status}
+
+
 def agent_label_flags(labels: Dict[str, str]) -> List[str]:
     """``--label k=v`` arguments for ``rancher/agent``."""
     out: List[str] = []

@@ -198,6 +198,12 @@ sudo mkdir -p /etc/triton-kubernetes
 {TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
 sudo install -m 0644 /tmp/tk-burnin-labels {BURNIN_LABEL_FILE}""",
                                    {"level": burnin}, gpu=True))
+        if ngpu > 1:
+            # per-link xGMI health: peer copy bandwidth of every GPU pair vs the node's median
+            frac = float(cfg.get("gpu_link_min_frac", 0.5) or 0.5)
+            plan.steps.append(Step("gpu_links", "gpu_links", f"""
+{TOOLS_DIR}/gpu-burnin --p2p --min-link-frac {frac} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
+cat /tmp/tk-link-labels | sudo tee -a {BURNIN_LABEL_FILE} >/dev/null""", {"min_frac": frac}, gpu=True))
         plan.steps.append(Step("gpu_labels", "gpu_labels", f"""
 sudo mkdir -p "$(dirname {LABEL_FILE})"
 {TOOLS_DIR}/amdgpu-topo-labeller | sudo tee {TOPOLOGY_FILE} >/dev/null

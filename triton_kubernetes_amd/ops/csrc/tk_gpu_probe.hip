@@ -883,10 +883,61 @@ extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inje
 extern "C" int tkg_screen_fp8(int dev, int M, int N, int K, int reps, long long inject, double* out);
 extern "C" const char* tkg_last_error();
 
+// --p2p: peer copy bandwidth of every ordered GPU pair, one pair at a time (each number is
+// one xGMI link's), against the node's median; same keys and verdict as
+// node/labels.py:link_labels.  A degraded link exits 1; a pair the runtime cannot measure
+// is reported as an error (exit 0: the node agent path treats it the same way).
+static int p2p_main(const char* labels_path, double min_frac) {
+  int n = 0;
+  if (tkp_device_count(&n) != 0 || n < 1) {
+    printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    return 2;
+  }
+  if (n < 2) {
+    printf("{\"skipped\":\"single GPU\"}\n");
+    if (labels_path) { FILE* f = fopen(labels_path, "w"); if (f) fclose(f); }
+    return 0;
+  }
+  std::vector<double> vals;
+  int errors = 0, no_peer = 0;
+  printf("{\"pairs\":{");
+  bool first = true;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (i == j) continue;
+      double out[2] = {0, 0};
+      if (tkp_p2p_bandwidth(i, j, 64ull << 20, 3, out) != 0) { ++errors; continue; }
+      if (out[1] == 0.0) ++no_peer;
+      vals.push_back(out[0]);
+      printf("%s\"%d-%d\":%.1f", first ? "" : ",", i, j, out[0]);
+      first = false;
+    }
+  std::vector<double> sorted = vals;
+  std::sort(sorted.begin(), sorted.end());
+  const size_t m = sorted.size();
+  const double median = m == 0 ? 0.0 : (m % 2 ? sorted[m / 2] : 0.5 * (sorted[m / 2 - 1] + sorted[m / 2]));
+  int degraded = 0;
+  for (double v : vals) degraded += v < min_frac * median;
+  const char* status = (errors || no_peer || m == 0) ? "error" : (degraded ? "degraded" : "passed");
+  printf("},\"min_gbps\":%.1f,\"median_gbps\":%.1f,\"degraded\":%d,\"errors\":%d,\"no_peer_access\":%d,"
+         "\"status\":\"%s\"}\n", m ? sorted[0] : 0.0, median, degraded, errors, no_peer, status);
+  if (labels_path && m) {
+    FILE* f = fopen(labels_path, "w");
+    if (!f) { fprintf(stderr, "cannot write %s\n", labels_path); return 2; }
+    fprintf(f, "amd.com/xgmi.link-check=%s\n", status);
+    fprintf(f, "amd.com/xgmi.p2p-min-gbps=%.0f\n", sorted[0]);
+    fprintf(f, "amd.com/xgmi.p2p-median-gbps=%.0f\n", median);
+    fclose(f);
+  }
+  return degraded ? 1 : 0;
+}
+
 int main(int argc, char** argv) {
   int dev = 0, all = 0;
   const char* level = "quick";
   const char* labels_path = nullptr;  // --labels FILE: node labels recording what was tested
+  int p2p = 0;                        // --p2p: per-link peer copy matrix instead of the burn-in
+  double min_link_frac = 0.5;
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
   for (int i = 1; i < argc; ++i) {
@@ -899,7 +950,10 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--min-gemm-tflops") && i + 1 < argc) min_gemm = atof(argv[++i]);
     else if (!strcmp(argv[i], "--min-gemm-fp8-tflops") && i + 1 < argc) min_gemm8 = atof(argv[++i]);
     else if (!strcmp(argv[i], "--labels") && i + 1 < argc) labels_path = argv[++i];
+    else if (!strcmp(argv[i], "--p2p")) p2p = 1;
+    else if (!strcmp(argv[i], "--min-link-frac") && i + 1 < argc) min_link_frac = atof(argv[++i]);
   }
+  if (p2p) return p2p_main(labels_path, min_link_frac);
   const bool full = !strcmp(level, "full");
   const size_t hbm_bytes = full ? (16ull << 30) : (1ull << 30);
   // quick: 1 GiB; full: every free byte of HBM but 4 GiB, in 16 GiB chunks held at once

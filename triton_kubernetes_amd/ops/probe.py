@@ -9,7 +9,7 @@ fails a threshold or the memtest marks the node not-ready.
 
 import ctypes
 from dataclasses import asdict, dataclass, field
-from typing import Any, Dict, List, Optional
+from typing import Any, Dict, List, Optional, Sequence
 
 from ..utils.trace import span
 from .native import load
@@ -166,6 +166,27 @@ def p2p_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 5) -
     out = (ctypes.c_double * 2)()
     _check(_lib().tkp_p2p_bandwidth(src, dst, nbytes, iters, out), "p2p_bandwidth")
     return {"gbps": out[0], "peer_access": bool(out[1])}
+
+
+def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3) -> Dict[str, Any]:
+    """Peer-to-peer copy bandwidth of every ordered GPU pair, one pair at a time (so each
+    number is one xGMI link's, not a share of a busy fabric): ``{"pairs": {"i-j": GB/s},
+    "peer_access": {"i-j": bool}, "errors": [...]}``.  A pair whose copy fails is recorded
+    as an error, not raised: the caller decides (``node/labels.py:link_labels``)."""
+    pairs: Dict[str, float] = {}
+    access: Dict[str, bool] = {}
+    errors: List[str] = []
+    for i in devices:
+        for j in devices:
+            if i == j:
+                continue
+            try:
+                r = p2p_bandwidth(i, j, nbytes, iters)
+                pairs[f"{i}-{j}"] = round(r["gbps"], 1)
+                access[f"{i}-{j}"] = r["peer_access"]
+            except ProbeError as exc:
+                errors.append(f"{i}->{j}: {exc}")
+    return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes}
 
 
 # --- burn-in policy ------------------------------------------------------------------
