@@ -52,3 +52,7 @@ fi
 if [ "$MODE" = kload ]; then
   step rccl_kernel_load 300 python scripts/rccl_kernel_load.py
 fi
+if [ "$MODE" = full ]; then
+  step bench_full 600 python bench.py --steps 3 --warmup 1 --warm-steps 0 --burnin full
+  TK_HIP_RUNTIME=system step bench_system 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
+fi
