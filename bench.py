@@ -276,6 +276,16 @@ def main() -> int:
         ctx.extras["agent_transport"] = AgentTransport(token=token)
         wf.new_cluster(ctx, backend)
         out = {}
+        report = ctx.extras.get("last_apply")
+        if report is not None:  # the GPU nodes' plan steps as the agents timed them
+            steps = {}
+            for key, run in report.runs.items():
+                detail = run.detail if isinstance(run.detail, dict) else {}
+                if run.info.mi355x:
+                    for st in detail.get("steps", []) or []:
+                        steps[st.get("name")] = max(steps.get(st.get("name"), 0.0), float(st.get("ms") or 0.0))
+            if steps:
+                out["gpu_node_step_ms"] = {k: round(v, 1) for k, v in steps.items()}
         rep = ctx.extras.get("last_readiness")
         if rep is not None:
             out["phase_s"] = rep.to_json()["phase_seconds"]
@@ -364,6 +374,9 @@ def main() -> int:
             if sp["name"].startswith(("ready.", "module.", "direct.apply", "apply", "bench.")):
                 phases.setdefault(sp["name"], []).append(sp["duration"])
         phase_ms = {k: round(sum(v) / max(1, args.steps) * 1000.0, 2) for k, v in sorted(phases.items())}
+        node_steps = [r["gpu_node_step_ms"] for r in results if "gpu_node_step_ms" in r]
+        for name in sorted({k for ns in node_steps for k in ns}):
+            phase_ms[f"gpu_node.{name}"] = round(sum(ns.get(name, 0.0) for ns in node_steps) / len(node_steps), 2)
         gate = [r["rccl"] for r in results if "rccl" in r]
         for k in ("init_total", "init_wait", "sweep"):
             if gate:

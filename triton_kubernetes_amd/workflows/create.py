@@ -56,6 +56,7 @@ def apply_and_persist(ctx: Context, backend: Backend, state: State, new_modules:
             with span("apply", executor=executor.name, modules=len(new_modules)):
                 executor.apply(state, backend)
         except BaseException as exc:
+            ctx.extras["last_apply"] = getattr(executor, "last_report", None)
             backend.persist_state(state)
             _write_status(backend, state.name, {"phase": "apply_failed", "modules": new_modules,
                                                 "error": str(exc), "time": time.time()})
@@ -63,6 +64,8 @@ def apply_and_persist(ctx: Context, backend: Backend, state: State, new_modules:
                 raise TKError(f"{exc}\n(desired state persisted; re-run to resume or destroy to clean up)") \
                     from exc
             raise
+        # per-module results (the DirectExecutor's report: node plans' step timings) for callers
+        ctx.extras["last_apply"] = getattr(executor, "last_report", None)
         backend.persist_state(state)
         _write_status(backend, state.name, {"phase": "applied", "modules": new_modules, "time": time.time()})
 
