@@ -56,3 +56,10 @@ if [ "$MODE" = full ]; then
   step bench_full 600 python bench.py --steps 3 --warmup 1 --warm-steps 0 --burnin full
   TK_HIP_RUNTIME=system step bench_system 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
 fi
+if [ "$MODE" = steps ]; then
+  step bench_steps 300 python bench.py --steps 3 --warmup 1 --warm-steps 0
+  step bench_steps_full 600 python bench.py --steps 2 --warmup 1 --warm-steps 0 --burnin full
+fi
+if [ "$MODE" = span ]; then
+  step memtest_span 300 python scripts/memtest_span_chunks.py
+fi

@@ -474,6 +474,8 @@ class NodeAgent:
         probe._lib()
         rccl._lib()
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
+        # the full burn-in's ~300 GB memtest memory is released off the bring-up path
+        probe.set_async_free(True)
         # burn-in arena: resident for the agent's lifetime, released after an idle period
         if os.environ.get("TK_PROBE_SCRATCH_CACHE", "1") != "0":
             level = os.environ.get("TK_PROBE_SCRATCH_LEVEL", "quick")
@@ -639,6 +641,10 @@ class NodeAgent:
             from ..ops import rccl
 
             rccl.drain()
+        if self.devices and self.topology_override is None and self.burnin_override is None:
+            from ..ops import probe
+
+            probe.wait_frees()
 
 
 def main(argv: Optional[List[str]] = None) -> int:

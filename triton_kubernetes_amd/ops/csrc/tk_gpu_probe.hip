@@ -29,6 +29,9 @@
 #include <hip/hip_runtime.h>
 
 #include <array>
+#include <atomic>
+#include <thread>
+#include <condition_variable>
 #include <chrono>
 #include <cstdlib>
 #include <cstdint>
@@ -731,9 +734,31 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
 // Memtest over a SPAN of HBM: `bytes` (0: all free HBM minus `headroom` bytes) held as
 // chunks of `chunk` bytes, all allocated at once so they cover distinct physical memory,
 // each filled with a per-pass pattern and verified.  out: [0] mismatching words,
-// [1] verify GB/s (last chunk, last pass), [2] bytes tested, [3] device HBM bytes.
+// [1] verify GB/s (last chunk, last pass), [2] bytes tested, [3] device HBM bytes,
+// [4] allocation ms, [5] fill+verify ms, [6] free ms (out must hold 7 doubles).
 // This is the `full` burn-in's memtest (round 1 tested a fixed 64 GiB of 288).
+// Releasing ~300 GB takes ~2.7 s on MI355X (profiles/round2/memtest_span_chunks.jsonl: the
+// fill+verify of all of it takes ~0.1 s).  With async frees on (tkp_set_async_free), the
+// chunks are released by a background thread once the verdict is known, so a node
+// bring-up does not wait for it; tkp_wait_frees() joins them (the agent calls it at stop,
+// and the next span memtest waits for the previous release before allocating).
+namespace {
+std::mutex g_free_mu;
+std::condition_variable g_free_cv;
+int g_frees_pending = 0;
+std::atomic<int> g_async_free{0};
+}  // namespace
+
+extern "C" void tkp_set_async_free(int on) { g_async_free.store(on); }
+
+extern "C" int tkp_wait_frees() {
+  std::unique_lock<std::mutex> lk(g_free_mu);
+  g_free_cv.wait(lk, [] { return g_frees_pending == 0; });
+  return 0;
+}
+
 extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t headroom, int passes, double* out) {
+  tkp_wait_frees();
   CHECK(hipSetDevice(dev));
   size_t free_b = 0, total_b = 0;
   CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -742,6 +767,7 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
   chunk = chunk / sizeof(uint4) * sizeof(uint4);
   std::vector<uint4*> chunks;
   std::vector<size_t> sizes;
+  const auto t_alloc = std::chrono::steady_clock::now();
   for (size_t done = 0; done < bytes && chunk > 0;) {
     const size_t want = (bytes - done < chunk ? bytes - done : chunk) / sizeof(uint4) * sizeof(uint4);
     if (want == 0) break;
@@ -754,6 +780,7 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
     sizes.push_back(want);
     done += want;
   }
+  const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc).count();
   unsigned long long* err = nullptr;
   CHECK(hipMalloc(&err, sizeof(unsigned long long)));
   hipStream_t s;
@@ -765,6 +792,7 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
   const int grid = stream_grid(dev, 16);
   float ms = 0.f;
   size_t tested = 0;
+  const auto t_test = std::chrono::steady_clock::now();
   for (size_t c = 0; c < chunks.size(); ++c) {
     const size_t n = sizes[c] / sizeof(uint4);
     for (int ps = 0; ps < (passes < 1 ? 1 : passes); ++ps) {
@@ -786,11 +814,32 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
   out[1] = sizes.empty() ? 0.0 : (double)sizes.back() / (ms * 1e-3) / 1e9;
   out[2] = (double)tested;
   out[3] = (double)total_b;
+  out[5] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_test).count();
+  out[4] = alloc_ms;
   TRACED(hipEventDestroy(t0));
   TRACED(hipEventDestroy(t1));
   TRACED(hipStreamDestroy(s));
-  for (uint4* p : chunks) TRACED(hipFree(p));
   TRACED(hipFree(err));
+  if (g_async_free.load()) {
+    {
+      std::lock_guard<std::mutex> lk(g_free_mu);
+      ++g_frees_pending;
+    }
+    std::thread([dev, chunks]() {
+      (void)hipSetDevice(dev);
+      for (uint4* p : chunks) (void)hipFree(p);
+      {
+        std::lock_guard<std::mutex> lk(g_free_mu);
+        --g_frees_pending;
+      }
+      g_free_cv.notify_all();
+    }).detach();
+    out[6] = 0.0;
+    return 0;
+  }
+  const auto t_free = std::chrono::steady_clock::now();
+  for (uint4* p : chunks) TRACED(hipFree(p));
+  out[6] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_free).count();
   return 0;
 }
 
@@ -975,7 +1024,7 @@ int main(int argc, char** argv) {
     const int d = devs[k];
     struct tkp_device_info info;
     memset(&info, 0, sizeof(info));
-    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[4] = {0, 0, 0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0},
+    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[7] = {0, 0, 0, 0, 0, 0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0},
            gm8[7] = {0, 0, 0, 0, -1, -1, 0};
     bool ok = tkp_device_info(d, &info) == 0 && tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, hbm) == 0 &&
               tkp_mfma_peak(d, 0, mfma_iters, 3, 2, bf16) == 0 && tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, fp8) == 0 &&

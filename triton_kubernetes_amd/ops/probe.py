@@ -59,6 +59,7 @@ def _lib():
     lib.tkp_memtest.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
     lib.tkp_memtest_span.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
+    lib.tkp_set_async_free.argtypes = [ctypes.c_int]
     lib.tkp_memtest_selfcheck.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_double)]
     lib.tkp_p2p_bandwidth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
@@ -151,9 +152,20 @@ def memtest_span(dev: int, nbytes: int = 0, chunk: int = 16 << 30, headroom: int
                  passes: int = 1) -> Dict[str, float]:
     """Memtest of ``nbytes`` of HBM (0: all free HBM but ``headroom``) held as ``chunk``-byte
     allocations at once, so the whole span is distinct physical memory."""
-    out = (ctypes.c_double * 4)()
+    out = (ctypes.c_double * 7)()
     _check(_lib().tkp_memtest_span(dev, nbytes, chunk, headroom, passes, out), "memtest_span")
-    return {"errors": int(out[0]), "verify_gbps": out[1], "bytes": int(out[2]), "hbm_bytes": int(out[3])}
+    return {"errors": int(out[0]), "verify_gbps": out[1], "bytes": int(out[2]), "hbm_bytes": int(out[3]),
+            "alloc_ms": round(out[4], 1), "test_ms": round(out[5], 1), "free_ms": round(out[6], 1)}
+
+
+def set_async_free(on: bool) -> None:
+    """Release the span memtest's chunks on a background thread (long-lived agents)."""
+    _lib().tkp_set_async_free(1 if on else 0)
+
+
+def wait_frees() -> None:
+    """Join pending background releases of span-memtest memory."""
+    _lib().tkp_wait_frees()
 
 
 def memtest_selfcheck(dev: int, nbytes: int, corrupt: int) -> int:
