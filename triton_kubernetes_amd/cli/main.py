@@ -42,10 +42,11 @@ VALID = {
     "backup": ["cluster"],
     "restore": ["cluster"],
     "userdata": ["node"],
+    "migrate": ["manager"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
 _ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
-             "restore": "restore", "userdata": "userdata"}
+             "restore": "restore", "userdata": "userdata", "migrate": "migrate"}
 
 
 class ArgError(Exception):
@@ -87,7 +88,9 @@ def build_parser() -> argparse.ArgumentParser:
                        ("wait", "Wait until a cluster is kubectl-ready (and GPU-ready) and report timings"),
                        ("backup", "Back up a cluster's namespaces to the state backend (local/manta) or S3"),
                        ("restore", "Restore a cluster's namespaces from a backup"),
-                       ("userdata", "Print cloud-init user-data that bootstraps a node (PXE/MAAS delivery)")):
+                       ("userdata", "Print cloud-init user-data that bootstraps a node (PXE/MAAS delivery)"),
+                       ("migrate", "Point a cluster manager's document (e.g. one written by the reference's "
+                                   "Terraform 0.11 modules) at this framework's modules")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
@@ -180,6 +183,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         from ..workflows.userdata import node_userdata
 
         node_userdata(ctx, backend)
+    elif command == "migrate":
+        from ..workflows.migrate import migrate_manager
+
+        migrate_manager(ctx, backend)
     elif command == "wait":
         from ..readiness.waiter import wait_after_create
         from ..workflows.select import select_cluster, select_manager

@@ -1,0 +1,103 @@
+"""``migrate manager``: move a cluster manager's document onto this framework's modules.
+
+A user switching from the reference has ``~/.triton-kubernetes/<manager>/main.tf.json``
+(or the Manta copy) whose module blocks point at the reference's Terraform 0.11 modules
+(``github.com/joyent/triton-kubernetes//terraform/modules/<name>?ref=master``,
+``create/manager.go:160-171``).  Terraform >= 0.12 cannot parse those, and the reference
+modules lack the MI355X host and add-on modules.  Module keys, variable names and the
+backend block are compatible by design, so migration is a source rewrite plus a check:
+
+1. every module block whose source is not this framework's source for that module (the
+   packaged tree, or ``source_url``/``source_ref``) is pointed at it;
+2. each rewritten block is checked against the new module the way ``terraform plan``
+   would (``terraform/hcl.py:check_inputs``): unknown arguments (dropped with
+   ``migrate_drop_unknown: true``, else reported and the migration refused), missing
+   required arguments (refused), failing validations (e.g. a Kubernetes release the
+   pinned Rancher does not ship: reported as a warning, because the running cluster keeps
+   its version until it is recreated);
+3. after confirmation the previous document is kept as the blob
+   ``main.tf.json.pre-migrate`` and the migrated one is persisted.
+
+Nothing is applied: the next ``create`` (or an explicit re-apply) runs the new modules.
+"""
+
+from typing import Any, Dict, List, Tuple
+
+from ..backend.base import Backend
+from ..config.context import Context
+from ..errors import ConfigError, TKError
+from ..models.common import source_for
+from ..terraform import hcl
+from ..terraform.catalog import local_module_dir, module_from_source
+from .create import NO_MANAGERS
+from .select import select_manager
+
+BACKUP_BLOB = "main.tf.json.pre-migrate"
+
+
+def plan_migration(ctx: Context, doc: Dict[str, Any], drop_unknown: bool = False
+                   ) -> Tuple[Dict[str, Dict[str, Any]], List[str], List[str]]:
+    """``(new module blocks by key, errors, warnings)`` for a document's ``module`` map."""
+    new_blocks: Dict[str, Dict[str, Any]] = {}
+    errors: List[str] = []
+    warnings: List[str] = []
+    for key, block in (doc.get("module") or {}).items():
+        src = str(block.get("source", ""))
+        info = module_from_source(src)
+        if info is None:
+            errors.append(f"module.{key}: unknown module source {src!r}")
+            continue
+        target = source_for(ctx, info.path)
+        if src == target:
+            continue
+        new = dict(block, source=target)
+        mod_dir = local_module_dir(target) or info.local_dir
+        problems = hcl.check_inputs(mod_dir, new)
+        for p in problems:
+            if p.startswith("unsupported argument "):
+                arg = p.split("'")[1]
+                if drop_unknown:
+                    new.pop(arg, None)
+                    warnings.append(f"module.{key}: dropped {arg!r} (not a variable of {info.name})")
+                else:
+                    errors.append(f"module.{key}: {p} of {info.name} (set migrate_drop_unknown: true to drop it)")
+            elif p.startswith("missing required argument "):
+                errors.append(f"module.{key}: {p} of {info.name}")
+            else:
+                warnings.append(f"module.{key}: {p} (terraform plan refuses this until it is changed)")
+        new_blocks[key] = new
+    return new_blocks, errors, warnings
+
+
+def migrate_manager(ctx: Context, backend: Backend) -> None:
+    managers = backend.states()
+    if not managers:
+        raise ConfigError(NO_MANAGERS)
+    manager = select_manager(ctx, managers)
+    state = backend.state(manager)
+    drop = ctx.settings.get_bool("migrate_drop_unknown") if ctx.is_set("migrate_drop_unknown") else False
+    new_blocks, errors, warnings = plan_migration(ctx, state.doc, drop)
+    for key in sorted(new_blocks):
+        ctx.echo(f"module.{key}: {state.module(key).get('source')} -> {new_blocks[key]['source']}")
+    for w in warnings:
+        ctx.echo(f"warning: {w}")
+    if errors:
+        raise TKError("migration refused:\n  " + "\n  ".join(errors))
+    if not new_blocks:
+        ctx.echo(f'Cluster manager "{manager}" already uses this framework\'s modules.')
+        return
+    if not ctx.confirm(f'Migrate "{manager}" ({len(new_blocks)} modules)', f'Migrate "{manager}"'):
+        ctx.echo("Migrate manager canceled.")
+        return
+    with backend.lock(manager):
+        try:
+            backend.write_blob(manager, BACKUP_BLOB, state.bytes())
+        except NotImplementedError:
+            pass
+        for key, block in new_blocks.items():
+            state.set_module(key, block)
+        backend.persist_state(state)
+    ctx.echo(f'Cluster manager "{manager}" migrated; the previous document is kept as {BACKUP_BLOB}.')
+
+
+__all__ = ["migrate_manager", "plan_migration", "BACKUP_BLOB"]
