@@ -117,6 +117,12 @@ def _replace(path, old, new):
     ("template directive", lambda d: _replace(d / "files" / "install_docker.sh.tftpl", "%{ endif ~}\n", "", ),
      "is never closed"),
     ("template missing file", lambda d: os.remove(d / "files" / "setup_rancher.sh.tftpl"), "missing file"),
+    # list()/map() were removed in Terraform 0.15; a typo'd function does not plan either
+    ("removed function", lambda d: _replace(d / "main.tf", "[terraform_data.install_docker]",
+                                                                  "list(terraform_data.install_docker)"),
+     "unknown function list()"),
+    ("provider not required", lambda d: _replace(d / "versions.tf", "    external = {", "    externall = {"),
+     "external needs provider 'external'"),
 ])
 def test_checker_catches_broken_fixture(tmp_path, case, edit, expect):
     rep = _broken_copy(tmp_path, edit)

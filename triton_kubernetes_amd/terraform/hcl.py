@@ -654,6 +654,44 @@ def object_keys(node: Node) -> Optional[Set[str]]:
 
 _BUILTIN_ROOTS = {"path", "count", "each", "self", "terraform"}
 
+# Terraform >= 1.3's built-in functions.  ``list()``/``map()`` are not here: they were
+# removed in 0.15, so a module still calling them would not plan (type constraints such
+# as ``map(string)`` are not calls and are skipped by :func:`_value_calls`).
+TERRAFORM_FUNCTIONS = frozenset("""
+abs ceil floor log max min parseint pow signum
+chomp endswith format formatlist indent join lower regex regexall replace split startswith
+strcontains strrev substr title trim trimprefix trimsuffix trimspace upper
+alltrue anytrue chunklist coalesce coalescelist compact concat contains distinct element flatten
+index keys length lookup matchkeys merge one range reverse setintersection setproduct setsubtract
+setunion slice sort sum transpose values zipmap
+base64decode base64encode base64gzip csvdecode jsondecode jsonencode textdecodebase64
+textencodebase64 urlencode yamldecode yamlencode
+abspath dirname pathexpand basename file fileexists fileset filebase64 templatefile
+formatdate plantimestamp timeadd timecmp timestamp
+base64sha256 base64sha512 bcrypt filebase64sha256 filebase64sha512 filemd5 filesha1 filesha256
+filesha512 md5 rsadecrypt sha1 sha256 sha512 uuid uuidv5
+cidrhost cidrnetmask cidrsubnet cidrsubnets
+can issensitive nonsensitive sensitive tobool tolist tomap tonumber toset tostring try type
+""".split())
+# resource/data types served by Terraform itself, not by a required provider
+_BUILTIN_RESOURCE_TYPES = {"terraform_data", "terraform_remote_state"}
+
+
+def _value_calls(body: Body, block_type: str = ""):
+    """Function-call nodes in value positions (a variable's ``type`` is a constraint)."""
+    for a in body.attributes:
+        if block_type == "variable" and a.name == "type":
+            continue
+        for n in walk(a.expr):
+            if n.kind == "call":
+                yield n
+    for b in body.blocks:
+        yield from _value_calls(b.body, b.type)
+
+
+def _provider_of(rtype: str) -> str:
+    return rtype.split("_", 1)[0]
+
 
 @dataclass
 class ModuleReport:
@@ -703,7 +741,19 @@ def check_module(module_dir: str) -> ModuleReport:
             elif b.type == "output" and b.labels:
                 outputs.add(b.labels[0])
     resource_types = {t for t, _ in resources}
+    providers: Set[str] = set()
+    for body in files.values():
+        for tb in body.blocks_of("terraform"):
+            for rp in tb.body.blocks_of("required_providers"):
+                providers |= {a.name for a in rp.body.attributes}
+    for rtype in sorted(resource_types | {t for t, _ in datas}):
+        if rtype not in _BUILTIN_RESOURCE_TYPES and _provider_of(rtype) not in providers:
+            errors.append(f"{name}: {rtype} needs provider {_provider_of(rtype)!r}, "
+                          f"which required_providers does not declare")
     for fn, body in files.items():
+        for call in _value_calls(body):
+            if call.value not in TERRAFORM_FUNCTIONS:
+                errors.append(f"{name}/{fn}: call to unknown function {call.value}()")
         for root, attrs, pos in references(body):
             where = f"{name}/{fn}"
             if root == "var":
