@@ -42,13 +42,6 @@ if [ "$MODE" = runtime ]; then
   step bench_sys2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
   TK_HIP_RUNTIME=torch step bench_torch2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
 fi
-if [ "$MODE" = ab ]; then
-  # A/B of the daemon-start RCCL code load, alternating arms
-  step bench_early1 300 python bench.py --steps 8 --warmup 1 --warm-steps 0
-  TK_RCCL_LOAD_EARLY=0 step bench_late1 300 python bench.py --steps 8 --warmup 1 --warm-steps 0
-  step bench_early2 300 python bench.py --steps 8 --warmup 1 --warm-steps 0
-  TK_RCCL_LOAD_EARLY=0 step bench_late2 300 python bench.py --steps 8 --warmup 1 --warm-steps 0
-fi
 if [ "$MODE" = kload ]; then
   step rccl_kernel_load 300 python scripts/rccl_kernel_load.py
 fi

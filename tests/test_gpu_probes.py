@@ -4,6 +4,7 @@ import json
 import os
 import subprocess
 import sys
+import time
 
 import pytest
 
@@ -183,6 +184,27 @@ def test_link_check_on_this_box(tmp_path):
         assert doc["status"] == "passed" and "amd.com/xgmi.link-check=passed" in labels.read_text()
     r = probe.p2p_bandwidth(0, 0, 64 << 20, 3)
     assert r["gbps"] > 100  # a device-local copy through the same path
+
+
+def test_link_matrix_rounds_cover_every_ordered_pair():
+    """tkp_link_matrix's round-robin schedule (odd n: a bye each round) over three
+    "devices" that are all GPU 0: every ordered pair is timed once, concurrently with the
+    other pairs of its round, and nothing is left allocated or mapped."""
+    import ctypes
+
+    from triton_kubernetes_amd.ops import probe
+
+    lib = probe._lib()
+    for n in (2, 3, 4):
+        gbps = (ctypes.c_double * (n * n))()
+        acc = (ctypes.c_int * (n * n))()
+        t0 = time.monotonic()
+        rc = lib.tkp_link_matrix((ctypes.c_int * n)(*([0] * n)), n, 32 << 20, 2, gbps, acc)
+        assert rc == 0, lib.tkp_last_error()
+        vals = [gbps[i * n + j] for i in range(n) for j in range(n) if i != j]
+        assert len(vals) == n * (n - 1) and all(v > 50 for v in vals), (n, vals)
+        assert all(gbps[i * n + i] == 0.0 for i in range(n))
+        assert time.monotonic() - t0 < 10
 
 
 def test_topology_amdsmi():

@@ -1,5 +1,6 @@
 """Node layer: bootstrap plans (shell + agent renderers), GPU labels, KFD topology, node agent."""
 
+import base64
 import json
 import os
 import subprocess
@@ -332,3 +333,42 @@ def test_multi_gpu_plan_checks_links():
     assert "gpu-burnin --p2p --min-link-frac 0.6" in plan.render_shell()
     one = build_host_plan(dict(cfg, gpu_count=1), "https://r", "tok", "ca", mi355x=True)
     assert "gpu_links" not in one.step_names()
+
+
+def test_one_node_cluster_gate_shares_the_rccl_local_sweep():
+    """A gate communicator spanning exactly the node's GPUs (a one-node cluster) is swept by
+    the plan's rccl_local step instead of a second init, and the gate answers from it."""
+    import tempfile
+
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.labels import synthetic_topology
+    from triton_kubernetes_amd.node.plan import BootstrapPlan, Step
+
+    agent = NodeAgent(name="n", mode="sim", devices=list(range(8)), token="t" * 24, root=tempfile.mkdtemp(),
+                      topology_override=synthetic_topology(8))
+    plan = BootstrapPlan("n", "worker", "http://r", "tok", "ca", steps=[Step("rccl_local", "rccl_local", "true")])
+    try:
+        # no pending gate: the synthetic node simulates its local check
+        assert agent.run_plan(plan)["steps"][0]["detail"] == {"simulated": True}
+        gate_sizes = [1 << 20, 64 << 20]
+        prep = agent.rccl_prepare(None, world=8, rank_base=0, ndev=8, max_bytes=64 << 20, sizes=gate_sizes)
+        uid = base64.b64decode(prep["uid"])
+        detail = agent.run_plan(plan)["steps"][0]["detail"]
+        assert detail["shared_with"] == "cluster_gate"
+        assert detail["sizes"] == sorted({1 << 20, 16 << 20, 64 << 20, 256 << 20})
+        assert agent._gates == {}  # taken by the step
+        res = agent.rccl_gate(0, 8, uid, gate_sizes, ndev=8)
+        assert res["shared_with"] == "rccl_local" and res["pipelined"] and res["sizes"] == gate_sizes
+        assert res["ranks"] == list(range(8)) and res["ok"]
+        # a gate over more than this node (another node's ranks) is never taken by the step
+        agent.rccl_prepare(None, world=16, rank_base=0, ndev=8, sizes=gate_sizes)
+        assert agent.run_plan(plan)["steps"][0]["detail"] == {"simulated": True}
+        assert len(agent._gates) == 1
+        # sizes the local sweep did not cover: a fresh communicator measures them
+        prep = agent.rccl_prepare(None, world=8, rank_base=0, ndev=8, sizes=[1 << 20])
+        agent._gates = {k: v for k, v in agent._gates.items() if k == base64.b64decode(prep["uid"])}
+        agent.run_plan(plan)
+        res = agent.rccl_gate(0, 8, base64.b64decode(prep["uid"]), [3 << 20], ndev=8)
+        assert "shared_with" not in res and res["sizes"] == [3 << 20]
+    finally:
+        agent.stop()

@@ -47,7 +47,7 @@ import threading
 import time
 import urllib.parse
 from dataclasses import dataclass, field
-from typing import Any, Callable, Dict, List, Optional
+from typing import Any, Callable, Dict, List, Optional, Tuple
 
 from ..cloud.http import HTTPClient
 from ..parallel.rccl_env import render_env_file, site_env_from_topology
@@ -123,7 +123,10 @@ class NodeAgent:
         # on the bring-up path (thread creation contends with RCCL/HIP work in the process)
         self._pool = cf.ThreadPoolExecutor(max_workers=len(self.devices) + 2,
                                            thread_name_prefix=f"tk-agent-{self.name}")
+        # uid -> (gate, created, {"world", "rank_base", "sizes"})
         self._gates: Dict[bytes, Any] = {}
+        # uid -> (SweepResult, finished): whole-node gates the rccl_local step already swept
+        self._gate_results: Dict[bytes, Any] = {}
         # one RCCL unique id kept ready (new_uid): the gate's first request gets it without
         # an ncclGetUniqueId on the bring-up path; the pool makes the next one afterwards
         self._spare_uid: Optional[bytes] = None
@@ -275,23 +278,37 @@ class NodeAgent:
         if a == "rccl_local":
             if len(self.devices) < 2:
                 return {"skipped": "single GPU"}
-            if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
+            taken = self._take_node_gate()
+            if taken is None and self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
                 return {"simulated": True}
             from ..ops import rccl
 
             # every local GPU as one communicator (grouped init), the verified sweep, and the
-            # ~0.5 s-per-communicator teardown off the plan (drained at stop)
-            self._used_rccl = True
+            # ~0.5 s-per-communicator teardown off the plan (drained at stop).  On a one-node
+            # cluster the gate's pending communicator is exactly that: sweep it (with the
+            # gate's sizes too) instead of a second init, and keep the result for the gate.
+            if self.topology_override is None:
+                self._used_rccl = True
             sizes = list(rccl.DEFAULT_SIZES)
-            gate = rccl.GateComm(self._make_uid(), len(self.devices), 0, self.devices, blocking=True,
-                                 prealloc_bytes=max(sizes))
+            if taken is not None:
+                uid, gate, meta = taken
+                sizes = sorted(set(sizes) | set(meta.get("sizes") or []))
+            else:
+                gate = rccl.GateComm(self._make_uid(), len(self.devices), 0, self.devices, blocking=True,
+                                     prealloc_bytes=max(sizes))
             res = gate.sweep(sizes, iters=10, warmup=2, async_teardown=True)
+            if taken is not None:
+                with self._gate_mu:
+                    self._gate_results[uid] = (res, time.time())
             floor = float(step.params.get("min_busbw", 0) or 0)
             if not res.ok:
                 raise StepFailed(step.name, "RCCL verification failed")
             if floor and res.peak_busbw < floor:
                 raise StepFailed(step.name, f"RCCL busbw {res.peak_busbw:.0f} GB/s below {floor:.0f}")
-            return res.to_json()
+            out = res.to_json()
+            if taken is not None:
+                out["shared_with"] = "cluster_gate"
+            return out
         if a == "agent":
             if plan.gpu is not None:
                 ctx["capacity"].setdefault("amd.com/gpu", len(self.devices))
@@ -363,8 +380,10 @@ class NodeAgent:
     def _expire_gates(self) -> None:
         now = time.time()
         with self._gate_mu:
-            stale = [k for k, (_, t) in self._gates.items() if now - t > self.GATE_TTL_S]
+            stale = [k for k, e in self._gates.items() if now - e[1] > self.GATE_TTL_S]
             gates = [self._gates.pop(k)[0] for k in stale]
+            for k in [k for k, e in self._gate_results.items() if now - e[1] > self.GATE_TTL_S]:
+                del self._gate_results[k]
         for g in gates:
             g.abort()
 
@@ -397,10 +416,12 @@ class NodeAgent:
         return uid
 
     def rccl_prepare(self, uid: Optional[bytes], world: int, rank_base: int, ndev: int = 1,
-                     max_bytes: int = 0) -> Dict[str, Any]:
+                     max_bytes: int = 0, sizes: Optional[List[int]] = None) -> Dict[str, Any]:
         """Start this node's share of a cluster communicator (non-blocking init; with
         ``max_bytes`` the init thread also allocates the sweep buffers).  ``uid`` None: this
-        node hosts the rendezvous — it takes a new unique id and returns it for the others."""
+        node hosts the rendezvous — it takes a new unique id and returns it for the others.
+        ``sizes``: the gate's message sizes, so a node that is the whole gate can sweep them
+        in its ``rccl_local`` step (:meth:`_take_node_gate`)."""
         devs = self._gate_devices(ndev)
         self._expire_gates()
         if uid is None:
@@ -415,7 +436,8 @@ class NodeAgent:
                 gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False, prealloc_bytes=max_bytes)
         with self._gate_mu:
             old = self._gates.pop(uid, None)
-            self._gates[uid] = (gate, time.time())
+            self._gates[uid] = (gate, time.time(), {"world": world, "rank_base": rank_base,
+                                                    "sizes": [int(x) for x in (sizes or [])]})
         if old is not None:
             old[0].abort()
         return {"ok": True, "ranks": list(range(rank_base, rank_base + len(devs))), "devices": devs,
@@ -424,16 +446,51 @@ class NodeAgent:
     def rccl_abort(self, uid: bytes) -> Dict[str, Any]:
         with self._gate_mu:
             entry = self._gates.pop(uid, None)
+            done = self._gate_results.pop(uid, None)
         if entry is not None:
             entry[0].abort()
-        return {"ok": True, "aborted": entry is not None}
+        return {"ok": True, "aborted": entry is not None or done is not None}
 
+    def _take_node_gate(self) -> Optional[Tuple[bytes, Any, Dict[str, Any]]]:
+        """A pending gate communicator that spans exactly this node's GPUs (a one-node
+        cluster: world == ndev, every rank here), taken out of the pending set.
+
+        Its all-reduce over the node's GPUs IS the node-level RCCL check, so ``rccl_local``
+        sweeps it instead of initialising a second communicator over the same GPUs on the
+        bring-up path, and the cluster gate later answers from that sweep."""
+        devs = list(self.devices)
+        with self._gate_mu:
+            for uid, (gate, _, meta) in list(self._gates.items()):
+                if (meta.get("world") == len(devs) and meta.get("rank_base") == 0
+                        and list(getattr(gate, "devices", [])) == devs):
+                    del self._gates[uid]
+                    return uid, gate, meta
+        return None
     def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10,
                   ndev: int = 1) -> Dict[str, Any]:
         """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
         communicator from rccl_prepare when there is one, else a fresh init."""
         with self._gate_mu:
             entry = self._gates.pop(uid, None)
+            done = self._gate_results.pop(uid, None)
+        if done is not None:
+            res = done[0]
+            if set(sizes) <= set(res.sizes):  # the rccl_local step swept this communicator
+                idx = [res.sizes.index(x) for x in sizes]
+                pick = lambda xs: [xs[i] for i in idx]  # noqa: E731
+                from ..ops.rccl import SweepResult
+
+                sub = SweepResult(res.world, res.dtype, list(sizes), pick(res.time_us), pick(res.algbw_gbps),
+                                  pick(res.busbw_gbps), pick(res.errors), res.init_ms, dict(res.phase_ms))
+                with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=True,
+                          shared_with="rccl_local"):
+                    out = sub.to_json()
+                out.update(pipelined=True, shared_with="rccl_local",
+                           ranks=list(range(rank, rank + len(self._gate_devices(ndev)))))
+                return out
+            # sizes the local sweep did not cover: the node is the whole gate, so a fresh
+            # communicator under a new id (every rank is here) measures them
+            uid = self._make_uid()
         pipelined = entry is not None
         with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=pipelined):
             if entry is not None:
@@ -590,7 +647,8 @@ class NodeAgent:
                         return self._reply(200, agent.rccl_prepare(uid,
                                                                    int(body["world"]), int(body["rank_base"]),
                                                                    int(body.get("ndev", 1)),
-                                                                   int(body.get("max_bytes", 0))))
+                                                                   int(body.get("max_bytes", 0)),
+                                                                   [int(x) for x in body.get("sizes") or []]))
                     if path == "/v1/rccl-gate":
                         uid = base64.b64decode(body["uid"])
                         return self._reply(200, agent.rccl_gate(int(body["rank"]), int(body["world"]), uid,
@@ -633,8 +691,9 @@ class NodeAgent:
             self._server.server_close()
             self._server = None
         with self._gate_mu:
-            pending = [g for g, _ in self._gates.values()]
+            pending = [e[0] for e in self._gates.values()]
             self._gates.clear()
+            self._gate_results.clear()
         for g in pending:
             g.abort()
         if getattr(self, "_used_rccl", False):

@@ -41,6 +41,7 @@
 #include <cstring>
 #include <string>
 #include <vector>
+#include <utility>
 #include <algorithm>
 #include <vector>
 
@@ -915,6 +916,112 @@ extern "C" int tkp_p2p_bandwidth(int src, int dst, size_t bytes, int iters, doub
   return 0;
 }
 
+// Every ordered pair of `n` local GPUs, measured in rounds of a round-robin pairing (the
+// circle method): a round is a perfect matching, so each GPU takes part in one copy per
+// round direction and every concurrent copy has its own xGMI link and copy engines.  An
+// 8-GPU node needs 7 rounds x 2 directions instead of 56 one-at-a-time measurements, and
+// buffers, streams and peer access are set up once.  gbps[i*n+j]: best copy i -> j (GB/s,
+// -1 when that copy failed); access[i*n+j]: j can map i's memory (the copy then runs peer
+// to peer rather than staged).  Peer access this call enabled is disabled again.
+extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, double* gbps, int* access) {
+  if (n < 2 || n > 64 || bytes == 0) {
+    snprintf(g_err, sizeof(g_err), "link matrix: %d devices, %zu bytes", n, bytes);
+    return -1;
+  }
+  std::vector<void*> buf(2 * n, nullptr);
+  std::vector<hipStream_t> st(n, nullptr);
+  std::vector<hipEvent_t> ev(2 * n, nullptr);
+  std::vector<std::pair<int, int>> enabled;
+  int rc = 0;
+  auto cleanup = [&]() {
+    for (int i = 0; i < n; ++i) {
+      (void)hipSetDevice(devs[i]);
+      if (st[i]) (void)hipStreamSynchronize(st[i]);
+      for (int k : {2 * i, 2 * i + 1}) {
+        if (ev[k]) (void)hipEventDestroy(ev[k]);
+        if (buf[k]) (void)hipFree(buf[k]);
+      }
+      if (st[i]) (void)hipStreamDestroy(st[i]);
+    }
+    for (auto& e : enabled) {
+      (void)hipSetDevice(devs[e.first]);
+      (void)hipDeviceDisablePeerAccess(devs[e.second]);
+    }
+    (void)hipGetLastError();
+  };
+  // per GPU: a source and a destination buffer, one stream (copies run on the receiver's)
+  for (int i = 0; i < n && rc == 0; ++i) {
+    hipError_t e = hipSetDevice(devs[i]);
+    if (e == hipSuccess) e = hipMalloc(&buf[2 * i], bytes);
+    if (e == hipSuccess) e = hipMalloc(&buf[2 * i + 1], bytes);
+    if (e == hipSuccess) e = hipMemsetAsync(buf[2 * i], 0x5a, bytes, 0);
+    if (e == hipSuccess) e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
+    if (e == hipSuccess) e = hipEventCreate(&ev[2 * i]);
+    if (e == hipSuccess) e = hipEventCreate(&ev[2 * i + 1]);
+    if (e == hipSuccess) e = hipDeviceSynchronize();
+    if (e != hipSuccess) rc = set_err("link matrix setup", e);
+  }
+  for (int i = 0; i < n && rc == 0; ++i)
+    for (int j = 0; j < n && rc == 0; ++j) {
+      gbps[i * n + j] = 0.0;
+      access[i * n + j] = 0;
+      if (i == j) continue;
+      int can = 0;
+      if (hipDeviceCanAccessPeer(&can, devs[j], devs[i]) != hipSuccess) can = 0;
+      access[i * n + j] = can;
+      if (!can) continue;
+      (void)hipSetDevice(devs[j]);
+      hipError_t e = hipDeviceEnablePeerAccess(devs[i], 0);
+      if (e == hipSuccess) enabled.emplace_back(j, i);
+      else if (e != hipErrorPeerAccessAlreadyEnabled) rc = set_err("hipDeviceEnablePeerAccess", e);
+      (void)hipGetLastError();
+    }
+  const int m = n + (n & 1);  // a bye slot when n is odd
+  std::vector<std::pair<int, int>> pairs;
+  for (int r = 0; r < m - 1 && rc == 0; ++r) {
+    pairs.clear();
+    for (int k = 0; k < m / 2; ++k) {
+      const int a = k == 0 ? m - 1 : (r + k) % (m - 1);
+      const int b = k == 0 ? r : (r - k + (m - 1)) % (m - 1);
+      if (a < n && b < n) pairs.emplace_back(a, b);
+    }
+    for (int dir = 0; dir < 2 && rc == 0; ++dir) {
+      std::vector<double> best(pairs.size(), 0.0);
+      std::vector<char> failed(pairs.size(), 0);
+      for (int it = -1; it < (iters < 1 ? 1 : iters); ++it) {  // it -1: untimed warm-up copy
+        for (size_t p = 0; p < pairs.size(); ++p) {
+          if (failed[p]) continue;
+          const int src = dir ? pairs[p].second : pairs[p].first, dst = dir ? pairs[p].first : pairs[p].second;
+          (void)hipSetDevice(devs[dst]);
+          hipError_t e = hipEventRecord(ev[2 * dst], st[dst]);
+          if (e == hipSuccess) e = hipMemcpyPeerAsync(buf[2 * dst + 1], devs[dst], buf[2 * src], devs[src], bytes, st[dst]);
+          if (e == hipSuccess) e = hipEventRecord(ev[2 * dst + 1], st[dst]);
+          if (e != hipSuccess) { failed[p] = 1; (void)hipGetLastError(); }
+        }
+        for (size_t p = 0; p < pairs.size(); ++p) {
+          if (failed[p]) continue;
+          const int dst = dir ? pairs[p].first : pairs[p].second;
+          (void)hipSetDevice(devs[dst]);
+          float ms = 0.f;
+          if (hipEventSynchronize(ev[2 * dst + 1]) != hipSuccess ||
+              hipEventElapsedTime(&ms, ev[2 * dst], ev[2 * dst + 1]) != hipSuccess) {
+            failed[p] = 1;
+            (void)hipGetLastError();
+            continue;
+          }
+          if (it >= 0 && ms > 0.f) best[p] = std::max(best[p], (double)bytes / (ms * 1e-3) / 1e9);
+        }
+      }
+      for (size_t p = 0; p < pairs.size(); ++p) {
+        const int src = dir ? pairs[p].second : pairs[p].first, dst = dir ? pairs[p].first : pairs[p].second;
+        gbps[src * n + dst] = failed[p] ? -1.0 : best[p];
+      }
+    }
+  }
+  cleanup();
+  return rc;
+}
+
 #ifdef TK_PROBE_MAIN
 // gpu-burnin: the on-node executable the SSH bootstrap runs (no Python needed).
 //   gpu-burnin [--all | --device N] [--level quick|full]
@@ -932,8 +1039,8 @@ extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inje
 extern "C" int tkg_screen_fp8(int dev, int M, int N, int K, int reps, long long inject, double* out);
 extern "C" const char* tkg_last_error();
 
-// --p2p: peer copy bandwidth of every ordered GPU pair, one pair at a time (each number is
-// one xGMI link's), against the node's median; same keys and verdict as
+// --p2p: peer copy bandwidth of every ordered GPU pair (tkp_link_matrix: concurrent copies
+// only on disjoint pairs, so each number is one xGMI link's), against the node's median; same keys and verdict as
 // node/labels.py:link_labels.  A degraded link exits 1; a pair the runtime cannot measure
 // is reported as an error (exit 0: the node agent path treats it the same way).
 static int p2p_main(const char* labels_path, double min_frac) {
@@ -947,18 +1054,23 @@ static int p2p_main(const char* labels_path, double min_frac) {
     if (labels_path) { FILE* f = fopen(labels_path, "w"); if (f) fclose(f); }
     return 0;
   }
-  std::vector<double> vals;
+  std::vector<double> vals, mat(n * n, 0.0);
+  std::vector<int> devs(n), acc(n * n, 0);
+  for (int i = 0; i < n; ++i) devs[i] = i;
+  if (tkp_link_matrix(devs.data(), n, 64ull << 20, 3, mat.data(), acc.data()) != 0) {
+    printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    return 2;
+  }
   int errors = 0, no_peer = 0;
   printf("{\"pairs\":{");
   bool first = true;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) {
       if (i == j) continue;
-      double out[2] = {0, 0};
-      if (tkp_p2p_bandwidth(i, j, 64ull << 20, 3, out) != 0) { ++errors; continue; }
-      if (out[1] == 0.0) ++no_peer;
-      vals.push_back(out[0]);
-      printf("%s\"%d-%d\":%.1f", first ? "" : ",", i, j, out[0]);
+      if (mat[i * n + j] < 0.0) { ++errors; continue; }
+      if (!acc[i * n + j]) ++no_peer;
+      vals.push_back(mat[i * n + j]);
+      printf("%s\"%d-%d\":%.1f", first ? "" : ",", i, j, mat[i * n + j]);
       first = false;
     }
   std::vector<double> sorted = vals;

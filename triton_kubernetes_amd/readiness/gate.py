@@ -104,7 +104,8 @@ class ClusterGate:
                 # starts its ranks; the others join with that id
                 m0 = self.members[0]
                 first = self.transport.post(m0.host, "/v1/rccl-prepare", {
-                    "world": self.world, "rank_base": m0.rank_base, "ndev": m0.ndev, "max_bytes": max(self.sizes)})
+                    "world": self.world, "rank_base": m0.rank_base, "ndev": m0.ndev, "max_bytes": max(self.sizes),
+                    "sizes": self.sizes})
                 uid = first["uid"]
                 with self._mu:
                     self.uid = uid  # abort() can release member 0 even if a later post fails
@@ -112,7 +113,7 @@ class ClusterGate:
                     def one(m: GateMember) -> Dict[str, Any]:
                         return self.transport.post(m.host, "/v1/rccl-prepare", {
                             "uid": uid, "world": self.world, "rank_base": m.rank_base, "ndev": m.ndev,
-                            "max_bytes": max(self.sizes)})
+                            "max_bytes": max(self.sizes), "sizes": self.sizes})
 
                     list(shared_pool("tk-gate", 64).map(one, self.members[1:]))
             with self._mu:
