@@ -90,3 +90,8 @@ def assert_blocks_match_modules(st) -> None:
         # what `terraform plan` would reject: types and the modules' own validation blocks
         problems = hcl.check_inputs(mod_dir, block)
         assert not problems, f"{key} -> {info.name}: {problems}"
+        # ... and every expression of the module evaluated for these inputs (terraform/plan.py)
+        from triton_kubernetes_amd.terraform.plan import plan_module
+
+        planned = plan_module(mod_dir, block, check_files=False)
+        assert planned.ok, f"{key} -> {info.name}: {planned.errors}"
