@@ -41,6 +41,12 @@ VARIANTS = {
     "debug_init": {"NCCL_DEBUG": "INFO", "NCCL_DEBUG_SUBSYS": "INIT"},
     "sampled": {"TK_SAMPLE": "1"},
     "torch_runtime": {"TK_HIP_RUNTIME": "torch"},
+    # comgr's on-disk cache of actions (the compressed-bundle UNBUNDLE among them): the first
+    # run fills it, later processes would read the extracted gfx950 code object back
+    "comgr_cache_fill": {"AMD_COMGR_CACHE": "1", "AMD_COMGR_CACHE_DIR": "/tmp/tk-comgr-cache"},
+    "comgr_cache_hit": {"AMD_COMGR_CACHE": "1", "AMD_COMGR_CACHE_DIR": "/tmp/tk-comgr-cache"},
+    "comgr_cache_hit2": {"AMD_COMGR_CACHE": "1", "AMD_COMGR_CACHE_DIR": "/tmp/tk-comgr-cache"},
+    "base2": {},
     "torch_runtime_all_off": {"TK_HIP_RUNTIME": "torch", "RCCL_MSCCL_ENABLE": "0", "RCCL_MSCCLPP_ENABLE": "0",
                               "NCCL_NET_PLUGIN": "none"},
 }
