@@ -134,7 +134,7 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     tpl = open(os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files",
                             "install_mi355x_node.sh.tftpl"), encoding="utf-8").read()
     values = {"gpu_count": 1, "gpu_burnin": "quick", "rccl_env_file": 'NCCL_DEBUG="INFO"', "rccl_min_busbw": 0,
-              "docker_engine_install_url": "https://example.invalid/docker.sh", "docker_install_sha256": "",
+              "gpu_link_min_frac": 0.5, "docker_engine_install_url": "https://example.invalid/docker.sh", "docker_install_sha256": "",
               "hostname": "gpu-tf-1",
               "rancher_registry_username": "", "rancher_registry_password": "", "rancher_registry": "",
               "rancher_agent_image": "rancher/rancher-agent:v2.8.5", "rancher_api_url": "https://rancher.example",

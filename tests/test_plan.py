@@ -44,6 +44,9 @@ def test_mi355x_host_renders_its_install_script():
     assert "tok123" in script and "gpu-1" in script and "--level 'full'" in script
     proc = subprocess.run(["bash", "-n"], input=script, capture_output=True, text=True, check=False)
     assert proc.returncode == 0, proc.stderr
+    assert "--min-link-frac 0.5 " in script  # the module default
+    tuned = plan_module(_dir(HOST), dict(HOST_INPUTS, gpu_link_min_frac="0.7"), check_files=False)
+    assert "--min-link-frac 0.7 " in tuned.rendered["install_mi355x_node.sh.tftpl"][0]
     # a control node becomes Rancher's "controlplane" role
     ctl = plan_module(_dir(HOST), dict(HOST_INPUTS, rancher_host_labels={"control": "true"}), check_files=False)
     assert ctl.locals["rancher_node_role"] == "controlplane"

@@ -128,6 +128,14 @@ def test_mi355x_node_and_addons():
                                      gpu="mi355x", hosts=["c"], rccl_min_busbw="150")), "m", key, None, st)
     assert st.module("node_baremetal_dev_dev-w-3")["rccl_min_busbw"] == "150"
     assert_blocks_match_modules(st)
+    baremetal.new_node(make_ctx(dict(NODE_BASE, node_count=1, ssh_user="u", bastion_host="", key_path="k",
+                                     gpu="mi355x", hosts=["e"], gpu_link_min_frac="0.7")), "m", key, None, st)
+    assert st.module("node_baremetal_dev_dev-w-4")["gpu_link_min_frac"] == "0.7"
+    assert_blocks_match_modules(st)
+    frac = make_ctx(dict(NODE_BASE, node_count=1, ssh_user="u", bastion_host="", key_path="k", gpu="mi355x",
+                         hosts=["f"], gpu_link_min_frac="2"))
+    assert _err(baremetal.new_node, frac, "m", key, None, st) == \
+        "gpu_link_min_frac must be a number between 0 and 1. Found '2'."
     neg = make_ctx(dict(NODE_BASE, node_count=1, ssh_user="u", bastion_host="", key_path="k", gpu="mi355x",
                         hosts=["d"], rccl_min_busbw="-1"))
     assert _err(baremetal.new_node, neg, "m", key, None, st) == "rccl_min_busbw must be a non-negative number. Found '-1'."

@@ -165,6 +165,14 @@ def _mi355x_fields(ctx: Context) -> Dict:
         except ValueError as exc:
             raise ConfigError(f"rccl_min_busbw must be a non-negative number. Found '{busbw}'.") from exc
         out["rccl_min_busbw"] = busbw
+    if s.is_set("gpu_link_min_frac"):
+        frac = s.get_string("gpu_link_min_frac")
+        try:
+            if not 0.0 <= float(frac) <= 1.0:
+                raise ValueError
+        except ValueError as exc:
+            raise ConfigError(f"gpu_link_min_frac must be a number between 0 and 1. Found '{frac}'.") from exc
+        out["gpu_link_min_frac"] = frac
     return out
 
 

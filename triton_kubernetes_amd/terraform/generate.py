@@ -1185,7 +1185,9 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("gpu_product", "MI355X"), Var("gpu_count", 8, "GPUs the node must expose"),
         Var("gpu_burnin", "quick", "quick | full | off"),
         Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
-        Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)")],
+        Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)"),
+        Var("gpu_link_min_frac", "0.5",
+            "fail the node when a GPU pair's peer copy bandwidth is below this fraction of the node median")],
         ROLE_LOCAL + f'''
 
 locals {{
@@ -1219,6 +1221,7 @@ resource "terraform_data" "install_mi355x_node" {{
       gpu_burnin                         = var.gpu_burnin
       rccl_env_file                      = local.rccl_env_file
       rccl_min_busbw                     = var.rccl_min_busbw
+      gpu_link_min_frac                  = var.gpu_link_min_frac
     }})]
   }}
 }}

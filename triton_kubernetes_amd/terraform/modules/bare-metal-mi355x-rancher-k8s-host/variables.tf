@@ -123,3 +123,9 @@ variable "rccl_min_busbw" {
   type        = string
   default     = "0"
 }
+
+variable "gpu_link_min_frac" {
+  description = "fail the node when a GPU pair's peer copy bandwidth is below this fraction of the node median"
+  type        = string
+  default     = "0.5"
+}
