@@ -61,6 +61,7 @@ def test_plan_rewrites_every_reference_source_to_the_packaged_modules():
     # 0.11 modules accepted a 6-character Rancher password and a v1.11 release
     assert any("rancher_admin_password" in w and "12 characters" in w for w in warnings)
     assert any("k8s_version" in w for w in warnings), warnings
+    assert not any(": plan: " in w for w in warnings), warnings  # every new module evaluates cleanly
     # arguments other than the source are carried over unchanged
     assert blocks["node_baremetal_prod_w-1"]["rancher_host_labels"] == {"worker": "true"}
     # an already-migrated document has nothing left to do

@@ -10,7 +10,8 @@ backend block are compatible by design, so migration is a source rewrite plus a 
 1. every module block whose source is not this framework's source for that module (the
    packaged tree, or ``source_url``/``source_ref``) is pointed at it;
 2. each rewritten block is checked against the new module the way ``terraform plan``
-   would (``terraform/hcl.py:check_inputs``): unknown arguments (dropped with
+   would (``terraform/hcl.py:check_inputs``, then ``terraform/plan.py`` evaluates every
+   expression of the module for the block's inputs): unknown arguments (dropped with
    ``migrate_drop_unknown: true``, else reported and the migration refused), missing
    required arguments (refused), failing validations (e.g. a Kubernetes release the
    pinned Rancher does not ship: reported as a warning, because the running cluster keeps
@@ -29,6 +30,7 @@ from ..errors import ConfigError, TKError
 from ..models.common import source_for
 from ..terraform import hcl
 from ..terraform.catalog import local_module_dir, module_from_source
+from ..terraform.plan import plan_module
 from .create import NO_MANAGERS
 from .select import select_manager
 
@@ -65,6 +67,10 @@ def plan_migration(ctx: Context, doc: Dict[str, Any], drop_unknown: bool = False
                 errors.append(f"module.{key}: {p} of {info.name}")
             else:
                 warnings.append(f"module.{key}: {p} (terraform plan refuses this until it is changed)")
+        if not any(e.startswith(f"module.{key}:") for e in errors):
+            # every expression of the new module for these inputs (terraform/plan.py)
+            for p in plan_module(mod_dir, new, check_files=False).errors:
+                warnings.append(f"module.{key}: plan: {p}")
         new_blocks[key] = new
     return new_blocks, errors, warnings
 
