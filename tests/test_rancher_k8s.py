@@ -53,6 +53,31 @@ def test_ensure_cluster_is_idempotent_s4(rancher):
     assert client.ensure_cluster("other").cluster_id != a.cluster_id
 
 
+def test_registration_token_filled_in_after_create(rancher):
+    """The token value appears only after the create returns (the server's controller
+    fills it in): the client polls the token object, and the S4 script does the same."""
+    import os
+
+    from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+
+    fake, client, outs = rancher
+    info = client.ensure_cluster("async")
+    assert info.registration_token and info.registration_token in fake.state.reg_tokens
+    script = os.path.join(MODULES_DIR, "bare-metal-rancher-k8s", "files", "ensure_cluster.sh")
+    query = {"name": "scripted", "version": "v1.28", "network": "flannel", "api_url": fake.url,
+             "access_key": outs["rancher_access_key"], "secret_key": outs["rancher_secret_key"]}
+    first = json.loads(subprocess.run(["bash", script], input=json.dumps(query), capture_output=True, text=True,
+                                      check=True, timeout=60).stdout)
+    assert first["registration_token"] in fake.state.reg_tokens
+    assert first["ca_checksum"] == ca_checksum(FAKE_CACERTS)
+    # the minor was resolved against the server's KDM list
+    rke = fake.state.clusters[first["cluster_id"]]["rancherKubernetesEngineConfig"]
+    assert rke["kubernetesVersion"].startswith("v1.28.")
+    again = json.loads(subprocess.run(["bash", script], input=json.dumps(query), capture_output=True, text=True,
+                                      check=True, timeout=60).stdout)
+    assert again == first  # found by name, token reused
+
+
 def test_registry_passed_to_rke(rancher):
     fake, client, _ = rancher
     info = client.ensure_cluster("reg", k8s_registry="r.example", k8s_registry_username="u",

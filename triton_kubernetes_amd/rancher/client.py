@@ -71,6 +71,7 @@ class RancherClient:
     def __init__(self, url: str, access_key: str = "", secret_key: str = "", verify_tls: bool = False,
                  timeout: float = 30.0):
         self.url = url.rstrip("/")
+        self.token_timeout = 120.0  # registration token value, filled in asynchronously
         self.access_key = access_key
         self.secret_key = secret_key
         self.last_version_note = ""  # set when resolve_k8s_version substituted a release
@@ -168,7 +169,12 @@ class RancherClient:
                 return data[0]["token"]
         resp = self.http.post_json("/v3/clusterregistrationtoken",
                                    {"clusterId": cluster_id, "type": "clusterRegistrationToken"})
-        return resp.get("token", "")
+        token = resp.get("token", "")
+        if token or not resp.get("id"):
+            return token
+        # the server's controller fills the value in after the create returns
+        return wait_until(lambda: self.http.get_json(f"/v3/clusterregistrationtokens/{resp['id']}").get("token"),
+                          self.token_timeout, f"cluster registration token {resp['id']}")
 
     def cacerts(self) -> str:
         return self.http.get_json("/v3/settings/cacerts").get("value", "") or ""

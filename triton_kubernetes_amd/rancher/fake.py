@@ -10,7 +10,10 @@ real server does after agents register:
 * S4 cluster endpoints (find/create cluster, registration tokens, cacerts).  A
   cluster whose ``kubernetesVersion`` is not in the server's KDM list (setting
   ``k8s-versions-current``: the pinned Rancher's RKE1 releases, versions.py) is
-  rejected with 422, as the real server does;
+  rejected with 422, as the real server does.  A new registration token's value is
+  filled in by the server's controller after the create returns
+  (``async_registration_tokens``, default on): the POST answers with an empty
+  ``token`` and the first read of the object after that sees it, so clients must poll;
 * ``POST /v3/connect/register`` — agent registration (``X-API-Tunnel-Token`` +
   base64 JSON ``X-API-Tunnel-Params`` with hostname, roles, labels, capacity),
   standing in for the rancher-agent websocket tunnel;
@@ -78,7 +81,7 @@ class _State:
 class FakeRancher:
     def __init__(self, rke_seconds: float = 0.0, node_ready_seconds: float = 0.0,
                  bootstrap_password: Optional[str] = None, host: str = "127.0.0.1", port: int = 0,
-                 k8s_versions: Optional[Sequence[str]] = None):
+                 k8s_versions: Optional[Sequence[str]] = None, async_registration_tokens: bool = True):
         # a server started without CATTLE_BOOTSTRAP_PASSWORD has a random one nobody knows
         pw = bootstrap_password if bootstrap_password is not None else secrets.token_hex(16)
         self.state = _State(rke_seconds, node_ready_seconds, pw,
@@ -86,9 +89,19 @@ class FakeRancher:
         # "<service>.<namespace>" -> "https://127.0.0.1:<port>" (where an in-cluster
         # webhook service of a test really listens)
         self.service_endpoints: Dict[str, str] = {}
+        self.async_registration_tokens = async_registration_tokens
         self._server = http.server.ThreadingHTTPServer((host, port), self._handler())
         self._server.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
+
+    def _token_view(self, tok: str, fill: bool = True) -> Dict[str, Any]:
+        """A registration token as the API shows it: its value only once the (simulated)
+        controller has filled it in — which happens on the first read after the create."""
+        t = self.state.reg_tokens[tok]
+        shown = tok if t["ready"] else ""
+        if fill:
+            t["ready"] = True
+        return {"id": t["id"], "clusterId": t["clusterId"], "token": shown}
 
     @classmethod
     def for_manager(cls, name: str, admin_password: str, **kw: Any) -> "FakeRancher":
@@ -321,7 +334,7 @@ class FakeRancher:
                     return 404, {"type": "error", "code": "NotFound"}
             if len(rest) == 2 and rest[1] == "clusterregistrationtokens":
                 with st.mu:
-                    data = [dict(t, token=tok) for tok, t in st.reg_tokens.items() if t["clusterId"] == cid]
+                    data = [self._token_view(tok) for tok, t in st.reg_tokens.items() if t["clusterId"] == cid]
                 return 200, {"data": data}
             if method == "DELETE":
                 with st.mu:
@@ -337,9 +350,21 @@ class FakeRancher:
                 return 200, dict(st.clusters[cid])
         if path == "/v3/clusterregistrationtoken" and method == "POST":
             tok = uuid.uuid4().hex + uuid.uuid4().hex[:8]
+            cid = body.get("clusterId")
             with st.mu:
-                st.reg_tokens[tok] = {"id": f"{body.get('clusterId')}:default-token", "clusterId": body.get("clusterId")}
-            return 201, {"token": tok, "clusterId": body.get("clusterId"), "type": "clusterRegistrationToken"}
+                if cid not in st.clusters:
+                    return 422, {"type": "error", "code": "InvalidReference", "fieldName": "clusterId"}
+                n = sum(1 for t in st.reg_tokens.values() if t["clusterId"] == cid)
+                st.reg_tokens[tok] = {"id": f"{cid}:crt-{n}", "clusterId": cid,
+                                      "ready": not self.async_registration_tokens}
+                return 201, dict(self._token_view(tok, fill=False), type="clusterRegistrationToken")
+        if path.startswith("/v3/clusterregistrationtokens/") and method == "GET":
+            tid = urllib.parse.unquote(path[len("/v3/clusterregistrationtokens/"):])
+            with st.mu:
+                tok = next((k for k, t in st.reg_tokens.items() if t["id"] == tid), None)
+                if tok is None:
+                    return 404, {"type": "error", "code": "NotFound"}
+                return 200, self._token_view(tok)
         if path == "/v3/nodes" and method == "GET":
             self._refresh()
             cids = query.get("clusterId")

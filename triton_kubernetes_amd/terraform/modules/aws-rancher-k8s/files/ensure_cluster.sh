@@ -4,7 +4,7 @@
 # and the checksum of the Rancher CA bundle.  Query keys: name, version, network,
 # api_url, access_key, secret_key, registry, registry_username, registry_password.
 exec python3 -c '
-import base64, hashlib, json, re, ssl, sys, urllib.parse, urllib.request
+import base64, hashlib, json, re, ssl, sys, time, urllib.parse, urllib.request
 
 q = json.load(sys.stdin)
 ctx = ssl.create_default_context()
@@ -52,8 +52,16 @@ else:
 if not cluster_id:
     sys.exit("Unable to create cluster!")
 tokens = call("GET", "/v3/clusters/%s/clusterregistrationtokens" % cluster_id).get("data") if found else []
-token = (tokens[0].get("token") if tokens else "") or call(
-    "POST", "/v3/clusterregistrationtoken", {"type": "clusterRegistrationToken", "clusterId": cluster_id}).get("token")
+token = tokens[0].get("token") if tokens else ""
+if not token:
+    created = call("POST", "/v3/clusterregistrationtoken", {"type": "clusterRegistrationToken",
+                                                             "clusterId": cluster_id})
+    token, delay, deadline = created.get("token"), 0.05, time.time() + 120
+    while not token and created.get("id") and time.time() < deadline:
+        # the server fills the value in after the create returns
+        time.sleep(delay)
+        delay = min(2.0, delay * 2)
+        token = call("GET", "/v3/clusterregistrationtokens/" + created["id"]).get("token")
 if not token:
     sys.exit("Unable to create cluster registration token!")
 cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
