@@ -33,7 +33,7 @@ from ..cloud.http import HTTPError
 from ..cloud.triton import HTTPSignatureSigner, MantaClient
 from ..errors import BackendError
 from ..state import State
-from .base import CONFIG_FILE, TFSTATE_FILE, Backend
+from .base import CONFIG_FILE, Backend
 
 ROOT = "/stor/triton-kubernetes"
 TF_ROOT = "/triton-kubernetes"

@@ -14,7 +14,7 @@ empty exactly as Go's encoder would.
 import ipaddress
 import re
 from dataclasses import dataclass
-from typing import Dict, List, Optional, Sequence, Tuple
+from typing import Dict, List, Optional, Sequence
 
 from ..config.context import Context, not_blank
 from ..errors import ConfigError
