@@ -184,6 +184,11 @@ def test_link_check_on_this_box(tmp_path):
         assert doc["status"] == "passed" and "amd.com/xgmi.link-check=passed" in labels.read_text()
     r = probe.p2p_bandwidth(0, 0, 64 << 20, 3)
     assert r["gbps"] > 100  # a device-local copy through the same path
+    cli = subprocess.run([sys.executable, "-m", "triton_kubernetes_amd", "gpu", "links"], capture_output=True,
+                         text=True, timeout=120)
+    assert cli.returncode == 0, cli.stderr
+    if probe.device_count() < 2:
+        assert json.loads(cli.stdout) == {"skipped": "single GPU"}
 
 
 def test_link_matrix_rounds_cover_every_ordered_pair():

@@ -372,3 +372,27 @@ def test_one_node_cluster_gate_shares_the_rccl_local_sweep():
         assert "shared_with" not in res and res["sizes"] == [3 << 20]
     finally:
         agent.stop()
+
+
+def test_gpu_links_cli_verdict(monkeypatch, capsys):
+    """``triton-kubernetes gpu links``: the pair matrix against the node median; a slow
+    link fails (exit 1) with the same labels the agent and the host script write."""
+    from triton_kubernetes_amd.ops import cli, probe
+
+    monkeypatch.setattr(probe, "device_count", lambda: 3)
+
+    def matrix(devs, nbytes=64 << 20, iters=3):
+        pairs = {f"{i}-{j}": 100.0 for i in devs for j in devs if i != j}
+        pairs["2-0"] = slow
+        return {"pairs": pairs, "peer_access": {k: True for k in pairs}, "errors": [], "bytes": nbytes}
+
+    monkeypatch.setattr(probe, "link_matrix", matrix)
+    slow = 90.0
+    assert cli.main(["links"]) == 0
+    doc = json.loads(capsys.readouterr().out)
+    assert doc["status"] == "passed" and doc["labels"]["amd.com/xgmi.link-check"] == "passed"
+    assert len(doc["pairs"]) == 6
+    slow = 20.0
+    assert cli.main(["links", "--min-frac", "0.5"]) == 1
+    doc = json.loads(capsys.readouterr().out)
+    assert doc["status"] == "degraded" and doc["degraded"]

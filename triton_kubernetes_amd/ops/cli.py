@@ -4,6 +4,7 @@
     python -m triton_kubernetes_amd.ops.cli topology
     python -m triton_kubernetes_amd.ops.cli labels
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
+    python -m triton_kubernetes_amd.ops.cli links [--min-frac F] [--mib M]
     python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
     python -m triton_kubernetes_amd.ops.cli gemm [--size N] [--reps R] [--schedule staggered|single-barrier] [--dtype bf16|fp8]
 
@@ -29,6 +30,9 @@ def main(argv: Sequence[str] = ()) -> int:
     r = sub.add_parser("rccl-local")
     r.add_argument("--ngpus", type=int, default=0)
     r.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
+    lk = sub.add_parser("links", help="per-link xGMI check: peer copy bandwidth of every ordered GPU pair")
+    lk.add_argument("--min-frac", type=float, default=0.5, help="fail below this fraction of the node median")
+    lk.add_argument("--mib", type=int, default=64, help="bytes per copy (MiB)")
     h = sub.add_parser("hbm")
     h.add_argument("--device", type=int, default=0)
     h.add_argument("--gib", type=float, default=4.0)
@@ -75,6 +79,18 @@ def main(argv: Sequence[str] = ()) -> int:
         res = rccl.sweep_local(n, dtype=args.dtype)
         print(json.dumps(res.to_json(), indent=2))
         return 0 if res.ok else 1
+    if args.cmd == "links":
+        from ..node.labels import link_labels
+        from . import probe
+
+        n = probe.device_count()
+        if n < 2:
+            print(json.dumps({"skipped": "single GPU"}))
+            return 0
+        matrix = probe.link_matrix(range(n), args.mib << 20)
+        verdict = link_labels(matrix, args.min_frac)
+        print(json.dumps(dict(verdict, pairs=matrix["pairs"]), indent=2, sort_keys=True))
+        return 1 if verdict["status"] == "degraded" else 0
     if args.cmd == "hbm":
         from . import probe
 
