@@ -27,6 +27,7 @@ module block the provider tests render.
 """
 
 import base64
+import contextvars
 import fnmatch
 import hashlib
 import json
@@ -149,16 +150,24 @@ def _kind(v: Any) -> str:
 # --- functions ----------------------------------------------------------------------------------
 # Files outside the module directory (SSH keys and the like) belong to the machine that
 # runs terraform; plan_module(check_files=False) treats a missing one as unknown.
-_FILES_STRICT = [True]
-_MODULE_DIR = [""]
-_RENDERED: List[Tuple[str, str]] = []  # (template file name, text) of fully known templatefile() calls
+@dataclass
+class _Run:
+    """The plan in progress (per thread / context): what file() may treat as unknown, and
+    the fully known templatefile() renderings collected for the report."""
+    check_files: bool = True
+    module_dir: str = ""
+    rendered: List[Tuple[str, str]] = field(default_factory=list)
+
+
+_RUN: contextvars.ContextVar = contextvars.ContextVar("tk_plan_run", default=_Run())
 
 
 def _f_file(path):
     p = os.path.expanduser(_tf_str(path))
     if not os.path.isfile(p):
-        inside = bool(_MODULE_DIR[0]) and os.path.abspath(p).startswith(_MODULE_DIR[0] + os.sep)
-        if not inside and not _FILES_STRICT[0]:
+        run = _RUN.get()
+        inside = bool(run.module_dir) and os.path.abspath(p).startswith(run.module_dir + os.sep)
+        if not inside and not run.check_files:
             return UNKNOWN
         raise PlanError(f"file({p!r}): no such file")
     with open(p, encoding="utf-8") as fh:
@@ -187,7 +196,7 @@ def _f_templatefile(path, variables):
         text = hcl.templatefile(src, variables, os.path.basename(path))
     except (hcl.TemplateError, KeyError, TypeError, IndexError) as exc:
         raise PlanError(f"templatefile({os.path.basename(path)!r}): {exc}") from exc
-    _RENDERED.append((os.path.basename(path), text))
+    _RUN.get().rendered.append((os.path.basename(path), text))
     return text
 
 
@@ -849,7 +858,7 @@ class _ModulePlan:
         if path is UNKNOWN:
             return
         p = os.path.expanduser(_tf_str(path))
-        if not os.path.exists(p) and (_FILES_STRICT[0] or p.startswith(self.dir + os.sep)):
+        if not os.path.exists(p) and (_RUN.get().check_files or p.startswith(self.dir + os.sep)):
             self.report.errors.append(f"{self.where(fn, src.pos)}: file provisioner source {p!r} does not exist")
 
     def eval_dynamic(self, fn: str, blk: Block, scope: _Scope) -> None:
@@ -950,17 +959,15 @@ def plan_module(module_dir: str, inputs: Dict[str, Any], check_files: bool = Tru
     ``file()`` outside the module that does not exist here (a user's SSH key path) is
     unknown rather than an error; the module's own files are always checked."""
     given = {k: v for k, v in inputs.items() if k != "source"}
-    saved = (_FILES_STRICT[0], _MODULE_DIR[0], list(_RENDERED))
-    _FILES_STRICT[0], _MODULE_DIR[0] = check_files, os.path.abspath(module_dir)
-    _RENDERED.clear()
+    run = _Run(check_files, os.path.abspath(module_dir))
+    token = _RUN.set(run)
     try:
         report = _ModulePlan(module_dir, given).run()
-        for name, text in _RENDERED:
-            report.rendered.setdefault(name, []).append(text)
-        return report
     finally:
-        _FILES_STRICT[0], _MODULE_DIR[0] = saved[:2]
-        _RENDERED[:] = saved[2]
+        _RUN.reset(token)
+    for name, text in run.rendered:
+        report.rendered.setdefault(name, []).append(text)
+    return report
 
 
 __all__ = ["PlanError", "PlanReport", "UNKNOWN", "plan_module", "evaluate", "FUNCTIONS"]
