@@ -239,6 +239,7 @@ class NodeAgent:
             return labels
         if a == "gpu_burnin":
             level = step.params.get("level", "quick")
+            self._quiesce_gpus()
             # every GPU of the node burns in concurrently (one host thread each;
             # the probes pin their device per thread)
             if len(self.devices) > 1:
@@ -350,6 +351,21 @@ class NodeAgent:
                     trimmed.append(g)
                 doc = dict(doc, gpus=trimmed)
         return doc
+
+    def _quiesce_gpus(self) -> None:
+        """Let GPU work left over from an earlier request finish before the throughput
+        gates run: a previous gate's communicator teardown and a previous full burn-in's
+        background release of its memtest memory would otherwise overlap (and slow) the
+        short burn-in kernels.  A fresh agent has neither pending."""
+        if self.burnin_override is not None or self.topology_override is not None or not self.devices:
+            return
+        from ..ops import probe
+
+        probe.wait_frees()
+        if getattr(self, "_used_rccl", False):
+            from ..ops import rccl
+
+            rccl.drain()
 
     def _burnin(self, dev: int, level: str) -> Dict[str, Any]:
         if self.burnin_override is not None:

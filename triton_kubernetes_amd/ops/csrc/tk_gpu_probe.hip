@@ -1120,7 +1120,7 @@ int main(int argc, char** argv) {
   // quick: 1 GiB; full: every free byte of HBM but 4 GiB, in 16 GiB chunks held at once
   const size_t mt_bytes = full ? 0 : (1ull << 30);
   const int mfma_iters = full ? 20000 : 2000;  // x MFMA_ACC (8) chains per wave
-  const int gemm_n = full ? 8192 : 4096, gemm_reps = full ? 5 : 2;  // ops/gemm.py:SCREEN_SIZES
+  const int gemm_n = full ? 8192 : 4096, gemm_reps = 5;  // ops/gemm.py:SCREEN_SIZES
   int n = 0;
   if (tkp_device_count(&n) != 0 || n < 1) {
     printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
@@ -1138,13 +1138,37 @@ int main(int argc, char** argv) {
     memset(&info, 0, sizeof(info));
     double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[7] = {0, 0, 0, 0, 0, 0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0},
            gm8[7] = {0, 0, 0, 0, -1, -1, 0};
-    bool ok = tkp_device_info(d, &info) == 0 && tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, hbm) == 0 &&
-              tkp_mfma_peak(d, 0, mfma_iters, 3, 2, bf16) == 0 && tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, fp8) == 0 &&
-              tkg_screen(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, gm) == 0 &&
-              tkg_screen_fp8(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, gm8) == 0 &&
+    // A throughput gate that reads below its floor is measured again (best of up to 3 runs,
+    // as ops/probe.py:run_burnin): a short kernel that overlapped other GPU work reads low
+    // once, a slow GPU every time.  A checksum mismatch in ANY GEMM run fails the GPU.
+    int remeasured = 0;
+    bool gemm_bad = false, gemm8_bad = false;
+    auto measure = [&](auto&& run, double* out, int n_out, double floor, bool* bad) -> bool {
+      if (run(out) != 0) return false;
+      if (bad) *bad = *bad || out[2] != 0.0 || out[3] != 0.0;
+      for (int r = 0; r < 2 && out[0] < floor; ++r) {
+        double again[7] = {0, 0, 0, 0, -1, -1, 0};
+        if (run(again) != 0) return false;
+        ++remeasured;
+        if (bad) *bad = *bad || again[2] != 0.0 || again[3] != 0.0;
+        if (again[0] > out[0]) memcpy(out, again, sizeof(double) * (size_t)n_out);
+      }
+      return true;
+    };
+    bool ok = tkp_device_info(d, &info) == 0 &&
+              measure([&](double* o) { return tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, o); }, hbm, 3, min_read,
+                      nullptr) &&
+              measure([&](double* o) { return tkp_mfma_peak(d, 0, mfma_iters, 3, 2, o); }, bf16, 2, min_bf16,
+                      nullptr) &&
+              measure([&](double* o) { return tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, o); }, fp8, 2, min_fp8,
+                      nullptr) &&
+              measure([&](double* o) { return tkg_screen(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, gm, 7,
+                      min_gemm, &gemm_bad) &&
+              measure([&](double* o) { return tkg_screen_fp8(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, gm8,
+                      7, min_gemm8, &gemm8_bad) &&
               tkp_memtest_span(d, mt_bytes, 16ull << 30, 4ull << 30, full ? 3 : 1, mt) == 0;
     if (!ok && tkg_last_error()[0] && !g_err[0]) snprintf(g_err, sizeof(g_err), "%s", tkg_last_error());
-    const bool gemm_ok = gm[2] == 0.0 && gm[3] == 0.0, gemm8_ok = gm8[2] == 0.0 && gm8[3] == 0.0;
+    const bool gemm_ok = !gemm_bad, gemm8_ok = !gemm8_bad;
     const bool pass = ok && strncmp(info.arch, "gfx950", 6) == 0 && hbm[0] >= min_read && bf16[0] >= min_bf16 &&
                       fp8[0] >= min_fp8 && gemm_ok && gm[0] >= min_gemm && gemm8_ok && gm8[0] >= min_gemm8 &&
                       mt[0] == 0.0;
@@ -1154,9 +1178,9 @@ int main(int argc, char** argv) {
     printf("%s{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"read_gbps\":%.1f,\"write_gbps\":%.1f,\"copy_gbps\":%.1f,"
            "\"bf16_tflops\":%.1f,\"fp8_tflops\":%.1f,\"gemm_tflops\":%.1f,\"gemm_checksum_ok\":%s,"
            "\"gemm_fp8_tflops\":%.1f,\"gemm_fp8_checksum_ok\":%s,"
-           "\"memtest_errors\":%.0f,\"memtest_bytes\":%.0f,\"hbm_bytes\":%.0f,\"ok\":%s%s%s%s}",
+           "\"memtest_errors\":%.0f,\"memtest_bytes\":%.0f,\"hbm_bytes\":%.0f,\"remeasured\":%d,\"ok\":%s%s%s%s}",
            k ? "," : "", d, info.arch, info.compute_units, hbm[0], hbm[1], hbm[2], bf16[0], fp8[0], gm[0],
-           gemm_ok ? "true" : "false", gm8[0], gemm8_ok ? "true" : "false", mt[0], mt[2], mt[3],
+           gemm_ok ? "true" : "false", gm8[0], gemm8_ok ? "true" : "false", mt[0], mt[2], mt[3], remeasured,
            pass ? "true" : "false", ok ? "" : ",\"error\":\"", ok ? "" : g_err, ok ? "" : "\"");
   }
   printf("],\"ok\":%s}\n", ok_all ? "true" : "false");

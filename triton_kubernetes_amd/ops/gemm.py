@@ -17,7 +17,8 @@ TILE_K = 64  # bf16 elements per K-tile (128 bytes of a row)
 TILE_K_FP8 = 128  # fp8 e4m3 elements per K-tile
 
 # level -> (M, N, K, timed reps)
-SCREEN_SIZES = {"quick": (4096, 4096, 4096, 2), "full": (8192, 8192, 8192, 5)}
+# quick: a 4096^3 GEMM is ~60-100 us, so best of 5 (each rep is one timed launch)
+SCREEN_SIZES = {"quick": (4096, 4096, 4096, 5), "full": (8192, 8192, 8192, 5)}
 
 
 class GemmError(RuntimeError):

@@ -213,6 +213,7 @@ def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3) 
 
 
 # --- burn-in policy ------------------------------------------------------------------
+REMEASURE = 2  # extra runs of a throughput gate that read below its floor
 LEVELS = {
     # level: (hbm bytes, hbm iters, mfma iters (x 8 accumulator chains per wave), memtest bytes, memtest passes)
     # memtest bytes 0 = every free byte of HBM but 4 GiB (memtest_span); quick tests 1 GiB
@@ -244,6 +245,7 @@ class BurninResult:
     gemm_fp8: Dict[str, Any] = field(default_factory=dict)
     memtest: Dict[str, float] = field(default_factory=dict)
     failures: List[str] = field(default_factory=list)
+    remeasured: List[str] = field(default_factory=list)  # throughput gates read low and measured again
 
     @property
     def ok(self) -> bool:
@@ -266,15 +268,33 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
         res.failures.append(f"arch {info.arch} is not gfx950")
     if info.compute_units < th.min_cus:
         res.failures.append(f"{info.compute_units} CUs < {th.min_cus}")
+    # Throughput gates are re-measured (best of up to REMEASURE + 1 runs) before they fail
+    # a node: a short kernel that overlapped other GPU work on the node (a previous
+    # communicator's teardown, another process) reads low once; a slow GPU reads low every
+    # time.  Correctness results (checksums, memtest words) are never retried away.
+    def best(measure, value, floor, what):
+        r = measure()
+        for _ in range(REMEASURE):
+            if value(r) >= floor:
+                break
+            again = measure()
+            res.remeasured.append(what)
+            if value(again) > value(r):
+                r = again
+        return r
+
     with span("burnin.hbm", dev=dev):
-        res.hbm = hbm_bandwidth(dev, hbm_bytes, hbm_iters)
-    if res.hbm["read_gbps"] < th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS:
+        floor = th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS
+        res.hbm = best(lambda: hbm_bandwidth(dev, hbm_bytes, hbm_iters), lambda r: r["read_gbps"], floor, "hbm")
+    if res.hbm["read_gbps"] < floor:
         res.failures.append(f"HBM read {res.hbm['read_gbps']:.0f} GB/s below "
                             f"{th.min_read_frac:.0%} of {MI355X_HBM_ACHIEVABLE_GBPS:.0f}")
     with span("burnin.mfma_bf16", dev=dev):
-        res.mfma["bf16"] = mfma_peak(dev, "bf16", mfma_iters)
+        res.mfma["bf16"] = best(lambda: mfma_peak(dev, "bf16", mfma_iters), lambda r: r["tflops"],
+                                th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS, "mfma_bf16")
     with span("burnin.mfma_fp8", dev=dev):
-        res.mfma["fp8"] = mfma_peak(dev, "fp8", mfma_iters // 2)
+        res.mfma["fp8"] = best(lambda: mfma_peak(dev, "fp8", mfma_iters // 2), lambda r: r["tflops"],
+                               th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS, "mfma_fp8")
     if res.mfma["bf16"]["tflops"] < th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS:
         res.failures.append(f"bf16 MFMA {res.mfma['bf16']['tflops']:.0f} TF below "
                             f"{th.min_bf16_frac:.0%} of dense peak")
@@ -286,16 +306,24 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
     m, n, k, reps = gemm.SCREEN_SIZES[level]
     for dtype, peak, frac in (("bf16", MI355X_BF16_DENSE_TFLOPS, th.min_gemm_frac),
                               ("fp8", MI355X_FP8_DENSE_TFLOPS, th.min_gemm_fp8_frac)):
-        with span(f"burnin.gemm_{dtype}", dev=dev):
+        name = "GEMM" if dtype == "bf16" else "fp8 GEMM"
+        runs = []
+
+        def screen_once(dtype=dtype, runs=runs):
             g = gemm.screen(dev, m, n, k, reps, dtype=dtype)
+            runs.append(g)
+            return g
+
+        with span(f"burnin.gemm_{dtype}", dev=dev):
+            g = best(screen_once, lambda r: r.tflops, frac * peak, f"gemm_{dtype}")
         if dtype == "bf16":
             res.gemm = g.to_json()
         else:
             res.gemm_fp8 = g.to_json()
-        name = "GEMM" if dtype == "bf16" else "fp8 GEMM"
-        if not g.ok:
-            res.failures.append(f"{name} checksum mismatch: {g.bad_rows} rows / {g.bad_columns} columns "
-                                f"(first at row {g.first_bad_row}, column {g.first_bad_column})")
+        bad = next((r for r in runs if not r.ok), None)  # a mismatch in ANY run fails the GPU
+        if bad is not None:
+            res.failures.append(f"{name} checksum mismatch: {bad.bad_rows} rows / {bad.bad_columns} columns "
+                                f"(first at row {bad.first_bad_row}, column {bad.first_bad_column})")
         if g.tflops < frac * peak:
             res.failures.append(f"{name} {g.tflops:.0f} TF below {frac:.0%} of dense {dtype} peak")
     with span("burnin.memtest", dev=dev):
