@@ -1,0 +1,76 @@
+"""Burn-in gate policy (``ops/probe.py:run_burnin``) with scripted measurements: a
+throughput gate that reads low once is measured again, a GPU that reads low every time
+fails, and a GEMM checksum mismatch in any run fails the GPU even if a later run is clean."""
+
+import pytest
+
+from triton_kubernetes_amd.ops import gemm, probe
+
+
+def _info():
+    return probe.DeviceInfo(0, "AMD Instinct MI355X", "gfx950:sramecc+:xnack-", 256, 64, 2400.0, 288.0, 287.0,
+                            4 << 20, "0000:05:00.0")
+
+
+def _screen(tflops, bad=0, dtype="bf16"):
+    return gemm.ScreenResult(4096, 4096, 4096, tflops, 0.1, bad, bad, 0 if bad else -1, 0 if bad else -1, 0.01,
+                             dtype)
+
+
+@pytest.fixture
+def scripted(monkeypatch):
+    """Queues of results per measurement; the last value repeats."""
+    script = {"hbm": [6800.0], "bf16": [1850.0], "fp8": [4000.0], "gemm_bf16": [_screen(1400.0)],
+              "gemm_fp8": [_screen(2500.0, dtype="fp8")]}
+    calls = {k: 0 for k in script}
+
+    def take(key):
+        i = calls[key]
+        calls[key] += 1
+        q = script[key]
+        return q[min(i, len(q) - 1)]
+
+    monkeypatch.setattr(probe, "device_info", lambda dev: _info())
+    monkeypatch.setattr(probe, "hbm_bandwidth", lambda *a, **k: {"read_gbps": take("hbm"), "write_gbps": 6000.0,
+                                                                  "copy_gbps": 5500.0})
+    monkeypatch.setattr(probe, "mfma_peak", lambda dev, dtype, iters, *a, **k: {"tflops": take(dtype)})
+    monkeypatch.setattr(gemm, "screen", lambda dev, m, n, k, reps, dtype="bf16": take(f"gemm_{dtype}"))
+    monkeypatch.setattr(probe, "memtest", lambda dev, nbytes, passes: {"errors": 0, "verify_gbps": 5000.0})
+    return script, calls
+
+
+def test_healthy_gpu_measured_once(scripted):
+    script, calls = scripted
+    res = probe.run_burnin(0, "quick")
+    assert res.ok and res.remeasured == [] and set(calls.values()) == {1}
+
+
+def test_one_low_reading_is_measured_again(scripted):
+    script, calls = scripted
+    script["gemm_fp8"] = [_screen(1334.0, dtype="fp8"), _screen(2450.0, dtype="fp8")]  # one overlapped run
+    script["hbm"] = [3000.0, 6900.0]
+    res = probe.run_burnin(0, "quick")
+    assert res.ok, res.failures
+    assert res.remeasured == ["hbm", "gemm_fp8"]
+    assert res.gemm_fp8["tflops"] == 2450.0 and res.hbm["read_gbps"] == 6900.0
+
+
+def test_slow_every_time_fails_after_three_runs(scripted):
+    script, calls = scripted
+    script["bf16"] = [900.0]
+    res = probe.run_burnin(0, "quick")
+    assert not res.ok and any("bf16 MFMA 900 TF" in f for f in res.failures)
+    assert calls["bf16"] == 1 + probe.REMEASURE
+
+
+def test_checksum_mismatch_is_never_retried_away(scripted):
+    script, calls = scripted
+    # a corrupted AND slow first run, then a clean fast one: the GPU still fails
+    script["gemm_bf16"] = [_screen(600.0, bad=3), _screen(1400.0)]
+    res = probe.run_burnin(0, "quick")
+    assert not res.ok and any("checksum mismatch" in f for f in res.failures)
+    # a corrupted run at full speed is not re-measured at all, and fails too
+    script["gemm_bf16"] = [_screen(1400.0, bad=1)]
+    calls["gemm_bf16"] = 0
+    res = probe.run_burnin(0, "quick")
+    assert not res.ok and calls["gemm_bf16"] == 1
