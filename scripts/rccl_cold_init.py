@@ -47,6 +47,9 @@ VARIANTS = {
     "comgr_cache_hit": {"AMD_COMGR_CACHE": "1", "AMD_COMGR_CACHE_DIR": "/tmp/tk-comgr-cache"},
     "comgr_cache_hit2": {"AMD_COMGR_CACHE": "1", "AMD_COMGR_CACHE_DIR": "/tmp/tk-comgr-cache"},
     "base2": {},
+    # ncclCommAbort instead of ncclCommDestroy once the verified sweep has drained the streams
+    "teardown_abort": {"TK_TEARDOWN_ABORT": "1"},
+    "teardown_abort2": {"TK_TEARDOWN_ABORT": "1"},
     "torch_runtime_all_off": {"TK_HIP_RUNTIME": "torch", "RCCL_MSCCL_ENABLE": "0", "RCCL_MSCCLPP_ENABLE": "0",
                               "NCCL_NET_PLUGIN": "none"},
 }
@@ -66,6 +69,8 @@ def child() -> None:
 
     mark("import")
     rccl._lib()
+    if os.environ.get("TK_TEARDOWN_ABORT") == "1":
+        rccl._lib().tkr_set_teardown_abort(1)
     probe._lib()
     mark("dlopen")
     probe.device_count()
