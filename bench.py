@@ -70,6 +70,9 @@ def parse_args():
     ap.add_argument("--agents", default="proc", choices=["proc", "inproc"],
                     help="proc: every agent in its own fresh process (the headline); inproc: agents as "
                          "objects in this process (the graft smoke: native libraries load here)")
+    ap.add_argument("--rccl-slim", default="on", choices=["on", "off"],
+                    help="on: node install step (before the timed region) prepares the single-target gfx950 "
+                         "RCCL the agents load (ops/rccl_slim.py; the agent unit's ExecStartPre on a real node)")
     ap.add_argument("--sim-gpu", action="store_true",
                     help="CPU dry run: synthetic topology, no burn-in kernels, no RCCL (never a valid measurement)")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
@@ -212,6 +215,22 @@ def main() -> int:
     from triton_kubernetes_amd.config import Context, Settings
     from triton_kubernetes_amd.parallel.transport import AgentTransport
     from triton_kubernetes_amd.utils.trace import TRACER, span
+
+    slim_meta = None
+    if args.rccl_slim == "off" or args.sim_gpu:
+        os.environ["TK_RCCL_SLIM"] = "0"  # inherited by the agent processes
+    elif local_rank == 0:
+        # node install (one-time per RCCL build, cached): what the agent's systemd unit runs
+        # as ExecStartPre on a real node.  Outside the timed region, like the OS image.
+        from triton_kubernetes_amd.ops import native, rccl_slim
+
+        src = native._torch_lib_dir()
+        if src:
+            try:
+                slim_meta = rccl_slim.prepare(src)
+            except (rccl_slim.SlimError, OSError) as exc:
+                print(f"warning: single-target RCCL not prepared ({exc}); agents load the full bundle",
+                      file=sys.stderr)
 
     token = os.environ.get("TK_BENCH_TOKEN", "bench-token-0123456789")
     work = tempfile.mkdtemp(prefix=f"tk-bench-r{rank}-")
@@ -400,7 +419,9 @@ def main() -> int:
                            "via the fake's connect API instead of docker run rancher/agent); real on MI355X: "
                            f"native topology + RDMA labels, per-GPU HBM/MFMA/memtest burn-in level={args.burnin}, "
                            f"cluster RCCL all-reduce gate {'off' if args.no_rccl_gate else 'on'} "
-                           f"(one communicator over all {n_gpus} GPUs)"),
+                           f"(one communicator over all {n_gpus} GPUs)"
+                           + ("; node install before the timed region: single-target gfx950 RCCL device code "
+                              "(ops/rccl_slim.py)" if slim_meta else "")),
             "config": {
                 "model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology labels",
                 "workers": workers, "gpus_per_worker": gpus_per_worker, "visible_gpus": visible,
@@ -414,6 +435,9 @@ def main() -> int:
                 "rancher": versions.RANCHER_VERSION, "k8s_version": versions.DEFAULT_K8S_VERSION,
                 # HIP runtime + RCCL the GPU agents ran on (ops/native.py:select_runtime)
                 "agent_hip_runtime": sorted(runtimes),
+                # node install step outside the timed region (ops/rccl_slim.py)
+                "rccl_slim": ({k: slim_meta[k] for k in ("prepare_s", "cached", "source_fatbin_bytes",
+                                                          "loaded_code_object_bytes")} if slim_meta else None),
             },
             "create_to_ready_s": ready,
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),

@@ -53,6 +53,14 @@ if [ "$MODE" = steps ]; then
   step bench_steps 300 python bench.py --steps 3 --warmup 1 --warm-steps 0
   step bench_steps_full 600 python bench.py --steps 2 --warmup 1 --warm-steps 0 --burnin full
 fi
+if [ "$MODE" = slim ]; then
+  # single-target RCCL (ops/rccl_slim.py): GPU test, then the cold bench with / without it, alternating
+  step slim_test 300 python -u -m pytest tests/test_gpu_probes.py -k slim -x -v -s --timeout 120 --timeout-method thread
+  step bench_slim1 300 python bench.py --steps 5 --warmup 1 --report gpurun_out/bench_slim1.json
+  step bench_noslim1 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --rccl-slim off --report gpurun_out/bench_noslim1.json
+  step bench_slim2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --report gpurun_out/bench_slim2.json
+  step bench_noslim2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --rccl-slim off --report gpurun_out/bench_noslim2.json
+fi
 if [ "$MODE" = span ]; then
   step memtest_span 300 python scripts/memtest_span_chunks.py
 fi

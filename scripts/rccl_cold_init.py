@@ -50,6 +50,11 @@ VARIANTS = {
     # ncclCommAbort instead of ncclCommDestroy once the verified sweep has drained the streams
     "teardown_abort": {"TK_TEARDOWN_ABORT": "1"},
     "teardown_abort2": {"TK_TEARDOWN_ABORT": "1"},
+    # ops/rccl_slim.py: gfx950-only, uncompressed device code (the parent prepares it first)
+    "slim": {"TK_HIP_RUNTIME": "@slim"},
+    "slim2": {"TK_HIP_RUNTIME": "@slim"},
+    "torch_runtime2": {"TK_HIP_RUNTIME": "torch"},
+    "slim_system": {"TK_HIP_RUNTIME": "@slim:/opt/rocm/lib"},
     "torch_runtime_all_off": {"TK_HIP_RUNTIME": "torch", "RCCL_MSCCL_ENABLE": "0", "RCCL_MSCCLPP_ENABLE": "0",
                               "NCCL_NET_PLUGIN": "none"},
 }
@@ -129,6 +134,12 @@ def parent() -> None:
     names = sys.argv[1:] or list(VARIANTS)
     for name in names:
         env = dict(os.environ, **VARIANTS[name])
+        if env.get("TK_HIP_RUNTIME", "").startswith("@slim"):
+            from triton_kubernetes_amd.ops import native, rccl_slim
+
+            meta = rccl_slim.prepare(env["TK_HIP_RUNTIME"].partition(":")[2] or native._torch_lib_dir())
+            print(json.dumps({"slim_prepare": meta}), flush=True)
+            env["TK_HIP_RUNTIME"] = meta["dir"]
         t0 = time.perf_counter()
         proc = subprocess.run([sys.executable, os.path.abspath(__file__), "--child"], env=env, capture_output=True,
                               text=True, timeout=300, check=False)

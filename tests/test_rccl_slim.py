@@ -1,0 +1,181 @@
+"""Single-target RCCL preparation (ops/rccl_slim.py) and its runtime selection (ops/native.py).
+
+CPU only: the in-tree gfx950 libraries stand in for ``librccl.so`` (their ``.hip_fatbin`` is
+an uncompressed host+gfx950 bundle); a compressed multi-target source is made from them with
+``clang-offload-bundler --compress``, the format of the PyTorch-ROCm and /opt/rocm RCCL builds.
+The GPU side (the slim library loads, and the first communicator init gets faster) is
+``tests/test_gpu_probes.py::test_slim_rccl_runtime_gate`` and ``profiles/round2/rccl_slim_ab.md``.
+"""
+
+import json
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+
+from triton_kubernetes_amd.ops import native, rccl_slim
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+GFX950 = rccl_slim.device_triple("gfx950")
+
+
+def _lib(name="libtk_gpu_probe.so"):
+    path = os.path.join(native.LIB_DIR, name)
+    if not os.path.exists(path):
+        pytest.skip(f"{name} not built")
+    return path
+
+
+def _section(path):
+    off, size = rccl_slim.elf_section(path, ".hip_fatbin")
+    with open(path, "rb") as fh:
+        fh.seek(off)
+        return off, size, fh.read(size)
+
+
+def _fake_runtime(tmp_path, lib):
+    """A runtime dir: ``librccl.so`` (a copy of ``lib``) plus a dependency next to it."""
+    src = tmp_path / "src"
+    src.mkdir()
+    shutil.copyfile(lib, src / "librccl.so")
+    (src / "libamdhip64.so").write_bytes(b"not really a library")
+    return str(src)
+
+
+def test_bundle_round_trip_and_alignment():
+    co = b"\x7fELF" + bytes(range(256)) * 40
+    data = rccl_slim.make_bundle([(rccl_slim.HOST_TRIPLE, b""), (GFX950, co)])
+    entries = rccl_slim.parse_bundle(data)
+    assert [e[0] for e in entries] == [rccl_slim.HOST_TRIPLE, GFX950]
+    _, off, size = entries[1]
+    assert off % rccl_slim.ALIGN == 0 and size == len(co) and data[off:off + size] == co
+    assert entries[0][1:] == (0, 0)
+
+
+def test_in_tree_library_sections_parse():
+    _, _, data = _section(_lib())
+    triples = [t for t, _, _ in rccl_slim.parse_bundle(data)]
+    assert GFX950 in triples
+
+
+def test_prepare_from_plain_bundle(tmp_path):
+    lib = _lib()
+    src = _fake_runtime(tmp_path, lib)
+    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False)
+    out = meta["dir"]
+    assert not meta["cached"] and meta["source_format"] == "bundle"
+    assert os.path.exists(os.path.join(out, "slim.json"))
+    # same size and section placement; a single device entry holding the original code object
+    assert os.path.getsize(os.path.join(out, "librccl.so")) == os.path.getsize(lib)
+    off0, size0, orig = _section(lib)
+    off1, size1, new = _section(os.path.join(out, "librccl.so"))
+    assert (off0, size0) == (off1, size1)
+    entries = rccl_slim.parse_bundle(new)
+    assert [t for t, _, _ in entries] == [rccl_slim.HOST_TRIPLE, GFX950]
+    want = next(orig[o:o + s] for t, o, s in rccl_slim.parse_bundle(orig) if t == GFX950)
+    _, o, s = entries[1]
+    assert new[o:o + s] == want
+    assert new[meta["bundle_bytes"]:] == b"\0" * (size1 - meta["bundle_bytes"])
+    # bytes outside the section are untouched
+    with open(lib, "rb") as a, open(os.path.join(out, "librccl.so"), "rb") as b:
+        x, y = a.read(), b.read()
+    assert x[:off0] == y[:off0] and x[off0 + size0:] == y[off0 + size0:]
+    # the rest of the runtime is linked in; a second prepare is a cache hit
+    assert os.path.islink(os.path.join(out, "libamdhip64.so"))
+    assert rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False)["cached"] is True
+    assert rccl_slim.cached(src, root=str(tmp_path / "cache")) == ""  # the stripped entry is another key
+
+
+@pytest.mark.skipif(not rccl_slim.find_tool("clang-offload-bundler"), reason="no ROCm LLVM bundler")
+def test_prepare_from_compressed_multi_target_bundle(tmp_path):
+    """The shape of the real RCCL builds: one compressed bundle of many targets."""
+    lib = _lib()
+    _, _, orig = _section(lib)
+    co = next(orig[o:o + s] for t, o, s in rccl_slim.parse_bundle(orig) if t == GFX950)
+    (tmp_path / "gfx950.co").write_bytes(co)
+    (tmp_path / "other.co").write_bytes(co[::-1])
+    (tmp_path / "host").write_bytes(b"")
+    bundler = rccl_slim.find_bundler()
+    targets = ",".join([rccl_slim.HOST_TRIPLE, rccl_slim.device_triple("gfx942"), GFX950])
+    subprocess.run([bundler, "--compress", "--type=o", f"--targets={targets}",
+                    f"--input={tmp_path / 'host'}", f"--input={tmp_path / 'other.co'}",
+                    f"--input={tmp_path / 'gfx950.co'}", f"--output={tmp_path / 'fat.bin'}"], check=True,
+                   capture_output=True)
+    fat = (tmp_path / "fat.bin").read_bytes()
+    assert fat.startswith(rccl_slim.COMPRESSED_MAGIC)
+    src = _fake_runtime(tmp_path, lib)
+    off, size, _ = _section(os.path.join(src, "librccl.so"))
+    assert len(fat) <= size
+    with open(os.path.join(src, "librccl.so"), "r+b") as fh:
+        fh.seek(off)
+        fh.write(fat + b"\0" * (size - len(fat)))
+    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"))
+    assert meta["source_format"] == "compressed"
+    _, _, new = _section(os.path.join(meta["dir"], "librccl.so"))
+    entries = rccl_slim.parse_bundle(new)
+    assert [t for t, _, _ in entries] == [rccl_slim.HOST_TRIPLE, GFX950]
+    _, o, s = entries[1]
+    got = new[o:o + s]
+    assert got[:4] == b"\x7fELF" and s == meta["loaded_code_object_bytes"] <= len(co)
+    # a target the bundle lacks is an error, and no partial entry is left behind
+    with pytest.raises(rccl_slim.SlimError, match="gfx1234"):
+        rccl_slim.prepare(src, arch="gfx1234", root=str(tmp_path / "cache2"))
+    assert not os.path.exists(tmp_path / "cache2") or os.listdir(tmp_path / "cache2") == []
+
+
+def test_partial_entry_is_never_used(tmp_path):
+    src = _fake_runtime(tmp_path, _lib())
+    d = rccl_slim.entry_dir(src, root=str(tmp_path / "cache"))
+    os.makedirs(d)
+    shutil.copyfile(os.path.join(src, "librccl.so"), os.path.join(d, "librccl.so"))
+    assert rccl_slim.cached(src, root=str(tmp_path / "cache")) == ""
+
+
+def test_source_change_invalidates_the_entry(tmp_path):
+    src = _fake_runtime(tmp_path, _lib())
+    root = str(tmp_path / "cache")
+    rccl_slim.prepare(src, root=root, strip=False)
+    k1 = rccl_slim.entry_dir(src, root=root)
+    os.utime(os.path.join(src, "librccl.so"), ns=(1, 1))
+    assert rccl_slim.entry_dir(src, root=root) != k1
+
+
+def test_non_elf_is_refused(tmp_path):
+    src = tmp_path / "src"
+    src.mkdir()
+    (src / "librccl.so").write_bytes(b"MZ" + b"\0" * 100)
+    with pytest.raises(rccl_slim.SlimError, match="not an ELF64"):
+        rccl_slim.prepare(str(src), root=str(tmp_path / "cache"))
+
+
+def _select(env):
+    code = "from triton_kubernetes_amd.ops import native; print(native.select_runtime())"
+    p = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, cwd=ROOT, timeout=120,
+                       env=dict(os.environ, **env))
+    assert p.returncode == 0, p.stderr
+    return p.stdout.strip()
+
+
+def test_auto_selects_the_prepared_slim_runtime(tmp_path):
+    torch_dir = native._torch_lib_dir()
+    if not torch_dir:
+        pytest.skip("no PyTorch-ROCm runtime")
+    root = str(tmp_path / "cache")
+    assert _select({"TK_HIP_RUNTIME": "auto", "TK_RCCL_SLIM_DIR": root}) == torch_dir
+    # prepared (the agent unit's ExecStartPre) -> auto picks it; TK_RCCL_SLIM=0 opts out
+    d = rccl_slim.entry_dir(torch_dir, root=root)
+    os.makedirs(d)
+    with open(os.path.join(d, "slim.json"), "w", encoding="utf-8") as fh:
+        json.dump({"dir": d}, fh)
+    assert _select({"TK_HIP_RUNTIME": "auto", "TK_RCCL_SLIM_DIR": root}) == d
+    assert _select({"TK_HIP_RUNTIME": "slim", "TK_RCCL_SLIM_DIR": root}) == d
+    assert _select({"TK_HIP_RUNTIME": "auto", "TK_RCCL_SLIM_DIR": root, "TK_RCCL_SLIM": "0"}) == torch_dir
+    assert _select({"TK_HIP_RUNTIME": "torch", "TK_RCCL_SLIM_DIR": root}) == torch_dir
+
+
+def test_cli_reports_errors_as_json(tmp_path):
+    p = subprocess.run([sys.executable, "-m", "triton_kubernetes_amd.ops.rccl_slim", "--source", str(tmp_path),
+                        "--root", str(tmp_path / "c")], capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert p.returncode == 1 and "librccl.so missing" in json.loads(p.stdout)["error"]

@@ -28,6 +28,7 @@ class NativeUnavailable(RuntimeError):
 
 
 _runtime_dir = None
+SYSTEM_LIB_DIR = "/opt/rocm/lib"
 _RUNTIME_LIBS = ("libhsa-runtime64.so", "libamd_comgr.so", "libamdhip64.so", "librccl.so")
 
 
@@ -49,23 +50,52 @@ def select_runtime() -> str:
     * ``auto`` (default): the builds bundled with an installed PyTorch-ROCm wheel (its
       ``lib/``, found without importing torch) when present -- the runtime and RCCL that
       ``torch.distributed`` jobs on the node use, and the one the GPU test-suite runs on
-      (tests import torch first) -- else ``/opt/rocm``;
+      (tests import torch first) -- else ``/opt/rocm``.  When the node has prepared the
+      single-target copy of that RCCL (``ops/rccl_slim.py``; the agent unit's
+      ``ExecStartPre``), its directory instead, unless ``TK_RCCL_SLIM=0``;
+    * ``slim``: that single-target directory, prepared now if the node has none yet;
     * ``system``: ``/opt/rocm`` (the libraries' RUNPATH);
     * ``torch``: the PyTorch-ROCm builds, required;
     * a path: a directory holding ``libamdhip64.so`` / ``librccl.so``.
 
-    Measured on MI355X (``profiles/round2/runtime_ab.md``): a cold process's first RCCL
-    communicator init takes ~0.9 s on the PyTorch-ROCm 7.0 build (RCCL 2.26.6) against
-    ~1.7 s on ``/opt/rocm`` 7.2 (RCCL 2.27.7), whose device code is one 544 MiB bundle."""
+    Measured on MI355X (``profiles/round2/runtime_ab.md``, ``profiles/round2/rccl_slim_ab.md``):
+    a cold process's first RCCL communicator init takes ~0.9 s on the PyTorch-ROCm 7.0 build
+    (RCCL 2.26.6), ~1.7 s on ``/opt/rocm`` 7.2 (RCCL 2.27.7), whose device code is one
+    544 MiB compressed bundle, and ~0.27 s on the single-target copy."""
     sel = os.environ.get("TK_HIP_RUNTIME", "auto") or "auto"
     if sel == "system":
         return "system"
-    if sel in ("auto", "torch"):
+    if sel in ("auto", "torch", "slim"):
         d = _torch_lib_dir()
+        if d and sel != "torch" and os.environ.get("TK_RCCL_SLIM", "1") != "0":
+            from . import rccl_slim
+
+            slim = rccl_slim.cached(d)
+            if slim:
+                return slim
+            if sel == "slim":
+                try:
+                    return str(rccl_slim.prepare(d)["dir"])
+                except (rccl_slim.SlimError, OSError) as exc:
+                    raise NativeUnavailable(f"TK_HIP_RUNTIME=slim: {exc}") from exc
         if d:
             return d
         if sel == "torch":
             raise NativeUnavailable("TK_HIP_RUNTIME=torch but no PyTorch-ROCm runtime is installed")
+        # no PyTorch-ROCm: /opt/rocm, or the single-target copy of its RCCL
+        if os.environ.get("TK_RCCL_SLIM", "1") != "0" and os.path.exists(os.path.join(SYSTEM_LIB_DIR, "librccl.so")):
+            from . import rccl_slim
+
+            slim = rccl_slim.cached(SYSTEM_LIB_DIR)
+            if slim:
+                return slim
+            if sel == "slim":
+                try:
+                    return str(rccl_slim.prepare(SYSTEM_LIB_DIR)["dir"])
+                except (rccl_slim.SlimError, OSError) as exc:
+                    raise NativeUnavailable(f"TK_HIP_RUNTIME=slim: {exc}") from exc
+        if sel == "slim":
+            raise NativeUnavailable("TK_HIP_RUNTIME=slim but no RCCL is installed")
         return "system"
     return sel
 

@@ -1,0 +1,326 @@
+"""Single-target RCCL for a node's cold communicator init.
+
+Why.  A fresh process's first RCCL communicator init on MI355X is dominated by
+loading RCCL's device code, not by the init itself (``profiles/round2/
+cold_rccl_init.md``): ``librccl.so`` carries its kernels for every GPU target
+(13 on the PyTorch-ROCm build) as ONE compressed offload bundle (``CCOB``), and
+the HIP runtime decompresses the whole bundle to find the gfx950 code object the
+first time a kernel is touched.  Every node agent, every ``rccl-ready`` gate and
+every cold create pays that again.
+
+What.  :func:`prepare` makes, once per node and per RCCL build, a copy of
+``librccl.so`` whose ``.hip_fatbin`` section holds an UNCOMPRESSED bundle with only
+the node's target (gfx950).  The section keeps its address and size (the new
+bundle is smaller and zero-padded), so nothing else in the ELF moves; the HIP
+runtime then maps the gfx950 code object straight out of the file.  The other
+libraries of the source directory are symlinked next to it (``librccl.so`` finds
+its dependencies through ``$ORIGIN``), so the directory is a drop-in runtime for
+``ops/native.py:select_runtime``.
+
+Cache.  ``$TK_RCCL_SLIM_DIR`` (default ``/var/lib/triton-kubernetes/rccl-slim``
+when writable, else ``~/.cache/triton-kubernetes/rccl-slim``), one subdirectory
+per source build (keyed by path, size, mtime and a hash of its first MiB).  A
+finished entry holds ``slim.json``; a partial one is never used.
+
+The compressed bundle is unpacked with ``clang-offload-bundler`` from the ROCm
+LLVM toolchain (``/opt/rocm/lib/llvm/bin`` or ``/opt/rocm/llvm/bin``); an
+already-uncompressed bundle is split here without it.
+"""
+
+import hashlib
+import json
+import os
+import shutil
+import struct
+import subprocess
+import tempfile
+import time
+from typing import Dict, List, Optional, Tuple
+
+BUNDLE_MAGIC = b"__CLANG_OFFLOAD_BUNDLE__"
+COMPRESSED_MAGIC = b"CCOB"
+HOST_TRIPLE = "host-x86_64-unknown-linux-gnu-"
+ALIGN = 4096
+_BUNDLER_DIRS = ("/opt/rocm/lib/llvm/bin", "/opt/rocm/llvm/bin")
+
+
+class SlimError(RuntimeError):
+    pass
+
+
+def device_triple(arch: str = "gfx950") -> str:
+    return f"hipv4-amdgcn-amd-amdhsa--{arch}"
+
+
+def cache_root() -> str:
+    env = os.environ.get("TK_RCCL_SLIM_DIR")
+    if env:
+        return env
+    system = "/var/lib/triton-kubernetes/rccl-slim"
+    parent = os.path.dirname(system)
+    if os.access(parent, os.W_OK) or (not os.path.exists(parent) and os.access(os.path.dirname(parent), os.W_OK)):
+        return system
+    return os.path.join(os.path.expanduser("~"), ".cache", "triton-kubernetes", "rccl-slim")
+
+
+def elf_section(path: str, name: str) -> Tuple[int, int]:
+    """(file offset, size) of section ``name`` in the ELF64 little-endian file ``path``."""
+    with open(path, "rb") as fh:
+        ident = fh.read(64)
+        if ident[:4] != b"\x7fELF" or ident[4] != 2 or ident[5] != 1:
+            raise SlimError(f"{path}: not an ELF64 little-endian file")
+        e_shoff, = struct.unpack_from("<Q", ident, 0x28)
+        e_shentsize, e_shnum, e_shstrndx = struct.unpack_from("<HHH", ident, 0x3A)
+        fh.seek(e_shoff)
+        table = fh.read(e_shentsize * e_shnum)
+        shdrs = [struct.unpack_from("<IIQQQQIIQQ", table, i * e_shentsize) for i in range(e_shnum)]
+        str_off, str_size = shdrs[e_shstrndx][4], shdrs[e_shstrndx][5]
+        fh.seek(str_off)
+        strtab = fh.read(str_size)
+    for sh_name, sh_type, _flags, _addr, sh_offset, sh_size, *_ in shdrs:
+        end = strtab.index(b"\0", sh_name)
+        if strtab[sh_name:end].decode() == name:
+            if sh_type == 8:  # SHT_NOBITS: no file bytes to rewrite
+                raise SlimError(f"{path}: section {name} has no file contents")
+            return sh_offset, sh_size
+    raise SlimError(f"{path}: no {name} section")
+
+
+def parse_bundle(data: bytes) -> List[Tuple[str, int, int]]:
+    """Entries (triple, offset, size) of an uncompressed offload bundle."""
+    if not data.startswith(BUNDLE_MAGIC):
+        raise SlimError("not an uncompressed offload bundle")
+    n, = struct.unpack_from("<Q", data, len(BUNDLE_MAGIC))
+    pos = len(BUNDLE_MAGIC) + 8
+    out = []
+    for _ in range(n):
+        off, size, tlen = struct.unpack_from("<QQQ", data, pos)
+        pos += 24
+        triple = data[pos:pos + tlen].decode()
+        pos += tlen
+        out.append((triple, off, size))
+    return out
+
+
+def make_bundle(entries: List[Tuple[str, bytes]]) -> bytes:
+    """Uncompressed offload bundle of ``entries`` (triple, payload), payloads 4 KiB aligned."""
+    header = len(BUNDLE_MAGIC) + 8 + sum(24 + len(t.encode()) for t, _ in entries)
+    offsets, pos = [], header
+    for _, payload in entries:
+        if payload:
+            pos = (pos + ALIGN - 1) // ALIGN * ALIGN
+        offsets.append(pos)
+        pos += len(payload)
+    buf = bytearray(pos)
+    buf[:len(BUNDLE_MAGIC)] = BUNDLE_MAGIC
+    struct.pack_into("<Q", buf, len(BUNDLE_MAGIC), len(entries))
+    p = len(BUNDLE_MAGIC) + 8
+    for (triple, payload), off in zip(entries, offsets):
+        t = triple.encode()
+        struct.pack_into("<QQQ", buf, p, off if payload else 0, len(payload), len(t))
+        p += 24
+        buf[p:p + len(t)] = t
+        p += len(t)
+        buf[off:off + len(payload)] = payload
+    return bytes(buf)
+
+
+def find_tool(name: str) -> str:
+    """``name`` from the ROCm LLVM toolchain (then PATH), or ``""``."""
+    for d in _BUNDLER_DIRS:
+        cand = os.path.join(d, name)
+        if os.access(cand, os.X_OK):
+            return cand
+    return shutil.which(name) or ""
+
+
+def find_bundler() -> str:
+    exe = find_tool("clang-offload-bundler")
+    if not exe:
+        raise SlimError("clang-offload-bundler not found (ROCm LLVM toolchain)")
+    return exe
+
+
+def strip_debug(co: bytes, workdir: str) -> bytes:
+    """``co`` without its DWARF sections (``llvm-objcopy --strip-debug``), or ``co`` unchanged
+    when the tool is missing.  RCCL's gfx950 code object is 277 MB of which 50 MB load onto
+    the GPU; the rest is debug info the runtime would read for nothing (only a GPU debugger
+    uses it, and none runs on a gated node)."""
+    tool = find_tool("llvm-objcopy")
+    if not tool:
+        return co
+    src, dst = os.path.join(workdir, "full.co"), os.path.join(workdir, "stripped.co")
+    with open(src, "wb") as fh:
+        fh.write(co)
+    run = subprocess.run([tool, "--strip-debug", src, dst], capture_output=True, text=True, check=False)
+    try:
+        if run.returncode != 0:
+            raise SlimError(f"llvm-objcopy --strip-debug: {run.stderr.strip()}")
+        with open(dst, "rb") as fh:
+            out = fh.read()
+    finally:
+        for p in (src, dst):
+            if os.path.exists(p):
+                os.unlink(p)
+    if out[:4] != b"\x7fELF":
+        raise SlimError("stripped code object is not an ELF file")
+    return out
+
+
+def compressed_size(data: bytes) -> int:
+    """Bytes of the compressed bundle at the start of ``data`` (a section may be padded past
+    it).  Header: magic, u16 version, u16 method, then the total size as u32 (v2) or u64
+    (v3); v1 has none, so the whole buffer is the bundle."""
+    version, = struct.unpack_from("<H", data, 4)
+    if version == 2:
+        total, = struct.unpack_from("<I", data, 8)
+    elif version >= 3:
+        total, = struct.unpack_from("<Q", data, 8)
+    else:
+        return len(data)
+    if not 16 <= total <= len(data):
+        raise SlimError(f"compressed bundle header gives {total} bytes in a {len(data)} byte section")
+    return total
+
+
+def extract_code_object(section: bytes, arch: str, workdir: str) -> bytes:
+    """The ``arch`` code object out of a (compressed or plain) offload bundle."""
+    triple = device_triple(arch)
+    if section.startswith(BUNDLE_MAGIC):
+        for t, off, size in parse_bundle(section):
+            if t == triple:
+                return section[off:off + size]
+        raise SlimError(f"bundle has no {triple} entry")
+    if not section.startswith(COMPRESSED_MAGIC):
+        raise SlimError("unknown .hip_fatbin format")
+    src = os.path.join(workdir, "fatbin.bin")
+    dst = os.path.join(workdir, f"{arch}.co")
+    with open(src, "wb") as fh:
+        fh.write(section[:compressed_size(section)])
+    run = subprocess.run([find_bundler(), "--unbundle", "--type=o", f"--input={src}", f"--targets={triple}",
+                          f"--output={dst}"], capture_output=True, text=True, check=False)
+    if run.returncode != 0:
+        # (a target the bundle lacks fails here: "Can't find bundles for ...")
+        raise SlimError(f"clang-offload-bundler --unbundle {triple}: {run.stderr.strip()}")
+    with open(dst, "rb") as fh:
+        co = fh.read()
+    if co[:4] != b"\x7fELF":
+        raise SlimError(f"extracted {triple} code object is not an ELF file")
+    return co
+
+
+def source_key(lib: str) -> str:
+    st = os.stat(lib)
+    h = hashlib.sha256(f"{os.path.realpath(lib)}|{st.st_size}|{st.st_mtime_ns}".encode())
+    with open(lib, "rb") as fh:
+        h.update(fh.read(1 << 20))
+    return h.hexdigest()[:20]
+
+
+def entry_dir(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, strip: bool = True) -> str:
+    key = source_key(os.path.join(src_dir, "librccl.so"))
+    return os.path.join(root or cache_root(), f"{arch}-{key}" + ("" if strip else "-debug"))
+
+
+def cached(src_dir: str, arch: str = "gfx950", root: Optional[str] = None) -> str:
+    """The finished slim runtime directory for ``src_dir``, or ``""``."""
+    try:
+        d = entry_dir(src_dir, arch, root)
+    except OSError:
+        return ""
+    return d if os.path.exists(os.path.join(d, "slim.json")) else ""
+
+
+def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, strip: bool = True) -> Dict[str, object]:
+    """Build (or find) the slim runtime directory for the RCCL in ``src_dir``.
+
+    Returns the entry's metadata (``dir``, sizes, ``prepare_s``; ``cached`` True when it
+    already existed).  Raises :class:`SlimError` when the library cannot be slimmed."""
+    t0 = time.perf_counter()
+    lib = os.path.join(src_dir, "librccl.so")
+    if not os.path.exists(lib):
+        raise SlimError(f"{lib} missing")
+    out = entry_dir(src_dir, arch, root, strip)
+    meta_path = os.path.join(out, "slim.json")
+    if os.path.exists(meta_path):
+        with open(meta_path, "r", encoding="utf-8") as fh:
+            meta = json.load(fh)
+        meta["cached"] = True
+        return meta
+    real = os.path.realpath(lib)
+    offset, size = elf_section(real, ".hip_fatbin")
+    with open(real, "rb") as fh:
+        fh.seek(offset)
+        section = fh.read(size)
+    os.makedirs(os.path.dirname(out), exist_ok=True)
+    tmp = tempfile.mkdtemp(prefix=os.path.basename(out) + ".tmp-", dir=os.path.dirname(out))
+    os.chmod(tmp, 0o755)  # agents may run as another user than the one that prepared it
+    try:
+        co = extract_code_object(section, arch, tmp)
+        full_bytes = len(co)
+        if strip:
+            co = strip_debug(co, tmp)
+        bundle = make_bundle([(HOST_TRIPLE, b""), (device_triple(arch), co)])
+        if len(bundle) > size:
+            raise SlimError(f"{arch} code object ({len(co)} B) does not fit the {size} B .hip_fatbin section")
+        for name in ("fatbin.bin", f"{arch}.co"):
+            p = os.path.join(tmp, name)
+            if os.path.exists(p):
+                os.unlink(p)
+        dst = os.path.join(tmp, "librccl.so")
+        shutil.copyfile(real, dst)
+        with open(dst, "r+b") as fh:
+            fh.seek(offset)
+            fh.write(bundle)
+            fh.write(b"\0" * (size - len(bundle)))
+        os.chmod(dst, 0o755)
+        # the rest of the runtime: librccl resolves libamdhip64 & co. through $ORIGIN
+        for name in sorted(os.listdir(src_dir)):
+            if name.startswith("lib") and ".so" in name and name != "librccl.so":
+                os.symlink(os.path.realpath(os.path.join(src_dir, name)), os.path.join(tmp, name))
+        meta = {"dir": out, "source": real, "arch": arch, "source_fatbin_bytes": size,
+                "source_format": "compressed" if section.startswith(COMPRESSED_MAGIC) else "bundle",
+                "code_object_bytes": full_bytes, "loaded_code_object_bytes": len(co),
+                "debug_stripped": len(co) < full_bytes, "bundle_bytes": len(bundle),
+                "prepare_s": round(time.perf_counter() - t0, 3)}
+        with open(os.path.join(tmp, "slim.json"), "w", encoding="utf-8") as fh:
+            json.dump(meta, fh, indent=1)
+        try:
+            os.rename(tmp, out)
+        except OSError:
+            if not os.path.exists(meta_path):  # lost a race to a finished entry: use it
+                raise
+            shutil.rmtree(tmp, ignore_errors=True)
+        meta["cached"] = False
+        return meta
+    except BaseException:
+        shutil.rmtree(tmp, ignore_errors=True)
+        raise
+
+
+def main(argv=None) -> int:
+    import argparse
+
+    ap = argparse.ArgumentParser(description="Prepare the single-target (gfx950) RCCL runtime directory")
+    ap.add_argument("--source", default="", help="directory holding librccl.so (default: the PyTorch-ROCm lib/ "
+                                                 "the agent runs on, else /opt/rocm/lib)")
+    ap.add_argument("--arch", default="gfx950")
+    ap.add_argument("--root", default="", help="cache root (default: TK_RCCL_SLIM_DIR or the node default)")
+    args = ap.parse_args(argv)
+    from .native import SYSTEM_LIB_DIR, _torch_lib_dir
+
+    src = args.source or _torch_lib_dir() or (SYSTEM_LIB_DIR if os.path.exists(SYSTEM_LIB_DIR) else "")
+    if not src:
+        print(json.dumps({"error": "no RCCL source directory (install PyTorch-ROCm or pass --source)"}))
+        return 2
+    try:
+        meta = prepare(src, args.arch, args.root or None)
+    except SlimError as exc:
+        print(json.dumps({"error": str(exc)}))
+        return 1
+    print(json.dumps(meta))
+    return 0
+
+
+if __name__ == "__main__":
+    raise SystemExit(main())
