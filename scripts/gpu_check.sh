@@ -61,6 +61,14 @@ if [ "$MODE" = slim ]; then
   step bench_slim2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --report gpurun_out/bench_slim2.json
   step bench_noslim2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0 --rccl-slim off --report gpurun_out/bench_noslim2.json
 fi
+if [ "$MODE" = shslim ]; then
+  # shell form (SSH / Terraform nodes): e2e scripts with the rccl_slim step, then rccl-ready's
+  # process wall on /opt/rocm's full bundle vs the shell-made single-target copy, alternating
+  step shslim_tests 600 python -u -m pytest tests/test_gpu_e2e.py tests/test_gpu_probes.py -k "rendered_shell or terraform_mi355x or slim" -x -v -s --timeout 280 --timeout-method thread
+  python -c "from triton_kubernetes_amd.terraform.scripts import RCCL_SLIM_FN as f; print(f)" > /tmp/tk-slim-fn.sh
+  step shslim_prep 300 bash -c '. /tmp/tk-slim-fn.sh; tk_rccl_slim /tmp/tk-shslim /opt/rocm'
+  step shslim_cold_init 600 python scripts/rccl_cold_init.py system shslim system2 shslim2
+fi
 if [ "$MODE" = span ]; then
   step memtest_span 300 python scripts/memtest_span_chunks.py
 fi

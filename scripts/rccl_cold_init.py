@@ -55,6 +55,11 @@ VARIANTS = {
     "slim2": {"TK_HIP_RUNTIME": "@slim"},
     "torch_runtime2": {"TK_HIP_RUNTIME": "torch"},
     "slim_system": {"TK_HIP_RUNTIME": "@slim:/opt/rocm/lib"},
+    # the shell form (terraform/scripts.py tk_rccl_slim), prepared by scripts/gpu_check.sh shslim
+    "shslim": {"TK_HIP_RUNTIME": "/tmp/tk-shslim/rocm"},
+    "shslim2": {"TK_HIP_RUNTIME": "/tmp/tk-shslim/rocm"},
+    "system": {"TK_HIP_RUNTIME": "system"},
+    "system2": {"TK_HIP_RUNTIME": "system"},
     "torch_runtime_all_off": {"TK_HIP_RUNTIME": "torch", "RCCL_MSCCL_ENABLE": "0", "RCCL_MSCCLPP_ENABLE": "0",
                               "NCCL_NET_PLUGIN": "none"},
 }

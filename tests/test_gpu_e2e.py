@@ -6,6 +6,7 @@ runs the native GPU steps for real: amd_smi topology labels, quick burn-in
 """
 
 import json
+import sys
 import tempfile
 
 import pytest
@@ -90,7 +91,8 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
     cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1, "gpu_burnin": "quick",
            "rccl_env": {"NCCL_DEBUG": "WARN"}}
     plan = build_host_plan(cfg, "https://rancher.example", "regtok", "cafe", mi355x=True)
-    script = plan.render_shell().replace("/etc/", f"{etc}/").replace(TOOLS_DIR, LIB_DIR)
+    script = (plan.render_shell().replace("/etc/", f"{etc}/").replace(TOOLS_DIR, LIB_DIR)
+              .replace("/var/lib/triton-kubernetes", str(tmp_path / "var")))
     env = dict(os.environ, PATH=f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
     proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=300)
     assert proc.returncode == 0, proc.stderr[-3000:]
@@ -105,6 +107,19 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
     assert rccl["NCCL_DEBUG"] == "WARN"
     if int(labels.get("amd.com/rdma.count", "0")) > 0:  # the box's RDMA ports land in the env
         assert rccl["NCCL_IB_HCA"].startswith("=")
+    # the rccl_slim step's single-target copy of /opt/rocm's RCCL runs a verified gate
+    slim = tmp_path / "var" / "rccl-slim" / "rocm"
+    assert (slim / "slim.json").exists(), proc.stderr[-2000:]
+    code = ("import json; from triton_kubernetes_amd.ops import native, rccl\n"
+            "g = rccl.GateComm(rccl.unique_id(), 1, 0, [0], blocking=True)\n"
+            "r = g.sweep([1 << 20], iters=3, warmup=1, async_teardown=False)\n"
+            "print(json.dumps({'ok': r.ok, 'runtime': native.runtime_dir(),\n"
+            "                  'mapped': native.runtime_dir() + '/librccl.so' in open('/proc/self/maps').read()}))\n")
+    gate = subprocess.run(["timeout", "-k", "5", "120", sys.executable, "-c", code], capture_output=True, text=True,
+                          env=dict(os.environ, TK_HIP_RUNTIME=os.path.realpath(slim)))
+    assert gate.returncode == 0, gate.stderr[-2000:]
+    doc = json.loads([ln for ln in gate.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["ok"] and doc["mapped"], doc
     calls = log.read_text()
     assert "hostnamectl set-hostname gpu-1" in calls
     assert "--ca-checksum cafe --worker" in calls and "--label amd.com/gpu.product-name=MI355X" in calls
@@ -142,7 +157,8 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
               "rancher_node_role": "worker"}
     tools, etc = tmp_path / "tools", tmp_path / "etc"
     script = (_templatefile(tpl, values).replace("/opt/triton-kubernetes/bin", str(tools))
-              .replace("/opt/triton-kubernetes/src", CSRC).replace("/etc/", f"{etc}/"))
+              .replace("/opt/triton-kubernetes/src", CSRC).replace("/etc/", f"{etc}/")
+              .replace("/var/lib/triton-kubernetes", str(tmp_path / "var")))
     bindir = tmp_path / "bin"
     bindir.mkdir()
     log = tmp_path / "calls.log"
@@ -155,6 +171,17 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     assert proc.returncode == 0, proc.stderr[-3000:]
     for exe in ("amdgpu-topo-labeller", "gpu-burnin", "rccl-ready"):
         assert os.access(tools / exe, os.X_OK), exe  # built on the node from the shipped sources
+    # rccl-ready's DT_RPATH names the node's single-target RCCL first (ahead of the box's
+    # LD_LIBRARY_PATH=/opt/rocm/lib)
+    slim = tmp_path / "var" / "rccl-slim" / "rocm"
+    assert (slim / "slim.json").exists(), proc.stderr[-2000:]
+    ldd = subprocess.run(["ldd", str(tools / "rccl-ready")], capture_output=True, text=True)
+    dyn = subprocess.run(["readelf", "-d", str(tools / "rccl-ready")], capture_output=True, text=True).stdout
+    assert f"{slim}/librccl.so.1" in ldd.stdout, [ln for ln in dyn.splitlines() if "PATH" in ln]
+    ready = subprocess.run(["timeout", "-k", "5", "120", str(tools / "rccl-ready"), "--ngpus", "1", "--iters", "3"],
+                           capture_output=True, text=True)
+    assert ready.returncode == 0, ready.stderr[-2000:]
+    assert json.loads([ln for ln in ready.stdout.splitlines() if ln.startswith("{")][-1])["ok"], ready.stdout
     burn = json.loads((etc / "triton-kubernetes/gpu-burnin.json").read_text())
     assert burn["ok"], burn
     labels = (etc / "triton-kubernetes/gpu-labels").read_text()

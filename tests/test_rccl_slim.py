@@ -179,3 +179,61 @@ def test_cli_reports_errors_as_json(tmp_path):
     p = subprocess.run([sys.executable, "-m", "triton_kubernetes_amd.ops.rccl_slim", "--source", str(tmp_path),
                         "--root", str(tmp_path / "c")], capture_output=True, text=True, cwd=ROOT, timeout=120)
     assert p.returncode == 1 and "librccl.so missing" in json.loads(p.stdout)["error"]
+
+
+@pytest.mark.skipif(not rccl_slim.find_tool("clang-offload-bundler"), reason="no ROCm LLVM bundler")
+def test_shell_form_matches_the_python_form(tmp_path):
+    """terraform/scripts.py tk_rccl_slim (SSH / Terraform nodes) on a fake ROCm tree whose
+    librccl carries a compressed 2-target bundle: one aligned gfx950 entry, soname aliases
+    on the copy, the ``rocm`` link the node tools' RUNPATH names, cached on a re-run."""
+    from triton_kubernetes_amd.terraform.scripts import RCCL_SLIM_FN
+
+    lib = _lib()
+    _, _, orig = _section(lib)
+    co = next(orig[o:o + s] for t, o, s in rccl_slim.parse_bundle(orig) if t == GFX950)
+    for name, data in (("gfx950.co", co), ("other.co", co[::-1]), ("host", b"")):
+        (tmp_path / name).write_bytes(data)
+    targets = ",".join([rccl_slim.HOST_TRIPLE, rccl_slim.device_triple("gfx942"), GFX950])
+    subprocess.run([rccl_slim.find_bundler(), "--compress", "--type=o", f"--targets={targets}",
+                    f"--input={tmp_path / 'host'}", f"--input={tmp_path / 'other.co'}",
+                    f"--input={tmp_path / 'gfx950.co'}", f"--output={tmp_path / 'fat.bin'}"], check=True,
+                   capture_output=True)
+    fat = (tmp_path / "fat.bin").read_bytes()
+    rocm = tmp_path / "rocm"
+    (rocm / "lib" / "llvm").mkdir(parents=True)
+    os.symlink(os.path.dirname(rccl_slim.find_bundler()), rocm / "lib" / "llvm" / "bin")
+    real = rocm / "lib" / "librccl.so.1.0.1"
+    shutil.copyfile(lib, real)
+    os.symlink("librccl.so.1.0.1", rocm / "lib" / "librccl.so")
+    os.symlink("librccl.so.1.0.1", rocm / "lib" / "librccl.so.1")
+    (rocm / "lib" / "libamdhip64.so.7").write_bytes(b"x")
+    off, size, _ = _section(str(real))
+    with open(real, "r+b") as fh:  # a compressed bundle shorter than its section
+        fh.seek(off)
+        fh.write(fat + b"\0" * (size - len(fat)))
+    root = tmp_path / "cache"
+    script = RCCL_SLIM_FN + f"\ntk_rccl_slim {root} {rocm}\n"
+    p = subprocess.run(["bash", "-c", script], capture_output=True, text=True, timeout=120)
+    assert p.returncode == 0, p.stderr
+    out = p.stdout.strip()
+    assert os.path.realpath(root / "rocm") == os.path.realpath(out)
+    new_lib = os.path.join(out, "librccl.so")
+    assert os.path.getsize(new_lib) == os.path.getsize(real)
+    _, _, new = _section(new_lib)
+    entries = [(t, o, s) for t, o, s in rccl_slim.parse_bundle(new) if s]
+    assert [t for t, _, _ in entries] == [GFX950] and entries[0][1] % 4096 == 0
+    assert new[entries[0][1]:entries[0][1] + 4] == b"\x7fELF"
+    assert os.readlink(os.path.join(out, "librccl.so.1")) == "librccl.so"
+    assert os.path.realpath(os.path.join(out, "libamdhip64.so.7")) == os.path.realpath(rocm / "lib" / "libamdhip64.so.7")
+    assert json.loads(open(os.path.join(out, "slim.json"), encoding="utf-8").read())["form"] == "shell"
+    again = subprocess.run(["bash", "-c", script], capture_output=True, text=True, timeout=120)
+    assert again.returncode == 0 and again.stdout.strip() == out
+
+
+def test_python_form_links_every_librccl_alias_to_the_copy(tmp_path):
+    src = _fake_runtime(tmp_path, _lib())
+    os.symlink("librccl.so", os.path.join(src, "librccl.so.1"))
+    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False)
+    assert os.readlink(os.path.join(meta["dir"], "librccl.so.1")) == "librccl.so"
+    path = rccl_slim.link(str(tmp_path / "cache"), "rocm", str(meta["dir"]))
+    assert os.path.realpath(path) == os.path.realpath(meta["dir"])

@@ -276,6 +276,13 @@ class NodeAgent:
             discovered = sorted(env)
             env.update(step.params.get("env", {}))
             return {"file": self.write_file("/etc/rccl/rccl.env", render_env_file(env)), "discovered": discovered}
+        if a == "rccl_slim":
+            # an agent chose its runtime at start (its unit's ExecStartPre prepared the
+            # single-target RCCL): report which one the gate runs on
+            from ..ops import native
+
+            rt = native._runtime_dir or native.select_runtime()
+            return {"runtime": rt, "slim": os.path.exists(os.path.join(str(rt), "slim.json"))}
         if a == "rccl_local":
             if len(self.devices) < 2:
                 return {"skipped": "single GPU"}

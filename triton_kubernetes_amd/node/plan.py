@@ -34,6 +34,7 @@ from dataclasses import asdict, dataclass, field
 from typing import Any, Dict, List, Optional
 
 from ..parallel.rccl_env import render_env_file
+from ..terraform.scripts import RCCL_SLIM_FN, RCCL_SLIM_ROOT
 
 from ..versions import AGENT_IMAGE as DEFAULT_AGENT_IMAGE
 from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
@@ -216,6 +217,12 @@ sudo mkdir -p "$(dirname {RCCL_ENV_FILE})"
 {render_env_file(env).rstrip()}
 TK_RCCL_EOF
 }} | sudo tee {RCCL_ENV_FILE} >/dev/null""", {"env": env}, gpu=True))
+        # single-target RCCL for the node tools (ops/rccl_slim.py; cached, so a no-op after
+        # the first bring-up); never fatal: without it the tools load the full bundle
+        plan.steps.append(Step("rccl_slim", "rccl_slim", f"""
+{RCCL_SLIM_FN}
+sudo bash -c "$(declare -f tk_rccl_slim); tk_rccl_slim {RCCL_SLIM_ROOT} ${{ROCM_PATH:-/opt/rocm}}" >/dev/null \\
+  || echo 'rccl slim: skipped, the node tools load the full RCCL bundle' >&2""", {"root": RCCL_SLIM_ROOT}, gpu=True))
         if ngpu > 1:
             plan.steps.append(Step("rccl_local", "rccl_local",
                                    f"{TOOLS_DIR}/rccl-ready --ngpus {ngpu} --min-busbw "

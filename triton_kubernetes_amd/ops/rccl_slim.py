@@ -276,8 +276,12 @@ def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, stri
         os.chmod(dst, 0o755)
         # the rest of the runtime: librccl resolves libamdhip64 & co. through $ORIGIN
         for name in sorted(os.listdir(src_dir)):
-            if name.startswith("lib") and ".so" in name and name != "librccl.so":
-                os.symlink(os.path.realpath(os.path.join(src_dir, name)), os.path.join(tmp, name))
+            if not name.startswith("lib") or ".so" not in name or name == "librccl.so":
+                continue
+            # every soname / version alias of librccl is the copy (an executable's NEEDED
+            # librccl.so.1 resolves here through RUNPATH or LD_LIBRARY_PATH)
+            target = "librccl.so" if name.startswith("librccl.so") else os.path.realpath(os.path.join(src_dir, name))
+            os.symlink(target, os.path.join(tmp, name))
         meta = {"dir": out, "source": real, "arch": arch, "source_fatbin_bytes": size,
                 "source_format": "compressed" if section.startswith(COMPRESSED_MAGIC) else "bundle",
                 "code_object_bytes": full_bytes, "loaded_code_object_bytes": len(co),
@@ -298,6 +302,16 @@ def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, stri
         raise
 
 
+def link(root: str, name: str, target: str) -> str:
+    """Point ``root/name`` at ``target`` atomically (``rocm``: the entry the node tools'
+    RUNPATH names)."""
+    path = os.path.join(root, name)
+    tmp = f"{path}.tmp-{os.getpid()}"
+    os.symlink(target, tmp)
+    os.replace(tmp, path)
+    return path
+
+
 def main(argv=None) -> int:
     import argparse
 
@@ -306,20 +320,28 @@ def main(argv=None) -> int:
                                                  "the agent runs on, else /opt/rocm/lib)")
     ap.add_argument("--arch", default="gfx950")
     ap.add_argument("--root", default="", help="cache root (default: TK_RCCL_SLIM_DIR or the node default)")
+    ap.add_argument("--all", action="store_true",
+                    help="the PyTorch-ROCm RCCL (agents) and /opt/rocm's (node tools, linked as <root>/rocm)")
     args = ap.parse_args(argv)
     from .native import SYSTEM_LIB_DIR, _torch_lib_dir
 
-    src = args.source or _torch_lib_dir() or (SYSTEM_LIB_DIR if os.path.exists(SYSTEM_LIB_DIR) else "")
-    if not src:
+    if args.all:
+        sources = [d for d in (_torch_lib_dir(), SYSTEM_LIB_DIR) if d and os.path.exists(os.path.join(d, "librccl.so"))]
+    else:
+        sources = [args.source or _torch_lib_dir() or (SYSTEM_LIB_DIR if os.path.exists(SYSTEM_LIB_DIR) else "")]
+    if not any(sources):
         print(json.dumps({"error": "no RCCL source directory (install PyTorch-ROCm or pass --source)"}))
         return 2
-    try:
-        meta = prepare(src, args.arch, args.root or None)
-    except SlimError as exc:
-        print(json.dumps({"error": str(exc)}))
-        return 1
-    print(json.dumps(meta))
-    return 0
+    rc = 0
+    for src in sources:
+        try:
+            meta = prepare(src, args.arch, args.root or None)
+            if os.path.realpath(src) == os.path.realpath(SYSTEM_LIB_DIR):
+                meta["link"] = link(os.path.dirname(str(meta["dir"])), "rocm", str(meta["dir"]))
+        except (SlimError, OSError) as exc:
+            meta, rc = {"source": src, "error": str(exc)}, 1
+        print(json.dumps(meta))
+    return rc
 
 
 if __name__ == "__main__":

@@ -198,6 +198,66 @@ sudo docker run -d --privileged --restart=unless-stopped --net=host \
   --ca-checksum '${rancher_cluster_ca_checksum}' --${rancher_node_role}${extra_agent_args}
 """
 
+# Single-target RCCL, shell form of ops/rccl_slim.py (nodes delivered by SSH / Terraform):
+# a copy of librccl whose .hip_fatbin holds only the gfx950 code object, uncompressed and
+# without DWARF, so a cold process's first communicator init skips decompressing every GPU
+# target (~0.5 s instead of ~1.7 s on /opt/rocm 7.2).  rccl-ready's search path looks in
+# <root>/rocm first: a DT_RPATH (--disable-new-dtags), which ROCm hosts' usual
+# LD_LIBRARY_PATH=/opt/rocm/lib cannot override the way it overrides a RUNPATH.  Written without brace expansions: the same text is a Terraform
+# templatefile fragment and plain bash.
+RCCL_SLIM_ROOT = "/var/lib/triton-kubernetes/rccl-slim"
+RCCL_SLIM_FN = r"""tk_rccl_slim() { # <cache root> <rocm dir>: prints the slim runtime directory
+  local root=$1 rocm=$2 llvm real key out tmp sec off size nb f n
+  llvm=$rocm/lib/llvm/bin; [ -x $llvm/clang-offload-bundler ] || llvm=$rocm/llvm/bin
+  for f in clang-offload-bundler llvm-objcopy llvm-readelf; do
+    [ -x $llvm/$f ] || { echo "rccl slim: $f not found" >&2; return 1; }
+  done
+  real=$(readlink -f $rocm/lib/librccl.so) || return 1
+  key=$(stat -c '%s-%Y' "$real")-$(head -c 1048576 "$real" | sha256sum | cut -c1-16)
+  out=$root/gfx950-sh-$key
+  if [ ! -f $out/slim.json ]; then
+    mkdir -p $root && tmp=$(mktemp -d $root/.tmp-XXXXXX) && chmod 755 $tmp || return 1
+    sec=$($llvm/llvm-readelf -S -W "$real" | sed 's/^ *\[ *[0-9]*\] *//' | awk '$1 == ".hip_fatbin" {print $4, $5}')
+    if [ -z "$sec" ]; then rm -rf $tmp; echo "rccl slim: no .hip_fatbin in $real" >&2; return 1; fi
+    off=$((16#$(echo $sec | cut -d' ' -f1))); size=$((16#$(echo $sec | cut -d' ' -f2))); nb=$size
+    # a compressed bundle (CCOB) may be shorter than its section: its header holds the size
+    if [ "$(head -c $((off + 4)) "$real" | tail -c 4)" = CCOB ]; then
+      case $(od -An -t u2 -j $((off + 4)) -N 2 "$real" | tr -d ' ') in
+        2) nb=$(od -An -t u4 -j $((off + 8)) -N 4 "$real" | tr -d ' ') ;;
+        1) ;;
+        *) nb=$(od -An -t u8 -j $((off + 8)) -N 8 "$real" | tr -d ' ') ;;
+      esac
+    fi
+    dd if="$real" of=$tmp/fat.bin iflag=skip_bytes,count_bytes skip=$off count=$nb status=none
+    : > $tmp/host
+    if ! { $llvm/clang-offload-bundler --unbundle --type=o --input=$tmp/fat.bin \
+             --targets=hipv4-amdgcn-amd-amdhsa--gfx950 --output=$tmp/full.co &&
+           $llvm/llvm-objcopy --strip-debug $tmp/full.co $tmp/gfx950.co &&
+           env -u OFFLOAD_BUNDLER_COMPRESS $llvm/clang-offload-bundler --type=o --bundle-align=4096 \
+             --targets=host-x86_64-unknown-linux-gnu-,hipv4-amdgcn-amd-amdhsa--gfx950 \
+             --input=$tmp/host --input=$tmp/gfx950.co --output=$tmp/new.bin &&
+           [ $(stat -c %s $tmp/new.bin) -le $size ]; }; then
+      rm -rf $tmp; echo 'rccl slim: cannot build the gfx950 bundle' >&2; return 1
+    fi
+    nb=$(stat -c %s $tmp/new.bin)
+    cp "$real" $tmp/librccl.so
+    head -c $size /dev/zero | dd of=$tmp/librccl.so oflag=seek_bytes seek=$off conv=notrunc status=none
+    dd if=$tmp/new.bin of=$tmp/librccl.so oflag=seek_bytes seek=$off conv=notrunc status=none
+    rm -f $tmp/fat.bin $tmp/full.co $tmp/gfx950.co $tmp/host $tmp/new.bin
+    for f in $rocm/lib/lib*.so*; do
+      n=$(basename $f)
+      case $n in
+        librccl.so) ;;
+        librccl.so*) ln -s librccl.so $tmp/$n ;;
+        *) ln -s "$(readlink -f $f)" $tmp/$n ;;
+      esac
+    done
+    printf '{"source": "%s", "arch": "gfx950", "form": "shell", "bundle_bytes": %s}\n' "$real" $nb > $tmp/slim.json
+    mv -T $tmp $out 2>/dev/null || rm -rf $tmp
+  fi
+  ln -sfn $out $root/rocm.tmp && mv -T $root/rocm.tmp $root/rocm && echo $out
+}"""
+
 INSTALL_MI355X_NODE = r"""#!/bin/bash
 # MI355X worker bootstrap: ROCm preflight, topology labels (N1), burn-in,
 # RCCL environment + node-level RCCL gate (N2), then the Rancher agent with
@@ -220,7 +280,9 @@ build() { # name, compiler, flags...
 }
 build amdgpu-topo-labeller g++ -O2 -std=c++17 -DTK_TOPO_MAIN -DTK_TOPO_AMDSMI -I$ROCM/include $S/tk_topo.cpp -L$ROCM/lib -lamd_smi -Wl,-rpath,$ROCM/lib
 build gpu-burnin $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip
-build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl
+build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl -Wl,--disable-new-dtags,-rpath,""" + RCCL_SLIM_ROOT + r"""/rocm:$ROCM/lib
+""" + RCCL_SLIM_FN + r"""
+sudo bash -c "$(declare -f tk_rccl_slim); tk_rccl_slim """ + RCCL_SLIM_ROOT + r""" $ROCM" >/dev/null || echo 'rccl slim: skipped, the node tools load the full RCCL bundle' >&2
 $T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/dev/null
 $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
 sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels
