@@ -24,8 +24,10 @@ def test_missing_runtime_dir_fails_loudly(tmp_path):
     assert p.returncode == 0 and p.stdout.startswith("refused") and "libamdhip64.so missing" in p.stdout
 
 
-def test_auto_prefers_the_pytorch_rocm_runtime():
-    p = _run("from triton_kubernetes_amd.ops import native; print(native.select_runtime())", TK_HIP_RUNTIME="auto")
+def test_auto_prefers_the_pytorch_rocm_runtime(tmp_path):
+    # (an empty single-target cache: tests/test_rccl_slim.py covers the prepared case)
+    p = _run("from triton_kubernetes_amd.ops import native; print(native.select_runtime())", TK_HIP_RUNTIME="auto",
+             TK_RCCL_SLIM_DIR=str(tmp_path))
     assert p.returncode == 0 and p.stdout.strip().endswith("torch/lib"), p.stdout + p.stderr
 
 

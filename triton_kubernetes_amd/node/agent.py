@@ -489,6 +489,7 @@ class NodeAgent:
                     del self._gates[uid]
                     return uid, gate, meta
         return None
+
     def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10,
                   ndev: int = 1) -> Dict[str, Any]:
         """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
