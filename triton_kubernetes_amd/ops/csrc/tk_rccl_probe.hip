@@ -231,13 +231,23 @@ extern "C" void tkr_set_async_teardown(int on) { g_async_teardown = on; }
 static std::atomic<int> g_teardown_abort{0};
 extern "C" void tkr_set_teardown_abort(int on) { g_teardown_abort = on; }
 
+// split of the last teardown (ms): buffer frees, communicator destroy/abort
+static std::atomic<double> g_teardown_free_ms{0.0}, g_teardown_comm_ms{0.0};
+extern "C" double tkr_last_teardown_ms(int which) {
+  return which == 0 ? g_teardown_free_ms.load() : which == 1 ? g_teardown_comm_ms.load() : -1.0;
+}
+
 static void teardown(ncclComm_t comm, RankBufs b, int device) {
   const bool abort = g_teardown_abort.load() != 0;
   auto work = [comm, b, device, abort]() mutable {
     (void)hipSetDevice(device);
+    auto t0 = std::chrono::steady_clock::now();
     free_bufs(b);
+    g_teardown_free_ms.store(ms_since(t0));
+    t0 = std::chrono::steady_clock::now();
     if (abort) ncclCommAbort(comm);
     else ncclCommDestroy(comm);
+    g_teardown_comm_ms.store(ms_since(t0));
   };
   if (g_async_teardown) {
     g_teardowns.submit(work);
