@@ -102,27 +102,42 @@ def parse_bundle(data: bytes) -> List[Tuple[str, int, int]]:
     return out
 
 
-def make_bundle(entries: List[Tuple[str, bytes]]) -> bytes:
-    """Uncompressed offload bundle of ``entries`` (triple, payload), payloads 4 KiB aligned."""
-    header = len(BUNDLE_MAGIC) + 8 + sum(24 + len(t.encode()) for t, _ in entries)
-    offsets, pos = [], header
-    for _, payload in entries:
-        if payload:
+def bundle_layout(entries: List[Tuple[str, int]]) -> Tuple[bytes, List[int], int]:
+    """Header bytes, payload offsets and total size of an uncompressed offload bundle whose
+    entries are (triple, payload size); payloads 4 KiB aligned (as hipcc lays them out)."""
+    header_len = len(BUNDLE_MAGIC) + 8 + sum(24 + len(t.encode()) for t, _ in entries)
+    offsets, pos = [], header_len
+    for _, n in entries:
+        if n:
             pos = (pos + ALIGN - 1) // ALIGN * ALIGN
         offsets.append(pos)
-        pos += len(payload)
-    buf = bytearray(pos)
-    buf[:len(BUNDLE_MAGIC)] = BUNDLE_MAGIC
-    struct.pack_into("<Q", buf, len(BUNDLE_MAGIC), len(entries))
-    p = len(BUNDLE_MAGIC) + 8
-    for (triple, payload), off in zip(entries, offsets):
+        pos += n
+    head = bytearray(BUNDLE_MAGIC + struct.pack("<Q", len(entries)))
+    for (triple, n), off in zip(entries, offsets):
         t = triple.encode()
-        struct.pack_into("<QQQ", buf, p, off if payload else 0, len(payload), len(t))
-        p += 24
-        buf[p:p + len(t)] = t
-        p += len(t)
+        head += struct.pack("<QQQ", off if n else 0, n, len(t)) + t
+    return bytes(head), offsets, pos
+
+
+def make_bundle(entries: List[Tuple[str, bytes]]) -> bytes:
+    """Uncompressed offload bundle of ``entries`` (triple, payload) in memory."""
+    head, offsets, total = bundle_layout([(t, len(p)) for t, p in entries])
+    buf = bytearray(total)
+    buf[:len(head)] = head
+    for (_, payload), off in zip(entries, offsets):
         buf[off:off + len(payload)] = payload
     return bytes(buf)
+
+
+def _copy_range(src: str, offset: int, length: int, dst: str) -> None:
+    with open(src, "rb") as fi, open(dst, "wb") as fo:
+        fi.seek(offset)
+        while length > 0:
+            chunk = fi.read(min(length, 16 << 20))
+            if not chunk:
+                raise SlimError(f"{src}: short read")
+            fo.write(chunk)
+            length -= len(chunk)
 
 
 def find_tool(name: str) -> str:
@@ -141,72 +156,66 @@ def find_bundler() -> str:
     return exe
 
 
-def strip_debug(co: bytes, workdir: str) -> bytes:
-    """``co`` without its DWARF sections (``llvm-objcopy --strip-debug``), or ``co`` unchanged
-    when the tool is missing.  RCCL's gfx950 code object is 277 MB of which 50 MB load onto
-    the GPU; the rest is debug info the runtime would read for nothing (only a GPU debugger
-    uses it, and none runs on a gated node)."""
+def strip_debug(src: str, dst: str) -> bool:
+    """``llvm-objcopy --strip-debug src dst``; False (nothing written) when the tool is
+    missing.  RCCL's gfx950 code object is 277 MB of which 50 MB load onto the GPU; the rest
+    is DWARF the runtime would read for nothing (only a GPU debugger uses it, and none runs
+    on a gated node)."""
     tool = find_tool("llvm-objcopy")
     if not tool:
-        return co
-    src, dst = os.path.join(workdir, "full.co"), os.path.join(workdir, "stripped.co")
-    with open(src, "wb") as fh:
-        fh.write(co)
+        return False
     run = subprocess.run([tool, "--strip-debug", src, dst], capture_output=True, text=True, check=False)
-    try:
-        if run.returncode != 0:
-            raise SlimError(f"llvm-objcopy --strip-debug: {run.stderr.strip()}")
-        with open(dst, "rb") as fh:
-            out = fh.read()
-    finally:
-        for p in (src, dst):
-            if os.path.exists(p):
-                os.unlink(p)
-    if out[:4] != b"\x7fELF":
-        raise SlimError("stripped code object is not an ELF file")
-    return out
+    if run.returncode != 0:
+        raise SlimError(f"llvm-objcopy --strip-debug: {run.stderr.strip()}")
+    return True
 
 
-def compressed_size(data: bytes) -> int:
-    """Bytes of the compressed bundle at the start of ``data`` (a section may be padded past
-    it).  Header: magic, u16 version, u16 method, then the total size as u32 (v2) or u64
-    (v3); v1 has none, so the whole buffer is the bundle."""
-    version, = struct.unpack_from("<H", data, 4)
+def compressed_size(head: bytes, section_size: int) -> int:
+    """Bytes of the compressed bundle starting a ``section_size`` byte section (which may be
+    padded past it), from its header ``head``: magic, u16 version, u16 method, then the
+    total size as u32 (v2) or u64 (v3); v1 has none, so the whole section is the bundle."""
+    version, = struct.unpack_from("<H", head, 4)
     if version == 2:
-        total, = struct.unpack_from("<I", data, 8)
+        total, = struct.unpack_from("<I", head, 8)
     elif version >= 3:
-        total, = struct.unpack_from("<Q", data, 8)
+        total, = struct.unpack_from("<Q", head, 8)
     else:
-        return len(data)
-    if not 16 <= total <= len(data):
-        raise SlimError(f"compressed bundle header gives {total} bytes in a {len(data)} byte section")
+        return section_size
+    if not 16 <= total <= section_size:
+        raise SlimError(f"compressed bundle header gives {total} bytes in a {section_size} byte section")
     return total
 
 
-def extract_code_object(section: bytes, arch: str, workdir: str) -> bytes:
-    """The ``arch`` code object out of a (compressed or plain) offload bundle."""
+def extract_code_object(lib: str, offset: int, size: int, arch: str, dst: str) -> None:
+    """Write the ``arch`` code object of the (compressed or plain) offload bundle at
+    ``lib[offset:offset+size]`` to ``dst``, streaming (the sections run to 0.5 GB)."""
     triple = device_triple(arch)
-    if section.startswith(BUNDLE_MAGIC):
-        for t, off, size in parse_bundle(section):
+    with open(lib, "rb") as fh:
+        fh.seek(offset)
+        head = fh.read(min(size, 1 << 16))
+    if head.startswith(BUNDLE_MAGIC):
+        for t, off, n in parse_bundle(head):
             if t == triple:
-                return section[off:off + size]
-        raise SlimError(f"bundle has no {triple} entry")
-    if not section.startswith(COMPRESSED_MAGIC):
+                _copy_range(lib, offset + off, n, dst)
+                break
+        else:
+            raise SlimError(f"bundle has no {triple} entry")
+    elif head.startswith(COMPRESSED_MAGIC):
+        src = dst + ".fatbin"
+        _copy_range(lib, offset, compressed_size(head, size), src)
+        try:
+            run = subprocess.run([find_bundler(), "--unbundle", "--type=o", f"--input={src}", f"--targets={triple}",
+                                  f"--output={dst}"], capture_output=True, text=True, check=False)
+        finally:
+            os.unlink(src)
+        if run.returncode != 0:
+            # (a target the bundle lacks fails here: "Can't find bundles for ...")
+            raise SlimError(f"clang-offload-bundler --unbundle {triple}: {run.stderr.strip()}")
+    else:
         raise SlimError("unknown .hip_fatbin format")
-    src = os.path.join(workdir, "fatbin.bin")
-    dst = os.path.join(workdir, f"{arch}.co")
-    with open(src, "wb") as fh:
-        fh.write(section[:compressed_size(section)])
-    run = subprocess.run([find_bundler(), "--unbundle", "--type=o", f"--input={src}", f"--targets={triple}",
-                          f"--output={dst}"], capture_output=True, text=True, check=False)
-    if run.returncode != 0:
-        # (a target the bundle lacks fails here: "Can't find bundles for ...")
-        raise SlimError(f"clang-offload-bundler --unbundle {triple}: {run.stderr.strip()}")
     with open(dst, "rb") as fh:
-        co = fh.read()
-    if co[:4] != b"\x7fELF":
-        raise SlimError(f"extracted {triple} code object is not an ELF file")
-    return co
+        if fh.read(4) != b"\x7fELF":
+            raise SlimError(f"extracted {triple} code object is not an ELF file")
 
 
 def source_key(lib: str) -> str:
@@ -249,30 +258,29 @@ def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, stri
         return meta
     real = os.path.realpath(lib)
     offset, size = elf_section(real, ".hip_fatbin")
-    with open(real, "rb") as fh:
-        fh.seek(offset)
-        section = fh.read(size)
     os.makedirs(os.path.dirname(out), exist_ok=True)
     tmp = tempfile.mkdtemp(prefix=os.path.basename(out) + ".tmp-", dir=os.path.dirname(out))
     os.chmod(tmp, 0o755)  # agents may run as another user than the one that prepared it
     try:
-        co = extract_code_object(section, arch, tmp)
-        full_bytes = len(co)
-        if strip:
-            co = strip_debug(co, tmp)
-        bundle = make_bundle([(HOST_TRIPLE, b""), (device_triple(arch), co)])
-        if len(bundle) > size:
-            raise SlimError(f"{arch} code object ({len(co)} B) does not fit the {size} B .hip_fatbin section")
-        for name in ("fatbin.bin", f"{arch}.co"):
-            p = os.path.join(tmp, name)
-            if os.path.exists(p):
-                os.unlink(p)
+        full, stripped = os.path.join(tmp, "full.co"), os.path.join(tmp, "stripped.co")
+        extract_code_object(real, offset, size, arch, full)
+        full_bytes = os.path.getsize(full)
+        co_path = stripped if strip and strip_debug(full, stripped) else full
+        co_bytes = os.path.getsize(co_path)
+        head, offsets, total = bundle_layout([(HOST_TRIPLE, 0), (device_triple(arch), co_bytes)])
+        if total > size:
+            raise SlimError(f"{arch} code object ({co_bytes} B) does not fit the {size} B .hip_fatbin section")
         dst = os.path.join(tmp, "librccl.so")
         shutil.copyfile(real, dst)
-        with open(dst, "r+b") as fh:
-            fh.seek(offset)
-            fh.write(bundle)
-            fh.write(b"\0" * (size - len(bundle)))
+        with open(dst, "r+b") as fo, open(co_path, "rb") as fi:
+            fo.seek(offset)
+            fo.write(head)
+            fo.write(b"\0" * (offsets[1] - len(head)))
+            shutil.copyfileobj(fi, fo, 16 << 20)
+            fo.write(b"\0" * (size - total))
+        for p in (full, stripped):
+            if os.path.exists(p):
+                os.unlink(p)
         os.chmod(dst, 0o755)
         # the rest of the runtime: librccl resolves libamdhip64 & co. through $ORIGIN
         for name in sorted(os.listdir(src_dir)):
@@ -282,10 +290,12 @@ def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, stri
             # librccl.so.1 resolves here through RUNPATH or LD_LIBRARY_PATH)
             target = "librccl.so" if name.startswith("librccl.so") else os.path.realpath(os.path.join(src_dir, name))
             os.symlink(target, os.path.join(tmp, name))
-        meta = {"dir": out, "source": real, "arch": arch, "source_fatbin_bytes": size,
-                "source_format": "compressed" if section.startswith(COMPRESSED_MAGIC) else "bundle",
-                "code_object_bytes": full_bytes, "loaded_code_object_bytes": len(co),
-                "debug_stripped": len(co) < full_bytes, "bundle_bytes": len(bundle),
+        with open(real, "rb") as fh:
+            fh.seek(offset)
+            fmt = "compressed" if fh.read(4) == COMPRESSED_MAGIC else "bundle"
+        meta = {"dir": out, "source": real, "arch": arch, "source_fatbin_bytes": size, "source_format": fmt,
+                "code_object_bytes": full_bytes, "loaded_code_object_bytes": co_bytes,
+                "debug_stripped": co_bytes < full_bytes, "bundle_bytes": total,
                 "prepare_s": round(time.perf_counter() - t0, 3)}
         with open(os.path.join(tmp, "slim.json"), "w", encoding="utf-8") as fh:
             json.dump(meta, fh, indent=1)
