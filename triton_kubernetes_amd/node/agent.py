@@ -220,8 +220,6 @@ class NodeAgent:
 
     def _run_step(self, plan: BootstrapPlan, step: Step, ctx: Dict[str, Any]) -> Any:
         a = step.action
-        if a.startswith("gpu_") or a == "rccl_local":
-            self._devices_ready()
         if a in ("firewall", "runtime", "hostname", "registry_login"):
             if self.mode == "exec":
                 return self._exec_runtime(plan, step)
@@ -559,13 +557,15 @@ class NodeAgent:
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
         # the full burn-in's ~300 GB memtest memory is released off the bring-up path
         probe.set_async_free(True)
-        # HIP init, the burn-in arena and each GPU's first hardware queues (~0.2 s together
-        # on MI355X, profiles/round2/burnin_cold.md) on a thread of their own: the agent
-        # serves meanwhile, and GPU steps wait for it (_devices_ready)
-        self._warm_error: Optional[BaseException] = None
-        self._warm_thread = threading.Thread(target=self._warm_devices, name=f"tk-agent-{self.name}-warm",
-                                             daemon=True)
-        self._warm_thread.start()
+        # burn-in arena: resident for the agent's lifetime, released after an idle period
+        if os.environ.get("TK_PROBE_SCRATCH_CACHE", "1") != "0":
+            level = os.environ.get("TK_PROBE_SCRATCH_LEVEL", "quick")
+            t1 = time.perf_counter()
+            list(self._pool.map(lambda d: probe.prealloc_scratch(d, level), self.devices))
+            self.startup_ms["hip_init_arena"] = round((time.perf_counter() - t1) * 1e3, 1)
+            idle_s = float(os.environ.get("TK_PROBE_SCRATCH_IDLE_S", "300") or 0)
+            if idle_s > 0:
+                self._start_janitor(idle_s)
         quiet = float(os.environ.get("TK_TEARDOWN_QUIET_MS", "0") or 0)
         if quiet > 0:
             rccl.set_teardown_quiet_ms(quiet)
@@ -576,36 +576,6 @@ class NodeAgent:
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later
             pass
-
-    def _warm_devices(self) -> None:
-        from ..ops import probe
-
-        t1 = time.perf_counter()
-        try:
-            # burn-in arena: resident for the agent's lifetime, released after an idle period
-            if os.environ.get("TK_PROBE_SCRATCH_CACHE", "1") != "0":
-                level = os.environ.get("TK_PROBE_SCRATCH_LEVEL", "quick")
-                for d in self.devices:
-                    probe.prealloc_scratch(d, level)
-                self.startup_ms["hip_init_arena"] = round((time.perf_counter() - t1) * 1e3, 1)
-                idle_s = float(os.environ.get("TK_PROBE_SCRATCH_IDLE_S", "300") or 0)
-                if idle_s > 0:
-                    self._start_janitor(idle_s)
-            t2 = time.perf_counter()
-            for d in self.devices:
-                probe.warm_queues(d)
-            self.startup_ms["hw_queues"] = round((time.perf_counter() - t2) * 1e3, 1)
-        except BaseException as exc:  # noqa: BLE001 - reported by the first GPU step
-            self._warm_error = exc
-        self.startup_ms["device_warm"] = round((time.perf_counter() - t1) * 1e3, 1)
-
-    def _devices_ready(self) -> None:
-        """Wait for the start-up device warm-up (warm_native); its failure fails the step."""
-        t = getattr(self, "_warm_thread", None)
-        if t is not None:
-            t.join()
-            if self._warm_error is not None:
-                raise RuntimeError(f"GPU warm-up failed: {self._warm_error}")
 
     def _start_janitor(self, idle_s: float) -> None:
         """One long-lived thread frees the burn-in arena once no plan has run for ``idle_s``
@@ -732,9 +702,6 @@ class NodeAgent:
         return f"http://{h}:{p}"
 
     def stop(self) -> None:
-        warm = getattr(self, "_warm_thread", None)
-        if warm is not None:
-            warm.join()  # it may still be starting the janitor
         cv = getattr(self, "_idle_cv", None)
         if cv is not None:
             with cv:

@@ -318,34 +318,6 @@ extern "C" int tkp_prealloc_scratch(int dev, size_t stream_bytes, size_t memtest
   return 0;
 }
 
-// The device's first hardware queues.  A process's first stream on an MI355X costs ~150 ms
-// (HIP creates the HSA queue behind it, with its context-save area, on first use); later
-// streams of the same priority reuse the pooled queue in < 1 ms.  A node agent calls this
-// once per device at start, off its request path, so the bring-up's burn-in and RCCL
-// streams find their queues ready.  One launch per stream also loads this library's code
-// object onto the device.
-__global__ void k_touch(unsigned* p) {
-  if (p && blockIdx.x == 0 && threadIdx.x == 0) p[0] = 0u;
-}
-
-extern "C" int tkp_warm_queues(int dev) {
-  CHECK(hipSetDevice(dev));
-  hipStream_t low = nullptr, normal = nullptr;
-  CHECK(burnin_stream(&low));
-  hipError_t e = hipStreamCreateWithFlags(&normal, hipStreamNonBlocking);
-  if (e == hipSuccess) {
-    k_touch<<<1, 64, 0, low>>>(nullptr);
-    k_touch<<<1, 64, 0, normal>>>(nullptr);
-    e = hipGetLastError();
-  }
-  if (e == hipSuccess) e = hipStreamSynchronize(low);
-  if (e == hipSuccess) e = hipStreamSynchronize(normal);
-  if (normal) (void)hipStreamDestroy(normal);
-  (void)hipStreamDestroy(low);
-  CHECK(e);
-  return 0;
-}
-
 // Frees every cached buffer not in use; returns the bytes released.
 extern "C" long long tkp_release_scratch() {
   std::lock_guard<std::mutex> lk(g_scr_mu);

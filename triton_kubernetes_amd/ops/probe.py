@@ -68,7 +68,6 @@ def _lib():
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.tkp_set_scratch_cache.argtypes = [ctypes.c_int]
     lib.tkp_prealloc_scratch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t]
-    lib.tkp_warm_queues.argtypes = [ctypes.c_int]
     lib.tkp_release_scratch.restype = ctypes.c_longlong
     return lib
 
@@ -354,13 +353,6 @@ def prealloc_scratch(dev: int, level: str = "quick") -> int:
     rc = lib.tkp_prealloc_scratch(dev, ctypes.c_size_t(hbm_bytes), ctypes.c_size_t(mt_bytes))
     _check(rc, f"prealloc_scratch(dev {dev})")
     return 2 * hbm_bytes + mt_bytes
-
-
-def warm_queues(dev: int) -> None:
-    """Create (and pool) ``dev``'s first hardware queues, at the burn-in's priority and the
-    default one: a process's first stream on an MI355X costs ~150 ms, later ones < 1 ms
-    (``tkp_warm_queues``; ``profiles/round2/burnin_cold.md``)."""
-    _check(_lib().tkp_warm_queues(dev), f"warm_queues(dev {dev})")
 
 
 def set_scratch_cache(on: bool) -> None:
