@@ -237,3 +237,12 @@ def test_python_form_links_every_librccl_alias_to_the_copy(tmp_path):
     assert os.readlink(os.path.join(meta["dir"], "librccl.so.1")) == "librccl.so"
     path = rccl_slim.link(str(tmp_path / "cache"), "rocm", str(meta["dir"]))
     assert os.path.realpath(path) == os.path.realpath(meta["dir"])
+
+
+def test_gpu_cli_prepares_and_reports(tmp_path):
+    src = _fake_runtime(tmp_path, _lib())
+    p = subprocess.run([sys.executable, "-m", "triton_kubernetes_amd", "gpu", "rccl-slim", "--source", src, "--root",
+                        str(tmp_path / "c")], capture_output=True, text=True, cwd=ROOT, timeout=120)
+    assert p.returncode == 0, p.stderr
+    meta = json.loads(p.stdout.strip().splitlines()[-1])
+    assert os.path.exists(os.path.join(meta["dir"], "slim.json")) and meta["cached"] is False
