@@ -361,15 +361,18 @@ class NodeAgent:
 
     def _quiesce_gpus(self) -> None:
         """Let GPU work left over from an earlier request finish before the throughput
-        gates run: a previous gate's communicator teardown and a previous full burn-in's
-        background release of its memtest memory would otherwise overlap (and slow) the
-        short burn-in kernels.  A fresh agent has neither pending."""
+        gates run: a previous full burn-in's background release of its ~300 GB memtest
+        memory would otherwise overlap (and slow) the short burn-in kernels.  A previous
+        gate's communicator teardown is NOT waited for (TK_QUIESCE_TEARDOWNS=1 restores
+        that): its ~0.5 s is spent inside ncclCommDestroy, and burn-ins measured next to
+        it read the same as after it (profiles/round2/teardown_overlap.jsonl); a one-off
+        low reading is re-measured by the burn-in itself (ops/probe.py:REMEASURE)."""
         if self.burnin_override is not None or self.topology_override is not None or not self.devices:
             return
         from ..ops import probe
 
         probe.wait_frees()
-        if getattr(self, "_used_rccl", False):
+        if getattr(self, "_used_rccl", False) and os.environ.get("TK_QUIESCE_TEARDOWNS") == "1":
             from ..ops import rccl
 
             rccl.drain()
