@@ -1,7 +1,7 @@
 """Diagnostic: where the full burn-in's span memtest spends its time (allocation, fill +
 verify, release) for three chunk sizes (profiles/round2/memtest_span_chunks.jsonl)."""
-import json, sys, time
-sys.path.insert(0, "/root/repo")
+import json, os, sys, time
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
 from triton_kubernetes_amd.ops import probe
 for chunk in (16 << 30, 64 << 30, 8 << 30):
     t = time.perf_counter()

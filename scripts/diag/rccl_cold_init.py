@@ -14,7 +14,7 @@ Each variant runs in a fresh child process (``--child``) that times, in order:
   init2      second init + sweep (the warm cost, for reference)
 
 With ``TK_SAMPLE=1`` the child samples every thread during ``init1`` with
-scripts/native/tk_sampler.so and reports the top frames per shared object.
+scripts/diag/native/tk_sampler.so and reports the top frames per shared object.
 Parent mode runs every variant and writes one JSON line each to stdout.
 """
 
@@ -27,7 +27,7 @@ import sys
 import time
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-ROOT = os.path.dirname(HERE)
+ROOT = os.path.dirname(os.path.dirname(HERE))
 sys.path.insert(0, ROOT)
 
 VARIANTS = {

@@ -33,7 +33,7 @@ if [ "$MODE" = all ] || [ "$MODE" = prof ]; then
   step prof_bench 600 rocprofv3 --kernel-trace --stats --output-format csv -d "$GRAFT_REPO_ROOT/gpurun_out/prof_bench" -o "bench_%pid%" -- python3 "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --warm-steps 0
 fi
 if [ "$MODE" = coldinit ]; then
-  step rccl_cold_init 600 python scripts/rccl_cold_init.py ${COLD_VARIANTS:-}
+  step rccl_cold_init 600 python scripts/diag/rccl_cold_init.py ${COLD_VARIANTS:-}
 fi
 if [ "$MODE" = runtime ]; then
   # cold bench on the system ROCm runtime vs the PyTorch-ROCm bundled runtime, alternating
@@ -43,7 +43,7 @@ if [ "$MODE" = runtime ]; then
   TK_HIP_RUNTIME=torch step bench_torch2 300 python bench.py --steps 5 --warmup 1 --warm-steps 0
 fi
 if [ "$MODE" = kload ]; then
-  step rccl_kernel_load 300 python scripts/rccl_kernel_load.py
+  step rccl_kernel_load 300 python scripts/diag/rccl_kernel_load.py
 fi
 if [ "$MODE" = full ]; then
   step bench_full 600 python bench.py --steps 3 --warmup 1 --warm-steps 0 --burnin full
@@ -67,8 +67,8 @@ if [ "$MODE" = shslim ]; then
   step shslim_tests 600 python -u -m pytest tests/test_gpu_e2e.py tests/test_gpu_probes.py -k "rendered_shell or terraform_mi355x or slim" -x -v -s --timeout 280 --timeout-method thread
   python -c "from triton_kubernetes_amd.terraform.scripts import RCCL_SLIM_FN as f; print(f)" > /tmp/tk-slim-fn.sh
   step shslim_prep 300 bash -c '. /tmp/tk-slim-fn.sh; tk_rccl_slim /tmp/tk-shslim /opt/rocm'
-  step shslim_cold_init 600 python scripts/rccl_cold_init.py system shslim system2 shslim2
+  step shslim_cold_init 600 python scripts/diag/rccl_cold_init.py system shslim system2 shslim2
 fi
 if [ "$MODE" = span ]; then
-  step memtest_span 300 python scripts/memtest_span_chunks.py
+  step memtest_span 300 python scripts/diag/memtest_span_chunks.py
 fi
