@@ -6,7 +6,7 @@ cd "$GRAFT_REPO_ROOT"
 mkdir -p gpurun_out
 export PYTHONPATH="$GRAFT_REPO_ROOT"
 LOG="$GRAFT_REPO_ROOT/gpurun_out/check.log"
-: > $LOG
+echo "# mode=${1:-all} $(date -u +%FT%TZ)" >> $LOG  # appended: chained modes keep every step's line
 step() {  # step <name> <seconds> <cmd...>
   local name=$1 secs=$2; shift 2  # env assignments before "step" apply to the command
   local t0=$(date +%s%N)
