@@ -241,7 +241,10 @@ static int stream_grid(int dev, int blocks_per_cu) {
 // it has been idle, and at stop).  Without the cache every call allocates and frees.
 // ---------------------------------------------------------------------------
 namespace {
-constexpr int kScratchSlots = 3;  // 0/1: stream a/b, 2: memtest
+// 0/1: stream a/b.  The (quick) memtest runs in slot 0 too: a burn-in runs its steps one
+// after another on a device, so one GiB serves both, and the agent's start-up allocates
+// 2 GiB per GPU instead of 3 (a call finding slot 0 busy allocates its own buffer).
+constexpr int kScratchSlots = 2;
 struct ScratchSlot {
   void* p = nullptr;
   size_t bytes = 0;
@@ -309,7 +312,7 @@ extern "C" void tkp_set_scratch_cache(int on) {
 // Allocates (or keeps) the stream pair and memtest slots for these sizes on `dev`.
 extern "C" int tkp_prealloc_scratch(int dev, size_t stream_bytes, size_t memtest_bytes) {
   CHECK(hipSetDevice(dev));
-  const size_t sizes[kScratchSlots] = {stream_bytes, stream_bytes, memtest_bytes};
+  const size_t sizes[kScratchSlots] = {std::max(stream_bytes, memtest_bytes), stream_bytes};
   for (int slot = 0; slot < kScratchSlots; ++slot) {
     void* p = nullptr;
     CHECK(scratch_get(dev, slot, sizes[slot], &p));
@@ -697,7 +700,7 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   const size_t n = bytes / sizeof(uint4);
   uint4* p = nullptr;
   unsigned long long* err = nullptr;
-  CHECK(scratch_get(dev, 2, n * sizeof(uint4), reinterpret_cast<void**>(&p)));
+  CHECK(scratch_get(dev, 0, n * sizeof(uint4), reinterpret_cast<void**>(&p)));
   CHECK(hipMalloc(&err, sizeof(unsigned long long)));
   hipStream_t s;
   CHECK(burnin_stream(&s));
@@ -725,7 +728,7 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   TRACED(hipEventDestroy(t0));
   TRACED(hipEventDestroy(t1));
   TRACED(hipStreamDestroy(s));
-  scratch_put(dev, 2, p);
+  scratch_put(dev, 0, p);
   TRACED(hipFree(err));
   return 0;
 }

@@ -352,7 +352,7 @@ def prealloc_scratch(dev: int, level: str = "quick") -> int:
     lib.tkp_set_scratch_cache(1)
     rc = lib.tkp_prealloc_scratch(dev, ctypes.c_size_t(hbm_bytes), ctypes.c_size_t(mt_bytes))
     _check(rc, f"prealloc_scratch(dev {dev})")
-    return 2 * hbm_bytes + mt_bytes
+    return max(hbm_bytes, mt_bytes) + hbm_bytes  # the memtest shares the first stream buffer
 
 
 def set_scratch_cache(on: bool) -> None:
