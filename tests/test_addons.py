@@ -278,8 +278,41 @@ def test_injector_certificate_is_kept_across_applies():
         assert again == private and secret() == first
         _, fresh = ex._apply_addons(dict(cfg, rccl_env_injector="false"))
         assert fresh == {}
+        # a certificate started with the walk (_prefetch_tls) is the one applied
+        import concurrent.futures as cf
+
+        pre = cf.Future()
+        pre.set_result(serving_cert(addons.INJECTOR, "kube-system"))
+        _, used = ex._apply_addons(dict(cfg), None, pre)
+        assert used["injector_tls"]["cert_pem"] == pre.result().cert_pem
     finally:
         fake.stop()
+
+
+def test_injector_certificate_starts_with_the_walk(monkeypatch):
+    """Terraform creates the add-on module's tls_* resources when the graph walk starts: the
+    DirectExecutor starts the certificate before any module runs, except when the tfstate
+    keeps one, the module is unchanged, or the injector is off."""
+    from triton_kubernetes_amd.executor.direct import DirectExecutor, ModuleRun
+    from triton_kubernetes_amd.k8s import tls as tls_mod
+    from triton_kubernetes_amd.terraform.catalog import module_from_source
+
+    made = []
+    monkeypatch.setattr(tls_mod, "serving_cert", lambda svc, ns: made.append((svc, ns)) or "cert")
+    info = module_from_source(f"{MODULES_DIR}/{addons.MODULE}")
+    host = module_from_source(f"{MODULES_DIR}/bare-metal-mi355x-rancher-k8s-host")
+    runs = {k: ModuleRun(k, info, dict(c), set(), h) for k, c, h in [
+        ("fresh", {}, "h1"), ("kept", {}, "h2"), ("same", {}, "h3"), ("off", {"rccl_env_injector": "false"}, "h4")]}
+    runs["node"] = ModuleRun("node", host, {}, set(), "h5")
+    tf = {"module_state": {"kept": {"hash": "old", "status": "ok", "private": {"injector_tls": {"ca_pem": "x"}}},
+                           "same": {"hash": "h3", "status": "ok"}}}
+    pool = DirectExecutor._prefetch_tls(runs, tf)
+    assert pool is not None
+    pool.shutdown(wait=True)
+    assert runs["fresh"].tls is not None and runs["fresh"].tls.result() == "cert"
+    assert all(runs[k].tls is None for k in ("kept", "same", "off", "node"))
+    assert made == [(addons.INJECTOR, "kube-system")]
+    assert DirectExecutor._prefetch_tls({"node": runs["node"]}, tf) is None
 
 
 def test_webhook_xgmi_placement():

@@ -119,6 +119,8 @@ class ModuleRun:
     # module-private state kept in the tfstate between applies (what a Terraform module keeps
     # in its resources' state, e.g. the add-ons' tls_* certificate)
     prev_private: Optional[Dict[str, Any]] = None
+    # add-on modules: the injector certificate, started when the walk starts (_prefetch_tls)
+    tls: Optional[cf.Future] = None
 
 
 @dataclass
@@ -233,6 +235,7 @@ class DirectExecutor(Executor):
         from ..parallel.fanout import shared_pool
 
         pool = shared_pool(f"tk-direct-{self.parallelism}", self.parallelism)
+        tls_pool = self._prefetch_tls(runs, tf)
         with span("direct.apply", modules=len(runs)):
             while pending or futures:
                 for key in sorted(pending):
@@ -281,9 +284,43 @@ class DirectExecutor(Executor):
                 for fut in done:
                     run = runs[keys_done[fut]]
                     self._event("module_done", key=run.key, status=run.status, seconds=run.end - run.start)
+        if tls_pool is not None:
+            tls_pool.shutdown(wait=False)  # an unused certificate (add-on blocked) finishes on its own
         report.wall = time.time() - t0
         self.last_report = report
         return report
+
+    @staticmethod
+    def _prefetch_tls(runs: Dict[str, ModuleRun], tf: Dict[str, Any]) -> Optional[cf.ThreadPoolExecutor]:
+        """Start every add-on module's injector certificate when the walk starts.
+
+        Terraform creates the module's ``tls_private_key`` / ``tls_*_cert`` resources as soon
+        as the graph walk begins (they reference no other module), not after the hosts the
+        module's manifests wait for; the three ``openssl`` runs (~27 ms) overlap the node
+        bring-up the same way here.  Skipped for a module whose certificate is kept in the
+        tfstate or that will be skipped as unchanged; an add-on whose injector switch is an
+        interpolation makes its certificate itself (``_apply_addons``)."""
+        from ..k8s import addons
+
+        wanted = []
+        for key, run in runs.items():
+            if run.info.kind != "addon":
+                continue
+            prev = tf["module_state"].get(key) or {}
+            if (prev.get("private") or {}).get("injector_tls"):
+                continue
+            if prev.get("hash") == run.hash and prev.get("status") == "ok":
+                continue
+            if addons.enabled("env", addons.module_cfg_defaults(run.cfg)):
+                wanted.append(run)
+        if not wanted:
+            return None
+        from ..k8s.tls import serving_cert
+
+        pool = cf.ThreadPoolExecutor(max_workers=len(wanted), thread_name_prefix="tk-tls")
+        for run in wanted:
+            run.tls = pool.submit(serving_cert, addons.INJECTOR, "kube-system")
+        return pool
 
     def _apply_module(self, run: ModuleRun, outputs: Dict[str, Dict[str, str]],
                       manager_name: str) -> Tuple[Dict[str, str], Any]:
@@ -304,7 +341,7 @@ class DirectExecutor(Executor):
                         self._event("module_retry", key=run.key, attempt=attempt + 1, error=str(exc))
                         time.sleep(self.retry_backoff * (2 ** attempt))
             if kind == "addon":
-                outs, private = self._apply_addons(cfg, run.prev_private)
+                outs, private = self._apply_addons(cfg, run.prev_private, run.tls)
                 return outs, {"private": private}
         raise ExecutorError(f"unsupported module kind {kind}")
 
@@ -369,10 +406,12 @@ class DirectExecutor(Executor):
 
     # --- addons -------------------------------------------------------------------------------------------
     def _apply_addons(self, cfg: Dict[str, Any],
-                      private: Optional[Dict[str, Any]] = None) -> Tuple[Dict[str, str], Dict[str, Any]]:
+                      private: Optional[Dict[str, Any]] = None,
+                      tls: Optional[cf.Future] = None) -> Tuple[Dict[str, str], Dict[str, Any]]:
         """The Terraform add-on module's objects, rendered from its own template files
         (``k8s/addons.py``), with the injector's serving certificate made by ``openssl``
-        (the module uses the ``tls`` provider) -- while the nodes still bootstrap.  The
+        (the module uses the ``tls`` provider) -- while the nodes still bootstrap (``tls``:
+        the one :meth:`_prefetch_tls` started with the walk).  The
         certificate is kept in the module's private tfstate entry and reused by later
         applies, as Terraform keeps its ``tls_*`` resources, so re-applying never leaves
         running webhook pods with a certificate the new ``caBundle`` rejects."""
@@ -390,8 +429,8 @@ class DirectExecutor(Executor):
             if kept:
                 cert = ServingCert(**kept)
             else:
-                with span("addons.tls", cluster=cid):
-                    cert = serving_cert(addons.INJECTOR, "kube-system")
+                with span("addons.tls", cluster=cid, prefetched=tls is not None):
+                    cert = tls.result() if tls is not None else serving_cert(addons.INJECTOR, "kube-system")
         manifests = addons.rendered_addons(cfg, cert)
         with span("addons.wait_active", cluster=cid):
             wait_until(lambda: client.cluster_state(cid) == "active", self.cluster_wait, f"cluster {cid} active")
