@@ -21,6 +21,7 @@ import urllib.parse
 from typing import Dict, Optional, Tuple
 
 from ..utils.sshkeys import PrivateKey, rsa_pkcs1v15_verify
+from ..utils.httpserver import Server as HTTPServer
 from .triton import parse_signature_header
 
 
@@ -34,7 +35,7 @@ class FakeManta:
         self.mu = threading.Lock()
         self.requests = 0
         self.rejected = 0
-        self._server = http.server.ThreadingHTTPServer(("127.0.0.1", 0), self._handler())
+        self._server = HTTPServer(("127.0.0.1", 0), self._handler())
         self._server.daemon_threads = True
 
     def add_key(self, key: PrivateKey, key_id: Optional[str] = None) -> None:

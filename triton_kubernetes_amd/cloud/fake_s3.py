@@ -8,6 +8,7 @@ import urllib.parse
 from typing import Dict, Tuple
 from xml.sax.saxutils import escape
 
+from ..utils.httpserver import Server as HTTPServer
 from .aws import sigv4_headers
 
 
@@ -20,7 +21,7 @@ class FakeS3:
         self.buckets = set()
         self.rejected = 0
         self.mu = threading.Lock()
-        self._server = http.server.ThreadingHTTPServer(("127.0.0.1", 0), self._handler())
+        self._server = HTTPServer(("127.0.0.1", 0), self._handler())
         self._server.daemon_threads = True
 
     @property

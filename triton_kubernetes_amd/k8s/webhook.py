@@ -40,6 +40,12 @@ from http.server import BaseHTTPRequestHandler, ThreadingHTTPServer
 from typing import Any, Dict, List, Optional
 
 GPU_RESOURCE = "amd.com/gpu"
+
+
+class _Server(ThreadingHTTPServer):
+    """Listen backlog of the system's somaxconn, not socketserver's 5 (utils/httpserver.py;
+    this file stays standalone: the injector pod runs it by itself)."""
+    request_queue_size = 4096
 OPT_OUT = "amd.com/rccl-env-inject"
 MARK = "amd.com/rccl-env"
 VOLUME = "tk-node-rccl-env"
@@ -255,7 +261,7 @@ def make_server(port: int, env_dir: str, certfile: str = "", keyfile: str = "",
                 return self._reply(400, json.dumps({"error": str(exc)}).encode())
             return self._reply(200, json.dumps(out).encode())
 
-    srv = ThreadingHTTPServer((host, port), H)
+    srv = _Server((host, port), H)
     srv.daemon_threads = True
     if certfile:
         ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)

@@ -53,6 +53,7 @@ from ..cloud.http import HTTPClient
 from ..parallel.rccl_env import render_env_file, site_env_from_topology
 from ..rancher.fake import tunnel_params
 from ..utils import procstat
+from ..utils.httpserver import Server as HTTPServer
 from ..utils.trace import span
 from .labels import burnin_labels, labels_from_topology, link_labels
 from .plan import BootstrapPlan, Step
@@ -696,7 +697,7 @@ class NodeAgent:
                     return self._reply(500, {"error": f"{type(exc).__name__}: {exc}"})
                 return self._reply(404, {"error": "not found"})
 
-        self._server = http.server.ThreadingHTTPServer((host, port), H)
+        self._server = HTTPServer((host, port), H)
         self._server.daemon_threads = True
         # short poll: stop() (server.shutdown) returns within ~20 ms instead of the default 0.5 s
         threading.Thread(target=self._server.serve_forever, kwargs={"poll_interval": 0.02},

@@ -48,6 +48,7 @@ import uuid
 from typing import Any, Dict, List, Optional, Sequence, Set, Tuple
 
 from ..versions import DEFAULT_K8S_VERSION, K8S_VERSIONS, PASSWORD_MIN_LENGTH, RANCHER_VERSION, bootstrap_password
+from ..utils.httpserver import Server as HTTPServer
 
 FAKE_CACERTS = "-----BEGIN CERTIFICATE-----\nMIIFAKECERTIFICATEFORTESTS\n-----END CERTIFICATE-----"
 
@@ -90,7 +91,7 @@ class FakeRancher:
         # webhook service of a test really listens)
         self.service_endpoints: Dict[str, str] = {}
         self.async_registration_tokens = async_registration_tokens
-        self._server = http.server.ThreadingHTTPServer((host, port), self._handler())
+        self._server = HTTPServer((host, port), self._handler())
         self._server.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
 
