@@ -13,8 +13,10 @@ is the in-process fake the tests use:
    DirectExecutor; the three hosts are sim-mode node agents.
 4. `create cluster`, Triton provider, 8 nodes, Manta state backend. The Triton CloudAPI
    listings and Manta are fakes with HTTP-signature checks. The apply goes through the
-   TerraformExecutor with a fake `terraform` on PATH, which records the document and
-   writes canned outputs.
+   TerraformExecutor with a fake `terraform` 1.5.7 on PATH, which enforces what a real
+   1.5 does (no `manta` backend, sensitive root outputs, the modules' `required_version`)
+   and keeps a tfstate; the executor carries that tfstate to and from FakeManta under
+   the Manta lock. After the timed creates: `get manager`, then `destroy manager`.
 
 Each config runs `--runs` times after one warm-up run. The script prints one JSON line
 per config with the median and min wall-clock in ms.
@@ -153,6 +155,16 @@ def config4(runs):
                               cloud=cloud), backend)
 
     r4 = timed(cluster, runs)
+    # the tfstate round-tripped through Manta: one lineage, one serial per apply
+    st = json.loads(backend.read_tfstate("tmgr"))
+    assert st["serial"] == runs + 2 and len(st["resources"]) == 1 + 9 * (runs + 1), st["serial"]
+    out = io.StringIO()
+    ctx = ctx_of({"cluster_manager": "tmgr", "executor": "terraform"})
+    ctx.out = out
+    wf.get_manager(ctx, backend)
+    assert "rancher_url = fake-cluster-manager__rancher_url" in out.getvalue()
+    wf.delete_manager(ctx_of({"cluster_manager": "tmgr", "executor": "terraform"}), backend)
+    assert backend.states() == [] and not any("/triton-kubernetes/tmgr" in p for p in manta.objects)
     assert manta.rejected == 0
     manta.stop()
     shutil.rmtree(work, ignore_errors=True)

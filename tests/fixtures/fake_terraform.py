@@ -1,59 +1,239 @@
 #!/usr/bin/env python3
 """Fake ``terraform`` executable (the Terraform double SURVEY.md §4 calls for).
 
-Behaviour by sub-command:
+It models the parts of Terraform the CLI depends on — and the failures a real Terraform
+of version ``$FAKE_TF_VERSION`` (default 1.5.7) reports — independently of the CLI's own
+code (nothing here imports ``triton_kubernetes_amd``):
 
-* ``version``            prints ``Terraform v$FAKE_TF_VERSION`` (default 1.5.7)
-* ``init``               records, succeeds
-* ``apply``              records; writes a tfstate with fake values for every
-                         root ``output`` of ``main.tf.json`` to the local backend path
-* ``destroy``            records, succeeds
-* ``output``             ``-json`` (root outputs) or ``-module=<key>`` (0.11 style)
+* ``version``  prints ``Terraform v$FAKE_TF_VERSION``;
+* ``init``     rejects a backend type this version lacks (>= 1.3: ``manta``, ``etcd``,
+               ``etcdv3``, ``artifactory``, ``swift`` — "Unsupported backend type"), a
+               local module directory that does not exist, and a module whose
+               ``required_version`` this version fails ("Unsupported Terraform Core
+               version");
+* ``apply`` / ``destroy`` / ``output`` validate the configuration first: from 0.15 a
+               root output whose value is a module output the module declares
+               ``sensitive = true`` must be ``sensitive`` itself ("Output refers to
+               sensitive values");
+* ``apply``    reads the prior state from the backend (``local`` path, relative to the
+               work dir or absolute), adds one resource per module block, writes fake
+               values for every root output, bumps ``serial`` and keeps ``lineage``;
+* ``destroy``  removes the ``-target``-ed modules' resources (all without targets) and
+               the outputs that read them;
+* ``output``   ``-json`` (root outputs, with ``sensitive``) or ``-module=<key>`` (0.11).
 
-Every call appends ``{"argv": [...], "cwd": ..., "doc": <main.tf.json>}`` to
-``$FAKE_TF_LOG``.  ``FAKE_TF_FAIL=<subcommand>`` makes that sub-command exit 1.
+Every call appends ``{"argv", "cwd", "doc", "prior"}`` to ``$FAKE_TF_LOG`` (``prior``:
+serial/lineage/modules of the state the command started from).  ``FAKE_TF_FAIL=<cmd>``
+makes that sub-command fail *after* applying half of the new modules (apply) — a
+partial state is written, as Terraform does.
 """
 
 import json
 import os
+import re
 import sys
+import uuid
+
+REMOVED_BACKENDS_1_3 = {"artifactory", "etcd", "etcdv3", "manta", "swift"}
+
+
+def vtuple(text):
+    parts = [int(x) for x in re.findall(r"\d+", text)[:3]]
+    return tuple(parts + [0] * (3 - len(parts)))
+
+
+def satisfied(version, constraint):
+    for term in constraint.split(","):
+        term = term.strip()
+        if not term:
+            continue
+        m = re.match(r"^(=|!=|>=|<=|>|<|~>)?\s*v?([\d.]+)$", term)
+        if not m:
+            return False
+        op, want = m.group(1) or "=", vtuple(m.group(2))
+        ndots = m.group(2).count(".")
+        ok = {"=": version == want, "!=": version != want, ">": version > want, ">=": version >= want,
+              "<": version < want, "<=": version <= want}.get(op)
+        if op == "~>":
+            upper = (want[0] + 1, 0, 0) if ndots <= 1 else (want[0], want[1] + 1, 0)
+            ok = want <= version < upper
+        if not ok:
+            return False
+    return True
+
+
+def fail(msg):
+    sys.stderr.write(f"\nError: {msg}\n\n")
+    return 1
+
+
+def local_dir(source):
+    path = source.split("?", 1)[0]
+    return path if path.startswith(("/", "./", "../")) else None
+
+
+def module_outputs(mod_dir):
+    """{output: sensitive} declared in the module's .tf files (top-level output blocks)."""
+    outs = {}
+    for fn in sorted(os.listdir(mod_dir)):
+        if not fn.endswith(".tf"):
+            continue
+        text = open(os.path.join(mod_dir, fn), encoding="utf-8").read()
+        for m in re.finditer(r'^output\s+"([^"]+)"\s*\{(.*?)^\}', text, re.S | re.M):
+            outs[m.group(1)] = re.search(r"^\s*sensitive\s*=\s*true\s*$", m.group(2), re.M) is not None
+    return outs
+
+
+def required_versions(mod_dir):
+    out = []
+    for fn in sorted(os.listdir(mod_dir)):
+        if fn.endswith(".tf"):
+            out += re.findall(r'required_version\s*=\s*"([^"]*)"', open(os.path.join(mod_dir, fn)).read())
+    return out
+
+
+def validate(doc, version):
+    """Configuration errors Terraform reports before doing anything (plan/apply/output)."""
+    modules = doc.get("module") or {}
+    for key, mod in modules.items():
+        d = local_dir(str(mod.get("source", "")))
+        if d is not None and not os.path.isdir(d):
+            return f"Unreadable module directory\n\nUnable to evaluate directory symlink: lstat {d}: no such file"
+    if version >= (0, 15, 0):
+        for name, out in (doc.get("output") or {}).items():
+            m = re.fullmatch(r"\$\{module\.([^.}]+)\.([^.}]+)\}", str(out.get("value", "")))
+            if not m or m.group(1) not in modules:
+                continue
+            d = local_dir(str(modules[m.group(1)].get("source", "")))
+            if d is None:
+                continue
+            if module_outputs(d).get(m.group(2)) and out.get("sensitive") is not True:
+                return ("Output refers to sensitive values\n\n  on main.tf.json line 1:\n"
+                        f'  output "{name}"\n\nTo reduce the risk of accidentally exporting sensitive data that '
+                        "was intended to be only internal, Terraform requires that any root module output "
+                        "containing sensitive data be explicitly marked as sensitive, to confirm your intent.")
+    return None
+
+
+def state_path(doc):
+    backend = ((doc.get("terraform") or {}).get("backend") or {})
+    if "local" in backend:
+        return backend["local"].get("path") or "terraform.tfstate"
+    if backend:  # a remote backend this fake stands in for: keep it beside the log
+        kind = next(iter(backend))
+        base = os.environ.get("FAKE_TF_REMOTE") or os.path.join(os.getcwd(), ".remote")
+        ident = json.dumps(backend[kind], sort_keys=True)
+        return os.path.join(base, kind, re.sub(r"[^A-Za-z0-9]+", "_", ident)[:120] + ".tfstate")
+    return "terraform.tfstate"
+
+
+def load_state(path):
+    if os.path.exists(path):
+        with open(path, "r", encoding="utf-8") as fh:
+            return json.load(fh)
+    return {}
+
+
+def save_state(path, st):
+    d = os.path.dirname(path)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    with open(path, "w", encoding="utf-8") as fh:
+        json.dump(st, fh)
+
+
+def state_modules(st):
+    return sorted({r["module"][len("module."):] for r in st.get("resources", []) if r.get("module")})
 
 
 def main() -> int:
     argv = sys.argv[1:]
     cmd = argv[0] if argv else ""
+    version_s = os.environ.get("FAKE_TF_VERSION", "1.5.7")
+    version = vtuple(version_s)
     doc = {}
     if os.path.exists("main.tf.json"):
         with open("main.tf.json", "r", encoding="utf-8") as fh:
             doc = json.load(fh)
+    path = state_path(doc)
+    prior = load_state(path) if doc else {}
     log = os.environ.get("FAKE_TF_LOG")
     if log:
         with open(log, "a", encoding="utf-8") as fh:
-            fh.write(json.dumps({"argv": argv, "cwd": os.getcwd(), "doc": doc}) + "\n")
-    if os.environ.get("FAKE_TF_FAIL") == cmd:
-        sys.stderr.write(f"Error: fake failure of {cmd}\n")
-        return 1
-    version = os.environ.get("FAKE_TF_VERSION", "1.5.7")
-    backend_path = (((doc.get("terraform") or {}).get("backend") or {}).get("local") or {}).get("path")
+            fh.write(json.dumps({"argv": argv, "cwd": os.getcwd(), "doc": doc,
+                                 "prior": {"serial": prior.get("serial"), "lineage": prior.get("lineage"),
+                                           "modules": state_modules(prior)}}) + "\n")
     if cmd == "version":
-        print(f"Terraform v{version}\non linux_amd64")
+        print(f"Terraform v{version_s}\non linux_amd64")
         return 0
+
+    if cmd == "init":
+        backend = ((doc.get("terraform") or {}).get("backend") or {})
+        for kind in backend:
+            if version >= (1, 3, 0) and kind in REMOVED_BACKENDS_1_3:
+                return fail(f'Unsupported backend type\n\nThere is no backend type named "{kind}".')
+        for key, mod in (doc.get("module") or {}).items():
+            d = local_dir(str(mod.get("source", "")))
+            if d is None:
+                continue
+            if not os.path.isdir(d):
+                return fail(f"Unreadable module directory\n\nmodule.{key}: {d} does not exist")
+            for req in required_versions(d):
+                if not satisfied(version, req):
+                    return fail(f"Unsupported Terraform Core version\n\n  on {d}/versions.tf:\n"
+                                f"Module module.{key} requires Terraform {req}; this is {version_s}.")
+        if os.environ.get("FAKE_TF_FAIL") == "init":
+            return fail("fake failure of init")
+        print("Terraform has been successfully initialized!")
+        return 0
+
+    if cmd in ("apply", "destroy", "output", "plan"):
+        problem = validate(doc, version)
+        if problem:
+            return fail(problem)
+
     if cmd == "apply":
-        outputs = {}
+        st = prior or {"version": 4, "lineage": str(uuid.uuid4()), "serial": 0, "resources": [], "outputs": {}}
+        st["terraform_version"] = version_s
+        have = set(state_modules(st))
+        new = [k for k in (doc.get("module") or {}) if k not in have]
+        failing = os.environ.get("FAKE_TF_FAIL") == "apply"
+        if failing:
+            new = new[: len(new) // 2]
+        for key in new:
+            st["resources"].append({"module": f"module.{key}", "mode": "managed", "type": "terraform_data",
+                                    "name": "fake", "instances": [{"attributes": {"id": str(uuid.uuid4())}}]})
+        done = set(state_modules(st))
+        outs = {}
         for name, spec in (doc.get("output") or {}).items():
-            outputs[name] = {"value": f"fake-{name}", "type": "string"}
-        if backend_path:
-            os.makedirs(os.path.dirname(backend_path), exist_ok=True)
-            with open(backend_path, "w", encoding="utf-8") as fh:
-                json.dump({"version": 4, "outputs": outputs}, fh)
-        print("Apply complete!")
+            m = re.fullmatch(r"\$\{module\.([^.}]+)\.[^}]+\}", str(spec.get("value", "")))
+            if m and m.group(1) not in done:
+                continue
+            outs[name] = {"value": f"fake-{name}", "type": "string", "sensitive": bool(spec.get("sensitive"))}
+        st["outputs"] = outs
+        st["serial"] = int(st.get("serial", 0)) + 1
+        save_state(path, st)
+        if failing:
+            return fail("fake failure of apply")
+        print(f"Apply complete! Resources: {len(new)} added, 0 changed, 0 destroyed.")
         return 0
+
+    if cmd == "destroy":
+        if os.environ.get("FAKE_TF_FAIL") == "destroy":
+            return fail("fake failure of destroy")
+        targets = [a.split("=", 1)[1] for a in argv if a.startswith("-target=")]
+        st = prior or {"version": 4, "lineage": str(uuid.uuid4()), "serial": 0, "resources": [], "outputs": {}}
+        gone = {t[len("module."):] for t in targets} if targets else set(state_modules(st))
+        st["resources"] = [r for r in st.get("resources", []) if r.get("module", "")[len("module."):] not in gone]
+        st["outputs"] = {k: v for k, v in (st.get("outputs") or {}).items()
+                         if not any(k.startswith(g + "__") for g in gone)}
+        st["serial"] = int(st.get("serial", 0)) + 1
+        save_state(path, st)
+        print(f"Destroy complete! Resources: {len(gone)} destroyed.")
+        return 0
+
     if cmd == "output":
-        state = {}
-        if backend_path and os.path.exists(backend_path):
-            with open(backend_path, "r", encoding="utf-8") as fh:
-                state = json.load(fh)
-        outs = state.get("outputs", {})
+        outs = prior.get("outputs", {})
         module = next((a.split("=", 1)[1] for a in argv if a.startswith("-module=")), None)
         if module is None and "-module" in argv:
             module = argv[argv.index("-module") + 1]
@@ -63,7 +243,7 @@ def main() -> int:
             print(json.dumps(outs))
         else:
             for k in sorted(outs):
-                print(f"{k} = {outs[k]['value']}")
+                print(f"{k} = " + ("<sensitive>" if outs[k].get("sensitive") else str(outs[k]["value"])))
         return 0
     return 0
 

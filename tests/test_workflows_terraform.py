@@ -97,8 +97,9 @@ def test_create_manager_cluster_node_and_destroy(tmp_path, monkeypatch, backend)
 
 
 def test_terraform_011_flags_and_module_outputs(tmp_path, monkeypatch, backend):
+    """0.11 runs the reference's own (0.11-syntax) modules; the packaged ones need >= 1.4."""
     log = install_fake_terraform(tmp_path, monkeypatch, version="0.11.2")
-    new_manager(make_ctx(MGR), backend)
+    new_manager(make_ctx(dict(MGR, source_url="github.com/joyent/triton-kubernetes", source_ref="master")), backend)
     apply = [c for c in tf_calls(log) if c["argv"][0] == "apply"][0]
     assert "output" not in apply["doc"]  # 0.11: no rendered root outputs
     open(log, "w").close()

@@ -2,7 +2,11 @@
 
 Layout: ``/stor/triton-kubernetes/<name>/{main.tf.json,terraform.tfstate}``.
 Terraform backend block: ``terraform.backend.manta = {account, key_material,
-key_id, path="/triton-kubernetes/<name>"}``.
+key_id, path="/triton-kubernetes/<name>"}`` — kept in the persisted document for
+format compatibility.  Terraform removed the ``manta`` backend in v1.3, so for
+Terraform >= 1.3 the executor swaps it for a ``local`` backend in its work dir and
+carries ``terraform.tfstate`` to and from this backend itself, under :meth:`lock`
+(``executor/terraform.py``).
 
 Deliberate fixes:
 
@@ -25,6 +29,7 @@ Deliberate fixes:
 import contextlib
 import json
 import os
+import threading
 import time
 import uuid
 from typing import Any, Iterator, List, Optional, Tuple
@@ -62,6 +67,7 @@ class MantaBackend(Backend):
             signer = HTTPSignatureSigner.from_path(account, key_path, key_id or None)
             client = MantaClient(manta_url, signer)
         self.client = client
+        self._held = threading.local()  # per-thread {name: depth} of locks held
         self.client.put_directory(ROOT)
 
     def _p(self, name: str, filename: Optional[str] = None) -> str:
@@ -128,12 +134,26 @@ class MantaBackend(Backend):
 
     @contextlib.contextmanager
     def lock(self, name: str, timeout: float = 60.0, ttl: float = 900.0, poll: float = 0.25) -> Iterator[None]:
-        """Exclusive lock on the manager's documents.
+        """Exclusive lock on the manager's documents (``main.tf.json`` and, for Terraform
+        >= 1.3, the CLI-carried ``terraform.tfstate``).
 
         Acquire: create ``.lock`` with ``If-None-Match: *`` (fails if any holder exists);
         a holder past its expiry is replaced with ``If-Match: <its etag>``, so of several
-        writers racing for an expired lock exactly one wins.  Release: delete with
-        ``If-Match: <our etag>`` (a lock taken over after expiring is left alone)."""
+        writers racing for an expired lock exactly one wins.  While held, a heartbeat
+        re-PUTs the lock (``If-Match`` our etag) every ``ttl/3`` so a Terraform apply longer
+        than the TTL keeps it.  Release: delete with ``If-Match: <our etag>`` (a lock taken
+        over after expiring is left alone).  Re-entrant within one thread: the workflow
+        holds it around the executor, which takes it again around the tfstate round trip."""
+        held = getattr(self._held, "names", None)
+        if held is None:
+            held = self._held.names = {}
+        if name in held:
+            held[name] += 1
+            try:
+                yield
+            finally:
+                held[name] -= 1
+            return
         token = uuid.uuid4().hex
         path = self._p(name, ".lock")
         deadline = time.monotonic() + timeout
@@ -157,7 +177,27 @@ class MantaBackend(Backend):
             if time.monotonic() > deadline:
                 raise BackendError(f"timed out waiting for the Manta state lock of '{name}'")
             time.sleep(poll)
+        current = [etag]
+        stop = threading.Event()
+
+        def heartbeat() -> None:
+            while not stop.wait(ttl / 3.0):
+                refreshed = json.dumps({"token": token, "expires": time.time() + ttl}).encode()
+                try:
+                    new = self.client.put_object(path, refreshed, if_match=current[0])
+                except Exception:  # transient: the next beat retries before the TTL runs out
+                    continue
+                if new is None:  # taken over: we lost it (an expired lock); stop renewing
+                    return
+                current[0] = new
+
+        beat = threading.Thread(target=heartbeat, name=f"manta-lock-{name}", daemon=True)
+        beat.start()
+        held[name] = 1
         try:
             yield
         finally:
-            self.client.delete(path, if_match=etag or None)
+            del held[name]
+            stop.set()
+            beat.join()
+            self.client.delete(path, if_match=current[0] or None)

@@ -14,10 +14,26 @@ Terraform           destroy                 module outputs
 >= 0.15             ``destroy -auto-approve``  root outputs ``<key>__<name>`` (rendered)
 ==================  ======================  ==========================================
 
-For >= 0.12 the rendered document gains one root ``output`` per catalog output
-of every module, so ``get manager|cluster`` keep working; the persisted
-document is unchanged.  ``-parallelism`` is configurable (the reference leaves
-it at Terraform's default of 10, which bounds node fan-out).
+The document Terraform sees (:func:`render`) differs from the persisted one in three
+version-dependent ways; the persisted ``main.tf.json`` keeps the reference's layout:
+
+* for >= 0.12 one root ``output`` per catalog output of every module, so ``get
+  manager|cluster`` keep working.  An output the module declares ``sensitive`` (the
+  Rancher secret key, the registration token — ``terraform/generate.py`` is the single
+  source, read through ``catalog.sensitive_outputs``) is rendered ``sensitive = true``:
+  from 0.15 Terraform rejects the whole configuration otherwise ("Output refers to
+  sensitive values").  ``terraform output -json`` still prints the values;
+* a state backend Terraform no longer has (``manta`` was removed in 1.3, reference
+  ``backend/manta/backend.go:196-205``) is replaced by a ``local`` backend inside the
+  work dir, and the CLI carries ``terraform.tfstate`` itself: downloaded from the state
+  backend before every command, uploaded after ``apply``/``destroy`` (also after a
+  failed one: Terraform records what it created before failing), all under the
+  backend's lock (the Manta conditional-PUT lock, ``backend/manta.py``);
+* modules from a local directory (the packaged tree) are checked against their
+  ``required_version`` before ``init``, so a too-old Terraform gets one clear error.
+
+``-parallelism`` is configurable (the reference leaves it at Terraform's default of 10,
+which bounds node fan-out).
 """
 
 import contextlib
@@ -27,17 +43,20 @@ import os
 import re
 import shutil
 import tempfile
+from dataclasses import dataclass
 from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 from ..backend.base import Backend
 from ..errors import ExecutorError
 from ..state import State
-from ..terraform.catalog import outputs_for_source
+from ..terraform import constraints
+from ..terraform.catalog import local_module_dir, module_from_source, outputs_for_source, sensitive_outputs
 from ..utils.jsonenc import dumps_go
 from .base import Executor, outputs_from_tfstate
 from .shell import ShellOptions, capture_command, run_shell_command
 
 _VERSION_RE = re.compile(r"Terraform v(\d+)\.(\d+)\.(\d+)")
+WORKDIR_TFSTATE = "terraform.tfstate"
 
 
 def parse_version(text: str) -> Tuple[int, int, int]:
@@ -51,18 +70,64 @@ def parse_version(text: str) -> Tuple[int, int, int]:
     return int(m.group(1)), int(m.group(2)), int(m.group(3))
 
 
-def render_document(state: State, version: Tuple[int, int, int]) -> bytes:
-    """The document Terraform sees (see module docstring)."""
-    if version < (0, 12, 0):
-        return state.bytes()
-    doc = copy.deepcopy(state.doc)
-    outputs = doc.setdefault("output", {})
+@dataclass
+class Rendered:
+    body: bytes
+    # the state backend is one this Terraform lacks: the CLI carries terraform.tfstate
+    managed_state: bool = False
+    backend_kind: str = ""
+
+
+def _backend_kind(doc: Dict) -> str:
+    block = ((doc.get("terraform") or {}).get("backend") or {})
+    return next(iter(block), "") if isinstance(block, dict) else ""
+
+
+def check_module_versions(state: State, version: Tuple[int, int, int]) -> None:
+    """Raise when a module from a local directory declares a ``required_version`` that
+    ``version`` does not meet (Terraform's own init error, reported up front)."""
+    seen = set()
     for key, mod in state.modules().items():
-        for out in outputs_for_source(str(mod.get("source", ""))):
-            outputs[f"{key}__{out}"] = {"value": f"${{module.{key}.{out}}}"}
-    if not outputs:
-        doc.pop("output")
-    return dumps_go(doc)
+        local = local_module_dir(str(mod.get("source", "")))
+        if local is None or local in seen:
+            continue
+        seen.add(local)
+        bad = constraints.unsupported_by(version, local)
+        if bad is not None:
+            raise ExecutorError(
+                f"module.{key} ({os.path.basename(local.rstrip('/'))}) requires Terraform {bad}; "
+                f"found v{constraints.fmt(version)}. Install a newer Terraform, or point source_url/source_ref "
+                "at modules written for this version.")
+
+
+def render(state: State, version: Tuple[int, int, int]) -> Rendered:
+    """The document Terraform sees (see module docstring)."""
+    doc = state.doc
+    kind = _backend_kind(doc)
+    managed = bool(kind) and constraints.backend_removed(kind, version)
+    if version < (0, 12, 0) and not managed:
+        return Rendered(state.bytes(), False, kind)
+    doc = copy.deepcopy(doc)
+    if managed:
+        doc["terraform"]["backend"] = {"local": {"path": WORKDIR_TFSTATE}}
+    if version >= (0, 12, 0):
+        outputs = doc.setdefault("output", {})
+        for key, mod in state.modules().items():
+            source = str(mod.get("source", ""))
+            info = module_from_source(source)
+            secret = set(sensitive_outputs(info.name)) if info else set()
+            for out in outputs_for_source(source):
+                block = {"value": f"${{module.{key}.{out}}}"}
+                if out in secret:
+                    block["sensitive"] = True
+                outputs[f"{key}__{out}"] = block
+        if not outputs:
+            doc.pop("output")
+    return Rendered(dumps_go(doc), managed, kind)
+
+
+def render_document(state: State, version: Tuple[int, int, int]) -> bytes:
+    return render(state, version).body
 
 
 class TerraformExecutor(Executor):
@@ -99,21 +164,54 @@ class TerraformExecutor(Executor):
         run_shell_command(self._opts(workdir), self.binary, *args)
 
     @contextlib.contextmanager
-    def workdir(self, state: State) -> Iterator[str]:
+    def workdir(self, state: State, backend: Optional[Backend] = None, write_back: bool = False) -> Iterator[str]:
+        """Temp dir with the rendered document, initialised.  With CLI-managed state the
+        tfstate comes from ``backend`` first and (``write_back``) goes back to it after the
+        body, under ``backend.lock``."""
+        version = self.version()
+        check_module_versions(state, version)
+        rendered = render(state, version)
+        if rendered.managed_state and backend is None:
+            raise ExecutorError(f"the {rendered.backend_kind} state backend needs the CLI to carry terraform.tfstate")
         tmp = tempfile.mkdtemp(prefix="triton-kubernetes-")
         self.last_workdir = tmp
+        keep = self.keep_workdir
         try:
             with open(os.path.join(tmp, "main.tf.json"), "wb") as fh:
-                fh.write(render_document(state, self.version()))
-            self._run(tmp, "init", "-force-copy", "-input=false")
-            yield tmp
+                fh.write(rendered.body)
+            if not rendered.managed_state:
+                self._run(tmp, "init", "-force-copy", "-input=false")
+                yield tmp
+                return
+            lock = backend.lock(state.name) if write_back else contextlib.nullcontext()
+            with lock:
+                prior = backend.read_tfstate(state.name)
+                path = os.path.join(tmp, WORKDIR_TFSTATE)
+                if prior:
+                    with open(path, "wb") as fh:
+                        fh.write(prior)
+                try:
+                    self._run(tmp, "init", "-force-copy", "-input=false")
+                    yield tmp
+                finally:
+                    if write_back and os.path.exists(path):
+                        with open(path, "rb") as fh:
+                            after = fh.read()
+                        if after != (prior or b""):
+                            try:
+                                backend.write_tfstate(state.name, after)
+                            except Exception as exc:
+                                keep = True
+                                raise ExecutorError(
+                                    f"could not upload terraform.tfstate to the {rendered.backend_kind} backend "
+                                    f"({exc}); it is kept at {path}") from exc
         finally:
-            if not self.keep_workdir:
+            if not keep:
                 shutil.rmtree(tmp, ignore_errors=True)
 
     # --- Executor API ---------------------------------------------------------------------
     def apply(self, state: State, backend: Backend) -> None:
-        with self.workdir(state) as wd:
+        with self.workdir(state, backend, write_back=True) as wd:
             args: List[str] = ["apply", "-auto-approve", "-input=false"]
             if self.parallelism:
                 args.append(f"-parallelism={self.parallelism}")
@@ -123,14 +221,14 @@ class TerraformExecutor(Executor):
         return ["-auto-approve"] if self.version() >= (0, 15, 0) else ["-force"]
 
     def destroy(self, state: State, backend: Backend, targets: Sequence[str]) -> None:
-        with self.workdir(state) as wd:
+        with self.workdir(state, backend, write_back=True) as wd:
             args = ["destroy", *self.destroy_flags()]
             if self.parallelism:
                 args.append(f"-parallelism={self.parallelism}")
             self._run(wd, *args, *[f"-target={t}" for t in targets])
 
     def outputs(self, state: State, backend: Backend, module_key: str) -> Dict[str, str]:
-        with self.workdir(state) as wd:
+        with self.workdir(state, backend) as wd:
             if self.version() < (0, 12, 0):
                 res = capture_command(self.binary, "output", "-json", f"-module={module_key}",
                                       working_dir=wd, env=self.env or None)
@@ -144,7 +242,7 @@ class TerraformExecutor(Executor):
     def print_outputs(self, state: State, backend: Backend, module_key: str, out) -> None:
         if self.version() < (0, 12, 0):
             # exactly the reference's behaviour: stream `terraform output -module`
-            with self.workdir(state) as wd:
+            with self.workdir(state, backend) as wd:
                 self._run(wd, "output", "-module", module_key)
             return
         super().print_outputs(state, backend, module_key, out)

@@ -158,3 +158,22 @@ def module_from_source(source: str) -> Optional[ModuleInfo]:
 def outputs_for_source(source: str) -> Tuple[str, ...]:
     info = module_from_source(source)
     return info.outputs if info else ()
+
+
+_SENSITIVE: Optional[Dict[str, Dict[str, bool]]] = None
+
+
+def sensitive_outputs(module_name: str) -> Tuple[str, ...]:
+    """Outputs of a catalog module declared ``sensitive = true`` (from the generator's
+    module definitions, the single source of truth for the rendered ``outputs.tf``)."""
+    global _SENSITIVE
+    if _SENSITIVE is None:
+        from .generate import output_sensitivity  # lazy: generate imports this module
+
+        _SENSITIVE = output_sensitivity()
+    return tuple(n for n, s in _SENSITIVE.get(module_name, {}).items() if s)
+
+
+def output_is_sensitive(source: str, output: str) -> bool:
+    info = module_from_source(source)
+    return info is not None and output in sensitive_outputs(info.name)

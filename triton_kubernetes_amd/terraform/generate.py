@@ -17,7 +17,8 @@ Design (rewritten for Terraform >= 1.x and a current Rancher):
   (the GCP disk is now attached, Q15; vSphere CPU/memory are variables, Q15);
 * ``bare-metal-mi355x-rancher-k8s-host`` and ``rancher-k8s-mi355x-addons``.
 
-Every module pins ``required_version >= 1.3`` and its providers'
+Every module pins ``required_version >= 1.4`` (``terraform_data`` is a 1.4 resource)
+and its providers'
 sources (``joyent/triton``, ``hashicorp/aws|google|azurerm|vsphere|external``).
 """
 
@@ -1355,11 +1356,23 @@ resource "terraform_data" "apply_addons" {
     return mods
 
 
+# ``terraform_data`` (every remote-exec / local-exec step of the modules) is new in 1.4
+REQUIRED_VERSION = ">= 1.4"
+MIN_TERRAFORM = (1, 4, 0)
+
+
+def output_sensitivity() -> Dict[str, Dict[str, bool]]:
+    """``{module: {output: sensitive}}`` straight from the module definitions — the one
+    source the catalog and the executor's root-output rendering read (Terraform >= 0.15
+    rejects a root output over a sensitive module output unless it is marked too)."""
+    return {m.name: {name: bool(sens) for name, _, sens in m.outputs} for m in modules()}
+
+
 def render_versions(mod: Module) -> str:
     req = [PROVIDERS[p][0] for p in mod.providers]
     body = "\n    ".join(req)
     block = f"  required_providers {{\n    {body}\n  }}\n" if req else ""
-    return f"terraform {{\n  required_version = \">= 1.3\"\n{block}}}\n"
+    return f"terraform {{\n  required_version = \"{REQUIRED_VERSION}\"\n{block}}}\n"
 
 
 def render_main(mod: Module) -> str:

@@ -1,5 +1,5 @@
 terraform {
-  required_version = ">= 1.3"
+  required_version = ">= 1.4"
   required_providers {
     aws = {
       source  = "hashicorp/aws"

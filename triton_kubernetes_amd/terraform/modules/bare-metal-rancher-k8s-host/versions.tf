@@ -1,3 +1,3 @@
 terraform {
-  required_version = ">= 1.3"
+  required_version = ">= 1.4"
 }

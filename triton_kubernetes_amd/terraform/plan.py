@@ -971,3 +971,55 @@ def plan_module(module_dir: str, inputs: Dict[str, Any], check_files: bool = Tru
 
 
 __all__ = ["PlanError", "PlanReport", "UNKNOWN", "plan_module", "evaluate", "FUNCTIONS"]
+
+
+def plan_root(doc: Dict[str, Any], version: Tuple[int, int, int]) -> List[str]:
+    """Checks on the *root* document (``main.tf.json`` as the executor renders it) that
+    depend on the Terraform version running it — the failures a real Terraform reports
+    before touching any resource:
+
+    * the backend type must exist in that version (``manta`` and four others were
+      removed in 1.3: "Unsupported backend type");
+    * every local module's ``required_version`` must accept the version;
+    * from 0.15, a root output whose value is a module output declared ``sensitive``
+      must be marked ``sensitive = true`` ("Output refers to sensitive values").
+
+    Module outputs' sensitivity is read from the module's own ``outputs.tf`` with the HCL
+    parser, not from the generator, so this check and the executor's rendering (which
+    reads the generator) are independent."""
+    from . import constraints
+    from .catalog import local_module_dir
+
+    errors: List[str] = []
+    backend = (doc.get("terraform") or {}).get("backend") or {}
+    for kind in backend:
+        if constraints.backend_removed(kind, version):
+            errors.append(f"terraform.backend.{kind}: there is no backend type named {kind!r} in Terraform "
+                          f"{constraints.fmt(version)} (removed in "
+                          f"{constraints.fmt(constraints.REMOVED_BACKENDS[kind])})")
+    modules = doc.get("module") or {}
+    sensitive: Dict[str, Dict[str, bool]] = {}
+    for key, mod in modules.items():
+        local = local_module_dir(str(mod.get("source", "")))
+        if local is None:
+            continue
+        bad = constraints.unsupported_by(version, local)
+        if bad is not None:
+            errors.append(f"module.{key}: required_version {bad!r} is not met by Terraform {constraints.fmt(version)}")
+        outs: Dict[str, bool] = {}
+        for body in hcl.check_module(local).files.values():
+            for b in body.blocks:
+                if b.type == "output" and b.labels:
+                    attr = b.body.attr("sensitive")
+                    outs[b.labels[0]] = attr is not None and evaluate(attr.expr, _Scope.__new__(_Scope)) is True
+        sensitive[key] = outs
+    if tuple(version) >= constraints.SENSITIVE_ROOT_OUTPUTS_FROM:
+        for name, out in (doc.get("output") or {}).items():
+            m = re.fullmatch(r"\$\{module\.([^.}]+)\.([^.}]+)\}", str((out or {}).get("value", "")))
+            if m and sensitive.get(m.group(1), {}).get(m.group(2)) and (out or {}).get("sensitive") is not True:
+                errors.append(f"output.{name}: refers to the sensitive output module.{m.group(1)}.{m.group(2)} "
+                              "and must be marked sensitive = true")
+    return errors
+
+
+__all__.append("plan_root")
