@@ -70,9 +70,10 @@ def parse_args():
     ap.add_argument("--agents", default="proc", choices=["proc", "inproc"],
                     help="proc: every agent in its own fresh process (the headline); inproc: agents as "
                          "objects in this process (the graft smoke: native libraries load here)")
-    ap.add_argument("--rccl-slim", default="on", choices=["on", "off"],
-                    help="on: node install step (before the timed region) prepares the single-target gfx950 "
-                         "RCCL the agents load (ops/rccl_slim.py; the agent unit's ExecStartPre on a real node)")
+    ap.add_argument("--rccl-slim", default="off", choices=["on", "off"],
+                    help="on: the node's opt-in single-target gfx950 RCCL copy (ops/rccl_slim.py), prepared and "
+                         "verified before the timed region, loaded by the agents (TK_HIP_RUNTIME=slim). Default "
+                         "off: the agents load /opt/rocm's HIP runtime and RCCL, the product default")
     ap.add_argument("--sim-gpu", action="store_true",
                     help="CPU dry run: synthetic topology, no burn-in kernels, no RCCL (never a valid measurement)")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
@@ -217,20 +218,17 @@ def main() -> int:
     from triton_kubernetes_amd.utils.trace import TRACER, span
 
     slim_meta = None
-    if args.rccl_slim == "off" or args.sim_gpu:
-        os.environ["TK_RCCL_SLIM"] = "0"  # inherited by the agent processes
-    elif local_rank == 0:
-        # node install (one-time per RCCL build, cached): what the agent's systemd unit runs
-        # as ExecStartPre on a real node.  Outside the timed region, like the OS image.
+    os.environ.setdefault("TK_HIP_RUNTIME", "system")  # inherited by the agent processes
+    if args.rccl_slim == "on" and not args.sim_gpu:
+        # the node's opt-in (one-time per RCCL build, cached, verified by a one-rank
+        # all-reduce before first use); outside the timed region, like the OS image
         from triton_kubernetes_amd.ops import native, rccl_slim
 
-        src = native._torch_lib_dir()
-        if src:
-            try:
-                slim_meta = rccl_slim.prepare(src)
-            except (rccl_slim.SlimError, OSError) as exc:
-                print(f"warning: single-target RCCL not prepared ({exc}); agents load the full bundle",
-                      file=sys.stderr)
+        if local_rank == 0:
+            slim_meta = rccl_slim.prepare(native.SYSTEM_LIB_DIR)
+        if distributed:
+            dist.barrier()
+        os.environ["TK_HIP_RUNTIME"] = "slim"
 
     token = os.environ.get("TK_BENCH_TOKEN", "bench-token-0123456789")
     work = tempfile.mkdtemp(prefix=f"tk-bench-r{rank}-")
@@ -420,8 +418,8 @@ def main() -> int:
                            f"native topology + RDMA labels, per-GPU HBM/MFMA/memtest burn-in level={args.burnin}, "
                            f"cluster RCCL all-reduce gate {'off' if args.no_rccl_gate else 'on'} "
                            f"(one communicator over all {n_gpus} GPUs)"
-                           + ("; node install before the timed region: single-target gfx950 RCCL device code "
-                              "(ops/rccl_slim.py)" if slim_meta else "")),
+                           + ("; opt-in node install before the timed region: verified single-target gfx950 "
+                              "RCCL copy (ops/rccl_slim.py)" if slim_meta else "")),
             "config": {
                 "model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology labels",
                 "workers": workers, "gpus_per_worker": gpus_per_worker, "visible_gpus": visible,
@@ -436,8 +434,9 @@ def main() -> int:
                 # HIP runtime + RCCL the GPU agents ran on (ops/native.py:select_runtime)
                 "agent_hip_runtime": sorted(runtimes),
                 # node install step outside the timed region (ops/rccl_slim.py)
-                "rccl_slim": ({k: slim_meta[k] for k in ("prepare_s", "cached", "source_fatbin_bytes",
-                                                          "loaded_code_object_bytes")} if slim_meta else None),
+                "rccl_slim": ({k: slim_meta.get(k) for k in ("prepare_s", "cached", "source_fatbin_bytes",
+                                                              "loaded_code_object_bytes", "verified")}
+                              if slim_meta else None),
             },
             "create_to_ready_s": ready,
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),

@@ -8,6 +8,7 @@ RCCL's bootstrap root), then waits until processes holding the remaining
 waits (an id that does not start with ``fa4e`` came from a simulated agent: no rendezvous).
 Every process then prints one result line.  ``FAKE_RCCL_FAIL_BASE=<rank base>``
 makes that process fail at once; ``FAKE_RCCL_NO_UID=1`` makes the root never print its id.
+``FAKE_RCCL_PIDDIR=<dir>``: each process records its pid there.
 The environment the gate script sourced is echoed back (``env``) so tests can check it.
 """
 
@@ -32,6 +33,10 @@ def main() -> int:
     ap.add_argument("--timeout-s", type=float)
     ap.add_argument("--min-busbw", type=float)
     a = ap.parse_args()
+    piddir = os.environ.get("FAKE_RCCL_PIDDIR")
+    if piddir:  # tests check that an aborted gate leaves no rank process behind
+        with open(os.path.join(piddir, f"{os.getpid()}.pid"), "w") as fh:
+            fh.write(str(a.rank_base))
     if os.environ.get("FAKE_RCCL_FAIL_BASE") == str(a.rank_base):
         print('{"error":"injected failure"}', file=sys.stderr)
         return 2

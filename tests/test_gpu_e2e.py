@@ -67,18 +67,25 @@ def _stub(bindir, name, body):
     p.chmod(0o755)
 
 
-def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
+@pytest.mark.parametrize("rccl_slim", ["off", "on"])
+def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim):
     """The SSH path's rendered bash bootstrap, run for real on the box: the native tools
-    (gpu-burnin, amdgpu-topo-labeller incl. --rccl-env) from ops/lib, /etc relocated under
-    tmp_path, and only sudo/docker/systemctl/hostnamectl/usermod/lsmod stubbed (no root
-    and no container runtime on the box)."""
+    (gpu-burnin, amdgpu-topo-labeller incl. --rccl-env, rccl-ready) copied from ops/lib,
+    /etc relocated under tmp_path, and only sudo/docker/systemctl/hostnamectl/usermod/lsmod
+    stubbed (no root and no container runtime on the box).  ``rccl_slim=on``: the opt-in
+    step verifies the single-target copy on the GPU before installing rccl-ready-slim."""
     import os
+    import shutil
     import subprocess
 
     from triton_kubernetes_amd.node.plan import TOOLS_DIR, build_host_plan, parse_step_markers
-    from triton_kubernetes_amd.ops.native import LIB_DIR
+    from triton_kubernetes_amd.ops.native import LIB_DIR, SYSTEM_LIB_DIR
     from triton_kubernetes_amd.parallel.rccl_env import parse_env_file
 
+    tools = tmp_path / "tools"
+    tools.mkdir()
+    for exe in ("amdgpu-topo-labeller", "gpu-burnin", "rccl-ready"):
+        shutil.copy2(os.path.join(LIB_DIR, exe), tools / exe)
     bindir = tmp_path / "bin"
     bindir.mkdir()
     log = tmp_path / "calls.log"
@@ -89,9 +96,9 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
     etc = tmp_path / "etc"
     (etc / "docker").mkdir(parents=True)
     cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1, "gpu_burnin": "quick",
-           "rccl_env": {"NCCL_DEBUG": "WARN"}}
+           "rccl_env": {"NCCL_DEBUG": "WARN"}, "rccl_slim": rccl_slim}
     plan = build_host_plan(cfg, "https://rancher.example", "regtok", "cafe", mi355x=True)
-    script = (plan.render_shell().replace("/etc/", f"{etc}/").replace(TOOLS_DIR, LIB_DIR)
+    script = (plan.render_shell().replace("/etc/", f"{etc}/").replace(TOOLS_DIR, str(tools))
               .replace("/var/lib/triton-kubernetes", str(tmp_path / "var")))
     env = dict(os.environ, PATH=f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
     proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=300)
@@ -107,19 +114,19 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path):
     assert rccl["NCCL_DEBUG"] == "WARN"
     if int(labels.get("amd.com/rdma.count", "0")) > 0:  # the box's RDMA ports land in the env
         assert rccl["NCCL_IB_HCA"].startswith("=")
-    # the rccl_slim step's single-target copy of /opt/rocm's RCCL runs a verified gate
-    slim = tmp_path / "var" / "rccl-slim" / "rocm"
-    assert (slim / "slim.json").exists(), proc.stderr[-2000:]
-    code = ("import json; from triton_kubernetes_amd.ops import native, rccl\n"
-            "g = rccl.GateComm(rccl.unique_id(), 1, 0, [0], blocking=True)\n"
-            "r = g.sweep([1 << 20], iters=3, warmup=1, async_teardown=False)\n"
-            "print(json.dumps({'ok': r.ok, 'runtime': native.runtime_dir(),\n"
-            "                  'mapped': native.runtime_dir() + '/librccl.so' in open('/proc/self/maps').read()}))\n")
-    gate = subprocess.run(["timeout", "-k", "5", "120", sys.executable, "-c", code], capture_output=True, text=True,
-                          env=dict(os.environ, TK_HIP_RUNTIME=os.path.realpath(slim)))
-    assert gate.returncode == 0, gate.stderr[-2000:]
-    doc = json.loads([ln for ln in gate.stdout.splitlines() if ln.startswith("{")][-1])
-    assert doc["ok"] and doc["mapped"], doc
+    # default: the installed RCCL; opt-in: the verified copy through the wrapper
+    if rccl_slim == "off":
+        assert not (tools / "rccl-ready-slim").exists()
+        tool, want = tools / "rccl-ready", os.path.join(SYSTEM_LIB_DIR, "librccl.so")
+    else:
+        assert (tools / "rccl-ready-slim").exists(), proc.stderr[-2000:]
+        env_vals = dict(ln.split("=", 1) for ln in (tools / "rccl-slim.env").read_text().splitlines())
+        tool, want = tools / "rccl-ready-slim", os.path.join(env_vals["TK_RCCL_SLIM_DIR"], "librccl.so")
+    ready = subprocess.run(["timeout", "-k", "5", "120", str(tool), "--ngpus", "1", "--iters", "3", "--max-mib", "8",
+                            "--expect-rccl", want], capture_output=True, text=True)
+    assert ready.returncode == 0, ready.stdout[-2000:] + ready.stderr[-2000:]
+    doc = json.loads([ln for ln in ready.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["ok"] and doc["rccl_mapped"], doc
     calls = log.read_text()
     assert "hostnamectl set-hostname gpu-1" in calls
     assert "--ca-checksum cafe --worker" in calls and "--label amd.com/gpu.product-name=MI355X" in calls
@@ -149,7 +156,8 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     tpl = open(os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files",
                             "install_mi355x_node.sh.tftpl"), encoding="utf-8").read()
     values = {"gpu_count": 1, "gpu_burnin": "quick", "rccl_env_file": 'NCCL_DEBUG="INFO"', "rccl_min_busbw": 0,
-              "gpu_link_min_frac": 0.5, "docker_engine_install_url": "https://example.invalid/docker.sh", "docker_install_sha256": "",
+              "gpu_link_min_frac": 0.5, "rccl_slim": "off",
+              "docker_engine_install_url": "https://example.invalid/docker.sh", "docker_install_sha256": "",
               "hostname": "gpu-tf-1",
               "rancher_registry_username": "", "rancher_registry_password": "", "rancher_registry": "",
               "rancher_agent_image": "rancher/rancher-agent:v2.8.5", "rancher_api_url": "https://rancher.example",
@@ -171,17 +179,15 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     assert proc.returncode == 0, proc.stderr[-3000:]
     for exe in ("amdgpu-topo-labeller", "gpu-burnin", "rccl-ready"):
         assert os.access(tools / exe, os.X_OK), exe  # built on the node from the shipped sources
-    # rccl-ready's DT_RPATH names the node's single-target RCCL first (ahead of the box's
-    # LD_LIBRARY_PATH=/opt/rocm/lib)
-    slim = tmp_path / "var" / "rccl-slim" / "rocm"
-    assert (slim / "slim.json").exists(), proc.stderr[-2000:]
-    ldd = subprocess.run(["ldd", str(tools / "rccl-ready")], capture_output=True, text=True)
+    # default (rccl_slim off): the node's rccl-ready runs on the installed /opt/rocm RCCL
+    assert not (tools / "rccl-ready-slim").exists()
     dyn = subprocess.run(["readelf", "-d", str(tools / "rccl-ready")], capture_output=True, text=True).stdout
-    assert f"{slim}/librccl.so.1" in ldd.stdout, [ln for ln in dyn.splitlines() if "PATH" in ln]
-    ready = subprocess.run(["timeout", "-k", "5", "120", str(tools / "rccl-ready"), "--ngpus", "1", "--iters", "3"],
-                           capture_output=True, text=True)
-    assert ready.returncode == 0, ready.stderr[-2000:]
-    assert json.loads([ln for ln in ready.stdout.splitlines() if ln.startswith("{")][-1])["ok"], ready.stdout
+    assert "(RPATH)" not in dyn and "rccl-slim" not in dyn, [ln for ln in dyn.splitlines() if "PATH" in ln]
+    ready = subprocess.run(["timeout", "-k", "5", "120", str(tools / "rccl-ready"), "--ngpus", "1", "--iters", "3",
+                            "--expect-rccl", "/opt/rocm/lib/librccl.so"], capture_output=True, text=True)
+    assert ready.returncode == 0, ready.stdout[-2000:] + ready.stderr[-2000:]
+    doc = json.loads([ln for ln in ready.stdout.splitlines() if ln.startswith("{")][-1])
+    assert doc["ok"] and doc["rccl_mapped"], doc
     burn = json.loads((etc / "triton-kubernetes/gpu-burnin.json").read_text())
     assert burn["ok"], burn
     labels = (etc / "triton-kubernetes/gpu-labels").read_text()

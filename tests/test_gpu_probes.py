@@ -303,28 +303,36 @@ def test_agent_pipelined_gate_over_http():
         agent.stop()
 
 
-def test_slim_rccl_runtime_gate(tmp_path):
-    """ops/rccl_slim.py on the box: the single-target RCCL loads in a fresh process (no torch),
-    its first communicator init + verified all-reduce pass, and the process really ran on it."""
+def test_default_runtime_maps_system_rccl_and_slim_is_verified_opt_in(tmp_path):
+    """by default a fresh process (no torch) runs on /opt/rocm's librccl.  The
+    single-target copy is opt-in: prepare() verifies it on the GPU (one-rank all-reduce in a
+    child that must map it) before TK_HIP_RUNTIME=slim may select it."""
     from triton_kubernetes_amd.ops import native, rccl_slim
 
-    src = native._torch_lib_dir()
-    if not src:
-        pytest.skip("no PyTorch-ROCm runtime")
-    meta = rccl_slim.prepare(src, root=str(tmp_path / "slim"))
-    assert meta["loaded_code_object_bytes"] < meta["code_object_bytes"]
     code = ("import json, time; from triton_kubernetes_amd.ops import native, rccl\n"
             "t = time.perf_counter(); g = rccl.GateComm(rccl.unique_id(), 1, 0, [0], blocking=True)\n"
             "init_ms = (time.perf_counter() - t) * 1e3\n"
             "r = g.sweep([1 << 20, 8 << 20], iters=3, warmup=1, async_teardown=False)\n"
-            "maps = open('/proc/self/maps').read()\n"
+            "maps = [ln.split()[-1] for ln in open('/proc/self/maps') if 'librccl' in ln]\n"
             "print(json.dumps({'ok': r.ok, 'init_ms': init_ms, 'runtime': native.runtime_dir(),\n"
-            "                  'slim_mapped': native.runtime_dir() + '/librccl.so' in maps,\n"
-            "                  'full_mapped': %r + '/librccl.so' in maps}))\n" % src)
-    proc = subprocess.run(["timeout", "-k", "5", "120", sys.executable, "-c", code], capture_output=True, text=True,
-                          cwd=ROOT, env=dict(os.environ, TK_RCCL_SLIM_DIR=str(tmp_path / "slim"),
-                                             TK_HIP_RUNTIME="auto"))
-    assert proc.returncode == 0, proc.stdout[-2000:] + proc.stderr[-2000:]
-    doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
-    print(json.dumps(dict(doc, prepare=meta)))
-    assert doc["ok"] and doc["runtime"] == meta["dir"] and doc["slim_mapped"] and not doc["full_mapped"]
+            "                  'rccl': sorted({os.path.realpath(m) for m in maps})}))\n")
+    code = "import os\n" + code
+
+    def run(**env):
+        e = dict(os.environ, TK_RCCL_SLIM_DIR=str(tmp_path / "slim"))
+        e.pop("TK_HIP_RUNTIME", None)
+        e.update(env)
+        proc = subprocess.run(["timeout", "-k", "5", "120", sys.executable, "-c", code], capture_output=True,
+                              text=True, cwd=ROOT, env=e)
+        assert proc.returncode == 0, proc.stdout[-2000:] + proc.stderr[-2000:]
+        return json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
+
+    default = run()
+    system_rccl = os.path.realpath(os.path.join(native.SYSTEM_LIB_DIR, "librccl.so"))
+    assert default["ok"] and default["runtime"] == "system" and default["rccl"] == [system_rccl], default
+    meta = rccl_slim.prepare(native.SYSTEM_LIB_DIR, root=str(tmp_path / "slim"))
+    assert meta["verified"] and meta["loaded_code_object_bytes"] < meta["code_object_bytes"]
+    slim = run(TK_HIP_RUNTIME="slim")
+    print(json.dumps({"default": default, "slim": slim, "prepare": meta}))
+    assert slim["ok"] and slim["runtime"] == meta["dir"]
+    assert slim["rccl"] == [os.path.realpath(os.path.join(str(meta["dir"]), "librccl.so"))]

@@ -24,11 +24,27 @@ def test_missing_runtime_dir_fails_loudly(tmp_path):
     assert p.returncode == 0 and p.stdout.startswith("refused") and "libamdhip64.so missing" in p.stdout
 
 
-def test_auto_prefers_the_pytorch_rocm_runtime(tmp_path):
-    # (an empty single-target cache: tests/test_rccl_slim.py covers the prepared case)
-    p = _run("from triton_kubernetes_amd.ops import native; print(native.select_runtime())", TK_HIP_RUNTIME="auto",
-             TK_RCCL_SLIM_DIR=str(tmp_path))
-    assert p.returncode == 0 and p.stdout.strip().endswith("torch/lib"), p.stdout + p.stderr
+def test_default_runtime_is_the_system_rocm(tmp_path):
+    """no bench-tuned runtime by default -- /opt/rocm's HIP and RCCL, the ROCm
+    the in-tree libraries are compiled against, even with a prepared slim cache present."""
+    env = dict(os.environ, TK_RCCL_SLIM_DIR=str(tmp_path))
+    env.pop("TK_HIP_RUNTIME", None)
+    p = subprocess.run([sys.executable, "-c", "from triton_kubernetes_amd.ops import native; print(native.select_runtime())"],
+                       capture_output=True, text=True, cwd=ROOT, timeout=120, env=env)
+    assert p.returncode == 0 and p.stdout.strip() == "system", p.stdout + p.stderr
+
+
+def test_node_tools_link_the_installed_rccl():
+    """rccl-ready and libtk_rccl resolve librccl through a RUNPATH of /opt/rocm only (no
+    DT_RPATH into a patched copy); the opt-in copy is reached only through the wrapper."""
+    from triton_kubernetes_amd.ops import build, native
+
+    build.build(only=["rccl-ready", "libtk_rccl.so"])
+    for name in ("rccl-ready", "libtk_rccl.so"):
+        out = subprocess.run(["readelf", "-d", native.lib_path(name)], capture_output=True, text=True).stdout
+        assert "(RPATH)" not in out, name
+        runpath = next(ln for ln in out.splitlines() if "(RUNPATH)" in ln)
+        assert "/opt/rocm" in runpath and "rccl-slim" not in runpath, runpath
 
 
 def test_torch_runtime_preloads_the_bundled_libraries():

@@ -30,9 +30,14 @@ def test_plan_steps_and_order():
                                rancher_registry_password="p"), "https://r", "tok", "sum", mi355x=True)
     # burn-in precedes labels so the agent's topology prefetch overlaps it
     assert gpu.step_names() == ["firewall", "runtime", "hostname", "registry_login", "gpu_preflight",
-                                "gpu_burnin", "gpu_links", "gpu_labels", "rccl_env", "rccl_slim", "rccl_local",
-                                "agent"]
+                                "gpu_burnin", "gpu_links", "gpu_labels", "rccl_env", "rccl_local", "agent"]
     assert gpu.gpu == {"product": "MI355X", "count": 8, "burnin": "quick"}
+    # the single-target RCCL copy is opt-in (a modified vendor binary)
+    assert "rccl-ready-slim" not in gpu.render_shell()
+    slim = build_host_plan(dict(GPU_WORKER, rccl_slim="on"), "https://r", "t", "s", mi355x=True)
+    assert slim.step_names().index("rccl_slim") == slim.step_names().index("rccl_local") - 1
+    _bash_syntax_ok(slim.render_shell())
+    assert "rccl-ready-slim" in slim.render_shell() and "--expect-rccl" in slim.render_shell()
     off = build_host_plan(dict(GPU_WORKER, gpu_burnin="off", gpu_count=1), "https://r", "t", "s", mi355x=True)
     assert "gpu_burnin" not in off.step_names() and "rccl_local" not in off.step_names()
 

@@ -54,6 +54,56 @@ def test_process_gate_fails_fast_when_a_node_fails(tools):
     assert time.monotonic() - t0 < 20  # not the deadline: the others were killed
 
 
+def _alive(pid):
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    # a zombie has exited; /proc says so
+    try:
+        with open(f"/proc/{pid}/stat") as fh:
+            return fh.read().split(")")[-1].split()[0] != "Z"
+    except OSError:
+        return False
+
+
+class _SSHLike(LocalTransport):
+    """Like ssh without a pty: the spawned process is a client whose death does not signal
+    the 'remote' shell (a grandchild here); only the channel's stdin closing reaches it."""
+
+    def spawn(self, host, script):
+        import subprocess
+
+        client = "import subprocess, sys; sys.exit(subprocess.run(['bash', '-c', sys.argv[1]]).returncode)"
+        return subprocess.Popen([sys.executable, "-c", client, script], stdin=subprocess.PIPE,
+                                stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, env=self._env())
+
+
+def test_failed_gate_leaves_no_rank_process_behind(tools, tmp_path):
+    """a node whose peer failed is blocked in communicator init; killing the gate
+    (its ssh client) must take that node's rccl-ready down too, not leave it holding GPUs."""
+    piddir = tmp_path / "pids"
+    piddir.mkdir()
+    d, env_file = tools
+    gate = ProcessGate(_SSHLike(env={"FAKE_RCCL_FAIL_BASE": "16", "FAKE_RCCL_PIDDIR": str(piddir)}),
+                       [HostRef("local")] * 3, [8] * 3, [1 << 20, 64 << 20], iters=5, timeout=60, tools_dir=d,
+                       env_file=env_file)
+    with pytest.raises(TKError, match="exited 2"):
+        gate.run()
+    pids = [int(p.name.split(".")[0]) for p in piddir.iterdir()]
+    assert len(pids) == 3  # all three started (the third failed at once)
+    deadline = time.monotonic() + 10
+    while any(_alive(p) for p in pids) and time.monotonic() < deadline:
+        time.sleep(0.1)
+    assert not [p for p in pids if _alive(p)]
+
+
+def test_gate_tool_timeout_is_the_init_budget():
+    s = gate_script("/x", 8, 0, 8, [1 << 20], 5, None, timeout_s=3600)
+    assert "--timeout-s 300 " in s
+    assert "--timeout-s 20 " in gate_script("/x", 8, 0, 8, [1 << 20], 5, None, timeout_s=20)
+
+
 def test_process_gate_deadline_without_unique_id(tools):
     with pytest.raises(TKError, match="no unique id"):
         _gate(tools, n=2, env={"FAKE_RCCL_NO_UID": "1"}, timeout=1.5).run()
@@ -61,7 +111,9 @@ def test_process_gate_deadline_without_unique_id(tools):
 
 def test_gate_script_shape():
     s = gate_script("/opt/triton-kubernetes/bin", 16, 8, 8, [1 << 20, 256 << 20], 5, "ab" * 128)
-    assert s.startswith("set -a; [ -r /etc/rccl/rccl.env ] && . /etc/rccl/rccl.env; set +a; exec ")
+    assert s.startswith("set -a; [ -r /etc/rccl/rccl.env ] && . /etc/rccl/rccl.env; set +a; ")
+    # installed RCCL by default; the verified opt-in wrapper only when the node has it
+    assert "t=/opt/triton-kubernetes/bin/rccl-ready; [ -x /opt/triton-kubernetes/bin/rccl-ready-slim ]" in s
     assert "--cluster --world 16 --rank-base 8 --ngpus 8 --max-mib 256 --iters 5" in s and "--uid abab" in s
     assert "--uid-out" in gate_script("/x", 8, 0, 8, [1 << 20], 5, None)
 

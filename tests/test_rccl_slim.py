@@ -63,7 +63,7 @@ def test_in_tree_library_sections_parse():
 def test_prepare_from_plain_bundle(tmp_path):
     lib = _lib()
     src = _fake_runtime(tmp_path, lib)
-    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False)
+    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False, verify_with_gpu=False)
     out = meta["dir"]
     assert not meta["cached"] and meta["source_format"] == "bundle"
     assert os.path.exists(os.path.join(out, "slim.json"))
@@ -84,7 +84,7 @@ def test_prepare_from_plain_bundle(tmp_path):
     assert x[:off0] == y[:off0] and x[off0 + size0:] == y[off0 + size0:]
     # the rest of the runtime is linked in; a second prepare is a cache hit
     assert os.path.islink(os.path.join(out, "libamdhip64.so"))
-    assert rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False)["cached"] is True
+    assert rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False, verify_with_gpu=False)["cached"] is True
     assert rccl_slim.cached(src, root=str(tmp_path / "cache")) == ""  # the stripped entry is another key
 
 
@@ -111,7 +111,7 @@ def test_prepare_from_compressed_multi_target_bundle(tmp_path):
     with open(os.path.join(src, "librccl.so"), "r+b") as fh:
         fh.seek(off)
         fh.write(fat + b"\0" * (size - len(fat)))
-    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"))
+    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), verify_with_gpu=False)
     assert meta["source_format"] == "compressed"
     _, _, new = _section(os.path.join(meta["dir"], "librccl.so"))
     entries = rccl_slim.parse_bundle(new)
@@ -121,7 +121,7 @@ def test_prepare_from_compressed_multi_target_bundle(tmp_path):
     assert got[:4] == b"\x7fELF" and s == meta["loaded_code_object_bytes"] <= len(co)
     # a target the bundle lacks is an error, and no partial entry is left behind
     with pytest.raises(rccl_slim.SlimError, match="gfx1234"):
-        rccl_slim.prepare(src, arch="gfx1234", root=str(tmp_path / "cache2"))
+        rccl_slim.prepare(src, arch="gfx1234", root=str(tmp_path / "cache2"), verify_with_gpu=False)
     assert not os.path.exists(tmp_path / "cache2") or os.listdir(tmp_path / "cache2") == []
 
 
@@ -136,7 +136,7 @@ def test_partial_entry_is_never_used(tmp_path):
 def test_source_change_invalidates_the_entry(tmp_path):
     src = _fake_runtime(tmp_path, _lib())
     root = str(tmp_path / "cache")
-    rccl_slim.prepare(src, root=root, strip=False)
+    rccl_slim.prepare(src, root=root, strip=False, verify_with_gpu=False)
     k1 = rccl_slim.entry_dir(src, root=root)
     os.utime(os.path.join(src, "librccl.so"), ns=(1, 1))
     assert rccl_slim.entry_dir(src, root=root) != k1
@@ -147,7 +147,7 @@ def test_non_elf_is_refused(tmp_path):
     src.mkdir()
     (src / "librccl.so").write_bytes(b"MZ" + b"\0" * 100)
     with pytest.raises(rccl_slim.SlimError, match="not an ELF64"):
-        rccl_slim.prepare(str(src), root=str(tmp_path / "cache"))
+        rccl_slim.prepare(str(src), root=str(tmp_path / "cache"), verify_with_gpu=False)
 
 
 def _select(env):
@@ -158,21 +158,53 @@ def _select(env):
     return p.stdout.strip()
 
 
-def test_auto_selects_the_prepared_slim_runtime(tmp_path):
-    torch_dir = native._torch_lib_dir()
-    if not torch_dir:
-        pytest.skip("no PyTorch-ROCm runtime")
+def test_slim_runtime_is_opt_in_and_verified_only(tmp_path):
+    """An unverified entry is never selected; TK_HIP_RUNTIME=slim (the opt-in) picks a
+    verified one; without the opt-in nothing picks it."""
     root = str(tmp_path / "cache")
-    assert _select({"TK_HIP_RUNTIME": "auto", "TK_RCCL_SLIM_DIR": root}) == torch_dir
-    # prepared (the agent unit's ExecStartPre) -> auto picks it; TK_RCCL_SLIM=0 opts out
-    d = rccl_slim.entry_dir(torch_dir, root=root)
+    d = rccl_slim.entry_dir(native.SYSTEM_LIB_DIR, root=root)
     os.makedirs(d)
     with open(os.path.join(d, "slim.json"), "w", encoding="utf-8") as fh:
         json.dump({"dir": d}, fh)
-    assert _select({"TK_HIP_RUNTIME": "auto", "TK_RCCL_SLIM_DIR": root}) == d
+    assert rccl_slim.cached(native.SYSTEM_LIB_DIR, root=root) == ""
+    with open(os.path.join(d, "slim.json"), "w", encoding="utf-8") as fh:
+        json.dump({"dir": d, "verified": {"time": 1}}, fh)
+    assert rccl_slim.cached(native.SYSTEM_LIB_DIR, root=root) == d
     assert _select({"TK_HIP_RUNTIME": "slim", "TK_RCCL_SLIM_DIR": root}) == d
-    assert _select({"TK_HIP_RUNTIME": "auto", "TK_RCCL_SLIM_DIR": root, "TK_RCCL_SLIM": "0"}) == torch_dir
-    assert _select({"TK_HIP_RUNTIME": "torch", "TK_RCCL_SLIM_DIR": root}) == torch_dir
+    assert _select({"TK_HIP_RUNTIME": "system", "TK_RCCL_SLIM_DIR": root}) == "system"
+
+
+def test_failed_verification_removes_the_entry(tmp_path, monkeypatch):
+    src = _fake_runtime(tmp_path, _lib())
+    root = str(tmp_path / "cache")
+
+    def boom(entry, timeout=180.0):
+        raise rccl_slim.SlimError("verifying: allreduce mismatch")
+
+    monkeypatch.setattr(rccl_slim, "verify", boom)
+    with pytest.raises(rccl_slim.SlimError, match="mismatch"):
+        rccl_slim.prepare(src, root=root, strip=False)
+    assert not os.path.exists(rccl_slim.entry_dir(src, root=root, strip=False))
+    assert [n for n in os.listdir(root) if not n.startswith(".")] == []
+    monkeypatch.setattr(rccl_slim, "verify", lambda entry, timeout=180.0: {"ok": True, "init_ms": 1.0,
+                                                                          "mapped": [entry + "/librccl.so"]})
+    meta = rccl_slim.prepare(src, root=root, strip=False)
+    assert meta["verified"]["mapped"] and meta["dir"] == rccl_slim.entry_dir(src, root=root, strip=False)
+
+
+def test_verify_child_without_gpu_reports_failure(tmp_path):
+    """On a machine without a GPU the verification child fails (it never passes by default)."""
+    src = _fake_runtime(tmp_path, _lib())
+    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False, verify_with_gpu=False)
+    env = dict(os.environ, TK_FORCE_NO_GPU="1")
+    with pytest.raises(rccl_slim.SlimError):
+        old = os.environ.copy()
+        try:
+            os.environ.update(env)
+            rccl_slim.verify(str(meta["dir"]), timeout=120)
+        finally:
+            os.environ.clear()
+            os.environ.update(old)
 
 
 def test_cli_reports_errors_as_json(tmp_path):
@@ -185,7 +217,7 @@ def test_cli_reports_errors_as_json(tmp_path):
 def test_shell_form_matches_the_python_form(tmp_path):
     """terraform/scripts.py tk_rccl_slim (SSH / Terraform nodes) on a fake ROCm tree whose
     librccl carries a compressed 2-target bundle: one aligned gfx950 entry, soname aliases
-    on the copy, the ``rocm`` link the node tools' RUNPATH names, cached on a re-run."""
+    on the copy, cached on a re-run; no link anything loads by default."""
     from triton_kubernetes_amd.terraform.scripts import RCCL_SLIM_FN
 
     lib = _lib()
@@ -216,7 +248,7 @@ def test_shell_form_matches_the_python_form(tmp_path):
     p = subprocess.run(["bash", "-c", script], capture_output=True, text=True, timeout=120)
     assert p.returncode == 0, p.stderr
     out = p.stdout.strip()
-    assert os.path.realpath(root / "rocm") == os.path.realpath(out)
+    assert not os.path.exists(root / "rocm")  # nothing points the node tools at it
     new_lib = os.path.join(out, "librccl.so")
     assert os.path.getsize(new_lib) == os.path.getsize(real)
     _, _, new = _section(new_lib)
@@ -233,7 +265,7 @@ def test_shell_form_matches_the_python_form(tmp_path):
 def test_python_form_links_every_librccl_alias_to_the_copy(tmp_path):
     src = _fake_runtime(tmp_path, _lib())
     os.symlink("librccl.so", os.path.join(src, "librccl.so.1"))
-    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False)
+    meta = rccl_slim.prepare(src, root=str(tmp_path / "cache"), strip=False, verify_with_gpu=False)
     assert os.readlink(os.path.join(meta["dir"], "librccl.so.1")) == "librccl.so"
     path = rccl_slim.link(str(tmp_path / "cache"), "rocm", str(meta["dir"]))
     assert os.path.realpath(path) == os.path.realpath(meta["dir"])
@@ -242,7 +274,46 @@ def test_python_form_links_every_librccl_alias_to_the_copy(tmp_path):
 def test_gpu_cli_prepares_and_reports(tmp_path):
     src = _fake_runtime(tmp_path, _lib())
     p = subprocess.run([sys.executable, "-m", "triton_kubernetes_amd", "gpu", "rccl-slim", "--source", src, "--root",
-                        str(tmp_path / "c")], capture_output=True, text=True, cwd=ROOT, timeout=120)
+                        str(tmp_path / "c"), "--no-verify"], capture_output=True, text=True, cwd=ROOT, timeout=120)
     assert p.returncode == 0, p.stderr
     meta = json.loads(p.stdout.strip().splitlines()[-1])
     assert os.path.exists(os.path.join(meta["dir"], "slim.json")) and meta["cached"] is False
+    assert "verified" not in meta and rccl_slim.cached(src, root=str(tmp_path / "c")) == ""
+
+
+def test_shell_enable_verifies_then_wraps_and_falls_back_when_stale(tmp_path):
+    """The opt-in on SSH / Terraform nodes: the copy is enabled only after rccl-ready ran a
+    one-rank all-reduce that mapped it; the wrapper uses it while the installed librccl is
+    unchanged and falls back (with a warning) after a ROCm upgrade."""
+    from triton_kubernetes_amd.terraform.scripts import RCCL_SLIM_ENABLE_FN
+
+    rocm, tools, copy = tmp_path / "rocm", tmp_path / "bin", tmp_path / "copy"
+    (rocm / "lib").mkdir(parents=True)
+    tools.mkdir()
+    copy.mkdir()
+    (rocm / "lib" / "librccl.so").write_bytes(b"installed")
+    (copy / "librccl.so").write_bytes(b"copy")
+    # stand-in rccl-ready: prints the LD_LIBRARY_PATH it ran with; --expect-rccl passes only
+    # when that library is first on the path (the real tool reads /proc/self/maps)
+    (tools / "rccl-ready").write_text(
+        '#!/bin/sh\nfor a in "$@"; do case $prev in --expect-rccl) exp=$a;; esac; prev=$a; done\n'
+        'echo "LD=$LD_LIBRARY_PATH"\n'
+        'if [ -n "$exp" ]; then [ "$(dirname "$exp")" = "${LD_LIBRARY_PATH%%:*}" ] && [ "$FAIL" != 1 ] || exit 1; fi\n')
+    (tools / "rccl-ready").chmod(0o755)
+    stub = f"tk_rccl_slim() {{ echo {copy}; }}\n"
+    run = lambda extra_env=None: subprocess.run(  # noqa: E731
+        ["bash", "-c", stub + RCCL_SLIM_ENABLE_FN + f"\ntk_rccl_slim_enable {tmp_path}/c {rocm} {tools}\n"],
+        capture_output=True, text=True, timeout=60, env=dict(os.environ, **(extra_env or {})))
+    p = run({"FAIL": "1"})
+    assert p.returncode != 0 and "failed its one-rank verified all-reduce" in p.stderr
+    assert not (tools / "rccl-ready-slim").exists() and not (tools / "rccl-slim.env").exists()
+    p = run()
+    assert p.returncode == 0, p.stderr
+    assert (tools / "rccl-ready-slim").exists()
+    env = dict(os.environ, ROCM_PATH=str(rocm))
+    env.pop("LD_LIBRARY_PATH", None)
+    w = subprocess.run([str(tools / "rccl-ready-slim"), "--ngpus", "8"], capture_output=True, text=True, env=env)
+    assert w.returncode == 0 and w.stdout.strip() == f"LD={copy}"
+    os.utime(rocm / "lib" / "librccl.so", ns=(10**9, 10**9))  # "upgraded"
+    w = subprocess.run([str(tools / "rccl-ready-slim"), "--ngpus", "8"], capture_output=True, text=True, env=env)
+    assert w.returncode == 0 and w.stdout.strip() == "LD=" and "librccl changed" in w.stderr

@@ -173,6 +173,15 @@ def _mi355x_fields(ctx: Context) -> Dict:
         except ValueError as exc:
             raise ConfigError(f"gpu_link_min_frac must be a number between 0 and 1. Found '{frac}'.") from exc
         out["gpu_link_min_frac"] = frac
+    if s.is_set("rccl_slim"):  # opt-in verified single-target RCCL (terraform/scripts.py)
+        slim = s.get_string("rccl_slim").lower()
+        if slim in ("true", "yes", "1"):
+            slim = "on"
+        if slim in ("false", "no", "0"):
+            slim = "off"
+        if slim not in ("on", "off"):
+            raise ConfigError(f"rccl_slim must be on or off. Found '{slim}'.")
+        out["rccl_slim"] = slim
     return out
 
 

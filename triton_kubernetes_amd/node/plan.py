@@ -34,7 +34,7 @@ from dataclasses import asdict, dataclass, field
 from typing import Any, Dict, List, Optional
 
 from ..parallel.rccl_env import render_env_file
-from ..terraform.scripts import RCCL_SLIM_FN, RCCL_SLIM_ROOT
+from ..terraform.scripts import RCCL_SLIM_ENABLE_FN, RCCL_SLIM_FN, RCCL_SLIM_ROOT
 
 from ..versions import AGENT_IMAGE as DEFAULT_AGENT_IMAGE
 from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
@@ -217,15 +217,21 @@ sudo mkdir -p "$(dirname {RCCL_ENV_FILE})"
 {render_env_file(env).rstrip()}
 TK_RCCL_EOF
 }} | sudo tee {RCCL_ENV_FILE} >/dev/null""", {"env": env}, gpu=True))
-        # single-target RCCL for the node tools (ops/rccl_slim.py; cached, so a no-op after
-        # the first bring-up); never fatal: without it the tools load the full bundle
-        plan.steps.append(Step("rccl_slim", "rccl_slim", f"""
+        slim = str(cfg.get("rccl_slim", "off") or "off").lower() == "on"
+        if slim:
+            # OPT-IN single-target RCCL (terraform/scripts.py): built, verified by a one-rank
+            # all-reduce that must map it, then used through rccl-ready-slim; never fatal
+            plan.steps.append(Step("rccl_slim", "rccl_slim", f"""
 {RCCL_SLIM_FN}
-sudo bash -c "$(declare -f tk_rccl_slim); tk_rccl_slim {RCCL_SLIM_ROOT} ${{ROCM_PATH:-/opt/rocm}}" >/dev/null \\
-  || echo 'rccl slim: skipped, the node tools load the full RCCL bundle' >&2""", {"root": RCCL_SLIM_ROOT}, gpu=True))
+{RCCL_SLIM_ENABLE_FN}
+sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enable {RCCL_SLIM_ROOT} ${{ROCM_PATH:-/opt/rocm}} {TOOLS_DIR}" >/dev/null \\
+  || echo 'rccl slim: not enabled, the node tools load the installed RCCL' >&2""", {"root": RCCL_SLIM_ROOT}, gpu=True))
         if ngpu > 1:
+            tool = f"{TOOLS_DIR}/rccl-ready"
+            if slim:
+                tool = f"$([ -x {TOOLS_DIR}/rccl-ready-slim ] && echo {TOOLS_DIR}/rccl-ready-slim || echo {tool})"
             plan.steps.append(Step("rccl_local", "rccl_local",
-                                   f"{TOOLS_DIR}/rccl-ready --ngpus {ngpu} --min-busbw "
+                                   f"{tool} --ngpus {ngpu} --min-busbw "
                                    f"{float(cfg.get('rccl_min_busbw', 0) or 0)}",
                                    {"count": ngpu, "min_busbw": float(cfg.get("rccl_min_busbw", 0) or 0)},
                                    gpu=True))

@@ -35,7 +35,6 @@ ARCH = os.environ.get("PYTORCH_ROCM_ARCH", "gfx950")
 HIP_FLAGS = ["-O3", "-std=c++17", f"--offload-arch={ARCH}", "-Wno-unused-result", "-Wno-unused-value",
              "-Wno-unused-command-line-argument"]
 RPATH = [f"-Wl,-rpath,{ROCM}/lib"]
-RCCL_SLIM_ROOT = "/var/lib/triton-kubernetes/rccl-slim"  # = terraform/scripts.py RCCL_SLIM_ROOT
 # VGPR-form MFMA accumulators: see the note at the top of csrc/tk_gpu_probe.hip
 MFMA_FLAGS = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
 
@@ -78,12 +77,11 @@ def targets() -> List[Target]:
         Target("libtk_rccl.so", [rccl],
                [hipcc, *HIP_FLAGS, "-fPIC", "-shared", rccl, "-o", out("libtk_rccl.so"), f"-L{ROCM}/lib",
                 "-lrccl", *RPATH]),
-        # the node's single-target RCCL first (ops/rccl_slim.py, terraform/scripts.py
-        # tk_rccl_slim), else /opt/rocm's: a DT_RPATH, searched before LD_LIBRARY_PATH (ROCm
-        # hosts commonly export LD_LIBRARY_PATH=/opt/rocm/lib, which would shadow a RUNPATH)
+        # /opt/rocm's RCCL (RUNPATH).  The opt-in single-target copy (rccl_slim) is reached
+        # only through the rccl-ready-slim wrapper, which checks it is verified and current
         Target("rccl-ready", [rccl],
                [hipcc, *HIP_FLAGS, "-DTK_RCCL_MAIN", rccl, "-o", out("rccl-ready"), f"-L{ROCM}/lib", "-lrccl",
-                f"-Wl,--disable-new-dtags,-rpath,{RCCL_SLIM_ROOT}/rocm:{ROCM}/lib"]),
+                *RPATH]),
         # in-process library: sysfs collector only, no libamd_smi (see csrc/tk_topo.cpp)
         Target("libtk_topo.so", [topo],
                ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", topo, "-o", out("libtk_topo.so")]),

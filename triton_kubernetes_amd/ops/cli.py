@@ -6,7 +6,7 @@
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
     python -m triton_kubernetes_amd.ops.cli links [--min-frac F] [--mib M]
     python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
-    python -m triton_kubernetes_amd.ops.cli rccl-slim [--all] [--source DIR] [--root DIR]
+    python -m triton_kubernetes_amd.ops.cli rccl-slim [--source DIR] [--root DIR] [--no-verify]
     python -m triton_kubernetes_amd.ops.cli gemm [--size N] [--reps R] [--schedule staggered|single-barrier] [--dtype bf16|fp8]
 
 Every command prints one JSON document; the exit status is non-zero when the
@@ -34,9 +34,9 @@ def main(argv: Sequence[str] = ()) -> int:
     lk = sub.add_parser("links", help="per-link xGMI check: peer copy bandwidth of every ordered GPU pair")
     lk.add_argument("--min-frac", type=float, default=0.5, help="fail below this fraction of the node median")
     lk.add_argument("--mib", type=int, default=64, help="bytes per copy (MiB)")
-    sl = sub.add_parser("rccl-slim", help="prepare the single-target (gfx950) RCCL for fast cold communicator init")
-    sl.add_argument("--all", action="store_true", help="the PyTorch-ROCm RCCL and /opt/rocm's")
+    sl = sub.add_parser("rccl-slim", help="opt-in: prepare and verify the single-target (gfx950) RCCL copy")
     sl.add_argument("--source", default="")
+    sl.add_argument("--no-verify", action="store_true", help="skip the GPU verification (the copy stays unused)")
     sl.add_argument("--root", default="")
     h = sub.add_parser("hbm")
     h.add_argument("--device", type=int, default=0)
@@ -99,8 +99,8 @@ def main(argv: Sequence[str] = ()) -> int:
     if args.cmd == "rccl-slim":
         from . import rccl_slim
 
-        return rccl_slim.main((["--all"] if args.all else []) + (["--source", args.source] if args.source else [])
-                              + (["--root", args.root] if args.root else []))
+        return rccl_slim.main((["--source", args.source] if args.source else [])
+                              + (["--root", args.root] if args.root else []) + (["--no-verify"] if args.no_verify else []))
     if args.cmd == "hbm":
         from . import probe
 

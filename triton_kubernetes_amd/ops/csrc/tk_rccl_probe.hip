@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <climits>
+#include <string>
 #include <atomic>
 #include <condition_variable>
 #include <functional>
@@ -742,6 +744,26 @@ static int cluster_main(int world, int rank_base, int ndev, const char* uid_hex,
   return ok ? 0 : 1;
 }
 
+// True when /proc/self/maps has a librccl mapping whose real path is `want`'s.
+static bool rccl_mapped(const char* want) {
+  char want_real[PATH_MAX];
+  if (!realpath(want, want_real)) return false;
+  FILE* f = fopen("/proc/self/maps", "r");
+  if (!f) return false;
+  char line[PATH_MAX + 256];
+  bool found = false;
+  while (!found && fgets(line, sizeof line, f)) {
+    const char* p = strchr(line, '/');
+    if (!p || !strstr(p, "librccl")) continue;
+    std::string path(p);
+    while (!path.empty() && (path.back() == '\n' || path.back() == ' ')) path.pop_back();
+    char real[PATH_MAX];
+    found = realpath(path.c_str(), real) && !strcmp(real, want_real);
+  }
+  fclose(f);
+  return found;
+}
+
 int main(int argc, char** argv) {
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
@@ -750,8 +772,9 @@ int main(int argc, char** argv) {
   }
   double min_busbw = 0.0, timeout_s = 600.0;
   int iters = 20, warmup = 5, dtype = 0, world = 0, rank_base = 0, max_mib = 64;
-  bool cluster = false, uid_out = false;
+  bool cluster = false, uid_out = false, max_set = false;
   const char* uid_hex = nullptr;
+  const char* expect_rccl = nullptr;  // --expect-rccl: the librccl this process must have mapped
   const int visible = ndev;
   for (int i = 1; i < argc; ++i) {
     if (!strcmp(argv[i], "--min-busbw") && i + 1 < argc) min_busbw = atof(argv[++i]);
@@ -763,8 +786,9 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--rank-base") && i + 1 < argc) rank_base = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--uid") && i + 1 < argc) uid_hex = argv[++i];
     else if (!strcmp(argv[i], "--uid-out")) uid_out = true;
-    else if (!strcmp(argv[i], "--max-mib") && i + 1 < argc) max_mib = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--max-mib") && i + 1 < argc) { max_mib = atoi(argv[++i]); max_set = true; }
     else if (!strcmp(argv[i], "--timeout-s") && i + 1 < argc) timeout_s = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--expect-rccl") && i + 1 < argc) expect_rccl = argv[++i];
   }
   if (ndev < 1 || ndev > visible) {
     fprintf(stderr, "{\"error\":\"--ngpus %d but %d visible\"}\n", ndev, visible);
@@ -778,7 +802,8 @@ int main(int argc, char** argv) {
     return cluster_main(world, rank_base, ndev, uid_hex, uid_out, max_mib, iters, dtype, min_busbw, timeout_s);
   }
   std::vector<size_t> sizes;
-  for (size_t b = 1u << 20; b <= (1ull << 30); b <<= 2) sizes.push_back(b);
+  const size_t top = max_set ? ((size_t)(max_mib < 1 ? 1 : max_mib) << 20) : (1ull << 30);
+  for (size_t b = 1u << 20; b <= top; b <<= 2) sizes.push_back(b);
   const int n = (int)sizes.size();
   std::vector<double> t(n), alg(n), bus(n), err(n);
   int rc = tkr_sweep_local(ndev, sizes.data(), n, iters, warmup, dtype, t.data(), alg.data(), bus.data(), err.data());
@@ -793,8 +818,15 @@ int main(int argc, char** argv) {
     printf("%s{\"bytes\":%zu,\"time_us\":%.2f,\"algbw_gbps\":%.2f,\"busbw_gbps\":%.2f,\"errors\":%.0f}", i ? "," : "",
            sizes[i], t[i], alg[i], bus[i], err[i]);
   }
-  const bool ok = errs == 0 && bus[n - 1] >= min_busbw;
-  printf("],\"ok\":%s}\n", ok ? "true" : "false");
+  bool ok = errs == 0 && bus[n - 1] >= min_busbw;
+  printf("]");
+  if (expect_rccl) {
+    // the opt-in single-target RCCL is verified by a run that provably loaded it
+    const bool mapped = rccl_mapped(expect_rccl);
+    printf(",\"expect_rccl\":\"%s\",\"rccl_mapped\":%s", expect_rccl, mapped ? "true" : "false");
+    ok = ok && mapped;
+  }
+  printf(",\"ok\":%s}\n", ok ? "true" : "false");
   return ok ? 0 : 1;
 }
 #endif

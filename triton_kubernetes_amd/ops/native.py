@@ -47,56 +47,36 @@ def select_runtime() -> str:
     """The HIP runtime + RCCL directory this process will use (``TK_HIP_RUNTIME``), without
     loading anything: ``"system"`` or a directory.
 
-    * ``auto`` (default): the builds bundled with an installed PyTorch-ROCm wheel (its
-      ``lib/``, found without importing torch) when present -- the runtime and RCCL that
-      ``torch.distributed`` jobs on the node use, and the one the GPU test-suite runs on
-      (tests import torch first) -- else ``/opt/rocm``.  When the node has prepared the
-      single-target copy of that RCCL (``ops/rccl_slim.py``; the agent unit's
-      ``ExecStartPre``), its directory instead, unless ``TK_RCCL_SLIM=0``;
-    * ``slim``: that single-target directory, prepared now if the node has none yet;
-    * ``system``: ``/opt/rocm`` (the libraries' RUNPATH);
-    * ``torch``: the PyTorch-ROCm builds, required;
+    * ``system`` (default): ``/opt/rocm`` -- the libraries' RUNPATH, the ROCm the in-tree
+      ``.so`` files are compiled against;
+    * ``torch``: the builds bundled with an installed PyTorch-ROCm wheel (its ``lib/``,
+      found without importing torch), required;
+    * ``slim``: opt-in single-target copy of ``/opt/rocm``'s RCCL (``ops/rccl_slim.py``),
+      prepared and verified now if the node has no verified copy yet;
     * a path: a directory holding ``libamdhip64.so`` / ``librccl.so``.
 
-    Measured on MI355X (``profiles/round2/runtime_ab.md``, ``profiles/round2/rccl_slim_ab.md``):
-    a cold process's first RCCL communicator init takes ~0.9 s on the PyTorch-ROCm 7.0 build
-    (RCCL 2.26.6), ~1.7 s on ``/opt/rocm`` 7.2 (RCCL 2.27.7), whose device code is one
-    544 MiB compressed bundle, and ~0.27 s on the single-target copy."""
-    sel = os.environ.get("TK_HIP_RUNTIME", "auto") or "auto"
+    A process that imports torch before loading a native library runs on torch's runtime
+    whatever this says (one HIP runtime per process)."""
+    sel = os.environ.get("TK_HIP_RUNTIME", "system") or "system"
     if sel == "system":
         return "system"
-    if sel in ("auto", "torch", "slim"):
+    if sel == "torch":
         d = _torch_lib_dir()
-        if d and sel != "torch" and os.environ.get("TK_RCCL_SLIM", "1") != "0":
-            from . import rccl_slim
-
-            slim = rccl_slim.cached(d)
-            if slim:
-                return slim
-            if sel == "slim":
-                try:
-                    return str(rccl_slim.prepare(d)["dir"])
-                except (rccl_slim.SlimError, OSError) as exc:
-                    raise NativeUnavailable(f"TK_HIP_RUNTIME=slim: {exc}") from exc
-        if d:
-            return d
-        if sel == "torch":
+        if not d:
             raise NativeUnavailable("TK_HIP_RUNTIME=torch but no PyTorch-ROCm runtime is installed")
-        # no PyTorch-ROCm: /opt/rocm, or the single-target copy of its RCCL
-        if os.environ.get("TK_RCCL_SLIM", "1") != "0" and os.path.exists(os.path.join(SYSTEM_LIB_DIR, "librccl.so")):
-            from . import rccl_slim
+        return d
+    if sel == "slim":
+        from . import rccl_slim
 
-            slim = rccl_slim.cached(SYSTEM_LIB_DIR)
-            if slim:
-                return slim
-            if sel == "slim":
-                try:
-                    return str(rccl_slim.prepare(SYSTEM_LIB_DIR)["dir"])
-                except (rccl_slim.SlimError, OSError) as exc:
-                    raise NativeUnavailable(f"TK_HIP_RUNTIME=slim: {exc}") from exc
-        if sel == "slim":
+        if not os.path.exists(os.path.join(SYSTEM_LIB_DIR, "librccl.so")):
             raise NativeUnavailable("TK_HIP_RUNTIME=slim but no RCCL is installed")
-        return "system"
+        slim = rccl_slim.cached(SYSTEM_LIB_DIR)
+        if slim:
+            return slim
+        try:
+            return str(rccl_slim.prepare(SYSTEM_LIB_DIR)["dir"])
+        except (rccl_slim.SlimError, OSError) as exc:
+            raise NativeUnavailable(f"TK_HIP_RUNTIME=slim: {exc}") from exc
     return sel
 
 

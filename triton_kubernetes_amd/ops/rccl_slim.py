@@ -17,6 +17,13 @@ libraries of the source directory are symlinked next to it (``librccl.so`` finds
 its dependencies through ``$ORIGIN``), so the directory is a drop-in runtime for
 ``ops/native.py:select_runtime``.
 
+Opt-in.  The copy is a modified vendor binary, so nothing uses it by default: the
+node tools and agents load ``/opt/rocm/lib/librccl.so``.  A node opts in with
+``rccl_slim = "on"`` (MI355X host module / node plan) or ``TK_HIP_RUNTIME=slim``
+(agent), and an entry is only ever used after :func:`verify` ran a one-rank
+all-reduce on it in a fresh process, checked the result and checked that the process
+really mapped the copy (``slim.json`` ``verified``).
+
 Cache.  ``$TK_RCCL_SLIM_DIR`` (default ``/var/lib/triton-kubernetes/rccl-slim``
 when writable, else ``~/.cache/triton-kubernetes/rccl-slim``), one subdirectory
 per source build (keyed by path, size, mtime and a hash of its first MiB).  A
@@ -231,20 +238,92 @@ def entry_dir(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, st
     return os.path.join(root or cache_root(), f"{arch}-{key}" + ("" if strip else "-debug"))
 
 
+def _meta(d: str) -> Dict[str, object]:
+    try:
+        with open(os.path.join(d, "slim.json"), "r", encoding="utf-8") as fh:
+            return json.load(fh)
+    except (OSError, ValueError):
+        return {}
+
+
 def cached(src_dir: str, arch: str = "gfx950", root: Optional[str] = None) -> str:
-    """The finished slim runtime directory for ``src_dir``, or ``""``."""
+    """The finished *and verified* slim runtime directory for ``src_dir``, or ``""``
+    (keyed by the current source library: a ROCm upgrade never reuses an old copy)."""
     try:
         d = entry_dir(src_dir, arch, root)
     except OSError:
         return ""
-    return d if os.path.exists(os.path.join(d, "slim.json")) else ""
+    return d if _meta(d).get("verified") else ""
 
 
-def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, strip: bool = True) -> Dict[str, object]:
-    """Build (or find) the slim runtime directory for the RCCL in ``src_dir``.
+VERIFY_BYTES = 4 << 20
+
+
+def verify(entry: str, timeout: float = 180.0) -> Dict[str, object]:
+    """One-rank verified all-reduce against the copy in ``entry``, in a fresh process
+    (``TK_HIP_RUNTIME=<entry>``): the child must map ``<entry>/librccl.so`` and the
+    all-reduce result must check.  Raises :class:`SlimError` otherwise."""
+    import sys
+
+    env = dict(os.environ, TK_HIP_RUNTIME=entry)
+    try:
+        proc = subprocess.run([sys.executable, "-m", "triton_kubernetes_amd.ops.rccl_slim", "--verify-child", entry],
+                              capture_output=True, text=True, timeout=timeout, env=env,
+                              cwd=os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__)))))
+    except subprocess.TimeoutExpired as exc:
+        raise SlimError(f"verifying {entry}: timed out after {timeout:.0f} s") from exc
+    line = (proc.stdout.strip().splitlines() or [""])[-1]
+    try:
+        res = json.loads(line)
+    except ValueError:
+        res = {}
+    if proc.returncode != 0 or not res.get("ok"):
+        raise SlimError(f"verifying {entry} failed (exit {proc.returncode}): "
+                        f"{res.get('error') or proc.stderr.strip()[-400:]}")
+    return res
+
+
+def _verify_child(entry: str) -> int:
+    """Child side of :func:`verify` (the runtime was selected from ``TK_HIP_RUNTIME``)."""
+    out: Dict[str, object] = {"entry": entry}
+    try:
+        from . import native, rccl
+
+        native.runtime_dir()
+        res = rccl.sweep_local(1, sizes=(VERIFY_BYTES,), iters=2, warmup=1)
+        with open("/proc/self/maps", "r", encoding="utf-8") as fh:
+            maps = {ln.split()[-1] for ln in fh if "librccl" in ln and "/" in ln}
+        want = os.path.realpath(os.path.join(entry, "librccl.so"))
+        mapped = sorted(maps)
+        out.update(allreduce_ok=res.ok, errors=res.errors, init_ms=round(res.init_ms, 3), mapped=mapped,
+                   ok=res.ok and any(os.path.realpath(m) == want for m in mapped))
+        if res.ok and not out["ok"]:
+            out["error"] = f"the process mapped {mapped}, not {want}"
+    except Exception as exc:  # noqa: BLE001 - reported to the parent
+        out.update(ok=False, error=f"{type(exc).__name__}: {exc}")
+    print(json.dumps(out), flush=True)
+    return 0 if out.get("ok") else 1
+
+
+def _record_verified(d: str, result: Dict[str, object]) -> Dict[str, object]:
+    meta = _meta(d)
+    meta["verified"] = {"time": time.time(), "init_ms": result.get("init_ms"), "mapped": result.get("mapped")}
+    tmp = os.path.join(d, f".slim.json.{os.getpid()}")
+    with open(tmp, "w", encoding="utf-8") as fh:
+        json.dump(meta, fh, indent=1)
+    os.replace(tmp, os.path.join(d, "slim.json"))
+    return meta
+
+
+def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, strip: bool = True,
+            verify_with_gpu: bool = True) -> Dict[str, object]:
+    """Build (or find) the slim runtime directory for the RCCL in ``src_dir`` and (unless
+    ``verify_with_gpu`` is False — CPU tests of the ELF surgery) :func:`verify` it before
+    it may be used.
 
     Returns the entry's metadata (``dir``, sizes, ``prepare_s``; ``cached`` True when it
-    already existed).  Raises :class:`SlimError` when the library cannot be slimmed."""
+    already existed).  Raises :class:`SlimError` when the library cannot be slimmed or
+    the copy fails verification (the entry is then removed)."""
     t0 = time.perf_counter()
     lib = os.path.join(src_dir, "librccl.so")
     if not os.path.exists(lib):
@@ -252,8 +331,13 @@ def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, stri
     out = entry_dir(src_dir, arch, root, strip)
     meta_path = os.path.join(out, "slim.json")
     if os.path.exists(meta_path):
-        with open(meta_path, "r", encoding="utf-8") as fh:
-            meta = json.load(fh)
+        meta = _meta(out)
+        if verify_with_gpu and not meta.get("verified"):
+            try:
+                meta = _record_verified(out, verify(out))
+            except SlimError:
+                shutil.rmtree(out, ignore_errors=True)
+                raise
         meta["cached"] = True
         return meta
     real = os.path.realpath(lib)
@@ -299,6 +383,9 @@ def prepare(src_dir: str, arch: str = "gfx950", root: Optional[str] = None, stri
                 "prepare_s": round(time.perf_counter() - t0, 3)}
         with open(os.path.join(tmp, "slim.json"), "w", encoding="utf-8") as fh:
             json.dump(meta, fh, indent=1)
+        if verify_with_gpu:  # before the entry exists under its final name
+            meta = _record_verified(tmp, verify(tmp))
+            meta["dir"] = out
         try:
             os.rename(tmp, out)
         except OSError:
@@ -326,26 +413,24 @@ def main(argv=None) -> int:
     import argparse
 
     ap = argparse.ArgumentParser(description="Prepare the single-target (gfx950) RCCL runtime directory")
-    ap.add_argument("--source", default="", help="directory holding librccl.so (default: the PyTorch-ROCm lib/ "
-                                                 "the agent runs on, else /opt/rocm/lib)")
+    ap.add_argument("--source", default="", help="directory holding librccl.so (default: /opt/rocm/lib)")
     ap.add_argument("--arch", default="gfx950")
     ap.add_argument("--root", default="", help="cache root (default: TK_RCCL_SLIM_DIR or the node default)")
-    ap.add_argument("--all", action="store_true",
-                    help="the PyTorch-ROCm RCCL (agents) and /opt/rocm's (node tools, linked as <root>/rocm)")
+    ap.add_argument("--no-verify", action="store_true", help="skip the GPU verification (the copy is then unusable)")
+    ap.add_argument("--verify-child", default="", help=argparse.SUPPRESS)
     args = ap.parse_args(argv)
-    from .native import SYSTEM_LIB_DIR, _torch_lib_dir
+    if args.verify_child:
+        return _verify_child(args.verify_child)
+    from .native import SYSTEM_LIB_DIR
 
-    if args.all:
-        sources = [d for d in (_torch_lib_dir(), SYSTEM_LIB_DIR) if d and os.path.exists(os.path.join(d, "librccl.so"))]
-    else:
-        sources = [args.source or _torch_lib_dir() or (SYSTEM_LIB_DIR if os.path.exists(SYSTEM_LIB_DIR) else "")]
+    sources = [args.source or (SYSTEM_LIB_DIR if os.path.exists(SYSTEM_LIB_DIR) else "")]
     if not any(sources):
-        print(json.dumps({"error": "no RCCL source directory (install PyTorch-ROCm or pass --source)"}))
+        print(json.dumps({"error": "no RCCL source directory (pass --source)"}))
         return 2
     rc = 0
     for src in sources:
         try:
-            meta = prepare(src, args.arch, args.root or None)
+            meta = prepare(src, args.arch, args.root or None, verify_with_gpu=not args.no_verify)
             if os.path.realpath(src) == os.path.realpath(SYSTEM_LIB_DIR):
                 meta["link"] = link(os.path.dirname(str(meta["dir"])), "rocm", str(meta["dir"]))
         except (SlimError, OSError) as exc:

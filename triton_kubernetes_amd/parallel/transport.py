@@ -66,7 +66,8 @@ class Transport:
     def spawn(self, host: HostRef, script: str) -> subprocess.Popen:
         """Start ``bash -c script`` on the host and return at once; stdout is a text pipe the
         caller reads while it runs (the process-mode RCCL gate needs rank 0's first line
-        before the other nodes can start)."""
+        before the other nodes can start).  stdin is a pipe the caller closes when done:
+        the script may watch it to learn that its caller went away."""
         raise NotImplementedError
 
 
@@ -133,7 +134,9 @@ class SSHTransport(Transport):
         self.run_script(host, f"chmod {mode:o} {shlex.quote(remote_path)}\n")
 
     def spawn(self, host: HostRef, script: str) -> subprocess.Popen:
-        return subprocess.Popen(self.ssh_argv(host, "bash -c " + shlex.quote(script)), stdin=subprocess.DEVNULL,
+        # stdin stays an open pipe: the remote side sees EOF when the caller closes it or
+        # this ssh client dies (readiness/process_gate.py's node-side watchdog)
+        return subprocess.Popen(self.ssh_argv(host, "bash -c " + shlex.quote(script)), stdin=subprocess.PIPE,
                                 stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True)
 
 
@@ -170,7 +173,7 @@ class LocalTransport(Transport):
         os.chmod(remote_path, mode)
 
     def spawn(self, host: HostRef, script: str) -> subprocess.Popen:
-        return subprocess.Popen(["bash", "-c", script], stdin=subprocess.DEVNULL, stdout=subprocess.PIPE,
+        return subprocess.Popen(["bash", "-c", script], stdin=subprocess.PIPE, stdout=subprocess.PIPE,
                                 stderr=subprocess.PIPE, text=True, env=self._env())
 
 

@@ -17,7 +17,16 @@ the gate runs one ``rccl-ready --cluster`` process per node over the host transp
 
 Each node's ``/etc/rccl/rccl.env`` (discovered RDMA ports, per-node overrides, written by
 the bootstrap) is sourced first, so the gate runs with the environment GPU pods get.
-A deadline bounds the whole gate; on expiry or the first failure every process is killed.
+A node that opted in to the verified single-target RCCL (``rccl-ready-slim`` present,
+``terraform/scripts.py``) runs the tool through that wrapper.
+
+A deadline bounds the whole gate; on expiry or the first failure every process is killed
+-- on the node too: the tool runs under a watchdog that reads the channel's stdin, which
+stays open while the gate holds it; when the gate ends (or its ``ssh`` client is killed,
+which closes the channel: ``ssh`` without a pty sends the remote side no SIGHUP) the
+watchdog sees EOF and kills the ranks, so an aborted gate never leaves a node's GPUs held
+by an orphaned ``rccl-ready`` blocked in communicator init.  The tool's own timeout is the
+init budget (``INIT_TIMEOUT_S``), not the whole readiness budget.
 
 A cluster that mixes both kinds of MI355X nodes gets ONE communicator too: agent hosts
 (``agent+URL`` addresses) join through their API (``/v1/rccl-prepare`` with the unique id,
@@ -41,16 +50,23 @@ from ..parallel.transport import HostRef
 from ..utils.trace import span
 
 ENV_FILE = "/etc/rccl/rccl.env"
+INIT_TIMEOUT_S = 300.0  # a node's rccl-ready gives up on communicator init after this
 
 
 def gate_script(tools_dir: str, world: int, rank_base: int, ngpus: int, sizes: Sequence[int], iters: int,
                 uid: Optional[str], min_busbw: float = 0.0, timeout_s: float = 600.0, env_file: str = ENV_FILE) -> str:
-    argv = [os.path.join(tools_dir, "rccl-ready"), "--cluster", "--world", str(world), "--rank-base", str(rank_base),
+    args = ["--cluster", "--world", str(world), "--rank-base", str(rank_base),
             "--ngpus", str(ngpus), "--max-mib", str(max(1, max(sizes) >> 20)), "--iters", str(iters),
-            "--timeout-s", str(int(timeout_s)), "--min-busbw", str(min_busbw)]
-    argv += ["--uid", uid] if uid else ["--uid-out"]
+            "--timeout-s", str(int(max(1.0, min(timeout_s, INIT_TIMEOUT_S)))), "--min-busbw", str(min_busbw)]
+    args += ["--uid", uid] if uid else ["--uid-out"]
+    tool, slim = shlex.quote(os.path.join(tools_dir, "rccl-ready")), shlex.quote(os.path.join(tools_dir, "rccl-ready-slim"))
     return (f"set -a; [ -r {shlex.quote(env_file)} ] && . {shlex.quote(env_file)}; set +a; "
-            f"exec {' '.join(shlex.quote(a) for a in argv)}")
+            f"t={tool}; [ -x {slim} ] && t={slim}; exec 3<&0; "
+            f'"$t" {" ".join(shlex.quote(a) for a in args)} </dev/null & pid=$!; '
+            # watchdog: the gate's end closes our stdin -> take the ranks down
+            "( cat <&3 >/dev/null 2>&1; kill -TERM $pid 2>/dev/null; sleep 3; kill -KILL $pid 2>/dev/null ) "
+            ">/dev/null 2>&1 & w=$!; "
+            "exec 3<&-; wait $pid; rc=$?; kill $w 2>/dev/null; exit $rc")
 
 
 class ProcessGate:
@@ -168,6 +184,11 @@ class ProcessGate:
                 if p.poll() is None:
                     p.kill()
                     p.wait()
+                if p.stdin is not None:  # EOF to the node-side watchdog (see module doc)
+                    try:
+                        p.stdin.close()
+                    except OSError:
+                        pass
             if not ok_run and uid_b64 is not None:
                 for i in range(len(self.hosts)):  # release agents' pending communicators
                     if self._is_agent(i):

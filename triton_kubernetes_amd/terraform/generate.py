@@ -149,6 +149,7 @@ VAR_VALIDATIONS = {
     "k8s_network_provider": ('contains(["calico", "flannel", "canal", "weave"], var.k8s_network_provider)',
                              "k8s_network_provider must be one of calico, flannel, canal, weave."),
     "gpu_burnin": ('contains(["quick", "full", "off"], var.gpu_burnin)', "gpu_burnin must be quick, full or off."),
+    "rccl_slim": ('contains(["on", "off"], var.rccl_slim)', "rccl_slim must be on or off."),
     "rancher_host_labels": ('length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], '
                             'keys(var.rancher_host_labels)[0])',
                             "rancher_host_labels must hold exactly one of worker, etcd or control."),
@@ -1188,7 +1189,11 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
         Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)"),
         Var("gpu_link_min_frac", "0.5",
-            "fail the node when a GPU pair's peer copy bandwidth is below this fraction of the node median")],
+            "fail the node when a GPU pair's peer copy bandwidth is below this fraction of the node median"),
+        Var("rccl_slim", "off",
+            "on: build a single-target (gfx950) copy of the node's librccl for faster cold communicator init, "
+            "verify it with a one-rank all-reduce, and run rccl-ready on it while it matches the installed "
+            "librccl (a modified vendor binary: off by default)")],
         ROLE_LOCAL + f'''
 
 locals {{
@@ -1223,6 +1228,7 @@ resource "terraform_data" "install_mi355x_node" {{
       rccl_env_file                      = local.rccl_env_file
       rccl_min_busbw                     = var.rccl_min_busbw
       gpu_link_min_frac                  = var.gpu_link_min_frac
+      rccl_slim                          = var.rccl_slim
     }})]
   }}
 }}

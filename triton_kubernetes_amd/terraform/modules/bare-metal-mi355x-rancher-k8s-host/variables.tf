@@ -129,3 +129,14 @@ variable "gpu_link_min_frac" {
   type        = string
   default     = "0.5"
 }
+
+variable "rccl_slim" {
+  description = "on: build a single-target (gfx950) copy of the node's librccl for faster cold communicator init, verify it with a one-rank all-reduce, and run rccl-ready on it while it matches the installed librccl (a modified vendor binary: off by default)"
+  type        = string
+  default     = "off"
+
+  validation {
+    condition     = contains(["on", "off"], var.rccl_slim)
+    error_message = "rccl_slim must be on or off."
+  }
+}

@@ -198,13 +198,16 @@ sudo docker run -d --privileged --restart=unless-stopped --net=host \
   --ca-checksum '${rancher_cluster_ca_checksum}' --${rancher_node_role}${extra_agent_args}
 """
 
-# Single-target RCCL, shell form of ops/rccl_slim.py (nodes delivered by SSH / Terraform):
-# a copy of librccl whose .hip_fatbin holds only the gfx950 code object, uncompressed and
-# without DWARF, so a cold process's first communicator init skips decompressing every GPU
-# target (~0.5 s instead of ~1.7 s on /opt/rocm 7.2).  rccl-ready's search path looks in
-# <root>/rocm first: a DT_RPATH (--disable-new-dtags), which ROCm hosts' usual
-# LD_LIBRARY_PATH=/opt/rocm/lib cannot override the way it overrides a RUNPATH.  Written without brace expansions: the same text is a Terraform
-# templatefile fragment and plain bash.
+# Single-target RCCL, shell form of ops/rccl_slim.py (nodes delivered by SSH / Terraform).
+# OPT-IN (rccl_slim = "on"): a copy of librccl whose .hip_fatbin holds only the gfx950 code
+# object, uncompressed and without DWARF, so a cold process's first communicator init skips
+# decompressing every GPU target.  It is a modified vendor binary, so by default nothing
+# uses it: rccl-ready loads /opt/rocm/lib/librccl.so (RUNPATH).  When enabled,
+# tk_rccl_slim_enable verifies the copy with a one-rank all-reduce that must map it, and
+# only then installs the rccl-ready-slim wrapper, which uses the copy while it still
+# matches the installed librccl (a ROCm upgrade falls back to the installed RCCL with a
+# warning).  Written without brace expansions: the same text is a Terraform templatefile
+# fragment and plain bash.
 RCCL_SLIM_ROOT = "/var/lib/triton-kubernetes/rccl-slim"
 RCCL_SLIM_FN = r"""tk_rccl_slim() { # <cache root> <rocm dir>: prints the slim runtime directory
   local root=$1 rocm=$2 llvm real key out tmp sec off size nb f n
@@ -255,7 +258,37 @@ RCCL_SLIM_FN = r"""tk_rccl_slim() { # <cache root> <rocm dir>: prints the slim r
     printf '{"source": "%s", "arch": "gfx950", "form": "shell", "bundle_bytes": %s}\n' "$real" $nb > $tmp/slim.json
     mv -T $tmp $out 2>/dev/null || rm -rf $tmp
   fi
-  ln -sfn $out $root/rocm.tmp && mv -T $root/rocm.tmp $root/rocm && echo $out
+  echo $out
+}"""
+
+# written next to the node tools by tk_rccl_slim_enable: the verified copy and its source
+RCCL_SLIM_ENV = "rccl-slim.env"
+RCCL_SLIM_ENABLE_FN = r"""tk_rccl_slim_enable() { # <cache root> <rocm dir> <tools dir>: opt-in, verified before use
+  local dir real
+  rm -f $3/""" + RCCL_SLIM_ENV + r""" $3/rccl-ready-slim
+  dir=$(tk_rccl_slim $1 $2) || return 1
+  real=$(readlink -f $2/lib/librccl.so) || return 1
+  if ! LD_LIBRARY_PATH=$dir $3/rccl-ready --ngpus 1 --max-mib 4 --iters 2 --expect-rccl $dir/librccl.so >/dev/null; then
+    echo "rccl slim: $dir failed its one-rank verified all-reduce; not enabled" >&2; return 1
+  fi
+  printf 'TK_RCCL_SLIM_DIR=%s\nTK_RCCL_SLIM_SOURCE=%s\nTK_RCCL_SLIM_KEY=%s\n' $dir "$real" "$(stat -c %s-%Y "$real")" \
+    > $3/""" + RCCL_SLIM_ENV + r"""
+  cat > $3/rccl-ready-slim <<'TK_SLIM_EOF'
+#!/bin/sh
+# rccl-ready on the verified single-target RCCL copy while it matches the installed librccl
+. "$(dirname "$0")/""" + RCCL_SLIM_ENV + r""""
+rocm=/opt/rocm; [ -n "$ROCM_PATH" ] && rocm=$ROCM_PATH
+real=$(readlink -f "$rocm/lib/librccl.so")
+if [ "$real" = "$TK_RCCL_SLIM_SOURCE" ] && [ "$(stat -c %s-%Y "$real")" = "$TK_RCCL_SLIM_KEY" ]; then
+  if [ -n "$LD_LIBRARY_PATH" ]; then LD_LIBRARY_PATH=$TK_RCCL_SLIM_DIR:$LD_LIBRARY_PATH; else LD_LIBRARY_PATH=$TK_RCCL_SLIM_DIR; fi
+  export LD_LIBRARY_PATH
+else
+  echo "rccl-ready-slim: librccl changed since the single-target copy was verified; using the installed RCCL (re-run the rccl_slim step)" >&2
+fi
+exec "$(dirname "$0")/rccl-ready" "$@"
+TK_SLIM_EOF
+  chmod 755 $3/rccl-ready-slim
+  echo $dir
 }"""
 
 INSTALL_MI355X_NODE = r"""#!/bin/bash
@@ -280,9 +313,17 @@ build() { # name, compiler, flags...
 }
 build amdgpu-topo-labeller g++ -O2 -std=c++17 -DTK_TOPO_MAIN -DTK_TOPO_AMDSMI -I$ROCM/include $S/tk_topo.cpp -L$ROCM/lib -lamd_smi -Wl,-rpath,$ROCM/lib
 build gpu-burnin $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip
-build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl -Wl,--disable-new-dtags,-rpath,""" + RCCL_SLIM_ROOT + r"""/rocm:$ROCM/lib
-""" + RCCL_SLIM_FN + r"""
-sudo bash -c "$(declare -f tk_rccl_slim); tk_rccl_slim """ + RCCL_SLIM_ROOT + r""" $ROCM" >/dev/null || echo 'rccl slim: skipped, the node tools load the full RCCL bundle' >&2
+build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl -Wl,-rpath,$ROCM/lib
+RCCL_READY=$T/rccl-ready
+sudo rm -f $T/""" + RCCL_SLIM_ENV + r""" $T/rccl-ready-slim
+%{ if rccl_slim == "on" ~}
+""" + RCCL_SLIM_FN + "\n" + RCCL_SLIM_ENABLE_FN + r"""
+if sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enable """ + RCCL_SLIM_ROOT + r""" $ROCM $T" >/dev/null; then
+  RCCL_READY=$T/rccl-ready-slim
+else
+  echo 'rccl slim: not enabled, the node tools load the installed RCCL' >&2
+fi
+%{ endif ~}
 $T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/dev/null
 $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
 sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels
@@ -298,7 +339,7 @@ TK_RCCL_EOF
 $T/gpu-burnin --p2p --min-link-frac ${gpu_link_min_frac} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
 cat /tmp/tk-link-labels | sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels >/dev/null
 set -a; . /etc/rccl/rccl.env; set +a
-$T/rccl-ready --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
+$RCCL_READY --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
 %{ endif ~}
 labels=$(cat /etc/triton-kubernetes/gpu-labels $([ -r /etc/triton-kubernetes/gpu-burnin-labels ] && echo /etc/triton-kubernetes/gpu-burnin-labels) | sed 's/^/--label /' | tr '\n' ' ')
 """ + DOCKER_INSTALL + r"""
