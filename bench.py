@@ -81,13 +81,16 @@ def parse_args():
 
 
 class AgentProc:
-    """One node agent in its own process (what systemd runs on a real node)."""
+    """One node agent in its own process (what systemd runs on a real node), serving TLS
+    with the credentials its cluster manager issued for its address (node/security.py)."""
 
-    def __init__(self, name: str, devices, token_file: str, root: str, synthetic: int = 0):
-        with open(token_file, "r", encoding="utf-8") as fh:
+    def __init__(self, name: str, devices, creds_dir: str, address: str, root: str, synthetic: int = 0,
+                 client_ctx=None):
+        with open(os.path.join(creds_dir, "agent-token"), "r", encoding="utf-8") as fh:
             self.token = fh.read().strip()
+        self.client_ctx = client_ctx
         argv = [sys.executable, "-u", "-m", "triton_kubernetes_amd.node.agent", "--mode", "sim",
-                "--listen", "127.0.0.1:0", "--name", name, "--token-file", token_file, "--root", root,
+                "--listen", f"{address}:0", "--name", name, "--credentials", creds_dir, "--root", root,
                 "--devices", ",".join(str(d) for d in devices)]
         if synthetic:
             argv += ["--synthetic-gpus", str(synthetic)]
@@ -132,7 +135,7 @@ class AgentProc:
             req = urllib.request.Request(self.url + "/v1/shutdown", data=b"{}", method="POST",
                                          headers={"X-TK-Agent-Token": self.token,
                                                   "Content-Type": "application/json"})
-            urllib.request.urlopen(req, timeout=10).read()
+            urllib.request.urlopen(req, timeout=10, context=self.client_ctx).read()
         except OSError:
             self.proc.send_signal(signal.SIGTERM)
 
@@ -151,17 +154,20 @@ class AgentProc:
 class InprocAgent:
     """Same interface as :class:`AgentProc`, the agent living in this process."""
 
-    def __init__(self, name: str, devices, token: str, root: str, synthetic: int = 0):
+    def __init__(self, name: str, devices, creds_dir: str, address: str, root: str, synthetic: int = 0):
         from triton_kubernetes_amd.node.agent import NodeAgent
+        from triton_kubernetes_amd.node.security import read_credentials
 
+        creds = read_credentials(creds_dir)
         self.name = name
-        self.agent = NodeAgent(name=name, mode="sim", devices=list(devices), token=token, root=root)
+        self.agent = NodeAgent(name=name, mode="sim", devices=list(devices), token=creds["token"], root=root,
+                               policy=creds["policy"])
         if synthetic:
             from triton_kubernetes_amd.node.labels import synthetic_topology
 
             self.agent.topology_override = synthetic_topology(synthetic)
             self.agent.burnin_override = lambda dev, level: {"ok": True, "simulated": True, "level": level}
-        self.url = self.agent.serve()
+        self.url = self.agent.serve(address, ssl_context=creds["ssl_context"])
 
     def wait_url(self, timeout: float = 0.0) -> str:
         return self.url
@@ -214,7 +220,6 @@ def main() -> int:
     from triton_kubernetes_amd import workflows as wf
     from triton_kubernetes_amd.backend import LocalBackend
     from triton_kubernetes_amd.config import Context, Settings
-    from triton_kubernetes_amd.parallel.transport import AgentTransport
     from triton_kubernetes_amd.utils.trace import TRACER, span
 
     slim_meta = None
@@ -230,23 +235,46 @@ def main() -> int:
             dist.barrier()
         os.environ["TK_HIP_RUNTIME"] = "slim"
 
-    token = os.environ.get("TK_BENCH_TOKEN", "bench-token-0123456789")
     work = tempfile.mkdtemp(prefix=f"tk-bench-r{rank}-")
-    token_file = os.path.join(work, "agent-token")
-    with open(token_file, "w", encoding="utf-8") as fh:
-        fh.write(token)
     synthetic = gpus_per_worker if args.sim_gpu else 0
+    fake = backend = ctx_base = None
+    devnull = open(os.devnull, "w", encoding="utf-8")  # workflow output (one handle for every step)
+    if rank == 0:
+        from triton_kubernetes_amd.rancher.fake import FakeRancher
+
+        fake = FakeRancher.for_manager("bench", "bench-admin-pw-0123").start()
+        backend = LocalBackend(os.path.join(work, "state"))
+        ctx_base = {"backend_provider": "local", "executor": "direct", "non-interactive": True,
+                    "cluster_manager": "bench"}
+        mgr = dict(ctx_base, manager_cloud_provider="baremetal", name="bench", rancher_admin_password="bench-admin-pw-0123",
+                   host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="~/.ssh/id_rsa")
+        wf.new_manager(Context(settings=Settings(mgr, env={}), out=devnull), backend)
+
+    # node enrollment (install time, before the timed region): the manager's agent PKI
+    # issues each node a TLS certificate for its address, its own token and the agent-image
+    # allow-list.  Every simulated node gets its own loopback address.
+    from triton_kubernetes_amd.node.security import AgentPKI, load_pki
+
+    pki_doc = [load_pki(backend, "bench").to_json() if rank == 0 else None]
+    if distributed:
+        dist.broadcast_object_list(pki_doc, src=0)
+    pki = AgentPKI.from_json(pki_doc[0])
+    addresses = {name: f"127.1.{rank}.{2 + k}" for k, (name, _) in enumerate(mine)}
+    if rank == 0:
+        addresses["control-plane"] = "127.1.0.250"
+    creds = {}
+    for name, addr in addresses.items():
+        creds[name] = os.path.join(work, "creds", name)
+        pki.issue(addr, [versions.AGENT_IMAGE]).write(creds[name])
+    client_ctx = pki.client_context()
 
     def start_agents(tag: str):
+        names = [(name, devs) for name, devs in mine] + ([("control-plane", [])] if rank == 0 else [])
         if args.agents == "inproc":
-            procs = [InprocAgent(name, devs, token, os.path.join(work, tag, name), synthetic) for name, devs in mine]
-            if rank == 0:
-                procs.append(InprocAgent("control-plane", [], token, os.path.join(work, tag, "cp")))
-            return procs
-        procs = [AgentProc(name, devs, token_file, os.path.join(work, tag, name), synthetic) for name, devs in mine]
-        if rank == 0:
-            procs.append(AgentProc("control-plane", [], token_file, os.path.join(work, tag, "cp")))
-        return procs
+            return [InprocAgent(name, devs, creds[name], addresses[name], os.path.join(work, tag, name),
+                                synthetic if devs else 0) for name, devs in names]
+        return [AgentProc(name, devs, creds[name], addresses[name], os.path.join(work, tag, name),
+                          synthetic if devs else 0, client_ctx) for name, devs in names]
 
     runtimes = set()
 
@@ -258,19 +286,6 @@ def main() -> int:
             dist.all_gather_object(every, local)
             local = [x for part in every for x in part]
         return dict(local)
-
-    fake = backend = ctx_base = None
-    devnull = open(os.devnull, "w", encoding="utf-8")  # workflow output (one handle for every step)
-    if rank == 0:
-        from triton_kubernetes_amd.rancher.fake import FakeRancher
-
-        fake = FakeRancher.for_manager("bench", "bench-admin-pw-0123").start()
-        backend = LocalBackend(os.path.join(work, "state"))
-        ctx_base = {"backend_provider": "local", "executor": "direct", "agent_token": token,
-                    "non-interactive": True, "cluster_manager": "bench"}
-        mgr = dict(ctx_base, manager_cloud_provider="baremetal", name="bench", rancher_admin_password="bench-admin-pw-0123",
-                   host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="~/.ssh/id_rsa")
-        wf.new_manager(Context(settings=Settings(mgr, env={}), out=devnull), backend)
 
     def create(i: int, urls) -> dict:
         """rank 0: one ``create cluster --wait`` against the agents at ``urls``."""
@@ -289,8 +304,8 @@ def main() -> int:
                         "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": gpu_hosts,
                         "gpu": "mi355x", "gpu_count": gpus_per_worker, "gpu_burnin": args.burnin},
                    ])
+        # the CLI's own agent transport: per-node tokens + TLS against the manager's CA
         ctx = Context(settings=Settings(cfg, env={}), out=devnull)
-        ctx.extras["agent_transport"] = AgentTransport(token=token)
         wf.new_cluster(ctx, backend)
         out = {}
         report = ctx.extras.get("last_apply")

@@ -19,6 +19,7 @@ import fcntl
 import os
 import shutil
 import tempfile
+import threading
 import time
 from typing import Any, Iterator, List, Optional, Tuple
 
@@ -49,6 +50,7 @@ class LocalBackend(Backend):
     def __init__(self, root: Optional[str] = None):
         root = root or os.environ.get("TRITON_KUBERNETES_HOME") or DEFAULT_ROOT
         self.root = os.path.abspath(os.path.expanduser(root))
+        self._held = threading.local()
         try:
             os.makedirs(self.root, exist_ok=True)
         except OSError as exc:
@@ -99,9 +101,20 @@ class LocalBackend(Backend):
 
     @contextlib.contextmanager
     def lock(self, name: str, timeout: float = 30.0) -> Iterator[None]:
-        # The lock lives next to (not inside) the manager directory so that a
-        # lock taken before the first persist does not make the name appear in
-        # states() (which lists directories).
+        # Re-entrant within a thread (a workflow holds it around the executor, which may
+        # take it again, e.g. to create the manager's node-agent PKI).  The lock lives next
+        # to (not inside) the manager directory so that a lock taken before the first
+        # persist does not make the name appear in states() (which lists directories).
+        held = getattr(self._held, "names", None)
+        if held is None:
+            held = self._held.names = {}
+        if held.get(name):
+            held[name] += 1
+            try:
+                yield
+            finally:
+                held[name] -= 1
+            return
         lock_path = os.path.join(self.root, f".{name}.lock")
         fd = os.open(lock_path, os.O_CREAT | os.O_RDWR, 0o600)
         deadline = time.monotonic() + timeout
@@ -116,7 +129,11 @@ class LocalBackend(Backend):
                     if time.monotonic() > deadline:
                         raise BackendError(f"timed out waiting for the state lock of '{name}' ({lock_path})")
                     time.sleep(0.05)
-            yield
+            held[name] = 1
+            try:
+                yield
+            finally:
+                held.pop(name, None)
         finally:
             with contextlib.suppress(OSError):
                 fcntl.flock(fd, fcntl.LOCK_UN)

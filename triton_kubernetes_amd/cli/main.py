@@ -6,6 +6,7 @@
     triton-kubernetes version
 
 Additions: ``wait cluster`` (the readiness waiter on an existing cluster),
+``credentials node`` (a node agent's TLS certificate, token and image allow-list),
 ``backup cluster`` / ``restore cluster`` (namespace backup to the state backend
 or S3 — advertised by the reference README, never implemented there),
 ``gpu …`` (the native MI355X probes), ``agent`` (the node agent) and
@@ -43,10 +44,11 @@ VALID = {
     "restore": ["cluster"],
     "userdata": ["node"],
     "migrate": ["manager"],
+    "credentials": ["node"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
 _ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
-             "restore": "restore", "userdata": "userdata", "migrate": "migrate"}
+             "restore": "restore", "userdata": "userdata", "migrate": "migrate", "credentials": "credentials"}
 
 
 class ArgError(Exception):
@@ -90,7 +92,9 @@ def build_parser() -> argparse.ArgumentParser:
                        ("restore", "Restore a cluster's namespaces from a backup"),
                        ("userdata", "Print cloud-init user-data that bootstraps a node (PXE/MAAS delivery)"),
                        ("migrate", "Point a cluster manager's document (e.g. one written by the reference's "
-                                   "Terraform 0.11 modules) at this framework's modules")):
+                                   "Terraform 0.11 modules) at this framework's modules"),
+                       ("credentials", "Issue a node agent's TLS certificate, token and image allow-list "
+                                       "(signed by the cluster manager's agent CA)")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
@@ -188,6 +192,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         from ..workflows.migrate import migrate_manager
 
         migrate_manager(ctx, backend)
+    elif command == "credentials":
+        from ..workflows.credentials import node_credentials
+
+        node_credentials(ctx, backend)
     elif command == "wait":
         from ..readiness.waiter import wait_after_create
         from ..workflows.select import select_cluster, select_manager

@@ -61,11 +61,15 @@ class HTTPClient:
     default_headers: Dict[str, str] = field(default_factory=dict)
     retries: int = 2
     retry_backoff: float = 0.2
+    # verify against this context's trust roots (e.g. a node-agent CA) instead of the system's
+    ssl_context: Optional[ssl.SSLContext] = None
 
     def __post_init__(self):
         self._local = threading.local()
 
     def _ssl_context(self) -> ssl.SSLContext:
+        if self.ssl_context is not None:
+            return self.ssl_context
         ctx = ssl.create_default_context()
         if not self.verify_tls:
             ctx.check_hostname = False

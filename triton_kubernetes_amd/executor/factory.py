@@ -5,7 +5,9 @@
 ``terraform_binary``        path/name of the Terraform CLI (default ``terraform``)
 ``terraform_parallelism``   ``-parallelism=N`` for apply/destroy (default: Terraform's 10)
 ``direct_parallelism``      max modules in flight in the DirectExecutor (default 64)
-``agent_token``             shared token for ``agent+http://`` hosts
+``agent_token``             development only: one shared token for every ``agent+`` host
+                            (default: per-node tokens and TLS from the manager's agent
+                            PKI, ``node/security.py``)
 ``rancher_bootstrap``       ``operator`` (default) | ``remote``
 ``node_cleanup``            run the agent cleanup script on destroy (default false)
 ``host_retries``            re-run a failed host bootstrap this many times (default 0)
@@ -41,11 +43,13 @@ def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
         par = s.get_int("terraform_parallelism") if s.is_set("terraform_parallelism") else None
         return TerraformExecutor(binary=tf_bin, parallelism=par)
     if kind == "direct":
-        from ..parallel.transport import AgentTransport, SSHTransport, TransportRouter
+        from ..parallel.transport import SSHTransport, TransportRouter
         from .direct import DirectExecutor
 
+        from ..readiness.waiter import agent_transport_for
+
         transport = ctx.extras.get("transport") or TransportRouter(
-            ssh=SSHTransport(), agent=AgentTransport(token=s.get_string("agent_token")))
+            ssh=SSHTransport(), agent=agent_transport_for(ctx, state.name if state is not None else ""))
         par = s.get_int("direct_parallelism") if s.is_set("direct_parallelism") else 64
         return DirectExecutor(transport=transport, parallelism=par,
                               rancher_bootstrap=s.get_string("rancher_bootstrap") or "operator",

@@ -5,13 +5,16 @@ host (a systemd unit on real nodes; a fresh process per simulated node and step 
 ``bench.py``; an in-process object in tests) and executes :class:`~.plan.BootstrapPlan`
 steps natively.
 
-Security model: the agent never executes shell text it receives.  A plan's
-``shell`` fields are only for the SSH renderer; the agent dispatches on the
-step ``action`` and runs fixed, agent-side argv lists built from *validated*
-parameters (hostname, image reference, registry).  Every request must carry
-the agent's token (``X-TK-Agent-Token``); the agent refuses to start without
-one, generating a random token when none is given, and listens on 127.0.0.1
-unless told otherwise.
+Security model (``node/security.py``): the agent never executes shell text it
+receives.  A plan's ``shell`` fields are only for the SSH renderer; the agent
+dispatches on the step ``action`` and runs fixed, agent-side argv lists built from
+*validated* parameters (hostname, image reference, registry).  Off loopback it
+serves only TLS, with a certificate for the node's address signed by its cluster
+manager's CA; plain HTTP needs ``--insecure-local`` and binds loopback only.  Every
+request must carry the node's own token (``X-TK-Agent-Token``, derived per node
+from the manager secret; a random one when none is given).  A plan whose agent
+step names an image outside the node's allow-list (:class:`AgentPolicy`, set by
+the manager at enrollment) is refused before any step runs (HTTP 403).
 
 Modes:
 
@@ -57,6 +60,7 @@ from ..utils.httpserver import Server as HTTPServer
 from ..utils.trace import span
 from .labels import burnin_labels, labels_from_topology, link_labels
 from .plan import BootstrapPlan, Step
+from .security import AgentPolicy, is_loopback
 
 MODES = ("sim", "exec")
 _HOSTNAME_RE = re.compile(r"^[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?(\.[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?)*$")
@@ -112,12 +116,18 @@ class NodeAgent:
     token: str = ""
     topology_override: Optional[Dict[str, Any]] = None
     burnin_override: Optional[Callable[[int, str], Dict[str, Any]]] = None
+    # the Rancher agent images this node may run (default: the pinned agent image)
+    policy: Optional[AgentPolicy] = None
 
     def __post_init__(self):
         if self.mode not in MODES:
             raise ValueError(f"mode must be one of {MODES}")
         if not self.token:
             self.token = secrets.token_urlsafe(24)
+        if self.policy is None:
+            from ..versions import AGENT_IMAGE
+
+            self.policy = AgentPolicy([AGENT_IMAGE])
         self.lock = threading.Lock()
         self._gate_mu = threading.Lock()
         # long-lived workers for topology prefetch and per-GPU burn-in: no thread is created
@@ -149,7 +159,15 @@ class NodeAgent:
         return full
 
     # --- plan execution ---------------------------------------------------------------------
+    def refused_images(self, plan: BootstrapPlan) -> List[str]:
+        """Agent-step images of ``plan`` outside this node's allow-list."""
+        return [str(s.params.get("image", "")) for s in plan.steps
+                if s.action == "agent" and not self.policy.allows(str(s.params.get("image", "")))]
+
     def run_plan(self, plan: BootstrapPlan) -> Dict[str, Any]:
+        bad = self.refused_images(plan)
+        if bad:
+            raise PermissionError(f"image {bad[0]!r} is not in this node's allow-list")
         results: List[StepResult] = []
         ctx: Dict[str, Any] = {"labels": {}, "capacity": {}}
         t_plan = time.perf_counter()
@@ -620,7 +638,12 @@ class NodeAgent:
                 cv.notify()
 
     # --- HTTP server ----------------------------------------------------------------------------
-    def serve(self, host: str = "127.0.0.1", port: int = 0) -> str:
+    def serve(self, host: str = "127.0.0.1", port: int = 0, ssl_context: Any = None) -> str:
+        """Serve the API; HTTPS with ``ssl_context`` (the node's certificate), plain HTTP
+        only on a loopback address."""
+        if ssl_context is None and not is_loopback(host):
+            raise ValueError(f"refusing to serve plain HTTP on {host}: give the agent its TLS credentials "
+                             "(node credentials) or use --insecure-local, which binds loopback only")
         agent = self
         self.warm_native()
 
@@ -628,6 +651,12 @@ class NodeAgent:
             protocol_version = "HTTP/1.1"
 
             def setup(self):
+                # TLS handshake here, on this connection's own thread with a deadline: a
+                # client that connects and stalls cannot block the accept loop
+                if ssl_context is not None:
+                    self.request.settimeout(10.0)
+                    self.request.do_handshake()
+                    self.request.settimeout(None)
                 super().setup()
                 # one request/response per segment: no Nagle/delayed-ACK stalls on keep-alive
                 self.request.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)
@@ -667,7 +696,11 @@ class NodeAgent:
                 try:
                     body = self._body()
                     if path == "/v1/plan":
-                        return self._reply(200, agent.run_plan(BootstrapPlan.from_json(body["plan"])))
+                        plan = BootstrapPlan.from_json(body["plan"])
+                        bad = agent.refused_images(plan)
+                        if bad:
+                            return self._reply(403, {"error": f"image {bad[0]!r} is not in this node's allow-list"})
+                        return self._reply(200, agent.run_plan(plan))
                     if path == "/v1/rccl-uid":
                         return self._reply(200, {"uid": base64.b64encode(agent.new_uid()).decode()})
                     if path == "/v1/rccl-prepare":
@@ -699,11 +732,14 @@ class NodeAgent:
 
         self._server = HTTPServer((host, port), H)
         self._server.daemon_threads = True
+        if ssl_context is not None:
+            self._server.socket = ssl_context.wrap_socket(self._server.socket, server_side=True,
+                                                          do_handshake_on_connect=False)
         # short poll: stop() (server.shutdown) returns within ~20 ms instead of the default 0.5 s
         threading.Thread(target=self._server.serve_forever, kwargs={"poll_interval": 0.02},
                          name=f"agent-{self.name}", daemon=True).start()
         h, p = self._server.server_address[:2]
-        return f"http://{h}:{p}"
+        return f"{'https' if ssl_context is not None else 'http'}://{h}:{p}"
 
     def stop(self) -> None:
         cv = getattr(self, "_idle_cv", None)
@@ -743,7 +779,12 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--listen", default="127.0.0.1:7946")
     ap.add_argument("--mode", default="exec", choices=MODES)
     ap.add_argument("--devices", default="", help="comma-separated local GPU indices")
-    ap.add_argument("--token-file", default="", help="file holding the shared agent token")
+    ap.add_argument("--credentials", default="",
+                    help="the node's credential directory (agent-token, agent.crt/.key, agent-policy.json; "
+                         "`triton-kubernetes credentials node`): serve TLS with the node's token and allow-list")
+    ap.add_argument("--insecure-local", action="store_true",
+                    help="plain HTTP on a loopback address (development, single-box tests)")
+    ap.add_argument("--token-file", default="", help="file holding the token (with --insecure-local)")
     ap.add_argument("--root", default="/")
     ap.add_argument("--name", default="", help="agent name (defaults to the listen host)")
     ap.add_argument("--synthetic-gpus", type=int, default=0,
@@ -751,12 +792,24 @@ def main(argv: Optional[List[str]] = None) -> int:
                          "no burn-in kernels, no RCCL")
     args = ap.parse_args(argv)
     token = ""
-    if args.token_file:
+    ssl_ctx = None
+    policy = None
+    host, _, port = args.listen.rpartition(":")
+    if args.credentials:
+        from .security import read_credentials
+
+        creds = read_credentials(args.credentials)
+        token, ssl_ctx, policy = creds["token"], creds["ssl_context"], creds["policy"]
+    elif not args.insecure_local:
+        ap.error("--credentials DIR is required (or --insecure-local for plain HTTP on loopback)")
+    elif not is_loopback(host):
+        ap.error(f"--insecure-local serves plain HTTP on loopback only, not {host}")
+    if args.token_file and not token:
         with open(args.token_file, "r", encoding="utf-8") as fh:
             token = fh.read().strip()
-    host, _, port = args.listen.rpartition(":")
     devices = [int(d) for d in args.devices.split(",") if d.strip()]
-    agent = NodeAgent(name=args.name or host, mode=args.mode, devices=devices, root=args.root, token=token)
+    agent = NodeAgent(name=args.name or host, mode=args.mode, devices=devices, root=args.root, token=token,
+                      policy=policy)
     if args.synthetic_gpus > 0:
         from .labels import synthetic_topology
 
@@ -770,14 +823,14 @@ def main(argv: Optional[List[str]] = None) -> int:
     # communicator teardowns drained, arena released), then a prompt exit
     signal.signal(signal.SIGTERM, lambda *_: agent.shutdown_requested.set())
     signal.signal(signal.SIGINT, lambda *_: agent.shutdown_requested.set())
-    url = agent.serve(host or "127.0.0.1", int(port))
+    url = agent.serve(host or "127.0.0.1", int(port), ssl_context=ssl_ctx)
     import gc
 
     gc.collect()
     gc.freeze()  # long-lived daemon: keep startup objects out of every later collection
     from ..ops import native
 
-    print(json.dumps({"listening": url, "token_from_file": bool(token),
+    print(json.dumps({"listening": url, "token_from_file": bool(token), "tls": ssl_ctx is not None,
                       "hip_runtime": native._runtime_dir or "not loaded",
                       "startup_ms": dict(getattr(agent, "startup_ms", {}),
                                          main_to_serve=round((time.perf_counter() - t_main) * 1e3, 1))}),

@@ -1,0 +1,200 @@
+"""Node-agent credentials: per-manager CA, per-node tokens, image allow-list.
+
+The node agent runs as root and starts ``docker run --privileged --net=host`` with the
+image a plan names, so its API is a root code-execution surface.  The reference had no
+agent: it delivered the bootstrap over SSH with the operator's key
+(``terraform/modules/bare-metal-rancher-k8s-host/main.tf:24-42``).  The agent keeps an
+equivalent bar:
+
+* **TLS** -- every cluster manager has its own CA (:class:`AgentPKI`, stored in the state
+  backend next to the manager's documents as ``agent-pki.json``, mode 0600 on the local
+  backend).  Each node agent serves a certificate for its address signed by that CA,
+  and the CLI verifies it against that CA only.  Plain HTTP is refused unless the agent
+  runs with ``--insecure-local``, which binds loopback only;
+* **per-node tokens** -- ``HMAC-SHA256(manager secret, "tk-agent-token" | address)``:
+  a token read off one node (or its credentials directory) is useless on every other
+  node, and tokens are never stored: the CLI derives them from the manager secret;
+* **image allow-list** -- the agent runs only the Rancher agent images its credentials
+  list (:class:`AgentPolicy`, written by the manager at enrollment: the manager's pinned
+  agent image, or a digest-pinned one); any other image in a plan is refused (403).
+
+``triton-kubernetes credentials node`` (``agent_address: <node>``) writes a node's credential
+directory (``agent-token``, ``agent.crt``, ``agent.key``, ``ca.crt``,
+``agent-policy.json``) for the node's ``/etc/triton-kubernetes/agent/``.
+"""
+
+import hashlib
+import hmac
+import ipaddress
+import json
+import os
+import secrets
+import ssl
+import tempfile
+import urllib.parse
+from dataclasses import dataclass, field
+from typing import Any, Dict, List, Optional
+
+from ..errors import TKError
+
+PKI_BLOB = "agent-pki.json"
+CRED_FILES = ("agent-token", "agent.crt", "agent.key", "ca.crt", "agent-policy.json")
+DEFAULT_CRED_DIR = "/etc/triton-kubernetes/agent"
+
+
+def agent_address(url_or_host: str) -> str:
+    """The node address a token / certificate is bound to: the host part of an agent URL
+    (``agent+https://10.0.0.5:7946`` -> ``10.0.0.5``), or the host given."""
+    s = url_or_host[len("agent+"):] if url_or_host.startswith("agent+") else url_or_host
+    if "://" in s:
+        host = urllib.parse.urlsplit(s).hostname or ""
+    else:
+        host = s.rsplit(":", 1)[0] if s.count(":") == 1 else s
+    return host.strip("[]").lower()
+
+
+def is_loopback(host: str) -> bool:
+    if host in ("localhost", ""):
+        return True
+    try:
+        return ipaddress.ip_address(host.strip("[]")).is_loopback
+    except ValueError:
+        return False
+
+
+@dataclass
+class AgentPolicy:
+    """What a node agent may run: the Rancher agent images it accepts.  An entry with a
+    digest (``repo@sha256:...``) matches only that digest; a tag entry matches that tag."""
+
+    images: List[str] = field(default_factory=list)
+
+    def allows(self, image: str) -> bool:
+        return image in self.images
+
+    def to_json(self) -> Dict[str, Any]:
+        return {"images": list(self.images)}
+
+    @classmethod
+    def from_json(cls, doc: Dict[str, Any]) -> "AgentPolicy":
+        imgs = doc.get("images") or []
+        if not isinstance(imgs, list) or not all(isinstance(i, str) and i for i in imgs):
+            raise TKError("agent policy: images must be a list of image references")
+        return cls(images=list(imgs))
+
+
+@dataclass
+class NodeCredentials:
+    address: str
+    token: str
+    cert_pem: str
+    key_pem: str
+    ca_pem: str
+    policy: AgentPolicy
+
+    def write(self, directory: str) -> List[str]:
+        os.makedirs(directory, mode=0o700, exist_ok=True)
+        files = {"agent-token": self.token + "\n", "agent.crt": self.cert_pem, "agent.key": self.key_pem,
+                 "ca.crt": self.ca_pem, "agent-policy.json": json.dumps(self.policy.to_json(), indent=1) + "\n"}
+        out = []
+        for name, text in files.items():
+            path = os.path.join(directory, name)
+            fd = os.open(path, os.O_WRONLY | os.O_CREAT | os.O_TRUNC, 0o600)
+            with os.fdopen(fd, "w", encoding="utf-8") as fh:
+                fh.write(text)
+            out.append(path)
+        return out
+
+
+@dataclass
+class AgentPKI:
+    """One cluster manager's agent trust root: CA + the secret node tokens derive from."""
+
+    ca_cert: str
+    ca_key: str
+    secret: bytes
+
+    @classmethod
+    def create(cls, manager: str) -> "AgentPKI":
+        from ..k8s.tls import make_ca
+
+        ca = make_ca(f"triton-kubernetes {manager} node agents")
+        return cls(ca.cert_pem, ca.key_pem, secrets.token_bytes(32))
+
+    def node_token(self, address: str) -> str:
+        mac = hmac.new(self.secret, b"tk-agent-token\0" + agent_address(address).encode(), hashlib.sha256)
+        return "tka1." + mac.hexdigest()
+
+    def issue(self, address: str, images: List[str], extra_names: Optional[List[str]] = None) -> NodeCredentials:
+        from ..k8s.tls import CA, issue
+
+        host = agent_address(address)
+        names = [host] + [n for n in (extra_names or []) if n != host]
+        cert = issue(CA(self.ca_cert, self.ca_key), host, names)
+        return NodeCredentials(host, self.node_token(host), cert.cert_pem, cert.key_pem, self.ca_cert,
+                               AgentPolicy(list(images)))
+
+    def client_context(self) -> ssl.SSLContext:
+        """Verifies agents against this manager's CA only (not the system trust store)."""
+        ctx = ssl.create_default_context(ssl.Purpose.SERVER_AUTH, cadata=self.ca_cert)
+        ctx.check_hostname = True
+        ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+        return ctx
+
+    def to_json(self) -> Dict[str, str]:
+        return {"ca_cert": self.ca_cert, "ca_key": self.ca_key, "secret": self.secret.hex()}
+
+    @classmethod
+    def from_json(cls, doc: Dict[str, str]) -> "AgentPKI":
+        return cls(doc["ca_cert"], doc["ca_key"], bytes.fromhex(doc["secret"]))
+
+
+def load_pki(backend: Any, manager: str, create: bool = True) -> Optional[AgentPKI]:
+    """The manager's agent PKI from the state backend (created on first use)."""
+    try:
+        raw = backend.read_blob(manager, PKI_BLOB)
+    except NotImplementedError:
+        raw = None
+    if raw:
+        return AgentPKI.from_json(json.loads(raw))
+    if not create:
+        return None
+    pki = AgentPKI.create(manager)
+    try:
+        with backend.lock(manager):
+            raw = backend.read_blob(manager, PKI_BLOB)  # another CLI may have won the race
+            if raw:
+                return AgentPKI.from_json(json.loads(raw))
+            backend.write_blob(manager, PKI_BLOB, json.dumps(pki.to_json()).encode())
+    except NotImplementedError:
+        pass
+    return pki
+
+
+def server_context(cert_pem: str, key_pem: str) -> ssl.SSLContext:
+    """TLS context of an agent serving ``cert_pem``."""
+    ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
+    ctx.minimum_version = ssl.TLSVersion.TLSv1_2
+    with tempfile.TemporaryDirectory(prefix="tk-agent-tls-") as d:
+        cp, kp = os.path.join(d, "c.pem"), os.path.join(d, "k.pem")
+        with open(cp, "w", encoding="utf-8") as fh:
+            fh.write(cert_pem)
+        fd = os.open(kp, os.O_WRONLY | os.O_CREAT, 0o600)
+        with os.fdopen(fd, "w", encoding="utf-8") as fh:
+            fh.write(key_pem)
+        ctx.load_cert_chain(cp, kp)
+    return ctx
+
+
+def read_credentials(directory: str) -> Dict[str, Any]:
+    """A node's credential directory -> ``{token, ssl_context, policy}``."""
+    def rd(name: str) -> str:
+        with open(os.path.join(directory, name), "r", encoding="utf-8") as fh:
+            return fh.read()
+
+    return {"token": rd("agent-token").strip(), "ssl_context": server_context(rd("agent.crt"), rd("agent.key")),
+            "policy": AgentPolicy.from_json(json.loads(rd("agent-policy.json")))}
+
+
+__all__ = ["AgentPKI", "AgentPolicy", "NodeCredentials", "load_pki", "server_context", "read_credentials",
+           "agent_address", "is_loopback", "PKI_BLOB", "DEFAULT_CRED_DIR"]

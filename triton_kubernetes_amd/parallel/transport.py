@@ -5,8 +5,9 @@
                      (ControlMaster) and optional ``ProxyJump`` through the
                      bastion — Terraform's ``remote-exec`` equivalent (T16), which
                      in the reference ignores the bastion for managers (Q11)
-``agent``            HTTP to a ``tk-node-agent`` (``agent+http://host:port``
-                     host strings); the agent runs plan steps natively
+``agent``            HTTPS to a ``tk-node-agent`` (``agent+https://host:port``
+                     host strings; ``agent+http://`` on loopback only); the agent
+                     runs plan steps natively
 ``local``            runs the rendered script with ``bash`` on this machine
                      (single-box development)
 ``recording``        test double: records plans/scripts, scripted failures
@@ -178,12 +179,21 @@ class LocalTransport(Transport):
 
 
 class AgentTransport(Transport):
+    """HTTP(S) to node agents (``node/security.py``).  With ``pki`` (the cluster manager's
+    agent CA + secret): each agent's token is derived for its address, ``https`` agents
+    are verified against that CA only, and a plain ``http`` agent is refused unless it is
+    on loopback.  Without ``pki`` (development, in-process tests): the shared ``token``
+    (or ``tokens[url]``)."""
+
     name = "agent"
 
-    def __init__(self, token: str = "", tokens: Optional[Dict[str, str]] = None, timeout: float = 3600):
+    def __init__(self, token: str = "", tokens: Optional[Dict[str, str]] = None, timeout: float = 3600,
+                 pki: Any = None):
         self.token = token
         self.tokens = dict(tokens or {})
         self.timeout = timeout
+        self.pki = pki
+        self._ctx = pki.client_context() if pki is not None else None
         self._clients: Dict[str, HTTPClient] = {}
         self._mu = threading.Lock()
 
@@ -192,8 +202,17 @@ class AgentTransport(Transport):
         with self._mu:
             c = self._clients.get(url)
             if c is None:
-                tok = self.tokens.get(url, self.token)
-                c = HTTPClient(base_url=url, timeout=self.timeout, retries=1,
+                if self.pki is not None:
+                    from ..node.security import agent_address, is_loopback
+
+                    addr = agent_address(url)
+                    if not url.startswith("https://") and not is_loopback(addr):
+                        raise ExecutorError(f"refusing plain HTTP to the node agent at {url}: agents off "
+                                            "loopback serve TLS (agent+https://)")
+                    tok = self.tokens.get(url) or self.pki.node_token(addr)
+                else:
+                    tok = self.tokens.get(url, self.token)
+                c = HTTPClient(base_url=url, timeout=self.timeout, retries=1, ssl_context=self._ctx,
                                default_headers={"X-TK-Agent-Token": tok})
                 self._clients[url] = c
             return c

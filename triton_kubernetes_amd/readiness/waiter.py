@@ -223,12 +223,23 @@ def gate_sizes(settings) -> List[int]:
     return sorted({1 << 20, mib << 20})
 
 
-def agent_transport_for(ctx) -> Any:
+def agent_transport_for(ctx, manager: str = "") -> Any:
+    """The transport to the node agents: the caller's (``ctx.extras``), else one built on
+    the cluster manager's agent PKI (per-node tokens, TLS against the manager's CA;
+    ``node/security.py``).  ``agent_token`` (a shared token, development only) overrides."""
     transport = ctx.extras.get("agent_transport")
     if transport is None:
         from ..parallel.transport import AgentTransport
 
-        transport = AgentTransport(token=ctx.settings.get_string("agent_token"))
+        shared = ctx.settings.get_string("agent_token")
+        backend = ctx.extras.get("backend")
+        if shared or backend is None or not manager:
+            transport = AgentTransport(token=shared)
+        else:
+            from ..node.security import load_pki
+
+            transport = AgentTransport(pki=load_pki(backend, manager))
+        ctx.extras["agent_transport"] = transport
     return transport
 
 
@@ -242,7 +253,7 @@ def early_gate(ctx, state, cluster_key: str) -> Any:
         return None
     from .gate import ClusterGate
 
-    gate = ClusterGate.from_state(state, cluster_key, agent_transport_for(ctx), gate_sizes(s))
+    gate = ClusterGate.from_state(state, cluster_key, agent_transport_for(ctx, state.name), gate_sizes(s))
     return gate.prepare_async() if gate is not None else None
 
 
@@ -253,7 +264,7 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
     client, spec = spec_from_state(state, backend, cluster_key, timeout, s.get_bool("rccl_gate"))
     spec.rccl_sizes = gate_sizes(s)
     mixed = any(h.scheme == "agent" for h in spec.rccl_process_hosts)
-    transport = agent_transport_for(ctx) if spec.rccl_gate and (spec.rccl_hosts or mixed) else None
+    transport = agent_transport_for(ctx, state.name) if spec.rccl_gate and (spec.rccl_hosts or mixed) else None
     if gate is not None and (not spec.rccl_hosts or gate.world != sum(spec.rccl_ndev or [1] * len(spec.rccl_hosts))):
         gate.abort()  # membership changed since it was prepared
         gate = None

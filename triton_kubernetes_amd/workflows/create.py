@@ -50,7 +50,7 @@ def _write_status(backend: Backend, name: str, status: Dict) -> None:
 
 def apply_and_persist(ctx: Context, backend: Backend, state: State, new_modules: List[str]) -> None:
     """Run the executor, then persist; on failure persist + record status (see module doc)."""
-    executor = executor_for(ctx, state)
+    executor = executor_for(ctx, state, backend)
     with backend.lock(state.name):
         try:
             with span("apply", executor=executor.name, modules=len(new_modules)):
@@ -76,6 +76,7 @@ def _apply_then_wait(ctx: Context, backend: Backend, state: State, cluster_key: 
     agent-managed GPU nodes the gate's communicator init is started before the
     apply, so it overlaps node bootstrap (readiness/gate.py)."""
     gate = None
+    ctx.extras["backend"] = backend
     if ctx.settings.get_bool("wait"):
         from ..readiness.waiter import early_gate
 

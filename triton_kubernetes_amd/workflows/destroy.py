@@ -30,7 +30,7 @@ def delete_manager(ctx: Context, backend: Backend) -> None:
         return
     with backend.lock(manager):
         with span("destroy", scope="manager"):
-            executor_for(ctx, state).destroy(state, backend, [])
+            executor_for(ctx, state, backend).destroy(state, backend, [])
         backend.delete_state(manager)
 
 
@@ -53,7 +53,7 @@ def delete_cluster(ctx: Context, backend: Backend) -> None:
     with backend.lock(manager):
         cleanup = _rancher_cleanup_info(ctx, backend, state, key)
         with span("destroy", scope="cluster", targets=len(targets)):
-            executor_for(ctx, state).destroy(state, backend, [f"module.{t}" for t in targets])
+            executor_for(ctx, state, backend).destroy(state, backend, [f"module.{t}" for t in targets])
         for t in targets:
             state.delete_module(t)
         backend.persist_state(state)
@@ -74,7 +74,7 @@ def delete_node(ctx: Context, backend: Backend) -> None:
         return
     with backend.lock(manager):
         with span("destroy", scope="node"):
-            executor_for(ctx, state).destroy(state, backend, [f"module.{node_key}"])
+            executor_for(ctx, state, backend).destroy(state, backend, [f"module.{node_key}"])
         state.delete_module(node_key)
         backend.persist_state(state)
 

@@ -20,7 +20,7 @@ def get_manager(ctx: Context, backend: Backend) -> None:
         raise ConfigError("No cluster managers.")
     manager = select_manager(ctx, managers)
     state = backend.state(manager)
-    executor_for(ctx, state).print_outputs(state, backend, MANAGER_KEY, ctx.out)
+    executor_for(ctx, state, backend).print_outputs(state, backend, MANAGER_KEY, ctx.out)
 
 
 def get_cluster(ctx: Context, backend: Backend) -> None:
@@ -33,4 +33,4 @@ def get_cluster(ctx: Context, backend: Backend) -> None:
     if not clusters:
         raise ConfigError("No clusters.")
     _, key = select_cluster(ctx, clusters, "Cluster to view")
-    executor_for(ctx, state).print_outputs(state, backend, key, ctx.out)
+    executor_for(ctx, state, backend).print_outputs(state, backend, key, ctx.out)

@@ -44,13 +44,16 @@ def select_node(ctx: Context, nodes: Dict[str, str], label: str = "Node to delet
     return hostname, nodes[hostname]
 
 
-def executor_for(ctx: Context, state: Optional[State] = None):
-    """The executor to run a document with.
+def executor_for(ctx: Context, state: Optional[State] = None, backend: Optional[Backend] = None):
+    """The executor to run a document with (``backend``: the manager's state backend,
+    which also holds its node-agent PKI).
 
     ``executor`` setting: ``terraform`` | ``direct`` | ``auto`` (default).  Auto
     uses Terraform when the binary is on ``PATH``; otherwise the native
     DirectExecutor if every module in the document is one it implements.
     """
+    if backend is not None:
+        ctx.extras["backend"] = backend
     if ctx.executor_factory is not None:
         return ctx.executor_factory(ctx)
     from ..executor.factory import build_executor
