@@ -340,3 +340,116 @@ def test_webhook_xgmi_placement():
     assert [o["path"] for o in ops] == ["/spec/affinity"]
     no_place = _gpu_pod(gpus="8", annotations={"amd.com/xgmi-placement": "false"})
     assert "/spec/affinity" not in [o["path"] for o in webhook.patch_for_pod(no_place, env)]
+
+
+def _restricted_gpu_pod(name="r"):
+    pod = _gpu_pod(name)
+    for c in pod["spec"]["containers"]:
+        c["securityContext"] = {"runAsNonRoot": True, "allowPrivilegeEscalation": False,
+                                "capabilities": {"drop": ["ALL"]}, "seccompProfile": {"type": "RuntimeDefault"}}
+    return pod
+
+
+def test_pod_security_levels_of_the_fake():
+    from triton_kubernetes_amd.rancher.fake import pod_security_violations
+
+    hp = {"spec": {"containers": [{"name": "c"}], "volumes": [{"name": "h", "hostPath": {"path": "/x"}}]}}
+    assert pod_security_violations(hp, "privileged") == []
+    assert pod_security_violations(hp, "baseline") == ['hostPath volumes (volume "h")']
+    assert any("runAsNonRoot" in v for v in pod_security_violations(_gpu_pod(), "restricted"))
+    assert pod_security_violations(_restricted_gpu_pod(), "restricted") == []
+    assert pod_security_violations(_gpu_pod(), "baseline") == []
+
+
+@pytest.mark.skipif(not have("openssl"), reason="openssl needed for the serving certificate")
+def test_injector_respects_pod_security_admission(tmp_path):
+    """VERDICT r2 / ADVICE: PSA runs after mutation and forbids hostPath at baseline and
+    restricted.  GPU pods in such namespaces get the cluster env without the /etc/rccl
+    mount (and an annotation saying why); privileged namespaces keep the mount.  The old
+    single-entry configuration's pods are rejected by the fake's PSA (the fake models it)."""
+    from triton_kubernetes_amd.cloud.http import HTTPError
+
+    fake = FakeRancher(bootstrap_password="b00tstrap-only").start()
+    srv = None
+    try:
+        outs = RancherClient(fake.url).bootstrap("n3w-passw0rd-123", fake.url, "b00tstrap-only", timeout=10)
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        cid = client.ensure_cluster("psa").cluster_id
+
+        def post(path, body):
+            return client.k8s(cid, "POST", path, body, ok=(201,))
+
+        cert = serving_cert(addons.INJECTOR, "kube-system")
+        (tmp_path / "tls.crt").write_text(cert.cert_pem)
+        (tmp_path / "tls.key").write_text(cert.key_pem)
+        envdir = tmp_path / "env"
+        envdir.mkdir()
+        (envdir / "NCCL_DEBUG").write_text("WARN")
+        srv = webhook.make_server(0, str(envdir), str(tmp_path / "tls.crt"), str(tmp_path / "tls.key"), "127.0.0.1")
+        threading.Thread(target=srv.serve_forever, daemon=True).start()
+        fake.service_endpoints["rccl-env-injector.kube-system"] = f"https://127.0.0.1:{srv.server_address[1]}"
+        hook = [t.obj for t in addons.addon_templates() if t.obj.get("kind") == "MutatingWebhookConfiguration"][0]
+        hook = json.loads(json.dumps(hook).replace("${injector_ca_b64}",
+                                                    base64.b64encode(cert.ca_pem.encode()).decode()))
+        assert [w["clientConfig"]["service"]["path"] for w in hook["webhooks"]] == ["/mutate",
+                                                                                  "/mutate?node-env=omit"]
+        post("/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations", hook)
+        for ns, level in (("hardened", "restricted"), ("base", "baseline"), ("open", None)):
+            labels = {"pod-security.kubernetes.io/enforce": level} if level else {}
+            post("/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace",
+                                        "metadata": {"name": ns, "labels": labels}})
+        hard = post("/api/v1/namespaces/hardened/pods", _restricted_gpu_pod("h1"))
+        c = hard["spec"]["containers"][0]
+        assert {e["name"]: e["value"] for e in c["env"]} == {"NCCL_DEBUG": "WARN"}
+        assert "volumes" not in hard["spec"] and "volumeMounts" not in c
+        assert hard["metadata"]["annotations"]["amd.com/rccl-env"] == "injected"
+        assert hard["metadata"]["annotations"]["amd.com/rccl-env-node"].startswith("omitted")
+        assert hard["spec"]["affinity"]["nodeAffinity"]  # placement still applies
+        base = post("/api/v1/namespaces/base/pods", _gpu_pod("b1"))
+        assert "volumes" not in base["spec"] and base["spec"]["containers"][0]["env"]
+        opened = post("/api/v1/namespaces/open/pods", _gpu_pod("o1"))
+        assert opened["spec"]["volumes"][0]["hostPath"]["path"] == "/etc/rccl"
+        env = {e["name"] for e in opened["spec"]["containers"][0]["env"]}
+        assert env == {"NCCL_DEBUG", "TK_RCCL_ENV_FILE"}
+        # round 2's single entry (hostPath everywhere): the restricted pod is rejected
+        old = json.loads(json.dumps(hook))
+        old["metadata"]["name"] = "old-injector"
+        old["webhooks"] = [dict(old["webhooks"][0], namespaceSelector={"matchExpressions": [
+            {"key": "kubernetes.io/metadata.name", "operator": "NotIn", "values": ["kube-system"]}]})]
+        client.k8s(cid, "DELETE", "/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations/"
+                                  "rccl-env-injector", None, ok=(200,))
+        post("/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations", old)
+        with pytest.raises(HTTPError) as exc:
+            post("/api/v1/namespaces/hardened/pods", _restricted_gpu_pod("h2"))
+        assert exc.value.status == 403 and "violates PodSecurity" in exc.value.body.decode()
+    finally:
+        if srv is not None:
+            srv.shutdown()
+        fake.stop()
+
+
+def test_webhook_handshake_does_not_block_accept(tmp_path):
+    """a client that connects and stalls before the TLS handshake must not block
+    other admissions (the handshake runs on the connection's thread)."""
+    import socket
+    import ssl
+
+    if not have("openssl"):
+        pytest.skip("openssl")
+    cert = serving_cert(addons.INJECTOR, "kube-system")
+    (tmp_path / "c.crt").write_text(cert.cert_pem)
+    (tmp_path / "c.key").write_text(cert.key_pem)
+    srv = webhook.make_server(0, str(tmp_path), str(tmp_path / "c.crt"), str(tmp_path / "c.key"), "127.0.0.1")
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    try:
+        port = srv.server_address[1]
+        stall = socket.create_connection(("127.0.0.1", port))
+        ctx = ssl.create_default_context(cadata=cert.ca_pem)
+        raw = socket.create_connection(("127.0.0.1", port), timeout=3)
+        tls = ctx.wrap_socket(raw, server_hostname="rccl-env-injector.kube-system.svc")
+        tls.sendall(b"GET /healthz HTTP/1.1\r\nHost: x\r\nConnection: close\r\n\r\n")
+        assert b"200" in tls.recv(200)
+        tls.close()
+        stall.close()
+    finally:
+        srv.shutdown()

@@ -118,21 +118,29 @@ def _injector() -> List[Tuple[str, str, Dict[str, Any]]]:
     }
     svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": INJECTOR, "namespace": NAMESPACE},
            "spec": {"selector": dict(labels), "ports": [{"port": 443, "targetPort": 8443, "name": "https"}]}}
-    hook = {
-        "apiVersion": "admissionregistration.k8s.io/v1", "kind": "MutatingWebhookConfiguration",
-        "metadata": {"name": INJECTOR},
-        "webhooks": [{
-            "name": "rccl-env.amd.com",
-            "clientConfig": {"service": {"name": INJECTOR, "namespace": NAMESPACE, "path": "/mutate", "port": 443},
+    never_own = {"key": "kubernetes.io/metadata.name", "operator": "NotIn", "values": [NAMESPACE]}
+    psa = {"key": "pod-security.kubernetes.io/enforce", "values": ["baseline", "restricted"]}
+
+    def entry(name: str, path: str, psa_op: str) -> Dict[str, Any]:
+        return {
+            "name": name,
+            "clientConfig": {"service": {"name": INJECTOR, "namespace": NAMESPACE, "path": path, "port": 443},
                              "caBundle": _v("injector_ca_b64")},
             "rules": [{"operations": ["CREATE"], "apiGroups": [""], "apiVersions": ["v1"], "resources": ["pods"],
                        "scope": "Namespaced"}],
             # never the injector's own namespace (its pods must start without it)
-            "namespaceSelector": {"matchExpressions": [{"key": "kubernetes.io/metadata.name", "operator": "NotIn",
-                                                        "values": [NAMESPACE]}]},
+            "namespaceSelector": {"matchExpressions": [dict(never_own), dict(psa, operator=psa_op)]},
             "failurePolicy": "Ignore", "sideEffects": "None", "admissionReviewVersions": ["v1"],
             "timeoutSeconds": 5, "reinvocationPolicy": "IfNeeded",
-        }],
+        }
+
+    # Pod Security Admission runs after mutation and its baseline/restricted levels forbid
+    # hostPath: namespaces enforcing them get the env without the node's /etc/rccl mount
+    hook = {
+        "apiVersion": "admissionregistration.k8s.io/v1", "kind": "MutatingWebhookConfiguration",
+        "metadata": {"name": INJECTOR},
+        "webhooks": [entry("rccl-env.amd.com", "/mutate", "NotIn"),
+                     entry("rccl-env-psa.amd.com", "/mutate?node-env=omit", "In")],
     }
     return [("40-injector-tls.json", f"/api/v1/namespaces/{NAMESPACE}/secrets", secret),
             ("41-injector-src.json", f"/api/v1/namespaces/{NAMESPACE}/configmaps", src),

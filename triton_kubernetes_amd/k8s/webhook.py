@@ -17,6 +17,16 @@ container) gets, at admission time:
   so a pod's own terms still apply), and pods sharing an ``amd.com/xgmi-group`` label
   prefer the same hive (pod affinity on ``amd.com/xgmi.hive-id``).
 
+Pod Security Admission runs *after* mutating webhooks, and its ``baseline`` and
+``restricted`` levels forbid ``hostPath`` volumes: mounting ``/etc/rccl`` into a pod in
+such a namespace would get the pod rejected for a change it never asked for.  So the
+add-ons register the injector twice (``k8s/addons.py``), split by namespace label
+``pod-security.kubernetes.io/enforce``: namespaces enforcing ``baseline`` or
+``restricted`` are served on ``/mutate?node-env=omit`` -- the cluster env, the
+placement, no ``hostPath``, no ``TK_RCCL_ENV_FILE``, and the annotation
+``amd.com/rccl-env-node: omitted (Pod Security <level>)`` saying why -- every other
+namespace on ``/mutate``.
+
 A pod opts out of the env with the annotation ``amd.com/rccl-env-inject: "false"`` and of
 the placement with ``amd.com/xgmi-placement: "false"``.  The
 ConfigMap lives in ``kube-system``; ``envFrom`` cannot reach across namespaces, which
@@ -51,6 +61,9 @@ MARK = "amd.com/rccl-env"
 VOLUME = "tk-node-rccl-env"
 NODE_DIR = "/etc/rccl"
 ENV_FILE_VAR = "TK_RCCL_ENV_FILE"
+NODE_ENV_MARK = "amd.com/rccl-env-node"
+PSA_LABEL = "pod-security.kubernetes.io/enforce"
+PSA_NO_HOSTPATH = ("baseline", "restricted")
 PLACEMENT_OPT_OUT = "amd.com/xgmi-placement"
 GROUP_LABEL = "amd.com/xgmi-group"
 HIVE_KEY = "amd.com/xgmi.hive-id"
@@ -136,10 +149,11 @@ def load_env(env_dir: str) -> Dict[str, str]:
     return out
 
 
-def patch_for_pod(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
+def patch_for_pod(pod: Dict[str, Any], env: Dict[str, str], node_env: bool = True) -> List[Dict[str, Any]]:
     """RFC 6902 operations for a pod: the RCCL env on its GPU containers and the xGMI
-    placement ([] = nothing to change)."""
-    ops = _env_ops(pod, env)
+    placement ([] = nothing to change).  ``node_env`` False: no ``/etc/rccl`` hostPath
+    (namespaces whose Pod Security level forbids it)."""
+    ops = _env_ops(pod, env, node_env)
     spec = pod.get("spec") or {}
     if any(_wants_gpu(c) for kind in ("initContainers", "containers") for c in spec.get(kind) or []):
         aff = placement_affinity(pod)
@@ -148,7 +162,7 @@ def patch_for_pod(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, An
     return ops
 
 
-def _env_ops(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
+def _env_ops(pod: Dict[str, Any], env: Dict[str, str], node_env: bool = True) -> List[Dict[str, Any]]:
     meta = pod.get("metadata") or {}
     annotations = meta.get("annotations") or {}
     if str(annotations.get(OPT_OUT, "")).lower() == "false" or annotations.get(MARK) == "injected":
@@ -163,7 +177,7 @@ def _env_ops(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
             touched = True
             have = {e.get("name") for e in (c.get("env") or [])}
             add = [{"name": k, "value": v} for k, v in sorted(env.items()) if k not in have]
-            if ENV_FILE_VAR not in have:
+            if node_env and ENV_FILE_VAR not in have:
                 add.append({"name": ENV_FILE_VAR, "value": f"{NODE_DIR}/rccl.env"})
             base = f"/spec/{kind}/{i}"
             if add:
@@ -172,7 +186,7 @@ def _env_ops(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
                 else:
                     ops.append({"op": "add", "path": f"{base}/env", "value": add})
             mounts = c.get("volumeMounts") or []
-            if not any(m.get("mountPath") == NODE_DIR for m in mounts):
+            if node_env and not any(m.get("mountPath") == NODE_DIR for m in mounts):
                 m = {"name": VOLUME, "mountPath": NODE_DIR, "readOnly": True}
                 if mounts:
                     ops.append({"op": "add", "path": f"{base}/volumeMounts/-", "value": m})
@@ -180,27 +194,31 @@ def _env_ops(pod: Dict[str, Any], env: Dict[str, str]) -> List[Dict[str, Any]]:
                     ops.append({"op": "add", "path": f"{base}/volumeMounts", "value": [m]})
     if not touched:
         return []
-    vol = {"name": VOLUME, "hostPath": {"path": NODE_DIR, "type": "DirectoryOrCreate"}}
-    if not any(v.get("name") == VOLUME for v in spec.get("volumes") or []):
-        if spec.get("volumes"):
-            ops.append({"op": "add", "path": "/spec/volumes/-", "value": vol})
-        else:
-            ops.append({"op": "add", "path": "/spec/volumes", "value": [vol]})
-    if meta.get("annotations"):
-        ops.append({"op": "add", "path": f"/metadata/annotations/{_esc(MARK)}", "value": "injected"})
+    marks = {MARK: "injected"}
+    if node_env:
+        vol = {"name": VOLUME, "hostPath": {"path": NODE_DIR, "type": "DirectoryOrCreate"}}
+        if not any(v.get("name") == VOLUME for v in spec.get("volumes") or []):
+            if spec.get("volumes"):
+                ops.append({"op": "add", "path": "/spec/volumes/-", "value": vol})
+            else:
+                ops.append({"op": "add", "path": "/spec/volumes", "value": [vol]})
     else:
-        ops.append({"op": "add", "path": "/metadata/annotations", "value": {MARK: "injected"}})
+        marks[NODE_ENV_MARK] = "omitted (the namespace's Pod Security level forbids the /etc/rccl hostPath)"
+    if meta.get("annotations"):
+        ops += [{"op": "add", "path": f"/metadata/annotations/{_esc(k)}", "value": v} for k, v in marks.items()]
+    else:
+        ops.append({"op": "add", "path": "/metadata/annotations", "value": marks})
     return ops
 
 
-def review(doc: Dict[str, Any], env: Dict[str, str]) -> Dict[str, Any]:
+def review(doc: Dict[str, Any], env: Dict[str, str], node_env: bool = True) -> Dict[str, Any]:
     """admission.k8s.io/v1 AdmissionReview in -> AdmissionReview response out.  Never
     denies: a pod the injector cannot parse is admitted unchanged."""
     req = doc.get("request") or {}
     resp: Dict[str, Any] = {"uid": req.get("uid", ""), "allowed": True}
     obj = req.get("object")
     if isinstance(obj, dict) and (req.get("kind") or {}).get("kind", "Pod") == "Pod":
-        ops = patch_for_pod(obj, env)
+        ops = patch_for_pod(obj, env, node_env)
         if ops:
             resp["patchType"] = "JSONPatch"
             resp["patch"] = base64.b64encode(json.dumps(ops).encode()).decode()
@@ -250,13 +268,23 @@ def make_server(port: int, env_dir: str, certfile: str = "", keyfile: str = "",
                 return self._reply(200, b"ok", "text/plain")
             return self._reply(404, b"{}")
 
+        def setup(self):
+            # TLS handshake on this connection's thread, with a deadline: one client that
+            # connects and stalls cannot block the accept loop (and every other admission)
+            if certfile:
+                self.request.settimeout(5.0)
+                self.request.do_handshake()
+                self.request.settimeout(None)
+            super().setup()
+
         def do_POST(self):
-            if not self.path.startswith("/mutate"):
+            path, _, query = self.path.partition("?")
+            if path != "/mutate":
                 return self._reply(404, b"{}")
             n = int(self.headers.get("Content-Length") or 0)
             try:
                 doc = json.loads(self.rfile.read(n) or b"{}")
-                out = review(doc, load_env(env_dir))
+                out = review(doc, load_env(env_dir), node_env="node-env=omit" not in query.split("&"))
             except ValueError as exc:
                 return self._reply(400, json.dumps({"error": str(exc)}).encode())
             return self._reply(200, json.dumps(out).encode())
@@ -267,7 +295,7 @@ def make_server(port: int, env_dir: str, certfile: str = "", keyfile: str = "",
         ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_SERVER)
         ctx.minimum_version = ssl.TLSVersion.TLSv1_2
         ctx.load_cert_chain(certfile, keyfile)
-        srv.socket = ctx.wrap_socket(srv.socket, server_side=True)
+        srv.socket = ctx.wrap_socket(srv.socket, server_side=True, do_handshake_on_connect=False)
     return srv
 
 

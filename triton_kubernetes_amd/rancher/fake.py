@@ -29,7 +29,15 @@ real server does after agents register:
   webhook is called over HTTPS, its certificate verified against the ``caBundle``
   for ``<service>.<namespace>.svc`` (``service_endpoints`` maps a service to the
   address it really listens on), and the returned JSONPatch is applied;
-  ``failurePolicy: Fail`` turns a webhook error into a rejected create.
+  ``failurePolicy: Fail`` turns a webhook error into a rejected create.  Namespace
+  selectors see the labels of the Namespace objects created through the proxy;
+* Pod Security Admission, after mutation as in a real API server: the namespace's
+  ``pod-security.kubernetes.io/enforce`` label (else ``default_pod_security``) at
+  ``baseline`` rejects host namespaces, privileged containers, added capabilities
+  beyond the default set, hostPath volumes and host ports; ``restricted`` also
+  requires ``runAsNonRoot``, ``allowPrivilegeEscalation: false``, dropping ``ALL``
+  capabilities, a RuntimeDefault/Localhost seccomp profile and only the restricted
+  volume types (403 ``violates PodSecurity``).
 
 Everything is in memory and thread-safe; it serves plain HTTP on 127.0.0.1.
 """
@@ -82,7 +90,8 @@ class _State:
 class FakeRancher:
     def __init__(self, rke_seconds: float = 0.0, node_ready_seconds: float = 0.0,
                  bootstrap_password: Optional[str] = None, host: str = "127.0.0.1", port: int = 0,
-                 k8s_versions: Optional[Sequence[str]] = None, async_registration_tokens: bool = True):
+                 k8s_versions: Optional[Sequence[str]] = None, async_registration_tokens: bool = True,
+                 default_pod_security: str = "privileged"):
         # a server started without CATTLE_BOOTSTRAP_PASSWORD has a random one nobody knows
         pw = bootstrap_password if bootstrap_password is not None else secrets.token_hex(16)
         self.state = _State(rke_seconds, node_ready_seconds, pw,
@@ -91,6 +100,9 @@ class FakeRancher:
         # webhook service of a test really listens)
         self.service_endpoints: Dict[str, str] = {}
         self.async_registration_tokens = async_registration_tokens
+        # Pod Security level of namespaces without an enforce label (the API server's
+        # AdmissionConfiguration default; Kubernetes' own default is privileged)
+        self.default_pod_security = default_pod_security
         self._server = HTTPServer((host, port), self._handler())
         self._server.daemon_threads = True
         self._thread: Optional[threading.Thread] = None
@@ -388,6 +400,14 @@ class FakeRancher:
     def _admit(self, cid: str, namespace: str, pod: Dict[str, Any]) -> Dict[str, Any]:
         return _admit_pod(self, cid, namespace, pod)
 
+    def namespace_labels(self, cid: str, namespace: str) -> Dict[str, str]:
+        """Labels of a Namespace created through the proxy (+ the automatic name label)."""
+        with self.state.mu:
+            ns = self.state.objects.get(f"{cid}|/api/v1/namespaces|{namespace}") or {}
+        labels = dict((ns.get("metadata") or {}).get("labels") or {})
+        labels["kubernetes.io/metadata.name"] = namespace
+        return labels
+
     def _register(self, h) -> Tuple[int, Any]:
         st = self.state
         token = h.headers.get("X-API-Tunnel-Token", "")
@@ -438,6 +458,13 @@ class FakeRancher:
                     body = self._admit(cid, parts[3], body)
                 except _Rejected as exc:
                     return 400, {"kind": "Status", "reason": "BadRequest", "code": 400, "message": str(exc)}
+                level = self.namespace_labels(cid, parts[3]).get(PSA_ENFORCE, self.default_pod_security)
+                problems = pod_security_violations(body, level)
+                if problems:
+                    name = (body.get("metadata") or {}).get("name", "")
+                    return 403, {"kind": "Status", "reason": "Forbidden", "code": 403,
+                                 "message": f'pods "{name}" is forbidden: violates PodSecurity "{level}:latest": '
+                                            + "; ".join(problems)}
             name = (body.get("metadata") or {}).get("name", uuid.uuid4().hex[:6])
             key = f"{cid}|{kpath}|{name}"
             with st.mu:
@@ -477,9 +504,59 @@ class _Rejected(Exception):
     pass
 
 
-def _ns_selected(selector: Dict[str, Any], namespace: str) -> bool:
-    """namespaceSelector on the ``kubernetes.io/metadata.name`` label (all the fake knows)."""
-    labels = {"kubernetes.io/metadata.name": namespace}
+PSA_ENFORCE = "pod-security.kubernetes.io/enforce"
+_BASELINE_CAPS = {"AUDIT_WRITE", "CHOWN", "DAC_OVERRIDE", "FOWNER", "FSETID", "KILL", "MKNOD", "NET_BIND_SERVICE",
+                  "SETFCAP", "SETGID", "SETPCAP", "SETUID", "SYS_CHROOT"}
+_RESTRICTED_VOLUMES = {"configMap", "csi", "downwardAPI", "emptyDir", "ephemeral", "persistentVolumeClaim",
+                       "projected", "secret"}
+
+
+def pod_security_violations(pod: Dict[str, Any], level: str) -> List[str]:
+    """Pod Security Standards checks (the subset a GPU workload meets) for ``level``:
+    ``privileged`` allows everything, ``baseline`` and ``restricted`` as documented."""
+    if level not in ("baseline", "restricted"):
+        return []
+    spec = pod.get("spec") or {}
+    containers = list(spec.get("initContainers") or []) + list(spec.get("containers") or [])
+    out: List[str] = []
+    for f in ("hostNetwork", "hostPID", "hostIPC"):
+        if spec.get(f):
+            out.append(f"host namespaces ({f}=true)")
+    host_path = [v.get("name") for v in spec.get("volumes") or [] if "hostPath" in v]
+    if host_path:
+        out.append("hostPath volumes (" + ", ".join(f'volume "{n}"' for n in host_path) + ")")
+    for c in containers:
+        sc = c.get("securityContext") or {}
+        if sc.get("privileged"):
+            out.append(f'privileged (container "{c.get("name")}")')
+        added = set(((sc.get("capabilities") or {}).get("add")) or [])
+        if added - _BASELINE_CAPS:
+            out.append(f'non-default capabilities (container "{c.get("name")}")')
+        if any(p.get("hostPort") for p in c.get("ports") or []):
+            out.append(f'hostPort (container "{c.get("name")}")')
+    if level == "restricted":
+        psc = spec.get("securityContext") or {}
+        bad_vol = [v.get("name") for v in spec.get("volumes") or []
+                   if not (set(v) - {"name"}) & _RESTRICTED_VOLUMES]
+        if bad_vol:
+            out.append("restricted volume types (" + ", ".join(f'volume "{n}"' for n in bad_vol) + ")")
+        for c in containers:
+            sc = c.get("securityContext") or {}
+            name = c.get("name")
+            if sc.get("allowPrivilegeEscalation") is not False:
+                out.append(f'allowPrivilegeEscalation != false (container "{name}")')
+            if "ALL" not in (((sc.get("capabilities") or {}).get("drop")) or []):
+                out.append(f'unrestricted capabilities (container "{name}" must drop ALL)')
+            if not (sc.get("runAsNonRoot", psc.get("runAsNonRoot"))):
+                out.append(f'runAsNonRoot != true (container "{name}")')
+            prof = (sc.get("seccompProfile") or psc.get("seccompProfile") or {}).get("type")
+            if prof not in ("RuntimeDefault", "Localhost"):
+                out.append(f'seccompProfile (container "{name}" must be RuntimeDefault or Localhost)')
+    return out
+
+
+def _ns_selected(selector: Dict[str, Any], labels: Dict[str, str]) -> bool:
+    """A namespaceSelector against the namespace's labels."""
     for k, v in (selector.get("matchLabels") or {}).items():
         if labels.get(k) != v:
             return False
@@ -535,7 +612,7 @@ def _admit_pod(fake: "FakeRancher", cid: str, namespace: str, pod: Dict[str, Any
         for hook in cfg.get("webhooks") or []:
             if not any(_rule_matches(r) for r in hook.get("rules") or []):
                 continue
-            if not _ns_selected(hook.get("namespaceSelector") or {}, namespace):
+            if not _ns_selected(hook.get("namespaceSelector") or {}, fake.namespace_labels(cid, namespace)):
                 continue
             review = {"apiVersion": "admission.k8s.io/v1", "kind": "AdmissionReview",
                       "request": {"uid": str(uuid.uuid4()), "kind": {"group": "", "version": "v1", "kind": "Pod"},
