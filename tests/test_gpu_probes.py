@@ -212,6 +212,27 @@ def test_link_matrix_rounds_cover_every_ordered_pair():
         assert time.monotonic() - t0 < 10
 
 
+def test_kernel_peer_read_matrix_and_floor():
+    """The primary link number is a kernel on the receiver reading the sender's memory
+    (k_peer_read).  On one GPU the "peers" are GPU 0 itself, so both methods time a
+    device-local transfer through the same schedule; every pair clears the absolute floor
+    and the verdict records the method."""
+    from triton_kubernetes_amd.node.labels import link_labels
+    from triton_kubernetes_amd.ops import probe
+
+    devs = [0, 0, 0, 0] if probe.device_count() < 2 else list(range(probe.device_count()))
+    kread = probe.link_matrix(devs, 64 << 20, 3, method="kernel-read")
+    sdma = probe.link_matrix(devs, 64 << 20, 3, method="sdma-copy")
+    print(json.dumps({"kernel-read": kread["pairs"], "sdma-copy": sdma["pairs"]}))
+    n = len(devs)
+    assert kread["method"] == "kernel-read" and not kread["errors"] and len(kread["pairs"]) == len(set(
+        f"{i}-{j}" for a, i in enumerate(devs) for b, j in enumerate(devs) if a != b))
+    assert all(v > probe.DEFAULT_MIN_LINK_GBPS for v in kread["pairs"].values()), kread
+    verdict = link_labels(kread)
+    assert verdict["status"] == "passed" and verdict["labels"]["amd.com/xgmi.p2p-method"] == "kernel-read"
+    assert n >= 2 and all(v > 0 for v in sdma["pairs"].values())
+
+
 def test_topology_amdsmi():
     from triton_kubernetes_amd.ops import topo
 
@@ -336,3 +357,31 @@ def test_default_runtime_maps_system_rccl_and_slim_is_verified_opt_in(tmp_path):
     print(json.dumps({"default": default, "slim": slim, "prepare": meta}))
     assert slim["ok"] and slim["runtime"] == meta["dir"]
     assert slim["rccl"] == [os.path.realpath(os.path.join(str(meta["dir"]), "librccl.so"))]
+
+
+@pytest.mark.parametrize("point", ["memtest_span.after_alloc", "memtest_span.after_launch"])
+def test_memtest_span_releases_everything_on_error(point):
+    """an error inside the span memtest must not leave its chunks (up to ~300 GB
+    in a full burn-in), the stream or the events allocated in a long-lived agent."""
+    from triton_kubernetes_amd.ops import probe
+
+    probe.wait_frees()
+    before = probe.free_bytes(0)
+    probe.set_fail_point(point)
+    try:
+        with pytest.raises(probe.ProbeError, match="injected failure"):
+            probe.memtest_span(0, 48 << 30, chunk=16 << 30)
+    finally:
+        probe.set_fail_point("")
+    after = probe.free_bytes(0)
+    assert after >= before - (1 << 30), (before, after)
+    # the next span memtest on the same GPU runs normally
+    ok = probe.memtest_span(0, 4 << 30, chunk=2 << 30)
+    assert ok["errors"] == 0 and ok["bytes"] == 4 << 30
+
+
+def test_memtest_span_with_nothing_allocatable_reports_zero():
+    from triton_kubernetes_amd.ops import probe
+
+    res = probe.memtest_span(0, 4 << 40, chunk=2 << 40)  # a 2 TiB chunk never fits
+    assert res["bytes"] == 0 and res["errors"] == 0

@@ -328,6 +328,36 @@ def test_link_labels_verdicts():
     assert link_labels({"pairs": {}, "errors": []})["status"] == "skipped"
 
 
+def test_link_check_absolute_floor_fails_a_uniformly_slow_fabric():
+    """relative-to-median alone passes a fabric whose every link is slow; the
+    absolute floor (default 38 GB/s: half of one xGMI link's ~76.8 GB/s one way) fails it."""
+    from triton_kubernetes_amd.node.labels import DEFAULT_MIN_LINK_GBPS, link_labels
+    from triton_kubernetes_amd.ops import probe
+
+    assert DEFAULT_MIN_LINK_GBPS == probe.DEFAULT_MIN_LINK_GBPS == probe.XGMI_LINK_ONE_WAY_GBPS / 2 - 0.4
+    n = 8
+    every = [f"{i}-{j}" for i in range(n) for j in range(n) if i != j]
+    acc = {p: True for p in every}
+    slow = link_labels({"pairs": {p: 25.0 for p in every}, "peer_access": acc, "method": "kernel-read"})
+    assert slow["status"] == "degraded" and slow["below_floor"] == sorted(every) and len(slow["degraded"]) == 56
+    assert slow["labels"]["amd.com/xgmi.p2p-method"] == "kernel-read"
+    # the same matrix with the floor off (0) passes: only the relative rule is left
+    assert link_labels({"pairs": {p: 25.0 for p in every}, "peer_access": acc}, min_gbps=0.0)["status"] == "passed"
+    # one bad link among healthy ones: relative rule
+    one = {p: 70.0 for p in every}
+    one["3-5"] = 30.0
+    v = link_labels({"pairs": one, "peer_access": acc})
+    assert v["status"] == "degraded" and v["degraded"] == ["3-5"] and v["below_floor"] == ["3-5"]
+    one["3-5"] = 40.0  # above the floor, but 0.57 of the median: passes at 0.5, fails at 0.6
+    assert link_labels({"pairs": one, "peer_access": acc})["status"] == "passed"
+    assert link_labels({"pairs": one, "peer_access": acc}, min_frac=0.6)["degraded"] == ["3-5"]
+    # a missing peer (no peer access, the kernel read could not run): error
+    missing = {p: 70.0 for p in every if p != "6-7"}
+    e = link_labels({"pairs": missing, "peer_access": dict(acc, **{"6-7": False}),
+                     "errors": ["6->7: peer read failed"]})
+    assert e["status"] == "error" and "6->7: peer read failed" in e["errors"]
+
+
 def test_multi_gpu_plan_checks_links():
     from triton_kubernetes_amd.node.plan import build_host_plan
 
@@ -336,7 +366,11 @@ def test_multi_gpu_plan_checks_links():
     plan = build_host_plan(cfg, "https://r", "tok", "ca", mi355x=True)
     names = plan.step_names()
     assert names.index("gpu_burnin") < names.index("gpu_links") < names.index("gpu_labels")
-    assert "gpu-burnin --p2p --min-link-frac 0.6" in plan.render_shell()
+    assert "gpu-burnin --p2p --min-link-frac 0.6 --min-link-gbps 38.0" in plan.render_shell()
+    step = next(st for st in plan.steps if st.name == "gpu_links")
+    assert step.params == {"min_frac": 0.6, "min_gbps": 38.0, "method": "kernel-read"}
+    floor = build_host_plan(dict(cfg, gpu_link_min_gbps=50), "https://r", "tok", "ca", mi355x=True)
+    assert "--min-link-gbps 50.0" in floor.render_shell()
     one = build_host_plan(dict(cfg, gpu_count=1), "https://r", "tok", "ca", mi355x=True)
     assert "gpu_links" not in one.step_names()
 
@@ -387,10 +421,11 @@ def test_gpu_links_cli_verdict(monkeypatch, capsys):
 
     monkeypatch.setattr(probe, "device_count", lambda: 3)
 
-    def matrix(devs, nbytes=64 << 20, iters=3):
+    def matrix(devs, nbytes=64 << 20, iters=3, method="kernel-read"):
         pairs = {f"{i}-{j}": 100.0 for i in devs for j in devs if i != j}
         pairs["2-0"] = slow
-        return {"pairs": pairs, "peer_access": {k: True for k in pairs}, "errors": [], "bytes": nbytes}
+        return {"pairs": pairs, "peer_access": {k: True for k in pairs}, "errors": [], "bytes": nbytes,
+                "method": method}
 
     monkeypatch.setattr(probe, "link_matrix", matrix)
     slow = 90.0
@@ -402,3 +437,11 @@ def test_gpu_links_cli_verdict(monkeypatch, capsys):
     assert cli.main(["links", "--min-frac", "0.5"]) == 1
     doc = json.loads(capsys.readouterr().out)
     assert doc["status"] == "degraded" and doc["degraded"]
+    # every link at 30 GB/s: the median rule passes, the absolute floor does not
+    slow = 30.0
+    monkeypatch.setattr(probe, "link_matrix", lambda devs, nbytes=0, iters=3, method="kernel-read": {
+        "pairs": {f"{i}-{j}": 30.0 for i in devs for j in devs if i != j}, "peer_access": {}, "errors": [],
+        "method": method})
+    assert cli.main(["links"]) == 1
+    assert json.loads(capsys.readouterr().out)["status"] == "degraded"
+    assert cli.main(["links", "--min-gbps", "20"]) == 0

@@ -173,6 +173,14 @@ def _mi355x_fields(ctx: Context) -> Dict:
         except ValueError as exc:
             raise ConfigError(f"gpu_link_min_frac must be a number between 0 and 1. Found '{frac}'.") from exc
         out["gpu_link_min_frac"] = frac
+    if s.is_set("gpu_link_min_gbps"):
+        floor = s.get_string("gpu_link_min_gbps")
+        try:
+            if float(floor) < 0:
+                raise ValueError
+        except ValueError as exc:
+            raise ConfigError(f"gpu_link_min_gbps must be a non-negative number. Found '{floor}'.") from exc
+        out["gpu_link_min_gbps"] = floor
     if s.is_set("rccl_slim"):  # opt-in verified single-target RCCL (terraform/scripts.py)
         slim = s.get_string("rccl_slim").lower()
         if slim in ("true", "yes", "1"):

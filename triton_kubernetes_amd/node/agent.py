@@ -276,7 +276,8 @@ class NodeAgent:
             ctx["labels"].update(burnin_labels(level, results))
             return out
         if a == "gpu_links":
-            # every ordered GPU pair's peer copy, one at a time: a degraded xGMI link fails the
+            # every ordered GPU pair's peer read (a kernel on the receiver), disjoint pairs at
+            # a time: a link below the node's median fraction or the absolute floor fails the
             # node; a pair the runtime cannot measure is recorded, not fatal
             if len(self.devices) < 2:
                 return {"skipped": "single GPU"}
@@ -284,7 +285,9 @@ class NodeAgent:
                 return {"simulated": True}
             from ..ops import probe
 
-            verdict = link_labels(probe.link_matrix(self.devices), float(step.params.get("min_frac", 0.5)))
+            verdict = link_labels(probe.link_matrix(self.devices, method=str(step.params.get("method", "kernel-read"))),
+                                  float(step.params.get("min_frac", 0.5)),
+                                  float(step.params.get("min_gbps", probe.DEFAULT_MIN_LINK_GBPS)))
             ctx["labels"].update(verdict["labels"])
             if verdict["status"] == "degraded":
                 raise StepFailed(step.name, f"degraded xGMI links: {verdict['degraded']}")

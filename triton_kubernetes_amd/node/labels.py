@@ -132,23 +132,34 @@ def burnin_labels(level: str, results: Dict[Any, Dict[str, Any]]) -> Dict[str, s
             "amd.com/gpu.burnin-hbm-tested-pct": f"{100.0 * frac:.1f}"}
 
 
-def link_labels(matrix: Dict[str, Any], min_frac: float = 0.5) -> Dict[str, Any]:
+DEFAULT_MIN_LINK_GBPS = 38.0  # = ops/probe.py (half of one xGMI link's ~76.8 GB/s one way)
+
+
+def link_labels(matrix: Dict[str, Any], min_frac: float = 0.5,
+                min_gbps: float = DEFAULT_MIN_LINK_GBPS) -> Dict[str, Any]:
     """Verdict and labels of a node's peer-to-peer link matrix (``ops/probe.py:link_matrix``
-    or ``gpu-burnin --p2p``): a pair below ``min_frac`` of the node's median is a degraded
-    xGMI link; a pair without peer access or whose copy failed is an error.  Returns
-    ``{"labels": {...}, "degraded": [...], "status": passed|degraded|error}``."""
+    or ``gpu-burnin --p2p``).  A pair is a degraded xGMI link when it is below ``min_frac``
+    of the node's median (one bad link) OR below the absolute floor ``min_gbps`` (a
+    uniformly slow fabric, whose median looks healthy); a pair without peer access or whose
+    transfer failed is an error.  Returns ``{"labels": {...}, "degraded": [...],
+    "below_floor": [...], "status": passed|degraded|error}``."""
     vals = sorted(matrix.get("pairs", {}).values())
     errors = list(matrix.get("errors", []))
     errors += [f"{p}: no peer access" for p, ok in sorted(matrix.get("peer_access", {}).items()) if not ok]
     if not vals:
-        return {"labels": {}, "degraded": [], "status": "error" if errors else "skipped"}
+        return {"labels": {}, "degraded": [], "below_floor": [], "errors": errors,
+                "status": "error" if errors else "skipped"}
     median = vals[len(vals) // 2] if len(vals) % 2 else 0.5 * (vals[len(vals) // 2 - 1] + vals[len(vals) // 2])
-    degraded = sorted(p for p, v in matrix["pairs"].items() if v < min_frac * median)
+    below = sorted(p for p, v in matrix["pairs"].items() if v < min_gbps)
+    degraded = sorted(p for p, v in matrix["pairs"].items() if v < min_frac * median or v < min_gbps)
     status = "error" if errors else ("degraded" if degraded else "passed")
     labels = {"amd.com/xgmi.link-check": status,
               "amd.com/xgmi.p2p-min-gbps": f"{vals[0]:.0f}",
               "amd.com/xgmi.p2p-median-gbps": f"{median:.0f}"}
-    return {"labels": labels, "degraded": degraded, "errors": errors, "status": status}
+    if matrix.get("method"):
+        labels["amd.com/xgmi.p2p-method"] = str(matrix["method"])
+    return {"labels": labels, "degraded": degraded, "below_floor": below, "errors": errors, "status": status,
+            "floor_gbps": min_gbps}
 
 
 def agent_label_flags(labels: Dict[str, str]) -> List[str]:

@@ -38,6 +38,7 @@ from ..terraform.scripts import RCCL_SLIM_ENABLE_FN, RCCL_SLIM_FN, RCCL_SLIM_ROO
 
 from ..versions import AGENT_IMAGE as DEFAULT_AGENT_IMAGE
 from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
+from .labels import DEFAULT_MIN_LINK_GBPS
 from .manager import docker_install_lines
 
 LABEL_FILE = "/etc/triton-kubernetes/gpu-labels"
@@ -200,11 +201,14 @@ sudo mkdir -p /etc/triton-kubernetes
 sudo install -m 0644 /tmp/tk-burnin-labels {BURNIN_LABEL_FILE}""",
                                    {"level": burnin}, gpu=True))
         if ngpu > 1:
-            # per-link xGMI health: peer copy bandwidth of every GPU pair vs the node's median
+            # per-link xGMI health: kernel-driven peer read of every GPU pair against the
+            # node's median (relative) and an absolute floor (a uniformly slow fabric)
             frac = float(cfg.get("gpu_link_min_frac", 0.5) or 0.5)
+            floor = float(cfg.get("gpu_link_min_gbps", DEFAULT_MIN_LINK_GBPS) or 0.0)
             plan.steps.append(Step("gpu_links", "gpu_links", f"""
-{TOOLS_DIR}/gpu-burnin --p2p --min-link-frac {frac} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
-cat /tmp/tk-link-labels | sudo tee -a {BURNIN_LABEL_FILE} >/dev/null""", {"min_frac": frac}, gpu=True))
+{TOOLS_DIR}/gpu-burnin --p2p --min-link-frac {frac} --min-link-gbps {floor} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
+cat /tmp/tk-link-labels | sudo tee -a {BURNIN_LABEL_FILE} >/dev/null""", {"min_frac": frac, "min_gbps": floor,
+                                                                       "method": "kernel-read"}, gpu=True))
         plan.steps.append(Step("gpu_labels", "gpu_labels", f"""
 sudo mkdir -p "$(dirname {LABEL_FILE})"
 {TOOLS_DIR}/amdgpu-topo-labeller | sudo tee {TOPOLOGY_FILE} >/dev/null

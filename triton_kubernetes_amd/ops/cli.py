@@ -4,7 +4,7 @@
     python -m triton_kubernetes_amd.ops.cli topology
     python -m triton_kubernetes_amd.ops.cli labels
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
-    python -m triton_kubernetes_amd.ops.cli links [--min-frac F] [--mib M]
+    python -m triton_kubernetes_amd.ops.cli links [--min-frac F] [--min-gbps G] [--method kernel-read|sdma-copy] [--mib M]
     python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
     python -m triton_kubernetes_amd.ops.cli rccl-slim [--source DIR] [--root DIR] [--no-verify]
     python -m triton_kubernetes_amd.ops.cli gemm [--size N] [--reps R] [--schedule staggered|single-barrier] [--dtype bf16|fp8]
@@ -31,8 +31,11 @@ def main(argv: Sequence[str] = ()) -> int:
     r = sub.add_parser("rccl-local")
     r.add_argument("--ngpus", type=int, default=0)
     r.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
-    lk = sub.add_parser("links", help="per-link xGMI check: peer copy bandwidth of every ordered GPU pair")
+    lk = sub.add_parser("links", help="per-link xGMI check: peer bandwidth of every ordered GPU pair")
     lk.add_argument("--min-frac", type=float, default=0.5, help="fail below this fraction of the node median")
+    lk.add_argument("--min-gbps", type=float, default=None,
+                    help="fail below this absolute GB/s (default: half of one link's ~76.8 GB/s one way)")
+    lk.add_argument("--method", default="kernel-read", choices=["kernel-read", "sdma-copy"])
     lk.add_argument("--mib", type=int, default=64, help="bytes per copy (MiB)")
     sl = sub.add_parser("rccl-slim", help="opt-in: prepare and verify the single-target (gfx950) RCCL copy")
     sl.add_argument("--source", default="")
@@ -92,8 +95,9 @@ def main(argv: Sequence[str] = ()) -> int:
         if n < 2:
             print(json.dumps({"skipped": "single GPU"}))
             return 0
-        matrix = probe.link_matrix(range(n), args.mib << 20)
-        verdict = link_labels(matrix, args.min_frac)
+        matrix = probe.link_matrix(range(n), args.mib << 20, method=args.method)
+        verdict = link_labels(matrix, args.min_frac,
+                              probe.DEFAULT_MIN_LINK_GBPS if args.min_gbps is None else args.min_gbps)
         print(json.dumps(dict(verdict, pairs=matrix["pairs"]), indent=2, sort_keys=True))
         return 1 if verdict["status"] == "degraded" else 0
     if args.cmd == "rccl-slim":

@@ -761,15 +761,54 @@ extern "C" int tkp_wait_frees() {
   return 0;
 }
 
+// Test hook: the named step of tkp_memtest_span fails as if its HIP call had (tests check
+// that every allocation, the stream and the events are released on such a path).
+static char g_fail_point[64] = "";
+extern "C" void tkp_set_fail_point(const char* name) {
+  snprintf(g_fail_point, sizeof(g_fail_point), "%s", name ? name : "");
+}
+static bool fail_point(const char* name) { return g_fail_point[0] && !strcmp(g_fail_point, name); }
+#define FAILPOINT(name)                                                  \
+  do {                                                                   \
+    if (fail_point(name)) {                                              \
+      snprintf(g_err, sizeof(g_err), "injected failure at %s", name);    \
+      return -1;                                                         \
+    }                                                                    \
+  } while (0)
+
+// Everything tkp_memtest_span holds; released on every return path unless the chunks were
+// handed to the background free thread.  A long-lived agent that hit one error in a full
+// burn-in would otherwise keep ~300 GB of the GPU allocated until it restarts.
+struct SpanHold {
+  int dev;
+  std::vector<uint4*> chunks;
+  unsigned long long* err = nullptr;
+  hipStream_t s = nullptr;
+  hipEvent_t t0 = nullptr, t1 = nullptr;
+  explicit SpanHold(int d) : dev(d) {}
+  ~SpanHold() {
+    (void)hipSetDevice(dev);
+    if (s) (void)hipStreamSynchronize(s);  // no kernel may still touch a chunk being freed
+    if (t0) (void)hipEventDestroy(t0);
+    if (t1) (void)hipEventDestroy(t1);
+    if (s) (void)hipStreamDestroy(s);
+    if (err) (void)hipFree(err);
+    for (uint4* p : chunks) (void)hipFree(p);
+    (void)hipGetLastError();
+  }
+};
+
 extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t headroom, int passes, double* out) {
   tkp_wait_frees();
   CHECK(hipSetDevice(dev));
   size_t free_b = 0, total_b = 0;
   CHECK(hipMemGetInfo(&free_b, &total_b));
+  for (int i = 0; i < 7; ++i) out[i] = 0.0;
+  out[3] = (double)total_b;
   if (bytes == 0) bytes = free_b > headroom ? free_b - headroom : 0;
   if (chunk == 0) chunk = 16ull << 30;
   chunk = chunk / sizeof(uint4) * sizeof(uint4);
-  std::vector<uint4*> chunks;
+  SpanHold hold(dev);
   std::vector<size_t> sizes;
   const auto t_alloc = std::chrono::steady_clock::now();
   for (size_t done = 0; done < bytes && chunk > 0;) {
@@ -780,55 +819,51 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
       (void)hipGetLastError();
       break;  // fragmentation: test what could be held
     }
-    chunks.push_back(p);
+    hold.chunks.push_back(p);
     sizes.push_back(want);
     done += want;
   }
-  const double alloc_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc).count();
-  unsigned long long* err = nullptr;
-  CHECK(hipMalloc(&err, sizeof(unsigned long long)));
-  hipStream_t s;
-  CHECK(burnin_stream(&s));
-  CHECK(hipMemsetAsync(err, 0, sizeof(unsigned long long), s));
-  hipEvent_t t0, t1;
-  CHECK(hipEventCreate(&t0));
-  CHECK(hipEventCreate(&t1));
+  out[4] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc).count();
+  if (hold.chunks.empty()) return 0;  // nothing could be held: tested = 0 bytes, no error
+  FAILPOINT("memtest_span.after_alloc");
+  CHECK(hipMalloc(&hold.err, sizeof(unsigned long long)));
+  CHECK(burnin_stream(&hold.s));
+  CHECK(hipMemsetAsync(hold.err, 0, sizeof(unsigned long long), hold.s));
+  CHECK(hipEventCreate(&hold.t0));
+  CHECK(hipEventCreate(&hold.t1));
   const int grid = stream_grid(dev, 16);
   float ms = 0.f;
   size_t tested = 0;
   const auto t_test = std::chrono::steady_clock::now();
-  for (size_t c = 0; c < chunks.size(); ++c) {
+  for (size_t c = 0; c < hold.chunks.size(); ++c) {
     const size_t n = sizes[c] / sizeof(uint4);
     for (int ps = 0; ps < (passes < 1 ? 1 : passes); ++ps) {
       const uint32_t seed = 0x1234567u + 0x9e3779b9u * (uint32_t)ps + 0x85ebca6bu * (uint32_t)c;
-      k_mem_fill<<<grid, STREAM_THREADS, 0, s>>>(chunks[c], n, seed);
-      CHECK(hipEventRecord(t0, s));
-      k_mem_check<<<grid, STREAM_THREADS, 0, s>>>(chunks[c], n, seed, err);
-      CHECK(hipEventRecord(t1, s));
+      k_mem_fill<<<grid, STREAM_THREADS, 0, hold.s>>>(hold.chunks[c], n, seed);
+      CHECK(hipEventRecord(hold.t0, hold.s));
+      k_mem_check<<<grid, STREAM_THREADS, 0, hold.s>>>(hold.chunks[c], n, seed, hold.err);
+      CHECK(hipEventRecord(hold.t1, hold.s));
     }
     tested += sizes[c];
   }
-  CHECK(hipEventSynchronize(t1));
-  CHECK(hipEventElapsedTime(&ms, t0, t1));
+  FAILPOINT("memtest_span.after_launch");
+  CHECK(hipEventSynchronize(hold.t1));
+  CHECK(hipEventElapsedTime(&ms, hold.t0, hold.t1));
   CHECK(hipGetLastError());
   unsigned long long h = 0;
-  CHECK(hipMemcpyAsync(&h, err, sizeof(h), hipMemcpyDeviceToHost, s));
-  CHECK(hipStreamSynchronize(s));
+  CHECK(hipMemcpyAsync(&h, hold.err, sizeof(h), hipMemcpyDeviceToHost, hold.s));
+  CHECK(hipStreamSynchronize(hold.s));
   out[0] = (double)h;
-  out[1] = sizes.empty() ? 0.0 : (double)sizes.back() / (ms * 1e-3) / 1e9;
+  out[1] = ms > 0.f ? (double)sizes.back() / (ms * 1e-3) / 1e9 : 0.0;
   out[2] = (double)tested;
-  out[3] = (double)total_b;
   out[5] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_test).count();
-  out[4] = alloc_ms;
-  TRACED(hipEventDestroy(t0));
-  TRACED(hipEventDestroy(t1));
-  TRACED(hipStreamDestroy(s));
-  TRACED(hipFree(err));
   if (g_async_free.load()) {
     {
       std::lock_guard<std::mutex> lk(g_free_mu);
       ++g_frees_pending;
     }
+    std::vector<uint4*> chunks;
+    chunks.swap(hold.chunks);  // the background thread owns them now
     std::thread([dev, chunks]() {
       (void)hipSetDevice(dev);
       for (uint4* p : chunks) (void)hipFree(p);
@@ -842,7 +877,8 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
     return 0;
   }
   const auto t_free = std::chrono::steady_clock::now();
-  for (uint4* p : chunks) TRACED(hipFree(p));
+  for (uint4* p : hold.chunks) TRACED(hipFree(p));
+  hold.chunks.clear();
   out[6] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_free).count();
   return 0;
 }
@@ -919,14 +955,38 @@ extern "C" int tkp_p2p_bandwidth(int src, int dst, size_t bytes, int iters, doub
   return 0;
 }
 
+// Kernel-driven peer read: the destination GPU's CUs pull the peer's buffer over xGMI
+// (16-byte non-temporal loads, 4 in flight per thread) into local memory.  This is how RCCL
+// and GPU workloads move data across the fabric, so it is the primary link number; the
+// SDMA engines behind hipMemcpyPeerAsync take another path and can hide a slow link.
+__global__ __launch_bounds__(STREAM_THREADS) void k_peer_read(const u32x4* __restrict__ remote,
+                                                              u32x4* __restrict__ local, size_t n) {
+  const size_t stride = (size_t)gridDim.x * blockDim.x;
+  size_t i = (size_t)blockIdx.x * blockDim.x + threadIdx.x;
+  for (; i + 3 * stride < n; i += 4 * stride) {
+    const u32x4 a = __builtin_nontemporal_load(remote + i);
+    const u32x4 b = __builtin_nontemporal_load(remote + i + stride);
+    const u32x4 c = __builtin_nontemporal_load(remote + i + 2 * stride);
+    const u32x4 d = __builtin_nontemporal_load(remote + i + 3 * stride);
+    local[i] = a;  // plain stores: non-temporal ones cost bandwidth here (see the note at the top)
+    local[i + stride] = b;
+    local[i + 2 * stride] = c;
+    local[i + 3 * stride] = d;
+  }
+  for (; i < n; i += stride) local[i] = __builtin_nontemporal_load(remote + i);
+}
+
 // Every ordered pair of `n` local GPUs, measured in rounds of a round-robin pairing (the
-// circle method): a round is a perfect matching, so each GPU takes part in one copy per
-// round direction and every concurrent copy has its own xGMI link and copy engines.  An
-// 8-GPU node needs 7 rounds x 2 directions instead of 56 one-at-a-time measurements, and
-// buffers, streams and peer access are set up once.  gbps[i*n+j]: best copy i -> j (GB/s,
-// -1 when that copy failed); access[i*n+j]: j can map i's memory (the copy then runs peer
-// to peer rather than staged).  Peer access this call enabled is disabled again.
-extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, double* gbps, int* access) {
+// circle method): a round is a perfect matching, so each GPU takes part in one transfer per
+// round direction and every concurrent transfer has its own xGMI link.  An 8-GPU node needs
+// 7 rounds x 2 directions instead of 56 one-at-a-time measurements, and buffers, streams and
+// peer access are set up once.  mode 1 (primary): the receiving GPU's kernel reads the
+// sender's memory (k_peer_read; needs peer access); mode 0: an SDMA peer copy
+// (hipMemcpyPeerAsync).  gbps[i*n+j]: best transfer i -> j (GB/s, -1 when it failed or, in
+// kernel mode, when j cannot map i's memory); access[i*n+j]: j can map i's memory.  Peer
+// access this call enabled is disabled again.
+extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int iters, int mode, double* gbps,
+                                    int* access) {
   if (n < 2 || n > 64 || bytes == 0) {
     snprintf(g_err, sizeof(g_err), "link matrix: %d devices, %zu bytes", n, bytes);
     return -1;
@@ -935,6 +995,8 @@ extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, 
   std::vector<hipStream_t> st(n, nullptr);
   std::vector<hipEvent_t> ev(2 * n, nullptr);
   std::vector<std::pair<int, int>> enabled;
+  std::vector<int> grid(n, 0);
+  bytes = bytes / sizeof(u32x4) * sizeof(u32x4);
   int rc = 0;
   auto cleanup = [&]() {
     for (int i = 0; i < n; ++i) {
@@ -963,6 +1025,7 @@ extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, 
     if (e == hipSuccess) e = hipEventCreate(&ev[2 * i + 1]);
     if (e == hipSuccess) e = hipDeviceSynchronize();
     if (e != hipSuccess) rc = set_err("link matrix setup", e);
+    else grid[i] = stream_grid(devs[i], 4);
   }
   for (int i = 0; i < n && rc == 0; ++i)
     for (int j = 0; j < n && rc == 0; ++j) {
@@ -996,8 +1059,18 @@ extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, 
           if (failed[p]) continue;
           const int src = dir ? pairs[p].second : pairs[p].first, dst = dir ? pairs[p].first : pairs[p].second;
           (void)hipSetDevice(devs[dst]);
+          if (mode == 1 && !access[src * n + dst] && devs[src] != devs[dst]) { failed[p] = 1; continue; }
           hipError_t e = hipEventRecord(ev[2 * dst], st[dst]);
-          if (e == hipSuccess) e = hipMemcpyPeerAsync(buf[2 * dst + 1], devs[dst], buf[2 * src], devs[src], bytes, st[dst]);
+          if (e == hipSuccess) {
+            if (mode == 1) {
+              k_peer_read<<<grid[dst], STREAM_THREADS, 0, st[dst]>>>(static_cast<const u32x4*>(buf[2 * src]),
+                                                                     static_cast<u32x4*>(buf[2 * dst + 1]),
+                                                                     bytes / sizeof(u32x4));
+              e = hipGetLastError();
+            } else {
+              e = hipMemcpyPeerAsync(buf[2 * dst + 1], devs[dst], buf[2 * src], devs[src], bytes, st[dst]);
+            }
+          }
           if (e == hipSuccess) e = hipEventRecord(ev[2 * dst + 1], st[dst]);
           if (e != hipSuccess) { failed[p] = 1; (void)hipGetLastError(); }
         }
@@ -1025,6 +1098,10 @@ extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, 
   return rc;
 }
 
+extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, double* gbps, int* access) {
+  return tkp_link_matrix_mode(devs, n, bytes, iters, 0, gbps, access);
+}
+
 #ifdef TK_PROBE_MAIN
 // gpu-burnin: the on-node executable the SSH bootstrap runs (no Python needed).
 //   gpu-burnin [--all | --device N] [--level quick|full]
@@ -1042,11 +1119,13 @@ extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inje
 extern "C" int tkg_screen_fp8(int dev, int M, int N, int K, int reps, long long inject, double* out);
 extern "C" const char* tkg_last_error();
 
-// --p2p: peer copy bandwidth of every ordered GPU pair (tkp_link_matrix: concurrent copies
-// only on disjoint pairs, so each number is one xGMI link's), against the node's median; same keys and verdict as
-// node/labels.py:link_labels.  A degraded link exits 1; a pair the runtime cannot measure
+// --p2p: peer bandwidth of every ordered GPU pair (tkp_link_matrix_mode: a kernel on the
+// receiver reading the sender's memory by default, SDMA copies with --p2p-method sdma-copy;
+// concurrent transfers only on disjoint pairs, so each number is one xGMI link's), against
+// the node's median (--min-link-frac) and an absolute floor (--min-link-gbps); same keys and
+// verdict as node/labels.py:link_labels.  A degraded link exits 1; a pair the runtime cannot measure
 // is reported as an error (exit 0: the node agent path treats it the same way).
-static int p2p_main(const char* labels_path, double min_frac) {
+static int p2p_main(const char* labels_path, double min_frac, double min_gbps, int mode) {
   int n = 0;
   if (tkp_device_count(&n) != 0 || n < 1) {
     printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
@@ -1060,7 +1139,7 @@ static int p2p_main(const char* labels_path, double min_frac) {
   std::vector<double> vals, mat(n * n, 0.0);
   std::vector<int> devs(n), acc(n * n, 0);
   for (int i = 0; i < n; ++i) devs[i] = i;
-  if (tkp_link_matrix(devs.data(), n, 64ull << 20, 3, mat.data(), acc.data()) != 0) {
+  if (tkp_link_matrix_mode(devs.data(), n, 64ull << 20, 3, mode, mat.data(), acc.data()) != 0) {
     printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
     return 2;
   }
@@ -1080,17 +1159,25 @@ static int p2p_main(const char* labels_path, double min_frac) {
   std::sort(sorted.begin(), sorted.end());
   const size_t m = sorted.size();
   const double median = m == 0 ? 0.0 : (m % 2 ? sorted[m / 2] : 0.5 * (sorted[m / 2 - 1] + sorted[m / 2]));
-  int degraded = 0;
-  for (double v : vals) degraded += v < min_frac * median;
+  // a link is degraded below min_frac of the node's median OR below the absolute floor
+  // (a uniformly slow fabric has a healthy-looking median)
+  int degraded = 0, below_floor = 0;
+  for (double v : vals) {
+    degraded += v < min_frac * median || v < min_gbps;
+    below_floor += v < min_gbps;
+  }
   const char* status = (errors || no_peer || m == 0) ? "error" : (degraded ? "degraded" : "passed");
-  printf("},\"min_gbps\":%.1f,\"median_gbps\":%.1f,\"degraded\":%d,\"errors\":%d,\"no_peer_access\":%d,"
-         "\"status\":\"%s\"}\n", m ? sorted[0] : 0.0, median, degraded, errors, no_peer, status);
+  printf("},\"method\":\"%s\",\"min_gbps\":%.1f,\"median_gbps\":%.1f,\"floor_gbps\":%.1f,\"degraded\":%d,"
+         "\"below_floor\":%d,\"errors\":%d,\"no_peer_access\":%d,\"status\":\"%s\"}\n",
+         mode ? "kernel-read" : "sdma-copy", m ? sorted[0] : 0.0, median, min_gbps, degraded, below_floor, errors,
+         no_peer, status);
   if (labels_path && m) {
     FILE* f = fopen(labels_path, "w");
     if (!f) { fprintf(stderr, "cannot write %s\n", labels_path); return 2; }
     fprintf(f, "amd.com/xgmi.link-check=%s\n", status);
     fprintf(f, "amd.com/xgmi.p2p-min-gbps=%.0f\n", sorted[0]);
     fprintf(f, "amd.com/xgmi.p2p-median-gbps=%.0f\n", median);
+    fprintf(f, "amd.com/xgmi.p2p-method=%s\n", mode ? "kernel-read" : "sdma-copy");
     fclose(f);
   }
   return degraded ? 1 : 0;
@@ -1102,6 +1189,8 @@ int main(int argc, char** argv) {
   const char* labels_path = nullptr;  // --labels FILE: node labels recording what was tested
   int p2p = 0;                        // --p2p: per-link peer copy matrix instead of the burn-in
   double min_link_frac = 0.5;
+  double min_link_gbps = 38.0;  // = ops/probe.py:DEFAULT_MIN_LINK_GBPS (half a link's one-way 76.8 GB/s)
+  int link_mode = 1;            // --p2p-method kernel-read (default) | sdma-copy
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
   for (int i = 1; i < argc; ++i) {
@@ -1116,8 +1205,10 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--labels") && i + 1 < argc) labels_path = argv[++i];
     else if (!strcmp(argv[i], "--p2p")) p2p = 1;
     else if (!strcmp(argv[i], "--min-link-frac") && i + 1 < argc) min_link_frac = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--min-link-gbps") && i + 1 < argc) min_link_gbps = atof(argv[++i]);
+    else if (!strcmp(argv[i], "--p2p-method") && i + 1 < argc) link_mode = strcmp(argv[++i], "sdma-copy") ? 1 : 0;
   }
-  if (p2p) return p2p_main(labels_path, min_link_frac);
+  if (p2p) return p2p_main(labels_path, min_link_frac, min_link_gbps, link_mode);
   const bool full = !strcmp(level, "full");
   const size_t hbm_bytes = full ? (16ull << 30) : (1ull << 30);
   // quick: 1 GiB; full: every free byte of HBM but 4 GiB, in 16 GiB chunks held at once

@@ -60,12 +60,16 @@ def _lib():
     lib.tkp_memtest_span.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_size_t, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
     lib.tkp_set_async_free.argtypes = [ctypes.c_int]
+    lib.tkp_set_fail_point.argtypes = [ctypes.c_char_p]
+    lib.tkp_set_fail_point.restype = None
     lib.tkp_memtest_selfcheck.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                           ctypes.POINTER(ctypes.c_double)]
     lib.tkp_p2p_bandwidth.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                       ctypes.POINTER(ctypes.c_double)]
     lib.tkp_link_matrix.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    lib.tkp_link_matrix_mode.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                         ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.tkp_set_scratch_cache.argtypes = [ctypes.c_int]
     lib.tkp_prealloc_scratch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t]
     lib.tkp_release_scratch.restype = ctypes.c_longlong
@@ -160,6 +164,16 @@ def memtest_span(dev: int, nbytes: int = 0, chunk: int = 16 << 30, headroom: int
             "alloc_ms": round(out[4], 1), "test_ms": round(out[5], 1), "free_ms": round(out[6], 1)}
 
 
+def set_fail_point(name: str) -> None:
+    """Tests only: make the named step of the span memtest fail ("" clears it)."""
+    _lib().tkp_set_fail_point(name.encode())
+
+
+def free_bytes(dev: int) -> int:
+    """Free HBM of ``dev`` right now (``hipMemGetInfo``)."""
+    return int(device_info(dev).free_mem_gib * 2 ** 30)
+
+
 def set_async_free(on: bool) -> None:
     """Release the span memtest's chunks on a background thread (long-lived agents)."""
     _lib().tkp_set_async_free(1 if on else 0)
@@ -182,34 +196,47 @@ def p2p_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 5) -
     return {"gbps": out[0], "peer_access": bool(out[1])}
 
 
-def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3) -> Dict[str, Any]:
-    """Peer-to-peer copy bandwidth of every ordered GPU pair: ``{"pairs": {"i-j": GB/s},
-    "peer_access": {"i-j": bool}, "errors": [...]}``.  ``tkp_link_matrix`` measures the pairs
-    in rounds of a round-robin pairing: copies run concurrently only on disjoint pairs, so
-    each number is still one xGMI link's, not a share of a busy fabric (8 GPUs: 14 timed
-    slots instead of 56).  A pair whose copy fails is recorded as an error, not raised: the
-    caller decides (``node/labels.py:link_labels``)."""
+# MI355X: 7 xGMI links per GPU of ~153.6 GB/s (both directions together), so ~76.8 GB/s per
+# direction.  The link check fails a pair below half of that, whatever the node's median.
+XGMI_LINK_ONE_WAY_GBPS = 76.8
+DEFAULT_MIN_LINK_GBPS = 38.0
+LINK_METHODS = {"sdma-copy": 0, "kernel-read": 1}
+
+
+def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3,
+                method: str = "kernel-read") -> Dict[str, Any]:
+    """Peer bandwidth of every ordered GPU pair: ``{"pairs": {"i-j": GB/s}, "peer_access":
+    {"i-j": bool}, "errors": [...], "method": ...}``.  ``kernel-read`` (default): a kernel on
+    the receiving GPU reads the sender's memory over xGMI, the way RCCL and workloads use the
+    fabric; ``sdma-copy``: ``hipMemcpyPeerAsync`` on the copy engines.  ``tkp_link_matrix_mode``
+    measures the pairs in rounds of a round-robin pairing: transfers run concurrently only on
+    disjoint pairs, so each number is still one xGMI link's, not a share of a busy fabric
+    (8 GPUs: 14 timed slots instead of 56).  A pair that fails is recorded as an error, not
+    raised: the caller decides (``node/labels.py:link_labels``)."""
     devs = list(devices)
     n = len(devs)
     pairs: Dict[str, float] = {}
     access: Dict[str, bool] = {}
     errors: List[str] = []
+    if method not in LINK_METHODS:
+        raise ValueError(f"link method must be one of {sorted(LINK_METHODS)}")
     if n < 2:
-        return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes}
+        return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes, "method": method}
     gbps = (ctypes.c_double * (n * n))()
     acc = (ctypes.c_int * (n * n))()
-    _check(_lib().tkp_link_matrix((ctypes.c_int * n)(*devs), n, nbytes, iters, gbps, acc), "link_matrix")
+    _check(_lib().tkp_link_matrix_mode((ctypes.c_int * n)(*devs), n, nbytes, iters, LINK_METHODS[method], gbps, acc),
+           "link_matrix")
     for a, i in enumerate(devs):
         for b, j in enumerate(devs):
             if a == b:
                 continue
             v = gbps[a * n + b]
+            access[f"{i}-{j}"] = bool(acc[a * n + b]) or i == j
             if v < 0:
-                errors.append(f"{i}->{j}: peer copy failed")
+                errors.append(f"{i}->{j}: peer {'read' if method == 'kernel-read' else 'copy'} failed")
                 continue
             pairs[f"{i}-{j}"] = round(v, 1)
-            access[f"{i}-{j}"] = bool(acc[a * n + b])
-    return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes}
+    return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes, "method": method}
 
 
 # --- burn-in policy ------------------------------------------------------------------

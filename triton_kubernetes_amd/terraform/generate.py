@@ -1190,6 +1190,9 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)"),
         Var("gpu_link_min_frac", "0.5",
             "fail the node when a GPU pair's peer copy bandwidth is below this fraction of the node median"),
+        Var("gpu_link_min_gbps", "38",
+            "fail the node when a GPU pair's kernel-driven peer read is below this many GB/s (absolute floor: "
+            "half of one xGMI link's ~76.8 GB/s one way)"),
         Var("rccl_slim", "off",
             "on: build a single-target (gfx950) copy of the node's librccl for faster cold communicator init, "
             "verify it with a one-rank all-reduce, and run rccl-ready on it while it matches the installed "
@@ -1228,6 +1231,7 @@ resource "terraform_data" "install_mi355x_node" {{
       rccl_env_file                      = local.rccl_env_file
       rccl_min_busbw                     = var.rccl_min_busbw
       gpu_link_min_frac                  = var.gpu_link_min_frac
+      gpu_link_min_gbps                  = var.gpu_link_min_gbps
       rccl_slim                          = var.rccl_slim
     }})]
   }}

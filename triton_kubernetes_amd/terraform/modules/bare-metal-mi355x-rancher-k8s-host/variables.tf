@@ -130,6 +130,12 @@ variable "gpu_link_min_frac" {
   default     = "0.5"
 }
 
+variable "gpu_link_min_gbps" {
+  description = "fail the node when a GPU pair's kernel-driven peer read is below this many GB/s (absolute floor: half of one xGMI link's ~76.8 GB/s one way)"
+  type        = string
+  default     = "38"
+}
+
 variable "rccl_slim" {
   description = "on: build a single-target (gfx950) copy of the node's librccl for faster cold communicator init, verify it with a one-rank all-reduce, and run rccl-ready on it while it matches the installed librccl (a modified vendor binary: off by default)"
   type        = string

@@ -336,7 +336,7 @@ ${rccl_env_file}
 TK_RCCL_EOF
 } | sudo tee /etc/rccl/rccl.env >/dev/null
 %{ if gpu_count > 1 ~}
-$T/gpu-burnin --p2p --min-link-frac ${gpu_link_min_frac} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
+$T/gpu-burnin --p2p --min-link-frac ${gpu_link_min_frac} --min-link-gbps ${gpu_link_min_gbps} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
 cat /tmp/tk-link-labels | sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels >/dev/null
 set -a; . /etc/rccl/rccl.env; set +a
 $RCCL_READY --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
