@@ -31,7 +31,8 @@ def test_plan_steps_and_order():
     # burn-in precedes labels so the agent's topology prefetch overlaps it
     assert gpu.step_names() == ["firewall", "runtime", "hostname", "registry_login", "gpu_preflight",
                                 "gpu_burnin", "gpu_links", "gpu_labels", "rccl_env", "rccl_local", "agent"]
-    assert gpu.gpu == {"product": "MI355X", "count": 8, "burnin": "quick"}
+    assert gpu.gpu == {"product": "MI355X", "count": 8, "burnin": "quick", "physical": 8, "compute_partition": "spx",
+                       "memory_partition": "nps1"}
     # the single-target RCCL copy is opt-in (a modified vendor binary)
     assert "rccl-ready-slim" not in gpu.render_shell()
     slim = build_host_plan(dict(GPU_WORKER, rccl_slim="on"), "https://r", "t", "s", mi355x=True)
@@ -309,7 +310,8 @@ def test_shell_plan_carries_burnin_labels():
 
     cfg = {"hostname": "g", "rancher_host_labels": {"worker": "true"}, "gpu_count": 8, "gpu_burnin": "full"}
     script = build_host_plan(cfg, "https://r", "tok", "ca", mi355x=True).render_shell()
-    assert "gpu-burnin --all --level full --labels /tmp/tk-burnin-labels" in script
+    assert ("gpu-burnin --all --level full --compute-partition spx --memory-partition nps1 "
+            "--labels /tmp/tk-burnin-labels") in script
     assert f"sudo rm -f {BURNIN_LABEL_FILE}" in script
     assert f"[ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}" in script
 

@@ -30,6 +30,12 @@ def _values(names, filled):
             out[n] = "Zm9v" if filled else ""
         elif n == "rccl_min_busbw":
             out[n] = 150 if filled else 0
+        elif n == "gpu_partitions":
+            out[n] = 8 if filled else 1
+        elif n == "gpu_compute_partition":
+            out[n] = "cpx" if filled else "spx"
+        elif n == "gpu_memory_partition":
+            out[n] = "nps2" if filled else "nps1"
         else:
             out[n] = f"v-{n}" if filled else ""
     return out

@@ -173,6 +173,11 @@ def _mi355x_fields(ctx: Context) -> Dict:
         except ValueError as exc:
             raise ConfigError(f"gpu_link_min_frac must be a number between 0 and 1. Found '{frac}'.") from exc
         out["gpu_link_min_frac"] = frac
+    if s.is_set("gpu_compute_partition") or s.is_set("gpu_memory_partition"):
+        from ..node.partition import normalize
+
+        c, m = normalize(s.get_string("gpu_compute_partition") or None, s.get_string("gpu_memory_partition") or None)
+        out["gpu_compute_partition"], out["gpu_memory_partition"] = c, m
     if s.is_set("gpu_link_min_gbps"):
         floor = s.get_string("gpu_link_min_gbps")
         try:

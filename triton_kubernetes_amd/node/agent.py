@@ -244,7 +244,20 @@ class NodeAgent:
                 return self._exec_runtime(plan, step)
             return {"simulated": True}
         if a == "gpu_preflight":
-            return self._gpu_preflight(int(step.params.get("count", len(self.devices))))
+            out = self._gpu_preflight(int(step.params.get("count", len(self.devices))))
+            if "compute_partition" in step.params:
+                # the node must run the cluster's partition modes (node/partition.py): checked
+                # against the topology the labeller reads (prefetched by run_plan)
+                from .partition import check, normalize, topology_modes
+
+                want = normalize(step.params.get("compute_partition"), step.params.get("memory_partition"))
+                fut = ctx.get("topology_future")
+                have = topology_modes(fut.result() if fut is not None else self._topology())
+                problem = check(want, have)
+                if problem:
+                    raise StepFailed(step.name, problem)
+                out["partition"] = {"compute": want[0], "memory": want[1]}
+            return out
         if a == "gpu_labels":
             fut = ctx.get("topology_future")
             topo = fut.result() if fut is not None else self._topology()
@@ -258,13 +271,15 @@ class NodeAgent:
             return labels
         if a == "gpu_burnin":
             level = step.params.get("level", "quick")
+            parts = (step.params.get("compute_partition", "spx"), step.params.get("memory_partition", "nps1"))
             self._quiesce_gpus()
-            # every GPU of the node burns in concurrently (one host thread each;
-            # the probes pin their device per thread)
+            # every (logical) GPU of the node burns in concurrently (one host thread each;
+            # the probes pin their device per thread); floors scaled to a partition's share
             if len(self.devices) > 1:
-                results = dict(zip(self.devices, self._pool.map(lambda d: self._burnin(d, level), self.devices)))
+                results = dict(zip(self.devices, self._pool.map(lambda d: self._burnin(d, level, parts),
+                                                                self.devices)))
             else:
-                results = {d: self._burnin(d, level) for d in self.devices}
+                results = {d: self._burnin(d, level, parts) for d in self.devices}
             out = {}
             for dev in self.devices:
                 res = results[dev]
@@ -399,12 +414,12 @@ class NodeAgent:
 
             rccl.drain()
 
-    def _burnin(self, dev: int, level: str) -> Dict[str, Any]:
+    def _burnin(self, dev: int, level: str, parts=("spx", "nps1")) -> Dict[str, Any]:
         if self.burnin_override is not None:
             return self.burnin_override(dev, level)
         from ..ops import probe
 
-        return probe.run_burnin(dev, level).to_json()
+        return probe.run_burnin(dev, level, probe.Thresholds.for_partition(*parts)).to_json()
 
     def _register(self, plan: BootstrapPlan, ctx: Dict[str, Any]) -> Dict[str, Any]:
         roles = {"etcd": plan.role == "etcd", "controlplane": plan.role == "controlplane",

@@ -5,7 +5,9 @@ plus xGMI keys used for topology-aware scheduling:
 
 =====================================  =============================================
 ``amd.com/gpu.present``                ``true``
-``amd.com/gpu.count``                  GPUs on the node
+``amd.com/gpu.count``                  physical GPUs on the node (distinct PCI functions)
+``amd.com/gpu.logical-count``          schedulable GPUs: compute partitions (``amd.com/gpu``)
+``amd.com/gpu.partitions-per-gpu``     compute partitions per physical GPU (1 in SPX)
 ``amd.com/gpu.product-name``           e.g. ``MI355X`` (from the market name)
 ``amd.com/gpu.family``                 ``AI`` for Instinct parts
 ``amd.com/gpu.device-id``              PCI device id
@@ -16,7 +18,8 @@ plus xGMI keys used for topology-aware scheduling:
 ``amd.com/gpu.memory-partition``       ``nps1`` / ``nps4`` ...
 ``amd.com/xgmi.hive-id``               hive id shared by the node's GPUs (hex)
 ``amd.com/xgmi.links-per-gpu``         min xGMI peers over GPUs
-``amd.com/xgmi.fully-connected``       every GPU has an xGMI link to every other
+``amd.com/xgmi.fully-connected``       every GPU has an xGMI link to every other; only
+                                       claimed in SPX (node/partition.py)
 =====================================  =============================================
 
 Pods that need all 8 GPUs on one xGMI hive use node affinity on
@@ -73,10 +76,14 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     gpus: List[Dict[str, Any]] = doc.get("gpus") or []
     if not gpus:
         return {"amd.com/gpu.present": "false"}
+    physical = len({g.get("bdf") or f"#{i}" for i, g in enumerate(gpus)})  # = node/partition.physical_count
     labels: Dict[str, str] = {
         "amd.com/gpu.present": "true",
-        "amd.com/gpu.count": str(len(gpus)),
+        "amd.com/gpu.count": str(physical),
+        "amd.com/gpu.logical-count": str(len(gpus)),
     }
+    if len(gpus) % physical == 0:
+        labels["amd.com/gpu.partitions-per-gpu"] = str(len(gpus) // physical)
     names = {product_name(g.get("market_name", ""), g.get("device_id", "")) for g in gpus
              if g.get("market_name") or str(g.get("device_id", "")).lower() in DEVICE_PRODUCTS}
     if len(names) == 1:
@@ -97,8 +104,11 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     targets = {g.get("target_graphics_version") for g in gpus if g.get("target_graphics_version")}
     if len(targets) == 1:
         labels["amd.com/gpu.target"] = _label_value(targets.pop())
+    cmodes = set()
     for key, label in (("compute_partition", "compute-partition"), ("memory_partition", "memory-partition")):
         vals = {str(g.get(key, "")).lower() for g in gpus if g.get(key)}
+        if key == "compute_partition":
+            cmodes = set(vals)
         if len(vals) == 1:
             labels[f"amd.com/gpu.{label}"] = _label_value(vals.pop())
     hives = {g.get("xgmi_hive_id") for g in gpus if g.get("xgmi_hive_id") not in (None, "", "0x0")}
@@ -109,8 +119,11 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
         peers = {lk["peer"] for lk in g.get("links", []) if lk.get("type") == "XGMI"}
         xgmi_peers.append(len(peers))
     labels["amd.com/xgmi.links-per-gpu"] = str(min(xgmi_peers))
-    labels["amd.com/xgmi.fully-connected"] = "true" if len(gpus) > 1 and min(xgmi_peers) == len(gpus) - 1 \
-        else "false"
+    # a compute partition is not a whole GPU with its own xGMI links: the full-mesh claim
+    # (what multi-GPU pods are placed on) holds in SPX only
+    whole = cmodes <= {"spx"} and physical == len(gpus)
+    labels["amd.com/xgmi.fully-connected"] = "true" if whole and len(gpus) > 1 and \
+        min(xgmi_peers) == len(gpus) - 1 else "false"
     ecc = [int(g.get("ecc_uncorrectable", 0)) for g in gpus]
     labels["amd.com/gpu.ecc-uncorrectable"] = str(sum(ecc))
     return labels

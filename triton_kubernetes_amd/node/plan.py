@@ -179,28 +179,43 @@ fi""", {"install_url": install_url}))
                                {"registry": reg, "username": reg_user, "password": reg_pass}))
     label_args = ""
     if mi355x:
-        ngpu = int(cfg.get("gpu_count", 8) or 8)
+        from .partition import modes_of, partitions_per_gpu
+
+        physical = int(cfg.get("gpu_count", 8) or 8)
+        cpart, mpart = modes_of(cfg)
+        ngpu = physical * partitions_per_gpu(cpart)  # logical GPUs: amd.com/gpu units, RCCL ranks
         burnin = cfg.get("gpu_burnin", "quick")
         env = dict(cfg.get("rccl_env") or {})
-        plan.gpu = {"product": cfg.get("gpu_product", "MI355X"), "count": ngpu, "burnin": burnin}
+        plan.gpu = {"product": cfg.get("gpu_product", "MI355X"), "count": ngpu, "burnin": burnin,
+                    "physical": physical, "compute_partition": cpart, "memory_partition": mpart}
         plan.steps.append(Step("gpu_preflight", "gpu_preflight", f"""
 lsmod | grep -q '^amdgpu' || {{ echo 'amdgpu kernel module not loaded' >&2; exit 1; }}
 test -c /dev/kfd || {{ echo '/dev/kfd missing' >&2; exit 1; }}
 test -d /dev/dri || {{ echo '/dev/dri missing' >&2; exit 1; }}
-local found
+local found f m
 found=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
-[ "$found" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs, found $found render nodes" >&2; exit 1; }}
+[ "$found" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs ({physical} x {cpart}), found $found render nodes" >&2; exit 1; }}
+for f in /sys/class/drm/renderD*/device/current_compute_partition /sys/class/drm/renderD*/device/current_memory_partition; do
+  [ -r "$f" ] || continue
+  m=$(tr 'A-Z' 'a-z' < "$f")
+  case $f in
+    *compute*) [ "$m" = {cpart} ] || {{ echo "compute partition is $m, the cluster expects {cpart}" >&2; exit 1; }} ;;
+    *) [ "$m" = {mpart} ] || {{ echo "memory partition is $m, the cluster expects {mpart}" >&2; exit 1; }} ;;
+  esac
+done
 sudo usermod -aG video,render "$(id -un)" || true
-sudo rm -f {BURNIN_LABEL_FILE}""", {"count": ngpu}, gpu=True))
+sudo rm -f {BURNIN_LABEL_FILE}""", {"count": ngpu, "compute_partition": cpart, "memory_partition": mpart},
+                               gpu=True))
         # burn-in before labels: the agent discovers the topology concurrently
         # with the burn-in kernels and only joins it at the labels step
         if burnin != "off":
             plan.steps.append(Step("gpu_burnin", "gpu_burnin", f"""
 sudo mkdir -p /etc/triton-kubernetes
-{TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
+{TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} --compute-partition {cpart} --memory-partition {mpart} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
 sudo install -m 0644 /tmp/tk-burnin-labels {BURNIN_LABEL_FILE}""",
-                                   {"level": burnin}, gpu=True))
-        if ngpu > 1:
+                                   {"level": burnin, "compute_partition": cpart, "memory_partition": mpart},
+                                   gpu=True))
+        if physical > 1 and cpart == "spx":  # links are a whole GPU's (a partition has no own)
             # per-link xGMI health: kernel-driven peer read of every GPU pair against the
             # node's median (relative) and an absolute floor (a uniformly slow fabric)
             frac = float(cfg.get("gpu_link_min_frac", 0.5) or 0.5)

@@ -1191,6 +1191,7 @@ int main(int argc, char** argv) {
   double min_link_frac = 0.5;
   double min_link_gbps = 38.0;  // = ops/probe.py:DEFAULT_MIN_LINK_GBPS (half a link's one-way 76.8 GB/s)
   int link_mode = 1;            // --p2p-method kernel-read (default) | sdma-copy
+  const char* cpart = "spx";    // --compute-partition spx|dpx|qpx|cpx
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
   for (int i = 1; i < argc; ++i) {
@@ -1207,8 +1208,19 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--min-link-frac") && i + 1 < argc) min_link_frac = atof(argv[++i]);
     else if (!strcmp(argv[i], "--min-link-gbps") && i + 1 < argc) min_link_gbps = atof(argv[++i]);
     else if (!strcmp(argv[i], "--p2p-method") && i + 1 < argc) link_mode = strcmp(argv[++i], "sdma-copy") ? 1 : 0;
+    else if (!strcmp(argv[i], "--compute-partition") && i + 1 < argc) cpart = argv[++i];
+    else if (!strcmp(argv[i], "--memory-partition") && i + 1 < argc) ++i;  // pools are only shared concurrently
   }
   if (p2p) return p2p_main(labels_path, min_link_frac, min_link_gbps, link_mode);
+  // a compute partition has 1/k of the chip's CUs (node/partition.py:compute_share): the
+  // throughput floors scale with it; the devices run one after another, so each may hold
+  // its memory pool alone for the memtest
+  const int parts = !strcmp(cpart, "cpx") ? 8 : !strcmp(cpart, "qpx") ? 4 : !strcmp(cpart, "dpx") ? 2 : 1;
+  min_read /= parts;
+  min_bf16 /= parts;
+  min_fp8 /= parts;
+  min_gemm /= parts;
+  min_gemm8 /= parts;
   const bool full = !strcmp(level, "full");
   const size_t hbm_bytes = full ? (16ull << 30) : (1ull << 30);
   // quick: 1 GiB; full: every free byte of HBM but 4 GiB, in 16 GiB chunks held at once

@@ -577,7 +577,14 @@ std::string render_labels(const Topology& t) {
     L["amd.com/gpu.present"] = "false";
   } else {
     L["amd.com/gpu.present"] = "true";
-    L["amd.com/gpu.count"] = std::to_string(gs.size());
+    // physical GPUs = distinct PCI functions (a GPU's compute partitions share one);
+    // = node/labels.py and node/partition.py:physical_count
+    std::set<std::string> bdfs;
+    for (size_t i = 0; i < gs.size(); ++i) bdfs.insert(gs[i].bdf.empty() ? "#" + std::to_string(i) : gs[i].bdf);
+    const size_t physical = bdfs.size();
+    L["amd.com/gpu.count"] = std::to_string(physical);
+    L["amd.com/gpu.logical-count"] = std::to_string(gs.size());
+    if (gs.size() % physical == 0) L["amd.com/gpu.partitions-per-gpu"] = std::to_string(gs.size() / physical);
     std::set<std::string> names, dev_ids, targets, cparts, mparts, hives;
     int64_t min_cu = INT64_MAX;
     uint64_t min_vram = UINT64_MAX;
@@ -612,7 +619,9 @@ std::string render_labels(const Topology& t) {
     if (mparts.size() == 1) L["amd.com/gpu.memory-partition"] = label_value(*mparts.begin());
     if (hives.size() == 1) L["amd.com/xgmi.hive-id"] = label_value(*hives.begin());
     L["amd.com/xgmi.links-per-gpu"] = std::to_string(min_xgmi);
-    L["amd.com/xgmi.fully-connected"] = (gs.size() > 1 && min_xgmi == gs.size() - 1) ? "true" : "false";
+    // a compute partition is not a whole GPU with its own xGMI links: SPX only
+    const bool whole = (cparts.empty() || (cparts.size() == 1 && *cparts.begin() == "spx")) && physical == gs.size();
+    L["amd.com/xgmi.fully-connected"] = (whole && gs.size() > 1 && min_xgmi == gs.size() - 1) ? "true" : "false";
     L["amd.com/gpu.ecc-uncorrectable"] = std::to_string(ecc);
   }
   // inter-node fabric: active RDMA ports

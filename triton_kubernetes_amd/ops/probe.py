@@ -260,6 +260,18 @@ class Thresholds:
     min_gemm_fp8_frac: float = 0.30
     require_gfx950: bool = True
     min_cus: int = MI355X_CUS
+    # a compute partition's share of the chip (node/partition.py): scales every throughput
+    # floor and the CU minimum; mem_share: its share of the HBM pool it allocates from
+    # (sizes the full memtest when partitions of one pool are tested concurrently)
+    share: float = 1.0
+    mem_share: float = 1.0
+
+    @classmethod
+    def for_partition(cls, compute: str = "spx", memory: str = "nps1") -> "Thresholds":
+        from ..node.partition import compute_share, memory_share, normalize
+
+        c, m = normalize(compute, memory)
+        return cls(min_cus=int(MI355X_CUS * compute_share(c)), share=compute_share(c), mem_share=memory_share(c, m))
 
 
 @dataclass
@@ -311,21 +323,21 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
         return r
 
     with span("burnin.hbm", dev=dev):
-        floor = th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS
+        floor = th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS * th.share
         res.hbm = best(lambda: hbm_bandwidth(dev, hbm_bytes, hbm_iters), lambda r: r["read_gbps"], floor, "hbm")
     if res.hbm["read_gbps"] < floor:
         res.failures.append(f"HBM read {res.hbm['read_gbps']:.0f} GB/s below "
                             f"{th.min_read_frac:.0%} of {MI355X_HBM_ACHIEVABLE_GBPS:.0f}")
     with span("burnin.mfma_bf16", dev=dev):
         res.mfma["bf16"] = best(lambda: mfma_peak(dev, "bf16", mfma_iters), lambda r: r["tflops"],
-                                th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS, "mfma_bf16")
+                                th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS * th.share, "mfma_bf16")
     with span("burnin.mfma_fp8", dev=dev):
         res.mfma["fp8"] = best(lambda: mfma_peak(dev, "fp8", mfma_iters // 2), lambda r: r["tflops"],
-                               th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS, "mfma_fp8")
-    if res.mfma["bf16"]["tflops"] < th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS:
+                               th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS * th.share, "mfma_fp8")
+    if res.mfma["bf16"]["tflops"] < th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS * th.share:
         res.failures.append(f"bf16 MFMA {res.mfma['bf16']['tflops']:.0f} TF below "
                             f"{th.min_bf16_frac:.0%} of dense peak")
-    if res.mfma["fp8"]["tflops"] < th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS:
+    if res.mfma["fp8"]["tflops"] < th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS * th.share:
         res.failures.append(f"fp8 MFMA {res.mfma['fp8']['tflops']:.0f} TF below "
                             f"{th.min_fp8_frac:.0%} of dense peak")
     from . import gemm
@@ -341,6 +353,7 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
             runs.append(g)
             return g
 
+        peak = peak * th.share
         with span(f"burnin.gemm_{dtype}", dev=dev):
             g = best(screen_once, lambda r: r.tflops, frac * peak, f"gemm_{dtype}")
         if dtype == "bf16":
@@ -357,6 +370,11 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
         if mt_bytes:
             res.memtest = memtest(dev, mt_bytes, mt_passes)
             res.memtest.update(bytes=mt_bytes, hbm_bytes=int(info.total_mem_gib * (1 << 30)))
+        elif th.mem_share < 1.0:
+            # concurrent partitions share one pool: each holds its share of what is free
+            headroom = max(512 << 20, int((4 << 30) * th.mem_share))
+            span_bytes = max(1 << 30, int(free_bytes(dev) * th.mem_share) - headroom)
+            res.memtest = memtest_span(dev, span_bytes, passes=mt_passes)
         else:
             res.memtest = memtest_span(dev, 0, passes=mt_passes)
     if res.memtest["errors"]:

@@ -175,14 +175,17 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
     rccl_ndev: List[int] = []
     proc_hosts: List[HostRef] = []
     proc_ndev: List[int] = []
+    from ..node.partition import logical_gpus
+
     for host in sorted(nodes):
         cfg = state.module(nodes[host]) or {}
         info = module_from_source(str(cfg.get("source", "")))
         if info is not None and info.mi355x:
+            # amd.com/gpu and RCCL ranks count logical GPUs: gpu_count x compute partitions
+            n = logical_gpus(cfg)
             if has_plugin:
-                gpu_nodes[host] = int(cfg.get("gpu_count", 8))
+                gpu_nodes[host] = n
             addr = str(cfg.get("host", ""))
-            n = int(cfg.get("gpu_count", 8) or 8)
             if addr.startswith("agent+"):
                 rccl_hosts.append(addr[len("agent+"):])
                 rccl_ndev.append(n)
@@ -204,7 +207,7 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
                 addr = str(cfg["host"])
                 ref = HostRef(addr, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
                               cfg.get("bastion_host") or "")
-                mixed.append((ref, int(cfg.get("gpu_count", 8) or 8)))
+                mixed.append((ref, logical_gpus(cfg)))
             proc_hosts, proc_ndev = [m[0] for m in mixed], [m[1] for m in mixed]
             rccl_hosts, rccl_ndev = [], []
         elif not (rccl_hosts or proc_hosts):

@@ -150,6 +150,10 @@ VAR_VALIDATIONS = {
                              "k8s_network_provider must be one of calico, flannel, canal, weave."),
     "gpu_burnin": ('contains(["quick", "full", "off"], var.gpu_burnin)', "gpu_burnin must be quick, full or off."),
     "rccl_slim": ('contains(["on", "off"], var.rccl_slim)', "rccl_slim must be on or off."),
+    "gpu_compute_partition": ('contains(["spx", "dpx", "qpx", "cpx"], var.gpu_compute_partition)',
+                              "gpu_compute_partition must be one of spx, dpx, qpx, cpx."),
+    "gpu_memory_partition": ('contains(["nps1", "nps2"], var.gpu_memory_partition)',
+                             "gpu_memory_partition must be nps1 or nps2."),
     "rancher_host_labels": ('length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], '
                             'keys(var.rancher_host_labels)[0])',
                             "rancher_host_labels must hold exactly one of worker, etcd or control."),
@@ -1190,6 +1194,10 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)"),
         Var("gpu_link_min_frac", "0.5",
             "fail the node when a GPU pair's peer copy bandwidth is below this fraction of the node median"),
+        Var("gpu_compute_partition", "spx",
+            "compute partition mode every GPU of the node must run in (spx | dpx | qpx | cpx); "
+            "amd.com/gpu = gpu_count x partitions per GPU"),
+        Var("gpu_memory_partition", "nps1", "memory partition mode every GPU of the node must run in (nps1 | nps2)"),
         Var("gpu_link_min_gbps", "38",
             "fail the node when a GPU pair's kernel-driven peer read is below this many GB/s (absolute floor: "
             "half of one xGMI link's ~76.8 GB/s one way)"),
@@ -1232,6 +1240,9 @@ resource "terraform_data" "install_mi355x_node" {{
       rccl_min_busbw                     = var.rccl_min_busbw
       gpu_link_min_frac                  = var.gpu_link_min_frac
       gpu_link_min_gbps                  = var.gpu_link_min_gbps
+      gpu_compute_partition              = var.gpu_compute_partition
+      gpu_memory_partition               = var.gpu_memory_partition
+      gpu_partitions                     = lookup({{ spx = 1, dpx = 2, qpx = 4, cpx = 8 }}, var.gpu_compute_partition, 1)
       rccl_slim                          = var.rccl_slim
     }})]
   }}

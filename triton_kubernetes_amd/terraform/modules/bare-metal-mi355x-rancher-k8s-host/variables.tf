@@ -130,6 +130,28 @@ variable "gpu_link_min_frac" {
   default     = "0.5"
 }
 
+variable "gpu_compute_partition" {
+  description = "compute partition mode every GPU of the node must run in (spx | dpx | qpx | cpx); amd.com/gpu = gpu_count x partitions per GPU"
+  type        = string
+  default     = "spx"
+
+  validation {
+    condition     = contains(["spx", "dpx", "qpx", "cpx"], var.gpu_compute_partition)
+    error_message = "gpu_compute_partition must be one of spx, dpx, qpx, cpx."
+  }
+}
+
+variable "gpu_memory_partition" {
+  description = "memory partition mode every GPU of the node must run in (nps1 | nps2)"
+  type        = string
+  default     = "nps1"
+
+  validation {
+    condition     = contains(["nps1", "nps2"], var.gpu_memory_partition)
+    error_message = "gpu_memory_partition must be nps1 or nps2."
+  }
+}
+
 variable "gpu_link_min_gbps" {
   description = "fail the node when a GPU pair's kernel-driven peer read is below this many GB/s (absolute floor: half of one xGMI link's ~76.8 GB/s one way)"
   type        = string

@@ -303,7 +303,16 @@ sudo mkdir -p $T /etc/triton-kubernetes /etc/rccl
 lsmod | grep -q '^amdgpu' || { echo 'amdgpu kernel module not loaded' >&2; exit 1; }
 test -c /dev/kfd || { echo '/dev/kfd missing' >&2; exit 1; }
 n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
-[ "$n" -ge ${gpu_count} ] || { echo "expected ${gpu_count} GPUs, found $n" >&2; exit 1; }
+[ "$n" -ge ${gpu_count * gpu_partitions} ] || { echo "expected ${gpu_count * gpu_partitions} GPUs (${gpu_count} x ${gpu_compute_partition}), found $n render nodes" >&2; exit 1; }
+# partition modes: verified, never changed here (repartitioning resets the GPUs)
+for f in /sys/class/drm/renderD*/device/current_compute_partition /sys/class/drm/renderD*/device/current_memory_partition; do
+  [ -r "$f" ] || continue
+  m=$(tr 'A-Z' 'a-z' < "$f")
+  case $f in
+    *compute*) [ "$m" = '${gpu_compute_partition}' ] || { echo "compute partition is $m, the cluster expects ${gpu_compute_partition}" >&2; exit 1; } ;;
+    *) [ "$m" = '${gpu_memory_partition}' ] || { echo "memory partition is $m, the cluster expects ${gpu_memory_partition}" >&2; exit 1; } ;;
+  esac
+done
 sudo usermod -aG video,render "$(id -un)" || true
 ROCM=$${ROCM_PATH:-/opt/rocm}
 build() { # name, compiler, flags...
@@ -328,18 +337,20 @@ $T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/de
 $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
 sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels
 %{ if gpu_burnin != "off" ~}
-$T/gpu-burnin --all --level '${gpu_burnin}' --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
+$T/gpu-burnin --all --level '${gpu_burnin}' --compute-partition ${gpu_compute_partition} --memory-partition ${gpu_memory_partition} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
 sudo install -m 0644 /tmp/tk-burnin-labels /etc/triton-kubernetes/gpu-burnin-labels
 %{ endif ~}
 { $T/amdgpu-topo-labeller --rccl-env || true; cat <<'TK_RCCL_EOF'
 ${rccl_env_file}
 TK_RCCL_EOF
 } | sudo tee /etc/rccl/rccl.env >/dev/null
-%{ if gpu_count > 1 ~}
+%{ if gpu_count > 1 && gpu_compute_partition == "spx" ~}
 $T/gpu-burnin --p2p --min-link-frac ${gpu_link_min_frac} --min-link-gbps ${gpu_link_min_gbps} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
 cat /tmp/tk-link-labels | sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels >/dev/null
+%{ endif ~}
+%{ if gpu_count * gpu_partitions > 1 ~}
 set -a; . /etc/rccl/rccl.env; set +a
-$RCCL_READY --ngpus ${gpu_count} --min-busbw ${rccl_min_busbw}
+$RCCL_READY --ngpus ${gpu_count * gpu_partitions} --min-busbw ${rccl_min_busbw}
 %{ endif ~}
 labels=$(cat /etc/triton-kubernetes/gpu-labels $([ -r /etc/triton-kubernetes/gpu-burnin-labels ] && echo /etc/triton-kubernetes/gpu-burnin-labels) | sed 's/^/--label /' | tr '\n' ' ')
 """ + DOCKER_INSTALL + r"""
