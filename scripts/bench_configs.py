@@ -142,11 +142,11 @@ def config4(runs):
     backend = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://tr.example", manta.url)
     wf.new_manager(ctx_of(dict(triton, backend_provider="manta", executor="terraform", manager_cloud_provider="triton",
                                name="tmgr", rancher_admin_password="tk-admin-pw-0123",
-                               master_triton_machine_package="k4-highcpu-kvm-1.75G"), cloud=cloud), backend)
+                               master_triton_machine_package="k4-highcpu-kvm-7.75G"), cloud=cloud), backend)
 
     def cluster(i):
         nodes = [{"rancher_host_label": lbl, "node_count": n, "hostname": f"t{i}-{lbl}",
-                  "triton_machine_package": "k4-highcpu-kvm-1.75G", **{k: triton[k] for k in (
+                  "triton_machine_package": "k4-highcpu-kvm-7.75G", **{k: triton[k] for k in (
                       "triton_network_names", "triton_image_name", "triton_image_version", "triton_ssh_user")}}
                  for lbl, n in (("etcd", 1), ("control", 1), ("worker", 6))]
         wf.new_cluster(ctx_of(dict(triton, backend_provider="manta", executor="terraform", cluster_manager="tmgr",

@@ -188,7 +188,7 @@ def _triton_vals(key):
 def test_triton_manager_cluster_node(key):
     cloud = FakeCloud()
     st = State("mgr")
-    triton.new_manager(make_ctx(dict(BASE_MGR, master_triton_machine_package="k4-highcpu-kvm-1.75G",
+    triton.new_manager(make_ctx(dict(BASE_MGR, master_triton_machine_package="k4-highcpu-kvm-7.75G",
                                      **_triton_vals(key)), cloud=cloud), st, "mgr")
     m = st.manager()
     from triton_kubernetes_amd.utils.sshkeys import load_private_key
@@ -208,14 +208,14 @@ def test_triton_manager_cluster_node(key):
 def test_triton_validation_errors(key):
     cloud = FakeCloud()
     st = State("mgr")
-    vals = dict(BASE_MGR, master_triton_machine_package="k4-highcpu-kvm-1.75G", **_triton_vals(key))
+    vals = dict(BASE_MGR, master_triton_machine_package="k4-highcpu-kvm-7.75G", **_triton_vals(key))
     vals["triton_network_names"] = ["nope"]
     assert _err(triton.new_manager, make_ctx(vals, cloud=cloud), st, "m") == \
         "Invalid Triton Network 'nope', must be one of the following: Joyent-SDC-Public, Joyent-SDC-Private, My-Fabric"
     vals = dict(BASE_MGR, master_triton_machine_package="huge", **_triton_vals(key))
     assert _err(triton.new_manager, make_ctx(vals, cloud=cloud), st, "m") == \
         "Invalid Master Triton Machine Package 'huge'"
-    vals = dict(BASE_MGR, master_triton_machine_package="k4-highcpu-kvm-1.75G", **_triton_vals(key))
+    vals = dict(BASE_MGR, master_triton_machine_package="k4-highcpu-kvm-7.75G", **_triton_vals(key))
     vals["triton_image_version"] = "1999"
     assert _err(triton.new_manager, make_ctx(vals, cloud=cloud), st, "m") == \
         "Invalid Triton Image Name and Version 'ubuntu-certified-16.04@1999'"
@@ -241,7 +241,7 @@ def test_aws_manager_cluster_node(tmp_path):
     cloud = FakeCloud()
     st = State("mgr")
     aws.new_manager(make_ctx(dict(BASE_MGR, aws_private_key_path="~/.ssh/id_rsa", aws_ssh_user="ubuntu",
-                                  aws_ami_id="ami-1", aws_instance_type="t2.micro", **AWS), cloud=cloud), st, "mgr")
+                                  aws_ami_id="ami-1", aws_instance_type="t3.medium", **AWS), cloud=cloud), st, "mgr")
     assert list(st.manager())[-11:] == ["aws_access_key", "aws_secret_key", "aws_region", "aws_vpc_cidr",
                                         "aws_subnet_cidr", "aws_public_key_path", "aws_private_key_path",
                                         "aws_key_name", "aws_ssh_user", "aws_ami_id", "aws_instance_type"]
@@ -299,7 +299,7 @@ def test_gcp_manager_cluster_node(gcp_creds, key, tmp_path):
     pub = tmp_path / "k.pub"
     pub.write_text("ssh-rsa AAAA")
     gcp.new_manager(make_ctx(dict(BASE_MGR, gcp_path_to_credentials=gcp_creds, gcp_compute_region="us-central1",
-                                  gcp_instance_zone="us-central1-a", gcp_machine_type="n1-standard-1",
+                                  gcp_instance_zone="us-central1-a", gcp_machine_type="n1-standard-2",
                                   gcp_image="ubuntu-1604-xenial-v20180222", gcp_public_key_path=str(pub),
                                   gcp_private_key_path=key, gcp_ssh_user="ubuntu"), cloud=cloud), st, "mgr")
     assert st.manager()["gcp_project_id"] == "my-project"
@@ -326,7 +326,7 @@ def test_azure_manager_cluster_node(tmp_path, key):
     st = State("mgr")
     pub = tmp_path / "k.pub"
     pub.write_text("ssh-rsa AAAA")
-    azure.new_manager(make_ctx(dict(BASE_MGR, azure_size="Standard_A0", azure_ssh_user="ubuntu",
+    azure.new_manager(make_ctx(dict(BASE_MGR, azure_size="Standard_D4s_v5", azure_ssh_user="ubuntu",
                                     azure_public_key_path=str(pub), azure_private_key_path=key, **AZ), cloud=cloud),
                       st, "mgr")
     assert st.manager()["azure_resource_group_name"] == ""
@@ -338,7 +338,7 @@ def test_azure_manager_cluster_node(tmp_path, key):
     n = st.module(f"node_azure_dev_{hosts[0]}")
     assert n["azure_subnet_id"] == "${module.cluster_azure_dev.azure_subnet_id}" and n["azure_disk_size"] == "100"
     assert_blocks_match_modules(st)
-    bad = make_ctx(dict(NODE_BASE, azure_size="Standard_A0", azure_ssh_user="u", azure_public_key_path=str(pub),
+    bad = make_ctx(dict(NODE_BASE, azure_size="Standard_D4s_v5", azure_ssh_user="u", azure_public_key_path=str(pub),
                         azure_disk_mount_path="/data"), cloud=cloud)
     assert _err(azure.new_node, bad, "m", ckey, None, st) == \
         "If azure_disk_mount_path is set, then azure_disk_size must also be set."

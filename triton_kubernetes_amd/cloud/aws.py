@@ -17,7 +17,9 @@ from typing import Dict, List, Optional
 from .http import HTTPClient
 
 EC2_API_VERSION = "2016-11-15"
-UBUNTU_AMI_FILTER = "*hvm-ssd/ubuntu-xenial-16.04-amd64-server*"
+# Ubuntu 22.04 LTS, which the pinned Docker 24.0 installer supports (sizing.py); the
+# reference filtered xenial 16.04 for its Docker 17.03 (create/manager_aws.go:426-436)
+from ..sizing import AWS_AMI_FILTER as UBUNTU_AMI_FILTER  # noqa: E402
 
 
 def _sign(key: bytes, msg: str) -> bytes:

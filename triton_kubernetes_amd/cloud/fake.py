@@ -15,6 +15,7 @@ class FakeTriton:
     images_: List[Image] = field(default_factory=lambda: [
         Image("i1", "ubuntu-certified-16.04", "20180222", "2018-02-22T00:00:00Z"),
         Image("i2", "ubuntu-certified-18.04", "20180808", "2018-08-08T00:00:00Z"),
+        Image("i3", "ubuntu-certified-22.04", "20240301", "2024-03-01T00:00:00Z"),
     ])
     packages_: List[Package] = field(default_factory=lambda: [
         Package("p2", "k4-highcpu-kvm-7.75G", 7936), Package("p1", "k4-highcpu-kvm-1.75G", 1792)])
@@ -38,8 +39,8 @@ class FakeEC2:
     regions_: List[str] = field(default_factory=lambda: ["us-east-1", "us-west-1", "us-west-2", "eu-west-1"])
     key_pairs_: List[str] = field(default_factory=lambda: ["existing-key"])
     amis_: List[AMI] = field(default_factory=lambda: [
-        AMI("ami-0001", "ubuntu/images/hvm-ssd/ubuntu-xenial-16.04-amd64-server-20180101", "2018-01-01"),
-        AMI("ami-0002", "ubuntu/images/hvm-ssd/ubuntu-xenial-16.04-amd64-server-20180301", "2018-03-01"),
+        AMI("ami-0001", "ubuntu/images/hvm-ssd/ubuntu-jammy-22.04-amd64-server-20240101", "2024-01-01"),
+        AMI("ami-0002", "ubuntu/images/hvm-ssd/ubuntu-jammy-22.04-amd64-server-20240301", "2024-03-01"),
     ])
 
     def regions(self):
@@ -61,10 +62,11 @@ class FakeGCP:
     regions_: List[str] = field(default_factory=lambda: ["us-central1", "us-east1"])
     zones_: Dict[str, List[str]] = field(default_factory=lambda: {
         "us-central1": ["us-central1-a", "us-central1-b"], "us-east1": ["us-east1-b"]})
-    machine_types_: List[str] = field(default_factory=lambda: ["n1-standard-1", "n1-standard-2"])
+    machine_types_: List[str] = field(default_factory=lambda: ["n1-standard-1", "n1-standard-2", "n1-standard-4"])
     images_: List[GCPImage] = field(default_factory=lambda: [
         GCPImage("ubuntu-1604-xenial-v20180222", "", "2018-02-22"),
-        GCPImage("ubuntu-1804-bionic-v20180808", "", "2018-08-08")])
+        GCPImage("ubuntu-1804-bionic-v20180808", "", "2018-08-08"),
+        GCPImage("ubuntu-2204-jammy-v20240301", "", "2024-03-01")])
 
     def regions(self):
         return list(self.regions_)
@@ -82,7 +84,7 @@ class FakeGCP:
 @dataclass
 class FakeAzure:
     locations_: List[str] = field(default_factory=lambda: ["westus2", "eastus"])
-    sizes_: List[str] = field(default_factory=lambda: ["Standard_A0", "Standard_D2_v2"])
+    sizes_: List[str] = field(default_factory=lambda: ["Standard_A0", "Standard_D2_v2", "Standard_D4s_v5"])
 
     def locations(self):
         return list(self.locations_)

@@ -11,6 +11,7 @@ import re
 from typing import Dict, List
 
 from ..config.context import Context, expand_home, file_exists, not_blank
+from .. import sizing
 from ..errors import ConfigError
 from ..state import State
 from .cloudctx import cloud, validation_enabled
@@ -105,9 +106,13 @@ def _ami(ctx: Context, ec2) -> str:
     return amis[idx].id
 
 
-def _instance_type(ctx: Context) -> str:
-    return ctx.resolve("aws_instance_type", "AWS Instance Type", default="t2.micro",
-                       validate=not_blank("Invalid Instance Type"))
+def _instance_type(ctx: Context, kind: str) -> str:
+    """Default from ``sizing.py`` (the module variable's default too): t3.medium for the
+    Rancher server, t3.large for nodes; a type known to be too small is refused."""
+    value = ctx.resolve("aws_instance_type", "AWS Instance Type", default=sizing.default_size("aws", kind)[1],
+                        validate=not_blank("Invalid Instance Type"))
+    sizing.check_size("aws", kind, value)
+    return value
 
 
 def _ec2(ctx: Context, creds: Dict[str, str], region: str):
@@ -136,7 +141,7 @@ def new_manager(ctx: Context, state: State, name: str) -> None:
         "aws_key_name": key["aws_key_name"],
         "aws_ssh_user": ssh_user,
         "aws_ami_id": _ami(ctx, ec2),
-        "aws_instance_type": _instance_type(ctx),
+        "aws_instance_type": _instance_type(ctx, "manager"),
     })
     state.set_manager(cfg)
 
@@ -204,7 +209,7 @@ def new_node(ctx: Context, manager: str, cluster: str, backend, state: State) ->
         "aws_security_group_id": f"${{module.{cluster}.aws_security_group_id}}",
         "aws_key_name": f"${{module.{cluster}.aws_key_name}}",
         "aws_ami_id": _ami(ctx, ec2),
-        "aws_instance_type": _instance_type(ctx),
+        "aws_instance_type": _instance_type(ctx, "host"),
     })
     ebs = _ebs(ctx)
     extra.update({"ebs_volume_device_name": ebs["ebs_volume_device_name"],

@@ -11,6 +11,7 @@ from typing import Dict, List, Optional
 
 from ..cloud.azure import ENVIRONMENTS
 from ..config.context import Context, expand_home, file_exists, not_blank
+from .. import sizing
 from ..errors import ConfigError
 from ..state import State
 from .cloudctx import cloud, validation_enabled
@@ -66,8 +67,10 @@ def _location(ctx: Context, api) -> str:
     return _validated(ctx, "azure_location", "Azure Location", api.locations() if api else None)
 
 
-def _size(ctx: Context, api, location: str) -> str:
-    return _validated(ctx, "azure_size", "Azure Size", api.vm_sizes(location) if api else None)
+def _size(ctx: Context, api, location: str, kind: str) -> str:
+    value = _validated(ctx, "azure_size", "Azure Size", api.vm_sizes(location) if api else None)
+    sizing.check_size("azure", kind, value)
+    return value
 
 
 def _ssh(ctx: Context, with_private: bool) -> Dict[str, str]:
@@ -85,7 +88,7 @@ def new_manager(ctx: Context, state: State, name: str) -> None:
     creds = _creds(ctx)
     api = _api(ctx, creds)
     location = _location(ctx, api)
-    size = _size(ctx, api, location)
+    size = _size(ctx, api, location, "manager")
     ssh = _ssh(ctx, with_private=True)
     cfg.update(creds)
     cfg.update({"azure_location": location, "azure_resource_group_name": "", "azure_size": size})
@@ -133,7 +136,7 @@ def new_node(ctx: Context, manager: str, cluster: str, backend, state: State) ->
         "azure_resource_group_name": f"${{module.{cluster}.azure_resource_group_name}}",
         "azure_network_security_group_id": f"${{module.{cluster}.azure_network_security_group_id}}",
         "azure_subnet_id": f"${{module.{cluster}.azure_subnet_id}}",
-        "azure_size": _size(ctx, api, creds["azure_location"]),
+        "azure_size": _size(ctx, api, creds["azure_location"], "host"),
     })
     extra.update(_ssh(ctx, with_private=False))
     extra.update(_disk(ctx))

@@ -12,6 +12,7 @@ host module attaches the disk.
 from typing import Dict, List, Optional
 
 from ..config.context import Context, expand_home, file_exists
+from .. import sizing
 from ..errors import ConfigError
 from ..state import State
 from ..cloud.gcp import project_id_from_credentials
@@ -56,11 +57,12 @@ def _region(ctx: Context, api) -> str:
                  "Compute Region")
 
 
-def _instance(ctx: Context, api, region: str) -> Dict[str, str]:
+def _instance(ctx: Context, api, region: str, kind: str) -> Dict[str, str]:
     zone = _pick(ctx, "gcp_instance_zone", "GCP Instance Zone", api.zones(region) if api else None,
                  "Instance Zone")
     mtype = _pick(ctx, "gcp_machine_type", "GCP Machine Type", api.machine_types(zone) if api else None,
                   "Machine Type")
+    sizing.check_size("gcp", kind, mtype)
     image = _pick(ctx, "gcp_image", "GCP Image", [i.name for i in api.images()] if api else None, "Image")
     return {"gcp_machine_type": mtype, "gcp_instance_zone": zone, "gcp_image": image}
 
@@ -70,7 +72,7 @@ def new_manager(ctx: Context, state: State, name: str) -> None:
     creds = _credentials(ctx)
     api = _api(ctx, creds)
     region = _region(ctx, api)
-    inst = _instance(ctx, api, region)
+    inst = _instance(ctx, api, region, "manager")
     pub = ctx.resolve("gcp_public_key_path", "GCP Public Key Path", default="~/.ssh/id_rsa.pub",
                       validate=file_exists())
     priv = ctx.resolve("gcp_private_key_path", "GCP Private Key Path", default="~/.ssh/id_rsa",
@@ -117,6 +119,6 @@ def new_node(ctx: Context, manager: str, cluster: str, backend, state: State) ->
         "gcp_compute_network_name": f"${{module.{cluster}.gcp_compute_network_name}}",
         "gcp_compute_firewall_host_tag": f"${{module.{cluster}.gcp_compute_firewall_host_tag}}",
     })
-    extra.update(_instance(ctx, api, creds["gcp_compute_region"]))
+    extra.update(_instance(ctx, api, creds["gcp_compute_region"], "host"))
     extra.update(_disk(ctx))
     return add_nodes(state, cluster, base, extra)

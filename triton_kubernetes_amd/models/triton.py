@@ -11,6 +11,7 @@ from typing import Dict, List, Optional
 
 from ..backend.select import resolve_triton_key_id
 from ..config.context import Context, expand_home, file_exists, not_blank
+from .. import sizing
 from ..errors import ConfigError
 from ..state import State
 from .cloudctx import cloud, validation_enabled
@@ -72,16 +73,20 @@ def _image(ctx: Context, api) -> Dict[str, str]:
 
 def _package(ctx: Context, api, key: str, label: str, invalid: str) -> str:
     packages = api.packages() if api is not None else None
+    kind = "manager" if key.startswith("master_") else "host"
     if ctx.is_set(key):
         value = ctx.get_string(key)
         if packages is not None and not any(p.name == value for p in packages):
             raise ConfigError(f"{invalid} '{value}'")
-        return value
-    if ctx.non_interactive:
+    elif ctx.non_interactive:
         raise ConfigError(f"{key} must be specified")
-    if not packages:
-        return ctx.prompter.prompt(label)
-    _, value = ctx.prompter.select(label, [p.name for p in packages], searchable=True)
+    elif not packages:
+        value = ctx.prompter.prompt(label, default=sizing.default_size("triton", kind)[1])
+    else:
+        _, value = ctx.prompter.select(label, [p.name for p in packages], searchable=True)
+    # the package listing knows the memory (MB); otherwise the known sizes table
+    mem = next((p.memory / 1024.0 for p in packages or [] if p.name == value and p.memory), None)
+    sizing.check_size("triton", kind, value, mem)
     return value
 
 

@@ -9,6 +9,7 @@ Deliberate fix: node CPU / memory are configurable
 
 from typing import Dict, List
 
+from .. import sizing
 from ..config.context import Context, expand_home, file_exists, not_blank
 from ..state import State
 from .common import add_nodes, base_cluster_config, base_node_config, omit_empty
@@ -51,5 +52,7 @@ def new_node(ctx: Context, manager: str, cluster: str, backend, state: State) ->
     for key in ("vsphere_num_cpus", "vsphere_memory_mb"):
         if ctx.is_set(key):
             extra[key] = ctx.get_string(key)
+    if "vsphere_memory_mb" in extra:
+        sizing.check_size("vsphere", "host", extra["vsphere_memory_mb"])
     omit_empty(extra, ["vsphere_user", "vsphere_password", "vsphere_server", "vsphere_template_name"])
     return add_nodes(state, cluster, base, extra)

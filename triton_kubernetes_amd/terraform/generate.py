@@ -29,7 +29,7 @@ import sys
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
-from .. import versions
+from .. import sizing, versions
 from . import scripts
 from .catalog import MODULES_DIR
 
@@ -444,7 +444,7 @@ def modules() -> List[Module]:
                            Var("triton_network_names", ["Joyent-SDC-Public"], type="list(string)"),
                            Var("triton_image_name", "ubuntu-certified-22.04"), Var("triton_image_version", None),
                            Var("triton_ssh_user", "ubuntu"),
-                           Var("master_triton_machine_package", "k4-highcpu-kvm-3.75G")],
+                           Var("master_triton_machine_package", sizing.default_size("triton", "manager")[1])],
                        f'''data "triton_network" "networks" {{
   count = length(var.triton_network_names)
   name  = var.triton_network_names[count.index]
@@ -484,7 +484,7 @@ locals {{
     mods.append(Module("aws-rancher", ["aws", "external"],
                        MANAGER_BASE + _rancher_image_vars() + AWS_CREDS + [
                            Var("aws_vpc_cidr", "10.0.0.0/16"), Var("aws_subnet_cidr", "10.0.2.0/24"),
-                           Var("aws_ami_id", None), Var("aws_instance_type", "t3.medium"), Var("aws_key_name", None),
+                           Var("aws_ami_id", None), Var("aws_instance_type", sizing.default_size("aws", "manager")[1]), Var("aws_key_name", None),
                            Var("aws_public_key_path", "~/.ssh/id_rsa.pub"), Var("aws_private_key_path", "~/.ssh/id_rsa"),
                            Var("aws_ssh_user", "ubuntu")],
                        f'''resource "aws_vpc" "default" {{
@@ -568,7 +568,7 @@ locals {{
     # T3 gcp-rancher
     mods.append(Module("gcp-rancher", ["gcp", "external"],
                        MANAGER_BASE + _rancher_image_vars() + GCP_CREDS + [
-                           Var("gcp_machine_type", "n1-standard-2"), Var("gcp_instance_zone", None),
+                           Var("gcp_machine_type", sizing.default_size("gcp", "manager")[1]), Var("gcp_instance_zone", None),
                            Var("gcp_image", "ubuntu-os-cloud/ubuntu-2204-lts"), Var("gcp_ssh_user", "ubuntu"),
                            Var("gcp_public_key_path", "~/.ssh/id_rsa.pub"), Var("gcp_private_key_path", "~/.ssh/id_rsa")],
                        f'''resource "google_compute_network" "default" {{
@@ -624,7 +624,7 @@ locals {{
                            Var("azure_virtual_network_address_space", "10.0.0.0/16"),
                            Var("azure_subnet_name", "rancher-subnet"), Var("azure_subnet_address_prefix", "10.0.2.0/24"),
                            Var("azurerm_network_security_group_name", "rancher-firewall"),
-                           Var("azure_resource_group_name", ""), Var("azure_size", "Standard_D4s_v5"),
+                           Var("azure_resource_group_name", ""), Var("azure_size", sizing.default_size("azure", "manager")[1]),
                            Var("azure_ssh_user", "ubuntu"), Var("azure_public_key_path", "~/.ssh/id_rsa.pub"),
                            Var("azure_private_key_path", "~/.ssh/id_rsa")],
                        f'''locals {{
@@ -921,7 +921,7 @@ data "vsphere_network" "network" {
     mods.append(Module("triton-rancher-k8s-host", ["triton"], HOST_BASE + TRITON_CREDS + [
         Var("triton_network_names", ["Joyent-SDC-Public"], type="list(string)"),
         Var("triton_image_name", "ubuntu-certified-22.04"), Var("triton_image_version", None),
-        Var("triton_ssh_user", "ubuntu"), Var("triton_machine_package", "k4-highcpu-kvm-3.75G")],
+        Var("triton_ssh_user", "ubuntu"), Var("triton_machine_package", sizing.default_size("triton", "host")[1])],
         ROLE_LOCAL + f'''
 
 data "triton_network" "networks" {{
@@ -953,7 +953,7 @@ resource "triton_machine" "host" {{
 
     # T13 aws-rancher-k8s-host
     mods.append(Module("aws-rancher-k8s-host", ["aws"], HOST_BASE + AWS_CREDS + [
-        Var("aws_ami_id", None), Var("aws_instance_type", "t3.large"), Var("aws_subnet_id", None),
+        Var("aws_ami_id", None), Var("aws_instance_type", sizing.default_size("aws", "host")[1]), Var("aws_subnet_id", None),
         Var("aws_security_group_id", None), Var("aws_key_name", None), Var("ebs_volume_device_name", ""),
         Var("ebs_volume_mount_path", ""), Var("ebs_volume_type", "gp3"), Var("ebs_volume_iops", ""),
         Var("ebs_volume_size", "")],
@@ -997,7 +997,7 @@ resource "aws_volume_attachment" "volume" {{
 
     # T14 gcp-rancher-k8s-host (the data disk is attached: Q15 fixed)
     mods.append(Module("gcp-rancher-k8s-host", ["gcp"], HOST_BASE + GCP_CREDS + [
-        Var("gcp_machine_type", "n1-standard-4"), Var("gcp_instance_zone", None),
+        Var("gcp_machine_type", sizing.default_size("gcp", "host")[1]), Var("gcp_instance_zone", None),
         Var("gcp_image", "ubuntu-os-cloud/ubuntu-2204-lts"), Var("gcp_compute_network_name", None),
         Var("gcp_compute_firewall_host_tag", None), Var("gcp_disk_type", ""), Var("gcp_disk_size", ""),
         Var("gcp_disk_mount_path", "")],
@@ -1040,7 +1040,7 @@ resource "google_compute_instance" "host" {{
     # T15 azure-rancher-k8s-host
     mods.append(Module("azure-rancher-k8s-host", ["azure"], HOST_BASE + AZURE_CREDS + AZURE_IMAGE + [
         Var("azure_resource_group_name", None), Var("azure_network_security_group_id", None),
-        Var("azure_subnet_id", None), Var("azure_size", "Standard_D4s_v5"), Var("azure_ssh_user", "ubuntu"),
+        Var("azure_subnet_id", None), Var("azure_size", sizing.default_size("azure", "host")[1]), Var("azure_ssh_user", "ubuntu"),
         Var("azure_public_key_path", "~/.ssh/id_rsa.pub"), Var("azure_disk_mount_path", ""),
         Var("azure_disk_size", "")],
         ROLE_LOCAL + f'''
@@ -1130,7 +1130,8 @@ resource "terraform_data" "install_rancher_agent" {{
     # T17 vsphere-rancher-k8s-host (CPU / memory are variables: Q15 fixed)
     mods.append(Module("vsphere-rancher-k8s-host", ["vsphere"], HOST_BASE + VSPHERE_CREDS + VSPHERE_NAMES + [
         Var("vsphere_template_name", None), Var("ssh_user", "ubuntu"), Var("key_path", "~/.ssh/id_rsa"),
-        Var("vsphere_num_cpus", "2"), Var("vsphere_memory_mb", "2048")],
+        Var("vsphere_num_cpus", sizing.VSPHERE_DEFAULT_CPUS),
+        Var("vsphere_memory_mb", sizing.default_size("vsphere", "host")[1])],
         ROLE_LOCAL + f'''
 
 data "vsphere_datacenter" "dc" {{

@@ -115,5 +115,5 @@ variable "triton_ssh_user" {
 variable "triton_machine_package" {
   description = "Triton machine package."
   type        = string
-  default     = "k4-highcpu-kvm-3.75G"
+  default     = "k4-highcpu-kvm-7.75G"
 }

@@ -118,5 +118,5 @@ variable "triton_ssh_user" {
 variable "master_triton_machine_package" {
   description = "Master triton machine package."
   type        = string
-  default     = "k4-highcpu-kvm-3.75G"
+  default     = "k4-highcpu-kvm-7.75G"
 }

@@ -128,5 +128,5 @@ variable "vsphere_num_cpus" {
 variable "vsphere_memory_mb" {
   description = "VSphere memory mb."
   type        = string
-  default     = "2048"
+  default     = "4096"
 }
