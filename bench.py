@@ -31,11 +31,13 @@ same create against agents kept resident across steps, round 1's headline) is
 reported only as the secondary ``warm_create_to_ready_s``, measured after the timed
 region.
 
-Simulated (``config.simulated_phases``): the Rancher server is the in-process v3
-fake, so RKE provisioning is instantaneous (``rke_provisioning``); the host runtime
-install (``runtime_install``: firewall, docker, hostname, registry login) and the
-``docker run rancher/agent`` container (``agent_container``) are sim-mode no-ops of the
-agents.  The reference publishes no number for this metric, so ``vs_baseline`` is null.
+The cluster is an RKE2 custom cluster (``provisioning.cattle.io/v1``, the default
+distribution of the pinned Rancher v2.10.3, versions.py).  Simulated
+(``config.simulated_phases``): the Rancher server is the in-process fake, so RKE2
+provisioning is instantaneous (``rke_provisioning``); the host steps (``runtime_install``:
+firewall, hostname) are sim-mode no-ops of the agents, and the node join
+(``agent_container``) fetches the server's ``system-agent-install.sh`` and registers as
+``rancher-system-agent`` through the fake's connect API instead of running the installer.  The reference publishes no number for this metric, so ``vs_baseline`` is null.
 
 Rank 0 prints one JSON line (the driver's contract).
 """
@@ -251,21 +253,21 @@ def main() -> int:
         wf.new_manager(Context(settings=Settings(mgr, env={}), out=devnull), backend)
 
     # node enrollment (install time, before the timed region): the manager's agent PKI
-    # issues each node a TLS certificate for its address, its own token and the agent-image
-    # allow-list.  Every simulated node gets its own loopback address.
+    # issues each node a TLS certificate for its address, its own token and the allow-list
+    # (the manager's agent image; its Rancher server, whose RKE2 installer the node runs).  Every simulated node gets its own loopback address.
     from triton_kubernetes_amd.node.security import AgentPKI, load_pki
 
-    pki_doc = [load_pki(backend, "bench").to_json() if rank == 0 else None]
+    pki_doc = [load_pki(backend, "bench").to_json() if rank == 0 else None, fake.url if rank == 0 else None]
     if distributed:
         dist.broadcast_object_list(pki_doc, src=0)
-    pki = AgentPKI.from_json(pki_doc[0])
+    pki, rancher_url = AgentPKI.from_json(pki_doc[0]), pki_doc[1]
     addresses = {name: f"127.1.{rank}.{2 + k}" for k, (name, _) in enumerate(mine)}
     if rank == 0:
         addresses["control-plane"] = "127.1.0.250"
     creds = {}
     for name, addr in addresses.items():
         creds[name] = os.path.join(work, "creds", name)
-        pki.issue(addr, [versions.AGENT_IMAGE]).write(creds[name])
+        pki.issue(addr, [versions.AGENT_IMAGE], servers=[rancher_url]).write(creds[name])
     client_ctx = pki.client_context()
 
     def start_agents(tag: str):
@@ -427,9 +429,10 @@ def main() -> int:
             "vs_baseline": None,
             "dtype": "bf16",
             "data": sim + ("synthetic cold create: fresh node-agent processes per step; simulated phases "
-                           "rke_provisioning (in-process Rancher v3 fake, instantaneous RKE), runtime_install "
-                           "(firewall/docker/hostname/registry-login no-ops) and agent_container (agent registers "
-                           "via the fake's connect API instead of docker run rancher/agent); real on MI355X: "
+                           "rke_provisioning (in-process Rancher v2.10 fake, RKE2 custom cluster, instantaneous "
+                           "provisioning), runtime_install (firewall/hostname no-ops) and agent_container (the node "
+                           "fetches system-agent-install.sh and registers as rancher-system-agent via the fake's "
+                           "connect API instead of running it); real on MI355X: "
                            f"native topology + RDMA labels, per-GPU HBM/MFMA/memtest burn-in level={args.burnin}, "
                            f"cluster RCCL all-reduce gate {'off' if args.no_rccl_gate else 'on'} "
                            f"(one communicator over all {n_gpus} GPUs)"
@@ -445,7 +448,8 @@ def main() -> int:
                           else "cold agents in the bench process (fresh NodeAgent objects per step)"),
                 "rccl_gate_max_mib": args.rccl_mib,
                 "simulated_phases": list(SIMULATED_PHASES),
-                "rancher": versions.RANCHER_VERSION, "k8s_version": versions.DEFAULT_K8S_VERSION,
+                "rancher": versions.RANCHER_VERSION, "k8s_distribution": versions.DEFAULT_DISTRIBUTION,
+                "k8s_version": versions.DEFAULT_K8S_VERSION,
                 # HIP runtime + RCCL the GPU agents ran on (ops/native.py:select_runtime)
                 "agent_hip_runtime": sorted(runtimes),
                 # node install step outside the timed region (ops/rccl_slim.py)

@@ -36,9 +36,9 @@ def pki():
     return AgentPKI.create("mgr")
 
 
-def _agent(pki, tmp_path, address, images=(AGENT_IMAGE,)):
+def _agent(pki, tmp_path, address, images=(AGENT_IMAGE,), servers=()):
     d = str(tmp_path / f"creds-{address}")
-    pki.issue(address, list(images)).write(d)
+    pki.issue(address, list(images), servers=list(servers)).write(d)
     creds = read_credentials(d)
     agent = NodeAgent(name=address, mode="sim", token=creds["token"], root=str(tmp_path / address),
                       policy=creds["policy"])
@@ -103,17 +103,49 @@ def test_unlisted_image_refused_before_any_step(pki, tmp_path):
     agent, url = _agent(pki, tmp_path, "127.1.9.4", images=["rancher/rancher-agent@sha256:" + "ab" * 32])
     try:
         tr = AgentTransport(pki=pki)
-        plan = build_host_plan(dict(WORKER, rancher_agent_image="evil/agent:latest"), "https://r", "tok", "sum")
+        plan = build_host_plan(dict(WORKER, k8s_distribution="rke1", rancher_agent_image="evil/agent:latest"),
+                               "https://r", "tok", "sum")
         with pytest.raises(HTTPError) as exc:
             tr.run_plan(HostRef("agent+" + url), plan)
         assert exc.value.status == 403 and "allow-list" in exc.value.body.decode()
         # the tag of the pinned repository is not the pinned digest either
-        plan2 = build_host_plan(dict(WORKER, rancher_agent_image="rancher/rancher-agent:v2.8.5"), "https://r", "t", "s")
+        plan2 = build_host_plan(dict(WORKER, k8s_distribution="rke1", rancher_agent_image="rancher/rancher-agent:v2.8.5"),
+                                "https://r", "t", "s")
         with pytest.raises(HTTPError):
             tr.run_plan(HostRef("agent+" + url), plan2)
         assert agent.history == []  # nothing ran
     finally:
         agent.stop()
+
+
+def test_rke2_join_only_through_an_allowed_server(pki, tmp_path):
+    """An RKE2 plan runs the installer of its Rancher server: a server outside the node's
+    allow-list (a plan pointing the node at someone else's installer) is refused with 403
+    before any step; the listed server passes (scheme/host/port compared)."""
+    from triton_kubernetes_amd.rancher.fake import FakeRancher
+
+    with FakeRancher.for_manager("mgr", "tk-admin-pw-0123") as rancher:
+        agent, url = _agent(pki, tmp_path, "127.1.9.7", servers=[rancher.url + "/"])
+        try:
+            tr = AgentTransport(pki=pki)
+            evil = build_host_plan(WORKER, "https://198.51.100.7", "tok", "sum")
+            with pytest.raises(HTTPError) as exc:
+                tr.run_plan(HostRef("agent+" + url), evil)
+            assert exc.value.status == 403 and "198.51.100.7" in exc.value.body.decode()
+            assert agent.history == []
+            # the listed server: the plan runs (here the token is unknown to Rancher, so the
+            # registration itself fails -- after the installer was fetched from the server)
+            res = tr.run_plan(HostRef("agent+" + url), build_host_plan(WORKER, rancher.url, "tok", "sum"))
+            assert [s["name"] for s in res["steps"]] == ["firewall", "hostname", "agent"]
+            assert not res["ok"] and "401" in res["error"]
+        finally:
+            agent.stop()
+    assert AgentPolicy(servers=["https://r.example"]).allows_server("https://R.example:443/x")
+    assert not AgentPolicy(servers=["https://r.example"]).allows_server("http://r.example")
+    assert not AgentPolicy().allows_server("http://127.0.0.1:9")
+    assert AgentPolicy(loopback_servers=True).allows_server("http://127.0.0.1:9")
+    with pytest.raises(TKError):
+        AgentPolicy.from_json({"images": [], "servers": ["ftp://x"]})
 
 
 def test_client_trusts_only_the_managers_ca(pki, tmp_path):
@@ -252,7 +284,16 @@ def test_cli_credentials_node(tmp_path, monkeypatch):
     rc = run(["--non-interactive", "--config", str(cfg), "credentials", "node"], out=out)
     assert rc == 0, out.getvalue()
     policy = json.loads((tmp_path / "creds" / "agent-policy.json").read_text())
-    assert policy == {"images": ["rancher/rancher-agent@sha256:" + "cd" * 32]}
+    # no manager state yet: no Rancher server to allow (RKE2 joins refused, and said so)
+    assert policy == {"images": ["rancher/rancher-agent@sha256:" + "cd" * 32], "servers": []}
+    assert "cannot join RKE2 clusters" in out.getvalue()
     pki = load_pki(be, "mgr", create=False)
     assert (tmp_path / "creds" / "agent-token").read_text().strip() == pki.node_token("10.2.3.4")
     assert (tmp_path / "creds" / "ca.crt").read_text() == pki.ca_cert
+    # once the manager is applied, its rancher_url is the allowed server
+    be.write_tfstate("mgr", json.dumps({"version": 4, "outputs": {
+        "cluster-manager__rancher_url": {"value": "https://10.9.8.7"}}}).encode())
+    rc = run(["--non-interactive", "--config", str(cfg), "credentials", "node"], out=io.StringIO())
+    assert rc == 0
+    policy = json.loads((tmp_path / "creds" / "agent-policy.json").read_text())
+    assert policy["servers"] == ["https://10.9.8.7"]

@@ -146,7 +146,7 @@ def test_check_inputs_evaluates_the_modules_validations():
             "k8s_version": "v1.28.10-rancher1-1", "k8s_network_provider": "calico"}
     assert hcl.check_inputs(mod, base) == []
     bad = hcl.check_inputs(mod, dict(base, k8s_version="v1.9.5-rancher1-1", k8s_network_provider="weird", extra=1))
-    assert any(e.startswith("k8s_version: k8s_version must be an RKE1 release") for e in bad), bad
+    assert any(e.startswith("k8s_version: k8s_version must be an RKE2 (") for e in bad), bad
     assert any(e.startswith("k8s_network_provider:") for e in bad) and "unsupported argument 'extra'" in bad
     assert "missing required argument 'name'" in hcl.check_inputs(mod, {k: v for k, v in base.items() if k != "name"})
     mgr = os.path.join(MODULES_DIR, "bare-metal-rancher")

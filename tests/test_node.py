@@ -23,14 +23,24 @@ def _bash_syntax_ok(script: str) -> None:
 
 
 def test_plan_steps_and_order():
+    # RKE2 (default): no container runtime or docker login (RKE2 brings containerd, registries
+    # come from the cluster's rkeConfig); RKE1: the reference's Docker + rancher-agent steps
     plain = build_host_plan(WORKER, "https://r", "tok", "sum")
-    assert plain.step_names() == ["firewall", "runtime", "hostname", "agent"]
+    assert plain.step_names() == ["firewall", "hostname", "agent"] and plain.distribution == "rke2"
     assert plain.gpu is None
-    gpu = build_host_plan(dict(GPU_WORKER, rancher_registry="reg.io", rancher_registry_username="u",
-                               rancher_registry_password="p"), "https://r", "tok", "sum", mi355x=True)
+    rke1 = build_host_plan(dict(WORKER, k8s_distribution="rke1"), "https://r", "tok", "sum")
+    assert rke1.step_names() == ["firewall", "runtime", "hostname", "agent"]
+    reg = dict(GPU_WORKER, rancher_registry="reg.io", rancher_registry_username="u", rancher_registry_password="p")
+    gpu = build_host_plan(dict(reg, k8s_distribution="rke1"), "https://r", "tok", "sum", mi355x=True)
     # burn-in precedes labels so the agent's topology prefetch overlaps it
     assert gpu.step_names() == ["firewall", "runtime", "hostname", "registry_login", "gpu_preflight",
                                 "gpu_burnin", "gpu_links", "gpu_labels", "rccl_env", "rccl_local", "agent"]
+    gpu2 = build_host_plan(reg, "https://r", "tok", "sum", mi355x=True)
+    assert gpu2.step_names() == ["firewall", "hostname", "gpu_preflight", "gpu_burnin", "gpu_links", "gpu_labels",
+                                 "rccl_env", "rccl_local", "agent"]
+    assert gpu2.steps[-1].params == {"server": "https://r", "role": "worker", "distribution": "rke2"}
+    with pytest.raises(ValueError):
+        build_host_plan(dict(WORKER, k8s_distribution="k3s"), "https://r", "tok", "sum")
     assert gpu.gpu == {"product": "MI355X", "count": 8, "burnin": "quick", "physical": 8, "compute_partition": "spx",
                        "memory_partition": "nps1"}
     # the single-target RCCL copy is opt-in (a modified vendor binary)
@@ -70,21 +80,29 @@ def _fake_bin(d, name, body):
     p.chmod(0o755)
 
 
-def test_local_transport_runs_plan_with_stub_tools(tmp_path):
-    """The rendered script runs end to end with stub sudo/docker; markers + the agent argv come back."""
+@pytest.mark.parametrize("dist", ["rke2", "rke1"])
+def test_local_transport_runs_plan_with_stub_tools(tmp_path, dist):
+    """The rendered script runs end to end with stub sudo/docker/curl; markers + the join argv come back."""
     bindir = tmp_path / "bin"
     bindir.mkdir()
     log = tmp_path / "sudo.log"
     _fake_bin(bindir, "sudo", f'echo "$*" >> {log}; cat >/dev/null 2>&1 || true')
     _fake_bin(bindir, "docker", "exit 0")
+    _fake_bin(bindir, "curl", f'echo "curl $*" >> {log}')
     env = {"PATH": f"{bindir}:/usr/bin:/bin"}
-    plan = build_host_plan(WORKER, "https://rancher.example", "regtok", "cafe", mi355x=False)
+    plan = build_host_plan(dict(WORKER, k8s_distribution=dist), "https://rancher.example", "regtok", "cafe",
+                           mi355x=False)
     res = LocalTransport(env=env).run_plan(HostRef("local"), plan)
     assert res["ok"], res
     assert [s["name"] for s in res["steps"]] == plan.step_names()
     calls = log.read_text()
     assert "hostnamectl set-hostname gpu-1" in calls
-    assert "--server https://rancher.example --token regtok --ca-checksum cafe --worker" in calls
+    if dist == "rke1":
+        assert "--server https://rancher.example --token regtok --ca-checksum cafe --worker" in calls
+    else:
+        assert "curl -fsSLk -o /tmp/tk-system-agent-install.sh https://rancher.example/system-agent-install.sh" in calls
+        assert ("sh /tmp/tk-system-agent-install.sh --server https://rancher.example --label cattle.io/os=linux "
+                "--token regtok --ca-checksum cafe --node-name gpu-1 --worker") in calls
 
 
 def test_local_transport_reports_failed_step(tmp_path):
@@ -183,7 +201,7 @@ def test_agent_burnin_failure_stops_plan(tmp_path):
     agent = NodeAgent("n1", "sim", devices=[0, 1], root=str(tmp_path), token="t",
                       topology_override=synthetic_topology(2),
                       burnin_override=lambda d, lvl: {"ok": d != 1, "failures": ["hbm"]})
-    res = agent.run_plan(build_host_plan(dict(GPU_WORKER, gpu_count=2), "http://x", "t", "s", mi355x=True))
+    res = agent.run_plan(build_host_plan(dict(GPU_WORKER, gpu_count=2), "http://127.0.0.1:9", "t", "s", mi355x=True))
     assert not res["ok"] and res["error"].startswith("gpu_burnin")
     assert "gpu_labels" not in [s["name"] for s in res["steps"]]
 
@@ -191,7 +209,7 @@ def test_agent_burnin_failure_stops_plan(tmp_path):
 def test_agent_preflight_counts_gpus(tmp_path):
     agent = NodeAgent("n1", "sim", devices=[0], root=str(tmp_path), token="t",
                       topology_override=synthetic_topology(1))
-    res = agent.run_plan(build_host_plan(GPU_WORKER, "http://x", "t", "s", mi355x=True))
+    res = agent.run_plan(build_host_plan(GPU_WORKER, "http://127.0.0.1:9", "t", "s", mi355x=True))
     assert not res["ok"] and "expected 8 GPUs, found 1" in res["error"]
 
 
@@ -218,7 +236,7 @@ def test_agent_rejects_bad_mode():
 
 def test_exec_mode_validates_hostname(tmp_path):
     agent = NodeAgent("n1", "exec", root=str(tmp_path), token="t")
-    plan = build_host_plan(dict(WORKER, hostname="bad host;reboot"), "http://x", "t", "s")
+    plan = build_host_plan(dict(WORKER, hostname="bad host;reboot"), "http://127.0.0.1:9", "t", "s")
     plan.steps = [s for s in plan.steps if s.action == "hostname"]
     res = agent.run_plan(plan)
     assert not res["ok"] and "invalid hostname" in res["error"]
@@ -238,7 +256,7 @@ def test_agent_janitor_frees_burnin_arena_when_idle(tmp_path, monkeypatch):
     agent = NodeAgent("n1", "sim", devices=[0], root=str(tmp_path), token="t",
                       topology_override=synthetic_topology(1), burnin_override=lambda d, lvl: {"ok": True})
     agent._start_janitor(0.1)
-    plan = build_host_plan(dict(GPU_WORKER, gpu_count=1), "http://x", "t", "s", mi355x=True)
+    plan = build_host_plan(dict(GPU_WORKER, gpu_count=1), "http://127.0.0.1:9", "t", "s", mi355x=True)
     plan.steps = [s for s in plan.steps if s.action != "agent"]
     assert agent.run_plan(plan)["ok"]
     assert events == []  # still within the idle window

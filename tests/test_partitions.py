@@ -167,11 +167,11 @@ def test_agent_preflight_checks_the_modes(cpx, native_ok, tmp_path):
     try:
         base = {"hostname": "g", "rancher_host_labels": {"worker": "true"}, "gpu_count": 8, "gpu_burnin": "quick"}
         good = agent.run_plan(build_host_plan(dict(base, gpu_compute_partition="cpx", gpu_memory_partition="nps2"),
-                                              "https://r", "t", "s", mi355x=True))
+                                              "http://127.0.0.1:9", "t", "s", mi355x=True))
         pre = next(s for s in good["steps"] if s["name"] == "gpu_preflight")
         assert pre["ok"] and pre["detail"]["partition"] == {"compute": "cpx", "memory": "nps2"}
         assert pre["detail"]["gpus"] == 64
-        bad = agent.run_plan(build_host_plan(base, "https://r", "t", "s", mi355x=True))
+        bad = agent.run_plan(build_host_plan(base, "http://127.0.0.1:9", "t", "s", mi355x=True))
         assert not bad["ok"] and "compute partition is CPX, the cluster expects SPX" in bad["error"]
     finally:
         agent.stop()

@@ -133,7 +133,8 @@ def test_waiter_runs_process_gate_for_ssh_nodes(tools):
                             ("g2", {"worker": True})):
             HTTPClient(base_url=fake.url).request("POST", "/v3/connect/register", data=b"{}", headers={
                 "X-API-Tunnel-Token": info.registration_token,
-                "X-API-Tunnel-Params": tunnel_params(host, roles, {}, {})})
+                "X-API-Tunnel-Params": tunnel_params(host, roles, {}, {}),
+                "X-Cattle-Agent-Kind": "system-agent"})  # an RKE2 cluster (the default)
         spec = ReadinessSpec(info.cluster_id, ["cp", "g1", "g2"], timeout=30, rccl_gate=True,
                              rccl_process_hosts=[HostRef("local"), HostRef("local")], rccl_process_ndev=[8, 8])
         rep = wait_ready(client, spec, host_transport=LocalTransport(), tools_dir=tools[0])

@@ -42,15 +42,46 @@ def test_bootstrap_s3(rancher):
 
 
 def test_ensure_cluster_is_idempotent_s4(rancher):
+    """RKE1 (the reference's v3 cluster): found by name, token reused."""
     fake, client, _ = rancher
-    a = client.ensure_cluster("dev", "v1.28.10-rancher1-1", "calico")
-    b = client.ensure_cluster("dev")
+    a = client.ensure_cluster("dev", "v1.28.15-rancher1-1", "calico")
+    b = client.ensure_cluster("dev", distribution="rke1")
     assert a.cluster_id == b.cluster_id and not a.existed and b.existed
     assert a.registration_token == b.registration_token  # reused, not re-created
     assert a.ca_checksum == ca_checksum(FAKE_CACERTS)
     rke = fake.state.clusters[a.cluster_id]["rancherKubernetesEngineConfig"]
-    assert rke["kubernetesVersion"] == "v1.28.10-rancher1-1" and rke["network"]["plugin"] == "calico"
-    assert client.ensure_cluster("other").cluster_id != a.cluster_id
+    assert rke["kubernetesVersion"] == "v1.28.15-rancher1-1" and rke["network"]["plugin"] == "calico"
+    assert client.ensure_cluster("other", distribution="rke1").cluster_id != a.cluster_id
+
+
+def test_ensure_rke2_cluster_is_idempotent(rancher):
+    """RKE2 (default): a provisioning.cattle.io/v1 Cluster in fleet-default; its management
+    cluster (c-m-...) holds the registration token."""
+    fake, client, _ = rancher
+    a = client.ensure_cluster("dev2", "v1.30.10+rke2r1", "cilium")
+    b = client.ensure_cluster("dev2")
+    assert a.cluster_id.startswith("c-m-") and a.cluster_id == b.cluster_id and not a.existed and b.existed
+    assert a.registration_token == b.registration_token
+    obj = fake.state.v2_clusters["fleet-default/dev2"]
+    assert obj["spec"]["kubernetesVersion"] == "v1.30.10+rke2r1"
+    assert obj["spec"]["rkeConfig"]["machineGlobalConfig"]["cni"] == "cilium"
+    assert obj["status"]["clusterName"] == a.cluster_id
+    # a name taken by the other distribution is refused both ways (nodes could not join it)
+    with pytest.raises(TKError, match="already exists as an RKE2 cluster"):
+        client.ensure_cluster("dev2", distribution="rke1")
+    client.ensure_cluster("dev1", distribution="rke1")
+    with pytest.raises(TKError, match="already exists as an RKE1 cluster"):
+        client.ensure_cluster("dev1", distribution="rke2")
+    # KDM: a release the server does not offer is replaced by its release of that minor,
+    # a minor it does not offer is refused before anything is created
+    c = client.ensure_cluster("dev3", "v1.31.2+rke2r1")
+    assert fake.state.v2_clusters["fleet-default/dev3"]["spec"]["kubernetesVersion"] == "v1.31.6+rke2r1"
+    assert "not offered" in client.last_version_note
+    with pytest.raises(TKError, match="not offered"):
+        client.ensure_cluster("old", "v1.27.16+rke2r2")
+    assert "fleet-default/old" not in fake.state.v2_clusters and c.cluster_id
+    client.delete_cluster(a.cluster_id)
+    assert "fleet-default/dev2" not in fake.state.v2_clusters and a.cluster_id not in fake.state.clusters
 
 
 def test_registration_token_filled_in_after_create(rancher):
@@ -64,34 +95,64 @@ def test_registration_token_filled_in_after_create(rancher):
     info = client.ensure_cluster("async")
     assert info.registration_token and info.registration_token in fake.state.reg_tokens
     script = os.path.join(MODULES_DIR, "bare-metal-rancher-k8s", "files", "ensure_cluster.sh")
-    query = {"name": "scripted", "version": "v1.28", "network": "flannel", "api_url": fake.url,
-             "access_key": outs["rancher_access_key"], "secret_key": outs["rancher_secret_key"]}
-    first = json.loads(subprocess.run(["bash", script], input=json.dumps(query), capture_output=True, text=True,
-                                      check=True, timeout=60).stdout)
-    assert first["registration_token"] in fake.state.reg_tokens
-    assert first["ca_checksum"] == ca_checksum(FAKE_CACERTS)
-    # the minor was resolved against the server's KDM list
-    rke = fake.state.clusters[first["cluster_id"]]["rancherKubernetesEngineConfig"]
-    assert rke["kubernetesVersion"].startswith("v1.28.")
-    again = json.loads(subprocess.run(["bash", script], input=json.dumps(query), capture_output=True, text=True,
-                                      check=True, timeout=60).stdout)
-    assert again == first  # found by name, token reused
+    for dist, version in (("rke1", "v1.28"), ("rke2", "v1.30")):
+        query = {"name": f"scripted-{dist}", "version": version, "network": "flannel", "distribution": dist,
+                 "api_url": fake.url, "access_key": outs["rancher_access_key"], "secret_key": outs["rancher_secret_key"]}
+        first = json.loads(subprocess.run(["bash", script], input=json.dumps(query), capture_output=True, text=True,
+                                          check=True, timeout=60).stdout)
+        assert first["registration_token"] in fake.state.reg_tokens
+        assert first["ca_checksum"] == ca_checksum(FAKE_CACERTS)
+        # the minor was resolved against the server's KDM list
+        if dist == "rke1":
+            rke = fake.state.clusters[first["cluster_id"]]["rancherKubernetesEngineConfig"]
+            assert rke["kubernetesVersion"].startswith("v1.28.")
+        else:
+            obj = fake.state.v2_clusters["fleet-default/scripted-rke2"]
+            assert obj["spec"]["kubernetesVersion"] == "v1.30.10+rke2r1"
+            assert first["cluster_id"] == obj["status"]["clusterName"]
+        again = json.loads(subprocess.run(["bash", script], input=json.dumps(query), capture_output=True, text=True,
+                                          check=True, timeout=60).stdout)
+        assert again == first  # found by name, token reused
 
 
 def test_registry_passed_to_rke(rancher):
     fake, client, _ = rancher
     info = client.ensure_cluster("reg", k8s_registry="r.example", k8s_registry_username="u",
-                                 k8s_registry_password="p")
+                                 k8s_registry_password="p", distribution="rke1")
     rke = fake.state.clusters[info.cluster_id]["rancherKubernetesEngineConfig"]
     assert rke["privateRegistries"] == [{"url": "r.example", "user": "u", "password": "p"}]
+    # RKE2: a docker.io mirror + credentials in the cluster's rkeConfig (nodes run no docker login)
+    client.ensure_cluster("reg2", k8s_registry="r.example", k8s_registry_username="u", k8s_registry_password="p")
+    regs = fake.state.v2_clusters["fleet-default/reg2"]["spec"]["rkeConfig"]["registries"]
+    assert regs["mirrors"]["docker.io"]["endpoint"] == ["https://r.example"]
+    # credentials live in a basic-auth Secret of fleet-default the config names
+    assert fake.registry_auth(regs["configs"]["r.example"]["authConfigSecretName"]) == {"username": "u",
+                                                                                         "password": "p"}
 
 
-def _register(fake, token, host, roles, labels=None, capacity=None):
+def _register(fake, token, host, roles, labels=None, capacity=None, kind="system-agent"):
     from triton_kubernetes_amd.cloud.http import HTTPClient
 
     hdrs = {"X-API-Tunnel-Token": token,
-            "X-API-Tunnel-Params": tunnel_params(host, roles, labels or {}, capacity or {})}
+            "X-API-Tunnel-Params": tunnel_params(host, roles, labels or {}, capacity or {}),
+            "X-Cattle-Agent-Kind": kind}
     return HTTPClient(base_url=fake.url).request("POST", "/v3/connect/register", headers=hdrs, data=b"{}").json()
+
+
+def test_agent_kind_must_match_the_distribution(rancher):
+    """An RKE2 cluster takes rancher-system-agent nodes only, an RKE1 cluster rancher-agent ones."""
+    from triton_kubernetes_amd.cloud.http import HTTPError
+
+    fake, client, _ = rancher
+    rke2 = client.ensure_cluster("k2")
+    rke1 = client.ensure_cluster("k1", distribution="rke1")
+    with pytest.raises(HTTPError) as exc:
+        _register(fake, rke2.registration_token, "a", {"worker": True}, kind="rancher-agent")
+    assert exc.value.status == 400 and b"rancher-system-agent" in exc.value.body
+    with pytest.raises(HTTPError):
+        _register(fake, rke1.registration_token, "b", {"worker": True})
+    _register(fake, rke2.registration_token, "a", {"worker": True})
+    _register(fake, rke1.registration_token, "b", {"worker": True}, kind="rancher-agent")
 
 
 def test_cluster_lifecycle_and_gpu_allocatable(rancher):
@@ -188,7 +249,8 @@ def test_addon_manifest_options():
     assert cm["data"]["HSA_ENABLE_IPC_MODE_LEGACY"] == "0"
 
 
-def test_terraform_cluster_script_against_fake(rancher, tmp_path):
+@pytest.mark.parametrize("dist,version", [("rke1", "v1.28.15-rancher1-1"), ("rke2", "v1.29.14+rke2r1")])
+def test_terraform_cluster_script_against_fake(rancher, tmp_path, dist, version):
     """The cluster modules' data "external" program (S4) speaks to Rancher like RancherClient does."""
     import subprocess
 
@@ -197,9 +259,9 @@ def test_terraform_cluster_script_against_fake(rancher, tmp_path):
     fake, client, outs = rancher
     script = tmp_path / "ensure_cluster.sh"
     script.write_text(scripts.RANCHER_CLUSTER)
-    query = {"name": "tf", "version": "v1.28.10-rancher1-1", "network": "calico", "api_url": fake.url,
+    query = {"name": "tf", "version": version, "network": "calico", "api_url": fake.url, "distribution": dist,
              "access_key": outs["rancher_access_key"], "secret_key": outs["rancher_secret_key"],
-             "registry": "", "registry_username": "", "registry_password": ""}
+             "registry": "r.example", "registry_username": "u", "registry_password": "p"}
 
     def run():
         proc = subprocess.run(["bash", str(script)], input=json.dumps(query), capture_output=True, text=True,
@@ -209,7 +271,15 @@ def test_terraform_cluster_script_against_fake(rancher, tmp_path):
 
     first, second = run(), run()
     assert first == second  # found by name, registration token reused
-    info = client.ensure_cluster("tf")
+    info = client.ensure_cluster("tf", distribution=dist)
     assert first == {"cluster_id": info.cluster_id, "registration_token": info.registration_token,
                      "ca_checksum": ca_checksum(FAKE_CACERTS)}
-    assert fake.state.clusters[info.cluster_id]["rancherKubernetesEngineConfig"]["network"]["plugin"] == "calico"
+    if dist == "rke1":
+        rke = fake.state.clusters[info.cluster_id]["rancherKubernetesEngineConfig"]
+        assert rke["network"]["plugin"] == "calico"
+        assert rke["privateRegistries"] == [{"url": "r.example", "user": "u", "password": "p"}]
+    else:
+        rke = fake.state.v2_clusters["fleet-default/tf"]["spec"]["rkeConfig"]
+        assert rke["machineGlobalConfig"]["cni"] == "calico"
+        secret = rke["registries"]["configs"]["r.example"]["authConfigSecretName"]
+        assert fake.registry_auth(secret) == {"username": "u", "password": "p"}

@@ -195,7 +195,7 @@ def test_agent_rccl_env_merges_discovered_nics(tmp_path):
                       topology_override=topology, burnin_override=lambda d, lvl: {"ok": True})
     cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
            "rccl_env": {"NCCL_IB_GID_INDEX": "5", "NCCL_DEBUG": "INFO"}}
-    plan = build_host_plan(cfg, "http://x", "t", "s", mi355x=True)
+    plan = build_host_plan(cfg, "http://127.0.0.1:9", "t", "s", mi355x=True)
     plan.steps = [s for s in plan.steps if s.action != "agent"]
     res = agent.run_plan(plan)
     assert res["ok"], res

@@ -1,5 +1,6 @@
 """Pinned versions are coherent across every delivery path, and the fake Rancher enforces
-what a real Rancher v2.8.5 enforces (bootstrap password, KDM Kubernetes list, password length).
+what a real Rancher v2.10.3 enforces (bootstrap password, KDM Kubernetes lists of RKE1 and RKE2,
+password length).
 
 Reference: ``/root/reference/create/cluster.go:349-356`` (k8s choices of its pinned
 server) and ``/root/reference/terraform/modules/triton-rancher/variables.tf:14-22``.
@@ -24,7 +25,7 @@ from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
 
 from helpers import make_ctx
 
-OLD = "v1.9.5-rancher1-1"  # the reference's default: no RKE1 release of Rancher 2.8
+OLD = "v1.9.5-rancher1-1"  # the reference's default: no RKE1 release of Rancher 2.10
 
 
 def _var_default(module: str, var: str) -> str:
@@ -35,10 +36,16 @@ def _var_default(module: str, var: str) -> str:
 
 
 def test_defaults_agree_everywhere():
-    assert versions.DEFAULT_K8S_VERSION in [v for _, v in versions.K8S_VERSIONS]
+    assert versions.DEFAULT_DISTRIBUTION == "rke2"
+    assert versions.DEFAULT_K8S_VERSION in [v for _, v in versions.RKE2_VERSIONS]
+    assert versions.DEFAULT_RKE1_VERSION in [v for _, v in versions.K8S_VERSIONS]
     for mod in ("bare-metal-rancher-k8s", "triton-rancher-k8s", "aws-rancher-k8s", "gcp-rancher-k8s",
                 "azure-rancher-k8s", "vsphere-rancher-k8s"):
         assert _var_default(mod, "k8s_version") == versions.DEFAULT_K8S_VERSION
+        assert _var_default(mod, "k8s_distribution") == versions.DEFAULT_DISTRIBUTION
+        assert _var_default(mod, "k8s_network_provider") in versions.RKE2_CNIS
+    for mod in ("bare-metal-rancher-k8s-host", "bare-metal-mi355x-rancher-k8s-host", "triton-rancher-k8s-host"):
+        assert _var_default(mod, "k8s_distribution") == versions.DEFAULT_DISTRIBUTION
     for mod in ("bare-metal-rancher", "triton-rancher", "aws-rancher", "gcp-rancher", "azure-rancher"):
         assert _var_default(mod, "rancher_server_image") == versions.SERVER_IMAGE
         assert _var_default(mod, "docker_engine_install_url") == versions.DOCKER_INSTALL_URL
@@ -59,15 +66,28 @@ def test_cli_rejects_kubernetes_releases_outside_the_pinned_rancher():
     st = State("mgr")
     st.set_manager({"source": "x", "name": "mgr"})
     ctx = make_ctx({"name": "dev", "k8s_version": OLD, "k8s_network_provider": "flannel"})
-    with pytest.raises(ConfigError, match="not offered by Rancher v2.8.5"):
+    with pytest.raises(ConfigError, match="not an RKE1 release offered by Rancher v2.10.3"):
         baremetal.new_cluster(ctx, None, st)
-    # the display name maps to the pinned release; a patch release of a pinned minor passes through
-    for given, want in (("v1.27", "v1.27.14-rancher1-1"), ("v1.28.12-rancher1-1", "v1.28.12-rancher1-1")):
+    # the display name maps to the pinned release of the distribution (RKE2 unless the
+    # release string or k8s_distribution says RKE1); a patch release of a pinned minor passes
+    for extra, given, want, dist in (({}, "v1.29", "v1.29.14+rke2r1", "rke2"),
+                                     ({"k8s_distribution": "rke1"}, "v1.28", "v1.28.15-rancher1-1", "rke1"),
+                                     ({}, "v1.28.12-rancher1-1", "v1.28.12-rancher1-1", "rke1"),
+                                     ({}, "v1.30.4+rke2r1", "v1.30.4+rke2r1", "rke2")):
         st = State("mgr")
         st.set_manager({"source": "x", "name": "mgr"})
-        baremetal.new_cluster(make_ctx({"name": "dev", "k8s_version": given, "k8s_network_provider": "flannel"}),
+        baremetal.new_cluster(make_ctx(dict(extra, name="dev", k8s_version=given, k8s_network_provider="flannel")),
                               None, st)
         assert st.get("module.cluster_baremetal_dev.k8s_version") == want
+        assert st.get("module.cluster_baremetal_dev.k8s_distribution") == dist
+    # an RKE1-only minor is not an RKE2 release; a release of the other distribution is refused
+    for bad, match in (({"k8s_version": "v1.28"}, "not an RKE2 release"),
+                       ({"k8s_version": "v1.29.14+rke2r1", "k8s_distribution": "rke1"}, "is an RKE2 release"),
+                       ({"k8s_version": "v1.29", "k8s_network_provider": "weave"}, "not a RKE2 network provider")):
+        st = State("mgr")
+        st.set_manager({"source": "x", "name": "mgr"})
+        with pytest.raises(ConfigError, match=match):
+            baremetal.new_cluster(make_ctx(dict({"name": "dev", "k8s_network_provider": "flannel"}, **bad)), None, st)
 
 
 def test_short_admin_password_rejected():
@@ -105,12 +125,21 @@ def test_same_minor_release_substituted_from_the_server_list():
             as fake:
         outs = RancherClient(fake.url).bootstrap("long-enough-pw", fake.url, "b00t-b00t-b00t", timeout=5)
         client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
-        info = client.ensure_cluster("dev", versions.DEFAULT_K8S_VERSION)
+        info = client.ensure_cluster("dev", "v1.28.10-rancher1-1")
         rke = fake.state.clusters[info.cluster_id]["rancherKubernetesEngineConfig"]
         assert rke["kubernetesVersion"] == "v1.28.15-rancher1-1"
         assert "using v1.28.15-rancher1-1" in client.last_version_note
         with pytest.raises(TKError):
             client.ensure_cluster("gone", "v1.26.15-rancher1-1")
+    with FakeRancher(bootstrap_password="b00t-b00t-b00t", rke2_versions=["v1.30.12+rke2r1"]) as fake:
+        outs = RancherClient(fake.url).bootstrap("long-enough-pw", fake.url, "b00t-b00t-b00t", timeout=5)
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        client.ensure_cluster("dev", "v1.30.10+rke2r1")
+        assert fake.state.v2_clusters["fleet-default/dev"]["spec"]["kubernetesVersion"] == "v1.30.12+rke2r1"
+        with pytest.raises(TKError, match="not offered"):
+            client.ensure_cluster("gone", versions.DEFAULT_K8S_VERSION)  # v1.31: not in this server's KDM
+        with pytest.raises(TKError, match="HTTP 422"):  # and the server itself refuses it
+            client.create_v2_cluster("gone", versions.DEFAULT_K8S_VERSION, "canal")
 
 
 def test_bootstrap_password_same_in_python_and_terraform():

@@ -46,7 +46,7 @@ from ..rancher.client import RancherClient, wait_until
 from ..state import State
 from ..terraform.catalog import ModuleInfo, module_from_source
 from ..utils.trace import span
-from ..versions import DEFAULT_K8S_VERSION, bootstrap_password
+from ..versions import DEFAULT_DISTRIBUTION, bootstrap_password, default_version
 from .base import Executor, outputs_from_tfstate
 from .tfstate import CODEC
 
@@ -377,9 +377,11 @@ class DirectExecutor(Executor):
     def _apply_cluster(self, cfg: Dict[str, Any]) -> Dict[str, str]:
         client = self.rancher_factory(cfg["rancher_api_url"], cfg.get("rancher_access_key", ""),
                                       cfg.get("rancher_secret_key", ""))
-        info = client.ensure_cluster(cfg["name"], cfg.get("k8s_version") or DEFAULT_K8S_VERSION,
-                                     cfg.get("k8s_network_provider") or "flannel", cfg.get("k8s_registry", ""),
-                                     cfg.get("k8s_registry_username", ""), cfg.get("k8s_registry_password", ""))
+        dist = cfg.get("k8s_distribution") or ""
+        info = client.ensure_cluster(cfg["name"], cfg.get("k8s_version") or default_version(dist or DEFAULT_DISTRIBUTION),
+                                     cfg.get("k8s_network_provider") or ("canal" if dist != "rke1" else "flannel"), cfg.get("k8s_registry", ""),
+                                     cfg.get("k8s_registry_username", ""), cfg.get("k8s_registry_password", ""),
+                                     distribution=dist)
         return info.outputs()
 
     # --- host ------------------------------------------------------------------------------------------------

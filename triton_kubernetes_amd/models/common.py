@@ -20,7 +20,8 @@ from ..config.context import Context, not_blank
 from ..errors import ConfigError
 from ..state import MANAGER_KEY, State
 from ..terraform.catalog import module_source, packaged_root
-from ..versions import K8S_VERSIONS, PASSWORD_MIN_LENGTH, normalize_k8s_version
+from ..versions import (DISTRIBUTIONS, PASSWORD_MIN_LENGTH, RKE2_CNIS, distribution_of, normalize_k8s_version,
+                        releases, resolve_distribution)
 
 # The reference defaults to its own GitHub repo (create/cluster.go:20-21), which is
 # where its modules live.  This CLI's modules ship inside the package, so the default
@@ -34,8 +35,12 @@ DNS1123_MESSAGE = ("A DNS-1123 subdomain must consist of lower case alphanumeric
                    "and must start and end with an alphanumeric character")
 
 # interactive choices: display name -> value (create/cluster.go:349-356 offers the
-# releases of its pinned Rancher; these are the pinned Rancher v2.8.5's, versions.py)
-K8S_NETWORK_PROVIDERS = ["calico", "flannel"]
+# releases of its pinned Rancher; these are the pinned Rancher v2.10.3's, versions.py).
+# The reference offered calico / flannel (RKE1); RKE2 ships canal (its default), calico,
+# cilium and flannel.
+NETWORK_PROVIDERS = {"rke2": list(RKE2_CNIS), "rke1": ["calico", "flannel", "canal", "weave"]}
+DISTRIBUTION_CHOICES = ["RKE2 (rancher-system-agent, containerd)",
+                        "RKE1 (end-of-life; Docker + rancher-agent, reference-era clusters)"]
 HOST_LABELS = ["worker", "etcd", "control"]
 _ATOI_RE = re.compile(r"^[+-]?[0-9]+$")
 
@@ -147,6 +152,7 @@ def base_cluster_config(ctx: Context, module_path: str) -> Dict:
         "rancher_api_url": f"${{module.{MANAGER_KEY}.rancher_url}}",
         "rancher_access_key": f"${{module.{MANAGER_KEY}.rancher_access_key}}",
         "rancher_secret_key": f"${{module.{MANAGER_KEY}.rancher_secret_key}}",
+        "k8s_distribution": "",
         "k8s_version": "",
         "k8s_network_provider": "",
         "rancher_registry": "",
@@ -161,14 +167,20 @@ def base_cluster_config(ctx: Context, module_path: str) -> Dict:
     if not name or not DNS1123_RE.match(name):
         raise ConfigError("Invalid Cluster Name")
     cfg["name"] = name
+    dist = cluster_distribution(ctx)
+    cfg["k8s_distribution"] = dist
+    pinned = releases(dist)
     cfg["k8s_version"] = ctx.resolve_choice("k8s_version", "Kubernetes Version",
-                                            [d for d, _ in K8S_VERSIONS], values=[v for _, v in K8S_VERSIONS])
+                                            [d for d, _ in pinned], values=[v for _, v in pinned])
     try:
-        cfg["k8s_version"] = normalize_k8s_version(cfg["k8s_version"])
+        cfg["k8s_version"] = normalize_k8s_version(cfg["k8s_version"], dist)
     except ValueError as exc:
         raise ConfigError(str(exc)) from None
-    cfg["k8s_network_provider"] = ctx.resolve_choice("k8s_network_provider", "Kubernetes Network Provider",
-                                                     K8S_NETWORK_PROVIDERS)
+    cnis = NETWORK_PROVIDERS[dist]
+    cfg["k8s_network_provider"] = ctx.resolve_choice("k8s_network_provider", "Kubernetes Network Provider", cnis)
+    if cfg["k8s_network_provider"] not in cnis:
+        raise ConfigError(f"k8s_network_provider '{cfg['k8s_network_provider']}' is not a {dist.upper()} network "
+                          f"provider; choose one of: {', '.join(cnis)}")
     cfg["rancher_registry"] = ctx.resolve("private_registry", "Private Registry", required=False,
                                           none_sentinel="None")
     _registry_creds(ctx, cfg, "rancher_registry", "private_registry_username", "private_registry_password",
@@ -181,6 +193,30 @@ def base_cluster_config(ctx: Context, module_path: str) -> Dict:
     return omit_empty(cfg, ["k8s_version", "k8s_network_provider", "rancher_registry",
                             "rancher_registry_username", "rancher_registry_password", "k8s_registry",
                             "k8s_registry_username", "k8s_registry_password"])
+
+
+def cluster_distribution(ctx: Context) -> str:
+    """``k8s_distribution`` of a new cluster: the setting, else the one its
+    ``k8s_version`` names (``...+rke2rN`` / ``...-rancherN-N``), else a prompt
+    (interactive) or RKE2 (silent)."""
+    explicit = ctx.get_string("k8s_distribution") if ctx.is_set("k8s_distribution") else ""
+    version = ctx.get_string("k8s_version") if ctx.is_set("k8s_version") else ""
+    if not explicit and not distribution_of(version) and not ctx.non_interactive:
+        explicit = ctx.resolve_choice("k8s_distribution", "Kubernetes Distribution", DISTRIBUTION_CHOICES,
+                                      values=list(DISTRIBUTIONS))
+    try:
+        return resolve_distribution(version, explicit)
+    except ValueError as exc:
+        raise ConfigError(str(exc)) from None
+
+
+def node_distribution(state: State, cluster: str) -> str:
+    """The distribution a cluster's nodes join with, read from its module block: its
+    ``k8s_distribution``, else the one its ``k8s_version`` names, else the module
+    default (``migrate manager`` writes ``rke1`` into reference-era blocks)."""
+    block = state.module(cluster) or {}
+    explicit = str(block.get("k8s_distribution") or "")
+    return explicit or distribution_of(str(block.get("k8s_version") or "")) or resolve_distribution()
 
 
 # --- base node -------------------------------------------------------------------------
@@ -207,6 +243,7 @@ def base_node_config(ctx: Context, module_path: str, cluster: str, state: State)
         "rancher_registry": state.get(f"module.{cluster}.rancher_registry"),
         "rancher_registry_username": state.get(f"module.{cluster}.rancher_registry_username"),
         "rancher_registry_password": state.get(f"module.{cluster}.rancher_registry_password"),
+        "k8s_distribution": node_distribution(state, cluster),
     }
     cfg["source"] = source_for(ctx, module_path)
 

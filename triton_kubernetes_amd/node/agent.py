@@ -8,21 +8,25 @@ steps natively.
 Security model (``node/security.py``): the agent never executes shell text it
 receives.  A plan's ``shell`` fields are only for the SSH renderer; the agent
 dispatches on the step ``action`` and runs fixed, agent-side argv lists built from
-*validated* parameters (hostname, image reference, registry).  Off loopback it
+*validated* parameters (hostname, image reference, registry, Rancher URL).  Off loopback it
 serves only TLS, with a certificate for the node's address signed by its cluster
 manager's CA; plain HTTP needs ``--insecure-local`` and binds loopback only.  Every
 request must carry the node's own token (``X-TK-Agent-Token``, derived per node
 from the manager secret; a random one when none is given).  A plan whose agent
-step names an image outside the node's allow-list (:class:`AgentPolicy`, set by
-the manager at enrollment) is refused before any step runs (HTTP 403).
+step names an image (RKE1) or a Rancher server (RKE2) outside the node's allow-list
+(:class:`AgentPolicy`, set by the manager at enrollment) is refused before any step
+runs (HTTP 403).
 
 Modes:
 
-* ``exec`` — runtime steps run the fixed commands (the container runtime must
-  already be installed; installing it is the SSH path's job);
+* ``exec`` — runtime steps run the fixed commands (RKE1: the container runtime must
+  already be installed; installing it is the SSH path's job); the ``agent`` step runs
+  ``docker run rancher/rancher-agent`` (RKE1) or the allowed server's
+  ``system-agent-install.sh`` (RKE2);
 * ``sim`` — runtime steps are recorded as no-ops (simulated hosts have no
   container runtime) and the ``agent`` step registers with Rancher through
-  ``POST /v3/connect/register`` instead of ``docker run rancher/agent``.
+  ``POST /v3/connect/register`` (``X-Cattle-Agent-Kind: system-agent`` for RKE2,
+  after fetching the installer as a real node does) instead.
 
 In both modes the MI355X steps call the native probes directly on the agent's
 GPUs: topology labeller (N1), HBM/MFMA/memtest burn-in, RCCL env file and the
@@ -46,6 +50,7 @@ import re
 import secrets
 import shutil
 import subprocess
+import tempfile
 import threading
 import time
 import urllib.parse
@@ -116,7 +121,8 @@ class NodeAgent:
     token: str = ""
     topology_override: Optional[Dict[str, Any]] = None
     burnin_override: Optional[Callable[[int, str], Dict[str, Any]]] = None
-    # the Rancher agent images this node may run (default: the pinned agent image)
+    # the Rancher agent images / servers this node may run (default: the pinned agent
+    # image; Rancher servers on loopback only)
     policy: Optional[AgentPolicy] = None
 
     def __post_init__(self):
@@ -127,7 +133,7 @@ class NodeAgent:
         if self.policy is None:
             from ..versions import AGENT_IMAGE
 
-            self.policy = AgentPolicy([AGENT_IMAGE])
+            self.policy = AgentPolicy([AGENT_IMAGE], loopback_servers=True)
         self.lock = threading.Lock()
         self._gate_mu = threading.Lock()
         # long-lived workers for topology prefetch and per-GPU burn-in: no thread is created
@@ -159,15 +165,25 @@ class NodeAgent:
         return full
 
     # --- plan execution ---------------------------------------------------------------------
-    def refused_images(self, plan: BootstrapPlan) -> List[str]:
-        """Agent-step images of ``plan`` outside this node's allow-list."""
-        return [str(s.params.get("image", "")) for s in plan.steps
-                if s.action == "agent" and not self.policy.allows(str(s.params.get("image", "")))]
+    def refusals(self, plan: BootstrapPlan) -> List[str]:
+        """Why this node refuses ``plan``: an agent step whose image (RKE1) or Rancher
+        server (RKE2) is outside the node's allow-list."""
+        out = []
+        for s in plan.steps:
+            if s.action != "agent":
+                continue
+            if s.params.get("distribution", plan.distribution) == "rke2":
+                server = str(s.params.get("server") or plan.rancher_url)
+                if not self.policy.allows_server(server) or server != plan.rancher_url:
+                    out.append(f"Rancher server {server!r} is not in this node's allow-list")
+            elif not self.policy.allows(str(s.params.get("image", ""))):
+                out.append(f"image {str(s.params.get('image', ''))!r} is not in this node's allow-list")
+        return out
 
     def run_plan(self, plan: BootstrapPlan) -> Dict[str, Any]:
-        bad = self.refused_images(plan)
+        bad = self.refusals(plan)
         if bad:
-            raise PermissionError(f"image {bad[0]!r} is not in this node's allow-list")
+            raise PermissionError(bad[0])
         results: List[StepResult] = []
         ctx: Dict[str, Any] = {"labels": {}, "capacity": {}}
         t_plan = time.perf_counter()
@@ -224,10 +240,12 @@ class NodeAgent:
         raise StepFailed(step.name, f"unknown runtime action {a!r}")
 
     def _exec_agent(self, plan: BootstrapPlan, step: Step, labels: Dict[str, str]) -> Any:
-        image = _check(_IMAGE_RE, step.params.get("image", ""), "agent image")
         role = plan.role if plan.role in _ROLES else ""
         if not role:
             raise ValueError(f"invalid role {plan.role!r}")
+        if step.params.get("distribution", plan.distribution) == "rke2":
+            return self._exec_system_agent(plan, role, labels)
+        image = _check(_IMAGE_RE, step.params.get("image", ""), "agent image")
         argv = ["docker", "run", "-d", "--privileged", "--restart=unless-stopped", "--net=host",
                 "-v", "/etc/kubernetes:/etc/kubernetes", "-v", "/var/run:/var/run", image,
                 "--server", _check(_URL_RE, plan.rancher_url, "rancher url"),
@@ -236,6 +254,34 @@ class NodeAgent:
         for k in sorted(labels):
             argv += ["--label", f"{k}={labels[k]}"]
         return self._run_argv(argv)
+
+    def _fetch_installer(self, plan: BootstrapPlan) -> bytes:
+        """The allowed server's ``system-agent-install.sh`` (Rancher serves it with its own
+        certificate, which the installer then pins through ``--ca-checksum``)."""
+        from ..versions import SYSTEM_AGENT_INSTALL_PATH
+
+        url = _check(_URL_RE, plan.rancher_url, "rancher url")
+        body = HTTPClient(base_url=url, verify_tls=False).request("GET", SYSTEM_AGENT_INSTALL_PATH).body
+        if not body.startswith(b"#!"):
+            raise RuntimeError(f"{url}{SYSTEM_AGENT_INSTALL_PATH} is not an installer script")
+        return body
+
+    def _exec_system_agent(self, plan: BootstrapPlan, role: str, labels: Dict[str, str]) -> Any:
+        script = self._fetch_installer(plan)
+        fd, path = tempfile.mkstemp(prefix="tk-system-agent-install-", suffix=".sh")
+        try:
+            with os.fdopen(fd, "wb") as fh:
+                fh.write(script)
+            argv = ["sh", path, "--server", _check(_URL_RE, plan.rancher_url, "rancher url"),
+                    "--label", "cattle.io/os=linux",
+                    "--token", _check(_TOKEN_RE, plan.token, "registration token"),
+                    "--ca-checksum", _check(_TOKEN_RE, plan.ca_checksum, "ca checksum"),
+                    "--node-name", _check(_HOSTNAME_RE, plan.hostname, "hostname"), f"--{role}"]
+            for k in sorted(labels):
+                argv += ["--label", f"{k}={labels[k]}"]
+            return self._run_argv(argv)
+        finally:
+            os.unlink(path)
 
     def _run_step(self, plan: BootstrapPlan, step: Step, ctx: Dict[str, Any]) -> Any:
         a = step.action
@@ -427,6 +473,9 @@ class NodeAgent:
         http = HTTPClient(base_url=plan.rancher_url, verify_tls=False)
         hdrs = {"X-API-Tunnel-Token": plan.token,
                 "X-API-Tunnel-Params": tunnel_params(plan.hostname, roles, ctx["labels"], ctx["capacity"])}
+        if plan.distribution == "rke2":
+            self._fetch_installer(plan)  # what a real node runs first
+            hdrs["X-Cattle-Agent-Kind"] = "system-agent"
         return http.request("POST", "/v3/connect/register", headers=hdrs, data=b"{}").json()
 
     # --- RCCL gate (this node's ranks) ---------------------------------------------------------
@@ -715,9 +764,9 @@ class NodeAgent:
                     body = self._body()
                     if path == "/v1/plan":
                         plan = BootstrapPlan.from_json(body["plan"])
-                        bad = agent.refused_images(plan)
+                        bad = agent.refusals(plan)
                         if bad:
-                            return self._reply(403, {"error": f"image {bad[0]!r} is not in this node's allow-list"})
+                            return self._reply(403, {"error": bad[0]})
                         return self._reply(200, agent.run_plan(plan))
                     if path == "/v1/rccl-uid":
                         return self._reply(200, {"uid": base64.b64encode(agent.new_uid()).decode()})
@@ -803,6 +852,9 @@ def main(argv: Optional[List[str]] = None) -> int:
     ap.add_argument("--insecure-local", action="store_true",
                     help="plain HTTP on a loopback address (development, single-box tests)")
     ap.add_argument("--token-file", default="", help="file holding the token (with --insecure-local)")
+    ap.add_argument("--allow-server", action="append", default=[],
+                    help="with --insecure-local: a Rancher server URL whose RKE2 installer the node may run "
+                         "(besides loopback ones); repeatable")
     ap.add_argument("--root", default="/")
     ap.add_argument("--name", default="", help="agent name (defaults to the listen host)")
     ap.add_argument("--synthetic-gpus", type=int, default=0,
@@ -822,6 +874,10 @@ def main(argv: Optional[List[str]] = None) -> int:
         ap.error("--credentials DIR is required (or --insecure-local for plain HTTP on loopback)")
     elif not is_loopback(host):
         ap.error(f"--insecure-local serves plain HTTP on loopback only, not {host}")
+    else:
+        from ..versions import AGENT_IMAGE
+
+        policy = AgentPolicy([AGENT_IMAGE], servers=list(args.allow_server), loopback_servers=True)
     if args.token_file and not token:
         with open(args.token_file, "r", encoding="utf-8") as fh:
             token = fh.read().strip()

@@ -15,16 +15,21 @@ Step catalogue (``action`` ids):
 
 ==================  ==============================================================
 ``firewall``        stop/disable firewalld (S5)
-``runtime``         install the container runtime if absent, overlay2 (S1/S5/S6)
+``runtime``         RKE1: install Docker if absent, overlay2 (S1/S5/S6); RKE2 brings
+                    its own containerd (no step)
 ``hostname``        ``hostnamectl set-hostname`` (S5)
-``registry_login``  ``docker login`` when registry credentials are given (S5)
+``registry_login``  RKE1: ``docker login`` when registry credentials are given (S5);
+                    RKE2 nodes get registries from the cluster's ``rkeConfig``
 ``gpu_preflight``   MI355X: amdgpu loaded, ``/dev/kfd`` + ``/dev/dri`` present, N GPUs
 ``gpu_labels``      MI355X: N1 topology labeller -> node labels file
 ``gpu_burnin``      MI355X: HBM / MFMA / memtest probes per GPU
 ``rccl_env``        MI355X: write ``/etc/rccl/rccl.env``
 ``rccl_local``      MI355X: node-level RCCL all-reduce sweep over the local GPUs (N2)
-``agent``           run ``rancher/agent`` with ``--server/--token/--ca-checksum/--<role>``
-                    and ``--label`` flags (GPU labels on MI355X nodes)
+``agent``           join: RKE2 -> the server's ``system-agent-install.sh`` (installs
+                    ``rancher-system-agent``) with ``--server/--token/--ca-checksum/
+                    --node-name/--<role>``; RKE1 -> ``docker run rancher/rancher-agent``
+                    with ``--server/--token/--ca-checksum/--<role>``; both with
+                    ``--label`` flags (GPU labels on MI355X nodes)
 ==================  ==============================================================
 """
 
@@ -37,6 +42,7 @@ from ..parallel.rccl_env import render_env_file
 from ..terraform.scripts import RCCL_SLIM_ENABLE_FN, RCCL_SLIM_FN, RCCL_SLIM_ROOT
 
 from ..versions import AGENT_IMAGE as DEFAULT_AGENT_IMAGE
+from ..versions import DEFAULT_DISTRIBUTION, SYSTEM_AGENT_INSTALL_PATH
 from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
 from .labels import DEFAULT_MIN_LINK_GBPS
 from .manager import docker_install_lines
@@ -68,6 +74,7 @@ class BootstrapPlan:
     ca_checksum: str
     steps: List[Step] = field(default_factory=list)
     gpu: Optional[Dict[str, Any]] = None
+    distribution: str = DEFAULT_DISTRIBUTION  # rke2 | rke1: how the agent step joins
 
     def step_names(self) -> List[str]:
         return [s.name for s in self.steps]
@@ -155,7 +162,11 @@ def build_host_plan(cfg: Dict[str, Any], rancher_url: str, token: str, ca_checks
     """Plan for a ``*-rancher-k8s-host`` module config with resolved interpolations."""
     role = host_role(cfg)
     hostname = cfg.get("hostname", "")
-    plan = BootstrapPlan(hostname, role, rancher_url, token, ca_checksum)
+    dist = str(cfg.get("k8s_distribution") or DEFAULT_DISTRIBUTION)
+    if dist not in ("rke2", "rke1"):
+        raise ValueError(f"k8s_distribution must be rke2 or rke1, not {dist!r}")
+    rke1 = dist == "rke1"
+    plan = BootstrapPlan(hostname, role, rancher_url, token, ca_checksum, distribution=dist)
     install_url = cfg.get("docker_engine_install_url") or DEFAULT_DOCKER_INSTALL_URL
     image = cfg.get("rancher_agent_image") or DEFAULT_AGENT_IMAGE
     reg, reg_user, reg_pass = (cfg.get("rancher_registry", ""), cfg.get("rancher_registry_username", ""),
@@ -165,7 +176,8 @@ if command -v firewalld >/dev/null 2>&1; then
   sudo systemctl stop firewalld.service || true
   sudo systemctl disable firewalld.service || true
 fi"""))
-    plan.steps.append(Step("runtime", "runtime", f"""
+    if rke1:
+        plan.steps.append(Step("runtime", "runtime", f"""
 {docker_install_lines(install_url, cfg.get("docker_install_sha256", "")).rstrip()}
 if [ ! -f /etc/docker/daemon.json ] || ! grep -q overlay2 /etc/docker/daemon.json; then
   echo '{{"storage-driver": "overlay2"}}' | sudo tee /etc/docker/daemon.json >/dev/null
@@ -173,7 +185,7 @@ if [ ! -f /etc/docker/daemon.json ] || ! grep -q overlay2 /etc/docker/daemon.jso
 fi""", {"install_url": install_url}))
     plan.steps.append(Step("hostname", "hostname", f"sudo hostnamectl set-hostname {_q(hostname)}",
                            {"hostname": hostname}))
-    if reg_user:
+    if reg_user and rke1:
         plan.steps.append(Step("registry_login", "registry_login",
                                f"echo {_q(reg_pass)} | sudo docker login -u {_q(reg_user)} --password-stdin {_q(reg)}",
                                {"registry": reg, "username": reg_user, "password": reg_pass}))
@@ -256,11 +268,22 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
                                    gpu=True))
         label_args = (f' $(cat {LABEL_FILE} $([ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}) '
                       f'| sed "s/^/--label /" | tr "\\n" " ")')
-    plan.steps.append(Step("agent", "agent", (
-        f"sudo docker run -d --privileged --restart=unless-stopped --net=host "
-        f"-v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run {_q(image)} "
-        f"--server {_q(rancher_url)} --token {_q(token)} --ca-checksum {_q(ca_checksum)} --{role}{label_args}"),
-        {"image": image, "role": role}))
+    if rke1:
+        plan.steps.append(Step("agent", "agent", (
+            f"sudo docker run -d --privileged --restart=unless-stopped --net=host "
+            f"-v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run {_q(image)} "
+            f"--server {_q(rancher_url)} --token {_q(token)} --ca-checksum {_q(ca_checksum)} --{role}{label_args}"),
+            {"image": image, "role": role, "distribution": "rke1"}))
+    else:
+        # the registration command Rancher shows for a custom RKE2 cluster: the server's
+        # installer sets up rancher-system-agent, which then installs RKE2 for the role
+        installer = rancher_url.rstrip("/") + SYSTEM_AGENT_INSTALL_PATH
+        plan.steps.append(Step("agent", "agent", (
+            f"curl -fsSLk -o /tmp/tk-system-agent-install.sh {_q(installer)}\n"
+            f"sudo sh /tmp/tk-system-agent-install.sh --server {_q(rancher_url)} --label cattle.io/os=linux "
+            f"--token {_q(token)} --ca-checksum {_q(ca_checksum)} --node-name {_q(hostname)} --{role}{label_args}\n"
+            f"rm -f /tmp/tk-system-agent-install.sh"),
+            {"server": rancher_url, "role": role, "distribution": "rke2"}))
     return plan
 
 

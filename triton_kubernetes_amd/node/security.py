@@ -14,9 +14,11 @@ equivalent bar:
 * **per-node tokens** -- ``HMAC-SHA256(manager secret, "tk-agent-token" | address)``:
   a token read off one node (or its credentials directory) is useless on every other
   node, and tokens are never stored: the CLI derives them from the manager secret;
-* **image allow-list** -- the agent runs only the Rancher agent images its credentials
-  list (:class:`AgentPolicy`, written by the manager at enrollment: the manager's pinned
-  agent image, or a digest-pinned one); any other image in a plan is refused (403).
+* **allow-list** -- the agent runs only the Rancher agent images its credentials list
+  (:class:`AgentPolicy`, written by the manager at enrollment: the manager's pinned agent
+  image, or a digest-pinned one), and joins an RKE2 cluster only through the
+  ``system-agent-install.sh`` of a Rancher server the list names (the manager's URL);
+  a plan naming any other image or server is refused (403) before any step runs.
 
 ``triton-kubernetes credentials node`` (``agent_address: <node>``) writes a node's credential
 directory (``agent-token``, ``agent.crt``, ``agent.key``, ``ca.crt``,
@@ -62,25 +64,57 @@ def is_loopback(host: str) -> bool:
         return False
 
 
+def server_origin(url: str) -> str:
+    """``https://Rancher.example:443/x`` -> ``https://rancher.example:443``: what a
+    server allow-list entry and a plan's Rancher URL are compared by."""
+    parts = urllib.parse.urlsplit(url.strip())
+    if parts.scheme not in ("https", "http") or not parts.hostname:
+        return ""
+    port = parts.port or (443 if parts.scheme == "https" else 80)
+    host = parts.hostname.lower()
+    return f"{parts.scheme}://{'[' + host + ']' if ':' in host else host}:{port}"
+
+
 @dataclass
 class AgentPolicy:
-    """What a node agent may run: the Rancher agent images it accepts.  An entry with a
-    digest (``repo@sha256:...``) matches only that digest; a tag entry matches that tag."""
+    """What a node agent may run: the Rancher agent images it accepts (RKE1: ``docker run``)
+    and the Rancher servers whose system-agent installer it may run (RKE2).  An image entry
+    with a digest (``repo@sha256:...``) matches only that digest; a tag entry matches that
+    tag.  A server entry matches by scheme, host and port.  ``loopback_servers`` (the
+    default policy of an agent started without credentials: in-process test agents and
+    ``--insecure-local`` development agents, which serve loopback only) also admits any
+    Rancher server on a loopback address."""
 
     images: List[str] = field(default_factory=list)
+    servers: List[str] = field(default_factory=list)
+    loopback_servers: bool = False
 
     def allows(self, image: str) -> bool:
         return image in self.images
 
+    def allows_server(self, url: str) -> bool:
+        origin = server_origin(url)
+        if not origin:
+            return False
+        if self.loopback_servers and is_loopback(urllib.parse.urlsplit(origin).hostname or ""):
+            return True
+        return origin in {server_origin(s) for s in self.servers}
+
     def to_json(self) -> Dict[str, Any]:
-        return {"images": list(self.images)}
+        doc: Dict[str, Any] = {"images": list(self.images), "servers": list(self.servers)}
+        if self.loopback_servers:
+            doc["loopback_servers"] = True
+        return doc
 
     @classmethod
     def from_json(cls, doc: Dict[str, Any]) -> "AgentPolicy":
         imgs = doc.get("images") or []
         if not isinstance(imgs, list) or not all(isinstance(i, str) and i for i in imgs):
             raise TKError("agent policy: images must be a list of image references")
-        return cls(images=list(imgs))
+        servers = doc.get("servers") or []
+        if not isinstance(servers, list) or not all(isinstance(u, str) and server_origin(u) for u in servers):
+            raise TKError("agent policy: servers must be a list of http(s) Rancher server URLs")
+        return cls(images=list(imgs), servers=list(servers), loopback_servers=doc.get("loopback_servers") is True)
 
 
 @dataclass
@@ -125,14 +159,15 @@ class AgentPKI:
         mac = hmac.new(self.secret, b"tk-agent-token\0" + agent_address(address).encode(), hashlib.sha256)
         return "tka1." + mac.hexdigest()
 
-    def issue(self, address: str, images: List[str], extra_names: Optional[List[str]] = None) -> NodeCredentials:
+    def issue(self, address: str, images: List[str], extra_names: Optional[List[str]] = None,
+              servers: Optional[List[str]] = None) -> NodeCredentials:
         from ..k8s.tls import CA, issue
 
         host = agent_address(address)
         names = [host] + [n for n in (extra_names or []) if n != host]
         cert = issue(CA(self.ca_cert, self.ca_key), host, names)
         return NodeCredentials(host, self.node_token(host), cert.cert_pem, cert.key_pem, self.ca_cert,
-                               AgentPolicy(list(images)))
+                               AgentPolicy(list(images), list(servers or [])))
 
     def client_context(self) -> ssl.SSLContext:
         """Verifies agents against this manager's CA only (not the system trust store)."""
@@ -197,4 +232,4 @@ def read_credentials(directory: str) -> Dict[str, Any]:
 
 
 __all__ = ["AgentPKI", "AgentPolicy", "NodeCredentials", "load_pki", "server_context", "read_credentials",
-           "agent_address", "is_loopback", "PKI_BLOB", "DEFAULT_CRED_DIR"]
+           "agent_address", "is_loopback", "server_origin", "PKI_BLOB", "DEFAULT_CRED_DIR"]

@@ -8,8 +8,12 @@ In-process replacements for the reference's shell + curl + jq scripts:
   non-expiring ``triton-kubernetes`` API token, change the admin password, set
   ``server-url``;
 * :meth:`RancherClient.ensure_cluster` — ``rancher_cluster.sh`` (S4): find or
-  create the RKE cluster by name, get or create its registration token, and the
-  CA checksum (sha256 of ``cacerts`` + newline, exactly what the script hashes);
+  create the cluster by name, get or create its registration token, and the
+  CA checksum (sha256 of ``cacerts`` + newline, exactly what the script hashes).
+  RKE2 (default, ``versions.py``): a ``provisioning.cattle.io/v1`` ``Cluster`` in
+  ``fleet-default`` with an ``rkeConfig``, whose management cluster (``status.clusterName``,
+  ``c-m-…``) carries the registration token nodes hand to ``system-agent-install.sh``;
+  RKE1: the reference's v3 ``cluster`` with ``rancherKubernetesEngineConfig``;
 * new: cluster / node status, Kubernetes API through Rancher's ``/k8s/clusters``
   proxy (used by the readiness waiter and the MI355X add-on step), cleanup.
 
@@ -25,7 +29,7 @@ from typing import Any, Callable, Dict, List, Optional
 
 from ..cloud.http import HTTPClient, HTTPError
 from ..errors import TKError
-from ..versions import DEFAULT_K8S_VERSION, resolve_against
+from ..versions import FLEET_NAMESPACE, default_version, resolve_against, resolve_distribution
 
 TOKEN_NAME = "triton-kubernetes"
 
@@ -191,27 +195,101 @@ class RancherClient:
         """RKE1 releases this server offers (its KDM list, setting ``k8s-versions-current``)."""
         return [v.strip() for v in self.setting("k8s-versions-current").split(",") if v.strip()]
 
-    def resolve_k8s_version(self, requested: str) -> str:
-        """``requested`` if offered, else the server's release of the same minor; a minor
-        the server does not offer is an error here rather than a failed RKE provision."""
+    def rke2_versions(self) -> List[str]:
+        """RKE2 releases this server offers (``/v1-rke2-release/releases``, from its KDM data)."""
         try:
-            version, note = resolve_against(requested, self.k8s_versions())
+            data = self.http.get_json("/v1-rke2-release/releases").get("data", [])
+        except HTTPError as exc:
+            if exc.status in (403, 404):
+                return []
+            raise
+        return [str(r.get("version") or r.get("id") or "") for r in data if r.get("version") or r.get("id")]
+
+    def resolve_k8s_version(self, requested: str, distribution: str = "rke1") -> str:
+        """``requested`` if offered, else the server's release of the same minor; a minor
+        the server does not offer is an error here rather than a failed provision."""
+        offered = self.rke2_versions() if distribution == "rke2" else self.k8s_versions()
+        try:
+            version, note = resolve_against(requested, offered)
         except ValueError as exc:
             raise TKError(str(exc)) from None
         self.last_version_note = note
         return version
 
-    def ensure_cluster(self, name: str, k8s_version: str = DEFAULT_K8S_VERSION, network_provider: str = "flannel",
+    # --- RKE2 (provisioning v2) ------------------------------------------------------------------
+    def find_v2_cluster(self, name: str) -> Optional[Dict[str, Any]]:
+        try:
+            return self.http.get_json(f"/v1/provisioning.cattle.io.clusters/{FLEET_NAMESPACE}/{name}")
+        except HTTPError as exc:
+            if exc.status == 404:
+                return None
+            raise
+
+    def create_v2_cluster(self, name: str, k8s_version: str, cni: str, k8s_registry: str = "",
+                          k8s_registry_username: str = "", k8s_registry_password: str = "") -> Dict[str, Any]:
+        """A custom RKE2 cluster: nodes are added by running the registration command."""
+        rke: Dict[str, Any] = {"machineGlobalConfig": {"cni": cni, "disable-kube-proxy": False},
+                               "machinePools": [], "upgradeStrategy": {"controlPlaneConcurrency": "1",
+                                                                       "workerConcurrency": "1"}}
+        if k8s_registry:
+            config: Dict[str, Any] = {}
+            if k8s_registry_username:
+                # registry credentials: a basic-auth Secret in fleet-default the config names
+                config["authConfigSecretName"] = self.create_registry_secret(k8s_registry_username,
+                                                                             k8s_registry_password)
+            rke["registries"] = {"mirrors": {"docker.io": {"endpoint": [f"https://{k8s_registry}"]}},
+                                 "configs": {k8s_registry: config}}
+        body = {"apiVersion": "provisioning.cattle.io/v1", "kind": "Cluster",
+                "metadata": {"name": name, "namespace": FLEET_NAMESPACE},
+                "spec": {"kubernetesVersion": k8s_version, "rkeConfig": rke}}
+        return self.http.post_json("/v1/provisioning.cattle.io.clusters", body)
+
+    def create_registry_secret(self, username: str, password: str) -> str:
+        """A ``kubernetes.io/basic-auth`` Secret in fleet-default -> its name."""
+        b64 = lambda v: base64.b64encode(v.encode()).decode()  # noqa: E731
+        body = {"type": "kubernetes.io/basic-auth",
+                "metadata": {"generateName": "registryconfig-auth-", "namespace": FLEET_NAMESPACE},
+                "data": {"username": b64(username), "password": b64(password)}}
+        return str(self.http.post_json("/v1/secrets", body)["metadata"]["name"])
+
+    def v2_management_id(self, name: str, timeout: float = 120.0) -> str:
+        """The management cluster (``c-m-…``) Rancher's controllers create for a
+        provisioning cluster, once ``status.clusterName`` is set."""
+        return wait_until(lambda: ((self.find_v2_cluster(name) or {}).get("status") or {}).get("clusterName"),
+                          timeout, f"the management cluster of {name}")
+
+    def ensure_cluster(self, name: str, k8s_version: str = "", network_provider: str = "flannel",
                        k8s_registry: str = "", k8s_registry_username: str = "",
-                       k8s_registry_password: str = "") -> ClusterInfo:
-        existing = self.find_cluster(name)
-        if existing is not None:
-            cluster_id, existed = existing.get("id", ""), True
+                       k8s_registry_password: str = "", distribution: str = "") -> ClusterInfo:
+        """Find or create cluster ``name`` of ``distribution`` (default: the one ``k8s_version``
+        names, else RKE2) -> id, registration token, CA checksum.  ``k8s_version`` defaults
+        to the pinned release of the distribution."""
+        try:
+            dist = resolve_distribution(k8s_version, distribution)
+        except ValueError as exc:
+            raise TKError(str(exc)) from None
+        k8s_version = k8s_version or default_version(dist)
+        other = self.find_cluster(name)  # v3: every cluster, RKE1 or the management side of RKE2
+        other_dist = None if other is None else ("rke2" if other.get("driver") == "rke2" else "rke1")
+        if other_dist is not None and other_dist != dist:
+            raise TKError(f"cluster '{name}' already exists as an {other_dist.upper()} cluster; "
+                          f"it cannot be reused as {dist.upper()}")
+        if dist == "rke2":
+            existing = self.find_v2_cluster(name)
+            existed = existing is not None
+            if not existed:
+                version = self.resolve_k8s_version(k8s_version, "rke2")
+                self.create_v2_cluster(name, version, network_provider, k8s_registry, k8s_registry_username,
+                                       k8s_registry_password)
+            cluster_id = self.v2_management_id(name)
         else:
-            k8s_version = self.resolve_k8s_version(k8s_version)
-            cluster_id = self.create_cluster(name, k8s_version, network_provider, k8s_registry,
-                                             k8s_registry_username, k8s_registry_password).get("id", "")
-            existed = False
+            if other is not None:
+                cluster_id, existed = other.get("id", ""), True
+            else:
+                k8s_version = self.resolve_k8s_version(k8s_version, "rke1")
+                cluster_id = self.create_cluster(name, k8s_version, network_provider, k8s_registry,
+                                                 k8s_registry_username, k8s_registry_password).get("id", "")
+                existed = False
         if not cluster_id:
             raise TKError("Unable to create cluster!")
         token = self.registration_token(cluster_id, create=not existed)
@@ -230,8 +308,15 @@ class RancherClient:
         return self.http.get_json("/v3/nodes", params={"clusterId": cluster_id}).get("data", [])
 
     def delete_cluster(self, cluster_id: str) -> None:
+        """Delete a cluster.  An RKE2 cluster's management object (``c-m-…``) is owned by
+        its provisioning cluster, which is what gets deleted (the controllers would
+        otherwise recreate the management cluster)."""
         try:
-            self.http.request("DELETE", f"/v3/clusters/{cluster_id}")
+            if cluster_id.startswith("c-m-"):
+                name = str(self.cluster(cluster_id).get("name", ""))
+                self.http.request("DELETE", f"/v1/provisioning.cattle.io.clusters/{FLEET_NAMESPACE}/{name}")
+            else:
+                self.http.request("DELETE", f"/v3/clusters/{cluster_id}")
         except HTTPError as exc:
             if exc.status != 404:
                 raise

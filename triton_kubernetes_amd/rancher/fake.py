@@ -10,13 +10,21 @@ real server does after agents register:
 * S4 cluster endpoints (find/create cluster, registration tokens, cacerts).  A
   cluster whose ``kubernetesVersion`` is not in the server's KDM list (setting
   ``k8s-versions-current``: the pinned Rancher's RKE1 releases, versions.py) is
-  rejected with 422, as the real server does.  A new registration token's value is
+  rejected with 422, as the real server does;
+* RKE2 custom clusters (provisioning v2): ``POST /v1/provisioning.cattle.io.clusters``
+  (``fleet-default``; a release outside ``/v1-rke2-release/releases`` or an unknown CNI
+  is rejected with 422), ``GET …/fleet-default/<name>`` whose ``status.clusterName``
+  (the ``c-m-…`` management cluster) the controllers fill in after the create returns;
+  the management cluster then behaves like an RKE1 one (tokens, nodes, proxy, state);
+  ``GET /system-agent-install.sh`` serves the node installer;  A new registration token's value is
   filled in by the server's controller after the create returns
   (``async_registration_tokens``, default on): the POST answers with an empty
   ``token`` and the first read of the object after that sees it, so clients must poll;
 * ``POST /v3/connect/register`` — agent registration (``X-API-Tunnel-Token`` +
   base64 JSON ``X-API-Tunnel-Params`` with hostname, roles, labels, capacity),
-  standing in for the rancher-agent websocket tunnel;
+  standing in for the rancher-agent websocket tunnel; ``X-Cattle-Agent-Kind:
+  system-agent`` marks an RKE2 node's ``rancher-system-agent``.  A node of the wrong
+  kind for its cluster's distribution is refused (400);
 * RKE simulation: a cluster turns ``active`` ``rke_seconds`` after it has at
   least one etcd, one controlplane and one worker node; nodes then report the
   Kubernetes ``Ready`` condition;
@@ -55,15 +63,21 @@ import urllib.parse
 import uuid
 from typing import Any, Dict, List, Optional, Sequence, Set, Tuple
 
-from ..versions import DEFAULT_K8S_VERSION, K8S_VERSIONS, PASSWORD_MIN_LENGTH, RANCHER_VERSION, bootstrap_password
+from ..versions import (DEFAULT_K8S_VERSION, FLEET_NAMESPACE, K8S_VERSIONS, PASSWORD_MIN_LENGTH, RANCHER_VERSION,
+                        RKE2_CNIS, RKE2_VERSIONS, SYSTEM_AGENT_INSTALL_PATH, bootstrap_password)
 from ..utils.httpserver import Server as HTTPServer
 
 FAKE_CACERTS = "-----BEGIN CERTIFICATE-----\nMIIFAKECERTIFICATEFORTESTS\n-----END CERTIFICATE-----"
+# what GET /system-agent-install.sh serves here: records its arguments (tests run it)
+SYSTEM_AGENT_INSTALL_SCRIPT = """#!/bin/sh
+# fake rancher-system-agent installer
+echo "system-agent-install $*" >> "${TK_FAKE_SYSTEM_AGENT_LOG:-/dev/null}"
+"""
 
 
 class _State:
     def __init__(self, rke_seconds: float, node_ready_seconds: float, admin_password: str,
-                 k8s_versions: Sequence[str]):
+                 k8s_versions: Sequence[str], rke2_versions: Sequence[str] = ()):
         self.mu = threading.RLock()
         self.cond = threading.Condition(self.mu)
         self.admin_password = admin_password
@@ -74,6 +88,9 @@ class _State:
                                          "k8s-version": DEFAULT_K8S_VERSION,
                                          "password-min-length": str(PASSWORD_MIN_LENGTH)}
         self.clusters: Dict[str, Dict[str, Any]] = {}
+        self.rke2_versions: List[str] = list(rke2_versions)
+        self.v2_clusters: Dict[str, Dict[str, Any]] = {}  # "<namespace>/<name>" -> provisioning object
+        self.secrets: Dict[str, Dict[str, Any]] = {}  # "<namespace>/<name>" -> Secret (management cluster)
         self.reg_tokens: Dict[str, Dict[str, Any]] = {}  # token -> {clusterId, id}
         self.nodes: Dict[str, Dict[str, Any]] = {}
         # indexes, so a request costs the same however many clusters the server holds
@@ -91,11 +108,12 @@ class FakeRancher:
     def __init__(self, rke_seconds: float = 0.0, node_ready_seconds: float = 0.0,
                  bootstrap_password: Optional[str] = None, host: str = "127.0.0.1", port: int = 0,
                  k8s_versions: Optional[Sequence[str]] = None, async_registration_tokens: bool = True,
-                 default_pod_security: str = "privileged"):
+                 default_pod_security: str = "privileged", rke2_versions: Optional[Sequence[str]] = None):
         # a server started without CATTLE_BOOTSTRAP_PASSWORD has a random one nobody knows
         pw = bootstrap_password if bootstrap_password is not None else secrets.token_hex(16)
         self.state = _State(rke_seconds, node_ready_seconds, pw,
-                            list(k8s_versions) if k8s_versions is not None else [v for _, v in K8S_VERSIONS])
+                            list(k8s_versions) if k8s_versions is not None else [v for _, v in K8S_VERSIONS],
+                            list(rke2_versions) if rke2_versions is not None else [v for _, v in RKE2_VERSIONS])
         # "<service>.<namespace>" -> "https://127.0.0.1:<port>" (where an in-cluster
         # webhook service of a test really listens)
         self.service_endpoints: Dict[str, str] = {}
@@ -299,8 +317,26 @@ class FakeRancher:
             return 401, {"type": "error", "code": "Unauthorized"}
         if path == "/v3/connect/register" and method == "POST":
             return self._register(h)
+        if path == SYSTEM_AGENT_INSTALL_PATH and method == "GET":
+            return 200, SYSTEM_AGENT_INSTALL_SCRIPT.encode()
         if not h._authed():
             return 401, {"type": "error", "code": "Unauthorized"}
+        if path == "/v1-rke2-release/releases" and method == "GET":
+            return 200, {"data": [{"id": v, "version": v, "type": "release"} for v in st.rke2_versions]}
+        if path == "/v1/provisioning.cattle.io.clusters" and method == "POST":
+            return self._create_v2(body)
+        if path == "/v1/secrets" and method == "POST":
+            meta = dict((body or {}).get("metadata") or {})
+            ns = meta.get("namespace") or "default"
+            name = meta.get("name") or (meta.get("generateName", "secret-") + uuid.uuid4().hex[:5])
+            with st.mu:
+                if f"{ns}/{name}" in st.secrets:
+                    return 409, {"type": "error", "code": "AlreadyExists"}
+                st.secrets[f"{ns}/{name}"] = dict(body, metadata=dict(meta, name=name, namespace=ns))
+                return 201, json.loads(json.dumps(st.secrets[f"{ns}/{name}"]))
+        if path.startswith("/v1/provisioning.cattle.io.clusters/"):
+            key = path[len("/v1/provisioning.cattle.io.clusters/"):]
+            return self._v2_cluster(method, key)
         if path == "/v3/token" and method == "POST":
             name, secret = f"token-{uuid.uuid4().hex[:5]}", uuid.uuid4().hex
             with st.mu:
@@ -335,7 +371,8 @@ class FakeRancher:
             with st.mu:
                 st.clusters[cid] = {"id": cid, "name": body.get("name", ""), "state": "provisioning",
                                     "transitioning": "yes", "rancherKubernetesEngineConfig":
-                                        body.get("rancherKubernetesEngineConfig", {}), "created": time.time()}
+                                        body.get("rancherKubernetesEngineConfig", {}), "created": time.time(),
+                                    "driver": "rancherKubernetesEngine", "version": {"gitVersion": version}}
                 st.cluster_nodes[cid] = {}
                 st.unsettled.add(cid)
                 return 201, dict(st.clusters[cid])
@@ -400,6 +437,72 @@ class FakeRancher:
     def _admit(self, cid: str, namespace: str, pod: Dict[str, Any]) -> Dict[str, Any]:
         return _admit_pod(self, cid, namespace, pod)
 
+    # --- RKE2 custom clusters (provisioning.cattle.io/v1) ------------------------------------------
+    def _create_v2(self, body: Dict[str, Any]) -> Tuple[int, Any]:
+        st = self.state
+        meta, spec = body.get("metadata") or {}, body.get("spec") or {}
+        ns, name = meta.get("namespace") or FLEET_NAMESPACE, meta.get("name", "")
+        version = spec.get("kubernetesVersion", "")
+        if version not in st.rke2_versions:
+            return 422, {"type": "error", "code": "Invalid", "fieldName": "spec.kubernetesVersion",
+                         "message": f"{version} is not a supported RKE2 version"}
+        cni = ((spec.get("rkeConfig") or {}).get("machineGlobalConfig") or {}).get("cni", "canal")
+        if cni not in RKE2_CNIS:
+            return 422, {"type": "error", "code": "Invalid", "message": f"unsupported cni {cni!r}"}
+        for host, conf in (((spec.get("rkeConfig") or {}).get("registries") or {}).get("configs") or {}).items():
+            unknown = set(conf) - {"authConfigSecretName", "caBundle", "insecureSkipVerify", "tlsSecretName"}
+            ref = conf.get("authConfigSecretName")
+            if unknown or (ref and f"{ns}/{ref}" not in st.secrets):
+                # the schema has no inline credentials: they live in a Secret of the namespace
+                return 422, {"type": "error", "code": "Invalid",
+                             "message": f"registries.configs[{host}]: unknown fields {sorted(unknown)} or "
+                                        f"missing secret {ref!r}"}
+        with st.mu:
+            if f"{ns}/{name}" in st.v2_clusters:
+                return 409, {"type": "error", "code": "AlreadyExists"}
+            obj = json.loads(json.dumps(body))
+            obj["metadata"].update(namespace=ns, uid=str(uuid.uuid4()))
+            obj["status"] = {"ready": False}  # clusterName: filled in by the controllers
+            st.v2_clusters[f"{ns}/{name}"] = obj
+            return 201, json.loads(json.dumps(obj))
+
+    def _v2_cluster(self, method: str, key: str) -> Tuple[int, Any]:
+        st = self.state
+        with st.mu:
+            obj = st.v2_clusters.get(key)
+            if obj is None:
+                return 404, {"type": "error", "code": "NotFound"}
+            if method == "DELETE":
+                st.v2_clusters.pop(key)
+                cid = obj["status"].get("clusterName")
+                if cid:
+                    st.clusters.pop(cid, None)
+                    for nid in st.cluster_nodes.pop(cid, {}):
+                        st.nodes.pop(nid, None)
+                return 200, {}
+            if not obj["status"].get("clusterName"):
+                # the provisioning controller creates the management cluster after the create
+                cid = f"c-m-{uuid.uuid4().hex[:8]}"
+                version = obj["spec"].get("kubernetesVersion", "")
+                st.clusters[cid] = {"id": cid, "name": obj["metadata"]["name"], "state": "provisioning",
+                                    "transitioning": "yes", "driver": "rke2", "created": time.time(),
+                                    "version": {"gitVersion": version}}
+                st.cluster_nodes[cid] = {}
+                st.unsettled.add(cid)
+                obj["status"]["clusterName"] = cid
+                return 200, json.loads(json.dumps(obj))
+            cid = obj["status"]["clusterName"]
+        self._refresh()
+        with st.mu:
+            obj["status"]["ready"] = (st.clusters.get(cid) or {}).get("state") == "active"
+            return 200, json.loads(json.dumps(obj))
+
+    def registry_auth(self, secret: str, namespace: str = FLEET_NAMESPACE) -> Dict[str, str]:
+        """Decoded ``username``/``password`` of a registry basic-auth Secret."""
+        with self.state.mu:
+            data = (self.state.secrets.get(f"{namespace}/{secret}") or {}).get("data") or {}
+        return {k: base64.b64decode(v).decode() for k, v in data.items()}
+
     def namespace_labels(self, cid: str, namespace: str) -> Dict[str, str]:
         """Labels of a Namespace created through the proxy (+ the automatic name label)."""
         with self.state.mu:
@@ -419,6 +522,13 @@ class FakeRancher:
             params = json.loads(base64.b64decode(h.headers.get("X-API-Tunnel-Params", "")) or b"{}")
         except ValueError:
             return 400, {"type": "error", "message": "bad tunnel params"}
+        kind = h.headers.get("X-Cattle-Agent-Kind", "rancher-agent")
+        with st.mu:
+            prov = "rke2" if (st.clusters.get(reg["clusterId"]) or {}).get("driver") == "rke2" else "rke1"
+        if (prov == "rke2") != (kind == "system-agent"):
+            want = "rancher-system-agent (system-agent-install.sh)" if prov == "rke2" else "rancher-agent"
+            return 400, {"type": "error", "code": "InvalidAgent",
+                         "message": f"{reg['clusterId']} is an {prov.upper()} cluster: nodes join with {want}"}
         node = params.get("node", {})
         hostname = node.get("requestedHostname", "")
         roles = {"etcd": bool(node.get("etcd")), "controlplane": bool(node.get("controlPlane")),
@@ -428,7 +538,7 @@ class FakeRancher:
             existing = [nid for nid, n in members.items() if n["hostname"] == hostname]
             nid = existing[0] if existing else f"m-{uuid.uuid4().hex[:6]}"
             st.nodes[nid] = members[nid] = {
-                "id": nid, "clusterId": reg["clusterId"], "hostname": hostname, "nodeName": hostname,
+                "id": nid, "clusterId": reg["clusterId"], "hostname": hostname, "nodeName": hostname, "agentKind": kind,
                 "roles": roles, "labels": dict(node.get("labels", {})), "capacity": dict(node.get("capacity", {})),
                 "state": "registering", "registered": time.time(), "ready_at": None}
             st.unsettled.add(reg["clusterId"])
@@ -448,9 +558,9 @@ class FakeRancher:
             return 200, {"kind": "NodeList", "items": self.k8s_nodes(cid)}
         if kpath == "/version":
             with st.mu:
-                v = st.clusters[cid]["rancherKubernetesEngineConfig"].get("kubernetesVersion", DEFAULT_K8S_VERSION)
+                v = (st.clusters[cid].get("version") or {}).get("gitVersion") or DEFAULT_K8S_VERSION
             major, minor = v.lstrip("v").split(".")[:2]
-            return 200, {"major": major, "minor": minor, "gitVersion": v.split("-")[0]}
+            return 200, {"major": major, "minor": minor, "gitVersion": v.split("-")[0].split("+")[0]}
         if method == "POST":
             parts = kpath.strip("/").split("/")
             if len(parts) == 5 and parts[:3] == ["api", "v1", "namespaces"] and parts[4] == "pods":

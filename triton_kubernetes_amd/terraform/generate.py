@@ -142,12 +142,21 @@ VAR_VALIDATIONS = {
                                "(Rancher >= 2.6) without quotes or backslashes."),
     "rancher_bootstrap_password": (_SHELL_SAFE[0].format("rancher_bootstrap_password"),
                                    _SHELL_SAFE[1].format("rancher_bootstrap_password")),
-    "k8s_version": ("contains([" + ", ".join(f'"{m}"' for m in versions.K8S_MINORS) + "], "
-                    'join(".", slice(split(".", var.k8s_version), 0, 2)))',
-                    f"k8s_version must be an RKE1 release of Rancher {versions.RANCHER_VERSION} "
-                    f"({', '.join(v for _, v in versions.K8S_VERSIONS)})."),
-    "k8s_network_provider": ('contains(["calico", "flannel", "canal", "weave"], var.k8s_network_provider)',
-                             "k8s_network_provider must be one of calico, flannel, canal, weave."),
+    # (which distribution the release belongs to is checked against k8s_distribution in a
+    # precondition: a validation block may only read its own variable before Terraform 1.9)
+    "k8s_version": ('(contains([' + ", ".join(f'"{m}"' for m in versions.RKE2_MINORS) + '], '
+                    'join(".", slice(split(".", var.k8s_version), 0, 2))) && '
+                    'length(regexall("[+]rke2r[0-9]+$", var.k8s_version)) > 0) || '
+                    '(contains([' + ", ".join(f'"{m}"' for m in versions.K8S_MINORS) + '], '
+                    'join(".", slice(split(".", var.k8s_version), 0, 2))) && '
+                    'length(regexall("-rancher[0-9]+-[0-9]+$", var.k8s_version)) > 0)',
+                    f"k8s_version must be an RKE2 ({', '.join(v for _, v in versions.RKE2_VERSIONS)}) or RKE1 "
+                    f"({', '.join(v for _, v in versions.K8S_VERSIONS)}) release of Rancher "
+                    f"{versions.RANCHER_VERSION}."),
+    "k8s_distribution": ('contains(["rke2", "rke1"], var.k8s_distribution)', "k8s_distribution must be rke2 or rke1."),
+    "k8s_network_provider": ('contains(["canal", "calico", "cilium", "flannel", "weave"], var.k8s_network_provider)',
+                             "k8s_network_provider must be one of canal, calico, cilium, flannel (RKE2) or weave "
+                             "(RKE1)."),
     "gpu_burnin": ('contains(["quick", "full", "off"], var.gpu_burnin)', "gpu_burnin must be quick, full or off."),
     "rccl_slim": ('contains(["on", "off"], var.rccl_slim)', "rccl_slim must be on or off."),
     "gpu_compute_partition": ('contains(["spx", "dpx", "qpx", "cpx"], var.gpu_compute_partition)',
@@ -211,12 +220,18 @@ MANAGER_BASE = [Var("name", None, "Human readable name used as prefix to generat
 CLUSTER_BASE = [
     Var("name", None, "Human readable name used as prefix to generated names."),
     Var("rancher_api_url", None), Var("rancher_access_key", None), Var("rancher_secret_key", None, sensitive=True),
-    Var("k8s_version", versions.DEFAULT_K8S_VERSION), Var("k8s_network_provider", "flannel"),
+    Var("k8s_distribution", versions.DEFAULT_DISTRIBUTION,
+        "rke2 (provisioning.cattle.io/v1 custom cluster, nodes join with rancher-system-agent) or rke1 "
+        "(v3 cluster + rancher-agent; reference-era documents)"),
+    Var("k8s_version", versions.DEFAULT_K8S_VERSION), Var("k8s_network_provider", "canal"),
     Var("rancher_registry", ""), Var("rancher_registry_username", ""), Var("rancher_registry_password", "", sensitive=True),
     Var("k8s_registry", ""), Var("k8s_registry_username", ""), Var("k8s_registry_password", "", sensitive=True),
 ]
 HOST_BASE = [
     Var("hostname", None), Var("rancher_api_url", None),
+    Var("k8s_distribution", versions.DEFAULT_DISTRIBUTION,
+        "the cluster's distribution: rke2 joins with the server's system-agent installer, rke1 with docker run "
+        "rancher/rancher-agent"),
     Var("rancher_cluster_registration_token", None, sensitive=True), Var("rancher_cluster_ca_checksum", None),
     Var("rancher_host_labels", None, "A single-key map: {worker|etcd|control = \"true\"}", "map(string)"),
 ] + _rancher_image_vars(server=False)
@@ -233,8 +248,9 @@ VSPHERE_CREDS = [Var("vsphere_user", None), Var("vsphere_password", None, sensit
 VSPHERE_NAMES = [Var("vsphere_datacenter_name", None), Var("vsphere_datastore_name", None),
                  Var("vsphere_resource_pool_name", None), Var("vsphere_network_name", None)]
 
-RKE_PORTS = [(22, 22), (80, 80), (443, 443), (2376, 2376), (2379, 2380), (6443, 6443), (8472, 8472),
-             (9099, 9099), (10250, 10252), (10254, 10256), (30000, 32767)]
+# RKE1 + RKE2 node ports (9345: the RKE2 supervisor, 2381: etcd metrics)
+RKE_PORTS = [(22, 22), (80, 80), (443, 443), (2376, 2376), (2379, 2381), (6443, 6443), (8472, 8472),
+             (9099, 9099), (9345, 9345), (10250, 10252), (10254, 10256), (30000, 32767)]
 
 ROLE_LOCAL = """locals {
   rancher_node_role_raw = keys(var.rancher_host_labels)[0]
@@ -361,6 +377,7 @@ def _agent_userdata(disk_device: str = '""', disk_mount: str = '""', extra: str 
     rancher_cluster_registration_token = var.rancher_cluster_registration_token
     rancher_cluster_ca_checksum        = var.rancher_cluster_ca_checksum
     rancher_node_role                  = local.rancher_node_role
+    k8s_distribution                   = var.k8s_distribution
     rancher_agent_image                = var.rancher_agent_image
     rancher_registry                   = var.rancher_registry
     rancher_registry_username          = var.rancher_registry_username
@@ -371,16 +388,23 @@ def _agent_userdata(disk_device: str = '""', disk_mount: str = '""', extra: str 
   }})'''
 
 
+RKE1_CNIS = ("calico", "flannel", "canal", "weave")
+
+
 def _cluster_data() -> str:
-    """S4 as a data source: find-or-create the RKE cluster by name, then its registration
-    token and CA checksum (files/ensure_cluster.sh, run on the operator machine)."""
+    """S4 as a data source: find-or-create the cluster by name (RKE2 or RKE1), then its
+    registration token and CA checksum (files/ensure_cluster.sh, run on the operator machine)."""
+    rke2_cnis = "[" + ", ".join(f'"{c}"' for c in versions.RKE2_CNIS) + "]"
+    rke1_cnis = "[" + ", ".join(f'"{c}"' for c in RKE1_CNIS) + "]"
+    rke2_cni_list, rke1_cni_list = ", ".join(versions.RKE2_CNIS), ", ".join(RKE1_CNIS)
     return f'''locals {{
   # everything ensure_cluster.sh needs, passed as its JSON query
   cluster_request = merge(
     {{
-      name    = var.name
-      version = var.k8s_version
-      network = var.k8s_network_provider
+      name         = var.name
+      version      = var.k8s_version
+      network      = var.k8s_network_provider
+      distribution = var.k8s_distribution
     }},
     {{
       api_url    = var.rancher_api_url
@@ -398,6 +422,16 @@ def _cluster_data() -> str:
 data "external" "cluster" {{
   program = ["bash", "${{path.module}}/files/ensure_cluster.sh"]
   query   = local.cluster_request
+  lifecycle {{
+    precondition {{
+      condition     = (var.k8s_distribution == "rke2") == (length(regexall("[+]rke2r[0-9]+$", var.k8s_version)) > 0)
+      error_message = "k8s_version must be a release of k8s_distribution (RKE2: vX.Y.Z+rke2rN, RKE1: vX.Y.Z-rancherN-N)."
+    }}
+    precondition {{
+      condition     = contains(var.k8s_distribution == "rke2" ? {rke2_cnis} : {rke1_cnis}, var.k8s_network_provider)
+      error_message = "k8s_network_provider is not a CNI of k8s_distribution (RKE2: {rke2_cni_list}; RKE1: {rke1_cni_list})."
+    }}
+  }}
 }}
 '''
 
@@ -1231,6 +1265,7 @@ resource "terraform_data" "install_mi355x_node" {{
       rancher_cluster_registration_token = var.rancher_cluster_registration_token
       rancher_cluster_ca_checksum        = var.rancher_cluster_ca_checksum
       rancher_node_role                  = local.rancher_node_role
+      k8s_distribution                   = var.k8s_distribution
       rancher_agent_image                = var.rancher_agent_image
       rancher_registry                   = var.rancher_registry
       rancher_registry_username          = var.rancher_registry_username

@@ -8,6 +8,17 @@ variable "rancher_api_url" {
   type        = string
 }
 
+variable "k8s_distribution" {
+  description = "the cluster's distribution: rke2 joins with the server's system-agent installer, rke1 with docker run rancher/rancher-agent"
+  type        = string
+  default     = "rke2"
+
+  validation {
+    condition     = contains(["rke2", "rke1"], var.k8s_distribution)
+    error_message = "k8s_distribution must be rke2 or rke1."
+  }
+}
+
 variable "rancher_cluster_registration_token" {
   description = "Registration token of the cluster the node joins."
   type        = string
@@ -44,7 +55,7 @@ variable "docker_install_sha256" {
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
   type        = string
-  default     = "rancher/rancher-agent:v2.8.5"
+  default     = "rancher/rancher-agent:v2.10.3"
 }
 
 variable "rancher_registry" {

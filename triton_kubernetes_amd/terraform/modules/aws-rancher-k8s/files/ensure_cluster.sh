@@ -1,10 +1,13 @@
 #!/bin/bash
-# S4 as a Terraform data "external" program (operator machine): find the RKE cluster
-# by name or create it, then its registration token (reused when the cluster existed)
-# and the checksum of the Rancher CA bundle.  Query keys: name, version, network,
-# api_url, access_key, secret_key, registry, registry_username, registry_password.
+# S4 as a Terraform data "external" program (operator machine): find the cluster by
+# name or create it, then its registration token (reused when the cluster existed) and
+# the checksum of the Rancher CA bundle.  Query keys: name, version, network,
+# distribution (rke2 | rke1), api_url, access_key, secret_key, registry,
+# registry_username, registry_password.  RKE2: a provisioning.cattle.io/v1 Cluster in
+# fleet-default whose management cluster (status.clusterName) holds the token; RKE1:
+# the v3 cluster with rancherKubernetesEngineConfig (the reference's flow).
 exec python3 -c '
-import base64, hashlib, json, re, ssl, sys, time, urllib.parse, urllib.request
+import base64, hashlib, json, re, ssl, sys, time, urllib.error, urllib.parse, urllib.request
 
 q = json.load(sys.stdin)
 ctx = ssl.create_default_context()
@@ -21,9 +24,21 @@ def call(method, path, body=None):
         return json.load(resp)
 
 
-def k8s_version(requested):
+def get_or_none(path):
+    try:
+        return call("GET", path)
+    except urllib.error.HTTPError as exc:
+        if exc.code == 404:
+            return None
+        raise
+
+
+def k8s_version(requested, rke2=False):
     # requested if the server offers it, else its newest release of the same minor
-    offered = [v for v in call("GET", "/v3/settings/k8s-versions-current").get("value", "").split(",") if v]
+    if rke2:
+        offered = [r.get("version") or r.get("id") for r in call("GET", "/v1-rke2-release/releases").get("data", [])]
+    else:
+        offered = [v for v in call("GET", "/v3/settings/k8s-versions-current").get("value", "").split(",") if v]
     if not offered or requested in offered:
         return requested
     minor = requested.split(".")[:2]
@@ -34,10 +49,49 @@ def k8s_version(requested):
     return max(same, key=lambda v: [int(x) for x in re.findall(r"[0-9]+", v)])
 
 
-found = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
-if found:
-    cluster_id = found[0]["id"]
-else:
+dist = q.get("distribution", "rke2")
+v3 = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
+if v3 and ("rke2" if v3[0].get("driver") == "rke2" else "rke1") != dist:
+    sys.exit("cluster %s already exists as an %s cluster; it cannot be reused as %s"
+             % (q["name"], "RKE1" if dist == "rke2" else "RKE2", dist.upper()))
+
+
+def ensure_rke2():
+    v2 = "/v1/provisioning.cattle.io.clusters"
+    path = v2 + "/fleet-default/" + urllib.parse.quote(q["name"])
+    existing = get_or_none(path)
+    found = [existing] if existing else []
+    if not found:
+        rke = {"machineGlobalConfig": {"cni": q["network"]}, "machinePools": []}
+        if q.get("registry"):
+            conf = {}
+            if q.get("registry_username"):
+                # credentials: a basic-auth Secret in fleet-default that the config names
+                b64 = lambda v: base64.b64encode(v.encode()).decode()
+                secret = call("POST", "/v1/secrets", {
+                    "type": "kubernetes.io/basic-auth",
+                    "metadata": {"generateName": "registryconfig-auth-", "namespace": "fleet-default"},
+                    "data": {"username": b64(q["registry_username"]), "password": b64(q.get("registry_password", ""))}})
+                conf["authConfigSecretName"] = secret["metadata"]["name"]
+            rke["registries"] = {"mirrors": {"docker.io": {"endpoint": ["https://" + q["registry"]]}},
+                                 "configs": {q["registry"]: conf}}
+        call("POST", v2, {"apiVersion": "provisioning.cattle.io/v1", "kind": "Cluster",
+                          "metadata": {"name": q["name"], "namespace": "fleet-default"},
+                          "spec": {"kubernetesVersion": k8s_version(q["version"], True), "rkeConfig": rke}})
+    cluster_id, delay, deadline = "", 0.05, time.time() + 120
+    while not cluster_id and time.time() < deadline:
+        # the provisioning controller creates the management cluster (c-m-...) after the create
+        cluster_id = ((get_or_none(path) or {}).get("status") or {}).get("clusterName", "")
+        if not cluster_id:
+            time.sleep(delay)
+            delay = min(2.0, delay * 2)
+    return found, cluster_id
+
+
+def ensure_rke1():
+    found = v3
+    if found:
+        return found, found[0]["id"]
     rke = {"type": "rancherKubernetesEngineConfig", "kubernetesVersion": k8s_version(q["version"]),
            "ignoreDockerVersion": False, "sshAgentAuth": False,
            "authentication": {"type": "authnConfig", "strategy": "x509"},
@@ -47,8 +101,11 @@ else:
     if q.get("registry"):
         rke["privateRegistries"] = [{"url": q["registry"], "user": q.get("registry_username", ""),
                                      "password": q.get("registry_password", "")}]
-    cluster_id = call("POST", "/v3/cluster", {"type": "cluster", "name": q["name"],
-                                              "rancherKubernetesEngineConfig": rke}).get("id", "")
+    return found, call("POST", "/v3/cluster", {"type": "cluster", "name": q["name"],
+                                               "rancherKubernetesEngineConfig": rke}).get("id", "")
+
+
+found, cluster_id = ensure_rke2() if dist == "rke2" else ensure_rke1()
 if not cluster_id:
     sys.exit("Unable to create cluster!")
 tokens = call("GET", "/v3/clusters/%s/clusterregistrationtokens" % cluster_id).get("data") if found else []

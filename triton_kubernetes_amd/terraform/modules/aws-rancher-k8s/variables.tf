@@ -19,25 +19,36 @@ variable "rancher_secret_key" {
   sensitive   = true
 }
 
+variable "k8s_distribution" {
+  description = "rke2 (provisioning.cattle.io/v1 custom cluster, nodes join with rancher-system-agent) or rke1 (v3 cluster + rancher-agent; reference-era documents)"
+  type        = string
+  default     = "rke2"
+
+  validation {
+    condition     = contains(["rke2", "rke1"], var.k8s_distribution)
+    error_message = "k8s_distribution must be rke2 or rke1."
+  }
+}
+
 variable "k8s_version" {
   description = "RKE Kubernetes version."
   type        = string
-  default     = "v1.28.10-rancher1-1"
+  default     = "v1.31.6+rke2r1"
 
   validation {
-    condition     = contains(["v1.28", "v1.27", "v1.26"], join(".", slice(split(".", var.k8s_version), 0, 2)))
-    error_message = "k8s_version must be an RKE1 release of Rancher v2.8.5 (v1.28.10-rancher1-1, v1.27.14-rancher1-1, v1.26.15-rancher1-1)."
+    condition     = (contains(["v1.31", "v1.30", "v1.29"], join(".", slice(split(".", var.k8s_version), 0, 2))) && length(regexall("[+]rke2r[0-9]+$", var.k8s_version)) > 0) || (contains(["v1.31", "v1.30", "v1.29", "v1.28"], join(".", slice(split(".", var.k8s_version), 0, 2))) && length(regexall("-rancher[0-9]+-[0-9]+$", var.k8s_version)) > 0)
+    error_message = "k8s_version must be an RKE2 (v1.31.6+rke2r1, v1.30.10+rke2r1, v1.29.14+rke2r1) or RKE1 (v1.31.6-rancher1-1, v1.30.10-rancher1-1, v1.29.14-rancher1-1, v1.28.15-rancher1-1) release of Rancher v2.10.3."
   }
 }
 
 variable "k8s_network_provider" {
   description = "CNI plugin of the cluster."
   type        = string
-  default     = "flannel"
+  default     = "canal"
 
   validation {
-    condition     = contains(["calico", "flannel", "canal", "weave"], var.k8s_network_provider)
-    error_message = "k8s_network_provider must be one of calico, flannel, canal, weave."
+    condition     = contains(["canal", "calico", "cilium", "flannel", "weave"], var.k8s_network_provider)
+    error_message = "k8s_network_provider must be one of canal, calico, cilium, flannel (RKE2) or weave (RKE1)."
   }
 }
 

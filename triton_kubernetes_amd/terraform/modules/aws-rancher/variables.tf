@@ -41,13 +41,13 @@ variable "docker_install_sha256" {
 variable "rancher_server_image" {
   description = "The Rancher Server image to use."
   type        = string
-  default     = "rancher/rancher:v2.8.5"
+  default     = "rancher/rancher:v2.10.3"
 }
 
 variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
   type        = string
-  default     = "rancher/rancher-agent:v2.8.5"
+  default     = "rancher/rancher-agent:v2.10.3"
 }
 
 variable "rancher_registry" {

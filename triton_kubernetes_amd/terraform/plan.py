@@ -835,6 +835,7 @@ class _ModulePlan:
                 self.report.errors.append(f"{self.where(fn, a.pos)}: {a.name}: {exc}")
         for nb in body.blocks:
             if nb.type == "lifecycle":
+                self.eval_conditions(fn, nb, scope)
                 continue
             if nb.type == "dynamic" and nb.labels:
                 self.eval_dynamic(fn, nb, scope)
@@ -843,6 +844,29 @@ class _ModulePlan:
             self.eval_body(fn, nb.body, inner)
             if nb.type == "provisioner" and nb.labels == ["file"]:
                 self.check_upload(fn, nb, inner)
+
+    def eval_conditions(self, fn: str, lifecycle: Block, scope: _Scope) -> None:
+        """``precondition`` blocks: a known false condition is the plan error Terraform
+        reports ("Resource precondition failed") with the block's ``error_message``."""
+        for cb in lifecycle.body.blocks:
+            if cb.type != "precondition":
+                continue
+            cond = cb.body.attr("condition")
+            if cond is None:
+                continue
+            try:
+                ok = evaluate(cond.expr, scope)
+            except PlanError as exc:
+                self.report.errors.append(f"{self.where(fn, cond.pos)}: precondition: {exc}")
+                continue
+            if ok is UNKNOWN or _bool(ok):
+                continue
+            msg_attr = cb.body.attr("error_message")
+            try:
+                msg = _tf_str(evaluate(msg_attr.expr, scope)) if msg_attr is not None else "condition false"
+            except PlanError:
+                msg = "condition false"
+            self.report.errors.append(f"{self.where(fn, cb.pos)}: precondition failed: {msg}")
 
     def check_upload(self, fn: str, blk: Block, scope: _Scope) -> None:
         """A ``file`` provisioner's ``source`` must exist where terraform runs."""

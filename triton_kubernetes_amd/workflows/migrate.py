@@ -16,7 +16,10 @@ backend block are compatible by design, so migration is a source rewrite plus a 
    required arguments (refused), failing validations (e.g. a Kubernetes release the
    pinned Rancher does not ship: reported as a warning, because the running cluster keeps
    its version until it is recreated);
-3. after confirmation the previous document is kept as the blob
+3. the reference only created RKE1 clusters (v3 cluster + ``rancher-agent``), so a
+   rewritten cluster or host block without ``k8s_distribution`` gets ``rke1`` -- the
+   module default is RKE2, and a running RKE1 cluster cannot take RKE2 nodes;
+4. after confirmation the previous document is kept as the blob
    ``main.tf.json.pre-migrate`` and the migrated one is persisted.
 
 Nothing is applied: the next ``create`` (or an explicit re-apply) runs the new modules.
@@ -54,6 +57,9 @@ def plan_migration(ctx: Context, doc: Dict[str, Any], drop_unknown: bool = False
             continue
         new = dict(block, source=target)
         mod_dir = local_module_dir(target) or info.local_dir
+        if "k8s_distribution" not in new and "k8s_distribution" in hcl.check_module(mod_dir).variables:
+            new["k8s_distribution"] = "rke1"
+            warnings.append(f"module.{key}: k8s_distribution set to rke1 (the reference's clusters are RKE1)")
         problems = hcl.check_inputs(mod_dir, new)
         for p in problems:
             if p.startswith("unsupported argument "):
