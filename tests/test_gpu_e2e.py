@@ -33,8 +33,9 @@ def test_real_gpu_bringup(tmp_path):
     try:
         new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
                                   host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
+        # the default distribution: an RKE2 custom cluster (nodes register as rancher-system-agent)
         ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="gpu",
-                            k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", gpu_addons=True,
+                            k8s_version="v1.31", k8s_network_provider="canal", gpu_addons=True,
                             wait=True, rccl_gate=True, nodes=[
                                 {"rancher_host_label": "control", "node_count": 1, "hostname": "cp", "ssh_user": "u",
                                  "bastion_host": "", "key_path": "k", "hosts": ["agent+" + cp_url]},
@@ -55,6 +56,8 @@ def test_real_gpu_bringup(tmp_path):
         hist = w.history[-1]
         burn = [s for s in hist["steps"] if s["name"] == "gpu_burnin"][0]
         assert burn["ok"] and burn["detail"]["0"]["ok"], burn
+        assert {n["agentKind"] for n in fake.state.nodes.values()} == {"system-agent"}
+        assert "fleet-default/gpu" in fake.state.v2_clusters
     finally:
         w.stop()
         cp.stop()
@@ -67,13 +70,15 @@ def _stub(bindir, name, body):
     p.chmod(0o755)
 
 
-@pytest.mark.parametrize("rccl_slim", ["off", "on"])
-def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim):
+@pytest.mark.parametrize("rccl_slim,dist", [("off", "rke2"), ("on", "rke1")])
+def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist):
     """The SSH path's rendered bash bootstrap, run for real on the box: the native tools
     (gpu-burnin, amdgpu-topo-labeller incl. --rccl-env, rccl-ready) copied from ops/lib,
-    /etc relocated under tmp_path, and only sudo/docker/systemctl/hostnamectl/usermod/lsmod
-    stubbed (no root and no container runtime on the box).  ``rccl_slim=on``: the opt-in
-    step verifies the single-target copy on the GPU before installing rccl-ready-slim."""
+    /etc relocated under tmp_path, and only sudo/docker/curl/systemctl/hostnamectl/usermod/lsmod
+    stubbed (no root, no container runtime, no Rancher on the box; the stub curl serves an
+    installer that records its arguments).  ``rccl_slim=on``: the opt-in step verifies the
+    single-target copy on the GPU before installing rccl-ready-slim.  RKE2 joins through the
+    system-agent installer, RKE1 through docker run rancher-agent."""
     import os
     import shutil
     import subprocess
@@ -92,11 +97,13 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim):
     _stub(bindir, "sudo", 'exec "$@"')
     for name in ("docker", "systemctl", "hostnamectl", "usermod"):
         _stub(bindir, name, f'echo "{name} $*" >> {log}')
+    _stub(bindir, "curl", 'while [ $# -gt 0 ]; do [ "$1" = -o ] && out=$2; shift; done\n'
+                          f'printf \'#!/bin/sh\\necho "system-agent-install $*" >> {log}\\n\' > "$out"')
     _stub(bindir, "lsmod", "echo 'Module Size Used by'; test -c /dev/kfd && echo 'amdgpu 1 0'")
     etc = tmp_path / "etc"
     (etc / "docker").mkdir(parents=True)
     cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1, "gpu_burnin": "quick",
-           "rccl_env": {"NCCL_DEBUG": "WARN"}, "rccl_slim": rccl_slim}
+           "rccl_env": {"NCCL_DEBUG": "WARN"}, "rccl_slim": rccl_slim, "k8s_distribution": dist}
     plan = build_host_plan(cfg, "https://rancher.example", "regtok", "cafe", mi355x=True)
     script = (plan.render_shell().replace("/etc/", f"{etc}/").replace(TOOLS_DIR, str(tools))
               .replace("/var/lib/triton-kubernetes", str(tmp_path / "var")))
@@ -129,7 +136,12 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim):
     assert doc["ok"] and doc["rccl_mapped"], doc
     calls = log.read_text()
     assert "hostnamectl set-hostname gpu-1" in calls
-    assert "--ca-checksum cafe --worker" in calls and "--label amd.com/gpu.product-name=MI355X" in calls
+    if dist == "rke2":
+        assert "system-agent-install --server https://rancher.example" in calls and "docker" not in calls
+        assert "--ca-checksum cafe --node-name gpu-1 --worker" in calls
+    else:
+        assert "docker run" in calls and "--ca-checksum cafe --worker" in calls
+    assert "--label amd.com/gpu.product-name=MI355X" in calls
     print(json.dumps({"steps": steps, "rccl_env": rccl}))
 
 

@@ -88,7 +88,7 @@ def test_local_transport_runs_plan_with_stub_tools(tmp_path, dist):
     log = tmp_path / "sudo.log"
     _fake_bin(bindir, "sudo", f'echo "$*" >> {log}; cat >/dev/null 2>&1 || true')
     _fake_bin(bindir, "docker", "exit 0")
-    _fake_bin(bindir, "curl", f'echo "curl $*" >> {log}')
+    _fake_bin(bindir, "curl", f'echo "curl $*" >> {log}; while [ $# -gt 0 ]; do [ "$1" = -o ] && : > "$2"; shift; done')
     env = {"PATH": f"{bindir}:/usr/bin:/bin"}
     plan = build_host_plan(dict(WORKER, k8s_distribution=dist), "https://rancher.example", "regtok", "cafe",
                            mi355x=False)
@@ -100,9 +100,23 @@ def test_local_transport_runs_plan_with_stub_tools(tmp_path, dist):
     if dist == "rke1":
         assert "--server https://rancher.example --token regtok --ca-checksum cafe --worker" in calls
     else:
-        assert "curl -fsSLk -o /tmp/tk-system-agent-install.sh https://rancher.example/system-agent-install.sh" in calls
-        assert ("sh /tmp/tk-system-agent-install.sh --server https://rancher.example --label cattle.io/os=linux "
+        assert "https://rancher.example/system-agent-install.sh" in calls
+        assert ("--server https://rancher.example --label cattle.io/os=linux "
                 "--token regtok --ca-checksum cafe --node-name gpu-1 --worker") in calls
+
+
+def test_a_failing_command_mid_step_fails_the_step(tmp_path):
+    """errexit holds inside every step body: a download that fails in the middle of the
+    join step fails it (the step is not judged by its last command)."""
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "calls.log"
+    _fake_bin(bindir, "sudo", f'echo "$*" >> {log}')
+    _fake_bin(bindir, "curl", "exit 6")  # could not resolve host
+    plan = build_host_plan(WORKER, "https://rancher.example", "t", "s")
+    res = LocalTransport(env={"PATH": f"{bindir}:/usr/bin:/bin"}).run_plan(HostRef("local"), plan)
+    assert not res["ok"] and "agent" in (res.get("error") or "")
+    assert "--server" not in log.read_text()  # the installer never ran
 
 
 def test_local_transport_reports_failed_step(tmp_path):

@@ -94,13 +94,14 @@ class BootstrapPlan:
             f"# triton-kubernetes node bootstrap: {self.hostname} ({self.role})",
             "set -euo pipefail",
             "_tk_now() { date +%s%3N; }",
-            # step bodies run inside _tk_step (bash scoping is dynamic): its locals carry a
-            # prefix no step body uses, so a body assigning e.g. `n=` cannot rename the step
-            "_tk_step() { local _tk_name=$1; shift; local _tk_t0; _tk_t0=$(_tk_now);",
+            # each step body runs in a subshell with errexit in force: a failing command
+            # anywhere in the body fails the step (a function called as an `if` condition
+            # would run with errexit ignored), and an `exit` in a body ends only its step
+            "_tk_step() { local _tk_name=$1; shift; local _tk_t0 _tk_rc; _tk_t0=$(_tk_now);",
             "  echo \"::tk-step $_tk_name start 0\";",
-            "  if \"$@\"; then echo \"::tk-step $_tk_name ok $(( $(_tk_now) - _tk_t0 ))\";",
-            "  else local _tk_rc=$?; echo \"::tk-step $_tk_name failed $(( $(_tk_now) - _tk_t0 ))\" >&2;",
-            "    exit $_tk_rc; fi; }",
+            "  set +e; ( set -e; \"$@\" ); _tk_rc=$?; set -e",
+            "  if [ $_tk_rc -eq 0 ]; then echo \"::tk-step $_tk_name ok $(( $(_tk_now) - _tk_t0 ))\";",
+            "  else echo \"::tk-step $_tk_name failed $(( $(_tk_now) - _tk_t0 ))\" >&2; exit $_tk_rc; fi; }",
         ]
         for s in self.steps:
             body = s.shell.strip("\n")
@@ -279,10 +280,11 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
         # installer sets up rancher-system-agent, which then installs RKE2 for the role
         installer = rancher_url.rstrip("/") + SYSTEM_AGENT_INSTALL_PATH
         plan.steps.append(Step("agent", "agent", (
-            f"curl -fsSLk -o /tmp/tk-system-agent-install.sh {_q(installer)}\n"
-            f"sudo sh /tmp/tk-system-agent-install.sh --server {_q(rancher_url)} --label cattle.io/os=linux "
-            f"--token {_q(token)} --ca-checksum {_q(ca_checksum)} --node-name {_q(hostname)} --{role}{label_args}\n"
-            f"rm -f /tmp/tk-system-agent-install.sh"),
+            "_tk_installer=$(mktemp)\n"
+            "trap 'rm -f \"$_tk_installer\"' EXIT\n"
+            f"curl -fsSLk -o \"$_tk_installer\" {_q(installer)}\n"
+            f"sudo sh \"$_tk_installer\" --server {_q(rancher_url)} --label cattle.io/os=linux "
+            f"--token {_q(token)} --ca-checksum {_q(ca_checksum)} --node-name {_q(hostname)} --{role}{label_args}"),
             {"server": rancher_url, "role": role, "distribution": "rke2"}))
     return plan
 

@@ -225,11 +225,12 @@ print(json.dumps({"cluster_id": cluster_id, "registration_token": token,
 # How a node joins its cluster: RKE2 -> the server's rancher-system-agent installer (RKE2
 # brings its own containerd: no Docker); RKE1 -> docker run rancher/rancher-agent.
 JOIN_CLUSTER = r"""%{ if k8s_distribution == "rke2" ~}
-curl -fsSLk -o /tmp/tk-system-agent-install.sh '${rancher_api_url}/system-agent-install.sh'
-sudo sh /tmp/tk-system-agent-install.sh --server '${rancher_api_url}' --label 'cattle.io/os=linux' \
+installer=$(mktemp)
+curl -fsSLk -o "$installer" '${rancher_api_url}/system-agent-install.sh'
+sudo sh "$installer" --server '${rancher_api_url}' --label 'cattle.io/os=linux' \
   --token '${rancher_cluster_registration_token}' --ca-checksum '${rancher_cluster_ca_checksum}' \
   --node-name '${hostname}' --${rancher_node_role}${extra_agent_args}
-rm -f /tmp/tk-system-agent-install.sh
+rm -f "$installer"
 %{ else ~}
 sudo docker run -d --privileged --restart=unless-stopped --net=host \
   -v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run '${rancher_agent_image}' \
