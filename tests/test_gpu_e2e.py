@@ -145,38 +145,30 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist):
     print(json.dumps({"steps": steps, "rccl_env": rccl}))
 
 
-def _templatefile(text: str, values: dict) -> str:
-    """Terraform's templatefile(), as terraform/hcl.py evaluates it (strip markers included)."""
-    from triton_kubernetes_amd.terraform.hcl import templatefile
-
-    return templatefile(text, values)
-
-
 def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     """The bare-metal-mi355x-rancher-k8s-host module's host script (what Terraform's
-    remote-exec runs), rendered like templatefile() and run on the box: it builds the
-    native tools from the shipped sources with hipcc/g++ on the node, then labels, burn-in,
-    RCCL env and the agent command.  Paths relocated under tmp_path; sudo/docker/
-    hostnamectl/usermod/lsmod stubbed."""
+    remote-exec runs), rendered from the module's own templatefile() call for concrete
+    module inputs (terraform/plan.py) and run on the box: it builds the native tools from
+    the shipped sources with hipcc/g++ on the node, then burn-in, labels, RCCL env and the
+    RKE2 join.  Paths relocated under tmp_path; sudo/curl/docker/hostnamectl/usermod/lsmod
+    stubbed (the stub curl serves an installer that records its arguments)."""
     import os
     import subprocess
 
     from triton_kubernetes_amd.ops.build import CSRC
     from triton_kubernetes_amd.parallel.rccl_env import parse_env_file
     from triton_kubernetes_amd.terraform.generate import MODULES_DIR
+    from triton_kubernetes_amd.terraform.plan import plan_module
 
-    tpl = open(os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files",
-                            "install_mi355x_node.sh.tftpl"), encoding="utf-8").read()
-    values = {"gpu_count": 1, "gpu_burnin": "quick", "rccl_env_file": 'NCCL_DEBUG="INFO"', "rccl_min_busbw": 0,
-              "gpu_link_min_frac": 0.5, "rccl_slim": "off",
-              "docker_engine_install_url": "https://example.invalid/docker.sh", "docker_install_sha256": "",
-              "hostname": "gpu-tf-1",
-              "rancher_registry_username": "", "rancher_registry_password": "", "rancher_registry": "",
-              "rancher_agent_image": "rancher/rancher-agent:v2.8.5", "rancher_api_url": "https://rancher.example",
+    inputs = {"hostname": "gpu-tf-1", "host": "10.0.0.5", "rancher_api_url": "https://rancher.example",
               "rancher_cluster_registration_token": "regtok", "rancher_cluster_ca_checksum": "cafe",
-              "rancher_node_role": "worker"}
+              "rancher_host_labels": {"worker": "true"}, "gpu_count": "1", "gpu_burnin": "quick",
+              "rccl_env": {"NCCL_DEBUG": "INFO"}, "k8s_distribution": "rke2"}
+    planned = plan_module(os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host"), inputs, check_files=False)
+    assert planned.ok, planned.errors
+    (rendered,) = planned.rendered["install_mi355x_node.sh.tftpl"]
     tools, etc = tmp_path / "tools", tmp_path / "etc"
-    script = (_templatefile(tpl, values).replace("/opt/triton-kubernetes/bin", str(tools))
+    script = (rendered.replace("/opt/triton-kubernetes/bin", str(tools))
               .replace("/opt/triton-kubernetes/src", CSRC).replace("/etc/", f"{etc}/")
               .replace("/var/lib/triton-kubernetes", str(tmp_path / "var")))
     bindir = tmp_path / "bin"
@@ -185,6 +177,8 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     _stub(bindir, "sudo", 'exec "$@"')
     for name in ("docker", "hostnamectl", "usermod"):
         _stub(bindir, name, f'echo "{name} $*" >> {log}')
+    _stub(bindir, "curl", 'while [ $# -gt 0 ]; do [ "$1" = -o ] && out=$2; shift; done\n'
+                          f'printf \'#!/bin/sh\\necho "system-agent-install $*" >> {log}\\n\' > "$out"')
     _stub(bindir, "lsmod", "echo 'Module Size Used by'; test -c /dev/kfd && echo 'amdgpu 1 0'")
     env = dict(os.environ, PATH=f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
     proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=280)
@@ -206,20 +200,24 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     assert "amd.com/gpu.product-name=MI355X" in labels
     assert parse_env_file((etc / "rccl/rccl.env").read_text())["NCCL_DEBUG"] == "INFO"
     calls = log.read_text()
-    assert "hostnamectl set-hostname gpu-tf-1" in calls
-    assert "--token regtok --ca-checksum cafe --worker --label amd.com/" in calls
+    assert "hostnamectl set-hostname gpu-tf-1" in calls and "docker" not in calls  # RKE2: no Docker
+    assert "system-agent-install --server https://rancher.example --label cattle.io/os=linux" in calls
+    assert "--token regtok --ca-checksum cafe --node-name gpu-tf-1 --worker --label amd.com/" in calls
     # the burn-in's coverage travels with the node
     assert "--label amd.com/gpu.burnin-level=quick" in calls and "--label amd.com/gpu.burnin=passed" in calls
     assert "--label amd.com/gpu.burnin-hbm-tested-gib=1" in calls
 
 
-def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch):
+@pytest.mark.parametrize("dist", ["rke2", "rke1"])
+def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch, dist):
     """The production node agent mode (``exec``) over HTTP on the box: GPU steps run in
     process (arena burn-in, sysfs labels, discovered RCCL env), runtime/agent steps run
-    their fixed argv against stubbed docker/hostnamectl (no container runtime on the box)."""
+    their fixed argv against stubbed docker/hostnamectl (no container runtime on the box).
+    RKE2: the agent fetches the (fake) server's system-agent-install.sh and runs it."""
     from triton_kubernetes_amd.node.agent import NodeAgent
     from triton_kubernetes_amd.node.plan import build_host_plan
     from triton_kubernetes_amd.parallel.transport import AgentTransport, HostRef
+    from triton_kubernetes_amd.rancher.fake import FakeRancher
 
     bindir = tmp_path / "bin"
     bindir.mkdir()
@@ -229,20 +227,30 @@ def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch):
     import os
 
     monkeypatch.setenv("PATH", f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
+    monkeypatch.setenv("TK_FAKE_SYSTEM_AGENT_LOG", str(log))  # what the fake's installer appends to
+    fake = FakeRancher().start()
     agent = NodeAgent(name="w-exec", mode="exec", devices=[0], token="exec-token-123456", root=str(tmp_path / "root"))
     url = agent.serve()
     try:
         cfg = {"hostname": "gpu-exec-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
-               "gpu_burnin": "quick", "rccl_env": {"NCCL_DEBUG": "WARN"}}
-        plan = build_host_plan(cfg, "https://rancher.example", "regtok123", "cafe0123", mi355x=True)
+               "gpu_burnin": "quick", "rccl_env": {"NCCL_DEBUG": "WARN"}, "k8s_distribution": dist}
+        server = fake.url if dist == "rke2" else "https://rancher.example"  # loopback: the default allow-list
+        plan = build_host_plan(cfg, server, "regtok123", "cafe0123", mi355x=True)
         res = AgentTransport(token="exec-token-123456").run_plan(HostRef("agent+" + url), plan)
     finally:
         agent.stop()
+        fake.stop()
     assert res["ok"], res
     names = [s["name"] for s in res["steps"]]
     assert names == plan.step_names() and all(s["ok"] for s in res["steps"])
     calls = log.read_text()
-    assert "hostnamectl set-hostname gpu-exec-1" in calls and "docker version" in calls
-    assert "--ca-checksum cafe0123 --worker --label amd.com/" in calls and "--label amd.com/gpu.count=1" in calls
+    assert "hostnamectl set-hostname gpu-exec-1" in calls
+    if dist == "rke2":
+        assert "docker" not in calls
+        assert f"system-agent-install --server {fake.url} --label cattle.io/os=linux" in calls
+        assert "--ca-checksum cafe0123 --node-name gpu-exec-1 --worker --label amd.com/" in calls
+    else:
+        assert "docker version" in calls and "--ca-checksum cafe0123 --worker --label amd.com/" in calls
+    assert "--label amd.com/gpu.count=1" in calls
     assert (tmp_path / "root/etc/rccl/rccl.env").read_text().count("NCCL_DEBUG") == 1
     print(json.dumps({s["name"]: round(s["ms"], 2) for s in res["steps"]}))

@@ -231,3 +231,33 @@ def test_direct_executor_refuses_a_name_of_the_other_distribution(env):
     with pytest.raises(Exception, match="already exists as an RKE1 cluster"):
         new_cluster(ctx, backend)
     assert fake.state.v2_clusters == {}
+
+
+def test_exec_mode_agent_runs_the_servers_installer(tmp_path, monkeypatch):
+    """``exec`` mode (the production agent): the RKE2 join downloads the allowed server's
+    system-agent-install.sh and runs it with a fixed argv (no shell text from the plan)."""
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.parallel.transport import AgentTransport, HostRef
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "calls.log"
+    stub = bindir / "hostnamectl"
+    stub.write_text(f'#!/bin/sh\necho "hostnamectl $*" >> {log}\n')
+    stub.chmod(0o755)
+    monkeypatch.setenv("PATH", f"{bindir}:/usr/bin:/bin")
+    monkeypatch.setenv("TK_FAKE_SYSTEM_AGENT_LOG", str(log))
+    with FakeRancher() as fake:
+        agent = NodeAgent(name="x", mode="exec", token=TOKEN, root=str(tmp_path / "root"))
+        url = agent.serve()
+        try:
+            plan = build_host_plan({"hostname": "w-1", "rancher_host_labels": {"worker": "true"}}, fake.url,
+                                   "regtok", "cafe")
+            res = AgentTransport(token=TOKEN).run_plan(HostRef("agent+" + url), plan)
+        finally:
+            agent.stop()
+    assert res["ok"], res
+    calls = log.read_text()
+    assert "hostnamectl set-hostname w-1" in calls
+    assert (f"system-agent-install --server {fake.url} --label cattle.io/os=linux --token regtok "
+            "--ca-checksum cafe --node-name w-1 --worker") in calls
