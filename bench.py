@@ -37,7 +37,10 @@ distribution of the pinned Rancher v2.10.3, versions.py).  Simulated
 provisioning is instantaneous (``rke_provisioning``); the host steps (``runtime_install``:
 firewall, hostname) are sim-mode no-ops of the agents, and the node join
 (``agent_container``) fetches the server's ``system-agent-install.sh`` and registers as
-``rancher-system-agent`` through the fake's connect API instead of running the installer.  The reference publishes no number for this metric, so ``vs_baseline`` is null.
+``rancher-system-agent`` through the fake's connect API instead of running the installer.
+The device-plugin DaemonSet's pod is scheduled by the fake's kubelet model (image, kubelet
+socket and ``/sys`` mounts, node selector, taints) and registers instantly
+(``device_plugin_pod``).  The reference publishes no number for this metric, so ``vs_baseline`` is null.
 
 Rank 0 prints one JSON line (the driver's contract).
 """
@@ -55,7 +58,7 @@ HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
 METRIC = "cluster create→kubectl-ready wall-clock (s), bare-metal at 1/2/4/8 workers"
-SIMULATED_PHASES = ["rke_provisioning", "runtime_install", "agent_container"]
+SIMULATED_PHASES = ["rke_provisioning", "runtime_install", "agent_container", "device_plugin_pod"]
 
 
 def parse_args():
@@ -432,7 +435,9 @@ def main() -> int:
                            "rke_provisioning (in-process Rancher v2.10 fake, RKE2 custom cluster, instantaneous "
                            "provisioning), runtime_install (firewall/hostname no-ops) and agent_container (the node "
                            "fetches system-agent-install.sh and registers as rancher-system-agent via the fake's "
-                           "connect API instead of running it); real on MI355X: "
+                           "connect API instead of running it) and device_plugin_pod (the plugin DaemonSet is "
+                           "scheduled by the fake's kubelet model and registers the node's GPUs instantly); "
+                           "real on MI355X: "
                            f"native topology + RDMA labels, per-GPU HBM/MFMA/memtest burn-in level={args.burnin}, "
                            f"cluster RCCL all-reduce gate {'off' if args.no_rccl_gate else 'on'} "
                            f"(one communicator over all {n_gpus} GPUs)"

@@ -8,6 +8,7 @@ import time
 
 import pytest
 
+from triton_kubernetes_amd import versions
 from triton_kubernetes_amd.errors import TKError
 from triton_kubernetes_amd.k8s.manifests import addon_manifests, apply_manifests, gpu_job_manifest
 from triton_kubernetes_amd.rancher.client import RancherClient, ca_checksum, wait_until
@@ -176,6 +177,61 @@ def test_cluster_lifecycle_and_gpu_allocatable(rancher):
     client.delete_cluster(info.cluster_id)
     client.delete_cluster(info.cluster_id)  # 404 tolerated
     assert client.find_cluster("gpu") is None
+
+
+def test_device_plugin_model_gates_gpu_allocatable(rancher):
+    """amd.com/gpu is advertised only where a real device-plugin pod would run and register:
+    the right image, the kubelet socket and /sys mounted, a node the pod schedules on
+    (Ready, GPU label, taints tolerated), after the plugin's start-up time."""
+    import copy
+
+    from triton_kubernetes_amd.k8s.manifests import device_plugin_daemonset
+
+    fake, client, _ = rancher
+    fake.state.device_plugin_seconds = 0.3
+    info = client.ensure_cluster("dp")
+    gpu = {"amd.com/gpu.present": "true"}
+    _register(fake, info.registration_token, "cp", {"etcd": True, "controlplane": True})
+    _register(fake, info.registration_token, "g1", {"worker": True}, gpu, {"amd.com/gpu": 8})
+    _register(fake, info.registration_token, "g2", {"worker": True}, {}, {"amd.com/gpu": 8})  # not labelled
+    from triton_kubernetes_amd.cloud.http import HTTPClient
+
+    tainted = {"X-API-Tunnel-Token": info.registration_token, "X-Cattle-Agent-Kind": "system-agent",
+               "X-API-Tunnel-Params": tunnel_params("g3", {"worker": True}, gpu, {"amd.com/gpu": 8},
+                                                    [{"key": "dedicated", "value": "x", "effect": "NoSchedule"}])}
+    HTTPClient(base_url=fake.url).request("POST", "/v3/connect/register", headers=tainted, data=b"{}")
+    wait_until(lambda: client.cluster_state(info.cluster_id) == "active", 5, "active")
+    path = "/apis/apps/v1/namespaces/kube-system/daemonsets"
+
+    def gpus():
+        return {n["metadata"]["name"]: n["status"]["allocatable"].get("amd.com/gpu")
+                for n in client.k8s_nodes(info.cluster_id)}
+
+    good = device_plugin_daemonset(versions.DEVICE_PLUGIN_IMAGE)
+    for bad in (device_plugin_daemonset(versions.NODE_LABELLER_IMAGE),  # the labeller tag is no plugin
+                device_plugin_daemonset("busybox:1.36")):
+        bad["metadata"]["name"] = "not-a-plugin"
+        client.k8s(info.cluster_id, "POST", path, bad)
+        no_socket = copy.deepcopy(good)
+        no_socket["metadata"]["name"] = "no-socket"
+        no_socket["spec"]["template"]["spec"]["containers"][0]["volumeMounts"] = [{"name": "sys", "mountPath": "/sys"}]
+        client.k8s(info.cluster_id, "POST", path, no_socket)
+        time.sleep(0.35)
+        assert set(gpus().values()) == {None}
+        client.k8s(info.cluster_id, "DELETE", f"{path}/not-a-plugin")
+        client.k8s(info.cluster_id, "DELETE", f"{path}/no-socket")
+    client.k8s(info.cluster_id, "POST", path, good)
+    ds = client.k8s(info.cluster_id, "GET", f"{path}/{good['metadata']['name']}")
+    assert ds["status"]["desiredNumberScheduled"] == 1 and ds["status"]["numberReady"] == 0
+    assert gpus()["g1"] is None  # the plugin pod is still starting
+    wait_until(lambda: gpus()["g1"] == "8", 5, "plugin registered")
+    # only g1: g2 lacks the GPU label (nodeSelector), g3's taint is not tolerated, cp has no GPUs
+    assert gpus() == {"cp": None, "g1": "8", "g2": None, "g3": None}
+    ds = client.k8s(info.cluster_id, "GET", f"{path}/{good['metadata']['name']}")
+    assert ds["status"]["numberReady"] == 1
+    # the plugin going away takes the resource with it
+    client.k8s(info.cluster_id, "DELETE", f"{path}/{good['metadata']['name']}")
+    assert gpus()["g1"] is None
 
 
 def test_bad_registration_token_rejected(rancher):

@@ -29,9 +29,19 @@ real server does after agents register:
   least one etcd, one controlplane and one worker node; nodes then report the
   Kubernetes ``Ready`` condition;
 * ``/k8s/clusters/<id>/...`` proxy: ``api/v1/nodes`` (labels, conditions,
-  allocatable) and a generic object store for applied manifests.  GPU nodes
-  advertise ``amd.com/gpu`` allocatable only once a DaemonSet whose name
-  contains ``device-plugin`` has been applied — as with the real ROCm plugin;
+  allocatable) and a generic object store for applied manifests;
+* device plugins, as the kubelet sees them: ``amd.com/gpu`` appears in a node's
+  capacity/allocatable only when a device-plugin pod runs on it and registers.  A
+  DaemonSet counts as the AMD GPU plugin when a container runs a
+  ``rocm/k8s-device-plugin`` image (not the labeller tag) and mounts the host's
+  ``/var/lib/kubelet/device-plugins`` (the registration socket) and ``/sys`` (where it
+  enumerates the KFD devices).  Its pod lands on a node only if the node is Ready, its
+  labels satisfy the ``nodeSelector`` and required node affinity, and the pod
+  tolerates the node's taints; it registers ``device_plugin_seconds`` after both the
+  DaemonSet and the node exist.  The count it registers is the number of GPU devices
+  the node has (what its agent reported at registration: the KFD GPU nodes, i.e.
+  logical GPUs under a partition mode).  DaemonSet reads carry ``status``
+  (``desiredNumberScheduled``, ``numberReady``);
 * mutating admission: a Pod created through the proxy goes through every applied
   ``MutatingWebhookConfiguration`` whose rules and namespace selector match — the
   webhook is called over HTTPS, its certificate verified against the ``caBundle``
@@ -98,8 +108,10 @@ class _State:
         self.unsettled: Set[str] = set()  # clusters not yet active, or with a node not yet active
         self.objects: Dict[str, Dict[str, Any]] = {}  # "<cluster>|<path>|<name>" -> object
         self.cluster_objects: Dict[str, Dict[str, None]] = {}  # cluster id -> its object keys, in creation order
+        self.object_times: Dict[str, float] = {}  # object key -> when it was created
         self.rke_seconds = rke_seconds
         self.node_ready_seconds = node_ready_seconds
+        self.device_plugin_seconds = 0.0
         self.requests = 0
         self.log: List[Tuple[str, str]] = []
 
@@ -108,12 +120,14 @@ class FakeRancher:
     def __init__(self, rke_seconds: float = 0.0, node_ready_seconds: float = 0.0,
                  bootstrap_password: Optional[str] = None, host: str = "127.0.0.1", port: int = 0,
                  k8s_versions: Optional[Sequence[str]] = None, async_registration_tokens: bool = True,
-                 default_pod_security: str = "privileged", rke2_versions: Optional[Sequence[str]] = None):
+                 default_pod_security: str = "privileged", rke2_versions: Optional[Sequence[str]] = None,
+                 device_plugin_seconds: float = 0.0):
         # a server started without CATTLE_BOOTSTRAP_PASSWORD has a random one nobody knows
         pw = bootstrap_password if bootstrap_password is not None else secrets.token_hex(16)
         self.state = _State(rke_seconds, node_ready_seconds, pw,
                             list(k8s_versions) if k8s_versions is not None else [v for _, v in K8S_VERSIONS],
                             list(rke2_versions) if rke2_versions is not None else [v for _, v in RKE2_VERSIONS])
+        self.state.device_plugin_seconds = device_plugin_seconds
         # "<service>.<namespace>" -> "https://127.0.0.1:<port>" (where an in-cluster
         # webhook service of a test really listens)
         self.service_endpoints: Dict[str, str] = {}
@@ -196,28 +210,92 @@ class FakeRancher:
                     if settled:
                         st.unsettled.discard(cid)
 
+    # --- kubelet / DaemonSet model ------------------------------------------------------------
+    def _daemonsets(self, cid: str) -> List[Tuple[str, Dict[str, Any]]]:
+        """(key, object) of the cluster's DaemonSets (caller holds the lock)."""
+        st = self.state
+        return [(k, st.objects[k]) for k in st.cluster_objects.get(cid, ())
+                if k.split("|")[1].endswith("/daemonsets") and k in st.objects]
+
+    @staticmethod
+    def _node_labels(n: Dict[str, Any]) -> Dict[str, str]:
+        labels = dict(n["labels"])
+        labels.setdefault("kubernetes.io/hostname", n["hostname"])
+        for r, on in n["roles"].items():
+            if on:
+                labels[f"node-role.kubernetes.io/{r}"] = "true"
+        return labels
+
+    def _runs_on(self, ds: Dict[str, Any], n: Dict[str, Any]) -> bool:
+        """Would a pod of ``ds`` be scheduled on node ``n`` (Ready, selector, affinity, taints)?"""
+        if n["state"] != "active":
+            return False
+        pod = ((ds.get("spec") or {}).get("template") or {}).get("spec") or {}
+        labels = self._node_labels(n)
+        if any(labels.get(k) != v for k, v in (pod.get("nodeSelector") or {}).items()):
+            return False
+        terms = (((pod.get("affinity") or {}).get("nodeAffinity") or {})
+                 .get("requiredDuringSchedulingIgnoredDuringExecution") or {}).get("nodeSelectorTerms")
+        if terms and not any(_match_expressions(t.get("matchExpressions") or [], labels) for t in terms):
+            return False
+        tolerations = pod.get("tolerations") or []
+        return all(_tolerated(t, tolerations) for t in n.get("taints") or []
+                   if t.get("effect") in ("NoSchedule", "NoExecute"))
+
+    @staticmethod
+    def _is_gpu_plugin(ds: Dict[str, Any]) -> bool:
+        """A DaemonSet whose pod can register ``amd.com/gpu`` with the kubelet."""
+        pod = ((ds.get("spec") or {}).get("template") or {}).get("spec") or {}
+        host = {v.get("name"): (v.get("hostPath") or {}).get("path") for v in pod.get("volumes") or []
+                if "hostPath" in v}
+        for c in pod.get("containers") or []:
+            repo, _, tag = str(c.get("image", "")).rpartition(":")
+            if repo not in DEVICE_PLUGIN_REPOS or tag.startswith("labeller"):
+                continue
+            mounted = {m.get("mountPath"): host.get(m.get("name")) for m in c.get("volumeMounts") or []}
+            if (mounted.get(DEVICE_PLUGIN_SOCKET_DIR) == DEVICE_PLUGIN_SOCKET_DIR
+                    and mounted.get("/sys") == "/sys"):
+                return True
+        return False
+
+    def _plugin_ready_at(self, cid: str, ds_key: str, n: Dict[str, Any]) -> float:
+        created = self.state.object_times.get(ds_key, 0.0)
+        return max(created, n.get("ready_at") or 0.0) + self.state.device_plugin_seconds
+
+    def _gpu_allocatable(self, cid: str, n: Dict[str, Any], now: float) -> Optional[int]:
+        """GPUs a running, registered device-plugin pod advertises on ``n`` (None: none)."""
+        devices = int(n["capacity"].get("amd.com/gpu", 0) or 0)
+        for key, ds in self._daemonsets(cid):
+            if self._is_gpu_plugin(ds) and self._runs_on(ds, n) and now >= self._plugin_ready_at(cid, key, n):
+                return devices
+        return None
+
+    def _daemonset_status(self, cid: str, key: str, ds: Dict[str, Any]) -> Dict[str, Any]:
+        now = time.time()
+        nodes = [n for n in self.state.cluster_nodes.get(cid, {}).values() if self._runs_on(ds, n)]
+        ready = [n for n in nodes if now >= self._plugin_ready_at(cid, key, n)]
+        return {"desiredNumberScheduled": len(nodes), "currentNumberScheduled": len(nodes),
+                "numberReady": len(ready), "numberAvailable": len(ready)}
+
     def device_plugin_applied(self, cluster_id: str) -> bool:
         with self.state.mu:
-            return any("daemonsets" in k and "device-plugin" in k
-                       for k in self.state.cluster_objects.get(cluster_id, ()))
+            return any(self._is_gpu_plugin(ds) for _, ds in self._daemonsets(cluster_id))
 
     def k8s_nodes(self, cluster_id: str) -> List[Dict[str, Any]]:
         self._refresh()
         st = self.state
-        plugin = self.device_plugin_applied(cluster_id)
         items = []
+        now = time.time()
         with st.mu:
             for n in st.cluster_nodes.get(cluster_id, {}).values():
                 ready = n["state"] == "active"
-                labels = dict(n["labels"])
-                for r, on in n["roles"].items():
-                    if on:
-                        labels[f"node-role.kubernetes.io/{r}"] = "true"
                 alloc = {"cpu": "64", "memory": "1Ti", "pods": "110"}
-                if plugin and "amd.com/gpu" in n["capacity"]:
-                    alloc["amd.com/gpu"] = str(n["capacity"]["amd.com/gpu"])
+                gpus = self._gpu_allocatable(cluster_id, n, now)
+                if gpus is not None:
+                    alloc["amd.com/gpu"] = str(gpus)
                 items.append({
-                    "metadata": {"name": n["hostname"], "labels": labels},
+                    "metadata": {"name": n["hostname"], "labels": self._node_labels(n)},
+                    "spec": {"taints": list(n.get("taints") or [])},
                     "status": {"conditions": [{"type": "Ready", "status": "True" if ready else "False"}],
                                "allocatable": alloc, "capacity": dict(alloc)},
                 })
@@ -540,6 +618,7 @@ class FakeRancher:
             st.nodes[nid] = members[nid] = {
                 "id": nid, "clusterId": reg["clusterId"], "hostname": hostname, "nodeName": hostname, "agentKind": kind,
                 "roles": roles, "labels": dict(node.get("labels", {})), "capacity": dict(node.get("capacity", {})),
+                "taints": [dict(t) for t in node.get("taints") or [] if isinstance(t, dict)],
                 "state": "registering", "registered": time.time(), "ready_at": None}
             st.unsettled.add(reg["clusterId"])
             st.cond.notify_all()
@@ -587,6 +666,7 @@ class FakeRancher:
                              "creationTimestamp": time.strftime("%Y-%m-%dT%H:%M:%SZ", time.gmtime())})
                 obj.setdefault("status", {})
                 st.objects[key] = obj
+                st.object_times[key] = time.time()
                 st.cluster_objects.setdefault(cid, {})[key] = None
             return 201, obj
         if method in ("PUT", "GET", "DELETE"):
@@ -595,14 +675,18 @@ class FakeRancher:
             with st.mu:
                 if method == "PUT":
                     st.objects[key] = body
+                    st.object_times.setdefault(key, time.time())
                     st.cluster_objects.setdefault(cid, {})[key] = None
                     return 200, body
                 if method == "DELETE":
                     if key not in st.objects:
                         return 404, {"code": 404}
                     st.cluster_objects.get(cid, {}).pop(key, None)
+                    st.object_times.pop(key, None)
                     return 200, st.objects.pop(key)
                 if key in st.objects:
+                    if base.endswith("/daemonsets"):
+                        return 200, dict(st.objects[key], status=self._daemonset_status(cid, key, st.objects[key]))
                     return 200, st.objects[key]
                 prefix = f"{cid}|{kpath}|"
                 items = [st.objects[k] for k in st.cluster_objects.get(cid, ()) if k.startswith(prefix)]
@@ -612,6 +696,44 @@ class FakeRancher:
 
 class _Rejected(Exception):
     pass
+
+
+DEVICE_PLUGIN_REPOS = ("rocm/k8s-device-plugin", "docker.io/rocm/k8s-device-plugin")
+DEVICE_PLUGIN_SOCKET_DIR = "/var/lib/kubelet/device-plugins"
+
+
+def _match_expressions(exprs: List[Dict[str, Any]], labels: Dict[str, str]) -> bool:
+    """A nodeSelectorTerm's ``matchExpressions`` (all must hold)."""
+    for e in exprs:
+        key, op, values = e.get("key", ""), e.get("operator", ""), list(e.get("values") or [])
+        have = key in labels
+        if op == "In" and not (have and labels[key] in values):
+            return False
+        if op == "NotIn" and have and labels[key] in values:
+            return False
+        if op == "Exists" and not have:
+            return False
+        if op == "DoesNotExist" and have:
+            return False
+        if op in ("Gt", "Lt"):
+            try:
+                v, ref = int(labels.get(key, "")), int(values[0])
+            except (ValueError, IndexError):
+                return False
+            if (op == "Gt" and not v > ref) or (op == "Lt" and not v < ref):
+                return False
+    return True
+
+
+def _tolerated(taint: Dict[str, Any], tolerations: List[Dict[str, Any]]) -> bool:
+    for t in tolerations:
+        if t.get("effect") and t.get("effect") != taint.get("effect"):
+            continue
+        if t.get("operator") == "Exists" and (not t.get("key") or t.get("key") == taint.get("key")):
+            return True
+        if t.get("key") == taint.get("key") and t.get("value", "") == taint.get("value", ""):
+            return True
+    return False
 
 
 PSA_ENFORCE = "pod-security.kubernetes.io/enforce"
@@ -741,9 +863,11 @@ def _admit_pod(fake: "FakeRancher", cid: str, namespace: str, pod: Dict[str, Any
 
 
 def tunnel_params(hostname: str, roles: Dict[str, bool], labels: Dict[str, str],
-                  capacity: Dict[str, Any]) -> str:
-    """The ``X-API-Tunnel-Params`` header a node agent sends (base64 JSON)."""
+                  capacity: Dict[str, Any], taints: Optional[List[Dict[str, str]]] = None) -> str:
+    """The ``X-API-Tunnel-Params`` header a node agent sends (base64 JSON).  ``capacity``
+    carries the node's GPU devices (``amd.com/gpu``: what a device plugin on it would
+    enumerate), not what the kubelet advertises."""
     node = {"requestedHostname": hostname, "etcd": roles.get("etcd", False),
             "controlPlane": roles.get("controlplane", False), "worker": roles.get("worker", False),
-            "labels": labels, "capacity": capacity}
+            "labels": labels, "capacity": capacity, "taints": list(taints or [])}
     return base64.b64encode(json.dumps({"node": node}).encode()).decode()
