@@ -44,7 +44,7 @@ def test_bench_torchrun_gloo(nproc, workers):
     # one worker node owns all N GPUs unless --workers splits them
     cfg = doc["config"]
     assert cfg["workers"] == workers and cfg["gpus_per_worker"] * workers == nproc
-    assert cfg["simulated_phases"] == ["rke_provisioning", "runtime_install", "agent_container"]
+    assert cfg["simulated_phases"] == ["rke_provisioning", "runtime_install", "agent_container", "device_plugin_pod"]
     assert cfg["start"].startswith("cold")
     assert doc["data"].startswith("SIM-GPU DRY RUN")
     for phase in cfg["simulated_phases"]:
