@@ -64,6 +64,12 @@ def test_real_gpu_bringup(tmp_path):
         fake.stop()
 
 
+# a curl that serves an empty /cacerts (a publicly trusted server) and an installer that
+# records its arguments
+CURL_STUB = """while [ $# -gt 0 ]; do case $1 in -o) out=$2; shift;; http*) url=$1;; esac; shift; done
+case $url in */cacerts) : > "$out";; *) printf '#!/bin/sh\\necho "system-agent-install $*" >> {log}\\n' > "$out";; esac"""
+
+
 def _stub(bindir, name, body):
     p = bindir / name
     p.write_text("#!/bin/bash\n" + body + "\n")
@@ -97,8 +103,7 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist):
     _stub(bindir, "sudo", 'exec "$@"')
     for name in ("docker", "systemctl", "hostnamectl", "usermod"):
         _stub(bindir, name, f'echo "{name} $*" >> {log}')
-    _stub(bindir, "curl", 'while [ $# -gt 0 ]; do [ "$1" = -o ] && out=$2; shift; done\n'
-                          f'printf \'#!/bin/sh\\necho "system-agent-install $*" >> {log}\\n\' > "$out"')
+    _stub(bindir, "curl", CURL_STUB.format(log=log))
     _stub(bindir, "lsmod", "echo 'Module Size Used by'; test -c /dev/kfd && echo 'amdgpu 1 0'")
     etc = tmp_path / "etc"
     (etc / "docker").mkdir(parents=True)
@@ -177,8 +182,7 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     _stub(bindir, "sudo", 'exec "$@"')
     for name in ("docker", "hostnamectl", "usermod"):
         _stub(bindir, name, f'echo "{name} $*" >> {log}')
-    _stub(bindir, "curl", 'while [ $# -gt 0 ]; do [ "$1" = -o ] && out=$2; shift; done\n'
-                          f'printf \'#!/bin/sh\\necho "system-agent-install $*" >> {log}\\n\' > "$out"')
+    _stub(bindir, "curl", CURL_STUB.format(log=log))
     _stub(bindir, "lsmod", "echo 'Module Size Used by'; test -c /dev/kfd && echo 'amdgpu 1 0'")
     env = dict(os.environ, PATH=f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
     proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=280)

@@ -261,3 +261,70 @@ def test_exec_mode_agent_runs_the_servers_installer(tmp_path, monkeypatch):
     assert "hostnamectl set-hostname w-1" in calls
     assert (f"system-agent-install --server {fake.url} --label cattle.io/os=linux --token regtok "
             "--ca-checksum cafe --node-name w-1 --worker") in calls
+
+
+def _https_rancher(tmp_path, cacerts_body: bytes):
+    """A TLS server standing in for Rancher's installer endpoints, its certificate for
+    127.0.0.1 signed by a CA whose PEM ``/cacerts`` serves (or ``cacerts_body``)."""
+    import http.server
+    import ssl
+    import threading
+
+    from triton_kubernetes_amd.k8s.tls import issue, make_ca
+    from triton_kubernetes_amd.node.security import server_context
+
+    ca = make_ca("rancher-test-ca")
+    cert = issue(ca, "127.0.0.1", ["127.0.0.1"])
+    body = cacerts_body if cacerts_body is not None else ca.cert_pem.encode()
+
+    class H(http.server.BaseHTTPRequestHandler):
+        def log_message(self, *a):
+            pass
+
+        def do_GET(self):
+            data = body if self.path == "/cacerts" else b"#!/bin/sh\necho installed\n"
+            self.send_response(200)
+            self.send_header("Content-Length", str(len(data)))
+            self.end_headers()
+            self.wfile.write(data)
+
+    srv = http.server.ThreadingHTTPServer(("127.0.0.1", 0), H)
+    srv.socket = server_context(cert.cert_pem, cert.key_pem).wrap_socket(srv.socket, server_side=True)
+    threading.Thread(target=srv.serve_forever, daemon=True).start()
+    return srv, f"https://127.0.0.1:{srv.server_address[1]}", body
+
+
+@pytest.mark.parametrize("tamper", [False, True])
+def test_installer_fetched_over_tls_pinned_by_the_ca_checksum(tmp_path, tamper):
+    """The RKE2 join trusts the installer only over TLS verified against the CA whose
+    sha256 is the cluster's --ca-checksum (agent and shell paths alike)."""
+    import hashlib
+
+    from triton_kubernetes_amd.node.plan import BootstrapPlan, build_host_plan
+
+    srv, url, pem = _https_rancher(tmp_path, None)
+    try:
+        checksum = hashlib.sha256(pem).hexdigest() if not tamper else "0" * 64
+        agent = NodeAgent(name="x", mode="sim", token=TOKEN, root=str(tmp_path / "r"))
+        plan = BootstrapPlan("w-1", "worker", url, "tok", checksum, distribution="rke2")
+        if tamper:
+            with pytest.raises(RuntimeError, match="does not match the cluster's CA checksum"):
+                agent._fetch_installer(plan)
+        else:
+            assert agent._fetch_installer(plan).startswith(b"#!/bin/sh")
+        agent.stop()
+        # the rendered shell step: real curl against the TLS server, sudo stubbed
+        bindir = tmp_path / "bin"
+        bindir.mkdir()
+        log = tmp_path / "sudo.log"
+        (bindir / "sudo").write_text(f'#!/bin/sh\necho "$*" >> {log}\n')
+        (bindir / "sudo").chmod(0o755)
+        shell_plan = build_host_plan({"hostname": "w-1", "rancher_host_labels": {"worker": "true"}}, url, "tok",
+                                     checksum)
+        from triton_kubernetes_amd.parallel.transport import HostRef, LocalTransport
+
+        res = LocalTransport(env={"PATH": f"{bindir}:/usr/bin:/bin"}).run_plan(HostRef("local"), shell_plan)
+        ran = log.exists() and "--server" in log.read_text()
+        assert res["ok"] is (not tamper) and ran is (not tamper), res
+    finally:
+        srv.shutdown()

@@ -278,11 +278,20 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
     else:
         # the registration command Rancher shows for a custom RKE2 cluster: the server's
         # installer sets up rancher-system-agent, which then installs RKE2 for the role
-        installer = rancher_url.rstrip("/") + SYSTEM_AGENT_INSTALL_PATH
+        # installer over TLS verified against the server's CA, which must first match the
+        # cluster's CA checksum (an empty CA: a publicly trusted certificate)
+        base = rancher_url.rstrip("/")
         plan.steps.append(Step("agent", "agent", (
-            "_tk_installer=$(mktemp)\n"
-            "trap 'rm -f \"$_tk_installer\"' EXIT\n"
-            f"curl -fsSLk -o \"$_tk_installer\" {_q(installer)}\n"
+            "_tk_installer=$(mktemp); _tk_ca=$(mktemp)\n"
+            "trap 'rm -f \"$_tk_installer\" \"$_tk_ca\"' EXIT\n"
+            f"curl -fsSLk -o \"$_tk_ca\" {_q(base + '/cacerts')}\n"
+            "if [ -s \"$_tk_ca\" ]; then\n"
+            f"  [ \"$(sha256sum < \"$_tk_ca\" | cut -d' ' -f1)\" = {_q(ca_checksum)} ] || "
+            "{ echo 'the Rancher CA does not match the cluster CA checksum' >&2; exit 1; }\n"
+            f"  curl -fsSL --cacert \"$_tk_ca\" -o \"$_tk_installer\" {_q(base + SYSTEM_AGENT_INSTALL_PATH)}\n"
+            "else\n"
+            f"  curl -fsSL -o \"$_tk_installer\" {_q(base + SYSTEM_AGENT_INSTALL_PATH)}\n"
+            "fi\n"
             f"sudo sh \"$_tk_installer\" --server {_q(rancher_url)} --label cattle.io/os=linux "
             f"--token {_q(token)} --ca-checksum {_q(ca_checksum)} --node-name {_q(hostname)} --{role}{label_args}"),
             {"server": rancher_url, "role": role, "distribution": "rke2"}))

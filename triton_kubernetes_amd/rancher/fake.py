@@ -397,6 +397,9 @@ class FakeRancher:
             return self._register(h)
         if path == SYSTEM_AGENT_INSTALL_PATH and method == "GET":
             return 200, SYSTEM_AGENT_INSTALL_SCRIPT.encode()
+        if path == "/cacerts" and method == "GET":  # unauthenticated, what the installers pin
+            with st.mu:
+                return 200, (st.settings.get("cacerts", "") + "\n").encode()
         if not h._authed():
             return 401, {"type": "error", "code": "Unauthorized"}
         if path == "/v1-rke2-release/releases" and method == "GET":

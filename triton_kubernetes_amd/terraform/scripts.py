@@ -225,12 +225,20 @@ print(json.dumps({"cluster_id": cluster_id, "registration_token": token,
 # How a node joins its cluster: RKE2 -> the server's rancher-system-agent installer (RKE2
 # brings its own containerd: no Docker); RKE1 -> docker run rancher/rancher-agent.
 JOIN_CLUSTER = r"""%{ if k8s_distribution == "rke2" ~}
-installer=$(mktemp)
-curl -fsSLk -o "$installer" '${rancher_api_url}/system-agent-install.sh'
+# the installer over TLS verified against the server's CA, which must first match the
+# cluster's CA checksum (an empty CA: a publicly trusted certificate)
+installer=$(mktemp); ca=$(mktemp)
+curl -fsSLk -o "$ca" '${rancher_api_url}/cacerts'
+if [ -s "$ca" ]; then
+  [ "$(sha256sum < "$ca" | cut -d' ' -f1)" = '${rancher_cluster_ca_checksum}' ] || { echo 'the Rancher CA does not match the cluster CA checksum' >&2; exit 1; }
+  curl -fsSL --cacert "$ca" -o "$installer" '${rancher_api_url}/system-agent-install.sh'
+else
+  curl -fsSL -o "$installer" '${rancher_api_url}/system-agent-install.sh'
+fi
 sudo sh "$installer" --server '${rancher_api_url}' --label 'cattle.io/os=linux' \
   --token '${rancher_cluster_registration_token}' --ca-checksum '${rancher_cluster_ca_checksum}' \
   --node-name '${hostname}' --${rancher_node_role}${extra_agent_args}
-rm -f "$installer"
+rm -f "$installer" "$ca"
 %{ else ~}
 sudo docker run -d --privileged --restart=unless-stopped --net=host \
   -v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run '${rancher_agent_image}' \
