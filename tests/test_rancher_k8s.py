@@ -28,6 +28,24 @@ def rancher():
 def test_ca_checksum_matches_reference_shasum():
     # rancher_cluster.sh: echo "$cacerts" | shasum -a 256  -> trailing newline included
     assert ca_checksum("abc") == hashlib.sha256(b"abc\n").hexdigest()
+    # Rancher's CAChecksum: one trailing newline, never two; no CA -> no checksum
+    assert ca_checksum("abc\n") == ca_checksum("abc")
+    assert ca_checksum("") == ""
+
+
+def test_served_cacerts_hash_to_the_cluster_checksum():
+    """What a node downloads from /cacerts hashes to the checksum the cluster reports,
+    whether or not the stored bundle ends with a newline."""
+    import urllib.request
+
+    for pem in (FAKE_CACERTS, FAKE_CACERTS.rstrip("\n") + "\n"):
+        fake = FakeRancher().start()
+        try:
+            fake.state.settings["cacerts"] = pem
+            body = urllib.request.urlopen(fake.url + "/cacerts", timeout=10).read()
+            assert hashlib.sha256(body).hexdigest() == ca_checksum(pem)
+        finally:
+            fake.stop()
 
 
 def test_bootstrap_s3(rancher):

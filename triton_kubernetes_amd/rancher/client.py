@@ -48,7 +48,11 @@ class ClusterInfo:
 
 
 def ca_checksum(cacerts: str) -> str:
-    return hashlib.sha256((cacerts + "\n").encode()).hexdigest()
+    """Rancher's own rule (what ``/cacerts`` serves and the agents hash): the bundle with
+    one trailing newline; an empty CA (a publicly trusted certificate) has no checksum."""
+    if not cacerts:
+        return ""
+    return hashlib.sha256((cacerts if cacerts.endswith("\n") else cacerts + "\n").encode()).hexdigest()
 
 
 def wait_until(fn: Callable[[], Any], timeout: float, what: str, first: float = 0.02,

@@ -399,7 +399,8 @@ class FakeRancher:
             return 200, SYSTEM_AGENT_INSTALL_SCRIPT.encode()
         if path == "/cacerts" and method == "GET":  # unauthenticated, what the installers pin
             with st.mu:
-                return 200, (st.settings.get("cacerts", "") + "\n").encode()
+                ca = st.settings.get("cacerts", "")
+                return 200, (ca if not ca or ca.endswith("\n") else ca + "\n").encode()
         if not h._authed():
             return 401, {"type": "error", "code": "Unauthorized"}
         if path == "/v1-rke2-release/releases" and method == "GET":

@@ -217,8 +217,10 @@ if not token:
 if not token:
     sys.exit("Unable to create cluster registration token!")
 cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
+if cacerts and not cacerts.endswith("\n"):
+    cacerts += "\n"  # Rancher hashes the bundle with one trailing newline, as /cacerts serves it
 print(json.dumps({"cluster_id": cluster_id, "registration_token": token,
-                  "ca_checksum": hashlib.sha256((cacerts + "\n").encode()).hexdigest()}))
+                  "ca_checksum": hashlib.sha256(cacerts.encode()).hexdigest() if cacerts else ""}))
 '
 """
 
