@@ -263,6 +263,33 @@ def test_exec_mode_agent_runs_the_servers_installer(tmp_path, monkeypatch):
             "--ca-checksum cafe --node-name w-1 --worker") in calls
 
 
+def test_exec_join_without_a_ca_checksum(tmp_path, monkeypatch):
+    """A server with a publicly trusted certificate reports no CA and no checksum: the
+    agent joins without --ca-checksum instead of refusing the empty value."""
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.parallel.transport import AgentTransport, HostRef
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "calls.log"
+    (bindir / "hostnamectl").write_text(f'#!/bin/sh\necho "hostnamectl $*" >> {log}\n')
+    (bindir / "hostnamectl").chmod(0o755)
+    monkeypatch.setenv("PATH", f"{bindir}:/usr/bin:/bin")
+    monkeypatch.setenv("TK_FAKE_SYSTEM_AGENT_LOG", str(log))
+    with FakeRancher() as fake:
+        agent = NodeAgent(name="x", mode="exec", token=TOKEN, root=str(tmp_path / "root"))
+        url = agent.serve()
+        try:
+            plan = build_host_plan({"hostname": "w-1", "rancher_host_labels": {"worker": "true"}}, fake.url,
+                                   "regtok", "")
+            res = AgentTransport(token=TOKEN).run_plan(HostRef("agent+" + url), plan)
+        finally:
+            agent.stop()
+    assert res["ok"], res
+    calls = log.read_text()
+    assert "--token regtok --node-name w-1 --worker" in calls and "--ca-checksum" not in calls
+
+
 def _https_rancher(tmp_path, cacerts_body: bytes):
     """A TLS server standing in for Rancher's installer endpoints, its certificate for
     127.0.0.1 signed by a CA whose PEM ``/cacerts`` serves (or ``cacerts_body``)."""

@@ -77,6 +77,14 @@ _URL_RE = re.compile(r"^https?://[A-Za-z0-9._:\[\]-]+(/[A-Za-z0-9._/-]*)?$")
 _ROLES = ("worker", "etcd", "controlplane")
 
 
+def _ca_args(plan: BootstrapPlan) -> List[str]:
+    """``--ca-checksum`` for the agent; none when the server's certificate is publicly
+    trusted (Rancher reports no CA and no checksum then)."""
+    if not plan.ca_checksum:
+        return []
+    return ["--ca-checksum", _check(_TOKEN_RE, plan.ca_checksum, "ca checksum")]
+
+
 class StepFailed(RuntimeError):
     def __init__(self, step: str, message: str):
         super().__init__(f"step {step} failed: {message}")
@@ -251,8 +259,7 @@ class NodeAgent:
         argv = ["docker", "run", "-d", "--privileged", "--restart=unless-stopped", "--net=host",
                 "-v", "/etc/kubernetes:/etc/kubernetes", "-v", "/var/run:/var/run", image,
                 "--server", _check(_URL_RE, plan.rancher_url, "rancher url"),
-                "--token", _check(_TOKEN_RE, plan.token, "registration token"),
-                "--ca-checksum", _check(_TOKEN_RE, plan.ca_checksum, "ca checksum"), f"--{role}"]
+                "--token", _check(_TOKEN_RE, plan.token, "registration token"), *_ca_args(plan), f"--{role}"]
         for k in sorted(labels):
             argv += ["--label", f"{k}={labels[k]}"]
         return self._run_argv(argv)
@@ -285,7 +292,7 @@ class NodeAgent:
             argv = ["sh", path, "--server", _check(_URL_RE, plan.rancher_url, "rancher url"),
                     "--label", "cattle.io/os=linux",
                     "--token", _check(_TOKEN_RE, plan.token, "registration token"),
-                    "--ca-checksum", _check(_TOKEN_RE, plan.ca_checksum, "ca checksum"),
+                    *_ca_args(plan),
                     "--node-name", _check(_HOSTNAME_RE, plan.hostname, "hostname"), f"--{role}"]
             for k in sorted(labels):
                 argv += ["--label", f"{k}={labels[k]}"]
