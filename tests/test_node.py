@@ -34,10 +34,13 @@ def test_plan_steps_and_order():
     gpu = build_host_plan(dict(reg, k8s_distribution="rke1"), "https://r", "tok", "sum", mi355x=True)
     # burn-in precedes labels so the agent's topology prefetch overlaps it
     assert gpu.step_names() == ["firewall", "runtime", "hostname", "registry_login", "gpu_preflight",
-                                "gpu_burnin", "gpu_links", "gpu_labels", "rccl_env", "rccl_local", "agent"]
+                                "gpu_burnin", "gpu_links", "gpu_labels", "gpu_health", "rccl_env", "rccl_local", "agent"]
     gpu2 = build_host_plan(reg, "https://r", "tok", "sum", mi355x=True)
     assert gpu2.step_names() == ["firewall", "hostname", "gpu_preflight", "gpu_burnin", "gpu_links", "gpu_labels",
-                                 "rccl_env", "rccl_local", "agent"]
+                                 "gpu_health", "rccl_env", "rccl_local", "agent"]
+    # gpu_health = off: no RAS verdict step
+    off = build_host_plan(dict(reg, gpu_health="off"), "https://r", "tok", "sum", mi355x=True)
+    assert "gpu_health" not in off.step_names()
     assert gpu2.steps[-1].params == {"server": "https://r", "role": "worker", "distribution": "rke2"}
     with pytest.raises(ValueError):
         build_host_plan(dict(WORKER, k8s_distribution="k3s"), "https://r", "tok", "sum")

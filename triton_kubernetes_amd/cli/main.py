@@ -7,6 +7,7 @@
 
 Additions: ``wait cluster`` (the readiness waiter on an existing cluster),
 ``credentials node`` (a node agent's TLS certificate, token and image allow-list),
+``health cluster`` (GPU RAS health of the MI355X nodes; optional taint fencing),
 ``backup cluster`` / ``restore cluster`` (namespace backup to the state backend
 or S3 — advertised by the reference README, never implemented there),
 ``gpu …`` (the native MI355X probes), ``agent`` (the node agent) and
@@ -45,10 +46,11 @@ VALID = {
     "userdata": ["node"],
     "migrate": ["manager"],
     "credentials": ["node"],
+    "health": ["cluster"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
 _ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
-             "restore": "restore", "userdata": "userdata", "migrate": "migrate", "credentials": "credentials"}
+             "restore": "restore", "userdata": "userdata", "migrate": "migrate", "credentials": "credentials", "health": "health"}
 
 
 class ArgError(Exception):
@@ -94,7 +96,9 @@ def build_parser() -> argparse.ArgumentParser:
                        ("migrate", "Point a cluster manager's document (e.g. one written by the reference's "
                                    "Terraform 0.11 modules) at this framework's modules"),
                        ("credentials", "Issue a node agent's TLS certificate, token and image allow-list "
-                                       "(signed by the cluster manager's agent CA)")):
+                                       "(signed by the cluster manager's agent CA)"),
+                       ("health", "Re-read the GPU health (ECC, retired pages) of a cluster's MI355X nodes and, "
+                                  "with health_taint, fence unhealthy ones")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
@@ -196,6 +200,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         from ..workflows.credentials import node_credentials
 
         node_credentials(ctx, backend)
+    elif command == "health":
+        from ..workflows.health import cluster_health
+
+        cluster_health(ctx, backend)
     elif command == "wait":
         from ..readiness.waiter import wait_after_create
         from ..workflows.select import select_cluster, select_manager

@@ -186,6 +186,17 @@ def _mi355x_fields(ctx: Context) -> Dict:
         except ValueError as exc:
             raise ConfigError(f"gpu_link_min_gbps must be a non-negative number. Found '{floor}'.") from exc
         out["gpu_link_min_gbps"] = floor
+    # GPU health policy at bring-up (node/health.py): fail | taint | off, and its limits
+    from ..node.health import limits_of, policy_of
+
+    raw = {k: s.get_string(k) for k in ("gpu_health", "gpu_max_uncorrectable_ecc", "gpu_max_retired_pages")
+           if s.is_set(k)}
+    if raw:
+        policy = policy_of(raw)
+        max_ue, max_bad = limits_of(raw)
+        out["gpu_health"] = policy
+        out["gpu_max_uncorrectable_ecc"] = str(max_ue)
+        out["gpu_max_retired_pages"] = "auto" if max_bad < 0 else str(max_bad)
     if s.is_set("rccl_slim"):  # opt-in verified single-target RCCL (terraform/scripts.py)
         slim = s.get_string("rccl_slim").lower()
         if slim in ("true", "yes", "1"):

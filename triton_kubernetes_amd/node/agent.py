@@ -32,7 +32,7 @@ In both modes the MI355X steps call the native probes directly on the agent's
 GPUs: topology labeller (N1), HBM/MFMA/memtest burn-in, RCCL env file and the
 node-level RCCL sweep (N2).
 
-HTTP API (JSON): ``GET /v1/info``, ``POST /v1/plan``, ``POST /v1/rccl-uid``,
+HTTP API (JSON): ``GET /v1/info``, ``GET /v1/health`` (GPU RAS verdict, ``node/health.py``), ``POST /v1/plan``, ``POST /v1/rccl-uid``,
 ``POST /v1/rccl-prepare`` (without a ``uid``: host the rendezvous and return it; start this node's ranks of the cluster-wide RCCL
 communicator, non-blocking), ``POST /v1/rccl-gate`` (run them: verified
 all-reduce sweep), ``POST /v1/rccl-abort``, ``POST /v1/cleanup``, ``POST /v1/shutdown``
@@ -83,6 +83,17 @@ def _ca_args(plan: BootstrapPlan) -> List[str]:
     if not plan.ca_checksum:
         return []
     return ["--ca-checksum", _check(_TOKEN_RE, plan.ca_checksum, "ca checksum")]
+
+
+_TAINT_RE = re.compile(r"^[A-Za-z0-9./-]{1,253}=[A-Za-z0-9._-]{0,63}:(NoSchedule|PreferNoSchedule|NoExecute)$")
+
+
+def _taint_args(taints: Optional[List[Dict[str, str]]]) -> List[str]:
+    """``--taints key=value:Effect`` per taint (both Rancher agents take the flag)."""
+    out: List[str] = []
+    for t in taints or []:
+        out += ["--taints", _check(_TAINT_RE, f"{t['key']}={t.get('value', '')}:{t['effect']}", "taint")]
+    return out
 
 
 class StepFailed(RuntimeError):
@@ -195,7 +206,7 @@ class NodeAgent:
         if bad:
             raise PermissionError(bad[0])
         results: List[StepResult] = []
-        ctx: Dict[str, Any] = {"labels": {}, "capacity": {}}
+        ctx: Dict[str, Any] = {"labels": {}, "capacity": {}, "taints": []}
         t_plan = time.perf_counter()
         self._touch()
         error = None
@@ -216,7 +227,8 @@ class NodeAgent:
                     break
         doc = {"hostname": plan.hostname, "ok": error is None, "error": error,
                "ms": (time.perf_counter() - t_plan) * 1e3,
-               "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"]}
+               "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"],
+               "taints": ctx["taints"]}
         self.history.append(doc)
         self._touch()
         return doc
@@ -249,12 +261,13 @@ class NodeAgent:
             return self._run_argv(["docker", "login", "-u", user, "--password-stdin", reg], stdin=password)
         raise StepFailed(step.name, f"unknown runtime action {a!r}")
 
-    def _exec_agent(self, plan: BootstrapPlan, step: Step, labels: Dict[str, str]) -> Any:
+    def _exec_agent(self, plan: BootstrapPlan, step: Step, labels: Dict[str, str],
+                    taints: Optional[List[Dict[str, str]]] = None) -> Any:
         role = plan.role if plan.role in _ROLES else ""
         if not role:
             raise ValueError(f"invalid role {plan.role!r}")
         if step.params.get("distribution", plan.distribution) == "rke2":
-            return self._exec_system_agent(plan, role, labels)
+            return self._exec_system_agent(plan, role, labels, taints)
         image = _check(_IMAGE_RE, step.params.get("image", ""), "agent image")
         argv = ["docker", "run", "-d", "--privileged", "--restart=unless-stopped", "--net=host",
                 "-v", "/etc/kubernetes:/etc/kubernetes", "-v", "/var/run:/var/run", image,
@@ -262,7 +275,7 @@ class NodeAgent:
                 "--token", _check(_TOKEN_RE, plan.token, "registration token"), *_ca_args(plan), f"--{role}"]
         for k in sorted(labels):
             argv += ["--label", f"{k}={labels[k]}"]
-        return self._run_argv(argv)
+        return self._run_argv(argv + _taint_args(taints))
 
     def _fetch_installer(self, plan: BootstrapPlan) -> bytes:
         """The allowed server's ``system-agent-install.sh``, over TLS verified against the
@@ -283,7 +296,8 @@ class NodeAgent:
             raise RuntimeError(f"{url}{SYSTEM_AGENT_INSTALL_PATH} is not an installer script")
         return body
 
-    def _exec_system_agent(self, plan: BootstrapPlan, role: str, labels: Dict[str, str]) -> Any:
+    def _exec_system_agent(self, plan: BootstrapPlan, role: str, labels: Dict[str, str],
+                           taints: Optional[List[Dict[str, str]]] = None) -> Any:
         script = self._fetch_installer(plan)
         fd, path = tempfile.mkstemp(prefix="tk-system-agent-install-", suffix=".sh")
         try:
@@ -296,7 +310,7 @@ class NodeAgent:
                     "--node-name", _check(_HOSTNAME_RE, plan.hostname, "hostname"), f"--{role}"]
             for k in sorted(labels):
                 argv += ["--label", f"{k}={labels[k]}"]
-            return self._run_argv(argv)
+            return self._run_argv(argv + _taint_args(taints))
         finally:
             os.unlink(path)
 
@@ -353,6 +367,24 @@ class NodeAgent:
             # what the burn-in covered travels with the node (level, HBM held by the memtest)
             ctx["labels"].update(burnin_labels(level, results))
             return out
+        if a == "gpu_health":
+            # RAS verdict per physical GPU (node/health.py) on the topology the labels came
+            # from; an unhealthy node fails (policy fail) or joins tainted (policy taint)
+            from .health import HEALTH_TAINT, evaluate, health_labels
+
+            topo = ctx.get("topology")
+            if topo is None:
+                fut = ctx.get("topology_future")
+                topo = fut.result() if fut is not None else self._topology()
+            verdict = evaluate(topo, int(step.params.get("max_uncorrectable", 0)),
+                               int(step.params.get("max_bad_pages", -1)))
+            self.write_file("/etc/triton-kubernetes/gpu-health.json", json.dumps(verdict))
+            ctx["labels"].update(health_labels(verdict))
+            if verdict["status"] != "healthy":
+                if step.params.get("policy", "fail") != "taint":
+                    raise StepFailed(step.name, "unhealthy GPUs (gpu_health = fail): " + "; ".join(verdict["reasons"]))
+                ctx["taints"].append(dict(HEALTH_TAINT))
+            return verdict
         if a == "gpu_links":
             # every ordered GPU pair's peer read (a kernel on the receiver), disjoint pairs at
             # a time: a link below the node's median fraction or the absolute floor fails the
@@ -421,9 +453,17 @@ class NodeAgent:
             if plan.gpu is not None:
                 ctx["capacity"].setdefault("amd.com/gpu", len(self.devices))
             if self.mode == "exec":
-                return self._exec_agent(plan, step, ctx["labels"])
+                return self._exec_agent(plan, step, ctx["labels"], ctx["taints"])
             return self._register(plan, ctx)
         raise StepFailed(step.name, f"unknown action {a!r}")
+
+    def health(self, max_uncorrectable: int = 0, max_bad_pages: int = -1) -> Dict[str, Any]:
+        """This node's GPU health verdict now (``GET /v1/health``; node/health.py)."""
+        from .health import evaluate
+
+        verdict = evaluate(self._topology(), max_uncorrectable, max_bad_pages)
+        verdict["node"] = self.name
+        return verdict
 
     def _gpu_preflight(self, expected: int) -> Dict[str, Any]:
         if self.topology_override is not None:
@@ -489,7 +529,8 @@ class NodeAgent:
                  "worker": plan.role == "worker"}
         http = HTTPClient(base_url=plan.rancher_url, verify_tls=False)
         hdrs = {"X-API-Tunnel-Token": plan.token,
-                "X-API-Tunnel-Params": tunnel_params(plan.hostname, roles, ctx["labels"], ctx["capacity"])}
+                "X-API-Tunnel-Params": tunnel_params(plan.hostname, roles, ctx["labels"], ctx["capacity"],
+                                                     ctx.get("taints"))}
         if plan.distribution == "rke2":
             self._fetch_installer(plan)  # what a real node runs first
             hdrs["X-Cattle-Agent-Kind"] = "system-agent"
@@ -771,6 +812,13 @@ class NodeAgent:
                         pending = len(agent._gates)
                     return self._reply(200, {"name": agent.name, "mode": agent.mode, "devices": agent.devices,
                                              "labels": agent.last_labels, "pending_gates": pending})
+                if urllib.parse.urlsplit(self.path).path == "/v1/health":
+                    try:
+                        q = urllib.parse.parse_qs(urllib.parse.urlsplit(self.path).query)
+                        return self._reply(200, agent.health(int(q.get("max_uncorrectable", ["0"])[0]),
+                                                             int(q.get("max_bad_pages", ["-1"])[0])))
+                    except Exception as exc:  # noqa: BLE001
+                        return self._reply(500, {"error": f"{type(exc).__name__}: {exc}"})
                 return self._reply(404, {"error": "not found"})
 
             def do_POST(self):

@@ -20,6 +20,9 @@ plus xGMI keys used for topology-aware scheduling:
 ``amd.com/xgmi.links-per-gpu``         min xGMI peers over GPUs
 ``amd.com/xgmi.fully-connected``       every GPU has an xGMI link to every other; only
                                        claimed in SPX (node/partition.py)
+``amd.com/gpu.ecc-uncorrectable``      uncorrectable ECC errors, summed over physical GPUs
+``amd.com/gpu.bad-pages``              retired VRAM pages (driver bad-page records), summed
+``amd.com/gpu.health``                 ``healthy`` / ``unhealthy`` (node/health.py policy)
 =====================================  =============================================
 
 Pods that need all 8 GPUs on one xGMI hive use node affinity on
@@ -124,8 +127,13 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     whole = cmodes <= {"spx"} and physical == len(gpus)
     labels["amd.com/xgmi.fully-connected"] = "true" if whole and len(gpus) > 1 and \
         min(xgmi_peers) == len(gpus) - 1 else "false"
-    ecc = [int(g.get("ecc_uncorrectable", 0)) for g in gpus]
-    labels["amd.com/gpu.ecc-uncorrectable"] = str(sum(ecc))
+    # RAS counters per physical GPU (its partitions report the same device's counters)
+    from .health import physical_gpus
+
+    phys = physical_gpus(doc)
+    labels["amd.com/gpu.ecc-uncorrectable"] = str(sum(p["ecc_uncorrectable"] for p in phys))
+    if any(p["bad_pages"] >= 0 for p in phys):
+        labels["amd.com/gpu.bad-pages"] = str(sum(max(0, p["bad_pages"]) for p in phys))
     return labels
 
 

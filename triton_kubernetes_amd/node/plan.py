@@ -23,13 +23,17 @@ Step catalogue (``action`` ids):
 ``gpu_preflight``   MI355X: amdgpu loaded, ``/dev/kfd`` + ``/dev/dri`` present, N GPUs
 ``gpu_labels``      MI355X: N1 topology labeller -> node labels file
 ``gpu_burnin``      MI355X: HBM / MFMA / memtest probes per GPU
+``gpu_health``      MI355X: RAS verdict (uncorrectable ECC, retired VRAM pages) under the
+                    cluster's ``gpu_health`` policy: fail the node, or join it tainted
+                    ``amd.com/gpu-health=unhealthy:NoSchedule`` (``node/health.py``)
 ``rccl_env``        MI355X: write ``/etc/rccl/rccl.env``
 ``rccl_local``      MI355X: node-level RCCL all-reduce sweep over the local GPUs (N2)
 ``agent``           join: RKE2 -> the server's ``system-agent-install.sh`` (installs
                     ``rancher-system-agent``) with ``--server/--token/--ca-checksum/
                     --node-name/--<role>``; RKE1 -> ``docker run rancher/rancher-agent``
                     with ``--server/--token/--ca-checksum/--<role>``; both with
-                    ``--label`` flags (GPU labels on MI355X nodes)
+                    ``--label`` flags (GPU labels on MI355X nodes) and ``--taints``
+                    (an unhealthy GPU node under the ``taint`` policy)
 ==================  ==============================================================
 """
 
@@ -50,6 +54,8 @@ from .manager import docker_install_lines
 LABEL_FILE = "/etc/triton-kubernetes/gpu-labels"
 BURNIN_LABEL_FILE = "/etc/triton-kubernetes/gpu-burnin-labels"
 TOPOLOGY_FILE = "/etc/triton-kubernetes/gpu-topology.json"
+HEALTH_FILE = "/etc/triton-kubernetes/gpu-health.json"
+TAINT_FILE = "/etc/triton-kubernetes/gpu-taints"  # key=value:Effect lines the join passes as --taints
 RCCL_ENV_FILE = "/etc/rccl/rccl.env"
 TOOLS_DIR = "/opt/triton-kubernetes/bin"
 
@@ -217,7 +223,7 @@ for f in /sys/class/drm/renderD*/device/current_compute_partition /sys/class/drm
   esac
 done
 sudo usermod -aG video,render "$(id -un)" || true
-sudo rm -f {BURNIN_LABEL_FILE}""", {"count": ngpu, "compute_partition": cpart, "memory_partition": mpart},
+sudo rm -f {BURNIN_LABEL_FILE} {TAINT_FILE}""", {"count": ngpu, "compute_partition": cpart, "memory_partition": mpart},
                                gpu=True))
         # burn-in before labels: the agent discovers the topology concurrently
         # with the burn-in kernels and only joins it at the labels step
@@ -241,6 +247,26 @@ cat /tmp/tk-link-labels | sudo tee -a {BURNIN_LABEL_FILE} >/dev/null""", {"min_f
 sudo mkdir -p "$(dirname {LABEL_FILE})"
 {TOOLS_DIR}/amdgpu-topo-labeller | sudo tee {TOPOLOGY_FILE} >/dev/null
 {TOOLS_DIR}/amdgpu-topo-labeller --labels | sudo tee {LABEL_FILE} >/dev/null""", gpu=True))
+        from .health import limits_of, policy_of, taint_flag
+
+        policy = policy_of(cfg)
+        if policy != "off":
+            # RAS verdict per physical GPU (node/health.py): exit 3 = a GPU is unhealthy
+            max_ue, max_bad = limits_of(cfg)
+            bad_arg = "auto" if max_bad < 0 else str(max_bad)
+            args = f"--health --max-uncorrectable {max_ue} --max-bad-pages {bad_arg}"
+            on_bad = (f"echo {_q(taint_flag())} | sudo tee {TAINT_FILE} >/dev/null" if policy == "taint" else
+                      "echo 'unhealthy GPUs (gpu_health = fail):' >&2; cat /tmp/tk-gpu-health.json >&2; exit 1")
+            plan.steps.append(Step("gpu_health", "gpu_health", f"""
+local rc=0
+{TOOLS_DIR}/amdgpu-topo-labeller {args} > /tmp/tk-gpu-health.json || rc=$?
+sudo install -m 0644 /tmp/tk-gpu-health.json {HEALTH_FILE}
+{{ {TOOLS_DIR}/amdgpu-topo-labeller {args} --labels || true; }} | sudo tee -a {BURNIN_LABEL_FILE} >/dev/null
+case $rc in
+  0) ;;
+  3) {on_bad} ;;
+  *) echo "GPU health check failed (exit $rc)" >&2; exit 1 ;;
+esac""", {"policy": policy, "max_uncorrectable": max_ue, "max_bad_pages": max_bad}, gpu=True))
         # discovered inter-node settings (active RDMA ports) first; the configured
         # values follow, so an explicit rccl_env key wins when the file is sourced
         plan.steps.append(Step("rccl_env", "rccl_env", f"""
@@ -268,7 +294,8 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
                                    {"count": ngpu, "min_busbw": float(cfg.get("rccl_min_busbw", 0) or 0)},
                                    gpu=True))
         label_args = (f' $(cat {LABEL_FILE} $([ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}) '
-                      f'| sed "s/^/--label /" | tr "\\n" " ")')
+                      f'| sed "s/^/--label /" | tr "\\n" " ")'
+                      f'$([ -r {TAINT_FILE} ] && sed "s/^/ --taints /" {TAINT_FILE} | tr -d "\\n")')
     if rke1:
         plan.steps.append(Step("agent", "agent", (
             f"sudo docker run -d --privileged --restart=unless-stopped --net=host "

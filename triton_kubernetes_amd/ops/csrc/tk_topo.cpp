@@ -81,6 +81,9 @@ struct GpuInfo {
   uint64_t hive_id = 0, xgmi_node_id = 0;
   uint32_t xgmi_lanes = 0;
   uint64_t ecc_correctable = 0, ecc_uncorrectable = 0;
+  // retired VRAM pages (the driver's bad-page records; -1: not reported), of which pending
+  // (marked bad, reserved at the next reset)
+  int64_t bad_pages = -1, bad_pages_pending = -1;
   std::vector<Link> links;
 };
 
@@ -208,6 +211,18 @@ Topology collect_amdsmi() {
       g.has_ecc = true;
       g.ecc_correctable = ec.correctable_count;
       g.ecc_uncorrectable = ec.uncorrectable_count;
+    }
+    uint32_t nbad = 0;
+    if (amdsmi_get_gpu_bad_page_info(h, &nbad, nullptr) == AMDSMI_STATUS_SUCCESS) {
+      g.bad_pages = nbad;
+      g.bad_pages_pending = 0;
+      if (nbad) {
+        std::vector<amdsmi_retired_page_record_t> rec(nbad);
+        uint32_t got = nbad;
+        if (amdsmi_get_gpu_bad_page_info(h, &got, rec.data()) == AMDSMI_STATUS_SUCCESS)
+          for (uint32_t k = 0; k < std::min(got, nbad); ++k)
+            g.bad_pages_pending += rec[k].status == AMDSMI_MEM_PAGE_STATUS_PENDING;
+      }
     }
     for (size_t j = 0; j < hs.size(); ++j) {
       if (j == i) continue;
@@ -396,6 +411,22 @@ Topology collect_sysfs(const std::string& root) {
         g.ecc_correctable += ce;
       }
       closedir(ras);
+      // the driver's bad-page records, one "0x<page> : 0x<size> : R|P|F" line each
+      // (R reserved, P pending until the next reset, F could not be reserved)
+      FILE* f = fopen((dev + "/ras/gpu_vram_bad_pages").c_str(), "r");
+      if (f) {
+        g.bad_pages = g.bad_pages_pending = 0;
+        char line[256];
+        while (fgets(line, sizeof(line), f)) {
+          const char* c = strrchr(line, ':');
+          if (!c || !strstr(line, "0x")) continue;
+          while (*++c == ' ') {
+          }
+          ++g.bad_pages;
+          g.bad_pages_pending += *c == 'P';
+        }
+        fclose(f);
+      }
     }
     // links to other GPU nodes (io_links: direct; p2p_links: indirect peers)
     std::set<size_t> seen;
@@ -505,6 +536,8 @@ std::string render_json(const Topology& t) {
     if (g.has_ecc)
       appendf(o, ",\"ecc_correctable\":%" PRIu64 ",\"ecc_uncorrectable\":%" PRIu64, g.ecc_correctable,
               g.ecc_uncorrectable);
+    if (g.bad_pages >= 0)
+      appendf(o, ",\"bad_pages\":%" PRId64 ",\"bad_pages_pending\":%" PRId64, g.bad_pages, g.bad_pages_pending);
     o += ",\"links\":[";
     for (size_t k = 0; k < g.links.size(); ++k) {
       const Link& l = g.links[k];
@@ -525,6 +558,96 @@ std::string render_json(const Topology& t) {
     o += "}";
   }
   o += "]}";
+  return o;
+}
+
+// --- GPU health ------------------------------------------------------------
+// Same rules as triton_kubernetes_amd/node/health.py:evaluate (tests compare the two on
+// fixture trees).  Judged per physical GPU -- its compute partitions share the PCI function
+// and report the same device's RAS counters, so the max over partitions counts once: a GPU
+// is unhealthy when its uncorrectable ECC errors exceed max_ue, or its retired VRAM pages
+// exceed max_bad (< 0: the amdgpu driver's default bad-page threshold, one page per 100 MiB
+// of VRAM rounded up, RAS_BAD_PAGE_COVER in amdgpu_ras.c).
+struct PhysGpu {
+  std::string bdf;
+  bool has_ecc = false;
+  uint64_t ue = 0, ce = 0, vram_mb = 0;
+  int64_t bad = -1, pending = -1;
+};
+
+std::vector<PhysGpu> physical_gpus(const Topology& t) {
+  std::vector<PhysGpu> out;
+  std::map<std::string, size_t> at;
+  for (size_t i = 0; i < t.gpus.size(); ++i) {
+    const GpuInfo& g = t.gpus[i];
+    const std::string key = g.bdf.empty() ? "#" + std::to_string(i) : g.bdf;
+    auto it = at.find(key);
+    if (it == at.end()) {
+      it = at.emplace(key, out.size()).first;
+      out.emplace_back();
+      out.back().bdf = g.bdf;
+    }
+    PhysGpu& p = out[it->second];
+    p.has_ecc = p.has_ecc || g.has_ecc;
+    p.ue = std::max(p.ue, g.ecc_uncorrectable);
+    p.ce = std::max(p.ce, g.ecc_correctable);
+    p.vram_mb = std::max(p.vram_mb, g.vram_mb);
+    p.bad = std::max(p.bad, g.bad_pages);
+    p.pending = std::max(p.pending, g.bad_pages_pending);
+  }
+  return out;
+}
+
+int64_t bad_page_limit(const PhysGpu& p, int64_t max_bad) {
+  if (max_bad >= 0) return max_bad;
+  return p.vram_mb ? static_cast<int64_t>((p.vram_mb + 99) / 100) : -1;  // -1: no limit known
+}
+
+std::string render_health(const Topology& t, int64_t max_ue, int64_t max_bad, bool labels) {
+  std::vector<std::string> reasons;
+  std::string gpus;
+  size_t bad_gpus = 0;
+  const auto phys = physical_gpus(t);
+  for (size_t i = 0; i < phys.size(); ++i) {
+    const PhysGpu& p = phys[i];
+    const int64_t limit = bad_page_limit(p, max_bad);
+    const std::string who = "GPU " + std::to_string(i) + (p.bdf.empty() ? "" : " (" + p.bdf + ")");
+    bool ok = true;
+    char b[256];
+    if (p.has_ecc && static_cast<int64_t>(p.ue) > max_ue) {
+      snprintf(b, sizeof(b), "%s: %" PRIu64 " uncorrectable ECC errors (max %" PRId64 ")", who.c_str(), p.ue, max_ue);
+      reasons.push_back(b);
+      ok = false;
+    }
+    if (p.bad >= 0 && limit >= 0 && p.bad > limit) {
+      snprintf(b, sizeof(b), "%s: %" PRId64 " retired VRAM pages (max %" PRId64 ")", who.c_str(), p.bad, limit);
+      reasons.push_back(b);
+      ok = false;
+    }
+    bad_gpus += !ok;
+    appendf(gpus, "%s{\"gpu\":%zu,\"bdf\":\"%s\",\"ok\":%s", i ? "," : "", i, esc(p.bdf).c_str(),
+            ok ? "true" : "false");
+    if (p.has_ecc)
+      appendf(gpus, ",\"ecc_uncorrectable\":%" PRIu64 ",\"ecc_correctable\":%" PRIu64, p.ue, p.ce);
+    if (p.bad >= 0)
+      appendf(gpus, ",\"bad_pages\":%" PRId64 ",\"bad_pages_pending\":%" PRId64, p.bad, p.pending);
+    if (limit >= 0) appendf(gpus, ",\"bad_page_limit\":%" PRId64, limit);
+    gpus += "}";
+  }
+  const bool healthy = reasons.empty();
+  if (labels) {
+    std::string o = std::string("amd.com/gpu.health=") + (healthy ? "healthy" : "unhealthy") + "\n";
+    o += "amd.com/gpu.unhealthy-count=" + std::to_string(bad_gpus) + "\n";
+    return o;
+  }
+  std::string o;
+  appendf(o, "{\"status\":\"%s\",\"max_uncorrectable\":%" PRId64 ",\"max_bad_pages\":", healthy ? "healthy" : "unhealthy",
+          max_ue);
+  if (max_bad >= 0) appendf(o, "%" PRId64, max_bad);
+  else o += "\"auto\"";
+  appendf(o, ",\"unhealthy_gpus\":%zu,\"reasons\":[", bad_gpus);
+  for (size_t i = 0; i < reasons.size(); ++i) appendf(o, "%s\"%s\"", i ? "," : "", esc(reasons[i]).c_str());
+  o += "],\"gpus\":[" + gpus + "]}";
   return o;
 }
 
@@ -589,7 +712,6 @@ std::string render_labels(const Topology& t) {
     int64_t min_cu = INT64_MAX;
     uint64_t min_vram = UINT64_MAX;
     size_t min_xgmi = SIZE_MAX;
-    uint64_t ecc = 0;
     for (const auto& g : gs) {
       if (!g.market_name.empty() || product_from_device_id(g.device_id)) names.insert(product_name(g));
       if (!g.device_id.empty() && g.device_id != "0x0") dev_ids.insert(g.device_id);
@@ -603,7 +725,6 @@ std::string render_labels(const Topology& t) {
       for (const auto& l : g.links)
         if (l.type == "XGMI") peers.insert(l.peer);
       min_xgmi = std::min(min_xgmi, peers.size());
-      ecc += g.ecc_uncorrectable;
     }
     if (names.size() == 1) {
       const std::string n = *names.begin();
@@ -622,7 +743,16 @@ std::string render_labels(const Topology& t) {
     // a compute partition is not a whole GPU with its own xGMI links: SPX only
     const bool whole = (cparts.empty() || (cparts.size() == 1 && *cparts.begin() == "spx")) && physical == gs.size();
     L["amd.com/xgmi.fully-connected"] = (whole && gs.size() > 1 && min_xgmi == gs.size() - 1) ? "true" : "false";
+    // RAS counters per physical GPU (its partitions report the same device's counters)
+    uint64_t ecc = 0;
+    int64_t bad = 0;
+    bool bad_known = false;
+    for (const auto& p : physical_gpus(t)) {
+      ecc += p.ue;
+      if (p.bad >= 0) bad += p.bad, bad_known = true;
+    }
     L["amd.com/gpu.ecc-uncorrectable"] = std::to_string(ecc);
+    if (bad_known) L["amd.com/gpu.bad-pages"] = std::to_string(bad);
   }
   // inter-node fabric: active RDMA ports
   size_t active = 0;
@@ -711,16 +841,28 @@ extern "C" int tkt_rccl_env_src(const char* root, char* buf, size_t len) {
   return copy_out(render_rccl_env(t), buf, len);
 }
 
+// Same contract; the payload is the health verdict JSON (labels: the health label set).
+extern "C" int tkt_health_src(const char* source, const char* root, long long max_ue, long long max_bad, int labels,
+                              char* buf, size_t len) {
+  const Topology t = collect(source, root);
+  const int rc = copy_out(t.status == 0 ? render_health(t, max_ue, max_bad, labels != 0) : std::string(), buf, len);
+  return rc < 0 ? rc : t.status;
+}
+
 extern "C" int tkt_topology_json(char* buf, size_t len) { return tkt_topology_json_src("amdsmi", "", buf, len); }
 
 extern "C" int tkt_topology_labels(char* buf, size_t len) { return tkt_topology_labels_src("amdsmi", "", buf, len); }
 
 #ifdef TK_TOPO_MAIN
-// amdgpu-topo-labeller [--labels|--rccl-env] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
+// amdgpu-topo-labeller [--labels|--rccl-env|--health] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
+//                      [--max-uncorrectable N] [--max-bad-pages N|auto]
 //   default: topology JSON on stdout; --labels: one `amd.com/...=value` per line;
-//   --rccl-env: the inter-node RCCL settings for the node's active RDMA ports
+//   --rccl-env: the inter-node RCCL settings for the node's active RDMA ports;
+//   --health: the GPU health verdict (JSON; with --labels the health labels), exit 3 when
+//   a GPU is unhealthy
 int main(int argc, char** argv) {
-  bool labels = false, rccl_env = false;
+  bool labels = false, rccl_env = false, health = false;
+  long long max_ue = 0, max_bad = -1;
   const char* source = "auto";
   const char* root = "";
   for (int i = 1; i < argc; ++i) {
@@ -728,12 +870,22 @@ int main(int argc, char** argv) {
       labels = true;
     } else if (strcmp(argv[i], "--rccl-env") == 0) {
       rccl_env = true;
+    } else if (strcmp(argv[i], "--health") == 0) {
+      health = true;
+    } else if (strcmp(argv[i], "--max-uncorrectable") == 0 && i + 1 < argc) {
+      max_ue = atoll(argv[++i]);
+    } else if (strcmp(argv[i], "--max-bad-pages") == 0 && i + 1 < argc) {
+      ++i;
+      max_bad = strcmp(argv[i], "auto") == 0 ? -1 : atoll(argv[i]);
     } else if (strcmp(argv[i], "--source") == 0 && i + 1 < argc) {
       source = argv[++i];
     } else if (strcmp(argv[i], "--sysfs-root") == 0 && i + 1 < argc) {
       root = argv[++i];
     } else {
-      fprintf(stderr, "usage: %s [--labels|--rccl-env] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]\n", argv[0]);
+      fprintf(stderr,
+              "usage: %s [--labels|--rccl-env|--health] [--source auto|amdsmi|sysfs] [--sysfs-root DIR] "
+              "[--max-uncorrectable N] [--max-bad-pages N|auto]\n",
+              argv[0]);
       return 64;
     }
   }
@@ -748,6 +900,15 @@ int main(int argc, char** argv) {
     return 0;
   }
   const Topology t = collect(source, root);
+  if (health) {
+    if (t.status != 0) {
+      fprintf(stderr, "amdgpu-topo-labeller: %s\n", t.error.c_str());
+      return 2;
+    }
+    const std::string verdict = render_health(t, max_ue, max_bad, false);
+    fputs(labels ? render_health(t, max_ue, max_bad, true).c_str() : (verdict + "\n").c_str(), stdout);
+    return verdict.find("\"status\":\"healthy\"") != std::string::npos ? 0 : 3;
+  }
   if (labels) {
     if (t.status != 0) {
       fprintf(stderr, "amdgpu-topo-labeller: %s\n", t.error.c_str());

@@ -105,6 +105,26 @@ def native_labels(source: str = "sysfs", sysfs_root: str = "") -> Dict[str, str]
     return dict(ln.split("=", 1) for ln in text.splitlines() if "=" in ln)
 
 
+def native_health(source: str = "sysfs", sysfs_root: str = "", max_uncorrectable: int = 0,
+                  max_bad_pages: int = -1) -> Dict[str, Any]:
+    """The labeller's GPU health verdict (``amdgpu-topo-labeller --health``), in-process."""
+    lib = load("libtk_topo.so")
+    fn = lib.tkt_health_src
+    fn.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_int,
+                   ctypes.c_char_p, ctypes.c_size_t]
+    fn.restype = ctypes.c_int
+    size = 1 << 16
+    while True:
+        buf = ctypes.create_string_buffer(size)
+        rc = fn(source.encode(), sysfs_root.encode(), max_uncorrectable, max_bad_pages, 0, buf, size)
+        if rc < 0:
+            size = -rc + 1
+            continue
+        if rc != 0:
+            raise NativeUnavailable(f"native labeller ({source}) failed with status {rc}")
+        return json.loads(buf.value.decode())
+
+
 def _read_props(path: str) -> Dict[str, int]:
     props: Dict[str, int] = {}
     try:

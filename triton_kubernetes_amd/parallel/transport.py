@@ -223,6 +223,9 @@ class AgentTransport(Transport):
     def post(self, host: HostRef, path: str, body: Dict[str, Any]) -> Dict[str, Any]:
         return self._client(host).post_json(path, body)
 
+    def get(self, host: HostRef, path: str, params: Optional[Dict[str, Any]] = None) -> Dict[str, Any]:
+        return self._client(host).request("GET", path, params=params).json()
+
     def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
         raise ExecutorError("the node agent does not execute shell scripts; use an agent plan or the ssh transport")
 

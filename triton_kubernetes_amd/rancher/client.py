@@ -23,6 +23,7 @@ reference's fixed ``sleep 5``.
 
 import base64
 import hashlib
+import json
 import time
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional
@@ -339,6 +340,14 @@ class RancherClient:
 
     def k8s_nodes(self, cluster_id: str) -> List[Dict[str, Any]]:
         return (self.k8s(cluster_id, "GET", "/api/v1/nodes") or {}).get("items", [])
+
+    def patch_node(self, cluster_id: str, name: str, patch: Dict[str, Any]) -> Dict[str, Any]:
+        """JSON merge patch (RFC 7386) of a Kubernetes Node: ``metadata.labels`` merge (null
+        removes a key), ``spec.taints`` is replaced whole."""
+        resp = self.http.request("PATCH", f"/k8s/clusters/{cluster_id}/api/v1/nodes/{name}",
+                                 data=json.dumps(patch).encode(),
+                                 headers={"Content-Type": "application/merge-patch+json"}, ok=(200,))
+        return resp.json()
 
     def kubeconfig(self, cluster_id: str) -> str:
         data = self.http.post_json(f"/v3/clusters/{cluster_id}?action=generateKubeconfig", {})

@@ -226,8 +226,10 @@ class FakeRancher:
                 labels[f"node-role.kubernetes.io/{r}"] = "true"
         return labels
 
-    def _runs_on(self, ds: Dict[str, Any], n: Dict[str, Any]) -> bool:
-        """Would a pod of ``ds`` be scheduled on node ``n`` (Ready, selector, affinity, taints)?"""
+    def _runs_on(self, ds: Dict[str, Any], n: Dict[str, Any], ds_key: str = "") -> bool:
+        """Does a pod of ``ds`` run on node ``n`` (Ready, selector, affinity, taints)?  As in
+        Kubernetes, a ``NoSchedule`` taint added after the pod was scheduled does not evict
+        it (only ``NoExecute`` does); one present at scheduling time keeps it off."""
         if n["state"] != "active":
             return False
         pod = ((ds.get("spec") or {}).get("template") or {}).get("spec") or {}
@@ -239,8 +241,11 @@ class FakeRancher:
         if terms and not any(_match_expressions(t.get("matchExpressions") or [], labels) for t in terms):
             return False
         tolerations = pod.get("tolerations") or []
+        scheduled = max(self.state.object_times.get(ds_key, 0.0), n.get("ready_at") or 0.0)
+        added = n.get("taint_added") or {}
         return all(_tolerated(t, tolerations) for t in n.get("taints") or []
-                   if t.get("effect") in ("NoSchedule", "NoExecute"))
+                   if t.get("effect") == "NoExecute"
+                   or (t.get("effect") == "NoSchedule" and added.get(t.get("key"), 0.0) <= scheduled))
 
     @staticmethod
     def _is_gpu_plugin(ds: Dict[str, Any]) -> bool:
@@ -266,13 +271,13 @@ class FakeRancher:
         """GPUs a running, registered device-plugin pod advertises on ``n`` (None: none)."""
         devices = int(n["capacity"].get("amd.com/gpu", 0) or 0)
         for key, ds in self._daemonsets(cid):
-            if self._is_gpu_plugin(ds) and self._runs_on(ds, n) and now >= self._plugin_ready_at(cid, key, n):
+            if self._is_gpu_plugin(ds) and self._runs_on(ds, n, key) and now >= self._plugin_ready_at(cid, key, n):
                 return devices
         return None
 
     def _daemonset_status(self, cid: str, key: str, ds: Dict[str, Any]) -> Dict[str, Any]:
         now = time.time()
-        nodes = [n for n in self.state.cluster_nodes.get(cid, {}).values() if self._runs_on(ds, n)]
+        nodes = [n for n in self.state.cluster_nodes.get(cid, {}).values() if self._runs_on(ds, n, key)]
         ready = [n for n in nodes if now >= self._plugin_ready_at(cid, key, n)]
         return {"desiredNumberScheduled": len(nodes), "currentNumberScheduled": len(nodes),
                 "numberReady": len(ready), "numberAvailable": len(ready)}
@@ -360,6 +365,9 @@ class FakeRancher:
             def do_DELETE(self):
                 self._dispatch("DELETE")
 
+            def do_PATCH(self):
+                self._dispatch("PATCH")
+
             def do_HEAD(self):
                 self._dispatch("HEAD")
 
@@ -370,7 +378,7 @@ class FakeRancher:
                 with st.mu:
                     st.requests += 1
                     st.log.append((method, self.path))
-                body = self._body() if method in ("POST", "PUT") else {}
+                body = self._body() if method in ("POST", "PUT", "PATCH") else {}
                 try:
                     code, obj = fake._route(method, path, query, body, self)
                 except Exception as exc:  # pragma: no cover - surfaced to the client
@@ -639,6 +647,8 @@ class FakeRancher:
         kpath = "/" + kpath
         if kpath == "/api/v1/nodes" and method == "GET":
             return 200, {"kind": "NodeList", "items": self.k8s_nodes(cid)}
+        if kpath.startswith("/api/v1/nodes/") and method == "PATCH":
+            return self._patch_node(cid, kpath[len("/api/v1/nodes/"):], body)
         if kpath == "/version":
             with st.mu:
                 v = (st.clusters[cid].get("version") or {}).get("gitVersion") or DEFAULT_K8S_VERSION
@@ -696,6 +706,34 @@ class FakeRancher:
                 items = [st.objects[k] for k in st.cluster_objects.get(cid, ()) if k.startswith(prefix)]
                 return 200, {"items": items}
         return 404, {"kind": "Status", "code": 404}
+
+
+    def _patch_node(self, cid: str, name: str, patch: Any) -> Tuple[int, Any]:
+        """JSON merge patch of a Node: labels merge (null deletes), ``spec.taints`` replaced."""
+        st = self.state
+        if not isinstance(patch, dict):
+            return 400, {"kind": "Status", "code": 400, "message": "merge patch must be an object"}
+        now = time.time()
+        with st.mu:
+            node = next((n for n in st.cluster_nodes.get(cid, {}).values() if n["hostname"] == name), None)
+            if node is None:
+                return 404, {"kind": "Status", "reason": "NotFound", "code": 404}
+            for k, v in ((patch.get("metadata") or {}).get("labels") or {}).items():
+                if v is None:
+                    node["labels"].pop(k, None)
+                else:
+                    node["labels"][k] = str(v)
+            spec = patch.get("spec") or {}
+            if "taints" in spec:
+                taints = [dict(t) for t in spec["taints"] or [] if isinstance(t, dict)]
+                added = node.setdefault("taint_added", {})
+                for t in taints:
+                    added.setdefault(t.get("key"), now)
+                for k in [k for k in added if k not in {t.get("key") for t in taints}]:
+                    del added[k]
+                node["taints"] = taints
+        items = {i["metadata"]["name"]: i for i in self.k8s_nodes(cid)}
+        return 200, items[name]
 
 
 class _Rejected(Exception):

@@ -70,6 +70,7 @@ class ClusterGate:
     def from_state(cls, state, cluster_key: str, transport: Any, sizes: Sequence[int],
                    iters: int = 5) -> Optional["ClusterGate"]:
         """Gate over the cluster's MI355X host modules; None unless every one is an agent host."""
+        from ..node.partition import logical_gpus
         from ..terraform.catalog import module_from_source
 
         urls: List[str] = []
@@ -83,7 +84,7 @@ class ClusterGate:
             if not addr.startswith("agent+"):
                 return None  # SSH-managed GPU node: no agent to hold a communicator
             urls.append(addr)
-            ndevs.append(int(cfg.get("gpu_count", 8) or 8))
+            ndevs.append(logical_gpus(cfg))  # RCCL ranks: GPUs x compute partitions
         if not urls:
             return None
         return cls(transport, members_from(urls, ndevs), sizes, iters)

@@ -7,7 +7,10 @@ Phases, each time-stamped (the BASELINE.json metric is ``ready - start``):
 2. ``nodes_ready``      every expected node is in the Kubernetes node list with
                         condition ``Ready=True`` (read through Rancher's k8s proxy);
 3. ``gpus_allocatable`` every MI355X node advertises ``amd.com/gpu`` equal to its
-                        expected count (device plugin up);
+                        expected count (device plugin up).  A node that joined with the
+                        GPU health taint (``gpu_health: taint``, ``node/health.py``) is
+                        left out of this check and of the gate, and listed in the
+                        report's ``gpu_unhealthy``;
 4. ``rccl_gate``        optional: one RCCL all-reduce sweep across every GPU of
                         the GPU nodes (N2) as one communicator -- run by the node
                         agents (``gate.py``; its init may already have been started,
@@ -44,6 +47,9 @@ class ReadinessSpec:
     rccl_process_hosts: List[Any] = field(default_factory=list)
     rccl_process_ndev: List[int] = field(default_factory=list)
     rccl_skip_reason: str = ""
+    # hostnames of rccl_hosts / rccl_process_hosts (same order): health-tainted ones leave the gate
+    rccl_names: List[str] = field(default_factory=list)
+    rccl_process_names: List[str] = field(default_factory=list)
 
 
 @dataclass
@@ -52,6 +58,7 @@ class ReadinessReport:
     phases: Dict[str, float] = field(default_factory=dict)
     nodes: Dict[str, Dict[str, Any]] = field(default_factory=dict)
     rccl: Optional[Dict[str, Any]] = None
+    gpu_unhealthy: List[str] = field(default_factory=list)  # GPU nodes that joined health-tainted
 
     @property
     def ready_seconds(self) -> float:
@@ -97,16 +104,29 @@ def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float
         items = wait_until(nodes_ready, left(), f"{len(want)} nodes Ready")
     rep.phases["nodes_ready"] = time.time()
 
-    if spec.gpu_nodes:
+    # GPU nodes that joined with the health taint: no device plugin, no gate ranks
+    from ..node.health import has_health_taint
+
+    unhealthy = {n for n in want if has_health_taint(items.get(n) or {})}
+    rep.gpu_unhealthy = sorted(unhealthy)
+    gpu_nodes = {h: n for h, n in spec.gpu_nodes.items() if h not in unhealthy}
+    rccl_hosts, rccl_ndev = _healthy(spec.rccl_hosts, spec.rccl_ndev, spec.rccl_names, unhealthy)
+    proc_hosts, proc_ndev = _healthy(spec.rccl_process_hosts, spec.rccl_process_ndev, spec.rccl_process_names,
+                                     unhealthy)
+    if gate is not None and len(rccl_hosts) != len(spec.rccl_hosts):
+        gate.abort()  # prepared over a node that is now out of the gate
+        gate = None
+
+    if gpu_nodes:
         def gpus() -> Optional[Dict[str, Dict[str, Any]]]:
             got = {i["metadata"]["name"]: i for i in client.k8s_nodes(spec.cluster_id)}
-            for host, n in spec.gpu_nodes.items():
+            for host, n in gpu_nodes.items():
                 alloc = ((got.get(host) or {}).get("status") or {}).get("allocatable", {})
                 if str(alloc.get("amd.com/gpu", "0")) != str(n):
                     return None
             return got
 
-        with span("ready.gpus", nodes=len(spec.gpu_nodes)):
+        with span("ready.gpus", nodes=len(gpu_nodes)):
             items = wait_until(gpus, left(), "amd.com/gpu allocatable on every GPU node")
         rep.phases["gpus_allocatable"] = time.time()
 
@@ -115,31 +135,41 @@ def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float
         rep.nodes[name] = {"labels": (it.get("metadata") or {}).get("labels", {}),
                            "allocatable": (it.get("status") or {}).get("allocatable", {})}
 
-    if spec.rccl_gate and spec.rccl_hosts:
+    if spec.rccl_gate and rccl_hosts:
         if gate is None:
             from .gate import ClusterGate, members_from
 
-            gate = ClusterGate(agent_transport, members_from(spec.rccl_hosts, spec.rccl_ndev or None),
+            gate = ClusterGate(agent_transport, members_from(rccl_hosts, rccl_ndev or None),
                                spec.rccl_sizes, spec.rccl_iters)
         with span("ready.rccl_gate", world=gate.world, nodes=len(gate.members)):
             rep.rccl = gate.run()
-    elif spec.rccl_gate and spec.rccl_process_hosts:
+    elif spec.rccl_gate and proc_hosts:
         from ..node.plan import TOOLS_DIR
         from ..parallel.transport import TransportRouter
         from .process_gate import ProcessGate
 
-        pgate = ProcessGate(host_transport or TransportRouter(), spec.rccl_process_hosts, spec.rccl_process_ndev,
+        pgate = ProcessGate(host_transport or TransportRouter(), proc_hosts, proc_ndev,
                             spec.rccl_sizes, spec.rccl_iters, timeout=left(), tools_dir=tools_dir or TOOLS_DIR,
                             agent_transport=agent_transport)
-        with span("ready.rccl_gate", world=pgate.world, nodes=len(spec.rccl_process_hosts), mode="process"):
+        with span("ready.rccl_gate", world=pgate.world, nodes=len(proc_hosts), mode="process"):
             rep.rccl = pgate.run()
     elif spec.rccl_skip_reason:
         rep.rccl = {"ok": None, "skipped": spec.rccl_skip_reason}
+    elif spec.rccl_gate and unhealthy:
+        rep.rccl = {"ok": None, "skipped": "every MI355X node joined with the GPU health taint"}
     if rep.rccl is not None and "skipped" not in rep.rccl:
         if not rep.rccl.get("ok"):
             raise TKError(f"RCCL readiness gate failed: {rep.rccl}")
         rep.phases["rccl_gate"] = time.time()
     return rep
+
+
+def _healthy(hosts: List[Any], ndev: List[int], names: List[str], unhealthy: set) -> "tuple[List[Any], List[int]]":
+    """``hosts`` / ``ndev`` without the entries whose hostname is in ``unhealthy``."""
+    if not unhealthy or not names:
+        return list(hosts), list(ndev)
+    keep = [i for i, n in enumerate(names) if n not in unhealthy]
+    return [hosts[i] for i in keep], ([ndev[i] for i in keep] if ndev else [])
 
 
 def rccl_gate(transport: Any, agent_urls: List[str], sizes: List[int], iters: int = 5,
@@ -173,8 +203,10 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
     gpu_nodes: Dict[str, int] = {}
     rccl_hosts: List[str] = []
     rccl_ndev: List[int] = []
+    rccl_names: List[str] = []
     proc_hosts: List[HostRef] = []
     proc_ndev: List[int] = []
+    proc_names: List[str] = []
     from ..node.partition import logical_gpus
 
     for host in sorted(nodes):
@@ -189,10 +221,12 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
             if addr.startswith("agent+"):
                 rccl_hosts.append(addr[len("agent+"):])
                 rccl_ndev.append(n)
+                rccl_names.append(host)
             elif addr:
                 proc_hosts.append(HostRef(addr, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
                                           cfg.get("bastion_host") or ""))
                 proc_ndev.append(n)
+                proc_names.append(host)
     skip = ""
     if rccl_gate:
         if rccl_hosts and proc_hosts:
@@ -207,14 +241,15 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
                 addr = str(cfg["host"])
                 ref = HostRef(addr, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
                               cfg.get("bastion_host") or "")
-                mixed.append((ref, logical_gpus(cfg)))
-            proc_hosts, proc_ndev = [m[0] for m in mixed], [m[1] for m in mixed]
-            rccl_hosts, rccl_ndev = [], []
+                mixed.append((ref, logical_gpus(cfg), host))
+            proc_hosts, proc_ndev, proc_names = [m[0] for m in mixed], [m[1] for m in mixed], [m[2] for m in mixed]
+            rccl_hosts, rccl_ndev, rccl_names = [], [], []
         elif not (rccl_hosts or proc_hosts):
             skip = "no MI355X nodes in the cluster"
     spec = ReadinessSpec(cl["rancher_cluster_id"], sorted(nodes), gpu_nodes, timeout,
                          rccl_gate and bool(rccl_hosts or proc_hosts), rccl_hosts, rccl_ndev,
-                         rccl_process_hosts=proc_hosts, rccl_process_ndev=proc_ndev, rccl_skip_reason=skip)
+                         rccl_process_hosts=proc_hosts, rccl_process_ndev=proc_ndev, rccl_skip_reason=skip,
+                         rccl_names=rccl_names, rccl_process_names=proc_names)
     return client, spec
 
 
@@ -277,6 +312,9 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
     ctx.extras["last_readiness"] = rep  # callers that time phases (bench.py) read it here
     ctx.echo(f"cluster ready in {rep.ready_seconds:.2f}s: " +
              json.dumps(rep.to_json()["phase_seconds"], sort_keys=True))
+    if rep.gpu_unhealthy:
+        ctx.echo("GPU nodes joined with the health taint (no GPU pods, not in the RCCL gate): "
+                 + ", ".join(rep.gpu_unhealthy) + " -- see `triton-kubernetes health cluster`")
     return rep
 
 

@@ -1236,6 +1236,13 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("gpu_link_min_gbps", "38",
             "fail the node when a GPU pair's kernel-driven peer read is below this many GB/s (absolute floor: "
             "half of one xGMI link's ~76.8 GB/s one way)"),
+        Var("gpu_health", "fail",
+            "GPU health policy (RAS counters): fail = an unhealthy GPU fails the node; taint = the node joins "
+            "tainted amd.com/gpu-health=unhealthy:NoSchedule (no GPU pods); off = not checked"),
+        Var("gpu_max_uncorrectable_ecc", "0", "uncorrectable ECC errors a GPU may have logged"),
+        Var("gpu_max_retired_pages", "auto",
+            "retired VRAM pages a GPU may have (auto: the amdgpu driver's default threshold, one page per "
+            "100 MiB of VRAM)"),
         Var("rccl_slim", "off",
             "on: build a single-target (gfx950) copy of the node's librccl for faster cold communicator init, "
             "verify it with a one-rank all-reduce, and run rccl-ready on it while it matches the installed "
@@ -1280,6 +1287,9 @@ resource "terraform_data" "install_mi355x_node" {{
       gpu_memory_partition               = var.gpu_memory_partition
       gpu_partitions                     = lookup({{ spx = 1, dpx = 2, qpx = 4, cpx = 8 }}, var.gpu_compute_partition, 1)
       rccl_slim                          = var.rccl_slim
+      gpu_health                         = var.gpu_health
+      gpu_max_uncorrectable_ecc          = var.gpu_max_uncorrectable_ecc
+      gpu_max_retired_pages              = var.gpu_max_retired_pages
     }})]
   }}
 }}

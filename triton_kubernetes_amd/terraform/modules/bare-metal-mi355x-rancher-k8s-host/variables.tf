@@ -169,6 +169,24 @@ variable "gpu_link_min_gbps" {
   default     = "38"
 }
 
+variable "gpu_health" {
+  description = "GPU health policy (RAS counters): fail = an unhealthy GPU fails the node; taint = the node joins tainted amd.com/gpu-health=unhealthy:NoSchedule (no GPU pods); off = not checked"
+  type        = string
+  default     = "fail"
+}
+
+variable "gpu_max_uncorrectable_ecc" {
+  description = "uncorrectable ECC errors a GPU may have logged"
+  type        = string
+  default     = "0"
+}
+
+variable "gpu_max_retired_pages" {
+  description = "retired VRAM pages a GPU may have (auto: the amdgpu driver's default threshold, one page per 100 MiB of VRAM)"
+  type        = string
+  default     = "auto"
+}
+
 variable "rccl_slim" {
   description = "on: build a single-target (gfx950) copy of the node's librccl for faster cold communicator init, verify it with a one-rank all-reduce, and run rccl-ready on it while it matches the installed librccl (a modified vendor binary: off by default)"
   type        = string

@@ -416,10 +416,26 @@ fi
 %{ endif ~}
 $T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/dev/null
 $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
-sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels
+sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels /etc/triton-kubernetes/gpu-taints
 %{ if gpu_burnin != "off" ~}
 $T/gpu-burnin --all --level '${gpu_burnin}' --compute-partition ${gpu_compute_partition} --memory-partition ${gpu_memory_partition} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
 sudo install -m 0644 /tmp/tk-burnin-labels /etc/triton-kubernetes/gpu-burnin-labels
+%{ endif ~}
+%{ if gpu_health != "off" ~}
+# GPU health (RAS): exit 3 = an unhealthy GPU; fail the node or join it tainted
+health_rc=0
+$T/amdgpu-topo-labeller --health --max-uncorrectable ${gpu_max_uncorrectable_ecc} --max-bad-pages ${gpu_max_retired_pages} > /tmp/tk-gpu-health.json || health_rc=$?
+sudo install -m 0644 /tmp/tk-gpu-health.json /etc/triton-kubernetes/gpu-health.json
+{ $T/amdgpu-topo-labeller --health --labels --max-uncorrectable ${gpu_max_uncorrectable_ecc} --max-bad-pages ${gpu_max_retired_pages} || true; } | sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels >/dev/null
+case $health_rc in
+  0) ;;
+%{ if gpu_health == "taint" ~}
+  3) echo 'amd.com/gpu-health=unhealthy:NoSchedule' | sudo tee /etc/triton-kubernetes/gpu-taints >/dev/null ;;
+%{ else ~}
+  3) echo 'unhealthy GPUs (gpu_health = fail):' >&2; cat /tmp/tk-gpu-health.json >&2; exit 1 ;;
+%{ endif ~}
+  *) echo "GPU health check failed (exit $health_rc)" >&2; exit 1 ;;
+esac
 %{ endif ~}
 { $T/amdgpu-topo-labeller --rccl-env || true; cat <<'TK_RCCL_EOF'
 ${rccl_env_file}
@@ -434,6 +450,7 @@ set -a; . /etc/rccl/rccl.env; set +a
 $RCCL_READY --ngpus ${gpu_count * gpu_partitions} --min-busbw ${rccl_min_busbw}
 %{ endif ~}
 labels=$(cat /etc/triton-kubernetes/gpu-labels $([ -r /etc/triton-kubernetes/gpu-burnin-labels ] && echo /etc/triton-kubernetes/gpu-burnin-labels) | sed 's/^/--label /' | tr '\n' ' ')
+if [ -r /etc/triton-kubernetes/gpu-taints ]; then labels="$labels $(sed 's/^/--taints /' /etc/triton-kubernetes/gpu-taints | tr '\n' ' ')"; fi
 %{ if k8s_distribution == "rke1" ~}
 """ + DOCKER_INSTALL + r"""
 %{ endif ~}
