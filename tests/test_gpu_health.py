@@ -108,6 +108,20 @@ def test_partitions_count_a_gpu_once(tmp_path, native_ok):
     assert labels_from_topology(doc)["amd.com/gpu.ecc-uncorrectable"] == "3"
 
 
+def test_aca_counters(tmp_path, native_ok):
+    """MI300/MI350-series drivers report per-block counts as ras/aca_<block> ("ue: N", "ce: N",
+    "de: N"); when the legacy <block>_err_count files are there too, only ACA counts."""
+    root = healthy_tree(str(tmp_path))
+    ras = os.path.join(root, "sys/class/drm/renderD130/device/ras")
+    for block, ue in (("umc", 1), ("gfx", 0), ("xgmi_wafl", 2)):
+        with open(os.path.join(ras, f"aca_{block}"), "w") as fh:
+            fh.write(f"ue: {ue}\nce: 3\nde: 0\n")
+    _ras(root, 130, ue=9, ce=9)  # legacy view of the same errors: not counted again
+    v = _both(root)
+    assert v["reasons"] == ["GPU 2 (0000:25:00.0): 3 uncorrectable ECC errors (max 0)"]
+    assert v["gpus"][2]["ecc_correctable"] == 9
+
+
 def test_no_ras_reported_is_not_judged(native_ok, tmp_path):
     root = make_tree(str(tmp_path))  # no ras directories at all
     v = _both(root)

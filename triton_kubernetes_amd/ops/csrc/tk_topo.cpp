@@ -396,9 +396,17 @@ Topology collect_sysfs(const std::string& root) {
     }
     DIR* ras = opendir((dev + "/ras").c_str());
     if (ras) {
+      // per-block error counters, "ue: N\nce: N[\nde: N]": aca_<block> on parts with the
+      // Accelerator Check Architecture (MI300 / MI350 series), <block>_err_count before it;
+      // when a driver exposes both, the ACA view is the one counted
+      std::vector<std::string> aca, legacy;
       while (dirent* e = readdir(ras)) {
         const std::string n = e->d_name;
-        if (n.size() < 10 || n.compare(n.size() - 10, 10, "_err_count") != 0) continue;
+        if (n.rfind("aca_", 0) == 0) aca.push_back(n);
+        else if (n.size() > 10 && n.compare(n.size() - 10, 10, "_err_count") == 0) legacy.push_back(n);
+      }
+      closedir(ras);
+      for (const auto& n : aca.empty() ? legacy : aca) {
         std::string c;
         if (!read_file(dev + "/ras/" + n, &c)) continue;
         unsigned long long ue = 0, ce = 0;
@@ -410,7 +418,6 @@ Topology collect_sysfs(const std::string& root) {
         g.ecc_uncorrectable += ue;
         g.ecc_correctable += ce;
       }
-      closedir(ras);
       // the driver's bad-page records, one "0x<page> : 0x<size> : R|P|F" line each
       // (R reserved, P pending until the next reset, F could not be reserved)
       FILE* f = fopen((dev + "/ras/gpu_vram_bad_pages").c_str(), "r");
