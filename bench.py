@@ -79,6 +79,10 @@ def parse_args():
                     help="on: the node's opt-in single-target gfx950 RCCL copy (ops/rccl_slim.py), prepared and "
                          "verified before the timed region, loaded by the agents (TK_HIP_RUNTIME=slim). Default "
                          "off: the agents load /opt/rocm's HIP runtime and RCCL, the product default")
+    ap.add_argument("--gpu-health", default="taint", choices=["fail", "taint", "off"],
+                    help="the GPU node's health policy (node/health.py).  taint (bench default): a GPU with "
+                         "uncorrectable ECC errors does not abort the run; the node joins tainted and the line "
+                         "lists it under gpu_unhealthy_nodes (its GPUs then sit out the GPU and RCCL checks)")
     ap.add_argument("--sim-gpu", action="store_true",
                     help="CPU dry run: synthetic topology, no burn-in kernels, no RCCL (never a valid measurement)")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
@@ -307,7 +311,8 @@ def main() -> int:
                         "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": [cp]},
                        {"rancher_host_label": "worker", "node_count": workers, "hostname": f"{name}-gpu",
                         "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": gpu_hosts,
-                        "gpu": "mi355x", "gpu_count": gpus_per_worker, "gpu_burnin": args.burnin},
+                        "gpu": "mi355x", "gpu_count": gpus_per_worker, "gpu_burnin": args.burnin,
+                        "gpu_health": args.gpu_health},
                    ])
         # the CLI's own agent transport: per-node tokens + TLS against the manager's CA
         ctx = Context(settings=Settings(cfg, env={}), out=devnull)
@@ -326,6 +331,7 @@ def main() -> int:
         rep = ctx.extras.get("last_readiness")
         if rep is not None:
             out["phase_s"] = rep.to_json()["phase_seconds"]
+            out["gpu_unhealthy"] = list(rep.gpu_unhealthy)
             ranks = (rep.rccl or {}).get("ranks") or []
             phases = [r.get("phase_ms") or {} for r in ranks]
             if phases:  # the gate's communicator phases, max over agents
@@ -449,6 +455,7 @@ def main() -> int:
                 "control_plane_nodes": 2, "global_batch": n_gpus, "seq_len": 0,
                 "parallelism": f"{workers} worker node(s) x {gpus_per_worker} GPU(s)",
                 "executor": "direct", "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate,
+                "gpu_health": args.gpu_health,
                 "start": ("cold (fresh agent processes per step)" if args.agents == "proc"
                           else "cold agents in the bench process (fresh NodeAgent objects per step)"),
                 "rccl_gate_max_mib": args.rccl_mib,
@@ -465,6 +472,8 @@ def main() -> int:
             "create_to_ready_s": ready,
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),
             "warm_create_to_ready_s": round(sum(warm) / len(warm), 4) if warm else None,
+            # GPU nodes that joined with the health taint in any timed step (normally none)
+            "gpu_unhealthy_nodes": sorted({h for r in results for h in r.get("gpu_unhealthy", [])}),
             "phase_ms_per_step": phase_ms,
         }
         print(json.dumps(line), flush=True)
