@@ -400,3 +400,14 @@ def test_health_on_the_box():
         if "ecc_uncorrectable" in a and "ecc_uncorrectable" in b:
             assert a["ecc_uncorrectable"] == b["ecc_uncorrectable"]
     assert topo.native_health("sysfs") == health.evaluate(topo.native_topology("sysfs"))
+
+
+@pytest.mark.gpu
+def test_gpu_health_cli_on_the_box(capsys):
+    from triton_kubernetes_amd.ops.cli import main
+
+    for source in ("sysfs", "amdsmi"):
+        rc = main(["health", "--source", source])
+        doc = json.loads(capsys.readouterr().out)
+        assert rc in (0, 3) and (rc == 0) == (doc["status"] == "healthy")
+        assert doc["gpus"] and doc["gpus"][0]["bad_page_limit"] > 0

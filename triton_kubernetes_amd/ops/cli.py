@@ -3,6 +3,7 @@
     python -m triton_kubernetes_amd.ops.cli burnin [--device N|--all] [--level quick|full]
     python -m triton_kubernetes_amd.ops.cli topology
     python -m triton_kubernetes_amd.ops.cli labels
+    python -m triton_kubernetes_amd.ops.cli health [--max-uncorrectable N] [--max-bad-pages N|auto] [--source sysfs|amdsmi]
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
     python -m triton_kubernetes_amd.ops.cli links [--min-frac F] [--min-gbps G] [--method kernel-read|sdma-copy] [--mib M]
     python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
@@ -28,6 +29,10 @@ def main(argv: Sequence[str] = ()) -> int:
     b.add_argument("--level", default="quick", choices=["quick", "full", "off"])
     sub.add_parser("topology")
     sub.add_parser("labels")
+    hl = sub.add_parser("health", help="GPU RAS health: uncorrectable ECC errors, retired VRAM pages (node/health.py)")
+    hl.add_argument("--max-uncorrectable", type=int, default=0)
+    hl.add_argument("--max-bad-pages", default="auto", help="a count, or auto (the driver's default threshold)")
+    hl.add_argument("--source", default="sysfs", choices=["sysfs", "amdsmi"])
     r = sub.add_parser("rccl-local")
     r.add_argument("--ngpus", type=int, default=0)
     r.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
@@ -80,6 +85,16 @@ def main(argv: Sequence[str] = ()) -> int:
 
         print(json.dumps(labels_from_topology(topo.discover()), indent=2, sort_keys=True))
         return 0
+    if args.cmd == "health":
+        from ..node.health import evaluate, limits_of
+        from . import topo
+
+        max_ue, max_bad = limits_of({"gpu_max_uncorrectable_ecc": args.max_uncorrectable,
+                                     "gpu_max_retired_pages": args.max_bad_pages})
+        doc = topo.native_topology("sysfs") if args.source == "sysfs" else topo.amdsmi_topology()
+        verdict = evaluate(doc, max_ue, max_bad)
+        print(json.dumps(verdict, indent=2))
+        return 0 if verdict["status"] == "healthy" else 3
     if args.cmd == "rccl-local":
         from . import probe, rccl
 
