@@ -68,6 +68,22 @@ def test_sanitize_rules():
     svc = sanitize({"kind": "Service", "metadata": {"name": "s", "uid": "u", "resourceVersion": "3"},
                     "spec": {"clusterIP": "1.2.3.4", "clusterIPs": ["1.2.3.4"], "ports": []}, "status": {}})
     assert svc == {"kind": "Service", "metadata": {"name": "s"}, "spec": {"ports": []}}
+    # a headless service stays headless
+    headless = sanitize({"kind": "Service", "metadata": {"name": "h"}, "spec": {"clusterIP": "None",
+                                                                                "clusterIPs": ["None"]}})
+    assert headless["spec"] == {"clusterIP": "None", "clusterIPs": ["None"]}
+    # a Job loses the selector and controller-uid labels the API server generated ...
+    gen = {"batch.kubernetes.io/controller-uid": "u1", "controller-uid": "u1", "job-name": "j",
+           "batch.kubernetes.io/job-name": "j", "app": "train"}
+    job = sanitize({"kind": "Job", "metadata": {"name": "j"},
+                    "spec": {"selector": {"matchLabels": {"batch.kubernetes.io/controller-uid": "u1"}},
+                             "template": {"metadata": {"labels": dict(gen)}, "spec": {}}}})
+    assert "selector" not in job["spec"] and job["spec"]["template"]["metadata"]["labels"] == {"app": "train"}
+    # ... unless it chose them itself
+    manual = sanitize({"kind": "Job", "metadata": {"name": "m"},
+                       "spec": {"manualSelector": True, "selector": {"matchLabels": {"app": "x"}},
+                                "template": {"metadata": {"labels": {"app": "x"}}}}})
+    assert manual["spec"]["selector"] == {"matchLabels": {"app": "x"}}
 
 
 def test_backup_to_state_backend_and_restore(cluster):
@@ -118,6 +134,8 @@ def test_backup_to_s3_with_signatures(cluster):
         second = backup_cluster(ctx, backend)
         assert first != second and ("bk", f"triton-kubernetes/mgr/{second}") in s3.objects
         assert s3.rejected == 0
+        # archives hold Secrets: stored with server-side encryption (a signed header)
+        assert s3.encryption[("bk", f"triton-kubernetes/mgr/{second}")] == "AES256"
         keys = S3Client(s3.access_key, s3.secret_key, s3.region, s3.url).list_keys("bk", "triton-kubernetes/")
         assert len(keys) == 2  # paginated 1 per page
         ctx = _ctx(backup_target="s3", s3_bucket="bk", aws_access_key=s3.access_key, aws_secret_key=s3.secret_key,

@@ -28,8 +28,10 @@ def _sign(key: bytes, msg: str) -> bytes:
 
 def sigv4_headers(method: str, url: str, body: bytes, access_key: str, secret_key: str, region: str,
                   service: str, now: Optional[datetime.datetime] = None,
-                  session_token: Optional[str] = None, content_sha256: bool = False) -> Dict[str, str]:
-    """Signature Version 4 headers for one request (AWS general reference algorithm)."""
+                  session_token: Optional[str] = None, content_sha256: bool = False,
+                  extra: Optional[Dict[str, str]] = None) -> Dict[str, str]:
+    """Signature Version 4 headers for one request (AWS general reference algorithm).
+    ``extra`` headers (e.g. ``x-amz-server-side-encryption``) are signed and returned."""
     now = now or datetime.datetime.utcnow()
     amz_date = now.strftime("%Y%m%dT%H%M%SZ")
     datestamp = now.strftime("%Y%m%d")
@@ -45,6 +47,8 @@ def sigv4_headers(method: str, url: str, body: bytes, access_key: str, secret_ke
         headers["x-amz-content-sha256"] = payload_hash
     if session_token:
         headers["x-amz-security-token"] = session_token
+    for k, v in (extra or {}).items():
+        headers[k.lower()] = str(v).strip()
     signed_headers = ";".join(sorted(headers))
     canonical_headers = "".join(f"{k}:{headers[k]}\n" for k in sorted(headers))
     canonical_request = "\n".join([method, canonical_uri, canonical_query, canonical_headers, signed_headers,
@@ -66,6 +70,7 @@ def sigv4_headers(method: str, url: str, body: bytes, access_key: str, secret_ke
         out["X-Amz-Security-Token"] = session_token
     if content_sha256:
         out["X-Amz-Content-Sha256"] = payload_hash
+    out.update(extra or {})
     return out
 
 
@@ -130,13 +135,15 @@ class S3Client:
         path = f"/{bucket}" + (f"/{urllib.parse.quote(key, safe='/-_.~')}" if key else "")
         return self.endpoint + path + (f"?{query}" if query else "")
 
-    def _req(self, method: str, url: str, body: bytes = b"", ok=(200,)):
+    def _req(self, method: str, url: str, body: bytes = b"", ok=(200,), extra: Optional[Dict[str, str]] = None):
         hdrs = sigv4_headers(method, url, body, self.access_key, self.secret_key, self.region, "s3",
-                             content_sha256=True)
+                             content_sha256=True, extra=extra)
         return self.http.request(method, url, headers=hdrs, data=body if body else None, ok=ok)
 
-    def put_object(self, bucket: str, key: str, data: bytes) -> None:
-        self._req("PUT", self._url(bucket, key), data, ok=(200, 201, 204))
+    def put_object(self, bucket: str, key: str, data: bytes, encrypt: bool = True) -> None:
+        """PUT an object; ``encrypt``: server-side encryption with S3-managed keys (SSE-S3)."""
+        self._req("PUT", self._url(bucket, key), data, ok=(200, 201, 204),
+                  extra={"x-amz-server-side-encryption": "AES256"} if encrypt else None)
 
     def get_object(self, bucket: str, key: str) -> bytes:
         return self._req("GET", self._url(bucket, key)).body

@@ -18,6 +18,7 @@ class FakeS3:
         self.access_key, self.secret_key, self.region = access_key, secret_key, region
         self.page_size = page_size
         self.objects: Dict[Tuple[str, str], bytes] = {}
+        self.encryption: Dict[Tuple[str, str], str] = {}  # x-amz-server-side-encryption per object
         self.buckets = set()
         self.rejected = 0
         self.mu = threading.Lock()
@@ -46,8 +47,15 @@ class FakeS3:
             now = datetime.datetime.strptime(amz_date, "%Y%m%dT%H%M%SZ")
         except ValueError:
             return False
+        # every other x-amz-* header the client signed (e.g. server-side encryption) is part
+        # of the signature: a header sent unsigned, or signed with another value, fails
+        signed = auth.split("SignedHeaders=", 1)[-1].split(",", 1)[0].split(";")
+        extra = {h: headers.get(h, "") for h in signed
+                 if h.startswith("x-amz-") and h not in ("x-amz-date", "x-amz-content-sha256", "x-amz-security-token")}
+        if any(k.lower().startswith("x-amz-") and k.lower() not in signed for k in headers.keys()):
+            return False
         want = sigv4_headers(method, self.url + path, body, self.access_key, self.secret_key, self.region, "s3",
-                             now=now, content_sha256=True)
+                             now=now, content_sha256=True, extra=extra)
         return want["Authorization"] == auth and headers.get("X-Amz-Content-Sha256") == want["X-Amz-Content-Sha256"]
 
     def _handler(self):
@@ -84,6 +92,7 @@ class FakeS3:
                     if method == "PUT":
                         fake.buckets.add(bucket)
                         fake.objects[(bucket, key)] = body
+                        fake.encryption[(bucket, key)] = self.headers.get("x-amz-server-side-encryption", "")
                         return self._reply(200)
                     if key:
                         data = fake.objects.get((bucket, key))

@@ -8,9 +8,13 @@ your clusters to manta/S3" (``README.md:16``), but the CLI never implemented it
   objects are namespaces, configmaps, secrets, services, service accounts, PVCs,
   deployments, statefulsets, daemonsets, jobs, cronjobs and ingresses.
   Server-populated fields are stripped: uid, resourceVersion, timestamps,
-  managedFields, status, cluster IPs. Objects owned by a controller are skipped,
-  because the controller re-creates them. The result is written as one JSON
-  archive either to the manager's state backend (local or Manta) or to S3.
+  managedFields, status, allocated cluster IPs (a headless service keeps
+  ``clusterIP: None``), a Job's generated selector and controller-uid labels (an API
+  server refuses to create a Job that carries them). Objects owned by a controller
+  are skipped, because the controller re-creates them. The result is written as one
+  JSON archive either to the manager's state backend (local or Manta, the index of
+  archives updated under the backend's lock) or to S3 (server-side encrypted: the
+  archive holds the namespaces' Secrets).
 * **Restore** creates the namespaces, then the objects, in dependency order. An
   object that already exists is replaced (PUT on 409), so a restore can be re-run.
 
@@ -51,6 +55,8 @@ RESOURCES: List[Tuple[str, str]] = [
     ("/apis/networking.k8s.io/v1/namespaces/{ns}/ingresses", "Ingress"),
 ]
 ARCHIVE_VERSION = 1
+_JOB_GENERATED_LABELS = ("controller-uid", "batch.kubernetes.io/controller-uid", "job-name",
+                         "batch.kubernetes.io/job-name")
 _META_DROP = ("uid", "resourceVersion", "creationTimestamp", "managedFields", "selfLink", "generation",
               "deletionTimestamp", "deletionGracePeriodSeconds")
 
@@ -76,8 +82,18 @@ def sanitize(obj: Dict[str, Any]) -> Optional[Dict[str, Any]]:
     ann.pop("kubectl.kubernetes.io/last-applied-configuration", None)
     if kind == "Service":
         spec = out.get("spec") or {}
-        for k in ("clusterIP", "clusterIPs"):
-            spec.pop(k, None)
+        if str(spec.get("clusterIP", "")) != "None":  # headless services stay headless
+            for k in ("clusterIP", "clusterIPs"):
+                spec.pop(k, None)
+    if kind == "Job":
+        # the API server generates selector + controller-uid labels and rejects a Job
+        # that brings its own (unless manualSelector): drop them, as velero does
+        spec = out.get("spec") or {}
+        if not spec.get("manualSelector"):
+            spec.pop("selector", None)
+            labels = ((spec.get("template") or {}).get("metadata") or {}).get("labels") or {}
+            for k in _JOB_GENERATED_LABELS:
+                labels.pop(k, None)
     if kind == "PersistentVolumeClaim":
         (out.get("spec") or {}).pop("volumeName", None)
     return out
@@ -106,11 +122,12 @@ class StateTarget:
         return [n for n in names if n.startswith(prefix)]
 
     def record(self, name: str) -> None:
-        index = self.backend.read_blob(self.manager, "backups.json")
-        names = json.loads(index) if index else []
-        if name not in names:
-            names.append(name)
-        self.backend.write_blob(self.manager, "backups.json", json.dumps(names).encode())
+        with self.backend.lock(self.manager):  # concurrent backups must not drop each other's entry
+            index = self.backend.read_blob(self.manager, "backups.json")
+            names = json.loads(index) if index else []
+            if name not in names:
+                names.append(name)
+            self.backend.write_blob(self.manager, "backups.json", json.dumps(names).encode())
 
 
 class S3Target:
