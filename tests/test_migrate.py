@@ -117,6 +117,26 @@ def test_migrate_refusal_leaves_the_document_alone():
     assert be.state("mgr").doc == doc and be.read_blob("mgr", BACKUP_BLOB) is None
 
 
+def test_migrate_refuses_a_document_changed_during_confirmation():
+    from triton_kubernetes_amd.state import State
+
+    be = _backend(reference_doc())
+    ctx = make_ctx({"cluster_manager": "mgr"})
+    real_confirm = ctx.confirm
+
+    def confirm(*a, **kw):  # another CLI persists while this one asks
+        changed = reference_doc()
+        changed["module"]["cluster-manager"]["name"] = "renamed"
+        be.persist_state(State("mgr", json.dumps(changed).encode()))
+        return real_confirm(*a, **kw)
+
+    ctx.confirm = confirm
+    with pytest.raises(TKError, match="changed while the migration was being confirmed"):
+        migrate_manager(ctx, be)
+    assert be.state("mgr").doc["module"]["cluster-manager"]["name"] == "renamed"
+    assert be.read_blob("mgr", BACKUP_BLOB) is None
+
+
 def test_cli_migrate_manager_on_the_local_backend(tk_home):
     """``triton-kubernetes migrate manager`` end to end on ~/.triton-kubernetes/<manager>/."""
     import io

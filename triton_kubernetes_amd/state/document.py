@@ -76,6 +76,7 @@ class State:
         if not isinstance(doc, dict):
             raise StateError(f"invalid state document for '{name}': top level must be an object")
         self._doc: Dict[str, Any] = doc
+        self._base: Optional[Dict[str, Any]] = None  # mark_base(): the document as read
 
     # --- generic dotted-path access (gabs Path/SetP/DeleteP semantics) -------
     @property
@@ -193,6 +194,57 @@ class State:
             cfg = backends[kind]
             return kind, cfg if isinstance(cfg, dict) else {}
         return None, {}
+
+    # --- concurrent writers ---------------------------------------------------------
+    def mark_base(self) -> "State":
+        """Remember the document as read from the backend: :meth:`rebase` later replays
+        only what this run changed on top of what is persisted then."""
+        self._base = copy.deepcopy(self._doc)
+        return self
+
+    def rebase(self, current: "State") -> List[str]:
+        """Three-way merge onto ``current`` (the persisted document, read under the backend
+        lock): every module (and top-level key) this run added, changed or deleted since
+        :meth:`mark_base` is applied to ``current``; everything else is ``current``'s, so
+        another CLI's clusters and nodes persisted meanwhile are kept.  Raises
+        :class:`StateError` when both changed the same module differently.  Returns the
+        keys another writer changed (empty: nobody did).  No-op without a base."""
+        if self._base is None:
+            return []
+        base = self._base
+        if current.doc == base:
+            return []
+        conflicts: List[str] = []
+
+        def merge(b: Dict[str, Any], m: Dict[str, Any], c: Dict[str, Any], skip: str = "") -> Dict[str, Any]:
+            out = {k: v for k, v in c.items() if k != skip}
+            for k in (set(b) | set(m)) - {skip}:
+                bv, mv = b.get(k), m.get(k)
+                if bv == mv:
+                    continue  # not ours
+                cv = c.get(k)
+                if cv != bv and cv != mv:
+                    conflicts.append(f"module.{k}" if not skip else k)
+                    continue
+                if mv is None:
+                    out.pop(k, None)
+                else:
+                    out[k] = copy.deepcopy(mv)
+            return out
+
+        others = sorted(k for k in set(base.get("module") or {}) | set(current.modules())
+                        if (base.get("module") or {}).get(k) != current.modules().get(k))
+        modules = merge(base.get("module") or {}, self.modules(), current.modules())
+        doc = merge(base, self._doc, current.doc, skip="module")
+        if conflicts:
+            raise StateError(f"'{self.name}' was changed by another triton-kubernetes run "
+                             f"({', '.join(sorted(conflicts))}); re-run the command")
+        if modules or "module" in self._doc or "module" in current.doc:
+            doc["module"] = modules
+        self._doc.clear()
+        self._doc.update(doc)
+        self._base = copy.deepcopy(self._doc)
+        return others
 
     # --- serialisation -----------------------------------------------------------
     def bytes(self) -> bytes:

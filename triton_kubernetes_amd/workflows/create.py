@@ -12,7 +12,10 @@ orphans whatever a failed apply created:
   resource that may exist) and records ``status.json`` = ``{"phase":
   "apply_failed", "modules": [...], "error": ...}`` in the backend;
 * ``create manager`` with the name of a manager whose first apply failed
-  resumes it instead of failing with "already exists".
+  resumes it instead of failing with "already exists";
+* two CLIs working on one manager (a shared Manta backend) do not overwrite each
+  other: under the backend lock the run's own changes are replayed onto the document
+  persisted meanwhile (``State.rebase``), and a module both changed is an error.
 """
 
 import json
@@ -52,6 +55,10 @@ def apply_and_persist(ctx: Context, backend: Backend, state: State, new_modules:
     """Run the executor, then persist; on failure persist + record status (see module doc)."""
     executor = executor_for(ctx, state, backend)
     with backend.lock(state.name):
+        # another run may have persisted clusters / nodes since this one read the document
+        others = state.rebase(backend.state(state.name))
+        if others:
+            ctx.echo(f"note: kept changes another run persisted meanwhile ({', '.join(others)})")
         try:
             with span("apply", executor=executor.name, modules=len(new_modules)):
                 executor.apply(state, backend)
@@ -67,6 +74,7 @@ def apply_and_persist(ctx: Context, backend: Backend, state: State, new_modules:
         # per-module results (the DirectExecutor's report: node plans' step timings) for callers
         ctx.extras["last_apply"] = getattr(executor, "last_report", None)
         backend.persist_state(state)
+        state.mark_base()
         _write_status(backend, state.name, {"phase": "applied", "modules": new_modules, "time": time.time()})
 
 
@@ -103,7 +111,7 @@ def new_manager(ctx: Context, backend: Backend) -> None:
         if read_status(backend, name).get("phase") != "apply_failed":
             raise ConfigError(f"A Cluster Manager with the name '{name}' already exists.")
         ctx.echo(f"Resuming creation of '{name}' after a failed apply.")
-    state = backend.state(name)
+    state = backend.state(name).mark_base()
     fn = MANAGER_PROVIDERS.get(provider)
     if fn is None:
         raise ConfigError(f"Unsupported cloud provider '{provider}', cannot create manager")
@@ -132,7 +140,7 @@ def new_cluster(ctx: Context, backend: Backend) -> Optional[str]:
     if not managers:
         raise ConfigError(NO_MANAGERS)
     manager = select_manager(ctx, managers)
-    state = backend.state(manager)
+    state = backend.state(manager).mark_base()
     provider = ctx.resolve_choice("cluster_cloud_provider", "Create Cluster in which Cloud Provider",
                                   CLUSTER_CHOICES, transform=str.lower)
     fn = CLUSTER_PROVIDERS.get(provider)
@@ -178,7 +186,7 @@ def new_node(ctx: Context, backend: Backend) -> Optional[List[str]]:
     if not managers:
         raise ConfigError(NO_MANAGERS)
     manager = select_manager(ctx, managers)
-    state = backend.state(manager)
+    state = backend.state(manager).mark_base()
     _, key = select_cluster(ctx, state.clusters(), "Cluster to deploy node to")
     parts = key.split("_")
     if len(parts) < 3:

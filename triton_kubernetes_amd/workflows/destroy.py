@@ -5,6 +5,10 @@
   MI355X add-on module if present), then drop those modules and persist;
 * node    — ``-target=module.<node>``, drop it, persist.
 
+The document is read again under the backend lock before anything is destroyed, so
+nodes another run added meanwhile are destroyed with their cluster and its clusters
+are kept in the persisted document.
+
 Extension (opt-in via ``rancher_cleanup: true``): also
 remove the cluster / node objects from Rancher after the destroy.
 """
@@ -29,6 +33,7 @@ def delete_manager(ctx: Context, backend: Backend) -> None:
         ctx.echo("Destroy manager canceled.")
         return
     with backend.lock(manager):
+        state = backend.state(manager)
         with span("destroy", scope="manager"):
             executor_for(ctx, state, backend).destroy(state, backend, [])
         backend.delete_state(manager)
@@ -44,13 +49,14 @@ def delete_cluster(ctx: Context, backend: Backend) -> None:
     if not ctx.confirm(f'Are you sure you want to destroy "{name}"', f'Destroy "{name}"'):
         ctx.echo("Destroy cluster canceled.")
         return
-    nodes = state.nodes(key)
-    targets = [key] + [nodes[h] for h in sorted(nodes)]
-    _, cluster_name = cluster_key_parts(key)
-    addon = addons_key(cluster_name)
-    if state.module(addon) is not None:
-        targets.insert(0, addon)
     with backend.lock(manager):
+        state = _reread(backend, manager, key)
+        nodes = state.nodes(key)
+        targets = [key] + [nodes[h] for h in sorted(nodes)]
+        _, cluster_name = cluster_key_parts(key)
+        addon = addons_key(cluster_name)
+        if state.module(addon) is not None:
+            targets.insert(0, addon)
         cleanup = _rancher_cleanup_info(ctx, backend, state, key)
         with span("destroy", scope="cluster", targets=len(targets)):
             executor_for(ctx, state, backend).destroy(state, backend, [f"module.{t}" for t in targets])
@@ -73,10 +79,19 @@ def delete_node(ctx: Context, backend: Backend) -> None:
         ctx.echo("Destroy node canceled.")
         return
     with backend.lock(manager):
+        state = _reread(backend, manager, node_key)
         with span("destroy", scope="node"):
             executor_for(ctx, state, backend).destroy(state, backend, [f"module.{node_key}"])
         state.delete_module(node_key)
         backend.persist_state(state)
+
+
+def _reread(backend: Backend, manager: str, key: str):
+    """The persisted document (under the lock); ``key`` must still be in it."""
+    state = backend.state(manager)
+    if state.module(key) is None:
+        raise ConfigError(f"module.{key} was removed by another triton-kubernetes run.")
+    return state
 
 
 def _rancher_cleanup_info(ctx: Context, backend: Backend, state, cluster_key: str):

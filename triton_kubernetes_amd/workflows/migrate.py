@@ -102,6 +102,11 @@ def migrate_manager(ctx: Context, backend: Backend) -> None:
         ctx.echo("Migrate manager canceled.")
         return
     with backend.lock(manager):
+        # the plan was made (and confirmed) on the document read before the lock: refuse
+        # rather than overwrite what another CLI persisted in between
+        if backend.state(manager).bytes() != state.bytes():
+            raise TKError(f'Cluster manager "{manager}" changed while the migration was being confirmed; '
+                          "run migrate again.")
         try:
             backend.write_blob(manager, BACKUP_BLOB, state.bytes())
         except NotImplementedError:
