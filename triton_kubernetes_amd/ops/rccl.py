@@ -120,8 +120,9 @@ def sweep_rank(rank: int, world: int, uid: bytes, device: int, sizes: Sequence[i
 
 class GateComm:
     """This process's ranks ``rank_base .. rank_base+len(devices)-1`` of a cluster-wide
-    communicator (``tkr_gate_*``).  ``blocking=False`` starts RCCL's non-blocking
-    init and returns at once, so the init overlaps whatever the caller does next;
+    communicator (``tkr_gate_*``).  ``blocking=False`` runs the grouped
+    ``ncclCommInitRank`` on a thread of its own and returns at once, so the init overlaps
+    whatever the caller does next;
     :meth:`sweep` waits for the rest, runs the verified all-reduce sweep and
     consumes the handle.  :meth:`abort` releases a gate that will never run."""
 
