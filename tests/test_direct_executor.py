@@ -105,8 +105,15 @@ def test_full_bringup_with_gpu_addons_and_wait(env):
     assert tf2["module_state"]["node_baremetal_dev_gpu-1"]["applied_at"] == \
         tf["module_state"]["node_baremetal_dev_gpu-1"]["applied_at"]
 
-    delete_node(make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", hostname="gpu-4")), backend)
+    cid = next(iter(fake.state.clusters))
+    assert any(n["hostname"] == "gpu-4" for n in fake.state.cluster_nodes[cid].values())
+    dn = make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", hostname="gpu-4", rancher_cleanup=True))
+    delete_node(dn, backend)
     assert "node_baremetal_dev_gpu-4" not in json.loads(backend.read_tfstate("mgr"))["module_outputs"]
+    # Q7 extension: the node's Rancher object is gone too (and with it the k8s node)
+    assert not any(n["hostname"] == "gpu-4" for n in fake.state.cluster_nodes[cid].values())
+    assert "gpu-4" not in {n["metadata"]["name"] for n in fake.k8s_nodes(cid)}
+    assert "Removed Rancher node" in output(dn)
     delete_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", rancher_cleanup=True)), backend)
     assert backend.state("mgr").clusters() == {}
     assert fake.state.clusters == {}  # Q7 extension: Rancher object removed

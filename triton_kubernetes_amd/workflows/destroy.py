@@ -10,7 +10,9 @@ nodes another run added meanwhile are destroyed with their cluster and its clust
 are kept in the persisted document.
 
 Extension (opt-in via ``rancher_cleanup: true``): also
-remove the cluster / node objects from Rancher after the destroy.
+remove the cluster object (``destroy cluster``) or the node's object (``destroy node``:
+the Rancher node with that hostname, which also drops it from the Kubernetes node list)
+from Rancher after the destroy.
 """
 
 from ..backend.base import Backend
@@ -80,10 +82,13 @@ def delete_node(ctx: Context, backend: Backend) -> None:
         return
     with backend.lock(manager):
         state = _reread(backend, manager, node_key)
+        cleanup = _rancher_node_cleanup_info(ctx, backend, state, key, hostname)
         with span("destroy", scope="node"):
             executor_for(ctx, state, backend).destroy(state, backend, [f"module.{node_key}"])
         state.delete_module(node_key)
         backend.persist_state(state)
+    if cleanup:
+        cleanup()
 
 
 def _reread(backend: Backend, manager: str, key: str):
@@ -92,6 +97,33 @@ def _reread(backend: Backend, manager: str, key: str):
     if state.module(key) is None:
         raise ConfigError(f"module.{key} was removed by another triton-kubernetes run.")
     return state
+
+
+def _rancher_node_cleanup_info(ctx: Context, backend: Backend, state, cluster_key: str, hostname: str):
+    """Return a callable deleting the node's Rancher object (opt-in), or ``None``."""
+    if not ctx.settings.get_bool("rancher_cleanup"):
+        return None
+    from ..executor.base import outputs_from_tfstate
+    from ..rancher.client import RancherClient
+    from ..state import MANAGER_KEY
+
+    raw = backend.read_tfstate(state.name)
+    mgr = outputs_from_tfstate(raw, MANAGER_KEY)
+    cid = outputs_from_tfstate(raw, cluster_key).get("rancher_cluster_id")
+    if not mgr.get("rancher_url") or not cid:
+        return None
+
+    def _cleanup():
+        client = RancherClient(mgr["rancher_url"], mgr.get("rancher_access_key", ""),
+                               mgr.get("rancher_secret_key", ""))
+        gone = [n["id"] for n in client.nodes(cid)
+                if hostname in (n.get("hostname"), n.get("nodeName"), n.get("requestedHostname"))]
+        for nid in gone:
+            client.delete_node(nid)
+        ctx.echo(f"Removed Rancher node {', '.join(gone)} ({hostname})" if gone else
+                 f"No Rancher node named {hostname} in cluster {cid}")
+
+    return _cleanup
 
 
 def _rancher_cleanup_info(ctx: Context, backend: Backend, state, cluster_key: str):
