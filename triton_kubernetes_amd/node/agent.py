@@ -505,7 +505,7 @@ class NodeAgent:
         memory would otherwise overlap (and slow) the short burn-in kernels.  A previous
         gate's communicator teardown is NOT waited for (TK_QUIESCE_TEARDOWNS=1 restores
         that): its ~0.5 s is spent inside ncclCommDestroy, and burn-ins measured next to
-        it read the same as after it (profiles/round2/teardown_overlap.jsonl); a one-off
+        it read the same as after it (round 2 A/B, in the git history of profiles/round2); a one-off
         low reading is re-measured by the burn-in itself (ops/probe.py:REMEASURE)."""
         if self.burnin_override is not None or self.topology_override is not None or not self.devices:
             return

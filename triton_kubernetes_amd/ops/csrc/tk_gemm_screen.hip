@@ -22,7 +22,7 @@
 //    1.41 / 1.54 PF at 4096^3 / 8192^3 on random data, MFMA pipe 77 % busy;
 //  * k_gemm_bt (schedule 0, "single-barrier", kept for A/B): whole [256][64] tiles in two
 //    buffers, one barrier per K-step, every wave reads then issues 64 MFMAs in lockstep —
-//    1.20 / 1.27 PF, MFMA pipe 61.5 % busy (profiles/round1_gemm_pmc.md);
+//    1.20 / 1.27 PF, MFMA pipe 61.5 % busy (profiles/round1/round1_gemm_pmc.md);
 //  * the LDS image is XOR-swizzled by 16-byte chunk (chunk ^ ((row >> 1) & 7)): the
 //    swizzle is applied to the per-lane GLOBAL source address (the LDS-DMA destination
 //    is lane-linear), so the 16 lanes of a ds_read_b128 group read 16 distinct bank
@@ -229,7 +229,7 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
   // the barrier each thread waits for its copy of step t+1 only (later ones keep flying),
   // so the barrier also publishes step t+1 to every wave.
   // (A variant with two wave groups staggered by one barrier slot measured the same at
-  // BK 64: 1162 / 1224 vs 1155 / 1238 TF at 4096^3 / 8192^3 — profiles/round1_gemm_pmc.md.)
+  // BK 64: 1162 / 1224 vs 1155 / 1238 TF at 4096^3 / 8192^3 — profiles/round1/round1_gemm_pmc.md.)
   for (int t = 0; t < nk; ++t) {
     read_frags(t);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -314,7 +314,7 @@ __global__ __launch_bounds__(THREADS) void k_gemm_bt(const __bf16* __restrict__ 
 // = 8 copies may stay in flight), Pb(t) retires A0/B0/B1 of t+1 (3 younger: vmcnt(6)); the
 // last K-tiles wait with vmcnt(0), where fewer younger copies exist.
 // (Variants measured on the way — four phases of 16 MFMAs, other wait placements, B1 refilled
-// early, no stagger — and their counters: profiles/round1_gemm_pmc.md.)
+// early, no stagger — and their counters: profiles/round1/round1_gemm_pmc.md.)
 namespace p8 {
 constexpr int KT_BYTES = 128, HROWS = 128;       // bytes of a row per K-tile; rows per half-tile
 constexpr int HBYTES = HROWS * KT_BYTES;         // 16 KiB
@@ -391,7 +391,7 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const void* __restrict__ A, c
   // for fp8 the MFMA's k positions are a permutation of the row's bytes, which leaves the
   // dot product unchanged.  The natural fp8 map (chunks 2 fq, 2 fq + 1) would put the two
   // lane quarters of a ds_read_b128 group on the same banks: 50 M conflict cycles per
-  // 8192^3 (profiles/round1_gemm_pmc.md); this one is conflict-free, as for bf16.
+  // 8192^3 (profiles/round1/round1_gemm_pmc.md); this one is conflict-free, as for bf16.
   u32x4 a[4][2], b[2][2][2];
   auto ld_frag = [&](const char* img, int r, u32x4* f) {
     f[0] = chunk(img, r, fq);
