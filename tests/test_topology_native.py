@@ -127,13 +127,31 @@ def test_executable_sysfs_root(tmp_path, native_ok):
     assert empty.returncode == 2 and "no KFD topology" in empty.stderr
 
 
-def add_rdma(root, nics):
+# a RoCE port's GID table as mlx5 fills it: link-local IPv6 as RoCE v1 / v2 (0, 1), then
+# the interface's IPv4 address, IPv4-mapped, as v1 / v2 (2, 3); empty slots read as zeros
+ROCE_GIDS = [("IB/RoCE v1", "fe80:0000:0000:0000:0a00:00ff:fe00:0001"),
+             ("RoCE v2", "fe80:0000:0000:0000:0a00:00ff:fe00:0001"),
+             ("IB/RoCE v1", "0000:0000:0000:0000:0000:ffff:0a00:0001"),
+             ("RoCE v2", "0000:0000:0000:0000:0000:ffff:0a00:0001"),
+             (None, "0000:0000:0000:0000:0000:0000:0000:0000")]
+
+
+def add_gids(port_dir, table):
+    for i, (kind, gid) in enumerate(table):
+        _write(f"{port_dir}/gids/{i}", gid + "\n")
+        if kind is not None:
+            _write(f"{port_dir}/gid_attrs/types/{i}", kind + "\n")
+
+
+def add_rdma(root, nics, gids=ROCE_GIDS):
     """RDMA devices under sys/class/infiniband: (name, state, link_layer, rate, netdev, numa)."""
     for name, state, layer, rate, netdev, numa in nics:
         dev = os.path.join(root, "sys/class/infiniband", name)
         _write(f"{dev}/ports/1/state", f"{state}\n")
         _write(f"{dev}/ports/1/link_layer", f"{layer}\n")
         _write(f"{dev}/ports/1/rate", f"{rate}\n")
+        if layer == "Ethernet" and gids:
+            add_gids(f"{dev}/ports/1", gids)
         pci = os.path.join(root, "sys/devices/pci0000:00", f"0000:{0x1a + len(name):02x}:00.0")
         _write(f"{pci}/numa_node", f"{numa}\n")
         os.makedirs(f"{pci}/net/{netdev}", exist_ok=True)
@@ -159,10 +177,33 @@ def test_rdma_nics_python_reader_labels_and_rccl_env(tmp_path):
     assert labels["amd.com/rdma.count"] == "2"
     assert labels["amd.com/rdma.link-layer"] == "ethernet" and labels["amd.com/rdma.rate-gbps"] == "200"
     env = site_env_from_topology({"nics": nics})
+    assert nics[0]["roce_v2_gid_index"] == 3 and "roce_v2_gid_index" not in nics[1]  # a DOWN port: not read
     assert env == {"NCCL_IB_HCA": "=mlx5_0:1,mlx5_2:1", "NCCL_IB_GID_INDEX": "3"}
     assert site_env_from_topology({"nics": []}) == {}
     ib = [dict(n, link_layer="InfiniBand") for n in nics]
     assert site_env_from_topology({"nics": ib}) == {"NCCL_IB_HCA": "=mlx5_0:1,mlx5_2:1"}
+
+
+@pytest.mark.parametrize("case", ["ipv6-only", "differ", "no-gids"])
+def test_roce_gid_discovery(tmp_path, native_ok, case):
+    """The RoCE v2 GID index is read from the ports' GID tables, not assumed: IPv4-mapped
+    first, else IPv6; NCCL_IB_GID_INDEX only when every RoCE port agrees (else RCCL picks
+    per port itself)."""
+    from triton_kubernetes_amd.parallel.rccl_env import site_env_from_topology
+
+    gids = {"ipv6-only": ROCE_GIDS[:2], "differ": ROCE_GIDS, "no-gids": None}[case]
+    root = add_rdma(make_tree(str(tmp_path), ngpu=2), RDMA, gids=gids)
+    if case == "differ":  # mlx5_2's IPv4 address sits at another index
+        add_gids(os.path.join(root, "sys/class/infiniband/mlx5_2/ports/1"),
+                 ROCE_GIDS[:2] + [(None, "0" * 4 + ":0000" * 7)] * 3 + ROCE_GIDS[2:4])
+    doc = topo.native_topology("sysfs", root)
+    assert doc["nics"] == topo.rdma_nics(root)
+    want = {"ipv6-only": [1, 1], "differ": [3, 6], "no-gids": [None, None]}[case]
+    active = [n for n in doc["nics"] if n["active"]]
+    assert [n.get("roce_v2_gid_index") for n in active] == want
+    env = topo.native_rccl_env(root)
+    assert env == site_env_from_topology(doc)
+    assert env.get("NCCL_IB_GID_INDEX") == ("1" if case == "ipv6-only" else None)
 
 
 def test_rdma_native_matches_python(tmp_path, native_ok):

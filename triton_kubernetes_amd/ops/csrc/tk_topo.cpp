@@ -93,6 +93,7 @@ struct NicInfo {
   std::string name, link_layer, netdev, bdf;
   int port = 0;             // first ACTIVE port (0: none active)
   uint64_t rate_gbps = 0;   // of that port
+  int gid_index = -1;       // RoCE v2 GID of that port (IPv4-mapped first); -1: none / not RoCE
   int64_t numa_node = -1;
 };
 
@@ -453,6 +454,22 @@ Topology collect_sysfs(const std::string& root) {
   return t;
 }
 
+// The RoCE v2 GID index of a port (ports/<n>/gid_attrs/types/<i> == "RoCE v2" and a
+// non-zero ports/<n>/gids/<i>), the first IPv4-mapped one (::ffff:a.b.c.d) if any, else the
+// first IPv6 one; -1 when the port has none (InfiniBand, or no address configured).
+int roce_v2_gid(const std::string& port_dir) {
+  int v6 = -1;
+  for (int i : numeric_entries(port_dir + "/gid_attrs/types")) {
+    std::string type, gid;
+    if (!read_file(port_dir + "/gid_attrs/types/" + std::to_string(i), &type) || type != "RoCE v2") continue;
+    if (!read_file(port_dir + "/gids/" + std::to_string(i), &gid)) continue;
+    if (gid.find_first_not_of("0:") == std::string::npos) continue;  // an empty slot
+    if (gid.rfind("0000:0000:0000:0000:0000:ffff:", 0) == 0) return i;
+    if (v6 < 0) v6 = i;
+  }
+  return v6;
+}
+
 // RDMA NICs: /sys/class/infiniband/<dev>/ports/<n>/{state,link_layer,rate}, the netdev
 // under <dev>/device/net and the PCI function <dev>/device points at.  Same for both
 // collectors (amd_smi does not describe NICs).  Mirrored in ops/topo.py:rdma_nics.
@@ -480,6 +497,7 @@ std::vector<NicInfo> collect_nics(const std::string& root) {
       nic.port = port;
       if (read_file(pd + "/link_layer", &s)) nic.link_layer = s;
       if (read_file(pd + "/rate", &s)) nic.rate_gbps = strtoull(s.c_str(), nullptr, 10);
+      nic.gid_index = roce_v2_gid(pd);
       break;
     }
     if (read_file(dev + "/device/numa_node", &s)) nic.numa_node = atoll(s.c_str());
@@ -561,6 +579,7 @@ std::string render_json(const Topology& t) {
             n.rate_gbps);
     if (!n.netdev.empty()) appendf(o, ",\"netdev\":\"%s\"", esc(n.netdev).c_str());
     if (!n.bdf.empty()) appendf(o, ",\"bdf\":\"%s\"", esc(n.bdf).c_str());
+    if (n.gid_index >= 0) appendf(o, ",\"roce_v2_gid_index\":%d", n.gid_index);
     if (n.numa_node >= 0) appendf(o, ",\"numa_node\":%" PRId64, n.numa_node);
     o += "}";
   }
@@ -782,18 +801,20 @@ std::string render_labels(const Topology& t) {
 // RCCL/NCCL settings for the inter-node fabric, one KEY="value" line each (sourced after
 // the static /etc/rccl/rccl.env defaults; explicit per-node overrides come later and win).
 // Mirrored in parallel/rccl_env.py:site_env_from_topology.
+// NCCL_IB_GID_INDEX is set only when every active RoCE port has its RoCE v2 GID at the
+// same index; otherwise RCCL picks one per port itself (RoCE v2, IPv4 first, by default).
 std::string render_rccl_env(const Topology& t) {
   std::string hca;
-  bool roce = false;
+  std::set<int> gids;
   for (const auto& n : t.nics) {
     if (n.port <= 0) continue;
     hca += (hca.empty() ? "" : ",") + n.name + ":" + std::to_string(n.port);
-    roce = roce || lower(n.link_layer) == "ethernet";
+    if (lower(n.link_layer) == "ethernet") gids.insert(n.gid_index);
   }
   std::string o;
   if (hca.empty()) return o;
   o += "NCCL_IB_HCA=\"=" + hca + "\"\n";  // leading '=': exact device names, not prefixes
-  if (roce) o += "NCCL_IB_GID_INDEX=\"3\"\n";  // RoCE v2 GID
+  if (gids.size() == 1 && *gids.begin() >= 0) o += "NCCL_IB_GID_INDEX=\"" + std::to_string(*gids.begin()) + "\"\n";
   return o;
 }
 

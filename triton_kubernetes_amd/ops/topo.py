@@ -198,6 +198,27 @@ def _read_text(path: str) -> Optional[str]:
         return None
 
 
+def roce_v2_gid(port_dir: str) -> int:
+    """The port's RoCE v2 GID index: the first IPv4-mapped one, else the first IPv6 one,
+    -1 when it has none (mirror of ``csrc/tk_topo.cpp:roce_v2_gid``)."""
+    try:
+        idx = sorted(int(i) for i in os.listdir(os.path.join(port_dir, "gid_attrs", "types")) if i.isdigit())
+    except OSError:
+        return -1
+    v6 = -1
+    for i in idx:
+        if _read_text(os.path.join(port_dir, "gid_attrs", "types", str(i))) != "RoCE v2":
+            continue
+        gid = _read_text(os.path.join(port_dir, "gids", str(i))) or ""
+        if not gid.strip("0:"):
+            continue  # an empty slot
+        if gid.startswith("0000:0000:0000:0000:0000:ffff:"):
+            return i
+        if v6 < 0:
+            v6 = i
+    return v6
+
+
 def rdma_nics(root: str = "") -> List[Dict[str, Any]]:
     """RDMA devices under ``<root>/sys/class/infiniband`` (the inter-node RCCL fabric).
 
@@ -228,6 +249,9 @@ def rdma_nics(root: str = "") -> List[Dict[str, Any]]:
             nic.update(port=port, active=True, link_layer=_read_text(os.path.join(pd, "link_layer")) or "")
             rate = (_read_text(os.path.join(pd, "rate")) or "").split()
             nic["rate_gbps"] = int(rate[0]) if rate and rate[0].isdigit() else 0
+            gid = roce_v2_gid(pd)
+            if gid >= 0:
+                nic["roce_v2_gid_index"] = gid
             break
         try:
             nets = sorted(n for n in os.listdir(os.path.join(dev, "device", "net")) if not n.startswith("."))

@@ -8,7 +8,8 @@ links of roughly 153 GB/s, so ring collectives are per-link bound and RCCL
 needs no socket/IB settings for it.  Inter-node traffic goes over RoCE/IB NICs
 whose names are site specific: the node's active RDMA ports are discovered on the
 host (:func:`site_env_from_topology`, ``amdgpu-topo-labeller --rccl-env``) and written
-as ``NCCL_IB_HCA`` (+ the RoCE v2 GID index); ``rccl_env`` overrides in the node
+as ``NCCL_IB_HCA`` (+ the ports' RoCE v2 GID index, read from ``gid_attrs/types``);
+``rccl_env`` overrides in the node
 config win over both the defaults and the discovered values.
 """
 
@@ -34,14 +35,17 @@ SITE_KEYS = ("NCCL_SOCKET_IFNAME", "NCCL_IB_HCA", "NCCL_IB_GID_INDEX", "NCCL_NET
 def site_env_from_topology(topology: Mapping[str, Any]) -> Dict[str, str]:
     """Inter-node settings derived from the node's RDMA NICs (``topology["nics"]``, as
     discovered by the labeller): every active port in ``NCCL_IB_HCA`` (exact names), and
-    the RoCE v2 GID index when any of them is Ethernet.  Mirror of
+    the RoCE v2 GID index the Ethernet ports share (``roce_v2_gid_index``).  Mirror of
     ``csrc/tk_topo.cpp:render_rccl_env``; explicit per-node ``rccl_env`` keys override it."""
     active = [n for n in topology.get("nics", []) or [] if n.get("port", 0) > 0]
     if not active:
         return {}
     env = {"NCCL_IB_HCA": "=" + ",".join(f"{n['name']}:{n['port']}" for n in active)}
-    if any(str(n.get("link_layer", "")).lower() == "ethernet" for n in active):
-        env["NCCL_IB_GID_INDEX"] = "3"
+    # the RoCE v2 GID index, when every active RoCE port has it at the same index; else
+    # RCCL picks one per port itself (RoCE v2, IPv4 first, by default)
+    gids = {int(n.get("roce_v2_gid_index", -1)) for n in active if str(n.get("link_layer", "")).lower() == "ethernet"}
+    if len(gids) == 1 and min(gids) >= 0:
+        env["NCCL_IB_GID_INDEX"] = str(min(gids))
     return env
 
 
