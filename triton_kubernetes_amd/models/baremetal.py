@@ -197,6 +197,10 @@ def _mi355x_fields(ctx: Context) -> Dict:
         out["gpu_health"] = policy
         out["gpu_max_uncorrectable_ecc"] = str(max_ue)
         out["gpu_max_retired_pages"] = "auto" if max_bad < 0 else str(max_bad)
+    if s.is_set("gpu_host_tuning"):  # NUMA balancing / IOMMU checks (node/hosttune.py)
+        from ..node.hosttune import policy_of as tuning_policy
+
+        out["gpu_host_tuning"] = tuning_policy({"gpu_host_tuning": s.get_string("gpu_host_tuning")})
     if s.is_set("rccl_slim"):  # opt-in verified single-target RCCL (terraform/scripts.py)
         slim = s.get_string("rccl_slim").lower()
         if slim in ("true", "yes", "1"):

@@ -334,6 +334,17 @@ class NodeAgent:
                 if problem:
                     raise StepFailed(step.name, problem)
                 out["partition"] = {"compute": want[0], "memory": want[1]}
+            tuning = step.params.get("host_tuning", "off")
+            if tuning != "off":
+                # NUMA auto-balancing and IOMMU mode (node/hosttune.py): labels, warnings
+                from . import hosttune
+
+                f = hosttune.facts(self.root)
+                ctx["labels"].update(hosttune.labels(f))
+                bad = hosttune.problems(f)
+                if bad and tuning == "enforce":
+                    raise StepFailed(step.name, "host tuning: " + "; ".join(bad))
+                out["host"] = dict(f, warnings=bad)
             return out
         if a == "gpu_labels":
             fut = ctx.get("topology_future")

@@ -20,7 +20,8 @@ Step catalogue (``action`` ids):
 ``hostname``        ``hostnamectl set-hostname`` (S5)
 ``registry_login``  RKE1: ``docker login`` when registry credentials are given (S5);
                     RKE2 nodes get registries from the cluster's ``rkeConfig``
-``gpu_preflight``   MI355X: amdgpu loaded, ``/dev/kfd`` + ``/dev/dri`` present, N GPUs
+``gpu_preflight``   MI355X: amdgpu loaded, ``/dev/kfd`` + ``/dev/dri`` present, N GPUs, the
+                    partition modes, host tuning (NUMA balancing, IOMMU mode: ``node/hosttune.py``)
 ``gpu_labels``      MI355X: N1 topology labeller -> node labels file
 ``gpu_burnin``      MI355X: HBM / MFMA / memtest probes per GPU
 ``gpu_health``      MI355X: RAS verdict (uncorrectable ECC, retired VRAM pages) under the
@@ -205,6 +206,10 @@ fi""", {"install_url": install_url}))
         ngpu = physical * partitions_per_gpu(cpart)  # logical GPUs: amd.com/gpu units, RCCL ranks
         burnin = cfg.get("gpu_burnin", "quick")
         env = dict(cfg.get("rccl_env") or {})
+        from .hosttune import policy_of as tuning_policy
+        from .hosttune import shell_check as host_tuning_check
+
+        tuning = tuning_policy(cfg)
         plan.gpu = {"product": cfg.get("gpu_product", "MI355X"), "count": ngpu, "burnin": burnin,
                     "physical": physical, "compute_partition": cpart, "memory_partition": mpart}
         plan.steps.append(Step("gpu_preflight", "gpu_preflight", f"""
@@ -223,15 +228,16 @@ for f in /sys/class/drm/renderD*/device/current_compute_partition /sys/class/drm
   esac
 done
 sudo usermod -aG video,render "$(id -un)" || true
-sudo rm -f {BURNIN_LABEL_FILE} {TAINT_FILE}""", {"count": ngpu, "compute_partition": cpart, "memory_partition": mpart},
-                               gpu=True))
+sudo rm -f {BURNIN_LABEL_FILE} {TAINT_FILE}
+{host_tuning_check(tuning, BURNIN_LABEL_FILE)}""", {"count": ngpu, "compute_partition": cpart, "memory_partition": mpart,
+                                               "host_tuning": tuning}, gpu=True))
         # burn-in before labels: the agent discovers the topology concurrently
         # with the burn-in kernels and only joins it at the labels step
         if burnin != "off":
             plan.steps.append(Step("gpu_burnin", "gpu_burnin", f"""
 sudo mkdir -p /etc/triton-kubernetes
 {TOOLS_DIR}/gpu-burnin --all --level {_q(burnin)} --compute-partition {cpart} --memory-partition {mpart} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
-sudo install -m 0644 /tmp/tk-burnin-labels {BURNIN_LABEL_FILE}""",
+sudo tee -a {BURNIN_LABEL_FILE} < /tmp/tk-burnin-labels >/dev/null""",
                                    {"level": burnin, "compute_partition": cpart, "memory_partition": mpart},
                                    gpu=True))
         if physical > 1 and cpart == "spx":  # links are a whole GPU's (a partition has no own)

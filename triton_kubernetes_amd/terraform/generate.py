@@ -1236,6 +1236,9 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("gpu_link_min_gbps", "38",
             "fail the node when a GPU pair's kernel-driven peer read is below this many GB/s (absolute floor: "
             "half of one xGMI link's ~76.8 GB/s one way)"),
+        Var("gpu_host_tuning", "warn",
+            "host settings check (NUMA auto-balancing off, IOMMU passthrough): warn = labels and warnings; "
+            "enforce = fail the node; off = not checked"),
         Var("gpu_health", "fail",
             "GPU health policy (RAS counters): fail = an unhealthy GPU fails the node; taint = the node joins "
             "tainted amd.com/gpu-health=unhealthy:NoSchedule (no GPU pods); off = not checked"),
@@ -1288,6 +1291,7 @@ resource "terraform_data" "install_mi355x_node" {{
       gpu_partitions                     = lookup({{ spx = 1, dpx = 2, qpx = 4, cpx = 8 }}, var.gpu_compute_partition, 1)
       rccl_slim                          = var.rccl_slim
       gpu_health                         = var.gpu_health
+      gpu_host_tuning                    = var.gpu_host_tuning
       gpu_max_uncorrectable_ecc          = var.gpu_max_uncorrectable_ecc
       gpu_max_retired_pages              = var.gpu_max_retired_pages
     }})]

@@ -169,6 +169,12 @@ variable "gpu_link_min_gbps" {
   default     = "38"
 }
 
+variable "gpu_host_tuning" {
+  description = "host settings check (NUMA auto-balancing off, IOMMU passthrough): warn = labels and warnings; enforce = fail the node; off = not checked"
+  type        = string
+  default     = "warn"
+}
+
 variable "gpu_health" {
   description = "GPU health policy (RAS counters): fail = an unhealthy GPU fails the node; taint = the node joins tainted amd.com/gpu-health=unhealthy:NoSchedule (no GPU pods); off = not checked"
   type        = string

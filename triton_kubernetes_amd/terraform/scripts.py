@@ -7,6 +7,8 @@ templates, and they fix the reference quirks Q10
 (hard-coded ``/home/ubuntu``, ``/etc/fstab`` overwritten with ``tee``).
 """
 
+from ..node.hosttune import shell_check as _host_tuning_check
+
 # download, verify (when docker_install_sha256 is set), run — no `curl | sh` of an unchecked stream
 DOCKER_INSTALL = r"""if ! command -v docker >/dev/null 2>&1; then
   curl -fsSL -o /tmp/tk-install-docker.sh '${docker_engine_install_url}'
@@ -417,9 +419,13 @@ fi
 $T/amdgpu-topo-labeller | sudo tee /etc/triton-kubernetes/gpu-topology.json >/dev/null
 $T/amdgpu-topo-labeller --labels | sudo tee /etc/triton-kubernetes/gpu-labels >/dev/null
 sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels /etc/triton-kubernetes/gpu-taints
+%{ if gpu_host_tuning != "off" ~}
+""" + _host_tuning_check(
+    "warn", "/etc/triton-kubernetes/gpu-burnin-labels", fail='${gpu_host_tuning == "enforce" ? "exit 1" : "true"}') + r"""
+%{ endif ~}
 %{ if gpu_burnin != "off" ~}
 $T/gpu-burnin --all --level '${gpu_burnin}' --compute-partition ${gpu_compute_partition} --memory-partition ${gpu_memory_partition} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
-sudo install -m 0644 /tmp/tk-burnin-labels /etc/triton-kubernetes/gpu-burnin-labels
+sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels < /tmp/tk-burnin-labels >/dev/null
 %{ endif ~}
 %{ if gpu_health != "off" ~}
 # GPU health (RAS): exit 3 = an unhealthy GPU; fail the node or join it tainted
