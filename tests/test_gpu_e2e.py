@@ -239,8 +239,10 @@ def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch, dist):
         cfg = {"hostname": "gpu-exec-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
                "gpu_burnin": "quick", "rccl_env": {"NCCL_DEBUG": "WARN"}, "k8s_distribution": dist}
         server = fake.url if dist == "rke2" else "https://rancher.example"  # loopback: the default allow-list
-        plan = build_host_plan(cfg, server, "regtok123", "cafe0123", mi355x=True)
+        cid, token, checksum = fake.registration("exec", dist) if dist == "rke2" else ("", "regtok123", "cafe0123")
+        plan = build_host_plan(cfg, server, token, checksum, mi355x=True)
         res = AgentTransport(token="exec-token-123456").run_plan(HostRef("agent+" + url), plan)
+        joined = fake.k8s_nodes(cid) if dist == "rke2" else []
     finally:
         agent.stop()
         fake.stop()
@@ -252,7 +254,11 @@ def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch, dist):
     if dist == "rke2":
         assert "docker" not in calls
         assert f"system-agent-install --server {fake.url} --label cattle.io/os=linux" in calls
-        assert "--ca-checksum cafe0123 --node-name gpu-exec-1 --worker --label amd.com/" in calls
+        assert f"--ca-checksum {checksum} --node-name gpu-exec-1 --worker --label amd.com/" in calls
+        # the installer checked the CA and registered the node, with the GPU labels
+        (node,) = joined
+        assert node["metadata"]["name"] == "gpu-exec-1"
+        assert node["metadata"]["labels"]["amd.com/gpu.product-name"] == "MI355X"
     else:
         assert "docker version" in calls and "--ca-checksum cafe0123 --worker --label amd.com/" in calls
     assert "--label amd.com/gpu.count=1" in calls

@@ -248,19 +248,29 @@ def test_exec_mode_agent_runs_the_servers_installer(tmp_path, monkeypatch):
     monkeypatch.setenv("PATH", f"{bindir}:/usr/bin:/bin")
     monkeypatch.setenv("TK_FAKE_SYSTEM_AGENT_LOG", str(log))
     with FakeRancher() as fake:
+        cid, token, checksum = fake.registration()
         agent = NodeAgent(name="x", mode="exec", token=TOKEN, root=str(tmp_path / "root"))
         url = agent.serve()
         try:
             plan = build_host_plan({"hostname": "w-1", "rancher_host_labels": {"worker": "true"}}, fake.url,
-                                   "regtok", "cafe")
+                                   token, checksum)
             res = AgentTransport(token=TOKEN).run_plan(HostRef("agent+" + url), plan)
+            # the installer verified the CA checksum and registered the node as a system agent
+            (node,) = fake.state.cluster_nodes[cid].values()
+            assert node["hostname"] == "w-1" and node["agentKind"] == "system-agent" and node["roles"]["worker"]
+            # a wrong checksum stops the installer before it registers anything
+            bad = build_host_plan({"hostname": "w-2", "rancher_host_labels": {"worker": "true"}}, fake.url, token,
+                                  "0" * 64)
+            res_bad = AgentTransport(token=TOKEN).run_plan(HostRef("agent+" + url), bad)
+            assert not res_bad["ok"] and "does not match --ca-checksum" in res_bad["error"]
+            assert len(fake.state.cluster_nodes[cid]) == 1
         finally:
             agent.stop()
     assert res["ok"], res
     calls = log.read_text()
     assert "hostnamectl set-hostname w-1" in calls
-    assert (f"system-agent-install --server {fake.url} --label cattle.io/os=linux --token regtok "
-            "--ca-checksum cafe --node-name w-1 --worker") in calls
+    assert (f"system-agent-install --server {fake.url} --label cattle.io/os=linux --token {token} "
+            f"--ca-checksum {checksum} --node-name w-1 --worker") in calls
 
 
 def test_exec_join_without_a_ca_checksum(tmp_path, monkeypatch):
@@ -277,17 +287,19 @@ def test_exec_join_without_a_ca_checksum(tmp_path, monkeypatch):
     monkeypatch.setenv("PATH", f"{bindir}:/usr/bin:/bin")
     monkeypatch.setenv("TK_FAKE_SYSTEM_AGENT_LOG", str(log))
     with FakeRancher() as fake:
+        cid, token, _ = fake.registration()
         agent = NodeAgent(name="x", mode="exec", token=TOKEN, root=str(tmp_path / "root"))
         url = agent.serve()
         try:
             plan = build_host_plan({"hostname": "w-1", "rancher_host_labels": {"worker": "true"}}, fake.url,
-                                   "regtok", "")
+                                   token, "")
             res = AgentTransport(token=TOKEN).run_plan(HostRef("agent+" + url), plan)
         finally:
             agent.stop()
+        assert [n["hostname"] for n in fake.state.cluster_nodes[cid].values()] == ["w-1"]
     assert res["ok"], res
     calls = log.read_text()
-    assert "--token regtok --node-name w-1 --worker" in calls and "--ca-checksum" not in calls
+    assert f"--token {token} --node-name w-1 --worker" in calls and "--ca-checksum" not in calls
 
 
 def _https_rancher(tmp_path, cacerts_body: bytes):

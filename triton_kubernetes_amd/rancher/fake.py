@@ -79,9 +79,37 @@ from ..utils.httpserver import Server as HTTPServer
 
 FAKE_CACERTS = "-----BEGIN CERTIFICATE-----\nMIIFAKECERTIFICATEFORTESTS\n-----END CERTIFICATE-----"
 # what GET /system-agent-install.sh serves here: records its arguments (tests run it)
-SYSTEM_AGENT_INSTALL_SCRIPT = """#!/bin/sh
-# fake rancher-system-agent installer
+SYSTEM_AGENT_INSTALL_SCRIPT = r"""#!/bin/sh
+# fake rancher-system-agent installer: takes the flags the real system-agent-install.sh
+# takes, checks --ca-checksum the way it does (sha256 of GET <server>/cacerts), then
+# registers the node with this server -- what the installed rancher-system-agent does
 echo "system-agent-install $*" >> "${TK_FAKE_SYSTEM_AGENT_LOG:-/dev/null}"
+server=""; token=""; checksum=""; name=""; etcd=false; cp=false; worker=false; labels=""; taints=""
+while [ $# -gt 0 ]; do
+  case "$1" in
+    --server) server=$2; shift 2 ;;
+    --token) token=$2; shift 2 ;;
+    --ca-checksum) checksum=$2; shift 2 ;;
+    --node-name) name=$2; shift 2 ;;
+    --label) labels="$labels${labels:+,}\"${2%%=*}\":\"${2#*=}\""; shift 2 ;;
+    --taints) _r=${2#*=}; taints="$taints${taints:+,}{\"key\":\"${2%%=*}\",\"value\":\"${_r%%:*}\",\"effect\":\"${_r#*:}\"}"; shift 2 ;;
+    --etcd) etcd=true; shift ;;
+    --controlplane) cp=true; shift ;;
+    --worker) worker=true; shift ;;
+    *) echo "system-agent-install: unknown option $1" >&2; exit 1 ;;
+  esac
+done
+[ -n "$server" ] && [ -n "$token" ] || { echo "system-agent-install: --server and --token are required" >&2; exit 1; }
+if [ -n "$checksum" ]; then
+  got=$(curl -fsSk "$server/cacerts" | sha256sum | cut -d' ' -f1)
+  [ "$got" = "$checksum" ] || { echo "system-agent-install: configured cacerts checksum ($got) does not match --ca-checksum ($checksum)" >&2; exit 1; }
+fi
+[ -n "$name" ] || name=$(hostname)
+params=$(printf '{"node":{"requestedHostname":"%s","etcd":%s,"controlPlane":%s,"worker":%s,"labels":{%s},"taints":[%s]}}' \
+  "$name" $etcd $cp $worker "$labels" "$taints" | base64 | tr -d '\n')
+curl -fsSk -o /dev/null -X POST -H "X-API-Tunnel-Token: $token" -H "X-API-Tunnel-Params: $params" \
+  -H "X-Cattle-Agent-Kind: system-agent" -d '{}' "$server/v3/connect/register" \
+  || { echo "system-agent-install: registration with $server failed" >&2; exit 1; }
 """
 
 
@@ -268,8 +296,10 @@ class FakeRancher:
         return max(created, n.get("ready_at") or 0.0) + self.state.device_plugin_seconds
 
     def _gpu_allocatable(self, cid: str, n: Dict[str, Any], now: float) -> Optional[int]:
-        """GPUs a running, registered device-plugin pod advertises on ``n`` (None: none)."""
-        devices = int(n["capacity"].get("amd.com/gpu", 0) or 0)
+        """GPUs a running, registered device-plugin pod advertises on ``n`` (None: none):
+        the devices the node agent reported, else what its labeller counted (a node joined
+        through the installer reports only labels)."""
+        devices = int(n["capacity"].get("amd.com/gpu", 0) or n["labels"].get("amd.com/gpu.logical-count", 0) or 0)
         for key, ds in self._daemonsets(cid):
             if self._is_gpu_plugin(ds) and self._runs_on(ds, n, key) and now >= self._plugin_ready_at(cid, key, n):
                 return devices
@@ -586,6 +616,23 @@ class FakeRancher:
         with st.mu:
             obj["status"]["ready"] = (st.clusters.get(cid) or {}).get("state") == "active"
             return 200, json.loads(json.dumps(obj))
+
+    def registration(self, name: str = "test", distribution: str = "rke2") -> Tuple[str, str, str]:
+        """``(cluster id, registration token, ca checksum)`` of a new cluster: what an admin
+        copies out of the UI's registration command (tests of the node-side join)."""
+        from .client import ca_checksum
+
+        st = self.state
+        with st.mu:
+            cid = f"c-m-{uuid.uuid4().hex[:8]}" if distribution == "rke2" else f"c-{uuid.uuid4().hex[:5]}"
+            st.clusters[cid] = {"id": cid, "name": name, "state": "provisioning", "transitioning": "yes",
+                                "driver": "rke2" if distribution == "rke2" else "rancherKubernetesEngine",
+                                "created": time.time(), "version": {"gitVersion": ""}}
+            st.cluster_nodes[cid] = {}
+            st.unsettled.add(cid)
+            tok = secrets.token_hex(16)
+            st.reg_tokens[tok] = {"id": f"{cid}:default-token", "clusterId": cid, "ready": True}
+            return cid, tok, ca_checksum(st.settings.get("cacerts", ""))
 
     def registry_auth(self, secret: str, namespace: str = FLEET_NAMESPACE) -> Dict[str, str]:
         """Decoded ``username``/``password`` of a registry basic-auth Secret."""
