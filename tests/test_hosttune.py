@@ -42,9 +42,8 @@ def test_facts_and_shell_twin(tmp_path, args, want):
     assert hosttune.labels(f) == {"amd.com/host.numa-balancing": want["numa_balancing"],
                                   "amd.com/host.iommu": want["iommu"]}
     # the shell check over the same tree: same labels, warnings, enforce exits 1
-    labels = tmp_path / "labels"
     for policy in ("warn", "enforce"):
-        labels.write_text("")
+        labels = tmp_path / policy / "etc" / "labels"  # its directory does not exist yet
         body = hosttune.shell_check(policy, str(labels)).replace("sudo ", "")
         for path in ("/proc/sys/kernel/numa_balancing", "/proc/cmdline", "/sys/class/iommu"):
             body = body.replace(path, root + path)

@@ -91,6 +91,7 @@ if grep -qwE '(amd_)?iommu=pt' /proc/cmdline; then _tk_io=pt
 elif grep -qwE '(amd_)?iommu=off' /proc/cmdline; then _tk_io=off
 elif [ -n "$(ls /sys/class/iommu 2>/dev/null)" ]; then _tk_io=translated
 else _tk_io=off; fi
+sudo mkdir -p "$(dirname {label_file})"
 printf 'amd.com/host.numa-balancing=%s\\namd.com/host.iommu=%s\\n' $_tk_nb $_tk_io | sudo tee -a {label_file} >/dev/null
 _tk_bad=0
 [ $_tk_nb = on ] && {{ echo 'host tuning: kernel.numa_balancing is on: set it to 0 (sysctl kernel.numa_balancing=0)' >&2; _tk_bad=1; }}
