@@ -411,3 +411,34 @@ def test_gpu_health_cli_on_the_box(capsys):
         doc = json.loads(capsys.readouterr().out)
         assert rc in (0, 3) and (rc == 0) == (doc["status"] == "healthy")
         assert doc["gpus"] and doc["gpus"][0]["bad_page_limit"] > 0
+
+
+def test_get_nodes_shows_gpu_state(tmp_path):
+    """``get nodes``: the cluster's nodes through Rancher's Kubernetes API, with the MI355X
+    columns (GPUs allocatable / counted, product, partition, burn-in, xGMI, health)."""
+    from triton_kubernetes_amd.cli.main import dispatch
+
+    from helpers import make_ctx
+
+    fake, agents, backend, ctx, new_cluster = _create(tmp_path, "taint")
+    try:
+        new_cluster(ctx, backend)
+        base = {"agent_token": "health-token-123456", "cluster_manager": "mgr", "cluster_name": "dev"}
+        table = make_ctx(base)
+        assert dispatch(table, backend, "get", "nodes") == 0
+        lines = [ln for ln in table.out.getvalue().splitlines() if ln and not ln.startswith("get nodes")]
+        assert lines[0].split() == ["NAME", "READY", "ROLES", "GPUS", "PRODUCT", "PARTITION", "BURN-IN", "XGMI",
+                                    "HEALTH"]
+        rows = {ln.split()[0]: ln.split() for ln in lines[1:]}
+        assert set(rows) == {"cp-1", "etcd-1", "gpu-1", "gpu-2"}
+        assert rows["gpu-1"][3:] == ["8/8", "MI355X", "spx/nps1", "passed(quick)", "mesh", "healthy"]
+        assert rows["gpu-2"][3] == "0/8" and rows["gpu-2"][-1] == "unhealthy,tainted"
+        assert rows["cp-1"][1] == "Ready" and rows["cp-1"][3] == "-"
+        js = make_ctx(dict(base, output="json"))
+        dispatch(js, backend, "get", "nodes")
+        docs = [json.loads(ln) for ln in js.out.getvalue().splitlines() if ln.startswith("{")]
+        assert {d["NAME"]: d["GPUS"] for d in docs}["gpu-1"] == "8/8"
+    finally:
+        for a in agents:
+            a.stop()
+        fake.stop()

@@ -5,7 +5,8 @@
     triton-kubernetes [--config FILE] [--non-interactive] get     manager|cluster
     triton-kubernetes version
 
-Additions: ``wait cluster`` (the readiness waiter on an existing cluster),
+Additions: ``get nodes`` (the cluster's nodes with their MI355X GPU state),
+``wait cluster`` (the readiness waiter on an existing cluster),
 ``credentials node`` (a node agent's TLS certificate, token and image allow-list),
 ``health cluster`` (GPU RAS health of the MI355X nodes; optional taint fencing),
 ``backup cluster`` / ``restore cluster`` (namespace backup to the state backend
@@ -39,7 +40,7 @@ except ImportError:
 VALID = {
     "create": ["manager", "cluster", "node"],
     "destroy": ["manager", "cluster", "node"],
-    "get": ["manager", "cluster"],
+    "get": ["manager", "cluster", "nodes"],
     "wait": ["cluster"],
     "backup": ["cluster"],
     "restore": ["cluster"],
@@ -179,7 +180,12 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
     elif command == "destroy":
         {"manager": wf.delete_manager, "cluster": wf.delete_cluster, "node": wf.delete_node}[what](ctx, backend)
     elif command == "get":
-        {"manager": wf.get_manager, "cluster": wf.get_cluster}[what](ctx, backend)
+        if what == "nodes":
+            from ..workflows.get import get_nodes
+
+            get_nodes(ctx, backend)
+        else:
+            {"manager": wf.get_manager, "cluster": wf.get_cluster}[what](ctx, backend)
     elif command == "backup":
         from ..workflows.backup import backup_cluster
 
