@@ -399,6 +399,8 @@ def test_health_on_the_box():
         assert a["bdf"] == b["bdf"]
         if "ecc_uncorrectable" in a and "ecc_uncorrectable" in b:
             assert a["ecc_uncorrectable"] == b["ecc_uncorrectable"]
+        if "pcie_max_width" in a and "pcie_max_width" in b:  # both collectors see the same link
+            assert (a["pcie_width"], a["pcie_max_width"]) == (b["pcie_width"], b["pcie_max_width"])
     assert topo.native_health("sysfs") == health.evaluate(topo.native_topology("sysfs"))
 
 
@@ -442,3 +444,24 @@ def test_get_nodes_shows_gpu_state(tmp_path):
         for a in agents:
             a.stop()
         fake.stop()
+
+
+def test_degraded_pcie_link(tmp_path, native_ok):
+    """A GPU whose PCIe link trained narrower than the device supports is unhealthy (the
+    speed is not judged: power management lowers it at idle); the narrowest link is a label."""
+    root = healthy_tree(str(tmp_path))
+    dev = os.path.join(root, "sys/class/drm/renderD134/device")
+    for attr, val in (("current_link_width", "8"), ("current_link_speed", "16.0 GT/s PCIe")):
+        with open(os.path.join(dev, attr), "w") as fh:
+            fh.write(val + "\n")
+    doc = topo.native_topology("sysfs", root)
+    g6 = doc["gpus"][6]
+    assert (g6["pcie_width"], g6["pcie_max_width"], g6["pcie_speed_gts"], g6["pcie_max_speed_gts"]) == (8, 16, 16.0, 32.0)
+    v = _both(root)
+    assert v["reasons"] == ["GPU 6 (0000:65:00.0): PCIe link trained at x8, the device supports x16"]
+    labels = topo.native_labels("sysfs", root)
+    assert labels["amd.com/gpu.pcie-width"] == "8" and labels == labels_from_topology(doc)
+    # a lower link speed alone (idle power management) is not a problem
+    with open(os.path.join(dev, "current_link_width"), "w") as fh:
+        fh.write("16\n")
+    assert _both(root)["status"] == "healthy"

@@ -18,6 +18,9 @@ device's counters, so the max over a GPU's partitions counts once:
 * unhealthy when retired VRAM pages > ``gpu_max_retired_pages``; the default (``auto``,
   -1) is the amdgpu driver's default bad-page threshold, one page per 100 MiB of VRAM
   rounded up (``RAS_BAD_PAGE_COVER`` in ``amdgpu_ras.c``): 2949 pages for 288 GiB;
+* unhealthy when its PCIe link to the host trained narrower than the device supports
+  (``current_link_width`` < ``max_link_width``: a badly seated card or riser halves host
+  transfers; the link *speed* is not judged, power management lowers it at idle);
 * a counter the platform does not report is not judged.
 
 What happens to an unhealthy node is the cluster's ``gpu_health`` setting:
@@ -79,7 +82,8 @@ def physical_gpus(doc: Dict[str, Any]) -> List[Dict[str, Any]]:
         if key not in at:
             at[key] = len(out)
             out.append({"bdf": g.get("bdf", ""), "has_ecc": False, "ecc_uncorrectable": 0, "ecc_correctable": 0,
-                        "vram_mb": 0, "bad_pages": -1, "bad_pages_pending": -1})
+                        "vram_mb": 0, "bad_pages": -1, "bad_pages_pending": -1, "pcie_width": -1,
+                        "pcie_max_width": -1})
         p = out[at[key]]
         p["has_ecc"] = p["has_ecc"] or "ecc_uncorrectable" in g
         p["ecc_uncorrectable"] = max(p["ecc_uncorrectable"], int(g.get("ecc_uncorrectable", 0) or 0))
@@ -87,6 +91,8 @@ def physical_gpus(doc: Dict[str, Any]) -> List[Dict[str, Any]]:
         p["vram_mb"] = max(p["vram_mb"], int(g.get("vram_mb", 0) or 0))
         p["bad_pages"] = max(p["bad_pages"], int(g.get("bad_pages", -1)))
         p["bad_pages_pending"] = max(p["bad_pages_pending"], int(g.get("bad_pages_pending", -1)))
+        p["pcie_width"] = max(p["pcie_width"], int(g.get("pcie_width", -1)))
+        p["pcie_max_width"] = max(p["pcie_max_width"], int(g.get("pcie_max_width", -1)))
     return out
 
 
@@ -110,6 +116,9 @@ def evaluate(doc: Dict[str, Any], max_uncorrectable: int = 0, max_bad_pages: int
         if p["bad_pages"] >= 0 and limit >= 0 and p["bad_pages"] > limit:
             reasons.append(f"{who}: {p['bad_pages']} retired VRAM pages (max {limit})")
             ok = False
+        if 0 < p["pcie_width"] < p["pcie_max_width"]:
+            reasons.append(f"{who}: PCIe link trained at x{p['pcie_width']}, the device supports x{p['pcie_max_width']}")
+            ok = False
         g: Dict[str, Any] = {"gpu": i, "bdf": p["bdf"], "ok": ok}
         if p["has_ecc"]:
             g.update(ecc_uncorrectable=p["ecc_uncorrectable"], ecc_correctable=p["ecc_correctable"])
@@ -117,6 +126,10 @@ def evaluate(doc: Dict[str, Any], max_uncorrectable: int = 0, max_bad_pages: int
             g.update(bad_pages=p["bad_pages"], bad_pages_pending=p["bad_pages_pending"])
         if limit >= 0:
             g["bad_page_limit"] = limit
+        if p["pcie_width"] >= 0:
+            g["pcie_width"] = p["pcie_width"]
+        if p["pcie_max_width"] >= 0:
+            g["pcie_max_width"] = p["pcie_max_width"]
         gpus.append(g)
     return {"status": "unhealthy" if reasons else "healthy", "max_uncorrectable": max_uncorrectable,
             "max_bad_pages": max_bad_pages if max_bad_pages >= 0 else "auto",

@@ -22,6 +22,7 @@ plus xGMI keys used for topology-aware scheduling:
                                        claimed in SPX (node/partition.py)
 ``amd.com/gpu.ecc-uncorrectable``      uncorrectable ECC errors, summed over physical GPUs
 ``amd.com/gpu.bad-pages``              retired VRAM pages (driver bad-page records), summed
+``amd.com/gpu.pcie-width``             the narrowest GPU's PCIe link width (lanes)
 ``amd.com/gpu.health``                 ``healthy`` / ``unhealthy`` (node/health.py policy)
 =====================================  =============================================
 
@@ -134,6 +135,9 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     labels["amd.com/gpu.ecc-uncorrectable"] = str(sum(p["ecc_uncorrectable"] for p in phys))
     if any(p["bad_pages"] >= 0 for p in phys):
         labels["amd.com/gpu.bad-pages"] = str(sum(max(0, p["bad_pages"]) for p in phys))
+    widths = [p["pcie_width"] for p in phys if p["pcie_width"] > 0]
+    if widths:
+        labels["amd.com/gpu.pcie-width"] = str(min(widths))  # the narrowest GPU link to the host
     return labels
 
 

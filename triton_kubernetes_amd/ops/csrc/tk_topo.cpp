@@ -84,6 +84,10 @@ struct GpuInfo {
   // retired VRAM pages (the driver's bad-page records; -1: not reported), of which pending
   // (marked bad, reserved at the next reset)
   int64_t bad_pages = -1, bad_pages_pending = -1;
+  // the GPU's PCIe link to the host (its PCI function; partitions have none): lanes and
+  // GT/s, current and the most the device supports (-1: not reported)
+  int64_t pcie_width = -1, pcie_max_width = -1;
+  double pcie_gts = -1.0, pcie_max_gts = -1.0;
   std::vector<Link> links;
 };
 
@@ -212,6 +216,17 @@ Topology collect_amdsmi() {
       g.has_ecc = true;
       g.ecc_correctable = ec.correctable_count;
       g.ecc_uncorrectable = ec.uncorrectable_count;
+    }
+    amdsmi_pcie_info_t pcie{};
+    if (amdsmi_get_pcie_info(h, &pcie) == AMDSMI_STATUS_SUCCESS) {
+      // speeds come as MT/s (current) and GT/s or MT/s (max, by release): GT/s here
+      auto gts = [](uint32_t v) { return v > 1000 ? v / 1000.0 : (double)v; };
+      if (pcie.pcie_metric.pcie_width && pcie.pcie_metric.pcie_width != 0xFFFF) g.pcie_width = pcie.pcie_metric.pcie_width;
+      if (pcie.pcie_static.max_pcie_width && pcie.pcie_static.max_pcie_width != 0xFFFF)
+        g.pcie_max_width = pcie.pcie_static.max_pcie_width;
+      if (pcie.pcie_metric.pcie_speed && pcie.pcie_metric.pcie_speed != 0xFFFFFFFFu) g.pcie_gts = gts(pcie.pcie_metric.pcie_speed);
+      if (pcie.pcie_static.max_pcie_speed && pcie.pcie_static.max_pcie_speed != 0xFFFFFFFFu)
+        g.pcie_max_gts = gts(pcie.pcie_static.max_pcie_speed);
     }
     uint32_t nbad = 0;
     if (amdsmi_get_gpu_bad_page_info(h, &nbad, nullptr) == AMDSMI_STATUS_SUCCESS) {
@@ -391,6 +406,11 @@ Topology collect_sysfs(const std::string& root) {
     if (read_file(dev + "/current_memory_partition", &s)) g.memory_partition = s;
     if (read_file(dev + "/numa_node", &s)) g.numa_node = std::max<int64_t>(0, atoll(s.c_str()));
     if (read_file(dev + "/product_name", &s) && !s.empty()) g.market_name = s;
+    // PCIe link (the PCI function's attributes, e.g. "32.0 GT/s PCIe" and "16")
+    if (read_file(dev + "/current_link_width", &s) && isdigit((unsigned char)s[0])) g.pcie_width = atoll(s.c_str());
+    if (read_file(dev + "/max_link_width", &s) && isdigit((unsigned char)s[0])) g.pcie_max_width = atoll(s.c_str());
+    if (read_file(dev + "/current_link_speed", &s) && isdigit((unsigned char)s[0])) g.pcie_gts = atof(s.c_str());
+    if (read_file(dev + "/max_link_speed", &s) && isdigit((unsigned char)s[0])) g.pcie_max_gts = atof(s.c_str());
     if (g.market_name.empty()) {
       const char* m = market_from_device_id(did);
       g.market_name = m ? m : "";
@@ -563,6 +583,10 @@ std::string render_json(const Topology& t) {
               g.ecc_uncorrectable);
     if (g.bad_pages >= 0)
       appendf(o, ",\"bad_pages\":%" PRId64 ",\"bad_pages_pending\":%" PRId64, g.bad_pages, g.bad_pages_pending);
+    if (g.pcie_width >= 0) appendf(o, ",\"pcie_width\":%" PRId64, g.pcie_width);
+    if (g.pcie_max_width >= 0) appendf(o, ",\"pcie_max_width\":%" PRId64, g.pcie_max_width);
+    if (g.pcie_gts >= 0) appendf(o, ",\"pcie_speed_gts\":%.1f", g.pcie_gts);
+    if (g.pcie_max_gts >= 0) appendf(o, ",\"pcie_max_speed_gts\":%.1f", g.pcie_max_gts);
     o += ",\"links\":[";
     for (size_t k = 0; k < g.links.size(); ++k) {
       const Link& l = g.links[k];
@@ -599,6 +623,7 @@ struct PhysGpu {
   bool has_ecc = false;
   uint64_t ue = 0, ce = 0, vram_mb = 0;
   int64_t bad = -1, pending = -1;
+  int64_t width = -1, max_width = -1;
 };
 
 std::vector<PhysGpu> physical_gpus(const Topology& t) {
@@ -620,6 +645,8 @@ std::vector<PhysGpu> physical_gpus(const Topology& t) {
     p.vram_mb = std::max(p.vram_mb, g.vram_mb);
     p.bad = std::max(p.bad, g.bad_pages);
     p.pending = std::max(p.pending, g.bad_pages_pending);
+    p.width = std::max(p.width, g.pcie_width);
+    p.max_width = std::max(p.max_width, g.pcie_max_width);
   }
   return out;
 }
@@ -650,6 +677,12 @@ std::string render_health(const Topology& t, int64_t max_ue, int64_t max_bad, bo
       reasons.push_back(b);
       ok = false;
     }
+    if (p.width > 0 && p.max_width > 0 && p.width < p.max_width) {
+      snprintf(b, sizeof(b), "%s: PCIe link trained at x%" PRId64 ", the device supports x%" PRId64, who.c_str(),
+               p.width, p.max_width);
+      reasons.push_back(b);
+      ok = false;
+    }
     bad_gpus += !ok;
     appendf(gpus, "%s{\"gpu\":%zu,\"bdf\":\"%s\",\"ok\":%s", i ? "," : "", i, esc(p.bdf).c_str(),
             ok ? "true" : "false");
@@ -658,6 +691,8 @@ std::string render_health(const Topology& t, int64_t max_ue, int64_t max_bad, bo
     if (p.bad >= 0)
       appendf(gpus, ",\"bad_pages\":%" PRId64 ",\"bad_pages_pending\":%" PRId64, p.bad, p.pending);
     if (limit >= 0) appendf(gpus, ",\"bad_page_limit\":%" PRId64, limit);
+    if (p.width >= 0) appendf(gpus, ",\"pcie_width\":%" PRId64, p.width);
+    if (p.max_width >= 0) appendf(gpus, ",\"pcie_max_width\":%" PRId64, p.max_width);
     gpus += "}";
   }
   const bool healthy = reasons.empty();
@@ -771,14 +806,16 @@ std::string render_labels(const Topology& t) {
     L["amd.com/xgmi.fully-connected"] = (whole && gs.size() > 1 && min_xgmi == gs.size() - 1) ? "true" : "false";
     // RAS counters per physical GPU (its partitions report the same device's counters)
     uint64_t ecc = 0;
-    int64_t bad = 0;
+    int64_t bad = 0, width = INT64_MAX;
     bool bad_known = false;
     for (const auto& p : physical_gpus(t)) {
       ecc += p.ue;
       if (p.bad >= 0) bad += p.bad, bad_known = true;
+      if (p.width > 0) width = std::min(width, p.width);
     }
     L["amd.com/gpu.ecc-uncorrectable"] = std::to_string(ecc);
     if (bad_known) L["amd.com/gpu.bad-pages"] = std::to_string(bad);
+    if (width != INT64_MAX) L["amd.com/gpu.pcie-width"] = std::to_string(width);  // narrowest GPU link
   }
   // inter-node fabric: active RDMA ports
   size_t active = 0;
