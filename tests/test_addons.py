@@ -98,9 +98,12 @@ def test_generated_templates_match_the_definition():
 def test_addon_images_are_pinned():
     cfg = {"device_plugin_image": "", "node_labeller_image": None}
     values = addons.addon_values(cfg)
-    for k in ("device_plugin_image", "node_labeller_image", "rccl_probe_image", "webhook_image"):
+    for k in ("device_plugin_image", "rccl_probe_image", "webhook_image"):
         assert values[k] and not values[k].endswith(":latest") and ":" in values[k], (k, values[k])
         assert _var_default(k) == values[k]
+    # the ROCm labeller is opt-in; its documented tag is pinned too
+    assert values["node_labeller_image"] == _var_default("node_labeller_image") == ""
+    assert ":" in versions.NODE_LABELLER_IMAGE and not versions.NODE_LABELLER_IMAGE.endswith(":latest")
     ctx = make_ctx({"gpu_addons": True})
     from triton_kubernetes_amd.models.baremetal import add_mi355x_addons
     from triton_kubernetes_amd.state import State
@@ -109,7 +112,7 @@ def test_addon_images_are_pinned():
     key = add_mi355x_addons(ctx, st, "cluster_baremetal_x", "x")
     mod = st.module(key)
     assert mod["device_plugin_image"] == versions.DEVICE_PLUGIN_IMAGE
-    assert mod["node_labeller_image"] == versions.NODE_LABELLER_IMAGE
+    assert mod["node_labeller_image"] == ""  # the ROCm labeller is opt-in
     assert mod["rccl_probe_image"] == versions.RCCL_PROBE_IMAGE and mod["rccl_env_injector"] == "true"
     declared = hcl.check_module(MOD).variables
     assert set(mod) - {"source"} <= declared
@@ -243,7 +246,7 @@ def test_apply_is_idempotent_with_rbac_and_injector():
         outs = client.bootstrap("n3w-passw0rd-123", fake.url, "b00tstrap-only", timeout=10)
         client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
         cid = client.ensure_cluster("x").cluster_id
-        objs = addons.rendered_addons({})
+        objs = addons.rendered_addons({"node_labeller_image": versions.NODE_LABELLER_IMAGE})
         first = apply_manifests(client, cid, objs)
         assert first == apply_manifests(client, cid, objs)  # 409 -> PUT
         assert "ClusterRoleBinding/amdgpu-node-labeller" in first and first[-1] == "Job/rccl-ready"
@@ -453,3 +456,20 @@ def test_webhook_handshake_does_not_block_accept(tmp_path):
         stall.close()
     finally:
         srv.shutdown()
+
+
+def test_rocm_labeller_is_opt_in_and_owns_no_bootstrap_key():
+    """Off by default; when enabled it writes only keys ``amdgpu-topo-labeller`` does not
+    (two writers of one key with different value formats would flip it every reconcile)."""
+    from triton_kubernetes_amd.k8s.manifests import ROCM_LABELLER_ARGS
+    from triton_kubernetes_amd.node.labels import labels_from_topology, synthetic_topology
+
+    assert not any(o["kind"] == "DaemonSet" and "labeller" in o["metadata"]["name"]
+                   for _, o in addons.rendered_addons({}))
+    ours = {k.split("/", 1)[1].split(".", 1)[1] for k in labels_from_topology(synthetic_topology())
+            if k.startswith("amd.com/gpu.")}
+    theirs = {a.lstrip("-") for a in ROCM_LABELLER_ARGS}
+    assert ours and not ours & theirs, ours & theirs
+    ds = [o for _, o in addons.rendered_addons({"node_labeller_image": versions.NODE_LABELLER_IMAGE})
+          if o["kind"] == "DaemonSet" and "labeller" in o["metadata"]["name"]]
+    assert ds and ds[0]["spec"]["template"]["spec"]["containers"][0]["args"] == list(ROCM_LABELLER_ARGS)

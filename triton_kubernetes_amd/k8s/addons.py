@@ -14,7 +14,8 @@ group  objects               what
 base   DaemonSet             ROCm device plugin (advertises ``amd.com/gpu``)
 base   ConfigMap             ``rccl-env``: cluster RCCL/HSA environment
 label  SA/ClusterRole/Bind.  RBAC the node labeller needs to patch node labels
-label  DaemonSet             ROCm node labeller (keeps ``amd.com/gpu.*`` fresh)
+label  DaemonSet             ROCm node labeller, opt-in (``node_labeller_image``):
+                             simd count, driver version, partitioning support
 env    Secret/ConfigMap/     the RCCL-env injector: a mutating admission webhook
        Deployment/Service/   (``k8s/webhook.py``) that gives every pod requesting
        MutatingWebhookConf.  ``amd.com/gpu`` the ``rccl-env`` values and the node's
@@ -237,7 +238,7 @@ def addon_values(cfg: Dict[str, Any], cert: Optional[Any] = None) -> Dict[str, s
 
     return {
         "device_plugin_image": cfg.get("device_plugin_image") or versions.DEVICE_PLUGIN_IMAGE,
-        "node_labeller_image": cfg.get("node_labeller_image") or versions.NODE_LABELLER_IMAGE,
+        "node_labeller_image": cfg.get("node_labeller_image") or "",
         "rccl_probe_image": cfg.get("rccl_probe_image") or versions.RCCL_PROBE_IMAGE,
         "webhook_image": cfg.get("webhook_image") or versions.WEBHOOK_IMAGE,
         "injector_ca_b64": b64(cert.ca_pem) if cert else "",
@@ -248,7 +249,7 @@ def addon_values(cfg: Dict[str, Any], cert: Optional[Any] = None) -> Dict[str, s
 
 def module_cfg_defaults(cfg: Dict[str, Any]) -> Dict[str, Any]:
     """The module's variable defaults applied to a document entry (what Terraform sees)."""
-    out = {"node_labeller_image": versions.NODE_LABELLER_IMAGE, "rccl_env_injector": "true", "rccl_gate": "true"}
+    out = {"node_labeller_image": "", "rccl_env_injector": "true", "rccl_gate": "true"}
     out.update({k: v for k, v in cfg.items() if v is not None})
     return out
 

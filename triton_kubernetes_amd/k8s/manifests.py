@@ -2,7 +2,8 @@
 
 * ROCm device plugin DaemonSet (advertises ``amd.com/gpu``), scheduled on nodes
   labelled ``amd.com/gpu.present=true`` by the bootstrap labeller;
-* ROCm node-labeller DaemonSet (optional, keeps ``amd.com/gpu.*`` labels fresh);
+* ROCm node-labeller DaemonSet (opt-in, ``node_labeller_image``): only the keys the
+  bootstrap labeller does not write (:data:`ROCM_LABELLER_ARGS`);
 * ``rccl-env`` ConfigMap carrying the RCCL/HSA environment for GPU pods (the
   injector webhook, ``webhook.py``, puts it into every pod requesting ``amd.com/gpu``);
 * :func:`gpu_job_manifest` — an example/utility Job that requests all 8 GPUs
@@ -20,6 +21,13 @@ NAMESPACE = "kube-system"
 DEVICE_PLUGIN_NAME = "amdgpu-device-plugin"
 LABELLER_NAME = "amdgpu-node-labeller"
 GPU_SELECTOR = {"amd.com/gpu.present": "true"}
+# The ROCm labeller's keys that ``amdgpu-topo-labeller`` does not write.  Its product-name,
+# family, device-id, cu-count and vram keys are ours too, in other value formats (its
+# product name is the marketing string, ours "MI355X"); both writing one key would flip
+# the label on every reconcile, and the bootstrap labeller's values are the ones node
+# selectors and the readiness waiter use.
+ROCM_LABELLER_ARGS = ("-simd-count", "-driver-version", "-compute-partitioning-supported",
+                      "-memory-partitioning-supported")
 
 
 def device_plugin_daemonset(image: str) -> Dict[str, Any]:
@@ -63,9 +71,7 @@ def labeller_daemonset(image: str) -> Dict[str, Any]:
                     "serviceAccountName": LABELLER_NAME,
                     "containers": [{
                         "name": "labeller", "image": image,
-                        "args": ["-vram", "-cu-count", "-simd-count", "-device-id", "-family", "-product-name",
-                                 "-driver-version", "-compute-partitioning-supported",
-                                 "-memory-partitioning-supported"],
+                        "args": list(ROCM_LABELLER_ARGS),
                         "env": [{"name": "DS_NODE_NAME", "valueFrom": {"fieldRef": {"fieldPath": "spec.nodeName"}}}],
                         "securityContext": {"privileged": True},
                         "volumeMounts": [{"name": "sys", "mountPath": "/sys"}, {"name": "dev", "mountPath": "/dev"}],

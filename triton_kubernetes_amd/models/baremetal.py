@@ -77,8 +77,8 @@ def add_mi355x_addons(ctx: Context, state: State, cluster: str, name: str) -> st
         "rancher_cluster_id": f"${{module.{cluster}.rancher_cluster_id}}",
         # pinned tags (versions.py), never :latest
         "device_plugin_image": s.get_string("device_plugin_image") or versions.DEVICE_PLUGIN_IMAGE,
-        "node_labeller_image": (s.get_string("node_labeller_image") if s.is_set("node_labeller_image")
-                                else versions.NODE_LABELLER_IMAGE),
+        # opt-in: the bootstrap labeller owns amd.com/gpu.* (k8s/manifests.py:ROCM_LABELLER_ARGS)
+        "node_labeller_image": s.get_string("node_labeller_image") if s.is_set("node_labeller_image") else "",
         "rccl_probe_image": s.get_string("rccl_probe_image") or versions.RCCL_PROBE_IMAGE,
         "webhook_image": s.get_string("webhook_image") or versions.WEBHOOK_IMAGE,
         "rccl_gate": "true" if s.get_bool("rccl_gate") or not s.is_set("rccl_gate") else "false",

@@ -1329,8 +1329,10 @@ data "external" "gpu_labels" {{
         Var("name", None), Var("rancher_api_url", None), Var("rancher_access_key", None),
         Var("rancher_secret_key", None, sensitive=True), Var("rancher_cluster_id", None),
         Var("device_plugin_image", versions.DEVICE_PLUGIN_IMAGE),
-        Var("node_labeller_image", versions.NODE_LABELLER_IMAGE,
-            "Node labeller image (empty: no labeller DaemonSet or its RBAC)."),
+        Var("node_labeller_image", "",
+            "ROCm node labeller image, opt-in (empty: no labeller DaemonSet or its RBAC).",
+            # the pinned tag is versions.NODE_LABELLER_IMAGE
+            ),
         Var("rccl_probe_image", versions.RCCL_PROBE_IMAGE,
             "Image of the node-level rccl-ready Job (runs the node's installed tools)."),
         Var("webhook_image", versions.WEBHOOK_IMAGE, "Python image running the RCCL-env injector webhook."),

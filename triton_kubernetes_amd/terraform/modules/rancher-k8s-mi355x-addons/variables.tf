@@ -31,9 +31,9 @@ variable "device_plugin_image" {
 }
 
 variable "node_labeller_image" {
-  description = "Node labeller image (empty: no labeller DaemonSet or its RBAC)."
+  description = "ROCm node labeller image, opt-in (empty: no labeller DaemonSet or its RBAC)."
   type        = string
-  default     = "rocm/k8s-device-plugin:labeller-1.31.0.6"
+  default     = ""
 }
 
 variable "rccl_probe_image" {

@@ -74,7 +74,7 @@ DOCKER_INSTALL_URL = f"https://releases.rancher.com/install-docker/{DOCKER_VERSI
 
 # MI355X add-ons (pinned tags, never :latest)
 DEVICE_PLUGIN_IMAGE = "rocm/k8s-device-plugin:1.31.0.6"
-NODE_LABELLER_IMAGE = "rocm/k8s-device-plugin:labeller-1.31.0.6"
+NODE_LABELLER_IMAGE = "rocm/k8s-device-plugin:labeller-1.31.0.6"  # opt-in (node_labeller_image)
 # the RCCL readiness Job runs the node's installed rccl-ready (hostPath /opt/triton-kubernetes
 # and /opt/rocm), so any small glibc image serves; pinned by tag
 RCCL_PROBE_IMAGE = "ubuntu:22.04"
