@@ -338,6 +338,14 @@ def test_health_cluster_reconciles_the_taint(tmp_path):
         assert health.has_health_taint(k8s["gpu-1"]) and not health.has_health_taint(k8s["gpu-2"])
         assert k8s["gpu-1"]["metadata"]["labels"]["amd.com/gpu.health"] == "unhealthy"
         assert k8s["gpu-2"]["metadata"]["labels"]["amd.com/gpu.health"] == "healthy"
+        # the RAS counters labels are refreshed from the same verdict
+        sick_labels = health.ras_labels(health.physical_gpus(_sick_topology()))
+        assert sick_labels["amd.com/gpu.ecc-uncorrectable"] != "0"
+        for k, v in sick_labels.items():
+            assert k8s["gpu-1"]["metadata"]["labels"][k] == v, k
+        assert k8s["gpu-1"]["metadata"]["labels"]["amd.com/gpu.unhealthy-count"] == "1"
+        assert k8s["gpu-2"]["metadata"]["labels"]["amd.com/gpu.unhealthy-count"] == "0"
+        assert k8s["gpu-2"]["metadata"]["labels"]["amd.com/gpu.ecc-uncorrectable"] == "0"
         # NoSchedule keeps new pods off but does not evict the running device plugin;
         # the healed node's plugin pod schedules now that the taint is gone
         assert k8s["gpu-1"]["status"]["allocatable"]["amd.com/gpu"] == "8"

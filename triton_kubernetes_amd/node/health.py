@@ -140,6 +140,18 @@ def health_labels(verdict: Dict[str, Any]) -> Dict[str, str]:
     return {HEALTH_LABEL: verdict["status"], "amd.com/gpu.unhealthy-count": str(verdict["unhealthy_gpus"])}
 
 
+def ras_labels(gpus: List[Dict[str, Any]]) -> Dict[str, str]:
+    """The RAS / link labels over physical GPUs -- :func:`physical_gpus` entries or a
+    verdict's ``gpus`` (a counter a GPU does not report is absent or -1)."""
+    labels = {"amd.com/gpu.ecc-uncorrectable": str(sum(max(0, int(p.get("ecc_uncorrectable", 0))) for p in gpus))}
+    if any(int(p.get("bad_pages", -1)) >= 0 for p in gpus):
+        labels["amd.com/gpu.bad-pages"] = str(sum(max(0, int(p.get("bad_pages", -1))) for p in gpus))
+    widths = [int(p["pcie_width"]) for p in gpus if int(p.get("pcie_width", -1)) > 0]
+    if widths:
+        labels["amd.com/gpu.pcie-width"] = str(min(widths))  # the narrowest GPU link to the host
+    return labels
+
+
 def has_health_taint(node: Dict[str, Any]) -> bool:
     """A Kubernetes Node object carrying :data:`HEALTH_TAINT`."""
     return any(t.get("key") == HEALTH_TAINT["key"] for t in ((node.get("spec") or {}).get("taints") or []))
@@ -152,4 +164,4 @@ def taint_flag(taint: Optional[Dict[str, str]] = None) -> str:
 
 
 __all__ = ["POLICIES", "HEALTH_TAINT", "HEALTH_LABEL", "policy_of", "limits_of", "physical_gpus", "evaluate",
-           "health_labels", "has_health_taint", "taint_flag", "bad_page_limit"]
+           "health_labels", "ras_labels", "has_health_taint", "taint_flag", "bad_page_limit"]

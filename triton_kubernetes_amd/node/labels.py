@@ -129,15 +129,10 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     labels["amd.com/xgmi.fully-connected"] = "true" if whole and len(gpus) > 1 and \
         min(xgmi_peers) == len(gpus) - 1 else "false"
     # RAS counters per physical GPU (its partitions report the same device's counters)
-    from .health import physical_gpus
+    from .health import physical_gpus, ras_labels
 
     phys = physical_gpus(doc)
-    labels["amd.com/gpu.ecc-uncorrectable"] = str(sum(p["ecc_uncorrectable"] for p in phys))
-    if any(p["bad_pages"] >= 0 for p in phys):
-        labels["amd.com/gpu.bad-pages"] = str(sum(max(0, p["bad_pages"]) for p in phys))
-    widths = [p["pcie_width"] for p in phys if p["pcie_width"] > 0]
-    if widths:
-        labels["amd.com/gpu.pcie-width"] = str(min(widths))  # the narrowest GPU link to the host
+    labels.update(ras_labels(phys))
     return labels
 
 

@@ -13,7 +13,8 @@ The verdicts are printed as one JSON line per node, then a summary.  With
 an unhealthy node gets :data:`~..node.health.HEALTH_TAINT` (``NoSchedule``: no new GPU
 pods; a device plugin already running there keeps running, as Kubernetes does for
 ``NoSchedule``) and the ``amd.com/gpu.health`` label; a node that is healthy again has the
-taint removed.  ``triton-kubernetes health cluster`` exits 0 either way; the verdict is
+taint removed.  The RAS labels the bootstrap labeller set (``amd.com/gpu.ecc-uncorrectable``,
+``.bad-pages``, ``.pcie-width``, ``.unhealthy-count``) are refreshed from the same verdict.  ``triton-kubernetes health cluster`` exits 0 either way; the verdict is
 in the output (``unhealthy: N``).
 
 Settings: ``cluster_manager``, ``cluster_name``, ``health_taint`` (default false),
@@ -27,7 +28,7 @@ from typing import Any, Dict, List
 from ..backend.base import Backend
 from ..config.context import Context
 from ..errors import ConfigError, TKError
-from ..node.health import HEALTH_LABEL, HEALTH_TAINT, has_health_taint, limits_of
+from ..node.health import HEALTH_TAINT, has_health_taint, health_labels, limits_of, ras_labels
 from ..node.plan import TOOLS_DIR
 from ..parallel.transport import HostRef
 from ..terraform.catalog import module_from_source
@@ -69,18 +70,19 @@ def _probe(ctx: Context, state, host: str, cfg: Dict[str, Any]) -> Dict[str, Any
 
 
 def _reconcile(client, cluster_id: str, node: Dict[str, Any], verdict: Dict[str, Any]) -> str:
-    """Add / remove the health taint and set the label; returns what changed ('' = nothing)."""
+    """Add / remove the health taint and set the labels; returns what changed ('' = nothing)."""
     name = node["metadata"]["name"]
     taints = [t for t in (node.get("spec") or {}).get("taints") or [] if t.get("key") != HEALTH_TAINT["key"]]
     unhealthy = verdict["status"] != "healthy"
     if unhealthy:
         taints.append(dict(HEALTH_TAINT))
     tainted = has_health_taint(node)
-    label = (node.get("metadata") or {}).get("labels", {}).get(HEALTH_LABEL)
-    if tainted == unhealthy and label == verdict["status"]:
+    want = health_labels(verdict)
+    want.update(ras_labels(verdict.get("gpus") or []))
+    have = (node.get("metadata") or {}).get("labels") or {}
+    if tainted == unhealthy and all(have.get(k) == v for k, v in want.items()):
         return ""
-    client.patch_node(cluster_id, name, {"metadata": {"labels": {HEALTH_LABEL: verdict["status"]}},
-                                         "spec": {"taints": taints}})
+    client.patch_node(cluster_id, name, {"metadata": {"labels": want}, "spec": {"taints": taints}})
     if tainted == unhealthy:
         return "labelled"
     return "tainted" if unhealthy else "untainted"
