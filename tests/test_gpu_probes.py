@@ -271,6 +271,12 @@ def test_native_labels_match_python_spec():
     assert via_sysfs["amd.com/gpu.product-name"] == "MI355X"
     assert via_sysfs["amd.com/gpu.target"] == "gfx950"
     assert via_sysfs["amd.com/gpu.vram"] == "288G"
+    # the document fields both collectors read agree too (PCIe link, driver version)
+    smi, sysfs = topo.amdsmi_topology(), topo.native_topology("sysfs")
+    assert smi["driver"]["version"] == sysfs["driver"]["version"]
+    for a, b in zip(smi["gpus"], sysfs["gpus"]):
+        for k in ("pcie_width", "pcie_max_width", "pcie_max_speed_gts"):
+            assert a.get(k) == b.get(k), k
 
 
 def test_gate_comm_nonblocking_then_sweep():

@@ -159,6 +159,9 @@ Topology collect_amdsmi() {
   if (!hs.empty() && amdsmi_get_gpu_driver_info(hs[0], &drv) == AMDSMI_STATUS_SUCCESS) {
     t.driver_name = drv.driver_name;
     t.driver_version = drv.driver_version;
+    // an in-tree amdgpu has no module version; amd_smi then reports the kernel banner
+    // ("Linux version ..."): report none, as /sys/module/amdgpu/version does
+    if (t.driver_version.rfind("Linux", 0) == 0) t.driver_version.clear();
   }
   for (size_t i = 0; i < hs.size(); ++i) {
     auto h = hs[i];
