@@ -211,7 +211,8 @@ def test_terraform_host_script_renders_the_policy():
             "rancher_registry_password": "", "gpu_count": 8, "gpu_burnin": "quick", "rccl_env_file": "", "rccl_min_busbw": "0",
             "gpu_link_min_frac": "0.5", "gpu_link_min_gbps": "38", "gpu_compute_partition": "spx",
             "gpu_memory_partition": "nps1", "gpu_partitions": 1, "rccl_slim": "off",
-            "gpu_max_uncorrectable_ecc": "0", "gpu_max_retired_pages": "auto", "gpu_host_tuning": "warn"}
+            "gpu_max_uncorrectable_ecc": "0", "gpu_max_retired_pages": "auto", "gpu_host_tuning": "warn",
+            "gpu_metrics_textfile": ""}
     fail = tfplan._f_templatefile(path, dict(base, gpu_health="fail"))
     taint = tfplan._f_templatefile(path, dict(base, gpu_health="taint"))
     off = tfplan._f_templatefile(path, dict(base, gpu_health="off"))

@@ -197,6 +197,10 @@ def _mi355x_fields(ctx: Context) -> Dict:
         out["gpu_health"] = policy
         out["gpu_max_uncorrectable_ecc"] = str(max_ue)
         out["gpu_max_retired_pages"] = "auto" if max_bad < 0 else str(max_bad)
+    if s.is_set("gpu_metrics_textfile"):  # node_exporter textfile (node/metrics.py)
+        from ..node.metrics import textfile_dir_of
+
+        out["gpu_metrics_textfile"] = textfile_dir_of({"gpu_metrics_textfile": s.get_string("gpu_metrics_textfile")})
     if s.is_set("gpu_host_tuning"):  # NUMA balancing / IOMMU checks (node/hosttune.py)
         from ..node.hosttune import policy_of as tuning_policy
 

@@ -32,7 +32,8 @@ In both modes the MI355X steps call the native probes directly on the agent's
 GPUs: topology labeller (N1), HBM/MFMA/memtest burn-in, RCCL env file and the
 node-level RCCL sweep (N2).
 
-HTTP API (JSON): ``GET /v1/info``, ``GET /v1/health`` (GPU RAS verdict, ``node/health.py``), ``POST /v1/plan``, ``POST /v1/rccl-uid``,
+HTTP API (JSON): ``GET /v1/info``, ``GET /v1/health`` (GPU RAS verdict, ``node/health.py``), ``GET /metrics``
+(Prometheus text: GPU RAS / PCIe now, the last bring-up's steps and measurements; ``node/metrics.py``), ``POST /v1/plan``, ``POST /v1/rccl-uid``,
 ``POST /v1/rccl-prepare`` (without a ``uid``: host the rendezvous and return it; start this node's ranks of the cluster-wide RCCL
 communicator, non-blocking), ``POST /v1/rccl-gate`` (run them: verified
 all-reduce sweep), ``POST /v1/rccl-abort``, ``POST /v1/cleanup``, ``POST /v1/shutdown``
@@ -170,6 +171,8 @@ class NodeAgent:
         self._spare_uid: Optional[bytes] = None
         self._uid_mu = threading.Lock()
         self.last_labels: Dict[str, str] = {}
+        # the health limits of the last gpu_health step (what /metrics judges by)
+        self.health_limits: Tuple[int, int] = (0, -1)
         self.history: List[Dict[str, Any]] = []
         self._server: Optional[http.server.ThreadingHTTPServer] = None
         self.shutdown_requested = threading.Event()
@@ -387,8 +390,9 @@ class NodeAgent:
             if topo is None:
                 fut = ctx.get("topology_future")
                 topo = fut.result() if fut is not None else self._topology()
-            verdict = evaluate(topo, int(step.params.get("max_uncorrectable", 0)),
-                               int(step.params.get("max_bad_pages", -1)))
+            self.health_limits = (int(step.params.get("max_uncorrectable", 0)),
+                                  int(step.params.get("max_bad_pages", -1)))
+            verdict = evaluate(topo, *self.health_limits)
             self.write_file("/etc/triton-kubernetes/gpu-health.json", json.dumps(verdict))
             ctx["labels"].update(health_labels(verdict))
             if verdict["status"] != "healthy":
@@ -396,6 +400,16 @@ class NodeAgent:
                     raise StepFailed(step.name, "unhealthy GPUs (gpu_health = fail): " + "; ".join(verdict["reasons"]))
                 ctx["taints"].append(dict(HEALTH_TAINT))
             return verdict
+        if a == "gpu_metrics":
+            # the textfile for node_exporter (an agent node also serves GET /metrics)
+            from .health import evaluate
+            from .metrics import TEXTFILE_NAME, gpu_metrics
+
+            topo = ctx.get("topology") or self._topology()
+            verdict = evaluate(topo, int(step.params.get("max_uncorrectable", 0)),
+                               int(step.params.get("max_bad_pages", -1)))
+            path = os.path.join(str(step.params["dir"]), TEXTFILE_NAME)
+            return {"file": self.write_file(path, gpu_metrics(verdict, self.name)), "served": "/metrics"}
         if a == "gpu_links":
             # every ordered GPU pair's peer read (a kernel on the receiver), disjoint pairs at
             # a time: a link below the node's median fraction or the absolute floor fails the
@@ -475,6 +489,15 @@ class NodeAgent:
         verdict = evaluate(self._topology(), max_uncorrectable, max_bad_pages)
         verdict["node"] = self.name
         return verdict
+
+    def metrics(self) -> str:
+        """``GET /metrics``: Prometheus text of the node (node/metrics.py)."""
+        from .metrics import bringup_metrics, gpu_metrics
+
+        text = bringup_metrics(self.history[-1] if self.history else None, self.name, self.mode)
+        if self.devices or self.topology_override is not None:
+            text += gpu_metrics(self.health(*self.health_limits), self.name)
+        return text
 
     def _gpu_preflight(self, expected: int) -> Dict[str, Any]:
         if self.topology_override is not None:
@@ -813,7 +836,11 @@ class NodeAgent:
                 return json.loads(self.rfile.read(n) or b"{}") if n else {}
 
             def _auth(self) -> bool:
-                return hmac.compare_digest(self.headers.get("X-TK-Agent-Token", ""), agent.token)
+                given = self.headers.get("X-TK-Agent-Token", "")
+                bearer = self.headers.get("Authorization", "")
+                if not given and bearer.startswith("Bearer "):  # Prometheus' scrape authorization
+                    given = bearer[len("Bearer "):]
+                return hmac.compare_digest(given, agent.token)
 
             def do_GET(self):
                 if not self._auth():
@@ -823,6 +850,19 @@ class NodeAgent:
                         pending = len(agent._gates)
                     return self._reply(200, {"name": agent.name, "mode": agent.mode, "devices": agent.devices,
                                              "labels": agent.last_labels, "pending_gates": pending})
+                if urllib.parse.urlsplit(self.path).path == "/metrics":
+                    from .metrics import CONTENT_TYPE
+
+                    try:
+                        body = agent.metrics().encode()
+                    except Exception as exc:  # noqa: BLE001
+                        return self._reply(500, {"error": f"{type(exc).__name__}: {exc}"})
+                    self.send_response(200)
+                    self.send_header("Content-Type", CONTENT_TYPE)
+                    self.send_header("Content-Length", str(len(body)))
+                    self.end_headers()
+                    self.wfile.write(body)
+                    return None
                 if urllib.parse.urlsplit(self.path).path == "/v1/health":
                     try:
                         q = urllib.parse.parse_qs(urllib.parse.urlsplit(self.path).query)

@@ -273,6 +273,15 @@ case $rc in
   3) {on_bad} ;;
   *) echo "GPU health check failed (exit $rc)" >&2; exit 1 ;;
 esac""", {"policy": policy, "max_uncorrectable": max_ue, "max_bad_pages": max_bad}, gpu=True))
+        from .metrics import textfile_dir_of, textfile_script
+
+        mdir = textfile_dir_of(cfg)
+        if mdir:
+            # opt-in: GPU health as Prometheus text for node_exporter, refreshed every minute
+            m_ue, m_bad = limits_of(cfg)
+            plan.steps.append(Step("gpu_metrics", "gpu_metrics",
+                                   textfile_script(TOOLS_DIR, mdir, str(m_ue), "auto" if m_bad < 0 else str(m_bad)),
+                                   {"dir": mdir, "max_uncorrectable": m_ue, "max_bad_pages": m_bad}, gpu=True))
         # discovered inter-node settings (active RDMA ports) first; the configured
         # values follow, so an explicit rccl_env key wins when the file is sourced
         plan.steps.append(Step("rccl_env", "rccl_env", f"""

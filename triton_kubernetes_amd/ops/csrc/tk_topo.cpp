@@ -659,59 +659,147 @@ int64_t bad_page_limit(const PhysGpu& p, int64_t max_bad) {
   return p.vram_mb ? static_cast<int64_t>((p.vram_mb + 99) / 100) : -1;  // -1: no limit known
 }
 
-std::string render_health(const Topology& t, int64_t max_ue, int64_t max_bad, bool labels) {
+struct HealthRow {
+  PhysGpu p;
+  int64_t limit = -1;
+  bool ok = true;
+};
+
+struct Verdict {
+  std::vector<HealthRow> rows;
   std::vector<std::string> reasons;
-  std::string gpus;
   size_t bad_gpus = 0;
+};
+
+Verdict judge(const Topology& t, int64_t max_ue, int64_t max_bad) {
+  Verdict v;
   const auto phys = physical_gpus(t);
   for (size_t i = 0; i < phys.size(); ++i) {
-    const PhysGpu& p = phys[i];
-    const int64_t limit = bad_page_limit(p, max_bad);
+    HealthRow r;
+    r.p = phys[i];
+    const PhysGpu& p = r.p;
+    r.limit = bad_page_limit(p, max_bad);
     const std::string who = "GPU " + std::to_string(i) + (p.bdf.empty() ? "" : " (" + p.bdf + ")");
-    bool ok = true;
     char b[256];
     if (p.has_ecc && static_cast<int64_t>(p.ue) > max_ue) {
       snprintf(b, sizeof(b), "%s: %" PRIu64 " uncorrectable ECC errors (max %" PRId64 ")", who.c_str(), p.ue, max_ue);
-      reasons.push_back(b);
-      ok = false;
+      v.reasons.push_back(b);
+      r.ok = false;
     }
-    if (p.bad >= 0 && limit >= 0 && p.bad > limit) {
-      snprintf(b, sizeof(b), "%s: %" PRId64 " retired VRAM pages (max %" PRId64 ")", who.c_str(), p.bad, limit);
-      reasons.push_back(b);
-      ok = false;
+    if (p.bad >= 0 && r.limit >= 0 && p.bad > r.limit) {
+      snprintf(b, sizeof(b), "%s: %" PRId64 " retired VRAM pages (max %" PRId64 ")", who.c_str(), p.bad, r.limit);
+      v.reasons.push_back(b);
+      r.ok = false;
     }
     if (p.width > 0 && p.max_width > 0 && p.width < p.max_width) {
       snprintf(b, sizeof(b), "%s: PCIe link trained at x%" PRId64 ", the device supports x%" PRId64, who.c_str(),
                p.width, p.max_width);
-      reasons.push_back(b);
-      ok = false;
+      v.reasons.push_back(b);
+      r.ok = false;
     }
-    bad_gpus += !ok;
+    v.bad_gpus += !r.ok;
+    v.rows.push_back(r);
+  }
+  return v;
+}
+
+std::string render_health(const Topology& t, int64_t max_ue, int64_t max_bad, bool labels) {
+  const Verdict v = judge(t, max_ue, max_bad);
+  const bool healthy = v.reasons.empty();
+  if (labels) {
+    std::string o = std::string("amd.com/gpu.health=") + (healthy ? "healthy" : "unhealthy") + "\n";
+    o += "amd.com/gpu.unhealthy-count=" + std::to_string(v.bad_gpus) + "\n";
+    return o;
+  }
+  std::string gpus;
+  for (size_t i = 0; i < v.rows.size(); ++i) {
+    const PhysGpu& p = v.rows[i].p;
     appendf(gpus, "%s{\"gpu\":%zu,\"bdf\":\"%s\",\"ok\":%s", i ? "," : "", i, esc(p.bdf).c_str(),
-            ok ? "true" : "false");
+            v.rows[i].ok ? "true" : "false");
     if (p.has_ecc)
       appendf(gpus, ",\"ecc_uncorrectable\":%" PRIu64 ",\"ecc_correctable\":%" PRIu64, p.ue, p.ce);
     if (p.bad >= 0)
       appendf(gpus, ",\"bad_pages\":%" PRId64 ",\"bad_pages_pending\":%" PRId64, p.bad, p.pending);
-    if (limit >= 0) appendf(gpus, ",\"bad_page_limit\":%" PRId64, limit);
+    if (v.rows[i].limit >= 0) appendf(gpus, ",\"bad_page_limit\":%" PRId64, v.rows[i].limit);
     if (p.width >= 0) appendf(gpus, ",\"pcie_width\":%" PRId64, p.width);
     if (p.max_width >= 0) appendf(gpus, ",\"pcie_max_width\":%" PRId64, p.max_width);
     gpus += "}";
-  }
-  const bool healthy = reasons.empty();
-  if (labels) {
-    std::string o = std::string("amd.com/gpu.health=") + (healthy ? "healthy" : "unhealthy") + "\n";
-    o += "amd.com/gpu.unhealthy-count=" + std::to_string(bad_gpus) + "\n";
-    return o;
   }
   std::string o;
   appendf(o, "{\"status\":\"%s\",\"max_uncorrectable\":%" PRId64 ",\"max_bad_pages\":", healthy ? "healthy" : "unhealthy",
           max_ue);
   if (max_bad >= 0) appendf(o, "%" PRId64, max_bad);
   else o += "\"auto\"";
-  appendf(o, ",\"unhealthy_gpus\":%zu,\"reasons\":[", bad_gpus);
-  for (size_t i = 0; i < reasons.size(); ++i) appendf(o, "%s\"%s\"", i ? "," : "", esc(reasons[i]).c_str());
+  appendf(o, ",\"unhealthy_gpus\":%zu,\"reasons\":[", v.bad_gpus);
+  for (size_t i = 0; i < v.reasons.size(); ++i) appendf(o, "%s\"%s\"", i ? "," : "", esc(v.reasons[i]).c_str());
   o += "],\"gpus\":[" + gpus + "]}";
+  return o;
+}
+
+// --- Prometheus text ----------------------------------------------------------
+// The GPU families of triton_kubernetes_amd/node/metrics.py:gpu_metrics -- same names, help
+// strings, label order and samples (tests compare the two) -- for node_exporter's textfile
+// collector on SSH / Terraform nodes.
+std::string prom_esc(const std::string& s) {
+  std::string o;
+  for (char c : s) {
+    if (c == '\\') o += "\\\\";
+    else if (c == '\n') o += "\\n";
+    else if (c == '"') o += "\\\"";
+    else o += c;
+  }
+  return o;
+}
+
+std::string render_prom(const Topology& t, int64_t max_ue, int64_t max_bad, const std::string& node) {
+  const Verdict v = judge(t, max_ue, max_bad);
+  struct Family {
+    const char* name;
+    const char* help;
+  };
+  static const Family fams[] = {
+      {"tk_gpu_healthy", "1 if the GPU passes the node's health rules, else 0"},
+      {"tk_gpu_ecc_uncorrectable_errors", "Uncorrectable ECC errors, summed over RAS blocks"},
+      {"tk_gpu_ecc_correctable_errors", "Correctable ECC errors, summed over RAS blocks"},
+      {"tk_gpu_retired_pages", "Retired VRAM pages (driver bad-page records)"},
+      {"tk_gpu_retired_pages_pending", "VRAM pages pending retirement"},
+      {"tk_gpu_retired_pages_limit", "Retired-page limit of the health rules"},
+      {"tk_gpu_pcie_link_width", "Trained PCIe link width (lanes)"},
+      {"tk_gpu_pcie_link_max_width", "PCIe link width the device supports (lanes)"},
+      {"tk_node_unhealthy_gpus", "Unhealthy physical GPUs on the node"},
+  };
+  const size_t nfam = sizeof(fams) / sizeof(fams[0]);
+  std::vector<std::string> rows(nfam);
+  const std::string n = prom_esc(node);
+  for (size_t i = 0; i < v.rows.size(); ++i) {
+    const HealthRow& r = v.rows[i];
+    const PhysGpu& p = r.p;
+    char lab[512];
+    snprintf(lab, sizeof(lab), "{node=\"%s\",gpu=\"%zu\",bdf=\"%s\"}", n.c_str(), i, prom_esc(p.bdf).c_str());
+    auto add = [&](size_t f, int64_t val) {
+      if (val < 0) return;
+      appendf(rows[f], "%s%s %" PRId64 "\n", fams[f].name, lab, val);
+    };
+    add(0, r.ok ? 1 : 0);
+    if (p.has_ecc) {
+      add(1, static_cast<int64_t>(p.ue));
+      add(2, static_cast<int64_t>(p.ce));
+    }
+    if (p.bad >= 0) {
+      add(3, p.bad);
+      add(4, p.pending);
+    }
+    add(5, r.limit);
+    add(6, p.width);
+    add(7, p.max_width);
+  }
+  appendf(rows[8], "tk_node_unhealthy_gpus{node=\"%s\"} %zu\n", n.c_str(), v.bad_gpus);
+  std::string o;
+  for (size_t f = 0; f < nfam; ++f) {
+    if (rows[f].empty()) continue;
+    appendf(o, "# HELP %s %s\n# TYPE %s gauge\n", fams[f].name, fams[f].help, fams[f].name);
+    o += rows[f];
+  }
   return o;
 }
 
@@ -922,14 +1010,17 @@ extern "C" int tkt_topology_json(char* buf, size_t len) { return tkt_topology_js
 extern "C" int tkt_topology_labels(char* buf, size_t len) { return tkt_topology_labels_src("amdsmi", "", buf, len); }
 
 #ifdef TK_TOPO_MAIN
-// amdgpu-topo-labeller [--labels|--rccl-env|--health] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
-//                      [--max-uncorrectable N] [--max-bad-pages N|auto]
+// amdgpu-topo-labeller [--labels|--rccl-env|--health|--prom] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
+//                      [--max-uncorrectable N] [--max-bad-pages N|auto] [--node NAME]
 //   default: topology JSON on stdout; --labels: one `amd.com/...=value` per line;
 //   --rccl-env: the inter-node RCCL settings for the node's active RDMA ports;
 //   --health: the GPU health verdict (JSON; with --labels the health labels), exit 3 when
-//   a GPU is unhealthy
+//   a GPU is unhealthy;
+//   --prom: the GPU health families as Prometheus text (node_exporter textfile collector;
+//   label node=NAME, default the host name), exit 0 whatever the verdict
 int main(int argc, char** argv) {
-  bool labels = false, rccl_env = false, health = false;
+  bool labels = false, rccl_env = false, health = false, prom = false;
+  std::string node;
   long long max_ue = 0, max_bad = -1;
   const char* source = "auto";
   const char* root = "";
@@ -940,6 +1031,10 @@ int main(int argc, char** argv) {
       rccl_env = true;
     } else if (strcmp(argv[i], "--health") == 0) {
       health = true;
+    } else if (strcmp(argv[i], "--prom") == 0) {
+      prom = true;
+    } else if (strcmp(argv[i], "--node") == 0 && i + 1 < argc) {
+      node = argv[++i];
     } else if (strcmp(argv[i], "--max-uncorrectable") == 0 && i + 1 < argc) {
       max_ue = atoll(argv[++i]);
     } else if (strcmp(argv[i], "--max-bad-pages") == 0 && i + 1 < argc) {
@@ -951,8 +1046,8 @@ int main(int argc, char** argv) {
       root = argv[++i];
     } else {
       fprintf(stderr,
-              "usage: %s [--labels|--rccl-env|--health] [--source auto|amdsmi|sysfs] [--sysfs-root DIR] "
-              "[--max-uncorrectable N] [--max-bad-pages N|auto]\n",
+              "usage: %s [--labels|--rccl-env|--health|--prom] [--source auto|amdsmi|sysfs] [--sysfs-root DIR] "
+              "[--max-uncorrectable N] [--max-bad-pages N|auto] [--node NAME]\n",
               argv[0]);
       return 64;
     }
@@ -968,6 +1063,18 @@ int main(int argc, char** argv) {
     return 0;
   }
   const Topology t = collect(source, root);
+  if (prom) {
+    if (t.status != 0) {
+      fprintf(stderr, "amdgpu-topo-labeller: %s\n", t.error.c_str());
+      return 2;
+    }
+    if (node.empty()) {
+      char host[256] = {0};
+      if (gethostname(host, sizeof(host) - 1) == 0) node = host;
+    }
+    fputs(render_prom(t, max_ue, max_bad, node).c_str(), stdout);
+    return 0;
+  }
   if (health) {
     if (t.status != 0) {
       fprintf(stderr, "amdgpu-topo-labeller: %s\n", t.error.c_str());

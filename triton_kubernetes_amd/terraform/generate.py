@@ -1243,6 +1243,9 @@ resource "terraform_data" "install_rancher_agent" {{
             "GPU health policy (RAS counters): fail = an unhealthy GPU fails the node; taint = the node joins "
             "tainted amd.com/gpu-health=unhealthy:NoSchedule (no GPU pods); off = not checked"),
         Var("gpu_max_uncorrectable_ecc", "0", "uncorrectable ECC errors a GPU may have logged"),
+        Var("gpu_metrics_textfile", "",
+            "node_exporter textfile collector directory: write the GPU health metrics there (tk_gpu.prom) "
+            "and refresh them every minute from a systemd timer (empty: off)"),
         Var("gpu_max_retired_pages", "auto",
             "retired VRAM pages a GPU may have (auto: the amdgpu driver's default threshold, one page per "
             "100 MiB of VRAM)"),
@@ -1294,6 +1297,7 @@ resource "terraform_data" "install_mi355x_node" {{
       gpu_host_tuning                    = var.gpu_host_tuning
       gpu_max_uncorrectable_ecc          = var.gpu_max_uncorrectable_ecc
       gpu_max_retired_pages              = var.gpu_max_retired_pages
+      gpu_metrics_textfile               = var.gpu_metrics_textfile
     }})]
   }}
 }}

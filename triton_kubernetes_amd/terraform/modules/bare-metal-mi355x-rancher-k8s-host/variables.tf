@@ -187,6 +187,12 @@ variable "gpu_max_uncorrectable_ecc" {
   default     = "0"
 }
 
+variable "gpu_metrics_textfile" {
+  description = "node_exporter textfile collector directory: write the GPU health metrics there (tk_gpu.prom) and refresh them every minute from a systemd timer (empty: off)"
+  type        = string
+  default     = ""
+}
+
 variable "gpu_max_retired_pages" {
   description = "retired VRAM pages a GPU may have (auto: the amdgpu driver's default threshold, one page per 100 MiB of VRAM)"
   type        = string

@@ -8,6 +8,7 @@ templates, and they fix the reference quirks Q10
 """
 
 from ..node.hosttune import shell_check as _host_tuning_check
+from ..node.metrics import textfile_script as _metrics_textfile
 
 # download, verify (when docker_install_sha256 is set), run — no `curl | sh` of an unchecked stream
 DOCKER_INSTALL = r"""if ! command -v docker >/dev/null 2>&1; then
@@ -442,6 +443,11 @@ case $health_rc in
 %{ endif ~}
   *) echo "GPU health check failed (exit $health_rc)" >&2; exit 1 ;;
 esac
+%{ endif ~}
+%{ if gpu_metrics_textfile != "" ~}
+# GPU health as Prometheus text for node_exporter's textfile collector, every minute
+""" + _metrics_textfile("/opt/triton-kubernetes/bin", "${gpu_metrics_textfile}", "${gpu_max_uncorrectable_ecc}",
+                        "${gpu_max_retired_pages}") + r"""
 %{ endif ~}
 { $T/amdgpu-topo-labeller --rccl-env || true; cat <<'TK_RCCL_EOF'
 ${rccl_env_file}
