@@ -7,6 +7,7 @@
 * the node agent serves it at ``GET /metrics`` with Prometheus' bearer authorization.
 """
 
+import json
 import os
 import subprocess
 
@@ -218,3 +219,22 @@ def test_textfile_setting_in_both_delivery_paths(tmp_path):
     want = metrics.textfile_script("/opt/triton-kubernetes/bin", "/var/lib/node_exporter/textfile", "2", "auto")
     assert want in on
     assert subprocess.run(["bash", "-n"], input=on, text=True).returncode == 0
+
+
+@pytest.mark.gpu
+def test_prom_on_the_box():
+    """Both collectors' --prom text on the MI355X equals the Python rendering of that
+    collector's verdict, and parses."""
+    for source in ("sysfs", "amdsmi"):
+        p = subprocess.run([executable("amdgpu-topo-labeller"), "--prom", "--node", "box", "--source", source],
+                           capture_output=True, text=True, timeout=120)
+        assert p.returncode == 0, p.stderr
+        print(source, p.stdout)
+        # amd_smi runs in the labeller executable (a child process), never in this one
+        v = subprocess.run([executable("amdgpu-topo-labeller"), "--health", "--source", source],
+                           capture_output=True, text=True, timeout=120)
+        assert v.returncode in (0, 3), v.stderr
+        assert p.stdout == metrics.gpu_metrics(json.loads(v.stdout), "box")
+        s = _samples(p.stdout)
+        assert s[("tk_node_unhealthy_gpus", (("node", "box"),))] >= 0
+        assert any(k[0] == "tk_gpu_pcie_link_width" for k in s)
