@@ -136,6 +136,12 @@ def test_agent_serves_metrics_with_bearer_auth(tmp_path):
     # judged with the limits the node was brought up with (5 uncorrectable allowed)
     gpu2 = [v for k, v in s.items() if k[0] == "tk_gpu_ecc_uncorrectable_errors" and ("gpu", "2") in k[1]]
     assert gpu2 == [3] and s[("tk_node_unhealthy_gpus", (("node", "gpu-7"),))] == 0
+    assert s[("tk_agent_gpu_collect_success", (("node", "gpu-7"),))] == 1
+    # a GPU read that fails costs the GPU families, not the endpoint
+    agent.topology_override = {"gpus": [{"bdf": "x", "bad_pages": "garbled"}]}
+    s = _samples(agent.metrics())
+    assert s[("tk_agent_gpu_collect_success", (("node", "gpu-7"),))] == 0 and s[("tk_bringup_success", (("node", "gpu-7"),))] == 1
+    assert not any(k[0].startswith("tk_gpu_healthy") for k in s)
 
 
 def _run_textfile_script(tmp_path, root, systemd: bool):

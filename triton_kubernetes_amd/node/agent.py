@@ -494,10 +494,13 @@ class NodeAgent:
         """``GET /metrics``: Prometheus text of the node (node/metrics.py)."""
         from .metrics import bringup_metrics, gpu_metrics
 
-        text = bringup_metrics(self.history[-1] if self.history else None, self.name, self.mode)
+        gpu_text, ok = "", None
         if self.devices or self.topology_override is not None:
-            text += gpu_metrics(self.health(*self.health_limits), self.name)
-        return text
+            try:  # a failed GPU read costs the GPU families of this scrape, not the endpoint
+                gpu_text, ok = gpu_metrics(self.health(*self.health_limits), self.name), True
+            except Exception:  # noqa: BLE001
+                ok = False
+        return bringup_metrics(self.history[-1] if self.history else None, self.name, self.mode, ok) + gpu_text
 
     def _gpu_preflight(self, expected: int) -> Dict[str, Any]:
         if self.topology_override is not None:

@@ -55,6 +55,7 @@ _GPU_FIELDS = [("ecc_uncorrectable", "tk_gpu_ecc_uncorrectable_errors"),
 
 BRINGUP_FAMILIES: List[Tuple[str, str, str]] = [
     ("tk_agent_info", "gauge", "Node agent (always 1; labels: node, mode)"),
+    ("tk_agent_gpu_collect_success", "gauge", "1 if the agent read the GPUs' RAS counters for this scrape"),
     ("tk_bringup_duration_seconds", "gauge", "Wall time of the node's last bootstrap plan"),
     ("tk_bringup_success", "gauge", "1 if the node's last bootstrap plan succeeded"),
     ("tk_bringup_step_duration_seconds", "gauge", "Wall time of each step of the last bootstrap plan"),
@@ -132,10 +133,13 @@ def _flatten(prefix: str, obj: Any) -> List[Tuple[str, float]]:
     return []
 
 
-def bringup_metrics(plan_doc: Optional[Dict[str, Any]], node: str, mode: str = "") -> str:
+def bringup_metrics(plan_doc: Optional[Dict[str, Any]], node: str, mode: str = "",
+                    gpu_collect_ok: Optional[bool] = None) -> str:
     """Families of the node's last bootstrap plan (an agent ``run_plan`` result)."""
     exp = Exposition(BRINGUP_FAMILIES)
     exp.add("tk_agent_info", 1, node=node, mode=mode)
+    if gpu_collect_ok is not None:
+        exp.add("tk_agent_gpu_collect_success", 1 if gpu_collect_ok else 0, node=node)
     if not plan_doc:
         return exp.render()
     exp.add("tk_bringup_duration_seconds", float(plan_doc.get("ms", 0.0)) / 1e3, node=node)
