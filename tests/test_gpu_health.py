@@ -357,6 +357,18 @@ def test_health_cluster_reconciles_the_taint(tmp_path):
         again = make_ctx(dict(base, health_taint=True))
         cluster_health(again, backend)
         assert '"taint": "unchanged"' in again.out.getvalue() and "tainted" not in again.out.getvalue()
+        # NoExecute: the taint's effect changes and the pods running there are evicted --
+        # the device plugin too, so the sick node stops advertising GPUs
+        evict = make_ctx(dict(base, health_taint=True, health_taint_effect="noexecute"))
+        cluster_health(evict, backend)
+        assert '"taint": "tainted NoExecute"' in evict.out.getvalue()
+        k8s = {n["metadata"]["name"]: n for n in fake.k8s_nodes(cid)}
+        assert [t["effect"] for t in k8s["gpu-1"]["spec"]["taints"] if t["key"] == health.HEALTH_TAINT["key"]] == \
+            ["NoExecute"]
+        assert k8s["gpu-1"]["status"]["allocatable"].get("amd.com/gpu", "0") == "0"
+        assert k8s["gpu-2"]["status"]["allocatable"]["amd.com/gpu"] == "8"
+        with pytest.raises(ConfigError, match="health_taint_effect must be one of NoSchedule, NoExecute"):
+            cluster_health(make_ctx(dict(base, health_taint=True, health_taint_effect="PreferNoSchedule")), backend)
         # a limit given here overrides the node modules'
         lenient = make_ctx(dict(base, gpu_max_uncorrectable_ecc=5))
         assert all(v["status"] == "healthy" for v in cluster_health(lenient, backend))

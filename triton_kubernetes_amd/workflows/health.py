@@ -17,7 +17,13 @@ taint removed.  The RAS labels the bootstrap labeller set (``amd.com/gpu.ecc-unc
 ``.bad-pages``, ``.pcie-width``, ``.unhealthy-count``) are refreshed from the same verdict.  ``triton-kubernetes health cluster`` exits 0 either way; the verdict is
 in the output (``unhealthy: N``).
 
+``health_taint_effect: NoExecute`` (default ``NoSchedule``) also evicts the pods already
+running on an unhealthy node -- GPU jobs and the device plugin, so the node's
+``amd.com/gpu`` drops to 0 -- for a GPU that started logging uncorrectable errors under a
+running job; pods that tolerate the taint stay.
+
 Settings: ``cluster_manager``, ``cluster_name``, ``health_taint`` (default false),
+``health_taint_effect`` (``NoSchedule`` | ``NoExecute``),
 ``gpu_max_uncorrectable_ecc`` / ``gpu_max_retired_pages`` (override the node modules').
 """
 
@@ -69,20 +75,36 @@ def _probe(ctx: Context, state, host: str, cfg: Dict[str, Any]) -> Dict[str, Any
     return doc
 
 
-def _reconcile(client, cluster_id: str, node: Dict[str, Any], verdict: Dict[str, Any]) -> str:
+EFFECTS = ("NoSchedule", "NoExecute")
+
+
+def _effect(ctx: Context) -> str:
+    raw = ctx.get_string("health_taint_effect") if ctx.is_set("health_taint_effect") else "NoSchedule"
+    match = {e.lower(): e for e in EFFECTS}.get(str(raw).lower())
+    if match is None:
+        raise ConfigError(f"health_taint_effect must be one of {', '.join(EFFECTS)}. Found '{raw}'.")
+    return match
+
+
+def _reconcile(client, cluster_id: str, node: Dict[str, Any], verdict: Dict[str, Any],
+               effect: str = "NoSchedule") -> str:
     """Add / remove the health taint and set the labels; returns what changed ('' = nothing)."""
     name = node["metadata"]["name"]
+    current = [t for t in (node.get("spec") or {}).get("taints") or [] if t.get("key") == HEALTH_TAINT["key"]]
     taints = [t for t in (node.get("spec") or {}).get("taints") or [] if t.get("key") != HEALTH_TAINT["key"]]
     unhealthy = verdict["status"] != "healthy"
     if unhealthy:
-        taints.append(dict(HEALTH_TAINT))
+        taints.append(dict(HEALTH_TAINT, effect=effect))
     tainted = has_health_taint(node)
     want = health_labels(verdict)
     want.update(ras_labels(verdict.get("gpus") or []))
     have = (node.get("metadata") or {}).get("labels") or {}
-    if tainted == unhealthy and all(have.get(k) == v for k, v in want.items()):
+    same_effect = not unhealthy or [t.get("effect") for t in current] == [effect]
+    if tainted == unhealthy and same_effect and all(have.get(k) == v for k, v in want.items()):
         return ""
     client.patch_node(cluster_id, name, {"metadata": {"labels": want}, "spec": {"taints": taints}})
+    if tainted and unhealthy and not same_effect:
+        return f"tainted {effect}"
     if tainted == unhealthy:
         return "labelled"
     return "tainted" if unhealthy else "untainted"
@@ -116,6 +138,7 @@ def cluster_health(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
                              "gpus": []})
     fence = ctx.settings.get_bool("health_taint") if ctx.is_set("health_taint") else False
     if fence:
+        effect = _effect(ctx)
         from ..readiness.waiter import spec_from_state
 
         client, spec = spec_from_state(state, backend, key)
@@ -124,7 +147,7 @@ def cluster_health(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
             if v["status"] == "unknown" or v["node"] not in k8s:
                 v["taint"] = "skipped"
                 continue
-            v["taint"] = _reconcile(client, spec.cluster_id, k8s[v["node"]], v) or "unchanged"
+            v["taint"] = _reconcile(client, spec.cluster_id, k8s[v["node"]], v, effect) or "unchanged"
     for v in verdicts:
         ctx.echo(json.dumps({k: v.get(k) for k in ("node", "status", "reasons", "taint") if k in v}, sort_keys=True))
     bad = [v["node"] for v in verdicts if v["status"] == "unhealthy"]
