@@ -451,11 +451,12 @@ def test_get_nodes_shows_gpu_state(tmp_path):
         assert dispatch(table, backend, "get", "nodes") == 0
         lines = [ln for ln in table.out.getvalue().splitlines() if ln and not ln.startswith("get nodes")]
         assert lines[0].split() == ["NAME", "READY", "ROLES", "GPUS", "PRODUCT", "PARTITION", "BURN-IN", "XGMI",
-                                    "HEALTH"]
+                                    "PCIE", "UE/PAGES", "HEALTH"]
         rows = {ln.split()[0]: ln.split() for ln in lines[1:]}
         assert set(rows) == {"cp-1", "etcd-1", "gpu-1", "gpu-2"}
-        assert rows["gpu-1"][3:] == ["8/8", "MI355X", "spx/nps1", "passed(quick)", "mesh", "healthy"]
+        assert rows["gpu-1"][3:] == ["8/8", "MI355X", "spx/nps1", "passed(quick)", "mesh", "x16", "0/0", "healthy"]
         assert rows["gpu-2"][3] == "0/8" and rows["gpu-2"][-1] == "unhealthy,tainted"
+        assert rows["gpu-2"][-2] == "2/0"
         assert rows["cp-1"][1] == "Ready" and rows["cp-1"][3] == "-"
         js = make_ctx(dict(base, output="json"))
         dispatch(js, backend, "get", "nodes")

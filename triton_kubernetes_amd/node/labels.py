@@ -198,7 +198,8 @@ def synthetic_topology(ngpus: int = 8, hive: str = "0xabc123", product: str = "A
         gpus.append({
             "index": i, "market_name": product, "device_id": "0x75a3", "compute_units": cus, "vram_mb": vram_mb,
             "target_graphics_version": "gfx950", "compute_partition": "SPX", "memory_partition": "NPS1",
-            "xgmi_hive_id": hive, "ecc_uncorrectable": 0,
+            "xgmi_hive_id": hive, "ecc_uncorrectable": 0, "ecc_correctable": 0, "bad_pages": 0,
+            "bad_pages_pending": 0, "pcie_width": 16, "pcie_max_width": 16,
             "links": [{"peer": j, "type": "XGMI", "hops": 1, "p2p": True} for j in range(ngpus) if j != i],
         })
     return {"source": "synthetic", "gpus": gpus}

@@ -23,7 +23,8 @@ from ..errors import ConfigError
 from ..state import MANAGER_KEY
 from .select import executor_for, select_cluster, select_manager
 
-NODE_COLUMNS = ("NAME", "READY", "ROLES", "GPUS", "PRODUCT", "PARTITION", "BURN-IN", "XGMI", "HEALTH")
+NODE_COLUMNS = ("NAME", "READY", "ROLES", "GPUS", "PRODUCT", "PARTITION", "BURN-IN", "XGMI", "PCIE", "UE/PAGES",
+                "HEALTH")
 
 
 def get_manager(ctx: Context, backend: Backend) -> None:
@@ -49,7 +50,7 @@ def get_cluster(ctx: Context, backend: Backend) -> None:
 
 
 def _node_row(item: Dict[str, Any]) -> Dict[str, str]:
-    from ..node.health import HEALTH_LABEL, has_health_taint
+    from ..node.health import HEALTH_LABEL, HEALTH_TAINT, has_health_taint
 
     meta, status = item.get("metadata") or {}, item.get("status") or {}
     labels = meta.get("labels") or {}
@@ -69,8 +70,14 @@ def _node_row(item: Dict[str, Any]) -> Dict[str, str]:
                           if "amd.com/gpu.burnin-level" in labels else labels.get("amd.com/gpu.burnin", "-"))
         row["XGMI"] = labels.get("amd.com/xgmi.link-check") or (
             "mesh" if labels.get("amd.com/xgmi.fully-connected") == "true" else "-")
+        row["PCIE"] = f"x{labels['amd.com/gpu.pcie-width']}" if "amd.com/gpu.pcie-width" in labels else "-"
+        row["UE/PAGES"] = (f"{labels.get('amd.com/gpu.ecc-uncorrectable', '-')}/"
+                           f"{labels.get('amd.com/gpu.bad-pages', '-')}")
         health = labels.get(HEALTH_LABEL, "-")
-        row["HEALTH"] = health + (",tainted" if has_health_taint(item) else "")
+        effects = [t.get("effect") for t in (item.get("spec") or {}).get("taints") or []
+                   if t.get("key") == HEALTH_TAINT["key"]]
+        row["HEALTH"] = health + (",tainted" if has_health_taint(item) else "") + (
+            ",evicting" if "NoExecute" in effects else "")
     else:
         row.update({c: "-" for c in NODE_COLUMNS[3:]})
     return row
