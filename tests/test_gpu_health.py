@@ -487,3 +487,17 @@ def test_degraded_pcie_link(tmp_path, native_ok):
     with open(os.path.join(dev, "current_link_width"), "w") as fh:
         fh.write("16\n")
     assert _both(root)["status"] == "healthy"
+
+
+def test_vbios_label(tmp_path, native_ok):
+    """One VBIOS on every GPU is a label; GPUs flashed apart read ``mixed`` (both labellers)."""
+    root = healthy_tree(str(tmp_path), compute="CPX")
+    labels = topo.native_labels("sysfs", root)
+    assert labels["amd.com/gpu.vbios"] == "113-M3550101-100"
+    assert labels == labels_from_topology(topo.native_topology("sysfs", root))
+    with open(os.path.join(root, "sys/class/drm/renderD136/device/vbios_version"), "w") as fh:
+        fh.write("113-M3550101-102\n")
+    doc = topo.native_topology("sysfs", root)
+    assert {g.get("vbios_version") for g in doc["gpus"]} == {"113-M3550101-100", "113-M3550101-102", None}
+    labels = topo.native_labels("sysfs", root)
+    assert labels["amd.com/gpu.vbios"] == "mixed" and labels == labels_from_topology(doc)

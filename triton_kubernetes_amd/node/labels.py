@@ -23,6 +23,7 @@ plus xGMI keys used for topology-aware scheduling:
 ``amd.com/gpu.ecc-uncorrectable``      uncorrectable ECC errors, summed over physical GPUs
 ``amd.com/gpu.bad-pages``              retired VRAM pages (driver bad-page records), summed
 ``amd.com/gpu.pcie-width``             the narrowest GPU's PCIe link width (lanes)
+``amd.com/gpu.vbios``                  the GPUs' VBIOS version (``mixed`` when they differ)
 ``amd.com/gpu.health``                 ``healthy`` / ``unhealthy`` (node/health.py policy)
 =====================================  =============================================
 
@@ -118,6 +119,10 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     hives = {g.get("xgmi_hive_id") for g in gpus if g.get("xgmi_hive_id") not in (None, "", "0x0")}
     if len(hives) == 1:
         labels["amd.com/xgmi.hive-id"] = _label_value(hives.pop())
+    # one VBIOS on every GPU, or "mixed" (a node whose GPUs were flashed apart)
+    vbioses = {g["vbios_version"] for g in gpus if g.get("vbios_version")}
+    if vbioses:
+        labels["amd.com/gpu.vbios"] = _label_value(vbioses.pop()) if len(vbioses) == 1 else "mixed"
     xgmi_peers = []
     for g in gpus:
         peers = {lk["peer"] for lk in g.get("links", []) if lk.get("type") == "XGMI"}

@@ -74,6 +74,7 @@ struct Link {
 struct GpuInfo {
   int64_t hip_id = -1, drm_render = -1, drm_card = -1;
   std::string bdf, market_name, vendor_id, device_id, serial, gfx, compute_partition, memory_partition;
+  std::string vbios;  // VBIOS version (e.g. "113-M3550101-100"); "" not reported
   int64_t rev_id = -1, compute_units = -1, oam_id = -1, numa_node = -1;
   uint64_t vram_mb = 0;
   uint32_t vram_bit_width = 0;
@@ -196,6 +197,8 @@ Topology collect_amdsmi() {
         g.gfx = gb;
       }
     }
+    amdsmi_vbios_info_t vb{};
+    if (amdsmi_get_gpu_vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) g.vbios = vb.version;
     amdsmi_vram_info_t vram{};
     if (amdsmi_get_gpu_vram_info(h, &vram) == AMDSMI_STATUS_SUCCESS) {
       g.vram_mb = vram.vram_size;
@@ -409,6 +412,7 @@ Topology collect_sysfs(const std::string& root) {
     if (read_file(dev + "/current_memory_partition", &s)) g.memory_partition = s;
     if (read_file(dev + "/numa_node", &s)) g.numa_node = std::max<int64_t>(0, atoll(s.c_str()));
     if (read_file(dev + "/product_name", &s) && !s.empty()) g.market_name = s;
+    if (read_file(dev + "/vbios_version", &s)) g.vbios = s;
     // PCIe link (the PCI function's attributes, e.g. "32.0 GT/s PCIe" and "16")
     if (read_file(dev + "/current_link_width", &s) && isdigit((unsigned char)s[0])) g.pcie_width = atoll(s.c_str());
     if (read_file(dev + "/max_link_width", &s) && isdigit((unsigned char)s[0])) g.pcie_max_width = atoll(s.c_str());
@@ -570,6 +574,7 @@ std::string render_json(const Topology& t) {
     if (!g.device_id.empty()) appendf(o, ",\"device_id\":\"%s\"", g.device_id.c_str());
     if (g.rev_id >= 0) appendf(o, ",\"rev_id\":%" PRId64, g.rev_id);
     if (!g.serial.empty()) appendf(o, ",\"asic_serial\":\"%s\"", esc(g.serial).c_str());
+    if (!g.vbios.empty()) appendf(o, ",\"vbios_version\":\"%s\"", esc(g.vbios).c_str());
     if (g.compute_units >= 0) appendf(o, ",\"compute_units\":%" PRId64, g.compute_units);
     if (g.oam_id >= 0) appendf(o, ",\"oam_id\":%" PRId64, g.oam_id);
     if (!g.gfx.empty()) appendf(o, ",\"target_graphics_version\":\"%s\"", g.gfx.c_str());
@@ -860,7 +865,7 @@ std::string render_labels(const Topology& t) {
     L["amd.com/gpu.count"] = std::to_string(physical);
     L["amd.com/gpu.logical-count"] = std::to_string(gs.size());
     if (gs.size() % physical == 0) L["amd.com/gpu.partitions-per-gpu"] = std::to_string(gs.size() / physical);
-    std::set<std::string> names, dev_ids, targets, cparts, mparts, hives;
+    std::set<std::string> names, dev_ids, targets, cparts, mparts, hives, vbioses;
     int64_t min_cu = INT64_MAX;
     uint64_t min_vram = UINT64_MAX;
     size_t min_xgmi = SIZE_MAX;
@@ -873,6 +878,7 @@ std::string render_labels(const Topology& t) {
       if (!g.compute_partition.empty()) cparts.insert(lower(g.compute_partition));
       if (!g.memory_partition.empty()) mparts.insert(lower(g.memory_partition));
       if (g.has_xgmi && g.hive_id) hives.insert(hex64(g.hive_id));
+      if (!g.vbios.empty()) vbioses.insert(g.vbios);
       std::set<size_t> peers;
       for (const auto& l : g.links)
         if (l.type == "XGMI") peers.insert(l.peer);
@@ -891,6 +897,8 @@ std::string render_labels(const Topology& t) {
     if (cparts.size() == 1) L["amd.com/gpu.compute-partition"] = label_value(*cparts.begin());
     if (mparts.size() == 1) L["amd.com/gpu.memory-partition"] = label_value(*mparts.begin());
     if (hives.size() == 1) L["amd.com/xgmi.hive-id"] = label_value(*hives.begin());
+    // one VBIOS on every GPU, or "mixed" (a node whose GPUs were flashed apart)
+    if (!vbioses.empty()) L["amd.com/gpu.vbios"] = vbioses.size() == 1 ? label_value(*vbioses.begin()) : "mixed";
     L["amd.com/xgmi.links-per-gpu"] = std::to_string(min_xgmi);
     // a compute partition is not a whole GPU with its own xGMI links: SPX only
     const bool whole = (cparts.empty() || (cparts.size() == 1 && *cparts.begin() == "spx")) && physical == gs.size();
