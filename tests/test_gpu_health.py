@@ -493,11 +493,11 @@ def test_vbios_label(tmp_path, native_ok):
     """One VBIOS on every GPU is a label; GPUs flashed apart read ``mixed`` (both labellers)."""
     root = healthy_tree(str(tmp_path), compute="CPX")
     labels = topo.native_labels("sysfs", root)
-    assert labels["amd.com/gpu.vbios"] == "113-M3550101-100"
+    assert labels["amd.com/gpu.vbios"] == "113-M355-01-1K1-020F"
     assert labels == labels_from_topology(topo.native_topology("sysfs", root))
     with open(os.path.join(root, "sys/class/drm/renderD136/device/vbios_version"), "w") as fh:
-        fh.write("113-M3550101-102\n")
+        fh.write("113-M355-01-1K1-021F\n")
     doc = topo.native_topology("sysfs", root)
-    assert {g.get("vbios_version") for g in doc["gpus"]} == {"113-M3550101-100", "113-M3550101-102", None}
+    assert {g.get("vbios_version") for g in doc["gpus"]} == {"113-M355-01-1K1-020F", "113-M355-01-1K1-021F", None}
     labels = topo.native_labels("sysfs", root)
     assert labels["amd.com/gpu.vbios"] == "mixed" and labels == labels_from_topology(doc)

@@ -74,7 +74,7 @@ struct Link {
 struct GpuInfo {
   int64_t hip_id = -1, drm_render = -1, drm_card = -1;
   std::string bdf, market_name, vendor_id, device_id, serial, gfx, compute_partition, memory_partition;
-  std::string vbios;  // VBIOS version (e.g. "113-M3550101-100"); "" not reported
+  std::string vbios;  // VBIOS version (e.g. "113-M355-01-1K1-020F"); "" not reported
   int64_t rev_id = -1, compute_units = -1, oam_id = -1, numa_node = -1;
   uint64_t vram_mb = 0;
   uint32_t vram_bit_width = 0;
@@ -198,7 +198,9 @@ Topology collect_amdsmi() {
       }
     }
     amdsmi_vbios_info_t vb{};
-    if (amdsmi_get_gpu_vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) g.vbios = vb.version;
+    // sysfs vbios_version is amd_smi's part_number ("113-M355-01-1K1-020F" on the box);
+    // amd_smi's version field is a build number
+    if (amdsmi_get_gpu_vbios_info(h, &vb) == AMDSMI_STATUS_SUCCESS) g.vbios = vb.part_number[0] ? vb.part_number : vb.version;
     amdsmi_vram_info_t vram{};
     if (amdsmi_get_gpu_vram_info(h, &vram) == AMDSMI_STATUS_SUCCESS) {
       g.vram_mb = vram.vram_size;
