@@ -501,3 +501,29 @@ def test_vbios_label(tmp_path, native_ok):
     assert {g.get("vbios_version") for g in doc["gpus"]} == {"113-M355-01-1K1-020F", "113-M355-01-1K1-021F", None}
     labels = topo.native_labels("sysfs", root)
     assert labels["amd.com/gpu.vbios"] == "mixed" and labels == labels_from_topology(doc)
+
+
+def test_readiness_reports_gpu_nodes_that_differ(tmp_path):
+    """Two MI355X nodes flashed with different VBIOS: the cluster is ready, and the report
+    and the CLI warn about it (``readiness/waiter.py:gpu_mismatch``)."""
+    from triton_kubernetes_amd.readiness.waiter import gpu_mismatch
+
+    fake, agents, backend, ctx, new_cluster = _create(tmp_path, "off")
+    try:
+        for agent, vb in ((agents[1], "113-M355-01-1K1-020F"), (agents[2], "113-M355-01-1K1-021F")):
+            for g in agent.topology_override["gpus"]:
+                g["vbios_version"] = vb
+        new_cluster(ctx, backend)
+        rep = ctx.extras["last_readiness"]
+        assert rep.gpu_mismatch == {"amd.com/gpu.vbios": {"113-M355-01-1K1-020F": ["gpu-1"],
+                                                          "113-M355-01-1K1-021F": ["gpu-2"]}}
+        assert "warning: MI355X nodes differ in amd.com/gpu.vbios" in ctx.out.getvalue()
+        assert rep.rccl["ok"]  # a warning, not a failed readiness
+    finally:
+        for a in agents:
+            a.stop()
+        fake.stop()
+    # non-GPU nodes are not compared; a label one node lacks reads "-"
+    assert gpu_mismatch({"cp": {"amd.com/gpu.present": "false"},
+                         "a": {"amd.com/gpu.present": "true", "amd.com/gpu.vram": "288G"},
+                         "b": {"amd.com/gpu.present": "true"}}) == {"amd.com/gpu.vram": {"288G": ["a"], "-": ["b"]}}

@@ -20,6 +20,11 @@ Phases, each time-stamped (the BASELINE.json metric is ``ready - start``):
                         cannot run the report says why (``rccl.skipped``).
 
 Polling is adaptive (20 ms doubling to 1 s), not the reference's fixed 5 s.
+
+The report also lists the GPU-node labels that differ across the cluster's MI355X nodes
+(``gpu_mismatch``: product, VBIOS, ISA target, partition modes, HBM, CUs, RDMA fabric):
+one RCCL job over nodes flashed or partitioned apart is a classic source of hangs and
+uneven bandwidth.  It is a warning, not a failed readiness.
 """
 
 import json
@@ -59,6 +64,8 @@ class ReadinessReport:
     nodes: Dict[str, Dict[str, Any]] = field(default_factory=dict)
     rccl: Optional[Dict[str, Any]] = None
     gpu_unhealthy: List[str] = field(default_factory=list)  # GPU nodes that joined health-tainted
+    # label -> value -> GPU nodes, for labels whose value differs across the GPU nodes
+    gpu_mismatch: Dict[str, Dict[str, List[str]]] = field(default_factory=dict)
 
     @property
     def ready_seconds(self) -> float:
@@ -69,6 +76,26 @@ class ReadinessReport:
         d["phase_seconds"] = {k: round(v - self.start, 4) for k, v in self.phases.items()}
         d["ready_seconds"] = round(self.ready_seconds, 4)
         return d
+
+
+# node labels every MI355X node of one cluster should share (node/labels.py)
+UNIFORM_LABELS = ("amd.com/gpu.product-name", "amd.com/gpu.vbios", "amd.com/gpu.target",
+                  "amd.com/gpu.compute-partition", "amd.com/gpu.memory-partition", "amd.com/gpu.vram",
+                  "amd.com/gpu.cu-count", "amd.com/rdma.link-layer", "amd.com/rdma.rate-gbps")
+
+
+def gpu_mismatch(node_labels: Dict[str, Dict[str, str]]) -> Dict[str, Dict[str, List[str]]]:
+    """The :data:`UNIFORM_LABELS` whose values differ across GPU nodes (``amd.com/gpu.present``);
+    a node without the label counts as ``"-"`` when another node has it."""
+    gpu = {n: lab for n, lab in node_labels.items() if lab.get("amd.com/gpu.present") == "true"}
+    out: Dict[str, Dict[str, List[str]]] = {}
+    for key in UNIFORM_LABELS:
+        by: Dict[str, List[str]] = {}
+        for n in sorted(gpu):
+            by.setdefault(gpu[n].get(key, "-"), []).append(n)
+        if len(by) > 1:
+            out[key] = by
+    return out
 
 
 def _node_ready(item: Dict[str, Any]) -> bool:
@@ -134,6 +161,7 @@ def wait_ready(client: RancherClient, spec: ReadinessSpec, start: Optional[float
         it = items.get(name, {})
         rep.nodes[name] = {"labels": (it.get("metadata") or {}).get("labels", {}),
                            "allocatable": (it.get("status") or {}).get("allocatable", {})}
+    rep.gpu_mismatch = gpu_mismatch({n: d["labels"] for n, d in rep.nodes.items()})
 
     if spec.rccl_gate and rccl_hosts:
         if gate is None:
@@ -315,8 +343,11 @@ def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[flo
     if rep.gpu_unhealthy:
         ctx.echo("GPU nodes joined with the health taint (no GPU pods, not in the RCCL gate): "
                  + ", ".join(rep.gpu_unhealthy) + " -- see `triton-kubernetes health cluster`")
+    for key, by in sorted(rep.gpu_mismatch.items()):
+        ctx.echo(f"warning: MI355X nodes differ in {key}: "
+                 + "; ".join(f"{v}: {', '.join(ns)}" for v, ns in sorted(by.items())))
     return rep
 
 
-__all__ = ["ReadinessSpec", "ReadinessReport", "wait_ready", "rccl_gate", "spec_from_state", "wait_after_create",
+__all__ = ["ReadinessSpec", "ReadinessReport", "UNIFORM_LABELS", "gpu_mismatch", "wait_ready", "rccl_gate", "spec_from_state", "wait_after_create",
            "early_gate", "agent_transport_for", "gate_sizes"]
