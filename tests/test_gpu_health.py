@@ -493,7 +493,8 @@ def test_vbios_label(tmp_path, native_ok):
     """One VBIOS on every GPU is a label; GPUs flashed apart read ``mixed`` (both labellers)."""
     root = healthy_tree(str(tmp_path), compute="CPX")
     labels = topo.native_labels("sysfs", root)
-    assert labels["amd.com/gpu.vbios"] == "113-M355-01-1K1-020F"
+    assert labels["amd.com/gpu.vbios"] == "113-M355-01-1K1-020F" and labels["amd.com/rocm.version"] == "7.2.0-43"
+    assert topo.native_topology("sysfs", root)["rocm"] == {"version": "7.2.0-43"}
     assert labels == labels_from_topology(topo.native_topology("sysfs", root))
     with open(os.path.join(root, "sys/class/drm/renderD136/device/vbios_version"), "w") as fh:
         fh.write("113-M355-01-1K1-021F\n")

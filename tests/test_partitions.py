@@ -33,6 +33,7 @@ def make_tree(root, ngpu=8, compute="SPX", memory="NPS1"):
     mparts = partition.MEMORY_PARTITIONS[memory.lower()]
     nodes = os.path.join(root, "sys/class/kfd/kfd/topology/nodes")
     _write(f"{nodes}/0/properties", "cpu_cores_count 96\nsimd_count 0\nmem_banks_count 1\n")
+    _write(os.path.join(root, "opt/rocm/.info/version"), "7.2.0-43\n")
     kfd = 0
     for g in range(ngpu):
         for p in range(parts):

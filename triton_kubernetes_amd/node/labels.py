@@ -24,6 +24,7 @@ plus xGMI keys used for topology-aware scheduling:
 ``amd.com/gpu.bad-pages``              retired VRAM pages (driver bad-page records), summed
 ``amd.com/gpu.pcie-width``             the narrowest GPU's PCIe link width (lanes)
 ``amd.com/gpu.vbios``                  the GPUs' VBIOS version (``mixed`` when they differ)
+``amd.com/rocm.version``               the node's ROCm userspace (``<ROCM_PATH>/.info/version``)
 ``amd.com/gpu.health``                 ``healthy`` / ``unhealthy`` (node/health.py policy)
 =====================================  =============================================
 
@@ -87,6 +88,9 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
         "amd.com/gpu.count": str(physical),
         "amd.com/gpu.logical-count": str(len(gpus)),
     }
+    rocm = (doc.get("rocm") or {}).get("version")
+    if rocm:
+        labels["amd.com/rocm.version"] = _label_value(rocm)
     if len(gpus) % physical == 0:
         labels["amd.com/gpu.partitions-per-gpu"] = str(len(gpus) // physical)
     names = {product_name(g.get("market_name", ""), g.get("device_id", "")) for g in gpus

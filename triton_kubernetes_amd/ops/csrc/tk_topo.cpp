@@ -107,6 +107,7 @@ struct Topology {
   int status = 0;
   std::string error;
   std::string driver_name, driver_version;
+  std::string rocm_version;  // the node's ROCm userspace (<ROCM_PATH>/.info/version)
   std::vector<GpuInfo> gpus;
   std::vector<NicInfo> nics;
 };
@@ -562,6 +563,7 @@ std::string render_json(const Topology& t) {
   if (!t.driver_name.empty())
     appendf(o, "\"driver\":{\"name\":\"%s\",\"version\":\"%s\"},", esc(t.driver_name).c_str(),
             esc(t.driver_version).c_str());
+  if (!t.rocm_version.empty()) appendf(o, "\"rocm\":{\"version\":\"%s\"},", esc(t.rocm_version).c_str());
   o += "\"gpus\":[";
   for (size_t i = 0; i < t.gpus.size(); ++i) {
     const GpuInfo& g = t.gpus[i];
@@ -859,6 +861,7 @@ std::string render_labels(const Topology& t) {
     L["amd.com/gpu.present"] = "false";
   } else {
     L["amd.com/gpu.present"] = "true";
+    if (!t.rocm_version.empty()) L["amd.com/rocm.version"] = label_value(t.rocm_version);
     // physical GPUs = distinct PCI functions (a GPU's compute partitions share one);
     // = node/labels.py and node/partition.py:physical_count
     std::set<std::string> bdfs;
@@ -971,6 +974,12 @@ Topology collect(const char* source, const char* root) {
   const std::string r = (root && *root) ? root : "";
   Topology t = collect_gpus(source ? source : "auto", r);
   t.nics = collect_nics(r);
+  // ROCm userspace version: the live system's ROCM_PATH, a fixture tree's /opt/rocm
+  const char* rp = getenv("ROCM_PATH");
+  const std::string info = r.empty() ? std::string(rp && *rp ? rp : "/opt/rocm") + "/.info/version"
+                                     : r + "/opt/rocm/.info/version";
+  std::string v;
+  if (read_file(info, &v)) t.rocm_version = v;
   return t;
 }
 
