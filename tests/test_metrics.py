@@ -228,6 +228,17 @@ def test_textfile_setting_in_both_delivery_paths(tmp_path):
 
 
 @pytest.mark.gpu
+def test_gpu_metrics_cli_on_the_box(capsys):
+    from triton_kubernetes_amd.ops.cli import main
+
+    for source in ("sysfs", "amdsmi"):
+        assert main(["metrics", "--node", "box", "--source", source]) == 0
+        text = capsys.readouterr().out
+        s = _samples(text)
+        assert s[("tk_node_unhealthy_gpus", (("node", "box"),))] >= 0 and "tk_gpu_healthy" in text
+
+
+@pytest.mark.gpu
 def test_prom_on_the_box():
     """Both collectors' --prom text on the MI355X equals the Python rendering of that
     collector's verdict, and parses."""

@@ -103,7 +103,7 @@ def build_parser() -> argparse.ArgumentParser:
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
-    g = sub.add_parser("gpu", help="MI355X node probes (burnin, topology, labels, health, rccl-local, rccl-slim, links, "
+    g = sub.add_parser("gpu", help="MI355X node probes (burnin, topology, labels, health, metrics, rccl-local, rccl-slim, links, "
                                       "hbm, mfma, gemm)")
     g.add_argument("gpu_args", nargs=argparse.REMAINDER)
     a = sub.add_parser("agent", help="Run the node agent (tk-node-agent)")

@@ -4,14 +4,15 @@
     python -m triton_kubernetes_amd.ops.cli topology
     python -m triton_kubernetes_amd.ops.cli labels
     python -m triton_kubernetes_amd.ops.cli health [--max-uncorrectable N] [--max-bad-pages N|auto] [--source sysfs|amdsmi]
+    python -m triton_kubernetes_amd.ops.cli metrics [--node NAME] [--max-uncorrectable N] [--max-bad-pages N|auto] [--source ...]
     python -m triton_kubernetes_amd.ops.cli rccl-local [--ngpus N]
     python -m triton_kubernetes_amd.ops.cli links [--min-frac F] [--min-gbps G] [--method kernel-read|sdma-copy] [--mib M]
     python -m triton_kubernetes_amd.ops.cli hbm|mfma [...] [--clock]
     python -m triton_kubernetes_amd.ops.cli rccl-slim [--source DIR] [--root DIR] [--no-verify]
     python -m triton_kubernetes_amd.ops.cli gemm [--size N] [--reps R] [--schedule staggered|single-barrier] [--dtype bf16|fp8]
 
-Every command prints one JSON document; the exit status is non-zero when the
-GPU(s) fail the gate.
+Every command prints one JSON document (``metrics``: Prometheus text); the exit status is
+non-zero when the GPU(s) fail the gate.
 """
 
 import argparse
@@ -33,6 +34,11 @@ def main(argv: Sequence[str] = ()) -> int:
     hl.add_argument("--max-uncorrectable", type=int, default=0)
     hl.add_argument("--max-bad-pages", default="auto", help="a count, or auto (the driver's default threshold)")
     hl.add_argument("--source", default="sysfs", choices=["sysfs", "amdsmi"])
+    mt = sub.add_parser("metrics", help="GPU health as Prometheus text (node/metrics.py; what the textfile timer writes)")
+    mt.add_argument("--node", default="", help="the node label (default: the host name)")
+    mt.add_argument("--max-uncorrectable", type=int, default=0)
+    mt.add_argument("--max-bad-pages", default="auto")
+    mt.add_argument("--source", default="sysfs", choices=["sysfs", "amdsmi"])
     r = sub.add_parser("rccl-local")
     r.add_argument("--ngpus", type=int, default=0)
     r.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
@@ -95,6 +101,18 @@ def main(argv: Sequence[str] = ()) -> int:
         verdict = evaluate(doc, max_ue, max_bad)
         print(json.dumps(verdict, indent=2))
         return 0 if verdict["status"] == "healthy" else 3
+    if args.cmd == "metrics":
+        import socket
+
+        from ..node.health import evaluate, limits_of
+        from ..node.metrics import gpu_metrics
+        from . import topo
+
+        max_ue, max_bad = limits_of({"gpu_max_uncorrectable_ecc": args.max_uncorrectable,
+                                     "gpu_max_retired_pages": args.max_bad_pages})
+        doc = topo.native_topology("sysfs") if args.source == "sysfs" else topo.amdsmi_topology()
+        sys.stdout.write(gpu_metrics(evaluate(doc, max_ue, max_bad), args.node or socket.gethostname()))
+        return 0
     if args.cmd == "rccl-local":
         from . import probe, rccl
 
