@@ -66,6 +66,9 @@ def test_partitions_are_one_gpu_each(tmp_path, native_ok):
     root = healthy_tree(str(tmp_path), compute="CPX")  # 8 partitions per GPU
     text = _native_prom(root, 'odd"name')
     assert text == metrics.gpu_metrics(topo.native_health("sysfs", root), 'odd"name')
+    weird = 'a\\b\nc"d'  # backslash, newline, quote: escaped alike by both
+    assert _native_prom(root, weird) == metrics.gpu_metrics(topo.native_health("sysfs", root), weird)
+    assert dict(next(k for k in _samples(_native_prom(root, weird)) if k[0] == "tk_node_unhealthy_gpus")[1])["node"] == weird
     healthy = [k for k in _samples(text) if k[0] == "tk_gpu_healthy"]
     assert len(healthy) == 8 and dict(healthy[0][1])["node"] == 'odd"name'
 
