@@ -25,6 +25,7 @@ import base64
 import hashlib
 import json
 import time
+import urllib.parse
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional
 
@@ -348,6 +349,23 @@ class RancherClient:
                                  data=json.dumps(patch).encode(),
                                  headers={"Content-Type": "application/merge-patch+json"}, ok=(200,))
         return resp.json()
+
+    def cordon(self, cluster_id: str, name: str, unschedulable: bool = True) -> Dict[str, Any]:
+        """``kubectl cordon`` / ``uncordon``: ``spec.unschedulable`` of the Node."""
+        return self.patch_node(cluster_id, name, {"spec": {"unschedulable": unschedulable}})
+
+    def node_pods(self, cluster_id: str, name: str) -> List[Dict[str, Any]]:
+        """Every pod bound to node ``name`` (all namespaces; a field selector)."""
+        q = urllib.parse.urlencode({"fieldSelector": f"spec.nodeName={name}"})
+        return (self.k8s(cluster_id, "GET", f"/api/v1/pods?{q}") or {}).get("items", [])
+
+    def evict_pod(self, cluster_id: str, namespace: str, name: str) -> int:
+        """POST an Eviction (policy/v1): 201 evicted, 429 refused by a PodDisruptionBudget
+        (retry later), 404 already gone."""
+        body = {"apiVersion": "policy/v1", "kind": "Eviction", "metadata": {"name": name, "namespace": namespace}}
+        resp = self.http.request("POST", f"/k8s/clusters/{cluster_id}/api/v1/namespaces/{namespace}/pods/{name}/eviction",
+                                 json_body=body, ok=(200, 201, 404, 429))
+        return resp.status
 
     def kubeconfig(self, cluster_id: str) -> str:
         data = self.http.post_json(f"/v3/clusters/{cluster_id}?action=generateKubeconfig", {})

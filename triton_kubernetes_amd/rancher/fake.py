@@ -330,7 +330,8 @@ class FakeRancher:
                     alloc["amd.com/gpu"] = str(gpus)
                 items.append({
                     "metadata": {"name": n["hostname"], "labels": self._node_labels(n)},
-                    "spec": {"taints": list(n.get("taints") or [])},
+                    "spec": dict({"taints": list(n.get("taints") or [])},
+                                 **({"unschedulable": True} if n.get("unschedulable") else {})),
                     "status": {"conditions": [{"type": "Ready", "status": "True" if ready else "False"}],
                                "allocatable": alloc, "capacity": dict(alloc)},
                 })
@@ -551,7 +552,7 @@ class FakeRancher:
                     st.cluster_nodes.get(n["clusterId"], {}).pop(n["id"], None)
             return 200, {}
         if path.startswith("/k8s/clusters/"):
-            return self._k8s(method, path, body)
+            return self._k8s(method, path, body, query)
         return 404, {"type": "error", "code": "NotFound", "path": path}
 
     def _admit(self, cid: str, namespace: str, pod: Dict[str, Any]) -> Dict[str, Any]:
@@ -684,7 +685,7 @@ class FakeRancher:
         self._refresh()
         return 201, {"id": nid, "clusterId": reg["clusterId"]}
 
-    def _k8s(self, method: str, path: str, body: Any) -> Tuple[int, Any]:
+    def _k8s(self, method: str, path: str, body: Any, query: Optional[Dict[str, List[str]]] = None) -> Tuple[int, Any]:
         st = self.state
         rest = path[len("/k8s/clusters/"):]
         cid, _, kpath = rest.partition("/")
@@ -696,6 +697,19 @@ class FakeRancher:
             return 200, {"kind": "NodeList", "items": self.k8s_nodes(cid)}
         if kpath.startswith("/api/v1/nodes/") and method == "PATCH":
             return self._patch_node(cid, kpath[len("/api/v1/nodes/"):], body)
+        if kpath == "/api/v1/pods" and method == "GET":
+            # every namespace's pods; the one field selector drain uses (spec.nodeName=...)
+            sel = dict(s.split("=", 1) for s in ((query or {}).get("fieldSelector") or [""])[0].split(",") if "=" in s)
+            with st.mu:
+                pods = [st.objects[k] for k in st.cluster_objects.get(cid, ())
+                        if k.split("|")[1].startswith("/api/v1/namespaces/") and k.split("|")[1].endswith("/pods")]
+            if "spec.nodeName" in sel:
+                pods = [p for p in pods if (p.get("spec") or {}).get("nodeName") == sel["spec.nodeName"]]
+            return 200, {"kind": "PodList", "items": pods}
+        parts = kpath.strip("/").split("/")
+        if (method == "POST" and len(parts) == 7 and parts[:3] == ["api", "v1", "namespaces"] and parts[4] == "pods"
+                and parts[6] == "eviction"):
+            return self._evict(cid, parts[3], parts[5])
         if kpath == "/version":
             with st.mu:
                 v = (st.clusters[cid].get("version") or {}).get("gitVersion") or DEFAULT_K8S_VERSION
@@ -771,6 +785,8 @@ class FakeRancher:
                 else:
                     node["labels"][k] = str(v)
             spec = patch.get("spec") or {}
+            if "unschedulable" in spec:  # cordon / uncordon
+                node["unschedulable"] = bool(spec["unschedulable"])
             if "taints" in spec:
                 taints = [dict(t) for t in spec["taints"] or [] if isinstance(t, dict)]
                 added = node.setdefault("taint_added", {})
@@ -781,6 +797,32 @@ class FakeRancher:
                 node["taints"] = taints
         items = {i["metadata"]["name"]: i for i in self.k8s_nodes(cid)}
         return 200, items[name]
+
+
+    # a pod annotated with this many refusals answers 429 (a PodDisruptionBudget at its
+    # minimum) that many times before the eviction goes through; "always" never does
+    PDB_ANNOTATION = "fake.triton-kubernetes.io/pdb-refusals"
+
+    def _evict(self, cid: str, namespace: str, name: str) -> Tuple[int, Any]:
+        """The Eviction subresource: the pod is deleted unless its budget refuses (429)."""
+        st = self.state
+        key = f"{cid}|/api/v1/namespaces/{namespace}/pods|{name}"
+        with st.mu:
+            pod = st.objects.get(key)
+            if pod is None:
+                return 404, {"kind": "Status", "reason": "NotFound", "code": 404}
+            ann = (pod.get("metadata") or {}).setdefault("annotations", {})
+            left = ann.get(self.PDB_ANNOTATION)
+            if left == "always" or (left and int(left) > 0):
+                if left != "always":
+                    ann[self.PDB_ANNOTATION] = str(int(left) - 1)
+                st.evictions_refused = getattr(st, "evictions_refused", 0) + 1
+                return 429, {"kind": "Status", "reason": "TooManyRequests", "code": 429,
+                             "message": "Cannot evict pod as it would violate the pod's disruption budget."}
+            st.objects.pop(key)
+            st.object_times.pop(key, None)
+            st.cluster_objects.get(cid, {}).pop(key, None)
+        return 201, {"kind": "Status", "status": "Success", "code": 201}
 
 
 class _Rejected(Exception):

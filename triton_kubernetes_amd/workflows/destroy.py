@@ -13,6 +13,10 @@ Extension (opt-in via ``rancher_cleanup: true``): also
 remove the cluster object (``destroy cluster``) or the node's object (``destroy node``:
 the Rancher node with that hostname, which also drops it from the Kubernetes node list)
 from Rancher after the destroy.
+
+``destroy node`` with ``drain: true`` first cordons the node and evicts its pods through
+the Eviction API (``workflows/drain.py``; ``drain_timeout`` seconds, default 600): the jobs
+on a GPU node being replaced are rescheduled before its host goes away.
 """
 
 from ..backend.base import Backend
@@ -80,6 +84,16 @@ def delete_node(ctx: Context, backend: Backend) -> None:
     if not ctx.confirm(f'Are you sure you want to destroy "{hostname}"', f'Destroy "{hostname}"'):
         ctx.echo("Destroy node canceled.")
         return
+    if ctx.settings.get_bool("drain"):
+        # before the lock: a drain waits on disruption budgets, the document is not touched
+        client, cid = _rancher_client(ctx, backend, state, key)
+        if client is None:
+            raise ConfigError(f"drain: cluster of {hostname} has no Rancher outputs yet (was it applied?)")
+        from .drain import drain_node
+
+        timeout = float(ctx.settings.get_string("drain_timeout") or 600)
+        with span("destroy.drain", node=hostname):
+            drain_node(client, cid, hostname, timeout, ctx.echo)
     with backend.lock(manager):
         state = _reread(backend, manager, node_key)
         cleanup = _rancher_node_cleanup_info(ctx, backend, state, key, hostname)
@@ -97,6 +111,21 @@ def _reread(backend: Backend, manager: str, key: str):
     if state.module(key) is None:
         raise ConfigError(f"module.{key} was removed by another triton-kubernetes run.")
     return state
+
+
+def _rancher_client(ctx: Context, backend: Backend, state, cluster_key: str):
+    """``(RancherClient, cluster id)`` from the executor's recorded outputs, or ``(None, "")``."""
+    from ..executor.base import outputs_from_tfstate
+    from ..rancher.client import RancherClient
+    from ..state import MANAGER_KEY
+
+    raw = backend.read_tfstate(state.name)
+    mgr = outputs_from_tfstate(raw, MANAGER_KEY)
+    cid = outputs_from_tfstate(raw, cluster_key).get("rancher_cluster_id")
+    if not mgr.get("rancher_url") or not cid:
+        return None, ""
+    factory = ctx.extras.get("rancher_factory") or RancherClient
+    return factory(mgr["rancher_url"], mgr.get("rancher_access_key", ""), mgr.get("rancher_secret_key", "")), cid
 
 
 def _rancher_node_cleanup_info(ctx: Context, backend: Backend, state, cluster_key: str, hostname: str):
