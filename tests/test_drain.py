@@ -96,3 +96,25 @@ def test_client_drain_primitives(env):  # noqa: F811 - fixture
     client.cordon(cid, "gpu-1")
     client.cordon(cid, "gpu-1", False)
     assert "unschedulable" not in next(n for n in client.k8s_nodes(cid) if n["metadata"]["name"] == "gpu-1")["spec"]
+
+
+def test_drain_cordon_uncordon_commands(env):  # noqa: F811 - fixture
+    from triton_kubernetes_amd.cli.main import dispatch
+
+    fake, agent, backend, base = env
+    cid = _cluster(fake, agent, backend, base)
+    _post(fake, cid, _pod("train-0", "gpu-1", ns="ml"))
+    sel = dict(base, cluster_manager="mgr", cluster_name="dev", hostname="gpu-1")
+
+    def unschedulable():
+        return next(n for n in fake.k8s_nodes(cid) if n["metadata"]["name"] == "gpu-1")["spec"].get("unschedulable")
+
+    ctx = make_ctx(sel)
+    assert dispatch(ctx, backend, "drain", "node") == 0
+    assert "Drained gpu-1: evicted 1 pod(s)" in output(ctx) and _pods_on(fake, cid, "gpu-1") == []
+    assert unschedulable() is True
+    assert "gpu-1" in backend.state("mgr").nodes("cluster_baremetal_dev")  # still in the cluster
+    ctx = make_ctx(sel)
+    assert dispatch(ctx, backend, "uncordon", "node") == 0 and "gpu-1 uncordoned" in output(ctx)
+    assert unschedulable() is None
+    assert dispatch(make_ctx(sel), backend, "cordon", "node") == 0 and unschedulable() is True

@@ -48,10 +48,14 @@ VALID = {
     "migrate": ["manager"],
     "credentials": ["node"],
     "health": ["cluster"],
+    "drain": ["node"],
+    "cordon": ["node"],
+    "uncordon": ["node"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
 _ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
-             "restore": "restore", "userdata": "userdata", "migrate": "migrate", "credentials": "credentials", "health": "health"}
+             "restore": "restore", "userdata": "userdata", "migrate": "migrate", "credentials": "credentials", "health": "health",
+             "drain": "drain", "cordon": "cordon", "uncordon": "uncordon"}
 
 
 class ArgError(Exception):
@@ -99,7 +103,10 @@ def build_parser() -> argparse.ArgumentParser:
                        ("credentials", "Issue a node agent's TLS certificate, token and image allow-list "
                                        "(signed by the cluster manager's agent CA)"),
                        ("health", "Re-read the GPU health (ECC, retired pages) of a cluster's MI355X nodes and, "
-                                  "with health_taint, fence unhealthy ones")):
+                                  "with health_taint, fence unhealthy ones"),
+                       ("drain", "Cordon a node and evict its pods (disruption budgets honoured)"),
+                       ("cordon", "Mark a node unschedulable"),
+                       ("uncordon", "Mark a node schedulable again")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
@@ -210,6 +217,14 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         from ..workflows.health import cluster_health
 
         cluster_health(ctx, backend)
+    elif command == "drain":
+        from ..workflows.drain import drain_command
+
+        drain_command(ctx, backend)
+    elif command in ("cordon", "uncordon"):
+        from ..workflows.drain import cordon_command
+
+        cordon_command(ctx, backend, command == "cordon")
     elif command == "wait":
         from ..readiness.waiter import wait_after_create
         from ..workflows.select import select_cluster, select_manager

@@ -14,6 +14,9 @@ done through Rancher's Kubernetes API:
 
 A drain that does not finish in time fails the destroy *before* anything is destroyed
 (the node stays cordoned, its module and host are untouched) and names the pods left.
+
+The same steps are day-2 commands on their own: ``drain node`` (cordon + evict, e.g. before
+a firmware update), ``cordon node`` and ``uncordon node`` (back into scheduling).
 """
 
 import time
@@ -71,4 +74,34 @@ def drain_node(client: Any, cluster_id: str, name: str, timeout: float = 600.0,
     return out
 
 
-__all__ = ["drain_node"]
+def _target(ctx, backend):
+    from ..errors import ConfigError
+    from .destroy import _rancher_client
+    from .select import select_cluster, select_manager, select_node
+
+    managers = backend.states()
+    if not managers:
+        raise ConfigError("No cluster managers.")
+    state = backend.state(select_manager(ctx, managers))
+    _, key = select_cluster(ctx, state.clusters(), "Cluster of the node", sort=False)
+    hostname, _ = select_node(ctx, state.nodes(key), "Node")
+    client, cid = _rancher_client(ctx, backend, state, key)
+    if client is None:
+        raise ConfigError(f"the cluster of {hostname} has no Rancher outputs yet (was it applied?)")
+    return client, cid, hostname
+
+
+def drain_command(ctx, backend) -> Dict[str, Any]:
+    """``drain node``: cordon + evict, the node stays in the cluster (cordoned)."""
+    client, cid, hostname = _target(ctx, backend)
+    return drain_node(client, cid, hostname, float(ctx.settings.get_string("drain_timeout") or 600), ctx.echo)
+
+
+def cordon_command(ctx, backend, unschedulable: bool) -> None:
+    """``cordon node`` / ``uncordon node``."""
+    client, cid, hostname = _target(ctx, backend)
+    client.cordon(cid, hostname, unschedulable)
+    ctx.echo(f"{hostname} {'cordoned' if unschedulable else 'uncordoned'}")
+
+
+__all__ = ["drain_node", "drain_command", "cordon_command"]
