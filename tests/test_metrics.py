@@ -258,3 +258,96 @@ def test_prom_on_the_box():
         s = _samples(p.stdout)
         assert s[("tk_node_unhealthy_gpus", (("node", "box"),))] >= 0
         assert any(k[0] == "tk_gpu_pcie_link_width" for k in s)
+
+
+def test_scrape_config_for_agent_nodes(tmp_path):
+    """``get scrape-config``: one job per agent node (its own token, the manager's agent CA),
+    secrets in files (0600), and the jobs actually scrape the agents' /metrics over TLS."""
+    import ssl
+    import stat
+
+    import yaml
+
+    from test_direct_executor import _manager, _nodes
+    from triton_kubernetes_amd import versions
+    from triton_kubernetes_amd.backend import LocalBackend
+    from triton_kubernetes_amd.cli.main import dispatch
+    from triton_kubernetes_amd.cloud.http import HTTPClient
+    from triton_kubernetes_amd.node.security import load_pki, read_credentials
+    from triton_kubernetes_amd.rancher.fake import FakeRancher
+    from triton_kubernetes_amd.workflows import new_cluster
+
+    from helpers import make_ctx, output
+
+    fake = FakeRancher.for_manager("mgr", "s3cret-passw0rd").start()
+    backend = LocalBackend(str(tmp_path / "state"))
+    base = {"executor": "direct"}
+    agents = []
+
+    def agent(name, addr, gpus=0):
+        d = tmp_path / f"creds-{name}"
+        pki.issue(addr, [versions.AGENT_IMAGE], servers=[fake.url]).write(str(d))
+        creds = read_credentials(str(d))
+        a = NodeAgent(name=name, mode="sim", devices=list(range(gpus)), token=creds["token"], root=str(tmp_path / name),
+                      topology_override=synthetic_topology(gpus) if gpus else None,
+                      burnin_override=lambda d, lvl: {"ok": True})
+        agents.append(a)
+        return "agent+" + a.serve(addr, ssl_context=creds["ssl_context"])
+
+    try:
+        _manager(fake, backend, base)
+        pki = load_pki(backend, "mgr")
+        cp = agent("cp", "127.0.0.1")
+        workers = [agent("w0", "127.0.0.2", 8), agent("w1", "127.0.0.3", 8)]
+        new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="dev",
+                                  k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico",
+                                  nodes=_nodes(cp, workers))), backend)
+        ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev",
+                            metrics_secrets_dir=str(tmp_path / "prom")))
+        assert dispatch(ctx, backend, "get", "scrape-config") == 0
+        lines = output(ctx).splitlines()
+        assert lines[0] == "get scrape-config called"  # the reference's breadcrumb, then the YAML
+        jobs = yaml.safe_load("\n".join(lines[1:]))
+        to_file = make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev",
+                                metrics_secrets_dir=str(tmp_path / "prom"), scrape_config_file=str(tmp_path / "s.yml")))
+        dispatch(to_file, backend, "get", "scrape-config")
+        assert yaml.safe_load((tmp_path / "s.yml").read_text()) == jobs
+        assert [j["job_name"] for j in jobs] == ["tk-dev-gpu-1", "tk-dev-gpu-2"]
+        secrets = sorted(os.listdir(tmp_path / "prom"))
+        assert secrets == ["mgr-agent-ca.pem", "mgr-dev-gpu-1.token", "mgr-dev-gpu-2.token"]
+        for f in secrets:
+            assert stat.S_IMODE(os.stat(tmp_path / "prom" / f).st_mode) == 0o600
+        assert "tka1." not in output(ctx)  # no secret printed
+        # scrape as Prometheus would: https, the CA file, server_name, the token file
+        for job, node in zip(jobs, ("w0", "w1")):
+            tls = ssl.create_default_context(cafile=job["tls_config"]["ca_file"])
+            target = job["static_configs"][0]["targets"][0]
+            with open(job["authorization"]["credentials_file"], encoding="utf-8") as fh:
+                token = fh.read()
+            resp = HTTPClient(base_url=f"https://{target}", ssl_context=tls).request(
+                "GET", "/metrics", headers={"Authorization": f"Bearer {token}"})
+            s = _samples(resp.body.decode())
+            assert s[("tk_bringup_success", (("node", node),))] == 1
+            assert any(k[0] == "tk_gpu_healthy" for k in s)
+        # an SSH / Terraform node with the textfile collector: a node_exporter job
+        st = backend.state("mgr")
+        key = st.nodes("cluster_baremetal_dev")["gpu-1"]
+        st.set_module(key, dict(st.module(key), host="10.0.0.9", gpu_metrics_textfile="/var/lib/node_exporter"))
+        backend.persist_state(st)
+        mixed = make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", node_exporter_port="9101",
+                              metrics_secrets_dir=str(tmp_path / "prom2"), scrape_config_file=str(tmp_path / "m.yml")))
+        dispatch(mixed, backend, "get", "scrape-config")
+        got = yaml.safe_load((tmp_path / "m.yml").read_text())
+        assert [j["job_name"] for j in got] == ["tk-dev-gpu-2", "tk-dev-node-exporter"]
+        assert got[1]["static_configs"] == [{"targets": ["10.0.0.9:9101"], "labels": {"cluster": "dev", "tk_node": "gpu-1"}}]
+        # another node's token is refused
+        with open(jobs[0]["authorization"]["credentials_file"], encoding="utf-8") as fh:
+            wrong = fh.read()
+        tls = ssl.create_default_context(cafile=jobs[1]["tls_config"]["ca_file"])
+        with pytest.raises(Exception, match="401"):
+            HTTPClient(base_url=f"https://{jobs[1]['static_configs'][0]['targets'][0]}", ssl_context=tls).request(
+                "GET", "/metrics", headers={"Authorization": f"Bearer {wrong}"})
+    finally:
+        for a in agents:
+            a.stop()
+        fake.stop()

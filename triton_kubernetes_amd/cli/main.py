@@ -40,7 +40,7 @@ except ImportError:
 VALID = {
     "create": ["manager", "cluster", "node"],
     "destroy": ["manager", "cluster", "node"],
-    "get": ["manager", "cluster", "nodes"],
+    "get": ["manager", "cluster", "nodes", "scrape-config"],
     "wait": ["cluster"],
     "backup": ["cluster"],
     "restore": ["cluster"],
@@ -191,6 +191,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
             from ..workflows.get import get_nodes
 
             get_nodes(ctx, backend)
+        elif what == "scrape-config":
+            from ..workflows.scrape import scrape_config
+
+            scrape_config(ctx, backend)
         else:
             {"manager": wf.get_manager, "cluster": wf.get_cluster}[what](ctx, backend)
     elif command == "backup":
