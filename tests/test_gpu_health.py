@@ -495,6 +495,7 @@ def test_vbios_label(tmp_path, native_ok):
     labels = topo.native_labels("sysfs", root)
     assert labels["amd.com/gpu.vbios"] == "113-M355-01-1K1-020F" and labels["amd.com/rocm.version"] == "7.2.0-43"
     assert topo.native_topology("sysfs", root)["rocm"] == {"version": "7.2.0-43"}
+    assert labels["amd.com/gpu.power-cap"] == "1400"
     assert labels == labels_from_topology(topo.native_topology("sysfs", root))
     with open(os.path.join(root, "sys/class/drm/renderD136/device/vbios_version"), "w") as fh:
         fh.write("113-M355-01-1K1-021F\n")
@@ -502,6 +503,13 @@ def test_vbios_label(tmp_path, native_ok):
     assert {g.get("vbios_version") for g in doc["gpus"]} == {"113-M355-01-1K1-020F", "113-M355-01-1K1-021F", None}
     labels = topo.native_labels("sysfs", root)
     assert labels["amd.com/gpu.vbios"] == "mixed" and labels == labels_from_topology(doc)
+    # one GPU capped at 1000 W: the label is the lowest cap (both labellers)
+    with open(os.path.join(root, "sys/class/drm/renderD136/device/hwmon/hwmon3/power1_cap"), "w") as fh:
+        fh.write("1000000000\n")
+    doc = topo.native_topology("sysfs", root)
+    assert doc["gpus"][8]["power_cap_w"] == 1000 and doc["gpus"][8]["power_cap_default_w"] == 1400
+    labels = topo.native_labels("sysfs", root)
+    assert labels["amd.com/gpu.power-cap"] == "1000" and labels == labels_from_topology(doc)
 
 
 def test_readiness_reports_gpu_nodes_that_differ(tmp_path):

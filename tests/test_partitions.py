@@ -61,6 +61,8 @@ def make_tree(root, ngpu=8, compute="SPX", memory="NPS1"):
                 _write(f"{dev}/mem_info_vram_total", f"{VRAM}\n")
                 for attr, val in (("current_link_width", "16"), ("max_link_width", "16"),
                                   ("vbios_version", "113-M355-01-1K1-020F"),
+                                  ("hwmon/hwmon3/power1_cap", "1400000000"),
+                                  ("hwmon/hwmon3/power1_cap_default", "1400000000"),
                                   ("current_link_speed", "32.0 GT/s PCIe"), ("max_link_speed", "32.0 GT/s PCIe")):
                     _write(f"{dev}/{attr}", val + "\n")
             else:

@@ -25,6 +25,7 @@ plus xGMI keys used for topology-aware scheduling:
 ``amd.com/gpu.pcie-width``             the narrowest GPU's PCIe link width (lanes)
 ``amd.com/gpu.vbios``                  the GPUs' VBIOS version (``mixed`` when they differ)
 ``amd.com/rocm.version``               the node's ROCm userspace (``<ROCM_PATH>/.info/version``)
+``amd.com/gpu.power-cap``              the lowest GPU board power cap (W)
 ``amd.com/gpu.health``                 ``healthy`` / ``unhealthy`` (node/health.py policy)
 =====================================  =============================================
 
@@ -127,6 +128,9 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
     vbioses = {g["vbios_version"] for g in gpus if g.get("vbios_version")}
     if vbioses:
         labels["amd.com/gpu.vbios"] = _label_value(vbioses.pop()) if len(vbioses) == 1 else "mixed"
+    caps = [int(g["power_cap_w"]) for g in gpus if int(g.get("power_cap_w", -1)) > 0]
+    if caps:
+        labels["amd.com/gpu.power-cap"] = str(min(caps))  # watts, the lowest GPU
     xgmi_peers = []
     for g in gpus:
         peers = {lk["peer"] for lk in g.get("links", []) if lk.get("type") == "XGMI"}

@@ -89,6 +89,8 @@ struct GpuInfo {
   // GT/s, current and the most the device supports (-1: not reported)
   int64_t pcie_width = -1, pcie_max_width = -1;
   double pcie_gts = -1.0, pcie_max_gts = -1.0;
+  // board power cap and its default, watts (the PCI function's hwmon; -1: not reported)
+  int64_t power_cap_w = -1, power_cap_default_w = -1;
   std::vector<Link> links;
 };
 
@@ -197,6 +199,11 @@ Topology collect_amdsmi() {
         snprintf(gb, sizeof(gb), "gfx%" PRIx64, a.target_graphics_version);
         g.gfx = gb;
       }
+    }
+    amdsmi_power_cap_info_t pc{};
+    if (amdsmi_get_power_cap_info(h, 0, &pc) == AMDSMI_STATUS_SUCCESS && pc.power_cap > 0) {  // uW on bare metal
+      g.power_cap_w = static_cast<int64_t>((pc.power_cap + 500000) / 1000000);
+      if (pc.default_power_cap > 0) g.power_cap_default_w = static_cast<int64_t>((pc.default_power_cap + 500000) / 1000000);
     }
     amdsmi_vbios_info_t vb{};
     // sysfs vbios_version is amd_smi's part_number ("113-M355-01-1K1-020F" on the box);
@@ -416,6 +423,19 @@ Topology collect_sysfs(const std::string& root) {
     if (read_file(dev + "/numa_node", &s)) g.numa_node = std::max<int64_t>(0, atoll(s.c_str()));
     if (read_file(dev + "/product_name", &s) && !s.empty()) g.market_name = s;
     if (read_file(dev + "/vbios_version", &s)) g.vbios = s;
+    // board power cap (hwmon of the PCI function, microwatts)
+    if (DIR* hw = opendir((dev + "/hwmon").c_str())) {
+      while (dirent* e = readdir(hw)) {
+        if (strncmp(e->d_name, "hwmon", 5) != 0) continue;
+        const std::string hd = dev + "/hwmon/" + e->d_name;
+        if (read_file(hd + "/power1_cap", &s) && isdigit((unsigned char)s[0]))
+          g.power_cap_w = static_cast<int64_t>((strtoull(s.c_str(), nullptr, 10) + 500000) / 1000000);
+        if (read_file(hd + "/power1_cap_default", &s) && isdigit((unsigned char)s[0]))
+          g.power_cap_default_w = static_cast<int64_t>((strtoull(s.c_str(), nullptr, 10) + 500000) / 1000000);
+        break;
+      }
+      closedir(hw);
+    }
     // PCIe link (the PCI function's attributes, e.g. "32.0 GT/s PCIe" and "16")
     if (read_file(dev + "/current_link_width", &s) && isdigit((unsigned char)s[0])) g.pcie_width = atoll(s.c_str());
     if (read_file(dev + "/max_link_width", &s) && isdigit((unsigned char)s[0])) g.pcie_max_width = atoll(s.c_str());
@@ -579,6 +599,8 @@ std::string render_json(const Topology& t) {
     if (g.rev_id >= 0) appendf(o, ",\"rev_id\":%" PRId64, g.rev_id);
     if (!g.serial.empty()) appendf(o, ",\"asic_serial\":\"%s\"", esc(g.serial).c_str());
     if (!g.vbios.empty()) appendf(o, ",\"vbios_version\":\"%s\"", esc(g.vbios).c_str());
+    if (g.power_cap_w > 0) appendf(o, ",\"power_cap_w\":%" PRId64, g.power_cap_w);
+    if (g.power_cap_default_w > 0) appendf(o, ",\"power_cap_default_w\":%" PRId64, g.power_cap_default_w);
     if (g.compute_units >= 0) appendf(o, ",\"compute_units\":%" PRId64, g.compute_units);
     if (g.oam_id >= 0) appendf(o, ",\"oam_id\":%" PRId64, g.oam_id);
     if (!g.gfx.empty()) appendf(o, ",\"target_graphics_version\":\"%s\"", g.gfx.c_str());
@@ -871,6 +893,7 @@ std::string render_labels(const Topology& t) {
     L["amd.com/gpu.logical-count"] = std::to_string(gs.size());
     if (gs.size() % physical == 0) L["amd.com/gpu.partitions-per-gpu"] = std::to_string(gs.size() / physical);
     std::set<std::string> names, dev_ids, targets, cparts, mparts, hives, vbioses;
+    int64_t min_cap = INT64_MAX;
     int64_t min_cu = INT64_MAX;
     uint64_t min_vram = UINT64_MAX;
     size_t min_xgmi = SIZE_MAX;
@@ -884,6 +907,7 @@ std::string render_labels(const Topology& t) {
       if (!g.memory_partition.empty()) mparts.insert(lower(g.memory_partition));
       if (g.has_xgmi && g.hive_id) hives.insert(hex64(g.hive_id));
       if (!g.vbios.empty()) vbioses.insert(g.vbios);
+      if (g.power_cap_w > 0) min_cap = std::min(min_cap, g.power_cap_w);
       std::set<size_t> peers;
       for (const auto& l : g.links)
         if (l.type == "XGMI") peers.insert(l.peer);
@@ -904,6 +928,7 @@ std::string render_labels(const Topology& t) {
     if (hives.size() == 1) L["amd.com/xgmi.hive-id"] = label_value(*hives.begin());
     // one VBIOS on every GPU, or "mixed" (a node whose GPUs were flashed apart)
     if (!vbioses.empty()) L["amd.com/gpu.vbios"] = vbioses.size() == 1 ? label_value(*vbioses.begin()) : "mixed";
+    if (min_cap != INT64_MAX) L["amd.com/gpu.power-cap"] = std::to_string(min_cap);  // watts, lowest GPU
     L["amd.com/xgmi.links-per-gpu"] = std::to_string(min_xgmi);
     // a compute partition is not a whole GPU with its own xGMI links: SPX only
     const bool whole = (cparts.empty() || (cparts.size() == 1 && *cparts.begin() == "spx")) && physical == gs.size();

@@ -23,7 +23,7 @@ Polling is adaptive (20 ms doubling to 1 s), not the reference's fixed 5 s.
 
 The report also lists the GPU-node labels that differ across the cluster's MI355X nodes
 (``gpu_mismatch``: product, VBIOS, ISA target, partition modes, HBM, CUs, RDMA fabric,
-ROCm userspace):
+ROCm userspace, power cap):
 one RCCL job over nodes flashed or partitioned apart is a classic source of hangs and
 uneven bandwidth.  It is a warning, not a failed readiness.
 """
@@ -83,7 +83,7 @@ class ReadinessReport:
 UNIFORM_LABELS = ("amd.com/gpu.product-name", "amd.com/gpu.vbios", "amd.com/gpu.target",
                   "amd.com/gpu.compute-partition", "amd.com/gpu.memory-partition", "amd.com/gpu.vram",
                   "amd.com/gpu.cu-count", "amd.com/rdma.link-layer", "amd.com/rdma.rate-gbps",
-                  "amd.com/rocm.version")
+                  "amd.com/rocm.version", "amd.com/gpu.power-cap")
 
 
 def gpu_mismatch(node_labels: Dict[str, Dict[str, str]]) -> Dict[str, Dict[str, List[str]]]:
