@@ -49,13 +49,14 @@ VALID = {
     "credentials": ["node"],
     "health": ["cluster"],
     "drain": ["node"],
+    "upgrade": ["cluster"],
     "cordon": ["node"],
     "uncordon": ["node"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
 _ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
              "restore": "restore", "userdata": "userdata", "migrate": "migrate", "credentials": "credentials", "health": "health",
-             "drain": "drain", "cordon": "cordon", "uncordon": "uncordon"}
+             "drain": "drain", "cordon": "cordon", "uncordon": "uncordon", "upgrade": "upgrade"}
 
 
 class ArgError(Exception):
@@ -105,6 +106,7 @@ def build_parser() -> argparse.ArgumentParser:
                        ("health", "Re-read the GPU health (ECC, retired pages) of a cluster's MI355X nodes and, "
                                   "with health_taint, fence unhealthy ones"),
                        ("drain", "Cordon a node and evict its pods (disruption budgets honoured)"),
+                       ("upgrade", "Upgrade a cluster's Kubernetes release (one minor at a time) and wait for it"),
                        ("cordon", "Mark a node unschedulable"),
                        ("uncordon", "Mark a node schedulable again")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
@@ -221,6 +223,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         from ..workflows.health import cluster_health
 
         cluster_health(ctx, backend)
+    elif command == "upgrade":
+        from ..workflows.upgrade import upgrade_cluster
+
+        upgrade_cluster(ctx, backend)
     elif command == "drain":
         from ..workflows.drain import drain_command
 

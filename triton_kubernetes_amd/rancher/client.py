@@ -307,6 +307,27 @@ class RancherClient:
     def cluster(self, cluster_id: str) -> Dict[str, Any]:
         return self.http.get_json(f"/v3/clusters/{cluster_id}")
 
+    def cluster_version(self, cluster_id: str) -> str:
+        """The Kubernetes release the cluster runs (``version.gitVersion``)."""
+        return str((self.cluster(cluster_id).get("version") or {}).get("gitVersion", ""))
+
+    def upgrade_cluster(self, cluster_id: str, version: str) -> None:
+        """Set the cluster's Kubernetes release: an RKE2 cluster's provisioning object
+        (``spec.kubernetesVersion``), an RKE1 cluster's ``rancherKubernetesEngineConfig``.
+        Rancher's controllers then upgrade the nodes (control plane first)."""
+        if cluster_id.startswith("c-m-"):
+            name = str(self.cluster(cluster_id).get("name", ""))
+            obj = self.find_v2_cluster(name)
+            if obj is None:
+                raise TKError(f"no provisioning cluster '{name}' for {cluster_id}")
+            obj.setdefault("spec", {})["kubernetesVersion"] = version
+            self.http.request("PUT", f"/v1/provisioning.cattle.io.clusters/{FLEET_NAMESPACE}/{name}", json_body=obj,
+                              ok=(200,))
+        else:
+            c = self.cluster(cluster_id)
+            c.setdefault("rancherKubernetesEngineConfig", {})["kubernetesVersion"] = version
+            self.http.request("PUT", f"/v3/clusters/{cluster_id}", json_body=c, ok=(200,))
+
     def cluster_state(self, cluster_id: str) -> str:
         return str(self.cluster(cluster_id).get("state", ""))
 

@@ -64,6 +64,7 @@ import base64
 import http.client
 import http.server
 import json
+import re
 import secrets
 import socket
 import ssl
@@ -140,6 +141,7 @@ class _State:
         self.rke_seconds = rke_seconds
         self.node_ready_seconds = node_ready_seconds
         self.device_plugin_seconds = 0.0
+        self.upgrade_seconds = 0.0  # a rolling Kubernetes upgrade's duration
         self.requests = 0
         self.log: List[Tuple[str, str]] = []
 
@@ -333,6 +335,8 @@ class FakeRancher:
                     "spec": dict({"taints": list(n.get("taints") or [])},
                                  **({"unschedulable": True} if n.get("unschedulable") else {})),
                     "status": {"conditions": [{"type": "Ready", "status": "True" if ready else "False"}],
+                               "nodeInfo": {"kubeletVersion": str(((st.clusters.get(cluster_id) or {})
+                                                                   .get("version") or {}).get("gitVersion", ""))},
                                "allocatable": alloc, "capacity": dict(alloc)},
                 })
         return items
@@ -457,7 +461,7 @@ class FakeRancher:
                 return 201, json.loads(json.dumps(st.secrets[f"{ns}/{name}"]))
         if path.startswith("/v1/provisioning.cattle.io.clusters/"):
             key = path[len("/v1/provisioning.cattle.io.clusters/"):]
-            return self._v2_cluster(method, key)
+            return self._v2_cluster(method, key, body)
         if path == "/v3/token" and method == "POST":
             name, secret = f"token-{uuid.uuid4().hex[:5]}", uuid.uuid4().hex
             with st.mu:
@@ -516,6 +520,12 @@ class FakeRancher:
                 return 200, {}
             if method == "POST" and query.get("action") == ["generateKubeconfig"]:
                 return 200, {"config": f"apiVersion: v1\nkind: Config\nclusters:\n- name: {cid}\n"}
+            if method == "PUT":
+                with st.mu:
+                    if st.clusters[cid].get("driver") == "rke2":  # the provisioning object owns it
+                        return 422, {"type": "error", "code": "Invalid",
+                                     "message": "an RKE2 cluster is changed through provisioning.cattle.io"}
+                    return self._upgrade(cid, body)
             self._refresh()
             with st.mu:
                 return 200, dict(st.clusters[cid])
@@ -559,6 +569,39 @@ class FakeRancher:
         return _admit_pod(self, cid, namespace, pod)
 
     # --- RKE2 custom clusters (provisioning.cattle.io/v1) ------------------------------------------
+    def _upgrade(self, cid: str, body: Any, v2: Optional[Dict[str, Any]] = None) -> Tuple[int, Any]:
+        """A cluster's new Kubernetes release (caller holds the lock): offered by the server,
+        not lower than the running one; the cluster reads ``upgrading`` until the (simulated)
+        rolling upgrade is over, and the kubelets report the new release."""
+        st = self.state
+        c = st.clusters.get(cid)
+        if c is None:
+            return 404, {"type": "error", "code": "NotFound"}
+        spec = (body or {}).get("spec") if v2 is not None else (body or {}).get("rancherKubernetesEngineConfig")
+        version = (spec or {}).get("kubernetesVersion", "")
+        offered = st.rke2_versions if v2 is not None else [v for v in st.settings["k8s-versions-current"].split(",") if v]
+        if version not in offered:
+            return 422, {"type": "error", "code": "Invalid", "fieldName": "kubernetesVersion",
+                         "message": f"{version} is not a supported Kubernetes version"}
+
+        def key(v: str) -> Tuple[int, ...]:
+            return tuple(int(x) for x in re.findall(r"\d+", v.split("+")[0].split("-")[0]))
+
+        current = (c.get("version") or {}).get("gitVersion", "")
+        if key(version) < key(current):
+            return 422, {"type": "error", "code": "Invalid", "message": f"cannot downgrade {current} to {version}"}
+        if version != current:
+            c["version"] = {"gitVersion": version}
+            c["state"], c["transitioning"] = "upgrading", "yes"
+            c["ready_at"] = time.time() + st.upgrade_seconds
+            st.unsettled.add(cid)
+            st.upgrades = getattr(st, "upgrades", 0) + 1
+        if v2 is not None:
+            v2["spec"]["kubernetesVersion"] = version
+            return 200, json.loads(json.dumps(v2))
+        c.setdefault("rancherKubernetesEngineConfig", {})["kubernetesVersion"] = version
+        return 200, dict(c)
+
     def _create_v2(self, body: Dict[str, Any]) -> Tuple[int, Any]:
         st = self.state
         meta, spec = body.get("metadata") or {}, body.get("spec") or {}
@@ -587,12 +630,14 @@ class FakeRancher:
             st.v2_clusters[f"{ns}/{name}"] = obj
             return 201, json.loads(json.dumps(obj))
 
-    def _v2_cluster(self, method: str, key: str) -> Tuple[int, Any]:
+    def _v2_cluster(self, method: str, key: str, body: Any = None) -> Tuple[int, Any]:
         st = self.state
         with st.mu:
             obj = st.v2_clusters.get(key)
             if obj is None:
                 return 404, {"type": "error", "code": "NotFound"}
+            if method == "PUT":
+                return self._upgrade(obj["status"].get("clusterName", ""), body, v2=obj)
             if method == "DELETE":
                 st.v2_clusters.pop(key)
                 cid = obj["status"].get("clusterName")
