@@ -439,6 +439,7 @@ def test_gpu_health_cli_on_the_box(capsys):
 def test_get_nodes_shows_gpu_state(tmp_path):
     """``get nodes``: the cluster's nodes through Rancher's Kubernetes API, with the MI355X
     columns (GPUs allocatable / counted, product, partition, burn-in, xGMI, health)."""
+    from triton_kubernetes_amd import versions
     from triton_kubernetes_amd.cli.main import dispatch
 
     from helpers import make_ctx
@@ -450,14 +451,15 @@ def test_get_nodes_shows_gpu_state(tmp_path):
         table = make_ctx(base)
         assert dispatch(table, backend, "get", "nodes") == 0
         lines = [ln for ln in table.out.getvalue().splitlines() if ln and not ln.startswith("get nodes")]
-        assert lines[0].split() == ["NAME", "READY", "ROLES", "GPUS", "PRODUCT", "PARTITION", "BURN-IN", "XGMI",
-                                    "PCIE", "UE/PAGES", "HEALTH"]
+        assert lines[0].split() == ["NAME", "READY", "ROLES", "VERSION", "GPUS", "PRODUCT", "PARTITION", "BURN-IN",
+                                    "XGMI", "PCIE", "UE/PAGES", "HEALTH"]
         rows = {ln.split()[0]: ln.split() for ln in lines[1:]}
         assert set(rows) == {"cp-1", "etcd-1", "gpu-1", "gpu-2"}
-        assert rows["gpu-1"][3:] == ["8/8", "MI355X", "spx/nps1", "passed(quick)", "mesh", "x16", "0/0", "healthy"]
-        assert rows["gpu-2"][3] == "0/8" and rows["gpu-2"][-1] == "unhealthy,tainted"
+        assert rows["gpu-1"][3] == versions.DEFAULT_K8S_VERSION
+        assert rows["gpu-1"][4:] == ["8/8", "MI355X", "spx/nps1", "passed(quick)", "mesh", "x16", "0/0", "healthy"]
+        assert rows["gpu-2"][4] == "0/8" and rows["gpu-2"][-1] == "unhealthy,tainted"
         assert rows["gpu-2"][-2] == "2/0"
-        assert rows["cp-1"][1] == "Ready" and rows["cp-1"][3] == "-"
+        assert rows["cp-1"][1] == "Ready" and rows["cp-1"][4] == "-"
         js = make_ctx(dict(base, output="json"))
         dispatch(js, backend, "get", "nodes")
         docs = [json.loads(ln) for ln in js.out.getvalue().splitlines() if ln.startswith("{")]

@@ -23,7 +23,7 @@ from ..errors import ConfigError
 from ..state import MANAGER_KEY
 from .select import executor_for, select_cluster, select_manager
 
-NODE_COLUMNS = ("NAME", "READY", "ROLES", "GPUS", "PRODUCT", "PARTITION", "BURN-IN", "XGMI", "PCIE", "UE/PAGES",
+NODE_COLUMNS = ("NAME", "READY", "ROLES", "VERSION", "GPUS", "PRODUCT", "PARTITION", "BURN-IN", "XGMI", "PCIE", "UE/PAGES",
                 "HEALTH")
 
 
@@ -59,7 +59,8 @@ def _node_row(item: Dict[str, Any]) -> Dict[str, str]:
                    if k.startswith("node-role.kubernetes.io/") and v in ("true", ""))
     gpu = labels.get("amd.com/gpu.present") == "true"
     row = {"NAME": meta.get("name", ""), "READY": "Ready" if ready == "True" else "NotReady",
-           "ROLES": ",".join(roles) or "-"}
+           "ROLES": ",".join(roles) or "-",
+           "VERSION": (status.get("nodeInfo") or {}).get("kubeletVersion") or "-"}
     if gpu:
         alloc = (status.get("allocatable") or {}).get("amd.com/gpu", "0")
         row["GPUS"] = f"{alloc}/{labels.get('amd.com/gpu.logical-count', labels.get('amd.com/gpu.count', '?'))}"
@@ -79,7 +80,7 @@ def _node_row(item: Dict[str, Any]) -> Dict[str, str]:
         row["HEALTH"] = health + (",tainted" if has_health_taint(item) else "") + (
             ",evicting" if "NoExecute" in effects else "")
     else:
-        row.update({c: "-" for c in NODE_COLUMNS[3:]})
+        row.update({c: "-" for c in NODE_COLUMNS[4:]})
     return row
 
 
