@@ -45,7 +45,8 @@ def test_userdata_node_from_applied_cluster(tmp_path):
         st = backend.state("mgr")
         baremetal.new_node(make_ctx({"rancher_host_label": "worker", "node_count": 1, "hostname": "gpu",
                                      "ssh_user": "u", "bastion_host": "", "key_path": "k", "hosts": ["10.9.0.1"],
-                                     "gpu": "mi355x", "rccl_env": {"NCCL_IB_HCA": "mlx5_0"}}),
+                                     "gpu": "mi355x", "rccl_env": {"NCCL_IB_HCA": "mlx5_0"},
+                                     "gpu_metrics_textfile": "/var/lib/node_exporter/textfile"}),
                            "mgr", "cluster_baremetal_pxe", None, st)
         backend.persist_state(st)
         ctx = make_ctx({"cluster_manager": "mgr", "cluster_name": "pxe", "hostname": "gpu-1"})
@@ -58,6 +59,8 @@ def test_userdata_node_from_applied_cluster(tmp_path):
         assert f"--token {token}" in files["/opt/triton-kubernetes/bootstrap.sh"]
         assert 'NCCL_IB_HCA="mlx5_0"' in files["/etc/rccl/rccl.env"]
         assert "gpu_burnin" in files["/opt/triton-kubernetes/bootstrap.sh"]
+        # the node_exporter textfile timer travels with the cloud-init delivery too
+        assert "tk-gpu-metrics.timer" in files["/opt/triton-kubernetes/bootstrap.sh"]
         with pytest.raises(TKError, match="A node named 'nope', does not exist."):
             node_userdata(make_ctx({"cluster_manager": "mgr", "cluster_name": "pxe", "hostname": "nope"}), backend)
     finally:
