@@ -530,6 +530,14 @@ def test_readiness_reports_gpu_nodes_that_differ(tmp_path):
                                                           "113-M355-01-1K1-021F": ["gpu-2"]}}
         assert "warning: MI355X nodes differ in amd.com/gpu.vbios" in ctx.out.getvalue()
         assert rep.rccl["ok"]  # a warning, not a failed readiness
+        from triton_kubernetes_amd.cli.main import dispatch
+
+        from helpers import make_ctx
+
+        table = make_ctx({"agent_token": "health-token-123456", "cluster_manager": "mgr", "cluster_name": "dev"})
+        dispatch(table, backend, "get", "nodes")
+        assert ("warning: MI355X nodes differ in amd.com/gpu.vbios: 113-M355-01-1K1-020F: gpu-1; "
+                "113-M355-01-1K1-021F: gpu-2") in table.out.getvalue()
     finally:
         for a in agents:
             a.stop()

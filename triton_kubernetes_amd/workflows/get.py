@@ -112,4 +112,10 @@ def get_nodes(ctx: Context, backend: Backend) -> List[Dict[str, str]]:
     ctx.echo("  ".join(c.ljust(widths[c]) for c in NODE_COLUMNS).rstrip())
     for r in rows:
         ctx.echo("  ".join(r[c].ljust(widths[c]) for c in NODE_COLUMNS).rstrip())
+    from ..readiness.waiter import gpu_mismatch
+
+    labels = {(i.get("metadata") or {}).get("name", ""): (i.get("metadata") or {}).get("labels") or {} for i in items}
+    for key, by in sorted(gpu_mismatch(labels).items()):
+        ctx.echo(f"warning: MI355X nodes differ in {key}: "
+                 + "; ".join(f"{v}: {', '.join(ns)}" for v, ns in sorted(by.items())))
     return rows
