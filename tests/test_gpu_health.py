@@ -546,3 +546,14 @@ def test_readiness_reports_gpu_nodes_that_differ(tmp_path):
     assert gpu_mismatch({"cp": {"amd.com/gpu.present": "false"},
                          "a": {"amd.com/gpu.present": "true", "amd.com/gpu.vram": "288G"},
                          "b": {"amd.com/gpu.present": "true"}}) == {"amd.com/gpu.vram": {"288G": ["a"], "-": ["b"]}}
+
+
+def test_thousands_of_retired_pages_are_counted(tmp_path, native_ok):
+    """A bad-page file far larger than any read buffer: every record counts (3000 > 2949,
+    the driver's threshold for 288 GiB)."""
+    root = healthy_tree(str(tmp_path))
+    _ras(root, 133, bad=["R"] * 2990 + ["P"] * 10)
+    v = _both(root)
+    g5 = v["gpus"][5]
+    assert (g5["bad_pages"], g5["bad_pages_pending"], g5["bad_page_limit"]) == (3000, 10, 2949)
+    assert v["reasons"] == ["GPU 5 (0000:55:00.0): 3000 retired VRAM pages (max 2949)"]

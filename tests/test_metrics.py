@@ -351,3 +351,14 @@ def test_scrape_config_for_agent_nodes(tmp_path):
         for a in agents:
             a.stop()
         fake.stop()
+
+
+def test_long_node_name_is_not_truncated(tmp_path, native_ok):
+    """Label values longer than any fixed buffer (an escaped 253-byte host name) render whole."""
+    from test_partitions import make_tree
+
+    root = make_tree(str(tmp_path))
+    node = ("n" * 120 + '"\\\\') * 2  # escaping doubles the quotes and backslashes
+    text = _native_prom(root, node)
+    assert text == metrics.gpu_metrics(topo.native_health("sysfs", root), node)
+    assert dict(next(k for k in _samples(text) if k[0] == "tk_node_unhealthy_gpus")[1])["node"] == node

@@ -56,11 +56,20 @@ std::string esc(const std::string& s) {
 void appendf(std::string& o, const char* fmt, ...) __attribute__((format(printf, 2, 3)));
 void appendf(std::string& o, const char* fmt, ...) {
   char buf[1024];
-  va_list ap;
+  va_list ap, again;
   va_start(ap, fmt);
-  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_copy(again, ap);
+  const int n = vsnprintf(buf, sizeof(buf), fmt, ap);
   va_end(ap);
-  o += buf;
+  if (n >= static_cast<int>(sizeof(buf))) {  // longer than the stack buffer: format again, sized exactly
+    std::string big(static_cast<size_t>(n) + 1, '\0');
+    vsnprintf(&big[0], big.size(), fmt, again);
+    big.resize(static_cast<size_t>(n));
+    o += big;
+  } else if (n > 0) {
+    o.append(buf, static_cast<size_t>(n));
+  }
+  va_end(again);
 }
 
 struct Link {
@@ -284,11 +293,11 @@ Topology collect_amdsmi() {
 bool read_file(const std::string& path, std::string* out) {
   FILE* f = fopen(path.c_str(), "r");
   if (!f) return false;
+  out->clear();
   char buf[4096];
-  size_t n = fread(buf, 1, sizeof(buf) - 1, f);
+  size_t n;
+  while ((n = fread(buf, 1, sizeof(buf), f)) > 0) out->append(buf, n);  // the whole file
   fclose(f);
-  buf[n] = 0;
-  *out = buf;
   while (!out->empty() && (out->back() == '\n' || out->back() == ' ')) out->pop_back();
   return true;
 }
@@ -805,11 +814,11 @@ std::string render_prom(const Topology& t, int64_t max_ue, int64_t max_bad, cons
   for (size_t i = 0; i < v.rows.size(); ++i) {
     const HealthRow& r = v.rows[i];
     const PhysGpu& p = r.p;
-    char lab[512];
-    snprintf(lab, sizeof(lab), "{node=\"%s\",gpu=\"%zu\",bdf=\"%s\"}", n.c_str(), i, prom_esc(p.bdf).c_str());
+    // any length: a node name is a host name (<= 253 bytes) but escaping can double it
+    const std::string lab = "{node=\"" + n + "\",gpu=\"" + std::to_string(i) + "\",bdf=\"" + prom_esc(p.bdf) + "\"}";
     auto add = [&](size_t f, int64_t val) {
       if (val < 0) return;
-      appendf(rows[f], "%s%s %" PRId64 "\n", fams[f].name, lab, val);
+      rows[f] += std::string(fams[f].name) + lab + " " + std::to_string(val) + "\n";
     };
     add(0, r.ok ? 1 : 0);
     if (p.has_ecc) {
@@ -824,7 +833,7 @@ std::string render_prom(const Topology& t, int64_t max_ue, int64_t max_bad, cons
     add(6, p.width);
     add(7, p.max_width);
   }
-  appendf(rows[8], "tk_node_unhealthy_gpus{node=\"%s\"} %zu\n", n.c_str(), v.bad_gpus);
+  rows[8] += "tk_node_unhealthy_gpus{node=\"" + n + "\"} " + std::to_string(v.bad_gpus) + "\n";
   std::string o;
   for (size_t f = 0; f < nfam; ++f) {
     if (rows[f].empty()) continue;
