@@ -15,10 +15,12 @@ from triton_kubernetes_amd.workflows import delete_node, new_cluster
 from helpers import make_ctx, output
 
 
-def _pod(name, node, ns="default", daemonset=False, refusals=None):
+def _pod(name, node, ns="default", daemonset=False, refusals=None, owner="Job"):
     meta = {"name": name, "namespace": ns}
     if daemonset:
         meta["ownerReferences"] = [{"kind": "DaemonSet", "name": "amdgpu-device-plugin"}]
+    elif owner:
+        meta["ownerReferences"] = [{"kind": owner, "name": f"{name}-owner"}]
     if refusals is not None:
         meta["annotations"] = {FakeRancher.PDB_ANNOTATION: str(refusals)}
     return {"apiVersion": "v1", "kind": "Pod", "metadata": meta,
@@ -118,3 +120,18 @@ def test_drain_cordon_uncordon_commands(env):  # noqa: F811 - fixture
     assert dispatch(ctx, backend, "uncordon", "node") == 0 and "gpu-1 uncordoned" in output(ctx)
     assert unschedulable() is None
     assert dispatch(make_ctx(sel), backend, "cordon", "node") == 0 and unschedulable() is True
+
+
+def test_unmanaged_pods_need_force(env):  # noqa: F811 - fixture
+    from triton_kubernetes_amd.cli.main import dispatch
+
+    fake, agent, backend, base = env
+    cid = _cluster(fake, agent, backend, base)
+    _post(fake, cid, _pod("scratch", "gpu-1", owner=None))  # a bare pod: gone for good once evicted
+    _post(fake, cid, _pod("train-0", "gpu-1", ns="ml"))
+    sel = dict(base, cluster_manager="mgr", cluster_name="dev", hostname="gpu-1")
+    with pytest.raises(TKError, match=r"runs pods no controller manages .*default/scratch; set drain_force"):
+        dispatch(make_ctx(sel), backend, "drain", "node")
+    assert _pods_on(fake, cid, "gpu-1") == ["scratch", "train-0"]  # nothing evicted
+    ctx = make_ctx(dict(sel, drain_force=True))
+    assert dispatch(ctx, backend, "drain", "node") == 0 and _pods_on(fake, cid, "gpu-1") == []

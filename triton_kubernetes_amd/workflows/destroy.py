@@ -93,7 +93,7 @@ def delete_node(ctx: Context, backend: Backend) -> None:
 
         timeout = float(ctx.settings.get_string("drain_timeout") or 600)
         with span("destroy.drain", node=hostname):
-            drain_node(client, cid, hostname, timeout, ctx.echo)
+            drain_node(client, cid, hostname, timeout, ctx.echo, ctx.settings.get_bool("drain_force"))
     with backend.lock(manager):
         state = _reread(backend, manager, node_key)
         cleanup = _rancher_node_cleanup_info(ctx, backend, state, key, hostname)

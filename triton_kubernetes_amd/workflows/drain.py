@@ -12,6 +12,10 @@ done through Rancher's Kubernetes API:
    static mirror pods are left, as ``kubectl drain --ignore-daemonsets`` does;
 3. wait until none of the evicted pods is bound to the node any more.
 
+As with ``kubectl drain``, a pod no controller manages (no ``ownerReferences``) would be
+gone for good once evicted: such pods stop the drain (after the cordon) unless
+``drain_force: true``.
+
 A drain that does not finish in time fails the destroy *before* anything is destroyed
 (the node stays cordoned, its module and host are untouched) and names the pods left.
 
@@ -40,13 +44,18 @@ def _ident(pod: Dict[str, Any]) -> str:
 
 
 def drain_node(client: Any, cluster_id: str, name: str, timeout: float = 600.0,
-               echo: Callable[[str], None] = lambda s: None) -> Dict[str, Any]:
+               echo: Callable[[str], None] = lambda s: None, force: bool = False) -> Dict[str, Any]:
     """Cordon ``name`` and evict its pods; returns ``{"evicted": [...], "kept": [...],
     "refusals": N, "seconds": S}``.  Raises :class:`TKError` when pods remain at the deadline."""
     t0 = time.time()
     deadline = t0 + timeout
     client.cordon(cluster_id, name)
-    kept = sorted(_ident(p) for p in client.node_pods(cluster_id, name) if not _evictable(p))
+    pods = client.node_pods(cluster_id, name)
+    kept = sorted(_ident(p) for p in pods if not _evictable(p))
+    bare = sorted(_ident(p) for p in pods if _evictable(p) and not (p.get("metadata") or {}).get("ownerReferences"))
+    if bare and not force:
+        raise TKError(f"{name} runs pods no controller manages (they would not come back): {', '.join(bare)}; "
+                      "set drain_force: true to evict them anyway (the node stays cordoned)")
     evicted: List[str] = []
     refusals = 0
     delay = 0.05
@@ -94,7 +103,8 @@ def _target(ctx, backend):
 def drain_command(ctx, backend) -> Dict[str, Any]:
     """``drain node``: cordon + evict, the node stays in the cluster (cordoned)."""
     client, cid, hostname = _target(ctx, backend)
-    return drain_node(client, cid, hostname, float(ctx.settings.get_string("drain_timeout") or 600), ctx.echo)
+    return drain_node(client, cid, hostname, float(ctx.settings.get_string("drain_timeout") or 600), ctx.echo,
+                      ctx.settings.get_bool("drain_force"))
 
 
 def cordon_command(ctx, backend, unschedulable: bool) -> None:
