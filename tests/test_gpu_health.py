@@ -333,6 +333,13 @@ def test_health_cluster_reconciles_the_taint(tmp_path):
         # the sick GPU is replaced; the other node logs an uncorrectable error
         w1.topology_override = synthetic_topology(8)
         w0.topology_override = _sick_topology()
+        # labels only: the counters and verdict labels move, no taint changes
+        relabel = make_ctx(dict(base, health_labels=True))
+        cluster_health(relabel, backend)
+        k8s = {n["metadata"]["name"]: n for n in fake.k8s_nodes(cid)}
+        assert k8s["gpu-1"]["metadata"]["labels"]["amd.com/gpu.health"] == "unhealthy"
+        assert not health.has_health_taint(k8s["gpu-1"]) and health.has_health_taint(k8s["gpu-2"])
+        assert k8s["gpu-2"]["metadata"]["labels"]["amd.com/gpu.health"] == "healthy"
         fence = make_ctx(dict(base, health_taint=True))
         assert dispatch(fence, backend, "health", "cluster") == 0
         k8s = {n["metadata"]["name"]: n for n in fake.k8s_nodes(cid)}

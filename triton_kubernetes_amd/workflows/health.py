@@ -22,7 +22,10 @@ running on an unhealthy node -- GPU jobs and the device plugin, so the node's
 ``amd.com/gpu`` drops to 0 -- for a GPU that started logging uncorrectable errors under a
 running job; pods that tolerate the taint stay.
 
-Settings: ``cluster_manager``, ``cluster_name``, ``health_taint`` (default false),
+``health_labels: true`` refreshes the health and RAS labels only (no taint is added or
+removed), for clusters whose taints another controller owns.
+
+Settings: ``cluster_manager``, ``cluster_name``, ``health_taint`` (default false), ``health_labels``,
 ``health_taint_effect`` (``NoSchedule`` | ``NoExecute``),
 ``gpu_max_uncorrectable_ecc`` / ``gpu_max_retired_pages`` (override the node modules').
 """
@@ -87,18 +90,24 @@ def _effect(ctx: Context) -> str:
 
 
 def _reconcile(client, cluster_id: str, node: Dict[str, Any], verdict: Dict[str, Any],
-               effect: str = "NoSchedule") -> str:
-    """Add / remove the health taint and set the labels; returns what changed ('' = nothing)."""
+               effect: str = "NoSchedule", fence: bool = True) -> str:
+    """Add / remove the health taint (``fence``) and set the labels; returns what changed
+    ('' = nothing)."""
     name = node["metadata"]["name"]
+    want = health_labels(verdict)
+    want.update(ras_labels(verdict.get("gpus") or []))
+    have = (node.get("metadata") or {}).get("labels") or {}
+    if not fence:
+        if all(have.get(k) == v for k, v in want.items()):
+            return ""
+        client.patch_node(cluster_id, name, {"metadata": {"labels": want}})
+        return "labelled"
     current = [t for t in (node.get("spec") or {}).get("taints") or [] if t.get("key") == HEALTH_TAINT["key"]]
     taints = [t for t in (node.get("spec") or {}).get("taints") or [] if t.get("key") != HEALTH_TAINT["key"]]
     unhealthy = verdict["status"] != "healthy"
     if unhealthy:
         taints.append(dict(HEALTH_TAINT, effect=effect))
     tainted = has_health_taint(node)
-    want = health_labels(verdict)
-    want.update(ras_labels(verdict.get("gpus") or []))
-    have = (node.get("metadata") or {}).get("labels") or {}
     same_effect = not unhealthy or [t.get("effect") for t in current] == [effect]
     if tainted == unhealthy and same_effect and all(have.get(k) == v for k, v in want.items()):
         return ""
@@ -137,8 +146,9 @@ def cluster_health(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
             verdicts.append({"node": h, "status": "unknown", "reasons": [f"{type(exc).__name__}: {exc}"],
                              "gpus": []})
     fence = ctx.settings.get_bool("health_taint") if ctx.is_set("health_taint") else False
-    if fence:
-        effect = _effect(ctx)
+    relabel = ctx.settings.get_bool("health_labels") if ctx.is_set("health_labels") else False
+    if fence or relabel:
+        effect = _effect(ctx) if fence else "NoSchedule"
         from ..readiness.waiter import spec_from_state
 
         client, spec = spec_from_state(state, backend, key)
@@ -147,7 +157,7 @@ def cluster_health(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
             if v["status"] == "unknown" or v["node"] not in k8s:
                 v["taint"] = "skipped"
                 continue
-            v["taint"] = _reconcile(client, spec.cluster_id, k8s[v["node"]], v, effect) or "unchanged"
+            v["taint"] = _reconcile(client, spec.cluster_id, k8s[v["node"]], v, effect, fence) or "unchanged"
     for v in verdicts:
         ctx.echo(json.dumps({k: v.get(k) for k in ("node", "status", "reasons", "taint") if k in v}, sort_keys=True))
     bad = [v["node"] for v in verdicts if v["status"] == "unhealthy"]
