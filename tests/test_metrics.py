@@ -362,3 +362,28 @@ def test_long_node_name_is_not_truncated(tmp_path, native_ok):
     text = _native_prom(root, node)
     assert text == metrics.gpu_metrics(topo.native_health("sysfs", root), node)
     assert dict(next(k for k in _samples(text) if k[0] == "tk_node_unhealthy_gpus")[1])["node"] == node
+
+
+def test_alert_rules_use_exported_metrics(tmp_path):
+    """``get alert-rules``: valid rule-file YAML whose expressions use only metric families
+    this framework exports."""
+    import re
+
+    import yaml
+
+    from triton_kubernetes_amd.backend import MemoryBackend
+    from triton_kubernetes_amd.cli.main import dispatch
+    from triton_kubernetes_amd.workflows.scrape import ALERTS
+
+    from helpers import make_ctx
+
+    ctx = make_ctx({"alert_rules_file": str(tmp_path / "rules.yml")})
+    assert dispatch(ctx, MemoryBackend(), "get", "alert-rules") == 0
+    doc = yaml.safe_load((tmp_path / "rules.yml").read_text())
+    rules = doc["groups"][0]["rules"]
+    assert [r["alert"] for r in rules] == [a["alert"] for a in ALERTS]
+    exported = {n for n, _, _ in metrics.GPU_FAMILIES + metrics.BRINGUP_FAMILIES}
+    for r in rules:
+        used = set(re.findall(r"\btk_[a-z_]+\b", r["expr"]))
+        assert used and used <= exported, (r["alert"], used - exported)
+        assert r["labels"]["severity"] in ("warning", "critical")

@@ -40,7 +40,7 @@ except ImportError:
 VALID = {
     "create": ["manager", "cluster", "node"],
     "destroy": ["manager", "cluster", "node"],
-    "get": ["manager", "cluster", "nodes", "scrape-config"],
+    "get": ["manager", "cluster", "nodes", "scrape-config", "alert-rules"],
     "wait": ["cluster"],
     "backup": ["cluster"],
     "restore": ["cluster"],
@@ -197,6 +197,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
             from ..workflows.scrape import scrape_config
 
             scrape_config(ctx, backend)
+        elif what == "alert-rules":
+            from ..workflows.scrape import alert_rules
+
+            alert_rules(ctx, backend)
         else:
             {"manager": wf.get_manager, "cluster": wf.get_cluster}[what](ctx, backend)
     elif command == "backup":

@@ -103,3 +103,46 @@ def scrape_config(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
 
 
 __all__ = ["scrape_config"]
+
+
+# --- alert rules --------------------------------------------------------------------------
+ALERTS: List[Dict[str, Any]] = [
+    {"alert": "TkGpuUnhealthy", "expr": "tk_gpu_healthy == 0", "for": "5m",
+     "labels": {"severity": "critical"},
+     "annotations": {"summary": "GPU {{ $labels.gpu }} ({{ $labels.bdf }}) on {{ $labels.node }} fails the health rules",
+                     "runbook": "triton-kubernetes health cluster (health_taint: true) fences the node"}},
+    {"alert": "TkGpuUncorrectableEcc", "expr": "increase(tk_gpu_ecc_uncorrectable_errors[1h]) > 0",
+     "labels": {"severity": "critical"},
+     "annotations": {"summary": "GPU {{ $labels.gpu }} on {{ $labels.node }} logged uncorrectable ECC errors"}},
+    {"alert": "TkGpuRetiredPagesNearLimit", "expr": "tk_gpu_retired_pages > 0.8 * tk_gpu_retired_pages_limit",
+     "for": "15m", "labels": {"severity": "warning"},
+     "annotations": {"summary": "GPU {{ $labels.gpu }} on {{ $labels.node }} retired over 80% of its VRAM page budget"}},
+    {"alert": "TkGpuPcieLinkDegraded", "expr": "tk_gpu_pcie_link_width < tk_gpu_pcie_link_max_width", "for": "5m",
+     "labels": {"severity": "warning"},
+     "annotations": {"summary": "GPU {{ $labels.gpu }} on {{ $labels.node }} runs x{{ $value }} below its PCIe width"}},
+    {"alert": "TkNodeBringupFailed", "expr": "tk_bringup_success == 0", "labels": {"severity": "warning"},
+     "annotations": {"summary": "the last bootstrap of {{ $labels.node }} failed"}},
+    {"alert": "TkAgentGpuReadFailing", "expr": "tk_agent_gpu_collect_success == 0", "for": "10m",
+     "labels": {"severity": "warning"},
+     "annotations": {"summary": "the node agent on {{ $labels.node }} cannot read its GPUs' RAS counters"}},
+]
+
+
+def alert_rules(ctx: Context, backend: Backend) -> Dict[str, Any]:
+    """``get alert-rules``: a Prometheus rule file over the node metrics (no cluster state
+    needed; ``alert_rules_file`` writes it to a file)."""
+    import yaml
+
+    doc = {"groups": [{"name": "triton-kubernetes-mi355x", "rules": ALERTS}]}
+    text = yaml.safe_dump(doc, sort_keys=False)
+    dest = ctx.settings.get_string("alert_rules_file")
+    if dest:
+        with open(os.path.expanduser(dest), "w", encoding="utf-8") as fh:
+            fh.write(text)
+        ctx.echo(f"wrote {len(ALERTS)} alert rule(s) to {dest}")
+    else:
+        ctx.echo(text.rstrip())
+    return doc
+
+
+__all__ += ["alert_rules", "ALERTS"]
