@@ -135,3 +135,28 @@ def _strings(res):
 
     walk(getattr(res, "resources", None) or getattr(res, "values", None) or res.__dict__)
     return out
+
+
+def test_gpu_policy_variables_are_validated():
+    """The MI355X host module's GPU policy variables carry validation blocks: the HCL input
+    check and the planner refuse what Terraform would ("Invalid value for variable")."""
+    import os
+
+    from triton_kubernetes_amd.terraform import hcl
+    from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+    from triton_kubernetes_amd.terraform.plan import plan_module
+
+    mod = os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host")
+    base = {"hostname": "g", "rancher_api_url": "https://r", "rancher_cluster_registration_token": "t",
+            "rancher_cluster_ca_checksum": "c", "rancher_host_labels": {"worker": "true"}, "host": "10.0.0.9"}
+    good = dict(base, gpu_health="taint", gpu_host_tuning="enforce", gpu_max_uncorrectable_ecc="2",
+                gpu_max_retired_pages="auto", gpu_metrics_textfile="/var/lib/node_exporter/textfile")
+    assert not [p for p in hcl.check_inputs(mod, good) if "gpu_" in p]
+    assert not [e for e in plan_module(mod, good, check_files=False).errors if "Invalid value" in e]
+    for key, bad in (("gpu_health", "warn"), ("gpu_host_tuning", "strict"), ("gpu_max_uncorrectable_ecc", "-1"),
+                     ("gpu_max_retired_pages", "lots"), ("gpu_metrics_textfile", "relative/dir"),
+                     ("gpu_metrics_textfile", "/var/../etc")):
+        problems = hcl.check_inputs(mod, dict(good, **{key: bad}))
+        assert any(key in p for p in problems), (key, bad, problems)
+        errors = plan_module(mod, dict(good, **{key: bad}), check_files=False).errors
+        assert any(f"Invalid value for variable '{key}'" in e for e in errors), (key, bad, errors)

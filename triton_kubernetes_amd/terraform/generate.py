@@ -163,6 +163,19 @@ VAR_VALIDATIONS = {
                               "gpu_compute_partition must be one of spx, dpx, qpx, cpx."),
     "gpu_memory_partition": ('contains(["nps1", "nps2"], var.gpu_memory_partition)',
                              "gpu_memory_partition must be nps1 or nps2."),
+    # GPU policies (node/health.py, node/hosttune.py, node/metrics.py)
+    "gpu_health": ('contains(["fail", "taint", "off"], var.gpu_health)', "gpu_health must be fail, taint or off."),
+    "gpu_host_tuning": ('contains(["warn", "enforce", "off"], var.gpu_host_tuning)',
+                        "gpu_host_tuning must be warn, enforce or off."),
+    "gpu_max_uncorrectable_ecc": ('length(regexall("^[0-9]+$", var.gpu_max_uncorrectable_ecc)) > 0',
+                                  "gpu_max_uncorrectable_ecc must be a non-negative integer."),
+    "gpu_max_retired_pages": ('var.gpu_max_retired_pages == "auto" || '
+                              'length(regexall("^[0-9]+$", var.gpu_max_retired_pages)) > 0',
+                              "gpu_max_retired_pages must be a non-negative integer or auto."),
+    "gpu_metrics_textfile": ('var.gpu_metrics_textfile == "" || '
+                             '(length(regexall("^/[A-Za-z0-9._/-]+$", var.gpu_metrics_textfile)) > 0 && '
+                             'length(regexall("/[.][.](/|$)", var.gpu_metrics_textfile)) == 0)',
+                             "gpu_metrics_textfile must be empty or an absolute directory path."),
     "rancher_host_labels": ('length(var.rancher_host_labels) == 1 && contains(["worker", "etcd", "control"], '
                             'keys(var.rancher_host_labels)[0])',
                             "rancher_host_labels must hold exactly one of worker, etcd or control."),
@@ -1334,9 +1347,8 @@ data "external" "gpu_labels" {{
         Var("rancher_secret_key", None, sensitive=True), Var("rancher_cluster_id", None),
         Var("device_plugin_image", versions.DEVICE_PLUGIN_IMAGE),
         Var("node_labeller_image", "",
-            "ROCm node labeller image, opt-in (empty: no labeller DaemonSet or its RBAC).",
-            # the pinned tag is versions.NODE_LABELLER_IMAGE
-            ),
+            f"ROCm node labeller image, opt-in (e.g. {versions.NODE_LABELLER_IMAGE}); it writes only keys the "
+            "bootstrap labeller does not. Empty: no labeller DaemonSet or its RBAC."),
         Var("rccl_probe_image", versions.RCCL_PROBE_IMAGE,
             "Image of the node-level rccl-ready Job (runs the node's installed tools)."),
         Var("webhook_image", versions.WEBHOOK_IMAGE, "Python image running the RCCL-env injector webhook."),

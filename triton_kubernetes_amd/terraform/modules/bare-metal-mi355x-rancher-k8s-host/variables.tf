@@ -173,30 +173,55 @@ variable "gpu_host_tuning" {
   description = "host settings check (NUMA auto-balancing off, IOMMU passthrough): warn = labels and warnings; enforce = fail the node; off = not checked"
   type        = string
   default     = "warn"
+
+  validation {
+    condition     = contains(["warn", "enforce", "off"], var.gpu_host_tuning)
+    error_message = "gpu_host_tuning must be warn, enforce or off."
+  }
 }
 
 variable "gpu_health" {
   description = "GPU health policy (RAS counters): fail = an unhealthy GPU fails the node; taint = the node joins tainted amd.com/gpu-health=unhealthy:NoSchedule (no GPU pods); off = not checked"
   type        = string
   default     = "fail"
+
+  validation {
+    condition     = contains(["fail", "taint", "off"], var.gpu_health)
+    error_message = "gpu_health must be fail, taint or off."
+  }
 }
 
 variable "gpu_max_uncorrectable_ecc" {
   description = "uncorrectable ECC errors a GPU may have logged"
   type        = string
   default     = "0"
+
+  validation {
+    condition     = length(regexall("^[0-9]+$", var.gpu_max_uncorrectable_ecc)) > 0
+    error_message = "gpu_max_uncorrectable_ecc must be a non-negative integer."
+  }
 }
 
 variable "gpu_metrics_textfile" {
   description = "node_exporter textfile collector directory: write the GPU health metrics there (tk_gpu.prom) and refresh them every minute from a systemd timer (empty: off)"
   type        = string
   default     = ""
+
+  validation {
+    condition     = var.gpu_metrics_textfile == "" || (length(regexall("^/[A-Za-z0-9._/-]+$", var.gpu_metrics_textfile)) > 0 && length(regexall("/[.][.](/|$)", var.gpu_metrics_textfile)) == 0)
+    error_message = "gpu_metrics_textfile must be empty or an absolute directory path."
+  }
 }
 
 variable "gpu_max_retired_pages" {
   description = "retired VRAM pages a GPU may have (auto: the amdgpu driver's default threshold, one page per 100 MiB of VRAM)"
   type        = string
   default     = "auto"
+
+  validation {
+    condition     = var.gpu_max_retired_pages == "auto" || length(regexall("^[0-9]+$", var.gpu_max_retired_pages)) > 0
+    error_message = "gpu_max_retired_pages must be a non-negative integer or auto."
+  }
 }
 
 variable "rccl_slim" {

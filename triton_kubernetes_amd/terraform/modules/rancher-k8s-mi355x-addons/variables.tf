@@ -31,7 +31,7 @@ variable "device_plugin_image" {
 }
 
 variable "node_labeller_image" {
-  description = "ROCm node labeller image, opt-in (empty: no labeller DaemonSet or its RBAC)."
+  description = "ROCm node labeller image, opt-in (e.g. rocm/k8s-device-plugin:labeller-1.31.0.6); it writes only keys the bootstrap labeller does not. Empty: no labeller DaemonSet or its RBAC."
   type        = string
   default     = ""
 }

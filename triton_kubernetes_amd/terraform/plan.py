@@ -734,6 +734,28 @@ class _ModulePlan:
         self.resource_values: Dict[Tuple[str, str, str], Any] = {}
         self.vars = self._inputs(inputs)
         self.scope = _Scope(self)
+        self._validate()
+
+    def _validate(self) -> None:
+        """The variables' ``validation`` blocks, as Terraform checks them before planning
+        ("Invalid value for variable"); a condition over an unknown value is skipped."""
+        for fn, b in self.blocks:
+            if b.type != "variable" or not b.labels or _is_unknown(self.vars.get(b.labels[0])):
+                continue
+            for vb in b.body.blocks:
+                cond = vb.body.attr("condition") if vb.type == "validation" else None
+                if cond is None:
+                    continue
+                try:
+                    ok = evaluate(cond.expr, self.scope)
+                    if _is_unknown(ok) or ok is not False:
+                        continue
+                    msg_attr = vb.body.attr("error_message")
+                    msg = evaluate(msg_attr.expr, self.scope) if msg_attr is not None else "validation failed"
+                except PlanError as exc:
+                    msg = f"validation condition: {exc}"
+                self.report.errors.append(f"{self.where(fn, vb.pos)}: Invalid value for variable "
+                                          f"{b.labels[0]!r}: {msg}")
 
     def where(self, fn: str, pos: int) -> str:
         return f"{self.name}/{fn}:{self.sources[fn].count(chr(10), 0, pos) + 1}"

@@ -76,7 +76,8 @@ def plan_migration(ctx: Context, doc: Dict[str, Any], drop_unknown: bool = False
         if not any(e.startswith(f"module.{key}:") for e in errors):
             # every expression of the new module for these inputs (terraform/plan.py)
             for p in plan_module(mod_dir, new, check_files=False).errors:
-                warnings.append(f"module.{key}: plan: {p}")
+                if "Invalid value for variable" not in p:  # check_inputs reported it above
+                    warnings.append(f"module.{key}: plan: {p}")
         new_blocks[key] = new
     return new_blocks, errors, warnings
 
