@@ -140,6 +140,8 @@ def test_agent_serves_metrics_with_bearer_auth(tmp_path):
     gpu2 = [v for k, v in s.items() if k[0] == "tk_gpu_ecc_uncorrectable_errors" and ("gpu", "2") in k[1]]
     assert gpu2 == [3] and s[("tk_node_unhealthy_gpus", (("node", "gpu-7"),))] == 0
     assert s[("tk_agent_gpu_collect_success", (("node", "gpu-7"),))] == 1
+    info = next(dict(k[1]) for k in s if k[0] == "tk_node_gpu_info")
+    assert info["product"] == "MI355X" and info["compute_partition"] == "spx" and info["node"] == "gpu-7"
     # a GPU read that fails costs the GPU families, not the endpoint
     agent.topology_override = {"gpus": [{"bdf": "x", "bad_pages": "garbled"}]}
     s = _samples(agent.metrics())

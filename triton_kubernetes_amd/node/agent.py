@@ -500,7 +500,8 @@ class NodeAgent:
                 gpu_text, ok = gpu_metrics(self.health(*self.health_limits), self.name), True
             except Exception:  # noqa: BLE001
                 ok = False
-        return bringup_metrics(self.history[-1] if self.history else None, self.name, self.mode, ok) + gpu_text
+        return bringup_metrics(self.history[-1] if self.history else None, self.name, self.mode, ok,
+                               self.last_labels) + gpu_text
 
     def _gpu_preflight(self, expected: int) -> Dict[str, Any]:
         if self.topology_override is not None:

@@ -56,6 +56,7 @@ _GPU_FIELDS = [("ecc_uncorrectable", "tk_gpu_ecc_uncorrectable_errors"),
 BRINGUP_FAMILIES: List[Tuple[str, str, str]] = [
     ("tk_agent_info", "gauge", "Node agent (always 1; labels: node, mode)"),
     ("tk_agent_gpu_collect_success", "gauge", "1 if the agent read the GPUs' RAS counters for this scrape"),
+    ("tk_node_gpu_info", "gauge", "Always 1; labels: the node's GPU product, VBIOS, ROCm, partition modes, power cap"),
     ("tk_bringup_duration_seconds", "gauge", "Wall time of the node's last bootstrap plan"),
     ("tk_bringup_success", "gauge", "1 if the node's last bootstrap plan succeeded"),
     ("tk_bringup_step_duration_seconds", "gauge", "Wall time of each step of the last bootstrap plan"),
@@ -133,11 +134,20 @@ def _flatten(prefix: str, obj: Any) -> List[Tuple[str, float]]:
     return []
 
 
+# node label -> info-metric label (node/labels.py)
+INFO_LABELS = (("amd.com/gpu.product-name", "product"), ("amd.com/gpu.vbios", "vbios"),
+               ("amd.com/rocm.version", "rocm"), ("amd.com/gpu.compute-partition", "compute_partition"),
+               ("amd.com/gpu.memory-partition", "memory_partition"), ("amd.com/gpu.power-cap", "power_cap_w"))
+
+
 def bringup_metrics(plan_doc: Optional[Dict[str, Any]], node: str, mode: str = "",
-                    gpu_collect_ok: Optional[bool] = None) -> str:
-    """Families of the node's last bootstrap plan (an agent ``run_plan`` result)."""
+                    gpu_collect_ok: Optional[bool] = None, labels: Optional[Dict[str, str]] = None) -> str:
+    """Families of the node's last bootstrap plan (an agent ``run_plan`` result); ``labels``:
+    the node labels it set (the info metric)."""
     exp = Exposition(BRINGUP_FAMILIES)
     exp.add("tk_agent_info", 1, node=node, mode=mode)
+    if labels and labels.get("amd.com/gpu.present") == "true":
+        exp.add("tk_node_gpu_info", 1, node=node, **{m: labels.get(k, "") for k, m in INFO_LABELS})
     if gpu_collect_ok is not None:
         exp.add("tk_agent_gpu_collect_success", 1 if gpu_collect_ok else 0, node=node)
     if not plan_doc:
