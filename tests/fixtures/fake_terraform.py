@@ -35,6 +35,8 @@ import sys
 import uuid
 
 REMOVED_BACKENDS_1_3 = {"artifactory", "etcd", "etcdv3", "manta", "swift"}
+# go-getter's forced getters (``<scheme>::<address>``) that Terraform's module installer has
+GETTER_SCHEMES = {"git", "hg", "s3", "gcs", "http", "https", "file"}
 
 
 def vtuple(text):
@@ -122,7 +124,9 @@ def state_path(doc):
     if backend:  # a remote backend this fake stands in for: keep it beside the log
         kind = next(iter(backend))
         base = os.environ.get("FAKE_TF_REMOTE") or os.path.join(os.getcwd(), ".remote")
-        ident = json.dumps(backend[kind], sort_keys=True)
+        # a remote state is addressed by where it lives, not by whose credentials read it
+        where = {k: v for k, v in backend[kind].items() if not re.search(r"key|secret|password|token", k)}
+        ident = json.dumps(where, sort_keys=True)
         return os.path.join(base, kind, re.sub(r"[^A-Za-z0-9]+", "_", ident)[:120] + ".tfstate")
     return "terraform.tfstate"
 
@@ -173,7 +177,13 @@ def main() -> int:
             if version >= (1, 3, 0) and kind in REMOVED_BACKENDS_1_3:
                 return fail(f'Unsupported backend type\n\nThere is no backend type named "{kind}".')
         for key, mod in (doc.get("module") or {}).items():
-            d = local_dir(str(mod.get("source", "")))
+            source = str(mod.get("source", ""))
+            scheme = re.match(r"^([A-Za-z0-9]+)::", source)
+            if scheme and scheme.group(1) not in GETTER_SCHEMES:
+                # go-getter's forced-getter syntax with a getter Terraform does not have
+                return fail(f'Failed to download module\n\nCould not download module "{key}" source code from '
+                            f'"{source}": download not supported for scheme \'{scheme.group(1)}\'.')
+            d = local_dir(source)
             if d is None:
                 continue
             if not os.path.isdir(d):

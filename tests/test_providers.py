@@ -9,6 +9,7 @@ import os
 
 import pytest
 
+from triton_kubernetes_amd import __version__
 from triton_kubernetes_amd.cloud.fake import FakeCloud
 from triton_kubernetes_amd.errors import TKError
 from triton_kubernetes_amd.models import aws, azure, baremetal, gcp, triton, vsphere
@@ -47,9 +48,9 @@ def test_baremetal_manager_document():
     baremetal.new_manager(make_ctx(dict(BASE_MGR, host="10.0.0.10", ssh_user="ubuntu", bastion_host="",
                                         key_path="~/.ssh/id_rsa")), st, "mgr")
     m = st.manager()
-    # default: this package's own module tree (a local path Terraform reads directly)
-    assert m["source"] == os.path.join(catalog.PACKAGE_ROOT, "terraform", "modules", "bare-metal-rancher")
-    assert os.path.isfile(os.path.join(m["source"], "main.tf"))
+    # default: this package's own module tree, named location-free (resolved only when run)
+    assert m["source"] == "tk::terraform/modules/bare-metal-rancher?ref=v" + __version__
+    assert os.path.isfile(os.path.join(catalog.local_module_dir(m["source"]), "main.tf"))
     assert list(m) == ["source", "name", "rancher_admin_password", "host", "ssh_user", "key_path"]
     assert m["key_path"] == "~/.ssh/id_rsa"  # not expanded (reference quirk Q11 kept)
     assert_blocks_match_modules(st)
@@ -120,7 +121,7 @@ def test_mi355x_node_and_addons():
     baremetal.new_node(make_ctx(dict(NODE_BASE, ssh_user="u", bastion_host="", key_path="k", gpu="mi355x",
                                      hosts=["a", "b"], rccl_env={"NCCL_SOCKET_IFNAME": "eth0"})), "m", key, None, st)
     n = st.module("node_baremetal_dev_dev-w-1")
-    assert n["source"].endswith("terraform/modules/bare-metal-mi355x-rancher-k8s-host")
+    assert n["source"].startswith("tk::terraform/modules/bare-metal-mi355x-rancher-k8s-host?ref=")
     assert n["gpu_count"] == "8" and n["gpu_burnin"] == "quick" and n["gpu_product"] == "MI355X"
     assert n["rccl_env"]["NCCL_SOCKET_IFNAME"] == "eth0" and n["rccl_env"]["HSA_FORCE_FINE_GRAIN_PCIE"] == "1"
     assert_blocks_match_modules(st)

@@ -44,7 +44,7 @@ from ..node.plan import TOOLS_DIR, build_host_plan
 from ..parallel.transport import HostRef, Transport, TransportRouter
 from ..rancher.client import RancherClient, wait_until
 from ..state import State
-from ..terraform.catalog import ModuleInfo, module_from_source
+from ..terraform.catalog import ModuleInfo, check_sources, module_from_source
 from ..utils.trace import span
 from ..versions import DEFAULT_DISTRIBUTION, bootstrap_password, default_version
 from .base import Executor, outputs_from_tfstate
@@ -179,13 +179,17 @@ class DirectExecutor(Executor):
 
     # --- planning -------------------------------------------------------------------------------------
     def plan(self, state: State) -> Dict[str, ModuleRun]:
+        check_sources(state.modules())  # a document pinned to other modules is refused, as by Terraform
         runs: Dict[str, ModuleRun] = {}
         for key, cfg in state.modules().items():
-            info = module_from_source(str(cfg.get("source", "")))
+            source = str(cfg.get("source", ""))
+            info = module_from_source(source)
             if info is None or info.name not in SUPPORTED:
                 raise ExecutorError(f"the direct executor does not implement module '{cfg.get('source')}' "
                                     f"(module.{key}); use `executor: terraform`")
-            h, deps = fingerprint(cfg)
+            # the module's identity, not where its source lives, is part of the hash: the same
+            # document applied from another install (another tk:: directory) re-applies nothing
+            h, deps = fingerprint(dict(cfg, source=info.name))
             runs[key] = ModuleRun(key, info, cfg, deps, h)
         # An add-on module is applied after every host of its cluster (Terraform
         # would need an explicit depends_on): a failed node then blocks it

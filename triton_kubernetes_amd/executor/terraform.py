@@ -50,7 +50,8 @@ from ..backend.base import Backend
 from ..errors import ExecutorError
 from ..state import State
 from ..terraform import constraints
-from ..terraform.catalog import local_module_dir, module_from_source, outputs_for_source, sensitive_outputs
+from ..terraform.catalog import (check_sources, is_packaged_source, local_module_dir, module_from_source,
+                                 outputs_for_source, resolve_source, sensitive_outputs)
 from ..utils.jsonenc import dumps_go
 from .base import Executor, outputs_from_tfstate
 from .shell import ShellOptions, capture_command, run_shell_command
@@ -85,7 +86,10 @@ def _backend_kind(doc: Dict) -> str:
 
 def check_module_versions(state: State, version: Tuple[int, int, int]) -> None:
     """Raise when a module from a local directory declares a ``required_version`` that
-    ``version`` does not meet (Terraform's own init error, reported up front)."""
+    ``version`` does not meet (Terraform's own init error, reported up front), when a
+    ``tk::`` source is pinned to another CLI version, or when an absolute-path source
+    written by another install (a pre-``tk::`` document) does not exist here."""
+    check_sources(state.modules())
     seen = set()
     for key, mod in state.modules().items():
         local = local_module_dir(str(mod.get("source", "")))
@@ -100,13 +104,34 @@ def check_module_versions(state: State, version: Tuple[int, int, int]) -> None:
                 "at modules written for this version.")
 
 
-def render(state: State, version: Tuple[int, int, int]) -> Rendered:
-    """The document Terraform sees (see module docstring)."""
-    doc = state.doc
+def resolve_sources(doc: Dict) -> Dict:
+    """``doc`` (copied when anything changes) with every ``tk::`` module source replaced
+    by this install's module directory (``terraform/catalog.py:resolve_source``)."""
+    modules = doc.get("module") or {}
+    if not any(is_packaged_source(str((m or {}).get("source", ""))) for m in modules.values()):
+        return doc
+    doc = dict(doc)
+    doc["module"] = {k: (dict(m, source=resolve_source(str(m["source"]), k))
+                         if is_packaged_source(str((m or {}).get("source", ""))) else m)
+                     for k, m in modules.items()}
+    return doc
+
+
+def render(state: State, version: Tuple[int, int, int], backend: Optional[Backend] = None) -> Rendered:
+    """The document Terraform sees (see module docstring).
+
+    With ``backend`` the backend block is this operator's (``state_terraform_config``),
+    when it is of the same kind as the persisted one: a shared document carries the key
+    path of whoever wrote it (``key_material``, reference ``backend/manta/backend.go:199``)."""
+    doc = resolve_sources(state.doc)
     kind = _backend_kind(doc)
+    if backend is not None and kind:
+        path, block = backend.state_terraform_config(state.name)
+        if path == f"terraform.backend.{kind}" and block != doc["terraform"]["backend"][kind]:
+            doc = dict(doc, terraform=dict(doc["terraform"], backend={kind: block}))
     managed = bool(kind) and constraints.backend_removed(kind, version)
     if version < (0, 12, 0) and not managed:
-        return Rendered(state.bytes(), False, kind)
+        return Rendered(dumps_go(doc), False, kind)
     doc = copy.deepcopy(doc)
     if managed:
         doc["terraform"]["backend"] = {"local": {"path": WORKDIR_TFSTATE}}
@@ -170,7 +195,7 @@ class TerraformExecutor(Executor):
         body, under ``backend.lock``."""
         version = self.version()
         check_module_versions(state, version)
-        rendered = render(state, version)
+        rendered = render(state, version, backend)
         if rendered.managed_state and backend is None:
             raise ExecutorError(f"the {rendered.backend_kind} state backend needs the CLI to carry terraform.tfstate")
         tmp = tempfile.mkdtemp(prefix="triton-kubernetes-")

@@ -19,15 +19,16 @@ from typing import Dict, List, Optional, Sequence
 from ..config.context import Context, not_blank
 from ..errors import ConfigError
 from ..state import MANAGER_KEY, State
-from ..terraform.catalog import module_source, packaged_root
+from ..terraform.catalog import module_source, packaged_source
 from ..versions import (DISTRIBUTIONS, PASSWORD_MIN_LENGTH, RKE2_CNIS, distribution_of, normalize_k8s_version,
                         releases, resolve_distribution)
 
 # The reference defaults to its own GitHub repo (create/cluster.go:20-21), which is
 # where its modules live.  This CLI's modules ship inside the package, so the default
-# is that directory (resolved at use: a zipapp extracts it to a cache first);
+# is the symbolic tk:: source of that tree (resolved to a directory only when an
+# executor runs the document; a zipapp extracts it to a cache first);
 # SOURCE_URL / SOURCE_REF still select a git or registry copy.
-DEFAULT_SOURCE_URL = ""  # "" = the packaged module tree (catalog.packaged_root())
+DEFAULT_SOURCE_URL = ""  # "" = the packaged module tree (catalog.packaged_source())
 DEFAULT_SOURCE_REF = "master"
 
 DNS1123_RE = re.compile(r"^[a-z0-9]([-a-z0-9]*[a-z0-9])?(\.[a-z0-9]([-a-z0-9]*[a-z0-9])?)*$")
@@ -53,9 +54,18 @@ def omit_empty(cfg: Dict, keys: Sequence[str]) -> Dict:
 
 
 def source_for(ctx: Context, module_path: str) -> str:
+    """The persisted ``source`` of a module block.
+
+    * default: the location-free ``tk::<module_path>?ref=v<version>`` of the modules this
+      CLI ships (``terraform/catalog.py``), resolved to this install's directory only in
+      the document an executor runs — so a shared (Manta) document applies from any
+      operator's machine, as the reference's GitHub sources do;
+    * ``source_url`` set: ``<url>//<module_path>?ref=<source_ref>`` (``create/manager.go:160-171``),
+      or ``<dir>/<module_path>`` when the URL is a local directory (a deliberate,
+      machine-local choice)."""
     url = ctx.get_string("source_url") if ctx.is_set("source_url") else DEFAULT_SOURCE_URL
     if not url:
-        url = packaged_root()
+        return packaged_source(module_path)
     ref = ctx.get_string("source_ref") if ctx.is_set("source_ref") else DEFAULT_SOURCE_REF
     return module_source(url, module_path, ref)
 

@@ -19,6 +19,8 @@ import os
 from dataclasses import dataclass, field
 from typing import Dict, List, Optional, Tuple
 
+from ..errors import ExecutorError
+
 MODULES_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "modules")
 
 MANAGER_OUTPUTS = ("rancher_url", "rancher_access_key", "rancher_secret_key")
@@ -142,10 +144,109 @@ def module_source(source_url: str, module_path: str, source_ref: str) -> str:
     return f"{source_url}//{module_path}?ref={source_ref}"
 
 
+# --- location-free sources of the packaged modules ------------------------------------
+#
+# The reference persists ``github.com/joyent/triton-kubernetes//terraform/modules/<m>?ref=``
+# (create/manager.go:160-171): any operator, on any machine, can apply the document.  This
+# CLI's modules ship inside the package, whose directory differs between machines, venvs
+# and versions, so the persisted document names them symbolically:
+#
+#     tk::terraform/modules/<module>?ref=v<package version>
+#
+# and only the document an executor runs (executor/terraform.py:render, the direct
+# executor's plan) sees the directory of *this* install.  A document pinned to another
+# version of the modules is refused until ``migrate manager`` re-pins it: silently
+# applying different module code to running infrastructure is what the pin prevents.
+PACKAGED_SCHEME = "tk::"
+
+
+def packaged_ref() -> str:
+    from .. import __version__
+
+    return f"v{__version__}"
+
+
+def packaged_source(module_path: str) -> str:
+    """The persisted source of a packaged module (``module_path`` = ``terraform/modules/<m>``)."""
+    return f"{PACKAGED_SCHEME}{module_path}?ref={packaged_ref()}"
+
+
+def is_packaged_source(source: str) -> bool:
+    return source.startswith(PACKAGED_SCHEME)
+
+
+def _packaged_parts(source: str) -> Tuple[str, str]:
+    """``(module name, ref)`` of a ``tk::`` source."""
+    body = source[len(PACKAGED_SCHEME):]
+    path, _, query = body.partition("?")
+    ref = ""
+    for part in query.split("&"):
+        if part.startswith("ref="):
+            ref = part[len("ref="):]
+    return path.rstrip("/").rsplit("/", 1)[-1], ref
+
+
+class ModuleRefMismatch(ExecutorError):
+    """A ``tk::`` source pinned to modules of another CLI version."""
+
+
+def resolve_source(source: str, key: str = "") -> str:
+    """The source Terraform is given: a ``tk::`` source becomes this install's module
+    directory; every other source is returned unchanged.
+
+    Raises :class:`ModuleRefMismatch` for a ``tk::`` source pinned to another version and
+    :class:`ExecutorError` for a module this package does not ship."""
+    if not is_packaged_source(source):
+        return source
+    name, ref = _packaged_parts(source)
+    where = f"module.{key}" if key else source
+    if name not in CATALOG:
+        raise ExecutorError(f"{where}: {source!r} names no module of this CLI")
+    want = packaged_ref()
+    if ref != want:
+        raise ModuleRefMismatch(
+            f"{where} is pinned to the triton-kubernetes modules {ref or '(no ref)'}, but this CLI ships {want}. "
+            "Run `triton-kubernetes migrate manager` to re-pin the document to the installed modules, "
+            f"or use triton-kubernetes {ref.lstrip('v') or 'of that version'} to operate on it.")
+    return os.path.join(packaged_root(), "terraform", "modules", name)
+
+
+def check_sources(modules: Dict[str, Dict]) -> None:
+    """Refuse a document this install cannot run, before anything is built on it: a
+    ``tk::`` source of another version or of an unknown module, or an absolute path into
+    another install's module tree that does not exist here (documents written before the
+    ``tk::`` form)."""
+    for key, mod in modules.items():
+        source = str((mod or {}).get("source", ""))
+        if is_packaged_source(source):
+            resolve_source(source, key)
+        elif packaged_module_of_path(source) is not None and not os.path.isdir(source.split("?", 1)[0]):
+            raise ExecutorError(
+                f"module.{key} points at {source}, a module directory of another triton-kubernetes install that "
+                "does not exist on this machine. Run `triton-kubernetes migrate manager` to rewrite the document's "
+                "module sources to the location-free tk:: form.")
+
+
 def local_module_dir(source: str) -> Optional[str]:
-    """The directory a local ``source`` points at (None for remote sources)."""
+    """The directory a local ``source`` points at (None for remote sources); a ``tk::``
+    source resolves to this install's module directory (see :func:`resolve_source`)."""
+    if is_packaged_source(source):
+        return resolve_source(source)
     path = source.split("?", 1)[0]
     return path if is_local_source(path) else None
+
+
+def packaged_module_of_path(source: str) -> Optional[ModuleInfo]:
+    """The catalog module an *absolute path* source names when that path is some
+    install's packaged tree (``.../terraform/modules/<m>``): what ``migrate manager``
+    rewrites to a ``tk::`` source."""
+    path = source.split("?", 1)[0].rstrip("/")
+    if not path.startswith("/"):
+        return None
+    parent, name = os.path.split(path)
+    if os.path.basename(parent) != "modules" or os.path.basename(os.path.dirname(parent)) != "terraform":
+        return None
+    return CATALOG.get(name)
 
 
 def module_from_source(source: str) -> Optional[ModuleInfo]:

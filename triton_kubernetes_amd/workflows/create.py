@@ -29,6 +29,7 @@ from ..models import CLUSTER_CHOICES, CLUSTER_PROVIDERS, MANAGER_CHOICES, MANAGE
 from ..models import NODE_PROVIDERS
 from ..models.common import nodes_added_message
 from ..state import State
+from ..terraform.catalog import check_sources
 from ..utils.trace import span
 from .select import executor_for, select_cluster, select_manager
 
@@ -141,6 +142,7 @@ def new_cluster(ctx: Context, backend: Backend) -> Optional[str]:
         raise ConfigError(NO_MANAGERS)
     manager = select_manager(ctx, managers)
     state = backend.state(manager).mark_base()
+    check_sources(state.modules())  # refused before any question is asked
     provider = ctx.resolve_choice("cluster_cloud_provider", "Create Cluster in which Cloud Provider",
                                   CLUSTER_CHOICES, transform=str.lower)
     fn = CLUSTER_PROVIDERS.get(provider)
@@ -187,6 +189,7 @@ def new_node(ctx: Context, backend: Backend) -> Optional[List[str]]:
         raise ConfigError(NO_MANAGERS)
     manager = select_manager(ctx, managers)
     state = backend.state(manager).mark_base()
+    check_sources(state.modules())  # refused before any question is asked
     _, key = select_cluster(ctx, state.clusters(), "Cluster to deploy node to")
     parts = key.split("_")
     if len(parts) < 3:

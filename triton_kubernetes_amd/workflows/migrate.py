@@ -8,7 +8,11 @@ modules lack the MI355X host and add-on modules.  Module keys, variable names an
 backend block are compatible by design, so migration is a source rewrite plus a check:
 
 1. every module block whose source is not this framework's source for that module (the
-   packaged tree, or ``source_url``/``source_ref``) is pointed at it;
+   location-free ``tk::terraform/modules/<m>?ref=v<version>`` of the packaged tree, or
+   ``source_url``/``source_ref``) is pointed at it.  This also re-pins documents written
+   by another version of this CLI (a ``tk::`` source with another ``ref``, which every
+   executor refuses) and rewrites the absolute paths of one operator's install that
+   documents of earlier versions persisted;
 2. each rewritten block is checked against the new module the way ``terraform plan``
    would (``terraform/hcl.py:check_inputs``, then ``terraform/plan.py`` evaluates every
    expression of the module for the block's inputs): unknown arguments (dropped with
