@@ -20,7 +20,13 @@ code (nothing here imports ``triton_kubernetes_amd``):
                values for every root output, bumps ``serial`` and keeps ``lineage``;
 * ``destroy``  removes the ``-target``-ed modules' resources (all without targets) and
                the outputs that read them;
-* ``output``   ``-json`` (root outputs, with ``sensitive``) or ``-module=<key>`` (0.11).
+* ``output``   ``-json`` (root outputs, with ``sensitive``) or ``-module=<key>`` (0.11);
+* ``-var=name=value`` must name a declared root ``variable`` ("Value for undeclared
+               variable");
+* with ``FAKE_TF_EXTERNAL=1``, ``data "external"`` programs run during refresh —
+               apply, plan, and destroy unless ``-refresh=false`` (targets + their
+               dependencies) — and a failing program fails the command; module outputs
+               that read a data source get its result.
 
 Every call appends ``{"argv", "cwd", "doc", "prior"}`` to ``$FAKE_TF_LOG`` (``prior``:
 serial/lineage/modules of the state the command started from).  ``FAKE_TF_FAIL=<cmd>``
@@ -31,6 +37,7 @@ partial state is written, as Terraform does.
 import json
 import os
 import re
+import subprocess
 import sys
 import uuid
 
@@ -150,6 +157,187 @@ def state_modules(st):
     return sorted({r["module"][len("module."):] for r in st.get("resources", []) if r.get("module")})
 
 
+# --- data "external" (FAKE_TF_EXTERNAL=1) -------------------------------------------------------
+#
+# Terraform reads data sources while refreshing: every apply and plan, and every destroy
+# unless -refresh=false (for a targeted destroy: the targets and what they depend on).  A
+# data "external" source runs its program on the operator machine with the query as JSON
+# on stdin; a non-zero exit fails the whole command.  Opt-in, because the programs of the
+# packaged modules really reach out (ssh to the manager, HTTP to Rancher): a test turns it
+# on with fakes for those on PATH / in process.  The query is evaluated by a tiny
+# evaluator that knows var.X, local.X (one level) and string literals: enough for the
+# modules' `query = { k = var.x }` / `query = local.request` (a merge of such maps).
+
+def _braced(text, start):
+    """The text between the brace at ``start`` and its match."""
+    depth = 0
+    for i in range(start, len(text)):
+        if text[i] == "{":
+            depth += 1
+        elif text[i] == "}":
+            depth -= 1
+            if depth == 0:
+                return text[start + 1:i]
+    return text[start + 1:]
+
+
+def _module_text(mod_dir):
+    return "\n".join(open(os.path.join(mod_dir, fn), encoding="utf-8").read()
+                     for fn in sorted(os.listdir(mod_dir)) if fn.endswith(".tf"))
+
+
+def _locals(text):
+    out = {}
+    for m in re.finditer(r"^locals\s*\{", text, re.M):
+        body = _braced(text, m.end() - 1)
+        for a in re.finditer(r"^  (\w+)\s*=\s*", body, re.M):
+            rest = body[a.end():]
+            if rest[:1] in "({[" or rest.startswith("merge("):
+                # a multi-line expression: up to the next top-level assignment
+                nxt = re.search(r"^  \w+\s*=", rest, re.M)
+                out[a.group(1)] = rest[:nxt.start()] if nxt else rest
+            else:
+                out[a.group(1)] = rest.split("\n", 1)[0].strip()
+    return out
+
+
+def _var_defaults(text):
+    out = {}
+    for m in re.finditer(r'^variable\s+"(\w+)"\s*\{', text, re.M):
+        d = re.search(r'^\s*default\s*=\s*"((?:[^"\\]|\\.)*)"', _braced(text, m.end() - 1), re.M)
+        if d:
+            out[m.group(1)] = d.group(1)
+    return out
+
+
+def _value(expr, inputs, defaults, local_exprs, depth=0):
+    expr = expr.strip()
+    m = re.fullmatch(r"var\.(\w+)", expr)
+    if m:
+        v = inputs.get(m.group(1), defaults.get(m.group(1), ""))
+        return v if isinstance(v, str) else json.dumps(v)
+    m = re.fullmatch(r"local\.(\w+)", expr)
+    if m and depth < 3 and m.group(1) in local_exprs:
+        return _value(local_exprs[m.group(1)], inputs, defaults, local_exprs, depth + 1)
+    m = re.fullmatch(r'"((?:[^"\\]|\\.)*)"', expr)
+    if m:
+        return m.group(1)
+    return ""
+
+
+def external_sources(mod_dir):
+    """[(name, program argv, query expression)] of a module's data "external" blocks."""
+    text = _module_text(mod_dir)
+    out = []
+    for m in re.finditer(r'^data\s+"external"\s+"(\w+)"\s*\{', text, re.M):
+        body = _braced(text, m.end() - 1)
+        prog = re.search(r"program\s*=\s*\[([^\]]*)\]", body)
+        argv = [s.replace("${path.module}", mod_dir) for s in re.findall(r'"([^"]*)"', prog.group(1))] if prog else []
+        q = re.search(r"^  query\s*=\s*", body, re.M)
+        qexpr = ""
+        if q:
+            rest = body[q.end():]
+            qexpr = "{" + _braced(rest, 0) + "}" if rest.startswith("{") else rest.split("\n", 1)[0]
+        out.append((m.group(1), argv, qexpr))
+    return out
+
+
+def evaluate_query(mod_dir, qexpr, inputs):
+    text = _module_text(mod_dir)
+    local_exprs, defaults = _locals(text), _var_defaults(text)
+    m = re.fullmatch(r"\s*local\.(\w+)\s*", qexpr)
+    if m:
+        qexpr = local_exprs.get(m.group(1), "")
+    return {k: _value(e, inputs, defaults, local_exprs)
+            for k, e in re.findall(r"^\s*(\w+)\s*=\s*([^\n]+?)\s*$", qexpr, re.M)}
+
+
+def data_outputs(mod_dir):
+    """{module output: (data source name, result key)} for outputs that read a data source."""
+    out = {}
+    text = _module_text(mod_dir)
+    for m in re.finditer(r'^output\s+"(\w+)"\s*\{', text, re.M):
+        v = re.search(r'value\s*=\s*data\.external\.(\w+)\.result(?:\["(\w+)"\]|\.(\w+))', _braced(text, m.end() - 1))
+        if v:
+            out[m.group(1)] = (v.group(1), v.group(2) or v.group(3))
+    return out
+
+
+def module_deps(block):
+    return set(re.findall(r"\$\{module\.([A-Za-z0-9_.-]+?)\.", json.dumps(block)))
+
+
+def refresh(doc, keys, root_vars, known_outputs):
+    """Read the data sources of ``keys`` (and what they depend on) in dependency order.
+    Returns ``(outputs by "<key>__<out>", error)``."""
+    modules = doc.get("module") or {}
+    want, todo = set(), list(keys)
+    while todo:
+        k = todo.pop()
+        if k in modules and k not in want:
+            want.add(k)
+            todo.extend(module_deps(modules[k]))
+    outs = dict(known_outputs)
+    done = set()
+
+    def sub(v):
+        if isinstance(v, str):
+            v = re.sub(r"\$\{var\.(\w+)\}", lambda m: str(root_vars.get(m.group(1), "")), v)
+            return re.sub(r"\$\{module\.([A-Za-z0-9_.-]+?)\.(\w+)\}",
+                          lambda m: str(outs.get(f"{m.group(1)}__{m.group(2)}", "")), v)
+        if isinstance(v, dict):
+            return {k: sub(x) for k, x in v.items()}
+        if isinstance(v, list):
+            return [sub(x) for x in v]
+        return v
+
+    while len(done) < len(want):
+        ready = sorted(k for k in want - done if not (module_deps(modules[k]) & want) - done)
+        if not ready:
+            return outs, "Cycle in module references"
+        for key in ready:
+            done.add(key)
+            d = local_dir(str(modules[key].get("source", "")))
+            if d is None:
+                continue
+            inputs = sub(modules[key])
+            results = {}
+            for name, argv, qexpr in external_sources(d):
+                query = evaluate_query(d, qexpr, inputs)
+                try:
+                    proc = subprocess.run(argv, input=json.dumps(query), capture_output=True,
+                                                        text=True, timeout=120)
+                except Exception as exc:  # noqa: BLE001
+                    return outs, f"External Program Execution Failed\n\n  with module.{key}.data.external.{name}: {exc}"
+                if proc.returncode != 0:
+                    return outs, (f"External Program Execution Failed\n\n  with module.{key}.data.external.{name}\n\n"
+                                  f"The data source received an unexpected error while attempting to execute the "
+                                  f"program.\n\nProgram: {argv[-1]}\nError Message: {proc.stderr.strip()}\n"
+                                  f"State: exit status {proc.returncode}")
+                try:
+                    results[name] = json.loads(proc.stdout)
+                except ValueError:
+                    return outs, f"Unexpected External Program Results\n\n  with module.{key}.data.external.{name}"
+            for out, (src, field) in data_outputs(d).items():
+                if src in results:
+                    outs[f"{key}__{out}"] = str(results[src].get(field, ""))
+    return outs, None
+
+
+def root_variables(doc, argv):
+    """Root variable values: declared defaults, then -var=name=value.  ``(values, error)``."""
+    declared = doc.get("variable") or {}
+    vals = {k: (v or {}).get("default", "") for k, v in declared.items()}
+    for a in argv:
+        if a.startswith("-var="):
+            name, _, value = a[len("-var="):].partition("=")
+            if name not in declared:
+                return vals, (f'Value for undeclared variable\n\nA variable named "{name}" was assigned on the '
+                              "command line, but the root module does not declare a variable of that name.")
+            vals[name] = value
+    return vals, None
+
+
 def main() -> int:
     argv = sys.argv[1:]
     cmd = argv[0] if argv else ""
@@ -202,6 +390,21 @@ def main() -> int:
         if problem:
             return fail(problem)
 
+    read = {}  # "<key>__<out>" values the data sources returned in this run's refresh
+    if cmd in ("apply", "destroy", "plan"):
+        root_vars, problem = root_variables(doc, argv)
+        if problem:
+            return fail(problem)
+        if os.environ.get("FAKE_TF_EXTERNAL") == "1" and "-refresh=false" not in argv:
+            targets = [a.split("=", 1)[1][len("module."):] for a in argv if a.startswith("-target=module.")]
+            keys = targets if (cmd == "destroy" and targets) else list(doc.get("module") or {})
+            if cmd == "destroy" and not targets:
+                keys = [k for k in keys if k in state_modules(prior)]
+            known = {k: v.get("value") for k, v in (prior.get("outputs") or {}).items()}
+            read, problem = refresh(doc, keys, root_vars, known)
+            if problem:
+                return fail(problem)
+
     if cmd == "apply":
         st = prior or {"version": 4, "lineage": str(uuid.uuid4()), "serial": 0, "resources": [], "outputs": {}}
         st["terraform_version"] = version_s
@@ -219,7 +422,8 @@ def main() -> int:
             m = re.fullmatch(r"\$\{module\.([^.}]+)\.[^}]+\}", str(spec.get("value", "")))
             if m and m.group(1) not in done:
                 continue
-            outs[name] = {"value": f"fake-{name}", "type": "string", "sensitive": bool(spec.get("sensitive"))}
+            value = read.get(name) or (prior.get("outputs") or {}).get(name, {}).get("value") or f"fake-{name}"
+            outs[name] = {"value": value, "type": "string", "sensitive": bool(spec.get("sensitive"))}
         st["outputs"] = outs
         st["serial"] = int(st.get("serial", 0)) + 1
         save_state(path, st)

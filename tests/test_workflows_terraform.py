@@ -81,15 +81,21 @@ def test_create_manager_cluster_node_and_destroy(tmp_path, monkeypatch, backend)
     delete_node(make_ctx({"cluster_manager": "mgr", "cluster_name": "dev", "hostname": "dev-worker-3",
                           "executor": "terraform"}), backend)
     destroy = [c for c in tf_calls(log) if c["argv"][0] == "destroy"][0]
-    assert destroy["argv"] == ["destroy", "-auto-approve", "-target=module.node_baremetal_dev_dev-worker-3"]
+    # the state is authoritative for a destroy: no refresh (which would re-run the create-side
+    # data sources), and the modules' data sources told it is a destroy should one run
+    assert destroy["argv"] == ["destroy", "-auto-approve", "-refresh=false", "-var=tk_operation=destroy",
+                               "-target=module.node_baremetal_dev_dev-worker-3"]
+    assert destroy["doc"]["variable"] == {"tk_operation": {"type": "string", "default": "apply"}}
+    assert destroy["doc"]["module"]["cluster_baremetal_dev"]["tk_operation"] == "${var.tk_operation}"
     assert "dev-worker-3" not in backend.state("mgr").nodes("cluster_baremetal_dev")
 
     # destroy the cluster: cluster + every node targeted, modules removed
     open(log, "w").close()
     delete_cluster(make_ctx({"cluster_manager": "mgr", "cluster_name": "dev", "executor": "terraform"}), backend)
     destroy = [c for c in tf_calls(log) if c["argv"][0] == "destroy"][0]
-    assert destroy["argv"][:3] == ["destroy", "-auto-approve", "-target=module.cluster_baremetal_dev"]
-    assert len(destroy["argv"]) == 3 + 4
+    assert destroy["argv"][:5] == ["destroy", "-auto-approve", "-refresh=false", "-var=tk_operation=destroy",
+                                    "-target=module.cluster_baremetal_dev"]
+    assert len(destroy["argv"]) == 5 + 4
     assert backend.state("mgr").clusters() == {}
 
     delete_manager(make_ctx({"cluster_manager": "mgr", "executor": "terraform"}), backend)
@@ -105,7 +111,7 @@ def test_terraform_011_flags_and_module_outputs(tmp_path, monkeypatch, backend):
     open(log, "w").close()
     delete_manager(make_ctx({"cluster_manager": "mgr", "executor": "terraform"}), backend)
     destroy = [c for c in tf_calls(log) if c["argv"][0] == "destroy"][0]
-    assert destroy["argv"] == ["destroy", "-force"]
+    assert destroy["argv"] == ["destroy", "-force", "-refresh=false"]  # reference modules: no tk_operation
 
 
 def test_duplicate_manager_name_and_failed_apply_resume(tmp_path, monkeypatch, backend):

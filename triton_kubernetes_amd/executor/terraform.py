@@ -30,7 +30,10 @@ version-dependent ways; the persisted ``main.tf.json`` keeps the reference's lay
   failed one: Terraform records what it created before failing), all under the
   backend's lock (the Manta conditional-PUT lock, ``backend/manta.py``);
 * modules from a local directory (the packaged tree) are checked against their
-  ``required_version`` before ``init``, so a too-old Terraform gets one clear error.
+  ``required_version`` before ``init``, so a too-old Terraform gets one clear error;
+* ``tk::`` module sources (``terraform/catalog.py``) become this install's module
+  directories, the backend block becomes the running operator's, and modules that take
+  ``tk_operation`` get it from a root variable, which ``destroy`` sets to ``destroy``.
 
 ``-parallelism`` is configurable (the reference leaves it at Terraform's default of 10,
 which bounds node fan-out).
@@ -50,8 +53,8 @@ from ..backend.base import Backend
 from ..errors import ExecutorError
 from ..state import State
 from ..terraform import constraints
-from ..terraform.catalog import (check_sources, is_packaged_source, local_module_dir, module_from_source,
-                                 outputs_for_source, resolve_source, sensitive_outputs)
+from ..terraform.catalog import (check_sources, declared_variables, is_packaged_source, local_module_dir,
+                                 module_from_source, outputs_for_source, resolve_source, sensitive_outputs)
 from ..utils.jsonenc import dumps_go
 from .base import Executor, outputs_from_tfstate
 from .shell import ShellOptions, capture_command, run_shell_command
@@ -77,6 +80,14 @@ class Rendered:
     # the state backend is one this Terraform lacks: the CLI carries terraform.tfstate
     managed_state: bool = False
     backend_kind: str = ""
+    # the root variable tk_operation is declared (some module takes it): -var may set it
+    operation_var: bool = False
+
+
+# The root variable through which the executor tells the modules' data sources which CLI
+# operation runs them (terraform/generate.py, ``tk_operation``): ``apply`` finds or
+# creates, ``destroy`` / ``read`` only find and tolerate hosts that are gone.
+OPERATION_VAR = "tk_operation"
 
 
 def _backend_kind(doc: Dict) -> str:
@@ -135,7 +146,15 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
     doc = copy.deepcopy(doc)
     if managed:
         doc["terraform"]["backend"] = {"local": {"path": WORKDIR_TFSTATE}}
+    operation_var = False
     if version >= (0, 12, 0):
+        for mod in (doc.get("module") or {}).values():
+            local = local_module_dir(str(mod.get("source", "")))
+            if local and OPERATION_VAR not in mod and OPERATION_VAR in declared_variables(local):
+                mod[OPERATION_VAR] = f"${{var.{OPERATION_VAR}}}"
+                operation_var = True
+        if operation_var:
+            doc.setdefault("variable", {})[OPERATION_VAR] = {"type": "string", "default": "apply"}
         outputs = doc.setdefault("output", {})
         for key, mod in state.modules().items():
             source = str(mod.get("source", ""))
@@ -148,7 +167,7 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
                 outputs[f"{key}__{out}"] = block
         if not outputs:
             doc.pop("output")
-    return Rendered(dumps_go(doc), managed, kind)
+    return Rendered(dumps_go(doc), managed, kind, operation_var)
 
 
 def render_document(state: State, version: Tuple[int, int, int]) -> bytes:
@@ -174,6 +193,7 @@ class TerraformExecutor(Executor):
         self._version = version
         self.keep_workdir = keep_workdir
         self.last_workdir: Optional[str] = None
+        self.last_rendered: Optional[Rendered] = None
 
     # --- helpers -------------------------------------------------------------------------
     def version(self) -> Tuple[int, int, int]:
@@ -196,6 +216,7 @@ class TerraformExecutor(Executor):
         version = self.version()
         check_module_versions(state, version)
         rendered = render(state, version, backend)
+        self.last_rendered = rendered
         if rendered.managed_state and backend is None:
             raise ExecutorError(f"the {rendered.backend_kind} state backend needs the CLI to carry terraform.tfstate")
         tmp = tempfile.mkdtemp(prefix="triton-kubernetes-")
@@ -246,8 +267,16 @@ class TerraformExecutor(Executor):
         return ["-auto-approve"] if self.version() >= (0, 15, 0) else ["-force"]
 
     def destroy(self, state: State, backend: Backend, targets: Sequence[str]) -> None:
+        """``terraform destroy`` of ``targets`` (all without).  The state is authoritative
+        for a destroy: ``-refresh=false`` skips the pre-destroy refresh, which would re-run
+        the create-side data sources (the API-key read over SSH from a manager host that may
+        be gone; the find-or-create of a Rancher cluster removed out of band, reference
+        ``terraform/modules/triton-rancher/main.tf:128-144``, ``rancher_cluster.sh:17-42``).
+        Should Terraform still read one, ``tk_operation=destroy`` makes it find-only."""
         with self.workdir(state, backend, write_back=True) as wd:
-            args = ["destroy", *self.destroy_flags()]
+            args = ["destroy", *self.destroy_flags(), "-refresh=false"]
+            if self.last_rendered is not None and self.last_rendered.operation_var:
+                args.append(f"-var={OPERATION_VAR}=destroy")
             if self.parallelism:
                 args.append(f"-parallelism={self.parallelism}")
             self._run(wd, *args, *[f"-target={t}" for t in targets])

@@ -87,8 +87,9 @@ REFERENCE_MODULES = [m.name for m in _MODULES if not m.mi355x]
 
 
 # The package directory: ``<PACKAGE_ROOT>/terraform/modules/<name>`` is this project's
-# module tree.  It is the default ``source_url`` (models/common.py), so documents point
-# at the modules that ship with this CLI instead of the reference's Terraform 0.11 ones.
+# module tree.  Documents name it location-free (``tk::`` sources, below) and executors
+# resolve those to it, so documents run the modules that ship with this CLI instead of
+# the reference's Terraform 0.11 ones.
 PACKAGE_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -225,6 +226,29 @@ def check_sources(modules: Dict[str, Dict]) -> None:
                 f"module.{key} points at {source}, a module directory of another triton-kubernetes install that "
                 "does not exist on this machine. Run `triton-kubernetes migrate manager` to rewrite the document's "
                 "module sources to the location-free tk:: form.")
+
+
+_DECLARED: Dict[Tuple[str, float], frozenset] = {}
+
+
+def declared_variables(mod_dir: str) -> frozenset:
+    """Names of the ``variable`` blocks a module directory declares (top level of its .tf
+    files), cached per directory and modification time."""
+    try:
+        stamp = max(os.path.getmtime(os.path.join(mod_dir, f)) for f in os.listdir(mod_dir) if f.endswith(".tf"))
+    except (OSError, ValueError):
+        return frozenset()
+    key = (mod_dir, stamp)
+    if key not in _DECLARED:
+        import re
+
+        names = set()
+        for fn in os.listdir(mod_dir):
+            if fn.endswith(".tf"):
+                with open(os.path.join(mod_dir, fn), encoding="utf-8") as fh:
+                    names.update(re.findall(r'^variable\s+"([^"]+)"', fh.read(), re.M))
+        _DECLARED[key] = frozenset(names)
+    return _DECLARED[key]
 
 
 def local_module_dir(source: str) -> Optional[str]:

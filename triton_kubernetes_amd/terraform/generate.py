@@ -129,6 +129,9 @@ VAR_DOCS = {
     "gpu_burnin": "Burn-in level run on every GPU before the node joins.",
     "rccl_env": "Extra RCCL/HSA environment written to /etc/rccl/rccl.env.",
     "docker_install_sha256": "SHA-256 the downloaded runtime install script must match (empty: not checked).",
+    "tk_operation": ("Which CLI operation runs this configuration (set by the executor through the root "
+                     "variable of the same name): apply runs the create-side data sources in full; destroy and read "
+                     "make them find-only and tolerant of hosts that are gone."),
     "rancher_bootstrap_password": ("First-login password of the Rancher server (CATTLE_BOOTSTRAP_PASSWORD); "
                                    "empty: derived from name and rancher_admin_password."),
 }
@@ -153,6 +156,8 @@ VAR_VALIDATIONS = {
                     f"k8s_version must be an RKE2 ({', '.join(v for _, v in versions.RKE2_VERSIONS)}) or RKE1 "
                     f"({', '.join(v for _, v in versions.K8S_VERSIONS)}) release of Rancher "
                     f"{versions.RANCHER_VERSION}."),
+    "tk_operation": ('contains(["apply", "destroy", "read"], var.tk_operation)',
+                     "tk_operation must be apply, destroy or read."),
     "k8s_distribution": ('contains(["rke2", "rke1"], var.k8s_distribution)', "k8s_distribution must be rke2 or rke1."),
     "k8s_network_provider": ('contains(["canal", "calico", "cilium", "flannel", "weave"], var.k8s_network_provider)',
                              "k8s_network_provider must be one of canal, calico, cilium, flannel (RKE2) or weave "
@@ -229,9 +234,9 @@ def _rancher_image_vars(server: bool = True) -> List[Var]:
 
 MANAGER_BASE = [Var("name", None, "Human readable name used as prefix to generated names."),
                 Var("rancher_admin_password", None, "The Rancher admin password", sensitive=True),
-                Var("rancher_bootstrap_password", "", sensitive=True)]
+                Var("rancher_bootstrap_password", "", sensitive=True), Var("tk_operation", "apply")]
 CLUSTER_BASE = [
-    Var("name", None, "Human readable name used as prefix to generated names."),
+    Var("name", None, "Human readable name used as prefix to generated names."), Var("tk_operation", "apply"),
     Var("rancher_api_url", None), Var("rancher_access_key", None), Var("rancher_secret_key", None, sensitive=True),
     Var("k8s_distribution", versions.DEFAULT_DISTRIBUTION,
         "rke2 (provisioning.cattle.io/v1 custom cluster, nodes join with rancher-system-agent) or rke1 "
@@ -354,6 +359,7 @@ data "external" "rancher_api_key" {{
     ssh_user     = local.ssh_user
     key_path     = local.key_path
     bastion_host = local.bastion_host
+    operation    = var.tk_operation
   }}
 }}
 '''
@@ -418,6 +424,7 @@ def _cluster_data() -> str:
       version      = var.k8s_version
       network      = var.k8s_network_provider
       distribution = var.k8s_distribution
+      operation    = var.tk_operation
     }},
     {{
       api_url    = var.rancher_api_url
@@ -1236,6 +1243,7 @@ resource "terraform_data" "install_rancher_agent" {{
     # MI355X bare-metal host
     mods.append(Module("bare-metal-mi355x-rancher-k8s-host", ["external"], HOST_BASE + [
         Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa"),
+        Var("tk_operation", "apply"),
         Var("gpu_product", "MI355X"), Var("gpu_count", 8, "GPUs the node must expose"),
         Var("gpu_burnin", "quick", "quick | full | off"),
         Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
@@ -1323,6 +1331,7 @@ data "external" "gpu_labels" {{
     ssh_user     = var.ssh_user
     key_path     = var.key_path
     bastion_host = var.bastion_host
+    operation    = var.tk_operation
   }}
 }}
 ''', [("gpu_node_labels", "data.external.gpu_labels.result.labels", False)],

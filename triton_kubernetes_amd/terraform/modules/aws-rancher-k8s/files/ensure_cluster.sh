@@ -6,6 +6,9 @@
 # registry_username, registry_password.  RKE2: a provisioning.cattle.io/v1 Cluster in
 # fleet-default whose management cluster (status.clusterName) holds the token; RKE1:
 # the v3 cluster with rancherKubernetesEngineConfig (the reference's flow).
+# Query key operation (the executor's tk_operation): apply finds or creates; destroy and
+# read only find -- a destroy must never re-create a cluster removed out of band -- and
+# a Rancher that is gone or unreachable then yields empty outputs instead of an error.
 exec python3 -c '
 import base64, hashlib, json, re, ssl, sys, time, urllib.error, urllib.parse, urllib.request
 
@@ -48,6 +51,28 @@ def k8s_version(requested, rke2=False):
                  % (requested, ", ".join(offered)))
     return max(same, key=lambda v: [int(x) for x in re.findall(r"[0-9]+", v)])
 
+
+def ca_checksum():
+    cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
+    if cacerts and not cacerts.endswith("\n"):
+        cacerts += "\n"  # Rancher hashes the bundle with one trailing newline, as /cacerts serves it
+    return hashlib.sha256(cacerts.encode()).hexdigest() if cacerts else ""
+
+
+op = q.get("operation", "apply")
+if op != "apply":
+    out = {"cluster_id": "", "registration_token": "", "ca_checksum": ""}
+    try:
+        found = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
+        if found:
+            out["cluster_id"] = found[0]["id"]
+            toks = call("GET", "/v3/clusters/%s/clusterregistrationtokens" % found[0]["id"]).get("data") or []
+            out["registration_token"] = (toks[0].get("token") or "") if toks else ""
+            out["ca_checksum"] = ca_checksum()
+    except Exception as exc:  # noqa: BLE001 - find-only: nothing to create, nothing to fail
+        sys.stderr.write("ensure_cluster (%s): %s\n" % (op, exc))
+    print(json.dumps(out))
+    sys.exit(0)
 
 dist = q.get("distribution", "rke2")
 v3 = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
@@ -121,9 +146,5 @@ if not token:
         token = call("GET", "/v3/clusterregistrationtokens/" + created["id"]).get("token")
 if not token:
     sys.exit("Unable to create cluster registration token!")
-cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
-if cacerts and not cacerts.endswith("\n"):
-    cacerts += "\n"  # Rancher hashes the bundle with one trailing newline, as /cacerts serves it
-print(json.dumps({"cluster_id": cluster_id, "registration_token": token,
-                  "ca_checksum": hashlib.sha256(cacerts.encode()).hexdigest() if cacerts else ""}))
+print(json.dumps({"cluster_id": cluster_id, "registration_token": token, "ca_checksum": ca_checksum()}))
 '

@@ -3,6 +3,17 @@ variable "name" {
   type        = string
 }
 
+variable "tk_operation" {
+  description = "Which CLI operation runs this configuration (set by the executor through the root variable of the same name): apply runs the create-side data sources in full; destroy and read make them find-only and tolerant of hosts that are gone."
+  type        = string
+  default     = "apply"
+
+  validation {
+    condition     = contains(["apply", "destroy", "read"], var.tk_operation)
+    error_message = "tk_operation must be apply, destroy or read."
+  }
+}
+
 variable "rancher_api_url" {
   description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
   type        = string

@@ -26,6 +26,17 @@ variable "rancher_bootstrap_password" {
   }
 }
 
+variable "tk_operation" {
+  description = "Which CLI operation runs this configuration (set by the executor through the root variable of the same name): apply runs the create-side data sources in full; destroy and read make them find-only and tolerant of hosts that are gone."
+  type        = string
+  default     = "apply"
+
+  validation {
+    condition     = contains(["apply", "destroy", "read"], var.tk_operation)
+    error_message = "tk_operation must be apply, destroy or read."
+  }
+}
+
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
   type        = string

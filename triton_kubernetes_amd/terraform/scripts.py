@@ -85,11 +85,18 @@ curl -ksf -u "$ak:$sk" -X PUT -H 'Content-Type: application/json' \
 READ_API_KEY = r"""#!/bin/bash
 # data "external" program: read the manager's ~/rancher_api_key over SSH.
 # Replaces the reference's matti/outputs/shell registry module.
+# Outside an apply (query key operation = destroy | read, the executor's tk_operation)
+# a manager that cannot be reached yields empty keys instead of an error: destroying
+# what is left of a manager whose host is gone must not depend on that host.
 set -euo pipefail
 eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
 opts=(-o BatchMode=yes -o StrictHostKeyChecking=no -o UserKnownHostsFile=/dev/null -o LogLevel=ERROR -i "${key_path/#\~/$HOME}")
 if [ -n "${bastion_host:-}" ]; then opts+=(-J "$ssh_user@$bastion_host"); fi
-tok=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_api_key')
+if ! tok=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_api_key'); then
+  if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": ""}'; exit 0; fi
+  echo "could not read the Rancher API key from $host" >&2
+  exit 1
+fi
 printf '%s' "$tok" | python3 -c '
 import json, sys
 t = json.load(sys.stdin)
@@ -104,6 +111,9 @@ RANCHER_CLUSTER = r"""#!/bin/bash
 # registry_username, registry_password.  RKE2: a provisioning.cattle.io/v1 Cluster in
 # fleet-default whose management cluster (status.clusterName) holds the token; RKE1:
 # the v3 cluster with rancherKubernetesEngineConfig (the reference's flow).
+# Query key operation (the executor's tk_operation): apply finds or creates; destroy and
+# read only find -- a destroy must never re-create a cluster removed out of band -- and
+# a Rancher that is gone or unreachable then yields empty outputs instead of an error.
 exec python3 -c '
 import base64, hashlib, json, re, ssl, sys, time, urllib.error, urllib.parse, urllib.request
 
@@ -146,6 +156,28 @@ def k8s_version(requested, rke2=False):
                  % (requested, ", ".join(offered)))
     return max(same, key=lambda v: [int(x) for x in re.findall(r"[0-9]+", v)])
 
+
+def ca_checksum():
+    cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
+    if cacerts and not cacerts.endswith("\n"):
+        cacerts += "\n"  # Rancher hashes the bundle with one trailing newline, as /cacerts serves it
+    return hashlib.sha256(cacerts.encode()).hexdigest() if cacerts else ""
+
+
+op = q.get("operation", "apply")
+if op != "apply":
+    out = {"cluster_id": "", "registration_token": "", "ca_checksum": ""}
+    try:
+        found = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
+        if found:
+            out["cluster_id"] = found[0]["id"]
+            toks = call("GET", "/v3/clusters/%s/clusterregistrationtokens" % found[0]["id"]).get("data") or []
+            out["registration_token"] = (toks[0].get("token") or "") if toks else ""
+            out["ca_checksum"] = ca_checksum()
+    except Exception as exc:  # noqa: BLE001 - find-only: nothing to create, nothing to fail
+        sys.stderr.write("ensure_cluster (%s): %s\n" % (op, exc))
+    print(json.dumps(out))
+    sys.exit(0)
 
 dist = q.get("distribution", "rke2")
 v3 = call("GET", "/v3/clusters?name=" + urllib.parse.quote(q["name"])).get("data") or []
@@ -219,11 +251,7 @@ if not token:
         token = call("GET", "/v3/clusterregistrationtokens/" + created["id"]).get("token")
 if not token:
     sys.exit("Unable to create cluster registration token!")
-cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
-if cacerts and not cacerts.endswith("\n"):
-    cacerts += "\n"  # Rancher hashes the bundle with one trailing newline, as /cacerts serves it
-print(json.dumps({"cluster_id": cluster_id, "registration_token": token,
-                  "ca_checksum": hashlib.sha256(cacerts.encode()).hexdigest() if cacerts else ""}))
+print(json.dumps({"cluster_id": cluster_id, "registration_token": token, "ca_checksum": ca_checksum()}))
 '
 """
 
@@ -478,7 +506,13 @@ set -euo pipefail
 eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
 opts=(-o BatchMode=yes -o StrictHostKeyChecking=no -o UserKnownHostsFile=/dev/null -o LogLevel=ERROR -i "${key_path/#\~/$HOME}")
 if [ -n "${bastion_host:-}" ]; then opts+=(-J "$ssh_user@$bastion_host"); fi
-ssh "${opts[@]}" "$ssh_user@$host" 'cat /etc/triton-kubernetes/gpu-labels; cat /etc/triton-kubernetes/gpu-burnin-labels 2>/dev/null || true' | python3 -c '
+if ! raw=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat /etc/triton-kubernetes/gpu-labels; cat /etc/triton-kubernetes/gpu-burnin-labels 2>/dev/null || true'); then
+  # outside an apply (operation destroy | read) a node that is gone has no labels to report
+  if [ "${operation:-apply}" != apply ]; then echo '{"labels": "{}"}'; exit 0; fi
+  echo "could not read the GPU labels of $host" >&2
+  exit 1
+fi
+printf '%s\n' "$raw" | python3 -c '
 import json, sys
 labels = dict(l.strip().split("=", 1) for l in sys.stdin if "=" in l)
 print(json.dumps({"labels": json.dumps(labels, sort_keys=True)}))'
