@@ -214,8 +214,15 @@ def test_injector_end_to_end_through_admission(tmp_path):
         client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
         created = client.k8s(cid, "POST", "/api/v1/namespaces/default/pods", _gpu_pod(), ok=(201,))
         env = {e["name"]: e["value"] for e in created["spec"]["containers"][0]["env"]}
-        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and env["TK_RCCL_ENV_FILE"] == "/etc/rccl/rccl.env"
+        # an unlabelled namespace: the cluster env, not the node's /etc/rccl (opt-in)
+        assert env["HSA_ENABLE_IPC_MODE_LEGACY"] == "0" and "TK_RCCL_ENV_FILE" not in env
         assert created["metadata"]["annotations"]["amd.com/rccl-env"] == "injected"
+        client.k8s(cid, "POST", "/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {
+            "name": "train", "labels": {"amd.com/rccl-node-env": "true"}}}, ok=(201,))
+        opted = client.k8s(cid, "POST", "/api/v1/namespaces/train/pods", _gpu_pod(), ok=(201,))
+        env = {e["name"]: e["value"] for e in opted["spec"]["containers"][0]["env"]}
+        assert env["TK_RCCL_ENV_FILE"] == "/etc/rccl/rccl.env"
+        assert opted["spec"]["volumes"][0]["hostPath"]["path"] == "/etc/rccl"
         # and the 8-GPU pod must land on one fully connected xGMI hive
         terms = created["spec"]["affinity"]["nodeAffinity"]["requiredDuringSchedulingIgnoredDuringExecution"][
             "nodeSelectorTerms"]
@@ -394,11 +401,13 @@ def test_injector_respects_pod_security_admission(tmp_path):
         hook = [t.obj for t in addons.addon_templates() if t.obj.get("kind") == "MutatingWebhookConfiguration"][0]
         hook = json.loads(json.dumps(hook).replace("${injector_ca_b64}",
                                                     base64.b64encode(cert.ca_pem.encode()).decode()))
-        assert [w["clientConfig"]["service"]["path"] for w in hook["webhooks"]] == ["/mutate",
+        assert [w["clientConfig"]["service"]["path"] for w in hook["webhooks"]] == ["/mutate", "/mutate",
                                                                                   "/mutate?node-env=omit"]
         post("/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations", hook)
-        for ns, level in (("hardened", "restricted"), ("base", "baseline"), ("open", None)):
-            labels = {"pod-security.kubernetes.io/enforce": level} if level else {}
+        for ns, labels in (("hardened", {"pod-security.kubernetes.io/enforce": "restricted"}),
+                           ("base", {"pod-security.kubernetes.io/enforce": "baseline"}), ("open", {}),
+                           ("priv", {"pod-security.kubernetes.io/enforce": "privileged"}),
+                           ("optin", {"amd.com/rccl-node-env": "true"})):
             post("/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace",
                                         "metadata": {"name": ns, "labels": labels}})
         hard = post("/api/v1/namespaces/hardened/pods", _restricted_gpu_pod("h1"))
@@ -407,13 +416,19 @@ def test_injector_respects_pod_security_admission(tmp_path):
         assert "volumes" not in hard["spec"] and "volumeMounts" not in c
         assert hard["metadata"]["annotations"]["amd.com/rccl-env"] == "injected"
         assert hard["metadata"]["annotations"]["amd.com/rccl-env-node"].startswith("omitted")
+        assert "amd.com/rccl-node-env=true" in hard["metadata"]["annotations"]["amd.com/rccl-env-node"]
         assert hard["spec"]["affinity"]["nodeAffinity"]  # placement still applies
         base = post("/api/v1/namespaces/base/pods", _gpu_pod("b1"))
         assert "volumes" not in base["spec"] and base["spec"]["containers"][0]["env"]
+        # an unlabelled namespace does not say which level applies: no hostPath either
         opened = post("/api/v1/namespaces/open/pods", _gpu_pod("o1"))
-        assert opened["spec"]["volumes"][0]["hostPath"]["path"] == "/etc/rccl"
-        env = {e["name"] for e in opened["spec"]["containers"][0]["env"]}
-        assert env == {"NCCL_DEBUG", "TK_RCCL_ENV_FILE"}
+        assert "volumes" not in opened["spec"] and opened["spec"]["containers"][0]["env"]
+        # the two opt-ins keep the node's /etc/rccl
+        for ns in ("priv", "optin"):
+            pod = post(f"/api/v1/namespaces/{ns}/pods", _gpu_pod(f"{ns}1"))
+            assert pod["spec"]["volumes"][0]["hostPath"]["path"] == "/etc/rccl", ns
+            assert {e["name"] for e in pod["spec"]["containers"][0]["env"]} == {"NCCL_DEBUG", "TK_RCCL_ENV_FILE"}
+            assert "amd.com/rccl-env-node" not in pod["metadata"]["annotations"]
         # round 2's single entry (hostPath everywhere): the restricted pod is rejected
         old = json.loads(json.dumps(hook))
         old["metadata"]["name"] = "old-injector"
@@ -424,6 +439,66 @@ def test_injector_respects_pod_security_admission(tmp_path):
         post("/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations", old)
         with pytest.raises(HTTPError) as exc:
             post("/api/v1/namespaces/hardened/pods", _restricted_gpu_pod("h2"))
+        assert exc.value.status == 403 and "violates PodSecurity" in exc.value.body.decode()
+    finally:
+        if srv is not None:
+            srv.shutdown()
+        fake.stop()
+
+
+@pytest.mark.skipif(not have("openssl"), reason="openssl needed for the serving certificate")
+def test_injector_under_cluster_default_pod_security(tmp_path):
+    """a cluster that enforces Pod Security by default (API-server
+    AdmissionConfiguration default; Rancher's rancher-restricted template, RKE2's CIS
+    profile) applies ``restricted`` to every namespace without a label.  Round 3's split
+    keyed on the label alone and added the hostPath there, so such pods were rejected; now
+    an unlabelled namespace's GPU pod is admitted with the cluster env, and a namespace
+    that opts in still gets /etc/rccl."""
+    from triton_kubernetes_amd.cloud.http import HTTPError
+
+    fake = FakeRancher(bootstrap_password="b00tstrap-only", default_pod_security="restricted").start()
+    srv = None
+    try:
+        outs = RancherClient(fake.url).bootstrap("n3w-passw0rd-123", fake.url, "b00tstrap-only", timeout=10)
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        cid = client.ensure_cluster("psa-default").cluster_id
+
+        def post(path, body):
+            return client.k8s(cid, "POST", path, body, ok=(201,))
+
+        cert = serving_cert(addons.INJECTOR, "kube-system")
+        (tmp_path / "tls.crt").write_text(cert.cert_pem)
+        (tmp_path / "tls.key").write_text(cert.key_pem)
+        envdir = tmp_path / "env"
+        envdir.mkdir()
+        (envdir / "NCCL_DEBUG").write_text("WARN")
+        (envdir / "NCCL_IB_HCA").write_text("rdma0")
+        srv = webhook.make_server(0, str(envdir), str(tmp_path / "tls.crt"), str(tmp_path / "tls.key"), "127.0.0.1")
+        threading.Thread(target=srv.serve_forever, daemon=True).start()
+        fake.service_endpoints["rccl-env-injector.kube-system"] = f"https://127.0.0.1:{srv.server_address[1]}"
+        hook = [t.obj for t in addons.addon_templates() if t.obj.get("kind") == "MutatingWebhookConfiguration"][0]
+        hook = json.loads(json.dumps(hook).replace("${injector_ca_b64}",
+                                                    base64.b64encode(cert.ca_pem.encode()).decode()))
+        post("/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations", hook)
+        post("/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "team-a"}})
+        post("/api/v1/namespaces", {"apiVersion": "v1", "kind": "Namespace", "metadata": {
+            "name": "hpc", "labels": {"pod-security.kubernetes.io/enforce": "privileged"}}})
+
+        pod = post("/api/v1/namespaces/team-a/pods", _restricted_gpu_pod("t1"))  # admitted
+        env = {e["name"]: e["value"] for e in pod["spec"]["containers"][0]["env"]}
+        assert env == {"NCCL_DEBUG": "WARN", "NCCL_IB_HCA": "rdma0"}  # the cluster env
+        assert "volumes" not in pod["spec"]
+        assert pod["metadata"]["annotations"]["amd.com/rccl-env-node"].startswith("omitted")
+        # the namespace that opts in (explicitly privileged) keeps the node's /etc/rccl
+        priv = post("/api/v1/namespaces/hpc/pods", _gpu_pod("h1"))
+        assert priv["spec"]["volumes"][0]["hostPath"]["path"] == "/etc/rccl"
+        # the fake enforces the default: a hostPath pod in the unlabelled namespace is refused,
+        # which is what round 3's injector did to every GPU pod there
+        hp = _restricted_gpu_pod("t2")
+        hp["spec"]["volumes"] = [{"name": "x", "hostPath": {"path": "/etc/rccl"}}]
+        hp["metadata"]["annotations"] = {"amd.com/rccl-env-inject": "false"}
+        with pytest.raises(HTTPError) as exc:
+            post("/api/v1/namespaces/team-a/pods", hp)
         assert exc.value.status == 403 and "violates PodSecurity" in exc.value.body.decode()
     finally:
         if srv is not None:

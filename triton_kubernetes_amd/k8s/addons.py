@@ -36,6 +36,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 from .. import versions
 from ..parallel.rccl_env import default_rccl_env
+from . import webhook
 from .manifests import (GPU_SELECTOR, LABELLER_NAME, NAMESPACE, device_plugin_daemonset, gpu_job_manifest,
                         labeller_daemonset, rccl_configmap)
 
@@ -120,9 +121,12 @@ def _injector() -> List[Tuple[str, str, Dict[str, Any]]]:
     svc = {"apiVersion": "v1", "kind": "Service", "metadata": {"name": INJECTOR, "namespace": NAMESPACE},
            "spec": {"selector": dict(labels), "ports": [{"port": 443, "targetPort": 8443, "name": "https"}]}}
     never_own = {"key": "kubernetes.io/metadata.name", "operator": "NotIn", "values": [NAMESPACE]}
-    psa = {"key": "pod-security.kubernetes.io/enforce", "values": ["baseline", "restricted"]}
+    opted_in = {"key": webhook.NODE_ENV_OPT_IN, "operator": "In", "values": ["true"]}
+    not_opted_in = dict(opted_in, operator="NotIn")
+    privileged = {"key": webhook.PSA_LABEL, "operator": "In", "values": ["privileged"]}
+    not_privileged = dict(privileged, operator="NotIn")
 
-    def entry(name: str, path: str, psa_op: str) -> Dict[str, Any]:
+    def entry(name: str, path: str, *select: Dict[str, Any]) -> Dict[str, Any]:
         return {
             "name": name,
             "clientConfig": {"service": {"name": INJECTOR, "namespace": NAMESPACE, "path": path, "port": 443},
@@ -130,18 +134,22 @@ def _injector() -> List[Tuple[str, str, Dict[str, Any]]]:
             "rules": [{"operations": ["CREATE"], "apiGroups": [""], "apiVersions": ["v1"], "resources": ["pods"],
                        "scope": "Namespaced"}],
             # never the injector's own namespace (its pods must start without it)
-            "namespaceSelector": {"matchExpressions": [dict(never_own), dict(psa, operator=psa_op)]},
+            "namespaceSelector": {"matchExpressions": [dict(never_own)] + [dict(e) for e in select]},
             "failurePolicy": "Ignore", "sideEffects": "None", "admissionReviewVersions": ["v1"],
             "timeoutSeconds": 5, "reinvocationPolicy": "IfNeeded",
         }
 
-    # Pod Security Admission runs after mutation and its baseline/restricted levels forbid
-    # hostPath: namespaces enforcing them get the env without the node's /etc/rccl mount
+    # Pod Security Admission runs after mutation, its baseline/restricted levels forbid
+    # hostPath, and a cluster-wide default level applies to namespaces without a label: the
+    # node's /etc/rccl mount goes only to namespaces that opt in (the rccl-node-env label, or
+    # an explicit privileged enforce label); every other namespace gets the env without it.
+    # (matchExpressions are ANDed: one entry per alternative, disjoint by construction.)
     hook = {
         "apiVersion": "admissionregistration.k8s.io/v1", "kind": "MutatingWebhookConfiguration",
         "metadata": {"name": INJECTOR},
-        "webhooks": [entry("rccl-env.amd.com", "/mutate", "NotIn"),
-                     entry("rccl-env-psa.amd.com", "/mutate?node-env=omit", "In")],
+        "webhooks": [entry("rccl-env-node.amd.com", "/mutate", opted_in),
+                     entry("rccl-env-privileged.amd.com", "/mutate", privileged, not_opted_in),
+                     entry("rccl-env.amd.com", "/mutate?node-env=omit", not_privileged, not_opted_in)],
     }
     return [("40-injector-tls.json", f"/api/v1/namespaces/{NAMESPACE}/secrets", secret),
             ("41-injector-src.json", f"/api/v1/namespaces/{NAMESPACE}/configmaps", src),

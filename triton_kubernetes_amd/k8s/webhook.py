@@ -19,13 +19,18 @@ container) gets, at admission time:
 
 Pod Security Admission runs *after* mutating webhooks, and its ``baseline`` and
 ``restricted`` levels forbid ``hostPath`` volumes: mounting ``/etc/rccl`` into a pod in
-such a namespace would get the pod rejected for a change it never asked for.  So the
-add-ons register the injector twice (``k8s/addons.py``), split by namespace label
-``pod-security.kubernetes.io/enforce``: namespaces enforcing ``baseline`` or
-``restricted`` are served on ``/mutate?node-env=omit`` -- the cluster env, the
-placement, no ``hostPath``, no ``TK_RCCL_ENV_FILE``, and the annotation
-``amd.com/rccl-env-node: omitted (Pod Security <level>)`` saying why -- every other
-namespace on ``/mutate``.
+such a namespace would get the pod rejected for a change it never asked for.  A
+namespace's label does not say which level applies to it: clusters that enforce Pod
+Security by default (an API-server ``AdmissionConfiguration`` default -- Rancher's
+``rancher-restricted`` PSA template, RKE2's CIS profile) apply it to every *unlabelled*
+namespace.  So the ``hostPath`` is opt-in, and the add-ons register the injector three
+times (``k8s/addons.py``), split by namespace label:
+
+* ``amd.com/rccl-node-env=true`` or ``pod-security.kubernetes.io/enforce=privileged``:
+  served on ``/mutate`` -- the cluster env plus the node's ``/etc/rccl``;
+* every other namespace: served on ``/mutate?node-env=omit`` -- the cluster env, the
+  placement, no ``hostPath``, no ``TK_RCCL_ENV_FILE``, and the annotation
+  ``amd.com/rccl-env-node: omitted (...)`` saying how to opt in.
 
 A pod opts out of the env with the annotation ``amd.com/rccl-env-inject: "false"`` and of
 the placement with ``amd.com/xgmi-placement: "false"``.  The
@@ -63,7 +68,7 @@ NODE_DIR = "/etc/rccl"
 ENV_FILE_VAR = "TK_RCCL_ENV_FILE"
 NODE_ENV_MARK = "amd.com/rccl-env-node"
 PSA_LABEL = "pod-security.kubernetes.io/enforce"
-PSA_NO_HOSTPATH = ("baseline", "restricted")
+NODE_ENV_OPT_IN = "amd.com/rccl-node-env"  # namespace label: "true" = mount the node's /etc/rccl
 PLACEMENT_OPT_OUT = "amd.com/xgmi-placement"
 GROUP_LABEL = "amd.com/xgmi-group"
 HIVE_KEY = "amd.com/xgmi.hive-id"
@@ -203,7 +208,8 @@ def _env_ops(pod: Dict[str, Any], env: Dict[str, str], node_env: bool = True) ->
             else:
                 ops.append({"op": "add", "path": "/spec/volumes", "value": [vol]})
     else:
-        marks[NODE_ENV_MARK] = "omitted (the namespace's Pod Security level forbids the /etc/rccl hostPath)"
+        marks[NODE_ENV_MARK] = (f"omitted (the /etc/rccl hostPath is opt-in: label the namespace {NODE_ENV_OPT_IN}=true "
+                                f"or {PSA_LABEL}=privileged)")
     if meta.get("annotations"):
         ops += [{"op": "add", "path": f"/metadata/annotations/{_esc(k)}", "value": v} for k, v in marks.items()]
     else:
