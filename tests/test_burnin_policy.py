@@ -74,3 +74,51 @@ def test_checksum_mismatch_is_never_retried_away(scripted):
     calls["gemm_bf16"] = 0
     res = probe.run_burnin(0, "quick")
     assert not res.ok and calls["gemm_bf16"] == 1
+
+
+def test_default_burnin_level_is_full():
+    """a node joining a cluster memtests its whole HBM by default; quick
+    stays an explicit choice.  Pinned at every place a default lives."""
+    import os
+    import re
+
+    from triton_kubernetes_amd.models import baremetal
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.state import State
+    from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+
+    from helpers import make_ctx
+
+    st = State("mgr")
+    name = baremetal.new_cluster(make_ctx({"name": "dev", "k8s_version": "v1.28.10-rancher1-1",
+                                           "k8s_network_provider": "flannel"}), None, st)
+    key = st.clusters()[name]
+    node = {"rancher_host_label": "worker", "node_count": 1, "hostname": "g", "ssh_user": "u", "bastion_host": "",
+            "key_path": "k", "hosts": ["10.0.0.20"], "gpu": "mi355x"}
+    baremetal.new_node(make_ctx(node), "mgr", key, None, st)
+    assert st.module("node_baremetal_dev_g-1")["gpu_burnin"] == "full"
+    baremetal.new_node(make_ctx(dict(node, hosts=["10.0.0.21"], gpu_burnin="quick")), "mgr", key, None, st)
+    assert st.module("node_baremetal_dev_g-2")["gpu_burnin"] == "quick"  # explicit choice kept
+    # the Terraform host module's own default
+    text = open(os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "variables.tf")).read()
+    block = re.search(r'variable "gpu_burnin" \{(.*?)\n\}', text, re.S).group(1)
+    assert re.search(r'default\s*=\s*"full"', block)
+    # a plan built from a block without the key, and the on-node executable's default
+    cfg = dict(st.module("node_baremetal_dev_g-1"))
+    cfg.pop("gpu_burnin")
+    plan = build_host_plan(cfg, "https://r", "t", "c", mi355x=True)
+    step = next(s for s in plan.steps if s.action == "gpu_burnin")
+    assert step.params["level"] == "full"
+    src = open(os.path.join(os.path.dirname(probe.__file__), "csrc", "tk_gpu_probe.hip")).read()
+    assert 'const char* level = "full";' in src
+
+
+def test_partitioned_full_memtest_frees_the_arena_before_sizing(scripted, monkeypatch):
+    order = []
+    monkeypatch.setattr(probe, "release_scratch", lambda dev=None: order.append(("release", dev)) or 0)
+    monkeypatch.setattr(probe, "free_bytes", lambda dev: order.append(("free", dev)) or (280 << 30))
+    monkeypatch.setattr(probe, "memtest_span", lambda dev, nbytes, passes=1: order.append(("span", nbytes)) or {
+        "errors": 0, "verify_gbps": 5000.0, "bytes": nbytes, "hbm_bytes": 288 << 30})
+    res = probe.run_burnin(0, "full", probe.Thresholds.for_partition("cpx", "nps2"))
+    assert res.ok, res.failures
+    assert [o[0] for o in order] == ["release", "free", "span"]

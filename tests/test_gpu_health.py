@@ -463,7 +463,7 @@ def test_get_nodes_shows_gpu_state(tmp_path):
         rows = {ln.split()[0]: ln.split() for ln in lines[1:]}
         assert set(rows) == {"cp-1", "etcd-1", "gpu-1", "gpu-2"}
         assert rows["gpu-1"][3] == versions.DEFAULT_K8S_VERSION
-        assert rows["gpu-1"][4:] == ["8/8", "MI355X", "spx/nps1", "passed(quick)", "mesh", "x16", "0/0", "healthy"]
+        assert rows["gpu-1"][4:] == ["8/8", "MI355X", "spx/nps1", "passed(full)", "mesh", "x16", "0/0", "healthy"]
         assert rows["gpu-2"][4] == "0/8" and rows["gpu-2"][-1] == "unhealthy,tainted"
         assert rows["gpu-2"][-2] == "2/0"
         assert rows["cp-1"][1] == "Ready" and rows["cp-1"][4] == "-"

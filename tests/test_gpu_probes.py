@@ -391,3 +391,71 @@ def test_memtest_span_with_nothing_allocatable_reports_zero():
 
     res = probe.memtest_span(0, 4 << 40, chunk=2 << 40)  # a 2 TiB chunk never fits
     assert res["bytes"] == 0 and res["errors"] == 0
+
+
+def test_memtest_span_tests_what_it_can_hold_when_hbm_shrinks():
+    """the span is sized from hipMemGetInfo when it runs; HBM another
+    process takes between that read and the allocations (simulated: chunk allocations after
+    the third fail) shrinks the span instead of failing it, and everything is released."""
+    from triton_kubernetes_amd.ops import probe
+
+    probe.wait_frees()
+    before = probe.free_bytes(0)
+    probe.set_fail_point("memtest_span.alloc_limit=3")
+    try:
+        res = probe.memtest_span(0, 8 << 30, chunk=1 << 30)
+    finally:
+        probe.set_fail_point("")
+    assert res["errors"] == 0 and res["bytes"] == 3 << 30
+    probe.wait_frees()
+    assert probe.free_bytes(0) >= before - (1 << 30)
+
+
+def test_full_span_leaves_other_processes_memory_alone(tmp_path):
+    """The driver's multi-rank SCALE shape: other processes hold contexts (and memory) on the
+    GPU while the agent's full memtest runs.  The span covers what is free then, minus the
+    headroom, and the other process's data is intact and it can still allocate."""
+    from triton_kubernetes_amd.ops import probe
+
+    holder = tmp_path / "holder.py"
+    holder.write_text(
+        "import sys, torch\n"
+        "x = torch.arange(16 << 28, dtype=torch.int32, device='cuda')  # 16 GiB\n"
+        "torch.cuda.synchronize(); print('held', flush=True)\n"
+        "sys.stdin.readline()\n"
+        "ok = bool((x == torch.arange(16 << 28, dtype=torch.int32, device='cuda')).all())\n"
+        "y = torch.empty(1 << 30, dtype=torch.uint8, device='cuda')\n"
+        "print('intact' if ok else 'corrupt', flush=True)\n")
+    proc = subprocess.Popen([sys.executable, str(holder)], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+    try:
+        assert proc.stdout.readline().strip() == "held"
+        probe.wait_frees()
+        free_now = probe.free_bytes(0)
+        res = probe.memtest_span(0, 0, headroom=4 << 30, passes=1)
+        print(json.dumps(dict(res, free_before=free_now)))
+        assert res["errors"] == 0
+        assert free_now - (5 << 30) <= res["bytes"] <= free_now - (4 << 30)
+        probe.wait_frees()
+        out, _ = proc.communicate("go\n", timeout=120)
+        assert proc.returncode == 0 and out.strip().endswith("intact"), out
+    finally:
+        if proc.poll() is None:
+            proc.kill()
+
+
+def test_full_span_memtests_the_burnin_arena_too(probe):
+    """A full burn-in's bandwidth step grows the agent's arena to 2 x 16 GiB; the span
+    memtest frees it first, so that HBM is tested rather than left beside the span."""
+    probe.set_scratch_cache(True)
+    try:
+        probe.prealloc_scratch(0, "full")
+        probe.wait_frees()
+        held_free = probe.free_bytes(0)
+        res = probe.memtest_span(0, 0, headroom=4 << 30, passes=1)
+        assert res["errors"] == 0
+        assert res["bytes"] > held_free  # the 32 GiB the arena held were part of the span
+        assert probe.release_scratch() == 0  # nothing was left cached
+    finally:
+        probe.release_scratch()
+        probe.set_scratch_cache(False)
+        probe.wait_frees()

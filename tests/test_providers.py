@@ -122,7 +122,7 @@ def test_mi355x_node_and_addons():
                                      hosts=["a", "b"], rccl_env={"NCCL_SOCKET_IFNAME": "eth0"})), "m", key, None, st)
     n = st.module("node_baremetal_dev_dev-w-1")
     assert n["source"].startswith("tk::terraform/modules/bare-metal-mi355x-rancher-k8s-host?ref=")
-    assert n["gpu_count"] == "8" and n["gpu_burnin"] == "quick" and n["gpu_product"] == "MI355X"
+    assert n["gpu_count"] == "8" and n["gpu_burnin"] == "full" and n["gpu_product"] == "MI355X"
     assert n["rccl_env"]["NCCL_SOCKET_IFNAME"] == "eth0" and n["rccl_env"]["HSA_FORCE_FINE_GRAIN_PCIE"] == "1"
     assert_blocks_match_modules(st)
     baremetal.new_node(make_ctx(dict(NODE_BASE, node_count=1, ssh_user="u", bastion_host="", key_path="k",

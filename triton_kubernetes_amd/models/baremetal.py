@@ -32,6 +32,7 @@ ADDONS_MODULE = "terraform/modules/rancher-k8s-mi355x-addons"
 
 GPU_TYPES = ["none", "mi355x"]
 BURNIN_LEVELS = ["quick", "full", "off"]
+DEFAULT_BURNIN = "full"
 
 
 def addons_key(cluster_name: str) -> str:
@@ -144,7 +145,9 @@ def _mi355x_fields(ctx: Context) -> Dict:
             raise ValueError
     except ValueError as exc:
         raise ConfigError(f"gpu_count must be greater than 0. Found '{count}'.") from exc
-    burnin = s.get_string("gpu_burnin").lower() if s.is_set("gpu_burnin") else "quick"
+    # full by default: a node entering a training fleet gets every free byte of its HBM
+    # memtested (~4-6 s per GPU, all GPUs at once), not the 1 GiB token check of quick
+    burnin = s.get_string("gpu_burnin").lower() if s.is_set("gpu_burnin") else DEFAULT_BURNIN
     if burnin not in BURNIN_LEVELS:
         raise ConfigError(f"Invalid gpu_burnin '{burnin}', must be one of the following: quick, full, off")
     env = default_rccl_env()

@@ -361,7 +361,7 @@ class NodeAgent:
                             "".join(f"{k}={v}\n" for k, v in sorted(labels.items())))
             return labels
         if a == "gpu_burnin":
-            level = step.params.get("level", "quick")
+            level = step.params.get("level", "full")
             parts = (step.params.get("compute_partition", "spx"), step.params.get("memory_partition", "nps1"))
             self._quiesce_gpus()
             # every (logical) GPU of the node burns in concurrently (one host thread each;

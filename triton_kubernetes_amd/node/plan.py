@@ -204,7 +204,7 @@ fi""", {"install_url": install_url}))
         physical = int(cfg.get("gpu_count", 8) or 8)
         cpart, mpart = modes_of(cfg)
         ngpu = physical * partitions_per_gpu(cpart)  # logical GPUs: amd.com/gpu units, RCCL ranks
-        burnin = cfg.get("gpu_burnin", "quick")
+        burnin = cfg.get("gpu_burnin", "full")
         env = dict(cfg.get("rccl_env") or {})
         from .hosttune import policy_of as tuning_policy
         from .hosttune import shell_check as host_tuning_check

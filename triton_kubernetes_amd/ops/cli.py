@@ -27,7 +27,7 @@ def main(argv: Sequence[str] = ()) -> int:
     b = sub.add_parser("burnin")
     b.add_argument("--device", type=int, default=0)
     b.add_argument("--all", action="store_true")
-    b.add_argument("--level", default="quick", choices=["quick", "full", "off"])
+    b.add_argument("--level", default="full", choices=["quick", "full", "off"])
     sub.add_parser("topology")
     sub.add_parser("labels")
     hl = sub.add_parser("health", help="GPU RAS health: uncorrectable ECC errors, retired VRAM pages (node/health.py)")

@@ -339,6 +339,26 @@ extern "C" long long tkp_release_scratch() {
   return freed;
 }
 
+// Frees `dev`'s cached buffers not in use (the span memtest calls it first: HBM the arena
+// holds would otherwise be left out of the test -- 32 GiB of stream buffers after a full
+// burn-in's bandwidth step).  Returns the bytes released.
+extern "C" long long tkp_release_scratch_dev(int dev) {
+  std::lock_guard<std::mutex> lk(g_scr_mu);
+  long long freed = 0;
+  auto it = g_scr.find(dev);
+  if (it == g_scr.end()) return 0;
+  (void)hipSetDevice(dev);
+  for (auto& s : it->second) {
+    if (s.p && !s.in_use) {
+      TRACED(hipFree(s.p));
+      freed += (long long)s.bytes;
+      s.p = nullptr;
+      s.bytes = 0;
+    }
+  }
+  return freed;
+}
+
 // out[0] = read GB/s, out[1] = write GB/s, out[2] = copy GB/s (bytes read + written).
 // Best of `iters` timed launches after one warm-up of each kernel.
 extern "C" int tkp_hbm_bandwidth(int dev, size_t bytes, int iters, int blocks_per_cu, double* out) {
@@ -763,11 +783,18 @@ extern "C" int tkp_wait_frees() {
 
 // Test hook: the named step of tkp_memtest_span fails as if its HIP call had (tests check
 // that every allocation, the stream and the events are released on such a path).
+// "memtest_span.alloc_limit=N": the span's chunk allocations after the first N fail, as when
+// another process takes HBM between hipMemGetInfo and the allocations.
 static char g_fail_point[64] = "";
 extern "C" void tkp_set_fail_point(const char* name) {
   snprintf(g_fail_point, sizeof(g_fail_point), "%s", name ? name : "");
 }
 static bool fail_point(const char* name) { return g_fail_point[0] && !strcmp(g_fail_point, name); }
+static long fail_point_value(const char* prefix) {  // N of "<prefix>=N"; -1 when not set
+  const size_t n = strlen(prefix);
+  if (strncmp(g_fail_point, prefix, n) != 0 || g_fail_point[n] != '=') return -1;
+  return strtol(g_fail_point + n + 1, nullptr, 10);
+}
 #define FAILPOINT(name)                                                  \
   do {                                                                   \
     if (fail_point(name)) {                                              \
@@ -801,6 +828,8 @@ struct SpanHold {
 extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t headroom, int passes, double* out) {
   tkp_wait_frees();
   CHECK(hipSetDevice(dev));
+  tkp_release_scratch_dev(dev);  // the arena's buffers are part of the span, not beside it
+  const long alloc_limit = fail_point_value("memtest_span.alloc_limit");
   size_t free_b = 0, total_b = 0;
   CHECK(hipMemGetInfo(&free_b, &total_b));
   for (int i = 0; i < 7; ++i) out[i] = 0.0;
@@ -815,9 +844,9 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
     const size_t want = (bytes - done < chunk ? bytes - done : chunk) / sizeof(uint4) * sizeof(uint4);
     if (want == 0) break;
     uint4* p = nullptr;
-    if (hipMalloc(&p, want) != hipSuccess) {
+    if ((alloc_limit >= 0 && (long)hold.chunks.size() >= alloc_limit) || hipMalloc(&p, want) != hipSuccess) {
       (void)hipGetLastError();
-      break;  // fragmentation: test what could be held
+      break;  // fragmentation, or HBM another process took since hipMemGetInfo: test what could be held
     }
     hold.chunks.push_back(p);
     sizes.push_back(want);
@@ -1104,7 +1133,7 @@ extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, 
 
 #ifdef TK_PROBE_MAIN
 // gpu-burnin: the on-node executable the SSH bootstrap runs (no Python needed).
-//   gpu-burnin [--all | --device N] [--level quick|full]
+//   gpu-burnin [--all | --device N] [--level quick|full]   (default full)
 //              [--min-read-gbps X] [--min-bf16-tflops Y] [--min-fp8-tflops Z] [--min-gemm-tflops G]
 //              [--min-gemm-fp8-tflops F]
 // Prints one JSON document; exit 1 when any GPU misses a threshold, the memtest finds a
@@ -1185,7 +1214,7 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
 
 int main(int argc, char** argv) {
   int dev = 0, all = 0;
-  const char* level = "quick";
+  const char* level = "full";  // = models/baremetal.py DEFAULT_BURNIN
   const char* labels_path = nullptr;  // --labels FILE: node labels recording what was tested
   int p2p = 0;                        // --p2p: per-link peer copy matrix instead of the burn-in
   double min_link_frac = 0.5;

@@ -73,6 +73,8 @@ def _lib():
     lib.tkp_set_scratch_cache.argtypes = [ctypes.c_int]
     lib.tkp_prealloc_scratch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t]
     lib.tkp_release_scratch.restype = ctypes.c_longlong
+    lib.tkp_release_scratch_dev.argtypes = [ctypes.c_int]
+    lib.tkp_release_scratch_dev.restype = ctypes.c_longlong
     return lib
 
 
@@ -243,8 +245,10 @@ def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3,
 REMEASURE = 2  # extra runs of a throughput gate that read below its floor
 LEVELS = {
     # level: (hbm bytes, hbm iters, mfma iters (x 8 accumulator chains per wave), memtest bytes, memtest passes)
-    # memtest bytes 0 = every free byte of HBM but 4 GiB (memtest_span); quick tests 1 GiB
-    # (0.35 % of 288 GiB) -- the node labels say which (node/labels.py:burnin_labels)
+    # memtest bytes 0 = every free byte of HBM but 4 GiB (memtest_span), sized from
+    # hipMemGetInfo when it runs; quick tests 1 GiB (0.35 % of 288 GiB).  full is the
+    # default of a node joining a cluster (models/baremetal.py); the node labels say which
+    # (node/labels.py:burnin_labels)
     "quick": (1 << 30, 3, 2000, 1 << 30, 1),
     "full": (16 << 30, 10, 20000, 0, 3),
 }
@@ -372,6 +376,8 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
             res.memtest.update(bytes=mt_bytes, hbm_bytes=int(info.total_mem_gib * (1 << 30)))
         elif th.mem_share < 1.0:
             # concurrent partitions share one pool: each holds its share of what is free
+            # (the arena's buffers are freed first: they are memtested, not left beside it)
+            release_scratch(dev)
             headroom = max(512 << 20, int((4 << 30) * th.mem_share))
             span_bytes = max(1 << 30, int(free_bytes(dev) * th.mem_share) - headroom)
             res.memtest = memtest_span(dev, span_bytes, passes=mt_passes)
@@ -405,6 +411,8 @@ def set_scratch_cache(on: bool) -> None:
     _lib().tkp_set_scratch_cache(1 if on else 0)
 
 
-def release_scratch() -> int:
-    """Free cached burn-in buffers; returns the bytes released."""
+def release_scratch(dev: Optional[int] = None) -> int:
+    """Free cached burn-in buffers (of ``dev`` only, when given); returns the bytes released."""
+    if dev is not None:
+        return int(_lib().tkp_release_scratch_dev(dev))
     return int(_lib().tkp_release_scratch())

@@ -1245,7 +1245,7 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa"),
         Var("tk_operation", "apply"),
         Var("gpu_product", "MI355X"), Var("gpu_count", 8, "GPUs the node must expose"),
-        Var("gpu_burnin", "quick", "quick | full | off"),
+        Var("gpu_burnin", "full", "quick | full | off"),
         Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
         Var("rccl_min_busbw", "0", "node-level all-reduce bus bandwidth gate (GB/s)"),
         Var("gpu_link_min_frac", "0.5",

@@ -126,7 +126,7 @@ variable "gpu_count" {
 variable "gpu_burnin" {
   description = "quick | full | off"
   type        = string
-  default     = "quick"
+  default     = "full"
 
   validation {
     condition     = contains(["quick", "full", "off"], var.gpu_burnin)
