@@ -9,9 +9,10 @@
 //    ncclCommInitAll + grouped calls (the node-level gate on an 8xMI355X node,
 //    where all traffic is point-to-point xGMI).
 //
-// For each message size: ncclAllReduce(sum) of a buffer holding (rank + 1) on
-// every rank, verified on device against world*(world+1)/2 (exact in f32 and
-// in bf16 for world <= 15), timed with HIP events over `iters` launches after
+// For each message size: ncclAllReduce(sum) of a buffer holding a per-rank value,
+// verified on device against the exact sum (tk_rccl_verify.h: rank + 1
+// in f32, and in bf16 up to 15 ranks; 1 per rank in bf16 beyond, exact up to 256
+// ranks, and bf16 refused above that), timed with HIP events over `iters` launches after
 // `warmup`.  Reported as algbw = bytes / t and busbw = algbw * 2(n-1)/n (the
 // ring all-reduce bus bandwidth, comparable with the per-link xGMI rate).
 //
@@ -21,6 +22,8 @@
 
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+
+#include "tk_rccl_verify.h"
 
 #include <climits>
 #include <string>
@@ -123,6 +126,16 @@ static void free_bufs(RankBufs& b) {
   b = RankBufs{};
 }
 
+static int check_verifiable(int dtype, int world) {
+  if (!tk_verifiable(dtype, world)) {
+    snprintf(g_err, sizeof(g_err),
+             "bf16 all-reduce sums of %d ranks are not exact in bf16 (8 significant bits, at most %d ranks); "
+             "gate in f32",
+             world, kBf16MaxWorld);
+    return -1;
+  }
+  return 0;
+}
 static int fill(RankBufs& b, size_t count, int dtype, float v) {
   if (dtype == 1) k_fill_bf16<<<512, 256, 0, b.stream>>>((__bf16*)b.send, count, v);
   else k_fill_f32<<<512, 256, 0, b.stream>>>((float*)b.send, count, v);
@@ -520,7 +533,8 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
   }
   phase_ms[1] = ms_since(t_phase);
   t_phase = std::chrono::steady_clock::now();
-  const float want = (float)g->world * (float)(g->world + 1) / 2.0f;
+  if (rc == 0) rc = check_verifiable(dtype, g->world);
+  const float want = tk_verify_sum(dtype, g->world);
   auto run = [&](size_t count, int n) -> int {
     for (int it = 0; it < n; ++it) {
       ncclResult_t r = ncclGroupStart();
@@ -540,7 +554,7 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
     const size_t count = sizes[s] / elem_size(dtype);
     for (int d = 0; d < ndev && rc == 0; ++d) {
       (void)hipSetDevice(g->devices[d]);
-      rc = fill(bufs[d], count, dtype, (float)(g->rank_base + d + 1));
+      rc = fill(bufs[d], count, dtype, tk_verify_value(dtype, g->world, g->rank_base + d));
     }
     if (rc || (rc = run(count, warmup)) != 0) break;
     for (int d = 0; d < ndev; ++d) { (void)hipSetDevice(g->devices[d]); (void)hipEventRecord(bufs[d].t0, bufs[d].stream); }
@@ -617,12 +631,12 @@ extern "C" int tkr_sweep_local(int ndev, const size_t* sizes, int nsizes, int it
     if (hipSetDevice(d) != hipSuccess) { rc = -1; break; }
     rc = alloc_bufs(bufs[d], max_bytes);
   }
-  const float want = (float)ndev * (float)(ndev + 1) / 2.0f;
+  const float want = tk_verify_sum(dtype, ndev);
   for (int s = 0; rc == 0 && s < nsizes; ++s) {
     const size_t count = sizes[s] / elem_size(dtype);
     for (int d = 0; d < ndev && rc == 0; ++d) {
       (void)hipSetDevice(d);
-      rc = fill(bufs[d], count, dtype, (float)(d + 1));
+      rc = fill(bufs[d], count, dtype, tk_verify_value(dtype, ndev, d));
     }
     if (rc) break;
     auto run = [&](int n) -> int {
@@ -797,6 +811,10 @@ int main(int argc, char** argv) {
   if (cluster) {
     if (world < ndev || rank_base < 0 || rank_base + ndev > world || (!uid_out && !uid_hex) || max_mib < 1) {
       fprintf(stderr, "{\"error\":\"cluster mode needs --world >= --rank-base + --ngpus and --uid or --uid-out\"}\n");
+      return 2;
+    }
+    if (check_verifiable(dtype, world)) {  // refused before any communicator exists
+      fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
       return 2;
     }
     return cluster_main(world, rank_base, ndev, uid_hex, uid_out, max_mib, iters, dtype, min_busbw, timeout_s);

@@ -91,6 +91,19 @@ class SweepResult:
         return d
 
 
+# = ops/csrc/tk_rccl_verify.h: bf16 sums are verified exactly up to this many ranks
+BF16_MAX_WORLD = 256
+
+
+def check_dtype(dtype: str, world: int) -> None:
+    """Refuse a gate whose result cannot be verified exactly (``tk_rccl_verify.h``)."""
+    if dtype not in ("f32", "bf16"):
+        raise ValueError(f"dtype must be f32 or bf16, not {dtype!r}")
+    if dtype == "bf16" and world > BF16_MAX_WORLD:
+        raise ValueError(f"a bf16 all-reduce over {world} ranks cannot be verified exactly (bf16 has 8 significant "
+                         f"bits: at most {BF16_MAX_WORLD} ranks); gate in f32")
+
+
 def _arrays(n: int):
     return [(ctypes.c_double * n)() for _ in range(4)]
 
@@ -99,6 +112,7 @@ def sweep_rank(rank: int, world: int, uid: bytes, device: int, sizes: Sequence[i
                iters: int = 10, warmup: int = 3, dtype: str = "f32", async_teardown: bool = False) -> SweepResult:
     """One rank of a multi-process sweep.  ``async_teardown`` moves the
     communicator destroy (~0.5 s) off this call; :func:`drain` joins it."""
+    check_dtype(dtype, world)
     n = len(sizes)
     sz = (ctypes.c_size_t * n)(*sizes)
     t, alg, bus, err = _arrays(n)
@@ -146,6 +160,11 @@ class GateComm:
               timeout_s: float = 600.0, async_teardown: bool = True) -> SweepResult:
         if self.handle is None:
             raise RCCLError("gate already consumed")
+        try:
+            check_dtype(dtype, self.world)
+        except ValueError:
+            self.abort()  # every rank refuses alike: release the communicator, do not leak it
+            raise
         n = len(sizes)
         sz = (ctypes.c_size_t * n)(*sizes)
         t, alg, bus, err = _arrays(n)
