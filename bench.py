@@ -84,7 +84,9 @@ def parse_args():
                          "uncorrectable ECC errors does not abort the run; the node joins tainted and the line "
                          "lists it under gpu_unhealthy_nodes (its GPUs then sit out the GPU and RCCL checks)")
     ap.add_argument("--sim-gpu", action="store_true",
-                    help="CPU dry run: synthetic topology, no burn-in kernels, no RCCL (never a valid measurement)")
+                    help="CPU dry run: synthetic topology, no burn-in kernels; the cluster RCCL gate runs over the "
+                         "libtk_rccl ABI stub (ops/csrc/tk_rccl_stub.cpp: every rank of the world joins and sweeps, "
+                         "no GPU); never a valid measurement")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
     return ap.parse_args()
 
@@ -205,8 +207,20 @@ def main() -> int:
         # control-plane sync only (CPU); the GPU collectives are the agents' native RCCL gate
         dist.init_process_group("gloo", init_method="env://")
     if args.sim_gpu:
-        args.no_rccl_gate = True
         visible = n_gpus
+        if not args.no_rccl_gate:
+            # the gate over the C ABI stub: the agents (this process's and their children)
+            # join one rendezvous directory, shared by every rank
+            from triton_kubernetes_amd.ops import native
+            from triton_kubernetes_amd.ops.build import build as build_native
+
+            if rank == 0:
+                build_native(only=["libtk_rccl_stub.so"])
+            where = [tempfile.mkdtemp(prefix="tk-bench-rccl-stub-") if rank == 0 else None]
+            if distributed:
+                dist.broadcast_object_list(where, src=0)
+            os.environ.update(TK_RCCL_LIB=os.path.join(native.LIB_DIR, "libtk_rccl_stub.so"),
+                              TK_RCCL_STUB_DIR=where[0], TK_GATE_BACKEND="rccl")
     else:
         visible = torch.cuda.device_count()
         torch.cuda.set_device(local_rank if visible > local_rank else 0)
@@ -333,6 +347,7 @@ def main() -> int:
             out["phase_s"] = rep.to_json()["phase_seconds"]
             out["gpu_unhealthy"] = list(rep.gpu_unhealthy)
             ranks = (rep.rccl or {}).get("ranks") or []
+            out["rccl_gate_ranks"] = sum(len(r.get("ranks") or []) for r in ranks)
             phases = [r.get("phase_ms") or {} for r in ranks]
             if phases:  # the gate's communicator phases, max over agents
                 out["rccl"] = {k: round(max(float(p.get(k, 0.0)) for p in phases), 3)
@@ -436,7 +451,8 @@ def main() -> int:
             "higher_is_better": False,
             "scaling": "weak",
             "vs_baseline": None,
-            "dtype": "bf16",
+            # a provisioning wall-clock: no tensor dtype, batch or sequence applies
+            "dtype": "n/a",
             "data": sim + ("synthetic cold create: fresh node-agent processes per step; simulated phases "
                            "rke_provisioning (in-process Rancher v2.10 fake, RKE2 custom cluster, instantaneous "
                            "provisioning), runtime_install (firewall/hostname no-ops) and agent_container (the node "
@@ -446,13 +462,15 @@ def main() -> int:
                            "real on MI355X: "
                            f"native topology + RDMA labels, per-GPU HBM/MFMA/memtest burn-in level={args.burnin}, "
                            f"cluster RCCL all-reduce gate {'off' if args.no_rccl_gate else 'on'} "
-                           f"(one communicator over all {n_gpus} GPUs)"
+                           f"(one communicator over all {n_gpus} GPUs"
+                           + (", over the libtk_rccl ABI stub" if args.sim_gpu and not args.no_rccl_gate else "")
+                           + ")"
                            + ("; opt-in node install before the timed region: verified single-target gfx950 "
                               "RCCL copy (ops/rccl_slim.py)" if slim_meta else "")),
             "config": {
                 "model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology labels",
                 "workers": workers, "gpus_per_worker": gpus_per_worker, "visible_gpus": visible,
-                "control_plane_nodes": 2, "global_batch": n_gpus, "seq_len": 0,
+                "control_plane_nodes": 2, "global_batch": "n/a", "seq_len": "n/a",
                 "parallelism": f"{workers} worker node(s) x {gpus_per_worker} GPU(s)",
                 "executor": "direct", "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate,
                 "gpu_health": args.gpu_health,
@@ -474,6 +492,8 @@ def main() -> int:
             "warm_create_to_ready_s": round(sum(warm) / len(warm), 4) if warm else None,
             # GPU nodes that joined with the health taint in any timed step (normally none)
             "gpu_unhealthy_nodes": sorted({h for r in results for h in r.get("gpu_unhealthy", [])}),
+            # ranks of the cluster RCCL gate per timed step (every GPU of the worker tier)
+            "rccl_gate_ranks": [r.get("rccl_gate_ranks", 0) for r in results],
             "phase_ms_per_step": phase_ms,
         }
         print(json.dumps(line), flush=True)

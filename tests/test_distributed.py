@@ -1,8 +1,10 @@
 """Multi-process paths on CPU: the bench harness under torchrun with the gloo control group.
 
-``--sim-gpu`` swaps the GPU steps for synthetic topology / no-op burn-in, so this
-checks the distributed plumbing (agent URL all-gather, barriers, max-over-ranks
-timing, rank-0 JSON line) — never a measurement.
+``--sim-gpu`` swaps the GPU steps for synthetic topology / no-op burn-in and runs the
+cluster RCCL gate over the libtk_rccl ABI stub (``ops/csrc/tk_rccl_stub.cpp``), so this
+checks the distributed plumbing (agent URL all-gather, barriers, max-over-ranks timing,
+rank-0 JSON line) and the gate's rank layout at the driver's 8-GPU shape — never a
+measurement.
 """
 
 import json
@@ -54,6 +56,9 @@ def test_bench_torchrun_gloo(nproc, workers):
     assert len(doc["create_to_ready_s"]) == 2 and doc["warm_create_to_ready_s"] > 0
     assert doc["phase_ms_per_step"]["module.host"] > 0
     assert doc["phase_ms_per_step"]["bench.agents_start"] > 0
+    # the gate ran over the libtk_rccl ABI stub: every GPU of the worker tier is a rank
+    assert doc["rccl_gate_ranks"] == [nproc, nproc] and "ABI stub" in doc["data"]
+    assert doc["dtype"] == cfg["global_batch"] == cfg["seq_len"] == "n/a"
 
 
 def test_bench_single_process_default():
@@ -86,3 +91,22 @@ def test_bench_masked_launcher_one_agent_per_rank():
     assert proc.returncode == 0, proc.stderr[-3000:]
     doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][0])
     assert doc["config"]["workers"] == 2 and doc["config"]["gpus_per_worker"] == 1
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("masked", [False, True])
+def test_bench_eight_ranks_gate_over_eight_gpus(masked):
+    """The driver's N=8 SCALE shape on the CPU.  Unmasked: rank 0's one agent drives all 8
+    ranks of the gate (ndev=8 grouped init); masked: 8 agents in 8 processes, one rank each,
+    meet in the stub's cross-process rendezvous."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=8",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "8", "--steps", "1", "--warmup", "0", "--warm-steps", "0", "--sim-gpu"]
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    if masked:
+        env["TK_BENCH_ASSUME_MASKED"] = "1"
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][0])
+    assert doc["n_gpus"] == 8 and doc["rccl_gate_ranks"] == [8]
+    assert doc["config"]["workers"] == (8 if masked else 1)

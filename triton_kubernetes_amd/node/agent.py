@@ -133,6 +133,9 @@ class _SimGate:
     def abort(self) -> None:
         pass
 
+    def cancel(self) -> None:
+        pass
+
 
 @dataclass
 class NodeAgent:
@@ -146,6 +149,10 @@ class NodeAgent:
     # the Rancher agent images / servers this node may run (default: the pinned agent
     # image; Rancher servers on loopback only)
     policy: Optional[AgentPolicy] = None
+    # cluster RCCL gate: "auto" = RCCL on real GPUs, a simulated gate on synthetic ones;
+    # "rccl" = the RCCL ABI even on synthetic GPUs (a dry run with TK_RCCL_LIB naming the
+    # ABI stub, ops/csrc/tk_rccl_stub.cpp)
+    gate_backend: str = field(default_factory=lambda: os.environ.get("TK_GATE_BACKEND", "auto"))
 
     def __post_init__(self):
         if self.mode not in MODES:
@@ -166,6 +173,8 @@ class NodeAgent:
         self._gates: Dict[bytes, Any] = {}
         # uid -> (SweepResult, finished): whole-node gates the rccl_local step already swept
         self._gate_results: Dict[bytes, Any] = {}
+        # uid -> gate whose sweep is running (waiting for peers): /v1/rccl-abort cancels it
+        self._sweeping: Dict[bytes, Any] = {}
         # one RCCL unique id kept ready (new_uid): the gate's first request gets it without
         # an ncclGetUniqueId on the bring-up path; the pool makes the next one afterwards
         self._spare_uid: Optional[bytes] = None
@@ -595,8 +604,13 @@ class NodeAgent:
         for g in gates:
             g.abort()
 
+    @property
+    def _sim_gate(self) -> bool:
+        """Synthetic GPUs without the RCCL ABI: the gate is simulated (no library call)."""
+        return self.topology_override is not None and self.gate_backend != "rccl"
+
     def _make_uid(self) -> bytes:
-        if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
+        if self._sim_gate:  # synthetic GPUs (tests / dry runs)
             return secrets.token_bytes(128)
         from ..ops import rccl
 
@@ -635,7 +649,7 @@ class NodeAgent:
         if uid is None:
             uid = self.new_uid()
         with span("node.rccl_prepare", node=self.name, rank_base=rank_base, world=world):
-            if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
+            if self._sim_gate:  # synthetic GPUs (tests / dry runs)
                 gate: Any = _SimGate(devs)
             else:
                 from ..ops import rccl
@@ -652,12 +666,18 @@ class NodeAgent:
                 "uid": base64.b64encode(uid).decode()}
 
     def rccl_abort(self, uid: bytes) -> Dict[str, Any]:
+        """Release this node's ranks of gate ``uid``: a pending communicator is aborted, and a
+        sweep waiting for peers is canceled (it fails at once instead of at its timeout:
+        another member of the gate failed)."""
         with self._gate_mu:
             entry = self._gates.pop(uid, None)
             done = self._gate_results.pop(uid, None)
+            running = self._sweeping.get(uid)
         if entry is not None:
             entry[0].abort()
-        return {"ok": True, "aborted": entry is not None or done is not None}
+        if running is not None:
+            running.cancel()
+        return {"ok": True, "aborted": entry is not None or done is not None, "canceled": running is not None}
 
     def _take_node_gate(self) -> Optional[Tuple[bytes, Any, Dict[str, Any]]]:
         """A pending gate communicator that spans exactly this node's GPUs (a one-node
@@ -676,7 +696,7 @@ class NodeAgent:
         return None
 
     def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10,
-                  ndev: int = 1) -> Dict[str, Any]:
+                  ndev: int = 1, timeout_s: float = 600.0) -> Dict[str, Any]:
         """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
         communicator from rccl_prepare when there is one, else a fresh init."""
         with self._gate_mu:
@@ -704,16 +724,22 @@ class NodeAgent:
         with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=pipelined):
             if entry is not None:
                 gate = entry[0]
-            elif self.topology_override is not None:
+            elif self._sim_gate:
                 gate = _SimGate(self._gate_devices(ndev))
             else:
                 from ..ops import rccl
 
                 self._used_rccl = True
                 gate = rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
-            # the communicator teardown is not part of the readiness answer: it is
-            # joined in stop() (or by the next process-exit drain), not here
-            res = gate.sweep(sizes, iters=iters, warmup=2, async_teardown=True)
+            with self._gate_mu:
+                self._sweeping[uid] = gate
+            try:
+                # the communicator teardown is not part of the readiness answer: it is
+                # joined in stop() (or by the next process-exit drain), not here
+                res = gate.sweep(sizes, iters=iters, warmup=2, async_teardown=True, timeout_s=timeout_s)
+            finally:
+                with self._gate_mu:
+                    self._sweeping.pop(uid, None)
         out = res.to_json()
         out["pipelined"] = pipelined
         out["ranks"] = list(range(rank, rank + len(gate.devices)))
@@ -902,7 +928,8 @@ class NodeAgent:
                         return self._reply(200, agent.rccl_gate(int(body["rank"]), int(body["world"]), uid,
                                                                 [int(s) for s in body.get("sizes", [1 << 20])],
                                                                 int(body.get("iters", 10)),
-                                                                int(body.get("ndev", 1))))
+                                                                int(body.get("ndev", 1)),
+                                                                float(body.get("timeout_s", 600.0))))
                     if path == "/v1/rccl-abort":
                         return self._reply(200, agent.rccl_abort(base64.b64decode(body["uid"])))
                     if path == "/v1/cleanup":

@@ -9,6 +9,7 @@ artifact                       source                                      toolc
 ``libtk_gemm.so``              ``csrc/tk_gemm_screen.hip`` (ABFT GEMM screen)  hipcc
 ``libtk_rccl.so``              ``csrc/tk_rccl_probe.hip`` (N2, RCCL)          hipcc
 ``rccl-ready``                 same, ``-DTK_RCCL_MAIN``                     hipcc
+``libtk_rccl_stub.so``         ``csrc/tk_rccl_stub.cpp`` (the ABI, no GPU)    g++
 ``libtk_topo.so``              ``csrc/tk_topo.cpp`` (N1, sysfs collector)    g++
 ``amdgpu-topo-labeller``       same + amd_smi, ``-DTK_TOPO_MAIN``           g++
 =============================  ==========================================  =========
@@ -66,6 +67,8 @@ def targets() -> List[Target]:
     rccl = os.path.join(CSRC, "tk_rccl_probe.hip")
     gemm = os.path.join(CSRC, "tk_gemm_screen.hip")
     topo = os.path.join(CSRC, "tk_topo.cpp")
+    stub = os.path.join(CSRC, "tk_rccl_stub.cpp")
+    rccl_h = [os.path.join(CSRC, "tk_rccl_group.h"), os.path.join(CSRC, "tk_rccl_verify.h")]
     out = lambda n: os.path.join(LIB, n)  # noqa: E731
     return [
         Target("libtk_gpu_probe.so", [probe],
@@ -74,14 +77,18 @@ def targets() -> List[Target]:
                [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-DTK_PROBE_MAIN", probe, gemm, "-o", out("gpu-burnin"), *RPATH]),
         Target("libtk_gemm.so", [gemm],
                [hipcc, *HIP_FLAGS, "-fPIC", "-shared", gemm, "-o", out("libtk_gemm.so"), *RPATH]),
-        Target("libtk_rccl.so", [rccl],
+        Target("libtk_rccl.so", [rccl, *rccl_h],
                [hipcc, *HIP_FLAGS, "-fPIC", "-shared", rccl, "-o", out("libtk_rccl.so"), f"-L{ROCM}/lib",
                 "-lrccl", *RPATH]),
         # /opt/rocm's RCCL (RUNPATH).  The opt-in single-target copy (rccl_slim) is reached
         # only through the rccl-ready-slim wrapper, which checks it is verified and current
-        Target("rccl-ready", [rccl],
+        Target("rccl-ready", [rccl, *rccl_h],
                [hipcc, *HIP_FLAGS, "-DTK_RCCL_MAIN", rccl, "-o", out("rccl-ready"), f"-L{ROCM}/lib", "-lrccl",
                 *RPATH]),
+        # the libtk_rccl C ABI without GPUs or RCCL: dry runs of the cluster gate (TK_RCCL_LIB)
+        Target("libtk_rccl_stub.so", [stub, *rccl_h],
+               ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", f"-I{CSRC}", stub, "-o", out("libtk_rccl_stub.so"),
+                "-lpthread"]),
         # in-process library: sysfs collector only, no libamd_smi (see csrc/tk_topo.cpp)
         Target("libtk_topo.so", [topo],
                ["g++", "-O2", "-std=c++17", "-fPIC", "-shared", topo, "-o", out("libtk_topo.so")]),

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "tk_rccl_group.h"
 #include "tk_rccl_verify.h"
 
 #include <climits>
@@ -315,6 +316,7 @@ struct Gate {
   std::condition_variable cv;
   int init_state = 0;  // 0 running, 1 ready, -2 failed
   bool abandoned = false;
+  bool cancel = false;  // tkr_gate_cancel: stop waiting for peers that will not come
   char err[512] = {0};
   std::thread init_thread;
   size_t prealloc_bytes = 0;     // sweep buffers allocated by the init thread after the comms
@@ -322,6 +324,8 @@ struct Gate {
 };
 static std::mutex g_gate_mu;
 static std::vector<std::pair<int, Gate*>> g_gates;
+// gates a tkr_gate_sweep is waiting on (taken out of g_gates): reachable by tkr_gate_cancel
+static std::vector<std::pair<int, Gate*>> g_sweeping;
 static int g_next_gate = 1;
 // inits released while still waiting for peers (their threads are detached)
 static std::atomic<int> g_abandoned{0};
@@ -355,20 +359,24 @@ static void destroy_comms(Gate* g, bool abort) {
   }
 }
 
+// RCCL and HIP behind tk_rccl_group.h's Api (the grouped-init sequence lives there, where a
+// CPU test checks it against a mock that enforces RCCL's contract).
+struct HipNcclApi {
+  using Comm = ncclComm_t;
+  static constexpr int kInvalidArgument = (int)ncclInvalidArgument;
+  ncclUniqueId id;
+  int group_start() { return (int)ncclGroupStart(); }
+  int group_end() { return (int)ncclGroupEnd(); }
+  int set_device(int dev) { return hipSetDevice(dev) == hipSuccess ? 0 : 1; }
+  int init_rank(Comm* c, int world, int rank) { return (int)ncclCommInitRank(c, world, id, rank); }
+  const char* error_string(int r) { return ncclGetErrorString((ncclResult_t)r); }
+};
+
 static void init_body(Gate* g, ncclUniqueId id) {
-  ncclResult_t r = ncclGroupStart();
-  for (size_t d = 0; d < g->devices.size() && r == ncclSuccess; ++d) {
-    if (hipSetDevice(g->devices[d]) != hipSuccess) {
-      snprintf(g->err, sizeof(g->err), "hipSetDevice(%d) failed", g->devices[d]);
-      r = ncclInvalidArgument;
-      break;
-    }
-    r = ncclCommInitRank(&g->comms[d], g->world, id, g->rank_base + (int)d);
-  }
-  ncclResult_t re = ncclGroupEnd();
-  if (r == ncclSuccess) r = re;
-  if (r != ncclSuccess && !g->err[0]) snprintf(g->err, sizeof(g->err), "ncclCommInitRank: %s", ncclGetErrorString(r));
-  if (r == ncclSuccess && g->prealloc_bytes) {
+  HipNcclApi api{id};
+  const int r = tk_group_init(api, g->world, g->rank_base, (int)g->devices.size(), g->devices.data(),
+                              g->comms.data(), g->err, sizeof(g->err));
+  if (r == 0 && g->prealloc_bytes) {
     // the sweep's buffers too, so the gate request only runs collectives
     g->bufs.resize(g->devices.size());
     for (size_t d = 0; d < g->devices.size(); ++d) {
@@ -384,7 +392,7 @@ static void init_body(Gate* g, ncclUniqueId id) {
   {
     std::lock_guard<std::mutex> lk(g->mu);
     g->init_ms = ms_since(g->t_begin);
-    g->init_state = r == ncclSuccess ? 1 : -2;
+    g->init_state = r == 0 ? 1 : -2;
     orphan = g->abandoned;
   }
   g->cv.notify_all();
@@ -396,11 +404,15 @@ static void init_body(Gate* g, ncclUniqueId id) {
   }
 }
 
-// 0 ready, -2 init failed, -3 timeout.
+// 0 ready, -2 init failed, -3 timeout, -4 canceled.
 static int gate_wait(Gate* g, double timeout_ms) {
   std::unique_lock<std::mutex> lk(g->mu);
   const bool done = g->cv.wait_for(lk, std::chrono::duration<double, std::milli>(timeout_ms),
-                                   [g] { return g->init_state != 0; });
+                                   [g] { return g->init_state != 0 || g->cancel; });
+  if (g->init_state == 0 && g->cancel) {
+    snprintf(g_err, sizeof(g_err), "gate canceled while its communicator waited for peers");
+    return -4;
+  }
   if (!done) {
     snprintf(g_err, sizeof(g_err), "communicator not ready after %.0f ms", timeout_ms);
     return -3;
@@ -434,10 +446,7 @@ static void release_gate(Gate* g, bool abort) {
 // thread also allocates the sweep buffers (largest message size) once the comms are up.
 extern "C" int tkr_gate_begin_ex(const unsigned char* uid128, int world, int rank_base, int ndev,
                                  const int* devices, int blocking, size_t prealloc_bytes) {
-  if (ndev < 1 || world < ndev || rank_base < 0 || rank_base + ndev > world) {
-    snprintf(g_err, sizeof(g_err), "bad gate geometry: world=%d rank_base=%d ndev=%d", world, rank_base, ndev);
-    return -1;
-  }
+  if (tk_check_geometry(world, rank_base, ndev, devices, g_err, sizeof(g_err))) return -1;
   ncclUniqueId id;
   memcpy(id.internal, uid128, NCCL_UNIQUE_ID_BYTES);
   Gate* g = new Gate();
@@ -492,6 +501,26 @@ extern "C" int tkr_gate_abort(int h) {
   return pending;
 }
 
+// Stops a gate: a pending one is aborted (as tkr_gate_abort); one whose tkr_gate_sweep is
+// waiting for its communicator's peers makes that sweep return -4 at once (a cluster gate
+// whose other member failed must not wait out its timeout).  0 done, -1 unknown handle.
+extern "C" int tkr_gate_cancel(int h) {
+  {
+    std::lock_guard<std::mutex> lk(g_gate_mu);
+    for (auto& e : g_sweeping)
+      if (e.first == h) {
+        Gate* g = e.second;
+        {
+          std::lock_guard<std::mutex> glk(g->mu);
+          g->cancel = true;
+        }
+        g->cv.notify_all();
+        return 0;
+      }
+  }
+  return tkr_gate_abort(h) < 0 ? -1 : 0;
+}
+
 extern "C" int tkr_gate_pending() {
   std::lock_guard<std::mutex> lk(g_gate_mu);
   return (int)g_gates.size();
@@ -504,11 +533,29 @@ extern "C" int tkr_gate_pending() {
 extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters, int warmup, int dtype,
                               double timeout_ms, double* time_us, double* algbw, double* busbw, double* errors,
                               double* phase_ms) {
-  Gate* g = take_gate(h);
+  Gate* g = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_gate_mu);
+    for (size_t i = 0; i < g_gates.size(); ++i)
+      if (g_gates[i].first == h) {
+        g = g_gates[i].second;
+        g_gates.erase(g_gates.begin() + (long)i);
+        g_sweeping.emplace_back(h, g);  // cancelable while it waits for peers
+        break;
+      }
+  }
   if (!g) { snprintf(g_err, sizeof(g_err), "unknown gate %d", h); return -1; }
   const int ndev = (int)g->devices.size();
   auto t_phase = std::chrono::steady_clock::now();
   int rc = gate_wait(g, timeout_ms);
+  {
+    std::lock_guard<std::mutex> lk(g_gate_mu);
+    for (size_t i = 0; i < g_sweeping.size(); ++i)
+      if (g_sweeping[i].second == g) {
+        g_sweeping.erase(g_sweeping.begin() + (long)i);
+        break;
+      }
+  }
   phase_ms[0] = ms_since(t_phase);
   phase_ms[4] = g->init_ms;
   if (rc) {

@@ -106,6 +106,10 @@ def runtime_dir() -> str:
 
 
 def lib_path(name: str) -> str:
+    """The in-tree library ``name``; ``TK_RCCL_LIB`` names another ``libtk_rccl.so`` (the ABI
+    stub ``libtk_rccl_stub.so`` for a dry run of the cluster gate without GPUs)."""
+    if name == "libtk_rccl.so" and os.environ.get("TK_RCCL_LIB"):
+        return os.environ["TK_RCCL_LIB"]
     return os.path.join(LIB_DIR, name)
 
 
@@ -114,7 +118,7 @@ def load(name: str, autobuild: bool = True) -> ctypes.CDLL:
         if name in _cache:
             return _cache[name]
         path = lib_path(name)
-        if not os.path.exists(path) and autobuild:
+        if not os.path.exists(path) and autobuild and os.path.dirname(path) == LIB_DIR:
             from .build import build
 
             try:
@@ -125,7 +129,7 @@ def load(name: str, autobuild: bool = True) -> ctypes.CDLL:
             raise NativeUnavailable(f"native library {path} is missing; run `python -m "
                                     "triton_kubernetes_amd.ops.build`")
         global _hip_before_torch
-        if name in _HIP_LIBS and _hip_before_torch is None:
+        if name in _HIP_LIBS and _hip_before_torch is None and os.path.dirname(path) == LIB_DIR:
             import sys
 
             _hip_before_torch = "torch" not in sys.modules

@@ -3,7 +3,7 @@
 import atexit
 import ctypes
 from dataclasses import asdict, dataclass, field
-from typing import Dict, List, Sequence
+from typing import Dict, List, Optional, Sequence
 
 from .native import load
 
@@ -43,6 +43,7 @@ def _lib():
                                       ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t]
     lib.tkr_gate_poll.argtypes = [ctypes.c_int]
     lib.tkr_gate_abort.argtypes = [ctypes.c_int]
+    lib.tkr_gate_cancel.argtypes = [ctypes.c_int]
     lib.tkr_gate_sweep.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_size_t), ctypes.c_int, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_int, ctypes.c_double, dp, dp, dp, dp, dp]
     global _ATEXIT
@@ -149,6 +150,7 @@ class GateComm:
         if h < 0:
             raise RCCLError(f"ranks {rank_base}+{len(self.devices)}/{world}: {_lib().tkr_last_error().decode()}")
         self.handle = h
+        self._sweeping: Optional[int] = None  # the handle a running sweep consumes
 
     def ready(self) -> bool:
         rc = _lib().tkr_gate_poll(self.handle)
@@ -171,12 +173,13 @@ class GateComm:
         ph = (ctypes.c_double * 5)()
         lib = _lib()
         lib.tkr_set_async_teardown(1 if async_teardown else 0)
+        self._sweeping, self.handle = self.handle, None
         try:
-            rc = lib.tkr_gate_sweep(self.handle, sz, n, iters, warmup, 1 if dtype == "bf16" else 0,
+            rc = lib.tkr_gate_sweep(self._sweeping, sz, n, iters, warmup, 1 if dtype == "bf16" else 0,
                                     timeout_s * 1e3, t, alg, bus, err, ph)
         finally:
             lib.tkr_set_async_teardown(0)
-            self.handle = None
+            self._sweeping = None
         if rc != 0:
             raise RCCLError(f"ranks {self.rank_base}+{len(self.devices)}/{self.world}: "
                             f"{lib.tkr_last_error().decode()}")
@@ -189,6 +192,15 @@ class GateComm:
         if self.handle is not None:
             _lib().tkr_gate_abort(self.handle)
             self.handle = None
+
+    def cancel(self) -> None:
+        """Stop this gate from another thread: a pending one is aborted; a sweep still
+        waiting for its peers returns at once with an error (``tkr_gate_cancel``)."""
+        h = self._sweeping if self._sweeping is not None else self.handle
+        if h is not None:
+            _lib().tkr_gate_cancel(h)
+            if h == self.handle:
+                self.handle = None
 
 
 def pending_gates() -> int:

@@ -16,6 +16,11 @@ Each node agent owns its node's GPUs and joins as ranks ``rank_base .. rank_base
 If preparation failed, ``run`` falls back to a fresh uid and a plain (non-pipelined)
 gate.  :meth:`ClusterGate.abort` releases prepared communicators when the gate will not
 run, for example when a node failed and the apply raised.
+
+A gate fails fast: RCCL gives a rank waiting for an absent peer no way out but its own
+timeout, so when one member's gate request fails (unreachable agent, failed init), ``run``
+at once cancels the others' (``/v1/rccl-abort`` on a running sweep, ``tkr_gate_cancel``)
+instead of letting every node wait out ``timeout_s``; the result names each member's error.
 """
 
 import concurrent.futures as cf
@@ -50,11 +55,13 @@ def members_from(urls: Sequence[str], ndevs: Optional[Sequence[int]] = None) -> 
 
 
 class ClusterGate:
-    def __init__(self, transport: Any, members: List[GateMember], sizes: Sequence[int], iters: int = 5):
+    def __init__(self, transport: Any, members: List[GateMember], sizes: Sequence[int], iters: int = 5,
+                 timeout_s: float = 300.0):
         if not members:
             raise ValueError("a cluster gate needs at least one member")
         self.transport = transport
         self.members = members
+        self.timeout_s = float(timeout_s)
         self.world = sum(m.ndev for m in members)
         self.sizes = list(sizes)
         self.iters = iters
@@ -142,15 +149,43 @@ class ClusterGate:
                 self.abort()
             self.uid = self.transport.post(self.members[0].host, "/v1/rccl-uid", {})["uid"]
         uid = self.uid
-        results = self._post_all("/v1/rccl-gate", lambda m: {
-            "uid": uid, "rank": m.rank_base, "world": self.world, "ndev": m.ndev,
-            "sizes": self.sizes, "iters": self.iters})
+        results = self._gate_all(uid)
         self.done = True
         ok = all(r.get("ok") for r in results)
         busbw = [max(r.get("busbw_gbps") or [0.0]) for r in results]
+        errors = [f"{m.url}: {r['error']}" for m, r in zip(self.members, results) if r.get("error")]
         return {"ok": ok, "world": self.world, "nodes": len(self.members), "pipelined": pipelined,
-                "prepare_error": self.prepare_error,
+                "prepare_error": self.prepare_error, "errors": errors,
                 "min_peak_busbw_gbps": min(busbw) if busbw else 0.0, "ranks": results}
+
+    def _gate_all(self, uid: str) -> List[Dict[str, Any]]:
+        """Every member's ``/v1/rccl-gate`` at once; the first failure cancels the rest."""
+        def one(m: GateMember) -> Dict[str, Any]:
+            try:
+                return self.transport.post(m.host, "/v1/rccl-gate", {
+                    "uid": uid, "rank": m.rank_base, "world": self.world, "ndev": m.ndev,
+                    "sizes": self.sizes, "iters": self.iters, "timeout_s": self.timeout_s})
+            except Exception as exc:  # noqa: BLE001 - reported per member
+                return {"ok": False, "error": f"{type(exc).__name__}: {exc}"}
+
+        if len(self.members) == 1:
+            return [one(self.members[0])]
+        futures = {shared_pool("tk-gate", 64).submit(one, m): i for i, m in enumerate(self.members)}
+        out: List[Dict[str, Any]] = [{} for _ in self.members]
+        canceled = False
+        for fut in cf.as_completed(futures):
+            i = futures[fut]
+            out[i] = fut.result()
+            if not out[i].get("ok") and not canceled:
+                canceled = True
+                with span("gate.cancel", world=self.world, failed=self.members[i].url):
+                    for j, m in enumerate(self.members):
+                        if j != i and not any(f.done() for f, k in futures.items() if k == j):
+                            try:
+                                self.transport.post(m.host, "/v1/rccl-abort", {"uid": uid})
+                            except Exception:  # noqa: BLE001 - its own timeout still ends it
+                                pass
+        return out
 
     def abort(self) -> None:
         """Release pending communicators on every agent (no-op once the gate ran)."""

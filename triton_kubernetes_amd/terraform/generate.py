@@ -1340,7 +1340,8 @@ data "external" "gpu_labels" {{
          "src/tk_gpu_probe.hip": os.path.join(CSRC, "tk_gpu_probe.hip"),
          "src/tk_gemm_screen.hip": os.path.join(CSRC, "tk_gemm_screen.hip"),
          "src/tk_rccl_probe.hip": os.path.join(CSRC, "tk_rccl_probe.hip"),
-         "src/tk_rccl_verify.h": os.path.join(CSRC, "tk_rccl_verify.h")}))
+         "src/tk_rccl_verify.h": os.path.join(CSRC, "tk_rccl_verify.h"),
+         "src/tk_rccl_group.h": os.path.join(CSRC, "tk_rccl_group.h")}))
 
     # MI355X cluster add-ons: one template per object from k8s/addons.py (the DirectExecutor
     # renders these same files), filtered by group, then applied through Rancher's k8s proxy
