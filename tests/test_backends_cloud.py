@@ -184,6 +184,33 @@ def test_encrypted_key_needs_passphrase(tmp_path):
     assert public_key_fingerprint(path, lambda: "hunter22") == load_private_key(path, "hunter22").fingerprint_md5()
 
 
+def test_openssh_key_passphrase_never_on_argv(tmp_path, monkeypatch):
+    """the passphrase of an encrypted OpenSSH key reaches ssh-keygen on
+    stdin; ``ps`` (every local user) sees only the argv."""
+    import subprocess
+
+    from triton_kubernetes_amd.utils import sshkeys
+
+    path = str(tmp_path / "enc-ed25519")
+    subprocess.run(["ssh-keygen", "-q", "-t", "ed25519", "-N", "c0rrect horse", "-f", path], check=True)
+    seen = []
+    real = subprocess.run
+
+    def spy(argv, *a, **kw):
+        seen.append((list(argv), kw.get("input")))
+        return real(argv, *a, **kw)
+
+    monkeypatch.setattr(sshkeys.subprocess, "run", spy)
+    key = load_private_key(path, "c0rrect horse")
+    want = real(["ssh-keygen", "-l", "-E", "md5", "-f", path + ".pub"], capture_output=True, text=True).stdout.split()[1]
+    assert "MD5:" + key.fingerprint_md5() == want
+    keygen = [argv for argv, _ in seen if argv[0] == "ssh-keygen"]
+    assert keygen and not any("c0rrect horse" in " ".join(argv) for argv, _ in seen)
+    assert any(inp and b"c0rrect horse" in inp for _, inp in seen)
+    with pytest.raises(sshkeys.KeyParseError, match="incorrect passphrase"):
+        load_private_key(path, "wrong")
+
+
 def test_manta_create_then_destroy_manager_removes_every_object(manta, tmp_path):
     """BASELINE config #4 teardown: status.json, backups and the lock are deleted before the
     directory (reference backend/manta/backend.go:160-194); Manta refuses a non-empty one."""

@@ -297,13 +297,17 @@ def _openssl_decrypt(text: str, passphrase: str) -> str:
 
 
 def _openssh_decrypt(text: str, passphrase: str) -> str:
-    """Decrypt an encrypted OpenSSH-format key on a private temp copy via ssh-keygen."""
+    """Decrypt an encrypted OpenSSH-format key on a private temp copy via ssh-keygen.
+
+    The passphrase goes to ssh-keygen's stdin, never its argv (which every local user can
+    read in ``ps``): without a controlling terminal (a new session) ssh-keygen reads the
+    old passphrase from stdin."""
     with tempfile.TemporaryDirectory(prefix="tk-key-") as d:
         path = os.path.join(d, "key")
         with open(os.open(path, os.O_WRONLY | os.O_CREAT, 0o600), "w") as fh:
             fh.write(text)
-        proc = subprocess.run(["ssh-keygen", "-q", "-p", "-P", passphrase, "-N", "", "-f", path],
-                              capture_output=True, check=False)
+        proc = subprocess.run(["ssh-keygen", "-q", "-p", "-N", "", "-f", path], input=(passphrase + "\n").encode(),
+                              capture_output=True, check=False, start_new_session=True)
         if proc.returncode != 0:
             raise KeyParseError("ssh: incorrect passphrase")
         with open(path, "r", encoding="utf-8") as fh:
