@@ -1,44 +1,131 @@
 #!/usr/bin/env python3
-"""Fake ``ssh`` client for the programs Terraform's ``data "external"`` sources run.
+"""Fake ``ssh`` client: reachability, host keys and (optionally) remote execution.
 
 A host is "up" when ``$FAKE_SSH_HOSTS/<host>/`` exists; that directory is its home and
-``/etc/triton-kubernetes``.  ``cat <file>`` commands print the file from there (``~/x``
-and ``/etc/triton-kubernetes/x`` both map to ``<dir>/x``); any other command succeeds
-silently.  A host that is down fails the way OpenSSH does: exit 255 with "connect to host
-... No route to host".  Options (``-o``, ``-i``, ``-J`` …) are accepted and ignored, but
-every call is appended to ``$FAKE_SSH_LOG`` when set.
+``/etc/triton-kubernetes``.  Its host key is ``<dir>/host_key`` (``"<type> <base64>"``),
+else one derived from its name.  A host that is down fails the way OpenSSH does: exit 255
+with "connect to host ... No route to host".
+
+Host keys are checked the way OpenSSH checks them, against ``-o UserKnownHostsFile=F``
+with ``-o StrictHostKeyChecking=``:
+
+* ``no``: not checked (nothing recorded);
+* ``accept-new``: an unknown host's key is appended to F, a known host's must match;
+* ``yes`` (or unset): it must be in F already.
+
+A mismatch prints OpenSSH's "REMOTE HOST IDENTIFICATION HAS CHANGED" banner and
+"Host key verification failed." and exits 255 before anything runs.  A ``ProxyCommand``
+of the form ``ssh <opts> -W %h:%p user@bastion`` checks the bastion's key the same way
+(with the hop's own options).
+
+Commands: ``cat <file>`` prints the file from the host directory (``~/x`` and
+``/etc/triton-kubernetes/x`` both map to ``<dir>/x``); with ``FAKE_SSH_EXEC=1`` the remote
+command (or stdin for ``bash -s``) runs locally under ``bash``; otherwise anything else
+succeeds silently.  Every call is appended to ``$FAKE_SSH_LOG`` when set.
 """
 
+import base64
+import hashlib
 import json
 import os
 import re
+import shlex
+import subprocess
 import sys
 
 WITH_VALUE = {"-o", "-i", "-J", "-p", "-l", "-F", "-E", "-b", "-c", "-m", "-L", "-R", "-D", "-W"}
 
 
-def main() -> int:
-    argv = sys.argv[1:]
-    i, opts = 0, []
+def parse(argv):
+    i, opts, flags = 0, {}, []
     while i < len(argv) and argv[i].startswith("-"):
-        opts.append(argv[i])
-        if argv[i] in WITH_VALUE and i + 1 < len(argv):
-            opts.append(argv[i + 1])
-            i += 1
+        a = argv[i]
+        if a in WITH_VALUE and i + 1 < len(argv):
+            if a == "-o":
+                k, _, v = argv[i + 1].partition("=")
+                opts[k.lower()] = v
+            else:
+                flags.append((a, argv[i + 1]))
+            i += 2
+            continue
+        flags.append((a, None))
         i += 1
-    if i >= len(argv):
+    return opts, flags, argv[i:]
+
+
+def host_key(host):
+    d = os.path.join(os.environ.get("FAKE_SSH_HOSTS", "/nonexistent"), host)
+    path = os.path.join(d, "host_key")
+    if os.path.exists(path):
+        return open(path, encoding="utf-8").read().strip()
+    blob = base64.b64encode(b"\x00\x00\x00\x0bssh-ed25519\x00\x00\x00\x20" + hashlib.sha256(host.encode()).digest())
+    return "ssh-ed25519 " + blob.decode()
+
+
+def check_key(host, opts):
+    """None when the connection may proceed, else OpenSSH's error text."""
+    mode = opts.get("stricthostkeychecking", "yes").lower()
+    if mode == "no":
+        return None
+    path = opts.get("userknownhostsfile", os.path.expanduser("~/.ssh/known_hosts")).split()[0]
+    want = host_key(host)
+    pinned = []
+    if path != "/dev/null" and os.path.exists(path):
+        for line in open(path, encoding="utf-8"):
+            parts = line.split()
+            if len(parts) >= 3 and host in parts[0].split(","):
+                pinned.append(f"{parts[1]} {parts[2]}")
+    if pinned:
+        if want in pinned:
+            return None
+        return ("@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@\n"
+                "@    WARNING: REMOTE HOST IDENTIFICATION HAS CHANGED!     @\n"
+                "@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@\n"
+                f"Host key for {host} has changed and you have requested strict checking.\n"
+                "Host key verification failed.\n")
+    if mode in ("accept-new", "off") and path != "/dev/null":
+        with open(path, "a", encoding="utf-8") as fh:
+            fh.write(f"{host} {want}\n")
+        return None
+    return f"No ED25519 host key is known for {host} and you have requested strict checking.\n" \
+           "Host key verification failed.\n"
+
+
+def main() -> int:
+    opts, flags, rest = parse(sys.argv[1:])
+    if not rest:
         sys.stderr.write("usage: ssh destination [command]\n")
         return 255
-    dest, command = argv[i], " ".join(argv[i + 1:])
+    dest, command = rest[0], " ".join(rest[1:])
     host = dest.rsplit("@", 1)[-1]
     log = os.environ.get("FAKE_SSH_LOG")
     if log:
         with open(log, "a", encoding="utf-8") as fh:
-            fh.write(json.dumps({"opts": opts, "host": host, "command": command}) + "\n")
-    home = os.path.join(os.environ.get("FAKE_SSH_HOSTS", "/nonexistent"), host)
+            fh.write(json.dumps({"opts": opts, "flags": flags, "host": host, "command": command}) + "\n")
+    hosts = os.environ.get("FAKE_SSH_HOSTS", "/nonexistent")
+    proxy = opts.get("proxycommand")
+    if proxy:  # the hop: its own options, its own key check
+        p_opts, _, p_rest = parse(shlex.split(proxy)[1:])
+        bastion = p_rest[0].rsplit("@", 1)[-1] if p_rest else ""
+        if not os.path.isdir(os.path.join(hosts, bastion)):
+            sys.stderr.write(f"ssh: connect to host {bastion} port 22: No route to host\n")
+            return 255
+        err = check_key(bastion, p_opts)
+        if err:
+            sys.stderr.write(err)
+            return 255
+    home = os.path.join(hosts, host)
     if not os.path.isdir(home):
         sys.stderr.write(f"ssh: connect to host {host} port 22: No route to host\n")
         return 255
+    err = check_key(host, opts)
+    if err:
+        sys.stderr.write(err)
+        return 255
+    if os.environ.get("FAKE_SSH_EXEC") == "1" and command:
+        if command.strip() == "bash -s":
+            return subprocess.run(["bash", "-s"], stdin=sys.stdin).returncode
+        return subprocess.run(["bash", "-c", command]).returncode
     for m in re.finditer(r"\bcat\s+(\S+)", command):
         path = os.path.join(home, os.path.basename(m.group(1)))
         if os.path.exists(path):

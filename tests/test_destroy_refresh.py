@@ -178,7 +178,8 @@ def test_find_only_scripts_outside_apply(tmp_path, env, rancher):
     read_key = os.path.join(catalog.MODULES_DIR, "bare-metal-rancher", "files", "read_api_key.sh")
     labels = os.path.join(catalog.MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files", "read_gpu_labels.sh")
     down = {"host": "10.9.9.9", "ssh_user": "u", "key_path": "k", "bastion_host": ""}
-    for script, empty in ((read_key, {"access_key": "", "secret_key": ""}), (labels, {"labels": "{}"})):
+    for script, empty in ((read_key, {"access_key": "", "secret_key": "", "known_hosts": ""}),
+                          (labels, {"labels": "{}", "known_hosts": ""})):
         res = subprocess.run(["bash", script], input=json.dumps(dict(down, operation="destroy")), capture_output=True,
                              text=True, timeout=60)
         assert res.returncode == 0 and json.loads(res.stdout) == empty, res.stderr
@@ -188,7 +189,9 @@ def test_find_only_scripts_outside_apply(tmp_path, env, rancher):
     res = subprocess.run(["bash", read_key], input=json.dumps({"host": "10.0.0.10", "ssh_user": "u", "key_path": "k",
                                                                "bastion_host": "", "operation": "apply"}),
                          capture_output=True, text=True, timeout=60, check=True)
-    assert json.loads(res.stdout) == {"access_key": "token-tk", "secret_key": "s3cret"}
+    got = json.loads(res.stdout)
+    assert (got["access_key"], got["secret_key"]) == ("token-tk", "s3cret")
+    assert got["known_hosts"].startswith("10.0.0.10 ssh-ed25519 ")  # first contact: pinned and reported
 
 
 def test_fake_terraform_refuses_undeclared_var(tmp_path):

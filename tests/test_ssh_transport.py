@@ -57,9 +57,15 @@ def test_ssh_argv_options(tmp_path):
     assert argv[0] == "ssh" and argv[-2:] == ["core@10.0.0.5", "bash -s"]
     joined = " ".join(argv)
     assert "BatchMode=yes" in joined and "ControlMaster=auto" in joined and f"ControlPath={tmp_path}/%C" in joined
-    assert "-J jump@bastion.example" in joined and os.path.expanduser("~/.ssh/k") in argv
+    assert os.path.expanduser("~/.ssh/k") in argv
+    # the bastion hop is a ProxyCommand with the same host-key options (-J would drop them)
+    proxy = next(a for a in argv if a.startswith("ProxyCommand="))
+    assert "-W %h:%p jump@bastion.example" in proxy and "StrictHostKeyChecking=accept-new" in proxy
+    # never the reference's StrictHostKeyChecking=no: trust on first use, a changed key refused
+    assert "StrictHostKeyChecking=no" not in joined and "UserKnownHostsFile=/dev/null" not in joined
+    assert "StrictHostKeyChecking=accept-new" in joined and f"UserKnownHostsFile={tmp_path}/known_hosts" in joined
     strict = SSHTransport(strict_host_keys=True, control_dir=str(tmp_path)).ssh_argv(HostRef("h"), "x")
-    assert "StrictHostKeyChecking=no" not in " ".join(strict)
+    assert "StrictHostKeyChecking=yes" in " ".join(strict)
 
 
 def test_cluster_over_ssh_runs_rendered_plans(tmp_path, fake_ssh):
@@ -81,9 +87,9 @@ def test_cluster_over_ssh_runs_rendered_plans(tmp_path, fake_ssh):
         calls = _calls(log)
         targets = sorted(c[-2] for c in calls)
         assert targets == ["core@10.1.0.1", "core@10.1.0.2", "core@10.1.0.3"]
-        jumped = [c for c in calls if "-J" in c]
+        jumped = [c for c in calls if any(a.startswith("ProxyCommand=") for a in c)]
         assert sorted(c[-2] for c in jumped) == ["core@10.1.0.2", "core@10.1.0.3"]
-        assert all(c[c.index("-J") + 1] == "core@jump.example" for c in jumped)
+        assert all(any(a.startswith("ProxyCommand=") and a.endswith("core@jump.example") for a in c) for c in jumped)
         sudo = open(sudo_log).read()
         assert "hostnamectl set-hostname e-1" in sudo and "hostnamectl set-hostname w-2" in sudo
         runs = [ln for ln in sudo.splitlines() if ln.startswith("docker run")]

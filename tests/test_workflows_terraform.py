@@ -43,7 +43,8 @@ def test_create_manager_cluster_node_and_destroy(tmp_path, monkeypatch, backend)
     log = install_fake_terraform(tmp_path, monkeypatch, version="1.5.7")
     new_manager(make_ctx(MGR), backend)
     calls = tf_calls(log)
-    assert [c["argv"][0] for c in calls] == ["version", "init", "apply"]
+    # the apply, then the read-back of the SSH host keys its key read pinned (parallel/hostkeys.py)
+    assert [c["argv"][0] for c in calls] == ["version", "init", "apply", "output"]
     assert calls[1]["argv"] == ["init", "-force-copy", "-input=false"]
     assert calls[2]["argv"] == ["apply", "-auto-approve", "-input=false"]
     assert os.path.basename(calls[2]["cwd"]).startswith("triton-kubernetes-")
@@ -85,7 +86,7 @@ def test_create_manager_cluster_node_and_destroy(tmp_path, monkeypatch, backend)
     # data sources), and the modules' data sources told it is a destroy should one run
     assert destroy["argv"] == ["destroy", "-auto-approve", "-refresh=false", "-var=tk_operation=destroy",
                                "-target=module.node_baremetal_dev_dev-worker-3"]
-    assert destroy["doc"]["variable"] == {"tk_operation": {"type": "string", "default": "apply"}}
+    assert destroy["doc"]["variable"]["tk_operation"] == {"type": "string", "default": "apply"}
     assert destroy["doc"]["module"]["cluster_baremetal_dev"]["tk_operation"] == "${var.tk_operation}"
     assert "dev-worker-3" not in backend.state("mgr").nodes("cluster_baremetal_dev")
 

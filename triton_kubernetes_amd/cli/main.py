@@ -52,11 +52,13 @@ VALID = {
     "upgrade": ["cluster"],
     "cordon": ["node"],
     "uncordon": ["node"],
+    "forget": ["host-key"],
 }
 # the reference's error text has the "destory" typo (cmd/destroy.go:22,31)
 _ARG_NAME = {"create": "create", "destroy": "destory", "get": "get", "wait": "wait", "backup": "backup",
              "restore": "restore", "userdata": "userdata", "migrate": "migrate", "credentials": "credentials", "health": "health",
-             "drain": "drain", "cordon": "cordon", "uncordon": "uncordon", "upgrade": "upgrade"}
+             "drain": "drain", "cordon": "cordon", "uncordon": "uncordon", "upgrade": "upgrade",
+             "forget": "forget"}
 
 
 class ArgError(Exception):
@@ -108,7 +110,8 @@ def build_parser() -> argparse.ArgumentParser:
                        ("drain", "Cordon a node and evict its pods (disruption budgets honoured)"),
                        ("upgrade", "Upgrade a cluster's Kubernetes release (one minor at a time) and wait for it"),
                        ("cordon", "Mark a node unschedulable"),
-                       ("uncordon", "Mark a node schedulable again")):
+                       ("uncordon", "Mark a node schedulable again"),
+                       ("forget", "Forget a reinstalled machine's pinned SSH host key (host setting)")):
         p = sub.add_parser(cmd, parents=[common], help=help_)
         p.add_argument("args", nargs="*")
     sub.add_parser("version", parents=[common], help="Print the version number of triton-kubernetes")
@@ -239,6 +242,10 @@ def dispatch(ctx, backend, command: str, what: str) -> int:
         from ..workflows.drain import cordon_command
 
         cordon_command(ctx, backend, command == "cordon")
+    elif command == "forget":
+        from ..workflows.hostkeys import forget_host_key
+
+        forget_host_key(ctx, backend)
     elif command == "wait":
         from ..readiness.waiter import wait_after_create
         from ..workflows.select import select_cluster, select_manager

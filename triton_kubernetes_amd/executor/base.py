@@ -31,7 +31,8 @@ class Executor:
     def print_outputs(self, state: State, backend: Backend, module_key: str, out) -> None:
         outs = self.outputs(state, backend, module_key)
         for k in sorted(outs):
-            out.write(f"{k} = {outs[k]}\n")
+            if not k.startswith("tk_"):  # the CLI's own bookkeeping (pinned host keys)
+                out.write(f"{k} = {outs[k]}\n")
         out.flush()
 
 

@@ -228,7 +228,23 @@ class DirectExecutor(Executor):
             failed = [f"module.{k}: {r.error}" for k, r in report.runs.items() if r.status == "failed"]
             raise ExecutorError("apply failed: " + "; ".join(failed))
 
+    def _bind_host_keys(self, backend: Backend, name: str):
+        """The manager's pinned SSH host keys for this run's SSH connections (they stay bound:
+        the readiness waiter's process gate reaches the same hosts)."""
+        from ..parallel.hostkeys import HostKeys
+
+        keys = HostKeys(backend, name)
+        self.transport.bind_host_keys(keys)
+        return keys
+
     def apply_report(self, state: State, backend: Backend) -> ApplyReport:
+        keys = self._bind_host_keys(backend, state.name)
+        try:
+            return self._apply_report(state, backend)
+        finally:
+            keys.save()  # first-contact keys pinned by this run
+
+    def _apply_report(self, state: State, backend: Backend) -> ApplyReport:
         t0 = time.time()
         runs = self.plan(state)
         tf = self._load_tfstate(backend, state.name)
@@ -448,6 +464,14 @@ class DirectExecutor(Executor):
 
     # --- destroy / outputs ------------------------------------------------------------------------------
     def destroy(self, state: State, backend: Backend, targets: List[str]) -> None:
+        keys = self._bind_host_keys(backend, state.name) if self.node_cleanup else None
+        try:
+            self._destroy(state, backend, targets)
+        finally:
+            if keys is not None:
+                keys.save()
+
+    def _destroy(self, state: State, backend: Backend, targets: List[str]) -> None:
         tf = self._load_tfstate(backend, state.name)
         keys = [t[len("module."):] if t.startswith("module.") else t for t in targets] or list(state.modules())
         if self.node_cleanup:

@@ -55,6 +55,7 @@ from ..state import State
 from ..terraform import constraints
 from ..terraform.catalog import (check_sources, declared_variables, is_packaged_source, local_module_dir,
                                  module_from_source, outputs_for_source, resolve_source, sensitive_outputs)
+from ..parallel.hostkeys import HostKeys, keys_for
 from ..utils.jsonenc import dumps_go
 from .base import Executor, outputs_from_tfstate
 from .shell import ShellOptions, capture_command, run_shell_command
@@ -88,6 +89,10 @@ class Rendered:
 # operation runs them (terraform/generate.py, ``tk_operation``): ``apply`` finds or
 # creates, ``destroy`` / ``read`` only find and tolerate hosts that are gone.
 OPERATION_VAR = "tk_operation"
+# ... and the one carrying the manager's pinned SSH host keys to their SSH reads
+KNOWN_HOSTS_VAR = "tk_known_hosts"
+# module output of the keys those reads pinned (merged back into the store after an apply)
+KNOWN_HOSTS_OUTPUT = "tk_ssh_known_hosts"
 
 
 def _backend_kind(doc: Dict) -> str:
@@ -128,12 +133,16 @@ def resolve_sources(doc: Dict) -> Dict:
     return doc
 
 
-def render(state: State, version: Tuple[int, int, int], backend: Optional[Backend] = None) -> Rendered:
+def render(state: State, version: Tuple[int, int, int], backend: Optional[Backend] = None,
+           known_hosts: str = "") -> Rendered:
     """The document Terraform sees (see module docstring).
 
     With ``backend`` the backend block is this operator's (``state_terraform_config``),
     when it is of the same kind as the persisted one: a shared document carries the key
-    path of whoever wrote it (``key_material``, reference ``backend/manta/backend.go:199``)."""
+    path of whoever wrote it (``key_material``, reference ``backend/manta/backend.go:199``).
+    ``known_hosts``: the manager's pinned SSH host keys (``parallel/hostkeys.py``), for the
+    modules' SSH reads (root variable) and their provisioner connections (``host_key``,
+    ``bastion_host_key`` of each pinned host)."""
     doc = resolve_sources(state.doc)
     kind = _backend_kind(doc)
     if backend is not None and kind:
@@ -146,15 +155,21 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
     doc = copy.deepcopy(doc)
     if managed:
         doc["terraform"]["backend"] = {"local": {"path": WORKDIR_TFSTATE}}
-    operation_var = False
+    root_vars: Dict[str, str] = {}
     if version >= (0, 12, 0):
         for mod in (doc.get("module") or {}).values():
             local = local_module_dir(str(mod.get("source", "")))
-            if local and OPERATION_VAR not in mod and OPERATION_VAR in declared_variables(local):
-                mod[OPERATION_VAR] = f"${{var.{OPERATION_VAR}}}"
-                operation_var = True
-        if operation_var:
-            doc.setdefault("variable", {})[OPERATION_VAR] = {"type": "string", "default": "apply"}
+            declared = declared_variables(local) if local else frozenset()
+            for var, default in ((OPERATION_VAR, "apply"), (KNOWN_HOSTS_VAR, known_hosts)):
+                if var in declared and var not in mod:
+                    mod[var] = f"${{var.{var}}}"
+                    root_vars[var] = default
+            for var, addr in (("host_key", mod.get("host")), ("bastion_host_key", mod.get("bastion_host"))):
+                pinned = keys_for(known_hosts, str(addr or "")) if known_hosts and addr else []
+                if var in declared and var not in mod and pinned:
+                    mod[var] = pinned[0]
+        for var, default in root_vars.items():
+            doc.setdefault("variable", {})[var] = {"type": "string", "default": default}
         outputs = doc.setdefault("output", {})
         for key, mod in state.modules().items():
             source = str(mod.get("source", ""))
@@ -167,7 +182,7 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
                 outputs[f"{key}__{out}"] = block
         if not outputs:
             doc.pop("output")
-    return Rendered(dumps_go(doc), managed, kind, operation_var)
+    return Rendered(dumps_go(doc), managed, kind, OPERATION_VAR in root_vars)
 
 
 def render_document(state: State, version: Tuple[int, int, int]) -> bytes:
@@ -194,6 +209,7 @@ class TerraformExecutor(Executor):
         self.keep_workdir = keep_workdir
         self.last_workdir: Optional[str] = None
         self.last_rendered: Optional[Rendered] = None
+        self.host_keys: Optional[HostKeys] = None
 
     # --- helpers -------------------------------------------------------------------------
     def version(self) -> Tuple[int, int, int]:
@@ -215,7 +231,8 @@ class TerraformExecutor(Executor):
         body, under ``backend.lock``."""
         version = self.version()
         check_module_versions(state, version)
-        rendered = render(state, version, backend)
+        keys = self.host_keys = HostKeys(backend, state.name) if backend is not None else None
+        rendered = render(state, version, backend, keys.text() if keys is not None else "")
         self.last_rendered = rendered
         if rendered.managed_state and backend is None:
             raise ExecutorError(f"the {rendered.backend_kind} state backend needs the CLI to carry terraform.tfstate")
@@ -262,6 +279,21 @@ class TerraformExecutor(Executor):
             if self.parallelism:
                 args.append(f"-parallelism={self.parallelism}")
             self._run(wd, *args)
+            self._pin_learned_keys(state, wd)
+
+    def _pin_learned_keys(self, state: State, wd: str) -> None:
+        """Merge the SSH host keys the modules' reads pinned on first contact (their
+        ``tk_ssh_known_hosts`` outputs) into the manager's store."""
+        if self.host_keys is None or self.version() < (0, 12, 0):
+            return
+        if not any(KNOWN_HOSTS_OUTPUT in outputs_for_source(str(m.get("source", "")))
+                   for m in state.modules().values()):
+            return
+        res = capture_command(self.binary, "output", "-json", working_dir=wd, env=self.env or None)
+        for name, out in (json.loads(res.stdout or "{}") or {}).items():
+            if name.endswith("__" + KNOWN_HOSTS_OUTPUT) and isinstance(out, dict) and out.get("value"):
+                self.host_keys.add(str(out["value"]))
+        self.host_keys.save()
 
     def destroy_flags(self) -> List[str]:
         return ["-auto-approve"] if self.version() >= (0, 15, 0) else ["-force"]

@@ -165,6 +165,7 @@ class NodeAgent:
             self.policy = AgentPolicy([AGENT_IMAGE], loopback_servers=True)
         self.lock = threading.Lock()
         self._gate_mu = threading.Lock()
+        self._stopped = False  # stop(): refuse requests on connections still open
         # long-lived workers for topology prefetch and per-GPU burn-in: no thread is created
         # on the bring-up path (thread creation contends with RCCL/HIP work in the process)
         self._pool = cf.ThreadPoolExecutor(max_workers=len(self.devices) + 2,
@@ -865,6 +866,13 @@ class NodeAgent:
                 n = int(self.headers.get("Content-Length") or 0)
                 return json.loads(self.rfile.read(n) or b"{}") if n else {}
 
+            def _gone(self) -> bool:
+                """The agent stopped: a keep-alive connection accepted before is not served."""
+                if agent._stopped:
+                    self.close_connection = True
+                    self._reply(503, {"error": "agent stopped"})
+                return agent._stopped
+
             def _auth(self) -> bool:
                 given = self.headers.get("X-TK-Agent-Token", "")
                 bearer = self.headers.get("Authorization", "")
@@ -873,6 +881,8 @@ class NodeAgent:
                 return hmac.compare_digest(given, agent.token)
 
             def do_GET(self):
+                if self._gone():
+                    return None
                 if not self._auth():
                     return self._reply(401, {"error": "unauthorized"})
                 if urllib.parse.urlsplit(self.path).path == "/v1/info":
@@ -903,6 +913,8 @@ class NodeAgent:
                 return self._reply(404, {"error": "not found"})
 
             def do_POST(self):
+                if self._gone():
+                    return None
                 if not self._auth():
                     return self._reply(401, {"error": "unauthorized"})
                 path = urllib.parse.urlsplit(self.path).path
@@ -956,6 +968,7 @@ class NodeAgent:
         return f"{'https' if ssl_context is not None else 'http'}://{h}:{p}"
 
     def stop(self) -> None:
+        self._stopped = True
         cv = getattr(self, "_idle_cv", None)
         if cv is not None:
             with cv:

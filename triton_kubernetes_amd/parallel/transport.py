@@ -2,9 +2,12 @@
 
 ===================  =============================================================
 ``ssh`` (default)    ``ssh``/``scp`` subprocesses with connection multiplexing
-                     (ControlMaster) and optional ``ProxyJump`` through the
-                     bastion — Terraform's ``remote-exec`` equivalent (T16), which
-                     in the reference ignores the bastion for managers (Q11)
+                     (ControlMaster) and an optional hop through the bastion —
+                     Terraform's ``remote-exec`` equivalent (T16), which in the
+                     reference ignores the bastion for managers (Q11).  Host keys
+                     are checked against the manager's pinned keys
+                     (``parallel/hostkeys.py``, bound by the executor): trust on
+                     first use, a changed key refused
 ``agent``            HTTPS to a ``tk-node-agent`` (``agent+https://host:port``
                      host strings; ``agent+http://`` on loopback only); the agent
                      runs plan steps natively
@@ -55,6 +58,9 @@ class HostRef:
 class Transport:
     name = "abstract"
 
+    def bind_host_keys(self, keys: Any) -> None:
+        """Use ``keys`` (:class:`~.hostkeys.HostKeys`) for SSH host-key checks from now on."""
+
     def run_plan(self, host: HostRef, plan: BootstrapPlan, timeout: float = 3600) -> Dict[str, Any]:
         raise NotImplementedError
 
@@ -87,24 +93,51 @@ class SSHTransport(Transport):
     name = "ssh"
 
     def __init__(self, strict_host_keys: bool = False, connect_timeout: int = 15, control_dir: Optional[str] = None,
-                 extra_opts: Optional[List[str]] = None):
+                 extra_opts: Optional[List[str]] = None, host_keys: Any = None):
+        # strict_host_keys: only hosts already in the user's own known_hosts (ssh's default
+        # files, StrictHostKeyChecking=yes).  Otherwise the manager's pinned keys when the
+        # executor bound them (bind_host_keys), else a private known_hosts for this
+        # transport's lifetime: either way trust on first use, a changed key refused.
         self.strict = strict_host_keys
         self.connect_timeout = connect_timeout
         self.control_dir = control_dir or tempfile.mkdtemp(prefix="tk-ssh-")
         self.extra = list(extra_opts or [])
+        self.host_keys = host_keys
+
+    def bind_host_keys(self, keys: Any) -> None:
+        self.host_keys = keys
+
+    def _key_opts(self) -> List[str]:
+        if self.strict:
+            return ["-o", "StrictHostKeyChecking=yes"]
+        if self.host_keys is not None:
+            return self.host_keys.ssh_options()
+        return ["-o", f"UserKnownHostsFile={self.control_dir}/known_hosts", "-o", "StrictHostKeyChecking=accept-new",
+                "-o", "HashKnownHosts=no", "-o", "GlobalKnownHostsFile=/dev/null"]
 
     def base_opts(self, host: HostRef) -> List[str]:
         opts = ["-o", "BatchMode=yes", "-o", f"ConnectTimeout={self.connect_timeout}",
                 "-o", "ControlMaster=auto", "-o", f"ControlPath={self.control_dir}/%C",
-                "-o", "ControlPersist=120s", "-o", "ServerAliveInterval=15"]
-        if not self.strict:
-            opts += ["-o", "StrictHostKeyChecking=no", "-o", "UserKnownHostsFile=/dev/null", "-o", "LogLevel=ERROR"]
-        if host.key_path:
-            opts += ["-i", os.path.expanduser(host.key_path)]
+                "-o", "ControlPersist=120s", "-o", "ServerAliveInterval=15", "-o", "LogLevel=ERROR"]
+        keys = self._key_opts()
+        opts += keys
+        key = ["-i", os.path.expanduser(host.key_path)] if host.key_path else []
+        opts += key
         if host.bastion_host:
+            # the hop checks the bastion's key the same way (-J would not pass these options on)
             user = host.bastion_user or host.ssh_user
-            opts += ["-J", f"{user}@{host.bastion_host}"]
+            hop = ["ssh", "-o", "BatchMode=yes", "-o", f"ConnectTimeout={self.connect_timeout}", *keys, *key,
+                   "-W", "%h:%p", f"{user}@{host.bastion_host}"]
+            opts += ["-o", "ProxyCommand=" + " ".join(shlex.quote(a) for a in hop)]
         return opts + self.extra
+
+    def _check_key(self, host: HostRef, rc: int, stderr: str) -> None:
+        from .hostkeys import looks_like_mismatch, mismatch_error
+
+        if rc == 255 and looks_like_mismatch(stderr or ""):
+            manager = getattr(self.host_keys, "manager", "")
+            raise mismatch_error(host.address if host.address in stderr or not host.bastion_host
+                                 else f"{host.address} (or its bastion {host.bastion_host})", stderr, manager)
 
     def ssh_argv(self, host: HostRef, remote_cmd: str) -> List[str]:
         return ["ssh", *self.base_opts(host), f"{host.ssh_user}@{host.address}", remote_cmd]
@@ -112,6 +145,7 @@ class SSHTransport(Transport):
     def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
         proc = subprocess.run(self.ssh_argv(host, "bash -s"), input=script, capture_output=True, text=True,
                               timeout=timeout, check=False)
+        self._check_key(host, proc.returncode, proc.stderr)
         if proc.returncode != 0:
             raise ExecutorError(f"ssh {host.ssh_user}@{host.address}: exit {proc.returncode}: "
                                 f"{proc.stderr[-800:]}")
@@ -121,6 +155,7 @@ class SSHTransport(Transport):
         t0 = time.perf_counter()
         proc = subprocess.run(self.ssh_argv(host, "bash -s"), input=plan.render_shell(), capture_output=True,
                               text=True, timeout=timeout, check=False)
+        self._check_key(host, proc.returncode, proc.stderr)
         return _shell_result(plan, proc.stdout, proc.returncode, (time.perf_counter() - t0) * 1e3, proc.stderr)
 
     def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
@@ -130,6 +165,7 @@ class SSHTransport(Transport):
         proc = subprocess.run(["scp", "-q", *self.base_opts(host), local_path,
                                f"{host.ssh_user}@{host.address}:{remote_path}"], capture_output=True, text=True,
                               check=False)
+        self._check_key(host, proc.returncode, proc.stderr)
         if proc.returncode != 0:
             raise ExecutorError(f"scp {local_path} -> {host.address}:{remote_path}: {proc.stderr[-500:]}")
         self.run_script(host, f"chmod {mode:o} {shlex.quote(remote_path)}\n")
@@ -282,6 +318,10 @@ class TransportRouter(Transport):
 
     def for_host(self, host: HostRef) -> Transport:
         return self.routes[host.scheme]
+
+    def bind_host_keys(self, keys: Any) -> None:
+        for t in self.routes.values():
+            t.bind_host_keys(keys)
 
     def run_plan(self, host, plan, timeout=3600):
         return self.for_host(host).run_plan(host, plan, timeout)

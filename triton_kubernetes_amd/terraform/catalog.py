@@ -23,7 +23,8 @@ from ..errors import ExecutorError
 
 MODULES_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "modules")
 
-MANAGER_OUTPUTS = ("rancher_url", "rancher_access_key", "rancher_secret_key")
+# tk_* outputs are the CLI's own bookkeeping (pinned SSH host keys), not shown by `get`
+MANAGER_OUTPUTS = ("rancher_url", "rancher_access_key", "rancher_secret_key", "tk_ssh_known_hosts")
 CLUSTER_OUTPUTS = ("rancher_cluster_id", "rancher_cluster_registration_token", "rancher_cluster_ca_checksum")
 
 
@@ -78,7 +79,8 @@ _MODULES: List[ModuleInfo] = [
                consumes=("vsphere_datacenter_name", "vsphere_datastore_name", "vsphere_resource_pool_name",
                          "vsphere_network_name")),
     # MI355X additions
-    ModuleInfo("bare-metal-mi355x-rancher-k8s-host", "host", "baremetal", ("gpu_node_labels",), mi355x=True),
+    ModuleInfo("bare-metal-mi355x-rancher-k8s-host", "host", "baremetal", ("gpu_node_labels", "tk_ssh_known_hosts"),
+               mi355x=True),
     ModuleInfo("rancher-k8s-mi355x-addons", "addon", "baremetal", ("addons_applied",), mi355x=True),
 ]
 

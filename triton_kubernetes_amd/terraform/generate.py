@@ -129,6 +129,10 @@ VAR_DOCS = {
     "gpu_burnin": "Burn-in level run on every GPU before the node joins.",
     "rccl_env": "Extra RCCL/HSA environment written to /etc/rccl/rccl.env.",
     "docker_install_sha256": "SHA-256 the downloaded runtime install script must match (empty: not checked).",
+    "tk_known_hosts": ("known_hosts lines of the cluster manager's pinned SSH host keys (set by the executor "
+                       "through the root variable of the same name, parallel/hostkeys.py)."),
+    "host_key": "Pinned SSH host key of host (\"<type> <base64>\", set by the executor; empty: not pinned yet).",
+    "bastion_host_key": "Pinned SSH host key of bastion_host (set by the executor; empty: not pinned yet).",
     "tk_operation": ("Which CLI operation runs this configuration (set by the executor through the root "
                      "variable of the same name): apply runs the create-side data sources in full; destroy and read "
                      "make them find-only and tolerant of hosts that are gone."),
@@ -234,7 +238,10 @@ def _rancher_image_vars(server: bool = True) -> List[Var]:
 
 MANAGER_BASE = [Var("name", None, "Human readable name used as prefix to generated names."),
                 Var("rancher_admin_password", None, "The Rancher admin password", sensitive=True),
-                Var("rancher_bootstrap_password", "", sensitive=True), Var("tk_operation", "apply")]
+                Var("rancher_bootstrap_password", "", sensitive=True), Var("tk_operation", "apply"),
+                Var("tk_known_hosts", "")]
+# SSH host keys pinned by the CLI (parallel/hostkeys.py), rendered by the executor
+PINNED_KEY_VARS = [Var("host_key", ""), Var("bastion_host_key", "")]
 CLUSTER_BASE = [
     Var("name", None, "Human readable name used as prefix to generated names."), Var("tk_operation", "apply"),
     Var("rancher_api_url", None), Var("rancher_access_key", None), Var("rancher_secret_key", None, sensitive=True),
@@ -279,6 +286,8 @@ MANAGER_OUTPUTS = [
     ("rancher_url", '"https://${local.rancher_master_ip}"', False),
     ("rancher_access_key", "data.external.rancher_api_key.result.access_key", False),
     ("rancher_secret_key", "data.external.rancher_api_key.result.secret_key", True),
+    # the host keys the key read pinned (parallel/hostkeys.py; not shown by `get manager`)
+    ("tk_ssh_known_hosts", "data.external.rancher_api_key.result.known_hosts", False),
 ]
 CLUSTER_OUTPUTS = [
     ("rancher_cluster_id", 'data.external.cluster.result["cluster_id"]', False),
@@ -290,6 +299,7 @@ OUTPUT_DOCS = {
     "rancher_access_key": "API access key created for triton-kubernetes.",
     "rancher_secret_key": "API secret key created for triton-kubernetes.",
     "rancher_cluster_id": "Rancher id of the cluster (found by name or created).",
+    "tk_ssh_known_hosts": "known_hosts lines of the hosts this module's SSH reads contacted (pinned by the CLI).",
     "rancher_cluster_registration_token": "Token nodes present when they register.",
     "rancher_cluster_ca_checksum": "Checksum of the Rancher CA bundle that agents pin.",
 }
@@ -360,17 +370,25 @@ data "external" "rancher_api_key" {{
     key_path     = local.key_path
     bastion_host = local.bastion_host
     operation    = var.tk_operation
+    known_hosts  = var.tk_known_hosts
   }}
 }}
 '''
 
 
 def _connection(host: str = "local.rancher_master_ip", user: str = "local.ssh_user", key: str = "local.key_path",
-                bastion: Optional[str] = "local.bastion_host") -> str:
+                bastion: Optional[str] = "local.bastion_host", pinned: bool = False) -> str:
+    """A provisioner ``connection``; ``pinned``: check the host's (and bastion's) key against
+    the keys the CLI pinned (``host_key`` / ``bastion_host_key``, rendered by the executor
+    from the manager's ``known_hosts``; empty = not pinned yet)."""
     lines = ["  connection {", '    type        = "ssh"', f"    user        = {user}", f"    host        = {host}",
              f"    private_key = file(pathexpand({key}))"]
+    if pinned:
+        lines.append('    host_key    = var.host_key == "" ? null : var.host_key')
     if bastion:
         lines.append(f"    bastion_host = {bastion} == \"\" ? null : {bastion}")
+        if pinned:
+            lines.append('    bastion_host_key = var.bastion_host_key == "" ? null : var.bastion_host_key')
     lines.append("  }")
     return "\n".join(lines)
 
@@ -783,7 +801,7 @@ locals {{
     mods.append(Module("bare-metal-rancher", ["external"],
                        MANAGER_BASE + _rancher_image_vars() + [
                            Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""),
-                           Var("key_path", "~/.ssh/id_rsa")],
+                           Var("key_path", "~/.ssh/id_rsa")] + PINNED_KEY_VARS,
                        '''locals {
   rancher_master_id = var.host
   rancher_master_ip = var.host
@@ -791,7 +809,7 @@ locals {{
   key_path          = var.key_path
   bastion_host      = var.bastion_host
 }
-''' + _manager_tail(_connection(), True), MANAGER_OUTPUTS, dict(MANAGER_FILES)))
+''' + _manager_tail(_connection(pinned=True), True), MANAGER_OUTPUTS, dict(MANAGER_FILES)))
 
     # T6 triton-rancher-k8s
     mods.append(Module("triton-rancher-k8s", ["external"], CLUSTER_BASE + TRITON_CREDS, _cluster_data(),
@@ -1169,12 +1187,13 @@ resource "azurerm_virtual_machine_data_disk_attachment" "data" {{
 
     # T16 bare-metal-rancher-k8s-host
     mods.append(Module("bare-metal-rancher-k8s-host", [], HOST_BASE + [
-        Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa")],
+        Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa")]
+        + PINNED_KEY_VARS,
         ROLE_LOCAL + f'''
 
 resource "terraform_data" "install_rancher_agent" {{
   triggers_replace = [var.host]
-{_connection("var.host", "var.ssh_user", "var.key_path", "var.bastion_host")}
+{_connection("var.host", "var.ssh_user", "var.key_path", "var.bastion_host", pinned=True)}
   provisioner "remote-exec" {{
     inline = [{_agent_userdata()}]
   }}
@@ -1243,7 +1262,7 @@ resource "terraform_data" "install_rancher_agent" {{
     # MI355X bare-metal host
     mods.append(Module("bare-metal-mi355x-rancher-k8s-host", ["external"], HOST_BASE + [
         Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa"),
-        Var("tk_operation", "apply"),
+        Var("tk_operation", "apply"), Var("tk_known_hosts", ""), *PINNED_KEY_VARS,
         Var("gpu_product", "MI355X"), Var("gpu_count", 8, "GPUs the node must expose"),
         Var("gpu_burnin", "full", "quick | full | off"),
         Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
@@ -1282,7 +1301,7 @@ locals {{
 
 resource "terraform_data" "install_mi355x_node" {{
   triggers_replace = [var.host]
-{_connection("var.host", "var.ssh_user", "var.key_path", "var.bastion_host")}
+{_connection("var.host", "var.ssh_user", "var.key_path", "var.bastion_host", pinned=True)}
   provisioner "remote-exec" {{
     inline = ["sudo mkdir -p /opt/triton-kubernetes/src && sudo chown $(id -un) /opt/triton-kubernetes/src"]
   }}
@@ -1332,9 +1351,11 @@ data "external" "gpu_labels" {{
     key_path     = var.key_path
     bastion_host = var.bastion_host
     operation    = var.tk_operation
+    known_hosts  = var.tk_known_hosts
   }}
 }}
-''', [("gpu_node_labels", "data.external.gpu_labels.result.labels", False)],
+''', [("gpu_node_labels", "data.external.gpu_labels.result.labels", False),
+          ("tk_ssh_known_hosts", "data.external.gpu_labels.result.known_hosts", False)],
         {"install_mi355x_node.sh.tftpl": scripts.INSTALL_MI355X_NODE, "read_gpu_labels.sh": scripts.READ_REMOTE_LABELS},
         {"src/tk_topo.cpp": os.path.join(CSRC, "tk_topo.cpp"),
          "src/tk_gpu_probe.hip": os.path.join(CSRC, "tk_gpu_probe.hip"),

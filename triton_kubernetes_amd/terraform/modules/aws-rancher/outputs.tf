@@ -13,3 +13,8 @@ output "rancher_secret_key" {
   value       = data.external.rancher_api_key.result.secret_key
   sensitive   = true
 }
+
+output "tk_ssh_known_hosts" {
+  description = "known_hosts lines of the hosts this module's SSH reads contacted (pinned by the CLI)."
+  value       = data.external.rancher_api_key.result.known_hosts
+}

@@ -37,6 +37,12 @@ variable "tk_operation" {
   }
 }
 
+variable "tk_known_hosts" {
+  description = "known_hosts lines of the cluster manager's pinned SSH host keys (set by the executor through the root variable of the same name, parallel/hostkeys.py)."
+  type        = string
+  default     = ""
+}
+
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
   type        = string

@@ -111,6 +111,24 @@ variable "tk_operation" {
   }
 }
 
+variable "tk_known_hosts" {
+  description = "known_hosts lines of the cluster manager's pinned SSH host keys (set by the executor through the root variable of the same name, parallel/hostkeys.py)."
+  type        = string
+  default     = ""
+}
+
+variable "host_key" {
+  description = "Pinned SSH host key of host (\"<type> <base64>\", set by the executor; empty: not pinned yet)."
+  type        = string
+  default     = ""
+}
+
+variable "bastion_host_key" {
+  description = "Pinned SSH host key of bastion_host (set by the executor; empty: not pinned yet)."
+  type        = string
+  default     = ""
+}
+
 variable "gpu_product" {
   description = "Gpu product."
   type        = string

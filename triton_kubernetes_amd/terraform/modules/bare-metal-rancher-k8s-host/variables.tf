@@ -99,3 +99,15 @@ variable "key_path" {
   type        = string
   default     = "~/.ssh/id_rsa"
 }
+
+variable "host_key" {
+  description = "Pinned SSH host key of host (\"<type> <base64>\", set by the executor; empty: not pinned yet)."
+  type        = string
+  default     = ""
+}
+
+variable "bastion_host_key" {
+  description = "Pinned SSH host key of bastion_host (set by the executor; empty: not pinned yet)."
+  type        = string
+  default     = ""
+}

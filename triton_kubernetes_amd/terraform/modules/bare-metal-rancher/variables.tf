@@ -37,6 +37,12 @@ variable "tk_operation" {
   }
 }
 
+variable "tk_known_hosts" {
+  description = "known_hosts lines of the cluster manager's pinned SSH host keys (set by the executor through the root variable of the same name, parallel/hostkeys.py)."
+  type        = string
+  default     = ""
+}
+
 variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
   type        = string
@@ -101,4 +107,16 @@ variable "key_path" {
   description = "Private key used for SSH."
   type        = string
   default     = "~/.ssh/id_rsa"
+}
+
+variable "host_key" {
+  description = "Pinned SSH host key of host (\"<type> <base64>\", set by the executor; empty: not pinned yet)."
+  type        = string
+  default     = ""
+}
+
+variable "bastion_host_key" {
+  description = "Pinned SSH host key of bastion_host (set by the executor; empty: not pinned yet)."
+  type        = string
+  default     = ""
 }
