@@ -288,7 +288,8 @@ def main() -> int:
     creds = {}
     for name, addr in addresses.items():
         creds[name] = os.path.join(work, "creds", name)
-        pki.issue(addr, [versions.AGENT_IMAGE], servers=[rancher_url]).write(creds[name])
+        pki.issue(addr, [versions.AGENT_IMAGE], servers=[rancher_url],
+                  distributions=[versions.DEFAULT_DISTRIBUTION]).write(creds[name])
     client_ctx = pki.client_context()
 
     def start_agents(tag: str):

@@ -148,6 +148,43 @@ def test_rke2_join_only_through_an_allowed_server(pki, tmp_path):
         AgentPolicy.from_json({"images": [], "servers": ["ftp://x"]})
 
 
+def test_rke1_plan_to_a_foreign_server_refused(pki, tmp_path):
+    """an RKE1 plan with the allow-listed image but a Rancher server the
+    node does not list was run (``docker run --privileged ... --server <theirs>``): a
+    token holder could hand the node to a Rancher they control.  Both distributions now
+    need an allowed server, and a node enrolled for RKE2 refuses RKE1 plans outright."""
+    def agent_with(address, **kw):
+        d = str(tmp_path / f"creds-{address}")
+        pki.issue(address, [AGENT_IMAGE], servers=["https://rancher.example"], **kw).write(d)
+        creds = read_credentials(d)
+        a = NodeAgent(name=address, mode="sim", token=creds["token"], root=str(tmp_path / address),
+                      policy=creds["policy"])
+        return a, a.serve(address, ssl_context=creds["ssl_context"])
+
+    tr = AgentTransport(pki=pki)
+    any_dist, url = agent_with("127.1.9.8")
+    rke2_only, url2 = agent_with("127.1.9.9", distributions=["rke2"])
+    try:
+        foreign = build_host_plan(dict(WORKER, k8s_distribution="rke1", rancher_agent_image=AGENT_IMAGE),
+                                  "https://203.0.113.9", "tok", "sum")
+        with pytest.raises(HTTPError) as exc:
+            tr.run_plan(HostRef("agent+" + url), foreign)
+        assert exc.value.status == 403 and "203.0.113.9" in exc.value.body.decode()
+        rke1 = build_host_plan(dict(WORKER, k8s_distribution="rke1", rancher_agent_image=AGENT_IMAGE),
+                               "https://rancher.example", "tok", "sum")
+        assert any_dist.refusals(rke1) == []  # enrolled for either: listed image and server pass
+        with pytest.raises(HTTPError) as exc:
+            tr.run_plan(HostRef("agent+" + url2), rke1)
+        assert exc.value.status == 403 and "distribution 'rke1'" in exc.value.body.decode()
+        assert any_dist.history == [] and rke2_only.history == []
+        assert AgentPolicy.from_json(rke2_only.policy.to_json()).distributions == ["rke2"]
+        with pytest.raises(TKError):
+            AgentPolicy.from_json({"images": [AGENT_IMAGE], "distributions": ["k3s"]})
+    finally:
+        any_dist.stop()
+        rke2_only.stop()
+
+
 def test_client_trusts_only_the_managers_ca(pki, tmp_path):
     other = AgentPKI.create("someone-else")
     agent, url = _agent(other, tmp_path, "127.1.9.5")
@@ -209,7 +246,7 @@ def test_create_cluster_over_tls_with_per_node_tokens(tmp_path):
             urls = []
             for i, addr in enumerate(("127.1.8.2", "127.1.8.3")):
                 d = str(tmp_path / f"c{i}")
-                pki.issue(addr, [AGENT_IMAGE]).write(d)
+                pki.issue(addr, [AGENT_IMAGE], servers=[rancher.url]).write(d)
                 creds = read_credentials(d)
                 ag = NodeAgent(name=addr, mode="sim", devices=list(range(8)) if i else [], token=creds["token"],
                                root=str(tmp_path / f"r{i}"), policy=creds["policy"],
@@ -285,7 +322,7 @@ def test_cli_credentials_node(tmp_path, monkeypatch):
     assert rc == 0, out.getvalue()
     policy = json.loads((tmp_path / "creds" / "agent-policy.json").read_text())
     # no manager state yet: no Rancher server to allow (RKE2 joins refused, and said so)
-    assert policy == {"images": ["rancher/rancher-agent@sha256:" + "cd" * 32], "servers": []}
+    assert policy == {"images": ["rancher/rancher-agent@sha256:" + "cd" * 32], "servers": [], "distributions": ["rke2"]}
     assert "cannot join RKE2 clusters" in out.getvalue()
     pki = load_pki(be, "mgr", create=False)
     assert (tmp_path / "creds" / "agent-token").read_text().strip() == pki.node_token("10.2.3.4")

@@ -200,17 +200,23 @@ class NodeAgent:
 
     # --- plan execution ---------------------------------------------------------------------
     def refusals(self, plan: BootstrapPlan) -> List[str]:
-        """Why this node refuses ``plan``: an agent step whose image (RKE1) or Rancher
-        server (RKE2) is outside the node's allow-list."""
+        """Why this node refuses ``plan``: an agent step for a distribution the node was not
+        enrolled for, or whose Rancher server (either distribution: RKE2 runs its installer,
+        RKE1 hands it to a privileged ``rancher-agent``) or image (RKE1) is outside the
+        node's allow-list."""
         out = []
         for s in plan.steps:
             if s.action != "agent":
                 continue
-            if s.params.get("distribution", plan.distribution) == "rke2":
-                server = str(s.params.get("server") or plan.rancher_url)
-                if not self.policy.allows_server(server) or server != plan.rancher_url:
-                    out.append(f"Rancher server {server!r} is not in this node's allow-list")
-            elif not self.policy.allows(str(s.params.get("image", ""))):
+            dist = str(s.params.get("distribution", plan.distribution))
+            if not self.policy.allows_distribution(dist):
+                out.append(f"distribution {dist!r} is not the one this node was enrolled for "
+                           f"({', '.join(self.policy.distributions)})")
+                continue
+            server = str(s.params.get("server") or plan.rancher_url)
+            if not self.policy.allows_server(server) or server != plan.rancher_url:
+                out.append(f"Rancher server {server!r} is not in this node's allow-list")
+            if dist != "rke2" and not self.policy.allows(str(s.params.get("image", ""))):
                 out.append(f"image {str(s.params.get('image', ''))!r} is not in this node's allow-list")
         return out
 

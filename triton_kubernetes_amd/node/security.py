@@ -88,9 +88,15 @@ class AgentPolicy:
     images: List[str] = field(default_factory=list)
     servers: List[str] = field(default_factory=list)
     loopback_servers: bool = False
+    # the distribution the node was enrolled for (rke2 | rke1); empty: either (credentials
+    # issued before the field existed, development agents)
+    distributions: List[str] = field(default_factory=list)
 
     def allows(self, image: str) -> bool:
         return image in self.images
+
+    def allows_distribution(self, dist: str) -> bool:
+        return not self.distributions or dist in self.distributions
 
     def allows_server(self, url: str) -> bool:
         origin = server_origin(url)
@@ -104,6 +110,8 @@ class AgentPolicy:
         doc: Dict[str, Any] = {"images": list(self.images), "servers": list(self.servers)}
         if self.loopback_servers:
             doc["loopback_servers"] = True
+        if self.distributions:
+            doc["distributions"] = list(self.distributions)
         return doc
 
     @classmethod
@@ -114,7 +122,11 @@ class AgentPolicy:
         servers = doc.get("servers") or []
         if not isinstance(servers, list) or not all(isinstance(u, str) and server_origin(u) for u in servers):
             raise TKError("agent policy: servers must be a list of http(s) Rancher server URLs")
-        return cls(images=list(imgs), servers=list(servers), loopback_servers=doc.get("loopback_servers") is True)
+        dists = doc.get("distributions") or []
+        if not isinstance(dists, list) or not all(d in ("rke2", "rke1") for d in dists):
+            raise TKError("agent policy: distributions must be a list of rke2 / rke1")
+        return cls(images=list(imgs), servers=list(servers), loopback_servers=doc.get("loopback_servers") is True,
+                   distributions=list(dists))
 
 
 @dataclass
@@ -160,14 +172,14 @@ class AgentPKI:
         return "tka1." + mac.hexdigest()
 
     def issue(self, address: str, images: List[str], extra_names: Optional[List[str]] = None,
-              servers: Optional[List[str]] = None) -> NodeCredentials:
+              servers: Optional[List[str]] = None, distributions: Optional[List[str]] = None) -> NodeCredentials:
         from ..k8s.tls import CA, issue
 
         host = agent_address(address)
         names = [host] + [n for n in (extra_names or []) if n != host]
         cert = issue(CA(self.ca_cert, self.ca_key), host, names)
         return NodeCredentials(host, self.node_token(host), cert.cert_pem, cert.key_pem, self.ca_cert,
-                               AgentPolicy(list(images), list(servers or [])))
+                               AgentPolicy(list(images), list(servers or []), distributions=list(distributions or [])))
 
     def client_context(self) -> ssl.SSLContext:
         """Verifies agents against this manager's CA only (not the system trust store)."""

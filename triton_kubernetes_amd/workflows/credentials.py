@@ -10,9 +10,13 @@ node may take its ``system-agent-install.sh`` from are the manager's ``rancher_u
 node's ``/etc/triton-kubernetes/agent/`` (the ``tk-node-agent`` unit reads them with
 ``--credentials``).
 
+The node is enrolled for one Kubernetes distribution (``agent_distribution``, default
+the pinned default, RKE2): a plan naming the other one is refused, so a token holder
+cannot switch an RKE2 node to the RKE1 path (a privileged ``rancher-agent`` container).
+
 Settings: ``cluster_manager``, ``agent_address`` (IP or DNS name the CLI reaches the
 agent at), ``agent_images`` (list, optional), ``agent_servers`` (list, optional),
-``credentials_dir`` (optional).
+``agent_distribution`` (rke2 | rke1, optional), ``credentials_dir`` (optional).
 """
 
 import os
@@ -55,8 +59,12 @@ def node_credentials(ctx: Context, backend: Backend) -> str:
     bad = [u for u in servers if not server_origin(u)]
     if bad:
         raise ConfigError(f"agent_servers: {bad[0]!r} is not an http(s) URL")
+    dist = (ctx.get_string("agent_distribution") if ctx.is_set("agent_distribution")
+            else versions.DEFAULT_DISTRIBUTION).lower()
+    if dist not in versions.DISTRIBUTIONS:
+        raise ConfigError(f"agent_distribution must be one of {', '.join(versions.DISTRIBUTIONS)}, not {dist!r}")
     out = ctx.get_string("credentials_dir") if ctx.is_set("credentials_dir") else f"agent-credentials-{address}"
-    creds = load_pki(backend, manager).issue(address, list(images), servers=list(servers))
+    creds = load_pki(backend, manager).issue(address, list(images), servers=list(servers), distributions=[dist])
     files = creds.write(os.path.abspath(os.path.expanduser(out)))
     ctx.echo(f"Agent credentials for {creds.address} (manager '{manager}') written to {os.path.dirname(files[0])}:")
     for f in files:
