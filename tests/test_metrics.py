@@ -331,6 +331,16 @@ def test_scrape_config_for_agent_nodes(tmp_path):
             s = _samples(resp.body.decode())
             assert s[("tk_bringup_success", (("node", node),))] == 1
             assert any(k[0] == "tk_gpu_healthy" for k in s)
+            # the scrape token is read-only -- the monitoring stack that holds it
+            # reads /metrics and /v1/health, but cannot post plans, shut down or run RCCL
+            assert token.startswith("tkm1.") and "tka1." not in token
+            client = HTTPClient(base_url=f"https://{target}", ssl_context=tls, retries=0)
+            assert client.request("GET", "/v1/health", headers={"Authorization": f"Bearer {token}"}).status == 200
+            for path in ("/v1/plan", "/v1/shutdown", "/v1/cleanup", "/v1/rccl-uid", "/v1/rccl-abort"):
+                with pytest.raises(Exception, match="401"):
+                    client.request("POST", path, json_body={}, headers={"X-TK-Agent-Token": token})
+            with pytest.raises(Exception, match="401"):
+                client.request("GET", "/v1/info", headers={"Authorization": f"Bearer {token}"})
         # an SSH / Terraform node with the textfile collector: a node_exporter job
         st = backend.state("mgr")
         key = st.nodes("cluster_baremetal_dev")["gpu-1"]

@@ -68,7 +68,7 @@ from ..utils.httpserver import Server as HTTPServer
 from ..utils.trace import span
 from .labels import burnin_labels, labels_from_topology, link_labels
 from .plan import BootstrapPlan, Step
-from .security import AgentPolicy, is_loopback
+from .security import AgentPolicy, is_loopback, metrics_token
 
 MODES = ("sim", "exec")
 _HOSTNAME_RE = re.compile(r"^[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?(\.[a-z0-9]([-a-z0-9]{0,61}[a-z0-9])?)*$")
@@ -865,6 +865,8 @@ class NodeAgent:
                 self.send_response(code)
                 self.send_header("Content-Type", "application/json")
                 self.send_header("Content-Length", str(len(body)))
+                if self.close_connection:  # the client must not reuse this connection
+                    self.send_header("Connection", "close")
                 self.end_headers()
                 self.wfile.write(body)
 
@@ -879,17 +881,22 @@ class NodeAgent:
                     self._reply(503, {"error": "agent stopped"})
                 return agent._stopped
 
-            def _auth(self) -> bool:
+            def _auth(self, read_only: bool = False) -> bool:
+                """The node's agent token; for the read-only endpoints (``read_only``) also its
+                scrape token (``security.metrics_token``), which is all Prometheus holds."""
                 given = self.headers.get("X-TK-Agent-Token", "")
                 bearer = self.headers.get("Authorization", "")
                 if not given and bearer.startswith("Bearer "):  # Prometheus' scrape authorization
                     given = bearer[len("Bearer "):]
-                return hmac.compare_digest(given, agent.token)
+                if hmac.compare_digest(given, agent.token):
+                    return True
+                return read_only and hmac.compare_digest(given, metrics_token(agent.token))
 
             def do_GET(self):
                 if self._gone():
                     return None
-                if not self._auth():
+                path = urllib.parse.urlsplit(self.path).path
+                if not self._auth(read_only=path in ("/metrics", "/v1/health")):
                     return self._reply(401, {"error": "unauthorized"})
                 if urllib.parse.urlsplit(self.path).path == "/v1/info":
                     with agent._gate_mu:
@@ -922,6 +929,8 @@ class NodeAgent:
                 if self._gone():
                     return None
                 if not self._auth():
+                    # the request body is not read: this connection cannot carry another request
+                    self.close_connection = True
                     return self._reply(401, {"error": "unauthorized"})
                 path = urllib.parse.urlsplit(self.path).path
                 try:

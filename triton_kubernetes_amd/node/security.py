@@ -233,6 +233,15 @@ def server_context(cert_pem: str, key_pem: str) -> ssl.SSLContext:
     return ctx
 
 
+def metrics_token(node_token: str) -> str:
+    """The read-only scrape token of a node: derived from its agent token one way (HMAC), so
+    the monitoring stack that holds it can read ``GET /metrics`` and ``GET /v1/health`` and
+    nothing else -- it cannot post plans, shut the agent down or run the RCCL endpoints, and
+    cannot recover the node's token.  The agent derives it from its own token; the CLI from
+    the token it derives for the node (``AgentPKI.node_token``)."""
+    return "tkm1." + hmac.new(node_token.encode(), b"tk-agent-metrics", hashlib.sha256).hexdigest()
+
+
 def read_credentials(directory: str) -> Dict[str, Any]:
     """A node's credential directory -> ``{token, ssl_context, policy}``."""
     def rd(name: str) -> str:
@@ -243,5 +252,5 @@ def read_credentials(directory: str) -> Dict[str, Any]:
             "policy": AgentPolicy.from_json(json.loads(rd("agent-policy.json")))}
 
 
-__all__ = ["AgentPKI", "AgentPolicy", "NodeCredentials", "load_pki", "server_context", "read_credentials",
+__all__ = ["AgentPKI", "AgentPolicy", "NodeCredentials", "load_pki", "server_context", "read_credentials", "metrics_token",
            "agent_address", "is_loopback", "server_origin", "PKI_BLOB", "DEFAULT_CRED_DIR"]

@@ -39,7 +39,7 @@ def _write_secret(path: str, data: str) -> None:
 def scrape_config(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
     import yaml
 
-    from ..node.security import agent_address, load_pki
+    from ..node.security import agent_address, load_pki, metrics_token
 
     managers = backend.states()
     if not managers:
@@ -75,7 +75,8 @@ def scrape_config(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
         for host, url in agents:
             u = urllib.parse.urlsplit(url)
             token_file = os.path.join(secrets_dir, f"{manager}-{name}-{host}.token")
-            _write_secret(token_file, shared or pki.node_token(agent_address(url)))
+            # the node's read-only scrape token, never its agent token (which can post plans)
+            _write_secret(token_file, metrics_token(shared or pki.node_token(agent_address(url))))
             job: Dict[str, Any] = {
                 "job_name": f"tk-{name}-{host}", "scheme": u.scheme or "https", "metrics_path": "/metrics",
                 "authorization": {"type": "Bearer", "credentials_file": token_file},
