@@ -385,6 +385,40 @@ def test_health_cluster_reconciles_the_taint(tmp_path):
         fake.stop()
 
 
+def test_health_taint_keeps_a_taint_added_meanwhile(tmp_path):
+    """spec.taints is replaced whole, so fencing a node from a node list read
+    earlier dropped a taint added since (the node-lifecycle controller's unreachable taint).
+    The patch now carries the node's resourceVersion; the API server answers 409 on a stale
+    one (the fake refuses it too) and the node is read again."""
+    from triton_kubernetes_amd.cloud.http import HTTPError
+    from triton_kubernetes_amd.rancher.client import RancherClient
+    from triton_kubernetes_amd.workflows.health import _reconcile
+
+    fake, agents, backend, ctx, new_cluster = _create(tmp_path, "taint")
+    try:
+        new_cluster(ctx, backend)
+        cid = list(fake.state.clusters)[0]
+        outs = json.loads(backend.read_tfstate("mgr"))["module_outputs"]["cluster-manager"]
+        client = RancherClient(fake.url, outs["rancher_access_key"], outs["rancher_secret_key"])
+        stale = next(n for n in client.k8s_nodes(cid) if n["metadata"]["name"] == "gpu-1")
+        unreachable = {"key": "node.kubernetes.io/unreachable", "effect": "NoExecute"}
+        client.patch_node(cid, "gpu-1", {"spec": {"taints": list(stale["spec"]["taints"]) + [unreachable]}})
+        # the fake refuses a patch against the old resourceVersion, as the API server does
+        with pytest.raises(HTTPError) as exc:
+            client.patch_node(cid, "gpu-1", {"metadata": {"resourceVersion": stale["metadata"]["resourceVersion"]},
+                                            "spec": {"taints": []}})
+        assert exc.value.status == 409
+        verdict = {"status": "unhealthy", "gpus": [], "unhealthy_gpus": 1}
+        assert _reconcile(client, cid, stale, verdict) == "tainted"
+        node = next(n for n in client.k8s_nodes(cid) if n["metadata"]["name"] == "gpu-1")
+        keys = [t["key"] for t in node["spec"]["taints"]]
+        assert "node.kubernetes.io/unreachable" in keys and health.HEALTH_TAINT["key"] in keys
+    finally:
+        for a in agents:
+            a.stop()
+        fake.stop()
+
+
 def test_health_probe_over_the_host_transport(tmp_path, native_ok):
     """SSH / Terraform nodes: the labeller runs on the node; exit 3 is a verdict, not an error."""
     from triton_kubernetes_amd.parallel.transport import LocalTransport

@@ -228,3 +228,29 @@ def test_manta_lock_is_reentrant_and_renewed(manta, monkeypatch):
         t.join()
         assert got == [False]  # still held: never looked expired
     assert path not in fake.objects
+
+
+def test_manta_lock_lost_to_a_takeover_refuses_writes(manta):
+    """a holder whose lock expired and was taken over (a suspended laptop) must
+    not go on writing the tfstate / document over the new holder's."""
+    import time
+
+    from triton_kubernetes_amd.errors import BackendError
+
+    fake, be = manta
+    path = "/acct/stor/triton-kubernetes/mgr/.lock"
+    st = State("mgr")
+    with be.lock("mgr", ttl=0.3):
+        be.persist_state(st)  # held: fine
+        # another CLI found the lock expired and replaced it (If-Match on the old etag)
+        fake.objects[path] = (json.dumps({"token": "other", "expires": time.time() + 900}).encode(),
+                              "application/json", "etag-of-the-other-writer")
+        time.sleep(0.45)  # the heartbeat's If-Match fails: the lock is lost
+        with pytest.raises(BackendError, match="taken over by another writer"):
+            be.write_tfstate("mgr", b"{}")
+        with pytest.raises(BackendError, match="taken over"):
+            be.persist_state(st)
+    assert json.loads(fake.objects[path][0])["token"] == "other"  # the new holder's lock is left alone
+    del fake.objects[path]
+    with be.lock("mgr"):
+        be.persist_state(st)  # a fresh lock writes again

@@ -65,8 +65,18 @@ def test_upgrade_rke1_cluster(env):  # noqa: F811 - fixture
     fake, agent, backend, base = env
     cid = _cluster(fake, agent, backend, base, "v1.28.15-rancher1-1")
     assert not cid.startswith("c-m-")
-    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", k8s_version="v1.29.14-rancher1-1"))
-    assert dispatch(ctx, backend, "upgrade", "cluster") == 0
+    # Rancher reports an RKE1 cluster's upstream version, not the RKE1 release string
+    assert fake.state.clusters[cid]["version"]["gitVersion"] == "v1.28.15"
+    fake.state.upgrade_seconds = 0.2
+    sel = dict(base, cluster_manager="mgr", cluster_name="dev")
+    ctx = make_ctx(dict(sel, k8s_version="v1.29.14-rancher1-1", wait_timeout=60))
+    assert dispatch(ctx, backend, "upgrade", "cluster") == 0  # the wait used to time out here
+    assert "cluster 'dev' runs v1.29.14-rancher1-1" in output(ctx)
     assert fake.state.clusters[cid]["rancherKubernetesEngineConfig"]["kubernetesVersion"] == "v1.29.14-rancher1-1"
     assert fake.state.clusters[cid]["state"] == "active"
+    nodes = fake.k8s_nodes(cid)
+    assert {n["status"]["nodeInfo"]["kubeletVersion"] for n in nodes} == {"v1.29.14"}
     assert backend.state("mgr").module("cluster_baremetal_dev")["k8s_version"] == "v1.29.14-rancher1-1"
+    again = make_ctx(dict(sel, k8s_version="v1.29.14-rancher1-1"))
+    dispatch(again, backend, "upgrade", "cluster")
+    assert "already runs v1.29.14" in output(again) and fake.state.upgrades == 1

@@ -82,7 +82,17 @@ class MantaBackend(Backend):
         raw = self.client.get_object(self._p(name, CONFIG_FILE))
         return State(name, raw if raw is not None else b"{}")
 
+    def _check_held(self, name: str) -> None:
+        """Refuse a write under a lock this thread held but lost: the heartbeat found it taken
+        over (it had expired, e.g. a suspended laptop), so another writer may have written
+        since; writing now would overwrite its work."""
+        lost = (getattr(self._held, "lost", None) or {}).get(name)
+        if lost is not None and lost.is_set():
+            raise BackendError(f"the Manta state lock of '{name}' was taken over by another writer while this "
+                               "run held it; not writing, to keep that writer's changes. Re-run the command.")
+
     def persist_state(self, state: State) -> None:
+        self._check_held(state.name)
         self.client.put_directory(self._p(state.name))
         self.client.put_object(self._p(state.name, CONFIG_FILE), state.bytes())
 
@@ -129,6 +139,7 @@ class MantaBackend(Backend):
         return self.client.get_object(self._p(name, filename))
 
     def write_blob(self, name: str, filename: str, data: bytes) -> None:
+        self._check_held(name)
         self.client.put_directory(self._p(name))
         self.client.put_object(self._p(name, filename), data)
 
@@ -179,6 +190,10 @@ class MantaBackend(Backend):
             time.sleep(poll)
         current = [etag]
         stop = threading.Event()
+        lost = threading.Event()
+        if getattr(self._held, "lost", None) is None:
+            self._held.lost = {}
+        self._held.lost[name] = lost
 
         def heartbeat() -> None:
             while not stop.wait(ttl / 3.0):
@@ -187,7 +202,8 @@ class MantaBackend(Backend):
                     new = self.client.put_object(path, refreshed, if_match=current[0])
                 except Exception:  # transient: the next beat retries before the TTL runs out
                     continue
-                if new is None:  # taken over: we lost it (an expired lock); stop renewing
+                if new is None:  # taken over: we lost it (an expired lock); every write refuses now
+                    lost.set()
                     return
                 current[0] = new
 
@@ -198,6 +214,8 @@ class MantaBackend(Backend):
             yield
         finally:
             del held[name]
+            self._held.lost.pop(name, None)
             stop.set()
             beat.join()
-            self.client.delete(path, if_match=current[0] or None)
+            if not lost.is_set():  # a lock taken over is the new holder's
+                self.client.delete(path, if_match=current[0] or None)

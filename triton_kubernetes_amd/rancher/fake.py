@@ -75,7 +75,7 @@ import uuid
 from typing import Any, Dict, List, Optional, Sequence, Set, Tuple
 
 from ..versions import (DEFAULT_K8S_VERSION, FLEET_NAMESPACE, K8S_VERSIONS, PASSWORD_MIN_LENGTH, RANCHER_VERSION,
-                        RKE2_CNIS, RKE2_VERSIONS, SYSTEM_AGENT_INSTALL_PATH, bootstrap_password)
+                        RKE2_CNIS, RKE2_VERSIONS, SYSTEM_AGENT_INSTALL_PATH, bootstrap_password, running_version)
 from ..utils.httpserver import Server as HTTPServer
 
 FAKE_CACERTS = "-----BEGIN CERTIFICATE-----\nMIIFAKECERTIFICATEFORTESTS\n-----END CERTIFICATE-----"
@@ -331,7 +331,8 @@ class FakeRancher:
                 if gpus is not None:
                     alloc["amd.com/gpu"] = str(gpus)
                 items.append({
-                    "metadata": {"name": n["hostname"], "labels": self._node_labels(n)},
+                    "metadata": {"name": n["hostname"], "labels": self._node_labels(n),
+                                 "resourceVersion": str(n.get("rv", 1))},
                     "spec": dict({"taints": list(n.get("taints") or [])},
                                  **({"unschedulable": True} if n.get("unschedulable") else {})),
                     "status": {"conditions": [{"type": "Ready", "status": "True" if ready else "False"}],
@@ -497,7 +498,9 @@ class FakeRancher:
                 st.clusters[cid] = {"id": cid, "name": body.get("name", ""), "state": "provisioning",
                                     "transitioning": "yes", "rancherKubernetesEngineConfig":
                                         body.get("rancherKubernetesEngineConfig", {}), "created": time.time(),
-                                    "driver": "rancherKubernetesEngine", "version": {"gitVersion": version}}
+                                    "driver": "rancherKubernetesEngine",
+                                    # Rancher reports an RKE1 cluster's upstream version
+                                    "version": {"gitVersion": running_version(version, "rke1")}}
                 st.cluster_nodes[cid] = {}
                 st.unsettled.add(cid)
                 return 201, dict(st.clusters[cid])
@@ -590,8 +593,9 @@ class FakeRancher:
         current = (c.get("version") or {}).get("gitVersion", "")
         if key(version) < key(current):
             return 422, {"type": "error", "code": "Invalid", "message": f"cannot downgrade {current} to {version}"}
-        if version != current:
-            c["version"] = {"gitVersion": version}
+        running = version if v2 is not None else running_version(version, "rke1")
+        if running != current:
+            c["version"] = {"gitVersion": running}
             c["state"], c["transitioning"] = "upgrading", "yes"
             c["ready_at"] = time.time() + st.upgrade_seconds
             st.unsettled.add(cid)
@@ -824,6 +828,13 @@ class FakeRancher:
             node = next((n for n in st.cluster_nodes.get(cid, {}).values() if n["hostname"] == name), None)
             if node is None:
                 return 404, {"kind": "Status", "reason": "NotFound", "code": 404}
+            # optimistic concurrency: a patch naming a resourceVersion applies to that one only
+            want = (patch.get("metadata") or {}).get("resourceVersion")
+            if want is not None and str(want) != str(node.get("rv", 1)):
+                return 409, {"kind": "Status", "reason": "Conflict", "code": 409,
+                             "message": f'Operation cannot be fulfilled on nodes "{name}": the object has been '
+                                        "modified; please apply your changes to the latest version and try again"}
+            node["rv"] = int(node.get("rv", 1)) + 1
             for k, v in ((patch.get("metadata") or {}).get("labels") or {}).items():
                 if v is None:
                     node["labels"].pop(k, None)

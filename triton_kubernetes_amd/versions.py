@@ -163,3 +163,10 @@ def resolve_against(requested: str, offered: Sequence[str]) -> Tuple[str, str]:
 
     best = max(same, key=key)
     return best, f"{requested} is not offered by the server; using {best}"
+
+
+def running_version(release: str, distribution: str) -> str:
+    """The version Rancher (``version.gitVersion``) and the kubelets (``kubeletVersion``)
+    report for a cluster running ``release``: RKE1 reports the upstream Kubernetes version
+    (``v1.30.10`` for ``v1.30.10-rancher1-1``), RKE2 the release itself (``v1.31.6+rke2r1``)."""
+    return re.sub(r"-rancher\d+-\d+$", "", release) if distribution == "rke1" else release

@@ -89,10 +89,37 @@ def _effect(ctx: Context) -> str:
     return match
 
 
+CONFLICT_RETRIES = 5
+
+
 def _reconcile(client, cluster_id: str, node: Dict[str, Any], verdict: Dict[str, Any],
                effect: str = "NoSchedule", fence: bool = True) -> str:
     """Add / remove the health taint (``fence``) and set the labels; returns what changed
-    ('' = nothing)."""
+    ('' = nothing).
+
+    ``spec.taints`` can only be replaced whole, so the patch carries the node's
+    ``metadata.resourceVersion``: a taint another controller added since the node was read
+    (the node-lifecycle controller's ``node.kubernetes.io/unreachable``, another operator's)
+    makes the API server answer 409, and the node is read again and the taints recomputed
+    from it, instead of being silently dropped."""
+    from ..cloud.http import HTTPError
+
+    name = node["metadata"]["name"]
+    for _ in range(CONFLICT_RETRIES):
+        try:
+            return _reconcile_once(client, cluster_id, node, verdict, effect, fence)
+        except HTTPError as exc:
+            if exc.status != 409:
+                raise
+            fresh = next((n for n in client.k8s_nodes(cluster_id) if n["metadata"]["name"] == name), None)
+            if fresh is None:
+                raise TKError(f"node {name} is gone from the cluster") from exc
+            node = fresh
+    raise TKError(f"node {name} kept changing while its health taint was updated; run health cluster again")
+
+
+def _reconcile_once(client, cluster_id: str, node: Dict[str, Any], verdict: Dict[str, Any],
+                    effect: str, fence: bool) -> str:
     name = node["metadata"]["name"]
     want = health_labels(verdict)
     want.update(ras_labels(verdict.get("gpus") or []))
@@ -111,7 +138,11 @@ def _reconcile(client, cluster_id: str, node: Dict[str, Any], verdict: Dict[str,
     same_effect = not unhealthy or [t.get("effect") for t in current] == [effect]
     if tainted == unhealthy and same_effect and all(have.get(k) == v for k, v in want.items()):
         return ""
-    client.patch_node(cluster_id, name, {"metadata": {"labels": want}, "spec": {"taints": taints}})
+    meta: Dict[str, Any] = {"labels": want}
+    rv = (node.get("metadata") or {}).get("resourceVersion")
+    if rv:
+        meta["resourceVersion"] = rv  # a precondition: 409 if the node changed since it was read
+    client.patch_node(cluster_id, name, {"metadata": meta, "spec": {"taints": taints}})
     if tainted and unhealthy and not same_effect:
         return f"tainted {effect}"
     if tainted == unhealthy:

@@ -30,7 +30,7 @@ from ..config.context import Context
 from ..errors import ConfigError, TKError
 from ..rancher.client import wait_until
 from ..utils.trace import span
-from ..versions import distribution_of, k8s_minor, resolve_distribution
+from ..versions import distribution_of, k8s_minor, resolve_distribution, running_version
 from .select import select_cluster, select_manager
 
 
@@ -77,7 +77,10 @@ def upgrade_cluster(ctx: Context, backend: Backend) -> Dict[str, Any]:
     target = client.resolve_k8s_version(requested, dist)
     if getattr(client, "last_version_note", ""):
         ctx.echo(client.last_version_note)
-    if target == current:
+    # what Rancher and the kubelets will report once the cluster runs the target (RKE1: the
+    # upstream version, without -rancherN-N)
+    want = running_version(target, dist)
+    if want == running_version(current, dist):
         ctx.echo(f"cluster '{name}' already runs {current}")
         return {"from": current, "to": target, "changed": False}
     check_upgrade(current, target)
@@ -101,9 +104,9 @@ def upgrade_cluster(ctx: Context, backend: Backend) -> Dict[str, Any]:
         timeout = float(ctx.settings.get_string("wait_timeout") or 3600)
 
         def upgraded() -> bool:
-            if client.cluster_version(cid) != target or client.cluster_state(cid) != "active":
+            if client.cluster_version(cid) != want or client.cluster_state(cid) != "active":
                 return False
-            return all((n.get("status") or {}).get("nodeInfo", {}).get("kubeletVersion") == target
+            return all((n.get("status") or {}).get("nodeInfo", {}).get("kubeletVersion") == want
                        for n in client.k8s_nodes(cid))
 
         with span("upgrade.rollout", cluster=cid):
