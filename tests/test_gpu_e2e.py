@@ -238,7 +238,7 @@ def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch, dist):
     try:
         cfg = {"hostname": "gpu-exec-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
                "gpu_burnin": "quick", "rccl_env": {"NCCL_DEBUG": "WARN"}, "k8s_distribution": dist}
-        server = fake.url if dist == "rke2" else "https://rancher.example"  # loopback: the default allow-list
+        server = fake.url  # loopback: the default allow-list (both distributions' plans are checked)
         cid, token, checksum = fake.registration("exec", dist) if dist == "rke2" else ("", "regtok123", "cafe0123")
         plan = build_host_plan(cfg, server, token, checksum, mi355x=True)
         res = AgentTransport(token="exec-token-123456").run_plan(HostRef("agent+" + url), plan)

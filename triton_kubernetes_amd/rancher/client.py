@@ -317,12 +317,20 @@ class RancherClient:
         Rancher's controllers then upgrade the nodes (control plane first)."""
         if cluster_id.startswith("c-m-"):
             name = str(self.cluster(cluster_id).get("name", ""))
-            obj = self.find_v2_cluster(name)
-            if obj is None:
-                raise TKError(f"no provisioning cluster '{name}' for {cluster_id}")
-            obj.setdefault("spec", {})["kubernetesVersion"] = version
-            self.http.request("PUT", f"/v1/provisioning.cattle.io.clusters/{FLEET_NAMESPACE}/{name}", json_body=obj,
-                              ok=(200,))
+            for attempt in range(5):
+                obj = self.find_v2_cluster(name)
+                if obj is None:
+                    raise TKError(f"no provisioning cluster '{name}' for {cluster_id}")
+                obj.setdefault("spec", {})["kubernetesVersion"] = version
+                try:
+                    # the object carries the resourceVersion it was read at: the controllers
+                    # update it too, so a conflict means re-read and re-apply
+                    self.http.request("PUT", f"/v1/provisioning.cattle.io.clusters/{FLEET_NAMESPACE}/{name}",
+                                      json_body=obj, ok=(200,))
+                    return
+                except HTTPError as exc:
+                    if exc.status != 409 or attempt == 4:
+                        raise
         else:
             c = self.cluster(cluster_id)
             c.setdefault("rancherKubernetesEngineConfig", {})["kubernetesVersion"] = version

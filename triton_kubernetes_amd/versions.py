@@ -18,7 +18,7 @@ The distribution follows from the release string (``v1.31.6+rke2r1`` vs
 ``v1.31.6-rancher1-1``) unless ``k8s_distribution`` says otherwise.  The CLI choices,
 the module defaults and validations, the Rancher client, the DirectExecutor and the
 bench all read these lists, and the fake Rancher server rejects anything else
-(``rancher/fake.py``).
+(``rancher/fake/``).
 
 Rancher ≥2.6 no longer starts with admin/admin: it takes the first admin
 password from ``CATTLE_BOOTSTRAP_PASSWORD`` (or generates a random one).  Every
