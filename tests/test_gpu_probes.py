@@ -420,10 +420,12 @@ def test_full_span_leaves_other_processes_memory_alone(tmp_path):
     holder = tmp_path / "holder.py"
     holder.write_text(
         "import sys, torch\n"
-        "x = torch.arange(16 << 28, dtype=torch.int32, device='cuda')  # 16 GiB\n"
+        "def chunk(k):  # 1 GiB of distinct int32 values (one arange kernel per GiB)\n"
+        "    return torch.arange(k << 28, (k + 1) << 28, dtype=torch.int32, device='cuda')\n"
+        "x = [chunk(k) for k in range(16)]  # 16 GiB\n"
         "torch.cuda.synchronize(); print('held', flush=True)\n"
         "sys.stdin.readline()\n"
-        "ok = bool((x == torch.arange(16 << 28, dtype=torch.int32, device='cuda')).all())\n"
+        "ok = all(bool((x[k] == chunk(k)).all()) for k in range(16))\n"
         "y = torch.empty(1 << 30, dtype=torch.uint8, device='cuda')\n"
         "print('intact' if ok else 'corrupt', flush=True)\n")
     proc = subprocess.Popen([sys.executable, str(holder)], stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
