@@ -11,7 +11,6 @@
 
 import json
 import os
-import ssl
 import subprocess
 import sys
 

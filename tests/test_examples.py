@@ -3,7 +3,6 @@
 import json
 import os
 
-import pytest
 
 from triton_kubernetes_amd.cli.main import run
 

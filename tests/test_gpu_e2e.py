@@ -6,7 +6,6 @@ runs the native GPU steps for real: amd_smi topology labels, quick burn-in
 """
 
 import json
-import sys
 import tempfile
 
 import pytest

@@ -1,6 +1,5 @@
 """Rancher v3 client (S3/S4 semantics) against the fake server; k8s add-on manifests; waiter timeouts."""
 
-import base64
 import hashlib
 import json
 import subprocess

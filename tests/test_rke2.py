@@ -306,7 +306,6 @@ def _https_rancher(tmp_path, cacerts_body: bytes):
     """A TLS server standing in for Rancher's installer endpoints, its certificate for
     127.0.0.1 signed by a CA whose PEM ``/cacerts`` serves (or ``cacerts_body``)."""
     import http.server
-    import ssl
     import threading
 
     from triton_kubernetes_amd.k8s.tls import issue, make_ca

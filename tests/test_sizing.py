@@ -13,7 +13,6 @@ import pytest
 
 from triton_kubernetes_amd import sizing
 from triton_kubernetes_amd.cloud import aws as aws_cloud
-from triton_kubernetes_amd.cloud.fake import FakeCloud
 from triton_kubernetes_amd.errors import ConfigError
 from triton_kubernetes_amd.models import aws
 from triton_kubernetes_amd.terraform import hcl

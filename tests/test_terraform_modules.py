@@ -7,7 +7,6 @@
   values) to syntactically valid bash.
 """
 
-import json
 import os
 import re
 import subprocess

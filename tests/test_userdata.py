@@ -9,7 +9,7 @@ from triton_kubernetes_amd.backend import LocalBackend
 from triton_kubernetes_amd.errors import TKError
 from triton_kubernetes_amd.node.plan import build_host_plan, render_cloud_init
 from triton_kubernetes_amd.rancher.fake import FakeRancher
-from triton_kubernetes_amd.workflows import new_cluster, new_manager, new_node
+from triton_kubernetes_amd.workflows import new_cluster, new_manager
 from triton_kubernetes_amd.workflows.userdata import node_userdata
 
 from helpers import make_ctx, output
