@@ -1,0 +1,212 @@
+"""The node agent's share of the cluster-wide RCCL gate (N2).
+
+A cluster gate is one RCCL communicator over every GPU of the worker tier: rank ``r`` of
+world ``W``, this node holding ranks ``rank_base .. rank_base+ndev-1`` (``ops/rccl.py``
+``GateComm``: grouped ``ncclCommInitRank`` over the node's GPUs in one process).  The
+readiness waiter (``readiness/gate.py``) drives it over the agent API:
+
+* ``POST /v1/rccl-uid`` / ``rccl-prepare`` -- a unique id (kept one ahead, off the
+  bring-up path) and a non-blocking init of this node's ranks, which overlaps the burn-in;
+* ``POST /v1/rccl-gate`` -- the verified all-reduce sweep on those ranks;
+* ``POST /v1/rccl-abort`` -- release them (another member failed): a pending init is
+  aborted and a sweep waiting for peers is canceled at once.
+
+On a one-node cluster the pending communicator spans exactly the node's GPUs, so the
+``rccl_local`` plan step sweeps it and the gate answers from that sweep
+(:meth:`AgentGateMixin._take_node_gate`).  Pending communicators expire after
+``GATE_TTL_S``.  Agents with synthetic GPUs use :class:`_SimGate` unless ``gate_backend``
+is ``rccl`` (the ABI stub, ``ops/csrc/tk_rccl_stub.cpp``).
+"""
+
+import base64
+import secrets
+import time
+from typing import Any, Dict, List, Optional, Tuple
+
+from ..utils.trace import span
+
+class _SimGate:
+    """Stand-in for ops.rccl.GateComm on agents with synthetic GPUs (no RCCL)."""
+
+    def __init__(self, devices: List[int]):
+        self.devices = list(devices)
+
+    def sweep(self, sizes, iters=10, warmup=3, dtype="f32", timeout_s=600.0, async_teardown=True):
+        from ..ops.rccl import SweepResult
+
+        n = len(sizes)
+        return SweepResult(len(self.devices), dtype, list(sizes), [0.0] * n, [0.0] * n, [0.0] * n, [0] * n, 0.0,
+                           {"simulated": 1.0})
+
+    def abort(self) -> None:
+        pass
+
+    def cancel(self) -> None:
+        pass
+
+class AgentGateMixin:
+    """Mixin of :class:`~.agent.NodeAgent`: this node's ranks of cluster RCCL gates."""
+
+    # --- RCCL gate (this node's ranks) ---------------------------------------------------------
+    # Gate communicators pending by uid: started by /v1/rccl-prepare, consumed by
+    # /v1/rccl-gate, released by /v1/rccl-abort, stop(), or expiry.
+    GATE_TTL_S = 900.0
+
+    def _gate_devices(self, ndev: int) -> List[int]:
+        devs = self.devices or [0]
+        if ndev < 1 or ndev > len(devs):
+            raise ValueError(f"gate wants {ndev} GPUs, agent has {len(devs)}")
+        return devs[:ndev]
+
+    def _expire_gates(self) -> None:
+        now = time.time()
+        with self._gate_mu:
+            stale = [k for k, e in self._gates.items() if now - e[1] > self.GATE_TTL_S]
+            gates = [self._gates.pop(k)[0] for k in stale]
+            for k in [k for k, e in self._gate_results.items() if now - e[1] > self.GATE_TTL_S]:
+                del self._gate_results[k]
+        for g in gates:
+            g.abort()
+
+    @property
+    def _sim_gate(self) -> bool:
+        """Synthetic GPUs without the RCCL ABI: the gate is simulated (no library call)."""
+        return self.topology_override is not None and self.gate_backend != "rccl"
+
+    def _make_uid(self) -> bytes:
+        if self._sim_gate:  # synthetic GPUs (tests / dry runs)
+            return secrets.token_bytes(128)
+        from ..ops import rccl
+
+        self._used_rccl = True
+        return rccl.unique_id()
+
+    def _refill_uid(self) -> None:
+        uid = self._make_uid()
+        with self._uid_mu:
+            if self._spare_uid is None:
+                self._spare_uid = uid
+
+    def new_uid(self) -> bytes:
+        """A fresh RCCL unique id (a bootstrap rendezvous address, specific to no cluster):
+        the spare if one is ready, otherwise made now; either way the next spare is made on
+        the agent's pool, off this request."""
+        with self._uid_mu:
+            uid, self._spare_uid = self._spare_uid, None
+        if uid is None:
+            uid = self._make_uid()
+        try:
+            self._pool.submit(self._refill_uid)
+        except RuntimeError:  # pool shut down: the agent is stopping
+            pass
+        return uid
+
+    def rccl_prepare(self, uid: Optional[bytes], world: int, rank_base: int, ndev: int = 1,
+                     max_bytes: int = 0, sizes: Optional[List[int]] = None) -> Dict[str, Any]:
+        """Start this node's share of a cluster communicator (non-blocking init; with
+        ``max_bytes`` the init thread also allocates the sweep buffers).  ``uid`` None: this
+        node hosts the rendezvous — it takes a new unique id and returns it for the others.
+        ``sizes``: the gate's message sizes, so a node that is the whole gate can sweep them
+        in its ``rccl_local`` step (:meth:`_take_node_gate`)."""
+        devs = self._gate_devices(ndev)
+        self._expire_gates()
+        if uid is None:
+            uid = self.new_uid()
+        with span("node.rccl_prepare", node=self.name, rank_base=rank_base, world=world):
+            if self._sim_gate:  # synthetic GPUs (tests / dry runs)
+                gate: Any = _SimGate(devs)
+            else:
+                from ..ops import rccl
+
+                self._used_rccl = True
+                gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False, prealloc_bytes=max_bytes)
+        with self._gate_mu:
+            old = self._gates.pop(uid, None)
+            self._gates[uid] = (gate, time.time(), {"world": world, "rank_base": rank_base,
+                                                    "sizes": [int(x) for x in (sizes or [])]})
+        if old is not None:
+            old[0].abort()
+        return {"ok": True, "ranks": list(range(rank_base, rank_base + len(devs))), "devices": devs,
+                "uid": base64.b64encode(uid).decode()}
+
+    def rccl_abort(self, uid: bytes) -> Dict[str, Any]:
+        """Release this node's ranks of gate ``uid``: a pending communicator is aborted, and a
+        sweep waiting for peers is canceled (it fails at once instead of at its timeout:
+        another member of the gate failed)."""
+        with self._gate_mu:
+            entry = self._gates.pop(uid, None)
+            done = self._gate_results.pop(uid, None)
+            running = self._sweeping.get(uid)
+        if entry is not None:
+            entry[0].abort()
+        if running is not None:
+            running.cancel()
+        return {"ok": True, "aborted": entry is not None or done is not None, "canceled": running is not None}
+
+    def _take_node_gate(self) -> Optional[Tuple[bytes, Any, Dict[str, Any]]]:
+        """A pending gate communicator that spans exactly this node's GPUs (a one-node
+        cluster: world == ndev, every rank here), taken out of the pending set.
+
+        Its all-reduce over the node's GPUs IS the node-level RCCL check, so ``rccl_local``
+        sweeps it instead of initialising a second communicator over the same GPUs on the
+        bring-up path, and the cluster gate later answers from that sweep."""
+        devs = list(self.devices)
+        with self._gate_mu:
+            for uid, (gate, _, meta) in list(self._gates.items()):
+                if (meta.get("world") == len(devs) and meta.get("rank_base") == 0
+                        and list(getattr(gate, "devices", [])) == devs):
+                    del self._gates[uid]
+                    return uid, gate, meta
+        return None
+
+    def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10,
+                  ndev: int = 1, timeout_s: float = 600.0) -> Dict[str, Any]:
+        """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
+        communicator from rccl_prepare when there is one, else a fresh init."""
+        with self._gate_mu:
+            entry = self._gates.pop(uid, None)
+            done = self._gate_results.pop(uid, None)
+        if done is not None:
+            res = done[0]
+            if set(sizes) <= set(res.sizes):  # the rccl_local step swept this communicator
+                idx = [res.sizes.index(x) for x in sizes]
+                pick = lambda xs: [xs[i] for i in idx]  # noqa: E731
+                from ..ops.rccl import SweepResult
+
+                sub = SweepResult(res.world, res.dtype, list(sizes), pick(res.time_us), pick(res.algbw_gbps),
+                                  pick(res.busbw_gbps), pick(res.errors), res.init_ms, dict(res.phase_ms))
+                with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=True,
+                          shared_with="rccl_local"):
+                    out = sub.to_json()
+                out.update(pipelined=True, shared_with="rccl_local",
+                           ranks=list(range(rank, rank + len(self._gate_devices(ndev)))))
+                return out
+            # sizes the local sweep did not cover: the node is the whole gate, so a fresh
+            # communicator under a new id (every rank is here) measures them
+            uid = self._make_uid()
+        pipelined = entry is not None
+        with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=pipelined):
+            if entry is not None:
+                gate = entry[0]
+            elif self._sim_gate:
+                gate = _SimGate(self._gate_devices(ndev))
+            else:
+                from ..ops import rccl
+
+                self._used_rccl = True
+                gate = rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
+            with self._gate_mu:
+                self._sweeping[uid] = gate
+            try:
+                # the communicator teardown is not part of the readiness answer: it is
+                # joined in stop() (or by the next process-exit drain), not here
+                res = gate.sweep(sizes, iters=iters, warmup=2, async_teardown=True, timeout_s=timeout_s)
+            finally:
+                with self._gate_mu:
+                    self._sweeping.pop(uid, None)
+        out = res.to_json()
+        out["pipelined"] = pipelined
+        out["ranks"] = list(range(rank, rank + len(gate.devices)))
+        return out
+
+__all__ = ["AgentGateMixin"]

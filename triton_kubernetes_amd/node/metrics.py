@@ -4,7 +4,7 @@ The reference has no metrics at all ("None beyond stdout"
 MI355X nodes is watched by Prometheus, so each node exposes what its bring-up measured and
 what its GPUs report now, in the text exposition format (version 0.0.4):
 
-* the node agent serves it at ``GET /metrics`` (``node/agent.py``; the agent token as
+* the node agent serves it at ``GET /metrics`` (``node/agent_http.py``; the agent token as
   ``Authorization: Bearer`` -- Prometheus' ``authorization`` scrape setting -- or
   ``X-TK-Agent-Token``);
 * SSH / Terraform nodes: ``amdgpu-topo-labeller --prom`` prints the GPU families

@@ -44,23 +44,13 @@ import uuid
 from typing import Any, Dict, List, Optional, Tuple
 
 from ...versions import running_version
+from ..connect import tunnel_params
 
 Reply = Tuple[int, Any]
 
 
 def _err(code: int, kind: str, message: str = "", **extra: Any) -> Reply:
     return code, dict({"type": "error", "code": kind, "message": message}, **extra)
-
-
-def tunnel_params(hostname: str, roles: Dict[str, bool], labels: Dict[str, str],
-                  capacity: Dict[str, Any], taints: Optional[List[Dict[str, str]]] = None) -> str:
-    """The ``X-API-Tunnel-Params`` header a node agent sends (base64 JSON).  ``capacity``
-    carries the node's GPU devices (``amd.com/gpu``: what a device plugin on it would
-    enumerate), not what the kubelet advertises."""
-    node = {"requestedHostname": hostname, "etcd": roles.get("etcd", False),
-            "controlPlane": roles.get("controlplane", False), "worker": roles.get("worker", False),
-            "labels": labels, "capacity": capacity, "taints": list(taints or [])}
-    return base64.b64encode(json.dumps({"node": node}).encode()).decode()
 
 
 def version_key(v: str) -> Tuple[int, ...]:
