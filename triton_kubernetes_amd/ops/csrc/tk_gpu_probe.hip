@@ -761,11 +761,18 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
 // [1] verify GB/s (last chunk, last pass), [2] bytes tested, [3] device HBM bytes,
 // [4] allocation ms, [5] fill+verify ms, [6] free ms (out must hold 7 doubles).
 // This is the `full` burn-in's memtest (round 1 tested a fixed 64 GiB of 288).
-// Releasing ~300 GB takes ~2.7 s on MI355X (profiles/round2/memtest_span_chunks.jsonl: the
-// fill+verify of all of it takes ~0.1 s).  With async frees on (tkp_set_async_free), the
-// chunks are released by a background thread once the verdict is known, so a node
-// bring-up does not wait for it; tkp_wait_frees() joins them (the agent calls it at stop,
-// and the next span memtest waits for the previous release before allocating).
+// Where its time goes on MI355X (profiles/round4/alloc_probe.jsonl, burnin_full_hip_api_stats.csv):
+// the fill+verify of ~300 GB takes ~0.3 s for 3 passes; the cost is the kernel driver's VRAM
+// clearing.  Freed VRAM is wiped before it is handed out again, at ~35 GB/s per GPU: an
+// allocation served from already-cleared memory takes ~0.3 ms per 16 GiB, one that must
+// wait for clearing ~480 ms per 16 GiB (or for the whole backlog of earlier frees).  A node
+// fresh from boot allocates the span in well under a second; right after another ~300 GB
+// was freed it takes up to ~6 s, and the release this span makes queues ~8 s of clearing
+// that any allocation soon after waits behind.  Nothing in user space changes that, so the
+// release is kept off the bring-up path: with async frees on (tkp_set_async_free), the
+// chunks are released by a background thread once the verdict is known; tkp_wait_frees()
+// joins them (the agent calls it at stop, and the next span memtest waits for the previous
+// release before allocating).
 namespace {
 std::mutex g_free_mu;
 std::condition_variable g_free_cv;
