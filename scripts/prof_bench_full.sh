@@ -5,7 +5,7 @@ set -o pipefail
 ROOT="$GRAFT_REPO_ROOT"
 mkdir -p "$ROOT/gpurun_out/prof_bench_full"
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 600 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv \
+timeout -k 10 600 rocprofv3 --kernel-trace --hip-runtime-trace --memory-copy-trace --output-format csv \
   -d "$ROOT/gpurun_out/prof_bench_full" -o "b_%pid%" -- \
   python3 "$ROOT/bench.py" --steps 1 --warmup 1 --burnin full --warm-steps 0 \
   --report "$ROOT/gpurun_out/prof_bench_full/report.json" > "$ROOT/gpurun_out/prof_bench_full/bench.log" 2>&1

@@ -122,3 +122,97 @@ def test_partitioned_full_memtest_frees_the_arena_before_sizing(scripted, monkey
     res = probe.run_burnin(0, "full", probe.Thresholds.for_partition("cpx", "nps2"))
     assert res.ok, res.failures
     assert [o[0] for o in order] == ["release", "free", "span"]
+
+
+@pytest.fixture
+def span_child(tmp_path, monkeypatch):
+    """A stand-in gpu-burnin: prints the verdict line its argv asks for, then 'releases' for
+    ``FAKE_RELEASE_S`` before it exits (what the real one's hipFree + driver clearing take)."""
+    import stat
+    import sys
+
+    exe = tmp_path / "gpu-burnin"
+    exe.write_text(f"""#!{sys.executable}
+import json, os, sys, time
+a = sys.argv
+open(os.environ["FAKE_SPAN_ARGV"], "a").write(" ".join(a[1:]) + "\\n")
+mode = os.environ.get("FAKE_SPAN_MODE", "ok")
+if mode == "silent":
+    sys.exit(3)
+if mode == "error":
+    print(json.dumps({{"ok": False, "error": "hipMalloc: out of memory"}}), flush=True)
+    sys.exit(2)
+n = int(a[a.index("--span-bytes") + 1]) or (300 << 30)
+print(json.dumps({{"ok": True, "errors": 0, "verify_gbps": 6100.0, "bytes": n, "hbm_bytes": 309 << 30,
+                  "alloc_ms": 412.0, "test_ms": 300.0}}), flush=True)
+time.sleep(float(os.environ.get("FAKE_RELEASE_S", "0")))
+""")
+    exe.chmod(exe.stat().st_mode | stat.S_IEXEC)
+    argv_log = tmp_path / "argv.log"
+    monkeypatch.setenv("FAKE_SPAN_ARGV", str(argv_log))
+    monkeypatch.setattr(probe, "BURNIN_EXE", str(exe))
+    released = []
+    monkeypatch.setattr(probe, "release_scratch", lambda dev=None: released.append(dev) or 0)
+
+    class _Lib:
+        def tkp_wait_frees(self):
+            return 0
+
+    monkeypatch.setattr(probe, "_lib", lambda: _Lib())
+    return argv_log, released
+
+
+def test_span_child_reports_before_it_releases(span_child, monkeypatch):
+    """The agent's full memtest runs in a gpu-burnin child: the verdict comes back as soon as
+    the child prints it; the release happens in the child, and wait_frees (and the same
+    device's next span) wait for it to exit."""
+    import time
+
+    argv_log, released = span_child
+    monkeypatch.setenv("FAKE_RELEASE_S", "1.5")
+    t0 = time.monotonic()
+    res = probe.memtest_span_process(3, 0, headroom=4 << 30, passes=3)
+    assert time.monotonic() - t0 < 1.2  # did not wait for the release
+    assert res["errors"] == 0 and res["bytes"] == 300 << 30 and res["free_ms"] == 0.0
+    assert released == [3]  # this process's arena is part of the span
+    assert argv_log.read_text().split() == ["--memtest-span", "--device", "3", "--span-bytes", "0",
+                                            "--span-headroom", str(4 << 30), "--span-passes", "3"]
+    assert [d for d, _ in probe._span_children] == [3]
+    probe.wait_frees()
+    assert time.monotonic() - t0 >= 1.4 and probe._span_children == []
+
+
+def test_span_child_waits_only_for_its_own_device(span_child, monkeypatch):
+    """Concurrent spans on other devices (every GPU of a node burns in at once) do not wait
+    for each other; a device's next span waits for its previous one's release."""
+    import time
+
+    monkeypatch.setenv("FAKE_RELEASE_S", "1.0")
+    t0 = time.monotonic()
+    probe.memtest_span_process(0, 1 << 30)
+    probe.memtest_span_process(1, 1 << 30)
+    assert time.monotonic() - t0 < 0.9
+    probe.memtest_span_process(0, 1 << 30)  # waits for device 0's first child
+    assert time.monotonic() - t0 >= 1.0
+    probe.wait_frees()
+
+
+def test_span_child_failures_are_errors(span_child, monkeypatch):
+    monkeypatch.setenv("FAKE_SPAN_MODE", "error")
+    with pytest.raises(probe.ProbeError, match="out of memory"):
+        probe.memtest_span_process(0)
+    monkeypatch.setenv("FAKE_SPAN_MODE", "silent")
+    with pytest.raises(probe.ProbeError, match="exited 3 without a verdict"):
+        probe.memtest_span_process(0)
+    probe.wait_frees()
+
+
+def test_full_burnin_uses_the_span_child_when_enabled(scripted, span_child, monkeypatch):
+    monkeypatch.setattr(probe, "memtest_span", lambda *a, **k: pytest.fail("in-process span used"))
+    probe.set_span_process(True)
+    try:
+        res = probe.run_burnin(0, "full")
+    finally:
+        probe.set_span_process(False)
+        probe.wait_frees()
+    assert res.ok and res.memtest["bytes"] == 300 << 30 and "process_ms" in res.memtest

@@ -461,3 +461,24 @@ def test_full_span_memtests_the_burnin_arena_too(probe):
         probe.release_scratch()
         probe.set_scratch_cache(False)
         probe.wait_frees()
+
+
+def test_full_span_in_a_child_process(probe):
+    """The agent's full memtest runs in ``gpu-burnin --memtest-span``: the verdict comes back
+    while the child still holds the span; once it has exited the HBM is free again, and
+    this process's HIP calls were never queued behind its frees."""
+    probe.wait_frees()
+    before = probe.free_bytes(0)
+    t0 = time.perf_counter()
+    res = probe.memtest_span_process(0, 0, headroom=4 << 30, passes=1, release_arena=False)
+    verdict_s = time.perf_counter() - t0
+    t1 = time.perf_counter()
+    probe.memtest(0, 256 << 20, 1)  # this process's GPU work right after the verdict
+    own_s = time.perf_counter() - t1
+    probe.wait_frees()
+    after = probe.free_bytes(0)
+    print(json.dumps(dict(res, verdict_s=round(verdict_s, 3), own_memtest_s=round(own_s, 3),
+                          free_before_gib=before / 2 ** 30, free_after_gib=after / 2 ** 30)))
+    assert res["errors"] == 0
+    assert before - (5 << 30) <= res["bytes"] <= before - (3 << 30)
+    assert after >= before - (1 << 30)

@@ -227,6 +227,9 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
         # the full burn-in's ~300 GB memtest memory is released off the bring-up path
         probe.set_async_free(True)
+        # ... and the full memtest's ~300 GB is held and released by a gpu-burnin child, so no
+        # hipFree of it blocks this process's other HIP calls (ops/probe.py:memtest_span_process)
+        probe.set_span_process(os.environ.get("TK_SPAN_PROCESS", "1") != "0")
         # burn-in arena: resident for the agent's lifetime, released after an idle period
         if os.environ.get("TK_PROBE_SCRATCH_CACHE", "1") != "0":
             level = os.environ.get("TK_PROBE_SCRATCH_LEVEL", "quick")

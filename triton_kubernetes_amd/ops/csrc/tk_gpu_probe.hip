@@ -782,6 +782,15 @@ std::atomic<int> g_async_free{0};
 
 extern "C" void tkp_set_async_free(int on) { g_async_free.store(on); }
 
+// gpu-burnin --memtest-span (a child of a long-lived agent): the span's chunks are kept past
+// the call, so the verdict is printed before any of them is released; the release (and the
+// driver's clearing it queues) then happens in that short-lived process, never under the
+// agent's HIP runtime, whose other calls would wait behind each hipFree.
+namespace {
+std::vector<void*> g_kept_chunks;
+int g_keep_span = 0;
+}  // namespace
+
 extern "C" int tkp_wait_frees() {
   std::unique_lock<std::mutex> lk(g_free_mu);
   g_free_cv.wait(lk, [] { return g_frees_pending == 0; });
@@ -893,6 +902,12 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
   out[1] = ms > 0.f ? (double)sizes.back() / (ms * 1e-3) / 1e9 : 0.0;
   out[2] = (double)tested;
   out[5] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_test).count();
+  if (g_keep_span) {
+    g_kept_chunks.insert(g_kept_chunks.end(), hold.chunks.begin(), hold.chunks.end());
+    hold.chunks.clear();
+    out[6] = 0.0;
+    return 0;
+  }
   if (g_async_free.load()) {
     {
       std::lock_guard<std::mutex> lk(g_free_mu);
@@ -1143,6 +1158,8 @@ extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, 
 //   gpu-burnin [--all | --device N] [--level quick|full]   (default full)
 //              [--min-read-gbps X] [--min-bf16-tflops Y] [--min-fp8-tflops Z] [--min-gemm-tflops G]
 //              [--min-gemm-fp8-tflops F]
+//   gpu-burnin --memtest-span --device N [--span-bytes B] [--span-headroom H] [--span-passes P]
+//              (the full memtest alone: one JSON line, printed before its memory is released)
 // Prints one JSON document; exit 1 when any GPU misses a threshold, the memtest finds a
 // mismatch or a GEMM fails its row/column checksums (thresholds: 60 % of 6.3 TB/s
 // achievable HBM read, 55 % of the 2.5 / 5 PF dense bf16 / fp8 MFMA peaks, bf16 / fp8 GEMMs
@@ -1228,6 +1245,9 @@ int main(int argc, char** argv) {
   double min_link_gbps = 38.0;  // = ops/probe.py:DEFAULT_MIN_LINK_GBPS (half a link's one-way 76.8 GB/s)
   int link_mode = 1;            // --p2p-method kernel-read (default) | sdma-copy
   const char* cpart = "spx";    // --compute-partition spx|dpx|qpx|cpx
+  int span_mode = 0;            // --memtest-span [--span-bytes B] [--span-headroom H] [--span-passes P]
+  size_t span_bytes = 0, span_headroom = 4ull << 30;
+  int span_passes = 3;
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
   for (int i = 1; i < argc; ++i) {
@@ -1246,8 +1266,27 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--p2p-method") && i + 1 < argc) link_mode = strcmp(argv[++i], "sdma-copy") ? 1 : 0;
     else if (!strcmp(argv[i], "--compute-partition") && i + 1 < argc) cpart = argv[++i];
     else if (!strcmp(argv[i], "--memory-partition") && i + 1 < argc) ++i;  // pools are only shared concurrently
+    else if (!strcmp(argv[i], "--memtest-span")) span_mode = 1;
+    else if (!strcmp(argv[i], "--span-bytes") && i + 1 < argc) span_bytes = strtoull(argv[++i], nullptr, 10);
+    else if (!strcmp(argv[i], "--span-headroom") && i + 1 < argc) span_headroom = strtoull(argv[++i], nullptr, 10);
+    else if (!strcmp(argv[i], "--span-passes") && i + 1 < argc) span_passes = atoi(argv[++i]);
   }
   if (p2p) return p2p_main(labels_path, min_link_frac, min_link_gbps, link_mode);
+  if (span_mode) {
+    // --memtest-span: the full memtest alone, for ops/probe.py:memtest_span_process.  One
+    // JSON line as soon as the verdict is known; the chunks are released after it.
+    double mt[7] = {0, 0, 0, 0, 0, 0, 0};
+    g_keep_span = 1;
+    const int rc = tkp_memtest_span(dev, span_bytes, 16ull << 30, span_headroom, span_passes, mt);
+    if (rc != 0) printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    else
+      printf("{\"ok\":true,\"errors\":%.0f,\"verify_gbps\":%.1f,\"bytes\":%.0f,\"hbm_bytes\":%.0f,"
+             "\"alloc_ms\":%.1f,\"test_ms\":%.1f}\n", mt[0], mt[1], mt[2], mt[3], mt[4], mt[5]);
+    fflush(stdout);
+    for (void* p : g_kept_chunks) (void)hipFree(p);
+    g_kept_chunks.clear();
+    return rc != 0 ? 2 : (mt[0] != 0.0 ? 1 : 0);
+  }
   // a compute partition has 1/k of the chip's CUs (node/partition.py:compute_share): the
   // throughput floors scale with it; the devices run one after another, so each may hold
   // its memory pool alone for the memtest

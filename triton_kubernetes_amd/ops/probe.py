@@ -8,11 +8,17 @@ fails a threshold or the memtest marks the node not-ready.
 """
 
 import ctypes
+import json
+import os
+import selectors
+import subprocess
+import threading
+import time
 from dataclasses import asdict, dataclass, field
 from typing import Any, Dict, List, Optional, Sequence
 
 from ..utils.trace import span
-from .native import load
+from .native import LIB_DIR, load
 
 # MI355X reference figures (dense; never the 2:1-sparsity marketing numbers)
 MI355X_HBM_ACHIEVABLE_GBPS = 6300.0
@@ -182,8 +188,91 @@ def set_async_free(on: bool) -> None:
 
 
 def wait_frees() -> None:
-    """Join pending background releases of span-memtest memory."""
+    """Join pending background releases of span-memtest memory (in this process, and the
+    ``gpu-burnin --memtest-span`` children still releasing theirs)."""
     _lib().tkp_wait_frees()
+    _wait_span_children()
+
+
+# --- the full memtest in a short-lived child process (long-lived agents) ----------------------
+# A full memtest holds ~300 GB.  Releasing it costs the kernel driver's VRAM clearing (~35 GB/s
+# per GPU, profiles/round4/alloc_probe.jsonl), and while a hipFree of a 16 GiB chunk waits for
+# that (~0.5 s), every other HIP call of the same process waits too: in an agent, the gate's
+# sweep and the plan's later GPU steps stalled for seconds behind the background release
+# (profiles/round4/README.md).  So an agent runs the span in ``gpu-burnin --memtest-span``: the
+# child prints its verdict as soon as it is known and releases the memory itself, outside the
+# agent's HIP runtime.  The next span (and ``wait_frees``) waits for it to exit.
+BURNIN_EXE = os.path.join(LIB_DIR, "gpu-burnin")
+_SPAN_PROCESS = False
+_span_children: List[Any] = []  # (device, child): children whose span may still be releasing
+_span_mu = threading.Lock()
+
+
+def set_span_process(on: bool) -> None:
+    """Run the full memtest (``run_burnin`` level ``full``) in a child process."""
+    global _SPAN_PROCESS
+    _SPAN_PROCESS = bool(on)
+
+
+def _wait_span_children(dev: Optional[int] = None) -> None:
+    """Wait for the span children (of ``dev`` only, when given) to exit."""
+    with _span_mu:
+        children = [c for c in _span_children if dev is None or c[0] == dev]
+    for _, proc in children:
+        proc.wait()
+    with _span_mu:
+        for c in children:
+            if c in _span_children:
+                _span_children.remove(c)
+
+
+def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, passes: int = 1,
+                         timeout: float = 900.0, release_arena: bool = True) -> Dict[str, float]:
+    """:func:`memtest_span` in a ``gpu-burnin --memtest-span`` child: returns as soon as the
+    child reports its verdict; the child releases the span afterwards (joined by
+    :func:`wait_frees`).  This process's burn-in arena is freed first, so its HBM is tested."""
+    if release_arena:
+        release_scratch(dev)
+    _lib().tkp_wait_frees()
+    _wait_span_children(dev)  # this device's previous span is released before this one allocates
+    argv = [BURNIN_EXE, "--memtest-span", "--device", str(int(dev)), "--span-bytes", str(int(nbytes)),
+            "--span-headroom", str(int(headroom)), "--span-passes", str(int(passes))]
+    t0 = time.perf_counter()
+    proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                            start_new_session=True)
+    with _span_mu:
+        _span_children.append((dev, proc))
+    line = ""
+    sel = selectors.DefaultSelector()
+    sel.register(proc.stdout, selectors.EVENT_READ)
+    try:
+        deadline = time.monotonic() + timeout
+        while not line:
+            left = deadline - time.monotonic()
+            if left <= 0 or not sel.select(timeout=left):
+                proc.kill()
+                raise ProbeError(f"memtest_span: gpu-burnin --memtest-span gave no verdict within {timeout:.0f} s")
+            line = proc.stdout.readline()
+            if not line and proc.poll() is not None:
+                raise ProbeError(f"memtest_span: gpu-burnin --memtest-span exited {proc.returncode} without a verdict")
+    finally:
+        sel.close()
+    try:
+        doc = json.loads(line)
+    except ValueError as exc:
+        proc.kill()
+        raise ProbeError(f"memtest_span: unreadable verdict {line[:200]!r}") from exc
+    if not doc.get("ok"):
+        raise ProbeError(f"memtest_span: {doc.get('error', 'failed')}")
+    return {"errors": int(doc["errors"]), "verify_gbps": float(doc["verify_gbps"]), "bytes": int(doc["bytes"]),
+            "hbm_bytes": int(doc["hbm_bytes"]), "alloc_ms": float(doc["alloc_ms"]), "test_ms": float(doc["test_ms"]),
+            "free_ms": 0.0, "process_ms": round((time.perf_counter() - t0) * 1e3, 1)}
+
+
+def _span(dev: int, nbytes: int, passes: int) -> Dict[str, float]:
+    if _SPAN_PROCESS:
+        return memtest_span_process(dev, nbytes, passes=passes)
+    return memtest_span(dev, nbytes, passes=passes)
 
 
 def memtest_selfcheck(dev: int, nbytes: int, corrupt: int) -> int:
@@ -380,9 +469,9 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
             release_scratch(dev)
             headroom = max(512 << 20, int((4 << 30) * th.mem_share))
             span_bytes = max(1 << 30, int(free_bytes(dev) * th.mem_share) - headroom)
-            res.memtest = memtest_span(dev, span_bytes, passes=mt_passes)
+            res.memtest = _span(dev, span_bytes, mt_passes)
         else:
-            res.memtest = memtest_span(dev, 0, passes=mt_passes)
+            res.memtest = _span(dev, 0, mt_passes)
     if res.memtest["errors"]:
         res.failures.append(f"memtest: {res.memtest['errors']} mismatching words")
     return res
