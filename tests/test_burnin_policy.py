@@ -176,7 +176,8 @@ def test_span_child_reports_before_it_releases(span_child, monkeypatch):
     assert res["errors"] == 0 and res["bytes"] == 300 << 30 and res["free_ms"] == 0.0
     assert released == [3]  # this process's arena is part of the span
     assert argv_log.read_text().split() == ["--memtest-span", "--device", "3", "--span-bytes", "0",
-                                            "--span-headroom", str(4 << 30), "--span-passes", "3"]
+                                            "--span-headroom", str(4 << 30), "--span-passes", "3",
+                                            "--span-chunk", str(probe.SPAN_CHILD_CHUNK)]
     assert [d for d, _ in probe._span_children] == [3]
     probe.wait_frees()
     assert time.monotonic() - t0 >= 1.4 and probe._span_children == []

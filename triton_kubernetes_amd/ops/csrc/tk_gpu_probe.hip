@@ -1158,7 +1158,7 @@ extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, 
 //   gpu-burnin [--all | --device N] [--level quick|full]   (default full)
 //              [--min-read-gbps X] [--min-bf16-tflops Y] [--min-fp8-tflops Z] [--min-gemm-tflops G]
 //              [--min-gemm-fp8-tflops F]
-//   gpu-burnin --memtest-span --device N [--span-bytes B] [--span-headroom H] [--span-passes P]
+//   gpu-burnin --memtest-span --device N [--span-bytes B] [--span-headroom H] [--span-passes P] [--span-chunk C]
 //              (the full memtest alone: one JSON line, printed before its memory is released)
 // Prints one JSON document; exit 1 when any GPU misses a threshold, the memtest finds a
 // mismatch or a GEMM fails its row/column checksums (thresholds: 60 % of 6.3 TB/s
@@ -1246,7 +1246,7 @@ int main(int argc, char** argv) {
   int link_mode = 1;            // --p2p-method kernel-read (default) | sdma-copy
   const char* cpart = "spx";    // --compute-partition spx|dpx|qpx|cpx
   int span_mode = 0;            // --memtest-span [--span-bytes B] [--span-headroom H] [--span-passes P]
-  size_t span_bytes = 0, span_headroom = 4ull << 30;
+  size_t span_bytes = 0, span_headroom = 4ull << 30, span_chunk = 16ull << 30;
   int span_passes = 3;
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
@@ -1270,6 +1270,7 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--span-bytes") && i + 1 < argc) span_bytes = strtoull(argv[++i], nullptr, 10);
     else if (!strcmp(argv[i], "--span-headroom") && i + 1 < argc) span_headroom = strtoull(argv[++i], nullptr, 10);
     else if (!strcmp(argv[i], "--span-passes") && i + 1 < argc) span_passes = atoi(argv[++i]);
+    else if (!strcmp(argv[i], "--span-chunk") && i + 1 < argc) span_chunk = strtoull(argv[++i], nullptr, 10);
   }
   if (p2p) return p2p_main(labels_path, min_link_frac, min_link_gbps, link_mode);
   if (span_mode) {
@@ -1277,7 +1278,7 @@ int main(int argc, char** argv) {
     // JSON line as soon as the verdict is known; the chunks are released after it.
     double mt[7] = {0, 0, 0, 0, 0, 0, 0};
     g_keep_span = 1;
-    const int rc = tkp_memtest_span(dev, span_bytes, 16ull << 30, span_headroom, span_passes, mt);
+    const int rc = tkp_memtest_span(dev, span_bytes, span_chunk, span_headroom, span_passes, mt);
     if (rc != 0) printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
     else
       printf("{\"ok\":true,\"errors\":%.0f,\"verify_gbps\":%.1f,\"bytes\":%.0f,\"hbm_bytes\":%.0f,"

@@ -201,8 +201,13 @@ def wait_frees() -> None:
 # sweep and the plan's later GPU steps stalled for seconds behind the background release
 # (profiles/round4/README.md).  So an agent runs the span in ``gpu-burnin --memtest-span``: the
 # child prints its verdict as soon as it is known and releases the memory itself, outside the
-# agent's HIP runtime.  The next span (and ``wait_frees``) waits for it to exit.
+# agent's HIP runtime.  The next span (and ``wait_frees``) waits for it to exit.  The child
+# holds the span in 1 GiB chunks: the release then blocks other GPU users (the driver
+# serialises their copies and frees behind each chunk's clearing, across processes) for
+# ~30 ms at a time instead of ~0.5 s (profiles/round4/span_chunk_ab.jsonl: the gate's sweep
+# after a full burn-in 4-6 ms with 1 GiB chunks, up to 0.5 s with 16 GiB ones).
 BURNIN_EXE = os.path.join(LIB_DIR, "gpu-burnin")
+SPAN_CHILD_CHUNK = int(float(os.environ.get("TK_SPAN_CHUNK_GIB", "1")) * (1 << 30))
 _SPAN_PROCESS = False
 _span_children: List[Any] = []  # (device, child): children whose span may still be releasing
 _span_mu = threading.Lock()
@@ -227,7 +232,7 @@ def _wait_span_children(dev: Optional[int] = None) -> None:
 
 
 def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, passes: int = 1,
-                         timeout: float = 900.0, release_arena: bool = True) -> Dict[str, float]:
+                         timeout: float = 900.0, release_arena: bool = True, chunk: int = 0) -> Dict[str, float]:
     """:func:`memtest_span` in a ``gpu-burnin --memtest-span`` child: returns as soon as the
     child reports its verdict; the child releases the span afterwards (joined by
     :func:`wait_frees`).  This process's burn-in arena is freed first, so its HBM is tested."""
@@ -236,7 +241,8 @@ def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, pas
     _lib().tkp_wait_frees()
     _wait_span_children(dev)  # this device's previous span is released before this one allocates
     argv = [BURNIN_EXE, "--memtest-span", "--device", str(int(dev)), "--span-bytes", str(int(nbytes)),
-            "--span-headroom", str(int(headroom)), "--span-passes", str(int(passes))]
+            "--span-headroom", str(int(headroom)), "--span-passes", str(int(passes)),
+            "--span-chunk", str(int(chunk or SPAN_CHILD_CHUNK))]
     t0 = time.perf_counter()
     proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
                             start_new_session=True)
