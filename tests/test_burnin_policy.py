@@ -217,3 +217,12 @@ def test_full_burnin_uses_the_span_child_when_enabled(scripted, span_child, monk
         probe.set_span_process(False)
         probe.wait_frees()
     assert res.ok and res.memtest["bytes"] == 300 << 30 and "process_ms" in res.memtest
+
+
+def test_a_stuck_span_child_is_killed(span_child, monkeypatch):
+    monkeypatch.setenv("FAKE_RELEASE_S", "60")
+    monkeypatch.setattr(probe, "SPAN_RELEASE_TIMEOUT_S", 0.5)
+    probe.memtest_span_process(0, 1 << 30)
+    (_, proc), = probe._span_children
+    probe.wait_frees()
+    assert proc.returncode is not None and proc.returncode < 0 and probe._span_children == []

@@ -208,6 +208,7 @@ def wait_frees() -> None:
 # after a full burn-in 4-6 ms with 1 GiB chunks, up to 0.5 s with 16 GiB ones).
 BURNIN_EXE = os.path.join(LIB_DIR, "gpu-burnin")
 SPAN_CHILD_CHUNK = int(float(os.environ.get("TK_SPAN_CHUNK_GIB", "1")) * (1 << 30))
+SPAN_RELEASE_TIMEOUT_S = 600.0
 _SPAN_PROCESS = False
 _span_children: List[Any] = []  # (device, child): children whose span may still be releasing
 _span_mu = threading.Lock()
@@ -224,7 +225,11 @@ def _wait_span_children(dev: Optional[int] = None) -> None:
     with _span_mu:
         children = [c for c in _span_children if dev is None or c[0] == dev]
     for _, proc in children:
-        proc.wait()
+        try:  # a release takes seconds; a child stuck far longer than that is killed
+            proc.wait(timeout=SPAN_RELEASE_TIMEOUT_S)
+        except subprocess.TimeoutExpired:
+            proc.kill()
+            proc.wait()
     with _span_mu:
         for c in children:
             if c in _span_children:
