@@ -1289,8 +1289,7 @@ int main(int argc, char** argv) {
     return rc != 0 ? 2 : (mt[0] != 0.0 ? 1 : 0);
   }
   // a compute partition has 1/k of the chip's CUs (node/partition.py:compute_share): the
-  // throughput floors scale with it; the devices run one after another, so each may hold
-  // its memory pool alone for the memtest
+  // throughput floors scale with it
   const int parts = !strcmp(cpart, "cpx") ? 8 : !strcmp(cpart, "qpx") ? 4 : !strcmp(cpart, "dpx") ? 2 : 1;
   min_read /= parts;
   min_bf16 /= parts;
@@ -1311,59 +1310,81 @@ int main(int argc, char** argv) {
   std::vector<int> devs;
   if (all) for (int d = 0; d < n; ++d) devs.push_back(d);
   else devs.push_back(dev);
-  bool ok_all = true;
-  double min_tested = -1.0, min_frac = -1.0;
-  printf("{\"level\":\"%s\",\"gpus\":[", level);
-  for (size_t k = 0; k < devs.size(); ++k) {
-    const int d = devs[k];
+  // One device's burn-in, on the calling thread (every probe pins its device per thread;
+  // error text is per thread too).
+  struct DevResult {
     struct tkp_device_info info;
-    memset(&info, 0, sizeof(info));
-    double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[7] = {0, 0, 0, 0, 0, 0, 0}, gm[7] = {0, 0, 0, 0, -1, -1, 0},
-           gm8[7] = {0, 0, 0, 0, -1, -1, 0};
+    double hbm[3], bf16[2], fp8[2], mt[7], gm[7], gm8[7];
+    int remeasured;
+    bool ok, pass, gemm_ok, gemm8_ok;
+    char err[512];
+  };
+  auto run_device = [&](int d, DevResult& r) {
+    memset(&r, 0, sizeof(r));
+    for (int i = 4; i < 6; ++i) r.gm[i] = r.gm8[i] = -1;
     // A throughput gate that reads below its floor is measured again (best of up to 3 runs,
     // as ops/probe.py:run_burnin): a short kernel that overlapped other GPU work reads low
     // once, a slow GPU every time.  A checksum mismatch in ANY GEMM run fails the GPU.
-    int remeasured = 0;
     bool gemm_bad = false, gemm8_bad = false;
     auto measure = [&](auto&& run, double* out, int n_out, double floor, bool* bad) -> bool {
       if (run(out) != 0) return false;
       if (bad) *bad = *bad || out[2] != 0.0 || out[3] != 0.0;
-      for (int r = 0; r < 2 && out[0] < floor; ++r) {
+      for (int k = 0; k < 2 && out[0] < floor; ++k) {
         double again[7] = {0, 0, 0, 0, -1, -1, 0};
         if (run(again) != 0) return false;
-        ++remeasured;
+        ++r.remeasured;
         if (bad) *bad = *bad || again[2] != 0.0 || again[3] != 0.0;
         if (again[0] > out[0]) memcpy(out, again, sizeof(double) * (size_t)n_out);
       }
       return true;
     };
-    bool ok = tkp_device_info(d, &info) == 0 &&
-              measure([&](double* o) { return tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, o); }, hbm, 3, min_read,
-                      nullptr) &&
-              measure([&](double* o) { return tkp_mfma_peak(d, 0, mfma_iters, 3, 2, o); }, bf16, 2, min_bf16,
-                      nullptr) &&
-              measure([&](double* o) { return tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, o); }, fp8, 2, min_fp8,
-                      nullptr) &&
-              measure([&](double* o) { return tkg_screen(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, gm, 7,
-                      min_gemm, &gemm_bad) &&
-              measure([&](double* o) { return tkg_screen_fp8(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, gm8,
-                      7, min_gemm8, &gemm8_bad) &&
-              tkp_memtest_span(d, mt_bytes, 16ull << 30, 4ull << 30, full ? 3 : 1, mt) == 0;
-    if (!ok && tkg_last_error()[0] && !g_err[0]) snprintf(g_err, sizeof(g_err), "%s", tkg_last_error());
-    const bool gemm_ok = !gemm_bad, gemm8_ok = !gemm8_bad;
-    const bool pass = ok && strncmp(info.arch, "gfx950", 6) == 0 && hbm[0] >= min_read && bf16[0] >= min_bf16 &&
-                      fp8[0] >= min_fp8 && gemm_ok && gm[0] >= min_gemm && gemm8_ok && gm8[0] >= min_gemm8 &&
-                      mt[0] == 0.0;
-    ok_all = ok_all && pass;
-    if (min_tested < 0 || mt[2] < min_tested) min_tested = mt[2];
-    if (mt[3] > 0 && (min_frac < 0 || mt[2] / mt[3] < min_frac)) min_frac = mt[2] / mt[3];
+    r.ok = tkp_device_info(d, &r.info) == 0 &&
+           measure([&](double* o) { return tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, o); }, r.hbm, 3, min_read,
+                   nullptr) &&
+           measure([&](double* o) { return tkp_mfma_peak(d, 0, mfma_iters, 3, 2, o); }, r.bf16, 2, min_bf16,
+                   nullptr) &&
+           measure([&](double* o) { return tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, o); }, r.fp8, 2, min_fp8,
+                   nullptr) &&
+           measure([&](double* o) { return tkg_screen(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, r.gm, 7,
+                   min_gemm, &gemm_bad) &&
+           measure([&](double* o) { return tkg_screen_fp8(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, r.gm8,
+                   7, min_gemm8, &gemm8_bad) &&
+           tkp_memtest_span(d, mt_bytes, 16ull << 30, 4ull << 30, full ? 3 : 1, r.mt) == 0;
+    snprintf(r.err, sizeof(r.err), "%s", g_err[0] ? g_err : tkg_last_error());
+    r.gemm_ok = !gemm_bad;
+    r.gemm8_ok = !gemm8_bad;
+    r.pass = r.ok && strncmp(r.info.arch, "gfx950", 6) == 0 && r.hbm[0] >= min_read && r.bf16[0] >= min_bf16 &&
+             r.fp8[0] >= min_fp8 && r.gemm_ok && r.gm[0] >= min_gemm && r.gemm8_ok && r.gm8[0] >= min_gemm8 &&
+             r.mt[0] == 0.0;
+  };
+  // Whole GPUs (SPX) have their own HBM: every device burns in at once, one thread each, as
+  // the node agent does (an 8-GPU node in about one GPU's time).  Partitions of one chip
+  // share its memory pools: one after another, so each may hold its pool alone.
+  std::vector<DevResult> results(devs.size());
+  if (parts == 1 && devs.size() > 1) {
+    std::vector<std::thread> workers;
+    for (size_t k = 0; k < devs.size(); ++k)
+      workers.emplace_back([&, k] { run_device(devs[k], results[k]); });
+    for (auto& t : workers) t.join();
+  } else {
+    for (size_t k = 0; k < devs.size(); ++k) run_device(devs[k], results[k]);
+  }
+  bool ok_all = true;
+  double min_tested = -1.0, min_frac = -1.0;
+  printf("{\"level\":\"%s\",\"gpus\":[", level);
+  for (size_t k = 0; k < devs.size(); ++k) {
+    const DevResult& r = results[k];
+    ok_all = ok_all && r.pass;
+    if (min_tested < 0 || r.mt[2] < min_tested) min_tested = r.mt[2];
+    if (r.mt[3] > 0 && (min_frac < 0 || r.mt[2] / r.mt[3] < min_frac)) min_frac = r.mt[2] / r.mt[3];
     printf("%s{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"read_gbps\":%.1f,\"write_gbps\":%.1f,\"copy_gbps\":%.1f,"
            "\"bf16_tflops\":%.1f,\"fp8_tflops\":%.1f,\"gemm_tflops\":%.1f,\"gemm_checksum_ok\":%s,"
            "\"gemm_fp8_tflops\":%.1f,\"gemm_fp8_checksum_ok\":%s,"
            "\"memtest_errors\":%.0f,\"memtest_bytes\":%.0f,\"hbm_bytes\":%.0f,\"remeasured\":%d,\"ok\":%s%s%s%s}",
-           k ? "," : "", d, info.arch, info.compute_units, hbm[0], hbm[1], hbm[2], bf16[0], fp8[0], gm[0],
-           gemm_ok ? "true" : "false", gm8[0], gemm8_ok ? "true" : "false", mt[0], mt[2], mt[3], remeasured,
-           pass ? "true" : "false", ok ? "" : ",\"error\":\"", ok ? "" : g_err, ok ? "" : "\"");
+           k ? "," : "", devs[k], r.info.arch, r.info.compute_units, r.hbm[0], r.hbm[1], r.hbm[2], r.bf16[0],
+           r.fp8[0], r.gm[0], r.gemm_ok ? "true" : "false", r.gm8[0], r.gemm8_ok ? "true" : "false", r.mt[0],
+           r.mt[2], r.mt[3], r.remeasured, r.pass ? "true" : "false", r.ok ? "" : ",\"error\":\"",
+           r.ok ? "" : r.err, r.ok ? "" : "\"");
   }
   printf("],\"ok\":%s}\n", ok_all ? "true" : "false");
   if (labels_path) {
