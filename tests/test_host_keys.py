@@ -131,6 +131,11 @@ def test_store_merge_and_forget(tmp_path):
     text = be.read_blob("m", hostkeys.BLOB).decode()
     assert hostkeys.keys_for(text, "h1") == ["ssh-ed25519 AAAA1"] and hostkeys.keys_for(text, "h2")
     assert a.forget("h1") == 1 and hostkeys.keys_for(be.read_blob("m", hostkeys.BLOB).decode(), "h1") == []
+    # OpenSSH writes "[host]:port" when an ssh_config Port is not 22: found and forgotten too
+    with open(a.path, "a") as fh:
+        fh.write("[h3]:2222 ssh-ed25519 AAAA3\n")
+    assert a.save() and a.keys_for("h3") == ["ssh-ed25519 AAAA3"]
+    assert a.forget("h3") == 1 and a.keys_for("h3") == []
     a.close()
     b.close()
     assert not os.path.exists(a.path)

@@ -70,6 +70,17 @@ def merge(old: str, new: str) -> str:
     return "".join(line + "\n" for line in lines)
 
 
+def _hosts_of(field: str) -> List[str]:
+    """The addresses a known_hosts host field names: ``a,b`` and OpenSSH's ``[a]:port`` form
+    (written when an ``ssh_config`` Port is not 22)."""
+    out = []
+    for name in field.split(","):
+        if name.startswith("[") and "]:" in name:
+            name = name[1:name.index("]:")]
+        out.append(name)
+    return out
+
+
 def keys_for(text: str, address: str) -> List[str]:
     """``["<type> <base64>", ...]`` pinned for ``address`` (Terraform's ``host_key`` takes
     one of these)."""
@@ -78,7 +89,7 @@ def keys_for(text: str, address: str) -> List[str]:
         parts = line.split(" ")
         if len(parts) < 3 or parts[0].startswith("@"):
             continue
-        if address in parts[0].split(","):
+        if address in _hosts_of(parts[0]):
             out.append(f"{parts[1]} {parts[2]}")
     return out
 
@@ -166,7 +177,7 @@ class HostKeys:
         """Drop every pinned key of ``address`` from the backend blob; returns how many."""
         with self.backend.lock(self.manager):
             lines = parse_lines(self._read_blob())
-            keep = [ln for ln in lines if address not in ln.split(" ")[0].split(",")]
+            keep = [ln for ln in lines if address not in _hosts_of(ln.split(" ")[0])]
             self.backend.write_blob(self.manager, BLOB, "".join(ln + "\n" for ln in keep).encode())
         self.reload()
         return len(lines) - len(keep)
