@@ -143,6 +143,7 @@ if mode == "error":
     print(json.dumps({{"ok": False, "error": "hipMalloc: out of memory"}}), flush=True)
     sys.exit(2)
 n = int(a[a.index("--span-bytes") + 1]) or (300 << 30)
+print("a library's banner on stdout", flush=True)
 print(json.dumps({{"ok": True, "errors": 0, "verify_gbps": 6100.0, "bytes": n, "hbm_bytes": 309 << 30,
                   "alloc_ms": 412.0, "test_ms": 300.0}}), flush=True)
 time.sleep(float(os.environ.get("FAKE_RELEASE_S", "0")))

@@ -10,7 +10,7 @@ fails a threshold or the memtest marks the node not-ready.
 import ctypes
 import json
 import os
-import selectors
+import queue
 import subprocess
 import threading
 import time
@@ -253,21 +253,26 @@ def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, pas
                             start_new_session=True)
     with _span_mu:
         _span_children.append((dev, proc))
-    line = ""
-    sel = selectors.DefaultSelector()
-    sel.register(proc.stdout, selectors.EVENT_READ)
+    # the verdict is the one JSON line (a library may print others); read on a thread, so a
+    # line already buffered behind an earlier one is not waited for
+    got: "queue.Queue[str]" = queue.Queue()
+
+    def read_verdict() -> None:
+        for text in proc.stdout:
+            if text.startswith("{"):
+                got.put(text)
+                return
+        got.put("")
+
+    threading.Thread(target=read_verdict, name=f"tk-span-{dev}", daemon=True).start()
     try:
-        deadline = time.monotonic() + timeout
-        while not line:
-            left = deadline - time.monotonic()
-            if left <= 0 or not sel.select(timeout=left):
-                proc.kill()
-                raise ProbeError(f"memtest_span: gpu-burnin --memtest-span gave no verdict within {timeout:.0f} s")
-            line = proc.stdout.readline()
-            if not line and proc.poll() is not None:
-                raise ProbeError(f"memtest_span: gpu-burnin --memtest-span exited {proc.returncode} without a verdict")
-    finally:
-        sel.close()
+        line = got.get(timeout=timeout)
+    except queue.Empty:
+        proc.kill()
+        raise ProbeError(f"memtest_span: gpu-burnin --memtest-span gave no verdict within {timeout:.0f} s") from None
+    if not line:
+        proc.wait(timeout=SPAN_RELEASE_TIMEOUT_S)
+        raise ProbeError(f"memtest_span: gpu-burnin --memtest-span exited {proc.returncode} without a verdict")
     try:
         doc = json.loads(line)
     except ValueError as exc:
