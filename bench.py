@@ -83,6 +83,10 @@ def parse_args():
                     help="the GPU node's health policy (node/health.py).  taint (bench default): a GPU with "
                          "uncorrectable ECC errors does not abort the run; the node joins tainted and the line "
                          "lists it under gpu_unhealthy_nodes (its GPUs then sit out the GPU and RCCL checks)")
+    ap.add_argument("--link-min-gbps", type=float, default=0.0,
+                    help="the GPU node's absolute xGMI link floor (gpu_link_min_gbps; the product default is 38). "
+                         "The bench records the link matrix (xgmi_links in the line) rather than certifying it: "
+                         "0 keeps only the relative check (a link below half the node's median still fails)")
     ap.add_argument("--sim-gpu", action="store_true",
                     help="CPU dry run: synthetic topology, no burn-in kernels; the cluster RCCL gate runs over the "
                          "libtk_rccl ABI stub (ops/csrc/tk_rccl_stub.cpp: every rank of the world joins and sweeps, "
@@ -327,7 +331,7 @@ def main() -> int:
                        {"rancher_host_label": "worker", "node_count": workers, "hostname": f"{name}-gpu",
                         "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k", "hosts": gpu_hosts,
                         "gpu": "mi355x", "gpu_count": gpus_per_worker, "gpu_burnin": args.burnin,
-                        "gpu_health": args.gpu_health},
+                        "gpu_health": args.gpu_health, "gpu_link_min_gbps": str(args.link_min_gbps)},
                    ])
         # the CLI's own agent transport: per-node tokens + TLS against the manager's CA
         ctx = Context(settings=Settings(cfg, env={}), out=devnull)
@@ -341,6 +345,14 @@ def main() -> int:
                 if run.info.mi355x:
                     for st in detail.get("steps", []) or []:
                         steps[st.get("name")] = max(steps.get(st.get("name"), 0.0), float(st.get("ms") or 0.0))
+                        links = st.get("detail") if st.get("name") == "gpu_links" else None
+                        if isinstance(links, dict) and links.get("labels"):
+                            # the measured xGMI matrix (node/labels.py:link_labels), per worker
+                            lab = links["labels"]
+                            out.setdefault("xgmi_links", []).append({
+                                "status": links.get("status"), "min_gbps": float(lab.get("amd.com/xgmi.p2p-min-gbps", 0)),
+                                "median_gbps": float(lab.get("amd.com/xgmi.p2p-median-gbps", 0)),
+                                "method": lab.get("amd.com/xgmi.p2p-method"), "floor_gbps": links.get("floor_gbps")})
             if steps:
                 out["gpu_node_step_ms"] = {k: round(v, 1) for k, v in steps.items()}
         rep = ctx.extras.get("last_readiness")
@@ -474,7 +486,7 @@ def main() -> int:
                 "control_plane_nodes": 2, "global_batch": "n/a", "seq_len": "n/a",
                 "parallelism": f"{workers} worker node(s) x {gpus_per_worker} GPU(s)",
                 "executor": "direct", "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate,
-                "gpu_health": args.gpu_health,
+                "gpu_health": args.gpu_health, "gpu_link_min_gbps": args.link_min_gbps,
                 "start": ("cold (fresh agent processes per step)" if args.agents == "proc"
                           else "cold agents in the bench process (fresh NodeAgent objects per step)"),
                 "rccl_gate_max_mib": args.rccl_mib,
@@ -495,6 +507,8 @@ def main() -> int:
             "gpu_unhealthy_nodes": sorted({h for r in results for h in r.get("gpu_unhealthy", [])}),
             # ranks of the cluster RCCL gate per timed step (every GPU of the worker tier)
             "rccl_gate_ranks": [r.get("rccl_gate_ranks", 0) for r in results],
+            # the GPU nodes' measured xGMI peer-read matrix (2+ GPUs per node), last timed step
+            "xgmi_links": next((r["xgmi_links"] for r in reversed(results) if r.get("xgmi_links")), None),
             "phase_ms_per_step": phase_ms,
         }
         print(json.dumps(line), flush=True)
