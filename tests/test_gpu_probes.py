@@ -482,3 +482,24 @@ def test_full_span_in_a_child_process(probe):
     assert res["errors"] == 0
     assert before - (5 << 30) <= res["bytes"] <= before - (3 << 30)
     assert after >= before - (1 << 30)
+
+
+def test_link_matrix_checks_the_data_it_moved():
+    """Each pair's received data is checked against the sender's pattern after its last
+    transfer: clean on a healthy device, and one flipped word (fail point) is reported on
+    exactly one pair, which the verdict marks corrupt."""
+    from triton_kubernetes_amd.node.labels import link_labels
+    from triton_kubernetes_amd.ops import probe
+
+    devs = [0, 0, 0] if probe.device_count() < 2 else list(range(min(4, probe.device_count())))
+    for method in ("kernel-read", "sdma-copy"):
+        clean = probe.link_matrix(devs, 32 << 20, 2, method=method)
+        assert not clean["errors"] and clean["data_errors"] == {}, clean
+    probe.set_fail_point("link_matrix.corrupt")
+    try:
+        hit = probe.link_matrix(devs, 32 << 20, 2, method="kernel-read")
+    finally:
+        probe.set_fail_point("")
+    assert list(hit["data_errors"].values()) == [1], hit
+    verdict = link_labels(hit, min_gbps=0.0)
+    assert verdict["status"] == "degraded" and verdict["corrupt"] == list(hit["data_errors"])

@@ -363,6 +363,10 @@ def test_link_labels_verdicts():
     err = link_labels({"pairs": pairs, "peer_access": dict({p: True for p in pairs}, **{"0-1": False})})
     assert err["status"] == "error"
     assert link_labels({"pairs": {}, "errors": []})["status"] == "skipped"
+    # full speed, wrong data: degraded whatever the bandwidth says
+    bad_data = link_labels({"pairs": pairs, "peer_access": {p: True for p in pairs}, "data_errors": {"1-0": 3}},
+                           min_gbps=0.0)
+    assert bad_data["status"] == "degraded" and bad_data["degraded"] == ["1-0"] and bad_data["corrupt"] == ["1-0"]
 
 
 def test_link_check_absolute_floor_fails_a_uniformly_slow_fabric():

@@ -173,9 +173,10 @@ def link_labels(matrix: Dict[str, Any], min_frac: float = 0.5,
     """Verdict and labels of a node's peer-to-peer link matrix (``ops/probe.py:link_matrix``
     or ``gpu-burnin --p2p``).  A pair is a degraded xGMI link when it is below ``min_frac``
     of the node's median (one bad link) OR below the absolute floor ``min_gbps`` (a
-    uniformly slow fabric, whose median looks healthy); a pair without peer access or whose
+    uniformly slow fabric, whose median looks healthy) OR when the data it delivered did not
+    match what was sent (``data_errors``: ``corrupt``); a pair without peer access or whose
     transfer failed is an error.  Returns ``{"labels": {...}, "degraded": [...],
-    "below_floor": [...], "status": passed|degraded|error}``."""
+    "below_floor": [...], "corrupt": [...], "status": passed|degraded|error}``."""
     vals = sorted(matrix.get("pairs", {}).values())
     errors = list(matrix.get("errors", []))
     errors += [f"{p}: no peer access" for p, ok in sorted(matrix.get("peer_access", {}).items()) if not ok]
@@ -184,15 +185,18 @@ def link_labels(matrix: Dict[str, Any], min_frac: float = 0.5,
                 "status": "error" if errors else "skipped"}
     median = vals[len(vals) // 2] if len(vals) % 2 else 0.5 * (vals[len(vals) // 2 - 1] + vals[len(vals) // 2])
     below = sorted(p for p, v in matrix["pairs"].items() if v < min_gbps)
-    degraded = sorted(p for p, v in matrix["pairs"].items() if v < min_frac * median or v < min_gbps)
+    # a link that delivered wrong data is degraded whatever its speed
+    corrupt = sorted(p for p, w in (matrix.get("data_errors") or {}).items() if w)
+    degraded = sorted(set(p for p, v in matrix["pairs"].items() if v < min_frac * median or v < min_gbps)
+                      | set(corrupt))
     status = "error" if errors else ("degraded" if degraded else "passed")
     labels = {"amd.com/xgmi.link-check": status,
               "amd.com/xgmi.p2p-min-gbps": f"{vals[0]:.0f}",
               "amd.com/xgmi.p2p-median-gbps": f"{median:.0f}"}
     if matrix.get("method"):
         labels["amd.com/xgmi.p2p-method"] = str(matrix["method"])
-    return {"labels": labels, "degraded": degraded, "below_floor": below, "errors": errors, "status": status,
-            "floor_gbps": min_gbps}
+    return {"labels": labels, "degraded": degraded, "below_floor": below, "corrupt": corrupt, "errors": errors,
+            "status": status, "floor_gbps": min_gbps}
 
 
 def agent_label_flags(labels: Dict[str, str]) -> List[str]:

@@ -1036,8 +1036,17 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_peer_read(const u32x4* __res
 // (hipMemcpyPeerAsync).  gbps[i*n+j]: best transfer i -> j (GB/s, -1 when it failed or, in
 // kernel mode, when j cannot map i's memory); access[i*n+j]: j can map i's memory.  Peer
 // access this call enabled is disabled again.
-extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int iters, int mode, double* gbps,
-                                    int* access) {
+//
+// Data check (errs != nullptr): every source buffer holds its own pattern (the memtest's,
+// seeded per GPU), and after each pair's last timed transfer a kernel on the receiver checks
+// what arrived against the sender's pattern: errs[i*n+j] = mismatching 32-bit words i -> j
+// (-1 when the pair was not measured).  A link that moves data at full speed but corrupts it
+// is caught here, not by the bandwidth verdict.  Fail point "link_matrix.corrupt" flips one
+// word of the first pair's received data (tests).
+__global__ void k_flip_word(uint32_t* p) { p[0] ^= 0x1u; }
+
+extern "C" int tkp_link_matrix_check(const int* devs, int n, size_t bytes, int iters, int mode, double* gbps,
+                                     int* access, double* errs) {
   if (n < 2 || n > 64 || bytes == 0) {
     snprintf(g_err, sizeof(g_err), "link matrix: %d devices, %zu bytes", n, bytes);
     return -1;
@@ -1047,7 +1056,11 @@ extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int it
   std::vector<hipEvent_t> ev(2 * n, nullptr);
   std::vector<std::pair<int, int>> enabled;
   std::vector<int> grid(n, 0);
+  std::vector<unsigned long long*> bad(n, nullptr);  // per receiver: mismatches of its current check
   bytes = bytes / sizeof(u32x4) * sizeof(u32x4);
+  const size_t words4 = bytes / sizeof(uint4);
+  const bool check = errs != nullptr;
+  bool flipped = false;
   int rc = 0;
   auto cleanup = [&]() {
     for (int i = 0; i < n; ++i) {
@@ -1058,6 +1071,7 @@ extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int it
         if (buf[k]) (void)hipFree(buf[k]);
       }
       if (st[i]) (void)hipStreamDestroy(st[i]);
+      if (bad[i]) (void)hipFree(bad[i]);
     }
     for (auto& e : enabled) {
       (void)hipSetDevice(devs[e.first]);
@@ -1070,7 +1084,13 @@ extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int it
     hipError_t e = hipSetDevice(devs[i]);
     if (e == hipSuccess) e = hipMalloc(&buf[2 * i], bytes);
     if (e == hipSuccess) e = hipMalloc(&buf[2 * i + 1], bytes);
-    if (e == hipSuccess) e = hipMemsetAsync(buf[2 * i], 0x5a, bytes, 0);
+    if (e == hipSuccess && !check) e = hipMemsetAsync(buf[2 * i], 0x5a, bytes, 0);
+    if (e == hipSuccess && check) e = hipMalloc(&bad[i], sizeof(unsigned long long));
+    if (e == hipSuccess && check) {  // the sender's pattern, seeded by its index in devs
+      k_mem_fill<<<stream_grid(devs[i], 16), STREAM_THREADS>>>(static_cast<uint4*>(buf[2 * i]), words4,
+                                                              0x11c0ffeeu + (uint32_t)i);
+      e = hipGetLastError();
+    }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
     if (e == hipSuccess) e = hipEventCreate(&ev[2 * i]);
     if (e == hipSuccess) e = hipEventCreate(&ev[2 * i + 1]);
@@ -1082,6 +1102,7 @@ extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int it
     for (int j = 0; j < n && rc == 0; ++j) {
       gbps[i * n + j] = 0.0;
       access[i * n + j] = 0;
+      if (check) errs[i * n + j] = i == j ? 0.0 : -1.0;
       if (i == j) continue;
       int can = 0;
       if (hipDeviceCanAccessPeer(&can, devs[j], devs[i]) != hipSuccess) can = 0;
@@ -1123,6 +1144,20 @@ extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int it
             }
           }
           if (e == hipSuccess) e = hipEventRecord(ev[2 * dst + 1], st[dst]);
+          if (e == hipSuccess && check && it == (iters < 1 ? 1 : iters) - 1) {
+            // after the timed transfer (same stream): what arrived vs the sender's pattern
+            uint4* got = static_cast<uint4*>(buf[2 * dst + 1]);
+            if (!flipped && fail_point("link_matrix.corrupt")) {
+              k_flip_word<<<1, 1, 0, st[dst]>>>(reinterpret_cast<uint32_t*>(got) + 7);
+              flipped = true;
+            }
+            e = hipMemsetAsync(bad[dst], 0, sizeof(unsigned long long), st[dst]);
+            if (e == hipSuccess) {
+              k_mem_check<<<grid[dst] * 4, STREAM_THREADS, 0, st[dst]>>>(got, words4, 0x11c0ffeeu + (uint32_t)src,
+                                                                         bad[dst]);
+              e = hipGetLastError();
+            }
+          }
           if (e != hipSuccess) { failed[p] = 1; (void)hipGetLastError(); }
         }
         for (size_t p = 0; p < pairs.size(); ++p) {
@@ -1142,11 +1177,25 @@ extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int it
       for (size_t p = 0; p < pairs.size(); ++p) {
         const int src = dir ? pairs[p].second : pairs[p].first, dst = dir ? pairs[p].first : pairs[p].second;
         gbps[src * n + dst] = failed[p] ? -1.0 : best[p];
+        if (check && !failed[p]) {
+          (void)hipSetDevice(devs[dst]);
+          unsigned long long h = 0;
+          if (hipStreamSynchronize(st[dst]) == hipSuccess &&
+              hipMemcpy(&h, bad[dst], sizeof(h), hipMemcpyDeviceToHost) == hipSuccess)
+            errs[src * n + dst] = (double)h;
+          else
+            (void)hipGetLastError();
+        }
       }
     }
   }
   cleanup();
   return rc;
+}
+
+extern "C" int tkp_link_matrix_mode(const int* devs, int n, size_t bytes, int iters, int mode, double* gbps,
+                                    int* access) {
+  return tkp_link_matrix_check(devs, n, bytes, iters, mode, gbps, access, nullptr);
 }
 
 extern "C" int tkp_link_matrix(const int* devs, int n, size_t bytes, int iters, double* gbps, int* access) {
@@ -1189,10 +1238,10 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
     if (labels_path) { FILE* f = fopen(labels_path, "w"); if (f) fclose(f); }
     return 0;
   }
-  std::vector<double> vals, mat(n * n, 0.0);
+  std::vector<double> vals, mat(n * n, 0.0), derr(n * n, 0.0);
   std::vector<int> devs(n), acc(n * n, 0);
   for (int i = 0; i < n; ++i) devs[i] = i;
-  if (tkp_link_matrix_mode(devs.data(), n, 64ull << 20, 3, mode, mat.data(), acc.data()) != 0) {
+  if (tkp_link_matrix_check(devs.data(), n, 64ull << 20, 3, mode, mat.data(), acc.data(), derr.data()) != 0) {
     printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
     return 2;
   }
@@ -1214,16 +1263,21 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
   const double median = m == 0 ? 0.0 : (m % 2 ? sorted[m / 2] : 0.5 * (sorted[m / 2 - 1] + sorted[m / 2]));
   // a link is degraded below min_frac of the node's median OR below the absolute floor
   // (a uniformly slow fabric has a healthy-looking median)
-  int degraded = 0, below_floor = 0;
-  for (double v : vals) {
-    degraded += v < min_frac * median || v < min_gbps;
-    below_floor += v < min_gbps;
-  }
+  int degraded = 0, below_floor = 0, corrupt = 0;
+  for (int i = 0; i < n; ++i)
+    for (int j = 0; j < n; ++j) {
+      if (i == j || mat[i * n + j] < 0.0) continue;
+      const double v = mat[i * n + j];
+      const bool bad_data = derr[i * n + j] > 0.0;  // delivered data differed from what was sent
+      degraded += v < min_frac * median || v < min_gbps || bad_data;
+      below_floor += v < min_gbps;
+      corrupt += bad_data;
+    }
   const char* status = (errors || no_peer || m == 0) ? "error" : (degraded ? "degraded" : "passed");
   printf("},\"method\":\"%s\",\"min_gbps\":%.1f,\"median_gbps\":%.1f,\"floor_gbps\":%.1f,\"degraded\":%d,"
-         "\"below_floor\":%d,\"errors\":%d,\"no_peer_access\":%d,\"status\":\"%s\"}\n",
-         mode ? "kernel-read" : "sdma-copy", m ? sorted[0] : 0.0, median, min_gbps, degraded, below_floor, errors,
-         no_peer, status);
+         "\"below_floor\":%d,\"corrupt\":%d,\"errors\":%d,\"no_peer_access\":%d,\"status\":\"%s\"}\n",
+         mode ? "kernel-read" : "sdma-copy", m ? sorted[0] : 0.0, median, min_gbps, degraded, below_floor, corrupt,
+         errors, no_peer, status);
   if (labels_path && m) {
     FILE* f = fopen(labels_path, "w");
     if (!f) { fprintf(stderr, "cannot write %s\n", labels_path); return 2; }

@@ -76,6 +76,9 @@ def _lib():
                                     ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
     lib.tkp_link_matrix_mode.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
                                          ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int)]
+    lib.tkp_link_matrix_check.argtypes = [ctypes.POINTER(ctypes.c_int), ctypes.c_int, ctypes.c_size_t, ctypes.c_int,
+                                          ctypes.c_int, ctypes.POINTER(ctypes.c_double), ctypes.POINTER(ctypes.c_int),
+                                          ctypes.POINTER(ctypes.c_double)]
     lib.tkp_set_scratch_cache.argtypes = [ctypes.c_int]
     lib.tkp_prealloc_scratch.argtypes = [ctypes.c_int, ctypes.c_size_t, ctypes.c_size_t]
     lib.tkp_release_scratch.restype = ctypes.c_longlong
@@ -319,7 +322,9 @@ def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3,
     measures the pairs in rounds of a round-robin pairing: transfers run concurrently only on
     disjoint pairs, so each number is still one xGMI link's, not a share of a busy fabric
     (8 GPUs: 14 timed slots instead of 56).  A pair that fails is recorded as an error, not
-    raised: the caller decides (``node/labels.py:link_labels``)."""
+    raised: the caller decides (``node/labels.py:link_labels``).  ``data_errors``: what
+    arrived was checked against the sender's pattern after each pair's last transfer
+    (mismatching 32-bit words per pair): a link that corrupts data at full speed."""
     devs = list(devices)
     n = len(devs)
     pairs: Dict[str, float] = {}
@@ -327,12 +332,15 @@ def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3,
     errors: List[str] = []
     if method not in LINK_METHODS:
         raise ValueError(f"link method must be one of {sorted(LINK_METHODS)}")
+    data_errors: Dict[str, int] = {}
     if n < 2:
-        return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes, "method": method}
+        return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes, "method": method,
+                "data_errors": data_errors}
     gbps = (ctypes.c_double * (n * n))()
     acc = (ctypes.c_int * (n * n))()
-    _check(_lib().tkp_link_matrix_mode((ctypes.c_int * n)(*devs), n, nbytes, iters, LINK_METHODS[method], gbps, acc),
-           "link_matrix")
+    errs = (ctypes.c_double * (n * n))()
+    _check(_lib().tkp_link_matrix_check((ctypes.c_int * n)(*devs), n, nbytes, iters, LINK_METHODS[method], gbps, acc,
+                                        errs), "link_matrix")
     for a, i in enumerate(devs):
         for b, j in enumerate(devs):
             if a == b:
@@ -343,7 +351,10 @@ def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3,
                 errors.append(f"{i}->{j}: peer {'read' if method == 'kernel-read' else 'copy'} failed")
                 continue
             pairs[f"{i}-{j}"] = round(v, 1)
-    return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes, "method": method}
+            if errs[a * n + b] > 0:
+                data_errors[f"{i}-{j}"] = int(errs[a * n + b])
+    return {"pairs": pairs, "peer_access": access, "errors": errors, "bytes": nbytes, "method": method,
+            "data_errors": data_errors}
 
 
 # --- burn-in policy ------------------------------------------------------------------
