@@ -503,3 +503,27 @@ def test_link_matrix_checks_the_data_it_moved():
     assert list(hit["data_errors"].values()) == [1], hit
     verdict = link_labels(hit, min_gbps=0.0)
     assert verdict["status"] == "degraded" and verdict["corrupt"] == list(hit["data_errors"])
+
+
+def test_eight_concurrent_burnins_in_one_process(probe):
+    """The agent burns in every GPU of a node at once, one thread each (node/agent_steps.py).
+    On a one-GPU box the eight threads share GPU 0: throughput is split eight ways (the
+    floors are off here), but the host code -- arena slots, streams, events, per-thread
+    errors, the GEMM screen's one-time setup -- runs eight-way concurrent for real, and every
+    correctness check must still hold."""
+    import concurrent.futures as cf
+
+    th = probe.Thresholds(min_read_frac=0.0, min_bf16_frac=0.0, min_fp8_frac=0.0, min_gemm_frac=0.0,
+                          min_gemm_fp8_frac=0.0)
+    probe.set_scratch_cache(True)
+    try:
+        with cf.ThreadPoolExecutor(max_workers=8) as pool:
+            results = list(pool.map(lambda _: probe.run_burnin(0, "quick", th), range(8)))
+    finally:
+        probe.release_scratch()
+    for r in results:
+        assert r.ok, r.failures
+        assert r.memtest["errors"] == 0 and r.gemm["ok"] and r.gemm_fp8["ok"], r.to_json()
+        assert r.hbm["read_gbps"] > 0 and r.mfma["bf16"]["tflops"] > 0
+    print(json.dumps({"read_gbps": [round(r.hbm["read_gbps"]) for r in results],
+                      "bf16_tflops": [round(r.mfma["bf16"]["tflops"]) for r in results]}))
