@@ -486,3 +486,46 @@ def test_gpu_links_cli_verdict(monkeypatch, capsys):
     assert cli.main(["links"]) == 1
     assert json.loads(capsys.readouterr().out)["status"] == "degraded"
     assert cli.main(["links", "--min-gbps", "20"]) == 0
+
+
+def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
+    """The agent's cluster gate runs RCCL in the agent process, and RCCL reads its settings
+    once per process: the node's /etc/rccl/rccl.env (else its discovered RDMA ports) goes into
+    the agent's environment before its first RCCL call; the rccl_env step updates what RCCL
+    has not read yet and reports it; the process's own settings win."""
+    import os
+
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.plan import Step
+    from triton_kubernetes_amd.parallel.rccl_env import render_env_file
+
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("NCCL_", "RCCL_"))}
+    env["NCCL_DEBUG"] = "INFO"  # set by the unit / operator: kept
+    monkeypatch.setattr(os, "environ", env)
+    agent = NodeAgent(name="n", mode="sim", devices=[0, 1], root=str(tmp_path))
+    try:
+        # no file yet (first boot): the node's RDMA ports decide
+        topo = {"gpus": [], "nics": [{"name": "mlx5_0", "port": 1, "link_layer": "Ethernet", "roce_v2_gid_index": 3},
+                                     {"name": "mlx5_1", "port": 1, "link_layer": "Ethernet", "roce_v2_gid_index": 3}]}
+        monkeypatch.setattr(agent, "_topology", lambda: topo)
+        applied = agent.apply_node_rccl_env()
+        assert applied == {"NCCL_IB_HCA": "=mlx5_0:1,mlx5_1:1", "NCCL_IB_GID_INDEX": "3"}
+        assert env["NCCL_IB_HCA"] == "=mlx5_0:1,mlx5_1:1" and env["NCCL_DEBUG"] == "INFO"
+
+        # the bring-up's rccl_env step: the configured values win in the file, and what
+        # differs from this process's environment is applied and reported
+        step = Step("rccl_env", "rccl_env", "", {"env": {"NCCL_SOCKET_IFNAME": "=bond0", "NCCL_DEBUG": "WARN",
+                                                          "HSA_FORCE_FINE_GRAIN_PCIE": "1"}})
+        out = agent._run_step(None, step, {"labels": {}, "capacity": {}, "taints": [], "topology": topo})
+        assert out["agent_env_updated"] == ["NCCL_DEBUG", "NCCL_SOCKET_IFNAME"]
+        assert env["NCCL_SOCKET_IFNAME"] == "=bond0" and "HSA_FORCE_FINE_GRAIN_PCIE" not in env
+
+        # a later start reads the file the bring-up wrote (the unit's own values still win)
+        for k in ("NCCL_IB_HCA", "NCCL_IB_GID_INDEX", "NCCL_SOCKET_IFNAME"):
+            del env[k]
+        (tmp_path / "etc/rccl/rccl.env").write_text(render_env_file({"NCCL_SOCKET_IFNAME": "=bond1", "NCCL_DEBUG": "TRACE",
+                                                                     "HSA_NO_SCRATCH_RECLAIM": "1"}))
+        again = agent.apply_node_rccl_env()
+        assert again == {"NCCL_SOCKET_IFNAME": "=bond1"} and env["NCCL_DEBUG"] == "WARN"
+    finally:
+        agent.stop()

@@ -68,6 +68,7 @@ from .security import AgentPolicy, is_loopback
 
 MODES = ("sim", "exec")
 
+
 @dataclass
 class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
     name: str = "node"
@@ -222,6 +223,9 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             return
         from ..ops import probe, rccl, topo
 
+        # RCCL reads its settings once per process, the bootstrap interface at the first
+        # unique id (made below): the node's RCCL environment goes in first
+        self.rccl_env_applied = self.apply_node_rccl_env()
         probe._lib()
         rccl._lib()
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
@@ -249,6 +253,34 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later
             pass
+
+    # RCCL settings the gate's communicators need from the node's environment: RCCL reads
+    # them once per process, so they must be in place before the agent's first RCCL call
+    RCCL_ENV_PREFIXES = ("NCCL_", "RCCL_")
+
+    def apply_node_rccl_env(self) -> Dict[str, str]:
+        """Put the node's RCCL settings into this process's environment, for the agent's own
+        communicators (the cluster gate): ``/etc/rccl/rccl.env`` when a bring-up wrote it (the
+        systemd unit also loads it, ``EnvironmentFile=``), else what the node's RDMA ports say
+        (``parallel/rccl_env.py:site_env_from_topology``: ``NCCL_IB_HCA``, the RoCE v2 GID
+        index) -- so even the first bring-up after boot gates over the right ports.  Keys the
+        process environment already sets win; returns what was applied."""
+        from ..parallel.rccl_env import parse_env_file, site_env_from_topology
+
+        try:
+            with open(self.path("/etc/rccl/rccl.env"), "r", encoding="utf-8") as fh:
+                env = parse_env_file(fh.read())
+        except OSError:
+            try:
+                env = site_env_from_topology(self._topology())
+            except Exception:  # noqa: BLE001 - no topology: RCCL's own defaults
+                env = {}
+        applied = {}
+        for k, v in env.items():
+            if k.startswith(self.RCCL_ENV_PREFIXES) and k not in os.environ:
+                os.environ[k] = v
+                applied[k] = v
+        return applied
 
     def _start_janitor(self, idle_s: float) -> None:
         """One long-lived thread frees the burn-in arena once no plan has run for ``idle_s``

@@ -280,7 +280,18 @@ class AgentStepsMixin:
             env = site_env_from_topology(ctx.get("topology") or {})
             discovered = sorted(env)
             env.update(step.params.get("env", {}))
-            return {"file": self.write_file("/etc/rccl/rccl.env", render_env_file(env)), "discovered": discovered}
+            out = {"file": self.write_file("/etc/rccl/rccl.env", render_env_file(env)), "discovered": discovered}
+            if self.topology_override is None and self.devices:
+                # this agent's own gate runs in this process: RCCL settings it has not read yet
+                # take effect now; ones RCCL already read (the bootstrap interface, fixed by the
+                # first unique id) take effect when the agent restarts (its unit loads the file)
+                changed = sorted(k for k, v in env.items()
+                                 if k.startswith(self.RCCL_ENV_PREFIXES) and os.environ.get(k) != str(v))
+                for k in changed:
+                    os.environ[k] = str(env[k])
+                if changed:
+                    out["agent_env_updated"] = changed
+            return out
         if a == "rccl_slim":
             # an agent chose its runtime at start (its unit's ExecStartPre prepared the
             # single-target RCCL): report which one the gate runs on
