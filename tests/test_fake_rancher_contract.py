@@ -336,7 +336,8 @@ def test_admission_cluster_default_level_applies_to_unlabelled_namespaces():
 def test_admission_webhook_failure_policy(fake, api):
     cid = _cluster_with_node(fake, api)
     k = f"/k8s/clusters/{cid}"
-    hook = {"name": "inject.example.com", "rules": [{"operations": ["CREATE"], "apiGroups": [""],
+    hook = {"name": "inject.example.com", "sideEffects": "None", "admissionReviewVersions": ["v1"],
+            "rules": [{"operations": ["CREATE"], "apiGroups": [""],
                                                      "apiVersions": ["v1"], "resources": ["pods"]}],
             "clientConfig": {"service": {"name": "nowhere", "namespace": "kube-system", "path": "/mutate"},
                              "caBundle": base64.b64encode(b"").decode()},
@@ -380,3 +381,28 @@ def test_client_upgrade_rereads_on_conflict(fake, api):
     client.upgrade_cluster(obj["status"]["clusterName"], RKE2_NEW)
     assert raced and fake.state.v2_clusters[f"{FLEET_NAMESPACE}/r1"]["spec"]["kubernetesVersion"] == RKE2_NEW
     assert [m for m, p in fake.state.log if m == "PUT"] == ["PUT", "PUT"]  # the 409, then the retry
+
+
+def test_k8s_webhook_configuration_validation(fake, api):
+    cid = _cluster_with_node(fake, api)
+    cfgs = f"/k8s/clusters/{cid}/apis/admissionregistration.k8s.io/v1/mutatingwebhookconfigurations"
+    good = {"name": "inject.amd.example.com", "sideEffects": "None", "admissionReviewVersions": ["v1"],
+            "clientConfig": {"service": {"name": "s", "namespace": "kube-system"}}, "failurePolicy": "Ignore",
+            "rules": []}
+    for change, want in (({"sideEffects": "Unknown"}, "sideEffects"),
+                         ({"admissionReviewVersions": []}, "admissionReviewVersions"),
+                         ({"name": "inject"}, "three segments"),
+                         ({"clientConfig": {}}, "exactly one of url or service"),
+                         ({"clientConfig": {"url": "https://x", "service": {"name": "s"}}}, "exactly one"),
+                         ({"failurePolicy": "Retry"}, "failurePolicy")):
+        code, out = api("POST", cfgs, {"metadata": {"name": "bad"}, "webhooks": [dict(good, **change)]})
+        assert code == 422 and want in out["message"], (change, out)
+    code, out = api("POST", cfgs, {"metadata": {"name": "dup"}, "webhooks": [good, good]})
+    assert code == 422 and "Duplicate" in out["message"]
+    assert api("POST", cfgs, {"metadata": {"name": "ok"}, "webhooks": [good]})[0] == 201
+    # the framework's own injector configuration passes the same validation
+    from triton_kubernetes_amd.rancher.fake.k8s import _webhook_config_problem
+    from triton_kubernetes_amd.k8s.addons import rendered_addons
+
+    mine = [obj for path, obj in rendered_addons({"gpu_count": 8}) if obj.get("kind") == "MutatingWebhookConfiguration"]
+    assert mine and all(_webhook_config_problem(o) == "" for o in mine)

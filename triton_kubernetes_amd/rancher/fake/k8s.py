@@ -39,6 +39,10 @@ Refusals, as a real API server words them (negative tests in
 * replace or merge-patch carrying a stale ``metadata.resourceVersion`` -> 409 ``Conflict``;
 * a Namespace whose ``pod-security.kubernetes.io/enforce`` label is not a Pod Security
   level -> 403 ``Forbidden`` (the PodSecurity admission plugin checks namespace labels);
+* a MutatingWebhookConfiguration that admissionregistration/v1 validation refuses (a webhook
+  name that is not fully qualified or repeats, ``sideEffects`` other than None /
+  NoneOnDryRun, no v1/v1beta1 ``admissionReviewVersions``, a ``clientConfig`` without
+  exactly one of url / service, an unknown ``failurePolicy``) -> 422 ``Invalid``;
 * a merge patch that is not a JSON object -> 400.
 """
 
@@ -48,7 +52,7 @@ import uuid
 from typing import Any, Dict, List, Optional, Tuple
 
 from ...versions import DEFAULT_K8S_VERSION
-from .admission import PSA_ENFORCE, PSA_LEVELS, admit_pod
+from .admission import PSA_ENFORCE, PSA_LEVELS, WEBHOOK_CONFIGS, admit_pod
 
 DEVICE_PLUGIN_REPOS = ("rocm/k8s-device-plugin", "docker.io/rocm/k8s-device-plugin")
 DEVICE_PLUGIN_SOCKET_DIR = "/var/lib/kubelet/device-plugins"
@@ -96,6 +100,33 @@ def tolerated(taint: Dict[str, Any], tolerations: List[Dict[str, Any]]) -> bool:
         if t.get("key") == taint.get("key") and t.get("value", "") == taint.get("value", ""):
             return True
     return False
+
+
+def _webhook_config_problem(cfg: Dict[str, Any]) -> str:
+    """What admissionregistration.k8s.io/v1 validation refuses in a
+    MutatingWebhookConfiguration ("" when valid): per webhook a fully qualified name,
+    ``sideEffects`` None/NoneOnDryRun, ``admissionReviewVersions`` naming v1 or v1beta1, and
+    a ``clientConfig`` with exactly one of ``url`` / ``service``."""
+    names = set()
+    for i, hook in enumerate(cfg.get("webhooks") or []):
+        at = f"webhooks[{i}]"
+        name = str(hook.get("name", ""))
+        if name.count(".") < 2:
+            return f'{at}.name: Invalid value: "{name}": should be a domain with at least three segments'
+        if name in names:
+            return f'{at}.name: Duplicate value: "{name}"'
+        names.add(name)
+        if hook.get("sideEffects") not in ("None", "NoneOnDryRun"):
+            return f"{at}.sideEffects: Required value: must be one of None, NoneOnDryRun"
+        versions = hook.get("admissionReviewVersions") or []
+        if not any(v in ("v1", "v1beta1") for v in versions):
+            return f"{at}.admissionReviewVersions: Required value: must include at least one of v1, v1beta1"
+        cc = hook.get("clientConfig") or {}
+        if ("url" in cc) == ("service" in cc):
+            return f"{at}.clientConfig: Required value: exactly one of url or service is required"
+        if hook.get("failurePolicy", "Fail") not in ("Fail", "Ignore"):
+            return f"{at}.failurePolicy: Unsupported value: \"{hook.get('failurePolicy')}\""
+    return ""
 
 
 def _namespace_of(kpath: str) -> Optional[str]:
@@ -310,6 +341,11 @@ class K8sCoreApi:
             with self.state.mu:
                 if not self._namespace_exists(cid, ns):
                     return _status(404, "NotFound", f'namespaces "{ns}" not found')
+        if kpath.rstrip("/") == WEBHOOK_CONFIGS:
+            problem = _webhook_config_problem(body)
+            if problem:
+                return _status(422, "Invalid", f'MutatingWebhookConfiguration.admissionregistration.k8s.io '
+                                               f'"{meta.get("name", "")}" is invalid: {problem}')
         if kpath.rstrip("/") == NAMESPACES:
             level = (meta.get("labels") or {}).get(PSA_ENFORCE)
             if level is not None and level not in PSA_LEVELS:
