@@ -36,7 +36,9 @@ def cluster(tmp_path):
         ("/apis/apps/v1/namespaces/ml/deployments",
          {"apiVersion": "apps/v1", "kind": "Deployment", "metadata": {"name": "trainer", "namespace": "ml",
                                                                      "annotations": {"a": "b"}},
-          "spec": {"replicas": 2}}),
+          "spec": {"replicas": 2, "selector": {"matchLabels": {"app": "trainer"}},
+                   "template": {"metadata": {"labels": {"app": "trainer"}},
+                                "spec": {"containers": [{"name": "t", "image": "rocm/pytorch:latest"}]}}}}),
         ("/api/v1/namespaces/ml/configmaps",
          {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "cfg", "namespace": "ml"}, "data": {"k": "v"}}),
         ("/api/v1/namespaces/ml/configmaps",
@@ -49,7 +51,9 @@ def cluster(tmp_path):
           "spec": {"clusterIP": "10.43.0.7", "ports": [{"port": 80}]}}),
         ("/apis/batch/v1/namespaces/web/jobs",
          {"apiVersion": "batch/v1", "kind": "Job", "metadata": {"name": "owned", "namespace": "web",
-                                                               "ownerReferences": [{"kind": "CronJob"}]}}),
+                                                               "ownerReferences": [{"kind": "CronJob"}]},
+          "spec": {"template": {"spec": {"restartPolicy": "Never",
+                                         "containers": [{"name": "j", "image": "busybox:1.36"}]}}}}),
         ("/api/v1/namespaces/web/configmaps",
          {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "site", "namespace": "web"}}),
     ]

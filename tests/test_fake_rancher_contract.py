@@ -261,7 +261,9 @@ def test_k8s_create_refusals(fake, api):
 def test_k8s_replace_refusals(fake, api):
     cid = _cluster_with_node(fake, api)
     col = f"/k8s/clusters/{cid}/apis/apps/v1/namespaces/kube-system/daemonsets"
-    code, created = api("POST", col, {"metadata": {"name": "ds"}, "spec": {}})
+    spec = {"selector": {"matchLabels": {"app": "ds"}},
+            "template": {"metadata": {"labels": {"app": "ds"}}, "spec": {"containers": [{"name": "c", "image": "i"}]}}}
+    code, created = api("POST", col, {"metadata": {"name": "ds"}, "spec": spec})
     assert code == 201
     assert api("PUT", f"{col}/missing", {"metadata": {"name": "missing"}})[0] == 404
     code, out = api("PUT", f"{col}/ds", {"metadata": {"name": "other"}})
@@ -274,6 +276,14 @@ def test_k8s_replace_refusals(fake, api):
     code, out = api("PUT", f"{col}/ds", created)  # stale now
     assert code == 409 and out["reason"] == "Conflict"
     assert api("DELETE", f"{col}/missing")[0] == 404
+    # the API server's order: existence, then the precondition, then the new content
+    invalid = {"metadata": {"name": "ds"}, "spec": {}}
+    assert api("PUT", f"{col}/missing", dict(invalid, metadata={"name": "missing"}))[0] == 404
+    stale = dict(invalid, metadata=dict(created["metadata"]))
+    assert api("PUT", f"{col}/ds", stale)[0] == 409
+    current = api("GET", f"{col}/ds")[1]
+    code, out = api("PUT", f"{col}/ds", dict(invalid, metadata=dict(current["metadata"])))
+    assert code == 422 and "spec.template.spec.containers" in out["message"]
 
 
 def test_k8s_node_patch_and_eviction_refusals(fake, api):
@@ -406,3 +416,35 @@ def test_k8s_webhook_configuration_validation(fake, api):
 
     mine = [obj for path, obj in rendered_addons({"gpu_count": 8}) if obj.get("kind") == "MutatingWebhookConfiguration"]
     assert mine and all(_webhook_config_problem(o) == "" for o in mine)
+
+
+def test_k8s_workload_validation(fake, api):
+    cid = _cluster_with_node(fake, api)
+    k = f"/k8s/clusters/{cid}"
+    tmpl = {"metadata": {"labels": {"app": "x"}}, "spec": {"containers": [{"name": "c", "image": "busybox"}]}}
+    ds = f"{k}/apis/apps/v1/namespaces/kube-system/daemonsets"
+    code, out = api("POST", ds, {"metadata": {"name": "a"}, "spec": {"template": tmpl}})
+    assert code == 422 and "spec.selector: Required" in out["message"]
+    code, out = api("POST", ds, {"metadata": {"name": "a"}, "spec": {"selector": {"matchLabels": {"app": "y"}},
+                                                                      "template": tmpl}})
+    assert code == 422 and "does not match template" in out["message"]
+    bare = {"metadata": {"labels": {"app": "x"}}, "spec": {"containers": [{"name": "c"}]}}
+    code, out = api("POST", ds, {"metadata": {"name": "a"}, "spec": {"selector": {"matchLabels": {"app": "x"}},
+                                                                      "template": bare}})
+    assert code == 422 and "name and image" in out["message"]
+    assert api("POST", ds, {"metadata": {"name": "a"}, "spec": {"selector": {"matchLabels": {"app": "x"}},
+                                                                 "template": tmpl}})[0] == 201
+    jobs = f"{k}/apis/batch/v1/namespaces/default/jobs"
+    code, out = api("POST", jobs, {"metadata": {"name": "j"}, "spec": {"template": tmpl}})  # restartPolicy Always
+    assert code == 422 and "restartPolicy" in out["message"]
+    never = json.loads(json.dumps(tmpl))
+    never["spec"]["restartPolicy"] = "Never"
+    assert api("POST", jobs, {"metadata": {"name": "j"}, "spec": {"template": never}})[0] == 201
+    # the framework's own add-ons pass the same validation
+    from triton_kubernetes_amd.k8s.addons import rendered_addons
+    from triton_kubernetes_amd.rancher.fake.k8s import _workload_problem
+
+    for path, obj in rendered_addons({"gpu_count": 8, "node_labeller_image": "rocm/k8s-device-plugin:labeller-x"}):
+        kind = path.rsplit("/", 1)[-1]
+        if kind in ("daemonsets", "deployments", "jobs"):
+            assert _workload_problem(kind, obj) == "", (path, obj["metadata"]["name"])

@@ -43,6 +43,9 @@ Refusals, as a real API server words them (negative tests in
   name that is not fully qualified or repeats, ``sideEffects`` other than None /
   NoneOnDryRun, no v1/v1beta1 ``admissionReviewVersions``, a ``clientConfig`` without
   exactly one of url / service, an unknown ``failurePolicy``) -> 422 ``Invalid``;
+* a DaemonSet / Deployment without a ``spec.selector`` matching its template's labels, a
+  Job whose template's ``restartPolicy`` is not Never / OnFailure, or a pod template
+  without named containers with images -> 422 ``Invalid``;
 * a merge patch that is not a JSON object -> 400.
 """
 
@@ -126,6 +129,33 @@ def _webhook_config_problem(cfg: Dict[str, Any]) -> str:
             return f"{at}.clientConfig: Required value: exactly one of url or service is required"
         if hook.get("failurePolicy", "Fail") not in ("Fail", "Ignore"):
             return f"{at}.failurePolicy: Unsupported value: \"{hook.get('failurePolicy')}\""
+    return ""
+
+
+def _workload_problem(kind: str, obj: Dict[str, Any]) -> str:
+    """What apps/v1 and batch/v1 validation refuses in a DaemonSet / Deployment / Job ("" when
+    valid): a pod template with containers that each have a name and an image; for
+    DaemonSets and Deployments a ``spec.selector`` whose ``matchLabels`` the template's labels
+    carry; for Jobs a ``restartPolicy`` of Never or OnFailure."""
+    spec = obj.get("spec") or {}
+    tmpl = spec.get("template") or {}
+    pod = tmpl.get("spec") or {}
+    containers = pod.get("containers") or []
+    if not containers:
+        return "spec.template.spec.containers: Required value"
+    for i, c in enumerate(containers):
+        if not c.get("name") or not c.get("image"):
+            return f"spec.template.spec.containers[{i}]: Required value: name and image"
+    if kind in ("daemonsets", "deployments"):
+        sel = (spec.get("selector") or {}).get("matchLabels") or {}
+        if not sel and not (spec.get("selector") or {}).get("matchExpressions"):
+            return "spec.selector: Required value"
+        labels = (tmpl.get("metadata") or {}).get("labels") or {}
+        if any(labels.get(k) != v for k, v in sel.items()):
+            return "spec.template.metadata.labels: Invalid value: `selector` does not match template `labels`"
+    if kind == "jobs" and pod.get("restartPolicy") not in ("Never", "OnFailure"):
+        return (f'spec.template.spec.restartPolicy: Required value: valid values: "OnFailure", "Never" '
+                f'(got {pod.get("restartPolicy")!r})')
     return ""
 
 
@@ -329,7 +359,10 @@ class K8sCoreApi:
 
     def _check_object(self, cid: str, kpath: str, body: Any) -> Optional[Reply]:
         """Refusals common to create and replace (see the module docstring); ``kpath`` is
-        the collection."""
+        the collection.  Placement (request body, namespace) first, then content."""
+        return self._check_placement(cid, kpath, body) or self._check_content(kpath, body)
+
+    def _check_placement(self, cid: str, kpath: str, body: Any) -> Optional[Reply]:
         if not isinstance(body, dict):
             return _status(400, "BadRequest", "the request body must be an object")
         meta = body.get("metadata") or {}
@@ -341,6 +374,18 @@ class K8sCoreApi:
             with self.state.mu:
                 if not self._namespace_exists(cid, ns):
                     return _status(404, "NotFound", f'namespaces "{ns}" not found')
+        return None
+
+    @staticmethod
+    def _check_content(kpath: str, body: Dict[str, Any]) -> Optional[Reply]:
+        """What validation and admission refuse in the object itself (after the API server
+        found where it goes and, on replace, that it exists and is current)."""
+        meta = body.get("metadata") or {}
+        kind = kpath.rstrip("/").rsplit("/", 1)[-1]
+        if kind in ("daemonsets", "deployments", "jobs"):
+            problem = _workload_problem(kind, body)
+            if problem:
+                return _status(422, "Invalid", f'{kind[:-1]} "{meta.get("name", "")}" is invalid: {problem}')
         if kpath.rstrip("/") == WEBHOOK_CONFIGS:
             problem = _webhook_config_problem(body)
             if problem:
@@ -391,7 +436,9 @@ class K8sCoreApi:
     def _replace(self, cid: str, kpath: str, body: Any) -> Reply:
         st = self.state
         base, _, name = kpath.rpartition("/")
-        bad = self._check_object(cid, base, body)
+        # as the API server orders them: request (400), existence (404), precondition (409),
+        # then validation and admission of the new content (422 / 403)
+        bad = self._check_placement(cid, base, body)
         if bad is not None:
             return bad
         meta = body.get("metadata") or {}
@@ -409,6 +456,9 @@ class K8sCoreApi:
                 return _status(409, "Conflict", f'Operation cannot be fulfilled on "{name}": the object has been '
                                                 "modified; please apply your changes to the latest version and "
                                                 "try again")
+            bad = self._check_content(base, body)
+            if bad is not None:
+                return bad
             obj = json.loads(json.dumps(body))
             m = obj.setdefault("metadata", {})
             m.update(name=name, uid=cur_meta.get("uid"), creationTimestamp=cur_meta.get("creationTimestamp"),
