@@ -44,8 +44,8 @@ def cluster(tmp_path):
         ("/api/v1/namespaces/ml/configmaps",
          {"apiVersion": "v1", "kind": "ConfigMap", "metadata": {"name": "kube-root-ca.crt", "namespace": "ml"}}),
         ("/api/v1/namespaces/ml/secrets",
-         {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "sa-tok", "namespace": "ml"},
-          "type": "kubernetes.io/service-account-token"}),
+         {"apiVersion": "v1", "kind": "Secret", "metadata": {"name": "sa-tok", "namespace": "ml", "annotations": {
+             "kubernetes.io/service-account.name": "default"}}, "type": "kubernetes.io/service-account-token"}),
         ("/api/v1/namespaces/ml/services",
          {"apiVersion": "v1", "kind": "Service", "metadata": {"name": "svc", "namespace": "ml"},
           "spec": {"clusterIP": "10.43.0.7", "ports": [{"port": 80}]}}),

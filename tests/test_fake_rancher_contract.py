@@ -448,3 +448,30 @@ def test_k8s_workload_validation(fake, api):
         kind = path.rsplit("/", 1)[-1]
         if kind in ("daemonsets", "deployments", "jobs"):
             assert _workload_problem(kind, obj) == "", (path, obj["metadata"]["name"])
+
+
+def test_k8s_core_object_validation(fake, api):
+    cid = _cluster_with_node(fake, api)
+    ns = f"/k8s/clusters/{cid}/api/v1/namespaces/kube-system"
+    cases = [
+        ("secrets", {"metadata": {"name": "s"}, "data": {"k": "not base64!"}}, "illegal base64"),
+        ("secrets", {"metadata": {"name": "s"}, "type": "kubernetes.io/tls", "data": {"tls.crt": "eA=="}},
+         "data[tls.key]: Required"),
+        ("secrets", {"metadata": {"name": "s"}, "type": "kubernetes.io/service-account-token"},
+         "service-account.name"),
+        ("configmaps", {"metadata": {"name": "c"}, "data": {"bad key": "v"}}, "valid config key"),
+        ("services", {"metadata": {"name": "svc"}, "spec": {"ports": [{"port": 70000}]}}, "between 1 and 65535"),
+    ]
+    for kind, body, want in cases:
+        code, out = api("POST", f"{ns}/{kind}", body)
+        assert code == 422 and want in out["message"], (kind, out)
+    rb = f"/k8s/clusters/{cid}/apis/rbac.authorization.k8s.io/v1/clusterrolebindings"
+    code, out = api("POST", rb, {"metadata": {"name": "b"}, "roleRef": {"kind": "ClusterRole", "name": "r"}})
+    assert code == 422 and "roleRef.apiGroup" in out["message"]
+    # the framework's own add-ons pass the same validation
+    from triton_kubernetes_amd.k8s.addons import rendered_addons
+    from triton_kubernetes_amd.k8s.tls import serving_cert
+    from triton_kubernetes_amd.rancher.fake.k8s import _core_problem
+
+    for path, obj in rendered_addons({"gpu_count": 8}, serving_cert("rccl-env-injector", "kube-system")):
+        assert _core_problem(path.rsplit("/", 1)[-1], obj) == "", (path, obj["metadata"]["name"])

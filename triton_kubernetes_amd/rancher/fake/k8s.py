@@ -46,10 +46,17 @@ Refusals, as a real API server words them (negative tests in
 * a DaemonSet / Deployment without a ``spec.selector`` matching its template's labels, a
   Job whose template's ``restartPolicy`` is not Never / OnFailure, or a pod template
   without named containers with images -> 422 ``Invalid``;
+* Secret data that is not base64, a TLS Secret without ``tls.crt`` / ``tls.key``, a
+  service-account token Secret without ``kubernetes.io/service-account.name``, ConfigMap /
+  Secret keys outside ``[-._a-zA-Z0-9]``, Service ports outside 1-65535, a (Cluster)RoleBinding
+  without a complete ``roleRef`` -> 422 ``Invalid``;
 * a merge patch that is not a JSON object -> 400.
 """
 
+import base64
+import binascii
 import json
+import re
 import time
 import uuid
 from typing import Any, Dict, List, Optional, Tuple
@@ -156,6 +163,47 @@ def _workload_problem(kind: str, obj: Dict[str, Any]) -> str:
     if kind == "jobs" and pod.get("restartPolicy") not in ("Never", "OnFailure"):
         return (f'spec.template.spec.restartPolicy: Required value: valid values: "OnFailure", "Never" '
                 f'(got {pod.get("restartPolicy")!r})')
+    return ""
+
+
+_DATA_KEY_RE = re.compile(r"^[-._a-zA-Z0-9]+$")
+
+
+def _core_problem(kind: str, obj: Dict[str, Any]) -> str:
+    """What core/v1 and rbac/v1 validation refuses in the other objects the add-ons apply
+    ("" when valid): Secret ``data`` that is not base64, a ``kubernetes.io/tls`` Secret
+    without ``tls.crt`` / ``tls.key``, a service-account token Secret without its
+    service-account annotation, ConfigMap / Secret keys outside ``[-._a-zA-Z0-9]``, Service
+    ports outside 1-65535, and (Cluster)RoleBindings without a complete ``roleRef``."""
+    if kind in ("secrets", "configmaps"):
+        for field in ("data", "binaryData") if kind == "configmaps" else ("data", "stringData"):
+            for key in (obj.get(field) or {}):
+                if not _DATA_KEY_RE.match(str(key)):
+                    return f"{field}[{key}]: Invalid value: a valid config key must consist of alphanumeric characters, '-', '_' or '.'"
+    if kind == "secrets":
+        data = obj.get("data") or {}
+        for key, val in data.items():
+            try:
+                base64.b64decode(str(val), validate=True)
+            except (ValueError, binascii.Error):
+                return f"data[{key}]: Invalid value: illegal base64 data"
+        have = set(data) | set(obj.get("stringData") or {})
+        if obj.get("type") == "kubernetes.io/tls":
+            for key in ("tls.crt", "tls.key"):
+                if key not in have:
+                    return f"data[{key}]: Required value"
+        if obj.get("type") == "kubernetes.io/service-account-token" and not (
+                (obj.get("metadata") or {}).get("annotations") or {}).get("kubernetes.io/service-account.name"):
+            return "metadata.annotations[kubernetes.io/service-account.name]: Required value"
+    if kind == "services":
+        for i, port in enumerate((obj.get("spec") or {}).get("ports") or []):
+            if not 1 <= int(port.get("port", 0) or 0) <= 65535:
+                return f"spec.ports[{i}].port: Invalid value: must be between 1 and 65535, inclusive"
+    if kind in ("rolebindings", "clusterrolebindings"):
+        ref = obj.get("roleRef") or {}
+        for key in ("apiGroup", "kind", "name"):
+            if not ref.get(key):
+                return f"roleRef.{key}: Required value"
     return ""
 
 
@@ -382,6 +430,9 @@ class K8sCoreApi:
         found where it goes and, on replace, that it exists and is current)."""
         meta = body.get("metadata") or {}
         kind = kpath.rstrip("/").rsplit("/", 1)[-1]
+        problem = _core_problem(kind, body)
+        if problem:
+            return _status(422, "Invalid", f'{kind[:-1]} "{meta.get("name", "")}" is invalid: {problem}')
         if kind in ("daemonsets", "deployments", "jobs"):
             problem = _workload_problem(kind, body)
             if problem:
