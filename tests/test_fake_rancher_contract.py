@@ -116,6 +116,9 @@ def test_v3_cluster_create_refusals(api):
     assert code == 422 and out["fieldName"] == "kubernetesVersion"
     code, out = api("POST", "/v3/cluster", {"rancherKubernetesEngineConfig": {"kubernetesVersion": RKE1}})
     assert code == 422 and out["code"] == "MissingRequired"
+    code, out = api("POST", "/v3/cluster", {"name": "c1", "rancherKubernetesEngineConfig":
+                                            {"kubernetesVersion": RKE1, "network": {"plugin": "cilium"}}})
+    assert code == 422 and out["fieldName"] == "rancherKubernetesEngineConfig.network.plugin"  # RKE2 only
     _rke1(api)
     code, out = api("POST", "/v3/cluster", {"name": "c1", "rancherKubernetesEngineConfig":
                                             {"kubernetesVersion": RKE1}})

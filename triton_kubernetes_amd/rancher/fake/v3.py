@@ -26,7 +26,8 @@ Refusals (negative tests in ``tests/test_fake_rancher_contract.py``, ``test_v3_*
   new password shorter than ``password-min-length`` (12) -> 422;
 * a setting the server does not have -> 404;
 * a cluster without a name -> 422; a name already taken -> 422 ``NotUnique``; a
-  ``kubernetesVersion`` outside ``k8s-versions-current`` -> 422; a downgrade -> 422; a
+  ``kubernetesVersion`` outside ``k8s-versions-current`` or a network plugin RKE1 does not
+  deploy -> 422; a downgrade -> 422; a
   ``PUT`` on an RKE2 (provisioning-owned) cluster -> 422;
 * a registration token for an unknown cluster -> 422; unknown cluster, token or node
   -> 404;
@@ -47,6 +48,8 @@ from ...versions import running_version
 from ..connect import tunnel_params
 
 Reply = Tuple[int, Any]
+# the network plugins RKE1 deploys (rancherKubernetesEngineConfig.network.plugin)
+RKE1_NETWORK_PLUGINS = ("canal", "flannel", "calico", "weave", "none")
 
 
 def _err(code: int, kind: str, message: str = "", **extra: Any) -> Reply:
@@ -158,6 +161,10 @@ class V3Api:
         if version not in offered:
             return _err(422, "InvalidBodyContent", f"{version} is not a supported Kubernetes version",
                         fieldName="kubernetesVersion")
+        plugin = ((body.get("rancherKubernetesEngineConfig") or {}).get("network") or {}).get("plugin", "canal")
+        if plugin not in RKE1_NETWORK_PLUGINS:
+            return _err(422, "InvalidOption", f"{plugin} is not a supported network plugin",
+                        fieldName="rancherKubernetesEngineConfig.network.plugin")
         cid = f"c-{uuid.uuid4().hex[:5]}"
         with st.mu:
             if any(c["name"] == name for c in st.clusters.values()):
