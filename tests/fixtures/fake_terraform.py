@@ -304,6 +304,10 @@ def refresh(doc, keys, root_vars, known_outputs):
             results = {}
             for name, argv, qexpr in external_sources(d):
                 query = evaluate_query(d, qexpr, inputs)
+                bad_q = sorted(k for k, v in (query or {}).items() if not isinstance(v, str))
+                if bad_q:  # the external data source's query is a map of strings
+                    return outs, (f"Incorrect attribute value type\n\n  with module.{key}.data.external.{name}: "
+                                  f"inappropriate value for attribute \"query\": element {bad_q[0]!r}: string required")
                 try:
                     proc = subprocess.run(argv, input=json.dumps(query), capture_output=True,
                                                         text=True, timeout=120)
@@ -318,6 +322,12 @@ def refresh(doc, keys, root_vars, known_outputs):
                     results[name] = json.loads(proc.stdout)
                 except ValueError:
                     return outs, f"Unexpected External Program Results\n\n  with module.{key}.data.external.{name}"
+                res = results[name]
+                if not isinstance(res, dict) or any(not isinstance(v, str) for v in res.values()):
+                    # what Terraform's external data source accepts: a flat JSON object of strings
+                    return outs, (f"Unexpected External Program Results\n\n  with module.{key}.data.external.{name}\n\n"
+                                  "The data source received unexpected results after executing the program.\n\n"
+                                  "Program output must be a JSON encoded map of string keys and string values.")
             for out, (src, field) in data_outputs(d).items():
                 if src in results:
                     outs[f"{key}__{out}"] = str(results[src].get(field, ""))
