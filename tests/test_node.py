@@ -499,7 +499,7 @@ def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
     from triton_kubernetes_amd.node.plan import Step
     from triton_kubernetes_amd.parallel.rccl_env import render_env_file
 
-    env = {k: v for k, v in os.environ.items() if not k.startswith(("NCCL_", "RCCL_"))}
+    env = {k: v for k, v in os.environ.items() if not k.startswith(("NCCL_", "RCCL_", "HSA_"))}
     env["NCCL_DEBUG"] = "INFO"  # set by the unit / operator: kept
     monkeypatch.setattr(os, "environ", env)
     agent = NodeAgent(name="n", mode="sim", devices=[0, 1], root=str(tmp_path))
@@ -526,6 +526,7 @@ def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
         (tmp_path / "etc/rccl/rccl.env").write_text(render_env_file({"NCCL_SOCKET_IFNAME": "=bond1", "NCCL_DEBUG": "TRACE",
                                                                      "HSA_NO_SCRATCH_RECLAIM": "1"}))
         again = agent.apply_node_rccl_env()
-        assert again == {"NCCL_SOCKET_IFNAME": "=bond1"} and env["NCCL_DEBUG"] == "WARN"
+        # at start HIP's HSA_* settings are taken too (HIP reads them once, at its initialisation)
+        assert again == {"NCCL_SOCKET_IFNAME": "=bond1", "HSA_NO_SCRATCH_RECLAIM": "1"} and env["NCCL_DEBUG"] == "WARN"
     finally:
         agent.stop()

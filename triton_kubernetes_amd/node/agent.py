@@ -255,8 +255,11 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             pass
 
     # RCCL settings the gate's communicators need from the node's environment: RCCL reads
-    # them once per process, so they must be in place before the agent's first RCCL call
+    # them once per process, so they must be in place before the agent's first RCCL call.
+    # HSA_* (the ROCm runtime's, e.g. fine-grained PCIe memory for RDMA) are read once at
+    # HIP's initialisation: they are applied at agent start only
     RCCL_ENV_PREFIXES = ("NCCL_", "RCCL_")
+    STARTUP_ENV_PREFIXES = RCCL_ENV_PREFIXES + ("HSA_",)
 
     def apply_node_rccl_env(self) -> Dict[str, str]:
         """Put the node's RCCL settings into this process's environment, for the agent's own
@@ -264,7 +267,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         systemd unit also loads it, ``EnvironmentFile=``), else what the node's RDMA ports say
         (``parallel/rccl_env.py:site_env_from_topology``: ``NCCL_IB_HCA``, the RoCE v2 GID
         index) -- so even the first bring-up after boot gates over the right ports.  Keys the
-        process environment already sets win; returns what was applied."""
+        process environment already sets win; returns what was applied.  Called before the
+        agent's first HIP or RCCL call (``warm_native``)."""
         from ..parallel.rccl_env import parse_env_file, site_env_from_topology
 
         try:
@@ -277,7 +281,7 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
                 env = {}
         applied = {}
         for k, v in env.items():
-            if k.startswith(self.RCCL_ENV_PREFIXES) and k not in os.environ:
+            if k.startswith(self.STARTUP_ENV_PREFIXES) and k not in os.environ:
                 os.environ[k] = v
                 applied[k] = v
         return applied
