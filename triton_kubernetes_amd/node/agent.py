@@ -225,7 +225,7 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
 
         # RCCL reads its settings once per process, the bootstrap interface at the first
         # unique id (made below): the node's RCCL environment goes in first
-        self.rccl_env_applied = self.apply_node_rccl_env()
+        self.rccl_env_applied = self.apply_node_rccl_env() if os.environ.get("TK_AGENT_RCCL_ENV", "1") != "0" else {}
         probe._lib()
         rccl._lib()
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
