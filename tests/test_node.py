@@ -490,9 +490,9 @@ def test_gpu_links_cli_verdict(monkeypatch, capsys):
 
 def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
     """The agent's cluster gate runs RCCL in the agent process, and RCCL reads its settings
-    once per process: the node's /etc/rccl/rccl.env (else its discovered RDMA ports) goes into
-    the agent's environment before its first RCCL call; the rccl_env step updates what RCCL
-    has not read yet and reports it; the process's own settings win."""
+    once per process: the node's /etc/rccl/rccl.env goes into the agent's environment before
+    its first RCCL call; the rccl_env step applies the configured settings RCCL has not read
+    yet and reports them; the process's own settings win."""
     import os
 
     from triton_kubernetes_amd.node.agent import NodeAgent
@@ -504,29 +504,25 @@ def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
     monkeypatch.setattr(os, "environ", env)
     agent = NodeAgent(name="n", mode="sim", devices=[0, 1], root=str(tmp_path))
     try:
-        # no file yet (first boot): the node's RDMA ports decide
-        topo = {"gpus": [], "nics": [{"name": "mlx5_0", "port": 1, "link_layer": "Ethernet", "roce_v2_gid_index": 3},
-                                     {"name": "mlx5_1", "port": 1, "link_layer": "Ethernet", "roce_v2_gid_index": 3}]}
-        monkeypatch.setattr(agent, "_topology", lambda: topo)
-        applied = agent.apply_node_rccl_env()
-        assert applied == {"NCCL_IB_HCA": "=mlx5_0:1,mlx5_1:1", "NCCL_IB_GID_INDEX": "3"}
-        assert env["NCCL_IB_HCA"] == "=mlx5_0:1,mlx5_1:1" and env["NCCL_DEBUG"] == "INFO"
+        # first boot, no file: RCCL detects the RDMA ports itself, nothing is set
+        assert agent.apply_node_rccl_env() == {} and "NCCL_IB_HCA" not in env
 
-        # the bring-up's rccl_env step: the configured values win in the file, and what
-        # differs from this process's environment is applied and reported
+        # the bring-up's rccl_env step: the file gets the discovered and the configured values;
+        # the configured ones that differ from this process's environment are applied now
+        topo = {"gpus": [], "nics": [{"name": "mlx5_0", "port": 1, "link_layer": "Ethernet", "roce_v2_gid_index": 3}]}
         step = Step("rccl_env", "rccl_env", "", {"env": {"NCCL_SOCKET_IFNAME": "=bond0", "NCCL_DEBUG": "WARN",
                                                           "HSA_FORCE_FINE_GRAIN_PCIE": "1"}})
         out = agent._run_step(None, step, {"labels": {}, "capacity": {}, "taints": [], "topology": topo})
         assert out["agent_env_updated"] == ["NCCL_DEBUG", "NCCL_SOCKET_IFNAME"]
         assert env["NCCL_SOCKET_IFNAME"] == "=bond0" and "HSA_FORCE_FINE_GRAIN_PCIE" not in env
+        assert "NCCL_IB_HCA" not in env and 'NCCL_IB_HCA="=mlx5_0:1"' in (tmp_path / "etc/rccl/rccl.env").read_text()
 
-        # a later start reads the file the bring-up wrote (the unit's own values still win)
-        for k in ("NCCL_IB_HCA", "NCCL_IB_GID_INDEX", "NCCL_SOCKET_IFNAME"):
-            del env[k]
+        # a later start reads the file (HIP's HSA_* settings too: HIP reads them once, at its
+        # initialisation); the unit's own values still win
+        del env["NCCL_SOCKET_IFNAME"]
         (tmp_path / "etc/rccl/rccl.env").write_text(render_env_file({"NCCL_SOCKET_IFNAME": "=bond1", "NCCL_DEBUG": "TRACE",
                                                                      "HSA_NO_SCRATCH_RECLAIM": "1"}))
         again = agent.apply_node_rccl_env()
-        # at start HIP's HSA_* settings are taken too (HIP reads them once, at its initialisation)
         assert again == {"NCCL_SOCKET_IFNAME": "=bond1", "HSA_NO_SCRATCH_RECLAIM": "1"} and env["NCCL_DEBUG"] == "WARN"
     finally:
         agent.stop()

@@ -263,22 +263,20 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
 
     def apply_node_rccl_env(self) -> Dict[str, str]:
         """Put the node's RCCL settings into this process's environment, for the agent's own
-        communicators (the cluster gate): ``/etc/rccl/rccl.env`` when a bring-up wrote it (the
-        systemd unit also loads it, ``EnvironmentFile=``), else what the node's RDMA ports say
-        (``parallel/rccl_env.py:site_env_from_topology``: ``NCCL_IB_HCA``, the RoCE v2 GID
-        index) -- so even the first bring-up after boot gates over the right ports.  Keys the
-        process environment already sets win; returns what was applied.  Called before the
-        agent's first HIP or RCCL call (``warm_native``)."""
-        from ..parallel.rccl_env import parse_env_file, site_env_from_topology
+        communicators (the cluster gate): ``/etc/rccl/rccl.env`` as the last bring-up wrote it
+        (the systemd unit loads the same file, ``EnvironmentFile=``; this covers agents started
+        another way).  Keys the process environment already sets win.  Without the file RCCL
+        detects the node's RDMA ports itself, which is what the discovered settings would say
+        (every active port; RoCE v2 GIDs) -- measured: setting them anyway added ~0.1-0.2 s to
+        a cold communicator init on MI355X (``profiles/round4/rccl_env_ab.txt``).  Returns
+        what was applied.  Called before the agent's first HIP or RCCL call (``warm_native``)."""
+        from ..parallel.rccl_env import parse_env_file
 
         try:
             with open(self.path("/etc/rccl/rccl.env"), "r", encoding="utf-8") as fh:
                 env = parse_env_file(fh.read())
         except OSError:
-            try:
-                env = site_env_from_topology(self._topology())
-            except Exception:  # noqa: BLE001 - no topology: RCCL's own defaults
-                env = {}
+            return {}
         applied = {}
         for k, v in env.items():
             if k.startswith(self.STARTUP_ENV_PREFIXES) and k not in os.environ:

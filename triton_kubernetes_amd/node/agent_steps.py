@@ -282,13 +282,15 @@ class AgentStepsMixin:
             env.update(step.params.get("env", {}))
             out = {"file": self.write_file("/etc/rccl/rccl.env", render_env_file(env)), "discovered": discovered}
             if self.topology_override is None and self.devices:
-                # this agent's own gate runs in this process: RCCL settings it has not read yet
-                # take effect now; ones RCCL already read (the bootstrap interface, fixed by the
-                # first unique id) take effect when the agent restarts (its unit loads the file)
-                changed = sorted(k for k, v in env.items()
+                # this agent's own gate runs in this process: the configured RCCL settings it
+                # has not read yet take effect now; ones RCCL already read (the bootstrap
+                # interface, fixed by the first unique id) when the agent restarts (its unit
+                # loads the file).  Discovered ones are what RCCL detects by itself
+                configured = step.params.get("env", {}) or {}
+                changed = sorted(k for k, v in configured.items()
                                  if k.startswith(self.RCCL_ENV_PREFIXES) and os.environ.get(k) != str(v))
                 for k in changed:
-                    os.environ[k] = str(env[k])
+                    os.environ[k] = str(configured[k])
                 if changed:
                     out["agent_env_updated"] = changed
             return out
