@@ -491,8 +491,8 @@ def test_gpu_links_cli_verdict(monkeypatch, capsys):
 def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
     """The agent's cluster gate runs RCCL in the agent process, and RCCL reads its settings
     once per process: the node's /etc/rccl/rccl.env goes into the agent's environment before
-    its first RCCL call; the rccl_env step applies the configured settings RCCL has not read
-    yet and reports them; the process's own settings win."""
+    its first RCCL call; the rccl_env step reports configured settings that differ (they take
+    effect at the next start); the process's own settings win."""
     import os
 
     from triton_kubernetes_amd.node.agent import NodeAgent
@@ -508,21 +508,21 @@ def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
         assert agent.apply_node_rccl_env() == {} and "NCCL_IB_HCA" not in env
 
         # the bring-up's rccl_env step: the file gets the discovered and the configured values;
-        # the configured ones that differ from this process's environment are applied now
+        # the configured ones that differ from this process's environment are reported, not
+        # changed under the running agent (RCCL threads read the environment)
         topo = {"gpus": [], "nics": [{"name": "mlx5_0", "port": 1, "link_layer": "Ethernet", "roce_v2_gid_index": 3}]}
         step = Step("rccl_env", "rccl_env", "", {"env": {"NCCL_SOCKET_IFNAME": "=bond0", "NCCL_DEBUG": "WARN",
                                                           "HSA_FORCE_FINE_GRAIN_PCIE": "1"}})
         out = agent._run_step(None, step, {"labels": {}, "capacity": {}, "taints": [], "topology": topo})
-        assert out["agent_env_updated"] == ["NCCL_DEBUG", "NCCL_SOCKET_IFNAME"]
-        assert env["NCCL_SOCKET_IFNAME"] == "=bond0" and "HSA_FORCE_FINE_GRAIN_PCIE" not in env
+        assert out["agent_env_differs"] == ["NCCL_DEBUG", "NCCL_SOCKET_IFNAME"]
+        assert "NCCL_SOCKET_IFNAME" not in env and env["NCCL_DEBUG"] == "INFO"
         assert "NCCL_IB_HCA" not in env and 'NCCL_IB_HCA="=mlx5_0:1"' in (tmp_path / "etc/rccl/rccl.env").read_text()
 
         # a later start reads the file (HIP's HSA_* settings too: HIP reads them once, at its
         # initialisation); the unit's own values still win
-        del env["NCCL_SOCKET_IFNAME"]
         (tmp_path / "etc/rccl/rccl.env").write_text(render_env_file({"NCCL_SOCKET_IFNAME": "=bond1", "NCCL_DEBUG": "TRACE",
                                                                      "HSA_NO_SCRATCH_RECLAIM": "1"}))
         again = agent.apply_node_rccl_env()
-        assert again == {"NCCL_SOCKET_IFNAME": "=bond1", "HSA_NO_SCRATCH_RECLAIM": "1"} and env["NCCL_DEBUG"] == "WARN"
+        assert again == {"NCCL_SOCKET_IFNAME": "=bond1", "HSA_NO_SCRATCH_RECLAIM": "1"} and env["NCCL_DEBUG"] == "INFO"
     finally:
         agent.stop()

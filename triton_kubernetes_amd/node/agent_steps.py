@@ -282,17 +282,16 @@ class AgentStepsMixin:
             env.update(step.params.get("env", {}))
             out = {"file": self.write_file("/etc/rccl/rccl.env", render_env_file(env)), "discovered": discovered}
             if self.topology_override is None and self.devices:
-                # this agent's own gate runs in this process: the configured RCCL settings it
-                # has not read yet take effect now; ones RCCL already read (the bootstrap
-                # interface, fixed by the first unique id) when the agent restarts (its unit
-                # loads the file).  Discovered ones are what RCCL detects by itself
+                # this agent's own gate runs RCCL in this process, with the environment the
+                # agent started with (it loads this file at start, and so does its unit).  The
+                # environment is not changed under a running agent: RCCL's threads read it
+                # (getenv) while a communicator initialises, and changing it then is a data
+                # race.  Configured settings that differ take effect at the agent's next start
                 configured = step.params.get("env", {}) or {}
-                changed = sorted(k for k, v in configured.items()
+                differs = sorted(k for k, v in configured.items()
                                  if k.startswith(self.RCCL_ENV_PREFIXES) and os.environ.get(k) != str(v))
-                for k in changed:
-                    os.environ[k] = str(configured[k])
-                if changed:
-                    out["agent_env_updated"] = changed
+                if differs:
+                    out["agent_env_differs"] = differs
             return out
         if a == "rccl_slim":
             # an agent chose its runtime at start (its unit's ExecStartPre prepared the
