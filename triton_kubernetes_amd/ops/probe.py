@@ -261,11 +261,14 @@ def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, pas
     got: "queue.Queue[str]" = queue.Queue()
 
     def read_verdict() -> None:
-        for text in proc.stdout:
-            if text.startswith("{"):
+        verdict = ""
+        for text in proc.stdout:  # read to the end: a child writing after its verdict never blocks on the pipe
+            if text.startswith("{") and not verdict:
+                verdict = text
                 got.put(text)
-                return
-        got.put("")
+        if not verdict:
+            got.put("")
+        proc.stdout.close()
 
     threading.Thread(target=read_verdict, name=f"tk-span-{dev}", daemon=True).start()
     try:
