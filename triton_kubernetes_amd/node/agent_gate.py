@@ -25,6 +25,7 @@ from typing import Any, Dict, List, Optional, Tuple
 
 from ..utils.trace import span
 
+
 class _SimGate:
     """Stand-in for ops.rccl.GateComm on agents with synthetic GPUs (no RCCL)."""
 
@@ -43,6 +44,7 @@ class _SimGate:
 
     def cancel(self) -> None:
         pass
+
 
 class AgentGateMixin:
     """Mixin of :class:`~.agent.NodeAgent`: this node's ranks of cluster RCCL gates."""
@@ -208,5 +210,6 @@ class AgentGateMixin:
         out["pipelined"] = pipelined
         out["ranks"] = list(range(rank, rank + len(gate.devices)))
         return out
+
 
 __all__ = ["AgentGateMixin"]
