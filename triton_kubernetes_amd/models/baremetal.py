@@ -21,7 +21,7 @@ from ..config.context import Context, expand_home, file_exists, not_blank
 from ..errors import ConfigError
 from ..state import MANAGER_KEY, State, cluster_key_parts
 from .. import versions
-from ..parallel.rccl_env import default_rccl_env
+from ..parallel.rccl_env import default_rccl_env, env_problems
 from .common import add_nodes, base_cluster_config, base_manager_config, base_node_config, omit_empty, source_for
 
 MANAGER_MODULE = "terraform/modules/bare-metal-rancher"
@@ -152,7 +152,12 @@ def _mi355x_fields(ctx: Context) -> Dict:
         raise ConfigError(f"Invalid gpu_burnin '{burnin}', must be one of the following: quick, full, off")
     env = default_rccl_env()
     overrides = s.get("rccl_env")
+    if s.is_set("rccl_env") and not isinstance(overrides, dict):
+        raise ConfigError("rccl_env must be a map of NCCL_*, RCCL_* and HSA_* settings.")
     if isinstance(overrides, dict):
+        bad = env_problems(overrides)
+        if bad:
+            raise ConfigError(f"Invalid {bad[0]}.")
         env.update({str(k): str(v) for k, v in overrides.items()})
     out = {
         "gpu_product": "MI355X",

@@ -11,9 +11,22 @@ host (:func:`site_env_from_topology`, ``amdgpu-topo-labeller --rccl-env``) and w
 as ``NCCL_IB_HCA`` (+ the ports' RoCE v2 GID index, read from ``gid_attrs/types``);
 ``rccl_env`` overrides in the node
 config win over both the defaults and the discovered values.
+
+What the file may hold (:func:`env_problems`).  The node agent's service loads it
+(``EnvironmentFile=``), the Terraform host script sources it, and the agent applies it at
+start, all as root.  So whoever can put a setting into it would otherwise run code there:
+``NCCL_NET_PLUGIN`` / ``NCCL_TUNER_PLUGIN`` / ``HSA_TOOLS_LIB`` / ``RCCL_ROCR_PATH`` load a
+library, ``NCCL_DEBUG_FILE`` / ``HSA_COREDUMP_PATTERN`` write a path, and a value with a
+newline or a quote adds lines of its own (``LD_PRELOAD=...``).  Only ``NCCL_*``, ``RCCL_*``
+and ``HSA_*`` keys are accepted, none that names a library, plugin, file, path or
+directory, and values are comma lists of plain tokens (an address range's ``/N`` allowed).
+The same rules are the host module's ``rccl_env`` variable validation
+(``terraform/generate.py``), the config check (``models/baremetal.py``) and the agent's
+plan refusal (``node/agent.py``).
 """
 
-from typing import Any, Dict, Mapping
+import re
+from typing import Any, Dict, List, Mapping
 
 # Values chosen for MI355X nodes; every one can be overridden per node.
 _DEFAULTS: Dict[str, str] = {
@@ -49,6 +62,39 @@ def site_env_from_topology(topology: Mapping[str, Any]) -> Dict[str, str]:
     return env
 
 
+# RE2-compatible (Terraform's regexall uses the same strings)
+ENV_KEY_RE = "^(NCCL|RCCL|HSA)_[A-Z0-9_]+$"
+ENV_KEY_DENY_RE = "(^|_)(PLUGIN|LIB|TOOLS|PATTERN|CONF|SCRIPT|DIR|PATH|[A-Z]*FILE)(_|$)"
+ENV_ITEM_RE = "^[A-Za-z0-9_.:=^+-]*(/[0-9]{1,3})?$"
+ENV_VALUE_MAX = 256
+
+
+def env_problems(env: Any) -> List[str]:
+    """Why ``env`` may not be a node's RCCL environment (empty: it may).  See the module
+    docstring."""
+    if not isinstance(env, Mapping):
+        return ["rccl_env must be a map of NCCL_*, RCCL_* and HSA_* settings"]
+    out = []
+    for k, v in env.items():
+        k, v = str(k), str(v)
+        if not re.fullmatch(ENV_KEY_RE, k):
+            out.append(f"rccl_env key {k[:64]!r}: only NCCL_*, RCCL_* and HSA_* settings (upper case) are accepted")
+            continue
+        if re.search(ENV_KEY_DENY_RE, k):
+            out.append(f"rccl_env key {k}: names a library, plugin, file or path, which the node's RCCL "
+                       "environment does not accept (the node agent's service loads it as root)")
+        if len(v) > ENV_VALUE_MAX or not all(re.fullmatch(ENV_ITEM_RE, item) for item in v.split(",")):
+            out.append(f"rccl_env {k}: value {v[:48]!r} may hold only a comma list of letters, digits and "
+                       f"_ . : = ^ + - (an address range's /N allowed), at most {ENV_VALUE_MAX} characters")
+    return out
+
+
+def check_env(env: Mapping[str, Any]) -> None:
+    bad = env_problems(env)
+    if bad:
+        raise ValueError("; ".join(bad))
+
+
 def default_rccl_env() -> Dict[str, str]:
     return dict(_DEFAULTS)
 
@@ -60,6 +106,7 @@ def merged_env(overrides: Mapping[str, str] = ()) -> Dict[str, str]:
 
 
 def render_env_file(env: Mapping[str, str]) -> str:
+    check_env(env)  # no writer can emit a setting, or a line, the file may not hold
     lines = ["# RCCL / HSA environment for MI355X (written by triton-kubernetes)"]
     for k in sorted(env):
         v = str(env[k]).replace('"', '\\"')

@@ -30,6 +30,7 @@ from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from .. import sizing, versions
+from ..parallel import rccl_env
 from . import scripts
 from .catalog import MODULES_DIR
 
@@ -143,6 +144,14 @@ VAR_DOCS = {
 # (HCL string "['\"\\\\]" is the RE2 class ['"\\]: single quote, double quote, backslash)
 _SHELL_SAFE = (r'length(regexall("[' + "'" + r'\"\\\\]", var.{0})) == 0', "{0} must not contain quotes or backslashes.")
 VAR_VALIDATIONS = {
+    # the node's RCCL environment file is loaded as root (parallel/rccl_env.py:env_problems)
+    "rccl_env": ('alltrue([for k, v in var.rccl_env : length(regexall("' + rccl_env.ENV_KEY_RE + '", k)) > 0 && '
+                 'length(regexall("' + rccl_env.ENV_KEY_DENY_RE + '", k)) == 0 && '
+                 f'length(v) <= {rccl_env.ENV_VALUE_MAX} && '
+                 'alltrue([for item in split(",", v) : length(regexall("' + rccl_env.ENV_ITEM_RE + '", item)) > 0])])',
+                 "rccl_env takes NCCL_*, RCCL_* and HSA_* settings whose values are comma lists of letters, digits and "
+                 "_ . : = ^ + - (an address range's /N allowed); settings that name a library, plugin, file, path or "
+                 "directory are not accepted."),
     "rancher_admin_password": (f'length(var.rancher_admin_password) >= {versions.PASSWORD_MIN_LENGTH} && '
                                + _SHELL_SAFE[0].format("rancher_admin_password"),
                                f"rancher_admin_password must be at least {versions.PASSWORD_MIN_LENGTH} characters "

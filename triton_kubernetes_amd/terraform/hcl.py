@@ -854,7 +854,11 @@ _FUNCS = {
     "contains": lambda lst, v: v in lst,
     "split": lambda sep, v: str(v).split(str(sep)),
     "slice": lambda lst, a, b: list(lst)[int(a):int(b)],
-    "regexall": lambda pat, v: __import__("re").findall(str(pat), str(v)),
+    # RE2's "$" matches only at the end of the text (Python's also before a final newline)
+    "regexall": lambda pat, v: __import__("re").findall(__import__("re").sub(r"(?<!\\)\$", r"\\Z", str(pat)),
+                                                        str(v)),
+    "alltrue": lambda items: all(x is True or x == "true" for x in items),
+    "anytrue": lambda items: any(x is True or x == "true" for x in items),
 }
 
 
@@ -943,6 +947,25 @@ def eval_expr(node: Node, env: Dict[str, Any]) -> Any:
         if fn is None:
             raise TemplateError(f"function {node.value}() is not supported by this evaluator")
         return fn(*[eval_expr(c, env) for c in node.children])
+    if k == "for":
+        # [for k, v in coll : value if cond] / {for k, v in coll : key => value if cond}; a
+        # map is walked in key order, as Terraform does
+        names = node.value["names"]
+        coll = eval_expr(node.children[0], env)
+        pairs = sorted(coll.items()) if isinstance(coll, dict) else list(enumerate(coll))
+        obj = node.value["object"]
+        body = node.children[1:3] if obj else node.children[1:2]
+        cond = node.children[len(body) + 1] if len(node.children) > len(body) + 1 else None
+        out_list, out_obj = [], {}
+        for key, val in pairs:
+            scope = dict(env, **({names[0]: key, names[1]: val} if len(names) == 2 else {names[0]: val}))
+            if cond is not None and not eval_expr(cond, scope):
+                continue
+            if obj:
+                out_obj[_to_str(eval_expr(body[0], scope))] = eval_expr(body[1], scope)
+            else:
+                out_list.append(eval_expr(body[0], scope))
+        return out_obj if obj else out_list
     raise TemplateError(f"unsupported expression {k}")
 
 

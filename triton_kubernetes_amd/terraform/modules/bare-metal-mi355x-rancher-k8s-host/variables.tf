@@ -156,6 +156,11 @@ variable "rccl_env" {
   description = "RCCL / HSA environment for GPU pods"
   type        = map(string)
   default     = {}
+
+  validation {
+    condition     = alltrue([for k, v in var.rccl_env : length(regexall("^(NCCL|RCCL|HSA)_[A-Z0-9_]+$", k)) > 0 && length(regexall("(^|_)(PLUGIN|LIB|TOOLS|PATTERN|CONF|SCRIPT|DIR|PATH|[A-Z]*FILE)(_|$)", k)) == 0 && length(v) <= 256 && alltrue([for item in split(",", v) : length(regexall("^[A-Za-z0-9_.:=^+-]*(/[0-9]{1,3})?$", item)) > 0])])
+    error_message = "rccl_env takes NCCL_*, RCCL_* and HSA_* settings whose values are comma lists of letters, digits and _ . : = ^ + - (an address range's /N allowed); settings that name a library, plugin, file, path or directory are not accepted."
+  }
 }
 
 variable "rccl_min_busbw" {

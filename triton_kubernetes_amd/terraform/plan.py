@@ -265,8 +265,30 @@ def _f_replace(s, sub, rep):
     return s.replace(sub, rep)
 
 
+def re2(pattern: str) -> str:
+    """A Terraform (RE2) pattern for Python's ``re``: RE2's ``$`` matches only at the end of
+    the text (without the ``m`` flag), Python's also before a final newline."""
+    return re.sub(r"(?<!\\)\$", r"\\Z", pattern)
+
+
+def _f_alltrue(items):
+    return all(_tf_bool(x) for x in items)
+
+
+def _f_anytrue(items):
+    return any(_tf_bool(x) for x in items)
+
+
+def _tf_bool(v):
+    if isinstance(v, bool):
+        return v
+    if v in ("true", "false"):
+        return v == "true"
+    raise PlanError(f"a bool is required, got {v!r}")
+
+
 def _f_regexall(pattern, s):
-    rx = re.compile(_tf_str(pattern))
+    rx = re.compile(re2(_tf_str(pattern)))
     out = []
     for m in rx.finditer(_tf_str(s)):
         if rx.groups == 0:
@@ -325,6 +347,8 @@ def _f_jsonencode(v):
 
 # name -> (callable, min args, max args or None)
 FUNCTIONS: Dict[str, Tuple[Callable[..., Any], int, Optional[int]]] = {
+    "alltrue": (_f_alltrue, 1, 1),
+    "anytrue": (_f_anytrue, 1, 1),
     "base64encode": (lambda s: base64.b64encode(_tf_str(s).encode()).decode(), 1, 1),
     "concat": (lambda *ls: [x for lst in ls for x in lst], 0, None),
     "contains": (_f_contains, 2, 2),
