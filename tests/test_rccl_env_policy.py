@@ -134,3 +134,22 @@ def test_host_module_validates_rccl_env():
         assert any("rccl_env" in p for p in problems), (bad, problems)
         errors = plan_module(mod, inputs, check_files=False).errors
         assert any("Invalid value for variable 'rccl_env'" in e for e in errors), (bad, errors)
+
+
+def test_agent_refuses_a_metrics_step_outside_an_absolute_directory(tmp_path):
+    """The metrics textfile is written by the agent as root: its directory is checked on the
+    node as at create (an absolute path without "..")."""
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.plan import BootstrapPlan, Step
+
+    agent = NodeAgent(name="n", mode="sim", devices=[], root=str(tmp_path))
+    try:
+        def plan(d):
+            return BootstrapPlan(hostname="n", role="worker", rancher_url="https://r", token="t", ca_checksum="c",
+                                 steps=[Step("gpu_metrics", "gpu_metrics", "", {"dir": d})])
+
+        for bad in ("relative/dir", "/var/../etc", "", None):
+            assert agent.refusals(plan(bad)), bad
+        assert agent.refusals(plan("/var/lib/node_exporter/textfile")) == []
+    finally:
+        agent.stop()

@@ -138,7 +138,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         RKE1 hands it to a privileged ``rancher-agent``) or image (RKE1) is outside the
         node's allow-list; an ``rccl_env`` step with a setting the node's RCCL environment
         may not hold (one naming a library, plugin or path, or a value that is not plain
-        tokens: ``parallel/rccl_env.py:env_problems``)."""
+        tokens: ``parallel/rccl_env.py:env_problems``); a ``gpu_metrics`` step whose
+        directory is not an absolute path free of ``..``."""
         from ..parallel.rccl_env import env_problems
 
         out = []
@@ -146,6 +147,18 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             if s.action == "rccl_env":
                 # the file this step writes is loaded as root by the agent's service
                 out.extend(env_problems(s.params.get("env", {}) or {}))
+                continue
+            if s.action == "gpu_metrics":
+                # the agent writes the textfile as root: an absolute directory, no "..",
+                # as the config check requires (node/metrics.py:textfile_dir_of)
+                from ..errors import ConfigError
+                from .metrics import textfile_dir_of
+
+                try:
+                    if not textfile_dir_of({"gpu_metrics_textfile": s.params.get("dir")}):
+                        out.append("gpu_metrics step without a directory")
+                except ConfigError as exc:
+                    out.append(str(exc))
                 continue
             if s.action != "agent":
                 continue
