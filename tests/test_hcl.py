@@ -159,3 +159,20 @@ def test_check_inputs_evaluates_the_modules_validations():
                                    "gpu_count": "eight"})
     assert any(e.startswith("rancher_host_labels:") for e in errs) and any(e.startswith("gpu_burnin:") for e in errs)
     assert any("gpu_count: 'eight' is not a number" == e for e in errs), errs
+
+
+@pytest.mark.parametrize("src,want", [
+    ('[for k, v in m : "${k}=${v}"]', ["a=1", "b=2"]),
+    ('[for v in l : upper(v) if v != "y"]', ["X", "Z"]),
+    ('[for i, v in l : i]', [0, 1, 2]),
+    ('{for k, v in m : v => k}', {"1": "a", "2": "b"}),
+    ('alltrue([for v in l : length(v) == 1])', True),
+    ('anytrue([for v in l : v == "q"])', False),
+    ('length(regexall("^W$", "W\\n"))', 0),  # RE2: "$" is the end of the text
+])
+def test_expression_evaluator_for_expressions_and_list_predicates(src, want):
+    """for-expressions (lists, maps in key order, object form, if filters), alltrue/anytrue,
+    and RE2's end-of-text "$": what the modules' variable validations use."""
+    body = hcl.parse(f"x = {src}\n")
+    expr = body.attr("x").expr
+    assert hcl.eval_expr(expr, {"m": {"b": "2", "a": "1"}, "l": ["x", "y", "z"]}) == want
