@@ -179,4 +179,5 @@ class AgentHTTPMixin:
         h, p = self._server.server_address[:2]
         return f"{'https' if ssl_context is not None else 'http'}://{h}:{p}"
 
+
 __all__ = ["AgentHTTPMixin"]
