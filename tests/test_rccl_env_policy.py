@@ -153,3 +153,32 @@ def test_agent_refuses_a_metrics_step_outside_an_absolute_directory(tmp_path):
         assert agent.refusals(plan("/var/lib/node_exporter/textfile")) == []
     finally:
         agent.stop()
+
+
+def test_numeric_gpu_settings_are_written_plainly_and_validated():
+    """The link floors and the busbw gate go into the host script's argv: the config writes
+    them as plain numbers (the form the module's validation accepts) and refuses the rest."""
+    from triton_kubernetes_amd.config import Context, Settings
+    from triton_kubernetes_amd.errors import ConfigError
+    from triton_kubernetes_amd.models.baremetal import _mi355x_fields
+    from triton_kubernetes_amd.terraform import hcl
+    from triton_kubernetes_amd.terraform.catalog import MODULES_DIR
+
+    def cfg(**kw):
+        return _mi355x_fields(Context(settings=Settings(dict({"non-interactive": True, "gpu": "mi355x",
+                                                              "gpu_count": "8"}, **kw), env={})))
+
+    got = cfg(rccl_min_busbw="1e3", gpu_link_min_gbps="38.50", gpu_link_min_frac=".5")
+    assert (got["rccl_min_busbw"], got["gpu_link_min_gbps"], got["gpu_link_min_frac"]) == ("1000", "38.5", "0.5")
+    for key, bad in (("rccl_min_busbw", "nan"), ("rccl_min_busbw", "-1"), ("gpu_link_min_gbps", "inf"),
+                     ("gpu_link_min_frac", "1.5"), ("gpu_link_min_gbps", "1; id")):
+        with pytest.raises(ConfigError, match=key):
+            cfg(**{key: bad})
+    mod = os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host")
+    base = {"hostname": "g", "rancher_api_url": "https://r", "rancher_cluster_registration_token": "t",
+            "rancher_cluster_ca_checksum": "c", "rancher_host_labels": {"worker": "true"}, "host": "10.0.0.9"}
+    assert not [p for p in hcl.check_inputs(mod, dict(base, rccl_min_busbw=got["rccl_min_busbw"],
+                                                      gpu_link_min_gbps=got["gpu_link_min_gbps"],
+                                                      gpu_link_min_frac=got["gpu_link_min_frac"])) if "min" in p]
+    for key, bad in (("rccl_min_busbw", "1; id"), ("gpu_link_min_gbps", "-3"), ("gpu_link_min_frac", "2")):
+        assert any(key in p for p in hcl.check_inputs(mod, dict(base, **{key: bad}))), key

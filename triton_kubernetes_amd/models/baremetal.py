@@ -15,6 +15,7 @@ MI355X additions (BASELINE.json north star):
   the RCCL readiness Job, applied once the cluster is active.
 """
 
+import math
 from typing import Dict, List
 
 from ..config.context import Context, expand_home, file_exists, not_blank
@@ -136,6 +137,19 @@ def new_node(ctx: Context, manager: str, cluster: str, backend, state: State) ->
     return add_nodes(state, cluster, base, extra, per_node=[{"host": h} for h in hosts])
 
 
+def _plain_number(text: str, message: str, hi: float = math.inf) -> str:
+    """A finite number in [0, hi], written plainly ("38", "0.5", "1000" for "1e3"): the form
+    the host module's validation accepts and its script passes to the node tools."""
+    try:
+        v = float(text)
+        if not (math.isfinite(v) and 0.0 <= v <= hi):
+            raise ValueError
+    except ValueError as exc:
+        raise ConfigError(f"{message}. Found '{text}'.") from exc
+    out = f"{v:.6f}".rstrip("0").rstrip(".")
+    return out or "0"
+
+
 def _mi355x_fields(ctx: Context) -> Dict:
     s = ctx.settings
     count = s.get_string("gpu_count") if s.is_set("gpu_count") else (
@@ -166,34 +180,19 @@ def _mi355x_fields(ctx: Context) -> Dict:
         "rccl_env": env,
     }
     if s.is_set("rccl_min_busbw"):
-        busbw = s.get_string("rccl_min_busbw")
-        try:
-            if float(busbw) < 0:
-                raise ValueError
-        except ValueError as exc:
-            raise ConfigError(f"rccl_min_busbw must be a non-negative number. Found '{busbw}'.") from exc
-        out["rccl_min_busbw"] = busbw
+        out["rccl_min_busbw"] = _plain_number(s.get_string("rccl_min_busbw"),
+                                              "rccl_min_busbw must be a non-negative number")
     if s.is_set("gpu_link_min_frac"):
-        frac = s.get_string("gpu_link_min_frac")
-        try:
-            if not 0.0 <= float(frac) <= 1.0:
-                raise ValueError
-        except ValueError as exc:
-            raise ConfigError(f"gpu_link_min_frac must be a number between 0 and 1. Found '{frac}'.") from exc
-        out["gpu_link_min_frac"] = frac
+        out["gpu_link_min_frac"] = _plain_number(s.get_string("gpu_link_min_frac"),
+                                                 "gpu_link_min_frac must be a number between 0 and 1", hi=1.0)
     if s.is_set("gpu_compute_partition") or s.is_set("gpu_memory_partition"):
         from ..node.partition import normalize
 
         c, m = normalize(s.get_string("gpu_compute_partition") or None, s.get_string("gpu_memory_partition") or None)
         out["gpu_compute_partition"], out["gpu_memory_partition"] = c, m
     if s.is_set("gpu_link_min_gbps"):
-        floor = s.get_string("gpu_link_min_gbps")
-        try:
-            if float(floor) < 0:
-                raise ValueError
-        except ValueError as exc:
-            raise ConfigError(f"gpu_link_min_gbps must be a non-negative number. Found '{floor}'.") from exc
-        out["gpu_link_min_gbps"] = floor
+        out["gpu_link_min_gbps"] = _plain_number(s.get_string("gpu_link_min_gbps"),
+                                                 "gpu_link_min_gbps must be a non-negative number")
     # GPU health policy at bring-up (node/health.py): fail | taint | off, and its limits
     from ..node.health import limits_of, policy_of
 

@@ -143,7 +143,15 @@ VAR_DOCS = {
 # values spliced into single-quoted shell words and JSON bodies by the bootstrap scripts
 # (HCL string "['\"\\\\]" is the RE2 class ['"\\]: single quote, double quote, backslash)
 _SHELL_SAFE = (r'length(regexall("[' + "'" + r'\"\\\\]", var.{0})) == 0', "{0} must not contain quotes or backslashes.")
+_NON_NEG = "^[0-9]+([.][0-9]+)?$"
 VAR_VALIDATIONS = {
+    # numbers the host script passes to the node tools' argv
+    "rccl_min_busbw": (f'length(regexall("{_NON_NEG}", var.rccl_min_busbw)) > 0',
+                       "rccl_min_busbw must be a non-negative number (GB/s)."),
+    "gpu_link_min_gbps": (f'length(regexall("{_NON_NEG}", var.gpu_link_min_gbps)) > 0',
+                          "gpu_link_min_gbps must be a non-negative number (GB/s)."),
+    "gpu_link_min_frac": ('length(regexall("^(0([.][0-9]+)?|1([.]0+)?|[.][0-9]+)$", var.gpu_link_min_frac)) > 0',
+                          "gpu_link_min_frac must be a number between 0 and 1."),
     # the node's RCCL environment file is loaded as root (parallel/rccl_env.py:env_problems)
     "rccl_env": ('alltrue([for k, v in var.rccl_env : length(regexall("' + rccl_env.ENV_KEY_RE + '", k)) > 0 && '
                  'length(regexall("' + rccl_env.ENV_KEY_DENY_RE + '", k)) == 0 && '

@@ -167,12 +167,22 @@ variable "rccl_min_busbw" {
   description = "node-level all-reduce bus bandwidth gate (GB/s)"
   type        = string
   default     = "0"
+
+  validation {
+    condition     = length(regexall("^[0-9]+([.][0-9]+)?$", var.rccl_min_busbw)) > 0
+    error_message = "rccl_min_busbw must be a non-negative number (GB/s)."
+  }
 }
 
 variable "gpu_link_min_frac" {
   description = "fail the node when a GPU pair's peer copy bandwidth is below this fraction of the node median"
   type        = string
   default     = "0.5"
+
+  validation {
+    condition     = length(regexall("^(0([.][0-9]+)?|1([.]0+)?|[.][0-9]+)$", var.gpu_link_min_frac)) > 0
+    error_message = "gpu_link_min_frac must be a number between 0 and 1."
+  }
 }
 
 variable "gpu_compute_partition" {
@@ -201,6 +211,11 @@ variable "gpu_link_min_gbps" {
   description = "fail the node when a GPU pair's kernel-driven peer read is below this many GB/s (absolute floor: half of one xGMI link's ~76.8 GB/s one way)"
   type        = string
   default     = "38"
+
+  validation {
+    condition     = length(regexall("^[0-9]+([.][0-9]+)?$", var.gpu_link_min_gbps)) > 0
+    error_message = "gpu_link_min_gbps must be a non-negative number (GB/s)."
+  }
 }
 
 variable "gpu_host_tuning" {
