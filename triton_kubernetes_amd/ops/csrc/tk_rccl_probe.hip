@@ -689,10 +689,15 @@ extern "C" int tkr_sweep_local(int ndev, const size_t* sizes, int nsizes, int it
     auto run = [&](int n) -> int {
       for (int it = 0; it < n; ++it) {
         NCCLCHECK(ncclGroupStart());
-        for (int d = 0; d < ndev; ++d)
-          NCCLCHECK(ncclAllReduce(bufs[d].send, bufs[d].recv, count, nccl_type(dtype), ncclSum, comms[d],
-                                  bufs[d].stream));
-        NCCLCHECK(ncclGroupEnd());
+        ncclResult_t r = ncclSuccess;
+        for (int d = 0; d < ndev && r == ncclSuccess; ++d)
+          r = ncclAllReduce(bufs[d].send, bufs[d].recv, count, nccl_type(dtype), ncclSum, comms[d], bufs[d].stream);
+        const ncclResult_t re = ncclGroupEnd();  // balanced even after a failed call inside the group
+        if (r == ncclSuccess) r = re;
+        if (r != ncclSuccess) {
+          snprintf(g_err, sizeof(g_err), "ncclAllReduce: %s", ncclGetErrorString(r));
+          return -2;
+        }
       }
       return 0;
     };
