@@ -13,7 +13,7 @@ import subprocess
 
 import pytest
 
-from triton_kubernetes_amd.terraform import catalog, generate, scripts
+from triton_kubernetes_amd.terraform import catalog, generate, hcl, scripts
 
 MODULES = generate.modules()
 BY_NAME = {m.name: m for m in MODULES}
@@ -176,3 +176,23 @@ def test_hcl_is_lexically_well_formed(mod):
         assert not _hcl_structure_errors(text), (mod.name, rel, _hcl_structure_errors(text))
     assert _hcl_structure_errors('a = { b = "x"') == ["line 1: '{' never closed"]
     assert _hcl_structure_errors('a = "${var.x}" }')[0].startswith("line 1: unbalanced")
+
+
+@pytest.mark.parametrize("module", ["bare-metal-mi355x-rancher-k8s-host", "bare-metal-rancher-k8s-host"])
+@pytest.mark.parametrize("key,bad", [
+    ("rancher_api_url", "https://r'; curl x | sh; '"), ("rancher_api_url", "ftp://r"),
+    ("rancher_cluster_registration_token", "t' $(id) '"), ("rancher_cluster_ca_checksum", "c;id"),
+    ("hostname", "h'x"), ("hostname", "-h"), ("rancher_registry_password", "p'w"),
+    ("rancher_agent_image", "rancher/agent; id"), ("docker_install_sha256", "zz"),
+])
+def test_host_modules_refuse_values_that_would_break_out_of_the_script(module, key, bad):
+    """The host scripts put these values inside single quotes or on a command line; the
+    modules' validations refuse quotes and shell syntax, as the node agent does for its own
+    steps (node/agent_steps.py)."""
+    mod = os.path.join(catalog.MODULES_DIR, module)
+    base = {"hostname": "gpu-1.example", "rancher_api_url": "https://rancher.example:8443",
+            "rancher_cluster_registration_token": "abc123xyz", "rancher_cluster_ca_checksum": "0a" * 32,
+            "rancher_host_labels": {"worker": "true"}, "host": "10.0.0.9"}
+    assert not [p for p in hcl.check_inputs(mod, base) if "must be" in p or "must not" in p]
+    problems = hcl.check_inputs(mod, dict(base, **{key: bad}))
+    assert any(key in p for p in problems), (key, bad, problems)

@@ -144,7 +144,27 @@ VAR_DOCS = {
 # (HCL string "['\"\\\\]" is the RE2 class ['"\\]: single quote, double quote, backslash)
 _SHELL_SAFE = (r'length(regexall("[' + "'" + r'\"\\\\]", var.{0})) == 0', "{0} must not contain quotes or backslashes.")
 _NON_NEG = "^[0-9]+([.][0-9]+)?$"
+# values the host scripts put inside single quotes or on a command line (the node agent checks
+# the same fields with node/agent_steps.py's patterns): no quote, space or shell syntax
+_URL = "^https?://[][A-Za-z0-9._:-]+(/[A-Za-z0-9._/-]*)?$"
+_SHELL_WORDS = {
+    "rancher_api_url": (_URL, "an http(s) URL"),
+    "rancher_cluster_registration_token": ("^[A-Za-z0-9._:-]{1,512}$", "a Rancher registration token"),
+    "rancher_cluster_ca_checksum": ("^[A-Za-z0-9]{0,128}$", "a hex checksum (or empty)"),
+    "rancher_agent_image": ("^[A-Za-z0-9][A-Za-z0-9._/:@-]{0,254}$", "a container image reference"),
+    "rancher_registry": ("^([A-Za-z0-9][A-Za-z0-9._/:@-]{0,254})?$", "a registry host (or empty)"),
+    "docker_engine_install_url": ("^(https?://[][A-Za-z0-9._:-]+(/[A-Za-z0-9._/~%+=-]*)?)?$",
+                                  "an http(s) URL (or empty)"),
+    "docker_install_sha256": ("^[A-Fa-f0-9]{0,64}$", "a sha256 hex digest (or empty)"),
+    "hostname": ("^[A-Za-z0-9]([-A-Za-z0-9.]{0,251}[A-Za-z0-9])?$", "a DNS host name"),
+}
 VAR_VALIDATIONS = {
+    **{name: (f'length(regexall("{pat}", var.{name})) > 0', f"{name} must be {what}.")
+       for name, (pat, what) in _SHELL_WORDS.items()},
+    "rancher_registry_username": (_SHELL_SAFE[0].format("rancher_registry_username"),
+                                  _SHELL_SAFE[1].format("rancher_registry_username")),
+    "rancher_registry_password": (_SHELL_SAFE[0].format("rancher_registry_password"),
+                                  _SHELL_SAFE[1].format("rancher_registry_password")),
     # numbers the host script passes to the node tools' argv
     "rccl_min_busbw": (f'length(regexall("{_NON_NEG}", var.rccl_min_busbw)) > 0',
                        "rccl_min_busbw must be a non-negative number (GB/s)."),

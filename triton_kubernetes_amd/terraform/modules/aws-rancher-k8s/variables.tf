@@ -17,6 +17,11 @@ variable "tk_operation" {
 variable "rancher_api_url" {
   description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
   type        = string
+
+  validation {
+    condition     = length(regexall("^https?://[][A-Za-z0-9._:-]+(/[A-Za-z0-9._/-]*)?$", var.rancher_api_url)) > 0
+    error_message = "rancher_api_url must be an http(s) URL."
+  }
 }
 
 variable "rancher_access_key" {
@@ -67,12 +72,22 @@ variable "rancher_registry" {
   description = "Private registry serving the Rancher images (empty: Docker Hub)."
   type        = string
   default     = ""
+
+  validation {
+    condition     = length(regexall("^([A-Za-z0-9][A-Za-z0-9._/:@-]{0,254})?$", var.rancher_registry)) > 0
+    error_message = "rancher_registry must be a registry host (or empty)."
+  }
 }
 
 variable "rancher_registry_username" {
   description = "User for rancher_registry."
   type        = string
   default     = ""
+
+  validation {
+    condition     = length(regexall("['\"\\\\]", var.rancher_registry_username)) == 0
+    error_message = "rancher_registry_username must not contain quotes or backslashes."
+  }
 }
 
 variable "rancher_registry_password" {
@@ -80,6 +95,11 @@ variable "rancher_registry_password" {
   type        = string
   default     = ""
   sensitive   = true
+
+  validation {
+    condition     = length(regexall("['\"\\\\]", var.rancher_registry_password)) == 0
+    error_message = "rancher_registry_password must not contain quotes or backslashes."
+  }
 }
 
 variable "k8s_registry" {

@@ -47,12 +47,22 @@ variable "docker_engine_install_url" {
   description = "The URL to the shell script to install the docker engine."
   type        = string
   default     = "https://releases.rancher.com/install-docker/24.0.sh"
+
+  validation {
+    condition     = length(regexall("^(https?://[][A-Za-z0-9._:-]+(/[A-Za-z0-9._/~%+=-]*)?)?$", var.docker_engine_install_url)) > 0
+    error_message = "docker_engine_install_url must be an http(s) URL (or empty)."
+  }
 }
 
 variable "docker_install_sha256" {
   description = "SHA-256 the downloaded runtime install script must match (empty: not checked)."
   type        = string
   default     = ""
+
+  validation {
+    condition     = length(regexall("^[A-Fa-f0-9]{0,64}$", var.docker_install_sha256)) > 0
+    error_message = "docker_install_sha256 must be a sha256 hex digest (or empty)."
+  }
 }
 
 variable "rancher_server_image" {
@@ -65,18 +75,33 @@ variable "rancher_agent_image" {
   description = "The Rancher Agent image to use."
   type        = string
   default     = "rancher/rancher-agent:v2.10.3"
+
+  validation {
+    condition     = length(regexall("^[A-Za-z0-9][A-Za-z0-9._/:@-]{0,254}$", var.rancher_agent_image)) > 0
+    error_message = "rancher_agent_image must be a container image reference."
+  }
 }
 
 variable "rancher_registry" {
   description = "The docker registry to use for rancher server and agent images"
   type        = string
   default     = ""
+
+  validation {
+    condition     = length(regexall("^([A-Za-z0-9][A-Za-z0-9._/:@-]{0,254})?$", var.rancher_registry)) > 0
+    error_message = "rancher_registry must be a registry host (or empty)."
+  }
 }
 
 variable "rancher_registry_username" {
   description = "The username to login as."
   type        = string
   default     = ""
+
+  validation {
+    condition     = length(regexall("['\"\\\\]", var.rancher_registry_username)) == 0
+    error_message = "rancher_registry_username must not contain quotes or backslashes."
+  }
 }
 
 variable "rancher_registry_password" {
@@ -84,6 +109,11 @@ variable "rancher_registry_password" {
   type        = string
   default     = ""
   sensitive   = true
+
+  validation {
+    condition     = length(regexall("['\"\\\\]", var.rancher_registry_password)) == 0
+    error_message = "rancher_registry_password must not contain quotes or backslashes."
+  }
 }
 
 variable "gcp_path_to_credentials" {

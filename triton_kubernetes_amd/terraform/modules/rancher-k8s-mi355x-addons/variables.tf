@@ -6,6 +6,11 @@ variable "name" {
 variable "rancher_api_url" {
   description = "Base URL of the Rancher server (the cluster manager's rancher_url output)."
   type        = string
+
+  validation {
+    condition     = length(regexall("^https?://[][A-Za-z0-9._:-]+(/[A-Za-z0-9._/-]*)?$", var.rancher_api_url)) > 0
+    error_message = "rancher_api_url must be an http(s) URL."
+  }
 }
 
 variable "rancher_access_key" {
