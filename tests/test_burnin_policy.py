@@ -170,10 +170,10 @@ def test_span_child_reports_before_it_releases(span_child, monkeypatch):
     import time
 
     argv_log, released = span_child
-    monkeypatch.setenv("FAKE_RELEASE_S", "1.5")
+    monkeypatch.setenv("FAKE_RELEASE_S", "3.0")
     t0 = time.monotonic()
     res = probe.memtest_span_process(3, 0, headroom=4 << 30, passes=3)
-    assert time.monotonic() - t0 < 1.2  # did not wait for the release
+    assert time.monotonic() - t0 < 2.5  # did not wait for the release (margin for a loaded CPU)
     assert res["errors"] == 0 and res["bytes"] == 300 << 30 and res["free_ms"] == 0.0
     assert released == [3]  # this process's arena is part of the span
     assert argv_log.read_text().split() == ["--memtest-span", "--device", "3", "--span-bytes", "0",
@@ -181,7 +181,7 @@ def test_span_child_reports_before_it_releases(span_child, monkeypatch):
                                             "--span-chunk", str(probe.SPAN_CHILD_CHUNK)]
     assert [d for d, _ in probe._span_children] == [3]
     probe.wait_frees()
-    assert time.monotonic() - t0 >= 1.4 and probe._span_children == []
+    assert time.monotonic() - t0 >= 2.9 and probe._span_children == []
 
 
 def test_span_child_waits_only_for_its_own_device(span_child, monkeypatch):
@@ -189,13 +189,13 @@ def test_span_child_waits_only_for_its_own_device(span_child, monkeypatch):
     for each other; a device's next span waits for its previous one's release."""
     import time
 
-    monkeypatch.setenv("FAKE_RELEASE_S", "1.0")
+    monkeypatch.setenv("FAKE_RELEASE_S", "2.5")
     t0 = time.monotonic()
     probe.memtest_span_process(0, 1 << 30)
     probe.memtest_span_process(1, 1 << 30)
-    assert time.monotonic() - t0 < 0.9
+    assert time.monotonic() - t0 < 2.2  # (margin for a loaded CPU)
     probe.memtest_span_process(0, 1 << 30)  # waits for device 0's first child
-    assert time.monotonic() - t0 >= 1.0
+    assert time.monotonic() - t0 >= 2.5
     probe.wait_frees()
 
 

@@ -171,7 +171,7 @@ def test_unsupported_module_and_parallel_fanout(env):
     t0 = time.time()
     new_cluster(ctx, backend)
     assert len(rec.plans) == 40
-    assert time.time() - t0 < 2.5, "node bootstrap must fan out concurrently"
+    assert time.time() - t0 < 5.0, "node bootstrap must fan out concurrently (one by one: 8 s)"
     assert client.ping()
 
 
