@@ -349,3 +349,28 @@ def test_fake_rancher_node_delete_keeps_cluster_index(env):
     client.http.request("DELETE", f"/v3/nodes/{gpu['id']}", ok=(200,))
     assert {n["metadata"]["name"] for n in fake.k8s_nodes(cid)} == {"cp-1", "etcd-1"}
     assert gpu["id"] not in fake.state.nodes and gpu["id"] not in fake.state.cluster_nodes[cid]
+
+
+def test_direct_executor_refuses_what_terraform_would(env):
+    """A document edited by hand (or written by another tool) with a value a module's
+    validation refuses: `terraform plan` would stop with "Invalid value for variable", and
+    the DirectExecutor stops the same way, before it touches a host."""
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    rec = RecordingTransport()
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="c1",
+                        k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel",
+                        nodes=[{"rancher_host_label": "worker", "node_count": 1, "hostname": "g", "ssh_user": "u",
+                                "bastion_host": "", "key_path": "k", "hosts": ["10.1.0.1"], "gpu": "mi355x",
+                                "gpu_count": 8}]))
+    ctx.extras["transport"] = TransportRouter(ssh=rec, agent=AgentTransport(token=TOKEN))
+    new_cluster(ctx, backend)
+    st = backend.state("mgr")
+    key = next(k for k, m in st.modules().items() if "mi355x-rancher-k8s-host" in str(m.get("source")))
+    mod = dict(st.module(key))
+    mod["rccl_env"] = dict(mod.get("rccl_env") or {}, NCCL_NET_PLUGIN="/tmp/evil.so")
+    st.set_module(key, mod)
+    plans_before = len(rec.plans)
+    with pytest.raises(TKError, match="rccl_env"):
+        DirectExecutor(transport=TransportRouter(ssh=rec, agent=AgentTransport(token=TOKEN))).apply(st, backend)
+    assert len(rec.plans) == plans_before

@@ -45,6 +45,7 @@ from ..parallel.transport import HostRef, Transport, TransportRouter
 from ..rancher.client import RancherClient, wait_until
 from ..state import State
 from ..terraform.catalog import ModuleInfo, check_sources, module_from_source
+from ..terraform import hcl
 from ..utils.trace import span
 from ..versions import DEFAULT_DISTRIBUTION, bootstrap_password, default_version
 from .base import Executor, outputs_from_tfstate
@@ -346,6 +347,12 @@ class DirectExecutor(Executor):
                       manager_name: str) -> Tuple[Dict[str, str], Any]:
         cfg = resolve(copy.deepcopy(run.cfg), outputs)
         kind = run.info.kind
+        # what `terraform plan` would refuse about this call (unknown or missing arguments,
+        # types, the variables' validation blocks), refused here too: the same document must
+        # not apply through one executor and fail through the other
+        problems = hcl.check_inputs(run.info.local_dir, cfg, cached=True)
+        if problems:
+            raise ExecutorError(f"module.{run.key} ({run.info.name}): " + "; ".join(problems[:3]))
         with span(f"module.{kind}", key=run.key, module=run.info.name):
             if kind == "manager":
                 return self._apply_manager(cfg), None

@@ -26,6 +26,7 @@ The reference ships Terraform 0.11 modules and has no checker; this is new
 
 import os
 import re
+import threading
 from dataclasses import dataclass, field
 from typing import Any, Dict, List, Optional, Set, Tuple
 
@@ -1055,12 +1056,32 @@ def _var_type_ok(vtype: str, value: Any) -> bool:
     return True
 
 
-def check_inputs(module_dir: str, inputs: Dict[str, Any]) -> List[str]:
+_REPORTS: Dict[str, Tuple[Tuple[Tuple[str, int], ...], "ModuleReport"]] = {}
+_REPORTS_MU = threading.Lock()
+
+
+def module_report(module_dir: str) -> "ModuleReport":
+    """:func:`check_module`, cached while the module's ``.tf`` files are unchanged (the
+    DirectExecutor checks every module call it applies; a parse per call would be waste)."""
+    stamp = tuple(sorted((fn, os.stat(os.path.join(module_dir, fn)).st_mtime_ns)
+                         for fn in os.listdir(module_dir) if fn.endswith(".tf")))
+    with _REPORTS_MU:
+        hit = _REPORTS.get(module_dir)
+    if hit is not None and hit[0] == stamp:
+        return hit[1]
+    rep = check_module(module_dir)
+    with _REPORTS_MU:
+        _REPORTS[module_dir] = (stamp, rep)
+    return rep
+
+
+def check_inputs(module_dir: str, inputs: Dict[str, Any], cached: bool = False) -> List[str]:
     """What ``terraform plan`` would reject about one module call: unknown inputs, missing
     required variables, values of the wrong type, and failing ``validation`` conditions
     (evaluated with this module's evaluator).  Inputs that are interpolations
-    (``${module...}``) are only known at apply time and skip the value checks."""
-    rep = check_module(module_dir)
+    (``${module...}``) are only known at apply time and skip the value checks.  ``cached``:
+    reuse the module's parse while its files are unchanged (:func:`module_report`)."""
+    rep = module_report(module_dir) if cached else check_module(module_dir)
     errors = list(rep.errors)
     given = {k: v for k, v in inputs.items() if k != "source"}
     errors += [f"unsupported argument {k!r}" for k in sorted(set(given) - rep.variables)]
