@@ -182,3 +182,11 @@ def test_numeric_gpu_settings_are_written_plainly_and_validated():
                                                       gpu_link_min_frac=got["gpu_link_min_frac"])) if "min" in p]
     for key, bad in (("rccl_min_busbw", "1; id"), ("gpu_link_min_gbps", "-3"), ("gpu_link_min_frac", "2")):
         assert any(key in p for p in hcl.check_inputs(mod, dict(base, **{key: bad}))), key
+
+
+def test_discovered_ports_with_odd_names_are_left_to_rccl():
+    topo = {"nics": [{"name": "mlx5_0", "port": 1, "link_layer": "InfiniBand"},
+                     {"name": "x\nLD_PRELOAD=/tmp/y", "port": 1, "link_layer": "InfiniBand"},
+                     {"name": "mlx5_1", "port": 0, "link_layer": "InfiniBand"}]}
+    env = site_env_from_topology(topo)
+    assert env == {"NCCL_IB_HCA": "=mlx5_0:1"} and env_problems(env) == []

@@ -50,7 +50,10 @@ def site_env_from_topology(topology: Mapping[str, Any]) -> Dict[str, str]:
     discovered by the labeller): every active port in ``NCCL_IB_HCA`` (exact names), and
     the RoCE v2 GID index the Ethernet ports share (``roce_v2_gid_index``).  Mirror of
     ``csrc/tk_topo.cpp:render_rccl_env``; explicit per-node ``rccl_env`` keys override it."""
-    active = [n for n in topology.get("nics", []) or [] if n.get("port", 0) > 0]
+    # a port whose name is not a plain device name (sysfs gives mlx5_0, bnxt_re1, irdma0, ...)
+    # is left to RCCL's own detection rather than written into a file loaded as root
+    active = [n for n in topology.get("nics", []) or [] if int(n.get("port", 0) or 0) > 0
+              and re.fullmatch(r"[A-Za-z0-9_.-]{1,64}", str(n.get("name", "")))]
     if not active:
         return {}
     env = {"NCCL_IB_HCA": "=" + ",".join(f"{n['name']}:{n['port']}" for n in active)}
