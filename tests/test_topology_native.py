@@ -277,3 +277,16 @@ def test_labeller_clean_under_asan_ubsan(tmp_path):
         if ref:
             want = subprocess.run([ref] + argv, capture_output=True, text=True).stdout
             assert run.stdout == want
+
+
+def test_rdma_port_with_an_odd_name_stays_out_of_the_rccl_env(tmp_path, native_ok):
+    """A port name that is not a plain device name is left to RCCL's own detection by both
+    renderers (the file is loaded as root): the C++ labeller and the Python mirror agree."""
+    from triton_kubernetes_amd.parallel.rccl_env import site_env_from_topology
+
+    odd = [("mlx5_0", "4: ACTIVE", "InfiniBand", "400 Gb/sec (4X NDR)", "ib0", 0),
+           ("x$(id)", "4: ACTIVE", "InfiniBand", "400 Gb/sec (4X NDR)", "ib1", 0)]
+    root = add_rdma(make_tree(str(tmp_path), ngpu=2), odd)
+    doc = topo.native_topology("sysfs", root)
+    assert sorted(n["name"] for n in doc["nics"]) == ["mlx5_0", "x$(id)"]
+    assert topo.native_rccl_env(root) == site_env_from_topology(doc) == {"NCCL_IB_HCA": "=mlx5_0:1"}

@@ -978,11 +978,21 @@ std::string render_labels(const Topology& t) {
 // Mirrored in parallel/rccl_env.py:site_env_from_topology.
 // NCCL_IB_GID_INDEX is set only when every active RoCE port has its RoCE v2 GID at the
 // same index; otherwise RCCL picks one per port itself (RoCE v2, IPv4 first, by default).
+// A plain device name (sysfs: mlx5_0, bnxt_re1, irdma0, ...): anything else is left to RCCL's
+// own detection rather than written into a file the node's services load as root
+// (parallel/rccl_env.py:site_env_from_topology applies the same rule).
+static bool plain_device_name(const std::string& s) {
+  if (s.empty() || s.size() > 64) return false;
+  for (char c : s)
+    if (!(std::isalnum(static_cast<unsigned char>(c)) || c == '_' || c == '.' || c == '-')) return false;
+  return true;
+}
+
 std::string render_rccl_env(const Topology& t) {
   std::string hca;
   std::set<int> gids;
   for (const auto& n : t.nics) {
-    if (n.port <= 0) continue;
+    if (n.port <= 0 || !plain_device_name(n.name)) continue;
     hca += (hca.empty() ? "" : ",") + n.name + ":" + std::to_string(n.port);
     if (lower(n.link_layer) == "ethernet") gids.insert(n.gid_index);
   }
