@@ -251,6 +251,7 @@ def test_provider_and_module_accept_the_modes():
         _mi355x_fields(make_ctx({"gpu_compute_partition": "spx", "gpu_memory_partition": "nps2"}))
     mod = os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host")
     assert hcl.check_inputs(mod, {"gpu_compute_partition": "cpx", "gpu_memory_partition": "nps2", "host": "h",
-                                  "hostname": "h", "rancher_api_url": "https://r", "rancher_cluster_registration_token": "t",
+                                  "hostname": "h", "rancher_api_url": "https://r",
+                                  "rancher_cluster_registration_token": "t",
                                   "rancher_cluster_ca_checksum": "c", "rancher_host_labels": {"worker": "true"}}) == []
     assert hcl.check_inputs(mod, {"gpu_compute_partition": "tpx"})

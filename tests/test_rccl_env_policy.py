@@ -17,7 +17,8 @@ from triton_kubernetes_amd.parallel.rccl_env import (default_rccl_env, env_probl
                                                       render_env_file, site_env_from_topology)
 
 DENIED_KEYS = ["NCCL_NET_PLUGIN", "NCCL_TUNER_PLUGIN", "NCCL_PROFILER_PLUGIN", "HSA_TOOLS_LIB", "RCCL_ROCR_PATH",
-               "NCCL_DEBUG_FILE", "NCCL_CONF_FILE", "NCCL_TOPO_FILE", "NCCL_TOPO_DUMP_FILE", "NCCL_GRAPH_DUMP_FILE_RANK",
+               "NCCL_DEBUG_FILE", "NCCL_CONF_FILE", "NCCL_TOPO_FILE", "NCCL_TOPO_DUMP_FILE",
+               "NCCL_GRAPH_DUMP_FILE_RANK",
                "HSA_COREDUMP_PATTERN", "HSA_MODEL_LIB", "HSA_MODEL_MEMFILE", "RCCL_REPLAY_FILE", "HSA_REV_COPY_DIR"]
 BAD_VALUES = ["WARN\nLD_PRELOAD=/tmp/x.so", 'WARN"', "$(id)", "`id`", "/tmp/evil.so", "lib/evil.so", "a b",
               "x" * 300, "WARN\\"]
