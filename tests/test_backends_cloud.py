@@ -288,24 +288,28 @@ def test_manta_expired_lock_taken_over_by_exactly_one(manta):
     be = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://triton", fake.url)
     be.client.put_directory("/stor/triton-kubernetes/mgr")
     be.client.put_object("/stor/triton-kubernetes/mgr/.lock", json.dumps({"token": "dead", "expires": 0}).encode())
-    winners = []
+    winners, losers = [], []
     start = threading.Barrier(4)
     release = threading.Event()
 
     def worker(i):
         start.wait()
         try:
-            with be.lock("mgr", timeout=0.3, poll=0.01):
+            with be.lock("mgr", timeout=1.0, poll=0.01):
                 winners.append(i)
-                release.wait(2)
+                release.wait(30)
         except Exception:  # noqa: BLE001 - the losers time out while the winner holds it
-            pass
+            losers.append(i)
 
     threads = [threading.Thread(target=worker, args=(i,)) for i in range(4)]
     for t in threads:
         t.start()
-    time.sleep(0.6)
+    # the winner holds the lock until every other thread has given up (on a loaded machine a
+    # loser's last attempt can still be in flight well after its timeout)
+    deadline = time.monotonic() + 30
+    while len(losers) < 3 and time.monotonic() < deadline:
+        time.sleep(0.02)
     release.set()
     for t in threads:
         t.join()
-    assert len(winners) == 1
+    assert len(winners) == 1 and len(losers) == 3
