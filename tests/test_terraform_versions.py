@@ -207,18 +207,20 @@ def test_manta_lock_is_reentrant_and_renewed(manta, monkeypatch):
 
     fake, be = manta
     path = "/acct/stor/triton-kubernetes/mgr/.lock"
-    with be.lock("mgr", ttl=0.3):
+    # TTL and waits sized for a loaded CPU (every Manta request is signed): the heartbeat
+    # renews well inside the TTL, and the other writer's wait spans more than one TTL
+    with be.lock("mgr", ttl=1.5):
         first = fake.objects[path]
         with be.lock("mgr"):  # same thread: no deadlock
             pass
         assert path in fake.objects
-        time.sleep(0.45)  # past the TTL: the heartbeat has re-PUT it
+        time.sleep(2.0)  # past the TTL: the heartbeat has re-PUT it
         assert fake.objects[path] != first
         got = []
 
         def other():
             try:
-                with be.lock("mgr", timeout=0.2, poll=0.02):
+                with be.lock("mgr", timeout=1.8, poll=0.05):
                     got.append(True)
             except TKError:
                 got.append(False)
