@@ -247,7 +247,10 @@ def test_manta_lock_lost_to_a_takeover_refuses_writes(manta):
         # another CLI found the lock expired and replaced it (If-Match on the old etag)
         fake.objects[path] = (json.dumps({"token": "other", "expires": time.time() + 900}).encode(),
                               "application/json", "etag-of-the-other-writer")
-        time.sleep(0.45)  # the heartbeat's If-Match fails: the lock is lost
+        # the heartbeat's If-Match fails: the lock is lost (waited for, not slept on: the
+        # heartbeat may run late on a loaded CPU)
+        lost = be._held.lost["mgr"]
+        assert lost.wait(10)
         with pytest.raises(BackendError, match="taken over by another writer"):
             be.write_tfstate("mgr", b"{}")
         with pytest.raises(BackendError, match="taken over"):
