@@ -400,19 +400,35 @@ def main() -> int:
             dist.barrier()
         sync()
 
-    for w in range(args.warmup):
-        barrier()
-        cold_step(-1 - w)
-    barrier()
-    TRACER.reset()
     results = []
-    t_start = time.perf_counter()
-    for i in range(args.steps):
-        results.append(cold_step(i))
-    sync()
-    if distributed:
-        dist.barrier()
-    elapsed = time.perf_counter() - t_start
+    try:
+        for w in range(args.warmup):
+            barrier()
+            cold_step(-1 - w)
+        barrier()
+        TRACER.reset()
+        t_start = time.perf_counter()
+        for i in range(args.steps):
+            results.append(cold_step(i))
+        sync()
+        if distributed:
+            dist.barrier()
+        elapsed = time.perf_counter() - t_start
+    except Exception as exc:
+        if rank == 0:
+            # a failed run still says what failed, in the line's own shape (value null), before
+            # the traceback: the first run on a new node shape must leave a diagnosis
+            print(json.dumps({
+                "metric": METRIC, "value": None, "unit": "s", "n_gpus": n_gpus, "steps": args.steps,
+                "warmup": args.warmup, "ms_per_step": None, "higher_is_better": False, "scaling": "weak",
+                "vs_baseline": None, "dtype": "n/a", "data": "FAILED: no measurement",
+                "config": {"model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology "
+                                    "labels", "workers": workers, "gpus_per_worker": gpus_per_worker,
+                           "visible_gpus": visible, "global_batch": "n/a", "seq_len": "n/a",
+                           "parallelism": f"{workers} worker node(s) x {gpus_per_worker} GPU(s)",
+                           "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate},
+                "error": f"{type(exc).__name__}: {exc}"[:2000], "completed_steps": len(results)}), flush=True)
+        raise
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)

@@ -110,3 +110,30 @@ def test_bench_eight_ranks_gate_over_eight_gpus(masked):
     doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][0])
     assert doc["n_gpus"] == 8 and doc["rccl_gate_ranks"] == [8]
     assert doc["config"]["workers"] == (8 if masked else 1)
+
+
+def test_bench_failure_still_prints_a_diagnostic_line():
+    """A run that fails (here: the second create) prints the line's shape with value null and
+    the error, then fails: the first run on a new node shape leaves a diagnosis."""
+    snippet = """
+import sys
+sys.path.insert(0, %r)
+sys.argv = ["bench.py", "--sim-gpu", "--steps", "2", "--warmup", "1", "--warm-steps", "0", "--agents", "inproc"]
+import triton_kubernetes_amd.workflows as wf
+orig, n = wf.new_cluster, []
+def boom(ctx, backend):
+    n.append(1)
+    if len(n) >= 2:
+        raise RuntimeError("gate failed on purpose")
+    return orig(ctx, backend)
+wf.new_cluster = boom
+import bench
+bench.main()
+""" % ROOT
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    res = subprocess.run([sys.executable, "-c", snippet], capture_output=True, text=True, timeout=300, env=env,
+                         cwd=ROOT)
+    assert res.returncode != 0
+    line = json.loads(next(ln for ln in res.stdout.splitlines() if ln.startswith("{")))
+    assert line["value"] is None and line["ms_per_step"] is None and line["completed_steps"] == 0
+    assert "gate failed on purpose" in line["error"] and line["n_gpus"] == 1
