@@ -292,8 +292,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         (the systemd unit loads the same file, ``EnvironmentFile=``; this covers agents started
         another way).  Keys the process environment already sets win.  Without the file RCCL
         detects the node's RDMA ports itself, which is what the discovered settings would say
-        (every active port; RoCE v2 GIDs) -- measured: setting them anyway added ~0.1-0.2 s to
-        a cold communicator init on MI355X (``profiles/round4/rccl_env_ab.txt``).  Returns
+        (every active port; RoCE v2 GIDs) -- measured: with them set, a cold create->ready on
+        MI355X was 0.07 and 0.25 s slower in two A/B pairs (``profiles/round4/rccl_env_ab.txt``).  Returns
         what was applied.  Called before the agent's first HIP or RCCL call (``warm_native``).
         A setting the file may not hold (``parallel/rccl_env.py:env_problems``: one naming a
         library, plugin or path; written by hand or by an older release) is skipped and listed
