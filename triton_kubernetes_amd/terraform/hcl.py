@@ -952,6 +952,8 @@ def eval_expr(node: Node, env: Dict[str, Any]) -> Any:
         # [for k, v in coll : value if cond] / {for k, v in coll : key => value if cond}; a
         # map is walked in key order, as Terraform does
         names = node.value["names"]
+        if node.value.get("group"):
+            raise TemplateError("grouping for-expressions (key => value...) are not supported by this evaluator")
         coll = eval_expr(node.children[0], env)
         pairs = sorted(coll.items()) if isinstance(coll, dict) else list(enumerate(coll))
         obj = node.value["object"]
