@@ -108,9 +108,19 @@ def test_agent_start_skips_file_settings_it_may_not_apply(tmp_path, monkeypatch)
                                                 'NCCL_SOCKET_IFNAME="/tmp/x"\n')
     agent = NodeAgent(name="n", mode="sim", devices=[], root=str(tmp_path))
     try:
-        assert agent.apply_node_rccl_env() == {"NCCL_DEBUG": "WARN"}
+        agent.rccl_env_applied = agent.apply_node_rccl_env()
+        assert agent.rccl_env_applied == {"NCCL_DEBUG": "WARN"}
         assert sorted(agent.rccl_env_skipped) == ["HSA_TOOLS_LIB", "NCCL_NET_PLUGIN", "NCCL_SOCKET_IFNAME"]
         assert "NCCL_NET_PLUGIN" not in env and "HSA_TOOLS_LIB" not in env
+        # and the operator can see it on the agent's API
+        import json
+        import urllib.request
+
+        url = agent.serve("127.0.0.1")
+        req = urllib.request.Request(url + "/v1/info", headers={"X-TK-Agent-Token": agent.token})
+        info = json.loads(urllib.request.urlopen(req, timeout=10).read())
+        assert info["rccl_env_applied"] == ["NCCL_DEBUG"]
+        assert sorted(info["rccl_env_skipped"]) == ["HSA_TOOLS_LIB", "NCCL_NET_PLUGIN", "NCCL_SOCKET_IFNAME"]
     finally:
         agent.stop()
 

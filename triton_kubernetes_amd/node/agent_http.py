@@ -99,7 +99,10 @@ class AgentHTTPMixin:
                     with agent._gate_mu:
                         pending = len(agent._gates)
                     return self._reply(200, {"name": agent.name, "mode": agent.mode, "devices": agent.devices,
-                                             "labels": agent.last_labels, "pending_gates": pending})
+                                             "labels": agent.last_labels, "pending_gates": pending,
+                                             # what the agent took from /etc/rccl/rccl.env at start
+                                             "rccl_env_applied": sorted(getattr(agent, "rccl_env_applied", {})),
+                                             "rccl_env_skipped": list(getattr(agent, "rccl_env_skipped", []))})
                 if urllib.parse.urlsplit(self.path).path == "/metrics":
                     from .metrics import CONTENT_TYPE
 
