@@ -25,6 +25,13 @@ Each timed step is a COLD create:
    ``amd.com/gpu`` allocatable, cluster-wide RCCL all-reduce gate across all N GPUs);
 3. the agents shut down (communicator teardown, HIP release), inside the step.
 
+The GPU node runs the product's default burn-in level (``full``: HBM/MFMA screens plus a
+memtest of all free HBM, ``models/baremetal.py`` DEFAULT_BURNIN); ``--burnin quick`` is the
+explicit opt-down and the line's ``config.burnin`` names the level.  Before every timed step,
+outside the timed region, the bench waits until the kernel driver has finished clearing the
+HBM the previous step released (``ops/hbm.py``; ``hbm_settle_s`` in the line): a node
+entering service starts with clear HBM, so no step pays its predecessor's ~300 GB release.
+
 ``value`` is the mean create -> kubectl-ready time (agent start to readiness);
 ``ms_per_step`` is the whole step including the agent shutdown.  A WARM number (the
 same create against agents kept resident across steps, round 1's headline) is
@@ -61,13 +68,25 @@ METRIC = "cluster create→kubectl-ready wall-clock (s), bare-metal at 1/2/4/8 w
 SIMULATED_PHASES = ["rke_provisioning", "runtime_install", "agent_container", "device_plugin_pod"]
 
 
+def _default_burnin() -> str:
+    from triton_kubernetes_amd.models.baremetal import DEFAULT_BURNIN
+
+    return DEFAULT_BURNIN
+
+
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--workers", type=int, default=1, help="worker nodes the N GPUs are split over")
-    ap.add_argument("--burnin", default="quick", choices=["quick", "full", "off"])
+    # the product's default level (models/baremetal.py DEFAULT_BURNIN, pinned by
+    # tests/test_bench_contract.py); quick is the explicit opt-down
+    ap.add_argument("--burnin", default=_default_burnin(), choices=["quick", "full", "off"])
+    ap.add_argument("--hbm-settle", default="on", choices=["on", "off"],
+                    help="on: before each step, outside the timed region, wait until the kernel driver has "
+                         "finished clearing the HBM the previous step released (ops/hbm.py), as on a node "
+                         "entering service.  off: the A/B (each step pays its predecessor's clearing)")
     ap.add_argument("--no-rccl-gate", action="store_true")
     ap.add_argument("--rccl-mib", type=int, default=64, help="largest RCCL gate message (MiB)")
     ap.add_argument("--warm-steps", type=int, default=2,
@@ -400,20 +419,42 @@ def main() -> int:
             dist.barrier()
         sync()
 
+    from triton_kubernetes_amd.ops import hbm
+
+    # this node's GPUs of the run, by their DRM cards (a shared host lists other tenants' GPUs
+    # too, whose releases must not hold up -- or end -- the wait)
+    my_cards = [] if args.sim_gpu else hbm.cards_for_pci(
+        (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
+        for p in (torch.cuda.get_device_properties(i) for i in range(visible)))
+
+    def settle() -> dict:
+        """Outside the timed region: the previous step's released HBM is cleared by the
+        driver before the next step starts (a node entering service starts clean).  Local
+        rank 0 watches the node's cards; every rank waits for it."""
+        got = {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
+        if args.hbm_settle == "on" and my_cards and local_rank == 0:
+            got = hbm.settle(cards=my_cards)
+        barrier()
+        return got
+
     results = []
+    settles = []
     try:
         for w in range(args.warmup):
+            settle()
             barrier()
             cold_step(-1 - w)
-        barrier()
         TRACER.reset()
-        t_start = time.perf_counter()
+        # the timed region is the K steps, each bracketed by a barrier + synchronize on both
+        # sides; the settle wait before each step is outside it (and reported as hbm_settle_s)
+        elapsed = 0.0
         for i in range(args.steps):
+            settles.append(settle())
+            barrier()
+            t_step = time.perf_counter()
             results.append(cold_step(i))
-        sync()
-        if distributed:
-            dist.barrier()
-        elapsed = time.perf_counter() - t_start
+            barrier()
+            elapsed += time.perf_counter() - t_step
     except Exception as exc:
         if rank == 0:
             # a failed run still says what failed, in the line's own shape (value null), before
@@ -448,6 +489,13 @@ def main() -> int:
                 dist.barrier()
             if i:
                 warm.append(time.perf_counter() - t0)
+            if rank == 0:
+                # untimed: destroy it again, which takes the resident hosts out of the cluster
+                # (node/cleanup.py) -- a host is a node of one cluster at a time
+                wf.delete_cluster(Context(settings=Settings(dict(ctx_base, cluster_name=f"bench-{1000 + i}"),
+                                                            env={}), out=devnull), backend)
+            if distributed:
+                dist.barrier()
         for p in procs:
             p.signal_stop()
         for p in procs:
@@ -494,6 +542,9 @@ def main() -> int:
                            f"(one communicator over all {n_gpus} GPUs"
                            + (", over the libtk_rccl ABI stub" if args.sim_gpu and not args.no_rccl_gate else "")
                            + ")"
+                           + ("; before each timed step, untimed, the bench waits for the driver to clear the HBM "
+                              "the previous step released (a node entering service starts clean)"
+                              if args.hbm_settle == "on" and not args.sim_gpu else "")
                            + ("; opt-in node install before the timed region: verified single-target gfx950 "
                               "RCCL copy (ops/rccl_slim.py)" if slim_meta else "")),
             "config": {
@@ -525,6 +576,14 @@ def main() -> int:
             "rccl_gate_ranks": [r.get("rccl_gate_ranks", 0) for r in results],
             # the GPU nodes' measured xGMI peer-read matrix (2+ GPUs per node), last timed step
             "xgmi_links": next((r["xgmi_links"] for r in reversed(results) if r.get("xgmi_links")), None),
+            # the GPU node's burn-in step, per timed step (max over worker nodes)
+            "gpu_burnin_ms": [r.get("gpu_node_step_ms", {}).get("gpu_burnin") for r in results],
+            # before each timed step, outside the timed region: the wait for the driver to clear
+            # the previous step's released HBM (ops/hbm.py; --hbm-settle off for the A/B)
+            "hbm_settle": args.hbm_settle,
+            "hbm_settle_cards": my_cards,
+            "hbm_settle_s": [s["waited_s"] for s in settles],
+            "hbm_settle_released_gib": [s["released_gib"] for s in settles],
             "phase_ms_per_step": phase_ms,
         }
         print(json.dumps(line), flush=True)

@@ -20,8 +20,9 @@ of the form ``ssh <opts> -W %h:%p user@bastion`` checks the bastion's key the sa
 
 Commands: ``cat <file>`` prints the file from the host directory (``~/x`` and
 ``/etc/triton-kubernetes/x`` both map to ``<dir>/x``); with ``FAKE_SSH_EXEC=1`` the remote
-command (or stdin for ``bash -s``) runs locally under ``bash``; otherwise anything else
-succeeds silently.  Every call is appended to ``$FAKE_SSH_LOG`` when set.
+command (or stdin for ``bash -s``) runs locally under ``bash`` -- with ``FAKE_SSH_HOST_ROOT=1``
+with ``TK_HOST_ROOT=<dir>/root``, the host's filesystem for the scripts that honour it
+(``node/cleanup.py``); otherwise anything else succeeds silently.  Every call is appended to ``$FAKE_SSH_LOG`` when set.
 """
 
 import base64
@@ -123,9 +124,13 @@ def main() -> int:
         sys.stderr.write(err)
         return 255
     if os.environ.get("FAKE_SSH_EXEC") == "1" and command:
+        env = None
+        if os.environ.get("FAKE_SSH_HOST_ROOT") == "1":  # the host's filesystem: <dir>/root
+            env = dict(os.environ, TK_HOST_ROOT=os.path.join(home, "root"))
+            os.makedirs(env["TK_HOST_ROOT"], exist_ok=True)
         if command.strip() == "bash -s":
-            return subprocess.run(["bash", "-s"], stdin=sys.stdin).returncode
-        return subprocess.run(["bash", "-c", command]).returncode
+            return subprocess.run(["bash", "-s"], stdin=sys.stdin, env=env).returncode
+        return subprocess.run(["bash", "-c", command], env=env).returncode
     for m in re.finditer(r"\bcat\s+(\S+)", command):
         path = os.path.join(home, os.path.basename(m.group(1)))
         if os.path.exists(path):

@@ -28,6 +28,15 @@ code (nothing here imports ``triton_kubernetes_amd``):
                dependencies) — and a failing program fails the command; module outputs
                that read a data source get its result.
 
+* with ``FAKE_TF_HOSTS=<dir>``, bare-metal host modules (``var.host`` + a cluster
+               registration token) model the host ``<dir>/<host>/root``: an apply records the
+               join (what ``system-agent-install.sh`` leaves: ``/var/lib/rancher/agent/
+               rancher2_connection_info.json``) and fails the module -- as the real join
+               fails -- on a host still joined to another cluster; a destroy runs the
+               module's destroy-time ``remote-exec`` (``when = destroy``) locally against
+               that root (``TK_HOST_ROOT``), honouring ``count = var.X ? 1 : 0`` and
+               ``on_failure = continue``.
+
 Every call appends ``{"argv", "cwd", "doc", "prior"}`` to ``$FAKE_TF_LOG`` (``prior``:
 serial/lineage/modules of the state the command started from).  ``FAKE_TF_FAIL=<cmd>``
 makes that sub-command fail *after* applying half of the new modules (apply) — a
@@ -334,6 +343,82 @@ def refresh(doc, keys, root_vars, known_outputs):
     return outs, None
 
 
+# --- bare-metal hosts (FAKE_TF_HOSTS) ------------------------------------------------------------
+
+HOST_CONNECTION = "var/lib/rancher/agent/rancher2_connection_info.json"
+
+
+def host_module(mod_dir):
+    text = _module_text(mod_dir)
+    return ('variable "host"' in text and 'variable "rancher_cluster_registration_token"' in text
+            and "host        = var.host" in text)
+
+
+def host_root(host):
+    return os.path.join(os.environ["FAKE_TF_HOSTS"], host, "root")
+
+
+def join_identity(doc_path, block):
+    m = re.search(r"\$\{module\.([^.}]+)\.", str(block.get("rancher_cluster_registration_token", "")))
+    return f"{os.path.abspath(doc_path)}:{m.group(1) if m else block.get('rancher_cluster_registration_token')}"
+
+
+def join_host(key, block, path):
+    """The host's side of an applied host module: ``None``, or the provisioner error."""
+    host = str(block.get("host", ""))
+    rec_path = os.path.join(host_root(host), HOST_CONNECTION)
+    ident = join_identity(path, block)
+    if os.path.exists(rec_path):
+        prev = json.load(open(rec_path, encoding="utf-8"))
+        if prev.get("cluster") != ident:
+            return (f"remote-exec provisioner error\n\n  with module.{key}.terraform_data.install\n\n"
+                    f"error executing \"/tmp/terraform_1.sh\": Process exited with status 1\n"
+                    f"system-agent-install: rancher-system-agent is already installed on this host and connected "
+                    f"to {prev.get('cluster')}: the node cannot join another cluster until it is uninstalled")
+    os.makedirs(os.path.dirname(rec_path), exist_ok=True)
+    with open(rec_path, "w", encoding="utf-8") as fh:
+        json.dump({"cluster": ident, "module": key}, fh)
+    return None
+
+
+def destroy_provisioners(mod_dir):
+    """[(count gate variable or None, script file)] of the destroy-time remote-exec
+    provisioners of the module's resources."""
+    text = _module_text(mod_dir)
+    out = []
+    for m in re.finditer(r'^resource\s+"\w+"\s+"\w+"\s*\{', text, re.M):
+        body = _braced(text, m.end() - 1)
+        gate = re.search(r"^\s*count\s*=\s*var\.(\w+)\s*\?\s*1\s*:\s*0\s*$", body, re.M)
+        for p in re.finditer(r'provisioner\s+"remote-exec"\s*\{', body):
+            pb = _braced(body, p.end() - 1)
+            if not re.search(r"^\s*when\s*=\s*destroy\s*$", pb, re.M):
+                continue
+            f = re.search(r'file\("\$\{path\.module\}/([^"]+)"\)', pb)
+            cont = re.search(r"^\s*on_failure\s*=\s*continue\s*$", pb, re.M) is not None
+            if f:
+                out.append((gate.group(1) if gate else None, os.path.join(mod_dir, f.group(1)), cont))
+    return out
+
+
+def destroy_host(key, block, mod_dir):
+    """Run the destroy-time provisioners of a host module against its host root."""
+    defaults = _var_defaults(_module_text(mod_dir))
+    for gate, script, cont in destroy_provisioners(mod_dir):
+        if gate is not None:
+            val = block.get(gate, defaults.get(gate, "true"))
+            if str(val).lower() in ("false", "0"):
+                continue  # count = 0: the resource (and its provisioner) does not exist
+        env = dict(os.environ, TK_HOST_ROOT=host_root(str(block.get("host", ""))))
+        proc = subprocess.run(["bash", script], env=env, capture_output=True, text=True, timeout=120)
+        sys.stdout.write(f"module.{key}: Destroying... (remote-exec)\n{proc.stdout}")
+        if proc.returncode != 0:
+            if not cont:
+                return f"remote-exec provisioner error (destroy) in module.{key}: exit {proc.returncode}"
+            sys.stderr.write(f"Warning: module.{key}: destroy-time provisioner failed (on_failure = continue): "
+                             f"{proc.stderr[-300:]}\n")
+    return None
+
+
 def root_variables(doc, argv):
     """Root variable values: declared defaults, then -var=name=value.  ``(values, error)``."""
     declared = doc.get("variable") or {}
@@ -423,6 +508,16 @@ def main() -> int:
         failing = os.environ.get("FAKE_TF_FAIL") == "apply"
         if failing:
             new = new[: len(new) // 2]
+        refused = []
+        if os.environ.get("FAKE_TF_HOSTS"):
+            for key in list(new):
+                block = (doc.get("module") or {})[key]
+                d = local_dir(str(block.get("source", "")))
+                if d and host_module(d):
+                    err = join_host(key, block, path)
+                    if err:
+                        refused.append(err)
+                        new.remove(key)
         for key in new:
             st["resources"].append({"module": f"module.{key}", "mode": "managed", "type": "terraform_data",
                                     "name": "fake", "instances": [{"attributes": {"id": str(uuid.uuid4())}}]})
@@ -439,6 +534,8 @@ def main() -> int:
         save_state(path, st)
         if failing:
             return fail("fake failure of apply")
+        if refused:
+            return fail("\n\nError: ".join(refused))
         print(f"Apply complete! Resources: {len(new)} added, 0 changed, 0 destroyed.")
         return 0
 
@@ -448,6 +545,14 @@ def main() -> int:
         targets = [a.split("=", 1)[1] for a in argv if a.startswith("-target=")]
         st = prior or {"version": 4, "lineage": str(uuid.uuid4()), "serial": 0, "resources": [], "outputs": {}}
         gone = {t[len("module."):] for t in targets} if targets else set(state_modules(st))
+        if os.environ.get("FAKE_TF_HOSTS"):
+            for key in sorted(gone & set(state_modules(st))):
+                block = (doc.get("module") or {}).get(key) or {}
+                d = local_dir(str(block.get("source", "")))
+                if d and host_module(d):
+                    err = destroy_host(key, block, d)
+                    if err:
+                        return fail(err)
         st["resources"] = [r for r in st.get("resources", []) if r.get("module", "")[len("module."):] not in gone]
         st["outputs"] = {k: v for k, v in (st.get("outputs") or {}).items()
                          if not any(k.startswith(g + "__") for g in gone)}

@@ -142,6 +142,9 @@ if mode == "silent":
 if mode == "error":
     print(json.dumps({{"ok": False, "error": "hipMalloc: out of memory"}}), flush=True)
     sys.exit(2)
+if mode == "stale":  # a gpu-burnin that predates --memtest-span: a whole burn-in's report
+    print(json.dumps({{"level": "full", "gpus": [{{"device": 0, "ok": True}}], "ok": True}}), flush=True)
+    sys.exit(0)
 n = int(a[a.index("--span-bytes") + 1]) or (300 << 30)
 print("a library's banner on stdout", flush=True)
 print(json.dumps({{"ok": True, "errors": 0, "verify_gbps": 6100.0, "bytes": n, "hbm_bytes": 309 << 30,
@@ -151,7 +154,7 @@ time.sleep(float(os.environ.get("FAKE_RELEASE_S", "0")))
     exe.chmod(exe.stat().st_mode | stat.S_IEXEC)
     argv_log = tmp_path / "argv.log"
     monkeypatch.setenv("FAKE_SPAN_ARGV", str(argv_log))
-    monkeypatch.setattr(probe, "BURNIN_EXE", str(exe))
+    monkeypatch.setattr(probe, "_burnin_exe", lambda: str(exe))
     released = []
     monkeypatch.setattr(probe, "release_scratch", lambda dev=None: released.append(dev) or 0)
 
@@ -207,6 +210,48 @@ def test_span_child_failures_are_errors(span_child, monkeypatch):
     with pytest.raises(probe.ProbeError, match="exited 3 without a verdict"):
         probe.memtest_span_process(0)
     probe.wait_frees()
+
+
+def test_span_child_stale_binary_is_an_error_not_a_keyerror(span_child, monkeypatch):
+    """a stale gpu-burnin that ignores --memtest-span prints a whole burn-in's
+    report (no ``errors``); that is a ProbeError naming the binary, not a KeyError."""
+    monkeypatch.setenv("FAKE_SPAN_MODE", "stale")
+    with pytest.raises(probe.ProbeError, match="no memtest-span verdict"):
+        probe.memtest_span_process(0)
+    probe.wait_frees()
+
+
+@pytest.mark.parametrize("how", ["missing", "unstartable"])
+def test_span_child_unusable_binary_falls_back_in_process(span_child, monkeypatch, tmp_path, how):
+    """A missing or stale gpu-burnin (NativeUnavailable from native.executable) or one that
+    cannot be started runs the same span memtest in this process, and says so."""
+    from triton_kubernetes_amd.ops import native
+
+    if how == "missing":
+        def nope():
+            raise native.NativeUnavailable("gpu-burnin is not built and building it failed: no hipcc")
+        monkeypatch.setattr(probe, "_burnin_exe", nope)
+    else:
+        monkeypatch.setattr(probe, "_burnin_exe", lambda: str(tmp_path / "no-such-gpu-burnin"))
+    calls = []
+    monkeypatch.setattr(probe, "memtest_span", lambda dev, nbytes, headroom, passes: calls.append(dev) or {
+        "errors": 0, "verify_gbps": 1.0, "bytes": 8, "hbm_bytes": 16, "alloc_ms": 0.0, "test_ms": 0.0,
+        "free_ms": 0.0})
+    res = probe.memtest_span_process(2, 0)
+    assert calls == [2] and res["errors"] == 0
+    assert ("no hipcc" if how == "missing" else "cannot start") in res["span_fallback"]
+
+
+def test_executable_refuses_a_stale_tool_it_cannot_rebuild(monkeypatch):
+    from triton_kubernetes_amd.ops import build, native
+
+    monkeypatch.setattr(build, "current", lambda name: False)
+
+    def fail(**kw):
+        raise RuntimeError("hipcc: not found")
+    monkeypatch.setattr(build, "build", fail)
+    with pytest.raises(native.NativeUnavailable, match="hipcc: not found"):
+        native.executable("gpu-burnin")
 
 
 def test_full_burnin_uses_the_span_child_when_enabled(scripted, span_child, monkeypatch):

@@ -307,11 +307,10 @@ def test_fingerprint_matches_hash_and_deps():
 def test_fake_rancher_settles_clusters(env):
     fake, agent, backend, base = env
     _manager(fake, backend, base)
-    cp = agent("cp")
-    for name in ("one", "two"):
+    for name in ("one", "two"):  # a host is a node of one cluster at a time: its own hosts each
         new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name=name,
                                   k8s_version="v1.28.10-rancher1-1", k8s_network_provider="flannel", wait=True,
-                                  nodes=_nodes(cp, [agent(f"{name}-w", gpus=8)]))), backend)
+                                  nodes=_nodes(agent(f"{name}-cp"), [agent(f"{name}-w", gpus=8)]))), backend)
     # a settled cluster is no longer walked by the simulation; each cluster lists its own nodes
     assert fake.state.unsettled == set()
     cids = {c["name"]: c["id"] for c in fake.state.clusters.values()}
@@ -374,3 +373,51 @@ def test_direct_executor_refuses_what_terraform_would(env):
     with pytest.raises(TKError, match="rccl_env"):
         DirectExecutor(transport=TransportRouter(ssh=rec, agent=AgentTransport(token=TOKEN))).apply(st, backend)
     assert len(rec.plans) == plans_before
+
+
+def test_apply_after_upgrade_accepts_pre_r4_module_hashes(env):
+    """module hashes persisted before the hash covered the module's identity (it
+    covered the source string the module was applied from) still match: the first apply
+    after an upgrade re-runs no module -- no host bootstrap on nodes in service."""
+    from triton_kubernetes_amd.executor.direct import fingerprint
+
+    fake, agent, backend, base = env
+    _manager(fake, backend, base)
+    cp = agent("cp")
+    workers = [agent("w0", gpus=8)]
+    new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_name="dev", cluster_cloud_provider="baremetal",
+                              name="dev", k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico",
+                              nodes=_nodes(cp, workers))), backend)
+    state_doc = {"module": backend.state("mgr").modules()}
+    tf = json.loads(backend.read_tfstate("mgr"))
+    # rewrite the tfstate as round 3 wrote it: sources at an absolute install path, hashes over them
+    old_root = "/usr/lib/python3/dist-packages/triton_kubernetes_amd/terraform/modules"
+    for key, entry in tf["module_state"].items():
+        cfg = state_doc["module"][key]
+        name = cfg["source"].split("?")[0].rstrip("/").rsplit("/", 1)[-1]
+        legacy_src = f"{old_root}/{name}"
+        entry["source"] = legacy_src
+        entry["hash"] = fingerprint(dict(cfg, source=legacy_src))[0]
+    from triton_kubernetes_amd.executor.tfstate import CODEC
+
+    backend.write_tfstate("mgr", CODEC.dumps("mgr", tf))
+    before = {k: v["applied_at"] for k, v in tf["module_state"].items()}
+
+    ex = DirectExecutor(transport=TransportRouter(agent=AgentTransport(token=TOKEN)))
+    report = ex.apply_report(backend.state("mgr"), backend)
+    assert report.ok and {r.status for r in report.runs.values()} == {"skipped"}
+    after = json.loads(backend.read_tfstate("mgr"))["module_state"]
+    assert {k: v["applied_at"] for k, v in after.items()} == before
+    # stored in today's form: the next apply matches directly
+    assert all(after[k]["hash"] == report.runs[k].hash for k in after)
+
+    # a changed config is still re-applied (the legacy form is not a blanket pass)
+    st = backend.state("mgr")
+    for key in list(after):
+        tf2 = json.loads(backend.read_tfstate("mgr"))
+        e = tf2["module_state"][key]
+        e["hash"] = "0" * 16
+        backend.write_tfstate("mgr", CODEC.dumps("mgr", tf2))
+        break
+    rep2 = ex.apply_report(st, backend)
+    assert rep2.runs[key].status == "ok"

@@ -124,3 +124,114 @@ def test_from_state_membership():
 def test_empty_gate_rejected():
     with pytest.raises(ValueError):
         ClusterGate(FakeAgents(), [], [1])
+
+
+# --- the agent side of an abort (the pop -> sweeping window) -------------------------
+
+
+def _sim_agent(tmp_path, gpus=2):
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.labels import synthetic_topology
+
+    a = NodeAgent(name="g", mode="sim", devices=list(range(gpus)), token="t" * 24, root=str(tmp_path))
+    a.topology_override = synthetic_topology(gpus)
+    return a
+
+
+def test_abort_before_the_gate_request_fails_it_at_once(tmp_path):
+    from triton_kubernetes_amd.node.agent_gate import GateAborted
+
+    a = _sim_agent(tmp_path)
+    try:
+        uid = b"U" * 128
+        res = a.rccl_abort(uid)
+        assert not res["aborted"] and not res["canceled"]
+        with pytest.raises(GateAborted):
+            a.rccl_gate(0, 4, uid, [1 << 20], ndev=2)
+        with pytest.raises(GateAborted):
+            a.rccl_prepare(uid, 4, 0, ndev=2)
+        assert not a._gates and not a._sweeping
+        # another uid is unaffected
+        assert a.rccl_gate(0, 2, b"V" * 128, [1 << 20], ndev=2)["ok"]
+    finally:
+        a.stop()
+
+
+def test_abort_while_the_communicator_starts_cancels_the_request(tmp_path, monkeypatch):
+    """The abort lands after the gate request took its (absent) pending entry and before its
+    fresh communicator exists: the request fails at once and releases what it made."""
+    from triton_kubernetes_amd.node import agent_gate
+    from triton_kubernetes_amd.node.agent_gate import GateAborted
+
+    a = _sim_agent(tmp_path)
+    started, go = threading.Event(), threading.Event()
+    aborted = []
+
+    class SlowGate(agent_gate._SimGate):
+        def __init__(self, devices):
+            started.set()
+            go.wait(5)
+            super().__init__(devices)
+
+        def abort(self):
+            aborted.append(self)
+
+    monkeypatch.setattr(agent_gate, "_SimGate", SlowGate)
+    uid = b"W" * 128
+    out = {}
+
+    def req():
+        try:
+            out["res"] = a.rccl_gate(0, 4, uid, [1 << 20], ndev=2)
+        except GateAborted as exc:
+            out["err"] = exc
+
+    t = threading.Thread(target=req)
+    t.start()
+    try:
+        assert started.wait(5)
+        res = a.rccl_abort(uid)
+        assert res["canceled"]  # found the request in its reserved slot
+        go.set()
+        t.join(5)
+        assert isinstance(out.get("err"), GateAborted) and len(aborted) == 1
+        assert not a._sweeping
+    finally:
+        go.set()
+        a.stop()
+
+
+def test_abort_during_prepare_releases_the_new_communicator(tmp_path, monkeypatch):
+    from triton_kubernetes_amd.node import agent_gate
+    from triton_kubernetes_amd.node.agent_gate import GateAborted
+
+    a = _sim_agent(tmp_path)
+    uid = b"X" * 128
+    aborted = []
+
+    class RacingGate(agent_gate._SimGate):
+        def __init__(self, devices):
+            a.rccl_abort(uid)  # lands while the prepare is starting its init
+            super().__init__(devices)
+
+        def abort(self):
+            aborted.append(self)
+
+    monkeypatch.setattr(agent_gate, "_SimGate", RacingGate)
+    try:
+        with pytest.raises(GateAborted):
+            a.rccl_prepare(uid, 4, 0, ndev=2)
+        assert len(aborted) == 1 and uid not in a._gates
+    finally:
+        a.stop()
+
+
+def test_aborted_uids_expire(tmp_path, monkeypatch):
+    a = _sim_agent(tmp_path)
+    try:
+        uid = b"Y" * 128
+        a.rccl_abort(uid)
+        monkeypatch.setattr(type(a), "ABORTED_TTL_S", -1.0)
+        assert a.rccl_gate(0, 2, uid, [1 << 20], ndev=2)["ok"]
+    finally:
+        a.stop()

@@ -39,7 +39,7 @@ from typing import Any, Callable, Dict, List, Optional, Set, Tuple
 
 from .. import __version__
 from ..backend.base import Backend
-from ..errors import ExecutorError, TKError
+from ..errors import ExecutorError
 from ..node.plan import TOOLS_DIR, build_host_plan
 from ..parallel.transport import HostRef, Transport, TransportRouter
 from ..rancher.client import RancherClient, wait_until
@@ -144,7 +144,7 @@ class DirectExecutor(Executor):
     def __init__(self, transport: Optional[Transport] = None, parallelism: int = 64,
                  rancher_factory: Optional[Callable[..., RancherClient]] = None, rancher_bootstrap: str = "operator",
                  node_timeout: float = 3600.0, cluster_wait: float = 1800.0, upload_tools: bool = True,
-                 node_cleanup: bool = False, on_event: Optional[Callable[[str, Dict[str, Any]], None]] = None,
+                 node_cleanup: bool = True, on_event: Optional[Callable[[str, Dict[str, Any]], None]] = None,
                  host_retries: int = 0, retry_backoff: float = 2.0):
         self.transport = transport or TransportRouter()
         self.parallelism = max(1, parallelism)
@@ -160,6 +160,8 @@ class DirectExecutor(Executor):
         self.host_retries = max(0, host_retries)
         self.retry_backoff = retry_backoff
         self.last_report: Optional[ApplyReport] = None
+        # host key -> the cleanup report of the last destroy (node/cleanup.py)
+        self.last_cleanup: Dict[str, Dict[str, Any]] = {}
         self._mu = threading.Lock()
 
     # --- tfstate ---------------------------------------------------------------------------------
@@ -257,6 +259,7 @@ class DirectExecutor(Executor):
 
         pool = shared_pool(f"tk-direct-{self.parallelism}", self.parallelism)
         tls_pool = self._prefetch_tls(runs, tf)
+        rehashed = False
         with span("direct.apply", modules=len(runs)):
             while pending or futures:
                 for key in sorted(pending):
@@ -268,8 +271,11 @@ class DirectExecutor(Executor):
                     if all(runs[d].status in ("ok", "skipped") for d in run.deps):
                         pending.discard(key)
                         prev = tf["module_state"].get(key)
-                        if prev and prev.get("hash") == run.hash and prev.get("status") == "ok" and key in outputs:
+                        if self._unchanged(run, prev) and key in outputs:
                             run.status = "skipped"
+                            if prev.get("hash") != run.hash:  # a pre-r4 hash: stored in today's form
+                                tf["module_state"][key] = dict(prev, hash=run.hash)
+                                rehashed = True
                             continue
                         run.start = time.time()
                         run.prev_private = (prev or {}).get("private")
@@ -305,11 +311,33 @@ class DirectExecutor(Executor):
                 for fut in done:
                     run = runs[keys_done[fut]]
                     self._event("module_done", key=run.key, status=run.status, seconds=run.end - run.start)
+        if rehashed:
+            self._save_tfstate(backend, state.name, tf)  # the upgraded hashes, whatever else ran
         if tls_pool is not None:
             tls_pool.shutdown(wait=False)  # an unused certificate (add-on blocked) finishes on its own
         report.wall = time.time() - t0
         self.last_report = report
         return report
+
+    @staticmethod
+    def _unchanged(run: ModuleRun, prev: Optional[Dict[str, Any]]) -> bool:
+        """``prev`` (the module's tfstate entry) records a successful apply of this config.
+
+        Since round 4 the hash covers the module's identity instead of its source string
+        (``plan``).  A hash persisted before that covers the source the module was applied
+        from, which the entry keeps: that form is accepted too (same module, same config), so
+        the first apply after an upgrade or a ``migrate manager`` re-runs nothing -- above all
+        no host bootstrap, whose full burn-in memtests a node that is in service."""
+        if not prev or prev.get("status") != "ok":
+            return False
+        if prev.get("hash") == run.hash:
+            return True
+        src = prev.get("source")
+        if not src:
+            return False
+        info = module_from_source(str(src))
+        return info is not None and info.name == run.info.name and \
+            fingerprint(dict(run.cfg, source=src))[0] == prev.get("hash")
 
     @staticmethod
     def _prefetch_tls(runs: Dict[str, ModuleRun], tf: Dict[str, Any]) -> Optional[cf.ThreadPoolExecutor]:
@@ -330,7 +358,7 @@ class DirectExecutor(Executor):
             prev = tf["module_state"].get(key) or {}
             if (prev.get("private") or {}).get("injector_tls"):
                 continue
-            if prev.get("hash") == run.hash and prev.get("status") == "ok":
+            if DirectExecutor._unchanged(run, prev):
                 continue
             if addons.enabled("env", addons.module_cfg_defaults(run.cfg)):
                 wanted.append(run)
@@ -478,23 +506,54 @@ class DirectExecutor(Executor):
             if keys is not None:
                 keys.save()
 
+    @staticmethod
+    def cleanup_wanted(cfg: Dict[str, Any]) -> bool:
+        """A host module's ``node_cleanup`` (default on: bare metal outlives its cluster)."""
+        v = cfg.get("node_cleanup", True)
+        return v if isinstance(v, bool) else str(v).strip().lower() not in ("false", "0", "no", "off", "")
+
+    def _cleanup_hosts(self, state: State, keys: List[str]) -> Dict[str, Dict[str, Any]]:
+        """Take every destroyed host out of its cluster, all hosts at once (node/cleanup.py):
+        SSH hosts run the cleanup script, agent hosts their fixed-argv ``/v1/cleanup``.  A
+        failure is reported (``last_cleanup``), not raised: a dead host must not pin the
+        document, and the host's join record refuses a later join until it is cleaned.  A
+        changed SSH host key is raised (nothing is destroyed): that host is not dead."""
+        from ..parallel.hostkeys import HostKeyChanged
+
+        work = []
+        for key in keys:
+            cfg = state.module(key) or {}
+            info = module_from_source(str(cfg.get("source", "")))
+            if info is None or info.kind != "host" or not self.cleanup_wanted(cfg):
+                continue
+            ref = HostRef(str(cfg.get("host", "")), cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
+                          cfg.get("bastion_host") or "")
+            work.append((key, str(cfg.get("hostname", key)), ref))
+        if not work:
+            return {}
+        from ..parallel.fanout import shared_pool
+
+        def one(item):
+            key, hostname, ref = item
+            t0 = time.time()
+            with span("destroy.cleanup", host=hostname, transport=ref.scheme):
+                try:
+                    rep = self.transport.cleanup_host(ref, timeout=600)
+                except HostKeyChanged:
+                    raise  # not a dead host: an impostor or a reinstall -- the destroy stops here
+                except Exception as exc:  # noqa: BLE001 - reported per host
+                    rep = {"ok": False, "error": f"{type(exc).__name__}: {exc}", "actions": []}
+            rep = dict(rep, hostname=hostname, seconds=round(time.time() - t0, 3))
+            self._event("host_cleanup", key=key, **{k: rep.get(k) for k in ("hostname", "ok", "error")})
+            return key, rep
+
+        pool = shared_pool(f"tk-direct-{self.parallelism}", self.parallelism)
+        return dict(pool.map(one, work))
+
     def _destroy(self, state: State, backend: Backend, targets: List[str]) -> None:
         tf = self._load_tfstate(backend, state.name)
         keys = [t[len("module."):] if t.startswith("module.") else t for t in targets] or list(state.modules())
-        if self.node_cleanup:
-            from ..node.manager import node_cleanup_script
-
-            for key in keys:
-                cfg = state.module(key) or {}
-                info = module_from_source(str(cfg.get("source", "")))
-                if info is not None and info.kind == "host":
-                    ref = HostRef(str(cfg.get("host", "")), cfg.get("ssh_user") or "ubuntu",
-                                  cfg.get("key_path") or "", cfg.get("bastion_host") or "")
-                    if ref.scheme != "agent":
-                        try:
-                            self.transport.run_script(ref, node_cleanup_script(), timeout=600)
-                        except TKError as exc:
-                            raise ExecutorError(f"cleanup of {cfg.get('hostname')}: {exc}") from exc
+        self.last_cleanup = self._cleanup_hosts(state, keys) if self.node_cleanup else {}
         for key in keys:
             tf["module_outputs"].pop(key, None)
             tf["module_state"].pop(key, None)

@@ -9,7 +9,9 @@
                             (default: per-node tokens and TLS from the manager's agent
                             PKI, ``node/security.py``)
 ``rancher_bootstrap``       ``operator`` (default) | ``remote``
-``node_cleanup``            run the agent cleanup script on destroy (default false)
+``node_cleanup``            take destroyed bare-metal hosts out of their cluster (uninstall the
+                            agent and RKE2/RKE1, node/cleanup.py; default true); a host
+                            module's own ``node_cleanup`` can turn it off for that host
 ``host_retries``            re-run a failed host bootstrap this many times (default 0)
 ``host_retry_backoff``      first retry delay in seconds, doubling per attempt (default 2)
 ==========================  ================================================================
@@ -53,7 +55,7 @@ def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
         par = s.get_int("direct_parallelism") if s.is_set("direct_parallelism") else 64
         return DirectExecutor(transport=transport, parallelism=par,
                               rancher_bootstrap=s.get_string("rancher_bootstrap") or "operator",
-                              node_cleanup=s.get_bool("node_cleanup"),
+                              node_cleanup=s.get_bool("node_cleanup") if s.is_set("node_cleanup") else True,
                               host_retries=s.get_int("host_retries") if s.is_set("host_retries") else 0,
                               retry_backoff=float(s.get_string("host_retry_backoff") or 2.0),
                               rancher_factory=ctx.extras.get("rancher_factory"))

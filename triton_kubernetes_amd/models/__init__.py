@@ -48,6 +48,6 @@ NODE_ENTRY_KEYS = {
             "gcp_disk_mount_path"],
     "azure": ["azure_size", "azure_ssh_user", "azure_public_key_path", "azure_disk_mount_path", "azure_disk_size"],
     "baremetal": ["ssh_user", "key_path", "bastion_host", "hosts", "gpu", "gpu_count", "gpu_burnin", "rccl_env",
-                  "rccl_min_busbw"],
+                  "rccl_min_busbw", "node_cleanup"],
     "vsphere": ["vsphere_template_name", "ssh_user", "key_path", "vsphere_num_cpus", "vsphere_memory_mb"],
 }

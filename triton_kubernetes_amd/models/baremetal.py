@@ -119,6 +119,9 @@ def new_node(ctx: Context, manager: str, cluster: str, backend, state: State) ->
         "ssh_user": ssh["ssh_user"],
         "key_path": ssh["key_path"],
     }
+    if ctx.is_set("node_cleanup"):
+        # the host module's destroy-time teardown (node/cleanup.py); unset: the module's default (on)
+        extra["node_cleanup"] = ctx.settings.get_bool("node_cleanup")
     if gpu == "mi355x":
         extra.update(_mi355x_fields(ctx))
 

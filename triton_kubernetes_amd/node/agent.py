@@ -109,6 +109,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         self._gate_results: Dict[bytes, Any] = {}
         # uid -> gate whose sweep is running (waiting for peers): /v1/rccl-abort cancels it
         self._sweeping: Dict[bytes, Any] = {}
+        # uid -> when /v1/rccl-abort named it: a later prepare/gate for it fails at once
+        self._aborted_uids: Dict[bytes, float] = {}
         # one RCCL unique id kept ready (new_uid): the gate's first request gets it without
         # an ncclGetUniqueId on the bring-up path; the pool makes the next one afterwards
         self._spare_uid: Optional[bytes] = None

@@ -46,13 +46,47 @@ class _SimGate:
         pass
 
 
+class GateAborted(RuntimeError):
+    """The gate was aborted (``/v1/rccl-abort``) before or while this request ran."""
+
+
+class _Reserved:
+    """A gate request's slot in ``_sweeping`` while its communicator is being created: an
+    abort that lands in that window marks it, and the request then releases what it made."""
+
+    devices: List[int] = []
+
+    def __init__(self) -> None:
+        self.canceled = False
+
+    def cancel(self) -> None:
+        self.canceled = True
+
+
 class AgentGateMixin:
-    """Mixin of :class:`~.agent.NodeAgent`: this node's ranks of cluster RCCL gates."""
+    """Mixin of :class:`~.agent.NodeAgent`: this node's ranks of cluster RCCL gates.
+
+    Abort ordering.  ``ClusterGate._gate_all`` (readiness/gate.py) sends ``/v1/rccl-abort``
+    to the other members while their gate requests are in flight, so an abort can land
+    before a member's request, between its take of the pending communicator and its sweep,
+    or during the sweep.  Every transition of a uid (pending -> sweeping, aborted) happens
+    under one hold of ``_gate_mu``, and an aborted uid is remembered for ``ABORTED_TTL_S``:
+    a later prepare or gate request for it fails at once instead of starting a fresh init
+    that would wait out its whole timeout for peers that are gone."""
 
     # --- RCCL gate (this node's ranks) ---------------------------------------------------------
     # Gate communicators pending by uid: started by /v1/rccl-prepare, consumed by
     # /v1/rccl-gate, released by /v1/rccl-abort, stop(), or expiry.
     GATE_TTL_S = 900.0
+    ABORTED_TTL_S = 900.0
+
+    def _is_aborted(self, uid: bytes) -> bool:
+        """(Caller holds ``_gate_mu``.)  ``uid`` was aborted recently; expires old entries."""
+        aborted = self.__dict__.setdefault("_aborted_uids", {})
+        now = time.time()
+        for k in [k for k, t in aborted.items() if now - t > self.ABORTED_TTL_S]:
+            del aborted[k]
+        return uid in aborted
 
     def _gate_devices(self, ndev: int) -> List[int]:
         devs = self.devices or [0]
@@ -114,6 +148,9 @@ class AgentGateMixin:
         self._expire_gates()
         if uid is None:
             uid = self.new_uid()
+        with self._gate_mu:
+            if self._is_aborted(uid):
+                raise GateAborted("gate aborted before this node's prepare")
         with span("node.rccl_prepare", node=self.name, rank_base=rank_base, world=world):
             if self._sim_gate:  # synthetic GPUs (tests / dry runs)
                 gate: Any = _SimGate(devs)
@@ -123,11 +160,16 @@ class AgentGateMixin:
                 self._used_rccl = True
                 gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False, prealloc_bytes=max_bytes)
         with self._gate_mu:
+            aborted = self._is_aborted(uid)  # an abort that landed during the init's start
             old = self._gates.pop(uid, None)
-            self._gates[uid] = (gate, time.time(), {"world": world, "rank_base": rank_base,
-                                                    "sizes": [int(x) for x in (sizes or [])]})
+            if not aborted:
+                self._gates[uid] = (gate, time.time(), {"world": world, "rank_base": rank_base,
+                                                        "sizes": [int(x) for x in (sizes or [])]})
         if old is not None:
             old[0].abort()
+        if aborted:
+            gate.abort()
+            raise GateAborted("gate aborted during this node's prepare")
         return {"ok": True, "ranks": list(range(rank_base, rank_base + len(devs))), "devices": devs,
                 "uid": base64.b64encode(uid).decode()}
 
@@ -136,6 +178,8 @@ class AgentGateMixin:
         sweep waiting for peers is canceled (it fails at once instead of at its timeout:
         another member of the gate failed)."""
         with self._gate_mu:
+            self._is_aborted(uid)
+            self.__dict__.setdefault("_aborted_uids", {})[uid] = time.time()
             entry = self._gates.pop(uid, None)
             done = self._gate_results.pop(uid, None)
             running = self._sweeping.get(uid)
@@ -165,10 +209,18 @@ class AgentGateMixin:
                   ndev: int = 1, timeout_s: float = 600.0) -> Dict[str, Any]:
         """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
         communicator from rccl_prepare when there is one, else a fresh init."""
+        key = uid  # the request's uid: /v1/rccl-abort names this one
         with self._gate_mu:
+            if self._is_aborted(key):
+                raise GateAborted("gate aborted before this node's sweep")
             entry = self._gates.pop(uid, None)
             done = self._gate_results.pop(uid, None)
+            # registered for cancel in the same hold that took it: no window in which an abort
+            # finds the gate neither pending nor sweeping
+            self._sweeping[key] = entry[0] if entry is not None else _Reserved()
         if done is not None:
+            with self._gate_mu:
+                self._sweeping.pop(key, None)
             res = done[0]
             if set(sizes) <= set(res.sizes):  # the rccl_local step swept this communicator
                 idx = [res.sizes.index(x) for x in sizes]
@@ -188,28 +240,35 @@ class AgentGateMixin:
             uid = self._make_uid()
         pipelined = entry is not None
         with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=pipelined):
-            if entry is not None:
-                gate = entry[0]
-            elif self._sim_gate:
-                gate = _SimGate(self._gate_devices(ndev))
-            else:
-                from ..ops import rccl
-
-                self._used_rccl = True
-                gate = rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
-            with self._gate_mu:
-                self._sweeping[uid] = gate
             try:
+                if entry is not None:
+                    gate = entry[0]
+                else:
+                    if self._sim_gate:
+                        gate = _SimGate(self._gate_devices(ndev))
+                    else:
+                        from ..ops import rccl
+
+                        self._used_rccl = True
+                        gate = rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
+                    with self._gate_mu:
+                        slot = self._sweeping.get(key)
+                        canceled = isinstance(slot, _Reserved) and slot.canceled
+                        if not canceled:
+                            self._sweeping[key] = gate
+                    if canceled:  # aborted while the communicator was being created
+                        gate.abort()
+                        raise GateAborted("gate aborted while this node's communicator started")
                 # the communicator teardown is not part of the readiness answer: it is
                 # joined in stop() (or by the next process-exit drain), not here
                 res = gate.sweep(sizes, iters=iters, warmup=2, async_teardown=True, timeout_s=timeout_s)
             finally:
                 with self._gate_mu:
-                    self._sweeping.pop(uid, None)
+                    self._sweeping.pop(key, None)
         out = res.to_json()
         out["pipelined"] = pipelined
         out["ranks"] = list(range(rank, rank + len(gate.devices)))
         return out
 
 
-__all__ = ["AgentGateMixin"]
+__all__ = ["AgentGateMixin", "GateAborted"]

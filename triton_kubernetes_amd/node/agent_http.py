@@ -25,6 +25,7 @@ import urllib.parse
 from typing import Any
 
 from ..utils.httpserver import Server as HTTPServer
+from .agent_gate import GateAborted
 from .plan import BootstrapPlan
 from .security import is_loopback, metrics_token
 
@@ -160,13 +161,14 @@ class AgentHTTPMixin:
                     if path == "/v1/rccl-abort":
                         return self._reply(200, agent.rccl_abort(base64.b64decode(body["uid"])))
                     if path == "/v1/cleanup":
-                        agent.last_labels = {}
-                        return self._reply(200, {"ok": True})
+                        return self._reply(200, agent.cleanup())
                     if path == "/v1/shutdown":
                         # the daemon's main loop (main()) stops the agent and exits; an
                         # embedded agent (no main loop) ignores it
                         agent.shutdown_requested.set()
                         return self._reply(200, {"ok": True})
+                except GateAborted as exc:
+                    return self._reply(409, {"error": f"GateAborted: {exc}", "aborted": True})
                 except Exception as exc:  # noqa: BLE001
                     return self._reply(500, {"error": f"{type(exc).__name__}: {exc}"})
                 return self._reply(404, {"error": "not found"})

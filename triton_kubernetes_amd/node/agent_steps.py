@@ -337,10 +337,42 @@ class AgentStepsMixin:
         if a == "agent":
             if plan.gpu is not None:
                 ctx["capacity"].setdefault("amd.com/gpu", len(self.devices))
+            from .cleanup import join_record, read_join_record, refusal, write_join_record
+
+            record_here = self._host_is_sandbox() or self.mode == "exec"
+            if record_here:  # a host still joined to another cluster is refused (node/cleanup.py)
+                why = refusal(read_join_record(self.path), plan.rancher_url, plan.token)
+                if why:
+                    raise StepFailed(step.name, why)
             if self.mode == "exec":
-                return self._exec_agent(plan, step, ctx["labels"], ctx["taints"])
-            return self._register(plan, ctx)
+                out = self._exec_agent(plan, step, ctx["labels"], ctx["taints"])
+            else:
+                out = self._register(plan, ctx)
+            if record_here:
+                write_join_record(self.path, join_record(plan.rancher_url, plan.token, plan.distribution,
+                                                         plan.hostname))
+            return out
         raise StepFailed(step.name, f"unknown action {a!r}")
+
+    def _host_is_sandbox(self) -> bool:
+        """A sim-mode agent models a host under its own root; with root ``/`` it models
+        nothing (it never writes to the machine it runs on)."""
+        return self.mode == "sim" and self.root not in ("", "/")
+
+    def cleanup(self) -> Dict[str, Any]:
+        """``POST /v1/cleanup``: take this host out of its cluster (node/cleanup.py) --
+        the vendor uninstallers at fixed paths, the RKE1 containers, the state directories
+        and the join record -- keeping this agent, the node tools and the runtime."""
+        from .cleanup import cleanup_host
+
+        self.last_labels = {}
+        if self.mode == "exec":
+            return cleanup_host(self.path, self._run_argv, docker=shutil.which("docker"))
+        if not self._host_is_sandbox():
+            return {"ok": True, "simulated": True, "actions": [], "ms": 0.0}
+        # sim: the host model's uninstallers (rancher/fake/hostsim.py) under this root
+        return dict(cleanup_host(self.path, self._run_argv, env=dict(os.environ, TK_HOST_ROOT=self.root)),
+                    simulated=True)
 
     def _gpu_preflight(self, expected: int) -> Dict[str, Any]:
         if self.topology_override is not None:
@@ -404,6 +436,12 @@ class AgentStepsMixin:
     def _register(self, plan: BootstrapPlan, ctx: Dict[str, Any]) -> Dict[str, Any]:
         roles = {"etcd": plan.role == "etcd", "controlplane": plan.role == "controlplane",
                  "worker": plan.role == "worker"}
+        if self._host_is_sandbox():  # what the real installer meets on this host
+            from ..rancher.fake import hostsim
+
+            why = hostsim.conflict(self.root, plan.rancher_url, plan.token)
+            if why:
+                raise RuntimeError(f"system-agent-install: {why}" if plan.distribution == "rke2" else why)
         http = HTTPClient(base_url=plan.rancher_url, verify_tls=False)
         hdrs = {"X-API-Tunnel-Token": plan.token,
                 "X-API-Tunnel-Params": tunnel_params(plan.hostname, roles, ctx["labels"], ctx["capacity"],
@@ -411,6 +449,11 @@ class AgentStepsMixin:
         if plan.distribution == "rke2":
             self._fetch_installer(plan)  # what a real node runs first
             hdrs["X-Cattle-Agent-Kind"] = "system-agent"
-        return http.request("POST", "/v3/connect/register", headers=hdrs, data=b"{}").json()
+        out = http.request("POST", "/v3/connect/register", headers=hdrs, data=b"{}").json()
+        if self._host_is_sandbox():
+            from ..rancher.fake import hostsim
+
+            hostsim.install(self.root, plan.rancher_url, plan.token, plan.distribution)
+        return out
 
 __all__ = ["AgentStepsMixin", "StepFailed", "StepResult"]

@@ -89,14 +89,3 @@ sk=$(printf '%s' "$tok" | python3 -c 'import json,sys; print(json.load(sys.stdin
 curl -ksf -u "$ak:$sk" -X PUT -H 'Content-Type: application/json' -d {_q(url_req)} "$R/v3/settings/server-url" >/dev/null
 printf '%s\\n' "$tok"
 """
-
-
-def node_cleanup_script() -> str:
-    """Remove the Rancher agent and RKE state from a host."""
-    return """#!/bin/bash
-set -uo pipefail
-ids=$(sudo docker ps -aq --filter 'ancestor=rancher/rancher-agent' 2>/dev/null; sudo docker ps -aq --filter 'label=io.rancher.rke.container.name' 2>/dev/null)
-[ -n "$ids" ] && sudo docker rm -f $ids >/dev/null
-sudo rm -rf /etc/kubernetes /var/lib/rancher /var/lib/etcd /etc/cni /opt/cni /var/lib/cni /etc/triton-kubernetes
-exit 0
-"""

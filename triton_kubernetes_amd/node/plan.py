@@ -49,6 +49,7 @@ from ..terraform.scripts import RCCL_SLIM_ENABLE_FN, RCCL_SLIM_FN, RCCL_SLIM_ROO
 from ..versions import AGENT_IMAGE as DEFAULT_AGENT_IMAGE
 from ..versions import DEFAULT_DISTRIBUTION, SYSTEM_AGENT_INSTALL_PATH
 from ..versions import DOCKER_INSTALL_URL as DEFAULT_DOCKER_INSTALL_URL
+from .cleanup import join_guard_shell, join_record_shell
 from .labels import DEFAULT_MIN_LINK_GBPS
 from .manager import docker_install_lines
 
@@ -311,11 +312,17 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
         label_args = (f' $(cat {LABEL_FILE} $([ -r {BURNIN_LABEL_FILE} ] && echo {BURNIN_LABEL_FILE}) '
                       f'| sed "s/^/--label /" | tr "\\n" " ")'
                       f'$([ -r {TAINT_FILE} ] && sed "s/^/ --taints /" {TAINT_FILE} | tr -d "\\n")')
+    # a host still joined to another cluster is refused before anything is installed, and a
+    # successful join is recorded (node/cleanup.py): reused bare metal is cleaned on destroy
+    guard = join_guard_shell(rancher_url, token)
+    record = join_record_shell(rancher_url, token, dist, hostname)
     if rke1:
         plan.steps.append(Step("agent", "agent", (
+            guard +
             f"sudo docker run -d --privileged --restart=unless-stopped --net=host "
             f"-v /etc/kubernetes:/etc/kubernetes -v /var/run:/var/run {_q(image)} "
-            f"--server {_q(rancher_url)} --token {_q(token)} --ca-checksum {_q(ca_checksum)} --{role}{label_args}"),
+            f"--server {_q(rancher_url)} --token {_q(token)} --ca-checksum {_q(ca_checksum)} --{role}{label_args}\n"
+            + record),
             {"image": image, "role": role, "distribution": "rke1"}))
     else:
         # the registration command Rancher shows for a custom RKE2 cluster: the server's
@@ -324,6 +331,7 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
         # cluster's CA checksum (an empty CA: a publicly trusted certificate)
         base = rancher_url.rstrip("/")
         plan.steps.append(Step("agent", "agent", (
+            guard +
             "_tk_installer=$(mktemp); _tk_ca=$(mktemp)\n"
             "trap 'rm -f \"$_tk_installer\" \"$_tk_ca\"' EXIT\n"
             f"curl -fsSLk -o \"$_tk_ca\" {_q(base + '/cacerts')}\n"
@@ -335,7 +343,8 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
             f"  curl -fsSL -o \"$_tk_installer\" {_q(base + SYSTEM_AGENT_INSTALL_PATH)}\n"
             "fi\n"
             f"sudo sh \"$_tk_installer\" --server {_q(rancher_url)} --label cattle.io/os=linux "
-            f"--token {_q(token)} --ca-checksum {_q(ca_checksum)} --node-name {_q(hostname)} --{role}{label_args}"),
+            f"--token {_q(token)} --ca-checksum {_q(ca_checksum)} --node-name {_q(hostname)} --{role}{label_args}\n"
+            + record),
             {"server": rancher_url, "role": role, "distribution": "rke2"}))
     return plan
 

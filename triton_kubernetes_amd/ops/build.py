@@ -15,11 +15,17 @@ artifact                       source                                      toolc
 =============================  ==========================================  =========
 
 Usage: ``python -m triton_kubernetes_amd.ops.build [--force] [-j N]``.
-Rebuilds only targets whose sources are newer than the artifact.
+Rebuilds only targets that are not current.  Every artifact gets a stamp
+(``lib/.stamps/<name>.sha256``): a sha256 over its sources' contents and its build command
+(paths made relative), written after a successful build.  An artifact is current when its
+stamp matches its sources -- not their mtimes, which a copy or an upload resets -- so a
+node tool can be checked against the sources it must have been built from (the MI355X
+host module's prebuilt tools, ``ops/probe.py``'s ``gpu-burnin`` child).
 """
 
 import argparse
 import concurrent.futures as cf
+import hashlib
 import os
 import shutil
 import subprocess
@@ -50,11 +56,58 @@ class Target:
     def output(self) -> str:
         return os.path.join(LIB, self.name)
 
+    @property
+    def stamp_path(self) -> str:
+        return os.path.join(LIB, ".stamps", self.name + ".sha256")
+
+    def source_hash(self) -> str:
+        """sha256 over the build command (locations replaced by placeholders, so the same
+        tree hashes the same wherever it is unpacked) and every source's name and bytes."""
+        return source_hash(self.name, self.sources, self.cmd)
+
+    def stamp(self) -> str:
+        try:
+            with open(self.stamp_path, "r", encoding="ascii") as fh:
+                return fh.read().strip()
+        except OSError:
+            return ""
+
     def stale(self) -> bool:
-        if not os.path.exists(self.output):
-            return True
-        mtime = os.path.getmtime(self.output)
-        return any(os.path.getmtime(s) > mtime for s in self.sources)
+        return not os.path.exists(self.output) or self.stamp() != self.source_hash()
+
+    def write_stamp(self) -> None:
+        os.makedirs(os.path.dirname(self.stamp_path), exist_ok=True)
+        tmp = self.stamp_path + ".tmp"
+        with open(tmp, "w", encoding="ascii") as fh:
+            fh.write(self.source_hash() + "\n")
+        os.replace(tmp, self.stamp_path)
+
+
+def source_hash(name: str, sources: Sequence[str], cmd: Sequence[str]) -> str:
+    h = hashlib.sha256()
+    h.update(name.encode() + b"\0")
+    for i, arg in enumerate(cmd):
+        # the compiler driver by name (hipcc is on PATH or under ROCm, either is the same)
+        arg = os.path.basename(arg) if i == 0 else arg.replace(LIB, "<lib>").replace(CSRC, "<csrc>").replace(
+            ROCM, "<rocm>")
+        h.update(arg.encode() + b"\0")
+    for src in sources:
+        h.update(os.path.basename(src).encode() + b"\0")
+        with open(src, "rb") as fh:
+            h.update(hashlib.sha256(fh.read()).digest())
+    return h.hexdigest()
+
+
+def target(name: str) -> "Target":
+    for t in targets():
+        if t.name == name:
+            return t
+    raise KeyError(name)
+
+
+def current(name: str) -> bool:
+    """The artifact ``name`` exists and was built from the sources in this tree."""
+    return not target(name).stale()
 
 
 def _hipcc() -> str:
@@ -102,6 +155,7 @@ def _run(t: Target) -> str:
     proc = subprocess.run(t.cmd, capture_output=True, text=True, check=False)
     if proc.returncode != 0:
         raise RuntimeError(f"building {t.name} failed:\n$ {' '.join(t.cmd)}\n{proc.stdout}\n{proc.stderr}")
+    t.write_stamp()
     return t.name
 
 

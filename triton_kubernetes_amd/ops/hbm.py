@@ -1,0 +1,96 @@
+"""HBM release backlog: wait until the kernel driver has finished clearing freed VRAM.
+
+The amdgpu driver clears VRAM that a process releases before it hands that memory out
+again (~35 GB/s per GPU, ``profiles/round4/alloc_probe.jsonl``).  Until the clear is done
+the memory is still accounted as used in the driver's VRAM manager
+(``/sys/class/drm/card*/device/mem_info_vram_used``), and an allocation that needs it
+waits: right after a full burn-in released ~300 GB, the next 16 GiB ``hipMalloc`` waited
+~6 s for the whole backlog.
+
+A node entering service starts with its HBM clear.  The bench therefore waits, between
+timed steps and outside the timed region, until the previous step's release has settled
+(:func:`settle`), so that a step is never charged for the clearing of its predecessor's
+memory.  Pure sysfs: no HIP call, so the waiting process does not touch the GPU.
+"""
+
+import glob
+import os
+import time
+from typing import Dict, Iterable, List, Optional, Tuple
+
+DRM_ROOT = "/sys/class/drm"
+
+
+def cards_for_pci(addresses: Iterable[Tuple[int, int, int]], drm_root: str = DRM_ROOT) -> List[str]:
+    """The DRM cards (``cardN``) of the GPUs at PCI ``(domain, bus, device)``: the GPUs this
+    process can see.  A shared host lists every GPU under ``/sys/class/drm``, other
+    tenants' too, whose allocations and releases must not be mistaken for ours."""
+    want = {(int(d), int(b), int(v)) for d, b, v in addresses}
+    out: List[str] = []
+    for dev in sorted(glob.glob(os.path.join(drm_root, "card*", "device"))):
+        card = dev.split(os.sep)[-2]
+        if "-" in card:
+            continue
+        bdf = os.path.basename(os.path.realpath(dev))  # e.g. 0000:75:00.0
+        try:
+            dom, bus, rest = bdf.split(":")
+            key = (int(dom, 16), int(bus, 16), int(rest.split(".")[0], 16))
+        except ValueError:
+            continue
+        if key in want:
+            out.append(card)
+    return out
+
+
+def vram_used(drm_root: str = DRM_ROOT, cards: Optional[Iterable[str]] = None) -> Dict[str, int]:
+    """``mem_info_vram_used`` of the amdgpu cards under ``drm_root`` (bytes, by card): every
+    card, or the ``cards`` named."""
+    only = set(cards) if cards is not None else None
+    out: Dict[str, int] = {}
+    for path in sorted(glob.glob(os.path.join(drm_root, "card*", "device", "mem_info_vram_used"))):
+        card = path.split(os.sep)[-3]
+        if "-" in card:  # connectors (card0-DP-1) share the device directory
+            continue
+        if only is not None and card not in only:
+            continue
+        try:
+            with open(path, "r", encoding="ascii") as fh:
+                out[card] = int(fh.read().strip() or 0)
+        except (OSError, ValueError):
+            continue
+    return out
+
+
+def settle(drm_root: str = DRM_ROOT, quiet_s: float = 0.5, poll_s: float = 0.02, timeout_s: float = 120.0,
+           baseline: Optional[int] = None, slack: int = 1 << 30,
+           cards: Optional[Iterable[str]] = None) -> Dict[str, float]:
+    """Block until the used VRAM of ``cards`` (default: every card) stops falling: none of
+    their ``mem_info_vram_used`` dropped during the last ``quiet_s`` seconds (the clearing
+    backlog drains at tens of GB/s, so a quiet window means it is empty), or their total is
+    within ``slack`` of ``baseline``.  Returns what it waited for; no cards: returns at once."""
+    cards = list(cards) if cards is not None else None
+    t0 = time.monotonic()
+    first = vram_used(drm_root, cards)
+    if not first:
+        return {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
+    last = dict(first)
+    quiet_since = t0
+    timed_out = False
+    while True:
+        total = sum(last.values())
+        if baseline is not None and total <= baseline + slack:
+            break
+        now = time.monotonic()
+        if now - quiet_since >= quiet_s:
+            break
+        if now - t0 >= timeout_s:
+            timed_out = True
+            break
+        time.sleep(poll_s)
+        cur = vram_used(drm_root, cards)
+        if any(cur.get(c, 0) < last.get(c, 0) for c in cur):
+            quiet_since = time.monotonic()
+        last = cur
+    return {"waited_s": round(time.monotonic() - t0, 4),
+            "released_gib": round(max(0, sum(first.values()) - sum(last.values())) / 2 ** 30, 2),
+            "cards": len(first), "timed_out": timed_out}

@@ -150,11 +150,21 @@ def gpu_present() -> bool:
 
 
 def executable(name: str) -> str:
-    path = lib_path(name)
-    if not os.path.exists(path):
-        from .build import build
+    """The in-tree tool ``name``, built from this tree's sources (``ops/build.py`` stamps):
+    a missing or stale tool is rebuilt when a compiler is there, else NativeUnavailable --
+    never a run of a binary that predates its sources (a stale ``gpu-burnin`` ignores the
+    flags it does not know and runs something else)."""
+    from .build import build, current
 
-        build(only=[name])
+    path = lib_path(name)
+    if not current(name):
+        try:
+            build(only=[name])
+        except Exception as exc:  # pragma: no cover - build env specific
+            raise NativeUnavailable(f"{name} is {'stale' if os.path.exists(path) else 'not built'} and "
+                                    f"building it failed: {exc}") from exc
+        if not current(name):
+            raise NativeUnavailable(f"{path} does not match its sources and could not be rebuilt")
     return path
 
 

@@ -18,6 +18,7 @@ from dataclasses import asdict, dataclass, field
 from typing import Any, Dict, List, Optional, Sequence
 
 from ..utils.trace import span
+from . import native
 from .native import LIB_DIR, load
 
 # MI355X reference figures (dense; never the 2:1-sparsity marketing numbers)
@@ -209,7 +210,13 @@ def wait_frees() -> None:
 # serialises their copies and frees behind each chunk's clearing, across processes) for
 # ~30 ms at a time instead of ~0.5 s (profiles/round4/span_chunk_ab.jsonl: the gate's sweep
 # after a full burn-in 4-6 ms with 1 GiB chunks, up to 0.5 s with 16 GiB ones).
-BURNIN_EXE = os.path.join(LIB_DIR, "gpu-burnin")
+
+
+def _burnin_exe() -> str:
+    """``gpu-burnin`` as built from this tree (NativeUnavailable if missing or stale)."""
+    return native.executable("gpu-burnin")
+
+
 SPAN_CHILD_CHUNK = int(float(os.environ.get("TK_SPAN_CHUNK_GIB", "1")) * (1 << 30))
 SPAN_RELEASE_TIMEOUT_S = 600.0
 _SPAN_PROCESS = False
@@ -248,12 +255,19 @@ def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, pas
         release_scratch(dev)
     _lib().tkp_wait_frees()
     _wait_span_children(dev)  # this device's previous span is released before this one allocates
-    argv = [BURNIN_EXE, "--memtest-span", "--device", str(int(dev)), "--span-bytes", str(int(nbytes)),
+    try:  # built from this tree's sources (a stale build would ignore --memtest-span)
+        exe = _burnin_exe()
+    except native.NativeUnavailable as exc:
+        return _span_in_process(dev, nbytes, headroom, passes, f"gpu-burnin unusable: {exc}")
+    argv = [exe, "--memtest-span", "--device", str(int(dev)), "--span-bytes", str(int(nbytes)),
             "--span-headroom", str(int(headroom)), "--span-passes", str(int(passes)),
             "--span-chunk", str(int(chunk or SPAN_CHILD_CHUNK))]
     t0 = time.perf_counter()
-    proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
-                            start_new_session=True)
+    try:
+        proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                                start_new_session=True)
+    except OSError as exc:
+        return _span_in_process(dev, nbytes, headroom, passes, f"cannot start {exe}: {exc}")
     with _span_mu:
         _span_children.append((dev, proc))
     # the verdict is the one JSON line (a library may print others); read on a thread, so a
@@ -284,11 +298,25 @@ def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, pas
     except ValueError as exc:
         proc.kill()
         raise ProbeError(f"memtest_span: unreadable verdict {line[:200]!r}") from exc
-    if not doc.get("ok"):
-        raise ProbeError(f"memtest_span: {doc.get('error', 'failed')}")
-    return {"errors": int(doc["errors"]), "verify_gbps": float(doc["verify_gbps"]), "bytes": int(doc["bytes"]),
-            "hbm_bytes": int(doc["hbm_bytes"]), "alloc_ms": float(doc["alloc_ms"]), "test_ms": float(doc["test_ms"]),
-            "free_ms": 0.0, "process_ms": round((time.perf_counter() - t0) * 1e3, 1)}
+    if not isinstance(doc, dict) or not doc.get("ok"):
+        raise ProbeError(f"memtest_span: {doc.get('error', 'failed') if isinstance(doc, dict) else doc!r}")
+    try:
+        return {"errors": int(doc["errors"]), "verify_gbps": float(doc["verify_gbps"]), "bytes": int(doc["bytes"]),
+                "hbm_bytes": int(doc["hbm_bytes"]), "alloc_ms": float(doc["alloc_ms"]),
+                "test_ms": float(doc["test_ms"]), "free_ms": 0.0,
+                "process_ms": round((time.perf_counter() - t0) * 1e3, 1)}
+    except (KeyError, TypeError, ValueError) as exc:
+        # not a --memtest-span verdict (a whole burn-in's report, say): no verdict at all
+        raise ProbeError(f"memtest_span: {exe} gave no memtest-span verdict ({type(exc).__name__}: {exc}): "
+                         f"{line[:200]!r}") from None
+
+
+def _span_in_process(dev: int, nbytes: int, headroom: int, passes: int, why: str) -> Dict[str, float]:
+    """The span memtest in this process (``gpu-burnin`` cannot run here): the same test,
+    released on this process's background thread; ``span_fallback`` says why."""
+    out: Dict[str, Any] = dict(memtest_span(dev, nbytes, headroom=headroom, passes=passes))
+    out["span_fallback"] = why
+    return out
 
 
 def _span(dev: int, nbytes: int, passes: int) -> Dict[str, float]:

@@ -31,7 +31,20 @@ from typing import Any, Callable, Dict, List, Optional
 
 from ..cloud.http import HTTPClient
 from ..errors import ExecutorError
+from ..node.cleanup import cleanup_script, parse_cleanup_markers
 from ..node.plan import BootstrapPlan, parse_step_markers
+
+
+def _cleanup_result(rc: int, stdout: str, stderr: str, where: str) -> Dict[str, Any]:
+    """A cleanup script's run -> its report (``node/cleanup.py`` markers); an exit without
+    the final marker (unreachable host: ssh's 255) is an error."""
+    rep = parse_cleanup_markers(stdout)
+    if not rep["complete"]:
+        rep.update(ok=False, error=f"{where}: exit {rc}: {(stderr or stdout)[-500:]}")
+    elif rc != 0:
+        failed = [a["what"] for a in rep["actions"] if a["status"] == "failed"]
+        rep["error"] = f"{where}: failed: {', '.join(failed) or 'exit ' + str(rc)}"
+    return rep
 
 
 @dataclass
@@ -68,6 +81,11 @@ class Transport:
         raise NotImplementedError
 
     def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
+        raise NotImplementedError
+
+    def cleanup_host(self, host: HostRef, timeout: float = 600) -> Dict[str, Any]:
+        """Take the host out of its cluster (``node/cleanup.py``): ``{"ok", "actions"}``,
+        plus ``"error"`` when the host could not be reached or the cleanup not run."""
         raise NotImplementedError
 
     def spawn(self, host: HostRef, script: str) -> subprocess.Popen:
@@ -158,6 +176,12 @@ class SSHTransport(Transport):
         self._check_key(host, proc.returncode, proc.stderr)
         return _shell_result(plan, proc.stdout, proc.returncode, (time.perf_counter() - t0) * 1e3, proc.stderr)
 
+    def cleanup_host(self, host: HostRef, timeout: float = 600) -> Dict[str, Any]:
+        proc = subprocess.run(self.ssh_argv(host, "bash -s"), input=cleanup_script(), capture_output=True,
+                              text=True, timeout=timeout, check=False)
+        self._check_key(host, proc.returncode, proc.stderr)
+        return _cleanup_result(proc.returncode, proc.stdout, proc.stderr, f"ssh {host.ssh_user}@{host.address}")
+
     def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
         dirname = os.path.dirname(remote_path)
         self.run_script(host, f"sudo mkdir -p {shlex.quote(dirname)} && sudo chown \"$(id -un)\" "
@@ -202,6 +226,11 @@ class LocalTransport(Transport):
         proc = subprocess.run(["bash", "-s"], input=plan.render_shell(), capture_output=True, text=True,
                               timeout=timeout, env=self._env(), check=False)
         return _shell_result(plan, proc.stdout, proc.returncode, (time.perf_counter() - t0) * 1e3, proc.stderr)
+
+    def cleanup_host(self, host: HostRef, timeout: float = 600) -> Dict[str, Any]:
+        proc = subprocess.run(["bash", "-s"], input=cleanup_script(), capture_output=True, text=True,
+                              timeout=timeout, env=self._env(), check=False)
+        return _cleanup_result(proc.returncode, proc.stdout, proc.stderr, "local")
 
     def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
         os.makedirs(os.path.dirname(remote_path), exist_ok=True)
@@ -265,6 +294,13 @@ class AgentTransport(Transport):
     def run_script(self, host: HostRef, script: str, timeout: float = 3600) -> str:
         raise ExecutorError("the node agent does not execute shell scripts; use an agent plan or the ssh transport")
 
+    def cleanup_host(self, host: HostRef, timeout: float = 600) -> Dict[str, Any]:
+        # the agent's own fixed-argv teardown (NodeAgent.cleanup): no script crosses the wire
+        try:
+            return self._client(host).post_json("/v1/cleanup", {})
+        except Exception as exc:  # noqa: BLE001 - reported, the destroy goes on
+            return {"ok": False, "error": f"{host.agent_url}: {type(exc).__name__}: {exc}", "actions": []}
+
     def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
         return None  # agents run the native probes in-process; nothing to upload
 
@@ -282,6 +318,7 @@ class RecordingTransport(Transport):
         self.plans: List[BootstrapPlan] = []
         self.scripts: List[str] = []
         self.files: List[str] = []
+        self.cleanups: List[str] = []
         self._mu = threading.Lock()
 
     def run_plan(self, host: HostRef, plan: BootstrapPlan, timeout: float = 3600) -> Dict[str, Any]:
@@ -304,6 +341,13 @@ class RecordingTransport(Transport):
     def put_file(self, host: HostRef, local_path: str, remote_path: str, mode: int = 0o755) -> None:
         with self._mu:
             self.files.append(remote_path)
+
+    def cleanup_host(self, host: HostRef, timeout: float = 600) -> Dict[str, Any]:
+        with self._mu:
+            self.cleanups.append(host.address)
+        if host.address in self.fail:
+            return {"ok": False, "error": self.fail[host.address], "actions": []}
+        return {"ok": True, "actions": []}
 
 
 class TransportRouter(Transport):
@@ -331,6 +375,9 @@ class TransportRouter(Transport):
 
     def put_file(self, host, local_path, remote_path, mode=0o755):
         return self.for_host(host).put_file(host, local_path, remote_path, mode)
+
+    def cleanup_host(self, host, timeout=600):
+        return self.for_host(host).cleanup_host(host, timeout)
 
     def spawn(self, host, script):
         return self.for_host(host).spawn(host, script)

@@ -14,7 +14,9 @@
   ``rkeConfig.registries.configs.<host>.authConfigSecretName`` refers to);
 * ``GET /system-agent-install.sh`` (unauthenticated) -- the node installer: a shell script
   that takes the real installer's flags, checks ``--ca-checksum`` against ``/cacerts`` and
-  registers the node (as ``rancher-system-agent``) through ``/v3/connect/register``.
+  registers the node (as ``rancher-system-agent``) through ``/v3/connect/register``.  Under
+  a ``TK_HOST_ROOT`` it also models the host (``hostsim.py``): it refuses a host still
+  holding another cluster's agent or RKE2, and leaves the installation and its uninstallers.
 
 Refusals (negative tests in ``tests/test_fake_rancher_contract.py``, ``test_v1_*``):
 
@@ -37,6 +39,7 @@ import uuid
 from typing import Any, Dict, List, Optional, Tuple
 
 from ...versions import FLEET_NAMESPACE, RKE2_CNIS, SYSTEM_AGENT_INSTALL_PATH
+from . import hostsim
 
 Reply = Tuple[int, Any]
 CLUSTERS = "/v1/provisioning.cattle.io.clusters"
@@ -69,12 +72,16 @@ if [ -n "$checksum" ]; then
   [ "$got" = "$checksum" ] || { echo "system-agent-install: configured cacerts checksum ($got) does not match --ca-checksum ($checksum)" >&2; exit 1; }
 fi
 [ -n "$name" ] || name=$(hostname)
+if [ -n "${TK_HOST_ROOT:-}" ]; then  # the host model (rancher/fake/hostsim.py)
+@@HOSTSIM@@
+fi
 params=$(printf '{"node":{"requestedHostname":"%s","etcd":%s,"controlPlane":%s,"worker":%s,"labels":{%s},"taints":[%s]}}' \
   "$name" $etcd $cp $worker "$labels" "$taints" | base64 | tr -d '\n')
 curl -fsSk -o /dev/null -X POST -H "X-API-Tunnel-Token: $token" -H "X-API-Tunnel-Params: $params" \
   -H "X-Cattle-Agent-Kind: system-agent" -d '{}' "$server/v3/connect/register" \
   || { echo "system-agent-install: registration with $server failed" >&2; exit 1; }
-"""
+if [ -n "${TK_HOST_ROOT:-}" ]; then _tk_install_files; fi
+""".replace("@@HOSTSIM@@", hostsim.installer_shell().rstrip("\n"))
 
 
 def _err(code: int, kind: str, message: str = "", **extra: Any) -> Reply:

@@ -31,6 +31,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from .. import sizing, versions
 from ..parallel import rccl_env
+from ..node.cleanup import cleanup_script
 from . import scripts
 from .catalog import MODULES_DIR
 
@@ -408,6 +409,48 @@ data "external" "rancher_api_key" {{
     bastion_host = local.bastion_host
     operation    = var.tk_operation
     known_hosts  = var.tk_known_hosts
+  }}
+}}
+'''
+
+
+NODE_CLEANUP_VAR = Var("node_cleanup", True,
+                       "on destroy, take the host out of its cluster: uninstall rancher-system-agent and RKE2 (or "
+                       "the RKE1 containers) and remove their state, keeping the node tools and the container "
+                       "runtime (bare metal outlives its cluster; node/cleanup.py)", "bool")
+
+
+def _node_cleanup(install: str) -> str:
+    """The bare-metal host's destroy-time teardown.  Destroy-time provisioners may reference
+    only ``self`` (and ``path``): the connection is kept in ``input``, refreshed by every
+    apply (``input`` changes update in place; only a new host replaces it, which tears
+    down the old host).  ``on_failure = continue``: a dead host must not pin the state."""
+    return f'''
+resource "terraform_data" "node_cleanup" {{
+  count            = var.node_cleanup ? 1 : 0
+  depends_on       = [terraform_data.{install}]
+  triggers_replace = [var.host]
+  input = {{
+    host             = var.host
+    user             = var.ssh_user
+    key_path         = var.key_path
+    host_key         = var.host_key
+    bastion_host     = var.bastion_host
+    bastion_host_key = var.bastion_host_key
+  }}
+  provisioner "remote-exec" {{
+    when       = destroy
+    on_failure = continue
+    connection {{
+      type             = "ssh"
+      user             = self.input.user
+      host             = self.input.host
+      private_key      = file(pathexpand(self.input.key_path))
+      host_key         = self.input.host_key == "" ? null : self.input.host_key
+      bastion_host     = self.input.bastion_host == "" ? null : self.input.bastion_host
+      bastion_host_key = self.input.bastion_host_key == "" ? null : self.input.bastion_host_key
+    }}
+    inline = [file("${{path.module}}/files/cleanup_host.sh")]
   }}
 }}
 '''
@@ -1225,7 +1268,7 @@ resource "azurerm_virtual_machine_data_disk_attachment" "data" {{
     # T16 bare-metal-rancher-k8s-host
     mods.append(Module("bare-metal-rancher-k8s-host", [], HOST_BASE + [
         Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa")]
-        + PINNED_KEY_VARS,
+        + PINNED_KEY_VARS + [NODE_CLEANUP_VAR],
         ROLE_LOCAL + f'''
 
 resource "terraform_data" "install_rancher_agent" {{
@@ -1235,7 +1278,7 @@ resource "terraform_data" "install_rancher_agent" {{
     inline = [{_agent_userdata()}]
   }}
 }}
-''', [], dict(HOST_FILES)))
+''' + _node_cleanup("install_rancher_agent"), [], dict(HOST_FILES, **{"cleanup_host.sh": cleanup_script()})))
 
     # T17 vsphere-rancher-k8s-host (CPU / memory are variables: Q15 fixed)
     mods.append(Module("vsphere-rancher-k8s-host", ["vsphere"], HOST_BASE + VSPHERE_CREDS + VSPHERE_NAMES + [
@@ -1299,7 +1342,7 @@ resource "terraform_data" "install_rancher_agent" {{
     # MI355X bare-metal host
     mods.append(Module("bare-metal-mi355x-rancher-k8s-host", ["external"], HOST_BASE + [
         Var("ssh_user", "ubuntu"), Var("host", None), Var("bastion_host", ""), Var("key_path", "~/.ssh/id_rsa"),
-        Var("tk_operation", "apply"), Var("tk_known_hosts", ""), *PINNED_KEY_VARS,
+        Var("tk_operation", "apply"), Var("tk_known_hosts", ""), *PINNED_KEY_VARS, NODE_CLEANUP_VAR,
         Var("gpu_product", "MI355X"), Var("gpu_count", 8, "GPUs the node must expose"),
         Var("gpu_burnin", "full", "quick | full | off"),
         Var("rccl_env", {}, "RCCL / HSA environment for GPU pods", "map(string)"),
@@ -1378,7 +1421,7 @@ resource "terraform_data" "install_mi355x_node" {{
     }})]
   }}
 }}
-
+''' + _node_cleanup("install_mi355x_node") + f'''
 data "external" "gpu_labels" {{
   depends_on = [terraform_data.install_mi355x_node]
   program    = ["bash", "${{path.module}}/files/read_gpu_labels.sh"]
@@ -1393,7 +1436,8 @@ data "external" "gpu_labels" {{
 }}
 ''', [("gpu_node_labels", "data.external.gpu_labels.result.labels", False),
           ("tk_ssh_known_hosts", "data.external.gpu_labels.result.known_hosts", False)],
-        {"install_mi355x_node.sh.tftpl": scripts.INSTALL_MI355X_NODE, "read_gpu_labels.sh": scripts.READ_REMOTE_LABELS},
+        {"install_mi355x_node.sh.tftpl": scripts.INSTALL_MI355X_NODE, "read_gpu_labels.sh": scripts.READ_REMOTE_LABELS,
+         "cleanup_host.sh": cleanup_script()},
         {"src/tk_topo.cpp": os.path.join(CSRC, "tk_topo.cpp"),
          "src/tk_gpu_probe.hip": os.path.join(CSRC, "tk_gpu_probe.hip"),
          "src/tk_gemm_screen.hip": os.path.join(CSRC, "tk_gemm_screen.hip"),

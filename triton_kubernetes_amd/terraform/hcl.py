@@ -585,6 +585,9 @@ def references(node: Any, bound: Optional[Set[str]] = None) -> List[Tuple[str, L
                         if a.name != "type":
                             visit(a.expr, b)
                     visit(Body(blocks=blk.body.blocks), b)
+                elif blk.type == "provisioner":  # `when = destroy`, `on_failure = continue`: keywords
+                    visit(Body(attributes=[a for a in blk.body.attributes if a.name not in ("when", "on_failure")],
+                               blocks=blk.body.blocks), b)
                 elif blk.type == "dynamic" and blk.labels:  # binds its label (or iterator) in content
                     it = blk.body.attr("iterator")
                     name = it.expr.value if it is not None and it.expr.kind == "trav" else blk.labels[0]

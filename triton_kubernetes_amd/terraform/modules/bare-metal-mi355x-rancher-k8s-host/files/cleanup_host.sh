@@ -1,0 +1,26 @@
+#!/bin/bash
+# triton-kubernetes host cleanup (node/cleanup.py): uninstall the cluster's agent and
+# Kubernetes distribution, keep the node tools and the container runtime
+set -uo pipefail
+R=${TK_HOST_ROOT:-}
+rc=0
+_tk_mark() { echo "::tk-cleanup $1 $2"; }
+for f in /usr/local/bin/rancher-system-agent-uninstall.sh /opt/rancher-system-agent/bin/rancher-system-agent-uninstall.sh /usr/local/bin/rke2-killall.sh /usr/local/bin/rke2-uninstall.sh /opt/rke2/bin/rke2-killall.sh /opt/rke2/bin/rke2-uninstall.sh; do
+  [ -x "$R$f" ] || continue
+  if sudo "$R$f" >/dev/null 2>&1; then _tk_mark "$f" ok; else _tk_mark "$f" failed; rc=1; fi
+done
+if command -v docker >/dev/null 2>&1; then
+  ids=$(for flt in ancestor=rancher/rancher-agent label=io.rancher.rke.container.name; do sudo docker ps -aq --filter "$flt" 2>/dev/null; done | sort -u)
+  if [ -n "$ids" ]; then
+    if sudo docker rm -f $ids >/dev/null 2>&1; then _tk_mark rke1-containers ok; else _tk_mark rke1-containers failed; rc=1; fi
+  fi
+fi
+# the kubelet's mounts (RKE1; rke2-killall.sh unmounts its own), deepest first
+mounts=$(awk -v p="$R/var/lib/kubelet" 'index($2, p) == 1 {print $2}' /proc/mounts 2>/dev/null | sort -r)
+for m in $mounts; do sudo umount "$m" >/dev/null 2>&1 || sudo umount -l "$m" >/dev/null 2>&1 || true; done
+for d in /etc/rancher /var/lib/rancher /etc/kubernetes /var/lib/etcd /var/lib/kubelet /etc/cni /opt/cni /var/lib/cni /var/run/calico /run/flannel /etc/triton-kubernetes/joined.json; do
+  [ -e "$R$d" ] || continue
+  if sudo rm -rf "$R$d"; then _tk_mark "$d" removed; else _tk_mark "$d" failed; rc=1; fi
+done
+echo "::tk-cleanup-done $rc"
+exit $rc

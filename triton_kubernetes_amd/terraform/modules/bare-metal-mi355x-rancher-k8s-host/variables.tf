@@ -179,6 +179,12 @@ variable "bastion_host_key" {
   default     = ""
 }
 
+variable "node_cleanup" {
+  description = "on destroy, take the host out of its cluster: uninstall rancher-system-agent and RKE2 (or the RKE1 containers) and remove their state, keeping the node tools and the container runtime (bare metal outlives its cluster; node/cleanup.py)"
+  type        = bool
+  default     = true
+}
+
 variable "gpu_product" {
   description = "Gpu product."
   type        = string

@@ -161,3 +161,9 @@ variable "bastion_host_key" {
   type        = string
   default     = ""
 }
+
+variable "node_cleanup" {
+  description = "on destroy, take the host out of its cluster: uninstall rancher-system-agent and RKE2 (or the RKE1 containers) and remove their state, keeping the node tools and the container runtime (bare metal outlives its cluster; node/cleanup.py)"
+  type        = bool
+  default     = true
+}

@@ -887,9 +887,41 @@ class _ModulePlan:
                 self.eval_dynamic(fn, nb, scope)
                 continue
             inner = scope.with_(self=_Instance("self")) if nb.type in ("connection", "provisioner") else scope
-            self.eval_body(fn, nb.body, inner)
+            if nb.type == "provisioner":
+                self.check_provisioner_meta(fn, nb)
+                self.eval_body(fn, nb.body, inner, skip=("when", "on_failure"))
+            else:
+                self.eval_body(fn, nb.body, inner)
             if nb.type == "provisioner" and nb.labels == ["file"]:
                 self.check_upload(fn, nb, inner)
+
+    # keyword meta-arguments of a provisioner, and what a destroy-time one may reference
+    PROVISIONER_KEYWORDS = {"when": ("create", "destroy"), "on_failure": ("continue", "fail")}
+    DESTROY_REFS = ("self", "count", "each", "path", "terraform")
+
+    def check_provisioner_meta(self, fn: str, blk: Block) -> None:
+        """``when`` / ``on_failure`` take keywords, not expressions; a destroy-time
+        provisioner (and its connection) may reference only ``self``, ``count.index``,
+        ``each.key``, ``path`` and ``terraform`` -- Terraform refuses anything else
+        ("Invalid reference from destroy provisioner")."""
+        destroy = False
+        for name, allowed in self.PROVISIONER_KEYWORDS.items():
+            a = blk.body.attr(name)
+            if a is None:
+                continue
+            word = a.expr.value if a.expr.kind == "trav" and isinstance(a.expr.value, str) else None
+            if word not in allowed:
+                self.report.errors.append(f"{self.where(fn, a.pos)}: {name}: must be one of {', '.join(allowed)}")
+            destroy = destroy or (name == "when" and word == "destroy")
+        if not destroy:
+            return
+        body = Body(attributes=[a for a in blk.body.attributes if a.name not in self.PROVISIONER_KEYWORDS],
+                    blocks=blk.body.blocks)
+        for root, _, pos in hcl.references(body):
+            if root not in self.DESTROY_REFS:
+                self.report.errors.append(
+                    f"{self.where(fn, pos)}: invalid reference from destroy provisioner: {root} (a destroy-time "
+                    f"provisioner may reference only self, count.index, each.key, path and terraform)")
 
     def eval_conditions(self, fn: str, lifecycle: Block, scope: _Scope) -> None:
         """``precondition`` blocks: a known false condition is the plan error Terraform

@@ -9,6 +9,13 @@ The document is read again under the backend lock before anything is destroyed, 
 nodes another run added meanwhile are destroyed with their cluster and its clusters
 are kept in the persisted document.
 
+Host teardown (on by default for bare metal: ``node_cleanup``): every
+destroyed bare-metal host is taken out of its cluster -- its rancher-system-agent and RKE2
+(or RKE1 containers) uninstalled, their state removed (``node/cleanup.py``) -- so the same
+host can join the next cluster.  The DirectExecutor does it over SSH or through the node
+agent; the Terraform host modules with a destroy-time provisioner.  A host whose cleanup
+failed is listed; its join record refuses the next join until it is cleaned.
+
 Extension (opt-in via ``rancher_cleanup: true``): also
 remove the cluster object (``destroy cluster``) or the node's object (``destroy node``:
 the Rancher node with that hostname, which also drops it from the Kubernetes node list)
@@ -41,7 +48,9 @@ def delete_manager(ctx: Context, backend: Backend) -> None:
     with backend.lock(manager):
         state = backend.state(manager)
         with span("destroy", scope="manager"):
-            executor_for(ctx, state, backend).destroy(state, backend, [])
+            executor = executor_for(ctx, state, backend)
+            executor.destroy(state, backend, [])
+        _report_cleanup(ctx, executor)
         backend.delete_state(manager)
 
 
@@ -65,7 +74,9 @@ def delete_cluster(ctx: Context, backend: Backend) -> None:
             targets.insert(0, addon)
         cleanup = _rancher_cleanup_info(ctx, backend, state, key)
         with span("destroy", scope="cluster", targets=len(targets)):
-            executor_for(ctx, state, backend).destroy(state, backend, [f"module.{t}" for t in targets])
+            executor = executor_for(ctx, state, backend)
+            executor.destroy(state, backend, [f"module.{t}" for t in targets])
+        _report_cleanup(ctx, executor)
         for t in targets:
             state.delete_module(t)
         backend.persist_state(state)
@@ -98,11 +109,26 @@ def delete_node(ctx: Context, backend: Backend) -> None:
         state = _reread(backend, manager, node_key)
         cleanup = _rancher_node_cleanup_info(ctx, backend, state, key, hostname)
         with span("destroy", scope="node"):
-            executor_for(ctx, state, backend).destroy(state, backend, [f"module.{node_key}"])
+            executor = executor_for(ctx, state, backend)
+            executor.destroy(state, backend, [f"module.{node_key}"])
+        _report_cleanup(ctx, executor)
         state.delete_module(node_key)
         backend.persist_state(state)
     if cleanup:
         cleanup()
+
+
+def _report_cleanup(ctx: Context, executor) -> None:
+    """One line per host the destroy took out of its cluster (the DirectExecutor's report;
+    Terraform prints its provisioners' output itself)."""
+    for key, rep in sorted((getattr(executor, "last_cleanup", None) or {}).items()):
+        host = rep.get("hostname", key)
+        if rep.get("ok"):
+            done = [a["what"].rsplit("/", 1)[-1] for a in rep.get("actions", []) if a.get("status") == "ok"]
+            ctx.echo(f"Cleaned up host {host}" + (f" ({', '.join(done)})" if done else ""))
+        else:
+            ctx.echo(f"WARNING: cleanup of host {host} failed: {rep.get('error', 'unknown error')}; "
+                     f"it cannot join another cluster until it is cleaned up")
 
 
 def _reread(backend: Backend, manager: str, key: str):
