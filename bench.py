@@ -364,6 +364,18 @@ def main() -> int:
                 if run.info.mi355x:
                     for st in detail.get("steps", []) or []:
                         steps[st.get("name")] = max(steps.get(st.get("name"), 0.0), float(st.get("ms") or 0.0))
+                        if st.get("name") == "gpu_burnin" and isinstance(st.get("detail"), dict):
+                            # each screen's wall time and the memtest's allocation, max over GPUs
+                            bp = out.setdefault("burnin_phase_ms", {})
+                            for res in st["detail"].values():
+                                if not isinstance(res, dict):
+                                    continue
+                                mt = res.get("memtest") or {}
+                                for k, v in list((res.get("phase_ms") or {}).items()) + [
+                                        ("memtest.alloc", mt.get("alloc_ms")), ("memtest.test", mt.get("test_ms")),
+                                        ("memtest.process", mt.get("process_ms"))]:
+                                    if v is not None:
+                                        bp[k] = round(max(bp.get(k, 0.0), float(v)), 1)
                         links = st.get("detail") if st.get("name") == "gpu_links" else None
                         if isinstance(links, dict) and links.get("labels"):
                             # the measured xGMI matrix (node/labels.py:link_labels), per worker
@@ -433,7 +445,7 @@ def main() -> int:
         rank 0 watches the node's cards; every rank waits for it."""
         got = {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
         if args.hbm_settle == "on" and my_cards and local_rank == 0:
-            got = hbm.settle(cards=my_cards)
+            got = hbm.settle(cards=my_cards, quiet_s=1.5)
         barrier()
         return got
 
@@ -576,8 +588,9 @@ def main() -> int:
             "rccl_gate_ranks": [r.get("rccl_gate_ranks", 0) for r in results],
             # the GPU nodes' measured xGMI peer-read matrix (2+ GPUs per node), last timed step
             "xgmi_links": next((r["xgmi_links"] for r in reversed(results) if r.get("xgmi_links")), None),
-            # the GPU node's burn-in step, per timed step (max over worker nodes)
+            # the GPU node's burn-in step, per timed step (max over worker nodes), and its screens
             "gpu_burnin_ms": [r.get("gpu_node_step_ms", {}).get("gpu_burnin") for r in results],
+            "burnin_phase_ms": [r.get("burnin_phase_ms") for r in results],
             # before each timed step, outside the timed region: the wait for the driver to clear
             # the previous step's released HBM (ops/hbm.py; --hbm-settle off for the A/B)
             "hbm_settle": args.hbm_settle,

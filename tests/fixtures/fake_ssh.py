@@ -6,8 +6,11 @@ A host is "up" when ``$FAKE_SSH_HOSTS/<host>/`` exists; that directory is its ho
 else one derived from its name.  A host that is down fails the way OpenSSH does: exit 255
 with "connect to host ... No route to host".
 
-Host keys are checked the way OpenSSH checks them, against ``-o UserKnownHostsFile=F``
-with ``-o StrictHostKeyChecking=``:
+A host may have several keys (``<dir>/host_keys``); it presents the one of the first
+algorithm in the client's ``HostKeyAlgorithms`` (OpenSSH's default order, Ed25519 first,
+without it), and ``UpdateHostKeys=yes`` pins the others after the first is verified.
+Host keys are checked the way OpenSSH checks them, per key type, against
+``-o UserKnownHostsFile=F`` with ``-o StrictHostKeyChecking=``:
 
 * ``no``: not checked (nothing recorded);
 * ``accept-new``: an unknown host's key is appended to F, a known host's must match;
@@ -54,30 +57,54 @@ def parse(argv):
     return opts, flags, argv[i:]
 
 
-def host_key(host):
+# OpenSSH's default host key algorithm order (Ed25519 first); rsa-sha2-* verify ssh-rsa keys
+OPENSSH_DEFAULT_ALGS = ["ssh-ed25519", "ecdsa-sha2-nistp256", "ecdsa-sha2-nistp384", "ecdsa-sha2-nistp521",
+                        "rsa-sha2-512", "rsa-sha2-256"]
+
+
+def host_keys(host):
+    """Every key of the host: ``<dir>/host_keys`` (one per line), ``<dir>/host_key``, or one
+    ed25519 key derived from its name."""
     d = os.path.join(os.environ.get("FAKE_SSH_HOSTS", "/nonexistent"), host)
-    path = os.path.join(d, "host_key")
-    if os.path.exists(path):
-        return open(path, encoding="utf-8").read().strip()
+    for name in ("host_keys", "host_key"):
+        path = os.path.join(d, name)
+        if os.path.exists(path):
+            return [" ".join(ln.split()[:2]) for ln in open(path, encoding="utf-8") if ln.strip()]
     blob = base64.b64encode(b"\x00\x00\x00\x0bssh-ed25519\x00\x00\x00\x20" + hashlib.sha256(host.encode()).digest())
-    return "ssh-ed25519 " + blob.decode()
+    return ["ssh-ed25519 " + blob.decode()]
+
+
+def host_key(host, opts=None):
+    """The key the host presents: the first of the client's HostKeyAlgorithms (OpenSSH's
+    default order without the option) the host has a key for."""
+    keys = host_keys(host)
+    algs = (opts or {}).get("hostkeyalgorithms")
+    for alg in (algs.split(",") if algs else OPENSSH_DEFAULT_ALGS):
+        ktype = "ssh-rsa" if alg.startswith("rsa-sha2-") else alg
+        for k in keys:
+            if k.split(" ", 1)[0] == ktype:
+                return k
+    return keys[0]
 
 
 def check_key(host, opts):
-    """None when the connection may proceed, else OpenSSH's error text."""
+    """None when the connection may proceed, else OpenSSH's error text.  As OpenSSH: a
+    pinned key of the presented key's type must match; no pinned key of that type is a new
+    key (accept-new adds it); UpdateHostKeys=yes then pins the host's other keys."""
     mode = opts.get("stricthostkeychecking", "yes").lower()
     if mode == "no":
         return None
     path = opts.get("userknownhostsfile", os.path.expanduser("~/.ssh/known_hosts")).split()[0]
-    want = host_key(host)
+    want = host_key(host, opts)
     pinned = []
     if path != "/dev/null" and os.path.exists(path):
         for line in open(path, encoding="utf-8"):
             parts = line.split()
-            if len(parts) >= 3 and host in parts[0].split(","):
+            if len(parts) >= 3 and host in parts[0].split(",") and parts[1] == want.split(" ", 1)[0]:
                 pinned.append(f"{parts[1]} {parts[2]}")
     if pinned:
         if want in pinned:
+            _update_host_keys(host, opts, path)
             return None
         return ("@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@@\n"
                 "@    WARNING: REMOTE HOST IDENTIFICATION HAS CHANGED!     @\n"
@@ -87,9 +114,22 @@ def check_key(host, opts):
     if mode in ("accept-new", "off") and path != "/dev/null":
         with open(path, "a", encoding="utf-8") as fh:
             fh.write(f"{host} {want}\n")
+        _update_host_keys(host, opts, path)
         return None
     return f"No ED25519 host key is known for {host} and you have requested strict checking.\n" \
            "Host key verification failed.\n"
+
+
+def _update_host_keys(host, opts, path):
+    if opts.get("updatehostkeys", "no").lower() != "yes" or path == "/dev/null":
+        return
+    have = set()
+    if os.path.exists(path):
+        have = {" ".join(ln.split()[:3]) for ln in open(path, encoding="utf-8") if ln.strip()}
+    with open(path, "a", encoding="utf-8") as fh:
+        for k in host_keys(host):
+            if f"{host} {k}" not in have:
+                fh.write(f"{host} {k}\n")
 
 
 def main() -> int:

@@ -176,3 +176,20 @@ def test_expression_evaluator_for_expressions_and_list_predicates(src, want):
     body = hcl.parse(f"x = {src}\n")
     expr = body.attr("x").expr
     assert hcl.eval_expr(expr, {"m": {"b": "2", "a": "1"}, "l": ["x", "y", "z"]}) == want
+
+
+def test_regexall_translates_only_bare_dollars():
+    """``$`` inside a character class or after an escaped backslash keeps its
+    RE2 meaning (``[$]`` a literal; ``\\\\$`` a backslash at the end)."""
+    from triton_kubernetes_amd.terraform import hcl as h
+
+    assert h.re2_pattern("^a$") == "^a\\Z"
+    assert h.re2_pattern("[$]x") == "[$]x"
+    assert h.re2_pattern("[^]$]+$") == "[^]$]+\\Z"
+    assert h.re2_pattern("\\\\$") == "\\\\\\Z"
+    assert h.re2_pattern("a\\$b") == "a\\$b"
+    regexall = h._FUNCS["regexall"]
+    assert regexall("[$]", "cost: $5") == ["$"]
+    assert regexall("\\\\$", "ends with \\") == ["\\"]
+    assert regexall("^ab$", "ab\n") == []  # RE2: no match before a final newline
+    assert regexall("^ab$", "ab") == ["ab"]

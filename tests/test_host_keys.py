@@ -179,3 +179,32 @@ def test_terraform_path_pins_the_manager_and_refuses_a_changed_key(tmp_path, hos
     with pytest.raises(TKError):
         new_cluster(make_ctx(cluster), backend)
     assert _pinned(backend) == pinned
+
+
+def test_host_with_several_key_types_pins_the_one_terraform_negotiates(tmp_path, hosts):
+    """a host with ed25519, ecdsa and rsa keys.  Go's x/crypto/ssh (Terraform's
+    provisioner client) prefers ECDSA, then RSA, then Ed25519; OpenSSH by default presents
+    Ed25519.  Every ssh of this framework offers Go's order, so the first contact pins the
+    ECDSA key, UpdateHostKeys pins the other two, and the Terraform render shows each
+    module the ECDSA key -- the one its connection will be presented."""
+    from triton_kubernetes_amd.executor.terraform import render
+
+    keys = {"ssh-ed25519": "AAAAC3NzaC1lZDI1NTE5AAAAIEDxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxx",
+            "ecdsa-sha2-nistp256": "AAAAE2VjZHNhLXNoYTItbmlzdHAyNTYAAAAIbmlzdHAyNTYAAABBBECDSAxxxxxxxxx",
+            "ssh-rsa": "AAAAB3NzaC1yc2EAAAADAQABAAABAQDRSAxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxxx"}
+    for h in ("10.1.0.1", "10.1.0.2", "jump.example"):
+        (hosts / h / "host_keys").write_text("".join(f"{t} {b}\n" for t, b in keys.items()))
+    with FakeRancher.for_manager("mgr", PW) as fake:
+        backend = _cluster(tmp_path, fake)
+    pinned = _pinned(backend)
+    first = [ln.split()[1] for ln in pinned.splitlines() if ln.startswith("10.1.0.1 ")]
+    assert first[0] == "ecdsa-sha2-nistp256" and sorted(first) == sorted(keys)  # negotiated first, then the rest
+    calls = [json.loads(ln) for ln in open(tmp_path / "ssh.jsonl")]
+    assert all(c["opts"]["hostkeyalgorithms"].split(",")[0] == "ecdsa-sha2-nistp256" and
+               c["opts"]["hostkeyalgorithms"].split(",")[-1] == "ssh-ed25519" for c in calls)
+    st = backend.state("mgr")
+    doc = json.loads(render(st, (1, 5, 7), known_hosts=pinned).body)
+    node = doc["module"]["node_baremetal_dev_e-1"]
+    assert node["host_key"] == f"ecdsa-sha2-nistp256 {keys['ecdsa-sha2-nistp256']}"
+    assert hostkeys.preferred_key([f"ssh-ed25519 x", "ssh-rsa y"]) == "ssh-rsa y"
+    assert hostkeys.preferred_key(["ssh-ed25519 x"]) == "ssh-ed25519 x"

@@ -55,7 +55,7 @@ from ..state import State
 from ..terraform import constraints
 from ..terraform.catalog import (check_sources, declared_variables, is_packaged_source, local_module_dir,
                                  module_from_source, outputs_for_source, resolve_source, sensitive_outputs)
-from ..parallel.hostkeys import HostKeys, keys_for
+from ..parallel.hostkeys import HostKeys, keys_for, preferred_key
 from ..utils.jsonenc import dumps_go
 from .base import Executor, outputs_from_tfstate
 from .shell import ShellOptions, capture_command, run_shell_command
@@ -167,7 +167,7 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
             for var, addr in (("host_key", mod.get("host")), ("bastion_host_key", mod.get("bastion_host"))):
                 pinned = keys_for(known_hosts, str(addr or "")) if known_hosts and addr else []
                 if var in declared and var not in mod and pinned:
-                    mod[var] = pinned[0]
+                    mod[var] = preferred_key(pinned)  # the type Terraform's Go client negotiates
         for var, default in root_vars.items():
             doc.setdefault("variable", {})[var] = {"type": "string", "default": default}
         outputs = doc.setdefault("output", {})

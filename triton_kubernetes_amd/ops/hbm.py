@@ -61,13 +61,17 @@ def vram_used(drm_root: str = DRM_ROOT, cards: Optional[Iterable[str]] = None) -
     return out
 
 
-def settle(drm_root: str = DRM_ROOT, quiet_s: float = 0.5, poll_s: float = 0.02, timeout_s: float = 120.0,
+def settle(drm_root: str = DRM_ROOT, quiet_s: float = 1.5, poll_s: float = 0.02, timeout_s: float = 120.0,
            baseline: Optional[int] = None, slack: int = 1 << 30,
            cards: Optional[Iterable[str]] = None) -> Dict[str, float]:
     """Block until the used VRAM of ``cards`` (default: every card) stops falling: none of
     their ``mem_info_vram_used`` dropped during the last ``quiet_s`` seconds (the clearing
     backlog drains at tens of GB/s, so a quiet window means it is empty), or their total is
-    within ``slack`` of ``baseline``.  Returns what it waited for; no cards: returns at once."""
+    within ``slack`` of ``baseline``.  Returns what it waited for; no cards: returns at once.
+
+    The driver returns a released allocation to the free pool whole, once it is cleared:
+    a 16 GiB one drops ``mem_info_vram_used`` in one step ~0.5 s after the previous
+    (``profiles/round5/vram_release.jsonl``), so the quiet window spans several of those."""
     cards = list(cards) if cards is not None else None
     t0 = time.monotonic()
     first = vram_used(drm_root, cards)

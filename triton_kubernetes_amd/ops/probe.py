@@ -7,6 +7,7 @@ spec, dense bf16 MFMA ~2.5 PFLOP/s, block-scaled fp8 ~5 PFLOP/s.  A GPU that
 fails a threshold or the memtest marks the node not-ready.
 """
 
+import contextlib
 import ctypes
 import json
 import os
@@ -436,6 +437,7 @@ class BurninResult:
     memtest: Dict[str, float] = field(default_factory=dict)
     failures: List[str] = field(default_factory=list)
     remeasured: List[str] = field(default_factory=list)  # throughput gates read low and measured again
+    phase_ms: Dict[str, float] = field(default_factory=dict)  # wall time of each screen, as run
 
     @property
     def ok(self) -> bool:
@@ -445,6 +447,17 @@ class BurninResult:
         d = asdict(self)
         d["ok"] = self.ok
         return d
+
+
+@contextlib.contextmanager
+def _phase(res: "BurninResult", name: str, dev: int):
+    """A burn-in screen: a trace span, and its wall time in ``res.phase_ms``."""
+    t0 = time.perf_counter()
+    with span(f"burnin.{name}", dev=dev):
+        try:
+            yield
+        finally:
+            res.phase_ms[name] = round(res.phase_ms.get(name, 0.0) + (time.perf_counter() - t0) * 1e3, 1)
 
 
 def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] = None) -> BurninResult:
@@ -473,16 +486,16 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
                 r = again
         return r
 
-    with span("burnin.hbm", dev=dev):
+    with _phase(res, "hbm", dev):
         floor = th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS * th.share
         res.hbm = best(lambda: hbm_bandwidth(dev, hbm_bytes, hbm_iters), lambda r: r["read_gbps"], floor, "hbm")
     if res.hbm["read_gbps"] < floor:
         res.failures.append(f"HBM read {res.hbm['read_gbps']:.0f} GB/s below "
                             f"{th.min_read_frac:.0%} of {MI355X_HBM_ACHIEVABLE_GBPS:.0f}")
-    with span("burnin.mfma_bf16", dev=dev):
+    with _phase(res, "mfma_bf16", dev):
         res.mfma["bf16"] = best(lambda: mfma_peak(dev, "bf16", mfma_iters), lambda r: r["tflops"],
                                 th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS * th.share, "mfma_bf16")
-    with span("burnin.mfma_fp8", dev=dev):
+    with _phase(res, "mfma_fp8", dev):
         res.mfma["fp8"] = best(lambda: mfma_peak(dev, "fp8", mfma_iters // 2), lambda r: r["tflops"],
                                th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS * th.share, "mfma_fp8")
     if res.mfma["bf16"]["tflops"] < th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS * th.share:
@@ -505,7 +518,7 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
             return g
 
         peak = peak * th.share
-        with span(f"burnin.gemm_{dtype}", dev=dev):
+        with _phase(res, f"gemm_{dtype}", dev):
             g = best(screen_once, lambda r: r.tflops, frac * peak, f"gemm_{dtype}")
         if dtype == "bf16":
             res.gemm = g.to_json()
@@ -517,7 +530,7 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
                                 f"(first at row {bad.first_bad_row}, column {bad.first_bad_column})")
         if g.tflops < frac * peak:
             res.failures.append(f"{name} {g.tflops:.0f} TF below {frac:.0%} of dense {dtype} peak")
-    with span("burnin.memtest", dev=dev):
+    with _phase(res, "memtest", dev):
         if mt_bytes:
             res.memtest = memtest(dev, mt_bytes, mt_passes)
             res.memtest.update(bytes=mt_bytes, hbm_bytes=int(info.total_mem_gib * (1 << 30)))

@@ -39,6 +39,28 @@ from typing import Dict, Iterable, List
 from ..errors import ExecutorError
 
 BLOB = "known_hosts"
+
+# Host key algorithms in the order Go's x/crypto/ssh (Terraform's provisioner connections)
+# prefers them: ECDSA, then RSA, then Ed25519 last -- OpenSSH's own default puts Ed25519
+# first.  Every ssh this framework runs offers this order, so the key it pins on first
+# contact is of the type Terraform will be shown later; UpdateHostKeys=yes pins the host's
+# other keys too (OpenSSH's hostkeys extension, after the first key was verified), and the
+# Terraform render picks the pinned key Go would negotiate (``preferred_key``).
+GO_HOSTKEY_ALGORITHMS = ("ecdsa-sha2-nistp256", "ecdsa-sha2-nistp384", "ecdsa-sha2-nistp521",
+                         "rsa-sha2-512", "rsa-sha2-256", "ssh-ed25519")
+# the key type (known_hosts field 2) each algorithm verifies
+_KEY_TYPE = {"rsa-sha2-512": "ssh-rsa", "rsa-sha2-256": "ssh-rsa"}
+NEGOTIATION_OPTS = ["-o", "HostKeyAlgorithms=" + ",".join(GO_HOSTKEY_ALGORITHMS), "-o", "UpdateHostKeys=yes"]
+
+
+def preferred_key(keys: List[str]) -> str:
+    """The pinned key (``"<type> <base64>"``) of the type Go's client negotiates first
+    among ``keys`` (all keys pinned for one host); ``""`` when none."""
+    rank = {}
+    for i, alg in enumerate(GO_HOSTKEY_ALGORITHMS):
+        rank.setdefault(_KEY_TYPE.get(alg, alg), i)
+    ranked = sorted(keys, key=lambda k: rank.get(k.split(" ", 1)[0], len(rank)))
+    return ranked[0] if ranked else ""
 # what OpenSSH prints when a pinned key does not match
 MISMATCH_MARKERS = ("Host key verification failed", "REMOTE HOST IDENTIFICATION HAS CHANGED",
                     "host key mismatch")
@@ -184,7 +206,7 @@ class HostKeys:
 
     def ssh_options(self) -> List[str]:
         return ["-o", f"UserKnownHostsFile={self.path}", "-o", "StrictHostKeyChecking=accept-new",
-                "-o", "HashKnownHosts=no", "-o", "GlobalKnownHostsFile=/dev/null"]
+                "-o", "HashKnownHosts=no", "-o", "GlobalKnownHostsFile=/dev/null", *NEGOTIATION_OPTS]
 
     def close(self) -> None:
         shutil.rmtree(self._dir, ignore_errors=True)
@@ -197,14 +219,15 @@ class HostKeys:
 
 
 def pinned_map(text: str, addresses: Iterable[str]) -> Dict[str, str]:
-    """``{address: "<type> <base64>"}`` of the addresses with a pinned key (the first)."""
+    """``{address: "<type> <base64>"}`` of the addresses with a pinned key (the one Go's
+    client negotiates: ``preferred_key``)."""
     out = {}
     for a in addresses:
         k = keys_for(text, a)
         if k:
-            out[a] = k[0]
+            out[a] = preferred_key(k)
     return out
 
 
 __all__ = ["HostKeys", "HostKeyChanged", "BLOB", "merge", "keys_for", "mismatch_error", "looks_like_mismatch",
-           "pinned_map"]
+           "pinned_map", "preferred_key", "GO_HOSTKEY_ALGORITHMS", "NEGOTIATION_OPTS"]

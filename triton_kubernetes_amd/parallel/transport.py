@@ -130,8 +130,10 @@ class SSHTransport(Transport):
             return ["-o", "StrictHostKeyChecking=yes"]
         if self.host_keys is not None:
             return self.host_keys.ssh_options()
+        from .hostkeys import NEGOTIATION_OPTS
+
         return ["-o", f"UserKnownHostsFile={self.control_dir}/known_hosts", "-o", "StrictHostKeyChecking=accept-new",
-                "-o", "HashKnownHosts=no", "-o", "GlobalKnownHostsFile=/dev/null"]
+                "-o", "HashKnownHosts=no", "-o", "GlobalKnownHostsFile=/dev/null", *NEGOTIATION_OPTS]
 
     def base_opts(self, host: HostRef) -> List[str]:
         opts = ["-o", "BatchMode=yes", "-o", f"ConnectTimeout={self.connect_timeout}",

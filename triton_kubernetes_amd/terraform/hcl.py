@@ -858,12 +858,39 @@ _FUNCS = {
     "contains": lambda lst, v: v in lst,
     "split": lambda sep, v: str(v).split(str(sep)),
     "slice": lambda lst, a, b: list(lst)[int(a):int(b)],
-    # RE2's "$" matches only at the end of the text (Python's also before a final newline)
-    "regexall": lambda pat, v: __import__("re").findall(__import__("re").sub(r"(?<!\\)\$", r"\\Z", str(pat)),
-                                                        str(v)),
+    "regexall": lambda pat, v: __import__("re").findall(re2_pattern(str(pat)), str(v)),
     "alltrue": lambda items: all(x is True or x == "true" for x in items),
     "anytrue": lambda items: any(x is True or x == "true" for x in items),
 }
+
+
+def re2_pattern(pat: str) -> str:
+    """An RE2 pattern (Terraform's ``regex``/``regexall``) for Python's ``re``: RE2's ``$``
+    matches only at the end of the text, Python's also before a final newline, so a bare
+    ``$`` becomes ``\\Z``.  Escaped pairs (``\\$``, ``\\\\``) and character classes
+    (``[$]``, ``[^]$]``) are copied as they are: there ``$`` is a literal."""
+    out: List[str] = []
+    i, n = 0, len(pat)
+    while i < n:
+        c = pat[i]
+        if c == "\\" and i + 1 < n:
+            out.append(pat[i:i + 2])
+            i += 2
+            continue
+        if c == "[":
+            j = i + 1
+            if j < n and pat[j] == "^":
+                j += 1
+            if j < n and pat[j] == "]":  # a leading ']' is a member, not the end
+                j += 1
+            while j < n and pat[j] != "]":
+                j += 2 if pat[j] == "\\" else 1
+            out.append(pat[i:j + 1])
+            i = j + 1
+            continue
+        out.append("\\Z" if c == "$" else c)
+        i += 1
+    return "".join(out)
 
 
 def _to_str(v: Any) -> str:

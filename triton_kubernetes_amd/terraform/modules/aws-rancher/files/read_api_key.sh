@@ -11,7 +11,10 @@ eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".joi
 # pinned on this first contact and reported back (result key known_hosts).
 kh=$(mktemp); err=$(mktemp); trap 'rm -f "$kh" "$err"' EXIT
 printf '%s\n' "${known_hosts:-}" > "$kh"
-ko=(-o "UserKnownHostsFile=$kh" -o StrictHostKeyChecking=accept-new -o HashKnownHosts=no -o GlobalKnownHostsFile=/dev/null)
+# host key algorithms in Go's order (Terraform's client): the key pinned here is the type
+# Terraform's provisioner connections negotiate; UpdateHostKeys pins the host's other keys
+ko=(-o "UserKnownHostsFile=$kh" -o StrictHostKeyChecking=accept-new -o HashKnownHosts=no -o GlobalKnownHostsFile=/dev/null
+    -o "HostKeyAlgorithms=ecdsa-sha2-nistp256,ecdsa-sha2-nistp384,ecdsa-sha2-nistp521,rsa-sha2-512,rsa-sha2-256,ssh-ed25519" -o UpdateHostKeys=yes)
 key="${key_path/#\~/$HOME}"
 opts=(-o BatchMode=yes -o LogLevel=ERROR "${ko[@]}" -i "$key")
 if [ -n "${bastion_host:-}" ]; then

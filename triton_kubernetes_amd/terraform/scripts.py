@@ -8,6 +8,7 @@ templates, and they fix the reference quirks Q10
 """
 
 from ..node.hosttune import shell_check as _host_tuning_check
+from ..parallel.hostkeys import GO_HOSTKEY_ALGORITHMS
 from ..node.metrics import textfile_script as _metrics_textfile
 
 # download, verify (when docker_install_sha256 is set), run — no `curl | sh` of an unchecked stream
@@ -87,7 +88,10 @@ SSH_PINNED = r"""# SSH with the cluster manager's pinned host keys (query key kn
 # pinned on this first contact and reported back (result key known_hosts).
 kh=$(mktemp); err=$(mktemp); trap 'rm -f "$kh" "$err"' EXIT
 printf '%s\n' "${known_hosts:-}" > "$kh"
-ko=(-o "UserKnownHostsFile=$kh" -o StrictHostKeyChecking=accept-new -o HashKnownHosts=no -o GlobalKnownHostsFile=/dev/null)
+# host key algorithms in Go's order (Terraform's client): the key pinned here is the type
+# Terraform's provisioner connections negotiate; UpdateHostKeys pins the host's other keys
+ko=(-o "UserKnownHostsFile=$kh" -o StrictHostKeyChecking=accept-new -o HashKnownHosts=no -o GlobalKnownHostsFile=/dev/null
+    -o "HostKeyAlgorithms=@@HKA@@" -o UpdateHostKeys=yes)
 key="${key_path/#\~/$HOME}"
 opts=(-o BatchMode=yes -o LogLevel=ERROR "${ko[@]}" -i "$key")
 if [ -n "${bastion_host:-}" ]; then
@@ -103,7 +107,7 @@ refused() {
   fi
   exit 1
 }
-"""
+""".replace("@@HKA@@", ",".join(GO_HOSTKEY_ALGORITHMS))
 
 READ_API_KEY = r"""#!/bin/bash
 # data "external" program: read the manager's ~/rancher_api_key over SSH.
