@@ -178,7 +178,7 @@ def test_find_only_scripts_outside_apply(tmp_path, env, rancher):
     read_key = os.path.join(catalog.MODULES_DIR, "bare-metal-rancher", "files", "read_api_key.sh")
     labels = os.path.join(catalog.MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files", "read_gpu_labels.sh")
     down = {"host": "10.9.9.9", "ssh_user": "u", "key_path": "k", "bastion_host": ""}
-    for script, empty in ((read_key, {"access_key": "", "secret_key": "", "known_hosts": ""}),
+    for script, empty in ((read_key, {"access_key": "", "secret_key": "", "known_hosts": "", "ca_certs": ""}),
                           (labels, {"labels": "{}", "known_hosts": ""})):
         res = subprocess.run(["bash", script], input=json.dumps(dict(down, operation="destroy")), capture_output=True,
                              text=True, timeout=60)

@@ -1,0 +1,244 @@
+"""The Rancher server's CA is pinned per cluster manager and verifies every HTTPS call
+(VERDICT r4 "Next round" #2; ``rancher/trust.py``).
+
+The fake Rancher serves HTTPS from its own CA (``FakeRancher(tls=True)``) and can switch to
+another one (``rotate_certificate``: an impostor on the path, or an unannounced rotation).
+"""
+
+import hashlib
+import json
+import os
+import re
+import subprocess
+import tempfile
+
+import pytest
+
+from triton_kubernetes_amd import versions
+from triton_kubernetes_amd import workflows as wf
+from triton_kubernetes_amd.backend import LocalBackend, MemoryBackend
+from triton_kubernetes_amd.errors import TKError
+from triton_kubernetes_amd.executor.direct import DirectExecutor
+from triton_kubernetes_amd.node.agent import NodeAgent
+from triton_kubernetes_amd.node.labels import synthetic_topology
+from triton_kubernetes_amd.parallel.transport import AgentTransport, RecordingTransport, TransportRouter
+from triton_kubernetes_amd.rancher import bootstrap_secret, trust
+from triton_kubernetes_amd.rancher.client import RancherClient
+from triton_kubernetes_amd.rancher.fake import FakeRancher
+from triton_kubernetes_amd.terraform import catalog
+
+from helpers import make_ctx, output
+
+PW = "tk-admin-pw-0123"
+TOKEN = "ca-pin-token-0123456"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.fixture
+def tls_env(tmp_path):
+    fake = FakeRancher.for_manager("mgr", PW, tls=True).start()
+    ca_file = tmp_path / "rancher-ca.pem"
+    ca_file.write_text(fake.ca_pem)
+    agents = []
+
+    def agent(name, gpus=0):
+        a = NodeAgent(name=name, mode="sim", devices=list(range(gpus)), token=TOKEN, root=tempfile.mkdtemp(),
+                      topology_override=synthetic_topology(gpus) if gpus else None,
+                      burnin_override=lambda d, l: {"ok": True})
+        agents.append(a)
+        return "agent+" + a.serve()
+
+    yield fake, str(ca_file), agent, LocalBackend(str(tmp_path / "state"))
+    for a in agents:
+        a.stop()
+    fake.stop()
+
+
+def _cluster(base, name, cp, gpu):
+    return dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name=name,
+                k8s_version=versions.DEFAULT_K8S_VERSION, k8s_network_provider="canal", nodes=[
+                    {"rancher_host_label": "control", "node_count": 1, "hostname": f"{name}-cp", "ssh_user": "u",
+                     "bastion_host": "", "key_path": "k", "hosts": [cp]},
+                    {"rancher_host_label": "worker", "node_count": 1, "hostname": f"{name}-gpu", "ssh_user": "u",
+                     "bastion_host": "", "key_path": "k", "hosts": [gpu], "gpu": "mi355x", "gpu_count": 8,
+                     "gpu_burnin": "quick"}])
+
+
+def test_direct_executor_pins_the_ca_and_refuses_a_switched_certificate(tls_env):
+    fake, ca_file, agent, backend = tls_env
+    base = {"executor": "direct", "agent_token": TOKEN}
+    wf.new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password=PW,
+                                 host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k",
+                                 rancher_ca_file=ca_file)), backend)
+    pinned = trust.load(backend, "mgr")
+    assert pinned is not None and pinned.pem == trust.normalize(fake.ca_pem) and pinned.source.startswith("file:")
+    assert fake.state.admin_password == PW  # the bootstrap went over verified TLS
+
+    # the pin persists: later commands verify without being told the CA again
+    wf.new_cluster(make_ctx(_cluster(base, "a", agent("cp"), agent("g", gpus=8))), backend)
+    tf = json.loads(backend.read_tfstate("mgr"))
+    checksum = tf["module_outputs"]["cluster_baremetal_a"]["rancher_cluster_ca_checksum"]
+    assert checksum == hashlib.sha256(trust.normalize(fake.ca_pem).encode()).hexdigest()
+    ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_name="a"))
+    wf.get_cluster(ctx, backend)
+
+    # the server now presents a certificate from another CA (an impostor on the path)
+    fake.rotate_certificate()
+    seen = fake.state.requests
+    with pytest.raises(TKError, match=r"does not verify .*against the Rancher CA pinned for this cluster manager"):
+        wf.new_cluster(make_ctx(_cluster(base, "b", agent("cp2"), agent("g2", gpus=8))), backend)
+    with pytest.raises(TKError, match="rancher_ca_file"):
+        wf.destroy.delete_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_name="a",
+                                                rancher_cleanup=True, node_cleanup=False)), backend)
+    assert fake.state.requests == seen  # not one request reached it: no API key was sent
+
+    # an operator who knows the CA was rotated on purpose re-pins it
+    new_ca = tempfile.NamedTemporaryFile("w", suffix=".pem", delete=False)
+    new_ca.write(fake.ca_pem)
+    new_ca.close()
+    wf.new_cluster(make_ctx(dict(_cluster(base, "c", agent("cp3"), agent("g3", gpus=8)),
+                                 rancher_ca_file=new_ca.name)), backend)
+    assert trust.load(backend, "mgr").pem == trust.normalize(fake.ca_pem)
+
+
+def test_adopted_https_server_without_a_ca_uses_the_system_store(tls_env):
+    fake, _, _, backend = tls_env
+    with pytest.raises(TKError, match=r"against the system trust store.*rancher_ca_file"):
+        wf.new_manager(make_ctx({"executor": "direct", "manager_cloud_provider": "baremetal", "name": "mgr",
+                                 "rancher_admin_password": PW, "host": "rancher+" + fake.url, "ssh_user": "ubuntu",
+                                 "bastion_host": "", "key_path": "k"}), backend)
+
+
+def test_ssh_managed_manager_is_pinned_from_its_host():
+    """A manager installed over SSH (here: one created before pinning existed) is pinned from
+    the file its install saved on the host, read over the pinned SSH session."""
+    from triton_kubernetes_amd.state import State
+
+    pem = "-----BEGIN CERTIFICATE-----\nMIIHOSTREADCA\n-----END CERTIFICATE-----"
+
+    class Host(RecordingTransport):
+        def run_script(self, host, script, timeout=3600):
+            super().run_script(host, script, timeout)
+            return pem + "\n" if "rancher_cacerts.pem" in script else ""
+
+    be = MemoryBackend()
+    st = State("mgr")
+    st.set_manager({"source": catalog.module_source(catalog.PACKAGE_ROOT, "terraform/modules/bare-metal-rancher", "x"),
+                    "name": "mgr", "host": "10.0.0.10", "ssh_user": "ubuntu", "key_path": "k",
+                    "rancher_admin_password": PW})
+    host = Host()
+    ex = DirectExecutor(transport=host)
+    tf = ex._load_tfstate(be, "mgr")
+    tf["module_state"]["cluster-manager"] = {"hash": "x", "status": "ok"}
+    ex._save_tfstate(be, "mgr", tf)
+    ex._load_trust(st, be)
+    got = trust.load(be, "mgr")
+    assert got.pem == pem + "\n" and got.source == "ssh:10.0.0.10"
+    assert host.scripts == ["cat ~/rancher_cacerts.pem\n"]
+
+
+def _ensure_cluster(q):
+    script = os.path.join(catalog.MODULES_DIR, "bare-metal-rancher-k8s", "files", "ensure_cluster.sh")
+    return subprocess.run(["bash", script], input=json.dumps(q), capture_output=True, text=True, timeout=60)
+
+
+def test_terraform_ensure_cluster_verifies_against_the_pinned_ca(tmp_path):
+    with FakeRancher(bootstrap_password="b00tstrap-only", tls=True) as fake:
+        pem = trust.normalize(fake.ca_pem)
+        outs = RancherClient(fake.url, trust=trust.RancherTrust(pem, "t")).bootstrap("n3w-passw0rd-123", fake.url,
+                                                                                  "b00tstrap-only", timeout=10)
+        q = {"name": "dev", "version": versions.DEFAULT_K8S_VERSION, "network": "canal", "distribution": "rke2",
+             "api_url": fake.url, "access_key": outs["rancher_access_key"], "secret_key": outs["rancher_secret_key"],
+             "ca_pem": pem, "operation": "apply"}
+        ok = _ensure_cluster(q)
+        assert ok.returncode == 0, ok.stderr
+        assert json.loads(ok.stdout)["ca_checksum"] == hashlib.sha256(pem.encode()).hexdigest()
+        fake.rotate_certificate()
+        refused = _ensure_cluster(q)
+        assert refused.returncode != 0
+        assert "does not verify against the CA pinned for this cluster manager" in refused.stderr
+        assert "refusing to send the API key" in refused.stderr
+
+
+def test_terraform_render_carries_the_pin_and_the_bootstrap_secret(tmp_path):
+    from triton_kubernetes_amd.executor.terraform import render
+    from triton_kubernetes_amd.models import baremetal
+
+    be = LocalBackend(str(tmp_path / "state"))
+    st = be.state("mgr")
+    baremetal.new_manager(make_ctx({"manager_cloud_provider": "baremetal", "name": "mgr",
+                                    "rancher_admin_password": PW, "host": "10.0.0.10", "ssh_user": "u",
+                                    "bastion_host": "", "key_path": "k"}), st, "mgr")
+    name = baremetal.new_cluster(make_ctx({"name": "dev", "k8s_version": versions.DEFAULT_K8S_VERSION,
+                                           "k8s_network_provider": "canal", "gpu_addons": True}), None, st)
+    pem = "-----BEGIN CERTIFICATE-----\nMIIPINNED\n-----END CERTIFICATE-----\n"
+    boot = bootstrap_secret.ensure(be, "mgr")
+    doc = json.loads(render(st, (1, 5, 7), be, "", pem, boot).body)
+    assert doc["variable"]["tk_rancher_ca"]["default"] == pem
+    assert doc["module"][st.clusters()[name]]["tk_rancher_ca"] == "${var.tk_rancher_ca}"
+    assert doc["module"][f"addons_baremetal_{name}"]["tk_rancher_ca"] == "${var.tk_rancher_ca}"
+    assert doc["module"]["cluster-manager"]["rancher_bootstrap_password"] == "${var.tk_rancher_bootstrap_password}"
+    assert doc["variable"]["tk_rancher_bootstrap_password"] == {"type": "string", "default": boot, "sensitive": True}
+    # nothing derived from the admin password anywhere in the rendered document
+    assert versions.bootstrap_password("mgr", PW) not in json.dumps(doc)
+
+
+# Where the framework still talks TLS without verifying a certificate chain, and why.  Any
+# other CERT_NONE / verify_tls=False / curl -k / --insecure is a regression.
+ALLOWED_UNVERIFIED = {
+    # the node's join: /cacerts fetched, then accepted only if its sha256 is the cluster's
+    # pinned --ca-checksum (what Rancher's own system-agent-install.sh does); and the
+    # sim-mode registration of the in-process fake
+    "triton_kubernetes_amd/node/agent_steps.py": {"verify_tls=False": 2},
+    # the same join rendered for SSH / Terraform hosts (checksum-checked)
+    "triton_kubernetes_amd/node/plan.py": {"curl -fsSLk": 1},
+    "triton_kubernetes_amd/terraform/scripts.py": {"curl -fsSLk": 1, "curl -ksf": 7, "curl -ks ": 1},
+    # on the manager host itself, against its own loopback https://127.0.0.1
+    "triton_kubernetes_amd/node/manager.py": {"curl -ksf": 8},
+    # the HTTP client's switch itself
+    "triton_kubernetes_amd/cloud/http.py": {"ssl.CERT_NONE": 1},
+}
+PATTERNS = ("verify_tls=False", "ssl.CERT_NONE", "curl -fsSLk", "curl -ksf", "curl -ks ", "curl --insecure ")
+
+
+def test_no_unverified_tls_outside_the_allowed_places():
+    found = {}
+    pkg = os.path.join(ROOT, "triton_kubernetes_amd")
+    for dirpath, _, files in os.walk(pkg):
+        if "/terraform/modules" in dirpath or "/rancher/fake" in dirpath or "__pycache__" in dirpath:
+            continue  # modules are generated from terraform/scripts.py; the fake is a test double
+        for fn in files:
+            if not fn.endswith(".py"):
+                continue
+            path = os.path.join(dirpath, fn)
+            text = open(path, encoding="utf-8").read()
+            rel = os.path.relpath(path, ROOT)
+            for pat in PATTERNS:
+                n = len(re.findall(re.escape(pat), text))
+                if n:
+                    found.setdefault(rel, {})[pat] = n
+    extra = {f: p for f, p in found.items() if f not in ALLOWED_UNVERIFIED}
+    assert not extra, extra
+    for f, pats in found.items():
+        for pat, n in pats.items():
+            assert n <= ALLOWED_UNVERIFIED[f].get(pat, 0), (f, pat, n)
+    # the loopback ones really are loopback
+    for f in ("triton_kubernetes_amd/node/manager.py",):
+        for line in open(os.path.join(ROOT, f)).read().splitlines():
+            if "curl -ksf" in line:  # R=https://127.0.0.1; ``post`` is used with "$R/..."
+                assert "127.0.0.1" in line or "$R/" in line or line.strip().startswith("post = "), line
+
+
+def test_rerun_after_the_password_change_still_logs_in():
+    """The random first-login password is used once; a re-run (the bootstrap interrupted
+    after the change, or a re-apply) logs in with the admin password instead."""
+    be = MemoryBackend()
+    boot = bootstrap_secret.ensure(be, "mgr")
+    with FakeRancher(bootstrap_password=boot, tls=True) as fake:
+        t = trust.RancherTrust(trust.normalize(fake.ca_pem), "t")
+        first = RancherClient(fake.url, trust=t).bootstrap(PW, fake.url, boot, timeout=10)
+        assert fake.state.admin_password == PW
+        again = RancherClient(fake.url, trust=t).bootstrap(PW, fake.url, bootstrap_secret.ensure(be, "mgr"),
+                                                           timeout=10)
+        assert first["rancher_access_key"] and again["rancher_access_key"]
+        assert bootstrap_secret.ensure(be, "mgr") == boot

@@ -142,20 +142,37 @@ def test_same_minor_release_substituted_from_the_server_list():
             client.create_v2_cluster("gone", versions.DEFAULT_K8S_VERSION, "canal")
 
 
-def test_bootstrap_password_same_in_python_and_terraform():
-    want = hashlib.sha256(b"tk-bootstrap:mgr:tk-admin-pw-0123").hexdigest()[:32]
-    assert versions.bootstrap_password("mgr", "tk-admin-pw-0123") == want
+def test_bootstrap_password_is_random_and_never_on_a_command_line(tmp_path):
+    """the first-login password is random, kept in the state backend (0600),
+    handed to the server in a 0600 env file removed after start, and no function of the
+    admin password appears in any host command line, container env or rendered script."""
+    import stat
+
+    from triton_kubernetes_amd.backend import LocalBackend
+    from triton_kubernetes_amd.rancher import bootstrap_secret
+
+    be = LocalBackend(str(tmp_path / "state"))
+    pw = bootstrap_secret.ensure(be, "mgr")
+    assert len(pw) >= 32 and bootstrap_secret.ensure(be, "mgr") == pw  # kept, not regenerated
+    blob = tmp_path / "state" / "mgr" / bootstrap_secret.BLOB
+    assert stat.S_IMODE(os.stat(blob).st_mode) == 0o600
+    assert pw != versions.bootstrap_password("mgr", "tk-admin-pw-0123")
+    admin = "tk-admin-pw-0123"
+    derived = versions.bootstrap_password("mgr", admin)
+    script = node_manager.manager_install_script({"rancher_admin_password": admin}, pw)
+    assert "--env-file" in script and "-e CATTLE_BOOTSTRAP_PASSWORD" not in script
+    assert admin not in script and derived not in script
+    run = next(ln for ln in script.splitlines() if "docker run" in ln)
+    assert pw not in run  # the command line names the file, not the value
+    assert "| sudo sh" not in script  # downloaded, then run
     for mod in ("bare-metal-rancher", "triton-rancher", "aws-rancher", "gcp-rancher", "azure-rancher"):
         main = open(os.path.join(MODULES_DIR, mod, "main.tf"), encoding="utf-8").read()
-        assert 'substr(sha256("tk-bootstrap:${var.name}:${var.rancher_admin_password}"), 0, 32)' in main
-        assert "bootstrap_password   = local.bootstrap_password" in main
+        assert "sha256(" not in main and "bootstrap_password = var.rancher_bootstrap_password" in main
         server = open(os.path.join(MODULES_DIR, mod, "files", "install_rancher_server.sh.tftpl")).read()
-        assert "-e CATTLE_BOOTSTRAP_PASSWORD='${bootstrap_password}'" in server
+        assert "--env-file" in server and "-e CATTLE_BOOTSTRAP_PASSWORD" not in server
         setup = open(os.path.join(MODULES_DIR, mod, "files", "setup_rancher.sh.tftpl")).read()
-        assert '"password":"admin"' not in setup and "login_as '${bootstrap_password}'" in setup
-    script = node_manager.manager_install_script({"rancher_admin_password": "x" * 12}, want)
-    assert f"-e CATTLE_BOOTSTRAP_PASSWORD={want}" in script
-    assert "| sudo sh" not in script  # downloaded, then run
+        assert "rancher_admin_password" not in setup  # set over SSH stdin by read_api_key.sh
+        assert '"password":"admin"' not in setup and "--data-binary @-" in setup
 
 
 def test_docker_install_checksum_is_enforced_when_given():

@@ -2,8 +2,9 @@
 
 All cloud/Rancher REST traffic goes through :class:`HTTPClient`: persistent
 per-host connections (``http.client`` keep-alive, one connection per thread),
-JSON helpers, optional TLS verification (Rancher uses self-signed certs: the
-reference calls it with ``curl --insecure``), and a request hook for signing
+JSON helpers, TLS verification (against the system store or a given context, e.g. a
+Rancher server's pinned CA, ``rancher/trust.py``; a failure is :class:`TLSVerificationError`,
+never retried), and a request hook for signing
 (Triton/Manta HTTP signatures, AWS SigV4, bearer tokens).
 """
 
@@ -18,6 +19,11 @@ from dataclasses import dataclass, field
 from typing import Any, Callable, Dict, Optional, Tuple
 
 from ..errors import TKError
+
+
+class TLSVerificationError(TKError):
+    """The server's certificate did not verify against the client's trust roots: never
+    retried, and no request (no credential) was sent."""
 
 
 class HTTPError(TKError):
@@ -63,6 +69,8 @@ class HTTPClient:
     retry_backoff: float = 0.2
     # verify against this context's trust roots (e.g. a node-agent CA) instead of the system's
     ssl_context: Optional[ssl.SSLContext] = None
+    # appended to a certificate verification failure: what the server was checked against
+    tls_hint: str = ""
 
     def __post_init__(self):
         self._local = threading.local()
@@ -144,6 +152,12 @@ class HTTPClient:
                 if resp.getheader("connection", "").lower() == "close":
                     self._drop(parts.scheme, parts.netloc)
                 break
+            except ssl.SSLCertVerificationError as exc:
+                self._drop(parts.scheme, parts.netloc)
+                raise TLSVerificationError(
+                    f"{method} {url}: TLS: the server's certificate does not verify ({exc})"
+                    + (f" against {self.tls_hint}" if self.tls_hint else "")
+                    + "; refusing to send the request") from exc
             except (ConnectionError, http.client.HTTPException, OSError) as exc:
                 self._drop(parts.scheme, parts.netloc)
                 if attempt >= self.retries:

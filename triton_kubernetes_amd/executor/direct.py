@@ -43,11 +43,11 @@ from ..errors import ExecutorError
 from ..node.plan import TOOLS_DIR, build_host_plan
 from ..parallel.transport import HostRef, Transport, TransportRouter
 from ..rancher.client import RancherClient, wait_until
-from ..state import State
+from ..state import MANAGER_KEY, State
 from ..terraform.catalog import ModuleInfo, check_sources, module_from_source
 from ..terraform import hcl
 from ..utils.trace import span
-from ..versions import DEFAULT_DISTRIBUTION, bootstrap_password, default_version
+from ..versions import DEFAULT_DISTRIBUTION, default_version
 from .base import Executor, outputs_from_tfstate
 from .tfstate import CODEC
 
@@ -145,10 +145,16 @@ class DirectExecutor(Executor):
                  rancher_factory: Optional[Callable[..., RancherClient]] = None, rancher_bootstrap: str = "operator",
                  node_timeout: float = 3600.0, cluster_wait: float = 1800.0, upload_tools: bool = True,
                  node_cleanup: bool = True, on_event: Optional[Callable[[str, Dict[str, Any]], None]] = None,
-                 host_retries: int = 0, retry_backoff: float = 2.0):
+                 host_retries: int = 0, retry_backoff: float = 2.0, ca_file: str = ""):
         self.transport = transport or TransportRouter()
         self.parallelism = max(1, parallelism)
-        self.rancher_factory = rancher_factory or (lambda url, ak="", sk="": RancherClient(url, ak, sk))
+        # the manager's pinned Rancher CA (rancher/trust.py), loaded per apply; every client
+        # this executor makes verifies the server against it
+        self.trust: Optional[Any] = None
+        self.ca_file = ca_file
+        self._trust_store: Optional[Tuple[Backend, str]] = None
+        self.rancher_factory = rancher_factory or (
+            lambda url, ak="", sk="": RancherClient(url, ak, sk, trust=self.trust))
         self.rancher_bootstrap = rancher_bootstrap
         self.node_timeout = node_timeout
         self.cluster_wait = cluster_wait
@@ -243,9 +249,48 @@ class DirectExecutor(Executor):
     def apply_report(self, state: State, backend: Backend) -> ApplyReport:
         keys = self._bind_host_keys(backend, state.name)
         try:
+            self._load_trust(state, backend)
             return self._apply_report(state, backend)
         finally:
             keys.save()  # first-contact keys pinned by this run
+
+    # --- the Rancher server's CA (rancher/trust.py) ----------------------------------------------
+    def _load_trust(self, state: State, backend: Backend) -> None:
+        """The manager's pinned CA for this run's clients.  ``rancher_ca_file`` re-pins (an
+        operator's deliberate act).  A manager created before pinning existed, installed
+        over SSH and already applied, is pinned now from its host (host-key-pinned SSH)."""
+        from ..rancher import trust as rtrust
+
+        self._trust_store = (backend, state.name)
+        self.trust = rtrust.load(backend, state.name)
+        if self.ca_file:
+            self._pin(rtrust.from_file(self.ca_file))
+            return
+        mgr = state.module(MANAGER_KEY) or {}
+        host = str(mgr.get("host", ""))
+        applied = (self._load_tfstate(backend, state.name)["module_state"].get(MANAGER_KEY) or {}).get("status") == "ok"
+        if self.trust is None and applied and host and not host.startswith("rancher+"):
+            self._pin(self._read_host_ca(mgr))
+
+    def _pin(self, trust: Any) -> None:
+        from ..rancher import trust as rtrust
+
+        self.trust = trust
+        if self._trust_store is not None:
+            rtrust.save(self._trust_store[0], self._trust_store[1], trust)
+
+    def _read_host_ca(self, cfg: Dict[str, Any]) -> Any:
+        """The CA bundle the manager host's install saved from ``https://127.0.0.1/cacerts``,
+        read over the host-key-pinned SSH session."""
+        from ..rancher.trust import HOST_CA_FILE, RancherTrust, normalize
+
+        host = str(cfg.get("host", ""))
+        ref = HostRef(host, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "~/.ssh/id_rsa",
+                      cfg.get("bastion_host") or "")
+        pem = self.transport.run_script(ref, f"cat {HOST_CA_FILE}\n", timeout=120)
+        if pem.strip() and "BEGIN CERTIFICATE" not in pem:
+            raise ExecutorError(f"{host}: {HOST_CA_FILE} holds no PEM certificate")
+        return RancherTrust(normalize(pem), f"ssh:{host}")
 
     def _apply_report(self, state: State, backend: Backend) -> ApplyReport:
         t0 = time.time()
@@ -406,17 +451,40 @@ class DirectExecutor(Executor):
         password = cfg.get("rancher_admin_password", "")
         # the server's first-login password (CATTLE_BOOTSTRAP_PASSWORD): given for an adopted
         # server, else the value every install path of this framework starts the server with
-        initial = cfg.get("rancher_bootstrap_password") or bootstrap_password(str(cfg.get("name", "")), password)
+        from ..rancher import bootstrap_secret
+        from ..rancher.trust import RancherTrust, normalize
+
         if host.startswith("rancher+"):
+            # an adopted server: its bootstrap password is given, or one an earlier version
+            # of this framework started it with (a login attempt only)
+            initial = cfg.get("rancher_bootstrap_password") or bootstrap_secret.legacy_password(
+                str(cfg.get("name", "")), password)
             url = host[len("rancher+"):]
+            if self.trust is None:
+                if url.startswith("https://"):
+                    # adopted over HTTPS without rancher_ca_file: a publicly trusted
+                    # certificate, verified by the system store (a private CA must be given)
+                    self._pin(RancherTrust("", "public"))
+                else:  # plain http (the in-process fake; loopback development): no TLS to pin
+                    self._pin(RancherTrust(normalize(self.rancher_factory(url).http.request(
+                        "GET", "/cacerts").body.decode()), f"server:{url}"))
             client = self.rancher_factory(url)
             return client.bootstrap(password, url, initial, timeout=self.cluster_wait)
+        # a server this framework starts: a random first-login password kept in the state
+        # backend (rancher/bootstrap_secret.py), never derived from the admin password
+        initial = cfg.get("rancher_bootstrap_password") or (
+            bootstrap_secret.ensure(*self._trust_store) if self._trust_store is not None else "")
+        if not initial:
+            raise ExecutorError("no state backend to keep the Rancher bootstrap password in")
         ref = HostRef(host, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "~/.ssh/id_rsa",
                       cfg.get("bastion_host") or "")
         from ..node.manager import manager_install_script, manager_setup_script
 
         with span("manager.install", host=host):
             self.transport.run_script(ref, manager_install_script(cfg, initial), timeout=self.node_timeout)
+        if not self.ca_file:
+            # the CA the server serves on the host itself, over the pinned SSH session
+            self._pin(self._read_host_ca(cfg))
         url = f"https://{host}"
         if self.rancher_bootstrap == "remote":
             with span("manager.setup_remote", host=host):

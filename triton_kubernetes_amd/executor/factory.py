@@ -13,6 +13,10 @@
                             agent and RKE2/RKE1, node/cleanup.py; default true); a host
                             module's own ``node_cleanup`` can turn it off for that host
 ``host_retries``            re-run a failed host bootstrap this many times (default 0)
+``rancher_ca_file``         PEM CA bundle of the Rancher server: pinned for the manager (an
+                            adopted server, a custom CA, a deliberate re-pin after a CA
+                            rotation); default: read on the manager host at create manager
+                            (rancher/trust.py)
 ``host_retry_backoff``      first retry delay in seconds, doubling per attempt (default 2)
 ==========================  ================================================================
 
@@ -43,7 +47,7 @@ def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
         from .terraform import TerraformExecutor
 
         par = s.get_int("terraform_parallelism") if s.is_set("terraform_parallelism") else None
-        return TerraformExecutor(binary=tf_bin, parallelism=par)
+        return TerraformExecutor(binary=tf_bin, parallelism=par, ca_file=s.get_string("rancher_ca_file") or "")
     if kind == "direct":
         from ..parallel.transport import SSHTransport, TransportRouter
         from .direct import DirectExecutor
@@ -58,5 +62,6 @@ def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
                               node_cleanup=s.get_bool("node_cleanup") if s.is_set("node_cleanup") else True,
                               host_retries=s.get_int("host_retries") if s.is_set("host_retries") else 0,
                               retry_backoff=float(s.get_string("host_retry_backoff") or 2.0),
-                              rancher_factory=ctx.extras.get("rancher_factory"))
+                              rancher_factory=ctx.extras.get("rancher_factory"),
+                              ca_file=s.get_string("rancher_ca_file") or "")
     raise ValueError(f"unknown executor '{kind}' (terraform | direct | auto)")

@@ -51,7 +51,7 @@ from typing import Dict, Iterator, List, Optional, Sequence, Tuple
 
 from ..backend.base import Backend
 from ..errors import ExecutorError
-from ..state import State
+from ..state import MANAGER_KEY, State
 from ..terraform import constraints
 from ..terraform.catalog import (check_sources, declared_variables, is_packaged_source, local_module_dir,
                                  module_from_source, outputs_for_source, resolve_source, sensitive_outputs)
@@ -93,6 +93,13 @@ OPERATION_VAR = "tk_operation"
 KNOWN_HOSTS_VAR = "tk_known_hosts"
 # module output of the keys those reads pinned (merged back into the store after an apply)
 KNOWN_HOSTS_OUTPUT = "tk_ssh_known_hosts"
+# the manager's pinned Rancher CA for the modules' Rancher calls (rancher/trust.py) ...
+RANCHER_CA_VAR = "tk_rancher_ca"
+# ... the manager module output it is first pinned from (read on the manager host)
+RANCHER_CA_OUTPUT = "tk_rancher_ca_certs"
+# the random first-login password (rancher/bootstrap_secret.py), a sensitive root variable
+# rendered into the manager modules' rancher_bootstrap_password
+BOOTSTRAP_VAR = "tk_rancher_bootstrap_password"
 
 
 def _backend_kind(doc: Dict) -> str:
@@ -134,7 +141,7 @@ def resolve_sources(doc: Dict) -> Dict:
 
 
 def render(state: State, version: Tuple[int, int, int], backend: Optional[Backend] = None,
-           known_hosts: str = "") -> Rendered:
+           known_hosts: str = "", rancher_ca: str = "", bootstrap_password: str = "") -> Rendered:
     """The document Terraform sees (see module docstring).
 
     With ``backend`` the backend block is this operator's (``state_terraform_config``),
@@ -142,7 +149,10 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
     path of whoever wrote it (``key_material``, reference ``backend/manta/backend.go:199``).
     ``known_hosts``: the manager's pinned SSH host keys (``parallel/hostkeys.py``), for the
     modules' SSH reads (root variable) and their provisioner connections (``host_key``,
-    ``bastion_host_key`` of each pinned host)."""
+    ``bastion_host_key`` of each pinned host).  ``rancher_ca``: its pinned Rancher CA
+    (``tk_rancher_ca`` of the cluster and add-on modules).  ``bootstrap_password``: the
+    random first-login password (``rancher_bootstrap_password`` of a manager module that
+    does not set one; a sensitive root variable)."""
     doc = resolve_sources(state.doc)
     kind = _backend_kind(doc)
     if backend is not None and kind:
@@ -160,16 +170,23 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
         for mod in (doc.get("module") or {}).values():
             local = local_module_dir(str(mod.get("source", "")))
             declared = declared_variables(local) if local else frozenset()
-            for var, default in ((OPERATION_VAR, "apply"), (KNOWN_HOSTS_VAR, known_hosts)):
+            for var, default in ((OPERATION_VAR, "apply"), (KNOWN_HOSTS_VAR, known_hosts),
+                                 (RANCHER_CA_VAR, rancher_ca)):
                 if var in declared and var not in mod:
                     mod[var] = f"${{var.{var}}}"
                     root_vars[var] = default
+            if bootstrap_password and "rancher_bootstrap_password" in declared and \
+                    not mod.get("rancher_bootstrap_password"):
+                mod["rancher_bootstrap_password"] = f"${{var.{BOOTSTRAP_VAR}}}"
+                root_vars[BOOTSTRAP_VAR] = bootstrap_password
             for var, addr in (("host_key", mod.get("host")), ("bastion_host_key", mod.get("bastion_host"))):
                 pinned = keys_for(known_hosts, str(addr or "")) if known_hosts and addr else []
                 if var in declared and var not in mod and pinned:
                     mod[var] = preferred_key(pinned)  # the type Terraform's Go client negotiates
         for var, default in root_vars.items():
             doc.setdefault("variable", {})[var] = {"type": "string", "default": default}
+            if var == BOOTSTRAP_VAR and version >= (0, 14, 0):
+                doc["variable"][var]["sensitive"] = True
         outputs = doc.setdefault("output", {})
         for key, mod in state.modules().items():
             source = str(mod.get("source", ""))
@@ -200,6 +217,7 @@ class TerraformExecutor(Executor):
         timeout: Optional[float] = None,
         version: Optional[Tuple[int, int, int]] = None,
         keep_workdir: bool = False,
+        ca_file: str = "",
     ):
         self.binary = binary
         self.parallelism = parallelism
@@ -210,6 +228,9 @@ class TerraformExecutor(Executor):
         self.last_workdir: Optional[str] = None
         self.last_rendered: Optional[Rendered] = None
         self.host_keys: Optional[HostKeys] = None
+        # the manager's pinned Rancher CA (rancher/trust.py); ca_file re-pins
+        self.trust = None
+        self.ca_file = ca_file
 
     # --- helpers -------------------------------------------------------------------------
     def version(self) -> Tuple[int, int, int]:
@@ -232,7 +253,21 @@ class TerraformExecutor(Executor):
         version = self.version()
         check_module_versions(state, version)
         keys = self.host_keys = HostKeys(backend, state.name) if backend is not None else None
-        rendered = render(state, version, backend, keys.text() if keys is not None else "")
+        ca, boot = "", ""
+        if backend is not None:
+            from ..rancher import bootstrap_secret, trust as rtrust
+
+            self.trust = rtrust.load(backend, state.name)
+            if self.ca_file:
+                self.trust = rtrust.from_file(self.ca_file)
+                rtrust.save(backend, state.name, self.trust)
+            ca = self.trust.pem if self.trust is not None else ""
+            src = str((state.module(MANAGER_KEY) or {}).get("source", ""))
+            local = local_module_dir(resolve_source(src, MANAGER_KEY) if is_packaged_source(src) else src) \
+                if src else None
+            if local and "rancher_bootstrap_password" in declared_variables(local):
+                boot = bootstrap_secret.ensure(backend, state.name)
+        rendered = render(state, version, backend, keys.text() if keys is not None else "", ca, boot)
         self.last_rendered = rendered
         if rendered.managed_state and backend is None:
             raise ExecutorError(f"the {rendered.backend_kind} state backend needs the CLI to carry terraform.tfstate")
@@ -279,21 +314,30 @@ class TerraformExecutor(Executor):
             if self.parallelism:
                 args.append(f"-parallelism={self.parallelism}")
             self._run(wd, *args)
-            self._pin_learned_keys(state, wd)
+            self._pin_learned_keys(state, wd, backend)
 
-    def _pin_learned_keys(self, state: State, wd: str) -> None:
+    def _pin_learned_keys(self, state: State, wd: str, backend: Optional[Backend] = None) -> None:
         """Merge the SSH host keys the modules' reads pinned on first contact (their
-        ``tk_ssh_known_hosts`` outputs) into the manager's store."""
+        ``tk_ssh_known_hosts`` outputs) into the manager's store, and pin the Rancher CA the
+        manager module read on its host (``rancher_ca_certs``) when none is pinned yet."""
         if self.host_keys is None or self.version() < (0, 12, 0):
             return
         if not any(KNOWN_HOSTS_OUTPUT in outputs_for_source(str(m.get("source", "")))
                    for m in state.modules().values()):
             return
         res = capture_command(self.binary, "output", "-json", working_dir=wd, env=self.env or None)
-        for name, out in (json.loads(res.stdout or "{}") or {}).items():
+        outs = json.loads(res.stdout or "{}") or {}
+        for name, out in outs.items():
             if name.endswith("__" + KNOWN_HOSTS_OUTPUT) and isinstance(out, dict) and out.get("value"):
                 self.host_keys.add(str(out["value"]))
         self.host_keys.save()
+        ca = outs.get(f"{MANAGER_KEY}__{RANCHER_CA_OUTPUT}")
+        if backend is not None and self.trust is None and isinstance(ca, dict) and ca.get("value") is not None:
+            from ..rancher import trust as rtrust
+
+            mgr = state.module(MANAGER_KEY) or {}
+            self.trust = rtrust.RancherTrust(rtrust.normalize(str(ca["value"])), f"ssh:{mgr.get('host', '')}")
+            rtrust.save(backend, state.name, self.trust)
 
     def destroy_flags(self) -> List[str]:
         return ["-auto-approve"] if self.version() >= (0, 15, 0) else ["-force"]

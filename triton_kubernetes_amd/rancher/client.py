@@ -29,7 +29,7 @@ import urllib.parse
 from dataclasses import dataclass
 from typing import Any, Callable, Dict, List, Optional
 
-from ..cloud.http import HTTPClient, HTTPError
+from ..cloud.http import HTTPClient, HTTPError, TLSVerificationError
 from ..errors import TKError
 from ..versions import FLEET_NAMESPACE, default_version, resolve_against, resolve_distribution
 
@@ -68,6 +68,8 @@ def wait_until(fn: Callable[[], Any], timeout: float, what: str, first: float = 
             value = fn()
             if value:
                 return value
+        except TLSVerificationError:
+            raise  # not a server that is still starting: another certificate (never retried)
         except (TKError, OSError) as exc:
             last_exc = exc
         if time.monotonic() >= deadline:
@@ -78,14 +80,24 @@ def wait_until(fn: Callable[[], Any], timeout: float, what: str, first: float = 
 
 
 class RancherClient:
-    def __init__(self, url: str, access_key: str = "", secret_key: str = "", verify_tls: bool = False,
-                 timeout: float = 30.0):
+    """``trust``: the server's pinned CA (``rancher/trust.py``): HTTPS is verified against
+    it alone, and cluster CA checksums are computed from it.  Without one the system trust
+    store verifies (a publicly trusted certificate, or a manager not pinned yet)."""
+
+    def __init__(self, url: str, access_key: str = "", secret_key: str = "", verify_tls: bool = True,
+                 timeout: float = 30.0, trust: Any = None):
         self.url = url.rstrip("/")
         self.token_timeout = 120.0  # registration token value, filled in asynchronously
         self.access_key = access_key
         self.secret_key = secret_key
         self.last_version_note = ""  # set when resolve_k8s_version substituted a release
-        self.http = HTTPClient(base_url=self.url, verify_tls=verify_tls, timeout=timeout)
+        self.trust = trust
+        tls = self.url.startswith("https://")
+        self.http = HTTPClient(base_url=self.url, verify_tls=verify_tls, timeout=timeout,
+                               ssl_context=trust.context() if trust is not None and tls and verify_tls else None,
+                               tls_hint=(trust.describe() if trust is not None else "the system trust store")
+                               + ". If the server's CA was rotated on purpose, pin the new one with "
+                                 "rancher_ca_file=<PEM bundle>")
         self._apply_auth()
 
     def _apply_auth(self) -> None:
@@ -100,6 +112,8 @@ class RancherClient:
         try:
             self.http.request("GET", "/ping", ok=(200,))
             return True
+        except TLSVerificationError:
+            raise
         except TKError:
             return False
 
@@ -301,7 +315,10 @@ class RancherClient:
         token = self.registration_token(cluster_id, create=not existed)
         if not token:
             raise TKError("Unable to create cluster registration token!")
-        return ClusterInfo(cluster_id, token, ca_checksum(self.cacerts()), existed)
+        # the checksum nodes pin: of the bundle pinned at create manager, not of what the
+        # server says now (over a channel that bundle verified, when there is one)
+        checksum = self.trust.checksum if self.trust is not None else ca_checksum(self.cacerts())
+        return ClusterInfo(cluster_id, token, checksum, existed)
 
     # --- status -------------------------------------------------------------------------------
     def cluster(self, cluster_id: str) -> Dict[str, Any]:

@@ -24,7 +24,8 @@ register:
   release; the cluster reads ``upgrading`` for ``upgrade_seconds`` and the kubelets then
   report the new release.
 
-Everything is in memory and thread-safe; it serves plain HTTP on 127.0.0.1.
+Everything is in memory and thread-safe; it serves plain HTTP on 127.0.0.1, or HTTPS with
+its own CA (``tls=True``; ``rotate_certificate`` switches CA, for the pinning tests).
 """
 
 import base64
@@ -92,7 +93,7 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
                  bootstrap_password: Optional[str] = None, host: str = "127.0.0.1", port: int = 0,
                  k8s_versions: Optional[Sequence[str]] = None, async_registration_tokens: bool = True,
                  default_pod_security: str = "privileged", rke2_versions: Optional[Sequence[str]] = None,
-                 device_plugin_seconds: float = 0.0):
+                 device_plugin_seconds: float = 0.0, tls: bool = False):
         if default_pod_security not in PSA_LEVELS:
             raise ValueError(f"default_pod_security must be one of {', '.join(PSA_LEVELS)}")
         # a server started without CATTLE_BOOTSTRAP_PASSWORD has a random one nobody knows
@@ -108,19 +109,62 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
         # Pod Security level of namespaces without an enforce label (the API server's
         # AdmissionConfiguration default; Kubernetes' own default is privileged)
         self.default_pod_security = default_pod_security
+        # tls: HTTPS with a certificate for 127.0.0.1 from the server's own CA, which
+        # /cacerts and the cacerts setting serve (what a Rancher install with its generated
+        # CA does); rotate_certificate() switches to another CA (an impostor, or a rotation)
+        self._tls_ctx = None
+        if tls:
+            self._tls_ctx = self._new_certificate()
         self._server = HTTPServer((host, port), self._handler())
         self._server.daemon_threads = True
+        if self._tls_ctx is not None:
+            self._server.socket = self._tls_ctx.wrap_socket(self._server.socket, server_side=True,
+                                                            do_handshake_on_connect=False)
         self._thread: Optional[threading.Thread] = None
+
+    def _new_certificate(self, ctx: Any = None) -> Any:
+        from ...k8s.tls import issue, make_ca
+
+        ca = make_ca(f"fake-rancher-ca-{secrets.token_hex(3)}")
+        cert = issue(ca, "127.0.0.1", ["127.0.0.1", "localhost"])
+        if ctx is None:
+            from ...node.security import server_context
+
+            ctx = server_context(cert.cert_pem, cert.key_pem)
+        else:  # later handshakes of the same listening socket present the new certificate
+            import os
+            import tempfile
+
+            with tempfile.TemporaryDirectory(prefix="tk-fake-rancher-") as d:
+                cp, kp = os.path.join(d, "c.pem"), os.path.join(d, "k.pem")
+                with open(cp, "w", encoding="utf-8") as fh:
+                    fh.write(cert.cert_pem)
+                with open(kp, "w", encoding="utf-8") as fh:
+                    fh.write(cert.key_pem)
+                ctx.load_cert_chain(cp, kp)
+        with self.state.mu:
+            self.state.settings["cacerts"] = ca.cert_pem
+        self.ca_pem = ca.cert_pem
+        return ctx
+
+    def rotate_certificate(self) -> str:
+        """Serve a certificate from a new CA from now on (and that CA from /cacerts);
+        returns the new CA's PEM."""
+        if self._tls_ctx is None:
+            raise ValueError("this fake serves plain HTTP")
+        self._new_certificate(self._tls_ctx)
+        return self.ca_pem
 
     @classmethod
     def for_manager(cls, name: str, admin_password: str, **kw: Any) -> "FakeRancher":
-        """A server started the way this framework starts one for manager ``name``."""
+        """A server started the way earlier versions of this framework started one for manager
+        ``name`` (the derived first-login password, ``rancher/bootstrap_secret.py``)."""
         return cls(bootstrap_password=bootstrap_password(name, admin_password), **kw)
 
     @property
     def url(self) -> str:
         host, port = self._server.server_address[:2]
-        return f"http://{host}:{port}"
+        return f"{'https' if self._tls_ctx is not None else 'http'}://{host}:{port}"
 
     def start(self) -> "FakeRancher":
         self._thread = threading.Thread(target=self._server.serve_forever, name="fake-rancher", daemon=True)
@@ -228,6 +272,10 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
             protocol_version = "HTTP/1.1"
 
             def setup(self):
+                if fake._tls_ctx is not None:  # the handshake on this connection's own thread
+                    self.request.settimeout(10.0)
+                    self.request.do_handshake()
+                    self.request.settimeout(None)
                 super().setup()
                 # one request/response per segment: no Nagle/delayed-ACK stalls on keep-alive
                 self.request.setsockopt(socket.IPPROTO_TCP, socket.TCP_NODELAY, 1)

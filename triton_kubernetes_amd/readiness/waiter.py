@@ -221,7 +221,11 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
     cl = outputs_from_tfstate(raw, cluster_key)
     if not mgr.get("rancher_url") or not cl.get("rancher_cluster_id"):
         raise TKError("cluster outputs unavailable; cannot wait for readiness")
-    client = RancherClient(mgr["rancher_url"], mgr.get("rancher_access_key", ""), mgr.get("rancher_secret_key", ""))
+    from ..rancher import trust
+
+    # verified against the manager's pinned CA (rancher/trust.py)
+    client = trust.client(backend, state.name, mgr["rancher_url"], mgr.get("rancher_access_key", ""),
+                          mgr.get("rancher_secret_key", ""))
     nodes = state.nodes(cluster_key)
     from ..models.baremetal import addons_key
     from ..state import cluster_key_parts

@@ -24,7 +24,7 @@ from ..errors import ExecutorError
 MODULES_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), "modules")
 
 # tk_* outputs are the CLI's own bookkeeping (pinned SSH host keys), not shown by `get`
-MANAGER_OUTPUTS = ("rancher_url", "rancher_access_key", "rancher_secret_key", "tk_ssh_known_hosts")
+MANAGER_OUTPUTS = ("rancher_url", "rancher_access_key", "rancher_secret_key", "tk_ssh_known_hosts", "tk_rancher_ca_certs")
 CLUSTER_OUTPUTS = ("rancher_cluster_id", "rancher_cluster_registration_token", "rancher_cluster_ca_checksum")
 
 

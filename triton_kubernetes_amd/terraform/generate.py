@@ -287,6 +287,8 @@ CLUSTER_BASE = [
         "rke2 (provisioning.cattle.io/v1 custom cluster, nodes join with rancher-system-agent) or rke1 "
         "(v3 cluster + rancher-agent; reference-era documents)"),
     Var("k8s_version", versions.DEFAULT_K8S_VERSION), Var("k8s_network_provider", "canal"),
+    Var("tk_rancher_ca", "", "PEM CA bundle the Rancher server is verified against (the manager's pinned CA, "
+        "rendered by the CLI; empty: a publicly trusted certificate)"),
     Var("rancher_registry", ""), Var("rancher_registry_username", ""), Var("rancher_registry_password", "", sensitive=True),
     Var("k8s_registry", ""), Var("k8s_registry_username", ""), Var("k8s_registry_password", "", sensitive=True),
 ]
@@ -326,6 +328,8 @@ MANAGER_OUTPUTS = [
     ("rancher_secret_key", "data.external.rancher_api_key.result.secret_key", True),
     # the host keys the key read pinned (parallel/hostkeys.py; not shown by `get manager`)
     ("tk_ssh_known_hosts", "data.external.rancher_api_key.result.known_hosts", False),
+    # the server's CA bundle as read on the manager host (rancher/trust.py pins it)
+    ("tk_rancher_ca_certs", "data.external.rancher_api_key.result.ca_certs", False),
 ]
 CLUSTER_OUTPUTS = [
     ("rancher_cluster_id", 'data.external.cluster.result["cluster_id"]', False),
@@ -338,6 +342,7 @@ OUTPUT_DOCS = {
     "rancher_secret_key": "API secret key created for triton-kubernetes.",
     "rancher_cluster_id": "Rancher id of the cluster (found by name or created).",
     "tk_ssh_known_hosts": "known_hosts lines of the hosts this module's SSH reads contacted (pinned by the CLI).",
+    "tk_rancher_ca_certs": "The Rancher server's CA bundle as its host serves it (pinned by the CLI; empty: public CA).",
     "rancher_cluster_registration_token": "Token nodes present when they register.",
     "rancher_cluster_ca_checksum": "Checksum of the Rancher CA bundle that agents pin.",
 }
@@ -367,10 +372,10 @@ resource "terraform_data" "install_docker" {{
         after = "\n  depends_on       = [terraform_data.install_docker]"
     return docker + f'''
 locals {{
-  # Rancher >= 2.6 first login (CATTLE_BOOTSTRAP_PASSWORD); the same derivation as
-  # triton_kubernetes_amd.versions.bootstrap_password, so every delivery path agrees
-  bootstrap_password = (var.rancher_bootstrap_password != "" ? var.rancher_bootstrap_password :
-    substr(sha256("tk-bootstrap:${{var.name}}:${{var.rancher_admin_password}}"), 0, 32))
+  # Rancher >= 2.6 first login (CATTLE_BOOTSTRAP_PASSWORD): random, kept in the state
+  # backend by the CLI and rendered here (rancher/bootstrap_secret.py) -- no function of
+  # the admin password
+  bootstrap_password = var.rancher_bootstrap_password
 }}
 
 resource "terraform_data" "install_rancher_master" {{
@@ -392,23 +397,25 @@ resource "terraform_data" "setup_rancher_k8s" {{
     inline = [templatefile("${{path.module}}/files/setup_rancher.sh.tftpl", {{
       rancher_host           = "https://127.0.0.1"
       host_registration_url  = "https://${{local.rancher_master_ip}}"
-      rancher_admin_password = var.rancher_admin_password
       bootstrap_password     = local.bootstrap_password
     }})]
   }}
 }}
 
-# The API key written by setup_rancher is read back over SSH.
+# The API key and the CA bundle setup_rancher saved are read back over SSH, which then also
+# carries the admin password (on the host's curl stdin, never a command line or a file).
 data "external" "rancher_api_key" {{
   depends_on = [terraform_data.setup_rancher_k8s]
   program    = ["bash", "${{path.module}}/files/read_api_key.sh"]
   query = {{
-    host         = local.rancher_master_ip
-    ssh_user     = local.ssh_user
-    key_path     = local.key_path
-    bastion_host = local.bastion_host
-    operation    = var.tk_operation
-    known_hosts  = var.tk_known_hosts
+    host               = local.rancher_master_ip
+    ssh_user           = local.ssh_user
+    key_path           = local.key_path
+    bastion_host       = local.bastion_host
+    operation          = var.tk_operation
+    known_hosts        = var.tk_known_hosts
+    admin_password     = var.rancher_admin_password
+    bootstrap_password = local.bootstrap_password
   }}
 }}
 '''
@@ -528,6 +535,7 @@ def _cluster_data() -> str:
       api_url    = var.rancher_api_url
       access_key = var.rancher_access_key
       secret_key = var.rancher_secret_key
+      ca_pem     = var.tk_rancher_ca
     }},
     {{
       registry          = var.k8s_registry
@@ -1458,6 +1466,8 @@ data "external" "gpu_labels" {{
     mods.append(Module("rancher-k8s-mi355x-addons", ["external", "tls"], [
         Var("name", None), Var("rancher_api_url", None), Var("rancher_access_key", None),
         Var("rancher_secret_key", None, sensitive=True), Var("rancher_cluster_id", None),
+        Var("tk_rancher_ca", "", "PEM CA bundle the Rancher server is verified against (the manager's pinned CA, "
+            "rendered by the CLI; empty: a publicly trusted certificate)"),
         Var("device_plugin_image", versions.DEVICE_PLUGIN_IMAGE),
         Var("node_labeller_image", "",
             f"ROCm node labeller image, opt-in (e.g. {versions.NODE_LABELLER_IMAGE}); it writes only keys the "
@@ -1550,6 +1560,7 @@ resource "terraform_data" "apply_addons" {
       RANCHER_URL        = var.rancher_api_url
       RANCHER_ACCESS_KEY = var.rancher_access_key
       RANCHER_SECRET_KEY = var.rancher_secret_key
+      RANCHER_CA         = var.tk_rancher_ca
       CLUSTER_ID         = var.rancher_cluster_id
     }
   }

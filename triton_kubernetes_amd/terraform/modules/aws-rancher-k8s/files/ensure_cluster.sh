@@ -13,8 +13,11 @@ exec python3 -c '
 import base64, hashlib, json, re, ssl, sys, time, urllib.error, urllib.parse, urllib.request
 
 q = json.load(sys.stdin)
-ctx = ssl.create_default_context()
-ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE  # self-signed Rancher certificates
+# TLS verified against the CA pinned for the manager (query key ca_pem = tk_rancher_ca,
+# rendered by the executor; rancher/trust.py); none pinned: a publicly trusted certificate
+pinned = q.get("ca_pem", "").strip()
+pinned = pinned + "\n" if pinned else ""
+ctx = ssl.create_default_context(cadata=pinned) if pinned else ssl.create_default_context()
 auth = "Basic " + base64.b64encode((q["access_key"] + ":" + q["secret_key"]).encode()).decode()
 
 
@@ -23,8 +26,16 @@ def call(method, path, body=None):
                                  data=None if body is None else json.dumps(body).encode(),
                                  headers={"Authorization": auth, "Accept": "application/json",
                                           "Content-Type": "application/json"})
-    with urllib.request.urlopen(req, context=ctx, timeout=60) as resp:
-        return json.load(resp)
+    try:
+        with urllib.request.urlopen(req, context=ctx, timeout=60) as resp:
+            return json.load(resp)
+    except urllib.error.URLError as exc:
+        if isinstance(exc.reason, ssl.SSLCertVerificationError):
+            sys.exit("the Rancher server at %s presented a certificate that does not verify against %s (%s): "
+                     "refusing to send the API key. If its CA was rotated on purpose, pin the new one with "
+                     "rancher_ca_file=<PEM bundle>" % (q["api_url"], "the CA pinned for this cluster manager"
+                                                       if pinned else "the system trust store", exc.reason))
+        raise
 
 
 def get_or_none(path):
@@ -53,7 +64,9 @@ def k8s_version(requested, rke2=False):
 
 
 def ca_checksum():
-    cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
+    # the checksum nodes pin: of the pinned bundle (read on the manager host), not of what the
+    # server says now
+    cacerts = pinned or call("GET", "/v3/settings/cacerts").get("value", "")
     if cacerts and not cacerts.endswith("\n"):
         cacerts += "\n"  # Rancher hashes the bundle with one trailing newline, as /cacerts serves it
     return hashlib.sha256(cacerts.encode()).hexdigest() if cacerts else ""

@@ -68,6 +68,12 @@ variable "k8s_network_provider" {
   }
 }
 
+variable "tk_rancher_ca" {
+  description = "PEM CA bundle the Rancher server is verified against (the manager's pinned CA, rendered by the CLI; empty: a publicly trusted certificate)"
+  type        = string
+  default     = ""
+}
+
 variable "rancher_registry" {
   description = "Private registry serving the Rancher images (empty: Docker Hub)."
   type        = string

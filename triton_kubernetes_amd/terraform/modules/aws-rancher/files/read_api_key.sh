@@ -1,9 +1,14 @@
 #!/bin/bash
-# data "external" program: read the manager's ~/rancher_api_key over SSH.
-# Replaces the reference's matti/outputs/shell registry module.
-# Outside an apply (query key operation = destroy | read, the executor's tk_operation)
-# a manager that cannot be reached yields empty keys instead of an error: destroying
-# what is left of a manager whose host is gone must not depend on that host.
+# data "external" program (operator machine): read the manager's ~/rancher_api_key and the
+# server's CA bundle (~/rancher_cacerts.pem, saved on the host from its own loopback) over
+# the pinned SSH session, then -- on apply -- set the admin password: a curl on the host
+# against its loopback, with the credentials and the request body on curl's stdin (a
+# config, "-K -"), which is this SSH session's stdin.  The admin password is never on a
+# command line, in a file or in a rendered script on the host (rancher/bootstrap_secret.py).
+# Replaces the reference's matti/outputs/shell registry module.  Outside an apply (query
+# key operation = destroy | read, the executor's tk_operation) a manager that cannot be
+# reached yields empty keys instead of an error: destroying what is left of a manager whose
+# host is gone must not depend on that host.
 set -euo pipefail
 eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
 # SSH with the cluster manager's pinned host keys (query key known_hosts, the executor's
@@ -31,10 +36,30 @@ refused() {
   exit 1
 }
 if ! tok=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_api_key' 2>"$err"); then
-  if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": ""}'; exit 0; fi
+  if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": "", "ca_certs": ""}'; exit 0; fi
   refused "read the Rancher API key"
 fi
-printf '%s' "$tok" | KH="$(pinned_for)" python3 -c '
+ca=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_cacerts.pem' 2>"$err") || ca=""
+if [ "${operation:-apply}" = apply ] && [ -n "${admin_password:-}" ] && [ "${admin_password:-}" != "${bootstrap_password:-}" ]; then
+  # curl config on stdin: user (the API token), the JSON body with both passwords
+  cfg=$(printf '%s' "$tok" | TKQ_admin="$admin_password" TKQ_boot="$bootstrap_password" python3 -c '
 import json, os, sys
 t = json.load(sys.stdin)
-print(json.dumps({"access_key": t["name"], "secret_key": t["token"].split(":", 1)[1], "known_hosts": os.environ["KH"]}))'
+q = lambda v: json.dumps(v)  # a curl config string: double-quoted, backslash escapes
+body = json.dumps({"currentPassword": os.environ["TKQ_boot"], "newPassword": os.environ["TKQ_admin"]})
+print("user = " + q(t["token"]))
+print("header = " + q("Content-Type: application/json"))
+print("data = " + q(body))')
+  code=$(printf '%s
+' "$cfg" | ssh "${opts[@]}" "$ssh_user@$host" \
+    'curl -ks -K - -o /dev/null -w "%{http_code}" -X POST "https://127.0.0.1/v3/users?action=changepassword"' 2>"$err") \
+    || refused "set the Rancher admin password"
+  # 422: the current password is no longer the bootstrap one -- set by an earlier run
+  case "$code" in 2??|422|"") ;; *) echo "setting the Rancher admin password on $host: HTTP $code" >&2; exit 1 ;; esac
+fi
+printf '%s' "$tok" | KH="$(pinned_for)" CA="$ca" python3 -c '
+import json, os, sys
+t = json.load(sys.stdin)
+ca = os.environ["CA"].strip()
+print(json.dumps({"access_key": t["name"], "secret_key": t["token"].split(":", 1)[1], "known_hosts": os.environ["KH"],
+                  "ca_certs": ca + "\n" if ca else ""}))'

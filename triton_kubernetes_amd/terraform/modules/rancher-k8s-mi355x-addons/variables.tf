@@ -29,6 +29,12 @@ variable "rancher_cluster_id" {
   type        = string
 }
 
+variable "tk_rancher_ca" {
+  description = "PEM CA bundle the Rancher server is verified against (the manager's pinned CA, rendered by the CLI; empty: a publicly trusted certificate)"
+  type        = string
+  default     = ""
+}
+
 variable "device_plugin_image" {
   description = "Device plugin image."
   type        = string

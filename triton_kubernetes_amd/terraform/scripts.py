@@ -48,37 +48,46 @@ INSTALL_RANCHER_SERVER = r"""#!/bin/bash
 set -euo pipefail
 for i in $(seq 1 600); do command -v docker >/dev/null 2>&1 && break; sleep 1; done
 for i in $(seq 1 600); do sudo docker image inspect '${rancher_server_image}' >/dev/null 2>&1 && break; sudo docker pull '${rancher_server_image}' || sleep 1; done
+[ -n '${bootstrap_password}' ] || { echo 'rancher_bootstrap_password is empty (the CLI passes the random one it keeps in the state backend)' >&2; exit 1; }
 if ! sudo docker ps --format '{{.Image}}' | grep -qx '${rancher_server_image}'; then
-  # Rancher >= 2.6 has no admin/admin: the first login uses this bootstrap password
-  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 \
-    -e CATTLE_BOOTSTRAP_PASSWORD='${bootstrap_password}' '${rancher_server_image}'
+  # Rancher >= 2.6 has no admin/admin: the first login uses this bootstrap password (random,
+  # kept in the state backend: rancher/bootstrap_secret.py), handed over in a 0600 env file
+  # that is removed once the container runs -- never on a command line
+  envf=$(umask 077; mktemp)
+  trap 'rm -f "$envf"' EXIT
+  cat > "$envf" <<'TK_BOOTSTRAP_EOF'
+CATTLE_BOOTSTRAP_PASSWORD=${bootstrap_password}
+TK_BOOTSTRAP_EOF
+  sudo docker run -d --restart=unless-stopped --privileged -p 80:80 -p 443:443 --env-file "$envf" \
+    '${rancher_server_image}'
+  rm -f "$envf"
 fi
 """
 
 SETUP_RANCHER = r"""#!/bin/bash
-# S3: bootstrap the Rancher API on the manager (token -> ~/rancher_api_key).
+# S3 on the manager: log in with the bootstrap password, create the API token
+# (-> ~/rancher_api_key), set server-url, and save the server's CA bundle as served here
+# (https://127.0.0.1: loopback, nothing between) to ~/rancher_cacerts.pem.  The admin
+# password is set from the operator side (read_api_key.sh), over TLS verified against that
+# bundle: it never reaches this host.  A re-run finds the token and only refreshes the CA.
 set -euo pipefail
 R='${rancher_host}'
 for i in $(seq 1 900); do curl -ksf "$R/ping" >/dev/null 2>&1 && break; sleep 1; done
+umask 077
+curl -ksf "$R/cacerts" > ~/rancher_cacerts.pem.tmp && mv ~/rancher_cacerts.pem.tmp ~/rancher_cacerts.pem
+[ -s ~/rancher_api_key ] && exit 0
 json() { python3 -c "import json,sys; print(json.load(sys.stdin)$1)"; }
-login_as() {
-  curl -ksf -X POST -H 'Content-Type: application/json' \
-    -d "{\"username\":\"admin\",\"password\":\"$1\",\"ttl\":60000,\"description\":\"Initial Token\"}" \
-    "$R/v3-public/localProviders/local?action=login"
-}
-# the bootstrap password the server was started with; a re-run after the password
-# change logs in with the admin password and skips the change
-changed=0
-login=$(login_as '${bootstrap_password}') || { login=$(login_as '${rancher_admin_password}'); changed=1; }
+login=$(curl -ksf -X POST -H 'Content-Type: application/json' --data-binary @- \
+  "$R/v3-public/localProviders/local?action=login" <<'TK_EOF'
+{"username":"admin","password":${jsonencode(bootstrap_password)},"ttl":60000,"description":"Initial Token"}
+TK_EOF
+)
 initial=$(printf '%s' "$login" | json '["token"]')
 tok=$(curl -ksf -u "$initial" -X POST -H 'Content-Type: application/json' \
   -d '{"type":"token","name":"triton-kubernetes","description":"Managed by triton-kubernetes","ttl":0}' "$R/v3/token")
-umask 077
 printf '%s' "$tok" > ~/rancher_api_key
 ak=$(printf '%s' "$tok" | json '["name"]')
 sk=$(printf '%s' "$tok" | json '["token"].split(":",1)[1]')
-[ "$changed" = 1 ] || curl -ksf -u "$ak:$sk" -X POST -H 'Content-Type: application/json' \
-  -d '{"currentPassword":"${bootstrap_password}","newPassword":"${rancher_admin_password}"}' "$R/v3/users?action=changepassword" >/dev/null
 curl -ksf -u "$ak:$sk" -X PUT -H 'Content-Type: application/json' \
   -d '{"name":"server-url","value":"${host_registration_url}"}' "$R/v3/settings/server-url" >/dev/null
 """
@@ -110,21 +119,46 @@ refused() {
 """.replace("@@HKA@@", ",".join(GO_HOSTKEY_ALGORITHMS))
 
 READ_API_KEY = r"""#!/bin/bash
-# data "external" program: read the manager's ~/rancher_api_key over SSH.
-# Replaces the reference's matti/outputs/shell registry module.
-# Outside an apply (query key operation = destroy | read, the executor's tk_operation)
-# a manager that cannot be reached yields empty keys instead of an error: destroying
-# what is left of a manager whose host is gone must not depend on that host.
+# data "external" program (operator machine): read the manager's ~/rancher_api_key and the
+# server's CA bundle (~/rancher_cacerts.pem, saved on the host from its own loopback) over
+# the pinned SSH session, then -- on apply -- set the admin password: a curl on the host
+# against its loopback, with the credentials and the request body on curl's stdin (a
+# config, "-K -"), which is this SSH session's stdin.  The admin password is never on a
+# command line, in a file or in a rendered script on the host (rancher/bootstrap_secret.py).
+# Replaces the reference's matti/outputs/shell registry module.  Outside an apply (query
+# key operation = destroy | read, the executor's tk_operation) a manager that cannot be
+# reached yields empty keys instead of an error: destroying what is left of a manager whose
+# host is gone must not depend on that host.
 set -euo pipefail
 eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".join(f"{k}={shlex.quote(str(v))}" for k,v in q.items()))')"
 """ + SSH_PINNED + r"""if ! tok=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_api_key' 2>"$err"); then
-  if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": ""}'; exit 0; fi
+  if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": "", "ca_certs": ""}'; exit 0; fi
   refused "read the Rancher API key"
 fi
-printf '%s' "$tok" | KH="$(pinned_for)" python3 -c '
+ca=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_cacerts.pem' 2>"$err") || ca=""
+if [ "${operation:-apply}" = apply ] && [ -n "${admin_password:-}" ] && [ "${admin_password:-}" != "${bootstrap_password:-}" ]; then
+  # curl config on stdin: user (the API token), the JSON body with both passwords
+  cfg=$(printf '%s' "$tok" | TKQ_admin="$admin_password" TKQ_boot="$bootstrap_password" python3 -c '
 import json, os, sys
 t = json.load(sys.stdin)
-print(json.dumps({"access_key": t["name"], "secret_key": t["token"].split(":", 1)[1], "known_hosts": os.environ["KH"]}))'
+q = lambda v: json.dumps(v)  # a curl config string: double-quoted, backslash escapes
+body = json.dumps({"currentPassword": os.environ["TKQ_boot"], "newPassword": os.environ["TKQ_admin"]})
+print("user = " + q(t["token"]))
+print("header = " + q("Content-Type: application/json"))
+print("data = " + q(body))')
+  code=$(printf '%s
+' "$cfg" | ssh "${opts[@]}" "$ssh_user@$host" \
+    'curl -ks -K - -o /dev/null -w "%{http_code}" -X POST "https://127.0.0.1/v3/users?action=changepassword"' 2>"$err") \
+    || refused "set the Rancher admin password"
+  # 422: the current password is no longer the bootstrap one -- set by an earlier run
+  case "$code" in 2??|422|"") ;; *) echo "setting the Rancher admin password on $host: HTTP $code" >&2; exit 1 ;; esac
+fi
+printf '%s' "$tok" | KH="$(pinned_for)" CA="$ca" python3 -c '
+import json, os, sys
+t = json.load(sys.stdin)
+ca = os.environ["CA"].strip()
+print(json.dumps({"access_key": t["name"], "secret_key": t["token"].split(":", 1)[1], "known_hosts": os.environ["KH"],
+                  "ca_certs": ca + "\n" if ca else ""}))'
 """
 
 RANCHER_CLUSTER = r"""#!/bin/bash
@@ -142,8 +176,11 @@ exec python3 -c '
 import base64, hashlib, json, re, ssl, sys, time, urllib.error, urllib.parse, urllib.request
 
 q = json.load(sys.stdin)
-ctx = ssl.create_default_context()
-ctx.check_hostname, ctx.verify_mode = False, ssl.CERT_NONE  # self-signed Rancher certificates
+# TLS verified against the CA pinned for the manager (query key ca_pem = tk_rancher_ca,
+# rendered by the executor; rancher/trust.py); none pinned: a publicly trusted certificate
+pinned = q.get("ca_pem", "").strip()
+pinned = pinned + "\n" if pinned else ""
+ctx = ssl.create_default_context(cadata=pinned) if pinned else ssl.create_default_context()
 auth = "Basic " + base64.b64encode((q["access_key"] + ":" + q["secret_key"]).encode()).decode()
 
 
@@ -152,8 +189,16 @@ def call(method, path, body=None):
                                  data=None if body is None else json.dumps(body).encode(),
                                  headers={"Authorization": auth, "Accept": "application/json",
                                           "Content-Type": "application/json"})
-    with urllib.request.urlopen(req, context=ctx, timeout=60) as resp:
-        return json.load(resp)
+    try:
+        with urllib.request.urlopen(req, context=ctx, timeout=60) as resp:
+            return json.load(resp)
+    except urllib.error.URLError as exc:
+        if isinstance(exc.reason, ssl.SSLCertVerificationError):
+            sys.exit("the Rancher server at %s presented a certificate that does not verify against %s (%s): "
+                     "refusing to send the API key. If its CA was rotated on purpose, pin the new one with "
+                     "rancher_ca_file=<PEM bundle>" % (q["api_url"], "the CA pinned for this cluster manager"
+                                                       if pinned else "the system trust store", exc.reason))
+        raise
 
 
 def get_or_none(path):
@@ -182,7 +227,9 @@ def k8s_version(requested, rke2=False):
 
 
 def ca_checksum():
-    cacerts = call("GET", "/v3/settings/cacerts").get("value", "")
+    # the checksum nodes pin: of the pinned bundle (read on the manager host), not of what the
+    # server says now
+    cacerts = pinned or call("GET", "/v3/settings/cacerts").get("value", "")
     if cacerts and not cacerts.endswith("\n"):
         cacerts += "\n"  # Rancher hashes the bundle with one trailing newline, as /cacerts serves it
     return hashlib.sha256(cacerts.encode()).hexdigest() if cacerts else ""
@@ -543,7 +590,14 @@ APPLY_ADDONS = r"""#!/bin/bash
 # MI355X cluster add-ons: wait for the cluster, then create the manifests in
 # $MANIFEST_DIR through Rancher's Kubernetes proxy (PUT on 409).
 set -euo pipefail
-api() { curl -ksf -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" -H 'Content-Type: application/json' "$@"; }
+# TLS verified against the manager's pinned CA (RANCHER_CA; empty: the system trust store)
+tls=()
+if [ -n "${RANCHER_CA:-}" ]; then
+  cafile=$(mktemp); trap 'rm -f "$cafile"' EXIT
+  printf '%s\n' "$RANCHER_CA" > "$cafile"
+  tls=(--cacert "$cafile")
+fi
+api() { curl -sf "${tls[@]}" -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" -H 'Content-Type: application/json' "$@"; }
 for i in $(seq 1 3600); do
   state=$(api "$RANCHER_URL/v3/clusters/$CLUSTER_ID" | python3 -c 'import json,sys; print(json.load(sys.stdin).get("state",""))' || true)
   [ "$state" = active ] && break
@@ -554,7 +608,7 @@ for f in "$MANIFEST_DIR"/*.json; do
   path=$(python3 -c 'import json,sys; print(json.load(open(sys.argv[1]))["path"])' "$f")
   obj=$(python3 -c 'import json,sys; print(json.dumps(json.load(open(sys.argv[1]))["object"]))' "$f")
   name=$(python3 -c 'import json,sys; print(json.load(open(sys.argv[1]))["object"]["metadata"]["name"])' "$f")
-  code=$(curl -ks -o /dev/null -w '%{http_code}' -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" \
+  code=$(curl -s "${tls[@]}" -o /dev/null -w '%{http_code}' -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" \
          -H 'Content-Type: application/json' -X POST -d "$obj" "$RANCHER_URL/k8s/clusters/$CLUSTER_ID$path")
   if [ "$code" = 409 ]; then api -X PUT -d "$obj" "$RANCHER_URL/k8s/clusters/$CLUSTER_ID$path/$name" >/dev/null
   elif [ "$code" -ge 300 ]; then echo "applying $f: HTTP $code" >&2; exit 1; fi

@@ -189,7 +189,10 @@ def _cluster_client(ctx: Context, backend: Backend) -> Tuple[str, str, str, Ranc
     cl = outputs_from_tfstate(raw, key)
     if not mgr.get("rancher_url") or not cl.get("rancher_cluster_id"):
         raise TKError(f"Cluster '{name}' has no Rancher outputs yet (was it applied?)")
-    factory = ctx.extras.get("rancher_factory") or RancherClient
+    from ..rancher import trust
+
+    factory = ctx.extras.get("rancher_factory") or (  # verified against the pinned CA (rancher/trust.py)
+        lambda url, ak="", sk="": trust.client(backend, manager, url, ak, sk))
     client = factory(mgr["rancher_url"], mgr.get("rancher_access_key", ""), mgr.get("rancher_secret_key", ""))
     return manager, name, cl["rancher_cluster_id"], client
 

@@ -142,7 +142,7 @@ def _reread(backend: Backend, manager: str, key: str):
 def _rancher_client(ctx: Context, backend: Backend, state, cluster_key: str):
     """``(RancherClient, cluster id)`` from the executor's recorded outputs, or ``(None, "")``."""
     from ..executor.base import outputs_from_tfstate
-    from ..rancher.client import RancherClient
+    from ..rancher import trust
     from ..state import MANAGER_KEY
 
     raw = backend.read_tfstate(state.name)
@@ -150,7 +150,9 @@ def _rancher_client(ctx: Context, backend: Backend, state, cluster_key: str):
     cid = outputs_from_tfstate(raw, cluster_key).get("rancher_cluster_id")
     if not mgr.get("rancher_url") or not cid:
         return None, ""
-    factory = ctx.extras.get("rancher_factory") or RancherClient
+
+    factory = ctx.extras.get("rancher_factory") or (  # verified against the pinned CA (rancher/trust.py)
+        lambda url, ak="", sk="": trust.client(backend, state.name, url, ak, sk))
     return factory(mgr["rancher_url"], mgr.get("rancher_access_key", ""), mgr.get("rancher_secret_key", "")), cid
 
 
@@ -159,7 +161,7 @@ def _rancher_node_cleanup_info(ctx: Context, backend: Backend, state, cluster_ke
     if not ctx.settings.get_bool("rancher_cleanup"):
         return None
     from ..executor.base import outputs_from_tfstate
-    from ..rancher.client import RancherClient
+    from ..rancher import trust
     from ..state import MANAGER_KEY
 
     raw = backend.read_tfstate(state.name)
@@ -169,8 +171,8 @@ def _rancher_node_cleanup_info(ctx: Context, backend: Backend, state, cluster_ke
         return None
 
     def _cleanup():
-        client = RancherClient(mgr["rancher_url"], mgr.get("rancher_access_key", ""),
-                               mgr.get("rancher_secret_key", ""))
+        client = trust.client(backend, state.name, mgr["rancher_url"], mgr.get("rancher_access_key", ""),
+                              mgr.get("rancher_secret_key", ""))
         gone = [n["id"] for n in client.nodes(cid)
                 if hostname in (n.get("hostname"), n.get("nodeName"), n.get("requestedHostname"))]
         for nid in gone:
@@ -186,7 +188,7 @@ def _rancher_cleanup_info(ctx: Context, backend: Backend, state, cluster_key: st
     if not ctx.settings.get_bool("rancher_cleanup"):
         return None
     from ..executor.base import outputs_from_tfstate
-    from ..rancher.client import RancherClient
+    from ..rancher import trust
     from ..state import MANAGER_KEY
 
     raw = backend.read_tfstate(state.name)
@@ -196,8 +198,8 @@ def _rancher_cleanup_info(ctx: Context, backend: Backend, state, cluster_key: st
         return None
 
     def _cleanup():
-        client = RancherClient(mgr["rancher_url"], mgr.get("rancher_access_key", ""),
-                               mgr.get("rancher_secret_key", ""))
+        client = trust.client(backend, state.name, mgr["rancher_url"], mgr.get("rancher_access_key", ""),
+                              mgr.get("rancher_secret_key", ""))
         client.delete_cluster(cl["rancher_cluster_id"])
         ctx.echo(f"Removed Rancher cluster {cl['rancher_cluster_id']}")
 

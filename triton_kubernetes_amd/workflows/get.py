@@ -98,9 +98,10 @@ def get_nodes(ctx: Context, backend: Backend) -> List[Dict[str, str]]:
     mgr, cl = executor.outputs(state, backend, MANAGER_KEY), executor.outputs(state, backend, key)
     if not mgr.get("rancher_url") or not cl.get("rancher_cluster_id"):
         raise ConfigError(f"Cluster '{name}' has no Rancher outputs yet (was it applied?)")
-    from ..rancher.client import RancherClient
+    from ..rancher import trust
 
-    factory = ctx.extras.get("rancher_factory") or RancherClient
+    factory = ctx.extras.get("rancher_factory") or (  # verified against the pinned CA (rancher/trust.py)
+        lambda url, ak="", sk="": trust.client(backend, state.name, url, ak, sk))
     client = factory(mgr["rancher_url"], mgr.get("rancher_access_key", ""), mgr.get("rancher_secret_key", ""))
     items = sorted(client.k8s_nodes(cl["rancher_cluster_id"]), key=lambda i: (i.get("metadata") or {}).get("name", ""))
     rows = [_node_row(i) for i in items]
