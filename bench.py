@@ -439,13 +439,16 @@ def main() -> int:
         (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
         for p in (torch.cuda.get_device_properties(i) for i in range(visible)))
 
+    floor = [None]  # the node's clean used-HBM level (the first wait measures it)
+
     def settle() -> dict:
         """Outside the timed region: the previous step's released HBM is cleared by the
         driver before the next step starts (a node entering service starts clean).  Local
         rank 0 watches the node's cards; every rank waits for it."""
         got = {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
         if args.hbm_settle == "on" and my_cards and local_rank == 0:
-            got = hbm.settle(cards=my_cards, quiet_s=1.5)
+            got = hbm.settle(cards=my_cards, floor=floor[0])
+            floor[0] = got["floor"]
         barrier()
         return got
 
@@ -597,6 +600,7 @@ def main() -> int:
             "hbm_settle_cards": my_cards,
             "hbm_settle_s": [s["waited_s"] for s in settles],
             "hbm_settle_released_gib": [s["released_gib"] for s in settles],
+            "hbm_settle_reached_floor": [s.get("reached_floor") for s in settles],
             "phase_ms_per_step": phase_ms,
         }
         print(json.dumps(line), flush=True)

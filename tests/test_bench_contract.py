@@ -82,11 +82,31 @@ def test_settle_waits_for_the_backlog_to_drain(tmp_path):
     assert not got["timed_out"]
 
 
-def test_settle_baseline_exits_early(tmp_path):
+def test_settle_floor_exits_early(tmp_path):
     _card(str(tmp_path), "card0", 8 << 30)
     t0 = time.monotonic()
-    got = hbm.settle(str(tmp_path), quiet_s=5.0, baseline=8 << 30)
-    assert time.monotonic() - t0 < 1.0 and not got["timed_out"]
+    got = hbm.settle(str(tmp_path), quiet_s=5.0, floor=8 << 30)
+    assert time.monotonic() - t0 < 1.0 and not got["timed_out"] and got["reached_floor"]
+
+
+def test_settle_waits_for_a_release_that_has_not_started(tmp_path):
+    """An exited process's memory comes back later (the driver's deferred teardown): with a
+    floor the wait holds on until the level is back, not just for a quiet window."""
+    path = _card(str(tmp_path), "card0", 40 << 30)
+
+    def later():
+        time.sleep(0.6)  # nothing for longer than the quiet window, then the release
+        for used in (24 << 30, 8 << 30, 1 << 30):
+            with open(path + ".tmp", "w") as fh:
+                fh.write(f"{used}\n")
+            os.replace(path + ".tmp", path)
+            time.sleep(0.05)
+
+    t = threading.Thread(target=later)
+    t.start()
+    got = hbm.settle(str(tmp_path), quiet_s=1.0, poll_s=0.005, timeout_s=10, floor=1 << 30, slack=0)
+    t.join()
+    assert got["reached_floor"] and got["waited_s"] >= 0.6 and got["floor"] == 1 << 30
 
 
 def test_settle_times_out_on_a_card_that_keeps_falling(tmp_path):

@@ -272,3 +272,103 @@ def test_a_stuck_span_child_is_killed(span_child, monkeypatch):
     (_, proc), = probe._span_children
     probe.wait_frees()
     assert proc.returncode is not None and proc.returncode < 0 and probe._span_children == []
+
+
+# --- the whole burn-in in a gpu-burnin child (node agents) -------------------------------------
+
+CHILD_OK = {
+    "ok": True, "device": 0,
+    "info": {"name": "AMD Instinct MI355X", "arch": "gfx950:sramecc+:xnack-", "compute_units": 256,
+             "wavefront_size": 64, "clock_khz": 2400000, "total_mem": 309 << 30, "free_mem": 300 << 30,
+             "l2_bytes": 4 << 20, "pci_domain": 0, "pci_bus": 117, "pci_device": 0},
+    "hbm": {"read_gbps": 6500.0, "write_gbps": 6200.0, "copy_gbps": 5800.0},
+    "bf16": {"tflops": 1950.0, "ms": 1.0}, "fp8": {"tflops": 4300.0, "ms": 1.0},
+    "gemm": {"tflops": 1400.0, "ms": 0.8, "bad_columns": 0, "bad_rows": 0, "first_bad_column": -1,
+             "first_bad_row": -1, "max_norm_error": 0.01},
+    "gemm_fp8": {"tflops": 2900.0, "ms": 0.4, "bad_columns": 0, "bad_rows": 0, "first_bad_column": -1,
+                 "first_bad_row": -1, "max_norm_error": 0.01},
+    "gemm_first_bad": None, "gemm_fp8_first_bad": None,
+    "memtest": {"errors": 0, "verify_gbps": 6100.0, "bytes": 300 << 30, "hbm_bytes": 309 << 30,
+                "alloc_ms": 900.0, "test_ms": 337.0},
+    "remeasured": [], "phase_ms": {"hbm": 180.0, "memtest": 1300.0},
+}
+
+
+@pytest.fixture
+def burnin_child(tmp_path, monkeypatch):
+    """A stand-in ``gpu-burnin --burnin-child``: prints the verdict in $FAKE_CHILD_DOC."""
+    import stat
+    import sys
+
+    exe = tmp_path / "gpu-burnin"
+    exe.write_text(f"""#!{sys.executable}
+import os, sys
+open(os.environ["FAKE_CHILD_ARGV"], "w").write(" ".join(sys.argv[1:]))
+print("a banner", flush=True)
+print(os.environ["FAKE_CHILD_DOC"], flush=True)
+""")
+    exe.chmod(exe.stat().st_mode | stat.S_IEXEC)
+    monkeypatch.setattr(probe, "_burnin_exe", lambda: str(exe))
+    monkeypatch.setenv("FAKE_CHILD_ARGV", str(tmp_path / "argv"))
+
+    class _Lib:
+        def tkp_wait_frees(self):
+            return 0
+
+    monkeypatch.setattr(probe, "_lib", lambda: _Lib())
+    monkeypatch.setattr(probe, "device_info", lambda dev: pytest.fail("in-process burn-in used"))
+    probe.set_burnin_process(True)
+    yield tmp_path / "argv"
+    probe.set_burnin_process(False)
+    probe.wait_frees()
+
+
+def test_burnin_child_passes_levels_and_floors_and_is_judged_here(burnin_child, monkeypatch):
+    import json
+
+    monkeypatch.setenv("FAKE_CHILD_DOC", json.dumps(CHILD_OK))
+    res = probe.run_burnin(0, "full")
+    assert res.ok, res.failures
+    assert res.device.is_gfx950 and res.memtest["bytes"] == 300 << 30 and "process" in res.phase_ms
+    argv = burnin_child.read_text().split()
+    assert argv[:3] == ["--burnin-child", "--device", "0"]
+    hbm_bytes, hbm_iters, mfma_iters, mt_bytes, passes = probe.LEVELS["full"]
+    opts = dict(zip(argv[3::2], argv[4::2]))
+    assert opts["--hbm-bytes"] == str(hbm_bytes) and opts["--memtest-bytes"] == "0" and opts["--memtest-passes"] == "3"
+    assert opts["--gemm"] == "8192,8192,8192,5" and opts["--span-chunk"] == str(probe.SPAN_CHILD_CHUNK)
+    assert float(opts["--min-read-gbps"]) == pytest.approx(probe._floors(probe.Thresholds())["read"], rel=1e-3)
+    labels = __import__("triton_kubernetes_amd.node.labels", fromlist=["burnin_labels"]).burnin_labels(
+        "full", {0: res.to_json()})
+    assert labels["amd.com/gpu.burnin"] == "passed"
+
+
+def test_burnin_child_failures_are_the_same_verdicts(burnin_child, monkeypatch):
+    import json
+
+    bad = dict(CHILD_OK, hbm={"read_gbps": 900.0, "write_gbps": 1.0, "copy_gbps": 1.0},
+               gemm_first_bad={"tflops": 1400.0, "ms": 1, "bad_columns": 2, "bad_rows": 1, "first_bad_column": 7,
+                               "first_bad_row": 3, "max_norm_error": 9.0},
+               memtest=dict(CHILD_OK["memtest"], errors=12))
+    monkeypatch.setenv("FAKE_CHILD_DOC", json.dumps(bad))
+    res = probe.run_burnin(0, "full")
+    assert not res.ok
+    text = "; ".join(res.failures)
+    assert "HBM read 900 GB/s below" in text and "memtest: 12 mismatching words" in text
+    assert "GEMM checksum mismatch: 1 rows / 2 columns (first at row 3, column 7)" in text
+    monkeypatch.setenv("FAKE_CHILD_DOC", json.dumps({"ok": False, "error": "hipMalloc: out of memory"}))
+    with pytest.raises(probe.ProbeError, match="out of memory"):
+        probe.run_burnin(0, "quick")
+    monkeypatch.setenv("FAKE_CHILD_DOC", json.dumps({"level": "full", "gpus": [], "ok": True}))  # a stale binary
+    with pytest.raises(probe.ProbeError, match="no burn-in verdict"):
+        probe.run_burnin(0, "quick")
+
+
+def test_partitions_of_one_pool_burn_in_in_process(burnin_child, monkeypatch):
+    """Concurrent partitions share an HBM pool: the span is sized per partition here, so
+    they keep the in-process path (the child tests a whole GPU's HBM)."""
+    called = []
+    monkeypatch.setattr(probe, "_burnin_child", lambda *a, **k: called.append(a))
+    monkeypatch.setattr(probe, "device_info", lambda dev: (_ for _ in ()).throw(RuntimeError("in-process")))
+    with pytest.raises(RuntimeError, match="in-process"):
+        probe.run_burnin(0, "full", probe.Thresholds.for_partition("cpx", "nps2"))
+    assert not called

@@ -261,8 +261,14 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         # ... and the full memtest's ~300 GB is held and released by a gpu-burnin child, so no
         # hipFree of it blocks this process's other HIP calls (ops/probe.py:memtest_span_process)
         probe.set_span_process(os.environ.get("TK_SPAN_PROCESS", "1") != "0")
-        # burn-in arena: resident for the agent's lifetime, released after an idle period
-        if os.environ.get("TK_PROBE_SCRATCH_CACHE", "1") != "0":
+        # the whole burn-in of a GPU runs in a gpu-burnin child: beside this process's RCCL
+        # communicator start, whose code-object loading held up the screens' launches here
+        # (ops/probe.py:_burnin_child)
+        burnin_child = os.environ.get("TK_BURNIN_PROCESS", "1") != "0"
+        probe.set_burnin_process(burnin_child)
+        # burn-in arena (in-process burn-ins only): resident for the agent's lifetime,
+        # released after an idle period
+        if os.environ.get("TK_PROBE_SCRATCH_CACHE", "0" if burnin_child else "1") != "0":
             level = os.environ.get("TK_PROBE_SCRATCH_LEVEL", "quick")
             t1 = time.perf_counter()
             list(self._pool.map(lambda d: probe.prealloc_scratch(d, level), self.devices))

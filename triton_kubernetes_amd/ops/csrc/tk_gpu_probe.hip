@@ -1290,7 +1290,139 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
   return degraded ? 1 : 0;
 }
 
+// --burnin-child: one GPU's whole burn-in in its own process, for ops/probe.py:run_burnin
+// in a node agent.  The agent's own HIP runtime is busy beside it (a cluster gate's RCCL
+// communicator starting: loading RCCL's code objects holds the runtime's locks, and the
+// screens' kernel launches waited behind it for 1.5-4 s, profiles/round5/breakdown.md), so
+// the screens run here instead.  The parameters and the pass/fail floors come from
+// ops/probe.py (LEVELS, Thresholds): this mode measures -- re-measuring a throughput below
+// its floor, as the agent would -- and reports; the agent judges.  One JSON line as soon as
+// the verdict is known; the span memtest's chunks are released after it.
+static void json_escape(const char* in, char* out, size_t cap) {
+  size_t o = 0;
+  for (; *in && o + 2 < cap; ++in) {
+    if (*in == '"' || *in == '\\') out[o++] = '\\';
+    out[o++] = (*in == '\n' || *in == '\r') ? ' ' : *in;
+  }
+  out[o] = 0;
+}
+
+static int burnin_child_main(int argc, char** argv) {
+  int dev = 0, hbm_iters = 3, mfma_iters = 2000, gm = 4096, gn = 4096, gk = 4096, greps = 5, passes = 1;
+  size_t hbm_bytes = 1ull << 30, mt_bytes = 1ull << 30, headroom = 4ull << 30, chunk = 1ull << 30;
+  double min_read = 0, min_bf16 = 0, min_fp8 = 0, min_gemm = 0, min_gemm8 = 0;
+  for (int i = 1; i + 1 < argc; ++i) {
+    const char* a = argv[i];
+    if (!strcmp(a, "--device")) dev = atoi(argv[++i]);
+    else if (!strcmp(a, "--hbm-bytes")) hbm_bytes = strtoull(argv[++i], nullptr, 10);
+    else if (!strcmp(a, "--hbm-iters")) hbm_iters = atoi(argv[++i]);
+    else if (!strcmp(a, "--mfma-iters")) mfma_iters = atoi(argv[++i]);
+    else if (!strcmp(a, "--gemm")) {  // M,N,K,reps
+      if (sscanf(argv[++i], "%d,%d,%d,%d", &gm, &gn, &gk, &greps) != 4) { printf("{\"ok\":false,\"error\":\"--gemm M,N,K,reps\"}\n"); return 2; }
+    } else if (!strcmp(a, "--memtest-bytes")) mt_bytes = strtoull(argv[++i], nullptr, 10);
+    else if (!strcmp(a, "--memtest-passes")) passes = atoi(argv[++i]);
+    else if (!strcmp(a, "--span-headroom")) headroom = strtoull(argv[++i], nullptr, 10);
+    else if (!strcmp(a, "--span-chunk")) chunk = strtoull(argv[++i], nullptr, 10);
+    else if (!strcmp(a, "--min-read-gbps")) min_read = atof(argv[++i]);
+    else if (!strcmp(a, "--min-bf16-tflops")) min_bf16 = atof(argv[++i]);
+    else if (!strcmp(a, "--min-fp8-tflops")) min_fp8 = atof(argv[++i]);
+    else if (!strcmp(a, "--min-gemm-tflops")) min_gemm = atof(argv[++i]);
+    else if (!strcmp(a, "--min-gemm-fp8-tflops")) min_gemm8 = atof(argv[++i]);
+  }
+  struct tkp_device_info info;
+  double hbm[3] = {0, 0, 0}, bf16[2] = {0, 0}, fp8[2] = {0, 0}, mt[7] = {0, 0, 0, 0, 0, 0, 0};
+  double g[2][7], gbad[2][7];
+  bool bad[2] = {false, false};
+  double ph[6] = {0, 0, 0, 0, 0, 0};
+  std::string remeasured;
+  auto fail = [&](const char* what) {
+    char e[600];
+    json_escape(g_err[0] ? g_err : tkg_last_error(), e, sizeof(e));
+    printf("{\"ok\":false,\"error\":\"%s: %s\"}\n", what, e);
+    fflush(stdout);
+    return 2;
+  };
+  auto now = [] { return std::chrono::steady_clock::now(); };
+  auto ms_since = [&](std::chrono::steady_clock::time_point t) {
+    return std::chrono::duration<double, std::milli>(now() - t).count();
+  };
+  // best of up to 3 runs for a value below its floor (ops/probe.py:REMEASURE); gemm runs
+  // also record the first with a checksum mismatch
+  auto best = [&](const char* what, auto&& run, double* out, int n, double floor, int gi) -> bool {
+    if (run(out) != 0) return false;
+    if (gi >= 0 && (out[2] != 0.0 || out[3] != 0.0) && !bad[gi]) { bad[gi] = true; memcpy(gbad[gi], out, sizeof(double) * 7); }
+    for (int k = 0; k < 2 && out[0] < floor; ++k) {
+      double again[7] = {0, 0, 0, 0, -1, -1, 0};
+      if (run(again) != 0) return false;
+      remeasured += std::string(remeasured.empty() ? "" : ",") + "\"" + what + "\"";
+      if (gi >= 0 && (again[2] != 0.0 || again[3] != 0.0) && !bad[gi]) { bad[gi] = true; memcpy(gbad[gi], again, sizeof(double) * 7); }
+      if (again[0] > out[0]) memcpy(out, again, sizeof(double) * (size_t)n);
+    }
+    return true;
+  };
+  for (int i = 0; i < 2; ++i) for (int j = 0; j < 7; ++j) g[i][j] = gbad[i][j] = (j == 4 || j == 5) ? -1 : 0;
+  if (tkp_device_info(dev, &info) != 0) return fail("device_info");
+  auto t = now();
+  if (!best("hbm", [&](double* o) { return tkp_hbm_bandwidth(dev, hbm_bytes, hbm_iters, 16, o); }, hbm, 3, min_read, -1))
+    return fail("hbm_bandwidth");
+  ph[0] = ms_since(t); t = now();
+  if (!best("mfma_bf16", [&](double* o) { return tkp_mfma_peak(dev, 0, mfma_iters, 3, 2, o); }, bf16, 2, min_bf16, -1))
+    return fail("mfma_peak[bf16]");
+  ph[1] = ms_since(t); t = now();
+  if (!best("mfma_fp8", [&](double* o) { return tkp_mfma_peak(dev, 1, mfma_iters / 2, 3, 2, o); }, fp8, 2, min_fp8, -1))
+    return fail("mfma_peak[fp8]");
+  ph[2] = ms_since(t); t = now();
+  if (!best("gemm_bf16", [&](double* o) { return tkg_screen(dev, gm, gn, gk, greps, -1, o); }, g[0], 7, min_gemm, 0))
+    return fail("gemm[bf16]");
+  ph[3] = ms_since(t); t = now();
+  if (!best("gemm_fp8", [&](double* o) { return tkg_screen_fp8(dev, gm, gn, gk, greps, -1, o); }, g[1], 7, min_gemm8, 1))
+    return fail("gemm[fp8]");
+  ph[4] = ms_since(t); t = now();
+  if (mt_bytes) {  // a fixed size (quick): one buffer
+    double o[2] = {0, 0};
+    if (tkp_memtest(dev, mt_bytes, passes, o) != 0) return fail("memtest");
+    mt[0] = o[0]; mt[1] = o[1]; mt[2] = (double)mt_bytes; mt[3] = (double)info.total_mem;
+  } else {  // every free byte but the headroom, held at once (full); released after the verdict
+    g_keep_span = 1;
+    if (tkp_memtest_span(dev, 0, chunk, headroom, passes, mt) != 0) return fail("memtest_span");
+  }
+  ph[5] = ms_since(t);
+  auto gemm_json = [](const double* x) {
+    static char buf[2][400];
+    static int which = 0;
+    char* b = buf[which ^= 1];
+    snprintf(b, 400, "{\"tflops\":%.3f,\"ms\":%.4f,\"bad_columns\":%.0f,\"bad_rows\":%.0f,\"first_bad_column\":%.0f,"
+             "\"first_bad_row\":%.0f,\"max_norm_error\":%.6g}", x[0], x[1], x[2], x[3], x[4], x[5], x[6]);
+    return (const char*)b;
+  };
+  char name[256], arch[128];
+  json_escape(info.name, name, sizeof(name));
+  json_escape(info.arch, arch, sizeof(arch));
+  printf("{\"ok\":true,\"device\":%d,\"info\":{\"name\":\"%s\",\"arch\":\"%s\",\"compute_units\":%d,"
+         "\"wavefront_size\":%d,\"clock_khz\":%d,\"total_mem\":%lld,\"free_mem\":%lld,\"l2_bytes\":%d,"
+         "\"pci_domain\":%d,\"pci_bus\":%d,\"pci_device\":%d},"
+         "\"hbm\":{\"read_gbps\":%.3f,\"write_gbps\":%.3f,\"copy_gbps\":%.3f},"
+         "\"bf16\":{\"tflops\":%.3f,\"ms\":%.4f},\"fp8\":{\"tflops\":%.3f,\"ms\":%.4f},",
+         dev, name, arch, info.compute_units, info.wavefront_size, info.clock_khz, info.total_mem, info.free_mem,
+         info.l2_bytes, info.pci_domain, info.pci_bus, info.pci_device, hbm[0], hbm[1], hbm[2], bf16[0], bf16[1],
+         fp8[0], fp8[1]);
+  printf("\"gemm\":%s,", gemm_json(g[0]));
+  printf("\"gemm_fp8\":%s,", gemm_json(g[1]));
+  printf("\"gemm_first_bad\":%s,", bad[0] ? gemm_json(gbad[0]) : "null");
+  printf("\"gemm_fp8_first_bad\":%s,", bad[1] ? gemm_json(gbad[1]) : "null");
+  printf("\"memtest\":{\"errors\":%.0f,\"verify_gbps\":%.1f,\"bytes\":%.0f,\"hbm_bytes\":%.0f,\"alloc_ms\":%.1f,"
+         "\"test_ms\":%.1f},\"remeasured\":[%s],\"phase_ms\":{\"hbm\":%.1f,\"mfma_bf16\":%.1f,\"mfma_fp8\":%.1f,"
+         "\"gemm_bf16\":%.1f,\"gemm_fp8\":%.1f,\"memtest\":%.1f}}\n",
+         mt[0], mt[1], mt[2], mt[3], mt[4], mt[5], remeasured.c_str(), ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
+  fflush(stdout);
+  for (void* q : g_kept_chunks) (void)hipFree(q);
+  g_kept_chunks.clear();
+  return 0;
+}
+
 int main(int argc, char** argv) {
+  for (int i = 1; i < argc; ++i)
+    if (!strcmp(argv[i], "--burnin-child")) return burnin_child_main(argc, argv);
   int dev = 0, all = 0;
   const char* level = "full";  // = models/baremetal.py DEFAULT_BURNIN
   const char* labels_path = nullptr;  // --labels FILE: node labels recording what was tested

@@ -61,28 +61,35 @@ def vram_used(drm_root: str = DRM_ROOT, cards: Optional[Iterable[str]] = None) -
     return out
 
 
-def settle(drm_root: str = DRM_ROOT, quiet_s: float = 1.5, poll_s: float = 0.02, timeout_s: float = 120.0,
-           baseline: Optional[int] = None, slack: int = 1 << 30,
+def settle(drm_root: str = DRM_ROOT, quiet_s: float = 5.0, poll_s: float = 0.02, timeout_s: float = 120.0,
+           floor: Optional[int] = None, slack: int = 1 << 30,
            cards: Optional[Iterable[str]] = None) -> Dict[str, float]:
-    """Block until the used VRAM of ``cards`` (default: every card) stops falling: none of
-    their ``mem_info_vram_used`` dropped during the last ``quiet_s`` seconds (the clearing
-    backlog drains at tens of GB/s, so a quiet window means it is empty), or their total is
-    within ``slack`` of ``baseline``.  Returns what it waited for; no cards: returns at once.
+    """Block until the used VRAM of ``cards`` (default: every card) is back within ``slack``
+    of ``floor`` -- the clean level an earlier call measured -- or, without a floor or when
+    it is not reached, until none of their ``mem_info_vram_used`` dropped for ``quiet_s``
+    seconds.  Returns what it waited for, and ``floor``: the lowest level seen (the next
+    call's floor).  No cards: returns at once.
 
-    The driver returns a released allocation to the free pool whole, once it is cleared:
-    a 16 GiB one drops ``mem_info_vram_used`` in one step ~0.5 s after the previous
-    (``profiles/round5/vram_release.jsonl``), so the quiet window spans several of those."""
+    The floor is what makes the wait reliable: a process that exits leaves its memory to
+    the driver, which returns it (cleared) only later, a whole allocation at a time -- a
+    16 GiB one ~0.5 s after the previous (``profiles/round5/vram_release.jsonl``) -- and the
+    release may not have begun when the wait starts, so no quiet window alone can tell
+    "nothing pending" from "not started yet"."""
     cards = list(cards) if cards is not None else None
     t0 = time.monotonic()
     first = vram_used(drm_root, cards)
     if not first:
-        return {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
+        return {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False, "floor": 0}
     last = dict(first)
+    lowest = sum(first.values())
     quiet_since = t0
     timed_out = False
+    reached = False
     while True:
         total = sum(last.values())
-        if baseline is not None and total <= baseline + slack:
+        lowest = min(lowest, total)
+        if floor is not None and total <= floor + slack:
+            reached = True
             break
         now = time.monotonic()
         if now - quiet_since >= quiet_s:
@@ -97,4 +104,5 @@ def settle(drm_root: str = DRM_ROOT, quiet_s: float = 1.5, poll_s: float = 0.02,
         last = cur
     return {"waited_s": round(time.monotonic() - t0, 4),
             "released_gib": round(max(0, sum(first.values()) - sum(last.values())) / 2 ** 30, 2),
-            "cards": len(first), "timed_out": timed_out}
+            "cards": len(first), "timed_out": timed_out, "reached_floor": reached,
+            "floor": min(lowest, floor) if floor is not None else lowest}

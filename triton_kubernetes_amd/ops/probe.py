@@ -16,7 +16,7 @@ import subprocess
 import threading
 import time
 from dataclasses import asdict, dataclass, field
-from typing import Any, Dict, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence, Tuple
 
 from ..utils.trace import span
 from . import native
@@ -263,12 +263,37 @@ def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, pas
     argv = [exe, "--memtest-span", "--device", str(int(dev)), "--span-bytes", str(int(nbytes)),
             "--span-headroom", str(int(headroom)), "--span-passes", str(int(passes)),
             "--span-chunk", str(int(chunk or SPAN_CHILD_CHUNK))]
+    try:
+        doc, process_ms = _child_verdict(argv, dev, timeout, "memtest_span")
+    except _ChildUnstartable as exc:
+        return _span_in_process(dev, nbytes, headroom, passes, str(exc))
+    if not doc.get("ok"):
+        raise ProbeError(f"memtest_span: {doc.get('error', 'failed')}")
+    try:
+        return {"errors": int(doc["errors"]), "verify_gbps": float(doc["verify_gbps"]), "bytes": int(doc["bytes"]),
+                "hbm_bytes": int(doc["hbm_bytes"]), "alloc_ms": float(doc["alloc_ms"]),
+                "test_ms": float(doc["test_ms"]), "free_ms": 0.0, "process_ms": process_ms}
+    except (KeyError, TypeError, ValueError) as exc:
+        # not a --memtest-span verdict (a whole burn-in's report, say): no verdict at all
+        raise ProbeError(f"memtest_span: {exe} gave no memtest-span verdict ({type(exc).__name__}: {exc}): "
+                         f"{json.dumps(doc)[:200]!r}") from None
+
+
+class _ChildUnstartable(native.NativeUnavailable):
+    """The ``gpu-burnin`` child could not be started (nothing ran on the GPU)."""
+
+
+def _child_verdict(argv: List[str], dev: int, timeout: float, what: str) -> Tuple[Dict[str, Any], float]:
+    """Start a ``gpu-burnin`` child for ``dev`` and return its JSON verdict (the first JSON
+    line it prints) and the ms until then.  The child is registered with the device's span
+    children: it releases what it holds after the verdict, and the next span on the device
+    (and :func:`wait_frees`) waits for it to exit."""
     t0 = time.perf_counter()
     try:
         proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
                                 start_new_session=True)
     except OSError as exc:
-        return _span_in_process(dev, nbytes, headroom, passes, f"cannot start {exe}: {exc}")
+        raise _ChildUnstartable(f"cannot start {argv[0]}: {exc}") from exc
     with _span_mu:
         _span_children.append((dev, proc))
     # the verdict is the one JSON line (a library may print others); read on a thread, so a
@@ -290,26 +315,19 @@ def memtest_span_process(dev: int, nbytes: int = 0, headroom: int = 4 << 30, pas
         line = got.get(timeout=timeout)
     except queue.Empty:
         proc.kill()
-        raise ProbeError(f"memtest_span: gpu-burnin --memtest-span gave no verdict within {timeout:.0f} s") from None
+        raise ProbeError(f"{what}: {os.path.basename(argv[0])} {argv[1]} gave no verdict within {timeout:.0f} s") \
+            from None
     if not line:
         proc.wait(timeout=SPAN_RELEASE_TIMEOUT_S)
-        raise ProbeError(f"memtest_span: gpu-burnin --memtest-span exited {proc.returncode} without a verdict")
+        raise ProbeError(f"{what}: {os.path.basename(argv[0])} {argv[1]} exited {proc.returncode} without a verdict")
     try:
         doc = json.loads(line)
     except ValueError as exc:
         proc.kill()
-        raise ProbeError(f"memtest_span: unreadable verdict {line[:200]!r}") from exc
-    if not isinstance(doc, dict) or not doc.get("ok"):
-        raise ProbeError(f"memtest_span: {doc.get('error', 'failed') if isinstance(doc, dict) else doc!r}")
-    try:
-        return {"errors": int(doc["errors"]), "verify_gbps": float(doc["verify_gbps"]), "bytes": int(doc["bytes"]),
-                "hbm_bytes": int(doc["hbm_bytes"]), "alloc_ms": float(doc["alloc_ms"]),
-                "test_ms": float(doc["test_ms"]), "free_ms": 0.0,
-                "process_ms": round((time.perf_counter() - t0) * 1e3, 1)}
-    except (KeyError, TypeError, ValueError) as exc:
-        # not a --memtest-span verdict (a whole burn-in's report, say): no verdict at all
-        raise ProbeError(f"memtest_span: {exe} gave no memtest-span verdict ({type(exc).__name__}: {exc}): "
-                         f"{line[:200]!r}") from None
+        raise ProbeError(f"{what}: unreadable verdict {line[:200]!r}") from exc
+    if not isinstance(doc, dict):
+        raise ProbeError(f"{what}: unreadable verdict {line[:200]!r}")
+    return doc, round((time.perf_counter() - t0) * 1e3, 1)
 
 
 def _span_in_process(dev: int, nbytes: int, headroom: int, passes: int, why: str) -> Dict[str, float]:
@@ -460,17 +478,120 @@ def _phase(res: "BurninResult", name: str, dev: int):
             res.phase_ms[name] = round(res.phase_ms.get(name, 0.0) + (time.perf_counter() - t0) * 1e3, 1)
 
 
+# --- the burn-in in a child process (node agents) --------------------------------------------
+# A node agent's HIP runtime is also where the cluster gate's RCCL communicator starts, and
+# starting one loads RCCL's code objects under the runtime's locks: the screens' kernel
+# launches in the same process waited behind it, 1.5 s at quick and up to 4 s at full
+# (profiles/round5/README.md).  An agent therefore runs each GPU's burn-in in a
+# ``gpu-burnin --burnin-child`` process of its own (set_burnin_process): the same
+# measurements with the parameters and floors of LEVELS / Thresholds, judged here by the
+# same rules (_judge).
+_BURNIN_PROCESS = False
+
+
+def set_burnin_process(on: bool) -> None:
+    """Run :func:`run_burnin` in ``gpu-burnin --burnin-child`` processes (node agents)."""
+    global _BURNIN_PROCESS
+    _BURNIN_PROCESS = bool(on)
+
+
+def _floors(th: Thresholds) -> Dict[str, float]:
+    return {"read": th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS * th.share,
+            "bf16": th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS * th.share,
+            "fp8": th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS * th.share,
+            "gemm_bf16": th.min_gemm_frac * MI355X_BF16_DENSE_TFLOPS * th.share,
+            "gemm_fp8": th.min_gemm_fp8_frac * MI355X_FP8_DENSE_TFLOPS * th.share}
+
+
+def _judge(res: BurninResult, th: Thresholds, first_bad: Dict[str, Optional[Dict[str, Any]]]) -> BurninResult:
+    """The burn-in's verdict from its measurements (in-process or from a child), appended
+    to ``res.failures``: arch and CUs, each throughput against its floor, any GEMM run
+    with a checksum mismatch (``first_bad``: the first such run per dtype), memtest words."""
+    info, fl = res.device, _floors(th)
+    if th.require_gfx950 and not info.is_gfx950:
+        res.failures.append(f"arch {info.arch} is not gfx950")
+    if info.compute_units < th.min_cus:
+        res.failures.append(f"{info.compute_units} CUs < {th.min_cus}")
+    if res.hbm["read_gbps"] < fl["read"]:
+        res.failures.append(f"HBM read {res.hbm['read_gbps']:.0f} GB/s below "
+                            f"{th.min_read_frac:.0%} of {MI355X_HBM_ACHIEVABLE_GBPS:.0f}")
+    if res.mfma["bf16"]["tflops"] < fl["bf16"]:
+        res.failures.append(f"bf16 MFMA {res.mfma['bf16']['tflops']:.0f} TF below "
+                            f"{th.min_bf16_frac:.0%} of dense peak")
+    if res.mfma["fp8"]["tflops"] < fl["fp8"]:
+        res.failures.append(f"fp8 MFMA {res.mfma['fp8']['tflops']:.0f} TF below "
+                            f"{th.min_fp8_frac:.0%} of dense peak")
+    for dtype, g, frac in (("bf16", res.gemm, th.min_gemm_frac), ("fp8", res.gemm_fp8, th.min_gemm_fp8_frac)):
+        name = "GEMM" if dtype == "bf16" else "fp8 GEMM"
+        bad = first_bad.get(dtype)
+        if bad is not None:  # a mismatch in ANY run fails the GPU
+            res.failures.append(f"{name} checksum mismatch: {int(bad['bad_rows'])} rows / "
+                                f"{int(bad['bad_columns'])} columns (first at row {int(bad['first_bad_row'])}, "
+                                f"column {int(bad['first_bad_column'])})")
+        if g["tflops"] < fl[f"gemm_{dtype}"]:
+            res.failures.append(f"{name} {g['tflops']:.0f} TF below {frac:.0%} of dense {dtype} peak")
+    if res.memtest["errors"]:
+        res.failures.append(f"memtest: {res.memtest['errors']} mismatching words")
+    return res
+
+
+def _burnin_child(dev: int, level: str, th: Thresholds, timeout: float = 900.0) -> BurninResult:
+    """:func:`run_burnin` in a ``gpu-burnin --burnin-child`` process (see above): the span
+    memtest's memory is released by the child after its verdict (joined by :func:`wait_frees`)."""
+    from . import gemm
+
+    hbm_bytes, hbm_iters, mfma_iters, mt_bytes, mt_passes = LEVELS[level]
+    m, n, k, reps = gemm.SCREEN_SIZES[level]
+    fl = _floors(th)
+    exe = _burnin_exe()
+    _lib().tkp_wait_frees()
+    _wait_span_children(dev)  # this device's previous span is released before this one allocates
+    argv = [exe, "--burnin-child", "--device", str(int(dev)), "--hbm-bytes", str(hbm_bytes),
+            "--hbm-iters", str(hbm_iters), "--mfma-iters", str(mfma_iters), "--gemm", f"{m},{n},{k},{reps}",
+            "--memtest-bytes", str(mt_bytes), "--memtest-passes", str(mt_passes),
+            "--span-headroom", str(4 << 30), "--span-chunk", str(SPAN_CHILD_CHUNK),
+            "--min-read-gbps", f"{fl['read']:.3f}", "--min-bf16-tflops", f"{fl['bf16']:.3f}",
+            "--min-fp8-tflops", f"{fl['fp8']:.3f}", "--min-gemm-tflops", f"{fl['gemm_bf16']:.3f}",
+            "--min-gemm-fp8-tflops", f"{fl['gemm_fp8']:.3f}"]
+    doc, process_ms = _child_verdict(argv, dev, timeout, "burn-in")
+    if not doc.get("ok"):
+        raise ProbeError(f"burn-in (gpu-burnin --burnin-child): {doc.get('error', 'failed')}")
+    try:
+        i = doc["info"]
+        info = DeviceInfo(index=dev, name=str(i["name"]), arch=str(i["arch"]), compute_units=int(i["compute_units"]),
+                          wavefront_size=int(i["wavefront_size"]), clock_mhz=int(i["clock_khz"]) / 1000.0,
+                          total_mem_gib=int(i["total_mem"]) / 2 ** 30, free_mem_gib=int(i["free_mem"]) / 2 ** 30,
+                          l2_bytes=int(i["l2_bytes"]),
+                          pci_bus_id=f"{int(i['pci_domain']):04x}:{int(i['pci_bus']):02x}:{int(i['pci_device']):02x}.0")
+        res = BurninResult(info, level, hbm={k2: float(v) for k2, v in doc["hbm"].items()},
+                           mfma={"bf16": dict(doc["bf16"]), "fp8": dict(doc["fp8"])},
+                           gemm=dict(doc["gemm"], m=m, n=n, k=k, dtype="bf16"),
+                           gemm_fp8=dict(doc["gemm_fp8"], m=m, n=n, k=k, dtype="fp8"),
+                           memtest=dict(doc["memtest"], free_ms=0.0, process_ms=process_ms),
+                           remeasured=list(doc.get("remeasured") or []),
+                           phase_ms=dict(doc.get("phase_ms") or {}))
+        for g in (res.gemm, res.gemm_fp8):
+            g["ok"] = not (g["bad_columns"] or g["bad_rows"])
+        res.memtest["errors"] = int(res.memtest["errors"])
+        res.phase_ms["process"] = process_ms
+        return _judge(res, th, {"bf16": doc.get("gemm_first_bad"), "fp8": doc.get("gemm_fp8_first_bad")})
+    except (KeyError, TypeError, ValueError) as exc:
+        raise ProbeError(f"burn-in: {exe} gave no burn-in verdict ({type(exc).__name__}: {exc})") from None
+
+
 def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] = None) -> BurninResult:
     th = thresholds or Thresholds()
+    # partitions of one HBM pool (mem_share < 1) burn in in-process: they share the pool
+    if level != "off" and _BURNIN_PROCESS and th.mem_share >= 1.0:
+        try:
+            return _burnin_child(dev, level, th)
+        except native.NativeUnavailable:
+            pass  # no usable gpu-burnin here: the same burn-in in this process
     info = device_info(dev)
     res = BurninResult(info, level)
     if level == "off":
         return res
     hbm_bytes, hbm_iters, mfma_iters, mt_bytes, mt_passes = LEVELS[level]
-    if th.require_gfx950 and not info.is_gfx950:
-        res.failures.append(f"arch {info.arch} is not gfx950")
-    if info.compute_units < th.min_cus:
-        res.failures.append(f"{info.compute_units} CUs < {th.min_cus}")
     # Throughput gates are re-measured (best of up to REMEASURE + 1 runs) before they fail
     # a node: a short kernel that overlapped other GPU work on the node (a previous
     # communicator's teardown, another process) reads low once; a slow GPU reads low every
@@ -486,30 +607,20 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
                 r = again
         return r
 
+    fl = _floors(th)
     with _phase(res, "hbm", dev):
-        floor = th.min_read_frac * MI355X_HBM_ACHIEVABLE_GBPS * th.share
-        res.hbm = best(lambda: hbm_bandwidth(dev, hbm_bytes, hbm_iters), lambda r: r["read_gbps"], floor, "hbm")
-    if res.hbm["read_gbps"] < floor:
-        res.failures.append(f"HBM read {res.hbm['read_gbps']:.0f} GB/s below "
-                            f"{th.min_read_frac:.0%} of {MI355X_HBM_ACHIEVABLE_GBPS:.0f}")
+        res.hbm = best(lambda: hbm_bandwidth(dev, hbm_bytes, hbm_iters), lambda r: r["read_gbps"], fl["read"], "hbm")
     with _phase(res, "mfma_bf16", dev):
-        res.mfma["bf16"] = best(lambda: mfma_peak(dev, "bf16", mfma_iters), lambda r: r["tflops"],
-                                th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS * th.share, "mfma_bf16")
+        res.mfma["bf16"] = best(lambda: mfma_peak(dev, "bf16", mfma_iters), lambda r: r["tflops"], fl["bf16"],
+                                "mfma_bf16")
     with _phase(res, "mfma_fp8", dev):
-        res.mfma["fp8"] = best(lambda: mfma_peak(dev, "fp8", mfma_iters // 2), lambda r: r["tflops"],
-                               th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS * th.share, "mfma_fp8")
-    if res.mfma["bf16"]["tflops"] < th.min_bf16_frac * MI355X_BF16_DENSE_TFLOPS * th.share:
-        res.failures.append(f"bf16 MFMA {res.mfma['bf16']['tflops']:.0f} TF below "
-                            f"{th.min_bf16_frac:.0%} of dense peak")
-    if res.mfma["fp8"]["tflops"] < th.min_fp8_frac * MI355X_FP8_DENSE_TFLOPS * th.share:
-        res.failures.append(f"fp8 MFMA {res.mfma['fp8']['tflops']:.0f} TF below "
-                            f"{th.min_fp8_frac:.0%} of dense peak")
+        res.mfma["fp8"] = best(lambda: mfma_peak(dev, "fp8", mfma_iters // 2), lambda r: r["tflops"], fl["fp8"],
+                               "mfma_fp8")
     from . import gemm
 
     m, n, k, reps = gemm.SCREEN_SIZES[level]
-    for dtype, peak, frac in (("bf16", MI355X_BF16_DENSE_TFLOPS, th.min_gemm_frac),
-                              ("fp8", MI355X_FP8_DENSE_TFLOPS, th.min_gemm_fp8_frac)):
-        name = "GEMM" if dtype == "bf16" else "fp8 GEMM"
+    first_bad: Dict[str, Optional[Dict[str, Any]]] = {}
+    for dtype in ("bf16", "fp8"):
         runs = []
 
         def screen_once(dtype=dtype, runs=runs):
@@ -517,19 +628,14 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
             runs.append(g)
             return g
 
-        peak = peak * th.share
         with _phase(res, f"gemm_{dtype}", dev):
-            g = best(screen_once, lambda r: r.tflops, frac * peak, f"gemm_{dtype}")
+            g = best(screen_once, lambda r: r.tflops, fl[f"gemm_{dtype}"], f"gemm_{dtype}")
         if dtype == "bf16":
             res.gemm = g.to_json()
         else:
             res.gemm_fp8 = g.to_json()
         bad = next((r for r in runs if not r.ok), None)  # a mismatch in ANY run fails the GPU
-        if bad is not None:
-            res.failures.append(f"{name} checksum mismatch: {bad.bad_rows} rows / {bad.bad_columns} columns "
-                                f"(first at row {bad.first_bad_row}, column {bad.first_bad_column})")
-        if g.tflops < frac * peak:
-            res.failures.append(f"{name} {g.tflops:.0f} TF below {frac:.0%} of dense {dtype} peak")
+        first_bad[dtype] = bad.to_json() if bad is not None else None
     with _phase(res, "memtest", dev):
         if mt_bytes:
             res.memtest = memtest(dev, mt_bytes, mt_passes)
@@ -543,9 +649,7 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
             res.memtest = _span(dev, span_bytes, mt_passes)
         else:
             res.memtest = _span(dev, 0, mt_passes)
-    if res.memtest["errors"]:
-        res.failures.append(f"memtest: {res.memtest['errors']} mismatching words")
-    return res
+    return _judge(res, th, first_bad)
 
 
 def prealloc_scratch(dev: int, level: str = "quick") -> int:
