@@ -1,8 +1,9 @@
 """End-to-end MI355X bring-up on the real GPU (``pytest -m gpu``).
 
 A bare-metal ``create cluster`` through the DirectExecutor whose worker agent
-runs the native GPU steps for real: amd_smi topology labels, quick burn-in
-(HBM/MFMA/memtest kernels), then the readiness waiter's RCCL gate.
+runs the native GPU steps for real: amd_smi topology labels, the default (full)
+burn-in (HBM/MFMA/GEMM screens and a memtest of every free byte of HBM), then the
+readiness waiter's RCCL gate.
 """
 
 import json
@@ -55,6 +56,20 @@ def test_real_gpu_bringup(tmp_path):
         hist = w.history[-1]
         burn = [s for s in hist["steps"] if s["name"] == "gpu_burnin"][0]
         assert burn["ok"] and burn["detail"]["0"]["ok"], burn
+        # the product default is the full burn-in: every free byte of HBM memtested, and the
+        # node's labels say so (>= 300 GB of the 288 GiB card when the GPU is one SPX/NPS1 device)
+        assert labels["amd.com/gpu.burnin"] == "passed" and labels["amd.com/gpu.burnin-level"] == "full"
+        tested_gib = int(labels["amd.com/gpu.burnin-hbm-tested-gib"])
+        if (labels.get("amd.com/gpu.compute-partition", "spx").lower(),
+                labels.get("amd.com/gpu.memory-partition", "nps1").lower()) == ("spx", "nps1"):
+            assert tested_gib * (1 << 30) >= 300e9, labels
+        else:
+            assert tested_gib >= 16, labels
+        # the gate's verdict: one RCCL all-reduce sweep over the node's GPU, passed
+        rep = ctx.extras["last_readiness"]
+        assert rep.rccl and rep.rccl["ok"] is True and rep.rccl.get("world", 1) == 1, rep.rccl
+        assert "rccl_gate" in rep.phases
+        print(json.dumps({"burnin_ms": burn.get("ms"), "hbm_tested_gib": tested_gib, "rccl": rep.rccl}, default=str))
         assert {n["agentKind"] for n in fake.state.nodes.values()} == {"system-agent"}
         assert "fleet-default/gpu" in fake.state.v2_clusters
     finally:
@@ -149,16 +164,22 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist):
     print(json.dumps({"steps": steps, "rccl_env": rccl}))
 
 
-def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
+@pytest.mark.parametrize("tools_from", ["prebuilt", "node-build"])
+def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path, tools_from):
     """The bare-metal-mi355x-rancher-k8s-host module's host script (what Terraform's
     remote-exec runs), rendered from the module's own templatefile() call for concrete
-    module inputs (terraform/plan.py) and run on the box: it builds the native tools from
-    the shipped sources with hipcc/g++ on the node, then burn-in, labels, RCCL env and the
-    RKE2 join.  Paths relocated under tmp_path; sudo/curl/docker/hostnamectl/usermod/lsmod
-    stubbed (the stub curl serves an installer that records its arguments)."""
+    module inputs (terraform/plan.py) and run on the box: the node tools, then burn-in,
+    labels, RCCL env and the RKE2 join.  ``prebuilt``: the CLI's staged gfx950 binaries
+    (node/tools.py) are installed -- hipcc is never called, even on a re-run -- and the
+    tool step's time is printed; ``node-build``: nothing staged, the node builds them from
+    the shipped sources with hipcc/g++.  Paths relocated under tmp_path;
+    sudo/curl/docker/hostnamectl/usermod/lsmod stubbed (the stub curl serves an installer
+    that records its arguments)."""
     import os
+    import re
     import subprocess
 
+    from triton_kubernetes_amd.node import tools as node_tools
     from triton_kubernetes_amd.ops.build import CSRC
     from triton_kubernetes_amd.parallel.rccl_env import parse_env_file
     from triton_kubernetes_amd.terraform.generate import MODULES_DIR
@@ -171,14 +192,20 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     planned = plan_module(os.path.join(MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host"), inputs, check_files=False)
     assert planned.ok, planned.errors
     (rendered,) = planned.rendered["install_mi355x_node.sh.tftpl"]
-    tools, etc = tmp_path / "tools", tmp_path / "etc"
+    tools, etc, prebuilt = tmp_path / "tools", tmp_path / "etc", tmp_path / "prebuilt"
+    prebuilt.mkdir()
+    if tools_from == "prebuilt":
+        assert set(node_tools.stage(str(prebuilt)).values()) == {"prebuilt"}
     script = (rendered.replace("/opt/triton-kubernetes/bin", str(tools))
-              .replace("/opt/triton-kubernetes/src", CSRC).replace("/etc/", f"{etc}/")
-              .replace("/var/lib/triton-kubernetes", str(tmp_path / "var")))
+              .replace("/opt/triton-kubernetes/src", CSRC).replace(node_tools.PREBUILT_DIR, str(prebuilt))
+              .replace("/etc/", f"{etc}/").replace("/var/lib/triton-kubernetes", str(tmp_path / "var")))
     bindir = tmp_path / "bin"
     bindir.mkdir()
     log = tmp_path / "calls.log"
     _stub(bindir, "sudo", 'exec "$@"')
+    hipcc_log = tmp_path / "hipcc.log"
+    _stub(bindir, "hipcc", f'echo "hipcc $*" >> {hipcc_log}; exec /opt/rocm/bin/hipcc "$@"')
+    script = script.replace("$R/bin/hipcc", "hipcc")  # the node's compiler: the counting stub
     for name in ("docker", "hostnamectl", "usermod"):
         _stub(bindir, name, f'echo "{name} $*" >> {log}')
     _stub(bindir, "curl", CURL_STUB.format(log=log))
@@ -187,7 +214,17 @@ def test_terraform_mi355x_host_script_runs_on_mi355x(tmp_path):
     proc = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=280)
     assert proc.returncode == 0, proc.stderr[-3000:]
     for exe in ("amdgpu-topo-labeller", "gpu-burnin", "rccl-ready"):
-        assert os.access(tools / exe, os.X_OK), exe  # built on the node from the shipped sources
+        assert os.access(tools / exe, os.X_OK), exe
+    tool_ms = int(re.search(r"node tools: (\d+) ms", proc.stdout).group(1))
+    hipcc_calls = hipcc_log.read_text().splitlines() if hipcc_log.exists() else []
+    print(json.dumps({"tools_from": tools_from, "node_tools_ms": tool_ms, "hipcc_calls": len(hipcc_calls)}))
+    if tools_from == "prebuilt":
+        assert hipcc_calls == [] and proc.stdout.count("prebuilt binary installed") == 3
+        again = subprocess.run(["bash", "-s"], input=script, capture_output=True, text=True, env=env, timeout=280)
+        assert again.returncode == 0, again.stderr[-3000:]
+        assert not hipcc_log.exists() and again.stdout.count("installed copy is current") == 3
+    else:
+        assert len(hipcc_calls) == 2 and proc.stdout.count("building with") == 3
     # default (rccl_slim off): the node's rccl-ready runs on the installed /opt/rocm RCCL
     assert not (tools / "rccl-ready-slim").exists()
     dyn = subprocess.run(["readelf", "-d", str(tools / "rccl-ready")], capture_output=True, text=True).stdout
@@ -263,3 +300,59 @@ def test_node_agent_exec_mode_on_mi355x(tmp_path, monkeypatch, dist):
     assert "--label amd.com/gpu.count=1" in calls
     assert (tmp_path / "root/etc/rccl/rccl.env").read_text().count("NCCL_DEBUG") == 1
     print(json.dumps({s["name"]: round(s["ms"], 2) for s in res["steps"]}))
+
+
+def test_exec_agent_rke2_teardown_then_another_cluster_on_mi355x(tmp_path, monkeypatch):
+    """Destroy-time host teardown on the box (node/cleanup.py): an exec-mode agent joins
+    cluster A through the fake's RKE2 installer (which models the host under TK_HOST_ROOT:
+    connection info, RKE2 state and the vendor uninstallers, rancher/fake/hostsim.py); a
+    join to cluster B is refused while A's install is there; ``/v1/cleanup`` runs the
+    uninstallers at their fixed paths and removes the state; then B's join succeeds, with
+    the GPU steps re-run on the card each time."""
+    import os
+
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.parallel.transport import AgentTransport, HostRef
+    from triton_kubernetes_amd.rancher.fake import FakeRancher, hostsim
+
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    log = tmp_path / "calls.log"
+    _stub(bindir, "hostnamectl", f'echo "hostnamectl $*" >> {log}')
+    root = tmp_path / "root"
+    monkeypatch.setenv("PATH", f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
+    monkeypatch.setenv("TK_FAKE_SYSTEM_AGENT_LOG", str(log))
+    monkeypatch.setenv("TK_HOST_ROOT", str(root))  # the fake installer models this host
+    fake = FakeRancher().start()
+    agent = NodeAgent(name="w-teardown", mode="exec", devices=[0], token="exec-token-123456", root=str(root))
+    url = agent.serve()
+    transport, ref = AgentTransport(token="exec-token-123456"), HostRef("agent+" + url)
+    cfg = {"hostname": "gpu-td-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
+           "gpu_burnin": "quick", "k8s_distribution": "rke2"}
+    try:
+        cid_a, tok_a, ck_a = fake.registration("a", "rke2")
+        first = transport.run_plan(ref, build_host_plan(cfg, fake.url, tok_a, ck_a, mi355x=True))
+        assert first["ok"], first
+        assert (root / hostsim.CONNECTION_INFO.lstrip("/")).exists()
+        cid_b, tok_b, ck_b = fake.registration("b", "rke2")
+        plan_b = build_host_plan(cfg, fake.url, tok_b, ck_b, mi355x=True)
+        refused = transport.run_plan(ref, plan_b)
+        assert not refused["ok"] and "another cluster" in json.dumps(refused), refused
+        rep = transport.cleanup_host(ref)
+        assert rep["ok"], rep
+        ran = [a["what"] for a in rep["actions"] if a.get("status") == "ok"]
+        assert any(w.endswith("rke2-uninstall.sh") for w in ran), rep
+        assert any(w.endswith("rancher-system-agent-uninstall.sh") for w in ran), rep
+        assert not (root / hostsim.CONNECTION_INFO.lstrip("/")).exists()
+        assert not (root / "var/lib/rancher").exists()
+        second = transport.run_plan(ref, plan_b)
+        assert second["ok"], second
+        (node,) = fake.k8s_nodes(cid_b)
+        assert node["metadata"]["labels"]["amd.com/gpu.product-name"] == "MI355X"
+        burn = [s for s in second["steps"] if s["name"] == "gpu_burnin"][0]
+        assert burn["ok"], burn
+    finally:
+        agent.stop()
+        fake.stop()
+    print(json.dumps({"cleanup_ms": rep.get("ms"), "actions": rep["actions"]}))

@@ -100,6 +100,9 @@ RANCHER_CA_OUTPUT = "tk_rancher_ca_certs"
 # the random first-login password (rancher/bootstrap_secret.py), a sensitive root variable
 # rendered into the manager modules' rancher_bootstrap_password
 BOOTSTRAP_VAR = "tk_rancher_bootstrap_password"
+# the staged prebuilt MI355X node tools (node/tools.py), uploaded by the MI355X host modules
+PREBUILT_VAR = "tk_prebuilt_tools"
+PREBUILT_SUBDIR = "tk-prebuilt-tools"
 
 
 def _backend_kind(doc: Dict) -> str:
@@ -141,7 +144,8 @@ def resolve_sources(doc: Dict) -> Dict:
 
 
 def render(state: State, version: Tuple[int, int, int], backend: Optional[Backend] = None,
-           known_hosts: str = "", rancher_ca: str = "", bootstrap_password: str = "") -> Rendered:
+           known_hosts: str = "", rancher_ca: str = "", bootstrap_password: str = "",
+           prebuilt_tools: str = "") -> Rendered:
     """The document Terraform sees (see module docstring).
 
     With ``backend`` the backend block is this operator's (``state_terraform_config``),
@@ -152,7 +156,8 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
     ``bastion_host_key`` of each pinned host).  ``rancher_ca``: its pinned Rancher CA
     (``tk_rancher_ca`` of the cluster and add-on modules).  ``bootstrap_password``: the
     random first-login password (``rancher_bootstrap_password`` of a manager module that
-    does not set one; a sensitive root variable)."""
+    does not set one; a sensitive root variable).  ``prebuilt_tools``: the directory of staged
+    node tools (``tk_prebuilt_tools`` of the MI355X host modules)."""
     doc = resolve_sources(state.doc)
     kind = _backend_kind(doc)
     if backend is not None and kind:
@@ -171,7 +176,7 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
             local = local_module_dir(str(mod.get("source", "")))
             declared = declared_variables(local) if local else frozenset()
             for var, default in ((OPERATION_VAR, "apply"), (KNOWN_HOSTS_VAR, known_hosts),
-                                 (RANCHER_CA_VAR, rancher_ca)):
+                                 (RANCHER_CA_VAR, rancher_ca), (PREBUILT_VAR, prebuilt_tools)):
                 if var in declared and var not in mod:
                     mod[var] = f"${{var.{var}}}"
                     root_vars[var] = default
@@ -202,6 +207,15 @@ def render(state: State, version: Tuple[int, int, int], backend: Optional[Backen
     return Rendered(dumps_go(doc), managed, kind, OPERATION_VAR in root_vars)
 
 
+def _takes(state: State, var: str) -> bool:
+    """Some module of ``state`` declares ``var`` and does not set it itself."""
+    for mod in (resolve_sources(state.doc).get("module") or {}).values():
+        local = local_module_dir(str(mod.get("source", "")))
+        if local and var in declared_variables(local) and var not in mod:
+            return True
+    return False
+
+
 def render_document(state: State, version: Tuple[int, int, int]) -> bytes:
     return render(state, version).body
 
@@ -218,6 +232,7 @@ class TerraformExecutor(Executor):
         version: Optional[Tuple[int, int, int]] = None,
         keep_workdir: bool = False,
         ca_file: str = "",
+        stage_tools: bool = True,
     ):
         self.binary = binary
         self.parallelism = parallelism
@@ -231,6 +246,9 @@ class TerraformExecutor(Executor):
         # the manager's pinned Rancher CA (rancher/trust.py); ca_file re-pins
         self.trust = None
         self.ca_file = ca_file
+        # stage the prebuilt MI355X node tools for the host modules that upload them
+        self.stage_tools = stage_tools
+        self.last_staged: Dict[str, str] = {}
 
     # --- helpers -------------------------------------------------------------------------
     def version(self) -> Tuple[int, int, int]:
@@ -246,10 +264,12 @@ class TerraformExecutor(Executor):
         run_shell_command(self._opts(workdir), self.binary, *args)
 
     @contextlib.contextmanager
-    def workdir(self, state: State, backend: Optional[Backend] = None, write_back: bool = False) -> Iterator[str]:
+    def workdir(self, state: State, backend: Optional[Backend] = None, write_back: bool = False,
+                stage: bool = False) -> Iterator[str]:
         """Temp dir with the rendered document, initialised.  With CLI-managed state the
         tfstate comes from ``backend`` first and (``write_back``) goes back to it after the
-        body, under ``backend.lock``."""
+        body, under ``backend.lock``.  ``stage`` (apply): the prebuilt node tools go into the
+        dir for the MI355X host modules to upload (``node/tools.py``)."""
         version = self.version()
         check_module_versions(state, version)
         keys = self.host_keys = HostKeys(backend, state.name) if backend is not None else None
@@ -267,14 +287,19 @@ class TerraformExecutor(Executor):
                 if src else None
             if local and "rancher_bootstrap_password" in declared_variables(local):
                 boot = bootstrap_secret.ensure(backend, state.name)
-        rendered = render(state, version, backend, keys.text() if keys is not None else "", ca, boot)
-        self.last_rendered = rendered
-        if rendered.managed_state and backend is None:
-            raise ExecutorError(f"the {rendered.backend_kind} state backend needs the CLI to carry terraform.tfstate")
         tmp = tempfile.mkdtemp(prefix="triton-kubernetes-")
         self.last_workdir = tmp
         keep = self.keep_workdir
         try:
+            prebuilt = ""
+            if stage and version >= (0, 12, 0) and self.stage_tools and _takes(state, PREBUILT_VAR):
+                from ..node import tools
+                prebuilt = os.path.join(tmp, PREBUILT_SUBDIR)
+                self.last_staged = tools.stage(prebuilt)
+            rendered = render(state, version, backend, keys.text() if keys is not None else "", ca, boot, prebuilt)
+            self.last_rendered = rendered
+            if rendered.managed_state and backend is None:
+                raise ExecutorError(f"the {rendered.backend_kind} state backend needs the CLI to carry terraform.tfstate")
             with open(os.path.join(tmp, "main.tf.json"), "wb") as fh:
                 fh.write(rendered.body)
             if not rendered.managed_state:
@@ -309,7 +334,7 @@ class TerraformExecutor(Executor):
 
     # --- Executor API ---------------------------------------------------------------------
     def apply(self, state: State, backend: Backend) -> None:
-        with self.workdir(state, backend, write_back=True) as wd:
+        with self.workdir(state, backend, write_back=True, stage=True) as wd:
             args: List[str] = ["apply", "-auto-approve", "-input=false"]
             if self.parallelism:
                 args.append(f"-parallelism={self.parallelism}")

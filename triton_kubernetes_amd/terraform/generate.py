@@ -32,6 +32,7 @@ from typing import Any, Dict, List, Optional, Sequence, Tuple
 from .. import sizing, versions
 from ..parallel import rccl_env
 from ..node.cleanup import cleanup_script
+from ..node.tools import PREBUILT_DIR, SOURCES_DIR
 from . import scripts
 from .catalog import MODULES_DIR
 
@@ -421,6 +422,12 @@ data "external" "rancher_api_key" {{
 '''
 
 
+# the MI355X host module's prebuilt node tools (node/tools.py), staged by the CLI
+PREBUILT_VAR = "tk_prebuilt_tools"
+PREBUILT_README = """The CLI uploads its prebuilt gfx950 node tools from a staging directory it passes as
+tk_prebuilt_tools; this placeholder is uploaded when none is passed.  The node then builds the
+tools from the shipped sources (files/src) with hipcc.  See triton_kubernetes_amd/node/tools.py.
+"""
 NODE_CLEANUP_VAR = Var("node_cleanup", True,
                        "on destroy, take the host out of its cluster: uninstall rancher-system-agent and RKE2 (or "
                        "the RKE1 containers) and remove their state, keeping the node tools and the container "
@@ -1380,22 +1387,30 @@ resource "terraform_data" "install_rancher_agent" {{
         Var("rccl_slim", "off",
             "on: build a single-target (gfx950) copy of the node's librccl for faster cold communicator init, "
             "verify it with a one-rank all-reduce, and run rccl-ready on it while it matches the installed "
-            "librccl (a modified vendor binary: off by default)")],
+            "librccl (a modified vendor binary: off by default)"),
+        Var(PREBUILT_VAR, "",
+            "directory of prebuilt gfx950 node tools, each with its <tool>.sha256 source stamp, that the CLI "
+            "stages (node/tools.py); empty: none uploaded, the node builds the tools with hipcc")],
         ROLE_LOCAL + f'''
 
 locals {{
   rccl_env_file = join("\\n", [for k in sort(keys(var.rccl_env)) : "${{k}}=\\"${{var.rccl_env[k]}}\\""])
+  prebuilt_tools = var.{PREBUILT_VAR} != "" ? var.{PREBUILT_VAR} : "${{path.module}}/files/prebuilt"
 }}
 
 resource "terraform_data" "install_mi355x_node" {{
   triggers_replace = [var.host]
 {_connection("var.host", "var.ssh_user", "var.key_path", "var.bastion_host", pinned=True)}
   provisioner "remote-exec" {{
-    inline = ["sudo mkdir -p /opt/triton-kubernetes/src && sudo chown $(id -un) /opt/triton-kubernetes/src"]
+    inline = ["sudo mkdir -p {SOURCES_DIR} {PREBUILT_DIR} && sudo chown $(id -un) {SOURCES_DIR} {PREBUILT_DIR} && rm -rf {PREBUILT_DIR}/*"]
   }}
   provisioner "file" {{
     source      = "${{path.module}}/files/src/"
-    destination = "/opt/triton-kubernetes/src"
+    destination = "{SOURCES_DIR}"
+  }}
+  provisioner "file" {{
+    source      = "${{local.prebuilt_tools}}/"
+    destination = "{PREBUILT_DIR}"
   }}
   provisioner "remote-exec" {{
     inline = [templatefile("${{path.module}}/files/install_mi355x_node.sh.tftpl", {{
@@ -1445,7 +1460,7 @@ data "external" "gpu_labels" {{
 ''', [("gpu_node_labels", "data.external.gpu_labels.result.labels", False),
           ("tk_ssh_known_hosts", "data.external.gpu_labels.result.known_hosts", False)],
         {"install_mi355x_node.sh.tftpl": scripts.INSTALL_MI355X_NODE, "read_gpu_labels.sh": scripts.READ_REMOTE_LABELS,
-         "cleanup_host.sh": cleanup_script()},
+         "cleanup_host.sh": cleanup_script(), "prebuilt/README": PREBUILT_README},
         {"src/tk_topo.cpp": os.path.join(CSRC, "tk_topo.cpp"),
          "src/tk_gpu_probe.hip": os.path.join(CSRC, "tk_gpu_probe.hip"),
          "src/tk_gemm_screen.hip": os.path.join(CSRC, "tk_gemm_screen.hip"),

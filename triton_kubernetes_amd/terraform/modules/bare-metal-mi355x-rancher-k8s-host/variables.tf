@@ -339,3 +339,9 @@ variable "rccl_slim" {
     error_message = "rccl_slim must be on or off."
   }
 }
+
+variable "tk_prebuilt_tools" {
+  description = "directory of prebuilt gfx950 node tools, each with its <tool>.sha256 source stamp, that the CLI stages (node/tools.py); empty: none uploaded, the node builds the tools with hipcc"
+  type        = string
+  default     = ""
+}

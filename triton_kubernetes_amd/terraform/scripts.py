@@ -10,6 +10,7 @@ templates, and they fix the reference quirks Q10
 from ..node.hosttune import shell_check as _host_tuning_check
 from ..parallel.hostkeys import GO_HOSTKEY_ALGORITHMS
 from ..node.metrics import textfile_script as _metrics_textfile
+from ..node.tools import NODE_TOOLS_FN, PREBUILT_DIR
 
 # download, verify (when docker_install_sha256 is set), run — no `curl | sh` of an unchecked stream
 DOCKER_INSTALL = r"""if ! command -v docker >/dev/null 2>&1; then
@@ -477,8 +478,8 @@ TK_SLIM_EOF
 INSTALL_MI355X_NODE = r"""#!/bin/bash
 # MI355X worker bootstrap: ROCm preflight, topology labels (N1), burn-in,
 # RCCL environment + node-level RCCL gate (N2), then the Rancher agent with
-# the GPU labels.  Tools are built on the node from the shipped sources when
-# no prebuilt binary was uploaded.
+# the GPU labels.  Node tools: the CLI's prebuilt gfx950 binaries when their
+# stamp matches the shipped sources (node/tools.py), else built here with hipcc.
 set -euo pipefail
 T=/opt/triton-kubernetes/bin
 S=/opt/triton-kubernetes/src
@@ -498,14 +499,8 @@ for f in /sys/class/drm/renderD*/device/current_compute_partition /sys/class/drm
 done
 sudo usermod -aG video,render "$(id -un)" || true
 ROCM=$${ROCM_PATH:-/opt/rocm}
-build() { # name, compiler, flags...
-  local name=$1; shift
-  # (re)built when missing or older than any shipped source
-  { [ -x "$T/$name" ] && [ -z "$(find "$S/" -newer "$T/$name" -print -quit)" ]; } || sudo "$@" -o "$T/$name"
-}
-build amdgpu-topo-labeller g++ -O2 -std=c++17 -DTK_TOPO_MAIN -DTK_TOPO_AMDSMI -I$ROCM/include $S/tk_topo.cpp -L$ROCM/lib -lamd_smi -Wl,-rpath,$ROCM/lib
-build gpu-burnin $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip
-build rccl-ready $ROCM/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$ROCM/lib -lrccl -Wl,-rpath,$ROCM/lib
+""" + NODE_TOOLS_FN + r"""
+tk_node_tools $T $S """ + PREBUILT_DIR + r""" $ROCM
 RCCL_READY=$T/rccl-ready
 sudo rm -f $T/""" + RCCL_SLIM_ENV + r""" $T/rccl-ready-slim
 %{ if rccl_slim == "on" ~}
