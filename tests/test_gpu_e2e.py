@@ -58,15 +58,17 @@ def test_real_gpu_bringup(tmp_path):
         assert burn["ok"] and burn["detail"]["0"]["ok"], burn
         # the product default is the full burn-in: every free byte of HBM memtested, and the
         # node's labels say so (>= 300 GB of the 288 GiB card when the GPU is one SPX/NPS1 device)
-        assert labels["amd.com/gpu.burnin"] == "passed" and labels["amd.com/gpu.burnin-level"] == "full"
-        tested_gib = int(labels["amd.com/gpu.burnin-hbm-tested-gib"])
+        rep = ctx.extras["last_readiness"]
+        # the labels the node joined with (the topology labels above plus the burn-in's)
+        (joined,) = [d["labels"] for d in rep.nodes.values() if d["labels"].get("amd.com/gpu.present") == "true"]
+        assert joined["amd.com/gpu.burnin"] == "passed" and joined["amd.com/gpu.burnin-level"] == "full", joined
+        tested_gib = int(joined["amd.com/gpu.burnin-hbm-tested-gib"])
         if (labels.get("amd.com/gpu.compute-partition", "spx").lower(),
                 labels.get("amd.com/gpu.memory-partition", "nps1").lower()) == ("spx", "nps1"):
             assert tested_gib * (1 << 30) >= 300e9, labels
         else:
             assert tested_gib >= 16, labels
         # the gate's verdict: one RCCL all-reduce sweep over the node's GPU, passed
-        rep = ctx.extras["last_readiness"]
         assert rep.rccl and rep.rccl["ok"] is True and rep.rccl.get("world", 1) == 1, rep.rccl
         assert "rccl_gate" in rep.phases
         print(json.dumps({"burnin_ms": burn.get("ms"), "hbm_tested_gib": tested_gib, "rccl": rep.rccl}, default=str))
