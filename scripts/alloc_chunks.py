@@ -22,7 +22,7 @@ for chunk in [int(c) for c in (sys.argv[1:] or ["1", "16", "4", "2", "1", "16"])
     s = hbm.settle(cards=cards, floor=floor, quiet_s=3.0)
     floor = s["floor"] if floor is None else min(floor, s["floor"])
     t0 = time.monotonic()
-    out = subprocess.run(["timeout", "-k", "10", "120", os.path.join(ROOT, "scripts/bin/alloc_probe"), "fresh",
+    out = subprocess.run(["timeout", "-k", "10", "120", os.path.join(ROOT, "scripts/native/alloc_probe"), "fresh",
                           str(chunk)], capture_output=True, text=True)
     wall = (time.monotonic() - t0) * 1e3
     if out.returncode != 0:

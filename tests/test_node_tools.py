@@ -204,3 +204,53 @@ def test_terraform_apply_stages_the_tools_for_mi355x_hosts(tmp_path, monkeypatch
     staged.clear()
     with ex.workdir(st, be) as wd:  # destroy / output: nothing staged
         assert not staged
+
+
+def test_machine_image_builds_with_the_same_stamped_function(node, tmp_path):
+    from triton_kubernetes_amd.images import packer
+
+    script = open(os.path.join(packer.FILES_DIR, "build-node-tools.sh")).read()
+    assert tools.NODE_TOOLS_FN in script
+    run, compiles, tmp = node
+    bindir = tmp / "stubs"
+    env = dict(os.environ, PATH=f"{bindir}:{os.environ['PATH']}", TK_SRC=str(tmp / "src"), TK_BIN=str(tmp / "img"),
+               ROCM_PATH=str(tmp / "rocm"))
+    # the image's last line runs the labeller: the stub compiler's output prints "built"
+    proc = subprocess.run(["bash", "-c", script], capture_output=True, text=True, env=env, timeout=60)
+    assert proc.returncode == 0, proc.stderr
+    assert len(compiles()) == 3
+    # a Terraform apply on a node made from that image: every tool is current, nothing compiled
+    _staged(tmp)
+    again = run(tmp / "img")
+    assert again.returncode == 0 and len(compiles()) == 3
+    assert again.stdout.count("installed copy is current") == 3
+
+
+def test_direct_executor_uploads_only_tools_the_host_lacks(tmp_path, monkeypatch):
+    from triton_kubernetes_amd.executor.direct import DirectExecutor
+    from triton_kubernetes_amd.node.plan import TOOLS_DIR
+    from triton_kubernetes_amd.ops import native
+    from triton_kubernetes_amd.parallel.transport import HostRef, RecordingTransport
+
+    host_stamps = {}
+
+    class Host(RecordingTransport):
+        def run_script(self, host, script, timeout=3600):
+            super().run_script(host, script, timeout)
+            if ".stamps/*.sha256" in script:
+                return "".join(f"{n} {s}\n" for n, s in host_stamps.items())
+            if "sudo tee" in script:
+                name = script.split(".stamps/")[1].split(".sha256")[0]
+                host_stamps[name] = script.split("echo ")[1].split(" |")[0]
+            return ""
+
+    monkeypatch.setattr(native, "executable", lambda name: f"/lib/{name}")
+    t = Host()
+    ex = DirectExecutor(transport=t)
+    ref = HostRef("10.0.0.30", "u", "k", "")
+    assert sorted(ex._upload_tools(ref)) == sorted(tools.TOOL_SOURCES)
+    assert sorted(t.files) == sorted(f"{TOOLS_DIR}/{n}" for n in tools.TOOL_SOURCES)
+    assert host_stamps == {n: tools.node_stamp(n) for n in tools.TOOL_SOURCES}
+    assert ex._upload_tools(ref) == []  # re-apply: nothing sent
+    host_stamps["gpu-burnin"] = "0" * 64  # built from other sources
+    assert ex._upload_tools(ref) == ["gpu-burnin"]

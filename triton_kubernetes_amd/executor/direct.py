@@ -523,11 +523,27 @@ class DirectExecutor(Executor):
             outs["gpu_node_labels"] = json.dumps(result.get("labels", {}), sort_keys=True)
         return outs, result
 
-    def _upload_tools(self, ref: HostRef) -> None:
+    def _upload_tools(self, ref: HostRef) -> List[str]:
+        """The prebuilt gfx950 node tools, each with its source stamp (``node/tools.py``,
+        the same stamp the Terraform host module and the machine image install): a tool the
+        host already has from these sources is not uploaded again.  Returns what was sent."""
+        from ..node import tools
         from ..ops.native import executable
 
-        for tool in ("amdgpu-topo-labeller", "gpu-burnin", "rccl-ready"):
+        have: Dict[str, str] = {}
+        for line in (self.transport.run_script(ref, tools.REMOTE_STAMPS.format(tools=TOOLS_DIR)) or "").splitlines():
+            name, _, stamp = line.strip().partition(" ")
+            have[name] = stamp.strip()
+        sent = []
+        for tool in tools.TOOL_SOURCES:
+            want = tools.node_stamp(tool)
+            if have.get(tool) == want:
+                continue
             self.transport.put_file(ref, executable(tool), f"{TOOLS_DIR}/{tool}")
+            self.transport.run_script(ref, f"sudo mkdir -p {TOOLS_DIR}/.stamps && echo {want} | "
+                                           f"sudo tee {TOOLS_DIR}/.stamps/{tool}.sha256 >/dev/null\n")
+            sent.append(tool)
+        return sent
 
     # --- addons -------------------------------------------------------------------------------------------
     def _apply_addons(self, cfg: Dict[str, Any],

@@ -1,4 +1,4 @@
-"""The MI355X node tools a Terraform-delivered host installs, shipped prebuilt.
+"""The MI355X node tools, shipped prebuilt and stamped with the sources they come from.
 
 The reference installs no GPU tooling at all (its host modules only run the Rancher agent
 container, ``terraform/modules/bare-metal-rancher-k8s-host/main.tf``).  Here an MI355X host
@@ -19,7 +19,10 @@ the ROCm compiler on production hosts, so:
   naming the tool.
 
 The stamp is over the sources, not mtimes (an upload resets those), so a binary built from
-other sources than the ones shipped is never installed.
+other sources than the ones shipped is never installed.  The other two delivery paths use
+the same stamp: the DirectExecutor uploads a tool over SSH only when the host's stamp for
+it differs (:data:`REMOTE_STAMPS`), and the machine image (``images/files/build-node-tools.sh``)
+builds with this same ``tk_node_tools``, so a node made from the image keeps its tools.
 """
 
 import hashlib
@@ -122,4 +125,12 @@ tk_node_tools() { # <tools dir> <sources dir> <prebuilt dir> <rocm dir>
   return $rc
 }"""
 
-__all__ = ["NODE_TOOLS_FN", "PREBUILT_DIR", "SOURCES_DIR", "TOOL_SOURCES", "node_stamp", "stage"]
+# "<tool> <stamp>" for every node tool installed with a stamp (DirectExecutor uploads)
+REMOTE_STAMPS = """for f in {tools}/.stamps/*.sha256; do
+  n=$(basename "$f" .sha256)
+  [ -f "$f" ] && [ -x "{tools}/$n" ] && echo "$n $(cat "$f")"
+done
+true
+"""
+
+__all__ = ["NODE_TOOLS_FN", "REMOTE_STAMPS", "PREBUILT_DIR", "SOURCES_DIR", "TOOL_SOURCES", "node_stamp", "stage"]
