@@ -372,3 +372,73 @@ def test_partitions_of_one_pool_burn_in_in_process(burnin_child, monkeypatch):
     with pytest.raises(RuntimeError, match="in-process"):
         probe.run_burnin(0, "full", probe.Thresholds.for_partition("cpx", "nps2"))
     assert not called
+
+
+def test_child_releases_its_hbm_only_when_the_hold_says(burnin_child, monkeypatch, tmp_path):
+    """The agent's release hold (node/agent_gate.py:_await_rccl_inits): the child gets
+    --hold-stdin and frees what it tested when its stdin closes, not at its verdict."""
+    import json
+    import sys
+    import threading
+    import time
+
+    exe = tmp_path / "gpu-burnin"
+    released = tmp_path / "released"
+    exe.write_text(f"""#!{sys.executable}
+import os, sys
+open(os.environ["FAKE_CHILD_ARGV"], "w").write(" ".join(sys.argv[1:]))
+print(os.environ["FAKE_CHILD_DOC"], flush=True)
+if "--hold-stdin" in sys.argv:
+    sys.stdin.read()  # until the parent closes the pipe
+open({str(released)!r}, "w").write("freed")
+""")
+    monkeypatch.setenv("FAKE_CHILD_DOC", json.dumps(CHILD_OK))
+    go = threading.Event()
+    probe.set_release_hold(go.wait)
+    try:
+        res = probe.run_burnin(0, "full")
+        assert res.ok
+        argv = burnin_child.read_text().split()
+        assert "--hold-stdin" in argv and argv[argv.index("--hold-max-ms") + 1] == str(probe.RELEASE_HOLD_MAX_MS)
+        time.sleep(0.3)
+        assert not released.exists()  # verdict in hand, HBM still held
+        go.set()
+        probe.wait_frees()
+        assert released.read_text() == "freed"
+    finally:
+        go.set()
+        probe.set_release_hold(None)
+    released.unlink()
+    assert probe.run_burnin(0, "full").ok  # no hold: released right after the verdict
+    probe.wait_frees()
+    assert released.exists() and "--hold-stdin" not in burnin_child.read_text()
+
+
+def test_agent_release_hold_waits_for_running_rccl_inits(monkeypatch):
+    import time
+
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.ops import rccl
+
+    running = [2]
+
+    def inits():
+        running[0] = max(0, running[0] - 1)
+        return running[0]
+
+    monkeypatch.setattr(rccl, "inits_running", inits)
+    a = NodeAgent(name="h", mode="sim", token="t" * 20)
+    a._await_rccl_inits()
+    assert running[0] == 0
+    monkeypatch.setattr(rccl, "inits_running", lambda: 1)  # an init that never finishes: bounded
+    monkeypatch.setattr(NodeAgent, "RELEASE_HOLD_S", 0.05)
+    t0 = time.monotonic()
+    a._await_rccl_inits()
+    assert time.monotonic() - t0 < 1.0
+
+
+def test_inits_running_is_zero_without_loading_libtk_rccl(monkeypatch):
+    from triton_kubernetes_amd.ops import native, rccl
+
+    monkeypatch.delitem(native._cache, "libtk_rccl.so", raising=False)
+    assert rccl.inits_running() == 0 and "libtk_rccl.so" not in native._cache

@@ -447,7 +447,9 @@ def test_full_span_leaves_other_processes_memory_alone(tmp_path):
 
 def test_full_span_memtests_the_burnin_arena_too(probe):
     """A full burn-in's bandwidth step grows the agent's arena to 2 x 16 GiB; the span
-    memtest frees it first, so that HBM is tested rather than left beside the span."""
+    memtest takes those buffers over and tests them in place (no free of 32 GiB, and no
+    driver clearing of it, just before the span's own allocations), so that HBM is tested
+    rather than left beside the span."""
     probe.set_scratch_cache(True)
     try:
         probe.prealloc_scratch(0, "full")

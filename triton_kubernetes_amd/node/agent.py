@@ -266,6 +266,10 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         # (ops/probe.py:_burnin_child)
         burnin_child = os.environ.get("TK_BURNIN_PROCESS", "1") != "0"
         probe.set_burnin_process(burnin_child)
+        # ...and releases the HBM it tested only once this agent's RCCL communicator inits
+        # are through: the driver's clearing of that release held their device-code load up
+        if os.environ.get("TK_BURNIN_RELEASE_HOLD", "1") != "0":
+            probe.set_release_hold(self._await_rccl_inits)
         # burn-in arena (in-process burn-ins only): resident for the agent's lifetime,
         # released after an idle period
         if os.environ.get("TK_PROBE_SCRATCH_CACHE", "0" if burnin_child else "1") != "0":

@@ -88,6 +88,20 @@ class AgentGateMixin:
             del aborted[k]
         return uid in aborted
 
+    # the longest a burn-in child keeps the HBM it tested for this agent's RCCL inits
+    RELEASE_HOLD_S = 20.0
+
+    def _await_rccl_inits(self) -> None:
+        """Return once no RCCL communicator init of this agent is running, or after
+        :attr:`RELEASE_HOLD_S` (``ops/probe.py:set_release_hold``: a burn-in child's ~300 GB
+        release, which the driver clears for seconds, would hold up the device-code load of
+        an init still running)."""
+        from ..ops import rccl
+
+        deadline = time.monotonic() + self.RELEASE_HOLD_S
+        while rccl.inits_running() > 0 and time.monotonic() < deadline:
+            time.sleep(0.005)
+
     def _gate_devices(self, ndev: int) -> List[int]:
         devs = self.devices or [0]
         if ndev < 1 or ndev > len(devs):

@@ -42,6 +42,8 @@
 #include <string>
 #include <vector>
 #include <utility>
+#include <poll.h>
+
 #include <algorithm>
 #include <vector>
 
@@ -841,10 +843,39 @@ struct SpanHold {
   }
 };
 
+// The arena's idle buffers, handed to a span memtest as chunks of its own: tested in place
+// and released with the span.  Freeing them first instead (the stream pair is 2 x 16 GiB after
+// a full burn-in's bandwidth step) left the driver ~1 s of VRAM clearing that the span's
+// allocations -- and other processes' copies, RCCL's code-object load among them -- waited
+// behind (profiles/round5/README.md).  Returns the bytes adopted.
+static size_t scratch_adopt(int dev, std::vector<uint4*>& chunks, std::vector<size_t>& sizes) {
+  std::lock_guard<std::mutex> lk(g_scr_mu);
+  auto it = g_scr.find(dev);
+  if (it == g_scr.end()) return 0;
+  size_t n = 0;
+  for (auto& s : it->second) {
+    if (s.p && !s.in_use && s.bytes >= sizeof(uint4)) {
+      chunks.push_back(static_cast<uint4*>(s.p));
+      sizes.push_back(s.bytes / sizeof(uint4) * sizeof(uint4));
+      n += s.bytes;
+      s.p = nullptr;
+      s.bytes = 0;
+    }
+  }
+  return n;
+}
+
 extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t headroom, int passes, double* out) {
   tkp_wait_frees();
   CHECK(hipSetDevice(dev));
-  tkp_release_scratch_dev(dev);  // the arena's buffers are part of the span, not beside it
+  // the arena's buffers are part of the span, not beside it: a sized-to-fit span (bytes 0)
+  // tests them in place (the hold owns them from here); an explicit size releases them
+  // first and allocates its own
+  SpanHold hold(dev);
+  std::vector<size_t> sizes;
+  if (bytes == 0) scratch_adopt(dev, hold.chunks, sizes);
+  else tkp_release_scratch_dev(dev);
+  const size_t n_adopted = hold.chunks.size();
   const long alloc_limit = fail_point_value("memtest_span.alloc_limit");
   size_t free_b = 0, total_b = 0;
   CHECK(hipMemGetInfo(&free_b, &total_b));
@@ -853,14 +884,12 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
   if (bytes == 0) bytes = free_b > headroom ? free_b - headroom : 0;
   if (chunk == 0) chunk = 16ull << 30;
   chunk = chunk / sizeof(uint4) * sizeof(uint4);
-  SpanHold hold(dev);
-  std::vector<size_t> sizes;
   const auto t_alloc = std::chrono::steady_clock::now();
   for (size_t done = 0; done < bytes && chunk > 0;) {
     const size_t want = (bytes - done < chunk ? bytes - done : chunk) / sizeof(uint4) * sizeof(uint4);
     if (want == 0) break;
     uint4* p = nullptr;
-    if ((alloc_limit >= 0 && (long)hold.chunks.size() >= alloc_limit) || hipMalloc(&p, want) != hipSuccess) {
+    if ((alloc_limit >= 0 && (long)(hold.chunks.size() - n_adopted) >= alloc_limit) || hipMalloc(&p, want) != hipSuccess) {
       (void)hipGetLastError();
       break;  // fragmentation, or HBM another process took since hipMemGetInfo: test what could be held
     }
@@ -869,6 +898,10 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
     done += want;
   }
   out[4] = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_alloc).count();
+  // adopted buffers last: released after the span's own chunks (the driver clears a small
+  // free without holding other GPU work up for long; the stream pair's 16 GiB go at the end)
+  std::rotate(hold.chunks.begin(), hold.chunks.begin() + n_adopted, hold.chunks.end());
+  std::rotate(sizes.begin(), sizes.begin() + n_adopted, sizes.end());
   if (hold.chunks.empty()) return 0;  // nothing could be held: tested = 0 bytes, no error
   FAILPOINT("memtest_span.after_alloc");
   CHECK(hipMalloc(&hold.err, sizeof(unsigned long long)));
@@ -1293,11 +1326,21 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
 // --burnin-child: one GPU's whole burn-in in its own process, for ops/probe.py:run_burnin
 // in a node agent.  The agent's own HIP runtime is busy beside it (a cluster gate's RCCL
 // communicator starting: loading RCCL's code objects holds the runtime's locks, and the
-// screens' kernel launches waited behind it for 1.5-4 s, profiles/round5/breakdown.md), so
+// screens' kernel launches waited behind it for 1.5-4 s, profiles/round5/README.md), so
 // the screens run here instead.  The parameters and the pass/fail floors come from
 // ops/probe.py (LEVELS, Thresholds): this mode measures -- re-measuring a throughput below
 // its floor, as the agent would -- and reports; the agent judges.  One JSON line as soon as
 // the verdict is known; the span memtest's chunks are released after it.
+// --hold-stdin: after the verdict, keep what the span holds until the parent closes this
+// process's stdin (or writes a line), at most `max_ms`.  The agent releases a burn-in's HBM
+// only once its own RCCL communicator inits are through: the driver's clearing of ~300 GB
+// holds up their copies and allocations (ops/probe.py:set_release_hold).
+static void hold_until_released(bool hold, int max_ms) {
+  if (!hold) return;
+  struct pollfd p = {0, POLLIN, 0};
+  (void)poll(&p, 1, max_ms);  // readable on a line and on EOF (parent closed the pipe or exited)
+}
+
 static void json_escape(const char* in, char* out, size_t cap) {
   size_t o = 0;
   for (; *in && o + 2 < cap; ++in) {
@@ -1311,9 +1354,14 @@ static int burnin_child_main(int argc, char** argv) {
   int dev = 0, hbm_iters = 3, mfma_iters = 2000, gm = 4096, gn = 4096, gk = 4096, greps = 5, passes = 1;
   size_t hbm_bytes = 1ull << 30, mt_bytes = 1ull << 30, headroom = 4ull << 30, chunk = 1ull << 30;
   double min_read = 0, min_bf16 = 0, min_fp8 = 0, min_gemm = 0, min_gemm8 = 0;
+  bool hold = false;
+  int hold_max_ms = 30000;
+  for (int i = 1; i < argc; ++i)
+    if (!strcmp(argv[i], "--hold-stdin")) hold = true;
   for (int i = 1; i + 1 < argc; ++i) {
     const char* a = argv[i];
     if (!strcmp(a, "--device")) dev = atoi(argv[++i]);
+    else if (!strcmp(a, "--hold-max-ms")) hold_max_ms = atoi(argv[++i]);
     else if (!strcmp(a, "--hbm-bytes")) hbm_bytes = strtoull(argv[++i], nullptr, 10);
     else if (!strcmp(a, "--hbm-iters")) hbm_iters = atoi(argv[++i]);
     else if (!strcmp(a, "--mfma-iters")) mfma_iters = atoi(argv[++i]);
@@ -1362,6 +1410,9 @@ static int burnin_child_main(int argc, char** argv) {
   };
   for (int i = 0; i < 2; ++i) for (int j = 0; j < 7; ++j) g[i][j] = gbad[i][j] = (j == 4 || j == 5) ? -1 : 0;
   if (tkp_device_info(dev, &info) != 0) return fail("device_info");
+  // the bandwidth step's buffers stay in the arena: the span memtest then tests them in
+  // place instead of freeing 2 x hbm_bytes just before its own allocations
+  tkp_set_scratch_cache(1);
   auto t = now();
   if (!best("hbm", [&](double* o) { return tkp_hbm_bandwidth(dev, hbm_bytes, hbm_iters, 16, o); }, hbm, 3, min_read, -1))
     return fail("hbm_bandwidth");
@@ -1415,6 +1466,7 @@ static int burnin_child_main(int argc, char** argv) {
          "\"gemm_bf16\":%.1f,\"gemm_fp8\":%.1f,\"memtest\":%.1f}}\n",
          mt[0], mt[1], mt[2], mt[3], mt[4], mt[5], remeasured.c_str(), ph[0], ph[1], ph[2], ph[3], ph[4], ph[5]);
   fflush(stdout);
+  hold_until_released(hold, hold_max_ms);
   for (void* q : g_kept_chunks) (void)hipFree(q);
   g_kept_chunks.clear();
   return 0;
@@ -1434,6 +1486,8 @@ int main(int argc, char** argv) {
   int span_mode = 0;            // --memtest-span [--span-bytes B] [--span-headroom H] [--span-passes P]
   size_t span_bytes = 0, span_headroom = 4ull << 30, span_chunk = 16ull << 30;
   int span_passes = 3;
+  bool hold = false;  // --hold-stdin [--hold-max-ms N]: span mode releases when the parent says
+  int hold_max_ms = 30000;
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
   for (int i = 1; i < argc; ++i) {
@@ -1447,6 +1501,8 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--min-gemm-fp8-tflops") && i + 1 < argc) min_gemm8 = atof(argv[++i]);
     else if (!strcmp(argv[i], "--labels") && i + 1 < argc) labels_path = argv[++i];
     else if (!strcmp(argv[i], "--p2p")) p2p = 1;
+    else if (!strcmp(argv[i], "--hold-stdin")) hold = true;
+    else if (!strcmp(argv[i], "--hold-max-ms") && i + 1 < argc) hold_max_ms = atoi(argv[++i]);
     else if (!strcmp(argv[i], "--min-link-frac") && i + 1 < argc) min_link_frac = atof(argv[++i]);
     else if (!strcmp(argv[i], "--min-link-gbps") && i + 1 < argc) min_link_gbps = atof(argv[++i]);
     else if (!strcmp(argv[i], "--p2p-method") && i + 1 < argc) link_mode = strcmp(argv[++i], "sdma-copy") ? 1 : 0;
@@ -1470,6 +1526,7 @@ int main(int argc, char** argv) {
       printf("{\"ok\":true,\"errors\":%.0f,\"verify_gbps\":%.1f,\"bytes\":%.0f,\"hbm_bytes\":%.0f,"
              "\"alloc_ms\":%.1f,\"test_ms\":%.1f}\n", mt[0], mt[1], mt[2], mt[3], mt[4], mt[5]);
     fflush(stdout);
+    hold_until_released(hold, hold_max_ms);
     for (void* p : g_kept_chunks) (void)hipFree(p);
     g_kept_chunks.clear();
     return rc != 0 ? 2 : (mt[0] != 0.0 ? 1 : 0);
@@ -1496,6 +1553,9 @@ int main(int argc, char** argv) {
   std::vector<int> devs;
   if (all) for (int d = 0; d < n; ++d) devs.push_back(d);
   else devs.push_back(dev);
+  // each GPU's bandwidth buffers stay in its arena and the full span tests them in place
+  // (tkp_memtest_span), rather than freeing 2 x 16 GiB just before the span allocates
+  tkp_set_scratch_cache(1);
   // One device's burn-in, on the calling thread (every probe pins its device per thread;
   // error text is per thread too).
   struct DevResult {

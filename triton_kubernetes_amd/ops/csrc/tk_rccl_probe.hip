@@ -330,6 +330,11 @@ static int g_next_gate = 1;
 // inits released while still waiting for peers (their threads are detached)
 static std::atomic<int> g_abandoned{0};
 extern "C" int tkr_gate_abandoned() { return g_abandoned.load(); }
+// communicator inits still running (begun, not yet ready or failed): a burn-in child that
+// is about to release its HBM waits for these -- the driver's clearing of the release holds
+// up the init's copies and allocations (ops/probe.py:set_release_hold)
+static std::atomic<int> g_inits_running{0};
+extern "C" int tkr_inits_running() { return g_inits_running.load(); }
 
 static Gate* take_gate(int h) {
   std::lock_guard<std::mutex> lk(g_gate_mu);
@@ -395,6 +400,7 @@ static void init_body(Gate* g, ncclUniqueId id) {
     g->init_state = r == 0 ? 1 : -2;
     orphan = g->abandoned;
   }
+  g_inits_running.fetch_sub(1);
   g->cv.notify_all();
   if (orphan) {  // released while initialising: nobody else will touch it
     for (size_t d = 0; d < g->bufs.size(); ++d) { (void)hipSetDevice(g->devices[d]); free_bufs(g->bufs[d]); }
@@ -457,6 +463,7 @@ extern "C" int tkr_gate_begin_ex(const unsigned char* uid128, int world, int ran
   g->prealloc_bytes = prealloc_bytes;
   g->t_begin = std::chrono::steady_clock::now();
   g_teardowns.touch();
+  g_inits_running.fetch_add(1);
   if (blocking) {
     init_body(g, id);
     if (g->init_state < 0) {

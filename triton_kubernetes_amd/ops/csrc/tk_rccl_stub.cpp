@@ -164,6 +164,7 @@ void tkr_set_teardown_quiet_ms(double) {}
 int tkr_teardowns_pending() { return 0; }
 int tkr_drain() { return 0; }
 int tkr_gate_abandoned() { return 0; }
+int tkr_inits_running() { return 0; }  // no device code to load: nothing a release could hold up
 int tkr_gate_pending() {
   std::lock_guard<std::mutex> lk(g_mu);
   return (int)g_gates.size();

@@ -16,7 +16,7 @@ import subprocess
 import threading
 import time
 from dataclasses import asdict, dataclass, field
-from typing import Any, Dict, List, Optional, Sequence, Tuple
+from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 from ..utils.trace import span
 from . import native
@@ -283,14 +283,45 @@ class _ChildUnstartable(native.NativeUnavailable):
     """The ``gpu-burnin`` child could not be started (nothing ran on the GPU)."""
 
 
+# Called (on a thread of its own) before a child releases the HBM it tested; None: release
+# at once.  The node agent waits here for its RCCL communicator inits (node/agent.py): the
+# driver clears a release of ~300 GB for seconds, and an init loading RCCL's device code
+# meanwhile waited behind that clearing (1.8 s -> 3.5 s, profiles/round5/README.md).
+_RELEASE_HOLD: Optional[Callable[[], None]] = None
+RELEASE_HOLD_MAX_MS = 30000  # the child releases by itself after this long
+
+
+def set_release_hold(fn: Optional[Callable[[], None]]) -> None:
+    """``fn`` returns when a burn-in child may release what it holds (see ``_RELEASE_HOLD``)."""
+    global _RELEASE_HOLD
+    _RELEASE_HOLD = fn
+
+
+def _release_after_hold(proc: Any, hold: Callable[[], None]) -> None:
+    try:
+        hold()
+    except Exception:  # noqa: BLE001 - the child must be released whatever the hold did
+        pass
+    finally:
+        try:
+            proc.stdin.close()  # EOF: the child frees and exits
+        except OSError:
+            pass
+
+
 def _child_verdict(argv: List[str], dev: int, timeout: float, what: str) -> Tuple[Dict[str, Any], float]:
     """Start a ``gpu-burnin`` child for ``dev`` and return its JSON verdict (the first JSON
     line it prints) and the ms until then.  The child is registered with the device's span
-    children: it releases what it holds after the verdict, and the next span on the device
-    (and :func:`wait_frees`) waits for it to exit."""
+    children: it releases what it holds after the verdict -- once the release hold says so
+    (:func:`set_release_hold`) -- and the next span on the device (and :func:`wait_frees`)
+    waits for it to exit."""
     t0 = time.perf_counter()
+    hold = _RELEASE_HOLD
+    if hold is not None:
+        argv = list(argv) + ["--hold-stdin", "--hold-max-ms", str(RELEASE_HOLD_MAX_MS)]
     try:
         proc = subprocess.Popen(argv, stdout=subprocess.PIPE, stderr=subprocess.DEVNULL, text=True,
+                                stdin=subprocess.PIPE if hold is not None else subprocess.DEVNULL,
                                 start_new_session=True)
     except OSError as exc:
         raise _ChildUnstartable(f"cannot start {argv[0]}: {exc}") from exc
@@ -326,8 +357,13 @@ def _child_verdict(argv: List[str], dev: int, timeout: float, what: str) -> Tupl
         proc.kill()
         raise ProbeError(f"{what}: unreadable verdict {line[:200]!r}") from exc
     if not isinstance(doc, dict):
+        proc.kill()
         raise ProbeError(f"{what}: unreadable verdict {line[:200]!r}")
-    return doc, round((time.perf_counter() - t0) * 1e3, 1)
+    ms = round((time.perf_counter() - t0) * 1e3, 1)
+    if hold is not None:
+        threading.Thread(target=_release_after_hold, args=(proc, hold), name=f"tk-release-{dev}",
+                         daemon=True).start()
+    return doc, ms
 
 
 def _span_in_process(dev: int, nbytes: int, headroom: int, passes: int, why: str) -> Dict[str, float]:

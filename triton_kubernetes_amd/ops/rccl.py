@@ -212,6 +212,15 @@ def abandoned_inits() -> int:
     return int(_lib().tkr_gate_abandoned())
 
 
+def inits_running() -> int:
+    """Communicator inits of this process still running (0 when libtk_rccl was never loaded:
+    nothing to wait for, and nothing is loaded to find out)."""
+    from . import native
+
+    lib = native._cache.get("libtk_rccl.so")
+    return int(lib.tkr_inits_running()) if lib is not None else 0
+
+
 def exit_now(code: int = 0) -> None:
     """Leave the process without the HIP/RCCL exit teardown, which cannot complete while an
     abandoned init thread is blocked in RCCL's bootstrap.  Flushes stdio first."""
