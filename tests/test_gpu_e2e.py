@@ -92,8 +92,9 @@ def _stub(bindir, name, body):
     p.chmod(0o755)
 
 
-@pytest.mark.parametrize("rccl_slim,dist", [("off", "rke2"), ("on", "rke1")])
-def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist):
+@pytest.mark.parametrize("rccl_slim,dist,burnin", [("off", "rke2", "quick"), ("on", "rke1", "quick"),
+                                                    ("off", "rke2", "full")])
+def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist, burnin):
     """The SSH path's rendered bash bootstrap, run for real on the box: the native tools
     (gpu-burnin, amdgpu-topo-labeller incl. --rccl-env, rccl-ready) copied from ops/lib,
     /etc relocated under tmp_path, and only sudo/docker/curl/systemctl/hostnamectl/usermod/lsmod
@@ -123,7 +124,7 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist):
     _stub(bindir, "lsmod", "echo 'Module Size Used by'; test -c /dev/kfd && echo 'amdgpu 1 0'")
     etc = tmp_path / "etc"
     (etc / "docker").mkdir(parents=True)
-    cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1, "gpu_burnin": "quick",
+    cfg = {"hostname": "gpu-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1, "gpu_burnin": burnin,
            "rccl_env": {"NCCL_DEBUG": "WARN"}, "rccl_slim": rccl_slim, "k8s_distribution": dist}
     plan = build_host_plan(cfg, "https://rancher.example", "regtok", "cafe", mi355x=True)
     script = (plan.render_shell().replace("/etc/", f"{etc}/").replace(TOOLS_DIR, str(tools))
@@ -136,6 +137,9 @@ def test_rendered_shell_bootstrap_runs_on_mi355x(tmp_path, rccl_slim, dist):
     assert all(steps.get(n, {}).get("status") == "ok" for n in plan.step_names()), steps
     burn = json.loads((etc / "triton-kubernetes/gpu-burnin.json").read_text())
     assert burn["ok"] and burn["gpus"] and all(g["ok"] for g in burn["gpus"]), burn
+    assert burn["level"] == burnin
+    if burnin == "full":  # every free byte but the headroom, on the SSH path too
+        assert all(g["memtest_bytes"] >= 0.9 * g["hbm_bytes"] for g in burn["gpus"]), burn
     labels = dict(ln.split("=", 1) for ln in (etc / "triton-kubernetes/gpu-labels").read_text().splitlines())
     assert labels["amd.com/gpu.count"] == "1" and labels["amd.com/gpu.target"] == "gfx950"
     rccl = parse_env_file((etc / "rccl/rccl.env").read_text())

@@ -1561,6 +1561,7 @@ int main(int argc, char** argv) {
   struct DevResult {
     struct tkp_device_info info;
     double hbm[3], bf16[2], fp8[2], mt[7], gm[7], gm8[7];
+    double ph[6];  // ms: hbm, mfma bf16, mfma fp8, gemm bf16, gemm fp8, memtest
     int remeasured;
     bool ok, pass, gemm_ok, gemm8_ok;
     char err[512];
@@ -1584,18 +1585,25 @@ int main(int argc, char** argv) {
       }
       return true;
     };
-    r.ok = tkp_device_info(d, &r.info) == 0 &&
+    auto t = std::chrono::steady_clock::now();
+    auto lap = [&](int i) {  // phase i's wall time, for the verdict's phase_ms
+      const auto n = std::chrono::steady_clock::now();
+      r.ph[i] = std::chrono::duration<double, std::milli>(n - t).count();
+      t = n;
+      return true;
+    };
+    r.ok = tkp_device_info(d, &r.info) == 0 && (t = std::chrono::steady_clock::now(), true) &&
            measure([&](double* o) { return tkp_hbm_bandwidth(d, hbm_bytes, 3, 16, o); }, r.hbm, 3, min_read,
-                   nullptr) &&
+                   nullptr) && lap(0) &&
            measure([&](double* o) { return tkp_mfma_peak(d, 0, mfma_iters, 3, 2, o); }, r.bf16, 2, min_bf16,
-                   nullptr) &&
+                   nullptr) && lap(1) &&
            measure([&](double* o) { return tkp_mfma_peak(d, 1, mfma_iters / 2, 3, 2, o); }, r.fp8, 2, min_fp8,
-                   nullptr) &&
+                   nullptr) && lap(2) &&
            measure([&](double* o) { return tkg_screen(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, r.gm, 7,
-                   min_gemm, &gemm_bad) &&
+                   min_gemm, &gemm_bad) && lap(3) &&
            measure([&](double* o) { return tkg_screen_fp8(d, gemm_n, gemm_n, gemm_n, gemm_reps, -1, o); }, r.gm8,
-                   7, min_gemm8, &gemm8_bad) &&
-           tkp_memtest_span(d, mt_bytes, 16ull << 30, 4ull << 30, full ? 3 : 1, r.mt) == 0;
+                   7, min_gemm8, &gemm8_bad) && lap(4) &&
+           tkp_memtest_span(d, mt_bytes, 16ull << 30, 4ull << 30, full ? 3 : 1, r.mt) == 0 && lap(5);
     snprintf(r.err, sizeof(r.err), "%s", g_err[0] ? g_err : tkg_last_error());
     r.gemm_ok = !gemm_bad;
     r.gemm8_ok = !gemm8_bad;
@@ -1626,11 +1634,13 @@ int main(int argc, char** argv) {
     printf("%s{\"device\":%d,\"arch\":\"%s\",\"cus\":%d,\"read_gbps\":%.1f,\"write_gbps\":%.1f,\"copy_gbps\":%.1f,"
            "\"bf16_tflops\":%.1f,\"fp8_tflops\":%.1f,\"gemm_tflops\":%.1f,\"gemm_checksum_ok\":%s,"
            "\"gemm_fp8_tflops\":%.1f,\"gemm_fp8_checksum_ok\":%s,"
-           "\"memtest_errors\":%.0f,\"memtest_bytes\":%.0f,\"hbm_bytes\":%.0f,\"remeasured\":%d,\"ok\":%s%s%s%s}",
+           "\"memtest_errors\":%.0f,\"memtest_bytes\":%.0f,\"hbm_bytes\":%.0f,\"remeasured\":%d,"
+           "\"phase_ms\":{\"hbm\":%.1f,\"mfma_bf16\":%.1f,\"mfma_fp8\":%.1f,\"gemm_bf16\":%.1f,\"gemm_fp8\":%.1f,"
+           "\"memtest\":%.1f,\"memtest.alloc\":%.1f,\"memtest.test\":%.1f,\"memtest.free\":%.1f},\"ok\":%s%s%s%s}",
            k ? "," : "", devs[k], r.info.arch, r.info.compute_units, r.hbm[0], r.hbm[1], r.hbm[2], r.bf16[0],
            r.fp8[0], r.gm[0], r.gemm_ok ? "true" : "false", r.gm8[0], r.gemm8_ok ? "true" : "false", r.mt[0],
-           r.mt[2], r.mt[3], r.remeasured, r.pass ? "true" : "false", r.ok ? "" : ",\"error\":\"",
-           r.ok ? "" : r.err, r.ok ? "" : "\"");
+           r.mt[2], r.mt[3], r.remeasured, r.ph[0], r.ph[1], r.ph[2], r.ph[3], r.ph[4], r.ph[5], r.mt[4], r.mt[5],
+           r.mt[6], r.pass ? "true" : "false", r.ok ? "" : ",\"error\":\"", r.ok ? "" : r.err, r.ok ? "" : "\"");
   }
   printf("],\"ok\":%s}\n", ok_all ? "true" : "false");
   if (labels_path) {
