@@ -442,3 +442,15 @@ def test_inits_running_is_zero_without_loading_libtk_rccl(monkeypatch):
 
     monkeypatch.delitem(native._cache, "libtk_rccl.so", raising=False)
     assert rccl.inits_running() == 0 and "libtk_rccl.so" not in native._cache
+
+
+def test_agent_stop_leaves_burnin_children_to_finish_their_release(monkeypatch):
+    """A child still freeing the HBM it tested finishes on its own (its stdin closes with the
+    agent); stopping the agent waits only for this process's own releases."""
+    from triton_kubernetes_amd.node.agent import NodeAgent
+
+    calls = []
+    monkeypatch.setattr(probe, "wait_frees", lambda children=True: calls.append(children))
+    a = NodeAgent(name="h", mode="sim", devices=[0], token="t" * 20)
+    a.stop()
+    assert calls == [False]

@@ -394,7 +394,9 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         if self.devices and self.topology_override is None and self.burnin_override is None:
             from ..ops import probe
 
-            probe.wait_frees()
+            # this process's own releases; a burn-in child still releasing what it tested
+            # finishes on its own (its stdin closes with this process: no hold outlives it)
+            probe.wait_frees(children=False)
 
 def main(argv: Optional[List[str]] = None) -> int:
     """``tk-node-agent``: serve the agent API on a host (127.0.0.1 by default)."""

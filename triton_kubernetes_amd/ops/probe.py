@@ -192,11 +192,12 @@ def set_async_free(on: bool) -> None:
     _lib().tkp_set_async_free(1 if on else 0)
 
 
-def wait_frees() -> None:
-    """Join pending background releases of span-memtest memory (in this process, and the
-    ``gpu-burnin --memtest-span`` children still releasing theirs)."""
+def wait_frees(children: bool = True) -> None:
+    """Join pending background releases of span-memtest memory (in this process, and --
+    ``children`` -- the ``gpu-burnin`` children still releasing theirs)."""
     _lib().tkp_wait_frees()
-    _wait_span_children()
+    if children:
+        _wait_span_children()
 
 
 # --- the full memtest in a short-lived child process (long-lived agents) ----------------------
