@@ -32,6 +32,12 @@ outside the timed region, the bench waits until the kernel driver has finished c
 HBM the previous step released (``ops/hbm.py``; ``hbm_settle_s`` in the line): a node
 entering service starts with clear HBM, so no step pays its predecessor's ~300 GB release.
 
+Node state carried across steps, as on a real node after its first GPU process: the page
+cache and the HIP runtime's code-object cache (ROCm comgr, on by default, ``~/.cache/comgr``),
+which the warmup's first RCCL init fills with librccl's unbundled gfx950 code.  A box's very
+first RCCL init takes ~5.5 s; later processes ~1.8 s (``config.comgr_cache`` gives its size
+before the warmup and before the timed steps).
+
 ``value`` is the mean create -> kubectl-ready time (agent start to readiness);
 ``ms_per_step`` is the whole step including the agent shutdown.  A WARM number (the
 same create against agents kept resident across steps, round 1's headline) is
@@ -66,6 +72,28 @@ sys.path.insert(0, HERE)
 
 METRIC = "cluster create→kubectl-ready wall-clock (s), bare-metal at 1/2/4/8 workers"
 SIMULATED_PHASES = ["rke_provisioning", "runtime_install", "agent_container", "device_plugin_pod"]
+
+
+def comgr_cache_dir() -> str:
+    """Where the HIP runtime's code-object cache lives (ROCm comgr, on by default): unbundled
+    and decompressed device code, keyed by its input.  librccl's gfx950 code comes out of a
+    13-target bundle; a process finding it here starts its first communicator in ~1.8 s
+    instead of ~5.5 s (profiles/round5/README.md)."""
+    if os.environ.get("AMD_COMGR_CACHE_DIR"):
+        return os.environ["AMD_COMGR_CACHE_DIR"]
+    base = os.environ.get("XDG_CACHE_HOME") or os.path.join(os.path.expanduser("~"), ".cache")
+    return os.path.join(base, "comgr")
+
+
+def dir_mib(path: str) -> float:
+    total = 0
+    for root, _, files in os.walk(path):
+        for f in files:
+            try:
+                total += os.path.getsize(os.path.join(root, f))
+            except OSError:
+                pass
+    return round(total / 2**20, 1)
 
 
 def _default_burnin() -> str:
@@ -452,6 +480,8 @@ def main() -> int:
         barrier()
         return got
 
+    comgr = {"dir": comgr_cache_dir(), "enabled": os.environ.get("AMD_COMGR_CACHE", "1") != "0",
+             "mib_at_start": dir_mib(comgr_cache_dir())}
     results = []
     settles = []
     try:
@@ -460,6 +490,7 @@ def main() -> int:
             barrier()
             cold_step(-1 - w)
         TRACER.reset()
+        comgr["mib_before_timed"] = dir_mib(comgr["dir"])
         # the timed region is the K steps, each bracketed by a barrier + synchronize on both
         # sides; the settle wait before each step is outside it (and reported as hbm_settle_s)
         elapsed = 0.0
@@ -581,6 +612,10 @@ def main() -> int:
                 "rccl_slim": ({k: slim_meta.get(k) for k in ("prepare_s", "cached", "source_fatbin_bytes",
                                                               "loaded_code_object_bytes", "verified")}
                               if slim_meta else None),
+                # node state the timed steps find, as a node does after its first GPU process: the
+                # HIP code-object cache the warmup's RCCL init filled (a fresh box's first init
+                # pays ~5.5 s instead of ~1.8 s, once)
+                "comgr_cache": comgr,
             },
             "create_to_ready_s": ready,
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),

@@ -147,3 +147,31 @@ def test_cards_for_pci_picks_this_process_gpus(tmp_path):
     assert hbm.vram_used(drm, cards=["card8"]) == {"card8": 200 << 30}
     assert hbm.cards_for_pci([(0, 0x99, 0)], drm) == []
     assert hbm.settle(drm, cards=[])["cards"] == 0
+
+
+def test_comgr_cache_dir_follows_comgr_own_lookup(monkeypatch, tmp_path):
+    """The line reports the code-object cache the timed steps find (node state the warmup
+    fills): comgr's own directory choice, explicit dir first, then XDG, then ~/.cache."""
+    import bench
+
+    monkeypatch.setenv("AMD_COMGR_CACHE_DIR", str(tmp_path / "x"))
+    assert bench.comgr_cache_dir() == str(tmp_path / "x")
+    monkeypatch.delenv("AMD_COMGR_CACHE_DIR")
+    monkeypatch.setenv("XDG_CACHE_HOME", str(tmp_path / "xdg"))
+    assert bench.comgr_cache_dir() == str(tmp_path / "xdg" / "comgr")
+    monkeypatch.delenv("XDG_CACHE_HOME")
+    monkeypatch.setenv("HOME", str(tmp_path / "home"))
+    assert bench.comgr_cache_dir() == str(tmp_path / "home" / ".cache" / "comgr")
+    (tmp_path / "home" / ".cache" / "comgr").mkdir(parents=True)
+    (tmp_path / "home" / ".cache" / "comgr" / "entry").write_bytes(b"\0" * (3 << 20))
+    assert bench.dir_mib(bench.comgr_cache_dir()) == 3.0
+
+
+def test_agent_unit_gives_comgr_a_cache_dir():
+    import os
+
+    from triton_kubernetes_amd.images import packer
+
+    unit = open(os.path.join(packer.FILES_DIR, "tk-node-agent.service")).read()
+    assert "Environment=AMD_COMGR_CACHE_DIR=/var/cache/triton-kubernetes/comgr" in unit
+    assert "CacheDirectory=triton-kubernetes/comgr" in unit
