@@ -4,6 +4,7 @@ The install script's ``tk_node_tools`` runs here against a sandbox: stub ``sudo`
 ``hipcc``/``g++`` that count their calls, the module's shipped sources and a staged
 prebuilt directory."""
 
+import hashlib
 import json
 import os
 import shutil
@@ -67,7 +68,9 @@ def test_stamp_is_the_one_the_node_computes_from_the_shipped_sources(node):
     run, compiles, tmp = node
     _staged(tmp)
     for name in tools.TOOL_SOURCES:
-        assert (tmp / "prebuilt" / f"{name}.sha256").read_text().strip() == tools.node_stamp(name)
+        stamp, binary_sum = (tmp / "prebuilt" / f"{name}.sha256").read_text().split()
+        assert stamp == tools.node_stamp(name)
+        assert binary_sum == hashlib.sha256((tmp / "prebuilt" / name).read_bytes()).hexdigest()
         # the module ships exactly the sources the stamp covers
         assert tools.node_stamp(name, str(tmp / "src")) == tools.node_stamp(name, CSRC)
     res = run(tmp / "bin")
@@ -109,6 +112,17 @@ def test_only_the_tool_whose_sources_changed_is_built(node):
     assert "gpu-burnin: no matching prebuilt binary; building with" in res.stdout
     # the node's own build is stamped too: the next apply keeps it
     assert run(tmp / "bin").returncode == 0 and len(compiles()) == 1
+
+
+def test_a_binary_damaged_on_the_way_is_rebuilt(node):
+    run, compiles, tmp = node
+    _staged(tmp)
+    with open(tmp / "prebuilt" / "gpu-burnin", "a") as fh:
+        fh.write("# truncated or altered in transit\n")
+    res = run(tmp / "bin")
+    assert res.returncode == 0, res.stderr
+    assert len(compiles()) == 1 and "-DTK_PROBE_MAIN" in compiles()[0]
+    assert res.stdout.count("prebuilt binary installed") == 2
 
 
 def test_stale_prebuilt_and_no_compiler_fails_naming_the_tool(node, tmp_path):
@@ -210,7 +224,7 @@ def test_machine_image_builds_with_the_same_stamped_function(node, tmp_path):
     from triton_kubernetes_amd.images import packer
 
     script = open(os.path.join(packer.FILES_DIR, "build-node-tools.sh")).read()
-    assert tools.NODE_TOOLS_FN in script
+    assert script == tools.image_build_script()  # python -m triton_kubernetes_amd.node.tools rewrites it
     run, compiles, tmp = node
     bindir = tmp / "stubs"
     env = dict(os.environ, PATH=f"{bindir}:{os.environ['PATH']}", TK_SRC=str(tmp / "src"), TK_BIN=str(tmp / "img"),

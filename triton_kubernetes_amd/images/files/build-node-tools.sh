@@ -2,8 +2,9 @@
 # Build the MI355X node tools for gfx950 from /opt/triton-kubernetes/src into
 # /opt/triton-kubernetes/bin, each stamped with the sha256 of the sources it was built
 # from.  tk_node_tools is the function the Terraform host module runs
-# (triton_kubernetes_amd/node/tools.py), so a node made from this image keeps these tools
-# at bring-up: nothing is uploaded or compiled again while the shipped sources match.
+# (triton_kubernetes_amd/node/tools.py, which writes this file), so a node made from this
+# image keeps these tools at bring-up: nothing is uploaded or compiled again while the
+# shipped sources match.
 set -euo pipefail
 S=${TK_SRC:-/opt/triton-kubernetes/src}
 T=${TK_BIN:-/opt/triton-kubernetes/bin}
@@ -20,7 +21,8 @@ tk_node_tool() { # <tools dir> <sources dir> <prebuilt dir> <name> "<sources>" <
     echo "$name: installed copy is current"
     return 0
   fi
-  if [ -x "$P/$name" ] && [ "$(cat "$P/$name.sha256" 2>/dev/null)" = "$want" ] && tk_libs_resolve "$P/$name"; then
+  if [ -x "$P/$name" ] && [ "$(cat "$P/$name.sha256" 2>/dev/null)" = "$want $(sha256sum < "$P/$name" | cut -d' ' -f1)" ] \
+      && tk_libs_resolve "$P/$name"; then
     sudo install -m 0755 "$P/$name" "$T/$name" || return 1
     echo "$name: prebuilt binary installed"
   elif command -v "$1" >/dev/null 2>&1; then

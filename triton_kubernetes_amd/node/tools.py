@@ -13,8 +13,9 @@ the ROCm compiler on production hosts, so:
 * the host module uploads that directory (``tk_prebuilt_tools``) beside the shipped sources,
   and its install script (``tk_node_tools``, :data:`NODE_TOOLS_FN`) computes the same stamp
   from the sources it was shipped.  Per tool: kept when the installed copy carries that
-  stamp (a re-apply compiles nothing); else the uploaded binary when its stamp matches and
-  its shared libraries resolve on the node; else built on the node (``hipcc``/``g++`` only
+  stamp (a re-apply compiles nothing); else the uploaded binary when its stamp matches, its
+  own sha256 is the one staged with it (it arrived whole) and its shared libraries resolve on
+  the node; else built on the node (``hipcc``/``g++`` only
   as this fallback, the builds in parallel); with no compiler there either, the node fails
   naming the tool.
 
@@ -78,8 +79,12 @@ def stage(dest: str, binary: Optional[Callable[[str], str]] = None, log=None) ->
             continue
         shutil.copyfile(path, os.path.join(dest, name))
         os.chmod(os.path.join(dest, name), 0o755)
+        with open(os.path.join(dest, name), "rb") as fh:
+            binary_sum = hashlib.sha256(fh.read()).hexdigest()
+        # "<source stamp> <sha256 of the binary>": the node installs it only when both hold
+        # (the shipped sources are the ones it was built from; it arrived whole)
         with open(os.path.join(dest, name + ".sha256"), "w", encoding="ascii") as fh:
-            fh.write(node_stamp(name) + "\n")
+            fh.write(f"{node_stamp(name)} {binary_sum}\n")
         out[name] = "prebuilt"
     return out
 
@@ -98,7 +103,8 @@ tk_node_tool() { # <tools dir> <sources dir> <prebuilt dir> <name> "<sources>" <
     echo "$name: installed copy is current"
     return 0
   fi
-  if [ -x "$P/$name" ] && [ "$(cat "$P/$name.sha256" 2>/dev/null)" = "$want" ] && tk_libs_resolve "$P/$name"; then
+  if [ -x "$P/$name" ] && [ "$(cat "$P/$name.sha256" 2>/dev/null)" = "$want $(sha256sum < "$P/$name" | cut -d' ' -f1)" ] \
+      && tk_libs_resolve "$P/$name"; then
     sudo install -m 0755 "$P/$name" "$T/$name" || return 1
     echo "$name: prebuilt binary installed"
   elif command -v "$1" >/dev/null 2>&1; then
@@ -125,6 +131,25 @@ tk_node_tools() { # <tools dir> <sources dir> <prebuilt dir> <rocm dir>
   return $rc
 }"""
 
+def image_build_script() -> str:
+    """``images/files/build-node-tools.sh``: the machine image's tool build (packer), on this
+    same ``tk_node_tools``.  ``python -m triton_kubernetes_amd.node.tools`` rewrites the file."""
+    return ("#!/bin/bash\n"
+            "# Build the MI355X node tools for gfx950 from /opt/triton-kubernetes/src into\n"
+            "# /opt/triton-kubernetes/bin, each stamped with the sha256 of the sources it was built\n"
+            "# from.  tk_node_tools is the function the Terraform host module runs\n"
+            "# (triton_kubernetes_amd/node/tools.py, which writes this file), so a node made from this\n"
+            "# image keeps these tools at bring-up: nothing is uploaded or compiled again while the\n"
+            "# shipped sources match.\n"
+            "set -euo pipefail\n"
+            "S=${TK_SRC:-/opt/triton-kubernetes/src}\n"
+            "T=${TK_BIN:-/opt/triton-kubernetes/bin}\n"
+            "ROCM=${ROCM_PATH:-/opt/rocm}\n"
+            + NODE_TOOLS_FN + "\n"
+            'tk_node_tools "$T" "$S" /nonexistent "$ROCM"\n'
+            '"$T/amdgpu-topo-labeller" --labels\n')
+
+
 # "<tool> <stamp>" for every node tool installed with a stamp (DirectExecutor uploads)
 REMOTE_STAMPS = """for f in {tools}/.stamps/*.sha256; do
   n=$(basename "$f" .sha256)
@@ -133,4 +158,11 @@ done
 true
 """
 
-__all__ = ["NODE_TOOLS_FN", "REMOTE_STAMPS", "PREBUILT_DIR", "SOURCES_DIR", "TOOL_SOURCES", "node_stamp", "stage"]
+if __name__ == "__main__":
+    from ..images import packer
+
+    with open(os.path.join(packer.FILES_DIR, "build-node-tools.sh"), "w", encoding="utf-8") as out:
+        out.write(image_build_script())
+    print("wrote", os.path.join(packer.FILES_DIR, "build-node-tools.sh"))
+
+__all__ = ["NODE_TOOLS_FN", "REMOTE_STAMPS", "image_build_script", "PREBUILT_DIR", "SOURCES_DIR", "TOOL_SOURCES", "node_stamp", "stage"]
