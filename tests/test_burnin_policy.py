@@ -454,3 +454,46 @@ def test_agent_stop_leaves_burnin_children_to_finish_their_release(monkeypatch):
     a = NodeAgent(name="h", mode="sim", devices=[0], token="t" * 20)
     a.stop()
     assert calls == [False]
+
+
+def test_link_matrix_in_a_child_process(burnin_child, monkeypatch, tmp_path):
+    """The agent's gpu_links step measures the peer-read matrix in ``gpu-burnin --p2p-child``
+    (beside its RCCL start, as the burn-in): same result form as the in-process matrix."""
+    import json
+    import sys
+
+    exe = tmp_path / "gpu-burnin"
+    exe.write_text(f"""#!{sys.executable}
+import json, os, sys
+open(os.environ["FAKE_CHILD_ARGV"], "w").write(" ".join(sys.argv[1:]))
+print(json.dumps({{"ok": True, "pairs": {{"0-1": 51.5, "1-0": 50.9}}, "peer_access": {{"0-1": True, "1-0": True}},
+                  "errors": [], "bytes": 67108864, "method": "kernel-read", "data_errors": {{"1-0": 3}}}}), flush=True)
+""")
+    got = probe.link_matrix_process([0, 1])
+    assert burnin_child.read_text().split() == ["--p2p-child", "--devices", "0,1", "--bytes", str(64 << 20),
+                                                "--iters", "3", "--p2p-method", "kernel-read"]
+    assert got == {"pairs": {"0-1": 51.5, "1-0": 50.9}, "peer_access": {"0-1": True, "1-0": True}, "errors": [],
+                   "bytes": 64 << 20, "method": "kernel-read", "data_errors": {"1-0": 3}}
+    from triton_kubernetes_amd.node.labels import link_labels
+
+    verdict = link_labels(got, 0.5, 38.0)
+    assert verdict["status"] == "degraded"  # the corrupted pair fails the node, as in process
+    exe.write_text(f"#!{sys.executable}\nprint('{{\"ok\": false, \"error\": \"hipSetDevice: invalid device\"}}')\n")
+    with pytest.raises(probe.ProbeError, match="invalid device"):
+        probe.link_matrix_process([0, 7])
+
+
+def test_agent_links_step_uses_the_child(monkeypatch):
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.plan import Step
+
+    used = []
+    monkeypatch.setattr(probe, "_BURNIN_PROCESS", True)
+    monkeypatch.setattr(probe, "link_matrix_process", lambda devs, method: used.append(("child", devs)) or {
+        "pairs": {"0-1": 50.0, "1-0": 50.0}, "peer_access": {}, "errors": [], "data_errors": {}})
+    monkeypatch.setattr(probe, "link_matrix", lambda devs, method: used.append(("here", devs)))
+    a = NodeAgent(name="h", mode="sim", devices=[0, 1], token="t" * 20)
+    step = Step("gpu_links", "gpu_links", "", {"min_frac": 0.5, "min_gbps": 38.0, "method": "kernel-read"})
+    ctx = {"labels": {}, "capacity": {}, "taints": []}
+    out = a._run_step(None, step, ctx)
+    assert used == [("child", [0, 1])] and out["status"] == "passed", (used, out)

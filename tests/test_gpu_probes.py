@@ -167,6 +167,20 @@ def test_process_gate_two_nodes_rendezvous_and_fail_fast(tmp_path):
     assert time.monotonic() - t0 < 60
 
 
+def test_link_matrix_child_matches_in_process():
+    """The agent's links step runs ``gpu-burnin --p2p-child``: the same matrix form as the
+    in-process measurement, for every GPU of the box (none to measure on a one-GPU box)."""
+    from triton_kubernetes_amd.ops import probe
+
+    devs = list(range(probe.device_count()))
+    child = probe.link_matrix_process(devs)
+    here = probe.link_matrix(devs)
+    assert set(child) == set(here) and child["method"] == here["method"] == "kernel-read"
+    assert set(child["pairs"]) == set(here["pairs"]) and not child["errors"] and not child["data_errors"]
+    for k, v in child["pairs"].items():  # 64 MiB peer reads: within a factor of two of each other
+        assert 0.5 * here["pairs"][k] <= v <= 2.0 * here["pairs"][k], (k, v, here["pairs"][k])
+
+
 def test_link_check_on_this_box(tmp_path):
     """The per-link xGMI check: on a one-GPU box it reports "single GPU" (exit 0, empty
     labels); the copy primitive it times still runs (device to itself)."""

@@ -266,10 +266,18 @@ class AgentStepsMixin:
                 return {"skipped": "single GPU"}
             if self.topology_override is not None:  # synthetic GPUs (tests / dry runs)
                 return {"simulated": True}
-            from ..ops import probe
+            from ..ops import native, probe
 
-            verdict = link_labels(probe.link_matrix(self.devices, method=str(step.params.get("method", "kernel-read"))),
-                                  float(step.params.get("min_frac", 0.5)),
+            method = str(step.params.get("method", "kernel-read"))
+            matrix = None
+            if probe._BURNIN_PROCESS:  # beside this process's RCCL start, as the burn-in
+                try:
+                    matrix = probe.link_matrix_process(self.devices, method=method)
+                except native.NativeUnavailable:
+                    matrix = None  # no current gpu-burnin: measured here
+            if matrix is None:
+                matrix = probe.link_matrix(self.devices, method=method)
+            verdict = link_labels(matrix, float(step.params.get("min_frac", 0.5)),
                                   float(step.params.get("min_gbps", probe.DEFAULT_MIN_LINK_GBPS)))
             ctx["labels"].update(verdict["labels"])
             if verdict["status"] == "degraded":

@@ -1362,6 +1362,50 @@ static void json_escape(const char* in, char* out, size_t cap) {
   out[o] = 0;
 }
 
+// --p2p-child --devices 0,1,..: the raw peer-read matrix of these devices, one JSON line in
+// ops/probe.py:link_matrix's form (the agent judges it, node/labels.py:link_labels).  A node
+// agent measures its links here rather than in its own process, where the cluster gate's
+// RCCL communicator start holds the HIP runtime while it loads RCCL's device code.
+static int p2p_child_main(const std::vector<int>& devs, size_t nbytes, int iters, int mode) {
+  const int n = (int)devs.size();
+  std::vector<double> mat(n * n, 0.0), derr(n * n, 0.0);
+  std::vector<int> acc(n * n, 0);
+  if (n >= 2 && tkp_link_matrix_check(devs.data(), n, nbytes, iters, mode, mat.data(), acc.data(), derr.data()) != 0) {
+    char e[600];
+    json_escape(g_err, e, sizeof(e));
+    printf("{\"ok\":false,\"error\":\"%s\"}\n", e);
+    fflush(stdout);
+    return 2;
+  }
+  std::string pairs, access, data_errors, errors;
+  for (int a = 0; a < n; ++a)
+    for (int b = 0; b < n; ++b) {
+      if (a == b) continue;
+      char key[64], buf[128];
+      snprintf(key, sizeof(key), "\"%d-%d\"", devs[a], devs[b]);
+      snprintf(buf, sizeof(buf), "%s%s:%s", access.empty() ? "" : ",", key, acc[a * n + b] ? "true" : "false");
+      access += buf;
+      if (mat[a * n + b] < 0.0) {
+        snprintf(buf, sizeof(buf), "%s\"%d->%d: peer %s failed\"", errors.empty() ? "" : ",", devs[a], devs[b],
+                 mode ? "read" : "copy");
+        errors += buf;
+        continue;
+      }
+      snprintf(buf, sizeof(buf), "%s%s:%.1f", pairs.empty() ? "" : ",", key, mat[a * n + b]);
+      pairs += buf;
+      if (derr[a * n + b] > 0.0) {
+        snprintf(buf, sizeof(buf), "%s%s:%.0f", data_errors.empty() ? "" : ",", key, derr[a * n + b]);
+        data_errors += buf;
+      }
+    }
+  printf("{\"ok\":true,\"pairs\":{%s},\"peer_access\":{%s},\"errors\":[%s],\"bytes\":%zu,\"method\":\"%s\","
+         "\"data_errors\":{%s}}\n", pairs.c_str(), access.c_str(), errors.c_str(), nbytes,
+         mode ? "kernel-read" : "sdma-copy", data_errors.c_str());
+  fflush(stdout);
+  if (quick_exit_wanted()) _exit(0);
+  return 0;
+}
+
 static int burnin_child_main(int argc, char** argv) {
   int dev = 0, hbm_iters = 3, mfma_iters = 2000, gm = 4096, gn = 4096, gk = 4096, greps = 5, passes = 1;
   size_t hbm_bytes = 1ull << 30, mt_bytes = 1ull << 30, headroom = 4ull << 30, chunk = 1ull << 30;
@@ -1488,6 +1532,24 @@ static int burnin_child_main(int argc, char** argv) {
 int main(int argc, char** argv) {
   for (int i = 1; i < argc; ++i)
     if (!strcmp(argv[i], "--burnin-child")) return burnin_child_main(argc, argv);
+  for (int i = 1; i < argc; ++i) {
+    if (strcmp(argv[i], "--p2p-child")) continue;
+    std::vector<int> devs;
+    size_t nbytes = 64ull << 20;
+    int iters = 3, mode = 1;
+    for (int k = 1; k + 1 < argc; ++k) {
+      if (!strcmp(argv[k], "--devices")) {
+        for (const char* c = argv[++k]; *c;) {
+          devs.push_back(atoi(c));
+          while (*c && *c != ',') ++c;
+          if (*c == ',') ++c;
+        }
+      } else if (!strcmp(argv[k], "--bytes")) nbytes = strtoull(argv[++k], nullptr, 10);
+      else if (!strcmp(argv[k], "--iters")) iters = atoi(argv[++k]);
+      else if (!strcmp(argv[k], "--p2p-method")) mode = strcmp(argv[++k], "sdma-copy") ? 1 : 0;
+    }
+    return p2p_child_main(devs, nbytes, iters, mode);
+  }
   const auto t_main = std::chrono::steady_clock::now();
   const bool trace = getenv("TK_BURNIN_TRACE") != nullptr;
   const bool fast_exit = quick_exit_wanted();

@@ -310,14 +310,15 @@ def _release_after_hold(proc: Any, hold: Callable[[], None]) -> None:
             pass
 
 
-def _child_verdict(argv: List[str], dev: int, timeout: float, what: str) -> Tuple[Dict[str, Any], float]:
+def _child_verdict(argv: List[str], dev: int, timeout: float, what: str,
+                   hold: bool = True) -> Tuple[Dict[str, Any], float]:
     """Start a ``gpu-burnin`` child for ``dev`` and return its JSON verdict (the first JSON
     line it prints) and the ms until then.  The child is registered with the device's span
     children: it releases what it holds after the verdict -- once the release hold says so
     (:func:`set_release_hold`) -- and the next span on the device (and :func:`wait_frees`)
     waits for it to exit."""
     t0 = time.perf_counter()
-    hold = _RELEASE_HOLD
+    hold = _RELEASE_HOLD if hold else None  # a child holding no HBM has nothing to release
     if hold is not None:
         argv = list(argv) + ["--hold-stdin", "--hold-max-ms", str(RELEASE_HOLD_MAX_MS)]
     try:
@@ -398,6 +399,25 @@ def p2p_bandwidth(src: int, dst: int, nbytes: int = 256 << 20, iters: int = 5) -
 XGMI_LINK_ONE_WAY_GBPS = 76.8
 DEFAULT_MIN_LINK_GBPS = 38.0
 LINK_METHODS = {"sdma-copy": 0, "kernel-read": 1}
+
+
+def link_matrix_process(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3,
+                        method: str = "kernel-read", timeout: float = 600.0) -> Dict[str, Any]:
+    """:func:`link_matrix` measured by a ``gpu-burnin --p2p-child`` process (same result):
+    a node agent's own HIP runtime may be busy loading RCCL's device code for the cluster
+    gate, and its kernel launches wait behind that load (``_burnin_child``).  Raises
+    ``NativeUnavailable`` (``_ChildUnstartable``) when the child cannot run."""
+    if method not in LINK_METHODS:
+        raise ValueError(f"link method must be one of {sorted(LINK_METHODS)}")
+    devs = [int(d) for d in devices]
+    argv = [_burnin_exe(), "--p2p-child", "--devices", ",".join(str(d) for d in devs), "--bytes", str(int(nbytes)),
+            "--iters", str(int(iters)), "--p2p-method", method]
+    doc, _ = _child_verdict(argv, devs[0] if devs else 0, timeout, "link_matrix", hold=False)
+    if not doc.get("ok"):
+        raise ProbeError(f"link_matrix: {doc.get('error', 'no verdict')}")
+    if "pairs" not in doc:
+        raise ProbeError(f"link_matrix: unreadable verdict {json.dumps(doc)[:200]}")
+    return {k: doc.get(k) for k in ("pairs", "peer_access", "errors", "bytes", "method", "data_errors")}
 
 
 def link_matrix(devices: Sequence[int], nbytes: int = 64 << 20, iters: int = 3,
