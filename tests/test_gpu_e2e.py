@@ -361,4 +361,16 @@ def test_exec_agent_rke2_teardown_then_another_cluster_on_mi355x(tmp_path, monke
     finally:
         agent.stop()
         fake.stop()
-    print(json.dumps({"cleanup_ms": rep.get("ms"), "actions": rep["actions"]}))
+    # the SSH / Terraform path's teardown: the same steps as a script (node/cleanup.py,
+    # markers ::tk-cleanup), run on this host model after B's join (sudo stubbed: no root here)
+    from triton_kubernetes_amd.parallel.transport import LocalTransport
+
+    _stub(bindir, "sudo", 'exec "$@"')
+    script_rep = LocalTransport(env={"TK_HOST_ROOT": str(root), "PATH": os.environ["PATH"]}).cleanup_host(
+        HostRef("local"))
+    assert script_rep["ok"], script_rep
+    assert [a["what"] for a in script_rep["actions"] if a.get("status") == "ok"] == [
+        "/usr/local/bin/rancher-system-agent-uninstall.sh", "/usr/local/bin/rke2-killall.sh",
+        "/usr/local/bin/rke2-uninstall.sh"], script_rep
+    assert not (root / hostsim.CONNECTION_INFO.lstrip("/")).exists() and not (root / "var/lib/rancher").exists()
+    print(json.dumps({"cleanup_ms": rep.get("ms"), "actions": rep["actions"], "script_actions": script_rep["actions"]}))
