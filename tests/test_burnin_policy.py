@@ -497,3 +497,22 @@ def test_agent_links_step_uses_the_child(monkeypatch):
     ctx = {"labels": {}, "capacity": {}, "taints": []}
     out = a._run_step(None, step, ctx)
     assert used == [("child", [0, 1])] and out["status"] == "passed", (used, out)
+
+
+def test_release_hold_also_waits_for_the_plans_link_matrix(monkeypatch):
+    import threading
+    import time
+
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.ops import rccl
+
+    monkeypatch.setattr(rccl, "inits_running", lambda: 0)
+    a = NodeAgent(name="h", mode="sim", token="t" * 20)
+    a._links_pending = True
+    done = threading.Event()
+    t = threading.Thread(target=lambda: (a._await_rccl_inits(), done.set()), daemon=True)
+    t.start()
+    time.sleep(0.2)
+    assert not done.is_set()  # still held: the link matrix is yet to be measured
+    a._links_pending = False
+    assert done.wait(2.0)

@@ -190,16 +190,25 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             # and burn-in kernels instead of running after them
             ctx["topology_future"] = self._pool.submit(self._topology)
         with self.lock:
-            for step in plan.steps:
-                t0 = time.perf_counter()
-                try:
-                    with span(f"node.{step.action}", node=plan.hostname):
-                        detail = self._run_step(plan, step, ctx)
-                    results.append(StepResult(step.name, True, (time.perf_counter() - t0) * 1e3, detail))
-                except Exception as exc:  # noqa: BLE001 - reported to the executor
-                    results.append(StepResult(step.name, False, (time.perf_counter() - t0) * 1e3, str(exc)))
-                    error = f"{step.name}: {exc}"
-                    break
+            # the burn-in children keep the HBM they tested until this plan's link matrix is
+            # measured too: the driver's clearing of their release would run beside it
+            self._links_pending = any(s.action == "gpu_links" for s in plan.steps)
+            try:
+                for step in plan.steps:
+                    t0 = time.perf_counter()
+                    try:
+                        with span(f"node.{step.action}", node=plan.hostname):
+                            detail = self._run_step(plan, step, ctx)
+                        results.append(StepResult(step.name, True, (time.perf_counter() - t0) * 1e3, detail))
+                    except Exception as exc:  # noqa: BLE001 - reported to the executor
+                        results.append(StepResult(step.name, False, (time.perf_counter() - t0) * 1e3, str(exc)))
+                        error = f"{step.name}: {exc}"
+                        break
+                    finally:
+                        if step.action == "gpu_links":
+                            self._links_pending = False
+            finally:
+                self._links_pending = False
         doc = {"hostname": plan.hostname, "ok": error is None, "error": error,
                "ms": (time.perf_counter() - t_plan) * 1e3,
                "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"],

@@ -92,14 +92,15 @@ class AgentGateMixin:
     RELEASE_HOLD_S = 20.0
 
     def _await_rccl_inits(self) -> None:
-        """Return once no RCCL communicator init of this agent is running, or after
-        :attr:`RELEASE_HOLD_S` (``ops/probe.py:set_release_hold``: a burn-in child's ~300 GB
-        release, which the driver clears for seconds, would hold up the device-code load of
-        an init still running)."""
+        """Return once no RCCL communicator init of this agent is running and the running
+        plan's link matrix is measured, or after :attr:`RELEASE_HOLD_S`
+        (``ops/probe.py:set_release_hold``: a burn-in child's ~300 GB release, which the
+        driver clears for seconds, would hold up the device-code load of an init still
+        running, and run beside the peer reads of the link check)."""
         from ..ops import rccl
 
         deadline = time.monotonic() + self.RELEASE_HOLD_S
-        while rccl.inits_running() > 0 and time.monotonic() < deadline:
+        while (rccl.inits_running() > 0 or getattr(self, "_links_pending", False)) and time.monotonic() < deadline:
             time.sleep(0.005)
 
     def _gate_devices(self, ndev: int) -> List[int]:
