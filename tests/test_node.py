@@ -32,11 +32,12 @@ def test_plan_steps_and_order():
     assert rke1.step_names() == ["firewall", "runtime", "hostname", "agent"]
     reg = dict(GPU_WORKER, rancher_registry="reg.io", rancher_registry_username="u", rancher_registry_password="p")
     gpu = build_host_plan(dict(reg, k8s_distribution="rke1"), "https://r", "tok", "sum", mi355x=True)
-    # burn-in precedes labels so the agent's topology prefetch overlaps it
+    # burn-in precedes labels so the agent's topology prefetch overlaps it; the link check
+    # precedes the burn-in (idle GPUs, not beside the clearing of the burn-in's release)
     assert gpu.step_names() == ["firewall", "runtime", "hostname", "registry_login", "gpu_preflight",
-                                "gpu_burnin", "gpu_links", "gpu_labels", "gpu_health", "rccl_env", "rccl_local", "agent"]
+                                "gpu_links", "gpu_burnin", "gpu_labels", "gpu_health", "rccl_env", "rccl_local", "agent"]
     gpu2 = build_host_plan(reg, "https://r", "tok", "sum", mi355x=True)
-    assert gpu2.step_names() == ["firewall", "hostname", "gpu_preflight", "gpu_burnin", "gpu_links", "gpu_labels",
+    assert gpu2.step_names() == ["firewall", "hostname", "gpu_preflight", "gpu_links", "gpu_burnin", "gpu_labels",
                                  "gpu_health", "rccl_env", "rccl_local", "agent"]
     # gpu_health = off: no RAS verdict step
     off = build_host_plan(dict(reg, gpu_health="off"), "https://r", "tok", "sum", mi355x=True)
@@ -406,7 +407,7 @@ def test_multi_gpu_plan_checks_links():
            "gpu_link_min_frac": 0.6}
     plan = build_host_plan(cfg, "https://r", "tok", "ca", mi355x=True)
     names = plan.step_names()
-    assert names.index("gpu_burnin") < names.index("gpu_links") < names.index("gpu_labels")
+    assert names.index("gpu_links") < names.index("gpu_burnin") < names.index("gpu_labels")
     assert "gpu-burnin --p2p --min-link-frac 0.6 --min-link-gbps 38.0" in plan.render_shell()
     step = next(st for st in plan.steps if st.name == "gpu_links")
     assert step.params == {"min_frac": 0.6, "min_gbps": 38.0, "method": "kernel-read"}

@@ -232,6 +232,17 @@ sudo usermod -aG video,render "$(id -un)" || true
 sudo rm -f {BURNIN_LABEL_FILE} {TAINT_FILE}
 {host_tuning_check(tuning, BURNIN_LABEL_FILE)}""", {"count": ngpu, "compute_partition": cpart, "memory_partition": mpart,
                                                "host_tuning": tuning}, gpu=True))
+        if physical > 1 and cpart == "spx":  # links are a whole GPU's (a partition has no own)
+            # per-link xGMI health: kernel-driven peer read of every GPU pair against the
+            # node's median (relative) and an absolute floor (a uniformly slow fabric).  Before
+            # the burn-in: the peer reads then run on idle GPUs, never beside the driver's
+            # clearing of the ~300 GB per GPU a full burn-in releases
+            frac = float(cfg.get("gpu_link_min_frac", 0.5) or 0.5)
+            floor = float(cfg.get("gpu_link_min_gbps", DEFAULT_MIN_LINK_GBPS) or 0.0)
+            plan.steps.append(Step("gpu_links", "gpu_links", f"""
+{TOOLS_DIR}/gpu-burnin --p2p --min-link-frac {frac} --min-link-gbps {floor} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
+cat /tmp/tk-link-labels | sudo tee -a {BURNIN_LABEL_FILE} >/dev/null""", {"min_frac": frac, "min_gbps": floor,
+                                                                       "method": "kernel-read"}, gpu=True))
         # burn-in before labels: the agent discovers the topology concurrently
         # with the burn-in kernels and only joins it at the labels step
         if burnin != "off":
@@ -241,15 +252,6 @@ sudo mkdir -p /etc/triton-kubernetes
 sudo tee -a {BURNIN_LABEL_FILE} < /tmp/tk-burnin-labels >/dev/null""",
                                    {"level": burnin, "compute_partition": cpart, "memory_partition": mpart},
                                    gpu=True))
-        if physical > 1 and cpart == "spx":  # links are a whole GPU's (a partition has no own)
-            # per-link xGMI health: kernel-driven peer read of every GPU pair against the
-            # node's median (relative) and an absolute floor (a uniformly slow fabric)
-            frac = float(cfg.get("gpu_link_min_frac", 0.5) or 0.5)
-            floor = float(cfg.get("gpu_link_min_gbps", DEFAULT_MIN_LINK_GBPS) or 0.0)
-            plan.steps.append(Step("gpu_links", "gpu_links", f"""
-{TOOLS_DIR}/gpu-burnin --p2p --min-link-frac {frac} --min-link-gbps {floor} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
-cat /tmp/tk-link-labels | sudo tee -a {BURNIN_LABEL_FILE} >/dev/null""", {"min_frac": frac, "min_gbps": floor,
-                                                                       "method": "kernel-read"}, gpu=True))
         plan.steps.append(Step("gpu_labels", "gpu_labels", f"""
 sudo mkdir -p "$(dirname {LABEL_FILE})"
 {TOOLS_DIR}/amdgpu-topo-labeller | sudo tee {TOPOLOGY_FILE} >/dev/null

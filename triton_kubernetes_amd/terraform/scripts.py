@@ -518,6 +518,12 @@ sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels /etc/triton-kubernetes/gpu-t
 """ + _host_tuning_check(
     "warn", "/etc/triton-kubernetes/gpu-burnin-labels", fail='${gpu_host_tuning == "enforce" ? "exit 1" : "true"}') + r"""
 %{ endif ~}
+# the xGMI link check first, on idle GPUs: a full burn-in's release of ~300 GB per GPU is
+# cleared by the driver for seconds after it, beside whatever runs next
+%{ if gpu_count > 1 && gpu_compute_partition == "spx" ~}
+$T/gpu-burnin --p2p --min-link-frac ${gpu_link_min_frac} --min-link-gbps ${gpu_link_min_gbps} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
+cat /tmp/tk-link-labels | sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels >/dev/null
+%{ endif ~}
 %{ if gpu_burnin != "off" ~}
 $T/gpu-burnin --all --level '${gpu_burnin}' --compute-partition ${gpu_compute_partition} --memory-partition ${gpu_memory_partition} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
 sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels < /tmp/tk-burnin-labels >/dev/null
@@ -547,10 +553,6 @@ esac
 ${rccl_env_file}
 TK_RCCL_EOF
 } | sudo tee /etc/rccl/rccl.env >/dev/null
-%{ if gpu_count > 1 && gpu_compute_partition == "spx" ~}
-$T/gpu-burnin --p2p --min-link-frac ${gpu_link_min_frac} --min-link-gbps ${gpu_link_min_gbps} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
-cat /tmp/tk-link-labels | sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels >/dev/null
-%{ endif ~}
 %{ if gpu_count * gpu_partitions > 1 ~}
 set -a; . /etc/rccl/rccl.env; set +a
 $RCCL_READY --ngpus ${gpu_count * gpu_partitions} --min-busbw ${rccl_min_busbw}
