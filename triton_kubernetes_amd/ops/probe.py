@@ -5,6 +5,13 @@ GPU before the node may advertise ``amd.com/gpu``.  Thresholds are fractions of
 MI355X figures (MI355X_MICROARCH.md): HBM3E ~6.3 TB/s achievable of 8 TB/s
 spec, dense bf16 MFMA ~2.5 PFLOP/s, block-scaled fp8 ~5 PFLOP/s.  A GPU that
 fails a threshold or the memtest marks the node not-ready.
+
+In a node agent (:func:`set_burnin_process`) each GPU's burn-in -- and the node's xGMI
+link matrix (:func:`link_matrix_process`) -- runs in a ``gpu-burnin`` child process: the
+agent's own HIP runtime is busy loading RCCL's device code for the cluster gate meanwhile.
+The child reports its measurements, this module judges them against the same floors as
+the in-process path, and the child keeps the HBM it tested until the agent's release hold
+(:func:`set_release_hold`) lets go.
 """
 
 import contextlib
