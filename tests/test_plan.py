@@ -9,7 +9,6 @@ import subprocess
 
 import pytest
 
-from triton_kubernetes_amd import versions
 from triton_kubernetes_amd.terraform import catalog, hcl
 from triton_kubernetes_amd.terraform.plan import UNKNOWN, _Scope, evaluate, plan_module
 

@@ -21,13 +21,13 @@ from triton_kubernetes_amd.errors import TKError
 from triton_kubernetes_amd.executor.direct import DirectExecutor
 from triton_kubernetes_amd.node.agent import NodeAgent
 from triton_kubernetes_amd.node.labels import synthetic_topology
-from triton_kubernetes_amd.parallel.transport import AgentTransport, RecordingTransport, TransportRouter
+from triton_kubernetes_amd.parallel.transport import RecordingTransport
 from triton_kubernetes_amd.rancher import bootstrap_secret, trust
 from triton_kubernetes_amd.rancher.client import RancherClient
 from triton_kubernetes_amd.rancher.fake import FakeRancher
 from triton_kubernetes_amd.terraform import catalog
 
-from helpers import make_ctx, output
+from helpers import make_ctx
 
 PW = "tk-admin-pw-0123"
 TOKEN = "ca-pin-token-0123456"

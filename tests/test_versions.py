@@ -6,7 +6,6 @@ Reference: ``/root/reference/create/cluster.go:349-356`` (k8s choices of its pin
 server) and ``/root/reference/terraform/modules/triton-rancher/variables.tf:14-22``.
 """
 
-import hashlib
 import os
 import re
 

@@ -27,7 +27,7 @@ from typing import Any, Callable, Dict, List, Optional, Sequence, Tuple
 
 from ..utils.trace import span
 from . import native
-from .native import LIB_DIR, load
+from .native import load
 
 # MI355X reference figures (dense; never the 2:1-sparsity marketing numbers)
 MI355X_HBM_ACHIEVABLE_GBPS = 6300.0
