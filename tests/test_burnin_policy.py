@@ -427,6 +427,7 @@ def test_agent_release_hold_waits_for_running_rccl_inits(monkeypatch):
         return running[0]
 
     monkeypatch.setattr(rccl, "inits_running", inits)
+    monkeypatch.setattr(rccl, "preloads_running", lambda: 0)
     a = NodeAgent(name="h", mode="sim", token="t" * 20)
     a._await_rccl_inits()
     assert running[0] == 0
@@ -507,6 +508,7 @@ def test_release_hold_also_waits_for_the_plans_link_matrix(monkeypatch):
     from triton_kubernetes_amd.ops import rccl
 
     monkeypatch.setattr(rccl, "inits_running", lambda: 0)
+    monkeypatch.setattr(rccl, "preloads_running", lambda: 0)
     a = NodeAgent(name="h", mode="sim", token="t" * 20)
     a._links_pending = True
     done = threading.Event()
@@ -516,3 +518,19 @@ def test_release_hold_also_waits_for_the_plans_link_matrix(monkeypatch):
     assert not done.is_set()  # still held: the link matrix is yet to be measured
     a._links_pending = False
     assert done.wait(2.0)
+
+
+def test_preload_exports_and_stub_abi():
+    """libtk_rccl exports the device-code preload and its counter; the ABI stub answers
+    "nothing to preload" (no RCCL device code behind it)."""
+    import ctypes
+    import os
+
+    from triton_kubernetes_amd.ops import native
+
+    stub = ctypes.CDLL(os.path.join(native.LIB_DIR, "libtk_rccl_stub.so"))
+    assert stub.tkr_preload_device_code(1, (ctypes.c_int * 1)(0)) == 1
+    assert stub.tkr_preloads_running() == 0
+    out = __import__("subprocess").run(["nm", "-D", os.path.join(native.LIB_DIR, "libtk_rccl.so")],
+                                       capture_output=True, text=True).stdout
+    assert " T tkr_preload_device_code" in out and " T tkr_preloads_running" in out and " T tkr_inits_running" in out

@@ -265,6 +265,10 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         probe._lib()
         rccl._lib()
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
+        if os.environ.get("TK_RCCL_PRELOAD", "0") == "1":
+            # RCCL's device code starts loading now, beside the rest of the start-up, not
+            # after the cluster gate's first request (tkr_preload_device_code)
+            self.startup_ms["rccl_preload_started"] = float(rccl.preload_device_code(self.devices))
         # the full burn-in's ~300 GB memtest memory is released off the bring-up path
         probe.set_async_free(True)
         # ... and the full memtest's ~300 GB is held and released by a gpu-burnin child, so no
@@ -400,6 +404,12 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             from ..ops import rccl
 
             rccl.drain()
+        if self.devices and self.topology_override is None:
+            from ..ops import rccl
+
+            deadline = time.monotonic() + 60.0  # a device-code preload still running: let it end
+            while rccl.preloads_running() > 0 and time.monotonic() < deadline:
+                time.sleep(0.01)
         if self.devices and self.topology_override is None and self.burnin_override is None:
             from ..ops import probe
 

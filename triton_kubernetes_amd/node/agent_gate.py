@@ -100,7 +100,8 @@ class AgentGateMixin:
         from ..ops import rccl
 
         deadline = time.monotonic() + self.RELEASE_HOLD_S
-        while (rccl.inits_running() > 0 or getattr(self, "_links_pending", False)) and time.monotonic() < deadline:
+        while ((rccl.inits_running() > 0 or rccl.preloads_running() > 0 or getattr(self, "_links_pending", False))
+               and time.monotonic() < deadline):
             time.sleep(0.005)
 
     def _gate_devices(self, ndev: int) -> List[int]:

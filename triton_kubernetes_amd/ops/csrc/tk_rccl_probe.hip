@@ -26,6 +26,8 @@
 #include "tk_rccl_group.h"
 #include "tk_rccl_verify.h"
 
+#include <dlfcn.h>
+
 #include <climits>
 #include <string>
 #include <atomic>
@@ -335,6 +337,45 @@ extern "C" int tkr_gate_abandoned() { return g_abandoned.load(); }
 // up the init's copies and allocations (ops/probe.py:set_release_hold)
 static std::atomic<int> g_inits_running{0};
 extern "C" int tkr_inits_running() { return g_inits_running.load(); }
+
+// RCCL's device code for `devs`, loaded on background threads now (one per device), before
+// any communicator: a node agent calls this as it starts, so the load -- most of a fresh
+// process's first ncclCommInitRank, which finds the code resident afterwards
+// (profiles/round2/cold_rccl_init.md) -- overlaps the rest of its start-up instead of
+// following the gate's first request.  The load is triggered by the attributes query of
+// one kernel librccl exports; the runtime loads the library's whole code object for the
+// device then.  Returns 0 when started, 1 when this librccl exports no known kernel handle
+// (nothing started), -1 when librccl is not loaded.
+static std::atomic<int> g_preloads_running{0};
+extern "C" int tkr_preloads_running() { return g_preloads_running.load(); }
+
+extern "C" int tkr_preload_device_code(int ndev, const int* devs) {
+  void* lib = dlopen("librccl.so.1", RTLD_LAZY | RTLD_NOLOAD);
+  if (!lib) {
+    snprintf(g_err, sizeof(g_err), "librccl.so.1 is not loaded");
+    return -1;
+  }
+  static const char* kHandles[] = {"_Z23ncclDevKernel_Generic_124ncclDevKernelArgsStorageILm4096EE",
+                                   "_Z23ncclDevKernel_Generic_224ncclDevKernelArgsStorageILm4096EE"};
+  const void* handle = nullptr;
+  for (const char* name : kHandles)
+    if ((handle = dlsym(lib, name)) != nullptr) break;
+  dlclose(lib);  // RTLD_NOLOAD took a reference of its own; the library stays loaded
+  if (!handle) return 1;
+  for (int i = 0; i < ndev; ++i) {
+    const int dev = devs[i];
+    g_preloads_running.fetch_add(1);
+    std::thread([dev, handle] {
+      if (hipSetDevice(dev) == hipSuccess) {
+        hipFuncAttributes a;
+        (void)hipFuncGetAttributes(&a, handle);
+        (void)hipGetLastError();
+      }
+      g_preloads_running.fetch_sub(1);
+    }).detach();
+  }
+  return 0;
+}
 
 static Gate* take_gate(int h) {
   std::lock_guard<std::mutex> lk(g_gate_mu);

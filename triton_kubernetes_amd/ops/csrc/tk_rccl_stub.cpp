@@ -165,6 +165,8 @@ int tkr_teardowns_pending() { return 0; }
 int tkr_drain() { return 0; }
 int tkr_gate_abandoned() { return 0; }
 int tkr_inits_running() { return 0; }  // no device code to load: nothing a release could hold up
+int tkr_preloads_running() { return 0; }
+int tkr_preload_device_code(int, const int*) { return 1; }  // no RCCL device code behind the stub
 int tkr_gate_pending() {
   std::lock_guard<std::mutex> lk(g_mu);
   return (int)g_gates.size();

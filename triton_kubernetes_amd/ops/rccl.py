@@ -221,6 +221,22 @@ def inits_running() -> int:
     return int(lib.tkr_inits_running()) if lib is not None else 0
 
 
+def preload_device_code(devices: Sequence[int]) -> bool:
+    """Start loading RCCL's device code for ``devices`` on background threads
+    (``tkr_preload_device_code``); True when started."""
+    devs = [int(d) for d in devices]
+    if not devs:
+        return False
+    return _lib().tkr_preload_device_code(len(devs), (ctypes.c_int * len(devs))(*devs)) == 0
+
+
+def preloads_running() -> int:
+    from . import native
+
+    lib = native._cache.get("libtk_rccl.so")
+    return int(lib.tkr_preloads_running()) if lib is not None else 0
+
+
 def exit_now(code: int = 0) -> None:
     """Leave the process without the HIP/RCCL exit teardown, which cannot complete while an
     abandoned init thread is blocked in RCCL's bootstrap.  Flushes stdio first."""
