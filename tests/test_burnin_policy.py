@@ -534,3 +534,41 @@ def test_preload_exports_and_stub_abi():
     out = __import__("subprocess").run(["nm", "-D", os.path.join(native.LIB_DIR, "libtk_rccl.so")],
                                        capture_output=True, text=True).stdout
     assert " T tkr_preload_device_code" in out and " T tkr_preloads_running" in out and " T tkr_inits_running" in out
+
+
+def test_eight_gpus_burn_in_concurrently_and_release_together(burnin_child, monkeypatch, tmp_path):
+    """An 8-GPU node: one child per GPU at once (the agent's pool), each told its own device,
+    each holding what it tested until the release hold lets go -- then all release."""
+    import concurrent.futures as cf
+    import json
+    import sys
+    import threading
+    import time
+
+    exe = tmp_path / "gpu-burnin"
+    exe.write_text(f"""#!{sys.executable}
+import json, os, sys, time
+dev = sys.argv[sys.argv.index("--device") + 1]
+doc = json.loads(os.environ["FAKE_CHILD_DOC"]); doc["device"] = int(dev)
+open(os.path.join({str(tmp_path)!r}, "started-" + dev), "w").write(str(time.monotonic()))
+print(json.dumps(doc), flush=True)
+if "--hold-stdin" in sys.argv:
+    sys.stdin.read()
+open(os.path.join({str(tmp_path)!r}, "released-" + dev), "w").write(str(time.monotonic()))
+""")
+    monkeypatch.setenv("FAKE_CHILD_DOC", json.dumps(CHILD_OK))
+    go = threading.Event()
+    probe.set_release_hold(go.wait)
+    try:
+        with cf.ThreadPoolExecutor(8) as pool:
+            results = list(pool.map(lambda d: probe.run_burnin(d, "full"), range(8)))
+        assert all(r.ok for r in results) and sorted(r.device.index for r in results) == list(range(8))
+        assert len(list(tmp_path.glob("started-*"))) == 8
+        time.sleep(0.2)
+        assert not list(tmp_path.glob("released-*"))  # every GPU's HBM still held
+        go.set()
+        probe.wait_frees()
+        assert sorted(p.name for p in tmp_path.glob("released-*")) == [f"released-{d}" for d in range(8)]
+    finally:
+        go.set()
+        probe.set_release_hold(None)
