@@ -336,6 +336,14 @@ def test_burnin_child_passes_levels_and_floors_and_is_judged_here(burnin_child, 
     opts = dict(zip(argv[3::2], argv[4::2]))
     assert opts["--hbm-bytes"] == str(hbm_bytes) and opts["--memtest-bytes"] == "0" and opts["--memtest-passes"] == "3"
     assert opts["--gemm"] == "8192,8192,8192,5" and opts["--span-chunk"] == str(probe.SPAN_CHILD_CHUNK)
+    assert opts["--span-headroom"] == str(4 << 30)
+    probe.set_span_headroom((4 << 30) + 7 * (512 << 20))  # an 8-GPU node's agent
+    try:
+        probe.run_burnin(0, "full")
+        opts = dict(zip(burnin_child.read_text().split()[3::2], burnin_child.read_text().split()[4::2]))
+        assert opts["--span-headroom"] == str((4 << 30) + 7 * (512 << 20))
+    finally:
+        probe.set_span_headroom(4 << 30)
     assert float(opts["--min-read-gbps"]) == pytest.approx(probe._floors(probe.Thresholds())["read"], rel=1e-3)
     labels = __import__("triton_kubernetes_amd.node.labels", fromlist=["burnin_labels"]).burnin_labels(
         "full", {0: res.to_json()})

@@ -279,6 +279,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         # (ops/probe.py:_burnin_child)
         burnin_child = os.environ.get("TK_BURNIN_PROCESS", "1") != "0"
         probe.set_burnin_process(burnin_child)
+        # the gate's communicator over this node's GPUs allocates while the span is held
+        probe.set_span_headroom((4 << 30) + (512 << 20) * max(0, len(self.devices) - 1))
         # ...and releases the HBM it tested only once this agent's RCCL communicator inits
         # are through: the driver's clearing of that release held their device-code load up
         if os.environ.get("TK_BURNIN_RELEASE_HOLD", "1") != "0":

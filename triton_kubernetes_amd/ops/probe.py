@@ -599,6 +599,18 @@ def _judge(res: BurninResult, th: Thresholds, first_bad: Dict[str, Optional[Dict
     return res
 
 
+# HBM a full span leaves free.  A node agent's cluster-gate communicator allocates its
+# buffers (per channel and peer, plus RCCL's device code on every GPU) while a child holds its
+# span -- the release waits for the init -- so a node of several GPUs leaves more
+# (set_span_headroom; node/agent.py: 4 GiB + 512 MiB per further GPU of the node).
+SPAN_HEADROOM = 4 << 30
+
+
+def set_span_headroom(nbytes: int) -> None:
+    global SPAN_HEADROOM
+    SPAN_HEADROOM = max(1 << 30, int(nbytes))
+
+
 def _burnin_child(dev: int, level: str, th: Thresholds, timeout: float = 900.0) -> BurninResult:
     """:func:`run_burnin` in a ``gpu-burnin --burnin-child`` process (see above): the span
     memtest's memory is released by the child after its verdict (joined by :func:`wait_frees`)."""
@@ -613,7 +625,7 @@ def _burnin_child(dev: int, level: str, th: Thresholds, timeout: float = 900.0) 
     argv = [exe, "--burnin-child", "--device", str(int(dev)), "--hbm-bytes", str(hbm_bytes),
             "--hbm-iters", str(hbm_iters), "--mfma-iters", str(mfma_iters), "--gemm", f"{m},{n},{k},{reps}",
             "--memtest-bytes", str(mt_bytes), "--memtest-passes", str(mt_passes),
-            "--span-headroom", str(4 << 30), "--span-chunk", str(SPAN_CHILD_CHUNK),
+            "--span-headroom", str(int(SPAN_HEADROOM)), "--span-chunk", str(SPAN_CHILD_CHUNK),
             "--min-read-gbps", f"{fl['read']:.3f}", "--min-bf16-tflops", f"{fl['bf16']:.3f}",
             "--min-fp8-tflops", f"{fl['fp8']:.3f}", "--min-gemm-tflops", f"{fl['gemm_bf16']:.3f}",
             "--min-gemm-fp8-tflops", f"{fl['gemm_fp8']:.3f}"]
