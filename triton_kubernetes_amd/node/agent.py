@@ -265,7 +265,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         probe._lib()
         rccl._lib()
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
-        if os.environ.get("TK_RCCL_PRELOAD", "0") == "1":
+        preload = os.environ.get("TK_RCCL_PRELOAD", "0")
+        if preload == "1":
             # RCCL's device code starts loading now, beside the rest of the start-up, not
             # after the cluster gate's first request (tkr_preload_device_code)
             self.startup_ms["rccl_preload_started"] = float(rccl.preload_device_code(self.devices))
@@ -301,6 +302,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         t2 = time.perf_counter()
         self._refill_uid()  # the first gate's unique id, ready before any request
         self.startup_ms["uid"] = round((time.perf_counter() - t2) * 1e3, 1)
+        if preload == "after-uid":  # the same, once RCCL's bootstrap has made the unique id
+            self.startup_ms["rccl_preload_started"] = float(rccl.preload_device_code(self.devices))
         try:
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later
