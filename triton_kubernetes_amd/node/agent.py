@@ -265,7 +265,9 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         probe._lib()
         rccl._lib()
         self.startup_ms["dlopen"] = round((time.perf_counter() - t0) * 1e3, 1)
-        preload = os.environ.get("TK_RCCL_PRELOAD", "0")
+        # 1 (default): right after dlopen; after-uid: once the unique id is made; 0: off
+        # (profiles/round5/rccl_preload_ab.jsonl: the gate's init 1.81 -> 1.73 s)
+        preload = os.environ.get("TK_RCCL_PRELOAD", "1")
         if preload == "1":
             # RCCL's device code starts loading now, beside the rest of the start-up, not
             # after the cluster gate's first request (tkr_preload_device_code)
