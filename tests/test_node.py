@@ -527,3 +527,24 @@ def test_agent_applies_the_node_rccl_env_to_its_own_gate(tmp_path, monkeypatch):
         assert again == {"NCCL_SOCKET_IFNAME": "=bond1", "HSA_NO_SCRATCH_RECLAIM": "1"} and env["NCCL_DEBUG"] == "INFO"
     finally:
         agent.stop()
+
+
+def test_sequential_plans_run_the_burn_in_after_the_rccl_check():
+    """A shell runs one step after another: the burn-in goes after the node's RCCL check (its
+    release is cleared by the driver for seconds after it); an agent keeps the burn-in first
+    and overlaps it with the gate's communicator start."""
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.terraform import catalog
+
+    cfg = {"hostname": "g", "rancher_host_labels": {"worker": "true"}, "gpu_count": 8}
+    agent = build_host_plan(cfg, "https://r", "tok", "ca", mi355x=True).step_names()
+    shell = build_host_plan(cfg, "https://r", "tok", "ca", mi355x=True, sequential=True).step_names()
+    assert agent.index("gpu_burnin") < agent.index("rccl_local")
+    assert shell.index("gpu_links") < shell.index("rccl_local") < shell.index("gpu_burnin") < shell.index("agent")
+    assert sorted(agent) == sorted(shell)
+    one = dict(cfg, gpu_count=1)  # no RCCL check on one GPU: the order stays
+    assert build_host_plan(one, "https://r", "tok", "ca", mi355x=True, sequential=True).step_names() == \
+        build_host_plan(one, "https://r", "tok", "ca", mi355x=True).step_names()
+    script = open(os.path.join(catalog.MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files",
+                               "install_mi355x_node.sh.tftpl")).read()
+    assert script.index("gpu-burnin --p2p") < script.index("$RCCL_READY --ngpus") < script.index("gpu-burnin --all")

@@ -512,7 +512,7 @@ class DirectExecutor(Executor):
         ref = HostRef(str(cfg.get("host", "")), cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "",
                       cfg.get("bastion_host") or "")
         plan = build_host_plan(cfg, cfg["rancher_api_url"], cfg["rancher_cluster_registration_token"],
-                               cfg["rancher_cluster_ca_checksum"], mi355x=mi355x)
+                               cfg["rancher_cluster_ca_checksum"], mi355x=mi355x, sequential=ref.scheme != "agent")
         if mi355x and self.upload_tools and ref.scheme == "ssh":
             self._upload_tools(ref)
         result = self.transport.run_plan(ref, plan, timeout=self.node_timeout)

@@ -167,8 +167,14 @@ def host_role(cfg: Dict[str, Any]) -> str:
 
 
 def build_host_plan(cfg: Dict[str, Any], rancher_url: str, token: str, ca_checksum: str,
-                    mi355x: bool = False) -> BootstrapPlan:
-    """Plan for a ``*-rancher-k8s-host`` module config with resolved interpolations."""
+                    mi355x: bool = False, sequential: bool = False) -> BootstrapPlan:
+    """Plan for a ``*-rancher-k8s-host`` module config with resolved interpolations.
+
+    ``sequential``: the plan runs as one shell script (SSH, cloud-init), each step after the
+    previous.  The burn-in then goes after the node's RCCL check: the driver clears the
+    ~300 GB per GPU it releases for seconds afterwards, and a communicator started meanwhile
+    waits behind that (profiles/round5/README.md).  A node agent runs the default order:
+    it overlaps the burn-in with the gate's communicator start and holds the release."""
     role = host_role(cfg)
     hostname = cfg.get("hostname", "")
     dist = str(cfg.get("k8s_distribution") or DEFAULT_DISTRIBUTION)
@@ -348,6 +354,10 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
             f"--token {_q(token)} --ca-checksum {_q(ca_checksum)} --node-name {_q(hostname)} --{role}{label_args}\n"
             + record),
             {"server": rancher_url, "role": role, "distribution": "rke2"}))
+    names = plan.step_names()
+    if sequential and "gpu_burnin" in names and "rccl_local" in names:
+        burn = plan.steps.pop(names.index("gpu_burnin"))
+        plan.steps.insert(plan.step_names().index("rccl_local") + 1, burn)
     return plan
 
 

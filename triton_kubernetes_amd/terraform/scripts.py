@@ -524,10 +524,6 @@ sudo rm -f /etc/triton-kubernetes/gpu-burnin-labels /etc/triton-kubernetes/gpu-t
 $T/gpu-burnin --p2p --min-link-frac ${gpu_link_min_frac} --min-link-gbps ${gpu_link_min_gbps} --labels /tmp/tk-link-labels | sudo tee /etc/triton-kubernetes/gpu-links.json
 cat /tmp/tk-link-labels | sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels >/dev/null
 %{ endif ~}
-%{ if gpu_burnin != "off" ~}
-$T/gpu-burnin --all --level '${gpu_burnin}' --compute-partition ${gpu_compute_partition} --memory-partition ${gpu_memory_partition} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
-sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels < /tmp/tk-burnin-labels >/dev/null
-%{ endif ~}
 %{ if gpu_health != "off" ~}
 # GPU health (RAS): exit 3 = an unhealthy GPU; fail the node or join it tainted
 health_rc=0
@@ -556,6 +552,12 @@ TK_RCCL_EOF
 %{ if gpu_count * gpu_partitions > 1 ~}
 set -a; . /etc/rccl/rccl.env; set +a
 $RCCL_READY --ngpus ${gpu_count * gpu_partitions} --min-busbw ${rccl_min_busbw}
+%{ endif ~}
+# the burn-in last of the GPU steps: the driver clears the ~300 GB per GPU a full burn-in
+# releases for seconds afterwards, and an RCCL communicator started meanwhile waits behind it
+%{ if gpu_burnin != "off" ~}
+$T/gpu-burnin --all --level '${gpu_burnin}' --compute-partition ${gpu_compute_partition} --memory-partition ${gpu_memory_partition} --labels /tmp/tk-burnin-labels | sudo tee /etc/triton-kubernetes/gpu-burnin.json
+sudo tee -a /etc/triton-kubernetes/gpu-burnin-labels < /tmp/tk-burnin-labels >/dev/null
 %{ endif ~}
 labels=$(cat /etc/triton-kubernetes/gpu-labels $([ -r /etc/triton-kubernetes/gpu-burnin-labels ] && echo /etc/triton-kubernetes/gpu-burnin-labels) | sed 's/^/--label /' | tr '\n' ' ')
 if [ -r /etc/triton-kubernetes/gpu-taints ]; then labels="$labels $(sed 's/^/--taints /' /etc/triton-kubernetes/gpu-taints | tr '\n' ' ')"; fi

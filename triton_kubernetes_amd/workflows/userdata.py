@@ -41,7 +41,8 @@ def node_userdata(ctx: Context, backend: Backend) -> str:
     except Exception as exc:  # noqa: BLE001 - unapplied cluster
         raise TKError(f"node '{hostname}': cluster outputs are not available yet (apply the cluster first): {exc}")
     plan = build_host_plan(resolved, resolved["rancher_api_url"], resolved["rancher_cluster_registration_token"],
-                           resolved["rancher_cluster_ca_checksum"], mi355x=bool(info and info.mi355x))
+                           resolved["rancher_cluster_ca_checksum"], mi355x=bool(info and info.mi355x),
+                           sequential=True)
     text = render_cloud_init(plan, resolved.get("rccl_env") if info and info.mi355x else None)
     ctx.out.write(text)
     return text
