@@ -704,12 +704,16 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_mem_check(const uint4* __res
     bad += (v.x != w.x) + (v.y != w.y) + (v.z != w.z) + (v.w != w.w);
   };
   size_t i = sl.begin + threadIdx.x;
+  // non-temporal loads, as the read stream: the data is read once, and plain loads of a
+  // chunk the fill had just written ran at 4.6 TB/s instead of 6.7 on a 1 GiB chunk
+  // (scripts/memtest_variants.hip; the fill keeps plain stores, 6.6 vs 5.9 TB/s)
+  const u32x4* q = reinterpret_cast<const u32x4*>(p);
   for (; i + (STREAM_UNROLL - 1) * STREAM_THREADS < sl.end; i += STREAM_UNROLL * STREAM_THREADS) {
-    uint4 v[STREAM_UNROLL];
+    u32x4 v[STREAM_UNROLL];
 #pragma unroll
-    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = p[i + u * STREAM_THREADS];
+    for (int u = 0; u < STREAM_UNROLL; ++u) v[u] = __builtin_nontemporal_load(q + i + u * STREAM_THREADS);
 #pragma unroll
-    for (int u = 0; u < STREAM_UNROLL; ++u) cmp(v[u], i + u * STREAM_THREADS);
+    for (int u = 0; u < STREAM_UNROLL; ++u) cmp(make_uint4(v[u].x, v[u].y, v[u].z, v[u].w), i + u * STREAM_THREADS);
   }
   for (; i < sl.end; i += STREAM_THREADS) cmp(p[i], i);
   // wave-level reduction: 64 lanes
