@@ -1,6 +1,7 @@
 #!/bin/bash
 # Host-code sanitizers on the MI355X: rccl-ready and gpu-burnin built with ASan/UBSan on the
 # host side only (device code is not instrumented), run against the real GPU.
+#   (.gpurunignore lists the two -asan binaries: drop those lines to send them with a gpurun call)
 #   build (CPU container): hipcc ... -Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined
 #                          -fno-gpu-sanitize  -> scripts/native/{rccl-ready,gpu-burnin}-asan
 set -o pipefail
