@@ -1351,10 +1351,16 @@ static void hold_until_released(bool hold, int max_ms) {
 // printed and flushed and every file closed by then, so the tool leaves with _exit and the
 // kernel reclaims the memory without the caller waiting: `gpu-burnin --all --level full`
 // 3.13 s -> 0.60 s (profiles/round5/README.md).  TK_BURNIN_EXIT=normal keeps the teardown
-// (host sanitizer runs, whose leak check runs at exit).
+// (host sanitizer runs, whose leak check runs at exit); so does running under rocprofv3.
 static bool quick_exit_wanted() {
   const char* m = getenv("TK_BURNIN_EXIT");
-  return !(m && !strcmp(m, "normal"));
+  if (m && !strcmp(m, "normal")) return false;
+  // a profiler's preloaded tool (rocprofv3) writes its results in the normal exit path
+  const char* pre = getenv("LD_PRELOAD");
+  if (pre && strstr(pre, "rocprof")) return false;
+  for (char** e = environ; e && *e; ++e)
+    if (!strncmp(*e, "ROCPROF", 7)) return false;
+  return true;
 }
 
 static void json_escape(const char* in, char* out, size_t cap) {
