@@ -175,3 +175,14 @@ def test_agent_unit_gives_comgr_a_cache_dir():
     unit = open(os.path.join(packer.FILES_DIR, "tk-node-agent.service")).read()
     assert "Environment=AMD_COMGR_CACHE_DIR=/var/cache/triton-kubernetes/comgr" in unit
     assert "CacheDirectory=triton-kubernetes/comgr" in unit
+
+
+def test_prewarm_is_one_device_code_load_in_a_throwaway_process():
+    """A fresh box's cold code-object cache is filled before the timed region, the way a
+    booted node's agent fills it: one preload of RCCL's device code, nothing else."""
+    import bench
+
+    code = bench._prewarm_code()
+    compile(code, "<prewarm>", "exec")
+    assert "rccl.preload_device_code([0])" in code and "GateComm" not in code
+    assert bench.COMGR_WARM_MIB < 540  # librccl's unbundled gfx950 code, once cached
