@@ -18,6 +18,8 @@ timeout -k 10 120 $B/rccl-ready-asan --ngpus 1 --iters 3 --max-mib 8 > gpurun_ou
        --mfma-iters 2000 --gemm 4096,4096,4096,2 --memtest-bytes 0 --memtest-passes 1 --span-chunk 1073741824 \
        > gpurun_out/asan_burnin_child_full.log 2>&1 \
   && timeout -k 10 120 $B/gpu-burnin-asan --p2p-child --devices 0 > gpurun_out/asan_p2p_child.log 2>&1 \
+  && timeout -k 10 120 $B/rccl-ready-asan --ngpus 1 --iters 3 --max-mib 8 --preload \
+       > gpurun_out/asan_rccl_ready_preload.log 2>&1 \
   && timeout -k 10 300 $B/gpu-burnin-asan --all --level full > gpurun_out/asan_burnin_all_full.log 2>&1
 rc=$?
 echo "host_asan rc=$rc"

@@ -886,7 +886,7 @@ int main(int argc, char** argv) {
   }
   double min_busbw = 0.0, timeout_s = 600.0;
   int iters = 20, warmup = 5, dtype = 0, world = 0, rank_base = 0, max_mib = 64;
-  bool cluster = false, uid_out = false, max_set = false;
+  bool cluster = false, uid_out = false, max_set = false, preload = false;
   const char* uid_hex = nullptr;
   const char* expect_rccl = nullptr;  // --expect-rccl: the librccl this process must have mapped
   const int visible = ndev;
@@ -903,11 +903,22 @@ int main(int argc, char** argv) {
     else if (!strcmp(argv[i], "--max-mib") && i + 1 < argc) { max_mib = atoi(argv[++i]); max_set = true; }
     else if (!strcmp(argv[i], "--timeout-s") && i + 1 < argc) timeout_s = atof(argv[++i]);
     else if (!strcmp(argv[i], "--expect-rccl") && i + 1 < argc) expect_rccl = argv[++i];
+    else if (!strcmp(argv[i], "--preload")) preload = true;  // tkr_preload_device_code first
   }
   if (ndev < 1 || ndev > visible) {
     fprintf(stderr, "{\"error\":\"--ngpus %d but %d visible\"}\n", ndev, visible);
     return 3;
   }
+  if (preload) {  // what a node agent does at start (the communicator then finds the code loaded)
+    std::vector<int> devs(ndev);
+    for (int d = 0; d < ndev; ++d) devs[d] = d;
+    if (tkr_preload_device_code(ndev, devs.data()) < 0) fprintf(stderr, "preload: %s\n", g_err);
+  }
+  struct PreloadJoin {  // no preload thread outlives main
+    ~PreloadJoin() {
+      while (tkr_preloads_running() > 0) std::this_thread::sleep_for(std::chrono::milliseconds(5));
+    }
+  } preload_join;
   if (cluster) {
     if (world < ndev || rank_base < 0 || rank_base + ndev > world || (!uid_out && !uid_hex) || max_mib < 1) {
       fprintf(stderr, "{\"error\":\"cluster mode needs --world >= --rank-base + --ngpus and --uid or --uid-out\"}\n");
