@@ -355,7 +355,9 @@ def test_installer_fetched_over_tls_pinned_by_the_ca_checksum(tmp_path, tamper):
         bindir = tmp_path / "bin"
         bindir.mkdir()
         log = tmp_path / "sudo.log"
-        (bindir / "sudo").write_text(f'#!/bin/sh\necho "$*" >> {log}\n')
+        # drains stdin like the real command would (a step's stdin is /dev/null; `printf | sudo
+        # tee` must not see its reader exit early: SIGPIPE under pipefail failed the step)
+        (bindir / "sudo").write_text(f'#!/bin/sh\necho "$*" >> {log}\ncat >/dev/null 2>&1 || true\n')
         (bindir / "sudo").chmod(0o755)
         shell_plan = build_host_plan({"hostname": "w-1", "rancher_host_labels": {"worker": "true"}}, url, "tok",
                                      checksum)
