@@ -548,3 +548,27 @@ def test_sequential_plans_run_the_burn_in_after_the_rccl_check():
     script = open(os.path.join(catalog.MODULES_DIR, "bare-metal-mi355x-rancher-k8s-host", "files",
                                "install_mi355x_node.sh.tftpl")).read()
     assert script.index("gpu-burnin --p2p") < script.index("$RCCL_READY --ngpus") < script.index("gpu-burnin --all")
+
+
+# a reader that stops early (grep -q, head) ends its writer with SIGPIPE, and under pipefail
+# that fails the pipeline even when the match was found: "amdgpu not loaded" on a node
+# whose lsmod output outgrew one pipe write
+_EARLY_READER = r"\|\s*(grep\s+-[A-Za-z]*q|head\b)"
+
+
+def test_rendered_shell_has_no_early_exit_readers():
+    import re
+
+    from triton_kubernetes_amd.terraform import generate
+
+    reg = dict(GPU_WORKER, rancher_registry="reg.io", rancher_registry_username="u", rancher_registry_password="p",
+               rccl_slim="on")
+    scripts = {"plan": build_host_plan(reg, "https://r", "t", "s", mi355x=True, sequential=True).render_shell(),
+               "plan-rke1": build_host_plan(dict(reg, k8s_distribution="rke1"), "https://r", "t", "s",
+                                            mi355x=True).render_shell()}
+    for mod in generate.modules():
+        for name, text in generate.rendered_files(mod).items():
+            if name.endswith((".sh", ".tftpl")):
+                scripts[f"{mod}/{name}"] = text
+    bad = {k: m.group(0) for k, s in scripts.items() for m in [re.search(_EARLY_READER, s)] if m}
+    assert not bad, bad

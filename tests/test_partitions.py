@@ -151,7 +151,7 @@ def test_shell_preflight_on_fixture_trees(tmp_path, cfg_modes, tree, ok):
            "gpu_compute_partition": cfg_modes[0], "gpu_memory_partition": cfg_modes[1]}
     plan = build_host_plan(cfg, "https://r", "t", "s", mi355x=True)
     step = next(s for s in plan.steps if s.name == "gpu_preflight")
-    body = (step.shell.replace("lsmod | grep -q '^amdgpu' ||", "true ||").replace("test -c /dev/kfd", "true")
+    body = (step.shell.replace("lsmod | grep '^amdgpu' >/dev/null ||", "true ||").replace("test -c /dev/kfd", "true")
             .replace("/dev/", f"{root}/dev/").replace("/sys/", f"{root}/sys/").replace("/etc/", f"{root}/etc/")
             .replace("sudo ", ""))
     bindir = tmp_path / "bin"

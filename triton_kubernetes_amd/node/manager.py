@@ -50,7 +50,7 @@ if command -v firewalld >/dev/null 2>&1; then sudo systemctl disable --now firew
   sudo systemctl restart docker
 fi
 {login}sudo docker pull {_q(image)}
-if ! sudo docker ps --format '{{{{.Image}}}}' | grep -qx {_q(image)}; then
+if ! sudo docker ps --format '{{{{.Image}}}}' | grep -x {_q(image)} >/dev/null; then
   # the first-login password through a 0600 env file, removed once the container runs:
   # never on a command line (ps) -- rancher/bootstrap_secret.py
   envf=$(umask 077; mktemp)

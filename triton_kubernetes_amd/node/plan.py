@@ -220,7 +220,7 @@ fi""", {"install_url": install_url}))
         plan.gpu = {"product": cfg.get("gpu_product", "MI355X"), "count": ngpu, "burnin": burnin,
                     "physical": physical, "compute_partition": cpart, "memory_partition": mpart}
         plan.steps.append(Step("gpu_preflight", "gpu_preflight", f"""
-lsmod | grep -q '^amdgpu' || {{ echo 'amdgpu kernel module not loaded' >&2; exit 1; }}
+lsmod | grep '^amdgpu' >/dev/null || {{ echo 'amdgpu kernel module not loaded' >&2; exit 1; }}
 test -c /dev/kfd || {{ echo '/dev/kfd missing' >&2; exit 1; }}
 test -d /dev/dri || {{ echo '/dev/dri missing' >&2; exit 1; }}
 local found f m

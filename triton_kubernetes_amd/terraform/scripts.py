@@ -50,7 +50,7 @@ set -euo pipefail
 for i in $(seq 1 600); do command -v docker >/dev/null 2>&1 && break; sleep 1; done
 for i in $(seq 1 600); do sudo docker image inspect '${rancher_server_image}' >/dev/null 2>&1 && break; sudo docker pull '${rancher_server_image}' || sleep 1; done
 [ -n '${bootstrap_password}' ] || { echo 'rancher_bootstrap_password is empty (the CLI passes the random one it keeps in the state backend)' >&2; exit 1; }
-if ! sudo docker ps --format '{{.Image}}' | grep -qx '${rancher_server_image}'; then
+if ! sudo docker ps --format '{{.Image}}' | grep -x '${rancher_server_image}' >/dev/null; then
   # Rancher >= 2.6 has no admin/admin: the first login uses this bootstrap password (random,
   # kept in the state backend: rancher/bootstrap_secret.py), handed over in a 0600 env file
   # that is removed once the container runs -- never on a command line
@@ -484,7 +484,7 @@ set -euo pipefail
 T=/opt/triton-kubernetes/bin
 S=/opt/triton-kubernetes/src
 sudo mkdir -p $T /etc/triton-kubernetes /etc/rccl
-lsmod | grep -q '^amdgpu' || { echo 'amdgpu kernel module not loaded' >&2; exit 1; }
+lsmod | grep '^amdgpu' >/dev/null || { echo 'amdgpu kernel module not loaded' >&2; exit 1; }
 test -c /dev/kfd || { echo '/dev/kfd missing' >&2; exit 1; }
 n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
 [ "$n" -ge ${gpu_count * gpu_partitions} ] || { echo "expected ${gpu_count * gpu_partitions} GPUs (${gpu_count} x ${gpu_compute_partition}), found $n render nodes" >&2; exit 1; }
