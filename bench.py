@@ -43,7 +43,8 @@ first loads RCCL's device code once in a throw-away process, as a booted node's 
 ``ms_per_step`` is the whole step including the agent shutdown.  A WARM number (the
 same create against agents kept resident across steps, round 1's headline) is
 reported only as the secondary ``warm_create_to_ready_s``, measured after the timed
-region.
+region, each create after the same untimed HBM settle as a cold step
+(``warm_hbm_settle_s``: the previous create's burn-in release being cleared).
 
 The cluster is an RKE2 custom cluster (``provisioning.cattle.io/v1``, the default
 distribution of the pinned Rancher v2.10.3, versions.py).  Simulated
@@ -553,14 +554,18 @@ def main() -> int:
     trace = TRACER.report()
 
     # secondary: warm creates against agents kept resident (outside the timed region)
-    warm = []
+    warm, warm_settles, warm_detail = [], [], []
     if args.warm_steps > 0:
         procs = start_agents("warm")
         urls = gather_urls(procs)
         for i in range(args.warm_steps + 1):  # the first one warms the agents, untimed
+            # as before a cold step: the previous create's burn-in released ~300 GB per GPU,
+            # which the driver clears before a node takes its next cluster (untimed)
+            warm_settles.append(settle()["waited_s"])
+            barrier()
             t0 = time.perf_counter()
             if rank == 0:
-                create(1000 + i, urls)
+                warm_detail.append(create(1000 + i, urls))
             if distributed:
                 dist.barrier()
             if i:
@@ -650,6 +655,10 @@ def main() -> int:
             "create_to_ready_s": ready,
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),
             "warm_create_to_ready_s": round(sum(warm) / len(warm), 4) if warm else None,
+            "warm_create_to_ready_each_s": [round(w, 4) for w in warm],
+            "warm_hbm_settle_s": [round(w, 3) for w in warm_settles],
+            "warm_gpu_burnin_ms": [d.get("gpu_node_step_ms", {}).get("gpu_burnin") for d in warm_detail[1:]],
+            "warm_rccl_init_ms": [(d.get("rccl") or {}).get("init_total") for d in warm_detail[1:]],
             # GPU nodes that joined with the health taint in any timed step (normally none)
             "gpu_unhealthy_nodes": sorted({h for r in results for h in r.get("gpu_unhealthy", [])}),
             # ranks of the cluster RCCL gate per timed step (every GPU of the worker tier)
@@ -671,7 +680,7 @@ def main() -> int:
         print(json.dumps(line), flush=True)
         if args.report:
             with open(args.report, "w", encoding="utf-8") as fh:
-                json.dump({"line": line, "steps": results, "warm_s": warm, "trace": trace}, fh, indent=1,
+                json.dump({"line": line, "steps": results, "warm_s": warm, "warm_steps": warm_detail, "trace": trace}, fh, indent=1,
                           default=str)
     devnull.close()
     if fake is not None:

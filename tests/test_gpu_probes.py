@@ -169,10 +169,12 @@ def test_process_gate_two_nodes_rendezvous_and_fail_fast(tmp_path):
 
 def test_link_matrix_child_matches_in_process():
     """The agent's links step runs ``gpu-burnin --p2p-child``: the same matrix form as the
-    in-process measurement, for every GPU of the box (none to measure on a one-GPU box)."""
+    in-process measurement, for every GPU of the box.  A one-GPU box lists GPU 0 three times
+    (pairs of a device with itself): the child's round-robin rounds, bye slot, peer reads and
+    data checks then run as on a multi-GPU node."""
     from triton_kubernetes_amd.ops import probe
 
-    devs = list(range(probe.device_count()))
+    devs = list(range(probe.device_count())) if probe.device_count() >= 2 else [0, 0, 0]
     child = probe.link_matrix_process(devs)
     here = probe.link_matrix(devs)
     assert set(child) == set(here) and child["method"] == here["method"] == "kernel-read"
