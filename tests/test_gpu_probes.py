@@ -61,6 +61,24 @@ def test_memtest_clean_and_detects_corruption(probe):
     assert probe.memtest_selfcheck(0, 64 << 20, 0) == 0
 
 
+def test_memtest_passes_are_complementary_pairs(probe):
+    """Pass 2k+1 writes the complement of pass 2k's pattern, so every bit is tested at 0 and
+    at 1.  A stuck-at-0 bit (fail point: bit 0 of N words cleared after each fill) then
+    mismatches in exactly one pass of the pair: two passes count exactly N, whatever the
+    pattern's value there (independent random patterns would count about N/2 per pass)."""
+    stuck = 4096
+    probe.set_fail_point(f"memtest.stuck0={stuck}")
+    try:
+        one = probe.memtest(0, 256 << 20, passes=1)
+        two = probe.memtest(0, 256 << 20, passes=2)
+        four = probe.memtest(0, 256 << 20, passes=4)
+    finally:
+        probe.set_fail_point("")
+    assert two["errors"] == stuck and four["errors"] == 2 * stuck, (one, two, four)
+    assert 0 < one["errors"] < stuck  # one pass alone sees only the words whose bit was 1
+    assert probe.memtest(0, 256 << 20, passes=2)["errors"] == 0
+
+
 def test_burnin_quick(probe):
     res = probe.run_burnin(0, "quick")
     print(json.dumps(res.to_json(), default=str))

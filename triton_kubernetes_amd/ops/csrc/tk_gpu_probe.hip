@@ -679,28 +679,40 @@ extern "C" int tkp_mfma_clock(int dev, int dtype, int iters, int blocks_per_cu, 
 // HBM pattern memtest: address-hash pattern, written and verified in
 // streaming passes; mismatches are counted per wave (ballot + popcount) and
 // added with one atomic per wave.
+// Passes come in complementary pairs (pass_pattern): pass 2k writes the pattern of seed k,
+// pass 2k+1 its bitwise complement, so with two or more passes every tested bit has held
+// both a 0 and a 1 (a stuck-at bit cannot hide).  Independent random patterns leave a bit
+// untested one way with probability 2^-(passes-1): a quarter of the bits after three.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ uint4 pattern(size_t i, uint32_t seed) {
+__device__ __forceinline__ uint4 pattern(size_t i, uint32_t seed, uint32_t flip = 0u) {
   const uint32_t h = hash32((uint32_t)i ^ seed ^ (uint32_t)(i >> 32) * 0x9e3779b9U);
-  return make_uint4(h, ~h, h ^ 0xa5a5a5a5U, h * 0x01000193U);
+  return make_uint4(h ^ flip, ~h ^ flip, h ^ 0xa5a5a5a5U ^ flip, (h * 0x01000193U) ^ flip);
 }
 
-__global__ __launch_bounds__(STREAM_THREADS) void k_mem_fill(uint4* __restrict__ p, size_t n, uint32_t seed) {
+// seed and complement mask of memtest pass `ps` (passes 2k and 2k+1 share seed k)
+static void pass_pattern(int ps, uint32_t base, uint32_t* seed, uint32_t* flip) {
+  *seed = base + 0x9e3779b9u * (uint32_t)(ps >> 1);
+  *flip = (ps & 1) ? 0xffffffffu : 0u;
+}
+
+__global__ __launch_bounds__(STREAM_THREADS) void k_mem_fill(uint4* __restrict__ p, size_t n, uint32_t seed,
+                                                              uint32_t flip) {
   const Slice sl = block_slice(n);  // same contiguous-slice traversal as the stream kernels
   size_t i = sl.begin + threadIdx.x;
   for (; i + (STREAM_UNROLL - 1) * STREAM_THREADS < sl.end; i += STREAM_UNROLL * STREAM_THREADS) {
 #pragma unroll
-    for (int u = 0; u < STREAM_UNROLL; ++u) p[i + u * STREAM_THREADS] = pattern(i + u * STREAM_THREADS, seed);
+    for (int u = 0; u < STREAM_UNROLL; ++u)
+      p[i + u * STREAM_THREADS] = pattern(i + u * STREAM_THREADS, seed, flip);
   }
-  for (; i < sl.end; i += STREAM_THREADS) p[i] = pattern(i, seed);
+  for (; i < sl.end; i += STREAM_THREADS) p[i] = pattern(i, seed, flip);
 }
 
 __global__ __launch_bounds__(STREAM_THREADS) void k_mem_check(const uint4* __restrict__ p, size_t n, uint32_t seed,
-                                                               unsigned long long* __restrict__ errors) {
+                                                               uint32_t flip, unsigned long long* __restrict__ errors) {
   const Slice sl = block_slice(n);
   uint32_t bad = 0;
   auto cmp = [&](const uint4 v, size_t j) {
-    const uint4 w = pattern(j, seed);
+    const uint4 w = pattern(j, seed, flip);
     bad += (v.x != w.x) + (v.y != w.y) + (v.z != w.z) + (v.w != w.w);
   };
   size_t i = sl.begin + threadIdx.x;
@@ -721,6 +733,15 @@ __global__ __launch_bounds__(STREAM_THREADS) void k_mem_check(const uint4* __res
   if ((threadIdx.x & 63) == 0 && bad) atomicAdd(errors, (unsigned long long)bad);
 }
 
+// Fail point "memtest.stuck0=N" (tests): after every fill, bit 0 of N words spread over the
+// buffer reads 0, as a stuck-at-0 cell would.  A bit written 1 mismatches once: in exactly
+// one pass of each complementary pair, so two passes count exactly N.
+__global__ void k_stuck0(uint32_t* w, size_t words, int count) {
+  const int k = blockIdx.x * blockDim.x + threadIdx.x;
+  if (k < count) w[(size_t)k * (words / (size_t)count)] &= ~1u;
+}
+static long fail_point_value(const char* prefix);
+
 // out[0] = mismatching 32-bit words, out[1] = verify GB/s of the last pass.
 extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   CHECK(hipSetDevice(dev));
@@ -738,10 +759,14 @@ extern "C" int tkp_memtest(int dev, size_t bytes, int passes, double* out) {
   const int grid = stream_grid(dev, 16);
   float ms = 0.f;
   for (int ps = 0; ps < (passes < 1 ? 1 : passes); ++ps) {
-    const uint32_t seed = 0x1234567u + 0x9e3779b9u * (uint32_t)ps;
-    k_mem_fill<<<grid, STREAM_THREADS, 0, s>>>(p, n, seed);
+    uint32_t seed, flip;
+    pass_pattern(ps, 0x1234567u, &seed, &flip);
+    k_mem_fill<<<grid, STREAM_THREADS, 0, s>>>(p, n, seed, flip);
+    const long stuck = fail_point_value("memtest.stuck0");
+    if (stuck > 0 && (size_t)stuck <= n * 4)
+      k_stuck0<<<(int)((stuck + 255) / 256), 256, 0, s>>>(reinterpret_cast<uint32_t*>(p), n * 4, (int)stuck);
     CHECK(hipEventRecord(t0, s));
-    k_mem_check<<<grid, STREAM_THREADS, 0, s>>>(p, n, seed, err);
+    k_mem_check<<<grid, STREAM_THREADS, 0, s>>>(p, n, seed, flip, err);
     CHECK(hipEventRecord(t1, s));
     CHECK(hipEventSynchronize(t1));
     CHECK(hipEventElapsedTime(&ms, t0, t1));
@@ -921,10 +946,11 @@ extern "C" int tkp_memtest_span(int dev, size_t bytes, size_t chunk, size_t head
   for (size_t c = 0; c < hold.chunks.size(); ++c) {
     const size_t n = sizes[c] / sizeof(uint4);
     for (int ps = 0; ps < (passes < 1 ? 1 : passes); ++ps) {
-      const uint32_t seed = 0x1234567u + 0x9e3779b9u * (uint32_t)ps + 0x85ebca6bu * (uint32_t)c;
-      k_mem_fill<<<grid, STREAM_THREADS, 0, hold.s>>>(hold.chunks[c], n, seed);
+      uint32_t seed, flip;
+      pass_pattern(ps, 0x1234567u + 0x85ebca6bu * (uint32_t)c, &seed, &flip);
+      k_mem_fill<<<grid, STREAM_THREADS, 0, hold.s>>>(hold.chunks[c], n, seed, flip);
       CHECK(hipEventRecord(hold.t0, hold.s));
-      k_mem_check<<<grid, STREAM_THREADS, 0, hold.s>>>(hold.chunks[c], n, seed, hold.err);
+      k_mem_check<<<grid, STREAM_THREADS, 0, hold.s>>>(hold.chunks[c], n, seed, flip, hold.err);
       CHECK(hipEventRecord(hold.t1, hold.s));
     }
     tested += sizes[c];
@@ -981,14 +1007,14 @@ extern "C" int tkp_memtest_selfcheck(int dev, size_t bytes, int corrupt, double*
   CHECK(hipMalloc(&err, sizeof(unsigned long long)));
   CHECK(hipMemset(err, 0, sizeof(unsigned long long)));
   const int grid = stream_grid(dev, 4);
-  k_mem_fill<<<grid, STREAM_THREADS>>>(p, n, 77u);
+  k_mem_fill<<<grid, STREAM_THREADS>>>(p, n, 77u, 0u);
   CHECK(hipDeviceSynchronize());
   for (int c = 0; c < corrupt && (size_t)c < n; ++c) {
     uint32_t junk = 0xdeadbeefu ^ (uint32_t)c;
     CHECK(hipMemcpy(reinterpret_cast<char*>(p + (size_t)c * (n / (corrupt + 1))), &junk, 4,
                     hipMemcpyHostToDevice));
   }
-  k_mem_check<<<grid, STREAM_THREADS>>>(p, n, 77u, err);
+  k_mem_check<<<grid, STREAM_THREADS>>>(p, n, 77u, 0u, err);
   CHECK(hipGetLastError());
   unsigned long long h = 0;
   CHECK(hipMemcpy(&h, err, sizeof(h), hipMemcpyDeviceToHost));
@@ -1126,7 +1152,7 @@ extern "C" int tkp_link_matrix_check(const int* devs, int n, size_t bytes, int i
     if (e == hipSuccess && check) e = hipMalloc(&bad[i], sizeof(unsigned long long));
     if (e == hipSuccess && check) {  // the sender's pattern, seeded by its index in devs
       k_mem_fill<<<stream_grid(devs[i], 16), STREAM_THREADS>>>(static_cast<uint4*>(buf[2 * i]), words4,
-                                                              0x11c0ffeeu + (uint32_t)i);
+                                                              0x11c0ffeeu + (uint32_t)i, 0u);
       e = hipGetLastError();
     }
     if (e == hipSuccess) e = hipStreamCreateWithFlags(&st[i], hipStreamNonBlocking);
@@ -1191,7 +1217,7 @@ extern "C" int tkp_link_matrix_check(const int* devs, int n, size_t bytes, int i
             }
             e = hipMemsetAsync(bad[dst], 0, sizeof(unsigned long long), st[dst]);
             if (e == hipSuccess) {
-              k_mem_check<<<grid[dst] * 4, STREAM_THREADS, 0, st[dst]>>>(got, words4, 0x11c0ffeeu + (uint32_t)src,
+              k_mem_check<<<grid[dst] * 4, STREAM_THREADS, 0, st[dst]>>>(got, words4, 0x11c0ffeeu + (uint32_t)src, 0u,
                                                                          bad[dst]);
               e = hipGetLastError();
             }
