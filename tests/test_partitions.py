@@ -255,3 +255,23 @@ def test_provider_and_module_accept_the_modes():
                                   "rancher_cluster_registration_token": "t",
                                   "rancher_cluster_ca_checksum": "c", "rancher_host_labels": {"worker": "true"}}) == []
     assert hcl.check_inputs(mod, {"gpu_compute_partition": "tpx"})
+
+
+def test_shell_preflight_without_render_nodes_says_so(tmp_path):
+    """Under the script's ``set -euo pipefail``, ``ls renderD* | wc -l`` fails when there is
+    no render node; the count must still come out as 0 and the step name the problem."""
+    import glob
+
+    from triton_kubernetes_amd.node.plan import build_host_plan
+
+    root = make_tree(str(tmp_path / "none"))
+    for f in glob.glob(f"{root}/dev/dri/renderD*"):
+        os.remove(f)
+    cfg = {"hostname": "g", "rancher_host_labels": {"worker": "true"}, "gpu_count": 8, "gpu_burnin": "off"}
+    step = next(s for s in build_host_plan(cfg, "https://r", "t", "s", mi355x=True).steps if s.name == "gpu_preflight")
+    body = (step.shell.replace("lsmod | grep '^amdgpu' >/dev/null ||", "true ||").replace("test -c /dev/kfd", "true")
+            .replace("/dev/", f"{root}/dev/").replace("/sys/", f"{root}/sys/").replace("/etc/", f"{root}/etc/")
+            .replace("sudo ", ""))
+    p = subprocess.run(["bash", "-c", "set -euo pipefail\nf() {\n" + body + "\n}\n( set -e; f )"], capture_output=True,
+                       text=True)
+    assert p.returncode == 1 and "found 0 render nodes" in p.stderr, (p.returncode, p.stderr)

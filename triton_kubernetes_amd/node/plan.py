@@ -224,7 +224,7 @@ lsmod | grep '^amdgpu' >/dev/null || {{ echo 'amdgpu kernel module not loaded' >
 test -c /dev/kfd || {{ echo '/dev/kfd missing' >&2; exit 1; }}
 test -d /dev/dri || {{ echo '/dev/dri missing' >&2; exit 1; }}
 local found f m
-found=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
+found=$(ls /dev/dri/renderD* 2>/dev/null | wc -l || true)  # pipefail: ls fails when there are none
 [ "$found" -ge {ngpu} ] || {{ echo "expected {ngpu} GPUs ({physical} x {cpart}), found $found render nodes" >&2; exit 1; }}
 for f in /sys/class/drm/renderD*/device/current_compute_partition /sys/class/drm/renderD*/device/current_memory_partition; do
   [ -r "$f" ] || continue

@@ -486,7 +486,7 @@ S=/opt/triton-kubernetes/src
 sudo mkdir -p $T /etc/triton-kubernetes /etc/rccl
 lsmod | grep '^amdgpu' >/dev/null || { echo 'amdgpu kernel module not loaded' >&2; exit 1; }
 test -c /dev/kfd || { echo '/dev/kfd missing' >&2; exit 1; }
-n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l)
+n=$(ls /dev/dri/renderD* 2>/dev/null | wc -l || true)  # pipefail: ls fails when there are none
 [ "$n" -ge ${gpu_count * gpu_partitions} ] || { echo "expected ${gpu_count * gpu_partitions} GPUs (${gpu_count} x ${gpu_compute_partition}), found $n render nodes" >&2; exit 1; }
 # partition modes: verified, never changed here (repartitioning resets the GPUs)
 for f in /sys/class/drm/renderD*/device/current_compute_partition /sys/class/drm/renderD*/device/current_memory_partition; do
