@@ -171,3 +171,19 @@ def test_azure_arm_client_credentials(rec):
     gets = [r for r in rec.requests if r[0] == "GET"]
     assert [r[2]["api-version"] for r in gets] == ["2016-06-01", "2017-12-01"]
     assert all(r[3]["Authorization"] == "Bearer arm-tok" for r in gets)
+
+
+def test_tls_contexts_are_built_once_per_process():
+    """Parsing the system trust store costs ~70 ms of CPU: every client and connection shares
+    one verifying context, and the unverified one loads no store at all."""
+    import ssl
+
+    from triton_kubernetes_amd.cloud.http import HTTPClient
+    from triton_kubernetes_amd.rancher.trust import RancherTrust
+
+    a, b = HTTPClient(base_url="https://a"), HTTPClient(base_url="https://b")
+    assert a._ssl_context() is b._ssl_context() is RancherTrust().context()
+    assert a._ssl_context().verify_mode == ssl.CERT_REQUIRED and a._ssl_context().check_hostname
+    off = HTTPClient(base_url="https://a", verify_tls=False)._ssl_context()
+    assert off is not a._ssl_context() and off.verify_mode == ssl.CERT_NONE and not off.check_hostname
+    assert off.cert_store_stats()["x509_ca"] == 0

@@ -58,6 +58,34 @@ Signer = Callable[[str, str, Dict[str, str], bytes], None]
 """``signer(method, url, headers, body)`` mutates ``headers`` in place."""
 
 
+_CTX_LOCK = threading.Lock()
+_CTX: Dict[str, ssl.SSLContext] = {}
+
+
+def _system_context() -> ssl.SSLContext:
+    """One verifying context over the system's trust store per process: building it parses
+    the whole CA bundle (~70 ms of CPU), and every new connection of every client had paid
+    that.  An SSLContext is safe to share between threads and connections."""
+    with _CTX_LOCK:
+        ctx = _CTX.get("system")
+        if ctx is None:
+            ctx = _CTX["system"] = ssl.create_default_context()
+        return ctx
+
+
+def _unverified_context() -> ssl.SSLContext:
+    """For the callers that verify by other means (a checksum over what they fetch): no trust
+    store is loaded at all."""
+    with _CTX_LOCK:
+        ctx = _CTX.get("none")
+        if ctx is None:
+            ctx = ssl.SSLContext(ssl.PROTOCOL_TLS_CLIENT)
+            ctx.check_hostname = False
+            ctx.verify_mode = ssl.CERT_NONE
+            _CTX["none"] = ctx
+        return ctx
+
+
 @dataclass
 class HTTPClient:
     base_url: str = ""
@@ -78,11 +106,7 @@ class HTTPClient:
     def _ssl_context(self) -> ssl.SSLContext:
         if self.ssl_context is not None:
             return self.ssl_context
-        ctx = ssl.create_default_context()
-        if not self.verify_tls:
-            ctx.check_hostname = False
-            ctx.verify_mode = ssl.CERT_NONE
-        return ctx
+        return _system_context() if self.verify_tls else _unverified_context()
 
     def _conn(self, scheme: str, netloc: str) -> http.client.HTTPConnection:
         pool = getattr(self._local, "pool", None)

@@ -57,7 +57,9 @@ class RancherTrust:
         certificate is publicly trusted); hostnames are checked."""
         if self.pem.strip():
             return ssl.create_default_context(cadata=self.pem)
-        return ssl.create_default_context()
+        from ..cloud.http import _system_context
+
+        return _system_context()  # built once per process: parsing the system store costs ~70 ms
 
     def describe(self) -> str:
         if not self.pem.strip():
