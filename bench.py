@@ -494,15 +494,25 @@ def main() -> int:
         for p in (torch.cuda.get_device_properties(i) for i in range(visible)))
 
     floor = [None]  # the node's clean used-HBM level (the first wait measures it)
+    warm_floor = [None]  # the same with the warm creates' resident agents up
 
-    def settle() -> dict:
+    def settle(resident: bool = False) -> dict:
         """Outside the timed region: the previous step's released HBM is cleared by the
         driver before the next step starts (a node entering service starts clean).  Local
-        rank 0 watches the node's cards; every rank waits for it."""
+        rank 0 watches the node's cards; every rank waits for it.
+
+        ``resident``: agents stay up across the waits (the warm creates) and keep HBM of
+        their own, so the clean level is above the cold one; the first such wait ends on a
+        quiet window and its end level is the floor of the later ones."""
         got = {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
         if args.hbm_settle == "on" and my_cards and local_rank == 0:
-            got = hbm.settle(cards=my_cards, floor=floor[0])
-            floor[0] = got["floor"]
+            if not resident:
+                got = hbm.settle(cards=my_cards, floor=floor[0])
+                floor[0] = got["floor"]
+            else:
+                got = hbm.settle(cards=my_cards, floor=warm_floor[0])
+                if not got.get("reached_floor") and not got.get("timed_out"):
+                    warm_floor[0] = sum(hbm.vram_used(cards=my_cards).values())
         barrier()
         return got
 
@@ -561,7 +571,7 @@ def main() -> int:
         for i in range(args.warm_steps + 1):  # the first one warms the agents, untimed
             # as before a cold step: the previous create's burn-in released ~300 GB per GPU,
             # which the driver clears before a node takes its next cluster (untimed)
-            warm_settles.append(settle()["waited_s"])
+            warm_settles.append(settle(resident=True))
             barrier()
             t0 = time.perf_counter()
             if rank == 0:
@@ -656,7 +666,7 @@ def main() -> int:
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),
             "warm_create_to_ready_s": round(sum(warm) / len(warm), 4) if warm else None,
             "warm_create_to_ready_each_s": [round(w, 4) for w in warm],
-            "warm_hbm_settle_s": [round(w, 3) for w in warm_settles],
+            "warm_hbm_settle_s": [round(w["waited_s"], 3) for w in warm_settles],
             "warm_gpu_burnin_ms": [d.get("gpu_node_step_ms", {}).get("gpu_burnin") for d in warm_detail[1:]],
             "warm_rccl_init_ms": [(d.get("rccl") or {}).get("init_total") for d in warm_detail[1:]],
             # GPU nodes that joined with the health taint in any timed step (normally none)
@@ -680,7 +690,7 @@ def main() -> int:
         print(json.dumps(line), flush=True)
         if args.report:
             with open(args.report, "w", encoding="utf-8") as fh:
-                json.dump({"line": line, "steps": results, "warm_s": warm, "warm_steps": warm_detail, "trace": trace}, fh, indent=1,
+                json.dump({"line": line, "steps": results, "warm_s": warm, "warm_steps": warm_detail, "warm_settles": warm_settles, "trace": trace}, fh, indent=1,
                           default=str)
     devnull.close()
     if fake is not None:
