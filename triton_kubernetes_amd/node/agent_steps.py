@@ -213,8 +213,11 @@ class AgentStepsMixin:
             parts = (step.params.get("compute_partition", "spx"), step.params.get("memory_partition", "nps1"))
             self._quiesce_gpus()
             # every (logical) GPU of the node burns in concurrently (one host thread each;
-            # the probes pin their device per thread); floors scaled to a partition's share
-            if len(self.devices) > 1:
+            # the probes pin their device per thread); floors scaled to a partition's share.
+            # A simulated burn-in (burnin_override: sim agents, tests) returns at once and runs
+            # inline: hundreds of sim agents in one process would otherwise each start a
+            # thread per synthetic GPU, which under one interpreter lock took ~0.1 s apiece
+            if len(self.devices) > 1 and self.burnin_override is None:
                 results = dict(zip(self.devices, self._pool.map(lambda d: self._burnin(d, level, parts),
                                                                 self.devices)))
             else:
