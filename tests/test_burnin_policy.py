@@ -580,3 +580,28 @@ open(os.path.join({str(tmp_path)!r}, "released-" + dev), "w").write(str(time.mon
     finally:
         go.set()
         probe.set_release_hold(None)
+
+
+def test_gpu_burnin_all_runs_the_same_levels_as_the_agent():
+    """``gpu-burnin --all`` (SSH / Terraform nodes) hard-codes its levels; the agent path takes
+    them from ``probe.LEVELS``.  Both must burn in the same way: the constants in the C++
+    source are read here and compared."""
+    import os
+    import re
+
+    from triton_kubernetes_amd.ops import probe
+
+    src = open(os.path.join(os.path.dirname(probe.__file__), "csrc", "tk_gpu_probe.hip"), encoding="utf-8").read()
+    body = src[src.index('const bool full = !strcmp(level, "full");'):]
+    body = body[:6000]  # the --all path: levels, then the per-GPU screens
+    hbm = re.search(r"hbm_bytes = full \? \((\d+)ull << (\d+)\) : \((\d+)ull << (\d+)\)", body)
+    mfma = re.search(r"mfma_iters = full \? (\d+) : (\d+);", body)
+    hbm_iters = re.search(r"tkp_hbm_bandwidth\(d, hbm_bytes, (\d+),", body)
+    passes = re.search(r"tkp_memtest_span\(d, mt_bytes, [^,]+, [^,]+, full \? (\d+) : (\d+)", body)
+    assert hbm and mfma and hbm_iters and passes
+    for level, k in (("full", 0), ("quick", 1)):
+        hb, hi, mi, mt_bytes, mp = probe.LEVELS[level]
+        assert hb == int(hbm.group(1 + 2 * k)) << int(hbm.group(2 + 2 * k)), level
+        assert hi == int(hbm_iters.group(1)), level
+        assert mi == int(mfma.group(1 + k)), level
+        assert mp == int(passes.group(1 + k)), level
