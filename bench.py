@@ -128,6 +128,20 @@ def _default_burnin() -> str:
     return DEFAULT_BURNIN
 
 
+def settle_cards(hbm, cards, floor: list, resident: bool) -> dict:
+    """One untimed wait for the driver's clearing on ``cards`` (``ops/hbm.py:settle``).
+    ``floor[0]`` is the clean used-HBM level, measured by the first wait and kept for the
+    next.  ``resident``: agents stay up across the waits and hold HBM of their own, so the
+    cold clean level is out of reach; a wait that ends on its quiet window instead records
+    the level it ended at as the floor of the later resident waits."""
+    got = hbm.settle(cards=cards, floor=floor[0])
+    if not resident:
+        floor[0] = got["floor"]
+    elif not got.get("reached_floor") and not got.get("timed_out"):
+        floor[0] = sum(hbm.vram_used(cards=cards).values())
+    return got
+
+
 def parse_args():
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
     ap.add_argument("--gpus", type=int, default=1)
@@ -506,13 +520,7 @@ def main() -> int:
         quiet window and its end level is the floor of the later ones."""
         got = {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
         if args.hbm_settle == "on" and my_cards and local_rank == 0:
-            if not resident:
-                got = hbm.settle(cards=my_cards, floor=floor[0])
-                floor[0] = got["floor"]
-            else:
-                got = hbm.settle(cards=my_cards, floor=warm_floor[0])
-                if not got.get("reached_floor") and not got.get("timed_out"):
-                    warm_floor[0] = sum(hbm.vram_used(cards=my_cards).values())
+            got = settle_cards(hbm, my_cards, warm_floor if resident else floor, resident)
         barrier()
         return got
 

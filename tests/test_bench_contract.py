@@ -186,3 +186,38 @@ def test_prewarm_is_one_device_code_load_in_a_throwaway_process():
     compile(code, "<prewarm>", "exec")
     assert "rccl.preload_device_code([0])" in code and "GateComm" not in code
     assert bench.COMGR_WARM_MIB < 540  # librccl's unbundled gfx950 code, once cached
+
+
+def test_resident_settles_learn_the_resident_floor():
+    """Warm creates keep their agents up: the first settle cannot reach the cold floor and
+    ends on its quiet window; its end level becomes the floor the later settles stop at."""
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+
+    class FakeHBM:
+        def __init__(self):
+            self.used, self.calls = 5 << 30, []
+
+        def settle(self, cards, floor):
+            self.calls.append(floor)
+            reached = floor is not None and self.used <= floor + (1 << 30)
+            return {"waited_s": 0.1, "floor": min(self.used, floor) if floor is not None else self.used,
+                    "reached_floor": reached, "timed_out": False}
+
+        def vram_used(self, cards):
+            return {c: self.used // len(cards) for c in cards}
+
+    hbm = FakeHBM()
+    cold = [None]
+    bench.settle_cards(hbm, ["card0"], cold, resident=False)
+    assert cold == [5 << 30]
+    hbm.used = 9 << 30  # resident agents up: 4 GiB of their own
+    warm = [None]
+    first = bench.settle_cards(hbm, ["card0"], warm, resident=True)
+    assert not first["reached_floor"] and warm == [9 << 30]
+    again = bench.settle_cards(hbm, ["card0"], warm, resident=True)
+    assert again["reached_floor"] and hbm.calls == [None, None, 9 << 30] and cold == [5 << 30]
