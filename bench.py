@@ -128,6 +128,16 @@ def _default_burnin() -> str:
     return DEFAULT_BURNIN
 
 
+def _stop_phases(results) -> dict:
+    per_step = []
+    for r in results:
+        docs = [d for name, d in (r.get("agent_stop_ms") or {}).items() if name.startswith("mi355x") and d]
+        if docs:
+            per_step.append({k: max(float(d.get(k) or 0.0) for d in docs) for k in docs[0]})
+    keys = sorted({k for st in per_step for k in st})
+    return {k: round(sum(st.get(k, 0.0) for st in per_step) / len(per_step), 1) for k in keys} if per_step else {}
+
+
 def settle_cards(hbm, cards, floor: list, resident: bool) -> dict:
     """One untimed wait for the driver's clearing on ``cards`` (``ops/hbm.py:settle``).
     ``floor[0]`` is the clean used-HBM level, measured by the first wait and kept for the
@@ -249,6 +259,13 @@ class AgentProc:
             except subprocess.TimeoutExpired:
                 os.killpg(self.proc.pid, signal.SIGKILL)
                 self.proc.wait()
+        try:  # the agent's last line: where its shutdown's time went
+            for ln in self.proc.stdout.read().splitlines():
+                if ln.startswith("{") and '"stopped"' in ln:
+                    doc = json.loads(ln)
+                    self.stop_ms = dict(doc.get("stop_phases_ms") or {}, total=doc.get("stop_ms"))
+        except (OSError, ValueError):
+            pass
         self.proc.stdout.close()
         return self.proc.returncode
 
@@ -486,6 +503,7 @@ def main() -> int:
             rcs = [p.stop() for p in procs]
         if any(rcs):
             raise RuntimeError(f"agent exit codes {rcs}")
+        out["agent_stop_ms"] = {p.name: getattr(p, "stop_ms", None) for p in procs}
         out.update(agents_start_s=round(t_agents - t0, 4), create_to_ready_s=round(t_ready - t0, 4),
                    step_s=round(time.perf_counter() - t0, 4))
         return out
@@ -672,6 +690,8 @@ def main() -> int:
             },
             "create_to_ready_s": ready,
             "agents_start_s_mean": round(sum(r["agents_start_s"] for r in results) / max(1, len(results)), 4),
+            # the GPU agents' shutdown (ms_per_step - value), by stage: max over agents, mean over steps
+            "gpu_agent_stop_ms": _stop_phases(results),
             "warm_create_to_ready_s": round(sum(warm) / len(warm), 4) if warm else None,
             "warm_create_to_ready_each_s": [round(w, 4) for w in warm],
             "warm_hbm_settle_s": [round(w["waited_s"], 3) for w in warm_settles],

@@ -389,6 +389,15 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
 
     def stop(self) -> None:
         self._stopped = True
+        t = time.perf_counter()
+        ms: Dict[str, float] = {}
+
+        def lap(name: str) -> None:
+            nonlocal t
+            now = time.perf_counter()
+            ms[name] = round((now - t) * 1e3, 1)
+            t = now
+
         cv = getattr(self, "_idle_cv", None)
         if cv is not None:
             with cv:
@@ -396,11 +405,14 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
                 cv.notify()
             self._janitor.join(timeout=30)
             self._janitor = None
+        lap("janitor")
         self._pool.shutdown(wait=True)
+        lap("pool")
         if self._server is not None:
             self._server.shutdown()
             self._server.server_close()
             self._server = None
+        lap("server")
         with self._gate_mu:
             pending = [e[0] for e in self._gates.values()]
             self._gates.clear()
@@ -411,18 +423,22 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             from ..ops import rccl
 
             rccl.drain()
+        lap("rccl_drain")
         if self.devices and self.topology_override is None:
             from ..ops import rccl
 
             deadline = time.monotonic() + 60.0  # a device-code preload still running: let it end
             while rccl.preloads_running() > 0 and time.monotonic() < deadline:
                 time.sleep(0.01)
+        lap("preloads")
         if self.devices and self.topology_override is None and self.burnin_override is None:
             from ..ops import probe
 
             # this process's own releases; a burn-in child still releasing what it tested
             # finishes on its own (its stdin closes with this process: no hold outlives it)
             probe.wait_frees(children=False)
+        lap("frees")
+        self.stop_ms = ms  # where a shutdown's time went (logged by main)
 
 def main(argv: Optional[List[str]] = None) -> int:
     """``tk-node-agent``: serve the agent API on a host (127.0.0.1 by default)."""
@@ -500,7 +516,8 @@ def main(argv: Optional[List[str]] = None) -> int:
         pass
     t0 = time.perf_counter()
     agent.stop()
-    print(json.dumps({"stopped": True, "stop_ms": round((time.perf_counter() - t0) * 1e3, 1)}), flush=True)
+    print(json.dumps({"stopped": True, "stop_ms": round((time.perf_counter() - t0) * 1e3, 1),
+                      "stop_phases_ms": getattr(agent, "stop_ms", {})}), flush=True)
     sys.stdout.flush()
     sys.stderr.flush()
     if getattr(agent, "_used_rccl", False):
