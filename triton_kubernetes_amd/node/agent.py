@@ -387,7 +387,11 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
                 self._last_active = time.monotonic()
                 cv.notify()
 
-    def stop(self) -> None:
+    def stop(self, drain_rccl: bool = True) -> None:
+        """Shut the agent down.  ``drain_rccl`` False: the caller leaves the process at once
+        (``main``'s quick exit), so the communicators' teardown is not waited for -- it only
+        frees device memory the kernel reclaims from an exiting process anyway, and its
+        frees queue behind the driver's wipe of a burn-in's release (~0.6 s per create)."""
         self._stopped = True
         t = time.perf_counter()
         ms: Dict[str, float] = {}
@@ -419,7 +423,7 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             self._gate_results.clear()
         for g in pending:
             g.abort()
-        if getattr(self, "_used_rccl", False):
+        if getattr(self, "_used_rccl", False) and drain_rccl:
             from ..ops import rccl
 
             rccl.drain()
@@ -515,7 +519,8 @@ def main(argv: Optional[List[str]] = None) -> int:
     while not agent.shutdown_requested.wait(3600):
         pass
     t0 = time.perf_counter()
-    agent.stop()
+    quick_exit = bool(agent.devices) and not _profiled() and os.environ.get("TK_AGENT_EXIT", "quick") != "normal"
+    agent.stop(drain_rccl=not quick_exit)
     print(json.dumps({"stopped": True, "stop_ms": round((time.perf_counter() - t0) * 1e3, 1),
                       "stop_phases_ms": getattr(agent, "stop_ms", {})}), flush=True)
     sys.stdout.flush()
@@ -527,10 +532,10 @@ def main(argv: Optional[List[str]] = None) -> int:
         # peers would hang a normal exit (which also lets tools such as rocprofv3 finalize)
         if rccl.abandoned_inits():
             rccl.exit_now(0)
-    if agent.devices and not _profiled() and os.environ.get("TK_AGENT_EXIT", "quick") != "normal":
-        # stop() has drained every communicator teardown and this process's releases: what a
-        # normal exit would add is the HIP runtime's own teardown, which the kernel does for
-        # an exiting process anyway (gpu-burnin's took 2.6 s behind the driver's VRAM wipe)
+    if quick_exit:
+        # what a normal exit would add is the HIP runtime's own teardown (and, undrained, the
+        # communicators'), which the kernel does for an exiting process anyway (gpu-burnin's
+        # took 2.6 s behind the driver's VRAM wipe)
         sys.stdout.flush()
         sys.stderr.flush()
         os._exit(0)
