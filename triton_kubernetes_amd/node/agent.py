@@ -520,7 +520,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         pass
     t0 = time.perf_counter()
     quick_exit = bool(agent.devices) and not _profiled() and os.environ.get("TK_AGENT_EXIT", "quick") != "normal"
-    agent.stop(drain_rccl=not quick_exit)
+    agent.stop(drain_rccl=not quick_exit or os.environ.get("TK_AGENT_STOP_DRAIN") == "1")
     print(json.dumps({"stopped": True, "stop_ms": round((time.perf_counter() - t0) * 1e3, 1),
                       "stop_phases_ms": getattr(agent, "stop_ms", {})}), flush=True)
     sys.stdout.flush()
