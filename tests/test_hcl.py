@@ -193,3 +193,30 @@ def test_regexall_translates_only_bare_dollars():
     assert regexall("\\\\$", "ends with \\") == ["\\"]
     assert regexall("^ab$", "ab\n") == []  # RE2: no match before a final newline
     assert regexall("^ab$", "ab") == ["ab"]
+
+
+def test_module_report_parses_once_under_concurrent_first_calls(tmp_path, monkeypatch):
+    """A cluster's host modules start their applies together; their input checks share one
+    parse of the module (the others wait for it) instead of each parsing it again."""
+    import threading
+    import time
+
+    src = os.path.join(catalog.MODULES_DIR, "bare-metal-rancher-k8s-host")
+    mod = tmp_path / "bare-metal-rancher-k8s-host"
+    shutil.copytree(src, mod)
+    calls = []
+    real = hcl.check_module
+
+    def slow_check(d):
+        calls.append(d)
+        time.sleep(0.05)
+        return real(d)
+
+    monkeypatch.setattr(hcl, "check_module", slow_check)
+    reports = []
+    threads = [threading.Thread(target=lambda: reports.append(hcl.module_report(str(mod)))) for _ in range(16)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert len(calls) == 1 and len(reports) == 16 and all(r is reports[0] for r in reports)
