@@ -221,3 +221,14 @@ def test_resident_settles_learn_the_resident_floor():
     assert not first["reached_floor"] and warm == [9 << 30]
     again = bench.settle_cards(hbm, ["card0"], warm, resident=True)
     assert again["reached_floor"] and hbm.calls == [None, None, 9 << 30] and cold == [5 << 30]
+
+
+def test_settle_slack_is_per_card(tmp_path):
+    """The floor is a sum over the node's cards: each card may sit a little above its own
+    clean level, so the default slack is 1 GiB per card (8 cards: 8 GiB), not 1 GiB in all."""
+    for i in range(8):
+        _card(str(tmp_path), f"card{i}", (1 << 30) + (900 << 20))  # 900 MiB above a 1 GiB floor each
+    got = hbm.settle(str(tmp_path), quiet_s=5.0, poll_s=0.005, timeout_s=10, floor=8 << 30)
+    assert got["reached_floor"] and got["waited_s"] < 1.0
+    got = hbm.settle(str(tmp_path), quiet_s=0.2, poll_s=0.005, timeout_s=10, floor=8 << 30, slack=1 << 30)
+    assert not got["reached_floor"]

@@ -62,12 +62,12 @@ def vram_used(drm_root: str = DRM_ROOT, cards: Optional[Iterable[str]] = None) -
 
 
 def settle(drm_root: str = DRM_ROOT, quiet_s: float = 5.0, poll_s: float = 0.02, timeout_s: float = 120.0,
-           floor: Optional[int] = None, slack: int = 1 << 30,
+           floor: Optional[int] = None, slack: Optional[int] = None,
            cards: Optional[Iterable[str]] = None) -> Dict[str, float]:
     """Block until the used VRAM of ``cards`` (default: every card) is back within ``slack``
-    of ``floor`` -- the clean level an earlier call measured -- or, without a floor or when
-    it is not reached, until none of their ``mem_info_vram_used`` dropped for ``quiet_s``
-    seconds.  Returns what it waited for, and ``floor``: the lowest level seen (the next
+    (default 1 GiB per card, the floor being a sum over the cards) of ``floor`` -- the
+    clean level an earlier call measured -- or, without a floor or when it is not reached,
+    until none of their ``mem_info_vram_used`` dropped for ``quiet_s`` seconds.  Returns what it waited for, and ``floor``: the lowest level seen (the next
     call's floor).  No cards: returns at once.
 
     The floor is what makes the wait reliable: a process that exits leaves its memory to
@@ -81,6 +81,8 @@ def settle(drm_root: str = DRM_ROOT, quiet_s: float = 5.0, poll_s: float = 0.02,
     if not first:
         return {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False, "floor": 0}
     last = dict(first)
+    if slack is None:
+        slack = len(first) << 30
     lowest = sum(first.values())
     quiet_since = t0
     timed_out = False
