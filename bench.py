@@ -146,9 +146,9 @@ def settle_cards(hbm, cards, floor: list, resident: bool) -> dict:
     the level it ended at as the floor of the later resident waits."""
     got = hbm.settle(cards=cards, floor=floor[0])
     if not resident:
-        floor[0] = got["floor"]
+        floor[0] = got["floor_by_card"]  # per card: one card still clearing is waited for
     elif not got.get("reached_floor") and not got.get("timed_out"):
-        floor[0] = sum(hbm.vram_used(cards=cards).values())
+        floor[0] = dict(hbm.vram_used(cards=cards))
     return got
 
 

@@ -204,8 +204,8 @@ def test_resident_settles_learn_the_resident_floor():
 
         def settle(self, cards, floor):
             self.calls.append(floor)
-            reached = floor is not None and self.used <= floor + (1 << 30)
-            return {"waited_s": 0.1, "floor": min(self.used, floor) if floor is not None else self.used,
+            reached = floor is not None and self.used <= floor["card0"] + (1 << 30)
+            return {"waited_s": 0.1, "floor_by_card": {"card0": min(self.used, floor["card0"]) if floor else self.used},
                     "reached_floor": reached, "timed_out": False}
 
         def vram_used(self, cards):
@@ -214,13 +214,13 @@ def test_resident_settles_learn_the_resident_floor():
     hbm = FakeHBM()
     cold = [None]
     bench.settle_cards(hbm, ["card0"], cold, resident=False)
-    assert cold == [5 << 30]
+    assert cold == [{"card0": 5 << 30}]
     hbm.used = 9 << 30  # resident agents up: 4 GiB of their own
     warm = [None]
     first = bench.settle_cards(hbm, ["card0"], warm, resident=True)
-    assert not first["reached_floor"] and warm == [9 << 30]
+    assert not first["reached_floor"] and warm == [{"card0": 9 << 30}]
     again = bench.settle_cards(hbm, ["card0"], warm, resident=True)
-    assert again["reached_floor"] and hbm.calls == [None, None, 9 << 30] and cold == [5 << 30]
+    assert again["reached_floor"] and hbm.calls == [None, None, {"card0": 9 << 30}] and cold == [{"card0": 5 << 30}]
 
 
 def test_settle_slack_is_per_card(tmp_path):
@@ -232,3 +232,25 @@ def test_settle_slack_is_per_card(tmp_path):
     assert got["reached_floor"] and got["waited_s"] < 1.0
     got = hbm.settle(str(tmp_path), quiet_s=0.2, poll_s=0.005, timeout_s=10, floor=8 << 30, slack=1 << 30)
     assert not got["reached_floor"]
+
+
+def test_settle_per_card_floor_waits_for_the_card_still_clearing(tmp_path):
+    """Per-card floors: seven idle cards at their level do not end the wait while the eighth
+    still has most of a burn-in's release to clear (a summed floor with 8 GiB of slack
+    would have let ~7 GiB of clearing run into the next step)."""
+    paths = [_card(str(tmp_path), f"card{i}", 1 << 30) for i in range(8)]
+    with open(paths[3], "w") as fh:
+        fh.write(f"{(1 << 30) + (7 << 30)}\n")  # 7 GiB left to clear on card3
+    floor = {f"card{i}": 1 << 30 for i in range(8)}
+
+    def later():
+        time.sleep(0.4)
+        with open(paths[3] + ".tmp", "w") as fh:
+            fh.write(f"{1 << 30}\n")
+        os.replace(paths[3] + ".tmp", paths[3])
+
+    t = threading.Thread(target=later)
+    t.start()
+    got = hbm.settle(str(tmp_path), quiet_s=5.0, poll_s=0.005, timeout_s=10, floor=floor)
+    t.join()
+    assert got["reached_floor"] and got["waited_s"] >= 0.4 and got["floor"] == floor

@@ -16,7 +16,7 @@ memory.  Pure sysfs: no HIP call, so the waiting process does not touch the GPU.
 import glob
 import os
 import time
-from typing import Dict, Iterable, List, Optional, Tuple
+from typing import Any, Dict, Iterable, List, Optional, Tuple, Union
 
 DRM_ROOT = "/sys/class/drm"
 
@@ -62,13 +62,16 @@ def vram_used(drm_root: str = DRM_ROOT, cards: Optional[Iterable[str]] = None) -
 
 
 def settle(drm_root: str = DRM_ROOT, quiet_s: float = 5.0, poll_s: float = 0.02, timeout_s: float = 120.0,
-           floor: Optional[int] = None, slack: Optional[int] = None,
-           cards: Optional[Iterable[str]] = None) -> Dict[str, float]:
-    """Block until the used VRAM of ``cards`` (default: every card) is back within ``slack``
-    (default 1 GiB per card, the floor being a sum over the cards) of ``floor`` -- the
-    clean level an earlier call measured -- or, without a floor or when it is not reached,
-    until none of their ``mem_info_vram_used`` dropped for ``quiet_s`` seconds.  Returns what it waited for, and ``floor``: the lowest level seen (the next
-    call's floor).  No cards: returns at once.
+           floor: Optional[Union[int, Dict[str, int]]] = None, slack: Optional[int] = None,
+           cards: Optional[Iterable[str]] = None) -> Dict[str, Any]:
+    """Block until the used VRAM of ``cards`` (default: every card) is back at ``floor`` --
+    the clean level an earlier call measured -- or, without a floor or when it is not
+    reached, until none of their ``mem_info_vram_used`` dropped for ``quiet_s`` seconds.
+    ``floor`` per card (a dict, ``floor_by_card`` of an earlier call): every card within
+    ``slack`` (default 1 GiB) of its own level, so one card still clearing a large release
+    is waited for whatever the others do.  ``floor`` as one number: the sum over the cards
+    within ``slack`` (default 1 GiB per card).  Returns what it waited for, ``floor`` (the
+    lowest level seen, in the form given) and ``floor_by_card``.  No cards: returns at once.
 
     The floor is what makes the wait reliable: a process that exits leaves its memory to
     the driver, which returns it (cleared) only later, a whole allocation at a time -- a
@@ -79,18 +82,24 @@ def settle(drm_root: str = DRM_ROOT, quiet_s: float = 5.0, poll_s: float = 0.02,
     t0 = time.monotonic()
     first = vram_used(drm_root, cards)
     if not first:
-        return {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False, "floor": 0}
+        return {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False, "floor": 0,
+                "floor_by_card": {}}
     last = dict(first)
+    per_card = isinstance(floor, dict)
     if slack is None:
-        slack = len(first) << 30
-    lowest = sum(first.values())
+        slack = (1 << 30) if per_card else len(first) << 30
+    low = dict(first)
     quiet_since = t0
     timed_out = False
     reached = False
     while True:
-        total = sum(last.values())
-        lowest = min(lowest, total)
-        if floor is not None and total <= floor + slack:
+        for c, v in last.items():
+            low[c] = min(low.get(c, v), v)
+        if per_card:
+            if all(v <= floor.get(c, v) + slack for c, v in last.items()):
+                reached = True
+                break
+        elif floor is not None and sum(last.values()) <= floor + slack:
             reached = True
             break
         now = time.monotonic()
@@ -104,7 +113,12 @@ def settle(drm_root: str = DRM_ROOT, quiet_s: float = 5.0, poll_s: float = 0.02,
         if any(cur.get(c, 0) < last.get(c, 0) for c in cur):
             quiet_since = time.monotonic()
         last = cur
+    by_card = {c: min(v, floor[c]) if per_card and c in floor else v for c, v in low.items()}
+    if per_card:
+        out_floor: Union[int, Dict[str, int]] = by_card
+    else:
+        out_floor = min(sum(low.values()), floor) if floor is not None else sum(low.values())
     return {"waited_s": round(time.monotonic() - t0, 4),
             "released_gib": round(max(0, sum(first.values()) - sum(last.values())) / 2 ** 30, 2),
             "cards": len(first), "timed_out": timed_out, "reached_floor": reached,
-            "floor": min(lowest, floor) if floor is not None else lowest}
+            "floor": out_floor, "floor_by_card": by_card}
