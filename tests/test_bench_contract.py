@@ -254,3 +254,20 @@ def test_settle_per_card_floor_waits_for_the_card_still_clearing(tmp_path):
     got = hbm.settle(str(tmp_path), quiet_s=5.0, poll_s=0.005, timeout_s=10, floor=floor)
     t.join()
     assert got["reached_floor"] and got["waited_s"] >= 0.4 and got["floor"] == floor
+
+
+def test_stop_phases_are_the_gpu_agents_max_then_mean_over_steps():
+    import importlib.util
+    import os
+
+    spec = importlib.util.spec_from_file_location("bench_mod2", os.path.join(os.path.dirname(__file__), "..", "bench.py"))
+    bench = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(bench)
+    results = [
+        {"agent_stop_ms": {"mi355x-0": {"rccl_drain": 10.0, "total": 20.0}, "mi355x-1": {"rccl_drain": 30.0, "total": 40.0},
+                           "control-plane": {"rccl_drain": 999.0, "total": 999.0}}},
+        {"agent_stop_ms": {"mi355x-0": {"rccl_drain": 50.0, "total": 60.0}, "mi355x-1": None}},
+        {},
+    ]
+    assert bench._stop_phases(results) == {"rccl_drain": 40.0, "total": 50.0}
+    assert bench._stop_phases([{}]) == {}

@@ -572,3 +572,19 @@ def test_rendered_shell_has_no_early_exit_readers():
                 scripts[f"{mod}/{name}"] = text
     bad = {k: m.group(0) for k, s in scripts.items() for m in [re.search(_EARLY_READER, s)] if m}
     assert not bad, bad
+
+
+def test_agent_stop_before_a_quick_exit_skips_the_rccl_drain(monkeypatch, tmp_path):
+    """``main`` leaves with ``_exit`` right after ``stop()``: the communicators' teardown is not
+    waited for then (``drain_rccl=False``); a plain ``stop()`` still drains."""
+    from triton_kubernetes_amd.ops import rccl
+
+    drained = []
+    monkeypatch.setattr(rccl, "drain", lambda *a, **k: drained.append(1))
+    for drain, want in ((False, []), (True, [1])):
+        drained.clear()
+        agent = NodeAgent("n1", "sim", devices=[0], root=str(tmp_path), token="t",
+                          topology_override=synthetic_topology(1), burnin_override=lambda d, lvl: {"ok": True})
+        agent._used_rccl = True
+        agent.stop(drain_rccl=drain)
+        assert drained == want and "rccl_drain" in agent.stop_ms
