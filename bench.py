@@ -69,6 +69,7 @@ import sys
 import tempfile
 import time
 
+_T_START = time.monotonic()  # the run's wall clock starts with this process (the budget's origin)
 HERE = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, HERE)
 
@@ -138,18 +139,116 @@ def _stop_phases(results) -> dict:
     return {k: round(sum(st.get(k, 0.0) for st in per_step) / len(per_step), 1) for k in keys} if per_step else {}
 
 
-def settle_cards(hbm, cards, floor: list, resident: bool) -> dict:
+def settle_cards(hbm, cards, floor: list, resident: bool, timeout_s=None) -> dict:
     """One untimed wait for the driver's clearing on ``cards`` (``ops/hbm.py:settle``).
     ``floor[0]`` is the clean used-HBM level, measured by the first wait and kept for the
     next.  ``resident``: agents stay up across the waits and hold HBM of their own, so the
     cold clean level is out of reach; a wait that ends on its quiet window instead records
-    the level it ended at as the floor of the later resident waits."""
-    got = hbm.settle(cards=cards, floor=floor[0])
+    the level it ended at as the floor of the later resident waits.  ``timeout_s``: the
+    run budget's cap on this wait (:class:`RunBudget`), None for the settle's own limit."""
+    got = hbm.settle(cards=cards, floor=floor[0], **({} if timeout_s is None else {"timeout_s": timeout_s}))
     if not resident:
         floor[0] = got["floor_by_card"]  # per card: one card still clearing is waited for
     elif not got.get("reached_floor") and not got.get("timed_out"):
         floor[0] = dict(hbm.vram_used(cards=cards))
     return got
+
+
+class RunBudget:
+    """Keeps one bench run inside the driver's wall-clock limit (its BENCH record shows
+    ``timeout_s`` 600) without touching what is measured.
+
+    Untimed work dominates a run: before each cold step the wait for the driver to clear
+    the previous step's ~280 GB-per-GPU release (8.4 s per step on one GPU, against a
+    2.3 s step), and after the timed region the secondary warm creates.  On an 8-GPU node
+    nobody has measured whether the driver clears eight cards in parallel; if it serialises
+    them, 25 settles would outlast any limit before the line prints.
+
+    After every step (warmup or timed) :meth:`plan` projects the run's end from what the
+    steps so far cost -- the slowest settle and the slowest step seen, for each step still
+    to come, plus the warm creates -- and, if the projection exceeds ``budget_s``, sheds
+    secondary work in this order:
+
+    1. ``warm_creates``: the secondary warm creates are skipped (``warm_create_to_ready_s``
+       null);
+    2. ``hbm_settle_capped``: each later settle waits at most what is left per remaining
+       step, so a step may start before the driver has finished clearing -- the step then
+       pays that clearing inside its timed region, which can only make ``value`` worse.
+
+    The ``--warmup`` and ``--steps`` counts are never cut: the line's ``steps`` and
+    ``warmup`` are what ran.  ``budget_s`` 0 turns the guard off."""
+
+    TAIL_S = 15.0  # after the last step: the agents' stop, the report, the process exit
+
+    def __init__(self, budget_s: float, t0: float = None, clock=time.monotonic):
+        self.budget_s = float(budget_s or 0.0)
+        self.clock = clock
+        self.t0 = _T_START if t0 is None else t0
+        self.settles = []
+        self.steps = []
+        self.shed = []
+        self.projected_s = None
+        self.settle_cap_s = None
+        self.warm_allowed = True
+
+    def record(self, settle_s: float, step_s: float) -> None:
+        self.settles.append(float(settle_s))
+        self.steps.append(float(step_s))
+
+    def plan(self, cold_left: int, warm_creates: int) -> None:
+        """Re-project after a step; ``cold_left`` cold steps (warmup + timed) and
+        ``warm_creates`` warm creates (each with its own settle) are still to run."""
+        if not self.steps:
+            return
+        settle, step = max(self.settles), max(self.steps)
+        elapsed = self.clock() - self.t0
+        warm = (settle + step) * warm_creates if self.warm_allowed else 0.0
+        proj = elapsed + cold_left * (settle + step) + warm + self.TAIL_S
+        self.projected_s = round(proj, 1)
+        if not self.budget_s or proj <= self.budget_s:
+            return
+        if warm and self.warm_allowed:
+            self.warm_allowed = False
+            self.shed.append("warm_creates")
+            proj -= warm
+        if proj > self.budget_s and cold_left:
+            cap = max(0.0, (self.budget_s - elapsed - self.TAIL_S - cold_left * step) / cold_left)
+            if self.settle_cap_s is None or cap < self.settle_cap_s:
+                self.settle_cap_s = round(cap, 2)
+            if "hbm_settle_capped" not in self.shed:
+                self.shed.append("hbm_settle_capped")
+
+    def report(self) -> dict:
+        return {"budget_s": self.budget_s or None, "projected_s": self.projected_s, "shed": list(self.shed),
+                "settle_cap_s": self.settle_cap_s, "elapsed_s": round(self.clock() - self.t0, 1)}
+
+
+def resolve_gpus(requested: int, world: int, visible: int, sim: bool, masked_env: bool = False) -> dict:
+    """How many GPUs the run measures, and how; raises :class:`GpuCountError` rather than
+    measuring fewer GPUs than asked.
+
+    * No launcher (``WORLD_SIZE`` unset or 1): ``--gpus N`` means N GPUs of this node, all
+      owned by this one process -- one node agent over devices 0..N-1, as a real 8xMI355X
+      node runs one agent.  Fewer than N visible is an error.
+    * Under ``torchrun``: one rank per GPU, so ``WORLD_SIZE`` must equal ``--gpus``.  A
+      launcher that masks each rank to its own GPU (fewer visible than ranks) gets one
+      1-GPU agent per rank."""
+    if requested < 1:
+        raise GpuCountError(f"--gpus {requested}: at least 1 GPU")
+    if world > 1 and world != requested:
+        raise GpuCountError(f"--gpus {requested} but WORLD_SIZE {world}: launch one rank per GPU")
+    if sim:
+        visible = requested
+    masked = world > 1 and (visible < requested or masked_env)
+    if masked and visible < 1:
+        raise GpuCountError(f"{requested} GPUs requested, {visible} visible to rank")
+    if not masked and visible < requested:
+        raise GpuCountError(f"{requested} GPUs requested, {visible} visible")
+    return {"n_gpus": requested, "visible": visible, "masked": masked}
+
+
+class GpuCountError(RuntimeError):
+    pass
 
 
 def parse_args():
@@ -189,6 +288,10 @@ def parse_args():
                          "libtk_rccl ABI stub (ops/csrc/tk_rccl_stub.cpp: every rank of the world joins and sweeps, "
                          "no GPU); never a valid measurement")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
+    ap.add_argument("--time-budget", type=float, default=420.0,
+                    help="wall-clock seconds the whole run should stay within (RunBudget): past it the secondary "
+                         "warm creates are shed, then the untimed settle waits are capped; the timed steps never "
+                         "are.  0: off")
     return ap.parse_args()
 
 
@@ -233,6 +336,7 @@ class AgentProc:
                 self.url = doc["listening"]
                 self.runtime = doc.get("hip_runtime", "")
                 self.startup_ms = doc.get("startup_ms", {})
+                self.preload = doc.get("rccl_preload") or {}
         sel.close()
         return self.url
 
@@ -287,6 +391,7 @@ class InprocAgent:
             self.agent.topology_override = synthetic_topology(synthetic)
             self.agent.burnin_override = lambda dev, level: {"ok": True, "simulated": True, "level": level}
         self.url = self.agent.serve(address, ssl_context=creds["ssl_context"])
+        self.preload = getattr(self.agent, "rccl_preload", None)
 
     def wait_url(self, timeout: float = 0.0) -> str:
         return self.url
@@ -299,6 +404,20 @@ class InprocAgent:
         return 0
 
 
+def failure_line(args, n_gpus, workers, gpus_per_worker, visible, error: str, completed: int = 0) -> dict:
+    """The line's shape for a run that measured nothing (``value`` null) and why."""
+    return {
+        "metric": METRIC, "value": None, "unit": "s", "n_gpus": n_gpus, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": None, "higher_is_better": False, "scaling": "weak",
+        "vs_baseline": None, "dtype": "n/a", "data": "FAILED: no measurement",
+        "config": {"model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology "
+                            "labels", "workers": workers, "gpus_per_worker": gpus_per_worker,
+                   "visible_gpus": visible, "global_batch": "n/a", "seq_len": "n/a",
+                   "parallelism": f"{workers} worker node(s) x {gpus_per_worker} GPU(s)",
+                   "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate},
+        "error": error[:2000], "completed_steps": completed}
+
+
 def main() -> int:
     args = parse_args()
     import torch
@@ -307,15 +426,23 @@ def main() -> int:
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
-    if world != args.gpus and rank == 0:
-        print(f"warning: --gpus {args.gpus} but WORLD_SIZE {world}; using WORLD_SIZE", file=sys.stderr)
-    n_gpus = world
+    # counting devices does not initialise HIP on this image; set_device below does
+    visible = 0 if args.sim_gpu else torch.cuda.device_count()
+    try:
+        shape = resolve_gpus(args.gpus, world, visible, args.sim_gpu,
+                             masked_env=os.environ.get("TK_BENCH_ASSUME_MASKED") == "1")
+    except GpuCountError as exc:
+        # never measure fewer GPUs than asked: the line says what was wrong, and the run fails
+        if rank == 0:
+            print(json.dumps(failure_line(args, args.gpus, None, None, visible, str(exc))), flush=True)
+        print(f"bench: {exc}", file=sys.stderr)
+        return 2
+    n_gpus, visible, masked = shape["n_gpus"], shape["visible"], shape["masked"]
     distributed = world > 1
     if distributed:
         # control-plane sync only (CPU); the GPU collectives are the agents' native RCCL gate
         dist.init_process_group("gloo", init_method="env://")
     if args.sim_gpu:
-        visible = n_gpus
         if not args.no_rccl_gate:
             # the gate over the C ABI stub: the agents (this process's and their children)
             # join one rendezvous directory, shared by every rank
@@ -330,12 +457,11 @@ def main() -> int:
             os.environ.update(TK_RCCL_LIB=os.path.join(native.LIB_DIR, "libtk_rccl_stub.so"),
                               TK_RCCL_STUB_DIR=where[0], TK_GATE_BACKEND="rccl")
     else:
-        visible = torch.cuda.device_count()
-        torch.cuda.set_device(local_rank if visible > local_rank else 0)
+        torch.cuda.set_device(0 if masked else min(local_rank, visible - 1))
 
-    # which agents this rank owns: (name, devices).  Unmasked: rank 0 owns every worker
-    # agent; masked (each rank sees one GPU): every rank owns a 1-GPU agent.
-    masked = (not args.sim_gpu and visible < n_gpus) or os.environ.get("TK_BENCH_ASSUME_MASKED") == "1"
+    # which agents this rank owns: (name, devices).  Unmasked (one process, or ranks that
+    # all see the node's GPUs): rank 0 owns every worker agent over devices 0..N-1; masked
+    # (each rank sees only its own GPU): every rank owns a 1-GPU agent.
     if masked:
         workers = n_gpus
         mine = [(f"mi355x-{rank}", [0])]
@@ -346,6 +472,7 @@ def main() -> int:
         per = n_gpus // workers
         mine = [(f"mi355x-{w}", list(range(w * per, (w + 1) * per))) for w in range(workers)] if rank == 0 else []
     gpus_per_worker = n_gpus // workers
+    budget = RunBudget(args.time_budget)
 
     from triton_kubernetes_amd import versions
     from triton_kubernetes_amd import workflows as wf
@@ -409,10 +536,13 @@ def main() -> int:
                           synthetic if devs else 0, client_ctx) for name, devs in names]
 
     runtimes = set()
+    preloads = set()  # the GPU agents' RCCL device-code preload handle (how:symbol)
 
     def gather_urls(procs):
         local = [(p.name, p.wait_url()) for p in procs]
         runtimes.update(getattr(p, "runtime", "") or "in-process" for p in procs if p.name != "control-plane")
+        preloads.update("{how}:{symbol}".format(**(getattr(p, "preload", None) or {"how": "none", "symbol": "none"}))
+                        for p in procs if p.name != "control-plane")
         if distributed:
             every = [None] * world
             dist.all_gather_object(every, local)
@@ -480,7 +610,12 @@ def main() -> int:
             phases = [r.get("phase_ms") or {} for r in ranks]
             if phases:  # the gate's communicator phases, max over agents
                 out["rccl"] = {k: round(max(float(p.get(k, 0.0)) for p in phases), 3)
-                               for k in ("init_total", "init_wait", "alloc", "sweep")}
+                               for k in ("init_total", "init_wait", "alloc", "sweep", "footprint_mib",
+                                         "footprint_total_mib")}
+            # an init that ran out of HBM beside the held burn-in spans and was retried
+            retried = [r.get("gate_retry") for r in ranks if r.get("gate_retry")]
+            if retried or (rep.rccl or {}).get("retry"):
+                out["gate_retry"] = retried or ["oom"]
                 out["rccl_peak_busbw_gbps"] = rep.rccl.get("min_peak_busbw_gbps")
         return out
 
@@ -520,27 +655,42 @@ def main() -> int:
     from triton_kubernetes_amd.ops import hbm
 
     # this node's GPUs of the run, by their DRM cards (a shared host lists other tenants' GPUs
-    # too, whose releases must not hold up -- or end -- the wait)
-    my_cards = [] if args.sim_gpu else hbm.cards_for_pci(
+    # too, whose releases must not hold up -- or end -- the wait): devices 0..N-1, or a
+    # masked rank's own GPU.  Unmasked, local rank 0 watches them for every rank; masked,
+    # every rank watches its own.
+    settler = masked or local_rank == 0
+    run_devices = [0] if masked else list(range(n_gpus))
+    my_cards = [] if args.sim_gpu or not settler else hbm.cards_for_pci(
         (p.pci_domain_id, p.pci_bus_id, p.pci_device_id)
-        for p in (torch.cuda.get_device_properties(i) for i in range(visible)))
+        for p in (torch.cuda.get_device_properties(i) for i in run_devices))
 
     floor = [None]  # the node's clean used-HBM level (the first wait measures it)
     warm_floor = [None]  # the same with the warm creates' resident agents up
 
     def settle(resident: bool = False) -> dict:
         """Outside the timed region: the previous step's released HBM is cleared by the
-        driver before the next step starts (a node entering service starts clean).  Local
-        rank 0 watches the node's cards; every rank waits for it.
+        driver before the next step starts (a node entering service starts clean).  Every
+        rank waits for the ranks that watch cards.
 
         ``resident``: agents stay up across the waits (the warm creates) and keep HBM of
         their own, so the clean level is above the cold one; the first such wait ends on a
         quiet window and its end level is the floor of the later ones."""
         got = {"waited_s": 0.0, "released_gib": 0.0, "cards": 0, "timed_out": False}
-        if args.hbm_settle == "on" and my_cards and local_rank == 0:
-            got = settle_cards(hbm, my_cards, warm_floor if resident else floor, resident)
+        if args.hbm_settle == "on" and my_cards:
+            got = settle_cards(hbm, my_cards, warm_floor if resident else floor, resident,
+                               timeout_s=budget.settle_cap_s)
         barrier()
         return got
+
+    def replan(cold_left: int, settle_s: float, step_s: float) -> None:
+        """Rank 0 re-projects the run (RunBudget) and every rank takes its decision."""
+        budget.record(settle_s, step_s)
+        if rank == 0:
+            budget.plan(cold_left, (args.warm_steps + 1) if args.warm_steps > 0 else 0)
+        if distributed:
+            got = [(budget.warm_allowed, budget.settle_cap_s, list(budget.shed))]
+            dist.broadcast_object_list(got, src=0)
+            budget.warm_allowed, budget.settle_cap_s, budget.shed = got[0]
 
     comgr = {"dir": comgr_cache_dir(), "enabled": os.environ.get("AMD_COMGR_CACHE", "1") != "0",
              "mib_at_start": dir_mib(comgr_cache_dir()), "prewarm_s": None}
@@ -553,35 +703,33 @@ def main() -> int:
     settles = []
     try:
         for w in range(args.warmup):
+            t_s = time.perf_counter()
             settle()
             barrier()
+            t_step = time.perf_counter()
             cold_step(-1 - w)
+            replan(args.warmup - w - 1 + args.steps, t_step - t_s, time.perf_counter() - t_step)
         TRACER.reset()
         comgr["mib_before_timed"] = dir_mib(comgr["dir"])
         # the timed region is the K steps, each bracketed by a barrier + synchronize on both
         # sides; the settle wait before each step is outside it (and reported as hbm_settle_s)
         elapsed = 0.0
         for i in range(args.steps):
+            t_s = time.perf_counter()
             settles.append(settle())
             barrier()
             t_step = time.perf_counter()
             results.append(cold_step(i))
             barrier()
-            elapsed += time.perf_counter() - t_step
+            took = time.perf_counter() - t_step
+            elapsed += took
+            replan(args.steps - i - 1, t_step - t_s, took)
     except Exception as exc:
         if rank == 0:
             # a failed run still says what failed, in the line's own shape (value null), before
             # the traceback: the first run on a new node shape must leave a diagnosis
-            print(json.dumps({
-                "metric": METRIC, "value": None, "unit": "s", "n_gpus": n_gpus, "steps": args.steps,
-                "warmup": args.warmup, "ms_per_step": None, "higher_is_better": False, "scaling": "weak",
-                "vs_baseline": None, "dtype": "n/a", "data": "FAILED: no measurement",
-                "config": {"model": "create cluster MI355X bare-metal N-worker + ROCm device-plugin + xGMI topology "
-                                    "labels", "workers": workers, "gpus_per_worker": gpus_per_worker,
-                           "visible_gpus": visible, "global_batch": "n/a", "seq_len": "n/a",
-                           "parallelism": f"{workers} worker node(s) x {gpus_per_worker} GPU(s)",
-                           "burnin": args.burnin, "rccl_gate": not args.no_rccl_gate},
-                "error": f"{type(exc).__name__}: {exc}"[:2000], "completed_steps": len(results)}), flush=True)
+            print(json.dumps(failure_line(args, n_gpus, workers, gpus_per_worker, visible,
+                                          f"{type(exc).__name__}: {exc}", len(results))), flush=True)
         raise
     if distributed:
         t = torch.tensor([elapsed], dtype=torch.float64)
@@ -591,7 +739,7 @@ def main() -> int:
 
     # secondary: warm creates against agents kept resident (outside the timed region)
     warm, warm_settles, warm_detail = [], [], []
-    if args.warm_steps > 0:
+    if args.warm_steps > 0 and budget.warm_allowed:
         procs = start_agents("warm")
         urls = gather_urls(procs)
         for i in range(args.warm_steps + 1):  # the first one warms the agents, untimed
@@ -662,6 +810,11 @@ def main() -> int:
                            + ("; before each timed step, untimed, the bench waits for the driver to clear the HBM "
                               "the previous step released (a node entering service starts clean)"
                               if args.hbm_settle == "on" and not args.sim_gpu else "")
+                           + ("; the run budget capped those waits at %.1f s, so a step may pay part of its "
+                              "predecessor's clearing inside the timed region" % budget.settle_cap_s
+                              if budget.settle_cap_s is not None else "")
+                           + ("; the secondary warm creates were shed by the run budget"
+                              if "warm_creates" in budget.shed else "")
                            + ("; opt-in node install before the timed region: verified single-target gfx950 "
                               "RCCL copy (ops/rccl_slim.py)" if slim_meta else "")),
             "config": {
@@ -679,6 +832,9 @@ def main() -> int:
                 "k8s_version": versions.DEFAULT_K8S_VERSION,
                 # HIP runtime + RCCL the GPU agents ran on (ops/native.py:select_runtime)
                 "agent_hip_runtime": sorted(runtimes),
+                # the kernel handle each GPU agent's RCCL device-code preload used ("none:none":
+                # nothing preloaded; the gate's first init then loads the code)
+                "agent_rccl_preload": sorted(preloads),
                 # node install step outside the timed region (ops/rccl_slim.py)
                 "rccl_slim": ({k: slim_meta.get(k) for k in ("prepare_s", "cached", "source_fatbin_bytes",
                                                               "loaded_code_object_bytes", "verified")}
@@ -699,6 +855,12 @@ def main() -> int:
             "warm_rccl_init_ms": [(d.get("rccl") or {}).get("init_total") for d in warm_detail[1:]],
             # GPU nodes that joined with the health taint in any timed step (normally none)
             "gpu_unhealthy_nodes": sorted({h for r in results for h in r.get("gpu_unhealthy", [])}),
+            # the gate communicator's device memory per GPU (MiB, max over agents, last timed step):
+            # what the burn-in span's headroom must leave (node/agent_gate.py:span_headroom)
+            "rccl_footprint_mib": next(({k: r["rccl"].get(k) for k in ("footprint_mib", "footprint_total_mib")}
+                                        for r in reversed(results) if r.get("rccl")), None),
+            # timed steps whose gate init ran out of HBM and was retried after the spans' release
+            "gate_retry_steps": [r["step"] for r in results if r.get("gate_retry")],
             # ranks of the cluster RCCL gate per timed step (every GPU of the worker tier)
             "rccl_gate_ranks": [r.get("rccl_gate_ranks", 0) for r in results],
             # the GPU nodes' measured xGMI peer-read matrix (2+ GPUs per node), last timed step
@@ -713,6 +875,9 @@ def main() -> int:
             "hbm_settle_s": [s["waited_s"] for s in settles],
             "hbm_settle_released_gib": [s["released_gib"] for s in settles],
             "hbm_settle_reached_floor": [s.get("reached_floor") for s in settles],
+            # the run's wall-clock guard (RunBudget): what it projected and what it shed to
+            # stay inside --time-budget (never a timed step)
+            "run_budget": budget.report(),
             "phase_ms_per_step": phase_ms,
         }
         print(json.dumps(line), flush=True)

@@ -271,3 +271,86 @@ def test_stop_phases_are_the_gpu_agents_max_then_mean_over_steps():
     ]
     assert bench._stop_phases(results) == {"rccl_drain": 40.0, "total": 50.0}
     assert bench._stop_phases([{}]) == {}
+
+
+class _Clock:
+    def __init__(self):
+        self.t = 0.0
+
+    def __call__(self):
+        return self.t
+
+
+def _run(bench, budget, clock, warmup, steps, settle_s, step_s, warm_steps=2):
+    """The bench's loop against a fake clock: each settle takes ``settle_s`` (capped by the
+    budget, as ``hbm.settle(timeout_s=...)`` caps it), each step ``step_s``."""
+    waited = []
+    total = warmup + steps
+    for k in range(total):
+        w = settle_s if budget.settle_cap_s is None else min(settle_s, budget.settle_cap_s)
+        waited.append(w)
+        clock.t += w + step_s
+        budget.record(w, step_s)
+        budget.plan(total - k - 1, warm_steps + 1)
+    if budget.warm_allowed:
+        clock.t += (warm_steps + 1) * (settle_s + step_s)
+    return waited
+
+
+def test_run_budget_keeps_everything_when_it_fits():
+    import bench
+
+    clock = _Clock()
+    b = bench.RunBudget(420, t0=0.0, clock=clock)
+    waited = _run(bench, b, clock, 5, 20, settle_s=8.4, step_s=2.3)  # the 1-GPU box of round 5
+    assert b.shed == [] and b.warm_allowed and b.settle_cap_s is None and waited == [8.4] * 25
+    assert clock.t < 420
+
+
+def test_run_budget_sheds_warm_creates_then_caps_slow_settles():
+    """A node whose driver clears 8 cards one after another: ~67 s per settle.  The warm
+    creates go first, then each settle is capped so the run ends inside the budget; the
+    25 cold steps all run."""
+    import bench
+
+    clock = _Clock()
+    b = bench.RunBudget(420, t0=0.0, clock=clock)
+    waited = _run(bench, b, clock, 5, 20, settle_s=67.0, step_s=3.0)
+    assert b.shed == ["warm_creates", "hbm_settle_capped"] and not b.warm_allowed
+    assert len(waited) == 25 and waited[0] == 67.0 and max(waited[2:]) < 67.0
+    assert clock.t + b.TAIL_S <= 420 + 1e-6
+    rep = b.report()
+    assert rep["budget_s"] == 420 and rep["shed"] == b.shed and rep["settle_cap_s"] == b.settle_cap_s
+
+
+def test_run_budget_sheds_only_the_warm_creates_when_that_suffices():
+    import bench
+
+    clock = _Clock()
+    b = bench.RunBudget(330, t0=0.0, clock=clock)
+    waited = _run(bench, b, clock, 5, 20, settle_s=9.0, step_s=2.5, warm_steps=10)
+    assert b.shed == ["warm_creates"] and b.settle_cap_s is None and waited == [9.0] * 25
+
+
+def test_run_budget_zero_is_off():
+    import bench
+
+    clock = _Clock()
+    b = bench.RunBudget(0, t0=0.0, clock=clock)
+    _run(bench, b, clock, 5, 20, settle_s=100.0, step_s=3.0)
+    assert b.shed == [] and b.warm_allowed and b.projected_s > 0
+
+
+def test_bench_settle_passes_the_budget_cap_to_the_wait():
+    import bench
+
+    seen = []
+
+    class FakeHBM:
+        def settle(self, cards, floor, **kw):
+            seen.append(kw)
+            return {"waited_s": 0.0, "floor_by_card": {}, "reached_floor": True, "timed_out": False}
+
+    bench.settle_cards(FakeHBM(), ["card0"], [None], resident=False)
+    bench.settle_cards(FakeHBM(), ["card0"], [None], resident=False, timeout_s=3.5)
+    assert seen == [{}, {"timeout_s": 3.5}]

@@ -542,6 +542,65 @@ def test_preload_exports_and_stub_abi():
     out = __import__("subprocess").run(["nm", "-D", os.path.join(native.LIB_DIR, "libtk_rccl.so")],
                                        capture_output=True, text=True).stdout
     assert " T tkr_preload_device_code" in out and " T tkr_preloads_running" in out and " T tkr_inits_running" in out
+    assert " T tkr_preload_symbol" in out and " T tkr_elf_kernel_symbol" in out
+
+
+def _elf_scan(path: str) -> str:
+    import ctypes
+    import os
+
+    from triton_kubernetes_amd.ops import native
+
+    stub = ctypes.CDLL(os.path.join(native.LIB_DIR, "libtk_rccl_stub.so"))
+    stub.tkr_elf_kernel_symbol.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+    buf = ctypes.create_string_buffer(1024)
+    n = stub.tkr_elf_kernel_symbol(path.encode(), buf, len(buf))
+    assert n == len(buf.value)
+    return buf.value.decode()
+
+
+def test_preload_scan_finds_a_kernel_handle_in_every_librccl_on_this_image():
+    """the preload looked up two mangled names only.  /opt/rocm's librccl
+    exports them; the librccl torch ships (the one a process that imported torch first has
+    loaded) names its kernels ``rcclGenericKernel<...>`` -- there the lookup found nothing
+    and the preload silently did nothing.  The scan (tk_elf_scan.h) finds an exported
+    device-kernel handle in both, and never a debug variant."""
+    import glob
+    import os
+
+    import torch
+
+    rocm = os.path.realpath("/opt/rocm/lib/librccl.so.1")
+    torch_rccl = os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")
+    checked = 0
+    for path in (rocm, torch_rccl):
+        if not os.path.exists(path):
+            continue
+        name = _elf_scan(path)
+        assert "ncclDevKernelArgsStorage" in name and "Debug" not in name, (path, name)
+        out = __import__("subprocess").run(["nm", "-D", "--defined-only", path], capture_output=True,
+                                           text=True).stdout
+        assert f" {name}" in out  # an exported, defined symbol: dlsym finds it
+        checked += 1
+    assert checked >= 1
+    if os.path.exists(rocm):
+        assert _elf_scan(rocm) == "_Z23ncclDevKernel_Generic_124ncclDevKernelArgsStorageILm4096EE"
+    if os.path.exists(torch_rccl):
+        assert _elf_scan(torch_rccl).startswith("_Z17rcclGenericKernel")
+
+
+def test_preload_scan_refuses_what_is_not_a_librccl(tmp_path):
+    import os
+
+    from triton_kubernetes_amd.ops import native
+
+    assert _elf_scan(os.path.join(native.LIB_DIR, "libtk_topo.so")) == ""  # an ELF without RCCL kernels
+    junk = tmp_path / "junk.so"
+    junk.write_bytes(b"\x7fELF" + b"\x02" + b"\x00" * 200)  # a truncated header
+    assert _elf_scan(str(junk)) == ""
+    assert _elf_scan(str(tmp_path / "missing.so")) == ""
+    (tmp_path / "empty.so").write_bytes(b"")
+    assert _elf_scan(str(tmp_path / "empty.so")) == ""
 
 
 def test_eight_gpus_burn_in_concurrently_and_release_together(burnin_child, monkeypatch, tmp_path):

@@ -137,3 +137,62 @@ bench.main()
     line = json.loads(next(ln for ln in res.stdout.splitlines() if ln.startswith("{")))
     assert line["value"] is None and line["ms_per_step"] is None and line["completed_steps"] == 0
     assert "gate failed on purpose" in line["error"] and line["n_gpus"] == 1
+
+
+def _line(stdout: str) -> dict:
+    return json.loads([ln for ln in stdout.splitlines() if ln.startswith("{")][-1])
+
+
+def test_bench_gpus_without_a_launcher_is_one_agent_over_n_gpus():
+    """``python bench.py --gpus 8`` (no torchrun, WORLD_SIZE unset): one process, one node
+    agent over devices 0..7, an 8-rank gate -- never a silent 1-GPU run (VERDICT r5 #2)."""
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["OMP_NUM_THREADS"] = "1"
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "8", "--steps", "1",
+                           "--warmup", "0", "--warm-steps", "0", "--sim-gpu"],
+                          capture_output=True, text=True, timeout=240, cwd=ROOT, env=env)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    assert "using WORLD_SIZE" not in proc.stderr
+    doc = _line(proc.stdout)
+    assert doc["n_gpus"] == 8 and doc["config"]["workers"] == 1 and doc["config"]["gpus_per_worker"] == 8
+    assert doc["rccl_gate_ranks"] == [8]
+
+
+def test_bench_fails_loudly_when_fewer_gpus_are_visible():
+    """Without ``--sim-gpu`` this container sees no GPU: ``--gpus 2`` must not measure 0 or 1
+    of them.  The line says what is wrong (value null) and the exit status is non-zero."""
+    env = dict(os.environ, OMP_NUM_THREADS="1")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "1",
+                           "--warmup", "0"], capture_output=True, text=True, timeout=120, cwd=ROOT, env=env)
+    assert proc.returncode == 2
+    doc = _line(proc.stdout)
+    assert doc["value"] is None and doc["n_gpus"] == 2
+    assert doc["error"] == "2 GPUs requested, 0 visible"
+
+
+def test_bench_torchrun_world_must_match_gpus():
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "4", "--steps", "1", "--warmup", "0", "--warm-steps", "0", "--sim-gpu"]
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT,
+                          env=dict(os.environ, OMP_NUM_THREADS="1"))
+    assert proc.returncode != 0
+    doc = _line(proc.stdout)
+    assert doc["value"] is None and "WORLD_SIZE 2" in doc["error"]
+
+
+def test_resolve_gpus_shapes():
+    sys.path.insert(0, ROOT)
+    import bench
+
+    assert bench.resolve_gpus(8, 1, 8, sim=False) == {"n_gpus": 8, "visible": 8, "masked": False}
+    assert bench.resolve_gpus(2, 1, 8, sim=False)["masked"] is False  # devices 0..1 of 8
+    assert bench.resolve_gpus(8, 8, 8, sim=False)["masked"] is False  # torchrun, every rank sees all
+    assert bench.resolve_gpus(8, 8, 1, sim=False)["masked"] is True   # torchrun, one GPU per rank
+    assert bench.resolve_gpus(8, 1, 0, sim=True)["visible"] == 8
+    for args, msg in (((8, 1, 1), "8 GPUs requested, 1 visible"), ((2, 1, 0), "2 GPUs requested, 0 visible"),
+                      ((4, 2, 4), "WORLD_SIZE 2"), ((0, 1, 1), "at least 1"), ((8, 8, 0), "0 visible to rank")):
+        with pytest.raises(bench.GpuCountError, match=msg):
+            bench.resolve_gpus(*args, sim=False)

@@ -563,3 +563,48 @@ def test_eight_concurrent_burnins_in_one_process(probe):
         assert r.hbm["read_gbps"] > 0 and r.mfma["bf16"]["tflops"] > 0
     print(json.dumps({"read_gbps": [round(r.hbm["read_gbps"]) for r in results],
                       "bf16_tflops": [round(r.mfma["bf16"]["tflops"]) for r in results]}))
+
+
+def test_rccl_preload_finds_a_kernel_handle_on_the_installed_librccl():
+    """``tkr_preload_device_code`` must start on the librccl this box runs --
+    /opt/rocm's (an agent's default runtime, no torch in the process) and torch's (a process
+    that imported torch first).  A ROCm update that renames RCCL's kernels past what the
+    scan recognises fails here, not as ~60 ms more on every create."""
+    code = ("import json, time; from triton_kubernetes_amd.ops import native, rccl\n"
+            "rccl.version()\n"
+            "ok = rccl.preload_device_code([0])\n"
+            "while rccl.preloads_running():\n"
+            "    time.sleep(0.01)\n"
+            "print(json.dumps(dict(rccl.preload_report(), started=ok, runtime=native.runtime_dir())), flush=True)\n"
+            "rccl.exit_now(0)\n")
+    env = dict(os.environ)
+    env.pop("TK_HIP_RUNTIME", None)
+    proc = subprocess.run(["timeout", "-k", "5", "120", sys.executable, "-c", code], capture_output=True, text=True,
+                          cwd=ROOT, env=env)
+    assert proc.returncode == 0, proc.stdout[-2000:] + proc.stderr[-2000:]
+    system = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
+    print(json.dumps({"system": system}))
+    assert system["runtime"] == "system" and system["started"] is True
+    assert system["how"] == "known" and "ncclDevKernel_Generic" in system["symbol"], system
+
+    import torch  # noqa: F401  (this process: torch's librccl, loaded first)
+    from triton_kubernetes_amd.ops import rccl
+
+    assert rccl.preload_device_code([0]) is True
+    while rccl.preloads_running():
+        time.sleep(0.01)
+    rep = rccl.preload_report()
+    print(json.dumps({"in_process": rep}))
+    assert rep["how"] in ("known", "scan") and "ncclDevKernelArgsStorage" in rep["symbol"], rep
+
+
+def test_bench_refuses_more_gpus_than_visible():
+    """on this one-GPU box ``bench.py --gpus 2`` (no launcher) must fail with
+    the reason in its line, never measure one GPU as two."""
+    proc = subprocess.run(["timeout", "-k", "5", "120", sys.executable, os.path.join(ROOT, "bench.py"), "--gpus",
+                           "2", "--steps", "1", "--warmup", "0"], capture_output=True, text=True, cwd=ROOT,
+                          env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
+    assert proc.returncode == 2, proc.stdout[-2000:] + proc.stderr[-2000:]
+    line = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
+    assert line["value"] is None and line["n_gpus"] == 2
+    assert line["error"] == "2 GPUs requested, 1 visible", line

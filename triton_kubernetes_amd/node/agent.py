@@ -272,6 +272,7 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
             # RCCL's device code starts loading now, beside the rest of the start-up, not
             # after the cluster gate's first request (tkr_preload_device_code)
             self.startup_ms["rccl_preload_started"] = float(rccl.preload_device_code(self.devices))
+            self.rccl_preload = rccl.preload_report()
         # the full burn-in's ~300 GB memtest memory is released off the bring-up path
         probe.set_async_free(True)
         # ... and the full memtest's ~300 GB is held and released by a gpu-burnin child, so no
@@ -283,7 +284,8 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         burnin_child = os.environ.get("TK_BURNIN_PROCESS", "1") != "0"
         probe.set_burnin_process(burnin_child)
         # the gate's communicator over this node's GPUs allocates while the span is held
-        probe.set_span_headroom((4 << 30) + (512 << 20) * max(0, len(self.devices) - 1))
+        # (the constant floor, or what this node's gates measured: node/agent_gate.py)
+        probe.set_span_headroom(self.span_headroom(len(self.devices)))
         # ...and releases the HBM it tested only once this agent's RCCL communicator inits
         # are through: the driver's clearing of that release held their device-code load up
         if os.environ.get("TK_BURNIN_RELEASE_HOLD", "1") != "0":
@@ -306,6 +308,7 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         self.startup_ms["uid"] = round((time.perf_counter() - t2) * 1e3, 1)
         if preload == "after-uid":  # the same, once RCCL's bootstrap has made the unique id
             self.startup_ms["rccl_preload_started"] = float(rccl.preload_device_code(self.devices))
+            self.rccl_preload = rccl.preload_report()
         try:
             topo.native_topology("sysfs", "/nonexistent")  # loads libtk_topo.so
         except Exception:  # noqa: BLE001 - topology falls back to other sources later
@@ -513,6 +516,9 @@ def main(argv: Optional[List[str]] = None) -> int:
 
     print(json.dumps({"listening": url, "token_from_file": bool(token), "tls": ssl_ctx is not None,
                       "hip_runtime": native._runtime_dir or "not loaded",
+                      # the kernel handle RCCL's device-code preload used, or "none" (a librccl
+                      # exporting no device kernel: the gate's first init then loads it)
+                      "rccl_preload": getattr(agent, "rccl_preload", {"symbol": "none", "how": "none"}),
                       "startup_ms": dict(getattr(agent, "startup_ms", {}),
                                          main_to_serve=round((time.perf_counter() - t_main) * 1e3, 1))}),
           flush=True)

@@ -46,6 +46,10 @@ class _SimGate:
         pass
 
 
+# appended to the error of an init that failed again after the spans' release
+RETRIED_MARK = "[gate_retry: oom, failed again after the held spans' release]"
+
+
 class GateAborted(RuntimeError):
     """The gate was aborted (``/v1/rccl-abort``) before or while this request ran."""
 
@@ -100,9 +104,111 @@ class AgentGateMixin:
         from ..ops import rccl
 
         deadline = time.monotonic() + self.RELEASE_HOLD_S
+        release_now = self._release_event()
         while ((rccl.inits_running() > 0 or rccl.preloads_running() > 0 or getattr(self, "_links_pending", False))
-               and time.monotonic() < deadline):
+               and time.monotonic() < deadline and not release_now.is_set()):
             time.sleep(0.005)
+
+    # --- a gate communicator that ran out of HBM beside held burn-in spans ----------------------
+    # A full burn-in's span leaves ``probe.SPAN_HEADROOM`` of each GPU free, and the gate's
+    # communicator init allocates into it while the span is held (the hold above).  On a node
+    # of 8 xGMI peers that headroom was a constant nobody had measured, so an init can run
+    # out of memory there.  Then every held span is released and the init is retried once
+    # (``gate_retry: oom`` in the answer), and the footprint each successful init measured
+    # (hipMemGetInfo around it, ``tk_rccl_probe.hip``) sets the node's headroom from then on
+    # (:meth:`_note_gate_footprint`), the constant staying the floor.
+
+    FOOTPRINT_FILE = "/etc/triton-kubernetes/gate-footprint.json"
+    HEADROOM_MARGIN = 1.25  # measured footprint x this, plus the floor's first GiB
+
+    def _release_event(self):
+        ev = self.__dict__.get("_release_now")
+        if ev is None:
+            import threading
+
+            ev = self.__dict__.setdefault("_release_now", threading.Event())
+        return ev
+
+    def _release_held_spans(self) -> float:
+        """Every burn-in child still holding the HBM it tested releases it now; returns once
+        they have exited (ms).  The driver clears the release afterwards, which the retried
+        init's allocations wait for."""
+        from ..ops import probe
+
+        t0 = time.perf_counter()
+        ev = self._release_event()
+        ev.set()
+        try:
+            probe.wait_frees()
+        finally:
+            ev.clear()
+        return round((time.perf_counter() - t0) * 1e3, 1)
+
+    def _sweep_oom_retry(self, first, remake, sweep):
+        """``sweep(first())``; when that fails because the communicator's init ran out of
+        device memory (``ops/rccl.is_oom_error``), release the held spans and run
+        ``sweep(remake())`` once.  Returns ``(result, retry detail or None)``."""
+        from ..ops import rccl
+
+        try:
+            return sweep(first()), None
+        except rccl.RCCLError as exc:
+            if not rccl.is_oom_error(str(exc)):
+                raise
+            first_error = str(exc)
+        with span("node.rccl_gate_retry", node=self.name, why="oom"):
+            released_ms = self._release_held_spans()
+            try:
+                res = sweep(remake())
+            except rccl.RCCLError as exc:
+                # once only: the cluster gate sees it was retried (RETRIED_MARK) and does not
+                raise rccl.RCCLError(f"{exc} {RETRIED_MARK}") from exc
+        return res, {"gate_retry": "oom", "first_error": first_error[:400], "spans_released_ms": released_ms}
+
+    def _note_gate_footprint(self, ndev: int, phase_ms: Dict[str, float]) -> None:
+        """Keep the largest per-GPU footprint a gate communicator over ``ndev`` of this node's
+        GPUs measured (``footprint_total_mib``: the communicator and its sweep buffers), and
+        size the burn-in span's headroom from it (never below the constant floor)."""
+        mib = float(phase_ms.get("footprint_total_mib") or 0.0)
+        if mib <= 0:
+            return
+        import json
+
+        from ..ops import probe
+
+        with self._gate_mu:
+            fp = self.__dict__.setdefault("_gate_footprints", self._load_gate_footprints())
+            key = str(int(ndev))
+            if mib <= float(fp.get(key, 0.0)):
+                return
+            fp[key] = round(mib, 1)
+            doc = dict(fp)
+        try:
+            self.write_file(self.FOOTPRINT_FILE, json.dumps(doc, sort_keys=True))
+        except Exception:  # noqa: BLE001 - a read-only root only loses the memory of it
+            pass
+        probe.set_span_headroom(self.span_headroom(len(self.devices)))
+
+    def _load_gate_footprints(self) -> Dict[str, float]:
+        import json
+
+        try:
+            with open(self.path(self.FOOTPRINT_FILE), "r", encoding="utf-8") as fh:
+                doc = json.load(fh)
+            return {str(k): float(v) for k, v in doc.items()} if isinstance(doc, dict) else {}
+        except (OSError, ValueError, TypeError):
+            return {}
+
+    def span_headroom(self, ndev: int) -> int:
+        """HBM a full burn-in span leaves free on each GPU of this node: the constant floor
+        (4 GiB + 512 MiB per further GPU), or the largest gate footprint this node has
+        measured for ``ndev`` GPUs (x :attr:`HEADROOM_MARGIN`, plus 1 GiB), whichever is more."""
+        floor = (4 << 30) + (512 << 20) * max(0, ndev - 1)
+        fp = self.__dict__.get("_gate_footprints")
+        if fp is None:
+            fp = self.__dict__.setdefault("_gate_footprints", self._load_gate_footprints())
+        mib = float(fp.get(str(int(ndev)), 0.0))
+        return max(floor, int(mib * self.HEADROOM_MARGIN * (1 << 20)) + (1 << 30))
 
     def _gate_devices(self, ndev: int) -> List[int]:
         devs = self.devices or [0]
@@ -222,9 +328,11 @@ class AgentGateMixin:
         return None
 
     def rccl_gate(self, rank: int, world: int, uid: bytes, sizes: List[int], iters: int = 10,
-                  ndev: int = 1, timeout_s: float = 600.0) -> Dict[str, Any]:
+                  ndev: int = 1, timeout_s: float = 600.0, release_holds: bool = False) -> Dict[str, Any]:
         """Run this node's ranks ``rank .. rank+ndev-1`` of the cluster gate: the pending
-        communicator from rccl_prepare when there is one, else a fresh init."""
+        communicator from rccl_prepare when there is one, else a fresh init.
+        ``release_holds``: the cluster gate's retry after a member's init ran out of device
+        memory -- the burn-in spans this node still holds are released first."""
         key = uid  # the request's uid: /v1/rccl-abort names this one
         with self._gate_mu:
             if self._is_aborted(key):
@@ -250,13 +358,20 @@ class AgentGateMixin:
                     out = sub.to_json()
                 out.update(pipelined=True, shared_with="rccl_local",
                            ranks=list(range(rank, rank + len(self._gate_devices(ndev)))))
+                if len(done) > 2 and done[2]:
+                    out.update(done[2])  # the rccl_local step's retry, reported with the gate
                 return out
             # sizes the local sweep did not cover: the node is the whole gate, so a fresh
             # communicator under a new id (every rank is here) measures them
             uid = self._make_uid()
         pipelined = entry is not None
+        retry: Optional[Dict[str, Any]] = None
         with span("node.rccl_gate", node=self.name, rank=rank, world=world, pipelined=pipelined):
             try:
+                if release_holds:
+                    # the cluster gate's retry after a member's init ran out of device memory:
+                    # this node's held spans go before its communicator allocates
+                    retry = {"gate_retry": "oom", "spans_released_ms": self._release_held_spans()}
                 if entry is not None:
                     gate = entry[0]
                 else:
@@ -276,14 +391,43 @@ class AgentGateMixin:
                         gate.abort()
                         raise GateAborted("gate aborted while this node's communicator started")
                 # the communicator teardown is not part of the readiness answer: it is
-                # joined in stop() (or by the next process-exit drain), not here
-                res = gate.sweep(sizes, iters=iters, warmup=2, async_teardown=True, timeout_s=timeout_s)
+                # joined in stop() (or by the next process-exit drain), not here.  A node that
+                # is the whole gate retries an init that ran out of memory by itself (every
+                # rank is here); a member of a larger gate reports it, and the cluster gate
+                # retries every member under a new id (readiness/gate.py)
+                first_gate = gate
+
+                def remake():
+                    nonlocal gate
+                    from ..ops import rccl
+
+                    fresh = rccl.GateComm(self._make_uid(), world, 0, list(first_gate.devices), blocking=False)
+                    with self._gate_mu:
+                        canceled = self._is_aborted(key)  # an abort during the spans' release
+                        if not canceled:
+                            self._sweeping[key] = fresh
+                    if canceled:
+                        fresh.abort()
+                        raise GateAborted("gate aborted while this node's communicator restarted")
+                    gate = fresh
+                    return fresh
+
+                def sweep(g):
+                    return g.sweep(sizes, iters=iters, warmup=2, async_teardown=True, timeout_s=timeout_s)
+
+                if world == len(gate.devices) and rank == 0 and not self._sim_gate and retry is None:
+                    res, retry = self._sweep_oom_retry(lambda: first_gate, remake, sweep)
+                else:
+                    res = sweep(gate)
             finally:
                 with self._gate_mu:
                     self._sweeping.pop(key, None)
+        self._note_gate_footprint(len(gate.devices), res.phase_ms)
         out = res.to_json()
         out["pipelined"] = pipelined
         out["ranks"] = list(range(rank, rank + len(gate.devices)))
+        if retry:
+            out.update(retry)
         return out
 
 

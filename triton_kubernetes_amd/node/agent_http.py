@@ -157,7 +157,8 @@ class AgentHTTPMixin:
                                                                 [int(s) for s in body.get("sizes", [1 << 20])],
                                                                 int(body.get("iters", 10)),
                                                                 int(body.get("ndev", 1)),
-                                                                float(body.get("timeout_s", 600.0))))
+                                                                float(body.get("timeout_s", 600.0)),
+                                                                bool(body.get("release_holds", False))))
                     if path == "/v1/rccl-abort":
                         return self._reply(200, agent.rccl_abort(base64.b64decode(body["uid"])))
                     if path == "/v1/cleanup":

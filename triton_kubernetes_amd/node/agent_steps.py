@@ -329,13 +329,20 @@ class AgentStepsMixin:
             if taken is not None:
                 uid, gate, meta = taken
                 sizes = sorted(set(sizes) | set(meta.get("sizes") or []))
-            else:
-                gate = rccl.GateComm(self._make_uid(), len(self.devices), 0, self.devices, blocking=True,
+
+            def fresh():
+                return rccl.GateComm(self._make_uid(), len(self.devices), 0, self.devices, blocking=True,
                                      prealloc_bytes=max(sizes))
-            res = gate.sweep(sizes, iters=10, warmup=2, async_teardown=True)
+
+            # an init that ran out of HBM beside the held burn-in spans: release them, retry
+            # once (node/agent_gate.py:_sweep_oom_retry)
+            res, retry = self._sweep_oom_retry(
+                (lambda: gate) if taken is not None else fresh, fresh,
+                lambda g: g.sweep(sizes, iters=10, warmup=2, async_teardown=True))
+            self._note_gate_footprint(len(self.devices), res.phase_ms)
             if taken is not None:
                 with self._gate_mu:
-                    self._gate_results[uid] = (res, time.time())
+                    self._gate_results[uid] = (res, time.time(), retry)
             floor = float(step.params.get("min_busbw", 0) or 0)
             if not res.ok:
                 raise StepFailed(step.name, "RCCL verification failed")
@@ -344,6 +351,8 @@ class AgentStepsMixin:
             out = res.to_json()
             if taken is not None:
                 out["shared_with"] = "cluster_gate"
+            if retry:
+                out.update(retry)
             return out
         if a == "agent":
             if plan.gpu is not None:

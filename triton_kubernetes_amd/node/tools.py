@@ -38,7 +38,7 @@ from ..ops.build import CSRC
 TOOL_SOURCES: Dict[str, List[str]] = {
     "amdgpu-topo-labeller": ["tk_topo.cpp"],
     "gpu-burnin": ["tk_gpu_probe.hip", "tk_gemm_screen.hip"],
-    "rccl-ready": ["tk_rccl_probe.hip", "tk_rccl_verify.h", "tk_rccl_group.h"],
+    "rccl-ready": ["tk_rccl_probe.hip", "tk_rccl_verify.h", "tk_rccl_group.h", "tk_elf_scan.h"],
 }
 PREBUILT_DIR = "/opt/triton-kubernetes/prebuilt"
 SOURCES_DIR = "/opt/triton-kubernetes/src"
@@ -124,7 +124,7 @@ tk_node_tools() { # <tools dir> <sources dir> <prebuilt dir> <rocm dir>
   pids="$pids $!"
   tk_node_tool "$T" "$S" "$P" gpu-burnin "tk_gpu_probe.hip tk_gemm_screen.hip" $R/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip -Wl,-rpath,$R/lib &
   pids="$pids $!"
-  tk_node_tool "$T" "$S" "$P" rccl-ready "tk_rccl_probe.hip tk_rccl_verify.h tk_rccl_group.h" $R/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$R/lib -lrccl -Wl,-rpath,$R/lib &
+  tk_node_tool "$T" "$S" "$P" rccl-ready "tk_rccl_probe.hip tk_rccl_verify.h tk_rccl_group.h tk_elf_scan.h" $R/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$R/lib -lrccl -Wl,-rpath,$R/lib &
   pids="$pids $!"
   for p in $pids; do wait "$p" || rc=1; done
   echo "node tools: $(( ($(date +%s%N) - t0) / 1000000 )) ms"

@@ -121,7 +121,8 @@ def targets() -> List[Target]:
     gemm = os.path.join(CSRC, "tk_gemm_screen.hip")
     topo = os.path.join(CSRC, "tk_topo.cpp")
     stub = os.path.join(CSRC, "tk_rccl_stub.cpp")
-    rccl_h = [os.path.join(CSRC, "tk_rccl_group.h"), os.path.join(CSRC, "tk_rccl_verify.h")]
+    rccl_h = [os.path.join(CSRC, "tk_rccl_group.h"), os.path.join(CSRC, "tk_rccl_verify.h"),
+              os.path.join(CSRC, "tk_elf_scan.h")]
     out = lambda n: os.path.join(LIB, n)  # noqa: E731
     return [
         Target("libtk_gpu_probe.so", [probe],

@@ -23,6 +23,7 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "tk_elf_scan.h"
 #include "tk_rccl_group.h"
 #include "tk_rccl_verify.h"
 
@@ -323,7 +324,20 @@ struct Gate {
   std::thread init_thread;
   size_t prealloc_bytes = 0;     // sweep buffers allocated by the init thread after the comms
   std::vector<RankBufs> bufs;    // (filled when prealloc_bytes > 0 and the init succeeded)
+  // device memory the init took, max over this gate's GPUs (hipMemGetInfo before and after):
+  // the communicators (RCCL's per-channel, per-peer buffers, its device code) and then the
+  // preallocated sweep buffers.  Device-wide: another process allocating meanwhile counts too
+  size_t footprint_comm = 0, footprint_total = 0;
 };
+// the footprint of the gate the calling thread last swept (tkr_last_footprint)
+static thread_local double g_last_footprint[2] = {0, 0};
+extern "C" double tkr_last_footprint(int which) { return which >= 0 && which < 2 ? g_last_footprint[which] : 0.0; }
+
+static size_t device_free(int dev) {
+  size_t free_b = 0, total_b = 0;
+  if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
+  return free_b;
+}
 static std::mutex g_gate_mu;
 static std::vector<std::pair<int, Gate*>> g_gates;
 // gates a tkr_gate_sweep is waiting on (taken out of g_gates): reachable by tkr_gate_cancel
@@ -344,10 +358,26 @@ extern "C" int tkr_inits_running() { return g_inits_running.load(); }
 // (profiles/round2/cold_rccl_init.md) -- overlaps the rest of its start-up instead of
 // following the gate's first request.  The load is triggered by the attributes query of
 // one kernel librccl exports; the runtime loads the library's whole code object for the
-// device then.  Returns 0 when started, 1 when this librccl exports no known kernel handle
-// (nothing started), -1 when librccl is not loaded.
+// device then.  The handle is looked up by name first (the names /opt/rocm's librccl
+// exports), then found by scanning the loaded librccl's dynamic symbols for any exported
+// device kernel (tk_elf_scan.h) -- torch's librccl names its kernels differently, and a
+// ROCm update may rename them.  Returns 0 when started, 1 when no kernel handle was found
+// (nothing started), -1 when librccl is not loaded.  tkr_preload_symbol names the handle
+// used and how it was found ("none" before a successful call).
 static std::atomic<int> g_preloads_running{0};
 extern "C" int tkr_preloads_running() { return g_preloads_running.load(); }
+static char g_preload_symbol[512] = "none";
+static char g_preload_how[16] = "none";
+extern "C" const char* tkr_preload_symbol() { return g_preload_symbol; }
+extern "C" const char* tkr_preload_how() { return g_preload_how; }
+
+// The kernel symbol tk_elf_scan.h finds in the ELF file at `path` ("" -> returns 0); for
+// tests and for the agent's start-up report.
+extern "C" int tkr_elf_kernel_symbol(const char* path, char* out, int cap) {
+  const std::string name = tk_elf_find_symbol(path, kTkRcclKernelNeedle, kTkRcclKernelReject);
+  if (cap > 0) snprintf(out, (size_t)cap, "%s", name.c_str());
+  return (int)name.size();
+}
 
 extern "C" int tkr_preload_device_code(int ndev, const int* devs) {
   void* lib = dlopen("librccl.so.1", RTLD_LAZY | RTLD_NOLOAD);
@@ -359,9 +389,28 @@ extern "C" int tkr_preload_device_code(int ndev, const int* devs) {
                                    "_Z23ncclDevKernel_Generic_224ncclDevKernelArgsStorageILm4096EE"};
   const void* handle = nullptr;
   for (const char* name : kHandles)
-    if ((handle = dlsym(lib, name)) != nullptr) break;
+    if ((handle = dlsym(lib, name)) != nullptr) {
+      snprintf(g_preload_symbol, sizeof(g_preload_symbol), "%s", name);
+      snprintf(g_preload_how, sizeof(g_preload_how), "known");
+      break;
+    }
+  if (!handle) {
+    // the file the loaded librccl came from: an exported function's dladdr
+    Dl_info info;
+    void* anchor = dlsym(lib, "ncclGetVersion");
+    if (anchor && dladdr(anchor, &info) && info.dli_fname) {
+      const std::string name = tk_elf_find_symbol(info.dli_fname, kTkRcclKernelNeedle, kTkRcclKernelReject);
+      if (!name.empty() && (handle = dlsym(lib, name.c_str())) != nullptr) {
+        snprintf(g_preload_symbol, sizeof(g_preload_symbol), "%s", name.c_str());
+        snprintf(g_preload_how, sizeof(g_preload_how), "scan");
+      }
+    }
+  }
   dlclose(lib);  // RTLD_NOLOAD took a reference of its own; the library stays loaded
-  if (!handle) return 1;
+  if (!handle) {
+    snprintf(g_err, sizeof(g_err), "librccl exports no device-kernel handle (%s)", kTkRcclKernelNeedle);
+    return 1;
+  }
   for (int i = 0; i < ndev; ++i) {
     const int dev = devs[i];
     g_preloads_running.fetch_add(1);
@@ -418,10 +467,48 @@ struct HipNcclApi {
   const char* error_string(int r) { return ncclGetErrorString((ncclResult_t)r); }
 };
 
+// An init that failed says what the devices had left: RCCL reports an allocation failure as
+// "unhandled cuda error" (or "unhandled system error"), and its own last-error text -- when
+// this librccl has ncclGetLastError -- names the failing call.  ops/rccl.py:is_oom_error reads
+// both (the agent releases held burn-in spans and retries once, node/agent_gate.py).
+static void annotate_init_error(Gate* g) {
+  using LastError = const char* (*)(ncclComm_t);
+  static LastError last = (LastError)dlsym(RTLD_DEFAULT, "ncclGetLastError");
+  size_t len = strnlen(g->err, sizeof(g->err));
+  if (last) {
+    const char* why = last(nullptr);
+    if (why && *why && len + 8 < sizeof(g->err)) {
+      snprintf(g->err + len, sizeof(g->err) - len, " [rccl: %s]", why);
+      len = strnlen(g->err, sizeof(g->err));
+    }
+  }
+  size_t low = SIZE_MAX;
+  int low_dev = -1;
+  for (int d : g->devices) {
+    const size_t f = device_free(d);
+    if (f < low) { low = f; low_dev = d; }
+  }
+  if (low_dev >= 0 && len + 8 < sizeof(g->err))
+    snprintf(g->err + len, sizeof(g->err) - len, " (device %d: %zu MiB free)", low_dev, low >> 20);
+}
+
 static void init_body(Gate* g, ncclUniqueId id) {
   HipNcclApi api{id};
+  const size_t nd = g->devices.size();
+  std::vector<size_t> before(nd);
+  for (size_t d = 0; d < nd; ++d) before[d] = device_free(g->devices[d]);
   const int r = tk_group_init(api, g->world, g->rank_base, (int)g->devices.size(), g->devices.data(),
                               g->comms.data(), g->err, sizeof(g->err));
+  if (r != 0) annotate_init_error(g);
+  auto taken = [&]() {
+    size_t most = 0;
+    for (size_t d = 0; d < nd; ++d) {
+      const size_t now = device_free(g->devices[d]);
+      if (before[d] > now && before[d] - now > most) most = before[d] - now;
+    }
+    return most;
+  };
+  if (r == 0) g->footprint_comm = g->footprint_total = taken();
   if (r == 0 && g->prealloc_bytes) {
     // the sweep's buffers too, so the gate request only runs collectives
     g->bufs.resize(g->devices.size());
@@ -433,6 +520,7 @@ static void init_body(Gate* g, ncclUniqueId id) {
         break;
       }
     }
+    g->footprint_total = taken();
   }
   bool orphan;
   {
@@ -610,6 +698,8 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
     release_gate(g, /*abort=*/true);
     return rc;
   }
+  g_last_footprint[0] = (double)g->footprint_comm;
+  g_last_footprint[1] = (double)g->footprint_total;
   if (g->init_thread.joinable()) g->init_thread.join();
   size_t max_bytes = 0;
   for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;

@@ -33,6 +33,7 @@
 #include <thread>
 #include <vector>
 
+#include "tk_elf_scan.h"
 #include "tk_rccl_group.h"
 #include "tk_rccl_verify.h"
 
@@ -50,7 +51,36 @@ struct StubGate {
   std::chrono::steady_clock::time_point t0;
   double init_ms = -1.0;
   std::atomic<bool> cancel{false};
+  std::string init_err;  // the init failed (the HBM model below): poll and sweep report it
 };
+thread_local double g_last_footprint[2] = {0, 0};
+
+// An HBM model for the gate's allocations, for tests of the agent's out-of-memory retry
+// (node/agent_gate.py): TK_RCCL_STUB_HBM_FREE names a file holding the bytes each GPU has
+// free (a test's burn-in child rewrites it as it holds and releases its span), and every GPU
+// of an init needs TK_RCCL_STUB_FOOTPRINT_MIB.  Short of that, the init fails with the
+// text libtk_rccl gives for RCCL's failed allocation.  Unset: every init fits.
+size_t stub_footprint() {
+  const char* f = getenv("TK_RCCL_STUB_FOOTPRINT_MIB");
+  return f && *f ? (size_t)strtoull(f, nullptr, 10) << 20 : 0;
+}
+
+bool stub_hbm_short(char* err, size_t errlen) {
+  const char* path = getenv("TK_RCCL_STUB_HBM_FREE");
+  if (!path || !*path) return false;
+  char buf[64] = {0};
+  const int fd = open(path, O_RDONLY);
+  if (fd < 0) return false;
+  const ssize_t n = read(fd, buf, sizeof(buf) - 1);
+  close(fd);
+  if (n <= 0) return false;
+  const size_t free_b = (size_t)strtoull(buf, nullptr, 10);
+  if (free_b >= stub_footprint()) return false;
+  snprintf(err, errlen,
+           "ncclCommInitRank: unhandled cuda error (run with NCCL_DEBUG=INFO for details) "
+           "[rccl: Cuda failure 'out of memory'] (device 0: %zu MiB free)", free_b >> 20);
+  return true;
+}
 std::map<int, StubGate*> g_gates;
 std::map<int, StubGate*> g_sweeping;  // gates inside tkr_gate_sweep (tkr_gate_cancel reaches them)
 
@@ -167,10 +197,18 @@ int tkr_gate_abandoned() { return 0; }
 int tkr_inits_running() { return 0; }  // no device code to load: nothing a release could hold up
 int tkr_preloads_running() { return 0; }
 int tkr_preload_device_code(int, const int*) { return 1; }  // no RCCL device code behind the stub
+const char* tkr_preload_symbol() { return "none"; }
+const char* tkr_preload_how() { return "none"; }
+int tkr_elf_kernel_symbol(const char* path, char* out, int cap) {  // the probe's scanner, on the CPU
+  const std::string name = tk_elf_find_symbol(path, kTkRcclKernelNeedle, kTkRcclKernelReject);
+  if (cap > 0) snprintf(out, (size_t)cap, "%s", name.c_str());
+  return (int)name.size();
+}
 int tkr_gate_pending() {
   std::lock_guard<std::mutex> lk(g_mu);
   return (int)g_gates.size();
 }
+double tkr_last_footprint(int which) { return which >= 0 && which < 2 ? g_last_footprint[which] : 0.0; }
 
 int tkr_gate_begin_ex(const unsigned char* uid128, int world, int rank_base, int ndev, const int* devices,
                       int blocking, size_t /*prealloc_bytes*/) {
@@ -185,6 +223,24 @@ int tkr_gate_begin_ex(const unsigned char* uid128, int world, int rank_base, int
   g->ndev = ndev;
   g->devices.assign(devices, devices + ndev);
   g->t0 = std::chrono::steady_clock::now();
+  char oom[512];
+  if (stub_hbm_short(oom, sizeof(oom))) {
+    if (blocking) {
+      snprintf(g_err, sizeof(g_err), "%s", oom);
+      log_call("begin", g, -2);
+      delete g;
+      return -2;
+    }
+    g->init_err = oom;  // a non-blocking init fails on its own thread: poll / sweep see it
+    int h;
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      h = g_next++;
+      g_gates[h] = g;
+    }
+    log_call("begin-oom", g, h);
+    return h;
+  }
   mkdir(base_dir().c_str(), 0755);
   mkdir(g->dir.c_str(), 0755);
   // one world size per unique id (the first rank to arrive records it)
@@ -242,14 +298,18 @@ int tkr_gate_poll(int h) {
     snprintf(g_err, sizeof(g_err), "unknown gate %d", h);
     return -1;
   }
+  if (!it->second->init_err.empty()) {
+    snprintf(g_err, sizeof(g_err), "%s", it->second->init_err.c_str());
+    return -2;
+  }
   return count_prefix(it->second->dir, "rank-") >= it->second->world ? 0 : 1;
 }
 
 int tkr_gate_abort(int h) {
   StubGate* g = take(h);
   if (!g) return -1;
-  const int pending = count_prefix(g->dir, "rank-") < g->world ? 1 : 0;
-  unclaim(g);
+  const int pending = g->init_err.empty() && count_prefix(g->dir, "rank-") < g->world ? 1 : 0;
+  if (g->init_err.empty()) unclaim(g);  // a failed init claimed nothing
   log_call("abort", g, pending);
   delete g;
   return pending;
@@ -285,6 +345,16 @@ int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int /*iters*/, int /*
     return -1;
   }
   const auto t = std::chrono::steady_clock::now();
+  if (!g->init_err.empty()) {
+    snprintf(g_err, sizeof(g_err), "%s", g->init_err.c_str());
+    {
+      std::lock_guard<std::mutex> lk(g_mu);
+      g_sweeping.erase(h);
+    }
+    log_call("sweep", g, -2);
+    delete g;
+    return -2;
+  }
   int rc = wait_for(g, "rank-", g->world, timeout_ms);  // the communicator's init
   if (g->init_ms < 0 && rc == 0) g->init_ms = ms_since(g->t0);
   phase_ms[0] = ms_since(t);
@@ -314,6 +384,7 @@ int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int /*iters*/, int /*
     }
     phase_ms[1] = 0.0;
     phase_ms[2] = ms_since(t) - phase_ms[0];
+    g_last_footprint[0] = g_last_footprint[1] = (double)stub_footprint();
     phase_ms[3] = 0.0;
     // the last rank to leave removes the rendezvous
     for (int d = 0; d < g->ndev; ++d) touch_excl(g->dir + "/done-" + std::to_string(g->rank_base + d));

@@ -185,6 +185,13 @@ class GateComm:
                             f"{lib.tkr_last_error().decode()}")
         phases = {"init_wait": round(ph[0], 3), "alloc": round(ph[1], 3), "sweep": round(ph[2], 3),
                   "teardown": round(ph[3], 3), "init_total": round(ph[4], 3)}
+        if hasattr(lib, "tkr_last_footprint"):
+            # device memory the init took per GPU (max over this process's ranks): the
+            # communicators, then with their preallocated sweep buffers (tk_rccl_probe.hip)
+            lib.tkr_last_footprint.restype = ctypes.c_double
+            lib.tkr_last_footprint.argtypes = [ctypes.c_int]
+            phases["footprint_mib"] = round(lib.tkr_last_footprint(0) / 2 ** 20, 1)
+            phases["footprint_total_mib"] = round(lib.tkr_last_footprint(1) / 2 ** 20, 1)
         return SweepResult(self.world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
                            float(ph[4]), phases)
 
@@ -201,6 +208,25 @@ class GateComm:
             _lib().tkr_gate_cancel(h)
             if h == self.handle:
                 self.handle = None
+
+
+# A failed init whose least-free GPU had less than this left ran out of memory, whatever
+# RCCL called the failure ("unhandled cuda error" / "unhandled system error")
+OOM_FREE_MIB = 2048
+
+
+def is_oom_error(text: str) -> bool:
+    """An RCCL communicator init that failed for lack of device memory, by the error text
+    libtk_rccl gives (``tk_rccl_probe.hip:annotate_init_error``): RCCL's own last error naming
+    an out-of-memory allocation, or an unhandled HIP/system error with a GPU nearly full."""
+    import re
+
+    low = (text or "").lower()
+    if "out of memory" in low or "outofmemory" in low:
+        return True
+    m = re.search(r"\(device \d+: (\d+) mib free\)", low)
+    return bool(m and ("unhandled cuda error" in low or "unhandled system error" in low)
+                and int(m.group(1)) < OOM_FREE_MIB)
 
 
 def pending_gates() -> int:
@@ -228,6 +254,26 @@ def preload_device_code(devices: Sequence[int]) -> bool:
     if not devs:
         return False
     return _lib().tkr_preload_device_code(len(devs), (ctypes.c_int * len(devs))(*devs)) == 0
+
+
+def preload_report() -> dict:
+    """Which kernel handle the last :func:`preload_device_code` used and how it was found
+    (``known``: one of the names /opt/rocm's librccl exports; ``scan``: found in the loaded
+    librccl's dynamic symbols, ``ops/csrc/tk_elf_scan.h``), or ``none``."""
+    lib = _lib()
+    lib.tkr_preload_symbol.restype = ctypes.c_char_p
+    lib.tkr_preload_how.restype = ctypes.c_char_p
+    return {"symbol": lib.tkr_preload_symbol().decode(), "how": lib.tkr_preload_how().decode()}
+
+
+def elf_kernel_symbol(path: str) -> str:
+    """The RCCL device-kernel handle the preload's scan finds in the library file at
+    ``path`` ("" when none): the same scanner, callable without a GPU."""
+    lib = _lib()
+    lib.tkr_elf_kernel_symbol.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
+    buf = ctypes.create_string_buffer(1024)
+    lib.tkr_elf_kernel_symbol(path.encode(), buf, len(buf))
+    return buf.value.decode()
 
 
 def preloads_running() -> int:

@@ -150,21 +150,33 @@ class ClusterGate:
             self.uid = self.transport.post(self.members[0].host, "/v1/rccl-uid", {})["uid"]
         uid = self.uid
         results = self._gate_all(uid)
+        retry = None
+        if not all(r.get("ok") for r in results) and any(_oom(r.get("error")) for r in results):
+            # a member's communicator init ran out of device memory beside its held burn-in
+            # spans (node/agent_gate.py): every member releases its spans, and the gate runs
+            # once more under a new id
+            first = [f"{m.url}: {r['error']}" for m, r in zip(self.members, results) if _oom(r.get("error"))]
+            with span("gate.retry", world=self.world, why="oom"):
+                self.uid = uid = self.transport.post(self.members[0].host, "/v1/rccl-uid", {})["uid"]
+                results = self._gate_all(uid, release_holds=True)
+            retry = {"why": "oom", "first_errors": first}
         self.done = True
         ok = all(r.get("ok") for r in results)
         busbw = [max(r.get("busbw_gbps") or [0.0]) for r in results]
         errors = [f"{m.url}: {r['error']}" for m, r in zip(self.members, results) if r.get("error")]
         return {"ok": ok, "world": self.world, "nodes": len(self.members), "pipelined": pipelined,
-                "prepare_error": self.prepare_error, "errors": errors,
+                "prepare_error": self.prepare_error, "errors": errors, "retry": retry,
                 "min_peak_busbw_gbps": min(busbw) if busbw else 0.0, "ranks": results}
 
-    def _gate_all(self, uid: str) -> List[Dict[str, Any]]:
+    def _gate_all(self, uid: str, release_holds: bool = False) -> List[Dict[str, Any]]:
         """Every member's ``/v1/rccl-gate`` at once; the first failure cancels the rest."""
         def one(m: GateMember) -> Dict[str, Any]:
+            body = {"uid": uid, "rank": m.rank_base, "world": self.world, "ndev": m.ndev,
+                    "sizes": self.sizes, "iters": self.iters, "timeout_s": self.timeout_s}
+            if release_holds:
+                body["release_holds"] = True
             try:
-                return self.transport.post(m.host, "/v1/rccl-gate", {
-                    "uid": uid, "rank": m.rank_base, "world": self.world, "ndev": m.ndev,
-                    "sizes": self.sizes, "iters": self.iters, "timeout_s": self.timeout_s})
+                return self.transport.post(m.host, "/v1/rccl-gate", body)
             except Exception as exc:  # noqa: BLE001 - reported per member
                 return {"ok": False, "error": f"{type(exc).__name__}: {exc}"}
 
@@ -200,6 +212,17 @@ class ClusterGate:
                 pass
         self.prepared = False
         self.uid = None
+
+
+def _oom(error: Optional[str]) -> bool:
+    """A member's init ran out of device memory, and that member has not retried it already
+    (a node that is the whole gate retries by itself, node/agent_gate.py)."""
+    if not error:
+        return False
+    from ..node.agent_gate import RETRIED_MARK
+    from ..ops.rccl import is_oom_error
+
+    return is_oom_error(error) and RETRIED_MARK not in error
 
 
 __all__ = ["ClusterGate", "GateMember", "members_from"]

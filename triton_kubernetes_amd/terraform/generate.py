@@ -1466,7 +1466,8 @@ data "external" "gpu_labels" {{
          "src/tk_gemm_screen.hip": os.path.join(CSRC, "tk_gemm_screen.hip"),
          "src/tk_rccl_probe.hip": os.path.join(CSRC, "tk_rccl_probe.hip"),
          "src/tk_rccl_verify.h": os.path.join(CSRC, "tk_rccl_verify.h"),
-         "src/tk_rccl_group.h": os.path.join(CSRC, "tk_rccl_group.h")}))
+         "src/tk_rccl_group.h": os.path.join(CSRC, "tk_rccl_group.h"),
+         "src/tk_elf_scan.h": os.path.join(CSRC, "tk_elf_scan.h")}))
 
     # MI355X cluster add-ons: one template per object from k8s/addons.py (the DirectExecutor
     # renders these same files), filtered by group, then applied through Rancher's k8s proxy
