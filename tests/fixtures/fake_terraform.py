@@ -34,8 +34,10 @@ code (nothing here imports ``triton_kubernetes_amd``):
                rancher2_connection_info.json``) and fails the module -- as the real join
                fails -- on a host still joined to another cluster; a destroy runs the
                module's destroy-time ``remote-exec`` (``when = destroy``) locally against
-               that root (``TK_HOST_ROOT``), honouring ``count = var.X ? 1 : 0`` and
-               ``on_failure = continue``.
+               that root (``TK_HOST_ROOT``) -- ``inline`` joined into one script, ``self.input``
+               the values of the last apply -- honouring ``count = var.X ? 1 : 0`` and
+               ``on_failure = continue``; a re-apply that takes such a ``count`` from 1 to 0
+               destroys that instance, running its destroy-time provisioner, as Terraform does.
 
 Every call appends ``{"argv", "cwd", "doc", "prior"}`` to ``$FAKE_TF_LOG`` (``prior``:
 serial/lineage/modules of the state the command started from).  ``FAKE_TF_FAIL=<cmd>``
@@ -213,8 +215,13 @@ def _locals(text):
 def _var_defaults(text):
     out = {}
     for m in re.finditer(r'^variable\s+"(\w+)"\s*\{', text, re.M):
-        d = re.search(r'^\s*default\s*=\s*"((?:[^"\\]|\\.)*)"', _braced(text, m.end() - 1), re.M)
+        body = _braced(text, m.end() - 1)
+        d = re.search(r'^\s*default\s*=\s*"((?:[^"\\]|\\.)*)"', body, re.M)
         if d:
+            out[m.group(1)] = d.group(1)
+            continue
+        d = re.search(r'^\s*default\s*=\s*(true|false|-?\d+)\s*$', body, re.M)
+        if d:  # a bool or number default, in its string form
             out[m.group(1)] = d.group(1)
     return out
 
@@ -381,41 +388,119 @@ def join_host(key, block, path):
     return None
 
 
+def _bracketed(text, start):
+    """The text between the bracket at ``start`` and its match (strings skipped)."""
+    depth, i, quote = 0, start, False
+    while i < len(text):
+        ch = text[i]
+        if quote:
+            if ch == "\\":
+                i += 1
+            elif ch == '"':
+                quote = False
+        elif ch == '"':
+            quote = True
+        elif ch in "[(":
+            depth += 1
+        elif ch in "])":
+            depth -= 1
+            if depth == 0:
+                return text[start + 1:i]
+        i += 1
+    return text[start + 1:]
+
+
 def destroy_provisioners(mod_dir):
-    """[(count gate variable or None, script file)] of the destroy-time remote-exec
-    provisioners of the module's resources."""
+    """The destroy-time remote-exec provisioners of the module's resources:
+    ``[(count gate variable or None, {input key: variable}, inline parts, on_failure
+    continue)]``; an inline part is ``("str", text)`` or ``("file", path)``."""
     text = _module_text(mod_dir)
     out = []
     for m in re.finditer(r'^resource\s+"\w+"\s+"\w+"\s*\{', text, re.M):
         body = _braced(text, m.end() - 1)
         gate = re.search(r"^\s*count\s*=\s*var\.(\w+)\s*\?\s*1\s*:\s*0\s*$", body, re.M)
+        inp = re.search(r"^\s*input\s*=\s*\{", body, re.M)
+        inputs = dict(re.findall(r"^\s*(\w+)\s*=\s*var\.(\w+)\s*$", _braced(body, inp.end() - 1), re.M)) if inp else {}
         for p in re.finditer(r'provisioner\s+"remote-exec"\s*\{', body):
             pb = _braced(body, p.end() - 1)
             if not re.search(r"^\s*when\s*=\s*destroy\s*$", pb, re.M):
                 continue
-            f = re.search(r'file\("\$\{path\.module\}/([^"]+)"\)', pb)
             cont = re.search(r"^\s*on_failure\s*=\s*continue\s*$", pb, re.M) is not None
-            if f:
-                out.append((gate.group(1) if gate else None, os.path.join(mod_dir, f.group(1)), cont))
+            il = re.search(r"\binline\s*=\s*\[", pb)
+            if not il:
+                continue
+            parts = []
+            for e in re.finditer(r'file\("\$\{path\.module\}/([^"]+)"\)|"((?:[^"\\]|\\.)*)"',
+                                 _bracketed(pb, il.end() - 1)):
+                parts.append(("file", os.path.join(mod_dir, e.group(1))) if e.group(1) else ("str", e.group(2)))
+            out.append((gate.group(1) if gate else None, inputs, parts, cont))
     return out
 
 
-def destroy_host(key, block, mod_dir):
+def module_vars(block, mod_dir):
+    """The module's variable values as applied: the block's arguments over the defaults
+    (strings, as Terraform interpolates them: ``true`` / ``false`` for bools)."""
+    vals = dict(_var_defaults(_module_text(mod_dir)))
+    for k, v in block.items():
+        vals[k] = ("true" if v else "false") if isinstance(v, bool) else v if isinstance(v, str) else json.dumps(v)
+    return vals
+
+
+def _falsy(v):
+    return str(v).lower() in ("false", "0")
+
+
+def run_destroy_provisioner(key, applied, inputs, parts, cont):
+    """One destroy-time remote-exec against the host root, ``self`` being the resource as
+    last applied (``applied``: the module's variable values then).  Terraform writes the
+    ``inline`` parts, joined by newlines, to one script and runs it."""
+    self_input = {k: applied.get(v, "") for k, v in inputs.items()}
+    lines = []
+    for kind, val in parts:
+        if kind == "file":
+            lines.append(open(val, encoding="utf-8").read())
+        else:
+            lines.append(re.sub(r"\$\{self\.input\.(\w+)\}", lambda m: str(self_input.get(m.group(1), "")),
+                                val.encode().decode("unicode_escape")))
+    env = dict(os.environ, TK_HOST_ROOT=host_root(str(applied.get("host", ""))))
+    proc = subprocess.run(["bash", "-s"], input="\n".join(lines), env=env, capture_output=True, text=True,
+                          timeout=120)
+    sys.stdout.write(f"module.{key}: Destroying... (remote-exec)\n{proc.stdout}")
+    if proc.returncode != 0:
+        if not cont:
+            return f"remote-exec provisioner error (destroy) in module.{key}: exit {proc.returncode}"
+        sys.stderr.write(f"Warning: module.{key}: destroy-time provisioner failed (on_failure = continue): "
+                         f"{proc.stderr[-300:]}\n")
+    return None
+
+
+def destroy_host(key, applied, mod_dir):
     """Run the destroy-time provisioners of a host module against its host root."""
-    defaults = _var_defaults(_module_text(mod_dir))
-    for gate, script, cont in destroy_provisioners(mod_dir):
-        if gate is not None:
-            val = block.get(gate, defaults.get(gate, "true"))
-            if str(val).lower() in ("false", "0"):
-                continue  # count = 0: the resource (and its provisioner) does not exist
-        env = dict(os.environ, TK_HOST_ROOT=host_root(str(block.get("host", ""))))
-        proc = subprocess.run(["bash", script], env=env, capture_output=True, text=True, timeout=120)
-        sys.stdout.write(f"module.{key}: Destroying... (remote-exec)\n{proc.stdout}")
-        if proc.returncode != 0:
-            if not cont:
-                return f"remote-exec provisioner error (destroy) in module.{key}: exit {proc.returncode}"
-            sys.stderr.write(f"Warning: module.{key}: destroy-time provisioner failed (on_failure = continue): "
-                             f"{proc.stderr[-300:]}\n")
+    for gate, inputs, parts, cont in destroy_provisioners(mod_dir):
+        if gate is not None and _falsy(applied.get(gate, "true")):
+            continue  # count = 0: the resource (and its provisioner) does not exist
+        err = run_destroy_provisioner(key, applied, inputs, parts, cont)
+        if err:
+            return err
+    return None
+
+
+def reapply_host(key, prior_vars, applied, mod_dir):
+    """An apply of a host module already in the state: a count-gated resource whose count
+    goes 1 -> 0 is destroyed, its destroy-time provisioner running (``self``: the resource
+    as last applied).  Other argument changes update in place."""
+    for gate, inputs, parts, cont in destroy_provisioners(mod_dir):
+        if gate is not None and not _falsy(prior_vars.get(gate, "true")) and _falsy(applied.get(gate, "true")):
+            err = run_destroy_provisioner(key, prior_vars, inputs, parts, cont)
+            if err:
+                return err
+    return None
+
+
+def applied_vars(st, key):
+    for r in st.get("resources", []):
+        if r.get("module") == f"module.{key}":
+            return ((r.get("instances") or [{}])[0].get("attributes") or {}).get("tk_vars")
     return None
 
 
@@ -518,9 +603,28 @@ def main() -> int:
                     if err:
                         refused.append(err)
                         new.remove(key)
+        if os.environ.get("FAKE_TF_HOSTS") and not failing:
+            for key in sorted(have & set(doc.get("module") or {})):
+                block = (doc.get("module") or {})[key]
+                d = local_dir(str(block.get("source", "")))
+                prior_vars = applied_vars(st, key)
+                if d and host_module(d) and prior_vars is not None:
+                    now = module_vars(block, d)
+                    err = reapply_host(key, prior_vars, now, d)
+                    if err:
+                        refused.append(err)
+                        continue
+                    for r in st["resources"]:
+                        if r.get("module") == f"module.{key}":
+                            r["instances"][0]["attributes"]["tk_vars"] = now  # updated in place
         for key in new:
+            attrs = {"id": str(uuid.uuid4())}
+            block = (doc.get("module") or {})[key]
+            d = local_dir(str(block.get("source", "")))
+            if d and os.path.isdir(d):
+                attrs["tk_vars"] = module_vars(block, d)
             st["resources"].append({"module": f"module.{key}", "mode": "managed", "type": "terraform_data",
-                                    "name": "fake", "instances": [{"attributes": {"id": str(uuid.uuid4())}}]})
+                                    "name": "fake", "instances": [{"attributes": attrs}]})
         done = set(state_modules(st))
         outs = {}
         for name, spec in (doc.get("output") or {}).items():
@@ -550,7 +654,9 @@ def main() -> int:
                 block = (doc.get("module") or {}).get(key) or {}
                 d = local_dir(str(block.get("source", "")))
                 if d and host_module(d):
-                    err = destroy_host(key, block, d)
+                    # self: the resource as last applied (the current configuration's values
+                    # only for a state written before they were recorded)
+                    err = destroy_host(key, applied_vars(st, key) or module_vars(block, d), d)
                     if err:
                         return fail(err)
         st["resources"] = [r for r in st.get("resources", []) if r.get("module", "")[len("module."):] not in gone]

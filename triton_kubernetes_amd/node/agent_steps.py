@@ -369,8 +369,9 @@ class AgentStepsMixin:
             else:
                 out = self._register(plan, ctx)
             if record_here:
+                rke1_image = step.params.get("image", "") if plan.distribution == "rke1" else ""
                 write_join_record(self.path, join_record(plan.rancher_url, plan.token, plan.distribution,
-                                                         plan.hostname))
+                                                         plan.hostname, rke1_image))
             return out
         raise StepFailed(step.name, f"unknown action {a!r}")
 

@@ -66,8 +66,44 @@ CLEAN_DIRS = (
     "/etc/cni", "/opt/cni", "/var/lib/cni", "/var/run/calico", "/run/flannel",
 )
 
-# RKE1: the agent container and every container RKE started (docker ps filters)
-RKE1_FILTERS = ("ancestor=rancher/rancher-agent", "label=io.rancher.rke.container.name")
+# RKE1: what the teardown removes, decided from what ``docker ps -a`` shows.  Not an
+# untagged ``--filter ancestor=rancher/rancher-agent``: Docker reads that as
+# ``rancher/rancher-agent:latest``, which matches no agent running a tagged image (the
+# pinned ``rancher/rancher-agent:v2.10.3``, or one behind a registry), so the agent -- run
+# with ``--restart=unless-stopped`` -- survived and kept the node in its old cluster.
+# * containers carrying either label: RKE's own (kubelet, etcd, kube-proxy, service-sidekick)
+#   and every container the kubelet started for a pod (``k8s_*`` and their ``k8s_POD_*``
+#   sandboxes: flannel, cattle-node-agent, the device plugin);
+# * containers whose image repository -- any registry prefix, any tag or digest -- is the
+#   agent's (``rancher/rancher-agent``, plus the exact image the join record names or
+#   Terraform passes as ``TK_AGENT_IMAGE``) or one of RKE's (its helper containers such as
+#   the port listeners and log linkers carry no label).
+RKE1_LABELS = ("io.rancher.rke.container.name", "io.kubernetes.pod.namespace")
+RKE1_REPOS = ("rancher/rancher-agent", "rancher/rke-tools", "rancher/hyperkube")
+
+
+def image_repository(ref: str) -> str:
+    """``[registry/]path`` of an image reference, without its tag or digest
+    (``reg:5000/rancher/rancher-agent:v2.10.3`` -> ``reg:5000/rancher/rancher-agent``)."""
+    ref = ref.split("@", 1)[0]
+    head, _, last = ref.rpartition("/")
+    last = last.split(":", 1)[0]
+    return f"{head}/{last}" if head else last
+
+
+def rke1_repos(record: Optional[Dict[str, Any]] = None, agent_image: str = "") -> List[str]:
+    """The image repositories whose containers an RKE1 teardown removes."""
+    repos = list(RKE1_REPOS)
+    for img in ((record or {}).get("agent_image", ""), agent_image):
+        if img and image_repository(img) not in repos:
+            repos.append(image_repository(img))
+    return repos
+
+
+def repo_matches(image: str, repos: List[str]) -> bool:
+    """``image`` (as ``docker ps`` shows it) is of one of ``repos``, with any registry prefix."""
+    r = image_repository(image)
+    return any(r == w or r.endswith("/" + w) for w in repos)
 
 
 def cluster_identity(server: str, token: str) -> str:
@@ -76,9 +112,15 @@ def cluster_identity(server: str, token: str) -> str:
     return hashlib.sha256(f"{server.rstrip('/')}\n{token}".encode()).hexdigest()[:24]
 
 
-def join_record(server: str, token: str, distribution: str, hostname: str) -> Dict[str, Any]:
-    return {"cluster": cluster_identity(server, token), "server": server.rstrip("/"),
-            "distribution": distribution, "hostname": hostname}
+def join_record(server: str, token: str, distribution: str, hostname: str,
+                agent_image: str = "") -> Dict[str, Any]:
+    """What a successful join records; ``agent_image``: the RKE1 agent image it ran (the
+    teardown removes that repository's containers whatever its registry and tag)."""
+    rec = {"cluster": cluster_identity(server, token), "server": server.rstrip("/"),
+           "distribution": distribution, "hostname": hostname}
+    if agent_image:
+        rec["agent_image"] = agent_image
+    return rec
 
 
 def refusal(record: Optional[Dict[str, Any]], server: str, token: str) -> Optional[str]:
@@ -113,9 +155,9 @@ def join_guard_shell(server: str, token: str) -> str:
         "fi\n")
 
 
-def join_record_shell(server: str, token: str, distribution: str, hostname: str) -> str:
+def join_record_shell(server: str, token: str, distribution: str, hostname: str, agent_image: str = "") -> str:
     """Shell lines for the end of a successful join step: write the join record."""
-    doc = json.dumps(join_record(server, token, distribution, hostname), sort_keys=True)
+    doc = json.dumps(join_record(server, token, distribution, hostname, agent_image), sort_keys=True)
     return (f"sudo mkdir -p \"${{TK_HOST_ROOT:-}}{os.path.dirname(JOIN_RECORD)}\"\n"
             f"printf '%s\\n' '{doc}' | sudo tee \"${{TK_HOST_ROOT:-}}{JOIN_RECORD}\" >/dev/null\n")
 
@@ -132,12 +174,30 @@ set -uo pipefail
 R=${{TK_HOST_ROOT:-}}
 rc=0
 _tk_mark() {{ echo "::tk-cleanup $1 $2"; }}
+if [ "${{TK_NODE_CLEANUP:-true}}" = false ]; then
+  # the host module's node_cleanup = false (Terraform's destroy-time provisioner): keep the host
+  echo "::tk-cleanup node_cleanup skipped"
+  echo "::tk-cleanup-done 0"
+  exit 0
+fi
 for f in {uninstallers}; do
   [ -x "$R$f" ] || continue
   if sudo "$R$f" >/dev/null 2>&1; then _tk_mark "$f" ok; else _tk_mark "$f" failed; rc=1; fi
 done
 if command -v docker >/dev/null 2>&1; then
-  ids=$(for flt in {" ".join(RKE1_FILTERS)}; do sudo docker ps -aq --filter "$flt" 2>/dev/null; done | sort -u)
+  # RKE1 (node/cleanup.py RKE1_LABELS, RKE1_REPOS): labelled containers, and containers of the
+  # agent's or RKE's image repositories with any registry prefix, tag or digest
+  _tk_repo() {{ local i="${{1%%@*}}" l; l="${{i##*/}}"; case "$l" in *:*) i="${{i%:*}}";; esac; echo "$i"; }}
+  repos="{" ".join(RKE1_REPOS)}"
+  rec_img=$(sed -n 's/.*"agent_image": *"\\([^"]*\\)".*/\\1/p' "$R{JOIN_RECORD}" 2>/dev/null || true)
+  for img in "${{TK_AGENT_IMAGE:-}}" "$rec_img"; do [ -n "$img" ] && repos="$repos $(_tk_repo "$img")"; done
+  ids=$( {{ for lab in {" ".join(RKE1_LABELS)}; do sudo docker ps -aq --filter "label=$lab" 2>/dev/null || true; done
+           sudo docker ps -a --format '{{{{.ID}}}} {{{{.Image}}}}' 2>/dev/null | awk -v repos="$repos" '
+             BEGIN {{ n = split(repos, want, " ") }}
+             {{ img = $2; sub(/@.*/, "", img); k = split(img, p, "/"); if (p[k] ~ /:/) sub(/:[^:\\/]*$/, "", img)
+               for (j = 1; j <= n; j++) {{ w = want[j]
+                 if (img == w || (length(img) > length(w) && substr(img, length(img) - length(w)) == "/" w)) {{ print $1; break }} }} }}' || true
+         }} | sort -u)
   if [ -n "$ids" ]; then
     if sudo docker rm -f $ids >/dev/null 2>&1; then _tk_mark rke1-containers ok; else _tk_mark rke1-containers failed; rc=1; fi
   fi
@@ -165,7 +225,8 @@ def parse_cleanup_markers(output: str) -> Dict[str, Any]:
         elif len(parts) >= 2 and parts[0] == "::tk-cleanup-done":
             done = parts[1] == "0"
     ok = done if done is not None else all(a["status"] != "failed" for a in actions)
-    return {"ok": bool(ok), "actions": actions, "complete": done is not None, "filters": list(RKE1_FILTERS)}
+    return {"ok": bool(ok), "actions": actions, "complete": done is not None,
+            "rke1": {"labels": list(RKE1_LABELS), "repositories": list(RKE1_REPOS)}}
 
 
 # --- the node agent's teardown (fixed argv lists, no shell text) -------------------------------
@@ -198,8 +259,15 @@ def cleanup_host(path: Callable[[str], str], run_argv: Callable[[List[str]], str
             ok = False
     if docker:
         try:
-            ids = sorted({i for flt in RKE1_FILTERS
-                          for i in run_argv([docker, "ps", "-aq", "--filter", flt]).split() if i})
+            found = set()
+            for lab in RKE1_LABELS:
+                found.update(run_argv([docker, "ps", "-aq", "--filter", f"label={lab}"]).split())
+            repos = rke1_repos(read_join_record(path))
+            for line in run_argv([docker, "ps", "-a", "--format", "{{.ID}} {{.Image}}"]).splitlines():
+                parts = line.split()
+                if len(parts) >= 2 and repo_matches(parts[1], repos):
+                    found.add(parts[0])
+            ids = sorted(found)
             if ids:
                 run_argv([docker, "rm", "-f", *ids])
                 actions.append({"what": "rke1-containers", "status": "ok", "count": str(len(ids))})

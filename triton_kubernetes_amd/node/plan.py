@@ -323,7 +323,7 @@ sudo bash -c "$(declare -f tk_rccl_slim tk_rccl_slim_enable); tk_rccl_slim_enabl
     # a host still joined to another cluster is refused before anything is installed, and a
     # successful join is recorded (node/cleanup.py): reused bare metal is cleaned on destroy
     guard = join_guard_shell(rancher_url, token)
-    record = join_record_shell(rancher_url, token, dist, hostname)
+    record = join_record_shell(rancher_url, token, dist, hostname, image if rke1 else "")
     if rke1:
         plan.steps.append(Step("agent", "agent", (
             guard +

@@ -438,10 +438,17 @@ def _node_cleanup(install: str) -> str:
     """The bare-metal host's destroy-time teardown.  Destroy-time provisioners may reference
     only ``self`` (and ``path``): the connection is kept in ``input``, refreshed by every
     apply (``input`` changes update in place; only a new host replaces it, which tears
-    down the old host).  ``on_failure = continue``: a dead host must not pin the state."""
+    down the old host).  ``on_failure = continue``: a dead host must not pin the state.
+
+    The resource always exists: ``node_cleanup`` travels in ``input`` and the script skips
+    the teardown when it is false (``TK_NODE_CLEANUP``).  A ``count = var.node_cleanup ? 1
+    : 0`` would make turning the flag off on a host in service destroy instance [0] -- and
+    so run the very teardown the flag is meant to prevent.  ``agent_image``
+    (``TK_AGENT_IMAGE``): the RKE1 agent image the join ran, whose containers the teardown
+    removes with any registry and tag.  Remote-exec joins ``inline`` into one script: the
+    shebang goes first."""
     return f'''
 resource "terraform_data" "node_cleanup" {{
-  count            = var.node_cleanup ? 1 : 0
   depends_on       = [terraform_data.{install}]
   triggers_replace = [var.host]
   input = {{
@@ -451,6 +458,8 @@ resource "terraform_data" "node_cleanup" {{
     host_key         = var.host_key
     bastion_host     = var.bastion_host
     bastion_host_key = var.bastion_host_key
+    node_cleanup     = var.node_cleanup
+    agent_image      = var.rancher_agent_image
   }}
   provisioner "remote-exec" {{
     when       = destroy
@@ -464,7 +473,11 @@ resource "terraform_data" "node_cleanup" {{
       bastion_host     = self.input.bastion_host == "" ? null : self.input.bastion_host
       bastion_host_key = self.input.bastion_host_key == "" ? null : self.input.bastion_host_key
     }}
-    inline = [file("${{path.module}}/files/cleanup_host.sh")]
+    inline = [
+      "#!/bin/bash",
+      "export TK_NODE_CLEANUP='${{self.input.node_cleanup}}' TK_AGENT_IMAGE='${{self.input.agent_image}}'",
+      file("${{path.module}}/files/cleanup_host.sh"),
+    ]
   }}
 }}
 '''
