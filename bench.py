@@ -500,12 +500,12 @@ def main() -> int:
     if rank == 0:
         from triton_kubernetes_amd.rancher.fake import FakeRancher
 
-        fake = FakeRancher.for_manager("bench", "bench-admin-pw-0123").start()
+        fake = FakeRancher().start()  # a random first-login password, given as rancher_bootstrap_password
         backend = LocalBackend(os.path.join(work, "state"))
         ctx_base = {"backend_provider": "local", "executor": "direct", "non-interactive": True,
                     "cluster_manager": "bench"}
         mgr = dict(ctx_base, manager_cloud_provider="baremetal", name="bench", rancher_admin_password="bench-admin-pw-0123",
-                   host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="~/.ssh/id_rsa")
+                   rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="~/.ssh/id_rsa")
         wf.new_manager(Context(settings=Settings(mgr, env={}), out=devnull), backend)
 
     # node enrollment (install time, before the timed region): the manager's agent PKI

@@ -88,7 +88,7 @@ def config2_3(runs):
     def mgr(i):
         backend = LocalBackend(os.path.join(root, f"m{i}"))
         wf.new_manager(ctx_of(dict(base, manager_cloud_provider="baremetal", name="mgr",
-                                   rancher_admin_password="tk-admin-pw-0123", host="rancher+" + fresh[i + 1].url, ssh_user="u",
+                                   rancher_admin_password="tk-admin-pw-0123", rancher_bootstrap_password=fresh[i + 1].bootstrap_password, host="rancher+" + fresh[i + 1].url, ssh_user="u",
                                    bastion_host="", key_path="k")), backend)
 
     r2 = timed(mgr, runs)
@@ -96,7 +96,7 @@ def config2_3(runs):
         f.stop()
     backend = LocalBackend(os.path.join(root, "c"))
     wf.new_manager(ctx_of(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
-                               host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
+                               rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
 
     def cluster(i):
         nodes = [{"rancher_host_label": "etcd", "node_count": 1, "hostname": f"c{i}-e", "ssh_user": "u",

@@ -60,7 +60,7 @@ def run(workers: int, gpus: int, root: str, parallelism: int = 0) -> dict:
     out = io.StringIO()
     wf.new_manager(Context(settings=Settings(dict(base, manager_cloud_provider="baremetal", name="mgr",
                                                   rancher_admin_password="tk-admin-pw-0123",
-                                                  host="rancher+" + fake.url, ssh_user="u", bastion_host="",
+                                                  rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="u", bastion_host="",
                                                   key_path="k"), env={}), out=out), backend)
     cfg = dict(base, cluster_cloud_provider="baremetal", name=f"fleet-{workers}",
                k8s_version=versions.DEFAULT_K8S_VERSION, k8s_network_provider="flannel", gpu_addons=True, wait=True,

@@ -180,7 +180,7 @@ def test_injector_end_to_end_through_admission(tmp_path):
         backend = LocalBackend(str(tmp_path / "state"))
         base = {"executor": "direct", "agent_token": TOKEN}
         new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr",
-                                  rancher_admin_password="s3cret-passw0rd", host="rancher+" + fake.url,
+                                  rancher_admin_password="s3cret-passw0rd", rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url,
                                   ssh_user="ubuntu", bastion_host="", key_path="k")), backend)
         cp, w = agent("cp"), agent("w", 8)
         nodes = [{"rancher_host_label": "control", "node_count": 1, "hostname": "cp", "ssh_user": "u",

@@ -236,7 +236,7 @@ def test_create_cluster_over_tls_with_per_node_tokens(tmp_path):
     be = LocalBackend(str(tmp_path / "state"))
     with FakeRancher.for_manager("mgr", "tk-admin-pw-0123") as rancher:
         wf.new_manager(make_ctx({"executor": "direct", "manager_cloud_provider": "baremetal", "name": "mgr",
-                                 "rancher_admin_password": "tk-admin-pw-0123", "host": "rancher+" + rancher.url,
+                                 "rancher_admin_password": "tk-admin-pw-0123", "rancher_bootstrap_password": rancher.bootstrap_password, "host": "rancher+" + rancher.url,
                                  "ssh_user": "u", "bastion_host": "", "key_path": "k"}), be)
         assert be.read_blob("mgr", PKI_BLOB)  # created with the manager (inside its apply lock)
         pki = load_pki(be, "mgr")

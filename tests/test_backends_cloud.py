@@ -224,7 +224,7 @@ def test_manta_create_then_destroy_manager_removes_every_object(manta, tmp_path)
     with FakeRancher.for_manager("mgr", pw) as rancher:
         wf.new_manager(make_ctx({"backend_provider": "manta", "executor": "direct",
                                  "manager_cloud_provider": "baremetal", "name": "mgr",
-                                 "rancher_admin_password": pw, "host": "rancher+" + rancher.url,
+                                 "rancher_admin_password": pw, "rancher_bootstrap_password": rancher.bootstrap_password, "host": "rancher+" + rancher.url,
                                  "ssh_user": "u", "bastion_host": "", "key_path": "k"}), be)
     be.write_blob("mgr", "backups.json", b'["b1"]')
     be.write_blob("mgr", "backup-b1.json", b"{}")

@@ -22,7 +22,7 @@ def cluster(tmp_path):
     backend = LocalBackend(str(tmp_path / "state"))
     base = {"executor": "direct"}
     new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
-                              host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
+                              rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
     new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="prod",
                               k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico")), backend)
     tf = json.loads(backend.read_tfstate("mgr"))

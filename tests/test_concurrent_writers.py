@@ -65,7 +65,7 @@ def manager():
     fake = FakeRancher.for_manager("mgr", "s3cret-passw0rd").start()
     backend = _Interleaved()
     new_manager(make_ctx({"executor": "direct", "manager_cloud_provider": "baremetal", "name": "mgr",
-                          "rancher_admin_password": "s3cret-passw0rd", "host": "rancher+" + fake.url,
+                          "rancher_admin_password": "s3cret-passw0rd", "rancher_bootstrap_password": fake.bootstrap_password, "host": "rancher+" + fake.url,
                           "ssh_user": "ubuntu", "bastion_host": "", "key_path": "k"}), backend)
     yield fake, backend
     fake.stop()

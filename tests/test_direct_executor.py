@@ -47,7 +47,7 @@ def env(tmp_path):
 
 def _manager(fake, backend, base):
     new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="s3cret-passw0rd",
-                              host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
+                              rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
                 backend)
 
 

@@ -32,7 +32,7 @@ def test_real_gpu_bringup(tmp_path):
     base = {"executor": "direct", "agent_token": token}
     try:
         new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
-                                  host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
+                                  rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
         # the default distribution: an RKE2 custom cluster (nodes register as rancher-system-agent)
         ctx = make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="gpu",
                             k8s_version="v1.31", k8s_network_provider="canal", gpu_addons=True,

@@ -260,7 +260,7 @@ def _create(tmp_path, policy):
     backend = LocalBackend(str(tmp_path / "state"))
     base = {"executor": "direct", "agent_token": token}
     new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="s3cret-passw0rd",
-                              host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")), backend)
+                              rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")), backend)
     cp = agent("cp")
     healthy, sick = agent("w0", synthetic_topology(8)), agent("w1", _sick_topology())
     nodes = [{"rancher_host_label": "control", "node_count": 1, "hostname": "cp", "ssh_user": "u", "bastion_host": "",

@@ -59,7 +59,7 @@ def _cluster(tmp_path, fake):
     backend = LocalBackend(str(tmp_path / "state"))
     base = {"executor": "direct"}
     new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password=PW,
-                              host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")), backend)
+                              rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")), backend)
     nodes = [{"rancher_host_label": "etcd", "node_count": 1, "hostname": "e", "ssh_user": "core",
               "bastion_host": "", "key_path": "k", "hosts": ["10.1.0.1"]},
              {"rancher_host_label": "worker", "node_count": 1, "hostname": "w", "ssh_user": "core",

@@ -295,7 +295,7 @@ def test_fake_installer_refuses_a_host_of_another_cluster(tmp_path):
 
 def _mgr(fake, backend, base):
     wf.new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password=PW,
-                                 host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
+                                 rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
                    backend)
 
 

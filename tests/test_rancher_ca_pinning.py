@@ -68,7 +68,7 @@ def test_direct_executor_pins_the_ca_and_refuses_a_switched_certificate(tls_env)
     fake, ca_file, agent, backend = tls_env
     base = {"executor": "direct", "agent_token": TOKEN}
     wf.new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password=PW,
-                                 host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k",
+                                 rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k",
                                  rancher_ca_file=ca_file)), backend)
     pinned = trust.load(backend, "mgr")
     assert pinned is not None and pinned.pem == trust.normalize(fake.ca_pem) and pinned.source.startswith("file:")
@@ -105,7 +105,7 @@ def test_adopted_https_server_without_a_ca_uses_the_system_store(tls_env):
     fake, _, _, backend = tls_env
     with pytest.raises(TKError, match=r"against the system trust store.*rancher_ca_file"):
         wf.new_manager(make_ctx({"executor": "direct", "manager_cloud_provider": "baremetal", "name": "mgr",
-                                 "rancher_admin_password": PW, "host": "rancher+" + fake.url, "ssh_user": "ubuntu",
+                                 "rancher_admin_password": PW, "rancher_bootstrap_password": fake.bootstrap_password, "host": "rancher+" + fake.url, "ssh_user": "ubuntu",
                                  "bastion_host": "", "key_path": "k"}), backend)
 
 

@@ -49,7 +49,7 @@ def env(tmp_path):
     backend = LocalBackend(str(tmp_path / "state"))
     base = {"executor": "direct", "agent_token": TOKEN}
     new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr",
-                              rancher_admin_password="s3cret-passw0rd", host="rancher+" + fake.url, ssh_user="ubuntu",
+                              rancher_admin_password="s3cret-passw0rd", rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu",
                               bastion_host="", key_path="k")), backend)
     yield fake, agent, backend, base
     for a in agents:

@@ -75,7 +75,7 @@ def test_cluster_over_ssh_runs_rendered_plans(tmp_path, fake_ssh):
         backend = LocalBackend(str(tmp_path / "state"))
         base = {"executor": "direct"}
         new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
-                                  host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
+                                  rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
                     backend)
         nodes = [{"rancher_host_label": "etcd", "node_count": 1, "hostname": "e", "ssh_user": "core",
                   "bastion_host": "", "key_path": "~/.ssh/id", "hosts": ["10.1.0.1"]},
@@ -109,7 +109,7 @@ def test_unreachable_host_fails_only_its_module(tmp_path, fake_ssh):
         backend = LocalBackend(str(tmp_path / "state"))
         base = {"executor": "direct"}
         new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
-                                  host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
+                                  rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="ubuntu", bastion_host="", key_path="k")),
                     backend)
         nodes = [{"rancher_host_label": "worker", "node_count": 2, "hostname": "w", "ssh_user": "core",
                   "bastion_host": "", "key_path": "k", "hosts": ["10.2.0.1", "fail-10.2.0.2"]}]

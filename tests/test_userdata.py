@@ -36,7 +36,7 @@ def test_userdata_node_from_applied_cluster(tmp_path):
         backend = LocalBackend(str(tmp_path / "state"))
         base = {"executor": "direct"}
         new_manager(make_ctx(dict(base, manager_cloud_provider="baremetal", name="mgr", rancher_admin_password="tk-admin-pw-0123",
-                                  host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
+                                  rancher_bootstrap_password=fake.bootstrap_password, host="rancher+" + fake.url, ssh_user="u", bastion_host="", key_path="k")), backend)
         new_cluster(make_ctx(dict(base, cluster_manager="mgr", cluster_cloud_provider="baremetal", name="pxe",
                                   k8s_version="v1.28.10-rancher1-1", k8s_network_provider="calico")), backend)
         # the node is only recorded (its delivery will be cloud-init): persist without applying the host

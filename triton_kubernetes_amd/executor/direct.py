@@ -39,6 +39,7 @@ from typing import Any, Callable, Dict, List, Optional, Set, Tuple
 
 from .. import __version__
 from ..backend.base import Backend
+from ..cloud.http import HTTPError
 from ..errors import ExecutorError
 from ..node.plan import TOOLS_DIR, build_host_plan
 from ..parallel.transport import HostRef, Transport, TransportRouter
@@ -455,10 +456,13 @@ class DirectExecutor(Executor):
         from ..rancher.trust import RancherTrust, normalize
 
         if host.startswith("rancher+"):
-            # an adopted server: its bootstrap password is given, or one an earlier version
-            # of this framework started it with (a login attempt only)
-            initial = cfg.get("rancher_bootstrap_password") or bootstrap_secret.legacy_password(
-                str(cfg.get("name", "")), password)
+            # an adopted server: its first-login password as given (rancher_bootstrap_password,
+            # kept in the state backend), or none -- a server already bootstrapped, which takes
+            # the admin password.  The legacy derivation of the admin password is tried only
+            # when the operator opted in (rancher_legacy_bootstrap): never sent otherwise
+            store = self._trust_store
+            initial = cfg.get("rancher_bootstrap_password") or (bootstrap_secret.load(*store) if store else "")
+            legacy = bool(store) and bootstrap_secret.legacy_allowed(*store)
             url = host[len("rancher+"):]
             if self.trust is None:
                 if url.startswith("https://"):
@@ -469,7 +473,22 @@ class DirectExecutor(Executor):
                     self._pin(RancherTrust(normalize(self.rancher_factory(url).http.request(
                         "GET", "/cacerts").body.decode()), f"server:{url}"))
             client = self.rancher_factory(url)
-            return client.bootstrap(password, url, initial, timeout=self.cluster_wait)
+            if initial:
+                return client.bootstrap(password, url, initial, timeout=self.cluster_wait)
+            try:  # no bootstrap password: the server must already take the admin password
+                return client.bootstrap(password, url, password, timeout=self.cluster_wait)
+            except HTTPError as exc:
+                if exc.status != 401:
+                    raise
+                if not legacy:
+                    raise ExecutorError(
+                        f"the adopted Rancher server {url} does not accept the admin password and no "
+                        f"rancher_bootstrap_password was given: set rancher_bootstrap_password (the server's "
+                        f"CATTLE_BOOTSTRAP_PASSWORD), or rancher_legacy_bootstrap: true for a server an "
+                        f"earlier version of triton-kubernetes started") from None
+            return client.bootstrap(password, url, bootstrap_secret.legacy_password(str(cfg.get("name", "")),
+                                                                                    password),
+                                    timeout=self.cluster_wait)
         # a server this framework starts: a random first-login password kept in the state
         # backend (rancher/bootstrap_secret.py), never derived from the admin password
         initial = cfg.get("rancher_bootstrap_password") or (

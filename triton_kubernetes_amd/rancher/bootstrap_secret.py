@@ -17,9 +17,13 @@ the container's life, and an offline brute-force oracle for the admin password. 
 * the Terraform manager modules take it as ``rancher_bootstrap_password``, rendered by the
   executor from the same blob (a sensitive root variable).
 
-An adopted server (``host: rancher+https://...``) was started by someone else: its
-``rancher_bootstrap_password`` is given, or it is one an earlier version of this framework
-started (:func:`legacy_password`, tried as a login only).
+An adopted server (``host: rancher+https://...``) was started by someone else.  Its
+first-login password is given as ``rancher_bootstrap_password`` (kept in this same blob,
+never in ``main.tf.json``), or the server is already bootstrapped and takes the admin
+password.  Nothing derived from the admin password goes to it unless the operator says the
+server is one an earlier version of this framework started (``rancher_legacy_bootstrap:
+true``, :func:`legacy_password`): that derivation is an offline brute-force oracle for the
+admin password, and an adopted server is not ours to hand it to.
 """
 
 import json
@@ -52,6 +56,25 @@ def ensure(backend: Any, manager: str) -> str:
     return pw
 
 
+def save_adopted(backend: Any, manager: str, password: str = "", legacy: bool = False) -> None:
+    """An adopted server's first-login password (``rancher_bootstrap_password``; may be
+    empty: an already-bootstrapped server) and whether the legacy derivation may be tried."""
+    try:
+        backend.write_blob(manager, BLOB, json.dumps({"password": password, "adopted": True,
+                                                      "legacy": bool(legacy)}).encode())
+    except NotImplementedError:
+        pass
+
+
+def legacy_allowed(backend: Any, manager: str) -> bool:
+    """The operator opted in to :func:`legacy_password` for this adopted server."""
+    try:
+        raw = backend.read_blob(manager, BLOB)
+    except NotImplementedError:
+        return False
+    return bool(raw) and bool(json.loads(raw).get("legacy"))
+
+
 def legacy_password(manager_name: str, admin_password: str) -> str:
     """What servers started by round <= 4 of this framework (and the test fake's
     ``for_manager``) hold: a login attempt against an adopted server, never sent to a host."""
@@ -60,4 +83,4 @@ def legacy_password(manager_name: str, admin_password: str) -> str:
     return bootstrap_password(manager_name, admin_password)
 
 
-__all__ = ["BLOB", "ensure", "legacy_password", "load"]
+__all__ = ["BLOB", "ensure", "legacy_allowed", "legacy_password", "load", "save_adopted"]

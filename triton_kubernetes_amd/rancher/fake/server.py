@@ -102,6 +102,9 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
                            list(k8s_versions) if k8s_versions is not None else [v for _, v in K8S_VERSIONS],
                            list(rke2_versions) if rke2_versions is not None else [v for _, v in RKE2_VERSIONS])
         self.state.device_plugin_seconds = device_plugin_seconds
+        self.bootstrap_password = pw
+        # every request body the server received (the tests check what was sent to it)
+        self.request_bodies: List[bytes] = []
         # "<service>.<namespace>" -> "https://127.0.0.1:<port>" (where an in-cluster
         # webhook service of a test really listens)
         self.service_endpoints: Dict[str, str] = {}
@@ -294,6 +297,7 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
             def _body(self) -> Any:
                 n = int(self.headers.get("Content-Length") or 0)
                 raw = self.rfile.read(n) if n else b""
+                fake.request_bodies.append(raw)
                 try:
                     return json.loads(raw) if raw else {}
                 except ValueError:

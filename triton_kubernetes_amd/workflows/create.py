@@ -120,6 +120,17 @@ def new_manager(ctx: Context, backend: Backend) -> None:
     if not ctx.confirm("Proceed with the manager creation", "Proceed"):
         ctx.echo("Manager creation canceled.")
         return
+    mgr = state.module("cluster-manager") or {}
+    if str(mgr.get("host", "")).startswith("rancher+"):
+        # an adopted Rancher server: its first-login password, if given, and the opt-in for
+        # the legacy derived one go to the state backend (rancher/bootstrap_secret.py), never
+        # into main.tf.json
+        from ..rancher import bootstrap_secret
+
+        given = ctx.get_string("rancher_bootstrap_password") if ctx.is_set("rancher_bootstrap_password") else ""
+        legacy = ctx.settings.get_bool("rancher_legacy_bootstrap") if ctx.is_set("rancher_legacy_bootstrap") \
+            else False
+        bootstrap_secret.save_adopted(backend, name, given, legacy)
     path, obj = backend.state_terraform_config(name)
     state.set_terraform_backend_config(path, obj)
     apply_and_persist(ctx, backend, state, ["cluster-manager"])
