@@ -197,3 +197,21 @@ def test_multi_node_gate_retries_every_member_with_released_spans(oom_node):
     finally:
         a.stop()
         b.stop()
+
+
+def test_an_implausible_footprint_never_becomes_the_headroom(oom_node, monkeypatch):
+    """A "footprint" of a burn-in span's size (what a device-wide free-memory delta read
+    while the burn-in child allocated, before the per-process accounting) is not kept: it
+    would have left the next full burn-in almost nothing to test."""
+    tmp_path, exe, free = oom_node
+    monkeypatch.setenv("TK_RCCL_STUB_FOOTPRINT_MIB", str(290 * 1024))
+    free.write_text(str(300 << 30))
+    agent = _agent()
+    url = agent.serve()
+    try:
+        res = ClusterGate(AgentTransport(token=TOKEN), members_from([url], [8]), SIZES, timeout_s=30).run()
+        assert res["ok"], res
+        assert not os.path.exists(agent.path(agent.FOOTPRINT_FILE))
+        assert agent.span_headroom(8) == (4 << 30) + 7 * (512 << 20)
+    finally:
+        agent.stop()

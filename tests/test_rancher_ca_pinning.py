@@ -109,32 +109,92 @@ def test_adopted_https_server_without_a_ca_uses_the_system_store(tls_env):
                                  "bastion_host": "", "key_path": "k"}), backend)
 
 
-def test_ssh_managed_manager_is_pinned_from_its_host():
-    """A manager installed over SSH (here: one created before pinning existed) is pinned from
-    the file its install saved on the host, read over the pinned SSH session."""
+class _ManagerHost(RecordingTransport):
+    """The manager host as SSH reaches it: the script really runs, with ``HOME`` the host's
+    home and a ``curl`` that answers ``https://127.0.0.1/cacerts`` with ``served`` (None: no
+    server listening)."""
+
+    def __init__(self, tmp_path, served):
+        super().__init__()
+        self.home = tmp_path / "home"
+        self.home.mkdir(exist_ok=True)
+        bindir = tmp_path / "hostbin"
+        bindir.mkdir(exist_ok=True)
+        (tmp_path / "served").write_text(served if served is not None else "")
+        fail = "exit 7" if served is None else f'cat {tmp_path / "served"}'
+        (bindir / "curl").write_text(f'#!/bin/sh\necho "$*" >> {tmp_path / "curl.log"}\n{fail}\n')
+        (bindir / "curl").chmod(0o755)
+        self.env = dict(os.environ, HOME=str(self.home), PATH=f"{bindir}:{os.environ['PATH']}")
+        self.curl_log = tmp_path / "curl.log"
+
+    def run_script(self, host, script, timeout=3600):
+        super().run_script(host, script, timeout)
+        proc = subprocess.run(["bash", "-s"], input=script, env=self.env, capture_output=True, text=True)
+        if proc.returncode:
+            from triton_kubernetes_amd.errors import ExecutorError
+
+            raise ExecutorError(f"{host.address}: exit {proc.returncode}: {proc.stderr.strip()}")
+        return proc.stdout
+
+
+def _applied_manager(host):
     from triton_kubernetes_amd.state import State
-
-    pem = "-----BEGIN CERTIFICATE-----\nMIIHOSTREADCA\n-----END CERTIFICATE-----"
-
-    class Host(RecordingTransport):
-        def run_script(self, host, script, timeout=3600):
-            super().run_script(host, script, timeout)
-            return pem + "\n" if "rancher_cacerts.pem" in script else ""
 
     be = MemoryBackend()
     st = State("mgr")
     st.set_manager({"source": catalog.module_source(catalog.PACKAGE_ROOT, "terraform/modules/bare-metal-rancher", "x"),
                     "name": "mgr", "host": "10.0.0.10", "ssh_user": "ubuntu", "key_path": "k",
                     "rancher_admin_password": PW})
-    host = Host()
     ex = DirectExecutor(transport=host)
     tf = ex._load_tfstate(be, "mgr")
     tf["module_state"]["cluster-manager"] = {"hash": "x", "status": "ok"}
     ex._save_tfstate(be, "mgr", tf)
+    return ex, st, be
+
+
+HOST_PEM = "-----BEGIN CERTIFICATE-----\nMIIHOSTREADCA\n-----END CERTIFICATE-----"
+
+
+def test_ssh_managed_manager_is_pinned_from_its_host(tmp_path):
+    """A manager installed over SSH (here: one created before pinning existed) is pinned from
+    the file its install saved on the host, read over the pinned SSH session."""
+    host = _ManagerHost(tmp_path, served="-----BEGIN CERTIFICATE-----\nOTHER\n-----END CERTIFICATE-----\n")
+    (host.home / "rancher_cacerts.pem").write_text(HOST_PEM + "\n")
+    ex, st, be = _applied_manager(host)
     ex._load_trust(st, be)
     got = trust.load(be, "mgr")
-    assert got.pem == pem + "\n" and got.source == "ssh:10.0.0.10"
-    assert host.scripts == ["cat ~/rancher_cacerts.pem\n"]
+    assert got.pem == HOST_PEM + "\n" and got.source == "ssh:10.0.0.10"
+    assert host.scripts == [trust.HOST_CA_READ] and not host.curl_log.exists()  # the saved file, no fetch
+
+
+def test_manager_from_before_the_saved_ca_is_read_from_its_loopback(tmp_path):
+    """a manager whose install never saved ~/rancher_cacerts.pem (an older
+    version) made every later apply fail on ``cat``.  Now the bundle is read on the host from
+    the server's own loopback, saved, and pinned."""
+    host = _ManagerHost(tmp_path, served=HOST_PEM + "\n")
+    ex, st, be = _applied_manager(host)
+    ex._load_trust(st, be)
+    assert trust.load(be, "mgr").pem == HOST_PEM + "\n"
+    assert "https://127.0.0.1/cacerts" in host.curl_log.read_text()
+    assert (host.home / "rancher_cacerts.pem").read_text() == HOST_PEM + "\n"
+
+
+def test_manager_with_a_public_certificate_pins_the_system_store(tmp_path):
+    host = _ManagerHost(tmp_path, served="")  # cacerts setting empty: a publicly trusted certificate
+    ex, st, be = _applied_manager(host)
+    ex._load_trust(st, be)
+    got = trust.load(be, "mgr")
+    assert got.pem == "" and (host.home / "rancher_cacerts.pem").exists()
+
+
+def test_unreadable_manager_ca_fails_instead_of_pinning_nothing(tmp_path):
+    from triton_kubernetes_amd.errors import ExecutorError
+
+    host = _ManagerHost(tmp_path, served=None)  # no file, no server
+    ex, st, be = _applied_manager(host)
+    with pytest.raises(ExecutorError, match="rancher_ca_file"):
+        ex._load_trust(st, be)
+    assert trust.load(be, "mgr") is None and not (host.home / "rancher_cacerts.pem").exists()
 
 
 def _ensure_cluster(q):
@@ -192,9 +252,12 @@ ALLOWED_UNVERIFIED = {
     "triton_kubernetes_amd/node/agent_steps.py": {"verify_tls=False": 2},
     # the same join rendered for SSH / Terraform hosts (checksum-checked)
     "triton_kubernetes_amd/node/plan.py": {"curl -fsSLk": 1},
-    "triton_kubernetes_amd/terraform/scripts.py": {"curl -fsSLk": 1, "curl -ksf": 7, "curl -ks ": 1},
+    # (curl -ks: the admin-password change and its check, on the manager host's loopback)
+    "triton_kubernetes_amd/terraform/scripts.py": {"curl -fsSLk": 1, "curl -ksf": 7, "curl -ks ": 2},
     # on the manager host itself, against its own loopback https://127.0.0.1
     "triton_kubernetes_amd/node/manager.py": {"curl -ksf": 8},
+    # ... and the CA read of a manager installed before its bundle was saved there
+    "triton_kubernetes_amd/rancher/trust.py": {"curl -ksf": 1},
     # the HTTP client's switch itself
     "triton_kubernetes_amd/cloud/http.py": {"ssl.CERT_NONE": 1},
 }
@@ -223,7 +286,10 @@ def test_no_unverified_tls_outside_the_allowed_places():
         for pat, n in pats.items():
             assert n <= ALLOWED_UNVERIFIED[f].get(pat, 0), (f, pat, n)
     # the loopback ones really are loopback
-    for f in ("triton_kubernetes_amd/node/manager.py",):
+    for line in open(os.path.join(ROOT, "triton_kubernetes_amd/terraform/scripts.py")).read().splitlines():
+        if "curl -ks " in line:
+            assert "https://127.0.0.1/" in line, line
+    for f in ("triton_kubernetes_amd/node/manager.py", "triton_kubernetes_amd/rancher/trust.py"):
         for line in open(os.path.join(ROOT, f)).read().splitlines():
             if "curl -ksf" in line:  # R=https://127.0.0.1; ``post`` is used with "$R/..."
                 assert "127.0.0.1" in line or "$R/" in line or line.strip().startswith("post = "), line
@@ -242,3 +308,71 @@ def test_rerun_after_the_password_change_still_logs_in():
                                                            timeout=10)
         assert first["rancher_access_key"] and again["rancher_access_key"]
         assert bootstrap_secret.ensure(be, "mgr") == boot
+
+
+def test_pinned_private_ca_verifies_the_chain_not_the_hostname(tmp_path):
+    """Rancher's docker-install certificate need not name the address the
+    CLI connects to.  With the server's own CA pinned, the chain is what is verified (CLI
+    client, ensure_cluster.sh, apply_addons.sh); a certificate from another CA is still
+    refused.  The system store ('public') keeps hostname checks."""
+    boot = "b00tstrap-only"
+    with FakeRancher(bootstrap_password=boot, tls=True, tls_names=["rancher.example.internal"]) as fake:
+        pinned = trust.RancherTrust(trust.normalize(fake.ca_pem), "t")
+        assert pinned.context().check_hostname is False
+        assert trust.RancherTrust("", "public").context().check_hostname is True
+        outs = RancherClient(fake.url, trust=pinned).bootstrap(PW, fake.url, boot, timeout=10)
+        q = {"name": "dev", "version": versions.DEFAULT_K8S_VERSION, "network": "canal", "distribution": "rke2",
+             "api_url": fake.url, "access_key": outs["rancher_access_key"], "secret_key": outs["rancher_secret_key"],
+             "ca_pem": pinned.pem, "operation": "apply"}
+        ok = _ensure_cluster(q)
+        assert ok.returncode == 0, ok.stderr
+        cid = json.loads(ok.stdout)["cluster_id"]
+        with fake.state.mu:
+            fake.state.clusters[cid]["state"] = "active"
+        mdir = tmp_path / "manifests"
+        mdir.mkdir()
+        (mdir / "00-ns.json").write_text(json.dumps({"path": "/api/v1/namespaces", "object": {
+            "apiVersion": "v1", "kind": "Namespace", "metadata": {"name": "tk-addons-test"}}}))
+        script = os.path.join(catalog.MODULES_DIR, "rancher-k8s-mi355x-addons", "files", "apply_addons.sh")
+        env = dict(os.environ, RANCHER_URL=fake.url, RANCHER_ACCESS_KEY=outs["rancher_access_key"],
+                   RANCHER_SECRET_KEY=outs["rancher_secret_key"], RANCHER_CA=pinned.pem, CLUSTER_ID=cid,
+                   MANIFEST_DIR=str(mdir))
+        applied = subprocess.run(["bash", script], env=env, capture_output=True, text=True, timeout=60)
+        assert applied.returncode == 0, applied.stderr
+        again = subprocess.run(["bash", script], env=env, capture_output=True, text=True, timeout=60)
+        assert again.returncode == 0, again.stderr  # 409 -> PUT
+        fake.rotate_certificate()  # another CA: refused everywhere
+        refused = subprocess.run(["bash", script], env=env, capture_output=True, text=True, timeout=60)
+        assert refused.returncode != 0 and "does not verify against the CA pinned" in refused.stderr
+        assert _ensure_cluster(q).returncode != 0
+        with pytest.raises(TKError):
+            RancherClient(fake.url, trust=pinned).login("admin", PW)
+
+
+@pytest.mark.parametrize("login_code,ok", [("201", True), ("401", False)])
+def test_read_api_key_checks_the_admin_password_after_a_refused_change(tmp_path, login_code, ok):
+    """HTTP 422 on the password change was taken as "already changed" -- a
+    wrong bootstrap password went unreported.  Now the admin password must then log in."""
+    home = tmp_path / "home"
+    home.mkdir()
+    (home / "rancher_api_key").write_text(json.dumps({"name": "token-tk", "token": "token-tk:s3cret"}))
+    (home / "rancher_cacerts.pem").write_text("")
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    (bindir / "ssh").write_text(f'#!/bin/bash\nfor a; do cmd=$a; done\nexport HOME={home}\nexec bash -c "$cmd"\n')
+    (bindir / "curl").write_text(f'#!/bin/bash\ncat >/dev/null\necho "$*" >> {tmp_path / "curl.log"}\n'
+                                 f'case "$*" in *changepassword*) printf 422;; *action=login*) printf {login_code};; '
+                                 f'esac\n')
+    for f in ("ssh", "curl"):
+        (bindir / f).chmod(0o755)
+    script = os.path.join(catalog.MODULES_DIR, "bare-metal-rancher", "files", "read_api_key.sh")
+    q = {"host": "10.0.0.10", "ssh_user": "u", "key_path": "k", "bastion_host": "", "operation": "apply",
+         "admin_password": PW, "bootstrap_password": "wrong-b00tstrap"}
+    res = subprocess.run(["bash", script], input=json.dumps(q), capture_output=True, text=True, timeout=60,
+                         env=dict(os.environ, PATH=f"{bindir}:{os.environ['PATH']}"))
+    assert "action=login" in (tmp_path / "curl.log").read_text()
+    if ok:  # set by an earlier run: the admin password logs in
+        assert res.returncode == 0, res.stderr
+        assert json.loads(res.stdout)["access_key"] == "token-tk"
+    else:
+        assert res.returncode != 0 and "is rancher_bootstrap_password the server's?" in res.stderr

@@ -282,13 +282,18 @@ class DirectExecutor(Executor):
 
     def _read_host_ca(self, cfg: Dict[str, Any]) -> Any:
         """The CA bundle the manager host's install saved from ``https://127.0.0.1/cacerts``,
-        read over the host-key-pinned SSH session."""
-        from ..rancher.trust import HOST_CA_FILE, RancherTrust, normalize
+        read over the host-key-pinned SSH session -- fetched there from the loopback first
+        when an older install never saved it (``trust.HOST_CA_READ``)."""
+        from ..rancher.trust import HOST_CA_FILE, HOST_CA_READ, RancherTrust, normalize
 
         host = str(cfg.get("host", ""))
         ref = HostRef(host, cfg.get("ssh_user") or "ubuntu", cfg.get("key_path") or "~/.ssh/id_rsa",
                       cfg.get("bastion_host") or "")
-        pem = self.transport.run_script(ref, f"cat {HOST_CA_FILE}\n", timeout=120)
+        try:
+            pem = self.transport.run_script(ref, HOST_CA_READ, timeout=120)
+        except ExecutorError as exc:
+            raise ExecutorError(f"{host}: cannot read the Rancher CA on the manager host ({exc}); give "
+                                f"rancher_ca_file to pin it") from None
         if pem.strip() and "BEGIN CERTIFICATE" not in pem:
             raise ExecutorError(f"{host}: {HOST_CA_FILE} holds no PEM certificate")
         return RancherTrust(normalize(pem), f"ssh:{host}")

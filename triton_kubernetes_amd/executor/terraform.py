@@ -357,11 +357,19 @@ class TerraformExecutor(Executor):
                 self.host_keys.add(str(out["value"]))
         self.host_keys.save()
         ca = outs.get(f"{MANAGER_KEY}__{RANCHER_CA_OUTPUT}")
-        if backend is not None and self.trust is None and isinstance(ca, dict) and ca.get("value") is not None:
+        key = outs.get(f"{MANAGER_KEY}__rancher_access_key")
+        # pinned only from a read that worked: read_api_key.sh yields empty keys (and an empty
+        # bundle) for a manager it could not reach outside an apply, and a bundle is either a
+        # PEM or empty because the server's cacerts setting is (a public certificate)
+        read_ok = isinstance(key, dict) and bool(key.get("value"))
+        value = ca.get("value") if isinstance(ca, dict) else None
+        if value and "BEGIN CERTIFICATE" not in str(value):
+            value = None
+        if backend is not None and self.trust is None and read_ok and value is not None:
             from ..rancher import trust as rtrust
 
             mgr = state.module(MANAGER_KEY) or {}
-            self.trust = rtrust.RancherTrust(rtrust.normalize(str(ca["value"])), f"ssh:{mgr.get('host', '')}")
+            self.trust = rtrust.RancherTrust(rtrust.normalize(str(value)), f"ssh:{mgr.get('host', '')}")
             rtrust.save(backend, state.name, self.trust)
 
     def destroy_flags(self) -> List[str]:

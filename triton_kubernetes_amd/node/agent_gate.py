@@ -120,6 +120,9 @@ class AgentGateMixin:
 
     FOOTPRINT_FILE = "/etc/triton-kubernetes/gate-footprint.json"
     HEADROOM_MARGIN = 1.25  # measured footprint x this, plus the floor's first GiB
+    # a larger "footprint" is not a communicator's: 8 ranks of RCCL on MI355X take ~1 GiB per
+    # GPU (profiles/round6/gate_footprint.jsonl: 0.8 GiB for one, device code included)
+    FOOTPRINT_MAX_MIB = 32 * 1024
 
     def _release_event(self):
         ev = self.__dict__.get("_release_now")
@@ -170,8 +173,8 @@ class AgentGateMixin:
         GPUs measured (``footprint_total_mib``: the communicator and its sweep buffers), and
         size the burn-in span's headroom from it (never below the constant floor)."""
         mib = float(phase_ms.get("footprint_total_mib") or 0.0)
-        if mib <= 0:
-            return
+        if mib <= 0 or mib > self.FOOTPRINT_MAX_MIB:
+            return  # not measured here (-1), or not a communicator's (a bound, never a headroom)
         import json
 
         from ..ops import probe

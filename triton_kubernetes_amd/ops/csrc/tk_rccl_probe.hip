@@ -28,6 +28,7 @@
 #include "tk_rccl_verify.h"
 
 #include <dlfcn.h>
+#include <unistd.h>
 
 #include <climits>
 #include <string>
@@ -324,12 +325,12 @@ struct Gate {
   std::thread init_thread;
   size_t prealloc_bytes = 0;     // sweep buffers allocated by the init thread after the comms
   std::vector<RankBufs> bufs;    // (filled when prealloc_bytes > 0 and the init succeeded)
-  // device memory the init took, max over this gate's GPUs (hipMemGetInfo before and after):
-  // the communicators (RCCL's per-channel, per-peer buffers, its device code) and then the
-  // preallocated sweep buffers.  Device-wide: another process allocating meanwhile counts too
-  size_t footprint_comm = 0, footprint_total = 0;
+  // device memory the init took, max over this gate's GPUs (this process's VRAM before and
+  // after, proc_vram): the communicators (RCCL's per-channel, per-peer buffers, its device
+  // code) and then the preallocated sweep buffers
+  long long footprint_comm = 0, footprint_total = 0;  // -1: not measurable here
 };
-// the footprint of the gate the calling thread last swept (tkr_last_footprint)
+// the footprint of the gate the calling thread last swept (tkr_last_footprint; -1: unknown)
 static thread_local double g_last_footprint[2] = {0, 0};
 extern "C" double tkr_last_footprint(int which) { return which >= 0 && which < 2 ? g_last_footprint[which] : 0.0; }
 
@@ -337,6 +338,60 @@ static size_t device_free(int dev) {
   size_t free_b = 0, total_b = 0;
   if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) return 0;
   return free_b;
+}
+
+// VRAM this process holds on HIP device `dev` (bytes), from the amdgpu KFD's per-process
+// accounting (/sys/class/kfd/kfd/proc/<pid>/vram_<gpu_id>); -1 when it cannot be read.  The
+// gate's footprint is measured with it, not with hipMemGetInfo: the device's free memory
+// also moves with the burn-in child allocating its ~280 GB span at the same moment (a
+// device-wide delta read 290 GB on MI355X, profiles/round6/README.md).
+static long long proc_vram(int dev) {
+  static std::mutex mu;
+  static std::vector<long long> gpu_id;  // HIP device -> KFD gpu_id (0: not found yet, -1: none)
+  unsigned long long gid = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    if ((int)gpu_id.size() <= dev) gpu_id.resize((size_t)dev + 1, 0);
+    if (gpu_id[dev] == 0) {
+      gpu_id[dev] = -1;
+      char bus[64] = {0};
+      unsigned dom = 0, b = 0, d = 0, f = 0;
+      if (hipDeviceGetPCIBusId(bus, sizeof(bus), dev) == hipSuccess &&
+          sscanf(bus, "%x:%x:%x.%x", &dom, &b, &d, &f) == 4) {
+        const unsigned long long loc = ((unsigned long long)b << 8) | (d << 3) | f;
+        for (int n = 0; n < 1024; ++n) {
+          char path[128];
+          snprintf(path, sizeof(path), "/sys/class/kfd/kfd/topology/nodes/%d/properties", n);
+          FILE* fp = fopen(path, "r");
+          if (!fp) break;
+          char key[64];
+          unsigned long long v = 0, nloc = ~0ull, ndom = ~0ull;
+          while (fscanf(fp, "%63s %llu", key, &v) == 2) {
+            if (!strcmp(key, "location_id")) nloc = v;
+            else if (!strcmp(key, "domain")) ndom = v;
+          }
+          fclose(fp);
+          if (nloc != loc || ndom != dom) continue;
+          snprintf(path, sizeof(path), "/sys/class/kfd/kfd/topology/nodes/%d/gpu_id", n);
+          if ((fp = fopen(path, "r")) != nullptr) {
+            if (fscanf(fp, "%llu", &v) == 1 && v) gpu_id[dev] = (long long)v;
+            fclose(fp);
+          }
+          break;
+        }
+      }
+    }
+    if (gpu_id[dev] <= 0) return -1;
+    gid = (unsigned long long)gpu_id[dev];
+  }
+  char path[128];
+  snprintf(path, sizeof(path), "/sys/class/kfd/kfd/proc/%d/vram_%llu", (int)getpid(), gid);
+  FILE* fp = fopen(path, "r");
+  if (!fp) return -1;
+  unsigned long long v = 0;
+  const int got = fscanf(fp, "%llu", &v);
+  fclose(fp);
+  return got == 1 ? (long long)v : -1;
 }
 static std::mutex g_gate_mu;
 static std::vector<std::pair<int, Gate*>> g_gates;
@@ -495,16 +550,17 @@ static void annotate_init_error(Gate* g) {
 static void init_body(Gate* g, ncclUniqueId id) {
   HipNcclApi api{id};
   const size_t nd = g->devices.size();
-  std::vector<size_t> before(nd);
-  for (size_t d = 0; d < nd; ++d) before[d] = device_free(g->devices[d]);
+  std::vector<long long> before(nd);
+  for (size_t d = 0; d < nd; ++d) before[d] = proc_vram(g->devices[d]);
   const int r = tk_group_init(api, g->world, g->rank_base, (int)g->devices.size(), g->devices.data(),
                               g->comms.data(), g->err, sizeof(g->err));
   if (r != 0) annotate_init_error(g);
-  auto taken = [&]() {
-    size_t most = 0;
+  auto taken = [&]() -> long long {  // this process's growth on its most-grown GPU; -1 unknown
+    long long most = 0;
     for (size_t d = 0; d < nd; ++d) {
-      const size_t now = device_free(g->devices[d]);
-      if (before[d] > now && before[d] - now > most) most = before[d] - now;
+      const long long now = proc_vram(g->devices[d]);
+      if (before[d] < 0 || now < 0) return -1;
+      if (now - before[d] > most) most = now - before[d];
     }
     return most;
   };

@@ -190,8 +190,10 @@ class GateComm:
             # communicators, then with their preallocated sweep buffers (tk_rccl_probe.hip)
             lib.tkr_last_footprint.restype = ctypes.c_double
             lib.tkr_last_footprint.argtypes = [ctypes.c_int]
-            phases["footprint_mib"] = round(lib.tkr_last_footprint(0) / 2 ** 20, 1)
-            phases["footprint_total_mib"] = round(lib.tkr_last_footprint(1) / 2 ** 20, 1)
+            # (-1: this process's VRAM could not be read -- no KFD accounting -- so not measured)
+            for i, k in enumerate(("footprint_mib", "footprint_total_mib")):
+                b = float(lib.tkr_last_footprint(i))
+                phases[k] = round(b / 2 ** 20, 1) if b >= 0 else -1.0
         return SweepResult(self.world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
                            float(ph[4]), phases)
 

@@ -93,7 +93,8 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
                  bootstrap_password: Optional[str] = None, host: str = "127.0.0.1", port: int = 0,
                  k8s_versions: Optional[Sequence[str]] = None, async_registration_tokens: bool = True,
                  default_pod_security: str = "privileged", rke2_versions: Optional[Sequence[str]] = None,
-                 device_plugin_seconds: float = 0.0, tls: bool = False):
+                 device_plugin_seconds: float = 0.0, tls: bool = False,
+                 tls_names: Optional[Sequence[str]] = None):
         if default_pod_security not in PSA_LEVELS:
             raise ValueError(f"default_pod_security must be one of {', '.join(PSA_LEVELS)}")
         # a server started without CATTLE_BOOTSTRAP_PASSWORD has a random one nobody knows
@@ -116,6 +117,9 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
         # /cacerts and the cacerts setting serve (what a Rancher install with its generated
         # CA does); rotate_certificate() switches to another CA (an impostor, or a rotation)
         self._tls_ctx = None
+        # the names the serving certificate carries (default: the loopback address this fake
+        # listens on); others model a certificate that does not name the address connected to
+        self.tls_names = list(tls_names) if tls_names else ["127.0.0.1", "localhost"]
         if tls:
             self._tls_ctx = self._new_certificate()
         self._server = HTTPServer((host, port), self._handler())
@@ -129,7 +133,7 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
         from ...k8s.tls import issue, make_ca
 
         ca = make_ca(f"fake-rancher-ca-{secrets.token_hex(3)}")
-        cert = issue(ca, "127.0.0.1", ["127.0.0.1", "localhost"])
+        cert = issue(ca, self.tls_names[0], self.tls_names)
         if ctx is None:
             from ...node.security import server_context
 

@@ -40,6 +40,24 @@ BLOB = "rancher-ca.json"
 # where a manager install leaves the server's CA bundle as read on the host (loopback)
 HOST_CA_FILE = "~/rancher_cacerts.pem"
 
+# Run on the manager host over the pinned SSH session: the saved bundle; a manager installed
+# before the bundle was saved there (an older version of this framework) has none, so it is
+# read now from the server's own loopback -- what the install does -- and saved.  An empty
+# output means the server's cacerts setting is empty (a publicly trusted certificate); a
+# server that cannot be read fails (exit 3), never an empty bundle.
+HOST_CA_READ = """f=~/rancher_cacerts.pem
+if [ ! -e "$f" ]; then
+  umask 077
+  if ! curl -ksf https://127.0.0.1/cacerts > "$f.tmp"; then
+    rm -f "$f.tmp"
+    echo "no $f on this host and https://127.0.0.1/cacerts cannot be read: is the Rancher server running? (or give rancher_ca_file)" >&2
+    exit 3
+  fi
+  mv "$f.tmp" "$f"
+fi
+cat "$f"
+"""
+
 
 @dataclass
 class RancherTrust:
@@ -54,9 +72,18 @@ class RancherTrust:
 
     def context(self) -> ssl.SSLContext:
         """Verify the server against the pinned bundle only (the system store when the
-        certificate is publicly trusted); hostnames are checked."""
+        certificate is publicly trusted).
+
+        With a private CA pinned the chain is verified but the hostname is not: the CA is
+        this one server's own (Rancher's generated CA, read over the host-key-pinned SSH
+        session), so a chain to it already authenticates the server, and the certificate
+        Rancher's docker install serves need not name the address the CLI connects to (its
+        dynamic listener adds names only as requests arrive; the first bootstrap call
+        precedes server-url).  The system store ('public') keeps hostname checks."""
         if self.pem.strip():
-            return ssl.create_default_context(cadata=self.pem)
+            ctx = ssl.create_default_context(cadata=self.pem)
+            ctx.check_hostname = False  # verify_mode stays CERT_REQUIRED
+            return ctx
         from ..cloud.http import _system_context
 
         return _system_context()  # built once per process: parsing the system store costs ~70 ms

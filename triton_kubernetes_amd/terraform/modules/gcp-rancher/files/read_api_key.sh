@@ -39,7 +39,27 @@ if ! tok=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_api_key' 2>"$err");
   if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": "", "ca_certs": ""}'; exit 0; fi
   refused "read the Rancher API key"
 fi
-ca=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_cacerts.pem' 2>"$err") || ca=""
+# the bundle as saved on the host, or -- an older install that never saved it -- read there
+# now from the server's own loopback (rancher/trust.py HOST_CA_READ).  Empty only when the
+# server's cacerts setting is (a publicly trusted certificate); a failed read fails here
+# rather than pinning an empty bundle
+if ! ca=$(ssh "${opts[@]}" "$ssh_user@$host" 'bash -s' 2>"$err" <<'TK_CA_EOF'
+f=~/rancher_cacerts.pem
+if [ ! -e "$f" ]; then
+  umask 077
+  if ! curl -ksf https://127.0.0.1/cacerts > "$f.tmp"; then
+    rm -f "$f.tmp"
+    echo "no $f on this host and https://127.0.0.1/cacerts cannot be read: is the Rancher server running? (or give rancher_ca_file)" >&2
+    exit 3
+  fi
+  mv "$f.tmp" "$f"
+fi
+cat "$f"
+TK_CA_EOF
+); then
+  if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": "", "ca_certs": ""}'; exit 0; fi
+  refused "read the Rancher CA bundle"
+fi
 if [ "${operation:-apply}" = apply ] && [ -n "${admin_password:-}" ] && [ "${admin_password:-}" != "${bootstrap_password:-}" ]; then
   # curl config on stdin: user (the API token), the JSON body with both passwords
   cfg=$(printf '%s' "$tok" | TKQ_admin="$admin_password" TKQ_boot="$bootstrap_password" python3 -c '
@@ -54,8 +74,22 @@ print("data = " + q(body))')
 ' "$cfg" | ssh "${opts[@]}" "$ssh_user@$host" \
     'curl -ks -K - -o /dev/null -w "%{http_code}" -X POST "https://127.0.0.1/v3/users?action=changepassword"' 2>"$err") \
     || refused "set the Rancher admin password"
-  # 422: the current password is no longer the bootstrap one -- set by an earlier run
-  case "$code" in 2??|422|"") ;; *) echo "setting the Rancher admin password on $host: HTTP $code" >&2; exit 1 ;; esac
+  # 422: the current password is no longer the bootstrap one -- set by an earlier run, or the
+  # bootstrap password is wrong: the admin password must then log in, or this is an error
+  case "$code" in
+    2??|"") ;;
+    422)
+      login_cfg=$(TKQ_admin="$admin_password" python3 -c '
+import json, os
+print("header = " + json.dumps("Content-Type: application/json"))
+print("data = " + json.dumps(json.dumps({"username": "admin", "password": os.environ["TKQ_admin"], "ttl": 60000,
+                                          "description": "triton-kubernetes admin password check"})))')
+      lc=$(printf '%s\n' "$login_cfg" | ssh "${opts[@]}" "$ssh_user@$host" \
+        'curl -ks -K - -o /dev/null -w "%{http_code}" -X POST "https://127.0.0.1/v3-public/localProviders/local?action=login"' \
+        2>"$err") || refused "check the Rancher admin password"
+      case "$lc" in 2??) ;; *) echo "setting the Rancher admin password on $host: the server refused the bootstrap password and the admin password does not log in (HTTP $lc): is rancher_bootstrap_password the server's?" >&2; exit 1 ;; esac ;;
+    *) echo "setting the Rancher admin password on $host: HTTP $code" >&2; exit 1 ;;
+  esac
 fi
 printf '%s' "$tok" | KH="$(pinned_for)" CA="$ca" python3 -c '
 import json, os, sys

@@ -11,6 +11,7 @@ from ..node.hosttune import shell_check as _host_tuning_check
 from ..parallel.hostkeys import GO_HOSTKEY_ALGORITHMS
 from ..node.metrics import textfile_script as _metrics_textfile
 from ..node.tools import NODE_TOOLS_FN, PREBUILT_DIR
+from ..rancher.trust import HOST_CA_READ as _HOST_CA_READ
 
 # download, verify (when docker_install_sha256 is set), run — no `curl | sh` of an unchecked stream
 DOCKER_INSTALL = r"""if ! command -v docker >/dev/null 2>&1; then
@@ -136,7 +137,16 @@ eval "$(python3 -c 'import json,shlex,sys; q=json.load(sys.stdin); print(" ".joi
   if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": "", "ca_certs": ""}'; exit 0; fi
   refused "read the Rancher API key"
 fi
-ca=$(ssh "${opts[@]}" "$ssh_user@$host" 'cat ~/rancher_cacerts.pem' 2>"$err") || ca=""
+# the bundle as saved on the host, or -- an older install that never saved it -- read there
+# now from the server's own loopback (rancher/trust.py HOST_CA_READ).  Empty only when the
+# server's cacerts setting is (a publicly trusted certificate); a failed read fails here
+# rather than pinning an empty bundle
+if ! ca=$(ssh "${opts[@]}" "$ssh_user@$host" 'bash -s' 2>"$err" <<'TK_CA_EOF'
+@@HOST_CA_READ@@TK_CA_EOF
+); then
+  if [ "${operation:-apply}" != apply ]; then echo '{"access_key": "", "secret_key": "", "known_hosts": "", "ca_certs": ""}'; exit 0; fi
+  refused "read the Rancher CA bundle"
+fi
 if [ "${operation:-apply}" = apply ] && [ -n "${admin_password:-}" ] && [ "${admin_password:-}" != "${bootstrap_password:-}" ]; then
   # curl config on stdin: user (the API token), the JSON body with both passwords
   cfg=$(printf '%s' "$tok" | TKQ_admin="$admin_password" TKQ_boot="$bootstrap_password" python3 -c '
@@ -151,8 +161,22 @@ print("data = " + q(body))')
 ' "$cfg" | ssh "${opts[@]}" "$ssh_user@$host" \
     'curl -ks -K - -o /dev/null -w "%{http_code}" -X POST "https://127.0.0.1/v3/users?action=changepassword"' 2>"$err") \
     || refused "set the Rancher admin password"
-  # 422: the current password is no longer the bootstrap one -- set by an earlier run
-  case "$code" in 2??|422|"") ;; *) echo "setting the Rancher admin password on $host: HTTP $code" >&2; exit 1 ;; esac
+  # 422: the current password is no longer the bootstrap one -- set by an earlier run, or the
+  # bootstrap password is wrong: the admin password must then log in, or this is an error
+  case "$code" in
+    2??|"") ;;
+    422)
+      login_cfg=$(TKQ_admin="$admin_password" python3 -c '
+import json, os
+print("header = " + json.dumps("Content-Type: application/json"))
+print("data = " + json.dumps(json.dumps({"username": "admin", "password": os.environ["TKQ_admin"], "ttl": 60000,
+                                          "description": "triton-kubernetes admin password check"})))')
+      lc=$(printf '%s\n' "$login_cfg" | ssh "${opts[@]}" "$ssh_user@$host" \
+        'curl -ks -K - -o /dev/null -w "%{http_code}" -X POST "https://127.0.0.1/v3-public/localProviders/local?action=login"' \
+        2>"$err") || refused "check the Rancher admin password"
+      case "$lc" in 2??) ;; *) echo "setting the Rancher admin password on $host: the server refused the bootstrap password and the admin password does not log in (HTTP $lc): is rancher_bootstrap_password the server's?" >&2; exit 1 ;; esac ;;
+    *) echo "setting the Rancher admin password on $host: HTTP $code" >&2; exit 1 ;;
+  esac
 fi
 printf '%s' "$tok" | KH="$(pinned_for)" CA="$ca" python3 -c '
 import json, os, sys
@@ -161,6 +185,8 @@ ca = os.environ["CA"].strip()
 print(json.dumps({"access_key": t["name"], "secret_key": t["token"].split(":", 1)[1], "known_hosts": os.environ["KH"],
                   "ca_certs": ca + "\n" if ca else ""}))'
 """
+
+READ_API_KEY = READ_API_KEY.replace("@@HOST_CA_READ@@", _HOST_CA_READ)
 
 RANCHER_CLUSTER = r"""#!/bin/bash
 # S4 as a Terraform data "external" program (operator machine): find the cluster by
@@ -182,6 +208,8 @@ q = json.load(sys.stdin)
 pinned = q.get("ca_pem", "").strip()
 pinned = pinned + "\n" if pinned else ""
 ctx = ssl.create_default_context(cadata=pinned) if pinned else ssl.create_default_context()
+if pinned:
+    ctx.check_hostname = False  # the chain to this server s own CA; rancher/trust.py RancherTrust.context
 auth = "Basic " + base64.b64encode((q["access_key"] + ":" + q["secret_key"]).encode()).decode()
 
 
@@ -587,29 +615,58 @@ print(json.dumps({"labels": json.dumps(labels, sort_keys=True), "known_hosts": o
 
 APPLY_ADDONS = r"""#!/bin/bash
 # MI355X cluster add-ons: wait for the cluster, then create the manifests in
-# $MANIFEST_DIR through Rancher's Kubernetes proxy (PUT on 409).
+# $MANIFEST_DIR through Rancher's Kubernetes proxy (PUT on 409).  TLS is verified against
+# the manager's pinned CA (RANCHER_CA; empty: the system trust store).  With a private CA the
+# chain is checked, not the hostname (rancher/trust.py RancherTrust.context): curl has no
+# such mode, so the calls are Python's.
 set -euo pipefail
-# TLS verified against the manager's pinned CA (RANCHER_CA; empty: the system trust store)
-tls=()
-if [ -n "${RANCHER_CA:-}" ]; then
-  cafile=$(mktemp); trap 'rm -f "$cafile"' EXIT
-  printf '%s\n' "$RANCHER_CA" > "$cafile"
-  tls=(--cacert "$cafile")
-fi
-api() { curl -sf "${tls[@]}" -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" -H 'Content-Type: application/json' "$@"; }
-for i in $(seq 1 3600); do
-  state=$(api "$RANCHER_URL/v3/clusters/$CLUSTER_ID" | python3 -c 'import json,sys; print(json.load(sys.stdin).get("state",""))' || true)
-  [ "$state" = active ] && break
-  sleep 1
-done
-[ "$state" = active ] || { echo "cluster $CLUSTER_ID not active" >&2; exit 1; }
-for f in "$MANIFEST_DIR"/*.json; do
-  path=$(python3 -c 'import json,sys; print(json.load(open(sys.argv[1]))["path"])' "$f")
-  obj=$(python3 -c 'import json,sys; print(json.dumps(json.load(open(sys.argv[1]))["object"]))' "$f")
-  name=$(python3 -c 'import json,sys; print(json.load(open(sys.argv[1]))["object"]["metadata"]["name"])' "$f")
-  code=$(curl -s "${tls[@]}" -o /dev/null -w '%{http_code}' -u "$RANCHER_ACCESS_KEY:$RANCHER_SECRET_KEY" \
-         -H 'Content-Type: application/json' -X POST -d "$obj" "$RANCHER_URL/k8s/clusters/$CLUSTER_ID$path")
-  if [ "$code" = 409 ]; then api -X PUT -d "$obj" "$RANCHER_URL/k8s/clusters/$CLUSTER_ID$path/$name" >/dev/null
-  elif [ "$code" -ge 300 ]; then echo "applying $f: HTTP $code" >&2; exit 1; fi
-done
+exec python3 -c '
+import base64, glob, json, os, ssl, sys, time, urllib.error, urllib.request
+
+ca = os.environ.get("RANCHER_CA", "").strip()
+if ca:
+    ctx = ssl.create_default_context(cadata=ca + "\n")
+    ctx.check_hostname = False  # the chain to this manager s own CA
+else:
+    ctx = ssl.create_default_context()
+url, cid = os.environ["RANCHER_URL"].rstrip("/"), os.environ["CLUSTER_ID"]
+auth = "Basic " + base64.b64encode((os.environ["RANCHER_ACCESS_KEY"] + ":" +
+                                    os.environ["RANCHER_SECRET_KEY"]).encode()).decode()
+
+
+def call(method, path, body=None):
+    req = urllib.request.Request(url + path, method=method, data=None if body is None else json.dumps(body).encode(),
+                                 headers={"Authorization": auth, "Content-Type": "application/json",
+                                          "Accept": "application/json"})
+    try:
+        with urllib.request.urlopen(req, context=ctx, timeout=60) as resp:
+            return resp.status, resp.read()
+    except urllib.error.HTTPError as exc:
+        return exc.code, exc.read()
+
+
+state = ""
+for _ in range(3600):
+    try:
+        code, raw = call("GET", "/v3/clusters/" + cid)
+        state = json.loads(raw).get("state", "") if code == 200 else ""
+    except (OSError, ValueError) as exc:
+        if isinstance(getattr(exc, "reason", None), ssl.SSLError) or isinstance(exc, ssl.SSLError):
+            sys.exit("the Rancher server certificate does not verify against the CA pinned for this cluster "
+                     "manager: " + str(exc))
+        state = ""
+    if state == "active":
+        break
+    time.sleep(1)
+if state != "active":
+    sys.exit("cluster " + cid + " not active")
+for f in sorted(glob.glob(os.path.join(os.environ["MANIFEST_DIR"], "*.json"))):
+    doc = json.load(open(f))
+    path, obj = doc["path"], doc["object"]
+    code, raw = call("POST", "/k8s/clusters/" + cid + path, obj)
+    if code == 409:
+        code, raw = call("PUT", "/k8s/clusters/" + cid + path + "/" + obj["metadata"]["name"], obj)
+    if code >= 300:
+        sys.exit("applying " + f + ": HTTP " + str(code))
+'
 """
