@@ -116,10 +116,13 @@ def test_whole_node_gate_retries_once_after_releasing_held_spans(oom_node):
         ops = [c["op"] for c in _calls(tmp_path) if c["op"].startswith("begin")]
         assert ops == ["begin-oom", "begin"]  # one failed init, one retry
         # the footprint the retried init measured is kept, and sizes the span's headroom
+        # ... and the out-of-memory init doubles the headroom the next burn-in leaves
+        floor = (4 << 30) + 7 * (512 << 20)
         fp = json.loads(open(agent.path(agent.FOOTPRINT_FILE)).read())
-        assert fp == {"8": float(FOOTPRINT_MIB)}
-        want = int(FOOTPRINT_MIB * agent.HEADROOM_MARGIN * (1 << 20)) + (1 << 30)
-        assert agent.span_headroom(8) == want > (4 << 30) + 7 * (512 << 20)
+        assert fp == {"8": float(FOOTPRINT_MIB), "oom:8": 2.0 * floor / (1 << 20)}
+        measured = int(FOOTPRINT_MIB * agent.HEADROOM_MARGIN * (1 << 20)) + (1 << 30)
+        want = max(measured, 2 * floor)
+        assert agent.span_headroom(8) == want > floor
         assert probe.SPAN_HEADROOM == want
         assert rank["phase_ms"]["footprint_total_mib"] == FOOTPRINT_MIB
     finally:
@@ -213,5 +216,30 @@ def test_an_implausible_footprint_never_becomes_the_headroom(oom_node, monkeypat
         assert res["ok"], res
         assert not os.path.exists(agent.path(agent.FOOTPRINT_FILE))
         assert agent.span_headroom(8) == (4 << 30) + 7 * (512 << 20)
+    finally:
+        agent.stop()
+
+
+def test_a_device_wide_footprint_is_kept_only_from_a_quiet_window(oom_node, monkeypatch):
+    """Without per-process accounting (an agent inside a PID namespace: the KFD keys its
+    entries by host pids) the footprint is the device's used-memory delta, which a burn-in
+    child allocating its span meanwhile inflates.  It is kept only when none of the agent's
+    burn-ins started, ran or was alive across the init."""
+    tmp_path, exe, free = oom_node
+    monkeypatch.setenv("TK_RCCL_STUB_FOOTPRINT_KIND", "2")
+    monkeypatch.setenv("TK_RCCL_STUB_FOOTPRINT_MIB", "900")
+    agent = _agent()
+    url = agent.serve()
+    try:
+        _hold_span(agent, exe)  # a child alive (holding its span) across the gate
+        free.write_text(str(RELEASED))
+        res = ClusterGate(AgentTransport(token=TOKEN), members_from([url], [8]), SIZES, timeout_s=30).run()
+        assert res["ok"] and res["ranks"][0]["phase_ms"]["footprint_kind"] == 2.0
+        assert not os.path.exists(agent.path(agent.FOOTPRINT_FILE))
+        agent._links_pending = False
+        probe.wait_frees()  # the child released and exited: a quiet window now
+        res = ClusterGate(AgentTransport(token=TOKEN), members_from([url], [8]), SIZES, timeout_s=30).run()
+        assert res["ok"]
+        assert json.loads(open(agent.path(agent.FOOTPRINT_FILE)).read()) == {"8": 900.0}
     finally:
         agent.stop()

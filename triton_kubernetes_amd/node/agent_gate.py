@@ -147,6 +147,16 @@ class AgentGateMixin:
             ev.clear()
         return round((time.perf_counter() - t0) * 1e3, 1)
 
+    def _new_gate(self, uid: bytes, world: int, rank_base: int, devices: List[int], **kw: Any) -> Any:
+        """A gate communicator (its init starts now), with the agent's burn-in activity at
+        its start (``window``: a device-wide footprint is kept only for a quiet window)."""
+        from ..ops import probe, rccl
+
+        window = probe.activity()
+        gate = rccl.GateComm(uid, world, rank_base, devices, **kw)
+        gate.window = window
+        return gate
+
     def _sweep_oom_retry(self, first, remake, sweep):
         """``sweep(first())``; when that fails because the communicator's init ran out of
         device memory (``ops/rccl.is_oom_error``), release the held spans and run
@@ -159,6 +169,7 @@ class AgentGateMixin:
             if not rccl.is_oom_error(str(exc)):
                 raise
             first_error = str(exc)
+        self._note_gate_oom(len(self.devices))
         with span("node.rccl_gate_retry", node=self.name, why="oom"):
             released_ms = self._release_held_spans()
             try:
@@ -168,20 +179,39 @@ class AgentGateMixin:
                 raise rccl.RCCLError(f"{exc} {RETRIED_MARK}") from exc
         return res, {"gate_retry": "oom", "first_error": first_error[:400], "spans_released_ms": released_ms}
 
-    def _note_gate_footprint(self, ndev: int, phase_ms: Dict[str, float]) -> None:
+    def _note_gate_footprint(self, ndev: int, phase_ms: Dict[str, float], window: Any = None) -> None:
         """Keep the largest per-GPU footprint a gate communicator over ``ndev`` of this node's
         GPUs measured (``footprint_total_mib``: the communicator and its sweep buffers), and
-        size the burn-in span's headroom from it (never below the constant floor)."""
+        size the burn-in span's headroom from it (never below the constant floor).
+
+        A device-wide measurement (``footprint_kind`` 2: no per-process accounting here)
+        counts everything allocated on the GPU meanwhile; it is kept only when none of this
+        agent's burn-ins started, ran or was alive from the init's start (``window``) to now."""
+        from ..ops import probe
+
         mib = float(phase_ms.get("footprint_total_mib") or 0.0)
         if mib <= 0 or mib > self.FOOTPRINT_MAX_MIB:
             return  # not measured here (-1), or not a communicator's (a bound, never a headroom)
+        if int(phase_ms.get("footprint_kind") or 0) != 1:
+            if window is None or window[1] != 0 or probe.activity() != window:
+                return
+        self._keep_footprint(str(int(ndev)), mib)
+
+    def _note_gate_oom(self, ndev: int) -> None:
+        """An init ran out of HBM beside held spans: the next burn-in of this node leaves
+        twice the headroom it left (at most :attr:`FOOTPRINT_MAX_MIB`), whatever is measured."""
+        from ..ops import probe
+
+        held = max(probe.SPAN_HEADROOM, self.span_headroom(ndev))  # what the spans left free
+        self._keep_footprint(f"oom:{int(ndev)}", min(self.FOOTPRINT_MAX_MIB, 2.0 * held / (1 << 20)))
+
+    def _keep_footprint(self, key: str, mib: float) -> None:
         import json
 
         from ..ops import probe
 
         with self._gate_mu:
             fp = self.__dict__.setdefault("_gate_footprints", self._load_gate_footprints())
-            key = str(int(ndev))
             if mib <= float(fp.get(key, 0.0)):
                 return
             fp[key] = round(mib, 1)
@@ -204,14 +234,16 @@ class AgentGateMixin:
 
     def span_headroom(self, ndev: int) -> int:
         """HBM a full burn-in span leaves free on each GPU of this node: the constant floor
-        (4 GiB + 512 MiB per further GPU), or the largest gate footprint this node has
-        measured for ``ndev`` GPUs (x :attr:`HEADROOM_MARGIN`, plus 1 GiB), whichever is more."""
+        (4 GiB + 512 MiB per further GPU), the largest gate footprint this node has measured
+        for ``ndev`` GPUs (x :attr:`HEADROOM_MARGIN`, plus 1 GiB), or twice the headroom an
+        init ran out of memory beside, whichever is most."""
         floor = (4 << 30) + (512 << 20) * max(0, ndev - 1)
         fp = self.__dict__.get("_gate_footprints")
         if fp is None:
             fp = self.__dict__.setdefault("_gate_footprints", self._load_gate_footprints())
         mib = float(fp.get(str(int(ndev)), 0.0))
-        return max(floor, int(mib * self.HEADROOM_MARGIN * (1 << 20)) + (1 << 30))
+        bumped = int(float(fp.get(f"oom:{int(ndev)}", 0.0)) * (1 << 20))  # after an out-of-memory init
+        return max(floor, int(mib * self.HEADROOM_MARGIN * (1 << 20)) + (1 << 30), bumped)
 
     def _gate_devices(self, ndev: int) -> List[int]:
         devs = self.devices or [0]
@@ -283,7 +315,7 @@ class AgentGateMixin:
                 from ..ops import rccl
 
                 self._used_rccl = True
-                gate = rccl.GateComm(uid, world, rank_base, devs, blocking=False, prealloc_bytes=max_bytes)
+                gate = self._new_gate(uid, world, rank_base, devs, blocking=False, prealloc_bytes=max_bytes)
         with self._gate_mu:
             aborted = self._is_aborted(uid)  # an abort that landed during the init's start
             old = self._gates.pop(uid, None)
@@ -384,7 +416,7 @@ class AgentGateMixin:
                         from ..ops import rccl
 
                         self._used_rccl = True
-                        gate = rccl.GateComm(uid, world, rank, self._gate_devices(ndev), blocking=False)
+                        gate = self._new_gate(uid, world, rank, self._gate_devices(ndev), blocking=False)
                     with self._gate_mu:
                         slot = self._sweeping.get(key)
                         canceled = isinstance(slot, _Reserved) and slot.canceled
@@ -404,7 +436,7 @@ class AgentGateMixin:
                     nonlocal gate
                     from ..ops import rccl
 
-                    fresh = rccl.GateComm(self._make_uid(), world, 0, list(first_gate.devices), blocking=False)
+                    fresh = self._new_gate(self._make_uid(), world, 0, list(first_gate.devices), blocking=False)
                     with self._gate_mu:
                         canceled = self._is_aborted(key)  # an abort during the spans' release
                         if not canceled:
@@ -425,7 +457,7 @@ class AgentGateMixin:
             finally:
                 with self._gate_mu:
                     self._sweeping.pop(key, None)
-        self._note_gate_footprint(len(gate.devices), res.phase_ms)
+        self._note_gate_footprint(len(gate.devices), res.phase_ms, getattr(gate, "window", None))
         out = res.to_json()
         out["pipelined"] = pipelined
         out["ranks"] = list(range(rank, rank + len(gate.devices)))

@@ -330,16 +330,19 @@ class AgentStepsMixin:
                 uid, gate, meta = taken
                 sizes = sorted(set(sizes) | set(meta.get("sizes") or []))
 
+            used = [gate] if taken is not None else []
+
             def fresh():
-                return rccl.GateComm(self._make_uid(), len(self.devices), 0, self.devices, blocking=True,
-                                     prealloc_bytes=max(sizes))
+                used.append(self._new_gate(self._make_uid(), len(self.devices), 0, self.devices, blocking=True,
+                                           prealloc_bytes=max(sizes)))
+                return used[-1]
 
             # an init that ran out of HBM beside the held burn-in spans: release them, retry
             # once (node/agent_gate.py:_sweep_oom_retry)
             res, retry = self._sweep_oom_retry(
                 (lambda: gate) if taken is not None else fresh, fresh,
                 lambda g: g.sweep(sizes, iters=10, warmup=2, async_teardown=True))
-            self._note_gate_footprint(len(self.devices), res.phase_ms)
+            self._note_gate_footprint(len(self.devices), res.phase_ms, getattr(used[-1], "window", None))
             if taken is not None:
                 with self._gate_mu:
                     self._gate_results[uid] = (res, time.time(), retry)

@@ -329,10 +329,11 @@ struct Gate {
   // after, proc_vram): the communicators (RCCL's per-channel, per-peer buffers, its device
   // code) and then the preallocated sweep buffers
   long long footprint_comm = 0, footprint_total = 0;  // -1: not measurable here
+  int footprint_kind = 0;                             // 1: this process's VRAM, 2: the device's
 };
 // the footprint of the gate the calling thread last swept (tkr_last_footprint; -1: unknown)
-static thread_local double g_last_footprint[2] = {0, 0};
-extern "C" double tkr_last_footprint(int which) { return which >= 0 && which < 2 ? g_last_footprint[which] : 0.0; }
+static thread_local double g_last_footprint[3] = {0, 0, 0};  // comm, with the sweep buffers, kind
+extern "C" double tkr_last_footprint(int which) { return which >= 0 && which < 3 ? g_last_footprint[which] : 0.0; }
 
 static size_t device_free(int dev) {
   size_t free_b = 0, total_b = 0;
@@ -550,15 +551,29 @@ static void annotate_init_error(Gate* g) {
 static void init_body(Gate* g, ncclUniqueId id) {
   HipNcclApi api{id};
   const size_t nd = g->devices.size();
+  // this process's VRAM when the KFD accounting is reachable (not from inside a PID
+  // namespace: its per-process entries are keyed by the host's pids), else the device's
+  // used memory -- which counts whatever else allocates meanwhile: the agent keeps such a
+  // number only for a window in which none of its burn-ins ran (node/agent_gate.py)
+  auto used = [](int dev, bool per_process) -> long long {
+    if (per_process) return proc_vram(dev);
+    size_t free_b = 0, total_b = 0;
+    if (hipSetDevice(dev) != hipSuccess || hipMemGetInfo(&free_b, &total_b) != hipSuccess) return -1;
+    return (long long)(total_b - free_b);
+  };
+  bool per_process = true;
   std::vector<long long> before(nd);
-  for (size_t d = 0; d < nd; ++d) before[d] = proc_vram(g->devices[d]);
+  for (size_t d = 0; d < nd && per_process; ++d) per_process = (before[d] = proc_vram(g->devices[d])) >= 0;
+  if (!per_process)
+    for (size_t d = 0; d < nd; ++d) before[d] = used(g->devices[d], false);
+  g->footprint_kind = per_process ? 1 : 2;
   const int r = tk_group_init(api, g->world, g->rank_base, (int)g->devices.size(), g->devices.data(),
                               g->comms.data(), g->err, sizeof(g->err));
   if (r != 0) annotate_init_error(g);
-  auto taken = [&]() -> long long {  // this process's growth on its most-grown GPU; -1 unknown
+  auto taken = [&]() -> long long {  // growth on the most-grown GPU; -1 unknown
     long long most = 0;
     for (size_t d = 0; d < nd; ++d) {
-      const long long now = proc_vram(g->devices[d]);
+      const long long now = used(g->devices[d], per_process);
       if (before[d] < 0 || now < 0) return -1;
       if (now - before[d] > most) most = now - before[d];
     }
@@ -756,6 +771,7 @@ extern "C" int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int iters,
   }
   g_last_footprint[0] = (double)g->footprint_comm;
   g_last_footprint[1] = (double)g->footprint_total;
+  g_last_footprint[2] = (double)g->footprint_kind;
   if (g->init_thread.joinable()) g->init_thread.join();
   size_t max_bytes = 0;
   for (int s = 0; s < nsizes; ++s) max_bytes = sizes[s] > max_bytes ? sizes[s] : max_bytes;

@@ -53,7 +53,7 @@ struct StubGate {
   std::atomic<bool> cancel{false};
   std::string init_err;  // the init failed (the HBM model below): poll and sweep report it
 };
-thread_local double g_last_footprint[2] = {0, 0};
+thread_local double g_last_footprint[3] = {0, 0, 0};
 
 // An HBM model for the gate's allocations, for tests of the agent's out-of-memory retry
 // (node/agent_gate.py): TK_RCCL_STUB_HBM_FREE names a file holding the bytes each GPU has
@@ -208,7 +208,7 @@ int tkr_gate_pending() {
   std::lock_guard<std::mutex> lk(g_mu);
   return (int)g_gates.size();
 }
-double tkr_last_footprint(int which) { return which >= 0 && which < 2 ? g_last_footprint[which] : 0.0; }
+double tkr_last_footprint(int which) { return which >= 0 && which < 3 ? g_last_footprint[which] : 0.0; }
 
 int tkr_gate_begin_ex(const unsigned char* uid128, int world, int rank_base, int ndev, const int* devices,
                       int blocking, size_t /*prealloc_bytes*/) {
@@ -385,6 +385,9 @@ int tkr_gate_sweep(int h, const size_t* sizes, int nsizes, int /*iters*/, int /*
     phase_ms[1] = 0.0;
     phase_ms[2] = ms_since(t) - phase_ms[0];
     g_last_footprint[0] = g_last_footprint[1] = (double)stub_footprint();
+    // 1: as if this process's own accounting; TK_RCCL_STUB_FOOTPRINT_KIND=2: a device-wide number
+    const char* kind = getenv("TK_RCCL_STUB_FOOTPRINT_KIND");
+    g_last_footprint[2] = kind && *kind ? atof(kind) : 1.0;
     phase_ms[3] = 0.0;
     // the last rank to leave removes the rendezvous
     for (int d = 0; d < g->ndev; ++d) touch_excl(g->dir + "/done-" + std::to_string(g->rank_base + d));

@@ -231,6 +231,34 @@ SPAN_RELEASE_TIMEOUT_S = 600.0
 _SPAN_PROCESS = False
 _span_children: List[Any] = []  # (device, child): children whose span may still be releasing
 _span_mu = threading.Lock()
+# GPU work this process started or ran that allocates device memory (burn-in children, and
+# in-process burn-ins): a device-wide free-memory delta is only this process's own when no
+# such work started, ran or was alive across it (:func:`activity`)
+_activity_starts = 0
+_activity_inproc = 0
+
+
+def activity() -> Tuple[int, int]:
+    """``(work started so far, work alive now)``.  Two equal snapshots with nothing alive
+    bracket a window in which no burn-in of this agent allocated or released HBM."""
+    with _span_mu:
+        alive = sum(1 for _, p in _span_children if p.poll() is None) + _activity_inproc
+        return _activity_starts, alive
+
+
+class _InProcess:
+    """An in-process burn-in, counted by :func:`activity`."""
+
+    def __enter__(self):
+        global _activity_starts, _activity_inproc
+        with _span_mu:
+            _activity_starts += 1
+            _activity_inproc += 1
+
+    def __exit__(self, *exc):
+        global _activity_inproc
+        with _span_mu:
+            _activity_inproc -= 1
 
 
 def set_span_process(on: bool) -> None:
@@ -335,7 +363,9 @@ def _child_verdict(argv: List[str], dev: int, timeout: float, what: str,
     except OSError as exc:
         raise _ChildUnstartable(f"cannot start {argv[0]}: {exc}") from exc
     with _span_mu:
+        global _activity_starts
         _span_children.append((dev, proc))
+        _activity_starts += 1
     # the verdict is the one JSON line (a library may print others); read on a thread, so a
     # line already buffered behind an earlier one is not waited for
     got: "queue.Queue[str]" = queue.Queue()
@@ -665,6 +695,12 @@ def run_burnin(dev: int, level: str = "quick", thresholds: Optional[Thresholds] 
             return _burnin_child(dev, level, th)
         except native.NativeUnavailable:
             pass  # no usable gpu-burnin here: the same burn-in in this process
+    with _InProcess():
+        return _run_burnin_here(dev, level, th)
+
+
+def _run_burnin_here(dev: int, level: str, th: "Thresholds") -> BurninResult:
+    """:func:`run_burnin` in this process."""
     info = device_info(dev)
     res = BurninResult(info, level)
     if level == "off":

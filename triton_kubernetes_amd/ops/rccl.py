@@ -194,6 +194,9 @@ class GateComm:
             for i, k in enumerate(("footprint_mib", "footprint_total_mib")):
                 b = float(lib.tkr_last_footprint(i))
                 phases[k] = round(b / 2 ** 20, 1) if b >= 0 else -1.0
+            # 1: this process's own VRAM (KFD accounting); 2: the device's used memory, which
+            # counts other allocations made meanwhile (a burn-in child's span)
+            phases["footprint_kind"] = float(lib.tkr_last_footprint(2))
         return SweepResult(self.world, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
                            float(ph[4]), phases)
 
