@@ -611,7 +611,7 @@ def main() -> int:
             if phases:  # the gate's communicator phases, max over agents
                 out["rccl"] = {k: round(max(float(p.get(k, 0.0)) for p in phases), 3)
                                for k in ("init_total", "init_wait", "alloc", "sweep", "footprint_mib",
-                                         "footprint_total_mib")}
+                                         "footprint_total_mib", "footprint_kind")}
             # an init that ran out of HBM beside the held burn-in spans and was retried
             retried = [r.get("gate_retry") for r in ranks if r.get("gate_retry")]
             if retried or (rep.rccl or {}).get("retry"):
@@ -856,8 +856,11 @@ def main() -> int:
             # GPU nodes that joined with the health taint in any timed step (normally none)
             "gpu_unhealthy_nodes": sorted({h for r in results for h in r.get("gpu_unhealthy", [])}),
             # the gate communicator's device memory per GPU (MiB, max over agents, last timed step):
-            # what the burn-in span's headroom must leave (node/agent_gate.py:span_headroom)
-            "rccl_footprint_mib": next(({k: r["rccl"].get(k) for k in ("footprint_mib", "footprint_total_mib")}
+            # what the burn-in span's headroom must leave (node/agent_gate.py:span_headroom).
+            # footprint_kind 1: the agent's own VRAM; 2: the device's used-memory delta, which
+            # in a cold step also counts the burn-in child allocating its span meanwhile
+            "rccl_footprint_mib": next(({k: r["rccl"].get(k) for k in ("footprint_mib", "footprint_total_mib",
+                                                                       "footprint_kind")}
                                         for r in reversed(results) if r.get("rccl")), None),
             # timed steps whose gate init ran out of HBM and was retried after the spans' release
             "gate_retry_steps": [r["step"] for r in results if r.get("gate_retry")],
