@@ -28,7 +28,7 @@ from ..errors import Canceled, ConfigError, TKError
 from ..models import CLUSTER_CHOICES, CLUSTER_PROVIDERS, MANAGER_CHOICES, MANAGER_PROVIDERS, NODE_ENTRY_KEYS
 from ..models import NODE_PROVIDERS
 from ..models.common import nodes_added_message
-from ..state import State
+from ..state import MANAGER_KEY, State
 from ..terraform.catalog import check_sources
 from ..utils.trace import span
 from .select import executor_for, select_cluster, select_manager
@@ -120,7 +120,7 @@ def new_manager(ctx: Context, backend: Backend) -> None:
     if not ctx.confirm("Proceed with the manager creation", "Proceed"):
         ctx.echo("Manager creation canceled.")
         return
-    mgr = state.module("cluster-manager") or {}
+    mgr = state.module(MANAGER_KEY) or {}
     if str(mgr.get("host", "")).startswith("rancher+"):
         # an adopted Rancher server: its first-login password, if given, and the opt-in for
         # the legacy derived one go to the state backend (rancher/bootstrap_secret.py), never
