@@ -49,6 +49,7 @@ def oom_node(tmp_path, monkeypatch):
     monkeypatch.setenv("TK_RCCL_STUB_HBM_FREE", str(free))
     monkeypatch.setenv("TK_RCCL_STUB_FOOTPRINT_MIB", str(FOOTPRINT_MIB))
     monkeypatch.setattr(native, "_cache", {})
+    monkeypatch.setattr(probe, "SPAN_HEADROOM", probe.SPAN_HEADROOM)  # restored after the test
     # the stand-in burn-in child: its verdict, then the span held (free stays low) until
     # stdin closes -- the release hold letting go -- then the span released
     exe = tmp_path / "gpu-burnin"
