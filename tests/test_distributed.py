@@ -158,6 +158,7 @@ def test_bench_gpus_without_a_launcher_is_one_agent_over_n_gpus():
     assert doc["rccl_gate_ranks"] == [8]
 
 
+@pytest.mark.skipif(os.path.exists("/dev/kfd"), reason="counts on no visible GPU (the GPU box has its own test)")
 def test_bench_fails_loudly_when_fewer_gpus_are_visible():
     """Without ``--sim-gpu`` this container sees no GPU: ``--gpus 2`` must not measure 0 or 1
     of them.  The line says what is wrong (value null) and the exit status is non-zero."""
