@@ -5,13 +5,16 @@ Metric (BASELINE.json): "cluster create->kubectl-ready wall-clock (s),
 bare-metal at 1/2/4/8 workers", measured on config #5: "create cluster MI355X
 bare-metal N-worker + ROCm device-plugin + xGMI topology labels".
 
-Shape.  ``--gpus N`` (the driver's N, one torchrun rank per GPU) is the number of
-MI355X GPUs the cluster's worker tier owns.  By default ONE worker node owns all of
-them -- one node agent with ``devices=0..N-1``, as on a real 8xMI355X node, so the
-per-node steps (burn-in of every GPU concurrently, topology labels) and the RCCL
-gate (``ndev=N`` grouped communicator init in one agent) run at node scale.
-``--workers W`` splits the N GPUs over W agents instead.  When the launcher masks
-devices per rank (each rank sees only its own GPU), every rank runs one 1-GPU agent.
+Shape.  ``--gpus N`` is the number of MI355X GPUs the cluster's worker tier owns.  By
+default ONE worker node owns all of them -- one node agent with ``devices=0..N-1``, as on a
+real 8xMI355X node, so the per-node steps (burn-in of every GPU concurrently, topology
+labels) and the RCCL gate (``ndev=N`` grouped communicator init in one agent) run at node
+scale.  ``--workers W`` splits the N GPUs over W agents instead.  The launch
+(:func:`resolve_gpus`): without a launcher one process drives all N GPUs (fewer visible:
+the run fails with its reason, never a smaller measurement); under ``torchrun`` there is
+one rank per GPU (``WORLD_SIZE == N``), and when the launcher masks devices per rank (each
+rank sees only its own GPU) every rank runs one 1-GPU agent.  :class:`RunBudget` keeps the
+run inside the driver's wall-clock limit by shedding untimed secondary work only.
 
 Each timed step is a COLD create:
 
