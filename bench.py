@@ -682,6 +682,12 @@ def main() -> int:
         if args.hbm_settle == "on" and my_cards:
             got = settle_cards(hbm, my_cards, warm_floor if resident else floor, resident,
                                timeout_s=budget.settle_cap_s)
+        elif args.sim_gpu and settler and os.environ.get("TK_BENCH_SIM_SETTLE_S"):
+            # CPU rehearsal of a slow driver clear (tests): the wait, capped as a real one is
+            want = float(os.environ["TK_BENCH_SIM_SETTLE_S"])
+            waited = want if budget.settle_cap_s is None else min(want, budget.settle_cap_s)
+            time.sleep(waited)
+            got = dict(got, waited_s=round(waited, 3), timed_out=waited < want)
         barrier()
         return got
 

@@ -197,3 +197,21 @@ def test_resolve_gpus_shapes():
                       ((4, 2, 4), "WORLD_SIZE 2"), ((0, 1, 1), "at least 1"), ((8, 8, 0), "0 visible to rank")):
         with pytest.raises(bench.GpuCountError, match=msg):
             bench.resolve_gpus(*args, sim=False)
+
+
+def test_bench_run_budget_end_to_end_under_torchrun():
+    """The budget in the real loop, over 2 gloo ranks, with a slow (simulated) driver clear
+    before each step: rank 0 decides, every rank follows -- the warm creates are shed, the
+    later settles capped, and every timed step still runs."""
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", "2", "--steps", "3", "--warmup", "1", "--warm-steps", "2", "--sim-gpu", "--time-budget", "20"]
+    env = dict(os.environ, OMP_NUM_THREADS="1", TK_BENCH_SIM_SETTLE_S="6")
+    proc = subprocess.run(cmd, capture_output=True, text=True, timeout=300, cwd=ROOT, env=env)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    doc = _line(proc.stdout)
+    rb = doc["run_budget"]
+    assert rb["shed"] == ["warm_creates", "hbm_settle_capped"] and rb["settle_cap_s"] < 6, rb
+    assert doc["steps"] == 3 and len(doc["create_to_ready_s"]) == 3 and doc["warm_create_to_ready_s"] is None
+    assert max(doc["hbm_settle_s"][1:]) < 6.0
+    assert "capped those waits" in doc["data"] and "warm creates were shed" in doc["data"]
