@@ -110,6 +110,7 @@ def test_bench_eight_ranks_gate_over_eight_gpus(masked):
     doc = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][0])
     assert doc["n_gpus"] == 8 and doc["rccl_gate_ranks"] == [8]
     assert doc["config"]["workers"] == (8 if masked else 1)
+    assert doc["config"]["gpus_per_worker"] == (1 if masked else 8)
 
 
 def test_bench_failure_still_prints_a_diagnostic_line():
