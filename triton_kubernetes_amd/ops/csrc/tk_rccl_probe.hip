@@ -30,6 +30,7 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <cerrno>
 #include <climits>
 #include <string>
 #include <atomic>
@@ -364,7 +365,10 @@ static long long proc_vram(int dev) {
           char path[128];
           snprintf(path, sizeof(path), "/sys/class/kfd/kfd/topology/nodes/%d/properties", n);
           FILE* fp = fopen(path, "r");
-          if (!fp) break;
+          if (!fp) {
+            if (errno == ENOENT) break;  // past the last node
+            continue;                    // a node this process may not read (another tenant's GPU)
+          }
           char key[64];
           unsigned long long v = 0, nloc = ~0ull, ndom = ~0ull;
           while (fscanf(fp, "%63s %llu", key, &v) == 2) {
