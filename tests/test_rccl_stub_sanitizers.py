@@ -19,6 +19,7 @@ CSRC = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))),
 
 DRIVER = r"""
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <thread>
 #include <vector>
@@ -30,6 +31,8 @@ int tkr_gate_begin_ex(const unsigned char*, int, int, int, const int*, int, size
 int tkr_gate_cancel(int);
 int tkr_gate_pending();
 int tkr_gate_sweep(int, const size_t*, int, int, int, int, double, double*, double*, double*, double*, double*);
+int tkr_elf_kernel_symbol(const char* path, char* out, int cap);
+int tkr_gate_poll(int);
 }
 
 static int sweep(int h, double timeout_ms, double* err_out) {
@@ -40,8 +43,15 @@ static int sweep(int h, double timeout_ms, double* err_out) {
   return rc;
 }
 
-int main() {
+int main(int argc, char** argv) {
   int failures = 0;
+  // 0. the preload's ELF scan (tk_elf_scan.h) over every file given: librccl builds, other
+  //    ELF files, truncated and corrupted ones -- bounds-checked, never a read past the map
+  for (int i = 1; i < argc; ++i) {
+    char name[512];
+    const int n = tkr_elf_kernel_symbol(argv[i], name, sizeof(name));
+    std::printf("scan %s -> %d %s\n", argv[i], n, n ? name : "-");
+  }
   // 1. one world of eight ranks, one thread each (the node agent's shape, ndev = 1 per thread)
   unsigned char uid[128];
   if (tkr_unique_id(uid)) return 10;
@@ -82,6 +92,25 @@ int main() {
   if (std::strstr(tkr_last_error(), "claimed twice") == nullptr) { std::printf("err %s\n", tkr_last_error()); ++failures; }
   tkr_gate_cancel(a);  // not sweeping: aborts it
   if (tkr_gate_pending() != 0) { std::printf("pending %d\n", tkr_gate_pending()); ++failures; }
+
+  // 4. the HBM model (TK_RCCL_STUB_HBM_FREE): a non-blocking init that does not fit fails
+  //    at poll and at sweep, with RCCL's out-of-memory text, and leaves nothing pending
+  if (const char* hbm = std::getenv("TEST_HBM_FREE_FILE")) {
+    setenv("TK_RCCL_STUB_HBM_FREE", hbm, 1);  // (the gates above had all the memory they wanted)
+    setenv("TK_RCCL_STUB_FOOTPRINT_MIB", "1024", 1);
+    unsigned char uid4[128];
+    if (tkr_unique_id(uid4)) return 13;
+    const int h4 = tkr_gate_begin_ex(uid4, 1, 0, 1, &dev0, 0, 0);
+    double e4 = 0;
+    const int p4 = tkr_gate_poll(h4);
+    const int s4 = sweep(h4, 1000.0, &e4);
+    if (h4 <= 0 || p4 != -2 || s4 != -2 || std::strstr(tkr_last_error(), "out of memory") == nullptr) {
+      std::printf("oom h %d poll %d sweep %d err %s\n", h4, p4, s4, tkr_last_error());
+      ++failures;
+    }
+    if (tkr_gate_pending() != 0) { std::printf("pending after oom %d\n", tkr_gate_pending()); ++failures; }
+    unsetenv("TK_RCCL_STUB_HBM_FREE");
+  }
   std::printf("stub driver: %d failure(s)\n", failures);
   return failures ? 1 : 0;
 }
@@ -100,10 +129,37 @@ def _build_and_run(tmp_path, flags, name):
     if build.returncode != 0 and "sanitize" in build.stderr and "not supported" in build.stderr:
         pytest.skip(f"{flags[0]} unavailable: {build.stderr[-200:]}")
     assert build.returncode == 0, build.stderr[-3000:]
+    free = tmp_path / "hbm-free"
+    free.write_text(str(100 << 20))  # 100 MiB free, 1 GiB needed
     env = dict(os.environ, TK_RCCL_STUB_DIR=str(tmp_path / "rendezvous"), ASAN_OPTIONS="detect_leaks=1",
-               TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1", UBSAN_OPTIONS="print_stacktrace=1")
-    run = subprocess.run([str(exe)], capture_output=True, text=True, timeout=240, env=env)
+               TSAN_OPTIONS="halt_on_error=1 second_deadlock_stack=1", UBSAN_OPTIONS="print_stacktrace=1",
+               TEST_HBM_FREE_FILE=str(free))
+    run = subprocess.run([str(exe), *_scan_inputs(tmp_path)], capture_output=True, text=True, timeout=240,
+                         env=env)
     return run
+
+
+def _scan_inputs(tmp_path):
+    """Files for the ELF scan: the librccl builds of this image, another ELF, and broken
+    copies (cut short of its section headers; section header offset pointing past the end;
+    a string-table index out of range)."""
+    import struct
+
+    import torch
+
+    libs = [p for p in (os.path.realpath("/opt/rocm/lib/librccl.so.1"),
+                        os.path.join(os.path.dirname(torch.__file__), "lib", "librccl.so")) if os.path.exists(p)]
+    out = list(libs) + [shutil.which("ls") or "/bin/ls", str(tmp_path / "missing.so")]
+    src = open(shutil.which("ls") or "/bin/ls", "rb").read()
+    (tmp_path / "short.so").write_bytes(src[: len(src) // 2])
+    bad = bytearray(src)
+    struct.pack_into("<Q", bad, 0x28, len(src) + 4096)  # e_shoff past the end
+    (tmp_path / "shoff.so").write_bytes(bytes(bad))
+    bad = bytearray(src)
+    struct.pack_into("<H", bad, 0x3E, 0xFFF0)  # e_shstrndx / links out of range: sections still bounded
+    (tmp_path / "strndx.so").write_bytes(bytes(bad))
+    out += [str(tmp_path / n) for n in ("short.so", "shoff.so", "strndx.so")]
+    return out
 
 
 def test_stub_clean_under_asan_ubsan(tmp_path):
@@ -111,6 +167,10 @@ def test_stub_clean_under_asan_ubsan(tmp_path):
     assert run.returncode == 0, run.stdout[-2000:] + run.stderr[-4000:]
     assert "stub driver: 0 failure(s)" in run.stdout
     assert "ERROR: AddressSanitizer" not in run.stderr and "runtime error" not in run.stderr
+    scans = [ln.split() for ln in run.stdout.splitlines() if ln.startswith("scan ")]
+    found = {os.path.basename(ln[1]): ln[4] for ln in scans}  # scan <path> -> <n> <symbol>
+    assert all(found[n] == "-" for n in ("short.so", "shoff.so", "missing.so", os.path.basename(shutil.which("ls")))), found
+    assert any("ncclDevKernelArgsStorage" in v for v in found.values())  # a librccl of the image
 
 
 def test_stub_clean_under_tsan(tmp_path):
