@@ -1018,7 +1018,12 @@ static int cluster_main(int world, int rank_base, int ndev, const char* uid_hex,
            sizes[i], t[i], alg[i], bus[i], err[i]);
   }
   const bool ok = errs == 0 && bus[n - 1] >= min_busbw;
-  printf("],\"ok\":%s}\n", ok ? "true" : "false");
+  // the communicator's device memory per GPU (node/agent_gate.py span_headroom; -1: unknown;
+  // kind 1: this process's own VRAM, 2: the device's used memory)
+  printf("],\"footprint_mib\":%.1f,\"footprint_total_mib\":%.1f,\"footprint_kind\":%.0f,\"ok\":%s}\n",
+         tkr_last_footprint(0) < 0 ? -1.0 : tkr_last_footprint(0) / 1048576.0,
+         tkr_last_footprint(1) < 0 ? -1.0 : tkr_last_footprint(1) / 1048576.0, tkr_last_footprint(2),
+         ok ? "true" : "false");
   fflush(stdout);
   tkr_drain();
   return ok ? 0 : 1;
