@@ -168,9 +168,9 @@ class RunBudget:
     them, 25 settles would outlast any limit before the line prints.
 
     After every step (warmup or timed) :meth:`plan` projects the run's end from what the
-    steps so far cost -- the slowest settle and the slowest step seen, for each step still
-    to come, plus the warm creates -- and, if the projection exceeds ``budget_s``, sheds
-    secondary work in this order:
+    steps so far cost -- the slowest settle and the slowest step of the last few, for each
+    step still to come, plus the warm creates -- and, while the projection exceeds
+    ``budget_s``, sheds secondary work in this order:
 
     1. ``warm_creates``: the secondary warm creates are skipped (``warm_create_to_ready_s``
        null);
@@ -178,10 +178,14 @@ class RunBudget:
        step, so a step may start before the driver has finished clearing -- the step then
        pays that clearing inside its timed region, which can only make ``value`` worse.
 
-    The ``--warmup`` and ``--steps`` counts are never cut: the line's ``steps`` and
-    ``warmup`` are what ran.  ``budget_s`` 0 turns the guard off."""
+    Every projection decides afresh: a run that caught up (a slow cold first step, then
+    ordinary ones) lifts the cap again, and the warm creates run if the time is there when
+    the timed steps are done.  ``shed`` reports what was actually given up.  The
+    ``--warmup`` and ``--steps`` counts are never cut: the line's ``steps`` and ``warmup``
+    are what ran.  ``budget_s`` 0 turns the guard off."""
 
     TAIL_S = 15.0  # after the last step: the agents' stop, the report, the process exit
+    RECENT = 3  # the projection prices each step still to come at the slowest of the last 3
 
     def __init__(self, budget_s: float, t0: float = None, clock=time.monotonic):
         self.budget_s = float(budget_s or 0.0)
@@ -189,41 +193,47 @@ class RunBudget:
         self.t0 = _T_START if t0 is None else t0
         self.settles = []
         self.steps = []
-        self.shed = []
+        self.caps_used = []  # the cap each capped settle ran under
         self.projected_s = None
         self.settle_cap_s = None
         self.warm_allowed = True
 
+    @property
+    def shed(self) -> list:
+        return (["warm_creates"] if not self.warm_allowed else []) + (["hbm_settle_capped"] if self.caps_used else [])
+
     def record(self, settle_s: float, step_s: float) -> None:
+        """One settle and the step after it; the settle ran under the cap in force now."""
         self.settles.append(float(settle_s))
         self.steps.append(float(step_s))
+        if self.settle_cap_s is not None:
+            self.caps_used.append(self.settle_cap_s)
 
     def plan(self, cold_left: int, warm_creates: int) -> None:
         """Re-project after a step; ``cold_left`` cold steps (warmup + timed) and
         ``warm_creates`` warm creates (each with its own settle) are still to run."""
         if not self.steps:
             return
-        settle, step = max(self.settles), max(self.steps)
+        # the slowest of the last few: a cold first step (fresh box) stops counting once the
+        # run has settled, a node whose clears grow keeps counting them
+        settle, step = max(self.settles[-self.RECENT:]), max(self.steps[-self.RECENT:])
         elapsed = self.clock() - self.t0
-        warm = (settle + step) * warm_creates if self.warm_allowed else 0.0
-        proj = elapsed + cold_left * (settle + step) + warm + self.TAIL_S
-        self.projected_s = round(proj, 1)
-        if not self.budget_s or proj <= self.budget_s:
+        warm = (settle + step) * warm_creates
+        base = elapsed + cold_left * (settle + step) + self.TAIL_S
+        self.projected_s = round(base + warm, 1)
+        if not self.budget_s or base + warm <= self.budget_s:
+            self.warm_allowed, self.settle_cap_s = True, None
             return
-        if warm and self.warm_allowed:
-            self.warm_allowed = False
-            self.shed.append("warm_creates")
-            proj -= warm
-        if proj > self.budget_s and cold_left:
-            cap = max(0.0, (self.budget_s - elapsed - self.TAIL_S - cold_left * step) / cold_left)
-            if self.settle_cap_s is None or cap < self.settle_cap_s:
-                self.settle_cap_s = round(cap, 2)
-            if "hbm_settle_capped" not in self.shed:
-                self.shed.append("hbm_settle_capped")
+        self.warm_allowed = not warm  # nothing to shed when no warm create is left
+        if base <= self.budget_s or not cold_left:
+            self.settle_cap_s = None
+            return
+        self.settle_cap_s = round(max(0.0, (self.budget_s - elapsed - self.TAIL_S - cold_left * step) / cold_left), 2)
 
     def report(self) -> dict:
-        return {"budget_s": self.budget_s or None, "projected_s": self.projected_s, "shed": list(self.shed),
-                "settle_cap_s": self.settle_cap_s, "elapsed_s": round(self.clock() - self.t0, 1)}
+        return {"budget_s": self.budget_s or None, "projected_s": self.projected_s, "shed": self.shed,
+                "settle_cap_s": min(self.caps_used) if self.caps_used else None, "capped_settles": len(self.caps_used),
+                "elapsed_s": round(self.clock() - self.t0, 1)}
 
 
 def resolve_gpus(requested: int, world: int, visible: int, sim: bool, masked_env: bool = False) -> dict:
@@ -291,7 +301,7 @@ def parse_args():
                          "libtk_rccl ABI stub (ops/csrc/tk_rccl_stub.cpp: every rank of the world joins and sweeps, "
                          "no GPU); never a valid measurement")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
-    ap.add_argument("--time-budget", type=float, default=420.0,
+    ap.add_argument("--time-budget", type=float, default=480.0,
                     help="wall-clock seconds the whole run should stay within (RunBudget): past it the secondary "
                          "warm creates are shed, then the untimed settle waits are capped; the timed steps never "
                          "are.  0: off")
@@ -697,9 +707,9 @@ def main() -> int:
         if rank == 0:
             budget.plan(cold_left, (args.warm_steps + 1) if args.warm_steps > 0 else 0)
         if distributed:
-            got = [(budget.warm_allowed, budget.settle_cap_s, list(budget.shed))]
+            got = [(budget.warm_allowed, budget.settle_cap_s)]
             dist.broadcast_object_list(got, src=0)
-            budget.warm_allowed, budget.settle_cap_s, budget.shed = got[0]
+            budget.warm_allowed, budget.settle_cap_s = got[0]
 
     comgr = {"dir": comgr_cache_dir(), "enabled": os.environ.get("AMD_COMGR_CACHE", "1") != "0",
              "mib_at_start": dir_mib(comgr_cache_dir()), "prewarm_s": None}
@@ -819,9 +829,9 @@ def main() -> int:
                            + ("; before each timed step, untimed, the bench waits for the driver to clear the HBM "
                               "the previous step released (a node entering service starts clean)"
                               if args.hbm_settle == "on" and not args.sim_gpu else "")
-                           + ("; the run budget capped those waits at %.1f s, so a step may pay part of its "
-                              "predecessor's clearing inside the timed region" % budget.settle_cap_s
-                              if budget.settle_cap_s is not None else "")
+                           + ("; the run budget capped %d of those waits (down to %.1f s), so a step may pay part "
+                              "of its predecessor's clearing inside the timed region"
+                              % (len(budget.caps_used), min(budget.caps_used)) if budget.caps_used else "")
                            + ("; the secondary warm creates were shed by the run budget"
                               if "warm_creates" in budget.shed else "")
                            + ("; opt-in node install before the timed region: verified single-target gfx950 "
