@@ -701,11 +701,16 @@ def main() -> int:
         barrier()
         return got
 
-    def replan(cold_left: int, settle_s: float, step_s: float) -> None:
+    def replan(cold_left: int, settle_s: float, step_s: float, what: str = "") -> None:
         """Rank 0 re-projects the run (RunBudget) and every rank takes its decision."""
         budget.record(settle_s, step_s)
         if rank == 0:
             budget.plan(cold_left, (args.warm_steps + 1) if args.warm_steps > 0 else 0)
+            # one progress line per step on stderr (stdout carries only the result line)
+            print(f"bench: {what} settle {settle_s:.1f} s, step {step_s:.2f} s, {cold_left} to go, "
+                  f"projected {budget.projected_s} s of {budget.budget_s or 'no'} budget"
+                  + (f", settle cap {budget.settle_cap_s} s" if budget.settle_cap_s is not None else ""),
+                  file=sys.stderr, flush=True)
         if distributed:
             got = [(budget.warm_allowed, budget.settle_cap_s)]
             dist.broadcast_object_list(got, src=0)
@@ -727,7 +732,7 @@ def main() -> int:
             barrier()
             t_step = time.perf_counter()
             cold_step(-1 - w)
-            replan(args.warmup - w - 1 + args.steps, t_step - t_s, time.perf_counter() - t_step)
+            replan(args.warmup - w - 1 + args.steps, t_step - t_s, time.perf_counter() - t_step, f"warmup {w + 1}")
         TRACER.reset()
         comgr["mib_before_timed"] = dir_mib(comgr["dir"])
         # the timed region is the K steps, each bracketed by a barrier + synchronize on both
@@ -742,7 +747,7 @@ def main() -> int:
             barrier()
             took = time.perf_counter() - t_step
             elapsed += took
-            replan(args.steps - i - 1, t_step - t_s, took)
+            replan(args.steps - i - 1, t_step - t_s, took, f"step {i + 1}")
     except Exception as exc:
         if rank == 0:
             # a failed run still says what failed, in the line's own shape (value null), before
