@@ -486,6 +486,10 @@ def main() -> int:
         mine = [(f"mi355x-{w}", list(range(w * per, (w + 1) * per))) for w in range(workers)] if rank == 0 else []
     gpus_per_worker = n_gpus // workers
     budget = RunBudget(args.time_budget)
+    if rank == 0:
+        print(f"bench: {n_gpus} GPU(s), {workers} worker(s) x {gpus_per_worker}, world {world}"
+              f"{' (masked ranks)' if masked else ''}, burn-in {args.burnin}, {args.warmup} warmup + {args.steps} steps",
+              file=sys.stderr, flush=True)
 
     from triton_kubernetes_amd import versions
     from triton_kubernetes_amd import workflows as wf
