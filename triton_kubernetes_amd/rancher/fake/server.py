@@ -104,8 +104,11 @@ class FakeRancher(V3Api, ProvisioningApi, K8sCoreApi):
                            list(rke2_versions) if rke2_versions is not None else [v for _, v in RKE2_VERSIONS])
         self.state.device_plugin_seconds = device_plugin_seconds
         self.bootstrap_password = pw
-        # every request body the server received (the tests check what was sent to it)
-        self.request_bodies: List[bytes] = []
+        # the request bodies the server received, the latest 20000 (the tests check what was
+        # sent to it; bounded for long runs such as the bench)
+        import collections
+
+        self.request_bodies: "collections.deque[bytes]" = collections.deque(maxlen=20000)
         # "<service>.<namespace>" -> "https://127.0.0.1:<port>" (where an in-cluster
         # webhook service of a test really listens)
         self.service_endpoints: Dict[str, str] = {}
