@@ -115,8 +115,10 @@ class AgentGateMixin:
     # of 8 xGMI peers that headroom was a constant nobody had measured, so an init can run
     # out of memory there.  Then every held span is released and the init is retried once
     # (``gate_retry: oom`` in the answer), and the footprint each successful init measured
-    # (hipMemGetInfo around it, ``tk_rccl_probe.hip``) sets the node's headroom from then on
-    # (:meth:`_note_gate_footprint`), the constant staying the floor.
+    # (this process's VRAM around it, or the device's from a window without burn-in
+    # activity: ``tk_rccl_probe.hip:proc_vram``) sets the node's headroom from then on
+    # (:meth:`_note_gate_footprint`), the constant staying the floor; an out-of-memory init
+    # doubles it (:meth:`_note_gate_oom`).
 
     FOOTPRINT_FILE = "/etc/triton-kubernetes/gate-footprint.json"
     HEADROOM_MARGIN = 1.25  # measured footprint x this, plus the floor's first GiB
@@ -216,10 +218,13 @@ class AgentGateMixin:
                 return
             fp[key] = round(mib, 1)
             doc = dict(fp)
-        try:
-            self.write_file(self.FOOTPRINT_FILE, json.dumps(doc, sort_keys=True))
-        except Exception:  # noqa: BLE001 - a read-only root only loses the memory of it
-            pass
+        # kept on the node (exec mode), or under a sim agent's own root; a sim agent with root
+        # / models no host and never writes to the machine it runs on
+        if self.mode == "exec" or self._host_is_sandbox():
+            try:
+                self.write_file(self.FOOTPRINT_FILE, json.dumps(doc, sort_keys=True))
+            except Exception:  # noqa: BLE001 - a read-only root only loses the memory of it
+                pass
         probe.set_span_headroom(self.span_headroom(len(self.devices)))
 
     def _load_gate_footprints(self) -> Dict[str, float]:
