@@ -46,10 +46,6 @@ class _SimGate:
         pass
 
 
-# appended to the error of an init that failed again after the spans' release
-RETRIED_MARK = "[gate_retry: oom, failed again after the held spans' release]"
-
-
 class GateAborted(RuntimeError):
     """The gate was aborted (``/v1/rccl-abort``) before or while this request ran."""
 
@@ -178,7 +174,7 @@ class AgentGateMixin:
                 res = sweep(remake())
             except rccl.RCCLError as exc:
                 # once only: the cluster gate sees it was retried (RETRIED_MARK) and does not
-                raise rccl.RCCLError(f"{exc} {RETRIED_MARK}") from exc
+                raise rccl.RCCLError(f"{exc} {rccl.OOM_RETRIED_MARK}") from exc
         return res, {"gate_retry": "oom", "first_error": first_error[:400], "spans_released_ms": released_ms}
 
     def _note_gate_footprint(self, ndev: int, phase_ms: Dict[str, float], window: Any = None) -> None:

@@ -218,6 +218,9 @@ class GateComm:
 # A failed init whose least-free GPU had less than this left ran out of memory, whatever
 # RCCL called the failure ("unhandled cuda error" / "unhandled system error")
 OOM_FREE_MIB = 2048
+# appended to the error of an init that failed again after the agent released its held
+# burn-in spans and retried (node/agent_gate.py): the cluster gate does not retry it again
+OOM_RETRIED_MARK = "[gate_retry: oom, failed again after the held spans' release]"
 
 
 def is_oom_error(text: str) -> bool:

@@ -219,10 +219,9 @@ def _oom(error: Optional[str]) -> bool:
     (a node that is the whole gate retries by itself, node/agent_gate.py)."""
     if not error:
         return False
-    from ..node.agent_gate import RETRIED_MARK
-    from ..ops.rccl import is_oom_error
+    from ..ops.rccl import OOM_RETRIED_MARK, is_oom_error
 
-    return is_oom_error(error) and RETRIED_MARK not in error
+    return is_oom_error(error) and OOM_RETRIED_MARK not in error
 
 
 __all__ = ["ClusterGate", "GateMember", "members_from"]
