@@ -2,9 +2,9 @@
 """The cluster gate communicator's device footprint on this box.
 
 A full burn-in's span leaves ``probe.SPAN_HEADROOM`` free per GPU while the gate's
-communicator initialises; this measures what that init takes (``tk_rccl_probe.hip``:
-hipMemGetInfo around the grouped init, then around the preallocated sweep buffers), for the
-sizes the readiness gate uses.  One JSON line per case; run in a fresh process each (RCCL's
+communicator initialises; this measures what that init takes (``tk_rccl_probe.hip``: this
+process's VRAM -- or, inside a PID namespace, the device's used memory -- around the grouped
+init, then around the preallocated sweep buffers), for the sizes the readiness gate uses.  One JSON line per case; run in a fresh process each (RCCL's
 device code loads once per process and counts in the first init only).
 
     python scripts/gate_footprint.py [--prealloc-mib 64] [--repeat 3] [--ndev N]
