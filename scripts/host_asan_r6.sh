@@ -2,7 +2,8 @@
 # Round 6's native host code under ASan/UBSan on the MI355X (device code not instrumented):
 # the gate path of rccl-ready (--cluster: tkr_gate_begin_ex -> init_body with the footprint
 # measurement, proc_vram's KFD lookup and its device-wide fallback) and the preload's symbol
-# lookup (--preload).  Build (CPU container):
+# lookup (--preload).  (.gpurunignore lists the -asan-r6 binary: drop that line to send it with a
+# gpurun call.)  Build (CPU container):
 #   hipcc -O1 -g -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN -Xarch_host -fsanitize=address \
 #     -Xarch_host -fsanitize=undefined -fno-gpu-sanitize ops/csrc/tk_rccl_probe.hip \
 #     -o scripts/native/rccl-ready-asan-r6 -L/opt/rocm/lib -lrccl -Wl,-rpath,/opt/rocm/lib
