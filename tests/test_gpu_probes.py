@@ -599,15 +599,20 @@ def test_rccl_preload_finds_a_kernel_handle_on_the_installed_librccl():
 
 
 def test_bench_refuses_more_gpus_than_visible():
-    """on this one-GPU box ``bench.py --gpus 2`` (no launcher) must fail with
-    the reason in its line, never measure one GPU as two."""
+    """``bench.py --gpus N`` (no launcher) with fewer than N GPUs visible (on
+    this one-GPU box: ``--gpus 2``) must fail with the reason in its line, never measure one
+    GPU as two."""
+    import torch
+
+    have = torch.cuda.device_count()
+    want = have + 1
     proc = subprocess.run(["timeout", "-k", "5", "120", sys.executable, os.path.join(ROOT, "bench.py"), "--gpus",
-                           "2", "--steps", "1", "--warmup", "0"], capture_output=True, text=True, cwd=ROOT,
+                           str(want), "--steps", "1", "--warmup", "0"], capture_output=True, text=True, cwd=ROOT,
                           env={k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")})
     assert proc.returncode == 2, proc.stdout[-2000:] + proc.stderr[-2000:]
     line = json.loads([ln for ln in proc.stdout.splitlines() if ln.startswith("{")][-1])
-    assert line["value"] is None and line["n_gpus"] == 2
-    assert line["error"] == "2 GPUs requested, 1 visible", line
+    assert line["value"] is None and line["n_gpus"] == want
+    assert line["error"] == f"{want} GPUs requested, {have} visible", line
 
 
 def test_gate_communicator_footprint_is_measured():
