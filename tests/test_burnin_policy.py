@@ -664,3 +664,55 @@ def test_gpu_burnin_all_runs_the_same_levels_as_the_agent():
         assert hi == int(hbm_iters.group(1)), level
         assert mi == int(mfma.group(1 + k)), level
         assert mp == int(passes.group(1 + k)), level
+
+
+def _matrix(n=4, gbps=50.0, slow=None, corrupt=None, errors=()):
+    pairs = {f"{i}-{j}": gbps for i in range(n) for j in range(n) if i != j}
+    for p, v in (slow or {}).items():
+        pairs[p] = v
+    return {"pairs": pairs, "peer_access": {p: True for p in pairs}, "errors": list(errors),
+            "data_errors": dict(corrupt or {}), "method": "kernel-read", "bytes": 64 << 20}
+
+
+def test_a_link_that_read_slow_once_is_measured_again():
+    """The burn-in's rule for throughput gates applies to the xGMI link matrix: a pair below
+    half the node's median is measured again (best of up to 3) before it fails the node --
+    the first 8-GPU run must not fail on one noisy read."""
+    from triton_kubernetes_amd.node.labels import best_link_verdict
+
+    runs = iter([_matrix(slow={"2-3": 12.0}), _matrix()])
+    got = best_link_verdict(lambda: next(runs), 0.5, 0.0)
+    assert got["status"] == "passed" and got["remeasured"] == 1 and got["matrix"]["pairs"]["2-3"] == 50.0
+
+
+def test_a_link_slow_every_time_still_fails_and_wrong_data_is_never_retried():
+    from triton_kubernetes_amd.node.labels import best_link_verdict
+
+    calls = []
+
+    def slow():
+        calls.append(1)
+        return _matrix(slow={"1-3": 10.0})
+
+    got = best_link_verdict(slow, 0.5, 0.0)
+    assert got["status"] == "degraded" and got["degraded"] == ["1-3"] and got["remeasured"] == 2 and len(calls) == 3
+    calls.clear()
+
+    def corrupt():
+        calls.append(1)
+        return _matrix(corrupt={"0-1": 7})
+
+    got = best_link_verdict(corrupt, 0.5, 0.0)
+    assert got["status"] == "degraded" and got["corrupt"] == ["0-1"] and len(calls) == 1
+    calls.clear()
+
+    def broken():
+        calls.append(1)
+        return _matrix(errors=["2->3: peer read failed"])
+
+    got = best_link_verdict(broken, 0.5, 0.0)
+    assert got["status"] == "error" and len(calls) == 1
+    # a pair that corrupted data in a retry stays corrupt after a faster read
+    runs = iter([_matrix(slow={"1-2": 10.0}), _matrix(corrupt={"1-2": 1})])
+    got = best_link_verdict(lambda: next(runs), 0.5, 0.0)
+    assert got["status"] == "degraded" and got["corrupt"] == ["1-2"] and got["remeasured"] == 1

@@ -1309,6 +1309,36 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
     printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
     return 2;
   }
+  // a matrix whose only fault is speed is measured again, best of up to 3 per pair (the
+  // burn-in's rule for throughput gates, node/labels.py:best_link_verdict); a pair that
+  // delivered wrong data, or could not be measured, is never retried away
+  int remeasured = 0;
+  for (; remeasured < 2; ++remeasured) {
+    std::vector<double> ok_vals;
+    bool unmeasured = false, bad_data = false;
+    for (int i = 0; i < n; ++i)
+      for (int j = 0; j < n; ++j) {
+        if (i == j) continue;
+        if (mat[i * n + j] < 0.0 || !acc[i * n + j]) unmeasured = true;
+        else ok_vals.push_back(mat[i * n + j]);
+        bad_data = bad_data || derr[i * n + j] > 0.0;
+      }
+    if (unmeasured || bad_data || ok_vals.empty()) break;
+    std::sort(ok_vals.begin(), ok_vals.end());
+    const size_t k = ok_vals.size();
+    const double med = k % 2 ? ok_vals[k / 2] : 0.5 * (ok_vals[k / 2 - 1] + ok_vals[k / 2]);
+    bool slow = false;
+    for (double v : ok_vals) slow = slow || v < min_frac * med || v < min_gbps;
+    if (!slow) break;
+    std::vector<double> again(n * n, 0.0), derr2(n * n, 0.0);
+    std::vector<int> acc2(n * n, 0);
+    if (tkp_link_matrix_check(devs.data(), n, 64ull << 20, 3, mode, again.data(), acc2.data(), derr2.data()) != 0)
+      break;  // the first measurement stands
+    for (int x = 0; x < n * n; ++x) {
+      if (again[x] > mat[x]) mat[x] = again[x];
+      derr[x] += derr2[x];
+    }
+  }
   int errors = 0, no_peer = 0;
   printf("{\"pairs\":{");
   bool first = true;
@@ -1339,9 +1369,10 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
     }
   const char* status = (errors || no_peer || m == 0) ? "error" : (degraded ? "degraded" : "passed");
   printf("},\"method\":\"%s\",\"min_gbps\":%.1f,\"median_gbps\":%.1f,\"floor_gbps\":%.1f,\"degraded\":%d,"
-         "\"below_floor\":%d,\"corrupt\":%d,\"errors\":%d,\"no_peer_access\":%d,\"status\":\"%s\"}\n",
+         "\"below_floor\":%d,\"corrupt\":%d,\"errors\":%d,\"no_peer_access\":%d,\"remeasured\":%d,"
+         "\"status\":\"%s\"}\n",
          mode ? "kernel-read" : "sdma-copy", m ? sorted[0] : 0.0, median, min_gbps, degraded, below_floor, corrupt,
-         errors, no_peer, status);
+         errors, no_peer, remeasured, status);
   if (labels_path && m) {
     FILE* f = fopen(labels_path, "w");
     if (!f) { fprintf(stderr, "cannot write %s\n", labels_path); return 2; }
