@@ -615,7 +615,8 @@ def main() -> int:
                             out.setdefault("xgmi_links", []).append({
                                 "status": links.get("status"), "min_gbps": float(lab.get("amd.com/xgmi.p2p-min-gbps", 0)),
                                 "median_gbps": float(lab.get("amd.com/xgmi.p2p-median-gbps", 0)),
-                                "method": lab.get("amd.com/xgmi.p2p-method"), "floor_gbps": links.get("floor_gbps")})
+                                "method": lab.get("amd.com/xgmi.p2p-method"), "floor_gbps": links.get("floor_gbps"),
+                                "remeasured": links.get("remeasured", 0)})
             if steps:
                 out["gpu_node_step_ms"] = {k: round(v, 1) for k, v in steps.items()}
         rep = ctx.extras.get("last_readiness")
