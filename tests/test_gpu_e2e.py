@@ -374,3 +374,63 @@ def test_exec_agent_rke2_teardown_then_another_cluster_on_mi355x(tmp_path, monke
         "/usr/local/bin/rke2-uninstall.sh"], script_rep
     assert not (root / hostsim.CONNECTION_INFO.lstrip("/")).exists() and not (root / "var/lib/rancher").exists()
     print(json.dumps({"cleanup_ms": rep.get("ms"), "actions": rep["actions"], "script_actions": script_rep["actions"]}))
+
+
+def test_exec_agent_rke1_teardown_then_another_cluster_on_mi355x(tmp_path, monkeypatch):
+    """VERDICT r5 #3 on the box: an exec-mode agent joins RKE1 cluster A through a docker
+    with Docker's own semantics (``fixtures/fake_docker.py``: the tagged agent, RKE's
+    containers, the kubelet's pods), cluster B is refused while A's join stands,
+    ``/v1/cleanup`` removes the agent and every pod container (the machine owner's stays),
+    then B joins -- the GPU steps running on the card each time."""
+    import os
+    import subprocess
+    import sys
+
+    from triton_kubernetes_amd import versions
+    from triton_kubernetes_amd.node.agent import NodeAgent
+    from triton_kubernetes_amd.node.plan import build_host_plan
+    from triton_kubernetes_amd.parallel.transport import AgentTransport, HostRef
+    from triton_kubernetes_amd.rancher.fake import FakeRancher
+
+    fake_docker = os.path.join(os.path.dirname(os.path.abspath(__file__)), "fixtures", "fake_docker.py")
+    bindir = tmp_path / "bin"
+    bindir.mkdir()
+    _stub(bindir, "docker", f'exec {sys.executable} {fake_docker} "$@"')
+    _stub(bindir, "hostnamectl", "exit 0")
+    root = tmp_path / "root"
+    monkeypatch.setenv("PATH", f"{bindir}:{os.environ.get('PATH', '/usr/bin:/bin')}")
+    monkeypatch.setenv("TK_HOST_ROOT", str(root))  # the fake docker keeps this host's containers
+
+    def containers():
+        path = root / "var/lib/docker/fake-containers.json"
+        return json.loads(path.read_text()) if path.exists() else []
+
+    subprocess.run(["docker", "run", "-d", "--name", "owners-nginx", "nginx:1.25"], check=True, capture_output=True)
+    fake = FakeRancher().start()
+    agent = NodeAgent(name="w-rke1", mode="exec", devices=[0], token="exec-token-123456", root=str(root))
+    url = agent.serve()
+    transport, ref = AgentTransport(token="exec-token-123456"), HostRef("agent+" + url)
+    cfg = {"hostname": "gpu-rke1-1", "rancher_host_labels": {"worker": "true"}, "gpu_count": 1,
+           "gpu_burnin": "quick", "k8s_distribution": "rke1"}
+    try:
+        first = transport.run_plan(ref, build_host_plan(cfg, fake.url, "regtokA123", "cafe0123", mi355x=True))
+        assert first["ok"], first
+        names = sorted(c["name"] for c in containers())
+        assert any(c["image"] == versions.AGENT_IMAGE and not c["name"].startswith("k8s_") for c in containers())
+        assert sum(n.startswith("k8s_") for n in names) == 4 and "kubelet" in names
+        plan_b = build_host_plan(cfg, fake.url, "regtokB456", "cafe0123", mi355x=True)
+        refused = transport.run_plan(ref, plan_b)
+        assert not refused["ok"] and "another cluster" in json.dumps(refused), refused
+        rep = transport.cleanup_host(ref)
+        assert rep["ok"], rep
+        assert [c["name"] for c in containers()] == ["owners-nginx"], containers()
+        second = transport.run_plan(ref, plan_b)
+        assert second["ok"], second
+        agents = [c for c in containers() if c["image"] == versions.AGENT_IMAGE and not c["name"].startswith("k8s_")]
+        assert len(agents) == 1 and "regtokB456" in agents[0]["args"]
+        burn = [s for s in second["steps"] if s["name"] == "gpu_burnin"][0]
+        assert burn["ok"], burn
+    finally:
+        agent.stop()
+        fake.stop()
+    print(json.dumps({"cleanup_ms": rep.get("ms"), "actions": rep["actions"]}))
