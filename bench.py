@@ -481,7 +481,10 @@ def main() -> int:
     else:
         workers = max(1, min(args.workers, n_gpus))
         if n_gpus % workers:
-            raise SystemExit(f"--workers {workers} does not divide {n_gpus} GPUs")
+            if rank == 0:
+                print(json.dumps(failure_line(args, n_gpus, workers, None, visible,
+                                              f"--workers {workers} does not divide {n_gpus} GPUs")), flush=True)
+            return 2
         per = n_gpus // workers
         mine = [(f"mi355x-{w}", list(range(w * per, (w + 1) * per))) for w in range(workers)] if rank == 0 else []
     gpus_per_worker = n_gpus // workers
