@@ -66,6 +66,7 @@ Rank 0 prints one JSON line (the driver's contract).
 import argparse
 import json
 import os
+import shutil
 import signal
 import subprocess
 import sys
@@ -547,8 +548,23 @@ def main() -> int:
                   distributions=[versions.DEFAULT_DISTRIBUTION]).write(creds[name])
     client_ctx = pki.client_context()
 
+    from triton_kubernetes_amd.node.agent_gate import AgentGateMixin
+
+    last_root = {}  # agent name -> its root in the previous step
+
     def start_agents(tag: str):
         names = [(name, devs) for name, devs in mine] + ([("control-plane", [])] if rank == 0 else [])
+        for name, _ in names:
+            # what a real node keeps across agent restarts and clusters: the gate footprints
+            # its earlier gates measured (the burn-in's headroom, node/agent_gate.py).  Every
+            # other file of the root is fresh (a cold step: a new cluster's join, new labels)
+            root = os.path.join(work, tag, name)
+            prev = os.path.join(last_root.get(name, ""), AgentGateMixin.FOOTPRINT_FILE.lstrip("/"))
+            if name in last_root and os.path.exists(prev):
+                dst = os.path.join(root, AgentGateMixin.FOOTPRINT_FILE.lstrip("/"))
+                os.makedirs(os.path.dirname(dst), exist_ok=True)
+                shutil.copyfile(prev, dst)
+            last_root[name] = root
         if args.agents == "inproc":
             return [InprocAgent(name, devs, creds[name], addresses[name], os.path.join(work, tag, name),
                                 synthetic if devs else 0) for name, devs in names]
@@ -660,6 +676,13 @@ def main() -> int:
         if any(rcs):
             raise RuntimeError(f"agent exit codes {rcs}")
         out["agent_stop_ms"] = {p.name: getattr(p, "stop_ms", None) for p in procs}
+        # what each GPU node keeps for its next burn-in: the gate footprints it measured
+        out["gate_footprints"] = {}
+        for name, _ in mine:
+            kept = os.path.join(last_root[name], AgentGateMixin.FOOTPRINT_FILE.lstrip("/"))
+            if os.path.exists(kept):
+                with open(kept, "r", encoding="utf-8") as fh:
+                    out["gate_footprints"][name] = json.load(fh)
         out.update(agents_start_s=round(t_agents - t0, 4), create_to_ready_s=round(t_ready - t0, 4),
                    step_s=round(time.perf_counter() - t0, 4))
         return out
@@ -896,6 +919,9 @@ def main() -> int:
                                         for r in reversed(results) if r.get("rccl")), None),
             # timed steps whose gate init ran out of HBM and was retried after the spans' release
             "gate_retry_steps": [r["step"] for r in results if r.get("gate_retry")],
+            # what the GPU nodes keep for their next burn-in's headroom after the last timed step
+            # (/etc/triton-kubernetes/gate-footprint.json, carried from step to step as on a node)
+            "node_gate_footprints": results[-1].get("gate_footprints") if results else None,
             # ranks of the cluster RCCL gate per timed step (every GPU of the worker tier)
             "rccl_gate_ranks": [r.get("rccl_gate_ranks", 0) for r in results],
             # the GPU nodes' measured xGMI peer-read matrix (2+ GPUs per node), last timed step
@@ -923,8 +949,6 @@ def main() -> int:
     devnull.close()
     if fake is not None:
         fake.stop()
-    import shutil
-
     shutil.rmtree(work, ignore_errors=True)  # the run's manager state, agent roots and node files
     if distributed:
         dist.barrier()

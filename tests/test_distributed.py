@@ -217,3 +217,19 @@ def test_bench_run_budget_end_to_end_under_torchrun():
     assert doc["steps"] == 3 and len(doc["create_to_ready_s"]) == 3 and doc["warm_create_to_ready_s"] is None
     assert max(doc["hbm_settle_s"][1:]) < 6.0
     assert "the run budget capped" in doc["data"] and "warm creates were shed" in doc["data"]
+
+
+def test_bench_carries_the_node_gate_footprint_from_step_to_step():
+    """A node keeps /etc/triton-kubernetes/gate-footprint.json across agent restarts; the
+    bench's cold steps start fresh agents in fresh roots but carry that file, as a node
+    would.  Over the ABI stub a gate reports a 900 MiB per-process footprint."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", TK_RCCL_STUB_FOOTPRINT_MIB="900")
+    for k in ("WORLD_SIZE", "RANK", "LOCAL_RANK"):
+        env.pop(k, None)
+    proc = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "2",
+                           "--warmup", "1", "--warm-steps", "0", "--sim-gpu"], capture_output=True, text=True,
+                          timeout=240, cwd=ROOT, env=env)
+    assert proc.returncode == 0, proc.stderr[-3000:]
+    doc = _line(proc.stdout)
+    assert doc["node_gate_footprints"] == {"mi355x-0": {"2": 900.0}}, doc["node_gate_footprints"]
+    assert doc["rccl_footprint_mib"]["footprint_total_mib"] == 900.0
