@@ -75,3 +75,24 @@ def test_triton_examples_offline(tk_home, tmp_path, monkeypatch):
     assert len(nodes) == 10
     roles = [next(iter(state["module"][k]["rancher_host_labels"])) for k in nodes]
     assert sorted(roles) == ["control"] * 3 + ["etcd"] * 3 + ["worker"] * 4
+
+
+def test_adopt_manager_example_via_cli(tk_home, tmp_path):
+    """The adopted-server example against the fake Rancher: the given bootstrap password is
+    used (and kept in the state backend, not in main.tf.json); nothing derived from the
+    admin password reaches the server."""
+    import yaml
+
+    from triton_kubernetes_amd import versions
+    from triton_kubernetes_amd.rancher.fake import FakeRancher
+
+    doc = yaml.safe_load(open(os.path.join(EX, "adopt-manager.yaml")))
+    with FakeRancher(bootstrap_password=doc["rancher_bootstrap_password"]) as fake:
+        path = _with_overrides(tmp_path, "adopt-manager.yaml", host="rancher+" + fake.url)
+        code, out = _cli("--non-interactive", "--config", path, "create", "manager")
+        assert code == 0, out
+        assert fake.state.admin_password == doc["rancher_admin_password"]
+        derived = versions.bootstrap_password(doc["name"], doc["rancher_admin_password"]).encode()
+        assert not any(derived in b for b in fake.request_bodies)
+    state_dir = tk_home / ".triton-kubernetes" / doc["name"]
+    assert doc["rancher_bootstrap_password"] not in (state_dir / "main.tf.json").read_text()
