@@ -39,7 +39,3 @@ class PromptAborted(TKError):
 
 class Canceled(Exception):
     """User declined a confirmation prompt; the workflow returns cleanly."""
-
-
-def must_be_specified(key: str) -> ConfigError:
-    return ConfigError(f"{key} must be specified")

@@ -18,7 +18,7 @@ MI355X additions (BASELINE.json north star):
 import math
 from typing import Dict, List
 
-from ..config.context import Context, expand_home, file_exists, not_blank
+from ..config.context import Context, file_exists, not_blank
 from ..errors import ConfigError
 from ..state import MANAGER_KEY, State, cluster_key_parts
 from .. import versions
@@ -225,7 +225,3 @@ def _mi355x_fields(ctx: Context) -> Dict:
             raise ConfigError(f"rccl_slim must be on or off. Found '{slim}'.")
         out["rccl_slim"] = slim
     return out
-
-
-def key_path_expanded(path: str) -> str:
-    return expand_home(path)

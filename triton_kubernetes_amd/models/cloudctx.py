@@ -1,6 +1,6 @@
 """Access to cloud listing clients from a workflow context."""
 
-from typing import Any, Optional
+from typing import Any
 
 from ..config.context import Context
 
@@ -18,10 +18,3 @@ def validation_enabled(ctx: Context) -> bool:
     if ctx.settings.is_set("cloud_validation"):
         return ctx.settings.get_bool("cloud_validation")
     return True
-
-
-def maybe_list(ctx: Context, fn, *args) -> Optional[Any]:
-    """Call a listing function unless validation is disabled."""
-    if not validation_enabled(ctx):
-        return None
-    return fn(*args)

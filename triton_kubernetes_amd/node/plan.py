@@ -38,7 +38,6 @@ Step catalogue (``action`` ids):
 ==================  ==============================================================
 """
 
-import json
 import shlex
 from dataclasses import asdict, dataclass, field
 from typing import Any, Dict, List, Optional
@@ -370,7 +369,3 @@ def parse_step_markers(output: str) -> Dict[str, Dict[str, Any]]:
             if len(parts) >= 4:
                 steps[parts[1]] = {"status": parts[2], "ms": int(parts[3]) if parts[3].isdigit() else 0}
     return steps
-
-
-def plan_json(plan: BootstrapPlan) -> str:
-    return json.dumps(plan.to_json())

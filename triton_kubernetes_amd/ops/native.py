@@ -142,13 +142,6 @@ def load(name: str, autobuild: bool = True) -> ctypes.CDLL:
         return lib
 
 
-def gpu_present() -> bool:
-    """True when the host exposes an AMD GPU (KFD device node or visible devices)."""
-    if os.environ.get("TK_FORCE_NO_GPU"):
-        return False
-    return os.path.exists("/dev/kfd")
-
-
 def executable(name: str) -> str:
     """The in-tree tool ``name``, built from this tree's sources (``ops/build.py`` stamps):
     a missing or stale tool is rebuilt when a compiler is there, else NativeUnavailable --

@@ -274,16 +274,6 @@ def preload_report() -> dict:
     return {"symbol": lib.tkr_preload_symbol().decode(), "how": lib.tkr_preload_how().decode()}
 
 
-def elf_kernel_symbol(path: str) -> str:
-    """The RCCL device-kernel handle the preload's scan finds in the library file at
-    ``path`` ("" when none): the same scanner, callable without a GPU."""
-    lib = _lib()
-    lib.tkr_elf_kernel_symbol.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int]
-    buf = ctypes.create_string_buffer(1024)
-    lib.tkr_elf_kernel_symbol(path.encode(), buf, len(buf))
-    return buf.value.decode()
-
-
 def preloads_running() -> int:
     from . import native
 
@@ -302,18 +292,9 @@ def exit_now(code: int = 0) -> None:
     os._exit(code)
 
 
-def set_async_teardown(on: bool) -> None:
-    """Run communicator teardown off the caller's critical path (see ``teardown`` in the HIP source)."""
-    _lib().tkr_set_async_teardown(1 if on else 0)
-
-
 def set_teardown_quiet_ms(ms: float) -> None:
     """Run queued communicator teardowns only after ``ms`` without gate activity."""
     _lib().tkr_set_teardown_quiet_ms(float(ms))
-
-
-def teardowns_pending() -> int:
-    return int(_lib().tkr_teardowns_pending())
 
 
 def drain() -> int:
@@ -331,12 +312,3 @@ def sweep_local(ndev: int, sizes: Sequence[int] = DEFAULT_SIZES, iters: int = 10
         raise RCCLError(_lib().tkr_last_error().decode())
     return SweepResult(ndev, dtype, list(sizes), list(t), list(alg), list(bus), [int(e) for e in err],
                        float(_lib().tkr_last_init_ms()))
-
-
-def min_busbw_threshold(world: int, fraction: float = 0.5) -> float:
-    """Gate for an intra-node sweep: a fraction of the per-GPU xGMI capacity
-    a ring can use (ring all-reduce drives 2 links per GPU at a time; RCCL's
-    multi-ring schedules can use more)."""
-    if world <= 1:
-        return 0.0
-    return fraction * 2 * XGMI_LINK_GBPS

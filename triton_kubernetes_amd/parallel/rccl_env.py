@@ -102,12 +102,6 @@ def default_rccl_env() -> Dict[str, str]:
     return dict(_DEFAULTS)
 
 
-def merged_env(overrides: Mapping[str, str] = ()) -> Dict[str, str]:
-    env = default_rccl_env()
-    env.update({str(k): str(v) for k, v in dict(overrides).items()})
-    return env
-
-
 def render_env_file(env: Mapping[str, str]) -> str:
     check_env(env)  # no writer can emit a setting, or a line, the file may not hold
     lines = ["# RCCL / HSA environment for MI355X (written by triton-kubernetes)"]

@@ -299,8 +299,3 @@ def sensitive_outputs(module_name: str) -> Tuple[str, ...]:
 
         _SENSITIVE = output_sensitivity()
     return tuple(n for n, s in _SENSITIVE.get(module_name, {}).items() if s)
-
-
-def output_is_sensitive(source: str, output: str) -> bool:
-    info = module_from_source(source)
-    return info is not None and output in sensitive_outputs(info.name)

@@ -53,22 +53,6 @@ def cgroup_cpu_dir() -> Optional[str]:
     return found
 
 
-def cpu_quota() -> Optional[float]:
-    """CPUs granted by the cgroup quota (None when unlimited / unknown)."""
-    d = cgroup_cpu_dir()
-    if not d:
-        return None
-    v2 = _read(os.path.join(d, "cpu.max"))
-    if v2:
-        q, _, p = v2.strip().partition(" ")
-        return None if q == "max" else int(q) / int(p or 100000)
-    q = _read(os.path.join(d, "cpu.cfs_quota_us"))
-    p = _read(os.path.join(d, "cpu.cfs_period_us"))
-    if q and p and int(q) > 0:
-        return int(q) / int(p)
-    return None
-
-
 def snapshot() -> Dict[str, float]:
     ru = resource.getrusage(resource.RUSAGE_SELF)
     out = {"cpu_s": ru.ru_utime + ru.ru_stime, "nvcsw": ru.ru_nvcsw, "nivcsw": ru.ru_nivcsw}
