@@ -146,3 +146,70 @@ def test_fp8_screen_passes_catches_fault_and_runs_at_rate():
     row, col = 777, 4095
     bad = gemm.screen(0, 4096, 4096, 4096, reps=1, inject=row * 4096 + col, dtype="fp8")
     assert not bad.ok and (bad.first_bad_row, bad.first_bad_column) == (row, col), bad
+
+
+# --- bf16 output (the vendor GEMM's output type), stream-ordered ----------------------------------
+
+
+@pytest.mark.parametrize("dtype", ["bf16", "fp8"])
+@pytest.mark.parametrize("m,n,k", [(256, 256, 128), (768, 512, 256), (1024, 1280, 2048)])
+def test_bf16_output_is_the_fp32_result_rounded_once(dtype, m, n, k):
+    """The bf16 epilogue (lane exchange, swizzled LDS image, 16-byte stores) against the fp32
+    output of the same kernel rounded to bf16 by torch: identical, element for element, so
+    any row, column or lane-pair mix-up of the transposition shows.  Asymmetric integer
+    data (exact in fp32) and random data both."""
+    import torch
+
+    from triton_kubernetes_amd.ops import gemm
+
+    el = torch.bfloat16 if dtype == "bf16" else torch.float8_e4m3fn
+    ia = (torch.arange(m * k, device="cuda").reshape(m, k) % 7 - 3).to(el)
+    ib = ((torch.arange(n * k, device="cuda").reshape(n, k) * 3 + torch.arange(n, device="cuda")[:, None]) % 5 - 2
+          ).to(el)
+    g = torch.Generator(device="cuda").manual_seed(m + 2 * n + k)
+    ra = (torch.rand((m, k), device="cuda", generator=g) * 2 - 1).to(el)
+    rb = (torch.rand((n, k), device="cuda", generator=g) * 2 - 1).to(el)
+    for a, b in ((ia, ib), (ra, rb)):
+        full = gemm.gemm_bt(a, b)
+        got = gemm.gemm_bt(a, b, out_dtype=torch.bfloat16)
+        assert got.dtype == torch.bfloat16 and got.shape == (m, n)
+        assert torch.equal(got, full.to(torch.bfloat16)), (got.float() - full).abs().max().item()
+    ref = ia.float() @ ib.float().T
+    assert torch.equal(gemm.gemm_bt(ia, ib, out_dtype=torch.bfloat16), ref.to(torch.bfloat16))
+
+
+def test_gemm_runs_on_torchs_current_stream():
+    """Queued on the caller's stream like a torch op: a GEMM on a side stream, whose inputs a
+    kernel on that same stream just wrote, sees them; nothing blocks the host."""
+    import torch
+
+    from triton_kubernetes_amd.ops import gemm
+
+    m = n = 512
+    k = 1024
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        a = torch.full((m, k), 0.5, device="cuda", dtype=torch.bfloat16)
+        b = torch.full((n, k), 0.25, device="cuda", dtype=torch.bfloat16)
+        a.mul_(2.0)  # queued on s just before the GEMM
+        out = gemm.gemm_bt(a, b, out_dtype=torch.bfloat16)
+    s.synchronize()
+    assert torch.equal(out, torch.full((m, n), 0.25 * k, device="cuda", dtype=torch.bfloat16))
+
+
+def test_bf16_output_refuses_what_it_cannot_write():
+    import torch
+
+    from triton_kubernetes_amd.ops import gemm
+
+    a = torch.zeros((256, 64), device="cuda", dtype=torch.bfloat16)
+    with pytest.raises(gemm.GemmError):
+        gemm.gemm_bt(a, a, out_dtype=torch.float16)
+    with pytest.raises(gemm.GemmError):  # 2-byte offset: not 16-byte aligned
+        gemm.gemm_bt(a, a, out=torch.empty(256 * 256 + 1, device="cuda", dtype=torch.bfloat16)[1:].view(256, 256))
+    try:
+        gemm.set_schedule("single-barrier")
+        with pytest.raises(gemm.GemmError):
+            gemm.gemm_bt(a, a, out_dtype=torch.bfloat16)
+    finally:
+        gemm.set_schedule("staggered")

@@ -506,7 +506,55 @@ __global__ __launch_bounds__(THREADS) void k_gemm8(const void* __restrict__ A, c
 
   // accumulator element (mh, nh, i, j, e): row = mh*128 + wr*64 + i*16 + fq*4 + e,
   //                                         col = nh*128 + wc*32 + j*16 + fr
-  if constexpr (MODE == 0) {
+  if constexpr (MODE == 2) {
+    // bf16 C (the vendor GEMM's output type) through a wave-private 16 KiB LDS image, so
+    // the global stores are 16 bytes per lane (a store tail of 4-byte stores is issue-bound).
+    // A lane holds rows fq*4 + e of column fr; it swaps two values with its neighbour fr ^ 1
+    // (DPP quad_perm [1,0,3,2]) so each lane has two bf16 pairs: even lanes rows e = 0, 1 at
+    // columns fr, fr + 1, odd lanes rows e = 2, 3 at fr - 1, fr.  The image is 4 blocks (mh,
+    // nh) of [64 rows][64 B]; dword column bit 3 is XORed with row bit 1, which leaves the
+    // ds_write_b32s 2-way (free) and the ds_read_b128s conflict-free.
+    barrier();  // every wave is past its last fragment read of the main loop
+    char* img = smem + wid * (4 * 64 * 64);
+    const int odd = fr & 1;
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < 2; ++j) {
+            const f32x4 v = acc[mh][nh][i][j];
+            const float s0 = odd ? v[0] : v[2], s1 = odd ? v[1] : v[3];
+            const float r0 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s0),
+                                                                                   0xB1, 0xF, 0xF, false));
+            const float r1 = __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, s1),
+                                                                                   0xB1, 0xF, 0xF, false));
+            typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2;
+            const bf16x2 p0 = {(__bf16)(odd ? r0 : v[0]), (__bf16)(odd ? v[2] : r0)};
+            const bf16x2 p1 = {(__bf16)(odd ? r1 : v[1]), (__bf16)(odd ? v[3] : r1)};
+            const int row = i * 16 + fq * 4 + odd * 2, cdw = j * 8 + (fr >> 1);
+            uint32_t* blk = reinterpret_cast<uint32_t*>(img + (mh * 2 + nh) * 4096);
+            blk[row * 16 + (cdw ^ (((row >> 1) & 1) << 3))] = __builtin_bit_cast(uint32_t, p0);
+            blk[(row + 1) * 16 + (cdw ^ ((((row + 1) >> 1) & 1) << 3))] = __builtin_bit_cast(uint32_t, p1);
+          }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    char* cb = reinterpret_cast<char*>(C);
+#pragma unroll
+    for (int mh = 0; mh < 2; ++mh)
+#pragma unroll
+      for (int nh = 0; nh < 2; ++nh)
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int r = q * 16 + (lane >> 2), c = lane & 3;
+          const u32x4 d =
+              *reinterpret_cast<const u32x4*>(img + (mh * 2 + nh) * 4096 + r * 64 + ((c ^ (((r >> 1) & 1) << 1)) * 16));
+          const size_t grow = (size_t)row0 + mh * 128 + wr * 64 + r;
+          const int gcol = col0 + nh * 128 + wc * 32 + c * 8;
+          *reinterpret_cast<u32x4*>(cb + (grow * N + gcol) * 2) = d;
+        }
+  } else if constexpr (MODE == 0) {
 #pragma unroll
     for (int mh = 0; mh < 2; ++mh)
 #pragma unroll
@@ -699,16 +747,20 @@ extern "C" int tkg_set_schedule(int s) {
   return schedule();
 }
 
+// mode 0: fp32 C, 1: screen (checksums only), 2: bf16 C (staggered schedule only)
 static hipError_t launch_gemm(int mode, int esize, const void* A, const void* B, float* C, float* colpart,
                               float* rowpart, int M, int N, int K, long long inject, hipStream_t s) {
   const int grid = (M / BM) * (N / BN);
   if (esize == 1) {  // fp8: staggered schedule only
     if (mode == 0) k_gemm8<0, 1><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+    else if (mode == 2) k_gemm8<2, 1><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
     else k_gemm8<1, 1><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
   } else if (schedule() == 1) {
     if (mode == 0) k_gemm8<0, 2><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
+    else if (mode == 2) k_gemm8<2, 2><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
     else k_gemm8<1, 2><<<grid, THREADS, p8::LDS, s>>>(A, B, C, colpart, rowpart, M, N, K, inject);
   } else {
+    if (mode == 2) return hipErrorInvalidValue;  // the single-barrier loop (A/B only) writes fp32
     const __bf16 *a = static_cast<const __bf16*>(A), *b = static_cast<const __bf16*>(B);
     if (mode == 0) k_gemm_bt<0><<<grid, THREADS, LDS_BYTES, s>>>(a, b, C, colpart, rowpart, M, N, K, inject);
     else k_gemm_bt<1><<<grid, THREADS, LDS_BYTES, s>>>(a, b, C, colpart, rowpart, M, N, K, inject);
@@ -720,7 +772,8 @@ static hipError_t set_lds_limit() {
   static hipError_t once = [] {
     const void* fns[] = {reinterpret_cast<const void*>(&k_gemm_bt<0>), reinterpret_cast<const void*>(&k_gemm_bt<1>),
                          reinterpret_cast<const void*>(&k_gemm8<0, 2>), reinterpret_cast<const void*>(&k_gemm8<1, 2>),
-                         reinterpret_cast<const void*>(&k_gemm8<0, 1>), reinterpret_cast<const void*>(&k_gemm8<1, 1>)};
+                         reinterpret_cast<const void*>(&k_gemm8<0, 1>), reinterpret_cast<const void*>(&k_gemm8<1, 1>),
+                         reinterpret_cast<const void*>(&k_gemm8<2, 2>), reinterpret_cast<const void*>(&k_gemm8<2, 1>)};
     for (const void* f : fns) {
       hipError_t e = hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 128 * 1024);
       if (e != hipSuccess) return e;
@@ -730,23 +783,34 @@ static hipError_t set_lds_limit() {
   return once;
 }
 
-// C[M][N] (fp32) = A[M][K] * B[N][K]^T for device pointers on `dev` (tests: torch tensors).
-static int gemm_bt(int dev, int esize, const void* A, const void* B, void* C, int M, int N, int K) {
+// Stream-ordered C = A * B^T, no host synchronisation (torch tensors on torch's stream: one
+// HIP runtime, see ops/native.py:require_torch_first).  esize 2: bf16 operands, 1: fp8
+// e4m3; out_bf16: C is bf16 (the vendor GEMM's output type), else fp32.  C must be 16-byte
+// aligned for bf16 output.  Returns 0, or -1 / a HIP error with tkg_last_error() set.
+extern "C" int tkg_gemm(int dev, int esize, const void* A, const void* B, void* C, int M, int N, int K, int out_bf16,
+                        void* stream) {
+  if (esize != 1 && esize != 2) {
+    snprintf(g_err, sizeof(g_err), "element size %d (1: fp8 e4m3, 2: bf16)", esize);
+    return -1;
+  }
   if (check_shape(M, N, K, esize)) return -1;
+  if (out_bf16 && (reinterpret_cast<uintptr_t>(C) & 15)) {
+    snprintf(g_err, sizeof(g_err), "bf16 C must be 16-byte aligned");
+    return -1;
+  }
+  if (out_bf16 && esize == 2 && schedule() != 1) {
+    snprintf(g_err, sizeof(g_err), "bf16 output needs the staggered schedule");
+    return -1;
+  }
+  int prev = 0;
+  CHECK(hipGetDevice(&prev));
   CHECK(hipSetDevice(dev));
   CHECK(set_lds_limit());
-  CHECK(launch_gemm(0, esize, A, B, (float*)C, nullptr, nullptr, M, N, K, -1, 0));
-  CHECK(hipDeviceSynchronize());
+  const hipError_t e = launch_gemm(out_bf16 ? 2 : 0, esize, A, B, static_cast<float*>(C), nullptr, nullptr, M, N, K,
+                                   -1, static_cast<hipStream_t>(stream));
+  CHECK(hipSetDevice(prev));
+  CHECK(e);
   return 0;
-}
-
-extern "C" int tkg_gemm_bt(int dev, const void* A, const void* B, void* C, int M, int N, int K) {
-  return gemm_bt(dev, 2, A, B, C, M, N, K);
-}
-
-// fp8 e4m3 A[M][K], B[N][K] (bytes) -> C fp32
-extern "C" int tkg_gemm_fp8_bt(int dev, const void* A, const void* B, void* C, int M, int N, int K) {
-  return gemm_bt(dev, 1, A, B, C, M, N, K);
 }
 
 // The screen: random A[M][K], B[N][K]; `reps` timed checksum-mode GEMMs (best time), then the

@@ -3,7 +3,9 @@
 ``screen(dev)`` runs an LDS-tiled bf16 MFMA GEMM on random operands and checks it with
 row/column checksums (algorithm-based fault tolerance); the burn-in fails a GPU whose
 GEMM disagrees with the independently computed checksums.  ``gemm_bt`` exposes the same
-kernel with a full fp32 C output for numerics tests against a PyTorch reference.
+kernel with a full C output (fp32, or bf16 as the vendor GEMM writes), stream-ordered on
+torch's current stream, for numerics tests against a PyTorch reference and for the
+comparison with hipBLASLt (``scripts/gemm_vs_lib.py``).
 """
 
 import ctypes
@@ -28,13 +30,12 @@ class GemmError(RuntimeError):
 def _lib():
     lib = load("libtk_gemm.so")
     lib.tkg_last_error.restype = ctypes.c_char_p
-    lib.tkg_gemm_bt.argtypes = [ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
-                                ctypes.c_int, ctypes.c_int, ctypes.c_int]
-    lib.tkg_gemm_fp8_bt.argtypes = lib.tkg_gemm_bt.argtypes
     lib.tkg_screen.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                ctypes.c_longlong, ctypes.POINTER(ctypes.c_double)]
     lib.tkg_screen_fp8.argtypes = lib.tkg_screen.argtypes
     lib.tkg_set_schedule.argtypes = [ctypes.c_int]
+    lib.tkg_gemm.argtypes = [ctypes.c_int, ctypes.c_int, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                             ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
     return lib
 
 
@@ -57,9 +58,11 @@ def check_shape(m: int, n: int, k: int, dtype: str = "bf16") -> None:
         raise GemmError(f"shape {m}x{n}x{k}: M and N must be multiples of {TILE_M}, K of {tk}")
 
 
-def gemm_bt(a, b, out=None):
-    """``out = a @ b.T`` in fp32 for CUDA tensors ``a [M,K]``, ``b [N,K]`` (contiguous), both
-    bf16 or both fp8 e4m3 (``torch.float8_e4m3fn``: the block-scaled MFMA with unit scales)."""
+def gemm_bt(a, b, out=None, out_dtype=None):
+    """``out = a @ b.T`` for CUDA tensors ``a [M,K]``, ``b [N,K]`` (contiguous), both bf16 or
+    both fp8 e4m3 (``torch.float8_e4m3fn``: the block-scaled MFMA with unit scales).  ``out``
+    (or ``out_dtype``) is fp32 (default) or bf16.  The kernel is queued on torch's current
+    stream of ``a``'s device, like a torch op: nothing waits for it here."""
     import torch
 
     from .native import require_torch_first
@@ -68,18 +71,23 @@ def gemm_bt(a, b, out=None):
     fp8 = getattr(torch, "float8_e4m3fn", None)
     if a.dtype != b.dtype or a.dtype not in (torch.bfloat16, fp8) or not (a.is_cuda and b.is_cuda):
         raise GemmError("gemm_bt wants two bf16 or two float8_e4m3fn CUDA tensors")
-    if not (a.is_contiguous() and b.is_contiguous()) or a.shape[1] != b.shape[1]:
-        raise GemmError("gemm_bt wants contiguous a [M,K] and b [N,K]")
+    if not (a.is_contiguous() and b.is_contiguous()) or a.shape[1] != b.shape[1] or a.device != b.device:
+        raise GemmError("gemm_bt wants contiguous a [M,K] and b [N,K] on one device")
     m, k = a.shape
     n = b.shape[0]
     dtype = "fp8" if a.dtype == fp8 else "bf16"
     check_shape(m, n, k, dtype)
+    want = out.dtype if out is not None else (out_dtype or torch.float32)
+    if want not in (torch.float32, torch.bfloat16):
+        raise GemmError("out must be fp32 or bf16")
     if out is None:
-        out = torch.empty((m, n), dtype=torch.float32, device=a.device)
-    elif out.shape != (m, n) or out.dtype != torch.float32 or not out.is_contiguous():
-        raise GemmError("out must be a contiguous fp32 [M,N] tensor")
-    fn = _lib().tkg_gemm_fp8_bt if dtype == "fp8" else _lib().tkg_gemm_bt
-    rc = fn(a.device.index or 0, a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k)
+        out = torch.empty((m, n), dtype=want, device=a.device)
+    elif out.shape != (m, n) or not out.is_contiguous() or out.device != a.device:
+        raise GemmError("out must be a contiguous [M,N] tensor on a's device")
+    dev = a.device.index if a.device.index is not None else torch.cuda.current_device()
+    stream = torch.cuda.current_stream(a.device).cuda_stream
+    rc = _lib().tkg_gemm(dev, 1 if dtype == "fp8" else 2, a.data_ptr(), b.data_ptr(), out.data_ptr(), m, n, k,
+                         1 if want == torch.bfloat16 else 0, stream)
     if rc != 0:
         raise GemmError(_lib().tkg_last_error().decode())
     return out
