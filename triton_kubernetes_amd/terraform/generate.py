@@ -926,7 +926,10 @@ locals {{
     # T7 aws-rancher-k8s
     mods.append(Module("aws-rancher-k8s", ["aws", "external"], CLUSTER_BASE + AWS_CREDS + [
         Var("aws_vpc_cidr", "10.0.0.0/16"), Var("aws_subnet_cidr", "10.0.2.0/24"),
-        Var("aws_public_key_path", "~/.ssh/id_rsa.pub"), Var("aws_key_name", None)],
+        Var("aws_public_key_path", "~/.ssh/id_rsa.pub"), Var("aws_key_name", None),
+        # declared by the reference's module too (never read there): a configuration that
+        # sets it on the cluster stays valid; every host module takes its own AMI
+        Var("aws_ami_id", "", "Accepted for compatibility; the hosts' AMI is set per node.")],
         _cluster_data() + f'''
 resource "aws_vpc" "default" {{
   cidr_block           = var.aws_vpc_cidr

@@ -165,3 +165,9 @@ variable "aws_key_name" {
   description = "AWS key name."
   type        = string
 }
+
+variable "aws_ami_id" {
+  description = "Accepted for compatibility; the hosts' AMI is set per node."
+  type        = string
+  default     = ""
+}
