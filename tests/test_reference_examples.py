@@ -42,7 +42,7 @@ MANAGER_STEPS = [
     ({"master_triton_machine_package": "k4-highcpu-kvm-7.75G"}, None),
 ]
 CLUSTER_STEPS = [
-    ({}, "v1.8.10-rancher1-1"),
+    ({}, "Kubernetes version 'v1.8.10-rancher1-1' is not an RKE1 release offered by Rancher"),
     ({"k8s_version": versions.DEFAULT_K8S_VERSION}, "has 1.75 GiB of memory"),
     ({"nodes": lambda nodes: [dict(n, triton_machine_package="k4-highcpu-kvm-7.75G") for n in nodes]}, None),
 ]
