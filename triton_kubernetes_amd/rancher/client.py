@@ -412,7 +412,3 @@ class RancherClient:
         resp = self.http.request("POST", f"/k8s/clusters/{cluster_id}/api/v1/namespaces/{namespace}/pods/{name}/eviction",
                                  json_body=body, ok=(200, 201, 404, 429))
         return resp.status
-
-    def kubeconfig(self, cluster_id: str) -> str:
-        data = self.http.post_json(f"/v3/clusters/{cluster_id}?action=generateKubeconfig", {})
-        return data.get("config", "")

@@ -305,10 +305,6 @@ class K8sCoreApi:
         return {"desiredNumberScheduled": len(nodes), "currentNumberScheduled": len(nodes),
                 "numberReady": len(ready), "numberAvailable": len(ready)}
 
-    def device_plugin_applied(self, cluster_id: str) -> bool:
-        with self.state.mu:
-            return any(self._is_gpu_plugin(ds) for _, ds in self._daemonsets(cluster_id))
-
     def k8s_nodes(self, cluster_id: str) -> List[Dict[str, Any]]:
         self._refresh()
         st = self.state

@@ -97,14 +97,6 @@ class ClusterGate:
         return cls(transport, members_from(urls, ndevs), sizes, iters)
 
     # --- pipelined init ---------------------------------------------------------------------------------
-    def _post_all(self, path: str, body_for) -> List[Dict[str, Any]]:
-        def one(m: GateMember) -> Dict[str, Any]:
-            return self.transport.post(m.host, path, body_for(m))
-
-        if len(self.members) == 1:
-            return [one(self.members[0])]
-        return list(shared_pool("tk-gate", 64).map(one, self.members))
-
     def _prepare(self) -> None:
         try:
             with span("gate.prepare", world=self.world):

@@ -135,13 +135,6 @@ class PrivateKey:
     def fingerprint_md5(self) -> str:
         return ":".join(f"{b:02x}" for b in hashlib.md5(self.public_blob).digest())
 
-    def fingerprint_sha256(self) -> str:
-        return "SHA256:" + base64.b64encode(hashlib.sha256(self.public_blob).digest()).decode().rstrip("=")
-
-    def authorized_key(self, comment: str = "") -> str:
-        line = f"{self.ssh_type} {base64.b64encode(self.public_blob).decode()}"
-        return f"{line} {comment}".rstrip()
-
     # --- signing -----------------------------------------------------------------
     def sign(self, data: bytes, hash_name: str = "sha256") -> bytes:
         if self.kind == "rsa":

@@ -87,10 +87,6 @@ class Tracer:
             "spans": [dict(asdict(s), duration=s.duration, rel_start=s.start - self.t0) for s in spans],
         }
 
-    def dump_json(self, path: str) -> None:
-        with open(path, "w", encoding="utf-8") as fh:
-            json.dump(self.report(), fh, indent=2)
-
     def chrome_events(self) -> List[Dict[str, Any]]:
         pid = os.getpid()
         with self._mu:
