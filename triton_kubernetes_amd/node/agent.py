@@ -72,6 +72,7 @@ MODES = ("sim", "exec")
 
 @dataclass
 class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
+    HISTORY_KEEP = 32  # plan results kept (history[-1] feeds /metrics); a daemon runs many
     name: str = "node"
     mode: str = "sim"
     devices: List[int] = field(default_factory=list)
@@ -214,6 +215,7 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
                "steps": [r.__dict__ for r in results], "labels": ctx["labels"], "capacity": ctx["capacity"],
                "taints": ctx["taints"]}
         self.history.append(doc)
+        del self.history[:-self.HISTORY_KEEP]  # a daemon's record of its last plans, not all
         self._touch()
         return doc
 

@@ -34,12 +34,28 @@ class Span:
 
 
 class Tracer:
-    def __init__(self):
+    """``max_spans``: the most recent spans kept.  A CLI run records a few hundred, but a
+    node agent is a daemon that records spans for every request it serves, for months; the
+    oldest go first (``dropped`` counts them)."""
+
+    MAX_SPANS = 20000
+
+    def __init__(self, max_spans: int = MAX_SPANS):
         self._mu = threading.Lock()
         self._local = threading.local()
         self.spans: List[Span] = []
         self.t0 = time.time()
         self.enabled = True
+        self.max_spans = max_spans
+        self.dropped = 0
+
+    def _keep(self, sp: Span) -> None:
+        """Append under ``_mu``; past 1.25 x the bound, trim to it (amortised)."""
+        self.spans.append(sp)
+        if len(self.spans) > self.max_spans + self.max_spans // 4:
+            cut = len(self.spans) - self.max_spans
+            del self.spans[:cut]
+            self.dropped += cut
 
     def _stack(self) -> List[Span]:
         st = getattr(self._local, "stack", None)
@@ -63,16 +79,17 @@ class Tracer:
             stack.pop()
             if self.enabled:
                 with self._mu:
-                    self.spans.append(sp)
+                    self._keep(sp)
 
     def mark(self, name: str, **attrs: Any) -> None:
         now = time.time()
         with self._mu:
-            self.spans.append(Span(name, now, now, threading.current_thread().name, None, dict(attrs)))
+            self._keep(Span(name, now, now, threading.current_thread().name, None, dict(attrs)))
 
     def reset(self) -> None:
         with self._mu:
             self.spans.clear()
+            self.dropped = 0
             self.t0 = time.time()
 
     def find(self, name: str) -> List[Span]:
@@ -85,6 +102,7 @@ class Tracer:
         return {
             "t0": self.t0,
             "spans": [dict(asdict(s), duration=s.duration, rel_start=s.start - self.t0) for s in spans],
+            "dropped": self.dropped,
         }
 
     def chrome_events(self) -> List[Dict[str, Any]]:
