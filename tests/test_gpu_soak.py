@@ -13,7 +13,7 @@ import pytest
 
 pytestmark = pytest.mark.gpu
 
-ROUNDS = 16
+ROUNDS = int(os.environ.get("TK_SOAK_ROUNDS", "16"))
 WARM = 4
 
 
