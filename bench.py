@@ -649,6 +649,8 @@ def main() -> int:
                 out["rccl"] = {k: round(max(float(p.get(k, 0.0)) for p in phases), 3)
                                for k in ("init_total", "init_wait", "alloc", "sweep", "footprint_mib",
                                          "footprint_total_mib", "footprint_kind")}
+                # 1 when every agent kept its measurement as a footprint (node/agent_gate.py)
+                out["rccl"]["footprint_kept"] = min(float(p.get("footprint_kept", 0.0)) for p in phases)
             # an init that ran out of HBM beside the held burn-in spans and was retried
             retried = [r.get("gate_retry") for r in ranks if r.get("gate_retry")]
             if retried or (rep.rccl or {}).get("retry"):
@@ -913,9 +915,10 @@ def main() -> int:
             # the gate communicator's device memory per GPU (MiB, max over agents, last timed step):
             # what the burn-in span's headroom must leave (node/agent_gate.py:span_headroom).
             # footprint_kind 1: the agent's own VRAM; 2: the device's used-memory delta, which
-            # in a cold step also counts the burn-in child allocating its span meanwhile
+            # in a cold step also counts the burn-in child allocating its span meanwhile: then
+            # footprint_kept is 0 and the node did not take it as a footprint
             "rccl_footprint_mib": next(({k: r["rccl"].get(k) for k in ("footprint_mib", "footprint_total_mib",
-                                                                       "footprint_kind")}
+                                                                       "footprint_kind", "footprint_kept")}
                                         for r in reversed(results) if r.get("rccl")), None),
             # timed steps whose gate init ran out of HBM and was retried after the spans' release
             "gate_retry_steps": [r["step"] for r in results if r.get("gate_retry")],

@@ -126,6 +126,7 @@ def test_whole_node_gate_retries_once_after_releasing_held_spans(oom_node):
         assert agent.span_headroom(8) == want > floor
         assert probe.SPAN_HEADROOM == want
         assert rank["phase_ms"]["footprint_total_mib"] == FOOTPRINT_MIB
+        assert rank["phase_ms"]["footprint_kept"] == 1.0  # the answer says it counted
     finally:
         agent.stop()
     # a later agent on this node starts with the measured headroom
@@ -215,6 +216,7 @@ def test_an_implausible_footprint_never_becomes_the_headroom(oom_node, monkeypat
     try:
         res = ClusterGate(AgentTransport(token=TOKEN), members_from([url], [8]), SIZES, timeout_s=30).run()
         assert res["ok"], res
+        assert res["ranks"][0]["phase_ms"]["footprint_kept"] == 0.0
         assert not os.path.exists(agent.path(agent.FOOTPRINT_FILE))
         assert agent.span_headroom(8) == (4 << 30) + 7 * (512 << 20)
     finally:
@@ -236,11 +238,12 @@ def test_a_device_wide_footprint_is_kept_only_from_a_quiet_window(oom_node, monk
         free.write_text(str(RELEASED))
         res = ClusterGate(AgentTransport(token=TOKEN), members_from([url], [8]), SIZES, timeout_s=30).run()
         assert res["ok"] and res["ranks"][0]["phase_ms"]["footprint_kind"] == 2.0
+        assert res["ranks"][0]["phase_ms"]["footprint_kept"] == 0.0
         assert not os.path.exists(agent.path(agent.FOOTPRINT_FILE))
         agent._links_pending = False
         probe.wait_frees()  # the child released and exited: a quiet window now
         res = ClusterGate(AgentTransport(token=TOKEN), members_from([url], [8]), SIZES, timeout_s=30).run()
-        assert res["ok"]
+        assert res["ok"] and res["ranks"][0]["phase_ms"]["footprint_kept"] == 1.0
         assert json.loads(open(agent.path(agent.FOOTPRINT_FILE)).read()) == {"8": 900.0}
     finally:
         agent.stop()

@@ -177,23 +177,25 @@ class AgentGateMixin:
                 raise rccl.RCCLError(f"{exc} {rccl.OOM_RETRIED_MARK}") from exc
         return res, {"gate_retry": "oom", "first_error": first_error[:400], "spans_released_ms": released_ms}
 
-    def _note_gate_footprint(self, ndev: int, phase_ms: Dict[str, float], window: Any = None) -> None:
+    def _note_gate_footprint(self, ndev: int, phase_ms: Dict[str, float], window: Any = None) -> bool:
         """Keep the largest per-GPU footprint a gate communicator over ``ndev`` of this node's
         GPUs measured (``footprint_total_mib``: the communicator and its sweep buffers), and
         size the burn-in span's headroom from it (never below the constant floor).
 
         A device-wide measurement (``footprint_kind`` 2: no per-process accounting here)
         counts everything allocated on the GPU meanwhile; it is kept only when none of this
-        agent's burn-ins started, ran or was alive from the init's start (``window``) to now."""
+        agent's burn-ins started, ran or was alive from the init's start (``window``) to now.
+        Returns whether it was kept (``footprint_kept`` in ``phase_ms``)."""
         from ..ops import probe
 
         mib = float(phase_ms.get("footprint_total_mib") or 0.0)
-        if mib <= 0 or mib > self.FOOTPRINT_MAX_MIB:
-            return  # not measured here (-1), or not a communicator's (a bound, never a headroom)
-        if int(phase_ms.get("footprint_kind") or 0) != 1:
-            if window is None or window[1] != 0 or probe.activity() != window:
-                return
-        self._keep_footprint(str(int(ndev)), mib)
+        kept = 0.0 < mib <= self.FOOTPRINT_MAX_MIB  # else not measured here (-1), or not a communicator's
+        if kept and int(phase_ms.get("footprint_kind") or 0) != 1:
+            kept = window is not None and window[1] == 0 and probe.activity() == window
+        phase_ms["footprint_kept"] = 1.0 if kept else 0.0  # the answer says whether it counted
+        if kept:
+            self._keep_footprint(str(int(ndev)), mib)
+        return kept
 
     def _note_gate_oom(self, ndev: int) -> None:
         """An init ran out of HBM beside held spans: the next burn-in of this node leaves
