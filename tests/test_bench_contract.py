@@ -127,7 +127,7 @@ def test_settle_times_out_on_a_card_that_keeps_falling(tmp_path):
     t = threading.Thread(target=fall)
     t.start()
     try:
-        got = hbm.settle(str(tmp_path), quiet_s=0.2, poll_s=0.005, timeout_s=0.5)
+        got = hbm.settle(str(tmp_path), quiet_s=0.4, poll_s=0.005, timeout_s=1.0)
     finally:
         stop.set()
         t.join()
