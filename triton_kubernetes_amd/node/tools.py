@@ -37,7 +37,7 @@ from ..ops.build import CSRC
 # tool -> the shipped sources it is built from (basenames under the module's files/src)
 TOOL_SOURCES: Dict[str, List[str]] = {
     "amdgpu-topo-labeller": ["tk_topo.cpp"],
-    "gpu-burnin": ["tk_gpu_probe.hip", "tk_gemm_screen.hip"],
+    "gpu-burnin": ["tk_gpu_probe.hip", "tk_gemm_screen.hip", "tk_link_verdict.h"],
     "rccl-ready": ["tk_rccl_probe.hip", "tk_rccl_verify.h", "tk_rccl_group.h", "tk_elf_scan.h"],
 }
 PREBUILT_DIR = "/opt/triton-kubernetes/prebuilt"
@@ -122,7 +122,7 @@ tk_node_tools() { # <tools dir> <sources dir> <prebuilt dir> <rocm dir>
   sudo mkdir -p "$T/.stamps" || return 1
   tk_node_tool "$T" "$S" "$P" amdgpu-topo-labeller "tk_topo.cpp" g++ -O2 -std=c++17 -DTK_TOPO_MAIN -DTK_TOPO_AMDSMI -I$R/include $S/tk_topo.cpp -L$R/lib -lamd_smi -Wl,-rpath,$R/lib &
   pids="$pids $!"
-  tk_node_tool "$T" "$S" "$P" gpu-burnin "tk_gpu_probe.hip tk_gemm_screen.hip" $R/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip -Wl,-rpath,$R/lib &
+  tk_node_tool "$T" "$S" "$P" gpu-burnin "tk_gpu_probe.hip tk_gemm_screen.hip tk_link_verdict.h" $R/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -mllvm -amdgpu-mfma-vgpr-form -DTK_PROBE_MAIN $S/tk_gpu_probe.hip $S/tk_gemm_screen.hip -Wl,-rpath,$R/lib &
   pids="$pids $!"
   tk_node_tool "$T" "$S" "$P" rccl-ready "tk_rccl_probe.hip tk_rccl_verify.h tk_rccl_group.h tk_elf_scan.h" $R/bin/hipcc -O3 -std=c++17 --offload-arch=gfx950 -DTK_RCCL_MAIN $S/tk_rccl_probe.hip -L$R/lib -lrccl -Wl,-rpath,$R/lib &
   pids="$pids $!"

@@ -123,11 +123,12 @@ def targets() -> List[Target]:
     stub = os.path.join(CSRC, "tk_rccl_stub.cpp")
     rccl_h = [os.path.join(CSRC, "tk_rccl_group.h"), os.path.join(CSRC, "tk_rccl_verify.h"),
               os.path.join(CSRC, "tk_elf_scan.h")]
+    link_h = os.path.join(CSRC, "tk_link_verdict.h")
     out = lambda n: os.path.join(LIB, n)  # noqa: E731
     return [
-        Target("libtk_gpu_probe.so", [probe],
+        Target("libtk_gpu_probe.so", [probe, link_h],
                [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-fPIC", "-shared", probe, "-o", out("libtk_gpu_probe.so"), *RPATH]),
-        Target("gpu-burnin", [probe, gemm],
+        Target("gpu-burnin", [probe, gemm, link_h],
                [hipcc, *HIP_FLAGS, *MFMA_FLAGS, "-DTK_PROBE_MAIN", probe, gemm, "-o", out("gpu-burnin"), *RPATH]),
         Target("libtk_gemm.so", [gemm],
                [hipcc, *HIP_FLAGS, "-fPIC", "-shared", gemm, "-o", out("libtk_gemm.so"), *RPATH]),

@@ -48,6 +48,8 @@
 #include <algorithm>
 #include <vector>
 
+#include "tk_link_verdict.h"
+
 typedef __attribute__((ext_vector_type(8))) __bf16 bf16x8;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
 typedef __attribute__((ext_vector_type(8))) int i32x8;
@@ -1302,7 +1304,7 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
     if (labels_path) { FILE* f = fopen(labels_path, "w"); if (f) fclose(f); }
     return 0;
   }
-  std::vector<double> vals, mat(n * n, 0.0), derr(n * n, 0.0);
+  std::vector<double> mat(n * n, 0.0), derr(n * n, 0.0);
   std::vector<int> devs(n), acc(n * n, 0);
   for (int i = 0; i < n; ++i) devs[i] = i;
   if (tkp_link_matrix_check(devs.data(), n, 64ull << 20, 3, mode, mat.data(), acc.data(), derr.data()) != 0) {
@@ -1313,23 +1315,8 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
   // burn-in's rule for throughput gates, node/labels.py:best_link_verdict); a pair that
   // delivered wrong data, or could not be measured, is never retried away
   int remeasured = 0;
-  for (; remeasured < 2; ++remeasured) {
-    std::vector<double> ok_vals;
-    bool unmeasured = false, bad_data = false;
-    for (int i = 0; i < n; ++i)
-      for (int j = 0; j < n; ++j) {
-        if (i == j) continue;
-        if (mat[i * n + j] < 0.0 || !acc[i * n + j]) unmeasured = true;
-        else ok_vals.push_back(mat[i * n + j]);
-        bad_data = bad_data || derr[i * n + j] > 0.0;
-      }
-    if (unmeasured || bad_data || ok_vals.empty()) break;
-    std::sort(ok_vals.begin(), ok_vals.end());
-    const size_t k = ok_vals.size();
-    const double med = k % 2 ? ok_vals[k / 2] : 0.5 * (ok_vals[k / 2 - 1] + ok_vals[k / 2]);
-    bool slow = false;
-    for (double v : ok_vals) slow = slow || v < min_frac * med || v < min_gbps;
-    if (!slow) break;
+  for (; remeasured < 2 && tk_link_slow_only(n, mat.data(), acc.data(), derr.data(), min_frac, min_gbps);
+       ++remeasured) {
     std::vector<double> again(n * n, 0.0), derr2(n * n, 0.0);
     std::vector<int> acc2(n * n, 0);
     if (tkp_link_matrix_check(devs.data(), n, 64ull << 20, 3, mode, again.data(), acc2.data(), derr2.data()) != 0)
@@ -1339,50 +1326,33 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
       derr[x] += derr2[x];
     }
   }
-  int errors = 0, no_peer = 0;
   printf("{\"pairs\":{");
   bool first = true;
   for (int i = 0; i < n; ++i)
     for (int j = 0; j < n; ++j) {
-      if (i == j) continue;
-      if (mat[i * n + j] < 0.0) { ++errors; continue; }
-      if (!acc[i * n + j]) ++no_peer;
-      vals.push_back(mat[i * n + j]);
+      if (i == j || mat[i * n + j] < 0.0) continue;
       printf("%s\"%d-%d\":%.1f", first ? "" : ",", i, j, mat[i * n + j]);
       first = false;
     }
-  std::vector<double> sorted = vals;
-  std::sort(sorted.begin(), sorted.end());
-  const size_t m = sorted.size();
-  const double median = m == 0 ? 0.0 : (m % 2 ? sorted[m / 2] : 0.5 * (sorted[m / 2 - 1] + sorted[m / 2]));
-  // a link is degraded below min_frac of the node's median OR below the absolute floor
-  // (a uniformly slow fabric has a healthy-looking median)
-  int degraded = 0, below_floor = 0, corrupt = 0;
-  for (int i = 0; i < n; ++i)
-    for (int j = 0; j < n; ++j) {
-      if (i == j || mat[i * n + j] < 0.0) continue;
-      const double v = mat[i * n + j];
-      const bool bad_data = derr[i * n + j] > 0.0;  // delivered data differed from what was sent
-      degraded += v < min_frac * median || v < min_gbps || bad_data;
-      below_floor += v < min_gbps;
-      corrupt += bad_data;
-    }
-  const char* status = (errors || no_peer || m == 0) ? "error" : (degraded ? "degraded" : "passed");
+  const TkLinkVerdict v = tk_link_verdict(n, mat.data(), acc.data(), derr.data(), min_frac, min_gbps);
+  const char* status = v.status;
   printf("},\"method\":\"%s\",\"min_gbps\":%.1f,\"median_gbps\":%.1f,\"floor_gbps\":%.1f,\"degraded\":%d,"
          "\"below_floor\":%d,\"corrupt\":%d,\"errors\":%d,\"no_peer_access\":%d,\"remeasured\":%d,"
          "\"status\":\"%s\"}\n",
-         mode ? "kernel-read" : "sdma-copy", m ? sorted[0] : 0.0, median, min_gbps, degraded, below_floor, corrupt,
-         errors, no_peer, remeasured, status);
+         mode ? "kernel-read" : "sdma-copy", v.min_gbps, v.median_gbps, min_gbps, v.degraded, v.below_floor,
+         v.corrupt, v.errors, v.no_peer, remeasured, status);
+  const size_t m = (size_t)v.measured;
+  const double median = v.median_gbps;
   if (labels_path && m) {
     FILE* f = fopen(labels_path, "w");
     if (!f) { fprintf(stderr, "cannot write %s\n", labels_path); return 2; }
     fprintf(f, "amd.com/xgmi.link-check=%s\n", status);
-    fprintf(f, "amd.com/xgmi.p2p-min-gbps=%.0f\n", sorted[0]);
+    fprintf(f, "amd.com/xgmi.p2p-min-gbps=%.0f\n", v.min_gbps);
     fprintf(f, "amd.com/xgmi.p2p-median-gbps=%.0f\n", median);
     fprintf(f, "amd.com/xgmi.p2p-method=%s\n", mode ? "kernel-read" : "sdma-copy");
     fclose(f);
   }
-  return degraded ? 1 : 0;
+  return v.degraded ? 1 : 0;
 }
 
 // --burnin-child: one GPU's whole burn-in in its own process, for ops/probe.py:run_burnin

@@ -1479,6 +1479,7 @@ data "external" "gpu_labels" {{
          "cleanup_host.sh": cleanup_script(), "prebuilt/README": PREBUILT_README},
         {"src/tk_topo.cpp": os.path.join(CSRC, "tk_topo.cpp"),
          "src/tk_gpu_probe.hip": os.path.join(CSRC, "tk_gpu_probe.hip"),
+         "src/tk_link_verdict.h": os.path.join(CSRC, "tk_link_verdict.h"),
          "src/tk_gemm_screen.hip": os.path.join(CSRC, "tk_gemm_screen.hip"),
          "src/tk_rccl_probe.hip": os.path.join(CSRC, "tk_rccl_probe.hip"),
          "src/tk_rccl_verify.h": os.path.join(CSRC, "tk_rccl_verify.h"),
