@@ -11,6 +11,8 @@ import os
 import subprocess
 
 import pytest
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
 
 from triton_kubernetes_amd.node.labels import labels_from_topology
 from triton_kubernetes_amd.ops import topo
@@ -290,3 +292,18 @@ def test_rdma_port_with_an_odd_name_stays_out_of_the_rccl_env(tmp_path, native_o
     doc = topo.native_topology("sysfs", root)
     assert sorted(n["name"] for n in doc["nics"]) == ["mlx5_0", "x$(id)"]
     assert topo.native_rccl_env(root) == site_env_from_topology(doc) == {"NCCL_IB_HCA": "=mlx5_0:1"}
+
+
+@settings(max_examples=60, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(ngpu=st.integers(1, 8), partition=st.sampled_from(["SPX", "DPX", "QPX", "CPX"]), mesh=st.booleans(),
+       hive=st.integers(1, 2 ** 63 - 1), ue=st.dictionaries(st.integers(0, 7), st.integers(0, 50), max_size=3))
+def test_native_labels_equal_python_spec_over_generated_nodes(native_ok, ngpu, partition, mesh, hive, ue):
+    """The C++ labeller and the Python spec (node/labels.py) over generated nodes: GPU count,
+    partition mode, xGMI mesh or none, hive id, uncorrectable-error counts."""
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        root = make_tree(d, ngpu=ngpu, hive=hive, partition=partition, mesh=mesh, ue=ue)
+        native = topo.native_labels("sysfs", root)
+        assert native == labels_from_topology(topo.native_topology("sysfs", root))
+        assert native["amd.com/gpu.count"] == str(ngpu)
