@@ -65,6 +65,7 @@ Rank 0 prints one JSON line (the driver's contract).
 
 import argparse
 import json
+import math
 import os
 import shutil
 import signal
@@ -194,6 +195,7 @@ class RunBudget:
         self.t0 = _T_START if t0 is None else t0
         self.settles = []
         self.steps = []
+        self._natural = []  # what each settle would have taken: its wait, or more when cut
         self.caps_used = []  # the cap each capped settle ran under
         self.projected_s = None
         self.settle_cap_s = None
@@ -203,10 +205,18 @@ class RunBudget:
     def shed(self) -> list:
         return (["warm_creates"] if not self.warm_allowed else []) + (["hbm_settle_capped"] if self.caps_used else [])
 
-    def record(self, settle_s: float, step_s: float) -> None:
-        """One settle and the step after it; the settle ran under the cap in force now."""
+    def record(self, settle_s: float, step_s: float, settle_cut: bool = False) -> None:
+        """One settle and the step after it; the settle ran under the cap in force now.
+        ``settle_cut``: the wait ended at its limit, not on the clearing done, so the clearing
+        would have taken longer: the projection keeps pricing settles at what they took
+        before rather than at the cut (a cap priced from its own cut waits would lift itself
+        and let the next full-length settle overrun the budget)."""
         self.settles.append(float(settle_s))
         self.steps.append(float(step_s))
+        nat = float(settle_s)
+        if settle_cut and self._natural:
+            nat = max(nat, self._natural[-1])
+        self._natural.append(nat)
         if self.settle_cap_s is not None:
             self.caps_used.append(self.settle_cap_s)
 
@@ -217,7 +227,7 @@ class RunBudget:
             return
         # the slowest of the last few: a cold first step (fresh box) stops counting once the
         # run has settled, a node whose clears grow keeps counting them
-        settle, step = max(self.settles[-self.RECENT:]), max(self.steps[-self.RECENT:])
+        settle, step = max(self._natural[-self.RECENT:]), max(self.steps[-self.RECENT:])
         elapsed = self.clock() - self.t0
         warm = (settle + step) * warm_creates
         base = elapsed + cold_left * (settle + step) + self.TAIL_S
@@ -229,7 +239,9 @@ class RunBudget:
         if base <= self.budget_s or not cold_left:
             self.settle_cap_s = None
             return
-        self.settle_cap_s = round(max(0.0, (self.budget_s - elapsed - self.TAIL_S - cold_left * step) / cold_left), 2)
+        # rounded down: a cap rounded up by 5 ms per settle would add up over a long run
+        self.settle_cap_s = math.floor(max(0.0, (self.budget_s - elapsed - self.TAIL_S - cold_left * step) / cold_left)
+                                       * 100) / 100
 
     def report(self) -> dict:
         return {"budget_s": self.budget_s or None, "projected_s": self.projected_s, "shed": self.shed,
@@ -734,9 +746,9 @@ def main() -> int:
         barrier()
         return got
 
-    def replan(cold_left: int, settle_s: float, step_s: float, what: str = "") -> None:
+    def replan(cold_left: int, settle_s: float, step_s: float, what: str = "", settle_cut: bool = False) -> None:
         """Rank 0 re-projects the run (RunBudget) and every rank takes its decision."""
-        budget.record(settle_s, step_s)
+        budget.record(settle_s, step_s, settle_cut)
         if rank == 0:
             budget.plan(cold_left, (args.warm_steps + 1) if args.warm_steps > 0 else 0)
             # one progress line per step on stderr (stdout carries only the result line)
@@ -761,11 +773,12 @@ def main() -> int:
     try:
         for w in range(args.warmup):
             t_s = time.perf_counter()
-            settle()
+            got = settle()
             barrier()
             t_step = time.perf_counter()
             cold_step(-1 - w)
-            replan(args.warmup - w - 1 + args.steps, t_step - t_s, time.perf_counter() - t_step, f"warmup {w + 1}")
+            replan(args.warmup - w - 1 + args.steps, t_step - t_s, time.perf_counter() - t_step, f"warmup {w + 1}",
+                   bool(got.get("timed_out")))
         TRACER.reset()
         comgr["mib_before_timed"] = dir_mib(comgr["dir"])
         # the timed region is the K steps, each bracketed by a barrier + synchronize on both
@@ -780,7 +793,7 @@ def main() -> int:
             barrier()
             took = time.perf_counter() - t_step
             elapsed += took
-            replan(args.steps - i - 1, t_step - t_s, took, f"step {i + 1}")
+            replan(args.steps - i - 1, t_step - t_s, took, f"step {i + 1}", bool(settles[-1].get("timed_out")))
     except Exception as exc:
         if rank == 0:
             # a failed run still says what failed, in the line's own shape (value null), before

@@ -12,6 +12,8 @@ import threading
 import time
 
 import pytest
+from hypothesis import given, settings
+from hypothesis import strategies as st
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
@@ -292,7 +294,7 @@ def _run(bench, budget, clock, warmup, steps, settle_s, step_s, warm_steps=2):
         w = settle_s if budget.settle_cap_s is None else min(settle_s, budget.settle_cap_s)
         waited.append(w)
         clock.t += w + step_s
-        budget.record(w, step_s)
+        budget.record(w, step_s, settle_cut=w < settle_s)  # a capped wait ends at its limit
         budget.plan(total - k - 1, warm_steps + 1)
     if budget.warm_allowed:
         clock.t += (warm_steps + 1) * (settle_s + step_s)
@@ -373,9 +375,41 @@ def test_run_budget_decides_afresh_after_a_slow_cold_first_step():
         step = 60.0 if k == 0 else 2.3
         waited.append(w)
         clock.t += w + step
-        b.record(w, step)
+        b.record(w, step, settle_cut=w < 8.4)
         b.plan(total - k - 1, 3)
     assert b.caps_used and b.caps_used[0] < 8.4  # the cold first step made it cap ...
     assert waited[-1] == 8.4 and b.settle_cap_s is None  # ... and ordinary steps lifted the cap
     assert b.warm_allowed and b.shed == ["hbm_settle_capped"]
     assert b.report()["capped_settles"] == len(b.caps_used) < 5
+
+
+@settings(max_examples=300, deadline=None)
+@given(settle=st.floats(0.0, 120.0), step=st.floats(0.5, 10.0), n=st.integers(1, 30), warm=st.sampled_from([0, 3]),
+       budget=st.floats(60.0, 600.0))
+def test_run_budget_holds_whenever_the_steps_themselves_fit(settle, step, n, warm, budget):
+    """A simulated run whose every settle wants ``settle`` seconds (the driver's clearing:
+    up to the settle's own 120 s limit) and every step takes ``step``.  Whenever the work
+    that cannot be shed fits -- the first settle (before any projection), every step and
+    the tail -- the run ends inside the budget, whatever the settles want; and all ``n``
+    steps run."""
+    from hypothesis import assume
+
+    import bench
+
+    assume(settle + n * step + bench.RunBudget.TAIL_S <= budget)
+    now = [0.0]
+    b = bench.RunBudget(budget, t0=0.0, clock=lambda: now[0])
+    ran = 0
+    for i in range(n):
+        waited = settle if b.settle_cap_s is None else min(settle, b.settle_cap_s)
+        now[0] += waited + step
+        ran += 1
+        b.record(waited, step, settle_cut=waited < settle)
+        b.plan(n - i - 1, warm)
+    if warm and b.warm_allowed:
+        for _ in range(warm):
+            now[0] += (settle if b.settle_cap_s is None else min(settle, b.settle_cap_s)) + step
+    now[0] += bench.RunBudget.TAIL_S
+    assert ran == n
+    assert now[0] <= budget + 1e-6, (now[0], b.report())
+    assert b.settle_cap_s is None or b.settle_cap_s >= 0.0
