@@ -38,6 +38,11 @@ def test_get_new_hostnames(existing, name, count, expected):
 
 def test_hostnames_atoi_semantics():
     assert new_hostnames(["w-+7", "w-1_0", "w- 9"], "w", 1) == ["w-8"]
+    # strconv.Atoi refuses a trailing newline and anything outside int64 (a 64-bit build)
+    assert new_hostnames(["w-5\n", "w-3"], "w", 1) == ["w-4"]
+    assert new_hostnames(["w-9223372036854775808", "w-2"], "w", 1) == ["w-3"]
+    assert new_hostnames(["w-9223372036854775806"], "w", 1) == ["w-9223372036854775807"]
+    assert new_hostnames(["w--9223372036854775809", "w-0"], "w", 1) == ["w-1"]
 
 
 # --- cmd/version_test.go ------------------------------------------------------------------------

@@ -289,6 +289,15 @@ def base_node_config(ctx: Context, module_path: str, cluster: str, state: State)
     return NodeBase(cfg, count)
 
 
+def _go_atoi(text: str) -> Optional[int]:
+    """Go's ``strconv.Atoi`` on a 64-bit build: an optional sign and decimal digits, nothing
+    else (not even a trailing newline), within int64; None where Atoi returns an error."""
+    if not _ATOI_RE.fullmatch(text):
+        return None
+    num = int(text)
+    return num if -(1 << 63) <= num < (1 << 63) else None
+
+
 def new_hostnames(existing: Sequence[str], prefix: str, count: int) -> List[str]:
     """``<prefix>-<n>`` numbered after the highest existing suffix (``create/node.go:350-380``)."""
     if count < 1:
@@ -298,10 +307,9 @@ def new_hostnames(existing: Sequence[str], prefix: str, count: int) -> List[str]
     for name in existing:
         if not name.startswith(target):
             continue
-        suffix = name[len(target):]
-        if not _ATOI_RE.match(suffix):  # strconv.Atoi semantics
+        num = _go_atoi(name[len(target):])
+        if num is None:
             continue
-        num = int(suffix)
         if num >= start:
             start = num + 1
     return [f"{prefix}-{start + i}" for i in range(count)]
