@@ -42,7 +42,9 @@ def harness(tmp_path_factory):
     d = tmp_path_factory.mktemp("linkv")
     src, exe = d / "h.cpp", d / "h"
     src.write_text(HARNESS)
-    subprocess.run(["g++", "-O1", "-std=c++17", "-Wall", "-Werror", "-I", CSRC, str(src), "-o", str(exe)], check=True)
+    # under ASan + UBSan: the verdict reads n*n arrays the harness sizes from its input
+    subprocess.run(["g++", "-O1", "-g", "-std=c++17", "-Wall", "-Werror", "-fsanitize=address,undefined",
+                    "-fno-sanitize-recover=all", "-I", CSRC, str(src), "-o", str(exe)], check=True)
     return str(exe)
 
 
