@@ -43,6 +43,7 @@ models use it.
 import hashlib
 import json
 import os
+import shlex
 import shutil
 import subprocess
 import time
@@ -158,8 +159,9 @@ def join_guard_shell(server: str, token: str) -> str:
 def join_record_shell(server: str, token: str, distribution: str, hostname: str, agent_image: str = "") -> str:
     """Shell lines for the end of a successful join step: write the join record."""
     doc = json.dumps(join_record(server, token, distribution, hostname, agent_image), sort_keys=True)
+    # quoted for the shell whatever the fields hold (a quote in a server URL stays data)
     return (f"sudo mkdir -p \"${{TK_HOST_ROOT:-}}{os.path.dirname(JOIN_RECORD)}\"\n"
-            f"printf '%s\\n' '{doc}' | sudo tee \"${{TK_HOST_ROOT:-}}{JOIN_RECORD}\" >/dev/null\n")
+            f"printf '%s\\n' {shlex.quote(doc)} | sudo tee \"${{TK_HOST_ROOT:-}}{JOIN_RECORD}\" >/dev/null\n")
 
 
 def cleanup_script() -> str:
