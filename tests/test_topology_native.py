@@ -307,3 +307,27 @@ def test_native_labels_equal_python_spec_over_generated_nodes(native_ok, ngpu, p
         native = topo.native_labels("sysfs", root)
         assert native == labels_from_topology(topo.native_topology("sysfs", root))
         assert native["amd.com/gpu.count"] == str(ngpu)
+
+
+K8S_LABEL_VALUE = r"(([A-Za-z0-9][-A-Za-z0-9_.]*)?[A-Za-z0-9])?"
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(version=st.text(alphabet=st.characters(blacklist_categories=("Cs",), blacklist_characters="\x00"),
+                       min_size=1, max_size=90))
+def test_free_text_becomes_the_same_valid_label_value_in_both(native_ok, version):
+    """Free text the node reports (here its ROCm version file) turns into the same label value
+    in the C++ labeller and in the Python spec, and that value is a valid Kubernetes label
+    value (at most 63 characters, alphanumeric at both ends) -- long, non-ASCII and
+    punctuation-heavy text included."""
+    import re
+    import tempfile
+
+    with tempfile.TemporaryDirectory() as d:
+        root = make_tree(d, ngpu=1)
+        _write(os.path.join(root, "opt/rocm/.info/version"), version)
+        native = topo.native_labels("sysfs", root)
+        doc = topo.native_topology("sysfs", root)
+        assert native == labels_from_topology(doc)
+        for v in native.values():
+            assert len(v) <= 63 and re.fullmatch(K8S_LABEL_VALUE, v), (version, v)

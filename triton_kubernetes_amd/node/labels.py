@@ -43,8 +43,11 @@ _VALUE_RE = re.compile(r"[^A-Za-z0-9._-]")
 
 
 def _label_value(v: Any) -> str:
+    """A Kubernetes label value: at most 63 characters, alphanumeric at both ends (the cut
+    can leave a '-', '.' or '_' last, which is trimmed again).  Mirrored in
+    ``ops/csrc/tk_topo.cpp:label_value``."""
     s = _VALUE_RE.sub("-", str(v)).strip("-._")
-    return s[:63]
+    return s[:63].rstrip("-._")
 
 
 # PCI device id -> product, for parts whose market name is not the SKU name

@@ -847,14 +847,22 @@ std::string render_prom(const Topology& t, int64_t max_ue, int64_t max_bad, cons
 // Same rules as triton_kubernetes_amd/node/labels.py:labels_from_topology (the
 // Python side is the spec; tests compare the two on fixtures and on the box).
 
-// Kubernetes label value: [A-Za-z0-9._-], trimmed of leading/trailing '-._', <= 63.
+// Kubernetes label value: [A-Za-z0-9._-], at most 63, alphanumeric at both ends.  Any other
+// character becomes one '-' (a UTF-8 sequence is one character, as in the Python spec: its
+// continuation bytes add nothing); trimmed of '-._' at both ends, and again after the cut.
 std::string label_value(const std::string& v) {
   std::string s;
-  for (char c : v) s += (isalnum(static_cast<unsigned char>(c)) || c == '.' || c == '_' || c == '-') ? c : '-';
-  size_t b = s.find_first_not_of("-._"), e = s.find_last_not_of("-._");
-  if (b == std::string::npos) return "";
-  s = s.substr(b, e - b + 1);
-  return s.size() > 63 ? s.substr(0, 63) : s;
+  for (char c : v) {
+    const unsigned char u = static_cast<unsigned char>(c);
+    if ((u & 0xC0) == 0x80) continue;  // UTF-8 continuation byte
+    s += (u < 0x80 && (isalnum(u) || c == '.' || c == '_' || c == '-')) ? c : '-';
+  }
+  auto trim = [](const std::string& x) {
+    size_t b = x.find_first_not_of("-._"), e = x.find_last_not_of("-._");
+    return b == std::string::npos ? std::string() : x.substr(b, e - b + 1);
+  };
+  s = trim(s);
+  return s.size() > 63 ? trim(s.substr(0, 63)) : s;
 }
 
 // PCI device id -> product, for parts whose market name is not the SKU name
