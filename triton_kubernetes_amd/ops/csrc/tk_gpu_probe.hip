@@ -1287,6 +1287,31 @@ extern "C" int tkg_screen(int dev, int M, int N, int K, int reps, long long inje
 extern "C" int tkg_screen_fp8(int dev, int M, int N, int K, int reps, long long inject, double* out);
 extern "C" const char* tkg_last_error();
 
+// a JSON string body: '"' and '\\' escaped, control characters as \u00XX (truncated to fit)
+static void json_escape(const char* in, char* out, size_t cap) {
+  size_t o = 0;
+  for (; *in; ++in) {
+    const unsigned char c = static_cast<unsigned char>(*in);
+    if (c < 0x20) {
+      if (o + 7 > cap) break;
+      o += (size_t)snprintf(out + o, cap - o, "\\u%04x", c);
+    } else {
+      const size_t need = (c == '"' || c == '\\') ? 2 : 1;
+      if (o + need + 1 > cap) break;
+      if (need == 2) out[o++] = '\\';
+      out[o++] = *in;
+    }
+  }
+  out[o] = 0;
+}
+
+// {"ok":false,"error":"<g_err>"} with the message escaped
+static void print_error_json(const char* msg) {
+  char e[1024];
+  json_escape(msg, e, sizeof(e));
+  printf("{\"ok\":false,\"error\":\"%s\"}\n", e);
+}
+
 // --p2p: peer bandwidth of every ordered GPU pair (tkp_link_matrix_mode: a kernel on the
 // receiver reading the sender's memory by default, SDMA copies with --p2p-method sdma-copy;
 // concurrent transfers only on disjoint pairs, so each number is one xGMI link's), against
@@ -1296,7 +1321,7 @@ extern "C" const char* tkg_last_error();
 static int p2p_main(const char* labels_path, double min_frac, double min_gbps, int mode) {
   int n = 0;
   if (tkp_device_count(&n) != 0 || n < 1) {
-    printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    print_error_json(g_err);
     return 2;
   }
   if (n < 2) {
@@ -1308,7 +1333,7 @@ static int p2p_main(const char* labels_path, double min_frac, double min_gbps, i
   std::vector<int> devs(n), acc(n * n, 0);
   for (int i = 0; i < n; ++i) devs[i] = i;
   if (tkp_link_matrix_check(devs.data(), n, 64ull << 20, 3, mode, mat.data(), acc.data(), derr.data()) != 0) {
-    printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    print_error_json(g_err);
     return 2;
   }
   // a matrix whose only fault is speed is measured again, best of up to 3 per pair (the
@@ -1390,14 +1415,6 @@ static bool quick_exit_wanted() {
   return true;
 }
 
-static void json_escape(const char* in, char* out, size_t cap) {
-  size_t o = 0;
-  for (; *in && o + 2 < cap; ++in) {
-    if (*in == '"' || *in == '\\') out[o++] = '\\';
-    out[o++] = (*in == '\n' || *in == '\r') ? ' ' : *in;
-  }
-  out[o] = 0;
-}
 
 // --p2p-child --devices 0,1,..: the raw peer-read matrix of these devices, one JSON line in
 // ops/probe.py:link_matrix's form (the agent judges it, node/labels.py:link_labels).  A node
@@ -1636,7 +1653,7 @@ int main(int argc, char** argv) {
     double mt[7] = {0, 0, 0, 0, 0, 0, 0};
     g_keep_span = 1;
     const int rc = tkp_memtest_span(dev, span_bytes, span_chunk, span_headroom, span_passes, mt);
-    if (rc != 0) printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    if (rc != 0) print_error_json(g_err);
     else
       printf("{\"ok\":true,\"errors\":%.0f,\"verify_gbps\":%.1f,\"bytes\":%.0f,\"hbm_bytes\":%.0f,"
              "\"alloc_ms\":%.1f,\"test_ms\":%.1f}\n", mt[0], mt[1], mt[2], mt[3], mt[4], mt[5]);
@@ -1664,7 +1681,7 @@ int main(int argc, char** argv) {
   const int gemm_n = full ? 8192 : 4096, gemm_reps = 5;  // ops/gemm.py:SCREEN_SIZES
   int n = 0;
   if (tkp_device_count(&n) != 0 || n < 1) {
-    printf("{\"ok\":false,\"error\":\"%s\"}\n", g_err);
+    print_error_json(g_err);
     return 2;
   }
   std::vector<int> devs;
