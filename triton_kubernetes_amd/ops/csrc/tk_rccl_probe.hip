@@ -951,6 +951,18 @@ extern "C" int tkr_sweep_local(int ndev, const size_t* sizes, int nsizes, int it
 }
 
 #ifdef TK_RCCL_MAIN
+// {"error":"<msg>"} on stderr, the message escaped (RCCL's own error text can hold quotes)
+static void print_error_json(const char* msg) {
+  std::string o;
+  for (const char* p = msg; *p; ++p) {
+    const unsigned char c = static_cast<unsigned char>(*p);
+    if (c == '"' || c == '\\') { o += '\\'; o += *p; }
+    else if (c < 0x20) { char b[8]; snprintf(b, sizeof(b), "\\u%04x", c); o += b; }
+    else o += *p;
+  }
+  fprintf(stderr, "{\"error\":\"%s\"}\n", o.c_str());
+}
+
 // Cluster mode (one process per node, all its GPUs): the cluster-wide gate for nodes that
 // have no node agent (SSH / Terraform delivery; readiness/ssh_gate.py fans it out).
 //   rank-0 node:  rccl-ready --cluster --world W --rank-base 0 --ngpus n --uid-out
@@ -996,7 +1008,7 @@ static int cluster_main(int world, int rank_base, int ndev, const char* uid_hex,
   const size_t max_bytes = sizes[n - 1];
   const int h = tkr_gate_begin_ex(uid, world, rank_base, ndev, devs.data(), /*blocking=*/0, max_bytes);
   if (h < 0) {
-    fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
+    print_error_json(g_err);
     return 2;
   }
   std::vector<double> t(n), alg(n), bus(n), err(n);
@@ -1004,7 +1016,7 @@ static int cluster_main(int world, int rank_base, int ndev, const char* uid_hex,
   const int rc = tkr_gate_sweep(h, sizes.data(), n, iters, 2, dtype, timeout_s * 1e3, t.data(), alg.data(),
                                 bus.data(), err.data(), ph);
   if (rc) {
-    fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
+    print_error_json(g_err);
     printf("{\"ok\":false,\"world\":%d,\"rank_base\":%d,\"ngpus\":%d,\"error\":\"sweep failed\"}\n", world,
            rank_base, ndev);
     return 2;
@@ -1096,7 +1108,7 @@ int main(int argc, char** argv) {
       return 2;
     }
     if (check_verifiable(dtype, world)) {  // refused before any communicator exists
-      fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
+      print_error_json(g_err);
       return 2;
     }
     return cluster_main(world, rank_base, ndev, uid_hex, uid_out, max_mib, iters, dtype, min_busbw, timeout_s);
@@ -1108,7 +1120,7 @@ int main(int argc, char** argv) {
   std::vector<double> t(n), alg(n), bus(n), err(n);
   int rc = tkr_sweep_local(ndev, sizes.data(), n, iters, warmup, dtype, t.data(), alg.data(), bus.data(), err.data());
   if (rc) {
-    fprintf(stderr, "{\"error\":\"%s\"}\n", g_err);
+    print_error_json(g_err);
     return 2;
   }
   double errs = 0;
