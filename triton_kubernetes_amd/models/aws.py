@@ -184,7 +184,7 @@ def _ebs(ctx: Context) -> Dict[str, str]:
     out["ebs_volume_device_name"] = s.get_string("ebs_volume_device_name") if s.is_set(
         "ebs_volume_device_name") else ctx.prompter.prompt(
         "EBS Volume Device Name", default="/dev/sdf",
-        validate=lambda v: None if EBS_DEVICE_RE.match(v) else
+        validate=lambda v: None if EBS_DEVICE_RE.fullmatch(v) else
         "Device name must follow the format: /dev/sd[f-p] (e.g. /dev/sdf, /dev/sdp")
     out["ebs_volume_mount_path"] = s.get_string("ebs_volume_mount_path") if s.is_set(
         "ebs_volume_mount_path") else ctx.prompter.prompt("EBS Volume Mount Path")

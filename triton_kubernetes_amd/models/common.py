@@ -173,8 +173,8 @@ def base_cluster_config(ctx: Context, module_path: str) -> Dict:
         "k8s_registry_password": "",
     }
     name = ctx.resolve("name", "Cluster Name",
-                       validate=lambda v: None if DNS1123_RE.match(v) else DNS1123_MESSAGE)
-    if not name or not DNS1123_RE.match(name):
+                       validate=lambda v: None if DNS1123_RE.fullmatch(v) else DNS1123_MESSAGE)
+    if not name or not DNS1123_RE.fullmatch(name):
         raise ConfigError("Invalid Cluster Name")
     cfg["name"] = name
     dist = cluster_distribution(ctx)

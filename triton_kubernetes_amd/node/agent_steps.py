@@ -77,7 +77,7 @@ class StepResult:
 
 
 def _check(pattern: re.Pattern, value: str, what: str) -> str:
-    if not isinstance(value, str) or not pattern.match(value):
+    if not isinstance(value, str) or not pattern.fullmatch(value):  # no trailing newline either
         raise ValueError(f"invalid {what}: {value!r}")
     return value
 

@@ -195,7 +195,7 @@ def textfile_dir_of(cfg: Dict[str, Any]) -> str:
     """``gpu_metrics_textfile``: node_exporter's ``--collector.textfile.directory`` on the
     node ("" = off, the default)."""
     d = str(cfg.get("gpu_metrics_textfile") or "").strip()
-    if d and (not _DIR_RE.match(d) or "/../" in d + "/"):
+    if d and (not _DIR_RE.fullmatch(d) or "/../" in d + "/"):
         from ..errors import ConfigError
 
         raise ConfigError(f"gpu_metrics_textfile must be an absolute directory path. Found '{d}'.")

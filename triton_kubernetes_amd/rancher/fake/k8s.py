@@ -178,7 +178,7 @@ def _core_problem(kind: str, obj: Dict[str, Any]) -> str:
     if kind in ("secrets", "configmaps"):
         for field in ("data", "binaryData") if kind == "configmaps" else ("data", "stringData"):
             for key in (obj.get(field) or {}):
-                if not _DATA_KEY_RE.match(str(key)):
+                if not _DATA_KEY_RE.fullmatch(str(key)):
                     return f"{field}[{key}]: Invalid value: a valid config key must consist of alphanumeric characters, '-', '_' or '.'"
     if kind == "secrets":
         data = obj.get("data") or {}

@@ -94,7 +94,7 @@ def bootstrap_password(manager_name: str, admin_password: str) -> str:
 
 def k8s_minor(version: str) -> Optional[str]:
     """``v1.28.10-rancher1-1`` / ``v1.28`` -> ``v1.28``; None if not a version string."""
-    m = _K8S_RE.match(version or "")
+    m = _K8S_RE.fullmatch(version or "")
     return f"v{m.group(1)}.{m.group(2)}" if m else None
 
 
