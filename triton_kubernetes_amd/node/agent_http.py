@@ -16,6 +16,7 @@ open are answered 503.
 """
 
 import base64
+import binascii
 import hmac
 import http.server
 import json
@@ -28,6 +29,15 @@ from ..utils.httpserver import Server as HTTPServer
 from .agent_gate import GateAborted
 from .plan import BootstrapPlan
 from .security import is_loopback, metrics_token
+
+MAX_BODY = 16 << 20  # bytes: the largest request body the agent reads
+
+
+class _BadRequest(Exception):
+    def __init__(self, code: int, msg: str):
+        super().__init__(msg)
+        self.code = code
+
 
 class AgentHTTPMixin:
     """Mixin of :class:`~.agent.NodeAgent`: the HTTP(S) server."""
@@ -69,8 +79,18 @@ class AgentHTTPMixin:
                 self.wfile.write(body)
 
             def _body(self):
-                n = int(self.headers.get("Content-Length") or 0)
-                return json.loads(self.rfile.read(n) or b"{}") if n else {}
+                """The request's JSON object.  A length that is not a count, or past
+                :data:`MAX_BODY` (a plan is a few KiB), is refused before anything is read."""
+                raw = self.headers.get("Content-Length") or "0"
+                if not raw.isdigit():
+                    raise _BadRequest(400, "Content-Length must be a byte count")
+                n = int(raw)
+                if n > MAX_BODY:
+                    raise _BadRequest(413, f"request body over {MAX_BODY} bytes")
+                doc = json.loads(self.rfile.read(n) or b"{}") if n else {}
+                if not isinstance(doc, dict):
+                    raise _BadRequest(400, "the request body must be a JSON object")
+                return doc
 
             def _gone(self) -> bool:
                 """The agent stopped: a keep-alive connection accepted before is not served."""
@@ -137,7 +157,10 @@ class AgentHTTPMixin:
                 try:
                     body = self._body()
                     if path == "/v1/plan":
-                        plan = BootstrapPlan.from_json(body["plan"])
+                        try:
+                            plan = BootstrapPlan.from_json(body["plan"])
+                        except (AttributeError, KeyError, TypeError, ValueError) as exc:
+                            raise _BadRequest(400, f"malformed plan: {type(exc).__name__}: {exc}") from exc
                         bad = agent.refusals(plan)
                         if bad:
                             return self._reply(403, {"error": bad[0]})
@@ -145,14 +168,14 @@ class AgentHTTPMixin:
                     if path == "/v1/rccl-uid":
                         return self._reply(200, {"uid": base64.b64encode(agent.new_uid()).decode()})
                     if path == "/v1/rccl-prepare":
-                        uid = base64.b64decode(body["uid"]) if body.get("uid") else None
+                        uid = base64.b64decode(body["uid"], validate=True) if body.get("uid") else None
                         return self._reply(200, agent.rccl_prepare(uid,
                                                                    int(body["world"]), int(body["rank_base"]),
                                                                    int(body.get("ndev", 1)),
                                                                    int(body.get("max_bytes", 0)),
                                                                    [int(x) for x in body.get("sizes") or []]))
                     if path == "/v1/rccl-gate":
-                        uid = base64.b64decode(body["uid"])
+                        uid = base64.b64decode(body["uid"], validate=True)
                         return self._reply(200, agent.rccl_gate(int(body["rank"]), int(body["world"]), uid,
                                                                 [int(s) for s in body.get("sizes", [1 << 20])],
                                                                 int(body.get("iters", 10)),
@@ -160,7 +183,7 @@ class AgentHTTPMixin:
                                                                 float(body.get("timeout_s", 600.0)),
                                                                 bool(body.get("release_holds", False))))
                     if path == "/v1/rccl-abort":
-                        return self._reply(200, agent.rccl_abort(base64.b64decode(body["uid"])))
+                        return self._reply(200, agent.rccl_abort(base64.b64decode(body["uid"], validate=True)))
                     if path == "/v1/cleanup":
                         return self._reply(200, agent.cleanup())
                     if path == "/v1/shutdown":
@@ -170,6 +193,13 @@ class AgentHTTPMixin:
                         return self._reply(200, {"ok": True})
                 except GateAborted as exc:
                     return self._reply(409, {"error": f"GateAborted: {exc}", "aborted": True})
+                except _BadRequest as exc:
+                    self.close_connection = True  # the body was not read: the stream is out of step
+                    return self._reply(exc.code, {"error": str(exc)})
+                except (KeyError, TypeError, ValueError, binascii.Error) as exc:
+                    # a request this agent cannot take (a missing or malformed field, a value a
+                    # step's validation refused): the caller's, not the node's, error
+                    return self._reply(400, {"error": f"{type(exc).__name__}: {exc}"})
                 except Exception as exc:  # noqa: BLE001
                     return self._reply(500, {"error": f"{type(exc).__name__}: {exc}"})
                 return self._reply(404, {"error": "not found"})
