@@ -1,0 +1,56 @@
+"""The CLI in non-interactive mode over generated silent-install files: whatever a value's
+type or text (null, numbers, lists, maps, empty, non-ASCII, path-like), every command ends
+in an exit code and a message -- a refusal or a result -- never in a Python traceback.  The
+files start from valid manager / cluster / node / get / destroy documents and have one to
+three values replaced (the reference's viper coerced types silently; this CLI refuses or
+converts them)."""
+
+import io
+import os
+
+import yaml
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from triton_kubernetes_amd.cli.main import run
+
+VALUES = st.sampled_from([None, 0, 7, -1, True, [], ["a"], {}, {"a": 1}, "", "x", 3.5, "10.0.0.1", "a b", "ü",
+                          "-", "../x", "1e9", "99999999999999999999"])
+MANAGER = {"backend_provider": "local", "name": "m", "manager_cloud_provider": "baremetal", "host": "10.0.0.1",
+           "ssh_user": "u", "bastion_host": "", "key_path": "/nonexistent/k", "rancher_admin_password": "long-enough-pw",
+           "executor": "terraform", "terraform_binary": "/nonexistent/terraform"}
+NODE = {"rancher_host_label": "worker", "node_count": 1, "hostname": "w", "hosts": ["10.0.0.2"], "ssh_user": "u",
+        "bastion_host": "", "key_path": "/nonexistent/k"}
+CLUSTER = {"backend_provider": "local", "cluster_manager": "m", "cluster_cloud_provider": "baremetal", "name": "c",
+           "k8s_version": "v1.31", "k8s_network_provider": "canal", "executor": "terraform",
+           "terraform_binary": "/nonexistent/terraform", "nodes": [NODE]}
+DOCS = {("create", "manager"): MANAGER, ("create", "cluster"): CLUSTER,
+        ("create", "node"): dict({k: v for k, v in CLUSTER.items() if k != "nodes"}, cluster_name="c", **NODE),
+        ("get", "manager"): {"backend_provider": "local", "cluster_manager": "m"},
+        ("get", "cluster"): {"backend_provider": "local", "cluster_manager": "m", "cluster_name": "c"},
+        ("destroy", "cluster"): {"backend_provider": "local", "cluster_manager": "m", "cluster_name": "c",
+                                 "executor": "terraform", "terraform_binary": "/nonexistent/terraform"}}
+
+
+@st.composite
+def configs(draw):
+    cmd = draw(st.sampled_from(sorted(DOCS)))
+    doc = dict(DOCS[cmd])
+    for key in draw(st.lists(st.sampled_from(sorted(doc)), min_size=1, max_size=3, unique=True)):
+        doc[key] = draw(VALUES)
+    if isinstance(doc.get("nodes"), list) and doc["nodes"] and draw(st.booleans()):
+        node = dict(NODE)
+        node[draw(st.sampled_from(sorted(NODE)))] = draw(VALUES)
+        doc["nodes"] = [node]
+    return cmd, doc
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(configs())
+def test_no_generated_config_ends_in_a_traceback(tk_home, tmp_path, case):
+    cmd, doc = case
+    path = os.path.join(str(tmp_path), "c.yaml")
+    with open(path, "w", encoding="utf-8") as fh:
+        fh.write(yaml.safe_dump(doc))
+    code = run(["--non-interactive", "--config", path, *cmd], out=io.StringIO())
+    assert isinstance(code, int)

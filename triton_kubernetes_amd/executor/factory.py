@@ -27,9 +27,17 @@ DirectExecutor when it implements every module of the document.
 from typing import Optional
 
 from ..config.context import Context
+from ..errors import ConfigError
 from ..state import State
 from .base import Executor
 from .shell import which
+
+
+def _float(text: str, key: str) -> float:
+    try:
+        return float(text)
+    except ValueError:
+        raise ConfigError(f"{key} must be a number of seconds. Found '{text}'.") from None
 
 
 def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
@@ -61,7 +69,7 @@ def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
                               rancher_bootstrap=s.get_string("rancher_bootstrap") or "operator",
                               node_cleanup=s.get_bool("node_cleanup") if s.is_set("node_cleanup") else True,
                               host_retries=s.get_int("host_retries") if s.is_set("host_retries") else 0,
-                              retry_backoff=float(s.get_string("host_retry_backoff") or 2.0),
+                              retry_backoff=_float(s.get_string("host_retry_backoff") or "2.0", "host_retry_backoff"),
                               rancher_factory=ctx.extras.get("rancher_factory"),
                               ca_file=s.get_string("rancher_ca_file") or "")
-    raise ValueError(f"unknown executor '{kind}' (terraform | direct | auto)")
+    raise ConfigError(f"executor must be one of terraform, direct, auto. Found '{kind}'.")

@@ -43,6 +43,8 @@ def run_shell_command(options: Optional[ShellOptions], command: str, *args: str)
         )
     except subprocess.TimeoutExpired as exc:
         raise ExecutorError(f"{command} {' '.join(args)}: timed out after {opts.timeout}s") from exc
+    except OSError as exc:  # a path that is not there, or not executable (Go: fork/exec <path>: ...)
+        raise ExecutorError(f"fork/exec {exe}: {exc.strerror or exc}") from exc
     if proc.returncode != 0:
         raise ExecutorError(f"exit status {proc.returncode}")
     return ShellResult(proc.returncode, proc.stdout or "", proc.stderr or "")
