@@ -220,7 +220,9 @@ def check_sources(modules: Dict[str, Dict]) -> None:
     another install's module tree that does not exist here (documents written before the
     ``tk::`` form)."""
     for key, mod in modules.items():
-        source = str((mod or {}).get("source", ""))
+        if not isinstance(mod, dict):  # Terraform refuses such a document too
+            raise ExecutorError(f"module.{key} in main.tf.json is not a module block (an object): {mod!r:.60}")
+        source = str(mod.get("source", ""))
         if is_packaged_source(source):
             resolve_source(source, key)
         elif packaged_module_of_path(source) is not None and not os.path.isdir(source.split("?", 1)[0]):
