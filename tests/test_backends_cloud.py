@@ -313,3 +313,24 @@ def test_manta_expired_lock_taken_over_by_exactly_one(manta):
     for t in threads:
         t.join()
     assert len(winners) == 1 and len(losers) == 3
+
+
+@pytest.mark.parametrize("held", [b"[1, 2]", b"not json", b'{"expires": "soon"}', b'"x"'])
+def test_manta_unreadable_lock_object_is_stale(manta, held):
+    """A lock object this CLI did not write (corrupt, another format) is taken over, not a
+    traceback."""
+    fake, key_path, key = manta
+    be = MantaBackend("acct", key_path, key.fingerprint_md5(), "https://triton", fake.url)
+    be.client.put_directory("/stor/triton-kubernetes/mgr")
+    be.client.put_object("/stor/triton-kubernetes/mgr/.lock", held)
+    with be.lock("mgr", timeout=5.0, poll=0.01):
+        pass
+
+
+def test_a_reply_that_is_not_json_is_an_error_with_its_first_bytes():
+    from triton_kubernetes_amd.cloud.http import Response
+    from triton_kubernetes_amd.errors import TKError
+
+    with pytest.raises(TKError, match="expected a JSON response \\(HTTP 200\\), got: b'<html>"):
+        Response(200, {}, b"<html>proxy error</html>", 0.0).json()
+    assert Response(204, {}, b"", 0.0).json() is None

@@ -179,9 +179,10 @@ class MantaBackend(Backend):
             if raw is not None and held_etag:
                 try:
                     holder = json.loads(raw)
-                except ValueError:
-                    holder = {}
-                if float(holder.get("expires", 0)) < time.time():
+                    expires = float(holder.get("expires", 0)) if isinstance(holder, dict) else 0.0
+                except (TypeError, ValueError):
+                    expires = 0.0  # a lock object that is not ours to read is stale
+                if expires < time.time():
                     etag = self.client.put_object(path, body, if_match=held_etag)
                     if etag is not None:
                         break

@@ -48,7 +48,13 @@ class Response:
     elapsed: float = 0.0
 
     def json(self) -> Any:
-        return json.loads(self.body or b"null")
+        """The body as JSON; a body that is not (a proxy's HTML page, a truncated reply) is an
+        error with its first bytes, not a bare ``JSONDecodeError``."""
+        try:
+            return json.loads(self.body or b"null")
+        except ValueError:
+            raise TKError(f"expected a JSON response (HTTP {self.status}), got: "
+                          f"{bytes(self.body[:120])!r}") from None
 
     def header(self, name: str, default: str = "") -> str:
         return self.headers.get(name.lower(), default)
