@@ -259,13 +259,22 @@ def parse_private_key(text: str, passphrase: Optional[str] = None) -> PrivateKey
         if passphrase is None:
             raise KeyParseError("ssh: this private key is passphrase protected")
         return parse_private_key(_openssl_decrypt(text, passphrase))
-    der = base64.b64decode("".join(b64.split()))
-    if label == "RSA PRIVATE KEY":
-        key = _rsa_from_pkcs1(der)
-    elif label == "PRIVATE KEY":
-        key = _from_pkcs8(der)
-    elif label == "EC PRIVATE KEY":
-        key = _ec_from_sec1(der)
+    try:
+        der = base64.b64decode("".join(b64.split()))
+        if label == "RSA PRIVATE KEY":
+            key = _rsa_from_pkcs1(der)
+        elif label == "PRIVATE KEY":
+            key = _from_pkcs8(der)
+        elif label == "EC PRIVATE KEY":
+            key = _ec_from_sec1(der)
+        else:
+            key = None
+    except (IndexError, KeyError, TypeError, ValueError, struct.error) as exc:
+        # a truncated or damaged file (a copy cut short, an edited line): the reference's
+        # ssh.ParsePrivateKey errors the same way, without a stack
+        raise KeyParseError(f"ssh: the {label} is damaged or truncated ({type(exc).__name__})") from None
+    if key is not None:
+        pass
     elif label == "OPENSSH PRIVATE KEY":
         try:
             key = _from_openssh(der)
@@ -273,6 +282,8 @@ def parse_private_key(text: str, passphrase: Optional[str] = None) -> PrivateKey
             if "passphrase" not in str(exc) or passphrase is None:
                 raise
             return parse_private_key(_openssh_decrypt(text, passphrase))
+        except (IndexError, KeyError, TypeError, ValueError, struct.error) as exc:
+            raise KeyParseError(f"ssh: the {label} is damaged or truncated ({type(exc).__name__})") from None
     else:
         raise KeyParseError(f"ssh: unsupported key type \"{label}\"")
     key.pem = text
