@@ -4,6 +4,7 @@ binds looser than ``<``, comparisons do not chain), unary operators and conditio
 tree is rendered with only the parentheses HCL's precedence needs, parsed, evaluated, and
 compared with a direct evaluation of the tree."""
 
+import pytest
 from hypothesis import given, settings
 from hypothesis import strategies as st
 
@@ -89,3 +90,44 @@ def test_hcl_precedence_is_not_pythons():
     assert hcl_value("true || false && false") is True
     assert hcl_value("!true == false") is True
     assert hcl_value("1 == 1 ? 2 + 3 : 4") == 5
+
+
+import glob  # noqa: E402
+import os  # noqa: E402
+
+_MODULES = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "triton_kubernetes_amd",
+                        "terraform", "modules")
+_SOURCES = sorted(glob.glob(os.path.join(_MODULES, "*", "*.tf")))
+_TEMPLATES = sorted(glob.glob(os.path.join(_MODULES, "*", "files", "*.tftpl")))
+_ALPHABET = '{}[]()"\'$%~<>=!?:,.\\\n\t #/*-+abcxuU0123'
+
+
+@settings(max_examples=300, deadline=None)
+@given(st.booleans(), st.integers(0, 10 ** 6), st.lists(st.tuples(st.sampled_from(["set", "insert", "delete"]),
+                                                                  st.integers(0, 10 ** 6), st.sampled_from(_ALPHABET)),
+                                                        min_size=1, max_size=6))
+def test_damaged_sources_raise_only_syntax_errors(template, pick, edits):
+    """Mutations of the shipped module sources and templates: the parser answers with its own
+    syntax error (file:line:col), never an IndexError, ValueError or OverflowError."""
+    files = _TEMPLATES if template else _SOURCES
+    with open(files[pick % len(files)], encoding="utf-8") as fh:
+        s = list(fh.read())
+    for op, pos, ch in edits:
+        i = pos % (len(s) + 1)
+        if op == "set" and s:
+            s[min(i, len(s) - 1)] = ch
+        elif op == "insert":
+            s.insert(i, ch)
+        else:
+            del s[i:i + 1 + pos % 20]
+    try:
+        (hcl.parse_template if template else hcl.parse)("".join(s))
+    except (hcl.HCLSyntaxError, hcl.TemplateError):
+        pass
+
+
+def test_unicode_escapes():
+    assert hcl_value('"a\\u00e9b\\U0001F600"') == "aéb\U0001F600"
+    for bad in ('"\\urerm"', '"\\u12"', '"\\UFFFFFFFF"', '"\\U00110000"'):
+        with pytest.raises(hcl.HCLSyntaxError):
+            hcl_value(bad)

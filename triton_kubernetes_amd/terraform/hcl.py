@@ -462,9 +462,16 @@ class _Parser:
                     buf.append({"n": "\n", "r": "\r", "t": "\t"}.get(esc, esc))
                     self.i += 2
                     continue
-                if esc == "u":
-                    buf.append(chr(int(s[self.i + 2:self.i + 6], 16)))
-                    self.i += 6
+                if esc in ("u", "U"):
+                    width = 4 if esc == "u" else 8
+                    digits = s[self.i + 2:self.i + 2 + width]
+                    if len(digits) != width or any(ch not in "0123456789abcdefABCDEF" for ch in digits):
+                        raise self.err(f"invalid escape \\{esc}{digits}: {width} hex digits expected")
+                    try:
+                        buf.append(chr(int(digits, 16)))
+                    except (ValueError, OverflowError):  # past U+10FFFF
+                        raise self.err(f"invalid escape \\{esc}{digits}: not a Unicode code point") from None
+                    self.i += 2 + width
                     continue
                 raise self.err(f"invalid escape \\{esc}")
             if s.startswith("$${", self.i) or s.startswith("%%{", self.i):
