@@ -8,6 +8,7 @@ converts them)."""
 import io
 import os
 
+import pytest
 import yaml
 from hypothesis import HealthCheck, given, settings
 from hypothesis import strategies as st
@@ -54,3 +55,19 @@ def test_no_generated_config_ends_in_a_traceback(tk_home, tmp_path, case):
         fh.write(yaml.safe_dump(doc))
     code = run(["--non-interactive", "--config", path, *cmd], out=io.StringIO())
     assert isinstance(code, int)
+
+
+@pytest.mark.parametrize("content,why", [
+    ("a: [\n", "is not valid YAML"),
+    ("a: !!python/object:os.system x\n", "is not valid YAML"),  # safe_load: no object construction
+    ("\t- bad indent\n", "is not valid YAML"),
+    ("- a\n- b\n", "must contain a mapping at the top level"),
+    (None, "No such file or directory"),
+])
+def test_config_files_that_cannot_be_used_are_refusals(tk_home, tmp_path, content, why):
+    path = tmp_path / "c.yaml"
+    if content is not None:
+        path.write_text(content)
+    out = io.StringIO()
+    assert run(["--non-interactive", "--config", str(path), "get", "manager"], out=out) == 1
+    assert why in out.getvalue()

@@ -182,12 +182,22 @@ class Settings:
 
 
 def load_config_file(path: str) -> Dict[str, Any]:
-    with open(path, "r", encoding="utf-8") as fh:
-        text = fh.read()
-    if path.endswith(".json"):
-        data = json.loads(text or "{}")
-    else:
-        data = yaml.safe_load(text) or {}
+    """The silent-install file's settings.  A file that cannot be read or parsed is a
+    :class:`ConfigError` naming the file and the parser's reason (the reference's viper
+    ignored such a file and went on without it, to fail later on a missing key)."""
+    try:
+        with open(path, "r", encoding="utf-8") as fh:
+            text = fh.read()
+    except (OSError, UnicodeDecodeError) as exc:
+        raise ConfigError(f"config file '{path}': {getattr(exc, 'strerror', None) or exc}") from None
+    try:
+        if path.endswith(".json"):
+            data = json.loads(text or "{}")
+        else:
+            data = yaml.safe_load(text) or {}
+    except (ValueError, yaml.YAMLError) as exc:
+        raise ConfigError(f"config file '{path}' is not valid {'JSON' if path.endswith('.json') else 'YAML'}: "
+                          f"{' '.join(str(exc).split())}") from None
     if not isinstance(data, dict):
         raise ConfigError(f"config file '{path}' must contain a mapping at the top level")
     return data
