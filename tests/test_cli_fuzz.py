@@ -71,3 +71,44 @@ def test_config_files_that_cannot_be_used_are_refusals(tk_home, tmp_path, conten
     out = io.StringIO()
     assert run(["--non-interactive", "--config", str(path), "get", "manager"], out=out) == 1
     assert why in out.getvalue()
+
+
+OTHER_CMDS = [("wait", "cluster"), ("backup", "cluster"), ("restore", "cluster"), ("userdata", "node"),
+              ("migrate", "manager"), ("credentials", "node"), ("health", "cluster"), ("drain", "node"),
+              ("upgrade", "cluster"), ("cordon", "node"), ("uncordon", "node"), ("forget", "host-key"),
+              ("get", "scrape-config")]
+OTHER_KEYS = ["cluster_manager", "cluster_name", "hostname", "namespace", "namespaces", "backup_target", "backup_name",
+              "s3_bucket", "health_taint", "max_uncorrectable", "drain_timeout", "force", "k8s_version", "source_url",
+              "migrate_drop_unknown", "host", "wait_timeout", "node_exporter_port", "rccl_gate_max_mib",
+              "host_retry_backoff", "executor"]
+MANAGER_DOC = {"module": {
+    "cluster-manager": {"source": "tk::terraform/modules/bare-metal-rancher?ref=v0.8.2", "name": "m", "host": "10.0.0.1"},
+    "cluster_baremetal_c": {"source": "tk::terraform/modules/bare-metal-rancher-k8s?ref=v0.8.2", "name": "c"},
+    "node_baremetal_c_w-1": {"source": "tk::terraform/modules/bare-metal-rancher-k8s-host?ref=v0.8.2",
+                             "hostname": "w-1"}}}
+
+
+@settings(max_examples=150, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+@given(st.sampled_from(OTHER_CMDS), st.dictionaries(st.sampled_from(OTHER_KEYS), VALUES, max_size=4))
+def test_day2_commands_over_generated_settings_never_end_in_a_traceback(tk_home, tmp_path, cmd, extra):
+    """The day-2 commands (wait, backup, restore, userdata, migrate, credentials, health,
+    drain, upgrade, cordon, forget, scrape-config) against a manager document that was never
+    applied, with generated values for their settings: numbers that are not numbers, a
+    ``source_url`` with no modules behind it, a node whose block lacks the cluster's
+    outputs."""
+    import json
+
+    d = tk_home / ".triton-kubernetes" / "m"
+    d.mkdir(parents=True, exist_ok=True)
+    (d / "main.tf.json").write_text(json.dumps(MANAGER_DOC))
+    doc = {"backend_provider": "local", "cluster_manager": "m", "cluster_name": "c", "hostname": "w-1",
+           "executor": "terraform", "terraform_binary": "/nonexistent/terraform", "wait_timeout": 1}
+    doc.update(extra)
+    path = os.path.join(str(tmp_path), "c.yaml")
+    with open(path, "w", encoding="utf-8") as fh:
+        fh.write(yaml.safe_dump(doc))
+    try:
+        code = run(["--non-interactive", "--config", path, *cmd], out=io.StringIO())
+    except SystemExit as exc:  # argparse's own refusals
+        code = exc.code
+    assert isinstance(code, int)

@@ -95,3 +95,14 @@ def test_a_cycle_ends_the_walk():
     assert st_["a"] == "ok" and st_["b"] == st_["c"] == "failed"
     assert report.runs["b"].error == "dependency cycle" and st_["d"] in ("failed", "blocked")
     assert set(ex.runs_of) == {"a"}
+
+
+def test_a_chain_of_dependents_of_a_failure_is_blocked_not_a_cycle():
+    """m10 sorts before m4 and m7, which depend on the failed m0: in the pass where m0's
+    failure is seen, m10 was still undecided when nothing was left running, and the walk
+    called it a dependency cycle.  The walk now settles each pass to a fixed point."""
+    graph = {"m0": set(), "m1": set(), "m2": {"m0"}, "m3": {"m0"}, "m4": {"m0"}, "m5": set(), "m6": {"m0", "m3"},
+             "m7": {"m0"}, "m8": set(), "m9": set(), "m10": {"m4", "m7", "m8"}, "m11": set()}
+    for seed in range(20):
+        report = DagExecutor(graph, ["m0", "m1"], 4, seed)._apply_report(_State(), MemoryBackend())
+        assert report.runs["m10"].status == "blocked", (seed, report.runs["m10"].error)

@@ -152,6 +152,26 @@ class Settings:
         except (TypeError, ValueError) as exc:
             raise ConfigError(f"{key} must be a valid number. Found '{value}'.") from exc
 
+    def get_float(self, key: str, default: float) -> float:
+        """A number of the settings (seconds, MiB); ``default`` when unset or empty, and a
+        :class:`ConfigError` naming the key for anything that is not a number."""
+        value = self.get(key)
+        if value is None or (isinstance(value, str) and not value.strip()):
+            return float(default)
+        if isinstance(value, bool):
+            raise ConfigError(f"{key} must be a number. Found '{value}'.")
+        try:
+            return float(str(value).strip())
+        except ValueError:
+            raise ConfigError(f"{key} must be a number. Found '{value}'.") from None
+
+    def get_int_or(self, key: str, default: int) -> int:
+        """:meth:`get_int` with a default for an unset or empty key."""
+        value = self.get(key)
+        if value is None or (isinstance(value, str) and not value.strip()):
+            return int(default)
+        return self.get_int(key)
+
     def get_string_slice(self, key: str) -> List[str]:
         """``viper.GetStringSlice``: lists as-is; strings split on whitespace/commas."""
         value = self.get(key)

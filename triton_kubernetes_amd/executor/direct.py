@@ -313,24 +313,32 @@ class DirectExecutor(Executor):
         rehashed = False
         with span("direct.apply", modules=len(runs)):
             while pending or futures:
-                for key in sorted(pending):
-                    run = runs[key]
-                    if any(runs[d].status in ("failed", "blocked") for d in run.deps):
-                        run.status, run.error = "blocked", "dependency failed"
-                        pending.discard(key)
-                        continue
-                    if all(runs[d].status in ("ok", "skipped") for d in run.deps):
-                        pending.discard(key)
-                        prev = tf["module_state"].get(key)
-                        if self._unchanged(run, prev) and key in outputs:
-                            run.status = "skipped"
-                            if prev.get("hash") != run.hash:  # a pre-r4 hash: stored in today's form
-                                tf["module_state"][key] = dict(prev, hash=run.hash)
-                                rehashed = True
+                # to a fixed point: a module blocked (or skipped) in this pass can decide one
+                # that sorted before it (a chain of dependents of a failed module), before
+                # "nothing running and nothing startable" may be read as a cycle
+                progress = True
+                while progress:
+                    progress = False
+                    for key in sorted(pending):
+                        run = runs[key]
+                        if any(runs[d].status in ("failed", "blocked") for d in run.deps):
+                            run.status, run.error = "blocked", "dependency failed"
+                            pending.discard(key)
+                            progress = True
                             continue
-                        run.start = time.time()
-                        run.prev_private = (prev or {}).get("private")
-                        futures[pool.submit(self._apply_module, run, dict(outputs), state.name)] = key
+                        if all(runs[d].status in ("ok", "skipped") for d in run.deps):
+                            pending.discard(key)
+                            progress = True
+                            prev = tf["module_state"].get(key)
+                            if self._unchanged(run, prev) and key in outputs:
+                                run.status = "skipped"
+                                if prev.get("hash") != run.hash:  # a pre-r4 hash: stored in today's form
+                                    tf["module_state"][key] = dict(prev, hash=run.hash)
+                                    rehashed = True
+                                continue
+                            run.start = time.time()
+                            run.prev_private = (prev or {}).get("private")
+                            futures[pool.submit(self._apply_module, run, dict(outputs), state.name)] = key
                 if not futures:
                     for key in pending:  # nothing running and nothing startable: a cycle
                         runs[key].status, runs[key].error = "failed", "dependency cycle"

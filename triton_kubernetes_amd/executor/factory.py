@@ -33,13 +33,6 @@ from .base import Executor
 from .shell import which
 
 
-def _float(text: str, key: str) -> float:
-    try:
-        return float(text)
-    except ValueError:
-        raise ConfigError(f"{key} must be a number of seconds. Found '{text}'.") from None
-
-
 def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
     s = ctx.settings
     kind = (s.get_string("executor") or "auto").lower()
@@ -69,7 +62,7 @@ def build_executor(ctx: Context, state: Optional[State] = None) -> Executor:
                               rancher_bootstrap=s.get_string("rancher_bootstrap") or "operator",
                               node_cleanup=s.get_bool("node_cleanup") if s.is_set("node_cleanup") else True,
                               host_retries=s.get_int("host_retries") if s.is_set("host_retries") else 0,
-                              retry_backoff=_float(s.get_string("host_retry_backoff") or "2.0", "host_retry_backoff"),
+                              retry_backoff=s.get_float("host_retry_backoff", 2.0),
                               rancher_factory=ctx.extras.get("rancher_factory"),
                               ca_file=s.get_string("rancher_ca_file") or "")
     raise ConfigError(f"executor must be one of terraform, direct, auto. Found '{kind}'.")

@@ -289,7 +289,7 @@ def spec_from_state(state, backend, cluster_key: str, timeout: float = 3600.0, r
 
 def gate_sizes(settings) -> List[int]:
     """RCCL gate message sizes: 1 MiB and ``rccl_gate_max_mib`` (default 64 MiB)."""
-    mib = int(float(settings.get_string("rccl_gate_max_mib") or 64)) if settings.is_set("rccl_gate_max_mib") else 64
+    mib = int(settings.get_float("rccl_gate_max_mib", 64))
     if mib < 1:
         raise TKError(f"rccl_gate_max_mib must be >= 1. Found '{mib}'.")
     return sorted({1 << 20, mib << 20})
@@ -332,7 +332,7 @@ def early_gate(ctx, state, cluster_key: str) -> Any:
 def wait_after_create(ctx, backend, state, cluster_key: str, start: Optional[float] = None,
                       gate: Any = None) -> ReadinessReport:
     s = ctx.settings
-    timeout = float(s.get_string("wait_timeout") or 3600)
+    timeout = s.get_float("wait_timeout", 3600)
     client, spec = spec_from_state(state, backend, cluster_key, timeout, s.get_bool("rccl_gate"))
     spec.rccl_sizes = gate_sizes(s)
     mixed = any(h.scheme == "agent" for h in spec.rccl_process_hosts)

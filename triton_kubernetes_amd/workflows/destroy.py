@@ -102,7 +102,7 @@ def delete_node(ctx: Context, backend: Backend) -> None:
             raise ConfigError(f"drain: cluster of {hostname} has no Rancher outputs yet (was it applied?)")
         from .drain import drain_node
 
-        timeout = float(ctx.settings.get_string("drain_timeout") or 600)
+        timeout = ctx.settings.get_float("drain_timeout", 600)
         with span("destroy.drain", node=hostname):
             drain_node(client, cid, hostname, timeout, ctx.echo, ctx.settings.get_bool("drain_force"))
     with backend.lock(manager):

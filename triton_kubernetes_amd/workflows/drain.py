@@ -103,7 +103,7 @@ def _target(ctx, backend):
 def drain_command(ctx, backend) -> Dict[str, Any]:
     """``drain node``: cordon + evict, the node stays in the cluster (cordoned)."""
     client, cid, hostname = _target(ctx, backend)
-    return drain_node(client, cid, hostname, float(ctx.settings.get_string("drain_timeout") or 600), ctx.echo,
+    return drain_node(client, cid, hostname, ctx.settings.get_float("drain_timeout", 600), ctx.echo,
                       ctx.settings.get_bool("drain_force"))
 
 

@@ -29,6 +29,7 @@ backend block are compatible by design, so migration is a source rewrite plus a 
 Nothing is applied: the next ``create`` (or an explicit re-apply) runs the new modules.
 """
 
+import os
 from typing import Any, Dict, List, Tuple
 
 from ..backend.base import Backend
@@ -51,6 +52,9 @@ def plan_migration(ctx: Context, doc: Dict[str, Any], drop_unknown: bool = False
     errors: List[str] = []
     warnings: List[str] = []
     for key, block in (doc.get("module") or {}).items():
+        if not isinstance(block, dict):
+            errors.append(f"module.{key}: not a module block (an object)")
+            continue
         src = str(block.get("source", ""))
         info = module_from_source(src)
         if info is None:
@@ -61,6 +65,9 @@ def plan_migration(ctx: Context, doc: Dict[str, Any], drop_unknown: bool = False
             continue
         new = dict(block, source=target)
         mod_dir = local_module_dir(target) or info.local_dir
+        if not os.path.isdir(mod_dir):
+            errors.append(f"module.{key}: the module directory of {target!r} ({mod_dir}) does not exist here")
+            continue
         if "k8s_distribution" not in new and "k8s_distribution" in hcl.check_module(mod_dir).variables:
             new["k8s_distribution"] = "rke1"
             warnings.append(f"module.{key}: k8s_distribution set to rke1 (the reference's clusters are RKE1)")

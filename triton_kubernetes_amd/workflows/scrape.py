@@ -85,7 +85,7 @@ def scrape_config(ctx: Context, backend: Backend) -> List[Dict[str, Any]]:
                 job["tls_config"] = {"ca_file": ca_file, "server_name": agent_address(url)}
             jobs.append(job)
     if textfile:
-        port = int(ctx.settings.get_string("node_exporter_port") or 9100)
+        port = ctx.settings.get_int_or("node_exporter_port", 9100)
         jobs.append({"job_name": f"tk-{name}-node-exporter",
                      "static_configs": [{"targets": [f"{a}:{port}"], "labels": {"cluster": name, "tk_node": h}}
                                         for h, a in textfile]})

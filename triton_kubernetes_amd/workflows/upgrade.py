@@ -101,7 +101,7 @@ def upgrade_cluster(ctx: Context, backend: Backend) -> Dict[str, Any]:
     out: Dict[str, Any] = {"from": current, "to": target, "changed": True}
     wait = ctx.settings.get_bool("wait") if ctx.is_set("wait") else True
     if wait:
-        timeout = float(ctx.settings.get_string("wait_timeout") or 3600)
+        timeout = ctx.settings.get_float("wait_timeout", 3600)
 
         def upgraded() -> bool:
             if client.cluster_version(cid) != want or client.cluster_state(cid) != "active":

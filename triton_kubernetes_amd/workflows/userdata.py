@@ -40,6 +40,11 @@ def node_userdata(ctx: Context, backend: Backend) -> str:
         resolved = resolve(cfg, outputs)
     except Exception as exc:  # noqa: BLE001 - unapplied cluster
         raise TKError(f"node '{hostname}': cluster outputs are not available yet (apply the cluster first): {exc}")
+    missing = [k for k in ("rancher_api_url", "rancher_cluster_registration_token", "rancher_cluster_ca_checksum")
+               if not isinstance(resolved.get(k), str)]
+    if missing:
+        raise TKError(f"node '{hostname}': its module block lacks {', '.join(missing)} (not a host module of a "
+                      "cluster of this manager?)")
     plan = build_host_plan(resolved, resolved["rancher_api_url"], resolved["rancher_cluster_registration_token"],
                            resolved["rancher_cluster_ca_checksum"], mi355x=bool(info and info.mi355x),
                            sequential=True)
