@@ -250,35 +250,127 @@ def test_agent_rccl_env_merges_discovered_nics(tmp_path):
     assert step["detail"]["discovered"] == ["NCCL_IB_GID_INDEX", "NCCL_IB_HCA"]
 
 
-def test_labeller_clean_under_asan_ubsan(tmp_path):
-    """Race/memory-safety check of the native labeller's host code (SURVEY.md §5.2: the
-    reference has none): the sysfs collector built with AddressSanitizer + UBSan runs the
-    JSON, --labels and --rccl-env paths over the fixture tree (GPUs + RDMA NICs) with no
-    sanitizer report and the same output as the regular build."""
+# the harness may preload a library of its own: ASan is told not to insist on coming first
+# rather than the child's environment being changed
+ASAN_ENV = {"ASAN_OPTIONS": "detect_leaks=1:abort_on_error=0:verify_asan_link_order=0",
+            "UBSAN_OPTIONS": "print_stacktrace=1"}
+
+
+@pytest.fixture(scope="module")
+def asan_labeller(tmp_path_factory):
     import shutil
 
     gxx = shutil.which("g++")
     if gxx is None:
         pytest.skip("g++ not available")
     src = os.path.join(os.path.dirname(topo.__file__), "csrc", "tk_topo.cpp")
-    exe = str(tmp_path / "labeller-asan")
+    exe = str(tmp_path_factory.mktemp("asan") / "labeller-asan")
     build = subprocess.run([gxx, "-O1", "-g", "-std=c++17", "-fsanitize=address,undefined", "-fno-omit-frame-pointer",
                             "-fno-sanitize-recover=all", "-DTK_TOPO_MAIN", src, "-o", exe],
                            capture_output=True, text=True)
     assert build.returncode == 0, build.stderr[-2000:]
+    return exe
+
+
+def _asan_run(exe, argv):
+    run = subprocess.run([exe] + argv, capture_output=True, text=True, env=dict(os.environ, **ASAN_ENV), timeout=60)
+    assert "Sanitizer" not in run.stderr and "runtime error" not in run.stderr, run.stderr[-3000:]
+    return run
+
+
+def test_labeller_clean_under_asan_ubsan(tmp_path, asan_labeller):
+    """Race/memory-safety check of the native labeller's host code (SURVEY.md §5.2: the
+    reference has none): the sysfs collector built with AddressSanitizer + UBSan runs the
+    JSON, --labels and --rccl-env paths over the fixture tree (GPUs + RDMA NICs) with no
+    sanitizer report and the same output as the regular build."""
     root = add_rdma(make_tree(str(tmp_path / "root"), ngpu=8, ue={3: 2}), RDMA)
-    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0", UBSAN_OPTIONS="print_stacktrace=1")
-    env.pop("LD_PRELOAD", None)
     ref = executable("amdgpu-topo-labeller") if os.path.exists(os.path.join(
         os.path.dirname(topo.__file__), "lib", "amdgpu-topo-labeller")) else None
     for args in ([], ["--labels"], ["--rccl-env"]):
         argv = args + (["--source", "sysfs"] if args != ["--rccl-env"] else []) + ["--sysfs-root", root]
-        run = subprocess.run([exe] + argv, capture_output=True, text=True, env=env)
+        run = _asan_run(asan_labeller, argv)
         assert run.returncode == 0, run.stderr[-3000:]
-        assert "Sanitizer" not in run.stderr and "runtime error" not in run.stderr, run.stderr[-3000:]
         if ref:
             want = subprocess.run([ref] + argv, capture_output=True, text=True).stdout
             assert run.stdout == want
+
+
+def _corrupt(root, how):
+    """One damage to a fixture tree, as a failing disk, a half-written driver attribute or
+    an odd kernel would leave sysfs."""
+    nodes = os.path.join(root, "sys/class/kfd/kfd/topology/nodes")
+    dev = os.path.join(root, "sys/class/drm/renderD129/device")
+    ib = os.path.join(root, "sys/class/infiniband/mlx5_0/ports/1")
+    if how == "empty-properties":
+        _write(f"{nodes}/2/properties", "")
+    elif how == "garbage-values":
+        _write(f"{nodes}/2/properties", "simd_count abc\nsimd_per_cu -4\ndrm_render_minor zz\nhive_id -1\n"
+                                        "location_id 0x\nunique_id 1e9\ngfx_target_version \n")
+    elif how == "huge-numbers":
+        _write(f"{nodes}/2/properties", "".join(f"{k} {'9' * 40}\n" for k in (
+            "simd_count", "simd_per_cu", "gfx_target_version", "location_id", "domain", "drm_render_minor",
+            "hive_id", "unique_id", "vendor_id", "device_id")))
+        _write(f"{nodes}/2/mem_banks/0/properties", f"heap_type 1\nsize_in_bytes {'9' * 40}\n")
+    elif how == "zero-cu":
+        _write(f"{nodes}/2/properties", "simd_count 1024\nsimd_per_cu 0\nvendor_id 4098\ndrm_render_minor 129\n")
+    elif how == "links-nowhere":
+        for n, to in enumerate((999, -1, 2, 18446744073709551615)):
+            _write(f"{nodes}/2/io_links/{n}/properties", f"type 11\nnode_from 2\nnode_to {to}\n")
+    elif how == "long-line":
+        _write(f"{nodes}/2/properties", "simd_count " + "1" * 200000 + "\nx" * 5000)
+        _write(f"{nodes}/2/name", "g" * 100000)
+    elif how == "binary-bytes":
+        with open(f"{nodes}/2/name", "wb") as fh:
+            fh.write(bytes(range(256)))
+        with open(f"{dev}/current_compute_partition", "wb") as fh:
+            fh.write(b"\xff\xfe\x00SPX\n")
+    elif how == "property-is-a-directory":
+        os.remove(f"{nodes}/2/properties")
+        os.makedirs(f"{nodes}/2/properties")
+        os.remove(f"{dev}/mem_info_vram_total")
+        os.makedirs(f"{dev}/mem_info_vram_total")
+    elif how == "drm-missing":
+        import shutil
+
+        shutil.rmtree(os.path.dirname(dev))
+    elif how == "ras-garbage":
+        _write(f"{dev}/ras/umc_err_count", "ue: \nce: -7\nue: 99999999999999999999999\n")
+        _write(f"{dev}/numa_node", "-1\n")
+        _write(f"{dev}/current_compute_partition", "\n")
+    elif how == "no-gpu-nodes":
+        import shutil
+
+        for n in range(1, 9):
+            shutil.rmtree(f"{nodes}/{n}")
+    elif how == "rdma-garbage":
+        _write(f"{ib}/state", "")
+        _write(f"{ib}/rate", "fast\n")
+        _write(f"{ib}/gids/0", "zz:" * 40 + "\n")
+        _write(f"{ib}/gid_attrs/types/0", "\x00" * 10)
+        os.remove(os.path.join(root, "sys/class/infiniband/mlx5_0/device"))
+        os.symlink("/nonexistent/device", os.path.join(root, "sys/class/infiniband/mlx5_0/device"))
+    return root
+
+
+CORRUPTIONS = ["empty-properties", "garbage-values", "huge-numbers", "zero-cu", "links-nowhere", "long-line",
+               "binary-bytes", "property-is-a-directory", "drm-missing", "ras-garbage", "no-gpu-nodes",
+               "rdma-garbage"]
+
+
+@pytest.mark.parametrize("how", CORRUPTIONS)
+def test_labeller_clean_under_asan_ubsan_over_damaged_sysfs(tmp_path, asan_labeller, how):
+    """The sanitizer build over damaged trees: each run ends with no AddressSanitizer or
+    UBSan report and with a documented status (0, or 2 when no GPU is left to label), and
+    what it prints is a JSON document or key=value lines."""
+    root = _corrupt(add_rdma(make_tree(str(tmp_path / "root"), ngpu=8), RDMA), how)
+    for args in ([], ["--labels"], ["--rccl-env"]):
+        argv = args + (["--source", "sysfs"] if args != ["--rccl-env"] else []) + ["--sysfs-root", root]
+        run = _asan_run(asan_labeller, argv)
+        assert run.returncode in (0, 2), (how, args, run.returncode, run.stderr[-3000:])
+        if run.returncode == 0 and not args:
+            json.loads(run.stdout)
+        elif run.returncode == 0:
+            assert all("=" in line for line in run.stdout.splitlines()), run.stdout[:500]
 
 
 def test_rdma_port_with_an_odd_name_stays_out_of_the_rccl_env(tmp_path, native_ok):
@@ -331,3 +423,21 @@ def test_free_text_becomes_the_same_valid_label_value_in_both(native_ok, version
         assert native == labels_from_topology(doc)
         for v in native.values():
             assert len(v) <= 63 and re.fullmatch(K8S_LABEL_VALUE, v), (version, v)
+
+
+@pytest.mark.parametrize("how", CORRUPTIONS)
+def test_in_process_readers_over_damaged_sysfs(tmp_path, native_ok, how):
+    """The in-process library and the Python KFD reader over the same damaged trees: a
+    document (or NativeUnavailable for a tree with no GPU left), never a decode error --
+    bytes that are not UTF-8 come through as U+FFFD on both sides."""
+    root = _corrupt(add_rdma(make_tree(str(tmp_path / "root"), ngpu=8), RDMA), how)
+    doc = topo.native_topology("sysfs", root)
+    assert doc["status"] in (0, 2)
+    py = topo.kfd_topology(os.path.join(root, "sys/class/kfd/kfd/topology/nodes"))
+    assert isinstance(py["gpus"], list)
+    if how == "binary-bytes":
+        names = [g["market_name"] for g in py["gpus"]]
+        assert any("�" in n for n in names)
+        assert json.loads(json.dumps(doc)) == doc
+    if doc["status"] == 0:
+        assert topo.native_labels("sysfs", root) == labels_from_topology(doc)

@@ -339,7 +339,7 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
 
         self.rccl_env_skipped = []
         try:
-            with open(self.path("/etc/rccl/rccl.env"), "r", encoding="utf-8") as fh:
+            with open(self.path("/etc/rccl/rccl.env"), "r", encoding="utf-8", errors="replace") as fh:
                 env = parse_env_file(fh.read())
         except OSError:
             return {}

@@ -36,7 +36,7 @@ def _reader(root: str) -> Callable[[str], Optional[str]]:
     def read(path: str) -> Optional[str]:
         full = os.path.join(root, path.lstrip("/")) if root not in ("", "/") else path
         try:
-            with open(full, "r", encoding="utf-8") as fh:
+            with open(full, "r", encoding="utf-8", errors="replace") as fh:
                 return fh.read().strip()
         except OSError:
             return None

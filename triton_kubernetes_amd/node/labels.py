@@ -104,7 +104,8 @@ def _gpu_labels(doc: Dict[str, Any]) -> Dict[str, str]:
         labels["amd.com/gpu.product-name"] = _label_value(name)
         if name.startswith("MI"):
             labels["amd.com/gpu.family"] = "AI"
-    dev_ids = {g.get("device_id") for g in gpus if g.get("device_id")}
+    # a GPU whose KFD node carries no device_id reads as 0x0: unknown, not a different id
+    dev_ids = {g.get("device_id") for g in gpus if g.get("device_id") not in (None, "", "0x0")}
     if len(dev_ids) == 1:
         labels["amd.com/gpu.device-id"] = _label_value(dev_ids.pop())
     cus = [int(g["compute_units"]) for g in gpus if g.get("compute_units")]

@@ -88,7 +88,7 @@ def sysfs_modes(root: str = "/") -> Tuple[Optional[str], Optional[str]]:
         vals = set()
         for p in glob.glob(os.path.join(root, "sys/class/drm/renderD*/device", name)):
             try:
-                with open(p, "r", encoding="utf-8") as fh:
+                with open(p, "r", encoding="utf-8", errors="replace") as fh:
                     v = fh.read().strip().lower()
             except OSError:
                 continue

@@ -43,12 +43,35 @@
 
 namespace {
 
+// Length of the well-formed UTF-8 sequence at s[i] (RFC 3629: no overlong forms, no
+// surrogates, nothing past U+10FFFF), 0 when the bytes there are not one.
+size_t utf8_len(const std::string& s, size_t i) {
+  const auto b = [&](size_t k) { return i + k < s.size() ? static_cast<unsigned char>(s[i + k]) : 0u; };
+  const unsigned c = b(0);
+  const auto cont = [&](size_t k) { return (b(k) & 0xC0) == 0x80; };
+  if (c >= 0xC2 && c <= 0xDF) return cont(1) ? 2 : 0;
+  if (c >= 0xE0 && c <= 0xEF) {
+    const unsigned lo = c == 0xE0 ? 0xA0 : 0x80, hi = c == 0xED ? 0x9F : 0xBF;
+    return b(1) >= lo && b(1) <= hi && cont(2) ? 3 : 0;
+  }
+  if (c >= 0xF0 && c <= 0xF4) {
+    const unsigned lo = c == 0xF0 ? 0x90 : 0x80, hi = c == 0xF4 ? 0x8F : 0xBF;
+    return b(1) >= lo && b(1) <= hi && cont(2) && cont(3) ? 4 : 0;
+  }
+  return 0;
+}
+
+// A JSON string body.  sysfs attributes are bytes: a byte that does not start a
+// well-formed UTF-8 sequence becomes U+FFFD, so the document always parses.
 std::string esc(const std::string& s) {
   std::string o;
-  for (unsigned char c : s) {
-    if (c == '"' || c == '\\') { o += '\\'; o += static_cast<char>(c); }
-    else if (c < 0x20) { char b[8]; snprintf(b, sizeof(b), "\\u%04x", c); o += b; }
-    else o += static_cast<char>(c);
+  for (size_t i = 0; i < s.size();) {
+    const unsigned char c = static_cast<unsigned char>(s[i]);
+    if (c == '"' || c == '\\') { o += '\\'; o += static_cast<char>(c); ++i; }
+    else if (c < 0x20 || c == 0x7F) { char b[8]; snprintf(b, sizeof(b), "\\u%04x", c); o += b; ++i; }
+    else if (c < 0x80) { o += static_cast<char>(c); ++i; }
+    else if (const size_t n = utf8_len(s, i)) { o.append(s, i, n); i += n; }
+    else { o += "\\ufffd"; ++i; }
   }
   return o;
 }

@@ -128,7 +128,7 @@ def native_health(source: str = "sysfs", sysfs_root: str = "", max_uncorrectable
 def _read_props(path: str) -> Dict[str, int]:
     props: Dict[str, int] = {}
     try:
-        with open(path, "r", encoding="utf-8") as fh:
+        with open(path, "r", encoding="utf-8", errors="replace") as fh:
             for line in fh:
                 parts = line.split()
                 if len(parts) == 2:
@@ -151,7 +151,7 @@ def kfd_topology(root: str = KFD_TOPOLOGY) -> Dict[str, Any]:
             continue
         name = ""
         try:
-            with open(os.path.join(node_dir, "name"), "r", encoding="utf-8") as fh:
+            with open(os.path.join(node_dir, "name"), "r", encoding="utf-8", errors="replace") as fh:
                 name = fh.read().strip()
         except OSError:
             pass
@@ -192,7 +192,7 @@ def kfd_topology(root: str = KFD_TOPOLOGY) -> Dict[str, Any]:
 
 def _read_text(path: str) -> Optional[str]:
     try:
-        with open(path, "r", encoding="utf-8") as fh:
+        with open(path, "r", encoding="utf-8", errors="replace") as fh:
             return fh.read().strip()
     except OSError:
         return None
