@@ -598,3 +598,33 @@ def test_thousands_of_retired_pages_are_counted(tmp_path, native_ok):
     g5 = v["gpus"][5]
     assert (g5["bad_pages"], g5["bad_pages_pending"], g5["bad_page_limit"]) == (3000, 10, 2949)
     assert v["reasons"] == ["GPU 5 (0000:55:00.0): 3000 retired VRAM pages (max 2949)"]
+
+
+@pytest.mark.parametrize("argv,needle", [
+    (["health", "--max-bad-pages", "lots"], "gpu_max_retired_pages"),
+    (["metrics", "--max-bad-pages", "-3"], "gpu_max_retired_pages"),
+    (["health", "--max-uncorrectable", "-1"], "gpu_max_uncorrectable_ecc"),
+    (["gemm", "--size", "100"], "multiples of 256"),
+])
+def test_tk_gpu_refusals_are_one_line(capsys, argv, needle):
+    """`tk-gpu` (ops/cli.py) refuses what it cannot use with one line and exit 2, not a
+    traceback."""
+    from triton_kubernetes_amd.ops.cli import main
+
+    assert main(argv) == 2
+    err = capsys.readouterr().err
+    assert err.startswith("tk-gpu: ") and needle in err and "Traceback" not in err
+
+
+def test_tk_gpu_health_without_gpus_is_not_healthy(tmp_path, monkeypatch, capsys, native_ok):
+    """A node where the collector finds no GPU (status 2) gets exit 2 from `tk-gpu health`
+    and `metrics`, as from `amdgpu-topo-labeller --health` / `--prom`, not a healthy verdict
+    over zero GPUs."""
+    from triton_kubernetes_amd.ops import cli, topo
+
+    empty = topo.native_topology("sysfs", str(tmp_path))
+    assert empty["status"] == 2
+    monkeypatch.setattr(topo, "native_topology", lambda source="sysfs", sysfs_root="": dict(empty))
+    for cmd in ("health", "metrics"):
+        assert cli.main([cmd]) == 2
+        assert "GPU collector failed (status 2)" in capsys.readouterr().err

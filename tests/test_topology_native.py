@@ -129,6 +129,25 @@ def test_executable_sysfs_root(tmp_path, native_ok):
     assert empty.returncode == 2 and "no KFD topology" in empty.stderr
 
 
+@pytest.mark.parametrize("flag,value", [("--max-uncorrectable", "abc"), ("--max-uncorrectable", "3x"),
+                                        ("--max-uncorrectable", ""), ("--max-uncorrectable", " 2"),
+                                        ("--max-uncorrectable", "99999999999999999999"),
+                                        ("--max-bad-pages", "lots"), ("--max-bad-pages", "auto2")])
+def test_health_thresholds_must_be_whole_numbers(tmp_path, native_ok, flag, value):
+    """A threshold that is not a whole number is a usage error (64), not 0: `atoll("abc")`
+    made every uncorrectable error count as too many, or none of them."""
+    root = make_tree(str(tmp_path))
+    exe = executable("amdgpu-topo-labeller")
+    bad = subprocess.run([exe, "--health", "--source", "sysfs", "--sysfs-root", root, flag, value],
+                         capture_output=True, text=True, timeout=60)
+    assert bad.returncode == 64 and "usage:" in bad.stderr
+    for good in (["--max-uncorrectable", "2", "--max-bad-pages", "auto"], ["--max-bad-pages", "-1"],
+                 ["--max-bad-pages", "10"]):
+        ok = subprocess.run([exe, "--health", "--source", "sysfs", "--sysfs-root", root] + good,
+                            capture_output=True, text=True, timeout=60)
+        assert ok.returncode == 0 and json.loads(ok.stdout)["status"] == "healthy", ok.stderr
+
+
 # a RoCE port's GID table as mlx5 fills it: link-local IPv6 as RoCE v1 / v2 (0, 1), then
 # the interface's IPv4 address, IPv4-mapped, as v1 / v2 (2, 3); empty slots read as zeros
 ROCE_GIDS = [("IB/RoCE v1", "fe80:0000:0000:0000:0a00:00ff:fe00:0001"),
@@ -363,12 +382,16 @@ def test_labeller_clean_under_asan_ubsan_over_damaged_sysfs(tmp_path, asan_label
     UBSan report and with a documented status (0, or 2 when no GPU is left to label), and
     what it prints is a JSON document or key=value lines."""
     root = _corrupt(add_rdma(make_tree(str(tmp_path / "root"), ngpu=8), RDMA), how)
-    for args in ([], ["--labels"], ["--rccl-env"]):
+    for args in ([], ["--labels"], ["--rccl-env"], ["--health"], ["--health", "--labels"], ["--prom", "--node", "n1"]):
         argv = args + (["--source", "sysfs"] if args != ["--rccl-env"] else []) + ["--sysfs-root", root]
         run = _asan_run(asan_labeller, argv)
-        assert run.returncode in (0, 2), (how, args, run.returncode, run.stderr[-3000:])
-        if run.returncode == 0 and not args:
+        # --health: 3 is its verdict "a GPU is unhealthy"
+        assert run.returncode in ((0, 2, 3) if "--health" in args else (0, 2)), \
+            (how, args, run.returncode, run.stderr[-3000:])
+        if run.returncode in (0, 3) and args in ([], ["--health"]):
             json.loads(run.stdout)
+        elif run.returncode == 0 and args[0] == "--prom":
+            assert all(ln.startswith("#") or " " in ln for ln in run.stdout.splitlines()), run.stdout[:500]
         elif run.returncode == 0:
             assert all("=" in line for line in run.stdout.splitlines()), run.stdout[:500]
 

@@ -22,6 +22,32 @@ from typing import Sequence
 
 
 def main(argv: Sequence[str] = ()) -> int:
+    """The command's exit code.  A refusal (a bad threshold, a GEMM size the kernel does not
+    take, a native library that is not there, a probe that failed) is one ``tk-gpu: ...``
+    line on stderr and exit 2, not a traceback."""
+    from ..errors import TKError
+    from .gemm import GemmError
+    from .native import NativeUnavailable
+    from .probe import ProbeError
+
+    try:
+        return _main(argv)
+    except (TKError, GemmError, NativeUnavailable, ProbeError, ValueError) as exc:
+        print(f"tk-gpu: {exc}", file=sys.stderr)
+        return 2
+
+
+def _collected(doc: dict) -> dict:
+    """A topology document the collector finished; a node with no GPU to judge (status 2,
+    as ``amdgpu-topo-labeller --health`` exits) is not a healthy one."""
+    if doc.get("status", 0) != 0:
+        from ..errors import TKError
+
+        raise TKError(f"GPU collector failed (status {doc.get('status')}): {doc.get('error', 'no detail')}")
+    return doc
+
+
+def _main(argv: Sequence[str]) -> int:
     ap = argparse.ArgumentParser(prog="tk-gpu")
     sub = ap.add_subparsers(dest="cmd", required=True)
     b = sub.add_parser("burnin")
@@ -97,7 +123,7 @@ def main(argv: Sequence[str] = ()) -> int:
 
         max_ue, max_bad = limits_of({"gpu_max_uncorrectable_ecc": args.max_uncorrectable,
                                      "gpu_max_retired_pages": args.max_bad_pages})
-        doc = topo.native_topology("sysfs") if args.source == "sysfs" else topo.amdsmi_topology()
+        doc = _collected(topo.native_topology("sysfs") if args.source == "sysfs" else topo.amdsmi_topology())
         verdict = evaluate(doc, max_ue, max_bad)
         print(json.dumps(verdict, indent=2))
         return 0 if verdict["status"] == "healthy" else 3
@@ -110,7 +136,7 @@ def main(argv: Sequence[str] = ()) -> int:
 
         max_ue, max_bad = limits_of({"gpu_max_uncorrectable_ecc": args.max_uncorrectable,
                                      "gpu_max_retired_pages": args.max_bad_pages})
-        doc = topo.native_topology("sysfs") if args.source == "sysfs" else topo.amdsmi_topology()
+        doc = _collected(topo.native_topology("sysfs") if args.source == "sysfs" else topo.amdsmi_topology())
         sys.stdout.write(gpu_metrics(evaluate(doc, max_ue, max_bad), args.node or socket.gethostname()))
         return 0
     if args.cmd == "rccl-local":

@@ -34,6 +34,7 @@
 #include <cstdarg>
 #include <cstdint>
 #include <cstdio>
+#include <cerrno>
 #include <cstdlib>
 #include <cstring>
 #include <map>
@@ -1104,6 +1105,17 @@ extern "C" int tkt_topology_json(char* buf, size_t len) { return tkt_topology_js
 extern "C" int tkt_topology_labels(char* buf, size_t len) { return tkt_topology_labels_src("amdsmi", "", buf, len); }
 
 #ifdef TK_TOPO_MAIN
+// A whole decimal int64 ("12", "-1"); "", "abc", "3x" and out-of-range values are not.
+static bool whole_int(const char* s, long long* out) {
+  if (!*s) return false;
+  char* end = nullptr;
+  errno = 0;
+  const long long v = strtoll(s, &end, 10);
+  if (*end || errno == ERANGE || isspace((unsigned char)*s)) return false;
+  *out = v;
+  return true;
+}
+
 // amdgpu-topo-labeller [--labels|--rccl-env|--health|--prom] [--source auto|amdsmi|sysfs] [--sysfs-root DIR]
 //                      [--max-uncorrectable N] [--max-bad-pages N|auto] [--node NAME]
 //   default: topology JSON on stdout; --labels: one `amd.com/...=value` per line;
@@ -1129,11 +1141,11 @@ int main(int argc, char** argv) {
       prom = true;
     } else if (strcmp(argv[i], "--node") == 0 && i + 1 < argc) {
       node = argv[++i];
-    } else if (strcmp(argv[i], "--max-uncorrectable") == 0 && i + 1 < argc) {
-      max_ue = atoll(argv[++i]);
-    } else if (strcmp(argv[i], "--max-bad-pages") == 0 && i + 1 < argc) {
+    } else if (strcmp(argv[i], "--max-uncorrectable") == 0 && i + 1 < argc && whole_int(argv[i + 1], &max_ue)) {
       ++i;
-      max_bad = strcmp(argv[i], "auto") == 0 ? -1 : atoll(argv[i]);
+    } else if (strcmp(argv[i], "--max-bad-pages") == 0 && i + 1 < argc &&
+               (strcmp(argv[i + 1], "auto") == 0 || whole_int(argv[i + 1], &max_bad))) {
+      if (strcmp(argv[++i], "auto") == 0) max_bad = -1;
     } else if (strcmp(argv[i], "--source") == 0 && i + 1 < argc) {
       source = argv[++i];
     } else if (strcmp(argv[i], "--sysfs-root") == 0 && i + 1 < argc) {
