@@ -34,7 +34,12 @@
 #include <condition_variable>
 #include <chrono>
 #include <cstdlib>
+#include <cerrno>
+#include <cmath>
 #include <cstdint>
+#include <initializer_list>
+#include <limits>
+#include <type_traits>
 #include <map>
 #include <mutex>
 #include <cstdio>
@@ -1622,30 +1627,78 @@ int main(int argc, char** argv) {
   int hold_max_ms = 30000;
   double min_read = 0.60 * 6300.0, min_bf16 = 0.55 * 2500.0, min_fp8 = 0.55 * 5000.0, min_gemm = 0.30 * 2500.0,
          min_gemm8 = 0.30 * 5000.0;
-  for (int i = 1; i < argc; ++i) {
-    if (!strcmp(argv[i], "--all")) all = 1;
-    else if (!strcmp(argv[i], "--device") && i + 1 < argc) dev = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--level") && i + 1 < argc) level = argv[++i];
-    else if (!strcmp(argv[i], "--min-read-gbps") && i + 1 < argc) min_read = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--min-bf16-tflops") && i + 1 < argc) min_bf16 = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--min-fp8-tflops") && i + 1 < argc) min_fp8 = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--min-gemm-tflops") && i + 1 < argc) min_gemm = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--min-gemm-fp8-tflops") && i + 1 < argc) min_gemm8 = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--labels") && i + 1 < argc) labels_path = argv[++i];
-    else if (!strcmp(argv[i], "--p2p")) p2p = 1;
-    else if (!strcmp(argv[i], "--hold-stdin")) hold = true;
-    else if (!strcmp(argv[i], "--hold-max-ms") && i + 1 < argc) hold_max_ms = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--min-link-frac") && i + 1 < argc) min_link_frac = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--min-link-gbps") && i + 1 < argc) min_link_gbps = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--p2p-method") && i + 1 < argc) link_mode = strcmp(argv[++i], "sdma-copy") ? 1 : 0;
-    else if (!strcmp(argv[i], "--compute-partition") && i + 1 < argc) cpart = argv[++i];
-    else if (!strcmp(argv[i], "--memory-partition") && i + 1 < argc) ++i;  // pools are only shared concurrently
-    else if (!strcmp(argv[i], "--memtest-span")) span_mode = 1;
-    else if (!strcmp(argv[i], "--span-bytes") && i + 1 < argc) span_bytes = strtoull(argv[++i], nullptr, 10);
-    else if (!strcmp(argv[i], "--span-headroom") && i + 1 < argc) span_headroom = strtoull(argv[++i], nullptr, 10);
-    else if (!strcmp(argv[i], "--span-passes") && i + 1 < argc) span_passes = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--span-chunk") && i + 1 < argc) span_chunk = strtoull(argv[++i], nullptr, 10);
+  // Every option and value is checked before the GPU is touched: a threshold that does not
+  // parse (atof("abc") == 0) would switch its check off, an unknown word would be ignored.
+  const char* bad = nullptr;
+  const auto want = [&](int& i) -> const char* {
+    if (i + 1 >= argc) { bad = argv[i]; return nullptr; }
+    return argv[++i];
+  };
+  const auto real = [&](int& i, double* out) {  // a finite number >= 0
+    const char* opt = argv[i];
+    const char* v = want(i);
+    if (!v) return;
+    char* end = nullptr;
+    const double x = strtod(v, &end);
+    if (!*v || *end || !std::isfinite(x) || x < 0) bad = opt;
+    else *out = x;
+  };
+  const auto count = [&](int& i, auto* out, unsigned long long lo) {  // a whole number >= lo
+    const char* opt = argv[i];
+    const char* v = want(i);
+    if (!v) return;
+    char* end = nullptr;
+    errno = 0;
+    const unsigned long long x = strtoull(v, &end, 10);
+    if (!isdigit((unsigned char)*v) || *end || errno == ERANGE || x < lo ||
+        x > (unsigned long long)std::numeric_limits<std::remove_pointer_t<decltype(out)>>::max())
+      bad = opt;
+    else *out = (std::remove_pointer_t<decltype(out)>)x;
+  };
+  const auto one_of = [&](int& i, const char** out, std::initializer_list<const char*> words) {
+    const char* opt = argv[i];
+    const char* v = want(i);
+    if (!v) return;
+    for (const char* w : words)
+      if (!strcmp(v, w)) { *out = v; return; }
+    bad = opt;
+  };
+  const char* link_method = "kernel-read";
+  const char* mem_part = "nps1";
+  for (int i = 1; i < argc && !bad; ++i) {
+    const char* a = argv[i];
+    if (!strcmp(a, "--all")) all = 1;
+    else if (!strcmp(a, "--device")) count(i, &dev, 0);
+    else if (!strcmp(a, "--level")) one_of(i, &level, {"quick", "full"});
+    else if (!strcmp(a, "--min-read-gbps")) real(i, &min_read);
+    else if (!strcmp(a, "--min-bf16-tflops")) real(i, &min_bf16);
+    else if (!strcmp(a, "--min-fp8-tflops")) real(i, &min_fp8);
+    else if (!strcmp(a, "--min-gemm-tflops")) real(i, &min_gemm);
+    else if (!strcmp(a, "--min-gemm-fp8-tflops")) real(i, &min_gemm8);
+    else if (!strcmp(a, "--labels")) { if (const char* v = want(i)) labels_path = v; }
+    else if (!strcmp(a, "--p2p")) p2p = 1;
+    else if (!strcmp(a, "--hold-stdin")) hold = true;
+    else if (!strcmp(a, "--hold-max-ms")) count(i, &hold_max_ms, 0);
+    else if (!strcmp(a, "--min-link-frac")) real(i, &min_link_frac);
+    else if (!strcmp(a, "--min-link-gbps")) real(i, &min_link_gbps);
+    else if (!strcmp(a, "--p2p-method")) one_of(i, &link_method, {"kernel-read", "sdma-copy"});
+    else if (!strcmp(a, "--compute-partition")) one_of(i, &cpart, {"spx", "dpx", "qpx", "cpx"});
+    else if (!strcmp(a, "--memory-partition")) one_of(i, &mem_part, {"nps1", "nps2"});  // = node/partition.py; pools are only shared concurrently
+    else if (!strcmp(a, "--memtest-span")) span_mode = 1;
+    else if (!strcmp(a, "--span-bytes")) count(i, &span_bytes, 0);
+    else if (!strcmp(a, "--span-headroom")) count(i, &span_headroom, 0);
+    else if (!strcmp(a, "--span-passes")) count(i, &span_passes, 1);
+    else if (!strcmp(a, "--span-chunk")) count(i, &span_chunk, 1);
+    else bad = a;
   }
+  if (bad) {
+    char e[256];
+    json_escape(bad, e, sizeof(e));
+    printf("{\"ok\":false,\"error\":\"usage: unknown option, or a bad or missing value, at '%s' (gpu-burnin "
+           "[--all|--device N] [--level quick|full] [--p2p] [--memtest-span] ...)\"}\n", e);
+    return 64;
+  }
+  link_mode = strcmp(link_method, "sdma-copy") ? 1 : 0;
   if (p2p) return p2p_main(labels_path, min_link_frac, min_link_gbps, link_mode);
   if (span_mode) {
     // --memtest-span: the full memtest alone, for ops/probe.py:memtest_span_process.  One

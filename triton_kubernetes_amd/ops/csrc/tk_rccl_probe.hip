@@ -30,8 +30,10 @@
 #include <dlfcn.h>
 #include <unistd.h>
 
+#include <cctype>
 #include <cerrno>
 #include <climits>
+#include <cmath>
 #include <string>
 #include <atomic>
 #include <condition_variable>
@@ -1062,32 +1064,64 @@ static bool rccl_mapped(const char* want) {
 }
 
 int main(int argc, char** argv) {
-  int ndev = 0;
-  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev < 1) {
-    fprintf(stderr, "{\"error\":\"no HIP devices\"}\n");
-    return 3;
-  }
   double min_busbw = 0.0, timeout_s = 600.0;
-  int iters = 20, warmup = 5, dtype = 0, world = 0, rank_base = 0, max_mib = 64;
+  int iters = 20, warmup = 5, dtype = 0, world = 0, rank_base = 0, max_mib = 64, ngpus = 0;
   bool cluster = false, uid_out = false, max_set = false, preload = false;
   const char* uid_hex = nullptr;
   const char* expect_rccl = nullptr;  // --expect-rccl: the librccl this process must have mapped
-  const int visible = ndev;
-  for (int i = 1; i < argc; ++i) {
-    if (!strcmp(argv[i], "--min-busbw") && i + 1 < argc) min_busbw = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--iters") && i + 1 < argc) iters = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--ngpus") && i + 1 < argc) ndev = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--bf16")) dtype = 1;
-    else if (!strcmp(argv[i], "--cluster")) cluster = true;
-    else if (!strcmp(argv[i], "--world") && i + 1 < argc) world = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--rank-base") && i + 1 < argc) rank_base = atoi(argv[++i]);
-    else if (!strcmp(argv[i], "--uid") && i + 1 < argc) uid_hex = argv[++i];
-    else if (!strcmp(argv[i], "--uid-out")) uid_out = true;
-    else if (!strcmp(argv[i], "--max-mib") && i + 1 < argc) { max_mib = atoi(argv[++i]); max_set = true; }
-    else if (!strcmp(argv[i], "--timeout-s") && i + 1 < argc) timeout_s = atof(argv[++i]);
-    else if (!strcmp(argv[i], "--expect-rccl") && i + 1 < argc) expect_rccl = argv[++i];
-    else if (!strcmp(argv[i], "--preload")) preload = true;  // tkr_preload_device_code first
+  // The command line is read before the GPU is touched: a value that does not parse
+  // (atof("abc") == 0 turned the bandwidth floor off) or an unknown option is a usage error.
+  const char* bad = nullptr;
+  const auto want = [&](int& i) -> const char* {
+    if (i + 1 >= argc) { bad = argv[i]; return nullptr; }
+    return argv[++i];
+  };
+  const auto real = [&](int& i, double* out, bool positive) {
+    const char* opt = argv[i];
+    const char* v = want(i);
+    if (!v) return;
+    char* end = nullptr;
+    const double x = strtod(v, &end);
+    if (!*v || *end || !std::isfinite(x) || x < 0 || (positive && x == 0)) bad = opt;
+    else *out = x;
+  };
+  const auto whole = [&](int& i, int* out, long lo) {
+    const char* opt = argv[i];
+    const char* v = want(i);
+    if (!v) return;
+    char* end = nullptr;
+    errno = 0;
+    const long x = strtol(v, &end, 10);
+    if (!*v || *end || errno == ERANGE || x < lo || x > INT_MAX || isspace((unsigned char)*v)) bad = opt;
+    else *out = (int)x;
+  };
+  for (int i = 1; i < argc && !bad; ++i) {
+    const char* a = argv[i];
+    if (!strcmp(a, "--min-busbw")) real(i, &min_busbw, false);
+    else if (!strcmp(a, "--iters")) whole(i, &iters, 1);
+    else if (!strcmp(a, "--ngpus")) whole(i, &ngpus, 1);
+    else if (!strcmp(a, "--bf16")) dtype = 1;
+    else if (!strcmp(a, "--cluster")) cluster = true;
+    else if (!strcmp(a, "--world")) whole(i, &world, 1);
+    else if (!strcmp(a, "--rank-base")) whole(i, &rank_base, 0);
+    else if (!strcmp(a, "--uid")) uid_hex = want(i);
+    else if (!strcmp(a, "--uid-out")) uid_out = true;
+    else if (!strcmp(a, "--max-mib")) { whole(i, &max_mib, 1); max_set = true; }
+    else if (!strcmp(a, "--timeout-s")) real(i, &timeout_s, true);
+    else if (!strcmp(a, "--expect-rccl")) expect_rccl = want(i);
+    else if (!strcmp(a, "--preload")) preload = true;  // tkr_preload_device_code first
+    else bad = a;
   }
+  if (bad) {
+    print_error_json(("usage: unknown option, or a bad or missing value, at '" + std::string(bad) + "'").c_str());
+    return 64;
+  }
+  int visible = 0;
+  if (hipGetDeviceCount(&visible) != hipSuccess || visible < 1) {
+    fprintf(stderr, "{\"error\":\"no HIP devices\"}\n");
+    return 3;
+  }
+  const int ndev = ngpus ? ngpus : visible;
   if (ndev < 1 || ndev > visible) {
     fprintf(stderr, "{\"error\":\"--ngpus %d but %d visible\"}\n", ndev, visible);
     return 3;
