@@ -277,12 +277,28 @@ class GpuCountError(RuntimeError):
     pass
 
 
-def parse_args():
+def _at_least(lo, kind=int):
+    """An argparse type: a finite number of ``kind`` >= ``lo`` (``--steps 0`` would time
+    nothing and divide by zero; a negative warm-up or budget means nothing)."""
+    def parse(text):
+        try:
+            v = kind(text)
+        except ValueError:
+            raise argparse.ArgumentTypeError(f"not a{'n integer' if kind is int else ' number'}: {text!r}")
+        if not math.isfinite(v) or v < lo:
+            raise argparse.ArgumentTypeError(f"must be a finite number >= {lo}: {text!r}")
+        return v
+
+    parse.__name__ = kind.__name__
+    return parse
+
+
+def parse_args(argv=None):
     ap = argparse.ArgumentParser(description=__doc__.splitlines()[0])
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=3)
-    ap.add_argument("--warmup", type=int, default=1)
-    ap.add_argument("--workers", type=int, default=1, help="worker nodes the N GPUs are split over")
+    ap.add_argument("--gpus", type=_at_least(1), default=1)
+    ap.add_argument("--steps", type=_at_least(1), default=3)
+    ap.add_argument("--warmup", type=_at_least(0), default=1)
+    ap.add_argument("--workers", type=_at_least(1), default=1, help="worker nodes the N GPUs are split over")
     # the product's default level (models/baremetal.py DEFAULT_BURNIN, pinned by
     # tests/test_bench_contract.py); quick is the explicit opt-down
     ap.add_argument("--burnin", default=_default_burnin(), choices=["quick", "full", "off"])
@@ -291,8 +307,8 @@ def parse_args():
                          "finished clearing the HBM the previous step released (ops/hbm.py), as on a node "
                          "entering service.  off: the A/B (each step pays its predecessor's clearing)")
     ap.add_argument("--no-rccl-gate", action="store_true")
-    ap.add_argument("--rccl-mib", type=int, default=64, help="largest RCCL gate message (MiB)")
-    ap.add_argument("--warm-steps", type=int, default=2,
+    ap.add_argument("--rccl-mib", type=_at_least(1), default=64, help="largest RCCL gate message (MiB)")
+    ap.add_argument("--warm-steps", type=_at_least(0), default=2,
                     help="secondary: creates against resident agents after the timed region (0: skip)")
     ap.add_argument("--agents", default="proc", choices=["proc", "inproc"],
                     help="proc: every agent in its own fresh process (the headline); inproc: agents as "
@@ -305,7 +321,7 @@ def parse_args():
                     help="the GPU node's health policy (node/health.py).  taint (bench default): a GPU with "
                          "uncorrectable ECC errors does not abort the run; the node joins tainted and the line "
                          "lists it under gpu_unhealthy_nodes (its GPUs then sit out the GPU and RCCL checks)")
-    ap.add_argument("--link-min-gbps", type=float, default=0.0,
+    ap.add_argument("--link-min-gbps", type=_at_least(0.0, float), default=0.0,
                     help="the GPU node's absolute xGMI link floor (gpu_link_min_gbps; the product default is 38). "
                          "The bench records the link matrix (xgmi_links in the line) rather than certifying it: "
                          "0 keeps only the relative check (a link below half the node's median still fails)")
@@ -314,11 +330,11 @@ def parse_args():
                          "libtk_rccl ABI stub (ops/csrc/tk_rccl_stub.cpp: every rank of the world joins and sweeps, "
                          "no GPU); never a valid measurement")
     ap.add_argument("--report", default="", help="write a per-step phase report (rank 0) to this file")
-    ap.add_argument("--time-budget", type=float, default=480.0,
+    ap.add_argument("--time-budget", type=_at_least(0.0, float), default=480.0,
                     help="wall-clock seconds the whole run should stay within (RunBudget): past it the secondary "
                          "warm creates are shed, then the untimed settle waits are capped; the timed steps never "
                          "are.  0: off")
-    return ap.parse_args()
+    return ap.parse_args(argv)
 
 
 class AgentProc:

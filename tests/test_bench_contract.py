@@ -413,3 +413,27 @@ def test_run_budget_holds_whenever_the_steps_themselves_fit(settle, step, n, war
     assert ran == n
     assert now[0] <= budget + 1e-6, (now[0], b.report())
     assert b.settle_cap_s is None or b.settle_cap_s >= 0.0
+
+
+@pytest.mark.parametrize("argv", [["--steps", "0"], ["--steps", "-2"], ["--gpus", "0"], ["--warmup", "-1"],
+                                  ["--workers", "0"], ["--rccl-mib", "0"], ["--warm-steps", "-1"],
+                                  ["--time-budget", "nan"], ["--time-budget", "-5"], ["--link-min-gbps", "inf"],
+                                  ["--steps", "3.5"], ["--gpus", "eight"]])
+def test_bench_refuses_counts_that_mean_nothing(argv, capsys):
+    """`--steps 0` timed nothing and divided by zero; a negative warm-up or budget meant
+    nothing.  argparse refuses them (exit 2) before anything starts."""
+    import bench
+
+    with pytest.raises(SystemExit) as exc:
+        bench.parse_args(argv)
+    assert exc.value.code == 2
+    assert "argument --" in capsys.readouterr().err
+
+
+def test_bench_accepts_the_drivers_command_lines():
+    import bench
+
+    for argv in ([], ["--gpus", "8", "--steps", "20", "--warmup", "5"], ["--steps", "1", "--warmup", "0"],
+                 ["--time-budget", "0", "--warm-steps", "0", "--link-min-gbps", "38.5"]):
+        args = bench.parse_args(argv)
+        assert args.steps >= 1 and args.warmup >= 0 and args.gpus >= 1
