@@ -333,3 +333,23 @@ def test_cli_credentials_node(tmp_path, monkeypatch):
     assert rc == 0
     policy = json.loads((tmp_path / "creds" / "agent-policy.json").read_text())
     assert policy["servers"] == ["https://10.9.8.7"]
+
+
+@pytest.mark.parametrize("extra,msg", [
+    (["--devices", "a,b"], "argument --devices"), (["--devices", "0,0"], "given twice"),
+    (["--devices", "-1"], "argument --devices"), (["--listen", "nohost"], "argument --listen"),
+    (["--listen", "127.0.0.1:99999"], "argument --listen"), (["--synthetic-gpus", "-3"], "argument --synthetic-gpus"),
+    (["--token-file", "/nonexistent/token"], "--token-file /nonexistent/token"),
+    (["--credentials", "/nonexistent/creds"], "--credentials /nonexistent/creds"),
+])
+def test_agent_command_line_refusals_are_argparse_errors(tmp_path, capsys, extra, msg):
+    """What systemd hands the daemon and it cannot use ends in one usage line and exit 2,
+    not a traceback from the middle of the start-up (an RCCL error for `--devices 0,0`)."""
+    from triton_kubernetes_amd.node import agent as agent_mod
+
+    argv = ["--mode", "sim", "--root", str(tmp_path)] + (["--insecure-local"] if "--credentials" not in extra else [])
+    with pytest.raises(SystemExit) as exc:
+        agent_mod.main(argv + extra)
+    assert exc.value.code == 2
+    err = capsys.readouterr().err
+    assert msg in err and "Traceback" not in err, err

@@ -449,15 +449,48 @@ class NodeAgent(AgentStepsMixin, AgentGateMixin, AgentHTTPMixin):
         lap("frees")
         self.stop_ms = ms  # where a shutdown's time went (logged by main)
 
+def _listen_arg(text: str) -> str:
+    """``HOST:PORT`` with a port of 0..65535 (0: any free port)."""
+    import argparse
+
+    host, sep, port = text.rpartition(":")
+    if not sep or not port.isdigit() or not 0 <= int(port) <= 65535 or not host:
+        raise argparse.ArgumentTypeError(f"HOST:PORT with a port of 0..65535, not {text!r}")
+    return text
+
+
+def _devices_arg(text: str) -> List[int]:
+    """Comma-separated local GPU indices, each once ("" = none)."""
+    import argparse
+
+    parts = [d.strip() for d in text.split(",") if d.strip()]
+    if not all(d.isdigit() for d in parts):
+        raise argparse.ArgumentTypeError(f"comma-separated GPU indices (0, 1, ...), not {text!r}")
+    devices = [int(d) for d in parts]
+    if len(set(devices)) != len(devices):
+        raise argparse.ArgumentTypeError(f"a GPU index given twice: {text!r}")
+    return devices
+
+
+def _count_arg(text: str) -> int:
+    import argparse
+
+    if not text.strip().isdigit():
+        raise argparse.ArgumentTypeError(f"a whole number >= 0, not {text!r}")
+    return int(text)
+
+
 def main(argv: Optional[List[str]] = None) -> int:
-    """``tk-node-agent``: serve the agent API on a host (127.0.0.1 by default)."""
+    """``tk-node-agent``: serve the agent API on a host (127.0.0.1 by default).  A command
+    line it cannot use (a bad listen address, GPU list, credential directory or token file)
+    is an argparse error (exit 2), not a traceback from deep inside the start-up."""
     import argparse
 
     t_main = time.perf_counter()
     ap = argparse.ArgumentParser(prog="tk-node-agent")
-    ap.add_argument("--listen", default="127.0.0.1:7946")
+    ap.add_argument("--listen", default="127.0.0.1:7946", type=_listen_arg)
     ap.add_argument("--mode", default="exec", choices=MODES)
-    ap.add_argument("--devices", default="", help="comma-separated local GPU indices")
+    ap.add_argument("--devices", default=[], type=_devices_arg, help="comma-separated local GPU indices")
     ap.add_argument("--credentials", default="",
                     help="the node's credential directory (agent-token, agent.crt/.key, agent-policy.json; "
                          "`triton-kubernetes credentials node`): serve TLS with the node's token and allow-list")
@@ -469,7 +502,7 @@ def main(argv: Optional[List[str]] = None) -> int:
                          "(besides loopback ones); repeatable")
     ap.add_argument("--root", default="/")
     ap.add_argument("--name", default="", help="agent name (defaults to the listen host)")
-    ap.add_argument("--synthetic-gpus", type=int, default=0,
+    ap.add_argument("--synthetic-gpus", type=_count_arg, default=0,
                     help="tests / CPU dry runs only: a synthetic MI355X topology with this many GPUs, "
                          "no burn-in kernels, no RCCL")
     args = ap.parse_args(argv)
@@ -480,7 +513,10 @@ def main(argv: Optional[List[str]] = None) -> int:
     if args.credentials:
         from .security import read_credentials
 
-        creds = read_credentials(args.credentials)
+        try:
+            creds = read_credentials(args.credentials)
+        except (OSError, ValueError) as exc:  # ssl.SSLError is an OSError
+            ap.error(f"--credentials {args.credentials}: {exc}")
         token, ssl_ctx, policy = creds["token"], creds["ssl_context"], creds["policy"]
     elif not args.insecure_local:
         ap.error("--credentials DIR is required (or --insecure-local for plain HTTP on loopback)")
@@ -491,9 +527,12 @@ def main(argv: Optional[List[str]] = None) -> int:
 
         policy = AgentPolicy([AGENT_IMAGE], servers=list(args.allow_server), loopback_servers=True)
     if args.token_file and not token:
-        with open(args.token_file, "r", encoding="utf-8") as fh:
-            token = fh.read().strip()
-    devices = [int(d) for d in args.devices.split(",") if d.strip()]
+        try:
+            with open(args.token_file, "r", encoding="utf-8") as fh:
+                token = fh.read().strip()
+        except (OSError, UnicodeDecodeError) as exc:
+            ap.error(f"--token-file {args.token_file}: {exc}")
+    devices = args.devices
     agent = NodeAgent(name=args.name or host, mode=args.mode, devices=devices, root=args.root, token=token,
                       policy=policy)
     if args.synthetic_gpus > 0:
