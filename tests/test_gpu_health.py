@@ -603,7 +603,7 @@ def test_thousands_of_retired_pages_are_counted(tmp_path, native_ok):
 @pytest.mark.parametrize("argv,needle", [
     (["health", "--max-bad-pages", "lots"], "gpu_max_retired_pages"),
     (["metrics", "--max-bad-pages", "-3"], "gpu_max_retired_pages"),
-    (["health", "--max-uncorrectable", "-1"], "gpu_max_uncorrectable_ecc"),
+    (["health", "--max-bad-pages", "1.5"], "gpu_max_retired_pages"),
     (["gemm", "--size", "100"], "multiples of 256"),
 ])
 def test_tk_gpu_refusals_are_one_line(capsys, argv, needle):
@@ -628,3 +628,18 @@ def test_tk_gpu_health_without_gpus_is_not_healthy(tmp_path, monkeypatch, capsys
     for cmd in ("health", "metrics"):
         assert cli.main([cmd]) == 2
         assert "GPU collector failed (status 2)" in capsys.readouterr().err
+
+
+@pytest.mark.parametrize("argv", [["hbm", "--gib", "-4"], ["hbm", "--gib", "nan"], ["hbm", "--blocks-per-cu", "0"],
+                                  ["mfma", "--iters", "0"], ["gemm", "--reps", "0"], ["gemm", "--size", "-256"],
+                                  ["links", "--mib", "0"], ["links", "--min-frac", "-0.5"], ["burnin", "--device", "-1"],
+                                  ["rccl-local", "--ngpus", "-2"], ["health", "--max-uncorrectable", "x"],
+                                  ["health", "--max-uncorrectable", "-1"]])
+def test_tk_gpu_sizes_and_counts_are_checked_before_the_gpu(argv, capsys):
+    """A negative size reached the native probes as a huge unsigned byte count; argparse
+    now refuses it (exit 2) before any GPU call."""
+    from triton_kubernetes_amd.ops.cli import main
+
+    with pytest.raises(SystemExit) as exc:
+        main(argv)
+    assert exc.value.code == 2 and "error: argument --" in capsys.readouterr().err

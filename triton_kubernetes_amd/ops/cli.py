@@ -37,6 +37,24 @@ def main(argv: Sequence[str] = ()) -> int:
         return 2
 
 
+def _num(lo, kind=int, above=False):
+    """An argparse type: a finite ``kind`` >= ``lo`` (> ``lo`` with ``above``).  A negative
+    size reached the native probes as a huge unsigned byte count."""
+    import math
+
+    def parse(text):
+        try:
+            v = kind(text)
+        except ValueError:
+            raise argparse.ArgumentTypeError(f"not a{'n integer' if kind is int else ' number'}: {text!r}")
+        if not math.isfinite(v) or v < lo or (above and v == lo):
+            raise argparse.ArgumentTypeError(f"must be {'>' if above else '>='} {lo}: {text!r}")
+        return v
+
+    parse.__name__ = kind.__name__
+    return parse
+
+
 def _collected(doc: dict) -> dict:
     """A topology document the collector finished; a node with no GPU to judge (status 2,
     as ``amdgpu-topo-labeller --health`` exits) is not a healthy one."""
@@ -51,46 +69,46 @@ def _main(argv: Sequence[str]) -> int:
     ap = argparse.ArgumentParser(prog="tk-gpu")
     sub = ap.add_subparsers(dest="cmd", required=True)
     b = sub.add_parser("burnin")
-    b.add_argument("--device", type=int, default=0)
+    b.add_argument("--device", type=_num(0), default=0)
     b.add_argument("--all", action="store_true")
     b.add_argument("--level", default="full", choices=["quick", "full", "off"])
     sub.add_parser("topology")
     sub.add_parser("labels")
     hl = sub.add_parser("health", help="GPU RAS health: uncorrectable ECC errors, retired VRAM pages (node/health.py)")
-    hl.add_argument("--max-uncorrectable", type=int, default=0)
+    hl.add_argument("--max-uncorrectable", type=_num(0), default=0)
     hl.add_argument("--max-bad-pages", default="auto", help="a count, or auto (the driver's default threshold)")
     hl.add_argument("--source", default="sysfs", choices=["sysfs", "amdsmi"])
     mt = sub.add_parser("metrics", help="GPU health as Prometheus text (node/metrics.py; what the textfile timer writes)")
     mt.add_argument("--node", default="", help="the node label (default: the host name)")
-    mt.add_argument("--max-uncorrectable", type=int, default=0)
+    mt.add_argument("--max-uncorrectable", type=_num(0), default=0)
     mt.add_argument("--max-bad-pages", default="auto")
     mt.add_argument("--source", default="sysfs", choices=["sysfs", "amdsmi"])
     r = sub.add_parser("rccl-local")
-    r.add_argument("--ngpus", type=int, default=0)
+    r.add_argument("--ngpus", type=_num(0), default=0)
     r.add_argument("--dtype", default="f32", choices=["f32", "bf16"])
     lk = sub.add_parser("links", help="per-link xGMI check: peer bandwidth of every ordered GPU pair")
-    lk.add_argument("--min-frac", type=float, default=0.5, help="fail below this fraction of the node median")
-    lk.add_argument("--min-gbps", type=float, default=None,
+    lk.add_argument("--min-frac", type=_num(0.0, float), default=0.5, help="fail below this fraction of the node median")
+    lk.add_argument("--min-gbps", type=_num(0.0, float), default=None,
                     help="fail below this absolute GB/s (default: half of one link's ~76.8 GB/s one way)")
     lk.add_argument("--method", default="kernel-read", choices=["kernel-read", "sdma-copy"])
-    lk.add_argument("--mib", type=int, default=64, help="bytes per copy (MiB)")
+    lk.add_argument("--mib", type=_num(1), default=64, help="bytes per copy (MiB)")
     sl = sub.add_parser("rccl-slim", help="opt-in: prepare and verify the single-target (gfx950) RCCL copy")
     sl.add_argument("--source", default="")
     sl.add_argument("--no-verify", action="store_true", help="skip the GPU verification (the copy stays unused)")
     sl.add_argument("--root", default="")
     h = sub.add_parser("hbm")
-    h.add_argument("--device", type=int, default=0)
-    h.add_argument("--gib", type=float, default=4.0)
-    h.add_argument("--blocks-per-cu", type=int, default=16)
+    h.add_argument("--device", type=_num(0), default=0)
+    h.add_argument("--gib", type=_num(0.0, float, above=True), default=4.0)
+    h.add_argument("--blocks-per-cu", type=_num(1), default=16)
     m = sub.add_parser("mfma")
-    m.add_argument("--device", type=int, default=0)
+    m.add_argument("--device", type=_num(0), default=0)
     m.add_argument("--dtype", default="bf16", choices=["bf16", "fp8", "f32"])
-    m.add_argument("--iters", type=int, default=20000)
-    m.add_argument("--blocks-per-cu", type=int, default=2)
+    m.add_argument("--iters", type=_num(1), default=20000)
+    m.add_argument("--blocks-per-cu", type=_num(1), default=2)
     g = sub.add_parser("gemm", help="checksum-verified GEMM screen (silent data corruption)")
-    g.add_argument("--device", type=int, default=0)
-    g.add_argument("--size", type=int, default=8192, help="M = N = K (a multiple of 256)")
-    g.add_argument("--reps", type=int, default=5)
+    g.add_argument("--device", type=_num(0), default=0)
+    g.add_argument("--size", type=_num(1), default=8192, help="M = N = K (a multiple of 256)")
+    g.add_argument("--reps", type=_num(1), default=5)
     g.add_argument("--schedule", default="staggered", choices=["staggered", "single-barrier"],
                    help="GEMM main loop (single-barrier: the earlier loop, for A/B; bf16 only)")
     g.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"],
