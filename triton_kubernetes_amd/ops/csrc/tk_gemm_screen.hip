@@ -736,8 +736,8 @@ static int g_sched = -1;
 
 static int schedule() {
   if (g_sched < 0) {
-    const char* e = getenv("TKG_SCHED");
-    g_sched = e ? atoi(e) : TKG_DEFAULT_SCHED;
+    const char* e = getenv("TKG_SCHED");  // "0" or "1"; anything else (atoi's 0) keeps the default
+    g_sched = e && (!strcmp(e, "0") || !strcmp(e, "1")) ? e[0] - '0' : TKG_DEFAULT_SCHED;
   }
   return (g_sched == 1 && BK * 2 == p8::KT_BYTES) ? 1 : 0;
 }
