@@ -464,3 +464,13 @@ def test_in_process_readers_over_damaged_sysfs(tmp_path, native_ok, how):
         assert json.loads(json.dumps(doc)) == doc
     if doc["status"] == 0:
         assert topo.native_labels("sysfs", root) == labels_from_topology(doc)
+
+
+def test_prom_text_stays_utf8_over_a_node_name_that_is_not(tmp_path, native_ok):
+    """The exposition format is UTF-8 (node_exporter drops a textfile that is not): a node
+    name with bytes that are not comes out with U+FFFD, quotes and backslashes escaped."""
+    root = make_tree(str(tmp_path), ngpu=2)
+    out = subprocess.run([executable("amdgpu-topo-labeller"), "--prom", "--source", "sysfs", "--sysfs-root", root,
+                          "--node", os.fsdecode(b'n\xff\xfe"x\\')], capture_output=True, timeout=60).stdout
+    text = out.decode("utf-8")
+    assert 'tk_gpu_healthy{node="n��\\"x\\\\",gpu="0"' in text

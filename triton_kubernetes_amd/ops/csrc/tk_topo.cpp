@@ -804,13 +804,18 @@ std::string render_health(const Topology& t, int64_t max_ue, int64_t max_bad, bo
 // The GPU families of triton_kubernetes_amd/node/metrics.py:gpu_metrics -- same names, help
 // strings, label order and samples (tests compare the two) -- for node_exporter's textfile
 // collector on SSH / Terraform nodes.
+// A label value (the exposition format is UTF-8: a byte that does not start a well-formed
+// sequence becomes U+FFFD, or node_exporter drops the whole textfile).
 std::string prom_esc(const std::string& s) {
   std::string o;
-  for (char c : s) {
-    if (c == '\\') o += "\\\\";
-    else if (c == '\n') o += "\\n";
-    else if (c == '"') o += "\\\"";
-    else o += c;
+  for (size_t i = 0; i < s.size();) {
+    const char c = s[i];
+    if (c == '\\') { o += "\\\\"; ++i; }
+    else if (c == '\n') { o += "\\n"; ++i; }
+    else if (c == '"') { o += "\\\""; ++i; }
+    else if (!(static_cast<unsigned char>(c) & 0x80)) { o += c; ++i; }
+    else if (const size_t n = utf8_len(s, i)) { o.append(s, i, n); i += n; }
+    else { o += "\xEF\xBF\xBD"; ++i; }
   }
   return o;
 }
